@@ -1,0 +1,184 @@
+"""ctypes bindings of include/gome/gome_abi.h (libgome.so).
+
+The library is the product: HIP kernels for gfx950 behind a C-ABI.  There is no
+CPU fallback — if libgome.so is missing or no GPU is present, the calls fail loudly.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import re
+
+import numpy as np
+
+from .workload import EVENT_DTYPE, LEVEL_DTYPE, NODE_DTYPE, ORDER_DTYPE
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libgome.so")
+HEADER = os.path.join(os.path.dirname(_HERE), "include", "gome", "gome_abi.h")
+
+GOME_OK, GOME_E_INVAL, GOME_E_CAPACITY, GOME_E_DEVICE, GOME_E_STATE, GOME_E_NOTFOUND = range(6)
+STATUS_NAMES = {0: "OK", 1: "E_INVAL", 2: "E_CAPACITY", 3: "E_DEVICE", 4: "E_STATE", 5: "E_NOTFOUND"}
+
+
+class GomeError(RuntimeError):
+    def __init__(self, status: int, msg: str):
+        super().__init__(f"{STATUS_NAMES.get(status, status)}: {msg}")
+        self.status = status
+
+
+class Config(C.Structure):
+    _fields_ = [("accuracy", C.c_uint32), ("device", C.c_int32), ("max_symbols", C.c_uint32),
+                ("max_batch", C.c_uint32), ("max_nodes", C.c_uint64), ("max_levels", C.c_uint64),
+                ("max_events", C.c_uint64), ("flags", C.c_uint32), ("pad", C.c_uint32)]
+
+
+class Stats(C.Structure):
+    _fields_ = [(n, C.c_uint64) for n in (
+        "n_orders", "n_add", "n_del", "n_dropped", "n_fills", "n_cancels", "n_rests",
+        "n_events", "n_resting", "n_levels", "max_segment", "n_segments")] + [
+        ("ms_total", C.c_double), ("ms_match", C.c_double)]
+
+    def as_dict(self):
+        return {n: getattr(self, n) for n, _ in self._fields_}
+
+
+_lib = None
+
+
+def load_library(path: str = LIB_PATH) -> C.CDLL:
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise RuntimeError(
+            f"libgome.so not found at {path}: build it with `python -m gome_amd.build` "
+            "(the engine has no CPU fallback)")
+    lib = C.CDLL(path)
+    P, VP = C.POINTER, C.c_void_p
+    lib.gome_create.argtypes = [P(Config), P(VP)]
+    lib.gome_destroy.argtypes = [VP]
+    lib.gome_destroy.restype = None
+    lib.gome_last_error.argtypes = [VP]
+    lib.gome_last_error.restype = C.c_char_p
+    lib.gome_abi_version.restype = C.c_uint32
+    lib.gome_submit_batch.argtypes = [VP, VP, C.c_size_t, C.c_uint64]
+    lib.gome_submit_batch_device.argtypes = [VP, VP, C.c_size_t, C.c_uint64, VP]
+    lib.gome_drain_events.argtypes = [VP, VP, C.c_size_t, P(C.c_size_t)]
+    lib.gome_pending_events.argtypes = [VP]
+    lib.gome_pending_events.restype = C.c_size_t
+    lib.gome_device_events.argtypes = [VP, P(VP), P(C.c_size_t)]
+    lib.gome_get_stats.argtypes = [VP, P(Stats)]
+    lib.gome_snapshot_levels.argtypes = [VP, C.c_uint32, VP, C.c_size_t, P(C.c_size_t)]
+    lib.gome_snapshot_fifo.argtypes = [VP, C.c_uint32, C.c_int64, VP, C.c_size_t, P(C.c_size_t)]
+    lib.gome_fixed_from_double.argtypes = [C.c_double, C.c_uint32, P(C.c_int64)]
+    lib.gome_render_match_result.argtypes = [VP, VP, C.c_uint32] + [C.c_char_p] * 6 + [
+        C.c_char_p, C.c_size_t]
+    lib.gome_render_match_result.restype = C.c_int64
+    for f in ("gome_create", "gome_submit_batch", "gome_submit_batch_device", "gome_drain_events",
+              "gome_device_events", "gome_get_stats", "gome_snapshot_levels", "gome_snapshot_fifo",
+              "gome_fixed_from_double"):
+        getattr(lib, f).restype = C.c_int32
+    _lib = lib
+    return lib
+
+
+def declared_functions(header: str = HEADER) -> list[str]:
+    """Every function the C-ABI header declares."""
+    txt = open(header).read()
+    return sorted(set(re.findall(r"\b(gome_[a-z_]+)\s*\(", txt)) - {"gome_status"})
+
+
+def fixed_from_double(x: float, accuracy: int = 8) -> int:
+    lib = load_library()
+    out = C.c_int64()
+    s = lib.gome_fixed_from_double(float(x), accuracy, C.byref(out))
+    if s != GOME_OK:
+        raise GomeError(s, f"{x!r} is outside the exact fixed-point domain at accuracy {accuracy}")
+    return out.value
+
+
+def render_match_result(ev: np.void, taker: np.void, symbol: str, taker_uuid: str, taker_oid: str,
+                        maker_uuid: str | None, maker_oid: str | None,
+                        maker_next_oid: str | None, accuracy: int = 8) -> str:
+    lib = load_library()
+    e = np.array([ev], dtype=EVENT_DTYPE)
+    t = np.array([taker], dtype=ORDER_DTYPE)
+    enc = lambda s: None if s is None else s.encode()
+    buf = C.create_string_buffer(8192)
+    n = lib.gome_render_match_result(e.ctypes.data, t.ctypes.data, accuracy, symbol.encode(),
+                                     taker_uuid.encode(), taker_oid.encode(), enc(maker_uuid),
+                                     enc(maker_oid), enc(maker_next_oid), buf, len(buf))
+    if n < 0:
+        raise GomeError(GOME_E_INVAL, "render failed")
+    return buf.raw[:n].decode()
+
+
+class Engine:
+    """One engine handle per GPU (include/gome/gome_abi.h)."""
+
+    def __init__(self, max_symbols: int, max_batch: int, max_nodes: int = 1 << 20,
+                 max_levels: int = 1 << 20, accuracy: int = 8, device: int = 0,
+                 max_events: int = 0):
+        self.lib = load_library()
+        cfg = Config(accuracy=accuracy, device=device, max_symbols=max_symbols,
+                     max_batch=max_batch, max_nodes=max_nodes, max_levels=max_levels,
+                     max_events=max_events)
+        h = C.c_void_p()
+        s = self.lib.gome_create(C.byref(cfg), C.byref(h))
+        if s != GOME_OK:
+            raise GomeError(s, self.lib.gome_last_error(None).decode())
+        self.h = h
+        self.max_batch = max_batch
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.gome_destroy(self.h)
+            self.h = None
+
+    __del__ = close
+
+    def _check(self, s):
+        if s != GOME_OK:
+            raise GomeError(s, self.lib.gome_last_error(self.h).decode())
+
+    def submit(self, rec: np.ndarray, seq_base: int = 0):
+        rec = np.ascontiguousarray(rec, dtype=ORDER_DTYPE)
+        self._check(self.lib.gome_submit_batch(self.h, rec.ctypes.data, len(rec), seq_base))
+
+    def submit_device(self, dev_ptr: int, n: int, seq_base: int = 0, stream: int | None = None):
+        self._check(self.lib.gome_submit_batch_device(self.h, C.c_void_p(dev_ptr), n, seq_base,
+                                                      C.c_void_p(stream or 0)))
+
+    def drain(self) -> np.ndarray:
+        n = self.lib.gome_pending_events(self.h)
+        out = np.zeros(n, EVENT_DTYPE)
+        got = C.c_size_t()
+        self._check(self.lib.gome_drain_events(self.h, out.ctypes.data, n, C.byref(got)))
+        return out[:got.value]
+
+    def device_events(self):
+        p, n = C.c_void_p(), C.c_size_t()
+        self._check(self.lib.gome_device_events(self.h, C.byref(p), C.byref(n)))
+        return p.value, n.value
+
+    def stats(self) -> dict:
+        st = Stats()
+        self._check(self.lib.gome_get_stats(self.h, C.byref(st)))
+        return st.as_dict()
+
+    def levels(self, symbol_id: int) -> np.ndarray:
+        n = C.c_size_t()
+        self._check(self.lib.gome_snapshot_levels(self.h, symbol_id, None, 0, C.byref(n)))
+        out = np.zeros(n.value, LEVEL_DTYPE)
+        self._check(self.lib.gome_snapshot_levels(self.h, symbol_id, out.ctypes.data, n.value,
+                                                  C.byref(n)))
+        return out
+
+    def fifo(self, symbol_id: int, price_fx: int) -> np.ndarray:
+        n = C.c_size_t()
+        self._check(self.lib.gome_snapshot_fifo(self.h, symbol_id, price_fx, None, 0, C.byref(n)))
+        out = np.zeros(n.value, NODE_DTYPE)
+        self._check(self.lib.gome_snapshot_fifo(self.h, symbol_id, price_fx, out.ctypes.data,
+                                                n.value, C.byref(n)))
+        return out

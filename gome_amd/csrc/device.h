@@ -1,0 +1,101 @@
+// device.h — device-side data layout of the MI355X matching engine.
+//
+// Book state lives in HBM and mirrors the reference's Redis key schema
+//  per symbol S:
+//   Level  <- S:depth field (depth), S:BUY / S:SALE membership (member bits),
+//             S:link:<price> "f"/"l" pointers (head/tail chunk + slot)
+//   Chunk  <- the JSON nodes of S:link:<price>, 32 FIFO slots per chunk (SoA)
+//   IdxEnt <- HGET S:link:<p> S:node:<oid> (engine.go:92-93) as an (S, oid) index
+#pragma once
+#include <stdint.h>
+
+namespace gome {
+
+constexpr int WAVE = 64;
+constexpr int CH = 32;                 // FIFO slots per chunk
+constexpr uint32_t NIL = 0xFFFFFFFFu;
+constexpr uint8_t M_BUY = 1, M_SALE = 2;  // side-set membership bits
+constexpr unsigned long long KEY_EMPTY = 0ull, KEY_TOMB = ~0ull;
+
+// One price level (32 B).  Levels of a book form an array sorted by price.
+struct Level {
+  int64_t price;
+  int64_t depth;     // == sum of live FIFO volumes (S:depth:<price>)
+  uint32_t head;     // head chunk id or NIL (FIFO empty)
+  uint32_t tail;     // tail chunk id or NIL
+  uint8_t hslot;     // first not-yet-consumed slot of the head chunk
+  uint8_t tslot;     // next free slot of the tail chunk
+  uint8_t member;    // M_BUY | M_SALE
+  uint8_t pad;
+  uint32_t nlive;    // live FIFO nodes
+};
+static_assert(sizeof(Level) == 32, "Level layout");
+
+// 32 FIFO slots (768 B).  rem < 0 marks a cancelled slot (tombstone).
+struct Chunk {
+  int64_t rem[CH];
+  uint32_t oid[CH];
+  uint32_t uuid[CH];
+  uint32_t ixs[CH];  // cancel-index slot of the node (O(1) erase on fill)
+  uint8_t tx[CH];    // raw Transaction of the resting order
+  uint32_t next;     // next chunk of the FIFO or NIL
+  uint32_t pad0;
+  int64_t price;     // level price (Q3 check on cancel)
+  uint8_t pad[768 - 688];
+};
+static_assert(sizeof(Chunk) == 768, "Chunk layout");
+
+struct Book {
+  uint32_t lvl_base, n_lvl, lvl_cap, pad;
+};
+
+struct IdxEnt {
+  unsigned long long key;  // ((S+1) << 32) | oid ; 0 empty, ~0 tombstone
+  uint32_t loc;            // chunk * CH + slot
+  uint32_t pad;
+};
+
+// error bits
+enum : uint32_t {
+  ERR_INPUT = 1u,        // record outside the domain (symbol range, volume, price)
+  ERR_LEVELS = 2u,       // level pool exhausted
+  ERR_CHUNKS = 4u,       // chunk pool exhausted
+  ERR_EVENTS = 8u,       // event arena exhausted
+  ERR_INDEX = 16u,       // cancel index full
+  ERR_CORRUPT = 32u,     // internal invariant violated
+};
+
+// counters (u64), per batch unless noted
+enum {
+  C_FILLS = 0, C_CANCELS, C_RESTS, C_DROPPED, C_ADD, C_DEL, C_EVENTS,
+  C_RESTING_DELTA, C_LEVELS_DELTA, C_MAXSEG, C_NSEG, C_NCTR = 16
+};
+
+struct Status {
+  unsigned long long ctr[C_NCTR];
+  uint32_t err;
+  uint32_t nseg;
+  uint32_t ev_bump;
+  uint32_t n_events;
+  int32_t free_top;
+  uint32_t freed_top;
+  uint32_t pad[2];
+};
+
+struct Dev {
+  Book* books;
+  uint32_t max_symbols;
+  Level* lvl;
+  uint32_t lvl_cap_total;
+  uint32_t* lvl_bump;
+  Chunk* ch;
+  uint32_t ch_cap;
+  uint32_t* ch_bump;
+  uint32_t* free_ids;
+  uint32_t* freed_ids;
+  IdxEnt* idx;
+  unsigned long long idx_mask;
+  Status* st;
+};
+
+}  // namespace gome

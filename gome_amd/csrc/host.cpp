@@ -1,0 +1,206 @@
+// host.cpp — host-side pieces of the drop-in boundary that do no device work:
+//   * exact fixed-point conversion (ordernode.go:76-87 via shopspring/decimal v1.2.0)
+//   * MatchResult JSON rendering byte-identical to Go encoding/json of
+//     engine.MatchResult (engine.go:24-28) / engine.OrderNode (ordernode.go:9-36)
+#include <charconv>
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "../../include/gome/gome_abi.h"
+
+namespace {
+
+// shopspring decimal.NewFromFloat keeps the shortest round-trip decimal of x;
+// Mul by NewFromFloat(10^acc) is exact; Float64() rounds the exact product to the
+// nearest float64.  The product is an integer iff the shortest decimal has at most
+// `acc` fractional digits; then the float64 is that integer whenever |v| < 2^53.
+gome_status fixed_from_double(double x, uint32_t acc, int64_t* out) {
+  if (!out || !std::isfinite(x) || acc > 18) return GOME_E_INVAL;
+  if (x == 0.0) { *out = 0; return GOME_OK; }
+  char buf[64];
+  auto r = std::to_chars(buf, buf + sizeof buf, x, std::chars_format::scientific);
+  if (r.ec != std::errc()) return GOME_E_INVAL;
+  *r.ptr = 0;
+  // buf = [-]d[.ddd]e[+-]XX
+  const char* p = buf;
+  bool neg = false;
+  if (*p == '-') { neg = true; ++p; }
+  char digits[40];
+  int nd = 0;
+  for (; *p && *p != 'e'; ++p)
+    if (*p != '.') digits[nd++] = *p;
+  if (*p != 'e') return GOME_E_INVAL;
+  int e10 = std::atoi(p + 1) - (nd - 1);  // x = digits * 10^e10
+  while (nd > 1 && digits[nd - 1] == '0') { --nd; ++e10; }
+  int shift = e10 + static_cast<int>(acc);
+  if (shift < 0) return GOME_E_INVAL;  // more than acc decimals: non-integer product (Q5)
+  const uint64_t lim = 1ULL << 53;
+  uint64_t v = 0;
+  for (int i = 0; i < nd; ++i) {
+    v = v * 10 + static_cast<uint64_t>(digits[i] - '0');
+    if (v >= lim) return GOME_E_INVAL;
+  }
+  for (int i = 0; i < shift; ++i) {
+    v *= 10;
+    if (v >= lim) return GOME_E_INVAL;
+  }
+  *out = neg ? -static_cast<int64_t>(v) : static_cast<int64_t>(v);
+  return GOME_OK;
+}
+
+// ---- Go encoding/json pieces -------------------------------------------------
+struct Out {
+  char* buf;
+  size_t cap, n = 0;
+  bool ok = true;
+  void put(const char* s, size_t k) {
+    if (n + k >= cap) { ok = false; return; }
+    std::memcpy(buf + n, s, k);
+    n += k;
+  }
+  void put(const char* s) { put(s, std::strlen(s)); }
+  void putc(char c) { put(&c, 1); }
+};
+
+// encoding/json string encoder with HTML escaping (the default for json.Marshal).
+void json_string(Out& o, const char* s) {
+  static const char hex[] = "0123456789abcdef";
+  o.putc('"');
+  for (const unsigned char* p = reinterpret_cast<const unsigned char*>(s); *p; ++p) {
+    unsigned char c = *p;
+    if (c == '"') o.put("\\\"");
+    else if (c == '\\') o.put("\\\\");
+    else if (c == '\n') o.put("\\n");
+    else if (c == '\r') o.put("\\r");
+    else if (c == '\t') o.put("\\t");
+    else if (c < 0x20 || c == '<' || c == '>' || c == '&') {
+      char u[7] = {'\\', 'u', '0', '0', hex[c >> 4], hex[c & 15], 0};
+      o.put(u, 6);
+    } else if (c == 0xE2 && p[1] == 0x80 && (p[2] == 0xA8 || p[2] == 0xA9)) {
+      o.put(p[2] == 0xA8 ? "\\u2028" : "\\u2029");
+      p += 2;
+    } else {
+      o.putc(static_cast<char>(c));
+    }
+  }
+  o.putc('"');
+}
+
+// encoding/json float64: strconv 'f' -1, or 'e' -1 outside [1e-6, 1e21) with the
+// exponent cleaned from e-09 to e-9.
+void json_float(Out& o, double f) {
+  char b[64];
+  double a = std::fabs(f);
+  if (a != 0 && (a < 1e-6 || a >= 1e21)) {
+    auto r = std::to_chars(b, b + sizeof b, f, std::chars_format::scientific);
+    size_t n = static_cast<size_t>(r.ptr - b);
+    if (n >= 4 && b[n - 4] == 'e' && b[n - 3] == '-' && b[n - 2] == '0') {
+      b[n - 2] = b[n - 1];
+      --n;
+    }
+    o.put(b, n);
+    return;
+  }
+  if (f == 0) { o.put(std::signbit(f) ? "-0" : "0"); return; }
+  auto r = std::to_chars(b, b + sizeof b, f, std::chars_format::fixed);
+  o.put(b, static_cast<size_t>(r.ptr - b));
+}
+
+void json_int(Out& o, long long v) {
+  char b[32];
+  int k = std::snprintf(b, sizeof b, "%lld", v);
+  o.put(b, static_cast<size_t>(k));
+}
+
+// decimal.NewFromFloat(price).String() for an integer-valued price (ordernode.go:106,115).
+std::string price_str(int64_t p) { return std::to_string(p); }
+
+struct NodeView {
+  int action;
+  const char* uuid;
+  const char* oid;
+  const char* symbol;
+  int transaction;
+  int64_t price, volume;
+  uint32_t accuracy;
+  bool is_first, is_last;
+  const char* next_oid;  // nullptr => NextNode ""
+};
+
+// encoding/json of OrderNode, fields in declaration order (ordernode.go:9-36), keys
+// built as SetOrderHashKey/SetListZsetKey/SetDepthHashKey/SetNodeName/SetNodeLink.
+void render_node(Out& o, const NodeView& v) {
+  std::string S(v.symbol), P = price_str(v.price);
+  bool sale = v.transaction == GOME_SALE;
+  o.put("{\"Action\":"); json_int(o, v.action);
+  o.put(",\"Uuid\":"); json_string(o, v.uuid);
+  o.put(",\"Oid\":"); json_string(o, v.oid);
+  o.put(",\"Symbol\":"); json_string(o, v.symbol);
+  o.put(",\"Transaction\":"); json_int(o, v.transaction);
+  o.put(",\"Price\":"); json_float(o, static_cast<double>(v.price));
+  o.put(",\"Volume\":"); json_float(o, static_cast<double>(v.volume));
+  o.put(",\"Accuracy\":"); json_int(o, v.accuracy);
+  o.put(",\"NodeName\":"); json_string(o, (S + ":node:" + v.oid).c_str());
+  o.put(",\"IsFirst\":"); o.put(v.is_first ? "true" : "false");
+  o.put(",\"IsLast\":"); o.put(v.is_last ? "true" : "false");
+  o.put(",\"PrevNode\":\"\"");
+  o.put(",\"NextNode\":");
+  json_string(o, v.next_oid ? (S + ":node:" + v.next_oid).c_str() : "");
+  o.put(",\"NodeLink\":"); json_string(o, (S + ":link:" + P).c_str());
+  o.put(",\"OrderHashKey\":"); json_string(o, (S + ":comparison").c_str());
+  o.put(",\"OrderHashField\":");
+  json_string(o, (S + ":" + v.uuid + ":" + v.oid).c_str());
+  o.put(",\"OrderListZsetKey\":"); json_string(o, (S + (sale ? ":SALE" : ":BUY")).c_str());
+  o.put(",\"OrderListZsetRKey\":"); json_string(o, (S + (sale ? ":BUY" : ":SALE")).c_str());
+  o.put(",\"OrderDepthHashKey\":"); json_string(o, (S + ":depth").c_str());
+  o.put(",\"OrderDepthHashField\":"); json_string(o, (S + ":depth:" + P).c_str());
+  o.putc('}');
+}
+
+}  // namespace
+
+extern "C" gome_status gome_fixed_from_double(double x, uint32_t accuracy, int64_t* out) {
+  return fixed_from_double(x, accuracy, out);
+}
+
+extern "C" int64_t gome_render_match_result(const gome_event* ev, const gome_order* taker,
+                                            uint32_t accuracy, const char* symbol,
+                                            const char* taker_uuid, const char* taker_oid,
+                                            const char* maker_uuid, const char* maker_oid,
+                                            const char* maker_next_oid, char* buf,
+                                            size_t cap) {
+  if (!ev || !taker || !symbol || !taker_uuid || !taker_oid || !buf) return -1;
+  Out o{buf, cap};
+  o.put("{\"Node\":");
+  if (ev->kind == GOME_EV_CANCEL) {
+    // engine.go:109 — MatchResult{Node: node, MatchNode: node, MatchVolume: 0}, with
+    // node.Volume overwritten by the stored remaining volume (engine.go:89,100).
+    NodeView n{taker->action, taker_uuid, taker_oid, symbol, taker->side, taker->price_fx,
+               ev->maker_volume_fx, accuracy, false, false, nullptr};
+    render_node(o, n);
+    o.put(",\"MatchNode\":");
+    render_node(o, n);
+  } else {
+    if (!maker_uuid || !maker_oid) return -1;
+    // Node: the taker after this fill (engine.go:154,171,190).
+    NodeView t{taker->action, taker_uuid, taker_oid, symbol, taker->side, taker->price_fx,
+               ev->taker_volume_fx, accuracy, false, false, nullptr};
+    render_node(o, t);
+    // MatchNode: the FIFO head as stored (IsFirst, PrevNode "", Action ADD).
+    NodeView m{GOME_ADD, maker_uuid, maker_oid, symbol, ev->maker_side, ev->price_fx,
+               ev->maker_volume_fx, accuracy, true, ev->maker_is_last != 0,
+               ev->maker_is_last ? nullptr : maker_next_oid};
+    if (!ev->maker_is_last && !maker_next_oid) return -1;
+    o.put(",\"MatchNode\":");
+    render_node(o, m);
+  }
+  o.put(",\"MatchVolume\":");
+  json_float(o, static_cast<double>(ev->match_volume_fx));
+  o.putc('}');
+  if (!o.ok) return -1;
+  buf[o.n] = 0;
+  return static_cast<int64_t>(o.n);
+}

@@ -1,0 +1,174 @@
+"""Seeded synthetic order streams for BASELINE.json configs 1-5.
+
+The reference's only load generators are gomengine/doorder.go (1,999 random limit
+orders) and gomengine/delorder.go (one cancel).  Their distribution is reproduced
+here, not their time-seeded stream (doorder.go:34-35 seeds from the clock):
+
+  side   ~ U{0,1}                                       doorder.go:37
+  price  = round2(U[0,1)), 0 -> 0.10                     doorder.go:38-41, :63-67
+  volume = round2(U[0,1)), 0 -> 1.00                     doorder.go:43-47
+
+In fixed point at accuracy 8 that is price_fx in {1e6 .. 1e8} step 1e6 and
+volume_fx in {1e6 .. 1e8} step 1e6.  Records use the gome_order layout of
+include/gome/gome_abi.h (32 bytes).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+ORDER_DTYPE = np.dtype([
+    ("price_fx", "<i8"), ("volume_fx", "<i8"), ("symbol_id", "<u4"), ("oid_id", "<u4"),
+    ("uuid_id", "<u4"), ("side", "u1"), ("action", "u1"), ("flags", "<u2"),
+])
+assert ORDER_DTYPE.itemsize == 32
+
+EVENT_DTYPE = np.dtype([
+    ("price_fx", "<i8"), ("match_volume_fx", "<i8"), ("maker_volume_fx", "<i8"),
+    ("taker_volume_fx", "<i8"), ("taker_seq", "<u4"), ("fill_idx", "<u4"),
+    ("symbol_id", "<u4"), ("maker_oid_id", "<u4"), ("maker_uuid_id", "<u4"),
+    ("maker_next_oid_id", "<u4"), ("kind", "u1"), ("maker_side", "u1"),
+    ("maker_is_last", "u1"), ("pad0", "u1"), ("pad1", "<u4"),
+])
+assert EVENT_DTYPE.itemsize == 64
+
+LEVEL_DTYPE = np.dtype([("price_fx", "<i8"), ("depth_fx", "<i8"), ("n_nodes", "<u4"),
+                        ("in_buy", "u1"), ("in_sale", "u1"), ("pad", "<u2")])
+NODE_DTYPE = np.dtype([("volume_fx", "<i8"), ("oid_id", "<u4"), ("uuid_id", "<u4"),
+                       ("side", "u1"), ("pad", "u1", (7,))])
+
+FX = 10 ** 8  # accuracy 8 (config.yaml.example:24)
+ADD, DEL = 1, 2
+
+
+def doorder_prices(rng: np.random.Generator, n: int, decimals: int = 2) -> np.ndarray:
+    """round(U[0,1), decimals) with 0 -> 0.10, in fixed point (doorder.go:38-41)."""
+    q = 10 ** decimals
+    k = np.rint(rng.random(n) * q).astype(np.int64)
+    k[k == 0] = q // 10
+    return k * (FX // q)
+
+
+def doorder_volumes(rng: np.random.Generator, n: int) -> np.ndarray:
+    """round2(U[0,1)) with 0 -> 1.00, in fixed point (doorder.go:43-47)."""
+    k = np.rint(rng.random(n) * 100).astype(np.int64)
+    k[k == 0] = 100
+    return k * (FX // 100)
+
+
+class ZipfSymbols:
+    """Symbol ranks ~ Zipf(s) over n symbols, mapped to ids by a fixed permutation."""
+
+    def __init__(self, n_symbols: int, s: float = 1.0, seed: int = 7):
+        w = 1.0 / np.arange(1, n_symbols + 1, dtype=np.float64) ** s
+        self.cdf = np.cumsum(w / w.sum())
+        self.cdf[-1] = 1.0
+        self.rank_to_id = np.random.default_rng(seed).permutation(n_symbols).astype(np.uint32)
+        self.id_to_rank = np.empty(n_symbols, np.uint32)
+        self.id_to_rank[self.rank_to_id] = np.arange(n_symbols, dtype=np.uint32)
+        self.n = n_symbols
+
+    def share_of_top(self) -> float:
+        return float(self.cdf[0])
+
+    def sample_ranks(self, rng, n):
+        return np.searchsorted(self.cdf, rng.random(n), side="right").astype(np.uint32)
+
+
+class Stream:
+    """Deterministic ADD-only doorder-distribution stream over many symbols.
+
+    cfg 1: n_symbols=1 (uuid 2, fresh oids) ; cfg 2: uniform over 1k symbols ;
+    cfg 3: Zipf(s) over 100k symbols ; cfg 5: price_decimals=4 over 1M symbols.
+    `owner=(rank, world)` keeps only symbols whose Zipf rank % world == rank
+    (round-robin over descending expected load).
+    """
+
+    def __init__(self, n_symbols: int, zipf_s: float | None = None, seed: int = 42,
+                 price_decimals: int = 2, owner: tuple[int, int] | None = None):
+        self.rng = np.random.default_rng(seed)
+        self.n_symbols = n_symbols
+        self.zipf = ZipfSymbols(n_symbols, zipf_s) if zipf_s else None
+        self.price_decimals = price_decimals
+        self.owner = owner
+        self.next_oid = 1
+
+    def _symbols(self, n):
+        if self.zipf is None:
+            ranks = self.rng.integers(0, self.n_symbols, n, dtype=np.uint32)
+            ids = ranks
+        else:
+            ranks = self.zipf.sample_ranks(self.rng, n)
+            ids = self.zipf.rank_to_id[ranks]
+        return ids, ranks
+
+    def batch(self, n: int) -> np.ndarray:
+        """Next n records of the global stream (before ownership filtering)."""
+        rec = np.zeros(n, ORDER_DTYPE)
+        ids, ranks = self._symbols(n)
+        rec["symbol_id"] = ids
+        rec["price_fx"] = doorder_prices(self.rng, n, self.price_decimals)
+        rec["volume_fx"] = doorder_volumes(self.rng, n)
+        rec["side"] = self.rng.integers(0, 2, n, dtype=np.uint8)
+        rec["action"] = ADD
+        rec["uuid_id"] = 2
+        rec["oid_id"] = np.arange(self.next_oid, self.next_oid + n, dtype=np.uint64).astype(np.uint32)
+        self.next_oid += n
+        if self.owner is not None:
+            r, w = self.owner
+            rec = rec[(ranks % w) == r]
+        return rec
+
+
+def cancel_mix(n: int, n_symbols: int, seed: int = 42, del_frac: float = 0.5,
+               aggressive_frac: float = 0.10, zipf_s: float | None = None,
+               price_decimals: int = 2) -> np.ndarray:
+    """Config 4: cancel-heavy mix (sequential generator; use for <= a few M records).
+
+    Each DEL targets a uniformly chosen previously-ADDed, not-yet-cancelled order
+    with its original symbol/side/price/uuid (a filled target is a no-op, as in the
+    reference, engine.go:96-98).  10% of ADDs are aggressive: BUY @ 1.00 or
+    SALE @ 0.01 with volume k * 10.00, k ~ U{1..16} (sweeps several levels).
+    """
+    rng = np.random.default_rng(seed)
+    rec = np.zeros(n, ORDER_DTYPE)
+    if zipf_s:
+        z = ZipfSymbols(n_symbols, zipf_s)
+        syms = z.rank_to_id[z.sample_ranks(rng, n)]
+    else:
+        syms = rng.integers(0, n_symbols, n, dtype=np.uint32)
+    prices = doorder_prices(rng, n, price_decimals)
+    vols = doorder_volumes(rng, n)
+    sides = rng.integers(0, 2, n, dtype=np.uint8)
+    is_del = rng.random(n) < del_frac
+    aggr = rng.random(n) < aggressive_frac
+    ks = rng.integers(1, 17, n)
+    pick = rng.random(n)
+    live: list[int] = []  # indices of ADDs not yet targeted
+    oid = 1
+    for i in range(n):
+        if is_del[i] and live:
+            j = int(pick[i] * len(live))
+            t = live[j]
+            live[j] = live[-1]
+            live.pop()
+            rec[i] = rec[t]
+            rec[i]["action"] = DEL
+            continue
+        rec[i]["action"] = ADD
+        rec[i]["symbol_id"] = syms[i]
+        rec[i]["side"] = sides[i]
+        rec[i]["uuid_id"] = 2
+        rec[i]["oid_id"] = oid
+        oid += 1
+        if aggr[i]:
+            rec[i]["price_fx"] = FX if sides[i] == 0 else FX // 100
+            rec[i]["volume_fx"] = int(ks[i]) * 10 * FX
+        else:
+            rec[i]["price_fx"] = prices[i]
+            rec[i]["volume_fx"] = vols[i]
+        live.append(i)
+    return rec
+
+
+def split_batches(rec: np.ndarray, batch: int):
+    return [rec[i:i + batch] for i in range(0, len(rec), batch)]

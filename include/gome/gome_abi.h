@@ -1,0 +1,201 @@
+/*
+ * gome_abi.h — C-ABI of the MI355X batch matching engine (drop-in for gome's
+ * order-matching hot path).
+ *
+ * The reference engine entry point is the Go function
+ *     func DoOrder(node OrderNode) bool              gomengine/engine/engine.go:46
+ * called once per message by the serial consumer loop
+ *     for d := range msgs { ... DoOrder(order) }      gomengine/engine/rabbitmq.go:116-125
+ * with book state in Redis (nodepool.go, nodelink.go) and one MatchResult JSON
+ * published per fill/cancel (engine.go:24-28,109-113,154-158,171-175,190-194).
+ *
+ * This header replaces that per-message call with a per-batch call: the caller
+ * (batching consumer, cgo backend) converts OrderNode messages to
+ * 32-byte gome_order records and submits them in consume order; the engine
+ * applies them with exactly the reference's sequential semantics per symbol and
+ * returns 64-byte gome_event records in the reference's publish order.
+ *
+ * Conventions: plain C types only, no exceptions or panics across the ABI,
+ * every call returns a gome_status, the handle is not thread-safe (one host
+ * thread per handle, as the reference has one consumer goroutine,
+ * rabbitmq.go:116).  The caller owns all host buffers for the call's duration;
+ * no pointer is retained across calls.
+ */
+#ifndef GOME_ABI_H
+#define GOME_ABI_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GOME_ABI_VERSION 1u
+
+/* ---- status codes (replace the reference's swallowed errors / panics,
+ *      rabbitmq.go:44-49,70-72,120-122; nodelink.go:132,142,157) ---------- */
+typedef int32_t gome_status;
+enum {
+  GOME_OK = 0,
+  GOME_E_INVAL = 1,     /* input outside the exact parity domain (Q5/Q7), bad args */
+  GOME_E_CAPACITY = 2,  /* a device pool (levels, nodes, index, events) is full    */
+  GOME_E_DEVICE = 3,    /* HIP runtime error / no device                           */
+  GOME_E_STATE = 4,     /* engine poisoned by an earlier fatal error                */
+  GOME_E_NOTFOUND = 5,  /* lookup miss (snapshot of an unknown symbol, ...)         */
+};
+
+/* ---- actions and sides ---------------------------------------------------- */
+enum { GOME_ADD = 1, GOME_DEL = 2 };      /* engine.go:14-18, main.go:14-18 */
+enum { GOME_BUY = 0, GOME_SALE = 1 };     /* api/order.proto:4-7            */
+/* side is the raw OrderRequest.transaction value; SALE iff side == 1, any other
+ * value is treated as BUY (ordernode.go:95, nodepool.go:89), and is echoed back
+ * unchanged in events (MatchNode.Transaction). */
+
+/* ---- records ------------------------------------------------------------- */
+
+/* One consumed OrderNode message (ordernode.go:9-36) in fixed point.
+ * price_fx / volume_fx = value * 10^accuracy exactly (ordernode.go:76-87, see
+ * gome_fixed_from_double).  The sequence number of a record is its index in the
+ * submitted batch (plus the batch's seq_base). */
+typedef struct gome_order {
+  int64_t price_fx;   /* OrderNode.Price  (limit price; request price for DEL)  */
+  int64_t volume_fx;  /* OrderNode.Volume (>= 0)                                */
+  uint32_t symbol_id; /* interned OrderNode.Symbol, < gome_config.max_symbols    */
+  uint32_t oid_id;    /* interned OrderNode.Oid   (unique per symbol, README:27) */
+  uint32_t uuid_id;   /* interned OrderNode.Uuid                                 */
+  uint8_t side;       /* raw OrderNode.Transaction                               */
+  uint8_t action;     /* OrderNode.Action: 1 ADD, 2 DEL, anything else ignored   */
+  uint16_t flags;     /* reserved, must be 0                                     */
+} gome_order;
+
+enum { GOME_EV_FILL = 1, GOME_EV_CANCEL = 2 };
+
+/* One published MatchResult (engine.go:24-28).
+ *   FILL   (engine.go:154,171,190): Node = taker after the fill, MatchNode = maker
+ *          as read from the FIFO head (IsFirst=true, PrevNode=""), MatchVolume = qty.
+ *   CANCEL (engine.go:109): Node = MatchNode = the DEL request with Volume = the
+ *          stored remaining volume; MatchVolume = 0.
+ * Events of one batch are returned in the reference publish order, i.e. sorted by
+ * (taker_seq, fill_idx). */
+typedef struct gome_event {
+  int64_t price_fx;         /* level price (= MatchNode.Price); DEL: request price  */
+  int64_t match_volume_fx;  /* MatchVolume                                           */
+  int64_t maker_volume_fx;  /* MatchNode.Volume: pre-fill if fully filled, else the
+                               maker's remaining volume; DEL: stored remaining       */
+  int64_t taker_volume_fx;  /* Node.Volume: taker remaining after this fill          */
+  uint32_t taker_seq;       /* index of the ADD/DEL in its batch                     */
+  uint32_t fill_idx;        /* 0,1,2... within one taker                             */
+  uint32_t symbol_id;
+  uint32_t maker_oid_id;    /* MatchNode.Oid                                         */
+  uint32_t maker_uuid_id;   /* MatchNode.Uuid                                        */
+  uint32_t maker_next_oid_id; /* MatchNode.NextNode = S:node:<this> unless is_last   */
+  uint8_t kind;             /* GOME_EV_FILL / GOME_EV_CANCEL                         */
+  uint8_t maker_side;       /* MatchNode.Transaction (raw)                           */
+  uint8_t maker_is_last;    /* MatchNode.IsLast (NextNode == "")                     */
+  uint8_t pad0;
+  uint32_t pad1;
+} gome_event;
+
+/* One price level of a book in the reference key schema (nodepool.go:61-115):
+ * bid/ask membership = presence of the price in S:BUY / S:SALE, depth = the
+ * S:depth:<price> field, nodes = length of the S:link:<price> FIFO. */
+typedef struct gome_level {
+  int64_t price_fx;
+  int64_t depth_fx;
+  uint32_t n_nodes;
+  uint8_t in_buy;   /* member of S:BUY  */
+  uint8_t in_sale;  /* member of S:SALE */
+  uint16_t pad;
+} gome_level;
+
+/* One resting node of a FIFO, in link order (nodelink.go, S:link:<price>). */
+typedef struct gome_node {
+  int64_t volume_fx;
+  uint32_t oid_id;
+  uint32_t uuid_id;
+  uint8_t side;
+  uint8_t pad[7];
+} gome_node;
+
+typedef struct gome_config {
+  uint32_t accuracy;       /* gomengine.accuracy (config.yaml.example:23-24), default 8 */
+  int32_t device;          /* HIP device ordinal (one handle per GPU)                    */
+  uint32_t max_symbols;    /* symbol_id range                                            */
+  uint32_t max_batch;      /* max records per submit                                     */
+  uint64_t max_nodes;      /* resting-order capacity (node pool)                         */
+  uint64_t max_levels;     /* level-record capacity (all books)                          */
+  uint64_t max_events;     /* event capacity per batch (0: derived from max_batch)       */
+  uint32_t flags;          /* reserved, 0                                                */
+  uint32_t pad;
+} gome_config;
+
+/* Per-batch counters of the last submit (and running totals). */
+typedef struct gome_stats {
+  uint64_t n_orders, n_add, n_del, n_dropped; /* dropped = ADD without admission marker */
+  uint64_t n_fills, n_cancels, n_rests, n_events;
+  uint64_t n_resting;                         /* resting nodes after the batch (total)  */
+  uint64_t n_levels;                          /* level records in use (total)           */
+  uint64_t max_segment;                       /* orders of the hottest book this batch  */
+  uint64_t n_segments;                        /* books touched this batch               */
+  double ms_total;                            /* device time of the batch pipeline      */
+  double ms_match;                            /* device time of match_books             */
+} gome_stats;
+
+typedef struct gome_engine gome_engine;
+
+/* ---- lifecycle ----------------------------------------------------------- */
+gome_status gome_create(const gome_config* cfg, gome_engine** out);
+void gome_destroy(gome_engine* e);
+const char* gome_last_error(const gome_engine* e); /* handle-local message, never NULL */
+uint32_t gome_abi_version(void);
+
+/* ---- hot path ------------------------------------------------------------ */
+/* Apply one batch of host records (replaces n calls of DoOrder, engine.go:46).
+ * Synchronous: on return the events are queued for gome_drain_events. */
+gome_status gome_submit_batch(gome_engine* e, const gome_order* orders, size_t n,
+                              uint64_t seq_base);
+/* Same, with the records already resident in device memory (HBM); `stream` is a
+ * hipStream_t or NULL.  Events stay on the device: read them with
+ * gome_device_events or copy them out with gome_drain_events. */
+gome_status gome_submit_batch_device(gome_engine* e, const gome_order* dev_orders,
+                                     size_t n, uint64_t seq_base, void* stream);
+/* Copy out up to cap pending events in publish order; *n_out = copied. */
+gome_status gome_drain_events(gome_engine* e, gome_event* out, size_t cap,
+                              size_t* n_out);
+size_t gome_pending_events(const gome_engine* e);
+/* Device pointer + count of the last batch's events (valid until next submit). */
+gome_status gome_device_events(gome_engine* e, const gome_event** dev_ptr,
+                               size_t* n);
+gome_status gome_get_stats(const gome_engine* e, gome_stats* out);
+
+/* ---- book state (Redis-schema view; snapshot / parity) ------ */
+/* Levels of one book in ascending price order, including empty levels that
+ * still carry a side-set membership (Q2).  *n_out = number of levels; when
+ * cap < *n_out only cap are written. */
+gome_status gome_snapshot_levels(gome_engine* e, uint32_t symbol_id,
+                                 gome_level* out, size_t cap, size_t* n_out);
+/* Nodes of the FIFO at one price, head first. */
+gome_status gome_snapshot_fifo(gome_engine* e, uint32_t symbol_id, int64_t price_fx,
+                               gome_node* out, size_t cap, size_t* n_out);
+
+/* ---- host helpers (no device work) --------------------------------------- */
+/* ordernode.go:76-87: Float64(decimal.NewFromFloat(x) * decimal.NewFromFloat(10^acc)).
+ * Succeeds iff that product is an integer with |v| < 2^53 (the domain on which the
+ * reference's float64 / Redis long-double arithmetic is exact integer arithmetic);
+ * otherwise GOME_E_INVAL (e.g. 0.123456789 at acc 8). */
+gome_status gome_fixed_from_double(double x, uint32_t accuracy, int64_t* out);
+/* Render one event as the reference's MatchResult JSON (Go encoding/json of
+ * engine.MatchResult, byte-identical).  Strings are the host's interned names;
+ * `taker` is the record at event->taker_seq.  Returns bytes written (excl. NUL)
+ * or a negative value if cap is too small. */
+int64_t gome_render_match_result(const gome_event* ev, const gome_order* taker,
+                                 uint32_t accuracy, const char* symbol,
+                                 const char* taker_uuid, const char* taker_oid,
+                                 const char* maker_uuid, const char* maker_oid,
+                                 const char* maker_next_oid, char* buf, size_t cap);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GOME_ABI_H */

@@ -375,7 +375,8 @@ __device__ __forceinline__ void free_chunk(WaveCtx& W, uint32_t c) {
 
 __device__ void free_chain(WaveCtx& W, uint32_t head, uint32_t tail) {
   uint32_t c = head;
-  while (c != NIL) {
+  for (uint32_t guard = 0; c != NIL; ++guard) {
+    if (guard > W.D.ch_cap) { set_err(W, ERR_CORRUPT); return; }
     uint32_t nx = (c == tail) ? NIL : uni(W.D.ch[c].next);
     free_chunk(W, c);
     c = nx;
@@ -546,7 +547,8 @@ __device__ int64_t match_level(WaveCtx& W, uint32_t k, int64_t T, uint32_t seq, 
   const bool hi = lane >= 32;
   Level lv = W.L[k];
   bool first = true;
-  while (lv.head != NIL && !W.fatal) {
+  for (uint32_t guard = 0; lv.head != NIL && !W.fatal; ++guard) {
+    if (guard > W.D.ch_cap) { set_err(W, ERR_CORRUPT); break; }
     const uint32_t head = lv.head;
     const uint32_t nxt = uni(W.D.ch[head].next);
     const uint32_t cid = hi ? nxt : head;
@@ -596,7 +598,7 @@ __device__ int64_t match_level(WaveCtx& W, uint32_t k, int64_t T, uint32_t seq, 
     if (!mhi && nxt != NIL && ((am >> ll) & 1ull)) {
       // next chunk is all tombstones: search further down the chain
       uint32_t c2 = uni(W.D.ch[nxt].next);
-      while (c2 != NIL) {
+      for (uint32_t guard = 0; c2 != NIL && guard <= W.D.ch_cap; ++guard) {
         uint32_t lim = (c2 == lv.tail) ? lv.tslot : CH;
         bool l2 = lane < lim && W.D.ch[c2].rem[lane < CH ? lane : 0] >= 0;
         unsigned long long m2 = __ballot(l2);
@@ -1031,8 +1033,11 @@ gome_status gome_engine::init(const gome_config& c) {
   bsum_cap = ceil_div(scan_max, SCAN_TILE) + 1;
 
   // ---- persistent book state
-  const unsigned long long nchunks =
-      std::min<unsigned long long>(cfg.max_nodes / 4 + cfg.max_levels, 0xF0000000ull);
+  // chunks: every non-empty level holds >= 1 (plus head/tail chunks partly consumed),
+  // and every 32 resting nodes fill one more
+  const unsigned long long nchunks = std::min<unsigned long long>(
+      cfg.max_nodes / 8 + 2 * std::min<unsigned long long>(cfg.max_levels, cfg.max_nodes) + 1024,
+      0xF0000000ull);
   const unsigned long long idx_cap = next_pow2(std::max<unsigned long long>(2 * cfg.max_nodes, 1024));
   if (!alloc(&D.books, ms, "books") || !alloc(&D.lvl, cfg.max_levels, "levels") ||
       !alloc(&D.lvl_bump, 1, "lvl_bump") || !alloc(&D.ch, nchunks, "chunks") ||

@@ -3,6 +3,14 @@ import sys
 
 import pytest
 
+# One HIP runtime per process: torch bundles its own libamdhip64.so.7 (same SONAME as
+# /opt/rocm's); importing torch first makes libgome.so bind to that one too, so tests
+# that hand torch device buffers to the engine share one runtime.
+try:
+    import torch  # noqa: F401
+except Exception:  # pragma: no cover
+    torch = None
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)

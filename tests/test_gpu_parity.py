@@ -1,0 +1,158 @@
+"""HIP engine parity (MI355X): events bit-exact vs the C oracle, MatchResult JSON
+byte-exact vs the literal transliteration, book state equal, on every config shape.
+All calls go through the C-ABI (libgome.so); there is no CPU fallback."""
+import numpy as np
+import pytest
+
+from gome_amd import workload as wl
+from gome_amd.abi import Engine, GomeError, GOME_E_INVAL
+from oracle.literal import run_batches
+from oracle.pyoracle import Oracle
+from tests.helpers import (Interner, engine_state_to_levels, literal_state_to_levels,
+                           random_batches, render_events, requests_to_records)
+
+pytestmark = pytest.mark.gpu
+
+
+def _engine(max_symbols, max_batch, max_nodes=1 << 20, max_levels=1 << 20):
+    return Engine(max_symbols=max_symbols, max_batch=max_batch, max_nodes=max_nodes,
+                  max_levels=max_levels)
+
+
+def _cmp_events(got: np.ndarray, exp: np.ndarray, tag=""):
+    assert len(got) == len(exp), f"{tag}: {len(got)} events vs oracle {len(exp)}"
+    if len(got) and not np.array_equal(got, exp):
+        bad = np.nonzero(got != exp)[0][0]
+        raise AssertionError(f"{tag}: first mismatch at event {bad}:\n gpu={got[bad]}\n orc={exp[bad]}")
+
+
+def _run_pair(batches, max_symbols, sample_syms=(), **kw):
+    eng = _engine(max_symbols, max(len(b) for b in batches), **kw)
+    orc = Oracle(max_symbols)
+    for i, b in enumerate(batches):
+        eng.submit(b)
+        got = eng.drain()
+        exp = orc.submit(b)
+        _cmp_events(got, exp, f"batch {i}")
+    for s in sample_syms:
+        lv_g, lv_o = eng.levels(s), orc.levels(s)
+        assert np.array_equal(lv_g, lv_o), f"levels of symbol {s}"
+        for p in lv_o["price_fx"]:
+            assert np.array_equal(eng.fifo(s, int(p)), orc.fifo(s, int(p))), f"fifo {s}@{p}"
+    st = eng.stats()
+    assert st["n_resting"] == orc.resting()
+    return eng, orc
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_quirk_streams_vs_literal(seed):
+    """Randomized Appendix-A quirk streams: rendered JSON == literal transliteration."""
+    symbols = ("eth2usdt", "btc2usdt", "ltc2usdt")
+    rng = np.random.default_rng(7000 + seed)
+    batches = random_batches(rng, n_batches=5, batch=80, symbols=symbols,
+                             del_frac=0.1 + 0.15 * (seed % 4))
+    leng, lit = run_batches(batches)
+    names = Interner()
+    for s in symbols:
+        names.id("sym", s)
+    eng = _engine(len(symbols), 256)
+    got = []
+    for b in batches:
+        rec = requests_to_records(b, names)
+        eng.submit(rec)
+        got += render_events(eng.drain(), rec, names)
+    assert got == lit
+    for s in symbols:
+        assert engine_state_to_levels(eng, names.id("sym", s), names) == \
+            literal_state_to_levels(leng.book_state(s))
+
+
+def test_config1_single_symbol():
+    st = wl.Stream(1, seed=42)
+    batches = [st.batch(20000) for _ in range(5)]
+    _run_pair(batches, 1, sample_syms=[0])
+
+
+def test_config2_uniform_1k():
+    st = wl.Stream(1000, seed=42)
+    batches = [st.batch(200000) for _ in range(3)]
+    _run_pair(batches, 1000, sample_syms=[0, 1, 500, 999])
+
+
+def test_config3_zipf_100k():
+    st = wl.Stream(100000, zipf_s=1.0, seed=42)
+    z = st.zipf
+    batches = [st.batch(1 << 19) for _ in range(3)]
+    hot = [int(z.rank_to_id[r]) for r in (0, 1, 2, 50, 5000)]
+    _run_pair(batches, 100000, sample_syms=hot, max_nodes=1 << 21, max_levels=1 << 23)
+
+
+def test_config4_cancel_mix():
+    rec = wl.cancel_mix(300000, 200, seed=42)
+    _run_pair(wl.split_batches(rec, 50000), 200, sample_syms=[0, 7, 199])
+
+
+def test_config4_cancel_mix_zipf_hot():
+    rec = wl.cancel_mix(200000, 1000, seed=3, zipf_s=1.0)
+    _run_pair(wl.split_batches(rec, 65536), 1000, sample_syms=list(range(0, 1000, 97)))
+
+
+def test_config5_deep_books():
+    """4-dp price grid -> up to 10k levels per book (level arrays far beyond 64 lanes)."""
+    st = wl.Stream(64, seed=5, price_decimals=4)
+    batches = [st.batch(100000) for _ in range(3)]
+    eng, orc = _run_pair(batches, 64, sample_syms=[0, 13, 63])
+    assert max(len(orc.levels(s)) for s in range(64)) > 1000
+
+
+def test_tiny_batches_and_many_batches():
+    rng = np.random.default_rng(11)
+    batches = random_batches(rng, n_batches=40, batch=7, symbols=("a", "b"), del_frac=0.35)
+    names = Interner()
+    recs = [requests_to_records(b, names) for b in batches]
+    _run_pair(recs, 2, sample_syms=[0, 1])
+
+
+def test_invalid_batch_rejected_without_state_change():
+    st = wl.Stream(4, seed=1)
+    good = st.batch(1000)
+    eng = _engine(4, 2048)
+    orc = Oracle(4)
+    eng.submit(good)
+    _cmp_events(eng.drain(), orc.submit(good))
+    bad = st.batch(10)
+    bad[3]["symbol_id"] = 99  # out of range
+    with pytest.raises(GomeError) as ei:
+        eng.submit(bad)
+    assert ei.value.status == GOME_E_INVAL
+    bad2 = st.batch(10)
+    bad2[0]["volume_fx"] = -5
+    with pytest.raises(GomeError):
+        eng.submit(bad2)
+    nxt = st.batch(1000)
+    eng.submit(nxt)
+    _cmp_events(eng.drain(), orc.submit(nxt))
+    for s in range(4):
+        assert np.array_equal(eng.levels(s), orc.levels(s))
+
+
+def test_empty_batch():
+    eng = _engine(2, 16)
+    eng.submit(np.zeros(0, wl.ORDER_DTYPE))
+    assert len(eng.drain()) == 0
+
+
+def test_device_submit_and_events():
+    """gome_submit_batch_device: records already resident in HBM; events stay on device."""
+    torch = pytest.importorskip("torch")
+    st = wl.Stream(100, seed=9)
+    b = st.batch(50000)
+    eng = _engine(100, 65536)
+    orc = Oracle(100)
+    t = torch.from_numpy(b.view(np.uint8).copy()).cuda()
+    torch.cuda.synchronize()
+    eng.submit_device(t.data_ptr(), len(b))
+    ptr, n = eng.device_events()
+    exp = orc.submit(b)
+    assert ptr and n == len(exp)
+    _cmp_events(eng.drain(), exp)

@@ -77,9 +77,10 @@ struct Status {
   uint32_t nseg;
   uint32_t ev_bump;
   uint32_t n_events;
-  int32_t free_top;
+  uint32_t nhot;       // segments handled by k_match_hot (first nhot of seg_order)
+  uint32_t pad0;
+  int32_t free_top;    // persists across batches
   uint32_t freed_top;
-  uint32_t pad[2];
 };
 
 struct Dev {

@@ -139,7 +139,10 @@ typedef struct gome_stats {
   uint64_t max_segment;                       /* orders of the hottest book this batch  */
   uint64_t n_segments;                        /* books touched this batch               */
   double ms_total;                            /* device time of the batch pipeline      */
-  double ms_match;                            /* device time of match_books             */
+  double ms_match;                            /* device time of the match phase (hot and
+                                                 cold books, concurrent)                 */
+  double ms_hot;                              /* device time of k_match_hot (hot books)  */
+  uint64_t n_hot;                             /* books applied by k_match_hot            */
 } gome_stats;
 
 typedef struct gome_engine gome_engine;

@@ -23,7 +23,8 @@ class _Stats(C.Structure):
     _fields_ = [(n, C.c_uint64) for n in (
         "n_orders", "n_add", "n_del", "n_dropped", "n_fills", "n_cancels", "n_rests",
         "n_events", "n_resting", "n_levels", "max_segment", "n_segments")] + [
-        ("ms_total", C.c_double), ("ms_match", C.c_double)]
+        ("ms_total", C.c_double), ("ms_match", C.c_double), ("ms_hot", C.c_double),
+        ("n_hot", C.c_uint64)]
 
 
 _lib = None

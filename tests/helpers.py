@@ -59,7 +59,7 @@ def render_events(events: np.ndarray, records: np.ndarray, names: Interner,
 
 
 def random_batches(rng: np.random.Generator, n_batches: int, batch: int, symbols=("eth2usdt", "btc2usdt"),
-                   del_frac: float = 0.3, quirks: bool = True, price_grid=None):
+                   del_frac: float = 0.3, quirks: bool = True, price_grid=None, oid_base: int = 1):
     """Randomized request streams exercising the reference quirks:
     wrong-side / wrong-price / wrong-uuid / unknown cancels (Q2, Q3), DEL before ADD and
     duplicate ADD in one batch (Q4), zero volumes (Q6), Transaction outside {0,1} (Q8),
@@ -68,7 +68,7 @@ def random_batches(rng: np.random.Generator, n_batches: int, batch: int, symbols
     price_grid = price_grid or [0.1, 0.2, 0.25, 0.3, 0.5, 0.55, 0.7, 0.9, 1.0]
     vol_grid = [0.01, 0.1, 0.25, 0.5, 1.0, 1.5, 3.0]
     added = []  # (sym, oid, uuid, side, price)
-    next_oid = 1
+    next_oid = oid_base
     out = []
     for _ in range(n_batches):
         b = []
@@ -146,3 +146,34 @@ def engine_state_to_levels(eng, sym_id: int, names: Interner) -> dict:
 def canon(js: str) -> str:
     """Stable re-serialisation (for readable diffs only; parity compares raw bytes)."""
     return json.dumps(json.loads(js), sort_keys=True)
+
+
+def golden_names():
+    return ["kat", "doorder_3k", "quirk_mix"]
+
+
+def load_golden(name):
+    from tests.golden.make_golden import load
+    g = load(name)
+    return g if isinstance(g, list) else [g]
+
+
+def replay_fixture(fx, make_backend):
+    """Replay a golden fixture through a backend (C oracle or HIP engine) and return
+    (rendered MatchResult JSON list, state dict in the fixture's format).
+    make_backend(n_symbols, max_batch) -> object with .submit(rec) -> events, .levels, .fifo"""
+    names = Interner()
+    batches = [[(a, r) for a, r in b] for b in fx["batches"]]
+    syms = sorted({r["symbol"] for b in batches for _, r in b})
+    for s in syms:
+        names.id("sym", s)
+    be = make_backend(len(syms), max(len(b) for b in batches))
+    out = []
+    for b in batches:
+        rec = requests_to_records(b, names)
+        out += render_events(be.submit(rec), rec, names)
+    state = {}
+    for s in syms:
+        lv = engine_state_to_levels(be, names.id("sym", s), names)
+        state[s] = {str(p): [d, ib, isl, [list(x) for x in fifo]] for p, (d, ib, isl, fifo) in sorted(lv.items())}
+    return out, state

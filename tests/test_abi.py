@@ -1,0 +1,67 @@
+"""CPU checks of the C-ABI boundary: libgome.so loads and exports every function the
+header declares; host helpers (fixed-point conversion, MatchResult rendering) behave
+as the reference; gome_create fails loudly (no CPU fallback) when no GPU is present."""
+import ctypes as C
+import math
+
+import numpy as np
+import pytest
+
+from gome_amd import abi
+from oracle.literal import scale
+
+
+def test_library_exports_every_declared_symbol():
+    lib = abi.load_library()
+    names = abi.declared_functions()
+    assert len(names) >= 14
+    for n in names:
+        assert hasattr(lib, n), n
+    assert lib.gome_abi_version() == 1
+
+
+def test_record_layouts_match_header():
+    from gome_amd.workload import EVENT_DTYPE, LEVEL_DTYPE, NODE_DTYPE, ORDER_DTYPE
+    assert ORDER_DTYPE.itemsize == 32 and EVENT_DTYPE.itemsize == 64
+    assert LEVEL_DTYPE.itemsize == 24 and NODE_DTYPE.itemsize == 24
+    assert C.sizeof(abi.Config) == 48
+
+
+@pytest.mark.parametrize("x", [0.0, 0.1, 0.29, 0.57, 1.0, 12.34, 0.00000001, 123456.12345678,
+                               -0.5, 90071992.54740991, 3.0e7, 1e-8])
+def test_fixed_point_matches_decimal_path(x):
+    """ordernode.go:76-87 via shopspring/decimal: exact where the product is an integer."""
+    v = scale(x, 8)
+    assert v == int(v)
+    assert abi.fixed_from_double(x, 8) == int(v)
+
+
+def test_fixed_point_random_two_decimals():
+    rng = np.random.default_rng(0)
+    for k in rng.integers(0, 10**6, 2000):
+        x = round(float(k) / 100, 2)
+        assert abi.fixed_from_double(x, 8) == int(scale(x, 8))
+
+
+@pytest.mark.parametrize("x", [0.123456789, 1e-9, 2.0 ** 53, 1e300, math.nan, math.inf, 0.1 + 0.2])
+def test_fixed_point_rejects_outside_domain(x):
+    """Q5: more than `accuracy` decimals (or >= 2^53 scaled) is outside the exact domain."""
+    with pytest.raises(abi.GomeError):
+        abi.fixed_from_double(x, 8)
+
+
+def test_fixed_point_other_accuracy():
+    assert abi.fixed_from_double(0.5, 2) == 50
+    with pytest.raises(abi.GomeError):
+        abi.fixed_from_double(12.5, 0)
+    assert abi.fixed_from_double(7.0, 0) == 7
+
+
+def test_create_without_gpu_fails_loudly():
+    pytest.importorskip("torch")
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    with pytest.raises(abi.GomeError) as ei:
+        abi.Engine(max_symbols=4, max_batch=16)
+    assert ei.value.status == abi.GOME_E_DEVICE

@@ -156,3 +156,93 @@ def test_device_submit_and_events():
     exp = orc.submit(b)
     assert ptr and n == len(exp)
     _cmp_events(eng.drain(), exp)
+
+
+# ---- hot books (segments >= 2048 orders take the LDS-resident k_match_hot path) -------
+def test_hot_book_quirks_vs_literal():
+    """One symbol, 2500-order batches (hot path) with every Appendix-A quirk."""
+    rng = np.random.default_rng(4242)
+    batches = random_batches(rng, n_batches=3, batch=2500, symbols=("eth2usdt",), del_frac=0.3)
+    leng, lit = run_batches(batches)
+    names = Interner()
+    names.id("sym", "eth2usdt")
+    eng = _engine(1, 8192)
+    got = []
+    for b in batches:
+        rec = requests_to_records(b, names)
+        eng.submit(rec)
+        assert eng.stats()["n_hot"] == 1
+        got += render_events(eng.drain(), rec, names)
+    assert got == lit
+    assert engine_state_to_levels(eng, 0, names) == literal_state_to_levels(leng.book_state("eth2usdt"))
+
+
+def test_hot_books_cancel_heavy():
+    """Config-4 mix on 4 symbols: every book is hot, half the stream cancels."""
+    rec = wl.cancel_mix(200000, 4, seed=17)
+    eng, orc = _run_pair(wl.split_batches(rec, 40000), 4, sample_syms=[0, 1, 2, 3])
+    assert eng.stats()["n_hot"] == 4
+
+
+def test_hot_and_cold_mixed_zipf_cancels():
+    rec = wl.cancel_mix(400000, 500, seed=23, zipf_s=1.2)
+    eng, orc = _run_pair(wl.split_batches(rec, 100000), 500, sample_syms=list(range(0, 500, 37)))
+    assert eng.stats()["n_hot"] >= 1
+
+
+def test_hot_book_spills_to_hbm():
+    """4-dp prices on 2 symbols: a hot book outgrows the LDS level array mid-segment
+    (spill to the HBM path), later batches start on the HBM path."""
+    st = wl.Stream(2, seed=31, price_decimals=4)
+    batches = [st.batch(24000) for _ in range(3)]
+    eng, orc = _run_pair(batches, 2, sample_syms=[0, 1])
+    assert len(orc.levels(0)) > 1024
+
+
+def test_hot_book_long_fifo_chunk_chains():
+    """Few price points, many resting orders per level: FIFOs span many chunks and the
+    head advances across chunk boundaries (cached head reloads, NextNode lookahead)."""
+    rng = np.random.default_rng(5)
+    n = 60000
+    rec = np.zeros(n, wl.ORDER_DTYPE)
+    rec["symbol_id"] = 0
+    rec["side"] = rng.integers(0, 2, n)
+    rec["price_fx"] = np.where(rec["side"] == 0, 49, 51) * 10**6
+    big = rng.random(n) < 0.05  # occasional aggressive orders sweeping several levels
+    rec["price_fx"][big & (rec["side"] == 0)] = 60 * 10**6
+    rec["price_fx"][big & (rec["side"] == 1)] = 40 * 10**6
+    rec["volume_fx"] = rng.integers(1, 20, n) * 10**6
+    rec["volume_fx"][big] = rng.integers(50, 400, big.sum()) * 10**6
+    rec["action"] = 1
+    rec["uuid_id"] = 2
+    rec["oid_id"] = np.arange(1, n + 1)
+    _run_pair(wl.split_batches(rec, 20000), 1, sample_syms=[0])
+
+
+# ---- golden fixtures (generated by the literal transliteration) --------------------------
+from tests.helpers import golden_names, load_golden, replay_fixture  # noqa: E402
+
+
+class _EngineBackend:
+    def __init__(self, ns, mb):
+        self.e = _engine(ns, max(mb, 16))
+
+    def submit(self, rec):
+        self.e.submit(rec)
+        return self.e.drain()
+
+    def levels(self, s):
+        return self.e.levels(s)
+
+    def fifo(self, s, p):
+        return self.e.fifo(s, p)
+
+
+_GOLDEN = [fx for n in golden_names() for fx in load_golden(n)]
+
+
+@pytest.mark.parametrize("fx", _GOLDEN, ids=[fx["name"] for fx in _GOLDEN])
+def test_engine_reproduces_golden(fx):
+    out, state = replay_fixture(fx, _EngineBackend)
+    assert out == fx["results"]
+    assert state == fx["state"]

@@ -50,6 +50,15 @@ def build_engine(force: bool = False, extra: list[str] | None = None) -> str:
     return LIB
 
 
+def build_stamps() -> str:
+    """Diagnostic build with in-kernel s_memtime phase stamps (never used by the product)."""
+    out = os.path.join(PKG, "libgome_stamps.so")
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-DGOME_STAMPS",
+           "-I", os.path.join(ROOT, "include"), *SOURCES, "-o", out]
+    _run(cmd)
+    return out
+
+
 def build_oracle(force: bool = False) -> str:
     src = os.path.join(ORACLE_DIR, "gome_oracle.c")
     deps = [src, os.path.join(ROOT, "include", "gome", "gome_abi.h")]

@@ -2,10 +2,11 @@
 //
 // Book state lives in HBM and mirrors the reference's Redis key schema
 //  per symbol S:
-//   Level  <- S:depth field (depth), S:BUY / S:SALE membership (member bits),
-//             S:link:<price> "f"/"l" pointers (head/tail chunk + slot)
-//   Chunk  <- the JSON nodes of S:link:<price>, 32 FIFO slots per chunk (SoA)
-//   IdxEnt <- HGET S:link:<p> S:node:<oid> (engine.go:92-93) as an (S, oid) index
+//   Level    <- S:depth field (depth), S:BUY / S:SALE membership (member bits),
+//               S:link:<price> "f"/"l" pointers (head/tail chunk + slot)
+//   Node     <- one JSON node of S:link:<price> (32 B, two 16-B halves)
+//   chunks   <- 32 consecutive Nodes of one FIFO (1 KiB) + a ChunkHdr
+//   IdxEnt   <- HGET S:link:<p> S:node:<oid> (engine.go:92-93) as an (S, oid) index
 #pragma once
 #include <stdint.h>
 
@@ -31,19 +32,23 @@ struct Level {
 };
 static_assert(sizeof(Level) == 32, "Level layout");
 
-// 32 FIFO slots (768 B).  rem < 0 marks a cancelled slot (tombstone).
-struct Chunk {
-  int64_t rem[CH];
-  uint32_t oid[CH];
-  uint32_t uuid[CH];
-  uint32_t ixs[CH];  // cancel-index slot of the node (O(1) erase on fill)
-  uint8_t tx[CH];    // raw Transaction of the resting order
-  uint32_t next;     // next chunk of the FIFO or NIL
-  uint32_t pad0;
-  int64_t price;     // level price (Q3 check on cancel)
-  uint8_t pad[768 - 688];
+// One FIFO slot (32 B).  rem < 0 marks a cancelled slot (tombstone).
+struct alignas(16) Node {
+  int64_t rem;       // remaining volume
+  uint32_t oid;
+  uint32_t uuid;
+  uint32_t ixs;      // cancel-index slot of the node (O(1) erase on fill)
+  uint8_t tx;        // raw Transaction of the resting order
+  uint8_t p0, p1, p2;
+  uint64_t pad;
 };
-static_assert(sizeof(Chunk) == 768, "Chunk layout");
+static_assert(sizeof(Node) == 32, "Node layout");
+
+struct ChunkHdr {
+  uint32_t next;     // next chunk of the FIFO or NIL
+  uint32_t pad;
+  int64_t price;     // level price (Q3 check on cancel)
+};
 
 struct Book {
   uint32_t lvl_base, n_lvl, lvl_cap, pad;
@@ -89,7 +94,8 @@ struct Dev {
   Level* lvl;
   uint32_t lvl_cap_total;
   uint32_t* lvl_bump;
-  Chunk* ch;
+  Node* nodes;         // chunk c, slot s -> nodes[c * CH + s]
+  ChunkHdr* chdr;
   uint32_t ch_cap;
   uint32_t* ch_bump;
   uint32_t* free_ids;

@@ -1,0 +1,604 @@
+// match_cold.h — match_books for cold books: one wavefront per book, book state in HBM.
+// Also the HBM path a hot book falls back to when it outgrows the LDS level array.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "../../include/gome/gome_abi.h"
+#include "device.h"
+#include "pipeline.h"
+#include "wave.h"
+
+namespace gome {
+
+// ============================================================== match_books
+struct BatchArgs {
+  const Prep* prep;           // segment-ordered records
+  const gome_order* ord;
+  uint32_t n;
+  const uint32_t* seg_start;  // [nseg + 1]
+  const uint32_t* seg_order;  // launch order (longest first; the first nhot are hot books)
+  gome_event* arena;          // per-wave event blocks, compacted afterwards
+  uint32_t arena_cap;
+  uint32_t* ev_count;         // events per batch index
+};
+
+constexpr uint32_t EVB = 32;      // events per arena block (cold books)
+constexpr uint32_t EVB_HOT = 256; // events per arena block (hot books)
+
+// Wave-uniform context of the book being matched.
+struct WaveCtx {
+  Dev D;
+  BatchArgs B;
+  uint32_t sym;
+  Level* L;          // the book's sorted level array (HBM)
+  uint32_t nl, cap, base;
+  uint32_t ev_base, ev_used, evb;
+  bool ev_ok, fatal;
+  unsigned long long fills, cancels, rests, dropped, adds, dels;
+  long long resting_delta, levels_delta;
+};
+
+__device__ __forceinline__ void set_err(WaveCtx& W, uint32_t e) {
+  if (lane_id() == 0) atomicOr(&W.D.st->err, e);
+  W.fatal = true;
+}
+
+// Mark the unused tail of the current event block invalid (taker_seq = NIL).
+__device__ __forceinline__ void ev_close(WaveCtx& W) {
+  if (W.ev_base == NIL || !W.ev_ok) return;
+  for (uint32_t j = W.ev_used + lane_id(); j < W.evb; j += 64) W.B.arena[W.ev_base + j].taker_seq = NIL;
+}
+
+__device__ __forceinline__ void ev_make_room(WaveCtx& W, uint32_t k) {
+  if (W.ev_base != NIL && W.ev_used + k <= W.evb) return;
+  const uint32_t lane = lane_id();
+  ev_close(W);
+  uint32_t b = 0;
+  if (lane == 0) b = atomicAdd(&W.D.st->ev_bump, W.evb);
+  b = uni(b);
+  if (b + W.evb > W.B.arena_cap) {
+    W.ev_ok = false;
+    if (lane == 0) atomicOr(&W.D.st->err, ERR_EVENTS);
+  }
+  W.ev_base = b;
+  W.ev_used = 0;
+}
+
+__device__ __forceinline__ uint32_t alloc_chunk(WaveCtx& W) {
+  uint32_t c = 0;
+  if (lane_id() == 0) {
+    int t = atomicSub(&W.D.st->free_top, 1);
+    c = (t > 0) ? W.D.free_ids[t - 1] : atomicAdd(W.D.ch_bump, 1u);
+  }
+  c = uni(c);
+  if (c >= W.D.ch_cap) { set_err(W, ERR_CHUNKS); return NIL; }
+  return c;
+}
+
+__device__ __forceinline__ void free_chunk(WaveCtx& W, uint32_t c) {
+  if (lane_id() == 0) W.D.freed_ids[atomicAdd(&W.D.st->freed_top, 1u)] = c;
+}
+
+__device__ __forceinline__ void free_chain(WaveCtx& W, uint32_t head, uint32_t tail) {
+  uint32_t c = head;
+  for (uint32_t guard = 0; c != NIL; ++guard) {
+    if (guard > W.D.ch_cap) { set_err(W, ERR_CORRUPT); return; }
+    uint32_t nx = (c == tail) ? NIL : uni(W.D.chdr[c].next);
+    free_chunk(W, c);
+    c = nx;
+  }
+}
+
+// ---- level array (sorted by price) --------------------------
+// Lower bound of p with a 64-ary wave search; returns true iff L[pos].price == p.
+__device__ __forceinline__ bool level_search_in(const Level* L, uint32_t nl, int64_t p, uint32_t& pos) {
+  const uint32_t lane = lane_id();
+  uint32_t lo = 0, hi = nl;
+  while (hi - lo > 64) {
+    uint32_t step = (hi - lo + 63) / 64;
+    uint32_t q = lo + lane * step;
+    bool v = q < hi;
+    int64_t pr = v ? L[q].price : 0;
+    uint32_t ns = __popcll(__ballot(v));
+    uint32_t cnt = __popcll(__ballot(v && pr < p));
+    uint32_t nlo = cnt ? lo + (cnt - 1) * step + 1 : lo;
+    uint32_t nhi = (cnt < ns) ? lo + cnt * step + 1 : hi;
+    lo = nlo;
+    hi = nhi;
+  }
+  uint32_t q = lo + lane;
+  bool v = q < hi;
+  int64_t pr = v ? L[q].price : 0;
+  pos = lo + __popcll(__ballot(v && pr < p));
+  return __ballot(v && pr == p) != 0;
+}
+
+__device__ __forceinline__ bool level_search(const WaveCtx& W, int64_t p, uint32_t& pos) {
+  return level_search_in(W.L, W.nl, p, pos);
+}
+
+// Drop levels with no observable state (no nodes, zero depth, no side membership);
+// equivalent to a never-touched price in the Redis schema.
+__device__ __forceinline__ void level_gc(WaveCtx& W) {
+  const uint32_t lane = lane_id();
+  const unsigned long long ltm = lt_mask();
+  uint32_t out = 0;
+  for (uint32_t w0 = 0; w0 < W.nl; w0 += 64) {
+    uint32_t k = w0 + lane;
+    bool keep = false;
+    Level x{};
+    if (k < W.nl) {
+      x = W.L[k];
+      keep = x.nlive != 0 || x.depth != 0 || x.member != 0;
+    }
+    unsigned long long m = __ballot(keep);
+    if (keep) W.L[out + __popcll(m & ltm)] = x;
+    out += __popcll(m);
+  }
+  W.levels_delta -= static_cast<long long>(W.nl - out);
+  W.nl = out;
+}
+
+__device__ __forceinline__ bool level_grow(WaveCtx& W) {
+  const uint32_t lane = lane_id();
+  uint32_t ncap = W.cap ? W.cap * 2 : 16;
+  uint32_t nb = 0;
+  if (lane == 0) nb = atomicAdd(W.D.lvl_bump, ncap);
+  nb = uni(nb);
+  if (static_cast<unsigned long long>(nb) + ncap > W.D.lvl_cap_total) {
+    set_err(W, ERR_LEVELS);
+    return false;
+  }
+  Level* NL = W.D.lvl + nb;
+  for (uint32_t w0 = 0; w0 < W.nl; w0 += 64) {
+    uint32_t k = w0 + lane;
+    if (k < W.nl) NL[k] = W.L[k];
+  }
+  W.L = NL;
+  W.cap = ncap;
+  W.base = nb;
+  return true;
+}
+
+// Insert an empty level for price p at lower-bound position pos (updated on GC).
+__device__ __forceinline__ bool level_insert(WaveCtx& W, int64_t p, uint32_t& pos) {
+  const uint32_t lane = lane_id();
+  if (W.nl == W.cap) {
+    if (W.nl) {
+      level_gc(W);
+      level_search(W, p, pos);
+    }
+    if (W.nl == W.cap && !level_grow(W)) return false;
+  }
+  for (int32_t top = static_cast<int32_t>(W.nl); top > static_cast<int32_t>(pos); top -= 64) {
+    int32_t lo = max(top - 64, static_cast<int32_t>(pos));
+    int32_t k = lo + static_cast<int32_t>(lane);
+    if (k < top) {
+      Level x = W.L[k];
+      W.L[k + 1] = x;
+    }
+  }
+  if (lane == 0) {
+    Level z{};
+    z.price = p;
+    z.head = z.tail = NIL;
+    W.L[pos] = z;
+  }
+  W.nl++;
+  W.levels_delta++;
+  return true;
+}
+
+// ---- (S, oid) -> node index (stands in for HGET S:link:<p> S:node:<oid>) -------
+__device__ __forceinline__ unsigned long long idx_key(uint32_t sym, uint32_t oid) {
+  return (static_cast<unsigned long long>(sym + 1) << 32) | oid;
+}
+
+__device__ __forceinline__ uint32_t idx_insert(WaveCtx& W, uint32_t oid, uint32_t loc) {
+  const uint32_t lane = lane_id();
+  const unsigned long long key = idx_key(W.sym, oid), mask = W.D.idx_mask;
+  unsigned long long h = mix64(key) & mask;
+  for (unsigned long long probe = 0; probe <= mask; probe += 64) {
+    const unsigned long long slot = (h + lane) & mask;
+    unsigned long long kv =
+        __hip_atomic_load(&W.D.idx[slot].key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned long long cand = __ballot(kv == KEY_EMPTY || kv == KEY_TOMB);
+    while (cand) {
+      uint32_t b = __builtin_ctzll(cand);
+      bool ok = false;
+      if (lane == b) {
+        unsigned long long exp = kv;
+        ok = atomicCAS(&W.D.idx[slot].key, exp, key) == exp;
+        if (ok) W.D.idx[slot].loc = loc;
+      }
+      if (__ballot(ok)) return static_cast<uint32_t>((h + b) & mask);
+      cand &= cand - 1;
+    }
+    h = (h + 64) & mask;
+  }
+  set_err(W, ERR_INDEX);
+  return NIL;
+}
+
+__device__ __forceinline__ bool idx_lookup(const WaveCtx& W, uint32_t oid, uint32_t& ixslot, uint32_t& loc) {
+  const uint32_t lane = lane_id();
+  const unsigned long long key = idx_key(W.sym, oid), mask = W.D.idx_mask;
+  unsigned long long h = mix64(key) & mask;
+  for (unsigned long long probe = 0; probe <= mask; probe += 64) {
+    const unsigned long long slot = (h + lane) & mask;
+    unsigned long long kv =
+        __hip_atomic_load(&W.D.idx[slot].key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned long long hit = __ballot(kv == key), emp = __ballot(kv == KEY_EMPTY);
+    unsigned long long any = hit | emp;
+    if (any) {
+      uint32_t b = __builtin_ctzll(any);
+      if (!((hit >> b) & 1ull)) return false;
+      uint32_t lc = (lane == b) ? W.D.idx[slot].loc : 0;
+      loc = __shfl(lc, b);
+      ixslot = static_cast<uint32_t>((h + b) & mask);
+      return true;
+    }
+    h = (h + 64) & mask;
+  }
+  return false;
+}
+
+__device__ __forceinline__ void idx_erase(WaveCtx& W, uint32_t ixslot) {
+  __hip_atomic_store(&W.D.idx[ixslot].key, KEY_TOMB, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// ---- MatchOrder at one level (engine.go:138-198) --------------------------------
+// Consumes the FIFO head of level k for a taker with remaining T.  Lanes 0..31 hold the
+// head chunk, lanes 32..63 the next chunk (for MatchNode.NextNode).  Per chunk, a prefix
+// scan over live volumes decides which makers are reached (reference recursion continues
+// while diff > 0), fully filled (diff >= 0) or partially filled (diff < 0).
+__device__ __forceinline__ int64_t match_level(WaveCtx& W, uint32_t k, int64_t T, uint32_t seq, uint32_t& fidx) {
+  const uint32_t lane = lane_id(), s = lane & 31u;
+  const bool hi = lane >= 32;
+  Level lv = W.L[k];
+  bool first = true;
+  for (uint32_t guard = 0; lv.head != NIL && !W.fatal; ++guard) {
+    if (guard > W.D.ch_cap) { set_err(W, ERR_CORRUPT); break; }
+    const uint32_t head = lv.head;
+    const uint32_t nxt = uni(W.D.chdr[head].next);
+    const uint32_t cid = hi ? nxt : head;
+    int64_t r = -1;
+    uint32_t o = 0, u = 0, ix = 0, t = 0;
+    bool inr = false;
+    if (cid != NIL) {
+      uint32_t lim = (cid == lv.tail) ? lv.tslot : CH;
+      uint32_t lo = hi ? 0u : lv.hslot;
+      inr = s >= lo && s < lim;
+    }
+    if (inr) {
+      const Node nd = W.D.nodes[cid * CH + s];
+      r = nd.rem;
+      o = nd.oid;
+      u = nd.uuid;
+      ix = nd.ixs;
+      t = nd.tx;
+    }
+    const bool live = inr && r >= 0;
+    const unsigned long long lm = __ballot(live);
+    const uint32_t mlo = static_cast<uint32_t>(lm), mhi = static_cast<uint32_t>(lm >> 32);
+    if (mlo == 0) {  // head chunk exhausted (consumed/cancelled slots only)
+      if (head == lv.tail) { set_err(W, ERR_CORRUPT); break; }
+      free_chunk(W, head);
+      lv.head = nxt;
+      lv.hslot = 0;
+      continue;
+    }
+    const int64_t x = (!hi && live) ? r : 0;
+    const int64_t incl = wave_incl_scan(x);
+    const int64_t excl = incl - x;
+    const uint32_t fl = __builtin_ctz(mlo);
+    const bool arr = !hi && live && (excl < T || (first && T == 0 && s == fl));
+    const bool pop = arr && incl <= T;
+    const int64_t f = pop ? r : (T - excl);
+    const unsigned long long am = __ballot(arr), pm = __ballot(pop);
+    const uint32_t narr = __popcll(am), npop = __popcll(pm);
+    const uint32_t la = 63 - __builtin_clzll(am);
+    // MatchNode.NextNode / IsLast: next live node after s in FIFO order.
+    const uint32_t after = (s < 31) ? (mlo & (~0u << (s + 1))) : 0u;
+    int src = after ? static_cast<int>(__builtin_ctz(after))
+                    : (mhi ? 32 + static_cast<int>(__builtin_ctz(mhi)) : -1);
+    uint32_t nx_oid = __shfl(o, src < 0 ? 0 : src);
+    bool is_last = src < 0;
+    const uint32_t ll = 31 - __clz(mlo);  // last live slot of the head chunk
+    if (!mhi && nxt != NIL && ((am >> ll) & 1ull)) {
+      // next chunk is all tombstones: search further down the chain
+      uint32_t c2 = uni(W.D.chdr[nxt].next);
+      for (uint32_t guard = 0; c2 != NIL && guard <= W.D.ch_cap; ++guard) {
+        uint32_t lim = (c2 == lv.tail) ? lv.tslot : CH;
+        bool l2 = lane < lim && W.D.nodes[c2 * CH + (lane < CH ? lane : 0)].rem >= 0;
+        unsigned long long m2 = __ballot(l2);
+        if (m2) {
+          uint32_t b = __builtin_ctzll(m2);
+          uint32_t oo = W.D.nodes[c2 * CH + b].oid;
+          if (lane == ll) { nx_oid = oo; is_last = false; }
+          break;
+        }
+        c2 = (c2 == lv.tail) ? NIL : uni(W.D.chdr[c2].next);
+      }
+    }
+    const int64_t tafter = T - excl - f;
+    const int64_t dafter = lv.depth - excl - f;
+    const bool clr = arr && dafter <= 0;  // DeletePoolDepth: ZREM maker's side (nodepool.go:76-83)
+    const unsigned long long clr_s = __ballot(clr && t == GOME_SALE), clr_b = __ballot(clr && t != GOME_SALE);
+    // publish (engine.go:154,171,190)
+    ev_make_room(W, narr);
+    if (arr && W.ev_ok) {
+      uint32_t rank = __popcll(am & lt_mask());
+      gome_event e;
+      e.price_fx = lv.price;
+      e.match_volume_fx = f;
+      e.maker_volume_fx = pop ? r : r - f;
+      e.taker_volume_fx = tafter;
+      e.taker_seq = seq;
+      e.fill_idx = fidx + rank;
+      e.symbol_id = W.sym;
+      e.maker_oid_id = o;
+      e.maker_uuid_id = u;
+      e.maker_next_oid_id = is_last ? 0u : nx_oid;
+      e.kind = GOME_EV_FILL;
+      e.maker_side = static_cast<uint8_t>(t);
+      e.maker_is_last = is_last ? 1 : 0;
+      e.pad0 = 0;
+      e.pad1 = 0;
+      W.B.arena[W.ev_base + W.ev_used + rank] = e;
+    }
+    W.ev_used += narr;
+    fidx += narr;
+    W.fills += narr;
+    const int64_t Tn = rl64(tafter, la);
+    lv.depth -= (T - Tn);
+    if (clr_s) lv.member &= static_cast<uint8_t>(~M_SALE);
+    if (clr_b) lv.member &= static_cast<uint8_t>(~M_BUY);
+    if (pop) idx_erase(W, ix);
+    lv.nlive -= npop;
+    W.resting_delta -= npop;
+    first = false;
+    if (!((pm >> la) & 1ull)) {  // partial fill of maker la: it keeps its FIFO position
+      if (lane == la) W.D.nodes[head * CH + s].rem = r - f;
+      lv.hslot = static_cast<uint8_t>(la);
+      T = 0;
+      break;
+    }
+    T = Tn;
+    lv.hslot = static_cast<uint8_t>(la + 1);
+    if (lv.nlive == 0) {
+      free_chain(W, lv.head, lv.tail);
+      lv.head = lv.tail = NIL;
+      lv.hslot = lv.tslot = 0;
+      break;
+    }
+    if (T <= 0) break;  // diff == 0: stop (engine.go:162-175)
+    // every live maker of the head chunk consumed, T > 0: continue down the FIFO
+    free_chunk(W, head);
+    lv.head = nxt;
+    lv.hslot = 0;
+  }
+  if (lane == 0) W.L[k] = lv;
+  return T;
+}
+
+// ---- rest the remaining volume (engine.go:80-82) ----------------------------------
+__device__ __forceinline__ void do_rest(WaveCtx& W, int64_t p, int64_t T, uint32_t oid, uint32_t uuid,
+                        uint32_t side) {
+  const uint32_t lane = lane_id();
+  uint32_t pos;
+  if (!level_search(W, p, pos) && !level_insert(W, p, pos)) return;
+  Level lv = W.L[pos];
+  lv.member |= (side == GOME_SALE) ? M_SALE : M_BUY;  // SetPoolDepth (ZADD own side)
+  lv.depth += T;                                       // SetPoolDepthVolume
+  if (lv.tail == NIL || lv.tslot == CH) {              // SetDepthLink: append at the tail
+    uint32_t c = alloc_chunk(W);
+    if (c == NIL) return;
+    if (lane == 0) {
+      W.D.chdr[c].next = NIL;
+      W.D.chdr[c].price = p;
+      if (lv.tail != NIL) W.D.chdr[lv.tail].next = c;
+    }
+    if (lv.tail == NIL) { lv.head = c; lv.hslot = 0; }
+    lv.tail = c;
+    lv.tslot = 0;
+  }
+  const uint32_t slot = lv.tslot, loc = lv.tail * CH + slot;
+  const uint32_t ix = idx_insert(W, oid, loc);
+  if (lane == 0) {
+    Node nd{};
+    nd.rem = T;
+    nd.oid = oid;
+    nd.uuid = uuid;
+    nd.ixs = ix;
+    nd.tx = static_cast<uint8_t>(side);
+    W.D.nodes[lv.tail * CH + slot] = nd;
+  }
+  lv.tslot = static_cast<uint8_t>(slot + 1);
+  lv.nlive++;
+  if (lane == 0) W.L[pos] = lv;
+  W.rests++;
+  W.resting_delta++;
+}
+
+// ---- SetOrder (engine.go:56-85) -------------------------------------------------
+__device__ __forceinline__ uint32_t do_add(WaveCtx& W, int64_t p, int64_t vol, uint32_t oid, uint32_t uuid,
+                           uint32_t side, uint32_t seq) {
+  const uint32_t lane = lane_id();
+  const bool sale = side == GOME_SALE;
+  const uint8_t opp = sale ? M_BUY : M_SALE;
+  int64_t T = vol;
+  bool crossed = false;
+  uint32_t fidx = 0;
+  // GetReverseDepth (nodepool.go:86-115): opposite-side levels crossing p, best first.
+  if (!sale) {
+    for (uint32_t w0 = 0; w0 < W.nl && !W.fatal; w0 += 64) {
+      const uint32_t k = w0 + lane;
+      const bool v = k < W.nl;
+      int64_t lp = 0;
+      uint8_t mem = 0;
+      if (v) { lp = W.L[k].price; mem = W.L[k].member; }
+      unsigned long long cm = __ballot(v && (mem & opp) && lp <= p);
+      const bool beyond = __ballot(v && lp > p) != 0;
+      while (cm && !W.fatal) {
+        const uint32_t kk = w0 + __builtin_ctzll(cm);
+        cm &= cm - 1;
+        crossed = true;
+        T = match_level(W, kk, T, seq, fidx);  // Match (engine.go:118-136)
+        if (T <= 0) goto matched;
+      }
+      if (beyond) break;
+    }
+  } else {
+    for (int32_t top = static_cast<int32_t>(W.nl); top > 0 && !W.fatal; top -= 64) {
+      const int32_t lo = top - 64, k = lo + static_cast<int32_t>(lane);
+      const bool v = k >= 0;
+      int64_t lp = 0;
+      uint8_t mem = 0;
+      if (v) { lp = W.L[k].price; mem = W.L[k].member; }
+      unsigned long long cm = __ballot(v && (mem & opp) && lp >= p);
+      const bool beyond = __ballot(v && lp < p) != 0;
+      while (cm && !W.fatal) {
+        const uint32_t b = 63 - __builtin_clzll(cm);
+        cm &= ~(1ull << b);
+        crossed = true;
+        T = match_level(W, static_cast<uint32_t>(lo + static_cast<int32_t>(b)), T, seq, fidx);
+        if (T <= 0) goto matched;
+      }
+      if (beyond) break;
+    }
+  }
+matched:
+  if ((!crossed || T > 0) && !W.fatal) do_rest(W, p, T, oid, uuid, side);
+  return fidx;
+}
+
+// ---- DeleteOrder (engine.go:87-116) ---------------------------------------------
+__device__ __forceinline__ uint32_t do_cancel(WaveCtx& W, int64_t p, uint32_t oid, uint32_t uuid, uint32_t side,
+                              uint32_t seq) {
+  const uint32_t lane = lane_id();
+  uint32_t ixslot, loc;
+  if (!idx_lookup(W, oid, ixslot, loc)) return 0;    // not in any FIFO: no event
+  const uint32_t cid = loc / CH, s = loc % CH;
+  if (uni(static_cast<uint32_t>(W.D.chdr[cid].price != p))) return 0;  // wrong price (Q3)
+  const int64_t r = rl64(W.D.nodes[cid * CH + s].rem, 0);
+  uint32_t pos;
+  if (r < 0 || !level_search(W, p, pos)) { set_err(W, ERR_CORRUPT); return 0; }
+  Level lv = W.L[pos];
+  lv.depth -= r;  // DeletePoolDepthVolume with the stored remaining volume
+  if (lv.depth <= 0) lv.member &= static_cast<uint8_t>(~((side == GOME_SALE) ? M_SALE : M_BUY));
+  if (lane == 0) W.D.nodes[cid * CH + s].rem = -1;
+  if (lane == 0) idx_erase(W, ixslot);
+  lv.nlive--;
+  W.resting_delta--;
+  if (lv.nlive == 0) {
+    free_chain(W, lv.head, lv.tail);
+    lv.head = lv.tail = NIL;
+    lv.hslot = lv.tslot = 0;
+  }
+  if (lane == 0) W.L[pos] = lv;
+  ev_make_room(W, 1);
+  if (lane == 0 && W.ev_ok) {
+    gome_event e;
+    e.price_fx = p;
+    e.match_volume_fx = 0;
+    e.maker_volume_fx = r;
+    e.taker_volume_fx = r;
+    e.taker_seq = seq;
+    e.fill_idx = 0;
+    e.symbol_id = W.sym;
+    e.maker_oid_id = oid;
+    e.maker_uuid_id = uuid;
+    e.maker_next_oid_id = 0;
+    e.kind = GOME_EV_CANCEL;
+    e.maker_side = static_cast<uint8_t>(side);
+    e.maker_is_last = 1;
+    e.pad0 = 0;
+    e.pad1 = 0;
+    W.B.arena[W.ev_base + W.ev_used] = e;
+  }
+  W.ev_used += 1;
+  W.cancels++;
+  return 1;
+}
+
+// Apply orders [b0, end) of the book in W (HBM-resident level array).
+__device__ __forceinline__ void process_global(WaveCtx& W, uint32_t b0, uint32_t end) {
+  const uint32_t lane = lane_id();
+  for (; b0 < end && !W.fatal; b0 += 64) {
+    const uint32_t cnt = min(64u, end - b0);
+    Prep q{};
+    if (lane < cnt) q = W.B.prep[b0 + lane];  // 64 records of this book, one per lane
+    for (uint32_t j = 0; j < cnt && !W.fatal; ++j) {
+      const uint32_t idx = rl(q.idx, j), a = rl(q.action, j);
+      uint32_t nev = 0;
+      if (a == GOME_ADD) {
+        W.adds++;
+        if (rl(q.adm, j)) {
+          nev = do_add(W, rl64(q.price, j), rl64(q.vol, j), rl(q.oid, j), rl(q.uuid, j), rl(q.side, j), idx);
+        } else {
+          W.dropped++;  // marker already consumed (engine.go:58-60)
+        }
+      } else if (a == GOME_DEL) {
+        W.dels++;
+        nev = do_cancel(W, rl64(q.price, j), rl(q.oid, j), rl(q.uuid, j), rl(q.side, j), idx);
+      }
+      if (lane == 0) W.B.ev_count[idx] = nev;
+    }
+  }
+}
+
+__device__ __forceinline__ void wave_finish(WaveCtx& W) {
+  const uint32_t lane = lane_id();
+  ev_close(W);
+  if (lane == 0) {
+    Book nb;
+    nb.lvl_base = W.base;
+    nb.n_lvl = W.nl;
+    nb.lvl_cap = W.cap;
+    nb.pad = 0;
+    W.D.books[W.sym] = nb;
+    unsigned long long* c = W.D.st->ctr;
+    if (W.fills) atomicAdd(&c[C_FILLS], W.fills);
+    if (W.cancels) atomicAdd(&c[C_CANCELS], W.cancels);
+    if (W.rests) atomicAdd(&c[C_RESTS], W.rests);
+    if (W.dropped) atomicAdd(&c[C_DROPPED], W.dropped);
+    if (W.adds) atomicAdd(&c[C_ADD], W.adds);
+    if (W.dels) atomicAdd(&c[C_DEL], W.dels);
+    if (W.resting_delta) atomicAdd(&c[C_RESTING_DELTA], static_cast<unsigned long long>(W.resting_delta));
+    if (W.levels_delta) atomicAdd(&c[C_LEVELS_DELTA], static_cast<unsigned long long>(W.levels_delta));
+  }
+}
+
+__device__ __forceinline__ void wave_init(WaveCtx& W, const Dev& D, const BatchArgs& B, uint32_t sym, uint32_t evb) {
+  W.D = D;
+  W.B = B;
+  W.sym = sym;
+  const Book bk = D.books[sym];
+  W.base = uni(bk.lvl_base);
+  W.nl = uni(bk.n_lvl);
+  W.cap = uni(bk.lvl_cap);
+  W.L = D.lvl + W.base;
+  W.ev_base = NIL;
+  W.ev_used = 0;
+  W.evb = evb;
+  W.ev_ok = true;
+  W.fatal = false;
+  W.fills = W.cancels = W.rests = W.dropped = W.adds = W.dels = 0;
+  W.resting_delta = W.levels_delta = 0;
+}
+
+// Cold books: one 64-thread workgroup (one wavefront) per book, state in HBM.
+__global__ __launch_bounds__(64) void k_match(Dev D, BatchArgs B) {
+  const uint32_t nhot = D.st->nhot;
+  if (blockIdx.x + nhot >= D.st->nseg || (D.st->err & ERR_INPUT)) return;
+  const uint32_t seg = B.seg_order[nhot + blockIdx.x];
+  const uint32_t beg = B.seg_start[seg], end = B.seg_start[seg + 1];
+  WaveCtx W;
+  wave_init(W, D, B, uni(B.ord[B.prep[beg].idx].symbol_id), EVB);
+  process_global(W, beg, end);
+  wave_finish(W);
+}
+
+
+}  // namespace gome

@@ -1,0 +1,298 @@
+// pipeline.h — batch-preparation kernels: exclusive scan, stable LSD radix sort by symbol,
+// validation, per-symbol segments (longest first), admission markers, prepared records.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "../../include/gome/gome_abi.h"
+#include "device.h"
+#include "wave.h"
+
+namespace gome {
+
+// ============================================================== scan (u32, exclusive)
+constexpr int SCAN_T = 256, SCAN_IPT = 8, SCAN_TILE = SCAN_T * SCAN_IPT;
+
+// Exclusive block scan of one value per thread (256 threads); returns prefix, sets total.
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* lds4, uint32_t& total) {
+  const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
+  uint32_t inc = wave_incl_scan_u32(v);
+  if (lane == 63) lds4[w] = inc;
+  __syncthreads();
+  uint32_t off = 0;
+  for (uint32_t i = 0; i < w; ++i) off += lds4[i];
+  total = lds4[0] + lds4[1] + lds4[2] + lds4[3];
+  __syncthreads();
+  return off + inc - v;
+}
+
+__global__ __launch_bounds__(SCAN_T) void k_scan_reduce(const uint32_t* in, uint32_t m,
+                                                        uint32_t* bsum) {
+  __shared__ uint32_t lds4[4];
+  const uint32_t base = blockIdx.x * SCAN_TILE + threadIdx.x * SCAN_IPT;
+  uint32_t s = 0;
+#pragma unroll
+  for (int i = 0; i < SCAN_IPT; ++i)
+    if (base + i < m) s += in[base + i];
+  uint32_t tot;
+  block_excl_scan(s, lds4, tot);
+  if (threadIdx.x == 0) bsum[blockIdx.x] = tot;
+}
+
+__global__ __launch_bounds__(SCAN_T) void k_scan_spine(uint32_t* bsum, uint32_t nb,
+                                                       uint32_t* total) {
+  __shared__ uint32_t lds4[4];
+  uint32_t carry = 0;
+  for (uint32_t c0 = 0; c0 < nb; c0 += SCAN_TILE) {
+    const uint32_t base = c0 + threadIdx.x * SCAN_IPT;
+    uint32_t v[SCAN_IPT], s = 0;
+#pragma unroll
+    for (int i = 0; i < SCAN_IPT; ++i) {
+      v[i] = (base + i < nb) ? bsum[base + i] : 0;
+      s += v[i];
+    }
+    uint32_t tot;
+    uint32_t pre = block_excl_scan(s, lds4, tot) + carry;
+#pragma unroll
+    for (int i = 0; i < SCAN_IPT; ++i)
+      if (base + i < nb) { bsum[base + i] = pre; pre += v[i]; }
+    carry += tot;
+  }
+  if (threadIdx.x == 0 && total) *total = carry;
+}
+
+__global__ __launch_bounds__(SCAN_T) void k_scan_down(const uint32_t* in, uint32_t m,
+                                                      const uint32_t* bsum, uint32_t* out) {
+  __shared__ uint32_t lds4[4];
+  const uint32_t base = blockIdx.x * SCAN_TILE + threadIdx.x * SCAN_IPT;
+  uint32_t v[SCAN_IPT], s = 0;
+#pragma unroll
+  for (int i = 0; i < SCAN_IPT; ++i) {
+    v[i] = (base + i < m) ? in[base + i] : 0;
+    s += v[i];
+  }
+  uint32_t tot;
+  uint32_t pre = block_excl_scan(s, lds4, tot) + bsum[blockIdx.x];
+#pragma unroll
+  for (int i = 0; i < SCAN_IPT; ++i)
+    if (base + i < m) { out[base + i] = pre; pre += v[i]; }
+}
+
+// ============================================================== radix sort by symbol
+constexpr int RS_T = 256, RS_IPT = 8, RS_TILE = RS_T * RS_IPT, RS_MAXBITS = 11;
+constexpr int RS_WAVE_ITEMS = RS_TILE / 4;  // contiguous items per wave
+
+template <bool FROM_ORD>
+__device__ __forceinline__ uint32_t rs_key(const gome_order* ord, const uint32_t* keys, uint32_t i) {
+  return FROM_ORD ? ord[i].symbol_id : keys[i];
+}
+
+template <bool FROM_ORD>
+__global__ __launch_bounds__(RS_T) void k_radix_hist(const gome_order* ord, const uint32_t* keys,
+                                                     uint32_t n, uint32_t shift, uint32_t bits,
+                                                     uint32_t* hist, uint32_t nblk) {
+  __shared__ uint32_t h[1 << RS_MAXBITS];
+  const uint32_t nb = 1u << bits, mask = nb - 1;
+  for (uint32_t i = threadIdx.x; i < nb; i += RS_T) h[i] = 0;
+  __syncthreads();
+  const uint32_t tile = blockIdx.x * RS_TILE;
+#pragma unroll
+  for (int it = 0; it < RS_IPT; ++it) {
+    uint32_t i = tile + it * RS_T + threadIdx.x;
+    if (i < n) atomicAdd(&h[(rs_key<FROM_ORD>(ord, keys, i) >> shift) & mask], 1u);
+  }
+  __syncthreads();
+  for (uint32_t d = threadIdx.x; d < nb; d += RS_T) hist[d * nblk + blockIdx.x] = h[d];
+}
+
+// Stable scatter: wave w of the block owns items [w*512, (w+1)*512) of the tile and ranks
+// them in rounds of 64 with a ballot-based match of equal digits (multi-split).
+template <bool FROM_ORD>
+__global__ __launch_bounds__(RS_T) void k_radix_scatter(const gome_order* ord,
+                                                        const uint32_t* keys_in,
+                                                        const uint32_t* vals_in, uint32_t n,
+                                                        uint32_t shift, uint32_t bits,
+                                                        const uint32_t* hist_scanned,
+                                                        uint32_t* keys_out, uint32_t* vals_out,
+                                                        uint32_t nblk) {
+  __shared__ uint32_t cnt[4][1 << RS_MAXBITS];
+  const uint32_t nb = 1u << bits, mask = nb - 1;
+  const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
+  for (uint32_t i = threadIdx.x; i < 4 * nb; i += RS_T) cnt[i / nb][i % nb] = 0;
+  __syncthreads();
+  const uint32_t base = blockIdx.x * RS_TILE + w * RS_WAVE_ITEMS;
+  uint32_t kk[RS_WAVE_ITEMS / 64], vv[RS_WAVE_ITEMS / 64], off[RS_WAVE_ITEMS / 64];
+  const unsigned long long ltm = lt_mask();
+#pragma unroll
+  for (int r = 0; r < RS_WAVE_ITEMS / 64; ++r) {
+    const uint32_t i = base + r * 64 + lane;
+    const bool valid = i < n;
+    uint32_t k = valid ? rs_key<FROM_ORD>(ord, keys_in, i) : 0;
+    uint32_t v = valid ? (FROM_ORD ? i : vals_in[i]) : 0;
+    uint32_t d = (k >> shift) & mask;
+    unsigned long long m = __ballot(valid);
+    for (uint32_t b = 0; b < bits; ++b) {
+      unsigned long long bb = __ballot((d >> b) & 1u);
+      m &= ((d >> b) & 1u) ? bb : ~bb;
+    }
+    uint32_t rank = __popcll(m & ltm);
+    uint32_t c = valid ? cnt[w][d] : 0;
+    off[r] = c + rank;
+    if (valid && rank == 0) cnt[w][d] = c + __popcll(m);
+    kk[r] = k;
+    vv[r] = v;
+  }
+  __syncthreads();
+  for (uint32_t d = threadIdx.x; d < nb; d += RS_T) {
+    uint32_t run = hist_scanned[d * nblk + blockIdx.x];
+    for (int ww = 0; ww < 4; ++ww) {
+      uint32_t t = cnt[ww][d];
+      cnt[ww][d] = run;
+      run += t;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < RS_WAVE_ITEMS / 64; ++r) {
+    const uint32_t i = base + r * 64 + lane;
+    if (i < n) {
+      uint32_t pos = cnt[w][(kk[r] >> shift) & mask] + off[r];
+      keys_out[pos] = kk[r];
+      vals_out[pos] = vv[r];
+    }
+  }
+}
+
+// ============================================================== validation
+__global__ void k_validate(const gome_order* ord, uint32_t n, uint32_t max_symbols, Status* st) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const gome_order o = ord[i];
+  const int64_t lim = 1ll << 53;
+  bool bad = o.symbol_id >= max_symbols || o.volume_fx < 0 || o.volume_fx >= lim ||
+             o.price_fx <= -lim || o.price_fx >= lim;
+  if (bad) atomicOr(&st->err, ERR_INPUT);
+}
+
+// ============================================================== segments
+__global__ void k_seg_flags(const uint32_t* skeys, uint32_t n, uint32_t* flags) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) flags[i] = (i == 0 || skeys[i] != skeys[i - 1]) ? 1u : 0u;
+}
+
+__global__ void k_seg_write(const uint32_t* skeys, uint32_t n, const uint32_t* segpos,
+                            uint32_t* seg_start, const Status* st) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n && (i == 0 || skeys[i] != skeys[i - 1])) seg_start[segpos[i]] = i;
+  if (i == 0) seg_start[st->nseg] = n;
+}
+
+// Longest-first launch order by floor(log2(len)) buckets (hot books start first).
+__global__ void k_seg_count(const uint32_t* seg_start, const Status* st, uint32_t* bcnt,
+                            unsigned long long* maxseg) {
+  __shared__ uint32_t h[32];
+  __shared__ uint32_t mx;
+  if (threadIdx.x < 32) h[threadIdx.x] = 0;
+  if (threadIdx.x == 0) mx = 0;
+  __syncthreads();
+  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s < st->nseg) {
+    uint32_t len = seg_start[s + 1] - seg_start[s];
+    atomicAdd(&h[31 - __clz(len)], 1u);
+    atomicMax(&mx, len);
+  }
+  __syncthreads();
+  if (threadIdx.x < 32 && h[threadIdx.x]) atomicAdd(&bcnt[threadIdx.x], h[threadIdx.x]);
+  if (threadIdx.x == 0 && mx) atomicMax(maxseg, (unsigned long long)mx);
+}
+
+__global__ void k_seg_bscan(uint32_t* bcnt, uint32_t* boff, Status* st, uint32_t hot_log2,
+                            uint32_t max_hot) {
+  if (threadIdx.x == 0) {
+    uint32_t off = 0, hot = 0;
+    for (int b = 31; b >= 0; --b) {
+      boff[b] = off;
+      off += bcnt[b];
+      if (static_cast<uint32_t>(b) >= hot_log2) hot += bcnt[b];
+    }
+    st->nhot = min(hot, max_hot);
+  }
+}
+
+// Block-aggregated bucket scatter (one global atomic per bucket per block).
+__global__ void k_seg_scatter(const uint32_t* seg_start, const Status* st, uint32_t* boff,
+                              uint32_t* seg_order) {
+  __shared__ uint32_t cnt[32], base[32];
+  if (threadIdx.x < 32) cnt[threadIdx.x] = 0;
+  __syncthreads();
+  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t b = 0, local = 0;
+  const bool v = s < st->nseg;
+  if (v) {
+    b = 31 - __clz(seg_start[s + 1] - seg_start[s]);
+    local = atomicAdd(&cnt[b], 1u);
+  }
+  __syncthreads();
+  if (threadIdx.x < 32 && cnt[threadIdx.x]) base[threadIdx.x] = atomicAdd(&boff[threadIdx.x], cnt[threadIdx.x]);
+  __syncthreads();
+  if (v) seg_order[base[b] + local] = s;
+}
+
+// ============================================================== admission (Q4)
+// Markers S:comparison[S:uuid:oid] are set at gRPC time for every ADD of the batch
+// (main.go:44-45) and tested+cleared at consume time (engine.go:58-62,90).  Under the
+// batch ingress model an ADD is admitted iff no earlier ADD/DEL of the batch carries
+// the same (S, uuid, oid).  claim[] holds the first claimant (seq+1) of a key's slot;
+// amin[] the smallest seq of the key.
+__global__ void k_adm(const gome_order* ord, uint32_t n, uint32_t* claim, uint32_t* amin,
+                      uint32_t* slot, uint32_t mask) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const gome_order g = ord[i];
+  if (g.action != GOME_ADD && g.action != GOME_DEL) { slot[i] = NIL; return; }
+  uint32_t h = static_cast<uint32_t>(
+      mix64((static_cast<unsigned long long>(g.symbol_id) << 40) ^
+            (static_cast<unsigned long long>(g.uuid_id) << 20) ^ mix64(g.oid_id))) & mask;
+  for (uint32_t probe = 0; probe <= mask; ++probe) {
+    uint32_t c = atomicCAS(&claim[h], 0u, i + 1);
+    if (c == 0) break;
+    const gome_order q = ord[c - 1];
+    if (q.symbol_id == g.symbol_id && q.uuid_id == g.uuid_id && q.oid_id == g.oid_id) break;
+    h = (h + 1) & mask;
+  }
+  atomicMin(&amin[h], i);
+  slot[i] = h;
+}
+
+// ============================================================== prepared records
+// One 32-B record per order in segment (symbol-sorted, stable) order, admission resolved:
+// the match kernels fetch 64 orders with one coalesced load instead of a chain of
+// dependent gathers (sorted index -> record -> admission slot -> admission min).
+struct Prep {
+  int64_t price;
+  int64_t vol;
+  uint32_t oid, uuid, idx;
+  uint8_t side, action, adm, pad;
+};
+static_assert(sizeof(Prep) == 32, "Prep layout");
+
+__global__ void k_prep(const gome_order* ord, uint32_t n, const uint32_t* sidx,
+                       const uint32_t* adm_slot, const uint32_t* amin, Prep* prep) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t j = sidx[i];
+  const gome_order o = ord[j];
+  Prep q;
+  q.price = o.price_fx;
+  q.vol = o.volume_fx;
+  q.oid = o.oid_id;
+  q.uuid = o.uuid_id;
+  q.idx = j;
+  q.side = o.side;
+  q.action = o.action;
+  q.adm = (o.action == GOME_ADD && amin[adm_slot[j]] == j) ? 1 : 0;
+  q.pad = 0;
+  prep[i] = q;
+}
+
+
+}  // namespace gome

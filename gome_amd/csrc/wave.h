@@ -1,0 +1,69 @@
+// wave.h — wavefront (64-lane) primitives for gfx950.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace gome {
+
+__device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63u; }
+__device__ __forceinline__ unsigned long long lt_mask() {
+  const uint32_t l = lane_id();
+  return l ? (~0ull >> (64 - l)) : 0ull;
+}
+__device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ uint32_t rl(uint32_t v, uint32_t j) { return __builtin_amdgcn_readlane(v, j); }
+__device__ __forceinline__ int64_t rl64(int64_t v, uint32_t j) {
+  const uint32_t lo = __builtin_amdgcn_readlane(static_cast<uint32_t>(v), j);
+  const uint32_t hi = __builtin_amdgcn_readlane(static_cast<uint32_t>(static_cast<uint64_t>(v) >> 32), j);
+  return static_cast<int64_t>((static_cast<uint64_t>(hi) << 32) | lo);
+}
+__device__ __forceinline__ int64_t uni64(int64_t v) { return rl64(v, __builtin_amdgcn_readfirstlane(lane_id())); }
+
+// Inclusive scan of a 64-bit value over the whole wave (LDS-crossbar shuffles).
+__device__ __forceinline__ int64_t wave_incl_scan(int64_t x) {
+  const uint32_t lane = lane_id();
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int64_t y = __shfl_up(x, off);
+    if (lane >= static_cast<uint32_t>(off)) x += y;
+  }
+  return x;
+}
+
+__device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t x) {
+  const uint32_t lane = lane_id();
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t y = __shfl_up(x, off);
+    if (lane >= static_cast<uint32_t>(off)) x += y;
+  }
+  return x;
+}
+
+// Inclusive scan of a 64-bit value over lanes 0..31 (rows 0 and 1) with DPP row shifts
+// (VALU-latency, no LDS crossbar) and one readlane to carry row 0 into row 1.
+// Lanes 32..63 return unspecified values.
+template <int CTRL>
+__device__ __forceinline__ int64_t dpp_shr64(int64_t x) {
+  const uint32_t lo = __builtin_amdgcn_update_dpp(0u, static_cast<uint32_t>(x), CTRL, 0xF, 0xF, false);
+  const uint32_t hi = __builtin_amdgcn_update_dpp(0u, static_cast<uint32_t>(static_cast<uint64_t>(x) >> 32),
+                                                  CTRL, 0xF, 0xF, false);
+  return static_cast<int64_t>((static_cast<uint64_t>(hi) << 32) | lo);
+}
+__device__ __forceinline__ int64_t scan32_i64(int64_t x) {
+  x += dpp_shr64<0x111>(x);  // row_shr:1
+  x += dpp_shr64<0x112>(x);  // row_shr:2
+  x += dpp_shr64<0x114>(x);  // row_shr:4
+  x += dpp_shr64<0x118>(x);  // row_shr:8
+  const int64_t row0 = rl64(x, 15);
+  if (lane_id() >= 16) x += row0;
+  return x;
+}
+
+__host__ __device__ __forceinline__ unsigned long long mix64(unsigned long long x) {
+  x ^= x >> 33; x *= 0xff51afd7ed558ccdULL; x ^= x >> 33;
+  x *= 0xc4ceb9fe1a85ec53ULL; x ^= x >> 33;
+  return x;
+}
+
+}  // namespace gome

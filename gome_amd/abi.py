@@ -38,7 +38,8 @@ class Stats(C.Structure):
         "n_orders", "n_add", "n_del", "n_dropped", "n_fills", "n_cancels", "n_rests",
         "n_events", "n_resting", "n_levels", "max_segment", "n_segments")] + [
         ("ms_total", C.c_double), ("ms_match", C.c_double), ("ms_hot", C.c_double),
-        ("n_hot", C.c_uint64)]
+        ("n_hot", C.c_uint64), ("n_hot_orders", C.c_uint64), ("n_hot_fills", C.c_uint64),
+        ("n_hot_rests", C.c_uint64), ("n_hot_cancels", C.c_uint64)]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_}

@@ -73,7 +73,9 @@ enum : uint32_t {
 // counters (u64), per batch unless noted
 enum {
   C_FILLS = 0, C_CANCELS, C_RESTS, C_DROPPED, C_ADD, C_DEL, C_EVENTS,
-  C_RESTING_DELTA, C_LEVELS_DELTA, C_MAXSEG, C_NSEG, C_NCTR = 16
+  C_RESTING_DELTA, C_LEVELS_DELTA, C_MAXSEG, C_NSEG,
+  C_HOT_ORDERS, C_HOT_FILLS, C_HOT_RESTS, C_HOT_CANCELS,  // k_match_hot only
+  C_NCTR = 16
 };
 
 struct Status {

@@ -369,6 +369,10 @@ gome_status gome_engine::run(const gome_order* d_ord, uint32_t n, hipStream_t s)
   (void)hipEventElapsedTime(&ms_hot, evh0, evh1);
   stats.ms_hot = ms_hot;
   stats.n_hot = st.nhot;
+  stats.n_hot_orders = st.ctr[C_HOT_ORDERS];
+  stats.n_hot_fills = st.ctr[C_HOT_FILLS];
+  stats.n_hot_rests = st.ctr[C_HOT_RESTS];
+  stats.n_hot_cancels = st.ctr[C_HOT_CANCELS];
   stats.n_orders = n;
   stats.n_add = st.ctr[C_ADD];
   stats.n_del = st.ctr[C_DEL];

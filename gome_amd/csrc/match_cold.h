@@ -406,13 +406,9 @@ __device__ __forceinline__ void do_rest(WaveCtx& W, int64_t p, int64_t T, uint32
   const uint32_t slot = lv.tslot, loc = lv.tail * CH + slot;
   const uint32_t ix = idx_insert(W, oid, loc);
   if (lane == 0) {
-    Node nd{};
-    nd.rem = T;
-    nd.oid = oid;
-    nd.uuid = uuid;
-    nd.ixs = ix;
-    nd.tx = static_cast<uint8_t>(side);
-    W.D.nodes[lv.tail * CH + slot] = nd;
+    Node* d = &W.D.nodes[loc];
+    st16_glb(d, v4(lo32(T), hi32(T), oid, uuid));
+    st16_glb(reinterpret_cast<char*>(d) + 16, v4(ix, side & 0xFFu, 0u, 0u));
   }
   lv.tslot = static_cast<uint8_t>(slot + 1);
   lv.nlive++;

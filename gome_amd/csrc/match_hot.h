@@ -74,6 +74,7 @@ struct PendEnt {
   uint32_t oid, loc, ix;
   uint8_t used, ins, dead, pad;
 };
+static_assert(sizeof(PendEnt) == 16, "PendEnt is stored as one uint4");
 
 // A hot book that must continue on the HBM path (deep book, or lane array full):
 // k_match_resume rests the spilled order's remainder and applies orders [next, end).
@@ -524,23 +525,18 @@ __device__ __forceinline__ bool hot_rest(HotCtx& H, int64_t p, int64_t T, uint32
   const bool in_cache = cs != CS_NONE && v.hd == v.tl;  // the tail is the cached head chunk
   if (!in_cache && lav == LA_NONE) lav = LA_UNKNOWN;     // a live node now follows the head chunk
   if (lane == 0) {
-    PendEnt e;
-    e.oid = oid;
-    e.loc = loc;
-    e.ix = NIL;
-    e.used = 1;
-    e.ins = 0;
-    e.dead = 0;
-    e.pad = 0;
-    H.pend[pidx] = e;
-    Node nd{};
-    nd.rem = T;
-    nd.oid = oid;
-    nd.uuid = uuid;
-    nd.ixs = PEND | pidx;
-    nd.tx = static_cast<uint8_t>(side);
-    if (in_cache) S->cs[cs][tslot] = nd;
-    else W.D.nodes[loc] = nd;
+    // PendEnt {oid, loc, ix = NIL, used = 1, ins = dead = 0}
+    st16_glb(&H.pend[pidx], v4(oid, loc, NIL, 1u));
+    const v4u a = v4(lo32(T), hi32(T), oid, uuid), b = v4(PEND | pidx, side & 0xFFu, 0u, 0u);
+    if (in_cache) {
+      Node* d = &S->cs[cs][tslot];
+      st16_lds(d, a);
+      st16_lds(reinterpret_cast<char*>(d) + 16, b);
+    } else {
+      Node* d = &W.D.nodes[loc];
+      st16_glb(d, a);
+      st16_glb(reinterpret_cast<char*>(d) + 16, b);
+    }
   }
   v.nv++;
   v.mf = mf_make(member, lav, hslot, tslot + 1, cs);
@@ -641,8 +637,8 @@ __device__ __forceinline__ void hot_flush(HotCtx& H) {
         cs = (w.w == cid) ? 4 * c + 3 : cs;
       }
       if (ok) {
-        if (cs != CS_NONE) H.S->cs[cs][e.loc % CH].ixs = static_cast<uint32_t>(h);
-        else W.D.nodes[e.loc].ixs = static_cast<uint32_t>(h);
+        if (cs != CS_NONE) *as_lds(&H.S->cs[cs][e.loc % CH].ixs) = static_cast<uint32_t>(h);
+        else *as_glb(&W.D.nodes[e.loc].ixs) = static_cast<uint32_t>(h);
       }
     }
   }
@@ -666,13 +662,13 @@ __device__ __forceinline__ uint32_t hot_cancel(HotCtx& H, int64_t p, uint32_t oi
   LvS v = lv_get(H, k);
   uint32_t member = mf_member(v.mf), hslot = mf_hslot(v.mf), tslot = mf_tslot(v.mf), cs = mf_cs(v.mf);
   const bool cached = cs != CS_NONE && v.hd == cid;
-  const int64_t r = cached ? rl64(S->cs[cs][sl].rem, 0) : rl64(W.D.nodes[loc].rem, 0);
+  const int64_t r = cached ? rl64(*as_lds(&S->cs[cs][sl].rem), 0) : rl64(*as_glb(&W.D.nodes[loc].rem), 0);
   if (r < 0) { set_err(W, ERR_CORRUPT); return 0; }
   v.dp -= r;  // DeletePoolDepthVolume with the stored remaining volume
   if (v.dp <= 0) member &= ~((side == GOME_SALE) ? M_SALE : M_BUY);  // the REQUEST's side (Q2)
   if (lane == 0) {
-    if (cached) S->cs[cs][sl].rem = -1;
-    else W.D.nodes[loc].rem = -1;
+    if (cached) *as_lds(&S->cs[cs][sl].rem) = -1;
+    else *as_glb(&W.D.nodes[loc].rem) = -1;
     idx_erase(W, ixslot);
   }
   v.nv--;
@@ -816,7 +812,14 @@ __global__ __launch_bounds__(64) void k_match_hot(Dev D, BatchArgs B, PendEnt* p
   hot_ev_flush(H);
   if (spilled) hot_resolve_pending(H);  // the HBM path expects real index slots
   hot_writeback(H);
-  if (lane == 0) resume[blockIdx.x] = rr;
+  if (lane == 0) {
+    resume[blockIdx.x] = rr;
+    unsigned long long* c = W.D.st->ctr;
+    atomicAdd(&c[C_HOT_ORDERS], static_cast<unsigned long long>((spilled ? rr.next : end) - beg));
+    atomicAdd(&c[C_HOT_FILLS], W.fills);
+    atomicAdd(&c[C_HOT_RESTS], W.rests);
+    atomicAdd(&c[C_HOT_CANCELS], W.cancels);
+  }
   wave_finish(W);
 #ifdef GOME_STAMPS
   if (lane == 0 && blockIdx.x < 256)

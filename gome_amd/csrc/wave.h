@@ -60,6 +60,25 @@ __device__ __forceinline__ int64_t scan32_i64(int64_t x) {
   return x;
 }
 
+// Explicit address spaces.  Where one source line may store to LDS or to HBM, the compiler
+// merges the two into a FLAT access, which counts against both vmcnt and lgkmcnt: every
+// later LDS wait then also waits for the HBM write.  Route such stores through these.
+#define GOME_LDS __attribute__((address_space(3)))
+#define GOME_GLB __attribute__((address_space(1)))
+template <class T>
+__device__ __forceinline__ GOME_LDS T* as_lds(T* p) { return (GOME_LDS T*)(p); }
+template <class T>
+__device__ __forceinline__ GOME_GLB T* as_glb(T* p) { return (GOME_GLB T*)(p); }
+typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ v4u v4(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+  v4u r = {a, b, c, d};
+  return r;
+}
+__device__ __forceinline__ void st16_lds(void* p, v4u v) { *(GOME_LDS v4u*)(p) = v; }
+__device__ __forceinline__ void st16_glb(void* p, v4u v) { *(GOME_GLB v4u*)(p) = v; }
+__device__ __forceinline__ uint32_t lo32(int64_t x) { return static_cast<uint32_t>(x); }
+__device__ __forceinline__ uint32_t hi32(int64_t x) { return static_cast<uint32_t>(static_cast<uint64_t>(x) >> 32); }
+
 __host__ __device__ __forceinline__ unsigned long long mix64(unsigned long long x) {
   x ^= x >> 33; x *= 0xff51afd7ed558ccdULL; x ^= x >> 33;
   x *= 0xc4ceb9fe1a85ec53ULL; x ^= x >> 33;

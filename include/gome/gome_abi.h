@@ -143,6 +143,8 @@ typedef struct gome_stats {
                                                  cold books, concurrent)                 */
   double ms_hot;                              /* device time of k_match_hot (hot books)  */
   uint64_t n_hot;                             /* books applied by k_match_hot            */
+  uint64_t n_hot_orders, n_hot_fills;         /* work done inside k_match_hot (roofline   */
+  uint64_t n_hot_rests, n_hot_cancels;        /* numerator of the hot kernel)             */
 } gome_stats;
 
 typedef struct gome_engine gome_engine;

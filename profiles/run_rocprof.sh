@@ -4,7 +4,7 @@
 # usage: bash profiles/run_rocprof.sh <tag> [bench args...]
 set -o pipefail
 TAG=${1:-r01}; shift
-ARGS=${@:---steps 3 --warmup 1 --batch 1048576 --no-cpu-baseline}
+ARGS=${@:---steps 3 --warmup 1 --no-cpu-baseline}
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 OUT=gpurun_out/prof_$TAG

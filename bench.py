@@ -77,6 +77,32 @@ def shard_stream(n_symbols, zipf_s, rank, world, seed):
     return batch, share, float(p[0])
 
 
+def combine_ranks(orders, fills, events, elapsed, lat, device):
+    """Whole-job totals over ranks: sums of work, MAX of the timed region and of each
+    step's latency (the slowest rank defines the job).  Works on any initialised process
+    group (RCCL on the GPU box, gloo in tests/test_multirank.py)."""
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([orders, fills, events], dtype=torch.float64, device=device)
+    dist.all_reduce(t)
+    e = torch.tensor([elapsed], dtype=torch.float64, device=device)
+    dist.all_reduce(e, op=dist.ReduceOp.MAX)
+    lt = torch.tensor(lat, dtype=torch.float64, device=device)
+    dist.all_reduce(lt, op=dist.ReduceOp.MAX)
+    o, f, ev = (float(x) for x in t.tolist())
+    return o, f, ev, float(e.item()), lt.tolist()
+
+
+def gather_summary(st, summary, gathered):
+    """Per-GPU trade/depth summary to every rank (the publisher feed)."""
+    import torch.distributed as dist
+    summary.zero_()
+    summary[0] = st["n_orders"]; summary[1] = st["n_fills"]; summary[2] = st["n_events"]
+    summary[3] = st["n_resting"]; summary[4] = st["max_segment"]
+    dist.all_gather_into_tensor(gathered, summary)
+    return gathered
+
+
 def cpu_baseline(batches, n_symbols, budget_s):
     """C oracle (oracle/gome_oracle.c, 1 thread) on the first batches of this rank's stream."""
     from oracle.pyoracle import Oracle
@@ -143,9 +169,7 @@ def main():
         eng.submit_device(b.data_ptr(), per_rank, seq_base=i * per_rank)
         st = eng.stats()
         if world > 1:  # per-GPU trade/depth summary to the publisher (RCCL all_gather)
-            summary[0] = st["n_orders"]; summary[1] = st["n_fills"]; summary[2] = st["n_events"]
-            summary[3] = st["n_resting"]; summary[4] = st["max_segment"]
-            dist.all_gather_into_tensor(gathered, summary)
+            gather_summary(st, summary, gathered)
         return st
 
     for i in range(warm):
@@ -174,15 +198,7 @@ def main():
     bhot = sum(hot_algorithmic_bytes(s) for s in sts) / steps
     max_seg = max(s["max_segment"] for s in sts)
     if world > 1:
-        t = torch.tensor([orders, fills, events], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t)
-        orders, fills, events = (float(x) for x in t.tolist())
-        e = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(e, op=dist.ReduceOp.MAX)
-        elapsed = float(e.item())
-        lt = torch.tensor(lat, dtype=torch.float64, device="cuda")
-        dist.all_reduce(lt, op=dist.ReduceOp.MAX)
-        lat = lt.tolist()
+        orders, fills, events, elapsed, lat = combine_ranks(orders, fills, events, elapsed, lat, "cuda")
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

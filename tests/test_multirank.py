@@ -1,0 +1,107 @@
+"""N>1 path on CPU: symbol sharding and the cross-rank reductions of bench.py
+over a world-size-2 gloo process group.
+
+Books never interact (ordernode.go:89-116: every key is prefixed by the symbol), so a
+GPU that owns a subset of the symbols must produce exactly the events the single engine
+produces for those symbols.  That is checked here with the C oracle as the engine on
+each "rank" (the GPU engine is checked against the same oracle in test_gpu_parity.py)."""
+import os
+import socket
+import tempfile
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+import bench
+from gome_amd import workload as wl
+from oracle.pyoracle import Oracle
+
+
+def test_shard_stream_partitions_symbols():
+    world, n_sym = 4, 1000
+    z = wl.ZipfSymbols(n_sym, 1.0)
+    seen = []
+    shares = 0.0
+    for r in range(world):
+        gen, share, top = bench.shard_stream(n_sym, 1.0, r, world, seed=3)
+        b = gen(20000)
+        ranks = z.id_to_rank[b["symbol_id"]]
+        assert np.all(ranks % world == r)
+        assert len(np.unique(b["oid_id"])) == len(b)
+        seen.append(set(b["symbol_id"].tolist()))
+        shares += share
+    assert abs(shares - 1.0) < 1e-9
+    for i in range(world):
+        for j in range(i + 1, world):
+            assert not (seen[i] & seen[j])
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_books_equal_global(world):
+    """Union over ranks of per-rank events (taker_seq mapped back) == global events."""
+    n_sym, seed, batch = 300, 11, 6000
+    g = wl.Stream(n_sym, zipf_s=1.0, seed=seed)
+    z = g.zipf
+    glob = [g.batch(batch) for _ in range(3)]
+    o = Oracle(n_sym)
+    ev_glob = [o.submit(b) for b in glob]
+    per_rank = [Oracle(n_sym) for _ in range(world)]
+    for bi, b in enumerate(glob):
+        ranks = z.id_to_rank[b["symbol_id"]]
+        parts = []
+        for r in range(world):
+            idx = np.nonzero(ranks % world == r)[0]
+            ev = per_rank[r].submit(b[idx])
+            ev = ev.copy()
+            ev["taker_seq"] = idx[ev["taker_seq"]]
+            parts.append(ev)
+        u = np.concatenate(parts)
+        u = u[np.lexsort((u["fill_idx"], u["taker_seq"]))]
+        assert len(u) == len(ev_glob[bi])
+        assert u.tobytes() == ev_glob[bi].tobytes()
+    assert sum(p.resting() for p in per_rank) == o.resting()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, out_dir):
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        o, f, e, el, lat = bench.combine_ranks(100.0 * (rank + 1), 10.0 * (rank + 1), 7.0,
+                                               1.5 + rank, [1.0 + rank, 5.0 - rank], "cpu")
+        st = {"n_orders": 1000 + rank, "n_fills": 10 * rank, "n_events": 20 * rank,
+              "n_resting": 5 + rank, "max_segment": 77 + rank}
+        summary = torch.zeros(32, dtype=torch.int64)
+        gathered = torch.zeros(32 * world, dtype=torch.int64)
+        bench.gather_summary(st, summary, gathered)
+        np.save(os.path.join(out_dir, f"r{rank}.npy"),
+                np.array([o, f, e, el] + lat + gathered.tolist(), dtype=np.float64))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world2_reductions():
+    world = 2
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_worker, args=(world, _free_port(), d), nprocs=world, join=True)
+        res = [np.load(os.path.join(d, f"r{r}.npy")) for r in range(world)]
+    for r in res:
+        o, f, e, el = r[:4]
+        assert o == 300.0 and f == 30.0 and e == 14.0   # sums over ranks
+        assert el == 2.5                                 # max elapsed
+        assert list(r[4:6]) == [2.0, 5.0]                # per-step max latency
+        g = r[6:].reshape(world, 32)
+        for rk in range(world):
+            assert list(g[rk, :5]) == [1000 + rk, 10 * rk, 20 * rk, 5 + rk, 77 + rk]
+    assert res[0].tobytes() == res[1].tobytes()

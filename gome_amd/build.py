@@ -5,6 +5,7 @@ repository snapshot (they are git-ignored, not gpurun-ignored).
 """
 from __future__ import annotations
 
+import glob
 import os
 import shutil
 import subprocess
@@ -21,7 +22,8 @@ HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
 ARCH = os.environ.get("GOME_OFFLOAD_ARCH", "gfx950")
 
 SOURCES = [os.path.join(CSRC, "engine.hip"), os.path.join(CSRC, "host.cpp")]
-HEADERS = [os.path.join(CSRC, "device.h"), os.path.join(ROOT, "include", "gome", "gome_abi.h")]
+HEADERS = sorted(glob.glob(os.path.join(CSRC, "*.h"))) + [os.path.join(ROOT, "include", "gome", "gome_abi.h"),
+                                                         os.path.abspath(__file__)]
 
 
 def _stale(out: str, deps: list[str]) -> bool:
@@ -39,11 +41,17 @@ def _run(cmd: list[str]):
     return r
 
 
+# SimplifyCFG's common-instruction sinking merges stores to different fields of the hot
+# kernel's per-level structs into one store through a phi of pointers, which keeps the
+# struct in scratch memory (a memory round trip on the per-order path).  Disable it.
+DEVICE_FLAGS = ["-mllvm", "-sink-common-insts=false"]
+
+
 def build_engine(force: bool = False, extra: list[str] | None = None) -> str:
     if force or _stale(LIB, SOURCES + HEADERS):
         tmp = LIB + ".tmp"
         cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-               "-Wall", "-Wno-unused-result", "-I", os.path.join(ROOT, "include"),
+               "-Wall", "-Wno-unused-result", *DEVICE_FLAGS, "-I", os.path.join(ROOT, "include"),
                *SOURCES, "-o", tmp] + (extra or [])
         _run(cmd)
         os.replace(tmp, LIB)
@@ -53,7 +61,7 @@ def build_engine(force: bool = False, extra: list[str] | None = None) -> str:
 def build_stamps() -> str:
     """Diagnostic build with in-kernel s_memtime phase stamps (never used by the product)."""
     out = os.path.join(PKG, "libgome_stamps.so")
-    cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-DGOME_STAMPS",
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-DGOME_STAMPS", *DEVICE_FLAGS,
            "-I", os.path.join(ROOT, "include"), *SOURCES, "-o", out]
     _run(cmd)
     return out

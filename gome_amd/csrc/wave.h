@@ -79,6 +79,14 @@ __device__ __forceinline__ void st16_glb(void* p, v4u v) { *(GOME_GLB v4u*)(p) =
 __device__ __forceinline__ uint32_t lo32(int64_t x) { return static_cast<uint32_t>(x); }
 __device__ __forceinline__ uint32_t hi32(int64_t x) { return static_cast<uint32_t>(static_cast<uint64_t>(x) >> 32); }
 
+// Keep a wave-uniform value in VGPRs: an inline-asm VGPR output is divergent to the
+// compiler, so later arithmetic on it stays VALU instead of occupying the (scarce) SGPR file.
+template <class T>
+__device__ __forceinline__ T vreg(T x) {
+  asm volatile("" : "+v"(x));
+  return x;
+}
+
 __host__ __device__ __forceinline__ unsigned long long mix64(unsigned long long x) {
   x ^= x >> 33; x *= 0xff51afd7ed558ccdULL; x ^= x >> 33;
   x *= 0xc4ceb9fe1a85ec53ULL; x ^= x >> 33;

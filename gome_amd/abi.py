@@ -17,6 +17,8 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libgome.so")
 HEADER = os.path.join(os.path.dirname(_HERE), "include", "gome", "gome_abi.h")
 
+GOME_FLAG_LEGACY_HOT = 1  # gome_config.flags: hot books on the legacy FIFO kernel
+
 GOME_OK, GOME_E_INVAL, GOME_E_CAPACITY, GOME_E_DEVICE, GOME_E_STATE, GOME_E_NOTFOUND = range(6)
 STATUS_NAMES = {0: "OK", 1: "E_INVAL", 2: "E_CAPACITY", 3: "E_DEVICE", 4: "E_STATE", 5: "E_NOTFOUND"}
 
@@ -39,7 +41,9 @@ class Stats(C.Structure):
         "n_events", "n_resting", "n_levels", "max_segment", "n_segments")] + [
         ("ms_total", C.c_double), ("ms_match", C.c_double), ("ms_hot", C.c_double),
         ("n_hot", C.c_uint64), ("n_hot_orders", C.c_uint64), ("n_hot_fills", C.c_uint64),
-        ("n_hot_rests", C.c_uint64), ("n_hot_cancels", C.c_uint64)]
+        ("n_hot_rests", C.c_uint64), ("n_hot_cancels", C.c_uint64),
+        ("n_flow_books", C.c_uint64), ("n_flow_orders", C.c_uint64), ("n_flow_touches", C.c_uint64),
+        ("ms_flow_plan", C.c_double)]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_}
@@ -121,11 +125,11 @@ class Engine:
 
     def __init__(self, max_symbols: int, max_batch: int, max_nodes: int = 1 << 20,
                  max_levels: int = 1 << 20, accuracy: int = 8, device: int = 0,
-                 max_events: int = 0):
+                 max_events: int = 0, flags: int = 0):
         self.lib = load_library()
         cfg = Config(accuracy=accuracy, device=device, max_symbols=max_symbols,
                      max_batch=max_batch, max_nodes=max_nodes, max_levels=max_levels,
-                     max_events=max_events)
+                     max_events=max_events, flags=flags)
         h = C.c_void_p()
         s = self.lib.gome_create(C.byref(cfg), C.byref(h))
         if s != GOME_OK:

@@ -51,8 +51,11 @@ struct ChunkHdr {
 };
 
 struct Book {
-  uint32_t lvl_base, n_lvl, lvl_cap, pad;
+  uint32_t lvl_base, n_lvl, lvl_cap, pad;  // pad: BOOK_* flags
 };
+// The book has seen state the aggregate (flow) plan cannot express: a cancel whose request
+// side differs from the node's side (Q2) or a zero-volume maker (Q6).  Sticky.
+constexpr uint32_t BOOK_QUIRK = 1u;
 
 struct IdxEnt {
   unsigned long long key;  // ((S+1) << 32) | oid ; 0 empty, ~0 tombstone
@@ -74,8 +77,9 @@ enum : uint32_t {
 enum {
   C_FILLS = 0, C_CANCELS, C_RESTS, C_DROPPED, C_ADD, C_DEL, C_EVENTS,
   C_RESTING_DELTA, C_LEVELS_DELTA, C_MAXSEG, C_NSEG,
-  C_HOT_ORDERS, C_HOT_FILLS, C_HOT_RESTS, C_HOT_CANCELS,  // k_match_hot only
-  C_NCTR = 16
+  C_HOT_ORDERS, C_HOT_FILLS, C_HOT_RESTS, C_HOT_CANCELS,  // hot books (flow + legacy)
+  C_FLOW_BOOKS, C_FLOW_ORDERS, C_FLOW_TOUCHES,            // hot books on the flow path
+  C_NCTR = 20
 };
 
 struct Status {

@@ -12,6 +12,8 @@
 //                     SetOrder / Match / MatchOrder / DeleteOrder (engine.go:56-206) with
 //                     64-lane ballots over the level array and a 32-lane prefix scan over
 //                     FIFO volumes to find how far a taker sweeps
+//   k_flow_*          hot books on the flow path (match_flow.h): a serial plan over level
+//                     aggregates, then parallel fills / FIFO rebuild (the batch's critical path)
 //   k_scan_* + k_ev_scatter   event compaction into publish order (taker_seq, fill_idx)
 //   k_recycle         freed FIFO chunks back to the free pool
 //
@@ -27,6 +29,7 @@
 #include "../../include/gome/gome_abi.h"
 #include "device.h"
 #include "match_cold.h"
+#include "match_flow.h"
 #include "match_hot.h"
 #include "pipeline.h"
 #include "wave.h"
@@ -76,8 +79,11 @@ struct gome_engine {
   gome_config cfg{};
   hipStream_t stream = nullptr;
   hipStream_t hot_stream = nullptr;
+  hipStream_t flow_stream = nullptr;
   bool own_stream = false;
   hipEvent_t fork{}, join{}, evh0{}, evh1{};
+  hipEvent_t joinf{}, evf0{}, evf1{};
+  FlowArgs F{};
   Prep* d_prep = nullptr;
   PendEnt* d_pend = nullptr;
   ResumeRec* d_resume = nullptr;
@@ -139,7 +145,9 @@ struct gome_engine {
     if (evm0) { (void)hipEventDestroy(evm0); (void)hipEventDestroy(evm1); }
     if (fork) { (void)hipEventDestroy(fork); (void)hipEventDestroy(join); }
     if (evh0) { (void)hipEventDestroy(evh0); (void)hipEventDestroy(evh1); }
+    if (evf0) { (void)hipEventDestroy(evf0); (void)hipEventDestroy(evf1); (void)hipEventDestroy(joinf); }
     if (hot_stream) (void)hipStreamDestroy(hot_stream);
+    if (flow_stream) (void)hipStreamDestroy(flow_stream);
     if (own_stream && stream) (void)hipStreamDestroy(stream);
   }
 
@@ -178,6 +186,10 @@ gome_status gome_engine::init(const gome_config& c) {
   HIPCHK(hipEventCreateWithFlags(&join, hipEventDisableTiming));
   HIPCHK(hipEventCreate(&evh0));
   HIPCHK(hipEventCreate(&evh1));
+  HIPCHK(hipStreamCreateWithFlags(&flow_stream, hipStreamNonBlocking));
+  HIPCHK(hipEventCreateWithFlags(&joinf, hipEventDisableTiming));
+  HIPCHK(hipEventCreate(&evf0));
+  HIPCHK(hipEventCreate(&evf1));
   HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_match_hot),
                              hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(HOT_LDS_BYTES)));
 
@@ -235,6 +247,18 @@ gome_status gome_engine::init(const gome_config& c) {
       !alloc(&d_resume, MAX_HOT, "resume records") ||
       !alloc(&d_arena, arena_cap, "event arena") || !alloc(&d_events, arena_cap, "events"))
     return GOME_E_CAPACITY;
+  // flow path (match_flow.h): per-hot-book headers and level slots, packed records, the
+  // touch log and its per-level views (FL_TOUCH_MUL entries per order), gathered makers
+  const uint64_t ntouch = static_cast<uint64_t>(FL_TOUCH_MUL) * nb;
+  F.ig_cap = static_cast<uint32_t>(std::min<uint64_t>(std::max<uint64_t>(cfg.max_nodes, 1u << 16), 0xF0000000ull));
+  F.enabled = (cfg.flags & GOME_FLAG_LEGACY_HOT) ? 0u : 1u;
+  if (!alloc(&F.hdr, MAX_HOT, "flow headers") || !alloc(&F.lvl, MAX_HOT * FL_CAP, "flow levels") ||
+      !alloc(&F.ord8, nb, "flow records") || !alloc(&F.log, ntouch, "flow touch log") ||
+      !alloc(&F.srt, ntouch, "flow level runs") || !alloc(&F.rs, ntouch, "flow new makers") ||
+      !alloc(&F.fbase, ntouch, "flow fill bases") || !alloc(&F.ig, F.ig_cap, "flow gathered makers") ||
+      !alloc(&F.ig_bump, 1, "flow gather bump"))
+    return GOME_E_CAPACITY;
+  HIPCHK(hipMemsetAsync(F.hdr, 0, sizeof(FlowHdr) * MAX_HOT, stream));
   HIPCHK(hipMemsetAsync(d_pend, 0, sizeof(PendEnt) * nb, stream));
   if (D.idx_mask >= PEND) return fail(GOME_E_INVAL, "gome_config.max_nodes too large (index > 2^31 slots)");
   HIPCHK(hipStreamSynchronize(stream));
@@ -328,22 +352,38 @@ gome_status gome_engine::run(const gome_order* d_ord, uint32_t n, hipStream_t s)
   B.arena_cap = arena_cap;
   B.ev_count = d_ev_count;
   const uint32_t grid = std::min<uint32_t>(n, cfg.max_symbols);
+  const uint32_t nhot_max = std::min<uint32_t>(MAX_HOT, grid);
   HIPCHK(hipEventRecord(evm0, s));
+  HIPCHK(hipMemsetAsync(F.ig_bump, 0, 4, s));
+  k_flow_prep<<<nhot_max, FL_PREP_T, 0, s>>>(D, B, F);
   HIPCHK(hipEventRecord(fork, s));
+  // flow path: serial plan of each eligible hot book, then its parallel reconstruction
+  HIPCHK(hipStreamWaitEvent(flow_stream, fork, 0));
+  HIPCHK(hipEventRecord(evf0, flow_stream));
+  k_flow_plan<<<nhot_max, 64, 0, flow_stream>>>(D, F);
+  HIPCHK(hipEventRecord(evf1, flow_stream));
+  k_flow_scatter<<<dim3(64, nhot_max), 256, 0, flow_stream>>>(D, F);
+  k_flow_level<<<dim3(FL_CAP, nhot_max), 64, 0, flow_stream>>>(D, F);
+  k_flow_count<<<dim3(64, nhot_max), 256, 0, flow_stream>>>(D, B, F);
+  k_flow_write<<<nhot_max, FL_WRITE_T, 0, flow_stream>>>(D, B, F);
+  HIPCHK(hipEventRecord(joinf, flow_stream));
+  // legacy hot path (books the flow path declined)
   HIPCHK(hipStreamWaitEvent(hot_stream, fork, 0));
   HIPCHK(hipEventRecord(evh0, hot_stream));
-  k_match_hot<<<std::min<uint32_t>(MAX_HOT, grid), 64, HOT_LDS_BYTES, hot_stream>>>(D, B, d_pend, d_resume);
+  k_match_hot<<<nhot_max, 64, HOT_LDS_BYTES, hot_stream>>>(D, B, d_pend, d_resume, F.hdr);
   HIPCHK(hipEventRecord(evh1, hot_stream));
-  k_match_resume<<<std::min<uint32_t>(MAX_HOT, grid), 64, 0, hot_stream>>>(D, B, d_resume);
+  k_match_resume<<<nhot_max, 64, 0, hot_stream>>>(D, B, d_resume);
   k_pend_apply<<<dim3(8, 64), 256, 0, hot_stream>>>(D, d_pend, d_seg_start, d_seg_order, B);
   HIPCHK(hipEventRecord(join, hot_stream));
   k_match<<<grid, 64, 0, s>>>(D, B);
   HIPCHK(hipStreamWaitEvent(s, join, 0));
+  HIPCHK(hipStreamWaitEvent(s, joinf, 0));
   HIPCHK(hipEventRecord(evm1, s));
 
   // ---- event compaction into publish order
   scan(d_ev_count, n, d_ev_off, &d_st->n_events, s);
   k_ev_scatter<<<2048, T256, 0, s>>>(d_arena, arena_cap, d_st, d_ev_off, d_events);
+  k_flow_events<<<dim3(64, nhot_max), 256, 0, s>>>(D, B, F, d_ev_off, d_events);
   k_recycle_copy<<<256, 256, 0, s>>>(D);
   k_recycle_fin<<<1, 64, 0, s>>>(D);
   HIPCHK(hipGetLastError());
@@ -363,11 +403,16 @@ gome_status gome_engine::run(const gome_order* d_ord, uint32_t n, hipStream_t s)
   }
   resting += st.ctr[C_RESTING_DELTA];
   levels += st.ctr[C_LEVELS_DELTA];
-  float ms_total = 0, ms_match = 0, ms_hot = 0;
+  float ms_total = 0, ms_match = 0, ms_hot = 0, ms_flow = 0;
   (void)hipEventElapsedTime(&ms_total, ev0, ev1);
   (void)hipEventElapsedTime(&ms_match, evm0, evm1);
   (void)hipEventElapsedTime(&ms_hot, evh0, evh1);
+  (void)hipEventElapsedTime(&ms_flow, evf0, evf1);
   stats.ms_hot = ms_hot;
+  stats.ms_flow_plan = ms_flow;
+  stats.n_flow_books = st.ctr[C_FLOW_BOOKS];
+  stats.n_flow_orders = st.ctr[C_FLOW_ORDERS];
+  stats.n_flow_touches = st.ctr[C_FLOW_TOUCHES];
   stats.n_hot = st.nhot;
   stats.n_hot_orders = st.ctr[C_HOT_ORDERS];
   stats.n_hot_fills = st.ctr[C_HOT_FILLS];

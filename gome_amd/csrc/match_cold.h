@@ -33,6 +33,7 @@ struct WaveCtx {
   Level* L;          // the book's sorted level array (HBM)
   uint32_t nl, cap, base;
   uint32_t ev_base, ev_used, evb;
+  uint32_t flags;    // Book flags (BOOK_QUIRK)
   bool ev_ok, fatal;
   unsigned long long fills, cancels, rests, dropped, adds, dels;
   long long resting_delta, levels_delta;
@@ -404,6 +405,7 @@ __device__ __forceinline__ void do_rest(WaveCtx& W, int64_t p, int64_t T, uint32
     lv.tslot = 0;
   }
   const uint32_t slot = lv.tslot, loc = lv.tail * CH + slot;
+  if (T == 0) W.flags |= BOOK_QUIRK;  // zero-volume maker (Q6)
   const uint32_t ix = idx_insert(W, oid, loc);
   if (lane == 0) {
     Node* d = &W.D.nodes[loc];
@@ -478,6 +480,8 @@ __device__ __forceinline__ uint32_t do_cancel(WaveCtx& W, int64_t p, uint32_t oi
   const uint32_t cid = loc / CH, s = loc % CH;
   if (uni(static_cast<uint32_t>(W.D.chdr[cid].price != p))) return 0;  // wrong price (Q3)
   const int64_t r = rl64(W.D.nodes[cid * CH + s].rem, 0);
+  const uint32_t ntx = uni(static_cast<uint32_t>(W.D.nodes[cid * CH + s].tx));
+  if ((ntx == GOME_SALE) != (side == GOME_SALE)) W.flags |= BOOK_QUIRK;  // wrong-side cancel (Q2)
   uint32_t pos;
   if (r < 0 || !level_search(W, p, pos)) { set_err(W, ERR_CORRUPT); return 0; }
   Level lv = W.L[pos];
@@ -552,7 +556,7 @@ __device__ __forceinline__ void wave_finish(WaveCtx& W) {
     nb.lvl_base = W.base;
     nb.n_lvl = W.nl;
     nb.lvl_cap = W.cap;
-    nb.pad = 0;
+    nb.pad = W.flags;
     W.D.books[W.sym] = nb;
     unsigned long long* c = W.D.st->ctr;
     if (W.fills) atomicAdd(&c[C_FILLS], W.fills);
@@ -574,6 +578,7 @@ __device__ __forceinline__ void wave_init(WaveCtx& W, const Dev& D, const BatchA
   W.base = uni(bk.lvl_base);
   W.nl = uni(bk.n_lvl);
   W.cap = uni(bk.lvl_cap);
+  W.flags = uni(bk.pad);
   W.L = D.lvl + W.base;
   W.ev_base = NIL;
   W.ev_used = 0;

@@ -1,0 +1,901 @@
+// match_flow.h — the "flow" path for hot books: match_books split into a minimal serial
+// plan over level aggregates and a fully parallel reconstruction of fills and FIFOs.
+//
+// Why.  Matching within one book is sequential (the reference's single consumer,
+// rabbitmq.go:116), so a Zipf-hot book is the batch's critical path and what bounds
+// throughput is the per-order latency of ONE wavefront.  The legacy hot kernel
+// (match_hot.h) carries the whole FIFO machinery on that serial path (head nodes, chunk
+// caches, event stores, index probes): ~1.8 us per order.  But the only state the ORDER
+// of operations really flows through is the per-level aggregate S:depth:<p> plus the
+// S:BUY / S:SALE membership (nodepool.go:61-115): which levels a taker sweeps and how much
+// it takes from each (engine.go:118-136) depend on nothing else.  Given those per-level
+// amounts, the individual fills follow from FIFO order alone (engine.go:138-198): the makers
+// of one level form a queue in "volume coordinates" — maker m occupies [E_m, E_m + v_m),
+// the level's consumption advances a cursor — so every fill is an interval intersection.
+//
+//   k_flow_prep    (parallel, one workgroup per hot book) eligibility, the book's sorted
+//                  price set (<= FL_CAP levels) and one packed 8-B record per order
+//                  {volume, level index, side}.
+//   k_flow_plan    (SERIAL, one wave per book) the aggregate state machine: depths in lane
+//                  registers, membership as scalar bit masks; per order it logs one 16-B
+//                  "touch" per level it rests at / consumes from, with the level-local rank.
+//   k_flow_scatter (parallel) touches -> per-level runs (rank gives the slot: no sort).
+//   k_flow_level   (one wave per level) segmented scans -> volume coordinates of each
+//                  consumption and each new maker; gathers the consumed prefix of the
+//                  level's resting FIFO (chunk chain), frees consumed chunks, erases their
+//                  cancel-index entries, writes the partially filled head back.
+//   k_flow_count   (parallel) events per touch by binary search -> ev_count[], fill_idx base.
+//   k_flow_events  (parallel, after the global publish-order scan) writes every MatchResult
+//                  directly at its final position (taker_seq, fill_idx).
+//   k_flow_write   (one workgroup per book) appends the surviving new makers to the FIFOs,
+//                  inserts them into the cancel index, rewrites the level array.
+//
+// Eligibility (else the book takes the legacy hot path, bit-exact as before): the segment
+// has no DEL and no zero-volume admitted ADD (quirk Q6), the book carries no quirk state
+// (Q2 wrong-side cancels / zero-volume makers ever seen, Book::flags), and the book's live
+// levels plus the batch's new prices fit FL_CAP lanes.  Under those conditions every live
+// level has nodes, positive depth and exactly one side-set membership, which is what makes
+// the aggregate plan exact.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "../../include/gome/gome_abi.h"
+#include "device.h"
+#include "match_cold.h"
+#include "pipeline.h"
+#include "wave.h"
+
+namespace gome {
+
+constexpr uint32_t FL_CAP = 128;          // levels per flow book (two lane sets)
+constexpr uint32_t FL_HASH = 1024;        // LDS price-set slots in k_flow_prep
+constexpr uint32_t FL_PREP_T = 256;
+constexpr uint32_t FL_TOUCH_MUL = 4;      // log capacity per order (touches <= 3n + L0)
+constexpr unsigned long long FL_KEY_OFF = 1ull << 62;
+
+// packed order record of the plan (8 B): volume [0,53), level [53,60), SALE bit 60, skip 61
+constexpr uint32_t OR_LI_SHIFT = 21, OR_SELL = 1u << 28, OR_SKIP = 1u << 29;
+
+enum : uint32_t { TK_CONS = 0, TK_REST = 1 };
+
+struct Touch {       // one level visited by one order (16 B)
+  uint32_t j;        // order index within the segment
+  uint32_t kr;       // level [0,7) | kind << 7 | rank within the level << 8
+  int64_t amt;       // volume taken from the level (CONS) or rested at it (REST)
+};
+static_assert(sizeof(Touch) == 16, "Touch layout");
+
+struct SEnt {        // a touch in its level's run (32 B)
+  uint32_t j, kind;
+  int64_t amt;
+  int64_t coord;     // CONS: cursor before; REST: maker start E (volume coordinates)
+  uint32_t t;        // log index
+  uint32_t pad;
+};
+static_assert(sizeof(SEnt) == 32, "SEnt layout");
+
+struct RsEnt {       // a new maker of the level, in FIFO order (32 B)
+  int64_t e;         // start coordinate
+  int64_t v;         // volume rested
+  uint32_t j;        // order index within the segment
+  uint32_t t;        // log index of the rest (existence test for MatchNode.NextNode)
+  uint32_t pad0, pad1;
+};
+static_assert(sizeof(RsEnt) == 32, "RsEnt layout");
+
+struct IgEnt {       // a resting maker from before the batch, gathered in FIFO order (32 B)
+  int64_t e, v;
+  uint32_t oid, uuid;
+  uint32_t tx, pad;
+};
+static_assert(sizeof(IgEnt) == 32, "IgEnt layout");
+
+struct FlowHdr {
+  uint32_t ok, nl, sym, ntouch;
+  uint32_t beg, end, nold, adds;
+  uint32_t dropped, rests, pad0, pad1;
+  unsigned long long amask[2], bmask[2];  // final S:SALE / S:BUY membership of the levels
+};
+
+struct FlowLvl {
+  int64_t price;
+  int64_t d0;        // depth at batch start (== sum of live FIFO volumes)
+  int64_t dfin;      // depth after the batch (plan)
+  int64_t cfin;      // volume consumed from the level this batch
+  uint32_t old;      // index in the book's old level array, NIL if new
+  uint32_t nv0;      // live nodes at batch start
+  uint32_t cnt;      // touches
+  uint32_t base;     // start of the level's run (book-local)
+  uint32_t nrest;    // new makers (REST touches)
+  uint32_t ig_base, ig_n, ig_all;  // gathered old makers; ig_all: no live node beyond them
+  uint32_t head, tail;             // FIFO chunk chain (after the gather)
+  uint32_t hslot, tslot;
+  uint32_t nlive0;   // old makers surviving the batch
+  uint32_t mem0;     // membership at batch start
+  uint32_t pad0, pad1;
+};
+static_assert(sizeof(FlowLvl) % 16 == 0, "FlowLvl alignment");
+
+struct FlowArgs {
+  FlowHdr* hdr;        // [MAX_HOT]
+  FlowLvl* lvl;        // [MAX_HOT * FL_CAP]
+  unsigned long long* ord8;  // [max_batch] packed records, segment order
+  Touch* log;          // [FL_TOUCH_MUL * max_batch], book h at FL_TOUCH_MUL * beg
+  SEnt* srt;           // same index space
+  RsEnt* rs;           // same index space
+  uint32_t* fbase;     // same index space: fill_idx of a touch's first event
+  IgEnt* ig;
+  uint32_t ig_cap;
+  uint32_t* ig_bump;
+  uint32_t enabled;
+  uint32_t pad;
+};
+
+__device__ __forceinline__ uint32_t fl_hash(unsigned long long key) {
+  return static_cast<uint32_t>(mix64(key) >> 20) & (FL_HASH - 1);
+}
+
+// ============================================================== k_flow_prep
+__global__ __launch_bounds__(FL_PREP_T) void k_flow_prep(Dev D, BatchArgs B, FlowArgs F) {
+  __shared__ unsigned long long hkey[FL_HASH];
+  __shared__ uint32_t hval[FL_HASH];
+  __shared__ unsigned long long ckey[FL_CAP + FL_PREP_T];
+  __shared__ uint32_t cslot[FL_CAP + FL_PREP_T];
+  __shared__ uint32_t ndist, nc, bad, adds, dropped;
+  const uint32_t h = blockIdx.x, tid = threadIdx.x;
+  if (h >= D.st->nhot) return;
+  FlowHdr* hd = &F.hdr[h];
+  const uint32_t seg = B.seg_order[h];
+  const uint32_t beg = B.seg_start[seg], end = B.seg_start[seg + 1];
+  const uint32_t sym = B.ord[B.prep[beg].idx].symbol_id;
+  const Book bk = D.books[sym];
+  for (uint32_t i = tid; i < FL_HASH; i += FL_PREP_T) { hkey[i] = 0; hval[i] = NIL; }
+  if (tid == 0) {
+    ndist = nc = adds = dropped = 0;
+    bad = (!F.enabled || (bk.pad & BOOK_QUIRK) || bk.n_lvl > 4 * FL_CAP || (D.st->err & ERR_INPUT) ||
+           (end - beg) >= (1u << 24)) ? 1u : 0u;
+  }
+  __syncthreads();
+  auto insert = [&](unsigned long long key, uint32_t val) {
+    uint32_t s = fl_hash(key);
+    for (uint32_t probe = 0; probe < FL_HASH; ++probe) {
+      const unsigned long long prev = atomicCAS(&hkey[s], 0ull, key);
+      if (prev == 0ull) {
+        if (val != NIL) hval[s] = val;
+        if (atomicAdd(&ndist, 1u) >= FL_CAP) bad = 1;
+        return;
+      }
+      if (prev == key) {
+        if (val != NIL) hval[s] = val;
+        return;
+      }
+      s = (s + 1) & (FL_HASH - 1);
+    }
+    bad = 1;
+  };
+  // live levels of the book (clean invariant: live <=> nodes, positive depth, one side)
+  const Level* L0 = D.lvl + bk.lvl_base;
+  if (!bad) {
+    for (uint32_t k = tid; k < bk.n_lvl; k += FL_PREP_T) {
+      const Level x = L0[k];
+      const uint32_t nm = (x.member & M_BUY ? 1u : 0u) + (x.member & M_SALE ? 1u : 0u);
+      if (x.nlive == 0) {
+        if (x.depth != 0 || x.member != 0) bad = 1;
+        continue;
+      }
+      if (x.depth <= 0 || nm != 1) { bad = 1; continue; }
+      insert(static_cast<unsigned long long>(x.price) + FL_KEY_OFF, k);
+    }
+  }
+  __syncthreads();
+  // the segment's orders
+  uint32_t my_adds = 0, my_drop = 0;
+  if (!bad) {
+    for (uint32_t b = beg + tid; b < end; b += FL_PREP_T) {
+      const Prep q = B.prep[b];
+      if (q.action == GOME_DEL) { bad = 1; break; }
+      if (q.action != GOME_ADD) continue;
+      my_adds++;
+      if (!q.adm) { my_drop++; continue; }
+      if (q.vol == 0) { bad = 1; break; }
+      insert(static_cast<unsigned long long>(q.price) + FL_KEY_OFF, NIL);
+      if (bad) break;
+    }
+  }
+  if (my_adds) atomicAdd(&adds, my_adds);
+  if (my_drop) atomicAdd(&dropped, my_drop);
+  __syncthreads();
+  if (bad || ndist > FL_CAP) {
+    if (tid == 0) hd->ok = 0;
+    return;
+  }
+  // compact the set, rank-sort it (<= FL_CAP keys)
+  for (uint32_t s = tid; s < FL_HASH; s += FL_PREP_T) {
+    if (hkey[s]) {
+      const uint32_t i = atomicAdd(&nc, 1u);
+      ckey[i] = hkey[s];
+      cslot[i] = s;
+    }
+  }
+  __syncthreads();
+  const uint32_t n = nc;
+  FlowLvl* LV = F.lvl + h * FL_CAP;
+  if (tid < n) {
+    const unsigned long long key = ckey[tid];
+    uint32_t r = 0;
+    for (uint32_t i = 0; i < n; ++i) r += ckey[i] < key ? 1u : 0u;
+    const uint32_t s = cslot[tid], old = hval[s];
+    FlowLvl f{};
+    f.price = static_cast<int64_t>(key - FL_KEY_OFF);
+    f.old = old;
+    f.head = f.tail = NIL;
+    f.ig_base = 0;
+    if (old != NIL) {
+      const Level x = L0[old];
+      f.d0 = x.depth;
+      f.nv0 = x.nlive;
+      f.head = x.head;
+      f.tail = x.tail;
+      f.hslot = x.hslot;
+      f.tslot = x.tslot;
+      f.mem0 = x.member;
+    }
+    LV[r] = f;
+    hval[s] = r;  // the slot now maps price -> level index (each slot has one owner thread)
+  }
+  __syncthreads();
+  for (uint32_t b = beg + tid; b < end; b += FL_PREP_T) {
+    const Prep q = B.prep[b];
+    unsigned long long rec = static_cast<unsigned long long>(OR_SKIP) << 32;
+    if (q.action == GOME_ADD && q.adm) {
+      const unsigned long long key = static_cast<unsigned long long>(q.price) + FL_KEY_OFF;
+      uint32_t s = fl_hash(key);
+      while (hkey[s] != key) s = (s + 1) & (FL_HASH - 1);
+      const uint32_t li = hval[s];
+      const uint32_t hi = static_cast<uint32_t>(static_cast<unsigned long long>(q.vol) >> 32) |
+                          (li << OR_LI_SHIFT) | (q.side == GOME_SALE ? OR_SELL : 0u);
+      rec = (static_cast<unsigned long long>(hi) << 32) | static_cast<uint32_t>(q.vol);
+    }
+    F.ord8[b] = rec;
+    B.ev_count[q.idx] = 0;
+  }
+  if (tid == 0) {
+    FlowHdr x{};
+    x.ok = 1;
+    x.nl = n;
+    x.sym = sym;
+    x.beg = beg;
+    x.end = end;
+    x.nold = bk.n_lvl;
+    x.adds = adds;
+    x.dropped = dropped;
+    *hd = x;
+  }
+}
+
+// ============================================================== k_flow_plan (serial)
+// One wave per flow book.  Lane l holds the depth of level l (D0) and l + 64 (D1), and the
+// number of touches logged at it so far (C0, C1); S:SALE / S:BUY membership are 128-bit
+// scalar masks (A, Bm).  Per order: GetReverseDepth = mask AND, best level = bit scan,
+// MatchOrder at the aggregate level = compare + subtract, rest = add + set bit.  Touches
+// are staged in lane registers (lane = slot) and stored 64 at a time.
+__device__ __forceinline__ int64_t fl_get(int64_t D0, int64_t D1, uint32_t k) {
+  const int64_t a = rl64(D0, k & 63u), b = rl64(D1, k & 63u);
+  return k < 64 ? a : b;
+}
+
+__global__ __launch_bounds__(64) void k_flow_plan(Dev D, FlowArgs F) {
+  const uint32_t h = blockIdx.x;
+  if (h >= D.st->nhot) return;
+  const FlowHdr* hd = &F.hdr[h];
+  if (!uni(hd->ok)) return;
+  __builtin_amdgcn_s_setprio(3);
+  const uint32_t lane = lane_id();
+  const uint32_t nl = uni(hd->nl), beg = uni(hd->beg), end = uni(hd->end), n = end - beg;
+  FlowLvl* LV = F.lvl + h * FL_CAP;
+  int64_t D0 = lane < nl ? LV[lane].d0 : 0, D1 = lane + 64 < nl ? LV[lane + 64].d0 : 0;
+  const uint32_t m0 = lane < nl ? LV[lane].mem0 : 0u, m1 = lane + 64 < nl ? LV[lane + 64].mem0 : 0u;
+  unsigned long long A0 = __ballot(m0 & M_SALE), A1 = __ballot(m1 & M_SALE);
+  unsigned long long B0 = __ballot(m0 & M_BUY), B1 = __ballot(m1 & M_BUY);
+  uint32_t C0 = 0, C1 = 0;
+  uint32_t lj = 0, lk = 0, la = 0, lb = 0, nacc = 0, lpos = 0, rests = 0;
+  GOME_GLB v4u* logp = (GOME_GLB v4u*)(F.log + FL_TOUCH_MUL * beg);
+  const uint32_t lcap = FL_TOUCH_MUL * n;  // touches <= 3n + levels
+  const unsigned long long* o8 = F.ord8 + beg;
+
+  auto touch = [&](uint32_t jj, uint32_t k, uint32_t kind, int64_t amt) {
+    const uint32_t c0 = rl(C0, k & 63u), c1 = rl(C1, k & 63u);
+    const uint32_t rank = k < 64 ? c0 : c1;
+    C0 += (lane == k) ? 1u : 0u;
+    C1 += (lane + 64 == k) ? 1u : 0u;
+    lj = wl_u32(lj, jj, nacc);
+    lk = wl_u32(lk, k | (kind << 7) | (rank << 8), nacc);
+    la = wl_u32(la, lo32(amt), nacc);
+    lb = wl_u32(lb, hi32(amt), nacc);
+    if (++nacc == 64) {
+      if (lpos + 64 <= lcap) logp[lpos + lane] = v4(lj, lk, la, lb);
+      lpos += 64;
+      nacc = 0;
+    }
+  };
+  auto setd = [&](uint32_t k, int64_t v) {
+    D0 = (lane == k) ? v : D0;
+    D1 = (lane + 64 == k) ? v : D1;
+  };
+
+  for (uint32_t b0 = 0; b0 < n; b0 += 64) {
+    const uint32_t cnt = min(64u, n - b0);
+    const unsigned long long rec = lane < cnt ? o8[b0 + lane] : (static_cast<unsigned long long>(OR_SKIP) << 32);
+    const uint32_t rlo = static_cast<uint32_t>(rec), rhi = static_cast<uint32_t>(rec >> 32);
+    for (uint32_t j = 0; j < cnt; ++j) {
+      const uint32_t xhi = rl(rhi, j);
+      if (xhi & OR_SKIP) continue;
+      const uint32_t jj = b0 + j;
+      int64_t T = static_cast<int64_t>((static_cast<uint64_t>(xhi & 0x1FFFFFu) << 32) | rl(rlo, j));
+      const uint32_t li = (xhi >> OR_LI_SHIFT) & 0x7Fu;
+      if (!(xhi & OR_SELL)) {
+        // BUY: asks at levels <= li, ascending (nodepool.go:86-104)
+        unsigned long long c0 = A0 & (li >= 63 ? ~0ull : ((2ull << li) - 1));
+        unsigned long long c1 = li < 64 ? 0ull : (A1 & (li >= 127 ? ~0ull : ((2ull << (li - 64)) - 1)));
+        while (c0 | c1) {
+          const uint32_t k = c0 ? static_cast<uint32_t>(__builtin_ctzll(c0)) : 64u + static_cast<uint32_t>(__builtin_ctzll(c1));
+          const int64_t d = fl_get(D0, D1, k);
+          if (T < d) {  // partial: the level keeps depth d - T (engine.go:176-194)
+            setd(k, d - T);
+            touch(jj, k, TK_CONS, T);
+            T = 0;
+            break;
+          }
+          setd(k, 0);  // the level empties: ZREM (nodepool.go:76-83)
+          if (k < 64) { A0 &= ~(1ull << k); c0 &= ~(1ull << k); }
+          else { A1 &= ~(1ull << (k - 64)); c1 &= ~(1ull << (k - 64)); }
+          touch(jj, k, TK_CONS, d);
+          T -= d;
+          if (T == 0) break;  // diff == 0: stop (engine.go:162-175)
+        }
+        if (T > 0) {  // rest (engine.go:80-82): depth += T, ZADD S:BUY
+          setd(li, fl_get(D0, D1, li) + T);
+          if (li < 64) B0 |= 1ull << li;
+          else B1 |= 1ull << (li - 64);
+          touch(jj, li, TK_REST, T);
+          rests++;
+        }
+      } else {
+        // SALE: bids at levels >= li, descending (nodepool.go:105-115)
+        unsigned long long c1 = B1 & (li < 64 ? ~0ull : (~0ull << (li - 64)));
+        unsigned long long c0 = li < 64 ? (B0 & (~0ull << li)) : 0ull;
+        while (c0 | c1) {
+          const uint32_t k = c1 ? 64u + 63u - static_cast<uint32_t>(__builtin_clzll(c1))
+                                : 63u - static_cast<uint32_t>(__builtin_clzll(c0));
+          const int64_t d = fl_get(D0, D1, k);
+          if (T < d) {
+            setd(k, d - T);
+            touch(jj, k, TK_CONS, T);
+            T = 0;
+            break;
+          }
+          setd(k, 0);
+          if (k < 64) { B0 &= ~(1ull << k); c0 &= ~(1ull << k); }
+          else { B1 &= ~(1ull << (k - 64)); c1 &= ~(1ull << (k - 64)); }
+          touch(jj, k, TK_CONS, d);
+          T -= d;
+          if (T == 0) break;
+        }
+        if (T > 0) {
+          setd(li, fl_get(D0, D1, li) + T);
+          if (li < 64) A0 |= 1ull << li;
+          else A1 |= 1ull << (li - 64);
+          touch(jj, li, TK_REST, T);
+          rests++;
+        }
+      }
+    }
+  }
+  if (nacc) {
+    if (lane < nacc && lpos + nacc <= lcap) logp[lpos + lane] = v4(lj, lk, la, lb);
+    lpos += nacc;
+  }
+  if (lpos > lcap) {  // cannot happen (touch bound); never read past the log
+    if (lane == 0) atomicOr(&D.st->err, ERR_CORRUPT);
+    lpos = 0;
+  }
+  // per-level results and run bases (exclusive scan of the touch counts)
+  const uint32_t i0 = wave_incl_scan_u32(C0), i1 = wave_incl_scan_u32(C1);
+  const uint32_t t0 = rl(i0, 63);
+  if (lane < nl) {
+    LV[lane].dfin = D0;
+    LV[lane].cnt = C0;
+    LV[lane].base = i0 - C0;
+  }
+  if (lane + 64 < nl) {
+    LV[lane + 64].dfin = D1;
+    LV[lane + 64].cnt = C1;
+    LV[lane + 64].base = t0 + i1 - C1;
+  }
+  if (lane == 0) {
+    FlowHdr* w = &F.hdr[h];
+    w->ntouch = lpos;
+    w->rests = rests;
+    w->amask[0] = A0;
+    w->amask[1] = A1;
+    w->bmask[0] = B0;
+    w->bmask[1] = B1;
+  }
+}
+
+// ============================================================== k_flow_scatter
+__global__ void k_flow_scatter(Dev D, FlowArgs F) {
+  __shared__ uint32_t base[FL_CAP];
+  const uint32_t h = blockIdx.y;
+  if (h >= D.st->nhot || !F.hdr[h].ok) return;
+  const FlowLvl* LV = F.lvl + h * FL_CAP;
+  for (uint32_t k = threadIdx.x; k < FL_CAP; k += blockDim.x) base[k] = LV[k].base;
+  __syncthreads();
+  const uint32_t nt = F.hdr[h].ntouch, L = FL_TOUCH_MUL * F.hdr[h].beg;
+  for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < nt; t += gridDim.x * blockDim.x) {
+    const Touch x = F.log[L + t];
+    const uint32_t k = x.kr & 127u;
+    SEnt e;
+    e.j = x.j;
+    e.kind = (x.kr >> 7) & 1u;
+    e.amt = x.amt;
+    e.coord = 0;
+    e.t = t;
+    e.pad = 0;
+    F.srt[L + base[k] + (x.kr >> 8)] = e;
+  }
+}
+
+// ============================================================== k_flow_level
+// One wave per (book, level): volume coordinates of the level's run, then the gather of
+// the consumed prefix of its resting FIFO.
+__global__ __launch_bounds__(64) void k_flow_level(Dev D, FlowArgs F) {
+  const uint32_t h = blockIdx.y, q = blockIdx.x;
+  if (h >= D.st->nhot) return;
+  const FlowHdr* hd = &F.hdr[h];
+  if (!uni(hd->ok) || q >= uni(hd->nl)) return;
+  const uint32_t lane = lane_id();
+  FlowLvl* Lq = &F.lvl[h * FL_CAP + q];
+  const uint32_t L = FL_TOUCH_MUL * uni(hd->beg);
+  const uint32_t base = uni(Lq->base), cnt = uni(Lq->cnt);
+  const int64_t d0 = uni64(Lq->d0);
+  SEnt* R = F.srt + L + base;
+  RsEnt* RS = F.rs + L + base;
+  int64_t cc = 0, rr = d0;
+  uint32_t nr = 0;
+  const unsigned long long ltm = lt_mask();
+  for (uint32_t c0 = 0; c0 < cnt; c0 += 64) {
+    const uint32_t i = c0 + lane;
+    const bool valid = i < cnt;
+    SEnt e{};
+    if (valid) e = R[i];
+    const bool isc = valid && e.kind == TK_CONS, isr = valid && e.kind == TK_REST;
+    const int64_t ac = isc ? e.amt : 0, ar = isr ? e.amt : 0;
+    const int64_t ic = wave_incl_scan(ac), ir = wave_incl_scan(ar);
+    const unsigned long long rm = __ballot(isr);
+    if (isc) R[i].coord = cc + ic - ac;
+    if (isr) {
+      const int64_t e0 = rr + ir - ar;
+      R[i].coord = e0;
+      RsEnt x;
+      x.e = e0;
+      x.v = e.amt;
+      x.j = e.j;
+      x.t = e.t;
+      x.pad0 = x.pad1 = 0;
+      RS[nr + __popcll(rm & ltm)] = x;
+    }
+    cc += rl64(ic, 63);
+    rr += rl64(ir, 63);
+    nr += __popcll(rm);
+  }
+  const int64_t cfin = cc;
+  uint32_t nv0 = uni(Lq->nv0), head = uni(Lq->head), tail = uni(Lq->tail);
+  uint32_t hslot = uni(Lq->hslot), tslot = uni(Lq->tslot);
+  uint32_t ig_base = 0, ng = 0, consumed = 0;
+  bool have_extra = false;
+  if (nv0 > 0 && cfin > 0) {
+    uint32_t b = 0;
+    if (lane == 0) b = atomicAdd(F.ig_bump, nv0);
+    ig_base = uni(b);
+    if (static_cast<unsigned long long>(ig_base) + nv0 > F.ig_cap) {
+      if (lane == 0) atomicOr(&D.st->err, ERR_CHUNKS);
+      return;
+    }
+    IgEnt* IG = F.ig + ig_base;
+    int64_t E = 0;
+    bool have_surv = false;
+    uint32_t c = head, s0 = hslot, nh = NIL, nhs = 0;
+    for (uint32_t guard = 0; c != NIL && !have_extra; ++guard) {
+      if (guard > D.ch_cap) { if (lane == 0) atomicOr(&D.st->err, ERR_CORRUPT); return; }
+      const uint32_t lim = (c == tail) ? tslot : CH;
+      const bool inr = lane < CH && lane >= s0 && lane < lim;
+      Node nd{};
+      if (inr) nd = D.nodes[c * CH + lane];
+      const bool live = inr && nd.rem >= 0;
+      const int64_t x = live ? nd.rem : 0;
+      const int64_t inc = wave_incl_scan(x);
+      const int64_t em = E + inc - x;
+      const unsigned long long beyond = __ballot(live && em >= cfin);
+      const uint32_t fb = beyond ? static_cast<uint32_t>(__builtin_ctzll(beyond)) : 64u;
+      const bool take = live && (em < cfin || lane == fb);
+      const unsigned long long tm = __ballot(take);
+      if (take) {
+        IgEnt g;
+        g.e = em;
+        g.v = nd.rem;
+        g.oid = nd.oid;
+        g.uuid = nd.uuid;
+        g.tx = nd.tx;
+        g.pad = 0;
+        IG[ng + __popcll(tm & ltm)] = g;
+      }
+      ng += __popcll(tm);
+      const bool cons = live && em + nd.rem <= cfin;
+      if (cons) __hip_atomic_store(&D.idx[nd.ixs].key, KEY_TOMB, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      consumed += __popcll(__ballot(cons));
+      if (!have_surv) {
+        const unsigned long long sv = __ballot(live && em + nd.rem > cfin);
+        if (sv) {
+          have_surv = true;
+          nh = c;
+          nhs = static_cast<uint32_t>(__builtin_ctzll(sv));
+          if (lane == nhs && em < cfin) D.nodes[c * CH + lane].rem = em + nd.rem - cfin;  // partial head
+        } else {
+          if (lane == 0) D.freed_ids[atomicAdd(&D.st->freed_top, 1u)] = c;  // fully consumed chunk
+        }
+      }
+      if (beyond) have_extra = true;
+      E += rl64(inc, 63);
+      const uint32_t nx = (c == tail) ? NIL : uni(D.chdr[c].next);
+      c = nx;
+      s0 = 0;
+    }
+    if (!have_surv) {
+      head = tail = NIL;
+      hslot = tslot = 0;
+    } else {
+      head = nh;
+      hslot = nhs;
+    }
+  }
+  if (lane == 0) {
+    Lq->cfin = cfin;
+    Lq->nrest = nr;
+    Lq->ig_base = ig_base;
+    Lq->ig_n = ng;
+    Lq->ig_all = have_extra ? 0u : 1u;
+    Lq->head = head;
+    Lq->tail = tail;
+    Lq->hslot = hslot;
+    Lq->tslot = tslot;
+    Lq->nlive0 = nv0 - consumed;
+  }
+}
+
+// ============================================================== events of one touch
+// Makers of level q in FIFO order: the gathered old makers IG[0, ig_n) (coordinates from 0),
+// then the new makers RS[0, nrest) (from d0).  Index of the maker covering coordinate x.
+__device__ __forceinline__ uint32_t fl_find(const IgEnt* IG, uint32_t ig_n, const RsEnt* RS, uint32_t nrest,
+                                            int64_t d0, int64_t x) {
+  if (x < d0) {
+    uint32_t lo = 0, hi = ig_n;  // last e <= x
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (IG[mid].e <= x) lo = mid; else hi = mid;
+    }
+    return lo;
+  }
+  uint32_t lo = 0, hi = nrest;
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (RS[mid].e <= x) lo = mid; else hi = mid;
+  }
+  return ig_n + lo;
+}
+
+struct FlTouchCtx {
+  const FlowLvl* Lq;
+  const IgEnt* IG;
+  const RsEnt* RS;
+  int64_t c, a;
+  uint32_t first, last;
+};
+
+__device__ __forceinline__ FlTouchCtx fl_touch_ctx(const FlowArgs& F, uint32_t h, uint32_t L, const Touch& x) {
+  FlTouchCtx t;
+  const uint32_t k = x.kr & 127u;
+  t.Lq = &F.lvl[h * FL_CAP + k];
+  const uint32_t base = t.Lq->base;
+  t.IG = F.ig + t.Lq->ig_base;
+  t.RS = F.rs + L + base;
+  t.c = F.srt[L + base + (x.kr >> 8)].coord;
+  t.a = x.amt;
+  const int64_t d0 = t.Lq->d0;
+  const uint32_t ig_n = t.Lq->ig_n, nrest = t.Lq->nrest;
+  t.first = fl_find(t.IG, ig_n, t.RS, nrest, d0, t.c);
+  t.last = fl_find(t.IG, ig_n, t.RS, nrest, d0, t.c + t.a - 1);
+  return t;
+}
+
+// ============================================================== k_flow_count
+// Thread per touch; the first touch of each order walks the order's touches (consecutive
+// in the log, best level first), fixing fill_idx bases and ev_count[taker].
+__global__ void k_flow_count(Dev D, BatchArgs B, FlowArgs F) {
+  const uint32_t h = blockIdx.y;
+  if (h >= D.st->nhot || !F.hdr[h].ok) return;
+  const uint32_t nt = F.hdr[h].ntouch, beg = F.hdr[h].beg, L = FL_TOUCH_MUL * beg;
+  unsigned long long fills = 0, pops = 0;
+  for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < nt; t += gridDim.x * blockDim.x) {
+    const Touch x = F.log[L + t];
+    if (t > 0 && F.log[L + t - 1].j == x.j) continue;
+    uint32_t acc = 0;
+    for (uint32_t u = t; u < nt; ++u) {
+      const Touch y = (u == t) ? x : F.log[L + u];
+      if (y.j != x.j) break;
+      F.fbase[L + u] = acc;
+      if (((y.kr >> 7) & 1u) == TK_CONS) {
+        const FlTouchCtx c = fl_touch_ctx(F, h, L, y);
+        const uint32_t ne = c.last - c.first + 1;
+        acc += ne;
+        fills += ne;
+        const int64_t lend = c.last < c.Lq->ig_n ? c.IG[c.last].e + c.IG[c.last].v
+                                                 : c.RS[c.last - c.Lq->ig_n].e + c.RS[c.last - c.Lq->ig_n].v;
+        pops += ne - (lend > c.c + c.a ? 1u : 0u);
+      }
+    }
+    B.ev_count[B.prep[beg + x.j].idx] = acc;
+  }
+  // wave-reduce the counters, one atomic per wave
+  for (int off = 32; off > 0; off >>= 1) {
+    fills += __shfl_xor(fills, off);
+    pops += __shfl_xor(pops, off);
+  }
+  if (lane_id() == 0 && fills) {
+    atomicAdd(&D.st->ctr[C_FILLS], fills);
+    atomicAdd(&D.st->ctr[C_HOT_FILLS], fills);
+    atomicAdd(&D.st->ctr[C_RESTING_DELTA], static_cast<unsigned long long>(-static_cast<long long>(pops)));
+  }
+}
+
+// ============================================================== k_flow_events
+// After the publish-order scan: every fill event at out[ev_off[taker] + fill_idx].
+__global__ void k_flow_events(Dev D, BatchArgs B, FlowArgs F, const uint32_t* ev_off, gome_event* out) {
+  const uint32_t h = blockIdx.y;
+  if (h >= D.st->nhot || !F.hdr[h].ok) return;
+  const uint32_t nt = F.hdr[h].ntouch, beg = F.hdr[h].beg, L = FL_TOUCH_MUL * beg, sym = F.hdr[h].sym;
+  for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < nt; t += gridDim.x * blockDim.x) {
+    const Touch x = F.log[L + t];
+    if (((x.kr >> 7) & 1u) != TK_CONS) continue;
+    const FlTouchCtx c = fl_touch_ctx(F, h, L, x);
+    const Prep tk = B.prep[beg + x.j];
+    // taker remaining before this level: volume minus what its better levels took
+    int64_t tb = tk.vol;
+    for (uint32_t u = t; u > 0; --u) {
+      const Touch y = F.log[L + u - 1];
+      if (y.j != x.j) break;
+      tb -= y.amt;
+    }
+    const uint32_t ig_n = c.Lq->ig_n, nrest = c.Lq->nrest, ig_all = c.Lq->ig_all;
+    const int64_t price = c.Lq->price;
+    gome_event* dst = out + ev_off[tk.idx] + F.fbase[L + t];
+    for (uint32_t m = c.first; m <= c.last; ++m) {
+      int64_t e, v;
+      uint32_t oid, uuid, tx;
+      if (m < ig_n) {
+        const IgEnt g = c.IG[m];
+        e = g.e; v = g.v; oid = g.oid; uuid = g.uuid; tx = g.tx;
+      } else {
+        const RsEnt r = c.RS[m - ig_n];
+        const Prep mk = B.prep[beg + r.j];
+        e = r.e; v = r.v; oid = mk.oid; uuid = mk.uuid; tx = mk.side;
+      }
+      const int64_t lo = e > c.c ? e : c.c;
+      const int64_t hi = (e + v < c.c + c.a) ? e + v : c.c + c.a;
+      const int64_t qty = hi - lo, pre = e + v - lo;
+      const bool full = e + v <= c.c + c.a;
+      // MatchNode.NextNode: the next node of the FIFO at the time of this fill
+      uint32_t nx = 0, last = 1;
+      if (m + 1 < ig_n) {
+        nx = c.IG[m + 1].oid;
+        last = 0;
+      } else if (ig_all || m + 1 > ig_n) {
+        const uint32_t r = m + 1 - ig_n;
+        if (r < nrest && c.RS[r].t < t) {
+          nx = B.prep[beg + c.RS[r].j].oid;
+          last = 0;
+        }
+      }
+      gome_event ev;
+      ev.price_fx = price;
+      ev.match_volume_fx = qty;
+      ev.maker_volume_fx = full ? pre : pre - qty;
+      ev.taker_volume_fx = tb - (hi - c.c);
+      ev.taker_seq = tk.idx;
+      ev.fill_idx = F.fbase[L + t] + (m - c.first);
+      ev.symbol_id = sym;
+      ev.maker_oid_id = oid;
+      ev.maker_uuid_id = uuid;
+      ev.maker_next_oid_id = nx;
+      ev.kind = GOME_EV_FILL;
+      ev.maker_side = static_cast<uint8_t>(tx);
+      ev.maker_is_last = static_cast<uint8_t>(last);
+      ev.pad0 = 0;
+      ev.pad1 = 0;
+      dst[m - c.first] = ev;
+    }
+  }
+}
+
+// ============================================================== k_flow_write
+// One workgroup per flow book: append the surviving new makers to their FIFOs (chunks from
+// the free stack / bump pool), insert them into the cancel index, rewrite the level array.
+constexpr uint32_t FL_WRITE_T = 256;
+
+__global__ __launch_bounds__(FL_WRITE_T) void k_flow_write(Dev D, BatchArgs B, FlowArgs F) {
+  __shared__ Level lv[FL_CAP];
+  __shared__ uint32_t keep[FL_CAP];
+  __shared__ uint32_t nout_s, base_s, cap_s;
+  const uint32_t h = blockIdx.x;
+  if (h >= D.st->nhot || !F.hdr[h].ok) return;
+  const FlowHdr hd = F.hdr[h];
+  const uint32_t lane = lane_id(), w = threadIdx.x >> 6, nw = FL_WRITE_T / 64;
+  const uint32_t L = FL_TOUCH_MUL * hd.beg;
+  const unsigned long long mask = D.idx_mask;
+  for (uint32_t q = w; q < hd.nl; q += nw) {
+    const FlowLvl f = F.lvl[h * FL_CAP + q];
+    const RsEnt* RS = F.rs + L + f.base;
+    // first new maker that survives the batch
+    uint32_t rf = 0;
+    if (f.cfin > f.d0) {
+      uint32_t lo = 0, hi = f.nrest;  // first r with e + v > cfin
+      while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (RS[mid].e + RS[mid].v > f.cfin) hi = mid; else lo = mid + 1;
+      }
+      rf = lo;
+    }
+    const uint32_t S = f.nrest - rf;
+    const bool fresh = f.nlive0 == 0;
+    const uint32_t s0 = fresh ? 0u : f.tslot;
+    const uint32_t room = fresh ? 0u : CH - s0;
+    const uint32_t need = S > room ? (S - room + CH - 1) / CH : 0u;
+    // claim `need` chunk ids: free stack first, then the bump pointer
+    int t = 0;
+    uint32_t nst = 0, bb = 0;
+    if (need) {
+      if (lane == 0) t = atomicSub(&D.st->free_top, static_cast<int>(need));
+      t = static_cast<int>(uni(static_cast<uint32_t>(t)));
+      nst = static_cast<uint32_t>(min(max(t, 0), static_cast<int>(need)));
+      if (lane == 0 && nst < need) bb = atomicAdd(D.ch_bump, need - nst);
+      bb = uni(bb);
+      if (bb + (need - nst) > D.ch_cap) {
+        if (lane == 0) atomicOr(&D.st->err, ERR_CHUNKS);
+        continue;
+      }
+    }
+    auto chunk_id = [&](uint32_t i) -> uint32_t {
+      return i < nst ? D.free_ids[t - static_cast<int>(nst) + static_cast<int>(i)] : bb + (i - nst);
+    };
+    for (uint32_t i = lane; i < need; i += 64) {
+      ChunkHdr c;
+      c.next = (i + 1 < need) ? chunk_id(i + 1) : NIL;
+      c.pad = 0;
+      c.price = f.price;
+      D.chdr[chunk_id(i)] = c;
+    }
+    if (need && !fresh && lane == 0) D.chdr[f.tail].next = chunk_id(0);
+    for (uint32_t i = lane; i < S; i += 64) {
+      const RsEnt r = RS[rf + i];
+      const Prep mk = B.prep[hd.beg + r.j];
+      const int64_t rem = (r.e < f.cfin) ? r.e + r.v - f.cfin : r.v;
+      uint32_t cid, slot;
+      if (!fresh && s0 + i < CH) {
+        cid = f.tail;
+        slot = s0 + i;
+      } else {
+        const uint32_t g = fresh ? i : i - room;
+        cid = chunk_id(g / CH);
+        slot = g % CH;
+      }
+      const uint32_t loc = cid * CH + slot;
+      const unsigned long long key = (static_cast<unsigned long long>(hd.sym + 1) << 32) | mk.oid;
+      unsigned long long hh = mix64(key) & mask, probe = 0;
+      for (; probe <= mask; ++probe, hh = (hh + 1) & mask) {
+        const unsigned long long kv = __hip_atomic_load(&D.idx[hh].key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((kv == KEY_EMPTY || kv == KEY_TOMB) && atomicCAS(&D.idx[hh].key, kv, key) == kv) break;
+      }
+      if (probe > mask) { atomicOr(&D.st->err, ERR_INDEX); continue; }
+      D.idx[hh].loc = loc;
+      Node nd{};
+      nd.rem = rem;
+      nd.oid = mk.oid;
+      nd.uuid = mk.uuid;
+      nd.ixs = static_cast<uint32_t>(hh);
+      nd.tx = mk.side;
+      D.nodes[loc] = nd;
+    }
+    if (lane == 0) {
+      Level x{};
+      x.price = f.price;
+      x.depth = f.dfin;
+      x.nlive = f.nlive0 + S;
+      uint32_t mem = 0;
+      if ((hd.amask[q >> 6] >> (q & 63)) & 1ull) mem |= M_SALE;
+      if ((hd.bmask[q >> 6] >> (q & 63)) & 1ull) mem |= M_BUY;
+      x.member = static_cast<uint8_t>(mem);
+      if (x.nlive == 0) {
+        x.head = x.tail = NIL;
+        x.hslot = x.tslot = 0;
+      } else if (fresh) {
+        x.head = chunk_id(0);
+        x.hslot = 0;
+        x.tail = chunk_id(need - 1);
+        x.tslot = static_cast<uint8_t>(S - (need - 1) * CH);
+      } else {
+        x.head = f.head;
+        x.hslot = static_cast<uint8_t>(f.hslot);
+        x.tail = need ? chunk_id(need - 1) : f.tail;
+        x.tslot = static_cast<uint8_t>(need ? (S - room) - (need - 1) * CH : s0 + S);
+      }
+      // clean-book invariant: nodes <=> positive depth <=> one side-set membership
+      const bool ok = (x.nlive > 0) == (x.depth > 0) && (x.nlive > 0) == (mem == M_BUY || mem == M_SALE) &&
+                      (x.nlive > 0 || mem == 0);
+      if (!ok) atomicOr(&D.st->err, ERR_CORRUPT);
+      lv[q] = x;
+      keep[q] = x.nlive > 0 ? 1u : 0u;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t c = 0;
+    for (uint32_t q = 0; q < hd.nl; ++q) {
+      const uint32_t k = keep[q];
+      keep[q] = k ? c : NIL;
+      c += k;
+    }
+    nout_s = c;
+    const Book bk = D.books[hd.sym];
+    uint32_t base = bk.lvl_base, cap = bk.lvl_cap;
+    if (c > cap) {
+      uint32_t ncap = 16;
+      while (ncap < c) ncap <<= 1;
+      const uint32_t nb = atomicAdd(D.lvl_bump, ncap);
+      if (static_cast<unsigned long long>(nb) + ncap > D.lvl_cap_total) {
+        atomicOr(&D.st->err, ERR_LEVELS);
+        cap = 0;
+      } else {
+        base = nb;
+        cap = ncap;
+      }
+    }
+    base_s = base;
+    cap_s = cap;
+  }
+  __syncthreads();
+  const uint32_t nout = nout_s;
+  if (nout > cap_s) return;
+  for (uint32_t q = threadIdx.x; q < hd.nl; q += FL_WRITE_T)
+    if (keep[q] != NIL) D.lvl[base_s + keep[q]] = lv[q];
+  if (threadIdx.x == 0) {
+    Book nb;
+    nb.lvl_base = base_s;
+    nb.n_lvl = nout;
+    nb.lvl_cap = cap_s;
+    nb.pad = 0;
+    D.books[hd.sym] = nb;
+    unsigned long long* c = D.st->ctr;
+    atomicAdd(&c[C_RESTS], static_cast<unsigned long long>(hd.rests));
+    atomicAdd(&c[C_HOT_RESTS], static_cast<unsigned long long>(hd.rests));
+    atomicAdd(&c[C_RESTING_DELTA], static_cast<unsigned long long>(hd.rests));
+    atomicAdd(&c[C_ADD], static_cast<unsigned long long>(hd.adds));
+    atomicAdd(&c[C_DROPPED], static_cast<unsigned long long>(hd.dropped));
+    atomicAdd(&c[C_LEVELS_DELTA], static_cast<unsigned long long>(static_cast<long long>(nout) - hd.nold));
+    atomicAdd(&c[C_HOT_ORDERS], static_cast<unsigned long long>(hd.end - hd.beg));
+    atomicAdd(&c[C_FLOW_BOOKS], 1ull);
+    atomicAdd(&c[C_FLOW_ORDERS], static_cast<unsigned long long>(hd.end - hd.beg));
+    atomicAdd(&c[C_FLOW_TOUCHES], static_cast<unsigned long long>(hd.ntouch));
+  }
+}
+
+}  // namespace gome

@@ -31,6 +31,7 @@
 #include "../../include/gome/gome_abi.h"
 #include "device.h"
 #include "match_cold.h"
+#include "match_flow.h"
 #include "wave.h"
 
 namespace gome {
@@ -112,6 +113,7 @@ struct HotLds {
   uint32_t freed[FREED];            // released chunk ids not yet published
   HotEnv env;
   uint32_t nfree, npool, nfreed, nflushed;  // pool / cache-slot / flush counters (rare paths)
+  uint32_t bflags;                          // Book flags (BOOK_QUIRK), rare-path writes
   ResumeRec rr;                             // written only when the lane book spills
 #ifdef GOME_STAMPS
   unsigned long long st[16];
@@ -169,13 +171,7 @@ __device__ __forceinline__ uint32_t sl_nxs(uint32_t sl) { return (sl >> 24) & 3u
 // Side-set bit of a raw Transaction value: SALE iff 1, anything else BUY (ordernode.go:95).
 __device__ __forceinline__ uint32_t side_bit(uint32_t tx) { return tx == GOME_SALE ? M_SALE : M_BUY; }
 
-// v_writelane_b32: replace lane l of `reg` with the uniform value v (no exec masking).
-// HIP exposes no builtin for it; bind the LLVM intrinsic so the compiler sees (and
-// hazard-checks) a real v_writelane.
-__device__ int gome_writelane_i32(int val, int lane, int old) __asm("llvm.amdgcn.writelane.i32");
-__device__ __forceinline__ uint32_t wl(uint32_t reg, uint32_t v, uint32_t l) {
-  return static_cast<uint32_t>(gome_writelane_i32(static_cast<int>(v), static_cast<int>(l), static_cast<int>(reg)));
-}
+__device__ __forceinline__ uint32_t wl(uint32_t reg, uint32_t v, uint32_t l) { return wl_u32(reg, v, l); }
 __device__ __forceinline__ int64_t wl64(int64_t reg, int64_t v, uint32_t l) {
   const uint32_t lo = wl(lo32(reg), lo32(v), l), hi = wl(hi32(reg), hi32(v), l);
   return static_cast<int64_t>((static_cast<uint64_t>(hi) << 32) | lo);
@@ -673,6 +669,7 @@ __device__ __forceinline__ void hot_rest_gen(HotCtx& H, uint32_t k, LvRec r, int
   uint32_t cs = sl_cs(r.sl), tslot = sl_ts(r.sl), nxs = sl_nxs(r.sl);
   const uint32_t pidx = H.npend++;
   const v4u na = v4(lo32(T), hi32(T), oid, uuid), nb = v4(PEND | pidx, side & 0xFFu, 0u, 0u);
+  if (T == 0) l0_lds4(&S->bflags, BOOK_QUIRK);  // zero-volume maker (Q6)
   uint32_t loc;
   if (r.tl == NIL) {  // empty FIFO (InitOrderLink, nodelink.go:12): new chunk = head = tail
     const uint32_t c = hot_alloc_chunk(H);
@@ -736,6 +733,7 @@ __device__ __forceinline__ void hot_rest_fast(HotCtx& H, uint32_t k, int64_t p, 
   }
   const uint32_t pidx = H.npend++;
   const uint32_t loc = r.tl * CH + ts;
+  if (T == 0) l0_lds4(&H.S->bflags, BOOK_QUIRK);  // zero-volume maker (Q6)
   const v4u na = v4(lo32(T), hi32(T), oid, uuid), nb = v4(PEND | pidx, side & 0xFFu, 0u, 0u);
   uint32_t mask = Q0 | Q2 | Q3;
   if (cs != CS_NONE && r.hd == r.tl) {  // tail == cached head chunk
@@ -1036,6 +1034,8 @@ __device__ __forceinline__ void hot_cancel_at(HotCtx& H, uint32_t k, uint32_t lo
   const bool inhead = cs != CS_NONE && cid == r.hd;
   const bool ishead = inhead && s == h.slot;
   const int64_t rem = ishead ? r.hrem : inhead ? uni64(*as_lds(&S->cs[cs][s].rem)) : uni64(*as_glb(&H.nodes[loc].rem));
+  const uint32_t ntx = ishead ? r.hx : inhead ? uni(*as_lds(&S->cs[cs][s].tx)) : uni(*as_glb(&H.nodes[loc].tx));
+  if ((ntx == GOME_SALE) != (side == GOME_SALE)) l0_lds4(&S->bflags, BOOK_QUIRK);  // wrong-side cancel (Q2)
   if (rem < 0) { hot_err(H, ERR_CORRUPT); return; }
   r.dp -= rem;  // DeletePoolDepthVolume with the stored remaining volume
   if (r.dp <= 0) mem_put(H, k, mem_get(H, k) & ~side_bit(side));  // ZREM from the REQUEST's side set (Q2)
@@ -1119,9 +1119,13 @@ __device__ __forceinline__ void hot_resolve_pending(HotCtx& H) {
 }
 
 __global__ __launch_bounds__(64) void k_match_hot(Dev D, BatchArgs B, PendEnt* pend_arena,
-                                                   ResumeRec* resume) {
+                                                   ResumeRec* resume, const FlowHdr* flow) {
   extern __shared__ __align__(16) unsigned char smem[];
   if (blockIdx.x >= D.st->nhot || (D.st->err & ERR_INPUT)) return;
+  if (flow[blockIdx.x].ok) {  // applied by the flow path (match_flow.h)
+    if (lane_id() == 0) resume[blockIdx.x].valid = 0;
+    return;
+  }
   __builtin_amdgcn_s_setprio(3);  // the hottest books are the batch's critical path
   const uint32_t lane = lane_id();
   const uint32_t seg = B.seg_order[blockIdx.x];
@@ -1164,6 +1168,7 @@ __global__ __launch_bounds__(64) void k_match_hot(Dev D, BatchArgs B, PendEnt* p
     S->env = e;
     S->nfree = NCS;
     S->npool = S->nfreed = S->nflushed = 0;
+    S->bflags = bk.pad;
     S->rr = ResumeRec{};
   }
 #ifdef GOME_STAMPS
@@ -1303,7 +1308,7 @@ __global__ __launch_bounds__(64) void k_match_hot(Dev D, BatchArgs B, PendEnt* p
     rp[0] = v4(rr.valid, rr.next, rr.rest, rr.oid);
     rp[1] = v4(rr.uuid, rr.side, 0u, 0u);  // pad0, pad1
     rp[2] = v4(lo32(rr.price), hi32(rr.price), lo32(rr.vol), hi32(rr.vol));
-    *(GOME_GLB v4u*)(&gp(E.books)[H.sym]) = v4(base, H.nl, cap, 0u);
+    *(GOME_GLB v4u*)(&gp(E.books)[H.sym]) = v4(base, H.nl, cap, S->bflags);
     GOME_GLB unsigned long long* c = gp(E.st)->ctr;
     const long long resting = static_cast<long long>(H.rests) - H.pops - H.cancels;
     auto add = [&](int i, long long v) { if (v) G_ADD(&c[i], static_cast<unsigned long long>(v)); };

@@ -19,6 +19,14 @@ __device__ __forceinline__ int64_t rl64(int64_t v, uint32_t j) {
 }
 __device__ __forceinline__ int64_t uni64(int64_t v) { return rl64(v, __builtin_amdgcn_readfirstlane(lane_id())); }
 
+// v_writelane_b32: replace lane l of `reg` with the uniform value v (no exec masking).
+// HIP exposes no builtin for it; bind the LLVM intrinsic so the compiler sees (and
+// hazard-checks) a real v_writelane.
+__device__ int gome_writelane_i32(int val, int lane, int old) __asm("llvm.amdgcn.writelane.i32");
+__device__ __forceinline__ uint32_t wl_u32(uint32_t reg, uint32_t v, uint32_t l) {
+  return static_cast<uint32_t>(gome_writelane_i32(static_cast<int>(v), static_cast<int>(l), static_cast<int>(reg)));
+}
+
 // Inclusive scan of a 64-bit value over the whole wave (LDS-crossbar shuffles).
 __device__ __forceinline__ int64_t wave_incl_scan(int64_t x) {
   const uint32_t lane = lane_id();

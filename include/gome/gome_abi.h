@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define GOME_ABI_VERSION 1u
+#define GOME_ABI_VERSION 2u
 
 /* ---- status codes (replace the reference's swallowed errors / panics,
  *      rabbitmq.go:44-49,70-72,120-122; nodelink.go:132,142,157) ---------- */
@@ -118,6 +118,10 @@ typedef struct gome_node {
   uint8_t pad[7];
 } gome_node;
 
+/* gome_config.flags: apply every hot book with the legacy one-wave FIFO kernel instead of
+ * the flow path (same results; for A/B measurement and parity cross-checks). */
+#define GOME_FLAG_LEGACY_HOT 1u
+
 typedef struct gome_config {
   uint32_t accuracy;       /* gomengine.accuracy (config.yaml.example:23-24), default 8 */
   int32_t device;          /* HIP device ordinal (one handle per GPU)                    */
@@ -126,7 +130,7 @@ typedef struct gome_config {
   uint64_t max_nodes;      /* resting-order capacity (node pool)                         */
   uint64_t max_levels;     /* level-record capacity (all books)                          */
   uint64_t max_events;     /* event capacity per batch (0: derived from max_batch)       */
-  uint32_t flags;          /* reserved, 0                                                */
+  uint32_t flags;          /* GOME_FLAG_* (0 = defaults)                                 */
   uint32_t pad;
 } gome_config;
 
@@ -145,6 +149,10 @@ typedef struct gome_stats {
   uint64_t n_hot;                             /* books applied by k_match_hot            */
   uint64_t n_hot_orders, n_hot_fills;         /* work done inside k_match_hot (roofline   */
   uint64_t n_hot_rests, n_hot_cancels;        /* numerator of the hot kernel)             */
+  uint64_t n_flow_books;                      /* hot books applied by the flow path       */
+  uint64_t n_flow_orders, n_flow_touches;     /* their orders / level touches (plan log)  */
+  double ms_flow_plan;                        /* device time of k_flow_plan (the serial
+                                                 plan of the flow books)                  */
 } gome_stats;
 
 typedef struct gome_engine gome_engine;

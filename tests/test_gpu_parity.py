@@ -246,3 +246,125 @@ def test_engine_reproduces_golden(fx):
     out, state = replay_fixture(fx, _EngineBackend)
     assert out == fx["results"]
     assert state == fx["state"]
+
+
+# ---- flow path (match_flow.h): hot ADD-only books via the serial aggregate plan ----------
+def _engine_flags(max_symbols, max_batch, flags, max_nodes=1 << 20, max_levels=1 << 20):
+    return Engine(max_symbols=max_symbols, max_batch=max_batch, max_nodes=max_nodes,
+                  max_levels=max_levels, flags=flags)
+
+
+def test_flow_path_taken_and_exact_single_symbol():
+    st = wl.Stream(1, seed=77)
+    batches = [st.batch(30000) for _ in range(4)]
+    eng, orc = _run_pair(batches, 1, sample_syms=[0])
+    s = eng.stats()
+    assert s["n_flow_books"] == 1 and s["n_flow_orders"] == 30000
+    assert s["n_flow_touches"] >= 30000
+
+
+def test_flow_zipf_hot_books_with_fifo_state():
+    st = wl.Stream(2000, zipf_s=1.1, seed=8)
+    z = st.zipf
+    batches = [st.batch(1 << 18) for _ in range(3)]
+    hot = [int(z.rank_to_id[r]) for r in (0, 1, 2, 3, 10, 40, 300)]
+    eng, orc = _run_pair(batches, 2000, sample_syms=hot)
+    assert eng.stats()["n_flow_books"] >= 4
+
+
+def test_flow_equals_legacy_hot_kernel():
+    """The same stream through the flow path and the legacy FIFO kernel: identical events
+    and identical book state (FIFOs included)."""
+    from gome_amd.abi import GOME_FLAG_LEGACY_HOT
+    st = wl.Stream(3, seed=19)
+    batches = [st.batch(12000) for _ in range(4)]
+    a = _engine_flags(3, 12000, 0)
+    b = _engine_flags(3, 12000, GOME_FLAG_LEGACY_HOT)
+    for bt in batches:
+        a.submit(bt)
+        b.submit(bt)
+        _cmp_events(a.drain(), b.drain(), "flow vs legacy")
+        assert a.stats()["n_flow_books"] == 3 and b.stats()["n_flow_books"] == 0
+    for s in range(3):
+        assert np.array_equal(a.levels(s), b.levels(s))
+        for p in b.levels(s)["price_fx"]:
+            assert np.array_equal(a.fifo(s, int(p)), b.fifo(s, int(p)))
+
+
+def test_flow_then_cancels_then_flow():
+    """Book state handed between paths: ADD-only batches (flow), cancel-heavy batches
+    (legacy hot kernel: DELs are not flow-eligible), then ADD-only again."""
+    rng = np.random.default_rng(99)
+    st = wl.Stream(2, seed=99)
+    adds1 = [st.batch(8000) for _ in range(2)]
+    eng = _engine(2, 16000)
+    orc = Oracle(2)
+    for b in adds1:
+        eng.submit(b)
+        _cmp_events(eng.drain(), orc.submit(b), "adds1")
+        assert eng.stats()["n_flow_books"] == 2
+    # cancel half of the resting book (correct sides/prices), plus new adds
+    resting = []
+    for s in range(2):
+        for lv in orc.levels(s):
+            for nd in orc.fifo(s, int(lv["price_fx"])):
+                resting.append((s, int(lv["price_fx"]), int(nd["oid_id"]), int(nd["uuid_id"]), int(nd["side"])))
+    rng.shuffle(resting)
+    dels = np.zeros(len(resting) // 2, wl.ORDER_DTYPE)
+    for i, (s, p, o, u, sd) in enumerate(resting[: len(dels)]):
+        dels[i] = (p, 10**6, s, o, u, sd, 2, 0)
+    mix = np.concatenate([dels, st.batch(4000)])
+    eng.submit(mix)
+    _cmp_events(eng.drain(), orc.submit(mix), "cancel batch")
+    assert eng.stats()["n_flow_books"] == 0
+    for b in [st.batch(8000) for _ in range(2)]:
+        eng.submit(b)
+        _cmp_events(eng.drain(), orc.submit(b), "adds2")
+        assert eng.stats()["n_flow_books"] == 2
+    for s in range(2):
+        assert np.array_equal(eng.levels(s), orc.levels(s))
+        for p in orc.levels(s)["price_fx"]:
+            assert np.array_equal(eng.fifo(s, int(p)), orc.fifo(s, int(p)))
+
+
+def test_flow_declines_quirky_book():
+    """A wrong-side cancel (Q2) marks the book; its later ADD-only batches stay on the
+    legacy kernel (the aggregate plan cannot express shared-price FIFOs)."""
+    st = wl.Stream(1, seed=5)
+    eng = _engine(1, 8192)
+    orc = Oracle(1)
+    b = st.batch(4000)
+    eng.submit(b)
+    _cmp_events(eng.drain(), orc.submit(b))
+    lv = orc.levels(0)[0]
+    nd = orc.fifo(0, int(lv["price_fx"]))[0]
+    q2 = np.zeros(1, wl.ORDER_DTYPE)
+    q2[0] = (int(lv["price_fx"]), 10**6, 0, int(nd["oid_id"]), int(nd["uuid_id"]), 1 - int(nd["side"]), 2, 0)
+    eng.submit(q2)
+    _cmp_events(eng.drain(), orc.submit(q2))
+    b = st.batch(4000)
+    eng.submit(b)
+    _cmp_events(eng.drain(), orc.submit(b))
+    assert eng.stats()["n_flow_books"] == 0
+    assert np.array_equal(eng.levels(0), orc.levels(0))
+
+
+def test_flow_sweeps_and_long_chains_vs_legacy_counts():
+    """Aggressive sweeps over few levels with deep FIFOs (many chunks consumed per batch)."""
+    rng = np.random.default_rng(12)
+    n = 90000
+    rec = np.zeros(n, wl.ORDER_DTYPE)
+    rec["symbol_id"] = 0
+    rec["side"] = rng.integers(0, 2, n)
+    base = np.where(rec["side"] == 0, rng.integers(40, 50, n), rng.integers(51, 61, n))
+    big = rng.random(n) < 0.08
+    base[big & (rec["side"] == 0)] = 70
+    base[big & (rec["side"] == 1)] = 30
+    rec["price_fx"] = base * 10**6
+    rec["volume_fx"] = rng.integers(1, 30, n) * 10**6
+    rec["volume_fx"][big] = rng.integers(100, 3000, big.sum()) * 10**6
+    rec["action"] = 1
+    rec["uuid_id"] = 3
+    rec["oid_id"] = np.arange(1, n + 1)
+    eng, orc = _run_pair(wl.split_batches(rec, 30000), 1, sample_syms=[0])
+    assert eng.stats()["n_flow_books"] == 1

@@ -49,6 +49,12 @@ def hot_algorithmic_bytes(st: dict) -> int:
             + 24 * st["n_hot_fills"] + 40 * st["n_hot_cancels"])
 
 
+def plan_algorithmic_bytes(st: dict) -> int:
+    """Bytes k_flow_plan must move per launch: one 8-B packed record read
+    per order of the flow books, one 16-B touch written per level an order visits."""
+    return 8 * st["n_flow_orders"] + 16 * st["n_flow_touches"]
+
+
 def shard_stream(n_symbols, zipf_s, rank, world, seed):
     """Generator of this rank's share of the global Zipf stream (conditional sampling
     over the ranks this GPU owns; equal in law to filtering the global stream)."""
@@ -194,8 +200,15 @@ def main():
     ms_match = sum(s["ms_match"] for s in sts) / steps
     ms_total = sum(s["ms_total"] for s in sts) / steps
     balg = sum(algorithmic_bytes(s) for s in sts) / steps
-    ms_hot = sum(s["ms_hot"] for s in sts) / steps
-    bhot = sum(hot_algorithmic_bytes(s) for s in sts) / steps
+    flow = sum(s["n_flow_books"] for s in sts) > 0
+    if flow:  # the flow path's serial plan is the dominant kernel
+        kname = "k_flow_plan (serial aggregate plan of the flow books)"
+        ms_hot = sum(s["ms_flow_plan"] for s in sts) / steps
+        bhot = sum(plan_algorithmic_bytes(s) for s in sts) / steps
+    else:
+        kname = "k_match_hot (match_books, hot books)"
+        ms_hot = sum(s["ms_hot"] for s in sts) / steps
+        bhot = sum(hot_algorithmic_bytes(s) for s in sts) / steps
     max_seg = max(s["max_segment"] for s in sts)
     if world > 1:
         orders, fills, events, elapsed, lat = combine_ranks(orders, fills, events, elapsed, lat, "cuda")
@@ -211,7 +224,7 @@ def main():
     if os.path.exists(args.traffic_json):
         try:
             tj = json.load(open(args.traffic_json))
-            traffic = tj.get("k_match_hot_hbm_bytes_per_launch")
+            traffic = tj.get("k_flow_plan_hbm_bytes_per_launch" if flow else "k_match_hot_hbm_bytes_per_launch")
         except (OSError, ValueError):
             traffic = None
 
@@ -248,7 +261,7 @@ def main():
                          "ns_per_order": round(ms_hot * 1e6 / max(max_seg, 1), 1)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6),
-                         "traffic": traffic, "kernel": "k_match_hot (match_books, hot books)",
+                         "traffic": traffic, "kernel": kname,
                          "kernel_ms": round(ms_hot, 3), "alg_bytes_per_launch": int(bhot),
                          "match_phase_alg_bytes": int(balg)},
             "cpu_baseline": cpu,

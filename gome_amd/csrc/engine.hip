@@ -253,7 +253,7 @@ gome_status gome_engine::init(const gome_config& c) {
   F.ig_cap = static_cast<uint32_t>(std::min<uint64_t>(std::max<uint64_t>(cfg.max_nodes, 1u << 16), 0xF0000000ull));
   F.enabled = (cfg.flags & GOME_FLAG_LEGACY_HOT) ? 0u : 1u;
   if (!alloc(&F.hdr, MAX_HOT, "flow headers") || !alloc(&F.lvl, MAX_HOT * FL_CAP, "flow levels") ||
-      !alloc(&F.ord8, nb, "flow records") || !alloc(&F.log, ntouch, "flow touch log") ||
+      !alloc(&F.ord8, nb + 16, "flow records") || !alloc(&F.log, ntouch, "flow touch log") ||
       !alloc(&F.srt, ntouch, "flow level runs") || !alloc(&F.rs, ntouch, "flow new makers") ||
       !alloc(&F.fbase, ntouch, "flow fill bases") || !alloc(&F.ig, F.ig_cap, "flow gathered makers") ||
       !alloc(&F.ig_bump, 1, "flow gather bump"))
@@ -362,7 +362,7 @@ gome_status gome_engine::run(const gome_order* d_ord, uint32_t n, hipStream_t s)
   HIPCHK(hipEventRecord(evf0, flow_stream));
   k_flow_plan<<<nhot_max, 64, 0, flow_stream>>>(D, F);
   HIPCHK(hipEventRecord(evf1, flow_stream));
-  k_flow_scatter<<<dim3(64, nhot_max), 256, 0, flow_stream>>>(D, F);
+  k_flow_sort<<<nhot_max, FL_SORT_T, 0, flow_stream>>>(D, F);
   k_flow_level<<<dim3(FL_CAP, nhot_max), 64, 0, flow_stream>>>(D, F);
   k_flow_count<<<dim3(64, nhot_max), 256, 0, flow_stream>>>(D, B, F);
   k_flow_write<<<nhot_max, FL_WRITE_T, 0, flow_stream>>>(D, B, F);

@@ -17,9 +17,11 @@
 //                  price set (<= FL_CAP levels) and one packed 8-B record per order
 //                  {volume, level index, side}.
 //   k_flow_plan    (SERIAL, one wave per book) the aggregate state machine: depths in lane
-//                  registers, membership as scalar bit masks; per order it logs one 16-B
-//                  "touch" per level it rests at / consumes from, with the level-local rank.
-//   k_flow_scatter (parallel) touches -> per-level runs (rank gives the slot: no sort).
+//                  registers, membership as scalar bit masks, orders read through the
+//                  scalar cache; per order it logs one 16-B "touch" per level it rests at /
+//                  consumes from.  Nothing else is on the serial path.
+//   k_flow_sort    (one workgroup per book) stable counting sort of the touches by level
+//                  -> per-level runs in time order.
 //   k_flow_level   (one wave per level) segmented scans -> volume coordinates of each
 //                  consumption and each new maker; gathers the consumed prefix of the
 //                  level's resting FIFO (chunk chain), frees consumed chunks, erases their
@@ -47,9 +49,11 @@
 
 namespace gome {
 
-constexpr uint32_t FL_CAP = 128;          // levels per flow book (two lane sets)
+constexpr uint32_t FL_CAP = 128;          // level slots per flow book (two lane sets)
+constexpr uint32_t FL_MAX = FL_CAP - 2;   // usable levels 1..126: slot 0 is the bid sentinel,
+                                          // slot 127 the ask sentinel (bit scans never miss)
 constexpr uint32_t FL_HASH = 1024;        // LDS price-set slots in k_flow_prep
-constexpr uint32_t FL_PREP_T = 256;
+constexpr uint32_t FL_PREP_T = 1024;
 constexpr uint32_t FL_TOUCH_MUL = 4;      // log capacity per order (touches <= 3n + L0)
 constexpr unsigned long long FL_KEY_OFF = 1ull << 62;
 
@@ -59,10 +63,11 @@ constexpr uint32_t OR_LI_SHIFT = 21, OR_SELL = 1u << 28, OR_SKIP = 1u << 29;
 enum : uint32_t { TK_CONS = 0, TK_REST = 1 };
 
 struct Touch {       // one level visited by one order (16 B)
-  uint32_t j;        // order index within the segment
-  uint32_t kr;       // level [0,7) | kind << 7 | rank within the level << 8
+  uint32_t kr;       // level [0,7) | kind << 7 | order index within the segment << 8
+  uint32_t pos;      // position in the level-sorted runs (set by k_flow_sort)
   int64_t amt;       // volume taken from the level (CONS) or rested at it (REST)
 };
+__device__ __forceinline__ uint32_t tk_j(const Touch& x) { return x.kr >> 8; }
 static_assert(sizeof(Touch) == 16, "Touch layout");
 
 struct SEnt {        // a touch in its level's run (32 B)
@@ -162,7 +167,7 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep(Dev D, BatchArgs B, Flo
       const unsigned long long prev = atomicCAS(&hkey[s], 0ull, key);
       if (prev == 0ull) {
         if (val != NIL) hval[s] = val;
-        if (atomicAdd(&ndist, 1u) >= FL_CAP) bad = 1;
+        if (atomicAdd(&ndist, 1u) >= FL_MAX) bad = 1;
         return;
       }
       if (prev == key) {
@@ -205,7 +210,7 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep(Dev D, BatchArgs B, Flo
   if (my_adds) atomicAdd(&adds, my_adds);
   if (my_drop) atomicAdd(&dropped, my_drop);
   __syncthreads();
-  if (bad || ndist > FL_CAP) {
+  if (bad || ndist > FL_MAX) {
     if (tid == 0) hd->ok = 0;
     return;
   }
@@ -240,8 +245,8 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep(Dev D, BatchArgs B, Flo
       f.tslot = x.tslot;
       f.mem0 = x.member;
     }
-    LV[r] = f;
-    hval[s] = r;  // the slot now maps price -> level index (each slot has one owner thread)
+    LV[r + 1] = f;
+    hval[s] = r + 1;  // the slot now maps price -> level index (each slot has one owner thread)
   }
   __syncthreads();
   for (uint32_t b = beg + tid; b < end; b += FL_PREP_T) {
@@ -274,15 +279,271 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep(Dev D, BatchArgs B, Flo
 }
 
 // ============================================================== k_flow_plan (serial)
-// One wave per flow book.  Lane l holds the depth of level l (D0) and l + 64 (D1), and the
-// number of touches logged at it so far (C0, C1); S:SALE / S:BUY membership are 128-bit
-// scalar masks (A, Bm).  Per order: GetReverseDepth = mask AND, best level = bit scan,
-// MatchOrder at the aggregate level = compare + subtract, rest = add + set bit.  Touches
-// are staged in lane registers (lane = slot) and stored 64 at a time.
-__device__ __forceinline__ int64_t fl_get(int64_t D0, int64_t D1, uint32_t k) {
-  const int64_t a = rl64(D0, k & 63u), b = rl64(D1, k & 63u);
-  return k < 64 ? a : b;
+// One wave per flow book; everything per order is wave-uniform (SALU + lane reads/writes):
+//   * depth of level k: lane k % 64 of the 64-bit lane pair D[k / 64] (two register sets);
+//   * S:SALE / S:BUY membership: 128-bit scalar masks A, Bm.  Slot 127 is a permanent ask
+//     and slot 0 a permanent bid (sentinels), so "best opposite level" is one bit scan and
+//     "does it cross" one compare, with no emptiness test;
+//   * orders: 8-B packed records read 8 at a time through the scalar cache (s_load_dwordx16,
+//     prefetched one group ahead), so no vector-memory wait sits on the order path;
+//   * the log: lane `nacc` of four staging VGPRs per touch (v_writelane), stored 64 touches
+//     at a time (fire and forget: nothing on the path ever waits for vector memory).
+typedef const __attribute__((address_space(4))) unsigned long long* fl_cptr;
+struct alignas(64) FlGroup {
+  unsigned long long o[8];
+};
+
+// r = a - b on 64-bit scalars; returns the borrow (a < b, unsigned) from SCC.
+__device__ __forceinline__ uint32_t fl_sub64(uint32_t alo, uint32_t ahi, uint32_t blo, uint32_t bhi,
+                                             uint32_t& rlo, uint32_t& rhi) {
+  uint32_t br;
+  asm volatile("s_sub_u32 %0, %3, %5\n\ts_subb_u32 %1, %4, %6\n\ts_cselect_b32 %2, 1, 0"
+               : "=&s"(rlo), "=&s"(rhi), "=&s"(br)
+               : "s"(alo), "s"(ahi), "s"(blo), "s"(bhi)
+               : "scc");
+  return br;
 }
+
+// r = a + b on 64-bit scalars.
+__device__ __forceinline__ void fl_add64(uint32_t alo, uint32_t ahi, uint32_t blo, uint32_t bhi,
+                                         uint32_t& rlo, uint32_t& rhi) {
+  asm volatile("s_add_u32 %0, %2, %4\n\ts_addc_u32 %1, %3, %5"
+               : "=&s"(rlo), "=&s"(rhi)
+               : "s"(alo), "s"(ahi), "s"(blo), "s"(bhi)
+               : "scc");
+}
+
+struct FlDepth {  // depths of levels 0..127 as four 32-bit lane registers
+  uint32_t l0, h0, l1, h1;
+};
+
+// Read level k; old values of lane k % 64 of both sets are returned for the write-back.
+__device__ __forceinline__ void fl_dget(const FlDepth& D, uint32_t k, uint32_t& lo, uint32_t& hi, uint32_t (&o)[4]) {
+  const uint32_t kl = k & 63u;
+  o[0] = rl(D.l0, kl);
+  o[1] = rl(D.h0, kl);
+  o[2] = rl(D.l1, kl);
+  o[3] = rl(D.h1, kl);
+  lo = k < 64 ? o[0] : o[2];
+  hi = k < 64 ? o[1] : o[3];
+}
+
+// Write level k (the other set's lane gets its old value back: no branch, no exec mask).
+__device__ __forceinline__ void fl_dset(FlDepth& D, uint32_t k, uint32_t lo, uint32_t hi, const uint32_t (&o)[4]) {
+  const uint32_t kl = k & 63u;
+  const bool s0 = k < 64;
+  D.l0 = wl_u32(D.l0, s0 ? lo : o[0], kl);
+  D.h0 = wl_u32(D.h0, s0 ? hi : o[1], kl);
+  D.l1 = wl_u32(D.l1, s0 ? o[2] : lo, kl);
+  D.h1 = wl_u32(D.h1, s0 ? o[3] : hi, kl);
+}
+
+__device__ __forceinline__ uint32_t fl_lowest(unsigned long long m0, unsigned long long m1) {
+  return m0 ? static_cast<uint32_t>(__builtin_ctzll(m0)) : 64u + static_cast<uint32_t>(__builtin_ctzll(m1));
+}
+__device__ __forceinline__ uint32_t fl_highest(unsigned long long m0, unsigned long long m1) {
+  return m1 ? 127u - static_cast<uint32_t>(__builtin_clzll(m1)) : 63u - static_cast<uint32_t>(__builtin_clzll(m0));
+}
+
+struct FlLog {
+  uint32_t lk, la, lb, pad;  // staging lanes
+  uint32_t nacc, lpos, lcap;
+  GOME_GLB v4u* p;
+};
+
+// One order of the plan as a single SALU/lane-register block (no compiler phi copies, no
+// VALU compares).  In: T (tlo:thi) > 0, li, side bit in xhi, order index jj.  Runs the
+// reference's SetOrder at the aggregate level (engine.go:56-85): sweep the crossing
+// opposite levels best first (full: depth 0 + ZREM, partial: depth - T), then rest T at li
+// (depth + T, ZADD own side).  Logs one touch per level.  Returns with T == 0 when the order
+// is done, or with T > 0 when the 64-touch staging filled mid-sweep (the caller stores it
+// and calls again: the sweep resumes from the updated state).
+#define FL_STEP_ASM                                                                        \
+  "s_bitcmp1_b32 %[xhi], 28\n\t"                                                           \
+  "s_cbranch_scc1 SELL_%=\n\t"                                                             \
+  "BUY_LOOP_%=:\n\t"                                                                       \
+  "s_ff1_i32_b64 %[k], %[A0]\n\t"                                                          \
+  "s_ff1_i32_b64 %[t0], %[A1]\n\t"                                                         \
+  "s_add_u32 %[t0], %[t0], 64\n\t"                                                         \
+  "s_cmp_lg_u64 %[A0], 0\n\t"                                                              \
+  "s_cselect_b32 %[k], %[k], %[t0]\n\t"                                                    \
+  "s_cmp_gt_u32 %[k], %[li]\n\t"                                                           \
+  "s_cbranch_scc1 BUY_REST_%=\n\t"                                                         \
+  "s_and_b32 %[kl], %[k], 63\n\t"                                                          \
+  "v_readlane_b32 %[o0], %[dl0], %[kl]\n\t"                                                \
+  "v_readlane_b32 %[o1], %[dh0], %[kl]\n\t"                                                \
+  "v_readlane_b32 %[o2], %[dl1], %[kl]\n\t"                                                \
+  "v_readlane_b32 %[o3], %[dh1], %[kl]\n\t"                                                \
+  "s_cmp_lt_u32 %[k], 64\n\t"                                                              \
+  "s_cselect_b32 %[dlo], %[o0], %[o2]\n\t"                                                 \
+  "s_cselect_b32 %[dhi], %[o1], %[o3]\n\t"                                                 \
+  "s_sub_u32 %[rlo], %[tlo], %[dlo]\n\t"                                                   \
+  "s_subb_u32 %[rhi], %[thi], %[dhi]\n\t"                                                  \
+  "s_cbranch_scc1 BUY_PART_%=\n\t"                                                         \
+  "s_cmp_lt_u32 %[k], 64\n\t"                                                              \
+  "s_cselect_b32 %[o0], 0, %[o0]\n\t"                                                      \
+  "s_cselect_b32 %[o1], 0, %[o1]\n\t"                                                      \
+  "s_cselect_b32 %[o2], %[o2], 0\n\t"                                                      \
+  "s_cselect_b32 %[o3], %[o3], 0\n\t"                                                      \
+  "s_mov_b32 m0, %[kl]\n\t"                                                             \
+  "v_writelane_b32 %[dl0], %[o0], m0\n\t"                                               \
+  "v_writelane_b32 %[dh0], %[o1], m0\n\t"                                               \
+  "v_writelane_b32 %[dl1], %[o2], m0\n\t"                                               \
+  "v_writelane_b32 %[dh1], %[o3], m0\n\t"                                               \
+  "s_cmp_lt_u32 %[k], 64\n\t"                                                              \
+  "s_cselect_b64 %[m], %[A0], %[A1]\n\t"                                                    \
+  "s_bitset0_b64 %[m], %[k]\n\t"                                                                   \
+  "s_cmp_lt_u32 %[k], 64\n\t"                                                              \
+  "s_cselect_b64 %[A0], %[m], %[A0]\n\t"                                                    \
+  "s_cselect_b64 %[A1], %[A1], %[m]\n\t"                                                    \
+  "s_or_b32 %[t0], %[jjs], %[k]\n\t"                                                       \
+  "s_mov_b32 m0, %[nacc]\n\t"                                                           \
+  "v_writelane_b32 %[lk], %[t0], m0\n\t"                                              \
+  "v_writelane_b32 %[la], %[dlo], m0\n\t"                                             \
+  "v_writelane_b32 %[lb], %[dhi], m0\n\t"                                             \
+  "s_add_u32 %[nacc], %[nacc], 1\n\t"                                                      \
+  "s_mov_b32 %[tlo], %[rlo]\n\t"                                                           \
+  "s_mov_b32 %[thi], %[rhi]\n\t"                                                           \
+  "s_or_b32 %[t0], %[rlo], %[rhi]\n\t"                                                     \
+  "s_cbranch_scc0 DONE_%=\n\t"                                                             \
+  "s_cmp_eq_u32 %[nacc], 64\n\t"                                                           \
+  "s_cbranch_scc1 DONE_%=\n\t"                                                             \
+  "s_branch BUY_LOOP_%=\n\t"                                                               \
+  "BUY_PART_%=:\n\t"                                                                       \
+  "s_sub_u32 %[rlo], %[dlo], %[tlo]\n\t"                                                   \
+  "s_subb_u32 %[rhi], %[dhi], %[thi]\n\t"                                                  \
+  "s_cmp_lt_u32 %[k], 64\n\t"                                                              \
+  "s_cselect_b32 %[o0], %[rlo], %[o0]\n\t"                                                 \
+  "s_cselect_b32 %[o1], %[rhi], %[o1]\n\t"                                                 \
+  "s_cselect_b32 %[o2], %[o2], %[rlo]\n\t"                                                 \
+  "s_cselect_b32 %[o3], %[o3], %[rhi]\n\t"                                                 \
+  "s_branch PART_TAIL_%=\n\t"                                                              \
+  "BUY_REST_%=:\n\t"                                                                       \
+  "s_and_b32 %[kl], %[li], 63\n\t"                                                         \
+  "v_readlane_b32 %[o0], %[dl0], %[kl]\n\t"                                                \
+  "v_readlane_b32 %[o1], %[dh0], %[kl]\n\t"                                                \
+  "v_readlane_b32 %[o2], %[dl1], %[kl]\n\t"                                                \
+  "v_readlane_b32 %[o3], %[dh1], %[kl]\n\t"                                                \
+  "s_cmp_lt_u32 %[li], 64\n\t"                                                              \
+  "s_cselect_b64 %[m], %[B0], %[B1]\n\t"                                                    \
+  "s_bitset1_b64 %[m], %[li]\n\t"                                                                   \
+  "s_cmp_lt_u32 %[li], 64\n\t"                                                              \
+  "s_cselect_b64 %[B0], %[m], %[B0]\n\t"                                                    \
+  "s_cselect_b64 %[B1], %[B1], %[m]\n\t"                                                    \
+  "s_branch REST_TAIL_%=\n\t"                                                              \
+  "SELL_%=:\n\t"                                                                           \
+  "SELL_LOOP_%=:\n\t"                                                                      \
+  "s_flbit_i32_b64 %[k], %[B0]\n\t"                                                        \
+  "s_sub_u32 %[k], 63, %[k]\n\t"                                                           \
+  "s_flbit_i32_b64 %[t0], %[B1]\n\t"                                                       \
+  "s_sub_u32 %[t0], 127, %[t0]\n\t"                                                        \
+  "s_cmp_lg_u64 %[B1], 0\n\t"                                                              \
+  "s_cselect_b32 %[k], %[t0], %[k]\n\t"                                                    \
+  "s_cmp_lt_u32 %[k], %[li]\n\t"                                                           \
+  "s_cbranch_scc1 SELL_REST_%=\n\t"                                                        \
+  "s_and_b32 %[kl], %[k], 63\n\t"                                                          \
+  "v_readlane_b32 %[o0], %[dl0], %[kl]\n\t"                                                \
+  "v_readlane_b32 %[o1], %[dh0], %[kl]\n\t"                                                \
+  "v_readlane_b32 %[o2], %[dl1], %[kl]\n\t"                                                \
+  "v_readlane_b32 %[o3], %[dh1], %[kl]\n\t"                                                \
+  "s_cmp_lt_u32 %[k], 64\n\t"                                                              \
+  "s_cselect_b32 %[dlo], %[o0], %[o2]\n\t"                                                 \
+  "s_cselect_b32 %[dhi], %[o1], %[o3]\n\t"                                                 \
+  "s_sub_u32 %[rlo], %[tlo], %[dlo]\n\t"                                                   \
+  "s_subb_u32 %[rhi], %[thi], %[dhi]\n\t"                                                  \
+  "s_cbranch_scc1 SELL_PART_%=\n\t"                                                        \
+  "s_cmp_lt_u32 %[k], 64\n\t"                                                              \
+  "s_cselect_b32 %[o0], 0, %[o0]\n\t"                                                      \
+  "s_cselect_b32 %[o1], 0, %[o1]\n\t"                                                      \
+  "s_cselect_b32 %[o2], %[o2], 0\n\t"                                                      \
+  "s_cselect_b32 %[o3], %[o3], 0\n\t"                                                      \
+  "s_mov_b32 m0, %[kl]\n\t"                                                             \
+  "v_writelane_b32 %[dl0], %[o0], m0\n\t"                                               \
+  "v_writelane_b32 %[dh0], %[o1], m0\n\t"                                               \
+  "v_writelane_b32 %[dl1], %[o2], m0\n\t"                                               \
+  "v_writelane_b32 %[dh1], %[o3], m0\n\t"                                               \
+  "s_cmp_lt_u32 %[k], 64\n\t"                                                              \
+  "s_cselect_b64 %[m], %[B0], %[B1]\n\t"                                                    \
+  "s_bitset0_b64 %[m], %[k]\n\t"                                                                   \
+  "s_cmp_lt_u32 %[k], 64\n\t"                                                              \
+  "s_cselect_b64 %[B0], %[m], %[B0]\n\t"                                                    \
+  "s_cselect_b64 %[B1], %[B1], %[m]\n\t"                                                    \
+  "s_or_b32 %[t0], %[jjs], %[k]\n\t"                                                       \
+  "s_mov_b32 m0, %[nacc]\n\t"                                                           \
+  "v_writelane_b32 %[lk], %[t0], m0\n\t"                                              \
+  "v_writelane_b32 %[la], %[dlo], m0\n\t"                                             \
+  "v_writelane_b32 %[lb], %[dhi], m0\n\t"                                             \
+  "s_add_u32 %[nacc], %[nacc], 1\n\t"                                                      \
+  "s_mov_b32 %[tlo], %[rlo]\n\t"                                                           \
+  "s_mov_b32 %[thi], %[rhi]\n\t"                                                           \
+  "s_or_b32 %[t0], %[rlo], %[rhi]\n\t"                                                     \
+  "s_cbranch_scc0 DONE_%=\n\t"                                                             \
+  "s_cmp_eq_u32 %[nacc], 64\n\t"                                                           \
+  "s_cbranch_scc1 DONE_%=\n\t"                                                             \
+  "s_branch SELL_LOOP_%=\n\t"                                                              \
+  "SELL_PART_%=:\n\t"                                                                      \
+  "s_sub_u32 %[rlo], %[dlo], %[tlo]\n\t"                                                   \
+  "s_subb_u32 %[rhi], %[dhi], %[thi]\n\t"                                                  \
+  "s_cmp_lt_u32 %[k], 64\n\t"                                                              \
+  "s_cselect_b32 %[o0], %[rlo], %[o0]\n\t"                                                 \
+  "s_cselect_b32 %[o1], %[rhi], %[o1]\n\t"                                                 \
+  "s_cselect_b32 %[o2], %[o2], %[rlo]\n\t"                                                 \
+  "s_cselect_b32 %[o3], %[o3], %[rhi]\n\t"                                                 \
+  "PART_TAIL_%=:\n\t"                                                                      \
+  "s_mov_b32 m0, %[kl]\n\t"                                                             \
+  "v_writelane_b32 %[dl0], %[o0], m0\n\t"                                               \
+  "v_writelane_b32 %[dh0], %[o1], m0\n\t"                                               \
+  "v_writelane_b32 %[dl1], %[o2], m0\n\t"                                               \
+  "v_writelane_b32 %[dh1], %[o3], m0\n\t"                                               \
+  "s_or_b32 %[t0], %[jjs], %[k]\n\t"                                                       \
+  "s_mov_b32 m0, %[nacc]\n\t"                                                           \
+  "v_writelane_b32 %[lk], %[t0], m0\n\t"                                              \
+  "v_writelane_b32 %[la], %[tlo], m0\n\t"                                             \
+  "v_writelane_b32 %[lb], %[thi], m0\n\t"                                             \
+  "s_add_u32 %[nacc], %[nacc], 1\n\t"                                                      \
+  "s_mov_b32 %[tlo], 0\n\t"                                                                \
+  "s_mov_b32 %[thi], 0\n\t"                                                                \
+  "s_branch DONE_%=\n\t"                                                                   \
+  "SELL_REST_%=:\n\t"                                                                      \
+  "s_and_b32 %[kl], %[li], 63\n\t"                                                         \
+  "v_readlane_b32 %[o0], %[dl0], %[kl]\n\t"                                                \
+  "v_readlane_b32 %[o1], %[dh0], %[kl]\n\t"                                                \
+  "v_readlane_b32 %[o2], %[dl1], %[kl]\n\t"                                                \
+  "v_readlane_b32 %[o3], %[dh1], %[kl]\n\t"                                                \
+  "s_cmp_lt_u32 %[li], 64\n\t"                                                              \
+  "s_cselect_b64 %[m], %[A0], %[A1]\n\t"                                                    \
+  "s_bitset1_b64 %[m], %[li]\n\t"                                                                   \
+  "s_cmp_lt_u32 %[li], 64\n\t"                                                              \
+  "s_cselect_b64 %[A0], %[m], %[A0]\n\t"                                                    \
+  "s_cselect_b64 %[A1], %[A1], %[m]\n\t"                                                    \
+  "REST_TAIL_%=:\n\t"                                                                      \
+  "s_cmp_lt_u32 %[li], 64\n\t"                                                             \
+  "s_cselect_b32 %[dlo], %[o0], %[o2]\n\t"                                                 \
+  "s_cselect_b32 %[dhi], %[o1], %[o3]\n\t"                                                 \
+  "s_add_u32 %[dlo], %[dlo], %[tlo]\n\t"                                                   \
+  "s_addc_u32 %[dhi], %[dhi], %[thi]\n\t"                                                  \
+  "s_cmp_lt_u32 %[li], 64\n\t"                                                             \
+  "s_cselect_b32 %[o0], %[dlo], %[o0]\n\t"                                                 \
+  "s_cselect_b32 %[o1], %[dhi], %[o1]\n\t"                                                 \
+  "s_cselect_b32 %[o2], %[o2], %[dlo]\n\t"                                                 \
+  "s_cselect_b32 %[o3], %[o3], %[dhi]\n\t"                                                 \
+  "s_mov_b32 m0, %[kl]\n\t"                                                             \
+  "v_writelane_b32 %[dl0], %[o0], m0\n\t"                                               \
+  "v_writelane_b32 %[dh0], %[o1], m0\n\t"                                               \
+  "v_writelane_b32 %[dl1], %[o2], m0\n\t"                                               \
+  "v_writelane_b32 %[dh1], %[o3], m0\n\t"                                               \
+  "s_or_b32 %[t0], %[jjs], %[li]\n\t"                                                      \
+  "s_or_b32 %[t0], %[t0], 128\n\t"                                                         \
+  "s_mov_b32 m0, %[nacc]\n\t"                                                           \
+  "v_writelane_b32 %[lk], %[t0], m0\n\t"                                              \
+  "v_writelane_b32 %[la], %[tlo], m0\n\t"                                             \
+  "v_writelane_b32 %[lb], %[thi], m0\n\t"                                             \
+  "s_add_u32 %[nacc], %[nacc], 1\n\t"                                                      \
+  "s_mov_b32 %[tlo], 0\n\t"                                                                \
+  "s_mov_b32 %[thi], 0\n\t"                                                                \
+  "DONE_%=:\n\t"                                                                           \
+  "s_or_b32 %[more], %[tlo], %[thi]"
+
 
 __global__ __launch_bounds__(64) void k_flow_plan(Dev D, FlowArgs F) {
   const uint32_t h = blockIdx.x;
@@ -293,129 +554,74 @@ __global__ __launch_bounds__(64) void k_flow_plan(Dev D, FlowArgs F) {
   const uint32_t lane = lane_id();
   const uint32_t nl = uni(hd->nl), beg = uni(hd->beg), end = uni(hd->end), n = end - beg;
   FlowLvl* LV = F.lvl + h * FL_CAP;
-  int64_t D0 = lane < nl ? LV[lane].d0 : 0, D1 = lane + 64 < nl ? LV[lane + 64].d0 : 0;
-  const uint32_t m0 = lane < nl ? LV[lane].mem0 : 0u, m1 = lane + 64 < nl ? LV[lane + 64].mem0 : 0u;
-  unsigned long long A0 = __ballot(m0 & M_SALE), A1 = __ballot(m1 & M_SALE);
-  unsigned long long B0 = __ballot(m0 & M_BUY), B1 = __ballot(m1 & M_BUY);
-  uint32_t C0 = 0, C1 = 0;
-  uint32_t lj = 0, lk = 0, la = 0, lb = 0, nacc = 0, lpos = 0, rests = 0;
-  GOME_GLB v4u* logp = (GOME_GLB v4u*)(F.log + FL_TOUCH_MUL * beg);
-  const uint32_t lcap = FL_TOUCH_MUL * n;  // touches <= 3n + levels
-  const unsigned long long* o8 = F.ord8 + beg;
+  const bool v0 = lane >= 1 && lane <= nl, v1 = lane + 64 <= nl;
+  const int64_t d0 = v0 ? LV[lane].d0 : 0, d1 = v1 ? LV[lane + 64].d0 : 0;
+  const uint32_t m0 = v0 ? LV[lane].mem0 : 0u, m1 = v1 ? LV[lane + 64].mem0 : 0u;
+  FlDepth Dp{lo32(d0), hi32(d0), lo32(d1), hi32(d1)};
+  unsigned long long A0 = __ballot(m0 & M_SALE), A1 = __ballot(m1 & M_SALE) | (1ull << 63);
+  unsigned long long B0 = __ballot(m0 & M_BUY) | 1ull, B1 = __ballot(m1 & M_BUY);
 
-  auto touch = [&](uint32_t jj, uint32_t k, uint32_t kind, int64_t amt) {
-    const uint32_t c0 = rl(C0, k & 63u), c1 = rl(C1, k & 63u);
-    const uint32_t rank = k < 64 ? c0 : c1;
-    C0 += (lane == k) ? 1u : 0u;
-    C1 += (lane + 64 == k) ? 1u : 0u;
-    lj = wl_u32(lj, jj, nacc);
-    lk = wl_u32(lk, k | (kind << 7) | (rank << 8), nacc);
-    la = wl_u32(la, lo32(amt), nacc);
-    lb = wl_u32(lb, hi32(amt), nacc);
-    if (++nacc == 64) {
-      if (lpos + 64 <= lcap) logp[lpos + lane] = v4(lj, lk, la, lb);
-      lpos += 64;
-      nacc = 0;
-    }
+  FlLog lg{vreg(0u), vreg(0u), vreg(0u), 0u, 0u, 0u, FL_TOUCH_MUL * n, (GOME_GLB v4u*)(F.log + FL_TOUCH_MUL * beg)};
+  const fl_cptr o8 = (fl_cptr)(F.ord8 + beg);
+  // groups of 8 records at the 64-B aligned address at or below beg (leading ones skipped)
+  const uint32_t skew = beg & 7u;
+  const fl_cptr ob = o8 - skew;
+  const uint32_t ngs = (n + skew + 7) / 8;
+  auto load_group = [&](uint32_t g) {
+    FlGroup r;
+#pragma unroll
+    for (uint32_t i = 0; i < 8; ++i) r.o[i] = ob[8 * g + i];
+    return r;
   };
-  auto setd = [&](uint32_t k, int64_t v) {
-    D0 = (lane == k) ? v : D0;
-    D1 = (lane + 64 == k) ? v : D1;
-  };
-
-  for (uint32_t b0 = 0; b0 < n; b0 += 64) {
-    const uint32_t cnt = min(64u, n - b0);
-    const unsigned long long rec = lane < cnt ? o8[b0 + lane] : (static_cast<unsigned long long>(OR_SKIP) << 32);
-    const uint32_t rlo = static_cast<uint32_t>(rec), rhi = static_cast<uint32_t>(rec >> 32);
-    for (uint32_t j = 0; j < cnt; ++j) {
-      const uint32_t xhi = rl(rhi, j);
+  FlGroup cur = load_group(0), nxt;
+  for (uint32_t g = 0; g < ngs; ++g) {
+#pragma unroll
+    for (uint32_t u = 0; u < 8; ++u) {
+      // Prefetch the next group once this one is in registers (SMEM returns out of order:
+      // any wait is lgkmcnt(0), so the load must not be in flight when cur is first used).
+      if (u == 1) nxt = load_group(g + 1 < ngs ? g + 1 : g);
+      const uint32_t jj = 8 * g + u - skew;  // wraps for the skew records: jj >= n
+      const uint32_t xhi = jj < n ? static_cast<uint32_t>(cur.o[u] >> 32) : OR_SKIP;
       if (xhi & OR_SKIP) continue;
-      const uint32_t jj = b0 + j;
-      int64_t T = static_cast<int64_t>((static_cast<uint64_t>(xhi & 0x1FFFFFu) << 32) | rl(rlo, j));
-      const uint32_t li = (xhi >> OR_LI_SHIFT) & 0x7Fu;
-      if (!(xhi & OR_SELL)) {
-        // BUY: asks at levels <= li, ascending (nodepool.go:86-104)
-        unsigned long long c0 = A0 & (li >= 63 ? ~0ull : ((2ull << li) - 1));
-        unsigned long long c1 = li < 64 ? 0ull : (A1 & (li >= 127 ? ~0ull : ((2ull << (li - 64)) - 1)));
-        while (c0 | c1) {
-          const uint32_t k = c0 ? static_cast<uint32_t>(__builtin_ctzll(c0)) : 64u + static_cast<uint32_t>(__builtin_ctzll(c1));
-          const int64_t d = fl_get(D0, D1, k);
-          if (T < d) {  // partial: the level keeps depth d - T (engine.go:176-194)
-            setd(k, d - T);
-            touch(jj, k, TK_CONS, T);
-            T = 0;
-            break;
-          }
-          setd(k, 0);  // the level empties: ZREM (nodepool.go:76-83)
-          if (k < 64) { A0 &= ~(1ull << k); c0 &= ~(1ull << k); }
-          else { A1 &= ~(1ull << (k - 64)); c1 &= ~(1ull << (k - 64)); }
-          touch(jj, k, TK_CONS, d);
-          T -= d;
-          if (T == 0) break;  // diff == 0: stop (engine.go:162-175)
-        }
-        if (T > 0) {  // rest (engine.go:80-82): depth += T, ZADD S:BUY
-          setd(li, fl_get(D0, D1, li) + T);
-          if (li < 64) B0 |= 1ull << li;
-          else B1 |= 1ull << (li - 64);
-          touch(jj, li, TK_REST, T);
-          rests++;
-        }
-      } else {
-        // SALE: bids at levels >= li, descending (nodepool.go:105-115)
-        unsigned long long c1 = B1 & (li < 64 ? ~0ull : (~0ull << (li - 64)));
-        unsigned long long c0 = li < 64 ? (B0 & (~0ull << li)) : 0ull;
-        while (c0 | c1) {
-          const uint32_t k = c1 ? 64u + 63u - static_cast<uint32_t>(__builtin_clzll(c1))
-                                : 63u - static_cast<uint32_t>(__builtin_clzll(c0));
-          const int64_t d = fl_get(D0, D1, k);
-          if (T < d) {
-            setd(k, d - T);
-            touch(jj, k, TK_CONS, T);
-            T = 0;
-            break;
-          }
-          setd(k, 0);
-          if (k < 64) { B0 &= ~(1ull << k); c0 &= ~(1ull << k); }
-          else { B1 &= ~(1ull << (k - 64)); c1 &= ~(1ull << (k - 64)); }
-          touch(jj, k, TK_CONS, d);
-          T -= d;
-          if (T == 0) break;
-        }
-        if (T > 0) {
-          setd(li, fl_get(D0, D1, li) + T);
-          if (li < 64) A0 |= 1ull << li;
-          else A1 |= 1ull << (li - 64);
-          touch(jj, li, TK_REST, T);
-          rests++;
-        }
+      uint32_t tlo = static_cast<uint32_t>(cur.o[u]), thi = xhi & 0x1FFFFFu;
+      const uint32_t li = (xhi >> OR_LI_SHIFT) & 0x7Fu, jjs = jj << 8;
+      for (uint32_t more = 0;;) {
+        uint32_t k, kl, t0, o0, o1, o2, o3, dlo, dhi, rlo, rhi;
+        unsigned long long m;
+        asm volatile(FL_STEP_ASM
+                     : [tlo] "+s"(tlo), [thi] "+s"(thi), [A0] "+s"(A0), [A1] "+s"(A1), [B0] "+s"(B0),
+                       [B1] "+s"(B1), [dl0] "+v"(Dp.l0), [dh0] "+v"(Dp.h0), [dl1] "+v"(Dp.l1),
+                       [dh1] "+v"(Dp.h1), [lk] "+v"(lg.lk), [la] "+v"(lg.la), [lb] "+v"(lg.lb),
+                       [nacc] "+s"(lg.nacc), [more] "+s"(more), [k] "=&s"(k), [kl] "=&s"(kl), [t0] "=&s"(t0), [o0] "=&s"(o0),
+                       [o1] "=&s"(o1), [o2] "=&s"(o2), [o3] "=&s"(o3), [dlo] "=&s"(dlo), [dhi] "=&s"(dhi),
+                       [rlo] "=&s"(rlo), [rhi] "=&s"(rhi), [m] "=&s"(m)
+                     : [xhi] "s"(xhi), [li] "s"(li), [jjs] "s"(jjs)
+                     : "scc", "m0");
+        // the step returns with T > 0 only when the staging filled mid-sweep
+        if (lg.nacc != 64) break;
+        if (lg.lpos + 64 <= lg.lcap) lg.p[lg.lpos + lane] = v4(lg.lk, 0u, lg.la, lg.lb);
+        lg.lpos += 64;
+        lg.nacc = 0;
+        if (more == 0) break;
       }
     }
+    cur = nxt;
   }
-  if (nacc) {
-    if (lane < nacc && lpos + nacc <= lcap) logp[lpos + lane] = v4(lj, lk, la, lb);
-    lpos += nacc;
+  if (lg.nacc) {
+    if (lane < lg.nacc && lg.lpos + lg.nacc <= lg.lcap) lg.p[lg.lpos + lane] = v4(lg.lk, 0u, lg.la, lg.lb);
+    lg.lpos += lg.nacc;
   }
-  if (lpos > lcap) {  // cannot happen (touch bound); never read past the log
+  if (lg.lpos > lg.lcap) {  // cannot happen (touch bound); never read past the log
     if (lane == 0) atomicOr(&D.st->err, ERR_CORRUPT);
-    lpos = 0;
+    lg.lpos = 0;
   }
-  // per-level results and run bases (exclusive scan of the touch counts)
-  const uint32_t i0 = wave_incl_scan_u32(C0), i1 = wave_incl_scan_u32(C1);
-  const uint32_t t0 = rl(i0, 63);
-  if (lane < nl) {
-    LV[lane].dfin = D0;
-    LV[lane].cnt = C0;
-    LV[lane].base = i0 - C0;
-  }
-  if (lane + 64 < nl) {
-    LV[lane + 64].dfin = D1;
-    LV[lane + 64].cnt = C1;
-    LV[lane + 64].base = t0 + i1 - C1;
-  }
+  const int64_t f0 = static_cast<int64_t>((static_cast<uint64_t>(Dp.h0) << 32) | Dp.l0);
+  const int64_t f1 = static_cast<int64_t>((static_cast<uint64_t>(Dp.h1) << 32) | Dp.l1);
+  if (v0) LV[lane].dfin = f0;
+  if (v1) LV[lane + 64].dfin = f1;
   if (lane == 0) {
     FlowHdr* w = &F.hdr[h];
-    w->ntouch = lpos;
-    w->rests = rests;
+    w->ntouch = lg.lpos;
     w->amask[0] = A0;
     w->amask[1] = A1;
     w->bmask[0] = B0;
@@ -423,26 +629,86 @@ __global__ __launch_bounds__(64) void k_flow_plan(Dev D, FlowArgs F) {
   }
 }
 
-// ============================================================== k_flow_scatter
-__global__ void k_flow_scatter(Dev D, FlowArgs F) {
-  __shared__ uint32_t base[FL_CAP];
-  const uint32_t h = blockIdx.y;
+// ============================================================== k_flow_sort
+// Stable counting sort of one book's touches by level: histogram -> run bases, then tiles of
+// FL_SORT_T touches ranked within each wave by a 7-bit ballot match (equal levels) and
+// across waves through LDS counters, so every level's run keeps log (= time) order.
+constexpr uint32_t FL_SORT_T = 1024, FL_SORT_W = FL_SORT_T / 64;
+
+__global__ __launch_bounds__(FL_SORT_T) void k_flow_sort(Dev D, FlowArgs F) {
+  __shared__ uint32_t hist[FL_CAP], run[FL_CAP];
+  __shared__ uint32_t wc[FL_SORT_W][FL_CAP];
+  __shared__ uint32_t nrest;
+  const uint32_t h = blockIdx.x, tid = threadIdx.x, w = tid >> 6;
   if (h >= D.st->nhot || !F.hdr[h].ok) return;
-  const FlowLvl* LV = F.lvl + h * FL_CAP;
-  for (uint32_t k = threadIdx.x; k < FL_CAP; k += blockDim.x) base[k] = LV[k].base;
+  const uint32_t nt = F.hdr[h].ntouch, L = FL_TOUCH_MUL * F.hdr[h].beg, nl = F.hdr[h].nl;
+  FlowLvl* LV = F.lvl + h * FL_CAP;
+  if (tid < FL_CAP) hist[tid] = 0;
+  if (tid == 0) nrest = 0;
+  for (uint32_t i = tid; i < FL_SORT_W * FL_CAP; i += FL_SORT_T) wc[i / FL_CAP][i % FL_CAP] = 0;
   __syncthreads();
-  const uint32_t nt = F.hdr[h].ntouch, L = FL_TOUCH_MUL * F.hdr[h].beg;
-  for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < nt; t += gridDim.x * blockDim.x) {
-    const Touch x = F.log[L + t];
-    const uint32_t k = x.kr & 127u;
-    SEnt e;
-    e.j = x.j;
-    e.kind = (x.kr >> 7) & 1u;
-    e.amt = x.amt;
-    e.coord = 0;
-    e.t = t;
-    e.pad = 0;
-    F.srt[L + base[k] + (x.kr >> 8)] = e;
+  uint32_t myr = 0;
+  for (uint32_t t = tid; t < nt; t += FL_SORT_T) {
+    const uint32_t kr = F.log[L + t].kr;
+    atomicAdd(&hist[kr & 127u], 1u);
+    myr += (kr >> 7) & 1u;
+  }
+  if (myr) atomicAdd(&nrest, myr);
+  __syncthreads();
+  if (tid == 0) F.hdr[h].rests = nrest;
+  if (tid == 0) {
+    uint32_t acc = 0;
+    for (uint32_t k = 0; k < FL_CAP; ++k) {
+      run[k] = acc;
+      acc += hist[k];
+    }
+  }
+  __syncthreads();
+  if (tid >= 1 && tid <= nl) {
+    LV[tid].cnt = hist[tid];
+    LV[tid].base = run[tid];
+  }
+  const unsigned long long ltm = lt_mask();
+  for (uint32_t t0 = 0; t0 < nt; t0 += FL_SORT_T) {
+    const uint32_t t = t0 + tid;
+    const bool valid = t < nt;
+    Touch x{};
+    if (valid) x = F.log[L + t];
+    const uint32_t k = valid ? (x.kr & 127u) : 0u;
+    unsigned long long same = __ballot(valid);
+#pragma unroll
+    for (uint32_t b = 0; b < 7; ++b) {
+      const unsigned long long bb = __ballot((k >> b) & 1u);
+      same &= ((k >> b) & 1u) ? bb : ~bb;
+    }
+    const uint32_t rank = __popcll(same & ltm);
+    if (valid && rank == 0) wc[w][k] = __popcll(same);
+    __syncthreads();
+    if (tid < FL_CAP) {
+      uint32_t r = run[tid];
+      for (uint32_t ww = 0; ww < FL_SORT_W; ++ww) {
+        const uint32_t c = wc[ww][tid];
+        wc[ww][tid] = r;
+        r += c;
+      }
+      run[tid] = r;
+    }
+    __syncthreads();
+    if (valid) {
+      SEnt e;
+      e.j = tk_j(x);
+      e.kind = (x.kr >> 7) & 1u;
+      e.amt = x.amt;
+      e.coord = 0;
+      e.t = t;
+      e.pad = 0;
+      const uint32_t pos = wc[w][k] + rank;
+      F.srt[L + pos] = e;
+      F.log[L + t].pos = pos;
+    }
+    __syncthreads();
+    for (uint32_t i = tid; i < FL_SORT_W * FL_CAP; i += FL_SORT_T) wc[i / FL_CAP][i % FL_CAP] = 0;
+    __syncthreads();
   }
 }
 
@@ -453,7 +719,7 @@ __global__ __launch_bounds__(64) void k_flow_level(Dev D, FlowArgs F) {
   const uint32_t h = blockIdx.y, q = blockIdx.x;
   if (h >= D.st->nhot) return;
   const FlowHdr* hd = &F.hdr[h];
-  if (!uni(hd->ok) || q >= uni(hd->nl)) return;
+  if (!uni(hd->ok) || q == 0 || q > uni(hd->nl)) return;
   const uint32_t lane = lane_id();
   FlowLvl* Lq = &F.lvl[h * FL_CAP + q];
   const uint32_t L = FL_TOUCH_MUL * uni(hd->beg);
@@ -609,7 +875,7 @@ __device__ __forceinline__ FlTouchCtx fl_touch_ctx(const FlowArgs& F, uint32_t h
   const uint32_t base = t.Lq->base;
   t.IG = F.ig + t.Lq->ig_base;
   t.RS = F.rs + L + base;
-  t.c = F.srt[L + base + (x.kr >> 8)].coord;
+  t.c = F.srt[L + x.pos].coord;
   t.a = x.amt;
   const int64_t d0 = t.Lq->d0;
   const uint32_t ig_n = t.Lq->ig_n, nrest = t.Lq->nrest;
@@ -628,11 +894,11 @@ __global__ void k_flow_count(Dev D, BatchArgs B, FlowArgs F) {
   unsigned long long fills = 0, pops = 0;
   for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < nt; t += gridDim.x * blockDim.x) {
     const Touch x = F.log[L + t];
-    if (t > 0 && F.log[L + t - 1].j == x.j) continue;
+    if (t > 0 && tk_j(F.log[L + t - 1]) == tk_j(x)) continue;
     uint32_t acc = 0;
     for (uint32_t u = t; u < nt; ++u) {
       const Touch y = (u == t) ? x : F.log[L + u];
-      if (y.j != x.j) break;
+      if (tk_j(y) != tk_j(x)) break;
       F.fbase[L + u] = acc;
       if (((y.kr >> 7) & 1u) == TK_CONS) {
         const FlTouchCtx c = fl_touch_ctx(F, h, L, y);
@@ -644,7 +910,7 @@ __global__ void k_flow_count(Dev D, BatchArgs B, FlowArgs F) {
         pops += ne - (lend > c.c + c.a ? 1u : 0u);
       }
     }
-    B.ev_count[B.prep[beg + x.j].idx] = acc;
+    B.ev_count[B.prep[beg + tk_j(x)].idx] = acc;
   }
   // wave-reduce the counters, one atomic per wave
   for (int off = 32; off > 0; off >>= 1) {
@@ -668,12 +934,12 @@ __global__ void k_flow_events(Dev D, BatchArgs B, FlowArgs F, const uint32_t* ev
     const Touch x = F.log[L + t];
     if (((x.kr >> 7) & 1u) != TK_CONS) continue;
     const FlTouchCtx c = fl_touch_ctx(F, h, L, x);
-    const Prep tk = B.prep[beg + x.j];
+    const Prep tk = B.prep[beg + tk_j(x)];
     // taker remaining before this level: volume minus what its better levels took
     int64_t tb = tk.vol;
     for (uint32_t u = t; u > 0; --u) {
       const Touch y = F.log[L + u - 1];
-      if (y.j != x.j) break;
+      if (tk_j(y) != tk_j(x)) break;
       tb -= y.amt;
     }
     const uint32_t ig_n = c.Lq->ig_n, nrest = c.Lq->nrest, ig_all = c.Lq->ig_all;
@@ -742,7 +1008,7 @@ __global__ __launch_bounds__(FL_WRITE_T) void k_flow_write(Dev D, BatchArgs B, F
   const uint32_t lane = lane_id(), w = threadIdx.x >> 6, nw = FL_WRITE_T / 64;
   const uint32_t L = FL_TOUCH_MUL * hd.beg;
   const unsigned long long mask = D.idx_mask;
-  for (uint32_t q = w; q < hd.nl; q += nw) {
+  for (uint32_t q = 1 + w; q <= hd.nl; q += nw) {
     const FlowLvl f = F.lvl[h * FL_CAP + q];
     const RsEnt* RS = F.rs + L + f.base;
     // first new maker that survives the batch
@@ -849,7 +1115,7 @@ __global__ __launch_bounds__(FL_WRITE_T) void k_flow_write(Dev D, BatchArgs B, F
   __syncthreads();
   if (threadIdx.x == 0) {
     uint32_t c = 0;
-    for (uint32_t q = 0; q < hd.nl; ++q) {
+    for (uint32_t q = 1; q <= hd.nl; ++q) {
       const uint32_t k = keep[q];
       keep[q] = k ? c : NIL;
       c += k;
@@ -875,7 +1141,7 @@ __global__ __launch_bounds__(FL_WRITE_T) void k_flow_write(Dev D, BatchArgs B, F
   __syncthreads();
   const uint32_t nout = nout_s;
   if (nout > cap_s) return;
-  for (uint32_t q = threadIdx.x; q < hd.nl; q += FL_WRITE_T)
+  for (uint32_t q = 1 + threadIdx.x; q <= hd.nl; q += FL_WRITE_T)
     if (keep[q] != NIL) D.lvl[base_s + keep[q]] = lv[q];
   if (threadIdx.x == 0) {
     Book nb;

@@ -256,7 +256,7 @@ gome_status gome_engine::init(const gome_config& c) {
       !alloc(&F.ord8, nb + 16, "flow records") || !alloc(&F.log, ntouch, "flow touch log") ||
       !alloc(&F.srt, ntouch, "flow level runs") || !alloc(&F.rs, ntouch, "flow new makers") ||
       !alloc(&F.fbase, ntouch, "flow fill bases") || !alloc(&F.ig, F.ig_cap, "flow gathered makers") ||
-      !alloc(&F.ig_bump, 1, "flow gather bump"))
+      !alloc(&F.ig_bump, 1, "flow gather bump") || !alloc(&F.toff, MAX_FLOW + 1, "flow touch offsets"))
     return GOME_E_CAPACITY;
   HIPCHK(hipMemsetAsync(F.hdr, 0, sizeof(FlowHdr) * MAX_HOT, stream));
   HIPCHK(hipMemsetAsync(d_pend, 0, sizeof(PendEnt) * nb, stream));
@@ -330,7 +330,7 @@ gome_status gome_engine::run(const gome_order* d_ord, uint32_t n, hipStream_t s)
   k_seg_write<<<gN, T256, 0, s>>>(skeys, n, d_tmp, d_seg_start, d_st);
   HIPCHK(hipMemsetAsync(d_bcnt, 0, 64 * sizeof(uint32_t), s));
   k_seg_count<<<gN, T256, 0, s>>>(d_seg_start, d_st, d_bcnt, &d_st->ctr[C_MAXSEG]);
-  k_seg_bscan<<<1, 64, 0, s>>>(d_bcnt, d_bcnt + 32, d_st, HOT_MIN_LOG2, MAX_HOT);
+  k_seg_bscan<<<1, 64, 0, s>>>(d_bcnt, d_bcnt + 32, d_st, FLOW_MIN_LOG2, MAX_FLOW);
   k_seg_scatter<<<gN, T256, 0, s>>>(d_seg_start, d_st, d_bcnt + 32, d_seg_order);
 
   // ---- admission markers
@@ -363,8 +363,9 @@ gome_status gome_engine::run(const gome_order* d_ord, uint32_t n, hipStream_t s)
   k_flow_plan<<<nhot_max, 64, 0, flow_stream>>>(D, F);
   HIPCHK(hipEventRecord(evf1, flow_stream));
   k_flow_sort<<<nhot_max, FL_SORT_T, 0, flow_stream>>>(D, F);
-  k_flow_level<<<dim3(FL_CAP, nhot_max), 64, 0, flow_stream>>>(D, F);
-  k_flow_count<<<dim3(64, nhot_max), 256, 0, flow_stream>>>(D, B, F);
+  k_flow_level<<<nhot_max, FL_LEVEL_T, 0, flow_stream>>>(D, F);
+  k_flow_toff<<<1, 1024, 0, flow_stream>>>(D, F);
+  k_flow_count<<<1024, 256, 0, flow_stream>>>(D, B, F);
   k_flow_write<<<nhot_max, FL_WRITE_T, 0, flow_stream>>>(D, B, F);
   HIPCHK(hipEventRecord(joinf, flow_stream));
   // legacy hot path (books the flow path declined)
@@ -375,7 +376,7 @@ gome_status gome_engine::run(const gome_order* d_ord, uint32_t n, hipStream_t s)
   k_match_resume<<<nhot_max, 64, 0, hot_stream>>>(D, B, d_resume);
   k_pend_apply<<<dim3(8, 64), 256, 0, hot_stream>>>(D, d_pend, d_seg_start, d_seg_order, B);
   HIPCHK(hipEventRecord(join, hot_stream));
-  k_match<<<grid, 64, 0, s>>>(D, B);
+  k_match<<<grid, 64, 0, s>>>(D, B, &F.hdr[0].ok, sizeof(FlowHdr) / sizeof(uint32_t));
   HIPCHK(hipStreamWaitEvent(s, join, 0));
   HIPCHK(hipStreamWaitEvent(s, joinf, 0));
   HIPCHK(hipEventRecord(evm1, s));
@@ -383,7 +384,7 @@ gome_status gome_engine::run(const gome_order* d_ord, uint32_t n, hipStream_t s)
   // ---- event compaction into publish order
   scan(d_ev_count, n, d_ev_off, &d_st->n_events, s);
   k_ev_scatter<<<2048, T256, 0, s>>>(d_arena, arena_cap, d_st, d_ev_off, d_events);
-  k_flow_events<<<dim3(64, nhot_max), 256, 0, s>>>(D, B, F, d_ev_off, d_events);
+  k_flow_events<<<1024, 256, 0, s>>>(D, B, F, d_ev_off, d_events);
   k_recycle_copy<<<256, 256, 0, s>>>(D);
   k_recycle_fin<<<1, 64, 0, s>>>(D);
   HIPCHK(hipGetLastError());

@@ -23,6 +23,14 @@ struct BatchArgs {
 };
 
 constexpr uint32_t EVB = 32;      // events per arena block (cold books)
+
+// Routing of a batch's books (seg_order is longest first).  The first nhot segments
+// (>= 2^FLOW_MIN_LOG2 orders, at most MAX_FLOW) are flow candidates (match_flow.h); a
+// candidate the flow path declines goes to the legacy LDS kernel when it has at least
+// LEGACY_HOT_MIN orders (match_hot.h), else to the cold kernel below, like every other book.
+constexpr uint32_t FLOW_MIN_LOG2 = 7;
+constexpr uint32_t MAX_FLOW = 4096;
+constexpr uint32_t LEGACY_HOT_MIN = 2048;
 constexpr uint32_t EVB_HOT = 256; // events per arena block (hot books)
 
 // Wave-uniform context of the book being matched.
@@ -589,12 +597,14 @@ __device__ __forceinline__ void wave_init(WaveCtx& W, const Dev& D, const BatchA
   W.resting_delta = W.levels_delta = 0;
 }
 
-// Cold books: one 64-thread workgroup (one wavefront) per book, state in HBM.
-__global__ __launch_bounds__(64) void k_match(Dev D, BatchArgs B) {
-  const uint32_t nhot = D.st->nhot;
-  if (blockIdx.x + nhot >= D.st->nseg || (D.st->err & ERR_INPUT)) return;
-  const uint32_t seg = B.seg_order[nhot + blockIdx.x];
+// Cold books: one 64-thread workgroup (one wavefront) per book, state in HBM.  Block i
+// takes seg_order[i]; flow candidates are skipped unless the flow path declined them and
+// they are too short for the legacy hot kernel (`flow_ok[i]`: FlowHdr::ok of candidate i).
+__global__ __launch_bounds__(64) void k_match(Dev D, BatchArgs B, const uint32_t* flow_ok, uint32_t ok_stride) {
+  if (blockIdx.x >= D.st->nseg || (D.st->err & ERR_INPUT)) return;
+  const uint32_t seg = B.seg_order[blockIdx.x];
   const uint32_t beg = B.seg_start[seg], end = B.seg_start[seg + 1];
+  if (blockIdx.x < D.st->nhot && (flow_ok[blockIdx.x * ok_stride] || end - beg >= LEGACY_HOT_MIN)) return;
   WaveCtx W;
   wave_init(W, D, B, uni(B.ord[B.prep[beg].idx].symbol_id), EVB);
   process_global(W, beg, end);

@@ -132,6 +132,7 @@ struct FlowArgs {
   IgEnt* ig;
   uint32_t ig_cap;
   uint32_t* ig_bump;
+  uint32_t* toff;      // [MAX_FLOW + 1] exclusive scan of the books' touch counts
   uint32_t enabled;
   uint32_t pad;
 };
@@ -713,13 +714,11 @@ __global__ __launch_bounds__(FL_SORT_T) void k_flow_sort(Dev D, FlowArgs F) {
 }
 
 // ============================================================== k_flow_level
-// One wave per (book, level): volume coordinates of the level's run, then the gather of
-// the consumed prefix of its resting FIFO.
-__global__ __launch_bounds__(64) void k_flow_level(Dev D, FlowArgs F) {
-  const uint32_t h = blockIdx.y, q = blockIdx.x;
-  if (h >= D.st->nhot) return;
+// One wave per level (waves of a per-book workgroup take the book's levels in turn):
+// volume coordinates of the level's run, then the gather of the consumed prefix of its
+// resting FIFO.
+__device__ __forceinline__ void fl_level_one(const Dev& D, const FlowArgs& F, uint32_t h, uint32_t q) {
   const FlowHdr* hd = &F.hdr[h];
-  if (!uni(hd->ok) || q == 0 || q > uni(hd->nl)) return;
   const uint32_t lane = lane_id();
   FlowLvl* Lq = &F.lvl[h * FL_CAP + q];
   const uint32_t L = FL_TOUCH_MUL * uni(hd->beg);
@@ -839,6 +838,14 @@ __global__ __launch_bounds__(64) void k_flow_level(Dev D, FlowArgs F) {
   }
 }
 
+constexpr uint32_t FL_LEVEL_T = 1024;
+__global__ __launch_bounds__(FL_LEVEL_T) void k_flow_level(Dev D, FlowArgs F) {
+  const uint32_t h = blockIdx.x;
+  if (h >= D.st->nhot || !F.hdr[h].ok) return;
+  const uint32_t nl = F.hdr[h].nl;
+  for (uint32_t q = 1 + (threadIdx.x >> 6); q <= nl; q += FL_LEVEL_T / 64) fl_level_one(D, F, h, uni(q));
+}
+
 // ============================================================== events of one touch
 // Makers of level q in FIFO order: the gathered old makers IG[0, ig_n) (coordinates from 0),
 // then the new makers RS[0, nrest) (from d0).  Index of the maker covering coordinate x.
@@ -884,15 +891,47 @@ __device__ __forceinline__ FlTouchCtx fl_touch_ctx(const FlowArgs& F, uint32_t h
   return t;
 }
 
+// Book of flattened touch index gt: the last h with toff[h] <= gt.
+__device__ __forceinline__ uint32_t fl_book_of(const FlowArgs& F, uint32_t nb, uint32_t gt) {
+  uint32_t lo = 0, hi = nb;
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (F.toff[mid] <= gt) lo = mid; else hi = mid;
+  }
+  return lo;
+}
+
+// Exclusive scan of the flow books' touch counts (declined candidates count 0).
+__global__ __launch_bounds__(1024) void k_flow_toff(Dev D, FlowArgs F) {
+  __shared__ uint32_t part[1024];
+  const uint32_t nb = D.st->nhot, tid = threadIdx.x;
+  const uint32_t per = (nb + 1023) / 1024, b0 = tid * per;
+  uint32_t s = 0;
+  for (uint32_t i = b0; i < b0 + per && i < nb; ++i) s += F.hdr[i].ok ? F.hdr[i].ntouch : 0u;
+  part[tid] = s;
+  __syncthreads();
+  if (tid == 0) {
+    uint32_t acc = 0;
+    for (uint32_t i = 0; i < 1024; ++i) { const uint32_t v = part[i]; part[i] = acc; acc += v; }
+    F.toff[nb] = acc;
+  }
+  __syncthreads();
+  uint32_t acc = part[tid];
+  for (uint32_t i = b0; i < b0 + per && i < nb; ++i) {
+    F.toff[i] = acc;
+    acc += F.hdr[i].ok ? F.hdr[i].ntouch : 0u;
+  }
+}
+
 // ============================================================== k_flow_count
 // Thread per touch; the first touch of each order walks the order's touches (consecutive
 // in the log, best level first), fixing fill_idx bases and ev_count[taker].
 __global__ void k_flow_count(Dev D, BatchArgs B, FlowArgs F) {
-  const uint32_t h = blockIdx.y;
-  if (h >= D.st->nhot || !F.hdr[h].ok) return;
-  const uint32_t nt = F.hdr[h].ntouch, beg = F.hdr[h].beg, L = FL_TOUCH_MUL * beg;
+  const uint32_t nb = D.st->nhot, total = F.toff[nb];
   unsigned long long fills = 0, pops = 0;
-  for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < nt; t += gridDim.x * blockDim.x) {
+  for (uint32_t gt = blockIdx.x * blockDim.x + threadIdx.x; gt < total; gt += gridDim.x * blockDim.x) {
+    const uint32_t h = fl_book_of(F, nb, gt), t = gt - F.toff[h];
+    const uint32_t nt = F.hdr[h].ntouch, beg = F.hdr[h].beg, L = FL_TOUCH_MUL * beg;
     const Touch x = F.log[L + t];
     if (t > 0 && tk_j(F.log[L + t - 1]) == tk_j(x)) continue;
     uint32_t acc = 0;
@@ -927,10 +966,10 @@ __global__ void k_flow_count(Dev D, BatchArgs B, FlowArgs F) {
 // ============================================================== k_flow_events
 // After the publish-order scan: every fill event at out[ev_off[taker] + fill_idx].
 __global__ void k_flow_events(Dev D, BatchArgs B, FlowArgs F, const uint32_t* ev_off, gome_event* out) {
-  const uint32_t h = blockIdx.y;
-  if (h >= D.st->nhot || !F.hdr[h].ok) return;
-  const uint32_t nt = F.hdr[h].ntouch, beg = F.hdr[h].beg, L = FL_TOUCH_MUL * beg, sym = F.hdr[h].sym;
-  for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < nt; t += gridDim.x * blockDim.x) {
+  const uint32_t nb = D.st->nhot, total = F.toff[nb];
+  for (uint32_t gt = blockIdx.x * blockDim.x + threadIdx.x; gt < total; gt += gridDim.x * blockDim.x) {
+    const uint32_t h = fl_book_of(F, nb, gt), t = gt - F.toff[h];
+    const uint32_t beg = F.hdr[h].beg, L = FL_TOUCH_MUL * beg, sym = F.hdr[h].sym;
     const Touch x = F.log[L + t];
     if (((x.kr >> 7) & 1u) != TK_CONS) continue;
     const FlTouchCtx c = fl_touch_ctx(F, h, L, x);

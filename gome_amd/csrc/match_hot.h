@@ -51,8 +51,7 @@ __device__ unsigned long long g_stamps[256 * NSTAMP];
 #define ST_ADD(i, v)
 #endif
 
-constexpr uint32_t HOT_MIN_LOG2 = 11;
-constexpr uint32_t MAX_HOT = 256;
+constexpr uint32_t MAX_HOT = MAX_FLOW;  // legacy hot kernel grid (candidates, see match_cold.h)
 constexpr uint32_t LRB_CAP = 128;  // levels held in lanes (2 register sets)
 constexpr uint32_t NCS = LRB_CAP;  // one head-chunk cache slot per resident level
 constexpr uint32_t CS_NONE = 0xFFu;
@@ -1122,8 +1121,9 @@ __global__ __launch_bounds__(64) void k_match_hot(Dev D, BatchArgs B, PendEnt* p
                                                    ResumeRec* resume, const FlowHdr* flow) {
   extern __shared__ __align__(16) unsigned char smem[];
   if (blockIdx.x >= D.st->nhot || (D.st->err & ERR_INPUT)) return;
-  if (flow[blockIdx.x].ok) {  // applied by the flow path (match_flow.h)
-    if (lane_id() == 0) resume[blockIdx.x].valid = 0;
+  if (flow[blockIdx.x].ok ||  // applied by the flow path (match_flow.h)
+      B.seg_start[B.seg_order[blockIdx.x] + 1] - B.seg_start[B.seg_order[blockIdx.x]] < LEGACY_HOT_MIN) {
+    if (lane_id() == 0) resume[blockIdx.x].valid = 0;  // declined and short: the cold kernel
     return;
   }
   __builtin_amdgcn_s_setprio(3);  // the hottest books are the batch's critical path

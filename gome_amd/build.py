@@ -22,7 +22,7 @@ HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
 ARCH = os.environ.get("GOME_OFFLOAD_ARCH", "gfx950")
 
 SOURCES = [os.path.join(CSRC, "engine.hip"), os.path.join(CSRC, "host.cpp")]
-HEADERS = sorted(glob.glob(os.path.join(CSRC, "*.h"))) + [os.path.join(ROOT, "include", "gome", "gome_abi.h"),
+HEADERS = sorted(glob.glob(os.path.join(CSRC, "*.h"))) + sorted(glob.glob(os.path.join(CSRC, "*.inc"))) + [os.path.join(ROOT, "include", "gome", "gome_abi.h"),
                                                          os.path.abspath(__file__)]
 
 

@@ -253,7 +253,7 @@ gome_status gome_engine::init(const gome_config& c) {
   F.ig_cap = static_cast<uint32_t>(std::min<uint64_t>(std::max<uint64_t>(cfg.max_nodes, 1u << 16), 0xF0000000ull));
   F.enabled = (cfg.flags & GOME_FLAG_LEGACY_HOT) ? 0u : 1u;
   if (!alloc(&F.hdr, MAX_HOT, "flow headers") || !alloc(&F.lvl, MAX_HOT * FL_CAP, "flow levels") ||
-      !alloc(&F.ord8, nb + 16, "flow records") || !alloc(&F.log, ntouch, "flow touch log") ||
+      !alloc(&F.ord8, static_cast<uint64_t>(FL_ORD8_MUL) * nb + FL_ORD8_PAD, "flow records") || !alloc(&F.log, ntouch, "flow touch log") ||
       !alloc(&F.srt, ntouch, "flow level runs") || !alloc(&F.rs, ntouch, "flow new makers") ||
       !alloc(&F.fbase, ntouch, "flow fill bases") || !alloc(&F.ig, F.ig_cap, "flow gathered makers") ||
       !alloc(&F.ig_bump, 1, "flow gather bump") || !alloc(&F.toff, MAX_FLOW + 1, "flow touch offsets"))

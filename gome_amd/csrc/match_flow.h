@@ -54,8 +54,13 @@ constexpr uint32_t FL_MAX = FL_CAP - 2;   // usable levels 1..126: slot 0 is the
                                           // slot 127 the ask sentinel (bit scans never miss)
 constexpr uint32_t FL_HASH = 1024;        // LDS price-set slots in k_flow_prep
 constexpr uint32_t FL_PREP_T = 1024;
-constexpr uint32_t FL_TOUCH_MUL = 4;      // log capacity per order (touches <= 3n + L0)
+constexpr uint32_t FL_TOUCH_MUL = 5;      // log capacity per order (touches <= 3n + L0, plus
+                                          // 64 entries of staging slack, n >= 128)
 constexpr unsigned long long FL_KEY_OFF = 1ull << 62;
+// Packed records of book `seg` start at the 4-aligned index at or above beg + 8 * seg and are
+// followed by SKIP records up to a multiple of 4: every book's stream is whole half-groups.
+__host__ __device__ constexpr uint32_t fl_obase(uint32_t beg, uint32_t seg) { return (beg + 8u * seg + 3u) & ~3u; }
+constexpr uint32_t FL_ORD8_MUL = 9, FL_ORD8_PAD = 64;  // ord8 capacity: 9 * max_batch + 64
 
 // packed order record of the plan (8 B): volume [0,53), level [53,60), SALE bit 60, skip 61
 constexpr uint32_t OR_LI_SHIFT = 21, OR_SELL = 1u << 28, OR_SKIP = 1u << 29;
@@ -98,7 +103,7 @@ static_assert(sizeof(IgEnt) == 32, "IgEnt layout");
 struct FlowHdr {
   uint32_t ok, nl, sym, ntouch;
   uint32_t beg, end, nold, adds;
-  uint32_t dropped, rests, pad0, pad1;
+  uint32_t dropped, rests, obase, pad1;  // obase: first packed record (4-aligned, padded)
   unsigned long long amask[2], bmask[2];  // final S:SALE / S:BUY membership of the levels
 };
 
@@ -250,6 +255,9 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep(Dev D, BatchArgs B, Flo
     hval[s] = r + 1;  // the slot now maps price -> level index (each slot has one owner thread)
   }
   __syncthreads();
+  const uint32_t obase = fl_obase(beg, seg);
+  if (tid < ((4u - ((end - beg) & 3u)) & 3u))  // padding to whole half-groups
+    F.ord8[obase + (end - beg) + tid] = static_cast<unsigned long long>(OR_SKIP) << 32;
   for (uint32_t b = beg + tid; b < end; b += FL_PREP_T) {
     const Prep q = B.prep[b];
     unsigned long long rec = static_cast<unsigned long long>(OR_SKIP) << 32;
@@ -262,7 +270,7 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep(Dev D, BatchArgs B, Flo
                           (li << OR_LI_SHIFT) | (q.side == GOME_SALE ? OR_SELL : 0u);
       rec = (static_cast<unsigned long long>(hi) << 32) | static_cast<uint32_t>(q.vol);
     }
-    F.ord8[b] = rec;
+    F.ord8[obase + (b - beg)] = rec;
     B.ev_count[q.idx] = 0;
   }
   if (tid == 0) {
@@ -275,6 +283,7 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep(Dev D, BatchArgs B, Flo
     x.nold = bk.n_lvl;
     x.adds = adds;
     x.dropped = dropped;
+    x.obase = obase;
     *hd = x;
   }
 }
@@ -352,198 +361,8 @@ struct FlLog {
   GOME_GLB v4u* p;
 };
 
-// One order of the plan as a single SALU/lane-register block (no compiler phi copies, no
-// VALU compares).  In: T (tlo:thi) > 0, li, side bit in xhi, order index jj.  Runs the
-// reference's SetOrder at the aggregate level (engine.go:56-85): sweep the crossing
-// opposite levels best first (full: depth 0 + ZREM, partial: depth - T), then rest T at li
-// (depth + T, ZADD own side).  Logs one touch per level.  Returns with T == 0 when the order
-// is done, or with T > 0 when the 64-touch staging filled mid-sweep (the caller stores it
-// and calls again: the sweep resumes from the updated state).
-#define FL_STEP_ASM                                                                        \
-  "s_bitcmp1_b32 %[xhi], 28\n\t"                                                           \
-  "s_cbranch_scc1 SELL_%=\n\t"                                                             \
-  "BUY_LOOP_%=:\n\t"                                                                       \
-  "s_ff1_i32_b64 %[k], %[A0]\n\t"                                                          \
-  "s_ff1_i32_b64 %[t0], %[A1]\n\t"                                                         \
-  "s_add_u32 %[t0], %[t0], 64\n\t"                                                         \
-  "s_cmp_lg_u64 %[A0], 0\n\t"                                                              \
-  "s_cselect_b32 %[k], %[k], %[t0]\n\t"                                                    \
-  "s_cmp_gt_u32 %[k], %[li]\n\t"                                                           \
-  "s_cbranch_scc1 BUY_REST_%=\n\t"                                                         \
-  "s_and_b32 %[kl], %[k], 63\n\t"                                                          \
-  "v_readlane_b32 %[o0], %[dl0], %[kl]\n\t"                                                \
-  "v_readlane_b32 %[o1], %[dh0], %[kl]\n\t"                                                \
-  "v_readlane_b32 %[o2], %[dl1], %[kl]\n\t"                                                \
-  "v_readlane_b32 %[o3], %[dh1], %[kl]\n\t"                                                \
-  "s_cmp_lt_u32 %[k], 64\n\t"                                                              \
-  "s_cselect_b32 %[dlo], %[o0], %[o2]\n\t"                                                 \
-  "s_cselect_b32 %[dhi], %[o1], %[o3]\n\t"                                                 \
-  "s_sub_u32 %[rlo], %[tlo], %[dlo]\n\t"                                                   \
-  "s_subb_u32 %[rhi], %[thi], %[dhi]\n\t"                                                  \
-  "s_cbranch_scc1 BUY_PART_%=\n\t"                                                         \
-  "s_cmp_lt_u32 %[k], 64\n\t"                                                              \
-  "s_cselect_b32 %[o0], 0, %[o0]\n\t"                                                      \
-  "s_cselect_b32 %[o1], 0, %[o1]\n\t"                                                      \
-  "s_cselect_b32 %[o2], %[o2], 0\n\t"                                                      \
-  "s_cselect_b32 %[o3], %[o3], 0\n\t"                                                      \
-  "s_mov_b32 m0, %[kl]\n\t"                                                             \
-  "v_writelane_b32 %[dl0], %[o0], m0\n\t"                                               \
-  "v_writelane_b32 %[dh0], %[o1], m0\n\t"                                               \
-  "v_writelane_b32 %[dl1], %[o2], m0\n\t"                                               \
-  "v_writelane_b32 %[dh1], %[o3], m0\n\t"                                               \
-  "s_cmp_lt_u32 %[k], 64\n\t"                                                              \
-  "s_cselect_b64 %[m], %[A0], %[A1]\n\t"                                                    \
-  "s_bitset0_b64 %[m], %[k]\n\t"                                                                   \
-  "s_cmp_lt_u32 %[k], 64\n\t"                                                              \
-  "s_cselect_b64 %[A0], %[m], %[A0]\n\t"                                                    \
-  "s_cselect_b64 %[A1], %[A1], %[m]\n\t"                                                    \
-  "s_or_b32 %[t0], %[jjs], %[k]\n\t"                                                       \
-  "s_mov_b32 m0, %[nacc]\n\t"                                                           \
-  "v_writelane_b32 %[lk], %[t0], m0\n\t"                                              \
-  "v_writelane_b32 %[la], %[dlo], m0\n\t"                                             \
-  "v_writelane_b32 %[lb], %[dhi], m0\n\t"                                             \
-  "s_add_u32 %[nacc], %[nacc], 1\n\t"                                                      \
-  "s_mov_b32 %[tlo], %[rlo]\n\t"                                                           \
-  "s_mov_b32 %[thi], %[rhi]\n\t"                                                           \
-  "s_or_b32 %[t0], %[rlo], %[rhi]\n\t"                                                     \
-  "s_cbranch_scc0 DONE_%=\n\t"                                                             \
-  "s_cmp_eq_u32 %[nacc], 64\n\t"                                                           \
-  "s_cbranch_scc1 DONE_%=\n\t"                                                             \
-  "s_branch BUY_LOOP_%=\n\t"                                                               \
-  "BUY_PART_%=:\n\t"                                                                       \
-  "s_sub_u32 %[rlo], %[dlo], %[tlo]\n\t"                                                   \
-  "s_subb_u32 %[rhi], %[dhi], %[thi]\n\t"                                                  \
-  "s_cmp_lt_u32 %[k], 64\n\t"                                                              \
-  "s_cselect_b32 %[o0], %[rlo], %[o0]\n\t"                                                 \
-  "s_cselect_b32 %[o1], %[rhi], %[o1]\n\t"                                                 \
-  "s_cselect_b32 %[o2], %[o2], %[rlo]\n\t"                                                 \
-  "s_cselect_b32 %[o3], %[o3], %[rhi]\n\t"                                                 \
-  "s_branch PART_TAIL_%=\n\t"                                                              \
-  "BUY_REST_%=:\n\t"                                                                       \
-  "s_and_b32 %[kl], %[li], 63\n\t"                                                         \
-  "v_readlane_b32 %[o0], %[dl0], %[kl]\n\t"                                                \
-  "v_readlane_b32 %[o1], %[dh0], %[kl]\n\t"                                                \
-  "v_readlane_b32 %[o2], %[dl1], %[kl]\n\t"                                                \
-  "v_readlane_b32 %[o3], %[dh1], %[kl]\n\t"                                                \
-  "s_cmp_lt_u32 %[li], 64\n\t"                                                              \
-  "s_cselect_b64 %[m], %[B0], %[B1]\n\t"                                                    \
-  "s_bitset1_b64 %[m], %[li]\n\t"                                                                   \
-  "s_cmp_lt_u32 %[li], 64\n\t"                                                              \
-  "s_cselect_b64 %[B0], %[m], %[B0]\n\t"                                                    \
-  "s_cselect_b64 %[B1], %[B1], %[m]\n\t"                                                    \
-  "s_branch REST_TAIL_%=\n\t"                                                              \
-  "SELL_%=:\n\t"                                                                           \
-  "SELL_LOOP_%=:\n\t"                                                                      \
-  "s_flbit_i32_b64 %[k], %[B0]\n\t"                                                        \
-  "s_sub_u32 %[k], 63, %[k]\n\t"                                                           \
-  "s_flbit_i32_b64 %[t0], %[B1]\n\t"                                                       \
-  "s_sub_u32 %[t0], 127, %[t0]\n\t"                                                        \
-  "s_cmp_lg_u64 %[B1], 0\n\t"                                                              \
-  "s_cselect_b32 %[k], %[t0], %[k]\n\t"                                                    \
-  "s_cmp_lt_u32 %[k], %[li]\n\t"                                                           \
-  "s_cbranch_scc1 SELL_REST_%=\n\t"                                                        \
-  "s_and_b32 %[kl], %[k], 63\n\t"                                                          \
-  "v_readlane_b32 %[o0], %[dl0], %[kl]\n\t"                                                \
-  "v_readlane_b32 %[o1], %[dh0], %[kl]\n\t"                                                \
-  "v_readlane_b32 %[o2], %[dl1], %[kl]\n\t"                                                \
-  "v_readlane_b32 %[o3], %[dh1], %[kl]\n\t"                                                \
-  "s_cmp_lt_u32 %[k], 64\n\t"                                                              \
-  "s_cselect_b32 %[dlo], %[o0], %[o2]\n\t"                                                 \
-  "s_cselect_b32 %[dhi], %[o1], %[o3]\n\t"                                                 \
-  "s_sub_u32 %[rlo], %[tlo], %[dlo]\n\t"                                                   \
-  "s_subb_u32 %[rhi], %[thi], %[dhi]\n\t"                                                  \
-  "s_cbranch_scc1 SELL_PART_%=\n\t"                                                        \
-  "s_cmp_lt_u32 %[k], 64\n\t"                                                              \
-  "s_cselect_b32 %[o0], 0, %[o0]\n\t"                                                      \
-  "s_cselect_b32 %[o1], 0, %[o1]\n\t"                                                      \
-  "s_cselect_b32 %[o2], %[o2], 0\n\t"                                                      \
-  "s_cselect_b32 %[o3], %[o3], 0\n\t"                                                      \
-  "s_mov_b32 m0, %[kl]\n\t"                                                             \
-  "v_writelane_b32 %[dl0], %[o0], m0\n\t"                                               \
-  "v_writelane_b32 %[dh0], %[o1], m0\n\t"                                               \
-  "v_writelane_b32 %[dl1], %[o2], m0\n\t"                                               \
-  "v_writelane_b32 %[dh1], %[o3], m0\n\t"                                               \
-  "s_cmp_lt_u32 %[k], 64\n\t"                                                              \
-  "s_cselect_b64 %[m], %[B0], %[B1]\n\t"                                                    \
-  "s_bitset0_b64 %[m], %[k]\n\t"                                                                   \
-  "s_cmp_lt_u32 %[k], 64\n\t"                                                              \
-  "s_cselect_b64 %[B0], %[m], %[B0]\n\t"                                                    \
-  "s_cselect_b64 %[B1], %[B1], %[m]\n\t"                                                    \
-  "s_or_b32 %[t0], %[jjs], %[k]\n\t"                                                       \
-  "s_mov_b32 m0, %[nacc]\n\t"                                                           \
-  "v_writelane_b32 %[lk], %[t0], m0\n\t"                                              \
-  "v_writelane_b32 %[la], %[dlo], m0\n\t"                                             \
-  "v_writelane_b32 %[lb], %[dhi], m0\n\t"                                             \
-  "s_add_u32 %[nacc], %[nacc], 1\n\t"                                                      \
-  "s_mov_b32 %[tlo], %[rlo]\n\t"                                                           \
-  "s_mov_b32 %[thi], %[rhi]\n\t"                                                           \
-  "s_or_b32 %[t0], %[rlo], %[rhi]\n\t"                                                     \
-  "s_cbranch_scc0 DONE_%=\n\t"                                                             \
-  "s_cmp_eq_u32 %[nacc], 64\n\t"                                                           \
-  "s_cbranch_scc1 DONE_%=\n\t"                                                             \
-  "s_branch SELL_LOOP_%=\n\t"                                                              \
-  "SELL_PART_%=:\n\t"                                                                      \
-  "s_sub_u32 %[rlo], %[dlo], %[tlo]\n\t"                                                   \
-  "s_subb_u32 %[rhi], %[dhi], %[thi]\n\t"                                                  \
-  "s_cmp_lt_u32 %[k], 64\n\t"                                                              \
-  "s_cselect_b32 %[o0], %[rlo], %[o0]\n\t"                                                 \
-  "s_cselect_b32 %[o1], %[rhi], %[o1]\n\t"                                                 \
-  "s_cselect_b32 %[o2], %[o2], %[rlo]\n\t"                                                 \
-  "s_cselect_b32 %[o3], %[o3], %[rhi]\n\t"                                                 \
-  "PART_TAIL_%=:\n\t"                                                                      \
-  "s_mov_b32 m0, %[kl]\n\t"                                                             \
-  "v_writelane_b32 %[dl0], %[o0], m0\n\t"                                               \
-  "v_writelane_b32 %[dh0], %[o1], m0\n\t"                                               \
-  "v_writelane_b32 %[dl1], %[o2], m0\n\t"                                               \
-  "v_writelane_b32 %[dh1], %[o3], m0\n\t"                                               \
-  "s_or_b32 %[t0], %[jjs], %[k]\n\t"                                                       \
-  "s_mov_b32 m0, %[nacc]\n\t"                                                           \
-  "v_writelane_b32 %[lk], %[t0], m0\n\t"                                              \
-  "v_writelane_b32 %[la], %[tlo], m0\n\t"                                             \
-  "v_writelane_b32 %[lb], %[thi], m0\n\t"                                             \
-  "s_add_u32 %[nacc], %[nacc], 1\n\t"                                                      \
-  "s_mov_b32 %[tlo], 0\n\t"                                                                \
-  "s_mov_b32 %[thi], 0\n\t"                                                                \
-  "s_branch DONE_%=\n\t"                                                                   \
-  "SELL_REST_%=:\n\t"                                                                      \
-  "s_and_b32 %[kl], %[li], 63\n\t"                                                         \
-  "v_readlane_b32 %[o0], %[dl0], %[kl]\n\t"                                                \
-  "v_readlane_b32 %[o1], %[dh0], %[kl]\n\t"                                                \
-  "v_readlane_b32 %[o2], %[dl1], %[kl]\n\t"                                                \
-  "v_readlane_b32 %[o3], %[dh1], %[kl]\n\t"                                                \
-  "s_cmp_lt_u32 %[li], 64\n\t"                                                              \
-  "s_cselect_b64 %[m], %[A0], %[A1]\n\t"                                                    \
-  "s_bitset1_b64 %[m], %[li]\n\t"                                                                   \
-  "s_cmp_lt_u32 %[li], 64\n\t"                                                              \
-  "s_cselect_b64 %[A0], %[m], %[A0]\n\t"                                                    \
-  "s_cselect_b64 %[A1], %[A1], %[m]\n\t"                                                    \
-  "REST_TAIL_%=:\n\t"                                                                      \
-  "s_cmp_lt_u32 %[li], 64\n\t"                                                             \
-  "s_cselect_b32 %[dlo], %[o0], %[o2]\n\t"                                                 \
-  "s_cselect_b32 %[dhi], %[o1], %[o3]\n\t"                                                 \
-  "s_add_u32 %[dlo], %[dlo], %[tlo]\n\t"                                                   \
-  "s_addc_u32 %[dhi], %[dhi], %[thi]\n\t"                                                  \
-  "s_cmp_lt_u32 %[li], 64\n\t"                                                             \
-  "s_cselect_b32 %[o0], %[dlo], %[o0]\n\t"                                                 \
-  "s_cselect_b32 %[o1], %[dhi], %[o1]\n\t"                                                 \
-  "s_cselect_b32 %[o2], %[o2], %[dlo]\n\t"                                                 \
-  "s_cselect_b32 %[o3], %[o3], %[dhi]\n\t"                                                 \
-  "s_mov_b32 m0, %[kl]\n\t"                                                             \
-  "v_writelane_b32 %[dl0], %[o0], m0\n\t"                                               \
-  "v_writelane_b32 %[dh0], %[o1], m0\n\t"                                               \
-  "v_writelane_b32 %[dl1], %[o2], m0\n\t"                                               \
-  "v_writelane_b32 %[dh1], %[o3], m0\n\t"                                               \
-  "s_or_b32 %[t0], %[jjs], %[li]\n\t"                                                      \
-  "s_or_b32 %[t0], %[t0], 128\n\t"                                                         \
-  "s_mov_b32 m0, %[nacc]\n\t"                                                           \
-  "v_writelane_b32 %[lk], %[t0], m0\n\t"                                              \
-  "v_writelane_b32 %[la], %[tlo], m0\n\t"                                             \
-  "v_writelane_b32 %[lb], %[thi], m0\n\t"                                             \
-  "s_add_u32 %[nacc], %[nacc], 1\n\t"                                                      \
-  "s_mov_b32 %[tlo], 0\n\t"                                                                \
-  "s_mov_b32 %[thi], 0\n\t"                                                                \
-  "DONE_%=:\n\t"                                                                           \
-  "s_or_b32 %[more], %[tlo], %[thi]"
+#include "flow_plan_asm.inc"
+
 
 
 __global__ __launch_bounds__(64) void k_flow_plan(Dev D, FlowArgs F) {
@@ -563,51 +382,18 @@ __global__ __launch_bounds__(64) void k_flow_plan(Dev D, FlowArgs F) {
   unsigned long long B0 = __ballot(m0 & M_BUY) | 1ull, B1 = __ballot(m1 & M_BUY);
 
   FlLog lg{vreg(0u), vreg(0u), vreg(0u), 0u, 0u, 0u, FL_TOUCH_MUL * n, (GOME_GLB v4u*)(F.log + FL_TOUCH_MUL * beg)};
-  const fl_cptr o8 = (fl_cptr)(F.ord8 + beg);
-  // groups of 8 records at the 64-B aligned address at or below beg (leading ones skipped)
-  const uint32_t skew = beg & 7u;
-  const fl_cptr ob = o8 - skew;
-  const uint32_t ngs = (n + skew + 7) / 8;
-  auto load_group = [&](uint32_t g) {
-    FlGroup r;
-#pragma unroll
-    for (uint32_t i = 0; i < 8; ++i) r.o[i] = ob[8 * g + i];
-    return r;
-  };
-  FlGroup cur = load_group(0), nxt;
-  for (uint32_t g = 0; g < ngs; ++g) {
-#pragma unroll
-    for (uint32_t u = 0; u < 8; ++u) {
-      // Prefetch the next group once this one is in registers (SMEM returns out of order:
-      // any wait is lgkmcnt(0), so the load must not be in flight when cur is first used).
-      if (u == 1) nxt = load_group(g + 1 < ngs ? g + 1 : g);
-      const uint32_t jj = 8 * g + u - skew;  // wraps for the skew records: jj >= n
-      const uint32_t xhi = jj < n ? static_cast<uint32_t>(cur.o[u] >> 32) : OR_SKIP;
-      if (xhi & OR_SKIP) continue;
-      uint32_t tlo = static_cast<uint32_t>(cur.o[u]), thi = xhi & 0x1FFFFFu;
-      const uint32_t li = (xhi >> OR_LI_SHIFT) & 0x7Fu, jjs = jj << 8;
-      for (uint32_t more = 0;;) {
-        uint32_t k, kl, t0, o0, o1, o2, o3, dlo, dhi, rlo, rhi;
-        unsigned long long m;
-        asm volatile(FL_STEP_ASM
-                     : [tlo] "+s"(tlo), [thi] "+s"(thi), [A0] "+s"(A0), [A1] "+s"(A1), [B0] "+s"(B0),
-                       [B1] "+s"(B1), [dl0] "+v"(Dp.l0), [dh0] "+v"(Dp.h0), [dl1] "+v"(Dp.l1),
-                       [dh1] "+v"(Dp.h1), [lk] "+v"(lg.lk), [la] "+v"(lg.la), [lb] "+v"(lg.lb),
-                       [nacc] "+s"(lg.nacc), [more] "+s"(more), [k] "=&s"(k), [kl] "=&s"(kl), [t0] "=&s"(t0), [o0] "=&s"(o0),
-                       [o1] "=&s"(o1), [o2] "=&s"(o2), [o3] "=&s"(o3), [dlo] "=&s"(dlo), [dhi] "=&s"(dhi),
-                       [rlo] "=&s"(rlo), [rhi] "=&s"(rhi), [m] "=&s"(m)
-                     : [xhi] "s"(xhi), [li] "s"(li), [jjs] "s"(jjs)
-                     : "scc", "m0");
-        // the step returns with T > 0 only when the staging filled mid-sweep
-        if (lg.nacc != 64) break;
-        if (lg.lpos + 64 <= lg.lcap) lg.p[lg.lpos + lane] = v4(lg.lk, 0u, lg.la, lg.lb);
-        lg.lpos += 64;
-        lg.nacc = 0;
-        if (more == 0) break;
-      }
-    }
-    cur = nxt;
-  }
+  // records are read in half-groups of 4 (the book's stream is padded to whole groups)
+  const uint32_t nh = (n + 3) / 4;
+  const unsigned long long ob = reinterpret_cast<unsigned long long>(F.ord8 + uni(hd->obase));
+  const unsigned long long logp = reinterpret_cast<unsigned long long>(F.log + FL_TOUCH_MUL * beg);
+  const uint32_t vl16 = lane * 16u;
+  uint32_t voff, vt;
+  asm volatile(FL_PLAN_ASM
+               : [A0] "+s"(A0), [A1] "+s"(A1), [B0] "+s"(B0), [B1] "+s"(B1), [dl0] "+v"(Dp.l0),
+                 [dh0] "+v"(Dp.h0), [dl1] "+v"(Dp.l1), [dh1] "+v"(Dp.h1), [lk] "+v"(lg.lk), [la] "+v"(lg.la),
+                 [lb] "+v"(lg.lb), [nacc] "+s"(lg.nacc), [lpos] "+s"(lg.lpos), [voff] "=&v"(voff), [vt] "=&v"(vt)
+               : [ob] "s"(ob), [nh] "s"(nh), [logp] "s"(logp), [lcap] "s"(lg.lcap), [vl16] "v"(vl16)
+               : FL_PLAN_CLOBBERS, "scc", "vcc", "memory");
   if (lg.nacc) {
     if (lane < lg.nacc && lg.lpos + lg.nacc <= lg.lcap) lg.p[lg.lpos + lane] = v4(lg.lk, 0u, lg.la, lg.lb);
     lg.lpos += lg.nacc;

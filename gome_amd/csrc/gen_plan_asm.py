@@ -175,117 +175,104 @@ def emit_flush(fl: str, back: str):
 
 def order(r: tuple[int, int]):
     """Apply one packed record s[r] (SetOrder, engine.go:56-85, at the aggregate level).
-    The record's registers become the taker's remaining volume T in place."""
+    The record's registers become the taker's remaining volume T in place.  Layout: rests
+    (the most common outcome) fall through; crossing branches out; every path ends with one
+    jump to the next order.  Lane values of non-member levels are don't-care (a level that
+    empties is only dropped from its mask; a rest onto a non-member level writes instead of
+    adds; k_flow_plan zeroes non-member lanes once at the end)."""
     lo, hi = f"s{r[0]}", f"s{r[1]}"
     T = (lo, hi)
     TT = f"s[{r[0]}:{r[1]}]"
     nxt = fresh("NX")
-    sell, bloop, bfull, brest, btop, blog = (fresh(x) for x in ("SE", "BL", "BF", "BR", "BT", "BG"))
-    sloop, sfull, srest, stop, slog = (fresh(x) for x in ("SL", "SF", "SR", "ST", "SG"))
-    bdeep, sdeep = fresh("BD"), fresh("SD")
-    e(f"s_add_u32 {JJS}, {JJS}, 256")           # (order index + 1) << 8
-    e(f"s_bitcmp1_b32 {hi}, 29")                # padding / dropped ADD / ignored action
-    e(f"s_cbranch_scc1 {nxt}")
-    e(f"s_bfe_u32 {LI}, {hi}, 0x70015")
-    e(f"s_bitcmp1_b32 {hi}, 28")
-    e(f"s_cbranch_scc1 {sell}")
-    e(f"s_and_b32 {hi}, {hi}, 0x1fffff")        # T = volume
-    # ---------------- BUY: asks <= li, ascending (nodepool.go:86-104)
-    e(f"{bloop}:")
-    e(f"s_cmp_gt_u32 {BA}, {LI}")
-    e(f"s_cbranch_scc1 {brest}")
-    e(f"s_sub_u32 {D[0]}, {T[0]}, {BAD[0]}")
-    e(f"s_subb_u32 {D[1]}, {T[1]}, {BAD[1]}")
-    e(f"s_cbranch_scc0 {bfull}")
-    # partial fill of the best ask: depth -= T (engine.go:176-194)
-    e(f"s_sub_u32 {BAD[0]}, {BAD[0]}, {T[0]}")
-    e(f"s_subb_u32 {BAD[1]}, {BAD[1]}, {T[1]}")
-    e(f"s_or_b32 {K}, {JJS}, {BA}")
-    log(K, T[0], T[1], False)
-    e(f"s_branch {nxt}")
-    # the best ask empties (engine.go:145-175, ZREM nodepool.go:76-83); next ask
-    e(f"{bfull}:")
-    e(f"s_or_b32 {K}, {JJS}, {BA}")
-    log(K, BAD[0], BAD[1], True)
-    e(f"s_mov_b64 {TT}, s[{D[0][1:]}:{D[1][1:]}]")
-    write(BA, "0", "0")
-    setbit("A", BA, "s_bitset0_b64")
-    lowest_ask()
-    read(BA, BAD[0], BAD[1])
-    e(f"s_or_b32 {T0}, {T[0]}, {T[1]}")
-    e(f"s_cbranch_scc0 {nxt}")                  # diff == 0: stop (engine.go:162-175)
-    e(f"s_branch {bloop}")
-    # rest at li (engine.go:80-82): depth += T, ZADD S:BUY
-    e(f"{brest}:")
-    e(f"s_cmp_eq_u32 {LI}, {BB}")
-    e(f"s_cbranch_scc1 {btop}")
-    e(f"s_cmp_gt_u32 {LI}, {BB}")
-    e(f"s_cbranch_scc0 {bdeep}")
-    # new best bid inside the spread (its depth was 0): evict the old one to its lane
-    write(BB, BBD[0], BBD[1])
-    e(f"s_mov_b32 {BB}, {LI}")
-    e(f"s_mov_b64 s[{BBD[0][1:]}:{BBD[1][1:]}], {TT}")
-    setbit("B", LI, "s_bitset1_b64")
-    e(f"{blog}:")
-    e(f"s_or_b32 {K}, {JJS}, {LI}")
-    e(f"s_bitset1_b32 {K}, 7")
-    log(K, T[0], T[1], False)
-    e(f"s_branch {nxt}")
-    e(f"{btop}:")
-    e(f"s_add_u32 {BBD[0]}, {BBD[0]}, {T[0]}")
-    e(f"s_addc_u32 {BBD[1]}, {BBD[1]}, {T[1]}")
-    e(f"s_branch {blog}")
-    e(f"{bdeep}:")
-    add_lane(LI, T[0], T[1])
-    setbit("B", LI, "s_bitset1_b64")
-    e(f"s_branch {blog}")
-    # ---------------- SALE: bids >= li, descending (nodepool.go:105-115)
-    e(f"{sell}:")
-    e(f"s_and_b32 {hi}, {hi}, 0x1fffff")
-    e(f"{sloop}:")
-    e(f"s_cmp_lt_u32 {BB}, {LI}")
-    e(f"s_cbranch_scc1 {srest}")
-    e(f"s_sub_u32 {D[0]}, {T[0]}, {BBD[0]}")
-    e(f"s_subb_u32 {D[1]}, {T[1]}, {BBD[1]}")
-    e(f"s_cbranch_scc0 {sfull}")
-    e(f"s_sub_u32 {BBD[0]}, {BBD[0]}, {T[0]}")
-    e(f"s_subb_u32 {BBD[1]}, {BBD[1]}, {T[1]}")
-    e(f"s_or_b32 {K}, {JJS}, {BB}")
-    log(K, T[0], T[1], False)
-    e(f"s_branch {nxt}")
-    e(f"{sfull}:")
-    e(f"s_or_b32 {K}, {JJS}, {BB}")
-    log(K, BBD[0], BBD[1], True)
-    e(f"s_mov_b64 {TT}, s[{D[0][1:]}:{D[1][1:]}]")
-    write(BB, "0", "0")
-    setbit("B", BB, "s_bitset0_b64")
-    highest_bid()
-    read(BB, BBD[0], BBD[1])
-    e(f"s_or_b32 {T0}, {T[0]}, {T[1]}")
-    e(f"s_cbranch_scc0 {nxt}")
-    e(f"s_branch {sloop}")
-    e(f"{srest}:")
-    e(f"s_cmp_eq_u32 {LI}, {BA}")
-    e(f"s_cbranch_scc1 {stop}")
-    e(f"s_cmp_lt_u32 {LI}, {BA}")
-    e(f"s_cbranch_scc0 {sdeep}")
-    write(BA, BAD[0], BAD[1])
-    e(f"s_mov_b32 {BA}, {LI}")
-    e(f"s_mov_b64 s[{BAD[0][1:]}:{BAD[1][1:]}], {TT}")
-    setbit("A", LI, "s_bitset1_b64")
-    e(f"{slog}:")
-    e(f"s_or_b32 {K}, {JJS}, {LI}")
-    e(f"s_bitset1_b32 {K}, 7")
-    log(K, T[0], T[1], False)
-    e(f"s_branch {nxt}")
-    e(f"{stop}:")
-    e(f"s_add_u32 {BAD[0]}, {BAD[0]}, {T[0]}")
-    e(f"s_addc_u32 {BAD[1]}, {BAD[1]}, {T[1]}")
-    e(f"s_branch {slog}")
-    e(f"{sdeep}:")
-    add_lane(LI, T[0], T[1])
-    setbit("A", LI, "s_bitset1_b64")
-    e(f"s_branch {slog}")
+    for side in ("B", "S"):
+        if side == "B":
+            own, opp = "B", "A"            # rests into S:BUY, crosses S:SALE
+            top, topd, otop, otopd = BB, BBD, BA, BAD
+        else:
+            own, opp = "A", "B"
+            top, topd, otop, otopd = BA, BAD, BB, BBD
+        loop, cross, full, notdeep, newtop, istop, dnew = (fresh(side + x) for x in ("L", "C", "F", "N", "W", "T", "D"))
+        if side == "B":
+            e(f"s_add_u32 {JJS}, {JJS}, 256")           # (order index + 1) << 8
+            e(f"s_bitcmp1_b32 {hi}, 29")                # padding / dropped ADD / ignored action
+            e(f"s_cbranch_scc1 {nxt}")
+            e(f"s_bfe_u32 {LI}, {hi}, 0x70015")
+            e(f"s_bitcmp1_b32 {hi}, 28")
+            sell = fresh("SE")
+            e(f"s_cbranch_scc1 {sell}")
+        else:
+            e(f"{sell}:")
+        e(f"s_and_b32 {hi}, {hi}, 0x1fffff")            # T = volume
+        e(f"{loop}:")
+        # crossing opposite level? BUY: best ask <= li; SALE: best bid >= li
+        e(f"s_cmp_{'le' if side == 'B' else 'ge'}_u32 {otop}, {LI}")
+        e(f"s_cbranch_scc1 {cross}")
+        # ---- rest at li (engine.go:80-82): depth += T, ZADD own side
+        e(f"s_cmp_{'lt' if side == 'B' else 'gt'}_u32 {LI}, {top}")   # strictly behind own top
+        e(f"s_cbranch_scc0 {notdeep}")
+        e(f"s_cmp_lt_u32 {LI}, 64")
+        e(f"s_cselect_b64 {M}, %[{own}0], %[{own}1]")
+        e(f"s_bitcmp1_b64 {M}, {LI}")
+        e(f"s_cbranch_scc0 {dnew}")
+        add_lane(LI, T[0], T[1])                          # existing level: lane += T
+        e(f"s_or_b32 {K}, {JJS}, {LI}")
+        e(f"s_bitset1_b32 {K}, 7")
+        log(K, T[0], T[1], False)
+        e(f"s_branch {nxt}")
+        e(f"{dnew}:")                                     # new level behind the top: lane = T
+        e(f"s_bitset1_b64 {M}, {LI}")
+        e(f"s_cmp_lt_u32 {LI}, 64")
+        e(f"s_cselect_b64 %[{own}0], {M}, %[{own}0]")
+        e(f"s_cselect_b64 %[{own}1], %[{own}1], {M}")
+        write(LI, T[0], T[1])
+        e(f"s_or_b32 {K}, {JJS}, {LI}")
+        e(f"s_bitset1_b32 {K}, 7")
+        log(K, T[0], T[1], False)
+        e(f"s_branch {nxt}")
+        e(f"{notdeep}:")
+        e(f"s_cmp_eq_u32 {LI}, {top}")
+        e(f"s_cbranch_scc1 {istop}")
+        # new own top inside the spread: evict the cached top to its lane
+        write(top, topd[0], topd[1])
+        e(f"s_mov_b32 {top}, {LI}")
+        e(f"s_mov_b64 s[{topd[0][1:]}:{topd[1][1:]}], {TT}")
+        setbit(own, LI, "s_bitset1_b64")
+        e(f"s_or_b32 {K}, {JJS}, {LI}")
+        e(f"s_bitset1_b32 {K}, 7")
+        log(K, T[0], T[1], False)
+        e(f"s_branch {nxt}")
+        e(f"{istop}:")
+        e(f"s_add_u32 {topd[0]}, {topd[0]}, {T[0]}")
+        e(f"s_addc_u32 {topd[1]}, {topd[1]}, {T[1]}")
+        e(f"s_or_b32 {K}, {JJS}, {LI}")
+        e(f"s_bitset1_b32 {K}, 7")
+        log(K, T[0], T[1], False)
+        e(f"s_branch {nxt}")
+        # ---- cross the best opposite level (MatchOrder, engine.go:138-198)
+        e(f"{cross}:")
+        e(f"s_sub_u32 {D[0]}, {T[0]}, {otopd[0]}")
+        e(f"s_subb_u32 {D[1]}, {T[1]}, {otopd[1]}")
+        e(f"s_cbranch_scc0 {full}")
+        # partial: the level keeps depth - T (engine.go:176-194)
+        e(f"s_sub_u32 {otopd[0]}, {otopd[0]}, {T[0]}")
+        e(f"s_subb_u32 {otopd[1]}, {otopd[1]}, {T[1]}")
+        e(f"s_or_b32 {K}, {JJS}, {otop}")
+        log(K, T[0], T[1], False)
+        e(f"s_branch {nxt}")
+        # full: the level empties (engine.go:145-175), ZREM (nodepool.go:76-83), next level
+        e(f"{full}:")
+        e(f"s_or_b32 {K}, {JJS}, {otop}")
+        log(K, otopd[0], otopd[1], True)
+        e(f"s_mov_b64 {TT}, s[{D[0][1:]}:{D[1][1:]}]")
+        setbit(opp, otop, "s_bitset0_b64")
+        if side == "B":
+            lowest_ask()
+        else:
+            highest_bid()
+        read(otop, otopd[0], otopd[1])
+        e(f"s_or_b32 {T0}, {T[0]}, {T[1]}")
+        e(f"s_cbranch_scc0 {nxt}")                      # diff == 0: stop (engine.go:162-175)
+        e(f"s_branch {loop}")
     e(f"{nxt}:")
 
 

@@ -402,8 +402,10 @@ __global__ __launch_bounds__(64) void k_flow_plan(Dev D, FlowArgs F) {
     if (lane == 0) atomicOr(&D.st->err, ERR_CORRUPT);
     lg.lpos = 0;
   }
-  const int64_t f0 = static_cast<int64_t>((static_cast<uint64_t>(Dp.h0) << 32) | Dp.l0);
-  const int64_t f1 = static_cast<int64_t>((static_cast<uint64_t>(Dp.h1) << 32) | Dp.l1);
+  // lanes of levels outside both side sets are don't-care in the loop: their depth is 0
+  const bool in0 = (((A0 | B0) >> lane) & 1ull) != 0, in1 = (((A1 | B1) >> lane) & 1ull) != 0;
+  const int64_t f0 = in0 ? static_cast<int64_t>((static_cast<uint64_t>(Dp.h0) << 32) | Dp.l0) : 0;
+  const int64_t f1 = in1 ? static_cast<int64_t>((static_cast<uint64_t>(Dp.h1) << 32) | Dp.l1) : 0;
   if (v0) LV[lane].dfin = f0;
   if (v1) LV[lane + 64].dfin = f1;
   if (lane == 0) {

@@ -194,8 +194,6 @@ def order(r: tuple[int, int]):
         loop, cross, full, notdeep, newtop, istop, dnew = (fresh(side + x) for x in ("L", "C", "F", "N", "W", "T", "D"))
         if side == "B":
             e(f"s_add_u32 {JJS}, {JJS}, 256")           # (order index + 1) << 8
-            e(f"s_bitcmp1_b32 {hi}, 29")                # padding / dropped ADD / ignored action
-            e(f"s_cbranch_scc1 {nxt}")
             e(f"s_bfe_u32 {LI}, {hi}, 0x70015")
             e(f"s_bitcmp1_b32 {hi}, 28")
             sell = fresh("SE")

@@ -62,8 +62,11 @@ constexpr unsigned long long FL_KEY_OFF = 1ull << 62;
 __host__ __device__ constexpr uint32_t fl_obase(uint32_t beg, uint32_t seg) { return (beg + 8u * seg + 3u) & ~3u; }
 constexpr uint32_t FL_ORD8_MUL = 9, FL_ORD8_PAD = 64;  // ord8 capacity: 9 * max_batch + 64
 
-// packed order record of the plan (8 B): volume [0,53), level [53,60), SALE bit 60, skip 61
-constexpr uint32_t OR_LI_SHIFT = 21, OR_SELL = 1u << 28, OR_SKIP = 1u << 29;
+// packed order record of the plan (8 B): volume [0,53), level [53,60), SALE bit 60.  A record
+// that must not touch the book (dropped ADD, ignored action, padding) is 0: a zero-volume BUY
+// rest at sentinel level 0, which changes nothing and whose touch no later kernel reads.
+constexpr uint32_t OR_LI_SHIFT = 21, OR_SELL = 1u << 28;
+constexpr unsigned long long OR_NOP = 0ull;
 
 enum : uint32_t { TK_CONS = 0, TK_REST = 1 };
 
@@ -257,10 +260,10 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep(Dev D, BatchArgs B, Flo
   __syncthreads();
   const uint32_t obase = fl_obase(beg, seg);
   if (tid < ((4u - ((end - beg) & 3u)) & 3u))  // padding to whole half-groups
-    F.ord8[obase + (end - beg) + tid] = static_cast<unsigned long long>(OR_SKIP) << 32;
+    F.ord8[obase + (end - beg) + tid] = OR_NOP;
   for (uint32_t b = beg + tid; b < end; b += FL_PREP_T) {
     const Prep q = B.prep[b];
-    unsigned long long rec = static_cast<unsigned long long>(OR_SKIP) << 32;
+    unsigned long long rec = OR_NOP;
     if (q.action == GOME_ADD && q.adm) {
       const unsigned long long key = static_cast<unsigned long long>(q.price) + FL_KEY_OFF;
       uint32_t s = fl_hash(key);
@@ -440,7 +443,7 @@ __global__ __launch_bounds__(FL_SORT_T) void k_flow_sort(Dev D, FlowArgs F) {
   for (uint32_t t = tid; t < nt; t += FL_SORT_T) {
     const uint32_t kr = F.log[L + t].kr;
     atomicAdd(&hist[kr & 127u], 1u);
-    myr += (kr >> 7) & 1u;
+    myr += ((kr >> 7) & 1u) && (kr & 127u) ? 1u : 0u;  // level-0 touches are no-op records
   }
   if (myr) atomicAdd(&nrest, myr);
   __syncthreads();
@@ -737,7 +740,7 @@ __global__ void k_flow_count(Dev D, BatchArgs B, FlowArgs F) {
         pops += ne - (lend > c.c + c.a ? 1u : 0u);
       }
     }
-    B.ev_count[B.prep[beg + tk_j(x)].idx] = acc;
+    if (tk_j(x) < F.hdr[h].end - beg) B.ev_count[B.prep[beg + tk_j(x)].idx] = acc;  // not padding
   }
   // wave-reduce the counters, one atomic per wave
   for (int off = 32; off > 0; off >>= 1) {

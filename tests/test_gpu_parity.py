@@ -368,3 +368,29 @@ def test_flow_sweeps_and_long_chains_vs_legacy_counts():
     rec["oid_id"] = np.arange(1, n + 1)
     eng, orc = _run_pair(wl.split_batches(rec, 30000), 1, sample_syms=[0])
     assert eng.stats()["n_flow_books"] == 1
+
+
+def test_flow_dropped_and_ignored_records():
+    """Q4 duplicate ADD keys (later ones dropped) and unknown actions inside an ADD-only hot
+    book: they reach the plan as no-op records; events, state and n_flow_books as expected."""
+    rng = np.random.default_rng(2024)
+    st = wl.Stream(2, seed=2024)
+    eng = _engine(2, 20000)
+    orc = Oracle(2)
+    for _ in range(3):
+        b = st.batch(12000)
+        dup = rng.choice(len(b), 300, replace=False)
+        extra = b[dup].copy()                       # same (S, uuid, oid): admission drops them
+        extra["volume_fx"] = 10**6
+        ign = b[rng.choice(len(b), 200, replace=False)].copy()
+        ign["action"] = 7                           # consumed and ignored (engine.go:46-54)
+        mix = np.concatenate([b, extra, ign])
+        mix = mix[rng.permutation(len(mix))]
+        eng.submit(mix)
+        _cmp_events(eng.drain(), orc.submit(mix), "dropped/ignored")
+        s = eng.stats()
+        assert s["n_flow_books"] == 2 and s["n_dropped"] > 0
+    for s_ in range(2):
+        assert np.array_equal(eng.levels(s_), orc.levels(s_))
+        for p in orc.levels(s_)["price_fx"]:
+            assert np.array_equal(eng.fifo(s_, int(p)), orc.fifo(s_, int(p)))

@@ -252,13 +252,13 @@ gome_status gome_engine::init(const gome_config& c) {
   const uint64_t ntouch = static_cast<uint64_t>(FL_TOUCH_MUL) * nb;
   F.ig_cap = static_cast<uint32_t>(std::min<uint64_t>(std::max<uint64_t>(cfg.max_nodes, 1u << 16), 0xF0000000ull));
   F.enabled = (cfg.flags & GOME_FLAG_LEGACY_HOT) ? 0u : 1u;
-  if (!alloc(&F.hdr, MAX_HOT, "flow headers") || !alloc(&F.lvl, MAX_HOT * FL_CAP, "flow levels") ||
+  if (!alloc(&F.hdr, MAX_FLOW, "flow headers") || !alloc(&F.lvl, MAX_FLOW * FL_CAP, "flow levels") ||
       !alloc(&F.ord8, static_cast<uint64_t>(FL_ORD8_MUL) * nb + FL_ORD8_PAD, "flow records") || !alloc(&F.log, ntouch, "flow touch log") ||
       !alloc(&F.srt, ntouch, "flow level runs") || !alloc(&F.rs, ntouch, "flow new makers") ||
       !alloc(&F.fbase, ntouch, "flow fill bases") || !alloc(&F.ig, F.ig_cap, "flow gathered makers") ||
       !alloc(&F.ig_bump, 1, "flow gather bump") || !alloc(&F.toff, MAX_FLOW + 1, "flow touch offsets"))
     return GOME_E_CAPACITY;
-  HIPCHK(hipMemsetAsync(F.hdr, 0, sizeof(FlowHdr) * MAX_HOT, stream));
+  HIPCHK(hipMemsetAsync(F.hdr, 0, sizeof(FlowHdr) * MAX_FLOW, stream));
   HIPCHK(hipMemsetAsync(d_pend, 0, sizeof(PendEnt) * nb, stream));
   if (D.idx_mask >= PEND) return fail(GOME_E_INVAL, "gome_config.max_nodes too large (index > 2^31 slots)");
   HIPCHK(hipStreamSynchronize(stream));
@@ -352,7 +352,7 @@ gome_status gome_engine::run(const gome_order* d_ord, uint32_t n, hipStream_t s)
   B.arena_cap = arena_cap;
   B.ev_count = d_ev_count;
   const uint32_t grid = std::min<uint32_t>(n, cfg.max_symbols);
-  const uint32_t nhot_max = std::min<uint32_t>(MAX_HOT, grid);
+  const uint32_t nhot_max = std::min<uint32_t>(MAX_FLOW, grid);
   HIPCHK(hipEventRecord(evm0, s));
   HIPCHK(hipMemsetAsync(F.ig_bump, 0, 4, s));
   k_flow_prep<<<nhot_max, FL_PREP_T, 0, s>>>(D, B, F);
@@ -371,9 +371,10 @@ gome_status gome_engine::run(const gome_order* d_ord, uint32_t n, hipStream_t s)
   // legacy hot path (books the flow path declined)
   HIPCHK(hipStreamWaitEvent(hot_stream, fork, 0));
   HIPCHK(hipEventRecord(evh0, hot_stream));
-  k_match_hot<<<nhot_max, 64, HOT_LDS_BYTES, hot_stream>>>(D, B, d_pend, d_resume, F.hdr);
+  const uint32_t nleg = std::min<uint32_t>(MAX_HOT, grid);
+  k_match_hot<<<nleg, 64, HOT_LDS_BYTES, hot_stream>>>(D, B, d_pend, d_resume, F.hdr);
   HIPCHK(hipEventRecord(evh1, hot_stream));
-  k_match_resume<<<nhot_max, 64, 0, hot_stream>>>(D, B, d_resume);
+  k_match_resume<<<nleg, 64, 0, hot_stream>>>(D, B, d_resume);
   k_pend_apply<<<dim3(8, 64), 256, 0, hot_stream>>>(D, d_pend, d_seg_start, d_seg_order, B);
   HIPCHK(hipEventRecord(join, hot_stream));
   k_match<<<grid, 64, 0, s>>>(D, B, &F.hdr[0].ok, sizeof(FlowHdr) / sizeof(uint32_t));

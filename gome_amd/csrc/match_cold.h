@@ -31,6 +31,7 @@ constexpr uint32_t EVB = 32;      // events per arena block (cold books)
 constexpr uint32_t FLOW_MIN_LOG2 = 7;
 constexpr uint32_t MAX_FLOW = 4096;
 constexpr uint32_t LEGACY_HOT_MIN = 2048;
+constexpr uint32_t MAX_LEGACY = 256;  // candidates the legacy hot kernel may take (grid size)
 constexpr uint32_t EVB_HOT = 256; // events per arena block (hot books)
 
 // Wave-uniform context of the book being matched.
@@ -604,7 +605,9 @@ __global__ __launch_bounds__(64) void k_match(Dev D, BatchArgs B, const uint32_t
   if (blockIdx.x >= D.st->nseg || (D.st->err & ERR_INPUT)) return;
   const uint32_t seg = B.seg_order[blockIdx.x];
   const uint32_t beg = B.seg_start[seg], end = B.seg_start[seg + 1];
-  if (blockIdx.x < D.st->nhot && (flow_ok[blockIdx.x * ok_stride] || end - beg >= LEGACY_HOT_MIN)) return;
+  if (blockIdx.x < D.st->nhot &&
+      (flow_ok[blockIdx.x * ok_stride] || (end - beg >= LEGACY_HOT_MIN && blockIdx.x < MAX_LEGACY)))
+    return;
   WaveCtx W;
   wave_init(W, D, B, uni(B.ord[B.prep[beg].idx].symbol_id), EVB);
   process_global(W, beg, end);

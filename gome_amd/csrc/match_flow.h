@@ -826,7 +826,7 @@ __global__ void k_flow_events(Dev D, BatchArgs B, FlowArgs F, const uint32_t* ev
 // ============================================================== k_flow_write
 // One workgroup per flow book: append the surviving new makers to their FIFOs (chunks from
 // the free stack / bump pool), insert them into the cancel index, rewrite the level array.
-constexpr uint32_t FL_WRITE_T = 256;
+constexpr uint32_t FL_WRITE_T = 1024;
 
 __global__ __launch_bounds__(FL_WRITE_T) void k_flow_write(Dev D, BatchArgs B, FlowArgs F) {
   __shared__ Level lv[FL_CAP];

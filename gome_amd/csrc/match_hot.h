@@ -51,7 +51,7 @@ __device__ unsigned long long g_stamps[256 * NSTAMP];
 #define ST_ADD(i, v)
 #endif
 
-constexpr uint32_t MAX_HOT = MAX_FLOW;  // legacy hot kernel grid (candidates, see match_cold.h)
+constexpr uint32_t MAX_HOT = MAX_LEGACY;  // legacy hot kernel grid (see match_cold.h)
 constexpr uint32_t LRB_CAP = 128;  // levels held in lanes (2 register sets)
 constexpr uint32_t NCS = LRB_CAP;  // one head-chunk cache slot per resident level
 constexpr uint32_t CS_NONE = 0xFFu;
@@ -1346,7 +1346,7 @@ __global__ __launch_bounds__(64) void k_match_resume(Dev D, BatchArgs B, const R
 // slot into its chunk (HBM; the kernel has written its LDS caches back).
 __global__ void k_pend_apply(const Dev D, PendEnt* pend, const uint32_t* seg_start,
                              const uint32_t* seg_order, const BatchArgs B) {
-  const uint32_t nhot = D.st->nhot;
+  const uint32_t nhot = min(D.st->nhot, MAX_HOT);
   const unsigned long long mask = D.idx_mask;
   for (uint32_t h = blockIdx.y; h < nhot; h += gridDim.y) {
     const uint32_t seg = seg_order[h];

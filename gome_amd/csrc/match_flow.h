@@ -106,8 +106,11 @@ static_assert(sizeof(IgEnt) == 32, "IgEnt layout");
 struct FlowHdr {
   uint32_t ok, nl, sym, ntouch;
   uint32_t beg, end, nold, adds;
-  uint32_t dropped, rests, obase, pad1;  // obase: first packed record (4-aligned, padded)
+  uint32_t dropped, rests, obase, w32;   // obase: first packed record (4-aligned, padded);
+                                        // w32: the 32-bit plan (volumes / depths in units of g)
   unsigned long long amask[2], bmask[2];  // final S:SALE / S:BUY membership of the levels
+  unsigned long long g;                   // volume unit of the book's plan (1 for the 64-bit plan)
+  unsigned long long pad2;
 };
 
 struct FlowLvl {
@@ -149,6 +152,22 @@ __device__ __forceinline__ uint32_t fl_hash(unsigned long long key) {
   return static_cast<uint32_t>(mix64(key) >> 20) & (FL_HASH - 1);
 }
 
+// Binary GCD (Stein) of two 64-bit values; gcd(0, x) = x.
+__device__ __forceinline__ unsigned long long fl_gcd(unsigned long long a, unsigned long long b) {
+  if (a == 0) return b;
+  if (b == 0) return a;
+  const int sh = __builtin_ctzll(a | b);
+  a >>= __builtin_ctzll(a);
+  do {
+    b >>= __builtin_ctzll(b);
+    if (a > b) { const unsigned long long t = a; a = b; b = t; }
+    b -= a;
+  } while (b);
+  return a << sh;
+}
+
+constexpr unsigned long long FL_SUM_CAP = 1ull << 62;  // saturation of the volume sum
+
 // ============================================================== k_flow_prep
 __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep(Dev D, BatchArgs B, FlowArgs F) {
   __shared__ unsigned long long hkey[FL_HASH];
@@ -156,6 +175,7 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep(Dev D, BatchArgs B, Flo
   __shared__ unsigned long long ckey[FL_CAP + FL_PREP_T];
   __shared__ uint32_t cslot[FL_CAP + FL_PREP_T];
   __shared__ uint32_t ndist, nc, bad, adds, dropped;
+  __shared__ unsigned long long wg[FL_PREP_T / 64], ws[FL_PREP_T / 64];
   const uint32_t h = blockIdx.x, tid = threadIdx.x;
   if (h >= D.st->nhot) return;
   FlowHdr* hd = &F.hdr[h];
@@ -189,6 +209,7 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep(Dev D, BatchArgs B, Flo
   };
   // live levels of the book (clean invariant: live <=> nodes, positive depth, one side)
   const Level* L0 = D.lvl + bk.lvl_base;
+  unsigned long long mg = 0, msum = 0;  // gcd and (saturating) sum of every volume the plan sees
   if (!bad) {
     for (uint32_t k = tid; k < bk.n_lvl; k += FL_PREP_T) {
       const Level x = L0[k];
@@ -198,6 +219,8 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep(Dev D, BatchArgs B, Flo
         continue;
       }
       if (x.depth <= 0 || nm != 1) { bad = 1; continue; }
+      mg = fl_gcd(mg, static_cast<unsigned long long>(x.depth));
+      msum = min(msum + static_cast<unsigned long long>(x.depth), FL_SUM_CAP);
       insert(static_cast<unsigned long long>(x.price) + FL_KEY_OFF, k);
     }
   }
@@ -212,12 +235,19 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep(Dev D, BatchArgs B, Flo
       my_adds++;
       if (!q.adm) { my_drop++; continue; }
       if (q.vol == 0) { bad = 1; break; }
+      mg = fl_gcd(mg, static_cast<unsigned long long>(q.vol));
+      msum = min(msum + static_cast<unsigned long long>(q.vol), FL_SUM_CAP);
       insert(static_cast<unsigned long long>(q.price) + FL_KEY_OFF, NIL);
       if (bad) break;
     }
   }
   if (my_adds) atomicAdd(&adds, my_adds);
   if (my_drop) atomicAdd(&dropped, my_drop);
+  for (int off = 32; off > 0; off >>= 1) {
+    mg = fl_gcd(mg, __shfl_xor(mg, off));
+    msum = min(msum + __shfl_xor(msum, off), FL_SUM_CAP);
+  }
+  if (lane_id() == 0) { wg[tid >> 6] = mg; ws[tid >> 6] = msum; }
   __syncthreads();
   if (bad || ndist > FL_MAX) {
     if (tid == 0) hd->ok = 0;
@@ -259,6 +289,16 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep(Dev D, BatchArgs B, Flo
   }
   __syncthreads();
   const uint32_t obase = fl_obase(beg, seg);
+  // volume unit of the plan: the 32-bit plan runs when every depth the book can reach,
+  // counted in units of the gcd of all its volumes, fits 32 bits
+  unsigned long long g = 0, sum = 0;
+  for (uint32_t w = 0; w < FL_PREP_T / 64; ++w) {
+    g = fl_gcd(g, wg[w]);
+    sum = min(sum + ws[w], FL_SUM_CAP);
+  }
+  if (g == 0) g = 1;
+  const bool w32 = sum < FL_SUM_CAP && sum / g < (1ull << 32);
+  if (!w32) g = 1;
   if (tid < ((4u - ((end - beg) & 3u)) & 3u))  // padding to whole half-groups
     F.ord8[obase + (end - beg) + tid] = OR_NOP;
   for (uint32_t b = beg + tid; b < end; b += FL_PREP_T) {
@@ -269,9 +309,11 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep(Dev D, BatchArgs B, Flo
       uint32_t s = fl_hash(key);
       while (hkey[s] != key) s = (s + 1) & (FL_HASH - 1);
       const uint32_t li = hval[s];
-      const uint32_t hi = static_cast<uint32_t>(static_cast<unsigned long long>(q.vol) >> 32) |
-                          (li << OR_LI_SHIFT) | (q.side == GOME_SALE ? OR_SELL : 0u);
-      rec = (static_cast<unsigned long long>(hi) << 32) | static_cast<uint32_t>(q.vol);
+      // w32: the volume in units of g (exact: an integer quotient < 2^32 of doubles < 2^53)
+      const unsigned long long v = w32 ? static_cast<unsigned long long>(static_cast<double>(q.vol) / static_cast<double>(g))
+                                       : static_cast<unsigned long long>(q.vol);
+      const uint32_t hi = static_cast<uint32_t>(v >> 32) | (li << OR_LI_SHIFT) | (q.side == GOME_SALE ? OR_SELL : 0u);
+      rec = (static_cast<unsigned long long>(hi) << 32) | static_cast<uint32_t>(v);
     }
     F.ord8[obase + (b - beg)] = rec;
     B.ev_count[q.idx] = 0;
@@ -287,6 +329,8 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep(Dev D, BatchArgs B, Flo
     x.adds = adds;
     x.dropped = dropped;
     x.obase = obase;
+    x.w32 = w32 ? 1u : 0u;
+    x.g = g;
     *hd = x;
   }
 }
@@ -378,7 +422,13 @@ __global__ __launch_bounds__(64) void k_flow_plan(Dev D, FlowArgs F) {
   const uint32_t nl = uni(hd->nl), beg = uni(hd->beg), end = uni(hd->end), n = end - beg;
   FlowLvl* LV = F.lvl + h * FL_CAP;
   const bool v0 = lane >= 1 && lane <= nl, v1 = lane + 64 <= nl;
-  const int64_t d0 = v0 ? LV[lane].d0 : 0, d1 = v1 ? LV[lane + 64].d0 : 0;
+  const bool w32 = uni(hd->w32) != 0;
+  const unsigned long long g = static_cast<unsigned long long>(uni64(static_cast<int64_t>(hd->g)));
+  int64_t d0 = v0 ? LV[lane].d0 : 0, d1 = v1 ? LV[lane + 64].d0 : 0;
+  if (w32) {  // depths in units of g (exact: g divides every volume and depth of the book)
+    d0 = static_cast<int64_t>(static_cast<unsigned long long>(d0) / g);
+    d1 = static_cast<int64_t>(static_cast<unsigned long long>(d1) / g);
+  }
   const uint32_t m0 = v0 ? LV[lane].mem0 : 0u, m1 = v1 ? LV[lane + 64].mem0 : 0u;
   FlDepth Dp{lo32(d0), hi32(d0), lo32(d1), hi32(d1)};
   unsigned long long A0 = __ballot(m0 & M_SALE), A1 = __ballot(m1 & M_SALE) | (1ull << 63);
@@ -391,12 +441,15 @@ __global__ __launch_bounds__(64) void k_flow_plan(Dev D, FlowArgs F) {
   const unsigned long long logp = reinterpret_cast<unsigned long long>(F.log + FL_TOUCH_MUL * beg);
   const uint32_t vl16 = lane * 16u;
   uint32_t voff, vt;
-  asm volatile(FL_PLAN_ASM
-               : [A0] "+s"(A0), [A1] "+s"(A1), [B0] "+s"(B0), [B1] "+s"(B1), [dl0] "+v"(Dp.l0),
-                 [dh0] "+v"(Dp.h0), [dl1] "+v"(Dp.l1), [dh1] "+v"(Dp.h1), [lk] "+v"(lg.lk), [la] "+v"(lg.la),
-                 [lb] "+v"(lg.lb), [nacc] "+s"(lg.nacc), [lpos] "+s"(lg.lpos), [voff] "=&v"(voff), [vt] "=&v"(vt)
-               : [ob] "s"(ob), [nh] "s"(nh), [logp] "s"(logp), [lcap] "s"(lg.lcap), [vl16] "v"(vl16)
-               : FL_PLAN_CLOBBERS, "scc", "vcc", "memory");
+#define FL_PLAN_OPERANDS                                                                          \
+  : [A0] "+s"(A0), [A1] "+s"(A1), [B0] "+s"(B0), [B1] "+s"(B1), [dl0] "+v"(Dp.l0), [dh0] "+v"(Dp.h0),   \
+    [dl1] "+v"(Dp.l1), [dh1] "+v"(Dp.h1), [lk] "+v"(lg.lk), [la] "+v"(lg.la), [lb] "+v"(lg.lb),         \
+    [nacc] "+s"(lg.nacc), [lpos] "+s"(lg.lpos), [voff] "=&v"(voff), [vt] "=&v"(vt)                      \
+  : [ob] "s"(ob), [nh] "s"(nh), [logp] "s"(logp), [lcap] "s"(lg.lcap), [vl16] "v"(vl16)                \
+  : FL_PLAN_CLOBBERS, "scc", "vcc", "memory"
+  if (w32) asm volatile(FL_PLAN_ASM32 FL_PLAN_OPERANDS);
+  else asm volatile(FL_PLAN_ASM64 FL_PLAN_OPERANDS);
+#undef FL_PLAN_OPERANDS
   if (lg.nacc) {
     if (lane < lg.nacc && lg.lpos + lg.nacc <= lg.lcap) lg.p[lg.lpos + lane] = v4(lg.lk, 0u, lg.la, lg.lb);
     lg.lpos += lg.nacc;
@@ -407,8 +460,10 @@ __global__ __launch_bounds__(64) void k_flow_plan(Dev D, FlowArgs F) {
   }
   // lanes of levels outside both side sets are don't-care in the loop: their depth is 0
   const bool in0 = (((A0 | B0) >> lane) & 1ull) != 0, in1 = (((A1 | B1) >> lane) & 1ull) != 0;
-  const int64_t f0 = in0 ? static_cast<int64_t>((static_cast<uint64_t>(Dp.h0) << 32) | Dp.l0) : 0;
-  const int64_t f1 = in1 ? static_cast<int64_t>((static_cast<uint64_t>(Dp.h1) << 32) | Dp.l1) : 0;
+  const uint64_t u0 = w32 ? static_cast<uint64_t>(Dp.l0) * g : (static_cast<uint64_t>(Dp.h0) << 32) | Dp.l0;
+  const uint64_t u1 = w32 ? static_cast<uint64_t>(Dp.l1) * g : (static_cast<uint64_t>(Dp.h1) << 32) | Dp.l1;
+  const int64_t f0 = in0 ? static_cast<int64_t>(u0) : 0;
+  const int64_t f1 = in1 ? static_cast<int64_t>(u1) : 0;
   if (v0) LV[lane].dfin = f0;
   if (v1) LV[lane + 64].dfin = f1;
   if (lane == 0) {
@@ -434,6 +489,7 @@ __global__ __launch_bounds__(FL_SORT_T) void k_flow_sort(Dev D, FlowArgs F) {
   const uint32_t h = blockIdx.x, tid = threadIdx.x, w = tid >> 6;
   if (h >= D.st->nhot || !F.hdr[h].ok) return;
   const uint32_t nt = F.hdr[h].ntouch, L = FL_TOUCH_MUL * F.hdr[h].beg, nl = F.hdr[h].nl;
+  const unsigned long long g = F.hdr[h].g;
   FlowLvl* LV = F.lvl + h * FL_CAP;
   if (tid < FL_CAP) hist[tid] = 0;
   if (tid == 0) nrest = 0;
@@ -495,8 +551,10 @@ __global__ __launch_bounds__(FL_SORT_T) void k_flow_sort(Dev D, FlowArgs F) {
       e.t = t;
       e.pad = 0;
       const uint32_t pos = wc[w][k] + rank;
+      e.amt = static_cast<int64_t>(static_cast<unsigned long long>(x.amt) * g);  // plan units -> fixed point
       F.srt[L + pos] = e;
       F.log[L + t].pos = pos;
+      if (g != 1) F.log[L + t].amt = e.amt;
     }
     __syncthreads();
     for (uint32_t i = tid; i < FL_SORT_W * FL_CAP; i += FL_SORT_T) wc[i / FL_CAP][i % FL_CAP] = 0;

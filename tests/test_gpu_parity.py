@@ -394,3 +394,21 @@ def test_flow_dropped_and_ignored_records():
         assert np.array_equal(eng.levels(s_), orc.levels(s_))
         for p in orc.levels(s_)["price_fx"]:
             assert np.array_equal(eng.fifo(s_, int(p)), orc.fifo(s_, int(p)))
+
+
+@pytest.mark.parametrize("vmax", [2**20, 2**45])
+def test_flow_plan_widths(vmax):
+    """Volumes with gcd 1: small ones take the 32-bit plan, volumes up to 2^45 (sum/gcd beyond
+    2^32) the 64-bit plan.  Both exact against the oracle, FIFOs included."""
+    rng = np.random.default_rng(vmax % 1000003)
+    n = 24000
+    rec = np.zeros(n, wl.ORDER_DTYPE)
+    rec["symbol_id"] = rng.integers(0, 2, n)
+    rec["side"] = rng.integers(0, 2, n)
+    rec["price_fx"] = rng.integers(1, 90, n) * 10**6
+    rec["volume_fx"] = rng.integers(1, vmax, n)
+    rec["action"] = 1
+    rec["uuid_id"] = 5
+    rec["oid_id"] = np.arange(1, n + 1)
+    eng, orc = _run_pair(wl.split_batches(rec, 8000), 2, sample_syms=[0, 1])
+    assert eng.stats()["n_flow_books"] == 2

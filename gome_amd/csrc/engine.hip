@@ -79,10 +79,10 @@ struct gome_engine {
   gome_config cfg{};
   hipStream_t stream = nullptr;
   hipStream_t hot_stream = nullptr;
-  hipStream_t flow_stream = nullptr;
+  hipStream_t flow_stream = nullptr, flow2_stream = nullptr;
   bool own_stream = false;
   hipEvent_t fork{}, join{}, evh0{}, evh1{};
-  hipEvent_t joinf{}, evf0{}, evf1{};
+  hipEvent_t joinf{}, joinf2{}, prep_h{}, prep_t{}, evf0{}, evf1{};
   FlowArgs F{};
   Prep* d_prep = nullptr;
   PendEnt* d_pend = nullptr;
@@ -145,9 +145,13 @@ struct gome_engine {
     if (evm0) { (void)hipEventDestroy(evm0); (void)hipEventDestroy(evm1); }
     if (fork) { (void)hipEventDestroy(fork); (void)hipEventDestroy(join); }
     if (evh0) { (void)hipEventDestroy(evh0); (void)hipEventDestroy(evh1); }
-    if (evf0) { (void)hipEventDestroy(evf0); (void)hipEventDestroy(evf1); (void)hipEventDestroy(joinf); }
+    if (evf0) {
+      (void)hipEventDestroy(evf0); (void)hipEventDestroy(evf1); (void)hipEventDestroy(joinf);
+      (void)hipEventDestroy(joinf2); (void)hipEventDestroy(prep_h); (void)hipEventDestroy(prep_t);
+    }
     if (hot_stream) (void)hipStreamDestroy(hot_stream);
     if (flow_stream) (void)hipStreamDestroy(flow_stream);
+    if (flow2_stream) (void)hipStreamDestroy(flow2_stream);
     if (own_stream && stream) (void)hipStreamDestroy(stream);
   }
 
@@ -188,6 +192,10 @@ gome_status gome_engine::init(const gome_config& c) {
   HIPCHK(hipEventCreate(&evh1));
   HIPCHK(hipStreamCreateWithFlags(&flow_stream, hipStreamNonBlocking));
   HIPCHK(hipEventCreateWithFlags(&joinf, hipEventDisableTiming));
+  HIPCHK(hipStreamCreateWithFlags(&flow2_stream, hipStreamNonBlocking));
+  HIPCHK(hipEventCreateWithFlags(&joinf2, hipEventDisableTiming));
+  HIPCHK(hipEventCreateWithFlags(&prep_h, hipEventDisableTiming));
+  HIPCHK(hipEventCreateWithFlags(&prep_t, hipEventDisableTiming));
   HIPCHK(hipEventCreate(&evf0));
   HIPCHK(hipEventCreate(&evf1));
   HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_match_hot),
@@ -256,7 +264,7 @@ gome_status gome_engine::init(const gome_config& c) {
       !alloc(&F.ord8, static_cast<uint64_t>(FL_ORD8_MUL) * nb + FL_ORD8_PAD, "flow records") || !alloc(&F.log, ntouch, "flow touch log") ||
       !alloc(&F.srt, ntouch, "flow level runs") || !alloc(&F.rs, ntouch, "flow new makers") ||
       !alloc(&F.fbase, ntouch, "flow fill bases") || !alloc(&F.ig, F.ig_cap, "flow gathered makers") ||
-      !alloc(&F.ig_bump, 1, "flow gather bump") || !alloc(&F.toff, MAX_FLOW + 1, "flow touch offsets"))
+      !alloc(&F.ig_bump, 1, "flow gather bump") || !alloc(&F.toff, MAX_FLOW + 2, "flow touch offsets"))
     return GOME_E_CAPACITY;
   HIPCHK(hipMemsetAsync(F.hdr, 0, sizeof(FlowHdr) * MAX_FLOW, stream));
   HIPCHK(hipMemsetAsync(d_pend, 0, sizeof(PendEnt) * nb, stream));
@@ -355,21 +363,46 @@ gome_status gome_engine::run(const gome_order* d_ord, uint32_t n, hipStream_t s)
   const uint32_t nhot_max = std::min<uint32_t>(MAX_FLOW, grid);
   HIPCHK(hipEventRecord(evm0, s));
   HIPCHK(hipMemsetAsync(F.ig_bump, 0, 4, s));
-  k_flow_prep<<<nhot_max, FL_PREP_T, 0, s>>>(D, B, F);
   HIPCHK(hipEventRecord(fork, s));
-  // flow path: serial plan of each eligible hot book, then its parallel reconstruction
+  // flow path: the head (longest FL_HEAD candidates, the batch's critical path) and the tail
+  // each run prep -> serial plan -> parallel reconstruction on their own stream, so the
+  // hottest book's plan starts after its own prep and the tail overlaps it
+  FlowArgs FH = F, FT = F;
+  FH.h0 = 0; FH.h1 = FL_HEAD; FH.tb = 0;
+  FT.h0 = FL_HEAD; FT.h1 = MAX_FLOW; FT.tb = FL_HEAD + 1;
+  const uint32_t nh_head = std::min<uint32_t>(FL_HEAD, nhot_max);
+  const uint32_t nh_tail = nhot_max > FL_HEAD ? nhot_max - FL_HEAD : 0;
   HIPCHK(hipStreamWaitEvent(flow_stream, fork, 0));
+  k_flow_prep<<<nh_head, FL_PREP_T, 0, flow_stream>>>(D, B, FH);
+  HIPCHK(hipEventRecord(prep_h, flow_stream));
   HIPCHK(hipEventRecord(evf0, flow_stream));
-  k_flow_plan<<<nhot_max, 64, 0, flow_stream>>>(D, F);
+  k_flow_plan<true><<<nh_head, 256, 0, flow_stream>>>(D, FH);
   HIPCHK(hipEventRecord(evf1, flow_stream));
-  k_flow_sort<<<nhot_max, FL_SORT_T, 0, flow_stream>>>(D, F);
-  k_flow_level<<<nhot_max, FL_LEVEL_T, 0, flow_stream>>>(D, F);
-  k_flow_toff<<<1, 1024, 0, flow_stream>>>(D, F);
-  k_flow_count<<<1024, 256, 0, flow_stream>>>(D, B, F);
-  k_flow_write<<<nhot_max, FL_WRITE_T, 0, flow_stream>>>(D, B, F);
+  k_flow_sort<<<nh_head, FL_SORT_T, 0, flow_stream>>>(D, FH);
+  k_flow_level<<<nh_head, FL_LEVEL_T, 0, flow_stream>>>(D, FH);
+  k_flow_toff<<<1, 1024, 0, flow_stream>>>(D, FH);
+  k_flow_count<<<1024, 256, 0, flow_stream>>>(D, B, FH);
+  k_flow_write<<<nh_head, FL_WRITE_T, 0, flow_stream>>>(D, B, FH);
   HIPCHK(hipEventRecord(joinf, flow_stream));
-  // legacy hot path (books the flow path declined)
+  // The tail's chain and the legacy hot kernels share the third stream: HIP maps more
+  // streams than hardware queues (4 per process, one taken by the caller) onto shared
+  // queues, which would serialise them behind the head.
   HIPCHK(hipStreamWaitEvent(hot_stream, fork, 0));
+  if (nh_tail) {
+    k_flow_prep<<<nh_tail, FL_PREP_T, 0, hot_stream>>>(D, B, FT);
+    HIPCHK(hipEventRecord(prep_t, hot_stream));
+    k_flow_plan<false><<<nh_tail, 64, 0, hot_stream>>>(D, FT);
+    k_flow_sort<<<nh_tail, FL_SORT_T, 0, hot_stream>>>(D, FT);
+    k_flow_level<<<nh_tail, FL_LEVEL_T, 0, hot_stream>>>(D, FT);
+    k_flow_toff<<<1, 1024, 0, hot_stream>>>(D, FT);
+    k_flow_count<<<1024, 256, 0, hot_stream>>>(D, B, FT);
+    k_flow_write<<<nh_tail, FL_WRITE_T, 0, hot_stream>>>(D, B, FT);
+  } else {
+    HIPCHK(hipEventRecord(prep_t, hot_stream));
+  }
+  // legacy hot path (books the flow path declined); it and the cold kernel read the preps'
+  // routing decisions (FlowHdr::ok)
+  HIPCHK(hipStreamWaitEvent(hot_stream, prep_h, 0));
   HIPCHK(hipEventRecord(evh0, hot_stream));
   const uint32_t nleg = std::min<uint32_t>(MAX_HOT, grid);
   k_match_hot<<<nleg, 64, HOT_LDS_BYTES, hot_stream>>>(D, B, d_pend, d_resume, F.hdr);
@@ -377,15 +410,19 @@ gome_status gome_engine::run(const gome_order* d_ord, uint32_t n, hipStream_t s)
   k_match_resume<<<nleg, 64, 0, hot_stream>>>(D, B, d_resume);
   k_pend_apply<<<dim3(8, 64), 256, 0, hot_stream>>>(D, d_pend, d_seg_start, d_seg_order, B);
   HIPCHK(hipEventRecord(join, hot_stream));
-  k_match<<<grid, 64, 0, s>>>(D, B, &F.hdr[0].ok, sizeof(FlowHdr) / sizeof(uint32_t));
+  HIPCHK(hipStreamWaitEvent(s, prep_h, 0));
+  HIPCHK(hipStreamWaitEvent(s, prep_t, 0));
+  k_match<<<std::min<uint32_t>(grid, COLD_BLOCKS), 64, 0, s>>>(D, B, &F.hdr[0].ok, sizeof(FlowHdr) / sizeof(uint32_t));
   HIPCHK(hipStreamWaitEvent(s, join, 0));
   HIPCHK(hipStreamWaitEvent(s, joinf, 0));
+
   HIPCHK(hipEventRecord(evm1, s));
 
   // ---- event compaction into publish order
   scan(d_ev_count, n, d_ev_off, &d_st->n_events, s);
   k_ev_scatter<<<2048, T256, 0, s>>>(d_arena, arena_cap, d_st, d_ev_off, d_events);
-  k_flow_events<<<1024, 256, 0, s>>>(D, B, F, d_ev_off, d_events);
+  k_flow_events<<<1024, 256, 0, s>>>(D, B, FH, d_ev_off, d_events);
+  if (nh_tail) k_flow_events<<<1024, 256, 0, s>>>(D, B, FT, d_ev_off, d_events);
   k_recycle_copy<<<256, 256, 0, s>>>(D);
   k_recycle_fin<<<1, 64, 0, s>>>(D);
   HIPCHK(hipGetLastError());

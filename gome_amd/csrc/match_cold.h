@@ -31,7 +31,11 @@ constexpr uint32_t EVB = 32;      // events per arena block (cold books)
 constexpr uint32_t FLOW_MIN_LOG2 = 7;
 constexpr uint32_t MAX_FLOW = 4096;
 constexpr uint32_t LEGACY_HOT_MIN = 2048;
-constexpr uint32_t MAX_LEGACY = 256;  // candidates the legacy hot kernel may take (grid size)
+constexpr uint32_t MAX_LEGACY = 256;
+#ifndef GOME_COLD_BLOCKS
+#define GOME_COLD_BLOCKS 256
+#endif
+constexpr uint32_t COLD_BLOCKS = GOME_COLD_BLOCKS;  // persistent cold-kernel blocks  // candidates the legacy hot kernel may take (grid size)
 constexpr uint32_t EVB_HOT = 256; // events per arena block (hot books)
 
 // Wave-uniform context of the book being matched.
@@ -601,17 +605,21 @@ __device__ __forceinline__ void wave_init(WaveCtx& W, const Dev& D, const BatchA
 // Cold books: one 64-thread workgroup (one wavefront) per book, state in HBM.  Block i
 // takes seg_order[i]; flow candidates are skipped unless the flow path declined them and
 // they are too short for the legacy hot kernel (`flow_ok[i]`: FlowHdr::ok of candidate i).
+// Persistent: block b takes books b, b + gridDim.x, ...  (a bounded number of waves in
+// flight keeps the cold books' latency-bound traffic from slowing the flow plan's loads;
+// they have slack: the plan of the hottest book is the batch's critical path).
 __global__ __launch_bounds__(64) void k_match(Dev D, BatchArgs B, const uint32_t* flow_ok, uint32_t ok_stride) {
-  if (blockIdx.x >= D.st->nseg || (D.st->err & ERR_INPUT)) return;
-  const uint32_t seg = B.seg_order[blockIdx.x];
-  const uint32_t beg = B.seg_start[seg], end = B.seg_start[seg + 1];
-  if (blockIdx.x < D.st->nhot &&
-      (flow_ok[blockIdx.x * ok_stride] || (end - beg >= LEGACY_HOT_MIN && blockIdx.x < MAX_LEGACY)))
-    return;
-  WaveCtx W;
-  wave_init(W, D, B, uni(B.ord[B.prep[beg].idx].symbol_id), EVB);
-  process_global(W, beg, end);
-  wave_finish(W);
+  if (D.st->err & ERR_INPUT) return;
+  const uint32_t nseg = D.st->nseg, nhot = D.st->nhot;
+  for (uint32_t i = blockIdx.x; i < nseg; i += gridDim.x) {
+    const uint32_t seg = B.seg_order[i];
+    const uint32_t beg = B.seg_start[seg], end = B.seg_start[seg + 1];
+    if (i < nhot && (flow_ok[i * ok_stride] || (end - beg >= LEGACY_HOT_MIN && i < MAX_LEGACY))) continue;
+    WaveCtx W;
+    wave_init(W, D, B, uni(B.ord[B.prep[beg].idx].symbol_id), EVB);
+    process_global(W, beg, end);
+    wave_finish(W);
+  }
 }
 
 

@@ -54,6 +54,7 @@ constexpr uint32_t FL_MAX = FL_CAP - 2;   // usable levels 1..126: slot 0 is the
                                           // slot 127 the ask sentinel (bit scans never miss)
 constexpr uint32_t FL_HASH = 1024;        // LDS price-set slots in k_flow_prep
 constexpr uint32_t FL_PREP_T = 1024;
+constexpr uint32_t FL_HEAD = 8;           // longest candidates on the critical-path stream
 constexpr uint32_t FL_TOUCH_MUL = 5;      // log capacity per order (touches <= 3n + L0, plus
                                           // 64 entries of staging slack, n >= 128)
 constexpr unsigned long long FL_KEY_OFF = 1ull << 62;
@@ -143,10 +144,14 @@ struct FlowArgs {
   IgEnt* ig;
   uint32_t ig_cap;
   uint32_t* ig_bump;
-  uint32_t* toff;      // [MAX_FLOW + 1] exclusive scan of the books' touch counts
+  uint32_t* toff;      // [MAX_FLOW + 2] per range: exclusive scan of the books' touch counts
   uint32_t enabled;
-  uint32_t pad;
+  // the candidates [h0, min(h1, nhot)) this launch covers (head and tail run on their own
+  // streams), and the range's offset in toff
+  uint32_t h0, h1, tb;
 };
+
+__device__ __forceinline__ uint32_t fl_hend(const Dev& D, const FlowArgs& F) { return min(F.h1, D.st->nhot); }
 
 __device__ __forceinline__ uint32_t fl_hash(unsigned long long key) {
   return static_cast<uint32_t>(mix64(key) >> 20) & (FL_HASH - 1);
@@ -176,8 +181,8 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep(Dev D, BatchArgs B, Flo
   __shared__ uint32_t cslot[FL_CAP + FL_PREP_T];
   __shared__ uint32_t ndist, nc, bad, adds, dropped;
   __shared__ unsigned long long wg[FL_PREP_T / 64], ws[FL_PREP_T / 64];
-  const uint32_t h = blockIdx.x, tid = threadIdx.x;
-  if (h >= D.st->nhot) return;
+  const uint32_t h = F.h0 + blockIdx.x, tid = threadIdx.x;
+  if (h >= fl_hend(D, F)) return;
   FlowHdr* hd = &F.hdr[h];
   const uint32_t seg = B.seg_order[h];
   const uint32_t beg = B.seg_start[seg], end = B.seg_start[seg + 1];
@@ -412,11 +417,27 @@ struct FlLog {
 
 
 
-__global__ __launch_bounds__(64) void k_flow_plan(Dev D, FlowArgs F) {
-  const uint32_t h = blockIdx.x;
-  if (h >= D.st->nhot) return;
+__device__ __forceinline__ void fl_plan_book(const Dev& D, const FlowArgs& F, uint32_t h);
+
+// EXCL: the block is 4 waves that each hold the whole register file of their SIMD (all 512
+// VGPR+AGPR), so no other wave can share the CU — in particular not its scalar unit, which
+// every instruction of the plan's critical path uses.  Waves 1-3 park at the barrier.
+template <bool EXCL>
+__global__ __launch_bounds__(EXCL ? 256 : 64) void k_flow_plan(Dev D, FlowArgs F) {
+  if (EXCL) {
+    asm volatile("" ::: "v255", "a255");
+    if (threadIdx.x >= 64) {
+      __syncthreads();
+      return;
+    }
+  }
+  const uint32_t h = F.h0 + blockIdx.x;
+  if (h < fl_hend(D, F) && uni(F.hdr[h].ok)) fl_plan_book(D, F, h);
+  if (EXCL) __syncthreads();
+}
+
+__device__ __forceinline__ void fl_plan_book(const Dev& D, const FlowArgs& F, uint32_t h) {
   const FlowHdr* hd = &F.hdr[h];
-  if (!uni(hd->ok)) return;
   __builtin_amdgcn_s_setprio(3);
   const uint32_t lane = lane_id();
   const uint32_t nl = uni(hd->nl), beg = uni(hd->beg), end = uni(hd->end), n = end - beg;
@@ -486,8 +507,8 @@ __global__ __launch_bounds__(FL_SORT_T) void k_flow_sort(Dev D, FlowArgs F) {
   __shared__ uint32_t hist[FL_CAP], run[FL_CAP];
   __shared__ uint32_t wc[FL_SORT_W][FL_CAP];
   __shared__ uint32_t nrest;
-  const uint32_t h = blockIdx.x, tid = threadIdx.x, w = tid >> 6;
-  if (h >= D.st->nhot || !F.hdr[h].ok) return;
+  const uint32_t h = F.h0 + blockIdx.x, tid = threadIdx.x, w = tid >> 6;
+  if (h >= fl_hend(D, F) || !F.hdr[h].ok) return;
   const uint32_t nt = F.hdr[h].ntouch, L = FL_TOUCH_MUL * F.hdr[h].beg, nl = F.hdr[h].nl;
   const unsigned long long g = F.hdr[h].g;
   FlowLvl* LV = F.lvl + h * FL_CAP;
@@ -689,8 +710,8 @@ __device__ __forceinline__ void fl_level_one(const Dev& D, const FlowArgs& F, ui
 
 constexpr uint32_t FL_LEVEL_T = 1024;
 __global__ __launch_bounds__(FL_LEVEL_T) void k_flow_level(Dev D, FlowArgs F) {
-  const uint32_t h = blockIdx.x;
-  if (h >= D.st->nhot || !F.hdr[h].ok) return;
+  const uint32_t h = F.h0 + blockIdx.x;
+  if (h >= fl_hend(D, F) || !F.hdr[h].ok) return;
   const uint32_t nl = F.hdr[h].nl;
   for (uint32_t q = 1 + (threadIdx.x >> 6); q <= nl; q += FL_LEVEL_T / 64) fl_level_one(D, F, h, uni(q));
 }
@@ -742,10 +763,11 @@ __device__ __forceinline__ FlTouchCtx fl_touch_ctx(const FlowArgs& F, uint32_t h
 
 // Book of flattened touch index gt: the last h with toff[h] <= gt.
 __device__ __forceinline__ uint32_t fl_book_of(const FlowArgs& F, uint32_t nb, uint32_t gt) {
+  const uint32_t* to = F.toff + F.tb;
   uint32_t lo = 0, hi = nb;
   while (hi - lo > 1) {
     const uint32_t mid = (lo + hi) >> 1;
-    if (F.toff[mid] <= gt) lo = mid; else hi = mid;
+    if (to[mid] <= gt) lo = mid; else hi = mid;
   }
   return lo;
 }
@@ -753,22 +775,24 @@ __device__ __forceinline__ uint32_t fl_book_of(const FlowArgs& F, uint32_t nb, u
 // Exclusive scan of the flow books' touch counts (declined candidates count 0).
 __global__ __launch_bounds__(1024) void k_flow_toff(Dev D, FlowArgs F) {
   __shared__ uint32_t part[1024];
-  const uint32_t nb = D.st->nhot, tid = threadIdx.x;
+  const uint32_t hend = fl_hend(D, F), nb = hend > F.h0 ? hend - F.h0 : 0u, tid = threadIdx.x;
+  const FlowHdr* hdr = F.hdr + F.h0;
+  uint32_t* toff = F.toff + F.tb;
   const uint32_t per = (nb + 1023) / 1024, b0 = tid * per;
   uint32_t s = 0;
-  for (uint32_t i = b0; i < b0 + per && i < nb; ++i) s += F.hdr[i].ok ? F.hdr[i].ntouch : 0u;
+  for (uint32_t i = b0; i < b0 + per && i < nb; ++i) s += hdr[i].ok ? hdr[i].ntouch : 0u;
   part[tid] = s;
   __syncthreads();
   if (tid == 0) {
     uint32_t acc = 0;
     for (uint32_t i = 0; i < 1024; ++i) { const uint32_t v = part[i]; part[i] = acc; acc += v; }
-    F.toff[nb] = acc;
+    toff[nb] = acc;
   }
   __syncthreads();
   uint32_t acc = part[tid];
   for (uint32_t i = b0; i < b0 + per && i < nb; ++i) {
-    F.toff[i] = acc;
-    acc += F.hdr[i].ok ? F.hdr[i].ntouch : 0u;
+    toff[i] = acc;
+    acc += hdr[i].ok ? hdr[i].ntouch : 0u;
   }
 }
 
@@ -776,10 +800,11 @@ __global__ __launch_bounds__(1024) void k_flow_toff(Dev D, FlowArgs F) {
 // Thread per touch; the first touch of each order walks the order's touches (consecutive
 // in the log, best level first), fixing fill_idx bases and ev_count[taker].
 __global__ void k_flow_count(Dev D, BatchArgs B, FlowArgs F) {
-  const uint32_t nb = D.st->nhot, total = F.toff[nb];
+  const uint32_t hend = fl_hend(D, F), nb = hend > F.h0 ? hend - F.h0 : 0u;
+  const uint32_t total = nb ? F.toff[F.tb + nb] : 0u;
   unsigned long long fills = 0, pops = 0;
   for (uint32_t gt = blockIdx.x * blockDim.x + threadIdx.x; gt < total; gt += gridDim.x * blockDim.x) {
-    const uint32_t h = fl_book_of(F, nb, gt), t = gt - F.toff[h];
+    const uint32_t hb = fl_book_of(F, nb, gt), h = F.h0 + hb, t = gt - F.toff[F.tb + hb];
     const uint32_t nt = F.hdr[h].ntouch, beg = F.hdr[h].beg, L = FL_TOUCH_MUL * beg;
     const Touch x = F.log[L + t];
     if (t > 0 && tk_j(F.log[L + t - 1]) == tk_j(x)) continue;
@@ -815,9 +840,10 @@ __global__ void k_flow_count(Dev D, BatchArgs B, FlowArgs F) {
 // ============================================================== k_flow_events
 // After the publish-order scan: every fill event at out[ev_off[taker] + fill_idx].
 __global__ void k_flow_events(Dev D, BatchArgs B, FlowArgs F, const uint32_t* ev_off, gome_event* out) {
-  const uint32_t nb = D.st->nhot, total = F.toff[nb];
+  const uint32_t hend = fl_hend(D, F), nb = hend > F.h0 ? hend - F.h0 : 0u;
+  const uint32_t total = nb ? F.toff[F.tb + nb] : 0u;
   for (uint32_t gt = blockIdx.x * blockDim.x + threadIdx.x; gt < total; gt += gridDim.x * blockDim.x) {
-    const uint32_t h = fl_book_of(F, nb, gt), t = gt - F.toff[h];
+    const uint32_t hb = fl_book_of(F, nb, gt), h = F.h0 + hb, t = gt - F.toff[F.tb + hb];
     const uint32_t beg = F.hdr[h].beg, L = FL_TOUCH_MUL * beg, sym = F.hdr[h].sym;
     const Touch x = F.log[L + t];
     if (((x.kr >> 7) & 1u) != TK_CONS) continue;
@@ -890,8 +916,8 @@ __global__ __launch_bounds__(FL_WRITE_T) void k_flow_write(Dev D, BatchArgs B, F
   __shared__ Level lv[FL_CAP];
   __shared__ uint32_t keep[FL_CAP];
   __shared__ uint32_t nout_s, base_s, cap_s;
-  const uint32_t h = blockIdx.x;
-  if (h >= D.st->nhot || !F.hdr[h].ok) return;
+  const uint32_t h = F.h0 + blockIdx.x;
+  if (h >= fl_hend(D, F) || !F.hdr[h].ok) return;
   const FlowHdr hd = F.hdr[h];
   const uint32_t lane = lane_id(), w = threadIdx.x >> 6, nw = FL_WRITE_T / 64;
   const uint32_t L = FL_TOUCH_MUL * hd.beg;

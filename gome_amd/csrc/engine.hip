@@ -264,8 +264,11 @@ gome_status gome_engine::init(const gome_config& c) {
       !alloc(&F.ord8, static_cast<uint64_t>(FL_ORD8_MUL) * nb + FL_ORD8_PAD, "flow records") || !alloc(&F.log, ntouch, "flow touch log") ||
       !alloc(&F.srt, ntouch, "flow level runs") || !alloc(&F.rs, ntouch, "flow new makers") ||
       !alloc(&F.fbase, ntouch, "flow fill bases") || !alloc(&F.ig, F.ig_cap, "flow gathered makers") ||
-      !alloc(&F.ig_bump, 1, "flow gather bump") || !alloc(&F.toff, MAX_FLOW + 2, "flow touch offsets"))
+      !alloc(&F.ig_bump, 1, "flow gather bump") || !alloc(&F.toff, MAX_FLOW + 2, "flow touch offsets") ||
+      !alloc(&F.lvout, static_cast<size_t>(MAX_FLOW) * FL_CAP, "flow final levels"))
     return GOME_E_CAPACITY;
+  F.maxt = ceil_div(ntouch, FL_TILE);
+  if (!alloc(&F.tcnt, static_cast<size_t>(FL_HEAD) * F.maxt * FL_CAP, "flow head tile counts")) return GOME_E_CAPACITY;
   HIPCHK(hipMemsetAsync(F.hdr, 0, sizeof(FlowHdr) * MAX_FLOW, stream));
   HIPCHK(hipMemsetAsync(d_pend, 0, sizeof(PendEnt) * nb, stream));
   if (D.idx_mask >= PEND) return fail(GOME_E_INVAL, "gome_config.max_nodes too large (index > 2^31 slots)");
@@ -378,11 +381,15 @@ gome_status gome_engine::run(const gome_order* d_ord, uint32_t n, hipStream_t s)
   HIPCHK(hipEventRecord(evf0, flow_stream));
   k_flow_plan<true><<<nh_head, 256, 0, flow_stream>>>(D, FH);
   HIPCHK(hipEventRecord(evf1, flow_stream));
-  k_flow_sort<<<nh_head, FL_SORT_T, 0, flow_stream>>>(D, FH);
-  k_flow_level<<<nh_head, FL_LEVEL_T, 0, flow_stream>>>(D, FH);
+  // the head's reconstruction: wide kernels (tile-parallel sort, one wave per level)
+  k_flow_sort_cnt<<<dim3(FL_SORT_GRID, nh_head), FL_TILE, 0, flow_stream>>>(D, FH);
+  k_flow_sort_scan<<<nh_head, FL_CAP, 0, flow_stream>>>(D, FH);
+  k_flow_sort_scatter<<<dim3(FL_SORT_GRID, nh_head), FL_TILE, 0, flow_stream>>>(D, FH);
+  k_flow_level_wide<<<dim3(FL_CAP, nh_head), 64, 0, flow_stream>>>(D, FH);
   k_flow_toff<<<1, 1024, 0, flow_stream>>>(D, FH);
   k_flow_count<<<1024, 256, 0, flow_stream>>>(D, B, FH);
-  k_flow_write<<<nh_head, FL_WRITE_T, 0, flow_stream>>>(D, B, FH);
+  k_flow_write_lv<<<dim3(FL_CAP, nh_head), 64, 0, flow_stream>>>(D, B, FH);
+  k_flow_write_fin<<<nh_head, 128, 0, flow_stream>>>(D, FH);
   HIPCHK(hipEventRecord(joinf, flow_stream));
   // The tail's chain and the legacy hot kernels share the third stream: HIP maps more
   // streams than hardware queues (4 per process, one taken by the caller) onto shared

@@ -145,6 +145,9 @@ struct FlowArgs {
   uint32_t ig_cap;
   uint32_t* ig_bump;
   uint32_t* toff;      // [MAX_FLOW + 2] per range: exclusive scan of the books' touch counts
+  uint32_t* tcnt;      // head sort: [FL_HEAD][maxt][FL_CAP] per-tile level counts, then offsets
+  Level* lvout;        // head write: [MAX_FLOW * FL_CAP] final level records
+  uint32_t maxt;       // tiles per head book (log capacity / FL_TILE)
   uint32_t enabled;
   // the candidates [h0, min(h1, nhot)) this launch covers (head and tail run on their own
   // streams), and the range's offset in toff
@@ -912,125 +915,122 @@ __global__ void k_flow_events(Dev D, BatchArgs B, FlowArgs F, const uint32_t* ev
 // the free stack / bump pool), insert them into the cancel index, rewrite the level array.
 constexpr uint32_t FL_WRITE_T = 1024;
 
-__global__ __launch_bounds__(FL_WRITE_T) void k_flow_write(Dev D, BatchArgs B, FlowArgs F) {
-  __shared__ Level lv[FL_CAP];
-  __shared__ uint32_t keep[FL_CAP];
-  __shared__ uint32_t nout_s, base_s, cap_s;
-  const uint32_t h = F.h0 + blockIdx.x;
-  if (h >= fl_hend(D, F) || !F.hdr[h].ok) return;
-  const FlowHdr hd = F.hdr[h];
-  const uint32_t lane = lane_id(), w = threadIdx.x >> 6, nw = FL_WRITE_T / 64;
+// Append level q's surviving new makers to its FIFO, insert them into the cancel index, and
+// return (on every lane) the level's final record.
+__device__ __forceinline__ Level fl_write_level(const Dev& D, const BatchArgs& B, const FlowArgs& F,
+                                                const FlowHdr& hd, uint32_t h, uint32_t q) {
+  const uint32_t lane = lane_id();
   const uint32_t L = FL_TOUCH_MUL * hd.beg;
   const unsigned long long mask = D.idx_mask;
-  for (uint32_t q = 1 + w; q <= hd.nl; q += nw) {
-    const FlowLvl f = F.lvl[h * FL_CAP + q];
-    const RsEnt* RS = F.rs + L + f.base;
-    // first new maker that survives the batch
-    uint32_t rf = 0;
-    if (f.cfin > f.d0) {
-      uint32_t lo = 0, hi = f.nrest;  // first r with e + v > cfin
-      while (lo < hi) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (RS[mid].e + RS[mid].v > f.cfin) hi = mid; else lo = mid + 1;
-      }
-      rf = lo;
+  const FlowLvl f = F.lvl[h * FL_CAP + q];
+  const RsEnt* RS = F.rs + L + f.base;
+  Level x{};
+  x.price = f.price;
+  x.head = x.tail = NIL;
+  // first new maker that survives the batch
+  uint32_t rf = 0;
+  if (f.cfin > f.d0) {
+    uint32_t lo = 0, hi = f.nrest;  // first r with e + v > cfin
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (RS[mid].e + RS[mid].v > f.cfin) hi = mid; else lo = mid + 1;
     }
-    const uint32_t S = f.nrest - rf;
-    const bool fresh = f.nlive0 == 0;
-    const uint32_t s0 = fresh ? 0u : f.tslot;
-    const uint32_t room = fresh ? 0u : CH - s0;
-    const uint32_t need = S > room ? (S - room + CH - 1) / CH : 0u;
-    // claim `need` chunk ids: free stack first, then the bump pointer
-    int t = 0;
-    uint32_t nst = 0, bb = 0;
-    if (need) {
-      if (lane == 0) t = atomicSub(&D.st->free_top, static_cast<int>(need));
-      t = static_cast<int>(uni(static_cast<uint32_t>(t)));
-      nst = static_cast<uint32_t>(min(max(t, 0), static_cast<int>(need)));
-      if (lane == 0 && nst < need) bb = atomicAdd(D.ch_bump, need - nst);
-      bb = uni(bb);
-      if (bb + (need - nst) > D.ch_cap) {
-        if (lane == 0) atomicOr(&D.st->err, ERR_CHUNKS);
-        continue;
-      }
-    }
-    auto chunk_id = [&](uint32_t i) -> uint32_t {
-      return i < nst ? D.free_ids[t - static_cast<int>(nst) + static_cast<int>(i)] : bb + (i - nst);
-    };
-    for (uint32_t i = lane; i < need; i += 64) {
-      ChunkHdr c;
-      c.next = (i + 1 < need) ? chunk_id(i + 1) : NIL;
-      c.pad = 0;
-      c.price = f.price;
-      D.chdr[chunk_id(i)] = c;
-    }
-    if (need && !fresh && lane == 0) D.chdr[f.tail].next = chunk_id(0);
-    for (uint32_t i = lane; i < S; i += 64) {
-      const RsEnt r = RS[rf + i];
-      const Prep mk = B.prep[hd.beg + r.j];
-      const int64_t rem = (r.e < f.cfin) ? r.e + r.v - f.cfin : r.v;
-      uint32_t cid, slot;
-      if (!fresh && s0 + i < CH) {
-        cid = f.tail;
-        slot = s0 + i;
-      } else {
-        const uint32_t g = fresh ? i : i - room;
-        cid = chunk_id(g / CH);
-        slot = g % CH;
-      }
-      const uint32_t loc = cid * CH + slot;
-      const unsigned long long key = (static_cast<unsigned long long>(hd.sym + 1) << 32) | mk.oid;
-      unsigned long long hh = mix64(key) & mask, probe = 0;
-      for (; probe <= mask; ++probe, hh = (hh + 1) & mask) {
-        const unsigned long long kv = __hip_atomic_load(&D.idx[hh].key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if ((kv == KEY_EMPTY || kv == KEY_TOMB) && atomicCAS(&D.idx[hh].key, kv, key) == kv) break;
-      }
-      if (probe > mask) { atomicOr(&D.st->err, ERR_INDEX); continue; }
-      D.idx[hh].loc = loc;
-      Node nd{};
-      nd.rem = rem;
-      nd.oid = mk.oid;
-      nd.uuid = mk.uuid;
-      nd.ixs = static_cast<uint32_t>(hh);
-      nd.tx = mk.side;
-      D.nodes[loc] = nd;
-    }
-    if (lane == 0) {
-      Level x{};
-      x.price = f.price;
-      x.depth = f.dfin;
-      x.nlive = f.nlive0 + S;
-      uint32_t mem = 0;
-      if ((hd.amask[q >> 6] >> (q & 63)) & 1ull) mem |= M_SALE;
-      if ((hd.bmask[q >> 6] >> (q & 63)) & 1ull) mem |= M_BUY;
-      x.member = static_cast<uint8_t>(mem);
-      if (x.nlive == 0) {
-        x.head = x.tail = NIL;
-        x.hslot = x.tslot = 0;
-      } else if (fresh) {
-        x.head = chunk_id(0);
-        x.hslot = 0;
-        x.tail = chunk_id(need - 1);
-        x.tslot = static_cast<uint8_t>(S - (need - 1) * CH);
-      } else {
-        x.head = f.head;
-        x.hslot = static_cast<uint8_t>(f.hslot);
-        x.tail = need ? chunk_id(need - 1) : f.tail;
-        x.tslot = static_cast<uint8_t>(need ? (S - room) - (need - 1) * CH : s0 + S);
-      }
-      // clean-book invariant: nodes <=> positive depth <=> one side-set membership
-      const bool ok = (x.nlive > 0) == (x.depth > 0) && (x.nlive > 0) == (mem == M_BUY || mem == M_SALE) &&
-                      (x.nlive > 0 || mem == 0);
-      if (!ok) atomicOr(&D.st->err, ERR_CORRUPT);
-      lv[q] = x;
-      keep[q] = x.nlive > 0 ? 1u : 0u;
+    rf = lo;
+  }
+  const uint32_t S = f.nrest - rf;
+  const bool fresh = f.nlive0 == 0;
+  const uint32_t s0 = fresh ? 0u : f.tslot;
+  const uint32_t room = fresh ? 0u : CH - s0;
+  const uint32_t need = S > room ? (S - room + CH - 1) / CH : 0u;
+  // claim `need` chunk ids: free stack first, then the bump pointer
+  int t = 0;
+  uint32_t nst = 0, bb = 0;
+  if (need) {
+    if (lane == 0) t = atomicSub(&D.st->free_top, static_cast<int>(need));
+    t = static_cast<int>(uni(static_cast<uint32_t>(t)));
+    nst = static_cast<uint32_t>(min(max(t, 0), static_cast<int>(need)));
+    if (lane == 0 && nst < need) bb = atomicAdd(D.ch_bump, need - nst);
+    bb = uni(bb);
+    if (bb + (need - nst) > D.ch_cap) {
+      if (lane == 0) atomicOr(&D.st->err, ERR_CHUNKS);
+      return x;
     }
   }
-  __syncthreads();
+  auto chunk_id = [&](uint32_t i) -> uint32_t {
+    return i < nst ? D.free_ids[t - static_cast<int>(nst) + static_cast<int>(i)] : bb + (i - nst);
+  };
+  for (uint32_t i = lane; i < need; i += 64) {
+    ChunkHdr c;
+    c.next = (i + 1 < need) ? chunk_id(i + 1) : NIL;
+    c.pad = 0;
+    c.price = f.price;
+    D.chdr[chunk_id(i)] = c;
+  }
+  if (need && !fresh && lane == 0) D.chdr[f.tail].next = chunk_id(0);
+  for (uint32_t i = lane; i < S; i += 64) {
+    const RsEnt r = RS[rf + i];
+    const Prep mk = B.prep[hd.beg + r.j];
+    const int64_t rem = (r.e < f.cfin) ? r.e + r.v - f.cfin : r.v;
+    uint32_t cid, slot;
+    if (!fresh && s0 + i < CH) {
+      cid = f.tail;
+      slot = s0 + i;
+    } else {
+      const uint32_t g = fresh ? i : i - room;
+      cid = chunk_id(g / CH);
+      slot = g % CH;
+    }
+    const uint32_t loc = cid * CH + slot;
+    const unsigned long long key = (static_cast<unsigned long long>(hd.sym + 1) << 32) | mk.oid;
+    unsigned long long hh = mix64(key) & mask, probe = 0;
+    for (; probe <= mask; ++probe, hh = (hh + 1) & mask) {
+      const unsigned long long kv = __hip_atomic_load(&D.idx[hh].key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if ((kv == KEY_EMPTY || kv == KEY_TOMB) && atomicCAS(&D.idx[hh].key, kv, key) == kv) break;
+    }
+    if (probe > mask) { atomicOr(&D.st->err, ERR_INDEX); continue; }
+    D.idx[hh].loc = loc;
+    Node nd{};
+    nd.rem = rem;
+    nd.oid = mk.oid;
+    nd.uuid = mk.uuid;
+    nd.ixs = static_cast<uint32_t>(hh);
+    nd.tx = mk.side;
+    D.nodes[loc] = nd;
+  }
+  x.depth = f.dfin;
+  x.nlive = f.nlive0 + S;
+  uint32_t mem = 0;
+  if ((hd.amask[q >> 6] >> (q & 63)) & 1ull) mem |= M_SALE;
+  if ((hd.bmask[q >> 6] >> (q & 63)) & 1ull) mem |= M_BUY;
+  x.member = static_cast<uint8_t>(mem);
+  if (x.nlive == 0) {
+    x.hslot = x.tslot = 0;
+  } else if (fresh) {
+    x.head = chunk_id(0);
+    x.hslot = 0;
+    x.tail = chunk_id(need - 1);
+    x.tslot = static_cast<uint8_t>(S - (need - 1) * CH);
+  } else {
+    x.head = f.head;
+    x.hslot = static_cast<uint8_t>(f.hslot);
+    x.tail = need ? chunk_id(need - 1) : f.tail;
+    x.tslot = static_cast<uint8_t>(need ? (S - room) - (need - 1) * CH : s0 + S);
+  }
+  // clean-book invariant: nodes <=> positive depth <=> one side-set membership
+  const bool ok = (x.nlive > 0) == (x.depth > 0) && (x.nlive > 0) == (mem == M_BUY || mem == M_SALE) &&
+                  (x.nlive > 0 || mem == 0);
+  if (!ok && lane == 0) atomicOr(&D.st->err, ERR_CORRUPT);
+  return x;
+}
+
+// Compact the book's final levels (lv[1..nl], LDS) into its level block, write the Book and
+// the batch counters.  Called by every thread of the block after lv is complete.
+__device__ __forceinline__ void fl_write_finish(const Dev& D, const FlowHdr& hd, Level* lv, uint32_t* keep,
+                                                uint32_t& base_s, uint32_t& cap_s, uint32_t& nout_s) {
   if (threadIdx.x == 0) {
     uint32_t c = 0;
     for (uint32_t q = 1; q <= hd.nl; ++q) {
-      const uint32_t k = keep[q];
+      const uint32_t k = lv[q].nlive > 0 ? 1u : 0u;
       keep[q] = k ? c : NIL;
       c += k;
     }
@@ -1055,7 +1055,7 @@ __global__ __launch_bounds__(FL_WRITE_T) void k_flow_write(Dev D, BatchArgs B, F
   __syncthreads();
   const uint32_t nout = nout_s;
   if (nout > cap_s) return;
-  for (uint32_t q = 1 + threadIdx.x; q <= hd.nl; q += FL_WRITE_T)
+  for (uint32_t q = 1 + threadIdx.x; q <= hd.nl; q += blockDim.x)
     if (keep[q] != NIL) D.lvl[base_s + keep[q]] = lv[q];
   if (threadIdx.x == 0) {
     Book nb;
@@ -1076,6 +1076,197 @@ __global__ __launch_bounds__(FL_WRITE_T) void k_flow_write(Dev D, BatchArgs B, F
     atomicAdd(&c[C_FLOW_ORDERS], static_cast<unsigned long long>(hd.end - hd.beg));
     atomicAdd(&c[C_FLOW_TOUCHES], static_cast<unsigned long long>(hd.ntouch));
   }
+}
+
+// Tail books: one workgroup per book, waves take its levels in turn, then finish.
+__global__ __launch_bounds__(FL_WRITE_T) void k_flow_write(Dev D, BatchArgs B, FlowArgs F) {
+  __shared__ Level lv[FL_CAP];
+  __shared__ uint32_t keep[FL_CAP];
+  __shared__ uint32_t nout_s, base_s, cap_s;
+  const uint32_t h = F.h0 + blockIdx.x;
+  if (h >= fl_hend(D, F) || !F.hdr[h].ok) return;
+  const FlowHdr hd = F.hdr[h];
+  const uint32_t w = threadIdx.x >> 6, nw = FL_WRITE_T / 64;
+  for (uint32_t q = 1 + w; q <= hd.nl; q += nw) {
+    const Level x = fl_write_level(D, B, F, hd, h, uni(q));
+    if (lane_id() == 0) lv[q] = x;
+  }
+  __syncthreads();
+  fl_write_finish(D, hd, lv, keep, base_s, cap_s, nout_s);
+}
+
+// Head books: one wave per (book, level) writes its FIFO and stores its final record ...
+__global__ __launch_bounds__(64) void k_flow_write_lv(Dev D, BatchArgs B, FlowArgs F) {
+  const uint32_t h = F.h0 + blockIdx.y, q = blockIdx.x;
+  if (h >= fl_hend(D, F) || !F.hdr[h].ok) return;
+  const FlowHdr hd = F.hdr[h];
+  if (q == 0 || q > hd.nl) return;
+  const Level x = fl_write_level(D, B, F, hd, h, q);
+  if (lane_id() == 0) F.lvout[h * FL_CAP + q] = x;
+}
+
+// ... then one workgroup per head book compacts the level array.
+__global__ __launch_bounds__(128) void k_flow_write_fin(Dev D, FlowArgs F) {
+  __shared__ Level lv[FL_CAP];
+  __shared__ uint32_t keep[FL_CAP];
+  __shared__ uint32_t nout_s, base_s, cap_s;
+  const uint32_t h = F.h0 + blockIdx.x;
+  if (h >= fl_hend(D, F) || !F.hdr[h].ok) return;
+  const FlowHdr hd = F.hdr[h];
+  for (uint32_t q = 1 + threadIdx.x; q <= hd.nl; q += blockDim.x) lv[q] = F.lvout[h * FL_CAP + q];
+  __syncthreads();
+  fl_write_finish(D, hd, lv, keep, base_s, cap_s, nout_s);
+}
+
+// ============================================================== head: wide sort and levels
+// The head books' touch logs are long (the hottest book: ~450k touches): sort them with one
+// workgroup per 1024-touch tile (count -> per-book scan -> scatter) instead of one per book,
+// and their levels with one wave per (book, level).
+constexpr uint32_t FL_TILE = 1024, FL_TILE_W = FL_TILE / 64, FL_SORT_GRID = 512;
+
+// stable in-tile rank of a touch among the tile's touches of the same level
+__device__ __forceinline__ uint32_t fl_tile_rank(uint32_t k, bool valid, uint32_t& cnt) {
+  unsigned long long same = __ballot(valid);
+#pragma unroll
+  for (uint32_t b = 0; b < 7; ++b) {
+    const unsigned long long bb = __ballot((k >> b) & 1u);
+    same &= ((k >> b) & 1u) ? bb : ~bb;
+  }
+  cnt = __popcll(same);
+  return __popcll(same & lt_mask());
+}
+
+__global__ __launch_bounds__(FL_TILE) void k_flow_sort_cnt(Dev D, FlowArgs F) {
+  __shared__ uint32_t wc[FL_TILE_W][FL_CAP];
+  __shared__ uint32_t nrest;
+  const uint32_t hb = blockIdx.y, h = F.h0 + hb, tid = threadIdx.x, w = tid >> 6;
+  if (h >= fl_hend(D, F) || !F.hdr[h].ok) return;
+  const uint32_t nt = F.hdr[h].ntouch, L = FL_TOUCH_MUL * F.hdr[h].beg;
+  const uint32_t ntile = (nt + FL_TILE - 1) / FL_TILE;
+  for (uint32_t tl = blockIdx.x; tl < ntile; tl += gridDim.x) {
+    for (uint32_t i = tid; i < FL_TILE_W * FL_CAP; i += FL_TILE) wc[i / FL_CAP][i % FL_CAP] = 0;
+    if (tid == 0) nrest = 0;
+    __syncthreads();
+    const uint32_t t = tl * FL_TILE + tid;
+    const bool valid = t < nt;
+    const uint32_t kr = valid ? F.log[L + t].kr : 0u, k = kr & 127u;
+    uint32_t cnt;
+    const uint32_t rank = fl_tile_rank(k, valid, cnt);
+    if (valid && rank == 0) wc[w][k] = cnt;
+    const unsigned long long rm = __ballot(valid && ((kr >> 7) & 1u) && k);
+    if (lane_id() == 0 && rm) atomicAdd(&nrest, static_cast<uint32_t>(__popcll(rm)));
+    __syncthreads();
+    if (tid < FL_CAP) {
+      uint32_t c = 0;
+      for (uint32_t ww = 0; ww < FL_TILE_W; ++ww) c += wc[ww][tid];
+      F.tcnt[(static_cast<size_t>(hb) * F.maxt + tl) * FL_CAP + tid] = c;
+    }
+    if (tid == 0 && nrest) atomicAdd(&F.hdr[h].rests, nrest);
+    __syncthreads();
+  }
+}
+
+// Per head book: level totals -> run bases (FlowLvl::cnt/base), then each tile's offset per
+// level (in place over the counts).
+__global__ __launch_bounds__(FL_CAP) void k_flow_sort_scan(Dev D, FlowArgs F) {
+  __shared__ uint32_t tot[FL_CAP];
+  const uint32_t hb = blockIdx.x, h = F.h0 + hb, k = threadIdx.x;
+  if (h >= fl_hend(D, F) || !F.hdr[h].ok) return;
+  const uint32_t nt = F.hdr[h].ntouch, nl = F.hdr[h].nl;
+  const uint32_t ntile = (nt + FL_TILE - 1) / FL_TILE;
+  uint32_t* tc = F.tcnt + static_cast<size_t>(hb) * F.maxt * FL_CAP;
+  uint32_t s = 0;
+  uint32_t tl = 0;
+  for (; tl + 8 <= ntile; tl += 8) {
+    uint32_t v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = tc[(tl + u) * FL_CAP + k];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s += v[u];
+  }
+  for (; tl < ntile; ++tl) s += tc[tl * FL_CAP + k];
+  tot[k] = s;
+  __syncthreads();
+  if (k == 0) {
+    uint32_t acc = 0;
+    for (uint32_t i = 0; i < FL_CAP; ++i) { const uint32_t v = tot[i]; tot[i] = acc; acc += v; }
+  }
+  __syncthreads();
+  const uint32_t base = tot[k];
+  if (k >= 1 && k <= nl) {
+    F.lvl[h * FL_CAP + k].cnt = s;
+    F.lvl[h * FL_CAP + k].base = base;
+  }
+  uint32_t run = base;
+  for (tl = 0; tl + 8 <= ntile; tl += 8) {
+    uint32_t v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = tc[(tl + u) * FL_CAP + k];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) { tc[(tl + u) * FL_CAP + k] = run; run += v[u]; }
+  }
+  for (; tl < ntile; ++tl) {
+    const uint32_t v = tc[tl * FL_CAP + k];
+    tc[tl * FL_CAP + k] = run;
+    run += v;
+  }
+}
+
+__global__ __launch_bounds__(FL_TILE) void k_flow_sort_scatter(Dev D, FlowArgs F) {
+  __shared__ uint32_t wc[FL_TILE_W][FL_CAP];
+  const uint32_t hb = blockIdx.y, h = F.h0 + hb, tid = threadIdx.x, w = tid >> 6;
+  if (h >= fl_hend(D, F) || !F.hdr[h].ok) return;
+  const uint32_t nt = F.hdr[h].ntouch, L = FL_TOUCH_MUL * F.hdr[h].beg;
+  const unsigned long long g = F.hdr[h].g;
+  const uint32_t ntile = (nt + FL_TILE - 1) / FL_TILE;
+  const uint32_t* tc = F.tcnt + static_cast<size_t>(hb) * F.maxt * FL_CAP;
+  for (uint32_t i = tid; i < FL_TILE_W * FL_CAP; i += FL_TILE) wc[i / FL_CAP][i % FL_CAP] = 0;
+  __syncthreads();
+  for (uint32_t tl = blockIdx.x; tl < ntile; tl += gridDim.x) {
+    const uint32_t t = tl * FL_TILE + tid;
+    const bool valid = t < nt;
+    Touch x{};
+    if (valid) x = F.log[L + t];
+    const uint32_t k = valid ? (x.kr & 127u) : 0u;
+    uint32_t cnt;
+    const uint32_t rank = fl_tile_rank(k, valid, cnt);
+    if (valid && rank == 0) wc[w][k] = cnt;
+    __syncthreads();
+    if (tid < FL_CAP) {  // prefix over the waves, from the tile's offset of each level
+      uint32_t r = tc[tl * FL_CAP + tid];
+      for (uint32_t ww = 0; ww < FL_TILE_W; ++ww) {
+        const uint32_t c = wc[ww][tid];
+        wc[ww][tid] = r;
+        r += c;
+      }
+    }
+    __syncthreads();
+    if (valid) {
+      SEnt e;
+      e.j = tk_j(x);
+      e.kind = (x.kr >> 7) & 1u;
+      e.amt = static_cast<int64_t>(static_cast<unsigned long long>(x.amt) * g);
+      e.coord = 0;
+      e.t = t;
+      e.pad = 0;
+      const uint32_t pos = wc[w][k] + rank;
+      F.srt[L + pos] = e;
+      F.log[L + t].pos = pos;
+      if (g != 1) F.log[L + t].amt = e.amt;
+    }
+    __syncthreads();
+    // stale wc entries of levels absent from the next tile are never read: only a wave's
+    // present levels are written before the prefix, and the prefix reads every level, so clear
+    for (uint32_t i = tid; i < FL_TILE_W * FL_CAP; i += FL_TILE) wc[i / FL_CAP][i % FL_CAP] = 0;
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(64) void k_flow_level_wide(Dev D, FlowArgs F) {
+  const uint32_t h = F.h0 + blockIdx.y, q = blockIdx.x;
+  if (h >= fl_hend(D, F) || !F.hdr[h].ok) return;
+  if (q == 0 || q > F.hdr[h].nl) return;
+  fl_level_one(D, F, h, q);
 }
 
 }  // namespace gome

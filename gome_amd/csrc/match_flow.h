@@ -201,6 +201,14 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep(Dev D, BatchArgs B, Flo
   auto insert = [&](unsigned long long key, uint32_t val) {
     uint32_t s = fl_hash(key);
     for (uint32_t probe = 0; probe < FL_HASH; ++probe) {
+      // a hot book hits a few dozen prices: read first, CAS only on a miss (no LDS atomic
+      // contention on the hot slots)
+      const unsigned long long cur = *reinterpret_cast<volatile unsigned long long*>(&hkey[s]);
+      if (cur == key && val == NIL) return;
+      if (cur != 0ull && cur != key) {
+        s = (s + 1) & (FL_HASH - 1);
+        continue;
+      }
       const unsigned long long prev = atomicCAS(&hkey[s], 0ull, key);
       if (prev == 0ull) {
         if (val != NIL) hval[s] = val;
@@ -236,17 +244,32 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep(Dev D, BatchArgs B, Flo
   // the segment's orders
   uint32_t my_adds = 0, my_drop = 0;
   if (!bad) {
-    for (uint32_t b = beg + tid; b < end; b += FL_PREP_T) {
-      const Prep q = B.prep[b];
+    // 4 independent record loads in flight per thread (one block per book is latency-bound)
+    for (uint32_t b0 = beg + tid; b0 < end && !bad; b0 += 4 * FL_PREP_T) {
+      Prep qs[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const uint32_t b = b0 + u * FL_PREP_T;
+        if (b < end) qs[u] = B.prep[b];
+        else qs[u].action = 0;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+      const Prep q = qs[u];
       if (q.action == GOME_DEL) { bad = 1; break; }
       if (q.action != GOME_ADD) continue;
       my_adds++;
       if (!q.adm) { my_drop++; continue; }
       if (q.vol == 0) { bad = 1; break; }
-      mg = fl_gcd(mg, static_cast<unsigned long long>(q.vol));
+      {  // gcd, with a cheap divisibility test first (exact: integers < 2^53 as doubles)
+        const unsigned long long v = static_cast<unsigned long long>(q.vol);
+        const double qd = static_cast<double>(v) / static_cast<double>(mg ? mg : 1);
+        if (mg == 0 || static_cast<unsigned long long>(qd) * mg != v) mg = fl_gcd(mg, v);
+      }
       msum = min(msum + static_cast<unsigned long long>(q.vol), FL_SUM_CAP);
       insert(static_cast<unsigned long long>(q.price) + FL_KEY_OFF, NIL);
       if (bad) break;
+      }
     }
   }
   if (my_adds) atomicAdd(&adds, my_adds);
@@ -309,8 +332,18 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep(Dev D, BatchArgs B, Flo
   if (!w32) g = 1;
   if (tid < ((4u - ((end - beg) & 3u)) & 3u))  // padding to whole half-groups
     F.ord8[obase + (end - beg) + tid] = OR_NOP;
-  for (uint32_t b = beg + tid; b < end; b += FL_PREP_T) {
-    const Prep q = B.prep[b];
+  for (uint32_t b0 = beg + tid; b0 < end; b0 += 4 * FL_PREP_T) {
+    Prep qs[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const uint32_t b = b0 + u * FL_PREP_T;
+      if (b < end) qs[u] = B.prep[b];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+    const uint32_t b = b0 + u * FL_PREP_T;
+    if (b >= end) break;
+    const Prep q = qs[u];
     unsigned long long rec = OR_NOP;
     if (q.action == GOME_ADD && q.adm) {
       const unsigned long long key = static_cast<unsigned long long>(q.price) + FL_KEY_OFF;
@@ -325,6 +358,7 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep(Dev D, BatchArgs B, Flo
     }
     F.ord8[obase + (b - beg)] = rec;
     B.ev_count[q.idx] = 0;
+    }
   }
   if (tid == 0) {
     FlowHdr x{};

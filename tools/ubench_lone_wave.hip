@@ -9,7 +9,7 @@
 
 __global__ void k(unsigned long long* out) {
   unsigned long long t0, t1;
-  unsigned a = threadIdx.x, b = 1, c = 2;
+  unsigned a = threadIdx.x, b = 1, c = 2, d1 = 3, d2 = 4;
   // 1) 512 dependent s_add
   t0 = __builtin_amdgcn_s_memtime();
   asm volatile(REP8(REP64("s_add_u32 %0, %0, 1\n\t")) : "+s"(b));
@@ -60,7 +60,35 @@ __global__ void k(unsigned long long* out) {
   asm volatile(REP8(REP64("s_bitcmp0_b32 %0, 31\n\ts_cbranch_scc1 3f\n\t3:\n\t")) : "+s"(b));
   t1 = __builtin_amdgcn_s_memtime();
   out[9] = t1 - t0;
-  out[10] = a + b + c;
+  // 11) s_cmp, 3 independent s_add, s_cbranch (not taken): is the branch cost SCC latency?
+  t0 = __builtin_amdgcn_s_memtime();
+  asm volatile(REP8(REP64("s_cmp_eq_u32 %0, 12345\n\ts_add_u32 %1, %1, 1\n\ts_add_u32 %2, %2, 1\n\t"
+                          "s_add_u32 %3, %3, 1\n\ts_cbranch_scc1 4f\n\t4:\n\t"))
+               : "+s"(b), "+s"(c), "+s"(d1), "+s"(d2));
+  t1 = __builtin_amdgcn_s_memtime();
+  out[10] = t1 - t0;
+  // 12) 4 s_add alone (reference for 11)
+  t0 = __builtin_amdgcn_s_memtime();
+  asm volatile(REP8(REP64("s_cmp_eq_u32 %0, 12345\n\ts_add_u32 %1, %1, 1\n\ts_add_u32 %2, %2, 1\n\t"
+                          "s_add_u32 %3, %3, 1\n\t"))
+               : "+s"(b), "+s"(c), "+s"(d1), "+s"(d2));
+  t1 = __builtin_amdgcn_s_memtime();
+  out[11] = t1 - t0;
+  // 13) s_cbranch_scc1 taken to a target 8 instructions ahead (skipping them)
+  t0 = __builtin_amdgcn_s_memtime();
+  asm volatile(REP8(REP64("s_cmp_eq_u32 %0, %0\n\ts_cbranch_scc1 5f\n\ts_add_u32 %1, %1, 1\n\ts_add_u32 %1, %1, 1\n\t"
+                          "s_add_u32 %1, %1, 1\n\ts_add_u32 %1, %1, 1\n\t5:\n\t"))
+               : "+s"(b), "+s"(c));
+  t1 = __builtin_amdgcn_s_memtime();
+  out[12] = t1 - t0;
+  // 14) v_readlane, then 5 independent SALU, then consume (hidden latency?)
+  t0 = __builtin_amdgcn_s_memtime();
+  asm volatile(REP8(REP64("v_readlane_b32 %0, %4, 3\n\ts_add_u32 %1, %1, 1\n\ts_add_u32 %2, %2, 1\n\t"
+                          "s_add_u32 %3, %3, 1\n\ts_add_u32 %1, %1, 1\n\ts_add_u32 %0, %0, 1\n\t"))
+               : "+s"(c), "+s"(b), "+s"(d1), "+s"(d2) : "v"(a));
+  t1 = __builtin_amdgcn_s_memtime();
+  out[13] = t1 - t0;
+  out[14] = a + b + c + d1 + d2;
 }
 
 int main() {
@@ -73,9 +101,11 @@ int main() {
   }
   const char* names[] = {"dep s_add", "2 indep s_add (per pair)", "s_branch taken", "s_cmp+cbranch not taken (pair)",
                          "v_readlane->s_add (pair)", "v_writelane", "s_sub+s_subb (pair)", "dep v_add",
-                         "s_mov exec + v_add (pair)", "s_bitcmp + cbranch taken (pair)"};
+                         "s_mov exec + v_add (pair)", "s_bitcmp + cbranch taken (pair)",
+                         "cmp,3 add,cbranch nt (group)", "cmp,3 add (group)", "cmp,cbranch taken over 4 (group)",
+                         "readlane,4 salu,consume (group)"};
   // s_memtime counts at a fixed 100 MHz reference on gfx9? print raw ticks per op
-  for (int i = 0; i < 10; ++i) printf("%-34s %8.3f ticks/op\n", names[i], h[i] / 512.0);
+  for (int i = 0; i < 14; ++i) printf("%-34s %8.3f ticks/op\n", names[i], h[i] / 512.0);
   hipFree(d);
   return 0;
 }

@@ -2,21 +2,26 @@
 
 The plan (match_flow.h) is the batch's critical path: one wavefront per book applies every
 order to the level aggregates one after another, so its cost is the latency of the
-instruction stream per order.  Lone-wave costs on gfx950 (tools/ubench_lone_wave.hip):
-4 cycles per SALU / VALU instruction, ~13 per conditional branch even when not taken, ~26
-taken, 20 per s_branch, ~20 from v_readlane to its SALU consumer.  So the loop is written
-out instruction by instruction (generated, 8 orders per double-buffered SMEM group pair):
+instruction stream per order.  Lone-wave costs on gfx950 (tools/ubench_lone_wave.hip,
+tools/ubench_branch3.hip, shader cycles): 4 per SALU / VALU instruction, ~12 per conditional
+branch not taken, ~24 taken, ~20 per s_branch, ~20 per v_readlane or per VALU write of an
+SGPR whatever the distance to the consumer.  Branches are the dominant cost, so:
   * the best ask / best bid levels and their depths live in SGPRs (top-of-book cache): a
-    partial fill at the top or a rest at the top is pure SALU;
-  * other levels' depths live in lane registers (level k: lane k % 64 of set k / 64): a rest
-    behind the top is an exec-masked VALU add (no readback), a new top evicts the old one
-    with v_writelane, only a sweep past the top reads a lane;
+    partial fill is pure SALU;
+  * other levels' depths live in lane registers (level k: lane k % 64 of set k / 64), with the
+    invariant "a lane that is not a resting level behind the cached top holds 0" (the cached
+    tops' lanes included).  A rest is then ONE branchless sequence whatever the level is
+    (deep / at the top / a new top that evicts the cached one into its lane): selects decide
+    the lane, the amount and the cached depth, and an exec-masked VALU add applies it;
   * membership S:SALE / S:BUY are 128-bit SGPR masks with sentinel levels 0 (bid) and 127
-    (ask), so the next level of a sweep is one bit scan;
-  * orders stream through the scalar cache in groups of 4 (s_load_dwordx8), the next group in
+    (ask), so the next level of a sweep is one bit scan; a promoted level's lane is read and
+    zeroed;
+  * every path ends with the next order's side dispatch (decode, one conditional branch) instead
+    of a jump to a common head, and the most frequent path falls through into the next slot;
+  * orders stream through the scalar cache in half-groups of 4 (s_load_dwordx8), the next one in
     flight while the current one is applied; the record registers become T in place;
   * touches are staged in lane registers (lane = M0, the staging count) and stored 64 at a
-    time from inside the loop; rests (the most common outcome) fall through.
+    time from inside the loop.
 
 Two variants: W=64 (volumes and depths as 64-bit SGPR pairs / two lane registers per set)
 and W=32 (the book's volumes divided by their GCD fit 32 bits: one register each, half the
@@ -33,12 +38,15 @@ import os
 # fixed registers (declared as clobbers of the asm statement)
 BUF = [(60, 61), (62, 63), (64, 65), (66, 67), (68, 69), (70, 71), (72, 73), (74, 75)]
 BA, BB = "s76", "s77"            # best ask / best bid level
-BAD, BBD = ("s78", "s79"), ("s80", "s81")  # their depths (authoritative while cached)
+BAD, BBD = ("s78", "s79"), ("s80", "s81")  # their depths (authoritative; their lanes hold 0)
+L = "s82"                        # lane target of a rest
 M = "s[84:85]"                   # 64-bit temp (mask word / one-hot)
 LI, K, T0, JJS = "s86", "s87", "s88", "s89"
 O = ["s90", "s91", "s92", "s93"]
-D = ("s94", "s95")               # temp (T - depth)
-HC = "s97"                       # half-groups left
+A, A1 = ("s90", "s91"), ("s92", "s93")     # lane amounts (set 0 / set 1) of a rest
+D = ("s94", "s95")               # T - depth of a crossed level; X (cached-depth amount) in rests
+X = D
+HC = "s97"                       # half-groups left + 1
 ADDR = "s[98:99]"                # SMEM address of the next half-group
 SAVE = "s100"                    # M0 (staging count) saved around lane writes
 CLOBBERS = [f"s{i}" for i in range(60, 101)]
@@ -62,9 +70,45 @@ class Gen:
         self.uid += 1
         return self.lab(f"{name}{self.uid}")
 
+    # ---- 64/32-bit scalar helpers on (lo, hi) pairs ------------------------------------
+    def pair(self, r) -> str:
+        return f"s[{r[0][1:]}:{r[1][1:]}]"
+
+    def sub(self, r, a, b):  # r = a - b, SCC = borrow
+        self.e(f"s_sub_u32 {r[0]}, {a[0]}, {b[0]}")
+        if self.w == 64:
+            self.e(f"s_subb_u32 {r[1]}, {a[1]}, {b[1]}")
+
+    def add(self, r, a, b):
+        self.e(f"s_add_u32 {r[0]}, {a[0]}, {b[0]}")
+        if self.w == 64:
+            self.e(f"s_addc_u32 {r[1]}, {a[1]}, {b[1]}")
+
+    def mov(self, r, a):
+        if self.w == 64:
+            self.e(f"s_mov_b64 {self.pair(r)}, {self.pair(a)}")
+        else:
+            self.e(f"s_mov_b32 {r[0]}, {a[0]}")
+
+    def csel(self, r, a, b):
+        """r = SCC ? a : b; a / b are pairs or the literal 0."""
+        def op(x):
+            return "0" if x == 0 else (self.pair(x) if self.w == 64 else x[0])
+        if self.w == 64:
+            self.e(f"s_cselect_b64 {self.pair(r)}, {op(a)}, {op(b)}")
+        else:
+            self.e(f"s_cselect_b32 {r[0]}, {op(a)}, {op(b)}")
+
+    def is_zero_scc(self, t):  # SCC = (t == 0)
+        if self.w == 64:
+            self.e(f"s_cmp_eq_u64 {self.pair(t)}, 0")
+        else:
+            self.e(f"s_cmp_eq_u32 {t[0]}, 0")
+
     # ---- lane registers -------------------------------------------------------------
-    def read(self, k: str, d: tuple[str, str]):
-        """d = depth of level k from the lane registers."""
+    def promote(self, k: str, d):
+        """d = depth of level k from the lane registers, and the lane is zeroed (level k
+        becomes a cached top).  Sentinel lanes may hold garbage; their depth is never used."""
         e = self.e
         e(f"s_and_b32 {T0}, {k}, 63")
         e(f"v_readlane_b32 {O[0]}, %[dl0], {T0}")
@@ -76,10 +120,20 @@ class Gen:
         e(f"s_cselect_b32 {d[0]}, {O[0]}, {O[2]}")
         if self.w == 64:
             e(f"s_cselect_b32 {d[1]}, {O[1]}, {O[3]}")
+        e(f"s_bfm_b64 {M}, 1, {k}")
+        e(f"s_cselect_b64 exec, {M}, 0")
+        e("v_mov_b32 %[dl0], 0")
+        if self.w == 64:
+            e("v_mov_b32 %[dh0], 0")
+        e(f"s_cselect_b64 exec, 0, {M}")
+        e("v_mov_b32 %[dl1], 0")
+        if self.w == 64:
+            e("v_mov_b32 %[dh1], 0")
 
-    def write(self, k: str, v: tuple[str, str]):
-        """Level k := v.  The other set's lane written is a sentinel lane (level 0: set 0
-        lane 0, level 127: set 1 lane 63), whose value is never used."""
+    def write(self, k: str, v):
+        """Level k := v (end of the loop: the cached tops go back to their lanes).  The other
+        set's lane written is a sentinel lane (level 0: set 0 lane 0, level 127: set 1 lane
+        63), whose value is never used."""
         e = self.e
         e(f"s_mov_b32 {SAVE}, m0")
         e(f"s_and_b32 {T0}, {k}, 63")
@@ -96,85 +150,60 @@ class Gen:
             e(f"v_writelane_b32 %[dh1], {v[1]}, m0")
         e(f"s_mov_b32 m0, {SAVE}")
 
-    def add_lane(self, k: str, t: tuple[str, str]):
-        """Level k += t in the lane registers (exec-masked VALU add, no readback)."""
+    def add_lane(self):
+        """Level L += A in the lane registers: the amount goes to the set of L, the other set's
+        lane L % 64 gets 0.  exec is left narrowed (only lane-select ops follow)."""
         e = self.e
+        e(f"s_cmp_lt_u32 {L}, 64")
+        self.csel(A1, 0, A)
+        self.csel(A, A, 0)
+        e(f"s_bfm_b64 exec, 1, {L}")
         if self.w == 64:
-            e(f"v_mov_b32 %[vt], {t[1]}")               # before exec narrows (set 1 needs it too)
-        e(f"s_lshl_b64 {M}, 1, {k}")
-        e(f"s_cmp_lt_u32 {k}, 64")
-        e(f"s_cselect_b64 exec, {M}, 0")
-        if self.w == 64:
-            e(f"v_add_co_u32_e32 %[dl0], vcc, {t[0]}, %[dl0]")
-            e(f"v_addc_co_u32_e32 %[dh0], vcc, %[vt], %[dh0], vcc")
+            e(f"v_mov_b32 %[vt], {A[1]}")
+            e(f"v_add_co_u32_e32 %[dl0], vcc, {A[0]}, %[dl0]")
+            e("v_addc_co_u32_e32 %[dh0], vcc, %[vt], %[dh0], vcc")
+            e(f"v_mov_b32 %[vt], {A1[1]}")
+            e(f"v_add_co_u32_e32 %[dl1], vcc, {A1[0]}, %[dl1]")
+            e("v_addc_co_u32_e32 %[dh1], vcc, %[vt], %[dh1], vcc")
         else:
-            e(f"v_add_u32_e32 %[dl0], {t[0]}, %[dl0]")
-        e(f"s_cmp_lt_u32 {k}, 64")
-        e(f"s_cselect_b64 exec, 0, {M}")
-        if self.w == 64:
-            e(f"v_add_co_u32_e32 %[dl1], vcc, {t[0]}, %[dl1]")
-            e(f"v_addc_co_u32_e32 %[dh1], vcc, %[vt], %[dh1], vcc")
-        else:
-            e(f"v_add_u32_e32 %[dl1], {t[0]}, %[dl1]")
-        e("s_mov_b64 exec, -1")
+            e(f"v_add_u32_e32 %[dl0], {A[0]}, %[dl0]")
+            e(f"v_add_u32_e32 %[dl1], {A1[0]}, %[dl1]")
 
     # ---- scalar state ---------------------------------------------------------------
     def setbit(self, mask: str, k: str, op: str):
-        """op = s_bitset1_b64 / s_bitset0_b64 on bit k of the 128-bit mask A or B."""
+        """op = s_bitset1_b64 / s_bitset0_b64 on bit k of the 128-bit mask A or B (neither the
+        bit op nor the selects write SCC)."""
         e = self.e
         m0, m1 = f"%[{mask}0]", f"%[{mask}1]"
         e(f"s_cmp_lt_u32 {k}, 64")
         e(f"s_cselect_b64 {M}, {m0}, {m1}")
         e(f"{op} {M}, {k}")
-        e(f"s_cmp_lt_u32 {k}, 64")
         e(f"s_cselect_b64 {m0}, {M}, {m0}")
         e(f"s_cselect_b64 {m1}, {m1}, {M}")
 
     def lowest_ask(self):
+        """BA = lowest bit of A (ff1 gives -1 = UINT_MAX on an empty word; A1 holds the
+        sentinel bit 127)."""
         e = self.e
         e(f"s_ff1_i32_b64 {BA}, %[A0]")
         e(f"s_ff1_i32_b64 {T0}, %[A1]")
         e(f"s_add_u32 {T0}, {T0}, 64")
-        e(f"s_cmp_lg_u64 %[A0], 0")
-        e(f"s_cselect_b32 {BA}, {BA}, {T0}")
+        e(f"s_min_u32 {BA}, {BA}, {T0}")
 
     def highest_bid(self):
+        """BB = highest bit of B (B0 holds the sentinel bit 0; an empty B1 gives 128 & 127 = 0)."""
         e = self.e
         e(f"s_flbit_i32_b64 {BB}, %[B0]")
         e(f"s_sub_u32 {BB}, 63, {BB}")
         e(f"s_flbit_i32_b64 {T0}, %[B1]")
         e(f"s_sub_u32 {T0}, 127, {T0}")
-        e(f"s_cmp_lg_u64 %[B1], 0")
-        e(f"s_cselect_b32 {BB}, {T0}, {BB}")
-
-    # 64/32-bit scalar arithmetic on (lo, hi) pairs
-    def sub(self, r, a, b):  # r = a - b, SCC = borrow
-        self.e(f"s_sub_u32 {r[0]}, {a[0]}, {b[0]}")
-        if self.w == 64:
-            self.e(f"s_subb_u32 {r[1]}, {a[1]}, {b[1]}")
-
-    def add(self, r, a, b):
-        self.e(f"s_add_u32 {r[0]}, {a[0]}, {b[0]}")
-        if self.w == 64:
-            self.e(f"s_addc_u32 {r[1]}, {a[1]}, {b[1]}")
-
-    def mov(self, r, a):
-        if self.w == 64:
-            self.e(f"s_mov_b64 s[{r[0][1:]}:{r[1][1:]}], s[{a[0][1:]}:{a[1][1:]}]")
-        else:
-            self.e(f"s_mov_b32 {r[0]}, {a[0]}")
-
-    def is_zero_scc(self, t):  # SCC = (t == 0)
-        if self.w == 64:
-            self.e(f"s_or_b32 {T0}, {t[0]}, {t[1]}")
-            self.e(f"s_cmp_eq_u32 {T0}, 0")
-        else:
-            self.e(f"s_cmp_eq_u32 {t[0]}, 0")
+        e(f"s_and_b32 {T0}, {T0}, 127")
+        e(f"s_max_u32 {BB}, {BB}, {T0}")
 
     # ---- touch staging --------------------------------------------------------------
     def log(self, kr: str, a, check: bool):
         """Stage one touch {kr, amount} in lane M0.  With check: store the staging once 60
-        touches are staged (the touches an order logs before its last one); the last touch of
+        touches are staged (touches an order logs before its last one); the last touch of
         an order needs no check (the staging is also flushed at half-group boundaries)."""
         e = self.e
         e(f"v_writelane_b32 %[lk], {kr}, m0")
@@ -196,6 +225,7 @@ class Gen:
         e = self.e
         skip = self.fresh("FS")
         e(f"{fl}:")
+        e("s_mov_b64 exec, -1")
         e(f"s_add_u32 {T0}, %[lpos], 64")
         e(f"s_cmp_gt_u32 {T0}, %[lcap]")
         e(f"s_cbranch_scc1 {skip}")
@@ -209,144 +239,168 @@ class Gen:
         e("s_mov_b32 m0, 0")
         e(f"s_branch {back}")
 
-    # ---- one order --------------------------------------------------------------------
-    def order(self, r: tuple[int, int]):
-        """Apply one packed record s[r] (SetOrder, engine.go:56-85, at the aggregate level).
-        Layout: rests fall through; crossing branches out; every path ends with one jump to
-        the next order.  Lane values of non-member levels are don't-care (a level that
-        empties only leaves its mask; a rest onto a non-member level writes instead of adds;
-        k_flow_plan zeroes non-member lanes once at the end)."""
+    # ---- one order slot ---------------------------------------------------------------
+    def dispatch(self, j: int, fall: bool):
+        """Enter slot j (the next order): decode it and branch on its side.  Slots 0 and 4 open a
+        half-group: jump to its head (or fall into it)."""
         e = self.e
-        lo, hi = f"s{r[0]}", f"s{r[1]}"
+        if j % 4 == 0:
+            if not fall:
+                e(f"s_branch {self.lab(f'H{j}')}")
+            return
+        hi = f"s{BUF[j][1]}"
+        e(f"s_add_u32 {JJS}, {JJS}, 256")          # (order index + 1) << 8
+        e(f"s_bfe_u32 {LI}, {hi}, 0x70015")
+        e(f"s_bitcmp1_b32 {hi}, 28")
+        e(f"s_cbranch_scc1 {self.lab(f'S{j}')}")
+        if not fall:
+            e(f"s_branch {self.lab(f'B{j}')}")
+
+    def rest(self, side: str, T):
+        """Rest T at LI (SetOrder engine.go:80-82: depth += T, ZADD own side), branchless.
+        BUY: own top BB, beyond = LI > BB.  SALE: own top BA, beyond = LI < BA.
+          at or beyond the top: the cached depth takes T (after a new top resets it);
+          beyond (a new top): the old top's depth goes to its lane, the new top is LI;
+          behind: the lane of LI takes T (its lane is 0 if the level is new)."""
+        e = self.e
+        buy = side == "B"
+        top, topd = (BB, BBD) if buy else (BA, BAD)
+        ge, gt = ("ge", "gt") if buy else ("le", "lt")
+        e(f"s_cmp_{ge}_u32 {LI}, {top}")
+        self.csel(X, T, 0)
+        self.csel(A, 0, T)
+        e(f"s_cmp_{gt}_u32 {LI}, {top}")
+        self.csel(A, topd, A)
+        e(f"s_cselect_b32 {L}, {top}, {LI}")
+        self.csel(topd, 0, topd)
+        e(f"s_{'max' if buy else 'min'}_u32 {top}, {top}, {LI}")
+        self.add(topd, topd, X)
+        self.add_lane()
+        self.setbit("B" if buy else "A", LI, "s_bitset1_b64")
+        e(f"s_or_b32 {K}, {JJS}, {LI}")
+        e(f"s_bitset1_b32 {K}, 7")
+        self.log(K, T, False)
+
+    def partial(self, side: str, T):
+        """The crossed level keeps depth - T (MatchOrder diff < 0, engine.go:176-194)."""
+        e = self.e
+        otop, otopd = (BA, BAD) if side == "B" else (BB, BBD)
+        self.sub(otopd, otopd, T)
+        e(f"s_or_b32 {K}, {JJS}, {otop}")
+        self.log(K, T, False)
+
+    def full(self, side: str, T, i: int):
+        """The crossed level empties (engine.go:145-175; ZREM nodepool.go:76-83); T -= depth;
+        the next opposite level is promoted.  diff == 0 stops the order (engine.go:162-175)."""
+        e = self.e
+        buy = side == "B"
+        otop, otopd = (BA, BAD) if buy else (BB, BBD)
+        e(f"s_or_b32 {K}, {JJS}, {otop}")
+        self.log(K, otopd, True)
+        self.mov(T, D)
+        self.setbit("A" if buy else "B", otop, "s_bitset0_b64")
+        if buy:
+            self.lowest_ask()
+        else:
+            self.highest_bid()
+        self.promote(otop, otopd)
+        self.is_zero_scc(T)
+        e(f"s_cbranch_scc1 {self.lab(f'DN{i}')}")
+        e(f"s_cmp_{'le' if buy else 'ge'}_u32 {otop}, {LI}")
+        e(f"s_cbranch_scc1 {self.lab(f'{side}X{i}')}")
+        e(f"s_branch {self.lab(f'{side}R{i}')}")
+
+    def slot(self, i: int):
+        """Order slot i (record BUF[i]); its side was decoded by the previous path.  Layout:
+        B entry, BUY rest, BUY partial, BUY full, SALE partial, SALE full, exact-fill exit,
+        S entry, SALE rest (falls into the next slot)."""
+        e = self.e
+        lo, hi = f"s{BUF[i][0]}", f"s{BUF[i][1]}"
         T = (lo, hi)          # 32-bit: T is lo; hi keeps the flags
-        Dd = D
-        bad, bbd = BAD, BBD
-        nxt = self.fresh("NX")
-        sell = self.fresh("SE")
-        for side in ("B", "S"):
-            if side == "B":
-                own, opp = "B", "A"            # rests into S:BUY, crosses S:SALE
-                top, topd, otop, otopd = BB, bbd, BA, bad
-            else:
-                own, opp = "A", "B"
-                top, topd, otop, otopd = BA, bad, BB, bbd
-            loop, cross, full, notdeep, istop, dnew = (self.fresh(side + x) for x in ("L", "C", "F", "N", "T", "D"))
-            if side == "B":
-                e(f"s_add_u32 {JJS}, {JJS}, 256")           # (order index + 1) << 8
-                e(f"s_bfe_u32 {LI}, {hi}, 0x70015")
-                e(f"s_bitcmp1_b32 {hi}, 28")
-                e(f"s_cbranch_scc1 {sell}")
-            else:
-                e(f"{sell}:")
-            if self.w == 64:
-                e(f"s_and_b32 {hi}, {hi}, 0x1fffff")        # T = volume
-            e(f"{loop}:")
-            # crossing opposite level? BUY: best ask <= li; SALE: best bid >= li
-            e(f"s_cmp_{'le' if side == 'B' else 'ge'}_u32 {otop}, {LI}")
-            e(f"s_cbranch_scc1 {cross}")
-            # ---- rest at li (engine.go:80-82): depth += T, ZADD own side
-            e(f"s_cmp_{'lt' if side == 'B' else 'gt'}_u32 {LI}, {top}")   # strictly behind own top
-            e(f"s_cbranch_scc0 {notdeep}")
-            e(f"s_cmp_lt_u32 {LI}, 64")
-            e(f"s_cselect_b64 {M}, %[{own}0], %[{own}1]")
-            e(f"s_bitcmp1_b64 {M}, {LI}")
-            e(f"s_cbranch_scc0 {dnew}")
-            self.add_lane(LI, T)                              # existing level: lane += T
-            e(f"s_or_b32 {K}, {JJS}, {LI}")
-            e(f"s_bitset1_b32 {K}, 7")
-            self.log(K, T, False)
-            e(f"s_branch {nxt}")
-            e(f"{dnew}:")                                     # new level behind the top: lane = T
-            e(f"s_bitset1_b64 {M}, {LI}")
-            e(f"s_cmp_lt_u32 {LI}, 64")
-            e(f"s_cselect_b64 %[{own}0], {M}, %[{own}0]")
-            e(f"s_cselect_b64 %[{own}1], %[{own}1], {M}")
-            self.write(LI, T)
-            e(f"s_or_b32 {K}, {JJS}, {LI}")
-            e(f"s_bitset1_b32 {K}, 7")
-            self.log(K, T, False)
-            e(f"s_branch {nxt}")
-            e(f"{notdeep}:")
-            e(f"s_cmp_eq_u32 {LI}, {top}")
-            e(f"s_cbranch_scc1 {istop}")
-            # new own top inside the spread: evict the cached top to its lane
-            self.write(top, topd)
-            e(f"s_mov_b32 {top}, {LI}")
-            self.mov(topd, T)
-            self.setbit(own, LI, "s_bitset1_b64")
-            e(f"s_or_b32 {K}, {JJS}, {LI}")
-            e(f"s_bitset1_b32 {K}, 7")
-            self.log(K, T, False)
-            e(f"s_branch {nxt}")
-            e(f"{istop}:")
-            self.add(topd, topd, T)
-            e(f"s_or_b32 {K}, {JJS}, {LI}")
-            e(f"s_bitset1_b32 {K}, 7")
-            self.log(K, T, False)
-            e(f"s_branch {nxt}")
-            # ---- cross the best opposite level (MatchOrder, engine.go:138-198)
-            e(f"{cross}:")
-            self.sub(Dd, T, otopd)
-            e(f"s_cbranch_scc0 {full}")
-            # partial: the level keeps depth - T (engine.go:176-194)
-            self.sub(otopd, otopd, T)
-            e(f"s_or_b32 {K}, {JJS}, {otop}")
-            self.log(K, T, False)
-            e(f"s_branch {nxt}")
-            # full: the level empties (engine.go:145-175), ZREM (nodepool.go:76-83), next level
-            e(f"{full}:")
-            e(f"s_or_b32 {K}, {JJS}, {otop}")
-            self.log(K, otopd, True)
-            self.mov(T, Dd)
-            self.setbit(opp, otop, "s_bitset0_b64")
-            if side == "B":
-                self.lowest_ask()
-            else:
-                self.highest_bid()
-            self.read(otop, otopd)
-            self.is_zero_scc(T)
-            e(f"s_cbranch_scc1 {nxt}")                      # diff == 0: stop (engine.go:162-175)
-            e(f"s_branch {loop}")
-        e(f"{nxt}:")
+        j = (i + 1) % 8
+        lab = self.lab
+        # --- BUY
+        e(f"{lab(f'B{i}')}:")
+        if self.w == 64:
+            e(f"s_and_b32 {hi}, {hi}, 0x1fffff")     # T = volume
+        e(f"s_cmp_le_u32 {BA}, {LI}")                # crossing the best ask?
+        e(f"s_cbranch_scc1 {lab(f'BX{i}')}")
+        e(f"{lab(f'BR{i}')}:")
+        self.rest("B", T)
+        self.dispatch(j, False)
+        e(f"{lab(f'BX{i}')}:")
+        self.sub(D, T, BAD)
+        e(f"s_cbranch_scc0 {lab(f'BF{i}')}")
+        self.partial("B", T)
+        self.dispatch(j, False)
+        e(f"{lab(f'BF{i}')}:")
+        self.full("B", T, i)
+        # --- SALE crossing paths
+        e(f"{lab(f'SX{i}')}:")
+        self.sub(D, T, BBD)
+        e(f"s_cbranch_scc0 {lab(f'SF{i}')}")
+        self.partial("S", T)
+        self.dispatch(j, False)
+        e(f"{lab(f'SF{i}')}:")
+        self.full("S", T, i)
+        e(f"{lab(f'DN{i}')}:")
+        self.dispatch(j, False)
+        # --- SALE entry and rest
+        e(f"{lab(f'S{i}')}:")
+        if self.w == 64:
+            e(f"s_and_b32 {hi}, {hi}, 0x1fffff")
+        e(f"s_cmp_ge_u32 {BB}, {LI}")                # crossing the best bid?
+        e(f"s_cbranch_scc1 {lab(f'SX{i}')}")
+        e(f"{lab(f'SR{i}')}:")
+        self.rest("S", T)
+        self.dispatch(j, j != 0)                     # falls into slot j (or the half head H4)
+
+    def head(self, j: int):
+        """Half-group head before slot j: count the half done, wait for this half's records,
+        prefetch the next half, make room for its touches, dispatch slot j."""
+        e = self.e
+        other = 68 - 8 * (j // 4)
+        fl, back = self.fresh("HF"), self.fresh("HB")
+        hi = f"s{BUF[j][1]}"
+        e(f"{self.lab(f'H{j}')}:")
+        e(f"s_sub_u32 {HC}, {HC}, 1")
+        e(f"s_cmp_eq_u32 {HC}, 0")
+        e(f"s_cbranch_scc1 {self.lab('DONE')}")
+        e("s_waitcnt lgkmcnt(0)")
+        e("s_add_u32 s98, s98, 32")
+        e("s_addc_u32 s99, s99, 0")
+        e(f"s_load_dwordx8 s[{other}:{other + 7}], {ADDR}, 0x0")   # prefetch the next half
+        e("s_cmp_ge_u32 m0, 60")                # room for this half's 4 last touches
+        e(f"s_cbranch_scc1 {fl}")
+        e(f"{back}:")
+        self.flushes.append((fl, back))
+        e(f"s_add_u32 {JJS}, {JJS}, 256")
+        e(f"s_bfe_u32 {LI}, {hi}, 0x70015")
+        e(f"s_bitcmp1_b32 {hi}, 28")
+        e(f"s_cbranch_scc1 {self.lab(f'S{j}')}")
 
     def build(self) -> list[str]:
         e = self.e
         done = self.lab("DONE")
-        loop = self.lab("HALF")
         e("s_waitcnt vmcnt(0)")
         e(f"s_mov_b64 {ADDR}, %[ob]")
-        e(f"s_mov_b32 {HC}, %[nh]")
+        e(f"s_add_u32 {HC}, %[nh], 1")
         e(f"s_mov_b32 {JJS}, 0xffffff00")          # (-1) << 8: the first record is order 0
         e("s_mov_b32 m0, %[nacc]")
         self.lowest_ask()
-        self.read(BA, BAD)
+        self.promote(BA, BAD)
         self.highest_bid()
-        self.read(BB, BBD)
-        e(f"s_cmp_eq_u32 {HC}, 0")
-        e(f"s_cbranch_scc1 {done}")
+        self.promote(BB, BBD)
         e(f"s_load_dwordx8 s[60:67], {ADDR}, 0x0")
-        e(f"{loop}:")
-        for half in range(2):
-            other = 68 - 8 * half
-            fl, back = self.fresh("HF"), self.fresh("HB")
-            e("s_waitcnt lgkmcnt(0)")
-            e("s_add_u32 s98, s98, 32")
-            e("s_addc_u32 s99, s99, 0")
-            e(f"s_load_dwordx8 s[{other}:{other + 7}], {ADDR}, 0x0")   # prefetch the next half
-            e("s_cmp_ge_u32 m0, 60")                # room for this half's 4 last touches
-            e(f"s_cbranch_scc1 {fl}")
-            e(f"{back}:")
-            self.flushes.append((fl, back))
-            for u in range(4):
-                self.order(BUF[4 * half + u])
-            e(f"s_sub_u32 {HC}, {HC}, 1")
-            e(f"s_cmp_eq_u32 {HC}, 0")
-            e(f"s_cbranch_scc1 {done}")
-        e(f"s_branch {loop}")
+        for i in range(8):
+            if i % 4 == 0:
+                self.head(i)
+            self.slot(i)
         for fl, back in self.flushes:
             self.emit_flush(fl, back)
         e(f"{done}:")
         e("s_waitcnt lgkmcnt(0)")
+        e("s_mov_b64 exec, -1")
         self.write(BA, BAD)
         self.write(BB, BBD)
         e("s_mov_b32 %[nacc], m0")

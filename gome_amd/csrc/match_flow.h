@@ -482,12 +482,13 @@ __device__ __forceinline__ void fl_plan_book(const Dev& D, const FlowArgs& F, ui
   const bool v0 = lane >= 1 && lane <= nl, v1 = lane + 64 <= nl;
   const bool w32 = uni(hd->w32) != 0;
   const unsigned long long g = static_cast<unsigned long long>(uni64(static_cast<int64_t>(hd->g)));
-  int64_t d0 = v0 ? LV[lane].d0 : 0, d1 = v1 ? LV[lane + 64].d0 : 0;
+  const uint32_t m0 = v0 ? LV[lane].mem0 : 0u, m1 = v1 ? LV[lane + 64].mem0 : 0u;
+  // the loop's invariant: lanes of levels outside both side sets hold 0
+  int64_t d0 = (m0 & (M_SALE | M_BUY)) ? LV[lane].d0 : 0, d1 = (m1 & (M_SALE | M_BUY)) ? LV[lane + 64].d0 : 0;
   if (w32) {  // depths in units of g (exact: g divides every volume and depth of the book)
     d0 = static_cast<int64_t>(static_cast<unsigned long long>(d0) / g);
     d1 = static_cast<int64_t>(static_cast<unsigned long long>(d1) / g);
   }
-  const uint32_t m0 = v0 ? LV[lane].mem0 : 0u, m1 = v1 ? LV[lane + 64].mem0 : 0u;
   FlDepth Dp{lo32(d0), hi32(d0), lo32(d1), hi32(d1)};
   unsigned long long A0 = __ballot(m0 & M_SALE), A1 = __ballot(m1 & M_SALE) | (1ull << 63);
   unsigned long long B0 = __ballot(m0 & M_BUY) | 1ull, B1 = __ballot(m1 & M_BUY);
@@ -516,7 +517,7 @@ __device__ __forceinline__ void fl_plan_book(const Dev& D, const FlowArgs& F, ui
     if (lane == 0) atomicOr(&D.st->err, ERR_CORRUPT);
     lg.lpos = 0;
   }
-  // lanes of levels outside both side sets are don't-care in the loop: their depth is 0
+  // the loop keeps non-member lanes at 0; masking by membership also drops the sentinel lanes
   const bool in0 = (((A0 | B0) >> lane) & 1ull) != 0, in1 = (((A1 | B1) >> lane) & 1ull) != 0;
   const uint64_t u0 = w32 ? static_cast<uint64_t>(Dp.l0) * g : (static_cast<uint64_t>(Dp.h0) << 32) | Dp.l0;
   const uint64_t u1 = w32 ? static_cast<uint64_t>(Dp.l1) * g : (static_cast<uint64_t>(Dp.h1) << 32) | Dp.l1;

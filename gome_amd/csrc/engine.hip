@@ -268,7 +268,9 @@ gome_status gome_engine::init(const gome_config& c) {
       !alloc(&F.lvout, static_cast<size_t>(MAX_FLOW) * FL_CAP, "flow final levels"))
     return GOME_E_CAPACITY;
   F.maxt = ceil_div(ntouch, FL_TILE);
-  if (!alloc(&F.tcnt, static_cast<size_t>(FL_HEAD) * F.maxt * FL_CAP, "flow head tile counts")) return GOME_E_CAPACITY;
+  if (!alloc(&F.tcnt, static_cast<size_t>(FL_HEAD) * F.maxt * FL_CAP, "flow head tile counts") ||
+      !alloc(&F.pscr, FL_HEAD, "flow head prep scratch"))
+    return GOME_E_CAPACITY;
   HIPCHK(hipMemsetAsync(F.hdr, 0, sizeof(FlowHdr) * MAX_FLOW, stream));
   HIPCHK(hipMemsetAsync(d_pend, 0, sizeof(PendEnt) * nb, stream));
   if (D.idx_mask >= PEND) return fail(GOME_E_INVAL, "gome_config.max_nodes too large (index > 2^31 slots)");
@@ -376,7 +378,10 @@ gome_status gome_engine::run(const gome_order* d_ord, uint32_t n, hipStream_t s)
   const uint32_t nh_head = std::min<uint32_t>(FL_HEAD, nhot_max);
   const uint32_t nh_tail = nhot_max > FL_HEAD ? nhot_max - FL_HEAD : 0;
   HIPCHK(hipStreamWaitEvent(flow_stream, fork, 0));
-  k_flow_prep<<<nh_head, FL_PREP_T, 0, flow_stream>>>(D, B, FH);
+  HIPCHK(hipMemsetAsync(F.pscr, 0, sizeof(FlPrepScr) * FL_HEAD, flow_stream));
+  k_flow_prep_a<<<dim3(FL_PG, nh_head), FL_PREP_T, 0, flow_stream>>>(D, B, FH);
+  k_flow_prep_b<<<nh_head, FL_PREP_T, 0, flow_stream>>>(D, B, FH);
+  k_flow_prep_c<<<dim3(FL_PG, nh_head), FL_PREP_T, 0, flow_stream>>>(D, B, FH);
   HIPCHK(hipEventRecord(prep_h, flow_stream));
   HIPCHK(hipEventRecord(evf0, flow_stream));
   k_flow_plan<true><<<nh_head, 256, 0, flow_stream>>>(D, FH);

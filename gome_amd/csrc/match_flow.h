@@ -148,6 +148,7 @@ struct FlowArgs {
   uint32_t* tcnt;      // head sort: [FL_HEAD][maxt][FL_CAP] per-tile level counts, then offsets
   Level* lvout;        // head write: [MAX_FLOW * FL_CAP] final level records
   uint32_t maxt;       // tiles per head book (log capacity / FL_TILE)
+  struct FlPrepScr* pscr;  // head prep scratch [FL_HEAD] (k_flow_prep_a/b/c)
   uint32_t enabled;
   // the candidates [h0, min(h1, nhot)) this launch covers (head and tail run on their own
   // streams), and the range's offset in toff
@@ -374,6 +375,293 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep(Dev D, BatchArgs B, Flo
     x.w32 = w32 ? 1u : 0u;
     x.g = g;
     *hd = x;
+  }
+}
+
+// ============================================================== head prep, wide
+// The head's books are long (the hottest holds ~8% of a batch): one workgroup per book is
+// latency-bound on its record loads, so the head preps in three launches.
+//   k_flow_prep_a  (FL_PG blocks per book) a slice of the orders each: distinct prices into the
+//                  book's global set, slice gcd / sum, counts, order-level ineligibility;
+//   k_flow_prep_b  (one block per book) live levels, eligibility, the sorted level table (same
+//                  as k_flow_prep), the price -> level map back to the global set;
+//   k_flow_prep_c  (FL_PG blocks per book) the packed records of the slice.
+constexpr uint32_t FL_PG = 64;
+struct FlPrepScr {
+  unsigned long long key[FL_HASH];  // price set (open addressing, fl_hash, linear probing)
+  uint32_t val[FL_HASH];            // after k_flow_prep_b: level index of each key
+  unsigned long long pg[FL_PG], ps[FL_PG];  // per-slice gcd and saturated sum of volumes
+  uint32_t adds, dropped, bad, pad;
+};
+
+__device__ __forceinline__ void fl_slice(uint32_t beg, uint32_t end, uint32_t x, uint32_t& b0, uint32_t& b1) {
+  const uint64_t len = end - beg;
+  b0 = beg + static_cast<uint32_t>(len * x / FL_PG);
+  b1 = beg + static_cast<uint32_t>(len * (x + 1) / FL_PG);
+}
+
+// Insert key into an open-addressed set of FL_HASH slots (read first, CAS only on an empty
+// slot).  Returns the slot, or FL_HASH when the set is full.  *fresh = this call added it.
+template <typename KeyPtr>
+__device__ __forceinline__ uint32_t fl_set_put(KeyPtr keys, unsigned long long key, bool* fresh) {
+  uint32_t s = fl_hash(key);
+  *fresh = false;
+  for (uint32_t probe = 0; probe < FL_HASH; ++probe) {
+    const unsigned long long cur = *reinterpret_cast<volatile unsigned long long*>(&keys[s]);
+    if (cur == key) return s;
+    if (cur == 0ull) {
+      const unsigned long long prev = atomicCAS(&keys[s], 0ull, key);
+      if (prev == 0ull) {
+        *fresh = true;
+        return s;
+      }
+      if (prev == key) return s;
+    }
+    s = (s + 1) & (FL_HASH - 1);
+  }
+  return FL_HASH;
+}
+
+__device__ __forceinline__ void fl_block_gcd_sum(unsigned long long& mg, unsigned long long& msum,
+                                                 unsigned long long* wg, unsigned long long* ws) {
+  for (int off = 32; off > 0; off >>= 1) {
+    mg = fl_gcd(mg, __shfl_xor(mg, off));
+    msum = min(msum + __shfl_xor(msum, off), FL_SUM_CAP);
+  }
+  if (lane_id() == 0) { wg[threadIdx.x >> 6] = mg; ws[threadIdx.x >> 6] = msum; }
+  __syncthreads();
+  mg = msum = 0;
+  for (uint32_t w = 0; w < FL_PREP_T / 64; ++w) {
+    mg = fl_gcd(mg, wg[w]);
+    msum = min(msum + ws[w], FL_SUM_CAP);
+  }
+}
+
+__global__ __launch_bounds__(FL_PREP_T) void k_flow_prep_a(Dev D, BatchArgs B, FlowArgs F) {
+  __shared__ unsigned long long hkey[FL_HASH];
+  __shared__ uint32_t ndist, bad, adds, dropped;
+  __shared__ unsigned long long wg[FL_PREP_T / 64], ws[FL_PREP_T / 64];
+  const uint32_t hb = blockIdx.y, h = F.h0 + hb, tid = threadIdx.x;
+  if (h >= fl_hend(D, F) || !F.enabled) return;
+  FlPrepScr* P = F.pscr + hb;
+  const uint32_t seg = B.seg_order[h];
+  uint32_t b0, b1;
+  fl_slice(B.seg_start[seg], B.seg_start[seg + 1], blockIdx.x, b0, b1);
+  for (uint32_t i = tid; i < FL_HASH; i += FL_PREP_T) hkey[i] = 0;
+  if (tid == 0) ndist = bad = adds = dropped = 0;
+  __syncthreads();
+  unsigned long long mg = 0, msum = 0;
+  uint32_t my_adds = 0, my_drop = 0, my_bad = 0;
+  for (uint32_t c0 = b0 + tid; c0 < b1 && !my_bad; c0 += 4 * FL_PREP_T) {
+    Prep qs[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const uint32_t b = c0 + u * FL_PREP_T;
+      if (b < b1) qs[u] = B.prep[b];
+      else qs[u].action = 0;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const Prep q = qs[u];
+      if (q.action == GOME_DEL) { my_bad = 1; break; }
+      if (q.action != GOME_ADD) continue;
+      my_adds++;
+      if (!q.adm) { my_drop++; continue; }
+      if (q.vol == 0) { my_bad = 1; break; }
+      const unsigned long long v = static_cast<unsigned long long>(q.vol);
+      const double qd = static_cast<double>(v) / static_cast<double>(mg ? mg : 1);
+      if (mg == 0 || static_cast<unsigned long long>(qd) * mg != v) mg = fl_gcd(mg, v);
+      msum = min(msum + v, FL_SUM_CAP);
+      bool fresh;
+      const uint32_t sl = fl_set_put(hkey, static_cast<unsigned long long>(q.price) + FL_KEY_OFF, &fresh);
+      if (sl == FL_HASH || (fresh && atomicAdd(&ndist, 1u) >= FL_MAX)) { my_bad = 1; break; }
+    }
+  }
+  if (my_adds) atomicAdd(&adds, my_adds);
+  if (my_drop) atomicAdd(&dropped, my_drop);
+  if (my_bad) bad = 1;
+  fl_block_gcd_sum(mg, msum, wg, ws);  // (synchronises the block)
+  if (tid == 0) {
+    P->pg[blockIdx.x] = mg;
+    P->ps[blockIdx.x] = msum;
+    if (adds) atomicAdd(&P->adds, adds);
+    if (dropped) atomicAdd(&P->dropped, dropped);
+    if (bad) atomicOr(&P->bad, 1u);
+  }
+  if (bad) return;
+  for (uint32_t i = tid; i < FL_HASH; i += FL_PREP_T) {
+    if (hkey[i]) {
+      bool fresh;
+      if (fl_set_put(P->key, hkey[i], &fresh) == FL_HASH) atomicOr(&P->bad, 1u);
+    }
+  }
+}
+
+__global__ __launch_bounds__(FL_PREP_T) void k_flow_prep_b(Dev D, BatchArgs B, FlowArgs F) {
+  __shared__ unsigned long long hkey[FL_HASH];
+  __shared__ uint32_t hval[FL_HASH];
+  __shared__ unsigned long long ckey[FL_CAP + FL_PREP_T];
+  __shared__ uint32_t cslot[FL_CAP + FL_PREP_T];
+  __shared__ uint32_t ndist, nc, bad;
+  __shared__ unsigned long long wg[FL_PREP_T / 64], ws[FL_PREP_T / 64];
+  const uint32_t hb = blockIdx.x, h = F.h0 + hb, tid = threadIdx.x;
+  if (h >= fl_hend(D, F)) return;
+  FlowHdr* hd = &F.hdr[h];
+  FlPrepScr* P = F.pscr + hb;
+  const uint32_t seg = B.seg_order[h];
+  const uint32_t beg = B.seg_start[seg], end = B.seg_start[seg + 1];
+  const uint32_t sym = B.ord[B.prep[beg].idx].symbol_id;
+  const Book bk = D.books[sym];
+  if (tid == 0) {
+    ndist = nc = 0;
+    bad = (!F.enabled || P->bad || (bk.pad & BOOK_QUIRK) || bk.n_lvl > 4 * FL_CAP || (D.st->err & ERR_INPUT) ||
+           (end - beg) >= (1u << 24)) ? 1u : 0u;
+  }
+  __syncthreads();
+  if (bad) {
+    if (tid == 0) hd->ok = 0;
+    return;
+  }
+  uint32_t my_n = 0;
+  for (uint32_t i = tid; i < FL_HASH; i += FL_PREP_T) {
+    hkey[i] = P->key[i];
+    hval[i] = NIL;
+    my_n += hkey[i] ? 1u : 0u;
+  }
+  if (my_n) atomicAdd(&ndist, my_n);
+  __syncthreads();
+  // live levels of the book (as k_flow_prep)
+  const Level* L0 = D.lvl + bk.lvl_base;
+  unsigned long long mg = 0, msum = 0;
+  if (tid < FL_PG) {
+    mg = P->pg[tid];
+    msum = P->ps[tid];
+  }
+  for (uint32_t k = tid; k < bk.n_lvl; k += FL_PREP_T) {
+    const Level x = L0[k];
+    const uint32_t nm = (x.member & M_BUY ? 1u : 0u) + (x.member & M_SALE ? 1u : 0u);
+    if (x.nlive == 0) {
+      if (x.depth != 0 || x.member != 0) bad = 1;
+      continue;
+    }
+    if (x.depth <= 0 || nm != 1) { bad = 1; continue; }
+    mg = fl_gcd(mg, static_cast<unsigned long long>(x.depth));
+    msum = min(msum + static_cast<unsigned long long>(x.depth), FL_SUM_CAP);
+    bool fresh;
+    const uint32_t sl = fl_set_put(hkey, static_cast<unsigned long long>(x.price) + FL_KEY_OFF, &fresh);
+    if (sl == FL_HASH) { bad = 1; continue; }
+    hval[sl] = k;
+    if (fresh) atomicAdd(&ndist, 1u);
+  }
+  fl_block_gcd_sum(mg, msum, wg, ws);  // (synchronises the block)
+  if (bad || ndist > FL_MAX) {
+    if (tid == 0) hd->ok = 0;
+    return;
+  }
+  for (uint32_t sl = tid; sl < FL_HASH; sl += FL_PREP_T) {
+    if (hkey[sl]) {
+      const uint32_t i = atomicAdd(&nc, 1u);
+      ckey[i] = hkey[sl];
+      cslot[i] = sl;
+    }
+  }
+  __syncthreads();
+  const uint32_t n = nc;
+  FlowLvl* LV = F.lvl + h * FL_CAP;
+  if (tid < n) {
+    const unsigned long long key = ckey[tid];
+    uint32_t r = 0;
+    for (uint32_t i = 0; i < n; ++i) r += ckey[i] < key ? 1u : 0u;
+    const uint32_t sl = cslot[tid], old = hval[sl];
+    FlowLvl f{};
+    f.price = static_cast<int64_t>(key - FL_KEY_OFF);
+    f.old = old;
+    f.head = f.tail = NIL;
+    f.ig_base = 0;
+    if (old != NIL) {
+      const Level x = L0[old];
+      f.d0 = x.depth;
+      f.nv0 = x.nlive;
+      f.head = x.head;
+      f.tail = x.tail;
+      f.hslot = x.hslot;
+      f.tslot = x.tslot;
+      f.mem0 = x.member;
+    }
+    LV[r + 1] = f;
+    hval[sl] = r + 1;
+  }
+  __syncthreads();
+  for (uint32_t i = tid; i < FL_HASH; i += FL_PREP_T) {
+    P->key[i] = hkey[i];
+    P->val[i] = hval[i];
+  }
+  unsigned long long g = mg ? mg : 1;
+  const bool w32 = msum < FL_SUM_CAP && msum / g < (1ull << 32);
+  if (!w32) g = 1;
+  const uint32_t obase = fl_obase(beg, seg);
+  if (tid < ((4u - ((end - beg) & 3u)) & 3u))  // padding to whole half-groups
+    F.ord8[obase + (end - beg) + tid] = OR_NOP;
+  if (tid == 0) {
+    FlowHdr x{};
+    x.ok = 1;
+    x.nl = n;
+    x.sym = sym;
+    x.beg = beg;
+    x.end = end;
+    x.nold = bk.n_lvl;
+    x.adds = P->adds;
+    x.dropped = P->dropped;
+    x.obase = obase;
+    x.w32 = w32 ? 1u : 0u;
+    x.g = g;
+    *hd = x;
+  }
+}
+
+__global__ __launch_bounds__(FL_PREP_T) void k_flow_prep_c(Dev D, BatchArgs B, FlowArgs F) {
+  __shared__ unsigned long long hkey[FL_HASH];
+  __shared__ uint32_t hval[FL_HASH];
+  const uint32_t hb = blockIdx.y, h = F.h0 + hb, tid = threadIdx.x;
+  if (h >= fl_hend(D, F) || !uni(F.hdr[h].ok)) return;
+  const FlPrepScr* P = F.pscr + hb;
+  const FlowHdr* hd = &F.hdr[h];
+  const uint32_t beg = hd->beg, obase = hd->obase;
+  const bool w32 = hd->w32 != 0;
+  const unsigned long long g = hd->g;
+  uint32_t b0, b1;
+  fl_slice(beg, hd->end, blockIdx.x, b0, b1);
+  for (uint32_t i = tid; i < FL_HASH; i += FL_PREP_T) {
+    hkey[i] = P->key[i];
+    hval[i] = P->val[i];
+  }
+  __syncthreads();
+  for (uint32_t c0 = b0 + tid; c0 < b1; c0 += 4 * FL_PREP_T) {
+    Prep qs[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const uint32_t b = c0 + u * FL_PREP_T;
+      if (b < b1) qs[u] = B.prep[b];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const uint32_t b = c0 + u * FL_PREP_T;
+      if (b >= b1) break;
+      const Prep q = qs[u];
+      unsigned long long rec = OR_NOP;
+      if (q.action == GOME_ADD && q.adm) {
+        const unsigned long long key = static_cast<unsigned long long>(q.price) + FL_KEY_OFF;
+        uint32_t s = fl_hash(key);
+        while (hkey[s] != key) s = (s + 1) & (FL_HASH - 1);
+        const uint32_t li = hval[s];
+        const unsigned long long v = w32 ? static_cast<unsigned long long>(static_cast<double>(q.vol) / static_cast<double>(g))
+                                         : static_cast<unsigned long long>(q.vol);
+        const uint32_t hi = static_cast<uint32_t>(v >> 32) | (li << OR_LI_SHIFT) | (q.side == GOME_SALE ? OR_SELL : 0u);
+        rec = (static_cast<unsigned long long>(hi) << 32) | static_cast<uint32_t>(v);
+      }
+      F.ord8[obase + (b - beg)] = rec;
+      B.ev_count[q.idx] = 0;
+    }
   }
 }
 

@@ -248,13 +248,25 @@ class Gen:
             if not fall:
                 e(f"s_branch {self.lab(f'H{j}')}")
             return
-        hi = f"s{BUF[j][1]}"
-        e(f"s_add_u32 {JJS}, {JJS}, 256")          # (order index + 1) << 8
-        e(f"s_bfe_u32 {LI}, {hi}, 0x70015")
-        e(f"s_bitcmp1_b32 {hi}, 28")
+        self.decode(j)
         e(f"s_cbranch_scc1 {self.lab(f'S{j}')}")
         if not fall:
             e(f"s_branch {self.lab(f'B{j}')}")
+
+    def decode(self, j: int):
+        """LI of record j and SCC = its side is SALE.  W64 record hi: volume bits 32..52 in
+        [0, 21), LI in [21, 28), SALE at 28; the touch key is JJS | level (| 128 for a rest),
+        JJS = order index << 8.  W32 record hi: LI in [0, 7), 1 << 7, the order index in
+        [8, 31), SALE at 31, i.e. the rest touch key itself (k_flow_* mask the index)."""
+        e = self.e
+        hi = f"s{BUF[j][1]}"
+        if self.w == 64:
+            e(f"s_add_u32 {JJS}, {JJS}, 256")      # (order index + 1) << 8
+            e(f"s_bfe_u32 {LI}, {hi}, 0x70015")
+            e(f"s_bitcmp1_b32 {hi}, 28")
+        else:
+            e(f"s_and_b32 {LI}, {hi}, 127")
+            e(f"s_bitcmp1_b32 {hi}, 31")
 
     def rest(self, side: str, T):
         """Rest T at LI (SetOrder engine.go:80-82: depth += T, ZADD own side), branchless.
@@ -277,9 +289,20 @@ class Gen:
         self.add(topd, topd, X)
         self.add_lane()
         self.setbit("B" if buy else "A", LI, "s_bitset1_b64")
-        e(f"s_or_b32 {K}, {JJS}, {LI}")
-        e(f"s_bitset1_b32 {K}, 7")
-        self.log(K, T, False)
+        if self.w == 64:
+            e(f"s_or_b32 {K}, {JJS}, {LI}")
+            e(f"s_bitset1_b32 {K}, 7")
+            self.log(K, T, False)
+        else:
+            self.log(self.hi_of(T), T, False)
+
+    def hi_of(self, T) -> str:
+        return T[1]
+
+    def cross_entry(self, T):
+        """First crossing of an order (W32): the consume key base, order index << 8."""
+        if self.w == 32:
+            self.e(f"s_and_b32 {JJS}, {self.hi_of(T)}, 0xffffff00")
 
     def partial(self, side: str, T):
         """The crossed level keeps depth - T (MatchOrder diff < 0, engine.go:176-194)."""
@@ -306,9 +329,12 @@ class Gen:
         self.promote(otop, otopd)
         self.is_zero_scc(T)
         e(f"s_cbranch_scc1 {self.lab(f'DN{i}')}")
-        e(f"s_cmp_{'le' if buy else 'ge'}_u32 {otop}, {LI}")
-        e(f"s_cbranch_scc1 {self.lab(f'{side}X{i}')}")
-        e(f"s_branch {self.lab(f'{side}R{i}')}")
+        e(f"s_cmp_{'le' if buy else 'ge'}_u32 {otop}, {LI}")   # still crossing?
+        e(f"s_cbranch_scc0 {self.lab(f'{side}R{i}')}")
+        self.sub(D, T, otopd)                                 # the next level, inline
+        e(f"s_cbranch_scc0 {self.lab(f'{side}F{i}')}")
+        self.partial(side, T)
+        self.dispatch((i + 1) % 8, False)
 
     def slot(self, i: int):
         """Order slot i (record BUF[i]); its side was decoded by the previous path.  Layout:
@@ -324,11 +350,12 @@ class Gen:
         if self.w == 64:
             e(f"s_and_b32 {hi}, {hi}, 0x1fffff")     # T = volume
         e(f"s_cmp_le_u32 {BA}, {LI}")                # crossing the best ask?
-        e(f"s_cbranch_scc1 {lab(f'BX{i}')}")
+        e(f"s_cbranch_scc1 {lab(f'BXE{i}')}")
         e(f"{lab(f'BR{i}')}:")
         self.rest("B", T)
         self.dispatch(j, False)
-        e(f"{lab(f'BX{i}')}:")
+        e(f"{lab(f'BXE{i}')}:")
+        self.cross_entry(T)
         self.sub(D, T, BAD)
         e(f"s_cbranch_scc0 {lab(f'BF{i}')}")
         self.partial("B", T)
@@ -336,7 +363,8 @@ class Gen:
         e(f"{lab(f'BF{i}')}:")
         self.full("B", T, i)
         # --- SALE crossing paths
-        e(f"{lab(f'SX{i}')}:")
+        e(f"{lab(f'SXE{i}')}:")
+        self.cross_entry(T)
         self.sub(D, T, BBD)
         e(f"s_cbranch_scc0 {lab(f'SF{i}')}")
         self.partial("S", T)
@@ -350,7 +378,7 @@ class Gen:
         if self.w == 64:
             e(f"s_and_b32 {hi}, {hi}, 0x1fffff")
         e(f"s_cmp_ge_u32 {BB}, {LI}")                # crossing the best bid?
-        e(f"s_cbranch_scc1 {lab(f'SX{i}')}")
+        e(f"s_cbranch_scc1 {lab(f'SXE{i}')}")
         e(f"{lab(f'SR{i}')}:")
         self.rest("S", T)
         self.dispatch(j, j != 0)                     # falls into slot j (or the half head H4)
@@ -374,9 +402,7 @@ class Gen:
         e(f"s_cbranch_scc1 {fl}")
         e(f"{back}:")
         self.flushes.append((fl, back))
-        e(f"s_add_u32 {JJS}, {JJS}, 256")
-        e(f"s_bfe_u32 {LI}, {hi}, 0x70015")
-        e(f"s_bitcmp1_b32 {hi}, 28")
+        self.decode(j)
         e(f"s_cbranch_scc1 {self.lab(f'S{j}')}")
 
     def build(self) -> list[str]:

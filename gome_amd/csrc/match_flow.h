@@ -67,6 +67,7 @@ constexpr uint32_t FL_ORD8_MUL = 9, FL_ORD8_PAD = 64;  // ord8 capacity: 9 * max
 // that must not touch the book (dropped ADD, ignored action, padding) is 0: a zero-volume BUY
 // rest at sentinel level 0, which changes nothing and whose touch no later kernel reads.
 constexpr uint32_t OR_LI_SHIFT = 21, OR_SELL = 1u << 28;
+constexpr uint32_t FL_MAX_ORDERS = (1u << 23) - 4;  // order index (padding included) fits [8, 31) of a touch key
 constexpr unsigned long long OR_NOP = 0ull;
 
 enum : uint32_t { TK_CONS = 0, TK_REST = 1 };
@@ -76,7 +77,7 @@ struct Touch {       // one level visited by one order (16 B)
   uint32_t pos;      // position in the level-sorted runs (set by k_flow_sort)
   int64_t amt;       // volume taken from the level (CONS) or rested at it (REST)
 };
-__device__ __forceinline__ uint32_t tk_j(const Touch& x) { return x.kr >> 8; }
+__device__ __forceinline__ uint32_t tk_j(const Touch& x) { return (x.kr >> 8) & 0x7FFFFFu; }  // bit 31: W32 records' side
 static_assert(sizeof(Touch) == 16, "Touch layout");
 
 struct SEnt {        // a touch in its level's run (32 B)
@@ -177,6 +178,21 @@ __device__ __forceinline__ unsigned long long fl_gcd(unsigned long long a, unsig
 
 constexpr unsigned long long FL_SUM_CAP = 1ull << 62;  // saturation of the volume sum
 
+// Packed plan record of order j of a book.  W64: hi = volume bits 32..52 | li << 21 |
+// SALE << 28 (no-op: 0).  W32 (volume in units of g < 2^32): hi = li | 1 << 7 | j << 8 |
+// SALE << 31, the key of the touch the order logs when it rests; a no-op (dropped / ignored
+// order, padding) rests 0 at the bid sentinel level 0: hi = 1 << 7 | j << 8.
+__device__ __forceinline__ unsigned long long fl_rec(bool live, uint32_t li, unsigned long long v, bool sell,
+                                                     uint32_t j, bool w32) {
+  if (w32) {
+    const uint32_t hi = (live ? li | (sell ? 0x80000000u : 0u) : 0u) | 0x80u | (j << 8);
+    return (static_cast<unsigned long long>(hi) << 32) | (live ? static_cast<uint32_t>(v) : 0u);
+  }
+  if (!live) return OR_NOP;
+  const uint32_t hi = static_cast<uint32_t>(v >> 32) | (li << OR_LI_SHIFT) | (sell ? OR_SELL : 0u);
+  return (static_cast<unsigned long long>(hi) << 32) | static_cast<uint32_t>(v);
+}
+
 // ============================================================== k_flow_prep
 __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep(Dev D, BatchArgs B, FlowArgs F) {
   __shared__ unsigned long long hkey[FL_HASH];
@@ -196,7 +212,7 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep(Dev D, BatchArgs B, Flo
   if (tid == 0) {
     ndist = nc = adds = dropped = 0;
     bad = (!F.enabled || (bk.pad & BOOK_QUIRK) || bk.n_lvl > 4 * FL_CAP || (D.st->err & ERR_INPUT) ||
-           (end - beg) >= (1u << 24)) ? 1u : 0u;
+           (end - beg) >= FL_MAX_ORDERS) ? 1u : 0u;
   }
   __syncthreads();
   auto insert = [&](unsigned long long key, uint32_t val) {
@@ -332,7 +348,7 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep(Dev D, BatchArgs B, Flo
   const bool w32 = sum < FL_SUM_CAP && sum / g < (1ull << 32);
   if (!w32) g = 1;
   if (tid < ((4u - ((end - beg) & 3u)) & 3u))  // padding to whole half-groups
-    F.ord8[obase + (end - beg) + tid] = OR_NOP;
+    F.ord8[obase + (end - beg) + tid] = fl_rec(false, 0, 0, false, end - beg + tid, w32);
   for (uint32_t b0 = beg + tid; b0 < end; b0 += 4 * FL_PREP_T) {
     Prep qs[4];
 #pragma unroll
@@ -345,7 +361,7 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep(Dev D, BatchArgs B, Flo
     const uint32_t b = b0 + u * FL_PREP_T;
     if (b >= end) break;
     const Prep q = qs[u];
-    unsigned long long rec = OR_NOP;
+    unsigned long long rec = fl_rec(false, 0, 0, false, b - beg, w32);
     if (q.action == GOME_ADD && q.adm) {
       const unsigned long long key = static_cast<unsigned long long>(q.price) + FL_KEY_OFF;
       uint32_t s = fl_hash(key);
@@ -354,8 +370,7 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep(Dev D, BatchArgs B, Flo
       // w32: the volume in units of g (exact: an integer quotient < 2^32 of doubles < 2^53)
       const unsigned long long v = w32 ? static_cast<unsigned long long>(static_cast<double>(q.vol) / static_cast<double>(g))
                                        : static_cast<unsigned long long>(q.vol);
-      const uint32_t hi = static_cast<uint32_t>(v >> 32) | (li << OR_LI_SHIFT) | (q.side == GOME_SALE ? OR_SELL : 0u);
-      rec = (static_cast<unsigned long long>(hi) << 32) | static_cast<uint32_t>(v);
+      rec = fl_rec(true, li, v, q.side == GOME_SALE, b - beg, w32);
     }
     F.ord8[obase + (b - beg)] = rec;
     B.ev_count[q.idx] = 0;
@@ -515,7 +530,7 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep_b(Dev D, BatchArgs B, F
   if (tid == 0) {
     ndist = nc = 0;
     bad = (!F.enabled || P->bad || (bk.pad & BOOK_QUIRK) || bk.n_lvl > 4 * FL_CAP || (D.st->err & ERR_INPUT) ||
-           (end - beg) >= (1u << 24)) ? 1u : 0u;
+           (end - beg) >= FL_MAX_ORDERS) ? 1u : 0u;
   }
   __syncthreads();
   if (bad) {
@@ -601,7 +616,7 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep_b(Dev D, BatchArgs B, F
   if (!w32) g = 1;
   const uint32_t obase = fl_obase(beg, seg);
   if (tid < ((4u - ((end - beg) & 3u)) & 3u))  // padding to whole half-groups
-    F.ord8[obase + (end - beg) + tid] = OR_NOP;
+    F.ord8[obase + (end - beg) + tid] = fl_rec(false, 0, 0, false, end - beg + tid, w32);
   if (tid == 0) {
     FlowHdr x{};
     x.ok = 1;
@@ -648,7 +663,7 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep_c(Dev D, BatchArgs B, F
       const uint32_t b = c0 + u * FL_PREP_T;
       if (b >= b1) break;
       const Prep q = qs[u];
-      unsigned long long rec = OR_NOP;
+      unsigned long long rec = fl_rec(false, 0, 0, false, b - beg, w32);
       if (q.action == GOME_ADD && q.adm) {
         const unsigned long long key = static_cast<unsigned long long>(q.price) + FL_KEY_OFF;
         uint32_t s = fl_hash(key);
@@ -656,8 +671,7 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep_c(Dev D, BatchArgs B, F
         const uint32_t li = hval[s];
         const unsigned long long v = w32 ? static_cast<unsigned long long>(static_cast<double>(q.vol) / static_cast<double>(g))
                                          : static_cast<unsigned long long>(q.vol);
-        const uint32_t hi = static_cast<uint32_t>(v >> 32) | (li << OR_LI_SHIFT) | (q.side == GOME_SALE ? OR_SELL : 0u);
-        rec = (static_cast<unsigned long long>(hi) << 32) | static_cast<uint32_t>(v);
+        rec = fl_rec(true, li, v, q.side == GOME_SALE, b - beg, w32);
       }
       F.ord8[obase + (b - beg)] = rec;
       B.ev_count[q.idx] = 0;

@@ -496,7 +496,12 @@ uint32_t gome_abi_version(void) { return GOME_ABI_VERSION; }
 #ifdef GOME_STAMPS
 // Diagnostic builds only: per-hot-wave phase cycle sums (see match_hot.h).
 int gome_debug_stamps(unsigned long long* out, size_t n) {
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(gome::g_stamps), std::min<size_t>(n, 256 * NSTAMP) * 8, 0,
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(gome::g_stamps), std::min<size_t>(n, 256 * NSTAMP) * 8, 0,
+                          hipMemcpyDeviceToHost) != hipSuccess)
+    return -1;
+  if (n <= 256 * NSTAMP) return 0;  // then the plan stamps of the head books
+  return hipMemcpyFromSymbol(out + 256 * NSTAMP, HIP_SYMBOL(gome::g_pstamps),
+                             std::min<size_t>(n - 256 * NSTAMP, gome::FL_HEAD * 4) * 8, 0,
                              hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
 }
 #endif

@@ -250,8 +250,12 @@ class Gen:
             return
         self.decode(j)
         e(f"s_cbranch_scc1 {self.lab(f'S{j}')}")
-        if not fall:
-            e(f"s_branch {self.lab(f'B{j}')}")
+        if not fall:                               # slot j's BUY entry, inline
+            if self.w == 64:
+                e(f"s_and_b32 s{BUF[j][1]}, s{BUF[j][1]}, 0x1fffff")
+            e(f"s_cmp_le_u32 {BA}, {LI}")
+            e(f"s_cbranch_scc1 {self.lab(f'BXE{j}')}")
+            e(f"s_branch {self.lab(f'BR{j}')}")
 
     def decode(self, j: int):
         """LI of record j and SCC = its side is SALE.  W64 record hi: volume bits 32..52 in

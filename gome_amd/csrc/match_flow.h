@@ -757,6 +757,11 @@ struct FlLog {
 
 
 __device__ __forceinline__ void fl_plan_book(const Dev& D, const FlowArgs& F, uint32_t h);
+#ifdef GOME_STAMPS
+// Diagnostic build only: per head book {shader cycles, 100 MHz ticks, orders, touches} of the
+// plan loop (read with gome_debug_stamps after the hot-kernel stamps).
+__device__ unsigned long long g_pstamps[FL_HEAD * 4];
+#endif
 
 // EXCL: the block is 4 waves that each hold the whole register file of their SIMD (all 512
 // VGPR+AGPR), so no other wave can share the CU — in particular not its scalar unit, which
@@ -808,9 +813,21 @@ __device__ __forceinline__ void fl_plan_book(const Dev& D, const FlowArgs& F, ui
     [nacc] "+s"(lg.nacc), [lpos] "+s"(lg.lpos), [voff] "=&v"(voff), [vt] "=&v"(vt)                      \
   : [ob] "s"(ob), [nh] "s"(nh), [logp] "s"(logp), [lcap] "s"(lg.lcap), [vl16] "v"(vl16)                \
   : FL_PLAN_CLOBBERS, "scc", "vcc", "memory"
+#ifdef GOME_STAMPS
+  const unsigned long long sc0 = __builtin_amdgcn_s_memtime(), sr0 = __builtin_amdgcn_s_memrealtime();
+#endif
   if (w32) asm volatile(FL_PLAN_ASM32 FL_PLAN_OPERANDS);
   else asm volatile(FL_PLAN_ASM64 FL_PLAN_OPERANDS);
 #undef FL_PLAN_OPERANDS
+#ifdef GOME_STAMPS
+  const unsigned long long sc1 = __builtin_amdgcn_s_memtime(), sr1 = __builtin_amdgcn_s_memrealtime();
+  if (lane == 0 && h < FL_HEAD) {
+    g_pstamps[h * 4 + 0] = sc1 - sc0;
+    g_pstamps[h * 4 + 1] = sr1 - sr0;
+    g_pstamps[h * 4 + 2] = n;
+    g_pstamps[h * 4 + 3] = lg.lpos + lg.nacc;
+  }
+#endif
   if (lg.nacc) {
     if (lane < lg.nacc && lg.lpos + lg.nacc <= lg.lcap) lg.p[lg.lpos + lane] = v4(lg.lk, 0u, lg.la, lg.lb);
     lg.lpos += lg.nacc;

@@ -58,6 +58,7 @@ class Gen:
         self.out: list[str] = []
         self.uid = 0
         self.flushes: list[tuple[str, str]] = []
+        self.slow: list[list[str]] = []      # out-of-line blocks, emitted after the loop
 
     def e(self, line: str):
         self.out.append(line)
@@ -323,7 +324,7 @@ class Gen:
         buy = side == "B"
         otop, otopd = (BA, BAD) if buy else (BB, BBD)
         e(f"s_or_b32 {K}, {JJS}, {otop}")
-        self.log(K, otopd, True)
+        self.log(K, otopd, False)        # (the staging check is folded into the test below)
         self.mov(T, D)
         self.setbit("A" if buy else "B", otop, "s_bitset0_b64")
         if buy:
@@ -331,10 +332,26 @@ class Gen:
         else:
             self.highest_bid()
         self.promote(otop, otopd)
+        # one branch for the common case "T > 0, room in the staging, the next level crosses
+        # too": T == 0 or a full staging make the limit a level that cannot cross
+        never = "0" if buy else "127"
+        cmp = "le" if buy else "ge"
+        slow, cont = self.lab(f"{side}SL{i}"), self.lab(f"{side}CN{i}")
         self.is_zero_scc(T)
-        e(f"s_cbranch_scc1 {self.lab(f'DN{i}')}")
-        e(f"s_cmp_{'le' if buy else 'ge'}_u32 {otop}, {LI}")   # still crossing?
-        e(f"s_cbranch_scc0 {self.lab(f'{side}R{i}')}")
+        e(f"s_cselect_b32 {T0}, {never}, {LI}")
+        e("s_cmp_ge_u32 m0, 60")
+        e(f"s_cselect_b32 {T0}, {never}, {T0}")
+        e(f"s_cmp_{cmp}_u32 {otop}, {T0}")
+        e(f"s_cbranch_scc0 {slow}")
+        fl = self.fresh("FL")
+        self.flushes.append((fl, slow))
+        blk = [f"{slow}:", "s_cmp_ge_u32 m0, 60", f"s_cbranch_scc1 {fl}"]
+        blk += ([f"s_cmp_eq_u64 {self.pair(T)}, 0"] if self.w == 64 else [f"s_cmp_eq_u32 {T[0]}, 0"])
+        blk += [f"s_cbranch_scc1 {self.lab(f'DN{i}')}",     # diff == 0: stop (engine.go:162-175)
+                f"s_cmp_{cmp}_u32 {otop}, {LI}", f"s_cbranch_scc1 {cont}",
+                f"s_branch {self.lab(f'{side}R{i}')}"]
+        self.slow.append(blk)
+        e(f"{cont}:")
         self.sub(D, T, otopd)                                 # the next level, inline
         e(f"s_cbranch_scc0 {self.lab(f'{side}F{i}')}")
         self.partial(side, T)
@@ -394,18 +411,22 @@ class Gen:
         other = 68 - 8 * (j // 4)
         fl, back = self.fresh("HF"), self.fresh("HB")
         hi = f"s{BUF[j][1]}"
+        # one branch for "the book is done or the staging needs room for this half's 4 last
+        # touches"; the out-of-line block tells them apart
         e(f"{self.lab(f'H{j}')}:")
         e(f"s_sub_u32 {HC}, {HC}, 1")
         e(f"s_cmp_eq_u32 {HC}, 0")
-        e(f"s_cbranch_scc1 {self.lab('DONE')}")
+        e(f"s_cselect_b32 {T0}, 99, m0")
+        e(f"s_cmp_ge_u32 {T0}, 60")
+        hs = self.fresh("HS")
+        e(f"s_cbranch_scc1 {hs}")
+        e(f"{back}:")
+        self.slow.append([f"{hs}:", f"s_cmp_eq_u32 {HC}, 0", f"s_cbranch_scc1 {self.lab('DONE')}", f"s_branch {fl}"])
+        self.flushes.append((fl, back))
         e("s_waitcnt lgkmcnt(0)")
         e("s_add_u32 s98, s98, 32")
         e("s_addc_u32 s99, s99, 0")
         e(f"s_load_dwordx8 s[{other}:{other + 7}], {ADDR}, 0x0")   # prefetch the next half
-        e("s_cmp_ge_u32 m0, 60")                # room for this half's 4 last touches
-        e(f"s_cbranch_scc1 {fl}")
-        e(f"{back}:")
-        self.flushes.append((fl, back))
         self.decode(j)
         e(f"s_cbranch_scc1 {self.lab(f'S{j}')}")
 
@@ -426,6 +447,9 @@ class Gen:
             if i % 4 == 0:
                 self.head(i)
             self.slot(i)
+        for blk in self.slow:
+            for line in blk:
+                e(line)
         for fl, back in self.flushes:
             self.emit_flush(fl, back)
         e(f"{done}:")
@@ -437,13 +461,27 @@ class Gen:
         return self.out
 
 
+ALIGN = int(os.environ.get("GOME_PLAN_ALIGN", "0"))   # log2 byte alignment of branch targets
+
+
+def aligned(lines: list[str]) -> list[str]:
+    if not ALIGN:
+        return lines
+    out = []
+    for line in lines:
+        if line.endswith(":"):
+            out.append(f".p2align {ALIGN}")
+        out.append(line)
+    return out
+
+
 def main():
     here = os.path.dirname(os.path.abspath(__file__))
     with open(os.path.join(here, "flow_plan_asm.inc"), "w") as f:
         f.write("// Generated by gen_plan_asm.py — do not edit.\n")
         for w in (64, 32):
             f.write(f"#define FL_PLAN_ASM{w} \\\n")
-            for line in Gen(w).build():
+            for line in aligned(Gen(w).build()):
                 f.write(f'  "{line}\\n\\t" \\\n')
             f.write('  ""\n')
         f.write("#define FL_PLAN_CLOBBERS " + ", ".join(f'"{c}"' for c in CLOBBERS) + "\n")

@@ -15,7 +15,7 @@ torch.zeros(1, device="cuda")
 from gome_amd import abi  # noqa: E402
 from gome_amd import workload as wl  # noqa: E402
 
-lib = abi.load_library(os.path.join(ROOT, "gome_amd", "libgome_stamps.so"))
+lib = abi.load_library(os.path.join(ROOT, "gome_amd", os.environ.get("GOME_STAMPS_LIB", "libgome_stamps.so")))
 lib.gome_debug_stamps.argtypes = [C.c_void_p, C.c_size_t]
 NST = 256 * 16
 N = 200000

@@ -50,6 +50,7 @@ HC = "s97"                       # half-groups left + 1
 ADDR = "s[98:99]"                # SMEM address of the next half-group
 SAVE = "s100"                    # M0 (staging count) saved around lane writes
 CLOBBERS = [f"s{i}" for i in range(60, 101)]
+COPY_REST = os.environ.get("GOME_PLAN_COPY", "0") == "1"   # measured: no gain, 1.35x code
 
 
 class Gen:
@@ -241,9 +242,11 @@ class Gen:
         e(f"s_branch {back}")
 
     # ---- one order slot ---------------------------------------------------------------
-    def dispatch(self, j: int, fall: bool):
+    def dispatch(self, j: int, fall: bool, copy: bool = COPY_REST):
         """Enter slot j (the next order): decode it and branch on its side.  Slots 0 and 4 open a
-        half-group: jump to its head (or fall into it)."""
+        half-group: jump to its head (or fall into it).  With copy, a BUY rest of slot j (the
+        most frequent transition that cannot fall through) runs from a private copy of the
+        rest body here instead of jumping to BR_j."""
         e = self.e
         if j % 4 == 0:
             if not fall:
@@ -256,7 +259,11 @@ class Gen:
                 e(f"s_and_b32 s{BUF[j][1]}, s{BUF[j][1]}, 0x1fffff")
             e(f"s_cmp_le_u32 {BA}, {LI}")
             e(f"s_cbranch_scc1 {self.lab(f'BXE{j}')}")
-            e(f"s_branch {self.lab(f'BR{j}')}")
+            if copy:
+                self.rest("B", (f"s{BUF[j][0]}", f"s{BUF[j][1]}"))
+                self.dispatch((j + 1) % 8, False, False)
+            else:
+                e(f"s_branch {self.lab(f'BR{j}')}")
 
     def decode(self, j: int):
         """LI of record j and SCC = its side is SALE.  W64 record hi: volume bits 32..52 in

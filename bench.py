@@ -50,9 +50,9 @@ def hot_algorithmic_bytes(st: dict) -> int:
 
 
 def plan_algorithmic_bytes(st: dict) -> int:
-    """Bytes k_flow_plan must move per launch: one 8-B packed record read
-    per order of the flow books, one 16-B touch written per level an order visits."""
-    return 8 * st["n_flow_orders"] + 16 * st["n_flow_touches"]
+    """Bytes k_flow_plan_head must move per launch: one 8-B packed record read
+    per order of the head's flow books, one 16-B touch written per level an order visits."""
+    return 8 * st["n_flow_head_orders"] + 16 * st["n_flow_head_touches"]
 
 
 def shard_stream(n_symbols, zipf_s, rank, world, seed):
@@ -202,7 +202,7 @@ def main():
     balg = sum(algorithmic_bytes(s) for s in sts) / steps
     flow = sum(s["n_flow_books"] for s in sts) > 0
     if flow:  # the flow path's serial plan is the dominant kernel
-        kname = "k_flow_plan (serial aggregate plan of the flow books)"
+        kname = "k_flow_plan_head (serial aggregate plan of the longest flow books)"
         ms_hot = sum(s["ms_flow_plan"] for s in sts) / steps
         bhot = sum(plan_algorithmic_bytes(s) for s in sts) / steps
     else:
@@ -224,7 +224,7 @@ def main():
     if os.path.exists(args.traffic_json):
         try:
             tj = json.load(open(args.traffic_json))
-            traffic = tj.get("k_flow_plan_hbm_bytes_per_launch" if flow else "k_match_hot_hbm_bytes_per_launch")
+            traffic = tj.get("k_flow_plan_head_hbm_bytes_per_launch" if flow else "k_match_hot_hbm_bytes_per_launch")
         except (OSError, ValueError):
             traffic = None
 

@@ -43,7 +43,8 @@ class Stats(C.Structure):
         ("n_hot", C.c_uint64), ("n_hot_orders", C.c_uint64), ("n_hot_fills", C.c_uint64),
         ("n_hot_rests", C.c_uint64), ("n_hot_cancels", C.c_uint64),
         ("n_flow_books", C.c_uint64), ("n_flow_orders", C.c_uint64), ("n_flow_touches", C.c_uint64),
-        ("ms_flow_plan", C.c_double)]
+        ("ms_flow_plan", C.c_double), ("n_flow_head_orders", C.c_uint64),
+        ("n_flow_head_touches", C.c_uint64)]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_}

@@ -79,6 +79,7 @@ enum {
   C_RESTING_DELTA, C_LEVELS_DELTA, C_MAXSEG, C_NSEG,
   C_HOT_ORDERS, C_HOT_FILLS, C_HOT_RESTS, C_HOT_CANCELS,  // hot books (flow + legacy)
   C_FLOW_BOOKS, C_FLOW_ORDERS, C_FLOW_TOUCHES,            // hot books on the flow path
+  C_FLOW_HEAD_ORDERS, C_FLOW_HEAD_TOUCHES,                // ... of which the head (k_flow_plan_head)
   C_NCTR = 20
 };
 

@@ -384,7 +384,7 @@ gome_status gome_engine::run(const gome_order* d_ord, uint32_t n, hipStream_t s)
   k_flow_prep_c<<<dim3(FL_PG, nh_head), FL_PREP_T, 0, flow_stream>>>(D, B, FH);
   HIPCHK(hipEventRecord(prep_h, flow_stream));
   HIPCHK(hipEventRecord(evf0, flow_stream));
-  k_flow_plan<true><<<nh_head, 256, 0, flow_stream>>>(D, FH);
+  k_flow_plan_head<<<nh_head, 256, 0, flow_stream>>>(D, FH);
   HIPCHK(hipEventRecord(evf1, flow_stream));
   // the head's reconstruction: wide kernels (tile-parallel sort, one wave per level)
   k_flow_sort_cnt<<<dim3(FL_SORT_GRID, nh_head), FL_TILE, 0, flow_stream>>>(D, FH);
@@ -403,7 +403,7 @@ gome_status gome_engine::run(const gome_order* d_ord, uint32_t n, hipStream_t s)
   if (nh_tail) {
     k_flow_prep<<<nh_tail, FL_PREP_T, 0, hot_stream>>>(D, B, FT);
     HIPCHK(hipEventRecord(prep_t, hot_stream));
-    k_flow_plan<false><<<nh_tail, 64, 0, hot_stream>>>(D, FT);
+    k_flow_plan_tail<<<nh_tail, 64, 0, hot_stream>>>(D, FT);
     k_flow_sort<<<nh_tail, FL_SORT_T, 0, hot_stream>>>(D, FT);
     k_flow_level<<<nh_tail, FL_LEVEL_T, 0, hot_stream>>>(D, FT);
     k_flow_toff<<<1, 1024, 0, hot_stream>>>(D, FT);
@@ -464,6 +464,8 @@ gome_status gome_engine::run(const gome_order* d_ord, uint32_t n, hipStream_t s)
   stats.n_flow_books = st.ctr[C_FLOW_BOOKS];
   stats.n_flow_orders = st.ctr[C_FLOW_ORDERS];
   stats.n_flow_touches = st.ctr[C_FLOW_TOUCHES];
+  stats.n_flow_head_orders = st.ctr[C_FLOW_HEAD_ORDERS];
+  stats.n_flow_head_touches = st.ctr[C_FLOW_HEAD_TOUCHES];
   stats.n_hot = st.nhot;
   stats.n_hot_orders = st.ctr[C_HOT_ORDERS];
   stats.n_hot_fills = st.ctr[C_HOT_FILLS];

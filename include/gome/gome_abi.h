@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define GOME_ABI_VERSION 2u
+#define GOME_ABI_VERSION 3u
 
 /* ---- status codes (replace the reference's swallowed errors / panics,
  *      rabbitmq.go:44-49,70-72,120-122; nodelink.go:132,142,157) ---------- */
@@ -151,8 +151,11 @@ typedef struct gome_stats {
   uint64_t n_hot_rests, n_hot_cancels;        /* numerator of the hot kernel)             */
   uint64_t n_flow_books;                      /* hot books applied by the flow path       */
   uint64_t n_flow_orders, n_flow_touches;     /* their orders / level touches (plan log)  */
-  double ms_flow_plan;                        /* device time of k_flow_plan (the serial
-                                                 plan of the flow books)                  */
+  double ms_flow_plan;                        /* device time of k_flow_plan_head (the
+                                                 serial plan of the longest flow books,
+                                                 the batch's critical path)               */
+  uint64_t n_flow_head_orders;                /* orders / touches of the books that        */
+  uint64_t n_flow_head_touches;               /* k_flow_plan_head planned (ABI >= 3)      */
 } gome_stats;
 
 typedef struct gome_engine gome_engine;

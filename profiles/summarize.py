@@ -1,10 +1,10 @@
 """Summarise a rocprofv3 run of bench.py (profiles/run_rocprof.sh) into profiles/<tag>.md
 and update profiles/traffic.json (PMC HBM bytes per launch of the roofline kernel,
-k_flow_plan: the serial aggregate plan of the flow books, the batch's critical path).
+k_flow_plan_head: the serial aggregate plan of the longest flow books, the batch's critical path).
 
 gfx950 corrections (MI355X_MICROARCH.md §HBM, cdna_hip_programming.md §7): FETCH_SIZE and
 WRITE_SIZE are in KiB; FETCH_SIZE reads half the bytes of wide (16 B/lane) coalesced
-streams.  k_flow_plan reads its records through the scalar cache (s_load_dwordx8) and
+streams.  k_flow_plan_head reads its records through the scalar cache (s_load_dwordx8) and
 writes its touch log with per-lane dword stores, neither a calibrated width, so both the
 raw and the x2 figure are reported and the raw one is used as the traffic estimate."""
 import csv
@@ -18,7 +18,7 @@ def rows(path):
         return list(csv.DictReader(f))
 
 
-KERNEL = "k_flow_plan"
+KERNEL = "k_flow_plan_head"
 
 
 def main(tag, src):
@@ -50,7 +50,7 @@ def main(tag, src):
         out += [f"FETCH_SIZE per {KERNEL} launch: {fetch_kib:.0f} KiB = {fb/1e6:.1f} MB (x2 wide-stream correction: {2*fb/1e6:.1f} MB)",
                 f"WRITE_SIZE per {KERNEL} launch: {write_kib:.0f} KiB = {wb/1e6:.1f} MB",
                 f"traffic estimate (FETCH+WRITE): {(fb+wb)/1e6:.1f} MB per launch"]
-        json.dump({"tag": tag, "kernel": KERNEL, "k_flow_plan_hbm_bytes_per_launch": int(fb + wb),
+        json.dump({"tag": tag, "kernel": KERNEL, "k_flow_plan_head_hbm_bytes_per_launch": int(fb + wb),
                    "fetch_bytes": int(fb), "write_bytes": int(wb),
                    "note": "rocprofv3 PMC, separate passes, KiB->bytes; FETCH_SIZE not x2-corrected"},
                   open(os.path.join(os.path.dirname(__file__), "traffic.json"), "w"), indent=1)

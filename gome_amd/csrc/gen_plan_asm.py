@@ -13,9 +13,10 @@ SGPR whatever the distance to the consumer.  Branches are the dominant cost, so:
     tops' lanes included).  A rest is then ONE branchless sequence whatever the level is
     (deep / at the top / a new top that evicts the cached one into its lane): selects decide
     the lane, the amount and the cached depth, and an exec-masked VALU add applies it;
-  * membership S:SALE / S:BUY are 128-bit SGPR masks with sentinel levels 0 (bid) and 127
-    (ask), so the next level of a sweep is one bit scan; a promoted level's lane is read and
-    zeroed;
+  * bids and asks have lane registers of their own, so side-set membership (S:BUY / S:SALE)
+    is "the lane is not 0": rests maintain no mask, and the next level of a sweep is two VALU
+    compares and a bit scan (sentinel levels 0 (bid) and 127 (ask) are nonzero lanes); a
+    promoted level's lane is read and zeroed;
   * every path ends with the next order's side dispatch (decode, one conditional branch) instead
     of a jump to a common head, and the most frequent path falls through into the next slot;
   * orders stream through the scalar cache in half-groups of 4 (s_load_dwordx8), the next one in
@@ -108,31 +109,38 @@ class Gen:
             self.e(f"s_cmp_eq_u32 {t[0]}, 0")
 
     # ---- lane registers -------------------------------------------------------------
-    def promote(self, k: str, d):
-        """d = depth of level k from the lane registers, and the lane is zeroed (level k
+    @staticmethod
+    def ln(sd: str, which: str) -> str:
+        """Lane register of side sd ("A": asks, "B": bids): l0 / l1 = low words of sets 0 / 1,
+        h0 / h1 = high words (W64)."""
+        return f"%[{sd.lower()}{which}]"
+
+    def promote(self, k: str, d, sd: str):
+        """d = depth of level k from side sd's lane registers, and the lane is zeroed (level k
         becomes a cached top).  Sentinel lanes may hold garbage; their depth is never used."""
         e = self.e
+        ln = self.ln
         e(f"s_and_b32 {T0}, {k}, 63")
-        e(f"v_readlane_b32 {O[0]}, %[dl0], {T0}")
-        e(f"v_readlane_b32 {O[2]}, %[dl1], {T0}")
+        e(f"v_readlane_b32 {O[0]}, {ln(sd, 'l0')}, {T0}")
+        e(f"v_readlane_b32 {O[2]}, {ln(sd, 'l1')}, {T0}")
         if self.w == 64:
-            e(f"v_readlane_b32 {O[1]}, %[dh0], {T0}")
-            e(f"v_readlane_b32 {O[3]}, %[dh1], {T0}")
+            e(f"v_readlane_b32 {O[1]}, {ln(sd, 'h0')}, {T0}")
+            e(f"v_readlane_b32 {O[3]}, {ln(sd, 'h1')}, {T0}")
         e(f"s_cmp_lt_u32 {k}, 64")
         e(f"s_cselect_b32 {d[0]}, {O[0]}, {O[2]}")
         if self.w == 64:
             e(f"s_cselect_b32 {d[1]}, {O[1]}, {O[3]}")
         e(f"s_bfm_b64 {M}, 1, {k}")
         e(f"s_cselect_b64 exec, {M}, 0")
-        e("v_mov_b32 %[dl0], 0")
+        e(f"v_mov_b32 {ln(sd, 'l0')}, 0")
         if self.w == 64:
-            e("v_mov_b32 %[dh0], 0")
+            e(f"v_mov_b32 {ln(sd, 'h0')}, 0")
         e(f"s_cselect_b64 exec, 0, {M}")
-        e("v_mov_b32 %[dl1], 0")
+        e(f"v_mov_b32 {ln(sd, 'l1')}, 0")
         if self.w == 64:
-            e("v_mov_b32 %[dh1], 0")
+            e(f"v_mov_b32 {ln(sd, 'h1')}, 0")
 
-    def write(self, k: str, v):
+    def write(self, k: str, v, sd: str):
         """Level k := v (end of the loop: the cached tops go back to their lanes).  The other
         set's lane written is a sentinel lane (level 0: set 0 lane 0, level 127: set 1 lane
         63), whose value is never used."""
@@ -143,16 +151,17 @@ class Gen:
         e(f"s_cselect_b32 {O[0]}, {T0}, 0")
         e(f"s_cselect_b32 {O[1]}, 63, {T0}")
         e(f"s_mov_b32 m0, {O[0]}")
-        e(f"v_writelane_b32 %[dl0], {v[0]}, m0")
+        ln = self.ln
+        e(f"v_writelane_b32 {ln(sd, 'l0')}, {v[0]}, m0")
         if self.w == 64:
-            e(f"v_writelane_b32 %[dh0], {v[1]}, m0")
+            e(f"v_writelane_b32 {ln(sd, 'h0')}, {v[1]}, m0")
         e(f"s_mov_b32 m0, {O[1]}")
-        e(f"v_writelane_b32 %[dl1], {v[0]}, m0")
+        e(f"v_writelane_b32 {ln(sd, 'l1')}, {v[0]}, m0")
         if self.w == 64:
-            e(f"v_writelane_b32 %[dh1], {v[1]}, m0")
+            e(f"v_writelane_b32 {ln(sd, 'h1')}, {v[1]}, m0")
         e(f"s_mov_b32 m0, {SAVE}")
 
-    def add_lane(self):
+    def add_lane(self, sd: str):
         """Level L += A in the lane registers: the amount goes to the set of L, the other set's
         lane L % 64 gets 0.  exec is left narrowed (only lane-select ops follow)."""
         e = self.e
@@ -160,44 +169,51 @@ class Gen:
         self.csel(A1, 0, A)
         self.csel(A, A, 0)
         e(f"s_bfm_b64 exec, 1, {L}")
+        ln = self.ln
+        l0, l1, h0, h1 = ln(sd, "l0"), ln(sd, "l1"), ln(sd, "h0"), ln(sd, "h1")
         if self.w == 64:
             e(f"v_mov_b32 %[vt], {A[1]}")
-            e(f"v_add_co_u32_e32 %[dl0], vcc, {A[0]}, %[dl0]")
-            e("v_addc_co_u32_e32 %[dh0], vcc, %[vt], %[dh0], vcc")
+            e(f"v_add_co_u32_e32 {l0}, vcc, {A[0]}, {l0}")
+            e(f"v_addc_co_u32_e32 {h0}, vcc, %[vt], {h0}, vcc")
             e(f"v_mov_b32 %[vt], {A1[1]}")
-            e(f"v_add_co_u32_e32 %[dl1], vcc, {A1[0]}, %[dl1]")
-            e("v_addc_co_u32_e32 %[dh1], vcc, %[vt], %[dh1], vcc")
+            e(f"v_add_co_u32_e32 {l1}, vcc, {A1[0]}, {l1}")
+            e(f"v_addc_co_u32_e32 {h1}, vcc, %[vt], {h1}, vcc")
         else:
-            e(f"v_add_u32_e32 %[dl0], {A[0]}, %[dl0]")
-            e(f"v_add_u32_e32 %[dl1], {A1[0]}, %[dl1]")
+            e(f"v_add_u32_e32 {l0}, {A[0]}, {l0}")
+            e(f"v_add_u32_e32 {l1}, {A1[0]}, {l1}")
 
     # ---- scalar state ---------------------------------------------------------------
-    def setbit(self, mask: str, k: str, op: str):
-        """op = s_bitset1_b64 / s_bitset0_b64 on bit k of the 128-bit mask A or B (neither the
-        bit op nor the selects write SCC)."""
+    def members(self, sd: str):
+        """M = lanes of set 0 of side sd holding a resting level (depth != 0), s[90:91] = set 1.
+        (A VALU compare writes 0 for inactive lanes: exec is widened first.)"""
         e = self.e
-        m0, m1 = f"%[{mask}0]", f"%[{mask}1]"
-        e(f"s_cmp_lt_u32 {k}, 64")
-        e(f"s_cselect_b64 {M}, {m0}, {m1}")
-        e(f"{op} {M}, {k}")
-        e(f"s_cselect_b64 {m0}, {M}, {m0}")
-        e(f"s_cselect_b64 {m1}, {m1}, {M}")
+        ln = self.ln
+        e("s_mov_b64 exec, -1")
+        for st, dst in (("0", M), ("1", "s[90:91]")):
+            if self.w == 64:
+                e(f"v_or_b32 %[vt], {ln(sd, 'l' + st)}, {ln(sd, 'h' + st)}")
+                e(f"v_cmp_ne_u32_e64 {dst}, 0, %[vt]")
+            else:
+                e(f"v_cmp_ne_u32_e64 {dst}, 0, {ln(sd, 'l' + st)}")
 
     def lowest_ask(self):
-        """BA = lowest bit of A (ff1 gives -1 = UINT_MAX on an empty word; A1 holds the
-        sentinel bit 127)."""
+        """BA = lowest resting ask level (ff1 gives -1 = UINT_MAX on an empty word; the ask
+        sentinel 127 is a nonzero lane)."""
         e = self.e
-        e(f"s_ff1_i32_b64 {BA}, %[A0]")
-        e(f"s_ff1_i32_b64 {T0}, %[A1]")
+        self.members("A")
+        e(f"s_ff1_i32_b64 {BA}, {M}")
+        e(f"s_ff1_i32_b64 {T0}, s[90:91]")
         e(f"s_add_u32 {T0}, {T0}, 64")
         e(f"s_min_u32 {BA}, {BA}, {T0}")
 
     def highest_bid(self):
-        """BB = highest bit of B (B0 holds the sentinel bit 0; an empty B1 gives 128 & 127 = 0)."""
+        """BB = highest resting bid level (the bid sentinel 0 is a nonzero lane; an empty set 1
+        gives 128 & 127 = 0)."""
         e = self.e
-        e(f"s_flbit_i32_b64 {BB}, %[B0]")
+        self.members("B")
+        e(f"s_flbit_i32_b64 {BB}, {M}")
         e(f"s_sub_u32 {BB}, 63, {BB}")
-        e(f"s_flbit_i32_b64 {T0}, %[B1]")
+        e(f"s_flbit_i32_b64 {T0}, s[90:91]")
         e(f"s_sub_u32 {T0}, 127, {T0}")
         e(f"s_and_b32 {T0}, {T0}, 127")
         e(f"s_max_u32 {BB}, {BB}, {T0}")
@@ -299,8 +315,7 @@ class Gen:
         self.csel(topd, 0, topd)
         e(f"s_{'max' if buy else 'min'}_u32 {top}, {top}, {LI}")
         self.add(topd, topd, X)
-        self.add_lane()
-        self.setbit("B" if buy else "A", LI, "s_bitset1_b64")
+        self.add_lane("B" if buy else "A")
         if self.w == 64:
             e(f"s_or_b32 {K}, {JJS}, {LI}")
             e(f"s_bitset1_b32 {K}, 7")
@@ -332,13 +347,12 @@ class Gen:
         otop, otopd = (BA, BAD) if buy else (BB, BBD)
         e(f"s_or_b32 {K}, {JJS}, {otop}")
         self.log(K, otopd, False)        # (the staging check is folded into the test below)
-        self.mov(T, D)
-        self.setbit("A" if buy else "B", otop, "s_bitset0_b64")
+        self.mov(T, D)              # (the emptied level's lane is 0: it leaves the side)
         if buy:
             self.lowest_ask()
         else:
             self.highest_bid()
-        self.promote(otop, otopd)
+        self.promote(otop, otopd, "A" if buy else "B")
         # one branch for the common case "T > 0, room in the staging, the next level crosses
         # too": T == 0 or a full staging make the limit a level that cannot cross
         never = "0" if buy else "127"
@@ -446,9 +460,9 @@ class Gen:
         e(f"s_mov_b32 {JJS}, 0xffffff00")          # (-1) << 8: the first record is order 0
         e("s_mov_b32 m0, %[nacc]")
         self.lowest_ask()
-        self.promote(BA, BAD)
+        self.promote(BA, BAD, "A")
         self.highest_bid()
-        self.promote(BB, BBD)
+        self.promote(BB, BBD, "B")
         e(f"s_load_dwordx8 s[60:67], {ADDR}, 0x0")
         for i in range(8):
             if i % 4 == 0:
@@ -462,8 +476,8 @@ class Gen:
         e(f"{done}:")
         e("s_waitcnt lgkmcnt(0)")
         e("s_mov_b64 exec, -1")
-        self.write(BA, BAD)
-        self.write(BB, BBD)
+        self.write(BA, BAD, "A")
+        self.write(BB, BBD, "B")
         e("s_mov_b32 %[nacc], m0")
         return self.out
 

@@ -794,15 +794,17 @@ __device__ __forceinline__ void fl_plan_book(const Dev& D, const FlowArgs& F, ui
   const bool w32 = uni(hd->w32) != 0;
   const unsigned long long g = static_cast<unsigned long long>(uni64(static_cast<int64_t>(hd->g)));
   const uint32_t m0 = v0 ? LV[lane].mem0 : 0u, m1 = v1 ? LV[lane + 64].mem0 : 0u;
-  // the loop's invariant: lanes of levels outside both side sets hold 0
-  int64_t d0 = (m0 & (M_SALE | M_BUY)) ? LV[lane].d0 : 0, d1 = (m1 & (M_SALE | M_BUY)) ? LV[lane + 64].d0 : 0;
+  // Bids and asks have lane registers of their own, and the loop's invariant is that a lane
+  // holds 0 unless its level rests on that side (membership = nonzero lane).  The sentinel
+  // levels 0 (bid) and 127 (ask) are nonzero lanes.
+  int64_t d0 = v0 ? LV[lane].d0 : 0, d1 = v1 ? LV[lane + 64].d0 : 0;
   if (w32) {  // depths in units of g (exact: g divides every volume and depth of the book)
     d0 = static_cast<int64_t>(static_cast<unsigned long long>(d0) / g);
     d1 = static_cast<int64_t>(static_cast<unsigned long long>(d1) / g);
   }
-  FlDepth Dp{lo32(d0), hi32(d0), lo32(d1), hi32(d1)};
-  unsigned long long A0 = __ballot(m0 & M_SALE), A1 = __ballot(m1 & M_SALE) | (1ull << 63);
-  unsigned long long B0 = __ballot(m0 & M_BUY) | 1ull, B1 = __ballot(m1 & M_BUY);
+  const int64_t a0 = (m0 & M_SALE) ? d0 : 0, a1 = (m1 & M_SALE) ? d1 : (lane == 63 ? 1 : 0);
+  const int64_t b0 = (m0 & M_BUY) ? d0 : (lane == 0 ? 1 : 0), b1 = (m1 & M_BUY) ? d1 : 0;
+  FlDepth Da{lo32(a0), hi32(a0), lo32(a1), hi32(a1)}, Db{lo32(b0), hi32(b0), lo32(b1), hi32(b1)};
 
   FlLog lg{vreg(0u), vreg(0u), vreg(0u), 0u, 0u, 0u, FL_TOUCH_MUL * n, (GOME_GLB v4u*)(F.log + FL_TOUCH_MUL * beg)};
   // records are read in half-groups of 4 (the book's stream is padded to whole groups)
@@ -812,8 +814,9 @@ __device__ __forceinline__ void fl_plan_book(const Dev& D, const FlowArgs& F, ui
   const uint32_t vl16 = lane * 16u;
   uint32_t voff, vt;
 #define FL_PLAN_OPERANDS                                                                          \
-  : [A0] "+s"(A0), [A1] "+s"(A1), [B0] "+s"(B0), [B1] "+s"(B1), [dl0] "+v"(Dp.l0), [dh0] "+v"(Dp.h0),   \
-    [dl1] "+v"(Dp.l1), [dh1] "+v"(Dp.h1), [lk] "+v"(lg.lk), [la] "+v"(lg.la), [lb] "+v"(lg.lb),         \
+  : [al0] "+v"(Da.l0), [ah0] "+v"(Da.h0), [al1] "+v"(Da.l1), [ah1] "+v"(Da.h1), [bl0] "+v"(Db.l0),     \
+    [bh0] "+v"(Db.h0), [bl1] "+v"(Db.l1), [bh1] "+v"(Db.h1), [lk] "+v"(lg.lk), [la] "+v"(lg.la),         \
+    [lb] "+v"(lg.lb),                                                                                 \
     [nacc] "+s"(lg.nacc), [lpos] "+s"(lg.lpos), [voff] "=&v"(voff), [vt] "=&v"(vt)                      \
   : [ob] "s"(ob), [nh] "s"(nh), [logp] "s"(logp), [lcap] "s"(lg.lcap), [vl16] "v"(vl16)                \
   : FL_PLAN_CLOBBERS, "scc", "vcc", "memory"
@@ -840,12 +843,17 @@ __device__ __forceinline__ void fl_plan_book(const Dev& D, const FlowArgs& F, ui
     if (lane == 0) atomicOr(&D.st->err, ERR_CORRUPT);
     lg.lpos = 0;
   }
-  // the loop keeps non-member lanes at 0; masking by membership also drops the sentinel lanes
-  const bool in0 = (((A0 | B0) >> lane) & 1ull) != 0, in1 = (((A1 | B1) >> lane) & 1ull) != 0;
-  const uint64_t u0 = w32 ? static_cast<uint64_t>(Dp.l0) * g : (static_cast<uint64_t>(Dp.h0) << 32) | Dp.l0;
-  const uint64_t u1 = w32 ? static_cast<uint64_t>(Dp.l1) * g : (static_cast<uint64_t>(Dp.h1) << 32) | Dp.l1;
-  const int64_t f0 = in0 ? static_cast<int64_t>(u0) : 0;
-  const int64_t f1 = in1 ? static_cast<int64_t>(u1) : 0;
+  // side sets from the nonzero lanes (the sentinel bits 127 / 0 are set, as the write kernels
+  // expect); a level rests on at most one side, so its final depth is the sum of its lanes
+  auto u64of = [&](uint32_t lo, uint32_t hi) -> uint64_t {
+    return w32 ? static_cast<uint64_t>(lo) * g : (static_cast<uint64_t>(hi) << 32) | lo;
+  };
+  const uint64_t ua0 = u64of(Da.l0, Da.h0), ua1 = u64of(Da.l1, Da.h1);
+  const uint64_t ub0 = u64of(Db.l0, Db.h0), ub1 = u64of(Db.l1, Db.h1);
+  const unsigned long long A0 = __ballot(ua0 != 0) & ~1ull, A1 = __ballot(ua1 != 0) | (1ull << 63);
+  const unsigned long long B0 = __ballot(ub0 != 0) | 1ull, B1 = __ballot(ub1 != 0) & ~(1ull << 63);
+  const int64_t f0 = lane == 0 ? 0 : static_cast<int64_t>(ua0 + ub0);
+  const int64_t f1 = lane == 63 ? 0 : static_cast<int64_t>(ua1 + ub1);
   if (v0) LV[lane].dfin = f0;
   if (v1) LV[lane + 64].dfin = f1;
   if (lane == 0) {

@@ -19,7 +19,7 @@ SGPR whatever the distance to the consumer.  Branches are the dominant cost, so:
     promoted level's lane is read and zeroed;
   * every path ends with the next order's side dispatch (decode, one conditional branch) instead
     of a jump to a common head, and the most frequent path falls through into the next slot;
-  * orders stream through the scalar cache in half-groups of 4 (s_load_dwordx8), the next one in
+  * orders stream through the scalar cache in half-groups of 8 (s_load_dwordx16), the next one in
     flight while the current one is applied; the record registers become T in place;
   * touches are staged in lane registers (lane = M0, the staging count) and stored 64 at a
     time from inside the loop.
@@ -37,7 +37,9 @@ from __future__ import annotations
 import os
 
 # fixed registers (declared as clobbers of the asm statement)
-BUF = [(60, 61), (62, 63), (64, 65), (66, 67), (68, 69), (70, 71), (72, 73), (74, 75)]
+HG = 8                           # records per half-group (one s_load_dwordx16)
+NS = 2 * HG                      # order slots: two half-groups, double-buffered
+BUF = [(44 + 2 * i, 45 + 2 * i) for i in range(HG)] + [(60 + 2 * i, 61 + 2 * i) for i in range(HG)]
 BA, BB = "s76", "s77"            # best ask / best bid level
 BAD, BBD = ("s78", "s79"), ("s80", "s81")  # their depths (authoritative; their lanes hold 0)
 L = "s82"                        # lane target of a rest
@@ -50,7 +52,7 @@ X = D
 HC = "s97"                       # half-groups left + 1
 ADDR = "s[98:99]"                # SMEM address of the next half-group
 SAVE = "s100"                    # M0 (staging count) saved around lane writes
-CLOBBERS = [f"s{i}" for i in range(60, 101)]
+CLOBBERS = [f"s{i}" for i in range(44, 101)]
 COPY_REST = os.environ.get("GOME_PLAN_COPY", "0") == "1"   # measured: no gain, 1.35x code
 
 
@@ -264,7 +266,7 @@ class Gen:
         most frequent transition that cannot fall through) runs from a private copy of the
         rest body here instead of jumping to BR_j."""
         e = self.e
-        if j % 4 == 0:
+        if j % HG == 0:
             if not fall:
                 e(f"s_branch {self.lab(f'H{j}')}")
             return
@@ -277,7 +279,7 @@ class Gen:
             e(f"s_cbranch_scc1 {self.lab(f'BXE{j}')}")
             if copy:
                 self.rest("B", (f"s{BUF[j][0]}", f"s{BUF[j][1]}"))
-                self.dispatch((j + 1) % 8, False, False)
+                self.dispatch((j + 1) % NS, False, False)
             else:
                 e(f"s_branch {self.lab(f'BR{j}')}")
 
@@ -360,13 +362,13 @@ class Gen:
         slow, cont = self.lab(f"{side}SL{i}"), self.lab(f"{side}CN{i}")
         self.is_zero_scc(T)
         e(f"s_cselect_b32 {T0}, {never}, {LI}")
-        e("s_cmp_ge_u32 m0, 60")
+        e(f"s_cmp_ge_u32 m0, {64 - HG}")          # (room for the half's HG final touches)
         e(f"s_cselect_b32 {T0}, {never}, {T0}")
         e(f"s_cmp_{cmp}_u32 {otop}, {T0}")
         e(f"s_cbranch_scc0 {slow}")
         fl = self.fresh("FL")
         self.flushes.append((fl, slow))
-        blk = [f"{slow}:", "s_cmp_ge_u32 m0, 60", f"s_cbranch_scc1 {fl}"]
+        blk = [f"{slow}:", f"s_cmp_ge_u32 m0, {64 - HG}", f"s_cbranch_scc1 {fl}"]
         blk += ([f"s_cmp_eq_u64 {self.pair(T)}, 0"] if self.w == 64 else [f"s_cmp_eq_u32 {T[0]}, 0"])
         blk += [f"s_cbranch_scc1 {self.lab(f'DN{i}')}",     # diff == 0: stop (engine.go:162-175)
                 f"s_cmp_{cmp}_u32 {otop}, {LI}", f"s_cbranch_scc1 {cont}",
@@ -376,7 +378,7 @@ class Gen:
         self.sub(D, T, otopd)                                 # the next level, inline
         e(f"s_cbranch_scc0 {self.lab(f'{side}F{i}')}")
         self.partial(side, T)
-        self.dispatch((i + 1) % 8, False)
+        self.dispatch((i + 1) % NS, False)
 
     def slot(self, i: int):
         """Order slot i (record BUF[i]); its side was decoded by the previous path.  Layout:
@@ -385,7 +387,7 @@ class Gen:
         e = self.e
         lo, hi = f"s{BUF[i][0]}", f"s{BUF[i][1]}"
         T = (lo, hi)          # 32-bit: T is lo; hi keeps the flags
-        j = (i + 1) % 8
+        j = (i + 1) % NS
         lab = self.lab
         # --- BUY
         e(f"{lab(f'B{i}')}:")
@@ -429,25 +431,25 @@ class Gen:
         """Half-group head before slot j: count the half done, wait for this half's records,
         prefetch the next half, make room for its touches, dispatch slot j."""
         e = self.e
-        other = 68 - 8 * (j // 4)
+        other = 60 if j == 0 else 44
         fl, back = self.fresh("HF"), self.fresh("HB")
         hi = f"s{BUF[j][1]}"
-        # one branch for "the book is done or the staging needs room for this half's 4 last
+        # one branch for "the book is done or the staging needs room for this half's HG last
         # touches"; the out-of-line block tells them apart
         e(f"{self.lab(f'H{j}')}:")
         e(f"s_sub_u32 {HC}, {HC}, 1")
         e(f"s_cmp_eq_u32 {HC}, 0")
         e(f"s_cselect_b32 {T0}, 99, m0")
-        e(f"s_cmp_ge_u32 {T0}, 60")
+        e(f"s_cmp_ge_u32 {T0}, {64 - HG}")
         hs = self.fresh("HS")
         e(f"s_cbranch_scc1 {hs}")
         e(f"{back}:")
         self.slow.append([f"{hs}:", f"s_cmp_eq_u32 {HC}, 0", f"s_cbranch_scc1 {self.lab('DONE')}", f"s_branch {fl}"])
         self.flushes.append((fl, back))
         e("s_waitcnt lgkmcnt(0)")
-        e("s_add_u32 s98, s98, 32")
+        e(f"s_add_u32 s98, s98, {8 * HG}")
         e("s_addc_u32 s99, s99, 0")
-        e(f"s_load_dwordx8 s[{other}:{other + 7}], {ADDR}, 0x0")   # prefetch the next half
+        e(f"s_load_dwordx16 s[{other}:{other + 15}], {ADDR}, 0x0")   # prefetch the next half
         self.decode(j)
         e(f"s_cbranch_scc1 {self.lab(f'S{j}')}")
 
@@ -463,9 +465,9 @@ class Gen:
         self.promote(BA, BAD, "A")
         self.highest_bid()
         self.promote(BB, BBD, "B")
-        e(f"s_load_dwordx8 s[60:67], {ADDR}, 0x0")
-        for i in range(8):
-            if i % 4 == 0:
+        e(f"s_load_dwordx16 s[44:59], {ADDR}, 0x0")
+        for i in range(NS):
+            if i % HG == 0:
                 self.head(i)
             self.slot(i)
         for blk in self.slow:

@@ -58,16 +58,17 @@ constexpr uint32_t FL_HEAD = 8;           // longest candidates on the critical-
 constexpr uint32_t FL_TOUCH_MUL = 5;      // log capacity per order (touches <= 3n + L0, plus
                                           // 64 entries of staging slack, n >= 128)
 constexpr unsigned long long FL_KEY_OFF = 1ull << 62;
-// Packed records of book `seg` start at the 4-aligned index at or above beg + 8 * seg and are
-// followed by SKIP records up to a multiple of 4: every book's stream is whole half-groups.
-__host__ __device__ constexpr uint32_t fl_obase(uint32_t beg, uint32_t seg) { return (beg + 8u * seg + 3u) & ~3u; }
+// Packed records of book `seg` start at the 8-aligned index at or above beg + 8 * seg and are
+// followed by no-op records up to a multiple of 8: every book's stream is whole half-groups
+// (ceil8(x) + ceil8(n) <= ceil8(x + n + 8): books never overlap).
+__host__ __device__ constexpr uint32_t fl_obase(uint32_t beg, uint32_t seg) { return (beg + 8u * seg + 7u) & ~7u; }
 constexpr uint32_t FL_ORD8_MUL = 9, FL_ORD8_PAD = 64;  // ord8 capacity: 9 * max_batch + 64
 
 // packed order record of the plan (8 B): volume [0,53), level [53,60), SALE bit 60.  A record
 // that must not touch the book (dropped ADD, ignored action, padding) is 0: a zero-volume BUY
 // rest at sentinel level 0, which changes nothing and whose touch no later kernel reads.
 constexpr uint32_t OR_LI_SHIFT = 21, OR_SELL = 1u << 28;
-constexpr uint32_t FL_MAX_ORDERS = (1u << 23) - 4;  // order index (padding included) fits [8, 31) of a touch key
+constexpr uint32_t FL_MAX_ORDERS = (1u << 23) - 8;  // order index (padding included) fits [8, 31) of a touch key
 constexpr unsigned long long OR_NOP = 0ull;
 
 enum : uint32_t { TK_CONS = 0, TK_REST = 1 };
@@ -347,7 +348,7 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep(Dev D, BatchArgs B, Flo
   if (g == 0) g = 1;
   const bool w32 = sum < FL_SUM_CAP && sum / g < (1ull << 32);
   if (!w32) g = 1;
-  if (tid < ((4u - ((end - beg) & 3u)) & 3u))  // padding to whole half-groups
+  if (tid < ((8u - ((end - beg) & 7u)) & 7u))  // padding to whole half-groups (8 records)
     F.ord8[obase + (end - beg) + tid] = fl_rec(false, 0, 0, false, end - beg + tid, w32);
   for (uint32_t b0 = beg + tid; b0 < end; b0 += 4 * FL_PREP_T) {
     Prep qs[4];
@@ -615,7 +616,7 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep_b(Dev D, BatchArgs B, F
   const bool w32 = msum < FL_SUM_CAP && msum / g < (1ull << 32);
   if (!w32) g = 1;
   const uint32_t obase = fl_obase(beg, seg);
-  if (tid < ((4u - ((end - beg) & 3u)) & 3u))  // padding to whole half-groups
+  if (tid < ((8u - ((end - beg) & 7u)) & 7u))  // padding to whole half-groups (8 records)
     F.ord8[obase + (end - beg) + tid] = fl_rec(false, 0, 0, false, end - beg + tid, w32);
   if (tid == 0) {
     FlowHdr x{};
@@ -807,8 +808,8 @@ __device__ __forceinline__ void fl_plan_book(const Dev& D, const FlowArgs& F, ui
   FlDepth Da{lo32(a0), hi32(a0), lo32(a1), hi32(a1)}, Db{lo32(b0), hi32(b0), lo32(b1), hi32(b1)};
 
   FlLog lg{vreg(0u), vreg(0u), vreg(0u), 0u, 0u, 0u, FL_TOUCH_MUL * n, (GOME_GLB v4u*)(F.log + FL_TOUCH_MUL * beg)};
-  // records are read in half-groups of 4 (the book's stream is padded to whole groups)
-  const uint32_t nh = (n + 3) / 4;
+  // records are read in half-groups of 8 (the book's stream is padded to whole groups)
+  const uint32_t nh = (n + 7) / 8;
   const unsigned long long ob = reinterpret_cast<unsigned long long>(F.ord8 + uni(hd->obase));
   const unsigned long long logp = reinterpret_cast<unsigned long long>(F.log + FL_TOUCH_MUL * beg);
   const uint32_t vl16 = lane * 16u;

@@ -54,6 +54,8 @@ ADDR = "s[98:99]"                # SMEM address of the next half-group
 SAVE = "s100"                    # M0 (staging count) saved around lane writes
 CLOBBERS = [f"s{i}" for i in range(44, 101)]
 COPY_REST = os.environ.get("GOME_PLAN_COPY", "0") == "1"   # measured: no gain, 1.35x code
+PF_DIST = int(os.environ.get("GOME_PLAN_PF", "0"))  # L2 prefetch distance in bytes (0: off);
+# k_flow_prep pads ord8 by FL_ORD8_PAD records, which must cover it
 
 
 class Gen:
@@ -450,6 +452,9 @@ class Gen:
         e(f"s_add_u32 s98, s98, {8 * HG}")
         e("s_addc_u32 s99, s99, 0")
         e(f"s_load_dwordx16 s[{other}:{other + 15}], {ADDR}, 0x0")   # prefetch the next half
+        if PF_DIST:  # warm L2 further ahead with a vector load (never waited for in the loop)
+            e("s_mov_b64 exec, 1")
+            e(f"global_load_dword %[vpf], %[vzero], {ADDR} offset:{PF_DIST}")
         self.decode(j)
         e(f"s_cbranch_scc1 {self.lab(f'S{j}')}")
 
@@ -466,6 +471,10 @@ class Gen:
         self.highest_bid()
         self.promote(BB, BBD, "B")
         e(f"s_load_dwordx16 s[44:59], {ADDR}, 0x0")
+        if PF_DIST:
+            e("s_mov_b64 exec, 1")
+            for off in range(64, PF_DIST, 64):
+                e(f"global_load_dword %[vpf], %[vzero], {ADDR} offset:{off}")
         for i in range(NS):
             if i % HG == 0:
                 self.head(i)
@@ -476,7 +485,7 @@ class Gen:
         for fl, back in self.flushes:
             self.emit_flush(fl, back)
         e(f"{done}:")
-        e("s_waitcnt lgkmcnt(0)")
+        e("s_waitcnt vmcnt(0) lgkmcnt(0)")      # (vpf is an asm output: no load may land later)
         e("s_mov_b64 exec, -1")
         self.write(BA, BAD, "A")
         self.write(BB, BBD, "B")

@@ -62,7 +62,7 @@ constexpr unsigned long long FL_KEY_OFF = 1ull << 62;
 // followed by no-op records up to a multiple of 8: every book's stream is whole half-groups
 // (ceil8(x) + ceil8(n) <= ceil8(x + n + 8): books never overlap).
 __host__ __device__ constexpr uint32_t fl_obase(uint32_t beg, uint32_t seg) { return (beg + 8u * seg + 7u) & ~7u; }
-constexpr uint32_t FL_ORD8_MUL = 9, FL_ORD8_PAD = 64;  // ord8 capacity: 9 * max_batch + 64
+constexpr uint32_t FL_ORD8_MUL = 9, FL_ORD8_PAD = 512;  // ord8 capacity: 9 * max_batch + 512 (>= the plan loop's L2 prefetch distance + 2 half-groups)
 
 // packed order record of the plan (8 B): volume [0,53), level [53,60), SALE bit 60.  A record
 // that must not touch the book (dropped ADD, ignored action, padding) is 0: a zero-volume BUY
@@ -813,13 +813,15 @@ __device__ __forceinline__ void fl_plan_book(const Dev& D, const FlowArgs& F, ui
   const unsigned long long ob = reinterpret_cast<unsigned long long>(F.ord8 + uni(hd->obase));
   const unsigned long long logp = reinterpret_cast<unsigned long long>(F.log + FL_TOUCH_MUL * beg);
   const uint32_t vl16 = lane * 16u;
-  uint32_t voff, vt;
+  uint32_t voff, vt, vpf;
+  const uint32_t vzero = 0;
 #define FL_PLAN_OPERANDS                                                                          \
   : [al0] "+v"(Da.l0), [ah0] "+v"(Da.h0), [al1] "+v"(Da.l1), [ah1] "+v"(Da.h1), [bl0] "+v"(Db.l0),     \
     [bh0] "+v"(Db.h0), [bl1] "+v"(Db.l1), [bh1] "+v"(Db.h1), [lk] "+v"(lg.lk), [la] "+v"(lg.la),         \
     [lb] "+v"(lg.lb),                                                                                 \
-    [nacc] "+s"(lg.nacc), [lpos] "+s"(lg.lpos), [voff] "=&v"(voff), [vt] "=&v"(vt)                      \
-  : [ob] "s"(ob), [nh] "s"(nh), [logp] "s"(logp), [lcap] "s"(lg.lcap), [vl16] "v"(vl16)                \
+    [nacc] "+s"(lg.nacc), [lpos] "+s"(lg.lpos), [voff] "=&v"(voff), [vt] "=&v"(vt), [vpf] "=&v"(vpf)    \
+  : [ob] "s"(ob), [nh] "s"(nh), [logp] "s"(logp), [lcap] "s"(lg.lcap), [vl16] "v"(vl16),              \
+    [vzero] "v"(vzero)                                                                                  \
   : FL_PLAN_CLOBBERS, "scc", "vcc", "memory"
 #ifdef GOME_STAMPS
   const unsigned long long sc0 = __builtin_amdgcn_s_memtime(), sr0 = __builtin_amdgcn_s_memrealtime();

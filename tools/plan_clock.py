@@ -16,7 +16,7 @@ import torch  # noqa: E402
 torch.zeros(1, device="cuda")  # the HIP runtime is initialised by torch first, as in bench.py
 from gome_amd import abi  # noqa: E402
 
-lib = abi.load_library(os.path.join(ROOT, "gome_amd", "libgome_stamps.so"))
+lib = abi.load_library(os.path.join(ROOT, "gome_amd", os.environ.get("GOME_STAMPS_LIB", "libgome_stamps.so")))
 lib.gome_debug_stamps.argtypes = [C.c_void_p, C.c_size_t]
 import bench  # noqa: E402
 

@@ -82,7 +82,7 @@ struct gome_engine {
   hipStream_t flow_stream = nullptr, flow2_stream = nullptr;
   bool own_stream = false;
   hipEvent_t fork{}, join{}, evh0{}, evh1{};
-  hipEvent_t joinf{}, joinf2{}, prep_h{}, prep_t{}, evf0{}, evf1{};
+  hipEvent_t joinf{}, joinf2{}, prep_h{}, prep_t{}, evf0{}, evf1{}, fork_adm{}, adm_done{}, evs{}, evt_done{};
   FlowArgs F{};
   Prep* d_prep = nullptr;
   PendEnt* d_pend = nullptr;
@@ -148,6 +148,8 @@ struct gome_engine {
     if (evf0) {
       (void)hipEventDestroy(evf0); (void)hipEventDestroy(evf1); (void)hipEventDestroy(joinf);
       (void)hipEventDestroy(joinf2); (void)hipEventDestroy(prep_h); (void)hipEventDestroy(prep_t);
+      (void)hipEventDestroy(fork_adm); (void)hipEventDestroy(adm_done); (void)hipEventDestroy(evs);
+      (void)hipEventDestroy(evt_done);
     }
     if (hot_stream) (void)hipStreamDestroy(hot_stream);
     if (flow_stream) (void)hipStreamDestroy(flow_stream);
@@ -198,6 +200,10 @@ gome_status gome_engine::init(const gome_config& c) {
   HIPCHK(hipEventCreateWithFlags(&prep_t, hipEventDisableTiming));
   HIPCHK(hipEventCreate(&evf0));
   HIPCHK(hipEventCreate(&evf1));
+  HIPCHK(hipEventCreateWithFlags(&fork_adm, hipEventDisableTiming));
+  HIPCHK(hipEventCreateWithFlags(&adm_done, hipEventDisableTiming));
+  HIPCHK(hipEventCreateWithFlags(&evs, hipEventDisableTiming));
+  HIPCHK(hipEventCreateWithFlags(&evt_done, hipEventDisableTiming));
   HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_match_hot),
                              hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(HOT_LDS_BYTES)));
 
@@ -308,6 +314,14 @@ gome_status gome_engine::run(const gome_order* d_ord, uint32_t n, hipStream_t s)
   // per-batch status reset (free_top / freed_top persist)
   HIPCHK(hipMemsetAsync(d_st, 0, offsetof(Status, free_top), s));
   const uint32_t T256 = 256, gN = ceil_div(n, T256);
+  // admission markers depend on the input records only: they run on the flow stream beside
+  // the validation, the radix sort and the segmentation (the batch's critical path)
+  HIPCHK(hipEventRecord(fork_adm, s));
+  HIPCHK(hipStreamWaitEvent(flow_stream, fork_adm, 0));
+  HIPCHK(hipMemsetAsync(d_claim, 0, (adm_mask + 1ull) * 4, flow_stream));
+  HIPCHK(hipMemsetAsync(d_amin, 0xFF, (adm_mask + 1ull) * 4, flow_stream));
+  k_adm<<<gN, T256, 0, flow_stream>>>(d_ord, n, d_claim, d_amin, d_adm_slot, adm_mask);
+  HIPCHK(hipEventRecord(adm_done, flow_stream));
   k_validate<<<gN, T256, 0, s>>>(d_ord, n, cfg.max_symbols, d_st);
 
   // ---- stable radix sort of (symbol_id, seq)
@@ -346,11 +360,8 @@ gome_status gome_engine::run(const gome_order* d_ord, uint32_t n, hipStream_t s)
   k_seg_bscan<<<1, 64, 0, s>>>(d_bcnt, d_bcnt + 32, d_st, FLOW_MIN_LOG2, MAX_FLOW);
   k_seg_scatter<<<gN, T256, 0, s>>>(d_seg_start, d_st, d_bcnt + 32, d_seg_order);
 
-  // ---- admission markers
-  HIPCHK(hipMemsetAsync(d_claim, 0, (adm_mask + 1ull) * 4, s));
-  HIPCHK(hipMemsetAsync(d_amin, 0xFF, (adm_mask + 1ull) * 4, s));
-  k_adm<<<gN, T256, 0, s>>>(d_ord, n, d_claim, d_amin, d_adm_slot, adm_mask);
-
+  // ---- admission markers (k_adm, launched above on the flow stream)
+  HIPCHK(hipStreamWaitEvent(s, adm_done, 0));
   k_prep<<<gN, T256, 0, s>>>(d_ord, n, sidx, d_adm_slot, d_amin, d_prep);
 
   // ---- match_books: one wavefront per book; hot books (LDS) on a second stream,
@@ -432,9 +443,15 @@ gome_status gome_engine::run(const gome_order* d_ord, uint32_t n, hipStream_t s)
 
   // ---- event compaction into publish order
   scan(d_ev_count, n, d_ev_off, &d_st->n_events, s);
+  if (nh_tail) {  // the tail's events beside the rest (all only need the scan; disjoint slots)
+    HIPCHK(hipEventRecord(evs, s));
+    HIPCHK(hipStreamWaitEvent(hot_stream, evs, 0));
+    k_flow_events<<<1024, 256, 0, hot_stream>>>(D, B, FT, d_ev_off, d_events);
+    HIPCHK(hipEventRecord(evt_done, hot_stream));
+  }
   k_ev_scatter<<<2048, T256, 0, s>>>(d_arena, arena_cap, d_st, d_ev_off, d_events);
   k_flow_events<<<1024, 256, 0, s>>>(D, B, FH, d_ev_off, d_events);
-  if (nh_tail) k_flow_events<<<1024, 256, 0, s>>>(D, B, FT, d_ev_off, d_events);
+  if (nh_tail) HIPCHK(hipStreamWaitEvent(s, evt_done, 0));
   k_recycle_copy<<<256, 256, 0, s>>>(D);
   k_recycle_fin<<<1, 64, 0, s>>>(D);
   HIPCHK(hipGetLastError());

@@ -412,3 +412,117 @@ def test_flow_plan_widths(vmax):
     rec["oid_id"] = np.arange(1, n + 1)
     eng, orc = _run_pair(wl.split_batches(rec, 8000), 2, sample_syms=[0, 1])
     assert eng.stats()["n_flow_books"] == 2
+
+
+# ---- plan-loop edge cases (gen_plan_asm.py): half-group padding, staging flushes inside
+#      sweeps, sentinel tops, the level cap, and both plan widths on each
+
+def _book(prices, vols, sides, sym=0, oid0=1, uuid=9):
+    n = len(prices)
+    r = np.zeros(n, wl.ORDER_DTYPE)
+    r["symbol_id"] = sym
+    r["price_fx"] = np.asarray(prices, np.int64) * 10**6
+    r["volume_fx"] = np.asarray(vols, np.int64)
+    r["side"] = sides
+    r["action"] = 1
+    r["uuid_id"] = uuid
+    r["oid_id"] = np.arange(oid0, oid0 + n)
+    return r
+
+
+@pytest.mark.gpu
+def test_flow_half_group_padding_residues():
+    """Books of 128..135 orders (every residue mod the 8-record half-group) and a few odd sizes,
+    one batch each on the same book: exact events, levels and FIFOs after every batch."""
+    rng = np.random.default_rng(31)
+    batches, oid = [], 1
+    for n in list(range(128, 136)) + [999, 1001, 2047]:
+        b = _book(rng.integers(30, 71, n), rng.integers(1, 40, n) * 10**6, rng.integers(0, 2, n), oid0=oid)
+        oid += n
+        batches.append(b)
+    eng, orc = _engine(1, 4096), Oracle(1)
+    for i, b in enumerate(batches):
+        eng.submit(b)
+        _cmp_events(eng.drain(), orc.submit(b), f"batch {i} ({len(b)} orders)")
+        assert eng.stats()["n_flow_books"] == 1, f"batch {i} not on the flow path"
+        assert np.array_equal(eng.levels(0), orc.levels(0)), f"levels after batch {i}"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("unit", [10**6, (1 << 34) + 1])
+def test_flow_staging_stress_sweeps(unit):
+    """Rounds of 8 small makers on consecutive levels followed by one taker that empties them
+    (exact fill or a partial at the last level): 8 level-emptying touches inside one order,
+    rounds of 9 orders straddling the 8-record half-groups, so the touch staging is flushed
+    inside sweeps.  unit 1e6 runs the 32-bit plan, (2^34 + 1) the 64-bit one."""
+    rng = np.random.default_rng(77 if unit == 10**6 else 78)
+    prices, vols, sides = [], [], []
+    for r in range(2400):
+        sell = r % 2 == 0                      # makers' side alternates per round
+        lv = np.arange(51, 59) if sell else np.arange(49, 41, -1)
+        v = rng.integers(1, 4, 8)
+        prices += list(lv)
+        vols += list(v)
+        sides += [1 if sell else 0] * 8
+        prices.append(58 if sell else 42)
+        vols.append(int(v.sum()) - int(rng.integers(0, 2)))
+        sides.append(0 if sell else 1)
+    rec = _book(prices, np.asarray(vols, np.int64) * unit, np.asarray(sides, np.uint8))
+    eng, orc = _run_pair(wl.split_batches(rec, 7200), 1, sample_syms=[0])
+    s = eng.stats()
+    assert s["n_flow_books"] == 1 and s["n_flow_touches"] > 1.7 * s["n_flow_orders"]
+
+
+@pytest.mark.gpu
+def test_flow_one_sided_books_and_sentinel_tops():
+    """Symbol 0 sees only BUYs, symbol 1 only SELLs (the opposite top stays at its sentinel
+    level); then a batch sweeps each side empty and rests behind the sentinels."""
+    rng = np.random.default_rng(5)
+    n = 3000
+    b0 = _book(rng.integers(10, 60, n), rng.integers(1, 9, n) * 10**6, np.zeros(n, np.uint8), sym=0, oid0=1)
+    b1 = _book(rng.integers(40, 90, n), rng.integers(1, 9, n) * 10**6, np.ones(n, np.uint8), sym=1, oid0=1)
+    first = np.concatenate([b0, b1])
+    tot0, tot1 = int(b0["volume_fx"].sum()), int(b1["volume_fx"].sum())
+    # 200 SELLs at the lowest price take every bid of symbol 0, then rest; mirrored for 1
+    s0 = _book([1] * 200, [tot0 // 100] * 200, np.ones(200, np.uint8), sym=0, oid0=10**6)
+    s1 = _book([99] * 200, [tot1 // 100] * 200, np.zeros(200, np.uint8), sym=1, oid0=10**6)
+    second = np.concatenate([s0, s1])
+    eng, orc = _run_pair([first, second, first.copy()], 2, sample_syms=[0, 1])
+    assert eng.stats()["n_flow_books"] == 2
+
+
+@pytest.mark.gpu
+def test_flow_one_order_sweeps_every_level():
+    """100 ask levels, then one BUY that takes all of them (one order logs more touches than the
+    staging holds) and rests the remainder; mirrored on the bid side in the next batch."""
+    rng = np.random.default_rng(9)
+    k = np.repeat(np.arange(2, 102), 3)
+    asks = _book(k, rng.integers(1, 5, len(k)) * 10**6, np.ones(len(k), np.uint8), oid0=1)
+    big = _book([105], [int(asks["volume_fx"].sum()) + 7 * 10**6], [0], oid0=9000)
+    filler = _book(rng.integers(110, 121, 150), [10**6] * 150, np.ones(150, np.uint8), oid0=10000)
+    b1 = np.concatenate([asks, big, filler])
+    bids = _book(k, rng.integers(1, 5, len(k)) * 10**6, np.zeros(len(k), np.uint8), oid0=20000)
+    big2 = _book([1], [int(bids["volume_fx"].sum()) + 7 * 10**6 + 10**8], [1], oid0=30000)
+    b2 = np.concatenate([bids, big2, _book([50] * 150, [10**6] * 150, np.zeros(150, np.uint8), oid0=40000)])
+    eng, orc = _engine(1, 1024), Oracle(1)
+    for i, b in enumerate((b1, b2)):
+        eng.submit(b)
+        _cmp_events(eng.drain(), orc.submit(b), f"batch {i}")
+        st = eng.stats()
+        assert st["n_flow_books"] == 1 and st["max_segment"] == len(b)
+        assert np.array_equal(eng.levels(0), orc.levels(0))
+        for p in orc.levels(0)["price_fx"]:
+            assert np.array_equal(eng.fifo(0, int(p)), orc.fifo(0, int(p)))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nlev", [126, 127])
+def test_flow_level_cap(nlev):
+    """A batch whose book reaches exactly 126 distinct prices runs on the flow path; 127 is
+    declined (legacy / cold kernels).  Both exact."""
+    rng = np.random.default_rng(nlev)
+    n = 4000
+    prices = np.concatenate([np.arange(1, nlev + 1), rng.integers(1, nlev + 1, n - nlev)])
+    rec = _book(prices, rng.integers(1, 20, n) * 10**6, rng.integers(0, 2, n))
+    eng, orc = _run_pair([rec], 1, sample_syms=[0])
+    assert eng.stats()["n_flow_books"] == (1 if nlev == 126 else 0)

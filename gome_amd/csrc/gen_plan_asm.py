@@ -52,7 +52,11 @@ X = D
 HC = "s97"                       # half-groups left + 1
 ADDR = "s[98:99]"                # SMEM address of the next half-group
 SAVE = "s100"                    # M0 (staging count) saved around lane writes
-CLOBBERS = [f"s{i}" for i in range(44, 101)]
+CLOBBERS = [f"s{i}" for i in range(44, 101)] + ["v32", "v33", "v34", "v35"]
+# W32 depth layout: one 64-bit lane pair per side, lane j = levels 2j (low word) and 2j+1 (high
+# word): asks in v[32:33], bids in v[34:35] (fixed registers: the pair must be consecutive).
+PAIR = {"A": (32, 33), "B": (34, 35)}
+ZERO = "s91"                     # W32: stays 0, the high word of the rest amount s[90:91]
 COPY_REST = os.environ.get("GOME_PLAN_COPY", "0") == "1"   # measured: no gain, 1.35x code
 PF_DIST = int(os.environ.get("GOME_PLAN_PF", "0"))  # L2 prefetch distance in bytes (0: off);
 # k_flow_prep pads ord8 by FL_ORD8_PAD records, which must cover it
@@ -124,6 +128,16 @@ class Gen:
         becomes a cached top).  Sentinel lanes may hold garbage; their depth is never used."""
         e = self.e
         ln = self.ln
+        if self.w == 32:
+            ev, od = PAIR[sd]
+            e(f"s_lshr_b32 {T0}, {k}, 1")
+            e(f"v_readlane_b32 {O[0]}, v{ev}, {T0}")
+            e(f"v_readlane_b32 {O[2]}, v{od}, {T0}")
+            e(f"s_bfm_b64 {M}, 1, {T0}")
+            e(f"s_bitcmp1_b32 {k}, 0")
+            e(f"s_cselect_b32 {d[0]}, {O[2]}, {O[0]}")
+            self.zero_half(ev, od)
+            return
         e(f"s_and_b32 {T0}, {k}, 63")
         e(f"v_readlane_b32 {O[0]}, {ln(sd, 'l0')}, {T0}")
         e(f"v_readlane_b32 {O[2]}, {ln(sd, 'l1')}, {T0}")
@@ -144,11 +158,57 @@ class Gen:
         if self.w == 64:
             e(f"v_mov_b32 {ln(sd, 'h1')}, 0")
 
+    def zero_half(self, ev: int, od: int):
+        """W32: zero the word of lane M (one-hot) selected by SCC (1: odd level)."""
+        e = self.e
+        e(f"s_cselect_b64 exec, {M}, 0")
+        e(f"v_mov_b32 v{od}, 0")
+        e(f"s_cselect_b64 exec, 0, {M}")
+        e(f"v_mov_b32 v{ev}, 0")
+
+    def next_top(self, sd: str):
+        """W32, after the cached top of side sd emptied: the next level of that side (asks: the
+        lowest resting one, bids: the highest; the sentinels 127 / 0 are nonzero words) becomes
+        the cached top: one 64-bit compare finds its lane pair, the pair's words pick the level."""
+        e = self.e
+        ev, od = PAIR[sd]
+        top, topd = (BA, BAD) if sd == "A" else (BB, BBD)
+        e("s_mov_b64 exec, -1")
+        e(f"v_cmp_ne_u64_e64 {M}, 0, v[{ev}:{od}]")
+        if sd == "A":
+            e(f"s_ff1_i32_b64 {T0}, {M}")
+        else:
+            e(f"s_flbit_i32_b64 {T0}, {M}")
+            e(f"s_sub_u32 {T0}, 63, {T0}")
+        e(f"v_readlane_b32 {O[0]}, v{ev}, {T0}")
+        e(f"v_readlane_b32 {O[2]}, v{od}, {T0}")
+        e(f"s_lshl_b32 {top}, {T0}, 1")
+        e(f"s_bfm_b64 {M}, 1, {T0}")
+        if sd == "A":   # lowest: the even level unless it is empty
+            e(f"s_cmp_eq_u32 {O[0]}, 0")
+        else:           # highest: the odd level unless it is empty
+            e(f"s_cmp_lg_u32 {O[2]}, 0")
+        e(f"s_cselect_b32 {topd[0]}, {O[2]}, {O[0]}")
+        e(f"s_cselect_b32 {T0}, 1, 0")
+        self.zero_half(ev, od)
+        e(f"s_add_u32 {top}, {top}, {T0}")
+
     def write(self, k: str, v, sd: str):
         """Level k := v (end of the loop: the cached tops go back to their lanes).  The other
         set's lane written is a sentinel lane (level 0: set 0 lane 0, level 127: set 1 lane
         63), whose value is never used."""
         e = self.e
+        if self.w == 32:
+            ev, od = PAIR[sd]
+            e(f"s_lshr_b32 {T0}, {k}, 1")
+            e(f"s_bfm_b64 {M}, 1, {T0}")
+            e(f"s_bitcmp1_b32 {k}, 0")
+            e(f"s_cselect_b64 exec, {M}, 0")
+            e(f"v_mov_b32 v{od}, {v[0]}")
+            e(f"s_cselect_b64 exec, 0, {M}")
+            e(f"v_mov_b32 v{ev}, {v[0]}")
+            e("s_mov_b64 exec, -1")
+            return
         e(f"s_mov_b32 {SAVE}, m0")
         e(f"s_and_b32 {T0}, {k}, 63")
         e(f"s_cmp_lt_u32 {k}, 64")
@@ -167,8 +227,17 @@ class Gen:
 
     def add_lane(self, sd: str):
         """Level L += A in the lane registers: the amount goes to the set of L, the other set's
-        lane L % 64 gets 0.  exec is left narrowed (only lane-select ops follow)."""
+        lane L % 64 gets 0.  exec is left narrowed (only lane-select ops follow).  W32: one 64-bit
+        add of A << (32 * (L & 1)) to lane pair L >> 1."""
         e = self.e
+        if self.w == 32:
+            ev, od = PAIR[sd]
+            e(f"s_lshr_b32 {T0}, {L}, 1")
+            e(f"s_bfm_b64 exec, 1, {T0}")
+            e(f"s_lshl_b32 {T0}, {L}, 5")            # (L & 1) << 5 in the low 6 bits
+            e(f"s_lshl_b64 s[92:93], s[90:91], {T0}")  # s91 = 0
+            e(f"v_lshl_add_u64 v[{ev}:{od}], s[92:93], 0, v[{ev}:{od}]")
+            return
         e(f"s_cmp_lt_u32 {L}, 64")
         self.csel(A1, 0, A)
         self.csel(A, A, 0)
@@ -352,11 +421,14 @@ class Gen:
         e(f"s_or_b32 {K}, {JJS}, {otop}")
         self.log(K, otopd, False)        # (the staging check is folded into the test below)
         self.mov(T, D)              # (the emptied level's lane is 0: it leaves the side)
-        if buy:
-            self.lowest_ask()
+        if self.w == 32:
+            self.next_top("A" if buy else "B")
         else:
-            self.highest_bid()
-        self.promote(otop, otopd, "A" if buy else "B")
+            if buy:
+                self.lowest_ask()
+            else:
+                self.highest_bid()
+            self.promote(otop, otopd, "A" if buy else "B")
         # one branch for the common case "T > 0, room in the staging, the next level crosses
         # too": T == 0 or a full staging make the limit a level that cannot cross
         never = "0" if buy else "127"
@@ -466,10 +538,20 @@ class Gen:
         e(f"s_add_u32 {HC}, %[nh], 1")
         e(f"s_mov_b32 {JJS}, 0xffffff00")          # (-1) << 8: the first record is order 0
         e("s_mov_b32 m0, %[nacc]")
-        self.lowest_ask()
-        self.promote(BA, BAD, "A")
-        self.highest_bid()
-        self.promote(BB, BBD, "B")
+        if self.w == 32:   # operands -> fixed lane pairs; s91 = 0
+            e("s_mov_b64 exec, -1")
+            for sd, nm in (("A", "a"), ("B", "b")):
+                ev, od = PAIR[sd]
+                e(f"v_mov_b32 v{ev}, %[{nm}l0]")
+                e(f"v_mov_b32 v{od}, %[{nm}l1]")
+            e(f"s_mov_b32 {ZERO}, 0")
+            self.next_top("A")
+            self.next_top("B")
+        else:
+            self.lowest_ask()
+            self.promote(BA, BAD, "A")
+            self.highest_bid()
+            self.promote(BB, BBD, "B")
         e(f"s_load_dwordx16 s[44:59], {ADDR}, 0x0")
         if PF_DIST:
             e("s_mov_b64 exec, 1")
@@ -489,6 +571,12 @@ class Gen:
         e("s_mov_b64 exec, -1")
         self.write(BA, BAD, "A")
         self.write(BB, BBD, "B")
+        if self.w == 32:   # fixed lane pairs -> operands
+            e("s_mov_b64 exec, -1")
+            for sd, nm in (("A", "a"), ("B", "b")):
+                ev, od = PAIR[sd]
+                e(f"v_mov_b32 %[{nm}l0], v{ev}")
+                e(f"v_mov_b32 %[{nm}l1], v{od}")
         e("s_mov_b32 %[nacc], m0")
         return self.out
 

@@ -806,6 +806,16 @@ __device__ __forceinline__ void fl_plan_book(const Dev& D, const FlowArgs& F, ui
   const int64_t a0 = (m0 & M_SALE) ? d0 : 0, a1 = (m1 & M_SALE) ? d1 : (lane == 63 ? 1 : 0);
   const int64_t b0 = (m0 & M_BUY) ? d0 : (lane == 0 ? 1 : 0), b1 = (m1 & M_BUY) ? d1 : 0;
   FlDepth Da{lo32(a0), hi32(a0), lo32(a1), hi32(a1)}, Db{lo32(b0), hi32(b0), lo32(b1), hi32(b1)};
+  if (w32) {  // the 32-bit plan's layout: lane j holds levels 2j (l0) and 2j + 1 (l1)
+    const uint32_t se = (2u * lane) & 63u, so = (2u * lane + 1u) & 63u;
+    const bool hiset = lane >= 32;
+    auto pick = [&](uint32_t x0, uint32_t x1, uint32_t src) {
+      const uint32_t v0 = __shfl(x0, src), v1 = __shfl(x1, src);
+      return hiset ? v1 : v0;
+    };
+    Da = FlDepth{pick(Da.l0, Da.l1, se), 0u, pick(Da.l0, Da.l1, so), 0u};
+    Db = FlDepth{pick(Db.l0, Db.l1, se), 0u, pick(Db.l0, Db.l1, so), 0u};
+  }
 
   FlLog lg{vreg(0u), vreg(0u), vreg(0u), 0u, 0u, 0u, FL_TOUCH_MUL * n, (GOME_GLB v4u*)(F.log + FL_TOUCH_MUL * beg)};
   // records are read in half-groups of 8 (the book's stream is padded to whole groups)
@@ -851,6 +861,16 @@ __device__ __forceinline__ void fl_plan_book(const Dev& D, const FlowArgs& F, ui
   auto u64of = [&](uint32_t lo, uint32_t hi) -> uint64_t {
     return w32 ? static_cast<uint64_t>(lo) * g : (static_cast<uint64_t>(hi) << 32) | lo;
   };
+  if (w32) {  // back to level k -> lane k % 64 of set k / 64
+    auto level = [&](uint32_t ev, uint32_t od, uint32_t k) {
+      const uint32_t e = __shfl(ev, (k >> 1) & 63u), o = __shfl(od, (k >> 1) & 63u);
+      return (k & 1u) ? o : e;
+    };
+    const uint32_t a_lo = level(Da.l0, Da.l1, lane), a_hi = level(Da.l0, Da.l1, lane + 64);
+    const uint32_t b_lo = level(Db.l0, Db.l1, lane), b_hi = level(Db.l0, Db.l1, lane + 64);
+    Da = FlDepth{a_lo, 0u, a_hi, 0u};
+    Db = FlDepth{b_lo, 0u, b_hi, 0u};
+  }
   const uint64_t ua0 = u64of(Da.l0, Da.h0), ua1 = u64of(Da.l1, Da.h1);
   const uint64_t ub0 = u64of(Db.l0, Db.h0), ub1 = u64of(Db.l1, Db.h1);
   const unsigned long long A0 = __ballot(ua0 != 0) & ~1ull, A1 = __ballot(ua1 != 0) | (1ull << 63);

@@ -82,7 +82,7 @@ struct gome_engine {
   hipStream_t flow_stream = nullptr, flow2_stream = nullptr;
   bool own_stream = false;
   hipEvent_t fork{}, join{}, evh0{}, evh1{};
-  hipEvent_t joinf{}, joinf2{}, prep_h{}, prep_t{}, evf0{}, evf1{}, fork_adm{}, adm_done{}, evs{}, evt_done{};
+  hipEvent_t joinf{}, joinf2{}, prep_h{}, prep_t{}, evf0{}, evf1{}, fork_adm{}, adm_done{};
   FlowArgs F{};
   Prep* d_prep = nullptr;
   PendEnt* d_pend = nullptr;
@@ -148,8 +148,7 @@ struct gome_engine {
     if (evf0) {
       (void)hipEventDestroy(evf0); (void)hipEventDestroy(evf1); (void)hipEventDestroy(joinf);
       (void)hipEventDestroy(joinf2); (void)hipEventDestroy(prep_h); (void)hipEventDestroy(prep_t);
-      (void)hipEventDestroy(fork_adm); (void)hipEventDestroy(adm_done); (void)hipEventDestroy(evs);
-      (void)hipEventDestroy(evt_done);
+      (void)hipEventDestroy(fork_adm); (void)hipEventDestroy(adm_done);
     }
     if (hot_stream) (void)hipStreamDestroy(hot_stream);
     if (flow_stream) (void)hipStreamDestroy(flow_stream);
@@ -202,8 +201,6 @@ gome_status gome_engine::init(const gome_config& c) {
   HIPCHK(hipEventCreate(&evf1));
   HIPCHK(hipEventCreateWithFlags(&fork_adm, hipEventDisableTiming));
   HIPCHK(hipEventCreateWithFlags(&adm_done, hipEventDisableTiming));
-  HIPCHK(hipEventCreateWithFlags(&evs, hipEventDisableTiming));
-  HIPCHK(hipEventCreateWithFlags(&evt_done, hipEventDisableTiming));
   HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_match_hot),
                              hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(HOT_LDS_BYTES)));
 
@@ -420,6 +417,8 @@ gome_status gome_engine::run(const gome_order* d_ord, uint32_t n, hipStream_t s)
     k_flow_toff<<<1, 1024, 0, hot_stream>>>(D, FT);
     k_flow_count<<<1024, 256, 0, hot_stream>>>(D, B, FT);
     k_flow_write<<<nh_tail, FL_WRITE_T, 0, hot_stream>>>(D, B, FT);
+    // the tail's events into the arena now (k_ev_scatter places them after the scan)
+    k_flow_events_arena<<<1024, 256, 0, hot_stream>>>(D, B, FT);
   } else {
     HIPCHK(hipEventRecord(prep_t, hot_stream));
   }
@@ -443,15 +442,8 @@ gome_status gome_engine::run(const gome_order* d_ord, uint32_t n, hipStream_t s)
 
   // ---- event compaction into publish order
   scan(d_ev_count, n, d_ev_off, &d_st->n_events, s);
-  if (nh_tail) {  // the tail's events beside the rest (all only need the scan; disjoint slots)
-    HIPCHK(hipEventRecord(evs, s));
-    HIPCHK(hipStreamWaitEvent(hot_stream, evs, 0));
-    k_flow_events<<<1024, 256, 0, hot_stream>>>(D, B, FT, d_ev_off, d_events);
-    HIPCHK(hipEventRecord(evt_done, hot_stream));
-  }
   k_ev_scatter<<<2048, T256, 0, s>>>(d_arena, arena_cap, d_st, d_ev_off, d_events);
   k_flow_events<<<1024, 256, 0, s>>>(D, B, FH, d_ev_off, d_events);
-  if (nh_tail) HIPCHK(hipStreamWaitEvent(s, evt_done, 0));
   k_recycle_copy<<<256, 256, 0, s>>>(D);
   k_recycle_fin<<<1, 64, 0, s>>>(D);
   HIPCHK(hipGetLastError());

@@ -1231,15 +1231,50 @@ __global__ void k_flow_count(Dev D, BatchArgs B, FlowArgs F) {
 
 // ============================================================== k_flow_events
 // After the publish-order scan: every fill event at out[ev_off[taker] + fill_idx].
-__global__ void k_flow_events(Dev D, BatchArgs B, FlowArgs F, const uint32_t* ev_off, gome_event* out) {
+// ARENA: the events go to the batch's event arena (one bump allocation per wave) for
+// k_ev_scatter to place, so they need not wait for the publish-order scan (the tail's books,
+// done long before the head's); else straight to out[ev_off[taker] + fill_idx].
+template <bool ARENA>
+__device__ __forceinline__ void fl_events(const Dev& D, const BatchArgs& B, const FlowArgs& F, const uint32_t* ev_off,
+                                          gome_event* out) {
   const uint32_t hend = fl_hend(D, F), nb = hend > F.h0 ? hend - F.h0 : 0u;
   const uint32_t total = nb ? F.toff[F.tb + nb] : 0u;
-  for (uint32_t gt = blockIdx.x * blockDim.x + threadIdx.x; gt < total; gt += gridDim.x * blockDim.x) {
-    const uint32_t hb = fl_book_of(F, nb, gt), h = F.h0 + hb, t = gt - F.toff[F.tb + hb];
-    const uint32_t beg = F.hdr[h].beg, L = FL_TOUCH_MUL * beg, sym = F.hdr[h].sym;
-    const Touch x = F.log[L + t];
-    if (((x.kr >> 7) & 1u) != TK_CONS) continue;
-    const FlTouchCtx c = fl_touch_ctx(F, h, L, x);
+  const uint32_t lane = lane_id(), stride = gridDim.x * blockDim.x;
+  for (uint32_t g0 = blockIdx.x * blockDim.x + (threadIdx.x & ~63u); g0 < total; g0 += stride) {
+    const uint32_t gt = g0 + lane;
+    uint32_t h = 0, L = 0, t = 0, cnt = 0;
+    Touch x{};
+    FlTouchCtx c{};
+    if (gt < total) {
+      const uint32_t hb = fl_book_of(F, nb, gt);
+      h = F.h0 + hb;
+      t = gt - F.toff[F.tb + hb];
+      L = FL_TOUCH_MUL * F.hdr[h].beg;
+      x = F.log[L + t];
+      if (((x.kr >> 7) & 1u) == TK_CONS) {
+        c = fl_touch_ctx(F, h, L, x);
+        cnt = c.last - c.first + 1;
+      }
+    }
+    gome_event* dst = nullptr;
+    if (ARENA) {
+      uint32_t inc = cnt;
+      for (uint32_t off = 1; off < 64; off <<= 1) {
+        const uint32_t v = __shfl_up(inc, off);
+        if (lane >= off) inc += v;
+      }
+      const uint32_t tot = __shfl(inc, 63);
+      uint32_t base = 0;
+      if (lane == 0 && tot) base = atomicAdd(&D.st->ev_bump, tot);
+      base = __shfl(base, 0);
+      if (base + tot > B.arena_cap) {
+        if (lane == 0 && tot) atomicOr(&D.st->err, ERR_EVENTS);
+        continue;
+      }
+      dst = B.arena + base + (inc - cnt);
+    }
+    if (!cnt) continue;
+    const uint32_t beg = F.hdr[h].beg, sym = F.hdr[h].sym;
     const Prep tk = B.prep[beg + tk_j(x)];
     // taker remaining before this level: volume minus what its better levels took
     int64_t tb = tk.vol;
@@ -1250,7 +1285,7 @@ __global__ void k_flow_events(Dev D, BatchArgs B, FlowArgs F, const uint32_t* ev
     }
     const uint32_t ig_n = c.Lq->ig_n, nrest = c.Lq->nrest, ig_all = c.Lq->ig_all;
     const int64_t price = c.Lq->price;
-    gome_event* dst = out + ev_off[tk.idx] + F.fbase[L + t];
+    if (!ARENA) dst = out + ev_off[tk.idx] + F.fbase[L + t];
     for (uint32_t m = c.first; m <= c.last; ++m) {
       int64_t e, v;
       uint32_t oid, uuid, tx;
@@ -1297,6 +1332,15 @@ __global__ void k_flow_events(Dev D, BatchArgs B, FlowArgs F, const uint32_t* ev
       dst[m - c.first] = ev;
     }
   }
+}
+
+__global__ __launch_bounds__(256) void k_flow_events(Dev D, BatchArgs B, FlowArgs F, const uint32_t* ev_off,
+                                                     gome_event* out) {
+  fl_events<false>(D, B, F, ev_off, out);
+}
+
+__global__ __launch_bounds__(256) void k_flow_events_arena(Dev D, BatchArgs B, FlowArgs F) {
+  fl_events<true>(D, B, F, nullptr, nullptr);
 }
 
 // ============================================================== k_flow_write

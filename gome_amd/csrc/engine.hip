@@ -318,6 +318,7 @@ gome_status gome_engine::run(const gome_order* d_ord, uint32_t n, hipStream_t s)
   HIPCHK(hipMemsetAsync(d_claim, 0, (adm_mask + 1ull) * 4, flow_stream));
   HIPCHK(hipMemsetAsync(d_amin, 0xFF, (adm_mask + 1ull) * 4, flow_stream));
   k_adm<<<gN, T256, 0, flow_stream>>>(d_ord, n, d_claim, d_amin, d_adm_slot, adm_mask);
+  k_adm_flag<<<gN, T256, 0, flow_stream>>>(d_ord, n, d_adm_slot, d_amin);
   HIPCHK(hipEventRecord(adm_done, flow_stream));
   k_validate<<<gN, T256, 0, s>>>(d_ord, n, cfg.max_symbols, d_st);
 
@@ -359,7 +360,7 @@ gome_status gome_engine::run(const gome_order* d_ord, uint32_t n, hipStream_t s)
 
   // ---- admission markers (k_adm, launched above on the flow stream)
   HIPCHK(hipStreamWaitEvent(s, adm_done, 0));
-  k_prep<<<gN, T256, 0, s>>>(d_ord, n, sidx, d_adm_slot, d_amin, d_prep);
+  k_prep<<<gN, T256, 0, s>>>(d_ord, n, sidx, d_adm_slot, d_prep);
 
   // ---- match_books: one wavefront per book; hot books (LDS) on a second stream,
   //      concurrently with the cold books (HBM)

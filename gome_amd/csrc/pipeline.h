@@ -275,8 +275,18 @@ struct Prep {
 };
 static_assert(sizeof(Prep) == 32, "Prep layout");
 
+// Admission verdict per input record, in place of its marker slot (1: an ADD that holds the
+// lowest index of its (S, uuid, oid) key, nodepool.go:14-28), so k_prep (on the critical path)
+// reads one flag instead of chasing slot -> minimum.  Runs beside the radix sort.
+__global__ void k_adm_flag(const gome_order* ord, uint32_t n, uint32_t* slot, const uint32_t* amin) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint8_t action = ord[i].action;
+  slot[i] = (action == GOME_ADD && amin[slot[i]] == i) ? 1u : 0u;
+}
+
 __global__ void k_prep(const gome_order* ord, uint32_t n, const uint32_t* sidx,
-                       const uint32_t* adm_slot, const uint32_t* amin, Prep* prep) {
+                       const uint32_t* adm_flag, Prep* prep) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint32_t j = sidx[i];
@@ -289,7 +299,7 @@ __global__ void k_prep(const gome_order* ord, uint32_t n, const uint32_t* sidx,
   q.idx = j;
   q.side = o.side;
   q.action = o.action;
-  q.adm = (o.action == GOME_ADD && amin[adm_slot[j]] == j) ? 1 : 0;
+  q.adm = static_cast<uint8_t>(adm_flag[j]);
   q.pad = 0;
   prep[i] = q;
 }

@@ -82,6 +82,9 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.gome_render_match_result.argtypes = [VP, VP, C.c_uint32] + [C.c_char_p] * 6 + [
         C.c_char_p, C.c_size_t]
     lib.gome_render_match_result.restype = C.c_int64
+    lib.gome_render_link_node.argtypes = [C.c_char_p, C.c_int64, C.c_uint32, C.c_int64, C.c_uint32] + [
+        C.c_char_p] * 5 + [C.c_size_t]
+    lib.gome_render_link_node.restype = C.c_int64
     for f in ("gome_create", "gome_submit_batch", "gome_submit_batch_device", "gome_drain_events",
               "gome_device_events", "gome_get_stats", "gome_snapshot_levels", "gome_snapshot_fifo",
               "gome_fixed_from_double"):
@@ -116,6 +119,19 @@ def render_match_result(ev: np.void, taker: np.void, symbol: str, taker_uuid: st
     n = lib.gome_render_match_result(e.ctypes.data, t.ctypes.data, accuracy, symbol.encode(),
                                      taker_uuid.encode(), taker_oid.encode(), enc(maker_uuid),
                                      enc(maker_oid), enc(maker_next_oid), buf, len(buf))
+    if n < 0:
+        raise GomeError(GOME_E_INVAL, "render failed")
+    return buf.raw[:n].decode()
+
+
+def render_link_node(symbol: str, price_fx: int, side: int, volume_fx: int, uuid: str, oid: str,
+                     prev_oid: str | None, next_oid: str | None, accuracy: int = 8) -> str:
+    """A resting node's JSON as the reference stores it in S:link:<price> (nodelink.go:119-122)."""
+    lib = load_library()
+    enc = lambda s: None if s is None else s.encode()
+    buf = C.create_string_buffer(4096)
+    n = lib.gome_render_link_node(symbol.encode(), int(price_fx), int(side), int(volume_fx), accuracy,
+                                  uuid.encode(), oid.encode(), enc(prev_oid), enc(next_oid), buf, len(buf))
     if n < 0:
         raise GomeError(GOME_E_INVAL, "render failed")
     return buf.raw[:n].decode()

@@ -128,6 +128,7 @@ struct NodeView {
   uint32_t accuracy;
   bool is_first, is_last;
   const char* next_oid;  // nullptr => NextNode ""
+  const char* prev_oid = nullptr;  // nullptr => PrevNode ""
 };
 
 // encoding/json of OrderNode, fields in declaration order (ordernode.go:9-36), keys
@@ -146,7 +147,8 @@ void render_node(Out& o, const NodeView& v) {
   o.put(",\"NodeName\":"); json_string(o, (S + ":node:" + v.oid).c_str());
   o.put(",\"IsFirst\":"); o.put(v.is_first ? "true" : "false");
   o.put(",\"IsLast\":"); o.put(v.is_last ? "true" : "false");
-  o.put(",\"PrevNode\":\"\"");
+  o.put(",\"PrevNode\":");
+  json_string(o, v.prev_oid ? (S + ":node:" + v.prev_oid).c_str() : "");
   o.put(",\"NextNode\":");
   json_string(o, v.next_oid ? (S + ":node:" + v.next_oid).c_str() : "");
   o.put(",\"NodeLink\":"); json_string(o, (S + ":link:" + P).c_str());
@@ -161,6 +163,22 @@ void render_node(Out& o, const NodeView& v) {
 }
 
 }  // namespace
+
+extern "C" int64_t gome_render_link_node(const char* symbol, int64_t price_fx, uint32_t side, int64_t volume_fx,
+                                         uint32_t accuracy, const char* uuid, const char* oid,
+                                         const char* prev_oid, const char* next_oid, char* buf, size_t cap) {
+  if (!symbol || !uuid || !oid || !buf) return -1;
+  Out o{buf, cap};
+  // a resting node as nodelink.go stores it (SetLinkNode, :119-122): the ADD that rested,
+  // its remaining volume, and the FIFO flags / neighbours kept by InitOrderLink, SetLast and
+  // DeleteLinkNode (:12-19, :53-64, :124-166)
+  NodeView v{GOME_ADD, uuid, oid, symbol, static_cast<int>(side), price_fx, volume_fx, accuracy,
+             prev_oid == nullptr, next_oid == nullptr, next_oid, prev_oid};
+  render_node(o, v);
+  if (!o.ok) return -1;
+  buf[o.n] = 0;
+  return static_cast<int64_t>(o.n);
+}
 
 extern "C" gome_status gome_fixed_from_double(double x, uint32_t accuracy, int64_t* out) {
   return fixed_from_double(x, accuracy, out);

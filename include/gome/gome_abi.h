@@ -210,6 +210,14 @@ int64_t gome_render_match_result(const gome_event* ev, const gome_order* taker,
                                  const char* taker_uuid, const char* taker_oid,
                                  const char* maker_uuid, const char* maker_oid,
                                  const char* maker_next_oid, char* buf, size_t cap);
+/* Render one resting node as the reference stores it in S:link:<price> under
+ * S:node:<oid> (nodelink.go:119-122; Go encoding/json of engine.OrderNode, byte-identical):
+ * the ADD that rested with its remaining volume, IsFirst / IsLast / PrevNode / NextNode from
+ * its FIFO neighbours (NULL = none).  Used by the snapshot writer (gome_amd/snapshot.py,
+ * SURVEY 8f rank 2).  Returns bytes written (excl. NUL) or a negative value. */
+int64_t gome_render_link_node(const char* symbol, int64_t price_fx, uint32_t side, int64_t volume_fx,
+                              uint32_t accuracy, const char* uuid, const char* oid,
+                              const char* prev_oid, const char* next_oid, char* buf, size_t cap);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,123 @@
+"""Checkpoint / resume in the reference's Redis key schema (gome_amd/snapshot.py, SURVEY §5 and
+§8f rank 2).  The checker is the literal transliteration (oracle/literal.py), whose FakeRedis
+holds exactly the keys the reference would hold after the same request stream."""
+import numpy as np
+import pytest
+
+from gome_amd import snapshot
+from gome_amd.abi import Engine, GomeError, render_link_node
+from oracle.literal import NewOrderNode, run_batches
+from tests.helpers import Interner, random_batches, render_events, requests_to_records
+
+SYMBOLS = ("eth2usdt", "btc2usdt", "ltc2usdt")
+
+
+def test_link_node_json_matches_literal():
+    """Resting node JSON (SetLinkNode) byte-identical to the literal's encoding/json."""
+    rng = np.random.default_rng(3)
+    for i in range(300):
+        S = str(rng.choice(SYMBOLS))
+        req = dict(uuid=f"u{int(rng.integers(9))}", oid=f"o{i}", symbol=S,
+                   transaction=int(rng.choice([0, 1, 1, 3])), price=float(rng.choice([0.1, 0.25, 0.5, 1.0, 37.5])),
+                   volume=float(rng.choice([0.01, 0.5, 3.0, 1234.5])))
+        n = NewOrderNode(req, 8)
+        n.Action = 1
+        prev = f"o{i - 1}" if rng.random() < 0.6 else None
+        nxt = f"o{i + 1}" if rng.random() < 0.6 else None
+        n.IsFirst, n.IsLast = prev is None, nxt is None
+        n.PrevNode = f"{S}:node:{prev}" if prev else ""
+        n.NextNode = f"{S}:node:{nxt}" if nxt else ""
+        got = render_link_node(S, int(n.Price), n.Transaction, int(n.Volume), req["uuid"], req["oid"], prev, nxt)
+        assert got == n.to_json()
+
+
+def _literal_keys(lit, symbols):
+    """The literal FakeRedis restricted to the book keys of the symbols (zero depth fields
+    dropped: see gome_amd/snapshot.py)."""
+    h, z = {}, {}
+    for key, fields in lit.cache.h.items():
+        S = key.split(":")[0]
+        if S not in symbols or key.endswith(":comparison"):
+            continue
+        if key.endswith(":depth"):
+            fields = {f: v for f, v in fields.items() if float(v) != 0.0}
+            if not fields:
+                continue
+        h[key] = dict(fields)
+    for key, members in lit.cache.z.items():
+        if key.split(":")[0] in symbols and members:
+            z[key] = dict(members)
+    return {"hash": h, "zset": z}
+
+
+def _run(seed, quirks):
+    rng = np.random.default_rng(seed)
+    batches = random_batches(rng, n_batches=4, batch=120, symbols=SYMBOLS, del_frac=0.25, quirks=quirks)
+    lit, lit_events = run_batches(batches)
+    names = Interner()
+    for s in SYMBOLS:
+        names.id("sym", s)
+    eng = Engine(max_symbols=len(SYMBOLS), max_batch=512, max_nodes=1 << 16, max_levels=1 << 14)
+    for b in batches:
+        eng.submit(requests_to_records(b, names))
+        eng.drain()
+    return rng, lit, eng, names
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(4))
+def test_snapshot_equals_literal_redis(seed):
+    """After the same quirk-laden stream, the engine's snapshot equals the reference's Redis
+    book keys: both side ZSETs, the depth HASH, every FIFO link HASH with its node JSON."""
+    _, lit, eng, names = _run(500 + seed, quirks=True)
+    snap = snapshot.redis_snapshot(eng, [names.id("sym", s) for s in SYMBOLS], names)
+    exp = _literal_keys(lit, SYMBOLS)
+    assert snap["zset"] == exp["zset"]
+    assert set(snap["hash"]) == set(exp["hash"])
+    for key in exp["hash"]:
+        assert snap["hash"][key] == exp["hash"][key], key
+    assert snapshot.to_resp(snap).count(b"HSET") == sum(len(v) for v in snap["hash"].values())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(3))
+def test_resume_from_snapshot_continues_identically(seed):
+    """Snapshot -> fresh engine (replayed rests, no fill) -> the same snapshot, and the next
+    batch gives the reference's MatchResults on both the original and the resumed engine."""
+    rng, lit, eng, names = _run(700 + seed, quirks=False)
+    sids = [names.id("sym", s) for s in SYMBOLS]
+    snap = snapshot.redis_snapshot(eng, sids, names)
+    eng2 = Engine(max_symbols=len(SYMBOLS), max_batch=4096, max_nodes=1 << 16, max_levels=1 << 14)
+    snapshot.restore(eng2, snap, names)
+    assert snapshot.redis_snapshot(eng2, sids, names) == snap
+    nxt = random_batches(rng, n_batches=1, batch=150, symbols=SYMBOLS, del_frac=0.25, quirks=False,
+                         oid_base=10**6)
+    rec = requests_to_records(nxt[0], names)
+    eng.submit(rec)
+    a = render_events(eng.drain(), rec, names)
+    eng2.submit(rec)
+    b = render_events(eng2.drain(), rec, names)
+    assert a == b and len(a) > 0
+
+
+@pytest.mark.gpu
+def test_restore_refuses_quirk_books():
+    """A wrong-side cancel (Q2, engine.go:87-116) ZREMs the request's side, so the BUY set keeps
+    a member with no FIFO and depth 0: the snapshot still equals the reference's Redis, but a
+    replay cannot rebuild it, and restore refuses instead of resuming a different book."""
+    names = Interner()
+    names.id("sym", "eth2usdt")
+    add = dict(uuid="u1", oid="o1", symbol="eth2usdt", transaction=0, price=0.5, volume=1.0)
+    add2 = dict(uuid="u1", oid="o2", symbol="eth2usdt", transaction=1, price=0.7, volume=2.0)
+    dele = dict(add, transaction=1)                 # cancel on the wrong side
+    batches = [[(1, add), (1, add2)], [(2, dele)]]
+    lit, _ = run_batches(batches)
+    eng = Engine(max_symbols=1, max_batch=16, max_nodes=1 << 10, max_levels=1 << 10)
+    for b in batches:
+        eng.submit(requests_to_records(b, names))
+        eng.drain()
+    snap = snapshot.redis_snapshot(eng, [0], names)
+    assert snap == _literal_keys(lit, ("eth2usdt",))
+    assert "50000000" in snap["zset"]["eth2usdt:BUY"]
+    with pytest.raises(GomeError):
+        snapshot.restore_records(snap, names)

@@ -267,7 +267,7 @@ gome_status gome_engine::init(const gome_config& c) {
       !alloc(&F.ord8, static_cast<uint64_t>(FL_ORD8_MUL) * nb + FL_ORD8_PAD, "flow records") || !alloc(&F.log, ntouch, "flow touch log") ||
       !alloc(&F.srt, ntouch, "flow level runs") || !alloc(&F.rs, ntouch, "flow new makers") ||
       !alloc(&F.fbase, ntouch, "flow fill bases") || !alloc(&F.ig, F.ig_cap, "flow gathered makers") ||
-      !alloc(&F.ig_bump, 1, "flow gather bump") || !alloc(&F.toff, MAX_FLOW + 2, "flow touch offsets") ||
+      !alloc(&F.ig_bump, 1, "flow gather bump") || !alloc(&F.toff, MAX_FLOW + 16, "flow touch offsets") ||
       !alloc(&F.lvout, static_cast<size_t>(MAX_FLOW) * FL_CAP, "flow final levels"))
     return GOME_E_CAPACITY;
   F.maxt = ceil_div(ntouch, FL_TILE);
@@ -381,10 +381,16 @@ gome_status gome_engine::run(const gome_order* d_ord, uint32_t n, hipStream_t s)
   // flow path: the head (longest FL_HEAD candidates, the batch's critical path) and the tail
   // each run prep -> serial plan -> parallel reconstruction on their own stream, so the
   // hottest book's plan starts after its own prep and the tail overlaps it
-  FlowArgs FH = F, FT = F;
+  // FH: the head's prep; FH0: the hottest book (plan + reconstruction on the flow stream,
+  // the batch's critical path); FH1: the other head books (on the tail's stream, done long
+  // before the hottest); FT: the tail.  tb: each range's slice of toff.
+  FlowArgs FH = F, FH0 = F, FH1 = F, FT = F;
   FH.h0 = 0; FH.h1 = FL_HEAD; FH.tb = 0;
-  FT.h0 = FL_HEAD; FT.h1 = MAX_FLOW; FT.tb = FL_HEAD + 1;
+  FH0.h0 = 0; FH0.h1 = 1; FH0.tb = 0;
+  FH1.h0 = 1; FH1.h1 = FL_HEAD; FH1.tb = 2;
+  FT.h0 = FL_HEAD; FT.h1 = MAX_FLOW; FT.tb = FL_HEAD + 3;
   const uint32_t nh_head = std::min<uint32_t>(FL_HEAD, nhot_max);
+  const uint32_t nh_near = nh_head > 1 ? nh_head - 1 : 0;
   const uint32_t nh_tail = nhot_max > FL_HEAD ? nhot_max - FL_HEAD : 0;
   HIPCHK(hipStreamWaitEvent(flow_stream, fork, 0));
   HIPCHK(hipMemsetAsync(F.pscr, 0, sizeof(FlPrepScr) * FL_HEAD, flow_stream));
@@ -393,17 +399,20 @@ gome_status gome_engine::run(const gome_order* d_ord, uint32_t n, hipStream_t s)
   k_flow_prep_c<<<dim3(FL_PG, nh_head), FL_PREP_T, 0, flow_stream>>>(D, B, FH);
   HIPCHK(hipEventRecord(prep_h, flow_stream));
   HIPCHK(hipEventRecord(evf0, flow_stream));
-  k_flow_plan_head<<<nh_head, 256, 0, flow_stream>>>(D, FH);
+  k_flow_plan_head<<<1, 256, 0, flow_stream>>>(D, FH0);
   HIPCHK(hipEventRecord(evf1, flow_stream));
-  // the head's reconstruction: wide kernels (tile-parallel sort, one wave per level)
-  k_flow_sort_cnt<<<dim3(FL_SORT_GRID, nh_head), FL_TILE, 0, flow_stream>>>(D, FH);
-  k_flow_sort_scan<<<nh_head, FL_CAP, 0, flow_stream>>>(D, FH);
-  k_flow_sort_scatter<<<dim3(FL_SORT_GRID, nh_head), FL_TILE, 0, flow_stream>>>(D, FH);
-  k_flow_level_wide<<<dim3(FL_CAP, nh_head), 64, 0, flow_stream>>>(D, FH);
-  k_flow_toff<<<1, 1024, 0, flow_stream>>>(D, FH);
-  k_flow_count<<<1024, 256, 0, flow_stream>>>(D, B, FH);
-  k_flow_write_lv<<<dim3(FL_CAP, nh_head), 64, 0, flow_stream>>>(D, B, FH);
-  k_flow_write_fin<<<nh_head, 128, 0, flow_stream>>>(D, FH);
+  // the hottest book's reconstruction: wide kernels (tile-parallel sort, one wave per level)
+  auto head_recon = [&](const FlowArgs& R, uint32_t nb, hipStream_t st) {
+    k_flow_sort_cnt<<<dim3(FL_SORT_GRID, nb), FL_TILE, 0, st>>>(D, R);
+    k_flow_sort_scan<<<nb, FL_CAP, 0, st>>>(D, R);
+    k_flow_sort_scatter<<<dim3(FL_SORT_GRID, nb), FL_TILE, 0, st>>>(D, R);
+    k_flow_level_wide<<<dim3(FL_CAP, nb), 64, 0, st>>>(D, R);
+    k_flow_toff<<<1, 1024, 0, st>>>(D, R);
+    k_flow_count<<<1024, 256, 0, st>>>(D, B, R);
+    k_flow_write_lv<<<dim3(FL_CAP, nb), 64, 0, st>>>(D, B, R);
+    k_flow_write_fin<<<nb, 128, 0, st>>>(D, R);
+  };
+  head_recon(FH0, 1, flow_stream);
   HIPCHK(hipEventRecord(joinf, flow_stream));
   // The tail's chain and the legacy hot kernels share the third stream: HIP maps more
   // streams than hardware queues (4 per process, one taken by the caller) onto shared
@@ -423,9 +432,15 @@ gome_status gome_engine::run(const gome_order* d_ord, uint32_t n, hipStream_t s)
   } else {
     HIPCHK(hipEventRecord(prep_t, hot_stream));
   }
+  // the other head books: plan, reconstruction and events (into the arena) after the tail
+  HIPCHK(hipStreamWaitEvent(hot_stream, prep_h, 0));
+  if (nh_near) {
+    k_flow_plan_near<<<nh_near, 256, 0, hot_stream>>>(D, FH1);
+    head_recon(FH1, nh_near, hot_stream);
+    k_flow_events_arena<<<1024, 256, 0, hot_stream>>>(D, B, FH1);
+  }
   // legacy hot path (books the flow path declined); it and the cold kernel read the preps'
   // routing decisions (FlowHdr::ok)
-  HIPCHK(hipStreamWaitEvent(hot_stream, prep_h, 0));
   HIPCHK(hipEventRecord(evh0, hot_stream));
   const uint32_t nleg = std::min<uint32_t>(MAX_HOT, grid);
   k_match_hot<<<nleg, 64, HOT_LDS_BYTES, hot_stream>>>(D, B, d_pend, d_resume, F.hdr);
@@ -444,7 +459,7 @@ gome_status gome_engine::run(const gome_order* d_ord, uint32_t n, hipStream_t s)
   // ---- event compaction into publish order
   scan(d_ev_count, n, d_ev_off, &d_st->n_events, s);
   k_ev_scatter<<<2048, T256, 0, s>>>(d_arena, arena_cap, d_st, d_ev_off, d_events);
-  k_flow_events<<<1024, 256, 0, s>>>(D, B, FH, d_ev_off, d_events);
+  k_flow_events<<<1024, 256, 0, s>>>(D, B, FH0, d_ev_off, d_events);
   k_recycle_copy<<<256, 256, 0, s>>>(D);
   k_recycle_fin<<<1, 64, 0, s>>>(D);
   HIPCHK(hipGetLastError());

@@ -33,9 +33,9 @@ constexpr uint32_t MAX_FLOW = 4096;
 constexpr uint32_t LEGACY_HOT_MIN = 2048;
 constexpr uint32_t MAX_LEGACY = 256;
 #ifndef GOME_COLD_BLOCKS
-#define GOME_COLD_BLOCKS 256
+#define GOME_COLD_BLOCKS 240  // leaves CUs free for the head plans' whole-CU blocks (launched later)
 #endif
-constexpr uint32_t COLD_BLOCKS = GOME_COLD_BLOCKS;  // persistent cold-kernel blocks  // candidates the legacy hot kernel may take (grid size)
+constexpr uint32_t COLD_BLOCKS = GOME_COLD_BLOCKS;  // persistent cold-kernel blocks
 constexpr uint32_t EVB_HOT = 256; // events per arena block (hot books)
 
 // Wave-uniform context of the book being matched.

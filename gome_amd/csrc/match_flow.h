@@ -146,7 +146,7 @@ struct FlowArgs {
   IgEnt* ig;
   uint32_t ig_cap;
   uint32_t* ig_bump;
-  uint32_t* toff;      // [MAX_FLOW + 2] per range: exclusive scan of the books' touch counts
+  uint32_t* toff;      // [MAX_FLOW + 16] per range (at tb): exclusive scan of the books' touch counts
   uint32_t* tcnt;      // head sort: [FL_HEAD][maxt][FL_CAP] per-tile level counts, then offsets
   Level* lvout;        // head write: [MAX_FLOW * FL_CAP] final level records
   uint32_t maxt;       // tiles per head book (log capacity / FL_TILE)
@@ -783,6 +783,8 @@ __device__ __forceinline__ void fl_plan_kernel(const Dev& D, const FlowArgs& F) 
 
 // The head's plan (the batch's critical path) and the tail's: distinct names for the profiles.
 __global__ __launch_bounds__(256) void k_flow_plan_head(Dev D, FlowArgs F) { fl_plan_kernel<true>(D, F); }
+// the other head books (planned on the tail's stream, beside the hottest)
+__global__ __launch_bounds__(256) void k_flow_plan_near(Dev D, FlowArgs F) { fl_plan_kernel<true>(D, F); }
 __global__ __launch_bounds__(64) void k_flow_plan_tail(Dev D, FlowArgs F) { fl_plan_kernel<false>(D, F); }
 
 __device__ __forceinline__ void fl_plan_book(const Dev& D, const FlowArgs& F, uint32_t h) {
@@ -1549,7 +1551,7 @@ __global__ __launch_bounds__(128) void k_flow_write_fin(Dev D, FlowArgs F) {
   for (uint32_t q = 1 + threadIdx.x; q <= hd.nl; q += blockDim.x) lv[q] = F.lvout[h * FL_CAP + q];
   __syncthreads();
   fl_write_finish(D, hd, lv, keep, base_s, cap_s, nout_s);
-  if (threadIdx.x == 0) {  // the head plan kernel's work (its roofline numerator)
+  if (threadIdx.x == 0 && F.h0 == 0) {  // k_flow_plan_head's work (its roofline numerator)
     atomicAdd(&D.st->ctr[C_FLOW_HEAD_ORDERS], static_cast<unsigned long long>(hd.end - hd.beg));
     atomicAdd(&D.st->ctr[C_FLOW_HEAD_TOUCHES], static_cast<unsigned long long>(hd.ntouch));
   }
@@ -1596,7 +1598,7 @@ __global__ __launch_bounds__(FL_TILE) void k_flow_sort_cnt(Dev D, FlowArgs F) {
     if (tid < FL_CAP) {
       uint32_t c = 0;
       for (uint32_t ww = 0; ww < FL_TILE_W; ++ww) c += wc[ww][tid];
-      F.tcnt[(static_cast<size_t>(hb) * F.maxt + tl) * FL_CAP + tid] = c;
+      F.tcnt[(static_cast<size_t>(h) * F.maxt + tl) * FL_CAP + tid] = c;  // (head books: h < FL_HEAD)
     }
     if (tid == 0 && nrest) atomicAdd(&F.hdr[h].rests, nrest);
     __syncthreads();
@@ -1611,7 +1613,7 @@ __global__ __launch_bounds__(FL_CAP) void k_flow_sort_scan(Dev D, FlowArgs F) {
   if (h >= fl_hend(D, F) || !F.hdr[h].ok) return;
   const uint32_t nt = F.hdr[h].ntouch, nl = F.hdr[h].nl;
   const uint32_t ntile = (nt + FL_TILE - 1) / FL_TILE;
-  uint32_t* tc = F.tcnt + static_cast<size_t>(hb) * F.maxt * FL_CAP;
+  uint32_t* tc = F.tcnt + static_cast<size_t>(h) * F.maxt * FL_CAP;
   uint32_t s = 0;
   uint32_t tl = 0;
   for (; tl + 8 <= ntile; tl += 8) {
@@ -1656,7 +1658,7 @@ __global__ __launch_bounds__(FL_TILE) void k_flow_sort_scatter(Dev D, FlowArgs F
   const uint32_t nt = F.hdr[h].ntouch, L = FL_TOUCH_MUL * F.hdr[h].beg;
   const unsigned long long g = F.hdr[h].g;
   const uint32_t ntile = (nt + FL_TILE - 1) / FL_TILE;
-  const uint32_t* tc = F.tcnt + static_cast<size_t>(hb) * F.maxt * FL_CAP;
+  const uint32_t* tc = F.tcnt + static_cast<size_t>(h) * F.maxt * FL_CAP;
   for (uint32_t i = tid; i < FL_TILE_W * FL_CAP; i += FL_TILE) wc[i / FL_CAP][i % FL_CAP] = 0;
   __syncthreads();
   for (uint32_t tl = blockIdx.x; tl < ntile; tl += gridDim.x) {

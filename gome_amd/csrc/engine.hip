@@ -317,10 +317,9 @@ gome_status gome_engine::run(const gome_order* d_ord, uint32_t n, hipStream_t s)
   HIPCHK(hipStreamWaitEvent(flow_stream, fork_adm, 0));
   HIPCHK(hipMemsetAsync(d_claim, 0, (adm_mask + 1ull) * 4, flow_stream));
   HIPCHK(hipMemsetAsync(d_amin, 0xFF, (adm_mask + 1ull) * 4, flow_stream));
-  k_adm<<<gN, T256, 0, flow_stream>>>(d_ord, n, d_claim, d_amin, d_adm_slot, adm_mask);
+  k_adm<<<gN, T256, 0, flow_stream>>>(d_ord, n, d_claim, d_amin, d_adm_slot, adm_mask, cfg.max_symbols, d_st);
   k_adm_flag<<<gN, T256, 0, flow_stream>>>(d_ord, n, d_adm_slot, d_amin);
   HIPCHK(hipEventRecord(adm_done, flow_stream));
-  k_validate<<<gN, T256, 0, s>>>(d_ord, n, cfg.max_symbols, d_st);
 
   // ---- stable radix sort of (symbol_id, seq)
   const uint32_t nblk = ceil_div(n, RS_TILE);

@@ -208,6 +208,10 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep(Dev D, BatchArgs B, Flo
   const uint32_t seg = B.seg_order[h];
   const uint32_t beg = B.seg_start[seg], end = B.seg_start[seg + 1];
   const uint32_t sym = B.ord[B.prep[beg].idx].symbol_id;
+  if (D.st->err & ERR_INPUT) {  // (the batch is rejected; sym may be out of range)
+    if (tid == 0) hd->ok = 0;
+    return;
+  }
   const Book bk = D.books[sym];
   for (uint32_t i = tid; i < FL_HASH; i += FL_PREP_T) { hkey[i] = 0; hval[i] = NIL; }
   if (tid == 0) {
@@ -527,6 +531,10 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep_b(Dev D, BatchArgs B, F
   const uint32_t seg = B.seg_order[h];
   const uint32_t beg = B.seg_start[seg], end = B.seg_start[seg + 1];
   const uint32_t sym = B.ord[B.prep[beg].idx].symbol_id;
+  if (D.st->err & ERR_INPUT) {  // (the batch is rejected; sym may be out of range)
+    if (tid == 0) hd->ok = 0;
+    return;
+  }
   const Book bk = D.books[sym];
   if (tid == 0) {
     ndist = nc = 0;

@@ -243,11 +243,18 @@ __global__ void k_seg_scatter(const uint32_t* seg_start, const Status* st, uint3
 // batch ingress model an ADD is admitted iff no earlier ADD/DEL of the batch carries
 // the same (S, uuid, oid).  claim[] holds the first claimant (seq+1) of a key's slot;
 // amin[] the smallest seq of the key.
+// Also validates the record (k_validate's check, folded in: one pass over the input).
 __global__ void k_adm(const gome_order* ord, uint32_t n, uint32_t* claim, uint32_t* amin,
-                      uint32_t* slot, uint32_t mask) {
+                      uint32_t* slot, uint32_t mask, uint32_t max_symbols, Status* st) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const gome_order g = ord[i];
+  {
+    const int64_t lim = 1ll << 53;
+    if (g.symbol_id >= max_symbols || g.volume_fx < 0 || g.volume_fx >= lim || g.price_fx <= -lim ||
+        g.price_fx >= lim)
+      atomicOr(&st->err, ERR_INPUT);
+  }
   if (g.action != GOME_ADD && g.action != GOME_DEL) { slot[i] = NIL; return; }
   uint32_t h = static_cast<uint32_t>(
       mix64((static_cast<unsigned long long>(g.symbol_id) << 40) ^

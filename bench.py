@@ -202,7 +202,7 @@ def main():
     balg = sum(algorithmic_bytes(s) for s in sts) / steps
     flow = sum(s["n_flow_books"] for s in sts) > 0
     if flow:  # the flow path's serial plan is the dominant kernel
-        kname = "k_flow_plan_head (serial aggregate plan of the longest flow books)"
+        kname = "k_flow_plan_head (serial aggregate plan of the hottest book)"
         ms_hot = sum(s["ms_flow_plan"] for s in sts) / steps
         bhot = sum(plan_algorithmic_bytes(s) for s in sts) / steps
     else:

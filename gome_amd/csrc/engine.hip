@@ -3,7 +3,8 @@
 // Replaces the reference's serial consumer (gomengine/engine/rabbitmq.go:116-125
 // calling engine.DoOrder, engine.go:46) with a per-batch device pipeline:
 //
-//   k_validate        domain check of the 32-B records (symbol range, volume >= 0, |v| < 2^53)
+//   (input domain check of the 32-B records — symbol range, volume >= 0, |v| < 2^53 — is
+//    done by k_adm, beside the radix sort)
 //   k_radix_hist/     stable LSD radix sort of (symbol_id, seq) -> per-symbol segments in
 //   k_radix_scatter   consume order (the reference is serial, so per-symbol order = arrival)
 //   k_seg_*           segment starts + longest-first launch order (hottest book starts first)
@@ -79,10 +80,10 @@ struct gome_engine {
   gome_config cfg{};
   hipStream_t stream = nullptr;
   hipStream_t hot_stream = nullptr;
-  hipStream_t flow_stream = nullptr, flow2_stream = nullptr;
+  hipStream_t flow_stream = nullptr;
   bool own_stream = false;
   hipEvent_t fork{}, join{}, evh0{}, evh1{};
-  hipEvent_t joinf{}, joinf2{}, prep_h{}, prep_t{}, evf0{}, evf1{}, fork_adm{}, adm_done{};
+  hipEvent_t joinf{}, prep_h{}, prep_t{}, evf0{}, evf1{}, fork_adm{}, adm_done{};
   FlowArgs F{};
   Prep* d_prep = nullptr;
   PendEnt* d_pend = nullptr;
@@ -147,12 +148,11 @@ struct gome_engine {
     if (evh0) { (void)hipEventDestroy(evh0); (void)hipEventDestroy(evh1); }
     if (evf0) {
       (void)hipEventDestroy(evf0); (void)hipEventDestroy(evf1); (void)hipEventDestroy(joinf);
-      (void)hipEventDestroy(joinf2); (void)hipEventDestroy(prep_h); (void)hipEventDestroy(prep_t);
+      (void)hipEventDestroy(prep_h); (void)hipEventDestroy(prep_t);
       (void)hipEventDestroy(fork_adm); (void)hipEventDestroy(adm_done);
     }
     if (hot_stream) (void)hipStreamDestroy(hot_stream);
     if (flow_stream) (void)hipStreamDestroy(flow_stream);
-    if (flow2_stream) (void)hipStreamDestroy(flow2_stream);
     if (own_stream && stream) (void)hipStreamDestroy(stream);
   }
 
@@ -193,8 +193,6 @@ gome_status gome_engine::init(const gome_config& c) {
   HIPCHK(hipEventCreate(&evh1));
   HIPCHK(hipStreamCreateWithFlags(&flow_stream, hipStreamNonBlocking));
   HIPCHK(hipEventCreateWithFlags(&joinf, hipEventDisableTiming));
-  HIPCHK(hipStreamCreateWithFlags(&flow2_stream, hipStreamNonBlocking));
-  HIPCHK(hipEventCreateWithFlags(&joinf2, hipEventDisableTiming));
   HIPCHK(hipEventCreateWithFlags(&prep_h, hipEventDisableTiming));
   HIPCHK(hipEventCreateWithFlags(&prep_t, hipEventDisableTiming));
   HIPCHK(hipEventCreate(&evf0));

@@ -58,6 +58,7 @@ CLOBBERS = [f"s{i}" for i in range(44, 101)] + ["v32", "v33", "v34", "v35"]
 PAIR = {"A": (32, 33), "B": (34, 35)}
 ZERO = "s91"                     # W32: stays 0, the high word of the rest amount s[90:91]
 COPY_REST = os.environ.get("GOME_PLAN_COPY", "0") == "1"   # measured: no gain, 1.35x code
+LOOP_OFS = int(os.environ.get("GOME_PLAN_OFS", "0"))  # 4-byte words after the 256-B alignment
 PF_DIST = int(os.environ.get("GOME_PLAN_PF", "0"))  # L2 prefetch distance in bytes (0: off);
 # k_flow_prep pads ord8 by FL_ORD8_PAD records, which must cover it
 
@@ -553,6 +554,12 @@ class Gen:
             self.highest_bid()
             self.promote(BB, BBD, "B")
         e(f"s_load_dwordx16 s[44:59], {ADDR}, 0x0")
+        # pin the loop's placement: the lone-wave fetch is sensitive to where the hand-made
+        # stream sits (a shift of the same code by a few bytes moved the hottest book's plan
+        # from 80 to 101 ns per order), so align it and pad to the measured best offset
+        e(".p2align 8")
+        for _ in range(LOOP_OFS):
+            e("s_nop 0")
         if PF_DIST:
             e("s_mov_b64 exec, 1")
             for off in range(64, PF_DIST, 64):

@@ -162,17 +162,6 @@ __global__ __launch_bounds__(RS_T) void k_radix_scatter(const gome_order* ord,
   }
 }
 
-// ============================================================== validation
-__global__ void k_validate(const gome_order* ord, uint32_t n, uint32_t max_symbols, Status* st) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const gome_order o = ord[i];
-  const int64_t lim = 1ll << 53;
-  bool bad = o.symbol_id >= max_symbols || o.volume_fx < 0 || o.volume_fx >= lim ||
-             o.price_fx <= -lim || o.price_fx >= lim;
-  if (bad) atomicOr(&st->err, ERR_INPUT);
-}
-
 // ============================================================== segments
 __global__ void k_seg_flags(const uint32_t* skeys, uint32_t n, uint32_t* flags) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;

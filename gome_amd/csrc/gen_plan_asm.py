@@ -57,7 +57,7 @@ CLOBBERS = [f"s{i}" for i in range(44, 101)] + ["v32", "v33", "v34", "v35"]
 # word): asks in v[32:33], bids in v[34:35] (fixed registers: the pair must be consecutive).
 PAIR = {"A": (32, 33), "B": (34, 35)}
 ZERO = "s91"                     # W32: stays 0, the high word of the rest amount s[90:91]
-COPY_REST = os.environ.get("GOME_PLAN_COPY", "0") == "1"   # measured: no gain, 1.35x code
+COPY_REST = os.environ.get("GOME_PLAN_COPY", "1") == "1"   # measured at a pinned placement: -2% cycles
 LOOP_OFS = int(os.environ.get("GOME_PLAN_OFS", "0"))  # 4-byte words after the 256-B alignment
 PF_DIST = int(os.environ.get("GOME_PLAN_PF", "0"))  # L2 prefetch distance in bytes (0: off);
 # k_flow_prep pads ord8 by FL_ORD8_PAD records, which must cover it

@@ -83,7 +83,7 @@ struct gome_engine {
   hipStream_t flow_stream = nullptr;
   bool own_stream = false;
   hipEvent_t fork{}, join{}, evh0{}, evh1{};
-  hipEvent_t joinf{}, prep_h{}, prep_t{}, evf0{}, evf1{}, fork_adm{}, adm_done{};
+  hipEvent_t joinf{}, prep_h{}, prep_t{}, evf0{}, evf1{}, fork_adm{}, adm_done{}, seg_done{};
   FlowArgs F{};
   Prep* d_prep = nullptr;
   PendEnt* d_pend = nullptr;
@@ -149,7 +149,7 @@ struct gome_engine {
     if (evf0) {
       (void)hipEventDestroy(evf0); (void)hipEventDestroy(evf1); (void)hipEventDestroy(joinf);
       (void)hipEventDestroy(prep_h); (void)hipEventDestroy(prep_t);
-      (void)hipEventDestroy(fork_adm); (void)hipEventDestroy(adm_done);
+      (void)hipEventDestroy(fork_adm); (void)hipEventDestroy(adm_done); (void)hipEventDestroy(seg_done);
     }
     if (hot_stream) (void)hipStreamDestroy(hot_stream);
     if (flow_stream) (void)hipStreamDestroy(flow_stream);
@@ -199,6 +199,7 @@ gome_status gome_engine::init(const gome_config& c) {
   HIPCHK(hipEventCreate(&evf1));
   HIPCHK(hipEventCreateWithFlags(&fork_adm, hipEventDisableTiming));
   HIPCHK(hipEventCreateWithFlags(&adm_done, hipEventDisableTiming));
+  HIPCHK(hipEventCreateWithFlags(&seg_done, hipEventDisableTiming));
   HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_match_hot),
                              hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(HOT_LDS_BYTES)));
 
@@ -355,12 +356,6 @@ gome_status gome_engine::run(const gome_order* d_ord, uint32_t n, hipStream_t s)
   k_seg_bscan<<<1, 64, 0, s>>>(d_bcnt, d_bcnt + 32, d_st, FLOW_MIN_LOG2, MAX_FLOW);
   k_seg_scatter<<<gN, T256, 0, s>>>(d_seg_start, d_st, d_bcnt + 32, d_seg_order);
 
-  // ---- admission markers (k_adm, launched above on the flow stream)
-  HIPCHK(hipStreamWaitEvent(s, adm_done, 0));
-  k_prep<<<gN, T256, 0, s>>>(d_ord, n, sidx, d_adm_slot, d_prep);
-
-  // ---- match_books: one wavefront per book; hot books (LDS) on a second stream,
-  //      concurrently with the cold books (HBM)
   BatchArgs B;
   B.prep = d_prep;
   B.ord = d_ord;
@@ -370,11 +365,10 @@ gome_status gome_engine::run(const gome_order* d_ord, uint32_t n, hipStream_t s)
   B.arena = d_arena;
   B.arena_cap = arena_cap;
   B.ev_count = d_ev_count;
+  B.sidx = sidx;
+  B.adm_flag = d_adm_slot;
   const uint32_t grid = std::min<uint32_t>(n, cfg.max_symbols);
   const uint32_t nhot_max = std::min<uint32_t>(MAX_FLOW, grid);
-  HIPCHK(hipEventRecord(evm0, s));
-  HIPCHK(hipMemsetAsync(F.ig_bump, 0, 4, s));
-  HIPCHK(hipEventRecord(fork, s));
   // flow path: the head (longest FL_HEAD candidates, the batch's critical path) and the tail
   // each run prep -> serial plan -> parallel reconstruction on their own stream, so the
   // hottest book's plan starts after its own prep and the tail overlaps it
@@ -389,7 +383,10 @@ gome_status gome_engine::run(const gome_order* d_ord, uint32_t n, hipStream_t s)
   const uint32_t nh_head = std::min<uint32_t>(FL_HEAD, nhot_max);
   const uint32_t nh_near = nh_head > 1 ? nh_head - 1 : 0;
   const uint32_t nh_tail = nhot_max > FL_HEAD ? nhot_max - FL_HEAD : 0;
-  HIPCHK(hipStreamWaitEvent(flow_stream, fork, 0));
+  // the head's prep gathers through the sort permutation (prep_at): it starts right after
+  // segmentation, beside k_prep
+  HIPCHK(hipEventRecord(seg_done, s));
+  HIPCHK(hipStreamWaitEvent(flow_stream, seg_done, 0));
   HIPCHK(hipMemsetAsync(F.pscr, 0, sizeof(FlPrepScr) * FL_HEAD, flow_stream));
   k_flow_prep_a<<<dim3(FL_PG, nh_head), FL_PREP_T, 0, flow_stream>>>(D, B, FH);
   k_flow_prep_b<<<nh_head, FL_PREP_T, 0, flow_stream>>>(D, B, FH);
@@ -398,6 +395,16 @@ gome_status gome_engine::run(const gome_order* d_ord, uint32_t n, hipStream_t s)
   HIPCHK(hipEventRecord(evf0, flow_stream));
   k_flow_plan_head<<<1, 256, 0, flow_stream>>>(D, FH0);
   HIPCHK(hipEventRecord(evf1, flow_stream));
+  // ---- admission markers (k_adm, launched above on the flow stream)
+  HIPCHK(hipStreamWaitEvent(s, adm_done, 0));
+
+  // ---- match_books: one wavefront per book; hot books (LDS) on a second stream,
+  //      concurrently with the cold books (HBM)
+  k_prep<<<gN, T256, 0, s>>>(d_ord, n, sidx, d_adm_slot, d_prep);
+  HIPCHK(hipEventRecord(evm0, s));
+  HIPCHK(hipMemsetAsync(F.ig_bump, 0, 4, s));
+  HIPCHK(hipEventRecord(fork, s));
+  HIPCHK(hipStreamWaitEvent(flow_stream, fork, 0));  // (k_prep, the gather bump)
   // the hottest book's reconstruction: wide kernels (tile-parallel sort, one wave per level)
   auto head_recon = [&](const FlowArgs& R, uint32_t nb, hipStream_t st) {
     k_flow_sort_cnt<<<dim3(FL_SORT_GRID, nb), FL_TILE, 0, st>>>(D, R);

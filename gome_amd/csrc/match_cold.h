@@ -20,7 +20,27 @@ struct BatchArgs {
   gome_event* arena;          // per-wave event blocks, compacted afterwards
   uint32_t arena_cap;
   uint32_t* ev_count;         // events per batch index
+  const uint32_t* sidx;       // segment position -> batch index (the radix sort's permutation)
+  const uint32_t* adm_flag;   // per batch index: admitted ADD (k_adm_flag)
 };
+
+// The Prep record of segment position b built from the input (what k_prep writes to
+// prep[b]), for the head's prep which runs before k_prep finishes.
+__device__ __forceinline__ Prep prep_at(const BatchArgs& B, uint32_t b) {
+  const uint32_t j = B.sidx[b];
+  const gome_order o = B.ord[j];
+  Prep q;
+  q.price = o.price_fx;
+  q.vol = o.volume_fx;
+  q.oid = o.oid_id;
+  q.uuid = o.uuid_id;
+  q.idx = j;
+  q.side = o.side;
+  q.action = o.action;
+  q.adm = static_cast<uint8_t>(B.adm_flag[j]);
+  q.pad = 0;
+  return q;
+}
 
 constexpr uint32_t EVB = 32;      // events per arena block (cold books)
 

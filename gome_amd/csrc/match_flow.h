@@ -477,7 +477,7 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep_a(Dev D, BatchArgs B, F
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const uint32_t b = c0 + u * FL_PREP_T;
-      if (b < b1) qs[u] = B.prep[b];
+      if (b < b1) qs[u] = prep_at(B, b);
       else qs[u].action = 0;
     }
 #pragma unroll
@@ -530,7 +530,7 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep_b(Dev D, BatchArgs B, F
   FlPrepScr* P = F.pscr + hb;
   const uint32_t seg = B.seg_order[h];
   const uint32_t beg = B.seg_start[seg], end = B.seg_start[seg + 1];
-  const uint32_t sym = B.ord[B.prep[beg].idx].symbol_id;
+  const uint32_t sym = B.ord[B.sidx[beg]].symbol_id;
   if (D.st->err & ERR_INPUT) {  // (the batch is rejected; sym may be out of range)
     if (tid == 0) hd->ok = 0;
     return;
@@ -665,7 +665,7 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep_c(Dev D, BatchArgs B, F
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const uint32_t b = c0 + u * FL_PREP_T;
-      if (b < b1) qs[u] = B.prep[b];
+      if (b < b1) qs[u] = prep_at(B, b);
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {

@@ -83,7 +83,7 @@ struct gome_engine {
   hipStream_t flow_stream = nullptr;
   bool own_stream = false;
   hipEvent_t fork{}, join{}, evh0{}, evh1{};
-  hipEvent_t joinf{}, prep_h{}, prep_t{}, evf0{}, evf1{}, fork_adm{}, adm_done{}, seg_done{};
+  hipEvent_t joinf{}, prep_h{}, prep_t{}, evf0{}, evf1{}, fork_adm{}, adm_done{}, seg_done{}, ev_scan{}, ev_hot{};
   FlowArgs F{};
   Prep* d_prep = nullptr;
   PendEnt* d_pend = nullptr;
@@ -150,6 +150,7 @@ struct gome_engine {
       (void)hipEventDestroy(evf0); (void)hipEventDestroy(evf1); (void)hipEventDestroy(joinf);
       (void)hipEventDestroy(prep_h); (void)hipEventDestroy(prep_t);
       (void)hipEventDestroy(fork_adm); (void)hipEventDestroy(adm_done); (void)hipEventDestroy(seg_done);
+      (void)hipEventDestroy(ev_scan); (void)hipEventDestroy(ev_hot);
     }
     if (hot_stream) (void)hipStreamDestroy(hot_stream);
     if (flow_stream) (void)hipStreamDestroy(flow_stream);
@@ -200,6 +201,8 @@ gome_status gome_engine::init(const gome_config& c) {
   HIPCHK(hipEventCreateWithFlags(&fork_adm, hipEventDisableTiming));
   HIPCHK(hipEventCreateWithFlags(&adm_done, hipEventDisableTiming));
   HIPCHK(hipEventCreateWithFlags(&seg_done, hipEventDisableTiming));
+  HIPCHK(hipEventCreateWithFlags(&ev_scan, hipEventDisableTiming));
+  HIPCHK(hipEventCreateWithFlags(&ev_hot, hipEventDisableTiming));
   HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_match_hot),
                              hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(HOT_LDS_BYTES)));
 
@@ -462,8 +465,13 @@ gome_status gome_engine::run(const gome_order* d_ord, uint32_t n, hipStream_t s)
 
   // ---- event compaction into publish order
   scan(d_ev_count, n, d_ev_off, &d_st->n_events, s);
+  // the hottest book's events and the arena scatter fill disjoint slots: run them side by side
+  HIPCHK(hipEventRecord(ev_scan, s));
+  HIPCHK(hipStreamWaitEvent(flow_stream, ev_scan, 0));
+  k_flow_events<<<1024, 256, 0, flow_stream>>>(D, B, FH0, d_ev_off, d_events);
+  HIPCHK(hipEventRecord(ev_hot, flow_stream));
   k_ev_scatter<<<2048, T256, 0, s>>>(d_arena, arena_cap, d_st, d_ev_off, d_events);
-  k_flow_events<<<1024, 256, 0, s>>>(D, B, FH0, d_ev_off, d_events);
+  HIPCHK(hipStreamWaitEvent(s, ev_hot, 0));
   k_recycle_copy<<<256, 256, 0, s>>>(D);
   k_recycle_fin<<<1, 64, 0, s>>>(D);
   HIPCHK(hipGetLastError());

@@ -55,11 +55,11 @@ def main(tag, src):
                    "note": "rocprofv3 PMC, separate passes, KiB->bytes; FETCH_SIZE not x2-corrected"},
                   open(os.path.join(os.path.dirname(__file__), "traffic.json"), "w"), indent=1)
     tr = rows(os.path.join(src, "trace", "run_kernel_trace.csv"))
-    starts = [int(r["Start_Timestamp"]) for r in tr if r["Kernel_Name"].startswith("k_validate")]
-    if starts:  # timeline of the last batch (batches start with k_validate)
-        t0 = max(starts)
+    starts = [int(r["Start_Timestamp"]) for r in tr if r["Kernel_Name"].startswith("k_adm")]
+    if starts:  # timeline of the last batch (k_adm and the radix sort open every batch)
+        t0 = max(starts) - 20000
         last = sorted((r for r in tr if int(r["Start_Timestamp"]) >= t0), key=lambda r: int(r["Start_Timestamp"]))
-        out += ["", "Timeline of the last batch (ms from its first kernel; queue = HIP stream's HW queue):", "",
+        out += ["", "Timeline of the last batch (ms from its admission kernel - 20 us; queue = HIP stream's HW queue):", "",
                 "| kernel | queue | start | end | dur |", "|---|---|---|---|---|"]
         for r in last:
             a0, a1 = (int(r["Start_Timestamp"]) - t0) / 1e6, (int(r["End_Timestamp"]) - t0) / 1e6

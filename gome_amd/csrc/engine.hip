@@ -400,6 +400,9 @@ gome_status gome_engine::run(const gome_order* d_ord, uint32_t n, hipStream_t s)
   HIPCHK(hipEventRecord(evf1, flow_stream));
   // ---- admission markers (k_adm, launched above on the flow stream)
   HIPCHK(hipStreamWaitEvent(s, adm_done, 0));
+  // k_prep gathers the same records as the head's prep: let the head's prep (the critical
+  // path) have the memory system first; the cold books have slack
+  HIPCHK(hipStreamWaitEvent(s, prep_h, 0));
 
   // ---- match_books: one wavefront per book; hot books (LDS) on a second stream,
   //      concurrently with the cold books (HBM)

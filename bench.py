@@ -1,16 +1,24 @@
 """bench.py — matched orders/sec of the MI355X batch matching engine (BASELINE.json metric).
 
-Workload (BASELINE.json configs[2], the config the metric is quoted on): 100k symbols,
-symbol rank ~ Zipf(s=1.0), doorder.go price/volume distribution (2-dp prices in
-(0, 1], 2-dp volumes), ADD-only, synthetic and seeded.  One step = one batch of
-`--batch` orders per GPU applied end to end on the device (validate + radix sort by
-symbol + admission + match_books + event compaction), records already resident in HBM.
+Workloads (BASELINE.json configs; `--workload`):
+  config3 (default, the config the metric is quoted on): 100k symbols, symbol rank ~
+          Zipf(s=1.0), doorder.go price/volume distribution (2-dp prices in (0, 1], 2-dp
+          volumes), ADD-only.
+  config4: config 3's symbols with the cancel-heavy mix: 50% DELs (each re-sends a uniformly
+          chosen earlier ADD no DEL targeted yet, delorder.go), 10% of ADDs aggressive (BUY @
+          1.00 / SALE @ 0.01, volume k * 10.00, k ~ U{1..16}).
+  config5: 1M symbols, Zipf(1.0), 4-dp price grid (deep books, up to 10k levels), 2-dp volumes.
+All synthetic and seeded.  One step = one batch of `--batch` orders per GPU applied end to end
+on the device (validate + radix sort by symbol + admission + match_books + event compaction),
+records already resident in HBM: that is `value`.  `e2e` then runs the same workload from
+host memory through the pipelined path (gome_submit_batch_async / gome_collect: H2D of batch
+k+1 and D2H of batch k-1's events overlap batch k's matching) — SURVEY §8d's primary metric.
 
-Multi-GPU (one process per GPU, torchrun): symbols are sharded round-robin over Zipf
-rank (rank r owns symbols whose Zipf rank % N == r), so every rank processes its own
-symbols' orders with no data-path collective (weak scaling: the global stream has
-N * batch orders per step).  The only collective is a per-step all_gather of a 32-word
-per-GPU summary for the publisher (RCCL over xGMI).
+Multi-GPU (one process per GPU, torchrun): symbols are sharded round-robin over Zipf rank
+(rank r owns symbols whose Zipf rank % N == r), so every rank processes its own symbols'
+orders with no data-path collective (weak scaling: the global stream has N * batch orders per
+step).  The only collective is a per-step all_gather of a 32-word per-GPU summary consumed by
+the rank-0 publisher (gome_amd/publisher.py; RCCL over xGMI).
 
 Prints ONE JSON line on rank 0.
 """
@@ -20,6 +28,7 @@ import argparse
 import json
 import os
 import sys
+import threading
 import time
 
 import numpy as np
@@ -28,13 +37,25 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from gome_amd import workload as wl  # noqa: E402
+from gome_amd.publisher import SUMMARY_WORDS, SummaryPublisher, pack_summary  # noqa: E402
 
 METRIC = "matched orders/sec (node) at 100k symbols; p99 batch match latency; HBM GB/s"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 
+WORKLOADS = {
+    "config3": dict(symbols=100000, zipf=1.0, decimals=2, del_frac=0.0, aggr=0.0,
+                    desc="config3: {symbols} symbols, Zipf(s={zipf}) symbol rank, doorder 2-dp price/volume, ADD-only"),
+    "config4": dict(symbols=100000, zipf=1.0, decimals=2, del_frac=0.5, aggr=0.1,
+                    desc="config4: {symbols} symbols, Zipf(s={zipf}), 50% DEL of earlier ADDs (delorder), "
+                         "10% aggressive ADDs (BUY@1.00 / SALE@0.01, k*10.00), doorder 2-dp"),
+    "config5": dict(symbols=1000000, zipf=1.0, decimals=4, del_frac=0.0, aggr=0.0,
+                    desc="config5: {symbols} symbols, Zipf(s={zipf}), 4-dp price grid (deep books), "
+                         "2-dp volumes, ADD-only"),
+}
+
 
 def algorithmic_bytes(st: dict) -> int:
-    """Bytes match_books must move per launch (DESIGN.md §Roofline):
+    """Bytes match_books must move per launch (DESIGN.md §5, SURVEY §8d):
     32 B per input record read, 64 B per event written, 24 B node write + 16 B index
     entry per resting order, 24 B node read per maker filled, 40 B (index probe + node)
     per cancel hit.  Level aggregates are not counted."""
@@ -43,10 +64,19 @@ def algorithmic_bytes(st: dict) -> int:
 
 
 def hot_algorithmic_bytes(st: dict) -> int:
-    """The same per-unit figures restricted to the work done inside k_match_hot."""
+    """The same per-unit figures restricted to the work done inside k_match_hot / the flow path."""
     ev = st["n_hot_fills"] + st["n_hot_cancels"]
     return (32 * st["n_hot_orders"] + 64 * ev + 40 * st["n_hot_rests"]
             + 24 * st["n_hot_fills"] + 40 * st["n_hot_cancels"])
+
+
+def cold_algorithmic_bytes(st: dict) -> int:
+    """The same per-unit figures for k_match (every book neither hot path applied)."""
+    o = st["n_orders"] - st["n_hot_orders"]
+    f = st["n_fills"] - st["n_hot_fills"]
+    c = st["n_cancels"] - st["n_hot_cancels"]
+    r = st["n_rests"] - st["n_hot_rests"]
+    return 32 * o + 64 * (f + c) + 40 * r + 24 * f + 40 * c
 
 
 def plan_algorithmic_bytes(st: dict) -> int:
@@ -55,7 +85,7 @@ def plan_algorithmic_bytes(st: dict) -> int:
     return 8 * st["n_flow_head_orders"] + 16 * st["n_flow_head_touches"]
 
 
-def shard_stream(n_symbols, zipf_s, rank, world, seed):
+def shard_stream(n_symbols, zipf_s, rank, world, seed, price_decimals=2):
     """Generator of this rank's share of the global Zipf stream (conditional sampling
     over the ranks this GPU owns; equal in law to filtering the global stream)."""
     z = wl.ZipfSymbols(n_symbols, zipf_s)
@@ -71,7 +101,7 @@ def shard_stream(n_symbols, zipf_s, rank, world, seed):
     def batch(n):
         rec = np.zeros(n, wl.ORDER_DTYPE)
         rec["symbol_id"] = ids[np.searchsorted(cdf, rng.random(n), side="right")]
-        rec["price_fx"] = wl.doorder_prices(rng, n)
+        rec["price_fx"] = wl.doorder_prices(rng, n, price_decimals)
         rec["volume_fx"] = wl.doorder_volumes(rng, n)
         rec["side"] = rng.integers(0, 2, n, dtype=np.uint8)
         rec["action"] = wl.ADD
@@ -81,6 +111,16 @@ def shard_stream(n_symbols, zipf_s, rank, world, seed):
         return rec
 
     return batch, share, float(p[0])
+
+
+def make_stream(workload, rank, world, seed):
+    """(batch(n) -> records, owned share, top-symbol share) of this rank's stream."""
+    W = WORKLOADS[workload]
+    if workload == "config3":  # the numpy stream round 1's headline was measured on
+        return shard_stream(W["symbols"], W["zipf"], rank, world, seed)
+    ns = wl.NativeStream(W["symbols"], W["zipf"], seed=seed, price_decimals=W["decimals"],
+                         del_frac=W["del_frac"], aggressive_frac=W["aggr"], rank=rank, world=world)
+    return ns.batch, ns.owned_share, ns.top_share
 
 
 def combine_ranks(orders, fills, events, elapsed, lat, device):
@@ -99,29 +139,52 @@ def combine_ranks(orders, fills, events, elapsed, lat, device):
     return o, f, ev, float(e.item()), lt.tolist()
 
 
-def gather_summary(st, summary, gathered):
+def gather_summary(st, summary, gathered, rank=0, step=0):
     """Per-GPU trade/depth summary to every rank (the publisher feed)."""
     import torch.distributed as dist
-    summary.zero_()
-    summary[0] = st["n_orders"]; summary[1] = st["n_fills"]; summary[2] = st["n_events"]
-    summary[3] = st["n_resting"]; summary[4] = st["max_segment"]
+    pack_summary(st, rank, step, summary)
     dist.all_gather_into_tensor(gathered, summary)
     return gathered
 
 
-def cpu_baseline(batches, n_symbols, budget_s):
-    """C oracle (oracle/gome_oracle.c, 1 thread) on the first batches of this rank's stream."""
+def cpu_baseline(batches, n_symbols, budget_s, threads=1):
+    """C oracle (oracle/gome_oracle.c) on the first batches of this rank's stream: 1 thread for
+    up to budget_s, then the same batches symbol-sharded over `threads` threads (one oracle per
+    thread; books never interact; ctypes calls release the GIL)."""
     from oracle.pyoracle import Oracle
     orc = Oracle(n_symbols)
-    done, t_cpu = 0, 0.0
+    done, t_cpu, used = 0, 0.0, 0
     for b in batches:
         t = time.perf_counter()
         orc.submit(b)
         t_cpu += time.perf_counter() - t
         done += len(b)
+        used += 1
         if t_cpu >= budget_s:
             break
-    return done / t_cpu, done, t_cpu
+    one = (done / t_cpu, done, t_cpu, used)
+    if threads <= 1:
+        return one, None
+    parts = [[b[(b["symbol_id"] % threads) == k] for b in batches[:used]] for k in range(threads)]
+    orcs = [Oracle(n_symbols) for _ in range(threads)]
+
+    def run(k):
+        for p in parts[k]:
+            orcs[k].submit(p)
+
+    ths = [threading.Thread(target=run, args=(k,)) for k in range(threads)]
+    t = time.perf_counter()
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    wall = time.perf_counter() - t
+    return one, (done / wall, done, wall, used)
+
+
+def pctl(xs, q):
+    s = sorted(xs)
+    return s[min(len(s) - 1, max(0, int(np.ceil(q * len(s))) - 1))]
 
 
 def main():
@@ -130,13 +193,15 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=1 << 22, help="orders per GPU per step")
-    ap.add_argument("--symbols", type=int, default=100000)
-    ap.add_argument("--zipf", type=float, default=1.0)
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="config3")
     ap.add_argument("--seed", type=int, default=42)
+    ap.add_argument("--e2e-steps", type=int, default=-1,
+                    help="timed steps of the host-to-host pipelined path (-1: = --steps, 0: off)")
     ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of CPU-baseline work")
+    ap.add_argument("--cpu-threads", type=int, default=8, help="threads of the sharded CPU baseline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
-                    help="PMC-measured HBM bytes per match_books launch (optional)")
+                    help="PMC-measured HBM bytes per launch of the dominant kernel (optional)")
     args = ap.parse_args()
 
     import torch
@@ -155,27 +220,40 @@ def main():
 
     from gome_amd.abi import Engine
 
+    W = WORKLOADS[args.workload]
+    n_symbols = W["symbols"]
     steps, warm = args.steps, args.warmup
-    gen, share, top_share = shard_stream(args.symbols, args.zipf, rank, world, args.seed)
+    e2e_steps = steps if args.e2e_steps < 0 else args.e2e_steps
+    e2e_warm = 2 if e2e_steps else 0
+    gen, share, top_share = make_stream(args.workload, rank, world, args.seed)
     per_rank = int(round(args.batch * world * share))
-    host_batches = [gen(per_rank) for _ in range(warm + steps)]
+    host_batches = [gen(per_rank).copy() for _ in range(warm + steps)]
     dev_batches = [torch.from_numpy(b.view(np.uint8)).cuda() for b in host_batches]
     torch.cuda.synchronize()
 
-    total_orders = per_rank * (warm + steps)
-    eng = Engine(max_symbols=args.symbols, max_batch=per_rank,
-                 max_nodes=max(1 << 20, int(total_orders * 0.3)),
-                 max_levels=max(1 << 22, 256 * args.symbols), device=local)
+    total_orders = per_rank * (warm + steps + e2e_warm + e2e_steps)
+    keep = 0.3 if args.workload == "config3" else 0.5
+    eng = Engine(max_symbols=n_symbols, max_batch=per_rank,
+                 max_nodes=max(1 << 20, int(total_orders * keep)),
+                 max_levels=max(1 << 22, 64 * n_symbols), device=local)
 
-    summary = torch.zeros(32, dtype=torch.int64, device="cuda")
-    gathered = torch.zeros(32 * world, dtype=torch.int64, device="cuda")
+    summary = torch.zeros(SUMMARY_WORDS, dtype=torch.int64, device="cuda")
+    gathered = torch.zeros(SUMMARY_WORDS * world, dtype=torch.int64, device="cuda")
+    pub = SummaryPublisher(world) if rank == 0 else None
+    seq = [0]
+
+    def publish(st, i):
+        if world > 1:  # per-GPU trade/depth summary to the publisher (RCCL all_gather)
+            gather_summary(st, summary, gathered, rank, i)
+            if pub is not None:
+                pub.consume(gathered)
 
     def step(i):
         b = dev_batches[i]
-        eng.submit_device(b.data_ptr(), per_rank, seq_base=i * per_rank)
+        eng.submit_device(b.data_ptr(), per_rank, seq_base=seq[0])
+        seq[0] += per_rank
         st = eng.stats()
-        if world > 1:  # per-GPU trade/depth summary to the publisher (RCCL all_gather)
-            gather_summary(st, summary, gathered)
+        publish(st, i)
         return st
 
     for i in range(warm):
@@ -183,6 +261,8 @@ def main():
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
+    if pub is not None:
+        pub = SummaryPublisher(world)  # the timed steps only
     lat, sts = [], []
     t0 = time.perf_counter()
     for i in range(warm, warm + steps):
@@ -197,45 +277,108 @@ def main():
     orders = sum(s["n_orders"] for s in sts)
     fills = sum(s["n_fills"] for s in sts)
     events = sum(s["n_events"] for s in sts)
+    cancels = sum(s["n_cancels"] for s in sts)
     ms_match = sum(s["ms_match"] for s in sts) / steps
     ms_total = sum(s["ms_total"] for s in sts) / steps
     balg = sum(algorithmic_bytes(s) for s in sts) / steps
-    flow = sum(s["n_flow_books"] for s in sts) > 0
-    if flow:  # the flow path's serial plan is the dominant kernel
-        kname = "k_flow_plan_head (serial aggregate plan of the hottest book)"
-        ms_hot = sum(s["ms_flow_plan"] for s in sts) / steps
-        bhot = sum(plan_algorithmic_bytes(s) for s in sts) / steps
-    else:
-        kname = "k_match_hot (match_books, hot books)"
-        ms_hot = sum(s["ms_hot"] for s in sts) / steps
-        bhot = sum(hot_algorithmic_bytes(s) for s in sts) / steps
+    # the dominant kernel: the longest of the hottest book's plan, the legacy hot kernel and
+    # the cold kernel (they run concurrently; the longest bounds the batch)
+    cands = {
+        "k_flow_plan_head": (sum(s["ms_flow_plan"] for s in sts) / steps,
+                             sum(plan_algorithmic_bytes(s) for s in sts) / steps,
+                             "serial aggregate plan of the hottest book"),
+        "k_match_hot": (sum(s["ms_hot"] for s in sts) / steps,
+                        sum(hot_algorithmic_bytes(s) for s in sts) / steps,
+                        "match_books, legacy hot books"),
+        "k_match": (sum(s["ms_cold"] for s in sts) / steps,
+                    sum(cold_algorithmic_bytes(s) for s in sts) / steps,
+                    "match_books, cold books"),
+    }
+    if sum(s["n_flow_books"] for s in sts) == 0:
+        cands.pop("k_flow_plan_head")
+    kname = max(cands, key=lambda k: cands[k][0])
+    ms_dom, bdom, kdesc = cands[kname]
     max_seg = max(s["max_segment"] for s in sts)
     if world > 1:
-        orders, fills, events, elapsed, lat = combine_ranks(orders, fills, events, elapsed, lat, "cuda")
+        g_orders, g_fills, g_events, elapsed, lat = combine_ranks(orders, fills, events, elapsed, lat, "cuda")
+    else:
+        g_orders, g_fills, g_events = orders, fills, events
+
+    # ---- end to end from host memory (pipelined submit / collect)
+    e2e = None
+    if e2e_steps:
+        bufs = [eng.host_buffer(per_rank) for _ in range(e2e_warm + e2e_steps)]
+        for b in bufs:
+            b[:] = gen(per_rank)
+        done_ev = [0]
+
+        def run_pipe(lo, hi, lats):
+            tsub = {}
+            for k in range(lo, hi):
+                tsub[k] = time.perf_counter()
+                eng.submit_async(bufs[k], seq_base=seq[0])
+                seq[0] += per_rank
+                if k > lo:
+                    ev, st = eng.collect(copy=False)
+                    done_ev[0] += len(ev)
+                    lats.append((time.perf_counter() - tsub[k - 1]) * 1e3)
+            ev, st = eng.collect(copy=False)
+            done_ev[0] += len(ev)
+            lats.append((time.perf_counter() - tsub[hi - 1]) * 1e3)
+
+        run_pipe(0, e2e_warm, [])
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        elat = []
+        done_ev[0] = 0
+        t1 = time.perf_counter()
+        run_pipe(e2e_warm, e2e_warm + e2e_steps, elat)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        e_el = time.perf_counter() - t1
+        e_orders, e_events = per_rank * e2e_steps, done_ev[0]
+        if world > 1:
+            e_orders, _, e_events, e_el, elat = combine_ranks(e_orders, 0.0, e_events, e_el, elat, "cuda")
+        e2e = {"value": round(e_orders / e_el, 1), "unit": "orders/s", "steps": e2e_steps,
+               "ms_per_step": round(e_el / e2e_steps * 1e3, 3),
+               "p50_batch_ms": round(pctl(elat, 0.5), 3), "p99_batch_ms": round(pctl(elat, 0.99), 3),
+               "events_per_s": round(e_events / e_el, 1),
+               "pcie_bytes_per_step": int(32 * per_rank * world + 64 * e_events / e2e_steps),
+               "path": "host records -> gome_submit_batch_async (H2D on a copy stream) -> device "
+                       "pipeline -> gome_collect (events D2H into page-locked memory); batch k+1's "
+                       "H2D and batch k-1's D2H overlap batch k"}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        v, done, t_cpu = cpu_baseline(host_batches, args.symbols, args.cpu_budget)
-        cpu = {"value": round(v, 1), "unit": "orders/s", "cores": 1, "kind": "port",
+        thr = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+        one, many = cpu_baseline(host_batches, n_symbols, args.cpu_budget, thr)
+        v1, done, t_cpu, used = one
+        cpu = {"value": round(v1, 1), "unit": "orders/s", "cores": 1, "kind": "port",
                "sample": f"oracle/gome_oracle.c (1 thread) on the first {done} orders "
-                         f"({done // per_rank} batches) of the same rank-0 stream, {t_cpu:.1f} s"}
+                         f"({used} batches) of the same rank-0 stream, {t_cpu:.1f} s",
+               "reference": "not runnable here: no Go toolchain, Redis or RabbitMQ on the box "
+                            "(BASELINE.md; the reference's CPU path is Go + Redis + RabbitMQ)"}
+        if many is not None:
+            cpu["sharded"] = {"value": round(many[0], 1), "unit": "orders/s", "cores": thr,
+                              "sample": f"same {done} orders, symbol-sharded over {thr} threads "
+                                        f"(one oracle per thread), {many[2]:.2f} s"}
 
     traffic = None
     if os.path.exists(args.traffic_json):
         try:
             tj = json.load(open(args.traffic_json))
-            traffic = tj.get("k_flow_plan_head_hbm_bytes_per_launch" if flow else "k_match_hot_hbm_bytes_per_launch")
+            traffic = tj.get(f"{args.workload}:{kname}_hbm_bytes_per_launch",
+                             tj.get(f"{kname}_hbm_bytes_per_launch") if args.workload == "config3" else None)
         except (OSError, ValueError):
             traffic = None
 
     if rank == 0:
-        achieved = bhot / (ms_hot * 1e-3) / 1e9 if ms_hot > 0 else 0.0
-        lat_sorted = sorted(lat)
-        p99 = lat_sorted[min(len(lat_sorted) - 1, int(np.ceil(0.99 * len(lat_sorted))) - 1)]
-        p50 = lat_sorted[len(lat_sorted) // 2]
+        achieved = bdom / (ms_dom * 1e-3) / 1e9 if ms_dom > 0 else 0.0
         out = {
             "metric": METRIC,
-            "value": round(orders / elapsed, 1),
+            "value": round(g_orders / elapsed, 1),
             "unit": "orders/s",
             "n_gpus": world,
             "steps": steps,
@@ -246,26 +389,33 @@ def main():
             "vs_baseline": None,
             "dtype": "int64",
             "data": "synthetic (seeded doorder.go distribution, Zipf symbols)",
-            "config": {"workload": f"config3: {args.symbols} symbols, Zipf(s={args.zipf}) symbol rank, "
-                                   "doorder 2-dp price/volume, ADD-only",
-                       "symbols": args.symbols, "zipf_s": args.zipf,
+            "config": {"workload": W["desc"].format(**W), "name": args.workload,
+                       "symbols": n_symbols, "zipf_s": W["zipf"],
                        "batch_per_gpu": per_rank, "global_batch": per_rank * world,
                        "parallelism": f"symbol-sharded x{world} (no data-path collective)"},
-            "p50_batch_ms": round(p50, 3),
-            "p99_batch_ms": round(p99, 3),
-            "fills_per_s": round(fills / elapsed, 1),
-            "events_per_s": round(events / elapsed, 1),
+            "p50_batch_ms": round(pctl(lat, 0.5), 3),
+            "p99_batch_ms": round(pctl(lat, 0.99), 3),
+            "fills_per_s": round(g_fills / elapsed, 1),
+            "events_per_s": round(g_events / elapsed, 1),
+            "cancels_per_batch": int(cancels / steps),
             "device_ms_per_batch": round(ms_total, 3),
             "match_books_ms": round(ms_match, 3),
+            "kernel_ms": {k: round(v[0], 3) for k, v in cands.items()},
             "hot_book": {"orders_per_batch": int(max_seg), "top_symbol_share": round(top_share, 5),
-                         "ns_per_order": round(ms_hot * 1e6 / max(max_seg, 1), 1)},
+                         "ns_per_order": round(cands.get("k_flow_plan_head", cands["k_match_hot"])[0] * 1e6
+                                               / max(max_seg, 1), 1),
+                         "path": "flow" if "k_flow_plan_head" in cands else "legacy"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6),
-                         "traffic": traffic, "kernel": kname,
-                         "kernel_ms": round(ms_hot, 3), "alg_bytes_per_launch": int(bhot),
+                         "traffic": traffic, "kernel": f"{kname} ({kdesc})",
+                         "kernel_ms": round(ms_dom, 3), "alg_bytes_per_launch": int(bdom),
                          "match_phase_alg_bytes": int(balg)},
+            "e2e": e2e,
             "cpu_baseline": cpu,
         }
+        if pub is not None and world > 1:
+            pub.check(int(g_orders), int(g_fills), int(g_events))
+            out["publisher"] = pub.summary()
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -16,8 +16,11 @@ from .workload import EVENT_DTYPE, LEVEL_DTYPE, NODE_DTYPE, ORDER_DTYPE
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libgome.so")
 HEADER = os.path.join(os.path.dirname(_HERE), "include", "gome", "gome_abi.h")
+HEADERS = [HEADER, os.path.join(os.path.dirname(_HERE), "include", "gome", "gome_loadgen.h")]
 
 GOME_FLAG_LEGACY_HOT = 1  # gome_config.flags: hot books on the legacy FIFO kernel
+GOME_ORD_ADM_HOST, GOME_ORD_ADMITTED = 1, 2  # gome_order.flags: host-resolved admission (ABI 4)
+GOME_MAX_INFLIGHT = 2
 
 GOME_OK, GOME_E_INVAL, GOME_E_CAPACITY, GOME_E_DEVICE, GOME_E_STATE, GOME_E_NOTFOUND = range(6)
 STATUS_NAMES = {0: "OK", 1: "E_INVAL", 2: "E_CAPACITY", 3: "E_DEVICE", 4: "E_STATE", 5: "E_NOTFOUND"}
@@ -44,7 +47,9 @@ class Stats(C.Structure):
         ("n_hot_rests", C.c_uint64), ("n_hot_cancels", C.c_uint64),
         ("n_flow_books", C.c_uint64), ("n_flow_orders", C.c_uint64), ("n_flow_touches", C.c_uint64),
         ("ms_flow_plan", C.c_double), ("n_flow_head_orders", C.c_uint64),
-        ("n_flow_head_touches", C.c_uint64)]
+        ("n_flow_head_touches", C.c_uint64), ("n_index_rebuilds", C.c_uint64),
+        ("idx_tombstones", C.c_uint64), ("n_flow_cancels", C.c_uint64), ("ms_cold", C.c_double),
+        ("lvl_used", C.c_uint64)]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_}
@@ -71,6 +76,14 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.gome_abi_version.restype = C.c_uint32
     lib.gome_submit_batch.argtypes = [VP, VP, C.c_size_t, C.c_uint64]
     lib.gome_submit_batch_device.argtypes = [VP, VP, C.c_size_t, C.c_uint64, VP]
+    lib.gome_submit_batch_async.argtypes = [VP, VP, C.c_size_t, C.c_uint64]
+    lib.gome_collect.argtypes = [VP, P(VP), P(C.c_size_t), P(Stats)]
+    lib.gome_inflight.argtypes = [VP]
+    lib.gome_inflight.restype = C.c_size_t
+    lib.gome_host_alloc.argtypes = [VP, C.c_size_t, P(VP)]
+    lib.gome_host_free.argtypes = [VP, VP]
+    lib.gome_host_free.restype = None
+    lib.gome_fixed_from_scaled.argtypes = [C.c_double, P(C.c_int64)]
     lib.gome_drain_events.argtypes = [VP, VP, C.c_size_t, P(C.c_size_t)]
     lib.gome_pending_events.argtypes = [VP]
     lib.gome_pending_events.restype = C.c_size_t
@@ -80,22 +93,30 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.gome_snapshot_fifo.argtypes = [VP, C.c_uint32, C.c_int64, VP, C.c_size_t, P(C.c_size_t)]
     lib.gome_fixed_from_double.argtypes = [C.c_double, C.c_uint32, P(C.c_int64)]
     lib.gome_render_match_result.argtypes = [VP, VP, C.c_uint32] + [C.c_char_p] * 6 + [
-        C.c_char_p, C.c_size_t]
+        VP, C.c_char_p, C.c_size_t]
     lib.gome_render_match_result.restype = C.c_int64
-    lib.gome_render_link_node.argtypes = [C.c_char_p, C.c_int64, C.c_uint32, C.c_int64, C.c_uint32] + [
+    lib.gome_render_link_node.argtypes = [C.c_char_p, C.c_int64, C.c_int32, C.c_int64, C.c_uint32] + [
         C.c_char_p] * 5 + [C.c_size_t]
     lib.gome_render_link_node.restype = C.c_int64
+    lib.gome_gen_create.argtypes = [VP, P(VP)]
+    lib.gome_gen_batch.argtypes = [VP, VP, C.c_size_t]
+    lib.gome_gen_shares.argtypes = [VP, P(C.c_double), P(C.c_double)]
+    lib.gome_gen_destroy.argtypes = [VP]
+    lib.gome_gen_destroy.restype = None
+    for f in ("gome_gen_create", "gome_gen_batch", "gome_gen_shares"):
+        getattr(lib, f).restype = C.c_int32
     for f in ("gome_create", "gome_submit_batch", "gome_submit_batch_device", "gome_drain_events",
               "gome_device_events", "gome_get_stats", "gome_snapshot_levels", "gome_snapshot_fifo",
-              "gome_fixed_from_double"):
+              "gome_fixed_from_double", "gome_fixed_from_scaled", "gome_submit_batch_async",
+              "gome_collect", "gome_host_alloc"):
         getattr(lib, f).restype = C.c_int32
     _lib = lib
     return lib
 
 
-def declared_functions(header: str = HEADER) -> list[str]:
-    """Every function the C-ABI header declares."""
-    txt = open(header).read()
+def declared_functions(headers=None) -> list[str]:
+    """Every function the C-ABI headers (include/gome/*.h) declare."""
+    txt = "".join(open(h).read() for h in (headers or HEADERS))
     return sorted(set(re.findall(r"\b(gome_[a-z_]+)\s*\(", txt)) - {"gome_status"})
 
 
@@ -108,17 +129,40 @@ def fixed_from_double(x: float, accuracy: int = 8) -> int:
     return out.value
 
 
+def fixed_from_scaled(v: float) -> int:
+    """An OrderNode Price / Volume as consumed from the doOrder queue (already scaled by
+    10^accuracy at gRPC time, main.go:41): exact integer below 2^53 or GomeError."""
+    lib = load_library()
+    out = C.c_int64()
+    s = lib.gome_fixed_from_scaled(float(v), C.byref(out))
+    if s != GOME_OK:
+        raise GomeError(s, f"{v!r} is not an exact scaled value (integer below 2^53)")
+    return out.value
+
+
+def tx_table_array(table) -> np.ndarray | None:
+    """Transaction code -> raw int32 table for the renderers (None = identity)."""
+    if table is None:
+        return None
+    a = np.arange(256, dtype=np.int32)
+    for code, raw in (table.items() if isinstance(table, dict) else enumerate(table)):
+        a[int(code)] = int(raw)
+    return a
+
+
 def render_match_result(ev: np.void, taker: np.void, symbol: str, taker_uuid: str, taker_oid: str,
                         maker_uuid: str | None, maker_oid: str | None,
-                        maker_next_oid: str | None, accuracy: int = 8) -> str:
+                        maker_next_oid: str | None, accuracy: int = 8, tx_table=None) -> str:
     lib = load_library()
     e = np.array([ev], dtype=EVENT_DTYPE)
     t = np.array([taker], dtype=ORDER_DTYPE)
     enc = lambda s: None if s is None else s.encode()
     buf = C.create_string_buffer(8192)
+    tt = tx_table if isinstance(tx_table, np.ndarray) else tx_table_array(tx_table)
     n = lib.gome_render_match_result(e.ctypes.data, t.ctypes.data, accuracy, symbol.encode(),
                                      taker_uuid.encode(), taker_oid.encode(), enc(maker_uuid),
-                                     enc(maker_oid), enc(maker_next_oid), buf, len(buf))
+                                     enc(maker_oid), enc(maker_next_oid),
+                                     None if tt is None else tt.ctypes.data, buf, len(buf))
     if n < 0:
         raise GomeError(GOME_E_INVAL, "render failed")
     return buf.raw[:n].decode()
@@ -126,7 +170,8 @@ def render_match_result(ev: np.void, taker: np.void, symbol: str, taker_uuid: st
 
 def render_link_node(symbol: str, price_fx: int, side: int, volume_fx: int, uuid: str, oid: str,
                      prev_oid: str | None, next_oid: str | None, accuracy: int = 8) -> str:
-    """A resting node's JSON as the reference stores it in S:link:<price> (nodelink.go:119-122)."""
+    """A resting node's JSON as the reference stores it in S:link:<price> (nodelink.go:119-122).
+    `side` is the raw int32 Transaction value."""
     lib = load_library()
     enc = lambda s: None if s is None else s.encode()
     buf = C.create_string_buffer(4096)
@@ -172,6 +217,33 @@ class Engine:
     def submit_device(self, dev_ptr: int, n: int, seq_base: int = 0, stream: int | None = None):
         self._check(self.lib.gome_submit_batch_device(self.h, C.c_void_p(dev_ptr), n, seq_base,
                                                       C.c_void_p(stream or 0)))
+
+    # ---- pipelined host path (gome_submit_batch_async / gome_collect)
+    def host_buffer(self, n: int) -> np.ndarray:
+        """Page-locked record buffer of n gome_orders (gome_host_alloc), freed with the engine."""
+        p = C.c_void_p()
+        self._check(self.lib.gome_host_alloc(self.h, max(n, 1) * ORDER_DTYPE.itemsize, C.byref(p)))
+        buf = (C.c_char * (max(n, 1) * ORDER_DTYPE.itemsize)).from_address(p.value)
+        return np.frombuffer(buf, dtype=ORDER_DTYPE)[:n]
+
+    def submit_async(self, rec: np.ndarray, seq_base: int = 0):
+        """Queue a batch (rec must stay alive and unchanged until collected)."""
+        assert rec.dtype == ORDER_DTYPE and rec.flags["C_CONTIGUOUS"]
+        self._check(self.lib.gome_submit_batch_async(self.h, rec.ctypes.data, len(rec), seq_base))
+
+    def collect(self, copy: bool = True):
+        """Events of the oldest in-flight batch (publish order) and its stats dict.  copy=False
+        returns a view of the engine's page-locked buffer (valid until the next collect)."""
+        p, n, st = C.c_void_p(), C.c_size_t(), Stats()
+        self._check(self.lib.gome_collect(self.h, C.byref(p), C.byref(n), C.byref(st)))
+        if n.value == 0:
+            return np.zeros(0, EVENT_DTYPE), st.as_dict()
+        buf = (C.c_char * (n.value * EVENT_DTYPE.itemsize)).from_address(p.value)
+        ev = np.frombuffer(buf, dtype=EVENT_DTYPE)
+        return (ev.copy() if copy else ev), st.as_dict()
+
+    def inflight(self) -> int:
+        return self.lib.gome_inflight(self.h)
 
     def drain(self) -> np.ndarray:
         n = self.lib.gome_pending_events(self.h)

@@ -21,9 +21,9 @@ ORACLE_LIB = os.path.join(ORACLE_DIR, "build", "liboracle.so")
 HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
 ARCH = os.environ.get("GOME_OFFLOAD_ARCH", "gfx950")
 
-SOURCES = [os.path.join(CSRC, "engine.hip"), os.path.join(CSRC, "host.cpp")]
-HEADERS = sorted(glob.glob(os.path.join(CSRC, "*.h"))) + sorted(glob.glob(os.path.join(CSRC, "*.inc"))) + [os.path.join(ROOT, "include", "gome", "gome_abi.h"),
-                                                         os.path.abspath(__file__)]
+SOURCES = [os.path.join(CSRC, "engine.hip"), os.path.join(CSRC, "host.cpp"), os.path.join(CSRC, "loadgen.cpp")]
+HEADERS = (sorted(glob.glob(os.path.join(CSRC, "*.h"))) + sorted(glob.glob(os.path.join(CSRC, "*.inc"))) +
+           sorted(glob.glob(os.path.join(ROOT, "include", "gome", "*.h"))) + [os.path.abspath(__file__)])
 
 
 def _stale(out: str, deps: list[str]) -> bool:

@@ -80,8 +80,15 @@ enum {
   C_HOT_ORDERS, C_HOT_FILLS, C_HOT_RESTS, C_HOT_CANCELS,  // hot books (flow + legacy)
   C_FLOW_BOOKS, C_FLOW_ORDERS, C_FLOW_TOUCHES,            // hot books on the flow path
   C_FLOW_HEAD_ORDERS, C_FLOW_HEAD_TOUCHES,                // ... of which the head (k_flow_plan_head)
-  C_NCTR = 20
+  C_FLOW_CANCELS,                                         // cancels applied on the flow path
+  C_NCTR = 21
 };
+
+// Level blocks (a book's sorted level array) come in power-of-two capacities 16 << c.  A
+// block a book outgrows is released to its class (a `freed` list during the batch, merged
+// into the class's free stack by k_lvl_recycle at batch end, so no block is reused within
+// the batch that released it); allocations pop the free stack before the bump pointer.
+constexpr uint32_t LVL_NCLS = 24;
 
 struct Status {
   unsigned long long ctr[C_NCTR];
@@ -90,9 +97,12 @@ struct Status {
   uint32_t ev_bump;
   uint32_t n_events;
   uint32_t nhot;       // segments handled by k_match_hot (first nhot of seg_order)
-  uint32_t pad0;
-  int32_t free_top;    // persists across batches
+  uint32_t lvl_used;   // level slots ever carved from the pool (lvl_bump at batch end)
+  // ---- everything below persists across batches (the per-batch reset stops here)
+  int32_t free_top;
   uint32_t freed_top;
+  int32_t lvl_free_top[LVL_NCLS];
+  uint32_t lvl_freed_top[LVL_NCLS];
 };
 
 struct Dev {
@@ -110,6 +120,49 @@ struct Dev {
   IdxEnt* idx;
   unsigned long long idx_mask;
   Status* st;
+  uint32_t* lvl_free;        // per class c: free stack at lvl_cls_off[c] (level-block bases)
+  uint32_t* lvl_freed;       // per class c: blocks released this batch
+  const uint32_t* lvl_cls_off;  // [LVL_NCLS + 1] offsets; class c holds lvl_cls_off[c+1]-off[c]
 };
+
+__device__ __forceinline__ uint32_t lvl_cls(uint32_t cap) { return (31u - __clz(cap)) - 4u; }
+
+// A level block of `cap` (16 << c) levels: the class's free stack, else the bump pointer.
+// Single-thread; NIL when the level pool is exhausted.
+struct LvlPool {
+  Status* st;
+  uint32_t* lvl_free;
+  uint32_t* lvl_freed;
+  const uint32_t* lvl_cls_off;
+  uint32_t* lvl_bump;
+  uint32_t lvl_cap_total;
+};
+__device__ __forceinline__ LvlPool lvl_pool(const Dev& D) {
+  return LvlPool{D.st, D.lvl_free, D.lvl_freed, D.lvl_cls_off, D.lvl_bump, D.lvl_cap_total};
+}
+
+__device__ __forceinline__ uint32_t lvl_block_alloc(const LvlPool& P, uint32_t cap) {
+  const uint32_t c = lvl_cls(cap);
+  const int t = atomicSub(&P.st->lvl_free_top[c], 1);
+  if (t > 0) return P.lvl_free[P.lvl_cls_off[c] + static_cast<uint32_t>(t) - 1u];
+  const uint32_t nb = atomicAdd(P.lvl_bump, cap);
+  if (static_cast<unsigned long long>(nb) + cap > P.lvl_cap_total) return NIL;
+  return nb;
+}
+__device__ __forceinline__ uint32_t lvl_block_alloc(const Dev& D, uint32_t cap) {
+  return lvl_block_alloc(lvl_pool(D), cap);
+}
+
+// Give back the block a book moved out of (single-thread).  A class holds at most
+// lvl_cap_total / cap blocks, which is its list's capacity.
+__device__ __forceinline__ void lvl_block_release(const LvlPool& P, uint32_t base, uint32_t cap) {
+  if (cap < 16u) return;
+  const uint32_t c = lvl_cls(cap);
+  const uint32_t i = atomicAdd(&P.st->lvl_freed_top[c], 1u);
+  if (P.lvl_cls_off[c] + i < P.lvl_cls_off[c + 1]) P.lvl_freed[P.lvl_cls_off[c] + i] = base;
+}
+__device__ __forceinline__ void lvl_block_release(const Dev& D, uint32_t base, uint32_t cap) {
+  lvl_block_release(lvl_pool(D), base, cap);
+}
 
 }  // namespace gome

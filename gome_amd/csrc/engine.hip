@@ -24,6 +24,8 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstring>
+#include <deque>
+#include <set>
 #include <string>
 #include <vector>
 
@@ -38,12 +40,19 @@
 using namespace gome;
 
 // ============================================================== event compaction
+// Arena events -> publish positions; the sequence number is seq_base + the batch index
+// (gome_event.taker_seq / seq_hi, ABI >= 4).
 __global__ void k_ev_scatter(const gome_event* arena, uint32_t cap, const Status* st,
-                             const uint32_t* ev_off, gome_event* out) {
+                             const uint32_t* ev_off, gome_event* out, unsigned long long seq_base) {
   const uint32_t used = min(st->ev_bump, cap);
   for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < used; j += gridDim.x * blockDim.x) {
-    const gome_event e = arena[j];
-    if (e.taker_seq != NIL) out[ev_off[e.taker_seq] + e.fill_idx] = e;
+    gome_event e = arena[j];
+    if (e.taker_seq == NIL) continue;
+    const uint32_t idx = e.taker_seq;
+    const unsigned long long sq = seq_base + idx;
+    e.taker_seq = static_cast<uint32_t>(sq);
+    e.seq_hi = static_cast<uint32_t>(sq >> 32);
+    out[ev_off[idx] + e.fill_idx] = e;
   }
 }
 
@@ -62,6 +71,53 @@ __global__ void k_recycle_fin(Dev D) {
   }
 }
 
+// Level blocks released this batch -> their class's free stack (block c = class c).
+__global__ __launch_bounds__(256) void k_lvl_recycle(Dev D) {
+  const uint32_t c = blockIdx.x;
+  const int top = max(D.st->lvl_free_top[c], 0);
+  const uint32_t off = D.lvl_cls_off[c], room = D.lvl_cls_off[c + 1] - off;
+  const uint32_t nf = min(D.st->lvl_freed_top[c], room - min(room, static_cast<uint32_t>(top)));
+  for (uint32_t i = threadIdx.x; i < nf; i += blockDim.x) D.lvl_free[off + top + i] = D.lvl_freed[off + i];
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    D.st->lvl_free_top[c] = top + static_cast<int>(nf);
+    D.st->lvl_freed_top[c] = 0;
+    if (c == 0) D.st->lvl_used = min(*D.lvl_bump, D.lvl_cap_total);
+  }
+}
+
+// Rebuild the (S, oid) cancel index from the live FIFO nodes (the table was zeroed): bounds
+// the probe length of lookups that miss (a cancel of a filled or unknown oid scans to the
+// first EMPTY slot, and erases only leave tombstones).  One wave per book, a lane per slot.
+__global__ __launch_bounds__(64) void k_idx_rebuild(Dev D) {
+  const uint32_t lane = lane_id();
+  const unsigned long long mask = D.idx_mask;
+  for (uint32_t sym = blockIdx.x; sym < D.max_symbols; sym += gridDim.x) {
+    const Book bk = D.books[sym];
+    const Level* L = D.lvl + bk.lvl_base;
+    for (uint32_t k = 0; k < bk.n_lvl; ++k) {
+      const Level x = L[k];
+      uint32_t c = x.head, s0 = x.hslot;
+      for (uint32_t guard = 0; c != NIL && guard <= D.ch_cap; ++guard) {
+        const uint32_t lim = (c == x.tail) ? x.tslot : CH;
+        if (lane < CH && lane >= s0 && lane < lim) {
+          Node* nd = &D.nodes[c * CH + lane];
+          if (nd->rem >= 0) {
+            const unsigned long long key = (static_cast<unsigned long long>(sym + 1) << 32) | nd->oid;
+            unsigned long long hh = mix64(key) & mask;
+            for (unsigned long long probe = 0; probe <= mask; ++probe, hh = (hh + 1) & mask)
+              if (atomicCAS(&D.idx[hh].key, KEY_EMPTY, key) == KEY_EMPTY) break;
+            D.idx[hh].loc = c * CH + lane;
+            nd->ixs = static_cast<uint32_t>(hh);
+          }
+        }
+        c = (c == x.tail) ? NIL : D.chdr[c].next;
+        s0 = 0;
+      }
+    }
+  }
+}
+
 // ============================================================== host runtime
 namespace {
 
@@ -74,28 +130,48 @@ uint64_t next_pow2(uint64_t x) {
   return p;
 }
 
+// One of the two batch slots: a batch's device records, its published events, its
+// status copy and its timing events.  Batch k uses slot k % 2, so batch k+1's H2D and
+// batch k-1's D2H never touch the buffers batch k's pipeline works on.
+struct Slot {
+  gome_order* d_orders = nullptr;
+  gome_event* d_events = nullptr;
+  uint32_t ev_cap = 0;
+  Status* h_st = nullptr;          // page-locked copy of the batch's Status
+  gome_event* h_events = nullptr;  // page-locked event copy (gome_collect)
+  size_t h_cap = 0;
+  hipEvent_t ev0{}, ev1{}, evm0{}, evm1{}, evh0{}, evh1{}, evf0{}, evf1{}, evc0{}, evc1{};
+  hipEvent_t h2d{}, done{};
+};
+
+struct Flight {
+  uint32_t slot, n;
+  uint64_t seq_base;
+};
+
 }  // namespace
 
 struct gome_engine {
   gome_config cfg{};
-  hipStream_t stream = nullptr;
-  hipStream_t hot_stream = nullptr;
-  hipStream_t flow_stream = nullptr;
-  bool own_stream = false;
-  hipEvent_t fork{}, join{}, evh0{}, evh1{};
-  hipEvent_t joinf{}, prep_h{}, prep_t{}, evf0{}, evf1{}, fork_adm{}, adm_done{}, seg_done{}, ev_scan{}, ev_hot{};
+  hipStream_t stream = nullptr;       // the pipeline's main stream
+  hipStream_t hot_stream = nullptr;   // tail / near-head flow books, legacy hot kernel
+  hipStream_t flow_stream = nullptr;  // the hottest book's plan (critical path)
+  hipStream_t copy_stream = nullptr;  // H2D of records, D2H of events (pipelined path)
+  hipEvent_t fork{}, join{}, joinf{}, prep_h{}, prep_t{}, fork_adm{}, adm_done{}, seg_done{}, ev_scan{}, ev_hot{};
+  Slot slots[GOME_MAX_INFLIGHT];
+  uint32_t next_slot = 0;
+  std::deque<Flight> flights;
   FlowArgs F{};
   Prep* d_prep = nullptr;
   PendEnt* d_pend = nullptr;
   ResumeRec* d_resume = nullptr;
   Dev D{};
   Status* d_st = nullptr;
-  Status* h_st = nullptr;
   // capacities
   uint32_t max_batch = 0, key_bits = 1, passes = 1, dbits = 1;
   uint32_t hist_cap = 0, bsum_cap = 0;
+  unsigned long long idx_cap = 0;
   // batch buffers
-  gome_order* d_orders = nullptr;
   uint32_t *d_k0 = nullptr, *d_v0 = nullptr, *d_k1 = nullptr, *d_v1 = nullptr;
   uint32_t* d_hist = nullptr;
   uint32_t* d_bsum = nullptr;
@@ -110,18 +186,19 @@ struct gome_engine {
   uint32_t* d_ev_count = nullptr;
   uint32_t* d_ev_off = nullptr;
   gome_event* d_arena = nullptr;
-  gome_event* d_events = nullptr;
   uint32_t arena_cap = 0;
-  hipEvent_t ev0{}, ev1{}, evm0{}, evm1{};
   // host-side state
   std::vector<gome_event> pending;
   size_t pending_pos = 0;
-  size_t dev_events = 0, dev_events_pos = 0;
+  size_t dev_events = 0, dev_events_pos = 0;  // events of the last device submit
+  uint32_t dev_slot = 0;
   gome_stats stats{};
   unsigned long long resting = 0, levels = 0;
+  unsigned long long idx_tomb = 0, n_rebuilds = 0;  // tombstones (upper bound) since the last rebuild
   bool poisoned = false;
   std::string err;
   std::vector<void*> allocs;
+  std::set<void*> host_allocs;
 
   gome_status fail(gome_status s, const std::string& m) {
     err = m;
@@ -139,27 +216,44 @@ struct gome_engine {
     *p = static_cast<T*>(q);
     return true;
   }
+  void release(void* p) {
+    for (auto it = allocs.begin(); it != allocs.end(); ++it)
+      if (*it == p) { (void)hipFree(p); allocs.erase(it); return; }
+  }
   ~gome_engine() {
+    if (stream) (void)hipStreamSynchronize(stream);
+    if (copy_stream) (void)hipStreamSynchronize(copy_stream);
     for (void* p : allocs) (void)hipFree(p);
-    if (h_st) (void)hipHostFree(h_st);
-    if (ev0) { (void)hipEventDestroy(ev0); (void)hipEventDestroy(ev1); }
-    if (evm0) { (void)hipEventDestroy(evm0); (void)hipEventDestroy(evm1); }
-    if (fork) { (void)hipEventDestroy(fork); (void)hipEventDestroy(join); }
-    if (evh0) { (void)hipEventDestroy(evh0); (void)hipEventDestroy(evh1); }
-    if (evf0) {
-      (void)hipEventDestroy(evf0); (void)hipEventDestroy(evf1); (void)hipEventDestroy(joinf);
-      (void)hipEventDestroy(prep_h); (void)hipEventDestroy(prep_t);
-      (void)hipEventDestroy(fork_adm); (void)hipEventDestroy(adm_done); (void)hipEventDestroy(seg_done);
-      (void)hipEventDestroy(ev_scan); (void)hipEventDestroy(ev_hot);
+    for (void* p : host_allocs) (void)hipHostFree(p);
+    for (Slot& S : slots) {
+      if (S.h_st) (void)hipHostFree(S.h_st);
+      if (S.h_events) (void)hipHostFree(S.h_events);
+      for (hipEvent_t ev : {S.ev0, S.ev1, S.evm0, S.evm1, S.evh0, S.evh1, S.evf0, S.evf1, S.evc0, S.evc1, S.h2d, S.done})
+        if (ev) (void)hipEventDestroy(ev);
     }
+    for (hipEvent_t ev : {fork, join, joinf, prep_h, prep_t, fork_adm, adm_done, seg_done, ev_scan, ev_hot})
+      if (ev) (void)hipEventDestroy(ev);
     if (hot_stream) (void)hipStreamDestroy(hot_stream);
     if (flow_stream) (void)hipStreamDestroy(flow_stream);
-    if (own_stream && stream) (void)hipStreamDestroy(stream);
+    if (copy_stream) (void)hipStreamDestroy(copy_stream);
+    if (stream) (void)hipStreamDestroy(stream);
   }
 
   gome_status init(const gome_config& c);
   void scan(const uint32_t* in, uint32_t m, uint32_t* out, uint32_t* total, hipStream_t s);
-  gome_status run(const gome_order* d_ord, uint32_t n, hipStream_t s);
+  gome_status enqueue(const gome_order* d_ord, uint32_t n, hipStream_t s, uint32_t slot, uint64_t seq_base,
+                      uint64_t inflight_n);
+  gome_status finish(uint32_t slot, uint32_t n);
+  gome_status check_submit(size_t n, const void* p);
+  uint32_t take_slot() {
+    const uint32_t k = next_slot;
+    next_slot = (next_slot + 1) % GOME_MAX_INFLIGHT;
+    return k;
+  }
+  gome_status collect(const gome_event** evs, size_t* nev);
+  gome_status collect_all();
+  gome_status spill_device_events();
+  gome_status queue_events(uint32_t slot, size_t n, hipStream_t s);
 };
 
 #define HIPCHK(x)                                                                    \
@@ -182,27 +276,18 @@ gome_status gome_engine::init(const gome_config& c) {
   if (cfg.device < 0 || cfg.device >= ndev) return fail(GOME_E_INVAL, "gome_config.device out of range");
   HIPCHK(hipSetDevice(cfg.device));
   HIPCHK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
-  own_stream = true;
-  HIPCHK(hipEventCreate(&ev0));
-  HIPCHK(hipEventCreate(&ev1));
-  HIPCHK(hipEventCreate(&evm0));
-  HIPCHK(hipEventCreate(&evm1));
   HIPCHK(hipStreamCreateWithFlags(&hot_stream, hipStreamNonBlocking));
-  HIPCHK(hipEventCreateWithFlags(&fork, hipEventDisableTiming));
-  HIPCHK(hipEventCreateWithFlags(&join, hipEventDisableTiming));
-  HIPCHK(hipEventCreate(&evh0));
-  HIPCHK(hipEventCreate(&evh1));
   HIPCHK(hipStreamCreateWithFlags(&flow_stream, hipStreamNonBlocking));
-  HIPCHK(hipEventCreateWithFlags(&joinf, hipEventDisableTiming));
-  HIPCHK(hipEventCreateWithFlags(&prep_h, hipEventDisableTiming));
-  HIPCHK(hipEventCreateWithFlags(&prep_t, hipEventDisableTiming));
-  HIPCHK(hipEventCreate(&evf0));
-  HIPCHK(hipEventCreate(&evf1));
-  HIPCHK(hipEventCreateWithFlags(&fork_adm, hipEventDisableTiming));
-  HIPCHK(hipEventCreateWithFlags(&adm_done, hipEventDisableTiming));
-  HIPCHK(hipEventCreateWithFlags(&seg_done, hipEventDisableTiming));
-  HIPCHK(hipEventCreateWithFlags(&ev_scan, hipEventDisableTiming));
-  HIPCHK(hipEventCreateWithFlags(&ev_hot, hipEventDisableTiming));
+  HIPCHK(hipStreamCreateWithFlags(&copy_stream, hipStreamNonBlocking));
+  for (hipEvent_t* ev : {&fork, &join, &joinf, &prep_h, &prep_t, &fork_adm, &adm_done, &seg_done, &ev_scan, &ev_hot})
+    HIPCHK(hipEventCreateWithFlags(ev, hipEventDisableTiming));
+  for (Slot& S : slots) {
+    for (hipEvent_t* ev : {&S.ev0, &S.ev1, &S.evm0, &S.evm1, &S.evh0, &S.evh1, &S.evf0, &S.evf1, &S.evc0, &S.evc1})
+      HIPCHK(hipEventCreate(ev));
+    HIPCHK(hipEventCreateWithFlags(&S.h2d, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&S.done, hipEventDisableTiming));
+    HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&S.h_st), sizeof(Status), hipHostMallocDefault));
+  }
   HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_match_hot),
                              hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(HOT_LDS_BYTES)));
 
@@ -222,25 +307,33 @@ gome_status gome_engine::init(const gome_config& c) {
   const unsigned long long nchunks = std::min<unsigned long long>(
       cfg.max_nodes / 8 + 2 * std::min<unsigned long long>(cfg.max_levels, cfg.max_nodes) + 1024,
       0xF0000000ull);
-  const unsigned long long idx_cap = next_pow2(std::max<unsigned long long>(2 * cfg.max_nodes, 1024));
+  idx_cap = next_pow2(std::max<unsigned long long>(2 * cfg.max_nodes, 1024));
+  // level-block free lists: class c (16 << c levels) holds at most max_levels >> (4 + c) blocks
+  std::vector<uint32_t> cls_off(LVL_NCLS + 1, 0);
+  for (uint32_t k = 0; k < LVL_NCLS; ++k)
+    cls_off[k + 1] = cls_off[k] + static_cast<uint32_t>((cfg.max_levels >> (4 + k)) + 1);
+  uint32_t* d_cls_off = nullptr;
   if (!alloc(&D.books, ms, "books") || !alloc(&D.lvl, cfg.max_levels, "levels") ||
       !alloc(&D.lvl_bump, 1, "lvl_bump") || !alloc(&D.nodes, nchunks * CH, "chunks") ||
       !alloc(&D.chdr, nchunks, "chunk headers") ||
       !alloc(&D.ch_bump, 1, "ch_bump") || !alloc(&D.free_ids, nchunks, "free_ids") ||
       !alloc(&D.freed_ids, nchunks, "freed_ids") || !alloc(&D.idx, idx_cap, "index") ||
-      !alloc(&d_st, 1, "status"))
+      !alloc(&d_st, 1, "status") || !alloc(&D.lvl_free, cls_off[LVL_NCLS], "level-block free lists") ||
+      !alloc(&D.lvl_freed, cls_off[LVL_NCLS], "level-block release lists") ||
+      !alloc(&d_cls_off, LVL_NCLS + 1, "level-block classes"))
     return GOME_E_CAPACITY;
+  D.lvl_cls_off = d_cls_off;
   D.max_symbols = ms;
   D.lvl_cap_total = static_cast<uint32_t>(cfg.max_levels);
   D.ch_cap = static_cast<uint32_t>(nchunks);
   D.idx_mask = idx_cap - 1;
   D.st = d_st;
+  HIPCHK(hipMemcpyAsync(d_cls_off, cls_off.data(), cls_off.size() * 4, hipMemcpyHostToDevice, stream));
   HIPCHK(hipMemsetAsync(D.books, 0, sizeof(Book) * ms, stream));
   HIPCHK(hipMemsetAsync(D.lvl_bump, 0, 4, stream));
   HIPCHK(hipMemsetAsync(D.ch_bump, 0, 4, stream));
   HIPCHK(hipMemsetAsync(D.idx, 0, sizeof(IdxEnt) * idx_cap, stream));
   HIPCHK(hipMemsetAsync(d_st, 0, sizeof(Status), stream));
-  HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&h_st), sizeof(Status), hipHostMallocDefault));
 
   // ---- per-batch buffers
   const uint32_t nb = max_batch;
@@ -249,7 +342,7 @@ gome_status gome_engine::init(const gome_config& c) {
                                   : 2ull * nb + EVB * std::min<uint64_t>(nb, ms) + 1024;
   if (evcap > 0xF0000000ull) evcap = 0xF0000000ull;
   arena_cap = static_cast<uint32_t>(evcap);
-  if (!alloc(&d_orders, nb, "orders") || !alloc(&d_k0, nb, "keys0") || !alloc(&d_v0, nb, "vals0") ||
+  if (!alloc(&d_k0, nb, "keys0") || !alloc(&d_v0, nb, "vals0") ||
       !alloc(&d_k1, nb, "keys1") || !alloc(&d_v1, nb, "vals1") || !alloc(&d_hist, hist_cap, "hist") ||
       !alloc(&d_bsum, bsum_cap, "scan") || !alloc(&d_tmp, nb, "segflags") ||
       !alloc(&d_seg_start, nb + 1, "seg_start") || !alloc(&d_seg_order, nb, "seg_order") ||
@@ -257,9 +350,12 @@ gome_status gome_engine::init(const gome_config& c) {
       !alloc(&d_amin, adm_mask + 1ull, "adm_min") || !alloc(&d_adm_slot, nb, "adm_slot") ||
       !alloc(&d_ev_count, nb, "ev_count") || !alloc(&d_ev_off, nb, "ev_off") ||
       !alloc(&d_prep, nb, "prep") || !alloc(&d_pend, nb, "pending inserts") ||
-      !alloc(&d_resume, MAX_HOT, "resume records") ||
-      !alloc(&d_arena, arena_cap, "event arena") || !alloc(&d_events, arena_cap, "events"))
+      !alloc(&d_resume, MAX_HOT, "resume records") || !alloc(&d_arena, arena_cap, "event arena"))
     return GOME_E_CAPACITY;
+  for (Slot& S : slots) {
+    if (!alloc(&S.d_orders, nb, "orders") || !alloc(&S.d_events, arena_cap, "events")) return GOME_E_CAPACITY;
+    S.ev_cap = arena_cap;
+  }
   // flow path (match_flow.h): per-hot-book headers and level slots, packed records, the
   // touch log and its per-level views (FL_TOUCH_MUL entries per order), gathered makers
   const uint64_t ntouch = static_cast<uint64_t>(FL_TOUCH_MUL) * nb;
@@ -291,26 +387,45 @@ void gome_engine::scan(const uint32_t* in, uint32_t m, uint32_t* out, uint32_t* 
   k_scan_down<<<nb, SCAN_T, 0, s>>>(in, m, d_bsum, out);
 }
 
-gome_status gome_engine::run(const gome_order* d_ord, uint32_t n, hipStream_t s) {
+// Enqueue batch `n` records at d_ord through the whole device pipeline on stream s (plus the
+// flow / hot streams it forks), publishing into slot `sl`.  Ends with the Status copy to the
+// slot's page-locked status and the slot's `done` event; finish() reads them.
+gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_t s, uint32_t sl,
+                                 uint64_t seq_base, uint64_t inflight_n) {
+  Slot& S = slots[sl];
   // conservative event bound: one partial per ADD + one event per DEL + one per popped
-  // maker (<= resting + ADDs) + block padding
+  // maker (<= resting + ADDs) + block padding; batches still in flight may add to resting
+  const unsigned long long rest_ub = resting + inflight_n;
   const unsigned long long bound =
-      2ull * n + resting + EVB * static_cast<unsigned long long>(std::min(n, cfg.max_symbols)) + EVB;
-  if (bound > arena_cap) {
-    if (bound > 0xF0000000ull) return fail(GOME_E_CAPACITY, "event bound exceeds 2^32");
+      2ull * n + rest_ub + EVB * static_cast<unsigned long long>(std::min(n, cfg.max_symbols)) + EVB;
+  if (bound > 0xF0000000ull) return fail(GOME_E_CAPACITY, "event bound exceeds 2^32");
+  if (bound > arena_cap || bound > S.ev_cap) {
+    // the arena only lives within one batch, and this slot's events were collected: wait for
+    // the batches in flight and grow both (the other slot keeps its events)
     HIPCHK(hipStreamSynchronize(s));
-    for (auto it = allocs.begin(); it != allocs.end();) {
-      if (*it == d_arena || *it == d_events) { (void)hipFree(*it); it = allocs.erase(it); }
-      else ++it;
+    HIPCHK(hipStreamSynchronize(stream));
+    const uint32_t ncap = static_cast<uint32_t>(std::min<unsigned long long>(bound + bound / 2, 0xF0000000ull));
+    if (bound > arena_cap) {
+      release(d_arena);
+      arena_cap = ncap;
+      if (!alloc(&d_arena, arena_cap, "event arena")) { poisoned = true; return GOME_E_CAPACITY; }
     }
-    arena_cap = static_cast<uint32_t>(std::min<unsigned long long>(bound + bound / 2, 0xF0000000ull));
-    if (!alloc(&d_arena, arena_cap, "event arena") || !alloc(&d_events, arena_cap, "events")) {
-      poisoned = true;
-      return GOME_E_CAPACITY;
+    if (bound > S.ev_cap) {
+      release(S.d_events);
+      S.ev_cap = ncap;
+      if (!alloc(&S.d_events, S.ev_cap, "events")) { poisoned = true; return GOME_E_CAPACITY; }
     }
   }
-  HIPCHK(hipEventRecord(ev0, s));
-  // per-batch status reset (free_top / freed_top persist)
+  // cancel-index hygiene: erases leave tombstones and lookups that miss stop only at an EMPTY
+  // slot, so rebuild the table from the live nodes before it fills up (70%)
+  if ((rest_ub + idx_tomb + 2 * inflight_n) * 10 > idx_cap * 7) {
+    HIPCHK(hipMemsetAsync(D.idx, 0, sizeof(IdxEnt) * idx_cap, s));
+    k_idx_rebuild<<<2048, 64, 0, s>>>(D);
+    idx_tomb = 0;
+    ++n_rebuilds;
+  }
+  HIPCHK(hipEventRecord(S.ev0, s));
+  // per-batch status reset (free_top / freed_top and the level pools persist)
   HIPCHK(hipMemsetAsync(d_st, 0, offsetof(Status, free_top), s));
   const uint32_t T256 = 256, gN = ceil_div(n, T256);
   // admission markers depend on the input records only: they run on the flow stream beside
@@ -325,7 +440,6 @@ gome_status gome_engine::run(const gome_order* d_ord, uint32_t n, hipStream_t s)
 
   // ---- stable radix sort of (symbol_id, seq)
   const uint32_t nblk = ceil_div(n, RS_TILE);
-  const uint32_t nbins = 1u << dbits;
   uint32_t *kin = nullptr, *vin = nullptr, *kout = d_k0, *vout = d_v0;
   for (uint32_t p = 0; p < passes; ++p) {
     const uint32_t shift = p * dbits;
@@ -341,7 +455,6 @@ gome_status gome_engine::run(const gome_order* d_ord, uint32_t n, hipStream_t s)
       k_radix_scatter<false><<<nblk, RS_T, 0, s>>>(nullptr, kin, vin, n, shift, bits, d_hist, kout,
                                                    vout, nblk);
     }
-    (void)nbins;
     kin = kout;
     vin = vout;
     kout = (kin == d_k0) ? d_k1 : d_k0;
@@ -370,6 +483,7 @@ gome_status gome_engine::run(const gome_order* d_ord, uint32_t n, hipStream_t s)
   B.ev_count = d_ev_count;
   B.sidx = sidx;
   B.adm_flag = d_adm_slot;
+  B.seq_base = seq_base;
   const uint32_t grid = std::min<uint32_t>(n, cfg.max_symbols);
   const uint32_t nhot_max = std::min<uint32_t>(MAX_FLOW, grid);
   // flow path: the head (longest FL_HEAD candidates, the batch's critical path) and the tail
@@ -395,9 +509,9 @@ gome_status gome_engine::run(const gome_order* d_ord, uint32_t n, hipStream_t s)
   k_flow_prep_b<<<nh_head, FL_PREP_T, 0, flow_stream>>>(D, B, FH);
   k_flow_prep_c<<<dim3(FL_PG, nh_head), FL_PREP_T, 0, flow_stream>>>(D, B, FH);
   HIPCHK(hipEventRecord(prep_h, flow_stream));
-  HIPCHK(hipEventRecord(evf0, flow_stream));
+  HIPCHK(hipEventRecord(S.evf0, flow_stream));
   k_flow_plan_head<<<1, 256, 0, flow_stream>>>(D, FH0);
-  HIPCHK(hipEventRecord(evf1, flow_stream));
+  HIPCHK(hipEventRecord(S.evf1, flow_stream));
   // ---- admission markers (k_adm, launched above on the flow stream)
   HIPCHK(hipStreamWaitEvent(s, adm_done, 0));
   // k_prep gathers the same records as the head's prep: let the head's prep (the critical
@@ -407,7 +521,7 @@ gome_status gome_engine::run(const gome_order* d_ord, uint32_t n, hipStream_t s)
   // ---- match_books: one wavefront per book; hot books (LDS) on a second stream,
   //      concurrently with the cold books (HBM)
   k_prep<<<gN, T256, 0, s>>>(d_ord, n, sidx, d_adm_slot, d_prep);
-  HIPCHK(hipEventRecord(evm0, s));
+  HIPCHK(hipEventRecord(S.evm0, s));
   HIPCHK(hipMemsetAsync(F.ig_bump, 0, 4, s));
   HIPCHK(hipEventRecord(fork, s));
   HIPCHK(hipStreamWaitEvent(flow_stream, fork, 0));  // (k_prep, the gather bump)
@@ -425,8 +539,8 @@ gome_status gome_engine::run(const gome_order* d_ord, uint32_t n, hipStream_t s)
   head_recon(FH0, 1, flow_stream);
   HIPCHK(hipEventRecord(joinf, flow_stream));
   // The tail's chain and the legacy hot kernels share the third stream: HIP maps more
-  // streams than hardware queues (4 per process, one taken by the caller) onto shared
-  // queues, which would serialise them behind the head.
+  // streams than hardware queues (4 per process) onto shared queues, which would serialise
+  // them behind the head.
   HIPCHK(hipStreamWaitEvent(hot_stream, fork, 0));
   if (nh_tail) {
     k_flow_prep<<<nh_tail, FL_PREP_T, 0, hot_stream>>>(D, B, FT);
@@ -451,41 +565,49 @@ gome_status gome_engine::run(const gome_order* d_ord, uint32_t n, hipStream_t s)
   }
   // legacy hot path (books the flow path declined); it and the cold kernel read the preps'
   // routing decisions (FlowHdr::ok)
-  HIPCHK(hipEventRecord(evh0, hot_stream));
+  HIPCHK(hipEventRecord(S.evh0, hot_stream));
   const uint32_t nleg = std::min<uint32_t>(MAX_HOT, grid);
   k_match_hot<<<nleg, 64, HOT_LDS_BYTES, hot_stream>>>(D, B, d_pend, d_resume, F.hdr);
-  HIPCHK(hipEventRecord(evh1, hot_stream));
+  HIPCHK(hipEventRecord(S.evh1, hot_stream));
   k_match_resume<<<nleg, 64, 0, hot_stream>>>(D, B, d_resume);
   k_pend_apply<<<dim3(8, 64), 256, 0, hot_stream>>>(D, d_pend, d_seg_start, d_seg_order, B);
   HIPCHK(hipEventRecord(join, hot_stream));
   HIPCHK(hipStreamWaitEvent(s, prep_h, 0));
   HIPCHK(hipStreamWaitEvent(s, prep_t, 0));
+  HIPCHK(hipEventRecord(S.evc0, s));
   k_match<<<std::min<uint32_t>(grid, COLD_BLOCKS), 64, 0, s>>>(D, B, &F.hdr[0].ok, sizeof(FlowHdr) / sizeof(uint32_t));
+  HIPCHK(hipEventRecord(S.evc1, s));
   HIPCHK(hipStreamWaitEvent(s, join, 0));
   HIPCHK(hipStreamWaitEvent(s, joinf, 0));
 
-  HIPCHK(hipEventRecord(evm1, s));
+  HIPCHK(hipEventRecord(S.evm1, s));
 
   // ---- event compaction into publish order
   scan(d_ev_count, n, d_ev_off, &d_st->n_events, s);
   // the hottest book's events and the arena scatter fill disjoint slots: run them side by side
   HIPCHK(hipEventRecord(ev_scan, s));
   HIPCHK(hipStreamWaitEvent(flow_stream, ev_scan, 0));
-  k_flow_events<<<1024, 256, 0, flow_stream>>>(D, B, FH0, d_ev_off, d_events);
+  k_flow_events<<<1024, 256, 0, flow_stream>>>(D, B, FH0, d_ev_off, S.d_events);
   HIPCHK(hipEventRecord(ev_hot, flow_stream));
-  k_ev_scatter<<<2048, T256, 0, s>>>(d_arena, arena_cap, d_st, d_ev_off, d_events);
+  k_ev_scatter<<<2048, T256, 0, s>>>(d_arena, arena_cap, d_st, d_ev_off, S.d_events, seq_base);
   HIPCHK(hipStreamWaitEvent(s, ev_hot, 0));
   k_recycle_copy<<<256, 256, 0, s>>>(D);
   k_recycle_fin<<<1, 64, 0, s>>>(D);
+  k_lvl_recycle<<<LVL_NCLS, 256, 0, s>>>(D);
   HIPCHK(hipGetLastError());
-  HIPCHK(hipEventRecord(ev1, s));
-  HIPCHK(hipMemcpyAsync(h_st, d_st, sizeof(Status), hipMemcpyDeviceToHost, s));
-  HIPCHK(hipStreamSynchronize(s));
+  HIPCHK(hipEventRecord(S.ev1, s));
+  HIPCHK(hipMemcpyAsync(S.h_st, d_st, sizeof(Status), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipEventRecord(S.done, s));
+  return GOME_OK;
+}
 
-  const Status& st = *h_st;
+// After slot `sl`'s done event: the batch's outcome, counters and timings.
+gome_status gome_engine::finish(uint32_t sl, uint32_t n) {
+  Slot& S = slots[sl];
+  const Status& st = *S.h_st;
   if (st.err & ERR_INPUT)
     return fail(GOME_E_INVAL, "batch rejected: a record is outside the exact domain "
-                              "(symbol_id >= max_symbols, volume < 0, or |value| >= 2^53)");
+                              "(symbol_id >= max_symbols, volume < 0, |value| >= 2^53, or unknown flags)");
   if (st.err) {
     poisoned = true;
     return fail((st.err & ERR_CORRUPT) ? GOME_E_STATE : GOME_E_CAPACITY,
@@ -494,11 +616,15 @@ gome_status gome_engine::run(const gome_order* d_ord, uint32_t n, hipStream_t s)
   }
   resting += st.ctr[C_RESTING_DELTA];
   levels += st.ctr[C_LEVELS_DELTA];
-  float ms_total = 0, ms_match = 0, ms_hot = 0, ms_flow = 0;
-  (void)hipEventElapsedTime(&ms_total, ev0, ev1);
-  (void)hipEventElapsedTime(&ms_match, evm0, evm1);
-  (void)hipEventElapsedTime(&ms_hot, evh0, evh1);
-  (void)hipEventElapsedTime(&ms_flow, evf0, evf1);
+  // index entries erased this batch (each leaves a tombstone): rests - net resting change
+  idx_tomb += st.ctr[C_RESTS] - st.ctr[C_RESTING_DELTA];
+  float ms_total = 0, ms_match = 0, ms_hot = 0, ms_flow = 0, ms_cold = 0;
+  (void)hipEventElapsedTime(&ms_cold, S.evc0, S.evc1);
+  stats.ms_cold = ms_cold;
+  (void)hipEventElapsedTime(&ms_total, S.ev0, S.ev1);
+  (void)hipEventElapsedTime(&ms_match, S.evm0, S.evm1);
+  (void)hipEventElapsedTime(&ms_hot, S.evh0, S.evh1);
+  (void)hipEventElapsedTime(&ms_flow, S.evf0, S.evf1);
   stats.ms_hot = ms_hot;
   stats.ms_flow_plan = ms_flow;
   stats.n_flow_books = st.ctr[C_FLOW_BOOKS];
@@ -525,9 +651,102 @@ gome_status gome_engine::run(const gome_order* d_ord, uint32_t n, hipStream_t s)
   stats.n_segments = st.nseg;
   stats.ms_total = ms_total;
   stats.ms_match = ms_match;
-  dev_events = st.n_events;
-  dev_events_pos = 0;
+  stats.n_index_rebuilds = n_rebuilds;
+  stats.idx_tombstones = idx_tomb;
+  stats.n_flow_cancels = st.ctr[C_FLOW_CANCELS];
+  stats.lvl_used = st.lvl_used;
   return GOME_OK;
+}
+
+gome_status gome_engine::check_submit(size_t n, const void* p) {
+  if (poisoned) return fail(GOME_E_STATE, "engine poisoned by an earlier fatal error");
+  if (n > max_batch) return fail(GOME_E_INVAL, "batch larger than max_batch");
+  if (n && !p) return fail(GOME_E_INVAL, "NULL records");
+  return GOME_OK;
+}
+
+// Copy `n` events of slot `sl` (device) to the host drain queue.
+gome_status gome_engine::queue_events(uint32_t sl, size_t n, hipStream_t s) {
+  if (pending_pos) {
+    pending.erase(pending.begin(), pending.begin() + static_cast<long>(pending_pos));
+    pending_pos = 0;
+  }
+  const size_t old = pending.size();
+  pending.resize(old + n);
+  if (n) {
+    HIPCHK(hipMemcpyAsync(pending.data() + old, slots[sl].d_events, n * sizeof(gome_event),
+                          hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+  }
+  return GOME_OK;
+}
+
+// Events of the last device submit that were not drained yet go to the host queue before
+// anything reuses their slot (never dropped).
+gome_status gome_engine::spill_device_events() {
+  if (dev_events_pos < dev_events) {
+    Slot& S = slots[dev_slot];
+    const size_t k = dev_events - dev_events_pos;
+    if (pending_pos) {
+      pending.erase(pending.begin(), pending.begin() + static_cast<long>(pending_pos));
+      pending_pos = 0;
+    }
+    const size_t old = pending.size();
+    pending.resize(old + k);
+    HIPCHK(hipMemcpy(pending.data() + old, S.d_events + dev_events_pos, k * sizeof(gome_event),
+                     hipMemcpyDeviceToHost));
+  }
+  dev_events = dev_events_pos = 0;
+  return GOME_OK;
+}
+
+gome_status gome_engine::collect(const gome_event** evs, size_t* nev) {
+  if (flights.empty()) return fail(GOME_E_NOTFOUND, "no batch in flight");
+  const Flight f = flights.front();
+  flights.pop_front();
+  *evs = nullptr;
+  *nev = 0;
+  if (f.n == 0) return GOME_OK;
+  Slot& S = slots[f.slot];
+  HIPCHK(hipEventSynchronize(S.done));
+  gome_status st = finish(f.slot, f.n);
+  if (st != GOME_OK) return st;
+  const size_t n = S.h_st->n_events;
+  if (n > S.h_cap) {
+    if (S.h_events) (void)hipHostFree(S.h_events);
+    S.h_events = nullptr;
+    S.h_cap = 0;
+    const size_t cap = n + n / 4 + 1024;
+    HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&S.h_events), cap * sizeof(gome_event), hipHostMallocDefault));
+    S.h_cap = cap;
+  }
+  if (n) {
+    HIPCHK(hipMemcpyAsync(S.h_events, S.d_events, n * sizeof(gome_event), hipMemcpyDeviceToHost, copy_stream));
+    HIPCHK(hipStreamSynchronize(copy_stream));
+  }
+  *evs = S.h_events;
+  *nev = n;
+  return GOME_OK;
+}
+
+// Every batch still in flight -> the drain queue (before a synchronous call).
+gome_status gome_engine::collect_all() {
+  gome_status first = GOME_OK;
+  while (!flights.empty()) {
+    const gome_event* evs = nullptr;
+    size_t n = 0;
+    gome_status st = collect(&evs, &n);
+    if (st != GOME_OK) {
+      if (first == GOME_OK) first = st;
+      continue;
+    }
+    if (pending_pos) {
+      pending.erase(pending.begin(), pending.begin() + static_cast<long>(pending_pos));
+      pending_pos = 0;
+    }
+    pending.insert(pending.end(), evs, evs + n);
+  }
+  return first;
 }
 
 // ============================================================== C-ABI
@@ -569,42 +788,95 @@ const char* gome_last_error(const gome_engine* e) {
   return e ? e->err.c_str() : g_create_err.c_str();
 }
 
-gome_status gome_submit_batch(gome_engine* e, const gome_order* orders, size_t n, uint64_t) {
+gome_status gome_submit_batch(gome_engine* e, const gome_order* orders, size_t n, uint64_t seq_base) {
   if (!e) return GOME_E_INVAL;
-  if (e->poisoned) return e->fail(GOME_E_STATE, "engine poisoned by an earlier fatal error");
-  if (n == 0) { e->dev_events = 0; return GOME_OK; }
-  if (!orders || n > e->max_batch) return e->fail(GOME_E_INVAL, "batch larger than max_batch");
-  for (size_t i = 0; i < n; ++i)
-    if (orders[i].flags != 0) return e->fail(GOME_E_INVAL, "gome_order.flags must be 0");
-  hipError_t he = hipMemcpyAsync(e->d_orders, orders, n * sizeof(gome_order),
-                                 hipMemcpyHostToDevice, e->stream);
+  gome_status st = e->collect_all();
+  if (st != GOME_OK) return st;
+  if ((st = e->spill_device_events()) != GOME_OK) return st;
+  if ((st = e->check_submit(n, orders)) != GOME_OK) return st;
+  if (n == 0) return GOME_OK;
+  const uint32_t sl = e->take_slot();
+  Slot& S = e->slots[sl];
+  hipError_t he = hipMemcpyAsync(S.d_orders, orders, n * sizeof(gome_order), hipMemcpyHostToDevice, e->stream);
   if (he != hipSuccess) return e->fail(GOME_E_DEVICE, hipGetErrorString(he));
-  gome_status s = e->run(e->d_orders, static_cast<uint32_t>(n), e->stream);
-  if (s != GOME_OK) return s;
-  // queue the batch's events on the host in publish order
-  const size_t old = e->pending.size() - e->pending_pos;
-  if (e->pending_pos) {
-    e->pending.erase(e->pending.begin(), e->pending.begin() + static_cast<long>(e->pending_pos));
-    e->pending_pos = 0;
-  }
-  e->pending.resize(old + e->dev_events);
-  if (e->dev_events) {
-    he = hipMemcpy(e->pending.data() + old, e->d_events, e->dev_events * sizeof(gome_event),
-                   hipMemcpyDeviceToHost);
-    if (he != hipSuccess) return e->fail(GOME_E_DEVICE, hipGetErrorString(he));
-  }
-  e->dev_events = 0;
-  return GOME_OK;
+  if ((st = e->enqueue(S.d_orders, static_cast<uint32_t>(n), e->stream, sl, seq_base, 0)) != GOME_OK) return st;
+  if ((he = hipEventSynchronize(S.done)) != hipSuccess) return e->fail(GOME_E_DEVICE, hipGetErrorString(he));
+  if ((st = e->finish(sl, static_cast<uint32_t>(n))) != GOME_OK) return st;
+  return e->queue_events(sl, S.h_st->n_events, e->stream);
 }
 
 gome_status gome_submit_batch_device(gome_engine* e, const gome_order* dev_orders, size_t n,
-                                     uint64_t, void* stream) {
+                                     uint64_t seq_base, void* stream) {
   if (!e) return GOME_E_INVAL;
-  if (e->poisoned) return e->fail(GOME_E_STATE, "engine poisoned by an earlier fatal error");
-  if (n == 0) { e->dev_events = 0; return GOME_OK; }
-  if (!dev_orders || n > e->max_batch) return e->fail(GOME_E_INVAL, "batch larger than max_batch");
+  gome_status st = e->collect_all();
+  if (st != GOME_OK) return st;
+  if ((st = e->spill_device_events()) != GOME_OK) return st;
+  if ((st = e->check_submit(n, dev_orders)) != GOME_OK) return st;
+  if (n == 0) return GOME_OK;
   hipStream_t s = stream ? static_cast<hipStream_t>(stream) : e->stream;
-  return e->run(dev_orders, static_cast<uint32_t>(n), s);
+  const uint32_t sl = e->take_slot();
+  Slot& S = e->slots[sl];
+  if ((st = e->enqueue(dev_orders, static_cast<uint32_t>(n), s, sl, seq_base, 0)) != GOME_OK) return st;
+  hipError_t he = hipEventSynchronize(S.done);
+  if (he != hipSuccess) return e->fail(GOME_E_DEVICE, hipGetErrorString(he));
+  if ((st = e->finish(sl, static_cast<uint32_t>(n))) != GOME_OK) return st;
+  e->dev_slot = sl;
+  e->dev_events = S.h_st->n_events;
+  e->dev_events_pos = 0;
+  return GOME_OK;
+}
+
+gome_status gome_submit_batch_async(gome_engine* e, const gome_order* orders, size_t n, uint64_t seq_base) {
+  if (!e) return GOME_E_INVAL;
+  if (e->flights.size() >= GOME_MAX_INFLIGHT)
+    return e->fail(GOME_E_STATE, "GOME_MAX_INFLIGHT batches in flight: gome_collect first");
+  gome_status st = e->spill_device_events();
+  if (st != GOME_OK) return st;
+  if ((st = e->check_submit(n, orders)) != GOME_OK) return st;
+  uint64_t inflight_n = 0;
+  for (const Flight& f : e->flights) inflight_n += f.n;
+  const uint32_t sl = e->take_slot();
+  if (n) {
+    Slot& S = e->slots[sl];
+    // the records travel on the copy stream (beside the batch in flight); the pipeline waits
+    hipError_t he = hipMemcpyAsync(S.d_orders, orders, n * sizeof(gome_order), hipMemcpyHostToDevice,
+                                   e->copy_stream);
+    if (he == hipSuccess) he = hipEventRecord(S.h2d, e->copy_stream);
+    if (he == hipSuccess) he = hipStreamWaitEvent(e->stream, S.h2d, 0);
+    if (he != hipSuccess) return e->fail(GOME_E_DEVICE, hipGetErrorString(he));
+    if ((st = e->enqueue(S.d_orders, static_cast<uint32_t>(n), e->stream, sl, seq_base, inflight_n)) != GOME_OK)
+      return st;
+  }
+  e->flights.push_back(Flight{sl, static_cast<uint32_t>(n), seq_base});
+  return GOME_OK;
+}
+
+gome_status gome_collect(gome_engine* e, const gome_event** events, size_t* n_events, gome_stats* stats) {
+  if (!e || !events || !n_events) return GOME_E_INVAL;
+  gome_status st = e->collect(events, n_events);
+  if (st == GOME_OK && stats) *stats = e->stats;
+  return st;
+}
+
+size_t gome_inflight(const gome_engine* e) { return e ? e->flights.size() : 0; }
+
+gome_status gome_host_alloc(gome_engine* e, size_t bytes, void** out) {
+  if (!e || !out) return GOME_E_INVAL;
+  *out = nullptr;
+  void* p = nullptr;
+  if (hipHostMalloc(&p, std::max<size_t>(bytes, 1), hipHostMallocDefault) != hipSuccess)
+    return e->fail(GOME_E_CAPACITY, "hipHostMalloc failed (" + std::to_string(bytes) + " B)");
+  e->host_allocs.insert(p);
+  *out = p;
+  return GOME_OK;
+}
+
+void gome_host_free(gome_engine* e, void* p) {
+  if (!e || !p) return;
+  auto it = e->host_allocs.find(p);
+  if (it == e->host_allocs.end()) return;
+  (void)hipHostFree(p);
+  e->host_allocs.erase(it);
 }
 
 size_t gome_pending_events(const gome_engine* e) {
@@ -625,8 +897,8 @@ gome_status gome_drain_events(gome_engine* e, gome_event* out, size_t cap, size_
   size_t dp = e->dev_events - e->dev_events_pos;
   if (c < cap && dp) {
     size_t k = std::min(cap - c, dp);
-    hipError_t he = hipMemcpy(out + c, e->d_events + e->dev_events_pos, k * sizeof(gome_event),
-                              hipMemcpyDeviceToHost);
+    hipError_t he = hipMemcpy(out + c, e->slots[e->dev_slot].d_events + e->dev_events_pos,
+                              k * sizeof(gome_event), hipMemcpyDeviceToHost);
     if (he != hipSuccess) return e->fail(GOME_E_DEVICE, hipGetErrorString(he));
     e->dev_events_pos += k;
     c += k;
@@ -637,7 +909,7 @@ gome_status gome_drain_events(gome_engine* e, gome_event* out, size_t cap, size_
 
 gome_status gome_device_events(gome_engine* e, const gome_event** dev_ptr, size_t* n) {
   if (!e || !dev_ptr || !n) return GOME_E_INVAL;
-  *dev_ptr = e->d_events;
+  *dev_ptr = e->slots[e->dev_slot].d_events;
   *n = e->dev_events;
   return GOME_OK;
 }
@@ -651,6 +923,7 @@ gome_status gome_get_stats(const gome_engine* e, gome_stats* out) {
 gome_status gome_snapshot_levels(gome_engine* e, uint32_t sym, gome_level* out, size_t cap,
                                  size_t* n_out) {
   if (!e || !n_out || (cap && !out)) return GOME_E_INVAL;
+  if (gome_status st = e->collect_all()) return st;
   if (sym >= e->cfg.max_symbols) return e->fail(GOME_E_NOTFOUND, "symbol_id out of range");
   Book bk;
   if (hipMemcpy(&bk, e->D.books + sym, sizeof bk, hipMemcpyDeviceToHost) != hipSuccess)
@@ -679,6 +952,7 @@ gome_status gome_snapshot_levels(gome_engine* e, uint32_t sym, gome_level* out, 
 gome_status gome_snapshot_fifo(gome_engine* e, uint32_t sym, int64_t price, gome_node* out,
                                size_t cap, size_t* n_out) {
   if (!e || !n_out || (cap && !out)) return GOME_E_INVAL;
+  if (gome_status st = e->collect_all()) return st;
   if (sym >= e->cfg.max_symbols) return e->fail(GOME_E_NOTFOUND, "symbol_id out of range");
   Book bk;
   if (hipMemcpy(&bk, e->D.books + sym, sizeof bk, hipMemcpyDeviceToHost) != hipSuccess)

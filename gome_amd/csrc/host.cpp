@@ -164,7 +164,7 @@ void render_node(Out& o, const NodeView& v) {
 
 }  // namespace
 
-extern "C" int64_t gome_render_link_node(const char* symbol, int64_t price_fx, uint32_t side, int64_t volume_fx,
+extern "C" int64_t gome_render_link_node(const char* symbol, int64_t price_fx, int32_t transaction, int64_t volume_fx,
                                          uint32_t accuracy, const char* uuid, const char* oid,
                                          const char* prev_oid, const char* next_oid, char* buf, size_t cap) {
   if (!symbol || !uuid || !oid || !buf) return -1;
@@ -172,7 +172,7 @@ extern "C" int64_t gome_render_link_node(const char* symbol, int64_t price_fx, u
   // a resting node as nodelink.go stores it (SetLinkNode, :119-122): the ADD that rested,
   // its remaining volume, and the FIFO flags / neighbours kept by InitOrderLink, SetLast and
   // DeleteLinkNode (:12-19, :53-64, :124-166)
-  NodeView v{GOME_ADD, uuid, oid, symbol, static_cast<int>(side), price_fx, volume_fx, accuracy,
+  NodeView v{GOME_ADD, uuid, oid, symbol, transaction, price_fx, volume_fx, accuracy,
              prev_oid == nullptr, next_oid == nullptr, next_oid, prev_oid};
   render_node(o, v);
   if (!o.ok) return -1;
@@ -184,19 +184,74 @@ extern "C" gome_status gome_fixed_from_double(double x, uint32_t accuracy, int64
   return fixed_from_double(x, accuracy, out);
 }
 
+// The doOrder queue carries OrderNodes whose Price / Volume were scaled at gRPC time
+// (main.go:41 -> ordernode.go:76-87): exact iff integer-valued and below 2^53.
+extern "C" gome_status gome_fixed_from_scaled(double v, int64_t* out) {
+  if (!out || !std::isfinite(v)) return GOME_E_INVAL;
+  const double lim = 9007199254740992.0;  // 2^53
+  if (!(std::fabs(v) < lim) || std::trunc(v) != v) return GOME_E_INVAL;
+  *out = static_cast<int64_t>(v);
+  return GOME_OK;
+}
+
 extern "C" int64_t gome_render_match_result(const gome_event* ev, const gome_order* taker,
                                             uint32_t accuracy, const char* symbol,
                                             const char* taker_uuid, const char* taker_oid,
                                             const char* maker_uuid, const char* maker_oid,
-                                            const char* maker_next_oid, char* buf,
-                                            size_t cap) {
+                                            const char* maker_next_oid, const int32_t* tx_table,
+                                            char* buf, size_t cap);
+
+extern "C" int64_t gome_render_events(const gome_event* ev, size_t n, const gome_order* batch, size_t batch_n,
+                                      uint64_t seq_base, uint32_t accuracy, const char* const* sym_names,
+                                      size_t n_sym, const char* const* uuid_names, size_t n_uuid,
+                                      const char* const* oid_names, size_t n_oid, const int32_t* tx_table,
+                                      char* buf, size_t cap) {
+  if ((n && (!ev || !batch)) || !sym_names || !uuid_names || !oid_names) return INT64_MIN;
+  size_t used = 0;
+  bool fits = buf != nullptr;
+  char tmp[16384];
+  for (size_t i = 0; i < n; ++i) {
+    const gome_event& e = ev[i];
+    const uint64_t seq = (static_cast<uint64_t>(e.seq_hi) << 32) | e.taker_seq;
+    if (seq < seq_base || seq - seq_base >= batch_n) return INT64_MIN;
+    const gome_order& t = batch[seq - seq_base];
+    if (t.symbol_id >= n_sym || t.uuid_id >= n_uuid || t.oid_id >= n_oid) return INT64_MIN;
+    const bool fill = e.kind == GOME_EV_FILL;
+    if (fill && (e.maker_uuid_id >= n_uuid || e.maker_oid_id >= n_oid ||
+                 (!e.maker_is_last && e.maker_next_oid_id >= n_oid)))
+      return INT64_MIN;
+    const int64_t k = gome_render_match_result(
+        &e, &t, accuracy, sym_names[t.symbol_id], uuid_names[t.uuid_id], oid_names[t.oid_id],
+        fill ? uuid_names[e.maker_uuid_id] : nullptr, fill ? oid_names[e.maker_oid_id] : nullptr,
+        (fill && !e.maker_is_last) ? oid_names[e.maker_next_oid_id] : nullptr, tx_table, tmp, sizeof tmp);
+    if (k < 0) return INT64_MIN;
+    if (fits && used + static_cast<size_t>(k) + 1 <= cap) {
+      std::memcpy(buf + used, tmp, static_cast<size_t>(k));
+      buf[used + static_cast<size_t>(k)] = '\n';
+    } else {
+      fits = false;
+    }
+    used += static_cast<size_t>(k) + 1;
+  }
+  return fits ? static_cast<int64_t>(used) : -static_cast<int64_t>(used);
+}
+
+extern "C" int64_t gome_render_match_result(const gome_event* ev, const gome_order* taker,
+                                            uint32_t accuracy, const char* symbol,
+                                            const char* taker_uuid, const char* taker_oid,
+                                            const char* maker_uuid, const char* maker_oid,
+                                            const char* maker_next_oid, const int32_t* tx_table,
+                                            char* buf, size_t cap) {
   if (!ev || !taker || !symbol || !taker_uuid || !taker_oid || !buf) return -1;
+  // Transaction codes -> the raw int32 values the reference echoes (Q8, gome_abi.h)
+  const int taker_tx = tx_table ? tx_table[taker->side] : taker->side;
+  const int maker_tx = tx_table ? tx_table[ev->maker_side] : ev->maker_side;
   Out o{buf, cap};
   o.put("{\"Node\":");
   if (ev->kind == GOME_EV_CANCEL) {
     // engine.go:109 — MatchResult{Node: node, MatchNode: node, MatchVolume: 0}, with
     // node.Volume overwritten by the stored remaining volume (engine.go:89,100).
-    NodeView n{taker->action, taker_uuid, taker_oid, symbol, taker->side, taker->price_fx,
+    NodeView n{taker->action, taker_uuid, taker_oid, symbol, taker_tx, taker->price_fx,
                ev->maker_volume_fx, accuracy, false, false, nullptr};
     render_node(o, n);
     o.put(",\"MatchNode\":");
@@ -204,11 +259,11 @@ extern "C" int64_t gome_render_match_result(const gome_event* ev, const gome_ord
   } else {
     if (!maker_uuid || !maker_oid) return -1;
     // Node: the taker after this fill (engine.go:154,171,190).
-    NodeView t{taker->action, taker_uuid, taker_oid, symbol, taker->side, taker->price_fx,
+    NodeView t{taker->action, taker_uuid, taker_oid, symbol, taker_tx, taker->price_fx,
                ev->taker_volume_fx, accuracy, false, false, nullptr};
     render_node(o, t);
     // MatchNode: the FIFO head as stored (IsFirst, PrevNode "", Action ADD).
-    NodeView m{GOME_ADD, maker_uuid, maker_oid, symbol, ev->maker_side, ev->price_fx,
+    NodeView m{GOME_ADD, maker_uuid, maker_oid, symbol, maker_tx, ev->price_fx,
                ev->maker_volume_fx, accuracy, true, ev->maker_is_last != 0,
                ev->maker_is_last ? nullptr : maker_next_oid};
     if (!ev->maker_is_last && !maker_next_oid) return -1;

@@ -22,6 +22,7 @@ struct BatchArgs {
   uint32_t* ev_count;         // events per batch index
   const uint32_t* sidx;       // segment position -> batch index (the radix sort's permutation)
   const uint32_t* adm_flag;   // per batch index: admitted ADD (k_adm_flag)
+  unsigned long long seq_base;  // sequence number of batch index 0 (published events)
 };
 
 // The Prep record of segment position b built from the input (what k_prep writes to
@@ -177,9 +178,9 @@ __device__ __forceinline__ bool level_grow(WaveCtx& W) {
   const uint32_t lane = lane_id();
   uint32_t ncap = W.cap ? W.cap * 2 : 16;
   uint32_t nb = 0;
-  if (lane == 0) nb = atomicAdd(W.D.lvl_bump, ncap);
+  if (lane == 0) nb = lvl_block_alloc(W.D, ncap);
   nb = uni(nb);
-  if (static_cast<unsigned long long>(nb) + ncap > W.D.lvl_cap_total) {
+  if (nb == NIL) {
     set_err(W, ERR_LEVELS);
     return false;
   }
@@ -188,6 +189,7 @@ __device__ __forceinline__ bool level_grow(WaveCtx& W) {
     uint32_t k = w0 + lane;
     if (k < W.nl) NL[k] = W.L[k];
   }
+  if (lane == 0) lvl_block_release(W.D, W.base, W.cap);  // reusable from the next batch on
   W.L = NL;
   W.cap = ncap;
   W.base = nb;
@@ -378,7 +380,7 @@ __device__ __forceinline__ int64_t match_level(WaveCtx& W, uint32_t k, int64_t T
       e.maker_side = static_cast<uint8_t>(t);
       e.maker_is_last = is_last ? 1 : 0;
       e.pad0 = 0;
-      e.pad1 = 0;
+      e.seq_hi = 0;
       W.B.arena[W.ev_base + W.ev_used + rank] = e;
     }
     W.ev_used += narr;
@@ -547,7 +549,7 @@ __device__ __forceinline__ uint32_t do_cancel(WaveCtx& W, int64_t p, uint32_t oi
     e.maker_side = static_cast<uint8_t>(side);
     e.maker_is_last = 1;
     e.pad0 = 0;
-    e.pad1 = 0;
+    e.seq_hi = 0;
     W.B.arena[W.ev_base + W.ev_used] = e;
   }
   W.ev_used += 1;

@@ -1328,7 +1328,9 @@ __device__ __forceinline__ void fl_events(const Dev& D, const BatchArgs& B, cons
       ev.match_volume_fx = qty;
       ev.maker_volume_fx = full ? pre : pre - qty;
       ev.taker_volume_fx = tb - (hi - c.c);
-      ev.taker_seq = tk.idx;
+      // arena events carry the batch index (k_ev_scatter adds seq_base); direct ones the sequence
+      const unsigned long long sq = ARENA ? tk.idx : B.seq_base + tk.idx;
+      ev.taker_seq = static_cast<uint32_t>(sq);
       ev.fill_idx = F.fbase[L + t] + (m - c.first);
       ev.symbol_id = sym;
       ev.maker_oid_id = oid;
@@ -1338,7 +1340,7 @@ __device__ __forceinline__ void fl_events(const Dev& D, const BatchArgs& B, cons
       ev.maker_side = static_cast<uint8_t>(tx);
       ev.maker_is_last = static_cast<uint8_t>(last);
       ev.pad0 = 0;
-      ev.pad1 = 0;
+      ev.seq_hi = static_cast<uint32_t>(sq >> 32);
       dst[m - c.first] = ev;
     }
   }
@@ -1483,11 +1485,12 @@ __device__ __forceinline__ void fl_write_finish(const Dev& D, const FlowHdr& hd,
     if (c > cap) {
       uint32_t ncap = 16;
       while (ncap < c) ncap <<= 1;
-      const uint32_t nb = atomicAdd(D.lvl_bump, ncap);
-      if (static_cast<unsigned long long>(nb) + ncap > D.lvl_cap_total) {
+      const uint32_t nb = lvl_block_alloc(D, ncap);
+      if (nb == NIL) {
         atomicOr(&D.st->err, ERR_LEVELS);
         cap = 0;
       } else {
+        lvl_block_release(D, base, cap);  // the book's old block (reusable from the next batch)
         base = nb;
         cap = ncap;
       }

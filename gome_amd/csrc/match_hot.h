@@ -101,6 +101,7 @@ struct HotEnv {
   Level* lvl;
   uint32_t* lvl_bump;
   ResumeRec* resume;
+  LvlPool lpool;
   uint32_t ch_cap, arena_cap, lvl_cap_total, lvl_base, lvl_cap, beg, end, pad;
 };
 
@@ -1157,6 +1158,7 @@ __global__ __launch_bounds__(64) void k_match_hot(Dev D, BatchArgs B, PendEnt* p
     e.lvl = D.lvl;
     e.lvl_bump = D.lvl_bump;
     e.resume = resume;
+    e.lpool = lvl_pool(D);
     e.ch_cap = D.ch_cap;
     e.arena_cap = B.arena_cap;
     e.lvl_cap_total = D.lvl_cap_total;
@@ -1296,9 +1298,13 @@ __global__ __launch_bounds__(64) void k_match_hot(Dev D, BatchArgs B, PendEnt* p
     uint32_t ncap = 16;
     while (ncap < H.nl) ncap <<= 1;
     uint32_t nb = 0;
-    if (lane == 0) nb = G_ADD(gp(E.lvl_bump), ncap);
+    if (lane == 0) {
+      const LvlPool P = S->env.lpool;
+      nb = lvl_block_alloc(P, ncap);
+      if (nb != NIL) lvl_block_release(P, base, cap);  // the book's old block
+    }
     nb = uni(nb);
-    if (static_cast<unsigned long long>(nb) + ncap > uni(E.lvl_cap_total)) hot_err(H, ERR_LEVELS);
+    if (nb == NIL) hot_err(H, ERR_LEVELS);
     else { base = nb; cap = ncap; }
   }
   if (H.nl <= cap) hot_writeback(H, gp(E.lvl) + base);

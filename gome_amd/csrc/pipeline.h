@@ -241,7 +241,7 @@ __global__ void k_adm(const gome_order* ord, uint32_t n, uint32_t* claim, uint32
   {
     const int64_t lim = 1ll << 53;
     if (g.symbol_id >= max_symbols || g.volume_fx < 0 || g.volume_fx >= lim || g.price_fx <= -lim ||
-        g.price_fx >= lim)
+        g.price_fx >= lim || (g.flags & ~GOME_ORD_FLAGS_MASK) != 0)
       atomicOr(&st->err, ERR_INPUT);
   }
   if (g.action != GOME_ADD && g.action != GOME_DEL) { slot[i] = NIL; return; }
@@ -274,11 +274,15 @@ static_assert(sizeof(Prep) == 32, "Prep layout");
 // Admission verdict per input record, in place of its marker slot (1: an ADD that holds the
 // lowest index of its (S, uuid, oid) key, nodepool.go:14-28), so k_prep (on the critical path)
 // reads one flag instead of chasing slot -> minimum.  Runs beside the radix sort.
+// A record whose admission the host resolved (GOME_ORD_ADM_HOST: the consumer keeps the
+// reference's pre-pool markers itself) carries the verdict in GOME_ORD_ADMITTED.
 __global__ void k_adm_flag(const gome_order* ord, uint32_t n, uint32_t* slot, const uint32_t* amin) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint8_t action = ord[i].action;
-  slot[i] = (action == GOME_ADD && amin[slot[i]] == i) ? 1u : 0u;
+  const uint16_t fl = ord[i].flags;
+  if (fl & GOME_ORD_ADM_HOST) slot[i] = (action == GOME_ADD && (fl & GOME_ORD_ADMITTED)) ? 1u : 0u;
+  else slot[i] = (action == GOME_ADD && amin[slot[i]] == i) ? 1u : 0u;
 }
 
 __global__ void k_prep(const gome_order* ord, uint32_t n, const uint32_t* sidx,

@@ -25,7 +25,9 @@ way and are refused.
 
 `names` maps interned ids to the reference's strings: any object with
 name(kind, id) -> str and id(kind, str) -> int, kinds "sym", "uuid", "oid" (the host owns
-the interning, as the Go consumer would).
+the interning, as the Go consumer would), and optionally tx_raw(code) -> int /
+tx_code(raw) -> int for Transaction values outside {0, 1} (gome_abi.h transaction codes;
+identity when absent).
 """
 from __future__ import annotations
 
@@ -37,6 +39,16 @@ from .abi import GOME_E_INVAL, GomeError, render_link_node
 from .workload import ADD, ORDER_DTYPE
 
 GOME_SALE = 1
+
+
+def _tx_raw(names, code: int) -> int:
+    f = getattr(names, "tx_raw", None)
+    return f(code) if f else code
+
+
+def _tx_code(names, raw: int) -> int:
+    f = getattr(names, "tx_code", None)
+    return f(raw) if f else raw
 
 
 def redis_snapshot(eng, symbol_ids, names, accuracy: int = 8) -> dict:
@@ -62,7 +74,7 @@ def redis_snapshot(eng, symbol_ids, names, accuracy: int = 8) -> dict:
             link = {"f": f"{S}:node:{oids[0]}", "l": f"{S}:node:{oids[-1]}"}
             for k, nd in enumerate(nodes):
                 link[f"{S}:node:{oids[k]}"] = render_link_node(
-                    S, p, int(nd["side"]), int(nd["volume_fx"]), names.name("uuid", int(nd["uuid_id"])),
+                    S, p, _tx_raw(names, int(nd["side"])), int(nd["volume_fx"]), names.name("uuid", int(nd["uuid_id"])),
                     oids[k], oids[k - 1] if k else None, oids[k + 1] if k + 1 < len(nodes) else None,
                     accuracy)
             hashes[f"{S}:link:{P}"] = link
@@ -127,6 +139,19 @@ def restore_records(snap: dict, names) -> np.ndarray:
     for (S, P), sd in sides.items():
         if len(sd) != 1 or (S, P, next(iter(sd))) not in members:
             raise GomeError(GOME_E_INVAL, f"{S}:link:{P} is not in its side set (quirk state)")
+    # a crossed book (best bid >= best ask) would fill on replay: refuse it before anything
+    # reaches the engine
+    best: dict[str, list] = {}
+    for (S, P, sd) in members:
+        b = best.setdefault(S, [None, None])
+        p = int(P)
+        if sd == "BUY":
+            b[0] = p if b[0] is None else max(b[0], p)
+        else:
+            b[1] = p if b[1] is None else min(b[1], p)
+    for S, (bid, ask) in best.items():
+        if bid is not None and ask is not None and bid >= ask:
+            raise GomeError(GOME_E_INVAL, f"{S}: snapshot book is crossed (bid {bid} >= ask {ask})")
     out = np.zeros(len(recs), ORDER_DTYPE)
     for i, (p, v, sid, oid, uuid, side) in enumerate(recs):
         out[i]["price_fx"] = p
@@ -134,16 +159,17 @@ def restore_records(snap: dict, names) -> np.ndarray:
         out[i]["symbol_id"] = sid
         out[i]["oid_id"] = oid
         out[i]["uuid_id"] = uuid
-        out[i]["side"] = side
+        out[i]["side"] = _tx_code(names, side)
         out[i]["action"] = ADD
     return out
 
 
 def restore(eng, snap: dict, names, seq_base: int = 0) -> int:
     """Rebuild the snapshot's books in an engine (resume).  Returns the orders replayed."""
-    rec = restore_records(snap, names)
-    if len(rec):
-        eng.submit(rec, seq_base)
+    rec = restore_records(snap, names)  # (validated, crossed books refused: nothing applied yet)
+    step = max(1, int(getattr(eng, "max_batch", len(rec) or 1)))
+    for i in range(0, len(rec), step):  # FIFO order is kept across chunks
+        eng.submit(rec[i:i + step], seq_base + i)
         ev = eng.drain()
         if len(ev):
             raise GomeError(GOME_E_INVAL, f"snapshot book is crossed: {len(ev)} fills on replay")

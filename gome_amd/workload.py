@@ -27,7 +27,7 @@ EVENT_DTYPE = np.dtype([
     ("taker_volume_fx", "<i8"), ("taker_seq", "<u4"), ("fill_idx", "<u4"),
     ("symbol_id", "<u4"), ("maker_oid_id", "<u4"), ("maker_uuid_id", "<u4"),
     ("maker_next_oid_id", "<u4"), ("kind", "u1"), ("maker_side", "u1"),
-    ("maker_is_last", "u1"), ("pad0", "u1"), ("pad1", "<u4"),
+    ("maker_is_last", "u1"), ("pad0", "u1"), ("seq_hi", "<u4"),
 ])
 assert EVENT_DTYPE.itemsize == 64
 
@@ -172,3 +172,52 @@ def cancel_mix(n: int, n_symbols: int, seed: int = 42, del_frac: float = 0.5,
 
 def split_batches(rec: np.ndarray, batch: int):
     return [rec[i:i + batch] for i in range(0, len(rec), batch)]
+
+
+class NativeStream:
+    """The native load generator (include/gome/gome_loadgen.h, libgome.so host code): the same
+    distributions as Stream / cancel_mix at bench scale (config 4's cancel mix in C++: each DEL
+    re-sends a uniformly chosen earlier ADD no DEL targeted yet).  Symbol ids follow
+    ZipfSymbols(n_symbols, s).rank_to_id (uniform symbols: identity)."""
+
+    def __init__(self, n_symbols: int, zipf_s: float | None = None, seed: int = 42,
+                 price_decimals: int = 2, del_frac: float = 0.0, aggressive_frac: float = 0.0,
+                 rank: int = 0, world: int = 1, uuid: int = 2, first_oid: int = 1):
+        import ctypes as C
+        from .abi import GomeError, load_library
+        self._C = C
+        self.lib = load_library()
+        self.zipf = ZipfSymbols(n_symbols, zipf_s) if zipf_s else None
+        self._perm = (self.zipf.rank_to_id if self.zipf is not None
+                      else np.arange(n_symbols, dtype=np.uint32)).astype(np.uint32)
+
+        class Cfg(C.Structure):
+            _fields_ = [("n_symbols", C.c_uint32), ("price_decimals", C.c_uint32), ("zipf_s", C.c_double),
+                        ("del_frac", C.c_double), ("aggressive_frac", C.c_double), ("seed", C.c_uint64),
+                        ("first_oid", C.c_uint64), ("rank_to_id", C.c_void_p), ("rank", C.c_uint32),
+                        ("world", C.c_uint32), ("uuid", C.c_uint32), ("accuracy", C.c_uint32)]
+        cfg = Cfg(n_symbols, price_decimals, float(zipf_s or 0.0), del_frac, aggressive_frac, seed,
+                  first_oid, self._perm.ctypes.data, rank, world, uuid, 8)
+        h = C.c_void_p()
+        st = self.lib.gome_gen_create(C.byref(cfg), C.byref(h))
+        if st != 0:
+            raise GomeError(st, "gome_gen_create")
+        self.h = h
+        own, top = C.c_double(), C.c_double()
+        self.lib.gome_gen_shares(h, C.byref(own), C.byref(top))
+        self.owned_share, self.top_share = own.value, top.value
+
+    def batch(self, n: int, out: np.ndarray | None = None) -> np.ndarray:
+        rec = out if out is not None else np.zeros(n, ORDER_DTYPE)
+        assert rec.dtype == ORDER_DTYPE and len(rec) >= n
+        st = self.lib.gome_gen_batch(self.h, rec.ctypes.data, n)
+        if st != 0:
+            raise RuntimeError(f"gome_gen_batch: {st}")
+        return rec[:n]
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.gome_gen_destroy(self.h)
+            self.h = None
+
+    __del__ = close

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define GOME_ABI_VERSION 3u
+#define GOME_ABI_VERSION 4u
 
 /* ---- status codes (replace the reference's swallowed errors / panics,
  *      rabbitmq.go:44-49,70-72,120-122; nodelink.go:132,142,157) ---------- */
@@ -48,25 +48,40 @@ enum {
 /* ---- actions and sides ---------------------------------------------------- */
 enum { GOME_ADD = 1, GOME_DEL = 2 };      /* engine.go:14-18, main.go:14-18 */
 enum { GOME_BUY = 0, GOME_SALE = 1 };     /* api/order.proto:4-7            */
-/* side is the raw OrderRequest.transaction value; SALE iff side == 1, any other
- * value is treated as BUY (ordernode.go:95, nodepool.go:89), and is echoed back
- * unchanged in events (MatchNode.Transaction). */
+/* Transaction codes.  OrderRequest.transaction is an int32 (order.proto:13,
+ * ordernode.go:14); the reference treats 1 as SALE and ANY other value as BUY
+ * (ordernode.go:95, nodepool.go:89; quirk Q8) and echoes the raw value in every
+ * MatchResult it publishes.  A record carries a one-byte code:
+ *   0 = BUY (Transaction 0), 1 = SALE (Transaction 1),
+ *   2..255 = a host-interned Transaction value outside {0, 1} (BUY semantics).
+ * The engine echoes the code in events (gome_event.maker_side); the renderers map
+ * codes back to the raw int32 through the caller's table (gome_tx_table). */
+#define GOME_TX_CODES 256
 
 /* ---- records ------------------------------------------------------------- */
 
+/* gome_order.flags (ABI >= 4).  By default admission (S:comparison, nodepool.go:14-28,
+ * engine.go:58-62,90; quirk Q4) follows the batch model: an ADD is admitted iff no
+ * earlier ADD or DEL of the same batch carries the same (symbol, uuid, oid).  A host
+ * that keeps the reference's pre-pool markers itself (set at gRPC time, main.go:44-45;
+ * gome_amd/consumer.py PrePool) resolves admission per record instead: */
+#define GOME_ORD_ADM_HOST 1u   /* admission decided by the host (ignore the batch rule) */
+#define GOME_ORD_ADMITTED 2u   /* ... and this ADD is admitted (its marker existed)      */
+#define GOME_ORD_FLAGS_MASK (GOME_ORD_ADM_HOST | GOME_ORD_ADMITTED)
+
 /* One consumed OrderNode message (ordernode.go:9-36) in fixed point.
  * price_fx / volume_fx = value * 10^accuracy exactly (ordernode.go:76-87, see
- * gome_fixed_from_double).  The sequence number of a record is its index in the
- * submitted batch (plus the batch's seq_base). */
+ * gome_fixed_from_double / gome_fixed_from_scaled).  The sequence number of a record
+ * is seq_base + its index in the submitted batch (gome_event.taker_seq / seq_hi). */
 typedef struct gome_order {
   int64_t price_fx;   /* OrderNode.Price  (limit price; request price for DEL)  */
   int64_t volume_fx;  /* OrderNode.Volume (>= 0)                                */
   uint32_t symbol_id; /* interned OrderNode.Symbol, < gome_config.max_symbols    */
   uint32_t oid_id;    /* interned OrderNode.Oid   (unique per symbol, README:27) */
   uint32_t uuid_id;   /* interned OrderNode.Uuid                                 */
-  uint8_t side;       /* raw OrderNode.Transaction                               */
+  uint8_t side;       /* Transaction code (see above): 1 SALE, anything else BUY */
   uint8_t action;     /* OrderNode.Action: 1 ADD, 2 DEL, anything else ignored   */
-  uint16_t flags;     /* reserved, must be 0                                     */
+  uint16_t flags;     /* GOME_ORD_* (0: batch admission model); other bits E_INVAL */
 } gome_order;
 
 enum { GOME_EV_FILL = 1, GOME_EV_CANCEL = 2 };
@@ -76,25 +91,27 @@ enum { GOME_EV_FILL = 1, GOME_EV_CANCEL = 2 };
  *          as read from the FIFO head (IsFirst=true, PrevNode=""), MatchVolume = qty.
  *   CANCEL (engine.go:109): Node = MatchNode = the DEL request with Volume = the
  *          stored remaining volume; MatchVolume = 0.
- * Events of one batch are returned in the reference publish order, i.e. sorted by
- * (taker_seq, fill_idx). */
+ * Sequence number of the taker (the ADD / DEL record) = (seq_hi << 32) | taker_seq =
+ * seq_base + its index in the batch (ABI >= 4; with seq_base = 0, taker_seq IS the batch
+ * index).  Events of one batch are returned in the reference publish order, i.e.
+ * sorted by (sequence number, fill_idx). */
 typedef struct gome_event {
   int64_t price_fx;         /* level price (= MatchNode.Price); DEL: request price  */
   int64_t match_volume_fx;  /* MatchVolume                                           */
   int64_t maker_volume_fx;  /* MatchNode.Volume: pre-fill if fully filled, else the
                                maker's remaining volume; DEL: stored remaining       */
   int64_t taker_volume_fx;  /* Node.Volume: taker remaining after this fill          */
-  uint32_t taker_seq;       /* index of the ADD/DEL in its batch                     */
+  uint32_t taker_seq;       /* low 32 bits of seq_base + batch index                 */
   uint32_t fill_idx;        /* 0,1,2... within one taker                             */
   uint32_t symbol_id;
   uint32_t maker_oid_id;    /* MatchNode.Oid                                         */
   uint32_t maker_uuid_id;   /* MatchNode.Uuid                                        */
   uint32_t maker_next_oid_id; /* MatchNode.NextNode = S:node:<this> unless is_last   */
   uint8_t kind;             /* GOME_EV_FILL / GOME_EV_CANCEL                         */
-  uint8_t maker_side;       /* MatchNode.Transaction (raw)                           */
+  uint8_t maker_side;       /* MatchNode.Transaction code                            */
   uint8_t maker_is_last;    /* MatchNode.IsLast (NextNode == "")                     */
   uint8_t pad0;
-  uint32_t pad1;
+  uint32_t seq_hi;          /* high 32 bits of seq_base + batch index                */
 } gome_event;
 
 /* One price level of a book in the reference key schema (nodepool.go:61-115):
@@ -156,6 +173,12 @@ typedef struct gome_stats {
                                                  the batch's critical path)               */
   uint64_t n_flow_head_orders;                /* orders / touches of the books that        */
   uint64_t n_flow_head_touches;               /* k_flow_plan_head planned (ABI >= 3)      */
+  uint64_t n_index_rebuilds;                  /* cancel-index rebuilds so far (ABI >= 4)   */
+  uint64_t idx_tombstones;                    /* index tombstones since (upper bound)     */
+  uint64_t n_flow_cancels;                    /* DELs applied on the flow path this batch */
+  double ms_cold;                             /* device time of k_match (cold books)      */
+  uint64_t lvl_used;                          /* level slots carved from the pool so far
+                                                 (released blocks are reused first)      */
 } gome_stats;
 
 typedef struct gome_engine gome_engine;
@@ -167,23 +190,50 @@ const char* gome_last_error(const gome_engine* e); /* handle-local message, neve
 uint32_t gome_abi_version(void);
 
 /* ---- hot path ------------------------------------------------------------ */
+/* Every submit applies its batch after every earlier one (per symbol in record order, as
+ * the reference's single consumer, rabbitmq.go:116).  Events of a batch are published in
+ * (sequence number, fill_idx) order.  A batch rejected with GOME_E_INVAL (a record outside
+ * the exact domain) leaves the book unchanged. */
+
 /* Apply one batch of host records (replaces n calls of DoOrder, engine.go:46).
  * Synchronous: on return the events are queued for gome_drain_events. */
 gome_status gome_submit_batch(gome_engine* e, const gome_order* orders, size_t n,
                               uint64_t seq_base);
 /* Same, with the records already resident in device memory (HBM); `stream` is a
  * hipStream_t or NULL.  Events stay on the device: read them with
- * gome_device_events or copy them out with gome_drain_events. */
+ * gome_device_events or copy them out with gome_drain_events (events of an earlier
+ * device batch not yet drained are moved to the host queue first, never dropped). */
 gome_status gome_submit_batch_device(gome_engine* e, const gome_order* dev_orders,
                                      size_t n, uint64_t seq_base, void* stream);
 /* Copy out up to cap pending events in publish order; *n_out = copied. */
 gome_status gome_drain_events(gome_engine* e, gome_event* out, size_t cap,
                               size_t* n_out);
 size_t gome_pending_events(const gome_engine* e);
-/* Device pointer + count of the last batch's events (valid until next submit). */
+/* Device pointer + count of the last device batch's events (valid until next submit). */
 gome_status gome_device_events(gome_engine* e, const gome_event** dev_ptr,
                                size_t* n);
 gome_status gome_get_stats(const gome_engine* e, gome_stats* out);
+
+/* ---- pipelined host path (ABI >= 4) ---------------------------------------- */
+/* The batching consumer's loop: submit batch k+1, then collect batch k.
+ * The copy of batch k+1's records to HBM and of batch k's events to the host run on a
+ * copy stream while the device applies the other batch, so PCIe hides under matching.
+ * At most GOME_MAX_INFLIGHT batches are in flight; `orders` must stay valid and
+ * unchanged until the batch is collected (memory from gome_host_alloc is page-locked,
+ * which makes the copy asynchronous).  Any synchronous call first collects every
+ * in-flight batch into the drain queue. */
+#define GOME_MAX_INFLIGHT 2u
+gome_status gome_submit_batch_async(gome_engine* e, const gome_order* orders, size_t n,
+                                    uint64_t seq_base);
+/* Wait for the oldest in-flight batch and copy its events to engine-owned page-locked
+ * memory: *events (publish order) stays valid until the next gome_collect or
+ * synchronous call.  stats (optional) = that batch's counters.  GOME_E_NOTFOUND when no
+ * batch is in flight; the batch's own status otherwise (E_INVAL: rejected, no events). */
+gome_status gome_collect(gome_engine* e, const gome_event** events, size_t* n_events,
+                         gome_stats* stats);
+size_t gome_inflight(const gome_engine* e);
+gome_status gome_host_alloc(gome_engine* e, size_t bytes, void** out);
+void gome_host_free(gome_engine* e, void* p);
 
 /* ---- book state (Redis-schema view; snapshot / parity) ------ */
 /* Levels of one book in ascending price order, including empty levels that
@@ -199,23 +249,43 @@ gome_status gome_snapshot_fifo(gome_engine* e, uint32_t symbol_id, int64_t price
 /* ordernode.go:76-87: Float64(decimal.NewFromFloat(x) * decimal.NewFromFloat(10^acc)).
  * Succeeds iff that product is an integer with |v| < 2^53 (the domain on which the
  * reference's float64 / Redis long-double arithmetic is exact integer arithmetic);
- * otherwise GOME_E_INVAL (e.g. 0.123456789 at acc 8). */
+ * otherwise GOME_E_INVAL (e.g. 0.123456789 at acc 8).  Use it on a
+ * gRPC OrderRequest (main.go:41 -> NewOrderNode). */
 gome_status gome_fixed_from_double(double x, uint32_t accuracy, int64_t* out);
+/* An OrderNode consumed from the doOrder queue already carries the scaled value
+ * (NewOrderNode ran at gRPC time, main.go:41, ordernode.go:76-87): accept it iff it is
+ * an integer-valued float64 with |v| < 2^53 (the exact domain), else GOME_E_INVAL. */
+gome_status gome_fixed_from_scaled(double scaled, int64_t* out);
 /* Render one event as the reference's MatchResult JSON (Go encoding/json of
  * engine.MatchResult, byte-identical).  Strings are the host's interned names;
- * `taker` is the record at event->taker_seq.  Returns bytes written (excl. NUL)
- * or a negative value if cap is too small. */
+ * `taker` is the record of the event's taker.  tx_table maps Transaction codes
+ * (gome_order.side, gome_event.maker_side) to the raw int32 Transaction values to echo;
+ * NULL = identity (codes 0..255 are the values).  Returns bytes written (excl. NUL) or
+ * a negative value if cap is too small. */
 int64_t gome_render_match_result(const gome_event* ev, const gome_order* taker,
                                  uint32_t accuracy, const char* symbol,
                                  const char* taker_uuid, const char* taker_oid,
                                  const char* maker_uuid, const char* maker_oid,
-                                 const char* maker_next_oid, char* buf, size_t cap);
+                                 const char* maker_next_oid, const int32_t* tx_table,
+                                 char* buf, size_t cap);
+/* Render a batch's events (publish order) as newline-terminated MatchResult JSON lines, the
+ * bytes the reference publishes to matchOrder (engine.go:109-113,154-194), for the batching
+ * consumer's sink.  `batch` / seq_base: the submitted records and the batch's seq_base (the
+ * taker of an event is batch[seq - seq_base]).  Names are the host's interned strings indexed
+ * by id (sym_names[symbol_id], ...; n_* = table sizes).  Returns bytes written, or
+ * -(bytes needed) when cap is too small, or INT64_MIN on a bad id. */
+int64_t gome_render_events(const gome_event* ev, size_t n, const gome_order* batch, size_t batch_n,
+                           uint64_t seq_base, uint32_t accuracy, const char* const* sym_names,
+                           size_t n_sym, const char* const* uuid_names, size_t n_uuid,
+                           const char* const* oid_names, size_t n_oid, const int32_t* tx_table,
+                           char* buf, size_t cap);
 /* Render one resting node as the reference stores it in S:link:<price> under
  * S:node:<oid> (nodelink.go:119-122; Go encoding/json of engine.OrderNode, byte-identical):
  * the ADD that rested with its remaining volume, IsFirst / IsLast / PrevNode / NextNode from
- * its FIFO neighbours (NULL = none).  Used by the snapshot writer (gome_amd/snapshot.py,
- * SURVEY 8f rank 2).  Returns bytes written (excl. NUL) or a negative value. */
-int64_t gome_render_link_node(const char* symbol, int64_t price_fx, uint32_t side, int64_t volume_fx,
+ * its FIFO neighbours (NULL = none).  `transaction` is the raw int32 value.  Used by the
+ * snapshot writer (gome_amd/snapshot.py).  Returns bytes written (excl.
+ * NUL) or a negative value. */
+int64_t gome_render_link_node(const char* symbol, int64_t price_fx, int32_t transaction, int64_t volume_fx,
                               uint32_t accuracy, const char* uuid, const char* oid,
                               const char* prev_oid, const char* next_oid, char* buf, size_t cap);
 

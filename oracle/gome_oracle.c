@@ -11,6 +11,10 @@
  * on a fake Redis (tests/test_oracle_parity.py), and against the committed
  * fixtures under tests/golden/ that literal.py generated.
  *
+ * ABI v4 record flags: GOME_ORD_ADM_HOST records take their admission verdict from
+ * GOME_ORD_ADMITTED (the consumer's pre-pool markers, gome_amd/consumer.py) instead of the
+ * batch rule, exactly as the engine's k_adm_flag does.
+ *
  * Model, per symbol S:
  *   - a price-keyed level table shared by both sides: depth (S:depth field,
  *     nodepool.go:61-68) and one FIFO (S:link:<price>, nodelink.go), plus one
@@ -311,7 +315,9 @@ int oracle_submit(oracle* o, const gome_order* r, uint64_t n) {
     o->st.n_orders++;
     if (q->action == GOME_ADD) {
       o->st.n_add++;
-      if (!adm_first(o, q)) { o->st.n_dropped++; continue; } /* engine.go:58-62 */
+      int adm = adm_first(o, q); /* engine.go:58-62 (batch model) */
+      if (q->flags & GOME_ORD_ADM_HOST) adm = (q->flags & GOME_ORD_ADMITTED) != 0; /* host markers */
+      if (!adm) { o->st.n_dropped++; continue; }
       do_add(o, q, (uint32_t)i);
     } else if (q->action == GOME_DEL) {
       o->st.n_del++;

@@ -16,6 +16,23 @@ class Interner:
     def __init__(self):
         self.fwd: dict[str, dict[str, int]] = {"sym": {}, "uuid": {}, "oid": {}}
         self.rev: dict[str, list[str]] = {"sym": [], "uuid": [], "oid": []}
+        self.tx_fwd = {0: 0, 1: 1}  # Transaction value -> code (gome_abi.h), 1 = SALE
+        self.tx_rev = [0, 1]
+
+    def tx_code(self, raw: int) -> int:
+        raw = int(raw)
+        if raw not in self.tx_fwd:
+            if len(self.tx_rev) == 256:
+                raise ValueError("more than 254 distinct Transaction values outside {0, 1}")
+            self.tx_fwd[raw] = len(self.tx_rev)
+            self.tx_rev.append(raw)
+        return self.tx_fwd[raw]
+
+    def tx_raw(self, code: int) -> int:
+        return self.tx_rev[int(code)] if int(code) < len(self.tx_rev) else int(code)
+
+    def tx_table(self):
+        return self.tx_rev
 
     def id(self, kind: str, s: str) -> int:
         d = self.fwd[kind]
@@ -37,7 +54,7 @@ def requests_to_records(batch, names: Interner, accuracy: int = 8) -> np.ndarray
         rec[i]["symbol_id"] = names.id("sym", r["symbol"])
         rec[i]["oid_id"] = names.id("oid", r["oid"])
         rec[i]["uuid_id"] = names.id("uuid", r["uuid"])
-        rec[i]["side"] = r["transaction"]
+        rec[i]["side"] = names.tx_code(r["transaction"])
         rec[i]["action"] = action
     return rec
 
@@ -54,7 +71,7 @@ def render_events(events: np.ndarray, records: np.ndarray, names: Interner,
             None if cancel else names.name("uuid", int(e["maker_uuid_id"])),
             None if cancel else names.name("oid", int(e["maker_oid_id"])),
             None if (cancel or e["maker_is_last"]) else names.name("oid", int(e["maker_next_oid_id"])),
-            accuracy))
+            accuracy, tx_table=names.tx_table()))
     return out
 
 
@@ -139,7 +156,7 @@ def engine_state_to_levels(eng, sym_id: int, names: Interner) -> dict:
         nodes = eng.fifo(sym_id, p)
         out[p] = (int(lv["depth_fx"]), bool(lv["in_buy"]), bool(lv["in_sale"]),
                   [(names.name("oid", int(n["oid_id"])), names.name("uuid", int(n["uuid_id"])),
-                    int(n["side"]), int(n["volume_fx"])) for n in nodes])
+                    names.tx_raw(int(n["side"])), int(n["volume_fx"])) for n in nodes])
     return out
 
 

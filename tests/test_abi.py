@@ -17,7 +17,7 @@ def test_library_exports_every_declared_symbol():
     assert len(names) >= 14
     for n in names:
         assert hasattr(lib, n), n
-    assert lib.gome_abi_version() == 3
+    assert lib.gome_abi_version() == 4
 
 
 def test_record_layouts_match_header():
@@ -65,3 +65,51 @@ def test_create_without_gpu_fails_loudly():
     with pytest.raises(abi.GomeError) as ei:
         abi.Engine(max_symbols=4, max_batch=16)
     assert ei.value.status == abi.GOME_E_DEVICE
+
+
+# ---- ABI v4 boundary fixes ------------------------------------------------------------
+@pytest.mark.parametrize("v", [0.0, 1.0, 50000000.0, 29000000.0, 2.0 ** 53 - 1, -12345.0, 1e15])
+def test_fixed_from_scaled_accepts_exact_integers(v):
+    """doOrder-queue OrderNodes carry Price / Volume already scaled at gRPC time (main.go:41,
+    ordernode.go:76-87): the consumer checks, it does not re-scale."""
+    assert abi.fixed_from_scaled(v) == int(v)
+
+
+@pytest.mark.parametrize("v", [0.5, 28999999.999999996, 2.0 ** 53, -(2.0 ** 53), math.nan, math.inf, 1e300])
+def test_fixed_from_scaled_rejects_non_integers(v):
+    with pytest.raises(abi.GomeError):
+        abi.fixed_from_scaled(v)
+
+
+def test_scaled_path_equals_decimal_path():
+    """NewOrderNode's scaling (literal.scale) then gome_fixed_from_scaled == the decimal path."""
+    rng = np.random.default_rng(3)
+    for k in rng.integers(1, 10**6, 500):
+        x = round(float(k) / 100, 2)
+        assert abi.fixed_from_scaled(scale(x, 8)) == abi.fixed_from_double(x, 8)
+
+
+def test_q8_transaction_257_kat_vs_literal():
+    """Q8: Transaction values outside {0,1} (257, -3, 2^31-1) are BUY and echoed raw
+    (ordernode.go:95, nodepool.go:89).  Records carry interned codes; the renderer maps them
+    back through the tx table.  JSON byte-identical to the literal transliteration."""
+    from oracle.literal import run_batches
+    from oracle.pyoracle import Oracle
+    from tests.helpers import Interner, render_events, requests_to_records
+    req = lambda a, oid, tx, p, v: (a, dict(uuid="u1", oid=str(oid), symbol="eth2usdt",
+                                            transaction=tx, price=p, volume=v))
+    batches = [[req(1, 1, 1, 0.5, 1.0), req(1, 2, 257, 0.6, 0.25), req(1, 3, -3, 0.5, 0.5),
+                req(1, 4, 2**31 - 1, 0.4, 0.3)],
+               [req(1, 5, 1, 0.3, 2.0), req(2, 4, 2**31 - 1, 0.4, 0.3), req(1, 6, 257, 0.7, 0.1)]]
+    _, lit = run_batches(batches)
+    names = Interner()
+    names.id("sym", "eth2usdt")
+    orc = Oracle(1)
+    got = []
+    for b in batches:
+        rec = requests_to_records(b, names)
+        assert set(rec["side"]) <= set(range(5))
+        got += render_events(orc.submit(rec), rec, names)
+    assert got == lit
+    assert any('"Transaction":257' in j for j in got)
+    assert any('"Transaction":2147483647' in j for j in got)

@@ -15,6 +15,7 @@ import torch.multiprocessing as mp
 
 import bench
 from gome_amd import workload as wl
+from gome_amd.publisher import SUMMARY_FIELDS, SummaryPublisher
 from oracle.pyoracle import Oracle
 
 
@@ -84,9 +85,14 @@ def _worker(rank, world, port, out_dir):
               "n_resting": 5 + rank, "max_segment": 77 + rank}
         summary = torch.zeros(32, dtype=torch.int64)
         gathered = torch.zeros(32 * world, dtype=torch.int64)
-        bench.gather_summary(st, summary, gathered)
+        pub = SummaryPublisher(world)
+        for step in range(3):  # the rank-0 publisher consumes every step's gathered summaries
+            bench.gather_summary(st, summary, gathered, rank, step)
+            pub.consume(gathered)
+        ok = pub.check(3 * (2000 + 1), 3 * 10, 3 * 20)
         np.save(os.path.join(out_dir, f"r{rank}.npy"),
-                np.array([o, f, e, el] + lat + gathered.tolist(), dtype=np.float64))
+                np.array([o, f, e, el] + lat + gathered.tolist() + [float(ok), float(pub.steps)],
+                         dtype=np.float64))
     finally:
         dist.destroy_process_group()
 
@@ -96,12 +102,15 @@ def test_gloo_world2_reductions():
     with tempfile.TemporaryDirectory() as d:
         mp.spawn(_worker, args=(world, _free_port(), d), nprocs=world, join=True)
         res = [np.load(os.path.join(d, f"r{r}.npy")) for r in range(world)]
+    idx = {f: i for i, f in enumerate(SUMMARY_FIELDS)}
     for r in res:
         o, f, e, el = r[:4]
         assert o == 300.0 and f == 30.0 and e == 14.0   # sums over ranks
         assert el == 2.5                                 # max elapsed
         assert list(r[4:6]) == [2.0, 5.0]                # per-step max latency
-        g = r[6:].reshape(world, 32)
+        g = r[6:6 + 32 * world].reshape(world, 32)
         for rk in range(world):
-            assert list(g[rk, :5]) == [1000 + rk, 10 * rk, 20 * rk, 5 + rk, 77 + rk]
+            row = [g[rk, idx[k]] for k in ("n_orders", "n_fills", "n_events", "n_resting", "max_segment", "rank", "step")]
+            assert row == [1000 + rk, 10 * rk, 20 * rk, 5 + rk, 77 + rk, rk, 2]
+        assert r[-2] == 1.0 and r[-1] == 3.0             # publisher totals == job totals
     assert res[0].tobytes() == res[1].tobytes()

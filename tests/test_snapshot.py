@@ -87,8 +87,9 @@ def test_resume_from_snapshot_continues_identically(seed):
     rng, lit, eng, names = _run(700 + seed, quirks=False)
     sids = [names.id("sym", s) for s in SYMBOLS]
     snap = snapshot.redis_snapshot(eng, sids, names)
-    eng2 = Engine(max_symbols=len(SYMBOLS), max_batch=4096, max_nodes=1 << 16, max_levels=1 << 14)
-    snapshot.restore(eng2, snap, names)
+    # a small max_batch: the replay is split into chunks (FIFO order kept across them)
+    eng2 = Engine(max_symbols=len(SYMBOLS), max_batch=16, max_nodes=1 << 16, max_levels=1 << 14)
+    assert snapshot.restore(eng2, snap, names) > 16
     assert snapshot.redis_snapshot(eng2, sids, names) == snap
     nxt = random_batches(rng, n_batches=1, batch=150, symbols=SYMBOLS, del_frac=0.25, quirks=False,
                          oid_base=10**6)
@@ -121,3 +122,25 @@ def test_restore_refuses_quirk_books():
     assert "50000000" in snap["zset"]["eth2usdt:BUY"]
     with pytest.raises(GomeError):
         snapshot.restore_records(snap, names)
+
+
+def test_restore_refuses_crossed_book_before_submitting():
+    """A snapshot whose best bid >= best ask would fill on replay: refused while validating,
+    before any record reaches an engine."""
+    names = Interner()
+    names.id("sym", "s")
+    names.id("uuid", "u")
+    node = lambda oid, tx, p, v, prev, nxt: render_link_node("s", p, tx, v, "u", oid, prev, nxt)
+    snap = {"hash": {"s:depth": {"s:depth:60000000": "100000000", "s:depth:50000000": "100000000"},
+                     "s:link:60000000": {"f": "s:node:a", "l": "s:node:a",
+                                         "s:node:a": node("a", 0, 60000000, 100000000, None, None)},
+                     "s:link:50000000": {"f": "s:node:b", "l": "s:node:b",
+                                         "s:node:b": node("b", 1, 50000000, 100000000, None, None)}},
+            "zset": {"s:BUY": {"60000000": 6e7}, "s:SALE": {"50000000": 5e7}}}
+    with pytest.raises(GomeError, match="crossed"):
+        snapshot.restore_records(snap, names)
+    snap["zset"] = {"s:BUY": {"50000000": 5e7}, "s:SALE": {"60000000": 6e7}}
+    snap["hash"]["s:link:60000000"]["s:node:a"] = node("a", 1, 60000000, 100000000, None, None)
+    snap["hash"]["s:link:50000000"]["s:node:b"] = node("b", 0, 50000000, 100000000, None, None)
+    rec = snapshot.restore_records(snap, names)
+    assert len(rec) == 2

@@ -235,7 +235,7 @@ def main():
     keep = 0.3 if args.workload == "config3" else 0.5
     eng = Engine(max_symbols=n_symbols, max_batch=per_rank,
                  max_nodes=max(1 << 20, int(total_orders * keep)),
-                 max_levels=max(1 << 22, 64 * n_symbols), device=local)
+                 max_levels=max(1 << 22, (256 if n_symbols <= 100000 else 128) * n_symbols), device=local)
 
     summary = torch.zeros(SUMMARY_WORDS, dtype=torch.int64, device="cuda")
     gathered = torch.zeros(SUMMARY_WORDS * world, dtype=torch.int64, device="cuda")

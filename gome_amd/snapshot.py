@@ -164,10 +164,11 @@ def restore_records(snap: dict, names) -> np.ndarray:
     return out
 
 
-def restore(eng, snap: dict, names, seq_base: int = 0) -> int:
-    """Rebuild the snapshot's books in an engine (resume).  Returns the orders replayed."""
+def restore(eng, snap: dict, names, seq_base: int = 0, chunk: int | None = None) -> int:
+    """Rebuild the snapshot's books in an engine (resume), in submits of at most the engine's
+    max_batch (or `chunk`) records.  Returns the orders replayed."""
     rec = restore_records(snap, names)  # (validated, crossed books refused: nothing applied yet)
-    step = max(1, int(getattr(eng, "max_batch", len(rec) or 1)))
+    step = max(1, min(int(getattr(eng, "max_batch", len(rec) or 1)), chunk or (1 << 62)))
     for i in range(0, len(rec), step):  # FIFO order is kept across chunks
         eng.submit(rec[i:i + step], seq_base + i)
         ev = eng.drain()

@@ -87,9 +87,9 @@ def test_resume_from_snapshot_continues_identically(seed):
     rng, lit, eng, names = _run(700 + seed, quirks=False)
     sids = [names.id("sym", s) for s in SYMBOLS]
     snap = snapshot.redis_snapshot(eng, sids, names)
-    # a small max_batch: the replay is split into chunks (FIFO order kept across them)
-    eng2 = Engine(max_symbols=len(SYMBOLS), max_batch=16, max_nodes=1 << 16, max_levels=1 << 14)
-    assert snapshot.restore(eng2, snap, names) > 16
+    # replayed in chunks of 16 records (FIFO order kept across them)
+    eng2 = Engine(max_symbols=len(SYMBOLS), max_batch=4096, max_nodes=1 << 16, max_levels=1 << 14)
+    assert snapshot.restore(eng2, snap, names, chunk=16) > 16
     assert snapshot.redis_snapshot(eng2, sids, names) == snap
     nxt = random_batches(rng, n_batches=1, batch=150, symbols=SYMBOLS, del_frac=0.25, quirks=False,
                          oid_base=10**6)

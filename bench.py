@@ -252,6 +252,7 @@ def main():
         b = dev_batches[i]
         eng.submit_device(b.data_ptr(), per_rank, seq_base=seq[0])
         seq[0] += per_rank
+        eng.release_device_events()  # events stay in HBM (a device-side consumer's input)
         st = eng.stats()
         publish(st, i)
         return st

@@ -88,6 +88,8 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.gome_pending_events.argtypes = [VP]
     lib.gome_pending_events.restype = C.c_size_t
     lib.gome_device_events.argtypes = [VP, P(VP), P(C.c_size_t)]
+    lib.gome_release_device_events.argtypes = [VP]
+    lib.gome_release_device_events.restype = C.c_int32
     lib.gome_get_stats.argtypes = [VP, P(Stats)]
     lib.gome_snapshot_levels.argtypes = [VP, C.c_uint32, VP, C.c_size_t, P(C.c_size_t)]
     lib.gome_snapshot_fifo.argtypes = [VP, C.c_uint32, C.c_int64, VP, C.c_size_t, P(C.c_size_t)]
@@ -256,6 +258,10 @@ class Engine:
         p, n = C.c_void_p(), C.c_size_t()
         self._check(self.lib.gome_device_events(self.h, C.byref(p), C.byref(n)))
         return p.value, n.value
+
+    def release_device_events(self):
+        """The caller consumed the last device batch's events on the device."""
+        self._check(self.lib.gome_release_device_events(self.h))
 
     def stats(self) -> dict:
         st = Stats()

@@ -914,6 +914,12 @@ gome_status gome_device_events(gome_engine* e, const gome_event** dev_ptr, size_
   return GOME_OK;
 }
 
+gome_status gome_release_device_events(gome_engine* e) {
+  if (!e) return GOME_E_INVAL;
+  e->dev_events = e->dev_events_pos = 0;
+  return GOME_OK;
+}
+
 gome_status gome_get_stats(const gome_engine* e, gome_stats* out) {
   if (!e || !out) return GOME_E_INVAL;
   *out = e->stats;

@@ -212,6 +212,9 @@ size_t gome_pending_events(const gome_engine* e);
 /* Device pointer + count of the last device batch's events (valid until next submit). */
 gome_status gome_device_events(gome_engine* e, const gome_event** dev_ptr,
                                size_t* n);
+/* A device-side consumer has taken the last device batch's events (read through
+ * gome_device_events): the next submit need not move them to the host drain queue. */
+gome_status gome_release_device_events(gome_engine* e);
 gome_status gome_get_stats(const gome_engine* e, gome_stats* out);
 
 /* ---- pipelined host path (ABI >= 4) ---------------------------------------- */

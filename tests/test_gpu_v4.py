@@ -119,6 +119,15 @@ def test_device_events_never_dropped():
     eng.submit(b2)  # before draining the device batch
     e2 = orc.submit(b2)
     _cmp(eng.drain(), np.concatenate([e1, e2]), "device then host")
+    # released device events are not moved to the host queue
+    b3, b4 = st.batch(1000), st.batch(1000)
+    t3 = torch.from_numpy(b3.view(np.uint8).copy()).cuda()
+    torch.cuda.synchronize()
+    eng.submit_device(t3.data_ptr(), len(b3))
+    orc.submit(b3)
+    eng.release_device_events()
+    eng.submit(b4)
+    _cmp(eng.drain(), orc.submit(b4), "after release")
 
 
 def test_pipelined_async_equals_oracle():

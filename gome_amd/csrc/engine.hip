@@ -338,8 +338,11 @@ gome_status gome_engine::init(const gome_config& c) {
   // ---- per-batch buffers
   const uint32_t nb = max_batch;
   adm_mask = static_cast<uint32_t>(next_pow2(2ull * nb + 16) - 1);
+  // events of one batch <= one partial per ADD + one per DEL + one per popped maker (<= the
+  // resting capacity + the batch's rests) + block padding: sized once, so a pipelined
+  // submit never waits to regrow it (HBM is plentiful; the regrowth path stays as a fallback)
   uint64_t evcap = cfg.max_events ? cfg.max_events
-                                  : 2ull * nb + EVB * std::min<uint64_t>(nb, ms) + 1024;
+                                  : 2ull * nb + cfg.max_nodes + EVB * std::min<uint64_t>(nb, ms) + 1024;
   if (evcap > 0xF0000000ull) evcap = 0xF0000000ull;
   arena_cap = static_cast<uint32_t>(evcap);
   if (!alloc(&d_k0, nb, "keys0") || !alloc(&d_v0, nb, "vals0") ||

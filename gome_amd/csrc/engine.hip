@@ -33,6 +33,7 @@
 #include "device.h"
 #include "match_cold.h"
 #include "match_flow.h"
+#include "match_flow_cancel.h"
 #include "match_hot.h"
 #include "pipeline.h"
 #include "wave.h"
@@ -195,6 +196,8 @@ struct gome_engine {
   gome_stats stats{};
   unsigned long long resting = 0, levels = 0;
   unsigned long long idx_tomb = 0, n_rebuilds = 0;  // tombstones (upper bound) since the last rebuild
+  uint32_t fc_gen = 0;            // batch generation of the cancel books' (symbol, oid) table
+  unsigned long long fc_hcap = 0;  // its entries
   bool poisoned = false;
   std::string err;
   std::vector<void*> allocs;
@@ -290,6 +293,9 @@ gome_status gome_engine::init(const gome_config& c) {
   }
   HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_match_hot),
                              hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(HOT_LDS_BYTES)));
+  // the head plans hold a cancel book's LDS ring (match_flow_cancel.h)
+  for (const void* k : {reinterpret_cast<const void*>(k_flow_plan_head), reinterpret_cast<const void*>(k_flow_plan_near)})
+    HIPCHK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(FC_HEAD_LDS)));
 
   max_batch = cfg.max_batch;
   uint32_t ms = cfg.max_symbols;
@@ -368,13 +374,22 @@ gome_status gome_engine::init(const gome_config& c) {
       !alloc(&F.ord8, static_cast<uint64_t>(FL_ORD8_MUL) * nb + FL_ORD8_PAD, "flow records") || !alloc(&F.log, ntouch, "flow touch log") ||
       !alloc(&F.srt, ntouch, "flow level runs") || !alloc(&F.rs, ntouch, "flow new makers") ||
       !alloc(&F.fbase, ntouch, "flow fill bases") || !alloc(&F.ig, F.ig_cap, "flow gathered makers") ||
-      !alloc(&F.ig_bump, 1, "flow gather bump") || !alloc(&F.toff, MAX_FLOW + 16, "flow touch offsets") ||
+      !alloc(&F.ig_bump, 1, "flow gather bump") || !alloc(&F.toff, 2 * FC_TOFF, "flow touch offsets") ||
       !alloc(&F.lvout, static_cast<size_t>(MAX_FLOW) * FL_CAP, "flow final levels"))
     return GOME_E_CAPACITY;
   F.maxt = ceil_div(ntouch, FL_TILE);
   if (!alloc(&F.tcnt, static_cast<size_t>(FL_HEAD) * F.maxt * FL_CAP, "flow head tile counts") ||
       !alloc(&F.pscr, FL_HEAD, "flow head prep scratch"))
     return GOME_E_CAPACITY;
+  // books with DELs (match_flow_cancel.h): ring images, per-position scratch, the (symbol, oid)
+  // table (generation-tagged: cleared once per 2048 batches)
+  fc_hcap = next_pow2(std::max<unsigned long long>(2ull * nb, 1024));
+  F.fc_hmask = fc_hcap - 1;
+  if (!alloc(&F.fc_img, fc_img_off(MAX_FLOW), "flow cancel ring images") || !alloc(&F.fc_del, nb, "flow cancel records") ||
+      !alloc(&F.fc_tg, nb, "flow cancel targets") || !alloc(&F.fc_rank, nb, "flow cancel ranks") ||
+      !alloc(&F.fc_hash, fc_hcap, "flow cancel table"))
+    return GOME_E_CAPACITY;
+  HIPCHK(hipMemsetAsync(F.fc_hash, 0, sizeof(FcHash) * fc_hcap, stream));
   HIPCHK(hipMemsetAsync(F.hdr, 0, sizeof(FlowHdr) * MAX_FLOW, stream));
   HIPCHK(hipMemsetAsync(d_pend, 0, sizeof(PendEnt) * nb, stream));
   if (D.idx_mask >= PEND) return fail(GOME_E_INVAL, "gome_config.max_nodes too large (index > 2^31 slots)");
@@ -437,6 +452,8 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   HIPCHK(hipStreamWaitEvent(flow_stream, fork_adm, 0));
   HIPCHK(hipMemsetAsync(d_claim, 0, (adm_mask + 1ull) * 4, flow_stream));
   HIPCHK(hipMemsetAsync(d_amin, 0xFF, (adm_mask + 1ull) * 4, flow_stream));
+  if ((++fc_gen & FC_GEN_MASK) == 0) HIPCHK(hipMemsetAsync(F.fc_hash, 0, sizeof(FcHash) * fc_hcap, flow_stream));
+  F.fc_gen = fc_gen;
   k_adm<<<gN, T256, 0, flow_stream>>>(d_ord, n, d_claim, d_amin, d_adm_slot, adm_mask, cfg.max_symbols, d_st);
   k_adm_flag<<<gN, T256, 0, flow_stream>>>(d_ord, n, d_adm_slot, d_amin);
   HIPCHK(hipEventRecord(adm_done, flow_stream));
@@ -500,6 +517,9 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   FH0.h0 = 0; FH0.h1 = 1; FH0.tb = 0;
   FH1.h0 = 1; FH1.h1 = FL_HEAD; FH1.tb = 2;
   FT.h0 = FL_HEAD; FT.h1 = MAX_FLOW; FT.tb = FL_HEAD + 3;
+  // the ranges' books with DELs count and place their events through a second toff region
+  FlowArgs FH0c = FH0, FH1c = FH1, FTc = FT;
+  FH0c.tb += FC_TOFF; FH1c.tb += FC_TOFF; FTc.tb += FC_TOFF;
   const uint32_t nh_head = std::min<uint32_t>(FL_HEAD, nhot_max);
   const uint32_t nh_near = nh_head > 1 ? nh_head - 1 : 0;
   const uint32_t nh_tail = nhot_max > FL_HEAD ? nhot_max - FL_HEAD : 0;
@@ -511,9 +531,21 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   k_flow_prep_a<<<dim3(FL_PG, nh_head), FL_PREP_T, 0, flow_stream>>>(D, B, FH);
   k_flow_prep_b<<<nh_head, FL_PREP_T, 0, flow_stream>>>(D, B, FH);
   k_flow_prep_c<<<dim3(FL_PG, nh_head), FL_PREP_T, 0, flow_stream>>>(D, B, FH);
+  // books with DELs: targets, windows, ring images, W32C records (or back to the legacy path)
+  auto cancel_prep = [&](const FlowArgs& R, uint32_t nb, uint32_t px, bool wide, hipStream_t st) {
+    k_fc_hash_claim<<<dim3(px, nb), 256, 0, st>>>(D, B, R);
+    k_fc_hash_count<<<dim3(px, nb), 256, 0, st>>>(D, B, R);
+    k_fc_resolve<<<dim3(px, nb), 256, 0, st>>>(D, B, R);
+    if (wide) k_fc_oldwalk_wide<<<dim3(FL_CAP, nb), 64, 0, st>>>(D, R);
+    else k_fc_oldwalk_book<<<nb, 1024, 0, st>>>(D, R);
+    k_fc_pass<<<nb, FC_PASS_T, 0, st>>>(D, B, R);
+    k_fc_unmark<<<dim3(px, nb), 256, 0, st>>>(D, B, R);
+    k_fc_route<<<ceil_div(nb, 256), 256, 0, st>>>(D, R);
+  };
+  cancel_prep(FH, nh_head, FL_PG, true, flow_stream);
   HIPCHK(hipEventRecord(prep_h, flow_stream));
   HIPCHK(hipEventRecord(S.evf0, flow_stream));
-  k_flow_plan_head<<<1, 256, 0, flow_stream>>>(D, FH0);
+  k_flow_plan_head<<<1, 256, FC_HEAD_LDS, flow_stream>>>(D, FH0);
   HIPCHK(hipEventRecord(S.evf1, flow_stream));
   // ---- admission markers (k_adm, launched above on the flow stream)
   HIPCHK(hipStreamWaitEvent(s, adm_done, 0));
@@ -534,12 +566,22 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
     k_flow_sort_scan<<<nb, FL_CAP, 0, st>>>(D, R);
     k_flow_sort_scatter<<<dim3(FL_SORT_GRID, nb), FL_TILE, 0, st>>>(D, R);
     k_flow_level_wide<<<dim3(FL_CAP, nb), 64, 0, st>>>(D, R);
-    k_flow_toff<<<1, 1024, 0, st>>>(D, R);
+    k_flow_toff<FL_OK_ADD><<<1, 1024, 0, st>>>(D, R);
     k_flow_count<<<1024, 256, 0, st>>>(D, B, R);
     k_flow_write_lv<<<dim3(FL_CAP, nb), 64, 0, st>>>(D, B, R);
     k_flow_write_fin<<<nb, 128, 0, st>>>(D, R);
   };
+  // books with DELs (match_flow_cancel.h); their events go to the arena
+  auto head_recon_c = [&](const FlowArgs& R, const FlowArgs& Rc, uint32_t nb, hipStream_t st) {
+    k_fc_level_wide<<<dim3(FL_CAP, nb), 64, 0, st>>>(D, R);
+    k_flow_toff<FL_OK_CANCEL><<<1, 1024, 0, st>>>(D, Rc);
+    k_fc_count<<<1024, 256, 0, st>>>(D, B, Rc);
+    k_fc_write_lv<<<dim3(FL_CAP, nb), 64, 0, st>>>(D, B, Rc);
+    k_fc_fin<<<nb, 128, 0, st>>>(D, Rc);
+    k_fc_events<<<1024, 256, 0, st>>>(D, B, Rc);
+  };
   head_recon(FH0, 1, flow_stream);
+  head_recon_c(FH0, FH0c, 1, flow_stream);
   HIPCHK(hipEventRecord(joinf, flow_stream));
   // The tail's chain and the legacy hot kernels share the third stream: HIP maps more
   // streams than hardware queues (4 per process) onto shared queues, which would serialise
@@ -547,23 +589,31 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   HIPCHK(hipStreamWaitEvent(hot_stream, fork, 0));
   if (nh_tail) {
     k_flow_prep<<<nh_tail, FL_PREP_T, 0, hot_stream>>>(D, B, FT);
+    cancel_prep(FT, nh_tail, 1, false, hot_stream);
     HIPCHK(hipEventRecord(prep_t, hot_stream));
     k_flow_plan_tail<<<nh_tail, 64, 0, hot_stream>>>(D, FT);
+    k_flow_plan_tail_c<<<nh_tail, 64, FC_TAIL_LDS, hot_stream>>>(D, FT);
     k_flow_sort<<<nh_tail, FL_SORT_T, 0, hot_stream>>>(D, FT);
     k_flow_level<<<nh_tail, FL_LEVEL_T, 0, hot_stream>>>(D, FT);
-    k_flow_toff<<<1, 1024, 0, hot_stream>>>(D, FT);
+    k_flow_toff<FL_OK_ADD><<<1, 1024, 0, hot_stream>>>(D, FT);
     k_flow_count<<<1024, 256, 0, hot_stream>>>(D, B, FT);
     k_flow_write<<<nh_tail, FL_WRITE_T, 0, hot_stream>>>(D, B, FT);
     // the tail's events into the arena now (k_ev_scatter places them after the scan)
     k_flow_events_arena<<<1024, 256, 0, hot_stream>>>(D, B, FT);
+    k_fc_level_book<<<nh_tail, 1024, 0, hot_stream>>>(D, FT);
+    k_flow_toff<FL_OK_CANCEL><<<1, 1024, 0, hot_stream>>>(D, FTc);
+    k_fc_count<<<1024, 256, 0, hot_stream>>>(D, B, FTc);
+    k_fc_write_book<<<nh_tail, FL_WRITE_T, 0, hot_stream>>>(D, B, FTc);
+    k_fc_events<<<1024, 256, 0, hot_stream>>>(D, B, FTc);
   } else {
     HIPCHK(hipEventRecord(prep_t, hot_stream));
   }
   // the other head books: plan, reconstruction and events (into the arena) after the tail
   HIPCHK(hipStreamWaitEvent(hot_stream, prep_h, 0));
   if (nh_near) {
-    k_flow_plan_near<<<nh_near, 256, 0, hot_stream>>>(D, FH1);
+    k_flow_plan_near<<<nh_near, 256, FC_HEAD_LDS, hot_stream>>>(D, FH1);
     head_recon(FH1, nh_near, hot_stream);
+    head_recon_c(FH1, FH1c, nh_near, hot_stream);
     k_flow_events_arena<<<1024, 256, 0, hot_stream>>>(D, B, FH1);
   }
   // legacy hot path (books the flow path declined); it and the cold kernel read the preps'

@@ -588,6 +588,293 @@ class Gen:
         return self.out
 
 
+# ---- W32C: the 32-bit plan of a book whose segment holds DELs -------------
+# Record (8 B): lo = ADD volume in units of g | DEL: window length n_b [0,16) | log2 C_k [16,21);
+# hi = level [0,7) | ring slot p [7,21) | DEL: maker SALE bit 29, DEL bit 30 | SALE (ADD) or 1
+# (DEL) bit 31.  Per level the plan also keeps R_k, the volume that ever arrived (lane pair
+# v[36:37], W32 layout), and every ADD owns a 16-B LDS ring entry {end, v, xv} (non-targeted
+# ADDs a dummy one): cleared when the ADD is consumed, {E + T, T} when it rests.  A DEL of
+# target m at level k takes r = clamp(end_m - (R_k - depth_k) + Xb, 0, v_m) where Xb sums xv over
+# the ring window of the n_b targets that arrived behind m (ranks rank_m + 1 ..): each DEL sets
+# its target's xv = v_m.  Touch keys come from an order counter (JJS, as the 64-bit plan):
+# rest = JJS | k | 1 << 7, consume = JJS | k, cancel = JJS | k | 1 << 31 (amount r).
+CREG = {"R": (36, 37)}
+VA, VE, VV, VZ, VW, VX, VL = 38, 40, 41, 42, 46, 47, 48  # LDS address, end / v (an even pair),
+                                                          # zeros v[42:44], window address / data,
+                                                          # lane id (gfx950 tuples are even-aligned)
+X0, X1, X2, X3 = "s79", "s81", "s83", "s96"              # free in the 32-bit layout
+CLOBBERS_C = [f"v{i}" for i in range(36, 50)]
+
+
+class GenC(Gen):
+    def __init__(self):
+        super().__init__(32)
+
+    def decode(self, j: int):
+        """LI and SCC = SALE-or-DEL of record j; the order counter advances (JJS = index << 8)."""
+        e = self.e
+        hi = f"s{BUF[j][1]}"
+        e(f"s_add_u32 {JJS}, {JJS}, 256")
+        e(f"s_and_b32 {LI}, {hi}, 127")
+        e(f"s_bitcmp1_b32 {hi}, 31")
+
+    def ring_clear(self, j: int):
+        """The ADD's ring entry := {0, 0, 0} (a target that never rests holds v = 0) and its
+        address stays in lane 0 of v38 for the rest."""
+        e = self.e
+        hi = f"s{BUF[j][1]}"
+        e(f"s_lshr_b32 {T0}, {hi}, 3")
+        e(f"s_and_b32 {T0}, {T0}, 0x3fff0")
+        e("s_mov_b64 exec, 1")
+        e(f"v_mov_b32 v{VA}, {T0}")
+        e(f"ds_write_b96 v{VA}, v[{VZ}:{VZ + 2}]")
+
+    def dispatch(self, j: int, fall: bool, copy: bool = COPY_REST):
+        e = self.e
+        if j % HG == 0:
+            if not fall:
+                e(f"s_branch {self.lab(f'H{j}')}")
+            return
+        self.decode(j)
+        e(f"s_cbranch_scc1 {self.lab(f'S{j}')}")
+        if not fall:                               # slot j's BUY entry, inline
+            self.ring_clear(j)
+            e(f"s_cmp_le_u32 {BA}, {LI}")
+            e(f"s_cbranch_scc1 {self.lab(f'BXE{j}')}")
+            if copy:
+                self.rest("B", (f"s{BUF[j][0]}", f"s{BUF[j][1]}"))
+                self.dispatch((j + 1) % NS, False, False)
+            else:
+                e(f"s_branch {self.lab(f'BR{j}')}")
+
+    def cross_entry(self, T):
+        pass  # JJS is the order counter
+
+    def rest(self, side: str, T):
+        """The 32-bit rest, then R_k += T, the ring entry := {E + T, T} (E = R_k before)."""
+        e = self.e
+        buy = side == "B"
+        top, topd = (BB, BBD) if buy else (BA, BAD)
+        ge, gt = ("ge", "gt") if buy else ("le", "lt")
+        e(f"s_cmp_{ge}_u32 {LI}, {top}")
+        self.csel(X, T, 0)
+        self.csel(A, 0, T)
+        e(f"s_cmp_{gt}_u32 {LI}, {top}")
+        self.csel(A, topd, A)
+        e(f"s_cselect_b32 {L}, {top}, {LI}")
+        self.csel(topd, 0, topd)
+        e(f"s_{'max' if buy else 'min'}_u32 {top}, {top}, {LI}")
+        self.add(topd, topd, X)
+        self.add_lane("B" if buy else "A")
+        # arrivals R_k (lane pair k >> 1, word k & 1) and the maker's arrival coordinate
+        ev, od = CREG["R"]
+        e(f"s_lshr_b32 {T0}, {LI}, 1")
+        e(f"v_readlane_b32 {X0}, v{ev}, {T0}")
+        e(f"v_readlane_b32 {X1}, v{od}, {T0}")
+        e(f"s_bfm_b64 exec, 1, {T0}")
+        e(f"s_lshl_b32 {T0}, {LI}, 5")
+        e(f"s_mov_b32 s90, {T[0]}")                 # (s91 = 0)
+        e(f"s_lshl_b64 s[92:93], s[90:91], {T0}")
+        e(f"v_lshl_add_u64 v[{ev}:{od}], s[92:93], 0, v[{ev}:{od}]")
+        e(f"s_bitcmp1_b32 {LI}, 0")
+        e(f"s_cselect_b32 {X0}, {X1}, {X0}")
+        e(f"s_add_u32 {X0}, {X0}, {T[0]}")
+        e("s_mov_b64 exec, 1")
+        e(f"v_mov_b32 v{VE}, {X0}")
+        e(f"v_mov_b32 v{VV}, {T[0]}")
+        e(f"ds_write_b64 v{VA}, v[{VE}:{VV}]")
+        e(f"s_or_b32 {K}, {JJS}, {LI}")
+        e(f"s_bitset1_b32 {K}, 7")
+        self.log(K, T, False)
+
+    def reduce_window(self, dst: str):
+        """dst = sum of the window data over the wave (DPP scan, lane 63 = total)."""
+        e = self.e
+        v = f"v{VX}"
+        for ctl in ("row_shr:1 bound_ctrl:0", "row_shr:2 bound_ctrl:0", "row_shr:4 bound_ctrl:0",
+                    "row_shr:8 bound_ctrl:0", "row_bcast:15 row_mask:0xa", "row_bcast:31 row_mask:0xc"):
+            e("s_nop 1")
+            e(f"v_add_u32_dpp {v}, {v}, {v} {ctl}")
+        e("s_nop 1")
+        e(f"v_readlane_b32 {dst}, {v}, 63")
+
+    def window_read(self, lanes: str, first: str):
+        """window data = xv of ring slots pbase | ((first + lane) & mask) for lanes < `lanes`
+        (others 0); X2 = mask, X1 = pbase."""
+        e = self.e
+        e("s_mov_b64 exec, -1")
+        e(f"v_mov_b32 v{VX}, 0")
+        e(f"s_bfm_b64 exec, {lanes}, 0")
+        e(f"v_add_u32 v{VW}, {first}, v{VL}")
+        e(f"v_and_b32 v{VW}, {X2}, v{VW}")
+        e(f"v_or_b32 v{VW}, {X1}, v{VW}")
+        e(f"v_lshlrev_b32 v{VW}, 4, v{VW}")
+        e(f"ds_read_b32 v{VX}, v{VW} offset:8")
+
+    def del_path(self, i: int):
+        """DeleteOrder (engine.go:87-116) on the aggregates of level LI."""
+        e = self.e
+        lo, hi = f"s{BUF[i][0]}", f"s{BUF[i][1]}"
+        lab = self.lab
+        ev, od = CREG["R"]
+        aev, aod = PAIR["A"]
+        bev, bod = PAIR["B"]
+        e(f"{lab(f'D{i}')}:")
+        e(f"s_lshr_b32 {T0}, {hi}, 3")
+        e(f"s_and_b32 {T0}, {T0}, 0x3fff0")                 # target entry (byte address)
+        e("s_mov_b64 exec, 1")
+        e(f"v_mov_b32 v{VA}, {T0}")
+        e(f"ds_read_b64 v[{VE}:{VV}], v{VA}")                 # {end_m, v_m}
+        e(f"s_lshr_b32 {X3}, {T0}, 4")                        # p
+        e(f"s_lshr_b32 {X1}, {lo}, 16")
+        e(f"s_bfm_b32 {X2}, {X1}, 0")                         # mask = C_k - 1
+        e(f"s_andn2_b32 {X1}, {X3}, {X2}")                    # pbase
+        e(f"s_add_u32 {X3}, {X3}, 1")                         # first window rank (mod C_k)
+        e(f"s_and_b32 {X0}, {lo}, 0xffff")                    # n_b
+        e(f"s_lshr_b32 {T0}, {LI}, 1")
+        e(f"v_readlane_b32 s92, v{ev}, {T0}")
+        e(f"v_readlane_b32 s93, v{od}, {T0}")
+        e(f"v_readlane_b32 s84, v{aev}, {T0}")
+        e(f"v_readlane_b32 s85, v{aod}, {T0}")
+        e(f"v_readlane_b32 s94, v{bev}, {T0}")
+        e(f"v_readlane_b32 s95, v{bod}, {T0}")
+        slow, back = lab(f"DW{i}"), lab(f"DWB{i}")
+        e(f"s_cmp_gt_u32 {X0}, 63")
+        e(f"s_cbranch_scc1 {slow}")
+        self.window_read(X0, X3)
+        e("s_waitcnt lgkmcnt(0)")
+        e("s_mov_b64 exec, -1")
+        self.reduce_window("s90")
+        e(f"{back}:")
+        # (the window sum is in s90; {end_m, v_m} in lane 0 of v[39:40])
+        e(f"v_readlane_b32 {X1}, v{VE}, 0")
+        e(f"v_readlane_b32 {X2}, v{VV}, 0")
+        e(f"s_bitcmp1_b32 {LI}, 0")
+        e("s_cselect_b32 s92, s93, s92")                       # R_k
+        e("s_cselect_b32 s84, s85, s84")                       # ask lane word
+        e("s_cselect_b32 s94, s95, s94")                       # bid lane word
+        e(f"s_cmp_eq_u32 {LI}, {BA}")
+        e(f"s_cselect_b32 {X3}, {BAD[0]}, 0")
+        e(f"s_add_u32 s84, s84, {X3}")
+        e(f"s_cmp_eq_u32 {LI}, {BB}")
+        e(f"s_cselect_b32 {X3}, {BBD[0]}, 0")
+        e(f"s_add_u32 s84, s84, {X3}")
+        e("s_add_u32 s84, s84, s94")                           # depth_k (one side is 0)
+        e("s_sub_u32 s92, s92, s84")                           # G_k = R_k - depth_k
+        e(f"s_add_u32 {X1}, {X1}, s90")                        # end_m + Xb
+        e(f"s_sub_u32 {X1}, {X1}, s92")                        # SCC: negative
+        e(f"s_cselect_b32 {X1}, 0, {X1}")
+        e(f"s_min_u32 {X1}, {X1}, {X2}")                       # r
+        e("s_mov_b64 exec, 1")
+        e(f"ds_write_b32 v{VA}, v{VV} offset:8")               # xv_m = v_m (DELed)
+        e(f"s_cmp_eq_u32 {X1}, 0")
+        e(f"s_cbranch_scc1 {lab(f'DZ{i}')}")                   # not found: no event (:96-98)
+        e(f"s_or_b32 {K}, {JJS}, {LI}")
+        e(f"s_bitset1_b32 {K}, 31")
+        e(f"s_mov_b32 s90, {X1}")
+        self.log(K, ("s90", "s91"), False)
+        e(f"s_bitcmp1_b32 {hi}, 29")
+        e(f"s_cbranch_scc1 {lab(f'DA{i}')}")
+        for sd in ("B", "A"):
+            if sd == "A":
+                e(f"{lab(f'DA{i}')}:")
+            top, topd = (BB, BBD) if sd == "B" else (BA, BAD)
+            pev, pod = PAIR[sd]
+            e(f"s_cmp_eq_u32 {LI}, {top}")
+            e(f"s_cbranch_scc1 {lab(f'DT{sd}{i}')}")
+            # a level behind the cached top: lane word k -= r (64-bit add of -r << 32 * (k & 1))
+            e(f"s_lshr_b32 {T0}, {LI}, 1")
+            e(f"s_bfm_b64 exec, 1, {T0}")
+            e(f"s_lshl_b32 {T0}, {LI}, 5")
+            e(f"s_sub_u32 s94, 0, {X1}")
+            e("s_mov_b32 s95, -1")
+            e(f"s_lshl_b64 s[92:93], s[94:95], {T0}")
+            e(f"v_lshl_add_u64 v[{pev}:{pod}], s[92:93], 0, v[{pev}:{pod}]")
+            self.dispatch((i + 1) % NS, False)
+            # the cached top: its depth drops; emptied -> the next level of the side (ZREM)
+            e(f"{lab(f'DT{sd}{i}')}:")
+            e(f"s_sub_u32 {topd[0]}, {topd[0]}, {X1}")
+            e(f"s_cmp_eq_u32 {topd[0]}, 0")
+            e(f"s_cbranch_scc0 {lab(f'DZ{i}')}")
+            self.next_top(sd)
+            self.dispatch((i + 1) % NS, False)
+        e(f"{lab(f'DZ{i}')}:")
+        self.dispatch((i + 1) % NS, False)
+        # windows longer than 63: 64 lanes at a time (out of line)
+        blk = [f"{slow}:", "s_mov_b32 s90, 0", f"s_mov_b32 {K}, 0"]
+        self.slow.append(blk)
+        sv = self.out
+        self.out = blk
+        loop = lab(f"DWL{i}")
+        e(f"{loop}:")
+        e(f"s_sub_u32 {L}, {X0}, {K}")
+        e(f"s_min_u32 {L}, {L}, 63")
+        e(f"s_add_u32 {T0}, {X3}, {K}")
+        self.window_read(L, T0)
+        e("s_waitcnt lgkmcnt(0)")
+        e("s_mov_b64 exec, -1")
+        self.reduce_window(L)
+        e(f"s_add_u32 s90, s90, {L}")
+        e(f"s_add_u32 {K}, {K}, 63")
+        e(f"s_cmp_lt_u32 {K}, {X0}")
+        e(f"s_cbranch_scc1 {loop}")
+        e("s_waitcnt lgkmcnt(0)")
+        e(f"s_branch {back}")
+        self.out = sv
+
+    def slot(self, i: int):
+        e = self.e
+        lo, hi = f"s{BUF[i][0]}", f"s{BUF[i][1]}"
+        T = (lo, hi)
+        j = (i + 1) % NS
+        lab = self.lab
+        e(f"{lab(f'B{i}')}:")
+        self.ring_clear(i)
+        e(f"s_cmp_le_u32 {BA}, {LI}")
+        e(f"s_cbranch_scc1 {lab(f'BXE{i}')}")
+        e(f"{lab(f'BR{i}')}:")
+        self.rest("B", T)
+        self.dispatch(j, False)
+        e(f"{lab(f'BXE{i}')}:")
+        self.sub(D, T, BAD)
+        e(f"s_cbranch_scc0 {lab(f'BF{i}')}")
+        self.partial("B", T)
+        self.dispatch(j, False)
+        e(f"{lab(f'BF{i}')}:")
+        self.full("B", T, i)
+        e(f"{lab(f'SXE{i}')}:")
+        self.sub(D, T, BBD)
+        e(f"s_cbranch_scc0 {lab(f'SF{i}')}")
+        self.partial("S", T)
+        self.dispatch(j, False)
+        e(f"{lab(f'SF{i}')}:")
+        self.full("S", T, i)
+        e(f"{lab(f'DN{i}')}:")
+        self.dispatch(j, False)
+        self.del_path(i)
+        e(f"{lab(f'S{i}')}:")
+        e(f"s_bitcmp1_b32 {hi}, 30")
+        e(f"s_cbranch_scc1 {lab(f'D{i}')}")
+        self.ring_clear(i)
+        e(f"s_cmp_ge_u32 {BB}, {LI}")
+        e(f"s_cbranch_scc1 {lab(f'SXE{i}')}")
+        e(f"{lab(f'SR{i}')}:")
+        self.rest("S", T)
+        self.dispatch(j, j != 0)
+
+    def build(self) -> list[str]:
+        e = self.e
+        e("s_mov_b64 exec, -1")
+        e(f"v_mbcnt_lo_u32_b32 v{VL}, -1, 0")
+        e(f"v_mbcnt_hi_u32_b32 v{VL}, -1, v{VL}")
+        for r in range(VZ, VZ + 3):
+            e(f"v_mov_b32 v{r}, 0")
+        ev, od = CREG["R"]
+        e(f"v_mov_b32 v{ev}, %[rl0]")
+        e(f"v_mov_b32 v{od}, %[rl1]")
+        return super().build()
+
+
 ALIGN = int(os.environ.get("GOME_PLAN_ALIGN", "0"))   # log2 byte alignment of branch targets
 
 
@@ -606,12 +893,13 @@ def main():
     here = os.path.dirname(os.path.abspath(__file__))
     with open(os.path.join(here, "flow_plan_asm.inc"), "w") as f:
         f.write("// Generated by gen_plan_asm.py — do not edit.\n")
-        for w in (64, 32):
+        for w, g in ((64, Gen(64)), (32, Gen(32)), ("32C", GenC())):
             f.write(f"#define FL_PLAN_ASM{w} \\\n")
-            for line in aligned(Gen(w).build()):
+            for line in aligned(g.build()):
                 f.write(f'  "{line}\\n\\t" \\\n')
             f.write('  ""\n')
         f.write("#define FL_PLAN_CLOBBERS " + ", ".join(f'"{c}"' for c in CLOBBERS) + "\n")
+        f.write("#define FL_PLAN_CLOBBERS_C " + ", ".join(f'"{c}"' for c in CLOBBERS_C) + "\n")
 
 
 if __name__ == "__main__":

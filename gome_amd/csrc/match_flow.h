@@ -71,7 +71,12 @@ constexpr uint32_t OR_LI_SHIFT = 21, OR_SELL = 1u << 28;
 constexpr uint32_t FL_MAX_ORDERS = (1u << 23) - 8;  // order index (padding included) fits [8, 31) of a touch key
 constexpr unsigned long long OR_NOP = 0ull;
 
-enum : uint32_t { TK_CONS = 0, TK_REST = 1 };
+enum : uint32_t { TK_CONS = 0, TK_REST = 1, TK_CANC = 2 };
+// kind of a logged touch key (W32C cancel touches carry bit 31; W32 rest keys carry the SALE
+// bit there, so the flag is only read for books with DELs)
+__device__ __forceinline__ uint32_t tk_kind(uint32_t kr, bool cancel_book) {
+  return (cancel_book && (kr >> 31)) ? TK_CANC : ((kr >> 7) & 1u);
+}
 
 struct Touch {       // one level visited by one order (16 B)
   uint32_t kr;       // level [0,7) | kind << 7 | order index within the segment << 8
@@ -114,7 +119,14 @@ struct FlowHdr {
   unsigned long long amask[2], bmask[2];  // final S:SALE / S:BUY membership of the levels
   unsigned long long g;                   // volume unit of the book's plan (1 for the 64-bit plan)
   unsigned long long pad2;
+  // books whose segment holds DELs (ok == FL_OK_CANCEL, match_flow_cancel.h)
+  uint32_t ndel;       // DEL records of the segment
+  uint32_t nslot;      // LDS ring entries of the plan (16 B each, the dummy entry included)
+  uint32_t ncancel;    // cancels applied (DELs that found their maker)
+  uint32_t fc_bad;     // set by the cancel prep: decline the book (legacy / cold kernels)
 };
+// FlowHdr::ok: 0 declined, FL_OK_ADD an ADD-only flow book, FL_OK_CANCEL a book with DELs
+constexpr uint32_t FL_OK_ADD = 1, FL_OK_CANCEL = 2;
 
 struct FlowLvl {
   int64_t price;
@@ -132,8 +144,28 @@ struct FlowLvl {
   uint32_t nlive0;   // old makers surviving the batch
   uint32_t mem0;     // membership at batch start
   uint32_t pad0, pad1;
+  // books with DELs (match_flow_cancel.h): targets of the level's DELs in the plan's LDS ring
+  uint32_t c_old;    // old (pre-batch) makers targeted by a DEL of the batch
+  uint32_t cring;    // ring entries of the level (a power of two >= every window + 1)
+  uint32_t rbase;    // first ring entry of the level (aligned to cring)
+  uint32_t ocan;     // cancelled volume of old makers (plan units), set by the recon
 };
 static_assert(sizeof(FlowLvl) % 16 == 0, "FlowLvl alignment");
+
+// The cancel plan's LDS ring (match_flow_cancel.h): 16-B entries {end, v, xv, pad} per targeted
+// maker (+ one dummy entry), an image per book built by the cancel prep.
+constexpr uint32_t FC_HEAD_SLOTS = 9216;  // head books own their CU (144 KiB of LDS)
+constexpr uint32_t FC_TAIL_SLOTS = 1024;  // tail books (16 KiB)
+constexpr uint32_t FC_HEAD_LDS = FC_HEAD_SLOTS * 16, FC_TAIL_LDS = FC_TAIL_SLOTS * 16;
+constexpr uint32_t FC_TOFF = MAX_FLOW + 16;  // second toff region for books with DELs
+constexpr uint32_t FC_GEN_MASK = 0x7FF;   // generation bits of an FcHash key
+__host__ __device__ constexpr uint64_t fc_img_off(uint32_t h) {
+  return h < FL_HEAD ? static_cast<uint64_t>(h) * FC_HEAD_SLOTS
+                     : static_cast<uint64_t>(FL_HEAD) * FC_HEAD_SLOTS + static_cast<uint64_t>(h - FL_HEAD) * FC_TAIL_SLOTS;
+}
+
+struct FcDel;  // a DEL record's target (match_flow_cancel.h)
+struct FcHash;
 
 struct FlowArgs {
   FlowHdr* hdr;        // [MAX_HOT]
@@ -155,6 +187,14 @@ struct FlowArgs {
   // the candidates [h0, min(h1, nhot)) this launch covers (head and tail run on their own
   // streams), and the range's offset in toff
   uint32_t h0, h1, tb;
+  // books with DELs (match_flow_cancel.h)
+  uint4* fc_img;       // LDS ring images, fc_img_off(h)
+  FcDel* fc_del;       // [max_batch] per segment position: the DEL's target
+  uint32_t* fc_tg;     // [max_batch] per segment position: ADD targeted by the DEL at (value - 1)
+  uint32_t* fc_rank;   // [max_batch] per segment position: a targeted ADD's rank in its level
+  FcHash* fc_hash;     // (symbol, oid) table of the cancel books' records
+  uint64_t fc_hmask;
+  uint32_t fc_gen;     // batch generation (FcHash entries of older batches are empty)
 };
 
 __device__ __forceinline__ uint32_t fl_hend(const Dev& D, const FlowArgs& F) { return min(F.h1, D.st->nhot); }
@@ -200,7 +240,7 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep(Dev D, BatchArgs B, Flo
   __shared__ uint32_t hval[FL_HASH];
   __shared__ unsigned long long ckey[FL_CAP + FL_PREP_T];
   __shared__ uint32_t cslot[FL_CAP + FL_PREP_T];
-  __shared__ uint32_t ndist, nc, bad, adds, dropped;
+  __shared__ uint32_t ndist, nc, bad, adds, dropped, dels;
   __shared__ unsigned long long wg[FL_PREP_T / 64], ws[FL_PREP_T / 64];
   const uint32_t h = F.h0 + blockIdx.x, tid = threadIdx.x;
   if (h >= fl_hend(D, F)) return;
@@ -215,7 +255,7 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep(Dev D, BatchArgs B, Flo
   const Book bk = D.books[sym];
   for (uint32_t i = tid; i < FL_HASH; i += FL_PREP_T) { hkey[i] = 0; hval[i] = NIL; }
   if (tid == 0) {
-    ndist = nc = adds = dropped = 0;
+    ndist = nc = adds = dropped = dels = 0;
     bad = (!F.enabled || (bk.pad & BOOK_QUIRK) || bk.n_lvl > 4 * FL_CAP || (D.st->err & ERR_INPUT) ||
            (end - beg) >= FL_MAX_ORDERS) ? 1u : 0u;
   }
@@ -264,7 +304,7 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep(Dev D, BatchArgs B, Flo
   }
   __syncthreads();
   // the segment's orders
-  uint32_t my_adds = 0, my_drop = 0;
+  uint32_t my_adds = 0, my_drop = 0, my_dels = 0;
   if (!bad) {
     // 4 independent record loads in flight per thread (one block per book is latency-bound)
     for (uint32_t b0 = beg + tid; b0 < end && !bad; b0 += 4 * FL_PREP_T) {
@@ -278,7 +318,7 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep(Dev D, BatchArgs B, Flo
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
       const Prep q = qs[u];
-      if (q.action == GOME_DEL) { bad = 1; break; }
+      if (q.action == GOME_DEL) { my_dels++; continue; }  // the cancel path (match_flow_cancel.h)
       if (q.action != GOME_ADD) continue;
       my_adds++;
       if (!q.adm) { my_drop++; continue; }
@@ -296,6 +336,7 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep(Dev D, BatchArgs B, Flo
   }
   if (my_adds) atomicAdd(&adds, my_adds);
   if (my_drop) atomicAdd(&dropped, my_drop);
+  if (my_dels) atomicAdd(&dels, my_dels);
   for (int off = 32; off > 0; off >>= 1) {
     mg = fl_gcd(mg, __shfl_xor(mg, off));
     msum = min(msum + __shfl_xor(msum, off), FL_SUM_CAP);
@@ -352,6 +393,10 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep(Dev D, BatchArgs B, Flo
   if (g == 0) g = 1;
   const bool w32 = sum < FL_SUM_CAP && sum / g < (1ull << 32);
   if (!w32) g = 1;
+  if (dels && !w32) {  // the cancel plan is 32-bit only
+    if (tid == 0) hd->ok = 0;
+    return;
+  }
   if (tid < ((8u - ((end - beg) & 7u)) & 7u))  // padding to whole half-groups (8 records)
     F.ord8[obase + (end - beg) + tid] = fl_rec(false, 0, 0, false, end - beg + tid, w32);
   for (uint32_t b0 = beg + tid; b0 < end; b0 += 4 * FL_PREP_T) {
@@ -383,7 +428,7 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep(Dev D, BatchArgs B, Flo
   }
   if (tid == 0) {
     FlowHdr x{};
-    x.ok = 1;
+    x.ok = dels ? FL_OK_CANCEL : FL_OK_ADD;
     x.nl = n;
     x.sym = sym;
     x.beg = beg;
@@ -394,6 +439,7 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep(Dev D, BatchArgs B, Flo
     x.obase = obase;
     x.w32 = w32 ? 1u : 0u;
     x.g = g;
+    x.ndel = dels;
     *hd = x;
   }
 }
@@ -411,7 +457,7 @@ struct FlPrepScr {
   unsigned long long key[FL_HASH];  // price set (open addressing, fl_hash, linear probing)
   uint32_t val[FL_HASH];            // after k_flow_prep_b: level index of each key
   unsigned long long pg[FL_PG], ps[FL_PG];  // per-slice gcd and saturated sum of volumes
-  uint32_t adds, dropped, bad, pad;
+  uint32_t adds, dropped, bad, dels;
 };
 
 __device__ __forceinline__ void fl_slice(uint32_t beg, uint32_t end, uint32_t x, uint32_t& b0, uint32_t& b1) {
@@ -459,7 +505,7 @@ __device__ __forceinline__ void fl_block_gcd_sum(unsigned long long& mg, unsigne
 
 __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep_a(Dev D, BatchArgs B, FlowArgs F) {
   __shared__ unsigned long long hkey[FL_HASH];
-  __shared__ uint32_t ndist, bad, adds, dropped;
+  __shared__ uint32_t ndist, bad, adds, dropped, dels;
   __shared__ unsigned long long wg[FL_PREP_T / 64], ws[FL_PREP_T / 64];
   const uint32_t hb = blockIdx.y, h = F.h0 + hb, tid = threadIdx.x;
   if (h >= fl_hend(D, F) || !F.enabled) return;
@@ -468,10 +514,10 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep_a(Dev D, BatchArgs B, F
   uint32_t b0, b1;
   fl_slice(B.seg_start[seg], B.seg_start[seg + 1], blockIdx.x, b0, b1);
   for (uint32_t i = tid; i < FL_HASH; i += FL_PREP_T) hkey[i] = 0;
-  if (tid == 0) ndist = bad = adds = dropped = 0;
+  if (tid == 0) ndist = bad = adds = dropped = dels = 0;
   __syncthreads();
   unsigned long long mg = 0, msum = 0;
-  uint32_t my_adds = 0, my_drop = 0, my_bad = 0;
+  uint32_t my_adds = 0, my_drop = 0, my_bad = 0, my_dels = 0;
   for (uint32_t c0 = b0 + tid; c0 < b1 && !my_bad; c0 += 4 * FL_PREP_T) {
     Prep qs[4];
 #pragma unroll
@@ -483,7 +529,7 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep_a(Dev D, BatchArgs B, F
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const Prep q = qs[u];
-      if (q.action == GOME_DEL) { my_bad = 1; break; }
+      if (q.action == GOME_DEL) { my_dels++; continue; }
       if (q.action != GOME_ADD) continue;
       my_adds++;
       if (!q.adm) { my_drop++; continue; }
@@ -499,6 +545,7 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep_a(Dev D, BatchArgs B, F
   }
   if (my_adds) atomicAdd(&adds, my_adds);
   if (my_drop) atomicAdd(&dropped, my_drop);
+  if (my_dels) atomicAdd(&dels, my_dels);
   if (my_bad) bad = 1;
   fl_block_gcd_sum(mg, msum, wg, ws);  // (synchronises the block)
   if (tid == 0) {
@@ -506,6 +553,7 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep_a(Dev D, BatchArgs B, F
     P->ps[blockIdx.x] = msum;
     if (adds) atomicAdd(&P->adds, adds);
     if (dropped) atomicAdd(&P->dropped, dropped);
+    if (dels) atomicAdd(&P->dels, dels);
     if (bad) atomicOr(&P->bad, 1u);
   }
   if (bad) return;
@@ -623,12 +671,17 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep_b(Dev D, BatchArgs B, F
   unsigned long long g = mg ? mg : 1;
   const bool w32 = msum < FL_SUM_CAP && msum / g < (1ull << 32);
   if (!w32) g = 1;
+  const uint32_t dels = P->dels;
+  if (dels && !w32) {  // the cancel plan is 32-bit only
+    if (tid == 0) hd->ok = 0;
+    return;
+  }
   const uint32_t obase = fl_obase(beg, seg);
   if (tid < ((8u - ((end - beg) & 7u)) & 7u))  // padding to whole half-groups (8 records)
     F.ord8[obase + (end - beg) + tid] = fl_rec(false, 0, 0, false, end - beg + tid, w32);
   if (tid == 0) {
     FlowHdr x{};
-    x.ok = 1;
+    x.ok = dels ? FL_OK_CANCEL : FL_OK_ADD;
     x.nl = n;
     x.sym = sym;
     x.beg = beg;
@@ -639,6 +692,7 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep_b(Dev D, BatchArgs B, F
     x.obase = obase;
     x.w32 = w32 ? 1u : 0u;
     x.g = g;
+    x.ndel = dels;
     *hd = x;
   }
 }
@@ -775,25 +829,46 @@ __device__ unsigned long long g_pstamps[FL_HEAD * 4];
 // EXCL: the block is 4 waves that each hold the whole register file of their SIMD (all 512
 // VGPR+AGPR), so no other wave can share the CU — in particular not its scalar unit, which
 // every instruction of the plan's critical path uses.  Waves 1-3 park at the barrier.
+extern __shared__ uint4 fl_ring[];  // the cancel plan's ring (dynamic LDS)
+
+// Books with DELs: the ring image -> LDS, by every thread of the block.
+__device__ __forceinline__ void fl_ring_load(const FlowArgs& F, uint32_t h) {
+  const uint32_t ns = F.hdr[h].nslot;
+  const uint4* img = F.fc_img + fc_img_off(h);
+  for (uint32_t i = threadIdx.x; i < ns; i += blockDim.x) fl_ring[i] = img[i];
+}
+
 template <bool EXCL>
-__device__ __forceinline__ void fl_plan_kernel(const Dev& D, const FlowArgs& F) {
+__device__ __forceinline__ void fl_plan_kernel(const Dev& D, const FlowArgs& F, uint32_t kind) {
+  const uint32_t h = F.h0 + blockIdx.x;
+  const bool mine = h < fl_hend(D, F) && uni(F.hdr[h].ok) == kind;
+  if (mine && kind == FL_OK_CANCEL) fl_ring_load(F, h);
   if (EXCL) {
     asm volatile("" ::: "v255", "a255");
+    __syncthreads();
     if (threadIdx.x >= 64) {
       __syncthreads();
       return;
     }
+  } else if (kind == FL_OK_CANCEL) {
+    __syncthreads();
   }
-  const uint32_t h = F.h0 + blockIdx.x;
-  if (h < fl_hend(D, F) && uni(F.hdr[h].ok)) fl_plan_book(D, F, h);
+  if (mine) fl_plan_book(D, F, h);
   if (EXCL) __syncthreads();
 }
 
 // The head's plan (the batch's critical path) and the tail's: distinct names for the profiles.
-__global__ __launch_bounds__(256) void k_flow_plan_head(Dev D, FlowArgs F) { fl_plan_kernel<true>(D, F); }
+// (The head kernels plan either kind of book: their block owns the CU and its LDS anyway.)
+__global__ __launch_bounds__(256) void k_flow_plan_head(Dev D, FlowArgs F) {
+  fl_plan_kernel<true>(D, F, uni(F.hdr[F.h0 + blockIdx.x < fl_hend(D, F) ? F.h0 + blockIdx.x : 0].ok));
+}
 // the other head books (planned on the tail's stream, beside the hottest)
-__global__ __launch_bounds__(256) void k_flow_plan_near(Dev D, FlowArgs F) { fl_plan_kernel<true>(D, F); }
-__global__ __launch_bounds__(64) void k_flow_plan_tail(Dev D, FlowArgs F) { fl_plan_kernel<false>(D, F); }
+__global__ __launch_bounds__(256) void k_flow_plan_near(Dev D, FlowArgs F) {
+  fl_plan_kernel<true>(D, F, uni(F.hdr[F.h0 + blockIdx.x < fl_hend(D, F) ? F.h0 + blockIdx.x : 0].ok));
+}
+__global__ __launch_bounds__(64) void k_flow_plan_tail(Dev D, FlowArgs F) { fl_plan_kernel<false>(D, F, FL_OK_ADD); }
+// tail books with DELs (a launch of its own: 16 KiB of LDS per block)
+__global__ __launch_bounds__(64) void k_flow_plan_tail_c(Dev D, FlowArgs F) { fl_plan_kernel<false>(D, F, FL_OK_CANCEL); }
 
 __device__ __forceinline__ void fl_plan_book(const Dev& D, const FlowArgs& F, uint32_t h) {
   const FlowHdr* hd = &F.hdr[h];
@@ -816,6 +891,9 @@ __device__ __forceinline__ void fl_plan_book(const Dev& D, const FlowArgs& F, ui
   const int64_t a0 = (m0 & M_SALE) ? d0 : 0, a1 = (m1 & M_SALE) ? d1 : (lane == 63 ? 1 : 0);
   const int64_t b0 = (m0 & M_BUY) ? d0 : (lane == 0 ? 1 : 0), b1 = (m1 & M_BUY) ? d1 : 0;
   FlDepth Da{lo32(a0), hi32(a0), lo32(a1), hi32(a1)}, Db{lo32(b0), hi32(b0), lo32(b1), hi32(b1)};
+  // books with DELs: R_k (volume that ever arrived, arrival coordinates from the old FIFO head)
+  // starts at the level's live volume
+  FlDepth Rv{lo32(d0), 0u, lo32(d1), 0u};
   if (w32) {  // the 32-bit plan's layout: lane j holds levels 2j (l0) and 2j + 1 (l1)
     const uint32_t se = (2u * lane) & 63u, so = (2u * lane + 1u) & 63u;
     const bool hiset = lane >= 32;
@@ -825,6 +903,7 @@ __device__ __forceinline__ void fl_plan_book(const Dev& D, const FlowArgs& F, ui
     };
     Da = FlDepth{pick(Da.l0, Da.l1, se), 0u, pick(Da.l0, Da.l1, so), 0u};
     Db = FlDepth{pick(Db.l0, Db.l1, se), 0u, pick(Db.l0, Db.l1, so), 0u};
+    Rv = FlDepth{pick(Rv.l0, Rv.l1, se), 0u, pick(Rv.l0, Rv.l1, so), 0u};
   }
 
   FlLog lg{vreg(0u), vreg(0u), vreg(0u), 0u, 0u, 0u, FL_TOUCH_MUL * n, (GOME_GLB v4u*)(F.log + FL_TOUCH_MUL * beg)};
@@ -846,8 +925,20 @@ __device__ __forceinline__ void fl_plan_book(const Dev& D, const FlowArgs& F, ui
 #ifdef GOME_STAMPS
   const unsigned long long sc0 = __builtin_amdgcn_s_memtime(), sr0 = __builtin_amdgcn_s_memrealtime();
 #endif
-  if (w32) asm volatile(FL_PLAN_ASM32 FL_PLAN_OPERANDS);
-  else asm volatile(FL_PLAN_ASM64 FL_PLAN_OPERANDS);
+  if (uni(hd->ok) == FL_OK_CANCEL) {
+    asm volatile(FL_PLAN_ASM32C
+      : [al0] "+v"(Da.l0), [ah0] "+v"(Da.h0), [al1] "+v"(Da.l1), [ah1] "+v"(Da.h1), [bl0] "+v"(Db.l0),
+        [bh0] "+v"(Db.h0), [bl1] "+v"(Db.l1), [bh1] "+v"(Db.h1), [lk] "+v"(lg.lk), [la] "+v"(lg.la),
+        [lb] "+v"(lg.lb), [nacc] "+s"(lg.nacc), [lpos] "+s"(lg.lpos), [voff] "=&v"(voff), [vt] "=&v"(vt),
+        [vpf] "=&v"(vpf)
+      : [ob] "s"(ob), [nh] "s"(nh), [logp] "s"(logp), [lcap] "s"(lg.lcap), [vl16] "v"(vl16),
+        [vzero] "v"(vzero), [rl0] "v"(Rv.l0), [rl1] "v"(Rv.l1)
+      : FL_PLAN_CLOBBERS, FL_PLAN_CLOBBERS_C, "scc", "vcc", "memory");
+  } else if (w32) {
+    asm volatile(FL_PLAN_ASM32 FL_PLAN_OPERANDS);
+  } else {
+    asm volatile(FL_PLAN_ASM64 FL_PLAN_OPERANDS);
+  }
 #undef FL_PLAN_OPERANDS
 #ifdef GOME_STAMPS
   const unsigned long long sc1 = __builtin_amdgcn_s_memtime(), sr1 = __builtin_amdgcn_s_memrealtime();
@@ -913,6 +1004,7 @@ __global__ __launch_bounds__(FL_SORT_T) void k_flow_sort(Dev D, FlowArgs F) {
   if (h >= fl_hend(D, F) || !F.hdr[h].ok) return;
   const uint32_t nt = F.hdr[h].ntouch, L = FL_TOUCH_MUL * F.hdr[h].beg, nl = F.hdr[h].nl;
   const unsigned long long g = F.hdr[h].g;
+  const bool cb = F.hdr[h].ok == FL_OK_CANCEL;
   FlowLvl* LV = F.lvl + h * FL_CAP;
   if (tid < FL_CAP) hist[tid] = 0;
   if (tid == 0) nrest = 0;
@@ -922,7 +1014,7 @@ __global__ __launch_bounds__(FL_SORT_T) void k_flow_sort(Dev D, FlowArgs F) {
   for (uint32_t t = tid; t < nt; t += FL_SORT_T) {
     const uint32_t kr = F.log[L + t].kr;
     atomicAdd(&hist[kr & 127u], 1u);
-    myr += ((kr >> 7) & 1u) && (kr & 127u) ? 1u : 0u;  // level-0 touches are no-op records
+    myr += tk_kind(kr, cb) == TK_REST && (kr & 127u) ? 1u : 0u;  // level-0 touches are no-op records
   }
   if (myr) atomicAdd(&nrest, myr);
   __syncthreads();
@@ -968,7 +1060,7 @@ __global__ __launch_bounds__(FL_SORT_T) void k_flow_sort(Dev D, FlowArgs F) {
     if (valid) {
       SEnt e;
       e.j = tk_j(x);
-      e.kind = (x.kr >> 7) & 1u;
+      e.kind = tk_kind(x.kr, cb);
       e.amt = x.amt;
       e.coord = 0;
       e.t = t;
@@ -1113,7 +1205,7 @@ __device__ __forceinline__ void fl_level_one(const Dev& D, const FlowArgs& F, ui
 constexpr uint32_t FL_LEVEL_T = 1024;
 __global__ __launch_bounds__(FL_LEVEL_T) void k_flow_level(Dev D, FlowArgs F) {
   const uint32_t h = F.h0 + blockIdx.x;
-  if (h >= fl_hend(D, F) || !F.hdr[h].ok) return;
+  if (h >= fl_hend(D, F) || F.hdr[h].ok != FL_OK_ADD) return;
   const uint32_t nl = F.hdr[h].nl;
   for (uint32_t q = 1 + (threadIdx.x >> 6); q <= nl; q += FL_LEVEL_T / 64) fl_level_one(D, F, h, uni(q));
 }
@@ -1174,7 +1266,9 @@ __device__ __forceinline__ uint32_t fl_book_of(const FlowArgs& F, uint32_t nb, u
   return lo;
 }
 
-// Exclusive scan of the flow books' touch counts (declined candidates count 0).
+// Exclusive scan of the flow books' touch counts (declined candidates count 0).  KIND: the books
+// the range's count / event kernels cover (FL_OK_ADD: k_flow_*, FL_OK_CANCEL: k_fc_*).
+template <uint32_t KIND>
 __global__ __launch_bounds__(1024) void k_flow_toff(Dev D, FlowArgs F) {
   __shared__ uint32_t part[1024];
   const uint32_t hend = fl_hend(D, F), nb = hend > F.h0 ? hend - F.h0 : 0u, tid = threadIdx.x;
@@ -1182,7 +1276,7 @@ __global__ __launch_bounds__(1024) void k_flow_toff(Dev D, FlowArgs F) {
   uint32_t* toff = F.toff + F.tb;
   const uint32_t per = (nb + 1023) / 1024, b0 = tid * per;
   uint32_t s = 0;
-  for (uint32_t i = b0; i < b0 + per && i < nb; ++i) s += hdr[i].ok ? hdr[i].ntouch : 0u;
+  for (uint32_t i = b0; i < b0 + per && i < nb; ++i) s += hdr[i].ok == KIND ? hdr[i].ntouch : 0u;
   part[tid] = s;
   __syncthreads();
   if (tid == 0) {
@@ -1194,7 +1288,7 @@ __global__ __launch_bounds__(1024) void k_flow_toff(Dev D, FlowArgs F) {
   uint32_t acc = part[tid];
   for (uint32_t i = b0; i < b0 + per && i < nb; ++i) {
     toff[i] = acc;
-    acc += hdr[i].ok ? hdr[i].ntouch : 0u;
+    acc += hdr[i].ok == KIND ? hdr[i].ntouch : 0u;
   }
 }
 
@@ -1530,7 +1624,7 @@ __global__ __launch_bounds__(FL_WRITE_T) void k_flow_write(Dev D, BatchArgs B, F
   __shared__ uint32_t keep[FL_CAP];
   __shared__ uint32_t nout_s, base_s, cap_s;
   const uint32_t h = F.h0 + blockIdx.x;
-  if (h >= fl_hend(D, F) || !F.hdr[h].ok) return;
+  if (h >= fl_hend(D, F) || F.hdr[h].ok != FL_OK_ADD) return;
   const FlowHdr hd = F.hdr[h];
   const uint32_t w = threadIdx.x >> 6, nw = FL_WRITE_T / 64;
   for (uint32_t q = 1 + w; q <= hd.nl; q += nw) {
@@ -1544,7 +1638,7 @@ __global__ __launch_bounds__(FL_WRITE_T) void k_flow_write(Dev D, BatchArgs B, F
 // Head books: one wave per (book, level) writes its FIFO and stores its final record ...
 __global__ __launch_bounds__(64) void k_flow_write_lv(Dev D, BatchArgs B, FlowArgs F) {
   const uint32_t h = F.h0 + blockIdx.y, q = blockIdx.x;
-  if (h >= fl_hend(D, F) || !F.hdr[h].ok) return;
+  if (h >= fl_hend(D, F) || F.hdr[h].ok != FL_OK_ADD) return;
   const FlowHdr hd = F.hdr[h];
   if (q == 0 || q > hd.nl) return;
   const Level x = fl_write_level(D, B, F, hd, h, q);
@@ -1557,7 +1651,7 @@ __global__ __launch_bounds__(128) void k_flow_write_fin(Dev D, FlowArgs F) {
   __shared__ uint32_t keep[FL_CAP];
   __shared__ uint32_t nout_s, base_s, cap_s;
   const uint32_t h = F.h0 + blockIdx.x;
-  if (h >= fl_hend(D, F) || !F.hdr[h].ok) return;
+  if (h >= fl_hend(D, F) || F.hdr[h].ok != FL_OK_ADD) return;
   const FlowHdr hd = F.hdr[h];
   for (uint32_t q = 1 + threadIdx.x; q <= hd.nl; q += blockDim.x) lv[q] = F.lvout[h * FL_CAP + q];
   __syncthreads();
@@ -1593,6 +1687,7 @@ __global__ __launch_bounds__(FL_TILE) void k_flow_sort_cnt(Dev D, FlowArgs F) {
   if (h >= fl_hend(D, F) || !F.hdr[h].ok) return;
   const uint32_t nt = F.hdr[h].ntouch, L = FL_TOUCH_MUL * F.hdr[h].beg;
   const uint32_t ntile = (nt + FL_TILE - 1) / FL_TILE;
+  const bool cb = F.hdr[h].ok == FL_OK_CANCEL;
   for (uint32_t tl = blockIdx.x; tl < ntile; tl += gridDim.x) {
     for (uint32_t i = tid; i < FL_TILE_W * FL_CAP; i += FL_TILE) wc[i / FL_CAP][i % FL_CAP] = 0;
     if (tid == 0) nrest = 0;
@@ -1603,7 +1698,7 @@ __global__ __launch_bounds__(FL_TILE) void k_flow_sort_cnt(Dev D, FlowArgs F) {
     uint32_t cnt;
     const uint32_t rank = fl_tile_rank(k, valid, cnt);
     if (valid && rank == 0) wc[w][k] = cnt;
-    const unsigned long long rm = __ballot(valid && ((kr >> 7) & 1u) && k);
+    const unsigned long long rm = __ballot(valid && tk_kind(kr, cb) == TK_REST && k);
     if (lane_id() == 0 && rm) atomicAdd(&nrest, static_cast<uint32_t>(__popcll(rm)));
     __syncthreads();
     if (tid < FL_CAP) {
@@ -1668,6 +1763,7 @@ __global__ __launch_bounds__(FL_TILE) void k_flow_sort_scatter(Dev D, FlowArgs F
   if (h >= fl_hend(D, F) || !F.hdr[h].ok) return;
   const uint32_t nt = F.hdr[h].ntouch, L = FL_TOUCH_MUL * F.hdr[h].beg;
   const unsigned long long g = F.hdr[h].g;
+  const bool cb = F.hdr[h].ok == FL_OK_CANCEL;
   const uint32_t ntile = (nt + FL_TILE - 1) / FL_TILE;
   const uint32_t* tc = F.tcnt + static_cast<size_t>(h) * F.maxt * FL_CAP;
   for (uint32_t i = tid; i < FL_TILE_W * FL_CAP; i += FL_TILE) wc[i / FL_CAP][i % FL_CAP] = 0;
@@ -1694,7 +1790,7 @@ __global__ __launch_bounds__(FL_TILE) void k_flow_sort_scatter(Dev D, FlowArgs F
     if (valid) {
       SEnt e;
       e.j = tk_j(x);
-      e.kind = (x.kr >> 7) & 1u;
+      e.kind = tk_kind(x.kr, cb);
       e.amt = static_cast<int64_t>(static_cast<unsigned long long>(x.amt) * g);
       e.coord = 0;
       e.t = t;
@@ -1714,7 +1810,7 @@ __global__ __launch_bounds__(FL_TILE) void k_flow_sort_scatter(Dev D, FlowArgs F
 
 __global__ __launch_bounds__(64) void k_flow_level_wide(Dev D, FlowArgs F) {
   const uint32_t h = F.h0 + blockIdx.y, q = blockIdx.x;
-  if (h >= fl_hend(D, F) || !F.hdr[h].ok) return;
+  if (h >= fl_hend(D, F) || F.hdr[h].ok != FL_OK_ADD) return;
   if (q == 0 || q > F.hdr[h].nl) return;
   fl_level_one(D, F, h, q);
 }

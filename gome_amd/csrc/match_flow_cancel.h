@@ -1,0 +1,1070 @@
+// match_flow_cancel.h — cancels on the flow path: hot books whose segment holds DELs.
+//
+// DeleteOrder (engine.go:87-116) removes a maker's *remaining* volume from its level (depth -=
+// stored remaining, ZREM when the level empties) and unlinks it (nodelink.go:124-166).  What a
+// cancel removes depends on how much of the maker was consumed before it, i.e. on FIFO order,
+// which the aggregate plan (match_flow.h) does not track.  It does not have to: in arrival
+// coordinates of a level (maker m occupies [E_m, E_m + v_m), E = volume that arrived before it)
+//
+//     r_m = clamp(E_m + v_m - G_k + Xb_m, 0, v_m),   G_k = R_k - depth_k (volume removed so far)
+//
+// where R_k is the volume that ever arrived at the level and Xb_m the volume of the makers
+// *behind* m that were cancelled before: while m is live they were untouched, so each removed
+// exactly its v_j; when m is gone the clamp gives 0 (tools/flow_cancel_model.py checks this
+// against the oracle).  So the plan (gen_plan_asm.py, W32C) keeps R_k beside the depths, and
+// every DEL's target ("targeted maker") owns an entry {end = E + v, v, xv} of an LDS ring per
+// level; a DEL reads its target's entry, sums xv over the window of targets that arrived behind
+// it (ranks rank_m + 1 .. rank_m + n_b) and sets its own xv = v_m.  Ring capacity C_k (a power
+// of two) exceeds every window, so an entry is reused only after every DEL that reads it.
+//
+// Prep (after the book's ordinary prep, which builds the level set and the 32-bit records):
+//   k_fc_hash_claim / k_fc_hash_count   (symbol, oid) table of the books' ADD / DEL records
+//   k_fc_resolve    each DEL's target: an earlier admitted ADD of the segment (new maker) or a
+//                   resting node (old maker, the cancel index); Q3 (wrong price) and DELs whose
+//                   oid is not resting are no-ops; Q2 (wrong side) and duplicate oids decline
+//   k_fc_oldwalk    old targets' FIFO ranks and arrival coordinates (a walk of their level)
+//   k_fc_pass       in segment order: new targets' ranks, each DEL's window, C_k; the ring
+//                   layout, its LDS image and the W32C records
+// Reconstruction (after the plan and the level sort of its touches):
+//   k_fc_level      per level: cancels -> their DEL's record; the consumption-space layout of
+//                   the makers (a cancelled maker only spans what was consumed before its
+//                   cancel), the gathered old makers, the new makers
+//   k_fc_count / k_fc_events   fills as interval intersections (zero-length makers skipped,
+//                   MatchNode.NextNode skips makers cancelled before the fill), cancel events,
+//                   tombstones of cancelled old makers
+//   k_fc_write      surviving new makers appended, the level records; k_fc_fin the book.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "../../include/gome/gome_abi.h"
+#include "device.h"
+#include "match_cold.h"
+#include "match_flow.h"
+#include "pipeline.h"
+#include "wave.h"
+
+namespace gome {
+
+struct FcHash {
+  unsigned long long key;  // gen << 53 | (symbol + 1) << 32 | oid; another generation = empty
+  uint32_t add_pos;        // first admitted ADD of the key (segment position), NIL none
+  uint32_t cnt;            // admitted ADDs (low 16 bits), DELs (high 16 bits)
+};
+static_assert(sizeof(FcHash) == 16, "FcHash layout");
+
+struct FcDel {
+  uint32_t kind;     // FC_NONE (no-op), FC_NEW, FC_OLD
+  uint32_t li;       // the target's level
+  uint32_t tgt;      // FC_NEW: the ADD's segment position; FC_OLD: the node (chunk * CH + slot)
+  uint32_t rank;     // the target's rank among the level's targets (arrival order)
+  uint32_t nb;       // window: targets that arrived behind the target before this DEL
+  uint32_t ixs;      // FC_OLD: the node's cancel-index slot
+  uint32_t oend, ov; // FC_OLD: arrival end / volume (plan units)
+  int64_t r;         // recon: volume cancelled (fixed point), 0 if the DEL found nothing
+  uint32_t ct;       // recon: touch index of the cancel, NIL if none
+  uint32_t pad;
+};
+static_assert(sizeof(FcDel) == 48, "FcDel layout");
+enum : uint32_t { FC_NONE = 0, FC_NEW = 1, FC_OLD = 2 };
+
+constexpr uint32_t FC_MAXKEY_SYM = (1u << 21) - 1;  // symbol + 1 fits 21 bits of the key
+
+__device__ __forceinline__ bool fc_book(const FlowArgs& F, uint32_t h) {
+  return F.hdr[h].ok == FL_OK_CANCEL && !F.hdr[h].fc_bad;
+}
+__device__ __forceinline__ void fc_decline(const FlowArgs& F, uint32_t h) {
+  atomicOr(&F.hdr[h].fc_bad, 1u);
+}
+__device__ __forceinline__ unsigned long long fc_key(const FlowArgs& F, uint32_t sym, uint32_t oid) {
+  return (static_cast<unsigned long long>(F.fc_gen & FC_GEN_MASK) << 53) |
+         (static_cast<unsigned long long>(sym + 1) << 32) | oid;
+}
+
+// Slice [b0, b1) of book h's segment for block x of `nx`.
+__device__ __forceinline__ void fc_slice(const FlowHdr& hd, uint32_t x, uint32_t nx, uint32_t& b0, uint32_t& b1) {
+  const uint64_t len = hd.end - hd.beg;
+  b0 = hd.beg + static_cast<uint32_t>(len * x / nx);
+  b1 = hd.beg + static_cast<uint32_t>(len * (x + 1) / nx);
+}
+
+__device__ __forceinline__ uint32_t fc_hash_find(const FlowArgs& F, unsigned long long key, bool claim) {
+  const unsigned long long gen_mask = static_cast<unsigned long long>(FC_GEN_MASK) << 53;
+  unsigned long long s = mix64(key) & F.fc_hmask;
+  for (unsigned long long probe = 0; probe <= F.fc_hmask; ++probe, s = (s + 1) & F.fc_hmask) {
+    unsigned long long cur = __hip_atomic_load(&F.fc_hash[s].key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (cur == key) return static_cast<uint32_t>(s);
+    const bool stale = cur == 0ull || (cur & gen_mask) != (key & gen_mask);
+    if (!stale) continue;
+    if (!claim) return NIL;
+    const unsigned long long prev = atomicCAS(&F.fc_hash[s].key, cur, key);
+    if (prev == cur) {
+      F.fc_hash[s].add_pos = NIL;
+      F.fc_hash[s].cnt = 0;
+      return static_cast<uint32_t>(s);
+    }
+    if (prev == key) return static_cast<uint32_t>(s);
+  }
+  return NIL;
+}
+
+// ---- prep 1: claim a table entry per key, reset the books' per-position scratch ----------
+// (The scratch of every book with DELs is reset, declined or not: k_fc_unmark reads it.)
+__global__ __launch_bounds__(256) void k_fc_hash_claim(Dev D, BatchArgs B, FlowArgs F) {
+  const uint32_t h = F.h0 + blockIdx.y;
+  if (h >= fl_hend(D, F) || F.hdr[h].ok != FL_OK_CANCEL) return;
+  const FlowHdr hd = F.hdr[h];
+  uint32_t b0, b1;
+  fc_slice(hd, blockIdx.x, gridDim.x, b0, b1);
+  const bool claim = hd.sym < FC_MAXKEY_SYM;
+  if (!claim && threadIdx.x == 0) fc_decline(F, h);
+  for (uint32_t b = b0 + threadIdx.x; b < b1; b += blockDim.x) {
+    F.fc_tg[b] = 0;
+    F.fc_rank[b] = NIL;
+    const Prep q = prep_at(B, b);
+    if (q.action == GOME_DEL) {
+      FcDel z{};
+      z.ct = NIL;
+      F.fc_del[b] = z;
+    }
+    if (claim && (q.action == GOME_DEL || (q.action == GOME_ADD && q.adm)))
+      if (fc_hash_find(F, fc_key(F, hd.sym, q.oid), true) == NIL) fc_decline(F, h);
+  }
+}
+
+// ---- prep 2: first admitted ADD and the counts of each key -------------------------------
+__global__ __launch_bounds__(256) void k_fc_hash_count(Dev D, BatchArgs B, FlowArgs F) {
+  const uint32_t h = F.h0 + blockIdx.y;
+  if (h >= fl_hend(D, F) || !fc_book(F, h)) return;
+  const FlowHdr hd = F.hdr[h];
+  uint32_t b0, b1;
+  fc_slice(hd, blockIdx.x, gridDim.x, b0, b1);
+  for (uint32_t b = b0 + threadIdx.x; b < b1; b += blockDim.x) {
+    const Prep q = prep_at(B, b);
+    const bool add = q.action == GOME_ADD && q.adm;
+    if (!add && q.action != GOME_DEL) continue;
+    const uint32_t s = fc_hash_find(F, fc_key(F, hd.sym, q.oid), false);
+    if (s == NIL) continue;  // (declined in prep 1)
+    if (add) {
+      atomicMin(&F.fc_hash[s].add_pos, b);
+      atomicAdd(&F.fc_hash[s].cnt, 1u);
+    } else {
+      atomicAdd(&F.fc_hash[s].cnt, 1u << 16);
+    }
+  }
+}
+
+// Level of price p in book h's level table (1..nl, ascending), 0 if absent.
+__device__ __forceinline__ uint32_t fc_level_of(const FlowLvl* LV, uint32_t nl, int64_t p) {
+  uint32_t lo = 1, hi = nl + 1;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (LV[mid].price < p) lo = mid + 1; else hi = mid;
+  }
+  return (lo <= nl && LV[lo].price == p) ? lo : 0u;
+}
+
+// Resting node of (sym, oid) through the cancel index (HGET S:link:<p> S:node:<oid>,
+// engine.go:92-93); NIL if none.
+__device__ __forceinline__ uint32_t fc_old_lookup(const Dev& D, uint32_t sym, uint32_t oid, uint32_t& ixs) {
+  const unsigned long long key = (static_cast<unsigned long long>(sym + 1) << 32) | oid;
+  unsigned long long s = mix64(key) & D.idx_mask;
+  for (unsigned long long probe = 0; probe <= D.idx_mask; ++probe, s = (s + 1) & D.idx_mask) {
+    const unsigned long long kv = __hip_atomic_load(&D.idx[s].key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (kv == key) {
+      ixs = static_cast<uint32_t>(s);
+      return D.idx[s].loc;
+    }
+    if (kv == KEY_EMPTY) return NIL;
+  }
+  return NIL;
+}
+
+// ---- prep 3: each DEL's target -------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_fc_resolve(Dev D, BatchArgs B, FlowArgs F) {
+  const uint32_t h = F.h0 + blockIdx.y;
+  if (h >= fl_hend(D, F) || !fc_book(F, h)) return;
+  const FlowHdr hd = F.hdr[h];
+  FlowLvl* LV = F.lvl + h * FL_CAP;
+  uint32_t b0, b1;
+  fc_slice(hd, blockIdx.x, gridDim.x, b0, b1);
+  for (uint32_t b = b0 + threadIdx.x; b < b1; b += blockDim.x) {
+    const Prep q = prep_at(B, b);
+    if (q.action != GOME_DEL) continue;
+    const uint32_t s = fc_hash_find(F, fc_key(F, hd.sym, q.oid), false);
+    if (s == NIL) continue;
+    const FcHash e = F.fc_hash[s];
+    const uint32_t nadd = e.cnt & 0xFFFFu, ndel = e.cnt >> 16;
+    if (nadd > 1 || ndel > 1) { fc_decline(F, h); continue; }  // reused oid (Q7) / repeated cancel
+    const bool sale = q.side == GOME_SALE;
+    FcDel d{};
+    d.ct = NIL;
+    uint32_t ixs = 0;
+    const uint32_t loc = fc_old_lookup(D, hd.sym, q.oid, ixs);
+    if (nadd == 1 && e.add_pos < b) {
+      if (loc != NIL) { fc_decline(F, h); continue; }  // the oid rests already: duplicate (Q7)
+      const Prep a = prep_at(B, e.add_pos);
+      if (a.price != q.price) continue;                 // S:link:<request price> misses (Q3)
+      if ((a.side == GOME_SALE) != sale) { fc_decline(F, h); continue; }  // wrong side (Q2)
+      d.kind = FC_NEW;
+      d.tgt = e.add_pos;
+      d.li = static_cast<uint32_t>(F.ord8[hd.obase + (e.add_pos - hd.beg)] >> 32) & 127u;
+      F.fc_del[b] = d;
+      F.fc_tg[e.add_pos] = b + 1;
+      continue;
+    }
+    if (nadd == 1) {  // the ADD comes after the DEL: the DEL finds nothing (or a duplicate)
+      if (loc != NIL) fc_decline(F, h);
+      continue;
+    }
+    if (loc == NIL) continue;                                             // not resting
+    if (D.chdr[loc / CH].price != q.price) continue;                     // Q3
+    const Node nd = D.nodes[loc];
+    if (nd.rem < 0) continue;
+    if ((nd.tx == GOME_SALE) != sale) { fc_decline(F, h); continue; }   // Q2
+    const uint32_t li = fc_level_of(LV, hd.nl, q.price);
+    if (li == 0) { fc_decline(F, h); continue; }
+    d.kind = FC_OLD;
+    d.tgt = loc;
+    d.ixs = ixs;
+    d.li = li;
+    F.fc_del[b] = d;
+    D.nodes[loc].pad = b + 1;  // marks the target for the walks (cleared when it is cancelled)
+    atomicAdd(&LV[li].c_old, 1u);
+  }
+}
+
+// ---- prep 4: old targets' FIFO ranks and arrival coordinates (one wave per level) -----------
+__device__ __forceinline__ void fc_oldwalk_level(const Dev& D, const FlowArgs& F, uint32_t h, uint32_t q) {
+  const FlowHdr& hd = F.hdr[h];
+  FlowLvl* Lq = F.lvl + h * FL_CAP + q;
+  const uint32_t cold = uni(Lq->c_old);
+  if (!cold) return;
+  const uint32_t lane = lane_id();
+  const unsigned long long g = hd.g;
+  const uint32_t tail = uni(Lq->tail), tslot = uni(Lq->tslot);
+  uint32_t c = uni(Lq->head), s0 = uni(Lq->hslot), seen = 0;
+  int64_t E = 0;
+  for (uint32_t guard = 0; c != NIL && seen < cold; ++guard) {
+    if (guard > D.ch_cap) { if (lane == 0) atomicOr(&D.st->err, ERR_CORRUPT); return; }
+    const uint32_t lim = (c == tail) ? tslot : CH;
+    const bool inr = lane < CH && lane >= s0 && lane < lim;
+    Node nd{};
+    if (inr) nd = D.nodes[c * CH + lane];
+    const bool live = inr && nd.rem >= 0;
+    const int64_t x = live ? nd.rem : 0;
+    const int64_t em = E + wave_incl_scan(x) - x;
+    const bool mk = live && nd.pad != 0;
+    const unsigned long long mm = __ballot(mk);
+    if (mk) {
+      FcDel* d = &F.fc_del[static_cast<uint32_t>(nd.pad) - 1u];
+      const uint64_t end = static_cast<uint64_t>(em + nd.rem);
+      if (end % g || static_cast<uint64_t>(nd.rem) % g) fc_decline(F, h);  // not in plan units
+      d->rank = seen + __popcll(mm & lt_mask());
+      d->oend = static_cast<uint32_t>(end / g);
+      d->ov = static_cast<uint32_t>(static_cast<uint64_t>(nd.rem) / g);
+    }
+    seen += __popcll(mm);
+    E += rl64(wave_incl_scan(x), 63);
+    c = (c == tail) ? NIL : uni(D.chdr[c].next);
+    s0 = 0;
+  }
+  if (seen != cold && lane == 0) fc_decline(F, h);
+}
+
+__global__ __launch_bounds__(64) void k_fc_oldwalk_wide(Dev D, FlowArgs F) {
+  const uint32_t h = F.h0 + blockIdx.y, q = blockIdx.x;
+  if (h >= fl_hend(D, F) || !fc_book(F, h) || q == 0 || q > F.hdr[h].nl) return;
+  fc_oldwalk_level(D, F, h, q);
+}
+
+__global__ __launch_bounds__(1024) void k_fc_oldwalk_book(Dev D, FlowArgs F) {
+  const uint32_t h = F.h0 + blockIdx.x;
+  if (h >= fl_hend(D, F) || !fc_book(F, h)) return;
+  for (uint32_t q = 1 + (threadIdx.x >> 6); q <= F.hdr[h].nl; q += blockDim.x / 64) fc_oldwalk_level(D, F, h, uni(q));
+}
+
+// ---- prep 5: ranks, windows, ring layout, image and W32C records (one block per book) -------
+constexpr uint32_t FC_PASS_T = 1024, FC_PASS_W = FC_PASS_T / 64;
+
+__global__ __launch_bounds__(FC_PASS_T) void k_fc_pass(Dev D, BatchArgs B, FlowArgs F) {
+  __shared__ uint32_t cnt[FL_CAP], cmax[FL_CAP], wc[FC_PASS_W][FL_CAP], cring[FL_CAP], rbase[FL_CAP];
+  __shared__ uint32_t nslot_s, bad_s;
+  const uint32_t h = F.h0 + blockIdx.x, tid = threadIdx.x, w = tid >> 6;
+  if (h >= fl_hend(D, F) || !fc_book(F, h)) return;
+  const FlowHdr hd = F.hdr[h];
+  FlowLvl* LV = F.lvl + h * FL_CAP;
+  const uint32_t n = hd.end - hd.beg, nl = hd.nl;
+  if (tid < FL_CAP) {
+    cnt[tid] = 0;
+    cmax[tid] = (tid >= 1 && tid <= nl) ? max(LV[tid].c_old, 1u) : 1u;
+  }
+  if (tid == 0) bad_s = 0;
+  __syncthreads();
+  const unsigned long long ltm = lt_mask();
+  // in segment order, tile by tile: a targeted ADD's rank = old targets of its level + targeted
+  // ADDs before it; a DEL's window = targets of the level that arrived before it - its target's
+  // rank - 1 (stable per-level counting across the waves of a tile)
+  for (uint32_t t0 = 0; t0 < n; t0 += FC_PASS_T) {
+    const uint32_t i = t0 + tid;
+    const uint32_t b = hd.beg + i;
+    bool isa = false, isd = false;
+    uint32_t k = 0;
+    FcDel d{};
+    if (i < n) {
+      const uint32_t tg = F.fc_tg[b];
+      if (tg) {
+        isa = true;
+        k = static_cast<uint32_t>(F.ord8[hd.obase + i] >> 32) & 127u;
+      } else if (prep_at(B, b).action == GOME_DEL) {
+        d = F.fc_del[b];
+        if (d.kind != FC_NONE) { isd = true; k = d.li; }
+      }
+    }
+    unsigned long long same = __ballot(isa);
+#pragma unroll
+    for (uint32_t bit = 0; bit < 7; ++bit) {
+      const unsigned long long bb = __ballot((k >> bit) & 1u);
+      same &= ((k >> bit) & 1u) ? bb : ~bb;
+    }
+    // same: the wave's targeted ADDs at level k (valid for every lane with that k)
+    const uint32_t before_w = __popcll(same & ltm);
+    if (isa && before_w == 0) wc[w][k] = __popcll(same);
+    __syncthreads();
+    if (tid < FL_CAP) {  // waves' counts -> exclusive offsets (from the tile's running count)
+      uint32_t r = cnt[tid];
+      for (uint32_t ww = 0; ww < FC_PASS_W; ++ww) {
+        const uint32_t c = wc[ww][tid];
+        wc[ww][tid] = r;
+        r += c;
+      }
+      cnt[tid] = r;
+    }
+    __syncthreads();
+    // wc[w][k] now = targeted ADDs at level k before wave w's first lane (all earlier tiles too)
+    const uint32_t before = (isa || isd) ? wc[w][k] + before_w : 0u;
+    if (isa) F.fc_rank[b] = LV[k].c_old + before;
+    __syncthreads();  // (a DEL may target an ADD of the same tile)
+    if (isd) {
+      const uint32_t rk = d.kind == FC_NEW ? F.fc_rank[d.tgt] : d.rank;
+      const uint32_t arrived = LV[k].c_old + before;
+      const uint32_t nb = arrived - rk - 1u;
+      F.fc_del[b].rank = rk;
+      F.fc_del[b].nb = nb;
+      atomicMax(&cmax[k], nb + 1u);
+      if (nb >= 0xFFFFu) bad_s = 1;
+    }
+    for (uint32_t x = tid; x < FC_PASS_W * FL_CAP; x += FC_PASS_T) wc[x / FL_CAP][x % FL_CAP] = 0;
+    __syncthreads();
+  }
+  // ring layout: power-of-two capacities, placed largest first (each base aligned to its size)
+  if (tid == 0) {
+    const uint32_t cap = h < FL_HEAD ? FC_HEAD_SLOTS : FC_TAIL_SLOTS;
+    uint32_t off = 0, top = 1;
+    for (uint32_t q = 1; q <= nl; ++q) {
+      uint32_t c = 1;
+      while (c < cmax[q] && c <= cap) c <<= 1;
+      cring[q] = c;
+      off += c;
+      top = max(top, c);
+    }
+    if (off + 1 > cap) {
+      bad_s = 1;  // (+ the dummy entry of untargeted ADDs and no-op records)
+    } else {
+      off = 0;
+      for (uint32_t c = top; c; c >>= 1)
+        for (uint32_t q = 1; q <= nl; ++q)
+          if (cring[q] == c) {
+            rbase[q] = off;
+            off += c;
+          }
+    }
+    nslot_s = off + 1;
+  }
+  __syncthreads();
+  if (bad_s) {
+    if (tid == 0) fc_decline(F, h);
+    return;
+  }
+  const uint32_t nslot = nslot_s, dummy = nslot - 1;
+  if (tid >= 1 && tid <= nl) {
+    LV[tid].cring = cring[tid];
+    LV[tid].rbase = rbase[tid];
+  }
+  uint4* img = F.fc_img + fc_img_off(h);
+  for (uint32_t x = tid; x < nslot; x += FC_PASS_T) img[x] = make_uint4(0u, 0u, 0u, 0u);
+  __syncthreads();
+  const uint32_t npad = (8u - (n & 7u)) & 7u;
+  for (uint32_t i = tid; i < n + npad; i += FC_PASS_T) {
+    const uint32_t b = hd.beg + i;
+    unsigned long long rec = static_cast<unsigned long long>(dummy << 7) << 32;  // no-op
+    if (i < n) {
+      const unsigned long long w32 = F.ord8[hd.obase + i];
+      const uint32_t hi = static_cast<uint32_t>(w32 >> 32), k = hi & 127u;
+      const uint32_t tg = F.fc_tg[b];
+      if (k) {  // an admitted ADD (32-bit record: level, volume in units of g, SALE bit 31)
+        const uint32_t slot = tg ? rbase[k] + (F.fc_rank[b] & (cring[k] - 1u)) : dummy;
+        rec = (static_cast<unsigned long long>(k | (slot << 7) | (hi & 0x80000000u)) << 32) |
+              static_cast<uint32_t>(w32);
+      } else if (prep_at(B, b).action == GOME_DEL) {
+        const FcDel d = F.fc_del[b];
+        if (d.kind != FC_NONE) {
+          const uint32_t kk = d.li, slot = rbase[kk] + (d.rank & (cring[kk] - 1u));
+          const bool sale = prep_at(B, b).side == GOME_SALE;
+          const uint32_t lgc = 31u - __clz(cring[kk]);
+          rec = (static_cast<unsigned long long>(kk | (slot << 7) | (sale ? 1u << 29 : 0u) | (3u << 30)) << 32) |
+                (d.nb | (lgc << 16));
+          if (d.kind == FC_OLD) img[slot] = make_uint4(d.oend, d.ov, 0u, 0u);
+        }
+      }
+    }
+    F.ord8[hd.obase + i] = rec;
+  }
+  if (tid == 0) F.hdr[h].nslot = nslot;
+}
+
+// ---- prep 6: books declined by the cancel prep go to the legacy hot / cold kernels: drop
+// their old targets' marks and route them there (FlowHdr::ok = 0)
+__global__ __launch_bounds__(256) void k_fc_unmark(Dev D, BatchArgs B, FlowArgs F) {
+  const uint32_t h = F.h0 + blockIdx.y;
+  if (h >= fl_hend(D, F) || F.hdr[h].ok != FL_OK_CANCEL || !F.hdr[h].fc_bad) return;
+  const FlowHdr hd = F.hdr[h];
+  uint32_t b0, b1;
+  fc_slice(hd, blockIdx.x, gridDim.x, b0, b1);
+  for (uint32_t b = b0 + threadIdx.x; b < b1; b += blockDim.x) {
+    if (prep_at(B, b).action != GOME_DEL) continue;
+    const FcDel d = F.fc_del[b];
+    if (d.kind == FC_OLD) D.nodes[d.tgt].pad = 0;
+  }
+}
+
+__global__ void k_fc_route(Dev D, FlowArgs F) {
+  const uint32_t h = F.h0 + blockIdx.x * blockDim.x + threadIdx.x;
+  if (h < fl_hend(D, F) && F.hdr[h].ok == FL_OK_CANCEL && F.hdr[h].fc_bad) F.hdr[h].ok = 0;
+}
+
+// ============================================================== reconstruction
+// Makers of a cancel book's level in FIFO order: the gathered old ones IG[0, ig_n) (IgEnt: e =
+// start in consumption space, v, oid, uuid, tx, pad = touch of its cancel or NIL), then the new
+// ones RS[0, nrest) (RsEnt: e = start, v = volume rested, j = order, t = touch of the rest,
+// pad0 = touch of its cancel or NIL).  Consumption space: a maker spans the volume consumed from
+// it — all of it, or what was consumed before its cancel — so consecutive makers abut and
+// a maker's length is the next one's start minus its own.
+struct FcLvlView {
+  const IgEnt* IG;
+  const RsEnt* RS;
+  uint32_t ig_n, nrest, ig_all;
+  int64_t base_new;  // start of the new makers (old live volume minus its cancelled part)
+  int64_t qend;      // end of the last new maker
+};
+
+__device__ __forceinline__ FcLvlView fc_view(const FlowArgs& F, uint32_t h, const FlowLvl& Lq) {
+  FcLvlView V;
+  V.IG = F.ig + Lq.ig_base;
+  V.RS = F.rs + FL_TOUCH_MUL * F.hdr[h].beg + Lq.base;
+  V.ig_n = Lq.ig_n;
+  V.nrest = Lq.nrest;
+  V.ig_all = Lq.ig_all;
+  V.base_new = Lq.d0 - static_cast<int64_t>(static_cast<uint64_t>(Lq.ocan) * F.hdr[h].g);
+  V.qend = static_cast<int64_t>((static_cast<uint64_t>(Lq.pad1) << 32) | Lq.pad0);
+  return V;
+}
+
+__device__ __forceinline__ int64_t fc_start(const FcLvlView& V, uint32_t m) {
+  return m < V.ig_n ? V.IG[m].e : V.RS[m - V.ig_n].e;
+}
+__device__ __forceinline__ int64_t fc_len(const FcLvlView& V, uint32_t m) {
+  if (m + 1 < V.ig_n) return V.IG[m + 1].e - V.IG[m].e;
+  // the last gathered old maker: the new makers follow it, or (not all gathered) it is an
+  // untargeted one, never cancelled
+  if (m + 1 == V.ig_n) return V.ig_all ? V.base_new - V.IG[m].e : V.IG[m].v;
+  if (m + 1 < V.ig_n + V.nrest) return V.RS[m + 1 - V.ig_n].e - V.RS[m - V.ig_n].e;
+  return V.qend - V.RS[m - V.ig_n].e;
+}
+__device__ __forceinline__ int64_t fc_vol(const FcLvlView& V, uint32_t m) {
+  return m < V.ig_n ? V.IG[m].v : V.RS[m - V.ig_n].v;
+}
+__device__ __forceinline__ uint32_t fc_ct(const FcLvlView& V, uint32_t m) {
+  return m < V.ig_n ? V.IG[m].pad : V.RS[m - V.ig_n].pad0;
+}
+// The maker spanning consumption point x: the last whose start <= x (a zero-length maker shares
+// its successor's start, so the search lands on the one with volume there).
+__device__ __forceinline__ uint32_t fc_find(const FcLvlView& V, int64_t x) {
+  if (x < V.base_new) {
+    uint32_t lo = 0, hi = V.ig_n;
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (V.IG[mid].e <= x) lo = mid; else hi = mid;
+    }
+    return lo;
+  }
+  uint32_t lo = 0, hi = V.nrest;
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (V.RS[mid].e <= x) lo = mid; else hi = mid;
+  }
+  return V.ig_n + lo;
+}
+
+// ---- k_fc_level: one wave per (book, level) ----------------------------------------------
+__device__ __forceinline__ void fc_level_one(const Dev& D, const FlowArgs& F, uint32_t h, uint32_t q) {
+  const FlowHdr* hd = &F.hdr[h];
+  const uint32_t lane = lane_id();
+  const unsigned long long ltm = lt_mask();
+  FlowLvl* Lq = &F.lvl[h * FL_CAP + q];
+  const uint32_t beg = uni(hd->beg);
+  const uint32_t L = FL_TOUCH_MUL * beg;
+  const unsigned long long g = static_cast<unsigned long long>(uni64(static_cast<int64_t>(hd->g)));
+  const uint32_t base = uni(Lq->base), cnt = uni(Lq->cnt);
+  const int64_t d0 = uni64(Lq->d0);
+  SEnt* R = F.srt + L + base;
+  RsEnt* RS = F.rs + L + base;
+  // 1. each cancel -> its DEL's record (r, touch); the consumption cursor before each consume
+  int64_t cc = 0, ocan = 0;
+  uint32_t nr = 0, ncan_old = 0;
+  for (uint32_t c0 = 0; c0 < cnt; c0 += 64) {
+    const uint32_t i = c0 + lane;
+    const bool valid = i < cnt;
+    SEnt e{};
+    if (valid) e = R[i];
+    const bool isc = valid && e.kind == TK_CONS, isx = valid && e.kind == TK_CANC;
+    if (isx) {
+      FcDel* d = &F.fc_del[beg + e.j];
+      d->r = e.amt;
+      d->ct = e.t;
+      if (d->kind == FC_OLD) { ocan += e.amt; ncan_old++; }
+    }
+    const int64_t ac = isc ? e.amt : 0;
+    const int64_t ic = wave_incl_scan(ac);
+    if (isc) R[i].coord = cc + ic - ac;
+    cc += rl64(ic, 63);
+    nr += __popcll(__ballot(valid && e.kind == TK_REST));
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    ocan += __shfl_xor(ocan, off);
+    ncan_old += __shfl_xor(ncan_old, off);
+  }
+  __threadfence();  // the DEL records are read back below (by other lanes)
+  const int64_t cfin = cc;
+  const int64_t base_new = d0 - ocan;
+  // 2. the new makers in FIFO (rest) order, their consumption-space starts and cancels
+  int64_t acc = base_new;
+  uint32_t k = 0;
+  for (uint32_t c0 = 0; c0 < cnt; c0 += 64) {
+    const uint32_t i = c0 + lane;
+    const bool valid = i < cnt;
+    SEnt e{};
+    if (valid) e = R[i];
+    const bool isr = valid && e.kind == TK_REST;
+    uint32_t ct = NIL;
+    int64_t len = 0;
+    if (isr) {
+      len = e.amt;
+      const uint32_t tg = F.fc_tg[beg + e.j];
+      if (tg) {
+        const FcDel d = F.fc_del[tg - 1u];
+        if (d.ct != NIL) { ct = d.ct; len = e.amt - d.r; }
+      }
+    }
+    const int64_t il = wave_incl_scan(len);
+    const unsigned long long rm = __ballot(isr);
+    if (isr) {
+      RsEnt x;
+      x.e = acc + il - len;
+      x.v = e.amt;
+      x.j = e.j;
+      x.t = e.t;
+      x.pad0 = ct;
+      x.pad1 = 0;
+      RS[k + __popcll(rm & ltm)] = x;
+    }
+    acc += rl64(il, 63);
+    k += __popcll(rm);
+  }
+  const int64_t qend = acc;
+  // 3. the old FIFO, gathered through the consumption end, then on through targeted makers (a
+  //    later cancel may remove them) to the first untargeted one (never cancelled, so a
+  //    MatchNode.NextNode search stops there)
+  const uint32_t nv0 = uni(Lq->nv0), tail = uni(Lq->tail), tslot = uni(Lq->tslot);
+  uint32_t head = uni(Lq->head), hslot = uni(Lq->hslot);
+  uint32_t ttail = tail, ttslot = tslot;
+  uint32_t ig_base = 0, ng = 0, consumed = 0;
+  bool ig_all = true;
+  if (nv0 > 0 && (cfin > 0 || uni(Lq->c_old))) {
+    uint32_t bb = 0;
+    if (lane == 0) bb = atomicAdd(F.ig_bump, nv0);
+    ig_base = uni(bb);
+    if (static_cast<unsigned long long>(ig_base) + nv0 > F.ig_cap) {
+      if (lane == 0) atomicOr(&D.st->err, ERR_CHUNKS);
+      return;
+    }
+    IgEnt* IG = F.ig + ig_base;
+    int64_t E = 0;
+    bool have_surv = false, stop = false;
+    uint32_t c = head, s0 = hslot, nh = NIL, nhs = 0;
+    for (uint32_t guard = 0; c != NIL && !stop; ++guard) {
+      if (guard > D.ch_cap) { if (lane == 0) atomicOr(&D.st->err, ERR_CORRUPT); return; }
+      const uint32_t lim = (c == tail) ? tslot : CH;
+      const bool inr = lane < CH && lane >= s0 && lane < lim;
+      Node nd{};
+      if (inr) nd = D.nodes[c * CH + lane];
+      const bool live = inr && nd.rem >= 0;
+      const bool targ = live && nd.pad != 0;
+      uint32_t ct = NIL;
+      int64_t len = live ? nd.rem : 0;
+      if (targ) {
+        const FcDel d = F.fc_del[static_cast<uint32_t>(nd.pad) - 1u];
+        if (d.ct != NIL) { ct = d.ct; len = nd.rem - d.r; }
+      }
+      const int64_t inc = wave_incl_scan(len);
+      const int64_t em = E + inc - len;
+      const unsigned long long after = __ballot(live && em >= cfin && !targ);
+      const uint32_t fb = after ? static_cast<uint32_t>(__builtin_ctzll(after)) : 64u;
+      const bool take = live && lane <= fb;
+      const unsigned long long tm = __ballot(take);
+      if (take) {
+        IgEnt gq;
+        gq.e = em;
+        gq.v = nd.rem;
+        gq.oid = nd.oid;
+        gq.uuid = nd.uuid;
+        gq.tx = nd.tx;
+        gq.pad = ct;
+        IG[ng + __popcll(tm & ltm)] = gq;
+      }
+      ng += __popcll(tm);
+      // fully consumed (uncancelled) makers leave with their index entries
+      const bool cons = live && ct == NIL && em + nd.rem <= cfin;
+      if (cons) __hip_atomic_store(&D.idx[nd.ixs].key, KEY_TOMB, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      consumed += __popcll(__ballot(cons));
+      if (!have_surv) {
+        const unsigned long long sv = __ballot(live && ct == NIL && em + nd.rem > cfin);
+        if (sv) {
+          have_surv = true;
+          nh = c;
+          nhs = static_cast<uint32_t>(__builtin_ctzll(sv));
+          if (lane == nhs && em < cfin) D.nodes[c * CH + lane].rem = em + nd.rem - cfin;  // partial head
+        } else {
+          // nothing survives in this chunk: consumed / cancelled makers only (k_fc_events
+          // tombstones the cancelled ones; the chunk goes back to the pool)
+          if (lane == 0) D.freed_ids[atomicAdd(&D.st->freed_top, 1u)] = c;
+        }
+      }
+      if (after) { stop = true; ig_all = false; }
+      E += rl64(inc, 63);
+      c = (c == tail) ? NIL : uni(D.chdr[c].next);
+      s0 = 0;
+    }
+    if (!have_surv && ig_all) {
+      head = ttail = NIL;
+      hslot = ttslot = 0;
+    } else if (have_surv) {
+      head = nh;
+      hslot = nhs;
+    }
+    // (!have_surv && !ig_all cannot happen: the untargeted stop maker survives)
+  }
+  if (lane == 0) {
+    Lq->cfin = cfin;
+    Lq->nrest = nr;
+    Lq->ig_base = ig_base;
+    Lq->ig_n = ng;
+    Lq->ig_all = ig_all ? 1u : 0u;
+    Lq->head = head;
+    Lq->tail = ttail;
+    Lq->hslot = hslot;
+    Lq->tslot = ttslot;
+    Lq->nlive0 = nv0 - consumed - ncan_old;
+    Lq->ocan = static_cast<uint32_t>(static_cast<uint64_t>(ocan) / g);
+    Lq->pad0 = static_cast<uint32_t>(static_cast<uint64_t>(qend));
+    Lq->pad1 = static_cast<uint32_t>(static_cast<uint64_t>(qend) >> 32);
+  }
+}
+
+__global__ __launch_bounds__(64) void k_fc_level_wide(Dev D, FlowArgs F) {
+  const uint32_t h = F.h0 + blockIdx.y, q = blockIdx.x;
+  if (h >= fl_hend(D, F) || !fc_book(F, h) || q == 0 || q > F.hdr[h].nl) return;
+  fc_level_one(D, F, h, q);
+}
+
+__global__ __launch_bounds__(1024) void k_fc_level_book(Dev D, FlowArgs F) {
+  const uint32_t h = F.h0 + blockIdx.x;
+  if (h >= fl_hend(D, F) || !fc_book(F, h)) return;
+  for (uint32_t q = 1 + (threadIdx.x >> 6); q <= F.hdr[h].nl; q += blockDim.x / 64) fc_level_one(D, F, h, uni(q));
+}
+
+// ---- fills of one consume touch ----------------------------------------------------------
+struct FcTouch {
+  FcLvlView V;
+  const FlowLvl* Lq;
+  int64_t c, a;           // cursor before the touch, amount
+  uint32_t first, last;   // makers spanned
+};
+
+__device__ __forceinline__ FcTouch fc_touch(const FlowArgs& F, uint32_t h, uint32_t L, const Touch& x) {
+  FcTouch T;
+  const uint32_t k = x.kr & 127u;
+  T.Lq = &F.lvl[h * FL_CAP + k];
+  T.V = fc_view(F, h, *T.Lq);
+  T.c = F.srt[L + x.pos].coord;
+  T.a = x.amt;
+  T.first = fc_find(T.V, T.c);
+  T.last = fc_find(T.V, T.c + T.a - 1);
+  return T;
+}
+
+// Fills of a consume touch: makers of [first, last] with volume in consumption space.
+__device__ __forceinline__ uint32_t fc_nfills(const FcTouch& T, uint32_t& pops) {
+  uint32_t nf = 0;
+  pops = 0;
+  for (uint32_t m = T.first; m <= T.last; ++m) {
+    const int64_t len = fc_len(T.V, m);
+    if (len <= 0) continue;
+    ++nf;
+    if (fc_start(T.V, m) + fc_vol(T.V, m) <= T.c + T.a) ++pops;  // filled to its whole volume
+  }
+  return nf;
+}
+
+// ---- k_fc_count: events per touch and per order (thread per touch of the range's books) ----
+__global__ void k_fc_count(Dev D, BatchArgs B, FlowArgs F) {
+  const uint32_t hend = fl_hend(D, F), nb = hend > F.h0 ? hend - F.h0 : 0u;
+  const uint32_t total = nb ? F.toff[F.tb + nb] : 0u;
+  unsigned long long fills = 0, pops = 0, cancels = 0;
+  for (uint32_t gt = blockIdx.x * blockDim.x + threadIdx.x; gt < total; gt += gridDim.x * blockDim.x) {
+    const uint32_t hb = fl_book_of(F, nb, gt), h = F.h0 + hb, t = gt - F.toff[F.tb + hb];
+    const uint32_t nt = F.hdr[h].ntouch, beg = F.hdr[h].beg, L = FL_TOUCH_MUL * beg;
+    const Touch x = F.log[L + t];
+    if (t > 0 && tk_j(F.log[L + t - 1]) == tk_j(x)) continue;
+    uint32_t acc = 0;
+    for (uint32_t u = t; u < nt; ++u) {
+      const Touch y = (u == t) ? x : F.log[L + u];
+      if (tk_j(y) != tk_j(x)) break;
+      F.fbase[L + u] = acc;
+      const uint32_t kind = tk_kind(y.kr, true);
+      if (kind == TK_CONS) {
+        uint32_t pp;
+        const uint32_t nf = fc_nfills(fc_touch(F, h, L, y), pp);
+        acc += nf;
+        fills += nf;
+        pops += pp;
+      } else if (kind == TK_CANC) {
+        acc += 1;
+        cancels += 1;
+      }
+    }
+    if (tk_j(x) < F.hdr[h].end - beg) B.ev_count[prep_at(B, beg + tk_j(x)).idx] = acc;  // not padding
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    fills += __shfl_xor(fills, off);
+    pops += __shfl_xor(pops, off);
+    cancels += __shfl_xor(cancels, off);
+  }
+  if (lane_id() == 0 && (fills || cancels)) {
+    unsigned long long* c = D.st->ctr;
+    atomicAdd(&c[C_FILLS], fills);
+    atomicAdd(&c[C_HOT_FILLS], fills);
+    atomicAdd(&c[C_CANCELS], cancels);
+    atomicAdd(&c[C_HOT_CANCELS], cancels);
+    atomicAdd(&c[C_FLOW_CANCELS], cancels);
+    atomicAdd(&c[C_RESTING_DELTA], static_cast<unsigned long long>(-static_cast<long long>(pops + cancels)));
+  }
+}
+
+// ---- k_fc_events: every MatchResult of the range's books, into the event arena -------------
+__global__ __launch_bounds__(256) void k_fc_events(Dev D, BatchArgs B, FlowArgs F) {
+  const uint32_t hend = fl_hend(D, F), nb = hend > F.h0 ? hend - F.h0 : 0u;
+  const uint32_t total = nb ? F.toff[F.tb + nb] : 0u;
+  const uint32_t lane = lane_id(), stride = gridDim.x * blockDim.x;
+  for (uint32_t g0 = blockIdx.x * blockDim.x + (threadIdx.x & ~63u); g0 < total; g0 += stride) {
+    const uint32_t gt = g0 + lane;
+    uint32_t h = 0, L = 0, t = 0, cnt = 0, kind = TK_REST;
+    Touch x{};
+    FcTouch T{};
+    if (gt < total) {
+      const uint32_t hb = fl_book_of(F, nb, gt);
+      h = F.h0 + hb;
+      t = gt - F.toff[F.tb + hb];
+      L = FL_TOUCH_MUL * F.hdr[h].beg;
+      x = F.log[L + t];
+      kind = tk_kind(x.kr, true);
+      if (kind == TK_CONS) {
+        uint32_t pp;
+        T = fc_touch(F, h, L, x);
+        cnt = fc_nfills(T, pp);
+      } else if (kind == TK_CANC) {
+        cnt = 1;
+      }
+    }
+    uint32_t inc = cnt;
+    for (uint32_t off = 1; off < 64; off <<= 1) {
+      const uint32_t v = __shfl_up(inc, off);
+      if (lane >= off) inc += v;
+    }
+    const uint32_t tot = __shfl(inc, 63);
+    uint32_t base = 0;
+    if (lane == 0 && tot) base = atomicAdd(&D.st->ev_bump, tot);
+    base = __shfl(base, 0);
+    if (base + tot > B.arena_cap) {
+      if (lane == 0 && tot) atomicOr(&D.st->err, ERR_EVENTS);
+      continue;
+    }
+    if (!cnt) continue;
+    gome_event* dst = B.arena + base + (inc - cnt);
+    const uint32_t beg = F.hdr[h].beg, sym = F.hdr[h].sym;
+    const Prep tk = prep_at(B, beg + tk_j(x));
+    const int64_t price = F.lvl[h * FL_CAP + (x.kr & 127u)].price;
+    if (kind == TK_CANC) {  // DeleteOrder's MatchResult (engine.go:109-113)
+      const FcDel d = F.fc_del[beg + tk_j(x)];
+      gome_event ev;
+      ev.price_fx = tk.price;
+      ev.match_volume_fx = 0;
+      ev.maker_volume_fx = x.amt;
+      ev.taker_volume_fx = x.amt;
+      ev.taker_seq = tk.idx;
+      ev.fill_idx = 0;
+      ev.symbol_id = sym;
+      ev.maker_oid_id = tk.oid;
+      ev.maker_uuid_id = tk.uuid;
+      ev.maker_next_oid_id = 0;
+      ev.kind = GOME_EV_CANCEL;
+      ev.maker_side = tk.side;
+      ev.maker_is_last = 1;
+      ev.pad0 = 0;
+      ev.seq_hi = 0;
+      dst[0] = ev;
+      if (d.kind == FC_OLD) {  // unlink (nodelink.go:124-166): a tombstone, the index entry erased
+        Node* nd = &D.nodes[d.tgt];
+        nd->rem = -1;
+        nd->pad = 0;
+        __hip_atomic_store(&D.idx[d.ixs].key, KEY_TOMB, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      continue;
+    }
+    // taker remaining before this level: volume minus what its better levels took
+    int64_t tb = tk.vol;
+    for (uint32_t u = t; u > 0; --u) {
+      const Touch y = F.log[L + u - 1];
+      if (tk_j(y) != tk_j(x)) break;
+      tb -= y.amt;
+    }
+    const FcLvlView& V = T.V;
+    const uint32_t fb = F.fbase[L + t];
+    uint32_t k = 0;
+    for (uint32_t m = T.first; m <= T.last; ++m) {
+      const int64_t len = fc_len(V, m);
+      if (len <= 0) continue;
+      const int64_t e = fc_start(V, m), v = fc_vol(V, m);
+      uint32_t oid, uuid, tx;
+      if (m < V.ig_n) {
+        const IgEnt gq = V.IG[m];
+        oid = gq.oid; uuid = gq.uuid; tx = gq.tx;
+      } else {
+        const Prep mk = prep_at(B, beg + V.RS[m - V.ig_n].j);
+        oid = mk.oid; uuid = mk.uuid; tx = mk.side;
+      }
+      const int64_t lo = e > T.c ? e : T.c;
+      const int64_t hi = (e + len < T.c + T.a) ? e + len : T.c + T.a;
+      const int64_t qty = hi - lo, pre = e + v - lo;  // remaining before this fill
+      const bool full = e + v <= T.c + T.a;
+      // MatchNode.NextNode: the next maker of the FIFO at the time of this fill — arrived
+      // before it, not cancelled before it (engine.go:138-198 reads the head node's link)
+      uint32_t nx = 0, last = 1;
+      for (uint32_t m2 = m + 1; m2 < V.ig_n + V.nrest; ++m2) {
+        if (m2 >= V.ig_n && V.RS[m2 - V.ig_n].t > t) break;  // not rested yet
+        const uint32_t ct = fc_ct(V, m2);
+        if (ct != NIL && ct < t) continue;                     // cancelled before
+        nx = m2 < V.ig_n ? V.IG[m2].oid : prep_at(B, beg + V.RS[m2 - V.ig_n].j).oid;
+        last = 0;
+        break;
+      }
+      gome_event ev;
+      ev.price_fx = price;
+      ev.match_volume_fx = qty;
+      ev.maker_volume_fx = full ? pre : pre - qty;
+      ev.taker_volume_fx = tb - (hi - T.c);
+      ev.taker_seq = tk.idx;
+      ev.fill_idx = fb + k;
+      ev.symbol_id = sym;
+      ev.maker_oid_id = oid;
+      ev.maker_uuid_id = uuid;
+      ev.maker_next_oid_id = nx;
+      ev.kind = GOME_EV_FILL;
+      ev.maker_side = static_cast<uint8_t>(tx);
+      ev.maker_is_last = static_cast<uint8_t>(last);
+      ev.pad0 = 0;
+      ev.seq_hi = 0;
+      dst[k] = ev;
+      ++k;
+    }
+  }
+}
+
+// ---- k_fc_write: surviving new makers appended, the final level record (wave per level) ----
+__device__ __forceinline__ Level fc_write_level(const Dev& D, const BatchArgs& B, const FlowArgs& F,
+                                                const FlowHdr& hd, uint32_t h, uint32_t q) {
+  const uint32_t lane = lane_id();
+  const unsigned long long ltm = lt_mask();
+  const unsigned long long mask = D.idx_mask;
+  const FlowLvl f = F.lvl[h * FL_CAP + q];
+  const FcLvlView V = fc_view(F, h, f);
+  Level x{};
+  x.price = f.price;
+  x.head = x.tail = NIL;
+  // survivors among the new makers: not cancelled, not filled to the end (in FIFO order); a
+  // maker starting before the consumption end keeps e + v - cfin
+  uint32_t S = 0;
+  for (uint32_t c0 = 0; c0 < V.nrest; c0 += 64) {
+    const uint32_t i = c0 + lane;
+    bool sv = false;
+    if (i < V.nrest) {
+      const RsEnt r = V.RS[i];
+      sv = r.pad0 == NIL && r.e + r.v > f.cfin;
+    }
+    S += __popcll(__ballot(sv));
+  }
+  const bool fresh = f.nlive0 == 0;
+  const uint32_t s0 = fresh ? 0u : f.tslot;
+  const uint32_t room = fresh ? 0u : CH - s0;
+  const uint32_t need = S > room ? (S - room + CH - 1) / CH : 0u;
+  int t = 0;
+  uint32_t nst = 0, bb = 0;
+  if (need) {
+    if (lane == 0) t = atomicSub(&D.st->free_top, static_cast<int>(need));
+    t = static_cast<int>(uni(static_cast<uint32_t>(t)));
+    nst = static_cast<uint32_t>(min(max(t, 0), static_cast<int>(need)));
+    if (lane == 0 && nst < need) bb = atomicAdd(D.ch_bump, need - nst);
+    bb = uni(bb);
+    if (bb + (need - nst) > D.ch_cap) {
+      if (lane == 0) atomicOr(&D.st->err, ERR_CHUNKS);
+      return x;
+    }
+  }
+  auto chunk_id = [&](uint32_t i) -> uint32_t {
+    return i < nst ? D.free_ids[t - static_cast<int>(nst) + static_cast<int>(i)] : bb + (i - nst);
+  };
+  for (uint32_t i = lane; i < need; i += 64) {
+    ChunkHdr c;
+    c.next = (i + 1 < need) ? chunk_id(i + 1) : NIL;
+    c.pad = 0;
+    c.price = f.price;
+    D.chdr[chunk_id(i)] = c;
+  }
+  if (need && !fresh && lane == 0) D.chdr[f.tail].next = chunk_id(0);
+  uint32_t w = 0;
+  for (uint32_t c0 = 0; c0 < V.nrest; c0 += 64) {
+    const uint32_t i = c0 + lane;
+    RsEnt r{};
+    bool sv = false;
+    if (i < V.nrest) {
+      r = V.RS[i];
+      sv = r.pad0 == NIL && r.e + r.v > f.cfin;
+    }
+    const unsigned long long sm = __ballot(sv);
+    if (sv) {
+      const uint32_t gi = w + __popcll(sm & ltm);
+      const Prep mk = prep_at(B, hd.beg + r.j);
+      const int64_t rem = (r.e < f.cfin) ? r.e + r.v - f.cfin : r.v;
+      uint32_t cid, slot;
+      if (!fresh && s0 + gi < CH) {
+        cid = f.tail;
+        slot = s0 + gi;
+      } else {
+        const uint32_t gg = fresh ? gi : gi - room;
+        cid = chunk_id(gg / CH);
+        slot = gg % CH;
+      }
+      const uint32_t loc = cid * CH + slot;
+      const unsigned long long key = (static_cast<unsigned long long>(hd.sym + 1) << 32) | mk.oid;
+      unsigned long long hh = mix64(key) & mask, probe = 0;
+      for (; probe <= mask; ++probe, hh = (hh + 1) & mask) {
+        const unsigned long long kv = __hip_atomic_load(&D.idx[hh].key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((kv == KEY_EMPTY || kv == KEY_TOMB) && atomicCAS(&D.idx[hh].key, kv, key) == kv) break;
+      }
+      if (probe > mask) {
+        atomicOr(&D.st->err, ERR_INDEX);
+      } else {
+        D.idx[hh].loc = loc;
+        Node nd{};
+        nd.rem = rem;
+        nd.oid = mk.oid;
+        nd.uuid = mk.uuid;
+        nd.ixs = static_cast<uint32_t>(hh);
+        nd.tx = mk.side;
+        D.nodes[loc] = nd;
+      }
+    }
+    w += __popcll(sm);
+  }
+  x.depth = f.dfin;
+  x.nlive = f.nlive0 + S;
+  uint32_t mem = 0;
+  if ((hd.amask[q >> 6] >> (q & 63)) & 1ull) mem |= M_SALE;
+  if ((hd.bmask[q >> 6] >> (q & 63)) & 1ull) mem |= M_BUY;
+  x.member = static_cast<uint8_t>(mem);
+  if (x.nlive == 0) {
+    x.hslot = x.tslot = 0;
+  } else if (fresh) {
+    x.head = chunk_id(0);
+    x.hslot = 0;
+    x.tail = chunk_id(need - 1);
+    x.tslot = static_cast<uint8_t>(S - (need - 1) * CH);
+  } else {
+    x.head = f.head;
+    x.hslot = static_cast<uint8_t>(f.hslot);
+    x.tail = need ? chunk_id(need - 1) : f.tail;
+    x.tslot = static_cast<uint8_t>(need ? (S - room) - (need - 1) * CH : s0 + S);
+  }
+  const bool ok = (x.nlive > 0) == (x.depth > 0) && (x.nlive > 0) == (mem == M_BUY || mem == M_SALE) &&
+                  (x.nlive > 0 || mem == 0);
+  if (!ok && lane == 0) atomicOr(&D.st->err, ERR_CORRUPT);
+  return x;
+}
+
+__global__ __launch_bounds__(64) void k_fc_write_lv(Dev D, BatchArgs B, FlowArgs F) {
+  const uint32_t h = F.h0 + blockIdx.y, q = blockIdx.x;
+  if (h >= fl_hend(D, F) || !fc_book(F, h)) return;
+  const FlowHdr hd = F.hdr[h];
+  if (q == 0 || q > hd.nl) return;
+  const Level x = fc_write_level(D, B, F, hd, h, q);
+  if (lane_id() == 0) F.lvout[h * FL_CAP + q] = x;
+}
+
+// The book: level array compaction and counters (as k_flow_write_fin), DELs and their stats.
+__global__ __launch_bounds__(128) void k_fc_fin(Dev D, FlowArgs F) {
+  __shared__ Level lv[FL_CAP];
+  __shared__ uint32_t keep[FL_CAP];
+  __shared__ uint32_t nout_s, base_s, cap_s;
+  const uint32_t h = F.h0 + blockIdx.x;
+  if (h >= fl_hend(D, F) || !fc_book(F, h)) return;
+  const FlowHdr hd = F.hdr[h];
+  for (uint32_t q = 1 + threadIdx.x; q <= hd.nl; q += blockDim.x) lv[q] = F.lvout[h * FL_CAP + q];
+  __syncthreads();
+  fl_write_finish(D, hd, lv, keep, base_s, cap_s, nout_s);
+  if (threadIdx.x == 0) {
+    atomicAdd(&D.st->ctr[C_DEL], static_cast<unsigned long long>(hd.ndel));
+    if (F.h0 == 0) {
+      atomicAdd(&D.st->ctr[C_FLOW_HEAD_ORDERS], static_cast<unsigned long long>(hd.end - hd.beg));
+      atomicAdd(&D.st->ctr[C_FLOW_HEAD_TOUCHES], static_cast<unsigned long long>(hd.ntouch));
+    }
+  }
+}
+
+// Tail books: one workgroup per book (waves take its levels), then the compaction.
+__global__ __launch_bounds__(FL_WRITE_T) void k_fc_write_book(Dev D, BatchArgs B, FlowArgs F) {
+  __shared__ Level lv[FL_CAP];
+  __shared__ uint32_t keep[FL_CAP];
+  __shared__ uint32_t nout_s, base_s, cap_s;
+  const uint32_t h = F.h0 + blockIdx.x;
+  if (h >= fl_hend(D, F) || !fc_book(F, h)) return;
+  const FlowHdr hd = F.hdr[h];
+  const uint32_t w = threadIdx.x >> 6, nw = FL_WRITE_T / 64;
+  for (uint32_t q = 1 + w; q <= hd.nl; q += nw) {
+    const Level x = fc_write_level(D, B, F, hd, h, uni(q));
+    if (lane_id() == 0) lv[q] = x;
+  }
+  __syncthreads();
+  fl_write_finish(D, hd, lv, keep, base_s, cap_s, nout_s);
+  if (threadIdx.x == 0) atomicAdd(&D.st->ctr[C_DEL], static_cast<unsigned long long>(hd.ndel));
+}
+
+}  // namespace gome

@@ -292,8 +292,8 @@ def test_flow_equals_legacy_hot_kernel():
 
 
 def test_flow_then_cancels_then_flow():
-    """Book state handed between paths: ADD-only batches (flow), cancel-heavy batches
-    (legacy hot kernel: DELs are not flow-eligible), then ADD-only again."""
+    """Book state handed between batches: ADD-only batches, a cancel-heavy batch (cancels of
+    makers at every FIFO position, on the flow path's cancel plan), then ADD-only again."""
     rng = np.random.default_rng(99)
     st = wl.Stream(2, seed=99)
     adds1 = [st.batch(8000) for _ in range(2)]
@@ -316,7 +316,7 @@ def test_flow_then_cancels_then_flow():
     mix = np.concatenate([dels, st.batch(4000)])
     eng.submit(mix)
     _cmp_events(eng.drain(), orc.submit(mix), "cancel batch")
-    assert eng.stats()["n_flow_books"] == 0
+    assert eng.stats()["n_flow_books"] == 2 and eng.stats()["n_flow_cancels"] > 1000
     for b in [st.batch(8000) for _ in range(2)]:
         eng.submit(b)
         _cmp_events(eng.drain(), orc.submit(b), "adds2")

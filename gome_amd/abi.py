@@ -89,6 +89,10 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.gome_pending_events.restype = C.c_size_t
     lib.gome_device_events.argtypes = [VP, P(VP), P(C.c_size_t)]
     lib.gome_release_device_events.argtypes = [VP]
+    lib.gome_debug_flow_books.argtypes = [VP, C.POINTER(C.c_uint32), C.c_size_t, C.POINTER(C.c_size_t)]
+    lib.gome_debug_flow_books.restype = C.c_int32
+    lib.gome_debug_peek.argtypes = [VP, C.c_uint32, C.c_uint64, C.c_uint64, VP]
+    lib.gome_debug_peek.restype = C.c_int32
     lib.gome_release_device_events.restype = C.c_int32
     lib.gome_get_stats.argtypes = [VP, P(Stats)]
     lib.gome_snapshot_levels.argtypes = [VP, C.c_uint32, VP, C.c_size_t, P(C.c_size_t)]
@@ -262,6 +266,24 @@ class Engine:
     def release_device_events(self):
         """The caller consumed the last device batch's events on the device."""
         self._check(self.lib.gome_release_device_events(self.h))
+
+    FLOW_BOOK_DTYPE = np.dtype([("kind", "<u4"), ("decline", "<u4"), ("symbol_id", "<u4"), ("orders", "<u4"),
+                                ("dels", "<u4"), ("levels", "<u4"), ("w32", "<u4"), ("ring", "<u4"),
+                                ("window", "<u4"), ("pad", "<u4")])
+
+    def debug_flow_books(self, cap: int = 4096) -> np.ndarray:
+        """The last batch's hot-book routing (gome_debug_flow_books; diagnostics)."""
+        out = np.zeros(cap, self.FLOW_BOOK_DTYPE)
+        n = C.c_size_t()
+        self._check(self.lib.gome_debug_flow_books(self.h, out.ctypes.data_as(C.POINTER(C.c_uint32)), cap,
+                                                   C.byref(n)))
+        return out[:n.value]
+
+    def debug_peek(self, which: int, offset: int, nbytes: int) -> bytes:
+        """Raw bytes of a flow-path scratch array after the last batch (gome_debug_peek)."""
+        buf = C.create_string_buffer(max(nbytes, 1))
+        self._check(self.lib.gome_debug_peek(self.h, which, offset, nbytes, buf))
+        return buf.raw[:nbytes]
 
     def stats(self) -> dict:
         st = Stats()

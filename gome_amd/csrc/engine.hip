@@ -535,6 +535,7 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   auto cancel_prep = [&](const FlowArgs& R, uint32_t nb, uint32_t px, bool wide, hipStream_t st) {
     k_fc_hash_claim<<<dim3(px, nb), 256, 0, st>>>(D, B, R);
     k_fc_hash_count<<<dim3(px, nb), 256, 0, st>>>(D, B, R);
+    k_fc_hash_first<<<dim3(px, nb), 256, 0, st>>>(D, B, R);
     k_fc_resolve<<<dim3(px, nb), 256, 0, st>>>(D, B, R);
     if (wide) k_fc_oldwalk_wide<<<dim3(FL_CAP, nb), 64, 0, st>>>(D, R);
     else k_fc_oldwalk_book<<<nb, 1024, 0, st>>>(D, R);
@@ -970,6 +971,46 @@ gome_status gome_device_events(gome_engine* e, const gome_event** dev_ptr, size_
 gome_status gome_release_device_events(gome_engine* e) {
   if (!e) return GOME_E_INVAL;
   e->dev_events = e->dev_events_pos = 0;
+  return GOME_OK;
+}
+
+gome_status gome_debug_flow_books(gome_engine* e, uint32_t* out, size_t cap, size_t* n_out) {
+  if (!e || !n_out || (cap && !out)) return GOME_E_INVAL;
+  gome_status s = e->collect_all();
+  if (s != GOME_OK) return s;
+  const size_t n = std::min<size_t>({cap, static_cast<size_t>(e->stats.n_hot), static_cast<size_t>(gome::MAX_FLOW)});
+  std::vector<gome::FlowHdr> h(n);
+  if (n && hipMemcpy(h.data(), e->F.hdr, n * sizeof(gome::FlowHdr), hipMemcpyDeviceToHost) != hipSuccess)
+    return e->fail(GOME_E_DEVICE, "gome_debug_flow_books: copy failed");
+  for (size_t i = 0; i < n; ++i) {
+    const gome::FlowHdr& x = h[i];
+    const uint32_t w[GOME_DEBUG_FLOW_WORDS] = {x.ok, x.fc_bad, x.sym, x.end - x.beg, x.ndel, x.nl, x.w32, x.nslot,
+                                               x.ncancel, 0u};
+    std::copy(w, w + GOME_DEBUG_FLOW_WORDS, out + i * GOME_DEBUG_FLOW_WORDS);
+  }
+  *n_out = n;
+  return GOME_OK;
+}
+
+gome_status gome_debug_peek(gome_engine* e, uint32_t which, uint64_t offset, uint64_t bytes, void* out) {
+  if (!e || (bytes && !out)) return GOME_E_INVAL;
+  gome_status s = e->collect_all();
+  if (s != GOME_OK) return s;
+  const uint64_t nb = e->max_batch;
+  const void* base = nullptr;
+  uint64_t size = 0;
+  switch (which) {
+    case 0: base = e->F.hdr; size = sizeof(gome::FlowHdr) * gome::MAX_FLOW; break;
+    case 1: base = e->F.lvl; size = sizeof(gome::FlowLvl) * gome::MAX_FLOW * gome::FL_CAP; break;
+    case 2: base = e->F.fc_del; size = sizeof(gome::FcDel) * nb; break;
+    case 3: base = e->F.fc_rank; size = 4 * nb; break;
+    case 4: base = e->F.fc_tg; size = 4 * nb; break;
+    case 5: base = e->F.ord8; size = 8 * (static_cast<uint64_t>(gome::FL_ORD8_MUL) * nb + gome::FL_ORD8_PAD); break;
+    default: return GOME_E_INVAL;
+  }
+  if (offset > size || bytes > size - offset) return GOME_E_INVAL;
+  if (bytes && hipMemcpy(out, static_cast<const char*>(base) + offset, bytes, hipMemcpyDeviceToHost) != hipSuccess)
+    return e->fail(GOME_E_DEVICE, "gome_debug_peek: copy failed");
   return GOME_OK;
 }
 

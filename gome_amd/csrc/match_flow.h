@@ -122,11 +122,16 @@ struct FlowHdr {
   // books whose segment holds DELs (ok == FL_OK_CANCEL, match_flow_cancel.h)
   uint32_t ndel;       // DEL records of the segment
   uint32_t nslot;      // LDS ring entries of the plan (16 B each, the dummy entry included)
-  uint32_t ncancel;    // cancels applied (DELs that found their maker)
+  uint32_t ncancel;    // the cancel prep's longest window + 1 (diagnostics)
   uint32_t fc_bad;     // set by the cancel prep: decline the book (legacy / cold kernels)
 };
 // FlowHdr::ok: 0 declined, FL_OK_ADD an ADD-only flow book, FL_OK_CANCEL a book with DELs
 constexpr uint32_t FL_OK_ADD = 1, FL_OK_CANCEL = 2;
+// FlowHdr::fc_bad: why the cancel prep declined a book (bits; diagnostics read them)
+enum : uint32_t {
+  FC_BAD_SYM = 1, FC_BAD_TABLE = 2, FC_BAD_Q7 = 4, FC_BAD_Q2 = 8, FC_BAD_LEVEL = 16, FC_BAD_UNIT = 32,
+  FC_BAD_WALK = 64, FC_BAD_RING = 128
+};
 
 struct FlowLvl {
   int64_t price;

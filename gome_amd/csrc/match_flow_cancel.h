@@ -48,9 +48,12 @@ namespace gome {
 struct FcHash {
   unsigned long long key;  // gen << 53 | (symbol + 1) << 32 | oid; another generation = empty
   uint32_t add_pos;        // first admitted ADD of the key (segment position), NIL none
-  uint32_t cnt;            // admitted ADDs (low 16 bits), DELs (high 16 bits)
+  uint32_t cnt;            // admitted ADDs
+  uint32_t del_first;      // the DEL that can find the maker: the first after the ADD (or the
+                           // first at all, for a resting maker); later ones find nothing
+  uint32_t pad[3];
 };
-static_assert(sizeof(FcHash) == 16, "FcHash layout");
+static_assert(sizeof(FcHash) == 32, "FcHash layout");
 
 struct FcDel {
   uint32_t kind;     // FC_NONE (no-op), FC_NEW, FC_OLD
@@ -72,8 +75,8 @@ constexpr uint32_t FC_MAXKEY_SYM = (1u << 21) - 1;  // symbol + 1 fits 21 bits o
 __device__ __forceinline__ bool fc_book(const FlowArgs& F, uint32_t h) {
   return F.hdr[h].ok == FL_OK_CANCEL && !F.hdr[h].fc_bad;
 }
-__device__ __forceinline__ void fc_decline(const FlowArgs& F, uint32_t h) {
-  atomicOr(&F.hdr[h].fc_bad, 1u);
+__device__ __forceinline__ void fc_decline(const FlowArgs& F, uint32_t h, uint32_t why) {
+  atomicOr(&F.hdr[h].fc_bad, why);
 }
 __device__ __forceinline__ unsigned long long fc_key(const FlowArgs& F, uint32_t sym, uint32_t oid) {
   return (static_cast<unsigned long long>(F.fc_gen & FC_GEN_MASK) << 53) |
@@ -100,9 +103,26 @@ __device__ __forceinline__ uint32_t fc_hash_find(const FlowArgs& F, unsigned lon
     if (prev == cur) {
       F.fc_hash[s].add_pos = NIL;
       F.fc_hash[s].cnt = 0;
+      F.fc_hash[s].del_first = NIL;
       return static_cast<uint32_t>(s);
     }
     if (prev == key) return static_cast<uint32_t>(s);
+  }
+  return NIL;
+}
+
+// Resting node of (sym, oid) through the cancel index (HGET S:link:<p> S:node:<oid>,
+// engine.go:92-93); NIL if none.
+__device__ __forceinline__ uint32_t fc_old_lookup(const Dev& D, uint32_t sym, uint32_t oid, uint32_t& ixs) {
+  const unsigned long long key = (static_cast<unsigned long long>(sym + 1) << 32) | oid;
+  unsigned long long s = mix64(key) & D.idx_mask;
+  for (unsigned long long probe = 0; probe <= D.idx_mask; ++probe, s = (s + 1) & D.idx_mask) {
+    const unsigned long long kv = __hip_atomic_load(&D.idx[s].key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (kv == key) {
+      ixs = static_cast<uint32_t>(s);
+      return D.idx[s].loc;
+    }
+    if (kv == KEY_EMPTY) return NIL;
   }
   return NIL;
 }
@@ -116,7 +136,7 @@ __global__ __launch_bounds__(256) void k_fc_hash_claim(Dev D, BatchArgs B, FlowA
   uint32_t b0, b1;
   fc_slice(hd, blockIdx.x, gridDim.x, b0, b1);
   const bool claim = hd.sym < FC_MAXKEY_SYM;
-  if (!claim && threadIdx.x == 0) fc_decline(F, h);
+  if (!claim && threadIdx.x == 0) fc_decline(F, h, FC_BAD_SYM);
   for (uint32_t b = b0 + threadIdx.x; b < b1; b += blockDim.x) {
     F.fc_tg[b] = 0;
     F.fc_rank[b] = NIL;
@@ -127,7 +147,7 @@ __global__ __launch_bounds__(256) void k_fc_hash_claim(Dev D, BatchArgs B, FlowA
       F.fc_del[b] = z;
     }
     if (claim && (q.action == GOME_DEL || (q.action == GOME_ADD && q.adm)))
-      if (fc_hash_find(F, fc_key(F, hd.sym, q.oid), true) == NIL) fc_decline(F, h);
+      if (fc_hash_find(F, fc_key(F, hd.sym, q.oid), true) == NIL) fc_decline(F, h, FC_BAD_TABLE);
   }
 }
 
@@ -147,9 +167,33 @@ __global__ __launch_bounds__(256) void k_fc_hash_count(Dev D, BatchArgs B, FlowA
     if (add) {
       atomicMin(&F.fc_hash[s].add_pos, b);
       atomicAdd(&F.fc_hash[s].cnt, 1u);
-    } else {
-      atomicAdd(&F.fc_hash[s].cnt, 1u << 16);
     }
+  }
+}
+
+// ---- prep 2b: the DEL of each key that can find its maker ----------------------------------
+__global__ __launch_bounds__(256) void k_fc_hash_first(Dev D, BatchArgs B, FlowArgs F) {
+  const uint32_t h = F.h0 + blockIdx.y;
+  if (h >= fl_hend(D, F) || !fc_book(F, h)) return;
+  const FlowHdr hd = F.hdr[h];
+  uint32_t b0, b1;
+  fc_slice(hd, blockIdx.x, gridDim.x, b0, b1);
+  for (uint32_t b = b0 + threadIdx.x; b < b1; b += blockDim.x) {
+    const Prep q = prep_at(B, b);
+    if (q.action != GOME_DEL) continue;
+    const uint32_t s = fc_hash_find(F, fc_key(F, hd.sym, q.oid), false);
+    if (s == NIL) continue;
+    // a DEL with another price misses S:link:<price> (Q3) and finds nothing either way
+    const uint32_t ap = F.fc_hash[s].add_pos;
+    bool finds = false;
+    if (ap == NIL) {
+      uint32_t ixs;
+      const uint32_t loc = fc_old_lookup(D, hd.sym, q.oid, ixs);
+      finds = loc != NIL && D.chdr[loc / CH].price == q.price;
+    } else {
+      finds = ap < b && prep_at(B, ap).price == q.price;
+    }
+    if (finds) atomicMin(&F.fc_hash[s].del_first, b);
   }
 }
 
@@ -161,22 +205,6 @@ __device__ __forceinline__ uint32_t fc_level_of(const FlowLvl* LV, uint32_t nl, 
     if (LV[mid].price < p) lo = mid + 1; else hi = mid;
   }
   return (lo <= nl && LV[lo].price == p) ? lo : 0u;
-}
-
-// Resting node of (sym, oid) through the cancel index (HGET S:link:<p> S:node:<oid>,
-// engine.go:92-93); NIL if none.
-__device__ __forceinline__ uint32_t fc_old_lookup(const Dev& D, uint32_t sym, uint32_t oid, uint32_t& ixs) {
-  const unsigned long long key = (static_cast<unsigned long long>(sym + 1) << 32) | oid;
-  unsigned long long s = mix64(key) & D.idx_mask;
-  for (unsigned long long probe = 0; probe <= D.idx_mask; ++probe, s = (s + 1) & D.idx_mask) {
-    const unsigned long long kv = __hip_atomic_load(&D.idx[s].key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (kv == key) {
-      ixs = static_cast<uint32_t>(s);
-      return D.idx[s].loc;
-    }
-    if (kv == KEY_EMPTY) return NIL;
-  }
-  return NIL;
 }
 
 // ---- prep 3: each DEL's target -------------------------------------------------------------
@@ -193,18 +221,22 @@ __global__ __launch_bounds__(256) void k_fc_resolve(Dev D, BatchArgs B, FlowArgs
     const uint32_t s = fc_hash_find(F, fc_key(F, hd.sym, q.oid), false);
     if (s == NIL) continue;
     const FcHash e = F.fc_hash[s];
-    const uint32_t nadd = e.cnt & 0xFFFFu, ndel = e.cnt >> 16;
-    if (nadd > 1 || ndel > 1) { fc_decline(F, h); continue; }  // reused oid (Q7) / repeated cancel
+    const uint32_t nadd = e.cnt;
+    if (nadd > 1) { fc_decline(F, h, FC_BAD_Q7); continue; }  // a reused oid (Q7)
     const bool sale = q.side == GOME_SALE;
     FcDel d{};
     d.ct = NIL;
     uint32_t ixs = 0;
     const uint32_t loc = fc_old_lookup(D, hd.sym, q.oid, ixs);
-    if (nadd == 1 && e.add_pos < b) {
-      if (loc != NIL) { fc_decline(F, h); continue; }  // the oid rests already: duplicate (Q7)
+    if (b != e.del_first) {  // the maker is gone by then (or its ADD comes later)
+      if (nadd == 1 && loc != NIL) fc_decline(F, h, FC_BAD_Q7);  // the oid rests already: duplicate (Q7)
+      continue;
+    }
+    if (nadd == 1) {
+      if (loc != NIL) { fc_decline(F, h, FC_BAD_Q7); continue; }  // the oid rests already: duplicate (Q7)
       const Prep a = prep_at(B, e.add_pos);
       if (a.price != q.price) continue;                 // S:link:<request price> misses (Q3)
-      if ((a.side == GOME_SALE) != sale) { fc_decline(F, h); continue; }  // wrong side (Q2)
+      if ((a.side == GOME_SALE) != sale) { fc_decline(F, h, FC_BAD_Q2); continue; }  // wrong side (Q2)
       d.kind = FC_NEW;
       d.tgt = e.add_pos;
       d.li = static_cast<uint32_t>(F.ord8[hd.obase + (e.add_pos - hd.beg)] >> 32) & 127u;
@@ -212,17 +244,13 @@ __global__ __launch_bounds__(256) void k_fc_resolve(Dev D, BatchArgs B, FlowArgs
       F.fc_tg[e.add_pos] = b + 1;
       continue;
     }
-    if (nadd == 1) {  // the ADD comes after the DEL: the DEL finds nothing (or a duplicate)
-      if (loc != NIL) fc_decline(F, h);
-      continue;
-    }
     if (loc == NIL) continue;                                             // not resting
     if (D.chdr[loc / CH].price != q.price) continue;                     // Q3
     const Node nd = D.nodes[loc];
     if (nd.rem < 0) continue;
-    if ((nd.tx == GOME_SALE) != sale) { fc_decline(F, h); continue; }   // Q2
+    if ((nd.tx == GOME_SALE) != sale) { fc_decline(F, h, FC_BAD_Q2); continue; }   // Q2
     const uint32_t li = fc_level_of(LV, hd.nl, q.price);
-    if (li == 0) { fc_decline(F, h); continue; }
+    if (li == 0) { fc_decline(F, h, FC_BAD_LEVEL); continue; }
     d.kind = FC_OLD;
     d.tgt = loc;
     d.ixs = ixs;
@@ -258,7 +286,7 @@ __device__ __forceinline__ void fc_oldwalk_level(const Dev& D, const FlowArgs& F
     if (mk) {
       FcDel* d = &F.fc_del[static_cast<uint32_t>(nd.pad) - 1u];
       const uint64_t end = static_cast<uint64_t>(em + nd.rem);
-      if (end % g || static_cast<uint64_t>(nd.rem) % g) fc_decline(F, h);  // not in plan units
+      if (end % g || static_cast<uint64_t>(nd.rem) % g) fc_decline(F, h, FC_BAD_UNIT);  // not in plan units
       d->rank = seen + __popcll(mm & lt_mask());
       d->oend = static_cast<uint32_t>(end / g);
       d->ov = static_cast<uint32_t>(static_cast<uint64_t>(nd.rem) / g);
@@ -268,7 +296,7 @@ __device__ __forceinline__ void fc_oldwalk_level(const Dev& D, const FlowArgs& F
     c = (c == tail) ? NIL : uni(D.chdr[c].next);
     s0 = 0;
   }
-  if (seen != cold && lane == 0) fc_decline(F, h);
+  if (seen != cold && lane == 0) fc_decline(F, h, FC_BAD_WALK);
 }
 
 __global__ __launch_bounds__(64) void k_fc_oldwalk_wide(Dev D, FlowArgs F) {
@@ -299,6 +327,7 @@ __global__ __launch_bounds__(FC_PASS_T) void k_fc_pass(Dev D, BatchArgs B, FlowA
     cmax[tid] = (tid >= 1 && tid <= nl) ? max(LV[tid].c_old, 1u) : 1u;
   }
   if (tid == 0) bad_s = 0;
+  for (uint32_t x = tid; x < FC_PASS_W * FL_CAP; x += FC_PASS_T) wc[x / FL_CAP][x % FL_CAP] = 0;
   __syncthreads();
   const unsigned long long ltm = lt_mask();
   // in segment order, tile by tile: a targeted ADD's rank = old targets of its level + targeted
@@ -351,7 +380,7 @@ __global__ __launch_bounds__(FC_PASS_T) void k_fc_pass(Dev D, BatchArgs B, FlowA
       F.fc_del[b].rank = rk;
       F.fc_del[b].nb = nb;
       atomicMax(&cmax[k], nb + 1u);
-      if (nb >= 0xFFFFu) bad_s = 1;
+      if (nb >= 0xFFFFu) atomicOr(&bad_s, FC_BAD_RING);
     }
     for (uint32_t x = tid; x < FC_PASS_W * FL_CAP; x += FC_PASS_T) wc[x / FL_CAP][x % FL_CAP] = 0;
     __syncthreads();
@@ -368,7 +397,7 @@ __global__ __launch_bounds__(FC_PASS_T) void k_fc_pass(Dev D, BatchArgs B, FlowA
       top = max(top, c);
     }
     if (off + 1 > cap) {
-      bad_s = 1;  // (+ the dummy entry of untargeted ADDs and no-op records)
+      bad_s |= FC_BAD_RING;  // (+ the dummy entry of untargeted ADDs and no-op records)
     } else {
       off = 0;
       for (uint32_t c = top; c; c >>= 1)
@@ -379,10 +408,14 @@ __global__ __launch_bounds__(FC_PASS_T) void k_fc_pass(Dev D, BatchArgs B, FlowA
           }
     }
     nslot_s = off + 1;
+    uint32_t mw = 0;
+    for (uint32_t q = 1; q <= nl; ++q) mw = max(mw, cmax[q]);
+    F.hdr[h].ncancel = mw;
+    F.hdr[h].nslot = nslot_s;  // (also when declined: diagnostics)
   }
   __syncthreads();
   if (bad_s) {
-    if (tid == 0) fc_decline(F, h);
+    if (tid == 0) fc_decline(F, h, bad_s);
     return;
   }
   const uint32_t nslot = nslot_s, dummy = nslot - 1;

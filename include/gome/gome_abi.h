@@ -216,6 +216,16 @@ gome_status gome_device_events(gome_engine* e, const gome_event** dev_ptr,
  * gome_device_events): the next submit need not move them to the host drain queue. */
 gome_status gome_release_device_events(gome_engine* e);
 gome_status gome_get_stats(const gome_engine* e, gome_stats* out);
+/* Diagnostics (tests, tuning): the last batch's hot-book routing, GOME_DEBUG_FLOW_WORDS words
+ * per candidate book, longest segment first: {flow kind (0 legacy / cold, 1 ADD-only flow,
+ * 2 flow with cancels), cancel-prep decline bits, symbol, orders, DELs, levels, 32-bit plan,
+ * ring entries needed, longest cancel window + 1, 0}.  *n_out = candidates written (<= cap). */
+#define GOME_DEBUG_FLOW_WORDS 10
+gome_status gome_debug_flow_books(gome_engine* e, uint32_t* out, size_t cap, size_t* n_out);
+/* Diagnostics: raw bytes [offset, offset + bytes) of one of the flow path's device scratch
+ * arrays after the last batch (0 headers, 1 level slots, 2 DEL records, 3 targeted-ADD ranks,
+ * 4 DEL-of-ADD links, 5 packed records). */
+gome_status gome_debug_peek(gome_engine* e, uint32_t which, uint64_t offset, uint64_t bytes, void* out);
 
 /* ---- pipelined host path (ABI >= 4) ---------------------------------------- */
 /* The batching consumer's loop: submit batch k+1, then collect batch k.

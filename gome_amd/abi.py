@@ -14,7 +14,7 @@ import numpy as np
 from .workload import EVENT_DTYPE, LEVEL_DTYPE, NODE_DTYPE, ORDER_DTYPE
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libgome.so")
+LIB_PATH = os.environ.get("GOME_LIB") or os.path.join(_HERE, "libgome.so")  # GOME_LIB: variant builds (tools/)
 HEADER = os.path.join(os.path.dirname(_HERE), "include", "gome", "gome_abi.h")
 HEADERS = [HEADER, os.path.join(os.path.dirname(_HERE), "include", "gome", "gome_loadgen.h")]
 

@@ -51,8 +51,8 @@ D = ("s94", "s95")               # T - depth of a crossed level; X (cached-depth
 X = D
 HC = "s97"                       # half-groups left + 1
 ADDR = "s[98:99]"                # SMEM address of the next half-group
-SAVE = "s100"                    # M0 (staging count) saved around lane writes
-CLOBBERS = [f"s{i}" for i in range(44, 101)] + ["v32", "v33", "v34", "v35"]
+SAVE = "s97"                     # M0 saved around the final lane writes (HC is dead by then)
+CLOBBERS = [f"s{i}" for i in range(44, 100)] + ["v32", "v33", "v34", "v35"]
 # W32 depth layout: one 64-bit lane pair per side, lane j = levels 2j (low word) and 2j+1 (high
 # word): asks in v[32:33], bids in v[34:35] (fixed registers: the pair must be consecutive).
 PAIR = {"A": (32, 33), "B": (34, 35)}
@@ -592,16 +592,21 @@ class Gen:
 # Record (8 B): lo = ADD volume in units of g | DEL: window length n_b [0,16) | log2 C_k [16,21);
 # hi = level [0,7) | ring slot p [7,21) | DEL: maker SALE bit 29, DEL bit 30 | SALE (ADD) or 1
 # (DEL) bit 31.  Per level the plan also keeps R_k, the volume that ever arrived (lane pair
-# v[36:37], W32 layout), and every ADD owns a 16-B LDS ring entry {end, v, xv} (non-targeted
-# ADDs a dummy one): cleared when the ADD is consumed, {E + T, T} when it rests.  A DEL of
-# target m at level k takes r = clamp(end_m - (R_k - depth_k) + Xb, 0, v_m) where Xb sums xv over
+# v[36:37], W32 layout), and every ADD owns a 16-B LDS ring entry {R pair, v, xv} (non-targeted
+# ADDs a dummy one): v = xv = 0 when the ADD crosses (it may never rest), {R pair before, T, 0}
+# when it rests (E = the level's word of the pair).  A DEL of target m at level k takes
+# r = clamp(E_m + v_m - (R_k - depth_k) + Xb, 0, v_m) where Xb sums xv over
 # the ring window of the n_b targets that arrived behind m (ranks rank_m + 1 ..): each DEL sets
 # its target's xv = v_m.  Touch keys come from an order counter (JJS, as the 64-bit plan):
 # rest = JJS | k | 1 << 7, consume = JJS | k, cancel = JJS | k | 1 << 31 (amount r).
 CREG = {"R": (36, 37)}
-VA, VE, VV, VZ, VW, VX, VL = 38, 40, 41, 42, 46, 47, 48  # LDS address, end / v (an even pair),
-                                                          # zeros v[42:44], window address / data,
-                                                          # lane id (gfx950 tuples are even-aligned)
+# v38 = T of a rest and v39 = 0 follow the R pair: a rest writes its entry {R pair, T, 0} in one
+# ds_write_b128 from lane LI >> 1 (the DEL picks E = the level's word of the pair)
+VV, VZ0 = 38, 39
+VE, VM = 40, 42              # a DEL's entry read {R lo, R hi, v} -> v[40:42]
+VA = 43                      # LDS address
+VG0, VG1 = 44, 45            # G_k words
+VW, VX, VL = 46, 47, 48      # window address / data, lane id
 X0, X1, X2, X3 = "s79", "s81", "s83", "s96"              # free in the 32-bit layout
 CLOBBERS_C = [f"v{i}" for i in range(36, 50)]
 
@@ -618,16 +623,19 @@ class GenC(Gen):
         e(f"s_and_b32 {LI}, {hi}, 127")
         e(f"s_bitcmp1_b32 {hi}, 31")
 
-    def ring_clear(self, j: int):
-        """The ADD's ring entry := {0, 0, 0} (a target that never rests holds v = 0) and its
-        address stays in lane 0 of v38 for the rest."""
+    def entry_addr(self, hi: str):
+        """X3 = byte address of the record's ring entry (slot [7, 21) of hi, 16-B entries)."""
+        self.e(f"s_lshr_b32 {X3}, {hi}, 3")
+        self.e(f"s_and_b32 {X3}, {X3}, 0x3fff0")
+
+    def cross_entry(self, T):
+        """An ADD that crosses may be filled completely and never rest: its entry's v and xv
+        := 0 now (an ADD that rests writes the whole entry)."""
         e = self.e
-        hi = f"s{BUF[j][1]}"
-        e(f"s_lshr_b32 {T0}, {hi}, 3")
-        e(f"s_and_b32 {T0}, {T0}, 0x3fff0")
+        self.entry_addr(T[1])
         e("s_mov_b64 exec, 1")
-        e(f"v_mov_b32 v{VA}, {T0}")
-        e(f"ds_write_b96 v{VA}, v[{VZ}:{VZ + 2}]")
+        e(f"v_mov_b32 v{VA}, {X3}")
+        e(f"ds_write2_b32 v{VA}, v{VZ0}, v{VZ0} offset0:2 offset1:3")
 
     def dispatch(self, j: int, fall: bool, copy: bool = COPY_REST):
         e = self.e
@@ -638,7 +646,6 @@ class GenC(Gen):
         self.decode(j)
         e(f"s_cbranch_scc1 {self.lab(f'S{j}')}")
         if not fall:                               # slot j's BUY entry, inline
-            self.ring_clear(j)
             e(f"s_cmp_le_u32 {BA}, {LI}")
             e(f"s_cbranch_scc1 {self.lab(f'BXE{j}')}")
             if copy:
@@ -647,11 +654,9 @@ class GenC(Gen):
             else:
                 e(f"s_branch {self.lab(f'BR{j}')}")
 
-    def cross_entry(self, T):
-        pass  # JJS is the order counter
-
     def rest(self, side: str, T):
-        """The 32-bit rest, then R_k += T, the ring entry := {E + T, T} (E = R_k before)."""
+        """The 32-bit rest, then R_k += T and the ring entry := {E + T, T, 0} (E = R_k before),
+        both from lane LI >> 1 of the R pair: no lane read on the path."""
         e = self.e
         buy = side == "B"
         top, topd = (BB, BBD) if buy else (BA, BAD)
@@ -666,23 +671,17 @@ class GenC(Gen):
         e(f"s_{'max' if buy else 'min'}_u32 {top}, {top}, {LI}")
         self.add(topd, topd, X)
         self.add_lane("B" if buy else "A")
-        # arrivals R_k (lane pair k >> 1, word k & 1) and the maker's arrival coordinate
         ev, od = CREG["R"]
+        self.entry_addr(T[1])
         e(f"s_lshr_b32 {T0}, {LI}, 1")
-        e(f"v_readlane_b32 {X0}, v{ev}, {T0}")
-        e(f"v_readlane_b32 {X1}, v{od}, {T0}")
         e(f"s_bfm_b64 exec, 1, {T0}")
-        e(f"s_lshl_b32 {T0}, {LI}, 5")
-        e(f"s_mov_b32 s90, {T[0]}")                 # (s91 = 0)
-        e(f"s_lshl_b64 s[92:93], s[90:91], {T0}")
-        e(f"v_lshl_add_u64 v[{ev}:{od}], s[92:93], 0, v[{ev}:{od}]")
-        e(f"s_bitcmp1_b32 {LI}, 0")
-        e(f"s_cselect_b32 {X0}, {X1}, {X0}")
-        e(f"s_add_u32 {X0}, {X0}, {T[0]}")
-        e("s_mov_b64 exec, 1")
-        e(f"v_mov_b32 v{VE}, {X0}")
         e(f"v_mov_b32 v{VV}, {T[0]}")
-        e(f"ds_write_b64 v{VA}, v[{VE}:{VV}]")
+        e(f"v_mov_b32 v{VA}, {X3}")
+        e(f"ds_write_b128 v{VA}, v[{ev}:{VZ0}]")          # {R pair (E = the level's word), T, 0}
+        e(f"s_lshl_b32 {T0}, {LI}, 5")
+        e(f"s_mov_b32 s90, {T[0]}")                      # (s91 = 0)
+        e(f"s_lshl_b64 s[92:93], s[90:91], {T0}")
+        e(f"v_lshl_add_u64 v[{ev}:{od}], s[92:93], 0, v[{ev}:{od}]")   # R_k += T
         e(f"s_or_b32 {K}, {JJS}, {LI}")
         e(f"s_bitset1_b32 {K}, 7")
         self.log(K, T, False)
@@ -709,10 +708,12 @@ class GenC(Gen):
         e(f"v_and_b32 v{VW}, {X2}, v{VW}")
         e(f"v_or_b32 v{VW}, {X1}, v{VW}")
         e(f"v_lshlrev_b32 v{VW}, 4, v{VW}")
-        e(f"ds_read_b32 v{VX}, v{VW} offset:8")
+        e(f"ds_read_b32 v{VX}, v{VW} offset:12")
 
     def del_path(self, i: int):
-        """DeleteOrder (engine.go:87-116) on the aggregates of level LI."""
+        """DeleteOrder (engine.go:87-116) on the aggregates of level LI: r = clamp(end_m + Xb -
+        G_k, 0, v_m) with G_k = R_k - depth_k read from lane LI >> 1 (one lane read) while the
+        entry's LDS read is in flight, the clamp in lane 0; the window (n_b > 0) out of line."""
         e = self.e
         lo, hi = f"s{BUF[i][0]}", f"s{BUF[i][1]}"
         lab = self.lab
@@ -720,55 +721,45 @@ class GenC(Gen):
         aev, aod = PAIR["A"]
         bev, bod = PAIR["B"]
         e(f"{lab(f'D{i}')}:")
-        e(f"s_lshr_b32 {T0}, {hi}, 3")
-        e(f"s_and_b32 {T0}, {T0}, 0x3fff0")                 # target entry (byte address)
-        e("s_mov_b64 exec, 1")
-        e(f"v_mov_b32 v{VA}, {T0}")
-        e(f"ds_read_b64 v[{VE}:{VV}], v{VA}")                 # {end_m, v_m}
-        e(f"s_lshr_b32 {X3}, {T0}, 4")                        # p
-        e(f"s_lshr_b32 {X1}, {lo}, 16")
-        e(f"s_bfm_b32 {X2}, {X1}, 0")                         # mask = C_k - 1
-        e(f"s_andn2_b32 {X1}, {X3}, {X2}")                    # pbase
-        e(f"s_add_u32 {X3}, {X3}, 1")                         # first window rank (mod C_k)
-        e(f"s_and_b32 {X0}, {lo}, 0xffff")                    # n_b
+        self.entry_addr(hi)
         e(f"s_lshr_b32 {T0}, {LI}, 1")
-        e(f"v_readlane_b32 s92, v{ev}, {T0}")
-        e(f"v_readlane_b32 s93, v{od}, {T0}")
-        e(f"v_readlane_b32 s84, v{aev}, {T0}")
-        e(f"v_readlane_b32 s85, v{aod}, {T0}")
-        e(f"v_readlane_b32 s94, v{bev}, {T0}")
-        e(f"v_readlane_b32 s95, v{bod}, {T0}")
-        slow, back = lab(f"DW{i}"), lab(f"DWB{i}")
-        e(f"s_cmp_gt_u32 {X0}, 63")
-        e(f"s_cbranch_scc1 {slow}")
-        self.window_read(X0, X3)
-        e("s_waitcnt lgkmcnt(0)")
-        e("s_mov_b64 exec, -1")
-        self.reduce_window("s90")
+        e(f"s_bfm_b64 exec, 1, {T0}")                         # lane LI >> 1 from here on
+        e(f"v_mov_b32 v{VA}, {X3}")
+        e(f"ds_read_b96 v[{VE}:{VM}], v{VA}")                 # {R pair at m's arrival, v_m}
+        e(f"s_and_b32 {X0}, {lo}, 0xffff")                    # n_b
+        e("s_mov_b32 s90, 0")                                 # Xb
+        e(f"s_cmp_lg_u32 {X0}, 0")
+        win, back = lab(f"DW{i}"), lab(f"DWB{i}")
+        e(f"s_cbranch_scc1 {win}")
         e(f"{back}:")
-        # (the window sum is in s90; {end_m, v_m} in lane 0 of v[39:40])
-        e(f"v_readlane_b32 {X1}, v{VE}, 0")
-        e(f"v_readlane_b32 {X2}, v{VV}, 0")
+        # G_k = R_k - depth_k: the level's words of the R / ask / bid pairs (a cached top's lane
+        # is 0, its depth is in SGPRs)
+        e(f"v_sub_u32 v{VG0}, v{ev}, v{aev}")
+        e(f"v_sub_u32 v{VG0}, v{VG0}, v{bev}")
+        e(f"v_sub_u32 v{VG1}, v{od}, v{aod}")
+        e(f"v_sub_u32 v{VG1}, v{VG1}, v{bod}")
         e(f"s_bitcmp1_b32 {LI}, 0")
-        e("s_cselect_b32 s92, s93, s92")                       # R_k
-        e("s_cselect_b32 s84, s85, s84")                       # ask lane word
-        e("s_cselect_b32 s94, s95, s94")                       # bid lane word
+        e("s_cselect_b64 vcc, -1, 0")
+        e(f"v_cndmask_b32 v{VG0}, v{VG0}, v{VG1}, vcc")
         e(f"s_cmp_eq_u32 {LI}, {BA}")
-        e(f"s_cselect_b32 {X3}, {BAD[0]}, 0")
-        e(f"s_add_u32 s84, s84, {X3}")
+        e(f"s_cselect_b32 {X1}, {BAD[0]}, 0")
         e(f"s_cmp_eq_u32 {LI}, {BB}")
-        e(f"s_cselect_b32 {X3}, {BBD[0]}, 0")
-        e(f"s_add_u32 s84, s84, {X3}")
-        e("s_add_u32 s84, s84, s94")                           # depth_k (one side is 0)
-        e("s_sub_u32 s92, s92, s84")                           # G_k = R_k - depth_k
-        e(f"s_add_u32 {X1}, {X1}, s90")                        # end_m + Xb
-        e(f"s_sub_u32 {X1}, {X1}, s92")                        # SCC: negative
-        e(f"s_cselect_b32 {X1}, 0, {X1}")
-        e(f"s_min_u32 {X1}, {X1}, {X2}")                       # r
-        e("s_mov_b64 exec, 1")
-        e(f"ds_write_b32 v{VA}, v{VV} offset:8")               # xv_m = v_m (DELed)
+        e(f"s_cselect_b32 {X2}, {BBD[0]}, 0")
+        e(f"s_add_u32 {X1}, {X1}, {X2}")
+        e(f"v_subrev_u32 v{VG0}, {X1}, v{VG0}")               # G_k
+        e("s_waitcnt lgkmcnt(0)")
+        # a = E_m + v_m + Xb (< 2^32: the window's makers arrived after m); r = a - G_k clamped
+        # to [0, v_m]; xv_m := v_m
+        e(f"v_cndmask_b32 v{VE}, v{VE}, v{VE + 1}, vcc")      # E_m
+        e(f"v_add_u32 v{VE}, v{VE}, v{VM}")
+        e(f"v_add_u32 v{VE}, s90, v{VE}")
+        e(f"v_sub_co_u32 v{VE}, vcc, v{VE}, v{VG0}")
+        e(f"v_cndmask_b32 v{VE}, v{VE}, v{VZ0}, vcc")
+        e(f"v_min_u32 v{VE}, v{VE}, v{VM}")
+        e(f"ds_write_b32 v{VA}, v{VM} offset:12")
+        e(f"v_readlane_b32 {X1}, v{VE}, {T0}")                # r
         e(f"s_cmp_eq_u32 {X1}, 0")
-        e(f"s_cbranch_scc1 {lab(f'DZ{i}')}")                   # not found: no event (:96-98)
+        e(f"s_cbranch_scc1 {lab(f'DZ{i}')}")                  # not found: no event (:96-98)
         e(f"s_or_b32 {K}, {JJS}, {LI}")
         e(f"s_bitset1_b32 {K}, 31")
         e(f"s_mov_b32 s90, {X1}")
@@ -800,11 +791,18 @@ class GenC(Gen):
             self.dispatch((i + 1) % NS, False)
         e(f"{lab(f'DZ{i}')}:")
         self.dispatch((i + 1) % NS, False)
-        # windows longer than 63: 64 lanes at a time (out of line)
-        blk = [f"{slow}:", "s_mov_b32 s90, 0", f"s_mov_b32 {K}, 0"]
+        # the window (out of line): Xb = sum of xv over ranks p + 1 .. p + n_b (mod C_k) of the
+        # level's ring, 63 lanes at a time
+        blk = [f"{win}:"]
         self.slow.append(blk)
         sv = self.out
         self.out = blk
+        e(f"s_lshr_b32 {X3}, {X3}, 4")                        # p
+        e(f"s_lshr_b32 {X1}, {lo}, 16")
+        e(f"s_bfm_b32 {X2}, {X1}, 0")                         # mask = C_k - 1
+        e(f"s_andn2_b32 {X1}, {X3}, {X2}")                    # pbase
+        e(f"s_add_u32 {X3}, {X3}, 1")                         # first window rank (mod C_k)
+        e(f"s_mov_b32 {K}, 0")
         loop = lab(f"DWL{i}")
         e(f"{loop}:")
         e(f"s_sub_u32 {L}, {X0}, {K}")
@@ -818,7 +816,8 @@ class GenC(Gen):
         e(f"s_add_u32 {K}, {K}, 63")
         e(f"s_cmp_lt_u32 {K}, {X0}")
         e(f"s_cbranch_scc1 {loop}")
-        e("s_waitcnt lgkmcnt(0)")
+        e(f"s_lshr_b32 {T0}, {LI}, 1")
+        e(f"s_bfm_b64 exec, 1, {T0}")
         e(f"s_branch {back}")
         self.out = sv
 
@@ -829,13 +828,13 @@ class GenC(Gen):
         j = (i + 1) % NS
         lab = self.lab
         e(f"{lab(f'B{i}')}:")
-        self.ring_clear(i)
         e(f"s_cmp_le_u32 {BA}, {LI}")
         e(f"s_cbranch_scc1 {lab(f'BXE{i}')}")
         e(f"{lab(f'BR{i}')}:")
         self.rest("B", T)
         self.dispatch(j, False)
         e(f"{lab(f'BXE{i}')}:")
+        self.cross_entry(T)
         self.sub(D, T, BAD)
         e(f"s_cbranch_scc0 {lab(f'BF{i}')}")
         self.partial("B", T)
@@ -843,6 +842,7 @@ class GenC(Gen):
         e(f"{lab(f'BF{i}')}:")
         self.full("B", T, i)
         e(f"{lab(f'SXE{i}')}:")
+        self.cross_entry(T)
         self.sub(D, T, BBD)
         e(f"s_cbranch_scc0 {lab(f'SF{i}')}")
         self.partial("S", T)
@@ -855,7 +855,6 @@ class GenC(Gen):
         e(f"{lab(f'S{i}')}:")
         e(f"s_bitcmp1_b32 {hi}, 30")
         e(f"s_cbranch_scc1 {lab(f'D{i}')}")
-        self.ring_clear(i)
         e(f"s_cmp_ge_u32 {BB}, {LI}")
         e(f"s_cbranch_scc1 {lab(f'SXE{i}')}")
         e(f"{lab(f'SR{i}')}:")
@@ -867,8 +866,7 @@ class GenC(Gen):
         e("s_mov_b64 exec, -1")
         e(f"v_mbcnt_lo_u32_b32 v{VL}, -1, 0")
         e(f"v_mbcnt_hi_u32_b32 v{VL}, -1, v{VL}")
-        for r in range(VZ, VZ + 3):
-            e(f"v_mov_b32 v{r}, 0")
+        e(f"v_mov_b32 v{VZ0}, 0")
         ev, od = CREG["R"]
         e(f"v_mov_b32 v{ev}, %[rl0]")
         e(f"v_mov_b32 v{od}, %[rl1]")
@@ -890,8 +888,10 @@ def aligned(lines: list[str]) -> list[str]:
 
 
 def main():
+    import sys
     here = os.path.dirname(os.path.abspath(__file__))
-    with open(os.path.join(here, "flow_plan_asm.inc"), "w") as f:
+    out = sys.argv[1] if len(sys.argv) > 1 else os.path.join(here, "flow_plan_asm.inc")
+    with open(out, "w") as f:
         f.write("// Generated by gen_plan_asm.py — do not edit.\n")
         for w, g in ((64, Gen(64)), (32, Gen(32)), ("32C", GenC())):
             f.write(f"#define FL_PLAN_ASM{w} \\\n")

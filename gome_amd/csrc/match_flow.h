@@ -157,7 +157,7 @@ struct FlowLvl {
 };
 static_assert(sizeof(FlowLvl) % 16 == 0, "FlowLvl alignment");
 
-// The cancel plan's LDS ring (match_flow_cancel.h): 16-B entries {end, v, xv, pad} per targeted
+// The cancel plan's LDS ring (match_flow_cancel.h): 16-B entries {R pair, v, xv} per targeted
 // maker (+ one dummy entry), an image per book built by the cancel prep.
 constexpr uint32_t FC_HEAD_SLOTS = 9216;  // head books own their CU (144 KiB of LDS)
 constexpr uint32_t FC_TAIL_SLOTS = 1024;  // tail books (16 KiB)

@@ -446,7 +446,7 @@ __global__ __launch_bounds__(FC_PASS_T) void k_fc_pass(Dev D, BatchArgs B, FlowA
           const uint32_t lgc = 31u - __clz(cring[kk]);
           rec = (static_cast<unsigned long long>(kk | (slot << 7) | (sale ? 1u << 29 : 0u) | (3u << 30)) << 32) |
                 (d.nb | (lgc << 16));
-          if (d.kind == FC_OLD) img[slot] = make_uint4(d.oend, d.ov, 0u, 0u);
+          if (d.kind == FC_OLD) img[slot] = make_uint4(d.oend - d.ov, d.oend - d.ov, d.ov, 0u);  // {E, E, v, xv}
         }
       }
     }

@@ -90,13 +90,15 @@ __global__ __launch_bounds__(256) void k_lvl_recycle(Dev D) {
 // Rebuild the (S, oid) cancel index from the live FIFO nodes (the table was zeroed): bounds
 // the probe length of lookups that miss (a cancel of a filled or unknown oid scans to the
 // first EMPTY slot, and erases only leave tombstones).  One wave per book, a lane per slot.
+// One wave per (symbol, level): the hottest book's FIFOs hold millions of nodes, so its levels
+// are walked side by side (blockIdx.y strides over a book's levels).
 __global__ __launch_bounds__(64) void k_idx_rebuild(Dev D) {
   const uint32_t lane = lane_id();
   const unsigned long long mask = D.idx_mask;
   for (uint32_t sym = blockIdx.x; sym < D.max_symbols; sym += gridDim.x) {
     const Book bk = D.books[sym];
     const Level* L = D.lvl + bk.lvl_base;
-    for (uint32_t k = 0; k < bk.n_lvl; ++k) {
+    for (uint32_t k = blockIdx.y; k < bk.n_lvl; k += gridDim.y) {
       const Level x = L[k];
       uint32_t c = x.head, s0 = x.hslot;
       for (uint32_t guard = 0; c != NIL && guard <= D.ch_cap; ++guard) {
@@ -197,6 +199,7 @@ struct gome_engine {
   unsigned long long resting = 0, levels = 0;
   unsigned long long idx_tomb = 0, n_rebuilds = 0;  // tombstones (upper bound) since the last rebuild
   uint32_t fc_gen = 0;            // batch generation of the cancel books' (symbol, oid) table
+  uint32_t fc_ring_lds = 0;       // dynamic LDS of the large-ring plans
   unsigned long long fc_hcap = 0;  // its entries
   bool poisoned = false;
   std::string err;
@@ -294,8 +297,16 @@ gome_status gome_engine::init(const gome_config& c) {
   HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_match_hot),
                              hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(HOT_LDS_BYTES)));
   // the head plans hold a cancel book's LDS ring (match_flow_cancel.h)
-  for (const void* k : {reinterpret_cast<const void*>(k_flow_plan_head), reinterpret_cast<const void*>(k_flow_plan_near)})
-    HIPCHK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(FC_HEAD_LDS)));
+  {
+    int lds = 0;
+    HIPCHK(hipDeviceGetAttribute(&lds, hipDeviceAttributeMaxSharedMemoryPerBlock, cfg.device));
+    F.fc_ring_cap = std::min<uint32_t>(FC_MAX_SLOTS, static_cast<uint32_t>(std::max(lds, 0)) / 16);
+    if (F.fc_ring_cap < FC_TAIL_SLOTS) return fail(GOME_E_DEVICE, "device LDS per workgroup below 16 KiB");
+    fc_ring_lds = F.fc_ring_cap * 16;
+    for (const void* k : {reinterpret_cast<const void*>(k_flow_plan_head), reinterpret_cast<const void*>(k_flow_plan_near),
+                          reinterpret_cast<const void*>(k_flow_plan_tail_cb)})
+      HIPCHK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(fc_ring_lds)));
+  }
 
   max_batch = cfg.max_batch;
   uint32_t ms = cfg.max_symbols;
@@ -385,7 +396,10 @@ gome_status gome_engine::init(const gome_config& c) {
   // table (generation-tagged: cleared once per 2048 batches)
   fc_hcap = next_pow2(std::max<unsigned long long>(2ull * nb, 1024));
   F.fc_hmask = fc_hcap - 1;
-  if (!alloc(&F.fc_img, fc_img_off(MAX_FLOW), "flow cancel ring images") || !alloc(&F.fc_del, nb, "flow cancel records") ||
+  // ring entries of a batch <= 2 * (targets + levels) per book: 2 * max_batch + 256 per candidate
+  F.fc_img_cap = static_cast<uint32_t>(std::min<uint64_t>(2ull * nb + 256ull * MAX_FLOW + FL_HEAD * FC_MAX_SLOTS, 0xF0000000ull));
+  if (!alloc(&F.fc_img, F.fc_img_cap, "flow cancel ring images") || !alloc(&F.fc_img_bump, 1, "flow cancel image bump") ||
+      !alloc(&F.fc_del, nb, "flow cancel records") ||
       !alloc(&F.fc_tg, nb, "flow cancel targets") || !alloc(&F.fc_rank, nb, "flow cancel ranks") ||
       !alloc(&F.fc_hash, fc_hcap, "flow cancel table"))
     return GOME_E_CAPACITY;
@@ -438,7 +452,7 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   // slot, so rebuild the table from the live nodes before it fills up (70%)
   if ((rest_ub + idx_tomb + 2 * inflight_n) * 10 > idx_cap * 7) {
     HIPCHK(hipMemsetAsync(D.idx, 0, sizeof(IdxEnt) * idx_cap, s));
-    k_idx_rebuild<<<2048, 64, 0, s>>>(D);
+    k_idx_rebuild<<<dim3(2048, 128), 64, 0, s>>>(D);
     idx_tomb = 0;
     ++n_rebuilds;
   }
@@ -525,6 +539,7 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   const uint32_t nh_tail = nhot_max > FL_HEAD ? nhot_max - FL_HEAD : 0;
   // the head's prep gathers through the sort permutation (prep_at): it starts right after
   // segmentation, beside k_prep
+  HIPCHK(hipMemsetAsync(F.fc_img_bump, 0, 4, s));  // (both ranges' cancel preps follow)
   HIPCHK(hipEventRecord(seg_done, s));
   HIPCHK(hipStreamWaitEvent(flow_stream, seg_done, 0));
   HIPCHK(hipMemsetAsync(F.pscr, 0, sizeof(FlPrepScr) * FL_HEAD, flow_stream));
@@ -546,7 +561,7 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   cancel_prep(FH, nh_head, FL_PG, true, flow_stream);
   HIPCHK(hipEventRecord(prep_h, flow_stream));
   HIPCHK(hipEventRecord(S.evf0, flow_stream));
-  k_flow_plan_head<<<1, 256, FC_HEAD_LDS, flow_stream>>>(D, FH0);
+  k_flow_plan_head<<<1, 256, fc_ring_lds, flow_stream>>>(D, FH0);
   HIPCHK(hipEventRecord(S.evf1, flow_stream));
   // ---- admission markers (k_adm, launched above on the flow stream)
   HIPCHK(hipStreamWaitEvent(s, adm_done, 0));
@@ -594,6 +609,7 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
     HIPCHK(hipEventRecord(prep_t, hot_stream));
     k_flow_plan_tail<<<nh_tail, 64, 0, hot_stream>>>(D, FT);
     k_flow_plan_tail_c<<<nh_tail, 64, FC_TAIL_LDS, hot_stream>>>(D, FT);
+    k_flow_plan_tail_cb<<<nh_tail, 64, fc_ring_lds, hot_stream>>>(D, FT);
     k_flow_sort<<<nh_tail, FL_SORT_T, 0, hot_stream>>>(D, FT);
     k_flow_level<<<nh_tail, FL_LEVEL_T, 0, hot_stream>>>(D, FT);
     k_flow_toff<FL_OK_ADD><<<1, 1024, 0, hot_stream>>>(D, FT);
@@ -612,7 +628,7 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   // the other head books: plan, reconstruction and events (into the arena) after the tail
   HIPCHK(hipStreamWaitEvent(hot_stream, prep_h, 0));
   if (nh_near) {
-    k_flow_plan_near<<<nh_near, 256, FC_HEAD_LDS, hot_stream>>>(D, FH1);
+    k_flow_plan_near<<<nh_near, 256, fc_ring_lds, hot_stream>>>(D, FH1);
     head_recon(FH1, nh_near, hot_stream);
     head_recon_c(FH1, FH1c, nh_near, hot_stream);
     k_flow_events_arena<<<1024, 256, 0, hot_stream>>>(D, B, FH1);

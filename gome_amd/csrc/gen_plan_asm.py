@@ -59,6 +59,10 @@ PAIR = {"A": (32, 33), "B": (34, 35)}
 ZERO = "s91"                     # W32: stays 0, the high word of the rest amount s[90:91]
 COPY_REST = os.environ.get("GOME_PLAN_COPY", "1") == "1"   # measured at a pinned placement: -2% cycles
 LOOP_OFS = int(os.environ.get("GOME_PLAN_OFS", "0"))  # 4-byte words after the 256-B alignment
+# timing experiments only (tools/build_variant.py): wait for each half-group's records right
+# after issuing them / drop the DEL's LDS wait (wrong results)
+SYNC_SMEM = os.environ.get("GOME_PLAN_SYNC_SMEM", "0") == "1"
+DEL_NOWAIT = os.environ.get("GOME_PLAN_DEL_NOWAIT", "0") == "1"
 PF_DIST = int(os.environ.get("GOME_PLAN_PF", "0"))  # L2 prefetch distance in bytes (0: off);
 # k_flow_prep pads ord8 by FL_ORD8_PAD records, which must cover it
 
@@ -525,6 +529,8 @@ class Gen:
         e(f"s_add_u32 s98, s98, {8 * HG}")
         e("s_addc_u32 s99, s99, 0")
         e(f"s_load_dwordx16 s[{other}:{other + 15}], {ADDR}, 0x0")   # prefetch the next half
+        if SYNC_SMEM:
+            e("s_waitcnt lgkmcnt(0)")
         if PF_DIST:  # warm L2 further ahead with a vector load (never waited for in the loop)
             e("s_mov_b64 exec, 1")
             e(f"global_load_dword %[vpf], %[vzero], {ADDR} offset:{PF_DIST}")
@@ -747,7 +753,8 @@ class GenC(Gen):
         e(f"s_cselect_b32 {X2}, {BBD[0]}, 0")
         e(f"s_add_u32 {X1}, {X1}, {X2}")
         e(f"v_subrev_u32 v{VG0}, {X1}, v{VG0}")               # G_k
-        e("s_waitcnt lgkmcnt(0)")
+        if not DEL_NOWAIT:
+            e("s_waitcnt lgkmcnt(0)")
         # a = E_m + v_m + Xb (< 2^32: the window's makers arrived after m); r = a - G_k clamped
         # to [0, v_m]; xv_m := v_m
         e(f"v_cndmask_b32 v{VE}, v{VE}, v{VE + 1}, vcc")      # E_m

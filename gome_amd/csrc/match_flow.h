@@ -118,7 +118,8 @@ struct FlowHdr {
                                         // w32: the 32-bit plan (volumes / depths in units of g)
   unsigned long long amask[2], bmask[2];  // final S:SALE / S:BUY membership of the levels
   unsigned long long g;                   // volume unit of the book's plan (1 for the 64-bit plan)
-  unsigned long long pad2;
+  uint32_t fc_img;     // books with DELs: first entry of the book's ring image (fc_img)
+  uint32_t fc_big;     //   its ring needs more than FC_TAIL_SLOTS entries
   // books whose segment holds DELs (ok == FL_OK_CANCEL, match_flow_cancel.h)
   uint32_t ndel;       // DEL records of the segment
   uint32_t nslot;      // LDS ring entries of the plan (16 B each, the dummy entry included)
@@ -158,16 +159,14 @@ struct FlowLvl {
 static_assert(sizeof(FlowLvl) % 16 == 0, "FlowLvl alignment");
 
 // The cancel plan's LDS ring (match_flow_cancel.h): 16-B entries {R pair, v, xv} per targeted
-// maker (+ one dummy entry), an image per book built by the cancel prep.
-constexpr uint32_t FC_HEAD_SLOTS = 9216;  // head books own their CU (144 KiB of LDS)
-constexpr uint32_t FC_TAIL_SLOTS = 1024;  // tail books (16 KiB)
-constexpr uint32_t FC_HEAD_LDS = FC_HEAD_SLOTS * 16, FC_TAIL_LDS = FC_TAIL_SLOTS * 16;
+// maker (+ one dummy entry), an image per book built by the cancel prep (bump-allocated).  A
+// ring of up to FC_TAIL_SLOTS entries plans in a 16-KiB workgroup; a larger one (up to
+// FlowArgs::fc_ring_cap, the device's LDS per workgroup) in a workgroup that owns its CU.
+constexpr uint32_t FC_MAX_SLOTS = 10240;  // 160 KiB: the most LDS a gfx950 workgroup can hold
+constexpr uint32_t FC_TAIL_SLOTS = 1024;
+constexpr uint32_t FC_TAIL_LDS = FC_TAIL_SLOTS * 16;
 constexpr uint32_t FC_TOFF = MAX_FLOW + 16;  // second toff region for books with DELs
 constexpr uint32_t FC_GEN_MASK = 0x7FF;   // generation bits of an FcHash key
-__host__ __device__ constexpr uint64_t fc_img_off(uint32_t h) {
-  return h < FL_HEAD ? static_cast<uint64_t>(h) * FC_HEAD_SLOTS
-                     : static_cast<uint64_t>(FL_HEAD) * FC_HEAD_SLOTS + static_cast<uint64_t>(h - FL_HEAD) * FC_TAIL_SLOTS;
-}
 
 struct FcDel;  // a DEL record's target (match_flow_cancel.h)
 struct FcHash;
@@ -193,7 +192,10 @@ struct FlowArgs {
   // streams), and the range's offset in toff
   uint32_t h0, h1, tb;
   // books with DELs (match_flow_cancel.h)
-  uint4* fc_img;       // LDS ring images, fc_img_off(h)
+  uint4* fc_img;       // LDS ring images (FlowHdr::fc_img), bump-allocated per batch
+  uint32_t* fc_img_bump;
+  uint32_t fc_img_cap; // entries
+  uint32_t fc_ring_cap;  // largest ring (entries): the device's LDS per workgroup / 16
   FcDel* fc_del;       // [max_batch] per segment position: the DEL's target
   uint32_t* fc_tg;     // [max_batch] per segment position: ADD targeted by the DEL at (value - 1)
   uint32_t* fc_rank;   // [max_batch] per segment position: a targeted ADD's rank in its level
@@ -839,14 +841,16 @@ extern __shared__ uint4 fl_ring[];  // the cancel plan's ring (dynamic LDS)
 // Books with DELs: the ring image -> LDS, by every thread of the block.
 __device__ __forceinline__ void fl_ring_load(const FlowArgs& F, uint32_t h) {
   const uint32_t ns = F.hdr[h].nslot;
-  const uint4* img = F.fc_img + fc_img_off(h);
+  const uint4* img = F.fc_img + F.hdr[h].fc_img;
   for (uint32_t i = threadIdx.x; i < ns; i += blockDim.x) fl_ring[i] = img[i];
 }
 
+// ring: for books with DELs, 0 any ring, 1 small rings only, 2 large rings only
 template <bool EXCL>
-__device__ __forceinline__ void fl_plan_kernel(const Dev& D, const FlowArgs& F, uint32_t kind) {
+__device__ __forceinline__ void fl_plan_kernel(const Dev& D, const FlowArgs& F, uint32_t kind, uint32_t ring = 0) {
   const uint32_t h = F.h0 + blockIdx.x;
-  const bool mine = h < fl_hend(D, F) && uni(F.hdr[h].ok) == kind;
+  const bool mine = h < fl_hend(D, F) && uni(F.hdr[h].ok) == kind &&
+                    (ring == 0 || (uni(F.hdr[h].fc_big) != 0) == (ring == 2));
   if (mine && kind == FL_OK_CANCEL) fl_ring_load(F, h);
   if (EXCL) {
     asm volatile("" ::: "v255", "a255");
@@ -873,7 +877,9 @@ __global__ __launch_bounds__(256) void k_flow_plan_near(Dev D, FlowArgs F) {
 }
 __global__ __launch_bounds__(64) void k_flow_plan_tail(Dev D, FlowArgs F) { fl_plan_kernel<false>(D, F, FL_OK_ADD); }
 // tail books with DELs (a launch of its own: 16 KiB of LDS per block)
-__global__ __launch_bounds__(64) void k_flow_plan_tail_c(Dev D, FlowArgs F) { fl_plan_kernel<false>(D, F, FL_OK_CANCEL); }
+__global__ __launch_bounds__(64) void k_flow_plan_tail_c(Dev D, FlowArgs F) { fl_plan_kernel<false>(D, F, FL_OK_CANCEL, 1); }
+// tail books with DELs whose ring exceeds FC_TAIL_SLOTS (the largest LDS allocation)
+__global__ __launch_bounds__(64) void k_flow_plan_tail_cb(Dev D, FlowArgs F) { fl_plan_kernel<false>(D, F, FL_OK_CANCEL, 2); }
 
 __device__ __forceinline__ void fl_plan_book(const Dev& D, const FlowArgs& F, uint32_t h) {
   const FlowHdr* hd = &F.hdr[h];

@@ -387,7 +387,7 @@ __global__ __launch_bounds__(FC_PASS_T) void k_fc_pass(Dev D, BatchArgs B, FlowA
   }
   // ring layout: power-of-two capacities, placed largest first (each base aligned to its size)
   if (tid == 0) {
-    const uint32_t cap = h < FL_HEAD ? FC_HEAD_SLOTS : FC_TAIL_SLOTS;
+    const uint32_t cap = F.fc_ring_cap;
     uint32_t off = 0, top = 1;
     for (uint32_t q = 1; q <= nl; ++q) {
       uint32_t c = 1;
@@ -408,6 +408,15 @@ __global__ __launch_bounds__(FC_PASS_T) void k_fc_pass(Dev D, BatchArgs B, FlowA
           }
     }
     nslot_s = off + 1;
+    if (!bad_s) {  // the book's image
+      const uint32_t base = atomicAdd(F.fc_img_bump, nslot_s);
+      if (static_cast<unsigned long long>(base) + nslot_s > F.fc_img_cap) {
+        bad_s |= FC_BAD_RING;
+      } else {
+        F.hdr[h].fc_img = base;
+        F.hdr[h].fc_big = nslot_s > FC_TAIL_SLOTS ? 1u : 0u;
+      }
+    }
     uint32_t mw = 0;
     for (uint32_t q = 1; q <= nl; ++q) mw = max(mw, cmax[q]);
     F.hdr[h].ncancel = mw;
@@ -423,7 +432,7 @@ __global__ __launch_bounds__(FC_PASS_T) void k_fc_pass(Dev D, BatchArgs B, FlowA
     LV[tid].cring = cring[tid];
     LV[tid].rbase = rbase[tid];
   }
-  uint4* img = F.fc_img + fc_img_off(h);
+  uint4* img = F.fc_img + F.hdr[h].fc_img;
   for (uint32_t x = tid; x < nslot; x += FC_PASS_T) img[x] = make_uint4(0u, 0u, 0u, 0u);
   __syncthreads();
   const uint32_t npad = (8u - (n & 7u)) & 7u;

@@ -12,7 +12,7 @@ from tools.debug_fc_tail import FCDEL, HDR  # noqa: E402
 N = int(sys.argv[1]) if len(sys.argv) > 1 else 1 << 22
 ns = wl.NativeStream(100000, 1.0, seed=1, price_decimals=2, del_frac=0.5, aggressive_frac=0.1)
 eng = Engine(max_symbols=100000, max_batch=N, max_nodes=1 << 24, max_levels=1 << 25)
-for bi in range(4):
+for bi in range(int(sys.argv[2]) if len(sys.argv) > 2 else 4):
     b = ns.batch(N)
     eng.submit(b)
     eng.release_device_events() if False else eng.drain()
@@ -35,4 +35,4 @@ for bi in range(4):
         q = np.percentile(nb, [50, 90, 99, 100])
         print(f"   window n_b p50 {q[0]:.0f} p90 {q[1]:.0f} p99 {q[2]:.0f} max {q[3]:.0f}; >63: {float((nb > 63).mean()):.3f}"
               f"  mean chunks {float(np.ceil(nb / 63).mean()):.2f}")
-    print("   routes:", np.unique(fb["kind"], return_counts=True))
+    print("   head routes (kind, decline, ring, window):", [(int(x["kind"]), int(x["decline"]), int(x["ring"]), int(x["window"])) for x in fb])

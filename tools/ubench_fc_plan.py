@@ -82,7 +82,41 @@ def native(rng, i):
     return _ns["s"].batch(N)
 
 
+def _sweeps(rng, i):
+    b = adds(rng, N, 1 + i * N)
+    ag = rng.random(N) < 0.1
+    b["price_fx"][ag] = np.where(b["side"][ag] == 0, wl.FX, wl.FX // 100)
+    b["volume_fx"][ag] = rng.integers(1, 17, int(ag.sum())) * 10 * wl.FX
+    return b
+
+
+def recent_dels(aggr):
+    """50% DELs, each of a uniformly chosen ADD among the last 256 untargeted ones (windows stay
+    short); `aggr` of the ADDs sweep (BUY @ 1.00 / SALE @ 0.01, 10..160 units)."""
+    def mk(rng, i):
+        b = adds(rng, N, 1 + i * N)
+        ag = rng.random(N) < aggr
+        b["price_fx"][ag] = np.where(b["side"][ag] == 0, wl.FX, wl.FX // 100)
+        b["volume_fx"][ag] = rng.integers(1, 17, int(ag.sum())) * 10 * wl.FX
+        d = rng.random(N) < 0.5
+        pool = []
+        for j in range(N):
+            if d[j] and pool:
+                k = pool.pop(int(rng.integers(len(pool))))
+                b[j] = b[k]
+                b[j]["action"] = wl.DEL
+            else:
+                d[j] = False
+                pool.append(j)
+                if len(pool) > 256:
+                    pool.pop(0)
+        return b
+    return mk
+
+
 run("ADD only (W32)", add_only)
 run("ADD + one no-op DEL (W32C)", one_noop)
 run("50% no-op DELs (W32C)", half_noop)
-run("config-4 generator, 1 symbol (W32C)", native)
+run("50% DELs of recent ADDs (W32C)", recent_dels(0.0))
+run("50% DELs of recent ADDs, 10% sweeps", recent_dels(0.1))
+run("ADD only, 10% sweeps (W32)", lambda rng, i: recent_dels(0.1)(rng, i)[:0] if False else _sweeps(rng, i))

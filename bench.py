@@ -113,6 +113,11 @@ def shard_stream(n_symbols, zipf_s, rank, world, seed, price_decimals=2):
     return batch, share, float(p[0])
 
 
+def note(msg):
+    """Progress on stderr (a long bench line must keep writing: GPU runners treat a silent run as hung)."""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def make_stream(workload, rank, world, seed):
     """(batch(n) -> records, owned share, top-symbol share) of this rank's stream."""
     W = WORKLOADS[workload]
@@ -227,6 +232,7 @@ def main():
     e2e_warm = 2 if e2e_steps else 0
     gen, share, top_share = make_stream(args.workload, rank, world, args.seed)
     per_rank = int(round(args.batch * world * share))
+    note(f"{args.workload}: generating {warm + steps} batches of {per_rank} records")
     host_batches = [gen(per_rank).copy() for _ in range(warm + steps)]
     dev_batches = [torch.from_numpy(b.view(np.uint8)).cuda() for b in host_batches]
     torch.cuda.synchronize()
@@ -259,6 +265,7 @@ def main():
 
     for i in range(warm):
         step(i)
+        note(f"warmup step {i + 1}/{warm}")
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -270,6 +277,8 @@ def main():
         ts = time.perf_counter()
         sts.append(step(i))
         lat.append((time.perf_counter() - ts) * 1e3)
+        if rank == 0:
+            note(f"step {i - warm + 1}/{steps}: {lat[-1]:.1f} ms")
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -323,6 +332,8 @@ def main():
                     ev, st = eng.collect(copy=False)
                     done_ev[0] += len(ev)
                     lats.append((time.perf_counter() - tsub[k - 1]) * 1e3)
+                    if rank == 0:
+                        note(f"e2e batch {k - 1}: {lats[-1]:.1f} ms")
             ev, st = eng.collect(copy=False)
             done_ev[0] += len(ev)
             lats.append((time.perf_counter() - tsub[hi - 1]) * 1e3)
@@ -354,6 +365,7 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         thr = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+        note("cpu baseline")
         one, many = cpu_baseline(host_batches, n_symbols, args.cpu_budget, thr)
         v1, done, t_cpu, used = one
         cpu = {"value": round(v1, 1), "unit": "orders/s", "cores": 1, "kind": "port",

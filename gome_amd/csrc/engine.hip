@@ -645,7 +645,8 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   HIPCHK(hipStreamWaitEvent(s, prep_h, 0));
   HIPCHK(hipStreamWaitEvent(s, prep_t, 0));
   HIPCHK(hipEventRecord(S.evc0, s));
-  k_match<<<std::min<uint32_t>(grid, COLD_BLOCKS), 64, 0, s>>>(D, B, &F.hdr[0].ok, sizeof(FlowHdr) / sizeof(uint32_t));
+  k_match<<<std::min<uint32_t>(ceil_div(grid, COLD_WAVES), COLD_BLOCKS), 64 * COLD_WAVES, 0, s>>>(
+      D, B, &F.hdr[0].ok, sizeof(FlowHdr) / sizeof(uint32_t));
   HIPCHK(hipEventRecord(S.evc1, s));
   HIPCHK(hipStreamWaitEvent(s, join, 0));
   HIPCHK(hipStreamWaitEvent(s, joinf, 0));

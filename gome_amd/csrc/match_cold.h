@@ -54,7 +54,7 @@ constexpr uint32_t MAX_FLOW = 4096;
 constexpr uint32_t LEGACY_HOT_MIN = 2048;
 constexpr uint32_t MAX_LEGACY = 256;
 #ifndef GOME_COLD_BLOCKS
-#define GOME_COLD_BLOCKS 240  // leaves CUs free for the head plans' whole-CU blocks (launched later)
+#define GOME_COLD_BLOCKS 128  // half the CUs: the rest stay free for the flow path (plans own whole CUs)
 #endif
 constexpr uint32_t COLD_BLOCKS = GOME_COLD_BLOCKS;  // persistent cold-kernel blocks
 constexpr uint32_t EVB_HOT = 256; // events per arena block (hot books)
@@ -64,8 +64,11 @@ struct WaveCtx {
   Dev D;
   BatchArgs B;
   uint32_t sym;
-  Level* L;          // the book's sorted level array (HBM)
-  uint32_t nl, cap, base;
+  Level* L;          // the book's sorted level array: HBM, or the wave's LDS copy (in_lds)
+  uint32_t nl, cap, base;  // cap: entries of L; base / hcap: the book's HBM level block
+  uint32_t hcap;
+  Level* lds;        // the wave's LDS level slots (COLD_LDS_LVLS), or nullptr
+  bool in_lds;
   uint32_t ev_base, ev_used, evb;
   uint32_t flags;    // Book flags (BOOK_QUIRK)
   bool ev_ok, fatal;
@@ -174,7 +177,36 @@ __device__ __forceinline__ void level_gc(WaveCtx& W) {
   W.nl = out;
 }
 
+// The book's levels held in LDS go (back) to an HBM block of at least `need` entries.
+__device__ __forceinline__ bool level_spill(WaveCtx& W, uint32_t need) {
+  const uint32_t lane = lane_id();
+  uint32_t base = W.base, cap = W.hcap;
+  if (need > cap) {
+    uint32_t ncap = 16;
+    while (ncap < need) ncap <<= 1;
+    uint32_t nb = 0;
+    if (lane == 0) nb = lvl_block_alloc(W.D, ncap);
+    nb = uni(nb);
+    if (nb == NIL) {
+      set_err(W, ERR_LEVELS);
+      return false;
+    }
+    if (lane == 0) lvl_block_release(W.D, W.base, W.hcap);  // reusable from the next batch on
+    base = nb;
+    cap = ncap;
+  }
+  Level* H = W.D.lvl + base;
+  for (uint32_t k = lane; k < W.nl; k += 64) H[k] = W.L[k];
+  W.base = base;
+  W.hcap = cap;
+  W.L = H;
+  W.cap = cap;
+  W.in_lds = false;
+  return true;
+}
+
 __device__ __forceinline__ bool level_grow(WaveCtx& W) {
+  if (W.in_lds) return level_spill(W, 2 * W.nl);
   const uint32_t lane = lane_id();
   uint32_t ncap = W.cap ? W.cap * 2 : 16;
   uint32_t nb = 0;
@@ -192,6 +224,7 @@ __device__ __forceinline__ bool level_grow(WaveCtx& W) {
   if (lane == 0) lvl_block_release(W.D, W.base, W.cap);  // reusable from the next batch on
   W.L = NL;
   W.cap = ncap;
+  W.hcap = ncap;
   W.base = nb;
   return true;
 }
@@ -583,16 +616,27 @@ __device__ __forceinline__ void process_global(WaveCtx& W, uint32_t b0, uint32_t
   }
 }
 
-__device__ __forceinline__ void wave_finish(WaveCtx& W) {
+__device__ __forceinline__ void wave_flush(WaveCtx& W);
+
+// The book's record; with `flush` also the wave's counters (a persistent cold wave keeps them
+// across its books and flushes once, see k_match).
+__device__ __forceinline__ void wave_finish(WaveCtx& W, bool flush = true) {
   const uint32_t lane = lane_id();
-  ev_close(W);
+  if (W.in_lds) level_spill(W, W.nl);
   if (lane == 0) {
     Book nb;
     nb.lvl_base = W.base;
     nb.n_lvl = W.nl;
-    nb.lvl_cap = W.cap;
+    nb.lvl_cap = W.hcap;
     nb.pad = W.flags;
     W.D.books[W.sym] = nb;
+  }
+  if (flush) wave_flush(W);
+}
+
+__device__ __forceinline__ void wave_flush(WaveCtx& W) {
+  ev_close(W);
+  if (lane_id() == 0) {
     unsigned long long* c = W.D.st->ctr;
     if (W.fills) atomicAdd(&c[C_FILLS], W.fills);
     if (W.cancels) atomicAdd(&c[C_CANCELS], W.cancels);
@@ -605,16 +649,35 @@ __device__ __forceinline__ void wave_finish(WaveCtx& W) {
   }
 }
 
-__device__ __forceinline__ void wave_init(WaveCtx& W, const Dev& D, const BatchArgs& B, uint32_t sym, uint32_t evb) {
-  W.D = D;
-  W.B = B;
+// The next book of a wave: its state, the event block continues (a persistent cold wave keeps
+// one partly filled block and its counters across books).
+// Cold books with few levels work on an LDS copy of their level array (every level search,
+// insert and update is then an LDS access instead of an HBM round trip); written back by
+// wave_finish.
+constexpr uint32_t COLD_LDS_LVLS = 128;
+
+__device__ __forceinline__ void wave_next_book(WaveCtx& W, uint32_t sym) {
   W.sym = sym;
-  const Book bk = D.books[sym];
+  const Book bk = W.D.books[sym];
   W.base = uni(bk.lvl_base);
   W.nl = uni(bk.n_lvl);
-  W.cap = uni(bk.lvl_cap);
+  W.cap = W.hcap = uni(bk.lvl_cap);
   W.flags = uni(bk.pad);
-  W.L = D.lvl + W.base;
+  W.L = W.D.lvl + W.base;
+  W.in_lds = W.lds != nullptr && W.nl <= COLD_LDS_LVLS;
+  if (W.in_lds) {
+    for (uint32_t k = lane_id(); k < W.nl; k += 64) W.lds[k] = W.L[k];
+    W.L = W.lds;
+    W.cap = COLD_LDS_LVLS;
+  }
+}
+
+__device__ __forceinline__ void wave_init(WaveCtx& W, const Dev& D, const BatchArgs& B, uint32_t sym, uint32_t evb,
+                                          Level* lds = nullptr) {
+  W.D = D;
+  W.B = B;
+  W.lds = lds;
+  wave_next_book(W, sym);
   W.ev_base = NIL;
   W.ev_used = 0;
   W.evb = evb;
@@ -624,24 +687,40 @@ __device__ __forceinline__ void wave_init(WaveCtx& W, const Dev& D, const BatchA
   W.resting_delta = W.levels_delta = 0;
 }
 
-// Cold books: one 64-thread workgroup (one wavefront) per book, state in HBM.  Block i
-// takes seg_order[i]; flow candidates are skipped unless the flow path declined them and
-// they are too short for the legacy hot kernel (`flow_ok[i]`: FlowHdr::ok of candidate i).
-// Persistent: block b takes books b, b + gridDim.x, ...  (a bounded number of waves in
-// flight keeps the cold books' latency-bound traffic from slowing the flow plan's loads;
-// they have slack: the plan of the hottest book is the batch's critical path).
-__global__ __launch_bounds__(64) void k_match(Dev D, BatchArgs B, const uint32_t* flow_ok, uint32_t ok_stride) {
+// Cold books: one wavefront per book, state in HBM.  Wave w of the grid takes books
+// seg_order[w], seg_order[w + waves], ...; flow candidates are skipped unless the flow path
+// declined them and they are too short for the legacy hot kernel (`flow_ok[i]`: FlowHdr::ok
+// of candidate i).  Every step of a cold book is a dependent HBM round trip, so the kernel
+// needs many waves in flight: COLD_WAVES per workgroup on at most COLD_BLOCKS workgroups
+// (fewer workgroups than CUs leaves whole CUs free for the flow plans' one-block-per-CU
+// kernels, launched later).  A wave keeps its event block and its counters across books.
+#ifndef GOME_COLD_WAVES
+#define GOME_COLD_WAVES 8
+#endif
+constexpr uint32_t COLD_WAVES = GOME_COLD_WAVES;
+__global__ __launch_bounds__(64 * COLD_WAVES) void k_match(Dev D, BatchArgs B, const uint32_t* flow_ok, uint32_t ok_stride) {
   if (D.st->err & ERR_INPUT) return;
   const uint32_t nseg = D.st->nseg, nhot = D.st->nhot;
-  for (uint32_t i = blockIdx.x; i < nseg; i += gridDim.x) {
+  const uint32_t nw = blockDim.x >> 6, stride = gridDim.x * nw;
+  __shared__ Level lvl_lds[COLD_WAVES][COLD_LDS_LVLS];
+  WaveCtx W;
+  bool started = false;
+  for (uint32_t i = blockIdx.x * nw + (threadIdx.x >> 6); i < nseg; i += stride) {
     const uint32_t seg = B.seg_order[i];
     const uint32_t beg = B.seg_start[seg], end = B.seg_start[seg + 1];
     if (i < nhot && (flow_ok[i * ok_stride] || (end - beg >= LEGACY_HOT_MIN && i < MAX_LEGACY))) continue;
-    WaveCtx W;
-    wave_init(W, D, B, uni(B.ord[B.prep[beg].idx].symbol_id), EVB);
+    const uint32_t sym = uni(B.ord[B.prep[beg].idx].symbol_id);
+    if (!started) {
+      wave_init(W, D, B, sym, EVB, lvl_lds[threadIdx.x >> 6]);
+      started = true;
+    } else {
+      wave_next_book(W, sym);
+    }
     process_global(W, beg, end);
-    wave_finish(W);
+    wave_finish(W, false);
+    if (W.fatal) break;
   }
+  if (started) wave_flush(W);
 }
 
 

@@ -264,23 +264,30 @@ def _buys(sym0, nsym, nprice, oid0, pbase=1):
 
 def test_level_blocks_reused():
     """A book that outgrows its level block releases it; blocks of that class are handed to
-    other books in later batches instead of carving new ones (VERDICT r1 #7)."""
-    eng = Engine(max_symbols=256, max_batch=8192, max_levels=1 << 16)
+    other books in later batches instead of carving new ones.  Cold books of
+    up to 128 levels grow in LDS and take one block of the final size at write-back; larger
+    ones grow block by block in HBM."""
+    eng = Engine(max_symbols=256, max_batch=30000, max_levels=1 << 17)
     orc = Oracle(256)
-    b1, oid = _buys(0, 100, 40, 1)          # 100 books grow 16 -> 32 -> 64 levels
+    b1, oid = _buys(0, 100, 40, 1)                  # 100 books of 40 levels: one 64-block each
     eng.submit(b1)
     _cmp(eng.drain(), orc.submit(b1))
     used1 = eng.stats()["lvl_used"]
-    assert used1 == 100 * (16 + 32 + 64)
-    b2, oid = _buys(100, 100, 10, oid)      # 100 new books of 10 levels: released 16-blocks
-    eng.submit(b2)
+    assert used1 == 100 * 64
+    b2, oid = _buys(0, 100, 60, oid, pbase=41)      # they grow to 100 levels: 128-blocks, the
+    eng.submit(b2)                                  # 64-blocks released
     _cmp(eng.drain(), orc.submit(b2))
-    assert eng.stats()["lvl_used"] == used1
-    b3, oid = _buys(100, 100, 12, oid, pbase=20)  # they grow to 22 levels: released 32-blocks
-    eng.submit(b3)
+    used2 = eng.stats()["lvl_used"]
+    assert used2 == used1 + 100 * 128
+    b3, oid = _buys(100, 100, 40, oid)              # 100 new books of 40 levels: the released
+    eng.submit(b3)                                  # 64-blocks
     _cmp(eng.drain(), orc.submit(b3))
-    assert eng.stats()["lvl_used"] == used1
-    _cmp_books(eng, orc, range(0, 200, 7), "levels")
+    assert eng.stats()["lvl_used"] == used2
+    b4, oid = _buys(0, 20, 100, oid, pbase=101)     # 200 levels: beyond the LDS copy, the HBM
+    eng.submit(b4)                                  # path (spill to 256-blocks)
+    _cmp(eng.drain(), orc.submit(b4))
+    assert eng.stats()["lvl_used"] == used2 + 20 * 256
+    _cmp_books(eng, orc, list(range(0, 200, 7)) + [0, 19], "levels")
 
 
 # ---- multi-GPU sharding with real engines (SURVEY §8e) ----------------------------------

@@ -10,14 +10,18 @@ from gome_amd.abi import Engine  # noqa: E402
 from tools.debug_fc_tail import FCDEL, HDR  # noqa: E402
 
 N = int(sys.argv[1]) if len(sys.argv) > 1 else 1 << 22
-ns = wl.NativeStream(100000, 1.0, seed=1, price_decimals=2, del_frac=0.5, aggressive_frac=0.1)
+ns = wl.NativeStream(100000, 1.0, seed=int(os.environ.get('SEED', '42')), price_decimals=2, del_frac=0.5, aggressive_frac=0.1)
 eng = Engine(max_symbols=100000, max_batch=N, max_nodes=1 << 24, max_levels=1 << 25)
 for bi in range(int(sys.argv[2]) if len(sys.argv) > 2 else 4):
     b = ns.batch(N)
     eng.submit(b)
     eng.release_device_events() if False else eng.drain()
     st = eng.stats()
-    fb = eng.debug_flow_books(8)
+    allb = eng.debug_flow_books()
+    bad = allb[allb["kind"] == 0]
+    print(f"   declined candidates: {len(bad)} of {len(allb)}; orders {int(bad['orders'].sum())}; "
+          f"reasons {np.unique(bad['decline'], return_counts=True)}; biggest {bad[np.argsort(-bad['orders'].astype(np.int64))][:3][['orders','dels','levels','ring','window','w32','decline']].tolist()}")
+    fb = allb[:8]
     hdr = np.frombuffer(eng.debug_peek(0, 0, HDR.itemsize * len(fb)), HDR)
     x = hdr[0]
     beg, end = int(x["beg"]), int(x["end"])

@@ -34,6 +34,7 @@
 #include "match_cold.h"
 #include "match_flow.h"
 #include "match_flow_cancel.h"
+#include "match_flow_deep.h"
 #include "match_hot.h"
 #include "pipeline.h"
 #include "wave.h"
@@ -303,9 +304,12 @@ gome_status gome_engine::init(const gome_config& c) {
     F.fc_ring_cap = std::min<uint32_t>(FC_MAX_SLOTS, static_cast<uint32_t>(std::max(lds, 0)) / 16);
     if (F.fc_ring_cap < FC_TAIL_SLOTS) return fail(GOME_E_DEVICE, "device LDS per workgroup below 16 KiB");
     fc_ring_lds = F.fc_ring_cap * 16;
+    if (fc_ring_lds < DEEP_CAP * 8) return fail(GOME_E_DEVICE, "device LDS per workgroup below 128 KiB");
     for (const void* k : {reinterpret_cast<const void*>(k_flow_plan_head), reinterpret_cast<const void*>(k_flow_plan_near),
                           reinterpret_cast<const void*>(k_flow_plan_tail_cb)})
       HIPCHK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(fc_ring_lds)));
+    HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_deep_prep_b), hipFuncAttributeMaxDynamicSharedMemorySize,
+                               static_cast<int>(DEEP_CAP * 8)));
   }
 
   max_batch = cfg.max_batch;
@@ -404,6 +408,13 @@ gome_status gome_engine::init(const gome_config& c) {
       !alloc(&F.fc_hash, fc_hcap, "flow cancel table"))
     return GOME_E_CAPACITY;
   HIPCHK(hipMemsetAsync(F.fc_hash, 0, sizeof(FcHash) * fc_hcap, stream));
+  // deep head books (match_flow_deep.h)
+  if (!alloc(&F.dlvl, static_cast<size_t>(FL_HEAD) * DEEP_CAP, "deep level tables") ||
+      !alloc(&F.dlvout, static_cast<size_t>(FL_HEAD) * DEEP_CAP, "deep final levels") ||
+      !alloc(&F.dh_key, static_cast<size_t>(FL_HEAD) * DEEP_HASH, "deep price sets") ||
+      !alloc(&F.dh_val, static_cast<size_t>(FL_HEAD) * DEEP_HASH, "deep price levels") ||
+      !alloc(&F.tlog, ntouch, "deep sort pass"))
+    return GOME_E_CAPACITY;
   HIPCHK(hipMemsetAsync(F.hdr, 0, sizeof(FlowHdr) * MAX_FLOW, stream));
   HIPCHK(hipMemsetAsync(d_pend, 0, sizeof(PendEnt) * nb, stream));
   if (D.idx_mask >= PEND) return fail(GOME_E_INVAL, "gome_config.max_nodes too large (index > 2^31 slots)");
@@ -546,6 +557,12 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   k_flow_prep_a<<<dim3(FL_PG, nh_head), FL_PREP_T, 0, flow_stream>>>(D, B, FH);
   k_flow_prep_b<<<nh_head, FL_PREP_T, 0, flow_stream>>>(D, B, FH);
   k_flow_prep_c<<<dim3(FL_PG, nh_head), FL_PREP_T, 0, flow_stream>>>(D, B, FH);
+  // head books with more levels than lanes: the deep prep (match_flow_deep.h)
+  HIPCHK(hipMemsetAsync(F.dh_key, 0, sizeof(unsigned long long) * FL_HEAD * DEEP_HASH, flow_stream));
+  HIPCHK(hipMemsetAsync(F.dh_val, 0xFF, sizeof(uint32_t) * FL_HEAD * DEEP_HASH, flow_stream));
+  k_deep_prep_a<<<dim3(FL_PG, nh_head), FL_PREP_T, 0, flow_stream>>>(D, B, FH);
+  k_deep_prep_b<<<nh_head, FL_PREP_T, DEEP_CAP * 8, flow_stream>>>(D, B, FH);
+  k_deep_prep_c<<<dim3(FL_PG, nh_head), FL_PREP_T, 0, flow_stream>>>(D, B, FH);
   // books with DELs: targets, windows, ring images, W32C records (or back to the legacy path)
   auto cancel_prep = [&](const FlowArgs& R, uint32_t nb, uint32_t px, bool wide, hipStream_t st) {
     k_fc_hash_claim<<<dim3(px, nb), 256, 0, st>>>(D, B, R);
@@ -581,11 +598,21 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
     k_flow_sort_cnt<<<dim3(FL_SORT_GRID, nb), FL_TILE, 0, st>>>(D, R);
     k_flow_sort_scan<<<nb, FL_CAP, 0, st>>>(D, R);
     k_flow_sort_scatter<<<dim3(FL_SORT_GRID, nb), FL_TILE, 0, st>>>(D, R);
+    // deep books: the two-pass level sort and the per-level reconstruction
+    k_deep_sort_cnt<1><<<dim3(FL_SORT_GRID, nb), FL_TILE, 0, st>>>(D, R);
+    k_deep_sort_scan<<<nb, FL_CAP, 0, st>>>(D, R);
+    k_deep_sort_scatter<1><<<dim3(FL_SORT_GRID, nb), FL_TILE, 0, st>>>(D, R);
+    k_deep_sort_cnt<2><<<dim3(FL_SORT_GRID, nb), FL_TILE, 0, st>>>(D, R);
+    k_deep_sort_scan<<<nb, FL_CAP, 0, st>>>(D, R);
+    k_deep_sort_scatter<2><<<dim3(FL_SORT_GRID, nb), FL_TILE, 0, st>>>(D, R);
     k_flow_level_wide<<<dim3(FL_CAP, nb), 64, 0, st>>>(D, R);
+    k_deep_level<<<dim3(DEEP_GRID, nb), 64, 0, st>>>(D, R);
     k_flow_toff<FL_OK_ADD><<<1, 1024, 0, st>>>(D, R);
     k_flow_count<<<1024, 256, 0, st>>>(D, B, R);
     k_flow_write_lv<<<dim3(FL_CAP, nb), 64, 0, st>>>(D, B, R);
     k_flow_write_fin<<<nb, 128, 0, st>>>(D, R);
+    k_deep_write_lv<<<dim3(DEEP_GRID, nb), 64, 0, st>>>(D, B, R);
+    k_deep_write_fin<<<nb, DEEP_FIN_T, 0, st>>>(D, R);
   };
   // books with DELs (match_flow_cancel.h); their events go to the arena
   auto head_recon_c = [&](const FlowArgs& R, const FlowArgs& Rc, uint32_t nb, hipStream_t st) {
@@ -1002,7 +1029,7 @@ gome_status gome_debug_flow_books(gome_engine* e, uint32_t* out, size_t cap, siz
   for (size_t i = 0; i < n; ++i) {
     const gome::FlowHdr& x = h[i];
     const uint32_t w[GOME_DEBUG_FLOW_WORDS] = {x.ok, x.fc_bad, x.sym, x.end - x.beg, x.ndel, x.nl, x.w32, x.nslot,
-                                               x.ncancel, 0u};
+                                               x.ncancel, x.deep};
     std::copy(w, w + GOME_DEBUG_FLOW_WORDS, out + i * GOME_DEBUG_FLOW_WORDS);
   }
   *n_out = n;

@@ -880,6 +880,207 @@ class GenC(Gen):
         return super().build()
 
 
+# ---- W32D: the 32-bit plan of a deep book (more levels than lanes) -----------
+# Depths live in LDS instead of lane registers: level k's bid depth at byte 8k, its ask depth at
+# 8k + 4 (DEEP_CAP levels, 128 KiB), with the same invariant as the lanes: a slot holds 0 unless
+# its level rests on that side behind the cached top.  Sentinels: level 0 is a permanent bid,
+# level DEEP_CAP - 1 a permanent ask.  A rest is one ds_add; the next level after the top empties
+# is found by reading 64 slots per step and a bit scan.  Records: lo = volume in units of g,
+# hi = level [0, 14) | SALE bit 31 (no-op: 0, a rest of 0 at the bid sentinel).  Touch keys
+# come from the order counter (JJS | 1 << 7 for a rest); the level goes to the touch's second
+# word (Touch::pos, read by the deep sort).
+DEEP_CAP = 16384
+VDA, VDD, VSA, VSD, VSL, VZD = 36, 37, 38, 39, 40, 41     # add address / data, scan address /
+CLOBBERS_D = [f"v{i}" for i in range(36, 42)]             # data, lane id, zero
+
+
+class GenD(Gen):
+    def __init__(self):
+        super().__init__(32)
+
+    def decode(self, j: int):
+        e = self.e
+        hi = f"s{BUF[j][1]}"
+        e(f"s_add_u32 {JJS}, {JJS}, 256")
+        e(f"s_and_b32 {LI}, {hi}, 0x3fff")
+        e(f"s_bitcmp1_b32 {hi}, 31")
+
+    def cross_entry(self, T):
+        pass  # JJS is the order counter
+
+    def logd(self, kr: str, a: str, lvl: str):
+        e = self.e
+        e(f"v_writelane_b32 %[lk], {kr}, m0")
+        e(f"v_writelane_b32 %[la], {a}, m0")
+        e(f"v_writelane_b32 %[lb], {lvl}, m0")
+        e("s_add_u32 m0, m0, 1")
+
+    def emit_flush(self, fl: str, back: str):
+        """As the lane plans, with the touch's level (%[lb]) in its second word."""
+        e = self.e
+        skip = self.fresh("FS")
+        e(f"{fl}:")
+        e("s_mov_b64 exec, -1")
+        e(f"s_add_u32 {T0}, %[lpos], 64")
+        e(f"s_cmp_gt_u32 {T0}, %[lcap]")
+        e(f"s_cbranch_scc1 {skip}")
+        e(f"s_lshl_b32 {T0}, %[lpos], 4")
+        e(f"v_add_u32 %[voff], {T0}, %[vl16]")
+        e("global_store_dword %[voff], %[lk], %[logp]")
+        e("global_store_dword %[voff], %[lb], %[logp] offset:4")
+        e("global_store_dword %[voff], %[la], %[logp] offset:8")
+        e("global_store_dword %[voff], %[vzero], %[logp] offset:12")
+        e(f"{skip}:")
+        e("s_add_u32 %[lpos], %[lpos], m0")
+        e("s_mov_b32 m0, 0")
+        e(f"s_branch {back}")
+
+    @staticmethod
+    def side_off(sd: str) -> int:
+        return 4 if sd == "A" else 0
+
+    def lds_add(self, lvl: str, amt: str, sd: str):
+        """Slot (lvl, sd) += amt (the amount may be 0)."""
+        e = self.e
+        e(f"s_lshl_b32 {T0}, {lvl}, 3")
+        e("s_mov_b64 exec, 1")
+        e(f"v_mov_b32 v{VDA}, {T0}")
+        e(f"v_mov_b32 v{VDD}, {amt}")
+        e(f"ds_add_u32 v{VDA}, v{VDD} offset:{self.side_off(sd)}")
+
+    def next_top(self, sd: str):
+        """After the cached top of side sd emptied: the next level of that side (asks: the lowest
+        nonzero slot above BA, bids: the highest below BB), 64 slots per step; its slot := 0."""
+        e = self.e
+        top, topd = (BA, BAD) if sd == "A" else (BB, BBD)
+        loop, found = self.fresh("NT"), self.fresh("NF")
+        off = self.side_off(sd)
+        if sd == "A":
+            e(f"s_add_u32 {T0}, {BA}, 1")
+        else:
+            e(f"s_sub_u32 {T0}, {BB}, 64")
+        e(f"{loop}:")
+        e("s_mov_b64 exec, -1")
+        e(f"v_add_u32 v{VSA}, {T0}, v{VSL}")
+        e(f"v_lshlrev_b32 v{VSA}, 3, v{VSA}")
+        e(f"ds_read_b32 v{VSD}, v{VSA} offset:{off}")
+        e("s_waitcnt lgkmcnt(0)")
+        e(f"v_cmp_ne_u32_e64 {M}, 0, v{VSD}")
+        if sd == "A":
+            e(f"s_ff1_i32_b64 {O[0]}, {M}")
+        else:
+            e(f"s_flbit_i32_b64 {O[0]}, {M}")
+        e(f"s_cmp_lt_i32 {O[0]}, 0")
+        e(f"s_cbranch_scc0 {found}")
+        e(f"s_{'add' if sd == 'A' else 'sub'}_u32 {T0}, {T0}, 64")
+        e(f"s_branch {loop}")
+        e(f"{found}:")
+        if sd == "B":
+            e(f"s_sub_u32 {O[0]}, 63, {O[0]}")
+        e(f"s_add_u32 {top}, {T0}, {O[0]}")
+        e(f"v_readlane_b32 {topd[0]}, v{VSD}, {O[0]}")
+        e(f"s_lshl_b64 exec, 1, {O[0]}")
+        e(f"ds_write_b32 v{VSA}, v{VZD} offset:{off}")
+
+    def rest(self, side: str, T):
+        """As the 32-bit rest, with the lane add replaced by an LDS add at slot (L, side)."""
+        e = self.e
+        buy = side == "B"
+        top, topd = (BB, BBD) if buy else (BA, BAD)
+        ge, gt = ("ge", "gt") if buy else ("le", "lt")
+        e(f"s_cmp_{ge}_u32 {LI}, {top}")
+        self.csel(X, T, 0)
+        self.csel(A, 0, T)
+        e(f"s_cmp_{gt}_u32 {LI}, {top}")
+        self.csel(A, topd, A)
+        e(f"s_cselect_b32 {L}, {top}, {LI}")
+        self.csel(topd, 0, topd)
+        e(f"s_{'max' if buy else 'min'}_u32 {top}, {top}, {LI}")
+        self.add(topd, topd, X)
+        self.lds_add(L, A[0], "B" if buy else "A")
+        e(f"s_or_b32 {K}, {JJS}, 0x80")
+        self.logd(K, T[0], LI)
+
+    def partial(self, side: str, T):
+        otop, otopd = (BA, BAD) if side == "B" else (BB, BBD)
+        self.sub(otopd, otopd, T)
+        self.logd(JJS, T[0], otop)
+
+    def full(self, side: str, T, i: int):
+        e = self.e
+        buy = side == "B"
+        otop, otopd = (BA, BAD) if buy else (BB, BBD)
+        self.logd(JJS, otopd[0], otop)
+        self.mov(T, D)
+        self.next_top("A" if buy else "B")
+        never = "0" if buy else str(DEEP_CAP - 1)
+        cmp = "le" if buy else "ge"
+        slow, cont = self.lab(f"{side}SL{i}"), self.lab(f"{side}CN{i}")
+        self.is_zero_scc(T)
+        e(f"s_cselect_b32 {T0}, {never}, {LI}")
+        e(f"s_cmp_ge_u32 m0, {64 - HG}")
+        e(f"s_cselect_b32 {T0}, {never}, {T0}")
+        e(f"s_cmp_{cmp}_u32 {otop}, {T0}")
+        e(f"s_cbranch_scc0 {slow}")
+        fl = self.fresh("FL")
+        self.flushes.append((fl, slow))
+        blk = [f"{slow}:", f"s_cmp_ge_u32 m0, {64 - HG}", f"s_cbranch_scc1 {fl}",
+               f"s_cmp_eq_u32 {T[0]}, 0", f"s_cbranch_scc1 {self.lab(f'DN{i}')}",
+               f"s_cmp_{cmp}_u32 {otop}, {LI}", f"s_cbranch_scc1 {cont}",
+               f"s_branch {self.lab(f'{side}R{i}')}"]
+        self.slow.append(blk)
+        e(f"{cont}:")
+        self.sub(D, T, otopd)
+        e(f"s_cbranch_scc0 {self.lab(f'{side}F{i}')}")
+        self.partial(side, T)
+        self.dispatch((i + 1) % NS, False)
+
+    def write(self, k: str, v, sd: str):
+        e = self.e
+        e(f"s_lshl_b32 {T0}, {k}, 3")
+        e("s_mov_b64 exec, 1")
+        e(f"v_mov_b32 v{VDA}, {T0}")
+        e(f"v_mov_b32 v{VDD}, {v[0]}")
+        e(f"ds_write_b32 v{VDA}, v{VDD} offset:{self.side_off(sd)}")
+
+    def build(self) -> list[str]:
+        e = self.e
+        done = self.lab("DONE")
+        e("s_waitcnt vmcnt(0)")
+        e(f"s_mov_b64 {ADDR}, %[ob]")
+        e(f"s_add_u32 {HC}, %[nh], 1")
+        e(f"s_mov_b32 {JJS}, 0xffffff00")
+        e("s_mov_b32 m0, %[nacc]")
+        e("s_mov_b64 exec, -1")
+        e(f"v_mbcnt_lo_u32_b32 v{VSL}, -1, 0")
+        e(f"v_mbcnt_hi_u32_b32 v{VSL}, -1, v{VSL}")
+        e(f"v_mov_b32 v{VZD}, 0")
+        e(f"s_mov_b32 {ZERO}, 0")
+        e(f"s_mov_b32 {BA}, 0")
+        self.next_top("A")
+        e(f"s_mov_b32 {BB}, {DEEP_CAP - 1}")
+        self.next_top("B")
+        e(f"s_load_dwordx16 s[44:59], {ADDR}, 0x0")
+        e(".p2align 8")
+        for i in range(NS):
+            if i % HG == 0:
+                self.head(i)
+            self.slot(i)
+        for blk in self.slow:
+            for line in blk:
+                e(line)
+        for fl, back in self.flushes:
+            self.emit_flush(fl, back)
+        e(f"{done}:")
+        e("s_waitcnt vmcnt(0) lgkmcnt(0)")
+        self.write(BA, BAD, "A")
+        self.write(BB, BBD, "B")
+        e("s_waitcnt lgkmcnt(0)")
+        e("s_mov_b64 exec, -1")
+        e("s_mov_b32 %[nacc], m0")
+        return self.out
+
+
 ALIGN = int(os.environ.get("GOME_PLAN_ALIGN", "0"))   # log2 byte alignment of branch targets
 
 
@@ -900,13 +1101,15 @@ def main():
     out = sys.argv[1] if len(sys.argv) > 1 else os.path.join(here, "flow_plan_asm.inc")
     with open(out, "w") as f:
         f.write("// Generated by gen_plan_asm.py — do not edit.\n")
-        for w, g in ((64, Gen(64)), (32, Gen(32)), ("32C", GenC())):
+        for w, g in ((64, Gen(64)), (32, Gen(32)), ("32C", GenC()), ("32D", GenD())):
             f.write(f"#define FL_PLAN_ASM{w} \\\n")
             for line in aligned(g.build()):
                 f.write(f'  "{line}\\n\\t" \\\n')
             f.write('  ""\n')
         f.write("#define FL_PLAN_CLOBBERS " + ", ".join(f'"{c}"' for c in CLOBBERS) + "\n")
         f.write("#define FL_PLAN_CLOBBERS_C " + ", ".join(f'"{c}"' for c in CLOBBERS_C) + "\n")
+        f.write("#define FL_PLAN_CLOBBERS_D " + ", ".join(f'"{c}"' for c in CLOBBERS_D) + "\n")
+        f.write(f"#define FL_DEEP_CAP {DEEP_CAP}\n")
 
 
 if __name__ == "__main__":

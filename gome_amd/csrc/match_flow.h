@@ -91,7 +91,7 @@ struct SEnt {        // a touch in its level's run (32 B)
   int64_t amt;
   int64_t coord;     // CONS: cursor before; REST: maker start E (volume coordinates)
   uint32_t t;        // log index
-  uint32_t pad;
+  uint32_t lvl;      // the level (deep books read a touch's level here)
 };
 static_assert(sizeof(SEnt) == 32, "SEnt layout");
 
@@ -125,9 +125,14 @@ struct FlowHdr {
   uint32_t nslot;      // LDS ring entries of the plan (16 B each, the dummy entry included)
   uint32_t ncancel;    // the cancel prep's longest window + 1 (diagnostics)
   uint32_t fc_bad;     // set by the cancel prep: decline the book (legacy / cold kernels)
+  uint32_t deep;       // the lane prep found more levels than FL_MAX: a deep-book candidate
+  uint32_t pad3[3];
 };
-// FlowHdr::ok: 0 declined, FL_OK_ADD an ADD-only flow book, FL_OK_CANCEL a book with DELs
-constexpr uint32_t FL_OK_ADD = 1, FL_OK_CANCEL = 2;
+// FlowHdr::ok: 0 declined, FL_OK_ADD an ADD-only flow book, FL_OK_CANCEL a book with DELs,
+// FL_OK_DEEP an ADD-only head book with more levels than the lane plans hold (match_flow_deep.h)
+constexpr uint32_t FL_OK_ADD = 1, FL_OK_CANCEL = 2, FL_OK_DEEP = 3;
+constexpr uint32_t DEEP_CAP = 16384;     // level slots of a deep book (0 and DEEP_CAP - 1: sentinels)
+constexpr uint32_t DEEP_HASH = 1u << 16; // price-set slots of a deep book (global memory)
 // FlowHdr::fc_bad: why the cancel prep declined a book (bits; diagnostics read them)
 enum : uint32_t {
   FC_BAD_SYM = 1, FC_BAD_TABLE = 2, FC_BAD_Q7 = 4, FC_BAD_Q2 = 8, FC_BAD_LEVEL = 16, FC_BAD_UNIT = 32,
@@ -155,6 +160,8 @@ struct FlowLvl {
   uint32_t cring;    // ring entries of the level (a power of two >= every window + 1)
   uint32_t rbase;    // first ring entry of the level (aligned to cring)
   uint32_t ocan;     // cancelled volume of old makers (plan units), set by the recon
+  uint32_t memf;     // deep books: membership after the batch (M_BUY / M_SALE)
+  uint32_t pad3[3];
 };
 static_assert(sizeof(FlowLvl) % 16 == 0, "FlowLvl alignment");
 
@@ -201,10 +208,21 @@ struct FlowArgs {
   uint32_t* fc_rank;   // [max_batch] per segment position: a targeted ADD's rank in its level
   FcHash* fc_hash;     // (symbol, oid) table of the cancel books' records
   uint64_t fc_hmask;
+  // deep books (match_flow_deep.h): level tables, final level records, price sets, sort scratch
+  FlowLvl* dlvl;       // [FL_HEAD * DEEP_CAP]
+  Level* dlvout;       // [FL_HEAD * DEEP_CAP]
+  unsigned long long* dh_key;  // [FL_HEAD * DEEP_HASH]
+  uint32_t* dh_val;    // [FL_HEAD * DEEP_HASH] level index (after the prep), else old index
+  Touch* tlog;         // the first sort pass's output (the log's index space)
   uint32_t fc_gen;     // batch generation (FcHash entries of older batches are empty)
 };
 
 __device__ __forceinline__ uint32_t fl_hend(const Dev& D, const FlowArgs& F) { return min(F.h1, D.st->nhot); }
+
+// The level table of book h (a deep book's is DEEP_CAP slots in F.dlvl).
+__device__ __forceinline__ FlowLvl* fl_lvls(const FlowArgs& F, uint32_t h) {
+  return F.hdr[h].ok == FL_OK_DEEP ? F.dlvl + static_cast<size_t>(h) * DEEP_CAP : F.lvl + static_cast<size_t>(h) * FL_CAP;
+}
 
 __device__ __forceinline__ uint32_t fl_hash(unsigned long long key) {
   return static_cast<uint32_t>(mix64(key) >> 20) & (FL_HASH - 1);
@@ -401,7 +419,7 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep(Dev D, BatchArgs B, Flo
   const bool w32 = sum < FL_SUM_CAP && sum / g < (1ull << 32);
   if (!w32) g = 1;
   if (dels && !w32) {  // the cancel plan is 32-bit only
-    if (tid == 0) hd->ok = 0;
+    if (tid == 0) { hd->ok = 0; hd->deep = 0; }
     return;
   }
   if (tid < ((8u - ((end - beg) & 7u)) & 7u))  // padding to whole half-groups (8 records)
@@ -465,6 +483,9 @@ struct FlPrepScr {
   uint32_t val[FL_HASH];            // after k_flow_prep_b: level index of each key
   unsigned long long pg[FL_PG], ps[FL_PG];  // per-slice gcd and saturated sum of volumes
   uint32_t adds, dropped, bad, dels;
+  uint32_t many;       // more distinct prices than the lane plans hold: a deep-book candidate
+  // the deep prep's own totals (match_flow_deep.h)
+  uint32_t d_adds, d_dropped, d_dels, d_bad, d_ndist;
 };
 
 __device__ __forceinline__ void fl_slice(uint32_t beg, uint32_t end, uint32_t x, uint32_t& b0, uint32_t& b1) {
@@ -512,7 +533,7 @@ __device__ __forceinline__ void fl_block_gcd_sum(unsigned long long& mg, unsigne
 
 __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep_a(Dev D, BatchArgs B, FlowArgs F) {
   __shared__ unsigned long long hkey[FL_HASH];
-  __shared__ uint32_t ndist, bad, adds, dropped, dels;
+  __shared__ uint32_t ndist, bad, adds, dropped, dels, many;
   __shared__ unsigned long long wg[FL_PREP_T / 64], ws[FL_PREP_T / 64];
   const uint32_t hb = blockIdx.y, h = F.h0 + hb, tid = threadIdx.x;
   if (h >= fl_hend(D, F) || !F.enabled) return;
@@ -521,11 +542,11 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep_a(Dev D, BatchArgs B, F
   uint32_t b0, b1;
   fl_slice(B.seg_start[seg], B.seg_start[seg + 1], blockIdx.x, b0, b1);
   for (uint32_t i = tid; i < FL_HASH; i += FL_PREP_T) hkey[i] = 0;
-  if (tid == 0) ndist = bad = adds = dropped = dels = 0;
+  if (tid == 0) ndist = bad = adds = dropped = dels = many = 0;
   __syncthreads();
   unsigned long long mg = 0, msum = 0;
-  uint32_t my_adds = 0, my_drop = 0, my_bad = 0, my_dels = 0;
-  for (uint32_t c0 = b0 + tid; c0 < b1 && !my_bad; c0 += 4 * FL_PREP_T) {
+  uint32_t my_adds = 0, my_drop = 0, my_bad = 0, my_dels = 0, my_many = 0;
+  for (uint32_t c0 = b0 + tid; c0 < b1 && !my_bad && !my_many; c0 += 4 * FL_PREP_T) {
     Prep qs[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
@@ -547,13 +568,14 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep_a(Dev D, BatchArgs B, F
       msum = min(msum + v, FL_SUM_CAP);
       bool fresh;
       const uint32_t sl = fl_set_put(hkey, static_cast<unsigned long long>(q.price) + FL_KEY_OFF, &fresh);
-      if (sl == FL_HASH || (fresh && atomicAdd(&ndist, 1u) >= FL_MAX)) { my_bad = 1; break; }
+      if (sl == FL_HASH || (fresh && atomicAdd(&ndist, 1u) >= FL_MAX)) { my_many = 1; break; }
     }
   }
   if (my_adds) atomicAdd(&adds, my_adds);
   if (my_drop) atomicAdd(&dropped, my_drop);
   if (my_dels) atomicAdd(&dels, my_dels);
   if (my_bad) bad = 1;
+  if (my_many) many = 1;
   fl_block_gcd_sum(mg, msum, wg, ws);  // (synchronises the block)
   if (tid == 0) {
     P->pg[blockIdx.x] = mg;
@@ -562,12 +584,13 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep_a(Dev D, BatchArgs B, F
     if (dropped) atomicAdd(&P->dropped, dropped);
     if (dels) atomicAdd(&P->dels, dels);
     if (bad) atomicOr(&P->bad, 1u);
+    if (many) atomicOr(&P->many, 1u);
   }
-  if (bad) return;
+  if (bad || many) return;
   for (uint32_t i = tid; i < FL_HASH; i += FL_PREP_T) {
     if (hkey[i]) {
       bool fresh;
-      if (fl_set_put(P->key, hkey[i], &fresh) == FL_HASH) atomicOr(&P->bad, 1u);
+      if (fl_set_put(P->key, hkey[i], &fresh) == FL_HASH) atomicOr(&P->many, 1u);  // (a deep candidate)
     }
   }
 }
@@ -577,7 +600,7 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep_b(Dev D, BatchArgs B, F
   __shared__ uint32_t hval[FL_HASH];
   __shared__ unsigned long long ckey[FL_CAP + FL_PREP_T];
   __shared__ uint32_t cslot[FL_CAP + FL_PREP_T];
-  __shared__ uint32_t ndist, nc, bad;
+  __shared__ uint32_t ndist, nc, bad, deepc;
   __shared__ unsigned long long wg[FL_PREP_T / 64], ws[FL_PREP_T / 64];
   const uint32_t hb = blockIdx.x, h = F.h0 + hb, tid = threadIdx.x;
   if (h >= fl_hend(D, F)) return;
@@ -587,18 +610,22 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep_b(Dev D, BatchArgs B, F
   const uint32_t beg = B.seg_start[seg], end = B.seg_start[seg + 1];
   const uint32_t sym = B.ord[B.sidx[beg]].symbol_id;
   if (D.st->err & ERR_INPUT) {  // (the batch is rejected; sym may be out of range)
-    if (tid == 0) hd->ok = 0;
+    if (tid == 0) { hd->ok = 0; hd->deep = 0; }
     return;
   }
   const Book bk = D.books[sym];
   if (tid == 0) {
     ndist = nc = 0;
-    bad = (!F.enabled || P->bad || (bk.pad & BOOK_QUIRK) || bk.n_lvl > 4 * FL_CAP || (D.st->err & ERR_INPUT) ||
-           (end - beg) >= FL_MAX_ORDERS) ? 1u : 0u;
+    const bool base_bad = !F.enabled || P->bad || (bk.pad & BOOK_QUIRK) || (D.st->err & ERR_INPUT) ||
+                          (end - beg) >= FL_MAX_ORDERS;
+    const bool many = P->many || bk.n_lvl > FL_MAX;
+    // more levels than lanes: the deep plan's candidate (match_flow_deep.h re-checks the rest)
+    deepc = (!base_bad && many && bk.n_lvl <= DEEP_CAP - 2) ? 1u : 0u;
+    bad = (base_bad || many) ? 1u : 0u;
   }
   __syncthreads();
   if (bad) {
-    if (tid == 0) hd->ok = 0;
+    if (tid == 0) { hd->ok = 0; hd->deep = deepc; }
     return;
   }
   uint32_t my_n = 0;
@@ -634,7 +661,7 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep_b(Dev D, BatchArgs B, F
   }
   fl_block_gcd_sum(mg, msum, wg, ws);  // (synchronises the block)
   if (bad || ndist > FL_MAX) {
-    if (tid == 0) hd->ok = 0;
+    if (tid == 0) { hd->ok = 0; hd->deep = (!bad && ndist <= DEEP_CAP - 2) ? 1u : 0u; }
     return;
   }
   for (uint32_t sl = tid; sl < FL_HASH; sl += FL_PREP_T) {
@@ -680,7 +707,7 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep_b(Dev D, BatchArgs B, F
   if (!w32) g = 1;
   const uint32_t dels = P->dels;
   if (dels && !w32) {  // the cancel plan is 32-bit only
-    if (tid == 0) hd->ok = 0;
+    if (tid == 0) { hd->ok = 0; hd->deep = 0; }
     return;
   }
   const uint32_t obase = fl_obase(beg, seg);
@@ -823,6 +850,7 @@ struct FlLog {
 };
 
 #include "flow_plan_asm.inc"
+static_assert(FL_DEEP_CAP == DEEP_CAP, "deep plan generated for another DEEP_CAP");
 
 
 
@@ -845,6 +873,40 @@ __device__ __forceinline__ void fl_ring_load(const FlowArgs& F, uint32_t h) {
   for (uint32_t i = threadIdx.x; i < ns; i += blockDim.x) fl_ring[i] = img[i];
 }
 
+// Deep books: the depth slots (W32 units; bid of level k at byte 8k, ask at 8k + 4) -> LDS by
+// every thread of the block, with the sentinels; back to FlowLvl (dfin, memf) after the plan.
+__device__ __forceinline__ void fl_deep_load(const FlowArgs& F, uint32_t h) {
+  uint32_t* dep = reinterpret_cast<uint32_t*>(fl_ring);
+  const FlowHdr& hd = F.hdr[h];
+  const FlowLvl* LV = fl_lvls(F, h);
+  const unsigned long long g = hd.g;
+  for (uint32_t k = threadIdx.x; k < DEEP_CAP; k += blockDim.x) {
+    uint32_t a = 0, b = 0;
+    if (k >= 1 && k <= hd.nl) {
+      const FlowLvl& f = LV[k];
+      const uint32_t d = static_cast<uint32_t>(static_cast<unsigned long long>(f.d0) / g);
+      if (f.mem0 & M_SALE) a = d;
+      if (f.mem0 & M_BUY) b = d;
+    }
+    if (k == 0) b = 1;
+    if (k == DEEP_CAP - 1) a = 1;
+    dep[2 * k] = b;
+    dep[2 * k + 1] = a;
+  }
+}
+
+__device__ __forceinline__ void fl_deep_store(const FlowArgs& F, uint32_t h) {
+  const uint32_t* dep = reinterpret_cast<const uint32_t*>(fl_ring);
+  const FlowHdr& hd = F.hdr[h];
+  FlowLvl* LV = fl_lvls(F, h);
+  const unsigned long long g = hd.g;
+  for (uint32_t k = 1 + threadIdx.x; k <= hd.nl; k += blockDim.x) {
+    const uint32_t b = dep[2 * k], a = dep[2 * k + 1];
+    LV[k].dfin = static_cast<int64_t>(static_cast<unsigned long long>(a + b) * g);  // (one side is 0)
+    LV[k].memf = (a ? M_SALE : 0u) | (b ? M_BUY : 0u);
+  }
+}
+
 // ring: for books with DELs, 0 any ring, 1 small rings only, 2 large rings only
 template <bool EXCL>
 __device__ __forceinline__ void fl_plan_kernel(const Dev& D, const FlowArgs& F, uint32_t kind, uint32_t ring = 0) {
@@ -852,18 +914,17 @@ __device__ __forceinline__ void fl_plan_kernel(const Dev& D, const FlowArgs& F, 
   const bool mine = h < fl_hend(D, F) && uni(F.hdr[h].ok) == kind &&
                     (ring == 0 || (uni(F.hdr[h].fc_big) != 0) == (ring == 2));
   if (mine && kind == FL_OK_CANCEL) fl_ring_load(F, h);
+  if (mine && kind == FL_OK_DEEP) fl_deep_load(F, h);
   if (EXCL) {
     asm volatile("" ::: "v255", "a255");
     __syncthreads();
-    if (threadIdx.x >= 64) {
-      __syncthreads();
-      return;
-    }
-  } else if (kind == FL_OK_CANCEL) {
+    if (threadIdx.x < 64 && mine) fl_plan_book(D, F, h);
     __syncthreads();
+    if (mine && kind == FL_OK_DEEP) fl_deep_store(F, h);
+    return;
   }
+  if (kind == FL_OK_CANCEL) __syncthreads();
   if (mine) fl_plan_book(D, F, h);
-  if (EXCL) __syncthreads();
 }
 
 // The head's plan (the batch's critical path) and the tail's: distinct names for the profiles.
@@ -881,8 +942,14 @@ __global__ __launch_bounds__(64) void k_flow_plan_tail_c(Dev D, FlowArgs F) { fl
 // tail books with DELs whose ring exceeds FC_TAIL_SLOTS (the largest LDS allocation)
 __global__ __launch_bounds__(64) void k_flow_plan_tail_cb(Dev D, FlowArgs F) { fl_plan_kernel<false>(D, F, FL_OK_CANCEL, 2); }
 
+__device__ __forceinline__ void fl_plan_deep(const Dev& D, const FlowArgs& F, uint32_t h);
+
 __device__ __forceinline__ void fl_plan_book(const Dev& D, const FlowArgs& F, uint32_t h) {
   const FlowHdr* hd = &F.hdr[h];
+  if (uni(hd->ok) == FL_OK_DEEP) {
+    fl_plan_deep(D, F, h);
+    return;
+  }
   __builtin_amdgcn_s_setprio(3);
   const uint32_t lane = lane_id();
   const uint32_t nl = uni(hd->nl), beg = uni(hd->beg), end = uni(hd->end), n = end - beg;
@@ -1001,6 +1068,37 @@ __device__ __forceinline__ void fl_plan_book(const Dev& D, const FlowArgs& F, ui
   }
 }
 
+// The deep plan (gen_plan_asm.py, W32D): depths in LDS (fl_deep_load), touches carry their level
+// in the second word.
+__device__ __forceinline__ void fl_plan_deep(const Dev& D, const FlowArgs& F, uint32_t h) {
+  const FlowHdr* hd = &F.hdr[h];
+  __builtin_amdgcn_s_setprio(3);
+  const uint32_t lane = lane_id();
+  const uint32_t beg = uni(hd->beg), end = uni(hd->end), n = end - beg;
+  FlLog lg{vreg(0u), vreg(0u), vreg(0u), 0u, 0u, 0u, FL_TOUCH_MUL * n, (GOME_GLB v4u*)(F.log + FL_TOUCH_MUL * beg)};
+  const uint32_t nh = (n + 7) / 8;
+  const unsigned long long ob = reinterpret_cast<unsigned long long>(F.ord8 + uni(hd->obase));
+  const unsigned long long logp = reinterpret_cast<unsigned long long>(F.log + FL_TOUCH_MUL * beg);
+  const uint32_t vl16 = lane * 16u;
+  uint32_t voff;
+  const uint32_t vzero = 0;
+  asm volatile(FL_PLAN_ASM32D
+               : [lk] "+v"(lg.lk), [la] "+v"(lg.la), [lb] "+v"(lg.lb), [nacc] "+s"(lg.nacc), [lpos] "+s"(lg.lpos),
+                 [voff] "=&v"(voff)
+               : [ob] "s"(ob), [nh] "s"(nh), [logp] "s"(logp), [lcap] "s"(lg.lcap), [vl16] "v"(vl16),
+                 [vzero] "v"(vzero)
+               : FL_PLAN_CLOBBERS, FL_PLAN_CLOBBERS_D, "scc", "vcc", "memory");
+  if (lg.nacc) {  // {key, level, amount, 0}
+    if (lane < lg.nacc && lg.lpos + lg.nacc <= lg.lcap) lg.p[lg.lpos + lane] = v4(lg.lk, lg.lb, lg.la, 0u);
+    lg.lpos += lg.nacc;
+  }
+  if (lg.lpos > lg.lcap) {
+    if (lane == 0) atomicOr(&D.st->err, ERR_CORRUPT);
+    lg.lpos = 0;
+  }
+  if (lane == 0) F.hdr[h].ntouch = lg.lpos;
+}
+
 // ============================================================== k_flow_sort
 // Stable counting sort of one book's touches by level: histogram -> run bases, then tiles of
 // FL_SORT_T touches ranked within each wave by a 7-bit ballot match (equal levels) and
@@ -1012,7 +1110,7 @@ __global__ __launch_bounds__(FL_SORT_T) void k_flow_sort(Dev D, FlowArgs F) {
   __shared__ uint32_t wc[FL_SORT_W][FL_CAP];
   __shared__ uint32_t nrest;
   const uint32_t h = F.h0 + blockIdx.x, tid = threadIdx.x, w = tid >> 6;
-  if (h >= fl_hend(D, F) || !F.hdr[h].ok) return;
+  if (h >= fl_hend(D, F) || !F.hdr[h].ok || F.hdr[h].ok == FL_OK_DEEP) return;
   const uint32_t nt = F.hdr[h].ntouch, L = FL_TOUCH_MUL * F.hdr[h].beg, nl = F.hdr[h].nl;
   const unsigned long long g = F.hdr[h].g;
   const bool cb = F.hdr[h].ok == FL_OK_CANCEL;
@@ -1075,7 +1173,7 @@ __global__ __launch_bounds__(FL_SORT_T) void k_flow_sort(Dev D, FlowArgs F) {
       e.amt = x.amt;
       e.coord = 0;
       e.t = t;
-      e.pad = 0;
+      e.lvl = k;
       const uint32_t pos = wc[w][k] + rank;
       e.amt = static_cast<int64_t>(static_cast<unsigned long long>(x.amt) * g);  // plan units -> fixed point
       F.srt[L + pos] = e;
@@ -1092,12 +1190,14 @@ __global__ __launch_bounds__(FL_SORT_T) void k_flow_sort(Dev D, FlowArgs F) {
 // One wave per level (waves of a per-book workgroup take the book's levels in turn):
 // volume coordinates of the level's run, then the gather of the consumed prefix of its
 // resting FIFO.
-__device__ __forceinline__ void fl_level_one(const Dev& D, const FlowArgs& F, uint32_t h, uint32_t q) {
+// (run_base / run_cnt: the level's run when the caller found it, deep books; else FlowLvl's)
+__device__ __forceinline__ void fl_level_one(const Dev& D, const FlowArgs& F, uint32_t h, uint32_t q,
+                                             uint32_t run_base = NIL, uint32_t run_cnt = 0) {
   const FlowHdr* hd = &F.hdr[h];
   const uint32_t lane = lane_id();
-  FlowLvl* Lq = &F.lvl[h * FL_CAP + q];
+  FlowLvl* Lq = fl_lvls(F, h) + q;
   const uint32_t L = FL_TOUCH_MUL * uni(hd->beg);
-  const uint32_t base = uni(Lq->base), cnt = uni(Lq->cnt);
+  const uint32_t base = run_base != NIL ? run_base : uni(Lq->base), cnt = run_base != NIL ? run_cnt : uni(Lq->cnt);
   const int64_t d0 = uni64(Lq->d0);
   SEnt* R = F.srt + L + base;
   RsEnt* RS = F.rs + L + base;
@@ -1252,8 +1352,9 @@ struct FlTouchCtx {
 
 __device__ __forceinline__ FlTouchCtx fl_touch_ctx(const FlowArgs& F, uint32_t h, uint32_t L, const Touch& x) {
   FlTouchCtx t;
-  const uint32_t k = x.kr & 127u;
-  t.Lq = &F.lvl[h * FL_CAP + k];
+  const bool deep = F.hdr[h].ok == FL_OK_DEEP;
+  const uint32_t k = deep ? F.srt[L + x.pos].lvl : (x.kr & 127u);
+  t.Lq = fl_lvls(F, h) + k;
   const uint32_t base = t.Lq->base;
   t.IG = F.ig + t.Lq->ig_base;
   t.RS = F.rs + L + base;
@@ -1287,7 +1388,8 @@ __global__ __launch_bounds__(1024) void k_flow_toff(Dev D, FlowArgs F) {
   uint32_t* toff = F.toff + F.tb;
   const uint32_t per = (nb + 1023) / 1024, b0 = tid * per;
   uint32_t s = 0;
-  for (uint32_t i = b0; i < b0 + per && i < nb; ++i) s += hdr[i].ok == KIND ? hdr[i].ntouch : 0u;
+  auto mine = [&](uint32_t ok) { return ok == KIND || (KIND == FL_OK_ADD && ok == FL_OK_DEEP); };
+  for (uint32_t i = b0; i < b0 + per && i < nb; ++i) s += mine(hdr[i].ok) ? hdr[i].ntouch : 0u;
   part[tid] = s;
   __syncthreads();
   if (tid == 0) {
@@ -1299,7 +1401,7 @@ __global__ __launch_bounds__(1024) void k_flow_toff(Dev D, FlowArgs F) {
   uint32_t acc = part[tid];
   for (uint32_t i = b0; i < b0 + per && i < nb; ++i) {
     toff[i] = acc;
-    acc += hdr[i].ok == KIND ? hdr[i].ntouch : 0u;
+    acc += mine(hdr[i].ok) ? hdr[i].ntouch : 0u;
   }
 }
 
@@ -1472,7 +1574,7 @@ __device__ __forceinline__ Level fl_write_level(const Dev& D, const BatchArgs& B
   const uint32_t lane = lane_id();
   const uint32_t L = FL_TOUCH_MUL * hd.beg;
   const unsigned long long mask = D.idx_mask;
-  const FlowLvl f = F.lvl[h * FL_CAP + q];
+  const FlowLvl f = fl_lvls(F, h)[q];
   const RsEnt* RS = F.rs + L + f.base;
   Level x{};
   x.price = f.price;
@@ -1550,8 +1652,12 @@ __device__ __forceinline__ Level fl_write_level(const Dev& D, const BatchArgs& B
   x.depth = f.dfin;
   x.nlive = f.nlive0 + S;
   uint32_t mem = 0;
-  if ((hd.amask[q >> 6] >> (q & 63)) & 1ull) mem |= M_SALE;
-  if ((hd.bmask[q >> 6] >> (q & 63)) & 1ull) mem |= M_BUY;
+  if (hd.ok == FL_OK_DEEP) {
+    mem = f.memf;
+  } else {
+    if ((hd.amask[q >> 6] >> (q & 63)) & 1ull) mem |= M_SALE;
+    if ((hd.bmask[q >> 6] >> (q & 63)) & 1ull) mem |= M_BUY;
+  }
   x.member = static_cast<uint8_t>(mem);
   if (x.nlive == 0) {
     x.hslot = x.tslot = 0;
@@ -1695,7 +1801,7 @@ __global__ __launch_bounds__(FL_TILE) void k_flow_sort_cnt(Dev D, FlowArgs F) {
   __shared__ uint32_t wc[FL_TILE_W][FL_CAP];
   __shared__ uint32_t nrest;
   const uint32_t hb = blockIdx.y, h = F.h0 + hb, tid = threadIdx.x, w = tid >> 6;
-  if (h >= fl_hend(D, F) || !F.hdr[h].ok) return;
+  if (h >= fl_hend(D, F) || !F.hdr[h].ok || F.hdr[h].ok == FL_OK_DEEP) return;
   const uint32_t nt = F.hdr[h].ntouch, L = FL_TOUCH_MUL * F.hdr[h].beg;
   const uint32_t ntile = (nt + FL_TILE - 1) / FL_TILE;
   const bool cb = F.hdr[h].ok == FL_OK_CANCEL;
@@ -1727,7 +1833,7 @@ __global__ __launch_bounds__(FL_TILE) void k_flow_sort_cnt(Dev D, FlowArgs F) {
 __global__ __launch_bounds__(FL_CAP) void k_flow_sort_scan(Dev D, FlowArgs F) {
   __shared__ uint32_t tot[FL_CAP];
   const uint32_t hb = blockIdx.x, h = F.h0 + hb, k = threadIdx.x;
-  if (h >= fl_hend(D, F) || !F.hdr[h].ok) return;
+  if (h >= fl_hend(D, F) || !F.hdr[h].ok || F.hdr[h].ok == FL_OK_DEEP) return;
   const uint32_t nt = F.hdr[h].ntouch, nl = F.hdr[h].nl;
   const uint32_t ntile = (nt + FL_TILE - 1) / FL_TILE;
   uint32_t* tc = F.tcnt + static_cast<size_t>(h) * F.maxt * FL_CAP;
@@ -1771,7 +1877,7 @@ __global__ __launch_bounds__(FL_CAP) void k_flow_sort_scan(Dev D, FlowArgs F) {
 __global__ __launch_bounds__(FL_TILE) void k_flow_sort_scatter(Dev D, FlowArgs F) {
   __shared__ uint32_t wc[FL_TILE_W][FL_CAP];
   const uint32_t hb = blockIdx.y, h = F.h0 + hb, tid = threadIdx.x, w = tid >> 6;
-  if (h >= fl_hend(D, F) || !F.hdr[h].ok) return;
+  if (h >= fl_hend(D, F) || !F.hdr[h].ok || F.hdr[h].ok == FL_OK_DEEP) return;
   const uint32_t nt = F.hdr[h].ntouch, L = FL_TOUCH_MUL * F.hdr[h].beg;
   const unsigned long long g = F.hdr[h].g;
   const bool cb = F.hdr[h].ok == FL_OK_CANCEL;
@@ -1805,7 +1911,7 @@ __global__ __launch_bounds__(FL_TILE) void k_flow_sort_scatter(Dev D, FlowArgs F
       e.amt = static_cast<int64_t>(static_cast<unsigned long long>(x.amt) * g);
       e.coord = 0;
       e.t = t;
-      e.pad = 0;
+      e.lvl = k;
       const uint32_t pos = wc[w][k] + rank;
       F.srt[L + pos] = e;
       F.log[L + t].pos = pos;

@@ -1,0 +1,512 @@
+// match_flow_deep.h — the flow path for deep head books: more price levels than the lane plans
+// hold (FL_MAX), up to DEEP_CAP - 2 (config 5's 4-dp price grid: ~10k levels per book).
+//
+// The matching semantics are the flow path's (match_flow.h): a serial aggregate plan over level
+// depths, then the parallel reconstruction of fills and FIFOs.  What changes with the level
+// count:
+//   k_deep_prep_a/b/c   the price set in a global-memory hash per book (DEEP_HASH slots), sorted
+//                       in LDS (bitonic, one workgroup), old levels merged; FlowLvl in F.dlvl;
+//                       32-bit records with a 14-bit level index (hi = level | SALE << 31)
+//   plan                gen_plan_asm.py W32D: depths in LDS (fl_deep_load / fl_deep_store),
+//                       the next level after an emptied top by 64-slot reads; a touch carries
+//                       its level in Touch::pos
+//   k_deep_sort_*       stable LSD sort of the touches by level, two 7-bit passes through
+//                       F.tlog (each pass the head sort's tile count / scan / scatter)
+//   k_deep_level        per level: its run (binary search of the sorted touches), then
+//                       fl_level_one; count and events are the ADD-only kernels (fl_touch_ctx
+//                       reads a deep touch's level from its sorted entry)
+//   k_deep_write_*      FIFO appends per level, the book's level array compacted by a scan.
+// Declines (the book goes to the legacy kernel, bit-exact as before): DELs in the segment,
+// zero-volume ADDs (Q6), quirk books, more than DEEP_CAP - 2 levels, volumes beyond the 32-bit
+// plan.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "../../include/gome/gome_abi.h"
+#include "device.h"
+#include "match_cold.h"
+#include "match_flow.h"
+#include "pipeline.h"
+#include "wave.h"
+
+namespace gome {
+
+__device__ __forceinline__ uint32_t fd_hash(unsigned long long key) {
+  return static_cast<uint32_t>(mix64(key) >> 16) & (DEEP_HASH - 1);
+}
+
+// Insert key (nonzero) into a book's price set; the slot, or NIL when full.
+__device__ __forceinline__ uint32_t fd_put(unsigned long long* keys, unsigned long long key, bool* fresh) {
+  uint32_t s = fd_hash(key);
+  *fresh = false;
+  for (uint32_t probe = 0; probe < DEEP_HASH; ++probe) {
+    const unsigned long long cur = __hip_atomic_load(&keys[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (cur == key) return s;
+    if (cur == 0ull) {
+      const unsigned long long prev = atomicCAS(&keys[s], 0ull, key);
+      if (prev == 0ull) {
+        *fresh = true;
+        return s;
+      }
+      if (prev == key) return s;
+    }
+    s = (s + 1) & (DEEP_HASH - 1);
+  }
+  return NIL;
+}
+
+__device__ __forceinline__ uint32_t fd_find(const unsigned long long* keys, unsigned long long key) {
+  uint32_t s = fd_hash(key);
+  for (uint32_t probe = 0; probe < DEEP_HASH; ++probe) {
+    const unsigned long long cur = keys[s];
+    if (cur == key) return s;
+    if (cur == 0ull) return NIL;
+    s = (s + 1) & (DEEP_HASH - 1);
+  }
+  return NIL;
+}
+
+__device__ __forceinline__ bool fd_candidate(const Dev& D, const FlowArgs& F, uint32_t h) {
+  return h < fl_hend(D, F) && h < FL_HEAD && F.hdr[h].deep && !F.hdr[h].ok;
+}
+
+// ---- prep a: per slice, the batch's prices into the set, gcd / sum, counts ----------------
+__global__ __launch_bounds__(FL_PREP_T) void k_deep_prep_a(Dev D, BatchArgs B, FlowArgs F) {
+  __shared__ uint32_t adds, dropped, dels, bad, nd;
+  __shared__ unsigned long long wg[FL_PREP_T / 64], ws[FL_PREP_T / 64];
+  const uint32_t hb = blockIdx.y, h = F.h0 + hb, tid = threadIdx.x;
+  if (!fd_candidate(D, F, h)) return;
+  FlPrepScr* P = F.pscr + hb;
+  unsigned long long* keys = F.dh_key + static_cast<size_t>(h) * DEEP_HASH;
+  const uint32_t seg = B.seg_order[h];
+  uint32_t b0, b1;
+  fl_slice(B.seg_start[seg], B.seg_start[seg + 1], blockIdx.x, b0, b1);
+  if (tid == 0) adds = dropped = dels = bad = nd = 0;
+  __syncthreads();
+  unsigned long long mg = 0, msum = 0;
+  uint32_t my_adds = 0, my_drop = 0, my_dels = 0, my_bad = 0, my_nd = 0;
+  for (uint32_t b = b0 + tid; b < b1; b += FL_PREP_T) {
+    const Prep q = prep_at(B, b);
+    if (q.action == GOME_DEL) { my_dels++; continue; }
+    if (q.action != GOME_ADD) continue;
+    my_adds++;
+    if (!q.adm) { my_drop++; continue; }
+    if (q.vol == 0) { my_bad = 1; continue; }  // a zero-volume maker (Q6)
+    const unsigned long long v = static_cast<unsigned long long>(q.vol);
+    mg = fl_gcd(mg, v);
+    msum = min(msum + v, FL_SUM_CAP);
+    bool fresh;
+    if (fd_put(keys, static_cast<unsigned long long>(q.price) + FL_KEY_OFF, &fresh) == NIL) my_bad = 1;
+    my_nd += fresh ? 1u : 0u;
+  }
+  if (my_adds) atomicAdd(&adds, my_adds);
+  if (my_drop) atomicAdd(&dropped, my_drop);
+  if (my_dels) atomicAdd(&dels, my_dels);
+  if (my_bad) bad = 1;
+  if (my_nd) atomicAdd(&nd, my_nd);
+  fl_block_gcd_sum(mg, msum, wg, ws);  // (synchronises the block)
+  if (tid == 0) {
+    P->pg[blockIdx.x] = mg;
+    P->ps[blockIdx.x] = msum;
+    if (adds) atomicAdd(&P->d_adds, adds);
+    if (dropped) atomicAdd(&P->d_dropped, dropped);
+    if (dels) atomicAdd(&P->d_dels, dels);
+    if (bad) atomicOr(&P->d_bad, 1u);
+    if (nd) atomicAdd(&P->d_ndist, nd);
+  }
+}
+
+// ---- prep b: old levels into the set, the sorted level table, the header -----------------
+// Dynamic LDS: DEEP_CAP keys (the sort).
+__global__ __launch_bounds__(FL_PREP_T) void k_deep_prep_b(Dev D, BatchArgs B, FlowArgs F) {
+  __shared__ uint32_t bad, ndist, nc;
+  __shared__ unsigned long long wg[FL_PREP_T / 64], ws[FL_PREP_T / 64];
+  const uint32_t hb = blockIdx.x, h = F.h0 + hb, tid = threadIdx.x;
+  if (!fd_candidate(D, F, h)) return;
+  FlowHdr* hd = &F.hdr[h];
+  FlPrepScr* P = F.pscr + hb;
+  unsigned long long* keys = F.dh_key + static_cast<size_t>(h) * DEEP_HASH;
+  uint32_t* vals = F.dh_val + static_cast<size_t>(h) * DEEP_HASH;
+  const uint32_t seg = B.seg_order[h];
+  const uint32_t beg = B.seg_start[seg], end = B.seg_start[seg + 1];
+  const uint32_t sym = B.ord[B.sidx[beg]].symbol_id;
+  const Book bk = D.books[sym];
+  if (tid == 0) {
+    // ADD-only for now: a segment with DELs keeps the legacy kernel
+    bad = (P->d_bad || P->d_dels || (bk.pad & BOOK_QUIRK) || bk.n_lvl > DEEP_CAP - 2) ? 1u : 0u;
+    ndist = P->d_ndist;
+    nc = 0;
+  }
+  __syncthreads();
+  if (bad) {
+    if (tid == 0) hd->deep = 0;
+    return;
+  }
+  const Level* L0 = D.lvl + bk.lvl_base;
+  unsigned long long mg = 0, msum = 0;
+  if (tid < FL_PG) {
+    mg = P->pg[tid];
+    msum = P->ps[tid];
+  }
+  for (uint32_t k = tid; k < bk.n_lvl; k += FL_PREP_T) {
+    const Level x = L0[k];
+    const uint32_t nm = (x.member & M_BUY ? 1u : 0u) + (x.member & M_SALE ? 1u : 0u);
+    if (x.nlive == 0) {
+      if (x.depth != 0 || x.member != 0) bad = 1;
+      continue;
+    }
+    if (x.depth <= 0 || nm != 1) { bad = 1; continue; }
+    mg = fl_gcd(mg, static_cast<unsigned long long>(x.depth));
+    msum = min(msum + static_cast<unsigned long long>(x.depth), FL_SUM_CAP);
+    bool fresh;
+    const uint32_t sl = fd_put(keys, static_cast<unsigned long long>(x.price) + FL_KEY_OFF, &fresh);
+    if (sl == NIL) { bad = 1; continue; }
+    vals[sl] = k;  // the old level (vals start NIL)
+    if (fresh) atomicAdd(&ndist, 1u);
+  }
+  fl_block_gcd_sum(mg, msum, wg, ws);  // (synchronises the block)
+  const unsigned long long g = mg ? mg : 1;
+  const bool w32 = msum < FL_SUM_CAP && msum / g < (1ull << 32);
+  if (bad || ndist > DEEP_CAP - 2 || !w32) {
+    if (tid == 0) hd->deep = 0;
+    return;
+  }
+  // the set's keys, sorted (bitonic over the next power of two)
+  const uint32_t n = ndist;
+  uint32_t np = 1024;
+  while (np < n) np <<= 1;
+  unsigned long long* sk = reinterpret_cast<unsigned long long*>(fl_ring);
+  for (uint32_t sl = tid; sl < DEEP_HASH; sl += FL_PREP_T) {
+    const unsigned long long key = keys[sl];
+    if (key) sk[atomicAdd(&nc, 1u)] = key;
+  }
+  __syncthreads();
+  for (uint32_t i = n + tid; i < np; i += FL_PREP_T) sk[i] = ~0ull;
+  __syncthreads();
+  for (uint32_t k = 2; k <= np; k <<= 1) {
+    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+      for (uint32_t i = tid; i < np; i += FL_PREP_T) {
+        const uint32_t p = i ^ j;
+        if (p > i) {
+          const unsigned long long a = sk[i], b = sk[p];
+          if ((a > b) == ((i & k) == 0)) {
+            sk[i] = b;
+            sk[p] = a;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  // level r + 1 = the r-th price; the set maps price -> level from here on
+  FlowLvl* LV = F.dlvl + static_cast<size_t>(h) * DEEP_CAP;
+  for (uint32_t r = tid; r < n; r += FL_PREP_T) {
+    const unsigned long long key = sk[r];
+    const uint32_t sl = fd_find(keys, key);
+    const uint32_t old = vals[sl];
+    FlowLvl f{};
+    f.price = static_cast<int64_t>(key - FL_KEY_OFF);
+    f.old = old;
+    f.head = f.tail = NIL;
+    if (old != NIL) {
+      const Level x = L0[old];
+      f.d0 = x.depth;
+      f.nv0 = x.nlive;
+      f.head = x.head;
+      f.tail = x.tail;
+      f.hslot = x.hslot;
+      f.tslot = x.tslot;
+      f.mem0 = x.member;
+    }
+    LV[r + 1] = f;
+    vals[sl] = r + 1;
+  }
+  const uint32_t obase = fl_obase(beg, seg);
+  if (tid < ((8u - ((end - beg) & 7u)) & 7u)) F.ord8[obase + (end - beg) + tid] = 0ull;  // no-op padding
+  if (tid == 0) {
+    FlowHdr x{};
+    x.ok = FL_OK_DEEP;
+    x.nl = n;
+    x.sym = sym;
+    x.beg = beg;
+    x.end = end;
+    x.nold = bk.n_lvl;
+    x.adds = P->d_adds;
+    x.dropped = P->d_dropped;
+    x.obase = obase;
+    x.w32 = 1;
+    x.g = g;
+    x.deep = 1;
+    *hd = x;
+  }
+}
+
+// ---- prep c: the 32-bit records (level index from the set) ---------------------------------
+__global__ __launch_bounds__(FL_PREP_T) void k_deep_prep_c(Dev D, BatchArgs B, FlowArgs F) {
+  const uint32_t hb = blockIdx.y, h = F.h0 + hb, tid = threadIdx.x;
+  if (h >= fl_hend(D, F) || h >= FL_HEAD || F.hdr[h].ok != FL_OK_DEEP) return;
+  const FlowHdr* hd = &F.hdr[h];
+  const unsigned long long* keys = F.dh_key + static_cast<size_t>(h) * DEEP_HASH;
+  const uint32_t* vals = F.dh_val + static_cast<size_t>(h) * DEEP_HASH;
+  const uint32_t beg = hd->beg, obase = hd->obase;
+  const unsigned long long g = hd->g;
+  uint32_t b0, b1;
+  fl_slice(beg, hd->end, blockIdx.x, b0, b1);
+  for (uint32_t b = b0 + tid; b < b1; b += FL_PREP_T) {
+    const Prep q = prep_at(B, b);
+    unsigned long long rec = 0ull;  // no-op: a rest of 0 at the bid sentinel
+    if (q.action == GOME_ADD && q.adm) {
+      const uint32_t li = vals[fd_find(keys, static_cast<unsigned long long>(q.price) + FL_KEY_OFF)];
+      const unsigned long long v = static_cast<unsigned long long>(static_cast<double>(q.vol) / static_cast<double>(g));
+      rec = (static_cast<unsigned long long>(li | (q.side == GOME_SALE ? 0x80000000u : 0u)) << 32) | v;
+    }
+    F.ord8[obase + (b - beg)] = rec;
+    B.ev_count[q.idx] = 0;
+  }
+}
+
+// ---- sort: two stable 7-bit passes by level (tile counts, per-book scan, scatter) ---------
+// PASS 1 reads the plan's log (level in Touch::pos) and writes F.tlog in low-7-bit order, the
+// touch's log index in the amount's high word; PASS 2 writes the level-ordered SEnt runs.
+template <int PASS>
+__device__ __forceinline__ uint32_t fd_key(const FlowArgs& F, uint32_t L, uint32_t t, Touch& x) {
+  x = (PASS == 1 ? F.log : F.tlog)[L + t];
+  return PASS == 1 ? (x.pos & 127u) : (x.pos >> 7);
+}
+
+template <int PASS>
+__global__ __launch_bounds__(FL_TILE) void k_deep_sort_cnt(Dev D, FlowArgs F) {
+  __shared__ uint32_t wc[FL_TILE_W][FL_CAP];
+  __shared__ uint32_t nrest;
+  const uint32_t hb = blockIdx.y, h = F.h0 + hb, tid = threadIdx.x, w = tid >> 6;
+  if (h >= fl_hend(D, F) || F.hdr[h].ok != FL_OK_DEEP) return;
+  const uint32_t nt = F.hdr[h].ntouch, L = FL_TOUCH_MUL * F.hdr[h].beg;
+  const uint32_t ntile = (nt + FL_TILE - 1) / FL_TILE;
+  for (uint32_t tl = blockIdx.x; tl < ntile; tl += gridDim.x) {
+    for (uint32_t i = tid; i < FL_TILE_W * FL_CAP; i += FL_TILE) wc[i / FL_CAP][i % FL_CAP] = 0;
+    if (tid == 0) nrest = 0;
+    __syncthreads();
+    const uint32_t t = tl * FL_TILE + tid;
+    const bool valid = t < nt;
+    Touch x{};
+    const uint32_t k = valid ? fd_key<PASS>(F, L, t, x) : 0u;
+    uint32_t cnt;
+    const uint32_t rank = fl_tile_rank(k, valid, cnt);
+    if (valid && rank == 0) wc[w][k] = cnt;
+    if (PASS == 1) {
+      const unsigned long long rm = __ballot(valid && ((x.kr >> 7) & 1u) == TK_REST && x.pos != 0);
+      if (lane_id() == 0 && rm) atomicAdd(&nrest, static_cast<uint32_t>(__popcll(rm)));
+    }
+    __syncthreads();
+    if (tid < FL_CAP) {
+      uint32_t c = 0;
+      for (uint32_t ww = 0; ww < FL_TILE_W; ++ww) c += wc[ww][tid];
+      F.tcnt[(static_cast<size_t>(h) * F.maxt + tl) * FL_CAP + tid] = c;
+    }
+    if (PASS == 1 && tid == 0 && nrest) atomicAdd(&F.hdr[h].rests, nrest);
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(FL_CAP) void k_deep_sort_scan(Dev D, FlowArgs F) {
+  __shared__ uint32_t tot[FL_CAP];
+  const uint32_t hb = blockIdx.x, h = F.h0 + hb, k = threadIdx.x;
+  if (h >= fl_hend(D, F) || F.hdr[h].ok != FL_OK_DEEP) return;
+  const uint32_t nt = F.hdr[h].ntouch;
+  const uint32_t ntile = (nt + FL_TILE - 1) / FL_TILE;
+  uint32_t* tc = F.tcnt + static_cast<size_t>(h) * F.maxt * FL_CAP;
+  uint32_t s = 0;
+  for (uint32_t tl = 0; tl < ntile; ++tl) s += tc[tl * FL_CAP + k];
+  tot[k] = s;
+  __syncthreads();
+  if (k == 0) {
+    uint32_t acc = 0;
+    for (uint32_t i = 0; i < FL_CAP; ++i) { const uint32_t v = tot[i]; tot[i] = acc; acc += v; }
+  }
+  __syncthreads();
+  uint32_t run = tot[k];
+  for (uint32_t tl = 0; tl < ntile; ++tl) {
+    const uint32_t v = tc[tl * FL_CAP + k];
+    tc[tl * FL_CAP + k] = run;
+    run += v;
+  }
+}
+
+template <int PASS>
+__global__ __launch_bounds__(FL_TILE) void k_deep_sort_scatter(Dev D, FlowArgs F) {
+  __shared__ uint32_t wc[FL_TILE_W][FL_CAP];
+  const uint32_t hb = blockIdx.y, h = F.h0 + hb, tid = threadIdx.x, w = tid >> 6;
+  if (h >= fl_hend(D, F) || F.hdr[h].ok != FL_OK_DEEP) return;
+  const uint32_t nt = F.hdr[h].ntouch, L = FL_TOUCH_MUL * F.hdr[h].beg;
+  const unsigned long long g = F.hdr[h].g;
+  const uint32_t ntile = (nt + FL_TILE - 1) / FL_TILE;
+  const uint32_t* tc = F.tcnt + static_cast<size_t>(h) * F.maxt * FL_CAP;
+  for (uint32_t i = tid; i < FL_TILE_W * FL_CAP; i += FL_TILE) wc[i / FL_CAP][i % FL_CAP] = 0;
+  __syncthreads();
+  for (uint32_t tl = blockIdx.x; tl < ntile; tl += gridDim.x) {
+    const uint32_t t = tl * FL_TILE + tid;
+    const bool valid = t < nt;
+    Touch x{};
+    const uint32_t k = valid ? fd_key<PASS>(F, L, t, x) : 0u;
+    uint32_t cnt;
+    const uint32_t rank = fl_tile_rank(k, valid, cnt);
+    if (valid && rank == 0) wc[w][k] = cnt;
+    __syncthreads();
+    if (tid < FL_CAP) {
+      uint32_t r = tc[tl * FL_CAP + tid];
+      for (uint32_t ww = 0; ww < FL_TILE_W; ++ww) {
+        const uint32_t c = wc[ww][tid];
+        wc[ww][tid] = r;
+        r += c;
+      }
+    }
+    __syncthreads();
+    if (valid) {
+      const uint32_t pos = wc[w][k] + rank;
+      const unsigned long long a = static_cast<unsigned long long>(x.amt);
+      if (PASS == 1) {
+        Touch y = x;
+        y.amt = static_cast<int64_t>((a & 0xFFFFFFFFull) | (static_cast<unsigned long long>(t) << 32));
+        F.tlog[L + pos] = y;
+      } else {
+        const uint32_t t0 = static_cast<uint32_t>(a >> 32);  // the touch's log index
+        SEnt e;
+        e.j = tk_j(x);
+        e.kind = (x.kr >> 7) & 1u;
+        e.amt = static_cast<int64_t>((a & 0xFFFFFFFFull) * g);  // plan units -> fixed point
+        e.coord = 0;
+        e.t = t0;
+        e.lvl = x.pos;
+        F.srt[L + pos] = e;
+        F.log[L + t0].pos = pos;
+        F.log[L + t0].amt = e.amt;
+      }
+    }
+    __syncthreads();
+    for (uint32_t i = tid; i < FL_TILE_W * FL_CAP; i += FL_TILE) wc[i / FL_CAP][i % FL_CAP] = 0;
+    __syncthreads();
+  }
+}
+
+// ---- levels: the run of each level, then the ADD-only level reconstruction -----------------
+// First index in srt[L, L + nt) whose level is >= q (wave-wide 64-ary search).
+__device__ __forceinline__ uint32_t fd_lower(const SEnt* R, uint32_t nt, uint32_t q) {
+  const uint32_t lane = lane_id();
+  uint32_t lo = 0, hi = nt;
+  while (hi - lo > 64) {
+    const uint32_t step = (hi - lo + 63) / 64;
+    const uint32_t i = lo + lane * step;
+    const bool v = i < hi;
+    const bool below = v && R[i].lvl < q;
+    const uint32_t ns = __popcll(__ballot(v)), c = __popcll(__ballot(below));
+    const uint32_t nlo = c ? lo + (c - 1) * step + 1 : lo;
+    const uint32_t nhi = c < ns ? lo + c * step + 1 : hi;
+    lo = nlo;
+    hi = min(nhi, hi);
+  }
+  const uint32_t i = lo + lane;
+  return lo + __popcll(__ballot(i < hi && R[i].lvl < q));
+}
+
+constexpr uint32_t DEEP_GRID = 1024;  // workgroups per deep book in the per-level kernels
+
+__global__ __launch_bounds__(64) void k_deep_level(Dev D, FlowArgs F) {
+  const uint32_t h = F.h0 + blockIdx.y;
+  if (h >= fl_hend(D, F) || F.hdr[h].ok != FL_OK_DEEP) return;
+  const uint32_t nl = F.hdr[h].nl, nt = F.hdr[h].ntouch, L = FL_TOUCH_MUL * F.hdr[h].beg;
+  FlowLvl* LV = fl_lvls(F, h);
+  for (uint32_t q = 1 + blockIdx.x; q <= nl; q += gridDim.x) {
+    const uint32_t b = fd_lower(F.srt + L, nt, q), e = fd_lower(F.srt + L, nt, q + 1);
+    if (lane_id() == 0) {
+      LV[q].base = b;
+      LV[q].cnt = e - b;
+    }
+    fl_level_one(D, F, h, q, b, e - b);
+  }
+}
+
+// ---- write: FIFO appends per level, then the level array ------------------------------------
+__global__ __launch_bounds__(64) void k_deep_write_lv(Dev D, BatchArgs B, FlowArgs F) {
+  const uint32_t h = F.h0 + blockIdx.y;
+  if (h >= fl_hend(D, F) || F.hdr[h].ok != FL_OK_DEEP) return;
+  const FlowHdr hd = F.hdr[h];
+  for (uint32_t q = 1 + blockIdx.x; q <= hd.nl; q += gridDim.x) {
+    const Level x = fl_write_level(D, B, F, hd, h, q);
+    if (lane_id() == 0) F.dlvout[static_cast<size_t>(h) * DEEP_CAP + q] = x;
+  }
+}
+
+constexpr uint32_t DEEP_FIN_T = 1024, DEEP_FIN_PER = DEEP_CAP / DEEP_FIN_T;
+
+__global__ __launch_bounds__(DEEP_FIN_T) void k_deep_write_fin(Dev D, FlowArgs F) {
+  __shared__ uint32_t part[DEEP_FIN_T];
+  __shared__ uint32_t base_s, cap_s, nout_s;
+  const uint32_t h = F.h0 + blockIdx.x, tid = threadIdx.x;
+  if (h >= fl_hend(D, F) || F.hdr[h].ok != FL_OK_DEEP) return;
+  const FlowHdr hd = F.hdr[h];
+  const Level* lv = F.dlvout + static_cast<size_t>(h) * DEEP_CAP;
+  // levels q0 .. q0 + DEEP_FIN_PER - 1 per thread (1-based)
+  const uint32_t q0 = 1 + tid * DEEP_FIN_PER;
+  uint32_t c = 0;
+  for (uint32_t u = 0; u < DEEP_FIN_PER; ++u) {
+    const uint32_t q = q0 + u;
+    if (q <= hd.nl && lv[q].nlive > 0) ++c;
+  }
+  part[tid] = c;
+  __syncthreads();
+  if (tid == 0) {
+    uint32_t acc = 0;
+    for (uint32_t i = 0; i < DEEP_FIN_T; ++i) { const uint32_t v = part[i]; part[i] = acc; acc += v; }
+    const uint32_t nout = acc;
+    nout_s = nout;
+    const Book bk = D.books[hd.sym];
+    uint32_t base = bk.lvl_base, cap = bk.lvl_cap;
+    if (nout > cap) {
+      uint32_t ncap = 16;
+      while (ncap < nout) ncap <<= 1;
+      const uint32_t nb = lvl_block_alloc(D, ncap);
+      if (nb == NIL) {
+        atomicOr(&D.st->err, ERR_LEVELS);
+        cap = 0;
+      } else {
+        lvl_block_release(D, base, cap);
+        base = nb;
+        cap = ncap;
+      }
+    }
+    base_s = base;
+    cap_s = cap;
+    if (nout <= cap) {
+      Book nb;
+      nb.lvl_base = base;
+      nb.n_lvl = nout;
+      nb.lvl_cap = cap;
+      nb.pad = 0;
+      D.books[hd.sym] = nb;
+    }
+    unsigned long long* ct = D.st->ctr;
+    atomicAdd(&ct[C_RESTS], static_cast<unsigned long long>(hd.rests));
+    atomicAdd(&ct[C_HOT_RESTS], static_cast<unsigned long long>(hd.rests));
+    atomicAdd(&ct[C_RESTING_DELTA], static_cast<unsigned long long>(hd.rests));
+    atomicAdd(&ct[C_ADD], static_cast<unsigned long long>(hd.adds));
+    atomicAdd(&ct[C_DROPPED], static_cast<unsigned long long>(hd.dropped));
+    atomicAdd(&ct[C_LEVELS_DELTA], static_cast<unsigned long long>(static_cast<long long>(nout) - hd.nold));
+    atomicAdd(&ct[C_HOT_ORDERS], static_cast<unsigned long long>(hd.end - hd.beg));
+    atomicAdd(&ct[C_FLOW_BOOKS], 1ull);
+    atomicAdd(&ct[C_FLOW_ORDERS], static_cast<unsigned long long>(hd.end - hd.beg));
+    atomicAdd(&ct[C_FLOW_TOUCHES], static_cast<unsigned long long>(hd.ntouch));
+    if (F.h0 == 0) {
+      atomicAdd(&ct[C_FLOW_HEAD_ORDERS], static_cast<unsigned long long>(hd.end - hd.beg));
+      atomicAdd(&ct[C_FLOW_HEAD_TOUCHES], static_cast<unsigned long long>(hd.ntouch));
+    }
+  }
+  __syncthreads();
+  if (nout_s > cap_s) return;  // (ERR_LEVELS)
+  uint32_t o = part[tid];
+  for (uint32_t u = 0; u < DEEP_FIN_PER; ++u) {
+    const uint32_t q = q0 + u;
+    if (q <= hd.nl && lv[q].nlive > 0) D.lvl[base_s + o++] = lv[q];
+  }
+}
+
+}  // namespace gome

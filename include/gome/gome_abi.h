@@ -219,7 +219,7 @@ gome_status gome_get_stats(const gome_engine* e, gome_stats* out);
 /* Diagnostics (tests, tuning): the last batch's hot-book routing, GOME_DEBUG_FLOW_WORDS words
  * per candidate book, longest segment first: {flow kind (0 legacy / cold, 1 ADD-only flow,
  * 2 flow with cancels), cancel-prep decline bits, symbol, orders, DELs, levels, 32-bit plan,
- * ring entries needed, longest cancel window + 1, 0}.  *n_out = candidates written (<= cap). */
+ * ring entries needed, longest cancel window + 1, deep-book candidate}.  *n_out = candidates written (<= cap). */
 #define GOME_DEBUG_FLOW_WORDS 10
 gome_status gome_debug_flow_books(gome_engine* e, uint32_t* out, size_t cap, size_t* n_out);
 /* Diagnostics: raw bytes [offset, offset + bytes) of one of the flow path's device scratch

@@ -306,7 +306,7 @@ gome_status gome_engine::init(const gome_config& c) {
     fc_ring_lds = F.fc_ring_cap * 16;
     if (fc_ring_lds < DEEP_CAP * 8) return fail(GOME_E_DEVICE, "device LDS per workgroup below 128 KiB");
     for (const void* k : {reinterpret_cast<const void*>(k_flow_plan_head), reinterpret_cast<const void*>(k_flow_plan_near),
-                          reinterpret_cast<const void*>(k_flow_plan_tail_cb)})
+                          reinterpret_cast<const void*>(k_flow_plan_tail_cb), reinterpret_cast<const void*>(k_flow_plan_tail_d)})
       HIPCHK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(fc_ring_lds)));
     HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_deep_prep_b), hipFuncAttributeMaxDynamicSharedMemorySize,
                                static_cast<int>(DEEP_CAP * 8)));
@@ -408,13 +408,22 @@ gome_status gome_engine::init(const gome_config& c) {
       !alloc(&F.fc_hash, fc_hcap, "flow cancel table"))
     return GOME_E_CAPACITY;
   HIPCHK(hipMemsetAsync(F.fc_hash, 0, sizeof(FcHash) * fc_hcap, stream));
-  // deep head books (match_flow_deep.h)
-  if (!alloc(&F.dlvl, static_cast<size_t>(FL_HEAD) * DEEP_CAP, "deep level tables") ||
-      !alloc(&F.dlvout, static_cast<size_t>(FL_HEAD) * DEEP_CAP, "deep final levels") ||
-      !alloc(&F.dh_key, static_cast<size_t>(FL_HEAD) * DEEP_HASH, "deep price sets") ||
-      !alloc(&F.dh_val, static_cast<size_t>(FL_HEAD) * DEEP_HASH, "deep price levels") ||
+  // deep books (match_flow_deep.h): per deep slot
+  F.dmaxt = F.maxt;
+  F.dtmaxt = ceil_div(F.maxt, 8);
+  if (!alloc(&F.dlvl, static_cast<size_t>(DEEP_SLOTS) * DEEP_CAP, "deep level tables") ||
+      !alloc(&F.dlvout, static_cast<size_t>(DEEP_SLOTS) * DEEP_CAP, "deep final levels") ||
+      !alloc(&F.dh_key, static_cast<size_t>(DEEP_SLOTS) * DEEP_HASH, "deep price sets") ||
+      !alloc(&F.dh_val, static_cast<size_t>(DEEP_SLOTS) * DEEP_HASH, "deep price levels") ||
+      !alloc(&F.dscr, DEEP_SLOTS, "deep prep scratch") ||
+      !alloc(&F.dtcnt, (static_cast<size_t>(FL_HEAD) * F.dmaxt + static_cast<size_t>(DEEP_SLOTS - FL_HEAD) * F.dtmaxt) * FL_CAP,
+             "deep sort tile counts") ||
+      !alloc(&F.dslot_h, DEEP_SLOTS, "deep slot books") ||
       !alloc(&F.tlog, ntouch, "deep sort pass"))
     return GOME_E_CAPACITY;
+  // the price sets start empty; each batch's deep books clear theirs when done
+  HIPCHK(hipMemsetAsync(F.dh_key, 0, sizeof(unsigned long long) * DEEP_SLOTS * DEEP_HASH, stream));
+  HIPCHK(hipMemsetAsync(F.dh_val, 0xFF, sizeof(uint32_t) * DEEP_SLOTS * DEEP_HASH, stream));
   HIPCHK(hipMemsetAsync(F.hdr, 0, sizeof(FlowHdr) * MAX_FLOW, stream));
   HIPCHK(hipMemsetAsync(d_pend, 0, sizeof(PendEnt) * nb, stream));
   if (D.idx_mask >= PEND) return fail(GOME_E_INVAL, "gome_config.max_nodes too large (index > 2^31 slots)");
@@ -542,6 +551,8 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   FH0.h0 = 0; FH0.h1 = 1; FH0.tb = 0;
   FH1.h0 = 1; FH1.h1 = FL_HEAD; FH1.tb = 2;
   FT.h0 = FL_HEAD; FT.h1 = MAX_FLOW; FT.tb = FL_HEAD + 3;
+  FH.ds0 = 0; FH.ds1 = FL_HEAD; FH0.ds0 = 0; FH0.ds1 = 1; FH1.ds0 = 1; FH1.ds1 = FL_HEAD;
+  FT.ds0 = FL_HEAD; FT.ds1 = DEEP_SLOTS;
   // the ranges' books with DELs count and place their events through a second toff region
   FlowArgs FH0c = FH0, FH1c = FH1, FTc = FT;
   FH0c.tb += FC_TOFF; FH1c.tb += FC_TOFF; FTc.tb += FC_TOFF;
@@ -551,6 +562,9 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   // the head's prep gathers through the sort permutation (prep_at): it starts right after
   // segmentation, beside k_prep
   HIPCHK(hipMemsetAsync(F.fc_img_bump, 0, 4, s));  // (both ranges' cancel preps follow)
+  // deep books: slots, price sets and prep scratch of both ranges
+  HIPCHK(hipMemsetAsync(F.dslot_h, 0xFF, 4 * DEEP_SLOTS, s));
+  HIPCHK(hipMemsetAsync(F.dscr, 0, sizeof(FlPrepScr) * DEEP_SLOTS, s));
   HIPCHK(hipEventRecord(seg_done, s));
   HIPCHK(hipStreamWaitEvent(flow_stream, seg_done, 0));
   HIPCHK(hipMemsetAsync(F.pscr, 0, sizeof(FlPrepScr) * FL_HEAD, flow_stream));
@@ -558,11 +572,13 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   k_flow_prep_b<<<nh_head, FL_PREP_T, 0, flow_stream>>>(D, B, FH);
   k_flow_prep_c<<<dim3(FL_PG, nh_head), FL_PREP_T, 0, flow_stream>>>(D, B, FH);
   // head books with more levels than lanes: the deep prep (match_flow_deep.h)
-  HIPCHK(hipMemsetAsync(F.dh_key, 0, sizeof(unsigned long long) * FL_HEAD * DEEP_HASH, flow_stream));
-  HIPCHK(hipMemsetAsync(F.dh_val, 0xFF, sizeof(uint32_t) * FL_HEAD * DEEP_HASH, flow_stream));
-  k_deep_prep_a<<<dim3(FL_PG, nh_head), FL_PREP_T, 0, flow_stream>>>(D, B, FH);
-  k_deep_prep_b<<<nh_head, FL_PREP_T, DEEP_CAP * 8, flow_stream>>>(D, B, FH);
-  k_deep_prep_c<<<dim3(FL_PG, nh_head), FL_PREP_T, 0, flow_stream>>>(D, B, FH);
+  auto deep_prep = [&](const FlowArgs& R, uint32_t px, hipStream_t st) {
+    const uint32_t ns = R.ds1 - R.ds0;
+    k_deep_prep_a<<<dim3(px, ns), FL_PREP_T, 0, st>>>(D, B, R);
+    k_deep_prep_b<<<ns, FL_PREP_T, DEEP_CAP * 8, st>>>(D, B, R);
+    k_deep_prep_c<<<dim3(px, ns), FL_PREP_T, 0, st>>>(D, B, R);
+  };
+  deep_prep(FH, FL_PG, flow_stream);
   // books with DELs: targets, windows, ring images, W32C records (or back to the legacy path)
   auto cancel_prep = [&](const FlowArgs& R, uint32_t nb, uint32_t px, bool wide, hipStream_t st) {
     k_fc_hash_claim<<<dim3(px, nb), 256, 0, st>>>(D, B, R);
@@ -593,26 +609,34 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   HIPCHK(hipMemsetAsync(F.ig_bump, 0, 4, s));
   HIPCHK(hipEventRecord(fork, s));
   HIPCHK(hipStreamWaitEvent(flow_stream, fork, 0));  // (k_prep, the gather bump)
+  // deep books: the two-pass level sort and the per-level reconstruction, then the writes
+  auto deep_sort_level = [&](const FlowArgs& R, uint32_t tiles, hipStream_t st) {
+    const uint32_t ns = R.ds1 - R.ds0;
+    k_deep_sort_cnt<1><<<dim3(tiles, ns), FL_TILE, 0, st>>>(D, R);
+    k_deep_sort_scan<<<ns, FL_CAP, 0, st>>>(D, R);
+    k_deep_sort_scatter<1><<<dim3(tiles, ns), FL_TILE, 0, st>>>(D, R);
+    k_deep_sort_cnt<2><<<dim3(tiles, ns), FL_TILE, 0, st>>>(D, R);
+    k_deep_sort_scan<<<ns, FL_CAP, 0, st>>>(D, R);
+    k_deep_sort_scatter<2><<<dim3(tiles, ns), FL_TILE, 0, st>>>(D, R);
+    k_deep_level<<<dim3(DEEP_GRID, ns), 64, 0, st>>>(D, R);
+  };
+  auto deep_write = [&](const FlowArgs& R, hipStream_t st) {
+    const uint32_t ns = R.ds1 - R.ds0;
+    k_deep_write_lv<<<dim3(DEEP_GRID, ns), 64, 0, st>>>(D, B, R);
+    k_deep_write_fin<<<ns, DEEP_FIN_T, 0, st>>>(D, R);
+  };
   // the hottest book's reconstruction: wide kernels (tile-parallel sort, one wave per level)
   auto head_recon = [&](const FlowArgs& R, uint32_t nb, hipStream_t st) {
     k_flow_sort_cnt<<<dim3(FL_SORT_GRID, nb), FL_TILE, 0, st>>>(D, R);
     k_flow_sort_scan<<<nb, FL_CAP, 0, st>>>(D, R);
     k_flow_sort_scatter<<<dim3(FL_SORT_GRID, nb), FL_TILE, 0, st>>>(D, R);
-    // deep books: the two-pass level sort and the per-level reconstruction
-    k_deep_sort_cnt<1><<<dim3(FL_SORT_GRID, nb), FL_TILE, 0, st>>>(D, R);
-    k_deep_sort_scan<<<nb, FL_CAP, 0, st>>>(D, R);
-    k_deep_sort_scatter<1><<<dim3(FL_SORT_GRID, nb), FL_TILE, 0, st>>>(D, R);
-    k_deep_sort_cnt<2><<<dim3(FL_SORT_GRID, nb), FL_TILE, 0, st>>>(D, R);
-    k_deep_sort_scan<<<nb, FL_CAP, 0, st>>>(D, R);
-    k_deep_sort_scatter<2><<<dim3(FL_SORT_GRID, nb), FL_TILE, 0, st>>>(D, R);
+    deep_sort_level(R, FL_SORT_GRID, st);
     k_flow_level_wide<<<dim3(FL_CAP, nb), 64, 0, st>>>(D, R);
-    k_deep_level<<<dim3(DEEP_GRID, nb), 64, 0, st>>>(D, R);
     k_flow_toff<FL_OK_ADD><<<1, 1024, 0, st>>>(D, R);
     k_flow_count<<<1024, 256, 0, st>>>(D, B, R);
     k_flow_write_lv<<<dim3(FL_CAP, nb), 64, 0, st>>>(D, B, R);
     k_flow_write_fin<<<nb, 128, 0, st>>>(D, R);
-    k_deep_write_lv<<<dim3(DEEP_GRID, nb), 64, 0, st>>>(D, B, R);
-    k_deep_write_fin<<<nb, DEEP_FIN_T, 0, st>>>(D, R);
+    deep_write(R, st);
   };
   // books with DELs (match_flow_cancel.h); their events go to the arena
   auto head_recon_c = [&](const FlowArgs& R, const FlowArgs& Rc, uint32_t nb, hipStream_t st) {
@@ -632,16 +656,20 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   HIPCHK(hipStreamWaitEvent(hot_stream, fork, 0));
   if (nh_tail) {
     k_flow_prep<<<nh_tail, FL_PREP_T, 0, hot_stream>>>(D, B, FT);
+    deep_prep(FT, 8, hot_stream);
     cancel_prep(FT, nh_tail, 1, false, hot_stream);
     HIPCHK(hipEventRecord(prep_t, hot_stream));
     k_flow_plan_tail<<<nh_tail, 64, 0, hot_stream>>>(D, FT);
     k_flow_plan_tail_c<<<nh_tail, 64, FC_TAIL_LDS, hot_stream>>>(D, FT);
     k_flow_plan_tail_cb<<<nh_tail, 64, fc_ring_lds, hot_stream>>>(D, FT);
+    k_flow_plan_tail_d<<<nh_tail, 256, fc_ring_lds, hot_stream>>>(D, FT);
     k_flow_sort<<<nh_tail, FL_SORT_T, 0, hot_stream>>>(D, FT);
     k_flow_level<<<nh_tail, FL_LEVEL_T, 0, hot_stream>>>(D, FT);
+    deep_sort_level(FT, 32, hot_stream);
     k_flow_toff<FL_OK_ADD><<<1, 1024, 0, hot_stream>>>(D, FT);
     k_flow_count<<<1024, 256, 0, hot_stream>>>(D, B, FT);
     k_flow_write<<<nh_tail, FL_WRITE_T, 0, hot_stream>>>(D, B, FT);
+    deep_write(FT, hot_stream);
     // the tail's events into the arena now (k_ev_scatter places them after the scan)
     k_flow_events_arena<<<1024, 256, 0, hot_stream>>>(D, B, FT);
     k_fc_level_book<<<nh_tail, 1024, 0, hot_stream>>>(D, FT);

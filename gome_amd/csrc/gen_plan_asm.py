@@ -891,7 +891,9 @@ class GenC(Gen):
 # word (Touch::pos, read by the deep sort).
 DEEP_CAP = 16384
 VDA, VDD, VSA, VSD, VSL, VZD = 36, 37, 38, 39, 40, 41     # add address / data, scan address /
-CLOBBERS_D = [f"v{i}" for i in range(36, 42)]             # data, lane id, zero
+SCAN_CHUNKS = int(os.environ.get("GOME_DEEP_CHUNKS", "8"))
+VSD2 = (39,) + tuple(range(42, 42 + SCAN_CHUNKS - 1))     # data (SCAN_CHUNKS x 64 slots per step),
+CLOBBERS_D = [f"v{i}" for i in range(36, 42 + SCAN_CHUNKS - 1)]  # lane id, zero
 
 
 class GenD(Gen):
@@ -950,11 +952,14 @@ class GenD(Gen):
 
     def next_top(self, sd: str):
         """After the cached top of side sd emptied: the next level of that side (asks: the lowest
-        nonzero slot above BA, bids: the highest below BB), 64 slots per step; its slot := 0."""
+        nonzero slot above BA, bids: the highest below BB), SCAN_CHUNKS x 64 slots per step (one
+        LDS round trip); its slot := 0."""
         e = self.e
         top, topd = (BA, BAD) if sd == "A" else (BB, BBD)
-        loop, found = self.fresh("NT"), self.fresh("NF")
+        loop, done = self.fresh("NT"), self.fresh("ND")
         off = self.side_off(sd)
+        span = 64 * SCAN_CHUNKS
+        # asks: chunk c covers levels T0 + 64c + lane; bids: T0 - 64c + lane (T0 = BB - 64 first)
         if sd == "A":
             e(f"s_add_u32 {T0}, {BA}, 1")
         else:
@@ -963,24 +968,48 @@ class GenD(Gen):
         e("s_mov_b64 exec, -1")
         e(f"v_add_u32 v{VSA}, {T0}, v{VSL}")
         e(f"v_lshlrev_b32 v{VSA}, 3, v{VSA}")
-        e(f"ds_read_b32 v{VSD}, v{VSA} offset:{off}")
+        for c in range(SCAN_CHUNKS):
+            o = off + (512 * c if sd == "A" else 0)
+            if sd == "A":
+                e(f"ds_read_b32 v{VSD2[c]}, v{VSA} offset:{o}")
+            elif c == 0:
+                e(f"ds_read_b32 v{VSD2[c]}, v{VSA} offset:{off}")
+        if sd == "B":   # downward chunks need negative offsets: separate addresses
+            for c in range(1, SCAN_CHUNKS):
+                e(f"v_subrev_u32 v{VDA}, {512 * c}, v{VSA}")
+                e(f"ds_read_b32 v{VSD2[c]}, v{VDA} offset:{off}")
         e("s_waitcnt lgkmcnt(0)")
-        e(f"v_cmp_ne_u32_e64 {M}, 0, v{VSD}")
-        if sd == "A":
-            e(f"s_ff1_i32_b64 {O[0]}, {M}")
-        else:
-            e(f"s_flbit_i32_b64 {O[0]}, {M}")
-        e(f"s_cmp_lt_i32 {O[0]}, 0")
-        e(f"s_cbranch_scc0 {found}")
-        e(f"s_{'add' if sd == 'A' else 'sub'}_u32 {T0}, {T0}, 64")
+        founds = []
+        for c in range(SCAN_CHUNKS):
+            f = self.fresh(f"NF{c}_")
+            founds.append(f)
+            e(f"v_cmp_ne_u32_e64 {M}, 0, v{VSD2[c]}")
+            if sd == "A":
+                e(f"s_ff1_i32_b64 {O[0]}, {M}")
+            else:
+                e(f"s_flbit_i32_b64 {O[0]}, {M}")
+            e(f"s_cmp_lt_i32 {O[0]}, 0")
+            e(f"s_cbranch_scc0 {f}")
+        e(f"s_{'add' if sd == 'A' else 'sub'}_u32 {T0}, {T0}, {span}")
         e(f"s_branch {loop}")
-        e(f"{found}:")
-        if sd == "B":
-            e(f"s_sub_u32 {O[0]}, 63, {O[0]}")
-        e(f"s_add_u32 {top}, {T0}, {O[0]}")
-        e(f"v_readlane_b32 {topd[0]}, v{VSD}, {O[0]}")
-        e(f"s_lshl_b64 exec, 1, {O[0]}")
-        e(f"ds_write_b32 v{VSA}, v{VZD} offset:{off}")
+        for c in range(SCAN_CHUNKS):
+            e(f"{founds[c]}:")
+            if sd == "B":
+                e(f"s_sub_u32 {O[0]}, 63, {O[0]}")
+            e(f"s_{'add' if sd == 'A' else 'sub'}_u32 {T0}, {T0}, {64 * c}")
+            e(f"s_add_u32 {top}, {T0}, {O[0]}")
+            e(f"v_readlane_b32 {topd[0]}, v{VSD2[c]}, {O[0]}")
+            e(f"s_lshl_b64 exec, 1, {O[0]}")
+            if sd == "A":
+                e(f"ds_write_b32 v{VSA}, v{VZD} offset:{off + 512 * c}")
+            elif c == 0:
+                e(f"ds_write_b32 v{VSA}, v{VZD} offset:{off}")
+            else:
+                e(f"v_subrev_u32 v{VDA}, {512 * c}, v{VSA}")
+                e(f"ds_write_b32 v{VDA}, v{VZD} offset:{off}")
+            if c != SCAN_CHUNKS - 1:
+                e(f"s_branch {done}")
+        e(f"{done}:")
 
     def rest(self, side: str, T):
         """As the 32-bit rest, with the lane add replaced by an LDS add at slot (L, side)."""

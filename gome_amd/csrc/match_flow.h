@@ -126,13 +126,15 @@ struct FlowHdr {
   uint32_t ncancel;    // the cancel prep's longest window + 1 (diagnostics)
   uint32_t fc_bad;     // set by the cancel prep: decline the book (legacy / cold kernels)
   uint32_t deep;       // the lane prep found more levels than FL_MAX: a deep-book candidate
-  uint32_t pad3[3];
+  uint32_t dslot;      // its deep slot (= h; candidates from DEEP_SLOTS on are never deep)
+  uint32_t pad3[2];
 };
 // FlowHdr::ok: 0 declined, FL_OK_ADD an ADD-only flow book, FL_OK_CANCEL a book with DELs,
 // FL_OK_DEEP an ADD-only head book with more levels than the lane plans hold (match_flow_deep.h)
 constexpr uint32_t FL_OK_ADD = 1, FL_OK_CANCEL = 2, FL_OK_DEEP = 3;
 constexpr uint32_t DEEP_CAP = 16384;     // level slots of a deep book (0 and DEEP_CAP - 1: sentinels)
 constexpr uint32_t DEEP_HASH = 1u << 16; // price-set slots of a deep book (global memory)
+constexpr uint32_t DEEP_SLOTS = 256;     // candidates 0..DEEP_SLOTS-1 may be deep books (slot = candidate)
 // FlowHdr::fc_bad: why the cancel prep declined a book (bits; diagnostics read them)
 enum : uint32_t {
   FC_BAD_SYM = 1, FC_BAD_TABLE = 2, FC_BAD_Q7 = 4, FC_BAD_Q2 = 8, FC_BAD_LEVEL = 16, FC_BAD_UNIT = 32,
@@ -208,11 +210,17 @@ struct FlowArgs {
   uint32_t* fc_rank;   // [max_batch] per segment position: a targeted ADD's rank in its level
   FcHash* fc_hash;     // (symbol, oid) table of the cancel books' records
   uint64_t fc_hmask;
-  // deep books (match_flow_deep.h): level tables, final level records, price sets, sort scratch
-  FlowLvl* dlvl;       // [FL_HEAD * DEEP_CAP]
-  Level* dlvout;       // [FL_HEAD * DEEP_CAP]
-  unsigned long long* dh_key;  // [FL_HEAD * DEEP_HASH]
-  uint32_t* dh_val;    // [FL_HEAD * DEEP_HASH] level index (after the prep), else old index
+  // deep books (match_flow_deep.h), per deep slot: level tables, final level records, price
+  // sets, prep scratch, sort tile counts
+  FlowLvl* dlvl;       // [DEEP_SLOTS * DEEP_CAP]
+  Level* dlvout;       // [DEEP_SLOTS * DEEP_CAP]
+  unsigned long long* dh_key;  // [DEEP_SLOTS * DEEP_HASH]
+  uint32_t* dh_val;    // [DEEP_SLOTS * DEEP_HASH] level index (after the prep), else old index
+  struct FlPrepScr* dscr;  // [DEEP_SLOTS]
+  uint32_t* dtcnt;     // sort tile counts: FL_CAP per tile, dmaxt tiles per head slot, dtmaxt per tail slot
+  uint32_t dmaxt, dtmaxt;
+  uint32_t* dslot_h;   // [DEEP_SLOTS] the book of each deep slot this batch (NIL: none)
+  uint32_t ds0, ds1;   // the deep slots a launch covers (the range's)
   Touch* tlog;         // the first sort pass's output (the log's index space)
   uint32_t fc_gen;     // batch generation (FcHash entries of older batches are empty)
 };
@@ -221,7 +229,8 @@ __device__ __forceinline__ uint32_t fl_hend(const Dev& D, const FlowArgs& F) { r
 
 // The level table of book h (a deep book's is DEEP_CAP slots in F.dlvl).
 __device__ __forceinline__ FlowLvl* fl_lvls(const FlowArgs& F, uint32_t h) {
-  return F.hdr[h].ok == FL_OK_DEEP ? F.dlvl + static_cast<size_t>(h) * DEEP_CAP : F.lvl + static_cast<size_t>(h) * FL_CAP;
+  return F.hdr[h].ok == FL_OK_DEEP ? F.dlvl + static_cast<size_t>(F.hdr[h].dslot) * DEEP_CAP
+                                   : F.lvl + static_cast<size_t>(h) * FL_CAP;
 }
 
 __device__ __forceinline__ uint32_t fl_hash(unsigned long long key) {
@@ -265,7 +274,7 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep(Dev D, BatchArgs B, Flo
   __shared__ uint32_t hval[FL_HASH];
   __shared__ unsigned long long ckey[FL_CAP + FL_PREP_T];
   __shared__ uint32_t cslot[FL_CAP + FL_PREP_T];
-  __shared__ uint32_t ndist, nc, bad, adds, dropped, dels;
+  __shared__ uint32_t ndist, nc, bad, adds, dropped, dels, many;
   __shared__ unsigned long long wg[FL_PREP_T / 64], ws[FL_PREP_T / 64];
   const uint32_t h = F.h0 + blockIdx.x, tid = threadIdx.x;
   if (h >= fl_hend(D, F)) return;
@@ -274,15 +283,15 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep(Dev D, BatchArgs B, Flo
   const uint32_t beg = B.seg_start[seg], end = B.seg_start[seg + 1];
   const uint32_t sym = B.ord[B.prep[beg].idx].symbol_id;
   if (D.st->err & ERR_INPUT) {  // (the batch is rejected; sym may be out of range)
-    if (tid == 0) hd->ok = 0;
+    if (tid == 0) { hd->ok = 0; hd->deep = 0; }
     return;
   }
   const Book bk = D.books[sym];
   for (uint32_t i = tid; i < FL_HASH; i += FL_PREP_T) { hkey[i] = 0; hval[i] = NIL; }
   if (tid == 0) {
     ndist = nc = adds = dropped = dels = 0;
-    bad = (!F.enabled || (bk.pad & BOOK_QUIRK) || bk.n_lvl > 4 * FL_CAP || (D.st->err & ERR_INPUT) ||
-           (end - beg) >= FL_MAX_ORDERS) ? 1u : 0u;
+    bad = (!F.enabled || (bk.pad & BOOK_QUIRK) || (D.st->err & ERR_INPUT) || (end - beg) >= FL_MAX_ORDERS) ? 1u : 0u;
+    many = bk.n_lvl > FL_MAX ? 1u : 0u;  // more levels than lanes: a deep candidate
   }
   __syncthreads();
   auto insert = [&](unsigned long long key, uint32_t val) {
@@ -299,7 +308,7 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep(Dev D, BatchArgs B, Flo
       const unsigned long long prev = atomicCAS(&hkey[s], 0ull, key);
       if (prev == 0ull) {
         if (val != NIL) hval[s] = val;
-        if (atomicAdd(&ndist, 1u) >= FL_MAX) bad = 1;
+        if (atomicAdd(&ndist, 1u) >= FL_MAX) many = 1;
         return;
       }
       if (prev == key) {
@@ -308,12 +317,12 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep(Dev D, BatchArgs B, Flo
       }
       s = (s + 1) & (FL_HASH - 1);
     }
-    bad = 1;
+    many = 1;
   };
   // live levels of the book (clean invariant: live <=> nodes, positive depth, one side)
   const Level* L0 = D.lvl + bk.lvl_base;
   unsigned long long mg = 0, msum = 0;  // gcd and (saturating) sum of every volume the plan sees
-  if (!bad) {
+  if (!bad && !many) {
     for (uint32_t k = tid; k < bk.n_lvl; k += FL_PREP_T) {
       const Level x = L0[k];
       const uint32_t nm = (x.member & M_BUY ? 1u : 0u) + (x.member & M_SALE ? 1u : 0u);
@@ -330,9 +339,9 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep(Dev D, BatchArgs B, Flo
   __syncthreads();
   // the segment's orders
   uint32_t my_adds = 0, my_drop = 0, my_dels = 0;
-  if (!bad) {
+  if (!bad && !many) {
     // 4 independent record loads in flight per thread (one block per book is latency-bound)
-    for (uint32_t b0 = beg + tid; b0 < end && !bad; b0 += 4 * FL_PREP_T) {
+    for (uint32_t b0 = beg + tid; b0 < end && !bad && !many; b0 += 4 * FL_PREP_T) {
       Prep qs[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
@@ -355,7 +364,7 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep(Dev D, BatchArgs B, Flo
       }
       msum = min(msum + static_cast<unsigned long long>(q.vol), FL_SUM_CAP);
       insert(static_cast<unsigned long long>(q.price) + FL_KEY_OFF, NIL);
-      if (bad) break;
+      if (bad || many) break;
       }
     }
   }
@@ -368,8 +377,15 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep(Dev D, BatchArgs B, Flo
   }
   if (lane_id() == 0) { wg[tid >> 6] = mg; ws[tid >> 6] = msum; }
   __syncthreads();
-  if (bad || ndist > FL_MAX) {
-    if (tid == 0) hd->ok = 0;
+  if (bad || many || ndist > FL_MAX) {
+    if (tid == 0) {
+      hd->ok = 0;
+      // too many levels for the lanes: a deep book if a deep slot is free (match_flow_deep.h)
+      const uint32_t slot = (!bad && bk.n_lvl <= DEEP_CAP - 2 && h < DEEP_SLOTS) ? h : NIL;
+      hd->deep = slot != NIL ? 1u : 0u;
+      hd->dslot = slot;
+      if (slot != NIL) F.dslot_h[slot] = h;
+    }
     return;
   }
   // compact the set, rank-sort it (<= FL_CAP keys)
@@ -625,7 +641,12 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep_b(Dev D, BatchArgs B, F
   }
   __syncthreads();
   if (bad) {
-    if (tid == 0) { hd->ok = 0; hd->deep = deepc; }
+    if (tid == 0) {
+      hd->ok = 0;
+      hd->deep = deepc;
+      hd->dslot = h;
+      if (deepc) F.dslot_h[h] = h;
+    }
     return;
   }
   uint32_t my_n = 0;
@@ -661,7 +682,12 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep_b(Dev D, BatchArgs B, F
   }
   fl_block_gcd_sum(mg, msum, wg, ws);  // (synchronises the block)
   if (bad || ndist > FL_MAX) {
-    if (tid == 0) { hd->ok = 0; hd->deep = (!bad && ndist <= DEEP_CAP - 2) ? 1u : 0u; }
+    if (tid == 0) {
+      hd->ok = 0;
+      hd->deep = (!bad && ndist <= DEEP_CAP - 2) ? 1u : 0u;
+      hd->dslot = h;
+      if (hd->deep) F.dslot_h[h] = h;
+    }
     return;
   }
   for (uint32_t sl = tid; sl < FL_HASH; sl += FL_PREP_T) {
@@ -941,6 +967,8 @@ __global__ __launch_bounds__(64) void k_flow_plan_tail(Dev D, FlowArgs F) { fl_p
 __global__ __launch_bounds__(64) void k_flow_plan_tail_c(Dev D, FlowArgs F) { fl_plan_kernel<false>(D, F, FL_OK_CANCEL, 1); }
 // tail books with DELs whose ring exceeds FC_TAIL_SLOTS (the largest LDS allocation)
 __global__ __launch_bounds__(64) void k_flow_plan_tail_cb(Dev D, FlowArgs F) { fl_plan_kernel<false>(D, F, FL_OK_CANCEL, 2); }
+// deep tail books (depths in LDS: a whole CU each, like the head)
+__global__ __launch_bounds__(256) void k_flow_plan_tail_d(Dev D, FlowArgs F) { fl_plan_kernel<true>(D, F, FL_OK_DEEP); }
 
 __device__ __forceinline__ void fl_plan_deep(const Dev& D, const FlowArgs& F, uint32_t h);
 

@@ -66,21 +66,60 @@ __device__ __forceinline__ uint32_t fd_find(const unsigned long long* keys, unsi
   return NIL;
 }
 
+// The book of deep slot ds (launches cover the slots [ds0, ds1) of their range), NIL if none.
+__device__ __forceinline__ uint32_t fd_book(const Dev& D, const FlowArgs& F, uint32_t i) {
+  const uint32_t ds = F.ds0 + i;
+  if (ds >= F.ds1) return NIL;
+  const uint32_t h = F.dslot_h[ds];
+  return (h != NIL && h < fl_hend(D, F) && F.hdr[h].dslot == ds) ? h : NIL;
+}
+
+// A deep slot's sort tile counts (seg_order is longest first: candidate h has at most
+// 1 / (h + 1) of the batch, so a tail slot needs at most an eighth of the head's tiles).
+__device__ __forceinline__ uint32_t* fd_tcnt(const FlowArgs& F, uint32_t ds) {
+  const size_t t = ds < FL_HEAD ? static_cast<size_t>(ds) * F.dmaxt
+                                : static_cast<size_t>(FL_HEAD) * F.dmaxt + static_cast<size_t>(ds - FL_HEAD) * F.dtmaxt;
+  return F.dtcnt + t * FL_CAP;
+}
+__device__ __forceinline__ uint32_t fd_tiles(const FlowArgs& F, uint32_t ds) { return ds < FL_HEAD ? F.dmaxt : F.dtmaxt; }
+
+// A slot's price set back to empty (kept clean between batches instead of a per-batch memset).
+__device__ __forceinline__ void fd_clear(const FlowArgs& F, uint32_t ds) {
+  unsigned long long* keys = F.dh_key + static_cast<size_t>(ds) * DEEP_HASH;
+  uint32_t* vals = F.dh_val + static_cast<size_t>(ds) * DEEP_HASH;
+  for (uint32_t i = threadIdx.x; i < DEEP_HASH; i += blockDim.x) {
+    keys[i] = 0ull;
+    vals[i] = NIL;
+  }
+}
+
 __device__ __forceinline__ bool fd_candidate(const Dev& D, const FlowArgs& F, uint32_t h) {
-  return h < fl_hend(D, F) && h < FL_HEAD && F.hdr[h].deep && !F.hdr[h].ok;
+  return h != NIL && F.hdr[h].deep && !F.hdr[h].ok;
+}
+
+__device__ __forceinline__ bool fd_deep(const FlowArgs& F, uint32_t h) {
+  return h != NIL && F.hdr[h].ok == FL_OK_DEEP;
+}
+
+// Slice x of nx of [beg, end).
+__device__ __forceinline__ void fd_slice(uint32_t beg, uint32_t end, uint32_t x, uint32_t nx, uint32_t& b0, uint32_t& b1) {
+  const uint64_t len = end - beg;
+  b0 = beg + static_cast<uint32_t>(len * x / nx);
+  b1 = beg + static_cast<uint32_t>(len * (x + 1) / nx);
 }
 
 // ---- prep a: per slice, the batch's prices into the set, gcd / sum, counts ----------------
 __global__ __launch_bounds__(FL_PREP_T) void k_deep_prep_a(Dev D, BatchArgs B, FlowArgs F) {
   __shared__ uint32_t adds, dropped, dels, bad, nd;
   __shared__ unsigned long long wg[FL_PREP_T / 64], ws[FL_PREP_T / 64];
-  const uint32_t hb = blockIdx.y, h = F.h0 + hb, tid = threadIdx.x;
+  const uint32_t h = fd_book(D, F, blockIdx.y), tid = threadIdx.x;
   if (!fd_candidate(D, F, h)) return;
-  FlPrepScr* P = F.pscr + hb;
-  unsigned long long* keys = F.dh_key + static_cast<size_t>(h) * DEEP_HASH;
+  const uint32_t ds = F.hdr[h].dslot;
+  FlPrepScr* P = F.dscr + ds;
+  unsigned long long* keys = F.dh_key + static_cast<size_t>(ds) * DEEP_HASH;
   const uint32_t seg = B.seg_order[h];
   uint32_t b0, b1;
-  fl_slice(B.seg_start[seg], B.seg_start[seg + 1], blockIdx.x, b0, b1);
+  fd_slice(B.seg_start[seg], B.seg_start[seg + 1], blockIdx.x, gridDim.x, b0, b1);
   if (tid == 0) adds = dropped = dels = bad = nd = 0;
   __syncthreads();
   unsigned long long mg = 0, msum = 0;
@@ -121,25 +160,28 @@ __global__ __launch_bounds__(FL_PREP_T) void k_deep_prep_a(Dev D, BatchArgs B, F
 __global__ __launch_bounds__(FL_PREP_T) void k_deep_prep_b(Dev D, BatchArgs B, FlowArgs F) {
   __shared__ uint32_t bad, ndist, nc;
   __shared__ unsigned long long wg[FL_PREP_T / 64], ws[FL_PREP_T / 64];
-  const uint32_t hb = blockIdx.x, h = F.h0 + hb, tid = threadIdx.x;
+  const uint32_t h = fd_book(D, F, blockIdx.x), tid = threadIdx.x;
   if (!fd_candidate(D, F, h)) return;
   FlowHdr* hd = &F.hdr[h];
-  FlPrepScr* P = F.pscr + hb;
-  unsigned long long* keys = F.dh_key + static_cast<size_t>(h) * DEEP_HASH;
-  uint32_t* vals = F.dh_val + static_cast<size_t>(h) * DEEP_HASH;
+  const uint32_t ds = hd->dslot;
+  FlPrepScr* P = F.dscr + ds;
+  unsigned long long* keys = F.dh_key + static_cast<size_t>(ds) * DEEP_HASH;
+  uint32_t* vals = F.dh_val + static_cast<size_t>(ds) * DEEP_HASH;
   const uint32_t seg = B.seg_order[h];
   const uint32_t beg = B.seg_start[seg], end = B.seg_start[seg + 1];
   const uint32_t sym = B.ord[B.sidx[beg]].symbol_id;
   const Book bk = D.books[sym];
   if (tid == 0) {
     // ADD-only for now: a segment with DELs keeps the legacy kernel
-    bad = (P->d_bad || P->d_dels || (bk.pad & BOOK_QUIRK) || bk.n_lvl > DEEP_CAP - 2) ? 1u : 0u;
+    const uint64_t tiles = (static_cast<uint64_t>(FL_TOUCH_MUL) * (end - beg) + FL_TILE - 1) / FL_TILE;
+    bad = (P->d_bad || P->d_dels || (bk.pad & BOOK_QUIRK) || bk.n_lvl > DEEP_CAP - 2 || tiles > fd_tiles(F, ds)) ? 1u : 0u;
     ndist = P->d_ndist;
     nc = 0;
   }
   __syncthreads();
   if (bad) {
     if (tid == 0) hd->deep = 0;
+    fd_clear(F, ds);
     return;
   }
   const Level* L0 = D.lvl + bk.lvl_base;
@@ -169,6 +211,7 @@ __global__ __launch_bounds__(FL_PREP_T) void k_deep_prep_b(Dev D, BatchArgs B, F
   const bool w32 = msum < FL_SUM_CAP && msum / g < (1ull << 32);
   if (bad || ndist > DEEP_CAP - 2 || !w32) {
     if (tid == 0) hd->deep = 0;
+    fd_clear(F, ds);
     return;
   }
   // the set's keys, sorted (bitonic over the next power of two)
@@ -199,7 +242,7 @@ __global__ __launch_bounds__(FL_PREP_T) void k_deep_prep_b(Dev D, BatchArgs B, F
     }
   }
   // level r + 1 = the r-th price; the set maps price -> level from here on
-  FlowLvl* LV = F.dlvl + static_cast<size_t>(h) * DEEP_CAP;
+  FlowLvl* LV = F.dlvl + static_cast<size_t>(ds) * DEEP_CAP;
   for (uint32_t r = tid; r < n; r += FL_PREP_T) {
     const unsigned long long key = sk[r];
     const uint32_t sl = fd_find(keys, key);
@@ -237,21 +280,22 @@ __global__ __launch_bounds__(FL_PREP_T) void k_deep_prep_b(Dev D, BatchArgs B, F
     x.w32 = 1;
     x.g = g;
     x.deep = 1;
+    x.dslot = ds;
     *hd = x;
   }
 }
 
 // ---- prep c: the 32-bit records (level index from the set) ---------------------------------
 __global__ __launch_bounds__(FL_PREP_T) void k_deep_prep_c(Dev D, BatchArgs B, FlowArgs F) {
-  const uint32_t hb = blockIdx.y, h = F.h0 + hb, tid = threadIdx.x;
-  if (h >= fl_hend(D, F) || h >= FL_HEAD || F.hdr[h].ok != FL_OK_DEEP) return;
+  const uint32_t h = fd_book(D, F, blockIdx.y), tid = threadIdx.x;
+  if (!fd_deep(F, h)) return;
   const FlowHdr* hd = &F.hdr[h];
-  const unsigned long long* keys = F.dh_key + static_cast<size_t>(h) * DEEP_HASH;
-  const uint32_t* vals = F.dh_val + static_cast<size_t>(h) * DEEP_HASH;
+  const unsigned long long* keys = F.dh_key + static_cast<size_t>(hd->dslot) * DEEP_HASH;
+  const uint32_t* vals = F.dh_val + static_cast<size_t>(hd->dslot) * DEEP_HASH;
   const uint32_t beg = hd->beg, obase = hd->obase;
   const unsigned long long g = hd->g;
   uint32_t b0, b1;
-  fl_slice(beg, hd->end, blockIdx.x, b0, b1);
+  fd_slice(beg, hd->end, blockIdx.x, gridDim.x, b0, b1);
   for (uint32_t b = b0 + tid; b < b1; b += FL_PREP_T) {
     const Prep q = prep_at(B, b);
     unsigned long long rec = 0ull;  // no-op: a rest of 0 at the bid sentinel
@@ -278,8 +322,8 @@ template <int PASS>
 __global__ __launch_bounds__(FL_TILE) void k_deep_sort_cnt(Dev D, FlowArgs F) {
   __shared__ uint32_t wc[FL_TILE_W][FL_CAP];
   __shared__ uint32_t nrest;
-  const uint32_t hb = blockIdx.y, h = F.h0 + hb, tid = threadIdx.x, w = tid >> 6;
-  if (h >= fl_hend(D, F) || F.hdr[h].ok != FL_OK_DEEP) return;
+  const uint32_t h = fd_book(D, F, blockIdx.y), tid = threadIdx.x, w = tid >> 6;
+  if (!fd_deep(F, h)) return;
   const uint32_t nt = F.hdr[h].ntouch, L = FL_TOUCH_MUL * F.hdr[h].beg;
   const uint32_t ntile = (nt + FL_TILE - 1) / FL_TILE;
   for (uint32_t tl = blockIdx.x; tl < ntile; tl += gridDim.x) {
@@ -301,7 +345,7 @@ __global__ __launch_bounds__(FL_TILE) void k_deep_sort_cnt(Dev D, FlowArgs F) {
     if (tid < FL_CAP) {
       uint32_t c = 0;
       for (uint32_t ww = 0; ww < FL_TILE_W; ++ww) c += wc[ww][tid];
-      F.tcnt[(static_cast<size_t>(h) * F.maxt + tl) * FL_CAP + tid] = c;
+      fd_tcnt(F, F.hdr[h].dslot)[static_cast<size_t>(tl) * FL_CAP + tid] = c;
     }
     if (PASS == 1 && tid == 0 && nrest) atomicAdd(&F.hdr[h].rests, nrest);
     __syncthreads();
@@ -310,11 +354,11 @@ __global__ __launch_bounds__(FL_TILE) void k_deep_sort_cnt(Dev D, FlowArgs F) {
 
 __global__ __launch_bounds__(FL_CAP) void k_deep_sort_scan(Dev D, FlowArgs F) {
   __shared__ uint32_t tot[FL_CAP];
-  const uint32_t hb = blockIdx.x, h = F.h0 + hb, k = threadIdx.x;
-  if (h >= fl_hend(D, F) || F.hdr[h].ok != FL_OK_DEEP) return;
+  const uint32_t h = fd_book(D, F, blockIdx.x), k = threadIdx.x;
+  if (!fd_deep(F, h)) return;
   const uint32_t nt = F.hdr[h].ntouch;
   const uint32_t ntile = (nt + FL_TILE - 1) / FL_TILE;
-  uint32_t* tc = F.tcnt + static_cast<size_t>(h) * F.maxt * FL_CAP;
+  uint32_t* tc = fd_tcnt(F, F.hdr[h].dslot);
   uint32_t s = 0;
   for (uint32_t tl = 0; tl < ntile; ++tl) s += tc[tl * FL_CAP + k];
   tot[k] = s;
@@ -335,12 +379,12 @@ __global__ __launch_bounds__(FL_CAP) void k_deep_sort_scan(Dev D, FlowArgs F) {
 template <int PASS>
 __global__ __launch_bounds__(FL_TILE) void k_deep_sort_scatter(Dev D, FlowArgs F) {
   __shared__ uint32_t wc[FL_TILE_W][FL_CAP];
-  const uint32_t hb = blockIdx.y, h = F.h0 + hb, tid = threadIdx.x, w = tid >> 6;
-  if (h >= fl_hend(D, F) || F.hdr[h].ok != FL_OK_DEEP) return;
+  const uint32_t h = fd_book(D, F, blockIdx.y), tid = threadIdx.x, w = tid >> 6;
+  if (!fd_deep(F, h)) return;
   const uint32_t nt = F.hdr[h].ntouch, L = FL_TOUCH_MUL * F.hdr[h].beg;
   const unsigned long long g = F.hdr[h].g;
   const uint32_t ntile = (nt + FL_TILE - 1) / FL_TILE;
-  const uint32_t* tc = F.tcnt + static_cast<size_t>(h) * F.maxt * FL_CAP;
+  const uint32_t* tc = fd_tcnt(F, F.hdr[h].dslot);
   for (uint32_t i = tid; i < FL_TILE_W * FL_CAP; i += FL_TILE) wc[i / FL_CAP][i % FL_CAP] = 0;
   __syncthreads();
   for (uint32_t tl = blockIdx.x; tl < ntile; tl += gridDim.x) {
@@ -411,8 +455,8 @@ __device__ __forceinline__ uint32_t fd_lower(const SEnt* R, uint32_t nt, uint32_
 constexpr uint32_t DEEP_GRID = 1024;  // workgroups per deep book in the per-level kernels
 
 __global__ __launch_bounds__(64) void k_deep_level(Dev D, FlowArgs F) {
-  const uint32_t h = F.h0 + blockIdx.y;
-  if (h >= fl_hend(D, F) || F.hdr[h].ok != FL_OK_DEEP) return;
+  const uint32_t h = fd_book(D, F, blockIdx.y);
+  if (!fd_deep(F, h)) return;
   const uint32_t nl = F.hdr[h].nl, nt = F.hdr[h].ntouch, L = FL_TOUCH_MUL * F.hdr[h].beg;
   FlowLvl* LV = fl_lvls(F, h);
   for (uint32_t q = 1 + blockIdx.x; q <= nl; q += gridDim.x) {
@@ -427,12 +471,12 @@ __global__ __launch_bounds__(64) void k_deep_level(Dev D, FlowArgs F) {
 
 // ---- write: FIFO appends per level, then the level array ------------------------------------
 __global__ __launch_bounds__(64) void k_deep_write_lv(Dev D, BatchArgs B, FlowArgs F) {
-  const uint32_t h = F.h0 + blockIdx.y;
-  if (h >= fl_hend(D, F) || F.hdr[h].ok != FL_OK_DEEP) return;
+  const uint32_t h = fd_book(D, F, blockIdx.y);
+  if (!fd_deep(F, h)) return;
   const FlowHdr hd = F.hdr[h];
   for (uint32_t q = 1 + blockIdx.x; q <= hd.nl; q += gridDim.x) {
     const Level x = fl_write_level(D, B, F, hd, h, q);
-    if (lane_id() == 0) F.dlvout[static_cast<size_t>(h) * DEEP_CAP + q] = x;
+    if (lane_id() == 0) F.dlvout[static_cast<size_t>(hd.dslot) * DEEP_CAP + q] = x;
   }
 }
 
@@ -441,10 +485,10 @@ constexpr uint32_t DEEP_FIN_T = 1024, DEEP_FIN_PER = DEEP_CAP / DEEP_FIN_T;
 __global__ __launch_bounds__(DEEP_FIN_T) void k_deep_write_fin(Dev D, FlowArgs F) {
   __shared__ uint32_t part[DEEP_FIN_T];
   __shared__ uint32_t base_s, cap_s, nout_s;
-  const uint32_t h = F.h0 + blockIdx.x, tid = threadIdx.x;
-  if (h >= fl_hend(D, F) || F.hdr[h].ok != FL_OK_DEEP) return;
+  const uint32_t h = fd_book(D, F, blockIdx.x), tid = threadIdx.x;
+  if (!fd_deep(F, h)) return;
   const FlowHdr hd = F.hdr[h];
-  const Level* lv = F.dlvout + static_cast<size_t>(h) * DEEP_CAP;
+  const Level* lv = F.dlvout + static_cast<size_t>(hd.dslot) * DEEP_CAP;
   // levels q0 .. q0 + DEEP_FIN_PER - 1 per thread (1-based)
   const uint32_t q0 = 1 + tid * DEEP_FIN_PER;
   uint32_t c = 0;
@@ -495,12 +539,13 @@ __global__ __launch_bounds__(DEEP_FIN_T) void k_deep_write_fin(Dev D, FlowArgs F
     atomicAdd(&ct[C_FLOW_BOOKS], 1ull);
     atomicAdd(&ct[C_FLOW_ORDERS], static_cast<unsigned long long>(hd.end - hd.beg));
     atomicAdd(&ct[C_FLOW_TOUCHES], static_cast<unsigned long long>(hd.ntouch));
-    if (F.h0 == 0) {
+    if (hd.dslot == 0) {  // the hottest book (k_flow_plan_head's work)
       atomicAdd(&ct[C_FLOW_HEAD_ORDERS], static_cast<unsigned long long>(hd.end - hd.beg));
       atomicAdd(&ct[C_FLOW_HEAD_TOUCHES], static_cast<unsigned long long>(hd.ntouch));
     }
   }
   __syncthreads();
+  fd_clear(F, hd.dslot);  // (the records were built in prep c)
   if (nout_s > cap_s) return;  // (ERR_LEVELS)
   uint32_t o = part[tid];
   for (uint32_t u = 0; u < DEEP_FIN_PER; ++u) {

@@ -140,3 +140,12 @@ def test_deep_shallow_handoff_and_noops():
         kinds.append(sorted(eng.debug_flow_books()["kind"].tolist()))
     _state_eq(eng, orc, range(2))
     assert kinds[0] == [DEEP, DEEP]
+
+
+def test_deep_tail_books():
+    """Config 5's shape at small scale: beyond the 8 head books, mid-size books with more levels
+    than lanes take deep slots on the tail's stream (up to DEEP_SLOTS - FL_HEAD per batch)."""
+    st = wl.Stream(400, zipf_s=1.0, seed=13, price_decimals=4)
+    batches = [st.batch(200000) for _ in range(4)]
+    eng, orc, deep = _run(batches, 400, syms=list(range(0, 400, 9)))
+    assert deep > 4 * 20

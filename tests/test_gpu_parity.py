@@ -518,11 +518,12 @@ def test_flow_one_order_sweeps_every_level():
 @pytest.mark.gpu
 @pytest.mark.parametrize("nlev", [126, 127])
 def test_flow_level_cap(nlev):
-    """A batch whose book reaches exactly 126 distinct prices runs on the flow path; 127 is
-    declined (legacy / cold kernels).  Both exact."""
+    """A batch whose book reaches exactly 126 distinct prices runs on the lane plan; 127 takes
+    the deep plan (match_flow_deep.h).  Both exact."""
     rng = np.random.default_rng(nlev)
     n = 4000
     prices = np.concatenate([np.arange(1, nlev + 1), rng.integers(1, nlev + 1, n - nlev)])
     rec = _book(prices, rng.integers(1, 20, n) * 10**6, rng.integers(0, 2, n))
     eng, orc = _run_pair([rec], 1, sample_syms=[0])
-    assert eng.stats()["n_flow_books"] == (1 if nlev == 126 else 0)
+    assert eng.stats()["n_flow_books"] == 1
+    assert int(eng.debug_flow_books()["kind"][0]) == (1 if nlev == 126 else 3)

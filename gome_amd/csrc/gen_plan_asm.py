@@ -596,23 +596,25 @@ class Gen:
 
 # ---- W32C: the 32-bit plan of a book whose segment holds DELs -------------
 # Record (8 B): lo = ADD volume in units of g | DEL: window length n_b [0,16) | log2 C_k [16,21);
-# hi = level [0,7) | ring slot p [7,21) | DEL: maker SALE bit 29, DEL bit 30 | SALE (ADD) or 1
+# hi = level [0,7) | ring slot p [7,22) | DEL: maker SALE bit 29, DEL bit 30 | SALE (ADD) or 1
 # (DEL) bit 31.  Per level the plan also keeps R_k, the volume that ever arrived (lane pair
-# v[36:37], W32 layout), and every ADD owns a 16-B LDS ring entry {R pair, v, xv} (non-targeted
-# ADDs a dummy one): v = xv = 0 when the ADD crosses (it may never rest), {R pair before, T, 0}
-# when it rests (E = the level's word of the pair).  A DEL of target m at level k takes
-# r = clamp(E_m + v_m - (R_k - depth_k) + Xb, 0, v_m) where Xb sums xv over
-# the ring window of the n_b targets that arrived behind m (ranks rank_m + 1 ..): each DEL sets
-# its target's xv = v_m.  Touch keys come from an order counter (JJS, as the 64-bit plan):
-# rest = JJS | k | 1 << 7, consume = JJS | k, cancel = JJS | k | 1 << 31 (amount r).
+# v[36:37], W32 layout), and every ADD owns an 8-B LDS ring entry {E, v | X << 31} (non-targeted
+# ADDs a dummy one): v = 0 when the ADD crosses (it may never rest), {R_k before, T} when it
+# rests; X marks a target that was cancelled (its cancelled volume is v).  A DEL of target m at
+# level k takes r = clamp(E_m + v_m - (R_k - depth_k) + Xb, 0, v_m) where Xb sums v over the
+# cancelled entries of the ring window of the n_b targets that arrived behind m (ranks rank_m +
+# 1 ..): each DEL sets its target's X.  The cancel plan runs only when every R_k < 2^31 (plan
+# units), so a window sum of flagged words is Xb + cnt * 2^31 and bit 31 drops out.  Touch keys
+# come from an order counter (JJS, as the 64-bit plan): rest = JJS | k | 1 << 7, consume = JJS |
+# k, cancel = JJS | k | 1 << 31 (amount r).
 CREG = {"R": (36, 37)}
-# v38 = T of a rest and v39 = 0 follow the R pair: a rest writes its entry {R pair, T, 0} in one
-# ds_write_b128 from lane LI >> 1 (the DEL picks E = the level's word of the pair)
-VV, VZ0 = 38, 39
-VE, VM = 40, 42              # a DEL's entry read {R lo, R hi, v} -> v[40:42]
+VZ0 = 39                     # stays 0
+VE, VM = 40, 41              # a rest's entry {E, T}; a DEL's entry read {E, v} -> v[40:41]
+VT = 42                      # window: flag mask
 VA = 43                      # LDS address
 VG0, VG1 = 44, 45            # G_k words
 VW, VX, VL = 46, 47, 48      # window address / data, lane id
+VF = 49                      # 1 << 31 (the cancelled flag)
 X0, X1, X2, X3 = "s79", "s81", "s83", "s96"              # free in the 32-bit layout
 CLOBBERS_C = [f"v{i}" for i in range(36, 50)]
 
@@ -630,18 +632,18 @@ class GenC(Gen):
         e(f"s_bitcmp1_b32 {hi}, 31")
 
     def entry_addr(self, hi: str):
-        """X3 = byte address of the record's ring entry (slot [7, 21) of hi, 16-B entries)."""
-        self.e(f"s_lshr_b32 {X3}, {hi}, 3")
-        self.e(f"s_and_b32 {X3}, {X3}, 0x3fff0")
+        """X3 = byte address of the record's ring entry (slot [7, 22) of hi, 8-B entries)."""
+        self.e(f"s_lshr_b32 {X3}, {hi}, 4")
+        self.e(f"s_and_b32 {X3}, {X3}, 0x3fff8")
 
     def cross_entry(self, T):
-        """An ADD that crosses may be filled completely and never rest: its entry's v and xv
-        := 0 now (an ADD that rests writes the whole entry)."""
+        """An ADD that crosses may be filled completely and never rest: its entry's v := 0 now
+        (an ADD that rests writes the whole entry)."""
         e = self.e
         self.entry_addr(T[1])
         e("s_mov_b64 exec, 1")
         e(f"v_mov_b32 v{VA}, {X3}")
-        e(f"ds_write2_b32 v{VA}, v{VZ0}, v{VZ0} offset0:2 offset1:3")
+        e(f"ds_write_b32 v{VA}, v{VZ0} offset:4")
 
     def dispatch(self, j: int, fall: bool, copy: bool = COPY_REST):
         e = self.e
@@ -661,8 +663,8 @@ class GenC(Gen):
                 e(f"s_branch {self.lab(f'BR{j}')}")
 
     def rest(self, side: str, T):
-        """The 32-bit rest, then R_k += T and the ring entry := {E + T, T, 0} (E = R_k before),
-        both from lane LI >> 1 of the R pair: no lane read on the path."""
+        """The 32-bit rest, then the ring entry := {E, T} (E = R_k before: the level's word of the
+        R pair shifted down) and R_k += T, both from lane LI >> 1: no lane read on the path."""
         e = self.e
         buy = side == "B"
         top, topd = (BB, BBD) if buy else (BA, BAD)
@@ -681,10 +683,11 @@ class GenC(Gen):
         self.entry_addr(T[1])
         e(f"s_lshr_b32 {T0}, {LI}, 1")
         e(f"s_bfm_b64 exec, 1, {T0}")
-        e(f"v_mov_b32 v{VV}, {T[0]}")
-        e(f"v_mov_b32 v{VA}, {X3}")
-        e(f"ds_write_b128 v{VA}, v[{ev}:{VZ0}]")          # {R pair (E = the level's word), T, 0}
         e(f"s_lshl_b32 {T0}, {LI}, 5")
+        e(f"v_lshrrev_b64 v[{VE}:{VM}], {T0}, v[{ev}:{od}]")   # v40 = E (the level's word)
+        e(f"v_mov_b32 v{VM}, {T[0]}")
+        e(f"v_mov_b32 v{VA}, {X3}")
+        e(f"ds_write_b64 v{VA}, v[{VE}:{VM}]")                # {E, T}
         e(f"s_mov_b32 s90, {T[0]}")                      # (s91 = 0)
         e(f"s_lshl_b64 s[92:93], s[90:91], {T0}")
         e(f"v_lshl_add_u64 v[{ev}:{od}], s[92:93], 0, v[{ev}:{od}]")   # R_k += T
@@ -704,8 +707,8 @@ class GenC(Gen):
         e(f"v_readlane_b32 {dst}, {v}, 63")
 
     def window_read(self, lanes: str, first: str):
-        """window data = xv of ring slots pbase | ((first + lane) & mask) for lanes < `lanes`
-        (others 0); X2 = mask, X1 = pbase."""
+        """window data = the {v | X << 31} word of ring slots pbase | ((first + lane) & mask) for
+        lanes < `lanes` (others 0); X2 = mask, X1 = pbase."""
         e = self.e
         e("s_mov_b64 exec, -1")
         e(f"v_mov_b32 v{VX}, 0")
@@ -713,8 +716,8 @@ class GenC(Gen):
         e(f"v_add_u32 v{VW}, {first}, v{VL}")
         e(f"v_and_b32 v{VW}, {X2}, v{VW}")
         e(f"v_or_b32 v{VW}, {X1}, v{VW}")
-        e(f"v_lshlrev_b32 v{VW}, 4, v{VW}")
-        e(f"ds_read_b32 v{VX}, v{VW} offset:12")
+        e(f"v_lshlrev_b32 v{VW}, 3, v{VW}")
+        e(f"ds_read_b32 v{VX}, v{VW} offset:4")
 
     def del_path(self, i: int):
         """DeleteOrder (engine.go:87-116) on the aggregates of level LI: r = clamp(end_m + Xb -
@@ -731,7 +734,7 @@ class GenC(Gen):
         e(f"s_lshr_b32 {T0}, {LI}, 1")
         e(f"s_bfm_b64 exec, 1, {T0}")                         # lane LI >> 1 from here on
         e(f"v_mov_b32 v{VA}, {X3}")
-        e(f"ds_read_b96 v[{VE}:{VM}], v{VA}")                 # {R pair at m's arrival, v_m}
+        e(f"ds_read_b64 v[{VE}:{VM}], v{VA}")                 # {E_m, v_m} (X is clear)
         e(f"s_and_b32 {X0}, {lo}, 0xffff")                    # n_b
         e("s_mov_b32 s90, 0")                                 # Xb
         e(f"s_cmp_lg_u32 {X0}, 0")
@@ -755,15 +758,14 @@ class GenC(Gen):
         e(f"v_subrev_u32 v{VG0}, {X1}, v{VG0}")               # G_k
         if not DEL_NOWAIT:
             e("s_waitcnt lgkmcnt(0)")
-        # a = E_m + v_m + Xb (< 2^32: the window's makers arrived after m); r = a - G_k clamped
-        # to [0, v_m]; xv_m := v_m
-        e(f"v_cndmask_b32 v{VE}, v{VE}, v{VE + 1}, vcc")      # E_m
+        # a = E_m + v_m + Xb (< 2^31: the window's makers arrived after m); r = a - G_k clamped
+        # to [0, v_m]; X_m := 1
         e(f"v_add_u32 v{VE}, v{VE}, v{VM}")
         e(f"v_add_u32 v{VE}, s90, v{VE}")
         e(f"v_sub_co_u32 v{VE}, vcc, v{VE}, v{VG0}")
         e(f"v_cndmask_b32 v{VE}, v{VE}, v{VZ0}, vcc")
         e(f"v_min_u32 v{VE}, v{VE}, v{VM}")
-        e(f"ds_write_b32 v{VA}, v{VM} offset:12")
+        e(f"ds_or_b32 v{VA}, v{VF} offset:4")
         e(f"v_readlane_b32 {X1}, v{VE}, {T0}")                # r
         e(f"s_cmp_eq_u32 {X1}, 0")
         e(f"s_cbranch_scc1 {lab(f'DZ{i}')}")                  # not found: no event (:96-98)
@@ -804,7 +806,7 @@ class GenC(Gen):
         self.slow.append(blk)
         sv = self.out
         self.out = blk
-        e(f"s_lshr_b32 {X3}, {X3}, 4")                        # p
+        e(f"s_lshr_b32 {X3}, {X3}, 3")                        # p
         e(f"s_lshr_b32 {X1}, {lo}, 16")
         e(f"s_bfm_b32 {X2}, {X1}, 0")                         # mask = C_k - 1
         e(f"s_andn2_b32 {X1}, {X3}, {X2}")                    # pbase
@@ -818,7 +820,10 @@ class GenC(Gen):
         self.window_read(L, T0)
         e("s_waitcnt lgkmcnt(0)")
         e("s_mov_b64 exec, -1")
+        e(f"v_ashrrev_i32 v{VT}, 31, v{VX}")                  # cancelled entries only
+        e(f"v_and_b32 v{VX}, v{VX}, v{VT}")
         self.reduce_window(L)
+        e(f"s_bitset0_b32 {L}, 31")                           # (- cnt * 2^31)
         e(f"s_add_u32 s90, s90, {L}")
         e(f"s_add_u32 {K}, {K}, 63")
         e(f"s_cmp_lt_u32 {K}, {X0}")
@@ -874,6 +879,7 @@ class GenC(Gen):
         e(f"v_mbcnt_lo_u32_b32 v{VL}, -1, 0")
         e(f"v_mbcnt_hi_u32_b32 v{VL}, -1, v{VL}")
         e(f"v_mov_b32 v{VZ0}, 0")
+        e(f"v_bfrev_b32 v{VF}, 1")
         ev, od = CREG["R"]
         e(f"v_mov_b32 v{ev}, %[rl0]")
         e(f"v_mov_b32 v{od}, %[rl1]")

@@ -122,7 +122,7 @@ struct FlowHdr {
   uint32_t fc_big;     //   its ring needs more than FC_TAIL_SLOTS entries
   // books whose segment holds DELs (ok == FL_OK_CANCEL, match_flow_cancel.h)
   uint32_t ndel;       // DEL records of the segment
-  uint32_t nslot;      // LDS ring entries of the plan (16 B each, the dummy entry included)
+  uint32_t nslot;      // LDS ring entries of the plan (8 B each, the dummy entry included)
   uint32_t ncancel;    // the cancel prep's longest window + 1 (diagnostics)
   uint32_t fc_bad;     // set by the cancel prep: decline the book (legacy / cold kernels)
   uint32_t deep;       // the lane prep found more levels than FL_MAX: a deep-book candidate
@@ -167,13 +167,15 @@ struct FlowLvl {
 };
 static_assert(sizeof(FlowLvl) % 16 == 0, "FlowLvl alignment");
 
-// The cancel plan's LDS ring (match_flow_cancel.h): 16-B entries {R pair, v, xv} per targeted
-// maker (+ one dummy entry), an image per book built by the cancel prep (bump-allocated).  A
-// ring of up to FC_TAIL_SLOTS entries plans in a 16-KiB workgroup; a larger one (up to
-// FlowArgs::fc_ring_cap, the device's LDS per workgroup) in a workgroup that owns its CU.
-constexpr uint32_t FC_MAX_SLOTS = 10240;  // 160 KiB: the most LDS a gfx950 workgroup can hold
-constexpr uint32_t FC_TAIL_SLOTS = 1024;
-constexpr uint32_t FC_TAIL_LDS = FC_TAIL_SLOTS * 16;
+// The cancel plan's LDS ring (match_flow_cancel.h): 8-B entries {E, v | cancelled << 31} per
+// targeted maker (+ one dummy entry), an image per book built by the cancel prep
+// (bump-allocated).  A ring of up to FC_TAIL_SLOTS entries plans in a 16-KiB workgroup; a larger
+// one (up to FlowArgs::fc_ring_cap, the device's LDS per workgroup) in a workgroup that owns its
+// CU.  Ring slots are 15-bit fields of the W32C records.
+constexpr uint32_t FC_MAX_SLOTS = 20480;  // 160 KiB: the most LDS a gfx950 workgroup can hold
+constexpr uint32_t FC_TAIL_SLOTS = 2048;
+constexpr uint32_t FC_TAIL_LDS = FC_TAIL_SLOTS * 8;
+static_assert(FC_MAX_SLOTS <= (1u << 15), "ring slots are 15-bit record fields");
 constexpr uint32_t FC_TOFF = MAX_FLOW + 16;  // second toff region for books with DELs
 constexpr uint32_t FC_GEN_MASK = 0x7FF;   // generation bits of an FcHash key
 
@@ -201,10 +203,10 @@ struct FlowArgs {
   // streams), and the range's offset in toff
   uint32_t h0, h1, tb;
   // books with DELs (match_flow_cancel.h)
-  uint4* fc_img;       // LDS ring images (FlowHdr::fc_img), bump-allocated per batch
+  uint2* fc_img;       // LDS ring images (FlowHdr::fc_img), bump-allocated per batch
   uint32_t* fc_img_bump;
   uint32_t fc_img_cap; // entries
-  uint32_t fc_ring_cap;  // largest ring (entries): the device's LDS per workgroup / 16
+  uint32_t fc_ring_cap;  // largest ring (entries): the device's LDS per workgroup / 8
   FcDel* fc_del;       // [max_batch] per segment position: the DEL's target
   uint32_t* fc_tg;     // [max_batch] per segment position: ADD targeted by the DEL at (value - 1)
   uint32_t* fc_rank;   // [max_batch] per segment position: a targeted ADD's rank in its level
@@ -432,7 +434,8 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep(Dev D, BatchArgs B, Flo
     sum = min(sum + ws[w], FL_SUM_CAP);
   }
   if (g == 0) g = 1;
-  const bool w32 = sum < FL_SUM_CAP && sum / g < (1ull << 32);
+  // (the cancel plan needs every R_k < 2^31: its ring entries carry a flag in bit 31)
+  const bool w32 = sum < FL_SUM_CAP && sum / g < (dels ? (1ull << 31) : (1ull << 32));
   if (!w32) g = 1;
   if (dels && !w32) {  // the cancel plan is 32-bit only
     if (tid == 0) { hd->ok = 0; hd->deep = 0; }
@@ -729,9 +732,10 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep_b(Dev D, BatchArgs B, F
     P->val[i] = hval[i];
   }
   unsigned long long g = mg ? mg : 1;
-  const bool w32 = msum < FL_SUM_CAP && msum / g < (1ull << 32);
-  if (!w32) g = 1;
   const uint32_t dels = P->dels;
+  // (the cancel plan needs every R_k < 2^31: its ring entries carry a flag in bit 31)
+  const bool w32 = msum < FL_SUM_CAP && msum / g < (dels ? (1ull << 31) : (1ull << 32));
+  if (!w32) g = 1;
   if (dels && !w32) {  // the cancel plan is 32-bit only
     if (tid == 0) { hd->ok = 0; hd->deep = 0; }
     return;
@@ -895,8 +899,9 @@ extern __shared__ uint4 fl_ring[];  // the cancel plan's ring (dynamic LDS)
 // Books with DELs: the ring image -> LDS, by every thread of the block.
 __device__ __forceinline__ void fl_ring_load(const FlowArgs& F, uint32_t h) {
   const uint32_t ns = F.hdr[h].nslot;
-  const uint4* img = F.fc_img + F.hdr[h].fc_img;
-  for (uint32_t i = threadIdx.x; i < ns; i += blockDim.x) fl_ring[i] = img[i];
+  const uint2* img = F.fc_img + F.hdr[h].fc_img;
+  uint2* ring = reinterpret_cast<uint2*>(fl_ring);
+  for (uint32_t i = threadIdx.x; i < ns; i += blockDim.x) ring[i] = img[i];
 }
 
 // Deep books: the depth slots (W32 units; bid of level k at byte 8k, ask at 8k + 4) -> LDS by

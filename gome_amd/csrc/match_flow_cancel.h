@@ -12,9 +12,9 @@
 // *behind* m that were cancelled before: while m is live they were untouched, so each removed
 // exactly its v_j; when m is gone the clamp gives 0 (tools/flow_cancel_model.py checks this
 // against the oracle).  So the plan (gen_plan_asm.py, W32C) keeps R_k beside the depths, and
-// every DEL's target ("targeted maker") owns an entry {end = E + v, v, xv} of an LDS ring per
-// level; a DEL reads its target's entry, sums xv over the window of targets that arrived behind
-// it (ranks rank_m + 1 .. rank_m + n_b) and sets its own xv = v_m.  Ring capacity C_k (a power
+// every DEL's target ("targeted maker") owns an entry {E, v | X << 31} of an LDS ring per
+// level; a DEL reads its target's entry, sums v over the cancelled (X) entries of the window of
+// targets that arrived behind it (ranks rank_m + 1 .. rank_m + n_b) and sets its target's X.  Ring capacity C_k (a power
 // of two) exceeds every window, so an entry is reused only after every DEL that reads it.
 //
 // Prep (after the book's ordinary prep, which builds the level set and the 32-bit records):
@@ -432,8 +432,8 @@ __global__ __launch_bounds__(FC_PASS_T) void k_fc_pass(Dev D, BatchArgs B, FlowA
     LV[tid].cring = cring[tid];
     LV[tid].rbase = rbase[tid];
   }
-  uint4* img = F.fc_img + F.hdr[h].fc_img;
-  for (uint32_t x = tid; x < nslot; x += FC_PASS_T) img[x] = make_uint4(0u, 0u, 0u, 0u);
+  uint2* img = F.fc_img + F.hdr[h].fc_img;
+  for (uint32_t x = tid; x < nslot; x += FC_PASS_T) img[x] = make_uint2(0u, 0u);
   __syncthreads();
   const uint32_t npad = (8u - (n & 7u)) & 7u;
   for (uint32_t i = tid; i < n + npad; i += FC_PASS_T) {
@@ -455,7 +455,7 @@ __global__ __launch_bounds__(FC_PASS_T) void k_fc_pass(Dev D, BatchArgs B, FlowA
           const uint32_t lgc = 31u - __clz(cring[kk]);
           rec = (static_cast<unsigned long long>(kk | (slot << 7) | (sale ? 1u << 29 : 0u) | (3u << 30)) << 32) |
                 (d.nb | (lgc << 16));
-          if (d.kind == FC_OLD) img[slot] = make_uint4(d.oend - d.ov, d.oend - d.ov, d.ov, 0u);  // {E, E, v, xv}
+          if (d.kind == FC_OLD) img[slot] = make_uint2(d.oend - d.ov, d.ov);  // {E, v}, not cancelled
         }
       }
     }

@@ -257,3 +257,27 @@ def test_flow_cancel_generation_wrap():
         eng.submit(b)
         _cmp(eng.drain(), orc.submit(b), f"batch {i}")
     _state_eq(eng, orc, [0])
+
+
+def test_flow_cancel_rings_beyond_16_byte_capacity():
+    """Two levels whose DEL windows need 8192-entry rings each (16384 entries: more than the
+    10240 a 160-KiB workgroup held with 16-B entries, within the 20480 of 8-B entries): the book
+    stays on the flow path (no FC_BAD_RING decline) and is exact."""
+    P = 10**6
+    rows, oid = [], 1
+    for p in (61, 62):
+        for k in range(4200):
+            rows.append((p * P, (1 + k % 5) * P, 0, oid, 3, 1, ADD, 0))
+            oid += 1
+    rows += [(40 * P, P, 0, 90000 + k, 3, 0, ADD, 0) for k in range(200)]   # bids below
+    # every maker is a target (a ring counts targets): the first DEL of each level has a
+    # window of 4199 targets (C_k = 8192); a taker between them
+    rows += [(61 * P, 0, 0, o, 3, 1, DEL, 0) for o in range(1, 2001)]
+    rows.append((61 * P, 7 * P, 0, 99000, 3, 0, ADD, 0))
+    rows += [(62 * P, 0, 0, o, 3, 1, DEL, 0) for o in range(4201, 8401, 2)]
+    rows += [(61 * P, 0, 0, o, 3, 1, DEL, 0) for o in range(2001, 4201)]
+    rows.append((62 * P, 9000 * P, 0, 99001, 3, 0, ADD, 0))                 # sweeps both levels
+    _, _, fc, fb = _run([_recs(rows)], 1)
+    fbk = ROUTES[-1][1]
+    assert int(fbk["decline"][0]) == 0 and int(fbk["ring"][0]) > 10240, _routes_msg()
+    assert fb == 1 and fc > 2000

@@ -74,7 +74,13 @@ struct WaveCtx {
   bool ev_ok, fatal;
   unsigned long long fills, cancels, rests, dropped, adds, dels;
   long long resting_delta, levels_delta;
+  // the wave's chunk pool: lane i < npool holds a free chunk id.  Allocations and frees go
+  // through it, so the shared free stack / bump pointer / freed list (one cache line of Status
+  // that every wave of the grid would otherwise hit once per allocation and per free) see one
+  // atomic per CPOOL chunks; the rest goes to the freed list at wave_flush.
+  uint32_t cpool, npool;
 };
+constexpr uint32_t CPOOL = 32;
 
 __device__ __forceinline__ void set_err(WaveCtx& W, uint32_t e) {
   if (lane_id() == 0) atomicOr(&W.D.st->err, e);
@@ -103,18 +109,47 @@ __device__ __forceinline__ void ev_make_room(WaveCtx& W, uint32_t k) {
 }
 
 __device__ __forceinline__ uint32_t alloc_chunk(WaveCtx& W) {
-  uint32_t c = 0;
-  if (lane_id() == 0) {
-    int t = atomicSub(&W.D.st->free_top, 1);
-    c = (t > 0) ? W.D.free_ids[t - 1] : atomicAdd(W.D.ch_bump, 1u);
+  const uint32_t lane = lane_id();
+  if (W.npool == 0) {  // claim CPOOL ids: the free stack first, then the bump pointer
+    int t = 0;
+    if (lane == 0) t = atomicSub(&W.D.st->free_top, static_cast<int>(CPOOL));
+    t = static_cast<int>(uni(static_cast<uint32_t>(t)));
+    const uint32_t nst = static_cast<uint32_t>(min(max(t, 0), static_cast<int>(CPOOL)));
+    uint32_t b = 0;
+    if (lane == 0 && nst < CPOOL) b = atomicAdd(W.D.ch_bump, CPOOL - nst);
+    b = uni(b);
+    if (lane < CPOOL)
+      W.cpool = (lane < nst) ? W.D.free_ids[t - static_cast<int>(nst) + static_cast<int>(lane)] : b + (lane - nst);
+    W.npool = CPOOL;
   }
-  c = uni(c);
+  W.npool--;
+  const uint32_t c = rl(W.cpool, W.npool);
   if (c >= W.D.ch_cap) { set_err(W, ERR_CHUNKS); return NIL; }
   return c;
 }
 
+// Pool ids lanes [lo, hi) -> the batch's freed list (recycled after the batch by k_recycle_*);
+// ids past the pool's capacity (a bump claim that overshot it) are dropped.
+__device__ __forceinline__ void pool_publish(WaveCtx& W, uint32_t lo, uint32_t hi) {
+  const uint32_t lane = lane_id();
+  const bool ok = lane >= lo && lane < hi && W.cpool < W.D.ch_cap;
+  const unsigned long long m = __ballot(ok);
+  if (!m) return;
+  uint32_t b = 0;
+  if (lane == 0) b = atomicAdd(&W.D.st->freed_top, static_cast<uint32_t>(__popcll(m)));
+  b = uni(b);
+  if (ok) W.D.freed_ids[b + __popcll(m & lt_mask())] = W.cpool;
+}
+
+// A chunk no FIFO references any more (its nodes are consumed, cancelled or erased from the
+// index): back to the wave's pool, reused by its next allocation.
 __device__ __forceinline__ void free_chunk(WaveCtx& W, uint32_t c) {
-  if (lane_id() == 0) W.D.freed_ids[atomicAdd(&W.D.st->freed_top, 1u)] = c;
+  if (W.npool == 64) {
+    pool_publish(W, 32, 64);
+    W.npool = 32;
+  }
+  if (lane_id() == W.npool) W.cpool = c;
+  W.npool++;
 }
 
 __device__ __forceinline__ void free_chain(WaveCtx& W, uint32_t head, uint32_t tail) {
@@ -636,6 +671,8 @@ __device__ __forceinline__ void wave_finish(WaveCtx& W, bool flush = true) {
 
 __device__ __forceinline__ void wave_flush(WaveCtx& W) {
   ev_close(W);
+  pool_publish(W, 0, W.npool);
+  W.npool = 0;
   if (lane_id() == 0) {
     unsigned long long* c = W.D.st->ctr;
     if (W.fills) atomicAdd(&c[C_FILLS], W.fills);
@@ -685,6 +722,8 @@ __device__ __forceinline__ void wave_init(WaveCtx& W, const Dev& D, const BatchA
   W.fatal = false;
   W.fills = W.cancels = W.rests = W.dropped = W.adds = W.dels = 0;
   W.resting_delta = W.levels_delta = 0;
+  W.cpool = NIL;
+  W.npool = 0;
 }
 
 // Cold books: one wavefront per book, state in HBM.  Wave w of the grid takes books

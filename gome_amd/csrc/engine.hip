@@ -304,7 +304,7 @@ gome_status gome_engine::init(const gome_config& c) {
     F.fc_ring_cap = std::min<uint32_t>(FC_MAX_SLOTS, static_cast<uint32_t>(std::max(lds, 0)) / 8);
     if (F.fc_ring_cap < FC_TAIL_SLOTS) return fail(GOME_E_DEVICE, "device LDS per workgroup below 16 KiB");
     fc_ring_lds = F.fc_ring_cap * 8;
-    if (fc_ring_lds < DEEP_CAP * 8) return fail(GOME_E_DEVICE, "device LDS per workgroup below 128 KiB");
+    if (fc_ring_lds < FL_DEEP_LDS) return fail(GOME_E_DEVICE, "device LDS per workgroup below 132 KiB");
     for (const void* k : {reinterpret_cast<const void*>(k_flow_plan_head), reinterpret_cast<const void*>(k_flow_plan_near),
                           reinterpret_cast<const void*>(k_flow_plan_tail_cb), reinterpret_cast<const void*>(k_flow_plan_tail_d)})
       HIPCHK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(fc_ring_lds)));

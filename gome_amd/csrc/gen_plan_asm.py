@@ -890,16 +890,20 @@ class GenC(Gen):
 # Depths live in LDS instead of lane registers: level k's bid depth at byte 8k, its ask depth at
 # 8k + 4 (DEEP_CAP levels, 128 KiB), with the same invariant as the lanes: a slot holds 0 unless
 # its level rests on that side behind the cached top.  Sentinels: level 0 is a permanent bid,
-# level DEEP_CAP - 1 a permanent ask.  A rest is one ds_add; the next level after the top empties
-# is found by reading 64 slots per step and a bit scan.  Records: lo = volume in units of g,
-# hi = level [0, 14) | SALE bit 31 (no-op: 0, a rest of 0 at the bid sentinel).  Touch keys
-# come from the order counter (JJS | 1 << 7 for a rest); the level goes to the touch's second
-# word (Touch::pos, read by the deep sort).
+# level DEEP_CAP - 1 a permanent ask.  A per-side occupancy bitmap mirrors "slot != 0" (bit k of
+# dword k >> 5; bids at DEEP_BM, asks at DEEP_BM + DEEP_CAP / 8): a rest is one ds_add plus one
+# ds_or of its bit, and the next level after the top empties is one 64-lane read of 64 bitmap
+# dwords (2048 levels) and two bit scans, then the level's slot (read and zeroed, its bit
+# cleared).  Records: lo = volume in units of g, hi = level [0, 14) | SALE bit 31 (no-op: 0, a
+# rest of 0 at the bid sentinel).  Touch keys come from the order counter (JJS | 1 << 7 for a
+# rest); the level goes to the touch's second word (Touch::pos, read by the deep sort).
 DEEP_CAP = 16384
-VDA, VDD, VSA, VSD, VSL, VZD = 36, 37, 38, 39, 40, 41     # add address / data, scan address /
-SCAN_CHUNKS = int(os.environ.get("GOME_DEEP_CHUNKS", "8"))
-VSD2 = (39,) + tuple(range(42, 42 + SCAN_CHUNKS - 1))     # data (SCAN_CHUNKS x 64 slots per step),
-CLOBBERS_D = [f"v{i}" for i in range(36, 42 + SCAN_CHUNKS - 1)]  # lane id, zero
+DEEP_BM = DEEP_CAP * 8                       # byte offset of the bid bitmap (asks follow)
+DEEP_BM_BYTES = 2 * DEEP_CAP // 8
+VDA, VDD, VSA, VSD, VSL, VZD = 36, 37, 38, 39, 40, 41   # slot address / data, scan address /
+VBA, VBD, VBASE_A, VBASE_B = 42, 43, 44, 45             # data, lane id, zero; bit address / data;
+CLOBBERS_D = [f"v{i}" for i in range(36, 46)]            # per-lane scan bases of the bitmaps
+BM = {"B": DEEP_BM, "A": DEEP_BM + DEEP_CAP // 8}
 
 
 class GenD(Gen):
@@ -958,64 +962,61 @@ class GenD(Gen):
 
     def next_top(self, sd: str):
         """After the cached top of side sd emptied: the next level of that side (asks: the lowest
-        nonzero slot above BA, bids: the highest below BB), SCAN_CHUNKS x 64 slots per step (one
-        LDS round trip); its slot := 0."""
+        set bit above BA, bids: the highest below BB; the sentinels' bits are always set).  Lane
+        i reads bitmap dword w0 + i (asks) / w0 - 63 + i (bids): every bit of the side below BA
+        (above BB) is 0 by the invariant, so the first dword needs no mask.  The level's slot
+        becomes the cached depth (read, then zeroed) and its bit is cleared."""
         e = self.e
         top, topd = (BA, BAD) if sd == "A" else (BB, BBD)
-        loop, done = self.fresh("NT"), self.fresh("ND")
+        loop, more = self.fresh("NT"), self.fresh("NM")
         off = self.side_off(sd)
-        span = 64 * SCAN_CHUNKS
-        # asks: chunk c covers levels T0 + 64c + lane; bids: T0 - 64c + lane (T0 = BB - 64 first)
+        base = VBASE_A if sd == "A" else VBASE_B
         if sd == "A":
             e(f"s_add_u32 {T0}, {BA}, 1")
         else:
-            e(f"s_sub_u32 {T0}, {BB}, 64")
+            e(f"s_sub_u32 {T0}, {BB}, 1")
+        e(f"s_lshr_b32 {T0}, {T0}, 5")                      # the dword of the first candidate
         e(f"{loop}:")
         e("s_mov_b64 exec, -1")
-        e(f"v_add_u32 v{VSA}, {T0}, v{VSL}")
-        e(f"v_lshlrev_b32 v{VSA}, 3, v{VSA}")
-        for c in range(SCAN_CHUNKS):
-            o = off + (512 * c if sd == "A" else 0)
-            if sd == "A":
-                e(f"ds_read_b32 v{VSD2[c]}, v{VSA} offset:{o}")
-            elif c == 0:
-                e(f"ds_read_b32 v{VSD2[c]}, v{VSA} offset:{off}")
-        if sd == "B":   # downward chunks need negative offsets: separate addresses
-            for c in range(1, SCAN_CHUNKS):
-                e(f"v_subrev_u32 v{VDA}, {512 * c}, v{VSA}")
-                e(f"ds_read_b32 v{VSD2[c]}, v{VDA} offset:{off}")
+        e(f"s_lshl_b32 {O[2]}, {T0}, 2")
+        e(f"v_add_u32 v{VSA}, {O[2]}, v{base}")
+        e(f"ds_read_b32 v{VSD}, v{VSA}")
         e("s_waitcnt lgkmcnt(0)")
-        founds = []
-        for c in range(SCAN_CHUNKS):
-            f = self.fresh(f"NF{c}_")
-            founds.append(f)
-            e(f"v_cmp_ne_u32_e64 {M}, 0, v{VSD2[c]}")
-            if sd == "A":
-                e(f"s_ff1_i32_b64 {O[0]}, {M}")
-            else:
-                e(f"s_flbit_i32_b64 {O[0]}, {M}")
-            e(f"s_cmp_lt_i32 {O[0]}, 0")
-            e(f"s_cbranch_scc0 {f}")
-        e(f"s_{'add' if sd == 'A' else 'sub'}_u32 {T0}, {T0}, {span}")
-        e(f"s_branch {loop}")
-        for c in range(SCAN_CHUNKS):
-            e(f"{founds[c]}:")
-            if sd == "B":
-                e(f"s_sub_u32 {O[0]}, 63, {O[0]}")
-            e(f"s_{'add' if sd == 'A' else 'sub'}_u32 {T0}, {T0}, {64 * c}")
-            e(f"s_add_u32 {top}, {T0}, {O[0]}")
-            e(f"v_readlane_b32 {topd[0]}, v{VSD2[c]}, {O[0]}")
-            e(f"s_lshl_b64 exec, 1, {O[0]}")
-            if sd == "A":
-                e(f"ds_write_b32 v{VSA}, v{VZD} offset:{off + 512 * c}")
-            elif c == 0:
-                e(f"ds_write_b32 v{VSA}, v{VZD} offset:{off}")
-            else:
-                e(f"v_subrev_u32 v{VDA}, {512 * c}, v{VSA}")
-                e(f"ds_write_b32 v{VDA}, v{VZD} offset:{off}")
-            if c != SCAN_CHUNKS - 1:
-                e(f"s_branch {done}")
-        e(f"{done}:")
+        e(f"v_cmp_ne_u32_e64 {M}, 0, v{VSD}")
+        e(f"s_{'ff1' if sd == 'A' else 'flbit'}_i32_b64 {O[0]}, {M}")
+        e(f"s_cmp_lt_i32 {O[0]}, 0")
+        e(f"s_cbranch_scc1 {more}")                         # no set bit in 2048 levels (rare)
+        self.slow.append([f"{more}:", f"s_{'add' if sd == 'A' else 'sub'}_u32 {T0}, {T0}, 64",
+                          f"s_branch {loop}"])
+        if sd == "A":
+            e(f"v_readlane_b32 {O[2]}, v{VSD}, {O[0]}")
+            e(f"s_ff1_i32_b32 {O[2]}, {O[2]}")
+            e(f"s_add_u32 {T0}, {T0}, {O[0]}")
+        else:
+            e(f"s_sub_u32 {O[0]}, 63, {O[0]}")              # the lane
+            e(f"v_readlane_b32 {O[2]}, v{VSD}, {O[0]}")
+            e(f"s_flbit_i32_b32 {O[2]}, {O[2]}")
+            e(f"s_sub_u32 {O[2]}, 31, {O[2]}")
+            e(f"s_sub_u32 {T0}, {T0}, 63")
+            e(f"s_add_u32 {T0}, {T0}, {O[0]}")
+        e(f"s_lshl_b32 {T0}, {T0}, 5")
+        e(f"s_add_u32 {top}, {T0}, {O[2]}")
+        # the slot: its depth becomes the cached one, the slot 0 (LDS ops of a wave run in order)
+        e(f"s_lshl_b32 {T0}, {top}, 3")
+        e("s_mov_b64 exec, 1")
+        e(f"v_mov_b32 v{VDA}, {T0}")
+        e(f"ds_read_b32 v{VDD}, v{VDA} offset:{off}")
+        e(f"ds_write_b32 v{VDA}, v{VZD} offset:{off}")
+        # its bit (set) is cleared
+        e(f"s_lshr_b32 {T0}, {top}, 3")
+        e(f"s_and_b32 {T0}, {T0}, 0x7fc")
+        e(f"s_add_u32 {T0}, {T0}, {BM[sd]}")
+        e(f"s_lshl_b32 {O[2]}, 1, {top}")
+        e(f"v_mov_b32 v{VBA}, {T0}")
+        e(f"v_mov_b32 v{VBD}, {O[2]}")
+        e(f"ds_xor_b32 v{VBA}, v{VBD}")
+        e("s_waitcnt lgkmcnt(0)")
+        e(f"v_readfirstlane_b32 {topd[0]}, v{VDD}")
 
     def rest(self, side: str, T):
         """As the 32-bit rest, with the lane add replaced by an LDS add at slot (L, side)."""
@@ -1033,6 +1034,15 @@ class GenD(Gen):
         e(f"s_{'max' if buy else 'min'}_u32 {top}, {top}, {LI}")
         self.add(topd, topd, X)
         self.lds_add(L, A[0], "B" if buy else "A")
+        # slot L is nonzero now iff A > 0 (A == 0: L is the cached top, whose bit stays 0)
+        e(f"s_min_u32 s79, {A[0]}, 1")
+        e(f"s_lshl_b32 s79, s79, {L}")
+        e(f"s_lshr_b32 s81, {L}, 3")
+        e(f"s_and_b32 s81, s81, 0x7fc")
+        e(f"s_add_u32 s81, s81, {BM['B' if buy else 'A']}")
+        e(f"v_mov_b32 v{VBA}, s81")
+        e(f"v_mov_b32 v{VBD}, s79")
+        e(f"ds_or_b32 v{VBA}, v{VBD}")
         e(f"s_or_b32 {K}, {JJS}, 0x80")
         self.logd(K, T[0], LI)
 
@@ -1090,6 +1100,9 @@ class GenD(Gen):
         e(f"v_mbcnt_lo_u32_b32 v{VSL}, -1, 0")
         e(f"v_mbcnt_hi_u32_b32 v{VSL}, -1, v{VSL}")
         e(f"v_mov_b32 v{VZD}, 0")
+        e(f"v_lshlrev_b32 v{VBASE_A}, 2, v{VSL}")
+        e(f"v_add_u32 v{VBASE_B}, {BM['B'] - 252}, v{VBASE_A}")   # lane i: dword w0 - 63 + i
+        e(f"v_add_u32 v{VBASE_A}, {BM['A']}, v{VBASE_A}")         # lane i: dword w0 + i
         e(f"s_mov_b32 {ZERO}, 0")
         e(f"s_mov_b32 {BA}, 0")
         self.next_top("A")
@@ -1145,6 +1158,8 @@ def main():
         f.write("#define FL_PLAN_CLOBBERS_C " + ", ".join(f'"{c}"' for c in CLOBBERS_C) + "\n")
         f.write("#define FL_PLAN_CLOBBERS_D " + ", ".join(f'"{c}"' for c in CLOBBERS_D) + "\n")
         f.write(f"#define FL_DEEP_CAP {DEEP_CAP}\n")
+        f.write(f"#define FL_DEEP_BM {DEEP_BM}\n")
+        f.write(f"#define FL_DEEP_LDS {DEEP_BM + DEEP_BM_BYTES}\n")
 
 
 if __name__ == "__main__":

@@ -881,6 +881,7 @@ struct FlLog {
 
 #include "flow_plan_asm.inc"
 static_assert(FL_DEEP_CAP == DEEP_CAP, "deep plan generated for another DEEP_CAP");
+static_assert(FL_DEEP_BM == DEEP_CAP * 8 && FL_DEEP_LDS <= FC_MAX_SLOTS * 8, "deep plan LDS layout");
 
 
 
@@ -923,6 +924,18 @@ __device__ __forceinline__ void fl_deep_load(const FlowArgs& F, uint32_t h) {
     if (k == DEEP_CAP - 1) a = 1;
     dep[2 * k] = b;
     dep[2 * k + 1] = a;
+  }
+  // the plan's occupancy bitmaps (bit k of dword k >> 5: slot k != 0), bids then asks
+  __syncthreads();
+  uint32_t* bm = dep + FL_DEEP_BM / 4;
+  const uint32_t lane = lane_id();
+  for (uint32_t k0 = (threadIdx.x & ~63u); k0 < DEEP_CAP; k0 += blockDim.x) {
+    const unsigned long long mb = __ballot(dep[2 * (k0 + lane)] != 0);
+    const unsigned long long ma = __ballot(dep[2 * (k0 + lane) + 1] != 0);
+    if (lane < 2) {
+      bm[(k0 >> 5) + lane] = static_cast<uint32_t>(mb >> (32 * lane));
+      bm[DEEP_CAP / 32 + (k0 >> 5) + lane] = static_cast<uint32_t>(ma >> (32 * lane));
+    }
   }
 }
 

@@ -993,9 +993,7 @@ __device__ __forceinline__ void fl_plan_deep(const Dev& D, const FlowArgs& F, ui
 __device__ __forceinline__ void fl_plan_book(const Dev& D, const FlowArgs& F, uint32_t h) {
   const FlowHdr* hd = &F.hdr[h];
   if (uni(hd->ok) == FL_OK_DEEP) {
-#ifndef GOME_XP_ADD_ONLY
     fl_plan_deep(D, F, h);
-#endif
     return;
   }
   __builtin_amdgcn_s_setprio(3);
@@ -1051,11 +1049,7 @@ __device__ __forceinline__ void fl_plan_book(const Dev& D, const FlowArgs& F, ui
 #ifdef GOME_STAMPS
   const unsigned long long sc0 = __builtin_amdgcn_s_memtime(), sr0 = __builtin_amdgcn_s_memrealtime();
 #endif
-#ifdef GOME_XP_ADD_ONLY
-  if (false) {
-#else
   if (uni(hd->ok) == FL_OK_CANCEL) {
-#endif
     asm volatile(FL_PLAN_ASM32C
       : [al0] "+v"(Da.l0), [ah0] "+v"(Da.h0), [al1] "+v"(Da.l1), [ah1] "+v"(Da.h1), [bl0] "+v"(Db.l0),
         [bh0] "+v"(Db.h0), [bl1] "+v"(Db.l1), [bh1] "+v"(Db.h1), [lk] "+v"(lg.lk), [la] "+v"(lg.la),

@@ -59,10 +59,9 @@ PAIR = {"A": (32, 33), "B": (34, 35)}
 ZERO = "s91"                     # W32: stays 0, the high word of the rest amount s[90:91]
 COPY_REST = os.environ.get("GOME_PLAN_COPY", "1") == "1"   # measured at a pinned placement: -2% cycles
 LOOP_OFS = int(os.environ.get("GOME_PLAN_OFS", "0"))  # 4-byte words after the 256-B alignment
-# timing experiments only (tools/build_variant.py): wait for each half-group's records right
-# after issuing them / drop the DEL's LDS wait (wrong results)
+# timing experiment only (tools/build_variant.py): wait for each half-group's records right
+# after issuing them
 SYNC_SMEM = os.environ.get("GOME_PLAN_SYNC_SMEM", "0") == "1"
-DEL_NOWAIT = os.environ.get("GOME_PLAN_DEL_NOWAIT", "0") == "1"
 PF_DIST = int(os.environ.get("GOME_PLAN_PF", "0"))  # L2 prefetch distance in bytes (0: off);
 # k_flow_prep pads ord8 by FL_ORD8_PAD records, which must cover it
 
@@ -719,10 +718,22 @@ class GenC(Gen):
         e(f"v_lshlrev_b32 v{VW}, 3, v{VW}")
         e(f"ds_read_b32 v{VX}, v{VW} offset:4")
 
+    def window_sum(self, lanes: str):
+        """After the window read landed: s-register `lanes` := the sum of v over its cancelled
+        (flagged) entries (each flagged word is v + 2^31; every sum stays below 2^31)."""
+        e = self.e
+        e("s_mov_b64 exec, -1")
+        e(f"v_ashrrev_i32 v{VT}, 31, v{VX}")                  # cancelled entries only
+        e(f"v_and_b32 v{VX}, v{VX}, v{VT}")
+        self.reduce_window(lanes)
+        e(f"s_bitset0_b32 {lanes}, 31")                       # (- cnt * 2^31)
+
     def del_path(self, i: int):
         """DeleteOrder (engine.go:87-116) on the aggregates of level LI: r = clamp(end_m + Xb -
-        G_k, 0, v_m) with G_k = R_k - depth_k read from lane LI >> 1 (one lane read) while the
-        entry's LDS read is in flight, the clamp in lane 0; the window (n_b > 0) out of line."""
+        G_k, 0, v_m).  The first 63 ranks of the window (ranks p + 1 .. of the level's ring:
+        every window but ~2% of them) and the target's entry are read together, G_k = R_k -
+        depth_k comes from lane LI >> 1 while both reads are in flight, then one wait, the
+        window's reduction and the clamp; longer windows finish out of line."""
         e = self.e
         lo, hi = f"s{BUF[i][0]}", f"s{BUF[i][1]}"
         lab = self.lab
@@ -730,17 +741,19 @@ class GenC(Gen):
         aev, aod = PAIR["A"]
         bev, bod = PAIR["B"]
         e(f"{lab(f'D{i}')}:")
-        self.entry_addr(hi)
+        self.entry_addr(hi)                                   # X3 = the entry's byte address
+        e(f"s_and_b32 {X0}, {lo}, 0xffff")                    # n_b
+        e(f"s_lshr_b32 {X1}, {lo}, 16")
+        e(f"s_bfm_b32 {X2}, {X1}, 0")                         # mask = C_k - 1
+        e(f"s_lshr_b32 {T0}, {X3}, 3")                        # p
+        e(f"s_andn2_b32 {X1}, {T0}, {X2}")                    # pbase
+        e(f"s_add_u32 {K}, {T0}, 1")                          # first window rank (mod C_k)
+        e(f"s_min_u32 {L}, {X0}, 63")
+        self.window_read(L, K)
         e(f"s_lshr_b32 {T0}, {LI}, 1")
-        e(f"s_bfm_b64 exec, 1, {T0}")                         # lane LI >> 1 from here on
+        e(f"s_bfm_b64 exec, 1, {T0}")                         # lane LI >> 1
         e(f"v_mov_b32 v{VA}, {X3}")
         e(f"ds_read_b64 v[{VE}:{VM}], v{VA}")                 # {E_m, v_m} (X is clear)
-        e(f"s_and_b32 {X0}, {lo}, 0xffff")                    # n_b
-        e("s_mov_b32 s90, 0")                                 # Xb
-        e(f"s_cmp_lg_u32 {X0}, 0")
-        win, back = lab(f"DW{i}"), lab(f"DWB{i}")
-        e(f"s_cbranch_scc1 {win}")
-        e(f"{back}:")
         # G_k = R_k - depth_k: the level's words of the R / ask / bid pairs (a cached top's lane
         # is 0, its depth is in SGPRs)
         e(f"v_sub_u32 v{VG0}, v{ev}, v{aev}")
@@ -751,13 +764,20 @@ class GenC(Gen):
         e("s_cselect_b64 vcc, -1, 0")
         e(f"v_cndmask_b32 v{VG0}, v{VG0}, v{VG1}, vcc")
         e(f"s_cmp_eq_u32 {LI}, {BA}")
-        e(f"s_cselect_b32 {X1}, {BAD[0]}, 0")
+        e(f"s_cselect_b32 s94, {BAD[0]}, 0")
         e(f"s_cmp_eq_u32 {LI}, {BB}")
-        e(f"s_cselect_b32 {X2}, {BBD[0]}, 0")
-        e(f"s_add_u32 {X1}, {X1}, {X2}")
-        e(f"v_subrev_u32 v{VG0}, {X1}, v{VG0}")               # G_k
-        if not DEL_NOWAIT:
-            e("s_waitcnt lgkmcnt(0)")
+        e(f"s_cselect_b32 s95, {BBD[0]}, 0")
+        e(f"s_add_u32 s94, s94, s95")
+        e(f"v_subrev_u32 v{VG0}, s94, v{VG0}")                # G_k
+        e("s_waitcnt lgkmcnt(0)")
+        self.window_sum(L)
+        e(f"s_mov_b32 s90, {L}")                              # Xb
+        win, back = lab(f"DW{i}"), lab(f"DWB{i}")
+        e(f"s_cmp_gt_u32 {X0}, 63")
+        e(f"s_cbranch_scc1 {win}")
+        e(f"{back}:")
+        e(f"s_lshr_b32 {T0}, {LI}, 1")
+        e(f"s_bfm_b64 exec, 1, {T0}")
         # a = E_m + v_m + Xb (< 2^31: the window's makers arrived after m); r = a - G_k clamped
         # to [0, v_m]; X_m := 1
         e(f"v_add_u32 v{VE}, v{VE}, v{VM}")
@@ -800,36 +820,24 @@ class GenC(Gen):
             self.dispatch((i + 1) % NS, False)
         e(f"{lab(f'DZ{i}')}:")
         self.dispatch((i + 1) % NS, False)
-        # the window (out of line): Xb = sum of xv over ranks p + 1 .. p + n_b (mod C_k) of the
-        # level's ring, 63 lanes at a time
+        # windows beyond 63 targets (out of line): the rest of the ranks, 63 lanes at a time
         blk = [f"{win}:"]
         self.slow.append(blk)
         sv = self.out
         self.out = blk
-        e(f"s_lshr_b32 {X3}, {X3}, 3")                        # p
-        e(f"s_lshr_b32 {X1}, {lo}, 16")
-        e(f"s_bfm_b32 {X2}, {X1}, 0")                         # mask = C_k - 1
-        e(f"s_andn2_b32 {X1}, {X3}, {X2}")                    # pbase
-        e(f"s_add_u32 {X3}, {X3}, 1")                         # first window rank (mod C_k)
-        e(f"s_mov_b32 {K}, 0")
+        e("s_mov_b32 s92, 63")
         loop = lab(f"DWL{i}")
         e(f"{loop}:")
-        e(f"s_sub_u32 {L}, {X0}, {K}")
+        e(f"s_sub_u32 {L}, {X0}, s92")
         e(f"s_min_u32 {L}, {L}, 63")
-        e(f"s_add_u32 {T0}, {X3}, {K}")
+        e(f"s_add_u32 {T0}, {K}, s92")
         self.window_read(L, T0)
         e("s_waitcnt lgkmcnt(0)")
-        e("s_mov_b64 exec, -1")
-        e(f"v_ashrrev_i32 v{VT}, 31, v{VX}")                  # cancelled entries only
-        e(f"v_and_b32 v{VX}, v{VX}, v{VT}")
-        self.reduce_window(L)
-        e(f"s_bitset0_b32 {L}, 31")                           # (- cnt * 2^31)
+        self.window_sum(L)
         e(f"s_add_u32 s90, s90, {L}")
-        e(f"s_add_u32 {K}, {K}, 63")
-        e(f"s_cmp_lt_u32 {K}, {X0}")
+        e("s_add_u32 s92, s92, 63")
+        e(f"s_cmp_lt_u32 s92, {X0}")
         e(f"s_cbranch_scc1 {loop}")
-        e(f"s_lshr_b32 {T0}, {LI}, 1")
-        e(f"s_bfm_b64 exec, 1, {T0}")
         e(f"s_branch {back}")
         self.out = sv
 

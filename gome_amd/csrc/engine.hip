@@ -585,9 +585,18 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
     k_fc_hash_count<<<dim3(px, nb), 256, 0, st>>>(D, B, R);
     k_fc_hash_first<<<dim3(px, nb), 256, 0, st>>>(D, B, R);
     k_fc_resolve<<<dim3(px, nb), 256, 0, st>>>(D, B, R);
-    if (wide) k_fc_oldwalk_wide<<<dim3(FL_CAP, nb), 64, 0, st>>>(D, R);
-    else k_fc_oldwalk_book<<<nb, 1024, 0, st>>>(D, R);
-    k_fc_pass<<<nb, FC_PASS_T, 0, st>>>(D, B, R);
+    if (wide) {  // the head: tile-parallel ranks, windows, layout and records
+      k_fc_oldwalk_wide<<<dim3(FL_CAP, nb), 64, 0, st>>>(D, R);
+      k_fc_pcnt<<<dim3(FL_SORT_GRID, nb), FL_TILE, 0, st>>>(D, B, R);
+      k_fc_pscan<<<nb, FL_CAP, 0, st>>>(D, R);
+      k_fc_prank<<<dim3(FL_SORT_GRID, nb), FL_TILE, 0, st>>>(D, B, R);
+      k_fc_pwin<<<dim3(px, nb), 256, 0, st>>>(D, B, R);
+      k_fc_playout<<<nb, 1024, 0, st>>>(D, R);
+      k_fc_precs<<<dim3(px, nb), 256, 0, st>>>(D, B, R);
+    } else {
+      k_fc_oldwalk_book<<<nb, 1024, 0, st>>>(D, R);
+      k_fc_pass<<<nb, FC_PASS_T, 0, st>>>(D, B, R);
+    }
     k_fc_unmark<<<dim3(px, nb), 256, 0, st>>>(D, B, R);
     k_fc_route<<<ceil_div(nb, 256), 256, 0, st>>>(D, R);
   };
@@ -662,7 +671,9 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
     k_flow_plan_tail<<<nh_tail, 64, 0, hot_stream>>>(D, FT);
     k_flow_plan_tail_c<<<nh_tail, 64, FC_TAIL_LDS, hot_stream>>>(D, FT);
     k_flow_plan_tail_cb<<<nh_tail, 64, fc_ring_lds, hot_stream>>>(D, FT);
-    k_flow_plan_tail_d<<<nh_tail, 256, fc_ring_lds, hot_stream>>>(D, FT);
+    // (only candidates below DEEP_SLOTS can be deep: no more whole-CU blocks than that, so the
+    // cold kernel launched beside it is not held back waiting for CUs)
+    k_flow_plan_tail_d<<<std::min<uint32_t>(nh_tail, DEEP_SLOTS - FL_HEAD), 256, FL_DEEP_LDS, hot_stream>>>(D, FT);
     k_flow_sort<<<nh_tail, FL_SORT_T, 0, hot_stream>>>(D, FT);
     k_flow_level<<<nh_tail, FL_LEVEL_T, 0, hot_stream>>>(D, FT);
     deep_sort_level(FT, 32, hot_stream);

@@ -464,6 +464,221 @@ __global__ __launch_bounds__(FC_PASS_T) void k_fc_pass(Dev D, BatchArgs B, FlowA
   if (tid == 0) F.hdr[h].nslot = nslot;
 }
 
+// ---- prep 5, tile-parallel (the head books, whose segments hold up to ~10^6 records) --------
+// The same quantities as k_fc_pass, computed as a stable counting pass over 1024-record tiles:
+// per tile the targeted ADDs of each level (F.tcnt, free before the plan), an exclusive scan over
+// the tiles from each level's old targets, then every targeted ADD's rank and every DEL's count
+// of targets that arrived before it; the windows (which need the ranks of targets in other
+// tiles), the ring layout and image, and the W32C records follow as separate launches.
+__device__ __forceinline__ bool fc_targeted_add(const FlowArgs& F, const FlowHdr& hd, uint32_t i, uint32_t& k) {
+  if (!F.fc_tg[hd.beg + i]) return false;
+  k = static_cast<uint32_t>(F.ord8[hd.obase + i] >> 32) & 127u;
+  return true;
+}
+
+__global__ __launch_bounds__(FL_TILE) void k_fc_pcnt(Dev D, BatchArgs B, FlowArgs F) {
+  __shared__ uint32_t wc[FL_TILE_W][FL_CAP];
+  const uint32_t h = F.h0 + blockIdx.y, tid = threadIdx.x, w = tid >> 6;
+  if (h >= fl_hend(D, F) || !fc_book(F, h)) return;
+  const FlowHdr hd = F.hdr[h];
+  const uint32_t n = hd.end - hd.beg, ntile = (n + FL_TILE - 1) / FL_TILE;
+  for (uint32_t tl = blockIdx.x; tl < ntile; tl += gridDim.x) {
+    for (uint32_t i = tid; i < FL_TILE_W * FL_CAP; i += FL_TILE) wc[i / FL_CAP][i % FL_CAP] = 0;
+    __syncthreads();
+    const uint32_t i = tl * FL_TILE + tid;
+    uint32_t k = 0, cnt;
+    const bool isa = i < n && fc_targeted_add(F, hd, i, k);
+    const uint32_t rank = fl_tile_rank(k, isa, cnt);
+    if (isa && rank == 0) wc[w][k] = cnt;
+    __syncthreads();
+    if (tid < FL_CAP) {
+      uint32_t c = 0;
+      for (uint32_t ww = 0; ww < FL_TILE_W; ++ww) c += wc[ww][tid];
+      F.tcnt[(static_cast<size_t>(h) * F.maxt + tl) * FL_CAP + tid] = c;
+    }
+    __syncthreads();
+  }
+}
+
+// Per book: tile offsets per level from its old targets (in place); the level's largest window
+// + 1 starts at max(old targets, 1) in FlowLvl::cring (the layout kernel rounds it up).
+__global__ __launch_bounds__(FL_CAP) void k_fc_pscan(Dev D, FlowArgs F) {
+  const uint32_t h = F.h0 + blockIdx.x, k = threadIdx.x;
+  if (h >= fl_hend(D, F) || !fc_book(F, h)) return;
+  const FlowHdr& hd = F.hdr[h];
+  FlowLvl* LV = F.lvl + h * FL_CAP;
+  const uint32_t ntile = (hd.end - hd.beg + FL_TILE - 1) / FL_TILE;
+  const bool lv = k >= 1 && k <= hd.nl;
+  uint32_t run = lv ? LV[k].c_old : 0u;
+  if (lv) LV[k].cring = max(run, 1u);
+  uint32_t* tc = F.tcnt + static_cast<size_t>(h) * F.maxt * FL_CAP;
+  for (uint32_t tl = 0; tl < ntile; ++tl) {
+    const uint32_t v = tc[tl * FL_CAP + k];
+    tc[tl * FL_CAP + k] = run;
+    run += v;
+  }
+}
+
+// Targeted ADDs' ranks; a DEL's count of its level's targets that arrived before it (in nb).
+__global__ __launch_bounds__(FL_TILE) void k_fc_prank(Dev D, BatchArgs B, FlowArgs F) {
+  __shared__ uint32_t wc[FL_TILE_W][FL_CAP];
+  const uint32_t h = F.h0 + blockIdx.y, tid = threadIdx.x, w = tid >> 6;
+  if (h >= fl_hend(D, F) || !fc_book(F, h)) return;
+  const FlowHdr hd = F.hdr[h];
+  const uint32_t n = hd.end - hd.beg, ntile = (n + FL_TILE - 1) / FL_TILE;
+  const uint32_t* tc = F.tcnt + static_cast<size_t>(h) * F.maxt * FL_CAP;
+  for (uint32_t tl = blockIdx.x; tl < ntile; tl += gridDim.x) {
+    for (uint32_t i = tid; i < FL_TILE_W * FL_CAP; i += FL_TILE) wc[i / FL_CAP][i % FL_CAP] = 0;
+    __syncthreads();
+    const uint32_t i = tl * FL_TILE + tid, b = hd.beg + i;
+    uint32_t k = 0;
+    bool isa = false, isd = false;
+    if (i < n) {
+      isa = fc_targeted_add(F, hd, i, k);
+      if (!isa && prep_at(B, b).action == GOME_DEL) {
+        const FcDel d = F.fc_del[b];
+        if (d.kind != FC_NONE) { isd = true; k = d.li; }
+      }
+    }
+    // ballot of the wave's targeted ADDs at this lane's level (DEL lanes take part in the
+    // level bits only)
+    unsigned long long same = __ballot(isa);
+#pragma unroll
+    for (uint32_t bit = 0; bit < 7; ++bit) {
+      const unsigned long long bb = __ballot((k >> bit) & 1u);
+      same &= ((k >> bit) & 1u) ? bb : ~bb;
+    }
+    const uint32_t before_w = __popcll(same & lt_mask());
+    if (isa && before_w == 0) wc[w][k] = __popcll(same);
+    __syncthreads();
+    if (tid < FL_CAP) {  // waves' counts -> offsets from the tile's offset of the level
+      uint32_t r = tc[tl * FL_CAP + tid];
+      for (uint32_t ww = 0; ww < FL_TILE_W; ++ww) {
+        const uint32_t c = wc[ww][tid];
+        wc[ww][tid] = r;
+        r += c;
+      }
+    }
+    __syncthreads();
+    if (isa) F.fc_rank[b] = wc[w][k] + before_w;
+    if (isd) F.fc_del[b].nb = wc[w][k] + before_w;  // (arrived; k_fc_pwin turns it into the window)
+    __syncthreads();
+  }
+}
+
+// Windows: nb = arrived - rank of the target - 1, the level's largest window + 1.
+__global__ __launch_bounds__(256) void k_fc_pwin(Dev D, BatchArgs B, FlowArgs F) {
+  const uint32_t h = F.h0 + blockIdx.y;
+  if (h >= fl_hend(D, F) || !fc_book(F, h)) return;
+  const FlowHdr hd = F.hdr[h];
+  FlowLvl* LV = F.lvl + h * FL_CAP;
+  uint32_t b0, b1, bad = 0;
+  fc_slice(hd, blockIdx.x, gridDim.x, b0, b1);
+  for (uint32_t b = b0 + threadIdx.x; b < b1; b += blockDim.x) {
+    if (prep_at(B, b).action != GOME_DEL) continue;
+    const FcDel d = F.fc_del[b];
+    if (d.kind == FC_NONE) continue;
+    const uint32_t rk = d.kind == FC_NEW ? F.fc_rank[d.tgt] : d.rank;
+    const uint32_t nb = d.nb - rk - 1u;
+    F.fc_del[b].rank = rk;
+    F.fc_del[b].nb = nb;
+    atomicMax(&LV[d.li].cring, nb + 1u);
+    if (nb >= 0xFFFFu) bad = FC_BAD_RING;
+  }
+  if (bad) fc_decline(F, h, bad);
+}
+
+// Per book: ring layout (power-of-two capacities, largest first), the image (bump-allocated,
+// zeroed); declines a book whose ring does not fit.
+__global__ __launch_bounds__(1024) void k_fc_playout(Dev D, FlowArgs F) {
+  __shared__ uint32_t nslot_s, bad_s;
+  const uint32_t h = F.h0 + blockIdx.x, tid = threadIdx.x;
+  if (h >= fl_hend(D, F) || !fc_book(F, h)) return;
+  FlowLvl* LV = F.lvl + h * FL_CAP;
+  const uint32_t nl = F.hdr[h].nl;
+  if (tid == 0) {
+    const uint32_t cap = F.fc_ring_cap;
+    uint32_t off = 0, top = 1, mw = 0, bad = 0;
+    for (uint32_t q = 1; q <= nl; ++q) {
+      const uint32_t cm = LV[q].cring;
+      mw = max(mw, cm);
+      uint32_t c = 1;
+      while (c < cm && c <= cap) c <<= 1;
+      LV[q].cring = c;
+      off += c;
+      top = max(top, c);
+    }
+    if (off + 1 > cap) {
+      bad = FC_BAD_RING;  // (+ the dummy entry of untargeted ADDs and no-op records)
+    } else {
+      off = 0;
+      for (uint32_t c = top; c; c >>= 1)
+        for (uint32_t q = 1; q <= nl; ++q)
+          if (LV[q].cring == c) {
+            LV[q].rbase = off;
+            off += c;
+          }
+    }
+    const uint32_t ns = off + 1;
+    if (!bad) {
+      const uint32_t base = atomicAdd(F.fc_img_bump, ns);
+      if (static_cast<unsigned long long>(base) + ns > F.fc_img_cap) {
+        bad = FC_BAD_RING;
+      } else {
+        F.hdr[h].fc_img = base;
+        F.hdr[h].fc_big = ns > FC_TAIL_SLOTS ? 1u : 0u;
+      }
+    }
+    F.hdr[h].ncancel = mw;
+    F.hdr[h].nslot = ns;
+    if (bad) fc_decline(F, h, bad);
+    nslot_s = ns;
+    bad_s = bad;
+  }
+  __syncthreads();
+  if (bad_s) return;
+  uint2* img = F.fc_img + F.hdr[h].fc_img;
+  for (uint32_t x = tid; x < nslot_s; x += blockDim.x) img[x] = make_uint2(0u, 0u);
+}
+
+// The W32C records (and the old targets' image entries), tile-parallel.
+__global__ __launch_bounds__(256) void k_fc_precs(Dev D, BatchArgs B, FlowArgs F) {
+  const uint32_t h = F.h0 + blockIdx.y;
+  if (h >= fl_hend(D, F) || !fc_book(F, h)) return;
+  const FlowHdr hd = F.hdr[h];
+  const FlowLvl* LV = F.lvl + h * FL_CAP;
+  const uint32_t n = hd.end - hd.beg, npad = (8u - (n & 7u)) & 7u, dummy = hd.nslot - 1;
+  uint2* img = F.fc_img + hd.fc_img;
+  const uint32_t tot = n + npad;
+  const uint32_t i0 = static_cast<uint32_t>(static_cast<uint64_t>(tot) * blockIdx.x / gridDim.x);
+  const uint32_t i1 = static_cast<uint32_t>(static_cast<uint64_t>(tot) * (blockIdx.x + 1) / gridDim.x);
+  for (uint32_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
+    const uint32_t b = hd.beg + i;
+    unsigned long long rec = static_cast<unsigned long long>(dummy << 7) << 32;  // no-op
+    if (i < n) {
+      const unsigned long long w32 = F.ord8[hd.obase + i];
+      const uint32_t hi = static_cast<uint32_t>(w32 >> 32), k = hi & 127u;
+      const uint32_t tg = F.fc_tg[b];
+      if (k) {  // an admitted ADD (32-bit record: level, volume in units of g, SALE bit 31)
+        const uint32_t slot = tg ? LV[k].rbase + (F.fc_rank[b] & (LV[k].cring - 1u)) : dummy;
+        rec = (static_cast<unsigned long long>(k | (slot << 7) | (hi & 0x80000000u)) << 32) |
+              static_cast<uint32_t>(w32);
+      } else if (prep_at(B, b).action == GOME_DEL) {
+        const FcDel d = F.fc_del[b];
+        if (d.kind != FC_NONE) {
+          const uint32_t kk = d.li, cr = LV[kk].cring, slot = LV[kk].rbase + (d.rank & (cr - 1u));
+          const bool sale = prep_at(B, b).side == GOME_SALE;
+          const uint32_t lgc = 31u - __clz(cr);
+          rec = (static_cast<unsigned long long>(kk | (slot << 7) | (sale ? 1u << 29 : 0u) | (3u << 30)) << 32) |
+                (d.nb | (lgc << 16));
+          if (d.kind == FC_OLD) img[slot] = make_uint2(d.oend - d.ov, d.ov);  // {E, v}, not cancelled
+        }
+      }
+    }
+    F.ord8[hd.obase + i] = rec;
+  }
+}
+
 // ---- prep 6: books declined by the cancel prep go to the legacy hot / cold kernels: drop
 // their old targets' marks and route them there (FlowHdr::ok = 0)
 __global__ __launch_bounds__(256) void k_fc_unmark(Dev D, BatchArgs B, FlowArgs F) {

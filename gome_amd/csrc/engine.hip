@@ -297,6 +297,8 @@ gome_status gome_engine::init(const gome_config& c) {
   }
   HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_match_hot),
                              hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(HOT_LDS_BYTES)));
+  HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_match),
+                             hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(COLD_LDS_BYTES)));
   // the head plans hold a cancel book's LDS ring (match_flow_cancel.h)
   {
     int lds = 0;
@@ -411,19 +413,22 @@ gome_status gome_engine::init(const gome_config& c) {
   // deep books (match_flow_deep.h): per deep slot
   F.dmaxt = F.maxt;
   F.dtmaxt = ceil_div(F.maxt, 8);
-  if (!alloc(&F.dlvl, static_cast<size_t>(DEEP_SLOTS) * DEEP_CAP, "deep level tables") ||
-      !alloc(&F.dlvout, static_cast<size_t>(DEEP_SLOTS) * DEEP_CAP, "deep final levels") ||
-      !alloc(&F.dh_key, static_cast<size_t>(DEEP_SLOTS) * DEEP_HASH, "deep price sets") ||
-      !alloc(&F.dh_val, static_cast<size_t>(DEEP_SLOTS) * DEEP_HASH, "deep price levels") ||
-      !alloc(&F.dscr, DEEP_SLOTS, "deep prep scratch") ||
-      !alloc(&F.dtcnt, (static_cast<size_t>(FL_HEAD) * F.dmaxt + static_cast<size_t>(DEEP_SLOTS - FL_HEAD) * F.dtmaxt) * FL_CAP,
+  // one deep slot per possible candidate (a book with >= 2^FLOW_MIN_LOG2 orders), at most MAX_FLOW
+  F.dslots = static_cast<uint32_t>(std::min<uint64_t>(MAX_FLOW, std::max<uint64_t>(FL_HEAD + 1, (nb >> FLOW_MIN_LOG2) + FL_HEAD)));
+  const size_t ds = F.dslots;
+  if (!alloc(&F.dlvl, ds * DEEP_CAP, "deep level tables") ||
+      !alloc(&F.dlvout, ds * DEEP_CAP, "deep final levels") ||
+      !alloc(&F.dh_key, ds * DEEP_HASH, "deep price sets") ||
+      !alloc(&F.dh_val, ds * DEEP_HASH, "deep price levels") ||
+      !alloc(&F.dscr, ds, "deep prep scratch") || !alloc(&F.dslot_n, 1, "deep slot count") ||
+      !alloc(&F.dtcnt, (static_cast<size_t>(FL_HEAD) * F.dmaxt + (ds - FL_HEAD) * F.dtmaxt) * FL_CAP,
              "deep sort tile counts") ||
-      !alloc(&F.dslot_h, DEEP_SLOTS, "deep slot books") ||
+      !alloc(&F.dslot_h, ds, "deep slot books") ||
       !alloc(&F.tlog, ntouch, "deep sort pass"))
     return GOME_E_CAPACITY;
   // the price sets start empty; each batch's deep books clear theirs when done
-  HIPCHK(hipMemsetAsync(F.dh_key, 0, sizeof(unsigned long long) * DEEP_SLOTS * DEEP_HASH, stream));
-  HIPCHK(hipMemsetAsync(F.dh_val, 0xFF, sizeof(uint32_t) * DEEP_SLOTS * DEEP_HASH, stream));
+  HIPCHK(hipMemsetAsync(F.dh_key, 0, sizeof(unsigned long long) * ds * DEEP_HASH, stream));
+  HIPCHK(hipMemsetAsync(F.dh_val, 0xFF, sizeof(uint32_t) * ds * DEEP_HASH, stream));
   HIPCHK(hipMemsetAsync(F.hdr, 0, sizeof(FlowHdr) * MAX_FLOW, stream));
   HIPCHK(hipMemsetAsync(d_pend, 0, sizeof(PendEnt) * nb, stream));
   if (D.idx_mask >= PEND) return fail(GOME_E_INVAL, "gome_config.max_nodes too large (index > 2^31 slots)");
@@ -552,7 +557,7 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   FH1.h0 = 1; FH1.h1 = FL_HEAD; FH1.tb = 2;
   FT.h0 = FL_HEAD; FT.h1 = MAX_FLOW; FT.tb = FL_HEAD + 3;
   FH.ds0 = 0; FH.ds1 = FL_HEAD; FH0.ds0 = 0; FH0.ds1 = 1; FH1.ds0 = 1; FH1.ds1 = FL_HEAD;
-  FT.ds0 = FL_HEAD; FT.ds1 = DEEP_SLOTS;
+  FT.ds0 = FL_HEAD; FT.ds1 = F.dslots;
   // the ranges' books with DELs count and place their events through a second toff region
   FlowArgs FH0c = FH0, FH1c = FH1, FTc = FT;
   FH0c.tb += FC_TOFF; FH1c.tb += FC_TOFF; FTc.tb += FC_TOFF;
@@ -563,8 +568,9 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   // segmentation, beside k_prep
   HIPCHK(hipMemsetAsync(F.fc_img_bump, 0, 4, s));  // (both ranges' cancel preps follow)
   // deep books: slots, price sets and prep scratch of both ranges
-  HIPCHK(hipMemsetAsync(F.dslot_h, 0xFF, 4 * DEEP_SLOTS, s));
-  HIPCHK(hipMemsetAsync(F.dscr, 0, sizeof(FlPrepScr) * DEEP_SLOTS, s));
+  HIPCHK(hipMemsetAsync(F.dslot_h, 0xFF, 4ull * F.dslots, s));
+  HIPCHK(hipMemsetAsync(F.dslot_n, 0, 4, s));
+  HIPCHK(hipMemsetAsync(F.dscr, 0, sizeof(FlPrepScr) * F.dslots, s));
   HIPCHK(hipEventRecord(seg_done, s));
   HIPCHK(hipStreamWaitEvent(flow_stream, seg_done, 0));
   HIPCHK(hipMemsetAsync(F.pscr, 0, sizeof(FlPrepScr) * FL_HEAD, flow_stream));
@@ -573,7 +579,7 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   k_flow_prep_c<<<dim3(FL_PG, nh_head), FL_PREP_T, 0, flow_stream>>>(D, B, FH);
   // head books with more levels than lanes: the deep prep (match_flow_deep.h)
   auto deep_prep = [&](const FlowArgs& R, uint32_t px, hipStream_t st) {
-    const uint32_t ns = R.ds1 - R.ds0;
+    const uint32_t ns = std::min<uint32_t>(R.ds1 - R.ds0, DEEP_GRID_T);  // (blocks walk the slots)
     k_deep_prep_a<<<dim3(px, ns), FL_PREP_T, 0, st>>>(D, B, R);
     k_deep_prep_b<<<ns, FL_PREP_T, DEEP_CAP * 8, st>>>(D, B, R);
     k_deep_prep_c<<<dim3(px, ns), FL_PREP_T, 0, st>>>(D, B, R);
@@ -620,17 +626,19 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   HIPCHK(hipStreamWaitEvent(flow_stream, fork, 0));  // (k_prep, the gather bump)
   // deep books: the two-pass level sort and the per-level reconstruction, then the writes
   auto deep_sort_level = [&](const FlowArgs& R, uint32_t tiles, hipStream_t st) {
-    const uint32_t ns = R.ds1 - R.ds0;
+    const uint32_t ns = std::min<uint32_t>(R.ds1 - R.ds0, DEEP_GRID_T);  // (blocks walk the slots)
     k_deep_sort_cnt<1><<<dim3(tiles, ns), FL_TILE, 0, st>>>(D, R);
     k_deep_sort_scan<<<ns, FL_CAP, 0, st>>>(D, R);
     k_deep_sort_scatter<1><<<dim3(tiles, ns), FL_TILE, 0, st>>>(D, R);
     k_deep_sort_cnt<2><<<dim3(tiles, ns), FL_TILE, 0, st>>>(D, R);
     k_deep_sort_scan<<<ns, FL_CAP, 0, st>>>(D, R);
     k_deep_sort_scatter<2><<<dim3(tiles, ns), FL_TILE, 0, st>>>(D, R);
+    k_deep_runs<<<dim3(64, ns), 256, 0, st>>>(D, R);
     k_deep_level<<<dim3(DEEP_GRID, ns), 64, 0, st>>>(D, R);
   };
   auto deep_write = [&](const FlowArgs& R, hipStream_t st) {
-    const uint32_t ns = R.ds1 - R.ds0;
+    const uint32_t ns = std::min<uint32_t>(R.ds1 - R.ds0, DEEP_GRID_T);  // (blocks walk the slots)
+    k_deep_claim<<<ns, DEEP_CLAIM_T, 0, st>>>(D, B, R);
     k_deep_write_lv<<<dim3(DEEP_GRID, ns), 64, 0, st>>>(D, B, R);
     k_deep_write_fin<<<ns, DEEP_FIN_T, 0, st>>>(D, R);
   };
@@ -659,39 +667,12 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   head_recon(FH0, 1, flow_stream);
   head_recon_c(FH0, FH0c, 1, flow_stream);
   HIPCHK(hipEventRecord(joinf, flow_stream));
-  // The tail's chain and the legacy hot kernels share the third stream: HIP maps more
-  // streams than hardware queues (4 per process) onto shared queues, which would serialise
-  // them behind the head.
+  // Streams (HIP maps more streams than its 4 hardware queues per process onto shared queues,
+  // which would serialise them): the hottest book on the flow stream; the other head books'
+  // plans (whole CUs, from the head's prep on) and then the legacy hot kernels on the hot
+  // stream; the tail's prep, the cold books and the tail's plans and reconstruction on the
+  // caller's stream.  Each chain ends well before the hottest book's.
   HIPCHK(hipStreamWaitEvent(hot_stream, fork, 0));
-  if (nh_tail) {
-    k_flow_prep<<<nh_tail, FL_PREP_T, 0, hot_stream>>>(D, B, FT);
-    deep_prep(FT, 8, hot_stream);
-    cancel_prep(FT, nh_tail, 1, false, hot_stream);
-    HIPCHK(hipEventRecord(prep_t, hot_stream));
-    k_flow_plan_tail<<<nh_tail, 64, 0, hot_stream>>>(D, FT);
-    k_flow_plan_tail_c<<<nh_tail, 64, FC_TAIL_LDS, hot_stream>>>(D, FT);
-    k_flow_plan_tail_cb<<<nh_tail, 64, fc_ring_lds, hot_stream>>>(D, FT);
-    // (only candidates below DEEP_SLOTS can be deep: no more whole-CU blocks than that, so the
-    // cold kernel launched beside it is not held back waiting for CUs)
-    k_flow_plan_tail_d<<<std::min<uint32_t>(nh_tail, DEEP_SLOTS - FL_HEAD), 256, FL_DEEP_LDS, hot_stream>>>(D, FT);
-    k_flow_sort<<<nh_tail, FL_SORT_T, 0, hot_stream>>>(D, FT);
-    k_flow_level<<<nh_tail, FL_LEVEL_T, 0, hot_stream>>>(D, FT);
-    deep_sort_level(FT, 32, hot_stream);
-    k_flow_toff<FL_OK_ADD><<<1, 1024, 0, hot_stream>>>(D, FT);
-    k_flow_count<<<1024, 256, 0, hot_stream>>>(D, B, FT);
-    k_flow_write<<<nh_tail, FL_WRITE_T, 0, hot_stream>>>(D, B, FT);
-    deep_write(FT, hot_stream);
-    // the tail's events into the arena now (k_ev_scatter places them after the scan)
-    k_flow_events_arena<<<1024, 256, 0, hot_stream>>>(D, B, FT);
-    k_fc_level_book<<<nh_tail, 1024, 0, hot_stream>>>(D, FT);
-    k_flow_toff<FL_OK_CANCEL><<<1, 1024, 0, hot_stream>>>(D, FTc);
-    k_fc_count<<<1024, 256, 0, hot_stream>>>(D, B, FTc);
-    k_fc_write_book<<<nh_tail, FL_WRITE_T, 0, hot_stream>>>(D, B, FTc);
-    k_fc_events<<<1024, 256, 0, hot_stream>>>(D, B, FTc);
-  } else {
-    HIPCHK(hipEventRecord(prep_t, hot_stream));
-  }
-  // the other head books: plan, reconstruction and events (into the arena) after the tail
   HIPCHK(hipStreamWaitEvent(hot_stream, prep_h, 0));
   if (nh_near) {
     k_flow_plan_near<<<nh_near, 256, fc_ring_lds, hot_stream>>>(D, FH1);
@@ -699,8 +680,15 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
     head_recon_c(FH1, FH1c, nh_near, hot_stream);
     k_flow_events_arena<<<1024, 256, 0, hot_stream>>>(D, B, FH1);
   }
+  if (nh_tail) {
+    k_flow_prep<<<nh_tail, FL_PREP_T, 0, s>>>(D, B, FT);
+    deep_prep(FT, 8, s);
+    cancel_prep(FT, nh_tail, 1, false, s);
+  }
+  HIPCHK(hipEventRecord(prep_t, s));
   // legacy hot path (books the flow path declined); it and the cold kernel read the preps'
   // routing decisions (FlowHdr::ok)
+  HIPCHK(hipStreamWaitEvent(hot_stream, prep_t, 0));
   HIPCHK(hipEventRecord(S.evh0, hot_stream));
   const uint32_t nleg = std::min<uint32_t>(MAX_HOT, grid);
   k_match_hot<<<nleg, 64, HOT_LDS_BYTES, hot_stream>>>(D, B, d_pend, d_resume, F.hdr);
@@ -708,12 +696,31 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   k_match_resume<<<nleg, 64, 0, hot_stream>>>(D, B, d_resume);
   k_pend_apply<<<dim3(8, 64), 256, 0, hot_stream>>>(D, d_pend, d_seg_start, d_seg_order, B);
   HIPCHK(hipEventRecord(join, hot_stream));
-  HIPCHK(hipStreamWaitEvent(s, prep_h, 0));
-  HIPCHK(hipStreamWaitEvent(s, prep_t, 0));
   HIPCHK(hipEventRecord(S.evc0, s));
-  k_match<<<std::min<uint32_t>(ceil_div(grid, COLD_WAVES), COLD_BLOCKS), 64 * COLD_WAVES, 0, s>>>(
+  k_match<<<std::min<uint32_t>(ceil_div(grid, COLD_WAVES), COLD_BLOCKS), 64 * COLD_WAVES, COLD_LDS_BYTES, s>>>(
       D, B, &F.hdr[0].ok, sizeof(FlowHdr) / sizeof(uint32_t));
   HIPCHK(hipEventRecord(S.evc1, s));
+  if (nh_tail) {  // the tail's plans and reconstruction
+    k_flow_plan_tail<<<nh_tail, 64, 0, s>>>(D, FT);
+    k_flow_plan_tail_c<<<nh_tail, 64, FC_TAIL_LDS, s>>>(D, FT);
+    k_flow_plan_tail_cb<<<nh_tail, 64, fc_ring_lds, s>>>(D, FT);
+    // (its blocks walk the tail's deep slots: at most DEEP_GRID_T whole-CU blocks)
+    k_flow_plan_tail_d<<<std::min<uint32_t>(nh_tail, DEEP_GRID_T), 256, FL_DEEP_LDS, s>>>(D, FT);
+    k_flow_sort<<<nh_tail, FL_SORT_T, 0, s>>>(D, FT);
+    k_flow_level<<<nh_tail, FL_LEVEL_T, 0, s>>>(D, FT);
+    deep_sort_level(FT, 32, s);
+    k_flow_toff<FL_OK_ADD><<<1, 1024, 0, s>>>(D, FT);
+    k_flow_count<<<1024, 256, 0, s>>>(D, B, FT);
+    k_flow_write<<<nh_tail, FL_WRITE_T, 0, s>>>(D, B, FT);
+    deep_write(FT, s);
+    // the tail's events into the arena now (k_ev_scatter places them after the scan)
+    k_flow_events_arena<<<1024, 256, 0, s>>>(D, B, FT);
+    k_fc_level_book<<<nh_tail, 1024, 0, s>>>(D, FT);
+    k_flow_toff<FL_OK_CANCEL><<<1, 1024, 0, s>>>(D, FTc);
+    k_fc_count<<<1024, 256, 0, s>>>(D, B, FTc);
+    k_fc_write_book<<<nh_tail, FL_WRITE_T, 0, s>>>(D, B, FTc);
+    k_fc_events<<<1024, 256, 0, s>>>(D, B, FTc);
+  }
   HIPCHK(hipStreamWaitEvent(s, join, 0));
   HIPCHK(hipStreamWaitEvent(s, joinf, 0));
 

@@ -691,7 +691,10 @@ __device__ __forceinline__ void wave_flush(WaveCtx& W) {
 // Cold books with few levels work on an LDS copy of their level array (every level search,
 // insert and update is then an LDS access instead of an HBM round trip); written back by
 // wave_finish.
-constexpr uint32_t COLD_LDS_LVLS = 128;
+#ifndef GOME_COLD_LDS_LVLS
+#define GOME_COLD_LDS_LVLS 128
+#endif
+constexpr uint32_t COLD_LDS_LVLS = GOME_COLD_LDS_LVLS;
 
 __device__ __forceinline__ void wave_next_book(WaveCtx& W, uint32_t sym) {
   W.sym = sym;
@@ -737,11 +740,12 @@ __device__ __forceinline__ void wave_init(WaveCtx& W, const Dev& D, const BatchA
 #define GOME_COLD_WAVES 8
 #endif
 constexpr uint32_t COLD_WAVES = GOME_COLD_WAVES;
+constexpr uint32_t COLD_LDS_BYTES = COLD_WAVES * COLD_LDS_LVLS * sizeof(Level);
 __global__ __launch_bounds__(64 * COLD_WAVES) void k_match(Dev D, BatchArgs B, const uint32_t* flow_ok, uint32_t ok_stride) {
   if (D.st->err & ERR_INPUT) return;
   const uint32_t nseg = D.st->nseg, nhot = D.st->nhot;
   const uint32_t nw = blockDim.x >> 6, stride = gridDim.x * nw;
-  __shared__ Level lvl_lds[COLD_WAVES][COLD_LDS_LVLS];
+  extern __shared__ Level lvl_lds[];  // COLD_WAVES x COLD_LDS_LVLS (dynamic: COLD_LDS_BYTES)
   WaveCtx W;
   bool started = false;
   for (uint32_t i = blockIdx.x * nw + (threadIdx.x >> 6); i < nseg; i += stride) {
@@ -750,7 +754,7 @@ __global__ __launch_bounds__(64 * COLD_WAVES) void k_match(Dev D, BatchArgs B, c
     if (i < nhot && (flow_ok[i * ok_stride] || (end - beg >= LEGACY_HOT_MIN && i < MAX_LEGACY))) continue;
     const uint32_t sym = uni(B.ord[B.prep[beg].idx].symbol_id);
     if (!started) {
-      wave_init(W, D, B, sym, EVB, lvl_lds[threadIdx.x >> 6]);
+      wave_init(W, D, B, sym, EVB, lvl_lds + (threadIdx.x >> 6) * COLD_LDS_LVLS);
       started = true;
     } else {
       wave_next_book(W, sym);

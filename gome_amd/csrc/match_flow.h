@@ -126,7 +126,7 @@ struct FlowHdr {
   uint32_t ncancel;    // the cancel prep's longest window + 1 (diagnostics)
   uint32_t fc_bad;     // set by the cancel prep: decline the book (legacy / cold kernels)
   uint32_t deep;       // the lane prep found more levels than FL_MAX: a deep-book candidate
-  uint32_t dslot;      // its deep slot (= h; candidates from DEEP_SLOTS on are never deep)
+  uint32_t dslot;      // its deep slot (head: = h; tail: handed out by k_flow_prep)
   uint32_t pad3[2];
 };
 // FlowHdr::ok: 0 declined, FL_OK_ADD an ADD-only flow book, FL_OK_CANCEL a book with DELs,
@@ -134,7 +134,10 @@ struct FlowHdr {
 constexpr uint32_t FL_OK_ADD = 1, FL_OK_CANCEL = 2, FL_OK_DEEP = 3;
 constexpr uint32_t DEEP_CAP = 16384;     // level slots of a deep book (0 and DEEP_CAP - 1: sentinels)
 constexpr uint32_t DEEP_HASH = 1u << 16; // price-set slots of a deep book (global memory)
-constexpr uint32_t DEEP_SLOTS = 256;     // candidates 0..DEEP_SLOTS-1 may be deep books (slot = candidate)
+constexpr uint32_t DEEP_GRID_T = 128;    // blocks (per dimension) of the tail's deep launches
+// Deep slots: the head's FL_HEAD candidates own slots 0..FL_HEAD-1; every other candidate whose
+// levels exceed the lanes takes the next free slot (FlowArgs::dslot_n) while FlowArgs::dslots
+// lasts (sized at gome_create: one per possible candidate, at most MAX_FLOW).
 // FlowHdr::fc_bad: why the cancel prep declined a book (bits; diagnostics read them)
 enum : uint32_t {
   FC_BAD_SYM = 1, FC_BAD_TABLE = 2, FC_BAD_Q7 = 4, FC_BAD_Q2 = 8, FC_BAD_LEVEL = 16, FC_BAD_UNIT = 32,
@@ -214,14 +217,16 @@ struct FlowArgs {
   uint64_t fc_hmask;
   // deep books (match_flow_deep.h), per deep slot: level tables, final level records, price
   // sets, prep scratch, sort tile counts
-  FlowLvl* dlvl;       // [DEEP_SLOTS * DEEP_CAP]
-  Level* dlvout;       // [DEEP_SLOTS * DEEP_CAP]
-  unsigned long long* dh_key;  // [DEEP_SLOTS * DEEP_HASH]
-  uint32_t* dh_val;    // [DEEP_SLOTS * DEEP_HASH] level index (after the prep), else old index
-  struct FlPrepScr* dscr;  // [DEEP_SLOTS]
+  FlowLvl* dlvl;       // [dslots * DEEP_CAP]
+  Level* dlvout;       // [dslots * DEEP_CAP]
+  unsigned long long* dh_key;  // [dslots * DEEP_HASH]
+  uint32_t* dh_val;    // [dslots * DEEP_HASH] level index (after the prep), else old index
+  struct FlPrepScr* dscr;  // [dslots]
   uint32_t* dtcnt;     // sort tile counts: FL_CAP per tile, dmaxt tiles per head slot, dtmaxt per tail slot
   uint32_t dmaxt, dtmaxt;
-  uint32_t* dslot_h;   // [DEEP_SLOTS] the book of each deep slot this batch (NIL: none)
+  uint32_t* dslot_h;   // [dslots] the book of each deep slot this batch (NIL: none)
+  uint32_t* dslot_n;   // tail deep slots handed out this batch
+  uint32_t dslots;     // deep slots (head included)
   uint32_t ds0, ds1;   // the deep slots a launch covers (the range's)
   Touch* tlog;         // the first sort pass's output (the log's index space)
   uint32_t fc_gen;     // batch generation (FcHash entries of older batches are empty)
@@ -383,7 +388,11 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep(Dev D, BatchArgs B, Flo
     if (tid == 0) {
       hd->ok = 0;
       // too many levels for the lanes: a deep book if a deep slot is free (match_flow_deep.h)
-      const uint32_t slot = (!bad && bk.n_lvl <= DEEP_CAP - 2 && h < DEEP_SLOTS) ? h : NIL;
+      uint32_t slot = NIL;
+      if (!bad && bk.n_lvl <= DEEP_CAP - 2) {
+        const uint32_t t = atomicAdd(F.dslot_n, 1u);
+        if (t < F.dslots - FL_HEAD) slot = FL_HEAD + t;
+      }
       hd->deep = slot != NIL ? 1u : 0u;
       hd->dslot = slot;
       if (slot != NIL) F.dslot_h[slot] = h;
@@ -505,6 +514,10 @@ struct FlPrepScr {
   uint32_t many;       // more distinct prices than the lane plans hold: a deep-book candidate
   // the deep prep's own totals (match_flow_deep.h)
   uint32_t d_adds, d_dropped, d_dels, d_bad, d_ndist;
+  // a deep tail book's chunk ids for its FIFO appends, claimed once for all its levels
+  // (k_deep_claim): id j = j < c_nst ? free_ids[c_t - c_nst + j] : c_bb + (j - c_nst)
+  int32_t c_t;
+  uint32_t c_nst, c_bb, c_ok;
 };
 
 __device__ __forceinline__ void fl_slice(uint32_t beg, uint32_t end, uint32_t x, uint32_t& b0, uint32_t& b1) {
@@ -985,8 +998,22 @@ __global__ __launch_bounds__(64) void k_flow_plan_tail(Dev D, FlowArgs F) { fl_p
 __global__ __launch_bounds__(64) void k_flow_plan_tail_c(Dev D, FlowArgs F) { fl_plan_kernel<false>(D, F, FL_OK_CANCEL, 1); }
 // tail books with DELs whose ring exceeds FC_TAIL_SLOTS (the largest LDS allocation)
 __global__ __launch_bounds__(64) void k_flow_plan_tail_cb(Dev D, FlowArgs F) { fl_plan_kernel<false>(D, F, FL_OK_CANCEL, 2); }
-// deep tail books (depths in LDS: a whole CU each, like the head)
-__global__ __launch_bounds__(256) void k_flow_plan_tail_d(Dev D, FlowArgs F) { fl_plan_kernel<true>(D, F, FL_OK_DEEP); }
+// deep tail books (depths in LDS: a whole CU each, like the head): each block walks the tail's
+// deep slots (handed out by k_flow_prep) in turn
+__global__ __launch_bounds__(256) void k_flow_plan_tail_d(Dev D, FlowArgs F) {
+  const uint32_t n = min(F.ds1 - F.ds0, *F.dslot_n);
+  for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
+    const uint32_t h = F.dslot_h[F.ds0 + i];
+    const bool mine = h != NIL && h < fl_hend(D, F) && F.hdr[h].ok == FL_OK_DEEP && F.hdr[h].dslot == F.ds0 + i;
+    if (mine) fl_deep_load(F, h);
+    asm volatile("" ::: "v255", "a255");
+    __syncthreads();
+    if (threadIdx.x < 64 && mine) fl_plan_book(D, F, h);
+    __syncthreads();
+    if (mine) fl_deep_store(F, h);
+    __syncthreads();
+  }
+}
 
 __device__ __forceinline__ void fl_plan_deep(const Dev& D, const FlowArgs& F, uint32_t h);
 
@@ -1236,9 +1263,11 @@ __global__ __launch_bounds__(FL_SORT_T) void k_flow_sort(Dev D, FlowArgs F) {
 // One wave per level (waves of a per-book workgroup take the book's levels in turn):
 // volume coordinates of the level's run, then the gather of the consumed prefix of its
 // resting FIFO.
-// (run_base / run_cnt: the level's run when the caller found it, deep books; else FlowLvl's)
+// (run_base / run_cnt: the level's run when the caller found it, deep books; else FlowLvl's.
+// ig_pre: the level's gathered-maker space when the caller claimed it, else claimed here.)
 __device__ __forceinline__ void fl_level_one(const Dev& D, const FlowArgs& F, uint32_t h, uint32_t q,
-                                             uint32_t run_base = NIL, uint32_t run_cnt = 0) {
+                                             uint32_t run_base = NIL, uint32_t run_cnt = 0,
+                                             uint32_t ig_pre = NIL) {
   const FlowHdr* hd = &F.hdr[h];
   const uint32_t lane = lane_id();
   FlowLvl* Lq = fl_lvls(F, h) + q;
@@ -1281,9 +1310,12 @@ __device__ __forceinline__ void fl_level_one(const Dev& D, const FlowArgs& F, ui
   uint32_t ig_base = 0, ng = 0, consumed = 0;
   bool have_extra = false;
   if (nv0 > 0 && cfin > 0) {
-    uint32_t b = 0;
-    if (lane == 0) b = atomicAdd(F.ig_bump, nv0);
-    ig_base = uni(b);
+    uint32_t b = ig_pre;
+    if (ig_pre == NIL) {
+      if (lane == 0) b = atomicAdd(F.ig_bump, nv0);
+      b = uni(b);
+    }
+    ig_base = b;
     if (static_cast<unsigned long long>(ig_base) + nv0 > F.ig_cap) {
       if (lane == 0) atomicOr(&D.st->err, ERR_CHUNKS);
       return;
@@ -1292,6 +1324,14 @@ __device__ __forceinline__ void fl_level_one(const Dev& D, const FlowArgs& F, ui
     int64_t E = 0;
     bool have_surv = false;
     uint32_t c = head, s0 = hslot, nh = NIL, nhs = 0;
+    uint32_t nfr = 0, fid = 0;  // fully consumed chunks, published 64 at a time
+    auto publish = [&]() {
+      uint32_t fb = 0;
+      if (lane == 0) fb = atomicAdd(&D.st->freed_top, nfr);
+      fb = uni(fb);
+      if (lane < nfr) D.freed_ids[fb + lane] = fid;
+      nfr = 0;
+    };
     for (uint32_t guard = 0; c != NIL && !have_extra; ++guard) {
       if (guard > D.ch_cap) { if (lane == 0) atomicOr(&D.st->err, ERR_CORRUPT); return; }
       const uint32_t lim = (c == tail) ? tslot : CH;
@@ -1327,8 +1367,9 @@ __device__ __forceinline__ void fl_level_one(const Dev& D, const FlowArgs& F, ui
           nh = c;
           nhs = static_cast<uint32_t>(__builtin_ctzll(sv));
           if (lane == nhs && em < cfin) D.nodes[c * CH + lane].rem = em + nd.rem - cfin;  // partial head
-        } else {
-          if (lane == 0) D.freed_ids[atomicAdd(&D.st->freed_top, 1u)] = c;  // fully consumed chunk
+        } else {  // a fully consumed chunk
+          if (lane == nfr) fid = c;
+          if (++nfr == 64) publish();
         }
       }
       if (beyond) have_extra = true;
@@ -1337,6 +1378,7 @@ __device__ __forceinline__ void fl_level_one(const Dev& D, const FlowArgs& F, ui
       c = nx;
       s0 = 0;
     }
+    if (nfr) publish();
     if (!have_surv) {
       head = tail = NIL;
       hslot = tslot = 0;
@@ -1615,8 +1657,36 @@ constexpr uint32_t FL_WRITE_T = 1024;
 
 // Append level q's surviving new makers to its FIFO, insert them into the cancel index, and
 // return (on every lane) the level's final record.
+// New makers of level q that survive the batch (from rf on) and the FIFO chunks their append
+// needs beyond the tail chunk's room.
+struct FlWPlan {
+  uint32_t rf, S, s0, room, need;
+  bool fresh;
+};
+__device__ __forceinline__ FlWPlan fl_wplan(const FlowLvl& f, const RsEnt* RS) {
+  FlWPlan w;
+  w.rf = 0;
+  if (f.cfin > f.d0) {
+    uint32_t lo = 0, hi = f.nrest;  // first r with e + v > cfin
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (RS[mid].e + RS[mid].v > f.cfin) hi = mid; else lo = mid + 1;
+    }
+    w.rf = lo;
+  }
+  w.S = f.nrest - w.rf;
+  w.fresh = f.nlive0 == 0;
+  w.s0 = w.fresh ? 0u : f.tslot;
+  w.room = w.fresh ? 0u : CH - w.s0;
+  w.need = w.S > w.room ? (w.S - w.room + CH - 1) / CH : 0u;
+  return w;
+}
+
+// claim: a deep tail book's pre-claimed chunk ids (k_deep_claim; FlowLvl::pad0 = the level's
+// first), else the level claims its own.
 __device__ __forceinline__ Level fl_write_level(const Dev& D, const BatchArgs& B, const FlowArgs& F,
-                                                const FlowHdr& hd, uint32_t h, uint32_t q) {
+                                                const FlowHdr& hd, uint32_t h, uint32_t q,
+                                                const FlPrepScr* claim = nullptr) {
   const uint32_t lane = lane_id();
   const uint32_t L = FL_TOUCH_MUL * hd.beg;
   const unsigned long long mask = D.idx_mask;
@@ -1625,25 +1695,19 @@ __device__ __forceinline__ Level fl_write_level(const Dev& D, const BatchArgs& B
   Level x{};
   x.price = f.price;
   x.head = x.tail = NIL;
-  // first new maker that survives the batch
-  uint32_t rf = 0;
-  if (f.cfin > f.d0) {
-    uint32_t lo = 0, hi = f.nrest;  // first r with e + v > cfin
-    while (lo < hi) {
-      const uint32_t mid = (lo + hi) >> 1;
-      if (RS[mid].e + RS[mid].v > f.cfin) hi = mid; else lo = mid + 1;
-    }
-    rf = lo;
-  }
-  const uint32_t S = f.nrest - rf;
-  const bool fresh = f.nlive0 == 0;
-  const uint32_t s0 = fresh ? 0u : f.tslot;
-  const uint32_t room = fresh ? 0u : CH - s0;
-  const uint32_t need = S > room ? (S - room + CH - 1) / CH : 0u;
+  const FlWPlan wp = fl_wplan(f, RS);
+  const uint32_t rf = wp.rf, S = wp.S, s0 = wp.s0, room = wp.room, need = wp.need;
+  const bool fresh = wp.fresh;
   // claim `need` chunk ids: free stack first, then the bump pointer
   int t = 0;
   uint32_t nst = 0, bb = 0;
-  if (need) {
+  if (need && claim) {  // ids [pad0, pad0 + need) of the book's claim
+    if (!claim->c_ok) return x;  // (ERR_CHUNKS set by the claim)
+    const uint32_t j0 = f.pad0, cn = claim->c_nst;
+    nst = j0 < cn ? min(cn - j0, need) : 0u;
+    t = claim->c_t - static_cast<int>(cn) + static_cast<int>(j0) + static_cast<int>(nst);
+    bb = claim->c_bb + (j0 + nst - cn);
+  } else if (need) {
     if (lane == 0) t = atomicSub(&D.st->free_top, static_cast<int>(need));
     t = static_cast<int>(uni(static_cast<uint32_t>(t)));
     nst = static_cast<uint32_t>(min(max(t, 0), static_cast<int>(need)));

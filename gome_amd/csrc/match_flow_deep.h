@@ -74,6 +74,12 @@ __device__ __forceinline__ uint32_t fd_book(const Dev& D, const FlowArgs& F, uin
   return (h != NIL && h < fl_hend(D, F) && F.hdr[h].dslot == ds) ? h : NIL;
 }
 
+// Deep slots a launch of this range walks: the head's are fixed (slot = candidate), the tail's
+// are handed out by its prep in the order it finds deep books (F.dslot_n).
+__device__ __forceinline__ uint32_t fd_nslots(const FlowArgs& F) {
+  return F.ds0 >= FL_HEAD ? min(F.ds1 - F.ds0, *F.dslot_n) : F.ds1 - F.ds0;
+}
+
 // A deep slot's sort tile counts (seg_order is longest first: candidate h has at most
 // 1 / (h + 1) of the batch, so a tail slot needs at most an eighth of the head's tiles).
 __device__ __forceinline__ uint32_t* fd_tcnt(const FlowArgs& F, uint32_t ds) {
@@ -109,10 +115,10 @@ __device__ __forceinline__ void fd_slice(uint32_t beg, uint32_t end, uint32_t x,
 }
 
 // ---- prep a: per slice, the batch's prices into the set, gcd / sum, counts ----------------
-__global__ __launch_bounds__(FL_PREP_T) void k_deep_prep_a(Dev D, BatchArgs B, FlowArgs F) {
+__device__ __forceinline__ void k_deep_prep_a_one(Dev D, BatchArgs B, FlowArgs F, uint32_t slot_i) {
   __shared__ uint32_t adds, dropped, dels, bad, nd;
   __shared__ unsigned long long wg[FL_PREP_T / 64], ws[FL_PREP_T / 64];
-  const uint32_t h = fd_book(D, F, blockIdx.y), tid = threadIdx.x;
+  const uint32_t h = fd_book(D, F, slot_i), tid = threadIdx.x;
   if (!fd_candidate(D, F, h)) return;
   const uint32_t ds = F.hdr[h].dslot;
   FlPrepScr* P = F.dscr + ds;
@@ -154,13 +160,19 @@ __global__ __launch_bounds__(FL_PREP_T) void k_deep_prep_a(Dev D, BatchArgs B, F
     if (nd) atomicAdd(&P->d_ndist, nd);
   }
 }
+__global__ __launch_bounds__(FL_PREP_T) void k_deep_prep_a(Dev D, BatchArgs B, FlowArgs F) {
+  for (uint32_t i = blockIdx.y; i < fd_nslots(F); i += gridDim.y) {
+    k_deep_prep_a_one(D, B, F, i);
+    __syncthreads();
+  }
+}
 
 // ---- prep b: old levels into the set, the sorted level table, the header -----------------
 // Dynamic LDS: DEEP_CAP keys (the sort).
-__global__ __launch_bounds__(FL_PREP_T) void k_deep_prep_b(Dev D, BatchArgs B, FlowArgs F) {
+__device__ __forceinline__ void k_deep_prep_b_one(Dev D, BatchArgs B, FlowArgs F, uint32_t slot_i) {
   __shared__ uint32_t bad, ndist, nc;
   __shared__ unsigned long long wg[FL_PREP_T / 64], ws[FL_PREP_T / 64];
-  const uint32_t h = fd_book(D, F, blockIdx.x), tid = threadIdx.x;
+  const uint32_t h = fd_book(D, F, slot_i), tid = threadIdx.x;
   if (!fd_candidate(D, F, h)) return;
   FlowHdr* hd = &F.hdr[h];
   const uint32_t ds = hd->dslot;
@@ -284,10 +296,16 @@ __global__ __launch_bounds__(FL_PREP_T) void k_deep_prep_b(Dev D, BatchArgs B, F
     *hd = x;
   }
 }
+__global__ __launch_bounds__(FL_PREP_T) void k_deep_prep_b(Dev D, BatchArgs B, FlowArgs F) {
+  for (uint32_t i = blockIdx.x; i < fd_nslots(F); i += gridDim.x) {
+    k_deep_prep_b_one(D, B, F, i);
+    __syncthreads();
+  }
+}
 
 // ---- prep c: the 32-bit records (level index from the set) ---------------------------------
-__global__ __launch_bounds__(FL_PREP_T) void k_deep_prep_c(Dev D, BatchArgs B, FlowArgs F) {
-  const uint32_t h = fd_book(D, F, blockIdx.y), tid = threadIdx.x;
+__device__ __forceinline__ void k_deep_prep_c_one(Dev D, BatchArgs B, FlowArgs F, uint32_t slot_i) {
+  const uint32_t h = fd_book(D, F, slot_i), tid = threadIdx.x;
   if (!fd_deep(F, h)) return;
   const FlowHdr* hd = &F.hdr[h];
   const unsigned long long* keys = F.dh_key + static_cast<size_t>(hd->dslot) * DEEP_HASH;
@@ -308,6 +326,12 @@ __global__ __launch_bounds__(FL_PREP_T) void k_deep_prep_c(Dev D, BatchArgs B, F
     B.ev_count[q.idx] = 0;
   }
 }
+__global__ __launch_bounds__(FL_PREP_T) void k_deep_prep_c(Dev D, BatchArgs B, FlowArgs F) {
+  for (uint32_t i = blockIdx.y; i < fd_nslots(F); i += gridDim.y) {
+    k_deep_prep_c_one(D, B, F, i);
+    __syncthreads();
+  }
+}
 
 // ---- sort: two stable 7-bit passes by level (tile counts, per-book scan, scatter) ---------
 // PASS 1 reads the plan's log (level in Touch::pos) and writes F.tlog in low-7-bit order, the
@@ -319,10 +343,10 @@ __device__ __forceinline__ uint32_t fd_key(const FlowArgs& F, uint32_t L, uint32
 }
 
 template <int PASS>
-__global__ __launch_bounds__(FL_TILE) void k_deep_sort_cnt(Dev D, FlowArgs F) {
+__device__ __forceinline__ void k_deep_sort_cnt_one(Dev D, FlowArgs F, uint32_t slot_i) {
   __shared__ uint32_t wc[FL_TILE_W][FL_CAP];
   __shared__ uint32_t nrest;
-  const uint32_t h = fd_book(D, F, blockIdx.y), tid = threadIdx.x, w = tid >> 6;
+  const uint32_t h = fd_book(D, F, slot_i), tid = threadIdx.x, w = tid >> 6;
   if (!fd_deep(F, h)) return;
   const uint32_t nt = F.hdr[h].ntouch, L = FL_TOUCH_MUL * F.hdr[h].beg;
   const uint32_t ntile = (nt + FL_TILE - 1) / FL_TILE;
@@ -351,10 +375,17 @@ __global__ __launch_bounds__(FL_TILE) void k_deep_sort_cnt(Dev D, FlowArgs F) {
     __syncthreads();
   }
 }
+template <int PASS>
+__global__ __launch_bounds__(FL_TILE) void k_deep_sort_cnt(Dev D, FlowArgs F) {
+  for (uint32_t i = blockIdx.y; i < fd_nslots(F); i += gridDim.y) {
+    k_deep_sort_cnt_one<PASS>(D, F, i);
+    __syncthreads();
+  }
+}
 
-__global__ __launch_bounds__(FL_CAP) void k_deep_sort_scan(Dev D, FlowArgs F) {
+__device__ __forceinline__ void k_deep_sort_scan_one(Dev D, FlowArgs F, uint32_t slot_i) {
   __shared__ uint32_t tot[FL_CAP];
-  const uint32_t h = fd_book(D, F, blockIdx.x), k = threadIdx.x;
+  const uint32_t h = fd_book(D, F, slot_i), k = threadIdx.x;
   if (!fd_deep(F, h)) return;
   const uint32_t nt = F.hdr[h].ntouch;
   const uint32_t ntile = (nt + FL_TILE - 1) / FL_TILE;
@@ -375,11 +406,17 @@ __global__ __launch_bounds__(FL_CAP) void k_deep_sort_scan(Dev D, FlowArgs F) {
     run += v;
   }
 }
+__global__ __launch_bounds__(FL_CAP) void k_deep_sort_scan(Dev D, FlowArgs F) {
+  for (uint32_t i = blockIdx.x; i < fd_nslots(F); i += gridDim.x) {
+    k_deep_sort_scan_one(D, F, i);
+    __syncthreads();
+  }
+}
 
 template <int PASS>
-__global__ __launch_bounds__(FL_TILE) void k_deep_sort_scatter(Dev D, FlowArgs F) {
+__device__ __forceinline__ void k_deep_sort_scatter_one(Dev D, FlowArgs F, uint32_t slot_i) {
   __shared__ uint32_t wc[FL_TILE_W][FL_CAP];
-  const uint32_t h = fd_book(D, F, blockIdx.y), tid = threadIdx.x, w = tid >> 6;
+  const uint32_t h = fd_book(D, F, slot_i), tid = threadIdx.x, w = tid >> 6;
   if (!fd_deep(F, h)) return;
   const uint32_t nt = F.hdr[h].ntouch, L = FL_TOUCH_MUL * F.hdr[h].beg;
   const unsigned long long g = F.hdr[h].g;
@@ -431,6 +468,13 @@ __global__ __launch_bounds__(FL_TILE) void k_deep_sort_scatter(Dev D, FlowArgs F
     __syncthreads();
   }
 }
+template <int PASS>
+__global__ __launch_bounds__(FL_TILE) void k_deep_sort_scatter(Dev D, FlowArgs F) {
+  for (uint32_t i = blockIdx.y; i < fd_nslots(F); i += gridDim.y) {
+    k_deep_sort_scatter_one<PASS>(D, F, i);
+    __syncthreads();
+  }
+}
 
 // ---- levels: the run of each level, then the ADD-only level reconstruction -----------------
 // First index in srt[L, L + nt) whose level is >= q (wave-wide 64-ary search).
@@ -454,38 +498,144 @@ __device__ __forceinline__ uint32_t fd_lower(const SEnt* R, uint32_t nt, uint32_
 
 constexpr uint32_t DEEP_GRID = 1024;  // workgroups per deep book in the per-level kernels
 
-__global__ __launch_bounds__(64) void k_deep_level(Dev D, FlowArgs F) {
-  const uint32_t h = fd_book(D, F, blockIdx.y);
+// The run of each level in the sorted touches: FlowLvl::base = its first, ::pad1 = its end
+// (0 for a level without touches; the deep prep zeroed both).
+__device__ __forceinline__ void k_deep_runs_one(Dev D, FlowArgs F, uint32_t slot_i) {
+  const uint32_t h = fd_book(D, F, slot_i);
+  if (!fd_deep(F, h)) return;
+  const uint32_t nt = F.hdr[h].ntouch, L = FL_TOUCH_MUL * F.hdr[h].beg;
+  const SEnt* R = F.srt + L;
+  FlowLvl* LV = fl_lvls(F, h);
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nt; i += gridDim.x * blockDim.x) {
+    const uint32_t q = R[i].lvl;
+    if (i == 0 || R[i - 1].lvl != q) LV[q].base = i;
+    if (i + 1 == nt || R[i + 1].lvl != q) LV[q].pad1 = i + 1;
+  }
+}
+__global__ __launch_bounds__(256) void k_deep_runs(Dev D, FlowArgs F) {
+  for (uint32_t i = blockIdx.y; i < fd_nslots(F); i += gridDim.y) k_deep_runs_one(D, F, i);
+}
+
+__device__ __forceinline__ void k_deep_level_one(Dev D, FlowArgs F, uint32_t slot_i) {
+  const uint32_t h = fd_book(D, F, slot_i);
   if (!fd_deep(F, h)) return;
   const uint32_t nl = F.hdr[h].nl, nt = F.hdr[h].ntouch, L = FL_TOUCH_MUL * F.hdr[h].beg;
   FlowLvl* LV = fl_lvls(F, h);
+  // the gathered-maker space of all this wave's levels in one claim (an upper bound: every
+  // level with resting makers, consumed or not; the books' resting nodes bound the total)
+  const uint32_t lane = lane_id();
+  uint32_t need = 0;
+  for (uint32_t q0 = 1 + blockIdx.x; q0 <= nl; q0 += 64 * gridDim.x) {
+    const uint32_t q = q0 + lane * gridDim.x;
+    need += q <= nl ? LV[q].nv0 : 0u;
+  }
+  need = rl(wave_incl_scan_u32(need), 63);
+  uint32_t ig = 0;
+  if (lane == 0 && need) ig = atomicAdd(F.ig_bump, need);
+  ig = uni(ig);
   for (uint32_t q = 1 + blockIdx.x; q <= nl; q += gridDim.x) {
-    const uint32_t b = fd_lower(F.srt + L, nt, q), e = fd_lower(F.srt + L, nt, q + 1);
+    const uint32_t e = uni(LV[q].pad1), b = e ? uni(LV[q].base) : 0u;  // (k_deep_runs)
     if (lane_id() == 0) {
       LV[q].base = b;
       LV[q].cnt = e - b;
     }
-    fl_level_one(D, F, h, q, b, e - b);
+    const uint32_t nv0 = uni(LV[q].nv0);
+    fl_level_one(D, F, h, q, b, e - b, ig);
+    ig += nv0;
+  }
+}
+__global__ __launch_bounds__(64) void k_deep_level(Dev D, FlowArgs F) {
+  for (uint32_t i = blockIdx.y; i < fd_nslots(F); i += gridDim.y) {
+    k_deep_level_one(D, F, i);
+    __syncthreads();
   }
 }
 
 // ---- write: FIFO appends per level, then the level array ------------------------------------
-__global__ __launch_bounds__(64) void k_deep_write_lv(Dev D, BatchArgs B, FlowArgs F) {
-  const uint32_t h = fd_book(D, F, blockIdx.y);
+// ---- FIFO chunks of all the book's appends, claimed at once --------------------------------
+// (a level claiming its own is two atomics on one shared line of Status; a deep book has
+// thousands of levels).  FlowLvl::pad0 := the level's first id in the book's claim.
+constexpr uint32_t DEEP_CLAIM_T = 1024;
+__device__ __forceinline__ void k_deep_claim_one(Dev D, BatchArgs B, FlowArgs F, uint32_t slot_i) {
+  __shared__ uint32_t part[DEEP_CLAIM_T];
+  __shared__ uint32_t tot_s;
+  const uint32_t h = fd_book(D, F, slot_i), tid = threadIdx.x;
   if (!fd_deep(F, h)) return;
   const FlowHdr hd = F.hdr[h];
+  FlowLvl* LV = fl_lvls(F, h);
+  const RsEnt* RS = F.rs + FL_TOUCH_MUL * hd.beg;
+  const uint32_t per = (hd.nl + DEEP_CLAIM_T - 1) / DEEP_CLAIM_T;
+  const uint32_t q0 = 1 + tid * per, q1 = min(hd.nl + 1, q0 + per);
+  uint32_t sum = 0;
+  for (uint32_t q = q0; q < q1; ++q) sum += fl_wplan(LV[q], RS + LV[q].base).need;
+  part[tid] = sum;
+  __syncthreads();
+  if (tid < 64) {  // exclusive scan of the 1024 partial sums by one wave
+    uint32_t v[DEEP_CLAIM_T / 64], acc = 0;
+#pragma unroll
+    for (uint32_t u = 0; u < DEEP_CLAIM_T / 64; ++u) { v[u] = part[tid * (DEEP_CLAIM_T / 64) + u]; acc += v[u]; }
+    const uint32_t incl = wave_incl_scan_u32(acc);
+    uint32_t run = incl - acc;
+#pragma unroll
+    for (uint32_t u = 0; u < DEEP_CLAIM_T / 64; ++u) { part[tid * (DEEP_CLAIM_T / 64) + u] = run; run += v[u]; }
+    if (tid == 63) tot_s = incl;
+  }
+  __syncthreads();
+  uint32_t off = part[tid];
+  for (uint32_t q = q0; q < q1; ++q) {
+    LV[q].pad0 = off;
+    off += fl_wplan(LV[q], RS + LV[q].base).need;
+  }
+  if (tid == 0) {
+    FlPrepScr* P = F.dscr + hd.dslot;
+    const uint32_t need = tot_s;
+    int t = 0;
+    uint32_t nst = 0, bb = 0, ok = 1;
+    if (need) {
+      t = atomicSub(&D.st->free_top, static_cast<int>(need));
+      nst = static_cast<uint32_t>(min(max(t, 0), static_cast<int>(need)));
+      if (nst < need) bb = atomicAdd(D.ch_bump, need - nst);
+      if (static_cast<unsigned long long>(bb) + (need - nst) > D.ch_cap) {
+        atomicOr(&D.st->err, ERR_CHUNKS);
+        ok = 0;
+      }
+    }
+    P->c_t = t;
+    P->c_nst = nst;
+    P->c_bb = bb;
+    P->c_ok = ok;
+  }
+}
+__global__ __launch_bounds__(DEEP_CLAIM_T) void k_deep_claim(Dev D, BatchArgs B, FlowArgs F) {
+  for (uint32_t i = blockIdx.x; i < fd_nslots(F); i += gridDim.x) {
+    k_deep_claim_one(D, B, F, i);
+    __syncthreads();
+  }
+}
+
+__device__ __forceinline__ void k_deep_write_lv_one(Dev D, BatchArgs B, FlowArgs F, uint32_t slot_i) {
+  const uint32_t h = fd_book(D, F, slot_i);
+  if (!fd_deep(F, h)) return;
+  const FlowHdr hd = F.hdr[h];
+  const FlPrepScr* claim = F.dscr + hd.dslot;
   for (uint32_t q = 1 + blockIdx.x; q <= hd.nl; q += gridDim.x) {
-    const Level x = fl_write_level(D, B, F, hd, h, q);
+    const Level x = fl_write_level(D, B, F, hd, h, q, claim);
     if (lane_id() == 0) F.dlvout[static_cast<size_t>(hd.dslot) * DEEP_CAP + q] = x;
+  }
+}
+__global__ __launch_bounds__(64) void k_deep_write_lv(Dev D, BatchArgs B, FlowArgs F) {
+  for (uint32_t i = blockIdx.y; i < fd_nslots(F); i += gridDim.y) {
+    k_deep_write_lv_one(D, B, F, i);
+    __syncthreads();
   }
 }
 
 constexpr uint32_t DEEP_FIN_T = 1024, DEEP_FIN_PER = DEEP_CAP / DEEP_FIN_T;
 
-__global__ __launch_bounds__(DEEP_FIN_T) void k_deep_write_fin(Dev D, FlowArgs F) {
+__device__ __forceinline__ void k_deep_write_fin_one(Dev D, FlowArgs F, uint32_t slot_i) {
   __shared__ uint32_t part[DEEP_FIN_T];
   __shared__ uint32_t base_s, cap_s, nout_s;
-  const uint32_t h = fd_book(D, F, blockIdx.x), tid = threadIdx.x;
+  const uint32_t h = fd_book(D, F, slot_i), tid = threadIdx.x;
   if (!fd_deep(F, h)) return;
   const FlowHdr hd = F.hdr[h];
   const Level* lv = F.dlvout + static_cast<size_t>(hd.dslot) * DEEP_CAP;
@@ -551,6 +701,12 @@ __global__ __launch_bounds__(DEEP_FIN_T) void k_deep_write_fin(Dev D, FlowArgs F
   for (uint32_t u = 0; u < DEEP_FIN_PER; ++u) {
     const uint32_t q = q0 + u;
     if (q <= hd.nl && lv[q].nlive > 0) D.lvl[base_s + o++] = lv[q];
+  }
+}
+__global__ __launch_bounds__(DEEP_FIN_T) void k_deep_write_fin(Dev D, FlowArgs F) {
+  for (uint32_t i = blockIdx.x; i < fd_nslots(F); i += gridDim.x) {
+    k_deep_write_fin_one(D, F, i);
+    __syncthreads();
   }
 }
 

@@ -239,8 +239,9 @@ def main():
 
     total_orders = per_rank * (warm + steps + e2e_warm + e2e_steps)
     keep = 0.3 if args.workload == "config3" else 0.5
+    # (+ two batches: the headroom a submit checks, in flight included, before it is applied)
     eng = Engine(max_symbols=n_symbols, max_batch=per_rank,
-                 max_nodes=max(1 << 20, int(total_orders * keep)),
+                 max_nodes=max(1 << 20, int(total_orders * keep)) + 2 * per_rank,
                  max_levels=max(1 << 22, (256 if n_symbols <= 100000 else 128) * n_symbols), device=local)
 
     summary = torch.zeros(SUMMARY_WORDS, dtype=torch.int64, device="cuda")

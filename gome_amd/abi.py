@@ -19,6 +19,7 @@ HEADER = os.path.join(os.path.dirname(_HERE), "include", "gome", "gome_abi.h")
 HEADERS = [HEADER, os.path.join(os.path.dirname(_HERE), "include", "gome", "gome_loadgen.h")]
 
 GOME_FLAG_LEGACY_HOT = 1  # gome_config.flags: hot books on the legacy FIFO kernel
+GOME_FLAG_NO_HEADROOM = 2  # gome_config.flags: no pool-headroom check before a submit
 GOME_ORD_ADM_HOST, GOME_ORD_ADMITTED = 1, 2  # gome_order.flags: host-resolved admission (ABI 4)
 GOME_MAX_INFLIGHT = 2
 

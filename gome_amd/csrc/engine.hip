@@ -252,6 +252,8 @@ struct gome_engine {
                       uint64_t inflight_n);
   gome_status finish(uint32_t slot, uint32_t n);
   gome_status check_submit(size_t n, const void* p);
+  gome_status check_capacity(unsigned long long adds, unsigned long long inflight_n);
+  gome_status check_capacity_host(const gome_order* o, size_t n, unsigned long long inflight_n);
   uint32_t take_slot() {
     const uint32_t k = next_slot;
     next_slot = (next_slot + 1) % GOME_MAX_INFLIGHT;
@@ -809,6 +811,35 @@ gome_status gome_engine::check_submit(size_t n, const void* p) {
   return GOME_OK;
 }
 
+// Pool headroom before anything is applied (a device-side capacity error poisons the handle):
+// every ADD may rest as a new maker on a new level.  `adds` is the batch's ADD count, or its
+// record count when the records are not readable here (device records); batches still in
+// flight count in full.  The FIFO chunk pool is sized from max_nodes / max_levels with slack
+// and level blocks can fragment, so a device-side error stays possible at the very edge of
+// the pools.  GOME_FLAG_NO_HEADROOM turns the check off.
+gome_status gome_engine::check_capacity(unsigned long long adds, unsigned long long inflight_n) {
+  if (cfg.flags & GOME_FLAG_NO_HEADROOM) return GOME_OK;
+  const unsigned long long add = adds + inflight_n, rest = resting + add, lv = levels + add;
+  if (rest > cfg.max_nodes || lv > cfg.max_levels)
+    return fail(GOME_E_CAPACITY,
+                "batch rejected before it was applied (book unchanged): up to " + std::to_string(add) +
+                    " new makers on top of " + std::to_string(resting) + " resting / " + std::to_string(levels) +
+                    " levels could exceed gome_config.max_nodes / max_levels; submit fewer ADDs or raise them");
+  return GOME_OK;
+}
+
+// ADD records of a host batch (counted only when the record count alone fails the check).
+static unsigned long long count_adds(const gome_order* o, size_t n) {
+  unsigned long long a = 0;
+  for (size_t i = 0; i < n; ++i) a += o[i].action == GOME_ADD ? 1u : 0u;
+  return a;
+}
+
+gome_status gome_engine::check_capacity_host(const gome_order* o, size_t n, unsigned long long inflight_n) {
+  if (check_capacity(n, inflight_n) == GOME_OK) return GOME_OK;
+  return check_capacity(count_adds(o, n), inflight_n);
+}
+
 // Copy `n` events of slot `sl` (device) to the host drain queue.
 gome_status gome_engine::queue_events(uint32_t sl, size_t n, hipStream_t s) {
   if (pending_pos) {
@@ -939,6 +970,7 @@ gome_status gome_submit_batch(gome_engine* e, const gome_order* orders, size_t n
   if ((st = e->spill_device_events()) != GOME_OK) return st;
   if ((st = e->check_submit(n, orders)) != GOME_OK) return st;
   if (n == 0) return GOME_OK;
+  if ((st = e->check_capacity_host(orders, n, 0)) != GOME_OK) return st;
   const uint32_t sl = e->take_slot();
   Slot& S = e->slots[sl];
   hipError_t he = hipMemcpyAsync(S.d_orders, orders, n * sizeof(gome_order), hipMemcpyHostToDevice, e->stream);
@@ -957,6 +989,7 @@ gome_status gome_submit_batch_device(gome_engine* e, const gome_order* dev_order
   if ((st = e->spill_device_events()) != GOME_OK) return st;
   if ((st = e->check_submit(n, dev_orders)) != GOME_OK) return st;
   if (n == 0) return GOME_OK;
+  if ((st = e->check_capacity(n, 0)) != GOME_OK) return st;
   hipStream_t s = stream ? static_cast<hipStream_t>(stream) : e->stream;
   const uint32_t sl = e->take_slot();
   Slot& S = e->slots[sl];
@@ -979,6 +1012,7 @@ gome_status gome_submit_batch_async(gome_engine* e, const gome_order* orders, si
   if ((st = e->check_submit(n, orders)) != GOME_OK) return st;
   uint64_t inflight_n = 0;
   for (const Flight& f : e->flights) inflight_n += f.n;
+  if (n && (st = e->check_capacity_host(orders, n, inflight_n)) != GOME_OK) return st;
   const uint32_t sl = e->take_slot();
   if (n) {
     Slot& S = e->slots[sl];

@@ -135,9 +135,15 @@ typedef struct gome_node {
   uint8_t pad[7];
 } gome_node;
 
-/* gome_config.flags: apply every hot book with the legacy one-wave FIFO kernel instead of
- * the flow path (same results; for A/B measurement and parity cross-checks). */
+/* gome_config.flags: GOME_FLAG_LEGACY_HOT applies every hot book with the legacy one-wave FIFO
+ * kernel instead of the flow path (same results; for A/B measurement and parity checks). */
 #define GOME_FLAG_LEGACY_HOT 1u
+/* By default a submit whose ADDs could push the resting makers past max_nodes or the level
+ * records past max_levels (every ADD resting on a new level; batches in flight counted in
+ * full) is rejected with GOME_E_CAPACITY before anything is applied: the book is unchanged
+ * and the handle stays usable (size max_nodes >= the resting makers + GOME_MAX_INFLIGHT
+ * batches).  This flag turns the check off (pools sized tightly on purpose). */
+#define GOME_FLAG_NO_HEADROOM 2u
 
 typedef struct gome_config {
   uint32_t accuracy;       /* gomengine.accuracy (config.yaml.example:23-24), default 8 */

@@ -8,7 +8,7 @@ import pytest
 
 import bench
 from gome_amd import workload as wl
-from gome_amd.abi import (Engine, GomeError, GOME_E_INVAL, GOME_E_NOTFOUND, GOME_E_STATE,
+from gome_amd.abi import (Engine, GomeError, GOME_FLAG_NO_HEADROOM, GOME_E_INVAL, GOME_E_NOTFOUND, GOME_E_STATE,
                           GOME_ORD_ADM_HOST, GOME_ORD_ADMITTED)
 from oracle.pyoracle import Oracle
 
@@ -45,7 +45,7 @@ def test_bench_config3_exact_4mi_batches():
     FL_HEAD, the touch-log bound, ord8 padding, event-arena regrowth.)"""
     n = 1 << 22
     gen, _, _ = bench.shard_stream(100000, 1.0, 0, 1, 42)
-    eng = Engine(max_symbols=100000, max_batch=n, max_nodes=int(3 * n * 0.3) + (1 << 20),
+    eng = Engine(max_symbols=100000, max_batch=n, max_nodes=int(3 * n * 0.3) + n + (1 << 20),
                  max_levels=1 << 23)
     orc = Oracle(100000)
     for i in range(3):
@@ -241,7 +241,7 @@ def test_index_rebuild_soak():
     """erases leave tombstones; a small index is rebuilt from the live nodes before it
     fills, cancels of filled / unknown oids stay exact, and every probe terminates."""
     g = wl.NativeStream(64, 1.0, seed=9, del_frac=0.5, aggressive_frac=0.1)
-    eng = Engine(max_symbols=64, max_batch=20000, max_nodes=4096)
+    eng = Engine(max_symbols=64, max_batch=20000, max_nodes=4096, flags=GOME_FLAG_NO_HEADROOM)
     orc = Oracle(64)
     for i in range(40):
         b = g.batch(20000).copy()
@@ -316,3 +316,43 @@ def test_sharded_engines_equal_single_engine(world):
         u = u[np.lexsort((u["fill_idx"], u["taker_seq"]))]
         assert u.tobytes() == exp.tobytes(), f"batch {bi}"
     assert sum(s.stats()["n_resting"] for s in shards) == one.stats()["n_resting"]
+
+
+# ---- transactional capacity errors ------------------------------------------------------
+def test_capacity_rejected_before_applying():
+    """a batch whose ADDs could push the resting makers past max_nodes is
+    rejected with E_CAPACITY before anything is applied: the book is unchanged and the handle
+    stays usable (cancels free room, then the same batch is accepted)."""
+    from gome_amd.abi import GOME_E_CAPACITY
+
+    def bids(oid0, n):  # BUYs that never cross (no asks): every one rests
+        r = np.zeros(n, wl.ORDER_DTYPE)
+        r["price_fx"] = (10 + np.arange(n) % 50) * 10**6
+        r["volume_fx"] = 10**6
+        r["symbol_id"] = np.arange(n) % 4
+        r["oid_id"] = np.arange(oid0, oid0 + n)
+        r["uuid_id"] = 3
+        r["side"] = 0
+        r["action"] = wl.ADD
+        return r
+
+    eng = Engine(max_symbols=4, max_batch=2000, max_nodes=3000, max_levels=1 << 16)
+    orc = Oracle(4)
+    for b in (bids(1, 1000), bids(1001, 1000)):
+        eng.submit(b)
+        _cmp(eng.drain(), orc.submit(b))
+    assert eng.stats()["n_resting"] == 2000
+    b3 = bids(2001, 1500)
+    with pytest.raises(GomeError) as ei:
+        eng.submit(b3)
+    assert ei.value.status == GOME_E_CAPACITY
+    assert eng.stats()["n_resting"] == 2000
+    _cmp_books(eng, orc, range(4), "after the rejected batch")
+    d = bids(1, 800)
+    d["action"] = wl.DEL
+    eng.submit(d)
+    _cmp(eng.drain(), orc.submit(d))
+    eng.submit(b3)
+    _cmp(eng.drain(), orc.submit(b3))
+    assert eng.stats()["n_resting"] == 2700
+    _cmp_books(eng, orc, range(4), "after the accepted batch")

@@ -1,6 +1,8 @@
 """bench.py — matched orders/sec of the MI355X batch matching engine (BASELINE.json metric).
 
 Workloads (BASELINE.json configs; `--workload`):
+  config2: 1k symbols, uniform symbol choice, doorder distribution, ADD-only (no hot symbol:
+          every book is a flow candidate of ~4k orders per 4 Mi batch).
   config3 (default, the config the metric is quoted on): 100k symbols, symbol rank ~
           Zipf(s=1.0), doorder.go price/volume distribution (2-dp prices in (0, 1], 2-dp
           volumes), ADD-only.
@@ -43,6 +45,8 @@ METRIC = "matched orders/sec (node) at 100k symbols; p99 batch match latency; HB
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 
 WORKLOADS = {
+    "config2": dict(symbols=1000, zipf=0.0, decimals=2, del_frac=0.0, aggr=0.0,
+                    desc="config2: {symbols} symbols, uniform symbol choice, doorder 2-dp price/volume, ADD-only"),
     "config3": dict(symbols=100000, zipf=1.0, decimals=2, del_frac=0.0, aggr=0.0,
                     desc="config3: {symbols} symbols, Zipf(s={zipf}) symbol rank, doorder 2-dp price/volume, ADD-only"),
     "config4": dict(symbols=100000, zipf=1.0, decimals=2, del_frac=0.5, aggr=0.1,
@@ -242,7 +246,8 @@ def main():
     # (+ two batches: the headroom a submit checks, in flight included, before it is applied)
     eng = Engine(max_symbols=n_symbols, max_batch=per_rank,
                  max_nodes=max(1 << 20, int(total_orders * keep)) + 2 * per_rank,
-                 max_levels=max(1 << 22, (256 if n_symbols <= 100000 else 128) * n_symbols), device=local)
+                 max_levels=max(1 << 22, (256 if n_symbols <= 100000 else 128) * n_symbols) + 2 * per_rank,
+                 device=local)
 
     summary = torch.zeros(SUMMARY_WORDS, dtype=torch.int64, device="cuda")
     gathered = torch.zeros(SUMMARY_WORDS * world, dtype=torch.int64, device="cuda")

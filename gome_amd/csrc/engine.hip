@@ -666,38 +666,20 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
     k_fc_fin<<<nb, 128, 0, st>>>(D, Rc);
     k_fc_events<<<1024, 256, 0, st>>>(D, B, Rc);
   };
-  head_recon(FH0, 1, flow_stream);
-  head_recon_c(FH0, FH0c, 1, flow_stream);
-  HIPCHK(hipEventRecord(joinf, flow_stream));
   // Streams (HIP maps more streams than its 4 hardware queues per process onto shared queues,
   // which would serialise them): the hottest book on the flow stream; the other head books'
   // plans (whole CUs, from the head's prep on) and then the legacy hot kernels on the hot
   // stream; the tail's prep, the cold books and the tail's plans and reconstruction on the
-  // caller's stream.  Each chain ends well before the hottest book's.
-  HIPCHK(hipStreamWaitEvent(hot_stream, fork, 0));
-  HIPCHK(hipStreamWaitEvent(hot_stream, prep_h, 0));
-  if (nh_near) {
-    k_flow_plan_near<<<nh_near, 256, fc_ring_lds, hot_stream>>>(D, FH1);
-    head_recon(FH1, nh_near, hot_stream);
-    head_recon_c(FH1, FH1c, nh_near, hot_stream);
-    k_flow_events_arena<<<1024, 256, 0, hot_stream>>>(D, B, FH1);
-  }
+  // caller's stream.  Each chain ends well before the hottest book's.  The host enqueues in
+  // order of need (a launch costs microseconds of host time, and a hundred of them would
+  // otherwise starve the caller's stream): the tail's chain first, then the other head
+  // books', then the hottest book's reconstruction (needed only when its plan ends).
   if (nh_tail) {
     k_flow_prep<<<nh_tail, FL_PREP_T, 0, s>>>(D, B, FT);
     deep_prep(FT, 8, s);
     cancel_prep(FT, nh_tail, 1, false, s);
   }
   HIPCHK(hipEventRecord(prep_t, s));
-  // legacy hot path (books the flow path declined); it and the cold kernel read the preps'
-  // routing decisions (FlowHdr::ok)
-  HIPCHK(hipStreamWaitEvent(hot_stream, prep_t, 0));
-  HIPCHK(hipEventRecord(S.evh0, hot_stream));
-  const uint32_t nleg = std::min<uint32_t>(MAX_HOT, grid);
-  k_match_hot<<<nleg, 64, HOT_LDS_BYTES, hot_stream>>>(D, B, d_pend, d_resume, F.hdr);
-  HIPCHK(hipEventRecord(S.evh1, hot_stream));
-  k_match_resume<<<nleg, 64, 0, hot_stream>>>(D, B, d_resume);
-  k_pend_apply<<<dim3(8, 64), 256, 0, hot_stream>>>(D, d_pend, d_seg_start, d_seg_order, B);
-  HIPCHK(hipEventRecord(join, hot_stream));
   HIPCHK(hipEventRecord(S.evc0, s));
   k_match<<<std::min<uint32_t>(ceil_div(grid, COLD_WAVES), COLD_BLOCKS), 64 * COLD_WAVES, COLD_LDS_BYTES, s>>>(
       D, B, &F.hdr[0].ok, sizeof(FlowHdr) / sizeof(uint32_t));
@@ -723,6 +705,27 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
     k_fc_write_book<<<nh_tail, FL_WRITE_T, 0, s>>>(D, B, FTc);
     k_fc_events<<<1024, 256, 0, s>>>(D, B, FTc);
   }
+  HIPCHK(hipStreamWaitEvent(hot_stream, fork, 0));
+  HIPCHK(hipStreamWaitEvent(hot_stream, prep_h, 0));
+  if (nh_near) {
+    k_flow_plan_near<<<nh_near, 256, fc_ring_lds, hot_stream>>>(D, FH1);
+    head_recon(FH1, nh_near, hot_stream);
+    head_recon_c(FH1, FH1c, nh_near, hot_stream);
+    k_flow_events_arena<<<1024, 256, 0, hot_stream>>>(D, B, FH1);
+  }
+  // legacy hot path (books the flow path declined); it and the cold kernel read the preps'
+  // routing decisions (FlowHdr::ok)
+  HIPCHK(hipStreamWaitEvent(hot_stream, prep_t, 0));
+  HIPCHK(hipEventRecord(S.evh0, hot_stream));
+  const uint32_t nleg = std::min<uint32_t>(MAX_HOT, grid);
+  k_match_hot<<<nleg, 64, HOT_LDS_BYTES, hot_stream>>>(D, B, d_pend, d_resume, F.hdr);
+  HIPCHK(hipEventRecord(S.evh1, hot_stream));
+  k_match_resume<<<nleg, 64, 0, hot_stream>>>(D, B, d_resume);
+  k_pend_apply<<<dim3(8, 64), 256, 0, hot_stream>>>(D, d_pend, d_seg_start, d_seg_order, B);
+  HIPCHK(hipEventRecord(join, hot_stream));
+  head_recon(FH0, 1, flow_stream);
+  head_recon_c(FH0, FH0c, 1, flow_stream);
+  HIPCHK(hipEventRecord(joinf, flow_stream));
   HIPCHK(hipStreamWaitEvent(s, join, 0));
   HIPCHK(hipStreamWaitEvent(s, joinf, 0));
 

@@ -1539,14 +1539,17 @@ __global__ void k_flow_count(Dev D, BatchArgs B, FlowArgs F) {
 // ARENA: the events go to the batch's event arena (one bump allocation per wave) for
 // k_ev_scatter to place, so they need not wait for the publish-order scan (the tail's books,
 // done long before the head's); else straight to out[ev_off[taker] + fill_idx].
+constexpr uint32_t FL_EV_T = 256;  // threads of the event kernels' blocks
 template <bool ARENA>
 __device__ __forceinline__ void fl_events(const Dev& D, const BatchArgs& B, const FlowArgs& F, const uint32_t* ev_off,
                                           gome_event* out) {
   const uint32_t hend = fl_hend(D, F), nb = hend > F.h0 ? hend - F.h0 : 0u;
   const uint32_t total = nb ? F.toff[F.tb + nb] : 0u;
-  const uint32_t lane = lane_id(), stride = gridDim.x * blockDim.x;
-  for (uint32_t g0 = blockIdx.x * blockDim.x + (threadIdx.x & ~63u); g0 < total; g0 += stride) {
-    const uint32_t gt = g0 + lane;
+  const uint32_t lane = lane_id(), w = threadIdx.x >> 6, stride = gridDim.x * blockDim.x;
+  __shared__ uint32_t wtot[FL_EV_T / 64], bbase;
+  // block tiles (every wave of the block iterates together: the arena is claimed once per tile)
+  for (uint32_t b0 = blockIdx.x * blockDim.x; b0 < total; b0 += stride) {
+    const uint32_t gt = b0 + threadIdx.x;
     uint32_t h = 0, L = 0, t = 0, cnt = 0;
     Touch x{};
     FlTouchCtx c{};
@@ -1568,15 +1571,22 @@ __device__ __forceinline__ void fl_events(const Dev& D, const BatchArgs& B, cons
         const uint32_t v = __shfl_up(inc, off);
         if (lane >= off) inc += v;
       }
-      const uint32_t tot = __shfl(inc, 63);
-      uint32_t base = 0;
-      if (lane == 0 && tot) base = atomicAdd(&D.st->ev_bump, tot);
-      base = __shfl(base, 0);
-      if (base + tot > B.arena_cap) {
-        if (lane == 0 && tot) atomicOr(&D.st->err, ERR_EVENTS);
-        continue;
+      if (lane == 63) wtot[w] = inc;
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        uint32_t t = 0;
+        for (uint32_t k = 0; k < FL_EV_T / 64; ++k) { const uint32_t v = wtot[k]; wtot[k] = t; t += v; }
+        bbase = t ? atomicAdd(&D.st->ev_bump, t) : 0u;
+        if (t && static_cast<unsigned long long>(bbase) + t > B.arena_cap) {
+          atomicOr(&D.st->err, ERR_EVENTS);
+          bbase = NIL;
+        }
       }
-      dst = B.arena + base + (inc - cnt);
+      __syncthreads();
+      const uint32_t base = bbase, wb = wtot[w];
+      __syncthreads();  // (wtot / bbase are rewritten by the next tile)
+      if (base == NIL) continue;
+      dst = B.arena + base + wb + (inc - cnt);
     }
     if (!cnt) continue;
     const uint32_t beg = F.hdr[h].beg, sym = F.hdr[h].sym;

@@ -1032,8 +1032,11 @@ __global__ __launch_bounds__(256) void k_fc_events(Dev D, BatchArgs B, FlowArgs 
   const uint32_t hend = fl_hend(D, F), nb = hend > F.h0 ? hend - F.h0 : 0u;
   const uint32_t total = nb ? F.toff[F.tb + nb] : 0u;
   const uint32_t lane = lane_id(), stride = gridDim.x * blockDim.x;
-  for (uint32_t g0 = blockIdx.x * blockDim.x + (threadIdx.x & ~63u); g0 < total; g0 += stride) {
-    const uint32_t gt = g0 + lane;
+  const uint32_t w = threadIdx.x >> 6;
+  __shared__ uint32_t wtot[FL_EV_T / 64], bbase;
+  // block tiles (every wave of the block iterates together: the arena is claimed once per tile)
+  for (uint32_t b0 = blockIdx.x * blockDim.x; b0 < total; b0 += stride) {
+    const uint32_t gt = b0 + threadIdx.x;
     uint32_t h = 0, L = 0, t = 0, cnt = 0, kind = TK_REST;
     Touch x{};
     FcTouch T{};
@@ -1057,16 +1060,22 @@ __global__ __launch_bounds__(256) void k_fc_events(Dev D, BatchArgs B, FlowArgs 
       const uint32_t v = __shfl_up(inc, off);
       if (lane >= off) inc += v;
     }
-    const uint32_t tot = __shfl(inc, 63);
-    uint32_t base = 0;
-    if (lane == 0 && tot) base = atomicAdd(&D.st->ev_bump, tot);
-    base = __shfl(base, 0);
-    if (base + tot > B.arena_cap) {
-      if (lane == 0 && tot) atomicOr(&D.st->err, ERR_EVENTS);
-      continue;
+    if (lane == 63) wtot[w] = inc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      uint32_t tt = 0;
+      for (uint32_t k = 0; k < FL_EV_T / 64; ++k) { const uint32_t v = wtot[k]; wtot[k] = tt; tt += v; }
+      bbase = tt ? atomicAdd(&D.st->ev_bump, tt) : 0u;
+      if (tt && static_cast<unsigned long long>(bbase) + tt > B.arena_cap) {
+        atomicOr(&D.st->err, ERR_EVENTS);
+        bbase = NIL;
+      }
     }
-    if (!cnt) continue;
-    gome_event* dst = B.arena + base + (inc - cnt);
+    __syncthreads();
+    const uint32_t base = bbase, wb = wtot[w];
+    __syncthreads();  // (wtot / bbase are rewritten by the next tile)
+    if (base == NIL || !cnt) continue;
+    gome_event* dst = B.arena + base + wb + (inc - cnt);
     const uint32_t beg = F.hdr[h].beg, sym = F.hdr[h].sym;
     const Prep tk = prep_at(B, beg + tk_j(x));
     const int64_t price = F.lvl[h * FL_CAP + (x.kr & 127u)].price;

@@ -515,10 +515,31 @@ struct FlPrepScr {
   // the deep prep's own totals (match_flow_deep.h)
   uint32_t d_adds, d_dropped, d_dels, d_bad, d_ndist;
   // a deep tail book's chunk ids for its FIFO appends, claimed once for all its levels
-  // (k_deep_claim): id j = j < c_nst ? free_ids[c_t - c_nst + j] : c_bb + (j - c_nst)
+  // (k_deep_claim; see FlClaim)
   int32_t c_t;
   uint32_t c_nst, c_bb, c_ok;
 };
+
+// A book's chunk ids for all its levels' FIFO appends, claimed at once: id j = j < c_nst ?
+// free_ids[c_t - c_nst + j] : c_bb + (j - c_nst); FlowLvl::pad0 = a level's first j.
+struct FlClaim {
+  int32_t c_t;
+  uint32_t c_nst, c_bb, c_ok;
+};
+
+// Claim `need` chunk ids (free stack first, then the bump pointer); single thread.
+__device__ __forceinline__ FlClaim fl_claim_chunks(const Dev& D, uint32_t need) {
+  FlClaim c{0, 0u, 0u, 1u};
+  if (!need) return c;
+  c.c_t = atomicSub(&D.st->free_top, static_cast<int>(need));
+  c.c_nst = static_cast<uint32_t>(min(max(c.c_t, 0), static_cast<int>(need)));
+  if (c.c_nst < need) c.c_bb = atomicAdd(D.ch_bump, need - c.c_nst);
+  if (static_cast<unsigned long long>(c.c_bb) + (need - c.c_nst) > D.ch_cap) {
+    atomicOr(&D.st->err, ERR_CHUNKS);
+    c.c_ok = 0;
+  }
+  return c;
+}
 
 __device__ __forceinline__ void fl_slice(uint32_t beg, uint32_t end, uint32_t x, uint32_t& b0, uint32_t& b1) {
   const uint64_t len = end - beg;
@@ -1466,6 +1487,18 @@ __device__ __forceinline__ uint32_t fl_book_of(const FlowArgs& F, uint32_t nb, u
   return lo;
 }
 
+// The same for every lane of a wave whose touches are consecutive from g0 (lane 0's): one
+// binary search per wave, then each lane steps over the (at most few) book boundaries after g0.
+// Called by every lane whose gt < total (lane 0 among them).
+__device__ __forceinline__ uint32_t fl_book_of_wave(const FlowArgs& F, uint32_t nb, uint32_t g0, uint32_t gt) {
+  uint32_t hb = 0;
+  if (lane_id() == 0) hb = fl_book_of(F, nb, g0);
+  hb = __shfl(hb, 0);
+  const uint32_t* to = F.toff + F.tb;
+  while (hb + 1 < nb && to[hb + 1] <= gt) ++hb;
+  return hb;
+}
+
 // Exclusive scan of the flow books' touch counts (declined candidates count 0).  KIND: the books
 // the range's count / event kernels cover (FL_OK_ADD: k_flow_*, FL_OK_CANCEL: k_fc_*).
 template <uint32_t KIND>
@@ -1501,7 +1534,7 @@ __global__ void k_flow_count(Dev D, BatchArgs B, FlowArgs F) {
   const uint32_t total = nb ? F.toff[F.tb + nb] : 0u;
   unsigned long long fills = 0, pops = 0;
   for (uint32_t gt = blockIdx.x * blockDim.x + threadIdx.x; gt < total; gt += gridDim.x * blockDim.x) {
-    const uint32_t hb = fl_book_of(F, nb, gt), h = F.h0 + hb, t = gt - F.toff[F.tb + hb];
+    const uint32_t hb = fl_book_of_wave(F, nb, gt - lane_id(), gt), h = F.h0 + hb, t = gt - F.toff[F.tb + hb];
     const uint32_t nt = F.hdr[h].ntouch, beg = F.hdr[h].beg, L = FL_TOUCH_MUL * beg;
     const Touch x = F.log[L + t];
     if (t > 0 && tk_j(F.log[L + t - 1]) == tk_j(x)) continue;
@@ -1549,12 +1582,14 @@ __device__ __forceinline__ void fl_events(const Dev& D, const BatchArgs& B, cons
   __shared__ uint32_t wtot[FL_EV_T / 64], bbase;
   // block tiles (every wave of the block iterates together: the arena is claimed once per tile)
   for (uint32_t b0 = blockIdx.x * blockDim.x; b0 < total; b0 += stride) {
-    const uint32_t gt = b0 + threadIdx.x;
+    const uint32_t gt = b0 + threadIdx.x, g0w = b0 + (threadIdx.x & ~63u);
     uint32_t h = 0, L = 0, t = 0, cnt = 0;
     Touch x{};
     FlTouchCtx c{};
+    uint32_t hbw = 0;
+    if (g0w < total) hbw = fl_book_of_wave(F, nb, g0w, gt < total ? gt : g0w);
     if (gt < total) {
-      const uint32_t hb = fl_book_of(F, nb, gt);
+      const uint32_t hb = hbw;
       h = F.h0 + hb;
       t = gt - F.toff[F.tb + hb];
       L = FL_TOUCH_MUL * F.hdr[h].beg;
@@ -1696,7 +1731,7 @@ __device__ __forceinline__ FlWPlan fl_wplan(const FlowLvl& f, const RsEnt* RS) {
 // first), else the level claims its own.
 __device__ __forceinline__ Level fl_write_level(const Dev& D, const BatchArgs& B, const FlowArgs& F,
                                                 const FlowHdr& hd, uint32_t h, uint32_t q,
-                                                const FlPrepScr* claim = nullptr) {
+                                                const FlClaim* claim = nullptr) {
   const uint32_t lane = lane_id();
   const uint32_t L = FL_TOUCH_MUL * hd.beg;
   const unsigned long long mask = D.idx_mask;
@@ -1855,17 +1890,33 @@ __device__ __forceinline__ void fl_write_finish(const Dev& D, const FlowHdr& hd,
   }
 }
 
-// Tail books: one workgroup per book, waves take its levels in turn, then finish.
+// Tail books: one workgroup per book; the chunk ids of all its appends in one claim, then
+// waves take its levels in turn, then finish.
 __global__ __launch_bounds__(FL_WRITE_T) void k_flow_write(Dev D, BatchArgs B, FlowArgs F) {
   __shared__ Level lv[FL_CAP];
   __shared__ uint32_t keep[FL_CAP];
   __shared__ uint32_t nout_s, base_s, cap_s;
+  __shared__ uint32_t need_s[FL_CAP];
+  __shared__ FlClaim claim_s;
   const uint32_t h = F.h0 + blockIdx.x;
   if (h >= fl_hend(D, F) || F.hdr[h].ok != FL_OK_ADD) return;
   const FlowHdr hd = F.hdr[h];
   const uint32_t w = threadIdx.x >> 6, nw = FL_WRITE_T / 64;
+  FlowLvl* LV = F.lvl + h * FL_CAP;
+  const RsEnt* RS = F.rs + FL_TOUCH_MUL * hd.beg;
+  for (uint32_t q = 1 + threadIdx.x; q <= hd.nl; q += FL_WRITE_T) need_s[q] = fl_wplan(LV[q], RS + LV[q].base).need;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t off = 0;
+    for (uint32_t q = 1; q <= hd.nl; ++q) {
+      LV[q].pad0 = off;
+      off += need_s[q];
+    }
+    claim_s = fl_claim_chunks(D, off);
+  }
+  __syncthreads();
   for (uint32_t q = 1 + w; q <= hd.nl; q += nw) {
-    const Level x = fl_write_level(D, B, F, hd, h, uni(q));
+    const Level x = fl_write_level(D, B, F, hd, h, uni(q), &claim_s);
     if (lane_id() == 0) lv[q] = x;
   }
   __syncthreads();

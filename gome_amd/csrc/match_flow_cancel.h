@@ -988,7 +988,7 @@ __global__ void k_fc_count(Dev D, BatchArgs B, FlowArgs F) {
   const uint32_t total = nb ? F.toff[F.tb + nb] : 0u;
   unsigned long long fills = 0, pops = 0, cancels = 0;
   for (uint32_t gt = blockIdx.x * blockDim.x + threadIdx.x; gt < total; gt += gridDim.x * blockDim.x) {
-    const uint32_t hb = fl_book_of(F, nb, gt), h = F.h0 + hb, t = gt - F.toff[F.tb + hb];
+    const uint32_t hb = fl_book_of_wave(F, nb, gt - lane_id(), gt), h = F.h0 + hb, t = gt - F.toff[F.tb + hb];
     const uint32_t nt = F.hdr[h].ntouch, beg = F.hdr[h].beg, L = FL_TOUCH_MUL * beg;
     const Touch x = F.log[L + t];
     if (t > 0 && tk_j(F.log[L + t - 1]) == tk_j(x)) continue;
@@ -1036,12 +1036,14 @@ __global__ __launch_bounds__(256) void k_fc_events(Dev D, BatchArgs B, FlowArgs 
   __shared__ uint32_t wtot[FL_EV_T / 64], bbase;
   // block tiles (every wave of the block iterates together: the arena is claimed once per tile)
   for (uint32_t b0 = blockIdx.x * blockDim.x; b0 < total; b0 += stride) {
-    const uint32_t gt = b0 + threadIdx.x;
+    const uint32_t gt = b0 + threadIdx.x, g0w = b0 + (threadIdx.x & ~63u);
     uint32_t h = 0, L = 0, t = 0, cnt = 0, kind = TK_REST;
     Touch x{};
     FcTouch T{};
+    uint32_t hbw = 0;
+    if (g0w < total) hbw = fl_book_of_wave(F, nb, g0w, gt < total ? gt : g0w);
     if (gt < total) {
-      const uint32_t hb = fl_book_of(F, nb, gt);
+      const uint32_t hb = hbw;
       h = F.h0 + hb;
       t = gt - F.toff[F.tb + hb];
       L = FL_TOUCH_MUL * F.hdr[h].beg;

@@ -588,22 +588,11 @@ __device__ __forceinline__ void k_deep_claim_one(Dev D, BatchArgs B, FlowArgs F,
   }
   if (tid == 0) {
     FlPrepScr* P = F.dscr + hd.dslot;
-    const uint32_t need = tot_s;
-    int t = 0;
-    uint32_t nst = 0, bb = 0, ok = 1;
-    if (need) {
-      t = atomicSub(&D.st->free_top, static_cast<int>(need));
-      nst = static_cast<uint32_t>(min(max(t, 0), static_cast<int>(need)));
-      if (nst < need) bb = atomicAdd(D.ch_bump, need - nst);
-      if (static_cast<unsigned long long>(bb) + (need - nst) > D.ch_cap) {
-        atomicOr(&D.st->err, ERR_CHUNKS);
-        ok = 0;
-      }
-    }
-    P->c_t = t;
-    P->c_nst = nst;
-    P->c_bb = bb;
-    P->c_ok = ok;
+    const FlClaim c = fl_claim_chunks(D, tot_s);
+    P->c_t = c.c_t;
+    P->c_nst = c.c_nst;
+    P->c_bb = c.c_bb;
+    P->c_ok = c.c_ok;
   }
 }
 __global__ __launch_bounds__(DEEP_CLAIM_T) void k_deep_claim(Dev D, BatchArgs B, FlowArgs F) {
@@ -617,7 +606,9 @@ __device__ __forceinline__ void k_deep_write_lv_one(Dev D, BatchArgs B, FlowArgs
   const uint32_t h = fd_book(D, F, slot_i);
   if (!fd_deep(F, h)) return;
   const FlowHdr hd = F.hdr[h];
-  const FlPrepScr* claim = F.dscr + hd.dslot;
+  const FlPrepScr* P = F.dscr + hd.dslot;
+  const FlClaim cl{P->c_t, P->c_nst, P->c_bb, P->c_ok};
+  const FlClaim* claim = &cl;
   for (uint32_t q = 1 + blockIdx.x; q <= hd.nl; q += gridDim.x) {
     const Level x = fl_write_level(D, B, F, hd, h, q, claim);
     if (lane_id() == 0) F.dlvout[static_cast<size_t>(hd.dslot) * DEEP_CAP + q] = x;

@@ -58,6 +58,25 @@ def test_bench_config3_exact_4mi_batches():
     assert eng.stats()["n_resting"] == orc.resting()
 
 
+def test_bench_config2_full_batches():
+    """bench.py --workload config2 exactly (1k symbols, uniform, 4 Mi-order batches): ~1000 flow
+    books of ~4k orders each, nearly all in the tail (per-book claims, per-wave book lookups,
+    block-tile arena claims), two batches vs the oracle, levels and FIFOs of 108 books."""
+    n = 1 << 22
+    gen, _, _ = bench.make_stream("config2", 0, 1, 42)
+    eng = Engine(max_symbols=1000, max_batch=n, max_nodes=3 * n, max_levels=1 << 23)
+    orc = Oracle(1000)
+    for i in range(2):
+        b = gen(n).copy()
+        eng.submit(b)
+        _cmp(eng.drain(), orc.submit(b), f"config2 batch {i}")
+        st = eng.stats()
+        assert st["n_flow_books"] >= 990
+    syms = list(range(8)) + np.random.default_rng(1).choice(1000, 100, replace=False).tolist()
+    _cmp_books(eng, orc, [int(s) for s in syms], "config2")
+    assert eng.stats()["n_resting"] == orc.resting()
+
+
 def test_bench_config4_native_stream():
     """bench.py --workload config4 (native generator: 50% DEL, 10% aggressive), 1 Mi batches."""
     n = 1 << 20

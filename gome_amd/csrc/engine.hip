@@ -409,6 +409,7 @@ gome_status gome_engine::init(const gome_config& c) {
   if (!alloc(&F.fc_img, F.fc_img_cap, "flow cancel ring images") || !alloc(&F.fc_img_bump, 1, "flow cancel image bump") ||
       !alloc(&F.fc_del, nb, "flow cancel records") ||
       !alloc(&F.fc_tg, nb, "flow cancel targets") || !alloc(&F.fc_rank, nb, "flow cancel ranks") ||
+      !alloc(&F.fc_dt, nb, "flow cancel DEL times") ||
       !alloc(&F.fc_hash, fc_hcap, "flow cancel table"))
     return GOME_E_CAPACITY;
   HIPCHK(hipMemsetAsync(F.fc_hash, 0, sizeof(FcHash) * fc_hcap, stream));
@@ -599,6 +600,7 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
       k_fc_pscan<<<nb, FL_CAP, 0, st>>>(D, R);
       k_fc_prank<<<dim3(FL_SORT_GRID, nb), FL_TILE, 0, st>>>(D, B, R);
       k_fc_pwin<<<dim3(px, nb), 256, 0, st>>>(D, B, R);
+      k_fc_pmax<<<dim3(FL_CAP, nb), 64, 0, st>>>(D, R);
       k_fc_playout<<<nb, 1024, 0, st>>>(D, R);
       k_fc_precs<<<dim3(px, nb), 256, 0, st>>>(D, B, R);
     } else {

@@ -594,26 +594,24 @@ class Gen:
 
 
 # ---- W32C: the 32-bit plan of a book whose segment holds DELs -------------
-# Record (8 B): lo = ADD volume in units of g | DEL: window length n_b [0,16) | log2 C_k [16,21);
+# Record (8 B): lo = ADD volume in units of g | DEL: push window wp [0,16) | log2 C_k [16,21);
 # hi = level [0,7) | ring slot p [7,22) | DEL: maker SALE bit 29, DEL bit 30 | SALE (ADD) or 1
 # (DEL) bit 31.  Per level the plan also keeps R_k, the volume that ever arrived (lane pair
-# v[36:37], W32 layout), and every ADD owns an 8-B LDS ring entry {E, v | X << 31} (non-targeted
-# ADDs a dummy one): v = 0 when the ADD crosses (it may never rest), {R_k before, T} when it
-# rests; X marks a target that was cancelled (its cancelled volume is v).  A DEL of target m at
-# level k takes r = clamp(E_m + v_m - (R_k - depth_k) + Xb, 0, v_m) where Xb sums v over the
-# cancelled entries of the ring window of the n_b targets that arrived behind m (ranks rank_m +
-# 1 ..): each DEL sets its target's X.  The cancel plan runs only when every R_k < 2^31 (plan
-# units), so a window sum of flagged words is Xb + cnt * 2^31 and bit 31 drops out.  Touch keys
-# come from an order counter (JJS, as the 64-bit plan): rest = JJS | k | 1 << 7, consume = JJS |
-# k, cancel = JJS | k | 1 << 31 (amount r).
+# v[36:37], W32 layout), and every ADD owns an 8-B LDS ring entry {E, v} (non-targeted ADDs a
+# dummy one): v = 0 when the ADD crosses (it may never rest), {R_k before, T} when it rests.  A
+# DEL of target m at level k takes r = clamp(E_m + v_m - (R_k - depth_k) + Xb_m, 0, v_m), where
+# Xb_m is the volume of the targets behind m cancelled before (each removed exactly its v).  It
+# is accumulated in place: a DEL adds its target's v to the E words of the wp ranks ahead of its
+# target that may still be pending (the prep's push windows, match_flow_cancel.h), so a DEL reads
+# one entry {E_m + Xb_m, v_m}.  The cancel plan runs only when every R_k < 2^31 (plan units), so
+# E + Xb + v stays below 2^31.  Touch keys come from an order counter (JJS, as the 64-bit plan):
+# rest = JJS | k | 1 << 7, consume = JJS | k, cancel = JJS | k | 1 << 31 (amount r).
 CREG = {"R": (36, 37)}
 VZ0 = 39                     # stays 0
-VE, VM = 40, 41              # a rest's entry {E, T}; a DEL's entry read {E, v} -> v[40:41]
-VT = 42                      # window: flag mask
+VE, VM = 40, 41              # a rest's entry {E, T}; a DEL's entry read {E + Xb, v} -> v[40:41]
 VA = 43                      # LDS address
 VG0, VG1 = 44, 45            # G_k words
-VW, VX, VL = 46, 47, 48      # window address / data, lane id
-VF = 49                      # 1 << 31 (the cancelled flag)
+VW, VL = 46, 48              # push addresses, lane id
 X0, X1, X2, X3 = "s79", "s81", "s83", "s96"              # free in the 32-bit layout
 CLOBBERS_C = [f"v{i}" for i in range(36, 50)]
 
@@ -694,46 +692,22 @@ class GenC(Gen):
         e(f"s_bitset1_b32 {K}, 7")
         self.log(K, T, False)
 
-    def reduce_window(self, dst: str):
-        """dst = sum of the window data over the wave (DPP scan, lane 63 = total)."""
+    def push_addr(self, first: str):
+        """v{VW} = byte address of ring slot pbase | ((first - lane) & mask) (X2 = mask, X1 =
+        pbase): lane l pushes to the rank `first` - l."""
         e = self.e
-        v = f"v{VX}"
-        for ctl in ("row_shr:1 bound_ctrl:0", "row_shr:2 bound_ctrl:0", "row_shr:4 bound_ctrl:0",
-                    "row_shr:8 bound_ctrl:0", "row_bcast:15 row_mask:0xa", "row_bcast:31 row_mask:0xc"):
-            e("s_nop 1")
-            e(f"v_add_u32_dpp {v}, {v}, {v} {ctl}")
-        e("s_nop 1")
-        e(f"v_readlane_b32 {dst}, {v}, 63")
-
-    def window_read(self, lanes: str, first: str):
-        """window data = the {v | X << 31} word of ring slots pbase | ((first + lane) & mask) for
-        lanes < `lanes` (others 0); X2 = mask, X1 = pbase."""
-        e = self.e
-        e("s_mov_b64 exec, -1")
-        e(f"v_mov_b32 v{VX}, 0")
-        e(f"s_bfm_b64 exec, {lanes}, 0")
-        e(f"v_add_u32 v{VW}, {first}, v{VL}")
+        e(f"v_sub_u32 v{VW}, {first}, v{VL}")
         e(f"v_and_b32 v{VW}, {X2}, v{VW}")
         e(f"v_or_b32 v{VW}, {X1}, v{VW}")
         e(f"v_lshlrev_b32 v{VW}, 3, v{VW}")
-        e(f"ds_read_b32 v{VX}, v{VW} offset:4")
-
-    def window_sum(self, lanes: str):
-        """After the window read landed: s-register `lanes` := the sum of v over its cancelled
-        (flagged) entries (each flagged word is v + 2^31; every sum stays below 2^31)."""
-        e = self.e
-        e("s_mov_b64 exec, -1")
-        e(f"v_ashrrev_i32 v{VT}, 31, v{VX}")                  # cancelled entries only
-        e(f"v_and_b32 v{VX}, v{VX}, v{VT}")
-        self.reduce_window(lanes)
-        e(f"s_bitset0_b32 {lanes}, 31")                       # (- cnt * 2^31)
 
     def del_path(self, i: int):
-        """DeleteOrder (engine.go:87-116) on the aggregates of level LI: r = clamp(end_m + Xb -
-        G_k, 0, v_m).  The first 63 ranks of the window (ranks p + 1 .. of the level's ring:
-        every window but ~2% of them) and the target's entry are read together, G_k = R_k -
-        depth_k comes from lane LI >> 1 while both reads are in flight, then one wait, the
-        window's reduction and the clamp; longer windows finish out of line."""
+        """DeleteOrder (engine.go:87-116) on the aggregates of level LI: r = clamp(E_m + Xb_m +
+        v_m - G_k, 0, v_m).  The target's entry already holds E_m + Xb_m (every earlier DEL of a
+        target behind m pushed its v there), so the path is one LDS read — by every lane, which
+        then holds v_m for this DEL's own push: v_m added to the entries of the wp ranks ahead of
+        m (ranks p - 1, p - 2, ..: 63 lanes at a time, the rest out of line; fire and forget).
+        G_k = R_k - depth_k comes from lane LI >> 1 while the read is in flight."""
         e = self.e
         lo, hi = f"s{BUF[i][0]}", f"s{BUF[i][1]}"
         lab = self.lab
@@ -742,18 +716,16 @@ class GenC(Gen):
         bev, bod = PAIR["B"]
         e(f"{lab(f'D{i}')}:")
         self.entry_addr(hi)                                   # X3 = the entry's byte address
-        e(f"s_and_b32 {X0}, {lo}, 0xffff")                    # n_b
+        e("s_mov_b64 exec, -1")
+        e(f"v_mov_b32 v{VA}, {X3}")
+        e(f"ds_read_b64 v[{VE}:{VM}], v{VA}")                 # {E_m + Xb_m, v_m} in every lane
+        e(f"s_and_b32 {X0}, {lo}, 0xffff")                    # wp
         e(f"s_lshr_b32 {X1}, {lo}, 16")
         e(f"s_bfm_b32 {X2}, {X1}, 0")                         # mask = C_k - 1
         e(f"s_lshr_b32 {T0}, {X3}, 3")                        # p
         e(f"s_andn2_b32 {X1}, {T0}, {X2}")                    # pbase
-        e(f"s_add_u32 {K}, {T0}, 1")                          # first window rank (mod C_k)
-        e(f"s_min_u32 {L}, {X0}, 63")
-        self.window_read(L, K)
-        e(f"s_lshr_b32 {T0}, {LI}, 1")
-        e(f"s_bfm_b64 exec, 1, {T0}")                         # lane LI >> 1
-        e(f"v_mov_b32 v{VA}, {X3}")
-        e(f"ds_read_b64 v[{VE}:{VM}], v{VA}")                 # {E_m, v_m} (X is clear)
+        e(f"s_sub_u32 {K}, {T0}, 1")                          # first rank pushed to: p - 1
+        self.push_addr(K)
         # G_k = R_k - depth_k: the level's words of the R / ask / bid pairs (a cached top's lane
         # is 0, its depth is in SGPRs)
         e(f"v_sub_u32 v{VG0}, v{ev}, v{aev}")
@@ -769,23 +741,21 @@ class GenC(Gen):
         e(f"s_cselect_b32 s95, {BBD[0]}, 0")
         e(f"s_add_u32 s94, s94, s95")
         e(f"v_subrev_u32 v{VG0}, s94, v{VG0}")                # G_k
+        e(f"s_min_u32 {L}, {X0}, 63")
         e("s_waitcnt lgkmcnt(0)")
-        self.window_sum(L)
-        e(f"s_mov_b32 s90, {L}")                              # Xb
+        e(f"s_bfm_b64 exec, {L}, 0")
+        e(f"ds_add_u32 v{VW}, v{VM}")                         # push v_m (E fields, offset 0)
         win, back = lab(f"DW{i}"), lab(f"DWB{i}")
         e(f"s_cmp_gt_u32 {X0}, 63")
         e(f"s_cbranch_scc1 {win}")
         e(f"{back}:")
         e(f"s_lshr_b32 {T0}, {LI}, 1")
         e(f"s_bfm_b64 exec, 1, {T0}")
-        # a = E_m + v_m + Xb (< 2^31: the window's makers arrived after m); r = a - G_k clamped
-        # to [0, v_m]; X_m := 1
+        # a = E_m + Xb_m + v_m (< 2^31); r = a - G_k clamped to [0, v_m]
         e(f"v_add_u32 v{VE}, v{VE}, v{VM}")
-        e(f"v_add_u32 v{VE}, s90, v{VE}")
         e(f"v_sub_co_u32 v{VE}, vcc, v{VE}, v{VG0}")
         e(f"v_cndmask_b32 v{VE}, v{VE}, v{VZ0}, vcc")
         e(f"v_min_u32 v{VE}, v{VE}, v{VM}")
-        e(f"ds_or_b32 v{VA}, v{VF} offset:4")
         e(f"v_readlane_b32 {X1}, v{VE}, {T0}")                # r
         e(f"s_cmp_eq_u32 {X1}, 0")
         e(f"s_cbranch_scc1 {lab(f'DZ{i}')}")                  # not found: no event (:96-98)
@@ -820,7 +790,7 @@ class GenC(Gen):
             self.dispatch((i + 1) % NS, False)
         e(f"{lab(f'DZ{i}')}:")
         self.dispatch((i + 1) % NS, False)
-        # windows beyond 63 targets (out of line): the rest of the ranks, 63 lanes at a time
+        # pushes beyond 63 ranks (out of line): 63 lanes at a time
         blk = [f"{win}:"]
         self.slow.append(blk)
         sv = self.out
@@ -830,11 +800,11 @@ class GenC(Gen):
         e(f"{loop}:")
         e(f"s_sub_u32 {L}, {X0}, s92")
         e(f"s_min_u32 {L}, {L}, 63")
-        e(f"s_add_u32 {T0}, {K}, s92")
-        self.window_read(L, T0)
-        e("s_waitcnt lgkmcnt(0)")
-        self.window_sum(L)
-        e(f"s_add_u32 s90, s90, {L}")
+        e(f"s_sub_u32 {T0}, {K}, s92")
+        e("s_mov_b64 exec, -1")
+        self.push_addr(T0)
+        e(f"s_bfm_b64 exec, {L}, 0")
+        e(f"ds_add_u32 v{VW}, v{VM}")
         e("s_add_u32 s92, s92, 63")
         e(f"s_cmp_lt_u32 s92, {X0}")
         e(f"s_cbranch_scc1 {loop}")
@@ -887,7 +857,6 @@ class GenC(Gen):
         e(f"v_mbcnt_lo_u32_b32 v{VL}, -1, 0")
         e(f"v_mbcnt_hi_u32_b32 v{VL}, -1, v{VL}")
         e(f"v_mov_b32 v{VZ0}, 0")
-        e(f"v_bfrev_b32 v{VF}, 1")
         ev, od = CREG["R"]
         e(f"v_mov_b32 v{ev}, %[rl0]")
         e(f"v_mov_b32 v{od}, %[rl1]")

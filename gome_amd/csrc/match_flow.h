@@ -166,7 +166,9 @@ struct FlowLvl {
   uint32_t rbase;    // first ring entry of the level (aligned to cring)
   uint32_t ocan;     // cancelled volume of old makers (plan units), set by the recon
   uint32_t memf;     // deep books: membership after the batch (M_BUY / M_SALE)
-  uint32_t pad3[3];
+  uint32_t ttot;     // targets of the level (old + new): ranks 0 .. ttot - 1
+  uint32_t tbase;    // first entry of the level's DEL-time array in FlowArgs::fc_dt (book-local)
+  uint32_t pad3;
 };
 static_assert(sizeof(FlowLvl) % 16 == 0, "FlowLvl alignment");
 
@@ -213,6 +215,8 @@ struct FlowArgs {
   FcDel* fc_del;       // [max_batch] per segment position: the DEL's target
   uint32_t* fc_tg;     // [max_batch] per segment position: ADD targeted by the DEL at (value - 1)
   uint32_t* fc_rank;   // [max_batch] per segment position: a targeted ADD's rank in its level
+  uint32_t* fc_dt;     // [max_batch] per book, per level, per target rank: its DEL's segment
+                       // position, then the prefix max of those (the push windows' search array)
   FcHash* fc_hash;     // (symbol, oid) table of the cancel books' records
   uint64_t fc_hmask;
   // deep books (match_flow_deep.h), per deep slot: level tables, final level records, price

@@ -65,7 +65,7 @@ struct FcDel {
   uint32_t oend, ov; // FC_OLD: arrival end / volume (plan units)
   int64_t r;         // recon: volume cancelled (fixed point), 0 if the DEL found nothing
   uint32_t ct;       // recon: touch index of the cancel, NIL if none
-  uint32_t pad;
+  uint32_t wp;       // push window: ranks rank - wp .. rank - 1 may still be pending
 };
 static_assert(sizeof(FcDel) == 48, "FcDel layout");
 enum : uint32_t { FC_NONE = 0, FC_NEW = 1, FC_OLD = 2 };
@@ -311,6 +311,71 @@ __global__ __launch_bounds__(1024) void k_fc_oldwalk_book(Dev D, FlowArgs F) {
   for (uint32_t q = 1 + (threadIdx.x >> 6); q <= F.hdr[h].nl; q += blockDim.x / 64) fc_oldwalk_level(D, F, h, uni(q));
 }
 
+// ---- push windows ----------------------------------------------------------------------------
+// The plan adds a cancelled target's volume v to the ring entries of the targets *ahead* of it
+// that are still pending (their DEL comes later), so each target's entry holds E + Xb by the time
+// its own DEL reads it: Xb needs no window read.  Ranks are dense per level (one DEL per target),
+// so with DT[r] = the segment position of rank r's DEL and PM its prefix maximum, the oldest
+// target still pending at a DEL at position b is the smallest r with PM[r] >= b, and the DEL
+// pushes to ranks r .. rank - 1 (wp of them; the ones between that are already cancelled do not
+// read their entries again).  Every pending target arrived within the ring window of its own
+// DEL, so ring capacities sized for the windows hold these ranks too.
+
+// Per level: its targets' count and their first entry of the book's DEL-time array (an exclusive
+// scan over the book's levels; `tot` = 0 for threads that are not levels).  Every thread of the
+// block calls it (threads k >= FL_CAP take no part).
+__device__ __forceinline__ void fc_time_bases(FlowLvl* LV, uint32_t k, uint32_t tot) {
+  __shared__ uint32_t wsum[FL_CAP / 64];
+  const bool in = k < FL_CAP;
+  const uint32_t inc = wave_incl_scan_u32(in ? tot : 0u), w = k >> 6;
+  if (in && (k & 63u) == 63u) wsum[w] = inc;
+  __syncthreads();
+  if (in && k >= 1) {
+    uint32_t base = inc - tot;
+    for (uint32_t ww = 0; ww < w; ++ww) base += wsum[ww];
+    LV[k].ttot = tot;
+    LV[k].tbase = base;
+  }
+  __syncthreads();
+}
+
+// In place: DT -> PM over each level's ranks (one wave per (book, level)).
+__device__ __forceinline__ void fc_time_pmax(uint32_t* dt, uint32_t n) {
+  uint32_t carry = 0;
+  for (uint32_t r0 = 0; r0 < n; r0 += 64) {
+    const uint32_t r = r0 + lane_id();
+    const uint32_t m = max(wave_incl_max_u32(r < n ? dt[r] : 0u), carry);
+    if (r < n) dt[r] = m;
+    carry = rl(m, 63);
+  }
+}
+
+// wp of a DEL at segment position b whose target has rank rk (pm[rk] >= b: its own DEL): back
+// from rk in doubling steps to a rank whose PM is below b, then a binary search in between.
+__device__ __forceinline__ uint32_t fc_push_window(const uint32_t* pm, uint32_t rk, uint32_t b) {
+  int32_t hi = static_cast<int32_t>(rk), lo = -1;
+  for (int32_t step = 1; step <= hi; step <<= 1) {
+    if (pm[hi - step] < b) {
+      lo = hi - step;
+      break;
+    }
+    hi -= step;
+  }
+  while (hi - lo > 1) {
+    const int32_t mid = lo + (hi - lo) / 2;
+    if (pm[mid] >= b) hi = mid;
+    else lo = mid;
+  }
+  return rk - static_cast<uint32_t>(hi);
+}
+
+__global__ __launch_bounds__(64) void k_fc_pmax(Dev D, FlowArgs F) {
+  const uint32_t h = F.h0 + blockIdx.y, q = blockIdx.x;
+  if (h >= fl_hend(D, F) || !fc_book(F, h) || q == 0 || q > F.hdr[h].nl) return;
+  const FlowLvl& L = F.lvl[h * FL_CAP + q];
+  fc_time_pmax(F.fc_dt + F.hdr[h].beg + L.tbase, L.ttot);
+}
+
 // ---- prep 5: ranks, windows, ring layout, image and W32C records (one block per book) -------
 constexpr uint32_t FC_PASS_T = 1024, FC_PASS_W = FC_PASS_T / 64;
 
@@ -385,6 +450,17 @@ __global__ __launch_bounds__(FC_PASS_T) void k_fc_pass(Dev D, BatchArgs B, FlowA
     for (uint32_t x = tid; x < FC_PASS_W * FL_CAP; x += FC_PASS_T) wc[x / FL_CAP][x % FL_CAP] = 0;
     __syncthreads();
   }
+  // push windows: per level the targets' DEL times, then their prefix maxima
+  fc_time_bases(LV, tid, (tid >= 1 && tid <= nl) ? LV[tid].c_old + cnt[tid] : 0u);
+  for (uint32_t i = tid; i < n; i += FC_PASS_T) {
+    const uint32_t b = hd.beg + i;
+    if (prep_at(B, b).action != GOME_DEL) continue;
+    const FcDel d = F.fc_del[b];
+    if (d.kind != FC_NONE) F.fc_dt[hd.beg + LV[d.li].tbase + d.rank] = b;
+  }
+  __syncthreads();
+  for (uint32_t q = 1 + w; q <= nl; q += FC_PASS_W) fc_time_pmax(F.fc_dt + hd.beg + LV[q].tbase, LV[q].ttot);
+  __syncthreads();
   // ring layout: power-of-two capacities, placed largest first (each base aligned to its size)
   if (tid == 0) {
     const uint32_t cap = F.fc_ring_cap;
@@ -453,8 +529,9 @@ __global__ __launch_bounds__(FC_PASS_T) void k_fc_pass(Dev D, BatchArgs B, FlowA
           const uint32_t kk = d.li, slot = rbase[kk] + (d.rank & (cring[kk] - 1u));
           const bool sale = prep_at(B, b).side == GOME_SALE;
           const uint32_t lgc = 31u - __clz(cring[kk]);
+          const uint32_t wp = fc_push_window(F.fc_dt + hd.beg + LV[kk].tbase, d.rank, b);
           rec = (static_cast<unsigned long long>(kk | (slot << 7) | (sale ? 1u << 29 : 0u) | (3u << 30)) << 32) |
-                (d.nb | (lgc << 16));
+                (wp | (lgc << 16));
           if (d.kind == FC_OLD) img[slot] = make_uint2(d.oend - d.ov, d.ov);  // {E, v}, not cancelled
         }
       }
@@ -517,6 +594,7 @@ __global__ __launch_bounds__(FL_CAP) void k_fc_pscan(Dev D, FlowArgs F) {
     tc[tl * FL_CAP + k] = run;
     run += v;
   }
+  fc_time_bases(LV, k, lv ? run : 0u);
 }
 
 // Targeted ADDs' ranks; a DEL's count of its level's targets that arrived before it (in nb).
@@ -582,6 +660,7 @@ __global__ __launch_bounds__(256) void k_fc_pwin(Dev D, BatchArgs B, FlowArgs F)
     const uint32_t nb = d.nb - rk - 1u;
     F.fc_del[b].rank = rk;
     F.fc_del[b].nb = nb;
+    F.fc_dt[hd.beg + LV[d.li].tbase + rk] = b;
     atomicMax(&LV[d.li].cring, nb + 1u);
     if (nb >= 0xFFFFu) bad = FC_BAD_RING;
   }
@@ -669,8 +748,9 @@ __global__ __launch_bounds__(256) void k_fc_precs(Dev D, BatchArgs B, FlowArgs F
           const uint32_t kk = d.li, cr = LV[kk].cring, slot = LV[kk].rbase + (d.rank & (cr - 1u));
           const bool sale = prep_at(B, b).side == GOME_SALE;
           const uint32_t lgc = 31u - __clz(cr);
+          const uint32_t wp = fc_push_window(F.fc_dt + hd.beg + LV[kk].tbase, d.rank, b);
           rec = (static_cast<unsigned long long>(kk | (slot << 7) | (sale ? 1u << 29 : 0u) | (3u << 30)) << 32) |
-                (d.nb | (lgc << 16));
+                (wp | (lgc << 16));
           if (d.kind == FC_OLD) img[slot] = make_uint2(d.oend - d.ov, d.ov);  // {E, v}, not cancelled
         }
       }

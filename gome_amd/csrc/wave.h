@@ -48,6 +48,16 @@ __device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t x) {
   return x;
 }
 
+__device__ __forceinline__ uint32_t wave_incl_max_u32(uint32_t x) {
+  const uint32_t lane = lane_id();
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t y = __shfl_up(x, off);
+    if (lane >= static_cast<uint32_t>(off)) x = max(x, y);
+  }
+  return x;
+}
+
 // Inclusive scan of a 64-bit value over lanes 0..31 (rows 0 and 1) with DPP row shifts
 // (VALU-latency, no LDS crossbar) and one readlane to carry row 0 into row 1.
 // Lanes 32..63 return unspecified values.

@@ -621,11 +621,15 @@ class GenC(Gen):
         super().__init__(32)
 
     def decode(self, j: int):
-        """LI and SCC = SALE-or-DEL of record j; the order counter advances (JJS = index << 8)."""
+        """LI of record j, a DEL branches to its path first (half the records of a cancel-heavy
+        stream: one taken branch instead of two), then SCC = SALE; the order counter advances
+        (JJS = index << 8)."""
         e = self.e
         hi = f"s{BUF[j][1]}"
         e(f"s_add_u32 {JJS}, {JJS}, 256")
         e(f"s_and_b32 {LI}, {hi}, 127")
+        e(f"s_bitcmp1_b32 {hi}, 30")
+        e(f"s_cbranch_scc1 {self.lab(f'D{j}')}")
         e(f"s_bitcmp1_b32 {hi}, 31")
 
     def entry_addr(self, hi: str):
@@ -843,8 +847,6 @@ class GenC(Gen):
         self.dispatch(j, False)
         self.del_path(i)
         e(f"{lab(f'S{i}')}:")
-        e(f"s_bitcmp1_b32 {hi}, 30")
-        e(f"s_cbranch_scc1 {lab(f'D{i}')}")
         e(f"s_cmp_ge_u32 {BB}, {LI}")
         e(f"s_cbranch_scc1 {lab(f'SXE{i}')}")
         e(f"{lab(f'SR{i}')}:")

@@ -409,7 +409,8 @@ gome_status gome_engine::init(const gome_config& c) {
   if (!alloc(&F.fc_img, F.fc_img_cap, "flow cancel ring images") || !alloc(&F.fc_img_bump, 1, "flow cancel image bump") ||
       !alloc(&F.fc_del, nb, "flow cancel records") ||
       !alloc(&F.fc_tg, nb, "flow cancel targets") || !alloc(&F.fc_rank, nb, "flow cancel ranks") ||
-      !alloc(&F.fc_dt, nb, "flow cancel DEL times") ||
+      !alloc(&F.fc_dt, nb, "flow cancel DEL times") || !alloc(&F.fc_tv, nb, "flow cancel target volumes") ||
+      !alloc(&F.tvol, static_cast<size_t>(FL_HEAD) * F.maxt * FC_KEYS, "flow head tile volumes") ||
       !alloc(&F.fc_hash, fc_hcap, "flow cancel table"))
     return GOME_E_CAPACITY;
   HIPCHK(hipMemsetAsync(F.fc_hash, 0, sizeof(FcHash) * fc_hcap, stream));
@@ -588,7 +589,7 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
     k_deep_prep_c<<<dim3(px, ns), FL_PREP_T, 0, st>>>(D, B, R);
   };
   deep_prep(FH, FL_PG, flow_stream);
-  // books with DELs: targets, windows, ring images, W32C records (or back to the legacy path)
+  // books with DELs: targets, windows, Q and the W32C DEL records (or back to the legacy path)
   auto cancel_prep = [&](const FlowArgs& R, uint32_t nb, uint32_t px, bool wide, hipStream_t st) {
     k_fc_hash_claim<<<dim3(px, nb), 256, 0, st>>>(D, B, R);
     k_fc_hash_count<<<dim3(px, nb), 256, 0, st>>>(D, B, R);
@@ -600,8 +601,6 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
       k_fc_pscan<<<nb, FL_CAP, 0, st>>>(D, R);
       k_fc_prank<<<dim3(FL_SORT_GRID, nb), FL_TILE, 0, st>>>(D, B, R);
       k_fc_pwin<<<dim3(px, nb), 256, 0, st>>>(D, B, R);
-      k_fc_pmax<<<dim3(FL_CAP, nb), 64, 0, st>>>(D, R);
-      k_fc_playout<<<nb, 1024, 0, st>>>(D, R);
       k_fc_precs<<<dim3(px, nb), 256, 0, st>>>(D, B, R);
     } else {
       k_fc_oldwalk_book<<<nb, 1024, 0, st>>>(D, R);

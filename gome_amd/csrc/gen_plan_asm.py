@@ -594,26 +594,19 @@ class Gen:
 
 
 # ---- W32C: the 32-bit plan of a book whose segment holds DELs -------------
-# Record (8 B): lo = ADD volume in units of g | DEL: push window wp [0,16) | log2 C_k [16,21);
-# hi = level [0,7) | ring slot p [7,22) | DEL: maker SALE bit 29, DEL bit 30 | SALE (ADD) or 1
-# (DEL) bit 31.  Per level the plan also keeps R_k, the volume that ever arrived (lane pair
-# v[36:37], W32 layout), and every ADD owns an 8-B LDS ring entry {E, v} (non-targeted ADDs a
-# dummy one): v = 0 when the ADD crosses (it may never rest), {R_k before, T} when it rests.  A
-# DEL of target m at level k takes r = clamp(E_m + v_m - (R_k - depth_k) + Xb_m, 0, v_m), where
-# Xb_m is the volume of the targets behind m cancelled before (each removed exactly its v).  It
-# is accumulated in place: a DEL adds its target's v to the E words of the wp ranks ahead of its
-# target that may still be pending (the prep's push windows, match_flow_cancel.h), so a DEL reads
-# one entry {E_m + Xb_m, v_m}.  The cancel plan runs only when every R_k < 2^31 (plan units), so
-# E + Xb + v stays below 2^31.  Touch keys come from an order counter (JJS, as the 64-bit plan):
-# rest = JJS | k | 1 << 7, consume = JJS | k, cancel = JJS | k | 1 << 31 (amount r).
-CREG = {"R": (36, 37)}
-VZ0 = 39                     # stays 0
-VE, VM = 40, 41              # a rest's entry {E, T}; a DEL's entry read {E + Xb, v} -> v[40:41]
-VA = 43                      # LDS address
-VG0, VG1 = 44, 45            # G_k words
-VW, VL = 46, 48              # push addresses, lane id
-X0, X1, X2, X3 = "s79", "s81", "s83", "s96"              # free in the 32-bit layout
-CLOBBERS_C = [f"v{i}" for i in range(36, 50)]
+# ADD records are the W32 records (hi = level | 1 << 7 | j << 8 | SALE << 31, lo = volume in
+# units of g; j < 2^22 in these books, so bit 30 is clear).  A DEL record: hi = level | v << 7 |
+# 1 << 30 | maker SALE << 31 (v < 2^22: the target's volume), lo = Q, the volume of the makers of
+# the target's side that arrived at the level after the target and before the DEL and were not
+# cancelled before it (computed by the cancel prep, match_flow_cancel.h).  While the target m is
+# live those makers are untouched (only the FIFO head is ever partly consumed, and a same-side
+# ADD at m's level cannot cross) and, if m itself was partly consumed, nothing ahead of it is
+# live; once m is gone (or never rested) the side's depth of the level is at most Q.  So
+# DeleteOrder (engine.go:87-116) removes r = clamp(depth - Q, 0, v): no per-maker state in the
+# plan.  A DEL that finds nothing (r = 0) logs no touch (M0 advances by r != 0).  Touch keys of
+# DELs and consumes come from an order counter (JJS = j << 8, no side bit).
+VE = 40                      # a DEL's depth word, then r (lane level >> 1)
+CLOBBERS_C = [f"v{VE}", f"v{VE + 1}"]
 
 
 class GenC(Gen):
@@ -621,9 +614,8 @@ class GenC(Gen):
         super().__init__(32)
 
     def decode(self, j: int):
-        """LI of record j, a DEL branches to its path first (half the records of a cancel-heavy
-        stream: one taken branch instead of two), then SCC = SALE; the order counter advances
-        (JJS = index << 8)."""
+        """The order counter advances; LI of record j; a DEL branches to its path first, then
+        SCC = SALE."""
         e = self.e
         hi = f"s{BUF[j][1]}"
         e(f"s_add_u32 {JJS}, {JJS}, 256")
@@ -632,237 +624,81 @@ class GenC(Gen):
         e(f"s_cbranch_scc1 {self.lab(f'D{j}')}")
         e(f"s_bitcmp1_b32 {hi}, 31")
 
-    def entry_addr(self, hi: str):
-        """X3 = byte address of the record's ring entry (slot [7, 22) of hi, 8-B entries)."""
-        self.e(f"s_lshr_b32 {X3}, {hi}, 4")
-        self.e(f"s_and_b32 {X3}, {X3}, 0x3fff8")
-
     def cross_entry(self, T):
-        """An ADD that crosses may be filled completely and never rest: its entry's v := 0 now
-        (an ADD that rests writes the whole entry)."""
-        e = self.e
-        self.entry_addr(T[1])
-        e("s_mov_b64 exec, 1")
-        e(f"v_mov_b32 v{VA}, {X3}")
-        e(f"ds_write_b32 v{VA}, v{VZ0} offset:4")
+        """(The consume key base is the order counter.)"""
 
-    def dispatch(self, j: int, fall: bool, copy: bool = COPY_REST):
+    def del_log(self, r: str):
+        """The cancel touch {JJS | level | 1 << 30 | SALE << 31, r}; M0 advances only when r != 0
+        (SCC = r != 0 on entry)."""
         e = self.e
-        if j % HG == 0:
-            if not fall:
-                e(f"s_branch {self.lab(f'H{j}')}")
-            return
-        self.decode(j)
-        e(f"s_cbranch_scc1 {self.lab(f'S{j}')}")
-        if not fall:                               # slot j's BUY entry, inline
-            e(f"s_cmp_le_u32 {BA}, {LI}")
-            e(f"s_cbranch_scc1 {self.lab(f'BXE{j}')}")
-            if copy:
-                self.rest("B", (f"s{BUF[j][0]}", f"s{BUF[j][1]}"))
-                self.dispatch((j + 1) % NS, False, False)
-            else:
-                e(f"s_branch {self.lab(f'BR{j}')}")
-
-    def rest(self, side: str, T):
-        """The 32-bit rest, then the ring entry := {E, T} (E = R_k before: the level's word of the
-        R pair shifted down) and R_k += T, both from lane LI >> 1: no lane read on the path."""
-        e = self.e
-        buy = side == "B"
-        top, topd = (BB, BBD) if buy else (BA, BAD)
-        ge, gt = ("ge", "gt") if buy else ("le", "lt")
-        e(f"s_cmp_{ge}_u32 {LI}, {top}")
-        self.csel(X, T, 0)
-        self.csel(A, 0, T)
-        e(f"s_cmp_{gt}_u32 {LI}, {top}")
-        self.csel(A, topd, A)
-        e(f"s_cselect_b32 {L}, {top}, {LI}")
-        self.csel(topd, 0, topd)
-        e(f"s_{'max' if buy else 'min'}_u32 {top}, {top}, {LI}")
-        self.add(topd, topd, X)
-        self.add_lane("B" if buy else "A")
-        ev, od = CREG["R"]
-        self.entry_addr(T[1])
-        e(f"s_lshr_b32 {T0}, {LI}, 1")
-        e(f"s_bfm_b64 exec, 1, {T0}")
-        e(f"s_lshl_b32 {T0}, {LI}, 5")
-        e(f"v_lshrrev_b64 v[{VE}:{VM}], {T0}, v[{ev}:{od}]")   # v40 = E (the level's word)
-        e(f"v_mov_b32 v{VM}, {T[0]}")
-        e(f"v_mov_b32 v{VA}, {X3}")
-        e(f"ds_write_b64 v{VA}, v[{VE}:{VM}]")                # {E, T}
-        e(f"s_mov_b32 s90, {T[0]}")                      # (s91 = 0)
-        e(f"s_lshl_b64 s[92:93], s[90:91], {T0}")
-        e(f"v_lshl_add_u64 v[{ev}:{od}], s[92:93], 0, v[{ev}:{od}]")   # R_k += T
-        e(f"s_or_b32 {K}, {JJS}, {LI}")
-        e(f"s_bitset1_b32 {K}, 7")
-        self.log(K, T, False)
-
-    def push_addr(self, first: str):
-        """v{VW} = byte address of ring slot pbase | ((first - lane) & mask) (X2 = mask, X1 =
-        pbase): lane l pushes to the rank `first` - l."""
-        e = self.e
-        e(f"v_sub_u32 v{VW}, {first}, v{VL}")
-        e(f"v_and_b32 v{VW}, {X2}, v{VW}")
-        e(f"v_or_b32 v{VW}, {X1}, v{VW}")
-        e(f"v_lshlrev_b32 v{VW}, 3, v{VW}")
+        e(f"v_writelane_b32 %[lk], {K}, m0")
+        e(f"v_writelane_b32 %[la], {r}, m0")
+        e("s_addc_u32 m0, m0, 0")
 
     def del_path(self, i: int):
-        """DeleteOrder (engine.go:87-116) on the aggregates of level LI: r = clamp(E_m + Xb_m +
-        v_m - G_k, 0, v_m).  The target's entry already holds E_m + Xb_m (every earlier DEL of a
-        target behind m pushed its v there), so the path is one LDS read — by every lane, which
-        then holds v_m for this DEL's own push: v_m added to the entries of the wp ranks ahead of
-        m (ranks p - 1, p - 2, ..: 63 lanes at a time, the rest out of line; fire and forget).
-        G_k = R_k - depth_k comes from lane LI >> 1 while the read is in flight."""
+        """DeleteOrder (engine.go:87-116) of a maker of side sd at level LI: r = clamp(depth - Q,
+        0, v), depth -= r.  A level behind the cached top: the depth word of lane LI >> 1 in VALU
+        (no branch on r; a word that reaches 0 leaves the side set by itself); the cached top:
+        SALU, and the next level of the side is promoted when it empties (ZREM)."""
         e = self.e
         lo, hi = f"s{BUF[i][0]}", f"s{BUF[i][1]}"
         lab = self.lab
-        ev, od = CREG["R"]
-        aev, aod = PAIR["A"]
-        bev, bod = PAIR["B"]
+        j = (i + 1) % NS
+        X1, XV, SH = "s94", "s95", "s96"
         e(f"{lab(f'D{i}')}:")
-        self.entry_addr(hi)                                   # X3 = the entry's byte address
-        e("s_mov_b64 exec, -1")
-        e(f"v_mov_b32 v{VA}, {X3}")
-        e(f"ds_read_b64 v[{VE}:{VM}], v{VA}")                 # {E_m + Xb_m, v_m} in every lane
-        e(f"s_and_b32 {X0}, {lo}, 0xffff")                    # wp
-        e(f"s_lshr_b32 {X1}, {lo}, 16")
-        e(f"s_bfm_b32 {X2}, {X1}, 0")                         # mask = C_k - 1
-        e(f"s_lshr_b32 {T0}, {X3}, 3")                        # p
-        e(f"s_andn2_b32 {X1}, {T0}, {X2}")                    # pbase
-        e(f"s_sub_u32 {K}, {T0}, 1")                          # first rank pushed to: p - 1
-        self.push_addr(K)
-        # G_k = R_k - depth_k: the level's words of the R / ask / bid pairs (a cached top's lane
-        # is 0, its depth is in SGPRs)
-        e(f"v_sub_u32 v{VG0}, v{ev}, v{aev}")
-        e(f"v_sub_u32 v{VG0}, v{VG0}, v{bev}")
-        e(f"v_sub_u32 v{VG1}, v{od}, v{aod}")
-        e(f"v_sub_u32 v{VG1}, v{VG1}, v{bod}")
-        e(f"s_bitcmp1_b32 {LI}, 0")
-        e("s_cselect_b64 vcc, -1, 0")
-        e(f"v_cndmask_b32 v{VG0}, v{VG0}, v{VG1}, vcc")
-        e(f"s_cmp_eq_u32 {LI}, {BA}")
-        e(f"s_cselect_b32 s94, {BAD[0]}, 0")
-        e(f"s_cmp_eq_u32 {LI}, {BB}")
-        e(f"s_cselect_b32 s95, {BBD[0]}, 0")
-        e(f"s_add_u32 s94, s94, s95")
-        e(f"v_subrev_u32 v{VG0}, s94, v{VG0}")                # G_k
-        e(f"s_min_u32 {L}, {X0}, 63")
-        e("s_waitcnt lgkmcnt(0)")
-        e(f"s_bfm_b64 exec, {L}, 0")
-        e(f"ds_add_u32 v{VW}, v{VM}")                         # push v_m (E fields, offset 0)
-        win, back = lab(f"DW{i}"), lab(f"DWB{i}")
-        e(f"s_cmp_gt_u32 {X0}, 63")
-        e(f"s_cbranch_scc1 {win}")
-        e(f"{back}:")
-        e(f"s_lshr_b32 {T0}, {LI}, 1")
-        e(f"s_bfm_b64 exec, 1, {T0}")
-        # a = E_m + Xb_m + v_m (< 2^31); r = a - G_k clamped to [0, v_m]
-        e(f"v_add_u32 v{VE}, v{VE}, v{VM}")
-        e(f"v_sub_co_u32 v{VE}, vcc, v{VE}, v{VG0}")
-        e(f"v_cndmask_b32 v{VE}, v{VE}, v{VZ0}, vcc")
-        e(f"v_min_u32 v{VE}, v{VE}, v{VM}")
-        e(f"v_readlane_b32 {X1}, v{VE}, {T0}")                # r
-        e(f"s_cmp_eq_u32 {X1}, 0")
-        e(f"s_cbranch_scc1 {lab(f'DZ{i}')}")                  # not found: no event (:96-98)
-        e(f"s_or_b32 {K}, {JJS}, {LI}")
-        e(f"s_bitset1_b32 {K}, 31")
-        e(f"s_mov_b32 s90, {X1}")
-        self.log(K, ("s90", "s91"), False)
-        e(f"s_bitcmp1_b32 {hi}, 29")
+        e(f"s_bfe_u32 {XV}, {hi}, 0x160007")                   # v
+        e(f"s_and_b32 {K}, {hi}, 0xc000007f")
+        e(f"s_or_b32 {K}, {K}, {JJS}")                          # the cancel touch key
+        e(f"s_bitcmp1_b32 {hi}, 31")
         e(f"s_cbranch_scc1 {lab(f'DA{i}')}")
         for sd in ("B", "A"):
             if sd == "A":
                 e(f"{lab(f'DA{i}')}:")
             top, topd = (BB, BBD) if sd == "B" else (BA, BAD)
-            pev, pod = PAIR[sd]
+            ev, od = PAIR[sd]
             e(f"s_cmp_eq_u32 {LI}, {top}")
             e(f"s_cbranch_scc1 {lab(f'DT{sd}{i}')}")
-            # a level behind the cached top: lane word k -= r (64-bit add of -r << 32 * (k & 1))
             e(f"s_lshr_b32 {T0}, {LI}, 1")
-            e(f"s_bfm_b64 exec, 1, {T0}")
-            e(f"s_lshl_b32 {T0}, {LI}, 5")
-            e(f"s_sub_u32 s94, 0, {X1}")
-            e("s_mov_b32 s95, -1")
-            e(f"s_lshl_b64 s[92:93], s[94:95], {T0}")
-            e(f"v_lshl_add_u64 v[{pev}:{pod}], s[92:93], 0, v[{pev}:{pod}]")
-            self.dispatch((i + 1) % NS, False)
-            # the cached top: its depth drops; emptied -> the next level of the side (ZREM)
+            e(f"s_bfm_b64 {M}, 1, {T0}")
+            e(f"s_lshl_b32 {SH}, {LI}, 5")                      # (LI & 1) << 5 in the low 6 bits
+            e(f"s_mov_b64 exec, {M}")
+            e(f"v_lshrrev_b64 v[{VE}:{VE + 1}], {SH}, v[{ev}:{od}]")  # v40 = the level's depth word
+            e(f"v_subrev_u32 v{VE}, {lo}, v{VE}")
+            e(f"v_max_i32 v{VE}, 0, v{VE}")                     # (depth, Q < 2^31)
+            e(f"v_min_u32 v{VE}, {XV}, v{VE}")                  # r
+            e(f"v_readlane_b32 {X1}, v{VE}, {T0}")
+            e(f"s_bitcmp1_b32 {LI}, 0")
+            e(f"s_cselect_b64 exec, {M}, 0")
+            e(f"v_sub_u32 v{od}, v{od}, v{VE}")
+            e(f"s_cselect_b64 exec, 0, {M}")
+            e(f"v_sub_u32 v{ev}, v{ev}, v{VE}")
+            e(f"s_cmp_lg_u32 {X1}, 0")
+            self.del_log(X1)
+            self.dispatch(j, False)
+            # the cached top
             e(f"{lab(f'DT{sd}{i}')}:")
+            e(f"s_sub_u32 {X1}, {topd[0]}, {lo}")              # SCC = borrow
+            e(f"s_cselect_b32 {X1}, 0, {X1}")
+            e(f"s_min_u32 {X1}, {X1}, {XV}")                    # r
             e(f"s_sub_u32 {topd[0]}, {topd[0]}, {X1}")
-            e(f"s_cmp_eq_u32 {topd[0]}, 0")
-            e(f"s_cbranch_scc0 {lab(f'DZ{i}')}")
+            e(f"s_cmp_lg_u32 {X1}, 0")
+            self.del_log(X1)
+            e(f"s_cmp_lg_u32 {topd[0]}, 0")
+            e(f"s_cbranch_scc1 {lab(f'DN{i}')}")
             self.next_top(sd)
-            self.dispatch((i + 1) % NS, False)
-        e(f"{lab(f'DZ{i}')}:")
-        self.dispatch((i + 1) % NS, False)
-        # pushes beyond 63 ranks (out of line): 63 lanes at a time
-        blk = [f"{win}:"]
-        self.slow.append(blk)
-        sv = self.out
-        self.out = blk
-        e("s_mov_b32 s92, 63")
-        loop = lab(f"DWL{i}")
-        e(f"{loop}:")
-        e(f"s_sub_u32 {L}, {X0}, s92")
-        e(f"s_min_u32 {L}, {L}, 63")
-        e(f"s_sub_u32 {T0}, {K}, s92")
-        e("s_mov_b64 exec, -1")
-        self.push_addr(T0)
-        e(f"s_bfm_b64 exec, {L}, 0")
-        e(f"ds_add_u32 v{VW}, v{VM}")
-        e("s_add_u32 s92, s92, 63")
-        e(f"s_cmp_lt_u32 s92, {X0}")
-        e(f"s_cbranch_scc1 {loop}")
-        e(f"s_branch {back}")
-        self.out = sv
+            self.dispatch(j, False)
 
     def slot(self, i: int):
-        e = self.e
-        lo, hi = f"s{BUF[i][0]}", f"s{BUF[i][1]}"
-        T = (lo, hi)
-        j = (i + 1) % NS
-        lab = self.lab
-        e(f"{lab(f'B{i}')}:")
-        e(f"s_cmp_le_u32 {BA}, {LI}")
-        e(f"s_cbranch_scc1 {lab(f'BXE{i}')}")
-        e(f"{lab(f'BR{i}')}:")
-        self.rest("B", T)
-        self.dispatch(j, False)
-        e(f"{lab(f'BXE{i}')}:")
-        self.cross_entry(T)
-        self.sub(D, T, BAD)
-        e(f"s_cbranch_scc0 {lab(f'BF{i}')}")
-        self.partial("B", T)
-        self.dispatch(j, False)
-        e(f"{lab(f'BF{i}')}:")
-        self.full("B", T, i)
-        e(f"{lab(f'SXE{i}')}:")
-        self.cross_entry(T)
-        self.sub(D, T, BBD)
-        e(f"s_cbranch_scc0 {lab(f'SF{i}')}")
-        self.partial("S", T)
-        self.dispatch(j, False)
-        e(f"{lab(f'SF{i}')}:")
-        self.full("S", T, i)
-        e(f"{lab(f'DN{i}')}:")
-        self.dispatch(j, False)
+        """Gen.slot (W32), the DEL paths placed before the SALE entry."""
+        sv = self.out
+        self.out = []
+        super().slot(i)
+        body = self.out
+        self.out = sv
+        k = body.index(f"{self.lab(f'S{i}')}:")
+        self.out.extend(body[:k])
         self.del_path(i)
-        e(f"{lab(f'S{i}')}:")
-        e(f"s_cmp_ge_u32 {BB}, {LI}")
-        e(f"s_cbranch_scc1 {lab(f'SXE{i}')}")
-        e(f"{lab(f'SR{i}')}:")
-        self.rest("S", T)
-        self.dispatch(j, j != 0)
-
-    def build(self) -> list[str]:
-        e = self.e
-        e("s_mov_b64 exec, -1")
-        e(f"v_mbcnt_lo_u32_b32 v{VL}, -1, 0")
-        e(f"v_mbcnt_hi_u32_b32 v{VL}, -1, v{VL}")
-        e(f"v_mov_b32 v{VZ0}, 0")
-        ev, od = CREG["R"]
-        e(f"v_mov_b32 v{ev}, %[rl0]")
-        e(f"v_mov_b32 v{od}, %[rl1]")
-        return super().build()
+        self.out.extend(body[k:])
 
 
 # ---- W32D: the 32-bit plan of a deep book (more levels than lanes, DESIGN.md §4.3) -----------

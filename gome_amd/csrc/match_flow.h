@@ -72,10 +72,11 @@ constexpr uint32_t FL_MAX_ORDERS = (1u << 23) - 8;  // order index (padding incl
 constexpr unsigned long long OR_NOP = 0ull;
 
 enum : uint32_t { TK_CONS = 0, TK_REST = 1, TK_CANC = 2 };
-// kind of a logged touch key (W32C cancel touches carry bit 31; W32 rest keys carry the SALE
-// bit there, so the flag is only read for books with DELs)
+// kind of a logged touch key (W32C cancel touches carry bit 30: the order index of a book with
+// DELs is below 2^22; bit 31 is the SALE bit of W32 rest keys and of cancel keys)
+constexpr uint32_t FC_MAX_ORDERS = (1u << 22) - 8;  // order index (padding included) of a W32C book
 __device__ __forceinline__ uint32_t tk_kind(uint32_t kr, bool cancel_book) {
-  return (cancel_book && (kr >> 31)) ? TK_CANC : ((kr >> 7) & 1u);
+  return (cancel_book && ((kr >> 30) & 1u)) ? TK_CANC : ((kr >> 7) & 1u);
 }
 
 struct Touch {       // one level visited by one order (16 B)
@@ -84,6 +85,9 @@ struct Touch {       // one level visited by one order (16 B)
   int64_t amt;       // volume taken from the level (CONS) or rested at it (REST)
 };
 __device__ __forceinline__ uint32_t tk_j(const Touch& x) { return (x.kr >> 8) & 0x7FFFFFu; }  // bit 31: W32 records' side
+// the order index of a touch of a book with DELs (bit 30: cancel)
+__device__ __forceinline__ uint32_t tk_jc(const Touch& x) { return (x.kr >> 8) & 0x3FFFFFu; }
+__device__ __forceinline__ uint32_t tk_jb(const Touch& x, bool cancel_book) { return cancel_book ? tk_jc(x) : tk_j(x); }
 static_assert(sizeof(Touch) == 16, "Touch layout");
 
 struct SEnt {        // a touch in its level's run (32 B)
@@ -127,7 +131,8 @@ struct FlowHdr {
   uint32_t fc_bad;     // set by the cancel prep: decline the book (legacy / cold kernels)
   uint32_t deep;       // the lane prep found more levels than FL_MAX: a deep-book candidate
   uint32_t dslot;      // its deep slot (head: = h; tail: handed out by k_flow_prep)
-  uint32_t pad3[2];
+  uint32_t nbsum;      // books with DELs: the DEL windows' total (the cancel prep's C loops)
+  uint32_t pad3;
 };
 // FlowHdr::ok: 0 declined, FL_OK_ADD an ADD-only flow book, FL_OK_CANCEL a book with DELs,
 // FL_OK_DEEP an ADD-only head book with more levels than the lane plans hold (match_flow_deep.h)
@@ -215,8 +220,9 @@ struct FlowArgs {
   FcDel* fc_del;       // [max_batch] per segment position: the DEL's target
   uint32_t* fc_tg;     // [max_batch] per segment position: ADD targeted by the DEL at (value - 1)
   uint32_t* fc_rank;   // [max_batch] per segment position: a targeted ADD's rank in its level
-  uint32_t* fc_dt;     // [max_batch] per book, per level, per target rank: its DEL's segment
-                       // position, then the prefix max of those (the push windows' search array)
+  uint32_t* fc_dt;     // [max_batch] per book, per level, per target rank: its DEL's segment position
+  uint32_t* fc_tv;     // [max_batch] same index: the target's volume (plan units) | SALE << 31
+  uint32_t* tvol;      // head prep: [FL_HEAD][maxt][2 * FL_CAP] per-tile ADD volume per (level, side)
   FcHash* fc_hash;     // (symbol, oid) table of the cancel books' records
   uint64_t fc_hmask;
   // deep books (match_flow_deep.h), per deep slot: level tables, final level records, price
@@ -1067,9 +1073,6 @@ __device__ __forceinline__ void fl_plan_book(const Dev& D, const FlowArgs& F, ui
   const int64_t a0 = (m0 & M_SALE) ? d0 : 0, a1 = (m1 & M_SALE) ? d1 : (lane == 63 ? 1 : 0);
   const int64_t b0 = (m0 & M_BUY) ? d0 : (lane == 0 ? 1 : 0), b1 = (m1 & M_BUY) ? d1 : 0;
   FlDepth Da{lo32(a0), hi32(a0), lo32(a1), hi32(a1)}, Db{lo32(b0), hi32(b0), lo32(b1), hi32(b1)};
-  // books with DELs: R_k (volume that ever arrived, arrival coordinates from the old FIFO head)
-  // starts at the level's live volume
-  FlDepth Rv{lo32(d0), 0u, lo32(d1), 0u};
   if (w32) {  // the 32-bit plan's layout: lane j holds levels 2j (l0) and 2j + 1 (l1)
     const uint32_t se = (2u * lane) & 63u, so = (2u * lane + 1u) & 63u;
     const bool hiset = lane >= 32;
@@ -1079,7 +1082,6 @@ __device__ __forceinline__ void fl_plan_book(const Dev& D, const FlowArgs& F, ui
     };
     Da = FlDepth{pick(Da.l0, Da.l1, se), 0u, pick(Da.l0, Da.l1, so), 0u};
     Db = FlDepth{pick(Db.l0, Db.l1, se), 0u, pick(Db.l0, Db.l1, so), 0u};
-    Rv = FlDepth{pick(Rv.l0, Rv.l1, se), 0u, pick(Rv.l0, Rv.l1, so), 0u};
   }
 
   FlLog lg{vreg(0u), vreg(0u), vreg(0u), 0u, 0u, 0u, FL_TOUCH_MUL * n, (GOME_GLB v4u*)(F.log + FL_TOUCH_MUL * beg)};
@@ -1108,7 +1110,7 @@ __device__ __forceinline__ void fl_plan_book(const Dev& D, const FlowArgs& F, ui
         [lb] "+v"(lg.lb), [nacc] "+s"(lg.nacc), [lpos] "+s"(lg.lpos), [voff] "=&v"(voff), [vt] "=&v"(vt),
         [vpf] "=&v"(vpf)
       : [ob] "s"(ob), [nh] "s"(nh), [logp] "s"(logp), [lcap] "s"(lg.lcap), [vl16] "v"(vl16),
-        [vzero] "v"(vzero), [rl0] "v"(Rv.l0), [rl1] "v"(Rv.l1)
+        [vzero] "v"(vzero)
       : FL_PLAN_CLOBBERS, FL_PLAN_CLOBBERS_C, "scc", "vcc", "memory");
   } else if (w32) {
     asm volatile(FL_PLAN_ASM32 FL_PLAN_OPERANDS);
@@ -1266,7 +1268,7 @@ __global__ __launch_bounds__(FL_SORT_T) void k_flow_sort(Dev D, FlowArgs F) {
     __syncthreads();
     if (valid) {
       SEnt e;
-      e.j = tk_j(x);
+      e.j = tk_jb(x, cb);
       e.kind = tk_kind(x.kr, cb);
       e.amt = x.amt;
       e.coord = 0;
@@ -2081,7 +2083,7 @@ __global__ __launch_bounds__(FL_TILE) void k_flow_sort_scatter(Dev D, FlowArgs F
     __syncthreads();
     if (valid) {
       SEnt e;
-      e.j = tk_j(x);
+      e.j = tk_jb(x, cb);
       e.kind = tk_kind(x.kr, cb);
       e.amt = static_cast<int64_t>(static_cast<unsigned long long>(x.amt) * g);
       e.coord = 0;

@@ -62,10 +62,11 @@ struct FcDel {
   uint32_t rank;     // the target's rank among the level's targets (arrival order)
   uint32_t nb;       // window: targets that arrived behind the target before this DEL
   uint32_t ixs;      // FC_OLD: the node's cancel-index slot
-  uint32_t oend, ov; // FC_OLD: arrival end / volume (plan units)
+  uint32_t oend, ov; // the target's arrival end / volume (plan units; FC_NEW: counted over the
+                     // segment's ADDs only)
   int64_t r;         // recon: volume cancelled (fixed point), 0 if the DEL found nothing
   uint32_t ct;       // recon: touch index of the cancel, NIL if none
-  uint32_t wp;       // push window: ranks rank - wp .. rank - 1 may still be pending
+  uint32_t va;       // volume of the segment's side-s ADDs at the level before the DEL
 };
 static_assert(sizeof(FcDel) == 48, "FcDel layout");
 enum : uint32_t { FC_NONE = 0, FC_NEW = 1, FC_OLD = 2 };
@@ -137,6 +138,7 @@ __global__ __launch_bounds__(256) void k_fc_hash_claim(Dev D, BatchArgs B, FlowA
   fc_slice(hd, blockIdx.x, gridDim.x, b0, b1);
   const bool claim = hd.sym < FC_MAXKEY_SYM;
   if (!claim && threadIdx.x == 0) fc_decline(F, h, FC_BAD_SYM);
+  if (hd.end - hd.beg + 8 > FC_MAX_ORDERS && blockIdx.x == 0 && threadIdx.x == 0) fc_decline(F, h, FC_BAD_RING);
   for (uint32_t b = b0 + threadIdx.x; b < b1; b += blockDim.x) {
     F.fc_tg[b] = 0;
     F.fc_rank[b] = NIL;
@@ -311,15 +313,20 @@ __global__ __launch_bounds__(1024) void k_fc_oldwalk_book(Dev D, FlowArgs F) {
   for (uint32_t q = 1 + (threadIdx.x >> 6); q <= F.hdr[h].nl; q += blockDim.x / 64) fc_oldwalk_level(D, F, h, uni(q));
 }
 
-// ---- push windows ----------------------------------------------------------------------------
-// The plan adds a cancelled target's volume v to the ring entries of the targets *ahead* of it
-// that are still pending (their DEL comes later), so each target's entry holds E + Xb by the time
-// its own DEL reads it: Xb needs no window read.  Ranks are dense per level (one DEL per target),
-// so with DT[r] = the segment position of rank r's DEL and PM its prefix maximum, the oldest
-// target still pending at a DEL at position b is the smallest r with PM[r] >= b, and the DEL
-// pushes to ranks r .. rank - 1 (wp of them; the ones between that are already cancelled do not
-// read their entries again).  Every pending target arrived within the ring window of its own
-// DEL, so ring capacities sized for the windows hold these ranks too.
+// ---- the DEL records' Q -----------------------------------------------------------------------
+// A DEL of maker m (level k, side s) at segment position b removes r = clamp(depth_s,k - Q, 0,
+// v_m) (gen_plan_asm.py, W32C; v_m = m's volume), where Q = the volume of the side-s makers that
+// arrived at level k after m and before b and were not cancelled before b
+// (tools/flow_cancel_model.py, plan_book_q, checks this against the oracle):
+//   Q = VA(b) - END(m) - C,   VA(x) = volume of the segment's admitted side-s ADDs at level k
+//                              before position x (the old makers: END(m) = oend - D0 for an old m,
+//                              i.e. the old volume behind m counts);
+//                              END(m) = VA(m) + v_m for a new m;
+//                              C = volume of the level's side-s targets ranked behind m (arrived
+//                              after it) whose DEL comes before b: they were untouched while m
+//                              was live, so each removed exactly its v.
+// Those targets are among the nb that arrived behind m before b (the DEL's window), so C is a
+// loop over ranks rank+1 .. rank+nb of the level's DEL times (DT) and volumes (TV).
 
 // Per level: its targets' count and their first entry of the book's DEL-time array (an exclusive
 // scan over the book's levels; `tot` = 0 for threads that are not levels).  Every thread of the
@@ -339,81 +346,142 @@ __device__ __forceinline__ void fc_time_bases(FlowLvl* LV, uint32_t k, uint32_t 
   __syncthreads();
 }
 
-// In place: DT -> PM over each level's ranks (one wave per (book, level)).
-__device__ __forceinline__ void fc_time_pmax(uint32_t* dt, uint32_t n) {
-  uint32_t carry = 0;
-  for (uint32_t r0 = 0; r0 < n; r0 += 64) {
-    const uint32_t r = r0 + lane_id();
-    const uint32_t m = max(wave_incl_max_u32(r < n ? dt[r] : 0u), carry);
-    if (r < n) dt[r] = m;
-    carry = rl(m, 63);
-  }
+constexpr uint32_t FC_KEYS = 2 * FL_CAP;     // (level, side) keys of the volume sums: level | SALE << 7
+constexpr uint32_t FC_NB_MAX = 0xFFFFu;     // a longer DEL window declines the book (FC_BAD_RING)
+constexpr uint32_t FC_MAX_V = 1u << 22;     // a target's volume (plan units) fits 22 bits of its DEL record
+// so does a segment whose windows add up past FC_NBSUM_MUL per record (+ FC_NBSUM_ADD): the
+// records' C loops stay a small multiple of the segment
+constexpr uint32_t FC_NBSUM_MUL = 256, FC_NBSUM_ADD = 1u << 24;
+
+// Record i of book h (segment position b = beg + i): an admitted ADD's (level, side) key and
+// volume (plan units), from its W32 record; NIL key for anything else.
+__device__ __forceinline__ uint32_t fc_add_key(const FlowArgs& F, const FlowHdr& hd, uint32_t i, uint32_t& v) {
+  const unsigned long long r = F.ord8[hd.obase + i];
+  const uint32_t hi = static_cast<uint32_t>(r >> 32), k = hi & 127u;
+  v = static_cast<uint32_t>(r);
+  return k ? (k | ((hi >> 31) << 7)) : NIL;
 }
 
-// wp of a DEL at segment position b whose target has rank rk (pm[rk] >= b: its own DEL): back
-// from rk in doubling steps to a rank whose PM is below b, then a binary search in between.
-__device__ __forceinline__ uint32_t fc_push_window(const uint32_t* pm, uint32_t rk, uint32_t b) {
-  int32_t hi = static_cast<int32_t>(rk), lo = -1;
-  for (int32_t step = 1; step <= hi; step <<= 1) {
-    if (pm[hi - step] < b) {
-      lo = hi - step;
-      break;
+// Volume of the lanes of this wave before this one whose ADD key equals `q` (akey: this lane's
+// ADD key or NIL).
+__device__ __forceinline__ uint32_t fc_wave_vol_before(uint32_t akey, uint32_t v, uint32_t q) {
+  const uint32_t lane = lane_id();
+  uint32_t s = 0;
+  for (uint32_t l = 0; l < 63; ++l) {
+    const uint32_t kl = __shfl(akey, l), vl = __shfl(v, l);
+    if (l < lane && kl == q) s += vl;
+  }
+  return s;
+}
+
+// The tile's per-wave ADD volumes per key -> exclusive offsets from base[key] (LDS wv[FL_TILE_W]
+// [FC_KEYS], every thread of a FL_TILE block calls it); base[key] advances by the tile's total
+// when `advance`.
+__device__ __forceinline__ void fc_tile_vol(uint32_t (*wv)[FC_KEYS], uint32_t* base, uint32_t akey, uint32_t v,
+                                            bool advance) {
+  const uint32_t tid = threadIdx.x, w = tid >> 6;
+  for (uint32_t x = tid; x < FL_TILE_W * FC_KEYS; x += blockDim.x) wv[x / FC_KEYS][x % FC_KEYS] = 0;
+  __syncthreads();
+  if (akey != NIL) atomicAdd(&wv[w][akey], v);
+  __syncthreads();
+  for (uint32_t key = tid; key < FC_KEYS; key += blockDim.x) {
+    uint32_t r = base[key];
+    for (uint32_t ww = 0; ww < FL_TILE_W; ++ww) {
+      const uint32_t c = wv[ww][key];
+      wv[ww][key] = r;
+      r += c;
     }
-    hi -= step;
+    if (advance) base[key] = r;
   }
-  while (hi - lo > 1) {
-    const int32_t mid = lo + (hi - lo) / 2;
-    if (pm[mid] >= b) hi = mid;
-    else lo = mid;
-  }
-  return rk - static_cast<uint32_t>(hi);
+  __syncthreads();
 }
 
-__global__ __launch_bounds__(64) void k_fc_pmax(Dev D, FlowArgs F) {
-  const uint32_t h = F.h0 + blockIdx.y, q = blockIdx.x;
-  if (h >= fl_hend(D, F) || !fc_book(F, h) || q == 0 || q > F.hdr[h].nl) return;
-  const FlowLvl& L = F.lvl[h * FL_CAP + q];
-  fc_time_pmax(F.fc_dt + F.hdr[h].beg + L.tbase, L.ttot);
+// A targeted ADD's arrival end (VA + v) and volume go to its DEL's record; a DEL gets VA.
+__device__ __forceinline__ void fc_put_va(const FlowArgs& F, uint32_t b, bool tgt_add, bool del, uint32_t va,
+                                          uint32_t v) {
+  if (tgt_add) {
+    FcDel* d = &F.fc_del[F.fc_tg[b] - 1u];
+    d->oend = va + v;
+    d->ov = v;
+  }
+  if (del) F.fc_del[b].va = va;
 }
 
-// ---- prep 5: ranks, windows, ring layout, image and W32C records (one block per book) -------
-constexpr uint32_t FC_PASS_T = 1024, FC_PASS_W = FC_PASS_T / 64;
+// Q of the DEL at b (see above) and its W32C record.
+__device__ __forceinline__ unsigned long long fc_del_rec(const FlowArgs& F, const FlowHdr& hd, const FlowLvl* LV,
+                                                         uint32_t b, const FcDel& d, bool sale) {
+  const uint32_t k = d.li;
+  const uint32_t* dt = F.fc_dt + hd.beg + LV[k].tbase;
+  const uint32_t* tv = F.fc_tv + hd.beg + LV[k].tbase;
+  uint32_t c = 0;
+  for (uint32_t x = d.rank + 1; x <= d.rank + d.nb; ++x) {
+    const uint32_t t = tv[x];
+    if ((t >> 31) == (sale ? 1u : 0u) && dt[x] < b) c += t & 0x7FFFFFFFu;
+  }
+  const uint32_t d0 = static_cast<uint32_t>(static_cast<unsigned long long>(LV[k].d0) / hd.g);
+  const uint32_t q = (d.kind == FC_OLD ? d0 - d.oend : 0u - d.oend) + d.va - c;
+  const uint32_t hi = k | (d.ov << 7) | (1u << 30) | (sale ? 0x80000000u : 0u);
+  return (static_cast<unsigned long long>(hi) << 32) | q;
+}
+
+// A DEL's window and its target's DEL time / volume by rank (both prep paths).
+__device__ __forceinline__ uint32_t fc_window(const FlowArgs& F, const FlowHdr& hd, const FlowLvl* LV, uint32_t b,
+                                              const FcDel& d, uint32_t rk, uint32_t arrived, bool sale) {
+  const uint32_t nb = arrived - rk - 1u;
+  F.fc_del[b].rank = rk;
+  F.fc_del[b].nb = nb;
+  const uint32_t x = hd.beg + LV[d.li].tbase + rk;
+  F.fc_dt[x] = b;
+  F.fc_tv[x] = d.ov | (sale ? 0x80000000u : 0u);
+  return nb;
+}
+
+// ---- prep 5: ranks, windows, Q and the W32C DEL records (one block per book) ----------------
+constexpr uint32_t FC_PASS_T = FL_TILE, FC_PASS_W = FC_PASS_T / 64;
 
 __global__ __launch_bounds__(FC_PASS_T) void k_fc_pass(Dev D, BatchArgs B, FlowArgs F) {
-  __shared__ uint32_t cnt[FL_CAP], cmax[FL_CAP], wc[FC_PASS_W][FL_CAP], cring[FL_CAP], rbase[FL_CAP];
-  __shared__ uint32_t nslot_s, bad_s;
+  __shared__ uint32_t cnt[FL_CAP], wc[FC_PASS_W][FL_CAP], cvol[FC_KEYS], wv[FC_PASS_W][FC_KEYS];
+  __shared__ uint32_t bad_s, mw_s, sum_s;
   const uint32_t h = F.h0 + blockIdx.x, tid = threadIdx.x, w = tid >> 6;
   if (h >= fl_hend(D, F) || !fc_book(F, h)) return;
   const FlowHdr hd = F.hdr[h];
   FlowLvl* LV = F.lvl + h * FL_CAP;
-  const uint32_t n = hd.end - hd.beg, nl = hd.nl;
-  if (tid < FL_CAP) {
-    cnt[tid] = 0;
-    cmax[tid] = (tid >= 1 && tid <= nl) ? max(LV[tid].c_old, 1u) : 1u;
-  }
-  if (tid == 0) bad_s = 0;
+  const uint32_t n = hd.end - hd.beg;
+  if (tid < FL_CAP) cnt[tid] = 0;
+  for (uint32_t x = tid; x < FC_KEYS; x += FC_PASS_T) cvol[x] = 0;
+  if (tid == 0) { bad_s = 0; mw_s = 0; sum_s = 0; }
   for (uint32_t x = tid; x < FC_PASS_W * FL_CAP; x += FC_PASS_T) wc[x / FL_CAP][x % FL_CAP] = 0;
   __syncthreads();
   const unsigned long long ltm = lt_mask();
   // in segment order, tile by tile: a targeted ADD's rank = old targets of its level + targeted
   // ADDs before it; a DEL's window = targets of the level that arrived before it - its target's
-  // rank - 1 (stable per-level counting across the waves of a tile)
+  // rank - 1 (stable per-level counting across the waves of a tile); the (level, side) ADD
+  // volumes before each targeted ADD and DEL
   for (uint32_t t0 = 0; t0 < n; t0 += FC_PASS_T) {
     const uint32_t i = t0 + tid;
     const uint32_t b = hd.beg + i;
-    bool isa = false, isd = false;
-    uint32_t k = 0;
+    bool isa = false, isd = false, sale = false;
+    uint32_t k = 0, v = 0, akey = NIL, qkey = NIL;
     FcDel d{};
     if (i < n) {
-      const uint32_t tg = F.fc_tg[b];
-      if (tg) {
+      akey = fc_add_key(F, hd, i, v);
+      if (F.fc_tg[b]) {
         isa = true;
-        k = static_cast<uint32_t>(F.ord8[hd.obase + i] >> 32) & 127u;
-      } else if (prep_at(B, b).action == GOME_DEL) {
+        k = akey & 127u;
+        qkey = akey;
+      } else if (akey == NIL && prep_at(B, b).action == GOME_DEL) {
         d = F.fc_del[b];
-        if (d.kind != FC_NONE) { isd = true; k = d.li; }
+        if (d.kind != FC_NONE) {
+          isd = true;
+          k = d.li;
+          sale = prep_at(B, b).side == GOME_SALE;
+          qkey = k | (sale ? 128u : 0u);
+        }
       }
     }
+    fc_tile_vol(wv, cvol, akey, v, true);
+    const uint32_t pre = fc_wave_vol_before(akey, v, qkey);
+    if (isa || isd) fc_put_va(F, b, isa, isd, wv[w][qkey] + pre, v);
     unsigned long long same = __ballot(isa);
 #pragma unroll
     for (uint32_t bit = 0; bit < 7; ++bit) {
@@ -438,115 +506,55 @@ __global__ __launch_bounds__(FC_PASS_T) void k_fc_pass(Dev D, BatchArgs B, FlowA
     const uint32_t before = (isa || isd) ? wc[w][k] + before_w : 0u;
     if (isa) F.fc_rank[b] = LV[k].c_old + before;
     __syncthreads();  // (a DEL may target an ADD of the same tile)
-    if (isd) {
+    if (isd) {  // (arrived before it, kept in nb until the level bases are known)
       const uint32_t rk = d.kind == FC_NEW ? F.fc_rank[d.tgt] : d.rank;
-      const uint32_t arrived = LV[k].c_old + before;
-      const uint32_t nb = arrived - rk - 1u;
       F.fc_del[b].rank = rk;
-      F.fc_del[b].nb = nb;
-      atomicMax(&cmax[k], nb + 1u);
-      if (nb >= 0xFFFFu) atomicOr(&bad_s, FC_BAD_RING);
+      F.fc_del[b].nb = LV[k].c_old + before;
     }
     for (uint32_t x = tid; x < FC_PASS_W * FL_CAP; x += FC_PASS_T) wc[x / FL_CAP][x % FL_CAP] = 0;
     __syncthreads();
   }
-  // push windows: per level the targets' DEL times, then their prefix maxima
-  fc_time_bases(LV, tid, (tid >= 1 && tid <= nl) ? LV[tid].c_old + cnt[tid] : 0u);
+  // per level the targets' DEL times and volumes by rank
+  fc_time_bases(LV, tid, (tid >= 1 && tid <= hd.nl) ? LV[tid].c_old + cnt[tid] : 0u);
+  uint32_t nbsum = 0;
   for (uint32_t i = tid; i < n; i += FC_PASS_T) {
     const uint32_t b = hd.beg + i;
     if (prep_at(B, b).action != GOME_DEL) continue;
     const FcDel d = F.fc_del[b];
-    if (d.kind != FC_NONE) F.fc_dt[hd.beg + LV[d.li].tbase + d.rank] = b;
+    if (d.kind == FC_NONE) continue;
+    const uint32_t nb = fc_window(F, hd, LV, b, d, d.rank, d.nb, prep_at(B, b).side == GOME_SALE);
+    nbsum += nb;
+    atomicMax(&mw_s, nb + 1u);
+    if (nb >= FC_NB_MAX) atomicOr(&bad_s, FC_BAD_RING);
+    if (d.ov >= FC_MAX_V) atomicOr(&bad_s, FC_BAD_UNIT);
   }
+  if (nbsum) atomicAdd(&sum_s, nbsum);
   __syncthreads();
-  for (uint32_t q = 1 + w; q <= nl; q += FC_PASS_W) fc_time_pmax(F.fc_dt + hd.beg + LV[q].tbase, LV[q].ttot);
-  __syncthreads();
-  // ring layout: power-of-two capacities, placed largest first (each base aligned to its size)
   if (tid == 0) {
-    const uint32_t cap = F.fc_ring_cap;
-    uint32_t off = 0, top = 1;
-    for (uint32_t q = 1; q <= nl; ++q) {
-      uint32_t c = 1;
-      while (c < cmax[q] && c <= cap) c <<= 1;
-      cring[q] = c;
-      off += c;
-      top = max(top, c);
-    }
-    if (off + 1 > cap) {
-      bad_s |= FC_BAD_RING;  // (+ the dummy entry of untargeted ADDs and no-op records)
-    } else {
-      off = 0;
-      for (uint32_t c = top; c; c >>= 1)
-        for (uint32_t q = 1; q <= nl; ++q)
-          if (cring[q] == c) {
-            rbase[q] = off;
-            off += c;
-          }
-    }
-    nslot_s = off + 1;
-    if (!bad_s) {  // the book's image
-      const uint32_t base = atomicAdd(F.fc_img_bump, nslot_s);
-      if (static_cast<unsigned long long>(base) + nslot_s > F.fc_img_cap) {
-        bad_s |= FC_BAD_RING;
-      } else {
-        F.hdr[h].fc_img = base;
-        F.hdr[h].fc_big = nslot_s > FC_TAIL_SLOTS ? 1u : 0u;
-      }
-    }
-    uint32_t mw = 0;
-    for (uint32_t q = 1; q <= nl; ++q) mw = max(mw, cmax[q]);
-    F.hdr[h].ncancel = mw;
-    F.hdr[h].nslot = nslot_s;  // (also when declined: diagnostics)
+    F.hdr[h].ncancel = mw_s;
+    F.hdr[h].nbsum = sum_s;
+    if (sum_s > FC_NBSUM_MUL * n + FC_NBSUM_ADD) bad_s |= FC_BAD_RING;
   }
   __syncthreads();
   if (bad_s) {
     if (tid == 0) fc_decline(F, h, bad_s);
     return;
   }
-  const uint32_t nslot = nslot_s, dummy = nslot - 1;
-  if (tid >= 1 && tid <= nl) {
-    LV[tid].cring = cring[tid];
-    LV[tid].rbase = rbase[tid];
-  }
-  uint2* img = F.fc_img + F.hdr[h].fc_img;
-  for (uint32_t x = tid; x < nslot; x += FC_PASS_T) img[x] = make_uint2(0u, 0u);
-  __syncthreads();
-  const uint32_t npad = (8u - (n & 7u)) & 7u;
-  for (uint32_t i = tid; i < n + npad; i += FC_PASS_T) {
+  for (uint32_t i = tid; i < n; i += FC_PASS_T) {
     const uint32_t b = hd.beg + i;
-    unsigned long long rec = static_cast<unsigned long long>(dummy << 7) << 32;  // no-op
-    if (i < n) {
-      const unsigned long long w32 = F.ord8[hd.obase + i];
-      const uint32_t hi = static_cast<uint32_t>(w32 >> 32), k = hi & 127u;
-      const uint32_t tg = F.fc_tg[b];
-      if (k) {  // an admitted ADD (32-bit record: level, volume in units of g, SALE bit 31)
-        const uint32_t slot = tg ? rbase[k] + (F.fc_rank[b] & (cring[k] - 1u)) : dummy;
-        rec = (static_cast<unsigned long long>(k | (slot << 7) | (hi & 0x80000000u)) << 32) |
-              static_cast<uint32_t>(w32);
-      } else if (prep_at(B, b).action == GOME_DEL) {
-        const FcDel d = F.fc_del[b];
-        if (d.kind != FC_NONE) {
-          const uint32_t kk = d.li, slot = rbase[kk] + (d.rank & (cring[kk] - 1u));
-          const bool sale = prep_at(B, b).side == GOME_SALE;
-          const uint32_t lgc = 31u - __clz(cring[kk]);
-          const uint32_t wp = fc_push_window(F.fc_dt + hd.beg + LV[kk].tbase, d.rank, b);
-          rec = (static_cast<unsigned long long>(kk | (slot << 7) | (sale ? 1u << 29 : 0u) | (3u << 30)) << 32) |
-                (wp | (lgc << 16));
-          if (d.kind == FC_OLD) img[slot] = make_uint2(d.oend - d.ov, d.ov);  // {E, v}, not cancelled
-        }
-      }
-    }
-    F.ord8[hd.obase + i] = rec;
+    if (prep_at(B, b).action != GOME_DEL) continue;
+    const FcDel d = F.fc_del[b];
+    if (d.kind != FC_NONE) F.ord8[hd.obase + i] = fc_del_rec(F, hd, LV, b, d, prep_at(B, b).side == GOME_SALE);
   }
-  if (tid == 0) F.hdr[h].nslot = nslot;
 }
 
 // ---- prep 5, tile-parallel (the head books, whose segments hold up to ~10^6 records) --------
 // The same quantities as k_fc_pass, computed as a stable counting pass over 1024-record tiles:
-// per tile the targeted ADDs of each level (F.tcnt, free before the plan), an exclusive scan over
-// the tiles from each level's old targets, then every targeted ADD's rank and every DEL's count
-// of targets that arrived before it; the windows (which need the ranks of targets in other
-// tiles), the ring layout and image, and the W32C records follow as separate launches.
+// per tile the targeted ADDs of each level and the ADD volume of each (level, side) key (F.tcnt
+// / F.tvol, free before the plan), exclusive scans over the tiles, then every targeted ADD's rank
+// and every DEL's count of targets that arrived before it with the volumes before both; the
+// windows (which need the ranks of targets in other tiles) and the DEL records follow as
+// separate launches.
 __device__ __forceinline__ bool fc_targeted_add(const FlowArgs& F, const FlowHdr& hd, uint32_t i, uint32_t& k) {
   if (!F.fc_tg[hd.beg + i]) return false;
   k = static_cast<uint32_t>(F.ord8[hd.obase + i] >> 32) & 127u;
@@ -554,17 +562,20 @@ __device__ __forceinline__ bool fc_targeted_add(const FlowArgs& F, const FlowHdr
 }
 
 __global__ __launch_bounds__(FL_TILE) void k_fc_pcnt(Dev D, BatchArgs B, FlowArgs F) {
-  __shared__ uint32_t wc[FL_TILE_W][FL_CAP];
+  __shared__ uint32_t wc[FL_TILE_W][FL_CAP], tv[FC_KEYS];
   const uint32_t h = F.h0 + blockIdx.y, tid = threadIdx.x, w = tid >> 6;
   if (h >= fl_hend(D, F) || !fc_book(F, h)) return;
   const FlowHdr hd = F.hdr[h];
   const uint32_t n = hd.end - hd.beg, ntile = (n + FL_TILE - 1) / FL_TILE;
   for (uint32_t tl = blockIdx.x; tl < ntile; tl += gridDim.x) {
     for (uint32_t i = tid; i < FL_TILE_W * FL_CAP; i += FL_TILE) wc[i / FL_CAP][i % FL_CAP] = 0;
+    for (uint32_t i = tid; i < FC_KEYS; i += FL_TILE) tv[i] = 0;
     __syncthreads();
     const uint32_t i = tl * FL_TILE + tid;
-    uint32_t k = 0, cnt;
+    uint32_t k = 0, cnt, v = 0, akey = NIL;
     const bool isa = i < n && fc_targeted_add(F, hd, i, k);
+    if (i < n) akey = fc_add_key(F, hd, i, v);
+    if (akey != NIL) atomicAdd(&tv[akey], v);
     const uint32_t rank = fl_tile_rank(k, isa, cnt);
     if (isa && rank == 0) wc[w][k] = cnt;
     __syncthreads();
@@ -573,12 +584,14 @@ __global__ __launch_bounds__(FL_TILE) void k_fc_pcnt(Dev D, BatchArgs B, FlowArg
       for (uint32_t ww = 0; ww < FL_TILE_W; ++ww) c += wc[ww][tid];
       F.tcnt[(static_cast<size_t>(h) * F.maxt + tl) * FL_CAP + tid] = c;
     }
+    for (uint32_t key = tid; key < FC_KEYS; key += FL_TILE)
+      F.tvol[(static_cast<size_t>(h) * F.maxt + tl) * FC_KEYS + key] = tv[key];
     __syncthreads();
   }
 }
 
-// Per book: tile offsets per level from its old targets (in place); the level's largest window
-// + 1 starts at max(old targets, 1) in FlowLvl::cring (the layout kernel rounds it up).
+// Per book: tile offsets per level from its old targets, per key from 0 (in place); the level
+// bases of the DEL-time arrays.
 __global__ __launch_bounds__(FL_CAP) void k_fc_pscan(Dev D, FlowArgs F) {
   const uint32_t h = F.h0 + blockIdx.x, k = threadIdx.x;
   if (h >= fl_hend(D, F) || !fc_book(F, h)) return;
@@ -587,37 +600,55 @@ __global__ __launch_bounds__(FL_CAP) void k_fc_pscan(Dev D, FlowArgs F) {
   const uint32_t ntile = (hd.end - hd.beg + FL_TILE - 1) / FL_TILE;
   const bool lv = k >= 1 && k <= hd.nl;
   uint32_t run = lv ? LV[k].c_old : 0u;
-  if (lv) LV[k].cring = max(run, 1u);
   uint32_t* tc = F.tcnt + static_cast<size_t>(h) * F.maxt * FL_CAP;
+  uint32_t* tvv = F.tvol + static_cast<size_t>(h) * F.maxt * FC_KEYS;
+  uint32_t rb = 0, rs = 0;
   for (uint32_t tl = 0; tl < ntile; ++tl) {
     const uint32_t v = tc[tl * FL_CAP + k];
     tc[tl * FL_CAP + k] = run;
     run += v;
+    const uint32_t vb = tvv[tl * FC_KEYS + k], vs = tvv[tl * FC_KEYS + FL_CAP + k];
+    tvv[tl * FC_KEYS + k] = rb;
+    tvv[tl * FC_KEYS + FL_CAP + k] = rs;
+    rb += vb;
+    rs += vs;
   }
   fc_time_bases(LV, k, lv ? run : 0u);
 }
 
-// Targeted ADDs' ranks; a DEL's count of its level's targets that arrived before it (in nb).
+// Targeted ADDs' ranks; a DEL's count of its level's targets that arrived before it (in nb); the
+// (level, side) volumes before both.
 __global__ __launch_bounds__(FL_TILE) void k_fc_prank(Dev D, BatchArgs B, FlowArgs F) {
-  __shared__ uint32_t wc[FL_TILE_W][FL_CAP];
+  __shared__ uint32_t wc[FL_TILE_W][FL_CAP], wv[FL_TILE_W][FC_KEYS], vb[FC_KEYS];
   const uint32_t h = F.h0 + blockIdx.y, tid = threadIdx.x, w = tid >> 6;
   if (h >= fl_hend(D, F) || !fc_book(F, h)) return;
   const FlowHdr hd = F.hdr[h];
   const uint32_t n = hd.end - hd.beg, ntile = (n + FL_TILE - 1) / FL_TILE;
   const uint32_t* tc = F.tcnt + static_cast<size_t>(h) * F.maxt * FL_CAP;
+  const uint32_t* tvv = F.tvol + static_cast<size_t>(h) * F.maxt * FC_KEYS;
   for (uint32_t tl = blockIdx.x; tl < ntile; tl += gridDim.x) {
     for (uint32_t i = tid; i < FL_TILE_W * FL_CAP; i += FL_TILE) wc[i / FL_CAP][i % FL_CAP] = 0;
+    for (uint32_t i = tid; i < FC_KEYS; i += FL_TILE) vb[i] = tvv[tl * FC_KEYS + i];
     __syncthreads();
     const uint32_t i = tl * FL_TILE + tid, b = hd.beg + i;
-    uint32_t k = 0;
+    uint32_t k = 0, v = 0, akey = NIL, qkey = NIL;
     bool isa = false, isd = false;
     if (i < n) {
+      akey = fc_add_key(F, hd, i, v);
       isa = fc_targeted_add(F, hd, i, k);
-      if (!isa && prep_at(B, b).action == GOME_DEL) {
+      if (isa) qkey = akey;
+      if (!isa && akey == NIL && prep_at(B, b).action == GOME_DEL) {
         const FcDel d = F.fc_del[b];
-        if (d.kind != FC_NONE) { isd = true; k = d.li; }
+        if (d.kind != FC_NONE) {
+          isd = true;
+          k = d.li;
+          qkey = k | (prep_at(B, b).side == GOME_SALE ? 128u : 0u);
+        }
       }
     }
+    fc_tile_vol(wv, vb, akey, v, false);
+    const uint32_t pre = fc_wave_vol_before(akey, v, qkey);
+    if (isa || isd) fc_put_va(F, b, isa, isd, wv[w][qkey] + pre, v);
     // ballot of the wave's targeted ADDs at this lane's level (DEL lanes take part in the
     // level bits only)
     unsigned long long same = __ballot(isa);
@@ -644,118 +675,54 @@ __global__ __launch_bounds__(FL_TILE) void k_fc_prank(Dev D, BatchArgs B, FlowAr
   }
 }
 
-// Windows: nb = arrived - rank of the target - 1, the level's largest window + 1.
+// Windows: nb = arrived - rank of the target - 1; DEL times and volumes by rank.
 __global__ __launch_bounds__(256) void k_fc_pwin(Dev D, BatchArgs B, FlowArgs F) {
+  __shared__ uint32_t sum_s, mw_s;
   const uint32_t h = F.h0 + blockIdx.y;
   if (h >= fl_hend(D, F) || !fc_book(F, h)) return;
   const FlowHdr hd = F.hdr[h];
   FlowLvl* LV = F.lvl + h * FL_CAP;
-  uint32_t b0, b1, bad = 0;
+  if (threadIdx.x == 0) { sum_s = 0; mw_s = 0; }
+  __syncthreads();
+  uint32_t b0, b1, bad = 0, nbsum = 0;
   fc_slice(hd, blockIdx.x, gridDim.x, b0, b1);
   for (uint32_t b = b0 + threadIdx.x; b < b1; b += blockDim.x) {
     if (prep_at(B, b).action != GOME_DEL) continue;
     const FcDel d = F.fc_del[b];
     if (d.kind == FC_NONE) continue;
     const uint32_t rk = d.kind == FC_NEW ? F.fc_rank[d.tgt] : d.rank;
-    const uint32_t nb = d.nb - rk - 1u;
-    F.fc_del[b].rank = rk;
-    F.fc_del[b].nb = nb;
-    F.fc_dt[hd.beg + LV[d.li].tbase + rk] = b;
-    atomicMax(&LV[d.li].cring, nb + 1u);
-    if (nb >= 0xFFFFu) bad = FC_BAD_RING;
+    const uint32_t nb = fc_window(F, hd, LV, b, d, rk, d.nb, prep_at(B, b).side == GOME_SALE);
+    nbsum += nb;
+    atomicMax(&mw_s, nb + 1u);
+    if (nb >= FC_NB_MAX) bad |= FC_BAD_RING;
+    if (d.ov >= FC_MAX_V) bad |= FC_BAD_UNIT;
+  }
+  if (nbsum) atomicAdd(&sum_s, nbsum);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (sum_s) atomicAdd(&F.hdr[h].nbsum, sum_s);
+    if (mw_s) atomicMax(&F.hdr[h].ncancel, mw_s);
   }
   if (bad) fc_decline(F, h, bad);
 }
 
-// Per book: ring layout (power-of-two capacities, largest first), the image (bump-allocated,
-// zeroed); declines a book whose ring does not fit.
-__global__ __launch_bounds__(1024) void k_fc_playout(Dev D, FlowArgs F) {
-  __shared__ uint32_t nslot_s, bad_s;
-  const uint32_t h = F.h0 + blockIdx.x, tid = threadIdx.x;
-  if (h >= fl_hend(D, F) || !fc_book(F, h)) return;
-  FlowLvl* LV = F.lvl + h * FL_CAP;
-  const uint32_t nl = F.hdr[h].nl;
-  if (tid == 0) {
-    const uint32_t cap = F.fc_ring_cap;
-    uint32_t off = 0, top = 1, mw = 0, bad = 0;
-    for (uint32_t q = 1; q <= nl; ++q) {
-      const uint32_t cm = LV[q].cring;
-      mw = max(mw, cm);
-      uint32_t c = 1;
-      while (c < cm && c <= cap) c <<= 1;
-      LV[q].cring = c;
-      off += c;
-      top = max(top, c);
-    }
-    if (off + 1 > cap) {
-      bad = FC_BAD_RING;  // (+ the dummy entry of untargeted ADDs and no-op records)
-    } else {
-      off = 0;
-      for (uint32_t c = top; c; c >>= 1)
-        for (uint32_t q = 1; q <= nl; ++q)
-          if (LV[q].cring == c) {
-            LV[q].rbase = off;
-            off += c;
-          }
-    }
-    const uint32_t ns = off + 1;
-    if (!bad) {
-      const uint32_t base = atomicAdd(F.fc_img_bump, ns);
-      if (static_cast<unsigned long long>(base) + ns > F.fc_img_cap) {
-        bad = FC_BAD_RING;
-      } else {
-        F.hdr[h].fc_img = base;
-        F.hdr[h].fc_big = ns > FC_TAIL_SLOTS ? 1u : 0u;
-      }
-    }
-    F.hdr[h].ncancel = mw;
-    F.hdr[h].nslot = ns;
-    if (bad) fc_decline(F, h, bad);
-    nslot_s = ns;
-    bad_s = bad;
-  }
-  __syncthreads();
-  if (bad_s) return;
-  uint2* img = F.fc_img + F.hdr[h].fc_img;
-  for (uint32_t x = tid; x < nslot_s; x += blockDim.x) img[x] = make_uint2(0u, 0u);
-}
-
-// The W32C records (and the old targets' image entries), tile-parallel.
+// The W32C DEL records (Q), tile-parallel; a book whose windows sum past the budget is declined.
 __global__ __launch_bounds__(256) void k_fc_precs(Dev D, BatchArgs B, FlowArgs F) {
   const uint32_t h = F.h0 + blockIdx.y;
   if (h >= fl_hend(D, F) || !fc_book(F, h)) return;
   const FlowHdr hd = F.hdr[h];
+  const uint32_t n = hd.end - hd.beg;
+  if (hd.nbsum > FC_NBSUM_MUL * n + FC_NBSUM_ADD) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) fc_decline(F, h, FC_BAD_RING);
+    return;
+  }
   const FlowLvl* LV = F.lvl + h * FL_CAP;
-  const uint32_t n = hd.end - hd.beg, npad = (8u - (n & 7u)) & 7u, dummy = hd.nslot - 1;
-  uint2* img = F.fc_img + hd.fc_img;
-  const uint32_t tot = n + npad;
-  const uint32_t i0 = static_cast<uint32_t>(static_cast<uint64_t>(tot) * blockIdx.x / gridDim.x);
-  const uint32_t i1 = static_cast<uint32_t>(static_cast<uint64_t>(tot) * (blockIdx.x + 1) / gridDim.x);
-  for (uint32_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
-    const uint32_t b = hd.beg + i;
-    unsigned long long rec = static_cast<unsigned long long>(dummy << 7) << 32;  // no-op
-    if (i < n) {
-      const unsigned long long w32 = F.ord8[hd.obase + i];
-      const uint32_t hi = static_cast<uint32_t>(w32 >> 32), k = hi & 127u;
-      const uint32_t tg = F.fc_tg[b];
-      if (k) {  // an admitted ADD (32-bit record: level, volume in units of g, SALE bit 31)
-        const uint32_t slot = tg ? LV[k].rbase + (F.fc_rank[b] & (LV[k].cring - 1u)) : dummy;
-        rec = (static_cast<unsigned long long>(k | (slot << 7) | (hi & 0x80000000u)) << 32) |
-              static_cast<uint32_t>(w32);
-      } else if (prep_at(B, b).action == GOME_DEL) {
-        const FcDel d = F.fc_del[b];
-        if (d.kind != FC_NONE) {
-          const uint32_t kk = d.li, cr = LV[kk].cring, slot = LV[kk].rbase + (d.rank & (cr - 1u));
-          const bool sale = prep_at(B, b).side == GOME_SALE;
-          const uint32_t lgc = 31u - __clz(cr);
-          const uint32_t wp = fc_push_window(F.fc_dt + hd.beg + LV[kk].tbase, d.rank, b);
-          rec = (static_cast<unsigned long long>(kk | (slot << 7) | (sale ? 1u << 29 : 0u) | (3u << 30)) << 32) |
-                (wp | (lgc << 16));
-          if (d.kind == FC_OLD) img[slot] = make_uint2(d.oend - d.ov, d.ov);  // {E, v}, not cancelled
-        }
-      }
-    }
-    F.ord8[hd.obase + i] = rec;
+  uint32_t b0, b1;
+  fc_slice(hd, blockIdx.x, gridDim.x, b0, b1);
+  for (uint32_t b = b0 + threadIdx.x; b < b1; b += blockDim.x) {
+    if (prep_at(B, b).action != GOME_DEL) continue;
+    const FcDel d = F.fc_del[b];
+    if (d.kind != FC_NONE) F.ord8[hd.obase + (b - hd.beg)] = fc_del_rec(F, hd, LV, b, d, prep_at(B, b).side == GOME_SALE);
   }
 }
 
@@ -1071,11 +1038,11 @@ __global__ void k_fc_count(Dev D, BatchArgs B, FlowArgs F) {
     const uint32_t hb = fl_book_of_wave(F, nb, gt - lane_id(), gt), h = F.h0 + hb, t = gt - F.toff[F.tb + hb];
     const uint32_t nt = F.hdr[h].ntouch, beg = F.hdr[h].beg, L = FL_TOUCH_MUL * beg;
     const Touch x = F.log[L + t];
-    if (t > 0 && tk_j(F.log[L + t - 1]) == tk_j(x)) continue;
+    if (t > 0 && tk_jc(F.log[L + t - 1]) == tk_jc(x)) continue;
     uint32_t acc = 0;
     for (uint32_t u = t; u < nt; ++u) {
       const Touch y = (u == t) ? x : F.log[L + u];
-      if (tk_j(y) != tk_j(x)) break;
+      if (tk_jc(y) != tk_jc(x)) break;
       F.fbase[L + u] = acc;
       const uint32_t kind = tk_kind(y.kr, true);
       if (kind == TK_CONS) {
@@ -1089,7 +1056,7 @@ __global__ void k_fc_count(Dev D, BatchArgs B, FlowArgs F) {
         cancels += 1;
       }
     }
-    if (tk_j(x) < F.hdr[h].end - beg) B.ev_count[prep_at(B, beg + tk_j(x)).idx] = acc;  // not padding
+    if (tk_jc(x) < F.hdr[h].end - beg) B.ev_count[prep_at(B, beg + tk_jc(x)).idx] = acc;  // not padding
   }
   for (int off = 32; off > 0; off >>= 1) {
     fills += __shfl_xor(fills, off);
@@ -1159,10 +1126,10 @@ __global__ __launch_bounds__(256) void k_fc_events(Dev D, BatchArgs B, FlowArgs 
     if (base == NIL || !cnt) continue;
     gome_event* dst = B.arena + base + wb + (inc - cnt);
     const uint32_t beg = F.hdr[h].beg, sym = F.hdr[h].sym;
-    const Prep tk = prep_at(B, beg + tk_j(x));
+    const Prep tk = prep_at(B, beg + tk_jc(x));
     const int64_t price = F.lvl[h * FL_CAP + (x.kr & 127u)].price;
     if (kind == TK_CANC) {  // DeleteOrder's MatchResult (engine.go:109-113)
-      const FcDel d = F.fc_del[beg + tk_j(x)];
+      const FcDel d = F.fc_del[beg + tk_jc(x)];
       gome_event ev;
       ev.price_fx = tk.price;
       ev.match_volume_fx = 0;
@@ -1192,7 +1159,7 @@ __global__ __launch_bounds__(256) void k_fc_events(Dev D, BatchArgs B, FlowArgs 
     int64_t tb = tk.vol;
     for (uint32_t u = t; u > 0; --u) {
       const Touch y = F.log[L + u - 1];
-      if (tk_j(y) != tk_j(x)) break;
+      if (tk_jc(y) != tk_jc(x)) break;
       tb -= y.amt;
     }
     const FcLvlView& V = T.V;

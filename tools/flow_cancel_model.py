@@ -130,7 +130,111 @@ def plan_book(old_fifo, seg):
     return r_of, depth, side, sum(1 << int(np.ceil(np.log2(c))) for c in C.values())
 
 
-def check(n_sym=50, batch=20000, nbatch=4, seed=1, del_frac=0.5, aggr=0.1, zipf=1.0):
+def plan_book_q(old_fifo, seg):
+    """The W32C plan as built (gen_plan_asm.py, match_flow_cancel.h): per level and side only the
+    depth; a DEL of maker m (level p, side s) at index i carries
+        Q = VA_s,p(i) - END(m) - C,   VA = volume of the segment's side-s ADDs at p before i,
+        END(m) = VA(m) + v_m (new m) or oend - D0 (old m: the old volume behind it counts),
+        C = volume of side-s targets ranked behind m whose DEL comes before i,
+    removes r = clamp(depth_s,p - Q, 0, v_m) (v_m: the target's full volume).  While m is live the
+    makers behind it are untouched (Q of them) and, if m was partly consumed, nothing is live
+    ahead of it; once m is gone the side's depth is at most Q.  Returns (r per DEL index, final
+    depth per price, final side per price).""" 
+    old_of = {}
+    for p, fifo in old_fifo.items():
+        for pos, (oid, side, rem) in enumerate(fifo):
+            old_of[oid] = (p, pos, side, rem)
+    add_at, tgt = {}, {}
+    for i, r in enumerate(seg):
+        oid = int(r["oid_id"])
+        if r["action"] == 1:
+            add_at[oid] = i
+        elif r["action"] == 2:
+            if oid in add_at and int(seg[add_at[oid]]["price_fx"]) == int(r["price_fx"]):
+                if all(d[1] != add_at[oid] for d in tgt.values() if d[0] == "new"):
+                    tgt[i] = ("new", add_at[oid])
+            elif oid in old_of and old_of[oid][0] == int(r["price_fx"]) and oid not in add_at:
+                if ("old", oid) not in tgt.values():
+                    tgt[i] = ("old", oid)
+    lvl_t = defaultdict(list)
+    for d, (kind, x) in tgt.items():
+        if kind == "old":
+            lvl_t[old_of[x][0]].append(((0, old_of[x][1]), (kind, x), d))
+        else:
+            lvl_t[int(seg[x]["price_fx"])].append(((1, x), (kind, x), d))
+    rank, tv, dt = {}, {}, {}
+    for p, lst in lvl_t.items():
+        lst.sort()
+        for k, (_, t, d) in enumerate(lst):
+            rank[t] = k
+            dt[(p, k)] = d
+            if t[0] == "old":
+                tv[(p, k)] = (old_of[t[1]][2], old_of[t[1]][3])
+            else:
+                tv[(p, k)] = (int(seg[t[1]]["side"]), int(seg[t[1]]["volume_fx"]))
+    d0 = {p: sum(x[2] for x in f) for p, f in old_fifo.items()}
+    oend = {}
+    for p, f in old_fifo.items():
+        e = 0
+        for oid, sd, rem in f:
+            e += rem
+            oend[oid] = e
+    # prep: Q per DEL
+    Q = {}
+    for i, t in tgt.items():
+        r = seg[i]
+        p, s = int(r["price_fx"]), int(r["side"])
+        va = sum(int(x["volume_fx"]) for x in seg[:i] if x["action"] == 1 and int(x["price_fx"]) == p and int(x["side"]) == s)
+        if t[0] == "new":
+            m = t[1]
+            end = sum(int(x["volume_fx"]) for x in seg[:m] if x["action"] == 1 and int(x["price_fx"]) == p
+                      and int(x["side"]) == s) + int(seg[m]["volume_fx"])
+        else:
+            end = oend[t[1]] - d0[p]
+        k = rank[t]
+        c = sum(v for (pp, kk), (sd, v) in tv.items() if pp == p and kk > k and sd == s and dt[(pp, kk)] < i)
+        Q[i] = (va - end - c, tv[(p, k)][1])
+    # the plan over side depths
+    dep = defaultdict(int)   # (price, side) -> depth
+    for p, fifo in old_fifo.items():
+        if fifo:
+            dep[(p, fifo[0][1])] = sum(x[2] for x in fifo)
+    r_of = {}
+    for i, r in enumerate(seg):
+        a, p, v, sd = int(r["action"]), int(r["price_fx"]), int(r["volume_fx"]), int(r["side"])
+        if a == 1:
+            T = v
+            opp = sorted((q for (q, s2), d in dep.items() if d > 0 and s2 == 1 - sd and (q >= p if sd == 1 else q <= p)),
+                         reverse=(sd == 1))
+            crossed = False
+            for q in opp:
+                crossed = True
+                take = min(T, dep[(q, 1 - sd)])
+                dep[(q, 1 - sd)] -= take
+                T -= take
+                if T <= 0:
+                    break
+            if crossed and T <= 0:
+                continue
+            dep[(p, sd)] += T
+        elif a == 2 and i in tgt:
+            d = dep[(p, sd)]
+            q, vm = Q[i]
+            rr = min(max(d - q, 0), vm)
+            dep[(p, sd)] = d - rr
+            r_of[i] = rr
+    depth, side = defaultdict(int), {}
+    for (p, s2), d in dep.items():
+        if d > 0:
+            depth[p] += d
+            side[p] = s2
+        else:
+            depth.setdefault(p, 0)
+    return r_of, depth, side, 0
+
+
+def check(n_sym=50, batch=20000, nbatch=4, seed=1, del_frac=0.5, aggr=0.1, zipf=1.0, plan=None):
+    plan = plan or plan_book
     g = wl.NativeStream(n_sym, zipf, seed=seed, del_frac=del_frac, aggressive_frac=aggr)
     orc = Oracle(n_sym)
     worst = 0
@@ -143,7 +247,7 @@ def check(n_sym=50, batch=20000, nbatch=4, seed=1, del_frac=0.5, aggr=0.1, zipf=
                 if len(f):
                     old[int(lv["price_fx"])] = [(int(x["oid_id"]), int(x["side"]), int(x["volume_fx"])) for x in f]
             seg = b[b["symbol_id"] == s]
-            r_of, depth, side, ringsum = plan_book(old, seg)
+            r_of, depth, side, ringsum = plan(old, seg)
             worst = max(worst, ringsum)
             idx = np.nonzero(b["symbol_id"] == s)[0]
             ev = orc_events_for(orc, b, s) if False else None
@@ -174,6 +278,10 @@ def check(n_sym=50, batch=20000, nbatch=4, seed=1, del_frac=0.5, aggr=0.1, zipf=
 seg_truth = {}
 
 if __name__ == "__main__":
+    for pl in (plan_book_q, plan_book):
+        print(pl.__name__)
+        check(n_sym=20, batch=6000, nbatch=3, plan=pl)
+        check(n_sym=3, batch=8000, nbatch=3, seed=7, plan=pl)
     check()
     check(n_sym=3, batch=30000, nbatch=3, seed=7)
     check(n_sym=200, batch=40000, nbatch=3, seed=3, aggr=0.02)

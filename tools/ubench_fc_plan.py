@@ -24,7 +24,7 @@ def adds(rng, n, oid0):
 
 
 def run(tag, mk):
-    eng = Engine(max_symbols=1, max_batch=N, max_nodes=1 << 22, max_levels=1 << 16)
+    eng = Engine(max_symbols=1, max_batch=N, max_nodes=1 << 22, max_levels=1 << 20)
     rng = np.random.default_rng(5)
     t = []
     for i in range(6):

@@ -269,7 +269,7 @@ class Engine:
         self._check(self.lib.gome_release_device_events(self.h))
 
     FLOW_BOOK_DTYPE = np.dtype([("kind", "<u4"), ("decline", "<u4"), ("symbol_id", "<u4"), ("orders", "<u4"),
-                                ("dels", "<u4"), ("levels", "<u4"), ("w32", "<u4"), ("ring", "<u4"),
+                                ("dels", "<u4"), ("levels", "<u4"), ("w32", "<u4"), ("wsum", "<u4"),
                                 ("window", "<u4"), ("deep", "<u4")])
 
     def debug_flow_books(self, cap: int = 4096) -> np.ndarray:

@@ -200,7 +200,7 @@ struct gome_engine {
   unsigned long long resting = 0, levels = 0;
   unsigned long long idx_tomb = 0, n_rebuilds = 0;  // tombstones (upper bound) since the last rebuild
   uint32_t fc_gen = 0;            // batch generation of the cancel books' (symbol, oid) table
-  uint32_t fc_ring_lds = 0;       // dynamic LDS of the large-ring plans
+  static constexpr uint32_t plan_lds = FL_DEEP_LDS;  // dynamic LDS of the head / deep plans
   unsigned long long fc_hcap = 0;  // its entries
   bool poisoned = false;
   std::string err;
@@ -301,17 +301,14 @@ gome_status gome_engine::init(const gome_config& c) {
                              hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(HOT_LDS_BYTES)));
   HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_match),
                              hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(COLD_LDS_BYTES)));
-  // the head plans hold a cancel book's LDS ring (match_flow_cancel.h)
+  // the head plans (and the deep tail plans) hold a deep book's depth slots in LDS
   {
     int lds = 0;
     HIPCHK(hipDeviceGetAttribute(&lds, hipDeviceAttributeMaxSharedMemoryPerBlock, cfg.device));
-    F.fc_ring_cap = std::min<uint32_t>(FC_MAX_SLOTS, static_cast<uint32_t>(std::max(lds, 0)) / 8);
-    if (F.fc_ring_cap < FC_TAIL_SLOTS) return fail(GOME_E_DEVICE, "device LDS per workgroup below 16 KiB");
-    fc_ring_lds = F.fc_ring_cap * 8;
-    if (fc_ring_lds < FL_DEEP_LDS) return fail(GOME_E_DEVICE, "device LDS per workgroup below 132 KiB");
+    if (lds < static_cast<int>(FL_DEEP_LDS)) return fail(GOME_E_DEVICE, "device LDS per workgroup below 132 KiB");
     for (const void* k : {reinterpret_cast<const void*>(k_flow_plan_head), reinterpret_cast<const void*>(k_flow_plan_near),
-                          reinterpret_cast<const void*>(k_flow_plan_tail_cb), reinterpret_cast<const void*>(k_flow_plan_tail_d)})
-      HIPCHK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(fc_ring_lds)));
+                          reinterpret_cast<const void*>(k_flow_plan_tail_d)})
+      HIPCHK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(plan_lds)));
     HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_deep_prep_b), hipFuncAttributeMaxDynamicSharedMemorySize,
                                static_cast<int>(DEEP_CAP * 8)));
   }
@@ -404,10 +401,7 @@ gome_status gome_engine::init(const gome_config& c) {
   // table (generation-tagged: cleared once per 2048 batches)
   fc_hcap = next_pow2(std::max<unsigned long long>(2ull * nb, 1024));
   F.fc_hmask = fc_hcap - 1;
-  // ring entries of a batch <= 2 * (targets + levels) per book: 2 * max_batch + 256 per candidate
-  F.fc_img_cap = static_cast<uint32_t>(std::min<uint64_t>(2ull * nb + 256ull * MAX_FLOW + FL_HEAD * FC_MAX_SLOTS, 0xF0000000ull));
-  if (!alloc(&F.fc_img, F.fc_img_cap, "flow cancel ring images") || !alloc(&F.fc_img_bump, 1, "flow cancel image bump") ||
-      !alloc(&F.fc_del, nb, "flow cancel records") ||
+  if (!alloc(&F.fc_del, nb, "flow cancel records") ||
       !alloc(&F.fc_tg, nb, "flow cancel targets") || !alloc(&F.fc_rank, nb, "flow cancel ranks") ||
       !alloc(&F.fc_dt, nb, "flow cancel DEL times") || !alloc(&F.fc_tv, nb, "flow cancel target volumes") ||
       !alloc(&F.tvol, static_cast<size_t>(FL_HEAD) * F.maxt * FC_KEYS, "flow head tile volumes") ||
@@ -570,7 +564,6 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   const uint32_t nh_tail = nhot_max > FL_HEAD ? nhot_max - FL_HEAD : 0;
   // the head's prep gathers through the sort permutation (prep_at): it starts right after
   // segmentation, beside k_prep
-  HIPCHK(hipMemsetAsync(F.fc_img_bump, 0, 4, s));  // (both ranges' cancel preps follow)
   // deep books: slots, price sets and prep scratch of both ranges
   HIPCHK(hipMemsetAsync(F.dslot_h, 0xFF, 4ull * F.dslots, s));
   HIPCHK(hipMemsetAsync(F.dslot_n, 0, 4, s));
@@ -612,7 +605,7 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   cancel_prep(FH, nh_head, FL_PG, true, flow_stream);
   HIPCHK(hipEventRecord(prep_h, flow_stream));
   HIPCHK(hipEventRecord(S.evf0, flow_stream));
-  k_flow_plan_head<<<1, 256, fc_ring_lds, flow_stream>>>(D, FH0);
+  k_flow_plan_head<<<1, 256, plan_lds, flow_stream>>>(D, FH0);
   HIPCHK(hipEventRecord(S.evf1, flow_stream));
   // ---- admission markers (k_adm, launched above on the flow stream)
   HIPCHK(hipStreamWaitEvent(s, adm_done, 0));
@@ -687,8 +680,7 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   HIPCHK(hipEventRecord(S.evc1, s));
   if (nh_tail) {  // the tail's plans and reconstruction
     k_flow_plan_tail<<<nh_tail, 64, 0, s>>>(D, FT);
-    k_flow_plan_tail_c<<<nh_tail, 64, FC_TAIL_LDS, s>>>(D, FT);
-    k_flow_plan_tail_cb<<<nh_tail, 64, fc_ring_lds, s>>>(D, FT);
+    k_flow_plan_tail_c<<<nh_tail, 64, 0, s>>>(D, FT);
     // (its blocks walk the tail's deep slots: at most DEEP_GRID_T whole-CU blocks)
     k_flow_plan_tail_d<<<std::min<uint32_t>(nh_tail, DEEP_GRID_T), 256, FL_DEEP_LDS, s>>>(D, FT);
     k_flow_sort<<<nh_tail, FL_SORT_T, 0, s>>>(D, FT);
@@ -709,7 +701,7 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   HIPCHK(hipStreamWaitEvent(hot_stream, fork, 0));
   HIPCHK(hipStreamWaitEvent(hot_stream, prep_h, 0));
   if (nh_near) {
-    k_flow_plan_near<<<nh_near, 256, fc_ring_lds, hot_stream>>>(D, FH1);
+    k_flow_plan_near<<<nh_near, 256, plan_lds, hot_stream>>>(D, FH1);
     head_recon(FH1, nh_near, hot_stream);
     head_recon_c(FH1, FH1c, nh_near, hot_stream);
     k_flow_events_arena<<<1024, 256, 0, hot_stream>>>(D, B, FH1);
@@ -1112,7 +1104,7 @@ gome_status gome_debug_flow_books(gome_engine* e, uint32_t* out, size_t cap, siz
     return e->fail(GOME_E_DEVICE, "gome_debug_flow_books: copy failed");
   for (size_t i = 0; i < n; ++i) {
     const gome::FlowHdr& x = h[i];
-    const uint32_t w[GOME_DEBUG_FLOW_WORDS] = {x.ok, x.fc_bad, x.sym, x.end - x.beg, x.ndel, x.nl, x.w32, x.nslot,
+    const uint32_t w[GOME_DEBUG_FLOW_WORDS] = {x.ok, x.fc_bad, x.sym, x.end - x.beg, x.ndel, x.nl, x.w32, x.nbsum,
                                                x.ncancel, x.deep};
     std::copy(w, w + GOME_DEBUG_FLOW_WORDS, out + i * GOME_DEBUG_FLOW_WORDS);
   }

@@ -122,17 +122,14 @@ struct FlowHdr {
                                         // w32: the 32-bit plan (volumes / depths in units of g)
   unsigned long long amask[2], bmask[2];  // final S:SALE / S:BUY membership of the levels
   unsigned long long g;                   // volume unit of the book's plan (1 for the 64-bit plan)
-  uint32_t fc_img;     // books with DELs: first entry of the book's ring image (fc_img)
-  uint32_t fc_big;     //   its ring needs more than FC_TAIL_SLOTS entries
   // books whose segment holds DELs (ok == FL_OK_CANCEL, match_flow_cancel.h)
   uint32_t ndel;       // DEL records of the segment
-  uint32_t nslot;      // LDS ring entries of the plan (8 B each, the dummy entry included)
   uint32_t ncancel;    // the cancel prep's longest window + 1 (diagnostics)
   uint32_t fc_bad;     // set by the cancel prep: decline the book (legacy / cold kernels)
   uint32_t deep;       // the lane prep found more levels than FL_MAX: a deep-book candidate
   uint32_t dslot;      // its deep slot (head: = h; tail: handed out by k_flow_prep)
   uint32_t nbsum;      // books with DELs: the DEL windows' total (the cancel prep's C loops)
-  uint32_t pad3;
+  uint32_t pad3[4];
 };
 // FlowHdr::ok: 0 declined, FL_OK_ADD an ADD-only flow book, FL_OK_CANCEL a book with DELs,
 // FL_OK_DEEP an ADD-only head book with more levels than the lane plans hold (match_flow_deep.h)
@@ -177,15 +174,6 @@ struct FlowLvl {
 };
 static_assert(sizeof(FlowLvl) % 16 == 0, "FlowLvl alignment");
 
-// The cancel plan's LDS ring (match_flow_cancel.h): 8-B entries {E, v | cancelled << 31} per
-// targeted maker (+ one dummy entry), an image per book built by the cancel prep
-// (bump-allocated).  A ring of up to FC_TAIL_SLOTS entries plans in a 16-KiB workgroup; a larger
-// one (up to FlowArgs::fc_ring_cap, the device's LDS per workgroup) in a workgroup that owns its
-// CU.  Ring slots are 15-bit fields of the W32C records.
-constexpr uint32_t FC_MAX_SLOTS = 20480;  // 160 KiB: the most LDS a gfx950 workgroup can hold
-constexpr uint32_t FC_TAIL_SLOTS = 2048;
-constexpr uint32_t FC_TAIL_LDS = FC_TAIL_SLOTS * 8;
-static_assert(FC_MAX_SLOTS <= (1u << 15), "ring slots are 15-bit record fields");
 constexpr uint32_t FC_TOFF = MAX_FLOW + 16;  // second toff region for books with DELs
 constexpr uint32_t FC_GEN_MASK = 0x7FF;   // generation bits of an FcHash key
 
@@ -213,10 +201,6 @@ struct FlowArgs {
   // streams), and the range's offset in toff
   uint32_t h0, h1, tb;
   // books with DELs (match_flow_cancel.h)
-  uint2* fc_img;       // LDS ring images (FlowHdr::fc_img), bump-allocated per batch
-  uint32_t* fc_img_bump;
-  uint32_t fc_img_cap; // entries
-  uint32_t fc_ring_cap;  // largest ring (entries): the device's LDS per workgroup / 8
   FcDel* fc_del;       // [max_batch] per segment position: the DEL's target
   uint32_t* fc_tg;     // [max_batch] per segment position: ADD targeted by the DEL at (value - 1)
   uint32_t* fc_rank;   // [max_batch] per segment position: a targeted ADD's rank in its level
@@ -925,7 +909,7 @@ struct FlLog {
 
 #include "flow_plan_asm.inc"
 static_assert(FL_DEEP_CAP == DEEP_CAP, "deep plan generated for another DEEP_CAP");
-static_assert(FL_DEEP_BM == DEEP_CAP * 8 && FL_DEEP_LDS <= FC_MAX_SLOTS * 8, "deep plan LDS layout");
+static_assert(FL_DEEP_BM == DEEP_CAP * 8 && FL_DEEP_LDS <= 160 * 1024, "deep plan LDS layout");
 
 
 
@@ -939,15 +923,7 @@ __device__ unsigned long long g_pstamps[FL_HEAD * 4];
 // EXCL: the block is 4 waves that each hold the whole register file of their SIMD (all 512
 // VGPR+AGPR), so no other wave can share the CU — in particular not its scalar unit, which
 // every instruction of the plan's critical path uses.  Waves 1-3 park at the barrier.
-extern __shared__ uint4 fl_ring[];  // the cancel plan's ring (dynamic LDS)
-
-// Books with DELs: the ring image -> LDS, by every thread of the block.
-__device__ __forceinline__ void fl_ring_load(const FlowArgs& F, uint32_t h) {
-  const uint32_t ns = F.hdr[h].nslot;
-  const uint2* img = F.fc_img + F.hdr[h].fc_img;
-  uint2* ring = reinterpret_cast<uint2*>(fl_ring);
-  for (uint32_t i = threadIdx.x; i < ns; i += blockDim.x) ring[i] = img[i];
-}
+extern __shared__ uint4 fl_ring[];  // the deep plan's depth slots and bitmaps (dynamic LDS)
 
 // Deep books: the depth slots (W32 units; bid of level k at byte 8k, ask at 8k + 4) -> LDS by
 // every thread of the block, with the sentinels; back to FlowLvl (dfin, memf) after the plan.
@@ -995,13 +971,10 @@ __device__ __forceinline__ void fl_deep_store(const FlowArgs& F, uint32_t h) {
   }
 }
 
-// ring: for books with DELs, 0 any ring, 1 small rings only, 2 large rings only
 template <bool EXCL>
-__device__ __forceinline__ void fl_plan_kernel(const Dev& D, const FlowArgs& F, uint32_t kind, uint32_t ring = 0) {
+__device__ __forceinline__ void fl_plan_kernel(const Dev& D, const FlowArgs& F, uint32_t kind) {
   const uint32_t h = F.h0 + blockIdx.x;
-  const bool mine = h < fl_hend(D, F) && uni(F.hdr[h].ok) == kind &&
-                    (ring == 0 || (uni(F.hdr[h].fc_big) != 0) == (ring == 2));
-  if (mine && kind == FL_OK_CANCEL) fl_ring_load(F, h);
+  const bool mine = h < fl_hend(D, F) && uni(F.hdr[h].ok) == kind;
   if (mine && kind == FL_OK_DEEP) fl_deep_load(F, h);
   if (EXCL) {
     asm volatile("" ::: "v255", "a255");
@@ -1011,7 +984,6 @@ __device__ __forceinline__ void fl_plan_kernel(const Dev& D, const FlowArgs& F, 
     if (mine && kind == FL_OK_DEEP) fl_deep_store(F, h);
     return;
   }
-  if (kind == FL_OK_CANCEL) __syncthreads();
   if (mine) fl_plan_book(D, F, h);
 }
 
@@ -1025,10 +997,8 @@ __global__ __launch_bounds__(256) void k_flow_plan_near(Dev D, FlowArgs F) {
   fl_plan_kernel<true>(D, F, uni(F.hdr[F.h0 + blockIdx.x < fl_hend(D, F) ? F.h0 + blockIdx.x : 0].ok));
 }
 __global__ __launch_bounds__(64) void k_flow_plan_tail(Dev D, FlowArgs F) { fl_plan_kernel<false>(D, F, FL_OK_ADD); }
-// tail books with DELs (a launch of its own: 16 KiB of LDS per block)
-__global__ __launch_bounds__(64) void k_flow_plan_tail_c(Dev D, FlowArgs F) { fl_plan_kernel<false>(D, F, FL_OK_CANCEL, 1); }
-// tail books with DELs whose ring exceeds FC_TAIL_SLOTS (the largest LDS allocation)
-__global__ __launch_bounds__(64) void k_flow_plan_tail_cb(Dev D, FlowArgs F) { fl_plan_kernel<false>(D, F, FL_OK_CANCEL, 2); }
+// tail books with DELs
+__global__ __launch_bounds__(64) void k_flow_plan_tail_c(Dev D, FlowArgs F) { fl_plan_kernel<false>(D, F, FL_OK_CANCEL); }
 // deep tail books (depths in LDS: a whole CU each, like the head): each block walks the tail's
 // deep slots (handed out by k_flow_prep) in turn
 __global__ __launch_bounds__(256) void k_flow_plan_tail_d(Dev D, FlowArgs F) {

@@ -3,28 +3,32 @@
 // DeleteOrder (engine.go:87-116) removes a maker's *remaining* volume from its level (depth -=
 // stored remaining, ZREM when the level empties) and unlinks it (nodelink.go:124-166).  What a
 // cancel removes depends on how much of the maker was consumed before it, i.e. on FIFO order,
-// which the aggregate plan (match_flow.h) does not track.  It does not have to: in arrival
-// coordinates of a level (maker m occupies [E_m, E_m + v_m), E = volume that arrived before it)
+// which the aggregate plan (match_flow.h) does not track.  It does not have to.  For a DEL of
+// maker m (level k, side s, volume v_m) let Q be the volume of the side-s makers that arrived at
+// level k after m and before the DEL and were not cancelled before it.  While m is live those
+// makers are untouched (only the FIFO head is ever partly consumed, and a same-side ADD at m's
+// level cannot cross), and if m was partly consumed nothing ahead of it is live; once m is gone
+// (or never rested) every live side-s maker of the level arrived after it.  So
 //
-//     r_m = clamp(E_m + v_m - G_k + Xb_m, 0, v_m),   G_k = R_k - depth_k (volume removed so far)
+//     r_m = clamp(depth_s,k - Q, 0, v_m)
 //
-// where R_k is the volume that ever arrived at the level and Xb_m the volume of the makers
-// *behind* m that were cancelled before: while m is live they were untouched, so each removed
-// exactly its v_j; when m is gone the clamp gives 0 (tools/flow_cancel_model.py checks this
-// against the oracle).  So the plan (gen_plan_asm.py, W32C) keeps R_k beside the depths, and
-// every DEL's target ("targeted maker") owns an entry {E, v | X << 31} of an LDS ring per
-// level; a DEL reads its target's entry, sums v over the cancelled (X) entries of the window of
-// targets that arrived behind it (ranks rank_m + 1 .. rank_m + n_b) and sets its target's X.  Ring capacity C_k (a power
-// of two) exceeds every window, so an entry is reused only after every DEL that reads it.
+// and Q needs nothing from the plan: it is a sum over the segment's records (volumes of the
+// same-side ADDs at the level between m and the DEL, minus the targets among them cancelled
+// before the DEL).  The prep computes it per DEL and writes it into the DEL's W32C record; the
+// plan (gen_plan_asm.py) keeps only the per-side depths.  tools/flow_cancel_model.py
+// (plan_book_q) checks the formula against the oracle.
 //
 // Prep (after the book's ordinary prep, which builds the level set and the 32-bit records):
 //   k_fc_hash_claim / k_fc_hash_count   (symbol, oid) table of the books' ADD / DEL records
 //   k_fc_resolve    each DEL's target: an earlier admitted ADD of the segment (new maker) or a
 //                   resting node (old maker, the cancel index); Q3 (wrong price) and DELs whose
 //                   oid is not resting are no-ops; Q2 (wrong side) and duplicate oids decline
-//   k_fc_oldwalk    old targets' FIFO ranks and arrival coordinates (a walk of their level)
-//   k_fc_pass       in segment order: new targets' ranks, each DEL's window, C_k; the ring
-//                   layout, its LDS image and the W32C records
+//   k_fc_oldwalk    old targets' FIFO ranks, arrival ends and volumes (a walk of their level)
+//   head books, tile-parallel: k_fc_pcnt / k_fc_pscan / k_fc_prank   targeted ADDs' ranks per
+//                   level, each DEL's count of targets that arrived before it, and the (level,
+//                   side) ADD volume before every targeted ADD and DEL; k_fc_pwin   windows, DEL
+//                   times and volumes by rank; k_fc_precs   Q and the DEL records
+//   tail books: k_fc_pass, the same in one block per book
 // Reconstruction (after the plan and the level sort of its touches):
 //   k_fc_level      per level: cancels -> their DEL's record; the consumption-space layout of
 //                   the makers (a cancelled maker only spans what was consumed before its
@@ -60,7 +64,8 @@ struct FcDel {
   uint32_t li;       // the target's level
   uint32_t tgt;      // FC_NEW: the ADD's segment position; FC_OLD: the node (chunk * CH + slot)
   uint32_t rank;     // the target's rank among the level's targets (arrival order)
-  uint32_t nb;       // window: targets that arrived behind the target before this DEL
+  uint32_t nb;       // window: targets that arrived behind the target before this DEL (the
+                     // candidates of Q's cancelled part)
   uint32_t ixs;      // FC_OLD: the node's cancel-index slot
   uint32_t oend, ov; // the target's arrival end / volume (plan units; FC_NEW: counted over the
                      // segment's ADDs only)

@@ -1,10 +1,11 @@
 """Cancels on the flow path (match_flow_cancel.h): hot books whose segment holds DELs, planned by
-the W32C aggregate plan (R_k and the per-level LDS ring of targeted makers, gen_plan_asm.py)
-and reconstructed in consumption space.  Every case is bit-exact against the C oracle (events,
-levels, FIFOs, resting count) and, where stated, identical to the legacy FIFO kernel.
+the W32C aggregate plan (per-side depths only: a DEL removes clamp(depth - Q, 0, v) with Q from
+the cancel prep, gen_plan_asm.py) and reconstructed in consumption space.  Every case is
+bit-exact against the C oracle (events, levels, FIFOs, resting count) and, where stated,
+identical to the legacy FIFO kernel.
 
-The design itself (r_m = clamp(E_m + v_m - G_k + Xb_m, 0, v_m)) is checked on the CPU by
-tools/flow_cancel_model.py; these are the device tests proper."""
+The formula itself is checked on the CPU by tools/flow_cancel_model.py (plan_book_q); these are
+the device tests proper."""
 import numpy as np
 import pytest
 
@@ -47,8 +48,8 @@ def _routes_msg():
         for x in fbk:
             c[(int(x["kind"]), int(x["decline"]), int(x["w32"]))] += 1
     bad = [x for _, fbk in ROUTES for x in fbk if x["decline"]]
-    worst = [(int(x["ring"]), int(x["window"]), int(x["orders"]), int(x["levels"])) for x in bad[:6]]
-    return "routing (kind, decline bits, w32): " + repr(dict(c)) + "; declined (ring, window, orders, levels): " + repr(worst)
+    worst = [(int(x["wsum"]), int(x["window"]), int(x["orders"]), int(x["levels"])) for x in bad[:6]]
+    return "routing (kind, decline bits, w32): " + repr(dict(c)) + "; declined (window sum, window, orders, levels): " + repr(worst)
 
 
 def _run(batches, ns, check_every=True):
@@ -141,8 +142,8 @@ def test_flow_cancel_fuzz_small_books(seed):
 
 @pytest.mark.parametrize("seed", range(3))
 def test_flow_cancel_fuzz_tail_books(seed):
-    """40 symbols: 8 head books (wide kernels) and 32 tail books (per-book kernels, 16 KiB
-    rings)."""
+    """40 symbols: 8 head books (tile-parallel prep) and 32 tail books (one prep block per
+    book)."""
     fz = _Fuzz(200 + seed, ns=40, nprice=5)
     batches = [fz.batch(20000) for _ in range(4)]
     eng, orc, fc, fb = _run(batches, 40, check_every=False)
@@ -186,7 +187,7 @@ def _recs(rows):
 
 def test_flow_cancel_long_windows():
     """300 makers at one level, each cancelled later in the batch in arrival order: windows of
-    up to 299 targets (the plan's out-of-line window loop), takers in between."""
+    up to 299 targets (the prep's C loop over them), takers in between."""
     rows, oid = [], 1
     for k in range(300):
         rows.append((51 * 10**6, (1 + k % 7) * 10**6, 0, oid, 3, 1, ADD, 0))

@@ -39,4 +39,4 @@ for bi in range(int(sys.argv[2]) if len(sys.argv) > 2 else 4):
         q = np.percentile(nb, [50, 90, 99, 100])
         print(f"   window n_b p50 {q[0]:.0f} p90 {q[1]:.0f} p99 {q[2]:.0f} max {q[3]:.0f}; >63: {float((nb > 63).mean()):.3f}"
               f"  mean chunks {float(np.ceil(nb / 63).mean()):.2f}")
-    print("   head routes (kind, decline, ring, window):", [(int(x["kind"]), int(x["decline"]), int(x["ring"]), int(x["window"])) for x in fb])
+    print("   head routes (kind, decline, window sum, window):", [(int(x["kind"]), int(x["decline"]), int(x["wsum"]), int(x["window"])) for x in fb])

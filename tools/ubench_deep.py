@@ -11,7 +11,7 @@ from gome_amd.abi import Engine  # noqa: E402
 N = 1 << 18
 for dec in (4, 3):
     st = wl.Stream(1, seed=7, price_decimals=dec)
-    eng = Engine(max_symbols=1, max_batch=N, max_nodes=1 << 23, max_levels=1 << 16)
+    eng = Engine(max_symbols=1, max_batch=N, max_nodes=1 << 23, max_levels=1 << 20)
     t = []
     for i in range(6):
         b = st.batch(N)

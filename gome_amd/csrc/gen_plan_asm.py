@@ -715,9 +715,10 @@ class GenC(Gen):
 DEEP_CAP = 16384
 DEEP_BM = DEEP_CAP * 8                       # byte offset of the bid bitmap (asks follow)
 DEEP_BM_BYTES = 2 * DEEP_CAP // 8
-VDA, VDD, VSA, VSD, VSL, VZD = 36, 37, 38, 39, 40, 41   # slot address / data, scan address /
-VBA, VBD, VBASE_A, VBASE_B = 42, 43, 44, 45             # data, lane id, zero; bit address / data;
-CLOBBERS_D = [f"v{i}" for i in range(36, 46)]            # per-lane scan bases of the bitmaps
+VDA, VDD, VSA, VSD, VSL, VZD = 36, 37, 38, 39, 40, 41   # slot address / data, group read address /
+VSUM_B, VSUM_A, VBASE_A, VBASE_B = 42, 43, 44, 45       # data, lane id, zero; group summaries;
+CLOBBERS_D = [f"v{i}" for i in range(36, 46)]            # per-lane slot offsets (8 * lane + side)
+VSUM = {"B": VSUM_B, "A": VSUM_A}
 BM = {"B": DEEP_BM, "A": DEEP_BM + DEEP_CAP // 8}
 
 
@@ -777,61 +778,73 @@ class GenD(Gen):
 
     def next_top(self, sd: str):
         """After the cached top of side sd emptied: the next level of that side (asks: the lowest
-        set bit above BA, bids: the highest below BB; the sentinels' bits are always set).  Lane
-        i reads bitmap dword w0 + i (asks) / w0 - 63 + i (bids): every bit of the side below BA
-        (above BB) is 0 by the invariant, so the first dword needs no mask.  The level's slot
-        becomes the cached depth (read, then zeroed) and its bit is cleared."""
+        nonzero slot above BA, bids: the highest below BB; the sentinels' slots are nonzero).  A
+        per-side summary register (lane i bit j: group 32i + j of 32 levels holds a nonzero
+        slot; 16 lanes cover the 16384 levels) gives the group without touching LDS: the
+        candidate's own summary word first, else a compare over the lanes beyond it.  One
+        32-lane read of the group's slots gives the level and its depth; the slot is zeroed and
+        the group's summary bit cleared when it was the group's only nonzero slot."""
         e = self.e
         top, topd = (BA, BAD) if sd == "A" else (BB, BBD)
-        loop, more = self.fresh("NT"), self.fresh("NM")
-        off = self.side_off(sd)
-        base = VBASE_A if sd == "A" else VBASE_B
-        if sd == "A":
-            e(f"s_add_u32 {T0}, {BA}, 1")
+        asks = sd == "A"
+        vs = VSUM[sd]
+        base = VBASE_A if asks else VBASE_B
+        more, cont = self.fresh("NM"), self.fresh("NC")
+        G, W, MK, LN = O[0], O[2], O[3], "s81"
+        if asks:
+            e(f"s_add_u32 {T0}, {BA}, 1")                    # the first candidate level
         else:
             e(f"s_sub_u32 {T0}, {BB}, 1")
-        e(f"s_lshr_b32 {T0}, {T0}, 5")                      # the dword of the first candidate
-        e(f"{loop}:")
-        e("s_mov_b64 exec, -1")
-        e(f"s_lshl_b32 {O[2]}, {T0}, 2")
-        e(f"v_add_u32 v{VSA}, {O[2]}, v{base}")
+        e(f"s_lshr_b32 s79, {T0}, 5")                       # its group
+        e(f"s_lshr_b32 {LN}, {T0}, 10")                     # the group's summary lane
+        e(f"v_readlane_b32 {W}, v{vs}, {LN}")
+        if asks:
+            e(f"s_lshl_b32 {MK}, -1, s79")                  # groups >= the candidate's
+        else:
+            e(f"s_lshl_b32 {MK}, -2, s79")
+            e(f"s_not_b32 {MK}, {MK}")                      # groups <= the candidate's
+        e(f"s_and_b32 {W}, {W}, {MK}")
+        e(f"s_cbranch_scc0 {more}")
+        blk = [f"{more}:", "s_mov_b64 exec, -1", f"v_cmp_ne_u32_e64 {M}, 0, v{vs}"]
+        if asks:   # lanes above LN
+            blk += ["s_mov_b64 s[92:93], -1", f"s_add_u32 {LN}, {LN}, 1", f"s_lshl_b64 s[92:93], s[92:93], {LN}",
+                    f"s_and_b64 {M}, {M}, s[92:93]", f"s_ff1_i32_b64 {LN}, {M}"]
+        else:      # lanes below LN
+            blk += [f"s_bfm_b64 s[92:93], {LN}, 0", f"s_and_b64 {M}, {M}, s[92:93]",
+                    f"s_flbit_i32_b64 {LN}, {M}", f"s_sub_u32 {LN}, 63, {LN}"]
+        blk += [f"v_readlane_b32 {W}, v{vs}, {LN}", f"s_branch {cont}"]
+        self.slow.append(blk)
+        e(f"{cont}:")
+        if asks:
+            e(f"s_ff1_i32_b32 {G}, {W}")
+        else:
+            e(f"s_flbit_i32_b32 {G}, {W}")
+            e(f"s_sub_u32 {G}, 31, {G}")
+        e(f"s_lshl_b32 {LN}, {LN}, 5")
+        e(f"s_add_u32 {G}, {G}, {LN}")                      # the group
+        e(f"s_lshl_b32 {W}, {G}, 8")                        # its first slot's byte offset
+        e("s_mov_b64 exec, 0xffffffff")
+        e(f"v_add_u32 v{VSA}, {W}, v{base}")
         e(f"ds_read_b32 v{VSD}, v{VSA}")
+        e(f"s_lshl_b32 s79, 1, {G}")                        # the group's summary bit
+        e(f"s_lshr_b32 {LN}, {G}, 5")
+        e(f"s_lshl_b32 {top}, {G}, 5")
         e("s_waitcnt lgkmcnt(0)")
         e(f"v_cmp_ne_u32_e64 {M}, 0, v{VSD}")
-        e(f"s_{'ff1' if sd == 'A' else 'flbit'}_i32_b64 {O[0]}, {M}")
-        e(f"s_cmp_lt_i32 {O[0]}, 0")
-        e(f"s_cbranch_scc1 {more}")                         # no set bit in 2048 levels (rare)
-        self.slow.append([f"{more}:", f"s_{'add' if sd == 'A' else 'sub'}_u32 {T0}, {T0}, 64",
-                          f"s_branch {loop}"])
-        if sd == "A":
-            e(f"v_readlane_b32 {O[2]}, v{VSD}, {O[0]}")
-            e(f"s_ff1_i32_b32 {O[2]}, {O[2]}")
-            e(f"s_add_u32 {T0}, {T0}, {O[0]}")
+        if asks:
+            e(f"s_ff1_i32_b64 {MK}, {M}")
         else:
-            e(f"s_sub_u32 {O[0]}, 63, {O[0]}")              # the lane
-            e(f"v_readlane_b32 {O[2]}, v{VSD}, {O[0]}")
-            e(f"s_flbit_i32_b32 {O[2]}, {O[2]}")
-            e(f"s_sub_u32 {O[2]}, 31, {O[2]}")
-            e(f"s_sub_u32 {T0}, {T0}, 63")
-            e(f"s_add_u32 {T0}, {T0}, {O[0]}")
-        e(f"s_lshl_b32 {T0}, {T0}, 5")
-        e(f"s_add_u32 {top}, {T0}, {O[2]}")
-        # the slot: its depth becomes the cached one, the slot 0 (LDS ops of a wave run in order)
-        e(f"s_lshl_b32 {T0}, {top}, 3")
-        e("s_mov_b64 exec, 1")
-        e(f"v_mov_b32 v{VDA}, {T0}")
-        e(f"ds_read_b32 v{VDD}, v{VDA} offset:{off}")
-        e(f"ds_write_b32 v{VDA}, v{VZD} offset:{off}")
-        # its bit (set) is cleared
-        e(f"s_lshr_b32 {T0}, {top}, 3")
-        e(f"s_and_b32 {T0}, {T0}, 0x7fc")
-        e(f"s_add_u32 {T0}, {T0}, {BM[sd]}")
-        e(f"s_lshl_b32 {O[2]}, 1, {top}")
-        e(f"v_mov_b32 v{VBA}, {T0}")
-        e(f"v_mov_b32 v{VBD}, {O[2]}")
-        e(f"ds_xor_b32 v{VBA}, v{VBD}")
-        e("s_waitcnt lgkmcnt(0)")
-        e(f"v_readfirstlane_b32 {topd[0]}, v{VDD}")
+            e(f"s_flbit_i32_b64 {MK}, {M}")
+            e(f"s_sub_u32 {MK}, 63, {MK}")
+        e(f"v_readlane_b32 {topd[0]}, v{VSD}, {MK}")
+        e(f"s_add_u32 {top}, {top}, {MK}")
+        e(f"s_bfm_b64 exec, 1, {MK}")
+        e(f"ds_write_b32 v{VSA}, v{VZD}")                   # the slot := 0
+        e(f"s_bcnt1_i32_b64 {W}, {M}")
+        e(f"s_cmp_eq_u32 {W}, 1")
+        e(f"s_cselect_b32 s79, s79, 0")
+        e(f"s_bfm_b64 exec, 1, {LN}")
+        e(f"v_xor_b32 v{vs}, s79, v{vs}")                   # the group emptied: its bit cleared
 
     def rest(self, side: str, T):
         """As the 32-bit rest, with the lane add replaced by an LDS add at slot (L, side)."""
@@ -849,15 +862,14 @@ class GenD(Gen):
         e(f"s_{'max' if buy else 'min'}_u32 {top}, {top}, {LI}")
         self.add(topd, topd, X)
         self.lds_add(L, A[0], "B" if buy else "A")
-        # slot L is nonzero now iff A > 0 (A == 0: L is the cached top, whose bit stays 0)
+        # slot L is nonzero now iff A > 0 (A == 0: L is the cached top, whose slot stays 0): its
+        # group's summary bit
         e(f"s_min_u32 s79, {A[0]}, 1")
-        e(f"s_lshl_b32 s79, s79, {L}")
-        e(f"s_lshr_b32 s81, {L}, 3")
-        e(f"s_and_b32 s81, s81, 0x7fc")
-        e(f"s_add_u32 s81, s81, {BM['B' if buy else 'A']}")
-        e(f"v_mov_b32 v{VBA}, s81")
-        e(f"v_mov_b32 v{VBD}, s79")
-        e(f"ds_or_b32 v{VBA}, v{VBD}")
+        e(f"s_lshr_b32 s81, {L}, 5")
+        e(f"s_lshl_b32 s79, s79, s81")
+        e(f"s_lshr_b32 s81, {L}, 10")
+        e(f"s_bfm_b64 exec, 1, s81")
+        e(f"v_or_b32 v{VSUM['B' if buy else 'A']}, s79, v{VSUM['B' if buy else 'A']}")
         e(f"s_or_b32 {K}, {JJS}, 0x80")
         self.logd(K, T[0], LI)
 
@@ -915,9 +927,10 @@ class GenD(Gen):
         e(f"v_mbcnt_lo_u32_b32 v{VSL}, -1, 0")
         e(f"v_mbcnt_hi_u32_b32 v{VSL}, -1, v{VSL}")
         e(f"v_mov_b32 v{VZD}, 0")
-        e(f"v_lshlrev_b32 v{VBASE_A}, 2, v{VSL}")
-        e(f"v_add_u32 v{VBASE_B}, {BM['B'] - 252}, v{VBASE_A}")   # lane i: dword w0 - 63 + i
-        e(f"v_add_u32 v{VBASE_A}, {BM['A']}, v{VBASE_A}")         # lane i: dword w0 + i
+        e(f"v_lshlrev_b32 v{VBASE_B}, 3, v{VSL}")                 # lane l: slot l of a group (bid)
+        e(f"v_add_u32 v{VBASE_A}, 4, v{VBASE_B}")                 # (ask)
+        e(f"v_mov_b32 v{VSUM_B}, %[sb]")
+        e(f"v_mov_b32 v{VSUM_A}, %[sa]")
         e(f"s_mov_b32 {ZERO}, 0")
         e(f"s_mov_b32 {BA}, 0")
         self.next_top("A")

@@ -1152,11 +1152,20 @@ __device__ __forceinline__ void fl_plan_deep(const Dev& D, const FlowArgs& F, ui
   const uint32_t vl16 = lane * 16u;
   uint32_t voff;
   const uint32_t vzero = 0;
+  // the plan's group summaries (lane i bit j: group 32i + j of 32 levels holds a nonzero slot of
+  // that side), from the bitmaps fl_deep_load built
+  const uint32_t* bm = reinterpret_cast<const uint32_t*>(fl_ring) + FL_DEEP_BM / 4;
+  uint32_t sb = 0, sa = 0;
+  if (lane < DEEP_CAP / 1024)
+    for (uint32_t j = 0; j < 32; ++j) {
+      sb |= (bm[32 * lane + j] != 0 ? 1u : 0u) << j;
+      sa |= (bm[DEEP_CAP / 32 + 32 * lane + j] != 0 ? 1u : 0u) << j;
+    }
   asm volatile(FL_PLAN_ASM32D
                : [lk] "+v"(lg.lk), [la] "+v"(lg.la), [lb] "+v"(lg.lb), [nacc] "+s"(lg.nacc), [lpos] "+s"(lg.lpos),
                  [voff] "=&v"(voff)
                : [ob] "s"(ob), [nh] "s"(nh), [logp] "s"(logp), [lcap] "s"(lg.lcap), [vl16] "v"(vl16),
-                 [vzero] "v"(vzero)
+                 [vzero] "v"(vzero), [sb] "v"(sb), [sa] "v"(sa)
                : FL_PLAN_CLOBBERS, FL_PLAN_CLOBBERS_D, "scc", "vcc", "memory");
   if (lg.nacc) {  // {key, level, amount, 0}
     if (lane < lg.nacc && lg.lpos + lg.nacc <= lg.lcap) lg.p[lg.lpos + lane] = v4(lg.lk, lg.lb, lg.la, 0u);

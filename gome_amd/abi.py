@@ -98,6 +98,7 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.gome_get_stats.argtypes = [VP, P(Stats)]
     lib.gome_snapshot_levels.argtypes = [VP, C.c_uint32, VP, C.c_size_t, P(C.c_size_t)]
     lib.gome_snapshot_fifo.argtypes = [VP, C.c_uint32, C.c_int64, VP, C.c_size_t, P(C.c_size_t)]
+    lib.gome_load_books.argtypes = [VP, C.c_size_t, VP, VP, VP, VP, C.c_size_t]
     lib.gome_fixed_from_double.argtypes = [C.c_double, C.c_uint32, P(C.c_int64)]
     lib.gome_render_match_result.argtypes = [VP, VP, C.c_uint32] + [C.c_char_p] * 6 + [
         VP, C.c_char_p, C.c_size_t]
@@ -115,7 +116,7 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     for f in ("gome_create", "gome_submit_batch", "gome_submit_batch_device", "gome_drain_events",
               "gome_device_events", "gome_get_stats", "gome_snapshot_levels", "gome_snapshot_fifo",
               "gome_fixed_from_double", "gome_fixed_from_scaled", "gome_submit_batch_async",
-              "gome_collect", "gome_host_alloc"):
+              "gome_collect", "gome_host_alloc", "gome_load_books"):
         getattr(lib, f).restype = C.c_int32
     _lib = lib
     return lib
@@ -290,6 +291,18 @@ class Engine:
         st = Stats()
         self._check(self.lib.gome_get_stats(self.h, C.byref(st)))
         return st.as_dict()
+
+    def load_books(self, books) -> None:
+        """gome_load_books: `books` = [(symbol_id, levels LEVEL_DTYPE ascending by price,
+        nodes NODE_DTYPE in FIFO order, level by level)] into this fresh engine."""
+        sym = np.array([b[0] for b in books], np.uint32)
+        nlv = np.array([len(b[1]) for b in books], np.uint32)
+        lv = np.concatenate([b[1] for b in books]) if books else np.zeros(0, LEVEL_DTYPE)
+        nd = np.concatenate([b[2] for b in books]) if books else np.zeros(0, NODE_DTYPE)
+        lv = np.ascontiguousarray(lv, LEVEL_DTYPE)
+        nd = np.ascontiguousarray(nd, NODE_DTYPE)
+        self._check(self.lib.gome_load_books(self.h, len(sym), sym.ctypes.data, nlv.ctypes.data, lv.ctypes.data,
+                                             nd.ctypes.data, len(nd)))
 
     def levels(self, symbol_id: int) -> np.ndarray:
         n = C.c_size_t()

@@ -26,6 +26,7 @@
 #include <cstring>
 #include <deque>
 #include <set>
+#include <unordered_set>
 #include <string>
 #include <vector>
 
@@ -252,6 +253,9 @@ struct gome_engine {
                       uint64_t inflight_n);
   gome_status finish(uint32_t slot, uint32_t n);
   gome_status check_submit(size_t n, const void* p);
+  gome_status load_books(size_t nb, const uint32_t* bsym, const uint32_t* bnlv, const gome_level* lv,
+                         const gome_node* nd, size_t nn);
+  bool used = false;  // a batch was submitted or books were loaded (gome_load_books needs a fresh engine)
   gome_status check_capacity(unsigned long long adds, unsigned long long inflight_n);
   gome_status check_capacity_host(const gome_order* o, size_t n, unsigned long long inflight_n);
   uint32_t take_slot() {
@@ -802,6 +806,7 @@ gome_status gome_engine::finish(uint32_t sl, uint32_t n) {
 
 gome_status gome_engine::check_submit(size_t n, const void* p) {
   if (poisoned) return fail(GOME_E_STATE, "engine poisoned by an earlier fatal error");
+  used = true;
   if (n > max_batch) return fail(GOME_E_INVAL, "batch larger than max_batch");
   if (n && !p) return fail(GOME_E_INVAL, "NULL records");
   return GOME_OK;
@@ -1138,6 +1143,142 @@ gome_status gome_get_stats(const gome_engine* e, gome_stats* out) {
   if (!e || !out) return GOME_E_INVAL;
   *out = e->stats;
   return GOME_OK;
+}
+
+// ---- gome_load_books: a Redis-schema book image straight into the pools of a fresh engine
+__global__ void k_load_index(IdxEnt* idx, const unsigned long long* slot, const IdxEnt* ent, size_t n) {
+  for (size_t i = blockIdx.x * static_cast<size_t>(blockDim.x) + threadIdx.x; i < n; i += gridDim.x * static_cast<size_t>(blockDim.x))
+    idx[slot[i]] = ent[i];
+}
+
+gome_status gome_engine::load_books(size_t nb, const uint32_t* bsym, const uint32_t* bnlv, const gome_level* lv,
+                                    const gome_node* nd, size_t nn) {
+  if (poisoned) return fail(GOME_E_STATE, "engine poisoned by an earlier fatal error");
+  if (used) return fail(GOME_E_STATE, "gome_load_books: load into a fresh engine (no batch submitted, nothing loaded)");
+  if ((nb && (!bsym || !bnlv)) || (nn && !nd)) return fail(GOME_E_INVAL, "gome_load_books: NULL arrays");
+  size_t nlv = 0;
+  for (size_t b = 0; b < nb; ++b) nlv += bnlv[b];
+  if (nlv && !lv) return fail(GOME_E_INVAL, "gome_load_books: NULL levels");
+  if (nn > cfg.max_nodes) return fail(GOME_E_CAPACITY, "gome_load_books: more nodes than max_nodes");
+  const uint32_t ms = D.max_symbols;
+  std::vector<Book> books(ms, Book{0, 0, 0, 0});
+  std::vector<uint8_t> seen(ms, 0);
+  std::vector<Level> lvl;
+  std::vector<Node> nodes;
+  std::vector<ChunkHdr> chdr;
+  std::vector<unsigned long long> islot;
+  std::vector<IdxEnt> ient;
+  std::unordered_set<unsigned long long> occ;
+  const unsigned long long mask = idx_cap - 1;
+  size_t li = 0, ni = 0;
+  for (size_t b = 0; b < nb; ++b) {
+    const uint32_t sym = bsym[b], n = bnlv[b];
+    if (sym >= ms || seen[sym]) return fail(GOME_E_INVAL, "gome_load_books: symbol out of range or repeated");
+    seen[sym] = 1;
+    uint32_t cap = 16;
+    while (cap < n) cap <<= 1;
+    if (cap > (16u << (LVL_NCLS - 1))) return fail(GOME_E_CAPACITY, "gome_load_books: book with too many levels");
+    const size_t base = lvl.size();
+    if (base + cap > cfg.max_levels) return fail(GOME_E_CAPACITY, "gome_load_books: levels exceed max_levels");
+    lvl.resize(base + cap, Level{});
+    bool quirk = false;
+    int64_t best_bid = INT64_MIN, best_ask = INT64_MAX;
+    for (uint32_t k = 0; k < n; ++k, ++li) {
+      const gome_level& g = lv[li];
+      if (k && g.price_fx <= lv[li - 1].price_fx) return fail(GOME_E_INVAL, "gome_load_books: prices not ascending");
+      if (ni + g.n_nodes > nn) return fail(GOME_E_INVAL, "gome_load_books: level node counts exceed n_nodes");
+      Level L{};
+      L.price = g.price_fx;
+      L.depth = g.depth_fx;
+      L.member = static_cast<uint8_t>((g.in_buy ? M_BUY : 0) | (g.in_sale ? M_SALE : 0));
+      L.head = L.tail = NIL;
+      L.nlive = g.n_nodes;
+      int64_t sum = 0;
+      uint32_t sides = 0, prev = NIL;
+      for (uint32_t j = 0; j < g.n_nodes; ++j, ++ni) {
+        const gome_node& x = nd[ni];
+        if (x.volume_fx < 0) return fail(GOME_E_INVAL, "gome_load_books: negative node volume");
+        if (j % CH == 0) {
+          const uint32_t c = static_cast<uint32_t>(chdr.size());
+          if (c >= D.ch_cap) return fail(GOME_E_CAPACITY, "gome_load_books: FIFO chunks exceed the pool");
+          chdr.push_back(ChunkHdr{NIL, 0, g.price_fx});
+          nodes.resize(static_cast<size_t>(c + 1) * CH, Node{});
+          if (prev != NIL) chdr[prev].next = c;
+          else L.head = c;
+          prev = c;
+        }
+        const uint32_t loc = prev * CH + j % CH;
+        Node& N = nodes[loc];
+        N.rem = x.volume_fx;
+        N.oid = x.oid_id;
+        N.uuid = x.uuid_id;
+        N.tx = x.side;
+        const unsigned long long key = (static_cast<unsigned long long>(sym + 1) << 32) | x.oid_id;
+        unsigned long long h = mix64(key) & mask;
+        while (occ.count(h)) h = (h + 1) & mask;
+        occ.insert(h);
+        N.ixs = static_cast<uint32_t>(h);
+        islot.push_back(h);
+        ient.push_back(IdxEnt{key, loc, 0});
+        sum += x.volume_fx;
+        sides |= x.side == GOME_SALE ? 2u : 1u;
+        if (x.volume_fx == 0) quirk = true;  // a zero-volume maker (Q6)
+      }
+      if (g.n_nodes) {
+        L.tail = prev;
+        L.tslot = static_cast<uint8_t>((g.n_nodes - 1) % CH + 1);
+      }
+      // the flow plans' invariant: a live level has nodes of one side, its depth is their sum
+      // and it is a member of exactly that side's set
+      const uint32_t want = sides == 1u ? M_BUY : (sides == 2u ? M_SALE : 0u);
+      if (!g.n_nodes || sum != g.depth_fx || sides == 3u || L.member != want) quirk = true;
+      if (L.member & M_BUY) best_bid = std::max(best_bid, g.price_fx);
+      if (L.member & M_SALE) best_ask = std::min(best_ask, g.price_fx);
+      lvl[base + k] = L;
+    }
+    if (best_bid >= best_ask) quirk = true;  // a crossed book (only reachable through quirks)
+    books[sym] = Book{static_cast<uint32_t>(base), n, cap, quirk ? BOOK_QUIRK : 0u};
+  }
+  if (ni != nn) return fail(GOME_E_INVAL, "gome_load_books: n_nodes differs from the levels' node counts");
+  if (occ.size() > idx_cap / 2) return fail(GOME_E_CAPACITY, "gome_load_books: cancel index over half full");
+  hipStream_t s = stream;
+  const uint32_t nch = static_cast<uint32_t>(chdr.size()), nl = static_cast<uint32_t>(lvl.size());
+  if (nl) HIPCHK(hipMemcpyAsync(D.lvl, lvl.data(), nl * sizeof(Level), hipMemcpyHostToDevice, s));
+  if (nch) {
+    HIPCHK(hipMemcpyAsync(D.nodes, nodes.data(), static_cast<size_t>(nch) * CH * sizeof(Node), hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(D.chdr, chdr.data(), nch * sizeof(ChunkHdr), hipMemcpyHostToDevice, s));
+  }
+  HIPCHK(hipMemcpyAsync(D.books, books.data(), static_cast<size_t>(ms) * sizeof(Book), hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(D.lvl_bump, &nl, 4, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(D.ch_bump, &nch, 4, hipMemcpyHostToDevice, s));
+  if (!islot.empty()) {
+    unsigned long long* d_slot = nullptr;
+    IdxEnt* d_ent = nullptr;
+    if (!alloc(&d_slot, islot.size(), "load index slots") || !alloc(&d_ent, ient.size(), "load index entries"))
+      return GOME_E_CAPACITY;
+    HIPCHK(hipMemcpyAsync(d_slot, islot.data(), islot.size() * 8, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(d_ent, ient.data(), ient.size() * sizeof(IdxEnt), hipMemcpyHostToDevice, s));
+    k_load_index<<<ceil_div(static_cast<uint32_t>(std::min<size_t>(islot.size(), 1u << 24)), 256), 256, 0, s>>>(
+        D.idx, d_slot, d_ent, islot.size());
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(s));
+    release(d_slot);
+    release(d_ent);
+  }
+  HIPCHK(hipStreamSynchronize(s));
+  resting = nn;
+  levels = nlv;
+  stats.n_resting = resting;
+  stats.n_levels = levels;
+  used = true;
+  return GOME_OK;
+}
+
+gome_status gome_load_books(gome_engine* e, size_t n_books, const uint32_t* book_sym, const uint32_t* book_nlv,
+                            const gome_level* levels, const gome_node* nodes, size_t n_nodes) {
+  if (!e) return GOME_E_INVAL;
+  if (gome_status st = e->collect_all()) return st;
+  return e->load_books(n_books, book_sym, book_nlv, levels, nodes, n_nodes);
 }
 
 gome_status gome_snapshot_levels(gome_engine* e, uint32_t sym, gome_level* out, size_t cap,

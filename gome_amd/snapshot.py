@@ -17,11 +17,15 @@ the reference never deletes a depth field, so prices whose depth went back to 0 
 reference treats a missing field exactly like "0" (HINCRBYFLOAT starts from 0; the
 ParseFloat error of an empty HGET gives 0 in DeletePoolDepth, nodepool.go:76-83).
 
-Resume replays the snapshot: every resting node becomes an ADD of its remaining volume, in
-FIFO order per level.  A snapshot of an uncrossed book produces no fill, so the engine
-rebuilds the same levels, FIFOs and cancel index.  Books whose depth differs from the sum
-of their FIFO (the reference's quirk states) cannot be rebuilt this
-way and are refused.
+Resume, two ways:
+  * `load` writes the books straight into the pools of a fresh engine (gome_load_books): every
+    state the reference's Redis can hold, quirk states included (a side-set member without a
+    FIFO after a wrong-side cancel, Q2; a depth that differs from the FIFO's sum; a zero-volume
+    maker, Q6), comes back exactly;
+  * `restore` replays the snapshot into any engine: every resting node becomes an ADD of its
+    remaining volume, in FIFO order per level.  A snapshot of an uncrossed book produces no
+    fill, so the engine rebuilds the same levels, FIFOs and cancel index.  Books in a quirk
+    state cannot be rebuilt this way and are refused.
 
 `names` maps interned ids to the reference's strings: any object with
 name(kind, id) -> str and id(kind, str) -> int, kinds "sym", "uuid", "oid" (the host owns
@@ -32,11 +36,12 @@ identity when absent).
 from __future__ import annotations
 
 import json
+from decimal import Decimal
 
 import numpy as np
 
 from .abi import GOME_E_INVAL, GomeError, render_link_node
-from .workload import ADD, ORDER_DTYPE
+from .workload import ADD, LEVEL_DTYPE, NODE_DTYPE, ORDER_DTYPE
 
 GOME_SALE = 1
 
@@ -175,3 +180,67 @@ def restore(eng, snap: dict, names, seq_base: int = 0, chunk: int | None = None)
         if len(ev):
             raise GomeError(GOME_E_INVAL, f"snapshot book is crossed: {len(ev)} fills on replay")
     return len(rec)
+
+
+def _fifo(key: str, link: dict) -> list:
+    """The node JSON objects of one S:link:<price> HASH in FIFO order (f, then NextNode)."""
+    out, name = [], link.get("f")
+    while name:
+        if name not in link or len(out) > len(link):
+            raise GomeError(GOME_E_INVAL, f"{key}: broken FIFO chain at {name}")
+        nd = json.loads(link[name])
+        out.append(nd)
+        name = nd["NextNode"]
+    if len(out) != len(link) - 2:
+        raise GomeError(GOME_E_INVAL, f"{key}: FIFO chain does not cover the level")
+    return out
+
+
+def book_images(snap: dict, names) -> list:
+    """The snapshot as gome_load_books images: [(symbol_id, levels, nodes)], one per symbol,
+    levels ascending by price.  A level is every price in S:BUY / S:SALE, with a nonzero
+    S:depth field or with an S:link HASH; nothing is checked for consistency (quirk states load
+    as they are)."""
+    per: dict[str, dict[int, list]] = {}
+
+    def lvl(S: str, p: int) -> list:
+        return per.setdefault(S, {}).setdefault(p, [0, 0, 0, []])
+
+    for key, members in snap["zset"].items():
+        S, _, sd = key.rpartition(":")
+        for m in members:
+            lvl(S, int(m))[0 if sd == "BUY" else 1] = 1
+    for key, fields in snap["hash"].items():
+        if key.endswith(":depth"):
+            S = key[:-len(":depth")]
+            for f, v in fields.items():
+                d = int(Decimal(v))
+                if d:
+                    lvl(S, int(f.rpartition(":")[2]))[2] = d
+        elif ":link:" in key:
+            S, _, P = key.partition(":link:")
+            lvl(S, int(P))[3] = _fifo(key, fields)
+    books = []
+    for S, lvls in per.items():
+        prices = sorted(lvls)
+        lv = np.zeros(len(prices), LEVEL_DTYPE)
+        nodes = []
+        for i, p in enumerate(prices):
+            b, a, d, fifo = lvls[p]
+            lv[i] = (p, d, len(fifo), b, a, 0)
+            for nd in fifo:
+                nodes.append((int(nd["Volume"]), names.id("oid", nd["Oid"]), names.id("uuid", nd["Uuid"]),
+                              _tx_code(names, int(nd["Transaction"]))))
+        na = np.zeros(len(nodes), NODE_DTYPE)
+        for i, (v, o, u, t) in enumerate(nodes):
+            na[i]["volume_fx"], na[i]["oid_id"], na[i]["uuid_id"], na[i]["side"] = v, o, u, t
+        books.append((names.id("sym", S), lv, na))
+    return books
+
+
+def load(eng, snap: dict, names) -> int:
+    """Resume: the snapshot's books straight into a fresh engine (gome_load_books), quirk states
+    included.  Returns the resting nodes loaded."""
+    books = book_images(snap, names)
+    eng.load_books(books)
+    return sum(len(b[2]) for b in books)

@@ -264,6 +264,23 @@ gome_status gome_snapshot_levels(gome_engine* e, uint32_t symbol_id,
 gome_status gome_snapshot_fifo(gome_engine* e, uint32_t symbol_id, int64_t price_fx,
                                gome_node* out, size_t cap, size_t* n_out);
 
+/* ---- book state load (restart from Redis) ------------------- */
+/* The reference restarts from whatever its Redis holds (nodepool.go:14-115,
+ * nodelink.go:12-166, ordernode.go:89-116).  gome_load_books writes such books straight
+ * into the device pools of a fresh engine (no batch submitted and nothing loaded before;
+ * otherwise GOME_E_STATE): the inverse of gome_snapshot_levels / gome_snapshot_fifo.
+ * Book b is symbol book_sym[b] (distinct, < max_symbols) with book_nlv[b] levels; the
+ * levels follow book by book in ascending price, and each level's n_nodes nodes follow in
+ * `nodes` in FIFO order (head first, side = Transaction code).  Every state the reference
+ * can hold loads as it is, quirk states included (a depth that differs from the FIFO's
+ * sum, a side-set member without nodes (Q2), a zero-volume maker (Q6), a FIFO of mixed
+ * sides); books in such a state are applied by the legacy kernels from then on.  Duplicate
+ * (symbol, oid) keys: lookups find the first in load order.  GOME_E_CAPACITY when the
+ * pools (max_levels, max_nodes) cannot hold the image. */
+gome_status gome_load_books(gome_engine* e, size_t n_books, const uint32_t* book_sym,
+                            const uint32_t* book_nlv, const gome_level* levels,
+                            const gome_node* nodes, size_t n_nodes);
+
 /* ---- host helpers (no device work) --------------------------------------- */
 /* ordernode.go:76-87: Float64(decimal.NewFromFloat(x) * decimal.NewFromFloat(10^acc)).
  * Succeeds iff that product is an integer with |v| < 2^53 (the domain on which the

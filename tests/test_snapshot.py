@@ -144,3 +144,105 @@ def test_restore_refuses_crossed_book_before_submitting():
     snap["hash"]["s:link:50000000"]["s:node:b"] = node("b", 0, 50000000, 100000000, None, None)
     rec = snapshot.restore_records(snap, names)
     assert len(rec) == 2
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(4))
+def test_load_quirk_snapshot_continues_identically(seed):
+    """Quirk-laden books (Q2 leftovers, zero-volume makers, unusual Transactions) loaded straight
+    into a fresh engine (gome_load_books): the same snapshot, and the same MatchResults and
+    snapshot as the engine they came from after two more quirk-laden batches."""
+    rng, lit, eng, names = _run(900 + seed, quirks=True)
+    sids = [names.id("sym", s) for s in SYMBOLS]
+    snap = snapshot.redis_snapshot(eng, sids, names)
+    eng2 = Engine(max_symbols=len(SYMBOLS), max_batch=512, max_nodes=1 << 16, max_levels=1 << 14)
+    assert snapshot.load(eng2, snap, names) == eng.stats()["n_resting"]
+    assert snapshot.redis_snapshot(eng2, sids, names) == snap
+    assert eng2.stats()["n_resting"] == eng.stats()["n_resting"]
+    for k in range(2):
+        nxt = random_batches(rng, n_batches=1, batch=150, symbols=SYMBOLS, del_frac=0.25, quirks=True,
+                             oid_base=10**6 * (k + 1))
+        rec = requests_to_records(nxt[0], names)
+        eng.submit(rec)
+        a = render_events(eng.drain(), rec, names)
+        eng2.submit(rec)
+        b = render_events(eng2.drain(), rec, names)
+        assert a == b, f"batch {k}"
+    assert snapshot.redis_snapshot(eng2, sids, names) == snapshot.redis_snapshot(eng, sids, names)
+
+
+@pytest.mark.gpu
+def test_load_restores_the_q2_book_replay_refuses():
+    """The Q2 book restore() refuses (a BUY member without FIFO, depth 0) loads exactly, and a
+    later SALE at that price sees the stale member as the reference does."""
+    names = Interner()
+    names.id("sym", "eth2usdt")
+    add = dict(uuid="u1", oid="o1", symbol="eth2usdt", transaction=0, price=0.5, volume=1.0)
+    add2 = dict(uuid="u1", oid="o2", symbol="eth2usdt", transaction=1, price=0.7, volume=2.0)
+    dele = dict(add, transaction=1)
+    sale = dict(uuid="u2", oid="o3", symbol="eth2usdt", transaction=1, price=0.5, volume=0.5)
+    batches = [[(1, add), (1, add2)], [(2, dele)]]
+    lit, _ = run_batches(batches + [[(1, sale)]])
+    eng = Engine(max_symbols=1, max_batch=16, max_nodes=1 << 10, max_levels=1 << 10)
+    for b in batches:
+        eng.submit(requests_to_records(b, names))
+        eng.drain()
+    snap = snapshot.redis_snapshot(eng, [0], names)
+    eng2 = Engine(max_symbols=1, max_batch=16, max_nodes=1 << 10, max_levels=1 << 10)
+    snapshot.load(eng2, snap, names)
+    assert snapshot.redis_snapshot(eng2, [0], names) == snap
+    rec = requests_to_records([(1, sale)], names)
+    eng.submit(rec)
+    eng2.submit(rec)
+    assert render_events(eng2.drain(), rec, names) == render_events(eng.drain(), rec, names)
+    assert snapshot.redis_snapshot(eng2, [0], names) == _literal_keys(lit, ("eth2usdt",))
+
+
+class _Ids:
+    """Names for numeric workload ids (the snapshot renders every id as its decimal text)."""
+
+    def name(self, kind, i):
+        return f"{kind}{i}"
+
+    def id(self, kind, s):
+        return int(s[len(kind):])
+
+
+@pytest.mark.gpu
+def test_load_flow_books_continues_identically():
+    """Clean books deep enough for the flow path (Zipf over 40 symbols, 20k-order batches with
+    cancels): loaded into a fresh engine they take the flow path on the next batch and give the
+    same events and books as the original engine."""
+    from gome_amd import workload as wl
+    g = wl.NativeStream(40, 1.0, seed=11, del_frac=0.3, aggressive_frac=0.05)
+    mk = lambda: Engine(max_symbols=40, max_batch=20000, max_nodes=1 << 20, max_levels=1 << 16)
+    eng = mk()
+    for _ in range(2):
+        eng.submit(g.batch(20000).copy())
+        eng.drain()
+    ids = _Ids()
+    snap = snapshot.redis_snapshot(eng, range(40), ids)
+    eng2 = mk()
+    snapshot.load(eng2, snap, ids)
+    assert snapshot.redis_snapshot(eng2, range(40), ids) == snap
+    b = g.batch(20000).copy()
+    eng.submit(b)
+    e1 = eng.drain()
+    eng2.submit(b)
+    e2 = eng2.drain()
+    assert eng2.stats()["n_flow_books"] > 0
+    assert np.array_equal(e1, e2)
+    for s in range(40):
+        assert np.array_equal(eng.levels(s), eng2.levels(s))
+
+
+def test_load_images_keep_quirk_states():
+    """book_images (CPU): a member without a FIFO and a depth without nodes are kept as levels."""
+    names = Interner()
+    names.id("sym", "s")
+    snap = {"hash": {"s:depth": {"s:depth:70000000": "200000000"}},
+            "zset": {"s:BUY": {"50000000": 5e7}}}
+    (sid, lv, nd), = snapshot.book_images(snap, names)
+    assert sid == 0 and len(nd) == 0
+    assert [(int(x["price_fx"]), int(x["depth_fx"]), int(x["in_buy"]), int(x["in_sale"])) for x in lv] == \
+        [(50000000, 0, 1, 0), (70000000, 200000000, 0, 0)]

@@ -78,17 +78,23 @@ def test_bench_config2_full_batches():
 
 
 def test_bench_config4_native_stream():
-    """bench.py --workload config4 (native generator: 50% DEL, 10% aggressive), 1 Mi batches."""
-    n = 1 << 20
-    g = wl.NativeStream(100000, 1.0, seed=42, del_frac=0.5, aggressive_frac=0.1)
-    eng = Engine(max_symbols=100000, max_batch=n, max_nodes=1 << 21, max_levels=1 << 23)
+    """bench.py --workload config4 exactly (make_stream("config4", 0, 1, 42): 100k Zipf symbols,
+    50% DEL, 10% aggressive), two 4 Mi-order batches: every event vs the oracle, the hottest
+    book's cancels on the flow path (the Q plan), levels and FIFOs of the 8 head books and 100
+    random books."""
+    n = 1 << 22
+    gen, _, _ = bench.make_stream("config4", 0, 1, 42)
+    eng = Engine(max_symbols=100000, max_batch=n, max_nodes=1 << 23, max_levels=1 << 23)
     orc = Oracle(100000)
-    for i in range(3):
-        b = g.batch(n).copy()
+    for i in range(2):
+        b = gen(n).copy()
         eng.submit(b)
         _cmp(eng.drain(), orc.submit(b), f"config4 batch {i}")
-        assert eng.stats()["n_cancels"] > 10000
+        st = eng.stats()
+        assert st["n_cancels"] > 500000 and st["n_flow_cancels"] > 100000
+    g = wl.NativeStream(100000, 1.0, seed=42)
     _cmp_books(eng, orc, _hot_and_random(g.zipf, 100000), "config4")
+    assert eng.stats()["n_resting"] == orc.resting()
 
 
 def test_bench_config5_one_million_symbols():

@@ -246,3 +246,32 @@ def test_load_images_keep_quirk_states():
     assert sid == 0 and len(nd) == 0
     assert [(int(x["price_fx"]), int(x["depth_fx"]), int(x["in_buy"]), int(x["in_sale"])) for x in lv] == \
         [(50000000, 0, 1, 0), (70000000, 200000000, 0, 0)]
+
+
+@pytest.mark.gpu
+def test_load_books_rejects_bad_images():
+    """gome_load_books checks its image: a used engine (E_STATE), a repeated symbol, prices
+    out of order and node counts that do not add up (E_INVAL); nothing is loaded then."""
+    from gome_amd.workload import LEVEL_DTYPE, NODE_DTYPE
+    lv = np.zeros(2, LEVEL_DTYPE)
+    lv[0] = (10, 5, 1, 1, 0, 0)
+    lv[1] = (20, 7, 1, 0, 1, 0)
+    nd = np.zeros(2, NODE_DTYPE)
+    nd[0]["volume_fx"], nd[0]["oid_id"], nd[0]["side"] = 5, 1, 0
+    nd[1]["volume_fx"], nd[1]["oid_id"], nd[1]["side"] = 7, 2, 1
+    mk = lambda: Engine(max_symbols=4, max_batch=16, max_nodes=1 << 10, max_levels=1 << 10)
+    with pytest.raises(GomeError):
+        mk().load_books([(0, lv, nd), (0, lv, nd)])          # repeated symbol
+    with pytest.raises(GomeError):
+        mk().load_books([(0, lv[::-1].copy(), nd)])          # prices not ascending
+    with pytest.raises(GomeError):
+        mk().load_books([(0, lv, nd[:1].copy())])            # node counts do not add up
+    e = mk()
+    e.load_books([(1, lv, nd)])
+    assert e.stats()["n_resting"] == 2 and len(e.levels(1)) == 2
+    with pytest.raises(GomeError):
+        e.load_books([(2, lv, nd)])                          # not a fresh engine any more
+    used = mk()
+    used.submit(np.zeros(0, __import__("gome_amd.workload", fromlist=["ORDER_DTYPE"]).ORDER_DTYPE))
+    with pytest.raises(GomeError):
+        used.load_books([(1, lv, nd)])

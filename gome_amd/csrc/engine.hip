@@ -401,7 +401,7 @@ gome_status gome_engine::init(const gome_config& c) {
   if (!alloc(&F.tcnt, static_cast<size_t>(FL_HEAD) * F.maxt * FL_CAP, "flow head tile counts") ||
       !alloc(&F.pscr, FL_HEAD, "flow head prep scratch"))
     return GOME_E_CAPACITY;
-  // books with DELs (match_flow_cancel.h): ring images, per-position scratch, the (symbol, oid)
+  // books with DELs (match_flow_cancel.h): per-position scratch, the (symbol, oid)
   // table (generation-tagged: cleared once per 2048 batches)
   fc_hcap = next_pow2(std::max<unsigned long long>(2ull * nb, 1024));
   F.fc_hmask = fc_hcap - 1;

@@ -143,7 +143,7 @@ constexpr uint32_t DEEP_GRID_T = 128;    // blocks (per dimension) of the tail's
 // FlowHdr::fc_bad: why the cancel prep declined a book (bits; diagnostics read them)
 enum : uint32_t {
   FC_BAD_SYM = 1, FC_BAD_TABLE = 2, FC_BAD_Q7 = 4, FC_BAD_Q2 = 8, FC_BAD_LEVEL = 16, FC_BAD_UNIT = 32,
-  FC_BAD_WALK = 64, FC_BAD_RING = 128
+  FC_BAD_WALK = 64, FC_BAD_RING = 128   // FC_BAD_RING: a DEL window / the windows' sum / the segment too long
 };
 
 struct FlowLvl {
@@ -162,10 +162,10 @@ struct FlowLvl {
   uint32_t nlive0;   // old makers surviving the batch
   uint32_t mem0;     // membership at batch start
   uint32_t pad0, pad1;
-  // books with DELs (match_flow_cancel.h): targets of the level's DELs in the plan's LDS ring
+  // books with DELs (match_flow_cancel.h): the targets of the level's DELs
   uint32_t c_old;    // old (pre-batch) makers targeted by a DEL of the batch
-  uint32_t cring;    // ring entries of the level (a power of two >= every window + 1)
-  uint32_t rbase;    // first ring entry of the level (aligned to cring)
+  uint32_t cring;    // (unused)
+  uint32_t rbase;    // (unused)
   uint32_t ocan;     // cancelled volume of old makers (plan units), set by the recon
   uint32_t memf;     // deep books: membership after the batch (M_BUY / M_SALE)
   uint32_t ttot;     // targets of the level (old + new): ranks 0 .. ttot - 1
@@ -437,7 +437,7 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep(Dev D, BatchArgs B, Flo
     sum = min(sum + ws[w], FL_SUM_CAP);
   }
   if (g == 0) g = 1;
-  // (the cancel plan needs every R_k < 2^31: its ring entries carry a flag in bit 31)
+  // (the cancel plan needs every depth and Q < 2^31: its DEL path clamps with signed arithmetic)
   const bool w32 = sum < FL_SUM_CAP && sum / g < (dels ? (1ull << 31) : (1ull << 32));
   if (!w32) g = 1;
   if (dels && !w32) {  // the cancel plan is 32-bit only
@@ -761,7 +761,7 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep_b(Dev D, BatchArgs B, F
   }
   unsigned long long g = mg ? mg : 1;
   const uint32_t dels = P->dels;
-  // (the cancel plan needs every R_k < 2^31: its ring entries carry a flag in bit 31)
+  // (the cancel plan needs every depth and Q < 2^31: its DEL path clamps with signed arithmetic)
   const bool w32 = msum < FL_SUM_CAP && msum / g < (dels ? (1ull << 31) : (1ull << 32));
   if (!w32) g = 1;
   if (dels && !w32) {  // the cancel plan is 32-bit only

@@ -432,6 +432,15 @@ def main():
             "e2e": e2e,
             "cpu_baseline": cpu,
         }
+        if "k_flow_plan_head" in cands and cands["k_flow_plan_head"][0] > 0:
+            # the bound that matters: one wavefront's serial plan of the hottest book (rank 0's)
+            plan_ms = cands["k_flow_plan_head"][0]
+            bound = g_orders / steps / (plan_ms * 1e-3)
+            out["critical_path"] = {"kernel": "k_flow_plan_head", "plan_ms": round(plan_ms, 3),
+                                    "bound_orders_per_s": round(bound, 1),
+                                    "frac": round(out["value"] / bound, 4),
+                                    "note": "orders per step / the hottest book's plan time: the batch "
+                                            "cannot end before that one wavefront does"}
         if pub is not None and world > 1:
             pub.check(int(g_orders), int(g_fills), int(g_events))
             out["publisher"] = pub.summary()

@@ -282,3 +282,23 @@ def test_flow_cancel_long_windows_two_levels():
     fbk = ROUTES[-1][1]
     assert int(fbk["decline"][0]) == 0 and int(fbk["window"][0]) > 4000, _routes_msg()
     assert fb == 1 and fc > 2000
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_flow_cancel_fuzz_wide_books(seed):
+    """Wider books (up to 80 levels), heavier sweeps and more cancels: DEL targets deep in the
+    FIFO, at the cached top, partly consumed heads, old makers several batches old, and levels
+    that change side between a maker's rest and its cancel (the Q plan's dead-target case)."""
+    fz = _Fuzz(300 + seed, ns=3, nprice=40, vmax=30, p_del=0.45, p_aggr=0.15, p_q3=0.02, p_early=0.02)
+    batches = [fz.batch(int(n)) for n in np.random.default_rng(50 + seed).integers(4000, 16000, 6)]
+    eng, orc, fc, fb = _run(batches, 3)
+    assert fc > 3000, "cancels did not take the flow path; " + _routes_msg()
+
+
+def test_flow_cancel_fuzz_many_tail_books():
+    """200 symbols of a few hundred orders each per batch (all tail books, one prep block per
+    book), 10-level books with sweeps and cancels."""
+    fz = _Fuzz(400, ns=200, nprice=10, vmax=12, p_del=0.4, p_aggr=0.1)
+    batches = [fz.batch(60000) for _ in range(3)]
+    eng, orc, fc, fb = _run(batches, 200, check_every=False)
+    assert fc > 10000 and fb >= 3 * 150, _routes_msg()

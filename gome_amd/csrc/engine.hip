@@ -657,7 +657,7 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   };
   // books with DELs (match_flow_cancel.h); their events go to the arena
   auto head_recon_c = [&](const FlowArgs& R, const FlowArgs& Rc, uint32_t nb, hipStream_t st) {
-    k_fc_level_wide<<<dim3(FL_CAP, nb), 64, 0, st>>>(D, R);
+    k_fc_level_blk<<<dim3(FL_CAP, nb), FC_LVB_T, 0, st>>>(D, R);
     k_flow_toff<FL_OK_CANCEL><<<1, 1024, 0, st>>>(D, Rc);
     k_fc_count<<<1024, 256, 0, st>>>(D, B, Rc);
     k_fc_write_lv<<<dim3(FL_CAP, nb), 64, 0, st>>>(D, B, Rc);

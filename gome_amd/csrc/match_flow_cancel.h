@@ -989,6 +989,210 @@ __device__ __forceinline__ void fc_level_one(const Dev& D, const FlowArgs& F, ui
   }
 }
 
+// Block-wide exclusive scan of one int64 per thread (FC_LVB_T threads); *total = the block's sum.
+constexpr uint32_t FC_LVB_T = 1024, FC_LVB_W = FC_LVB_T / 64;
+__device__ __forceinline__ int64_t fc_blk_excl(int64_t x, int64_t* total) {
+  __shared__ int64_t ws[FC_LVB_W];
+  const uint32_t w = threadIdx.x >> 6;
+  const int64_t inc = wave_incl_scan(x);
+  if ((threadIdx.x & 63u) == 63u) ws[w] = inc;
+  __syncthreads();
+  int64_t before = 0, tot = 0;
+  for (uint32_t k = 0; k < FC_LVB_W; ++k) {
+    const int64_t v = ws[k];
+    before += k < w ? v : 0;
+    tot += v;
+  }
+  __syncthreads();  // (ws is reused by the next call)
+  *total = tot;
+  return before + inc - x;
+}
+
+// fc_level_one with a whole block (FC_LVB_T threads) on one level: the level's touches in
+// block-wide chunks (the long levels of the hottest books hold tens of thousands of touches,
+// which one wave walks 64 at a time); the old FIFO's gather stays with wave 0.
+__device__ __forceinline__ void fc_level_blk(const Dev& D, const FlowArgs& F, uint32_t h, uint32_t q) {
+  __shared__ int64_t red_s[2];
+  __shared__ uint32_t nr_s, ncan_s;
+  const FlowHdr* hd = &F.hdr[h];
+  const uint32_t tid = threadIdx.x, lane = lane_id();
+  FlowLvl* Lq = &F.lvl[h * FL_CAP + q];
+  const uint32_t beg = hd->beg;
+  const uint32_t L = FL_TOUCH_MUL * beg;
+  const unsigned long long g = static_cast<unsigned long long>(hd->g);
+  const uint32_t base = Lq->base, cnt = Lq->cnt;
+  const int64_t d0 = Lq->d0;
+  SEnt* R = F.srt + L + base;
+  RsEnt* RS = F.rs + L + base;
+  if (tid == 0) { red_s[0] = 0; nr_s = 0; ncan_s = 0; }
+  __syncthreads();
+  // 1. each cancel -> its DEL's record (r, touch); the consumption cursor before each consume
+  int64_t cc = 0, ocan = 0;
+  uint32_t nr = 0, ncan_old = 0;
+  for (uint32_t c0 = 0; c0 < cnt; c0 += FC_LVB_T) {
+    const uint32_t i = c0 + tid;
+    const bool valid = i < cnt;
+    SEnt e{};
+    if (valid) e = R[i];
+    const bool isc = valid && e.kind == TK_CONS, isx = valid && e.kind == TK_CANC;
+    if (isx) {
+      FcDel* d = &F.fc_del[beg + e.j];
+      d->r = e.amt;
+      d->ct = e.t;
+      if (d->kind == FC_OLD) { ocan += e.amt; ncan_old++; }
+    }
+    int64_t tot;
+    const int64_t ex = fc_blk_excl(isc ? e.amt : 0, &tot);
+    if (isc) R[i].coord = cc + ex;
+    cc += tot;
+    nr += valid && e.kind == TK_REST ? 1u : 0u;
+  }
+  if (ocan) atomicAdd(reinterpret_cast<unsigned long long*>(&red_s[0]), static_cast<unsigned long long>(ocan));
+  if (nr) atomicAdd(&nr_s, nr);
+  if (ncan_old) atomicAdd(&ncan_s, ncan_old);
+  __threadfence();  // the DEL records are read back below (by other threads)
+  __syncthreads();
+  const int64_t ocan_t = red_s[0];
+  const int64_t cfin = cc;
+  const int64_t base_new = d0 - ocan_t;
+  // 2. the new makers in FIFO (rest) order, their consumption-space starts and cancels
+  int64_t acc = base_new;
+  uint32_t k = 0;
+  for (uint32_t c0 = 0; c0 < cnt; c0 += FC_LVB_T) {
+    const uint32_t i = c0 + tid;
+    const bool valid = i < cnt;
+    SEnt e{};
+    if (valid) e = R[i];
+    const bool isr = valid && e.kind == TK_REST;
+    uint32_t ct = NIL;
+    int64_t len = 0;
+    if (isr) {
+      len = e.amt;
+      const uint32_t tg = F.fc_tg[beg + e.j];
+      if (tg) {
+        const FcDel d = F.fc_del[tg - 1u];
+        if (d.ct != NIL) { ct = d.ct; len = e.amt - d.r; }
+      }
+    }
+    int64_t tot, ntot;
+    const int64_t ex = fc_blk_excl(len, &tot);
+    const int64_t rk = fc_blk_excl(isr ? 1 : 0, &ntot);
+    if (isr) {
+      RsEnt x;
+      x.e = acc + ex;
+      x.v = e.amt;
+      x.j = e.j;
+      x.t = e.t;
+      x.pad0 = ct;
+      x.pad1 = 0;
+      RS[k + static_cast<uint32_t>(rk)] = x;
+    }
+    acc += tot;
+    k += static_cast<uint32_t>(ntot);
+  }
+  const int64_t qend = acc;
+  // 3. the old FIFO (wave 0), as fc_level_one
+  if (tid >= 64) return;
+  const unsigned long long ltm = lt_mask();
+  const uint32_t nv0 = Lq->nv0, tail = Lq->tail, tslot = Lq->tslot;
+  uint32_t head = Lq->head, hslot = Lq->hslot;
+  uint32_t ttail = tail, ttslot = tslot;
+  uint32_t ig_base = 0, ng = 0, consumed = 0;
+  bool ig_all = true;
+  if (nv0 > 0 && (cfin > 0 || Lq->c_old)) {
+    uint32_t bb = 0;
+    if (lane == 0) bb = atomicAdd(F.ig_bump, nv0);
+    ig_base = uni(bb);
+    if (static_cast<unsigned long long>(ig_base) + nv0 > F.ig_cap) {
+      if (lane == 0) atomicOr(&D.st->err, ERR_CHUNKS);
+      return;
+    }
+    IgEnt* IG = F.ig + ig_base;
+    int64_t E = 0;
+    bool have_surv = false, stop = false;
+    uint32_t c = head, s0 = hslot, nh = NIL, nhs = 0;
+    for (uint32_t guard = 0; c != NIL && !stop; ++guard) {
+      if (guard > D.ch_cap) { if (lane == 0) atomicOr(&D.st->err, ERR_CORRUPT); return; }
+      const uint32_t lim = (c == tail) ? tslot : CH;
+      const bool inr = lane < CH && lane >= s0 && lane < lim;
+      Node nd{};
+      if (inr) nd = D.nodes[c * CH + lane];
+      const bool live = inr && nd.rem >= 0;
+      const bool targ = live && nd.pad != 0;
+      uint32_t ct = NIL;
+      int64_t len = live ? nd.rem : 0;
+      if (targ) {
+        const FcDel d = F.fc_del[static_cast<uint32_t>(nd.pad) - 1u];
+        if (d.ct != NIL) { ct = d.ct; len = nd.rem - d.r; }
+      }
+      const int64_t inc = wave_incl_scan(len);
+      const int64_t em = E + inc - len;
+      const unsigned long long after = __ballot(live && em >= cfin && !targ);
+      const uint32_t fb = after ? static_cast<uint32_t>(__builtin_ctzll(after)) : 64u;
+      const bool take = live && lane <= fb;
+      const unsigned long long tm = __ballot(take);
+      if (take) {
+        IgEnt gq;
+        gq.e = em;
+        gq.v = nd.rem;
+        gq.oid = nd.oid;
+        gq.uuid = nd.uuid;
+        gq.tx = nd.tx;
+        gq.pad = ct;
+        IG[ng + __popcll(tm & ltm)] = gq;
+      }
+      ng += __popcll(tm);
+      const bool cons = live && ct == NIL && em + nd.rem <= cfin;
+      if (cons) __hip_atomic_store(&D.idx[nd.ixs].key, KEY_TOMB, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      consumed += __popcll(__ballot(cons));
+      if (!have_surv) {
+        const unsigned long long sv = __ballot(live && ct == NIL && em + nd.rem > cfin);
+        if (sv) {
+          have_surv = true;
+          nh = c;
+          nhs = static_cast<uint32_t>(__builtin_ctzll(sv));
+          if (lane == nhs && em < cfin) D.nodes[c * CH + lane].rem = em + nd.rem - cfin;  // partial head
+        } else {
+          if (lane == 0) D.freed_ids[atomicAdd(&D.st->freed_top, 1u)] = c;
+        }
+      }
+      if (after) { stop = true; ig_all = false; }
+      E += rl64(inc, 63);
+      c = (c == tail) ? NIL : uni(D.chdr[c].next);
+      s0 = 0;
+    }
+    if (!have_surv && ig_all) {
+      head = ttail = NIL;
+      hslot = ttslot = 0;
+    } else if (have_surv) {
+      head = nh;
+      hslot = nhs;
+    }
+  }
+  if (lane == 0) {
+    Lq->cfin = cfin;
+    Lq->nrest = nr_s;
+    Lq->ig_base = ig_base;
+    Lq->ig_n = ng;
+    Lq->ig_all = ig_all ? 1u : 0u;
+    Lq->head = head;
+    Lq->tail = ttail;
+    Lq->hslot = hslot;
+    Lq->tslot = ttslot;
+    Lq->nlive0 = nv0 - consumed - ncan_s;
+    Lq->ocan = static_cast<uint32_t>(static_cast<uint64_t>(ocan_t) / g);
+    Lq->pad0 = static_cast<uint32_t>(static_cast<uint64_t>(qend));
+    Lq->pad1 = static_cast<uint32_t>(static_cast<uint64_t>(qend) >> 32);
+  }
+}
+
+// The head books' levels: a block per (book, level).
+__global__ __launch_bounds__(FC_LVB_T) void k_fc_level_blk(Dev D, FlowArgs F) {
+  const uint32_t h = F.h0 + blockIdx.y, q = blockIdx.x;
+  if (h >= fl_hend(D, F) || !fc_book(F, h) || q == 0 || q > F.hdr[h].nl) return;
+  fc_level_blk(D, F, h, q);
+}
+
 __global__ __launch_bounds__(64) void k_fc_level_wide(Dev D, FlowArgs F) {
   const uint32_t h = F.h0 + blockIdx.y, q = blockIdx.x;
   if (h >= fl_hend(D, F) || !fc_book(F, h) || q == 0 || q > F.hdr[h].nl) return;

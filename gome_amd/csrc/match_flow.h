@@ -593,7 +593,10 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep_a(Dev D, BatchArgs B, F
   __syncthreads();
   unsigned long long mg = 0, msum = 0;
   uint32_t my_adds = 0, my_drop = 0, my_bad = 0, my_dels = 0, my_many = 0;
-  for (uint32_t c0 = b0 + tid; c0 < b1 && !my_bad && !my_many; c0 += 4 * FL_PREP_T) {
+  // (every thread stops once the block's distinct prices overflowed: a deep candidate, whose
+  // own prep starts over)
+  for (uint32_t c0 = b0 + tid; c0 < b1 && !my_bad && !my_many && *reinterpret_cast<volatile uint32_t*>(&ndist) <= FL_MAX;
+       c0 += 4 * FL_PREP_T) {
     Prep qs[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {

@@ -31,6 +31,9 @@
 #include <vector>
 
 #include "../../include/gome/gome_abi.h"
+#ifdef GOME_ROCPRIM_SORT
+#include <rocprim/rocprim.hpp>
+#endif
 #include "device.h"
 #include "match_cold.h"
 #include "match_flow.h"
@@ -178,6 +181,8 @@ struct gome_engine {
   unsigned long long idx_cap = 0;
   // batch buffers
   uint32_t *d_k0 = nullptr, *d_v0 = nullptr, *d_k1 = nullptr, *d_v1 = nullptr;
+  unsigned char* d_rp_tmp = nullptr;  // GOME_ROCPRIM_SORT: rocPRIM's radix-sort scratch
+  size_t rp_bytes = 0;
   uint32_t* d_hist = nullptr;
   uint32_t* d_bsum = nullptr;
   uint32_t* d_tmp = nullptr;  // flags / segpos (n)
@@ -381,6 +386,10 @@ gome_status gome_engine::init(const gome_config& c) {
       !alloc(&d_prep, nb, "prep") || !alloc(&d_pend, nb, "pending inserts") ||
       !alloc(&d_resume, MAX_HOT, "resume records") || !alloc(&d_arena, arena_cap, "event arena"))
     return GOME_E_CAPACITY;
+#ifdef GOME_ROCPRIM_SORT
+  HIPCHK(rocprim::radix_sort_pairs(nullptr, rp_bytes, d_k1, d_k0, d_v1, d_v0, static_cast<size_t>(nb), 0u, key_bits, stream));
+  if (!alloc(&d_rp_tmp, rp_bytes, "radix sort scratch")) return GOME_E_CAPACITY;
+#endif
   for (Slot& S : slots) {
     if (!alloc(&S.d_orders, nb, "orders") || !alloc(&S.d_events, arena_cap, "events")) return GOME_E_CAPACITY;
     S.ev_cap = arena_cap;
@@ -500,6 +509,12 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   HIPCHK(hipEventRecord(adm_done, flow_stream));
 
   // ---- stable radix sort of (symbol_id, seq)
+#ifdef GOME_ROCPRIM_SORT
+  k_sort_keys<<<gN, T256, 0, s>>>(d_ord, n, d_k1, d_v1);
+  HIPCHK(rocprim::radix_sort_pairs(d_rp_tmp, rp_bytes, d_k1, d_k0, d_v1, d_v0, static_cast<size_t>(n), 0u, key_bits, s));
+  const uint32_t* skeys = d_k0;
+  const uint32_t* sidx = d_v0;
+#else
   const uint32_t nblk = ceil_div(n, RS_TILE);
   uint32_t *kin = nullptr, *vin = nullptr, *kout = d_k0, *vout = d_v0;
   for (uint32_t p = 0; p < passes; ++p) {
@@ -523,6 +538,7 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   }
   const uint32_t* skeys = kin;
   const uint32_t* sidx = vin;
+#endif
 
   // ---- segments (one per symbol present), longest first
   k_seg_flags<<<gN, T256, 0, s>>>(skeys, n, d_tmp);

@@ -86,6 +86,15 @@ __device__ __forceinline__ uint32_t rs_key(const gome_order* ord, const uint32_t
   return FROM_ORD ? ord[i].symbol_id : keys[i];
 }
 
+// (GOME_ROCPRIM_SORT) keys = symbol ids, values = record indices, for rocPRIM's radix sort
+__global__ __launch_bounds__(256) void k_sort_keys(const gome_order* ord, uint32_t n, uint32_t* keys, uint32_t* vals) {
+  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+  if (i < n) {
+    keys[i] = ord[i].symbol_id;
+    vals[i] = i;
+  }
+}
+
 template <bool FROM_ORD>
 __global__ __launch_bounds__(RS_T) void k_radix_hist(const gome_order* ord, const uint32_t* keys,
                                                      uint32_t n, uint32_t shift, uint32_t bits,

@@ -563,6 +563,33 @@ __device__ __forceinline__ uint32_t fl_set_put(KeyPtr keys, unsigned long long k
   return FL_HASH;
 }
 
+// fl_set_put for k_flow_prep_a's per-block sets, which only ever need FL_MAX + 1 keys: a probe
+// chain longer than FL_PUT_PROBES counts as an overflow (FL_HASH), as does a block whose distinct
+// count already passed FL_MAX.  A deep book fills the table with ~FL_HASH keys in its first
+// round of inserts, and unbounded linear probing in that full table cost ~0.7 ms per batch.
+// (A false overflow only sends a shallow book to the deep candidates: still exact.)
+constexpr uint32_t FL_PUT_PROBES = 32;
+__device__ __forceinline__ uint32_t fl_set_put_small(unsigned long long* keys, const uint32_t* ndist,
+                                                     unsigned long long key, bool* fresh) {
+  uint32_t s = fl_hash(key);
+  *fresh = false;
+  for (uint32_t probe = 0; probe < FL_PUT_PROBES; ++probe) {
+    if (*reinterpret_cast<const volatile uint32_t*>(ndist) > FL_MAX) return FL_HASH;
+    const unsigned long long cur = *reinterpret_cast<volatile unsigned long long*>(&keys[s]);
+    if (cur == key) return s;
+    if (cur == 0ull) {
+      const unsigned long long prev = atomicCAS(&keys[s], 0ull, key);
+      if (prev == 0ull) {
+        *fresh = true;
+        return s;
+      }
+      if (prev == key) return s;
+    }
+    s = (s + 1) & (FL_HASH - 1);
+  }
+  return FL_HASH;
+}
+
 __device__ __forceinline__ void fl_block_gcd_sum(unsigned long long& mg, unsigned long long& msum,
                                                  unsigned long long* wg, unsigned long long* ws) {
   for (int off = 32; off > 0; off >>= 1) {
@@ -617,7 +644,7 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep_a(Dev D, BatchArgs B, F
       if (mg == 0 || static_cast<unsigned long long>(qd) * mg != v) mg = fl_gcd(mg, v);
       msum = min(msum + v, FL_SUM_CAP);
       bool fresh;
-      const uint32_t sl = fl_set_put(hkey, static_cast<unsigned long long>(q.price) + FL_KEY_OFF, &fresh);
+      const uint32_t sl = fl_set_put_small(hkey, &ndist, static_cast<unsigned long long>(q.price) + FL_KEY_OFF, &fresh);
       if (sl == FL_HASH || (fresh && atomicAdd(&ndist, 1u) >= FL_MAX)) { my_many = 1; break; }
     }
   }

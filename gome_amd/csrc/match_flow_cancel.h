@@ -412,21 +412,32 @@ __device__ __forceinline__ void fc_put_va(const FlowArgs& F, uint32_t b, bool tg
   if (del) F.fc_del[b].va = va;
 }
 
-// Q of the DEL at b (see above) and its W32C record.
-__device__ __forceinline__ unsigned long long fc_del_rec(const FlowArgs& F, const FlowHdr& hd, const FlowLvl* LV,
-                                                         uint32_t b, const FcDel& d, bool sale) {
-  const uint32_t k = d.li;
-  const uint32_t* dt = F.fc_dt + hd.beg + LV[k].tbase;
-  const uint32_t* tv = F.fc_tv + hd.beg + LV[k].tbase;
+// C of the DEL at b: the volume of its window's side-s targets cancelled before it.
+__device__ __forceinline__ uint32_t fc_del_c(const FlowArgs& F, const FlowHdr& hd, const FlowLvl* LV, uint32_t b,
+                                             const FcDel& d, bool sale, uint32_t x0 = 1, uint32_t dx = 1) {
+  const uint32_t* dt = F.fc_dt + hd.beg + LV[d.li].tbase;
+  const uint32_t* tv = F.fc_tv + hd.beg + LV[d.li].tbase;
   uint32_t c = 0;
-  for (uint32_t x = d.rank + 1; x <= d.rank + d.nb; ++x) {
+  for (uint32_t x = d.rank + x0; x <= d.rank + d.nb; x += dx) {
     const uint32_t t = tv[x];
     if ((t >> 31) == (sale ? 1u : 0u) && dt[x] < b) c += t & 0x7FFFFFFFu;
   }
+  return c;
+}
+
+// Q of the DEL at b (see above, C given) and its W32C record.
+__device__ __forceinline__ unsigned long long fc_del_rec_c(const FlowHdr& hd, const FlowLvl* LV, const FcDel& d,
+                                                           bool sale, uint32_t c) {
+  const uint32_t k = d.li;
   const uint32_t d0 = static_cast<uint32_t>(static_cast<unsigned long long>(LV[k].d0) / hd.g);
   const uint32_t q = (d.kind == FC_OLD ? d0 - d.oend : 0u - d.oend) + d.va - c;
   const uint32_t hi = k | (d.ov << 7) | (1u << 30) | (sale ? 0x80000000u : 0u);
   return (static_cast<unsigned long long>(hi) << 32) | q;
+}
+
+__device__ __forceinline__ unsigned long long fc_del_rec(const FlowArgs& F, const FlowHdr& hd, const FlowLvl* LV,
+                                                         uint32_t b, const FcDel& d, bool sale) {
+  return fc_del_rec_c(hd, LV, d, sale, fc_del_c(F, hd, LV, b, d, sale));
 }
 
 // A DEL's window and its target's DEL time / volume by rank (both prep paths).
@@ -724,10 +735,39 @@ __global__ __launch_bounds__(256) void k_fc_precs(Dev D, BatchArgs B, FlowArgs F
   const FlowLvl* LV = F.lvl + h * FL_CAP;
   uint32_t b0, b1;
   fc_slice(hd, blockIdx.x, gridDim.x, b0, b1);
-  for (uint32_t b = b0 + threadIdx.x; b < b1; b += blockDim.x) {
-    if (prep_at(B, b).action != GOME_DEL) continue;
-    const FcDel d = F.fc_del[b];
-    if (d.kind != FC_NONE) F.ord8[hd.obase + (b - hd.beg)] = fc_del_rec(F, hd, LV, b, d, prep_at(B, b).side == GOME_SALE);
+  const uint32_t lane = lane_id();
+  // a DEL with a short window loops over it alone; the wave shares the long ones (the
+  // hottest books' busiest levels hold thousands of targets)
+  for (uint32_t bw = b0 + (threadIdx.x & ~63u); bw < b1; bw += blockDim.x) {
+    const uint32_t b = bw + lane;
+    FcDel d{};
+    bool isd = false, sale = false;
+    if (b < b1) {
+      const Prep q = prep_at(B, b);
+      if (q.action == GOME_DEL) {
+        d = F.fc_del[b];
+        isd = d.kind != FC_NONE;
+        sale = q.side == GOME_SALE;
+      }
+    }
+    const bool longw = isd && d.nb > 32;
+    if (isd && !longw) F.ord8[hd.obase + (b - hd.beg)] = fc_del_rec(F, hd, LV, b, d, sale);
+    for (unsigned long long lm = __ballot(longw); lm; lm &= lm - 1) {
+      const uint32_t src = static_cast<uint32_t>(__builtin_ctzll(lm));
+      FcDel ds{};
+      ds.kind = __shfl(d.kind, src);
+      ds.li = __shfl(d.li, src);
+      ds.rank = __shfl(d.rank, src);
+      ds.nb = __shfl(d.nb, src);
+      ds.oend = __shfl(d.oend, src);
+      ds.ov = __shfl(d.ov, src);
+      ds.va = __shfl(d.va, src);
+      const uint32_t bs = __shfl(b, src);
+      const bool ss = __shfl(sale ? 1u : 0u, src) != 0u;
+      uint32_t c = fc_del_c(F, hd, LV, bs, ds, ss, 1u + lane, 64u);
+      for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off);
+      if (lane == src) F.ord8[hd.obase + (bs - hd.beg)] = fc_del_rec_c(hd, LV, ds, ss, c);
+    }
   }
 }
 

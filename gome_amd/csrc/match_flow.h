@@ -1301,9 +1301,69 @@ __global__ __launch_bounds__(FL_SORT_T) void k_flow_sort(Dev D, FlowArgs F) {
 // resting FIFO.
 // (run_base / run_cnt: the level's run when the caller found it, deep books; else FlowLvl's.
 // ig_pre: the level's gathered-maker space when the caller claimed it, else claimed here.)
+// Block-wide exclusive scan of one int64 per thread (FL_LVB_T threads); *total = the block's sum.
+constexpr uint32_t FL_LVB_T = 1024, FL_LVB_W = FL_LVB_T / 64;
+__device__ __forceinline__ int64_t fl_blk_excl(int64_t x, int64_t* total) {
+  __shared__ int64_t ws[FL_LVB_W];
+  const uint32_t w = threadIdx.x >> 6;
+  const int64_t inc = wave_incl_scan(x);
+  if ((threadIdx.x & 63u) == 63u) ws[w] = inc;
+  __syncthreads();
+  int64_t before = 0, tot = 0;
+  for (uint32_t k = 0; k < FL_LVB_W; ++k) {
+    const int64_t v = ws[k];
+    before += k < w ? v : 0;
+    tot += v;
+  }
+  __syncthreads();  // (ws is reused by the next call)
+  *total = tot;
+  return before + inc - x;
+}
+
+// fl_level_one's touch scan with a whole block (FL_LVB_T threads) on one level: the level's
+// touches in block-wide chunks (the hottest book's levels hold thousands of touches).
+__device__ __forceinline__ void fl_level_scan_blk(const FlowArgs& F, uint32_t h, uint32_t q, int64_t& cfin,
+                                                  uint32_t& nr) {
+  const FlowHdr* hd = &F.hdr[h];
+  FlowLvl* Lq = fl_lvls(F, h) + q;
+  const uint32_t L = FL_TOUCH_MUL * hd->beg, base = Lq->base, cnt = Lq->cnt;
+  SEnt* R = F.srt + L + base;
+  RsEnt* RS = F.rs + L + base;
+  int64_t cc = 0, rr = Lq->d0;
+  uint32_t n = 0;
+  for (uint32_t c0 = 0; c0 < cnt; c0 += FL_LVB_T) {
+    const uint32_t i = c0 + threadIdx.x;
+    const bool valid = i < cnt;
+    SEnt e{};
+    if (valid) e = R[i];
+    const bool isc = valid && e.kind == TK_CONS, isr = valid && e.kind == TK_REST;
+    int64_t tc, tr, tn;
+    const int64_t xc = fl_blk_excl(isc ? e.amt : 0, &tc);
+    const int64_t xr = fl_blk_excl(isr ? e.amt : 0, &tr);
+    const int64_t xn = fl_blk_excl(isr ? 1 : 0, &tn);
+    if (isc) R[i].coord = cc + xc;
+    if (isr) {
+      const int64_t e0 = rr + xr;
+      R[i].coord = e0;
+      RsEnt x;
+      x.e = e0;
+      x.v = e.amt;
+      x.j = e.j;
+      x.t = e.t;
+      x.pad0 = x.pad1 = 0;
+      RS[n + static_cast<uint32_t>(xn)] = x;
+    }
+    cc += tc;
+    rr += tr;
+    n += static_cast<uint32_t>(tn);
+  }
+  cfin = cc;
+  nr = n;
+}
+
 __device__ __forceinline__ void fl_level_one(const Dev& D, const FlowArgs& F, uint32_t h, uint32_t q,
                                              uint32_t run_base = NIL, uint32_t run_cnt = 0,
-                                             uint32_t ig_pre = NIL) {
+                                             uint32_t ig_pre = NIL, int64_t pre_cfin = -1, uint32_t pre_nr = 0) {
   const FlowHdr* hd = &F.hdr[h];
   const uint32_t lane = lane_id();
   FlowLvl* Lq = fl_lvls(F, h) + q;
@@ -1315,7 +1375,11 @@ __device__ __forceinline__ void fl_level_one(const Dev& D, const FlowArgs& F, ui
   int64_t cc = 0, rr = d0;
   uint32_t nr = 0;
   const unsigned long long ltm = lt_mask();
-  for (uint32_t c0 = 0; c0 < cnt; c0 += 64) {
+  if (pre_cfin >= 0) {  // (the touch scan ran block-wide: fl_level_scan_blk)
+    cc = pre_cfin;
+    nr = pre_nr;
+  }
+  for (uint32_t c0 = 0; pre_cfin < 0 && c0 < cnt; c0 += 64) {
     const uint32_t i = c0 + lane;
     const bool valid = i < cnt;
     SEnt e{};
@@ -2111,11 +2175,14 @@ __global__ __launch_bounds__(FL_TILE) void k_flow_sort_scatter(Dev D, FlowArgs F
   }
 }
 
-__global__ __launch_bounds__(64) void k_flow_level_wide(Dev D, FlowArgs F) {
+__global__ __launch_bounds__(FL_LVB_T) void k_flow_level_wide(Dev D, FlowArgs F) {
   const uint32_t h = F.h0 + blockIdx.y, q = blockIdx.x;
   if (h >= fl_hend(D, F) || F.hdr[h].ok != FL_OK_ADD) return;
   if (q == 0 || q > F.hdr[h].nl) return;
-  fl_level_one(D, F, h, q);
+  int64_t cfin;
+  uint32_t nr;
+  fl_level_scan_blk(F, h, q, cfin, nr);
+  if (threadIdx.x < 64) fl_level_one(D, F, h, q, NIL, 0, NIL, cfin, nr);
 }
 
 }  // namespace gome

@@ -1029,24 +1029,7 @@ __device__ __forceinline__ void fc_level_one(const Dev& D, const FlowArgs& F, ui
   }
 }
 
-// Block-wide exclusive scan of one int64 per thread (FC_LVB_T threads); *total = the block's sum.
-constexpr uint32_t FC_LVB_T = 1024, FC_LVB_W = FC_LVB_T / 64;
-__device__ __forceinline__ int64_t fc_blk_excl(int64_t x, int64_t* total) {
-  __shared__ int64_t ws[FC_LVB_W];
-  const uint32_t w = threadIdx.x >> 6;
-  const int64_t inc = wave_incl_scan(x);
-  if ((threadIdx.x & 63u) == 63u) ws[w] = inc;
-  __syncthreads();
-  int64_t before = 0, tot = 0;
-  for (uint32_t k = 0; k < FC_LVB_W; ++k) {
-    const int64_t v = ws[k];
-    before += k < w ? v : 0;
-    tot += v;
-  }
-  __syncthreads();  // (ws is reused by the next call)
-  *total = tot;
-  return before + inc - x;
-}
+constexpr uint32_t FC_LVB_T = FL_LVB_T;
 
 // fc_level_one with a whole block (FC_LVB_T threads) on one level: the level's touches in
 // block-wide chunks (the long levels of the hottest books hold tens of thousands of touches,
@@ -1082,7 +1065,7 @@ __device__ __forceinline__ void fc_level_blk(const Dev& D, const FlowArgs& F, ui
       if (d->kind == FC_OLD) { ocan += e.amt; ncan_old++; }
     }
     int64_t tot;
-    const int64_t ex = fc_blk_excl(isc ? e.amt : 0, &tot);
+    const int64_t ex = fl_blk_excl(isc ? e.amt : 0, &tot);
     if (isc) R[i].coord = cc + ex;
     cc += tot;
     nr += valid && e.kind == TK_REST ? 1u : 0u;
@@ -1115,8 +1098,8 @@ __device__ __forceinline__ void fc_level_blk(const Dev& D, const FlowArgs& F, ui
       }
     }
     int64_t tot, ntot;
-    const int64_t ex = fc_blk_excl(len, &tot);
-    const int64_t rk = fc_blk_excl(isr ? 1 : 0, &ntot);
+    const int64_t ex = fl_blk_excl(len, &tot);
+    const int64_t rk = fl_blk_excl(isr ? 1 : 0, &ntot);
     if (isr) {
       RsEnt x;
       x.e = acc + ex;

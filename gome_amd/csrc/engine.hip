@@ -1257,6 +1257,7 @@ gome_status gome_engine::load_books(size_t nb, const uint32_t* bsym, const uint3
   }
   if (ni != nn) return fail(GOME_E_INVAL, "gome_load_books: n_nodes differs from the levels' node counts");
   if (occ.size() > idx_cap / 2) return fail(GOME_E_CAPACITY, "gome_load_books: cancel index over half full");
+  used = true;  // (from here on the pools are written: no second attempt on this engine)
   hipStream_t s = stream;
   const uint32_t nch = static_cast<uint32_t>(chdr.size()), nl = static_cast<uint32_t>(lvl.size());
   if (nl) HIPCHK(hipMemcpyAsync(D.lvl, lvl.data(), nl * sizeof(Level), hipMemcpyHostToDevice, s));

@@ -10,11 +10,11 @@ from tests.test_gpu_flow_cancel import _Fuzz  # noqa: E402
 
 HDR = np.dtype([("ok", "<u4"), ("nl", "<u4"), ("sym", "<u4"), ("ntouch", "<u4"), ("beg", "<u4"), ("end", "<u4"),
                 ("nold", "<u4"), ("adds", "<u4"), ("dropped", "<u4"), ("rests", "<u4"), ("obase", "<u4"),
-                ("w32", "<u4"), ("amask", "<u8", 2), ("bmask", "<u8", 2), ("g", "<u8"), ("fc_img", "<u4"), ("fc_big", "<u4"),
-                ("ndel", "<u4"), ("nslot", "<u4"), ("ncancel", "<u4"), ("fc_bad", "<u4"),
-                ("deep", "<u4"), ("dslot", "<u4"), ("pad3", "<u4", 2)])
+                ("w32", "<u4"), ("amask", "<u8", 2), ("bmask", "<u8", 2), ("g", "<u8"),
+                ("ndel", "<u4"), ("ncancel", "<u4"), ("fc_bad", "<u4"),
+                ("deep", "<u4"), ("dslot", "<u4"), ("nbsum", "<u4"), ("pad3", "<u4", 4)])
 FCDEL = np.dtype([("kind", "<u4"), ("li", "<u4"), ("tgt", "<u4"), ("rank", "<u4"), ("nb", "<u4"), ("ixs", "<u4"),
-                  ("oend", "<u4"), ("ov", "<u4"), ("r", "<i8"), ("ct", "<u4"), ("pad", "<u4")])
+                  ("oend", "<u4"), ("ov", "<u4"), ("r", "<i8"), ("ct", "<u4"), ("va", "<u4")])
 assert HDR.itemsize == 128 and FCDEL.itemsize == 48
 
 ns = int(sys.argv[1]) if len(sys.argv) > 1 else 40
@@ -38,7 +38,7 @@ for bi in range(3):
         rk = np.frombuffer(eng.debug_peek(3, 4 * beg, 4 * (end - beg)), "<u4")
         tg = np.frombuffer(eng.debug_peek(4, 4 * beg, 4 * (end - beg)), "<u4")
         seg = b[b["symbol_id"] == x["sym"]]
-        print(f"  book h={h} sym={x['sym']} n={end - beg} ndel={x['ndel']} bad={x['fc_bad']} ring={x['nslot']} "
+        print(f"  book h={h} sym={x['sym']} n={end - beg} ndel={x['ndel']} bad={x['fc_bad']} wsum={x['nbsum']} "
               f"win={x['ncancel']} g={x['g']}")
         isdel = seg["action"] == 2
         for i in np.nonzero(isdel & (d["kind"] != 0))[0][:400]:

@@ -20,7 +20,7 @@ for bi in range(int(sys.argv[2]) if len(sys.argv) > 2 else 4):
     allb = eng.debug_flow_books()
     bad = allb[allb["kind"] == 0]
     print(f"   declined candidates: {len(bad)} of {len(allb)}; orders {int(bad['orders'].sum())}; "
-          f"reasons {np.unique(bad['decline'], return_counts=True)}; biggest {bad[np.argsort(-bad['orders'].astype(np.int64))][:3][['orders','dels','levels','ring','window','w32','decline']].tolist()}")
+          f"reasons {np.unique(bad['decline'], return_counts=True)}; biggest {bad[np.argsort(-bad['orders'].astype(np.int64))][:3][['orders','dels','levels','wsum','window','w32','decline']].tolist()}")
     fb = allb[:8]
     hdr = np.frombuffer(eng.debug_peek(0, 0, HDR.itemsize * len(fb)), HDR)
     x = hdr[0]
@@ -34,7 +34,7 @@ for bi in range(int(sys.argv[2]) if len(sys.argv) > 2 else 4):
     nb = eff["nb"].astype(np.int64)
     print(f"batch {bi}: plan {st['ms_flow_plan']:.2f} ms, hot n={end - beg} dels={int(isdel.sum())} "
           f"effective={len(eff)} (new {int((eff['kind'] == 1).sum())}, old {int((eff['kind'] == 2).sum())}) "
-          f"cancels={int((eff['ct'] != 0xFFFFFFFF).sum())} levels={x['nl']} ring={x['nslot']} maxwin={x['ncancel']}")
+          f"cancels={int((eff['ct'] != 0xFFFFFFFF).sum())} levels={x['nl']} wsum={x['nbsum']} maxwin={x['ncancel']}")
     if len(nb):
         q = np.percentile(nb, [50, 90, 99, 100])
         print(f"   window n_b p50 {q[0]:.0f} p90 {q[1]:.0f} p99 {q[2]:.0f} max {q[3]:.0f}; >63: {float((nb > 63).mean()):.3f}"

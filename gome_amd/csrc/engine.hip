@@ -667,7 +667,7 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
     k_flow_level_wide<<<dim3(FL_CAP, nb), FL_LVB_T, 0, st>>>(D, R);
     k_flow_toff<FL_OK_ADD><<<1, 1024, 0, st>>>(D, R);
     k_flow_count<<<1024, 256, 0, st>>>(D, B, R);
-    k_flow_write_lv<<<dim3(FL_CAP, nb), 64, 0, st>>>(D, B, R);
+    k_flow_write_lv_blk<<<dim3(FL_CAP, nb), FL_LVB_T, 0, st>>>(D, B, R);
     k_flow_write_fin<<<nb, 128, 0, st>>>(D, R);
     deep_write(R, st);
   };

@@ -2002,14 +2002,118 @@ __global__ __launch_bounds__(FL_WRITE_T) void k_flow_write(Dev D, BatchArgs B, F
   fl_write_finish(D, hd, lv, keep, base_s, cap_s, nout_s);
 }
 
-// Head books: one wave per (book, level) writes its FIFO and stores its final record ...
-__global__ __launch_bounds__(64) void k_flow_write_lv(Dev D, BatchArgs B, FlowArgs F) {
-  const uint32_t h = F.h0 + blockIdx.y, q = blockIdx.x;
+// Head books: fl_write_level with a whole block (FL_LVB_T threads) per (book, level) -- the chunk
+// headers and the surviving new makers (thousands on the hottest book's levels) in block-wide
+// strides -- storing the level's final record ...
+__global__ __launch_bounds__(FL_LVB_T) void k_flow_write_lv_blk(Dev D, BatchArgs B, FlowArgs F) {
+  __shared__ int t_s;
+  __shared__ uint32_t nst_s, bb_s, bad_s;
+  const uint32_t h = F.h0 + blockIdx.y, q = blockIdx.x, tid = threadIdx.x;
   if (h >= fl_hend(D, F) || F.hdr[h].ok != FL_OK_ADD) return;
   const FlowHdr hd = F.hdr[h];
   if (q == 0 || q > hd.nl) return;
-  const Level x = fl_write_level(D, B, F, hd, h, q);
-  if (lane_id() == 0) F.lvout[h * FL_CAP + q] = x;
+  const uint32_t L = FL_TOUCH_MUL * hd.beg;
+  const unsigned long long mask = D.idx_mask;
+  const FlowLvl f = fl_lvls(F, h)[q];
+  const RsEnt* RS = F.rs + L + f.base;
+  const FlWPlan wp = fl_wplan(f, RS);
+  const uint32_t rf = wp.rf, S = wp.S, s0 = wp.s0, room = wp.room, need = wp.need;
+  const bool fresh = wp.fresh;
+  if (tid == 0) {  // claim `need` chunk ids: free stack first, then the bump pointer
+    int t = 0;
+    uint32_t nst = 0, bb = 0;
+    if (need) {
+      t = atomicSub(&D.st->free_top, static_cast<int>(need));
+      nst = static_cast<uint32_t>(min(max(t, 0), static_cast<int>(need)));
+      if (nst < need) bb = atomicAdd(D.ch_bump, need - nst);
+    }
+    t_s = t;
+    nst_s = nst;
+    bb_s = bb;
+    bad_s = need && bb + (need - nst) > D.ch_cap ? 1u : 0u;
+    if (bad_s) atomicOr(&D.st->err, ERR_CHUNKS);
+  }
+  __syncthreads();
+  if (bad_s) {
+    if (tid == 0) {
+      Level x{};
+      x.price = f.price;
+      x.head = x.tail = NIL;
+      F.lvout[h * FL_CAP + q] = x;
+    }
+    return;
+  }
+  const int t = t_s;
+  const uint32_t nst = nst_s, bb = bb_s;
+  auto chunk_id = [&](uint32_t i) -> uint32_t {
+    return i < nst ? D.free_ids[t - static_cast<int>(nst) + static_cast<int>(i)] : bb + (i - nst);
+  };
+  for (uint32_t i = tid; i < need; i += FL_LVB_T) {
+    ChunkHdr c;
+    c.next = (i + 1 < need) ? chunk_id(i + 1) : NIL;
+    c.pad = 0;
+    c.price = f.price;
+    D.chdr[chunk_id(i)] = c;
+  }
+  if (need && !fresh && tid == 0) D.chdr[f.tail].next = chunk_id(0);
+  for (uint32_t i = tid; i < S; i += FL_LVB_T) {
+    const RsEnt r = RS[rf + i];
+    const Prep mk = B.prep[hd.beg + r.j];
+    const int64_t rem = (r.e < f.cfin) ? r.e + r.v - f.cfin : r.v;
+    uint32_t cid, slot;
+    if (!fresh && s0 + i < CH) {
+      cid = f.tail;
+      slot = s0 + i;
+    } else {
+      const uint32_t g = fresh ? i : i - room;
+      cid = chunk_id(g / CH);
+      slot = g % CH;
+    }
+    const uint32_t loc = cid * CH + slot;
+    const unsigned long long key = (static_cast<unsigned long long>(hd.sym + 1) << 32) | mk.oid;
+    unsigned long long hh = mix64(key) & mask, probe = 0;
+    for (; probe <= mask; ++probe, hh = (hh + 1) & mask) {
+      const unsigned long long kv = __hip_atomic_load(&D.idx[hh].key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if ((kv == KEY_EMPTY || kv == KEY_TOMB) && atomicCAS(&D.idx[hh].key, kv, key) == kv) break;
+    }
+    if (probe > mask) { atomicOr(&D.st->err, ERR_INDEX); continue; }
+    D.idx[hh].loc = loc;
+    Node nd{};
+    nd.rem = rem;
+    nd.oid = mk.oid;
+    nd.uuid = mk.uuid;
+    nd.ixs = static_cast<uint32_t>(hh);
+    nd.tx = mk.side;
+    D.nodes[loc] = nd;
+  }
+  if (tid != 0) return;
+  Level x{};
+  x.price = f.price;
+  x.head = x.tail = NIL;
+  x.depth = f.dfin;
+  x.nlive = f.nlive0 + S;
+  uint32_t mem = 0;
+  if ((hd.amask[q >> 6] >> (q & 63)) & 1ull) mem |= M_SALE;
+  if ((hd.bmask[q >> 6] >> (q & 63)) & 1ull) mem |= M_BUY;
+  x.member = static_cast<uint8_t>(mem);
+  if (x.nlive == 0) {
+    x.hslot = x.tslot = 0;
+  } else if (fresh) {
+    x.head = chunk_id(0);
+    x.hslot = 0;
+    x.tail = chunk_id(need - 1);
+    x.tslot = static_cast<uint8_t>(S - (need - 1) * CH);
+  } else {
+    x.head = f.head;
+    x.hslot = static_cast<uint8_t>(f.hslot);
+    x.tail = need ? chunk_id(need - 1) : f.tail;
+    x.tslot = static_cast<uint8_t>(need ? (S - room) - (need - 1) * CH : s0 + S);
+  }
+  // clean-book invariant: nodes <=> positive depth <=> one side-set membership
+  const bool ok = (x.nlive > 0) == (x.depth > 0) && (x.nlive > 0) == (mem == M_BUY || mem == M_SALE) &&
+                  (x.nlive > 0 || mem == 0);
+  if (!ok) atomicOr(&D.st->err, ERR_CORRUPT);
+  F.lvout[h * FL_CAP + q] = x;
 }
 
 // ... then one workgroup per head book compacts the level array.

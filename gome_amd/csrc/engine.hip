@@ -189,8 +189,7 @@ struct gome_engine {
   uint32_t* d_seg_start = nullptr;
   uint32_t* d_seg_order = nullptr;
   uint32_t* d_bcnt = nullptr;  // 32 counts + 32 offsets
-  uint32_t* d_claim = nullptr;
-  uint32_t* d_amin = nullptr;
+  unsigned long long* d_adm = nullptr;  // admission table (k_adm)
   uint32_t* d_adm_slot = nullptr;
   uint32_t adm_mask = 0;
   uint32_t* d_ev_count = nullptr;
@@ -380,8 +379,8 @@ gome_status gome_engine::init(const gome_config& c) {
       !alloc(&d_k1, nb, "keys1") || !alloc(&d_v1, nb, "vals1") || !alloc(&d_hist, hist_cap, "hist") ||
       !alloc(&d_bsum, bsum_cap, "scan") || !alloc(&d_tmp, nb, "segflags") ||
       !alloc(&d_seg_start, nb + 1, "seg_start") || !alloc(&d_seg_order, nb, "seg_order") ||
-      !alloc(&d_bcnt, 64, "buckets") || !alloc(&d_claim, adm_mask + 1ull, "adm_claim") ||
-      !alloc(&d_amin, adm_mask + 1ull, "adm_min") || !alloc(&d_adm_slot, nb, "adm_slot") ||
+      !alloc(&d_bcnt, 64, "buckets") || !alloc(&d_adm, adm_mask + 1ull, "adm_table") ||
+      !alloc(&d_adm_slot, nb, "adm_slot") ||
       !alloc(&d_ev_count, nb, "ev_count") || !alloc(&d_ev_off, nb, "ev_off") ||
       !alloc(&d_prep, nb, "prep") || !alloc(&d_pend, nb, "pending inserts") ||
       !alloc(&d_resume, MAX_HOT, "resume records") || !alloc(&d_arena, arena_cap, "event arena"))
@@ -500,12 +499,11 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   // the validation, the radix sort and the segmentation (the batch's critical path)
   HIPCHK(hipEventRecord(fork_adm, s));
   HIPCHK(hipStreamWaitEvent(flow_stream, fork_adm, 0));
-  HIPCHK(hipMemsetAsync(d_claim, 0, (adm_mask + 1ull) * 4, flow_stream));
-  HIPCHK(hipMemsetAsync(d_amin, 0xFF, (adm_mask + 1ull) * 4, flow_stream));
+  HIPCHK(hipMemsetAsync(d_adm, 0, (adm_mask + 1ull) * 8, flow_stream));
   if ((++fc_gen & FC_GEN_MASK) == 0) HIPCHK(hipMemsetAsync(F.fc_hash, 0, sizeof(FcHash) * fc_hcap, flow_stream));
   F.fc_gen = fc_gen;
-  k_adm<<<gN, T256, 0, flow_stream>>>(d_ord, n, d_claim, d_amin, d_adm_slot, adm_mask, cfg.max_symbols, d_st);
-  k_adm_flag<<<gN, T256, 0, flow_stream>>>(d_ord, n, d_adm_slot, d_amin);
+  k_adm<<<gN, T256, 0, flow_stream>>>(d_ord, n, d_adm, d_adm_slot, adm_mask, cfg.max_symbols, d_st);
+  k_adm_flag<<<gN, T256, 0, flow_stream>>>(d_ord, n, d_adm_slot, d_adm);
   HIPCHK(hipEventRecord(adm_done, flow_stream));
 
   // ---- stable radix sort of (symbol_id, seq)

@@ -239,11 +239,14 @@ __global__ void k_seg_scatter(const uint32_t* seg_start, const Status* st, uint3
 // Markers S:comparison[S:uuid:oid] are set at gRPC time for every ADD of the batch
 // (main.go:44-45) and tested+cleared at consume time (engine.go:58-62,90).  Under the
 // batch ingress model an ADD is admitted iff no earlier ADD/DEL of the batch carries
-// the same (S, uuid, oid).  claim[] holds the first claimant (seq+1) of a key's slot;
-// amin[] the smallest seq of the key.
+// the same (S, uuid, oid).  One open-addressing table of 64-bit words: a key's slot holds
+// its fingerprint (high half, never 0) and the smallest batch index of the key seen so far
+// (low half).  A record whose key is new claims an empty slot with one CAS; a repeat of the
+// key lowers the index with one 64-bit atomicMin (same high half, so the minimum is over
+// the indices).  Slots whose fingerprint matches are confirmed against the claimant's record.
 // Also validates the record (k_validate's check, folded in: one pass over the input).
-__global__ void k_adm(const gome_order* ord, uint32_t n, uint32_t* claim, uint32_t* amin,
-                      uint32_t* slot, uint32_t mask, uint32_t max_symbols, Status* st) {
+__global__ void k_adm(const gome_order* ord, uint32_t n, unsigned long long* tab, uint32_t* slot, uint32_t mask,
+                      uint32_t max_symbols, Status* st) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const gome_order g = ord[i];
@@ -254,17 +257,22 @@ __global__ void k_adm(const gome_order* ord, uint32_t n, uint32_t* claim, uint32
       atomicOr(&st->err, ERR_INPUT);
   }
   if (g.action != GOME_ADD && g.action != GOME_DEL) { slot[i] = NIL; return; }
-  uint32_t h = static_cast<uint32_t>(
-      mix64((static_cast<unsigned long long>(g.symbol_id) << 40) ^
-            (static_cast<unsigned long long>(g.uuid_id) << 20) ^ mix64(g.oid_id))) & mask;
+  const unsigned long long km = mix64((static_cast<unsigned long long>(g.symbol_id) << 40) ^
+                                      (static_cast<unsigned long long>(g.uuid_id) << 20) ^ mix64(g.oid_id));
+  const unsigned long long mine = ((km >> 32) | 0x80000000ull) << 32 | i;
+  uint32_t h = static_cast<uint32_t>(km) & mask;
   for (uint32_t probe = 0; probe <= mask; ++probe) {
-    uint32_t c = atomicCAS(&claim[h], 0u, i + 1);
+    const unsigned long long c = atomicCAS(&tab[h], 0ull, mine);
     if (c == 0) break;
-    const gome_order q = ord[c - 1];
-    if (q.symbol_id == g.symbol_id && q.uuid_id == g.uuid_id && q.oid_id == g.oid_id) break;
+    if ((c >> 32) == (mine >> 32)) {
+      const gome_order q = ord[static_cast<uint32_t>(c)];
+      if (q.symbol_id == g.symbol_id && q.uuid_id == g.uuid_id && q.oid_id == g.oid_id) {
+        if (c > mine) atomicMin(&tab[h], mine);
+        break;
+      }
+    }
     h = (h + 1) & mask;
   }
-  atomicMin(&amin[h], i);
   slot[i] = h;
 }
 
@@ -285,13 +293,13 @@ static_assert(sizeof(Prep) == 32, "Prep layout");
 // reads one flag instead of chasing slot -> minimum.  Runs beside the radix sort.
 // A record whose admission the host resolved (GOME_ORD_ADM_HOST: the consumer keeps the
 // reference's pre-pool markers itself) carries the verdict in GOME_ORD_ADMITTED.
-__global__ void k_adm_flag(const gome_order* ord, uint32_t n, uint32_t* slot, const uint32_t* amin) {
+__global__ void k_adm_flag(const gome_order* ord, uint32_t n, uint32_t* slot, const unsigned long long* tab) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint8_t action = ord[i].action;
   const uint16_t fl = ord[i].flags;
   if (fl & GOME_ORD_ADM_HOST) slot[i] = (action == GOME_ADD && (fl & GOME_ORD_ADMITTED)) ? 1u : 0u;
-  else slot[i] = (action == GOME_ADD && amin[slot[i]] == i) ? 1u : 0u;
+  else slot[i] = (action == GOME_ADD && static_cast<uint32_t>(tab[slot[i]]) == i) ? 1u : 0u;
 }
 
 __global__ void k_prep(const gome_order* ord, uint32_t n, const uint32_t* sidx,

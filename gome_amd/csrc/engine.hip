@@ -518,16 +518,14 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   for (uint32_t p = 0; p < passes; ++p) {
     const uint32_t shift = p * dbits;
     const uint32_t bits = std::min(dbits, key_bits - shift);
-    if (p == 0) {
-      k_radix_hist<true><<<nblk, RS_T, 0, s>>>(d_ord, nullptr, n, shift, bits, d_hist, nblk);
+    if (p == 0) {  // the keys out of the records into d_k1 (the second pass's output) first
+      k_radix_hist<true><<<nblk, RS_T, 0, s>>>(d_ord, nullptr, d_k1, n, shift, bits, d_hist, nblk);
       scan(d_hist, (1u << bits) * nblk, d_hist, nullptr, s);
-      k_radix_scatter<true><<<nblk, RS_T, 0, s>>>(d_ord, nullptr, nullptr, n, shift, bits, d_hist,
-                                                  kout, vout, nblk);
+      k_radix_scatter<true><<<nblk, RS_T, 0, s>>>(d_k1, nullptr, n, shift, bits, d_hist, kout, vout, nblk);
     } else {
-      k_radix_hist<false><<<nblk, RS_T, 0, s>>>(nullptr, kin, n, shift, bits, d_hist, nblk);
+      k_radix_hist<false><<<nblk, RS_T, 0, s>>>(nullptr, kin, nullptr, n, shift, bits, d_hist, nblk);
       scan(d_hist, (1u << bits) * nblk, d_hist, nullptr, s);
-      k_radix_scatter<false><<<nblk, RS_T, 0, s>>>(nullptr, kin, vin, n, shift, bits, d_hist, kout,
-                                                   vout, nblk);
+      k_radix_scatter<false><<<nblk, RS_T, 0, s>>>(kin, vin, n, shift, bits, d_hist, kout, vout, nblk);
     }
     kin = kout;
     vin = vout;

@@ -95,10 +95,12 @@ __global__ __launch_bounds__(256) void k_sort_keys(const gome_order* ord, uint32
   }
 }
 
+// FROM_ORD (the first pass): the keys come from the records, and the kernel also writes
+// them to keys_out, so the first scatter reads 4 B per order instead of the 32-B record.
 template <bool FROM_ORD>
 __global__ __launch_bounds__(RS_T) void k_radix_hist(const gome_order* ord, const uint32_t* keys,
-                                                     uint32_t n, uint32_t shift, uint32_t bits,
-                                                     uint32_t* hist, uint32_t nblk) {
+                                                     uint32_t* keys_out, uint32_t n, uint32_t shift,
+                                                     uint32_t bits, uint32_t* hist, uint32_t nblk) {
   __shared__ uint32_t h[1 << RS_MAXBITS];
   const uint32_t nb = 1u << bits, mask = nb - 1;
   for (uint32_t i = threadIdx.x; i < nb; i += RS_T) h[i] = 0;
@@ -107,7 +109,11 @@ __global__ __launch_bounds__(RS_T) void k_radix_hist(const gome_order* ord, cons
 #pragma unroll
   for (int it = 0; it < RS_IPT; ++it) {
     uint32_t i = tile + it * RS_T + threadIdx.x;
-    if (i < n) atomicAdd(&h[(rs_key<FROM_ORD>(ord, keys, i) >> shift) & mask], 1u);
+    if (i < n) {
+      const uint32_t k = rs_key<FROM_ORD>(ord, keys, i);
+      if (FROM_ORD) keys_out[i] = k;
+      atomicAdd(&h[(k >> shift) & mask], 1u);
+    }
   }
   __syncthreads();
   for (uint32_t d = threadIdx.x; d < nb; d += RS_T) hist[d * nblk + blockIdx.x] = h[d];
@@ -115,9 +121,9 @@ __global__ __launch_bounds__(RS_T) void k_radix_hist(const gome_order* ord, cons
 
 // Stable scatter: wave w of the block owns items [w*512, (w+1)*512) of the tile and ranks
 // them in rounds of 64 with a ballot-based match of equal digits (multi-split).
-template <bool FROM_ORD>
-__global__ __launch_bounds__(RS_T) void k_radix_scatter(const gome_order* ord,
-                                                        const uint32_t* keys_in,
+// IDV (the first pass): the values are the record indices themselves.
+template <bool IDV>
+__global__ __launch_bounds__(RS_T) void k_radix_scatter(const uint32_t* keys_in,
                                                         const uint32_t* vals_in, uint32_t n,
                                                         uint32_t shift, uint32_t bits,
                                                         const uint32_t* hist_scanned,
@@ -135,8 +141,8 @@ __global__ __launch_bounds__(RS_T) void k_radix_scatter(const gome_order* ord,
   for (int r = 0; r < RS_WAVE_ITEMS / 64; ++r) {
     const uint32_t i = base + r * 64 + lane;
     const bool valid = i < n;
-    uint32_t k = valid ? rs_key<FROM_ORD>(ord, keys_in, i) : 0;
-    uint32_t v = valid ? (FROM_ORD ? i : vals_in[i]) : 0;
+    uint32_t k = valid ? keys_in[i] : 0;
+    uint32_t v = valid ? (IDV ? i : vals_in[i]) : 0;
     uint32_t d = (k >> shift) & mask;
     unsigned long long m = __ballot(valid);
     for (uint32_t b = 0; b < bits; ++b) {

@@ -381,3 +381,33 @@ def test_capacity_rejected_before_applying():
     _cmp(eng.drain(), orc.submit(b3))
     assert eng.stats()["n_resting"] == 2700
     _cmp_books(eng, orc, range(4), "after the accepted batch")
+
+
+# ---- admission (Q4) under heavy key reuse -------------------------------------------------
+def _run_admission(batches, n_symbols, syms):
+    eng = Engine(max_symbols=n_symbols, max_batch=max(len(b) for b in batches), max_nodes=1 << 20,
+                 max_levels=1 << 20)
+    orc = Oracle(n_symbols)
+    for i, b in enumerate(batches):
+        eng.submit(b)
+        _cmp(eng.drain(), orc.submit(b), f"batch {i}")
+    _cmp_books(eng, orc, syms)
+    assert eng.stats()["n_resting"] == orc.resting()
+    return eng
+
+
+def test_admission_keys_repeated_within_batches():
+    """Every (symbol, uuid, oid) key repeats tens of times inside its batch among ADDs and DELs:
+    only an ADD ahead of every other record of its key is admitted (engine.go:58-62,90).  An oid
+    names one key (its symbol and uuid) and never recurs in a later batch, so no oid is admitted
+    twice (Q7 stays outside the domain, tests/helpers.py:random_batches).  The hot books stay on
+    the flow path with most of their ADDs dropped."""
+    rec = wl.cancel_mix(160000, 40, seed=19, zipf_s=1.0)
+    rng = np.random.default_rng(19)
+    batches = wl.split_batches(rec, 40000)
+    for k, b in enumerate(batches):
+        oid = 1 + k * 200000 + b["symbol_id"].astype(np.int64) * 5000 + rng.integers(0, 250, len(b))
+        b["oid_id"] = oid.astype(b["oid_id"].dtype)
+        b["uuid_id"] = (1 + oid % 2).astype(b["uuid_id"].dtype)
+    eng = _run_admission(batches, 40, range(40))
+    assert eng.stats()["n_flow_books"] > 0

@@ -166,6 +166,7 @@ struct gome_engine {
   hipStream_t flow_stream = nullptr;  // the hottest book's plan (critical path)
   hipStream_t copy_stream = nullptr;  // H2D of records, D2H of events (pipelined path)
   hipEvent_t fork{}, join{}, joinf{}, prep_h{}, prep_t{}, fork_adm{}, adm_done{}, seg_done{}, ev_scan{}, ev_hot{};
+  hipEvent_t cnt_fork{}, cnt_done{};  // the hottest book's k_flow_count beside its writes
   Slot slots[GOME_MAX_INFLIGHT];
   uint32_t next_slot = 0;
   std::deque<Flight> flights;
@@ -243,7 +244,7 @@ struct gome_engine {
       for (hipEvent_t ev : {S.ev0, S.ev1, S.evm0, S.evm1, S.evh0, S.evh1, S.evf0, S.evf1, S.evc0, S.evc1, S.h2d, S.done})
         if (ev) (void)hipEventDestroy(ev);
     }
-    for (hipEvent_t ev : {fork, join, joinf, prep_h, prep_t, fork_adm, adm_done, seg_done, ev_scan, ev_hot})
+    for (hipEvent_t ev : {fork, join, joinf, prep_h, prep_t, fork_adm, adm_done, seg_done, ev_scan, ev_hot, cnt_fork, cnt_done})
       if (ev) (void)hipEventDestroy(ev);
     if (hot_stream) (void)hipStreamDestroy(hot_stream);
     if (flow_stream) (void)hipStreamDestroy(flow_stream);
@@ -296,7 +297,8 @@ gome_status gome_engine::init(const gome_config& c) {
   HIPCHK(hipStreamCreateWithFlags(&hot_stream, hipStreamNonBlocking));
   HIPCHK(hipStreamCreateWithFlags(&flow_stream, hipStreamNonBlocking));
   HIPCHK(hipStreamCreateWithFlags(&copy_stream, hipStreamNonBlocking));
-  for (hipEvent_t* ev : {&fork, &join, &joinf, &prep_h, &prep_t, &fork_adm, &adm_done, &seg_done, &ev_scan, &ev_hot})
+  for (hipEvent_t* ev : {&fork, &join, &joinf, &prep_h, &prep_t, &fork_adm, &adm_done, &seg_done, &ev_scan, &ev_hot,
+                         &cnt_fork, &cnt_done})
     HIPCHK(hipEventCreateWithFlags(ev, hipEventDisableTiming));
   for (Slot& S : slots) {
     for (hipEvent_t* ev : {&S.ev0, &S.ev1, &S.evm0, &S.evm1, &S.evh0, &S.evh1, &S.evf0, &S.evf1, &S.evc0, &S.evc1})
@@ -654,18 +656,26 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
     k_deep_write_lv<<<dim3(DEEP_GRID, ns), 64, 0, st>>>(D, B, R);
     k_deep_write_fin<<<ns, DEEP_FIN_T, 0, st>>>(D, R);
   };
-  // the hottest book's reconstruction: wide kernels (tile-parallel sort, one wave per level)
-  auto head_recon = [&](const FlowArgs& R, uint32_t nb, hipStream_t st) {
+  // the hottest book's reconstruction: wide kernels (tile-parallel sort, one wave per level).
+  // cs: the stream of k_flow_count (it reads the plan's log and the level records, the writes
+  // read neither its output nor it theirs, so it may run beside them on another stream)
+  auto head_recon = [&](const FlowArgs& R, uint32_t nb, hipStream_t st, hipStream_t cs) -> gome_status {
     k_flow_sort_cnt<<<dim3(FL_SORT_GRID, nb), FL_TILE, 0, st>>>(D, R);
     k_flow_sort_scan<<<nb, FL_CAP, 0, st>>>(D, R);
     k_flow_sort_scatter<<<dim3(FL_SORT_GRID, nb), FL_TILE, 0, st>>>(D, R);
     deep_sort_level(R, FL_SORT_GRID, st);
     k_flow_level_wide<<<dim3(FL_CAP, nb), FL_LVB_T, 0, st>>>(D, R);
     k_flow_toff<FL_OK_ADD><<<1, 1024, 0, st>>>(D, R);
-    k_flow_count<<<1024, 256, 0, st>>>(D, B, R);
+    if (cs != st) {
+      HIPCHK(hipEventRecord(cnt_fork, st));
+      HIPCHK(hipStreamWaitEvent(cs, cnt_fork, 0));
+    }
+    k_flow_count<<<1024, 256, 0, cs>>>(D, B, R);
+    if (cs != st) HIPCHK(hipEventRecord(cnt_done, cs));
     k_flow_write_lv_blk<<<dim3(FL_CAP, nb), FL_LVB_T, 0, st>>>(D, B, R);
     k_flow_write_fin<<<nb, 128, 0, st>>>(D, R);
     deep_write(R, st);
+    return GOME_OK;
   };
   // books with DELs (match_flow_cancel.h); their events go to the arena
   auto head_recon_c = [&](const FlowArgs& R, const FlowArgs& Rc, uint32_t nb, hipStream_t st) {
@@ -718,7 +728,7 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   HIPCHK(hipStreamWaitEvent(hot_stream, prep_h, 0));
   if (nh_near) {
     k_flow_plan_near<<<nh_near, 256, plan_lds, hot_stream>>>(D, FH1);
-    head_recon(FH1, nh_near, hot_stream);
+    if (head_recon(FH1, nh_near, hot_stream, hot_stream) != GOME_OK) return GOME_E_DEVICE;
     head_recon_c(FH1, FH1c, nh_near, hot_stream);
     k_flow_events_arena<<<1024, 256, 0, hot_stream>>>(D, B, FH1);
   }
@@ -732,8 +742,10 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   k_match_resume<<<nleg, 64, 0, hot_stream>>>(D, B, d_resume);
   k_pend_apply<<<dim3(8, 64), 256, 0, hot_stream>>>(D, d_pend, d_seg_start, d_seg_order, B);
   HIPCHK(hipEventRecord(join, hot_stream));
-  head_recon(FH0, 1, flow_stream);
+  // (the hot stream's own work ended long before the hottest book's plan does)
+  if (head_recon(FH0, 1, flow_stream, hot_stream) != GOME_OK) return GOME_E_DEVICE;
   head_recon_c(FH0, FH0c, 1, flow_stream);
+  HIPCHK(hipStreamWaitEvent(flow_stream, cnt_done, 0));
   HIPCHK(hipEventRecord(joinf, flow_stream));
   HIPCHK(hipStreamWaitEvent(s, join, 0));
   HIPCHK(hipStreamWaitEvent(s, joinf, 0));

@@ -166,7 +166,7 @@ struct gome_engine {
   hipStream_t flow_stream = nullptr;  // the hottest book's plan (critical path)
   hipStream_t copy_stream = nullptr;  // H2D of records, D2H of events (pipelined path)
   hipEvent_t fork{}, join{}, joinf{}, prep_h{}, prep_t{}, fork_adm{}, adm_done{}, seg_done{}, ev_scan{}, ev_hot{};
-  hipEvent_t cnt_fork{}, cnt_done{};  // the hottest book's k_flow_count beside its writes
+  hipEvent_t dp_fork{}, cnt_fork{}, cnt_done{};  // the hottest book's deep chain and k_flow_count beside its writes
   Slot slots[GOME_MAX_INFLIGHT];
   uint32_t next_slot = 0;
   std::deque<Flight> flights;
@@ -244,7 +244,7 @@ struct gome_engine {
       for (hipEvent_t ev : {S.ev0, S.ev1, S.evm0, S.evm1, S.evh0, S.evh1, S.evf0, S.evf1, S.evc0, S.evc1, S.h2d, S.done})
         if (ev) (void)hipEventDestroy(ev);
     }
-    for (hipEvent_t ev : {fork, join, joinf, prep_h, prep_t, fork_adm, adm_done, seg_done, ev_scan, ev_hot, cnt_fork, cnt_done})
+    for (hipEvent_t ev : {fork, join, joinf, prep_h, prep_t, fork_adm, adm_done, seg_done, ev_scan, ev_hot, dp_fork, cnt_fork, cnt_done})
       if (ev) (void)hipEventDestroy(ev);
     if (hot_stream) (void)hipStreamDestroy(hot_stream);
     if (flow_stream) (void)hipStreamDestroy(flow_stream);
@@ -298,7 +298,7 @@ gome_status gome_engine::init(const gome_config& c) {
   HIPCHK(hipStreamCreateWithFlags(&flow_stream, hipStreamNonBlocking));
   HIPCHK(hipStreamCreateWithFlags(&copy_stream, hipStreamNonBlocking));
   for (hipEvent_t* ev : {&fork, &join, &joinf, &prep_h, &prep_t, &fork_adm, &adm_done, &seg_done, &ev_scan, &ev_hot,
-                         &cnt_fork, &cnt_done})
+                         &dp_fork, &cnt_fork, &cnt_done})
     HIPCHK(hipEventCreateWithFlags(ev, hipEventDisableTiming));
   for (Slot& S : slots) {
     for (hipEvent_t* ev : {&S.ev0, &S.ev1, &S.evm0, &S.evm1, &S.evh0, &S.evh1, &S.evf0, &S.evf1, &S.evc0, &S.evc1})
@@ -657,24 +657,35 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
     k_deep_write_fin<<<ns, DEEP_FIN_T, 0, st>>>(D, R);
   };
   // the hottest book's reconstruction: wide kernels (tile-parallel sort, one wave per level).
-  // cs: the stream of k_flow_count (it reads the plan's log and the level records, the writes
-  // read neither its output nor it theirs, so it may run beside them on another stream)
+  // cs: the stream of the deep books' chain and of k_flow_count.  The deep kernels work on
+  // other books than the flow sort / level / write kernels, and k_flow_count reads the plan's
+  // log and the level records, which the writes neither read from it nor change, so with
+  // cs != st they run beside the writes; k_flow_count still comes after both level passes.
   auto head_recon = [&](const FlowArgs& R, uint32_t nb, hipStream_t st, hipStream_t cs) -> gome_status {
+    const bool split = cs != st;
+    if (split) {  // the deep books' level sort (other books than the ones below) beside it
+      HIPCHK(hipEventRecord(dp_fork, st));
+      HIPCHK(hipStreamWaitEvent(cs, dp_fork, 0));
+      deep_sort_level(R, FL_SORT_GRID, cs);
+    }
     k_flow_sort_cnt<<<dim3(FL_SORT_GRID, nb), FL_TILE, 0, st>>>(D, R);
     k_flow_sort_scan<<<nb, FL_CAP, 0, st>>>(D, R);
     k_flow_sort_scatter<<<dim3(FL_SORT_GRID, nb), FL_TILE, 0, st>>>(D, R);
-    deep_sort_level(R, FL_SORT_GRID, st);
+    if (!split) deep_sort_level(R, FL_SORT_GRID, st);
     k_flow_level_wide<<<dim3(FL_CAP, nb), FL_LVB_T, 0, st>>>(D, R);
     k_flow_toff<FL_OK_ADD><<<1, 1024, 0, st>>>(D, R);
-    if (cs != st) {
+    if (split) {
       HIPCHK(hipEventRecord(cnt_fork, st));
       HIPCHK(hipStreamWaitEvent(cs, cnt_fork, 0));
     }
     k_flow_count<<<1024, 256, 0, cs>>>(D, B, R);
-    if (cs != st) HIPCHK(hipEventRecord(cnt_done, cs));
+    if (split) {
+      deep_write(R, cs);
+      HIPCHK(hipEventRecord(cnt_done, cs));
+    }
     k_flow_write_lv_blk<<<dim3(FL_CAP, nb), FL_LVB_T, 0, st>>>(D, B, R);
     k_flow_write_fin<<<nb, 128, 0, st>>>(D, R);
-    deep_write(R, st);
+    if (!split) deep_write(R, st);
     return GOME_OK;
   };
   // books with DELs (match_flow_cancel.h); their events go to the arena

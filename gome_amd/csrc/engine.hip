@@ -667,6 +667,7 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
       HIPCHK(hipEventRecord(dp_fork, st));
       HIPCHK(hipStreamWaitEvent(cs, dp_fork, 0));
       deep_sort_level(R, FL_SORT_GRID, cs);
+      deep_write(R, cs);  // (k_flow_count reads neither the claims nor the writes)
     }
     k_flow_sort_cnt<<<dim3(FL_SORT_GRID, nb), FL_TILE, 0, st>>>(D, R);
     k_flow_sort_scan<<<nb, FL_CAP, 0, st>>>(D, R);
@@ -679,10 +680,7 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
       HIPCHK(hipStreamWaitEvent(cs, cnt_fork, 0));
     }
     k_flow_count<<<1024, 256, 0, cs>>>(D, B, R);
-    if (split) {
-      deep_write(R, cs);
-      HIPCHK(hipEventRecord(cnt_done, cs));
-    }
+    if (split) HIPCHK(hipEventRecord(cnt_done, cs));
     k_flow_write_lv_blk<<<dim3(FL_CAP, nb), FL_LVB_T, 0, st>>>(D, B, R);
     k_flow_write_fin<<<nb, 128, 0, st>>>(D, R);
     if (!split) deep_write(R, st);
@@ -756,10 +754,10 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   // (the hot stream's own work ended long before the hottest book's plan does)
   if (head_recon(FH0, 1, flow_stream, hot_stream) != GOME_OK) return GOME_E_DEVICE;
   head_recon_c(FH0, FH0c, 1, flow_stream);
-  HIPCHK(hipStreamWaitEvent(flow_stream, cnt_done, 0));
   HIPCHK(hipEventRecord(joinf, flow_stream));
   HIPCHK(hipStreamWaitEvent(s, join, 0));
   HIPCHK(hipStreamWaitEvent(s, joinf, 0));
+  HIPCHK(hipStreamWaitEvent(s, cnt_done, 0));
 
   HIPCHK(hipEventRecord(S.evm1, s));
 

@@ -132,6 +132,16 @@ def make_stream(workload, rank, world, seed):
     return ns.batch, ns.owned_share, ns.top_share
 
 
+def hot_symbols(workload, rank, world, k=8):
+    """Symbol ids of this rank's k hottest books (its lowest owned Zipf ranks): the books whose
+    top-of-book digests go into the publisher summary."""
+    W = WORKLOADS[workload]
+    own = np.arange(rank, W["symbols"], world)[:k]
+    if not W["zipf"]:
+        return own.astype(np.uint32)
+    return wl.ZipfSymbols(W["symbols"], W["zipf"]).rank_to_id[own]
+
+
 def combine_ranks(orders, fills, events, elapsed, lat, device):
     """Whole-job totals over ranks: sums of work, MAX of the timed region and of each
     step's latency (the slowest rank defines the job).  Works on any initialised process
@@ -148,10 +158,10 @@ def combine_ranks(orders, fills, events, elapsed, lat, device):
     return o, f, ev, float(e.item()), lt.tolist()
 
 
-def gather_summary(st, summary, gathered, rank=0, step=0):
+def gather_summary(st, summary, gathered, rank=0, step=0, digests=None):
     """Per-GPU trade/depth summary to every rank (the publisher feed)."""
     import torch.distributed as dist
-    pack_summary(st, rank, step, summary)
+    pack_summary(st, rank, step, summary, digests)
     dist.all_gather_into_tensor(gathered, summary)
     return gathered
 
@@ -209,6 +219,11 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of CPU-baseline work")
     ap.add_argument("--cpu-threads", type=int, default=8, help="threads of the sharded CPU baseline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--backend", choices=("nccl", "gloo"), default="nccl",
+                    help="process-group backend (nccl = RCCL over xGMI; gloo: CPU collectives, for tests)")
+    ap.add_argument("--same-device", action="store_true",
+                    help="every rank on device 0 (rehearsing the N-rank path on a one-GPU box)")
+    ap.add_argument("--step-log", default="", help="write each timed step's engine counters (JSONL)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="PMC-measured HBM bytes per launch of the dominant kernel (optional)")
     args = ap.parse_args()
@@ -223,9 +238,14 @@ def main():
         if world == 1 and args.gpus > 1:
             print(f"--gpus {args.gpus} needs torchrun with {args.gpus} processes", file=sys.stderr)
             sys.exit(2)
-    torch.cuda.set_device(local)
+    dev = 0 if args.same_device else local
+    torch.cuda.set_device(dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group("gloo")
+    cdev = "cuda" if args.backend == "nccl" else "cpu"  # where the collectives' tensors live
 
     from gome_amd.abi import Engine
 
@@ -247,16 +267,19 @@ def main():
     eng = Engine(max_symbols=n_symbols, max_batch=per_rank,
                  max_nodes=max(1 << 20, int(total_orders * keep)) + 2 * per_rank,
                  max_levels=max(1 << 22, (256 if n_symbols <= 100000 else 128) * n_symbols) + 2 * per_rank,
-                 device=local)
+                 device=dev)
 
-    summary = torch.zeros(SUMMARY_WORDS, dtype=torch.int64, device="cuda")
-    gathered = torch.zeros(SUMMARY_WORDS * world, dtype=torch.int64, device="cuda")
+    summary = torch.zeros(SUMMARY_WORDS, dtype=torch.int64, device=cdev)
+    gathered = torch.zeros(SUMMARY_WORDS * world, dtype=torch.int64, device=cdev)
     pub = SummaryPublisher(world) if rank == 0 else None
     seq = [0]
+    hot = hot_symbols(args.workload, rank, world)
+    last_dg = [None]
 
     def publish(st, i):
         if world > 1:  # per-GPU trade/depth summary to the publisher (RCCL all_gather)
-            gather_summary(st, summary, gathered, rank, i)
+            last_dg[0] = eng.top_of_book(hot)  # depth digests of this rank's hottest books
+            gather_summary(st, summary, gathered, rank, i, last_dg[0])
             if pub is not None:
                 pub.consume(gathered)
 
@@ -289,6 +312,11 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    if args.step_log and rank == 0:
+        with open(args.step_log, "w") as f:
+            for i, (s_, l_) in enumerate(zip(sts, lat)):
+                f.write(json.dumps(dict(step=i, wall_ms=round(l_, 3), **{k: (round(v, 4) if isinstance(v, float) else v)
+                                                                         for k, v in s_.items()})) + "\n")
 
     orders = sum(s["n_orders"] for s in sts)
     fills = sum(s["n_fills"] for s in sts)
@@ -315,8 +343,19 @@ def main():
     kname = max(cands, key=lambda k: cands[k][0])
     ms_dom, bdom, kdesc = cands[kname]
     max_seg = max(s["max_segment"] for s in sts)
+    digest_check = None
     if world > 1:
-        g_orders, g_fills, g_events, elapsed, lat = combine_ranks(orders, fills, events, elapsed, lat, "cuda")
+        g_orders, g_fills, g_events, elapsed, lat = combine_ranks(orders, fills, events, elapsed, lat, cdev)
+        # every rank checks the digests it published last against its books' snapshots
+        # (gome_snapshot_levels); the publisher gets the mismatch count
+        from gome_amd.publisher import digests_from_levels
+        bad = 0
+        for d in last_dg[0]:
+            want = digests_from_levels(eng.levels(int(d["symbol_id"])))
+            bad += int(any(int(d[k]) != v for k, v in want.items()))
+        t = torch.tensor([bad, len(last_dg[0])], dtype=torch.int64, device=cdev)
+        dist.all_reduce(t)
+        digest_check = {"checked": int(t[1].item()), "mismatches": int(t[0].item())}
     else:
         g_orders, g_fills, g_events = orders, fills, events
 
@@ -358,7 +397,7 @@ def main():
         e_el = time.perf_counter() - t1
         e_orders, e_events = per_rank * e2e_steps, done_ev[0]
         if world > 1:
-            e_orders, _, e_events, e_el, elat = combine_ranks(e_orders, 0.0, e_events, e_el, elat, "cuda")
+            e_orders, _, e_events, e_el, elat = combine_ranks(e_orders, 0.0, e_events, e_el, elat, cdev)
         e2e = {"value": round(e_orders / e_el, 1), "unit": "orders/s", "steps": e2e_steps,
                "ms_per_step": round(e_el / e2e_steps * 1e3, 3),
                "p50_batch_ms": round(pctl(elat, 0.5), 3), "p99_batch_ms": round(pctl(elat, 0.99), 3),
@@ -444,6 +483,8 @@ def main():
         if pub is not None and world > 1:
             pub.check(int(g_orders), int(g_fills), int(g_events))
             out["publisher"] = pub.summary()
+            out["publisher"]["digest_check"] = digest_check
+            out["config"]["backend"] = args.backend + (" (all ranks on device 0)" if args.same_device else "")
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -23,6 +23,11 @@ GOME_FLAG_NO_HEADROOM = 2  # gome_config.flags: no pool-headroom check before a 
 GOME_ORD_ADM_HOST, GOME_ORD_ADMITTED = 1, 2  # gome_order.flags: host-resolved admission (ABI 4)
 GOME_MAX_INFLIGHT = 2
 
+TOB_DTYPE = np.dtype([("symbol_id", "<u4"), ("n_levels", "<u4"), ("bid_price_fx", "<i8"), ("bid_depth_fx", "<i8"),
+                      ("ask_price_fx", "<i8"), ("ask_depth_fx", "<i8"), ("bid_nodes", "<u4"), ("ask_nodes", "<u4"),
+                      ("flags", "<u4"), ("pad", "<u4")])
+assert TOB_DTYPE.itemsize == 56
+
 GOME_OK, GOME_E_INVAL, GOME_E_CAPACITY, GOME_E_DEVICE, GOME_E_STATE, GOME_E_NOTFOUND = range(6)
 STATUS_NAMES = {0: "OK", 1: "E_INVAL", 2: "E_CAPACITY", 3: "E_DEVICE", 4: "E_STATE", 5: "E_NOTFOUND"}
 
@@ -50,7 +55,7 @@ class Stats(C.Structure):
         ("ms_flow_plan", C.c_double), ("n_flow_head_orders", C.c_uint64),
         ("n_flow_head_touches", C.c_uint64), ("n_index_rebuilds", C.c_uint64),
         ("idx_tombstones", C.c_uint64), ("n_flow_cancels", C.c_uint64), ("ms_cold", C.c_double),
-        ("lvl_used", C.c_uint64)]
+        ("lvl_used", C.c_uint64), ("n_dup_oid", C.c_uint64)]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_}
@@ -96,6 +101,9 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.gome_debug_peek.restype = C.c_int32
     lib.gome_release_device_events.restype = C.c_int32
     lib.gome_get_stats.argtypes = [VP, P(Stats)]
+    lib.gome_dup_records.argtypes = [VP, P(C.c_uint32), C.c_size_t, P(C.c_size_t)]
+    lib.gome_take_deferred.argtypes = [VP]
+    lib.gome_top_of_book.argtypes = [VP, VP, C.c_size_t, VP]
     lib.gome_snapshot_levels.argtypes = [VP, C.c_uint32, VP, C.c_size_t, P(C.c_size_t)]
     lib.gome_snapshot_fifo.argtypes = [VP, C.c_uint32, C.c_int64, VP, C.c_size_t, P(C.c_size_t)]
     lib.gome_load_books.argtypes = [VP, C.c_size_t, VP, VP, VP, VP, C.c_size_t]
@@ -106,6 +114,9 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.gome_render_link_node.argtypes = [C.c_char_p, C.c_int64, C.c_int32, C.c_int64, C.c_uint32] + [
         C.c_char_p] * 5 + [C.c_size_t]
     lib.gome_render_link_node.restype = C.c_int64
+    lib.gome_render_events.argtypes = [VP, C.c_size_t, VP, C.c_size_t, C.c_uint64, C.c_uint32, VP, C.c_size_t,
+                                       VP, C.c_size_t, VP, C.c_size_t, VP, VP, C.c_size_t]
+    lib.gome_render_events.restype = C.c_int64
     lib.gome_gen_create.argtypes = [VP, P(VP)]
     lib.gome_gen_batch.argtypes = [VP, VP, C.c_size_t]
     lib.gome_gen_shares.argtypes = [VP, P(C.c_double), P(C.c_double)]
@@ -116,7 +127,8 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     for f in ("gome_create", "gome_submit_batch", "gome_submit_batch_device", "gome_drain_events",
               "gome_device_events", "gome_get_stats", "gome_snapshot_levels", "gome_snapshot_fifo",
               "gome_fixed_from_double", "gome_fixed_from_scaled", "gome_submit_batch_async",
-              "gome_collect", "gome_host_alloc", "gome_load_books"):
+              "gome_collect", "gome_host_alloc", "gome_load_books", "gome_dup_records",
+              "gome_take_deferred", "gome_top_of_book"):
         getattr(lib, f).restype = C.c_int32
     _lib = lib
     return lib
@@ -165,15 +177,19 @@ def render_match_result(ev: np.void, taker: np.void, symbol: str, taker_uuid: st
     e = np.array([ev], dtype=EVENT_DTYPE)
     t = np.array([taker], dtype=ORDER_DTYPE)
     enc = lambda s: None if s is None else s.encode()
-    buf = C.create_string_buffer(8192)
     tt = tx_table if isinstance(tx_table, np.ndarray) else tx_table_array(tx_table)
-    n = lib.gome_render_match_result(e.ctypes.data, t.ctypes.data, accuracy, symbol.encode(),
-                                     taker_uuid.encode(), taker_oid.encode(), enc(maker_uuid),
-                                     enc(maker_oid), enc(maker_next_oid),
-                                     None if tt is None else tt.ctypes.data, buf, len(buf))
-    if n < 0:
-        raise GomeError(GOME_E_INVAL, "render failed")
-    return buf.raw[:n].decode()
+    size = 8192
+    while True:  # a short buffer returns -(bytes needed)
+        buf = C.create_string_buffer(size)
+        n = lib.gome_render_match_result(e.ctypes.data, t.ctypes.data, accuracy, symbol.encode(),
+                                         taker_uuid.encode(), taker_oid.encode(), enc(maker_uuid),
+                                         enc(maker_oid), enc(maker_next_oid),
+                                         None if tt is None else tt.ctypes.data, buf, len(buf))
+        if n >= 0:
+            return buf.raw[:n].decode()
+        if n == -(1 << 63):
+            raise GomeError(GOME_E_INVAL, "render failed (missing argument)")
+        size = -n
 
 
 def render_link_node(symbol: str, price_fx: int, side: int, volume_fx: int, uuid: str, oid: str,
@@ -182,12 +198,16 @@ def render_link_node(symbol: str, price_fx: int, side: int, volume_fx: int, uuid
     `side` is the raw int32 Transaction value."""
     lib = load_library()
     enc = lambda s: None if s is None else s.encode()
-    buf = C.create_string_buffer(4096)
-    n = lib.gome_render_link_node(symbol.encode(), int(price_fx), int(side), int(volume_fx), accuracy,
-                                  uuid.encode(), oid.encode(), enc(prev_oid), enc(next_oid), buf, len(buf))
-    if n < 0:
-        raise GomeError(GOME_E_INVAL, "render failed")
-    return buf.raw[:n].decode()
+    size = 4096
+    while True:  # a short buffer returns -(bytes needed)
+        buf = C.create_string_buffer(size)
+        n = lib.gome_render_link_node(symbol.encode(), int(price_fx), int(side), int(volume_fx), accuracy,
+                                      uuid.encode(), oid.encode(), enc(prev_oid), enc(next_oid), buf, len(buf))
+        if n >= 0:
+            return buf.raw[:n].decode()
+        if n == -(1 << 63):
+            raise GomeError(GOME_E_INVAL, "render failed (missing argument)")
+        size = -n
 
 
 class Engine:
@@ -291,6 +311,28 @@ class Engine:
         st = Stats()
         self._check(self.lib.gome_get_stats(self.h, C.byref(st)))
         return st.as_dict()
+
+    def dup_records(self) -> np.ndarray:
+        """Batch indices of the last finished batch's ADDs rejected by the duplicate-oid rule."""
+        n = C.c_size_t()
+        self._check(self.lib.gome_dup_records(self.h, None, 0, C.byref(n)))
+        out = np.zeros(n.value, np.uint32)
+        if n.value:
+            self._check(self.lib.gome_dup_records(self.h, out.ctypes.data_as(C.POINTER(C.c_uint32)), n.value,
+                                                  C.byref(n)))
+        return out
+
+    def top_of_book(self, symbols) -> np.ndarray:
+        """gome_top_of_book: best bid / ask, their depths and FIFO lengths per symbol (TOB_DTYPE)."""
+        syms = np.ascontiguousarray(symbols, dtype=np.uint32)
+        out = np.zeros(len(syms), TOB_DTYPE)
+        self._check(self.lib.gome_top_of_book(self.h, syms.ctypes.data, len(syms), out.ctypes.data))
+        return out
+
+    def take_deferred(self) -> tuple[int, str]:
+        """(status, message) of the first in-flight batch failure a synchronous call collected."""
+        s = self.lib.gome_take_deferred(self.h)
+        return s, (self.lib.gome_last_error(self.h).decode() if s != GOME_OK else "")
 
     def load_books(self, books) -> None:
         """gome_load_books: `books` = [(symbol_id, levels LEVEL_DTYPE ascending by price,

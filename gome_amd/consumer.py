@@ -22,16 +22,27 @@ Here:
                   encoding/json) to the sink in publish order;
   * MatchSink     the matchOrder queue plus ConsumeMatchOrder's decode-and-log.
 
-A message whose JSON does not decode is consumed and ignored (the reference decodes into a
-zero OrderNode, whose Action 0 DoOrder ignores).  A message whose Price / Volume is not an
-exact scaled integer below 2^53 (quirk Q5) is outside the parity domain: it is counted in
-`rejected` and not submitted.
+Decoding follows Go's json.Unmarshal into an OrderNode (rabbitmq.go:118-124 prints the error
+and still calls DoOrder): a syntax error decodes nothing (a zero OrderNode, whose Action 0
+DoOrder ignores); otherwise each field whose JSON value fits its Go type is set and any other
+field (wrong type, overflow, null) stays zero, so `"Price":"abc"` is an order at price 0.
+`process()` never raises on message content.  A message outside the parity domain is counted
+in `rejected` and not submitted: a Price / Volume that is not an exact scaled integer below
+2^53 (quirk Q5), or a 255th distinct Transaction value outside {0, 1} (the engine carries
+Transaction as a one-byte code, gome_abi.h).  The engine applies the duplicate-oid rule (Q7,
+gome_abi.h) to the admitted ADDs; `dups` counts them.
+
+Admission markers are resolved against a staged view of the pre-pool and the consumption is
+committed only once the engine accepted the batch: a batch the engine refuses (for example
+GOME_E_CAPACITY before anything is applied) can be resubmitted with the same verdicts.
 """
 from __future__ import annotations
 
 import ctypes as C
 import json
+import math
 import queue as _queue
+import re
 import threading
 import time
 
@@ -102,6 +113,14 @@ class PrePool:
         self._s: set = set()
         self._lock = threading.Lock()
 
+    def stage(self) -> "StagedMarkers":
+        return StagedMarkers(self)
+
+    def commit(self, consumed: set):
+        """Remove the markers a staged batch consumed (after the engine accepted the batch)."""
+        with self._lock:
+            self._s -= consumed
+
     def set(self, symbol: str, uuid: str, oid: str):  # SetPrePool (main.go:44-45)
         with self._lock:
             self._s.add((symbol, uuid, oid))
@@ -121,6 +140,94 @@ class PrePool:
 
     def __len__(self):
         return len(self._s)
+
+
+class StagedMarkers:
+    """One batch's admission verdicts against the pre-pool, in queue order, without consuming
+    anything yet: an ADD is admitted iff its marker exists and no earlier record of the batch
+    consumed it (ExistsPrePool + DeletePrePool, engine.go:58-62,90)."""
+
+    def __init__(self, pool: PrePool):
+        self.pool, self.consumed = pool, set()
+
+    def consume_add(self, symbol: str, uuid: str, oid: str) -> bool:
+        k = (symbol, uuid, oid)
+        if k in self.consumed:
+            return False
+        with self.pool._lock:
+            ok = k in self.pool._s
+        if ok:
+            self.consumed.add(k)
+        return ok
+
+    def consume_del(self, symbol: str, uuid: str, oid: str):
+        with self.pool._lock:
+            if (symbol, uuid, oid) in self.pool._s:
+                self.consumed.add((symbol, uuid, oid))
+
+    def commit(self):
+        self.pool.commit(self.consumed)
+        self.consumed = set()
+
+
+# ---- Go encoding/json Unmarshal of the consumed OrderNode (ordernode.go:9-36) -----------------
+# Only the fields the engine reads; the key fields (OrderHashKey, NodeName, ...) are the ones
+# NewOrderNode derives from them at gRPC time (ordernode.go:89-117).
+_GO_FIELDS = {"action": ("Action", "i", 8), "uuid": ("Uuid", "s", 0), "oid": ("Oid", "s", 0),
+              "symbol": ("Symbol", "s", 0), "transaction": ("Transaction", "i", 32),
+              "price": ("Price", "f", 0), "volume": ("Volume", "f", 0)}
+
+
+_LONE_SURROGATE = re.compile("[\ud800-\udfff]")
+
+
+class _Lit(str):
+    """Literal text of a JSON number (Go converts numbers from the literal)."""
+
+
+class _Pairs(list):
+    """A JSON object's (key, value) pairs in document order."""
+
+
+def _reject_constant(tok):
+    raise ValueError(tok)  # NaN / Infinity are not JSON to Go
+
+
+def decode_order_node(body) -> dict:
+    """The OrderNode fields json.Unmarshal leaves: {"Action", "Uuid", "Oid", "Symbol",
+    "Transaction", "Price", "Volume"}.  Never raises.  Keys match exactly or case-insensitively
+    (Go's field matching); later duplicates win; an int field takes only an integer literal
+    within its width (Action int8, Transaction int32), a float field any finite number, a
+    string field only a string; anything else (and null) leaves the zero value."""
+    out = {"Action": 0, "Uuid": "", "Oid": "", "Symbol": "", "Transaction": 0, "Price": 0.0, "Volume": 0.0}
+    try:
+        doc = json.loads(body, parse_int=_Lit, parse_float=_Lit, parse_constant=_reject_constant,
+                         object_pairs_hook=_Pairs)
+    except (ValueError, TypeError, RecursionError):
+        return out  # syntax error: Unmarshal decodes nothing
+    if not isinstance(doc, _Pairs):
+        return out
+    for key, val in doc:
+        f = _GO_FIELDS.get(key.casefold())  # (Unicode folding, as Go's EqualFold: 'ſ' ~ 's')
+        if f is None or val is None:
+            continue
+        name, kind, bits = f
+        if kind == "s":
+            if isinstance(val, str) and not isinstance(val, _Lit):
+                out[name] = _LONE_SURROGATE.sub("\ufffd", val)  # Go decodes a lone \\uD8xx as U+FFFD
+        elif isinstance(val, _Lit):
+            if kind == "f":
+                x = float(val)
+                if not math.isinf(x):  # ParseFloat out of range: UnmarshalTypeError, skipped
+                    out[name] = x
+            else:
+                try:
+                    x = int(val, 10)  # ParseInt: no fraction, no exponent
+                except ValueError:
+                    continue
+                if -(1 << (bits - 1)) <= x < (1 << (bits - 1)):
+                    out[name] = x
+    return out
 
 
 def _order_node_json(req: dict, action: int, price: float, volume: float, accuracy: int) -> str:
@@ -196,12 +303,9 @@ class BatchingConsumer:
         self.max_wait = max_wait_us * 1e-6
         self.acc = accuracy
         self.lib = load_library()
-        self.lib.gome_render_events.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t, C.c_uint64,
-                                                C.c_uint32, C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t,
-                                                C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p, C.c_size_t]
-        self.lib.gome_render_events.restype = C.c_int64
         self.seq = 0
-        self.consumed = self.rejected = self.batches = 0
+        self.consumed = self.rejected = self.batches = self.dups = 0
+        self._staged = None
         self._buf = C.create_string_buffer(1 << 20)
 
     # ---- draining ------------------------------------------------------------------
@@ -227,43 +331,39 @@ class BatchingConsumer:
 
     # ---- one batch -------------------------------------------------------------------
     def records(self, msgs) -> np.ndarray:
-        """Decode, convert and admit (in queue order) -> gome_order records."""
+        """Decode, convert and admit (in queue order) -> gome_order records.  The admission
+        verdicts come from a staged view of the pre-pool (committed by process() once the
+        engine took the batch)."""
         N = self.names
+        pre = self._staged = self.pre.stage()
         rec = np.zeros(len(msgs), ORDER_DTYPE)
         keep = np.ones(len(msgs), bool)
         for i, body in enumerate(msgs):
+            o = decode_order_node(body)
+            act, sym, uuid, oid = o["Action"], o["Symbol"], o["Uuid"], o["Oid"]
+            if act not in (ADD, DEL):
+                continue  # DoOrder ignores any other Action (engine.go:46-54): a zero record
             try:
-                o = json.loads(body)
-                act = int(o.get("Action", 0))
-                sym, uuid, oid = str(o.get("Symbol", "")), str(o.get("Uuid", "")), str(o.get("Oid", ""))
-                tx = int(o.get("Transaction", 0))
-                price, vol = o.get("Price", 0.0), o.get("Volume", 0.0)
-            except (ValueError, TypeError, AttributeError):
-                rec[i]["action"] = 0  # zero OrderNode: DoOrder ignores it
+                p, v = fixed_from_scaled(o["Price"]), fixed_from_scaled(o["Volume"])
+                code = N.tx_code(o["Transaction"])
+            except GomeError:
+                keep[i] = False  # outside the parity domain (Q5, or the Transaction code space)
+                self.rejected += 1
+                if act == ADD:
+                    pre.consume_add(sym, uuid, oid)
+                else:
+                    pre.consume_del(sym, uuid, oid)
                 continue
-            if act in (ADD, DEL):
-                try:
-                    p, v = fixed_from_scaled(price), fixed_from_scaled(vol)
-                except GomeError:
-                    keep[i] = False  # Q5: outside the exact domain
-                    self.rejected += 1
-                    if act == ADD:
-                        self.pre.consume_add(sym, uuid, oid)
-                    else:
-                        self.pre.consume_del(sym, uuid, oid)
-                    continue
-            else:
-                p = v = 0
             r = rec[i]
             r["price_fx"], r["volume_fx"] = p, v
             r["symbol_id"], r["uuid_id"], r["oid_id"] = N.id("sym", sym), N.id("uuid", uuid), N.id("oid", oid)
-            r["side"] = N.tx_code(tx)
-            r["action"] = act & 0xFF if 0 <= act < 256 else 0
+            r["side"] = code
+            r["action"] = act
             if act == ADD:
-                ok = self.pre.consume_add(sym, uuid, oid)
+                ok = pre.consume_add(sym, uuid, oid)
                 r["flags"] = GOME_ORD_ADM_HOST | (GOME_ORD_ADMITTED if ok else 0)
-            elif act == DEL:
-                self.pre.consume_del(sym, uuid, oid)
+            else:
+                pre.consume_del(sym, uuid, oid)
                 r["flags"] = GOME_ORD_ADM_HOST
         return rec[keep]
 
@@ -284,16 +384,21 @@ class BatchingConsumer:
         return self._buf.raw[:k].decode().split("\n")[:-1]
 
     def process(self, msgs) -> int:
-        """Apply one drained batch; returns the MatchResults published."""
-        self.consumed += len(msgs)
+        """Apply one drained batch; returns the MatchResults published.  Raises only when the
+        engine refuses the batch (GomeError, e.g. E_CAPACITY before anything was applied); the
+        pre-pool is then untouched and the same messages can be processed again."""
         rec = self.records(msgs)
-        if len(rec) == 0:
-            return 0
         if len(rec) > self.eng.max_batch:
             raise GomeError(1, "batch larger than the engine's max_batch")
         base = self.seq
-        self.eng.submit(rec, seq_base=base)
+        if len(rec):
+            self.eng.submit(rec, seq_base=base)
+        self._staged.commit()  # the engine took the batch: its markers are consumed
+        self.consumed += len(msgs)
+        if len(rec) == 0:
+            return 0
         self.seq += len(rec)
+        self.dups += int(self.eng.stats()["n_dup_oid"])
         ev = self.eng.drain()
         lines = self.render(ev, rec, base)
         self.sink.publish_many(lines)

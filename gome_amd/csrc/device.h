@@ -81,7 +81,8 @@ enum {
   C_FLOW_BOOKS, C_FLOW_ORDERS, C_FLOW_TOUCHES,            // hot books on the flow path
   C_FLOW_HEAD_ORDERS, C_FLOW_HEAD_TOUCHES,                // ... of which the head (k_flow_plan_head)
   C_FLOW_CANCELS,                                         // cancels applied on the flow path
-  C_NCTR = 21
+  C_DUP,                                                  // ADDs rejected as duplicate oids (Q7)
+  C_NCTR = 22
 };
 
 // Level blocks (a book's sorted level array) come in power-of-two capacities 16 << c.  A

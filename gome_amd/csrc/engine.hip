@@ -31,9 +31,6 @@
 #include <vector>
 
 #include "../../include/gome/gome_abi.h"
-#ifdef GOME_ROCPRIM_SORT
-#include <rocprim/rocprim.hpp>
-#endif
 #include "device.h"
 #include "match_cold.h"
 #include "match_flow.h"
@@ -126,6 +123,41 @@ __global__ __launch_bounds__(64) void k_idx_rebuild(Dev D) {
   }
 }
 
+// Top-of-book digests (the publisher's depth summary): per requested symbol, the
+// best bid (highest S:BUY member) and best ask (lowest S:SALE member) with their S:depth fields
+// and FIFO lengths, as GetReverseDepth's first level would report them (nodepool.go:86-115).
+// A thread per symbol walks the book's sorted level block.
+__global__ void k_tob(Dev D, const uint32_t* syms, uint32_t n, gome_tob* out) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  gome_tob t{};
+  t.symbol_id = syms[i];
+  if (t.symbol_id < D.max_symbols) {
+    const Book bk = D.books[t.symbol_id];
+    const Level* L = D.lvl + bk.lvl_base;
+    bool bid = false, ask = false;
+    for (uint32_t k = 0; k < bk.n_lvl; ++k) {
+      const Level x = L[k];
+      if (!x.nlive && !x.depth && !x.member) continue;
+      ++t.n_levels;
+      if (!ask && (x.member & M_SALE)) {
+        ask = true;
+        t.ask_price_fx = x.price;
+        t.ask_depth_fx = x.depth;
+        t.ask_nodes = x.nlive;
+      }
+      if (x.member & M_BUY) {
+        bid = true;
+        t.bid_price_fx = x.price;
+        t.bid_depth_fx = x.depth;
+        t.bid_nodes = x.nlive;
+      }
+    }
+    t.flags = (bid ? 1u : 0u) | (ask ? 2u : 0u);
+  }
+  out[i] = t;
+}
+
 // ============================================================== host runtime
 namespace {
 
@@ -147,6 +179,7 @@ struct Slot {
   uint32_t ev_cap = 0;
   Status* h_st = nullptr;          // page-locked copy of the batch's Status
   gome_event* h_events = nullptr;  // page-locked event copy (gome_collect)
+  uint32_t* d_dup = nullptr;       // batch indices of the ADDs rejected as duplicate oids (Q7)
   size_t h_cap = 0;
   hipEvent_t ev0{}, ev1{}, evm0{}, evm1{}, evh0{}, evh1{}, evf0{}, evf1{}, evc0{}, evc1{};
   hipEvent_t h2d{}, done{};
@@ -182,8 +215,6 @@ struct gome_engine {
   unsigned long long idx_cap = 0;
   // batch buffers
   uint32_t *d_k0 = nullptr, *d_v0 = nullptr, *d_k1 = nullptr, *d_v1 = nullptr;
-  unsigned char* d_rp_tmp = nullptr;  // GOME_ROCPRIM_SORT: rocPRIM's radix-sort scratch
-  size_t rp_bytes = 0;
   uint32_t* d_hist = nullptr;
   uint32_t* d_bsum = nullptr;
   uint32_t* d_tmp = nullptr;  // flags / segpos (n)
@@ -191,6 +222,7 @@ struct gome_engine {
   uint32_t* d_seg_order = nullptr;
   uint32_t* d_bcnt = nullptr;  // 32 counts + 32 offsets
   unsigned long long* d_adm = nullptr;  // admission table (k_adm)
+  unsigned long long* d_dup = nullptr;  // (S, oid) table of the admitted ADDs (duplicate-oid rule)
   uint32_t* d_adm_slot = nullptr;
   uint32_t adm_mask = 0;
   uint32_t* d_ev_count = nullptr;
@@ -199,6 +231,10 @@ struct gome_engine {
   uint32_t arena_cap = 0;
   // host-side state
   std::vector<gome_event> pending;
+  std::vector<uint32_t> dup_idx;  // the last finished batch's duplicate-oid rejections (sorted)
+  uint32_t* d_tob_syms = nullptr;  // gome_top_of_book's device buffers
+  gome_tob* d_tob = nullptr;
+  size_t tob_cap = 0;
   size_t pending_pos = 0;
   size_t dev_events = 0, dev_events_pos = 0;  // events of the last device submit
   uint32_t dev_slot = 0;
@@ -210,6 +246,8 @@ struct gome_engine {
   unsigned long long fc_hcap = 0;  // its entries
   bool poisoned = false;
   std::string err;
+  gome_status deferred = GOME_OK;  // an in-flight batch's failure collected by a synchronous call
+  std::string deferred_msg;
   std::vector<void*> allocs;
   std::set<void*> host_allocs;
 
@@ -286,7 +324,8 @@ gome_status gome_engine::init(const gome_config& c) {
   if (cfg.accuracy == 0) cfg.accuracy = 8;
   if (!cfg.max_symbols || !cfg.max_batch || !cfg.max_nodes || !cfg.max_levels)
     return fail(GOME_E_INVAL, "gome_config: max_symbols, max_batch, max_nodes, max_levels must be > 0");
-  if (cfg.max_batch > (1u << 30) || cfg.max_levels > 0xF0000000ull)
+  // (max_batch <= 2^28 keeps the admission tables' slots below 2^30: k_adm flags bit 31)
+  if (cfg.max_batch > (1u << 28) || cfg.max_levels > 0xF0000000ull)
     return fail(GOME_E_INVAL, "gome_config: capacity out of range");
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
@@ -382,17 +421,16 @@ gome_status gome_engine::init(const gome_config& c) {
       !alloc(&d_bsum, bsum_cap, "scan") || !alloc(&d_tmp, nb, "segflags") ||
       !alloc(&d_seg_start, nb + 1, "seg_start") || !alloc(&d_seg_order, nb, "seg_order") ||
       !alloc(&d_bcnt, 64, "buckets") || !alloc(&d_adm, adm_mask + 1ull, "adm_table") ||
+      !alloc(&d_dup, adm_mask + 1ull, "duplicate-oid table") ||
       !alloc(&d_adm_slot, nb, "adm_slot") ||
       !alloc(&d_ev_count, nb, "ev_count") || !alloc(&d_ev_off, nb, "ev_off") ||
       !alloc(&d_prep, nb, "prep") || !alloc(&d_pend, nb, "pending inserts") ||
       !alloc(&d_resume, MAX_HOT, "resume records") || !alloc(&d_arena, arena_cap, "event arena"))
     return GOME_E_CAPACITY;
-#ifdef GOME_ROCPRIM_SORT
-  HIPCHK(rocprim::radix_sort_pairs(nullptr, rp_bytes, d_k1, d_k0, d_v1, d_v0, static_cast<size_t>(nb), 0u, key_bits, stream));
-  if (!alloc(&d_rp_tmp, rp_bytes, "radix sort scratch")) return GOME_E_CAPACITY;
-#endif
   for (Slot& S : slots) {
-    if (!alloc(&S.d_orders, nb, "orders") || !alloc(&S.d_events, arena_cap, "events")) return GOME_E_CAPACITY;
+    if (!alloc(&S.d_orders, nb, "orders") || !alloc(&S.d_events, arena_cap, "events") ||
+        !alloc(&S.d_dup, nb, "duplicate-oid list"))
+      return GOME_E_CAPACITY;
     S.ev_cap = arena_cap;
   }
   // flow path (match_flow.h): per-hot-book headers and level slots, packed records, the
@@ -504,17 +542,14 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   HIPCHK(hipMemsetAsync(d_adm, 0, (adm_mask + 1ull) * 8, flow_stream));
   if ((++fc_gen & FC_GEN_MASK) == 0) HIPCHK(hipMemsetAsync(F.fc_hash, 0, sizeof(FcHash) * fc_hcap, flow_stream));
   F.fc_gen = fc_gen;
-  k_adm<<<gN, T256, 0, flow_stream>>>(d_ord, n, d_adm, d_adm_slot, adm_mask, cfg.max_symbols, d_st);
-  k_adm_flag<<<gN, T256, 0, flow_stream>>>(d_ord, n, d_adm_slot, d_adm);
+  HIPCHK(hipMemsetAsync(d_dup, 0, (adm_mask + 1ull) * 8, flow_stream));
+  k_adm<<<gN, T256, 0, flow_stream>>>(d_ord, n, d_adm, d_adm_slot, adm_mask, cfg.max_symbols, d_st, D.books, D.idx,
+                                      D.idx_mask);
+  k_adm_flag<<<gN, T256, 0, flow_stream>>>(d_ord, n, d_adm_slot, d_adm, d_dup, adm_mask);
+  k_dup_flag<<<gN, T256, 0, flow_stream>>>(n, d_adm_slot, d_dup, d_st, S.d_dup);
   HIPCHK(hipEventRecord(adm_done, flow_stream));
 
   // ---- stable radix sort of (symbol_id, seq)
-#ifdef GOME_ROCPRIM_SORT
-  k_sort_keys<<<gN, T256, 0, s>>>(d_ord, n, d_k1, d_v1);
-  HIPCHK(rocprim::radix_sort_pairs(d_rp_tmp, rp_bytes, d_k1, d_k0, d_v1, d_v0, static_cast<size_t>(n), 0u, key_bits, s));
-  const uint32_t* skeys = d_k0;
-  const uint32_t* sidx = d_v0;
-#else
   const uint32_t nblk = ceil_div(n, RS_TILE);
   uint32_t *kin = nullptr, *vin = nullptr, *kout = d_k0, *vout = d_v0;
   for (uint32_t p = 0; p < passes; ++p) {
@@ -536,7 +571,6 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   }
   const uint32_t* skeys = kin;
   const uint32_t* sidx = vin;
-#endif
 
   // ---- segments (one per symbol present), longest first
   k_seg_flags<<<gN, T256, 0, s>>>(skeys, n, d_tmp);
@@ -784,6 +818,7 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
 gome_status gome_engine::finish(uint32_t sl, uint32_t n) {
   Slot& S = slots[sl];
   const Status& st = *S.h_st;
+  dup_idx.clear();
   if (st.err & ERR_INPUT)
     return fail(GOME_E_INVAL, "batch rejected: a record is outside the exact domain "
                               "(symbol_id >= max_symbols, volume < 0, |value| >= 2^53, or unknown flags)");
@@ -834,12 +869,18 @@ gome_status gome_engine::finish(uint32_t sl, uint32_t n) {
   stats.idx_tombstones = idx_tomb;
   stats.n_flow_cancels = st.ctr[C_FLOW_CANCELS];
   stats.lvl_used = st.lvl_used;
+  stats.n_dup_oid = st.ctr[C_DUP];
+  if (const uint64_t nd = std::min<uint64_t>(st.ctr[C_DUP], n)) {
+    dup_idx.resize(nd);
+    HIPCHK(hipMemcpy(dup_idx.data(), S.d_dup, nd * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    std::sort(dup_idx.begin(), dup_idx.end());
+  }
   return GOME_OK;
 }
 
+// (`used`, which gome_load_books checks, is set only when a batch is actually enqueued)
 gome_status gome_engine::check_submit(size_t n, const void* p) {
   if (poisoned) return fail(GOME_E_STATE, "engine poisoned by an earlier fatal error");
-  used = true;
   if (n > max_batch) return fail(GOME_E_INVAL, "batch larger than max_batch");
   if (n && !p) return fail(GOME_E_INVAL, "NULL records");
   return GOME_OK;
@@ -938,15 +979,26 @@ gome_status gome_engine::collect(const gome_event** evs, size_t* nev) {
   return GOME_OK;
 }
 
-// Every batch still in flight -> the drain queue (before a synchronous call).
+// Every batch still in flight -> the drain queue (before a synchronous call).  A batch that
+// was rejected (GOME_E_INVAL: nothing applied) does not fail the synchronous call that collected
+// it: its status and message are kept as the deferred failure (gome_take_deferred) and the call
+// goes on.  Only a failure that leaves the engine unusable (poisoned, or a HIP error) is returned.
 gome_status gome_engine::collect_all() {
-  gome_status first = GOME_OK;
+  gome_status fatal = GOME_OK;
   while (!flights.empty()) {
     const gome_event* evs = nullptr;
     size_t n = 0;
+    const uint64_t base = flights.front().seq_base;
     gome_status st = collect(&evs, &n);
     if (st != GOME_OK) {
-      if (first == GOME_OK) first = st;
+      if (!poisoned && st == GOME_E_INVAL) {
+        if (deferred == GOME_OK) {
+          deferred = st;
+          deferred_msg = "in-flight batch (seq_base " + std::to_string(base) + ") rejected: " + err;
+        }
+      } else if (fatal == GOME_OK) {
+        fatal = st;
+      }
       continue;
     }
     if (pending_pos) {
@@ -955,7 +1007,7 @@ gome_status gome_engine::collect_all() {
     }
     pending.insert(pending.end(), evs, evs + n);
   }
-  return first;
+  return fatal;
 }
 
 // ============================================================== C-ABI
@@ -1007,6 +1059,7 @@ gome_status gome_submit_batch(gome_engine* e, const gome_order* orders, size_t n
   if ((st = e->check_capacity_host(orders, n, 0)) != GOME_OK) return st;
   const uint32_t sl = e->take_slot();
   Slot& S = e->slots[sl];
+  e->used = true;
   hipError_t he = hipMemcpyAsync(S.d_orders, orders, n * sizeof(gome_order), hipMemcpyHostToDevice, e->stream);
   if (he != hipSuccess) return e->fail(GOME_E_DEVICE, hipGetErrorString(he));
   if ((st = e->enqueue(S.d_orders, static_cast<uint32_t>(n), e->stream, sl, seq_base, 0)) != GOME_OK) return st;
@@ -1027,6 +1080,7 @@ gome_status gome_submit_batch_device(gome_engine* e, const gome_order* dev_order
   hipStream_t s = stream ? static_cast<hipStream_t>(stream) : e->stream;
   const uint32_t sl = e->take_slot();
   Slot& S = e->slots[sl];
+  e->used = true;
   if ((st = e->enqueue(dev_orders, static_cast<uint32_t>(n), s, sl, seq_base, 0)) != GOME_OK) return st;
   hipError_t he = hipEventSynchronize(S.done);
   if (he != hipSuccess) return e->fail(GOME_E_DEVICE, hipGetErrorString(he));
@@ -1050,6 +1104,7 @@ gome_status gome_submit_batch_async(gome_engine* e, const gome_order* orders, si
   const uint32_t sl = e->take_slot();
   if (n) {
     Slot& S = e->slots[sl];
+    e->used = true;
     // the records travel on the copy stream (beside the batch in flight); the pipeline waits
     hipError_t he = hipMemcpyAsync(S.d_orders, orders, n * sizeof(gome_order), hipMemcpyHostToDevice,
                                    e->copy_stream);
@@ -1098,6 +1153,7 @@ size_t gome_pending_events(const gome_engine* e) {
 
 gome_status gome_drain_events(gome_engine* e, gome_event* out, size_t cap, size_t* n_out) {
   if (!e || !n_out || (cap && !out)) return GOME_E_INVAL;
+  if (gome_status s = e->collect_all()) return s;
   size_t c = 0;
   size_t hp = e->pending.size() - e->pending_pos;
   if (hp) {
@@ -1176,6 +1232,54 @@ gome_status gome_get_stats(const gome_engine* e, gome_stats* out) {
   if (!e || !out) return GOME_E_INVAL;
   *out = e->stats;
   return GOME_OK;
+}
+
+gome_status gome_top_of_book(gome_engine* e, const uint32_t* symbols, size_t n, gome_tob* out) {
+  if (!e || (n && (!symbols || !out))) return GOME_E_INVAL;
+  if (gome_status s = e->collect_all()) return s;
+  if (n == 0) return GOME_OK;
+  if (n > (1u << 20)) return e->fail(GOME_E_INVAL, "gome_top_of_book: more than 2^20 symbols");
+  if (n > e->tob_cap) {  // (kept between calls: the publisher asks every batch)
+    if (e->d_tob_syms) e->release(e->d_tob_syms);
+    if (e->d_tob) e->release(e->d_tob);
+    e->d_tob_syms = nullptr;
+    e->d_tob = nullptr;
+    e->tob_cap = 0;
+    const size_t cap = std::max<size_t>(n, 64);
+    if (!e->alloc(&e->d_tob_syms, cap, "tob symbols") || !e->alloc(&e->d_tob, cap, "tob digests"))
+      return GOME_E_CAPACITY;
+    e->tob_cap = cap;
+  }
+  uint32_t* d_syms = e->d_tob_syms;
+  gome_tob* d_out = e->d_tob;
+  hipStream_t s = e->stream;
+  gome_status st = GOME_OK;
+  if (hipMemcpyAsync(d_syms, symbols, n * 4, hipMemcpyHostToDevice, s) != hipSuccess) st = GOME_E_DEVICE;
+  if (st == GOME_OK) {
+    k_tob<<<static_cast<uint32_t>((n + 63) / 64), 64, 0, s>>>(e->D, d_syms, static_cast<uint32_t>(n), d_out);
+    if (hipGetLastError() != hipSuccess ||
+        hipMemcpyAsync(out, d_out, n * sizeof(gome_tob), hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+      st = GOME_E_DEVICE;
+  }
+  return st == GOME_OK ? GOME_OK : e->fail(st, "gome_top_of_book: device error");
+}
+
+gome_status gome_dup_records(const gome_engine* e, uint32_t* out, size_t cap, size_t* n_out) {
+  if (!e || !n_out || (cap && !out)) return GOME_E_INVAL;
+  const size_t n = e->dup_idx.size();
+  std::copy(e->dup_idx.begin(), e->dup_idx.begin() + static_cast<long>(std::min(cap, n)), out);
+  *n_out = n;
+  return GOME_OK;
+}
+
+gome_status gome_take_deferred(gome_engine* e) {
+  if (!e) return GOME_E_INVAL;
+  const gome_status s = e->deferred;
+  if (s != GOME_OK) e->err = e->deferred_msg;
+  e->deferred = GOME_OK;
+  e->deferred_msg.clear();
+  return s;
 }
 
 // ---- gome_load_books: a Redis-schema book image straight into the pools of a fresh engine

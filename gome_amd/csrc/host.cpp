@@ -52,13 +52,15 @@ gome_status fixed_from_double(double x, uint32_t acc, int64_t* out) {
 }
 
 // ---- Go encoding/json pieces -------------------------------------------------
+// Output cursor: writes while the bytes (plus a NUL) fit in cap, and counts every byte either
+// way, so a caller whose buffer is short learns the size it needs (n + 1).
 struct Out {
   char* buf;
   size_t cap, n = 0;
   bool ok = true;
   void put(const char* s, size_t k) {
-    if (n + k >= cap) { ok = false; return; }
-    std::memcpy(buf + n, s, k);
+    if (ok && n + k < cap) std::memcpy(buf + n, s, k);
+    else ok = false;
     n += k;
   }
   void put(const char* s) { put(s, std::strlen(s)); }
@@ -167,7 +169,7 @@ void render_node(Out& o, const NodeView& v) {
 extern "C" int64_t gome_render_link_node(const char* symbol, int64_t price_fx, int32_t transaction, int64_t volume_fx,
                                          uint32_t accuracy, const char* uuid, const char* oid,
                                          const char* prev_oid, const char* next_oid, char* buf, size_t cap) {
-  if (!symbol || !uuid || !oid || !buf) return -1;
+  if (!symbol || !uuid || !oid || (!buf && cap)) return INT64_MIN;
   Out o{buf, cap};
   // a resting node as nodelink.go stores it (SetLinkNode, :119-122): the ADD that rested,
   // its remaining volume, and the FIFO flags / neighbours kept by InitOrderLink, SetLast and
@@ -175,7 +177,7 @@ extern "C" int64_t gome_render_link_node(const char* symbol, int64_t price_fx, i
   NodeView v{GOME_ADD, uuid, oid, symbol, transaction, price_fx, volume_fx, accuracy,
              prev_oid == nullptr, next_oid == nullptr, next_oid, prev_oid};
   render_node(o, v);
-  if (!o.ok) return -1;
+  if (!o.ok) return -static_cast<int64_t>(o.n + 1);
   buf[o.n] = 0;
   return static_cast<int64_t>(o.n);
 }
@@ -209,7 +211,7 @@ extern "C" int64_t gome_render_events(const gome_event* ev, size_t n, const gome
   if ((n && (!ev || !batch)) || !sym_names || !uuid_names || !oid_names) return INT64_MIN;
   size_t used = 0;
   bool fits = buf != nullptr;
-  char tmp[16384];
+  char none[1];
   for (size_t i = 0; i < n; ++i) {
     const gome_event& e = ev[i];
     const uint64_t seq = (static_cast<uint64_t>(e.seq_hi) << 32) | e.taker_seq;
@@ -220,18 +222,24 @@ extern "C" int64_t gome_render_events(const gome_event* ev, size_t n, const gome
     if (fill && (e.maker_uuid_id >= n_uuid || e.maker_oid_id >= n_oid ||
                  (!e.maker_is_last && e.maker_next_oid_id >= n_oid)))
       return INT64_MIN;
-    const int64_t k = gome_render_match_result(
+    // straight into the caller's buffer while it fits (the line, its '\n' and the renderer's
+    // NUL), else a sizing pass (cap 0) that only counts
+    const size_t room = fits && cap > used ? cap - used : 0;
+    int64_t k = gome_render_match_result(
         &e, &t, accuracy, sym_names[t.symbol_id], uuid_names[t.uuid_id], oid_names[t.oid_id],
         fill ? uuid_names[e.maker_uuid_id] : nullptr, fill ? oid_names[e.maker_oid_id] : nullptr,
-        (fill && !e.maker_is_last) ? oid_names[e.maker_next_oid_id] : nullptr, tx_table, tmp, sizeof tmp);
-    if (k < 0) return INT64_MIN;
-    if (fits && used + static_cast<size_t>(k) + 1 <= cap) {
-      std::memcpy(buf + used, tmp, static_cast<size_t>(k));
-      buf[used + static_cast<size_t>(k)] = '\n';
+        (fill && !e.maker_is_last) ? oid_names[e.maker_next_oid_id] : nullptr, tx_table,
+        room ? buf + used : none, room);
+    if (k == INT64_MIN) return INT64_MIN;
+    size_t len;
+    if (k >= 0) {  // (it fit with its NUL, so its '\n' fits too)
+      len = static_cast<size_t>(k);
+      buf[used + len] = '\n';
     } else {
       fits = false;
+      len = k >= 0 ? static_cast<size_t>(k) : static_cast<size_t>(-k) - 1;
     }
-    used += static_cast<size_t>(k) + 1;
+    used += len + 1;
   }
   return fits ? static_cast<int64_t>(used) : -static_cast<int64_t>(used);
 }
@@ -242,7 +250,7 @@ extern "C" int64_t gome_render_match_result(const gome_event* ev, const gome_ord
                                             const char* maker_uuid, const char* maker_oid,
                                             const char* maker_next_oid, const int32_t* tx_table,
                                             char* buf, size_t cap) {
-  if (!ev || !taker || !symbol || !taker_uuid || !taker_oid || !buf) return -1;
+  if (!ev || !taker || !symbol || !taker_uuid || !taker_oid || (!buf && cap)) return INT64_MIN;
   // Transaction codes -> the raw int32 values the reference echoes (Q8, gome_abi.h)
   const int taker_tx = tx_table ? tx_table[taker->side] : taker->side;
   const int maker_tx = tx_table ? tx_table[ev->maker_side] : ev->maker_side;
@@ -257,7 +265,7 @@ extern "C" int64_t gome_render_match_result(const gome_event* ev, const gome_ord
     o.put(",\"MatchNode\":");
     render_node(o, n);
   } else {
-    if (!maker_uuid || !maker_oid) return -1;
+    if (!maker_uuid || !maker_oid) return INT64_MIN;
     // Node: the taker after this fill (engine.go:154,171,190).
     NodeView t{taker->action, taker_uuid, taker_oid, symbol, taker_tx, taker->price_fx,
                ev->taker_volume_fx, accuracy, false, false, nullptr};
@@ -266,14 +274,14 @@ extern "C" int64_t gome_render_match_result(const gome_event* ev, const gome_ord
     NodeView m{GOME_ADD, maker_uuid, maker_oid, symbol, maker_tx, ev->price_fx,
                ev->maker_volume_fx, accuracy, true, ev->maker_is_last != 0,
                ev->maker_is_last ? nullptr : maker_next_oid};
-    if (!ev->maker_is_last && !maker_next_oid) return -1;
+    if (!ev->maker_is_last && !maker_next_oid) return INT64_MIN;
     o.put(",\"MatchNode\":");
     render_node(o, m);
   }
   o.put(",\"MatchVolume\":");
   json_float(o, static_cast<double>(ev->match_volume_fx));
   o.putc('}');
-  if (!o.ok) return -1;
+  if (!o.ok) return -static_cast<int64_t>(o.n + 1);  // the buffer size it needs
   buf[o.n] = 0;
   return static_cast<int64_t>(o.n);
 }

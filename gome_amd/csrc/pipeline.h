@@ -86,15 +86,6 @@ __device__ __forceinline__ uint32_t rs_key(const gome_order* ord, const uint32_t
   return FROM_ORD ? ord[i].symbol_id : keys[i];
 }
 
-// (GOME_ROCPRIM_SORT) keys = symbol ids, values = record indices, for rocPRIM's radix sort
-__global__ __launch_bounds__(256) void k_sort_keys(const gome_order* ord, uint32_t n, uint32_t* keys, uint32_t* vals) {
-  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
-  if (i < n) {
-    keys[i] = ord[i].symbol_id;
-    vals[i] = i;
-  }
-}
-
 // FROM_ORD (the first pass): the keys come from the records, and the kernel also writes
 // them to keys_out, so the first scatter reads 4 B per order instead of the 32-B record.
 template <bool FROM_ORD>
@@ -250,19 +241,40 @@ __global__ void k_seg_scatter(const uint32_t* seg_start, const Status* st, uint3
 // (low half).  A record whose key is new claims an empty slot with one CAS; a repeat of the
 // key lowers the index with one 64-bit atomicMin (same high half, so the minimum is over
 // the indices).  Slots whose fingerprint matches are confirmed against the claimant's record.
-// Also validates the record (k_validate's check, folded in: one pass over the input).
+// Also validates the record (k_validate's check, folded in: one pass over the input), and for
+// an ADD probes the (S, oid) cancel index as the previous batch left it: ADM_RESTING marks an
+// ADD whose oid already rests in its book (the duplicate-oid rule, k_dup_flag).
+constexpr uint32_t ADM_RESTING = 0x80000000u;
+
+// Read-only probe of the (S, oid) cancel index: does a live node carry this key?
+__device__ __forceinline__ bool idx_live(const IdxEnt* idx, unsigned long long mask, unsigned long long key) {
+  unsigned long long h = mix64(key) & mask;
+  for (unsigned long long probe = 0; probe <= mask; ++probe, h = (h + 1) & mask) {
+    const unsigned long long k = idx[h].key;
+    if (k == key) return true;
+    if (k == KEY_EMPTY) return false;
+  }
+  return false;
+}
+
 __global__ void k_adm(const gome_order* ord, uint32_t n, unsigned long long* tab, uint32_t* slot, uint32_t mask,
-                      uint32_t max_symbols, Status* st) {
+                      uint32_t max_symbols, Status* st, const Book* books, const IdxEnt* idx,
+                      unsigned long long idx_mask) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const gome_order g = ord[i];
   {
     const int64_t lim = 1ll << 53;
     if (g.symbol_id >= max_symbols || g.volume_fx < 0 || g.volume_fx >= lim || g.price_fx <= -lim ||
-        g.price_fx >= lim || (g.flags & ~GOME_ORD_FLAGS_MASK) != 0)
+        g.price_fx >= lim || (g.flags & ~GOME_ORD_FLAGS_MASK) != 0) {
       atomicOr(&st->err, ERR_INPUT);
+      slot[i] = NIL;
+      return;  // (the batch is rejected; nothing below may index by symbol_id)
+    }
   }
   if (g.action != GOME_ADD && g.action != GOME_DEL) { slot[i] = NIL; return; }
+  const bool resting = g.action == GOME_ADD && books[g.symbol_id].n_lvl != 0 &&
+                       idx_live(idx, idx_mask, (static_cast<unsigned long long>(g.symbol_id) + 1) << 32 | g.oid_id);
   const unsigned long long km = mix64((static_cast<unsigned long long>(g.symbol_id) << 40) ^
                                       (static_cast<unsigned long long>(g.uuid_id) << 20) ^ mix64(g.oid_id));
   const unsigned long long mine = ((km >> 32) | 0x80000000ull) << 32 | i;
@@ -279,7 +291,7 @@ __global__ void k_adm(const gome_order* ord, uint32_t n, unsigned long long* tab
     }
     h = (h + 1) & mask;
   }
-  slot[i] = h;
+  slot[i] = h | (resting ? ADM_RESTING : 0u);
 }
 
 // ============================================================== prepared records
@@ -299,13 +311,56 @@ static_assert(sizeof(Prep) == 32, "Prep layout");
 // reads one flag instead of chasing slot -> minimum.  Runs beside the radix sort.
 // A record whose admission the host resolved (GOME_ORD_ADM_HOST: the consumer keeps the
 // reference's pre-pool markers itself) carries the verdict in GOME_ORD_ADMITTED.
-__global__ void k_adm_flag(const gome_order* ord, uint32_t n, uint32_t* slot, const unsigned long long* tab) {
+//
+// Duplicate oids.  The reference names a resting node S:node:<oid> with
+// no uuid (ordernode.go:110-112, nodelink.go:119-122) and assumes oids unique per symbol
+// (README.md:27); a second live node with the same name corrupts its FIFO.  The boundary rule,
+// the same on every path and in the oracle: an admitted ADD whose (S, oid) rests in the book at
+// batch start (k_adm's index probe) or was carried by an earlier admitted ADD of the same batch
+// is not applied (dropped like an ADD without a marker), counted (gome_stats.n_dup_oid) and its
+// batch index reported (gome_dup_records).  So after k_adm_flag, an admitted ADD's slot holds
+// its (S, oid) slot of `dup` (whose low half ends as the smallest admitted index of the key),
+// plus ADM_RESTING; every other record NIL.  k_dup_flag leaves the final 0 / 1 verdict.
+__global__ void k_adm_flag(const gome_order* ord, uint32_t n, uint32_t* slot, const unsigned long long* tab,
+                           unsigned long long* dup, uint32_t mask) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const uint8_t action = ord[i].action;
-  const uint16_t fl = ord[i].flags;
-  if (fl & GOME_ORD_ADM_HOST) slot[i] = (action == GOME_ADD && (fl & GOME_ORD_ADMITTED)) ? 1u : 0u;
-  else slot[i] = (action == GOME_ADD && static_cast<uint32_t>(tab[slot[i]]) == i) ? 1u : 0u;
+  const gome_order g = ord[i];
+  const uint32_t s = slot[i];
+  bool adm;
+  if (s == NIL || g.action != GOME_ADD) adm = false;
+  else if (g.flags & GOME_ORD_ADM_HOST) adm = (g.flags & GOME_ORD_ADMITTED) != 0;
+  else adm = static_cast<uint32_t>(tab[s & ~ADM_RESTING]) == i;
+  if (!adm) { slot[i] = NIL; return; }
+  const unsigned long long key = (static_cast<unsigned long long>(g.symbol_id) + 1) << 32 | g.oid_id;
+  const unsigned long long km = mix64(key ^ 0x9E3779B97F4A7C15ull);
+  const unsigned long long mine = ((km >> 32) | 0x80000000ull) << 32 | i;
+  uint32_t h = static_cast<uint32_t>(km) & mask;
+  for (uint32_t probe = 0; probe <= mask; ++probe) {
+    const unsigned long long c = atomicCAS(&dup[h], 0ull, mine);
+    if (c == 0) break;
+    if ((c >> 32) == (mine >> 32)) {
+      const gome_order q = ord[static_cast<uint32_t>(c)];
+      if (q.symbol_id == g.symbol_id && q.oid_id == g.oid_id) {
+        if (c > mine) atomicMin(&dup[h], mine);
+        break;
+      }
+    }
+    h = (h + 1) & mask;
+  }
+  slot[i] = h | (s & ADM_RESTING);
+}
+
+// Final admission verdicts (0 / 1) after the duplicate-oid rule; rejected ADDs are counted and
+// listed (list: this batch slot's index buffer, in no particular order; the host sorts it).
+__global__ void k_dup_flag(uint32_t n, uint32_t* slot, const unsigned long long* dup, Status* st, uint32_t* list) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t s = slot[i];
+  if (s == NIL) { slot[i] = 0; return; }
+  const bool rej = (s & ADM_RESTING) || static_cast<uint32_t>(dup[s & ~ADM_RESTING]) != i;
+  slot[i] = rej ? 0u : 1u;
+  if (rej) list[atomicAdd(&st->ctr[C_DUP], 1ull)] = i;
 }
 
 __global__ void k_prep(const gome_order* ord, uint32_t n, const uint32_t* sidx,

@@ -31,14 +31,14 @@
 extern "C" {
 #endif
 
-#define GOME_ABI_VERSION 4u
+#define GOME_ABI_VERSION 5u
 
 /* ---- status codes (replace the reference's swallowed errors / panics,
  *      rabbitmq.go:44-49,70-72,120-122; nodelink.go:132,142,157) ---------- */
 typedef int32_t gome_status;
 enum {
   GOME_OK = 0,
-  GOME_E_INVAL = 1,     /* input outside the exact parity domain (Q5/Q7), bad args */
+  GOME_E_INVAL = 1,     /* input outside the exact parity domain (Q5), bad args      */
   GOME_E_CAPACITY = 2,  /* a device pool (levels, nodes, index, events) is full    */
   GOME_E_DEVICE = 3,    /* HIP runtime error / no device                           */
   GOME_E_STATE = 4,     /* engine poisoned by an earlier fatal error                */
@@ -77,7 +77,8 @@ typedef struct gome_order {
   int64_t price_fx;   /* OrderNode.Price  (limit price; request price for DEL)  */
   int64_t volume_fx;  /* OrderNode.Volume (>= 0)                                */
   uint32_t symbol_id; /* interned OrderNode.Symbol, < gome_config.max_symbols    */
-  uint32_t oid_id;    /* interned OrderNode.Oid   (unique per symbol, README:27) */
+  uint32_t oid_id;    /* interned OrderNode.Oid (unique per symbol, README:27; see
+                         the duplicate-oid rule below)                            */
   uint32_t uuid_id;   /* interned OrderNode.Uuid                                 */
   uint8_t side;       /* Transaction code (see above): 1 SALE, anything else BUY */
   uint8_t action;     /* OrderNode.Action: 1 ADD, 2 DEL, anything else ignored   */
@@ -185,6 +186,9 @@ typedef struct gome_stats {
   double ms_cold;                             /* device time of k_match (cold books)      */
   uint64_t lvl_used;                          /* level slots carved from the pool so far
                                                  (released blocks are reused first)      */
+  uint64_t n_dup_oid;                         /* ADDs of the batch rejected by the
+                                                 duplicate-oid rule (ABI >= 5; also counted
+                                                 in n_dropped)                           */
 } gome_stats;
 
 typedef struct gome_engine gome_engine;
@@ -199,7 +203,17 @@ uint32_t gome_abi_version(void);
 /* Every submit applies its batch after every earlier one (per symbol in record order, as
  * the reference's single consumer, rabbitmq.go:116).  Events of a batch are published in
  * (sequence number, fill_idx) order.  A batch rejected with GOME_E_INVAL (a record outside
- * the exact domain) leaves the book unchanged. */
+ * the exact domain) leaves the book unchanged.
+ *
+ * Duplicate oids (ABI >= 5).  The reference names a resting node
+ * S:node:<oid> without the uuid (ordernode.go:110-112, nodelink.go:119-122) and assumes oids
+ * unique per symbol (README.md:27): a second live node of the same name corrupts the FIFO.
+ * Rule, on every path: an ADD that admission lets through (batch rule or GOME_ORD_ADMITTED)
+ * is NOT applied when its (symbol, oid) rests in the book at the start of its batch, or was
+ * carried by an earlier admitted ADD of the same batch.  It publishes nothing, as an ADD
+ * without an admission marker (engine.go:58); gome_stats.n_dup_oid counts the batch's
+ * rejections and gome_dup_records lists their batch indices.  (Reusing an oid once its node
+ * is gone, in a later batch, is an ordinary ADD.) */
 
 /* Apply one batch of host records (replaces n calls of DoOrder, engine.go:46).
  * Synchronous: on return the events are queued for gome_drain_events. */
@@ -211,17 +225,26 @@ gome_status gome_submit_batch(gome_engine* e, const gome_order* orders, size_t n
  * device batch not yet drained are moved to the host queue first, never dropped). */
 gome_status gome_submit_batch_device(gome_engine* e, const gome_order* dev_orders,
                                      size_t n, uint64_t seq_base, void* stream);
-/* Copy out up to cap pending events in publish order; *n_out = copied. */
+/* Copy out up to cap pending events in publish order; *n_out = copied.  Batches still in
+ * flight (gome_submit_batch_async) are collected into the queue first. */
 gome_status gome_drain_events(gome_engine* e, gome_event* out, size_t cap,
                               size_t* n_out);
+/* Events waiting in the drain queue (in-flight batches not included: collect them first, or
+ * call gome_drain_events, which does). */
 size_t gome_pending_events(const gome_engine* e);
-/* Device pointer + count of the last device batch's events (valid until next submit). */
+/* Device pointer + count of the last gome_submit_batch_device batch's events (valid until the
+ * next submit; host batches, synchronous or in flight, are not among them). */
 gome_status gome_device_events(gome_engine* e, const gome_event** dev_ptr,
                                size_t* n);
 /* A device-side consumer has taken the last device batch's events (read through
  * gome_device_events): the next submit need not move them to the host drain queue. */
 gome_status gome_release_device_events(gome_engine* e);
+/* Counters of the last batch that finished (gome_submit_batch*, gome_collect or a synchronous
+ * call's collection); batches still in flight are not included. */
 gome_status gome_get_stats(const gome_engine* e, gome_stats* out);
+/* Batch indices (ascending) of the ADDs the duplicate-oid rule rejected in the last finished
+ * batch (ABI >= 5); *n_out = their number (only cap are written). */
+gome_status gome_dup_records(const gome_engine* e, uint32_t* out, size_t cap, size_t* n_out);
 /* Diagnostics (tests, tuning): the last batch's hot-book routing, GOME_DEBUG_FLOW_WORDS words
  * per candidate book, longest segment first: {flow kind (0 legacy / cold, 1 ADD-only flow,
  * 2 flow with cancels), cancel-prep decline bits, symbol, orders, DELs, levels, 32-bit plan,
@@ -239,8 +262,11 @@ gome_status gome_debug_peek(gome_engine* e, uint32_t which, uint64_t offset, uin
  * copy stream while the device applies the other batch, so PCIe hides under matching.
  * At most GOME_MAX_INFLIGHT batches are in flight; `orders` must stay valid and
  * unchanged until the batch is collected (memory from gome_host_alloc is page-locked,
- * which makes the copy asynchronous).  Any synchronous call first collects every
- * in-flight batch into the drain queue. */
+ * which makes the copy asynchronous).  gome_submit_batch, gome_submit_batch_device,
+ * gome_drain_events, gome_snapshot_*, gome_load_books and gome_debug_* first collect every
+ * in-flight batch into the drain queue.  A batch collected that way that was rejected
+ * (GOME_E_INVAL, nothing applied) does not fail that call: the call goes on and the failure
+ * is kept for gome_take_deferred. */
 #define GOME_MAX_INFLIGHT 2u
 gome_status gome_submit_batch_async(gome_engine* e, const gome_order* orders, size_t n,
                                     uint64_t seq_base);
@@ -251,6 +277,9 @@ gome_status gome_submit_batch_async(gome_engine* e, const gome_order* orders, si
 gome_status gome_collect(gome_engine* e, const gome_event** events, size_t* n_events,
                          gome_stats* stats);
 size_t gome_inflight(const gome_engine* e);
+/* The first failure of an in-flight batch that a synchronous call collected since the last
+ * gome_take_deferred (its message then in gome_last_error), or GOME_OK; clears it. */
+gome_status gome_take_deferred(gome_engine* e);
 gome_status gome_host_alloc(gome_engine* e, size_t bytes, void** out);
 void gome_host_free(gome_engine* e, void* p);
 
@@ -263,6 +292,21 @@ gome_status gome_snapshot_levels(gome_engine* e, uint32_t symbol_id,
 /* Nodes of the FIFO at one price, head first. */
 gome_status gome_snapshot_fifo(gome_engine* e, uint32_t symbol_id, int64_t price_fx,
                                gome_node* out, size_t cap, size_t* n_out);
+
+/* Top-of-book digest of one book (ABI >= 5): what GetReverseDepth's first level reports for a
+ * taker of either side (nodepool.go:86-115) — the highest S:BUY member and the lowest S:SALE
+ * member with their S:depth fields and FIFO lengths.  flags bit 0: a bid exists, bit 1: an
+ * ask exists (prices and depths are 0 otherwise).  n_levels = the book's observable levels
+ * (as gome_snapshot_levels counts them).  The publisher's per-GPU depth summary. */
+typedef struct gome_tob {
+  uint32_t symbol_id;
+  uint32_t n_levels;
+  int64_t bid_price_fx, bid_depth_fx;
+  int64_t ask_price_fx, ask_depth_fx;
+  uint32_t bid_nodes, ask_nodes;
+  uint32_t flags, pad;
+} gome_tob;
+gome_status gome_top_of_book(gome_engine* e, const uint32_t* symbols, size_t n, gome_tob* out);
 
 /* ---- book state load (restart from Redis) ------------------- */
 /* The reference restarts from whatever its Redis holds (nodepool.go:14-115,
@@ -296,8 +340,8 @@ gome_status gome_fixed_from_scaled(double scaled, int64_t* out);
  * engine.MatchResult, byte-identical).  Strings are the host's interned names;
  * `taker` is the record of the event's taker.  tx_table maps Transaction codes
  * (gome_order.side, gome_event.maker_side) to the raw int32 Transaction values to echo;
- * NULL = identity (codes 0..255 are the values).  Returns bytes written (excl. NUL) or
- * a negative value if cap is too small. */
+ * NULL = identity (codes 0..255 are the values).  Returns bytes written (excl. NUL), or
+ * -(bytes needed incl. NUL) when cap is too small, or INT64_MIN on a NULL argument. */
 int64_t gome_render_match_result(const gome_event* ev, const gome_order* taker,
                                  uint32_t accuracy, const char* symbol,
                                  const char* taker_uuid, const char* taker_oid,
@@ -320,7 +364,7 @@ int64_t gome_render_events(const gome_event* ev, size_t n, const gome_order* bat
  * the ADD that rested with its remaining volume, IsFirst / IsLast / PrevNode / NextNode from
  * its FIFO neighbours (NULL = none).  `transaction` is the raw int32 value.  Used by the
  * snapshot writer (gome_amd/snapshot.py).  Returns bytes written (excl.
- * NUL) or a negative value. */
+ * NUL), or -(bytes needed incl. NUL) when cap is too small, or INT64_MIN on a NULL argument. */
 int64_t gome_render_link_node(const char* symbol, int64_t price_fx, int32_t transaction, int64_t volume_fx,
                               uint32_t accuracy, const char* uuid, const char* oid,
                               const char* prev_oid, const char* next_oid, char* buf, size_t cap);

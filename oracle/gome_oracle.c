@@ -22,7 +22,10 @@
  *   - an (S, oid) -> node index standing in for HGET S:link:<p> S:node:<oid>
  *     (engine.go:92-93), with the price compared explicitly (Q3);
  *   - per-batch admission markers (S:comparison, nodepool.go:14-28) under the
- *     deterministic ingress model of literal.run_batches (Q4).
+ *     deterministic ingress model of literal.run_batches (Q4);
+ *   - the boundary's duplicate-oid rule (Q7, gome_abi.h): an admitted ADD whose (S, oid)
+ *     rests at batch start, or was carried by an earlier admitted ADD of the batch, is not
+ *     applied (literal.py's consumer applies the same rule before DoOrder).
  * All arithmetic is int64 on value*10^accuracy (exact on the parity domain).
  */
 #include <stdint.h>
@@ -68,6 +71,10 @@ typedef struct oracle {
   uint64_t* adm; /* stores hashed (sym,uuid,oid) triple as two words */
   uint32_t* adm3;
   uint64_t admcap;
+  uint64_t* dupk;   /* (S, oid) keys of the batch's admitted ADDs (Q7) */
+  uint8_t* rest0;   /* per record: an ADD whose (S, oid) rests at batch start */
+  uint32_t* dups;   /* batch indices rejected by the Q7 rule */
+  uint64_t ndups, rest0cap;
   /* events */
   gome_event* ev;
   uint64_t nev, capev;
@@ -279,6 +286,16 @@ static int adm_first(oracle* o, const gome_order* r) {
   }
 }
 
+/* First admitted ADD of (S, oid) in this batch?  (Q7, the earlier-in-batch half) */
+static int dup_first(oracle* o, uint64_t key) {
+  uint64_t m = o->admcap - 1, h = mix64(key ^ 0x9E3779B97F4A7C15ULL) & m;
+  for (;;) {
+    if (!o->dupk[h]) { o->dupk[h] = key; return 1; }
+    if (o->dupk[h] == key) return 0;
+    h = (h + 1) & m;
+  }
+}
+
 /* ---------------------------------------------------------------- API */
 oracle* oracle_create(uint32_t max_symbols) {
   oracle* o = (oracle*)calloc(1, sizeof(oracle));
@@ -292,6 +309,7 @@ void oracle_destroy(oracle* o) {
   if (!o) return;
   for (uint32_t s = 0; s < o->max_symbols; ++s) free(o->books[s].lv);
   free(o->books); free(o->nodes); free(o->idx); free(o->adm); free(o->adm3); free(o->ev);
+  free(o->dupk); free(o->rest0); free(o->dups);
   free(o);
 }
 
@@ -304,12 +322,25 @@ int oracle_submit(oracle* o, const gome_order* r, uint64_t n) {
   uint64_t need = 16;
   while (need < 2 * n) need <<= 1;
   if (need > o->admcap) {
-    free(o->adm); free(o->adm3);
+    free(o->adm); free(o->adm3); free(o->dupk);
     o->admcap = need;
     o->adm = (uint64_t*)malloc(need * sizeof(uint64_t));
     o->adm3 = (uint32_t*)malloc(need * 3 * sizeof(uint32_t));
+    o->dupk = (uint64_t*)malloc(need * sizeof(uint64_t));
+  }
+  if (n > o->rest0cap) {
+    free(o->rest0); free(o->dups);
+    o->rest0cap = n;
+    o->rest0 = (uint8_t*)malloc(n);
+    o->dups = (uint32_t*)malloc(n * sizeof(uint32_t));
   }
   memset(o->adm, 0, o->admcap * sizeof(uint64_t));
+  memset(o->dupk, 0, o->admcap * sizeof(uint64_t));
+  /* Q7: which ADDs' (S, oid) rest in the book as the batch starts */
+  for (uint64_t i = 0; i < n; ++i)
+    o->rest0[i] = r[i].action == GOME_ADD && idx_find(o, okey(r[i].symbol_id, r[i].oid_id)) >= 0;
+  o->ndups = 0;
+  o->st.n_dup_oid = 0;
   for (uint64_t i = 0; i < n; ++i) {
     const gome_order* q = &r[i];
     o->st.n_orders++;
@@ -318,6 +349,12 @@ int oracle_submit(oracle* o, const gome_order* r, uint64_t n) {
       int adm = adm_first(o, q); /* engine.go:58-62 (batch model) */
       if (q->flags & GOME_ORD_ADM_HOST) adm = (q->flags & GOME_ORD_ADMITTED) != 0; /* host markers */
       if (!adm) { o->st.n_dropped++; continue; }
+      if (!dup_first(o, okey(q->symbol_id, q->oid_id)) || o->rest0[i]) { /* Q7 */
+        o->st.n_dropped++;
+        o->st.n_dup_oid++;
+        o->dups[o->ndups++] = (uint32_t)i;
+        continue;
+      }
       do_add(o, q, (uint32_t)i);
     } else if (q->action == GOME_DEL) {
       o->st.n_del++;
@@ -330,6 +367,11 @@ int oracle_submit(oracle* o, const gome_order* r, uint64_t n) {
 }
 
 uint64_t oracle_num_events(const oracle* o) { return o->nev; }
+/* Batch indices (ascending) of the last batch's Q7 rejections. */
+uint64_t oracle_dup_records(const oracle* o, uint32_t* out, uint64_t cap) {
+  for (uint64_t i = 0; i < o->ndups && i < cap; ++i) out[i] = o->dups[i];
+  return o->ndups;
+}
 const gome_event* oracle_events(const oracle* o) { return o->ev; }
 void oracle_clear_events(oracle* o) { o->nev = 0; }
 void oracle_get_stats(const oracle* o, gome_stats* s) { *s = o->st; }

@@ -27,12 +27,16 @@ Third-party behaviour restated here (not vendored in the reference; go.mod):
   github.com/go-redis/redis/v8 v8.0.0-beta.8  float64 args -> strconv 'f', -1
   Redis server HINCRBYFLOAT                   long double add, "%.17Lf" trimmed
   Go encoding/json                             struct field order, shortest floats,
-                                               'e' form outside [1e-6, 1e21), HTML escaping
+                                               'e' form outside [1e-6, 1e21), HTML escaping;
+                                               Unmarshal: syntax error -> nothing decoded,
+                                               mistyped / overflowing / null field -> left
+                                               zero, keys matched case-insensitively
 """
 from __future__ import annotations
 
 import json
 import math
+import re
 from decimal import Decimal, getcontext
 from fractions import Fraction
 
@@ -115,6 +119,68 @@ NODE_FIELDS = (
     ("OrderDepthHashKey", "str"), ("OrderDepthHashField", "str"),
 )
 _ZERO = {"int": 0, "str": "", "float": 0.0, "bool": False}
+_INT_BITS = {"Action": 8, "Transaction": 32, "Accuracy": 64}  # int8 / int32 / int (ordernode.go:10-16)
+
+
+class _Num(str):
+    """A JSON number's literal text (Go decodes numbers from the literal)."""
+
+
+class _Obj(list):
+    """A JSON object as its (key, value) pairs in order."""
+
+
+def _no_constant(name):
+    raise ValueError(f"invalid character in JSON: {name}")  # Go has no NaN / Infinity literals
+
+
+def _go_field_value(kind: str, name: str, v):
+    """encoding/json's literalStore for one struct field (go1.x decode.go): returns the value, or
+    None when Go leaves the field unchanged (null, or an UnmarshalTypeError it records and skips)."""
+    if v is None:
+        return None  # null into a non-pointer field has no effect
+    if kind == "str":  # (a lone surrogate escape decodes to U+FFFD)
+        return re.sub("[\ud800-\udfff]", "\ufffd", v) if isinstance(v, str) and not isinstance(v, _Num) else None
+    if kind == "bool":
+        return v if isinstance(v, bool) else None
+    if not isinstance(v, _Num):
+        return None
+    if kind == "float":
+        f = float(v)  # strconv.ParseFloat(s, 64): out of range -> ErrRange -> skipped
+        return None if math.isinf(f) else f
+    # kind == "int": strconv.ParseInt(s, 10, 64) (no fraction or exponent), then OverflowInt
+    try:
+        n = int(v, 10)
+    except ValueError:
+        return None
+    b = _INT_BITS[name]
+    return n if -(1 << (b - 1)) <= n < (1 << (b - 1)) else None
+
+
+def go_unmarshal_order_node(body: str) -> "OrderNode":
+    """json.Unmarshal(body, &OrderNode{}) as rabbitmq.go:118-121 runs it (the error is printed
+    and DoOrder still runs): a syntax error decodes nothing (zero node, Action 0, ignored by
+    DoOrder); otherwise every field whose JSON value fits its Go type is set, keys matched
+    exactly or case-insensitively, later duplicates winning; a field of the wrong type, an
+    overflowing number or a null stays zero."""
+    node = OrderNode()
+    try:
+        d = json.loads(body, parse_int=_Num, parse_float=_Num, parse_constant=_no_constant,
+                       object_pairs_hook=_Obj)
+    except (ValueError, TypeError):
+        return node
+    if not isinstance(d, _Obj):
+        return node  # null: no effect; any other top-level type: UnmarshalTypeError
+    exact = {n: (n, k) for n, k in NODE_FIELDS}
+    folded = {n.casefold(): (n, k) for n, k in NODE_FIELDS}
+    for key, v in d:
+        f = exact.get(key) or folded.get(key.casefold())
+        if f is None:
+            continue
+        x = _go_field_value(f[1], f[0], v)
+        if x is not None:
+            setattr(node, f[0], x)
+    return node
 
 
 class OrderNode:
@@ -448,9 +514,37 @@ class GomeLiteral:
         self.PublishNewOrder(n)
 
     def consume(self):  # rabbitmq.go:116-125, one message at a time
+        """One drained batch.  Before DoOrder, the batching consumer's duplicate-oid rule (the
+        boundary's, gome_abi.h): an ADD that holds its admission marker
+        but whose (Symbol, Oid) rests in the book as the batch starts, or was carried by an
+        earlier admitted ADD of the batch, is consumed (marker cleared, engine.go:62) and not
+        applied.  `self.dups` = the batch indices of such ADDs."""
         q, self.do_order_q = self.do_order_q, []
-        for body in q:
-            self.DoOrder(OrderNode.from_json(body))
+        resting = self.resting_oids()
+        seen = set()
+        self.dups = []
+        for i, body in enumerate(q):
+            node = go_unmarshal_order_node(body)
+            if node.Action == ADD and self.ExistsPrePool(node):
+                key = (node.Symbol, node.Oid)
+                if key in resting or key in seen:
+                    self.DeletePrePool(node)
+                    self.dups.append(i)
+                    continue
+                seen.add(key)
+            self.DoOrder(node)
+
+    def resting_oids(self) -> set:
+        """(Symbol, Oid) of every node resting in a FIFO (an S:node:<oid> field of S:link:<p>)."""
+        out = set()
+        for key, hv in self.cache.h.items():
+            if ":link:" not in key:
+                continue
+            for f, v in hv.items():
+                if f not in ("f", "l"):
+                    nd = OrderNode.from_json(v)
+                    out.add((nd.Symbol, nd.Oid))
+        return out
 
     def take_results(self) -> list[str]:
         out, self.match_q = self.match_q, []

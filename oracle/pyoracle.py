@@ -14,17 +14,10 @@ _ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if _ROOT not in sys.path:
     sys.path.insert(0, _ROOT)
 
+from gome_amd.abi import Stats as _Stats  # noqa: E402  (the gome_stats layout; no library load)
 from gome_amd.workload import EVENT_DTYPE, LEVEL_DTYPE, NODE_DTYPE, ORDER_DTYPE  # noqa: E402
 
 LIB = os.path.join(_ROOT, "oracle", "build", "liboracle.so")
-
-
-class _Stats(C.Structure):
-    _fields_ = [(n, C.c_uint64) for n in (
-        "n_orders", "n_add", "n_del", "n_dropped", "n_fills", "n_cancels", "n_rests",
-        "n_events", "n_resting", "n_levels", "max_segment", "n_segments")] + [
-        ("ms_total", C.c_double), ("ms_match", C.c_double), ("ms_hot", C.c_double),
-        ("n_hot", C.c_uint64)]
 
 
 _lib = None
@@ -55,6 +48,8 @@ def lib():
         L.oracle_snapshot_levels.restype = C.c_uint64
         L.oracle_snapshot_fifo.argtypes = [VP, C.c_uint32, C.c_int64, VP, C.c_uint64]
         L.oracle_snapshot_fifo.restype = C.c_uint64
+        L.oracle_dup_records.argtypes = [VP, VP, C.c_uint64]
+        L.oracle_dup_records.restype = C.c_uint64
         _lib = L
     return _lib
 
@@ -85,6 +80,14 @@ class Oracle:
         s = _Stats()
         self.L.oracle_get_stats(self.h, C.byref(s))
         return {n: getattr(s, n) for n, _ in s._fields_}
+
+    def dup_records(self) -> np.ndarray:
+        """Batch indices of the last batch's ADDs rejected by the duplicate-oid rule (Q7)."""
+        n = self.L.oracle_dup_records(self.h, None, 0)
+        out = np.zeros(n, np.uint32)
+        if n:
+            self.L.oracle_dup_records(self.h, out.ctypes.data, n)
+        return out
 
     def resting(self) -> int:
         return self.L.oracle_resting(self.h)

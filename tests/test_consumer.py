@@ -32,6 +32,9 @@ class _OracleEngine:
         ev, self._ev = self._ev, None
         return ev
 
+    def stats(self):
+        return self.o.stats()
+
 
 def _schedule(seed, n_ops=900, symbols=("eth2usdt", "btc2usdt", "a<b&c")):
     """Random interleaving of gRPC calls ("add"/"del", req) and consumption ("take", k)."""
@@ -95,14 +98,16 @@ def _run(ops, engine, lit_json: bool):
             lit.grpc_delete_order(arg)
             q.append(lit.do_order_q[-1]) if lit_json else ing.delete_order(arg)
         else:
+            # the reference consumes one message at a time; the duplicate-oid rule (Q7) is per
+            # batch, so the literal consumes the same batches the consumer drains
             k = min(arg, len(lit.do_order_q))
-            head, lit.do_order_q = lit.do_order_q[:k], lit.do_order_q[k:]
-            saved, lit.do_order_q = lit.do_order_q, head
-            lit.consume()
-            lit.do_order_q = saved
-            lit_out += lit.take_results()
             while k:
                 m = min(k, cons.max_batch)
+                head, lit.do_order_q = lit.do_order_q[:m], lit.do_order_q[m:]
+                saved, lit.do_order_q = lit.do_order_q, head
+                lit.consume()
+                lit.do_order_q = saved
+                lit_out += lit.take_results()
                 cons.process(q[:m])
                 del q[:m]
                 k -= m
@@ -139,3 +144,249 @@ def test_consumer_matches_literal_gpu(seed):
     lit_out, got, cons = _run(_schedule(200 + seed, n_ops=1500), Engine(max_symbols=3, max_batch=128), True)
     assert len(lit_out) > 100
     assert got == lit_out
+
+
+# ---- Go json.Unmarshal at the boundary ----------------------
+def _msg(action=1, sym="s", uuid="u", oid="1", tx=0, price="50000000", vol="100000000", extra=""):
+    # (Accuracy is the server's constant in every message the gRPC side writes, ordernode.go:56-58;
+    # the renderer echoes the engine's accuracy, so the messages carry it)
+    return ('{"Action":%s,"Uuid":"%s","Oid":"%s","Symbol":"%s","Transaction":%s,"Price":%s,"Volume":%s,'
+            '"Accuracy":8%s}' % (action, uuid, oid, sym, tx, price, vol, extra))
+
+
+# messages that decode partially under Go's encoding/json: the mistyped field stays zero and the
+# message is still dispatched (rabbitmq.go:118-124)
+ODD_MESSAGES = [
+    _msg(oid="1", price='"abc"'),                      # Price string -> 0: an ADD at price 0
+    _msg(oid="2", price="null"),                       # null -> no effect -> 0
+    _msg(oid="3", tx='"x"', price="60000000"),         # Transaction string -> 0 (BUY)
+    _msg(oid="4", action="300"),                       # int8 overflow -> Action 0: ignored
+    _msg(oid="5", action="1.0"),                       # not an integer literal -> Action 0
+    _msg(oid="6", tx="1", price="40000000", vol="1e400"),  # float overflow -> Volume 0 (Q6)
+    _msg(oid="7", tx="1", price="40000000", vol="30000000", extra=',"price":45000000'),  # later key wins
+    '{"action":1,"uuid":"u","oid":"8","symbol":"s","transaction":1,"price":45000000,"volume":5000000,"accuracy":8}',
+    _msg(oid="9", tx="4294967297"),                    # int32 overflow -> 0 (BUY)
+    _msg(oid="10", price="true"),                      # bool into float -> 0
+    '[1,2,3]', 'null', '{"Action":1', '{"Action":NaN}',  # non-object / syntax errors: zero node
+    _msg(oid="11", sym='a\\ud800b', tx="1", price="50000000"),  # lone surrogate -> U+FFFD
+    _msg(oid="12", price="5e7", vol="1E8"),            # exponent floats are fine for float64
+]
+
+
+def _odd_schedule():
+    ops = []
+    for m in ODD_MESSAGES:
+        ops.append(("raw", m))
+    ops.append(("take", 10**9))
+    # then ordinary traffic crossing what rested
+    for k in range(20):
+        ops.append(("add", dict(uuid="v", oid=str(100 + k), symbol="s", transaction=k % 2,
+                                price=0.4 + 0.05 * (k % 4), volume=0.5)))
+    ops.append(("take", 10**9))
+    return ops
+
+
+def _run_raw(ops, engine):
+    """Like _run, but "raw" ops put a message body on the queue as the reference's gRPC side
+    would have (its admission marker set for the (Symbol, Uuid, Oid) Go decodes from it)."""
+    from oracle.literal import go_unmarshal_order_node
+    lit = GomeLiteral()
+    pre, sink, names = PrePool(), MatchSink(), Names()
+    q: list = []
+    cons = BatchingConsumer(engine, pre, sink, names, max_batch=engine.max_batch)
+    lit_out = []
+    for op, arg in ops:
+        if op == "raw":
+            nd = go_unmarshal_order_node(arg)
+            nd.SetOrderHashKey()
+            nd.SetNodeName()
+            nd.SetDepthHashKey()
+            nd.SetNodeLink()
+            nd.SetListZsetKey()
+            lit.SetPrePool(nd)
+            pre.set(nd.Symbol, nd.Uuid, nd.Oid)
+            lit.do_order_q.append(nd.to_json())  # the literal consumes Go's view of the message
+            q.append(arg)
+        elif op == "add":
+            lit.grpc_do_order(arg)
+            pre.set(arg["symbol"], arg["uuid"], arg["oid"])
+            q.append(lit.do_order_q[-1])
+        else:
+            k = min(arg, len(q))
+            while k:
+                m = min(k, cons.max_batch)
+                head, lit.do_order_q = lit.do_order_q[:m], lit.do_order_q[m:]
+                saved, lit.do_order_q = lit.do_order_q, head
+                lit.consume()
+                lit.do_order_q = saved
+                lit_out += lit.take_results()
+                cons.process(q[:m])
+                del q[:m]
+                k -= m
+    return lit_out, sink.q, cons
+
+
+def test_decode_like_go_unmarshal():
+    from gome_amd.consumer import decode_order_node
+    from oracle.literal import go_unmarshal_order_node
+    for m in ODD_MESSAGES:
+        a = decode_order_node(m)
+        b = go_unmarshal_order_node(m)
+        assert a == {k: getattr(b, k) for k in a}, m
+    d = decode_order_node(ODD_MESSAGES[0])
+    assert d["Action"] == 1 and d["Price"] == 0.0 and d["Volume"] == 1e8
+    assert decode_order_node(ODD_MESSAGES[3])["Action"] == 0
+    assert decode_order_node(ODD_MESSAGES[6])["Price"] == 45000000.0
+    assert decode_order_node(ODD_MESSAGES[7])["Oid"] == "8"
+    assert decode_order_node(ODD_MESSAGES[-2])["Symbol"] == "a�b"
+
+
+def test_consumer_odd_messages_match_literal_cpu():
+    lit_out, got, cons = _run_raw(_odd_schedule(), _OracleEngine(4, 64))
+    assert len(lit_out) > 5
+    assert got == lit_out
+    assert cons.consumed == len(ODD_MESSAGES) + 20 and cons.rejected == 0
+
+
+class _RefusingEngine(_OracleEngine):
+    """Refuses the first `k` submits as the engine's pool-headroom check does (E_CAPACITY before
+    anything is applied)."""
+
+    def __init__(self, n_sym, max_batch, k):
+        super().__init__(n_sym, max_batch)
+        self.k = k
+
+    def submit(self, rec, seq_base=0):
+        from gome_amd.abi import GOME_E_CAPACITY, GomeError
+        if self.k:
+            self.k -= 1
+            raise GomeError(GOME_E_CAPACITY, "batch rejected before it was applied")
+        super().submit(rec, seq_base)
+
+
+def test_consumer_batch_refused_then_resubmitted_cpu():
+    """a batch the engine refuses leaves the pre-pool markers untouched, so processing
+    the same messages again admits exactly as the first attempt would have."""
+    from gome_amd.abi import GomeError
+    ops = _schedule(321, n_ops=300)
+    lit_out, want, _ = _run(ops, _OracleEngine(3, 64), True)
+    lit = GomeLiteral()
+    pre, sink, names = PrePool(), MatchSink(), Names()
+    cons = BatchingConsumer(_RefusingEngine(3, 64, 0), pre, sink, names, max_batch=64)
+    q: list = []
+    refused = 0
+    for op, arg in ops:
+        if op == "add":
+            lit.grpc_do_order(arg)
+            pre.set(arg["symbol"], arg["uuid"], arg["oid"])
+            q.append(lit.do_order_q.pop())
+        elif op == "del":
+            lit.grpc_delete_order(arg)
+            q.append(lit.do_order_q.pop())
+        else:
+            k = min(arg, len(q))
+            while k:
+                m = min(k, 64)
+                cons.eng.k = 1  # every batch is refused once
+                n_pre = len(pre)
+                with pytest.raises(GomeError):
+                    cons.process(q[:m])
+                assert len(pre) == n_pre  # no marker consumed
+                refused += 1
+                cons.process(q[:m])
+                del q[:m]
+                k -= m
+    assert refused > 5
+    assert sink.q == want == lit_out
+
+
+def test_render_events_long_ids():
+    """ids longer than any fixed staging buffer render (no 'unknown id' error); a
+    short buffer returns -(bytes needed)."""
+    import ctypes as C
+    from gome_amd.abi import load_library
+    from gome_amd.workload import EVENT_DTYPE, ORDER_DTYPE
+    lib = load_library()
+    lib.gome_render_events.restype = C.c_int64
+    long_oid = "o" * 40000
+    rec = np.zeros(1, ORDER_DTYPE)
+    rec[0] = (5 * 10**7, 10**8, 0, 0, 0, 0, 1, 0)
+    ev = np.zeros(1, EVENT_DTYPE)
+    ev[0]["kind"], ev[0]["price_fx"], ev[0]["maker_volume_fx"], ev[0]["taker_volume_fx"] = 2, 5 * 10**7, 10**8, 10**8
+    ev[0]["maker_is_last"] = 1
+    tab = lambda *s: (C.c_char_p * len(s))(*[x.encode() for x in s])
+    sym, uu, oo = tab("s"), tab("u"), tab(long_oid)
+    args = lambda buf, cap: (ev.ctypes.data, 1, rec.ctypes.data, 1, 0, 8, C.cast(sym, C.c_void_p), 1,
+                             C.cast(uu, C.c_void_p), 1, C.cast(oo, C.c_void_p), 1, None, buf, cap)
+    need = lib.gome_render_events(*args(None, 0))
+    assert need < 0 and -need > 2 * 40000
+    buf = C.create_string_buffer(-need)
+    n = lib.gome_render_events(*args(buf, -need))
+    assert n == -need
+    line = buf.raw[:n].decode()
+    assert line.endswith("}\n") and line.count(long_oid) == 6  # Oid, NodeName and OrderHashField, twice
+
+
+@pytest.mark.gpu
+def test_consumer_odd_messages_match_literal_gpu():
+    from gome_amd.abi import Engine
+    lit_out, got, cons = _run_raw(_odd_schedule(), Engine(max_symbols=4, max_batch=64))
+    assert len(lit_out) > 5 and got == lit_out
+
+
+@pytest.mark.gpu
+def test_consumer_capacity_refusal_then_bigger_engine_gpu():
+    """A real E_CAPACITY refusal (pool headroom, nothing applied): the markers survive, and the
+    same messages processed by an engine with larger pools publish what the literal publishes."""
+    from gome_amd.abi import GOME_E_CAPACITY, Engine, GomeError
+    ops = [op for op in _schedule(77, n_ops=400) if op[0] != "take"] + [("take", 10**9)]
+    lit_out, want, _ = _run(ops, _OracleEngine(3, 512), True)
+    lit = GomeLiteral()
+    pre, sink = PrePool(), MatchSink()
+    q = []
+    for op, arg in ops[:-1]:
+        (lit.grpc_do_order if op == "add" else lit.grpc_delete_order)(arg)
+        if op == "add":
+            pre.set(arg["symbol"], arg["uuid"], arg["oid"])
+        q.append(lit.do_order_q.pop())
+    small = Engine(max_symbols=3, max_batch=512, max_nodes=16, max_levels=1 << 12)
+    cons = BatchingConsumer(small, pre, sink, max_batch=512)
+    n_pre = len(pre)
+    with pytest.raises(GomeError) as ei:
+        cons.process(q)
+    assert ei.value.status == GOME_E_CAPACITY and len(pre) == n_pre and sink.q == []
+    cons.eng = Engine(max_symbols=3, max_batch=512)
+    cons.process(q)
+    assert sink.q == want == lit_out
+
+
+# ---- multi-GPU routing (gome_amd/router.py, SURVEY §8e) ------------------------------------
+@pytest.mark.parametrize("world", [2, 4])
+def test_consumer_through_router_matches_literal_cpu(world):
+    """The consumer in front of N handles (symbols owned by load rank mod N; with 3 symbols and
+    N = 4 one handle never gets a record): the merged publish stream is byte-identical."""
+    from gome_amd.router import Router, owner_table
+    r = Router([_OracleEngine(3, 64) for _ in range(world)], owner_table(3, world, np.array([0, 1, 2])))
+    lit_out, got, cons = _run(_schedule(400 + world), r, True)
+    assert len(lit_out) > 100 and got == lit_out
+    r.close()
+
+
+def test_router_hash_owner_for_unknown_symbols():
+    from gome_amd.router import owner_table
+    own = owner_table(1000, 4, np.array([5, -1, 7]))
+    assert own[0] == 1 and own[2] == 3
+    assert set(own[3:].tolist()) == {0, 1, 2, 3}
+    assert np.array_equal(own, owner_table(1000, 4, np.array([5, -1, 7])))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 4])
+def test_consumer_through_router_matches_literal_gpu(world):
+    from gome_amd.abi import Engine
+    from gome_amd.router import Router, owner_table
+    r = Router([Engine(max_symbols=3, max_batch=128) for _ in range(world)],
+               owner_table(3, world, np.array([0, 1, 2])))
+    lit_out, got, cons = _run(_schedule(500 + world, n_ops=1500), r, True)
+    assert len(lit_out) > 100 and got == lit_out
+    r.close()

@@ -1,0 +1,197 @@
+"""Duplicate oids — the boundary rule of include/gome/gome_abi.h.
+
+The reference names a resting node S:node:<oid> without its uuid (ordernode.go:110-112,
+nodelink.go:119-122) and assumes oids unique per symbol (README.md:27); a second live node of the
+same name corrupts its FIFO.  Rule: an admitted ADD whose (symbol, oid) rests in the book at the
+start of its batch, or was carried by an earlier admitted ADD of the same batch, is not applied,
+counted (gome_stats.n_dup_oid) and listed (gome_dup_records).  The literal transliteration applies
+it in its consumer before DoOrder (oracle/literal.py GomeLiteral.consume), the C oracle in
+oracle_submit, the engine in k_adm / k_adm_flag / k_dup_flag before any path sees the batch."""
+import numpy as np
+import pytest
+
+from gome_amd import workload as wl
+from oracle.literal import run_batches
+from oracle.pyoracle import Oracle
+from tests.helpers import Interner, render_events, requests_to_records
+
+ADD, DEL = 1, 2
+
+
+def _req(a, oid, uuid="u1", sym="s", tx=0, p=0.5, v=1.0):
+    return (a, dict(uuid=uuid, oid=str(oid), symbol=sym, transaction=tx, price=p, volume=v))
+
+
+# Each case: batches of requests; expected batch indices rejected per batch.
+KATS = {
+    # same batch, same (S, oid), another uuid: the second ADD is rejected (it would name the same node)
+    "same_batch_other_uuid": ([[_req(ADD, 7, "u1"), _req(ADD, 7, "u2", p=0.6)]], [[1]]),
+    # same key twice: Q4 drops the second (no marker left), not the duplicate rule
+    "same_key_is_q4": ([[_req(ADD, 7, "u1"), _req(ADD, 7, "u1")]], [[]]),
+    # resting from an earlier batch, re-added under another uuid: rejected
+    "resting_at_batch_start": ([[_req(ADD, 7, "u1")], [_req(ADD, 7, "u2", p=0.4)]], [[], [0]]),
+    # filled in an earlier batch, then reused: an ordinary ADD
+    "reuse_after_fill": ([[_req(ADD, 7, "u1", tx=1, p=0.5)], [_req(ADD, 8, "u9", p=0.5)],
+                          [_req(ADD, 7, "u2", p=0.3)]], [[], [], []]),
+    # cancelled in an earlier batch, then reused
+    "reuse_after_cancel": ([[_req(ADD, 7, "u1")], [_req(DEL, 7, "u1")], [_req(ADD, 7, "u2")]], [[], [], []]),
+    # filled within the batch, then reused in the same batch: still rejected (static rule)
+    "filled_then_reused_same_batch": ([[_req(ADD, 7, "u1", tx=1, p=0.5), _req(ADD, 8, "u9", p=0.5),
+                                        _req(ADD, 7, "u2", p=0.3)]], [[2]]),
+    # an ADD that admission drops (its DEL came first) does not count as carrying the oid
+    "dropped_add_does_not_count": ([[_req(DEL, 7, "u1"), _req(ADD, 7, "u1"), _req(ADD, 7, "u2")]], [[]]),
+    # resting at batch start, cancelled earlier in the batch: the re-ADD is still rejected
+    "resting_cancelled_then_readded": ([[_req(ADD, 7, "u1")], [_req(DEL, 7, "u1"), _req(ADD, 7, "u2")]],
+                                       [[], [1]]),
+    # another symbol's oid 7 is a different node
+    "other_symbol": ([[_req(ADD, 7, "u1", sym="a"), _req(ADD, 7, "u1", sym="b")]], [[]]),
+}
+
+
+def _literal(batches):
+    from oracle.literal import GomeLiteral
+    eng = GomeLiteral()
+    out, dups = [], []
+    for b in batches:
+        for a, r in b:
+            (eng.grpc_do_order if a == ADD else eng.grpc_delete_order)(r)
+        eng.consume()
+        out += eng.take_results()
+        dups.append(list(eng.dups))
+    return out, dups
+
+
+def _oracle(batches):
+    names = Interner()
+    for s in sorted({r["symbol"] for b in batches for _, r in b}):
+        names.id("sym", s)
+    orc = Oracle(len(names.rev["sym"]))
+    out, dups = [], []
+    for b in batches:
+        rec = requests_to_records(b, names)
+        out += render_events(orc.submit(rec), rec, names)
+        dups.append(orc.dup_records().tolist())
+        assert orc.stats()["n_dup_oid"] == len(dups[-1])
+    return out, dups
+
+
+@pytest.mark.parametrize("case", sorted(KATS))
+def test_dup_oid_kat_literal_vs_oracle(case):
+    batches, want = KATS[case]
+    lit, lit_dups = _literal(batches)
+    orc, orc_dups = _oracle(batches)
+    assert lit == orc
+    assert lit_dups == orc_dups == want
+
+
+def _divergent_stream(n=160000, n_symbols=40, batch=40000, seed=19):
+    """The stream on which round 2's engine diverged from the oracle: the
+    cancel mix with per-batch oids 1 + k*1000 + U[0,1000) and uuids U{1,2}, so one oid is
+    admitted under both uuids in one symbol many times per batch."""
+    rec = wl.cancel_mix(n, n_symbols, seed=seed, zipf_s=1.0)
+    rng = np.random.default_rng(seed)
+    batches = wl.split_batches(rec, batch)
+    for k, b in enumerate(batches):
+        b["oid_id"] = (1 + k * 1000 + rng.integers(0, 1000, len(b))).astype(b["oid_id"].dtype)
+        b["uuid_id"] = rng.integers(1, 3, len(b)).astype(b["uuid_id"].dtype)
+    return batches
+
+
+def _records_to_requests(b):
+    out = []
+    for r in b:
+        out.append((int(r["action"]), dict(uuid="u%d" % r["uuid_id"], oid=str(int(r["oid_id"])),
+                                           symbol="s%d" % r["symbol_id"], transaction=int(r["side"]),
+                                           price=int(r["price_fx"]) / 1e8, volume=int(r["volume_fx"]) / 1e8)))
+    return out
+
+
+def test_divergent_stream_literal_vs_oracle_small():
+    """A 12k-record cut of the divergent stream (3 batches of 4000, oids colliding in every batch
+    and, with a narrower oid window, across batches): the literal transliteration (rule in its
+    consumer) and the C oracle publish the same MatchResults and reject the same records."""
+    batches = _divergent_stream(n=12000, n_symbols=8, batch=4000, seed=23)
+    for k, b in enumerate(batches):  # oids 1..300 in every batch: reuse across batches too
+        b["oid_id"] = (1 + np.random.default_rng(k).integers(0, 300, len(b))).astype(b["oid_id"].dtype)
+    reqs = [_records_to_requests(b) for b in batches]
+    lit, lit_dups = _literal(reqs)
+    orc, orc_dups = _oracle(reqs)
+    assert sum(len(d) for d in orc_dups) > 500
+    assert lit_dups == orc_dups
+    assert lit == orc
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("legacy", [False, True])
+def test_divergent_stream_gpu_vs_oracle(legacy):
+    """The exact round-2 divergent stream on the GPU, every event and the rejected indices vs the
+    C oracle: flow + cold books (default) and every hot book on the legacy kernel."""
+    from gome_amd.abi import GOME_FLAG_LEGACY_HOT, Engine
+    from tests.test_gpu_v4 import _cmp, _cmp_books
+    batches = _divergent_stream()
+    eng = Engine(max_symbols=40, max_batch=40000, max_nodes=1 << 20, max_levels=1 << 20,
+                 flags=GOME_FLAG_LEGACY_HOT if legacy else 0)
+    orc = Oracle(40)
+    total = prev_dropped = 0
+    for i, b in enumerate(batches):
+        eng.submit(b)
+        _cmp(eng.drain(), orc.submit(b), f"batch {i}")
+        d = orc.dup_records()
+        assert np.array_equal(eng.dup_records(), d), f"batch {i}: rejected records"
+        assert eng.stats()["n_dup_oid"] == len(d)
+        dropped = orc.stats()["n_dropped"]  # (the oracle's counters are cumulative)
+        assert eng.stats()["n_dropped"] == dropped - prev_dropped
+        prev_dropped = dropped
+        total += len(d)
+    assert total > 10000
+    _cmp_books(eng, orc, range(40), "divergent stream")
+    assert eng.stats()["n_resting"] == orc.resting()
+    if not legacy:
+        assert eng.stats()["n_flow_books"] > 0
+
+
+def _assign_books(b):
+    """Book 0 hot (flow), book 1 ~100 orders (cold), books 2 / 3 quirky with ~5000 / ~500 orders
+    (declined: the legacy kernel / the cold kernel)."""
+    i = np.arange(len(b))
+    b["symbol_id"] = np.select([i % 400 == 0, i % 8 == 1, i % 80 == 3], [1, 2, 3], 0)
+    return b
+
+
+@pytest.mark.gpu
+def test_resting_oid_readded_on_flow_cold_and_legacy_books():
+    """Oids resting at batch start re-added under another uuid, in a hot (flow) book, a cold book
+    and two quirky books (legacy and cold kernels), mixed with fresh ADDs: rejected on every path."""
+    from gome_amd.abi import Engine
+    from tests.test_gpu_v4 import _cmp, _cmp_books
+    rng = np.random.default_rng(5)
+    g = wl.Stream(4, seed=11)
+    eng = Engine(max_symbols=4, max_batch=60000, max_nodes=1 << 20, max_levels=1 << 16)
+    orc = Oracle(4)
+    first = _assign_books(g.batch(40000))
+    q2 = np.zeros(4, wl.ORDER_DTYPE)  # a wrong-side cancel (Q2) marks books 2 and 3 quirky
+    q2[:] = (50 * 10**6, 10**6, 2, 10**9, 1, 0, wl.ADD, 0)
+    q2[1]["action"], q2[1]["side"] = wl.DEL, 1
+    q2[2:] = q2[:2]
+    q2["symbol_id"][2:] = 3
+    first = np.concatenate([first, q2])
+    eng.submit(first)
+    _cmp(eng.drain(), orc.submit(first), "first")
+    rest = [(s, int(x["oid_id"])) for s in range(4) for p in orc.levels(s)["price_fx"]
+            for x in orc.fifo(s, int(p))]
+    assert len({s for s, _ in rest}) == 4
+    nxt = _assign_books(g.batch(40000))
+    pick = rng.choice(len(nxt), 3000, replace=False)
+    for j, k in zip(pick, rng.choice(len(rest), 3000)):
+        s, o = rest[k]
+        nxt[j]["symbol_id"], nxt[j]["oid_id"], nxt[j]["uuid_id"] = s, o, 77 + (j % 3)
+    for i in range(3):
+        eng.submit(nxt)
+        _cmp(eng.drain(), orc.submit(nxt), f"re-added {i}")
+        assert np.array_equal(eng.dup_records(), orc.dup_records()), f"batch {i}"
+        if i == 0:
+            assert len(orc.dup_records()) > 1000
+        fl = eng.debug_flow_books()
+        assert (fl["kind"] > 0).any() and (fl["kind"] == 0).any(), fl  # flow and legacy books
+        nxt = _assign_books(g.batch(40000))
+    _cmp_books(eng, orc, range(4), "re-added oids")

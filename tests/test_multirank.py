@@ -15,7 +15,7 @@ import torch.multiprocessing as mp
 
 import bench
 from gome_amd import workload as wl
-from gome_amd.publisher import SUMMARY_FIELDS, SummaryPublisher
+from gome_amd.publisher import SUMMARY_FIELDS, SUMMARY_WORDS, SummaryPublisher
 from oracle.pyoracle import Oracle
 
 
@@ -83,8 +83,8 @@ def _worker(rank, world, port, out_dir):
                                                1.5 + rank, [1.0 + rank, 5.0 - rank], "cpu")
         st = {"n_orders": 1000 + rank, "n_fills": 10 * rank, "n_events": 20 * rank,
               "n_resting": 5 + rank, "max_segment": 77 + rank}
-        summary = torch.zeros(32, dtype=torch.int64)
-        gathered = torch.zeros(32 * world, dtype=torch.int64)
+        summary = torch.zeros(SUMMARY_WORDS, dtype=torch.int64)
+        gathered = torch.zeros(SUMMARY_WORDS * world, dtype=torch.int64)
         pub = SummaryPublisher(world)
         for step in range(3):  # the rank-0 publisher consumes every step's gathered summaries
             bench.gather_summary(st, summary, gathered, rank, step)
@@ -108,7 +108,7 @@ def test_gloo_world2_reductions():
         assert o == 300.0 and f == 30.0 and e == 14.0   # sums over ranks
         assert el == 2.5                                 # max elapsed
         assert list(r[4:6]) == [2.0, 5.0]                # per-step max latency
-        g = r[6:6 + 32 * world].reshape(world, 32)
+        g = r[6:6 + SUMMARY_WORDS * world].reshape(world, SUMMARY_WORDS)
         for rk in range(world):
             row = [g[rk, idx[k]] for k in ("n_orders", "n_fills", "n_events", "n_resting", "max_segment", "rank", "step")]
             assert row == [1000 + rk, 10 * rk, 20 * rk, 5 + rk, 77 + rk, rk, 2]

@@ -89,6 +89,32 @@ def plan_algorithmic_bytes(st: dict) -> int:
     return 8 * st["n_flow_head_orders"] + 16 * st["n_flow_head_touches"]
 
 
+# The pipeline's phases that can be the batch's longest (gome_stats.ms_phase, gome_abi.h GOME_PH_*):
+# the kernel each is named after and its algorithmic bytes per launch (SURVEY §8d per-unit
+# figures over the phase's units; tail = the flow books outside the head).
+def phase_candidates(st: dict) -> dict:
+    from gome_amd.abi import PHASES
+    ms = dict(zip(PHASES, st["ms_phase"]))
+    n = st["n_orders"]
+    to = st["n_flow_orders"] - st["n_flow_head_orders"]      # tail orders / touches / fills
+    tt = st["n_flow_touches"] - st["n_flow_head_touches"]
+    tf = st["n_flow_tail_fills"]
+    tr = st["n_rests"] * to // max(n, 1)
+    return {
+        "k_flow_plan_tail": (ms["tail_plan"], 8 * to + 16 * tt, "serial plans of the tail's flow books"),
+        "k_flow_count": (ms["tail_count"], 20 * tt + 4 * to, "tail: events per touch (binary searches)"),
+        "k_flow_events_arena": (ms["tail_events"], 64 * tf + 16 * tt, "tail: fill events into the arena"),
+        "k_flow_level": (ms["tail_level"], 64 * tt + 24 * tf, "tail: per-level reconstruction"),
+        "k_flow_write": (ms["tail_write"], 32 * tt + 40 * tr, "tail: FIFO appends and level arrays"),
+        "k_flow_sort": (ms["tail_sort"], 32 * tt, "tail: touches sorted by level"),
+        "k_flow_prep": (ms["tail_prep"], 40 * to, "tail: books' prep"),
+        "k_radix_scatter": (ms["sort"], 68 * n, "radix sort by symbol + segments"),
+        "k_adm": (ms["admission"], 48 * n, "admission (Q4) and duplicate oids (Q7)"),
+        "k_prep": (ms["records"], 68 * n, "symbol-sorted records"),
+        "k_ev_scatter": (ms["publish"], 128 * st["n_events"] + 8 * n, "publish-order scan and event scatter"),
+    }
+
+
 def shard_stream(n_symbols, zipf_s, rank, world, seed, price_decimals=2):
     """Generator of this rank's share of the global Zipf stream (conditional sampling
     over the ranks this GPU owns; equal in law to filtering the global stream)."""
@@ -223,6 +249,8 @@ def main():
                     help="process-group backend (nccl = RCCL over xGMI; gloo: CPU collectives, for tests)")
     ap.add_argument("--same-device", action="store_true",
                     help="every rank on device 0 (rehearsing the N-rank path on a one-GPU box)")
+    ap.add_argument("--pool-nodes", type=int, default=0, help="gome_config.max_nodes (0: sized from the run)")
+    ap.add_argument("--pool-levels", type=int, default=0, help="gome_config.max_levels (0: sized from the run)")
     ap.add_argument("--step-log", default="", help="write each timed step's engine counters (JSONL)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="PMC-measured HBM bytes per launch of the dominant kernel (optional)")
@@ -265,8 +293,8 @@ def main():
     keep = 0.3 if args.workload == "config3" else 0.5
     # (+ two batches: the headroom a submit checks, in flight included, before it is applied)
     eng = Engine(max_symbols=n_symbols, max_batch=per_rank,
-                 max_nodes=max(1 << 20, int(total_orders * keep)) + 2 * per_rank,
-                 max_levels=max(1 << 22, (256 if n_symbols <= 100000 else 128) * n_symbols) + 2 * per_rank,
+                 max_nodes=args.pool_nodes or max(1 << 20, int(total_orders * keep)) + 2 * per_rank,
+                 max_levels=args.pool_levels or max(1 << 22, (256 if n_symbols <= 100000 else 128) * n_symbols) + 2 * per_rank,
                  device=dev)
 
     summary = torch.zeros(SUMMARY_WORDS, dtype=torch.int64, device=cdev)
@@ -301,6 +329,7 @@ def main():
     if pub is not None:
         pub = SummaryPublisher(world)  # the timed steps only
     lat, sts = [], []
+    slog = open(args.step_log, "w") if args.step_log and rank == 0 else None
     t0 = time.perf_counter()
     for i in range(warm, warm + steps):
         ts = time.perf_counter()
@@ -308,15 +337,15 @@ def main():
         lat.append((time.perf_counter() - ts) * 1e3)
         if rank == 0:
             note(f"step {i - warm + 1}/{steps}: {lat[-1]:.1f} ms")
+        if slog is not None:  # (written as it goes: a run that fails later keeps its steps)
+            slog.write(json.dumps(dict(step=i - warm, wall_ms=round(lat[-1], 3), **sts[-1])) + "\n")
+            slog.flush()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    if args.step_log and rank == 0:
-        with open(args.step_log, "w") as f:
-            for i, (s_, l_) in enumerate(zip(sts, lat)):
-                f.write(json.dumps(dict(step=i, wall_ms=round(l_, 3), **{k: (round(v, 4) if isinstance(v, float) else v)
-                                                                         for k, v in s_.items()})) + "\n")
+    if slog is not None:
+        slog.close()
 
     orders = sum(s["n_orders"] for s in sts)
     fills = sum(s["n_fills"] for s in sts)
@@ -340,6 +369,11 @@ def main():
     }
     if sum(s["n_flow_books"] for s in sts) == 0:
         cands.pop("k_flow_plan_head")
+    # the other phases of the pipeline (the tail's chain, the sort, admission, publishing): with
+    # no hot symbol (config 2) one of them is the longest
+    per = [phase_candidates(s) for s in sts]
+    for k in per[0]:
+        cands[k] = (sum(p[k][0] for p in per) / steps, sum(p[k][1] for p in per) / steps, per[0][k][2])
     kname = max(cands, key=lambda k: cands[k][0])
     ms_dom, bdom, kdesc = cands[kname]
     max_seg = max(s["max_segment"] for s in sts)
@@ -458,7 +492,7 @@ def main():
             "cancels_per_batch": int(cancels / steps),
             "device_ms_per_batch": round(ms_total, 3),
             "match_books_ms": round(ms_match, 3),
-            "kernel_ms": {k: round(v[0], 3) for k, v in cands.items()},
+            "kernel_ms": {k: round(v[0], 3) for k, v in sorted(cands.items(), key=lambda kv: -kv[1][0])},
             "hot_book": {"orders_per_batch": int(max_seg), "top_symbol_share": round(top_share, 5),
                          "ns_per_order": round(cands.get("k_flow_plan_head", cands["k_match_hot"])[0] * 1e6
                                                / max(max_seg, 1), 1),

@@ -28,6 +28,10 @@ TOB_DTYPE = np.dtype([("symbol_id", "<u4"), ("n_levels", "<u4"), ("bid_price_fx"
                       ("flags", "<u4"), ("pad", "<u4")])
 assert TOB_DTYPE.itemsize == 56
 
+# gome_stats.ms_phase indices (GOME_PH_*, gome_abi.h)
+PHASES = ["admission", "sort", "head_prep", "head_recon", "records", "tail_prep", "tail_plan", "tail_sort",
+          "tail_level", "tail_count", "tail_write", "tail_events", "near", "publish"]
+
 GOME_OK, GOME_E_INVAL, GOME_E_CAPACITY, GOME_E_DEVICE, GOME_E_STATE, GOME_E_NOTFOUND = range(6)
 STATUS_NAMES = {0: "OK", 1: "E_INVAL", 2: "E_CAPACITY", 3: "E_DEVICE", 4: "E_STATE", 5: "E_NOTFOUND"}
 
@@ -55,10 +59,13 @@ class Stats(C.Structure):
         ("ms_flow_plan", C.c_double), ("n_flow_head_orders", C.c_uint64),
         ("n_flow_head_touches", C.c_uint64), ("n_index_rebuilds", C.c_uint64),
         ("idx_tombstones", C.c_uint64), ("n_flow_cancels", C.c_uint64), ("ms_cold", C.c_double),
-        ("lvl_used", C.c_uint64), ("n_dup_oid", C.c_uint64)]
+        ("lvl_used", C.c_uint64), ("n_dup_oid", C.c_uint64), ("n_flow_tail_fills", C.c_uint64),
+        ("ms_phase", C.c_double * 16)]
 
     def as_dict(self):
-        return {n: getattr(self, n) for n, _ in self._fields_}
+        d = {n: getattr(self, n) for n, _ in self._fields_}
+        d["ms_phase"] = list(self.ms_phase)
+        return d
 
 
 _lib = None
@@ -274,9 +281,10 @@ class Engine:
         return self.lib.gome_inflight(self.h)
 
     def drain(self) -> np.ndarray:
+        got = C.c_size_t()
+        self._check(self.lib.gome_drain_events(self.h, None, 0, C.byref(got)))  # collects in-flight batches
         n = self.lib.gome_pending_events(self.h)
         out = np.zeros(n, EVENT_DTYPE)
-        got = C.c_size_t()
         self._check(self.lib.gome_drain_events(self.h, out.ctypes.data, n, C.byref(got)))
         return out[:got.value]
 

@@ -82,7 +82,8 @@ enum {
   C_FLOW_HEAD_ORDERS, C_FLOW_HEAD_TOUCHES,                // ... of which the head (k_flow_plan_head)
   C_FLOW_CANCELS,                                         // cancels applied on the flow path
   C_DUP,                                                  // ADDs rejected as duplicate oids (Q7)
-  C_NCTR = 22
+  C_FLOW_TAIL_FILLS,                                      // fills of the tail's flow books
+  C_NCTR = 23
 };
 
 // Level blocks (a book's sorted level array) come in power-of-two capacities 16 << c.  A

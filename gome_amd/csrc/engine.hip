@@ -23,6 +23,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <set>
@@ -183,6 +184,8 @@ struct Slot {
   size_t h_cap = 0;
   hipEvent_t ev0{}, ev1{}, evm0{}, evm1{}, evh0{}, evh1{}, evf0{}, evf1{}, evc0{}, evc1{};
   hipEvent_t h2d{}, done{};
+  hipEvent_t ph[GOME_NPHASE][2]{};  // GOME_PH_* phase brackets (ph_on: recorded this batch)
+  bool ph_on[GOME_NPHASE]{};
 };
 
 struct Flight {
@@ -211,6 +214,7 @@ struct gome_engine {
   Status* d_st = nullptr;
   // capacities
   uint32_t max_batch = 0, key_bits = 1, passes = 1, dbits = 1;
+  uint32_t tail_grid = 1024;  // blocks of the tail's per-touch kernels (GOME_TAIL_GRID)
   uint32_t hist_cap = 0, bsum_cap = 0;
   unsigned long long idx_cap = 0;
   // batch buffers
@@ -222,7 +226,11 @@ struct gome_engine {
   uint32_t* d_seg_order = nullptr;
   uint32_t* d_bcnt = nullptr;  // 32 counts + 32 offsets
   unsigned long long* d_adm = nullptr;  // admission table (k_adm)
-  unsigned long long* d_dup = nullptr;  // (S, oid) table of the admitted ADDs (duplicate-oid rule)
+  unsigned long long* d_dup = nullptr;  // (S, uuid, oid) table of the records whose (S, oid) repeats
+  uint8_t* d_multi = nullptr;           // per (S, oid) slot: the key repeats in the batch
+  uint32_t* d_first = nullptr;          // per (S, oid) slot: its first admitted ADD (NIL between batches)
+  uint32_t *d_adm_slot2 = nullptr, *d_adm_aux = nullptr;  // per record: (S, uuid, oid) / (S, oid) slot
+  uint32_t* d_oid_max = nullptr;        // per symbol: the highest oid an admitted ADD carried
   uint32_t* d_adm_slot = nullptr;
   uint32_t adm_mask = 0;
   uint32_t* d_ev_count = nullptr;
@@ -281,6 +289,9 @@ struct gome_engine {
       if (S.h_events) (void)hipHostFree(S.h_events);
       for (hipEvent_t ev : {S.ev0, S.ev1, S.evm0, S.evm1, S.evh0, S.evh1, S.evf0, S.evf1, S.evc0, S.evc1, S.h2d, S.done})
         if (ev) (void)hipEventDestroy(ev);
+      for (auto& pr : S.ph)
+        for (hipEvent_t ev : pr)
+          if (ev) (void)hipEventDestroy(ev);
     }
     for (hipEvent_t ev : {fork, join, joinf, prep_h, prep_t, fork_adm, adm_done, seg_done, ev_scan, ev_hot, dp_fork, cnt_fork, cnt_done})
       if (ev) (void)hipEventDestroy(ev);
@@ -342,6 +353,8 @@ gome_status gome_engine::init(const gome_config& c) {
   for (Slot& S : slots) {
     for (hipEvent_t* ev : {&S.ev0, &S.ev1, &S.evm0, &S.evm1, &S.evh0, &S.evh1, &S.evf0, &S.evf1, &S.evc0, &S.evc1})
       HIPCHK(hipEventCreate(ev));
+    for (auto& pr : S.ph)
+      for (hipEvent_t& ev : pr) HIPCHK(hipEventCreate(&ev));
     HIPCHK(hipEventCreateWithFlags(&S.h2d, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&S.done, hipEventDisableTiming));
     HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&S.h_st), sizeof(Status), hipHostMallocDefault));
@@ -363,6 +376,7 @@ gome_status gome_engine::init(const gome_config& c) {
   }
 
   max_batch = cfg.max_batch;
+  if (const char* g = std::getenv("GOME_TAIL_GRID")) tail_grid = std::max(64, std::atoi(g));  // (tuning)
   uint32_t ms = cfg.max_symbols;
   key_bits = (ms <= 1) ? 1 : 32 - __builtin_clz(ms - 1);
   passes = (key_bits + RS_MAXBITS - 1) / RS_MAXBITS;
@@ -408,7 +422,7 @@ gome_status gome_engine::init(const gome_config& c) {
 
   // ---- per-batch buffers
   const uint32_t nb = max_batch;
-  adm_mask = static_cast<uint32_t>(next_pow2(2ull * nb + 16) - 1);
+  adm_mask = static_cast<uint32_t>(std::min<uint64_t>(next_pow2(2ull * nb + 16), 1ull << 29) - 1);  // (ADM_SLOT)
   // events of one batch <= one partial per ADD + one per DEL + one per popped maker (<= the
   // resting capacity + the batch's rests) + block padding: sized once, so a pipelined
   // submit never waits to regrow it (HBM is plentiful; the regrowth path stays as a fallback)
@@ -421,7 +435,11 @@ gome_status gome_engine::init(const gome_config& c) {
       !alloc(&d_bsum, bsum_cap, "scan") || !alloc(&d_tmp, nb, "segflags") ||
       !alloc(&d_seg_start, nb + 1, "seg_start") || !alloc(&d_seg_order, nb, "seg_order") ||
       !alloc(&d_bcnt, 64, "buckets") || !alloc(&d_adm, adm_mask + 1ull, "adm_table") ||
-      !alloc(&d_dup, adm_mask + 1ull, "duplicate-oid table") ||
+      !alloc(&d_dup, adm_mask + 1ull, "admission key table") ||
+      !alloc(&d_multi, adm_mask + 1ull, "admission repeat flags") ||
+      !alloc(&d_first, adm_mask + 1ull, "first admitted ADDs") ||
+      !alloc(&d_adm_slot2, nb, "admission key slots") || !alloc(&d_adm_aux, nb, "admission shared slots") ||
+      !alloc(&d_oid_max, cfg.max_symbols, "oid watermarks") ||
       !alloc(&d_adm_slot, nb, "adm_slot") ||
       !alloc(&d_ev_count, nb, "ev_count") || !alloc(&d_ev_off, nb, "ev_off") ||
       !alloc(&d_prep, nb, "prep") || !alloc(&d_pend, nb, "pending inserts") ||
@@ -480,6 +498,11 @@ gome_status gome_engine::init(const gome_config& c) {
   HIPCHK(hipMemsetAsync(F.dh_key, 0, sizeof(unsigned long long) * ds * DEEP_HASH, stream));
   HIPCHK(hipMemsetAsync(F.dh_val, 0xFF, sizeof(uint32_t) * ds * DEEP_HASH, stream));
   HIPCHK(hipMemsetAsync(F.hdr, 0, sizeof(FlowHdr) * MAX_FLOW, stream));
+  // the admission tables that k_adm_clean keeps empty between batches
+  HIPCHK(hipMemsetAsync(d_dup, 0, (adm_mask + 1ull) * 8, stream));
+  HIPCHK(hipMemsetAsync(d_multi, 0, adm_mask + 1ull, stream));
+  HIPCHK(hipMemsetAsync(d_first, 0xFF, (adm_mask + 1ull) * 4, stream));
+  HIPCHK(hipMemsetAsync(d_oid_max, 0, 4ull * cfg.max_symbols, stream));
   HIPCHK(hipMemsetAsync(d_pend, 0, sizeof(PendEnt) * nb, stream));
   if (D.idx_mask >= PEND) return fail(GOME_E_INVAL, "gome_config.max_nodes too large (index > 2^31 slots)");
   HIPCHK(hipStreamSynchronize(stream));
@@ -532,6 +555,12 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
     ++n_rebuilds;
   }
   HIPCHK(hipEventRecord(S.ev0, s));
+  for (bool& on : S.ph_on) on = false;
+  // GOME_PH_* brackets (gome_stats.ms_phase): one event pair per phase on its stream
+  auto mark = [&](int ph, int end, hipStream_t st) -> hipError_t {
+    S.ph_on[ph] = true;
+    return hipEventRecord(S.ph[ph][end], st);
+  };
   // per-batch status reset (free_top / freed_top and the level pools persist)
   HIPCHK(hipMemsetAsync(d_st, 0, offsetof(Status, free_top), s));
   const uint32_t T256 = 256, gN = ceil_div(n, T256);
@@ -542,14 +571,19 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   HIPCHK(hipMemsetAsync(d_adm, 0, (adm_mask + 1ull) * 8, flow_stream));
   if ((++fc_gen & FC_GEN_MASK) == 0) HIPCHK(hipMemsetAsync(F.fc_hash, 0, sizeof(FcHash) * fc_hcap, flow_stream));
   F.fc_gen = fc_gen;
-  HIPCHK(hipMemsetAsync(d_dup, 0, (adm_mask + 1ull) * 8, flow_stream));
+  HIPCHK(mark(GOME_PH_ADMISSION, 0, flow_stream));
   k_adm<<<gN, T256, 0, flow_stream>>>(d_ord, n, d_adm, d_adm_slot, adm_mask, cfg.max_symbols, d_st, D.books, D.idx,
-                                      D.idx_mask);
-  k_adm_flag<<<gN, T256, 0, flow_stream>>>(d_ord, n, d_adm_slot, d_adm, d_dup, adm_mask);
-  k_dup_flag<<<gN, T256, 0, flow_stream>>>(n, d_adm_slot, d_dup, d_st, S.d_dup);
+                                      D.idx_mask, d_oid_max, d_multi);
+  k_adm_flag<<<gN, T256, 0, flow_stream>>>(d_ord, n, d_adm_slot, d_multi, d_dup, d_adm_slot2, d_adm_aux, adm_mask, d_st,
+                                           S.d_dup);
+  k_adm_res<<<gN, T256, 0, flow_stream>>>(d_ord, n, d_adm_slot, d_dup, d_adm_slot2, d_first);
+  k_adm_dup<<<gN, T256, 0, flow_stream>>>(n, d_adm_slot, d_first, d_st, S.d_dup);
+  k_adm_clean<<<gN, T256, 0, flow_stream>>>(n, d_adm_aux, d_adm_slot2, d_dup, d_first, d_multi);
+  HIPCHK(mark(GOME_PH_ADMISSION, 1, flow_stream));
   HIPCHK(hipEventRecord(adm_done, flow_stream));
 
   // ---- stable radix sort of (symbol_id, seq)
+  HIPCHK(mark(GOME_PH_SORT, 0, s));
   const uint32_t nblk = ceil_div(n, RS_TILE);
   uint32_t *kin = nullptr, *vin = nullptr, *kout = d_k0, *vout = d_v0;
   for (uint32_t p = 0; p < passes; ++p) {
@@ -580,6 +614,7 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   k_seg_count<<<gN, T256, 0, s>>>(d_seg_start, d_st, d_bcnt, &d_st->ctr[C_MAXSEG]);
   k_seg_bscan<<<1, 64, 0, s>>>(d_bcnt, d_bcnt + 32, d_st, FLOW_MIN_LOG2, MAX_FLOW);
   k_seg_scatter<<<gN, T256, 0, s>>>(d_seg_start, d_st, d_bcnt + 32, d_seg_order);
+  HIPCHK(mark(GOME_PH_SORT, 1, s));
 
   BatchArgs B;
   B.prep = d_prep;
@@ -623,6 +658,7 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   HIPCHK(hipEventRecord(seg_done, s));
   HIPCHK(hipStreamWaitEvent(flow_stream, seg_done, 0));
   HIPCHK(hipMemsetAsync(F.pscr, 0, sizeof(FlPrepScr) * FL_HEAD, flow_stream));
+  HIPCHK(mark(GOME_PH_HEAD_PREP, 0, flow_stream));
   k_flow_prep_a<<<dim3(FL_PG, nh_head), FL_PREP_T, 0, flow_stream>>>(D, B, FH);
   k_flow_prep_b<<<nh_head, FL_PREP_T, 0, flow_stream>>>(D, B, FH);
   k_flow_prep_c<<<dim3(FL_PG, nh_head), FL_PREP_T, 0, flow_stream>>>(D, B, FH);
@@ -655,6 +691,7 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
     k_fc_route<<<ceil_div(nb, 256), 256, 0, st>>>(D, R);
   };
   cancel_prep(FH, nh_head, FL_PG, true, flow_stream);
+  HIPCHK(mark(GOME_PH_HEAD_PREP, 1, flow_stream));
   HIPCHK(hipEventRecord(prep_h, flow_stream));
   HIPCHK(hipEventRecord(S.evf0, flow_stream));
   k_flow_plan_head<<<1, 256, plan_lds, flow_stream>>>(D, FH0);
@@ -667,7 +704,9 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
 
   // ---- match_books: one wavefront per book; hot books (LDS) on a second stream,
   //      concurrently with the cold books (HBM)
+  HIPCHK(mark(GOME_PH_RECORDS, 0, s));
   k_prep<<<gN, T256, 0, s>>>(d_ord, n, sidx, d_adm_slot, d_prep);
+  HIPCHK(mark(GOME_PH_RECORDS, 1, s));
   HIPCHK(hipEventRecord(S.evm0, s));
   HIPCHK(hipMemsetAsync(F.ig_bump, 0, 4, s));
   HIPCHK(hipEventRecord(fork, s));
@@ -738,9 +777,11 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   // otherwise starve the caller's stream): the tail's chain first, then the other head
   // books', then the hottest book's reconstruction (needed only when its plan ends).
   if (nh_tail) {
+    HIPCHK(mark(GOME_PH_TAIL_PREP, 0, s));
     k_flow_prep<<<nh_tail, FL_PREP_T, 0, s>>>(D, B, FT);
     deep_prep(FT, 8, s);
     cancel_prep(FT, nh_tail, 1, false, s);
+    HIPCHK(mark(GOME_PH_TAIL_PREP, 1, s));
   }
   HIPCHK(hipEventRecord(prep_t, s));
   HIPCHK(hipEventRecord(S.evc0, s));
@@ -748,32 +789,46 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
       D, B, &F.hdr[0].ok, sizeof(FlowHdr) / sizeof(uint32_t));
   HIPCHK(hipEventRecord(S.evc1, s));
   if (nh_tail) {  // the tail's plans and reconstruction
+    HIPCHK(mark(GOME_PH_TAIL_PLAN, 0, s));
     k_flow_plan_tail<<<nh_tail, 64, 0, s>>>(D, FT);
     k_flow_plan_tail_c<<<nh_tail, 64, 0, s>>>(D, FT);
     // (its blocks walk the tail's deep slots: at most DEEP_GRID_T whole-CU blocks)
     k_flow_plan_tail_d<<<std::min<uint32_t>(nh_tail, DEEP_GRID_T), 256, FL_DEEP_LDS, s>>>(D, FT);
+    HIPCHK(mark(GOME_PH_TAIL_PLAN, 1, s));
+    HIPCHK(mark(GOME_PH_TAIL_SORT, 0, s));
     k_flow_sort<<<nh_tail, FL_SORT_T, 0, s>>>(D, FT);
+    HIPCHK(mark(GOME_PH_TAIL_SORT, 1, s));
+    HIPCHK(mark(GOME_PH_TAIL_LEVEL, 0, s));
     k_flow_level<<<nh_tail, FL_LEVEL_T, 0, s>>>(D, FT);
     deep_sort_level(FT, 32, s);
+    HIPCHK(mark(GOME_PH_TAIL_LEVEL, 1, s));
+    HIPCHK(mark(GOME_PH_TAIL_COUNT, 0, s));
     k_flow_toff<FL_OK_ADD><<<1, 1024, 0, s>>>(D, FT);
-    k_flow_count<<<1024, 256, 0, s>>>(D, B, FT);
+    k_flow_count<<<tail_grid, 256, 0, s>>>(D, B, FT);
+    HIPCHK(mark(GOME_PH_TAIL_COUNT, 1, s));
+    HIPCHK(mark(GOME_PH_TAIL_WRITE, 0, s));
     k_flow_write<<<nh_tail, FL_WRITE_T, 0, s>>>(D, B, FT);
     deep_write(FT, s);
+    HIPCHK(mark(GOME_PH_TAIL_WRITE, 1, s));
     // the tail's events into the arena now (k_ev_scatter places them after the scan)
-    k_flow_events_arena<<<1024, 256, 0, s>>>(D, B, FT);
+    HIPCHK(mark(GOME_PH_TAIL_EVENTS, 0, s));
+    k_flow_events_arena<<<tail_grid, 256, 0, s>>>(D, B, FT);
     k_fc_level_book<<<nh_tail, 1024, 0, s>>>(D, FT);
     k_flow_toff<FL_OK_CANCEL><<<1, 1024, 0, s>>>(D, FTc);
     k_fc_count<<<1024, 256, 0, s>>>(D, B, FTc);
     k_fc_write_book<<<nh_tail, FL_WRITE_T, 0, s>>>(D, B, FTc);
     k_fc_events<<<1024, 256, 0, s>>>(D, B, FTc);
+    HIPCHK(mark(GOME_PH_TAIL_EVENTS, 1, s));
   }
   HIPCHK(hipStreamWaitEvent(hot_stream, fork, 0));
   HIPCHK(hipStreamWaitEvent(hot_stream, prep_h, 0));
   if (nh_near) {
+    HIPCHK(mark(GOME_PH_NEAR, 0, hot_stream));
     k_flow_plan_near<<<nh_near, 256, plan_lds, hot_stream>>>(D, FH1);
     if (head_recon(FH1, nh_near, hot_stream, hot_stream) != GOME_OK) return GOME_E_DEVICE;
     head_recon_c(FH1, FH1c, nh_near, hot_stream);
     k_flow_events_arena<<<1024, 256, 0, hot_stream>>>(D, B, FH1);
+    HIPCHK(mark(GOME_PH_NEAR, 1, hot_stream));
   }
   // legacy hot path (books the flow path declined); it and the cold kernel read the preps'
   // routing decisions (FlowHdr::ok)
@@ -784,10 +839,14 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   HIPCHK(hipEventRecord(S.evh1, hot_stream));
   k_match_resume<<<nleg, 64, 0, hot_stream>>>(D, B, d_resume);
   k_pend_apply<<<dim3(8, 64), 256, 0, hot_stream>>>(D, d_pend, d_seg_start, d_seg_order, B);
+  // oid watermarks for the next batches' duplicate-oid probe (the hot stream has slack here)
+  k_oid_max<<<gN, T256, 0, hot_stream>>>(n, skeys, d_prep, d_oid_max);
   HIPCHK(hipEventRecord(join, hot_stream));
   // (the hot stream's own work ended long before the hottest book's plan does)
+  HIPCHK(mark(GOME_PH_HEAD_RECON, 0, flow_stream));
   if (head_recon(FH0, 1, flow_stream, hot_stream) != GOME_OK) return GOME_E_DEVICE;
   head_recon_c(FH0, FH0c, 1, flow_stream);
+  HIPCHK(mark(GOME_PH_HEAD_RECON, 1, flow_stream));
   HIPCHK(hipEventRecord(joinf, flow_stream));
   HIPCHK(hipStreamWaitEvent(s, join, 0));
   HIPCHK(hipStreamWaitEvent(s, joinf, 0));
@@ -796,6 +855,7 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   HIPCHK(hipEventRecord(S.evm1, s));
 
   // ---- event compaction into publish order
+  HIPCHK(mark(GOME_PH_PUBLISH, 0, s));
   scan(d_ev_count, n, d_ev_off, &d_st->n_events, s);
   // the hottest book's events and the arena scatter fill disjoint slots: run them side by side
   HIPCHK(hipEventRecord(ev_scan, s));
@@ -804,6 +864,7 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   HIPCHK(hipEventRecord(ev_hot, flow_stream));
   k_ev_scatter<<<2048, T256, 0, s>>>(d_arena, arena_cap, d_st, d_ev_off, S.d_events, seq_base);
   HIPCHK(hipStreamWaitEvent(s, ev_hot, 0));
+  HIPCHK(mark(GOME_PH_PUBLISH, 1, s));
   k_recycle_copy<<<256, 256, 0, s>>>(D);
   k_recycle_fin<<<1, 64, 0, s>>>(D);
   k_lvl_recycle<<<LVL_NCLS, 256, 0, s>>>(D);
@@ -870,6 +931,12 @@ gome_status gome_engine::finish(uint32_t sl, uint32_t n) {
   stats.n_flow_cancels = st.ctr[C_FLOW_CANCELS];
   stats.lvl_used = st.lvl_used;
   stats.n_dup_oid = st.ctr[C_DUP];
+  stats.n_flow_tail_fills = st.ctr[C_FLOW_TAIL_FILLS];
+  for (int k = 0; k < GOME_NPHASE; ++k) {
+    float ms = 0;
+    if (S.ph_on[k]) (void)hipEventElapsedTime(&ms, S.ph[k][0], S.ph[k][1]);
+    stats.ms_phase[k] = ms;
+  }
   if (const uint64_t nd = std::min<uint64_t>(st.ctr[C_DUP], n)) {
     dup_idx.resize(nd);
     HIPCHK(hipMemcpy(dup_idx.data(), S.d_dup, nd * sizeof(uint32_t), hipMemcpyDeviceToHost));
@@ -1300,6 +1367,7 @@ gome_status gome_engine::load_books(size_t nb, const uint32_t* bsym, const uint3
   const uint32_t ms = D.max_symbols;
   std::vector<Book> books(ms, Book{0, 0, 0, 0});
   std::vector<uint8_t> seen(ms, 0);
+  std::vector<uint32_t> oid_max(ms, 0);  // the duplicate-oid rule's probe filter (k_adm)
   std::vector<Level> lvl;
   std::vector<Node> nodes;
   std::vector<ChunkHdr> chdr;
@@ -1350,6 +1418,7 @@ gome_status gome_engine::load_books(size_t nb, const uint32_t* bsym, const uint3
         N.oid = x.oid_id;
         N.uuid = x.uuid_id;
         N.tx = x.side;
+        oid_max[sym] = std::max(oid_max[sym], x.oid_id);
         const unsigned long long key = (static_cast<unsigned long long>(sym + 1) << 32) | x.oid_id;
         unsigned long long h = mix64(key) & mask;
         while (occ.count(h)) h = (h + 1) & mask;
@@ -1387,6 +1456,7 @@ gome_status gome_engine::load_books(size_t nb, const uint32_t* bsym, const uint3
     HIPCHK(hipMemcpyAsync(D.chdr, chdr.data(), nch * sizeof(ChunkHdr), hipMemcpyHostToDevice, s));
   }
   HIPCHK(hipMemcpyAsync(D.books, books.data(), static_cast<size_t>(ms) * sizeof(Book), hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(d_oid_max, oid_max.data(), static_cast<size_t>(ms) * 4, hipMemcpyHostToDevice, s));
   HIPCHK(hipMemcpyAsync(D.lvl_bump, &nl, 4, hipMemcpyHostToDevice, s));
   HIPCHK(hipMemcpyAsync(D.ch_bump, &nch, 4, hipMemcpyHostToDevice, s));
   if (!islot.empty()) {

@@ -1642,6 +1642,7 @@ __global__ void k_flow_count(Dev D, BatchArgs B, FlowArgs F) {
   if (lane_id() == 0 && fills) {
     atomicAdd(&D.st->ctr[C_FILLS], fills);
     atomicAdd(&D.st->ctr[C_HOT_FILLS], fills);
+    if (F.h0 >= FL_HEAD) atomicAdd(&D.st->ctr[C_FLOW_TAIL_FILLS], fills);
     atomicAdd(&D.st->ctr[C_RESTING_DELTA], static_cast<unsigned long long>(-static_cast<long long>(pops)));
   }
 }

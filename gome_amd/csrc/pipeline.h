@@ -232,19 +232,37 @@ __global__ void k_seg_scatter(const uint32_t* seg_start, const Status* st, uint3
   if (v) seg_order[base[b] + local] = s;
 }
 
-// ============================================================== admission (Q4)
+// ============================================================== admission (Q4, Q7)
 // Markers S:comparison[S:uuid:oid] are set at gRPC time for every ADD of the batch
 // (main.go:44-45) and tested+cleared at consume time (engine.go:58-62,90).  Under the
 // batch ingress model an ADD is admitted iff no earlier ADD/DEL of the batch carries
-// the same (S, uuid, oid).  One open-addressing table of 64-bit words: a key's slot holds
-// its fingerprint (high half, never 0) and the smallest batch index of the key seen so far
-// (low half).  A record whose key is new claims an empty slot with one CAS; a repeat of the
-// key lowers the index with one 64-bit atomicMin (same high half, so the minimum is over
-// the indices).  Slots whose fingerprint matches are confirmed against the claimant's record.
-// Also validates the record (k_validate's check, folded in: one pass over the input), and for
-// an ADD probes the (S, oid) cancel index as the previous batch left it: ADM_RESTING marks an
-// ADD whose oid already rests in its book (the duplicate-oid rule, k_dup_flag).
-constexpr uint32_t ADM_RESTING = 0x80000000u;
+// the same (S, uuid, oid).  A record whose admission the host resolved (GOME_ORD_ADM_HOST: the
+// consumer keeps the reference's pre-pool markers itself) carries the verdict in
+// GOME_ORD_ADMITTED.
+//
+// Duplicate oids (SURVEY Appendix A, Q7).  The reference names a resting node S:node:<oid> with
+// no uuid (ordernode.go:110-112, nodelink.go:119-122) and assumes oids unique per symbol
+// (README.md:27); a second live node with the same name corrupts its FIFO.  The boundary rule,
+// the same on every path and in the oracle: an admitted ADD whose (S, oid) rests in the book at
+// batch start, or was carried by an earlier admitted ADD of the same batch, is not applied
+// (dropped like an ADD without a marker), counted (gome_stats.n_dup_oid) and its batch index
+// reported (gome_dup_records).
+//
+// Both rules key on (S, oid) first.  k_adm puts every ADD / DEL into one open-addressing table
+// of 64-bit words keyed (S, oid): a key's slot holds its fingerprint (high half, never 0) and
+// the smallest batch index of the key seen so far (low half): a new key claims an empty slot
+// with one CAS, a repeat lowers the index with one 64-bit atomicMin and marks the slot `multi`.
+// A record alone with its (S, oid) in the batch (every record of a stream with fresh oids)
+// needs nothing else: an ADD is admitted (batch rule) or takes the host's verdict, and is a
+// duplicate only if its oid rests at batch start.  Only keys seen more than once take the
+// second table, keyed (S, uuid, oid) for the batch rule, and the first admitted ADD per (S, oid)
+// (k_adm_multi, k_adm_res, k_adm_dup); k_adm_clean leaves those tables empty for the next batch.
+//
+// "Rests at batch start" is a read-only probe of the (S, oid) cancel index, and only for an ADD
+// whose oid is not above the highest oid any ADD of its book ever carried (oid_max, kept by
+// k_oid_max): fresh, increasing oids (interned in arrival order) never probe.
+constexpr uint32_t ADM_RESTING = 0x80000000u, ADM_MULTI = 0x40000000u, ADM_OK = 0x20000000u;
+constexpr uint32_t ADM_SLOT = 0x1FFFFFFFu;  // (table slots < 2^29)
 
 // Read-only probe of the (S, oid) cancel index: does a live node carry this key?
 __device__ __forceinline__ bool idx_live(const IdxEnt* idx, unsigned long long mask, unsigned long long key) {
@@ -257,9 +275,36 @@ __device__ __forceinline__ bool idx_live(const IdxEnt* idx, unsigned long long m
   return false;
 }
 
+// Insert `key` (its record index i) into a fingerprint / min-index table; returns the slot and
+// whether the key was there before.  same(c): the record of index c carries the same key.
+template <class Same>
+__device__ __forceinline__ uint32_t adm_insert(unsigned long long* tab, uint32_t mask, unsigned long long km, uint32_t i,
+                                               Same same, bool& repeat) {
+  const unsigned long long mine = ((km >> 32) | 0x80000000ull) << 32 | i;
+  uint32_t h = static_cast<uint32_t>(km) & mask;
+  repeat = false;
+  for (uint32_t probe = 0; probe <= mask; ++probe) {
+    const unsigned long long c = atomicCAS(&tab[h], 0ull, mine);
+    if (c == 0) break;
+    if ((c >> 32) == (mine >> 32) && same(static_cast<uint32_t>(c))) {
+      repeat = true;
+      if (c > mine) atomicMin(&tab[h], mine);
+      break;
+    }
+    h = (h + 1) & mask;
+  }
+  return h;
+}
+
+__device__ __forceinline__ unsigned long long key_so(const gome_order& g) {
+  return (static_cast<unsigned long long>(g.symbol_id) + 1) << 32 | g.oid_id;
+}
+
+// Pass 1 (every record): validation (k_validate's check, folded in), the (S, oid) table, the
+// resting probe.  slot[i] := its (S, oid) slot | ADM_RESTING, or NIL (not an ADD / DEL).
 __global__ void k_adm(const gome_order* ord, uint32_t n, unsigned long long* tab, uint32_t* slot, uint32_t mask,
                       uint32_t max_symbols, Status* st, const Book* books, const IdxEnt* idx,
-                      unsigned long long idx_mask) {
+                      unsigned long long idx_mask, const uint32_t* oid_max, uint8_t* multi) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const gome_order g = ord[i];
@@ -273,25 +318,89 @@ __global__ void k_adm(const gome_order* ord, uint32_t n, unsigned long long* tab
     }
   }
   if (g.action != GOME_ADD && g.action != GOME_DEL) { slot[i] = NIL; return; }
-  const bool resting = g.action == GOME_ADD && books[g.symbol_id].n_lvl != 0 &&
-                       idx_live(idx, idx_mask, (static_cast<unsigned long long>(g.symbol_id) + 1) << 32 | g.oid_id);
+  const bool resting = g.action == GOME_ADD && g.oid_id <= oid_max[g.symbol_id] && books[g.symbol_id].n_lvl != 0 &&
+                       idx_live(idx, idx_mask, key_so(g));
+  bool repeat;
+  const uint32_t h = adm_insert(tab, mask, mix64(key_so(g)), i, [&](uint32_t c) {
+    const gome_order q = ord[c];
+    return q.symbol_id == g.symbol_id && q.oid_id == g.oid_id;
+  }, repeat);
+  if (repeat) multi[h] = 1;
+  slot[i] = h | (resting ? ADM_RESTING : 0u);
+}
+
+// Pass 2: records alone with their (S, oid) get their final 0 / 1 verdict (a rejected resting
+// duplicate is counted and listed: list = this batch slot's buffer, the host sorts it);
+// the others enter the (S, uuid, oid) table (slot2) and keep slot | ADM_MULTI.  aux[i] = the
+// (S, oid) slot of a shared key's record, else NIL (for k_adm_clean).
+__global__ void k_adm_flag(const gome_order* ord, uint32_t n, uint32_t* slot, const uint8_t* multi,
+                           unsigned long long* tab2, uint32_t* slot2, uint32_t* aux, uint32_t mask, Status* st,
+                           uint32_t* list) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t s = slot[i];
+  const bool shared = s != NIL && multi[s & ADM_SLOT];
+  aux[i] = shared ? (s & ADM_SLOT) : NIL;
+  if (s == NIL) { slot[i] = 0; return; }
+  const gome_order g = ord[i];
+  if (!shared) {
+    if (g.action != GOME_ADD) { slot[i] = 0; return; }
+    const bool adm = (g.flags & GOME_ORD_ADM_HOST) ? (g.flags & GOME_ORD_ADMITTED) != 0 : true;
+    const bool dup = adm && (s & ADM_RESTING);
+    slot[i] = adm && !dup ? 1u : 0u;
+    if (dup) list[atomicAdd(&st->ctr[C_DUP], 1ull)] = i;
+    return;
+  }
   const unsigned long long km = mix64((static_cast<unsigned long long>(g.symbol_id) << 40) ^
                                       (static_cast<unsigned long long>(g.uuid_id) << 20) ^ mix64(g.oid_id));
-  const unsigned long long mine = ((km >> 32) | 0x80000000ull) << 32 | i;
-  uint32_t h = static_cast<uint32_t>(km) & mask;
-  for (uint32_t probe = 0; probe <= mask; ++probe) {
-    const unsigned long long c = atomicCAS(&tab[h], 0ull, mine);
-    if (c == 0) break;
-    if ((c >> 32) == (mine >> 32)) {
-      const gome_order q = ord[static_cast<uint32_t>(c)];
-      if (q.symbol_id == g.symbol_id && q.uuid_id == g.uuid_id && q.oid_id == g.oid_id) {
-        if (c > mine) atomicMin(&tab[h], mine);
-        break;
-      }
-    }
-    h = (h + 1) & mask;
-  }
-  slot[i] = h | (resting ? ADM_RESTING : 0u);
+  bool repeat;
+  slot2[i] = adm_insert(tab2, mask, km, i, [&](uint32_t c) {
+    const gome_order q = ord[c];
+    return q.symbol_id == g.symbol_id && q.uuid_id == g.uuid_id && q.oid_id == g.oid_id;
+  }, repeat);
+  slot[i] = s | ADM_MULTI;
+}
+
+// Pass 3 (shared keys): the batch rule / host verdict; an admitted ADD offers its index as the
+// key's first admitted ADD (first[] is NIL between batches).
+__global__ void k_adm_res(const gome_order* ord, uint32_t n, uint32_t* slot, const unsigned long long* tab2,
+                          const uint32_t* slot2, uint32_t* first) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t s = slot[i];
+  if (!(s & ADM_MULTI)) return;
+  const gome_order g = ord[i];
+  if (g.action != GOME_ADD) return;
+  const bool adm = (g.flags & GOME_ORD_ADM_HOST) ? (g.flags & GOME_ORD_ADMITTED) != 0
+                                                 : static_cast<uint32_t>(tab2[slot2[i]]) == i;
+  if (!adm) return;
+  atomicMin(&first[s & ADM_SLOT], i);
+  slot[i] = s | ADM_OK;
+}
+
+// Pass 4 (shared keys): final verdicts; an admitted ADD that is not its key's first admitted ADD,
+// or whose oid rests at batch start, is a duplicate.
+__global__ void k_adm_dup(uint32_t n, uint32_t* slot, const uint32_t* first, Status* st, uint32_t* list) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t s = slot[i];
+  if (!(s & ADM_MULTI)) return;
+  const bool adm = (s & ADM_OK) != 0;
+  const bool dup = adm && ((s & ADM_RESTING) || first[s & ADM_SLOT] != i);
+  slot[i] = adm && !dup ? 1u : 0u;
+  if (dup) list[atomicAdd(&st->ctr[C_DUP], 1ull)] = i;
+}
+
+// Pass 5 (shared keys): their entries of the second table, first[] and multi[] back to empty.
+__global__ void k_adm_clean(uint32_t n, const uint32_t* aux, const uint32_t* slot2, unsigned long long* tab2,
+                            uint32_t* first, uint8_t* multi) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t h = aux[i];
+  if (h == NIL) return;
+  tab2[slot2[i]] = 0ull;
+  first[h] = NIL;
+  multi[h] = 0;
 }
 
 // ============================================================== prepared records
@@ -306,62 +415,32 @@ struct Prep {
 };
 static_assert(sizeof(Prep) == 32, "Prep layout");
 
-// Admission verdict per input record, in place of its marker slot (1: an ADD that holds the
-// lowest index of its (S, uuid, oid) key, nodepool.go:14-28), so k_prep (on the critical path)
-// reads one flag instead of chasing slot -> minimum.  Runs beside the radix sort.
-// A record whose admission the host resolved (GOME_ORD_ADM_HOST: the consumer keeps the
-// reference's pre-pool markers itself) carries the verdict in GOME_ORD_ADMITTED.
-//
-// Duplicate oids (SURVEY Appendix A, Q7).  The reference names a resting node S:node:<oid> with
-// no uuid (ordernode.go:110-112, nodelink.go:119-122) and assumes oids unique per symbol
-// (README.md:27); a second live node with the same name corrupts its FIFO.  The boundary rule,
-// the same on every path and in the oracle: an admitted ADD whose (S, oid) rests in the book at
-// batch start (k_adm's index probe) or was carried by an earlier admitted ADD of the same batch
-// is not applied (dropped like an ADD without a marker), counted (gome_stats.n_dup_oid) and its
-// batch index reported (gome_dup_records).  So after k_adm_flag, an admitted ADD's slot holds
-// its (S, oid) slot of `dup` (whose low half ends as the smallest admitted index of the key),
-// plus ADM_RESTING; every other record NIL.  k_dup_flag leaves the final 0 / 1 verdict.
-__global__ void k_adm_flag(const gome_order* ord, uint32_t n, uint32_t* slot, const unsigned long long* tab,
-                           unsigned long long* dup, uint32_t mask) {
+// oid_max[S] = the highest oid any applied ADD of book S carried (the resting probe's filter).
+// Over the symbol-sorted records (Prep: oid and the final admission verdict), one atomicMax per
+// symbol run of a wave.
+__global__ void k_oid_max(uint32_t n, const uint32_t* skeys, const Prep* prep, uint32_t* oid_max) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const gome_order g = ord[i];
-  const uint32_t s = slot[i];
-  bool adm;
-  if (s == NIL || g.action != GOME_ADD) adm = false;
-  else if (g.flags & GOME_ORD_ADM_HOST) adm = (g.flags & GOME_ORD_ADMITTED) != 0;
-  else adm = static_cast<uint32_t>(tab[s & ~ADM_RESTING]) == i;
-  if (!adm) { slot[i] = NIL; return; }
-  const unsigned long long key = (static_cast<unsigned long long>(g.symbol_id) + 1) << 32 | g.oid_id;
-  const unsigned long long km = mix64(key ^ 0x9E3779B97F4A7C15ull);
-  const unsigned long long mine = ((km >> 32) | 0x80000000ull) << 32 | i;
-  uint32_t h = static_cast<uint32_t>(km) & mask;
-  for (uint32_t probe = 0; probe <= mask; ++probe) {
-    const unsigned long long c = atomicCAS(&dup[h], 0ull, mine);
-    if (c == 0) break;
-    if ((c >> 32) == (mine >> 32)) {
-      const gome_order q = ord[static_cast<uint32_t>(c)];
-      if (q.symbol_id == g.symbol_id && q.oid_id == g.oid_id) {
-        if (c > mine) atomicMin(&dup[h], mine);
-        break;
-      }
-    }
-    h = (h + 1) & mask;
+  const uint32_t lane = lane_id();
+  const bool v = i < n;
+  const uint32_t sym = v ? skeys[i] : NIL;
+  uint32_t o = 0;
+  if (v) {
+    const Prep q = prep[i];
+    if (q.action == GOME_ADD && q.adm) o = q.oid;
   }
-  slot[i] = h | (s & ADM_RESTING);
+  // a run = lanes of one symbol; the run's last lane takes the run's max
+  const uint32_t prev = __shfl_up(sym, 1), next = __shfl_down(sym, 1);
+  const bool head = lane == 0 || prev != sym, tail = lane == 63 || next != sym;
+  const unsigned long long heads = __ballot(head);
+  const uint32_t start = 63u - __clzll(heads & ((2ull << lane) - 1));  // this lane's run start
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t y = __shfl_up(o, off);
+    if (lane >= static_cast<uint32_t>(off) && lane - off >= start) o = max(o, y);
+  }
+  if (v && tail && o > 0) atomicMax(&oid_max[sym], o);
 }
 
-// Final admission verdicts (0 / 1) after the duplicate-oid rule; rejected ADDs are counted and
-// listed (list: this batch slot's index buffer, in no particular order; the host sorts it).
-__global__ void k_dup_flag(uint32_t n, uint32_t* slot, const unsigned long long* dup, Status* st, uint32_t* list) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const uint32_t s = slot[i];
-  if (s == NIL) { slot[i] = 0; return; }
-  const bool rej = (s & ADM_RESTING) || static_cast<uint32_t>(dup[s & ~ADM_RESTING]) != i;
-  slot[i] = rej ? 0u : 1u;
-  if (rej) list[atomicAdd(&st->ctr[C_DUP], 1ull)] = i;
-}
 
 __global__ void k_prep(const gome_order* ord, uint32_t n, const uint32_t* sidx,
                        const uint32_t* adm_flag, Prep* prep) {

@@ -25,7 +25,7 @@ from .workload import EVENT_DTYPE, ORDER_DTYPE
 _SUM_KEYS = ("n_orders", "n_add", "n_del", "n_dropped", "n_fills", "n_cancels", "n_rests", "n_events",
              "n_resting", "n_levels", "n_segments", "n_hot", "n_hot_orders", "n_hot_fills", "n_hot_rests",
              "n_hot_cancels", "n_flow_books", "n_flow_orders", "n_flow_touches", "n_flow_head_orders",
-             "n_flow_head_touches", "n_flow_cancels", "n_dup_oid", "n_index_rebuilds", "idx_tombstones",
+             "n_flow_head_touches", "n_flow_cancels", "n_dup_oid", "n_flow_tail_fills", "n_index_rebuilds", "idx_tombstones",
              "lvl_used")
 _TOTAL_KEYS = ("n_resting", "n_levels", "n_index_rebuilds", "idx_tombstones", "lvl_used")
 _MAX_KEYS = ("max_segment", "ms_total", "ms_match", "ms_hot", "ms_flow_plan", "ms_cold")

@@ -158,6 +158,26 @@ typedef struct gome_config {
   uint32_t pad;
 } gome_config;
 
+/* gome_stats.ms_phase (ABI >= 5): device time of the pipeline's phases in the last batch, each
+ * timed on the stream it runs on (phases on different streams overlap). */
+enum {
+  GOME_PH_ADMISSION = 0, /* admission markers and the duplicate-oid rule (Q4, Q7)         */
+  GOME_PH_SORT,          /* radix sort by symbol, segments                                */
+  GOME_PH_HEAD_PREP,     /* the head books' preps (lane, deep, cancel)                     */
+  GOME_PH_HEAD_RECON,    /* the hottest book's reconstruction after its plan              */
+  GOME_PH_RECORDS,       /* k_prep: the symbol-sorted 32-B records                        */
+  GOME_PH_TAIL_PREP,     /* tail books: prep (k_flow_prep, deep and cancel preps)          */
+  GOME_PH_TAIL_PLAN,     /* tail books: serial plans (k_flow_plan_tail, _c, _d)           */
+  GOME_PH_TAIL_SORT,     /* tail books: touches sorted by level (k_flow_sort)             */
+  GOME_PH_TAIL_LEVEL,    /* tail books: level reconstruction (k_flow_level, deep levels)  */
+  GOME_PH_TAIL_COUNT,    /* tail books: events per touch (k_flow_toff, k_flow_count)      */
+  GOME_PH_TAIL_WRITE,    /* tail books: FIFO appends, level arrays (k_flow_write, deep)   */
+  GOME_PH_TAIL_EVENTS,   /* tail books: events into the arena, the cancel books' chain    */
+  GOME_PH_NEAR,          /* the other head books: plans and reconstruction               */
+  GOME_PH_PUBLISH,       /* publish-order scan, the hottest book's events, arena scatter  */
+  GOME_NPHASE = 16
+};
+
 /* Per-batch counters of the last submit (and running totals). */
 typedef struct gome_stats {
   uint64_t n_orders, n_add, n_del, n_dropped; /* dropped = ADD without admission marker */
@@ -189,6 +209,8 @@ typedef struct gome_stats {
   uint64_t n_dup_oid;                         /* ADDs of the batch rejected by the
                                                  duplicate-oid rule (ABI >= 5; also counted
                                                  in n_dropped)                           */
+  uint64_t n_flow_tail_fills;                 /* fills of the tail's flow books (ABI >= 5) */
+  double ms_phase[GOME_NPHASE];               /* GOME_PH_* device times (ABI >= 5)        */
 } gome_stats;
 
 typedef struct gome_engine gome_engine;

@@ -383,6 +383,17 @@ uint64_t oracle_resting(const oracle* o) {
   return t;
 }
 
+/* Observable levels over all books (sizing studies). */
+uint64_t oracle_levels_total(const oracle* o) {
+  uint64_t t = 0;
+  for (uint32_t s = 0; s < o->max_symbols; ++s)
+    for (uint32_t k = 0; k < o->books[s].n; ++k) {
+      const olevel* L = &o->books[s].lv[k];
+      t += (L->nnodes || L->depth || L->member) ? 1u : 0u;
+    }
+  return t;
+}
+
 /* Levels with any observable state (nodes, depth or membership), ascending. */
 uint64_t oracle_snapshot_levels(const oracle* o, uint32_t sym, gome_level* out, uint64_t cap) {
   if (sym >= o->max_symbols) return 0;

@@ -48,6 +48,8 @@ def lib():
         L.oracle_snapshot_levels.restype = C.c_uint64
         L.oracle_snapshot_fifo.argtypes = [VP, C.c_uint32, C.c_int64, VP, C.c_uint64]
         L.oracle_snapshot_fifo.restype = C.c_uint64
+        L.oracle_levels_total.argtypes = [VP]
+        L.oracle_levels_total.restype = C.c_uint64
         L.oracle_dup_records.argtypes = [VP, VP, C.c_uint64]
         L.oracle_dup_records.restype = C.c_uint64
         _lib = L
@@ -88,6 +90,9 @@ class Oracle:
         if n:
             self.L.oracle_dup_records(self.h, out.ctypes.data, n)
         return out
+
+    def levels_total(self) -> int:
+        return self.L.oracle_levels_total(self.h)
 
     def resting(self) -> int:
         return self.L.oracle_resting(self.h)

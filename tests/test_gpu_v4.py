@@ -225,13 +225,16 @@ def test_host_resolved_admission_flags():
     exp = orc.submit(ref)
     _cmp(eng.drain(), exp, "host admission")
     assert eng.stats()["n_dropped"] == len(b) // 2
-    # duplicate key, host-admitted twice in one batch: both rest
+    # duplicate key, host-admitted twice in one batch: the second names a node that the first
+    # already made (S:node:<oid>): the duplicate-oid rule drops it (gome_abi.h, Q7)
     d = np.zeros(2, wl.ORDER_DTYPE)
     d[:] = (10**6, 10**6, 0, 999999, 5, 0, 1, GOME_ORD_ADM_HOST | GOME_ORD_ADMITTED)
     d[1]["price_fx"] = 2 * 10**6 // 4  # another (non-crossing) price
     eng.submit(d)
     eng.drain()
-    assert eng.stats()["n_dropped"] == 0 and eng.stats()["n_rests"] == 2
+    st = eng.stats()
+    assert st["n_dropped"] == 1 and st["n_dup_oid"] == 1 and st["n_rests"] == 1
+    assert eng.dup_records().tolist() == [1]
 
 
 def test_q8_transaction_codes_on_gpu_vs_literal():

@@ -271,7 +271,9 @@ def test_load_books_rejects_bad_images():
     assert e.stats()["n_resting"] == 2 and len(e.levels(1)) == 2
     with pytest.raises(GomeError):
         e.load_books([(2, lv, nd)])                          # not a fresh engine any more
-    used = mk()
-    used.submit(np.zeros(0, __import__("gome_amd.workload", fromlist=["ORDER_DTYPE"]).ORDER_DTYPE))
+    used = mk()  # (an empty or refused submit does not count as use: tests/test_gpu_r3.py)
+    one = np.zeros(1, __import__("gome_amd.workload", fromlist=["ORDER_DTYPE"]).ORDER_DTYPE)
+    one[0] = (10, 5, 3, 9, 1, 0, 1, 0)
+    used.submit(one)
     with pytest.raises(GomeError):
         used.load_books([(1, lv, nd)])

@@ -6,6 +6,7 @@
 #   c5:    config-5 60 timed steps with the per-step log (pools sized for the run)
 #   c2grid: config-2 bench lines with GOME_TAIL_GRID = 1024 / 4096 (the tail's per-touch kernels)
 #   c3:    config-3 default bench line
+#   c5t:   config-5 60 steps under rocprofv3 --kernel-trace (what grows as the books deepen)
 set -o pipefail
 TAG=${1:-r3m}; shift
 PARTS=${@:-sweep c2 c3t c5}
@@ -39,6 +40,10 @@ for P in $PARTS; do
         --no-cpu-baseline > $OUT/c2_g$G.jsonl 2> $OUT/c2_g$G.log || exit 5
       tail -1 $OUT/c2_g$G.jsonl | cut -c100-300
     done ;;
+  c5t)
+    timeout -k 10 600 rocprofv3 --kernel-trace --stats -T --output-format csv -d $OUT/c5trace -o run \
+      -- python3 bench.py --workload config5 --steps 60 --warmup 2 --e2e-steps 0 --no-cpu-baseline \
+      --pool-nodes 80000000 --pool-levels 160000000 --step-log $OUT/c5t_steps.jsonl > $OUT/c5_trace.log 2>&1 || exit 7 ;;
   c3)
     timeout -k 10 300 python3 -u bench.py --steps 20 --warmup 5 --no-cpu-baseline > $OUT/c3.jsonl 2> $OUT/c3.log || exit 6
     tail -1 $OUT/c3.jsonl | cut -c100-300 ;;

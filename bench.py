@@ -10,6 +10,7 @@ Workloads (BASELINE.json configs; `--workload`):
           chosen earlier ADD no DEL targeted yet, delorder.go), 10% of ADDs aggressive (BUY @
           1.00 / SALE @ 0.01, volume k * 10.00, k ~ U{1..16}).
   config5: 1M symbols, Zipf(1.0), 4-dp price grid (deep books, up to 10k levels), 2-dp volumes.
+  config5c: config 5's grid with config 4's 50% DELs and 10% aggressive ADDs (cancels on deep books).
 All synthetic and seeded.  One step = one batch of `--batch` orders per GPU applied end to end
 on the device (validate + radix sort by symbol + admission + match_books + event compaction),
 records already resident in HBM: that is `value`.  `e2e` then runs the same workload from
@@ -55,6 +56,9 @@ WORKLOADS = {
     "config5": dict(symbols=1000000, zipf=1.0, decimals=4, del_frac=0.0, aggr=0.0,
                     desc="config5: {symbols} symbols, Zipf(s={zipf}), 4-dp price grid (deep books), "
                          "2-dp volumes, ADD-only"),
+    "config5c": dict(symbols=1000000, zipf=1.0, decimals=4, del_frac=0.5, aggr=0.1,
+                     desc="config5c: config 5's {symbols} symbols and 4-dp grid (deep books) with config 4's "
+                          "cancel-heavy mix: 50% DEL of earlier ADDs, 10% aggressive ADDs"),
 }
 
 

@@ -460,7 +460,7 @@ gome_status gome_engine::init(const gome_config& c) {
   if (!alloc(&F.hdr, MAX_FLOW, "flow headers") || !alloc(&F.lvl, MAX_FLOW * FL_CAP, "flow levels") ||
       !alloc(&F.ord8, static_cast<uint64_t>(FL_ORD8_MUL) * nb + FL_ORD8_PAD, "flow records") || !alloc(&F.log, ntouch, "flow touch log") ||
       !alloc(&F.srt, ntouch, "flow level runs") || !alloc(&F.rs, ntouch, "flow new makers") ||
-      !alloc(&F.fbase, ntouch, "flow fill bases") || !alloc(&F.mk, ntouch, "flow touch makers") || !alloc(&F.ig, F.ig_cap, "flow gathered makers") ||
+      !alloc(&F.fbase, ntouch, "flow fill bases") || !alloc(&F.ig, F.ig_cap, "flow gathered makers") ||
       !alloc(&F.ig_bump, 1, "flow gather bump") || !alloc(&F.toff, 2 * FC_TOFF, "flow touch offsets") ||
       !alloc(&F.lvout, static_cast<size_t>(MAX_FLOW) * FL_CAP, "flow final levels"))
     return GOME_E_CAPACITY;
@@ -729,7 +729,7 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   auto deep_write = [&](const FlowArgs& R, hipStream_t st) {
     const uint32_t ns = std::min<uint32_t>(R.ds1 - R.ds0, DEEP_GRID_T);  // (blocks walk the slots)
     k_deep_claim<<<ns, DEEP_CLAIM_T, 0, st>>>(D, B, R);
-    k_deep_write_lv<<<dim3(DEEP_GRID, ns), 64, 0, st>>>(D, B, R);
+    k_deep_write_lv<<<dim3(DEEP_CAP / 64, ns), 64, 0, st>>>(D, B, R);
     k_deep_write_fin<<<ns, DEEP_FIN_T, 0, st>>>(D, R);
   };
   // the hottest book's reconstruction: wide kernels (tile-parallel sort, one wave per level).

@@ -188,7 +188,6 @@ struct FlowArgs {
   SEnt* srt;           // same index space
   RsEnt* rs;           // same index space
   uint32_t* fbase;     // same index space: fill_idx of a touch's first event
-  uint2* mk;           // srt's index space: a consume touch's first / last maker (fl_level_marks)
   IgEnt* ig;
   uint32_t ig_cap;
   uint32_t* ig_bump;
@@ -1383,26 +1382,9 @@ __device__ __forceinline__ uint32_t fl_find(const IgEnt* IG, uint32_t ig_n, cons
   return ig_n + lo;
 }
 
-// The makers each consume touch of a level overlaps, as indices into the level's makers in
-// consumption order (the gathered old makers IG, then the new ones RS): first / last, found once
-// here, where the level's makers were just written (L2-hot), instead of by every later reader
-// (k_flow_count and k_flow_events read them through fl_touch_ctx).  Threads tid of nthr.
-__device__ __forceinline__ void fl_level_marks(const FlowArgs& F, uint32_t L, uint32_t base, uint32_t cnt,
-                                               const IgEnt* IG, uint32_t ig_n, const RsEnt* RS, uint32_t nrest,
-                                               int64_t d0, uint32_t tid, uint32_t nthr) {
-  const SEnt* R = F.srt + L + base;
-  uint2* MK = F.mk + L + base;
-  for (uint32_t i = tid; i < cnt; i += nthr) {
-    const SEnt e = R[i];
-    if (e.kind != TK_CONS) continue;
-    MK[i] = make_uint2(fl_find(IG, ig_n, RS, nrest, d0, e.coord), fl_find(IG, ig_n, RS, nrest, d0, e.coord + e.amt - 1));
-  }
-}
-
 __device__ __forceinline__ void fl_level_one(const Dev& D, const FlowArgs& F, uint32_t h, uint32_t q,
                                              uint32_t run_base = NIL, uint32_t run_cnt = 0,
-                                             uint32_t ig_pre = NIL, int64_t pre_cfin = -1, uint32_t pre_nr = 0,
-                                             bool marks = true) {
+                                             uint32_t ig_pre = NIL, int64_t pre_cfin = -1, uint32_t pre_nr = 0) {
   const FlowHdr* hd = &F.hdr[h];
   const uint32_t lane = lane_id();
   FlowLvl* Lq = fl_lvls(F, h) + q;
@@ -1538,10 +1520,6 @@ __device__ __forceinline__ void fl_level_one(const Dev& D, const FlowArgs& F, ui
     Lq->tslot = tslot;
     Lq->nlive0 = nv0 - consumed;
   }
-  if (marks) {  // (this wave wrote IG / RS: its stores complete before its lanes read them back)
-    __threadfence_block();
-    fl_level_marks(F, L, base, cnt, F.ig + ig_base, ng, RS, nr, d0, lane, 64);
-  }
 }
 
 constexpr uint32_t FL_LEVEL_T = 1024;
@@ -1570,9 +1548,10 @@ __device__ __forceinline__ FlTouchCtx fl_touch_ctx(const FlowArgs& F, uint32_t h
   t.RS = F.rs + L + base;
   t.c = F.srt[L + x.pos].coord;
   t.a = x.amt;
-  const uint2 m = F.mk[L + x.pos];  // (fl_level_marks)
-  t.first = m.x;
-  t.last = m.y;
+  const int64_t d0 = t.Lq->d0;
+  const uint32_t ig_n = t.Lq->ig_n, nrest = t.Lq->nrest;
+  t.first = fl_find(t.IG, ig_n, t.RS, nrest, d0, t.c);
+  t.last = fl_find(t.IG, ig_n, t.RS, nrest, d0, t.c + t.a - 1);
   return t;
 }
 
@@ -2308,14 +2287,7 @@ __global__ __launch_bounds__(FL_LVB_T) void k_flow_level_wide(Dev D, FlowArgs F)
   int64_t cfin;
   uint32_t nr;
   fl_level_scan_blk(F, h, q, cfin, nr);
-  if (threadIdx.x < 64) fl_level_one(D, F, h, q, NIL, 0, NIL, cfin, nr, false);
-  __threadfence();
-  __syncthreads();
-  // the level's consume touches' makers, with the whole block (the hottest book's levels)
-  const FlowLvl* Lq = fl_lvls(F, h) + q;
-  const uint32_t L = FL_TOUCH_MUL * F.hdr[h].beg, base = Lq->base;
-  fl_level_marks(F, L, base, Lq->cnt, F.ig + Lq->ig_base, Lq->ig_n, F.rs + L + base, Lq->nrest, Lq->d0, threadIdx.x,
-                 FL_LVB_T);
+  if (threadIdx.x < 64) fl_level_one(D, F, h, q, NIL, 0, NIL, cfin, nr);
 }
 
 }  // namespace gome

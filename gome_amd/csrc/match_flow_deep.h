@@ -12,10 +12,12 @@
 //                       its level in Touch::pos
 //   k_deep_sort_*       stable LSD sort of the touches by level, two 7-bit passes through
 //                       F.tlog (each pass the head sort's tile count / scan / scatter)
-//   k_deep_level        per level: its run (binary search of the sorted touches), then
-//                       fl_level_one; count and events are the ADD-only kernels (fl_touch_ctx
-//                       reads a deep touch's level from its sorted entry)
-//   k_deep_write_*      FIFO appends per level, the book's level array compacted by a scan.
+//   k_deep_runs/level   the run of each touched level in the sorted touches, then fl_level_one
+//                       on the touched levels only (the prep leaves an untouched level final);
+//                       count and events are the ADD-only kernels (fl_touch_ctx reads a deep
+//                       touch's level from its sorted entry)
+//   k_deep_write_*      FIFO appends per touched level (untouched ones copied lane-parallel),
+//                       the book's level array compacted by a scan.
 // Declines (the book goes to the legacy kernel, bit-exact as before): DELs in the segment,
 // zero-volume ADDs (Q6), quirk books, more than DEEP_CAP - 2 levels, volumes beyond the 32-bit
 // plan.
@@ -263,6 +265,7 @@ __device__ __forceinline__ void k_deep_prep_b_one(Dev D, BatchArgs B, FlowArgs F
     f.price = static_cast<int64_t>(key - FL_KEY_OFF);
     f.old = old;
     f.head = f.tail = NIL;
+    f.ig_all = 1;  // (what k_deep_level leaves on a level the batch does not touch: it skips them)
     if (old != NIL) {
       const Level x = L0[old];
       f.d0 = x.depth;
@@ -272,6 +275,7 @@ __device__ __forceinline__ void k_deep_prep_b_one(Dev D, BatchArgs B, FlowArgs F
       f.hslot = x.hslot;
       f.tslot = x.tslot;
       f.mem0 = x.member;
+      f.nlive0 = x.nlive;
     }
     LV[r + 1] = f;
     vals[sl] = r + 1;
@@ -516,32 +520,27 @@ __global__ __launch_bounds__(256) void k_deep_runs(Dev D, FlowArgs F) {
   for (uint32_t i = blockIdx.y; i < fd_nslots(F); i += gridDim.y) k_deep_runs_one(D, F, i);
 }
 
+// Only the levels the batch touched: a deep book holds thousands of levels (config 5's grow to
+// ~10k) and most see no touch in a batch; the prep left those in the state fl_level_one would give
+// them (nothing consumed or rested, every old node live, ig_all).  A wave takes the levels whose
+// run starts in its 64 sorted touches.
 __device__ __forceinline__ void k_deep_level_one(Dev D, FlowArgs F, uint32_t slot_i) {
   const uint32_t h = fd_book(D, F, slot_i);
   if (!fd_deep(F, h)) return;
-  const uint32_t nl = F.hdr[h].nl, nt = F.hdr[h].ntouch, L = FL_TOUCH_MUL * F.hdr[h].beg;
+  const uint32_t nt = F.hdr[h].ntouch, L = FL_TOUCH_MUL * F.hdr[h].beg;
   FlowLvl* LV = fl_lvls(F, h);
-  // the gathered-maker space of all this wave's levels in one claim (an upper bound: every
-  // level with resting makers, consumed or not; the books' resting nodes bound the total)
+  const SEnt* R = F.srt + L;
   const uint32_t lane = lane_id();
-  uint32_t need = 0;
-  for (uint32_t q0 = 1 + blockIdx.x; q0 <= nl; q0 += 64 * gridDim.x) {
-    const uint32_t q = q0 + lane * gridDim.x;
-    need += q <= nl ? LV[q].nv0 : 0u;
-  }
-  need = rl(wave_incl_scan_u32(need), 63);
-  uint32_t ig = 0;
-  if (lane == 0 && need) ig = atomicAdd(F.ig_bump, need);
-  ig = uni(ig);
-  for (uint32_t q = 1 + blockIdx.x; q <= nl; q += gridDim.x) {
-    const uint32_t e = uni(LV[q].pad1), b = e ? uni(LV[q].base) : 0u;  // (k_deep_runs)
-    if (lane_id() == 0) {
-      LV[q].base = b;
-      LV[q].cnt = e - b;
+  for (uint32_t i0 = blockIdx.x * 64u; i0 < nt; i0 += gridDim.x * 64u) {
+    const uint32_t i = i0 + lane;
+    const uint32_t lv = i < nt ? R[i].lvl : 0u;
+    const bool head = i < nt && (i == 0 || R[i - 1].lvl != lv);
+    for (unsigned long long hm = __ballot(head); hm; hm &= hm - 1) {
+      const uint32_t q = uni(rl(lv, static_cast<uint32_t>(__builtin_ctzll(hm))));
+      const uint32_t e = uni(LV[q].pad1), b = uni(LV[q].base);  // (k_deep_runs)
+      if (lane == 0) LV[q].cnt = e - b;
+      fl_level_one(D, F, h, q, b, e - b);
     }
-    const uint32_t nv0 = uni(LV[q].nv0);
-    fl_level_one(D, F, h, q, b, e - b, ig);
-    ig += nv0;
   }
 }
 __global__ __launch_bounds__(64) void k_deep_level(Dev D, FlowArgs F) {
@@ -609,9 +608,39 @@ __device__ __forceinline__ void k_deep_write_lv_one(Dev D, BatchArgs B, FlowArgs
   const FlPrepScr* P = F.dscr + hd.dslot;
   const FlClaim cl{P->c_t, P->c_nst, P->c_bb, P->c_ok};
   const FlClaim* claim = &cl;
-  for (uint32_t q = 1 + blockIdx.x; q <= hd.nl; q += gridDim.x) {
-    const Level x = fl_write_level(D, B, F, hd, h, q, claim);
-    if (lane_id() == 0) F.dlvout[static_cast<size_t>(hd.dslot) * DEEP_CAP + q] = x;
+  const FlowLvl* LV = fl_lvls(F, h);
+  Level* out = F.dlvout + static_cast<size_t>(hd.dslot) * DEEP_CAP;
+  const uint32_t lane = lane_id();
+  // A wave takes 64 consecutive levels: the untouched ones (no touch, so no append and nothing
+  // consumed: the prep's FlowLvl is final) one per lane, then the touched ones one at a time.
+  for (uint32_t q0 = 1 + blockIdx.x * 64u; q0 <= hd.nl; q0 += gridDim.x * 64u) {
+    const uint32_t q = q0 + lane;
+    const bool v = q <= hd.nl;
+    const bool touched = v && LV[q].cnt != 0;
+    if (v && !touched) {
+      const FlowLvl& f = LV[q];
+      Level x{};
+      x.price = f.price;
+      x.depth = f.dfin;
+      x.nlive = f.nlive0;
+      x.member = static_cast<uint8_t>(f.memf);
+      x.head = x.tail = NIL;
+      if (x.nlive > 0) {
+        x.head = f.head;
+        x.hslot = static_cast<uint8_t>(f.hslot);
+        x.tail = f.tail;
+        x.tslot = static_cast<uint8_t>(f.tslot);
+      }
+      const bool ok = (x.nlive > 0) == (x.depth > 0) && (x.nlive > 0) == (f.memf == M_BUY || f.memf == M_SALE) &&
+                      (x.nlive > 0 || f.memf == 0);
+      if (!ok) atomicOr(&D.st->err, ERR_CORRUPT);
+      out[q] = x;
+    }
+    for (unsigned long long tm = __ballot(touched); tm; tm &= tm - 1) {
+      const uint32_t qq = q0 + static_cast<uint32_t>(__builtin_ctzll(tm));
+      const Level x = fl_write_level(D, B, F, hd, h, qq, claim);
+      if (lane == 0) out[qq] = x;
+    }
   }
 }
 __global__ __launch_bounds__(64) void k_deep_write_lv(Dev D, BatchArgs B, FlowArgs F) {

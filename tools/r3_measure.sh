@@ -7,6 +7,7 @@
 #   c2grid: config-2 bench lines with GOME_TAIL_GRID = 1024 / 4096 (the tail's per-touch kernels)
 #   c3:    config-3 default bench line
 #   c5t:   config-5 60 steps under rocprofv3 --kernel-trace (what grows as the books deepen)
+#   ab:    config-2 / config-3 bench lines of each gome_amd/libgome_*.so variant beside libgome.so
 set -o pipefail
 TAG=${1:-r3m}; shift
 PARTS=${@:-sweep c2 c3t c5}
@@ -31,7 +32,7 @@ for P in $PARTS; do
         -- python3 bench.py --steps 5 --warmup 2 --batch $B --e2e-steps 0 --no-cpu-baseline > $OUT/c3_trace_$B.log 2>&1 || exit 4
     done ;;
   c5)
-    timeout -k 10 500 python3 -u bench.py --workload config5 --steps 60 --warmup 2 --e2e-steps 10 --no-cpu-baseline \
+    timeout -k 10 500 python3 -u bench.py --workload config5 --steps 60 --warmup 2 --e2e-steps 4 --no-cpu-baseline \
       --pool-nodes 80000000 --pool-levels 160000000 --step-log $OUT/c5_steps.jsonl > $OUT/c5.jsonl 2> $OUT/c5.log || exit 2
     tail -1 $OUT/c5.jsonl | cut -c100-260 ;;
   c2grid)
@@ -44,6 +45,17 @@ for P in $PARTS; do
     timeout -k 10 600 rocprofv3 --kernel-trace --stats -T --output-format csv -d $OUT/c5trace -o run \
       -- python3 bench.py --workload config5 --steps 60 --warmup 2 --e2e-steps 0 --no-cpu-baseline \
       --pool-nodes 80000000 --pool-levels 160000000 --step-log $OUT/c5t_steps.jsonl > $OUT/c5_trace.log 2>&1 || exit 7 ;;
+  ab)  # A/B of the variant builds in gome_amd/libgome_*.so against libgome.so, alternating
+    for R in 1 2; do
+      for V in "" $(cd gome_amd && ls libgome_*.so 2>/dev/null); do
+        N=${V:-libgome.so}
+        for W in config2 config3; do
+          GOME_LIB=${V:+$PWD/gome_amd/$V} timeout -k 10 300 python3 -u bench.py --workload $W --steps 10 --warmup 3 \
+            --e2e-steps 0 --no-cpu-baseline > $OUT/ab_${W}_${N%.so}_$R.jsonl 2> $OUT/ab_${W}_${N%.so}_$R.log || exit 8
+          echo "$W $N $R $(tail -1 $OUT/ab_${W}_${N%.so}_$R.jsonl | cut -c1-200)"
+        done
+      done
+    done ;;
   c3)
     timeout -k 10 300 python3 -u bench.py --steps 20 --warmup 5 --no-cpu-baseline > $OUT/c3.jsonl 2> $OUT/c3.log || exit 6
     tail -1 $OUT/c3.jsonl | cut -c100-300 ;;

@@ -106,8 +106,8 @@ def phase_candidates(st: dict) -> dict:
     tr = st["n_rests"] * to // max(n, 1)
     return {
         "k_flow_plan_tail": (ms["tail_plan"], 8 * to + 16 * tt, "serial plans of the tail's flow books"),
-        "k_flow_count": (ms["tail_count"], 20 * tt + 4 * to, "tail: events per touch (binary searches)"),
-        "k_flow_events_arena": (ms["tail_events"], 64 * tf + 16 * tt, "tail: fill events into the arena"),
+        "k_flow_events_fused": (ms["tail_count"] + ms["tail_events"], 64 * tf + 36 * tt + 4 * to,
+                                "tail: events per touch (binary searches) into the arena, ev_count"),
         "k_flow_level": (ms["tail_level"], 64 * tt + 24 * tf, "tail: per-level reconstruction"),
         "k_flow_write": (ms["tail_write"], 32 * tt + 40 * tr, "tail: FIFO appends and level arrays"),
         "k_flow_sort": (ms["tail_sort"], 32 * tt, "tail: touches sorted by level"),

@@ -737,7 +737,9 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   // other books than the flow sort / level / write kernels, and k_flow_count reads the plan's
   // log and the level records, which the writes neither read from it nor change, so with
   // cs != st they run beside the writes; k_flow_count still comes after both level passes.
-  auto head_recon = [&](const FlowArgs& R, uint32_t nb, hipStream_t st, hipStream_t cs) -> gome_status {
+  // fused: the books' events go to the arena, and k_flow_events_fused counts them there (no
+  // k_flow_count).
+  auto head_recon = [&](const FlowArgs& R, uint32_t nb, hipStream_t st, hipStream_t cs, bool fused) -> gome_status {
     const bool split = cs != st;
     if (split) {  // the deep books' level sort (other books than the ones below) beside it
       HIPCHK(hipEventRecord(dp_fork, st));
@@ -754,7 +756,7 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
       HIPCHK(hipEventRecord(cnt_fork, st));
       HIPCHK(hipStreamWaitEvent(cs, cnt_fork, 0));
     }
-    k_flow_count<<<1024, 256, 0, cs>>>(D, B, R);
+    if (!fused) k_flow_count<<<1024, 256, 0, cs>>>(D, B, R);
     if (split) {  // (the publish scan waits for the count, the batch's end for the deep writes)
       HIPCHK(hipEventRecord(cnt_done, cs));
       deep_write(R, cs);  // (after the count, which reads neither the claims nor the writes)
@@ -810,7 +812,6 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
     HIPCHK(mark(GOME_PH_TAIL_LEVEL, 1, s));
     HIPCHK(mark(GOME_PH_TAIL_COUNT, 0, s));
     k_flow_toff<FL_OK_ADD><<<1, 1024, 0, s>>>(D, FT);
-    k_flow_count<<<tail_grid, 256, 0, s>>>(D, B, FT);
     HIPCHK(mark(GOME_PH_TAIL_COUNT, 1, s));
     HIPCHK(mark(GOME_PH_TAIL_WRITE, 0, s));
     k_flow_write<<<nh_tail, FL_WRITE_T, 0, s>>>(D, B, FT);
@@ -818,7 +819,7 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
     HIPCHK(mark(GOME_PH_TAIL_WRITE, 1, s));
     // the tail's events into the arena now (k_ev_scatter places them after the scan)
     HIPCHK(mark(GOME_PH_TAIL_EVENTS, 0, s));
-    k_flow_events_arena<<<tail_grid, 256, 0, s>>>(D, B, FT);
+    k_flow_events_fused<<<tail_grid, FL_EV_T, 0, s>>>(D, B, FT);
     k_fc_level_book<<<nh_tail, 1024, 0, s>>>(D, FT);
     k_flow_toff<FL_OK_CANCEL><<<1, 1024, 0, s>>>(D, FTc);
     k_fc_count<<<1024, 256, 0, s>>>(D, B, FTc);
@@ -831,9 +832,9 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   if (nh_near) {
     HIPCHK(mark(GOME_PH_NEAR, 0, hot_stream));
     k_flow_plan_near<<<nh_near, 256, plan_lds, hot_stream>>>(D, FH1);
-    if (head_recon(FH1, nh_near, hot_stream, hot_stream) != GOME_OK) return GOME_E_DEVICE;
+    if (head_recon(FH1, nh_near, hot_stream, hot_stream, true) != GOME_OK) return GOME_E_DEVICE;
     head_recon_c(FH1, FH1c, nh_near, hot_stream);
-    k_flow_events_arena<<<1024, 256, 0, hot_stream>>>(D, B, FH1);
+    k_flow_events_fused<<<1024, FL_EV_T, 0, hot_stream>>>(D, B, FH1);
     HIPCHK(mark(GOME_PH_NEAR, 1, hot_stream));
   }
   // legacy hot path (books the flow path declined); it and the cold kernel read the preps'
@@ -850,7 +851,7 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   HIPCHK(hipEventRecord(join, hot_stream));
   // (the hot stream's own work ended long before the hottest book's plan does)
   HIPCHK(mark(GOME_PH_HEAD_RECON, 0, flow_stream));
-  if (head_recon(FH0, 1, flow_stream, hot_stream) != GOME_OK) return GOME_E_DEVICE;
+  if (head_recon(FH0, 1, flow_stream, hot_stream, false) != GOME_OK) return GOME_E_DEVICE;
   head_recon_c(FH0, FH0c, 1, flow_stream);
   HIPCHK(mark(GOME_PH_HEAD_RECON, 1, flow_stream));
   HIPCHK(hipEventRecord(joinf, flow_stream));

@@ -1775,6 +1775,169 @@ __global__ __launch_bounds__(256) void k_flow_events_arena(Dev D, BatchArgs B, F
   fl_events<true>(D, B, F, nullptr, nullptr);
 }
 
+// Segmented inclusive wave scan: lane i sums lanes s..i, s = the last lane <= i with `head` set
+// (lane 0 always starts a segment).
+template <typename T>
+__device__ __forceinline__ T wave_seg_incl(T v, unsigned long long heads) {
+  const uint32_t lane = lane_id();
+  const unsigned long long le = heads | 1ull;
+  const uint32_t s = 63u - static_cast<uint32_t>(__builtin_clzll(le & (lane == 63 ? ~0ull : ((2ull << lane) - 1ull))));
+#pragma unroll
+  for (uint32_t off = 1; off < 64; off <<= 1) {
+    const T u = __shfl_up(v, off);
+    if (lane >= off && lane - off >= s) v += u;
+  }
+  return v;
+}
+
+// ============================================================== k_flow_events_fused
+// The books whose events go to the arena (the tail, the near head books): k_flow_count and
+// k_flow_events_arena in one pass over the touches.  An order's touches are consecutive in its
+// book's log, so its fill_idx bases and the volume its better levels took are segmented scans
+// over the touches (a wave's first lane walks back into an order begun before the wave); the
+// order's last touch writes ev_count[taker].
+__global__ __launch_bounds__(FL_EV_T) void k_flow_events_fused(Dev D, BatchArgs B, FlowArgs F) {
+  const uint32_t hend = fl_hend(D, F), nb = hend > F.h0 ? hend - F.h0 : 0u;
+  const uint32_t total = nb ? F.toff[F.tb + nb] : 0u;
+  const uint32_t lane = lane_id(), w = threadIdx.x >> 6, stride = gridDim.x * blockDim.x;
+  __shared__ uint32_t wtot[FL_EV_T / 64], bbase;
+  unsigned long long fills = 0, pops = 0;
+  for (uint32_t b0 = blockIdx.x * blockDim.x; b0 < total; b0 += stride) {
+    const uint32_t gt = b0 + threadIdx.x, g0w = b0 + (threadIdx.x & ~63u);
+    const bool valid = gt < total;
+    uint32_t h = 0, L = 0, t = 0, nt = 0, beg = 0, j = 0, cnt = 0;
+    Touch x{};
+    FlTouchCtx c{};
+    bool first = true, last = true;
+    if (g0w < total) {
+      const uint32_t hb = fl_book_of_wave(F, nb, g0w, valid ? gt : g0w);
+      if (valid) {
+        h = F.h0 + hb;
+        t = gt - F.toff[F.tb + hb];
+        nt = F.hdr[h].ntouch;
+        beg = F.hdr[h].beg;
+        L = FL_TOUCH_MUL * beg;
+        x = F.log[L + t];
+        j = tk_j(x);
+        first = t == 0 || tk_j(F.log[L + t - 1]) != j;
+        last = t + 1 == nt || tk_j(F.log[L + t + 1]) != j;
+        if (((x.kr >> 7) & 1u) == TK_CONS) {
+          c = fl_touch_ctx(F, h, L, x);
+          cnt = c.last - c.first + 1;
+          fills += cnt;
+          const int64_t lend = c.last < c.Lq->ig_n ? c.IG[c.last].e + c.IG[c.last].v
+                                                   : c.RS[c.last - c.Lq->ig_n].e + c.RS[c.last - c.Lq->ig_n].v;
+          pops += cnt - (lend > c.c + c.a ? 1u : 0u);
+        }
+      }
+    }
+    // the order's events and volume before this touch: segmented scans, plus lane 0's carry
+    const unsigned long long heads = __ballot(first);
+    uint32_t carry_n = 0;
+    int64_t carry_a = 0;
+    if (lane == 0 && !first) {
+      for (uint32_t u = t; u > 0; --u) {
+        const Touch y = F.log[L + u - 1];
+        if (tk_j(y) != j) break;
+        carry_a += y.amt;
+        if (((y.kr >> 7) & 1u) == TK_CONS) {
+          const FlTouchCtx cy = fl_touch_ctx(F, h, L, y);
+          carry_n += cy.last - cy.first + 1;
+        }
+      }
+    }
+    const bool in_first_seg = !(heads & 1ull) && ((heads & (lane == 63 ? ~0ull : ((2ull << lane) - 1ull))) == 0ull);
+    carry_n = __shfl(carry_n, 0);
+    carry_a = __shfl(carry_a, 0);
+    const uint32_t n_incl = wave_seg_incl<uint32_t>(cnt, heads) + (in_first_seg ? carry_n : 0u);
+    const int64_t a_incl = wave_seg_incl<int64_t>(valid ? x.amt : 0, heads) + (in_first_seg ? carry_a : 0);
+    const uint32_t fb = n_incl - cnt;  // the touch's fill_idx base within its order
+    const int64_t a_before = a_incl - (valid ? x.amt : 0);
+    if (valid && last && j < F.hdr[h].end - beg) B.ev_count[B.prep[beg + j].idx] = n_incl;  // (not padding)
+    // arena slots: one bump allocation per block tile
+    uint32_t inc = cnt;
+    for (uint32_t off = 1; off < 64; off <<= 1) {
+      const uint32_t v = __shfl_up(inc, off);
+      if (lane >= off) inc += v;
+    }
+    if (lane == 63) wtot[w] = inc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      uint32_t s = 0;
+      for (uint32_t k = 0; k < FL_EV_T / 64; ++k) { const uint32_t v = wtot[k]; wtot[k] = s; s += v; }
+      bbase = s ? atomicAdd(&D.st->ev_bump, s) : 0u;
+      if (s && static_cast<unsigned long long>(bbase) + s > B.arena_cap) {
+        atomicOr(&D.st->err, ERR_EVENTS);
+        bbase = NIL;
+      }
+    }
+    __syncthreads();
+    const uint32_t base = bbase, wb = wtot[w];
+    __syncthreads();  // (wtot / bbase are rewritten by the next tile)
+    if (base == NIL || !cnt) continue;
+    gome_event* dst = B.arena + base + wb + (inc - cnt);
+    const uint32_t sym = F.hdr[h].sym;
+    const Prep tk = B.prep[beg + j];
+    const int64_t tb = tk.vol - a_before;  // taker remaining before this level
+    const uint32_t ig_n = c.Lq->ig_n, nrest = c.Lq->nrest, ig_all = c.Lq->ig_all;
+    const int64_t price = c.Lq->price;
+    for (uint32_t m = c.first; m <= c.last; ++m) {
+      int64_t e, v;
+      uint32_t oid, uuid, tx;
+      if (m < ig_n) {
+        const IgEnt g = c.IG[m];
+        e = g.e; v = g.v; oid = g.oid; uuid = g.uuid; tx = g.tx;
+      } else {
+        const RsEnt r = c.RS[m - ig_n];
+        const Prep mk = B.prep[beg + r.j];
+        e = r.e; v = r.v; oid = mk.oid; uuid = mk.uuid; tx = mk.side;
+      }
+      const int64_t lo = e > c.c ? e : c.c;
+      const int64_t hi = (e + v < c.c + c.a) ? e + v : c.c + c.a;
+      const int64_t qty = hi - lo, pre = e + v - lo;
+      const bool full = e + v <= c.c + c.a;
+      uint32_t nx = 0, lst = 1;  // MatchNode.NextNode at the time of this fill
+      if (m + 1 < ig_n) {
+        nx = c.IG[m + 1].oid;
+        lst = 0;
+      } else if (ig_all || m + 1 > ig_n) {
+        const uint32_t r = m + 1 - ig_n;
+        if (r < nrest && c.RS[r].t < t) {
+          nx = B.prep[beg + c.RS[r].j].oid;
+          lst = 0;
+        }
+      }
+      gome_event ev;
+      ev.price_fx = price;
+      ev.match_volume_fx = qty;
+      ev.maker_volume_fx = full ? pre : pre - qty;
+      ev.taker_volume_fx = tb - (hi - c.c);
+      ev.taker_seq = tk.idx;  // (the batch index: k_ev_scatter adds seq_base)
+      ev.fill_idx = fb + (m - c.first);
+      ev.symbol_id = sym;
+      ev.maker_oid_id = oid;
+      ev.maker_uuid_id = uuid;
+      ev.maker_next_oid_id = nx;
+      ev.kind = GOME_EV_FILL;
+      ev.maker_side = static_cast<uint8_t>(tx);
+      ev.maker_is_last = static_cast<uint8_t>(lst);
+      ev.pad0 = 0;
+      ev.seq_hi = 0;
+      dst[m - c.first] = ev;
+    }
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    fills += __shfl_xor(fills, off);
+    pops += __shfl_xor(pops, off);
+  }
+  if (lane_id() == 0 && fills) {
+    atomicAdd(&D.st->ctr[C_FILLS], fills);
+    atomicAdd(&D.st->ctr[C_HOT_FILLS], fills);
+    if (F.h0 >= FL_HEAD) atomicAdd(&D.st->ctr[C_FLOW_TAIL_FILLS], fills);
+    atomicAdd(&D.st->ctr[C_RESTING_DELTA], static_cast<unsigned long long>(-static_cast<long long>(pops)));
+  }
+}
+
 // ============================================================== k_flow_write
 // One workgroup per flow book: append the surviving new makers to their FIFOs (chunks from
 // the free stack / bump pool), insert them into the cancel index, rewrite the level array.

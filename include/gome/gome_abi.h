@@ -170,9 +170,9 @@ enum {
   GOME_PH_TAIL_PLAN,     /* tail books: serial plans (k_flow_plan_tail, _c, _d)           */
   GOME_PH_TAIL_SORT,     /* tail books: touches sorted by level (k_flow_sort)             */
   GOME_PH_TAIL_LEVEL,    /* tail books: level reconstruction (k_flow_level, deep levels)  */
-  GOME_PH_TAIL_COUNT,    /* tail books: events per touch (k_flow_toff, k_flow_count)      */
+  GOME_PH_TAIL_COUNT,    /* tail books: the touch offsets (k_flow_toff)                   */
   GOME_PH_TAIL_WRITE,    /* tail books: FIFO appends, level arrays (k_flow_write, deep)   */
-  GOME_PH_TAIL_EVENTS,   /* tail books: events into the arena, the cancel books' chain    */
+  GOME_PH_TAIL_EVENTS,   /* tail books: events + ev_count (k_flow_events_fused), DEL books */
   GOME_PH_NEAR,          /* the other head books: plans and reconstruction               */
   GOME_PH_PUBLISH,       /* publish-order scan, the hottest book's events, arena scatter  */
   GOME_NPHASE = 16

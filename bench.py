@@ -106,10 +106,10 @@ def phase_candidates(st: dict) -> dict:
     tr = st["n_rests"] * to // max(n, 1)
     return {
         "k_flow_plan_tail": (ms["tail_plan"], 8 * to + 16 * tt, "serial plans of the tail's flow books"),
-        "k_flow_events_fused": (ms["tail_count"] + ms["tail_events"], 64 * tf + 36 * tt + 4 * to,
-                                "tail: events per touch (binary searches) into the arena, ev_count"),
+        "k_flow_write_events": (ms["tail_write"], 64 * tf + 36 * tt + 4 * to + 32 * tt + 40 * tr,
+                                "tail: FIFO appends and level arrays beside the events (binary searches) "
+                                "into the arena"),
         "k_flow_level": (ms["tail_level"], 64 * tt + 24 * tf, "tail: per-level reconstruction"),
-        "k_flow_write": (ms["tail_write"], 32 * tt + 40 * tr, "tail: FIFO appends and level arrays"),
         "k_flow_sort": (ms["tail_sort"], 32 * tt, "tail: touches sorted by level"),
         "k_flow_prep": (ms["tail_prep"], 40 * to, "tail: books' prep"),
         "k_radix_scatter": (ms["sort"], 68 * n, "radix sort by symbol + segments"),
@@ -495,6 +495,7 @@ def main():
             "events_per_s": round(g_events / elapsed, 1),
             "cancels_per_batch": int(cancels / steps),
             "device_ms_per_batch": round(ms_total, 3),
+            "host_enqueue_ms": round(sum(s["ms_host_enqueue"] for s in sts) / steps, 3),
             "match_books_ms": round(ms_match, 3),
             "kernel_ms": {k: round(v[0], 3) for k, v in sorted(cands.items(), key=lambda kv: -kv[1][0])},
             "hot_book": {"orders_per_batch": int(max_seg), "top_symbol_share": round(top_share, 5),

@@ -60,7 +60,8 @@ class Stats(C.Structure):
         ("n_flow_head_touches", C.c_uint64), ("n_index_rebuilds", C.c_uint64),
         ("idx_tombstones", C.c_uint64), ("n_flow_cancels", C.c_uint64), ("ms_cold", C.c_double),
         ("lvl_used", C.c_uint64), ("n_dup_oid", C.c_uint64), ("n_flow_tail_fills", C.c_uint64),
-        ("ms_phase", C.c_double * 16)]
+        ("ms_phase", C.c_double * 16),
+        ("ms_host_enqueue", C.c_double)]
 
     def as_dict(self):
         d = {n: getattr(self, n) for n, _ in self._fields_}

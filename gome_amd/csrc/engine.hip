@@ -22,6 +22,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -186,6 +187,7 @@ struct Slot {
   hipEvent_t h2d{}, done{};
   hipEvent_t ph[GOME_NPHASE][2]{};  // GOME_PH_* phase brackets (ph_on: recorded this batch)
   bool ph_on[GOME_NPHASE]{};
+  double ms_enqueue = 0;  // host wall time of enqueue()
 };
 
 struct Flight {
@@ -462,9 +464,11 @@ gome_status gome_engine::init(const gome_config& c) {
       !alloc(&F.srt, ntouch, "flow level runs") || !alloc(&F.rs, ntouch, "flow new makers") ||
       !alloc(&F.fbase, ntouch, "flow fill bases") || !alloc(&F.ig, F.ig_cap, "flow gathered makers") ||
       !alloc(&F.ig_bump, 1, "flow gather bump") || !alloc(&F.toff, 2 * FC_TOFF, "flow touch offsets") ||
+      !alloc(&F.tmap, 6ull * (ntouch / 64 + 2), "flow touch-group books") ||
       !alloc(&F.lvout, static_cast<size_t>(MAX_FLOW) * FL_CAP, "flow final levels"))
     return GOME_E_CAPACITY;
   F.maxt = ceil_div(ntouch, FL_TILE);
+  F.tmap_stride = static_cast<uint32_t>(ntouch / 64 + 2);
   if (!alloc(&F.tcnt, static_cast<size_t>(FL_HEAD) * F.maxt * FL_CAP, "flow head tile counts") ||
       !alloc(&F.pscr, FL_HEAD, "flow head prep scratch"))
     return GOME_E_CAPACITY;
@@ -524,6 +528,7 @@ void gome_engine::scan(const uint32_t* in, uint32_t m, uint32_t* out, uint32_t* 
 gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_t s, uint32_t sl,
                                  uint64_t seq_base, uint64_t inflight_n) {
   Slot& S = slots[sl];
+  const auto t_enq = std::chrono::steady_clock::now();
   // conservative event bound: one partial per ADD + one event per DEL + one per popped
   // maker (<= resting + ADDs) + block padding; batches still in flight may add to resting
   const unsigned long long rest_ub = resting + inflight_n;
@@ -641,14 +646,21 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   // before the hottest); FT: the tail.  tb: each range's slice of toff.
   FlowArgs FH = F, FH0 = F, FH1 = F, FT = F;
   FH.h0 = 0; FH.h1 = FL_HEAD; FH.tb = 0;
-  FH0.h0 = 0; FH0.h1 = 1; FH0.tb = 0;
-  FH1.h0 = 1; FH1.h1 = FL_HEAD; FH1.tb = 2;
-  FT.h0 = FL_HEAD; FT.h1 = MAX_FLOW; FT.tb = FL_HEAD + 3;
+  FH0.h0 = 0; FH0.h1 = 1; FH0.tb = 0; FH0.mb = 0;
+  FH1.h0 = 1; FH1.h1 = FL_HEAD; FH1.tb = 2; FH1.mb = 1;
+  FT.h0 = FL_HEAD; FT.h1 = MAX_FLOW; FT.tb = FL_HEAD + 3; FT.mb = 2;
   FH.ds0 = 0; FH.ds1 = FL_HEAD; FH0.ds0 = 0; FH0.ds1 = 1; FH1.ds0 = 1; FH1.ds1 = FL_HEAD;
   FT.ds0 = FL_HEAD; FT.ds1 = F.dslots;
   // the ranges' books with DELs count and place their events through a second toff region
   FlowArgs FH0c = FH0, FH1c = FH1, FTc = FT;
   FH0c.tb += FC_TOFF; FH1c.tb += FC_TOFF; FTc.tb += FC_TOFF;
+  FH0c.mb += 3; FH1c.mb += 3; FTc.mb += 3;
+  // a range's touch offsets, then its group map
+  auto toff = [&](const FlowArgs& R, bool cancel, hipStream_t st) {
+    if (cancel) k_flow_toff<FL_OK_CANCEL><<<1, 1024, 0, st>>>(D, R);
+    else k_flow_toff<FL_OK_ADD><<<1, 1024, 0, st>>>(D, R);
+    k_flow_tmap<<<std::min<uint32_t>(ceil_div(R.h1 - R.h0, 4), 1024), 256, 0, st>>>(D, R);
+  };
   const uint32_t nh_head = std::min<uint32_t>(FL_HEAD, nhot_max);
   const uint32_t nh_near = nh_head > 1 ? nh_head - 1 : 0;
   const uint32_t nh_tail = nhot_max > FL_HEAD ? nhot_max - FL_HEAD : 0;
@@ -703,7 +715,7 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   HIPCHK(hipStreamWaitEvent(s, adm_done, 0));
   // k_prep gathers the same records as the head's prep: let the head's prep (the critical
   // path) have the memory system first; the cold books have slack
-  HIPCHK(hipStreamWaitEvent(s, prep_h, 0));
+  HIPCHK(hipStreamWaitEvent(s, prep_h, 0));  // (A/B r3j: without it config 2 -0.14 ms, config 3 +0.2 ms)
 
   // ---- match_books: one wavefront per book; hot books (LDS) on a second stream,
   //      concurrently with the cold books (HBM)
@@ -751,7 +763,7 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
     k_flow_sort_scatter<<<dim3(FL_SORT_GRID, nb), FL_TILE, 0, st>>>(D, R);
     if (!split) deep_sort_level(R, FL_SORT_GRID, st);
     k_flow_level_wide<<<dim3(FL_CAP, nb), FL_LVB_T, 0, st>>>(D, R);
-    k_flow_toff<FL_OK_ADD><<<1, 1024, 0, st>>>(D, R);
+    toff(R, false, st);
     if (split) {
       HIPCHK(hipEventRecord(cnt_fork, st));
       HIPCHK(hipStreamWaitEvent(cs, cnt_fork, 0));
@@ -770,7 +782,7 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   // books with DELs (match_flow_cancel.h); their events go to the arena
   auto head_recon_c = [&](const FlowArgs& R, const FlowArgs& Rc, uint32_t nb, hipStream_t st) {
     k_fc_level_blk<<<dim3(FL_CAP, nb), FC_LVB_T, 0, st>>>(D, R);
-    k_flow_toff<FL_OK_CANCEL><<<1, 1024, 0, st>>>(D, Rc);
+    toff(Rc, true, st);
     k_fc_count<<<1024, 256, 0, st>>>(D, B, Rc);
     k_fc_write_lv<<<dim3(FL_CAP, nb), 64, 0, st>>>(D, B, Rc);
     k_fc_fin<<<nb, 128, 0, st>>>(D, Rc);
@@ -811,17 +823,17 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
     deep_sort_level(FT, 32, s);
     HIPCHK(mark(GOME_PH_TAIL_LEVEL, 1, s));
     HIPCHK(mark(GOME_PH_TAIL_COUNT, 0, s));
-    k_flow_toff<FL_OK_ADD><<<1, 1024, 0, s>>>(D, FT);
+    toff(FT, false, s);
     HIPCHK(mark(GOME_PH_TAIL_COUNT, 1, s));
+    // the flow books' writes beside their events (into the arena: k_ev_scatter places them
+    // after the publish scan), then the deep books' writes
     HIPCHK(mark(GOME_PH_TAIL_WRITE, 0, s));
-    k_flow_write<<<nh_tail, FL_WRITE_T, 0, s>>>(D, B, FT);
-    deep_write(FT, s);
+    k_flow_write_events<<<nh_tail + ceil_div(tail_grid * FL_EV_T, FL_WRITE_T), FL_WRITE_T, 0, s>>>(D, B, FT, nh_tail);
     HIPCHK(mark(GOME_PH_TAIL_WRITE, 1, s));
-    // the tail's events into the arena now (k_ev_scatter places them after the scan)
     HIPCHK(mark(GOME_PH_TAIL_EVENTS, 0, s));
-    k_flow_events_fused<<<tail_grid, FL_EV_T, 0, s>>>(D, B, FT);
+    deep_write(FT, s);
     k_fc_level_book<<<nh_tail, 1024, 0, s>>>(D, FT);
-    k_flow_toff<FL_OK_CANCEL><<<1, 1024, 0, s>>>(D, FTc);
+    toff(FTc, true, s);
     k_fc_count<<<1024, 256, 0, s>>>(D, B, FTc);
     k_fc_write_book<<<nh_tail, FL_WRITE_T, 0, s>>>(D, B, FTc);
     k_fc_events<<<1024, 256, 0, s>>>(D, B, FTc);
@@ -880,6 +892,7 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   HIPCHK(hipEventRecord(S.ev1, s));
   HIPCHK(hipMemcpyAsync(S.h_st, d_st, sizeof(Status), hipMemcpyDeviceToHost, s));
   HIPCHK(hipEventRecord(S.done, s));
+  S.ms_enqueue = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_enq).count();
   return GOME_OK;
 }
 
@@ -945,6 +958,7 @@ gome_status gome_engine::finish(uint32_t sl, uint32_t n) {
     if (S.ph_on[k]) (void)hipEventElapsedTime(&ms, S.ph[k][0], S.ph[k][1]);
     stats.ms_phase[k] = ms;
   }
+  stats.ms_host_enqueue = S.ms_enqueue;
   if (const uint64_t nd = std::min<uint64_t>(st.ctr[C_DUP], n)) {
     dup_idx.resize(nd);
     HIPCHK(hipMemcpy(dup_idx.data(), S.d_dup, nd * sizeof(uint32_t), hipMemcpyDeviceToHost));

@@ -224,6 +224,10 @@ struct FlowArgs {
   uint32_t ds0, ds1;   // the deep slots a launch covers (the range's)
   Touch* tlog;         // the first sort pass's output (the log's index space)
   uint32_t fc_gen;     // batch generation (FcHash entries of older batches are empty)
+  // per range (region mb): the book of each 64-touch group of the range's flattened touches
+  // (k_flow_tmap), so a wave finds its book with one load instead of a search of toff
+  uint32_t* tmap;
+  uint32_t tmap_stride, mb;
 };
 
 __device__ __forceinline__ uint32_t fl_hend(const Dev& D, const FlowArgs& F) { return min(F.h1, D.st->nhot); }
@@ -1551,28 +1555,19 @@ __device__ __forceinline__ FlTouchCtx fl_touch_ctx(const FlowArgs& F, uint32_t h
   const int64_t d0 = t.Lq->d0;
   const uint32_t ig_n = t.Lq->ig_n, nrest = t.Lq->nrest;
   t.first = fl_find(t.IG, ig_n, t.RS, nrest, d0, t.c);
-  t.last = fl_find(t.IG, ig_n, t.RS, nrest, d0, t.c + t.a - 1);
+  // most touches end inside their first maker: probe it before searching for the last
+  const uint32_t f = t.first;
+  const int64_t xl = t.c + t.a - 1;
+  const int64_t fend = f < ig_n ? t.IG[f].e + t.IG[f].v : t.RS[f - ig_n].e + t.RS[f - ig_n].v;
+  t.last = xl < fend ? f : fl_find(t.IG, ig_n, t.RS, nrest, d0, xl);
   return t;
 }
 
-// Book of flattened touch index gt: the last h with toff[h] <= gt.
-__device__ __forceinline__ uint32_t fl_book_of(const FlowArgs& F, uint32_t nb, uint32_t gt) {
-  const uint32_t* to = F.toff + F.tb;
-  uint32_t lo = 0, hi = nb;
-  while (hi - lo > 1) {
-    const uint32_t mid = (lo + hi) >> 1;
-    if (to[mid] <= gt) lo = mid; else hi = mid;
-  }
-  return lo;
-}
-
-// The same for every lane of a wave whose touches are consecutive from g0 (lane 0's): one
-// binary search per wave, then each lane steps over the (at most few) book boundaries after g0.
-// Called by every lane whose gt < total (lane 0 among them).
+// The same for every lane of a wave whose touches are consecutive from g0 (lane 0's, a multiple
+// of 64): the book of g0's group from the range's map, then each lane steps over the (at most
+// few) book boundaries after g0.  Called by every lane whose gt < total (lane 0 among them).
 __device__ __forceinline__ uint32_t fl_book_of_wave(const FlowArgs& F, uint32_t nb, uint32_t g0, uint32_t gt) {
-  uint32_t hb = 0;
-  if (lane_id() == 0) hb = fl_book_of(F, nb, g0);
-  hb = __shfl(hb, 0);
+  uint32_t hb = F.tmap[static_cast<size_t>(F.mb) * F.tmap_stride + (g0 >> 6)];
   const uint32_t* to = F.toff + F.tb;
   while (hb + 1 < nb && to[hb + 1] <= gt) ++hb;
   return hb;
@@ -1602,6 +1597,18 @@ __global__ __launch_bounds__(1024) void k_flow_toff(Dev D, FlowArgs F) {
   for (uint32_t i = b0; i < b0 + per && i < nb; ++i) {
     toff[i] = acc;
     acc += mine(hdr[i].ok) ? hdr[i].ntouch : 0u;
+  }
+}
+
+// The range's group map (FlowArgs::tmap), one wave per book: group g (touches [64g, 64g + 64))
+// belongs to the book holding touch 64g.
+__global__ __launch_bounds__(256) void k_flow_tmap(Dev D, FlowArgs F) {
+  const uint32_t hend = fl_hend(D, F), nb = hend > F.h0 ? hend - F.h0 : 0u;
+  const uint32_t* to = F.toff + F.tb;
+  uint32_t* map = F.tmap + static_cast<size_t>(F.mb) * F.tmap_stride;
+  for (uint32_t i = blockIdx.x * 4 + (threadIdx.x >> 6); i < nb; i += gridDim.x * 4) {
+    const uint32_t g0 = (to[i] + 63) >> 6, g1 = (to[i + 1] + 63) >> 6;
+    for (uint32_t g = g0 + lane_id(); g < g1; g += 64) map[g] = i;
   }
 }
 
@@ -1796,13 +1803,16 @@ __device__ __forceinline__ T wave_seg_incl(T v, unsigned long long heads) {
 // book's log, so its fill_idx bases and the volume its better levels took are segmented scans
 // over the touches (a wave's first lane walks back into an order begun before the wave); the
 // order's last touch writes ev_count[taker].
-__global__ __launch_bounds__(FL_EV_T) void k_flow_events_fused(Dev D, BatchArgs B, FlowArgs F) {
+// Blocks bid of nblk, T threads each.
+template <uint32_t T>
+__device__ __forceinline__ void fl_events_fused(const Dev& D, const BatchArgs& B, const FlowArgs& F, uint32_t bid,
+                                                uint32_t nblk) {
   const uint32_t hend = fl_hend(D, F), nb = hend > F.h0 ? hend - F.h0 : 0u;
   const uint32_t total = nb ? F.toff[F.tb + nb] : 0u;
-  const uint32_t lane = lane_id(), w = threadIdx.x >> 6, stride = gridDim.x * blockDim.x;
-  __shared__ uint32_t wtot[FL_EV_T / 64], bbase;
+  const uint32_t lane = lane_id(), w = threadIdx.x >> 6, stride = nblk * T;
+  __shared__ uint32_t wtot[T / 64], bbase;
   unsigned long long fills = 0, pops = 0;
-  for (uint32_t b0 = blockIdx.x * blockDim.x; b0 < total; b0 += stride) {
+  for (uint32_t b0 = bid * T; b0 < total; b0 += stride) {
     const uint32_t gt = b0 + threadIdx.x, g0w = b0 + (threadIdx.x & ~63u);
     const bool valid = gt < total;
     uint32_t h = 0, L = 0, t = 0, nt = 0, beg = 0, j = 0, cnt = 0;
@@ -1864,7 +1874,7 @@ __global__ __launch_bounds__(FL_EV_T) void k_flow_events_fused(Dev D, BatchArgs 
     __syncthreads();
     if (threadIdx.x == 0) {
       uint32_t s = 0;
-      for (uint32_t k = 0; k < FL_EV_T / 64; ++k) { const uint32_t v = wtot[k]; wtot[k] = s; s += v; }
+      for (uint32_t k = 0; k < T / 64; ++k) { const uint32_t v = wtot[k]; wtot[k] = s; s += v; }
       bbase = s ? atomicAdd(&D.st->ev_bump, s) : 0u;
       if (s && static_cast<unsigned long long>(bbase) + s > B.arena_cap) {
         atomicOr(&D.st->err, ERR_EVENTS);
@@ -1936,6 +1946,9 @@ __global__ __launch_bounds__(FL_EV_T) void k_flow_events_fused(Dev D, BatchArgs 
     if (F.h0 >= FL_HEAD) atomicAdd(&D.st->ctr[C_FLOW_TAIL_FILLS], fills);
     atomicAdd(&D.st->ctr[C_RESTING_DELTA], static_cast<unsigned long long>(-static_cast<long long>(pops)));
   }
+}
+__global__ __launch_bounds__(FL_EV_T) void k_flow_events_fused(Dev D, BatchArgs B, FlowArgs F) {
+  fl_events_fused<FL_EV_T>(D, B, F, blockIdx.x, gridDim.x);
 }
 
 // ============================================================== k_flow_write
@@ -2135,13 +2148,12 @@ __device__ __forceinline__ void fl_write_finish(const Dev& D, const FlowHdr& hd,
 
 // Tail books: one workgroup per book; the chunk ids of all its appends in one claim, then
 // waves take its levels in turn, then finish.
-__global__ __launch_bounds__(FL_WRITE_T) void k_flow_write(Dev D, BatchArgs B, FlowArgs F) {
+__device__ __forceinline__ void fl_write_book(const Dev& D, const BatchArgs& B, const FlowArgs& F, uint32_t h) {
   __shared__ Level lv[FL_CAP];
   __shared__ uint32_t keep[FL_CAP];
   __shared__ uint32_t nout_s, base_s, cap_s;
   __shared__ uint32_t need_s[FL_CAP];
   __shared__ FlClaim claim_s;
-  const uint32_t h = F.h0 + blockIdx.x;
   if (h >= fl_hend(D, F) || F.hdr[h].ok != FL_OK_ADD) return;
   const FlowHdr hd = F.hdr[h];
   const uint32_t w = threadIdx.x >> 6, nw = FL_WRITE_T / 64;
@@ -2164,6 +2176,20 @@ __global__ __launch_bounds__(FL_WRITE_T) void k_flow_write(Dev D, BatchArgs B, F
   }
   __syncthreads();
   fl_write_finish(D, hd, lv, keep, base_s, cap_s, nout_s);
+}
+__global__ __launch_bounds__(FL_WRITE_T) void k_flow_write(Dev D, BatchArgs B, FlowArgs F) {
+  fl_write_book(D, B, F, F.h0 + blockIdx.x);
+}
+
+// The tail's writes and events in one launch (both need only the level pass, and both wait on
+// memory latency, so they overlap): blocks [0, nwb) write book h0 + blockIdx.x, the rest run the
+// fused event pass in FL_WRITE_T-thread tiles.
+__global__ __launch_bounds__(FL_WRITE_T) void k_flow_write_events(Dev D, BatchArgs B, FlowArgs F, uint32_t nwb) {
+  if (blockIdx.x < nwb) {
+    fl_write_book(D, B, F, F.h0 + blockIdx.x);
+    return;
+  }
+  fl_events_fused<FL_WRITE_T>(D, B, F, blockIdx.x - nwb, gridDim.x - nwb);
 }
 
 // Head books: fl_write_level with a whole block (FL_LVB_T threads) per (book, level) -- the chunk

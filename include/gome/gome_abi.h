@@ -170,9 +170,10 @@ enum {
   GOME_PH_TAIL_PLAN,     /* tail books: serial plans (k_flow_plan_tail, _c, _d)           */
   GOME_PH_TAIL_SORT,     /* tail books: touches sorted by level (k_flow_sort)             */
   GOME_PH_TAIL_LEVEL,    /* tail books: level reconstruction (k_flow_level, deep levels)  */
-  GOME_PH_TAIL_COUNT,    /* tail books: the touch offsets (k_flow_toff)                   */
-  GOME_PH_TAIL_WRITE,    /* tail books: FIFO appends, level arrays (k_flow_write, deep)   */
-  GOME_PH_TAIL_EVENTS,   /* tail books: events + ev_count (k_flow_events_fused), DEL books */
+  GOME_PH_TAIL_COUNT,    /* tail books: the touch offsets and group map (k_flow_toff/tmap) */
+  GOME_PH_TAIL_WRITE,    /* tail books: FIFO appends, level arrays, events and ev_count
+                            in one launch (k_flow_write_events)                         */
+  GOME_PH_TAIL_EVENTS,   /* tail books: the deep books' writes, the DEL books' chain      */
   GOME_PH_NEAR,          /* the other head books: plans and reconstruction               */
   GOME_PH_PUBLISH,       /* publish-order scan, the hottest book's events, arena scatter  */
   GOME_NPHASE = 16
@@ -211,6 +212,9 @@ typedef struct gome_stats {
                                                  in n_dropped)                           */
   uint64_t n_flow_tail_fills;                 /* fills of the tail's flow books (ABI >= 5) */
   double ms_phase[GOME_NPHASE];               /* GOME_PH_* device times (ABI >= 5)        */
+  double ms_host_enqueue;                     /* host wall time the batch's launches took
+                                                 (ABI >= 5): the GPU cannot finish before
+                                                 the last one is issued                  */
 } gome_stats;
 
 typedef struct gome_engine gome_engine;

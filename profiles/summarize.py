@@ -1,6 +1,6 @@
 """Summarise a rocprofv3 run of bench.py (profiles/run_rocprof.sh) into profiles/<tag>.md
-and update profiles/traffic.json (PMC HBM bytes per launch of the roofline kernel,
-k_flow_plan_head: the serial aggregate plan of the longest flow books, the batch's critical path).
+and update profiles/traffic.json (PMC HBM bytes per launch of the bench line's roofline kernel,
+keyed "<workload>:<kernel>_hbm_bytes_per_launch"; other entries are kept).
 
 gfx950 corrections (MI355X_MICROARCH.md §HBM, cdna_hip_programming.md §7): FETCH_SIZE and
 WRITE_SIZE are in KiB; FETCH_SIZE reads half the bytes of wide (16 B/lane) coalesced
@@ -18,18 +18,17 @@ def rows(path):
         return list(csv.DictReader(f))
 
 
-KERNEL = "k_flow_plan_head"
-
-
 def main(tag, src):
     st = rows(os.path.join(src, "trace", "run_kernel_stats.csv"))
     bench = None
     for line in open(os.path.join(src, "bench_trace.log")):
         if line.startswith("{"):
             bench = json.loads(line)
+    KERNEL = bench["roofline"]["kernel"].split(" ")[0] if bench else "k_flow_plan_head"
+    workload = bench["config"].get("name", "config3") if bench else "config3"
     def pmc(sub, name):
         vals = [float(r["Counter_Value"]) for r in rows(os.path.join(src, sub, "run_counter_collection.csv"))
-                if r["Kernel_Name"] == KERNEL and r["Counter_Name"] == name]
+                if r["Kernel_Name"].split("(")[0].replace("void ", "").strip() == KERNEL and r["Counter_Name"] == name]
         return sum(vals) / len(vals) if vals else None
     fetch_kib, write_kib = pmc("fetch", "FETCH_SIZE"), pmc("write", "WRITE_SIZE")
     out = [f"# rocprofv3 summary `{tag}`", "",
@@ -38,7 +37,7 @@ def main(tag, src):
            "| kernel | calls | avg ns | % |", "|---|---|---|---|"]
     for r in st[:16]:
         out.append(f"| {r['Name']} | {r['Calls']} | {float(r['AverageNs']):.0f} | {float(r['Percentage']):.3f} |")
-    km = next(r for r in st if r["Name"] == KERNEL)
+    km = next(r for r in st if r["Name"].split("(")[0].replace("void ", "").strip() == KERNEL)
     out += ["", f"{KERNEL} average duration (rocprof, all launches incl. warmup): "
                 f"{float(km['AverageNs'])/1e6:.3f} ms"]
     if bench:
@@ -50,10 +49,12 @@ def main(tag, src):
         out += [f"FETCH_SIZE per {KERNEL} launch: {fetch_kib:.0f} KiB = {fb/1e6:.1f} MB (x2 wide-stream correction: {2*fb/1e6:.1f} MB)",
                 f"WRITE_SIZE per {KERNEL} launch: {write_kib:.0f} KiB = {wb/1e6:.1f} MB",
                 f"traffic estimate (FETCH+WRITE): {(fb+wb)/1e6:.1f} MB per launch"]
-        json.dump({"tag": tag, "kernel": KERNEL, "k_flow_plan_head_hbm_bytes_per_launch": int(fb + wb),
-                   "fetch_bytes": int(fb), "write_bytes": int(wb),
-                   "note": "rocprofv3 PMC, separate passes, KiB->bytes; FETCH_SIZE not x2-corrected"},
-                  open(os.path.join(os.path.dirname(__file__), "traffic.json"), "w"), indent=1)
+        tp = os.path.join(os.path.dirname(__file__), "traffic.json")
+        tj = json.load(open(tp)) if os.path.exists(tp) else {}
+        tj[f"{workload}:{KERNEL}_hbm_bytes_per_launch"] = int(fb + wb)
+        tj[f"{workload}:{KERNEL}_detail"] = {"tag": tag, "fetch_bytes": int(fb), "write_bytes": int(wb),
+                                             "note": "rocprofv3 PMC, separate passes, KiB->bytes; FETCH_SIZE not x2-corrected"}
+        json.dump(tj, open(tp, "w"), indent=1)
     tr = rows(os.path.join(src, "trace", "run_kernel_trace.csv"))
     starts = [int(r["Start_Timestamp"]) for r in tr if r["Kernel_Name"].startswith("k_adm")]
     if starts:  # timeline of the last batch (k_adm and the radix sort open every batch)

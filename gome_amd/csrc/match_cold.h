@@ -81,6 +81,7 @@ struct WaveCtx {
   uint32_t cpool, npool;
 };
 constexpr uint32_t CPOOL = 32;
+constexpr uint32_t COLD_SCAN_FROM = 256;  // levels above which do_add's scan starts at the spread
 
 __device__ __forceinline__ void set_err(WaveCtx& W, uint32_t e) {
   if (lane_id() == 0) atomicOr(&W.D.st->err, e);
@@ -531,9 +532,39 @@ __device__ __forceinline__ uint32_t do_add(WaveCtx& W, int64_t p, int64_t vol, u
   int64_t T = vol;
   bool crossed = false;
   uint32_t fidx = 0;
-  // GetReverseDepth (nodepool.go:86-115): opposite-side levels crossing p, best first.
+  // GetReverseDepth (nodepool.go:86-115): opposite-side levels crossing p, best first.  In a
+  // book without quirks every bid is below every ask (a rest follows a complete sweep), so on a
+  // deep book the scan starts just above the highest bid <= p (BUY) or just below the lowest
+  // ask >= p (SALE) instead of walking the book's other side from its far end.
+  uint32_t up0 = 0;
+  int32_t dn0 = static_cast<int32_t>(W.nl);
+  if (!(W.flags & BOOK_QUIRK) && W.nl > COLD_SCAN_FROM) {
+    uint32_t pos;
+    const bool at = level_search(W, p, pos);
+    if (!sale) {
+      for (int32_t hi = static_cast<int32_t>(pos + (at ? 1u : 0u)); hi > 0; hi -= 64) {
+        const int32_t lo = max(hi - 64, 0), k = lo + static_cast<int32_t>(lane);
+        const bool v = k < hi;
+        const unsigned long long bm = __ballot(v && (W.L[v ? k : 0].member & M_BUY));
+        if (bm) {
+          up0 = static_cast<uint32_t>(lo) + 64u - static_cast<uint32_t>(__builtin_clzll(bm));
+          break;
+        }
+      }
+    } else {
+      for (uint32_t w0 = pos; w0 < W.nl; w0 += 64) {
+        const uint32_t k = w0 + lane;
+        const bool v = k < W.nl;
+        const unsigned long long am = __ballot(v && (W.L[v ? k : 0].member & M_SALE));
+        if (am) {
+          dn0 = static_cast<int32_t>(w0 + static_cast<uint32_t>(__builtin_ctzll(am)));
+          break;
+        }
+      }
+    }
+  }
   if (!sale) {
-    for (uint32_t w0 = 0; w0 < W.nl && !W.fatal; w0 += 64) {
+    for (uint32_t w0 = up0; w0 < W.nl && !W.fatal; w0 += 64) {
       const uint32_t k = w0 + lane;
       const bool v = k < W.nl;
       int64_t lp = 0;
@@ -551,7 +582,7 @@ __device__ __forceinline__ uint32_t do_add(WaveCtx& W, int64_t p, int64_t vol, u
       if (beyond) break;
     }
   } else {
-    for (int32_t top = static_cast<int32_t>(W.nl); top > 0 && !W.fatal; top -= 64) {
+    for (int32_t top = dn0; top > 0 && !W.fatal; top -= 64) {
       const int32_t lo = top - 64, k = lo + static_cast<int32_t>(lane);
       const bool v = k >= 0;
       int64_t lp = 0;

@@ -204,7 +204,7 @@ struct gome_engine {
   hipStream_t flow_stream = nullptr;  // the hottest book's plan (critical path)
   hipStream_t copy_stream = nullptr;  // H2D of records, D2H of events (pipelined path)
   hipEvent_t fork{}, join{}, joinf{}, prep_h{}, prep_t{}, fork_adm{}, adm_done{}, seg_done{}, ev_scan{}, ev_hot{};
-  hipEvent_t dp_fork{}, cnt_fork{}, cnt_done{}, dw_done{};  // the hottest book's deep chain, k_flow_count beside its writes
+  hipEvent_t dp_fork{}, cnt_fork{}, cnt_done{}, dw_done{}, dl_done{};  // the hottest book's deep chain, k_flow_count beside its writes
   Slot slots[GOME_MAX_INFLIGHT];
   uint32_t next_slot = 0;
   std::deque<Flight> flights;
@@ -351,7 +351,7 @@ gome_status gome_engine::init(const gome_config& c) {
   HIPCHK(hipStreamCreateWithFlags(&flow_stream, hipStreamNonBlocking));
   HIPCHK(hipStreamCreateWithFlags(&copy_stream, hipStreamNonBlocking));
   for (hipEvent_t* ev : {&fork, &join, &joinf, &prep_h, &prep_t, &fork_adm, &adm_done, &seg_done, &ev_scan, &ev_hot,
-                         &dp_fork, &cnt_fork, &cnt_done, &dw_done})
+                         &dp_fork, &cnt_fork, &cnt_done, &dw_done, &dl_done})
     HIPCHK(hipEventCreateWithFlags(ev, hipEventDisableTiming));
   for (Slot& S : slots) {
     for (hipEvent_t* ev : {&S.ev0, &S.ev1, &S.evm0, &S.evm1, &S.evh0, &S.evh1, &S.evf0, &S.evf1, &S.evc0, &S.evc1})
@@ -685,23 +685,45 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
     k_deep_prep_c<<<dim3(px, ns), FL_PREP_T, 0, st>>>(D, B, R);
   };
   deep_prep(FH, FL_PG, flow_stream);
-  // books with DELs: targets, windows, Q and the W32C DEL records (or back to the legacy path)
+  // deep books: the two-pass stable sort of a log by level (touches, or the cancel prep's keys)
+  // and each level's run
+  auto deep_sort = [&](const FlowArgs& R, uint32_t tiles, hipStream_t st) {
+    const uint32_t ns = std::min<uint32_t>(R.ds1 - R.ds0, DEEP_GRID_T);  // (blocks walk the slots)
+    k_deep_sort_cnt<1><<<dim3(tiles, ns), FL_TILE, 0, st>>>(D, R);
+    k_deep_sort_scan<<<ns, FL_CAP, 0, st>>>(D, R);
+    k_deep_sort_scatter<1><<<dim3(tiles, ns), FL_TILE, 0, st>>>(D, R);
+    k_deep_sort_cnt<2><<<dim3(tiles, ns), FL_TILE, 0, st>>>(D, R);
+    k_deep_sort_scan<<<ns, FL_CAP, 0, st>>>(D, R);
+    k_deep_sort_scatter<2><<<dim3(tiles, ns), FL_TILE, 0, st>>>(D, R);
+    k_deep_runs<<<dim3(64, ns), 256, 0, st>>>(D, R);
+  };
+  // books with DELs: targets, windows, Q and the W32C / W32DC DEL records (or back to the legacy
+  // path).  The deep books' ranks come from a sort of their records by level (match_flow_deep.h).
   auto cancel_prep = [&](const FlowArgs& R, uint32_t nb, uint32_t px, bool wide, hipStream_t st) {
+    const uint32_t ns = std::min<uint32_t>(R.ds1 - R.ds0, DEEP_GRID_T);
     k_fc_hash_claim<<<dim3(px, nb), 256, 0, st>>>(D, B, R);
     k_fc_hash_count<<<dim3(px, nb), 256, 0, st>>>(D, B, R);
     k_fc_hash_first<<<dim3(px, nb), 256, 0, st>>>(D, B, R);
     k_fc_resolve<<<dim3(px, nb), 256, 0, st>>>(D, B, R);
+    k_fd_oldwalk<<<dim3(DEEP_GRID, ns), 64, 0, st>>>(D, R);
+    k_fd_ckeys<<<dim3(wide ? 256 : 16, ns), 256, 0, st>>>(D, B, R);
+    deep_sort(R, wide ? FL_SORT_GRID : 32, st);
+    k_fd_crank<<<dim3(DEEP_GRID, ns), 64, 0, st>>>(D, B, R);
+    k_fd_tbase<<<ns, DEEP_CLAIM_T, 0, st>>>(D, R);
     if (wide) {  // the head: tile-parallel ranks, windows, layout and records
       k_fc_oldwalk_wide<<<dim3(FL_CAP, nb), 64, 0, st>>>(D, R);
       k_fc_pcnt<<<dim3(FL_SORT_GRID, nb), FL_TILE, 0, st>>>(D, B, R);
       k_fc_pscan<<<nb, FL_CAP, 0, st>>>(D, R);
       k_fc_prank<<<dim3(FL_SORT_GRID, nb), FL_TILE, 0, st>>>(D, B, R);
-      k_fc_pwin<<<dim3(px, nb), 256, 0, st>>>(D, B, R);
-      k_fc_precs<<<dim3(px, nb), 256, 0, st>>>(D, B, R);
+      k_fc_pwin<<<dim3(px, nb), 256, 0, st>>>(D, B, R, 0u);
+      k_fc_precs<<<dim3(px, nb), 256, 0, st>>>(D, B, R, 0u);
     } else {
       k_fc_oldwalk_book<<<nb, 1024, 0, st>>>(D, R);
       k_fc_pass<<<nb, FC_PASS_T, 0, st>>>(D, B, R);
+      k_fc_pwin<<<dim3(px, nb), 256, 0, st>>>(D, B, R, 1u);
+      k_fc_precs<<<dim3(px, nb), 256, 0, st>>>(D, B, R, 1u);
     }
+    k_fd_decline<<<ns, 256, 0, st>>>(D, R);
     k_fc_unmark<<<dim3(px, nb), 256, 0, st>>>(D, B, R);
     k_fc_route<<<ceil_div(nb, 256), 256, 0, st>>>(D, R);
   };
@@ -729,13 +751,7 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   // deep books: the two-pass level sort and the per-level reconstruction, then the writes
   auto deep_sort_level = [&](const FlowArgs& R, uint32_t tiles, hipStream_t st) {
     const uint32_t ns = std::min<uint32_t>(R.ds1 - R.ds0, DEEP_GRID_T);  // (blocks walk the slots)
-    k_deep_sort_cnt<1><<<dim3(tiles, ns), FL_TILE, 0, st>>>(D, R);
-    k_deep_sort_scan<<<ns, FL_CAP, 0, st>>>(D, R);
-    k_deep_sort_scatter<1><<<dim3(tiles, ns), FL_TILE, 0, st>>>(D, R);
-    k_deep_sort_cnt<2><<<dim3(tiles, ns), FL_TILE, 0, st>>>(D, R);
-    k_deep_sort_scan<<<ns, FL_CAP, 0, st>>>(D, R);
-    k_deep_sort_scatter<2><<<dim3(tiles, ns), FL_TILE, 0, st>>>(D, R);
-    k_deep_runs<<<dim3(64, ns), 256, 0, st>>>(D, R);
+    deep_sort(R, tiles, st);
     k_deep_level<<<dim3(DEEP_GRID, ns), 64, 0, st>>>(D, R);
   };
   auto deep_write = [&](const FlowArgs& R, hipStream_t st) {
@@ -757,6 +773,7 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
       HIPCHK(hipEventRecord(dp_fork, st));
       HIPCHK(hipStreamWaitEvent(cs, dp_fork, 0));
       deep_sort_level(R, FL_SORT_GRID, cs);
+      HIPCHK(hipEventRecord(dl_done, cs));  // (a deep book with DELs: k_fc_count / events wait)
     }
     k_flow_sort_cnt<<<dim3(FL_SORT_GRID, nb), FL_TILE, 0, st>>>(D, R);
     k_flow_sort_scan<<<nb, FL_CAP, 0, st>>>(D, R);
@@ -780,13 +797,15 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
     return GOME_OK;
   };
   // books with DELs (match_flow_cancel.h); their events go to the arena
-  auto head_recon_c = [&](const FlowArgs& R, const FlowArgs& Rc, uint32_t nb, hipStream_t st) {
+  auto head_recon_c = [&](const FlowArgs& R, const FlowArgs& Rc, uint32_t nb, hipStream_t st, bool split) -> gome_status {
     k_fc_level_blk<<<dim3(FL_CAP, nb), FC_LVB_T, 0, st>>>(D, R);
+    if (split) HIPCHK(hipStreamWaitEvent(st, dl_done, 0));  // (the deep books' level pass ran on cs)
     toff(Rc, true, st);
     k_fc_count<<<1024, 256, 0, st>>>(D, B, Rc);
     k_fc_write_lv<<<dim3(FL_CAP, nb), 64, 0, st>>>(D, B, Rc);
     k_fc_fin<<<nb, 128, 0, st>>>(D, Rc);
     k_fc_events<<<1024, 256, 0, st>>>(D, B, Rc);
+    return GOME_OK;
   };
   // Streams (HIP maps more streams than its 4 hardware queues per process onto shared queues,
   // which would serialise them): the hottest book on the flow stream; the other head books'
@@ -845,7 +864,7 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
     HIPCHK(mark(GOME_PH_NEAR, 0, hot_stream));
     k_flow_plan_near<<<nh_near, 256, plan_lds, hot_stream>>>(D, FH1);
     if (head_recon(FH1, nh_near, hot_stream, hot_stream, true) != GOME_OK) return GOME_E_DEVICE;
-    head_recon_c(FH1, FH1c, nh_near, hot_stream);
+    if (head_recon_c(FH1, FH1c, nh_near, hot_stream, false) != GOME_OK) return GOME_E_DEVICE;
     k_flow_events_fused<<<1024, FL_EV_T, 0, hot_stream>>>(D, B, FH1);
     HIPCHK(mark(GOME_PH_NEAR, 1, hot_stream));
   }
@@ -864,7 +883,7 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   // (the hot stream's own work ended long before the hottest book's plan does)
   HIPCHK(mark(GOME_PH_HEAD_RECON, 0, flow_stream));
   if (head_recon(FH0, 1, flow_stream, hot_stream, false) != GOME_OK) return GOME_E_DEVICE;
-  head_recon_c(FH0, FH0c, 1, flow_stream);
+  if (head_recon_c(FH0, FH0c, 1, flow_stream, true) != GOME_OK) return GOME_E_DEVICE;
   HIPCHK(mark(GOME_PH_HEAD_RECON, 1, flow_stream));
   HIPCHK(hipEventRecord(joinf, flow_stream));
   HIPCHK(hipStreamWaitEvent(s, join, 0));

@@ -957,6 +957,112 @@ class GenD(Gen):
         return self.out
 
 
+# ---- W32DC: the deep plan of a book whose segment holds DELs ---------------
+# ADD records are the W32D records.  A DEL record: hi = level [0, 14) | v << 14 (v < 2^16: the
+# target's volume) | 1 << 30 | maker SALE << 31, lo = Q (as W32C: match_flow_cancel.h).  It removes
+# r = clamp(depth - Q, 0, v) from the maker side's depth of the level: the cached top in SALU (the
+# next level is promoted when it empties), any other level through its LDS slot (one round trip).
+# A slot a DEL empties keeps its group's summary bit: next_top clears a bit whose group it finds
+# empty and searches on.  A DEL that finds nothing logs no touch; its touch key is JJS | 1 << 30 |
+# SALE << 31 (k_fc_* read it as a cancel), its level in the touch's second word.
+class GenDC(GenD):
+    def decode(self, j: int):
+        e = self.e
+        hi = f"s{BUF[j][1]}"
+        e(f"s_add_u32 {JJS}, {JJS}, 256")
+        e(f"s_and_b32 {LI}, {hi}, 0x3fff")
+        e(f"s_bitcmp1_b32 {hi}, 30")
+        e(f"s_cbranch_scc1 {self.lab(f'D{j}')}")
+        e(f"s_bitcmp1_b32 {hi}, 31")
+
+    def del_log(self, r: str):
+        """The cancel touch {K, level, r}; M0 advances only when r != 0 (SCC = r != 0 on entry)."""
+        e = self.e
+        e(f"v_writelane_b32 %[lk], {K}, m0")
+        e(f"v_writelane_b32 %[la], {r}, m0")
+        e(f"v_writelane_b32 %[lb], {LI}, m0")
+        e("s_addc_u32 m0, m0, 0")
+
+    def del_path(self, i: int):
+        e = self.e
+        lo, hi = f"s{BUF[i][0]}", f"s{BUF[i][1]}"
+        lab = self.lab
+        j = (i + 1) % NS
+        X1, XV, X2 = "s94", "s95", "s96"
+        e(f"{lab(f'D{i}')}:")
+        e(f"s_bfe_u32 {XV}, {hi}, 0x10000e")                 # v (bits 14..29)
+        e(f"s_and_b32 {K}, {hi}, 0xc0000000")
+        e(f"s_or_b32 {K}, {K}, {JJS}")                        # the cancel touch key
+        e(f"s_bitcmp1_b32 {hi}, 31")
+        e(f"s_cbranch_scc1 {lab(f'DA{i}')}")
+        for sd in ("B", "A"):
+            if sd == "A":
+                e(f"{lab(f'DA{i}')}:")
+            top, topd = (BB, BBD) if sd == "B" else (BA, BAD)
+            e(f"s_cmp_eq_u32 {LI}, {top}")
+            e(f"s_cbranch_scc1 {lab(f'DT{sd}{i}')}")
+            # a level behind the top: its slot, read, reduced, written back
+            e(f"s_lshl_b32 {T0}, {LI}, 3")
+            e("s_mov_b64 exec, 1")
+            e(f"v_mov_b32 v{VDA}, {T0}")
+            e(f"ds_read_b32 v{VDD}, v{VDA} offset:{self.side_off(sd)}")
+            e("s_waitcnt lgkmcnt(0)")
+            e(f"v_readfirstlane_b32 {X1}, v{VDD}")            # depth
+            e(f"s_sub_u32 {X2}, {X1}, {lo}")                  # SCC = borrow
+            e(f"s_cselect_b32 {X2}, 0, {X2}")
+            e(f"s_min_u32 {X2}, {X2}, {XV}")                  # r
+            e(f"s_sub_u32 {X1}, {X1}, {X2}")
+            e(f"v_mov_b32 v{VDD}, {X1}")
+            e(f"ds_write_b32 v{VDA}, v{VDD} offset:{self.side_off(sd)}")
+            e(f"s_cmp_lg_u32 {X2}, 0")
+            self.del_log(X2)
+            self.dispatch(j, False)
+            # the cached top
+            e(f"{lab(f'DT{sd}{i}')}:")
+            e(f"s_sub_u32 {X1}, {topd[0]}, {lo}")
+            e(f"s_cselect_b32 {X1}, 0, {X1}")
+            e(f"s_min_u32 {X1}, {X1}, {XV}")                  # r
+            e(f"s_sub_u32 {topd[0]}, {topd[0]}, {X1}")
+            e(f"s_cmp_lg_u32 {X1}, 0")
+            self.del_log(X1)
+            e(f"s_cmp_lg_u32 {topd[0]}, 0")
+            e(f"s_cbranch_scc1 {lab(f'DN{i}')}")
+            self.next_top(sd)
+            self.dispatch(j, False)
+
+    def slot(self, i: int):
+        """GenD's slot, the DEL paths placed before the SALE entry."""
+        sv = self.out
+        self.out = []
+        super().slot(i)
+        body = self.out
+        self.out = sv
+        k = body.index(f"{self.lab(f'S{i}')}:")
+        self.out.extend(body[:k])
+        self.del_path(i)
+        self.out.extend(body[k:])
+
+    def next_top(self, sd: str):
+        """GenD.next_top, restarted after clearing the summary bit of a group it finds empty (a
+        DEL emptied its last slot)."""
+        start, stale = self.fresh("NT"), self.fresh("NS")
+        self.e(f"{start}:")
+        sv = self.out
+        self.out = []
+        super().next_top(sd)
+        body = self.out
+        self.out = sv
+        vs = VSUM[sd]
+        M_ = M
+        k = body.index(f"v_cmp_ne_u32_e64 {M_}, 0, v{VSD}") + 1
+        self.out.extend(body[:k])
+        self.e(f"s_cmp_eq_u64 {M_}, 0")
+        self.e(f"s_cbranch_scc1 {stale}")
+        self.out.extend(body[k:])
+        # s79 = the group's summary bit, s81 = its summary lane (set before the group read)
+        self.slow.append([f"{stale}:", "s_bfm_b64 exec, 1, s81", f"v_xor_b32 v{vs}, s79, v{vs}", f"s_branch {start}"])
+
+
 ALIGN = int(os.environ.get("GOME_PLAN_ALIGN", "0"))   # log2 byte alignment of branch targets
 
 
@@ -977,7 +1083,7 @@ def main():
     out = sys.argv[1] if len(sys.argv) > 1 else os.path.join(here, "flow_plan_asm.inc")
     with open(out, "w") as f:
         f.write("// Generated by gen_plan_asm.py — do not edit.\n")
-        for w, g in ((64, Gen(64)), (32, Gen(32)), ("32C", GenC()), ("32D", GenD())):
+        for w, g in ((64, Gen(64)), (32, Gen(32)), ("32C", GenC()), ("32D", GenD()), ("32DC", GenDC())):
             f.write(f"#define FL_PLAN_ASM{w} \\\n")
             for line in aligned(g.build()):
                 f.write(f'  "{line}\\n\\t" \\\n')

@@ -129,7 +129,8 @@ struct FlowHdr {
   uint32_t deep;       // the lane prep found more levels than FL_MAX: a deep-book candidate
   uint32_t dslot;      // its deep slot (head: = h; tail: handed out by k_flow_prep)
   uint32_t nbsum;      // books with DELs: the DEL windows' total (the cancel prep's C loops)
-  uint32_t pad3[4];
+  uint32_t dc;         // a deep book whose segment holds DELs (the W32DC plan)
+  uint32_t pad3[3];
 };
 // FlowHdr::ok: 0 declined, FL_OK_ADD an ADD-only flow book, FL_OK_CANCEL a book with DELs,
 // FL_OK_DEEP an ADD-only head book with more levels than the lane plans hold (match_flow_deep.h)
@@ -1195,12 +1196,21 @@ __device__ __forceinline__ void fl_plan_deep(const Dev& D, const FlowArgs& F, ui
       sb |= (bm[32 * lane + j] != 0 ? 1u : 0u) << j;
       sa |= (bm[DEEP_CAP / 32 + 32 * lane + j] != 0 ? 1u : 0u) << j;
     }
-  asm volatile(FL_PLAN_ASM32D
-               : [lk] "+v"(lg.lk), [la] "+v"(lg.la), [lb] "+v"(lg.lb), [nacc] "+s"(lg.nacc), [lpos] "+s"(lg.lpos),
-                 [voff] "=&v"(voff)
-               : [ob] "s"(ob), [nh] "s"(nh), [logp] "s"(logp), [lcap] "s"(lg.lcap), [vl16] "v"(vl16),
-                 [vzero] "v"(vzero), [sb] "v"(sb), [sa] "v"(sa)
-               : FL_PLAN_CLOBBERS, FL_PLAN_CLOBBERS_D, "scc", "vcc", "memory");
+  if (uni(hd->dc)) {  // DELs in the segment (gen_plan_asm.py W32DC)
+    asm volatile(FL_PLAN_ASM32DC
+                 : [lk] "+v"(lg.lk), [la] "+v"(lg.la), [lb] "+v"(lg.lb), [nacc] "+s"(lg.nacc), [lpos] "+s"(lg.lpos),
+                   [voff] "=&v"(voff)
+                 : [ob] "s"(ob), [nh] "s"(nh), [logp] "s"(logp), [lcap] "s"(lg.lcap), [vl16] "v"(vl16),
+                   [vzero] "v"(vzero), [sb] "v"(sb), [sa] "v"(sa)
+                 : FL_PLAN_CLOBBERS, FL_PLAN_CLOBBERS_D, "scc", "vcc", "memory");
+  } else {
+    asm volatile(FL_PLAN_ASM32D
+                 : [lk] "+v"(lg.lk), [la] "+v"(lg.la), [lb] "+v"(lg.lb), [nacc] "+s"(lg.nacc), [lpos] "+s"(lg.lpos),
+                   [voff] "=&v"(voff)
+                 : [ob] "s"(ob), [nh] "s"(nh), [logp] "s"(logp), [lcap] "s"(lg.lcap), [vl16] "v"(vl16),
+                   [vzero] "v"(vzero), [sb] "v"(sb), [sa] "v"(sa)
+                 : FL_PLAN_CLOBBERS, FL_PLAN_CLOBBERS_D, "scc", "vcc", "memory");
+  }
   if (lg.nacc) {  // {key, level, amount, 0}
     if (lane < lg.nacc && lg.lpos + lg.nacc <= lg.lcap) lg.p[lg.lpos + lane] = v4(lg.lk, lg.lb, lg.la, 0u);
     lg.lpos += lg.nacc;
@@ -1583,8 +1593,11 @@ __global__ __launch_bounds__(1024) void k_flow_toff(Dev D, FlowArgs F) {
   uint32_t* toff = F.toff + F.tb;
   const uint32_t per = (nb + 1023) / 1024, b0 = tid * per;
   uint32_t s = 0;
-  auto mine = [&](uint32_t ok) { return ok == KIND || (KIND == FL_OK_ADD && ok == FL_OK_DEEP); };
-  for (uint32_t i = b0; i < b0 + per && i < nb; ++i) s += mine(hdr[i].ok) ? hdr[i].ntouch : 0u;
+  // (deep books with DELs count with the books with DELs: k_fc_count / k_fc_events)
+  auto mine = [&](const FlowHdr& x) {
+    return x.ok == FL_OK_DEEP ? (KIND == (x.dc ? FL_OK_CANCEL : FL_OK_ADD)) : x.ok == KIND;
+  };
+  for (uint32_t i = b0; i < b0 + per && i < nb; ++i) s += mine(hdr[i]) ? hdr[i].ntouch : 0u;
   part[tid] = s;
   __syncthreads();
   if (tid == 0) {
@@ -1596,7 +1609,7 @@ __global__ __launch_bounds__(1024) void k_flow_toff(Dev D, FlowArgs F) {
   uint32_t acc = part[tid];
   for (uint32_t i = b0; i < b0 + per && i < nb; ++i) {
     toff[i] = acc;
-    acc += mine(hdr[i].ok) ? hdr[i].ntouch : 0u;
+    acc += mine(hdr[i]) ? hdr[i].ntouch : 0u;
   }
 }
 

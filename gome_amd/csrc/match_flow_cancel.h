@@ -78,9 +78,19 @@ enum : uint32_t { FC_NONE = 0, FC_NEW = 1, FC_OLD = 2 };
 
 constexpr uint32_t FC_MAXKEY_SYM = (1u << 21) - 1;  // symbol + 1 fits 21 bits of the key
 
-__device__ __forceinline__ bool fc_book(const FlowArgs& F, uint32_t h) {
+// A book whose segment holds DELs: a lane book (FL_OK_CANCEL) or a deep one (FL_OK_DEEP, dc).
+__device__ __forceinline__ bool fc_dels(const FlowArgs& F, uint32_t h) {
+  return F.hdr[h].ok == FL_OK_CANCEL || (F.hdr[h].ok == FL_OK_DEEP && F.hdr[h].dc);
+}
+__device__ __forceinline__ bool fc_book(const FlowArgs& F, uint32_t h) { return fc_dels(F, h) && !F.hdr[h].fc_bad; }
+// the lane books only (the kernels whose per-level state is FL_CAP wide)
+__device__ __forceinline__ bool fc_lane(const FlowArgs& F, uint32_t h) {
   return F.hdr[h].ok == FL_OK_CANCEL && !F.hdr[h].fc_bad;
 }
+__device__ __forceinline__ bool fc_deep(const FlowArgs& F, uint32_t h) {
+  return F.hdr[h].ok == FL_OK_DEEP && F.hdr[h].dc && !F.hdr[h].fc_bad;
+}
+constexpr uint32_t FD_MAX_V = 1u << 16;  // a deep book's DEL target volume (plan units): 16 bits of its record
 __device__ __forceinline__ void fc_decline(const FlowArgs& F, uint32_t h, uint32_t why) {
   atomicOr(&F.hdr[h].fc_bad, why);
 }
@@ -137,7 +147,7 @@ __device__ __forceinline__ uint32_t fc_old_lookup(const Dev& D, uint32_t sym, ui
 // (The scratch of every book with DELs is reset, declined or not: k_fc_unmark reads it.)
 __global__ __launch_bounds__(256) void k_fc_hash_claim(Dev D, BatchArgs B, FlowArgs F) {
   const uint32_t h = F.h0 + blockIdx.y;
-  if (h >= fl_hend(D, F) || F.hdr[h].ok != FL_OK_CANCEL) return;
+  if (h >= fl_hend(D, F) || !fc_dels(F, h)) return;
   const FlowHdr hd = F.hdr[h];
   uint32_t b0, b1;
   fc_slice(hd, blockIdx.x, gridDim.x, b0, b1);
@@ -219,7 +229,8 @@ __global__ __launch_bounds__(256) void k_fc_resolve(Dev D, BatchArgs B, FlowArgs
   const uint32_t h = F.h0 + blockIdx.y;
   if (h >= fl_hend(D, F) || !fc_book(F, h)) return;
   const FlowHdr hd = F.hdr[h];
-  FlowLvl* LV = F.lvl + h * FL_CAP;
+  FlowLvl* LV = fl_lvls(F, h);
+  const uint32_t lmask = hd.ok == FL_OK_DEEP ? 0x3FFFu : 127u;  // a record's level bits
   uint32_t b0, b1;
   fc_slice(hd, blockIdx.x, gridDim.x, b0, b1);
   for (uint32_t b = b0 + threadIdx.x; b < b1; b += blockDim.x) {
@@ -246,7 +257,7 @@ __global__ __launch_bounds__(256) void k_fc_resolve(Dev D, BatchArgs B, FlowArgs
       if ((a.side == GOME_SALE) != sale) { fc_decline(F, h, FC_BAD_Q2); continue; }  // wrong side (Q2)
       d.kind = FC_NEW;
       d.tgt = e.add_pos;
-      d.li = static_cast<uint32_t>(F.ord8[hd.obase + (e.add_pos - hd.beg)] >> 32) & 127u;
+      d.li = static_cast<uint32_t>(F.ord8[hd.obase + (e.add_pos - hd.beg)] >> 32) & lmask;
       F.fc_del[b] = d;
       F.fc_tg[e.add_pos] = b + 1;
       continue;
@@ -271,7 +282,7 @@ __global__ __launch_bounds__(256) void k_fc_resolve(Dev D, BatchArgs B, FlowArgs
 // ---- prep 4: old targets' FIFO ranks and arrival coordinates (one wave per level) -----------
 __device__ __forceinline__ void fc_oldwalk_level(const Dev& D, const FlowArgs& F, uint32_t h, uint32_t q) {
   const FlowHdr& hd = F.hdr[h];
-  FlowLvl* Lq = F.lvl + h * FL_CAP + q;
+  FlowLvl* Lq = fl_lvls(F, h) + q;
   const uint32_t cold = uni(Lq->c_old);
   if (!cold) return;
   const uint32_t lane = lane_id();
@@ -308,13 +319,13 @@ __device__ __forceinline__ void fc_oldwalk_level(const Dev& D, const FlowArgs& F
 
 __global__ __launch_bounds__(64) void k_fc_oldwalk_wide(Dev D, FlowArgs F) {
   const uint32_t h = F.h0 + blockIdx.y, q = blockIdx.x;
-  if (h >= fl_hend(D, F) || !fc_book(F, h) || q == 0 || q > F.hdr[h].nl) return;
+  if (h >= fl_hend(D, F) || !fc_lane(F, h) || q == 0 || q > F.hdr[h].nl) return;
   fc_oldwalk_level(D, F, h, q);
 }
 
 __global__ __launch_bounds__(1024) void k_fc_oldwalk_book(Dev D, FlowArgs F) {
   const uint32_t h = F.h0 + blockIdx.x;
-  if (h >= fl_hend(D, F) || !fc_book(F, h)) return;
+  if (h >= fl_hend(D, F) || !fc_lane(F, h)) return;
   for (uint32_t q = 1 + (threadIdx.x >> 6); q <= F.hdr[h].nl; q += blockDim.x / 64) fc_oldwalk_level(D, F, h, uni(q));
 }
 
@@ -431,7 +442,7 @@ __device__ __forceinline__ unsigned long long fc_del_rec_c(const FlowHdr& hd, co
   const uint32_t k = d.li;
   const uint32_t d0 = static_cast<uint32_t>(static_cast<unsigned long long>(LV[k].d0) / hd.g);
   const uint32_t q = (d.kind == FC_OLD ? d0 - d.oend : 0u - d.oend) + d.va - c;
-  const uint32_t hi = k | (d.ov << 7) | (1u << 30) | (sale ? 0x80000000u : 0u);
+  const uint32_t hi = (hd.ok == FL_OK_DEEP ? k | (d.ov << 14) : k | (d.ov << 7)) | (1u << 30) | (sale ? 0x80000000u : 0u);
   return (static_cast<unsigned long long>(hi) << 32) | q;
 }
 
@@ -459,7 +470,7 @@ __global__ __launch_bounds__(FC_PASS_T) void k_fc_pass(Dev D, BatchArgs B, FlowA
   __shared__ uint32_t cnt[FL_CAP], wc[FC_PASS_W][FL_CAP], cvol[FC_KEYS], wv[FC_PASS_W][FC_KEYS];
   __shared__ uint32_t bad_s, mw_s, sum_s;
   const uint32_t h = F.h0 + blockIdx.x, tid = threadIdx.x, w = tid >> 6;
-  if (h >= fl_hend(D, F) || !fc_book(F, h)) return;
+  if (h >= fl_hend(D, F) || !fc_lane(F, h)) return;
   const FlowHdr hd = F.hdr[h];
   FlowLvl* LV = F.lvl + h * FL_CAP;
   const uint32_t n = hd.end - hd.beg;
@@ -580,7 +591,7 @@ __device__ __forceinline__ bool fc_targeted_add(const FlowArgs& F, const FlowHdr
 __global__ __launch_bounds__(FL_TILE) void k_fc_pcnt(Dev D, BatchArgs B, FlowArgs F) {
   __shared__ uint32_t wc[FL_TILE_W][FL_CAP], tv[FC_KEYS];
   const uint32_t h = F.h0 + blockIdx.y, tid = threadIdx.x, w = tid >> 6;
-  if (h >= fl_hend(D, F) || !fc_book(F, h)) return;
+  if (h >= fl_hend(D, F) || !fc_lane(F, h)) return;
   const FlowHdr hd = F.hdr[h];
   const uint32_t n = hd.end - hd.beg, ntile = (n + FL_TILE - 1) / FL_TILE;
   for (uint32_t tl = blockIdx.x; tl < ntile; tl += gridDim.x) {
@@ -610,7 +621,7 @@ __global__ __launch_bounds__(FL_TILE) void k_fc_pcnt(Dev D, BatchArgs B, FlowArg
 // bases of the DEL-time arrays.
 __global__ __launch_bounds__(FL_CAP) void k_fc_pscan(Dev D, FlowArgs F) {
   const uint32_t h = F.h0 + blockIdx.x, k = threadIdx.x;
-  if (h >= fl_hend(D, F) || !fc_book(F, h)) return;
+  if (h >= fl_hend(D, F) || !fc_lane(F, h)) return;
   const FlowHdr& hd = F.hdr[h];
   FlowLvl* LV = F.lvl + h * FL_CAP;
   const uint32_t ntile = (hd.end - hd.beg + FL_TILE - 1) / FL_TILE;
@@ -637,7 +648,7 @@ __global__ __launch_bounds__(FL_CAP) void k_fc_pscan(Dev D, FlowArgs F) {
 __global__ __launch_bounds__(FL_TILE) void k_fc_prank(Dev D, BatchArgs B, FlowArgs F) {
   __shared__ uint32_t wc[FL_TILE_W][FL_CAP], wv[FL_TILE_W][FC_KEYS], vb[FC_KEYS];
   const uint32_t h = F.h0 + blockIdx.y, tid = threadIdx.x, w = tid >> 6;
-  if (h >= fl_hend(D, F) || !fc_book(F, h)) return;
+  if (h >= fl_hend(D, F) || !fc_lane(F, h)) return;
   const FlowHdr hd = F.hdr[h];
   const uint32_t n = hd.end - hd.beg, ntile = (n + FL_TILE - 1) / FL_TILE;
   const uint32_t* tc = F.tcnt + static_cast<size_t>(h) * F.maxt * FL_CAP;
@@ -692,12 +703,14 @@ __global__ __launch_bounds__(FL_TILE) void k_fc_prank(Dev D, BatchArgs B, FlowAr
 }
 
 // Windows: nb = arrived - rank of the target - 1; DEL times and volumes by rank.
-__global__ __launch_bounds__(256) void k_fc_pwin(Dev D, BatchArgs B, FlowArgs F) {
+// only_deep: the deep books alone (the tail's lane books take k_fc_pass)
+__global__ __launch_bounds__(256) void k_fc_pwin(Dev D, BatchArgs B, FlowArgs F, uint32_t only_deep) {
   __shared__ uint32_t sum_s, mw_s;
   const uint32_t h = F.h0 + blockIdx.y;
-  if (h >= fl_hend(D, F) || !fc_book(F, h)) return;
+  if (h >= fl_hend(D, F) || !fc_book(F, h) || (only_deep && F.hdr[h].ok != FL_OK_DEEP)) return;
   const FlowHdr hd = F.hdr[h];
-  FlowLvl* LV = F.lvl + h * FL_CAP;
+  FlowLvl* LV = fl_lvls(F, h);
+  const uint32_t vmax = hd.ok == FL_OK_DEEP ? FD_MAX_V : FC_MAX_V;
   if (threadIdx.x == 0) { sum_s = 0; mw_s = 0; }
   __syncthreads();
   uint32_t b0, b1, bad = 0, nbsum = 0;
@@ -711,7 +724,7 @@ __global__ __launch_bounds__(256) void k_fc_pwin(Dev D, BatchArgs B, FlowArgs F)
     nbsum += nb;
     atomicMax(&mw_s, nb + 1u);
     if (nb >= FC_NB_MAX) bad |= FC_BAD_RING;
-    if (d.ov >= FC_MAX_V) bad |= FC_BAD_UNIT;
+    if (d.ov >= vmax) bad |= FC_BAD_UNIT;
   }
   if (nbsum) atomicAdd(&sum_s, nbsum);
   __syncthreads();
@@ -723,16 +736,16 @@ __global__ __launch_bounds__(256) void k_fc_pwin(Dev D, BatchArgs B, FlowArgs F)
 }
 
 // The W32C DEL records (Q), tile-parallel; a book whose windows sum past the budget is declined.
-__global__ __launch_bounds__(256) void k_fc_precs(Dev D, BatchArgs B, FlowArgs F) {
+__global__ __launch_bounds__(256) void k_fc_precs(Dev D, BatchArgs B, FlowArgs F, uint32_t only_deep) {
   const uint32_t h = F.h0 + blockIdx.y;
-  if (h >= fl_hend(D, F) || !fc_book(F, h)) return;
+  if (h >= fl_hend(D, F) || !fc_book(F, h) || (only_deep && F.hdr[h].ok != FL_OK_DEEP)) return;
   const FlowHdr hd = F.hdr[h];
   const uint32_t n = hd.end - hd.beg;
   if (hd.nbsum > FC_NBSUM_MUL * n + FC_NBSUM_ADD) {
     if (blockIdx.x == 0 && threadIdx.x == 0) fc_decline(F, h, FC_BAD_RING);
     return;
   }
-  const FlowLvl* LV = F.lvl + h * FL_CAP;
+  const FlowLvl* LV = fl_lvls(F, h);
   uint32_t b0, b1;
   fc_slice(hd, blockIdx.x, gridDim.x, b0, b1);
   const uint32_t lane = lane_id();
@@ -775,7 +788,7 @@ __global__ __launch_bounds__(256) void k_fc_precs(Dev D, BatchArgs B, FlowArgs F
 // their old targets' marks and route them there (FlowHdr::ok = 0)
 __global__ __launch_bounds__(256) void k_fc_unmark(Dev D, BatchArgs B, FlowArgs F) {
   const uint32_t h = F.h0 + blockIdx.y;
-  if (h >= fl_hend(D, F) || F.hdr[h].ok != FL_OK_CANCEL || !F.hdr[h].fc_bad) return;
+  if (h >= fl_hend(D, F) || !fc_dels(F, h) || !F.hdr[h].fc_bad) return;
   const FlowHdr hd = F.hdr[h];
   uint32_t b0, b1;
   fc_slice(hd, blockIdx.x, gridDim.x, b0, b1);
@@ -788,7 +801,10 @@ __global__ __launch_bounds__(256) void k_fc_unmark(Dev D, BatchArgs B, FlowArgs 
 
 __global__ void k_fc_route(Dev D, FlowArgs F) {
   const uint32_t h = F.h0 + blockIdx.x * blockDim.x + threadIdx.x;
-  if (h < fl_hend(D, F) && F.hdr[h].ok == FL_OK_CANCEL && F.hdr[h].fc_bad) F.hdr[h].ok = 0;
+  if (h < fl_hend(D, F) && fc_dels(F, h) && F.hdr[h].fc_bad) {
+    F.hdr[h].ok = 0;  // (a declined deep book's price set was cleared by k_fd_decline)
+    F.hdr[h].deep = 0;
+  }
 }
 
 // ============================================================== reconstruction
@@ -859,7 +875,7 @@ __device__ __forceinline__ void fc_level_one(const Dev& D, const FlowArgs& F, ui
   const FlowHdr* hd = &F.hdr[h];
   const uint32_t lane = lane_id();
   const unsigned long long ltm = lt_mask();
-  FlowLvl* Lq = &F.lvl[h * FL_CAP + q];
+  FlowLvl* Lq = fl_lvls(F, h) + q;
   const uint32_t beg = uni(hd->beg);
   const uint32_t L = FL_TOUCH_MUL * beg;
   const unsigned long long g = static_cast<unsigned long long>(uni64(static_cast<int64_t>(hd->g)));
@@ -1212,19 +1228,19 @@ __device__ __forceinline__ void fc_level_blk(const Dev& D, const FlowArgs& F, ui
 // The head books' levels: a block per (book, level).
 __global__ __launch_bounds__(FC_LVB_T) void k_fc_level_blk(Dev D, FlowArgs F) {
   const uint32_t h = F.h0 + blockIdx.y, q = blockIdx.x;
-  if (h >= fl_hend(D, F) || !fc_book(F, h) || q == 0 || q > F.hdr[h].nl) return;
+  if (h >= fl_hend(D, F) || !fc_lane(F, h) || q == 0 || q > F.hdr[h].nl) return;
   fc_level_blk(D, F, h, q);
 }
 
 __global__ __launch_bounds__(64) void k_fc_level_wide(Dev D, FlowArgs F) {
   const uint32_t h = F.h0 + blockIdx.y, q = blockIdx.x;
-  if (h >= fl_hend(D, F) || !fc_book(F, h) || q == 0 || q > F.hdr[h].nl) return;
+  if (h >= fl_hend(D, F) || !fc_lane(F, h) || q == 0 || q > F.hdr[h].nl) return;
   fc_level_one(D, F, h, q);
 }
 
 __global__ __launch_bounds__(1024) void k_fc_level_book(Dev D, FlowArgs F) {
   const uint32_t h = F.h0 + blockIdx.x;
-  if (h >= fl_hend(D, F) || !fc_book(F, h)) return;
+  if (h >= fl_hend(D, F) || !fc_lane(F, h)) return;
   for (uint32_t q = 1 + (threadIdx.x >> 6); q <= F.hdr[h].nl; q += blockDim.x / 64) fc_level_one(D, F, h, uni(q));
 }
 
@@ -1238,8 +1254,8 @@ struct FcTouch {
 
 __device__ __forceinline__ FcTouch fc_touch(const FlowArgs& F, uint32_t h, uint32_t L, const Touch& x) {
   FcTouch T;
-  const uint32_t k = x.kr & 127u;
-  T.Lq = &F.lvl[h * FL_CAP + k];
+  const uint32_t k = F.hdr[h].ok == FL_OK_DEEP ? F.srt[L + x.pos].lvl : (x.kr & 127u);
+  T.Lq = fl_lvls(F, h) + k;
   T.V = fc_view(F, h, *T.Lq);
   T.c = F.srt[L + x.pos].coord;
   T.a = x.amt;
@@ -1359,7 +1375,6 @@ __global__ __launch_bounds__(256) void k_fc_events(Dev D, BatchArgs B, FlowArgs 
     gome_event* dst = B.arena + base + wb + (inc - cnt);
     const uint32_t beg = F.hdr[h].beg, sym = F.hdr[h].sym;
     const Prep tk = prep_at(B, beg + tk_jc(x));
-    const int64_t price = F.lvl[h * FL_CAP + (x.kr & 127u)].price;
     if (kind == TK_CANC) {  // DeleteOrder's MatchResult (engine.go:109-113)
       const FcDel d = F.fc_del[beg + tk_jc(x)];
       gome_event ev;
@@ -1395,6 +1410,7 @@ __global__ __launch_bounds__(256) void k_fc_events(Dev D, BatchArgs B, FlowArgs 
       tb -= y.amt;
     }
     const FcLvlView& V = T.V;
+    const int64_t price = T.Lq->price;
     const uint32_t fb = F.fbase[L + t];
     uint32_t k = 0;
     for (uint32_t m = T.first; m <= T.last; ++m) {
@@ -1452,7 +1468,7 @@ __device__ __forceinline__ Level fc_write_level(const Dev& D, const BatchArgs& B
   const uint32_t lane = lane_id();
   const unsigned long long ltm = lt_mask();
   const unsigned long long mask = D.idx_mask;
-  const FlowLvl f = F.lvl[h * FL_CAP + q];
+  const FlowLvl f = fl_lvls(F, h)[q];
   const FcLvlView V = fc_view(F, h, f);
   Level x{};
   x.price = f.price;
@@ -1545,8 +1561,12 @@ __device__ __forceinline__ Level fc_write_level(const Dev& D, const BatchArgs& B
   x.depth = f.dfin;
   x.nlive = f.nlive0 + S;
   uint32_t mem = 0;
-  if ((hd.amask[q >> 6] >> (q & 63)) & 1ull) mem |= M_SALE;
-  if ((hd.bmask[q >> 6] >> (q & 63)) & 1ull) mem |= M_BUY;
+  if (hd.ok == FL_OK_DEEP) {
+    mem = f.memf;
+  } else {
+    if ((hd.amask[q >> 6] >> (q & 63)) & 1ull) mem |= M_SALE;
+    if ((hd.bmask[q >> 6] >> (q & 63)) & 1ull) mem |= M_BUY;
+  }
   x.member = static_cast<uint8_t>(mem);
   if (x.nlive == 0) {
     x.hslot = x.tslot = 0;
@@ -1569,7 +1589,7 @@ __device__ __forceinline__ Level fc_write_level(const Dev& D, const BatchArgs& B
 
 __global__ __launch_bounds__(64) void k_fc_write_lv(Dev D, BatchArgs B, FlowArgs F) {
   const uint32_t h = F.h0 + blockIdx.y, q = blockIdx.x;
-  if (h >= fl_hend(D, F) || !fc_book(F, h)) return;
+  if (h >= fl_hend(D, F) || !fc_lane(F, h)) return;
   const FlowHdr hd = F.hdr[h];
   if (q == 0 || q > hd.nl) return;
   const Level x = fc_write_level(D, B, F, hd, h, q);
@@ -1582,7 +1602,7 @@ __global__ __launch_bounds__(128) void k_fc_fin(Dev D, FlowArgs F) {
   __shared__ uint32_t keep[FL_CAP];
   __shared__ uint32_t nout_s, base_s, cap_s;
   const uint32_t h = F.h0 + blockIdx.x;
-  if (h >= fl_hend(D, F) || !fc_book(F, h)) return;
+  if (h >= fl_hend(D, F) || !fc_lane(F, h)) return;
   const FlowHdr hd = F.hdr[h];
   for (uint32_t q = 1 + threadIdx.x; q <= hd.nl; q += blockDim.x) lv[q] = F.lvout[h * FL_CAP + q];
   __syncthreads();
@@ -1602,7 +1622,7 @@ __global__ __launch_bounds__(FL_WRITE_T) void k_fc_write_book(Dev D, BatchArgs B
   __shared__ uint32_t keep[FL_CAP];
   __shared__ uint32_t nout_s, base_s, cap_s;
   const uint32_t h = F.h0 + blockIdx.x;
-  if (h >= fl_hend(D, F) || !fc_book(F, h)) return;
+  if (h >= fl_hend(D, F) || !fc_lane(F, h)) return;
   const FlowHdr hd = F.hdr[h];
   const uint32_t w = threadIdx.x >> 6, nw = FL_WRITE_T / 64;
   for (uint32_t q = 1 + w; q <= hd.nl; q += nw) {

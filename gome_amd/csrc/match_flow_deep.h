@@ -28,6 +28,7 @@
 #include "device.h"
 #include "match_cold.h"
 #include "match_flow.h"
+#include "match_flow_cancel.h"
 #include "pipeline.h"
 #include "wave.h"
 
@@ -186,9 +187,9 @@ __device__ __forceinline__ void k_deep_prep_b_one(Dev D, BatchArgs B, FlowArgs F
   const uint32_t sym = B.ord[B.sidx[beg]].symbol_id;
   const Book bk = D.books[sym];
   if (tid == 0) {
-    // ADD-only for now: a segment with DELs keeps the legacy kernel
+    // (a segment with DELs takes the W32DC plan after the cancel prep)
     const uint64_t tiles = (static_cast<uint64_t>(FL_TOUCH_MUL) * (end - beg) + FL_TILE - 1) / FL_TILE;
-    bad = (P->d_bad || P->d_dels || (bk.pad & BOOK_QUIRK) || bk.n_lvl > DEEP_CAP - 2 || tiles > fd_tiles(F, ds)) ? 1u : 0u;
+    bad = (P->d_bad || (bk.pad & BOOK_QUIRK) || bk.n_lvl > DEEP_CAP - 2 || tiles > fd_tiles(F, ds)) ? 1u : 0u;
     ndist = P->d_ndist;
     nc = 0;
   }
@@ -297,6 +298,8 @@ __device__ __forceinline__ void k_deep_prep_b_one(Dev D, BatchArgs B, FlowArgs F
     x.g = g;
     x.deep = 1;
     x.dslot = ds;
+    x.ndel = P->d_dels;
+    x.dc = P->d_dels ? 1u : 0u;
     *hd = x;
   }
 }
@@ -424,6 +427,7 @@ __device__ __forceinline__ void k_deep_sort_scatter_one(Dev D, FlowArgs F, uint3
   if (!fd_deep(F, h)) return;
   const uint32_t nt = F.hdr[h].ntouch, L = FL_TOUCH_MUL * F.hdr[h].beg;
   const unsigned long long g = F.hdr[h].g;
+  const bool dc = F.hdr[h].dc != 0;
   const uint32_t ntile = (nt + FL_TILE - 1) / FL_TILE;
   const uint32_t* tc = fd_tcnt(F, F.hdr[h].dslot);
   for (uint32_t i = tid; i < FL_TILE_W * FL_CAP; i += FL_TILE) wc[i / FL_CAP][i % FL_CAP] = 0;
@@ -456,8 +460,8 @@ __device__ __forceinline__ void k_deep_sort_scatter_one(Dev D, FlowArgs F, uint3
       } else {
         const uint32_t t0 = static_cast<uint32_t>(a >> 32);  // the touch's log index
         SEnt e;
-        e.j = tk_j(x);
-        e.kind = (x.kr >> 7) & 1u;
+        e.j = dc ? tk_jc(x) : tk_j(x);
+        e.kind = tk_kind(x.kr, dc);
         e.amt = static_cast<int64_t>((a & 0xFFFFFFFFull) * g);  // plan units -> fixed point
         e.coord = 0;
         e.t = t0;
@@ -531,6 +535,7 @@ __device__ __forceinline__ void k_deep_level_one(Dev D, FlowArgs F, uint32_t slo
   FlowLvl* LV = fl_lvls(F, h);
   const SEnt* R = F.srt + L;
   const uint32_t lane = lane_id();
+  const bool dc = F.hdr[h].dc != 0;
   for (uint32_t i0 = blockIdx.x * 64u; i0 < nt; i0 += gridDim.x * 64u) {
     const uint32_t i = i0 + lane;
     const uint32_t lv = i < nt ? R[i].lvl : 0u;
@@ -539,7 +544,12 @@ __device__ __forceinline__ void k_deep_level_one(Dev D, FlowArgs F, uint32_t slo
       const uint32_t q = uni(rl(lv, static_cast<uint32_t>(__builtin_ctzll(hm))));
       const uint32_t e = uni(LV[q].pad1), b = uni(LV[q].base);  // (k_deep_runs)
       if (lane == 0) LV[q].cnt = e - b;
-      fl_level_one(D, F, h, q, b, e - b);
+      if (dc) {
+        __threadfence_block();  // (fc_level_one reads the count back)
+        fc_level_one(D, F, h, q);
+      } else {
+        fl_level_one(D, F, h, q, b, e - b);
+      }
     }
   }
 }
@@ -559,7 +569,7 @@ __device__ __forceinline__ void k_deep_claim_one(Dev D, BatchArgs B, FlowArgs F,
   __shared__ uint32_t part[DEEP_CLAIM_T];
   __shared__ uint32_t tot_s;
   const uint32_t h = fd_book(D, F, slot_i), tid = threadIdx.x;
-  if (!fd_deep(F, h)) return;
+  if (!fd_deep(F, h) || F.hdr[h].dc) return;  // (a book with DELs claims per level: fc_write_level)
   const FlowHdr hd = F.hdr[h];
   FlowLvl* LV = fl_lvls(F, h);
   const RsEnt* RS = F.rs + FL_TOUCH_MUL * hd.beg;
@@ -638,7 +648,7 @@ __device__ __forceinline__ void k_deep_write_lv_one(Dev D, BatchArgs B, FlowArgs
     }
     for (unsigned long long tm = __ballot(touched); tm; tm &= tm - 1) {
       const uint32_t qq = q0 + static_cast<uint32_t>(__builtin_ctzll(tm));
-      const Level x = fl_write_level(D, B, F, hd, h, qq, claim);
+      const Level x = hd.dc ? fc_write_level(D, B, F, hd, h, qq) : fl_write_level(D, B, F, hd, h, qq, claim);
       if (lane == 0) out[qq] = x;
     }
   }
@@ -709,6 +719,7 @@ __device__ __forceinline__ void k_deep_write_fin_one(Dev D, FlowArgs F, uint32_t
     atomicAdd(&ct[C_FLOW_BOOKS], 1ull);
     atomicAdd(&ct[C_FLOW_ORDERS], static_cast<unsigned long long>(hd.end - hd.beg));
     atomicAdd(&ct[C_FLOW_TOUCHES], static_cast<unsigned long long>(hd.ntouch));
+    if (hd.dc) atomicAdd(&ct[C_DEL], static_cast<unsigned long long>(hd.ndel));
     if (hd.dslot == 0) {  // the hottest book (k_flow_plan_head's work)
       atomicAdd(&ct[C_FLOW_HEAD_ORDERS], static_cast<unsigned long long>(hd.end - hd.beg));
       atomicAdd(&ct[C_FLOW_HEAD_TOUCHES], static_cast<unsigned long long>(hd.ntouch));
@@ -726,6 +737,170 @@ __device__ __forceinline__ void k_deep_write_fin_one(Dev D, FlowArgs F, uint32_t
 __global__ __launch_bounds__(DEEP_FIN_T) void k_deep_write_fin(Dev D, FlowArgs F) {
   for (uint32_t i = blockIdx.x; i < fd_nslots(F); i += gridDim.x) {
     k_deep_write_fin_one(D, F, i);
+    __syncthreads();
+  }
+}
+
+// ============================================================== deep books with DELs: cancel prep
+// The quantities k_fc_pass computes for a lane book with per-level LDS counters (every targeted
+// ADD's rank and arrival end, every DEL's count of its level's targets that arrived before it and
+// its side's ADD volume before it; match_flow_cancel.h), for a book with up to DEEP_CAP levels:
+// the segment's records sorted stably by level (the deep touch sort, on a key log written over
+// F.log before the plan needs it), then one wave per level walks its run in segment order.
+
+// Old targets' FIFO ranks and arrival ends: a wave per level that holds old targets.
+__device__ __forceinline__ void k_fd_oldwalk_one(Dev D, FlowArgs F, uint32_t slot_i) {
+  const uint32_t h = fd_book(D, F, slot_i);
+  if (h == NIL || !fc_deep(F, h)) return;
+  const uint32_t nl = F.hdr[h].nl;
+  const FlowLvl* LV = fl_lvls(F, h);
+  for (uint32_t q = 1 + blockIdx.x; q <= nl; q += gridDim.x)
+    if (uni(LV[q].c_old)) fc_oldwalk_level(D, F, h, q);
+}
+__global__ __launch_bounds__(64) void k_fd_oldwalk(Dev D, FlowArgs F) {
+  for (uint32_t i = blockIdx.y; i < fd_nslots(F); i += gridDim.y) k_fd_oldwalk_one(D, F, i);
+}
+
+// The key log: record i of the segment at its level (an admitted ADD's, or a DEL's target's;
+// level 0 for the rest), kr = i << 8 (no kind bits).  FlowHdr::ntouch = the segment's length
+// until the plan sets the touch count.
+__device__ __forceinline__ void k_fd_ckeys_one(Dev D, BatchArgs B, FlowArgs F, uint32_t slot_i) {
+  const uint32_t h = fd_book(D, F, slot_i);
+  if (h == NIL || !fc_deep(F, h)) return;
+  const FlowHdr& hd = F.hdr[h];
+  const uint32_t n = hd.end - hd.beg, L = FL_TOUCH_MUL * hd.beg;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const uint32_t b = hd.beg + i;
+    const unsigned long long r = F.ord8[hd.obase + i];  // (DEL records are still no-ops)
+    uint32_t lvl = static_cast<uint32_t>(r >> 32) & 0x3FFFu;
+    if (!r && prep_at(B, b).action == GOME_DEL) {
+      const FcDel d = F.fc_del[b];
+      if (d.kind != FC_NONE) lvl = d.li;
+    }
+    Touch x;
+    x.kr = i << 8;
+    x.pos = lvl;
+    x.amt = 0;
+    F.log[L + i] = x;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) F.hdr[h].ntouch = n;
+}
+__global__ __launch_bounds__(256) void k_fd_ckeys(Dev D, BatchArgs B, FlowArgs F) {
+  for (uint32_t i = blockIdx.y; i < fd_nslots(F); i += gridDim.y) k_fd_ckeys_one(D, B, F, i);
+}
+
+// One level's run R[b, e) of sorted keys, in segment order: running ADD volumes per side and the
+// count of targeted ADDs (from the level's old targets).
+__device__ __forceinline__ void fd_crank_level(const BatchArgs& B, const FlowArgs& F, const FlowHdr& hd, FlowLvl* LV,
+                                               const SEnt* R, uint32_t q, uint32_t b, uint32_t e) {
+  const uint32_t lane = lane_id();
+  int64_t sb = 0, sa = 0;
+  uint32_t tc = uni(LV[q].c_old);
+  for (uint32_t c0 = b; c0 < e; c0 += 64) {
+    const uint32_t i = c0 + lane;
+    const bool valid = i < e;
+    const uint32_t j = valid ? R[i].j : 0u, bs = hd.beg + j;
+    bool isadd = false, targ = false, isdel = false, sale = false;
+    uint32_t v = 0;
+    if (valid) {
+      const unsigned long long r = F.ord8[hd.obase + j];
+      if (r) {
+        isadd = true;
+        v = static_cast<uint32_t>(r);
+        sale = (r >> 63) != 0;
+        targ = F.fc_tg[bs] != 0;
+      } else {
+        isdel = true;  // (a DEL with a target: the only other records with a level)
+        sale = prep_at(B, bs).side == GOME_SALE;
+      }
+    }
+    const int64_t ab = (isadd && !sale) ? v : 0, aa = (isadd && sale) ? v : 0;
+    const uint32_t t1 = targ ? 1u : 0u;
+    const int64_t ib = wave_incl_scan(ab), ia = wave_incl_scan(aa);
+    const uint32_t it = wave_incl_scan_u32(t1);
+    const uint32_t before_t = tc + it - t1;
+    const uint32_t before_v = static_cast<uint32_t>(sale ? sa + ia - aa : sb + ib - ab);
+    if (targ) {  // (k_fc_pass: fc_put_va and the rank)
+      FcDel* d = &F.fc_del[F.fc_tg[bs] - 1u];
+      d->oend = before_v + v;
+      d->ov = v;
+      F.fc_rank[bs] = before_t;
+    }
+    if (isdel) {  // (arrived: k_fc_pwin turns it into the window)
+      F.fc_del[bs].nb = before_t;
+      F.fc_del[bs].va = before_v;
+    }
+    sb += rl64(ib, 63);
+    sa += rl64(ia, 63);
+    tc += rl(it, 63);
+  }
+  if (lane == 0) LV[q].ttot = tc;
+}
+
+__device__ __forceinline__ void k_fd_crank_one(Dev D, BatchArgs B, FlowArgs F, uint32_t slot_i) {
+  const uint32_t h = fd_book(D, F, slot_i);
+  if (h == NIL || !fc_deep(F, h)) return;
+  const FlowHdr& hd = F.hdr[h];
+  const uint32_t nt = hd.ntouch, L = FL_TOUCH_MUL * hd.beg;
+  FlowLvl* LV = fl_lvls(F, h);
+  const SEnt* R = F.srt + L;
+  const uint32_t lane = lane_id();
+  for (uint32_t i0 = blockIdx.x * 64u; i0 < nt; i0 += gridDim.x * 64u) {
+    const uint32_t i = i0 + lane;
+    const uint32_t lv = i < nt ? R[i].lvl : 0u;
+    const bool head = i < nt && lv != 0 && (i == 0 || R[i - 1].lvl != lv);
+    for (unsigned long long hm = __ballot(head); hm; hm &= hm - 1) {
+      const uint32_t q = uni(rl(lv, static_cast<uint32_t>(__builtin_ctzll(hm))));
+      fd_crank_level(B, F, hd, LV, R, q, uni(LV[q].base), uni(LV[q].pad1));  // (k_deep_runs)
+    }
+  }
+}
+__global__ __launch_bounds__(64) void k_fd_crank(Dev D, BatchArgs B, FlowArgs F) {
+  for (uint32_t i = blockIdx.y; i < fd_nslots(F); i += gridDim.y) k_fd_crank_one(D, B, F, i);
+}
+
+// Per level the first entry of the book's DEL-time array (an exclusive scan of the levels'
+// target counts; one block per book).
+__device__ __forceinline__ void k_fd_tbase_one(Dev D, FlowArgs F, uint32_t slot_i) {
+  __shared__ uint32_t part[DEEP_CLAIM_T];
+  const uint32_t h = fd_book(D, F, slot_i), tid = threadIdx.x;
+  if (h == NIL || !fc_deep(F, h)) return;
+  const uint32_t nl = F.hdr[h].nl;
+  FlowLvl* LV = fl_lvls(F, h);
+  const uint32_t per = (nl + DEEP_CLAIM_T - 1) / DEEP_CLAIM_T;
+  const uint32_t q0 = 1 + tid * per, q1 = min(nl + 1, q0 + per);
+  uint32_t sum = 0;
+  for (uint32_t q = q0; q < q1; ++q) sum += LV[q].ttot;
+  part[tid] = sum;
+  __syncthreads();
+  if (tid < 64) {
+    uint32_t v[DEEP_CLAIM_T / 64], acc = 0;
+#pragma unroll
+    for (uint32_t u = 0; u < DEEP_CLAIM_T / 64; ++u) { v[u] = part[tid * (DEEP_CLAIM_T / 64) + u]; acc += v[u]; }
+    uint32_t run = wave_incl_scan_u32(acc) - acc;
+#pragma unroll
+    for (uint32_t u = 0; u < DEEP_CLAIM_T / 64; ++u) { part[tid * (DEEP_CLAIM_T / 64) + u] = run; run += v[u]; }
+  }
+  __syncthreads();
+  uint32_t off = part[tid];
+  for (uint32_t q = q0; q < q1; ++q) {
+    LV[q].tbase = off;
+    off += LV[q].ttot;
+  }
+}
+__global__ __launch_bounds__(DEEP_CLAIM_T) void k_fd_tbase(Dev D, FlowArgs F) {
+  for (uint32_t i = blockIdx.x; i < fd_nslots(F); i += gridDim.x) {
+    k_fd_tbase_one(D, F, i);
+    __syncthreads();
+  }
+}
+
+// A deep book the cancel prep declined goes to the legacy kernels: its price set back to empty
+// (before k_fc_route takes it off the deep path).
+__global__ __launch_bounds__(256) void k_fd_decline(Dev D, FlowArgs F) {
+  for (uint32_t i = blockIdx.x; i < fd_nslots(F); i += gridDim.x) {
+    const uint32_t h = fd_book(D, F, i);
+    if (h != NIL && F.hdr[h].ok == FL_OK_DEEP && F.hdr[h].dc && F.hdr[h].fc_bad) fd_clear(F, F.hdr[h].dslot);
     __syncthreads();
   }
 }

@@ -97,19 +97,23 @@ def test_bench_config5_exact_4mi_batches():
 
 @pytest.mark.gpu
 def test_bench_config5c_exact():
-    """bench.py --workload config5c (config 5's 4-dp grid with config 4's 50% DELs and 10%
-    aggressive ADDs): the hot books' segments hold thousands of distinct prices and DELs, every
-    event and the books' levels and FIFOs against the C oracle."""
+    """bench.py --workload config5c exactly (config 5's 4-dp grid with config 4's 50% DELs and
+    10% aggressive ADDs), three 4 Mi-order batches as the bench runs them: the
+    hot books' segments hold ~10k distinct prices and DELs, so they take the deep plan with DELs
+    (W32DC, FlowHdr::dc); every event and the books' levels and FIFOs against the C oracle."""
     import bench
-    n = 1 << 21
+    n = 1 << 22
     gen, _, _ = bench.make_stream("config5c", 0, 1, 42)
     eng = Engine(max_symbols=1_000_000, max_batch=n, max_nodes=3 * n + (1 << 20), max_levels=(64 << 20) + 2 * n)
     orc = Oracle(1_000_000)
-    for i in range(2):
+    for i in range(3):
         b = gen(n).copy()
         eng.submit(b)
         _cmp(eng.drain(), orc.submit(b), f"config5c batch {i}")
-        assert eng.stats()["n_del"] > n // 4
+        st = eng.stats()
+        assert st["n_del"] > n // 4 and st["n_flow_cancels"] > n // 20
+        fl = eng.debug_flow_books()
+        assert (fl["kind"][:8] == 3).all() and (fl["decline"] == 0).all()  # the head: deep books with DELs
     g = wl.NativeStream(1_000_000, 1.0, seed=42, price_decimals=4)
     syms = [int(g.zipf.rank_to_id[r]) for r in range(8)]
     syms += np.random.default_rng(5).choice(1_000_000, 100, replace=False).tolist()

@@ -64,9 +64,12 @@ LOOP_OFS = int(os.environ.get("GOME_PLAN_OFS", "0"))  # 4-byte words after the 2
 SYNC_SMEM = os.environ.get("GOME_PLAN_SYNC_SMEM", "0") == "1"
 PF_DIST = int(os.environ.get("GOME_PLAN_PF", "0"))  # L2 prefetch distance in bytes (0: off);
 # k_flow_prep pads ord8 by FL_ORD8_PAD records, which must cover it
+PF_DEEP = int(os.environ.get("GOME_PLAN_PFD", "0"))  # the same for the deep plans (GenD, GenDC)
 
 
 class Gen:
+    pf = PF_DIST
+
     def __init__(self, width: int):
         self.w = width
         self.out: list[str] = []
@@ -530,9 +533,9 @@ class Gen:
         e(f"s_load_dwordx16 s[{other}:{other + 15}], {ADDR}, 0x0")   # prefetch the next half
         if SYNC_SMEM:
             e("s_waitcnt lgkmcnt(0)")
-        if PF_DIST:  # warm L2 further ahead with a vector load (never waited for in the loop)
+        if self.pf:  # warm L2 further ahead with a vector load (never waited for in the loop)
             e("s_mov_b64 exec, 1")
-            e(f"global_load_dword %[vpf], %[vzero], {ADDR} offset:{PF_DIST}")
+            e(f"global_load_dword %[vpf], %[vzero], {ADDR} offset:{self.pf}")
         self.decode(j)
         e(f"s_cbranch_scc1 {self.lab(f'S{j}')}")
 
@@ -565,9 +568,9 @@ class Gen:
         e(".p2align 8")
         for _ in range(LOOP_OFS):
             e("s_nop 0")
-        if PF_DIST:
+        if self.pf:
             e("s_mov_b64 exec, 1")
-            for off in range(64, PF_DIST, 64):
+            for off in range(64, self.pf, 64):
                 e(f"global_load_dword %[vpf], %[vzero], {ADDR} offset:{off}")
         for i in range(NS):
             if i % HG == 0:
@@ -723,6 +726,8 @@ BM = {"B": DEEP_BM, "A": DEEP_BM + DEEP_CAP // 8}
 
 
 class GenD(Gen):
+    pf = PF_DEEP
+
     def __init__(self):
         super().__init__(32)
 
@@ -938,6 +943,10 @@ class GenD(Gen):
         self.next_top("B")
         e(f"s_load_dwordx16 s[44:59], {ADDR}, 0x0")
         e(".p2align 8")
+        if self.pf:
+            e("s_mov_b64 exec, 1")
+            for off in range(64, self.pf, 64):
+                e(f"global_load_dword %[vpf], %[vzero], {ADDR} offset:{off}")
         for i in range(NS):
             if i % HG == 0:
                 self.head(i)

@@ -1185,7 +1185,7 @@ __device__ __forceinline__ void fl_plan_deep(const Dev& D, const FlowArgs& F, ui
   const unsigned long long ob = reinterpret_cast<unsigned long long>(F.ord8 + uni(hd->obase));
   const unsigned long long logp = reinterpret_cast<unsigned long long>(F.log + FL_TOUCH_MUL * beg);
   const uint32_t vl16 = lane * 16u;
-  uint32_t voff;
+  uint32_t voff, vpf;
   const uint32_t vzero = 0;
   // the plan's group summaries (lane i bit j: group 32i + j of 32 levels holds a nonzero slot of
   // that side), from the bitmaps fl_deep_load built
@@ -1199,14 +1199,14 @@ __device__ __forceinline__ void fl_plan_deep(const Dev& D, const FlowArgs& F, ui
   if (uni(hd->dc)) {  // DELs in the segment (gen_plan_asm.py W32DC)
     asm volatile(FL_PLAN_ASM32DC
                  : [lk] "+v"(lg.lk), [la] "+v"(lg.la), [lb] "+v"(lg.lb), [nacc] "+s"(lg.nacc), [lpos] "+s"(lg.lpos),
-                   [voff] "=&v"(voff)
+                   [voff] "=&v"(voff), [vpf] "=&v"(vpf)
                  : [ob] "s"(ob), [nh] "s"(nh), [logp] "s"(logp), [lcap] "s"(lg.lcap), [vl16] "v"(vl16),
                    [vzero] "v"(vzero), [sb] "v"(sb), [sa] "v"(sa)
                  : FL_PLAN_CLOBBERS, FL_PLAN_CLOBBERS_D, "scc", "vcc", "memory");
   } else {
     asm volatile(FL_PLAN_ASM32D
                  : [lk] "+v"(lg.lk), [la] "+v"(lg.la), [lb] "+v"(lg.lb), [nacc] "+s"(lg.nacc), [lpos] "+s"(lg.lpos),
-                   [voff] "=&v"(voff)
+                   [voff] "=&v"(voff), [vpf] "=&v"(vpf)
                  : [ob] "s"(ob), [nh] "s"(nh), [logp] "s"(logp), [lcap] "s"(lg.lcap), [vl16] "v"(vl16),
                    [vzero] "v"(vzero), [sb] "v"(sb), [sa] "v"(sa)
                  : FL_PLAN_CLOBBERS, FL_PLAN_CLOBBERS_D, "scc", "vcc", "memory");

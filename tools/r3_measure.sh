@@ -56,6 +56,21 @@ for P in $PARTS; do
         done
       done
     done ;;
+  abdeep)  # the same for the deep workloads
+    for R in 1 2; do
+      for V in "" $(cd gome_amd && ls libgome_*.so 2>/dev/null); do
+        N=${V:-libgome.so}
+        for W in config5 config5c; do
+          GOME_LIB=${V:+$PWD/gome_amd/$V} timeout -k 10 300 python3 -u bench.py --workload $W --steps 8 --warmup 2 \
+            --e2e-steps 0 --no-cpu-baseline > $OUT/ab_${W}_${N%.so}_$R.jsonl 2> $OUT/ab_${W}_${N%.so}_$R.log || exit 10
+          echo "$W $N $R $(tail -1 $OUT/ab_${W}_${N%.so}_$R.jsonl | grep -o '"ms_per_step": [0-9.]*'; tail -1 $OUT/ab_${W}_${N%.so}_$R.jsonl | grep -o '"ns_per_order": [0-9.]*')"
+        done
+      done
+    done ;;
+  c5e2e)  # config 5 with a longer pipelined end-to-end leg (pools sized for 40 + 16 steps)
+    timeout -k 10 500 python3 -u bench.py --workload config5 --steps 40 --warmup 2 --e2e-steps 16 --no-cpu-baseline \
+      --pool-nodes 80000000 --pool-levels 160000000 > $OUT/c5e2e.jsonl 2> $OUT/c5e2e.log || exit 9
+    tail -1 $OUT/c5e2e.jsonl | cut -c100-260 ;;
   c3)
     timeout -k 10 300 python3 -u bench.py --steps 20 --warmup 5 --no-cpu-baseline > $OUT/c3.jsonl 2> $OUT/c3.log || exit 6
     tail -1 $OUT/c3.jsonl | cut -c100-300 ;;

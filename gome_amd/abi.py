@@ -20,6 +20,8 @@ HEADERS = [HEADER, os.path.join(os.path.dirname(_HERE), "include", "gome", "gome
 
 GOME_FLAG_LEGACY_HOT = 1  # gome_config.flags: hot books on the legacy FIFO kernel
 GOME_FLAG_NO_HEADROOM = 2  # gome_config.flags: no pool-headroom check before a submit
+GOME_FLAG_CHAINS_ALWAYS = 4  # gome_config.flags: enqueue the deep / cancel chains on every batch
+GOME_FLAG_CHAINS_NEVER = 8  # gome_config.flags: never (deep books and books with DELs: legacy / cold)
 GOME_ORD_ADM_HOST, GOME_ORD_ADMITTED = 1, 2  # gome_order.flags: host-resolved admission (ABI 4)
 GOME_MAX_INFLIGHT = 2
 
@@ -61,7 +63,7 @@ class Stats(C.Structure):
         ("idx_tombstones", C.c_uint64), ("n_flow_cancels", C.c_uint64), ("ms_cold", C.c_double),
         ("lvl_used", C.c_uint64), ("n_dup_oid", C.c_uint64), ("n_flow_tail_fills", C.c_uint64),
         ("ms_phase", C.c_double * 16),
-        ("ms_host_enqueue", C.c_double)]
+        ("ms_host_enqueue", C.c_double), ("chains", C.c_uint32), ("chains_wanted", C.c_uint32)]
 
     def as_dict(self):
         d = {n: getattr(self, n) for n, _ in self._fields_}

@@ -83,7 +83,9 @@ enum {
   C_FLOW_CANCELS,                                         // cancels applied on the flow path
   C_DUP,                                                  // ADDs rejected as duplicate oids (Q7)
   C_FLOW_TAIL_FILLS,                                      // fills of the tail's flow books
-  C_NCTR = 23
+  C_WANT_DEEP, C_WANT_CANC,                               // flow candidates that asked for the deep /
+                                                          // cancel chain (enqueued or not)
+  C_NCTR = 25
 };
 
 // Level blocks (a book's sorted level array) come in power-of-two capacities 16 << c.  A

@@ -188,6 +188,7 @@ struct Slot {
   hipEvent_t ph[GOME_NPHASE][2]{};  // GOME_PH_* phase brackets (ph_on: recorded this batch)
   bool ph_on[GOME_NPHASE]{};
   double ms_enqueue = 0;  // host wall time of enqueue()
+  uint32_t chains = 0;    // the flow chains (FL_CH_*) the batch enqueued
 };
 
 struct Flight {
@@ -313,6 +314,14 @@ struct gome_engine {
   gome_status load_books(size_t nb, const uint32_t* bsym, const uint32_t* bnlv, const gome_level* lv,
                          const gome_node* nd, size_t nn);
   bool used = false;  // a batch was submitted or books were loaded (gome_load_books needs a fresh engine)
+  // finished batches in a row whose flow candidates asked for no deep / cancel chain
+  uint32_t deep_quiet = 0, canc_quiet = 0;
+  uint32_t pick_chains() const {
+    if (cfg.flags & GOME_FLAG_CHAINS_NEVER) return 0u;
+    const bool all = (cfg.flags & GOME_FLAG_CHAINS_ALWAYS) != 0;
+    return ((all || deep_quiet < GOME_CHAIN_QUIET) ? FL_CH_DEEP : 0u) |
+           ((all || canc_quiet < GOME_CHAIN_QUIET) ? FL_CH_CANCEL : 0u);
+  }
   gome_status check_capacity(unsigned long long adds, unsigned long long inflight_n);
   gome_status check_capacity_host(const gome_order* o, size_t n, unsigned long long inflight_n);
   uint32_t take_slot() {
@@ -644,6 +653,11 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   // FH: the head's prep; FH0: the hottest book (plan + reconstruction on the flow stream,
   // the batch's critical path); FH1: the other head books (on the tail's stream, done long
   // before the hottest); FT: the tail.  tb: each range's slice of toff.
+  // the deep / cancel chains only while recent batches needed them (GOME_CHAIN_QUIET)
+  const uint32_t ch = pick_chains();
+  const bool c_deep = (ch & FL_CH_DEEP) != 0, c_canc = (ch & FL_CH_CANCEL) != 0;
+  S.chains = ch;
+  F.chains = ch;
   FlowArgs FH = F, FH0 = F, FH1 = F, FT = F;
   FH.h0 = 0; FH.h1 = FL_HEAD; FH.tb = 0;
   FH0.h0 = 0; FH0.h1 = 1; FH0.tb = 0; FH0.mb = 0;
@@ -667,9 +681,11 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   // the head's prep gathers through the sort permutation (prep_at): it starts right after
   // segmentation, beside k_prep
   // deep books: slots, price sets and prep scratch of both ranges
-  HIPCHK(hipMemsetAsync(F.dslot_h, 0xFF, 4ull * F.dslots, s));
-  HIPCHK(hipMemsetAsync(F.dslot_n, 0, 4, s));
-  HIPCHK(hipMemsetAsync(F.dscr, 0, sizeof(FlPrepScr) * F.dslots, s));
+  if (c_deep) {
+    HIPCHK(hipMemsetAsync(F.dslot_h, 0xFF, 4ull * F.dslots, s));
+    HIPCHK(hipMemsetAsync(F.dslot_n, 0, 4, s));
+    HIPCHK(hipMemsetAsync(F.dscr, 0, sizeof(FlPrepScr) * F.dslots, s));
+  }
   HIPCHK(hipEventRecord(seg_done, s));
   HIPCHK(hipStreamWaitEvent(flow_stream, seg_done, 0));
   HIPCHK(hipMemsetAsync(F.pscr, 0, sizeof(FlPrepScr) * FL_HEAD, flow_stream));
@@ -684,7 +700,7 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
     k_deep_prep_b<<<ns, FL_PREP_T, DEEP_CAP * 8, st>>>(D, B, R);
     k_deep_prep_c<<<dim3(px, ns), FL_PREP_T, 0, st>>>(D, B, R);
   };
-  deep_prep(FH, FL_PG, flow_stream);
+  if (c_deep) deep_prep(FH, FL_PG, flow_stream);
   // deep books: the two-pass stable sort of a log by level (touches, or the cancel prep's keys)
   // and each level's run
   auto deep_sort = [&](const FlowArgs& R, uint32_t tiles, hipStream_t st) {
@@ -705,11 +721,13 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
     k_fc_hash_count<<<dim3(px, nb), 256, 0, st>>>(D, B, R);
     k_fc_hash_first<<<dim3(px, nb), 256, 0, st>>>(D, B, R);
     k_fc_resolve<<<dim3(px, nb), 256, 0, st>>>(D, B, R);
-    k_fd_oldwalk<<<dim3(DEEP_GRID, ns), 64, 0, st>>>(D, R);
-    k_fd_ckeys<<<dim3(wide ? 256 : 16, ns), 256, 0, st>>>(D, B, R);
-    deep_sort(R, wide ? FL_SORT_GRID : 32, st);
-    k_fd_crank<<<dim3(DEEP_GRID, ns), 64, 0, st>>>(D, B, R);
-    k_fd_tbase<<<ns, DEEP_CLAIM_T, 0, st>>>(D, R);
+    if (c_deep) {  // deep books with DELs (W32DC)
+      k_fd_oldwalk<<<dim3(DEEP_GRID, ns), 64, 0, st>>>(D, R);
+      k_fd_ckeys<<<dim3(wide ? 256 : 16, ns), 256, 0, st>>>(D, B, R);
+      deep_sort(R, wide ? FL_SORT_GRID : 32, st);
+      k_fd_crank<<<dim3(DEEP_GRID, ns), 64, 0, st>>>(D, B, R);
+      k_fd_tbase<<<ns, DEEP_CLAIM_T, 0, st>>>(D, R);
+    }
     if (wide) {  // the head: tile-parallel ranks, windows, layout and records
       k_fc_oldwalk_wide<<<dim3(FL_CAP, nb), 64, 0, st>>>(D, R);
       k_fc_pcnt<<<dim3(FL_SORT_GRID, nb), FL_TILE, 0, st>>>(D, B, R);
@@ -723,16 +741,23 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
       k_fc_pwin<<<dim3(px, nb), 256, 0, st>>>(D, B, R, 1u);
       k_fc_precs<<<dim3(px, nb), 256, 0, st>>>(D, B, R, 1u);
     }
-    k_fd_decline<<<ns, 256, 0, st>>>(D, R);
+    if (c_deep) k_fd_decline<<<ns, 256, 0, st>>>(D, R);
     k_fc_unmark<<<dim3(px, nb), 256, 0, st>>>(D, B, R);
     k_fc_route<<<ceil_div(nb, 256), 256, 0, st>>>(D, R);
   };
-  cancel_prep(FH, nh_head, FL_PG, true, flow_stream);
+  if (c_canc) cancel_prep(FH, nh_head, FL_PG, true, flow_stream);
   HIPCHK(mark(GOME_PH_HEAD_PREP, 1, flow_stream));
   HIPCHK(hipEventRecord(prep_h, flow_stream));
   HIPCHK(hipEventRecord(S.evf0, flow_stream));
   k_flow_plan_head<<<1, 256, plan_lds, flow_stream>>>(D, FH0);
   HIPCHK(hipEventRecord(S.evf1, flow_stream));
+  // the other head books' plans need only the head's prep: each takes a whole CU, so they go
+  // first, before the tail's prep and plans spread their waves over every CU
+  HIPCHK(hipStreamWaitEvent(hot_stream, prep_h, 0));
+  if (nh_near) {
+    HIPCHK(mark(GOME_PH_NEAR, 0, hot_stream));
+    k_flow_plan_near<<<nh_near, 256, plan_lds, hot_stream>>>(D, FH1);
+  }
   // ---- admission markers (k_adm, launched above on the flow stream)
   HIPCHK(hipStreamWaitEvent(s, adm_done, 0));
   // k_prep gathers the same records as the head's prep: let the head's prep (the critical
@@ -772,13 +797,13 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
     if (split) {  // the deep books' level sort (other books than the ones below) beside it
       HIPCHK(hipEventRecord(dp_fork, st));
       HIPCHK(hipStreamWaitEvent(cs, dp_fork, 0));
-      deep_sort_level(R, FL_SORT_GRID, cs);
+      if (c_deep) deep_sort_level(R, FL_SORT_GRID, cs);
       HIPCHK(hipEventRecord(dl_done, cs));  // (a deep book with DELs: k_fc_count / events wait)
     }
     k_flow_sort_cnt<<<dim3(FL_SORT_GRID, nb), FL_TILE, 0, st>>>(D, R);
     k_flow_sort_scan<<<nb, FL_CAP, 0, st>>>(D, R);
     k_flow_sort_scatter<<<dim3(FL_SORT_GRID, nb), FL_TILE, 0, st>>>(D, R);
-    if (!split) deep_sort_level(R, FL_SORT_GRID, st);
+    if (!split && c_deep) deep_sort_level(R, FL_SORT_GRID, st);
     k_flow_level_wide<<<dim3(FL_CAP, nb), FL_LVB_T, 0, st>>>(D, R);
     toff(R, false, st);
     if (split) {
@@ -788,16 +813,17 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
     if (!fused) k_flow_count<<<1024, 256, 0, cs>>>(D, B, R);
     if (split) {  // (the publish scan waits for the count, the batch's end for the deep writes)
       HIPCHK(hipEventRecord(cnt_done, cs));
-      deep_write(R, cs);  // (after the count, which reads neither the claims nor the writes)
+      if (c_deep) deep_write(R, cs);  // (after the count, which reads neither the claims nor the writes)
       HIPCHK(hipEventRecord(dw_done, cs));
     }
     k_flow_write_lv_blk<<<dim3(FL_CAP, nb), FL_LVB_T, 0, st>>>(D, B, R);
     k_flow_write_fin<<<nb, 128, 0, st>>>(D, R);
-    if (!split) deep_write(R, st);
+    if (!split && c_deep) deep_write(R, st);
     return GOME_OK;
   };
   // books with DELs (match_flow_cancel.h); their events go to the arena
   auto head_recon_c = [&](const FlowArgs& R, const FlowArgs& Rc, uint32_t nb, hipStream_t st, bool split) -> gome_status {
+    if (!c_canc) return GOME_OK;
     k_fc_level_blk<<<dim3(FL_CAP, nb), FC_LVB_T, 0, st>>>(D, R);
     if (split) HIPCHK(hipStreamWaitEvent(st, dl_done, 0));  // (the deep books' level pass ran on cs)
     toff(Rc, true, st);
@@ -818,8 +844,8 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   if (nh_tail) {
     HIPCHK(mark(GOME_PH_TAIL_PREP, 0, s));
     k_flow_prep<<<nh_tail, FL_PREP_T, 0, s>>>(D, B, FT);
-    deep_prep(FT, 8, s);
-    cancel_prep(FT, nh_tail, 1, false, s);
+    if (c_deep) deep_prep(FT, 8, s);
+    if (c_canc) cancel_prep(FT, nh_tail, 1, false, s);
     HIPCHK(mark(GOME_PH_TAIL_PREP, 1, s));
   }
   HIPCHK(hipEventRecord(prep_t, s));
@@ -830,16 +856,16 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   if (nh_tail) {  // the tail's plans and reconstruction
     HIPCHK(mark(GOME_PH_TAIL_PLAN, 0, s));
     k_flow_plan_tail<<<nh_tail, 64, 0, s>>>(D, FT);
-    k_flow_plan_tail_c<<<nh_tail, 64, 0, s>>>(D, FT);
+    if (c_canc) k_flow_plan_tail_c<<<nh_tail, 64, 0, s>>>(D, FT);
     // (its blocks walk the tail's deep slots: at most DEEP_GRID_T whole-CU blocks)
-    k_flow_plan_tail_d<<<std::min<uint32_t>(nh_tail, DEEP_GRID_T), 256, FL_DEEP_LDS, s>>>(D, FT);
+    if (c_deep) k_flow_plan_tail_d<<<std::min<uint32_t>(nh_tail, DEEP_GRID_T), 256, FL_DEEP_LDS, s>>>(D, FT);
     HIPCHK(mark(GOME_PH_TAIL_PLAN, 1, s));
     HIPCHK(mark(GOME_PH_TAIL_SORT, 0, s));
     k_flow_sort<<<nh_tail, FL_SORT_T, 0, s>>>(D, FT);
     HIPCHK(mark(GOME_PH_TAIL_SORT, 1, s));
     HIPCHK(mark(GOME_PH_TAIL_LEVEL, 0, s));
     k_flow_level<<<nh_tail, FL_LEVEL_T, 0, s>>>(D, FT);
-    deep_sort_level(FT, 32, s);
+    if (c_deep) deep_sort_level(FT, 32, s);
     HIPCHK(mark(GOME_PH_TAIL_LEVEL, 1, s));
     HIPCHK(mark(GOME_PH_TAIL_COUNT, 0, s));
     toff(FT, false, s);
@@ -850,19 +876,18 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
     k_flow_write_events<<<nh_tail + ceil_div(tail_grid * FL_EV_T, FL_WRITE_T), FL_WRITE_T, 0, s>>>(D, B, FT, nh_tail);
     HIPCHK(mark(GOME_PH_TAIL_WRITE, 1, s));
     HIPCHK(mark(GOME_PH_TAIL_EVENTS, 0, s));
-    deep_write(FT, s);
-    k_fc_level_book<<<nh_tail, 1024, 0, s>>>(D, FT);
-    toff(FTc, true, s);
-    k_fc_count<<<1024, 256, 0, s>>>(D, B, FTc);
-    k_fc_write_book<<<nh_tail, FL_WRITE_T, 0, s>>>(D, B, FTc);
-    k_fc_events<<<1024, 256, 0, s>>>(D, B, FTc);
+    if (c_deep) deep_write(FT, s);
+    if (c_canc) {
+      k_fc_level_book<<<nh_tail, 1024, 0, s>>>(D, FT);
+      toff(FTc, true, s);
+      k_fc_count<<<1024, 256, 0, s>>>(D, B, FTc);
+      k_fc_write_book<<<nh_tail, FL_WRITE_T, 0, s>>>(D, B, FTc);
+      k_fc_events<<<1024, 256, 0, s>>>(D, B, FTc);
+    }
     HIPCHK(mark(GOME_PH_TAIL_EVENTS, 1, s));
   }
-  HIPCHK(hipStreamWaitEvent(hot_stream, fork, 0));
-  HIPCHK(hipStreamWaitEvent(hot_stream, prep_h, 0));
+  HIPCHK(hipStreamWaitEvent(hot_stream, fork, 0));  // (their reconstruction reads k_prep's records)
   if (nh_near) {
-    HIPCHK(mark(GOME_PH_NEAR, 0, hot_stream));
-    k_flow_plan_near<<<nh_near, 256, plan_lds, hot_stream>>>(D, FH1);
     if (head_recon(FH1, nh_near, hot_stream, hot_stream, true) != GOME_OK) return GOME_E_DEVICE;
     if (head_recon_c(FH1, FH1c, nh_near, hot_stream, false) != GOME_OK) return GOME_E_DEVICE;
     k_flow_events_fused<<<1024, FL_EV_T, 0, hot_stream>>>(D, B, FH1);
@@ -978,6 +1003,11 @@ gome_status gome_engine::finish(uint32_t sl, uint32_t n) {
     stats.ms_phase[k] = ms;
   }
   stats.ms_host_enqueue = S.ms_enqueue;
+  const bool want_deep = st.ctr[C_WANT_DEEP] != 0, want_canc = st.ctr[C_WANT_CANC] != 0;
+  deep_quiet = want_deep ? 0u : std::min<uint32_t>(deep_quiet + 1u, GOME_CHAIN_QUIET);
+  canc_quiet = want_canc ? 0u : std::min<uint32_t>(canc_quiet + 1u, GOME_CHAIN_QUIET);
+  stats.chains = S.chains;
+  stats.chains_wanted = (want_deep ? FL_CH_DEEP : 0u) | (want_canc ? FL_CH_CANCEL : 0u);
   if (const uint64_t nd = std::min<uint64_t>(st.ctr[C_DUP], n)) {
     dup_idx.resize(nd);
     HIPCHK(hipMemcpy(dup_idx.data(), S.d_dup, nd * sizeof(uint32_t), hipMemcpyDeviceToHost));

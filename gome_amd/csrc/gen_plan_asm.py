@@ -1072,6 +1072,234 @@ class GenDC(GenD):
         self.slow.append([f"{stale}:", "s_bfm_b64 exec, 1, s81", f"v_xor_b32 v{vs}, s79, v{vs}", f"s_branch {start}"])
 
 
+# ---- W32DV: the deep plan with the depths in VGPRs --------------------------
+# A clean book's bids all lie below its asks, so one depth word per level suffices (its side is
+# where it lies relative to the cached tops): level k's word is lane k & 63 of v[VB + (k >> 6)],
+# NVR registers, NVL = 64 * NVR levels (the ask sentinel is level NVL - 1, the bid sentinel level
+# 0).  The same invariant as the lane plans (a word is 0 unless its level rests behind the cached
+# top of its side).  Words are read and written through the GPR index mode (s_set_gpr_idx_on:
+# one SALU instruction, no memory round trip, no lgkmcnt wait behind the record stream's scalar
+# loads); the staging count moves from M0 (which the index mode overwrites) to SGPR MC.  One
+# summary VGPR: lane i bit j = register 32i + j holds a nonzero word (set by every rest, cleared
+# by the promotion that takes a register's last word; a DEL that empties a word leaves it set and
+# the promotion clears it when it finds the register empty).  The promotion after the top empties
+# is: one summary lane read, one register copy, one compare across its lanes, one lane read.  The
+# words come from and go back to a compact LDS array (word k at byte 4k), the cached tops are
+# handed in and out as operands.
+VB, NVR = 64, 192
+NVL = 64 * NVR
+MC = "s83"
+VLB, VAM, VTR, VSM = 36, 37, 39, 42    # lane * 4 (LDS base); amount; register copy; summary
+CLOBBERS_DV = [f"v{i}" for i in (VLB, VAM, VTR, VSM)] + [f"v{i}" for i in range(VB, VB + NVR)]
+
+
+class GenDV(GenD):
+    def logd(self, kr: str, a: str, lvl: str):
+        """(v_writelane takes its lane from M0: an SGPR lane select beside an SGPR source breaks
+        gfx9's one-SGPR constant bus limit.)"""
+        e = self.e
+        e(f"s_mov_b32 M0LANE, {MC}")
+        e(f"v_writelane_b32 %[lk], {kr}, M0LANE")
+        e(f"v_writelane_b32 %[la], {a}, M0LANE")
+        e(f"v_writelane_b32 %[lb], {lvl}, M0LANE")
+        e(f"s_add_u32 {MC}, {MC}, 1")
+
+    def word_add(self, lvl: str, amt: str):
+        """Word lvl += amt (the amount may be 0); exec is left narrowed."""
+        e = self.e
+        e(f"s_lshr_b32 {T0}, {lvl}, 6")
+        e(f"s_and_b32 s79, {lvl}, 63")
+        e("s_lshl_b64 exec, 1, s79")
+        e(f"v_mov_b32 v{VAM}, {amt}")
+        e(f"s_set_gpr_idx_on {T0}, gpr_idx(SRC0,DST)")
+        e(f"v_add_u32 v{VB}, v{VB}, v{VAM}")
+        e("s_set_gpr_idx_off")
+
+    def word_set(self, lvl: str, val: str):
+        e = self.e
+        e(f"s_lshr_b32 {T0}, {lvl}, 6")
+        e(f"s_and_b32 s79, {lvl}, 63")
+        e("s_lshl_b64 exec, 1, s79")
+        e(f"v_mov_b32 v{VAM}, {val}")
+        e(f"s_set_gpr_idx_on {T0}, gpr_idx(DST)")
+        e(f"v_mov_b32 v{VB}, v{VAM}")
+        e("s_set_gpr_idx_off")
+
+    def next_top(self, sd: str):
+        """After the cached top of side sd emptied: asks, the lowest nonzero word above BA; bids,
+        the highest below BB (the sentinels are nonzero words).  T0 = the candidate level c; the
+        first register at or beyond c's (R) whose summary bit is set is G; its nonzero words beyond
+        c give the level.  (G == R with none beyond c: search on from the next register; G != R with
+        none at all: a stale bit, cleared, and the search restarts.)"""
+        e = self.e
+        top, topd = (BA, BAD) if sd == "A" else (BB, BBD)
+        asks = sd == "A"
+        start, more, cont, nxt = self.fresh("NT"), self.fresh("NM"), self.fresh("NC"), self.fresh("NX")
+        G, W, MK, LN, R = O[0], O[2], O[3], "s81", "s79"
+        MS = "s[94:95]"
+        if asks:
+            e(f"s_add_u32 {T0}, {BA}, 1")
+        else:
+            e(f"s_sub_u32 {T0}, {BB}, 1")
+        e(f"{start}:")
+        e(f"s_lshr_b32 {R}, {T0}, 6")                        # c's register
+        e(f"s_lshr_b32 {LN}, {T0}, 11")                      # its summary lane
+        e(f"v_readlane_b32 {W}, v{VSM}, {LN}")
+        if asks:
+            e(f"s_lshl_b32 {MK}, -1, {R}")                   # registers >= R (bit R & 31)
+        else:
+            e(f"s_lshl_b32 {MK}, -2, {R}")
+            e(f"s_not_b32 {MK}, {MK}")                       # registers <= R
+        e(f"s_and_b32 {W}, {W}, {MK}")
+        e(f"s_cbranch_scc0 {more}")
+        blk = [f"{more}:", "s_mov_b64 exec, -1", f"v_cmp_ne_u32_e64 {M}, 0, v{VSM}"]
+        if asks:   # summary lanes above LN
+            blk += [f"s_mov_b64 {MS}, -1", f"s_add_u32 {LN}, {LN}, 1", f"s_lshl_b64 {MS}, {MS}, {LN}",
+                    f"s_and_b64 {M}, {M}, {MS}", f"s_ff1_i32_b64 {LN}, {M}"]
+        else:      # below LN
+            blk += [f"s_bfm_b64 {MS}, {LN}, 0", f"s_and_b64 {M}, {M}, {MS}",
+                    f"s_flbit_i32_b64 {LN}, {M}", f"s_sub_u32 {LN}, 63, {LN}"]
+        blk += [f"v_readlane_b32 {W}, v{VSM}, {LN}", f"s_branch {cont}"]
+        self.slow.append(blk)
+        e(f"{cont}:")
+        if asks:
+            e(f"s_ff1_i32_b32 {G}, {W}")
+        else:
+            e(f"s_flbit_i32_b32 {G}, {W}")
+            e(f"s_sub_u32 {G}, 31, {G}")
+        e(f"s_lshl_b32 {LN}, {LN}, 5")
+        e(f"s_add_u32 {G}, {G}, {LN}")                      # the register
+        e("s_mov_b64 exec, -1")
+        e(f"s_set_gpr_idx_on {G}, gpr_idx(SRC0)")
+        e(f"v_mov_b32 v{VTR}, v{VB}")
+        e("s_set_gpr_idx_off")
+        e(f"v_cmp_ne_u32_e64 {M}, 0, v{VTR}")
+        if asks:   # lanes >= c & 63 when G == R
+            e(f"s_lshl_b64 {MS}, -1, {T0}")
+        else:      # lanes <= c & 63
+            e(f"s_lshl_b64 {MS}, -2, {T0}")
+            e(f"s_not_b64 {MS}, {MS}")
+        e(f"s_cmp_eq_u32 {G}, {R}")
+        e(f"s_cselect_b64 {MS}, {MS}, -1")
+        e(f"s_and_b64 {MS}, {MS}, {M}")
+        e(f"s_cbranch_scc0 {nxt}")
+        stale = self.fresh("NS")
+        blk = [f"{nxt}:", f"s_cmp_eq_u32 {G}, {R}", f"s_cbranch_scc0 {stale}"]
+        if asks:   # on from the next register
+            blk += [f"s_add_u32 {T0}, {R}, 1", f"s_lshl_b32 {T0}, {T0}, 6"]
+        else:      # (R > 0: the bid sentinel is word 0 of register 0)
+            blk += [f"s_lshl_b32 {T0}, {R}, 6", f"s_sub_u32 {T0}, {T0}, 1"]
+        blk += [f"s_branch {start}",
+                f"{stale}:", f"s_lshl_b32 {W}, 1, {G}", f"s_lshr_b32 {LN}, {G}, 5", f"s_lshl_b64 exec, 1, {LN}",
+                f"v_xor_b32 v{VSM}, {W}, v{VSM}", f"s_branch {start}"]
+        self.slow.append(blk)
+        if asks:
+            e(f"s_ff1_i32_b64 {MK}, {MS}")
+        else:
+            e(f"s_flbit_i32_b64 {MK}, {MS}")
+            e(f"s_sub_u32 {MK}, 63, {MK}")
+        e(f"v_readlane_b32 {topd[0]}, v{VTR}, {MK}")
+        e(f"s_lshl_b32 {top}, {G}, 6")
+        e(f"s_add_u32 {top}, {top}, {MK}")
+        e(f"s_lshl_b64 exec, 1, {MK}")
+        e(f"s_set_gpr_idx_on {G}, gpr_idx(DST)")
+        e(f"v_mov_b32 v{VB}, 0")                            # the word := 0 (a cached top)
+        e("s_set_gpr_idx_off")
+        e(f"s_bcnt1_i32_b64 {W}, {M}")
+        e(f"s_cmp_eq_u32 {W}, 1")
+        e(f"s_cselect_b32 {W}, 1, 0")
+        e(f"s_lshl_b32 {W}, {W}, {G}")                      # the register emptied: its bit
+        e(f"s_lshr_b32 {LN}, {G}, 5")
+        e(f"s_lshl_b64 exec, 1, {LN}")
+        e(f"v_xor_b32 v{VSM}, {W}, v{VSM}")
+
+    def rest(self, side: str, T):
+        """As GenD.rest, the amount added to word L and its register's summary bit set."""
+        e = self.e
+        buy = side == "B"
+        top, topd = (BB, BBD) if buy else (BA, BAD)
+        ge, gt = ("ge", "gt") if buy else ("le", "lt")
+        e(f"s_cmp_{ge}_u32 {LI}, {top}")
+        self.csel(X, T, 0)
+        self.csel(A, 0, T)
+        e(f"s_cmp_{gt}_u32 {LI}, {top}")
+        self.csel(A, topd, A)
+        e(f"s_cselect_b32 {L}, {top}, {LI}")
+        self.csel(topd, 0, topd)
+        e(f"s_{'max' if buy else 'min'}_u32 {top}, {top}, {LI}")
+        self.add(topd, topd, X)
+        self.word_add(L, A[0])
+        # word L is nonzero now iff A > 0 (A == 0: L is the cached top, whose word stays 0)
+        e(f"s_min_u32 s79, {A[0]}, 1")
+        e(f"s_lshl_b32 s79, s79, {T0}")                     # T0 = L >> 6: bit (L >> 6) & 31
+        e(f"s_lshr_b32 s81, {T0}, 5")
+        e("s_lshl_b64 exec, 1, s81")
+        e(f"v_or_b32 v{VSM}, s79, v{VSM}")
+        e(f"s_or_b32 {K}, {JJS}, 0x80")
+        self.logd(K, T[0], LI)
+
+    def full(self, side: str, T, i: int):
+        sv = self.out
+        self.out = []
+        super().full(side, T, i)
+        body = self.out
+        self.out = sv
+        # the sell side's "never crosses" limit is the ask sentinel's level
+        self.out.extend(x.replace(f", {DEEP_CAP - 1}", f", {NVL - 1}") if x.startswith("s_cselect_b32") else x
+                        for x in body)
+
+    def write(self, k: str, v, sd: str):
+        self.word_set(k, v[0])
+
+    def build(self) -> list[str]:
+        e = self.e
+        done = self.lab("DONE")
+        e("s_waitcnt vmcnt(0)")
+        e(f"s_mov_b64 {ADDR}, %[ob]")
+        e(f"s_add_u32 {HC}, %[nh], 1")
+        e(f"s_mov_b32 {JJS}, 0xffffff00")
+        e("s_mov_b32 m0, %[nacc]")
+        e("s_mov_b64 exec, -1")
+        e(f"v_mbcnt_lo_u32_b32 v{VLB}, -1, 0")
+        e(f"v_mbcnt_hi_u32_b32 v{VLB}, -1, v{VLB}")
+        e(f"v_lshlrev_b32 v{VLB}, 2, v{VLB}")
+        for r in range(NVR):                                   # the words from the compact array
+            e(f"ds_read_b32 v{VB + r}, v{VLB} offset:{256 * r}")
+        e(f"v_mov_b32 v{VSM}, %[sv]")
+        e(f"s_mov_b32 {BA}, %[ba]")
+        e(f"s_mov_b32 {BB}, %[bb]")
+        e(f"s_mov_b32 {BAD[0]}, %[bad]")
+        e(f"s_mov_b32 {BBD[0]}, %[bbd]")
+        e(f"s_mov_b32 {ZERO}, 0")
+        e("s_waitcnt lgkmcnt(0)")
+        e(f"s_load_dwordx16 s[44:59], {ADDR}, 0x0")
+        e(".p2align 8")
+        for i in range(NS):
+            if i % HG == 0:
+                self.head(i)
+            self.slot(i)
+        for blk in self.slow:
+            for line in blk:
+                e(line)
+        for fl, back in self.flushes:
+            self.emit_flush(fl, back)
+        e(f"{done}:")
+        e("s_waitcnt vmcnt(0) lgkmcnt(0)")
+        self.write(BA, BAD, "A")
+        self.write(BB, BBD, "B")
+        e("s_mov_b64 exec, -1")
+        for r in range(NVR):
+            e(f"ds_write_b32 v{VLB}, v{VB + r} offset:{256 * r}")
+        e("s_waitcnt lgkmcnt(0)")
+        e(f"s_mov_b32 %[oba], {BA}")
+        e(f"s_mov_b32 %[obb], {BB}")
+        e("s_mov_b32 %[nacc], m0")
+        # the staging count lives in MC (the index mode overwrites M0); M0 is loaded from it for
+        # the lane writes only
+        import re
+        return [re.sub(r"\bm0\b", MC, x).replace("M0LANE", "m0") for x in self.out]
+
+
 ALIGN = int(os.environ.get("GOME_PLAN_ALIGN", "0"))   # log2 byte alignment of branch targets
 
 
@@ -1092,7 +1320,8 @@ def main():
     out = sys.argv[1] if len(sys.argv) > 1 else os.path.join(here, "flow_plan_asm.inc")
     with open(out, "w") as f:
         f.write("// Generated by gen_plan_asm.py — do not edit.\n")
-        for w, g in ((64, Gen(64)), (32, Gen(32)), ("32C", GenC()), ("32D", GenD()), ("32DC", GenDC())):
+        for w, g in ((64, Gen(64)), (32, Gen(32)), ("32C", GenC()), ("32D", GenD()), ("32DC", GenDC()),
+                     ("32DV", GenDV())):
             f.write(f"#define FL_PLAN_ASM{w} \\\n")
             for line in aligned(g.build()):
                 f.write(f'  "{line}\\n\\t" \\\n')
@@ -1100,6 +1329,8 @@ def main():
         f.write("#define FL_PLAN_CLOBBERS " + ", ".join(f'"{c}"' for c in CLOBBERS) + "\n")
         f.write("#define FL_PLAN_CLOBBERS_C " + ", ".join(f'"{c}"' for c in CLOBBERS_C) + "\n")
         f.write("#define FL_PLAN_CLOBBERS_D " + ", ".join(f'"{c}"' for c in CLOBBERS_D) + "\n")
+        f.write("#define FL_PLAN_CLOBBERS_DV " + ", ".join(f'"{c}"' for c in CLOBBERS_DV) + "\n")
+        f.write(f"#define FL_DEEP_NVL {NVL}\n")
         f.write(f"#define FL_DEEP_CAP {DEEP_CAP}\n")
         f.write(f"#define FL_DEEP_BM {DEEP_BM}\n")
         f.write(f"#define FL_DEEP_LDS {DEEP_BM + DEEP_BM_BYTES}\n")

@@ -130,11 +130,13 @@ struct FlowHdr {
   uint32_t dslot;      // its deep slot (head: = h; tail: handed out by k_flow_prep)
   uint32_t nbsum;      // books with DELs: the DEL windows' total (the cancel prep's C loops)
   uint32_t dc;         // a deep book whose segment holds DELs (the W32DC plan)
-  uint32_t pad3[3];
+  uint32_t dv_ba;      // W32DV: the best ask after the plan (asks lie at or above it)
+  uint32_t pad3[2];
 };
 // FlowHdr::ok: 0 declined, FL_OK_ADD an ADD-only flow book, FL_OK_CANCEL a book with DELs,
 // FL_OK_DEEP an ADD-only head book with more levels than the lane plans hold (match_flow_deep.h)
 constexpr uint32_t FL_OK_ADD = 1, FL_OK_CANCEL = 2, FL_OK_DEEP = 3;
+constexpr uint32_t FL_CH_DEEP = 1, FL_CH_CANCEL = 2;  // FlowArgs::chains
 constexpr uint32_t DEEP_CAP = 16384;     // level slots of a deep book (0 and DEEP_CAP - 1: sentinels)
 constexpr uint32_t DEEP_HASH = 1u << 16; // price-set slots of a deep book (global memory)
 constexpr uint32_t DEEP_GRID_T = 128;    // blocks (per dimension) of the tail's deep launches
@@ -198,6 +200,9 @@ struct FlowArgs {
   uint32_t maxt;       // tiles per head book (log capacity / FL_TILE)
   struct FlPrepScr* pscr;  // head prep scratch [FL_HEAD] (k_flow_prep_a/b/c)
   uint32_t enabled;
+  // the chains this batch enqueued (FL_CH_*): a candidate that needs one that is not there is
+  // declined to the legacy / cold kernels (and counted in C_WANT_*, which re-enables it)
+  uint32_t chains;
   // the candidates [h0, min(h1, nhot)) this launch covers (head and tail run on their own
   // streams), and the range's offset in toff
   uint32_t h0, h1, tb;
@@ -388,7 +393,9 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep(Dev D, BatchArgs B, Flo
       hd->ok = 0;
       // too many levels for the lanes: a deep book if a deep slot is free (match_flow_deep.h)
       uint32_t slot = NIL;
-      if (!bad && bk.n_lvl <= DEEP_CAP - 2) {
+      const bool want = !bad && bk.n_lvl <= DEEP_CAP - 2;
+      if (want) atomicAdd(&D.st->ctr[C_WANT_DEEP], 1ull);
+      if (want && (F.chains & FL_CH_DEEP)) {
         const uint32_t t = atomicAdd(F.dslot_n, 1u);
         if (t < F.dslots - FL_HEAD) slot = FL_HEAD + t;
       }
@@ -480,7 +487,8 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep(Dev D, BatchArgs B, Flo
   }
   if (tid == 0) {
     FlowHdr x{};
-    x.ok = dels ? FL_OK_CANCEL : FL_OK_ADD;
+    if (dels) atomicAdd(&D.st->ctr[C_WANT_CANC], 1ull);
+    x.ok = dels ? ((F.chains & FL_CH_CANCEL) ? FL_OK_CANCEL : 0u) : FL_OK_ADD;
     x.nl = n;
     x.sym = sym;
     x.beg = beg;
@@ -703,6 +711,8 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep_b(Dev D, BatchArgs B, F
     const bool many = P->many || bk.n_lvl > FL_MAX;
     // more levels than lanes: the deep plan's candidate (match_flow_deep.h re-checks the rest)
     deepc = (!base_bad && many && bk.n_lvl <= DEEP_CAP - 2) ? 1u : 0u;
+    if (deepc) atomicAdd(&D.st->ctr[C_WANT_DEEP], 1ull);
+    if (!(F.chains & FL_CH_DEEP)) deepc = 0;
     bad = (base_bad || many) ? 1u : 0u;
   }
   __syncthreads();
@@ -751,6 +761,8 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep_b(Dev D, BatchArgs B, F
     if (tid == 0) {
       hd->ok = 0;
       hd->deep = (!bad && ndist <= DEEP_CAP - 2) ? 1u : 0u;
+      if (hd->deep) atomicAdd(&D.st->ctr[C_WANT_DEEP], 1ull);
+      if (!(F.chains & FL_CH_DEEP)) hd->deep = 0;
       hd->dslot = h;
       if (hd->deep) F.dslot_h[h] = h;
     }
@@ -808,7 +820,8 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep_b(Dev D, BatchArgs B, F
     F.ord8[obase + (end - beg) + tid] = fl_rec(false, 0, 0, false, end - beg + tid, w32);
   if (tid == 0) {
     FlowHdr x{};
-    x.ok = dels ? FL_OK_CANCEL : FL_OK_ADD;
+    if (dels) atomicAdd(&D.st->ctr[C_WANT_CANC], 1ull);
+    x.ok = dels ? ((F.chains & FL_CH_CANCEL) ? FL_OK_CANCEL : 0u) : FL_OK_ADD;
     x.nl = n;
     x.sym = sym;
     x.beg = beg;
@@ -945,6 +958,21 @@ struct FlLog {
 #include "flow_plan_asm.inc"
 static_assert(FL_DEEP_CAP == DEEP_CAP, "deep plan generated for another DEEP_CAP");
 static_assert(FL_DEEP_BM == DEEP_CAP * 8 && FL_DEEP_LDS <= 160 * 1024, "deep plan LDS layout");
+// W32DV's LDS: the words (word k at 4k), then FL_DV_HDR words: the cached tops and their depths
+// (ask, bid, ask depth, bid depth) and the summary (FL_DEEP_NVL / 64 / 32 lanes)
+constexpr uint32_t FL_DV_HDR = 4 + FL_DEEP_NVL / 2048;
+static_assert((FL_DEEP_NVL + FL_DV_HDR) * 4 <= FL_DEEP_LDS && FL_DEEP_NVL <= DEEP_CAP, "VGPR deep plan's word array");
+#ifndef GOME_DEEP_LDS_ONLY
+constexpr bool FL_DEEP_VGPR = true;   // W32DV (depths in VGPRs) for ADD-only deep books that fit
+#else
+constexpr bool FL_DEEP_VGPR = false;  // (variant build: every deep book on the LDS plan)
+#endif
+
+// Does deep book h take the VGPR plan (gen_plan_asm.py W32DV)?  ADD-only, levels and the two
+// sentinels within its FL_DEEP_NVL words.
+__device__ __forceinline__ bool fl_deep_vgpr(const FlowHdr& hd) {
+  return FL_DEEP_VGPR && !hd.dc && hd.nl + 2 <= FL_DEEP_NVL;
+}
 
 
 
@@ -967,6 +995,36 @@ __device__ __forceinline__ void fl_deep_load(const FlowArgs& F, uint32_t h) {
   const FlowHdr& hd = F.hdr[h];
   const FlowLvl* LV = fl_lvls(F, h);
   const unsigned long long g = hd.g;
+  if (fl_deep_vgpr(hd)) {  // W32DV: one word per level (a clean book's bids lie below its asks)
+    uint32_t* hw = dep + FL_DEEP_NVL;
+    if (threadIdx.x < FL_DV_HDR) hw[threadIdx.x] = threadIdx.x == 0 ? FL_DEEP_NVL - 1 : 0u;
+    __syncthreads();
+    for (uint32_t k = threadIdx.x; k < FL_DEEP_NVL; k += blockDim.x) {
+      uint32_t w = (k == 0 || k == FL_DEEP_NVL - 1) ? 1u : 0u;  // the sentinels
+      if (k >= 1 && k <= hd.nl) {
+        const FlowLvl& f = LV[k];
+        if (f.mem0 & (M_SALE | M_BUY)) w = static_cast<uint32_t>(static_cast<unsigned long long>(f.d0) / g);
+        if (w && (f.mem0 & M_SALE)) atomicMin(&hw[0], k);  // the best ask / bid: the cached tops
+        if (w && (f.mem0 & M_BUY)) atomicMax(&hw[1], k);
+      }
+      dep[k] = w;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {  // the tops' depths leave their words (the plan's invariant)
+      hw[2] = dep[hw[0]];
+      hw[3] = dep[hw[1]];
+      dep[hw[0]] = 0;
+      dep[hw[1]] = 0;
+    }
+    __syncthreads();
+    // the summary: bit r % 32 of word r / 32 = register r (words 64r .. 64r + 63) is nonzero
+    for (uint32_t r = threadIdx.x; r < FL_DEEP_NVL / 64; r += blockDim.x) {
+      uint32_t nz = 0;
+      for (uint32_t i = 0; i < 64; ++i) nz |= dep[64 * r + i];
+      if (nz) atomicOr(&hw[4 + r / 32], 1u << (r % 32));
+    }
+    return;
+  }
   for (uint32_t k = threadIdx.x; k < DEEP_CAP; k += blockDim.x) {
     uint32_t a = 0, b = 0;
     if (k >= 1 && k <= hd.nl) {
@@ -999,6 +1057,15 @@ __device__ __forceinline__ void fl_deep_store(const FlowArgs& F, uint32_t h) {
   const FlowHdr& hd = F.hdr[h];
   FlowLvl* LV = fl_lvls(F, h);
   const unsigned long long g = hd.g;
+  if (fl_deep_vgpr(hd)) {  // W32DV: asks lie at or above the final best ask
+    const uint32_t ba = hd.dv_ba;
+    for (uint32_t k = 1 + threadIdx.x; k <= hd.nl; k += blockDim.x) {
+      const uint32_t w = dep[k];
+      LV[k].dfin = static_cast<int64_t>(static_cast<unsigned long long>(w) * g);
+      LV[k].memf = w ? (k >= ba ? M_SALE : M_BUY) : 0u;
+    }
+    return;
+  }
   for (uint32_t k = 1 + threadIdx.x; k <= hd.nl; k += blockDim.x) {
     const uint32_t b = dep[2 * k], a = dep[2 * k + 1];
     LV[k].dfin = static_cast<int64_t>(static_cast<unsigned long long>(a + b) * g);  // (one side is 0)
@@ -1196,7 +1263,21 @@ __device__ __forceinline__ void fl_plan_deep(const Dev& D, const FlowArgs& F, ui
       sb |= (bm[32 * lane + j] != 0 ? 1u : 0u) << j;
       sa |= (bm[DEEP_CAP / 32 + 32 * lane + j] != 0 ? 1u : 0u) << j;
     }
-  if (uni(hd->dc)) {  // DELs in the segment (gen_plan_asm.py W32DC)
+  if (fl_deep_vgpr(*hd)) {  // W32DV: the words from LDS into VGPRs inside the asm, tops as operands
+    // the cached tops, their depths and the summary, from fl_deep_load
+    const uint32_t* hw = reinterpret_cast<const uint32_t*>(fl_ring) + FL_DEEP_NVL;
+    const uint32_t ba = uni(hw[0]), bb = uni(hw[1]), bad = uni(hw[2]), bbd = uni(hw[3]);
+    const uint32_t sv = lane < FL_DEEP_NVL / 2048 ? hw[4 + lane] : 0u;
+    uint32_t oba, obb;
+    asm volatile(FL_PLAN_ASM32DV
+                 : [lk] "+v"(lg.lk), [la] "+v"(lg.la), [lb] "+v"(lg.lb), [nacc] "+s"(lg.nacc), [lpos] "+s"(lg.lpos),
+                   [voff] "=&v"(voff), [vpf] "=&v"(vpf), [oba] "=s"(oba), [obb] "=s"(obb)
+                 : [ob] "s"(ob), [nh] "s"(nh), [logp] "s"(logp), [lcap] "s"(lg.lcap), [vl16] "v"(vl16),
+                   [vzero] "v"(vzero), [sv] "v"(sv), [ba] "s"(ba), [bb] "s"(bb), [bad] "s"(bad), [bbd] "s"(bbd)
+                 : FL_PLAN_CLOBBERS, FL_PLAN_CLOBBERS_DV, "scc", "vcc", "memory");
+    if (lane == 0) F.hdr[h].dv_ba = oba;  // (fl_deep_store: asks lie at or above it)
+    (void)obb;
+  } else if (uni(hd->dc)) {  // DELs in the segment (gen_plan_asm.py W32DC)
     asm volatile(FL_PLAN_ASM32DC
                  : [lk] "+v"(lg.lk), [la] "+v"(lg.la), [lb] "+v"(lg.lb), [nacc] "+s"(lg.nacc), [lpos] "+s"(lg.lpos),
                    [voff] "=&v"(voff), [vpf] "=&v"(vpf)
@@ -2079,8 +2160,8 @@ __device__ __forceinline__ Level fl_write_level(const Dev& D, const BatchArgs& B
   if (hd.ok == FL_OK_DEEP) {
     mem = f.memf;
   } else {
-    if ((hd.amask[q >> 6] >> (q & 63)) & 1ull) mem |= M_SALE;
-    if ((hd.bmask[q >> 6] >> (q & 63)) & 1ull) mem |= M_BUY;
+    if (((q < 64 ? hd.amask[0] : hd.amask[1]) >> (q & 63)) & 1ull) mem |= M_SALE;
+    if (((q < 64 ? hd.bmask[0] : hd.bmask[1]) >> (q & 63)) & 1ull) mem |= M_BUY;
   }
   x.member = static_cast<uint8_t>(mem);
   if (x.nlive == 0) {
@@ -2296,8 +2377,8 @@ __global__ __launch_bounds__(FL_LVB_T) void k_flow_write_lv_blk(Dev D, BatchArgs
   x.depth = f.dfin;
   x.nlive = f.nlive0 + S;
   uint32_t mem = 0;
-  if ((hd.amask[q >> 6] >> (q & 63)) & 1ull) mem |= M_SALE;
-  if ((hd.bmask[q >> 6] >> (q & 63)) & 1ull) mem |= M_BUY;
+  if (((q < 64 ? hd.amask[0] : hd.amask[1]) >> (q & 63)) & 1ull) mem |= M_SALE;
+  if (((q < 64 ? hd.bmask[0] : hd.bmask[1]) >> (q & 63)) & 1ull) mem |= M_BUY;
   x.member = static_cast<uint8_t>(mem);
   if (x.nlive == 0) {
     x.hslot = x.tslot = 0;

@@ -1564,8 +1564,8 @@ __device__ __forceinline__ Level fc_write_level(const Dev& D, const BatchArgs& B
   if (hd.ok == FL_OK_DEEP) {
     mem = f.memf;
   } else {
-    if ((hd.amask[q >> 6] >> (q & 63)) & 1ull) mem |= M_SALE;
-    if ((hd.bmask[q >> 6] >> (q & 63)) & 1ull) mem |= M_BUY;
+    if (((q < 64 ? hd.amask[0] : hd.amask[1]) >> (q & 63)) & 1ull) mem |= M_SALE;
+    if (((q < 64 ? hd.bmask[0] : hd.bmask[1]) >> (q & 63)) & 1ull) mem |= M_BUY;
   }
   x.member = static_cast<uint8_t>(mem);
   if (x.nlive == 0) {

@@ -78,7 +78,10 @@ __global__ __launch_bounds__(SCAN_T) void k_scan_down(const uint32_t* in, uint32
 }
 
 // ============================================================== radix sort by symbol
-constexpr int RS_T = 256, RS_IPT = 8, RS_TILE = RS_T * RS_IPT, RS_MAXBITS = 11;
+#ifndef GOME_RS_MAXBITS
+#define GOME_RS_MAXBITS 11
+#endif
+constexpr int RS_T = 256, RS_IPT = 8, RS_TILE = RS_T * RS_IPT, RS_MAXBITS = GOME_RS_MAXBITS;
 constexpr int RS_WAVE_ITEMS = RS_TILE / 4;  // contiguous items per wave
 
 template <bool FROM_ORD>

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define GOME_ABI_VERSION 5u
+#define GOME_ABI_VERSION 6u
 
 /* ---- status codes (replace the reference's swallowed errors / panics,
  *      rabbitmq.go:44-49,70-72,120-122; nodelink.go:132,142,157) ---------- */
@@ -145,6 +145,17 @@ typedef struct gome_node {
  * and the handle stays usable (size max_nodes >= the resting makers + GOME_MAX_INFLIGHT
  * batches).  This flag turns the check off (pools sized tightly on purpose). */
 #define GOME_FLAG_NO_HEADROOM 2u
+/* The flow path's deep-book and cancel chains (match_flow_deep.h, match_flow_cancel.h: ~70
+ * kernel launches per batch) are enqueued only while recent batches needed them: a chain is
+ * dropped after GOME_CHAIN_QUIET finished batches in which no flow candidate asked for it, and
+ * comes back on the next submit after one did (a host submit whose records hold a DEL enqueues
+ * the cancel chain at once).  A candidate that asks for a chain the batch did not enqueue is
+ * applied by the legacy / cold kernels instead (same results, slower for that batch).
+ * GOME_FLAG_CHAINS_ALWAYS enqueues both chains on every batch; GOME_FLAG_CHAINS_NEVER never
+ * (every deep book and every book with DELs on the legacy / cold kernels; A/B and tests). */
+#define GOME_FLAG_CHAINS_ALWAYS 4u
+#define GOME_FLAG_CHAINS_NEVER 8u
+#define GOME_CHAIN_QUIET 4u
 
 typedef struct gome_config {
   uint32_t accuracy;       /* gomengine.accuracy (config.yaml.example:23-24), default 8 */
@@ -215,6 +226,10 @@ typedef struct gome_stats {
   double ms_host_enqueue;                     /* host wall time the batch's launches took
                                                  (ABI >= 5): the GPU cannot finish before
                                                  the last one is issued                  */
+  uint32_t chains;                            /* flow chains this batch enqueued (ABI >= 6):
+                                                 1 = deep books, 2 = books with DELs     */
+  uint32_t chains_wanted;                     /* chains its candidates asked for (same bits;
+                                                 wanted and not enqueued: legacy / cold)  */
 } gome_stats;
 
 typedef struct gome_engine gome_engine;

@@ -1,0 +1,47 @@
+#!/bin/bash
+# Round-3 session-2 GPU check: new tests first, then the whole GPU suite, then bench lines and a
+# config-2 trace.  usage: bash tools/r3b.sh <tag> [parts...]  (parts: new suite c2 c3 c4 c5 c5c c2t)
+set -o pipefail
+TAG=${1:-r3b}; shift
+PARTS=${@:-new suite c2 c3}
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+OUT=gpurun_out/$TAG
+mkdir -p $OUT
+for P in $PARTS; do
+  case $P in
+  new)
+    timeout -k 10 400 python -u -m pytest tests/test_gpu_chains.py -x -v --timeout 300 --timeout-method thread \
+      > $OUT/new.log 2>&1 || { tail -40 $OUT/new.log; exit 1; }
+    tail -3 $OUT/new.log ;;
+  suite)
+    timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
+      > $OUT/suite.log 2>&1 || { tail -40 $OUT/suite.log; exit 2; }
+    tail -3 $OUT/suite.log ;;
+  c2|c3|c4|c5|c5c)
+    W=config${P#c}
+    timeout -k 10 300 python3 -u bench.py --workload $W --steps 10 --warmup 5 --e2e-steps 0 --no-cpu-baseline \
+      > $OUT/$P.jsonl 2> $OUT/$P.log || { tail -20 $OUT/$P.log; exit 3; }
+    python3 -c "import json,sys; d=json.loads(open('$OUT/$P.jsonl').readlines()[-1]); print('$P', d['value'], d['ms_per_step'], d['hot_book'], d['kernel_ms'])" ;;
+  c2t)
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats -T --output-format csv -d $OUT/c2trace -o run \
+      -- python3 bench.py --workload config2 --steps 5 --warmup 5 --e2e-steps 0 --no-cpu-baseline > $OUT/c2_trace.log 2>&1 || exit 4 ;;
+  c3t)
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats -T --output-format csv -d $OUT/c3trace -o run \
+      -- python3 bench.py --workload config3 --steps 5 --warmup 5 --e2e-steps 0 --no-cpu-baseline > $OUT/c3_trace.log 2>&1 || exit 5 ;;
+  ubd)  # deep plan ns/record on a one-symbol 4-dp book: VGPR plan vs the LDS plan variant
+    for V in "" libgome_ldsdeep.so; do
+      GOME_LIB=${V:+$PWD/gome_amd/$V} timeout -k 10 200 python3 -u tools/ubench_deep.py > $OUT/ubd_${V:-main}.log 2>&1 || { tail -20 $OUT/ubd_${V:-main}.log; exit 6; }
+      echo "${V:-libgome.so}: $(cat $OUT/ubd_${V:-main}.log | tr '\n' ' ')"
+    done ;;
+  c5ab)  # config 5 / 5c bench lines, VGPR plan vs the LDS plan variant
+    for V in "" libgome_ldsdeep.so; do
+      for W in config5 config5c; do
+        GOME_LIB=${V:+$PWD/gome_amd/$V} timeout -k 10 300 python3 -u bench.py --workload $W --steps 8 --warmup 3 \
+          --e2e-steps 0 --no-cpu-baseline > $OUT/ab_${W}_${V:-main}.jsonl 2> $OUT/ab_${W}_${V:-main}.log || { tail -20 $OUT/ab_${W}_${V:-main}.log; exit 7; }
+        python3 -c "import json; d=json.loads(open('$OUT/ab_${W}_${V:-main}.jsonl').readlines()[-1]); print('$W ${V:-main}', d['value'], d['ms_per_step'], d['hot_book'])"
+      done
+    done ;;
+  esac
+done
+echo done

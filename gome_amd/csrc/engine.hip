@@ -205,7 +205,7 @@ struct gome_engine {
   hipStream_t flow_stream = nullptr;  // the hottest book's plan (critical path)
   hipStream_t copy_stream = nullptr;  // H2D of records, D2H of events (pipelined path)
   hipEvent_t fork{}, join{}, joinf{}, prep_h{}, prep_t{}, fork_adm{}, adm_done{}, seg_done{}, ev_scan{}, ev_hot{};
-  hipEvent_t dp_fork{}, cnt_fork{}, cnt_done{}, dw_done{}, dl_done{};  // the hottest book's deep chain, k_flow_count beside its writes
+  hipEvent_t dp_fork{}, cnt_fork{}, cnt_done{}, dw_done{}, dl_done{}, tl_done{};  // the hottest book's deep chain, k_flow_count beside its writes
   Slot slots[GOME_MAX_INFLIGHT];
   uint32_t next_slot = 0;
   std::deque<Flight> flights;
@@ -218,6 +218,12 @@ struct gome_engine {
   // capacities
   uint32_t max_batch = 0, key_bits = 1, passes = 1, dbits = 1;
   uint32_t tail_grid = 4096;  // blocks of the tail's per-touch kernels (GOME_TAIL_GRID; 4096 measured 5% faster than 1024 on config 2)
+  // the tail's writes (caller's stream) and events (hot stream, after the near books and the
+  // legacy kernels) as two kernels side by side, when the last batch had no dominant book: 0.07 ms
+  // faster on config 2, but the split events kernel's traffic slows a concurrent hottest-book
+  // plan (config 3: +0.2 ms), so with a hot book the fused launch (GOME_TAIL_SPLIT=0/1 forces)
+  int tail_split = -1;
+  uint64_t last_maxseg = 0, last_n = 0;  // the last finished batch's hottest book / size
   uint32_t hist_cap = 0, bsum_cap = 0;
   unsigned long long idx_cap = 0;
   // batch buffers
@@ -297,7 +303,7 @@ struct gome_engine {
           if (ev) (void)hipEventDestroy(ev);
     }
     for (hipEvent_t ev : {fork, join, joinf, prep_h, prep_t, fork_adm, adm_done, seg_done, ev_scan, ev_hot, dp_fork, cnt_fork, cnt_done,
-                          dw_done})
+                          dw_done, dl_done, tl_done})
       if (ev) (void)hipEventDestroy(ev);
     if (hot_stream) (void)hipStreamDestroy(hot_stream);
     if (flow_stream) (void)hipStreamDestroy(flow_stream);
@@ -360,7 +366,7 @@ gome_status gome_engine::init(const gome_config& c) {
   HIPCHK(hipStreamCreateWithFlags(&flow_stream, hipStreamNonBlocking));
   HIPCHK(hipStreamCreateWithFlags(&copy_stream, hipStreamNonBlocking));
   for (hipEvent_t* ev : {&fork, &join, &joinf, &prep_h, &prep_t, &fork_adm, &adm_done, &seg_done, &ev_scan, &ev_hot,
-                         &dp_fork, &cnt_fork, &cnt_done, &dw_done, &dl_done})
+                         &dp_fork, &cnt_fork, &cnt_done, &dw_done, &dl_done, &tl_done})
     HIPCHK(hipEventCreateWithFlags(ev, hipEventDisableTiming));
   for (Slot& S : slots) {
     for (hipEvent_t* ev : {&S.ev0, &S.ev1, &S.evm0, &S.evm1, &S.evh0, &S.evh1, &S.evf0, &S.evf1, &S.evc0, &S.evc1})
@@ -389,6 +395,7 @@ gome_status gome_engine::init(const gome_config& c) {
 
   max_batch = cfg.max_batch;
   if (const char* g = std::getenv("GOME_TAIL_GRID")) tail_grid = std::max(64, std::atoi(g));  // (tuning)
+  if (const char* g = std::getenv("GOME_TAIL_SPLIT")) tail_split = std::atoi(g) != 0 ? 1 : 0;  // (A/B)
   uint32_t ms = cfg.max_symbols;
   key_bits = (ms <= 1) ? 1 : 32 - __builtin_clz(ms - 1);
   passes = (key_bits + RS_MAXBITS - 1) / RS_MAXBITS;
@@ -471,7 +478,7 @@ gome_status gome_engine::init(const gome_config& c) {
   if (!alloc(&F.hdr, MAX_FLOW, "flow headers") || !alloc(&F.lvl, MAX_FLOW * FL_CAP, "flow levels") ||
       !alloc(&F.ord8, static_cast<uint64_t>(FL_ORD8_MUL) * nb + FL_ORD8_PAD, "flow records") || !alloc(&F.log, ntouch, "flow touch log") ||
       !alloc(&F.srt, ntouch, "flow level runs") || !alloc(&F.rs, ntouch, "flow new makers") ||
-      !alloc(&F.fbase, ntouch, "flow fill bases") || !alloc(&F.ig, F.ig_cap, "flow gathered makers") ||
+      !alloc(&F.fbase, ntouch, "flow fill bases") || !alloc(&F.tfc, ntouch, "flow touch fills") || !alloc(&F.ig, F.ig_cap, "flow gathered makers") ||
       !alloc(&F.ig_bump, 1, "flow gather bump") || !alloc(&F.toff, 2 * FC_TOFF, "flow touch offsets") ||
       !alloc(&F.tmap, 6ull * (ntouch / 64 + 2), "flow touch-group books") ||
       !alloc(&F.lvout, static_cast<size_t>(MAX_FLOW) * FL_CAP, "flow final levels"))
@@ -658,6 +665,7 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   const bool c_deep = (ch & FL_CH_DEEP) != 0, c_canc = (ch & FL_CH_CANCEL) != 0;
   S.chains = ch;
   F.chains = ch;
+  const bool split_tail = tail_split >= 0 ? tail_split != 0 : last_maxseg * 16 < last_n;
   FlowArgs FH = F, FH0 = F, FH1 = F, FT = F;
   FH.h0 = 0; FH.h1 = FL_HEAD; FH.tb = 0;
   FH0.h0 = 0; FH0.h1 = 1; FH0.tb = 0; FH0.mb = 0;
@@ -873,7 +881,12 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
     // the flow books' writes beside their events (into the arena: k_ev_scatter places them
     // after the publish scan), then the deep books' writes
     HIPCHK(mark(GOME_PH_TAIL_WRITE, 0, s));
-    k_flow_write_events<<<nh_tail + ceil_div(tail_grid * FL_EV_T, FL_WRITE_T), FL_WRITE_T, 0, s>>>(D, B, FT, nh_tail);
+    if (split_tail) {
+      HIPCHK(hipEventRecord(tl_done, s));  // (the events run on the hot stream, below)
+      k_flow_write<<<nh_tail, FL_WRITE_T, 0, s>>>(D, B, FT);
+    } else {
+      k_flow_write_events<<<nh_tail + ceil_div(tail_grid * FL_EV_T, FL_WRITE_T), FL_WRITE_T, 0, s>>>(D, B, FT, nh_tail);
+    }
     HIPCHK(mark(GOME_PH_TAIL_WRITE, 1, s));
     HIPCHK(mark(GOME_PH_TAIL_EVENTS, 0, s));
     if (c_deep) deep_write(FT, s);
@@ -904,6 +917,10 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   k_pend_apply<<<dim3(8, 64), 256, 0, hot_stream>>>(D, d_pend, d_seg_start, d_seg_order, B);
   // oid watermarks for the next batches' duplicate-oid probe (the hot stream has slack here)
   k_oid_max<<<gN, T256, 0, hot_stream>>>(n, skeys, d_prep, d_oid_max);
+  if (nh_tail && split_tail) {  // the tail's events beside its writes (arena; k_ev_scatter places them)
+    HIPCHK(hipStreamWaitEvent(hot_stream, tl_done, 0));
+    k_flow_events_fused<<<tail_grid, FL_EV_T, 0, hot_stream>>>(D, B, FT);
+  }
   HIPCHK(hipEventRecord(join, hot_stream));
   // (the hot stream's own work ended long before the hottest book's plan does)
   HIPCHK(mark(GOME_PH_HEAD_RECON, 0, flow_stream));
@@ -1007,6 +1024,8 @@ gome_status gome_engine::finish(uint32_t sl, uint32_t n) {
   deep_quiet = want_deep ? 0u : std::min<uint32_t>(deep_quiet + 1u, GOME_CHAIN_QUIET);
   canc_quiet = want_canc ? 0u : std::min<uint32_t>(canc_quiet + 1u, GOME_CHAIN_QUIET);
   stats.chains = S.chains;
+  last_maxseg = st.ctr[C_MAXSEG];
+  last_n = n;
   stats.chains_wanted = (want_deep ? FL_CH_DEEP : 0u) | (want_canc ? FL_CH_CANCEL : 0u);
   if (const uint64_t nd = std::min<uint64_t>(st.ctr[C_DUP], n)) {
     dup_idx.resize(nd);

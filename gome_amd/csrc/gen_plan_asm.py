@@ -1300,6 +1300,92 @@ class GenDV(GenD):
         return [re.sub(r"\bm0\b", MC, x).replace("M0LANE", "m0") for x in self.out]
 
 
+# ---- W32DVC: W32DV with DELs (W32DC's records and Q formula on the VGPR words) --------------
+# One word per level has no side: a DEL of a maker on side sd at a level that now rests on the
+# other side (or is the other side's cached top) finds nothing there (its side's depth is 0), so
+# its v is zeroed first (r = clamp(d - Q, 0, 0) = 0, the word written back unchanged).
+class GenDVC(GenDV):
+    def decode(self, j: int):
+        GenDC.decode(self, j)
+
+    def del_log(self, r: str):
+        """The cancel touch {K, level, r}; the count advances only when r != 0 (SCC on entry)."""
+        e = self.e
+        e(f"s_mov_b32 M0LANE, {MC}")
+        e(f"v_writelane_b32 %[lk], {K}, M0LANE")
+        e(f"v_writelane_b32 %[la], {r}, M0LANE")
+        e(f"v_writelane_b32 %[lb], {LI}, M0LANE")
+        e(f"s_addc_u32 {MC}, {MC}, 0")
+
+    def del_path(self, i: int):
+        e = self.e
+        lo, hi = f"s{BUF[i][0]}", f"s{BUF[i][1]}"
+        lab = self.lab
+        j = (i + 1) % NS
+        X1, XV, X2 = "s94", "s95", "s96"
+        e(f"{lab(f'D{i}')}:")
+        e(f"s_bfe_u32 {XV}, {hi}, 0x10000e")                 # v (bits 14..29)
+        e(f"s_and_b32 {K}, {hi}, 0xc0000000")
+        e(f"s_or_b32 {K}, {K}, {JJS}")                        # the cancel touch key
+        e(f"s_bitcmp1_b32 {hi}, 31")
+        e(f"s_cbranch_scc1 {lab(f'DA{i}')}")
+        for sd in ("B", "A"):
+            if sd == "A":
+                e(f"{lab(f'DA{i}')}:")
+            top, topd = (BB, BBD) if sd == "B" else (BA, BAD)
+            e(f"s_cmp_eq_u32 {LI}, {top}")
+            e(f"s_cbranch_scc1 {lab(f'DT{sd}{i}')}")
+            # a level on the other side's half of the book: nothing of side sd rests there
+            if sd == "B":
+                e(f"s_cmp_ge_u32 {LI}, {BA}")
+            else:
+                e(f"s_cmp_le_u32 {LI}, {BB}")
+            e(f"s_cselect_b32 {XV}, 0, {XV}")
+            # a level behind the top: its word, reduced, written back
+            e(f"s_lshr_b32 {T0}, {LI}, 6")
+            e(f"s_and_b32 s79, {LI}, 63")
+            e("s_lshl_b64 exec, 1, s79")
+            e(f"s_set_gpr_idx_on {T0}, gpr_idx(SRC0)")
+            e(f"v_mov_b32 v{VTR}, v{VB}")
+            e("s_set_gpr_idx_off")
+            e(f"v_readlane_b32 {X1}, v{VTR}, s79")             # depth
+            e(f"s_sub_u32 {X2}, {X1}, {lo}")                  # SCC = borrow
+            e(f"s_cselect_b32 {X2}, 0, {X2}")
+            e(f"s_min_u32 {X2}, {X2}, {XV}")                  # r
+            e(f"s_sub_u32 {X1}, {X1}, {X2}")
+            e(f"v_mov_b32 v{VAM}, {X1}")
+            e(f"s_set_gpr_idx_on {T0}, gpr_idx(DST)")
+            e(f"v_mov_b32 v{VB}, v{VAM}")
+            e("s_set_gpr_idx_off")
+            e(f"s_cmp_lg_u32 {X2}, 0")
+            self.del_log(X2)
+            self.dispatch(j, False)
+            # the cached top
+            e(f"{lab(f'DT{sd}{i}')}:")
+            e(f"s_sub_u32 {X1}, {topd[0]}, {lo}")
+            e(f"s_cselect_b32 {X1}, 0, {X1}")
+            e(f"s_min_u32 {X1}, {X1}, {XV}")                  # r
+            e(f"s_sub_u32 {topd[0]}, {topd[0]}, {X1}")
+            e(f"s_cmp_lg_u32 {X1}, 0")
+            self.del_log(X1)
+            e(f"s_cmp_lg_u32 {topd[0]}, 0")
+            e(f"s_cbranch_scc1 {lab(f'DN{i}')}")
+            self.next_top(sd)
+            self.dispatch(j, False)
+
+    def slot(self, i: int):
+        """GenDV's slot, the DEL paths placed before the SALE entry."""
+        sv = self.out
+        self.out = []
+        super().slot(i)
+        body = self.out
+        self.out = sv
+        k = body.index(f"{self.lab(f'S{i}')}:")
+        self.out.extend(body[:k])
+        self.del_path(i)
+        self.out.extend(body[k:])
+
+
 ALIGN = int(os.environ.get("GOME_PLAN_ALIGN", "0"))   # log2 byte alignment of branch targets
 
 
@@ -1321,7 +1407,7 @@ def main():
     with open(out, "w") as f:
         f.write("// Generated by gen_plan_asm.py — do not edit.\n")
         for w, g in ((64, Gen(64)), (32, Gen(32)), ("32C", GenC()), ("32D", GenD()), ("32DC", GenDC()),
-                     ("32DV", GenDV())):
+                     ("32DV", GenDV()), ("32DVC", GenDVC())):
             f.write(f"#define FL_PLAN_ASM{w} \\\n")
             for line in aligned(g.build()):
                 f.write(f'  "{line}\\n\\t" \\\n')

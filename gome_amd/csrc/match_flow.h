@@ -108,6 +108,13 @@ struct RsEnt {       // a new maker of the level, in FIFO order (32 B)
 };
 static_assert(sizeof(RsEnt) == 32, "RsEnt layout");
 
+struct FlTouchFc {   // the makers a CONS touch fills (set by the level pass, read by the event passes)
+  uint32_t first, last;  // FIFO-order maker indices (old makers IG[0, ig_n), then new ones)
+  uint32_t lvl, pad;     // its level
+  int64_t coord;         // the consumption cursor before it (volume coordinates)
+};
+static_assert(sizeof(FlTouchFc) == 24, "FlTouchFc layout");
+
 struct IgEnt {       // a resting maker from before the batch, gathered in FIFO order (32 B)
   int64_t e, v;
   uint32_t oid, uuid;
@@ -191,6 +198,7 @@ struct FlowArgs {
   SEnt* srt;           // same index space
   RsEnt* rs;           // same index space
   uint32_t* fbase;     // same index space: fill_idx of a touch's first event
+  FlTouchFc* tfc;      // same index space (log order): a CONS touch's makers (fl_level_fc)
   IgEnt* ig;
   uint32_t ig_cap;
   uint32_t* ig_bump;
@@ -968,10 +976,10 @@ constexpr bool FL_DEEP_VGPR = true;   // W32DV (depths in VGPRs) for ADD-only de
 constexpr bool FL_DEEP_VGPR = false;  // (variant build: every deep book on the LDS plan)
 #endif
 
-// Does deep book h take the VGPR plan (gen_plan_asm.py W32DV)?  ADD-only, levels and the two
-// sentinels within its FL_DEEP_NVL words.
+// Does deep book h take the VGPR plan (gen_plan_asm.py W32DV, W32DVC with DELs)?  Its levels and
+// the two sentinels within the FL_DEEP_NVL words.
 __device__ __forceinline__ bool fl_deep_vgpr(const FlowHdr& hd) {
-  return FL_DEEP_VGPR && !hd.dc && hd.nl + 2 <= FL_DEEP_NVL;
+  return FL_DEEP_VGPR && hd.nl + 2 <= FL_DEEP_NVL;
 }
 
 
@@ -1269,12 +1277,18 @@ __device__ __forceinline__ void fl_plan_deep(const Dev& D, const FlowArgs& F, ui
     const uint32_t ba = uni(hw[0]), bb = uni(hw[1]), bad = uni(hw[2]), bbd = uni(hw[3]);
     const uint32_t sv = lane < FL_DEEP_NVL / 2048 ? hw[4 + lane] : 0u;
     uint32_t oba, obb;
-    asm volatile(FL_PLAN_ASM32DV
-                 : [lk] "+v"(lg.lk), [la] "+v"(lg.la), [lb] "+v"(lg.lb), [nacc] "+s"(lg.nacc), [lpos] "+s"(lg.lpos),
-                   [voff] "=&v"(voff), [vpf] "=&v"(vpf), [oba] "=s"(oba), [obb] "=s"(obb)
-                 : [ob] "s"(ob), [nh] "s"(nh), [logp] "s"(logp), [lcap] "s"(lg.lcap), [vl16] "v"(vl16),
-                   [vzero] "v"(vzero), [sv] "v"(sv), [ba] "s"(ba), [bb] "s"(bb), [bad] "s"(bad), [bbd] "s"(bbd)
-                 : FL_PLAN_CLOBBERS, FL_PLAN_CLOBBERS_DV, "scc", "vcc", "memory");
+#define FL_DV_OPERANDS                                                                                        \
+  : [lk] "+v"(lg.lk), [la] "+v"(lg.la), [lb] "+v"(lg.lb), [nacc] "+s"(lg.nacc), [lpos] "+s"(lg.lpos),         \
+    [voff] "=&v"(voff), [vpf] "=&v"(vpf), [oba] "=s"(oba), [obb] "=s"(obb)                                     \
+  : [ob] "s"(ob), [nh] "s"(nh), [logp] "s"(logp), [lcap] "s"(lg.lcap), [vl16] "v"(vl16), [vzero] "v"(vzero), \
+    [sv] "v"(sv), [ba] "s"(ba), [bb] "s"(bb), [bad] "s"(bad), [bbd] "s"(bbd)                                   \
+  : FL_PLAN_CLOBBERS, FL_PLAN_CLOBBERS_DV, "scc", "vcc", "memory"
+    if (uni(hd->dc)) {
+      asm volatile(FL_PLAN_ASM32DVC FL_DV_OPERANDS);
+    } else {
+      asm volatile(FL_PLAN_ASM32DV FL_DV_OPERANDS);
+    }
+#undef FL_DV_OPERANDS
     if (lane == 0) F.hdr[h].dv_ba = oba;  // (fl_deep_store: asks lie at or above it)
     (void)obb;
   } else if (uni(hd->dc)) {  // DELs in the segment (gen_plan_asm.py W32DC)
@@ -1477,9 +1491,36 @@ __device__ __forceinline__ uint32_t fl_find(const IgEnt* IG, uint32_t ig_n, cons
   return ig_n + lo;
 }
 
+// The makers every CONS touch of level q fills (first / last in FIFO order), with its cursor and
+// level, into F.tfc at the touch's log index: binary searches over the level's makers, done here
+// where the level's maker arrays were just written (L2-hot), so the event passes read one entry
+// per touch instead of searching.  Threads tid, tid + nthr, ... of the caller take the touches.
+__device__ __forceinline__ void fl_level_fc(const FlowArgs& F, uint32_t L, uint32_t q, uint32_t base, uint32_t cnt,
+                                            const IgEnt* IG, uint32_t ig_n, uint32_t nrest, int64_t d0, uint32_t tid,
+                                            uint32_t nthr) {
+  const SEnt* R = F.srt + L + base;
+  const RsEnt* RS = F.rs + L + base;
+  for (uint32_t i = tid; i < cnt; i += nthr) {
+    const SEnt e = R[i];
+    if (e.kind != TK_CONS) continue;
+    const uint32_t f = fl_find(IG, ig_n, RS, nrest, d0, e.coord);
+    // most touches end inside their first maker: probe it before searching for the last
+    const int64_t xl = e.coord + e.amt - 1;
+    const int64_t fend = f < ig_n ? IG[f].e + IG[f].v : RS[f - ig_n].e + RS[f - ig_n].v;
+    FlTouchFc x;
+    x.first = f;
+    x.last = xl < fend ? f : fl_find(IG, ig_n, RS, nrest, d0, xl);
+    x.lvl = q;
+    x.pad = 0;
+    x.coord = e.coord;
+    F.tfc[L + e.t] = x;
+  }
+}
+
 __device__ __forceinline__ void fl_level_one(const Dev& D, const FlowArgs& F, uint32_t h, uint32_t q,
                                              uint32_t run_base = NIL, uint32_t run_cnt = 0,
-                                             uint32_t ig_pre = NIL, int64_t pre_cfin = -1, uint32_t pre_nr = 0) {
+                                             uint32_t ig_pre = NIL, int64_t pre_cfin = -1, uint32_t pre_nr = 0,
+                                             bool fc_here = true) {
   const FlowHdr* hd = &F.hdr[h];
   const uint32_t lane = lane_id();
   FlowLvl* Lq = fl_lvls(F, h) + q;
@@ -1615,6 +1656,7 @@ __device__ __forceinline__ void fl_level_one(const Dev& D, const FlowArgs& F, ui
     Lq->tslot = tslot;
     Lq->nlive0 = nv0 - consumed;
   }
+  if (fc_here && cfin > 0) fl_level_fc(F, L, q, base, cnt, F.ig + ig_base, ng, nr, d0, lane, 64);
 }
 
 constexpr uint32_t FL_LEVEL_T = 1024;
@@ -1633,25 +1675,18 @@ struct FlTouchCtx {
   uint32_t first, last;
 };
 
-__device__ __forceinline__ FlTouchCtx fl_touch_ctx(const FlowArgs& F, uint32_t h, uint32_t L, const Touch& x) {
-  FlTouchCtx t;
-  const bool deep = F.hdr[h].ok == FL_OK_DEEP;
-  const uint32_t k = deep ? F.srt[L + x.pos].lvl : (x.kr & 127u);
-  t.Lq = fl_lvls(F, h) + k;
-  const uint32_t base = t.Lq->base;
-  t.IG = F.ig + t.Lq->ig_base;
-  t.RS = F.rs + L + base;
-  t.c = F.srt[L + x.pos].coord;
-  t.a = x.amt;
-  const int64_t d0 = t.Lq->d0;
-  const uint32_t ig_n = t.Lq->ig_n, nrest = t.Lq->nrest;
-  t.first = fl_find(t.IG, ig_n, t.RS, nrest, d0, t.c);
-  // most touches end inside their first maker: probe it before searching for the last
-  const uint32_t f = t.first;
-  const int64_t xl = t.c + t.a - 1;
-  const int64_t fend = f < ig_n ? t.IG[f].e + t.IG[f].v : t.RS[f - ig_n].e + t.RS[f - ig_n].v;
-  t.last = xl < fend ? f : fl_find(t.IG, ig_n, t.RS, nrest, d0, xl);
-  return t;
+// CONS touch t (log index) of book h: its level and the makers it fills (fl_level_fc).
+__device__ __forceinline__ FlTouchCtx fl_touch_ctx(const FlowArgs& F, uint32_t h, uint32_t L, const Touch& x, uint32_t t) {
+  FlTouchCtx c;
+  const FlTouchFc tf = F.tfc[L + t];
+  c.Lq = fl_lvls(F, h) + tf.lvl;
+  c.IG = F.ig + c.Lq->ig_base;
+  c.RS = F.rs + L + c.Lq->base;
+  c.c = tf.coord;
+  c.a = x.amt;
+  c.first = tf.first;
+  c.last = tf.last;
+  return c;
 }
 
 // The same for every lane of a wave whose touches are consecutive from g0 (lane 0's, a multiple
@@ -1724,7 +1759,7 @@ __global__ void k_flow_count(Dev D, BatchArgs B, FlowArgs F) {
       if (tk_j(y) != tk_j(x)) break;
       F.fbase[L + u] = acc;
       if (((y.kr >> 7) & 1u) == TK_CONS) {
-        const FlTouchCtx c = fl_touch_ctx(F, h, L, y);
+        const FlTouchCtx c = fl_touch_ctx(F, h, L, y, u);
         const uint32_t ne = c.last - c.first + 1;
         acc += ne;
         fills += ne;
@@ -1776,7 +1811,7 @@ __device__ __forceinline__ void fl_events(const Dev& D, const BatchArgs& B, cons
       L = FL_TOUCH_MUL * F.hdr[h].beg;
       x = F.log[L + t];
       if (((x.kr >> 7) & 1u) == TK_CONS) {
-        c = fl_touch_ctx(F, h, L, x);
+        c = fl_touch_ctx(F, h, L, x, t);
         cnt = c.last - c.first + 1;
       }
     }
@@ -1926,7 +1961,7 @@ __device__ __forceinline__ void fl_events_fused(const Dev& D, const BatchArgs& B
         first = t == 0 || tk_j(F.log[L + t - 1]) != j;
         last = t + 1 == nt || tk_j(F.log[L + t + 1]) != j;
         if (((x.kr >> 7) & 1u) == TK_CONS) {
-          c = fl_touch_ctx(F, h, L, x);
+          c = fl_touch_ctx(F, h, L, x, t);
           cnt = c.last - c.first + 1;
           fills += cnt;
           const int64_t lend = c.last < c.Lq->ig_n ? c.IG[c.last].e + c.IG[c.last].v
@@ -1945,7 +1980,7 @@ __device__ __forceinline__ void fl_events_fused(const Dev& D, const BatchArgs& B
         if (tk_j(y) != j) break;
         carry_a += y.amt;
         if (((y.kr >> 7) & 1u) == TK_CONS) {
-          const FlTouchCtx cy = fl_touch_ctx(F, h, L, y);
+          const FlTouchCtx cy = fl_touch_ctx(F, h, L, y, u - 1);
           carry_n += cy.last - cy.first + 1;
         }
       }
@@ -2570,7 +2605,12 @@ __global__ __launch_bounds__(FL_LVB_T) void k_flow_level_wide(Dev D, FlowArgs F)
   int64_t cfin;
   uint32_t nr;
   fl_level_scan_blk(F, h, q, cfin, nr);
-  if (threadIdx.x < 64) fl_level_one(D, F, h, q, NIL, 0, NIL, cfin, nr);
+  if (threadIdx.x < 64) fl_level_one(D, F, h, q, NIL, 0, NIL, cfin, nr, false);
+  __syncthreads();  // (wave 0's level record, then the whole block searches)
+  const FlowLvl* Lq = F.lvl + h * FL_CAP + q;
+  if (cfin > 0)
+    fl_level_fc(F, FL_TOUCH_MUL * F.hdr[h].beg, q, Lq->base, Lq->cnt, F.ig + Lq->ig_base, Lq->ig_n, Lq->nrest, Lq->d0,
+                threadIdx.x, FL_LVB_T);
 }
 
 }  // namespace gome

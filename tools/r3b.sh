@@ -42,6 +42,24 @@ for P in $PARTS; do
         python3 -c "import json; d=json.loads(open('$OUT/ab_${W}_${V:-main}.jsonl').readlines()[-1]); print('$W ${V:-main}', d['value'], d['ms_per_step'], d['hot_book'])"
       done
     done ;;
+  abv)  # bench lines of each variant build gome_amd/libgome_*.so beside libgome.so (configs from ABW)
+    for V in "" $(cd gome_amd && ls libgome_*.so 2>/dev/null); do
+      for W in ${ABW:-config2 config3}; do
+        GOME_LIB=${V:+$PWD/gome_amd/$V} timeout -k 10 300 python3 -u bench.py --workload $W --steps 8 --warmup 5 \
+          --e2e-steps 0 --no-cpu-baseline > $OUT/abv_${W}_${V:-main}.jsonl 2> $OUT/abv_${W}_${V:-main}.log || { tail -20 $OUT/abv_${W}_${V:-main}.log; exit 8; }
+        python3 -c "import json; d=json.loads(open('$OUT/abv_${W}_${V:-main}.jsonl').readlines()[-1]); print('$W ${V:-main}', d['value'], d['ms_per_step'], d['hot_book']['ns_per_order'], d['kernel_ms'])"
+      done
+    done ;;
+  split)  # GOME_TAIL_SPLIT A/B on configs 2 and 3, alternating
+    for R in 1 2; do
+      for SP in 1 0; do
+        for W in config2 config3; do
+          GOME_TAIL_SPLIT=$SP timeout -k 10 300 python3 -u bench.py --workload $W --steps 8 --warmup 5 --e2e-steps 0 \
+            --no-cpu-baseline > $OUT/sp${SP}_${W}_$R.jsonl 2> $OUT/sp${SP}_${W}_$R.log || { tail -20 $OUT/sp${SP}_${W}_$R.log; exit 9; }
+          python3 -c "import json; d=json.loads(open('$OUT/sp${SP}_${W}_$R.jsonl').readlines()[-1]); print('split $SP $W $R', d['value'], d['ms_per_step'])"
+        done
+      done
+    done ;;
   esac
 done
 echo done

@@ -223,6 +223,7 @@ struct gome_engine {
   // faster on config 2, but the split events kernel's traffic slows a concurrent hottest-book
   // plan (config 3: +0.2 ms), so with a hot book the fused launch (GOME_TAIL_SPLIT=0/1 forces)
   int tail_split = -1;
+  bool adm_fast = true;  // k_adm_pre's fresh-batch test (GOME_ADM_FAST=0: every batch through the tables; A/B)
   uint64_t last_maxseg = 0, last_n = 0;  // the last finished batch's hottest book / size
   uint32_t hist_cap = 0, bsum_cap = 0;
   unsigned long long idx_cap = 0;
@@ -240,6 +241,8 @@ struct gome_engine {
   uint32_t* d_first = nullptr;          // per (S, oid) slot: its first admitted ADD (NIL between batches)
   uint32_t *d_adm_slot2 = nullptr, *d_adm_aux = nullptr;  // per record: (S, uuid, oid) / (S, oid) slot
   uint32_t* d_oid_max = nullptr;        // per symbol: the highest oid an admitted ADD carried
+  uint32_t* d_adm_ctl = nullptr;        // k_adm_ctl / k_adm_pre: oid watermark, not-fresh flag, batch max oid
+  uint32_t oid_gmax_load = 0;           // (gome_load_books' copy source)
   uint32_t* d_adm_slot = nullptr;
   uint32_t adm_mask = 0;
   uint32_t* d_ev_count = nullptr;
@@ -396,6 +399,7 @@ gome_status gome_engine::init(const gome_config& c) {
   max_batch = cfg.max_batch;
   if (const char* g = std::getenv("GOME_TAIL_GRID")) tail_grid = std::max(64, std::atoi(g));  // (tuning)
   if (const char* g = std::getenv("GOME_TAIL_SPLIT")) tail_split = std::atoi(g) != 0 ? 1 : 0;  // (A/B)
+  if (const char* g = std::getenv("GOME_ADM_FAST")) adm_fast = std::atoi(g) != 0;              // (A/B)
   uint32_t ms = cfg.max_symbols;
   key_bits = (ms <= 1) ? 1 : 32 - __builtin_clz(ms - 1);
   passes = (key_bits + RS_MAXBITS - 1) / RS_MAXBITS;
@@ -458,7 +462,7 @@ gome_status gome_engine::init(const gome_config& c) {
       !alloc(&d_multi, adm_mask + 1ull, "admission repeat flags") ||
       !alloc(&d_first, adm_mask + 1ull, "first admitted ADDs") ||
       !alloc(&d_adm_slot2, nb, "admission key slots") || !alloc(&d_adm_aux, nb, "admission shared slots") ||
-      !alloc(&d_oid_max, cfg.max_symbols, "oid watermarks") ||
+      !alloc(&d_oid_max, cfg.max_symbols, "oid watermarks") || !alloc(&d_adm_ctl, 3, "admission control") ||
       !alloc(&d_adm_slot, nb, "adm_slot") ||
       !alloc(&d_ev_count, nb, "ev_count") || !alloc(&d_ev_off, nb, "ev_off") ||
       !alloc(&d_prep, nb, "prep") || !alloc(&d_pend, nb, "pending inserts") ||
@@ -524,6 +528,8 @@ gome_status gome_engine::init(const gome_config& c) {
   HIPCHK(hipMemsetAsync(d_multi, 0, adm_mask + 1ull, stream));
   HIPCHK(hipMemsetAsync(d_first, 0xFF, (adm_mask + 1ull) * 4, stream));
   HIPCHK(hipMemsetAsync(d_oid_max, 0, 4ull * cfg.max_symbols, stream));
+  HIPCHK(hipMemsetAsync(d_adm_ctl, 0, 12, stream));
+  HIPCHK(hipMemsetAsync(d_adm, 0, (adm_mask + 1ull) * 8, stream));  // (k_adm_flag leaves it empty)
   HIPCHK(hipMemsetAsync(d_pend, 0, sizeof(PendEnt) * nb, stream));
   if (D.idx_mask >= PEND) return fail(GOME_E_INVAL, "gome_config.max_nodes too large (index > 2^31 slots)");
   HIPCHK(hipStreamSynchronize(stream));
@@ -625,17 +631,18 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   // the validation, the radix sort and the segmentation (the batch's critical path), enqueued
   // after the sort so that the main stream's first kernels reach the GPU first
   HIPCHK(hipStreamWaitEvent(flow_stream, fork_adm, 0));
-  HIPCHK(hipMemsetAsync(d_adm, 0, (adm_mask + 1ull) * 8, flow_stream));
+  k_adm_ctl<<<1, 1, 0, flow_stream>>>(d_adm_ctl, adm_fast ? 1u : 0u);
+  k_adm_pre<<<std::min<uint32_t>(gN, 1024), T256, 0, flow_stream>>>(d_ord, n, d_adm_ctl);
   if ((++fc_gen & FC_GEN_MASK) == 0) HIPCHK(hipMemsetAsync(F.fc_hash, 0, sizeof(FcHash) * fc_hcap, flow_stream));
   F.fc_gen = fc_gen;
   HIPCHK(mark(GOME_PH_ADMISSION, 0, flow_stream));
   k_adm<<<gN, T256, 0, flow_stream>>>(d_ord, n, d_adm, d_adm_slot, adm_mask, cfg.max_symbols, d_st, D.books, D.idx,
-                                      D.idx_mask, d_oid_max, d_multi);
+                                      D.idx_mask, d_oid_max, d_multi, d_adm_ctl + 1);
   k_adm_flag<<<gN, T256, 0, flow_stream>>>(d_ord, n, d_adm_slot, d_multi, d_dup, d_adm_slot2, d_adm_aux, adm_mask, d_st,
-                                           S.d_dup);
-  k_adm_res<<<gN, T256, 0, flow_stream>>>(d_ord, n, d_adm_slot, d_dup, d_adm_slot2, d_first);
-  k_adm_dup<<<gN, T256, 0, flow_stream>>>(n, d_adm_slot, d_first, d_st, S.d_dup);
-  k_adm_clean<<<gN, T256, 0, flow_stream>>>(n, d_adm_aux, d_adm_slot2, d_dup, d_first, d_multi);
+                                           S.d_dup, d_adm, d_adm_ctl + 1);
+  k_adm_res<<<gN, T256, 0, flow_stream>>>(d_ord, n, d_adm_slot, d_dup, d_adm_slot2, d_first, d_adm_ctl + 1);
+  k_adm_dup<<<gN, T256, 0, flow_stream>>>(n, d_adm_slot, d_first, d_st, S.d_dup, d_adm_ctl + 1);
+  k_adm_clean<<<gN, T256, 0, flow_stream>>>(n, d_adm_aux, d_adm_slot2, d_dup, d_first, d_multi, d_adm_ctl + 1);
   HIPCHK(mark(GOME_PH_ADMISSION, 1, flow_stream));
   HIPCHK(hipEventRecord(adm_done, flow_stream));
 
@@ -809,7 +816,7 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
       HIPCHK(hipEventRecord(dl_done, cs));  // (a deep book with DELs: k_fc_count / events wait)
     }
     k_flow_sort_cnt<<<dim3(FL_SORT_GRID, nb), FL_TILE, 0, st>>>(D, R);
-    k_flow_sort_scan<<<nb, FL_CAP, 0, st>>>(D, R);
+    k_flow_sort_scan<<<nb, FL_CAP * FL_SCAN_P, 0, st>>>(D, R);
     k_flow_sort_scatter<<<dim3(FL_SORT_GRID, nb), FL_TILE, 0, st>>>(D, R);
     if (!split && c_deep) deep_sort_level(R, FL_SORT_GRID, st);
     k_flow_level_wide<<<dim3(FL_CAP, nb), FL_LVB_T, 0, st>>>(D, R);
@@ -1547,6 +1554,8 @@ gome_status gome_engine::load_books(size_t nb, const uint32_t* bsym, const uint3
   }
   HIPCHK(hipMemcpyAsync(D.books, books.data(), static_cast<size_t>(ms) * sizeof(Book), hipMemcpyHostToDevice, s));
   HIPCHK(hipMemcpyAsync(d_oid_max, oid_max.data(), static_cast<size_t>(ms) * 4, hipMemcpyHostToDevice, s));
+  oid_gmax_load = *std::max_element(oid_max.begin(), oid_max.end());  // (k_adm_pre's watermark)
+  HIPCHK(hipMemcpyAsync(d_adm_ctl, &oid_gmax_load, 4, hipMemcpyHostToDevice, s));
   HIPCHK(hipMemcpyAsync(D.lvl_bump, &nl, 4, hipMemcpyHostToDevice, s));
   HIPCHK(hipMemcpyAsync(D.ch_bump, &nch, 4, hipMemcpyHostToDevice, s));
   if (!islot.empty()) {

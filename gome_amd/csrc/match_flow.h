@@ -1491,29 +1491,74 @@ __device__ __forceinline__ uint32_t fl_find(const IgEnt* IG, uint32_t ig_n, cons
   return ig_n + lo;
 }
 
+// Wave-cooperative fl_find: every lane's query q (lanes with !valid ignored), b a maker at or
+// before every valid query's.  Windows of 64 consecutive makers from b (one coalesced read into
+// the lanes) searched by shuffles; a query beyond FL_FC_WIN windows searches alone.  Makers'
+// starts strictly ascend (no zero-volume maker in a clean book), IG then RS, from 0.
+constexpr int FL_FC_WIN = 3;
+__device__ __forceinline__ uint32_t fl_wave_find(const IgEnt* IG, uint32_t ig_n, const RsEnt* RS, uint32_t nrest,
+                                                 int64_t d0, bool valid, int64_t q, uint32_t b) {
+  const uint32_t nm = ig_n + nrest, lane = lane_id();
+  uint32_t res = NIL;
+  bool done = !valid;
+  for (int w = 0; w < FL_FC_WIN && !__all(done); ++w) {
+    const uint32_t m = b + lane;
+    const int64_t st = m < nm ? (m < ig_n ? IG[m].e : RS[m - ig_n].e) : INT64_MAX;
+    const int64_t last = __shfl(st, 63);
+    const bool here = !done && (q < last || b + 63 >= nm);
+    // (every lane takes part in the shuffles; the count of the window's starts <= q)
+    const int64_t qq = here ? q : INT64_MIN;
+    uint32_t pos = 0;
+#pragma unroll
+    for (uint32_t step = 32; step; step >>= 1) {
+      const int64_t sv = __shfl(st, static_cast<int>(pos + step - 1));
+      if (sv <= qq) pos += step;
+    }
+    if (here) {
+      res = b + pos - 1;
+      done = true;
+    }
+    b += 63;  // (the window's last maker opens the next one)
+  }
+  if (!done) res = fl_find(IG, ig_n, RS, nrest, d0, q);
+  return res;
+}
+
 // The makers every CONS touch of level q fills (first / last in FIFO order), with its cursor and
-// level, into F.tfc at the touch's log index: binary searches over the level's makers, done here
-// where the level's maker arrays were just written (L2-hot), so the event passes read one entry
-// per touch instead of searching.  Threads tid, tid + nthr, ... of the caller take the touches.
+// level, into F.tfc at the touch's log index, where the level's maker arrays were just written
+// (L2-hot), so the event passes read one entry per touch instead of searching.  Waves w, w + nw,
+// ... of the caller take the level's touches 64 at a time.  The consumption starts at coordinate
+// 0 (maker 0) and advances, so a lone wave (nw == 1) starts each chunk's windows where the last
+// chunk's ended; interleaved waves find their chunk's first maker by one search.
 __device__ __forceinline__ void fl_level_fc(const FlowArgs& F, uint32_t L, uint32_t q, uint32_t base, uint32_t cnt,
-                                            const IgEnt* IG, uint32_t ig_n, uint32_t nrest, int64_t d0, uint32_t tid,
-                                            uint32_t nthr) {
+                                            const IgEnt* IG, uint32_t ig_n, uint32_t nrest, int64_t d0, uint32_t w,
+                                            uint32_t nw) {
   const SEnt* R = F.srt + L + base;
   const RsEnt* RS = F.rs + L + base;
-  for (uint32_t i = tid; i < cnt; i += nthr) {
-    const SEnt e = R[i];
-    if (e.kind != TK_CONS) continue;
-    const uint32_t f = fl_find(IG, ig_n, RS, nrest, d0, e.coord);
-    // most touches end inside their first maker: probe it before searching for the last
-    const int64_t xl = e.coord + e.amt - 1;
-    const int64_t fend = f < ig_n ? IG[f].e + IG[f].v : RS[f - ig_n].e + RS[f - ig_n].v;
-    FlTouchFc x;
-    x.first = f;
-    x.last = xl < fend ? f : fl_find(IG, ig_n, RS, nrest, d0, xl);
-    x.lvl = q;
-    x.pad = 0;
-    x.coord = e.coord;
-    F.tfc[L + e.t] = x;
+  const uint32_t lane = lane_id();
+  uint32_t carry = 0;  // (nw == 1) the maker the next chunk's windows start at
+  for (uint32_t i0 = w * 64; i0 < cnt; i0 += nw * 64) {
+    const uint32_t i = i0 + lane;
+    SEnt e{};
+    if (i < cnt) e = R[i];
+    const bool cons = i < cnt && e.kind == TK_CONS;
+    const unsigned long long cm = __ballot(cons);
+    if (!cm) continue;
+    const int64_t x = e.coord + e.amt - 1;
+    const int l0 = static_cast<int>(__builtin_ctzll(cm)), l1 = 63 - static_cast<int>(__builtin_clzll(cm));
+    const uint32_t b = nw == 1 ? carry : fl_find(IG, ig_n, RS, nrest, d0, __shfl(e.coord, l0));
+    const uint32_t f = fl_wave_find(IG, ig_n, RS, nrest, d0, cons, e.coord, b);
+    const uint32_t l = fl_wave_find(IG, ig_n, RS, nrest, d0, cons, x, __shfl(f, l0));
+    carry = __shfl(l, l1);
+    if (cons) {
+      FlTouchFc y;
+      y.first = f;
+      y.last = l;
+      y.lvl = q;
+      y.pad = 0;
+      y.coord = e.coord;
+      F.tfc[L + e.t] = y;
+    }
   }
 }
 
@@ -1656,7 +1701,7 @@ __device__ __forceinline__ void fl_level_one(const Dev& D, const FlowArgs& F, ui
     Lq->tslot = tslot;
     Lq->nlive0 = nv0 - consumed;
   }
-  if (fc_here && cfin > 0) fl_level_fc(F, L, q, base, cnt, F.ig + ig_base, ng, nr, d0, lane, 64);
+  if (fc_here && cfin > 0) fl_level_fc(F, L, q, base, cnt, F.ig + ig_base, ng, nr, d0, 0, 1);
 }
 
 constexpr uint32_t FL_LEVEL_T = 1024;
@@ -2503,44 +2548,59 @@ __global__ __launch_bounds__(FL_TILE) void k_flow_sort_cnt(Dev D, FlowArgs F) {
 
 // Per head book: level totals -> run bases (FlowLvl::cnt/base), then each tile's offset per
 // level (in place over the counts).
-__global__ __launch_bounds__(FL_CAP) void k_flow_sort_scan(Dev D, FlowArgs F) {
-  __shared__ uint32_t tot[FL_CAP];
-  const uint32_t hb = blockIdx.x, h = F.h0 + hb, k = threadIdx.x;
+// FL_SCAN_P threads per level, each over a contiguous range of the tiles (the hottest book has
+// ~450 tiles: one thread per level walking them all twice took 26 us on the critical path).
+constexpr uint32_t FL_SCAN_P = 8;
+__global__ __launch_bounds__(FL_CAP * FL_SCAN_P) void k_flow_sort_scan(Dev D, FlowArgs F) {
+  __shared__ uint32_t part[FL_SCAN_P][FL_CAP];
+  __shared__ uint32_t tot[FL_CAP], cnt[FL_CAP];
+  const uint32_t hb = blockIdx.x, h = F.h0 + hb, k = threadIdx.x % FL_CAP, p = threadIdx.x / FL_CAP;
   if (h >= fl_hend(D, F) || !F.hdr[h].ok || F.hdr[h].ok == FL_OK_DEEP) return;
   const uint32_t nt = F.hdr[h].ntouch, nl = F.hdr[h].nl;
   const uint32_t ntile = (nt + FL_TILE - 1) / FL_TILE;
+  const uint32_t per = (ntile + FL_SCAN_P - 1) / FL_SCAN_P, t0 = min(p * per, ntile), t1 = min(t0 + per, ntile);
   uint32_t* tc = F.tcnt + static_cast<size_t>(h) * F.maxt * FL_CAP;
   uint32_t s = 0;
-  uint32_t tl = 0;
-  for (; tl + 8 <= ntile; tl += 8) {
+  uint32_t tl = t0;
+  for (; tl + 8 <= t1; tl += 8) {
     uint32_t v[8];
 #pragma unroll
     for (int u = 0; u < 8; ++u) v[u] = tc[(tl + u) * FL_CAP + k];
 #pragma unroll
     for (int u = 0; u < 8; ++u) s += v[u];
   }
-  for (; tl < ntile; ++tl) s += tc[tl * FL_CAP + k];
-  tot[k] = s;
+  for (; tl < t1; ++tl) s += tc[tl * FL_CAP + k];
+  part[p][k] = s;
   __syncthreads();
-  if (k == 0) {
+  if (p == 0) {  // the level's parts -> their offsets within the level, and its total
     uint32_t acc = 0;
-    for (uint32_t i = 0; i < FL_CAP; ++i) { const uint32_t v = tot[i]; tot[i] = acc; acc += v; }
+    for (uint32_t q = 0; q < FL_SCAN_P; ++q) {
+      const uint32_t v = part[q][k];
+      part[q][k] = acc;
+      acc += v;
+    }
+    cnt[k] = acc;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t acc = 0;
+    for (uint32_t i = 0; i < FL_CAP; ++i) { tot[i] = acc; acc += cnt[i]; }
   }
   __syncthreads();
   const uint32_t base = tot[k];
-  if (k >= 1 && k <= nl) {
-    F.lvl[h * FL_CAP + k].cnt = s;
+  if (p == 0 && k >= 1 && k <= nl) {
+    F.lvl[h * FL_CAP + k].cnt = cnt[k];
     F.lvl[h * FL_CAP + k].base = base;
   }
-  uint32_t run = base;
-  for (tl = 0; tl + 8 <= ntile; tl += 8) {
+  uint32_t run = base + part[p][k];
+  for (tl = t0; tl + 8 <= t1; tl += 8) {
     uint32_t v[8];
 #pragma unroll
     for (int u = 0; u < 8; ++u) v[u] = tc[(tl + u) * FL_CAP + k];
 #pragma unroll
     for (int u = 0; u < 8; ++u) { tc[(tl + u) * FL_CAP + k] = run; run += v[u]; }
   }
-  for (; tl < ntile; ++tl) {
+  for (; tl < t1; ++tl) {
     const uint32_t v = tc[tl * FL_CAP + k];
     tc[tl * FL_CAP + k] = run;
     run += v;
@@ -2610,7 +2670,7 @@ __global__ __launch_bounds__(FL_LVB_T) void k_flow_level_wide(Dev D, FlowArgs F)
   const FlowLvl* Lq = F.lvl + h * FL_CAP + q;
   if (cfin > 0)
     fl_level_fc(F, FL_TOUCH_MUL * F.hdr[h].beg, q, Lq->base, Lq->cnt, F.ig + Lq->ig_base, Lq->ig_n, Lq->nrest, Lq->d0,
-                threadIdx.x, FL_LVB_T);
+                threadIdx.x >> 6, FL_LVB_T / 64);
 }
 
 }  // namespace gome

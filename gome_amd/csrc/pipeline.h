@@ -305,9 +305,40 @@ __device__ __forceinline__ unsigned long long key_so(const gome_order& g) {
 
 // Pass 1 (every record): validation (k_validate's check, folded in), the (S, oid) table, the
 // resting probe.  slot[i] := its (S, oid) slot | ADM_RESTING, or NIL (not an ADD / DEL).
+// Fresh batches (k_adm_pre): every record an ADD or an ignored action, oids strictly increasing
+// in batch order and above every oid an admitted ADD ever carried (or a loaded node holds).  No
+// (S, oid) repeats in such a batch and none rests, so each ADD's verdict is its own (admitted by
+// the batch rule, or the host's) and the tables are not touched.  Any other batch sets *notfast.
+// ctl: [0] the watermark (no oid of an earlier batch is above it), [1] not fresh, [2] this batch's
+// highest oid (folded into [0] by the next batch's k_adm_ctl: an upper bound of every oid an
+// admitted ADD ever carried, so "above it" is safe).  Launch with at most a few thousand blocks.
+__global__ void k_adm_ctl(uint32_t* ctl, uint32_t fast) {
+  ctl[0] = max(ctl[0], ctl[2]);
+  ctl[2] = 0;
+  ctl[1] = fast ? 0u : 1u;
+}
+__global__ void k_adm_pre(const gome_order* ord, uint32_t n, uint32_t* ctl) {
+  __shared__ uint32_t bmax;
+  if (threadIdx.x == 0) bmax = 0;
+  __syncthreads();
+  bool bad = false;
+  uint32_t mx = 0;
+  const uint32_t g0 = ctl[0];
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const uint32_t oid = ord[i].oid_id, prev = i ? ord[i - 1].oid_id : g0;
+    if (ord[i].action == GOME_DEL || oid <= prev) bad = true;
+    mx = max(mx, oid);
+  }
+  for (int off = 32; off > 0; off >>= 1) mx = max(mx, static_cast<uint32_t>(__shfl_xor(mx, off)));
+  if (__any(bad) && lane_id() == 0) atomicOr(&ctl[1], 1u);
+  if (lane_id() == 0) atomicMax(&bmax, mx);
+  __syncthreads();
+  if (threadIdx.x == 0 && bmax) atomicMax(&ctl[2], bmax);  // (one device atomic per block)
+}
+
 __global__ void k_adm(const gome_order* ord, uint32_t n, unsigned long long* tab, uint32_t* slot, uint32_t mask,
                       uint32_t max_symbols, Status* st, const Book* books, const IdxEnt* idx,
-                      unsigned long long idx_mask, const uint32_t* oid_max, uint8_t* multi) {
+                      unsigned long long idx_mask, const uint32_t* oid_max, uint8_t* multi, const uint32_t* notfast) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const gome_order g = ord[i];
@@ -319,6 +350,10 @@ __global__ void k_adm(const gome_order* ord, uint32_t n, unsigned long long* tab
       slot[i] = NIL;
       return;  // (the batch is rejected; nothing below may index by symbol_id)
     }
+  }
+  if (!*notfast) {  // a fresh batch: the final verdict at once (k_adm_flag .. k_adm_clean return)
+    slot[i] = g.action == GOME_ADD && (!(g.flags & GOME_ORD_ADM_HOST) || (g.flags & GOME_ORD_ADMITTED)) ? 1u : 0u;
+    return;
   }
   if (g.action != GOME_ADD && g.action != GOME_DEL) { slot[i] = NIL; return; }
   const bool resting = g.action == GOME_ADD && g.oid_id <= oid_max[g.symbol_id] && books[g.symbol_id].n_lvl != 0 &&
@@ -338,11 +373,12 @@ __global__ void k_adm(const gome_order* ord, uint32_t n, unsigned long long* tab
 // (S, oid) slot of a shared key's record, else NIL (for k_adm_clean).
 __global__ void k_adm_flag(const gome_order* ord, uint32_t n, uint32_t* slot, const uint8_t* multi,
                            unsigned long long* tab2, uint32_t* slot2, uint32_t* aux, uint32_t mask, Status* st,
-                           uint32_t* list) {
+                           uint32_t* list, unsigned long long* tab, const uint32_t* notfast) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
+  if (i >= n || !*notfast) return;
   const uint32_t s = slot[i];
   const bool shared = s != NIL && multi[s & ADM_SLOT];
+  if (s != NIL) tab[s & ADM_SLOT] = 0ull;  // (k_adm's probes are over: the table is left empty)
   aux[i] = shared ? (s & ADM_SLOT) : NIL;
   if (s == NIL) { slot[i] = 0; return; }
   const gome_order g = ord[i];
@@ -367,9 +403,9 @@ __global__ void k_adm_flag(const gome_order* ord, uint32_t n, uint32_t* slot, co
 // Pass 3 (shared keys): the batch rule / host verdict; an admitted ADD offers its index as the
 // key's first admitted ADD (first[] is NIL between batches).
 __global__ void k_adm_res(const gome_order* ord, uint32_t n, uint32_t* slot, const unsigned long long* tab2,
-                          const uint32_t* slot2, uint32_t* first) {
+                          const uint32_t* slot2, uint32_t* first, const uint32_t* notfast) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
+  if (i >= n || !*notfast) return;
   const uint32_t s = slot[i];
   if (!(s & ADM_MULTI)) return;
   const gome_order g = ord[i];
@@ -383,9 +419,10 @@ __global__ void k_adm_res(const gome_order* ord, uint32_t n, uint32_t* slot, con
 
 // Pass 4 (shared keys): final verdicts; an admitted ADD that is not its key's first admitted ADD,
 // or whose oid rests at batch start, is a duplicate.
-__global__ void k_adm_dup(uint32_t n, uint32_t* slot, const uint32_t* first, Status* st, uint32_t* list) {
+__global__ void k_adm_dup(uint32_t n, uint32_t* slot, const uint32_t* first, Status* st, uint32_t* list,
+                          const uint32_t* notfast) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
+  if (i >= n || !*notfast) return;
   const uint32_t s = slot[i];
   if (!(s & ADM_MULTI)) return;
   const bool adm = (s & ADM_OK) != 0;
@@ -396,9 +433,9 @@ __global__ void k_adm_dup(uint32_t n, uint32_t* slot, const uint32_t* first, Sta
 
 // Pass 5 (shared keys): their entries of the second table, first[] and multi[] back to empty.
 __global__ void k_adm_clean(uint32_t n, const uint32_t* aux, const uint32_t* slot2, unsigned long long* tab2,
-                            uint32_t* first, uint8_t* multi) {
+                            uint32_t* first, uint8_t* multi, const uint32_t* notfast) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
+  if (i >= n || !*notfast) return;
   const uint32_t h = aux[i];
   if (h == NIL) return;
   tab2[slot2[i]] = 0ull;

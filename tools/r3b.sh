@@ -60,6 +60,27 @@ for P in $PARTS; do
         done
       done
     done ;;
+  envab)  # A/B of an engine env knob: ENVAB="NAME" values 1 / 0, configs from ABW, alternating
+    for R in 1 2; do
+      for SP in 1 0; do
+        for W in ${ABW:-config2 config3}; do
+          env $ENVAB=$SP timeout -k 10 300 python3 -u bench.py --workload $W --steps 8 --warmup 5 --e2e-steps 0 \
+            --no-cpu-baseline > $OUT/ab${SP}_${W}_$R.jsonl 2> $OUT/ab${SP}_${W}_$R.log || { tail -20 $OUT/ab${SP}_${W}_$R.log; exit 10; }
+          python3 -c "import json; d=json.loads(open('$OUT/ab${SP}_${W}_$R.jsonl').readlines()[-1]); print('$ENVAB=$SP $W $R', d['value'], d['ms_per_step'], d['hot_book']['ns_per_order'])"
+        done
+      done
+    done ;;
+  pmc)  # FETCH_SIZE / WRITE_SIZE (KiB) and SQ occupancy counters per kernel, one pass each (workload PW)
+    W=${PW:-config2}
+    i=0
+    for grp in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR"; do
+      i=$((i+1))
+      timeout -s KILL 200 rocprofv3 --pmc $grp --output-format csv -d $OUT/pmc$i -o run -- python3 bench.py --workload $W \
+        --steps 3 --warmup 2 --e2e-steps 0 --no-cpu-baseline > $OUT/pmc$i.log 2>&1 || { echo "pmc pass $i failed"; exit 11; }
+    done
+    python3 tools/pmc_kernels.py $OUT/pmc1/run_counter_collection.csv $OUT/pmc2/run_counter_collection.csv > $OUT/pmc_bytes.txt
+    python3 tools/pmc_kernels.py $OUT/pmc3/run_counter_collection.csv > $OUT/pmc_sq.txt
+    head -20 $OUT/pmc_bytes.txt ;;
   esac
 done
 echo done

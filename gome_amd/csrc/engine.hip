@@ -47,19 +47,28 @@ using namespace gome;
 // ============================================================== event compaction
 // Arena events -> publish positions; the sequence number is seq_base + the batch index
 // (gome_event.taker_seq / seq_hi, ABI >= 4).
+// Four lanes per 64-B event, 16 B each: a wave reads 1 KiB of the arena per load instruction and
+// writes each event as one whole line (a lane per event read and wrote 64 separate 16-B pieces per
+// instruction).  Quarter 2 holds taker_seq and fill_idx, quarter 3 seq_hi.
 __global__ void k_ev_scatter(const gome_event* arena, uint32_t cap, const Status* st,
                              const uint32_t* ev_off, gome_event* out, unsigned long long seq_base) {
   const uint32_t used = min(st->ev_bump, cap);
-  for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < used; j += gridDim.x * blockDim.x) {
-    gome_event e = arena[j];
-    if (e.taker_seq == NIL) continue;
-    const uint32_t idx = e.taker_seq;
+  const uint32_t qt = threadIdx.x & 3u;
+  const uint4* src = reinterpret_cast<const uint4*>(arena);
+  uint4* dst = reinterpret_cast<uint4*>(out);
+  for (uint32_t j = (blockIdx.x * blockDim.x + threadIdx.x) >> 2; j < used; j += (gridDim.x * blockDim.x) >> 2) {
+    uint4 v = src[4ull * j + qt];
+    const uint32_t idx = __shfl(v.x, static_cast<int>((threadIdx.x & ~3u) | 2u) & 63);   // taker_seq
+    const uint32_t fi = __shfl(v.y, static_cast<int>((threadIdx.x & ~3u) | 2u) & 63);    // fill_idx
+    if (idx == NIL) continue;
     const unsigned long long sq = seq_base + idx;
-    e.taker_seq = static_cast<uint32_t>(sq);
-    e.seq_hi = static_cast<uint32_t>(sq >> 32);
-    out[ev_off[idx] + e.fill_idx] = e;
+    if (qt == 2) v.x = static_cast<uint32_t>(sq);
+    if (qt == 3) v.w = static_cast<uint32_t>(sq >> 32);
+    dst[4ull * (ev_off[idx] + fi) + qt] = v;
   }
 }
+static_assert(offsetof(gome_event, taker_seq) == 32 && offsetof(gome_event, fill_idx) == 36 &&
+              offsetof(gome_event, seq_hi) == 60 && sizeof(gome_event) == 64, "k_ev_scatter's quarters");
 
 // Freed FIFO chunks of this batch -> free pool (two kernels: copy, then counters).
 __global__ void k_recycle_copy(Dev D) {
@@ -825,7 +834,7 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
       HIPCHK(hipEventRecord(cnt_fork, st));
       HIPCHK(hipStreamWaitEvent(cs, cnt_fork, 0));
     }
-    if (!fused) k_flow_count<<<1024, 256, 0, cs>>>(D, B, R);
+    if (!fused) k_flow_count_fused<<<1024, FL_EV_T, 0, cs>>>(D, B, R);
     if (split) {  // (the publish scan waits for the count, the batch's end for the deep writes)
       HIPCHK(hipEventRecord(cnt_done, cs));
       if (c_deep) deep_write(R, cs);  // (after the count, which reads neither the claims nor the writes)

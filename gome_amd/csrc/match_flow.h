@@ -1395,8 +1395,11 @@ __global__ __launch_bounds__(FL_SORT_T) void k_flow_sort(Dev D, FlowArgs F) {
       const uint32_t pos = wc[w][k] + rank;
       e.amt = static_cast<int64_t>(static_cast<unsigned long long>(x.amt) * g);  // plan units -> fixed point
       F.srt[L + pos] = e;
-      F.log[L + t].pos = pos;
-      if (g != 1) F.log[L + t].amt = e.amt;
+      if (cb) {  // (the cancel kernels read the run position and fixed-point amounts from the log;
+                 // the ADD books' event kernels scale the plan units themselves: fl_amt_unit)
+        F.log[L + t].pos = pos;
+        if (g != 1) F.log[L + t].amt = e.amt;
+      }
     }
     __syncthreads();
     for (uint32_t i = tid; i < FL_SORT_W * FL_CAP; i += FL_SORT_T) wc[i / FL_CAP][i % FL_CAP] = 0;
@@ -1581,7 +1584,20 @@ __device__ __forceinline__ void fl_level_one(const Dev& D, const FlowArgs& F, ui
     cc = pre_cfin;
     nr = pre_nr;
   }
-  for (uint32_t c0 = 0; pre_cfin < 0 && c0 < cnt; c0 += 64) {
+  // a lone wave with the fill contexts (fl_level_fc) to make: the level's total consumption first
+  // (the old makers' gather needs it), then one scan that writes the new makers and the contexts
+  // from registers (no cursor round trip through the sorted runs)
+  const bool fused_fc = fc_here && pre_cfin < 0;
+  if (fused_fc) {
+    int64_t sc = 0;
+    for (uint32_t c0 = 0; c0 < cnt; c0 += 64) {
+      const uint32_t i = c0 + lane;
+      if (i < cnt && R[i].kind == TK_CONS) sc += R[i].amt;
+    }
+    for (int off = 32; off > 0; off >>= 1) sc += __shfl_xor(sc, off);
+    cc = sc;
+  }
+  for (uint32_t c0 = 0; pre_cfin < 0 && !fused_fc && c0 < cnt; c0 += 64) {
     const uint32_t i = c0 + lane;
     const bool valid = i < cnt;
     SEnt e{};
@@ -1689,6 +1705,50 @@ __device__ __forceinline__ void fl_level_one(const Dev& D, const FlowArgs& F, ui
       hslot = nhs;
     }
   }
+  if (fused_fc) {  // the scan: new makers, and each CONS touch's makers (old ones: IG, complete)
+    const IgEnt* IG = F.ig + ig_base;
+    int64_t c1 = 0;
+    uint32_t carry = 0;
+    for (uint32_t c0 = 0; c0 < cnt; c0 += 64) {
+      const uint32_t i = c0 + lane;
+      const bool valid = i < cnt;
+      SEnt e{};
+      if (valid) e = R[i];
+      const bool isc = valid && e.kind == TK_CONS, isr = valid && e.kind == TK_REST;
+      const int64_t ac = isc ? e.amt : 0, ar = isr ? e.amt : 0;
+      const int64_t ic = wave_incl_scan(ac), ir = wave_incl_scan(ar);
+      const unsigned long long rm = __ballot(isr), cm = __ballot(isc);
+      if (isr) {
+        RsEnt x;
+        x.e = rr + ir - ar;
+        x.v = e.amt;
+        x.j = e.j;
+        x.t = e.t;
+        x.pad0 = x.pad1 = 0;
+        RS[nr + __popcll(rm & ltm)] = x;
+      }
+      nr += __popcll(rm);
+      rr += rl64(ir, 63);
+      if (cm) {  // (a consume fills makers that rested before it: up to this chunk's, written above)
+        __threadfence_block();
+        const int64_t c = c1 + ic - ac, x = c + ac - 1;
+        const int l0 = static_cast<int>(__builtin_ctzll(cm)), l1 = 63 - static_cast<int>(__builtin_clzll(cm));
+        const uint32_t f = fl_wave_find(IG, ng, RS, nr, d0, isc, c, carry);
+        const uint32_t l = fl_wave_find(IG, ng, RS, nr, d0, isc, x, __shfl(f, l0));
+        carry = __shfl(l, l1);
+        if (isc) {
+          FlTouchFc y;
+          y.first = f;
+          y.last = l;
+          y.lvl = q;
+          y.pad = 0;
+          y.coord = c;
+          F.tfc[L + e.t] = y;
+        }
+      }
+      c1 += rl64(ic, 63);
+    }
+  }
   if (lane == 0) {
     Lq->cfin = cfin;
     Lq->nrest = nr;
@@ -1701,7 +1761,6 @@ __device__ __forceinline__ void fl_level_one(const Dev& D, const FlowArgs& F, ui
     Lq->tslot = tslot;
     Lq->nlive0 = nv0 - consumed;
   }
-  if (fc_here && cfin > 0) fl_level_fc(F, L, q, base, cnt, F.ig + ig_base, ng, nr, d0, 0, 1);
 }
 
 constexpr uint32_t FL_LEVEL_T = 1024;
@@ -1720,6 +1779,12 @@ struct FlTouchCtx {
   uint32_t first, last;
 };
 
+// The fixed-point value of one plan unit in book h's log: a lane ADD book's log keeps the plan's
+// units (its sort leaves the log alone); deep and cancel books' logs were converted.
+__device__ __forceinline__ int64_t fl_amt_unit(const FlowArgs& F, uint32_t h) {
+  return F.hdr[h].ok == FL_OK_ADD ? static_cast<int64_t>(F.hdr[h].g) : 1;
+}
+
 // CONS touch t (log index) of book h: its level and the makers it fills (fl_level_fc).
 __device__ __forceinline__ FlTouchCtx fl_touch_ctx(const FlowArgs& F, uint32_t h, uint32_t L, const Touch& x, uint32_t t) {
   FlTouchCtx c;
@@ -1728,7 +1793,7 @@ __device__ __forceinline__ FlTouchCtx fl_touch_ctx(const FlowArgs& F, uint32_t h
   c.IG = F.ig + c.Lq->ig_base;
   c.RS = F.rs + L + c.Lq->base;
   c.c = tf.coord;
-  c.a = x.amt;
+  c.a = x.amt * fl_amt_unit(F, h);
   c.first = tf.first;
   c.last = tf.last;
   return c;
@@ -1892,7 +1957,7 @@ __device__ __forceinline__ void fl_events(const Dev& D, const BatchArgs& B, cons
     for (uint32_t u = t; u > 0; --u) {
       const Touch y = F.log[L + u - 1];
       if (tk_j(y) != tk_j(x)) break;
-      tb -= y.amt;
+      tb -= y.amt * fl_amt_unit(F, h);
     }
     const uint32_t ig_n = c.Lq->ig_n, nrest = c.Lq->nrest, ig_all = c.Lq->ig_all;
     const int64_t price = c.Lq->price;
@@ -1978,7 +2043,9 @@ __device__ __forceinline__ T wave_seg_incl(T v, unsigned long long heads) {
 // over the touches (a wave's first lane walks back into an order begun before the wave); the
 // order's last touch writes ev_count[taker].
 // Blocks bid of nblk, T threads each.
-template <uint32_t T>
+// COUNT: the hottest book's count pass (its events are written after the publish scan, straight to
+// their positions, by k_flow_events): each touch's fill_idx base to F.fbase, ev_count, no arena.
+template <uint32_t T, bool COUNT = false>
 __device__ __forceinline__ void fl_events_fused(const Dev& D, const BatchArgs& B, const FlowArgs& F, uint32_t bid,
                                                 uint32_t nblk) {
   const uint32_t hend = fl_hend(D, F), nb = hend > F.h0 ? hend - F.h0 : 0u;
@@ -1990,6 +2057,7 @@ __device__ __forceinline__ void fl_events_fused(const Dev& D, const BatchArgs& B
     const uint32_t gt = b0 + threadIdx.x, g0w = b0 + (threadIdx.x & ~63u);
     const bool valid = gt < total;
     uint32_t h = 0, L = 0, t = 0, nt = 0, beg = 0, j = 0, cnt = 0;
+    int64_t gm = 1;
     Touch x{};
     FlTouchCtx c{};
     bool first = true, last = true;
@@ -1998,6 +2066,7 @@ __device__ __forceinline__ void fl_events_fused(const Dev& D, const BatchArgs& B
       if (valid) {
         h = F.h0 + hb;
         t = gt - F.toff[F.tb + hb];
+        gm = fl_amt_unit(F, h);
         nt = F.hdr[h].ntouch;
         beg = F.hdr[h].beg;
         L = FL_TOUCH_MUL * beg;
@@ -2023,7 +2092,7 @@ __device__ __forceinline__ void fl_events_fused(const Dev& D, const BatchArgs& B
       for (uint32_t u = t; u > 0; --u) {
         const Touch y = F.log[L + u - 1];
         if (tk_j(y) != j) break;
-        carry_a += y.amt;
+        carry_a += y.amt * gm;
         if (((y.kr >> 7) & 1u) == TK_CONS) {
           const FlTouchCtx cy = fl_touch_ctx(F, h, L, y, u - 1);
           carry_n += cy.last - cy.first + 1;
@@ -2034,10 +2103,15 @@ __device__ __forceinline__ void fl_events_fused(const Dev& D, const BatchArgs& B
     carry_n = __shfl(carry_n, 0);
     carry_a = __shfl(carry_a, 0);
     const uint32_t n_incl = wave_seg_incl<uint32_t>(cnt, heads) + (in_first_seg ? carry_n : 0u);
-    const int64_t a_incl = wave_seg_incl<int64_t>(valid ? x.amt : 0, heads) + (in_first_seg ? carry_a : 0);
+    const int64_t xa = valid ? x.amt * gm : 0;  // (plan units -> fixed point: fl_amt_unit)
+    const int64_t a_incl = wave_seg_incl<int64_t>(xa, heads) + (in_first_seg ? carry_a : 0);
     const uint32_t fb = n_incl - cnt;  // the touch's fill_idx base within its order
-    const int64_t a_before = a_incl - (valid ? x.amt : 0);
+    const int64_t a_before = a_incl - xa;
     if (valid && last && j < F.hdr[h].end - beg) B.ev_count[B.prep[beg + j].idx] = n_incl;  // (not padding)
+    if (COUNT) {
+      if (valid) F.fbase[L + t] = fb;
+      continue;
+    }
     // arena slots: one bump allocation per block tile
     uint32_t inc = cnt;
     for (uint32_t off = 1; off < 64; off <<= 1) {
@@ -2123,6 +2197,9 @@ __device__ __forceinline__ void fl_events_fused(const Dev& D, const BatchArgs& B
 }
 __global__ __launch_bounds__(FL_EV_T) void k_flow_events_fused(Dev D, BatchArgs B, FlowArgs F) {
   fl_events_fused<FL_EV_T>(D, B, F, blockIdx.x, gridDim.x);
+}
+__global__ __launch_bounds__(FL_EV_T) void k_flow_count_fused(Dev D, BatchArgs B, FlowArgs F) {
+  fl_events_fused<FL_EV_T, true>(D, B, F, blockIdx.x, gridDim.x);
 }
 
 // ============================================================== k_flow_write
@@ -2647,8 +2724,10 @@ __global__ __launch_bounds__(FL_TILE) void k_flow_sort_scatter(Dev D, FlowArgs F
       e.lvl = k;
       const uint32_t pos = wc[w][k] + rank;
       F.srt[L + pos] = e;
-      F.log[L + t].pos = pos;
-      if (g != 1) F.log[L + t].amt = e.amt;
+      if (cb) {  // (as k_flow_sort)
+        F.log[L + t].pos = pos;
+        if (g != 1) F.log[L + t].amt = e.amt;
+      }
     }
     __syncthreads();
     // stale wc entries of levels absent from the next tile are never read: only a wave's

@@ -256,6 +256,8 @@ def main():
     ap.add_argument("--pool-nodes", type=int, default=0, help="gome_config.max_nodes (0: sized from the run)")
     ap.add_argument("--pool-levels", type=int, default=0, help="gome_config.max_levels (0: sized from the run)")
     ap.add_argument("--step-log", default="", help="write each timed step's engine counters (JSONL)")
+    ap.add_argument("--no-phase-pass", action="store_true",
+                    help="skip the untimed replay with per-phase timing events (kernel_ms of the phases)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="PMC-measured HBM bytes per launch of the dominant kernel (optional)")
     args = ap.parse_args()
@@ -373,13 +375,6 @@ def main():
     }
     if sum(s["n_flow_books"] for s in sts) == 0:
         cands.pop("k_flow_plan_head")
-    # the other phases of the pipeline (the tail's chain, the sort, admission, publishing): with
-    # no hot symbol (config 2) one of them is the longest
-    per = [phase_candidates(s) for s in sts]
-    for k in per[0]:
-        cands[k] = (sum(p[k][0] for p in per) / steps, sum(p[k][1] for p in per) / steps, per[0][k][2])
-    kname = max(cands, key=lambda k: cands[k][0])
-    ms_dom, bdom, kdesc = cands[kname]
     max_seg = max(s["max_segment"] for s in sts)
     digest_check = None
     if world > 1:
@@ -445,6 +440,32 @@ def main():
                        "pipeline -> gome_collect (events D2H into page-locked memory); batch k+1's "
                        "H2D and batch k-1's D2H overlap batch k"}
 
+    # ---- the other phases of the pipeline (the tail's chain, the sort, admission, publishing):
+    # with no hot symbol (config 2) one of them is the longest.  Their device times need ~24
+    # timing-event records per batch (GOME_FLAG_PHASES, 0.12 ms of config 2's batch), so they
+    # come from an untimed replay of the same batches on a fresh engine, never from the timed
+    # steps above; rank 0 only (no collective inside).
+    phase_src = None
+    if rank == 0 and not args.no_phase_pass:
+        from gome_amd.abi import GOME_FLAG_PHASES
+        note("phase pass (untimed replay with per-phase timing events)")
+        cfg = dict(eng.cfg_kwargs)
+        eng.close()
+        eng = Engine(**dict(cfg, flags=cfg.get("flags", 0) | GOME_FLAG_PHASES))
+        sq, per = 0, []
+        for i in range(warm + steps):
+            eng.submit_device(dev_batches[i].data_ptr(), per_rank, seq_base=sq)
+            sq += per_rank
+            eng.release_device_events()
+            if i >= warm:
+                per.append(phase_candidates(eng.stats()))
+        for k in per[0]:
+            cands[k] = (sum(p[k][0] for p in per) / steps, sum(p[k][1] for p in per) / steps, per[0][k][2])
+        phase_src = (f"k_flow_plan_head / k_match_hot / k_match: the timed steps; the other phases: an "
+                     f"untimed replay of the same {warm + steps} batches with GOME_FLAG_PHASES")
+    kname = max(cands, key=lambda k: cands[k][0])
+    ms_dom, bdom, kdesc = cands[kname]
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         thr = max(1, min(args.cpu_threads, os.cpu_count() or 1))
@@ -498,6 +519,7 @@ def main():
             "host_enqueue_ms": round(sum(s["ms_host_enqueue"] for s in sts) / steps, 3),
             "match_books_ms": round(ms_match, 3),
             "kernel_ms": {k: round(v[0], 3) for k, v in sorted(cands.items(), key=lambda kv: -kv[1][0])},
+            "kernel_ms_source": phase_src,
             "hot_book": {"orders_per_batch": int(max_seg), "top_symbol_share": round(top_share, 5),
                          "ns_per_order": round(cands.get("k_flow_plan_head", cands["k_match_hot"])[0] * 1e6
                                                / max(max_seg, 1), 1),

@@ -22,6 +22,7 @@ GOME_FLAG_LEGACY_HOT = 1  # gome_config.flags: hot books on the legacy FIFO kern
 GOME_FLAG_NO_HEADROOM = 2  # gome_config.flags: no pool-headroom check before a submit
 GOME_FLAG_CHAINS_ALWAYS = 4  # gome_config.flags: enqueue the deep / cancel chains on every batch
 GOME_FLAG_CHAINS_NEVER = 8  # gome_config.flags: never (deep books and books with DELs: legacy / cold)
+GOME_FLAG_PHASES = 16  # gome_config.flags: record the per-phase timing events (gome_stats.ms_phase)
 GOME_ORD_ADM_HOST, GOME_ORD_ADMITTED = 1, 2  # gome_order.flags: host-resolved admission (ABI 4)
 GOME_MAX_INFLIGHT = 2
 
@@ -236,6 +237,9 @@ class Engine:
             raise GomeError(s, self.lib.gome_last_error(None).decode())
         self.h = h
         self.max_batch = max_batch
+        self.cfg_kwargs = dict(max_symbols=max_symbols, max_batch=max_batch, max_nodes=max_nodes,
+                               max_levels=max_levels, accuracy=accuracy, device=device,
+                               max_events=max_events, flags=flags)
 
     def close(self):
         if getattr(self, "h", None):

@@ -232,7 +232,10 @@ struct gome_engine {
   // faster on config 2, but the split events kernel's traffic slows a concurrent hottest-book
   // plan (config 3: +0.2 ms), so with a hot book the fused launch (GOME_TAIL_SPLIT=0/1 forces)
   int tail_split = -1;
-  bool adm_fast = true;  // k_adm_pre's fresh-batch test (GOME_ADM_FAST=0: every batch through the tables; A/B)
+  bool adm_fast = true;
+  // GOME_PH_* timing events (gome_stats.ms_phase): ~24 event records per batch, 0.12 ms on config 2's
+  // critical path, so only on request (GOME_FLAG_PHASES, or GOME_PHASES=1)
+  bool phases = false;  // k_adm_pre's fresh-batch test (GOME_ADM_FAST=0: every batch through the tables; A/B)
   uint64_t last_maxseg = 0, last_n = 0;  // the last finished batch's hottest book / size
   uint32_t hist_cap = 0, bsum_cap = 0;
   unsigned long long idx_cap = 0;
@@ -409,6 +412,8 @@ gome_status gome_engine::init(const gome_config& c) {
   if (const char* g = std::getenv("GOME_TAIL_GRID")) tail_grid = std::max(64, std::atoi(g));  // (tuning)
   if (const char* g = std::getenv("GOME_TAIL_SPLIT")) tail_split = std::atoi(g) != 0 ? 1 : 0;  // (A/B)
   if (const char* g = std::getenv("GOME_ADM_FAST")) adm_fast = std::atoi(g) != 0;              // (A/B)
+  phases = (cfg.flags & GOME_FLAG_PHASES) != 0;
+  if (const char* g = std::getenv("GOME_PHASES")) phases = std::atoi(g) != 0;
   uint32_t ms = cfg.max_symbols;
   key_bits = (ms <= 1) ? 1 : 32 - __builtin_clz(ms - 1);
   passes = (key_bits + RS_MAXBITS - 1) / RS_MAXBITS;
@@ -595,6 +600,7 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   for (bool& on : S.ph_on) on = false;
   // GOME_PH_* brackets (gome_stats.ms_phase): one event pair per phase on its stream
   auto mark = [&](int ph, int end, hipStream_t st) -> hipError_t {
+    if (!phases) return hipSuccess;
     S.ph_on[ph] = true;
     return hipEventRecord(S.ph[ph][end], st);
   };

@@ -156,6 +156,9 @@ typedef struct gome_node {
 #define GOME_FLAG_CHAINS_ALWAYS 4u
 #define GOME_FLAG_CHAINS_NEVER 8u
 #define GOME_CHAIN_QUIET 4u
+/* gome_stats.ms_phase (per-phase device times) needs ~24 timing-event records per batch on the
+ * pipeline's streams (0.12 ms per config-2 batch); they are recorded only with this flag. */
+#define GOME_FLAG_PHASES 16u
 
 typedef struct gome_config {
   uint32_t accuracy;       /* gomengine.accuracy (config.yaml.example:23-24), default 8 */
@@ -222,7 +225,8 @@ typedef struct gome_stats {
                                                  duplicate-oid rule (ABI >= 5; also counted
                                                  in n_dropped)                           */
   uint64_t n_flow_tail_fills;                 /* fills of the tail's flow books (ABI >= 5) */
-  double ms_phase[GOME_NPHASE];               /* GOME_PH_* device times (ABI >= 5)        */
+  double ms_phase[GOME_NPHASE];               /* GOME_PH_* device times (ABI >= 5; 0 unless
+                                                 GOME_FLAG_PHASES, ABI >= 6)              */
   double ms_host_enqueue;                     /* host wall time the batch's launches took
                                                  (ABI >= 5): the GPU cannot finish before
                                                  the last one is issued                  */

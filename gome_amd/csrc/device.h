@@ -127,7 +127,20 @@ struct Dev {
   uint32_t* lvl_free;        // per class c: free stack at lvl_cls_off[c] (level-block bases)
   uint32_t* lvl_freed;       // per class c: blocks released this batch
   const uint32_t* lvl_cls_off;  // [LVL_NCLS + 1] offsets; class c holds lvl_cls_off[c+1]-off[c]
+  unsigned long long* ctr_s;    // [CTR_STRIPES][CTR_STRIDE] striped batch counters (ctr_add)
 };
+
+// The batch counters are added by thousands of waves.  Device-scope atomics on one address (or
+// one cache line) serialise -- 64k of them cost ~0.3 ms on the tail's event pass -- so the adds
+// go to one of CTR_STRIPES 256-B stripes (by workgroup) and k_ctr_fold sums the stripes into
+// Status::ctr at the batch's end (and zeroes them).  Counters a kernel reads back during the
+// batch (C_DUP: a list index; C_MAXSEG: atomicMax) stay on Status.
+constexpr uint32_t CTR_STRIPES = 64, CTR_STRIDE = 32;
+static_assert(C_NCTR <= CTR_STRIDE, "one stripe holds every counter");
+__device__ __forceinline__ void ctr_add(const Dev& D, uint32_t c, unsigned long long v) {
+  const uint32_t s = (blockIdx.x + 13u * blockIdx.y) & (CTR_STRIPES - 1);
+  atomicAdd(&D.ctr_s[s * CTR_STRIDE + c], v);
+}
 
 __device__ __forceinline__ uint32_t lvl_cls(uint32_t cap) { return (31u - __clz(cap)) - 4u; }
 

@@ -86,6 +86,18 @@ __global__ void k_recycle_fin(Dev D) {
 }
 
 // Level blocks released this batch -> their class's free stack (block c = class c).
+// Batch end: the striped counters (ctr_add) into Status::ctr, the stripes zeroed for the next batch.
+__global__ void k_ctr_fold(Dev D) {
+  const uint32_t c = threadIdx.x;
+  if (c >= C_NCTR) return;
+  unsigned long long v = 0;
+  for (uint32_t k = 0; k < CTR_STRIPES; ++k) {
+    v += D.ctr_s[k * CTR_STRIDE + c];
+    D.ctr_s[k * CTR_STRIDE + c] = 0;
+  }
+  D.st->ctr[c] += v;
+}
+
 __global__ __launch_bounds__(256) void k_lvl_recycle(Dev D) {
   const uint32_t c = blockIdx.x;
   const int top = max(D.st->lvl_free_top[c], 0);
@@ -232,6 +244,8 @@ struct gome_engine {
   // faster on config 2, but the split events kernel's traffic slows a concurrent hottest-book
   // plan (config 3: +0.2 ms), so with a hot book the fused launch (GOME_TAIL_SPLIT=0/1 forces)
   int tail_split = -1;
+  bool tail_serial = false;
+  uint32_t ev_xp = 0;  // the split tail's events after its writes on one stream (solo kernel times)
   bool adm_fast = true;
   // GOME_PH_* timing events (gome_stats.ms_phase): ~24 event records per batch, 0.12 ms on config 2's
   // critical path, so only on request (GOME_FLAG_PHASES, or GOME_PHASES=1)
@@ -411,6 +425,8 @@ gome_status gome_engine::init(const gome_config& c) {
   max_batch = cfg.max_batch;
   if (const char* g = std::getenv("GOME_TAIL_GRID")) tail_grid = std::max(64, std::atoi(g));  // (tuning)
   if (const char* g = std::getenv("GOME_TAIL_SPLIT")) tail_split = std::atoi(g) != 0 ? 1 : 0;  // (A/B)
+  if (const char* g = std::getenv("GOME_TAIL_SERIAL")) tail_serial = std::atoi(g) != 0;         // (profiling)
+  if (const char* g = std::getenv("GOME_EV_XP")) ev_xp = static_cast<uint32_t>(std::atoi(g));     // (profiling)
   if (const char* g = std::getenv("GOME_ADM_FAST")) adm_fast = std::atoi(g) != 0;              // (A/B)
   phases = (cfg.flags & GOME_FLAG_PHASES) != 0;
   if (const char* g = std::getenv("GOME_PHASES")) phases = std::atoi(g) != 0;
@@ -442,7 +458,8 @@ gome_status gome_engine::init(const gome_config& c) {
       !alloc(&D.freed_ids, nchunks, "freed_ids") || !alloc(&D.idx, idx_cap, "index") ||
       !alloc(&d_st, 1, "status") || !alloc(&D.lvl_free, cls_off[LVL_NCLS], "level-block free lists") ||
       !alloc(&D.lvl_freed, cls_off[LVL_NCLS], "level-block release lists") ||
-      !alloc(&d_cls_off, LVL_NCLS + 1, "level-block classes"))
+      !alloc(&d_cls_off, LVL_NCLS + 1, "level-block classes") ||
+      !alloc(&D.ctr_s, CTR_STRIPES * CTR_STRIDE, "counter stripes"))
     return GOME_E_CAPACITY;
   D.lvl_cls_off = d_cls_off;
   D.max_symbols = ms;
@@ -456,6 +473,7 @@ gome_status gome_engine::init(const gome_config& c) {
   HIPCHK(hipMemsetAsync(D.ch_bump, 0, 4, stream));
   HIPCHK(hipMemsetAsync(D.idx, 0, sizeof(IdxEnt) * idx_cap, stream));
   HIPCHK(hipMemsetAsync(d_st, 0, sizeof(Status), stream));
+  HIPCHK(hipMemsetAsync(D.ctr_s, 0, 8ull * CTR_STRIPES * CTR_STRIDE, stream));
 
   // ---- per-batch buffers
   const uint32_t nb = max_batch;
@@ -687,6 +705,7 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   const bool c_deep = (ch & FL_CH_DEEP) != 0, c_canc = (ch & FL_CH_CANCEL) != 0;
   S.chains = ch;
   F.chains = ch;
+  F.xp = ev_xp;
   const bool split_tail = tail_split >= 0 ? tail_split != 0 : last_maxseg * 16 < last_n;
   FlowArgs FH = F, FH0 = F, FH1 = F, FT = F;
   FH.h0 = 0; FH.h1 = FL_HEAD; FH.tb = 0;
@@ -906,6 +925,7 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
     if (split_tail) {
       HIPCHK(hipEventRecord(tl_done, s));  // (the events run on the hot stream, below)
       k_flow_write<<<nh_tail, FL_WRITE_T, 0, s>>>(D, B, FT);
+      if (tail_serial) k_flow_events_fused_w<<<ceil_div(tail_grid * FL_EV_T, FL_WRITE_T), FL_WRITE_T, 0, s>>>(D, B, FT);
     } else {
       k_flow_write_events<<<nh_tail + ceil_div(tail_grid * FL_EV_T, FL_WRITE_T), FL_WRITE_T, 0, s>>>(D, B, FT, nh_tail);
     }
@@ -939,9 +959,9 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   k_pend_apply<<<dim3(8, 64), 256, 0, hot_stream>>>(D, d_pend, d_seg_start, d_seg_order, B);
   // oid watermarks for the next batches' duplicate-oid probe (the hot stream has slack here)
   k_oid_max<<<gN, T256, 0, hot_stream>>>(n, skeys, d_prep, d_oid_max);
-  if (nh_tail && split_tail) {  // the tail's events beside its writes (arena; k_ev_scatter places them)
+  if (nh_tail && split_tail && !tail_serial) {  // the tail's events beside its writes (arena; k_ev_scatter places them)
     HIPCHK(hipStreamWaitEvent(hot_stream, tl_done, 0));
-    k_flow_events_fused<<<tail_grid, FL_EV_T, 0, hot_stream>>>(D, B, FT);
+    k_flow_events_fused_w<<<ceil_div(tail_grid * FL_EV_T, FL_WRITE_T), FL_WRITE_T, 0, hot_stream>>>(D, B, FT);
   }
   HIPCHK(hipEventRecord(join, hot_stream));
   // (the hot stream's own work ended long before the hottest book's plan does)
@@ -955,6 +975,7 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   HIPCHK(hipStreamWaitEvent(s, cnt_done, 0));
 
   HIPCHK(hipEventRecord(S.evm1, s));
+  if (ev_xp & 2u) HIPCHK(hipMemsetAsync(&d_st->ev_bump, 0, 4, s));  // (experiment: nothing was written)
 
   // ---- event compaction into publish order
   HIPCHK(mark(GOME_PH_PUBLISH, 0, s));
@@ -971,6 +992,7 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   k_recycle_copy<<<256, 256, 0, s>>>(D);
   k_recycle_fin<<<1, 64, 0, s>>>(D);
   k_lvl_recycle<<<LVL_NCLS, 256, 0, s>>>(D);
+  k_ctr_fold<<<1, 64, 0, s>>>(D);
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(S.ev1, s));
   HIPCHK(hipMemcpyAsync(S.h_st, d_st, sizeof(Status), hipMemcpyDeviceToHost, s));

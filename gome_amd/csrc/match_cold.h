@@ -705,15 +705,14 @@ __device__ __forceinline__ void wave_flush(WaveCtx& W) {
   pool_publish(W, 0, W.npool);
   W.npool = 0;
   if (lane_id() == 0) {
-    unsigned long long* c = W.D.st->ctr;
-    if (W.fills) atomicAdd(&c[C_FILLS], W.fills);
-    if (W.cancels) atomicAdd(&c[C_CANCELS], W.cancels);
-    if (W.rests) atomicAdd(&c[C_RESTS], W.rests);
-    if (W.dropped) atomicAdd(&c[C_DROPPED], W.dropped);
-    if (W.adds) atomicAdd(&c[C_ADD], W.adds);
-    if (W.dels) atomicAdd(&c[C_DEL], W.dels);
-    if (W.resting_delta) atomicAdd(&c[C_RESTING_DELTA], static_cast<unsigned long long>(W.resting_delta));
-    if (W.levels_delta) atomicAdd(&c[C_LEVELS_DELTA], static_cast<unsigned long long>(W.levels_delta));
+    if (W.fills) ctr_add(W.D, C_FILLS, W.fills);
+    if (W.cancels) ctr_add(W.D, C_CANCELS, W.cancels);
+    if (W.rests) ctr_add(W.D, C_RESTS, W.rests);
+    if (W.dropped) ctr_add(W.D, C_DROPPED, W.dropped);
+    if (W.adds) ctr_add(W.D, C_ADD, W.adds);
+    if (W.dels) ctr_add(W.D, C_DEL, W.dels);
+    if (W.resting_delta) ctr_add(W.D, C_RESTING_DELTA, static_cast<unsigned long long>(W.resting_delta));
+    if (W.levels_delta) ctr_add(W.D, C_LEVELS_DELTA, static_cast<unsigned long long>(W.levels_delta));
   }
 }
 

@@ -211,6 +211,7 @@ struct FlowArgs {
   // the chains this batch enqueued (FL_CH_*): a candidate that needs one that is not there is
   // declined to the legacy / cold kernels (and counted in C_WANT_*, which re-enables it)
   uint32_t chains;
+  uint32_t xp;  // (profiling experiments, GOME_EV_XP; 0 in the product)
   // the candidates [h0, min(h1, nhot)) this launch covers (head and tail run on their own
   // streams), and the range's offset in toff
   uint32_t h0, h1, tb;
@@ -402,7 +403,7 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep(Dev D, BatchArgs B, Flo
       // too many levels for the lanes: a deep book if a deep slot is free (match_flow_deep.h)
       uint32_t slot = NIL;
       const bool want = !bad && bk.n_lvl <= DEEP_CAP - 2;
-      if (want) atomicAdd(&D.st->ctr[C_WANT_DEEP], 1ull);
+      if (want) ctr_add(D, C_WANT_DEEP, 1ull);
       if (want && (F.chains & FL_CH_DEEP)) {
         const uint32_t t = atomicAdd(F.dslot_n, 1u);
         if (t < F.dslots - FL_HEAD) slot = FL_HEAD + t;
@@ -495,7 +496,7 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep(Dev D, BatchArgs B, Flo
   }
   if (tid == 0) {
     FlowHdr x{};
-    if (dels) atomicAdd(&D.st->ctr[C_WANT_CANC], 1ull);
+    if (dels) ctr_add(D, C_WANT_CANC, 1ull);
     x.ok = dels ? ((F.chains & FL_CH_CANCEL) ? FL_OK_CANCEL : 0u) : FL_OK_ADD;
     x.nl = n;
     x.sym = sym;
@@ -719,7 +720,7 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep_b(Dev D, BatchArgs B, F
     const bool many = P->many || bk.n_lvl > FL_MAX;
     // more levels than lanes: the deep plan's candidate (match_flow_deep.h re-checks the rest)
     deepc = (!base_bad && many && bk.n_lvl <= DEEP_CAP - 2) ? 1u : 0u;
-    if (deepc) atomicAdd(&D.st->ctr[C_WANT_DEEP], 1ull);
+    if (deepc) ctr_add(D, C_WANT_DEEP, 1ull);
     if (!(F.chains & FL_CH_DEEP)) deepc = 0;
     bad = (base_bad || many) ? 1u : 0u;
   }
@@ -769,7 +770,7 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep_b(Dev D, BatchArgs B, F
     if (tid == 0) {
       hd->ok = 0;
       hd->deep = (!bad && ndist <= DEEP_CAP - 2) ? 1u : 0u;
-      if (hd->deep) atomicAdd(&D.st->ctr[C_WANT_DEEP], 1ull);
+      if (hd->deep) ctr_add(D, C_WANT_DEEP, 1ull);
       if (!(F.chains & FL_CH_DEEP)) hd->deep = 0;
       hd->dslot = h;
       if (hd->deep) F.dslot_h[h] = h;
@@ -828,7 +829,7 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep_b(Dev D, BatchArgs B, F
     F.ord8[obase + (end - beg) + tid] = fl_rec(false, 0, 0, false, end - beg + tid, w32);
   if (tid == 0) {
     FlowHdr x{};
-    if (dels) atomicAdd(&D.st->ctr[C_WANT_CANC], 1ull);
+    if (dels) ctr_add(D, C_WANT_CANC, 1ull);
     x.ok = dels ? ((F.chains & FL_CH_CANCEL) ? FL_OK_CANCEL : 0u) : FL_OK_ADD;
     x.nl = n;
     x.sym = sym;
@@ -1886,139 +1887,166 @@ __global__ void k_flow_count(Dev D, BatchArgs B, FlowArgs F) {
     pops += __shfl_xor(pops, off);
   }
   if (lane_id() == 0 && fills) {
-    atomicAdd(&D.st->ctr[C_FILLS], fills);
-    atomicAdd(&D.st->ctr[C_HOT_FILLS], fills);
-    if (F.h0 >= FL_HEAD) atomicAdd(&D.st->ctr[C_FLOW_TAIL_FILLS], fills);
-    atomicAdd(&D.st->ctr[C_RESTING_DELTA], static_cast<unsigned long long>(-static_cast<long long>(pops)));
+    ctr_add(D, C_FILLS, fills);
+    ctr_add(D, C_HOT_FILLS, fills);
+    if (F.h0 >= FL_HEAD) ctr_add(D, C_FLOW_TAIL_FILLS, fills);
+    ctr_add(D, C_RESTING_DELTA, static_cast<unsigned long long>(-static_cast<long long>(pops)));
   }
 }
 
 // ============================================================== k_flow_events
-// After the publish-order scan: every fill event at out[ev_off[taker] + fill_idx].
-// ARENA: the events go to the batch's event arena (one bump allocation per wave) for
-// k_ev_scatter to place, so they need not wait for the publish-order scan (the tail's books,
-// done long before the head's); else straight to out[ev_off[taker] + fill_idx].
-constexpr uint32_t FL_EV_T = 256;  // threads of the event kernels' blocks
+// Lane-per-event emission.  A CONS touch fills makers first..last of its level; the touches of a
+// wave hold very different counts (one taker sweeping a level of hundreds of makers beside takers
+// filling one), so the events are not written by their touch's lane: each lane keeps its touch's
+// context (FlEvLane, cnt == 0 for none), and the wave enumerates its events 64 at a time, every
+// lane finding its touch by a binary search over the wave's inclusive counts (shuffles, no LDS).
+// A lane's maker is usually the next lane's MatchNode.NextNode: taken by a shuffle, not reloaded.
+// Stores of consecutive events are consecutive 64-B slots (coalesced).
+struct FlEvLane {
+  uint32_t inc;        // events of the wave's lanes <= this one
+  uint32_t mb;         // maker index of wave event e: e + mb
+  uint32_t dbase;      // its slot: dst[dbase + m]
+  uint32_t fbm;        // its fill_idx: fbm + m
+  uint32_t ig_n, nra;  // nra: new makers | ig_all << 31
+  uint32_t igb, rsb, beg, t, idx, sym;
+  int64_t c, ca, tbc, price;  // cursor before the touch, cursor after, taker volume + c, level price
+};
+
+__device__ __forceinline__ void fl_ev_lane(FlEvLane& r, const FlTouchCtx& c, uint32_t L, uint32_t beg, uint32_t t,
+                                           uint32_t idx, uint32_t sym, int64_t tb) {
+  r.ig_n = c.Lq->ig_n;
+  r.nra = c.Lq->nrest | (c.Lq->ig_all ? 0x80000000u : 0u);
+  r.igb = c.Lq->ig_base;
+  r.rsb = L + c.Lq->base;
+  r.beg = beg;
+  r.t = t;
+  r.idx = idx;
+  r.sym = sym;
+  r.c = c.c;
+  r.ca = c.c + c.a;
+  r.tbc = tb + c.c;
+  r.price = c.Lq->price;
+}
+
 template <bool ARENA>
-__device__ __forceinline__ void fl_events(const Dev& D, const BatchArgs& B, const FlowArgs& F, const uint32_t* ev_off,
-                                          gome_event* out) {
-  const uint32_t hend = fl_hend(D, F), nb = hend > F.h0 ? hend - F.h0 : 0u;
-  const uint32_t total = nb ? F.toff[F.tb + nb] : 0u;
-  const uint32_t lane = lane_id(), w = threadIdx.x >> 6, stride = gridDim.x * blockDim.x;
-  __shared__ uint32_t wtot[FL_EV_T / 64], bbase;
-  // block tiles (every wave of the block iterates together: the arena is claimed once per tile)
-  for (uint32_t b0 = blockIdx.x * blockDim.x; b0 < total; b0 += stride) {
-    const uint32_t gt = b0 + threadIdx.x, g0w = b0 + (threadIdx.x & ~63u);
-    uint32_t h = 0, L = 0, t = 0, cnt = 0;
-    Touch x{};
-    FlTouchCtx c{};
-    uint32_t hbw = 0;
-    if (g0w < total) hbw = fl_book_of_wave(F, nb, g0w, gt < total ? gt : g0w);
-    if (gt < total) {
-      const uint32_t hb = hbw;
-      h = F.h0 + hb;
-      t = gt - F.toff[F.tb + hb];
-      L = FL_TOUCH_MUL * F.hdr[h].beg;
-      x = F.log[L + t];
-      if (((x.kr >> 7) & 1u) == TK_CONS) {
-        c = fl_touch_ctx(F, h, L, x, t);
-        cnt = c.last - c.first + 1;
-      }
+__device__ __forceinline__ void fl_emit_wave(const BatchArgs& B, const FlowArgs& F, gome_event* dst, const FlEvLane& x) {
+  const uint32_t lane = lane_id();
+  const uint32_t tot = __shfl(x.inc, 63);
+  for (uint32_t e0 = 0; e0 < tot; e0 += 64) {
+    const uint32_t e = e0 + lane;
+    const bool v = e < tot;
+    uint32_t lo = 0, hi = 63;  // the first lane k with inc[k] > e (inc[63] == tot)
+#pragma unroll
+    for (int it = 0; it < 6; ++it) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (__shfl(x.inc, static_cast<int>(mid)) > e) hi = mid; else lo = mid + 1;
     }
-    gome_event* dst = nullptr;
-    if (ARENA) {
-      uint32_t inc = cnt;
-      for (uint32_t off = 1; off < 64; off <<= 1) {
-        const uint32_t v = __shfl_up(inc, off);
-        if (lane >= off) inc += v;
-      }
-      if (lane == 63) wtot[w] = inc;
-      __syncthreads();
-      if (threadIdx.x == 0) {
-        uint32_t t = 0;
-        for (uint32_t k = 0; k < FL_EV_T / 64; ++k) { const uint32_t v = wtot[k]; wtot[k] = t; t += v; }
-        bbase = t ? atomicAdd(&D.st->ev_bump, t) : 0u;
-        if (t && static_cast<unsigned long long>(bbase) + t > B.arena_cap) {
-          atomicOr(&D.st->err, ERR_EVENTS);
-          bbase = NIL;
-        }
-      }
-      __syncthreads();
-      const uint32_t base = bbase, wb = wtot[w];
-      __syncthreads();  // (wtot / bbase are rewritten by the next tile)
-      if (base == NIL) continue;
-      dst = B.arena + base + wb + (inc - cnt);
-    }
-    if (!cnt) continue;
-    const uint32_t beg = F.hdr[h].beg, sym = F.hdr[h].sym;
-    const Prep tk = B.prep[beg + tk_j(x)];
-    // taker remaining before this level: volume minus what its better levels took
-    int64_t tb = tk.vol;
-    for (uint32_t u = t; u > 0; --u) {
-      const Touch y = F.log[L + u - 1];
-      if (tk_j(y) != tk_j(x)) break;
-      tb -= y.amt * fl_amt_unit(F, h);
-    }
-    const uint32_t ig_n = c.Lq->ig_n, nrest = c.Lq->nrest, ig_all = c.Lq->ig_all;
-    const int64_t price = c.Lq->price;
-    if (!ARENA) dst = out + ev_off[tk.idx] + F.fbase[L + t];
-    for (uint32_t m = c.first; m <= c.last; ++m) {
-      int64_t e, v;
-      uint32_t oid, uuid, tx;
+    const int k = static_cast<int>(lo);
+    const uint32_t m = e + __shfl(x.mb, k);
+    const uint32_t ig_n = __shfl(x.ig_n, k), nra = __shfl(x.nra, k), igb = __shfl(x.igb, k);
+    const uint32_t rsb = __shfl(x.rsb, k), beg = __shfl(x.beg, k), t = __shfl(x.t, k);
+    // (every shuffle before any lane leaves: a shuffle reads 0 from an inactive lane)
+    const int64_t c = __shfl(x.c, k), ca = __shfl(x.ca, k), tbc = __shfl(x.tbc, k), price = __shfl(x.price, k);
+    const uint32_t idx = __shfl(x.idx, k), fbm = __shfl(x.fbm, k), sym = __shfl(x.sym, k), dbase = __shfl(x.dbase, k);
+    int64_t me = 0, mv = 0;
+    uint32_t oid = 0, uuid = 0, tx = 0, rt = 0;
+    if (v) {
       if (m < ig_n) {
-        const IgEnt g = c.IG[m];
-        e = g.e; v = g.v; oid = g.oid; uuid = g.uuid; tx = g.tx;
+        const IgEnt g = F.ig[igb + m];
+        me = g.e; mv = g.v; oid = g.oid; uuid = g.uuid; tx = g.tx;
       } else {
-        const RsEnt r = c.RS[m - ig_n];
+        const RsEnt r = F.rs[rsb + m - ig_n];
         const Prep mk = B.prep[beg + r.j];
-        e = r.e; v = r.v; oid = mk.oid; uuid = mk.uuid; tx = mk.side;
+        me = r.e; mv = r.v; oid = mk.oid; uuid = mk.uuid; tx = mk.side; rt = r.t;
       }
-      const int64_t lo = e > c.c ? e : c.c;
-      const int64_t hi = (e + v < c.c + c.a) ? e + v : c.c + c.a;
-      const int64_t qty = hi - lo, pre = e + v - lo;
-      const bool full = e + v <= c.c + c.a;
-      // MatchNode.NextNode: the next node of the FIFO at the time of this fill
-      uint32_t nx = 0, last = 1;
-      if (m + 1 < ig_n) {
-        nx = c.IG[m + 1].oid;
-        last = 0;
-      } else if (ig_all || m + 1 > ig_n) {
-        const uint32_t r = m + 1 - ig_n;
-        if (r < nrest && c.RS[r].t < t) {
-          nx = B.prep[beg + c.RS[r].j].oid;
-          last = 0;
-        }
-      }
-      gome_event ev;
-      ev.price_fx = price;
-      ev.match_volume_fx = qty;
-      ev.maker_volume_fx = full ? pre : pre - qty;
-      ev.taker_volume_fx = tb - (hi - c.c);
-      // arena events carry the batch index (k_ev_scatter adds seq_base); direct ones the sequence
-      const unsigned long long sq = ARENA ? tk.idx : B.seq_base + tk.idx;
-      ev.taker_seq = static_cast<uint32_t>(sq);
-      ev.fill_idx = F.fbase[L + t] + (m - c.first);
-      ev.symbol_id = sym;
-      ev.maker_oid_id = oid;
-      ev.maker_uuid_id = uuid;
-      ev.maker_next_oid_id = nx;
-      ev.kind = GOME_EV_FILL;
-      ev.maker_side = static_cast<uint8_t>(tx);
-      ev.maker_is_last = static_cast<uint8_t>(last);
-      ev.pad0 = 0;
-      ev.seq_hi = static_cast<uint32_t>(sq >> 32);
-      dst[m - c.first] = ev;
     }
+    // MatchNode.NextNode at the time of this fill: maker m + 1 of the same touch is the next lane's
+    const uint32_t kn = __shfl_down(static_cast<uint32_t>(k), 1), oidn = __shfl_down(oid, 1), rtn = __shfl_down(rt, 1);
+    if (!v) continue;
+    const bool nbr = lane < 63 && e + 1 < tot && kn == static_cast<uint32_t>(k);
+    const uint32_t nrest = nra & 0x7FFFFFFFu;
+    uint32_t nx = 0, lst = 1;
+    if (m + 1 < ig_n) {
+      nx = nbr ? oidn : F.ig[igb + m + 1].oid;
+      lst = 0;
+    } else if ((nra >> 31) || m + 1 > ig_n) {
+      const uint32_t r = m + 1 - ig_n;
+      if (nbr) {
+        if (rtn < t) { nx = oidn; lst = 0; }
+      } else if (r < nrest) {
+        const RsEnt rr = F.rs[rsb + r];
+        if (rr.t < t) { nx = B.prep[beg + rr.j].oid; lst = 0; }
+      }
+    }
+    const int64_t lo_ = me > c ? me : c;
+    const int64_t hi_ = (me + mv < ca) ? me + mv : ca;
+    const int64_t qty = hi_ - lo_, pre = me + mv - lo_;
+    const bool full = me + mv <= ca;
+    const unsigned long long sq = ARENA ? idx : B.seq_base + idx;  // arena: the batch index (k_ev_scatter)
+    gome_event ev;
+    ev.price_fx = price;
+    ev.match_volume_fx = qty;
+    ev.maker_volume_fx = full ? pre : pre - qty;
+    ev.taker_volume_fx = tbc - hi_;
+    ev.taker_seq = static_cast<uint32_t>(sq);
+    ev.fill_idx = fbm + m;
+    ev.symbol_id = sym;
+    ev.maker_oid_id = oid;
+    ev.maker_uuid_id = uuid;
+    ev.maker_next_oid_id = nx;
+    ev.kind = GOME_EV_FILL;
+    ev.maker_side = static_cast<uint8_t>(tx);
+    ev.maker_is_last = static_cast<uint8_t>(lst);
+    ev.pad0 = 0;
+    ev.seq_hi = static_cast<uint32_t>(sq >> 32);
+    dst[dbase + m] = ev;
   }
 }
 
+// After the publish-order scan: every fill event of the hottest book at out[ev_off[taker] + fill_idx]
+// (fill_idx bases from the count pass, F.fbase).
+constexpr uint32_t FL_EV_T = 256;  // threads of the event kernels' blocks
+constexpr uint32_t FL_WRITE_T = 1024;  // ... of the tail's (and of k_flow_write's)
 __global__ __launch_bounds__(256) void k_flow_events(Dev D, BatchArgs B, FlowArgs F, const uint32_t* ev_off,
                                                      gome_event* out) {
-  fl_events<false>(D, B, F, ev_off, out);
-}
-
-__global__ __launch_bounds__(256) void k_flow_events_arena(Dev D, BatchArgs B, FlowArgs F) {
-  fl_events<true>(D, B, F, nullptr, nullptr);
+  const uint32_t hend = fl_hend(D, F), nb = hend > F.h0 ? hend - F.h0 : 0u;
+  const uint32_t total = nb ? F.toff[F.tb + nb] : 0u;
+  const uint32_t lane = lane_id(), stride = gridDim.x * blockDim.x;
+  for (uint32_t b0 = blockIdx.x * blockDim.x + (threadIdx.x & ~63u); b0 < total; b0 += stride) {
+    const uint32_t gt = b0 + lane;
+    uint32_t cnt = 0, first = 0;
+    FlEvLane r{};
+    const uint32_t hb = fl_book_of_wave(F, nb, b0, gt < total ? gt : b0);
+    if (gt < total) {
+      const uint32_t h = F.h0 + hb, t = gt - F.toff[F.tb + hb], beg = F.hdr[h].beg, L = FL_TOUCH_MUL * beg;
+      const Touch x = F.log[L + t];
+      if (((x.kr >> 7) & 1u) == TK_CONS) {
+        const FlTouchCtx c = fl_touch_ctx(F, h, L, x, t);
+        cnt = c.last - c.first + 1;
+        first = c.first;
+        const Prep tk = B.prep[beg + tk_j(x)];
+        int64_t tb = tk.vol;  // taker remaining before this level: volume minus its better levels
+        const int64_t gm = fl_amt_unit(F, h);
+        for (uint32_t u = t; u > 0; --u) {
+          const Touch y = F.log[L + u - 1];
+          if (tk_j(y) != tk_j(x)) break;
+          tb -= y.amt * gm;
+        }
+        fl_ev_lane(r, c, L, beg, t, tk.idx, F.hdr[h].sym, tb);
+        const uint32_t fb = F.fbase[L + t];
+        r.fbm = fb - c.first;
+        r.dbase = ev_off[tk.idx] + fb - c.first;
+      }
+    }
+    uint32_t inc = cnt;
+    for (uint32_t off = 1; off < 64; off <<= 1) {
+      const uint32_t v = __shfl_up(inc, off);
+      if (lane >= off) inc += v;
+    }
+    r.inc = inc;
+    r.mb = first - (inc - cnt);
+    fl_emit_wave<false>(B, F, out, r);
+  }
 }
 
 // Segmented inclusive wave scan: lane i sums lanes s..i, s = the last lane <= i with `head` set
@@ -2038,7 +2066,7 @@ __device__ __forceinline__ T wave_seg_incl(T v, unsigned long long heads) {
 
 // ============================================================== k_flow_events_fused
 // The books whose events go to the arena (the tail, the near head books): k_flow_count and
-// k_flow_events_arena in one pass over the touches.  An order's touches are consecutive in its
+// the arena event writes in one pass over the touches.  An order's touches are consecutive in its
 // book's log, so its fill_idx bases and the volume its better levels took are segmented scans
 // over the touches (a wave's first lane walks back into an order begun before the wave); the
 // order's last touch writes ev_count[taker].
@@ -2088,7 +2116,7 @@ __device__ __forceinline__ void fl_events_fused(const Dev& D, const BatchArgs& B
     const unsigned long long heads = __ballot(first);
     uint32_t carry_n = 0;
     int64_t carry_a = 0;
-    if (lane == 0 && !first) {
+    if (lane == 0 && !first && !(F.xp & 8u)) {
       for (uint32_t u = t; u > 0; --u) {
         const Touch y = F.log[L + u - 1];
         if (tk_j(y) != j) break;
@@ -2112,6 +2140,10 @@ __device__ __forceinline__ void fl_events_fused(const Dev& D, const BatchArgs& B
       if (valid) F.fbase[L + t] = fb;
       continue;
     }
+    if (F.xp & 1u) {  // (experiment: the touch pass alone)
+      if (valid && n_incl == 0xFFFFFFFFu) F.fbase[L + t] = fb;
+      continue;
+    }
     // arena slots: one bump allocation per block tile
     uint32_t inc = cnt;
     for (uint32_t off = 1; off < 64; off <<= 1) {
@@ -2132,71 +2164,48 @@ __device__ __forceinline__ void fl_events_fused(const Dev& D, const BatchArgs& B
     __syncthreads();
     const uint32_t base = bbase, wb = wtot[w];
     __syncthreads();  // (wtot / bbase are rewritten by the next tile)
-    if (base == NIL || !cnt) continue;
-    gome_event* dst = B.arena + base + wb + (inc - cnt);
-    const uint32_t sym = F.hdr[h].sym;
-    const Prep tk = B.prep[beg + j];
-    const int64_t tb = tk.vol - a_before;  // taker remaining before this level
-    const uint32_t ig_n = c.Lq->ig_n, nrest = c.Lq->nrest, ig_all = c.Lq->ig_all;
-    const int64_t price = c.Lq->price;
-    for (uint32_t m = c.first; m <= c.last; ++m) {
-      int64_t e, v;
-      uint32_t oid, uuid, tx;
-      if (m < ig_n) {
-        const IgEnt g = c.IG[m];
-        e = g.e; v = g.v; oid = g.oid; uuid = g.uuid; tx = g.tx;
-      } else {
-        const RsEnt r = c.RS[m - ig_n];
-        const Prep mk = B.prep[beg + r.j];
-        e = r.e; v = r.v; oid = mk.oid; uuid = mk.uuid; tx = mk.side;
-      }
-      const int64_t lo = e > c.c ? e : c.c;
-      const int64_t hi = (e + v < c.c + c.a) ? e + v : c.c + c.a;
-      const int64_t qty = hi - lo, pre = e + v - lo;
-      const bool full = e + v <= c.c + c.a;
-      uint32_t nx = 0, lst = 1;  // MatchNode.NextNode at the time of this fill
-      if (m + 1 < ig_n) {
-        nx = c.IG[m + 1].oid;
-        lst = 0;
-      } else if (ig_all || m + 1 > ig_n) {
-        const uint32_t r = m + 1 - ig_n;
-        if (r < nrest && c.RS[r].t < t) {
-          nx = B.prep[beg + c.RS[r].j].oid;
-          lst = 0;
-        }
-      }
-      gome_event ev;
-      ev.price_fx = price;
-      ev.match_volume_fx = qty;
-      ev.maker_volume_fx = full ? pre : pre - qty;
-      ev.taker_volume_fx = tb - (hi - c.c);
-      ev.taker_seq = tk.idx;  // (the batch index: k_ev_scatter adds seq_base)
-      ev.fill_idx = fb + (m - c.first);
-      ev.symbol_id = sym;
-      ev.maker_oid_id = oid;
-      ev.maker_uuid_id = uuid;
-      ev.maker_next_oid_id = nx;
-      ev.kind = GOME_EV_FILL;
-      ev.maker_side = static_cast<uint8_t>(tx);
-      ev.maker_is_last = static_cast<uint8_t>(lst);
-      ev.pad0 = 0;
-      ev.seq_hi = 0;
-      dst[m - c.first] = ev;
+    if (base == NIL) continue;
+    FlEvLane r{};
+    r.inc = inc;
+    if (cnt) {
+      const Prep tk = B.prep[beg + j];
+      fl_ev_lane(r, c, L, beg, t, tk.idx, F.hdr[h].sym, tk.vol - a_before);  // (taker remaining before the level)
+      r.mb = c.first - (inc - cnt);
+      r.dbase = base + wb + (inc - cnt) - c.first;
+      r.fbm = fb - c.first;
     }
+    if (F.xp & 2u) {  // (experiment: no emission)
+      if (r.inc == 0xFFFFFFFFu) B.arena[0].fill_idx = r.mb;
+      continue;
+    }
+    fl_emit_wave<true>(B, F, B.arena, r);
   }
+  // the block's counts, then one stripe add per counter (ctr_add)
   for (int off = 32; off > 0; off >>= 1) {
     fills += __shfl_xor(fills, off);
     pops += __shfl_xor(pops, off);
   }
-  if (lane_id() == 0 && fills) {
-    atomicAdd(&D.st->ctr[C_FILLS], fills);
-    atomicAdd(&D.st->ctr[C_HOT_FILLS], fills);
-    if (F.h0 >= FL_HEAD) atomicAdd(&D.st->ctr[C_FLOW_TAIL_FILLS], fills);
-    atomicAdd(&D.st->ctr[C_RESTING_DELTA], static_cast<unsigned long long>(-static_cast<long long>(pops)));
+  __shared__ unsigned long long wf[T / 64], wp[T / 64];
+  if (lane == 0) { wf[w] = fills; wp[w] = pops; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    fills = pops = 0;
+    for (uint32_t k = 0; k < T / 64; ++k) { fills += wf[k]; pops += wp[k]; }
+    if (fills) {
+      ctr_add(D, C_FILLS, fills);
+      ctr_add(D, C_HOT_FILLS, fills);
+      if (F.h0 >= FL_HEAD) ctr_add(D, C_FLOW_TAIL_FILLS, fills);
+      ctr_add(D, C_RESTING_DELTA, static_cast<unsigned long long>(-static_cast<long long>(pops)));
+    }
   }
 }
 __global__ __launch_bounds__(FL_EV_T) void k_flow_events_fused(Dev D, BatchArgs B, FlowArgs F) {
   fl_events_fused<FL_EV_T>(D, B, F, blockIdx.x, gridDim.x);
+}
+// The tail's events: one arena claim per 1024 touches (a claim is a device-scope atomic on one
+// address: 256-touch tiles made 22k of them on config 2's tail).
+__global__ __launch_bounds__(FL_WRITE_T) void k_flow_events_fused_w(Dev D, BatchArgs B, FlowArgs F) {
+  fl_events_fused<FL_WRITE_T>(D, B, F, blockIdx.x, gridDim.x);
 }
 __global__ __launch_bounds__(FL_EV_T) void k_flow_count_fused(Dev D, BatchArgs B, FlowArgs F) {
   fl_events_fused<FL_EV_T, true>(D, B, F, blockIdx.x, gridDim.x);
@@ -2205,7 +2214,6 @@ __global__ __launch_bounds__(FL_EV_T) void k_flow_count_fused(Dev D, BatchArgs B
 // ============================================================== k_flow_write
 // One workgroup per flow book: append the surviving new makers to their FIFOs (chunks from
 // the free stack / bump pool), insert them into the cancel index, rewrite the level array.
-constexpr uint32_t FL_WRITE_T = 1024;
 
 // Append level q's surviving new makers to its FIFO, insert them into the cancel index, and
 // return (on every lane) the level's final record.
@@ -2383,47 +2391,170 @@ __device__ __forceinline__ void fl_write_finish(const Dev& D, const FlowHdr& hd,
     nb.lvl_cap = cap_s;
     nb.pad = 0;
     D.books[hd.sym] = nb;
-    unsigned long long* c = D.st->ctr;
-    atomicAdd(&c[C_RESTS], static_cast<unsigned long long>(hd.rests));
-    atomicAdd(&c[C_HOT_RESTS], static_cast<unsigned long long>(hd.rests));
-    atomicAdd(&c[C_RESTING_DELTA], static_cast<unsigned long long>(hd.rests));
-    atomicAdd(&c[C_ADD], static_cast<unsigned long long>(hd.adds));
-    atomicAdd(&c[C_DROPPED], static_cast<unsigned long long>(hd.dropped));
-    atomicAdd(&c[C_LEVELS_DELTA], static_cast<unsigned long long>(static_cast<long long>(nout) - hd.nold));
-    atomicAdd(&c[C_HOT_ORDERS], static_cast<unsigned long long>(hd.end - hd.beg));
-    atomicAdd(&c[C_FLOW_BOOKS], 1ull);
-    atomicAdd(&c[C_FLOW_ORDERS], static_cast<unsigned long long>(hd.end - hd.beg));
-    atomicAdd(&c[C_FLOW_TOUCHES], static_cast<unsigned long long>(hd.ntouch));
+    ctr_add(D, C_RESTS, static_cast<unsigned long long>(hd.rests));
+    ctr_add(D, C_HOT_RESTS, static_cast<unsigned long long>(hd.rests));
+    ctr_add(D, C_RESTING_DELTA, static_cast<unsigned long long>(hd.rests));
+    ctr_add(D, C_ADD, static_cast<unsigned long long>(hd.adds));
+    ctr_add(D, C_DROPPED, static_cast<unsigned long long>(hd.dropped));
+    ctr_add(D, C_LEVELS_DELTA, static_cast<unsigned long long>(static_cast<long long>(nout) - hd.nold));
+    ctr_add(D, C_HOT_ORDERS, static_cast<unsigned long long>(hd.end - hd.beg));
+    ctr_add(D, C_FLOW_BOOKS, 1ull);
+    ctr_add(D, C_FLOW_ORDERS, static_cast<unsigned long long>(hd.end - hd.beg));
+    ctr_add(D, C_FLOW_TOUCHES, static_cast<unsigned long long>(hd.ntouch));
   }
 }
 
-// Tail books: one workgroup per book; the chunk ids of all its appends in one claim, then
-// waves take its levels in turn, then finish.
+// Tail books: one workgroup per book.  Thread i plans level i + 1 (fl_wplan); one block scan
+// of the levels' surviving new makers and new chunks, one chunk claim for the book; then every
+// thread takes surviving makers of the whole book (its level by a binary search over the scan),
+// so the book's FIFO appends and index inserts are all in flight at once instead of one level
+// per wave in turn (a tail book's level holds a few new makers: most of a wave idled); the
+// chunk headers the same way; then the level records and the finish.
 __device__ __forceinline__ void fl_write_book(const Dev& D, const BatchArgs& B, const FlowArgs& F, uint32_t h) {
+  static_assert(FL_CAP <= 128, "one wave plans a book's levels, two per lane");
   __shared__ Level lv[FL_CAP];
   __shared__ uint32_t keep[FL_CAP];
   __shared__ uint32_t nout_s, base_s, cap_s;
-  __shared__ uint32_t need_s[FL_CAP];
+  __shared__ uint32_t rof[FL_CAP + 1], cof[FL_CAP + 1];  // exclusive scans: surviving makers, new chunks
+  __shared__ uint32_t wrf[FL_CAP], wtl[FL_CAP], wbs[FL_CAP], ws0[FL_CAP];  // ws0: s0 | fresh << 31
+  __shared__ int64_t wcf[FL_CAP];
   __shared__ FlClaim claim_s;
   if (h >= fl_hend(D, F) || F.hdr[h].ok != FL_OK_ADD) return;
   const FlowHdr hd = F.hdr[h];
-  const uint32_t w = threadIdx.x >> 6, nw = FL_WRITE_T / 64;
-  FlowLvl* LV = F.lvl + h * FL_CAP;
-  const RsEnt* RS = F.rs + FL_TOUCH_MUL * hd.beg;
-  for (uint32_t q = 1 + threadIdx.x; q <= hd.nl; q += FL_WRITE_T) need_s[q] = fl_wplan(LV[q], RS + LV[q].base).need;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    uint32_t off = 0;
-    for (uint32_t q = 1; q <= hd.nl; ++q) {
-      LV[q].pad0 = off;
-      off += need_s[q];
+  const uint32_t tid = threadIdx.x, lane = lane_id(), nl = hd.nl;
+  const FlowLvl* LV = F.lvl + h * FL_CAP;
+  const uint32_t L = FL_TOUCH_MUL * hd.beg;
+  const unsigned long long mask = D.idx_mask;
+  if (tid < 64) {  // wave 0: levels 2 lane + 1 and 2 lane + 2
+    int64_t x = 0, x0 = 0;  // (S, need) packed: need < 2^32 over a book
+#pragma unroll
+    for (uint32_t u = 0; u < 2; ++u) {
+      const uint32_t i = 2 * tid + u;
+      if (i < nl) {
+        const FlowLvl& f = LV[i + 1];
+        const FlWPlan wp = fl_wplan(f, F.rs + L + f.base);
+        wrf[i] = wp.rf;
+        wtl[i] = f.tail;
+        wbs[i] = f.base;
+        ws0[i] = wp.s0 | (wp.fresh ? 0x80000000u : 0u);
+        wcf[i] = f.cfin;
+        const int64_t v = (static_cast<int64_t>(wp.S) << 32) | wp.need;
+        if (u == 0) x0 = v;
+        x += v;
+      }
     }
-    claim_s = fl_claim_chunks(D, off);
+    const int64_t ex = wave_incl_scan(x) - x;
+    rof[2 * tid] = static_cast<uint32_t>(ex >> 32);
+    cof[2 * tid] = static_cast<uint32_t>(ex);
+    rof[2 * tid + 1] = static_cast<uint32_t>((ex + x0) >> 32);
+    cof[2 * tid + 1] = static_cast<uint32_t>(ex + x0);
+    if (tid == 63) {
+      const int64_t tot = ex + x;
+      rof[128] = static_cast<uint32_t>(tot >> 32);
+      cof[128] = static_cast<uint32_t>(tot);
+      claim_s = fl_claim_chunks(D, static_cast<uint32_t>(tot));
+    }
   }
   __syncthreads();
-  for (uint32_t q = 1 + w; q <= hd.nl; q += nw) {
-    const Level x = fl_write_level(D, B, F, hd, h, uni(q), &claim_s);
-    if (lane_id() == 0) lv[q] = x;
+  const FlClaim cl = claim_s;
+  auto cid = [&](uint32_t c) -> uint32_t {  // the book's c-th new chunk
+    return c < cl.c_nst ? D.free_ids[cl.c_t - static_cast<int>(cl.c_nst) + static_cast<int>(c)] : cl.c_bb + (c - cl.c_nst);
+  };
+  // the last level i (0-based) with off[i] <= g (off[0] = 0 <= g; nl >= 1)
+  auto level_of = [&](const uint32_t* off, uint32_t g) -> uint32_t {
+    uint32_t lo = 0, hi = nl - 1;
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi + 1) >> 1;
+      if (off[mid] <= g) lo = mid; else hi = mid - 1;
+    }
+    return lo;
+  };
+  const uint32_t nch = cof[nl], nsv = rof[nl];
+  if (cl.c_ok) {
+    for (uint32_t c = tid; c < nch; c += FL_WRITE_T) {
+      const uint32_t i = level_of(cof, c);
+      ChunkHdr ch;
+      ch.next = c + 1 < cof[i + 1] ? cid(c + 1) : NIL;
+      ch.pad = 0;
+      ch.price = LV[i + 1].price;
+      D.chdr[cid(c)] = ch;
+    }
+  }
+  for (uint32_t g = tid; g < nsv; g += FL_WRITE_T) {
+    const uint32_t i = level_of(rof, g), k = g - rof[i];
+    const bool needs = cof[i + 1] > cof[i];
+    if (needs && !cl.c_ok) continue;  // (ERR_CHUNKS set by the claim)
+    const RsEnt r = F.rs[L + wbs[i] + wrf[i] + k];
+    const Prep mk = B.prep[hd.beg + r.j];
+    const int64_t cfin = wcf[i];
+    const int64_t rem = (r.e < cfin) ? r.e + r.v - cfin : r.v;
+    const uint32_t s0 = ws0[i] & 0x7FFFFFFFu;
+    const bool fresh = ws0[i] >> 31;
+    const uint32_t room = fresh ? 0u : CH - s0;
+    uint32_t c, slot;
+    if (!fresh && s0 + k < CH) {
+      c = wtl[i];
+      slot = s0 + k;
+    } else {
+      const uint32_t gg = fresh ? k : k - room;
+      c = cid(cof[i] + gg / CH);
+      slot = gg % CH;
+    }
+    const uint32_t loc = c * CH + slot;
+    const unsigned long long key = (static_cast<unsigned long long>(hd.sym + 1) << 32) | mk.oid;
+    unsigned long long hh = mix64(key) & mask, probe = 0;
+    for (; probe <= mask; ++probe, hh = (hh + 1) & mask) {
+      const unsigned long long kv = __hip_atomic_load(&D.idx[hh].key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if ((kv == KEY_EMPTY || kv == KEY_TOMB) && atomicCAS(&D.idx[hh].key, kv, key) == kv) break;
+    }
+    if (probe > mask) { atomicOr(&D.st->err, ERR_INDEX); continue; }
+    D.idx[hh].loc = loc;
+    Node nd{};
+    nd.rem = rem;
+    nd.oid = mk.oid;
+    nd.uuid = mk.uuid;
+    nd.ixs = static_cast<uint32_t>(hh);
+    nd.tx = mk.side;
+    D.nodes[loc] = nd;
+  }
+  if (tid < nl) {  // the level's final record
+    const FlowLvl& f = LV[tid + 1];
+    const uint32_t q = tid + 1, S = rof[tid + 1] - rof[tid], need = cof[tid + 1] - cof[tid];
+    const uint32_t s0 = ws0[tid] & 0x7FFFFFFFu;
+    const bool fresh = ws0[tid] >> 31;
+    const uint32_t room = fresh ? 0u : CH - s0;
+    Level x{};
+    x.price = f.price;
+    x.head = x.tail = NIL;
+    if (need && !cl.c_ok) {
+      lv[q] = x;
+    } else {
+      if (need && !fresh) D.chdr[f.tail].next = cid(cof[tid]);
+      x.depth = f.dfin;
+      x.nlive = f.nlive0 + S;
+      uint32_t mem = 0;
+      if (((q < 64 ? hd.amask[0] : hd.amask[1]) >> (q & 63)) & 1ull) mem |= M_SALE;
+      if (((q < 64 ? hd.bmask[0] : hd.bmask[1]) >> (q & 63)) & 1ull) mem |= M_BUY;
+      x.member = static_cast<uint8_t>(mem);
+      if (x.nlive == 0) {
+        x.hslot = x.tslot = 0;
+      } else if (fresh) {
+        x.head = cid(cof[tid]);
+        x.hslot = 0;
+        x.tail = cid(cof[tid] + need - 1);
+        x.tslot = static_cast<uint8_t>(S - (need - 1) * CH);
+      } else {
+        x.head = f.head;
+        x.hslot = static_cast<uint8_t>(f.hslot);
+        x.tail = need ? cid(cof[tid] + need - 1) : f.tail;
+        x.tslot = static_cast<uint8_t>(need ? (S - room) - (need - 1) * CH : s0 + S);
+      }
+      // clean-book invariant: nodes <=> positive depth <=> one side-set membership
+      const bool ok = (x.nlive > 0) == (x.depth > 0) && (x.nlive > 0) == (mem == M_BUY || mem == M_SALE) &&
+                      (x.nlive > 0 || mem == 0);
+      if (!ok) atomicOr(&D.st->err, ERR_CORRUPT);
+      lv[q] = x;
+    }
   }
   __syncthreads();
   fl_write_finish(D, hd, lv, keep, base_s, cap_s, nout_s);
@@ -2569,8 +2700,8 @@ __global__ __launch_bounds__(128) void k_flow_write_fin(Dev D, FlowArgs F) {
   __syncthreads();
   fl_write_finish(D, hd, lv, keep, base_s, cap_s, nout_s);
   if (threadIdx.x == 0 && F.h0 == 0) {  // k_flow_plan_head's work (its roofline numerator)
-    atomicAdd(&D.st->ctr[C_FLOW_HEAD_ORDERS], static_cast<unsigned long long>(hd.end - hd.beg));
-    atomicAdd(&D.st->ctr[C_FLOW_HEAD_TOUCHES], static_cast<unsigned long long>(hd.ntouch));
+    ctr_add(D, C_FLOW_HEAD_ORDERS, static_cast<unsigned long long>(hd.end - hd.beg));
+    ctr_add(D, C_FLOW_HEAD_TOUCHES, static_cast<unsigned long long>(hd.ntouch));
   }
 }
 

@@ -1312,13 +1312,12 @@ __global__ void k_fc_count(Dev D, BatchArgs B, FlowArgs F) {
     cancels += __shfl_xor(cancels, off);
   }
   if (lane_id() == 0 && (fills || cancels)) {
-    unsigned long long* c = D.st->ctr;
-    atomicAdd(&c[C_FILLS], fills);
-    atomicAdd(&c[C_HOT_FILLS], fills);
-    atomicAdd(&c[C_CANCELS], cancels);
-    atomicAdd(&c[C_HOT_CANCELS], cancels);
-    atomicAdd(&c[C_FLOW_CANCELS], cancels);
-    atomicAdd(&c[C_RESTING_DELTA], static_cast<unsigned long long>(-static_cast<long long>(pops + cancels)));
+    ctr_add(D, C_FILLS, fills);
+    ctr_add(D, C_HOT_FILLS, fills);
+    ctr_add(D, C_CANCELS, cancels);
+    ctr_add(D, C_HOT_CANCELS, cancels);
+    ctr_add(D, C_FLOW_CANCELS, cancels);
+    ctr_add(D, C_RESTING_DELTA, static_cast<unsigned long long>(-static_cast<long long>(pops + cancels)));
   }
 }
 
@@ -1608,10 +1607,10 @@ __global__ __launch_bounds__(128) void k_fc_fin(Dev D, FlowArgs F) {
   __syncthreads();
   fl_write_finish(D, hd, lv, keep, base_s, cap_s, nout_s);
   if (threadIdx.x == 0) {
-    atomicAdd(&D.st->ctr[C_DEL], static_cast<unsigned long long>(hd.ndel));
+    ctr_add(D, C_DEL, static_cast<unsigned long long>(hd.ndel));
     if (F.h0 == 0) {
-      atomicAdd(&D.st->ctr[C_FLOW_HEAD_ORDERS], static_cast<unsigned long long>(hd.end - hd.beg));
-      atomicAdd(&D.st->ctr[C_FLOW_HEAD_TOUCHES], static_cast<unsigned long long>(hd.ntouch));
+      ctr_add(D, C_FLOW_HEAD_ORDERS, static_cast<unsigned long long>(hd.end - hd.beg));
+      ctr_add(D, C_FLOW_HEAD_TOUCHES, static_cast<unsigned long long>(hd.ntouch));
     }
   }
 }
@@ -1631,7 +1630,7 @@ __global__ __launch_bounds__(FL_WRITE_T) void k_fc_write_book(Dev D, BatchArgs B
   }
   __syncthreads();
   fl_write_finish(D, hd, lv, keep, base_s, cap_s, nout_s);
-  if (threadIdx.x == 0) atomicAdd(&D.st->ctr[C_DEL], static_cast<unsigned long long>(hd.ndel));
+  if (threadIdx.x == 0) ctr_add(D, C_DEL, static_cast<unsigned long long>(hd.ndel));
 }
 
 }  // namespace gome

@@ -191,7 +191,7 @@ __device__ __forceinline__ void k_deep_prep_b_one(Dev D, BatchArgs B, FlowArgs F
     const uint64_t tiles = (static_cast<uint64_t>(FL_TOUCH_MUL) * (end - beg) + FL_TILE - 1) / FL_TILE;
     bad = (P->d_bad || (bk.pad & BOOK_QUIRK) || bk.n_lvl > DEEP_CAP - 2 || tiles > fd_tiles(F, ds)) ? 1u : 0u;
     if (!bad && P->d_dels) {  // the W32DC plan needs the cancel chain
-      atomicAdd(&D.st->ctr[C_WANT_CANC], 1ull);
+      ctr_add(D, C_WANT_CANC, 1ull);
       if (!(F.chains & FL_CH_CANCEL)) bad = 1;
     }
     ndist = P->d_ndist;
@@ -712,21 +712,20 @@ __device__ __forceinline__ void k_deep_write_fin_one(Dev D, FlowArgs F, uint32_t
       nb.pad = 0;
       D.books[hd.sym] = nb;
     }
-    unsigned long long* ct = D.st->ctr;
-    atomicAdd(&ct[C_RESTS], static_cast<unsigned long long>(hd.rests));
-    atomicAdd(&ct[C_HOT_RESTS], static_cast<unsigned long long>(hd.rests));
-    atomicAdd(&ct[C_RESTING_DELTA], static_cast<unsigned long long>(hd.rests));
-    atomicAdd(&ct[C_ADD], static_cast<unsigned long long>(hd.adds));
-    atomicAdd(&ct[C_DROPPED], static_cast<unsigned long long>(hd.dropped));
-    atomicAdd(&ct[C_LEVELS_DELTA], static_cast<unsigned long long>(static_cast<long long>(nout) - hd.nold));
-    atomicAdd(&ct[C_HOT_ORDERS], static_cast<unsigned long long>(hd.end - hd.beg));
-    atomicAdd(&ct[C_FLOW_BOOKS], 1ull);
-    atomicAdd(&ct[C_FLOW_ORDERS], static_cast<unsigned long long>(hd.end - hd.beg));
-    atomicAdd(&ct[C_FLOW_TOUCHES], static_cast<unsigned long long>(hd.ntouch));
-    if (hd.dc) atomicAdd(&ct[C_DEL], static_cast<unsigned long long>(hd.ndel));
+    ctr_add(D, C_RESTS, static_cast<unsigned long long>(hd.rests));
+    ctr_add(D, C_HOT_RESTS, static_cast<unsigned long long>(hd.rests));
+    ctr_add(D, C_RESTING_DELTA, static_cast<unsigned long long>(hd.rests));
+    ctr_add(D, C_ADD, static_cast<unsigned long long>(hd.adds));
+    ctr_add(D, C_DROPPED, static_cast<unsigned long long>(hd.dropped));
+    ctr_add(D, C_LEVELS_DELTA, static_cast<unsigned long long>(static_cast<long long>(nout) - hd.nold));
+    ctr_add(D, C_HOT_ORDERS, static_cast<unsigned long long>(hd.end - hd.beg));
+    ctr_add(D, C_FLOW_BOOKS, 1ull);
+    ctr_add(D, C_FLOW_ORDERS, static_cast<unsigned long long>(hd.end - hd.beg));
+    ctr_add(D, C_FLOW_TOUCHES, static_cast<unsigned long long>(hd.ntouch));
+    if (hd.dc) ctr_add(D, C_DEL, static_cast<unsigned long long>(hd.ndel));
     if (hd.dslot == 0) {  // the hottest book (k_flow_plan_head's work)
-      atomicAdd(&ct[C_FLOW_HEAD_ORDERS], static_cast<unsigned long long>(hd.end - hd.beg));
-      atomicAdd(&ct[C_FLOW_HEAD_TOUCHES], static_cast<unsigned long long>(hd.ntouch));
+      ctr_add(D, C_FLOW_HEAD_ORDERS, static_cast<unsigned long long>(hd.end - hd.beg));
+      ctr_add(D, C_FLOW_HEAD_TOUCHES, static_cast<unsigned long long>(hd.ntouch));
     }
   }
   __syncthreads();

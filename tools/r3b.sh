@@ -26,6 +26,15 @@ for P in $PARTS; do
   c2t)
     timeout -k 10 300 rocprofv3 --kernel-trace --stats -T --output-format csv -d $OUT/c2trace -o run \
       -- python3 bench.py --workload config2 --steps 5 --warmup 5 --e2e-steps 0 --no-cpu-baseline > $OUT/c2_trace.log 2>&1 || exit 4 ;;
+  c2ts)  # config-2 trace with the tail's events after its writes (solo kernel times)
+    GOME_TAIL_SERIAL=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats -T --output-format csv -d $OUT/c2strace -o run \
+      -- python3 bench.py --workload config2 --steps 5 --warmup 5 --e2e-steps 0 --no-cpu-baseline --no-phase-pass > $OUT/c2s_trace.log 2>&1 || exit 4 ;;
+  xp)  # config-2 traces of the event-pass experiments (GOME_EV_XP values from XPV), tail serial
+    for X in ${XPV:-0 1 2}; do
+      GOME_EV_XP=$X GOME_TAIL_SERIAL=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats -T --output-format csv -d $OUT/xp$X -o run \
+        -- python3 bench.py --workload config2 --steps 5 --warmup 5 --e2e-steps 0 --no-cpu-baseline --no-phase-pass > $OUT/xp$X.log 2>&1 || exit 4
+      python3 tools/timeline.py $OUT/xp$X/run_kernel_trace.csv 2 | grep -E "k_flow_events_fused  grid 1048576|k_flow_write  grid" | sed "s/^/xp$X /"
+    done ;;
   c3t)
     timeout -k 10 300 rocprofv3 --kernel-trace --stats -T --output-format csv -d $OUT/c3trace -o run \
       -- python3 bench.py --workload config3 --steps 5 --warmup 5 --e2e-steps 0 --no-cpu-baseline > $OUT/c3_trace.log 2>&1 || exit 5 ;;

@@ -1566,10 +1566,26 @@ __device__ __forceinline__ void fl_level_fc(const FlowArgs& F, uint32_t L, uint3
   }
 }
 
+// A workgroup's fully consumed chunk ids, staged in LDS and published with one claim on
+// Status::freed_top at the workgroup's end (fl_freed_flush): a device-scope atomic per level on
+// that one word serialised the tail's level pass.  Ids beyond the stage go straight out.
+constexpr uint32_t FL_FREED_LDS = 1024;
+struct FlFreed {
+  uint32_t n;
+  uint32_t ids[FL_FREED_LDS];
+};
+__device__ __forceinline__ void fl_freed_flush(const Dev& D, FlFreed* stg) {
+  __shared__ uint32_t fb_s;
+  const uint32_t n = min(stg->n, FL_FREED_LDS);
+  if (threadIdx.x == 0) fb_s = n ? atomicAdd(&D.st->freed_top, n) : 0u;
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) D.freed_ids[fb_s + i] = stg->ids[i];
+}
+
 __device__ __forceinline__ void fl_level_one(const Dev& D, const FlowArgs& F, uint32_t h, uint32_t q,
                                              uint32_t run_base = NIL, uint32_t run_cnt = 0,
                                              uint32_t ig_pre = NIL, int64_t pre_cfin = -1, uint32_t pre_nr = 0,
-                                             bool fc_here = true) {
+                                             bool fc_here = true, FlFreed* stg = nullptr) {
   const FlowHdr* hd = &F.hdr[h];
   const uint32_t lane = lane_id();
   FlowLvl* Lq = fl_lvls(F, h) + q;
@@ -1646,9 +1662,22 @@ __device__ __forceinline__ void fl_level_one(const Dev& D, const FlowArgs& F, ui
     uint32_t nfr = 0, fid = 0;  // fully consumed chunks, published 64 at a time
     auto publish = [&]() {
       uint32_t fb = 0;
-      if (lane == 0) fb = atomicAdd(&D.st->freed_top, nfr);
-      fb = uni(fb);
-      if (lane < nfr) D.freed_ids[fb + lane] = fid;
+      if (stg) {  // the workgroup's stage first; what does not fit goes out
+        if (lane == 0) fb = atomicAdd(&stg->n, nfr);
+        fb = uni(fb);
+        const uint32_t fit = fb < FL_FREED_LDS ? min(nfr, FL_FREED_LDS - fb) : 0u;
+        if (lane < fit) stg->ids[fb + lane] = fid;
+        if (fit < nfr) {
+          uint32_t gb = 0;
+          if (lane == 0) gb = atomicAdd(&D.st->freed_top, nfr - fit);
+          gb = uni(gb);
+          if (lane >= fit && lane < nfr) D.freed_ids[gb + lane - fit] = fid;
+        }
+      } else {
+        if (lane == 0) fb = atomicAdd(&D.st->freed_top, nfr);
+        fb = uni(fb);
+        if (lane < nfr) D.freed_ids[fb + lane] = fid;
+      }
       nfr = 0;
     };
     for (uint32_t guard = 0; c != NIL && !have_extra; ++guard) {
@@ -1765,11 +1794,43 @@ __device__ __forceinline__ void fl_level_one(const Dev& D, const FlowArgs& F, ui
 }
 
 constexpr uint32_t FL_LEVEL_T = 1024;
+// Tail books: one workgroup per book, its waves take the levels in turn.  The book's gathered-
+// maker space is claimed once (every touched level with old makers: a superset of the levels
+// that gather, within F.ig_cap since their makers are live nodes), and its freed chunks are
+// published once (FlFreed): per-level claims on those two words serialised the pass.
 __global__ __launch_bounds__(FL_LEVEL_T) void k_flow_level(Dev D, FlowArgs F) {
+  static_assert(FL_CAP <= 128, "one wave scans a book's levels, two per lane");
+  __shared__ uint32_t igo[FL_CAP];
+  __shared__ FlFreed stg;
   const uint32_t h = F.h0 + blockIdx.x;
   if (h >= fl_hend(D, F) || F.hdr[h].ok != FL_OK_ADD) return;
-  const uint32_t nl = F.hdr[h].nl;
-  for (uint32_t q = 1 + (threadIdx.x >> 6); q <= nl; q += FL_LEVEL_T / 64) fl_level_one(D, F, h, uni(q));
+  const uint32_t nl = F.hdr[h].nl, tid = threadIdx.x;
+  const FlowLvl* LV = fl_lvls(F, h);
+  if (tid < 64) {
+    uint32_t v0 = 0, v1 = 0;
+    const uint32_t q0 = 2 * tid + 1, q1 = 2 * tid + 2;
+    if (q0 <= nl && LV[q0].cnt) v0 = LV[q0].nv0;
+    if (q1 <= nl && LV[q1].cnt) v1 = LV[q1].nv0;
+    const uint32_t x = v0 + v1;
+    uint32_t inc = x;
+    for (uint32_t off = 1; off < 64; off <<= 1) {
+      const uint32_t u = __shfl_up(inc, off);
+      if (tid >= off) inc += u;
+    }
+    const uint32_t tot = __shfl(inc, 63);
+    uint32_t b = 0;
+    if (tid == 0) b = tot ? atomicAdd(F.ig_bump, tot) : 0u;
+    b = __shfl(b, 0);
+    const uint32_t ex = b + inc - x;
+    if (q0 < FL_CAP) igo[q0] = v0 ? ex : NIL;
+    if (q1 < FL_CAP) igo[q1] = v1 ? ex + v0 : NIL;
+    if (tid == 0) stg.n = 0;
+  }
+  __syncthreads();
+  for (uint32_t q = 1 + (tid >> 6); q <= nl; q += FL_LEVEL_T / 64)
+    fl_level_one(D, F, h, uni(q), NIL, 0, igo[q], -1, 0, true, &stg);
+  __syncthreads();
+  fl_freed_flush(D, &stg);
 }
 
 struct FlTouchCtx {
@@ -1849,48 +1910,6 @@ __global__ __launch_bounds__(256) void k_flow_tmap(Dev D, FlowArgs F) {
   for (uint32_t i = blockIdx.x * 4 + (threadIdx.x >> 6); i < nb; i += gridDim.x * 4) {
     const uint32_t g0 = (to[i] + 63) >> 6, g1 = (to[i + 1] + 63) >> 6;
     for (uint32_t g = g0 + lane_id(); g < g1; g += 64) map[g] = i;
-  }
-}
-
-// ============================================================== k_flow_count
-// Thread per touch; the first touch of each order walks the order's touches (consecutive
-// in the log, best level first), fixing fill_idx bases and ev_count[taker].
-__global__ void k_flow_count(Dev D, BatchArgs B, FlowArgs F) {
-  const uint32_t hend = fl_hend(D, F), nb = hend > F.h0 ? hend - F.h0 : 0u;
-  const uint32_t total = nb ? F.toff[F.tb + nb] : 0u;
-  unsigned long long fills = 0, pops = 0;
-  for (uint32_t gt = blockIdx.x * blockDim.x + threadIdx.x; gt < total; gt += gridDim.x * blockDim.x) {
-    const uint32_t hb = fl_book_of_wave(F, nb, gt - lane_id(), gt), h = F.h0 + hb, t = gt - F.toff[F.tb + hb];
-    const uint32_t nt = F.hdr[h].ntouch, beg = F.hdr[h].beg, L = FL_TOUCH_MUL * beg;
-    const Touch x = F.log[L + t];
-    if (t > 0 && tk_j(F.log[L + t - 1]) == tk_j(x)) continue;
-    uint32_t acc = 0;
-    for (uint32_t u = t; u < nt; ++u) {
-      const Touch y = (u == t) ? x : F.log[L + u];
-      if (tk_j(y) != tk_j(x)) break;
-      F.fbase[L + u] = acc;
-      if (((y.kr >> 7) & 1u) == TK_CONS) {
-        const FlTouchCtx c = fl_touch_ctx(F, h, L, y, u);
-        const uint32_t ne = c.last - c.first + 1;
-        acc += ne;
-        fills += ne;
-        const int64_t lend = c.last < c.Lq->ig_n ? c.IG[c.last].e + c.IG[c.last].v
-                                                 : c.RS[c.last - c.Lq->ig_n].e + c.RS[c.last - c.Lq->ig_n].v;
-        pops += ne - (lend > c.c + c.a ? 1u : 0u);
-      }
-    }
-    if (tk_j(x) < F.hdr[h].end - beg) B.ev_count[B.prep[beg + tk_j(x)].idx] = acc;  // not padding
-  }
-  // wave-reduce the counters, one atomic per wave
-  for (int off = 32; off > 0; off >>= 1) {
-    fills += __shfl_xor(fills, off);
-    pops += __shfl_xor(pops, off);
-  }
-  if (lane_id() == 0 && fills) {
-    ctr_add(D, C_FILLS, fills);
-    ctr_add(D, C_HOT_FILLS, fills);
-    if (F.h0 >= FL_HEAD) ctr_add(D, C_FLOW_TAIL_FILLS, fills);
-    ctr_add(D, C_RESTING_DELTA, static_cast<unsigned long long>(-static_cast<long long>(pops)));
   }
 }
 
@@ -2080,35 +2099,47 @@ __device__ __forceinline__ void fl_events_fused(const Dev& D, const BatchArgs& B
   const uint32_t total = nb ? F.toff[F.tb + nb] : 0u;
   const uint32_t lane = lane_id(), w = threadIdx.x >> 6, stride = nblk * T;
   __shared__ uint32_t wtot[T / 64], bbase;
-  unsigned long long fills = 0, pops = 0;
+  unsigned long long fills = 0;
   for (uint32_t b0 = bid * T; b0 < total; b0 += stride) {
     const uint32_t gt = b0 + threadIdx.x, g0w = b0 + (threadIdx.x & ~63u);
     const bool valid = gt < total;
-    uint32_t h = 0, L = 0, t = 0, nt = 0, beg = 0, j = 0, cnt = 0;
+    uint32_t h = 0, L = 0, t = 0, beg = 0, j = 0, cnt = 0, hend_j = 0, sym = 0;
     int64_t gm = 1;
     Touch x{};
-    FlTouchCtx c{};
+    FlTouchFc tf{};
+    Prep tk{};
+    const FlowLvl* Lq = nullptr;
     bool first = true, last = true;
+    // (loads issued in dependence order, each stage's together: book -> header -> the touch, its
+    // neighbours and its fill context -> the taker's record and the level)
     if (g0w < total) {
       const uint32_t hb = fl_book_of_wave(F, nb, g0w, valid ? gt : g0w);
       if (valid) {
         h = F.h0 + hb;
         t = gt - F.toff[F.tb + hb];
-        gm = fl_amt_unit(F, h);
-        nt = F.hdr[h].ntouch;
-        beg = F.hdr[h].beg;
+        const FlowHdr& H = F.hdr[h];
+        gm = H.ok == FL_OK_ADD ? static_cast<int64_t>(H.g) : 1;  // (fl_amt_unit)
+        const uint32_t nt = H.ntouch;
+        beg = H.beg;
+        hend_j = H.end - beg;
+        sym = H.sym;
         L = FL_TOUCH_MUL * beg;
         x = F.log[L + t];
+        const uint32_t jm = t > 0 ? tk_j(F.log[L + t - 1]) : NIL, jp = t + 1 < nt ? tk_j(F.log[L + t + 1]) : NIL;
+        if (!COUNT) tf = F.tfc[L + t];  // (a CONS touch's; read before its kind is known)
         j = tk_j(x);
-        first = t == 0 || tk_j(F.log[L + t - 1]) != j;
-        last = t + 1 == nt || tk_j(F.log[L + t + 1]) != j;
-        if (((x.kr >> 7) & 1u) == TK_CONS) {
-          c = fl_touch_ctx(F, h, L, x, t);
-          cnt = c.last - c.first + 1;
+        first = jm != j;
+        last = jp != j;
+        const bool cons = ((x.kr >> 7) & 1u) == TK_CONS;
+        if (COUNT) {
+          if (cons) tf = F.tfc[L + t];
+        } else if (j < hend_j) {
+          tk = B.prep[beg + j];  // (padding records are never CONS and rest nowhere)
+        }
+        if (cons) {
+          if (!COUNT) Lq = fl_lvls(F, h) + tf.lvl;
+          cnt = tf.last - tf.first + 1;
           fills += cnt;
-          const int64_t lend = c.last < c.Lq->ig_n ? c.IG[c.last].e + c.IG[c.last].v
-                                                   : c.RS[c.last - c.Lq->ig_n].e + c.RS[c.last - c.Lq->ig_n].v;
-          pops += cnt - (lend > c.c + c.a ? 1u : 0u);
         }
       }
     }
@@ -2122,8 +2153,8 @@ __device__ __forceinline__ void fl_events_fused(const Dev& D, const BatchArgs& B
         if (tk_j(y) != j) break;
         carry_a += y.amt * gm;
         if (((y.kr >> 7) & 1u) == TK_CONS) {
-          const FlTouchCtx cy = fl_touch_ctx(F, h, L, y, u - 1);
-          carry_n += cy.last - cy.first + 1;
+          const FlTouchFc ty = F.tfc[L + u - 1];
+          carry_n += ty.last - ty.first + 1;
         }
       }
     }
@@ -2135,11 +2166,12 @@ __device__ __forceinline__ void fl_events_fused(const Dev& D, const BatchArgs& B
     const int64_t a_incl = wave_seg_incl<int64_t>(xa, heads) + (in_first_seg ? carry_a : 0);
     const uint32_t fb = n_incl - cnt;  // the touch's fill_idx base within its order
     const int64_t a_before = a_incl - xa;
-    if (valid && last && j < F.hdr[h].end - beg) B.ev_count[B.prep[beg + j].idx] = n_incl;  // (not padding)
     if (COUNT) {
+      if (valid && last && j < hend_j) B.ev_count[B.prep[beg + j].idx] = n_incl;  // (not padding)
       if (valid) F.fbase[L + t] = fb;
       continue;
     }
+    if (valid && last && j < hend_j) B.ev_count[tk.idx] = n_incl;
     if (F.xp & 1u) {  // (experiment: the touch pass alone)
       if (valid && n_incl == 0xFFFFFFFFu) F.fbase[L + t] = fb;
       continue;
@@ -2168,11 +2200,21 @@ __device__ __forceinline__ void fl_events_fused(const Dev& D, const BatchArgs& B
     FlEvLane r{};
     r.inc = inc;
     if (cnt) {
-      const Prep tk = B.prep[beg + j];
-      fl_ev_lane(r, c, L, beg, t, tk.idx, F.hdr[h].sym, tk.vol - a_before);  // (taker remaining before the level)
-      r.mb = c.first - (inc - cnt);
-      r.dbase = base + wb + (inc - cnt) - c.first;
-      r.fbm = fb - c.first;
+      r.ig_n = Lq->ig_n;
+      r.nra = Lq->nrest | (Lq->ig_all ? 0x80000000u : 0u);
+      r.igb = Lq->ig_base;
+      r.rsb = L + Lq->base;
+      r.price = Lq->price;
+      r.beg = beg;
+      r.t = t;
+      r.idx = tk.idx;
+      r.sym = sym;
+      r.c = tf.coord;
+      r.ca = tf.coord + x.amt * gm;
+      r.tbc = tk.vol - a_before + tf.coord;  // (taker remaining before the level, + c)
+      r.mb = tf.first - (inc - cnt);
+      r.dbase = base + wb + (inc - cnt) - tf.first;
+      r.fbm = fb - tf.first;
     }
     if (F.xp & 2u) {  // (experiment: no emission)
       if (r.inc == 0xFFFFFFFFu) B.arena[0].fill_idx = r.mb;
@@ -2180,22 +2222,19 @@ __device__ __forceinline__ void fl_events_fused(const Dev& D, const BatchArgs& B
     }
     fl_emit_wave<true>(B, F, B.arena, r);
   }
-  // the block's counts, then one stripe add per counter (ctr_add)
-  for (int off = 32; off > 0; off >>= 1) {
-    fills += __shfl_xor(fills, off);
-    pops += __shfl_xor(pops, off);
-  }
-  __shared__ unsigned long long wf[T / 64], wp[T / 64];
-  if (lane == 0) { wf[w] = fills; wp[w] = pops; }
+  // the block's fills, then one stripe add per counter (ctr_add).  (The makers the fills pop are
+  // counted by the writes, per level: fl_level_pops.)
+  for (int off = 32; off > 0; off >>= 1) fills += __shfl_xor(fills, off);
+  __shared__ unsigned long long wf[T / 64];
+  if (lane == 0) wf[w] = fills;
   __syncthreads();
   if (threadIdx.x == 0) {
-    fills = pops = 0;
-    for (uint32_t k = 0; k < T / 64; ++k) { fills += wf[k]; pops += wp[k]; }
+    fills = 0;
+    for (uint32_t k = 0; k < T / 64; ++k) fills += wf[k];
     if (fills) {
       ctr_add(D, C_FILLS, fills);
       ctr_add(D, C_HOT_FILLS, fills);
       if (F.h0 >= FL_HEAD) ctr_add(D, C_FLOW_TAIL_FILLS, fills);
-      ctr_add(D, C_RESTING_DELTA, static_cast<unsigned long long>(-static_cast<long long>(pops)));
     }
   }
 }
@@ -2242,11 +2281,19 @@ __device__ __forceinline__ FlWPlan fl_wplan(const FlowLvl& f, const RsEnt* RS) {
   return w;
 }
 
+// Makers of level f the batch's fills popped (filled to their whole volume): its consumed old
+// makers and its new makers wholly inside the consumption (fl_wplan's rf).  Counted here, per
+// level, rather than per fill by the event passes (where it cost a dependent load per touch).
+__device__ __forceinline__ uint32_t fl_level_pops(const FlowLvl& f, uint32_t rf) { return f.nv0 - f.nlive0 + rf; }
+__device__ __forceinline__ void ctr_pops(const Dev& D, uint32_t pops) {
+  if (pops) ctr_add(D, C_RESTING_DELTA, static_cast<unsigned long long>(-static_cast<long long>(pops)));
+}
+
 // claim: a deep tail book's pre-claimed chunk ids (k_deep_claim; FlowLvl::pad0 = the level's
 // first), else the level claims its own.
 __device__ __forceinline__ Level fl_write_level(const Dev& D, const BatchArgs& B, const FlowArgs& F,
                                                 const FlowHdr& hd, uint32_t h, uint32_t q,
-                                                const FlClaim* claim = nullptr) {
+                                                const FlClaim* claim = nullptr, uint32_t* pops = nullptr) {
   const uint32_t lane = lane_id();
   const uint32_t L = FL_TOUCH_MUL * hd.beg;
   const unsigned long long mask = D.idx_mask;
@@ -2258,6 +2305,7 @@ __device__ __forceinline__ Level fl_write_level(const Dev& D, const BatchArgs& B
   const FlWPlan wp = fl_wplan(f, RS);
   const uint32_t rf = wp.rf, S = wp.S, s0 = wp.s0, room = wp.room, need = wp.need;
   const bool fresh = wp.fresh;
+  if (pops) *pops += fl_level_pops(f, rf);
   // claim `need` chunk ids: free stack first, then the bump pointer
   int t = 0;
   uint32_t nst = 0, bb = 0;
@@ -2419,6 +2467,7 @@ __device__ __forceinline__ void fl_write_book(const Dev& D, const BatchArgs& B, 
   __shared__ uint32_t wrf[FL_CAP], wtl[FL_CAP], wbs[FL_CAP], ws0[FL_CAP];  // ws0: s0 | fresh << 31
   __shared__ int64_t wcf[FL_CAP];
   __shared__ FlClaim claim_s;
+  __shared__ uint32_t pops_s;
   if (h >= fl_hend(D, F) || F.hdr[h].ok != FL_OK_ADD) return;
   const FlowHdr hd = F.hdr[h];
   const uint32_t tid = threadIdx.x, lane = lane_id(), nl = hd.nl;
@@ -2448,6 +2497,7 @@ __device__ __forceinline__ void fl_write_book(const Dev& D, const BatchArgs& B, 
     cof[2 * tid] = static_cast<uint32_t>(ex);
     rof[2 * tid + 1] = static_cast<uint32_t>((ex + x0) >> 32);
     cof[2 * tid + 1] = static_cast<uint32_t>(ex + x0);
+    if (tid == 0) pops_s = 0;
     if (tid == 63) {
       const int64_t tot = ex + x;
       rof[128] = static_cast<uint32_t>(tot >> 32);
@@ -2519,6 +2569,7 @@ __device__ __forceinline__ void fl_write_book(const Dev& D, const BatchArgs& B, 
   }
   if (tid < nl) {  // the level's final record
     const FlowLvl& f = LV[tid + 1];
+    if (const uint32_t p = fl_level_pops(f, wrf[tid])) atomicAdd(&pops_s, p);
     const uint32_t q = tid + 1, S = rof[tid + 1] - rof[tid], need = cof[tid + 1] - cof[tid];
     const uint32_t s0 = ws0[tid] & 0x7FFFFFFFu;
     const bool fresh = ws0[tid] >> 31;
@@ -2557,6 +2608,7 @@ __device__ __forceinline__ void fl_write_book(const Dev& D, const BatchArgs& B, 
     }
   }
   __syncthreads();
+  if (tid == 0) ctr_pops(D, pops_s);
   fl_write_finish(D, hd, lv, keep, base_s, cap_s, nout_s);
 }
 __global__ __launch_bounds__(FL_WRITE_T) void k_flow_write(Dev D, BatchArgs B, FlowArgs F) {
@@ -2659,6 +2711,7 @@ __global__ __launch_bounds__(FL_LVB_T) void k_flow_write_lv_blk(Dev D, BatchArgs
     D.nodes[loc] = nd;
   }
   if (tid != 0) return;
+  ctr_pops(D, fl_level_pops(f, rf));
   Level x{};
   x.price = f.price;
   x.head = x.tail = NIL;

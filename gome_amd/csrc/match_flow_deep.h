@@ -625,6 +625,7 @@ __device__ __forceinline__ void k_deep_write_lv_one(Dev D, BatchArgs B, FlowArgs
   const FlowLvl* LV = fl_lvls(F, h);
   Level* out = F.dlvout + static_cast<size_t>(hd.dslot) * DEEP_CAP;
   const uint32_t lane = lane_id();
+  uint32_t pops = 0;  // (ADD books: fl_level_pops; books with DELs count theirs in k_fc_count)
   // A wave takes 64 consecutive levels: the untouched ones (no touch, so no append and nothing
   // consumed: the prep's FlowLvl is final) one per lane, then the touched ones one at a time.
   for (uint32_t q0 = 1 + blockIdx.x * 64u; q0 <= hd.nl; q0 += gridDim.x * 64u) {
@@ -652,10 +653,11 @@ __device__ __forceinline__ void k_deep_write_lv_one(Dev D, BatchArgs B, FlowArgs
     }
     for (unsigned long long tm = __ballot(touched); tm; tm &= tm - 1) {
       const uint32_t qq = q0 + static_cast<uint32_t>(__builtin_ctzll(tm));
-      const Level x = hd.dc ? fc_write_level(D, B, F, hd, h, qq) : fl_write_level(D, B, F, hd, h, qq, claim);
+      const Level x = hd.dc ? fc_write_level(D, B, F, hd, h, qq) : fl_write_level(D, B, F, hd, h, qq, claim, &pops);
       if (lane == 0) out[qq] = x;
     }
   }
+  if (lane == 0) ctr_pops(D, pops);
 }
 __global__ __launch_bounds__(64) void k_deep_write_lv(Dev D, BatchArgs B, FlowArgs F) {
   for (uint32_t i = blockIdx.y; i < fd_nslots(F); i += gridDim.y) {

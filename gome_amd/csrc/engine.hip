@@ -245,6 +245,7 @@ struct gome_engine {
   // plan (config 3: +0.2 ms), so with a hot book the fused launch (GOME_TAIL_SPLIT=0/1 forces)
   int tail_split = -1;
   bool tail_serial = false;
+  int prep_wait = -1;  // k_prep after the head's prep always (1) / adaptive (-1; GOME_PREP_WAIT, A/B)
   uint32_t ev_xp = 0;  // the split tail's events after its writes on one stream (solo kernel times)
   bool adm_fast = true;
   // GOME_PH_* timing events (gome_stats.ms_phase): ~24 event records per batch, 0.12 ms on config 2's
@@ -426,6 +427,7 @@ gome_status gome_engine::init(const gome_config& c) {
   if (const char* g = std::getenv("GOME_TAIL_GRID")) tail_grid = std::max(64, std::atoi(g));  // (tuning)
   if (const char* g = std::getenv("GOME_TAIL_SPLIT")) tail_split = std::atoi(g) != 0 ? 1 : 0;  // (A/B)
   if (const char* g = std::getenv("GOME_TAIL_SERIAL")) tail_serial = std::atoi(g) != 0;         // (profiling)
+  if (const char* g = std::getenv("GOME_PREP_WAIT")) prep_wait = std::atoi(g) != 0 ? 1 : 0;       // (A/B)
   if (const char* g = std::getenv("GOME_EV_XP")) ev_xp = static_cast<uint32_t>(std::atoi(g));     // (profiling)
   if (const char* g = std::getenv("GOME_ADM_FAST")) adm_fast = std::atoi(g) != 0;              // (A/B)
   phases = (cfg.flags & GOME_FLAG_PHASES) != 0;
@@ -811,7 +813,9 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   HIPCHK(hipStreamWaitEvent(s, adm_done, 0));
   // k_prep gathers the same records as the head's prep: let the head's prep (the critical
   // path) have the memory system first; the cold books have slack
-  HIPCHK(hipStreamWaitEvent(s, prep_h, 0));  // (A/B r3j: without it config 2 -0.14 ms, config 3 +0.2 ms)
+  // (only when one book dominates the batch, the split_tail test: A/B r3j, without the wait
+  // config 2 -0.14 ms, config 3 +0.2 ms; with no dominant book the tail's chain is the critical path)
+  if (!split_tail || prep_wait > 0) HIPCHK(hipStreamWaitEvent(s, prep_h, 0));
 
   // ---- match_books: one wavefront per book; hot books (LDS) on a second stream,
   //      concurrently with the cold books (HBM)

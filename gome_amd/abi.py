@@ -95,6 +95,8 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.gome_submit_batch_device.argtypes = [VP, VP, C.c_size_t, C.c_uint64, VP]
     lib.gome_submit_batch_async.argtypes = [VP, VP, C.c_size_t, C.c_uint64]
     lib.gome_collect.argtypes = [VP, P(VP), P(C.c_size_t), P(Stats)]
+    lib.gome_submit_batch_device_async.argtypes = [VP, VP, C.c_size_t, C.c_uint64]
+    lib.gome_collect_device.argtypes = [VP, P(VP), P(C.c_size_t), P(Stats)]
     lib.gome_inflight.argtypes = [VP]
     lib.gome_inflight.restype = C.c_size_t
     lib.gome_host_alloc.argtypes = [VP, C.c_size_t, P(VP)]
@@ -139,7 +141,8 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
               "gome_device_events", "gome_get_stats", "gome_snapshot_levels", "gome_snapshot_fifo",
               "gome_fixed_from_double", "gome_fixed_from_scaled", "gome_submit_batch_async",
               "gome_collect", "gome_host_alloc", "gome_load_books", "gome_dup_records",
-              "gome_take_deferred", "gome_top_of_book"):
+              "gome_take_deferred", "gome_top_of_book", "gome_submit_batch_device_async",
+              "gome_collect_device"):
         getattr(lib, f).restype = C.c_int32
     _lib = lib
     return lib
@@ -259,6 +262,17 @@ class Engine:
     def submit_device(self, dev_ptr: int, n: int, seq_base: int = 0, stream: int | None = None):
         self._check(self.lib.gome_submit_batch_device(self.h, C.c_void_p(dev_ptr), n, seq_base,
                                                       C.c_void_p(stream or 0)))
+
+    # ---- pipelined device path (gome_submit_batch_device_async / gome_collect_device)
+    def submit_device_async(self, dev_ptr: int, n: int, seq_base: int = 0):
+        """Queue a batch already in HBM (it must stay unchanged until collected)."""
+        self._check(self.lib.gome_submit_batch_device_async(self.h, C.c_void_p(dev_ptr), n, seq_base))
+
+    def collect_device(self):
+        """(device pointer, count) of the oldest in-flight device batch's events and its stats."""
+        p, n, st = C.c_void_p(), C.c_size_t(), Stats()
+        self._check(self.lib.gome_collect_device(self.h, C.byref(p), C.byref(n), C.byref(st)))
+        return (p.value or 0), n.value, st.as_dict()
 
     # ---- pipelined host path (gome_submit_batch_async / gome_collect)
     def host_buffer(self, n: int) -> np.ndarray:

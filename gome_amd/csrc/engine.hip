@@ -215,6 +215,7 @@ struct Slot {
 struct Flight {
   uint32_t slot, n;
   uint64_t seq_base;
+  bool dev;  // records in the caller's HBM (gome_submit_batch_device_async)
 };
 
 }  // namespace
@@ -1190,6 +1191,10 @@ gome_status gome_engine::collect(const gome_event** evs, size_t* nev) {
 // goes on.  Only a failure that leaves the engine unusable (poisoned, or a HIP error) is returned.
 gome_status gome_engine::collect_all() {
   gome_status fatal = GOME_OK;
+  // (a device batch collected by gome_collect_device is older than those still in flight)
+  if (!flights.empty()) {
+    if (gome_status st = spill_device_events()) return st;
+  }
   while (!flights.empty()) {
     const gome_event* evs = nullptr;
     size_t n = 0;
@@ -1319,7 +1324,54 @@ gome_status gome_submit_batch_async(gome_engine* e, const gome_order* orders, si
     if ((st = e->enqueue(S.d_orders, static_cast<uint32_t>(n), e->stream, sl, seq_base, inflight_n)) != GOME_OK)
       return st;
   }
-  e->flights.push_back(Flight{sl, static_cast<uint32_t>(n), seq_base});
+  e->flights.push_back(Flight{sl, static_cast<uint32_t>(n), seq_base, false});
+  return GOME_OK;
+}
+
+gome_status gome_submit_batch_device_async(gome_engine* e, const gome_order* dev_orders, size_t n,
+                                           uint64_t seq_base) {
+  if (!e) return GOME_E_INVAL;
+  if (e->flights.size() >= GOME_MAX_INFLIGHT)
+    return e->fail(GOME_E_STATE, "GOME_MAX_INFLIGHT batches in flight: gome_collect first");
+  gome_status st = e->spill_device_events();
+  if (st != GOME_OK) return st;
+  if ((st = e->check_submit(n, dev_orders)) != GOME_OK) return st;
+  uint64_t inflight_n = 0;
+  for (const Flight& f : e->flights) inflight_n += f.n;
+  if (n && (st = e->check_capacity(n, inflight_n)) != GOME_OK) return st;
+  const uint32_t sl = e->take_slot();
+  if (n) {
+    e->used = true;
+    if ((st = e->enqueue(dev_orders, static_cast<uint32_t>(n), e->stream, sl, seq_base, inflight_n)) != GOME_OK)
+      return st;
+  }
+  e->flights.push_back(Flight{sl, static_cast<uint32_t>(n), seq_base, true});
+  return GOME_OK;
+}
+
+gome_status gome_collect_device(gome_engine* e, const gome_event** dev_events, size_t* n_events,
+                                gome_stats* stats) {
+  if (!e || !dev_events || !n_events) return GOME_E_INVAL;
+  *dev_events = nullptr;
+  *n_events = 0;
+  if (e->flights.empty()) return e->fail(GOME_E_NOTFOUND, "no batch in flight");
+  const Flight f = e->flights.front();
+  if (!f.dev) return e->fail(GOME_E_STATE, "the oldest batch in flight is a host batch: gome_collect");
+  e->flights.pop_front();
+  gome_status st = e->spill_device_events();
+  if (st != GOME_OK) return st;
+  if (f.n) {
+    Slot& S = e->slots[f.slot];
+    hipError_t he = hipEventSynchronize(S.done);
+    if (he != hipSuccess) return e->fail(GOME_E_DEVICE, hipGetErrorString(he));
+    if ((st = e->finish(f.slot, f.n)) != GOME_OK) return st;
+    e->dev_slot = f.slot;
+    e->dev_events = S.h_st->n_events;
+    e->dev_events_pos = 0;
+    *dev_events = S.d_events;
+    *n_events = e->dev_events;
+  }
+  if (stats) *stats = e->stats;
   return GOME_OK;
 }
 

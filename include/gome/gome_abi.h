@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define GOME_ABI_VERSION 6u
+#define GOME_ABI_VERSION 7u
 
 /* ---- status codes (replace the reference's swallowed errors / panics,
  *      rabbitmq.go:44-49,70-72,120-122; nodelink.go:132,142,157) ---------- */
@@ -322,6 +322,17 @@ gome_status gome_submit_batch_async(gome_engine* e, const gome_order* orders, si
 gome_status gome_collect(gome_engine* e, const gome_event** events, size_t* n_events,
                          gome_stats* stats);
 size_t gome_inflight(const gome_engine* e);
+/* The same pipeline with the records already in HBM (ABI >= 7): submit device batch k+1, then
+ * collect device batch k, so the host's enqueue of one batch hides under the device's work on
+ * the other.  `dev_orders` must stay valid and unchanged until the batch is collected.  The
+ * collect returns the batch's events in device memory (publish order, as gome_device_events):
+ * valid until the next submit or collect, which first moves them to the host drain queue
+ * unless gome_release_device_events said a device-side consumer took them.  GOME_E_STATE when the
+ * oldest batch in flight is a host batch (gome_collect takes those). */
+gome_status gome_submit_batch_device_async(gome_engine* e, const gome_order* dev_orders, size_t n,
+                                           uint64_t seq_base);
+gome_status gome_collect_device(gome_engine* e, const gome_event** dev_events, size_t* n_events,
+                                gome_stats* stats);
 /* The first failure of an in-flight batch that a synchronous call collected since the last
  * gome_take_deferred (its message then in gome_last_error), or GOME_OK; clears it. */
 gome_status gome_take_deferred(gome_engine* e);

@@ -35,6 +35,17 @@ for P in $PARTS; do
         -- python3 bench.py --workload config2 --steps 5 --warmup 5 --e2e-steps 0 --no-cpu-baseline --no-phase-pass > $OUT/xp$X.log 2>&1 || exit 4
       python3 tools/timeline.py $OUT/xp$X/run_kernel_trace.csv 2 | grep -E "k_flow_events_fused  grid 1048576|k_flow_write  grid" | sed "s/^/xp$X /"
     done ;;
+  pipe)  # synchronous vs pipelined steps (bench.py --sync), configs from ABW, alternating
+    for R in 1 2; do
+      for M in sync pipe; do
+        for W in ${ABW:-config2 config3}; do
+          F=""; [ $M = sync ] && F="--sync"
+          timeout -k 10 300 python3 -u bench.py --workload $W --steps 10 --warmup 5 --e2e-steps 0 --no-cpu-baseline \
+            --no-phase-pass $F > $OUT/${M}_${W}_$R.jsonl 2> $OUT/${M}_${W}_$R.log || { tail -20 $OUT/${M}_${W}_$R.log; exit 12; }
+          python3 -c "import json; d=json.loads(open('$OUT/${M}_${W}_$R.jsonl').readlines()[-1]); print('$M $W $R', d['value'], d['ms_per_step'], d['p50_batch_ms'])"
+        done
+      done
+    done ;;
   c3t)
     timeout -k 10 300 rocprofv3 --kernel-trace --stats -T --output-format csv -d $OUT/c3trace -o run \
       -- python3 bench.py --workload config3 --steps 5 --warmup 5 --e2e-steps 0 --no-cpu-baseline > $OUT/c3_trace.log 2>&1 || exit 5 ;;

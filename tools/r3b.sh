@@ -46,6 +46,12 @@ for P in $PARTS; do
         done
       done
     done ;;
+  sweep)  # config 3 batch sweep: value vs the critical-path bound (bench.py critical_path)
+    for B in 1048576 2097152 4194304; do
+      timeout -k 10 300 python3 -u bench.py --workload config3 --batch $B --steps 10 --warmup 4 --e2e-steps 0 \
+        --no-cpu-baseline > $OUT/sweep_$B.jsonl 2> $OUT/sweep_$B.log || { tail -20 $OUT/sweep_$B.log; exit 13; }
+      python3 -c "import json; d=json.loads(open('$OUT/sweep_$B.jsonl').readlines()[-1]); print('$B', d['value'], d['ms_per_step'], d['critical_path'])"
+    done ;;
   c3t)
     timeout -k 10 300 rocprofv3 --kernel-trace --stats -T --output-format csv -d $OUT/c3trace -o run \
       -- python3 bench.py --workload config3 --steps 5 --warmup 5 --e2e-steps 0 --no-cpu-baseline > $OUT/c3_trace.log 2>&1 || exit 5 ;;

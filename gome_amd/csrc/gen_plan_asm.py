@@ -1105,24 +1105,22 @@ class GenDV(GenD):
         e(f"s_add_u32 {MC}, {MC}, 1")
 
     def word_add(self, lvl: str, amt: str):
-        """Word lvl += amt (the amount may be 0); exec is left narrowed."""
+        """Word lvl += amt (the amount may be 0); exec is left narrowed.  (The 64-bit shift takes
+        its count mod 64: lane lvl & 63 without a mask; the SGPR amount is the add's src0, the
+        indexed word its src1 and destination.)"""
         e = self.e
         e(f"s_lshr_b32 {T0}, {lvl}, 6")
-        e(f"s_and_b32 s79, {lvl}, 63")
-        e("s_lshl_b64 exec, 1, s79")
-        e(f"v_mov_b32 v{VAM}, {amt}")
-        e(f"s_set_gpr_idx_on {T0}, gpr_idx(SRC0,DST)")
-        e(f"v_add_u32 v{VB}, v{VB}, v{VAM}")
+        e(f"s_lshl_b64 exec, 1, {lvl}")
+        e(f"s_set_gpr_idx_on {T0}, gpr_idx(SRC1,DST)")
+        e(f"v_add_u32 v{VB}, {amt}, v{VB}")
         e("s_set_gpr_idx_off")
 
     def word_set(self, lvl: str, val: str):
         e = self.e
         e(f"s_lshr_b32 {T0}, {lvl}, 6")
-        e(f"s_and_b32 s79, {lvl}, 63")
-        e("s_lshl_b64 exec, 1, s79")
-        e(f"v_mov_b32 v{VAM}, {val}")
+        e(f"s_lshl_b64 exec, 1, {lvl}")
         e(f"s_set_gpr_idx_on {T0}, gpr_idx(DST)")
-        e(f"v_mov_b32 v{VB}, v{VAM}")
+        e(f"v_mov_b32 v{VB}, {val}")
         e("s_set_gpr_idx_off")
 
     def next_top(self, sd: str):
@@ -1170,10 +1168,8 @@ class GenDV(GenD):
         e(f"s_lshl_b32 {LN}, {LN}, 5")
         e(f"s_add_u32 {G}, {G}, {LN}")                      # the register
         e("s_mov_b64 exec, -1")
-        e(f"s_set_gpr_idx_on {G}, gpr_idx(SRC0)")
-        e(f"v_mov_b32 v{VTR}, v{VB}")
-        e("s_set_gpr_idx_off")
-        e(f"v_cmp_ne_u32_e64 {M}, 0, v{VTR}")
+        e(f"s_set_gpr_idx_on {G}, gpr_idx(SRC0)")          # (on until the word's read below)
+        e(f"v_cmp_ne_u32_e64 {M}, v{VB}, 0")
         if asks:   # lanes >= c & 63 when G == R
             e(f"s_lshl_b64 {MS}, -1, {T0}")
         else:      # lanes <= c & 63
@@ -1184,7 +1180,7 @@ class GenDV(GenD):
         e(f"s_and_b64 {MS}, {MS}, {M}")
         e(f"s_cbranch_scc0 {nxt}")
         stale = self.fresh("NS")
-        blk = [f"{nxt}:", f"s_cmp_eq_u32 {G}, {R}", f"s_cbranch_scc0 {stale}"]
+        blk = [f"{nxt}:", "s_set_gpr_idx_off", f"s_cmp_eq_u32 {G}, {R}", f"s_cbranch_scc0 {stale}"]
         if asks:   # on from the next register
             blk += [f"s_add_u32 {T0}, {R}, 1", f"s_lshl_b32 {T0}, {T0}, 6"]
         else:      # (R > 0: the bid sentinel is word 0 of register 0)
@@ -1198,7 +1194,8 @@ class GenDV(GenD):
         else:
             e(f"s_flbit_i32_b64 {MK}, {MS}")
             e(f"s_sub_u32 {MK}, 63, {MK}")
-        e(f"v_readlane_b32 {topd[0]}, v{VTR}, {MK}")
+        e(f"v_readlane_b32 {topd[0]}, v{VB}, {MK}")
+        e("s_set_gpr_idx_off")
         e(f"s_lshl_b32 {top}, {G}, 6")
         e(f"s_add_u32 {top}, {top}, {MK}")
         e(f"s_lshl_b64 exec, 1, {MK}")

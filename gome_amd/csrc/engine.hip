@@ -245,9 +245,8 @@ struct gome_engine {
   // faster on config 2, but the split events kernel's traffic slows a concurrent hottest-book
   // plan (config 3: +0.2 ms), so with a hot book the fused launch (GOME_TAIL_SPLIT=0/1 forces)
   int tail_split = -1;
-  bool tail_serial = false;
+  bool tail_serial = false;  // the split tail's events after its writes on one stream (GOME_TAIL_SERIAL: solo kernel times)
   int prep_wait = -1;  // k_prep after the head's prep always (1) / adaptive (-1; GOME_PREP_WAIT, A/B)
-  uint32_t ev_xp = 0;  // the split tail's events after its writes on one stream (solo kernel times)
   bool adm_fast = true;
   // GOME_PH_* timing events (gome_stats.ms_phase): ~24 event records per batch, 0.12 ms on config 2's
   // critical path, so only on request (GOME_FLAG_PHASES, or GOME_PHASES=1)
@@ -429,7 +428,6 @@ gome_status gome_engine::init(const gome_config& c) {
   if (const char* g = std::getenv("GOME_TAIL_SPLIT")) tail_split = std::atoi(g) != 0 ? 1 : 0;  // (A/B)
   if (const char* g = std::getenv("GOME_TAIL_SERIAL")) tail_serial = std::atoi(g) != 0;         // (profiling)
   if (const char* g = std::getenv("GOME_PREP_WAIT")) prep_wait = std::atoi(g) != 0 ? 1 : 0;       // (A/B)
-  if (const char* g = std::getenv("GOME_EV_XP")) ev_xp = static_cast<uint32_t>(std::atoi(g));     // (profiling)
   if (const char* g = std::getenv("GOME_ADM_FAST")) adm_fast = std::atoi(g) != 0;              // (A/B)
   phases = (cfg.flags & GOME_FLAG_PHASES) != 0;
   if (const char* g = std::getenv("GOME_PHASES")) phases = std::atoi(g) != 0;
@@ -708,7 +706,6 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   const bool c_deep = (ch & FL_CH_DEEP) != 0, c_canc = (ch & FL_CH_CANCEL) != 0;
   S.chains = ch;
   F.chains = ch;
-  F.xp = ev_xp;
   const bool split_tail = tail_split >= 0 ? tail_split != 0 : last_maxseg * 16 < last_n;
   FlowArgs FH = F, FH0 = F, FH1 = F, FT = F;
   FH.h0 = 0; FH.h1 = FL_HEAD; FH.tb = 0;
@@ -980,7 +977,6 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   HIPCHK(hipStreamWaitEvent(s, cnt_done, 0));
 
   HIPCHK(hipEventRecord(S.evm1, s));
-  if (ev_xp & 2u) HIPCHK(hipMemsetAsync(&d_st->ev_bump, 0, 4, s));  // (experiment: nothing was written)
 
   // ---- event compaction into publish order
   HIPCHK(mark(GOME_PH_PUBLISH, 0, s));

@@ -211,7 +211,6 @@ struct FlowArgs {
   // the chains this batch enqueued (FL_CH_*): a candidate that needs one that is not there is
   // declined to the legacy / cold kernels (and counted in C_WANT_*, which re-enables it)
   uint32_t chains;
-  uint32_t xp;  // (profiling experiments, GOME_EV_XP; 0 in the product)
   // the candidates [h0, min(h1, nhot)) this launch covers (head and tail run on their own
   // streams), and the range's offset in toff
   uint32_t h0, h1, tb;
@@ -2147,7 +2146,7 @@ __device__ __forceinline__ void fl_events_fused(const Dev& D, const BatchArgs& B
     const unsigned long long heads = __ballot(first);
     uint32_t carry_n = 0;
     int64_t carry_a = 0;
-    if (lane == 0 && !first && !(F.xp & 8u)) {
+    if (lane == 0 && !first) {
       for (uint32_t u = t; u > 0; --u) {
         const Touch y = F.log[L + u - 1];
         if (tk_j(y) != j) break;
@@ -2172,10 +2171,6 @@ __device__ __forceinline__ void fl_events_fused(const Dev& D, const BatchArgs& B
       continue;
     }
     if (valid && last && j < hend_j) B.ev_count[tk.idx] = n_incl;
-    if (F.xp & 1u) {  // (experiment: the touch pass alone)
-      if (valid && n_incl == 0xFFFFFFFFu) F.fbase[L + t] = fb;
-      continue;
-    }
     // arena slots: one bump allocation per block tile
     uint32_t inc = cnt;
     for (uint32_t off = 1; off < 64; off <<= 1) {
@@ -2215,10 +2210,6 @@ __device__ __forceinline__ void fl_events_fused(const Dev& D, const BatchArgs& B
       r.mb = tf.first - (inc - cnt);
       r.dbase = base + wb + (inc - cnt) - tf.first;
       r.fbm = fb - tf.first;
-    }
-    if (F.xp & 2u) {  // (experiment: no emission)
-      if (r.inc == 0xFFFFFFFFu) B.arena[0].fill_idx = r.mb;
-      continue;
     }
     fl_emit_wave<true>(B, F, B.arena, r);
   }

@@ -86,6 +86,13 @@ __global__ void k_recycle_fin(Dev D) {
 }
 
 // Level blocks released this batch -> their class's free stack (block c = class c).
+// The slot's segmentation results into the batch's Status (after its per-batch reset).
+__global__ void k_sort_status(Status* st, const Status* sst) {
+  st->nseg = sst->nseg;
+  st->nhot = sst->nhot;
+  st->ctr[C_MAXSEG] = sst->ctr[C_MAXSEG];
+}
+
 // Batch end: the striped counters (ctr_add) into Status::ctr, the stripes zeroed for the next batch.
 __global__ void k_ctr_fold(Dev D) {
   const uint32_t c = threadIdx.x;
@@ -210,6 +217,15 @@ struct Slot {
   bool ph_on[GOME_NPHASE]{};
   double ms_enqueue = 0;  // host wall time of enqueue()
   uint32_t chains = 0;    // the flow chains (FL_CH_*) the batch enqueued
+  // the batch's radix sort and segments (per slot: with two batches in flight the next
+  // batch's sort runs during this one's hottest plan, see enqueue)
+  uint32_t *k0 = nullptr, *v0 = nullptr, *k1 = nullptr, *v1 = nullptr, *hist = nullptr, *bsum = nullptr;
+  uint32_t* tmp = nullptr;        // flags / segpos (n)
+  uint32_t* seg_start = nullptr;
+  uint32_t* seg_order = nullptr;
+  uint32_t* bcnt = nullptr;       // 32 counts + 32 offsets
+  Status* sst = nullptr;          // the segmentation's nseg / nhot / C_MAXSEG, copied to Status by k_sort_status
+  hipEvent_t sorted{};
 };
 
 struct Flight {
@@ -254,14 +270,9 @@ struct gome_engine {
   uint64_t last_maxseg = 0, last_n = 0;  // the last finished batch's hottest book / size
   uint32_t hist_cap = 0, bsum_cap = 0;
   unsigned long long idx_cap = 0;
-  // batch buffers
-  uint32_t *d_k0 = nullptr, *d_v0 = nullptr, *d_k1 = nullptr, *d_v1 = nullptr;
-  uint32_t* d_hist = nullptr;
+  // batch buffers (the sort's and the segments' are per slot: Slot)
   uint32_t* d_bsum = nullptr;
-  uint32_t* d_tmp = nullptr;  // flags / segpos (n)
-  uint32_t* d_seg_start = nullptr;
-  uint32_t* d_seg_order = nullptr;
-  uint32_t* d_bcnt = nullptr;  // 32 counts + 32 offsets
+  bool sort_ahead = true;  // pipelined batches sort on the copy stream during the last one's plan (GOME_SORT_AHEAD=0: A/B)
   unsigned long long* d_adm = nullptr;  // admission table (k_adm)
   unsigned long long* d_dup = nullptr;  // (S, uuid, oid) table of the records whose (S, oid) repeats
   uint8_t* d_multi = nullptr;           // per (S, oid) slot: the key repeats in the batch
@@ -326,7 +337,8 @@ struct gome_engine {
     for (Slot& S : slots) {
       if (S.h_st) (void)hipHostFree(S.h_st);
       if (S.h_events) (void)hipHostFree(S.h_events);
-      for (hipEvent_t ev : {S.ev0, S.ev1, S.evm0, S.evm1, S.evh0, S.evh1, S.evf0, S.evf1, S.evc0, S.evc1, S.h2d, S.done})
+      for (hipEvent_t ev : {S.ev0, S.ev1, S.evm0, S.evm1, S.evh0, S.evh1, S.evf0, S.evf1, S.evc0, S.evc1, S.h2d, S.done,
+                            S.sorted})
         if (ev) (void)hipEventDestroy(ev);
       for (auto& pr : S.ph)
         for (hipEvent_t ev : pr)
@@ -342,9 +354,9 @@ struct gome_engine {
   }
 
   gome_status init(const gome_config& c);
-  void scan(const uint32_t* in, uint32_t m, uint32_t* out, uint32_t* total, hipStream_t s);
+  void scan(const uint32_t* in, uint32_t m, uint32_t* out, uint32_t* total, hipStream_t s, uint32_t* bsum = nullptr);
   gome_status enqueue(const gome_order* d_ord, uint32_t n, hipStream_t s, uint32_t slot, uint64_t seq_base,
-                      uint64_t inflight_n);
+                      uint64_t inflight_n, bool ahead = false);
   gome_status finish(uint32_t slot, uint32_t n);
   gome_status check_submit(size_t n, const void* p);
   gome_status load_books(size_t nb, const uint32_t* bsym, const uint32_t* bnlv, const gome_level* lv,
@@ -405,6 +417,7 @@ gome_status gome_engine::init(const gome_config& c) {
       for (hipEvent_t& ev : pr) HIPCHK(hipEventCreate(&ev));
     HIPCHK(hipEventCreateWithFlags(&S.h2d, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&S.done, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&S.sorted, hipEventDisableTiming));
     HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&S.h_st), sizeof(Status), hipHostMallocDefault));
   }
   HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_match_hot),
@@ -428,6 +441,7 @@ gome_status gome_engine::init(const gome_config& c) {
   if (const char* g = std::getenv("GOME_TAIL_SPLIT")) tail_split = std::atoi(g) != 0 ? 1 : 0;  // (A/B)
   if (const char* g = std::getenv("GOME_TAIL_SERIAL")) tail_serial = std::atoi(g) != 0;         // (profiling)
   if (const char* g = std::getenv("GOME_PREP_WAIT")) prep_wait = std::atoi(g) != 0 ? 1 : 0;       // (A/B)
+  if (const char* g = std::getenv("GOME_SORT_AHEAD")) sort_ahead = std::atoi(g) != 0;           // (A/B)
   if (const char* g = std::getenv("GOME_ADM_FAST")) adm_fast = std::atoi(g) != 0;              // (A/B)
   phases = (cfg.flags & GOME_FLAG_PHASES) != 0;
   if (const char* g = std::getenv("GOME_PHASES")) phases = std::atoi(g) != 0;
@@ -486,11 +500,13 @@ gome_status gome_engine::init(const gome_config& c) {
                                   : 2ull * nb + cfg.max_nodes + EVB * std::min<uint64_t>(nb, ms) + 1024;
   if (evcap > 0xF0000000ull) evcap = 0xF0000000ull;
   arena_cap = static_cast<uint32_t>(evcap);
-  if (!alloc(&d_k0, nb, "keys0") || !alloc(&d_v0, nb, "vals0") ||
-      !alloc(&d_k1, nb, "keys1") || !alloc(&d_v1, nb, "vals1") || !alloc(&d_hist, hist_cap, "hist") ||
-      !alloc(&d_bsum, bsum_cap, "scan") || !alloc(&d_tmp, nb, "segflags") ||
-      !alloc(&d_seg_start, nb + 1, "seg_start") || !alloc(&d_seg_order, nb, "seg_order") ||
-      !alloc(&d_bcnt, 64, "buckets") || !alloc(&d_adm, adm_mask + 1ull, "adm_table") ||
+  for (Slot& S : slots)
+    if (!alloc(&S.k0, nb, "keys0") || !alloc(&S.v0, nb, "vals0") || !alloc(&S.k1, nb, "keys1") ||
+        !alloc(&S.v1, nb, "vals1") || !alloc(&S.hist, hist_cap, "hist") || !alloc(&S.bsum, bsum_cap, "sort scan") ||
+        !alloc(&S.tmp, nb, "segflags") || !alloc(&S.seg_start, nb + 1, "seg_start") ||
+        !alloc(&S.seg_order, nb, "seg_order") || !alloc(&S.bcnt, 64, "buckets") || !alloc(&S.sst, 1, "sort status"))
+      return GOME_E_CAPACITY;
+  if (!alloc(&d_bsum, bsum_cap, "scan") || !alloc(&d_adm, adm_mask + 1ull, "adm_table") ||
       !alloc(&d_dup, adm_mask + 1ull, "admission key table") ||
       !alloc(&d_multi, adm_mask + 1ull, "admission repeat flags") ||
       !alloc(&d_first, adm_mask + 1ull, "first admitted ADDs") ||
@@ -570,18 +586,19 @@ gome_status gome_engine::init(const gome_config& c) {
 }
 
 void gome_engine::scan(const uint32_t* in, uint32_t m, uint32_t* out, uint32_t* total,
-                       hipStream_t s) {
+                       hipStream_t s, uint32_t* bsum) {
   const uint32_t nb = ceil_div(m, SCAN_TILE);
-  k_scan_reduce<<<nb, SCAN_T, 0, s>>>(in, m, d_bsum);
-  k_scan_spine<<<1, SCAN_T, 0, s>>>(d_bsum, nb, total);
-  k_scan_down<<<nb, SCAN_T, 0, s>>>(in, m, d_bsum, out);
+  if (!bsum) bsum = d_bsum;  // (the sorts' scans have their slot's: they may run beside a batch's)
+  k_scan_reduce<<<nb, SCAN_T, 0, s>>>(in, m, bsum);
+  k_scan_spine<<<1, SCAN_T, 0, s>>>(bsum, nb, total);
+  k_scan_down<<<nb, SCAN_T, 0, s>>>(in, m, bsum, out);
 }
 
 // Enqueue batch `n` records at d_ord through the whole device pipeline on stream s (plus the
 // flow / hot streams it forks), publishing into slot `sl`.  Ends with the Status copy to the
 // slot's page-locked status and the slot's `done` event; finish() reads them.
 gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_t s, uint32_t sl,
-                                 uint64_t seq_base, uint64_t inflight_n) {
+                                 uint64_t seq_base, uint64_t inflight_n, bool ahead) {
   Slot& S = slots[sl];
   const auto t_enq = std::chrono::steady_clock::now();
   // conservative event bound: one partial per ADD + one event per DEL + one per popped
@@ -623,43 +640,63 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
     S.ph_on[ph] = true;
     return hipEventRecord(S.ph[ph][end], st);
   };
-  // per-batch status reset (free_top / freed_top and the level pools persist)
-  HIPCHK(hipMemsetAsync(d_st, 0, offsetof(Status, free_top), s));
+  // ---- stable radix sort of (symbol_id, seq) and the segments, into the slot's buffers.  They
+  // read only the records, so a pipelined batch (ahead: its records are complete on the copy
+  // stream, H2D included) sorts there as soon as the batch before it has started its hottest
+  // book's plan (that batch's head prep done: prep_h, recorded by its enqueue), beside that
+  // plan; the caller's stream picks the results up with one small status copy.
+  // (only when one book dominates the batch: with none, the caller's stream carries the batch's
+  // critical path from start to end and the early sort only competes with the batch before;
+  // A/B: config 3 -0.1..0.2 ms, config 2 +0.02 ms)
+  const bool dominant = !(last_maxseg * 16 < last_n);
+  hipStream_t ss = (ahead && sort_ahead && dominant) ? copy_stream : s;
+  // per-batch status reset (free_top / freed_top and the level pools persist); admission
+  // (flow stream) starts from fork_adm, beside the sort when both are on the caller's stream
+  auto status_reset = [&]() -> hipError_t {
+    hipError_t he = hipMemsetAsync(d_st, 0, offsetof(Status, free_top), s);
+    return he == hipSuccess ? hipEventRecord(fork_adm, s) : he;
+  };
+  if (ss == s) HIPCHK(status_reset());
+  else HIPCHK(hipStreamWaitEvent(ss, prep_h, 0));
   const uint32_t T256 = 256, gN = ceil_div(n, T256);
-  HIPCHK(hipEventRecord(fork_adm, s));  // (admission, enqueued after the sort, starts from here)
-  // ---- stable radix sort of (symbol_id, seq)
-  HIPCHK(mark(GOME_PH_SORT, 0, s));
+  HIPCHK(mark(GOME_PH_SORT, 0, ss));
+  HIPCHK(hipMemsetAsync(S.sst, 0, sizeof(Status), ss));
   const uint32_t nblk = ceil_div(n, RS_TILE);
-  uint32_t *kin = nullptr, *vin = nullptr, *kout = d_k0, *vout = d_v0;
+  uint32_t *kin = nullptr, *vin = nullptr, *kout = S.k0, *vout = S.v0;
   for (uint32_t p = 0; p < passes; ++p) {
     const uint32_t shift = p * dbits;
     const uint32_t bits = std::min(dbits, key_bits - shift);
-    if (p == 0) {  // the keys out of the records into d_k1 (the second pass's output) first
-      k_radix_hist<true><<<nblk, RS_T, 0, s>>>(d_ord, nullptr, d_k1, n, shift, bits, d_hist, nblk);
-      scan(d_hist, (1u << bits) * nblk, d_hist, nullptr, s);
-      k_radix_scatter<true><<<nblk, RS_T, 0, s>>>(d_k1, nullptr, n, shift, bits, d_hist, kout, vout, nblk);
+    if (p == 0) {  // the keys out of the records into k1 (the second pass's output) first
+      k_radix_hist<true><<<nblk, RS_T, 0, ss>>>(d_ord, nullptr, S.k1, n, shift, bits, S.hist, nblk);
+      scan(S.hist, (1u << bits) * nblk, S.hist, nullptr, ss, S.bsum);
+      k_radix_scatter<true><<<nblk, RS_T, 0, ss>>>(S.k1, nullptr, n, shift, bits, S.hist, kout, vout, nblk);
     } else {
-      k_radix_hist<false><<<nblk, RS_T, 0, s>>>(nullptr, kin, nullptr, n, shift, bits, d_hist, nblk);
-      scan(d_hist, (1u << bits) * nblk, d_hist, nullptr, s);
-      k_radix_scatter<false><<<nblk, RS_T, 0, s>>>(kin, vin, n, shift, bits, d_hist, kout, vout, nblk);
+      k_radix_hist<false><<<nblk, RS_T, 0, ss>>>(nullptr, kin, nullptr, n, shift, bits, S.hist, nblk);
+      scan(S.hist, (1u << bits) * nblk, S.hist, nullptr, ss, S.bsum);
+      k_radix_scatter<false><<<nblk, RS_T, 0, ss>>>(kin, vin, n, shift, bits, S.hist, kout, vout, nblk);
     }
     kin = kout;
     vin = vout;
-    kout = (kin == d_k0) ? d_k1 : d_k0;
-    vout = (vin == d_v0) ? d_v1 : d_v0;
+    kout = (kin == S.k0) ? S.k1 : S.k0;
+    vout = (vin == S.v0) ? S.v1 : S.v0;
   }
   const uint32_t* skeys = kin;
   const uint32_t* sidx = vin;
-
-  // ---- segments (one per symbol present), longest first
-  k_seg_flags<<<gN, T256, 0, s>>>(skeys, n, d_tmp);
-  scan(d_tmp, n, d_tmp, &d_st->nseg, s);
-  k_seg_write<<<gN, T256, 0, s>>>(skeys, n, d_tmp, d_seg_start, d_st);
-  HIPCHK(hipMemsetAsync(d_bcnt, 0, 64 * sizeof(uint32_t), s));
-  k_seg_count<<<gN, T256, 0, s>>>(d_seg_start, d_st, d_bcnt, &d_st->ctr[C_MAXSEG]);
-  k_seg_bscan<<<1, 64, 0, s>>>(d_bcnt, d_bcnt + 32, d_st, FLOW_MIN_LOG2, MAX_FLOW);
-  k_seg_scatter<<<gN, T256, 0, s>>>(d_seg_start, d_st, d_bcnt + 32, d_seg_order);
-  HIPCHK(mark(GOME_PH_SORT, 1, s));
+  // segments (one per symbol present), longest first
+  k_seg_flags<<<gN, T256, 0, ss>>>(skeys, n, S.tmp);
+  scan(S.tmp, n, S.tmp, &S.sst->nseg, ss, S.bsum);
+  k_seg_write<<<gN, T256, 0, ss>>>(skeys, n, S.tmp, S.seg_start, S.sst);
+  HIPCHK(hipMemsetAsync(S.bcnt, 0, 64 * sizeof(uint32_t), ss));
+  k_seg_count<<<gN, T256, 0, ss>>>(S.seg_start, S.sst, S.bcnt, &S.sst->ctr[C_MAXSEG]);
+  k_seg_bscan<<<1, 64, 0, ss>>>(S.bcnt, S.bcnt + 32, S.sst, FLOW_MIN_LOG2, MAX_FLOW);
+  k_seg_scatter<<<gN, T256, 0, ss>>>(S.seg_start, S.sst, S.bcnt + 32, S.seg_order);
+  HIPCHK(mark(GOME_PH_SORT, 1, ss));
+  if (ss != s) {
+    HIPCHK(hipEventRecord(S.sorted, ss));
+    HIPCHK(status_reset());
+    HIPCHK(hipStreamWaitEvent(s, S.sorted, 0));
+  }
+  k_sort_status<<<1, 1, 0, s>>>(d_st, S.sst);
 
   // admission markers depend on the input records only: they run on the flow stream beside
   // the validation, the radix sort and the segmentation (the batch's critical path), enqueued
@@ -685,8 +722,8 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   B.prep = d_prep;
   B.ord = d_ord;
   B.n = n;
-  B.seg_start = d_seg_start;
-  B.seg_order = d_seg_order;
+  B.seg_start = S.seg_start;
+  B.seg_order = S.seg_order;
   B.arena = d_arena;
   B.arena_cap = arena_cap;
   B.ev_count = d_ev_count;
@@ -958,7 +995,7 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   k_match_hot<<<nleg, 64, HOT_LDS_BYTES, hot_stream>>>(D, B, d_pend, d_resume, F.hdr);
   HIPCHK(hipEventRecord(S.evh1, hot_stream));
   k_match_resume<<<nleg, 64, 0, hot_stream>>>(D, B, d_resume);
-  k_pend_apply<<<dim3(8, 64), 256, 0, hot_stream>>>(D, d_pend, d_seg_start, d_seg_order, B);
+  k_pend_apply<<<dim3(8, 64), 256, 0, hot_stream>>>(D, d_pend, S.seg_start, S.seg_order, B);
   // oid watermarks for the next batches' duplicate-oid probe (the hot stream has slack here)
   k_oid_max<<<gN, T256, 0, hot_stream>>>(n, skeys, d_prep, d_oid_max);
   if (nh_tail && split_tail && !tail_serial) {  // the tail's events beside its writes (arena; k_ev_scatter places them)
@@ -1317,7 +1354,7 @@ gome_status gome_submit_batch_async(gome_engine* e, const gome_order* orders, si
     if (he == hipSuccess) he = hipEventRecord(S.h2d, e->copy_stream);
     if (he == hipSuccess) he = hipStreamWaitEvent(e->stream, S.h2d, 0);
     if (he != hipSuccess) return e->fail(GOME_E_DEVICE, hipGetErrorString(he));
-    if ((st = e->enqueue(S.d_orders, static_cast<uint32_t>(n), e->stream, sl, seq_base, inflight_n)) != GOME_OK)
+    if ((st = e->enqueue(S.d_orders, static_cast<uint32_t>(n), e->stream, sl, seq_base, inflight_n, true)) != GOME_OK)
       return st;
   }
   e->flights.push_back(Flight{sl, static_cast<uint32_t>(n), seq_base, false});
@@ -1338,7 +1375,7 @@ gome_status gome_submit_batch_device_async(gome_engine* e, const gome_order* dev
   const uint32_t sl = e->take_slot();
   if (n) {
     e->used = true;
-    if ((st = e->enqueue(dev_orders, static_cast<uint32_t>(n), e->stream, sl, seq_base, inflight_n)) != GOME_OK)
+    if ((st = e->enqueue(dev_orders, static_cast<uint32_t>(n), e->stream, sl, seq_base, inflight_n, true)) != GOME_OK)
       return st;
   }
   e->flights.push_back(Flight{sl, static_cast<uint32_t>(n), seq_base, true});

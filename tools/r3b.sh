@@ -29,6 +29,23 @@ for P in $PARTS; do
   c2ts)  # config-2 trace with the tail's events after its writes (solo kernel times)
     GOME_TAIL_SERIAL=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats -T --output-format csv -d $OUT/c2strace -o run \
       -- python3 bench.py --workload config2 --steps 5 --warmup 5 --e2e-steps 0 --no-cpu-baseline --no-phase-pass > $OUT/c2s_trace.log 2>&1 || exit 4 ;;
+  pipe)  # synchronous vs pipelined steps (bench.py --sync), configs from ABW, alternating
+    for R in 1 2; do
+      for M in sync pipe; do
+        for W in ${ABW:-config2 config3}; do
+          F=""; [ $M = sync ] && F="--sync"
+          timeout -k 10 300 python3 -u bench.py --workload $W --steps 10 --warmup 5 --e2e-steps 0 --no-cpu-baseline \
+            --no-phase-pass $F > $OUT/${M}_${W}_$R.jsonl 2> $OUT/${M}_${W}_$R.log || { tail -20 $OUT/${M}_${W}_$R.log; exit 12; }
+          python3 -c "import json; d=json.loads(open('$OUT/${M}_${W}_$R.jsonl').readlines()[-1]); print('$M $W $R', d['value'], d['ms_per_step'], d['p50_batch_ms'])"
+        done
+      done
+    done ;;
+  sweep)  # config 3 batch sweep: value vs the critical-path bound (bench.py critical_path)
+    for B in 1048576 2097152 4194304; do
+      timeout -k 10 300 python3 -u bench.py --workload config3 --batch $B --steps 10 --warmup 4 --e2e-steps 0 \
+        --no-cpu-baseline > $OUT/sweep_$B.jsonl 2> $OUT/sweep_$B.log || { tail -20 $OUT/sweep_$B.log; exit 13; }
+      python3 -c "import json; d=json.loads(open('$OUT/sweep_$B.jsonl').readlines()[-1]); print('$B', d['value'], d['ms_per_step'], d['critical_path'])"
+    done ;;
   c3t)
     timeout -k 10 300 rocprofv3 --kernel-trace --stats -T --output-format csv -d $OUT/c3trace -o run \
       -- python3 bench.py --workload config3 --steps 5 --warmup 5 --e2e-steps 0 --no-cpu-baseline > $OUT/c3_trace.log 2>&1 || exit 5 ;;

@@ -272,7 +272,7 @@ struct gome_engine {
   unsigned long long idx_cap = 0;
   // batch buffers (the sort's and the segments' are per slot: Slot)
   uint32_t* d_bsum = nullptr;
-  bool sort_ahead = true;  // pipelined batches sort on the copy stream during the last one's plan (GOME_SORT_AHEAD=0: A/B)
+  bool sort_ahead = false;  // pipelined device batches sort on the copy stream during the last one's plan (GOME_SORT_AHEAD=1; DESIGN 4.5: off, measured mixed)
   unsigned long long* d_adm = nullptr;  // admission table (k_adm)
   unsigned long long* d_dup = nullptr;  // (S, uuid, oid) table of the records whose (S, oid) repeats
   uint8_t* d_multi = nullptr;           // per (S, oid) slot: the key repeats in the batch
@@ -1354,7 +1354,8 @@ gome_status gome_submit_batch_async(gome_engine* e, const gome_order* orders, si
     if (he == hipSuccess) he = hipEventRecord(S.h2d, e->copy_stream);
     if (he == hipSuccess) he = hipStreamWaitEvent(e->stream, S.h2d, 0);
     if (he != hipSuccess) return e->fail(GOME_E_DEVICE, hipGetErrorString(he));
-    if ((st = e->enqueue(S.d_orders, static_cast<uint32_t>(n), e->stream, sl, seq_base, inflight_n, true)) != GOME_OK)
+    // (no sort ahead here: on the copy stream it delayed the event copies; e2e +2 ms per config-3 batch)
+    if ((st = e->enqueue(S.d_orders, static_cast<uint32_t>(n), e->stream, sl, seq_base, inflight_n)) != GOME_OK)
       return st;
   }
   e->flights.push_back(Flight{sl, static_cast<uint32_t>(n), seq_base, false});

@@ -115,7 +115,8 @@ def phase_candidates(st: dict) -> dict:
         "k_radix_scatter": (ms["sort"], 68 * n, "radix sort by symbol + segments"),
         "k_adm": (ms["admission"], 48 * n, "admission (Q4) and duplicate oids (Q7)"),
         "k_prep": (ms["records"], 68 * n, "symbol-sorted records"),
-        "k_ev_scatter": (ms["publish"], 128 * st["n_events"] + 8 * n, "publish-order scan and event scatter"),
+        "k_publish": (ms["publish"], 128 * st["n_events"] + 8 * n,
+                      "publish-order scan, arena event scatter and the hottest book's events"),
     }
 
 

@@ -15,7 +15,7 @@
 //                     FIFO volumes to find how far a taker sweeps
 //   k_flow_*          hot books on the flow path (match_flow.h): a serial plan over level
 //                     aggregates, then parallel fills / FIFO rebuild (the batch's critical path)
-//   k_scan_* + k_ev_scatter   event compaction into publish order (taker_seq, fill_idx)
+//   k_scan_* + k_publish      event compaction into publish order (taker_seq, fill_idx)
 //   k_recycle         freed FIFO chunks back to the free pool
 //
 // Everything is integer / byte work (no MFMA).  See DESIGN.md for layout and rooflines.
@@ -50,13 +50,14 @@ using namespace gome;
 // Four lanes per 64-B event, 16 B each: a wave reads 1 KiB of the arena per load instruction and
 // writes each event as one whole line (a lane per event read and wrote 64 separate 16-B pieces per
 // instruction).  Quarter 2 holds taker_seq and fill_idx, quarter 3 seq_hi.
-__global__ void k_ev_scatter(const gome_event* arena, uint32_t cap, const Status* st,
-                             const uint32_t* ev_off, gome_event* out, unsigned long long seq_base) {
+__device__ __forceinline__ void ev_scatter(const gome_event* arena, uint32_t cap, const Status* st,
+                                           const uint32_t* ev_off, gome_event* out, unsigned long long seq_base,
+                                           uint32_t bid, uint32_t nblk) {
   const uint32_t used = min(st->ev_bump, cap);
   const uint32_t qt = threadIdx.x & 3u;
   const uint4* src = reinterpret_cast<const uint4*>(arena);
   uint4* dst = reinterpret_cast<uint4*>(out);
-  for (uint32_t j = (blockIdx.x * blockDim.x + threadIdx.x) >> 2; j < used; j += (gridDim.x * blockDim.x) >> 2) {
+  for (uint32_t j = (bid * blockDim.x + threadIdx.x) >> 2; j < used; j += (nblk * blockDim.x) >> 2) {
     uint4 v = src[4ull * j + qt];
     const uint32_t idx = __shfl(v.x, static_cast<int>((threadIdx.x & ~3u) | 2u) & 63);   // taker_seq
     const uint32_t fi = __shfl(v.y, static_cast<int>((threadIdx.x & ~3u) | 2u) & 63);    // fill_idx
@@ -68,7 +69,17 @@ __global__ void k_ev_scatter(const gome_event* arena, uint32_t cap, const Status
   }
 }
 static_assert(offsetof(gome_event, taker_seq) == 32 && offsetof(gome_event, fill_idx) == 36 &&
-              offsetof(gome_event, seq_hi) == 60 && sizeof(gome_event) == 64, "k_ev_scatter's quarters");
+              offsetof(gome_event, seq_hi) == 60 && sizeof(gome_event) == 64, "ev_scatter's quarters");
+
+// After the publish-order scan, in one launch (no hop to a second stream and back): blocks
+// [0, nscat) place the arena's events, the rest write the hottest book's events (fl_events_hot).
+constexpr uint32_t PUB_SCAT = 2048, PUB_HOT = 1024;
+__global__ __launch_bounds__(256) void k_publish(Dev D, BatchArgs B, FlowArgs F, const gome_event* arena,
+                                                 uint32_t cap, const uint32_t* ev_off, gome_event* out,
+                                                 unsigned long long seq_base) {
+  if (blockIdx.x < PUB_SCAT) ev_scatter(arena, cap, D.st, ev_off, out, seq_base, blockIdx.x, PUB_SCAT);
+  else fl_events_hot(D, B, F, ev_off, out, blockIdx.x - PUB_SCAT, gridDim.x - PUB_SCAT);
+}
 
 // Freed FIFO chunks of this batch -> free pool (two kernels: copy, then counters).
 __global__ void k_recycle_copy(Dev D) {
@@ -242,7 +253,7 @@ struct gome_engine {
   hipStream_t hot_stream = nullptr;   // tail / near-head flow books, legacy hot kernel
   hipStream_t flow_stream = nullptr;  // the hottest book's plan (critical path)
   hipStream_t copy_stream = nullptr;  // H2D of records, D2H of events (pipelined path)
-  hipEvent_t fork{}, join{}, joinf{}, prep_h{}, prep_t{}, fork_adm{}, adm_done{}, seg_done{}, ev_scan{}, ev_hot{};
+  hipEvent_t fork{}, join{}, joinf{}, prep_h{}, prep_t{}, fork_adm{}, adm_done{}, seg_done{};
   hipEvent_t dp_fork{}, cnt_fork{}, cnt_done{}, dw_done{}, dl_done{}, tl_done{};  // the hottest book's deep chain, k_flow_count beside its writes
   Slot slots[GOME_MAX_INFLIGHT];
   uint32_t next_slot = 0;
@@ -344,7 +355,7 @@ struct gome_engine {
         for (hipEvent_t ev : pr)
           if (ev) (void)hipEventDestroy(ev);
     }
-    for (hipEvent_t ev : {fork, join, joinf, prep_h, prep_t, fork_adm, adm_done, seg_done, ev_scan, ev_hot, dp_fork, cnt_fork, cnt_done,
+    for (hipEvent_t ev : {fork, join, joinf, prep_h, prep_t, fork_adm, adm_done, seg_done, dp_fork, cnt_fork, cnt_done,
                           dw_done, dl_done, tl_done})
       if (ev) (void)hipEventDestroy(ev);
     if (hot_stream) (void)hipStreamDestroy(hot_stream);
@@ -407,7 +418,7 @@ gome_status gome_engine::init(const gome_config& c) {
   HIPCHK(hipStreamCreateWithFlags(&hot_stream, hipStreamNonBlocking));
   HIPCHK(hipStreamCreateWithFlags(&flow_stream, hipStreamNonBlocking));
   HIPCHK(hipStreamCreateWithFlags(&copy_stream, hipStreamNonBlocking));
-  for (hipEvent_t* ev : {&fork, &join, &joinf, &prep_h, &prep_t, &fork_adm, &adm_done, &seg_done, &ev_scan, &ev_hot,
+  for (hipEvent_t* ev : {&fork, &join, &joinf, &prep_h, &prep_t, &fork_adm, &adm_done, &seg_done,
                          &dp_fork, &cnt_fork, &cnt_done, &dw_done, &dl_done, &tl_done})
     HIPCHK(hipEventCreateWithFlags(ev, hipEventDisableTiming));
   for (Slot& S : slots) {
@@ -958,7 +969,7 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
     HIPCHK(mark(GOME_PH_TAIL_COUNT, 0, s));
     toff(FT, false, s);
     HIPCHK(mark(GOME_PH_TAIL_COUNT, 1, s));
-    // the flow books' writes beside their events (into the arena: k_ev_scatter places them
+    // the flow books' writes beside their events (into the arena: k_publish places them
     // after the publish scan), then the deep books' writes
     HIPCHK(mark(GOME_PH_TAIL_WRITE, 0, s));
     if (split_tail) {
@@ -998,7 +1009,7 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   k_pend_apply<<<dim3(8, 64), 256, 0, hot_stream>>>(D, d_pend, S.seg_start, S.seg_order, B);
   // oid watermarks for the next batches' duplicate-oid probe (the hot stream has slack here)
   k_oid_max<<<gN, T256, 0, hot_stream>>>(n, skeys, d_prep, d_oid_max);
-  if (nh_tail && split_tail && !tail_serial) {  // the tail's events beside its writes (arena; k_ev_scatter places them)
+  if (nh_tail && split_tail && !tail_serial) {  // the tail's events beside its writes (arena; k_publish places them)
     HIPCHK(hipStreamWaitEvent(hot_stream, tl_done, 0));
     k_flow_events_fused_w<<<ceil_div(tail_grid * FL_EV_T, FL_WRITE_T), FL_WRITE_T, 0, hot_stream>>>(D, B, FT);
   }
@@ -1019,12 +1030,7 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   HIPCHK(mark(GOME_PH_PUBLISH, 0, s));
   scan(d_ev_count, n, d_ev_off, &d_st->n_events, s);
   // the hottest book's events and the arena scatter fill disjoint slots: run them side by side
-  HIPCHK(hipEventRecord(ev_scan, s));
-  HIPCHK(hipStreamWaitEvent(flow_stream, ev_scan, 0));
-  k_flow_events<<<1024, 256, 0, flow_stream>>>(D, B, FH0, d_ev_off, S.d_events);
-  HIPCHK(hipEventRecord(ev_hot, flow_stream));
-  k_ev_scatter<<<2048, T256, 0, s>>>(d_arena, arena_cap, d_st, d_ev_off, S.d_events, seq_base);
-  HIPCHK(hipStreamWaitEvent(s, ev_hot, 0));
+  k_publish<<<PUB_SCAT + PUB_HOT, T256, 0, s>>>(D, B, FH0, d_arena, arena_cap, d_ev_off, S.d_events, seq_base);
   HIPCHK(mark(GOME_PH_PUBLISH, 1, s));
   HIPCHK(hipStreamWaitEvent(s, dw_done, 0));
   k_recycle_copy<<<256, 256, 0, s>>>(D);

@@ -2000,7 +2000,7 @@ __device__ __forceinline__ void fl_emit_wave(const BatchArgs& B, const FlowArgs&
     const int64_t hi_ = (me + mv < ca) ? me + mv : ca;
     const int64_t qty = hi_ - lo_, pre = me + mv - lo_;
     const bool full = me + mv <= ca;
-    const unsigned long long sq = ARENA ? idx : B.seq_base + idx;  // arena: the batch index (k_ev_scatter)
+    const unsigned long long sq = ARENA ? idx : B.seq_base + idx;  // arena: the batch index (k_publish)
     gome_event ev;
     ev.price_fx = price;
     ev.match_volume_fx = qty;
@@ -2025,12 +2025,13 @@ __device__ __forceinline__ void fl_emit_wave(const BatchArgs& B, const FlowArgs&
 // (fill_idx bases from the count pass, F.fbase).
 constexpr uint32_t FL_EV_T = 256;  // threads of the event kernels' blocks
 constexpr uint32_t FL_WRITE_T = 1024;  // ... of the tail's (and of k_flow_write's)
-__global__ __launch_bounds__(256) void k_flow_events(Dev D, BatchArgs B, FlowArgs F, const uint32_t* ev_off,
-                                                     gome_event* out) {
+// (blocks bid of nblk; k_publish runs it beside the arena scatter in one launch)
+__device__ __forceinline__ void fl_events_hot(const Dev& D, const BatchArgs& B, const FlowArgs& F,
+                                              const uint32_t* ev_off, gome_event* out, uint32_t bid, uint32_t nblk) {
   const uint32_t hend = fl_hend(D, F), nb = hend > F.h0 ? hend - F.h0 : 0u;
   const uint32_t total = nb ? F.toff[F.tb + nb] : 0u;
-  const uint32_t lane = lane_id(), stride = gridDim.x * blockDim.x;
-  for (uint32_t b0 = blockIdx.x * blockDim.x + (threadIdx.x & ~63u); b0 < total; b0 += stride) {
+  const uint32_t lane = lane_id(), stride = nblk * blockDim.x;
+  for (uint32_t b0 = bid * blockDim.x + (threadIdx.x & ~63u); b0 < total; b0 += stride) {
     const uint32_t gt = b0 + lane;
     uint32_t cnt = 0, first = 0;
     FlEvLane r{};
@@ -2065,6 +2066,10 @@ __global__ __launch_bounds__(256) void k_flow_events(Dev D, BatchArgs B, FlowArg
     r.mb = first - (inc - cnt);
     fl_emit_wave<false>(B, F, out, r);
   }
+}
+__global__ __launch_bounds__(256) void k_flow_events(Dev D, BatchArgs B, FlowArgs F, const uint32_t* ev_off,
+                                                     gome_event* out) {
+  fl_events_hot(D, B, F, ev_off, out, blockIdx.x, gridDim.x);
 }
 
 // Segmented inclusive wave scan: lane i sums lanes s..i, s = the last lane <= i with `head` set

@@ -266,7 +266,7 @@ __device__ __forceinline__ uint32_t lds_get(const uint32_t& c) { return uni(c); 
 __device__ __forceinline__ void lds_set(uint32_t& c, uint32_t v) { l0_lds4(&c, v); }
 
 // ---- events --------------------------------------------------------------------------
-// Events go to per-wave blocks of EVB_HOT in the batch's arena (k_ev_scatter compacts
+// Events go to per-wave blocks of EVB_HOT in the batch's arena (k_publish compacts
 // them into publish order); unused tails are marked taker_seq = NIL.
 __device__ __forceinline__ void hot_ev_close(HotCtx& H) {
   if (H.ev_base == NIL || H.fatal) return;

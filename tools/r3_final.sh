@@ -21,6 +21,9 @@ for P in $PARTS; do
         || { tail -20 $OUT/${W}_bench.log; exit 3; }
       python3 -c "import json; d=json.loads(open('$OUT/${W}_bench.jsonl').readlines()[-1]); print('$W', d['value'], d['ms_per_step'], d['e2e']['value'], d['hot_book']['ns_per_order'], d['roofline']['kernel'][:40], d['roofline']['frac'])"
     done ;;
+  smoke)
+    timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.txt 2>&1 || { tail -20 $OUT/smoke.txt; exit 8; }
+    tail -1 $OUT/smoke.txt ;;
   prof3)
     bash profiles/run_rocprof.sh ${TAG}_config3 --steps 3 --warmup 1 --no-cpu-baseline --e2e-steps 0 || exit 4
     python3 profiles/summarize.py ${TAG}_config3 gpurun_out/prof_${TAG}_config3 || exit 5 ;;

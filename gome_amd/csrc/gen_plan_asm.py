@@ -1226,9 +1226,10 @@ class GenDV(GenD):
         e(f"s_{'max' if buy else 'min'}_u32 {top}, {top}, {LI}")
         self.add(topd, topd, X)
         self.word_add(L, A[0])
-        # word L is nonzero now iff A > 0 (A == 0: L is the cached top, whose word stays 0)
-        e(f"s_min_u32 s79, {A[0]}, 1")
-        e(f"s_lshl_b32 s79, s79, {T0}")                     # T0 = L >> 6: bit (L >> 6) & 31
+        # word L's register's summary bit, set even when A == 0 (L is the cached top, whose word
+        # stays 0): a bit over an all-zero register is stale, which next_top tolerates (it
+        # searches on, or clears the bit), and a rest at the top is rare enough to pay for it
+        e(f"s_lshl_b32 s79, 1, {T0}")                       # T0 = L >> 6: bit (L >> 6) & 31
         e(f"s_lshr_b32 s81, {T0}, 5")
         e("s_lshl_b64 exec, 1, s81")
         e(f"v_or_b32 v{VSM}, s79, v{VSM}")

@@ -64,7 +64,8 @@ class Stats(C.Structure):
         ("idx_tombstones", C.c_uint64), ("n_flow_cancels", C.c_uint64), ("ms_cold", C.c_double),
         ("lvl_used", C.c_uint64), ("n_dup_oid", C.c_uint64), ("n_flow_tail_fills", C.c_uint64),
         ("ms_phase", C.c_double * 16),
-        ("ms_host_enqueue", C.c_double), ("chains", C.c_uint32), ("chains_wanted", C.c_uint32)]
+        ("ms_host_enqueue", C.c_double), ("chains", C.c_uint32), ("chains_wanted", C.c_uint32),
+        ("n_quirk_checked", C.c_uint64), ("n_requalified", C.c_uint64)]
 
     def as_dict(self):
         d = {n: getattr(self, n) for n, _ in self._fields_}
@@ -240,6 +241,7 @@ class Engine:
             raise GomeError(s, self.lib.gome_last_error(None).decode())
         self.h = h
         self.max_batch = max_batch
+        self.max_symbols = max_symbols
         self.cfg_kwargs = dict(max_symbols=max_symbols, max_batch=max_batch, max_nodes=max_nodes,
                                max_levels=max_levels, accuracy=accuracy, device=device,
                                max_events=max_events, flags=flags)

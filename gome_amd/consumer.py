@@ -28,8 +28,10 @@ DoOrder ignores); otherwise each field whose JSON value fits its Go type is set 
 field (wrong type, overflow, null) stays zero, so `"Price":"abc"` is an order at price 0.
 `process()` never raises on message content.  A message outside the parity domain is counted
 in `rejected` and not submitted: a Price / Volume that is not an exact scaled integer below
-2^53 (quirk Q5), or a 255th distinct Transaction value outside {0, 1} (the engine carries
-Transaction as a one-byte code, gome_abi.h).  The engine applies the duplicate-oid rule (Q7,
+2^53 (quirk Q5), a negative Volume, a Symbol beyond the engine's max_symbols distinct symbols,
+or a 255th distinct Transaction value outside {0, 1} (the engine carries Transaction as a
+one-byte code, gome_abi.h).  Raw bytes decode as Go does: invalid UTF-8 becomes U+FFFD, one
+per byte.  The engine applies the duplicate-oid rule (Q7,
 gome_abi.h) to the admitted ADDs; `dups` counts them.
 
 Admission markers are resolved against a staged view of the pre-pool and the consumption is
@@ -38,6 +40,7 @@ GOME_E_CAPACITY before anything is applied) can be resubmitted with the same ver
 """
 from __future__ import annotations
 
+import codecs
 import ctypes as C
 import json
 import math
@@ -193,6 +196,19 @@ def _reject_constant(tok):
     raise ValueError(tok)  # NaN / Infinity are not JSON to Go
 
 
+def _go_bytes_to_str(body) -> str:
+    """Go's encoding/json replaces every byte of invalid UTF-8 with U+FFFD, one per byte
+    (utf8.DecodeRune returns (RuneError, 1)); Python's 'replace' would merge a truncated sequence."""
+    return body.decode("utf-8", errors="gome_go_bytes")
+
+
+def _go_replace(exc):
+    return "\ufffd", exc.start + 1
+
+
+codecs.register_error("gome_go_bytes", _go_replace)
+
+
 def decode_order_node(body) -> dict:
     """The OrderNode fields json.Unmarshal leaves: {"Action", "Uuid", "Oid", "Symbol",
     "Transaction", "Price", "Volume"}.  Never raises.  Keys match exactly or case-insensitively
@@ -200,6 +216,8 @@ def decode_order_node(body) -> dict:
     within its width (Action int8, Transaction int32), a float field any finite number, a
     string field only a string; anything else (and null) leaves the zero value."""
     out = {"Action": 0, "Uuid": "", "Oid": "", "Symbol": "", "Transaction": 0, "Price": 0.0, "Volume": 0.0}
+    if isinstance(body, (bytes, bytearray, memoryview)):
+        body = _go_bytes_to_str(bytes(body))
     try:
         doc = json.loads(body, parse_int=_Lit, parse_float=_Lit, parse_constant=_reject_constant,
                          object_pairs_hook=_Pairs)
@@ -303,6 +321,7 @@ class BatchingConsumer:
         self.max_wait = max_wait_us * 1e-6
         self.acc = accuracy
         self.lib = load_library()
+        self.max_symbols = getattr(engine, "max_symbols", None)
         self.seq = 0
         self.consumed = self.rejected = self.batches = self.dups = 0
         self._staged = None
@@ -345,9 +364,15 @@ class BatchingConsumer:
                 continue  # DoOrder ignores any other Action (engine.go:46-54): a zero record
             try:
                 p, v = fixed_from_scaled(o["Price"]), fixed_from_scaled(o["Volume"])
+                if v < 0:  # (the engine's record domain: volume >= 0, gome_abi.h)
+                    raise GomeError(1, "negative Volume")
+                if self.max_symbols is not None and N.fwd["sym"].get(sym, len(N.rev["sym"])) >= self.max_symbols:
+                    raise GomeError(1, "more distinct Symbols than the engine's max_symbols")
                 code = N.tx_code(o["Transaction"])
             except GomeError:
-                keep[i] = False  # outside the parity domain (Q5, or the Transaction code space)
+                # outside the parity domain (Q5, a negative Volume), or beyond the engine's symbol
+                # range or Transaction code space: not submitted, so it cannot refuse the batch
+                keep[i] = False
                 self.rejected += 1
                 if act == ADD:
                     pre.consume_add(sym, uuid, oid)

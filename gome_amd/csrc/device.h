@@ -53,8 +53,10 @@ struct ChunkHdr {
 struct Book {
   uint32_t lvl_base, n_lvl, lvl_cap, pad;  // pad: BOOK_* flags
 };
-// The book has seen state the aggregate (flow) plan cannot express: a cancel whose request
-// side differs from the node's side (Q2) or a zero-volume maker (Q6).  Sticky.
+// The book holds (or may hold) state the aggregate (flow) plan cannot express: set by a cancel
+// whose request side differs from the node's side (Q2), a zero-volume maker (Q6), or a load of
+// such a state.  Cleared after a batch by k_requalify (match_requal.h) once the book's state
+// is again one the flow plans assume (the reference's state heals: nodepool.go:76-83).
 constexpr uint32_t BOOK_QUIRK = 1u;
 
 struct IdxEnt {
@@ -85,7 +87,8 @@ enum {
   C_FLOW_TAIL_FILLS,                                      // fills of the tail's flow books
   C_WANT_DEEP, C_WANT_CANC,                               // flow candidates that asked for the deep /
                                                           // cancel chain (enqueued or not)
-  C_NCTR = 25
+  C_QUIRK_CHECKED, C_REQUAL,                              // quirk books checked / requalified (k_requalify)
+  C_NCTR = 27
 };
 
 // Level blocks (a book's sorted level array) come in power-of-two capacities 16 << c.  A
@@ -102,6 +105,8 @@ struct Status {
   uint32_t n_events;
   uint32_t nhot;       // segments handled by k_match_hot (first nhot of seg_order)
   uint32_t lvl_used;   // level slots ever carved from the pool (lvl_bump at batch end)
+  uint32_t nquirk;     // books the cold / resume waves finished with BOOK_QUIRK (Dev::quirk)
+  uint32_t pad_q;
   // ---- everything below persists across batches (the per-batch reset stops here)
   int32_t free_top;
   uint32_t freed_top;
@@ -128,6 +133,8 @@ struct Dev {
   uint32_t* lvl_freed;       // per class c: blocks released this batch
   const uint32_t* lvl_cls_off;  // [LVL_NCLS + 1] offsets; class c holds lvl_cls_off[c+1]-off[c]
   unsigned long long* ctr_s;    // [CTR_STRIPES][CTR_STRIDE] striped batch counters (ctr_add)
+  uint32_t* quirk;              // [quirk_cap] symbols of this batch's quirk books (k_requalify's input)
+  uint32_t quirk_cap;
 };
 
 // The batch counters are added by thousands of waves.  Device-scope atomics on one address (or
@@ -140,6 +147,13 @@ static_assert(C_NCTR <= CTR_STRIDE, "one stripe holds every counter");
 __device__ __forceinline__ void ctr_add(const Dev& D, uint32_t c, unsigned long long v) {
   const uint32_t s = (blockIdx.x + 13u * blockIdx.y) & (CTR_STRIPES - 1);
   atomicAdd(&D.ctr_s[s * CTR_STRIDE + c], v);
+}
+
+// A book a wave finished with BOOK_QUIRK set: k_requalify checks it after the batch (one
+// thread; a list that overflows leaves the book flagged until a later batch lists it).
+__device__ __forceinline__ void quirk_note(const Dev& D, uint32_t sym) {
+  const uint32_t i = atomicAdd(&D.st->nquirk, 1u);
+  if (i < D.quirk_cap) D.quirk[i] = sym;
 }
 
 __device__ __forceinline__ uint32_t lvl_cls(uint32_t cap) { return (31u - __clz(cap)) - 4u; }

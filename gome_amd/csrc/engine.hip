@@ -39,6 +39,7 @@
 #include "match_flow_cancel.h"
 #include "match_flow_deep.h"
 #include "match_hot.h"
+#include "match_requal.h"
 #include "pipeline.h"
 #include "wave.h"
 
@@ -203,6 +204,8 @@ __global__ void k_tob(Dev D, const uint32_t* syms, uint32_t n, gome_tob* out) {
 namespace {
 
 thread_local std::string g_create_err;
+
+constexpr uint32_t QUIRK_CAP = 1u << 16;  // quirk books checked per batch (Dev::quirk)
 
 uint32_t ceil_div(uint64_t a, uint64_t b) { return static_cast<uint32_t>((a + b - 1) / b); }
 uint64_t next_pow2(uint64_t x) {
@@ -485,8 +488,10 @@ gome_status gome_engine::init(const gome_config& c) {
       !alloc(&d_st, 1, "status") || !alloc(&D.lvl_free, cls_off[LVL_NCLS], "level-block free lists") ||
       !alloc(&D.lvl_freed, cls_off[LVL_NCLS], "level-block release lists") ||
       !alloc(&d_cls_off, LVL_NCLS + 1, "level-block classes") ||
-      !alloc(&D.ctr_s, CTR_STRIPES * CTR_STRIDE, "counter stripes"))
+      !alloc(&D.ctr_s, CTR_STRIPES * CTR_STRIDE, "counter stripes") ||
+      !alloc(&D.quirk, QUIRK_CAP, "quirk book list"))
     return GOME_E_CAPACITY;
+  D.quirk_cap = QUIRK_CAP;
   D.lvl_cls_off = d_cls_off;
   D.max_symbols = ms;
   D.lvl_cap_total = static_cast<uint32_t>(cfg.max_levels);
@@ -720,10 +725,10 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   HIPCHK(mark(GOME_PH_ADMISSION, 0, flow_stream));
   k_adm<<<gN, T256, 0, flow_stream>>>(d_ord, n, d_adm, d_adm_slot, adm_mask, cfg.max_symbols, d_st, D.books, D.idx,
                                       D.idx_mask, d_oid_max, d_multi, d_adm_ctl + 1);
-  k_adm_flag<<<gN, T256, 0, flow_stream>>>(d_ord, n, d_adm_slot, d_multi, d_dup, d_adm_slot2, d_adm_aux, adm_mask, d_st,
-                                           S.d_dup, d_adm, d_adm_ctl + 1);
+  k_adm_flag<<<gN, T256, 0, flow_stream>>>(d_ord, n, d_adm_slot, d_multi, d_dup, d_adm_slot2, d_adm_aux, adm_mask,
+                                           d_adm, d_adm_ctl + 1);
   k_adm_res<<<gN, T256, 0, flow_stream>>>(d_ord, n, d_adm_slot, d_dup, d_adm_slot2, d_first, d_adm_ctl + 1);
-  k_adm_dup<<<gN, T256, 0, flow_stream>>>(n, d_adm_slot, d_first, d_st, S.d_dup, d_adm_ctl + 1);
+  k_adm_dup<<<gN, T256, 0, flow_stream>>>(n, d_adm_slot, d_first, d_adm_ctl + 1);
   k_adm_clean<<<gN, T256, 0, flow_stream>>>(n, d_adm_aux, d_adm_slot2, d_dup, d_first, d_multi, d_adm_ctl + 1);
   HIPCHK(mark(GOME_PH_ADMISSION, 1, flow_stream));
   HIPCHK(hipEventRecord(adm_done, flow_stream));
@@ -741,6 +746,7 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   B.sidx = sidx;
   B.adm_flag = d_adm_slot;
   B.seq_base = seq_base;
+  B.dup_list = S.d_dup;
   const uint32_t grid = std::min<uint32_t>(n, cfg.max_symbols);
   const uint32_t nhot_max = std::min<uint32_t>(MAX_FLOW, grid);
   // flow path: the head (longest FL_HEAD candidates, the batch's critical path) and the tail
@@ -1033,6 +1039,8 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   k_publish<<<PUB_SCAT + PUB_HOT, T256, 0, s>>>(D, B, FH0, d_arena, arena_cap, d_ev_off, S.d_events, seq_base);
   HIPCHK(mark(GOME_PH_PUBLISH, 1, s));
   HIPCHK(hipStreamWaitEvent(s, dw_done, 0));
+  // quirk books whose state healed go back to the flow path from the next batch on
+  k_requalify<<<64, 256, 0, s>>>(D, B, F.hdr, d_resume);
   k_recycle_copy<<<256, 256, 0, s>>>(D);
   k_recycle_fin<<<1, 64, 0, s>>>(D);
   k_lvl_recycle<<<LVL_NCLS, 256, 0, s>>>(D);
@@ -1115,6 +1123,8 @@ gome_status gome_engine::finish(uint32_t sl, uint32_t n) {
   last_maxseg = st.ctr[C_MAXSEG];
   last_n = n;
   stats.chains_wanted = (want_deep ? FL_CH_DEEP : 0u) | (want_canc ? FL_CH_CANCEL : 0u);
+  stats.n_quirk_checked = st.ctr[C_QUIRK_CHECKED];
+  stats.n_requalified = st.ctr[C_REQUAL];
   if (const uint64_t nd = std::min<uint64_t>(st.ctr[C_DUP], n)) {
     dup_idx.resize(nd);
     HIPCHK(hipMemcpy(dup_idx.data(), S.d_dup, nd * sizeof(uint32_t), hipMemcpyDeviceToHost));
@@ -1260,6 +1270,20 @@ gome_status gome_engine::collect_all() {
 }
 
 // ============================================================== C-ABI
+// Every entry point that touches the device switches to the handle's device first and restores
+// the caller's on return: a host thread may drive handles on several GPUs (gome_amd/router.py),
+// and allocations, copies and launches go to the thread's current device.
+struct DevGuard {
+  int prev = -1, dev;
+  explicit DevGuard(int d) : dev(d) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) (void)hipSetDevice(dev);
+  }
+  ~DevGuard() {
+    if (prev >= 0 && prev != dev) (void)hipSetDevice(prev);
+  }
+};
+
 extern "C" {
 
 uint32_t gome_abi_version(void) { return GOME_ABI_VERSION; }
@@ -1282,17 +1306,24 @@ gome_status gome_create(const gome_config* cfg, gome_engine** out) {
   *out = nullptr;
   gome_engine* e = new (std::nothrow) gome_engine();
   if (!e) { g_create_err = "gome_create: out of host memory"; return GOME_E_CAPACITY; }
-  gome_status s = e->init(*cfg);
+  int prev = -1;
+  if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+  gome_status s = e->init(*cfg);  // (switches to cfg->device; the caller's device is restored below)
   if (s != GOME_OK) {
     g_create_err = e->err;
     delete e;
-    return s;
+  } else {
+    *out = e;
   }
-  *out = e;
-  return GOME_OK;
+  if (prev >= 0) (void)hipSetDevice(prev);
+  return s;
 }
 
-void gome_destroy(gome_engine* e) { delete e; }
+void gome_destroy(gome_engine* e) {
+  if (!e) return;
+  DevGuard dg(e->cfg.device);
+  delete e;
+}
 
 const char* gome_last_error(const gome_engine* e) {
   return e ? e->err.c_str() : g_create_err.c_str();
@@ -1300,6 +1331,7 @@ const char* gome_last_error(const gome_engine* e) {
 
 gome_status gome_submit_batch(gome_engine* e, const gome_order* orders, size_t n, uint64_t seq_base) {
   if (!e) return GOME_E_INVAL;
+  DevGuard dg(e->cfg.device);
   gome_status st = e->collect_all();
   if (st != GOME_OK) return st;
   if ((st = e->spill_device_events()) != GOME_OK) return st;
@@ -1320,6 +1352,7 @@ gome_status gome_submit_batch(gome_engine* e, const gome_order* orders, size_t n
 gome_status gome_submit_batch_device(gome_engine* e, const gome_order* dev_orders, size_t n,
                                      uint64_t seq_base, void* stream) {
   if (!e) return GOME_E_INVAL;
+  DevGuard dg(e->cfg.device);
   gome_status st = e->collect_all();
   if (st != GOME_OK) return st;
   if ((st = e->spill_device_events()) != GOME_OK) return st;
@@ -1342,6 +1375,7 @@ gome_status gome_submit_batch_device(gome_engine* e, const gome_order* dev_order
 
 gome_status gome_submit_batch_async(gome_engine* e, const gome_order* orders, size_t n, uint64_t seq_base) {
   if (!e) return GOME_E_INVAL;
+  DevGuard dg(e->cfg.device);
   if (e->flights.size() >= GOME_MAX_INFLIGHT)
     return e->fail(GOME_E_STATE, "GOME_MAX_INFLIGHT batches in flight: gome_collect first");
   gome_status st = e->spill_device_events();
@@ -1371,6 +1405,7 @@ gome_status gome_submit_batch_async(gome_engine* e, const gome_order* orders, si
 gome_status gome_submit_batch_device_async(gome_engine* e, const gome_order* dev_orders, size_t n,
                                            uint64_t seq_base) {
   if (!e) return GOME_E_INVAL;
+  DevGuard dg(e->cfg.device);
   if (e->flights.size() >= GOME_MAX_INFLIGHT)
     return e->fail(GOME_E_STATE, "GOME_MAX_INFLIGHT batches in flight: gome_collect first");
   gome_status st = e->spill_device_events();
@@ -1392,6 +1427,7 @@ gome_status gome_submit_batch_device_async(gome_engine* e, const gome_order* dev
 gome_status gome_collect_device(gome_engine* e, const gome_event** dev_events, size_t* n_events,
                                 gome_stats* stats) {
   if (!e || !dev_events || !n_events) return GOME_E_INVAL;
+  DevGuard dg(e->cfg.device);
   *dev_events = nullptr;
   *n_events = 0;
   if (e->flights.empty()) return e->fail(GOME_E_NOTFOUND, "no batch in flight");
@@ -1417,6 +1453,7 @@ gome_status gome_collect_device(gome_engine* e, const gome_event** dev_events, s
 
 gome_status gome_collect(gome_engine* e, const gome_event** events, size_t* n_events, gome_stats* stats) {
   if (!e || !events || !n_events) return GOME_E_INVAL;
+  DevGuard dg(e->cfg.device);
   gome_status st = e->collect(events, n_events);
   if (st == GOME_OK && stats) *stats = e->stats;
   return st;
@@ -1450,6 +1487,7 @@ size_t gome_pending_events(const gome_engine* e) {
 
 gome_status gome_drain_events(gome_engine* e, gome_event* out, size_t cap, size_t* n_out) {
   if (!e || !n_out || (cap && !out)) return GOME_E_INVAL;
+  DevGuard dg(e->cfg.device);
   if (gome_status s = e->collect_all()) return s;
   size_t c = 0;
   size_t hp = e->pending.size() - e->pending_pos;
@@ -1487,6 +1525,7 @@ gome_status gome_release_device_events(gome_engine* e) {
 
 gome_status gome_debug_flow_books(gome_engine* e, uint32_t* out, size_t cap, size_t* n_out) {
   if (!e || !n_out || (cap && !out)) return GOME_E_INVAL;
+  DevGuard dg(e->cfg.device);
   gome_status s = e->collect_all();
   if (s != GOME_OK) return s;
   const size_t n = std::min<size_t>({cap, static_cast<size_t>(e->stats.n_hot), static_cast<size_t>(gome::MAX_FLOW)});
@@ -1505,6 +1544,7 @@ gome_status gome_debug_flow_books(gome_engine* e, uint32_t* out, size_t cap, siz
 
 gome_status gome_debug_peek(gome_engine* e, uint32_t which, uint64_t offset, uint64_t bytes, void* out) {
   if (!e || (bytes && !out)) return GOME_E_INVAL;
+  DevGuard dg(e->cfg.device);
   gome_status s = e->collect_all();
   if (s != GOME_OK) return s;
   const uint64_t nb = e->max_batch;
@@ -1533,6 +1573,7 @@ gome_status gome_get_stats(const gome_engine* e, gome_stats* out) {
 
 gome_status gome_top_of_book(gome_engine* e, const uint32_t* symbols, size_t n, gome_tob* out) {
   if (!e || (n && (!symbols || !out))) return GOME_E_INVAL;
+  DevGuard dg(e->cfg.device);
   if (gome_status s = e->collect_all()) return s;
   if (n == 0) return GOME_OK;
   if (n > (1u << 20)) return e->fail(GOME_E_INVAL, "gome_top_of_book: more than 2^20 symbols");
@@ -1717,6 +1758,7 @@ gome_status gome_engine::load_books(size_t nb, const uint32_t* bsym, const uint3
 gome_status gome_load_books(gome_engine* e, size_t n_books, const uint32_t* book_sym, const uint32_t* book_nlv,
                             const gome_level* levels, const gome_node* nodes, size_t n_nodes) {
   if (!e) return GOME_E_INVAL;
+  DevGuard dg(e->cfg.device);
   if (gome_status st = e->collect_all()) return st;
   return e->load_books(n_books, book_sym, book_nlv, levels, nodes, n_nodes);
 }
@@ -1724,6 +1766,7 @@ gome_status gome_load_books(gome_engine* e, size_t n_books, const uint32_t* book
 gome_status gome_snapshot_levels(gome_engine* e, uint32_t sym, gome_level* out, size_t cap,
                                  size_t* n_out) {
   if (!e || !n_out || (cap && !out)) return GOME_E_INVAL;
+  DevGuard dg(e->cfg.device);
   if (gome_status st = e->collect_all()) return st;
   if (sym >= e->cfg.max_symbols) return e->fail(GOME_E_NOTFOUND, "symbol_id out of range");
   Book bk;
@@ -1753,6 +1796,7 @@ gome_status gome_snapshot_levels(gome_engine* e, uint32_t sym, gome_level* out, 
 gome_status gome_snapshot_fifo(gome_engine* e, uint32_t sym, int64_t price, gome_node* out,
                                size_t cap, size_t* n_out) {
   if (!e || !n_out || (cap && !out)) return GOME_E_INVAL;
+  DevGuard dg(e->cfg.device);
   if (gome_status st = e->collect_all()) return st;
   if (sym >= e->cfg.max_symbols) return e->fail(GOME_E_NOTFOUND, "symbol_id out of range");
   Book bk;

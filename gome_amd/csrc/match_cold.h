@@ -23,6 +23,7 @@ struct BatchArgs {
   const uint32_t* sidx;       // segment position -> batch index (the radix sort's permutation)
   const uint32_t* adm_flag;   // per batch index: admitted ADD (k_adm_flag)
   unsigned long long seq_base;  // sequence number of batch index 0 (published events)
+  uint32_t* dup_list;         // batch indices of the ADDs the duplicate-oid rule rejected (Q7)
 };
 
 // The Prep record of segment position b built from the input (what k_prep writes to
@@ -668,7 +669,12 @@ __device__ __forceinline__ void process_global(WaveCtx& W, uint32_t b0, uint32_t
       uint32_t nev = 0;
       if (a == GOME_ADD) {
         W.adds++;
-        if (rl(q.adm, j)) {
+        const uint32_t adm = rl(q.adm, j);
+        uint32_t ixs, loc;
+        if (adm == ADM_V_CHECK && idx_lookup(W, rl(q.oid, j), ixs, loc)) {
+          W.dropped++;  // (S, oid) names a live node: the duplicate-oid rule (Q7, pipeline.h)
+          if (lane == 0) dup_note(W.D.st, W.B.dup_list, idx);
+        } else if (adm != ADM_V_NO) {
           nev = do_add(W, rl64(q.price, j), rl64(q.vol, j), rl(q.oid, j), rl(q.uuid, j), rl(q.side, j), idx);
         } else {
           W.dropped++;  // marker already consumed (engine.go:58-60)
@@ -696,6 +702,7 @@ __device__ __forceinline__ void wave_finish(WaveCtx& W, bool flush = true) {
     nb.lvl_cap = W.hcap;
     nb.pad = W.flags;
     W.D.books[W.sym] = nb;
+    if (W.flags & BOOK_QUIRK) quirk_note(W.D, W.sym);  // (k_requalify)
   }
   if (flush) wave_flush(W);
 }

@@ -375,7 +375,7 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep(Dev D, BatchArgs B, Flo
       if (q.action != GOME_ADD) continue;
       my_adds++;
       if (!q.adm) { my_drop++; continue; }
-      if (q.vol == 0) { bad = 1; break; }
+      if (q.vol == 0 || q.adm == ADM_V_CHECK) { bad = 1; break; }  // (Q6; Q7 candidates: serial kernels)
       {  // gcd, with a cheap divisibility test first (exact: integers < 2^53 as doubles)
         const unsigned long long v = static_cast<unsigned long long>(q.vol);
         const double qd = static_cast<double>(v) / static_cast<double>(mg ? mg : 1);
@@ -659,7 +659,7 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep_a(Dev D, BatchArgs B, F
       if (q.action != GOME_ADD) continue;
       my_adds++;
       if (!q.adm) { my_drop++; continue; }
-      if (q.vol == 0) { my_bad = 1; break; }
+      if (q.vol == 0 || q.adm == ADM_V_CHECK) { my_bad = 1; break; }  // (Q6; Q7 candidates: serial kernels)
       const unsigned long long v = static_cast<unsigned long long>(q.vol);
       const double qd = static_cast<double>(v) / static_cast<double>(mg ? mg : 1);
       if (mg == 0 || static_cast<unsigned long long>(qd) * mg != v) mg = fl_gcd(mg, v);

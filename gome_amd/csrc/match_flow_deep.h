@@ -139,7 +139,7 @@ __device__ __forceinline__ void k_deep_prep_a_one(Dev D, BatchArgs B, FlowArgs F
     if (q.action != GOME_ADD) continue;
     my_adds++;
     if (!q.adm) { my_drop++; continue; }
-    if (q.vol == 0) { my_bad = 1; continue; }  // a zero-volume maker (Q6)
+    if (q.vol == 0 || q.adm == ADM_V_CHECK) { my_bad = 1; continue; }  // a zero-volume maker (Q6), a Q7 candidate
     const unsigned long long v = static_cast<unsigned long long>(q.vol);
     mg = fl_gcd(mg, v);
     msum = min(msum + v, FL_SUM_CAP);

@@ -102,6 +102,7 @@ struct HotEnv {
   uint32_t* lvl_bump;
   ResumeRec* resume;
   LvlPool lpool;
+  uint32_t* dup_list;  // (BatchArgs::dup_list)
   uint32_t ch_cap, arena_cap, lvl_cap_total, lvl_base, lvl_cap, beg, end, pad;
 };
 
@@ -1078,6 +1079,14 @@ __device__ __forceinline__ uint32_t hot_cancel(HotCtx& H, int64_t p, uint32_t oi
   return H.fatal ? 0u : 1u;
 }
 
+// Duplicate-oid rule (Q7): does (S, oid) name a live node now?  The index after the pending
+// inserts of this segment's rests (the deferred inserts of nodes consumed since are dead).
+__device__ __forceinline__ bool hot_oid_live(HotCtx& H, uint32_t oid) {
+  if (lds_get(H.S->nflushed) < H.npend) hot_flush(H);
+  uint32_t ixslot, loc;
+  return hot_idx_lookup(H, oid, ixslot, loc);
+}
+
 // Write the book back to HBM: head volumes into their cached chunks, every cached chunk,
 // then the level array into the book's level block.
 __device__ __forceinline__ void hot_writeback(HotCtx& H, GOME_GLB Level* Lv) {
@@ -1159,6 +1168,7 @@ __global__ __launch_bounds__(64) void k_match_hot(Dev D, BatchArgs B, PendEnt* p
     e.lvl_bump = D.lvl_bump;
     e.resume = resume;
     e.lpool = lvl_pool(D);
+    e.dup_list = B.dup_list;
     e.ch_cap = D.ch_cap;
     e.arena_cap = B.arena_cap;
     e.lvl_cap_total = D.lvl_cap_total;
@@ -1238,7 +1248,12 @@ __global__ __launch_bounds__(64) void k_match_hot(Dev D, BatchArgs B, PendEnt* p
       const uint32_t fl = rl(y.w, j), a = (fl >> 8) & 0xFFu;
       uint32_t nev = 0;
       if (a == GOME_ADD) {
-        if ((fl >> 16) & 1u) {
+        const uint32_t admv = (fl >> 16) & 0xFFu;
+        if (admv == ADM_V_CHECK && hot_oid_live(H, rl(y.x, j))) {
+          // (S, oid) names a live node: the duplicate-oid rule (Q7, pipeline.h)
+          H.dropped += 1u;
+          if (lane == 0) dup_note(S->env.st, S->env.dup_list, rl(y.z, j));
+        } else if (admv != ADM_V_NO) {
           int64_t trest = 0;
           const int64_t p = static_cast<int64_t>((static_cast<uint64_t>(rl(x.y, j)) << 32) | rl(x.x, j));
           const int64_t v = static_cast<int64_t>((static_cast<uint64_t>(rl(x.w, j)) << 32) | rl(x.z, j));
@@ -1281,7 +1296,7 @@ __global__ __launch_bounds__(64) void k_match_hot(Dev D, BatchArgs B, PendEnt* p
     const bool mine = lane < j;
     H.adds += __popcll(__ballot(mine && act == GOME_ADD));
     H.dels += __popcll(__ballot(mine && act == GOME_DEL));
-    H.dropped += __popcll(__ballot(mine && act == GOME_ADD && !((y.w >> 16) & 1u)));
+    H.dropped += __popcll(__ballot(mine && act == GOME_ADD && ((y.w >> 16) & 0xFFu) == ADM_V_NO));
     if (mine) gp(S->env.ev_count)[y.z] = evc;
   }
   if (spilled) hot_resolve_pending(H);  // the HBM path expects real index slots

@@ -246,10 +246,14 @@ __global__ void k_seg_scatter(const uint32_t* seg_start, const Status* st, uint3
 // Duplicate oids.  The reference names a resting node S:node:<oid> with
 // no uuid (ordernode.go:110-112, nodelink.go:119-122) and assumes oids unique per symbol
 // (README.md:27); a second live node with the same name corrupts its FIFO.  The boundary rule,
-// the same on every path and in the oracle: an admitted ADD whose (S, oid) rests in the book at
-// batch start, or was carried by an earlier admitted ADD of the same batch, is not applied
-// (dropped like an ADD without a marker), counted (gome_stats.n_dup_oid) and its batch index
-// reported (gome_dup_records).
+// the same on every path and in the oracle: an admitted ADD whose (S, oid) names a live node when
+// the ADD is applied is not applied (dropped like an ADD without a marker), counted
+// (gome_stats.n_dup_oid) and its batch index reported (gome_dup_records).  Whether the node is
+// still live depends on the matching before it in the batch, so admission only marks the
+// candidates: an admitted ADD whose (S, oid) rests at batch start, or was carried by an earlier
+// admitted ADD of the batch, gets verdict ADM_V_CHECK (2).  The flow preps decline a book with
+// one; the serial kernels (match_cold.h, match_hot.h) probe the cancel index as they reach it.
+// Every ADD the rule rejects is a candidate, so the rule depends on the queue order only.
 //
 // Both rules key on (S, oid) first.  k_adm puts every ADD / DEL into one open-addressing table
 // of 64-bit words keyed (S, oid): a key's slot holds its fingerprint (high half, never 0) and
@@ -266,6 +270,8 @@ __global__ void k_seg_scatter(const uint32_t* seg_start, const Status* st, uint3
 // k_oid_max): fresh, increasing oids (interned in arrival order) never probe.
 constexpr uint32_t ADM_RESTING = 0x80000000u, ADM_MULTI = 0x40000000u, ADM_OK = 0x20000000u;
 constexpr uint32_t ADM_SLOT = 0x1FFFFFFFu;  // (table slots < 2^29)
+// final verdicts (Prep::adm): not admitted, admitted, admitted but its (S, oid) may be live (Q7)
+constexpr uint32_t ADM_V_NO = 0u, ADM_V_YES = 1u, ADM_V_CHECK = 2u;
 
 // Read-only probe of the (S, oid) cancel index: does a live node carry this key?
 __device__ __forceinline__ bool idx_live(const IdxEnt* idx, unsigned long long mask, unsigned long long key) {
@@ -367,13 +373,12 @@ __global__ void k_adm(const gome_order* ord, uint32_t n, unsigned long long* tab
   slot[i] = h | (resting ? ADM_RESTING : 0u);
 }
 
-// Pass 2: records alone with their (S, oid) get their final 0 / 1 verdict (a rejected resting
-// duplicate is counted and listed: list = this batch slot's buffer, the host sorts it);
-// the others enter the (S, uuid, oid) table (slot2) and keep slot | ADM_MULTI.  aux[i] = the
-// (S, oid) slot of a shared key's record, else NIL (for k_adm_clean).
+// Pass 2: records alone with their (S, oid) get their final verdict (ADM_V_CHECK when the key
+// rests at batch start); the others enter the (S, uuid, oid) table (slot2) and keep
+// slot | ADM_MULTI.  aux[i] = the (S, oid) slot of a shared key's record, else NIL (k_adm_clean).
 __global__ void k_adm_flag(const gome_order* ord, uint32_t n, uint32_t* slot, const uint8_t* multi,
-                           unsigned long long* tab2, uint32_t* slot2, uint32_t* aux, uint32_t mask, Status* st,
-                           uint32_t* list, unsigned long long* tab, const uint32_t* notfast) {
+                           unsigned long long* tab2, uint32_t* slot2, uint32_t* aux, uint32_t mask,
+                           unsigned long long* tab, const uint32_t* notfast) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n || !*notfast) return;
   const uint32_t s = slot[i];
@@ -385,9 +390,7 @@ __global__ void k_adm_flag(const gome_order* ord, uint32_t n, uint32_t* slot, co
   if (!shared) {
     if (g.action != GOME_ADD) { slot[i] = 0; return; }
     const bool adm = (g.flags & GOME_ORD_ADM_HOST) ? (g.flags & GOME_ORD_ADMITTED) != 0 : true;
-    const bool dup = adm && (s & ADM_RESTING);
-    slot[i] = adm && !dup ? 1u : 0u;
-    if (dup) list[atomicAdd(&st->ctr[C_DUP], 1ull)] = i;
+    slot[i] = !adm ? ADM_V_NO : (s & ADM_RESTING) ? ADM_V_CHECK : ADM_V_YES;
     return;
   }
   const unsigned long long km = mix64((static_cast<unsigned long long>(g.symbol_id) << 40) ^
@@ -418,17 +421,20 @@ __global__ void k_adm_res(const gome_order* ord, uint32_t n, uint32_t* slot, con
 }
 
 // Pass 4 (shared keys): final verdicts; an admitted ADD that is not its key's first admitted ADD,
-// or whose oid rests at batch start, is a duplicate.
-__global__ void k_adm_dup(uint32_t n, uint32_t* slot, const uint32_t* first, Status* st, uint32_t* list,
-                          const uint32_t* notfast) {
+// or whose oid rests at batch start, is a candidate of the duplicate-oid rule (ADM_V_CHECK).
+__global__ void k_adm_dup(uint32_t n, uint32_t* slot, const uint32_t* first, const uint32_t* notfast) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n || !*notfast) return;
   const uint32_t s = slot[i];
   if (!(s & ADM_MULTI)) return;
   const bool adm = (s & ADM_OK) != 0;
-  const bool dup = adm && ((s & ADM_RESTING) || first[s & ADM_SLOT] != i);
-  slot[i] = adm && !dup ? 1u : 0u;
-  if (dup) list[atomicAdd(&st->ctr[C_DUP], 1ull)] = i;
+  const bool check = adm && ((s & ADM_RESTING) || first[s & ADM_SLOT] != i);
+  slot[i] = !adm ? ADM_V_NO : check ? ADM_V_CHECK : ADM_V_YES;
+}
+
+// An ADD with verdict ADM_V_CHECK that the serial kernels found live: rejected (one thread).
+__device__ __forceinline__ void dup_note(Status* st, uint32_t* list, uint32_t i) {
+  list[atomicAdd(&st->ctr[C_DUP], 1ull)] = i;
 }
 
 // Pass 5 (shared keys): their entries of the second table, first[] and multi[] back to empty.

@@ -26,7 +26,7 @@ _SUM_KEYS = ("n_orders", "n_add", "n_del", "n_dropped", "n_fills", "n_cancels", 
              "n_resting", "n_levels", "n_segments", "n_hot", "n_hot_orders", "n_hot_fills", "n_hot_rests",
              "n_hot_cancels", "n_flow_books", "n_flow_orders", "n_flow_touches", "n_flow_head_orders",
              "n_flow_head_touches", "n_flow_cancels", "n_dup_oid", "n_flow_tail_fills", "n_index_rebuilds", "idx_tombstones",
-             "lvl_used")
+             "lvl_used", "n_quirk_checked", "n_requalified")
 _TOTAL_KEYS = ("n_resting", "n_levels", "n_index_rebuilds", "idx_tombstones", "lvl_used")
 _MAX_KEYS = ("max_segment", "ms_total", "ms_match", "ms_hot", "ms_flow_plan", "ms_cold")
 
@@ -61,6 +61,8 @@ class Router:
         self.owner = np.asarray(owner, dtype=np.int32)
         assert self.owner.min(initial=0) >= 0 and self.owner.max(initial=0) < self.world
         self.max_batch = min(int(e.max_batch) for e in self.engines)
+        # (symbol ids the owner table and every handle accept)
+        self.max_symbols = min([len(self.owner)] + [int(getattr(e, "max_symbols", len(self.owner))) for e in self.engines])
         self._pool = ThreadPoolExecutor(max_workers=self.world) if self.world > 1 else None
         self._ev = np.zeros(0, EVENT_DTYPE)
         self._stats: list[dict] = [{} for _ in self.engines]

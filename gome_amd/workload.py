@@ -221,3 +221,38 @@ class NativeStream:
             self.h = None
 
     __del__ = close
+
+
+def inject_quirks(rec: np.ndarray, sym: int, levels: np.ndarray, fifo, mode: str = "heal") -> dict:
+    """Rewrite the first records of symbol `sym` in `rec` (in place) into the two legal inputs
+    that put a book in a quirk state:
+      * Q2: wrong-side cancels (`transaction` flipped, price and oid right) of every maker of one
+        bid level, which empty its FIFO while DeletePoolDepth ZREMs the *ask* set
+        (engine.go:87-116, nodepool.go:76-83): the level stays in S:BUY with no FIFO;
+      * Q6: a zero-volume BUY ADD ("Volume": null decodes to 0) at another bid level, which rests
+        as a zero-volume maker behind that level's FIFO (engine.go:69-82).
+    mode "heal": the Q2 level is the best bid and the Q6 level the second best, where the stream
+    soon rests and consumes again (the reference's state heals); mode "stuck": the Q2 level is
+    the lowest bid, which the stream never reaches again (the quirk stays).  `levels` / `fifo`
+    are the book's state before `rec` (gome_snapshot_levels / gome_snapshot_fifo, or the
+    oracle's).  Returns what was injected."""
+    bids = levels[(levels["in_buy"] != 0) & (levels["in_sale"] == 0) & (levels["n_nodes"] > 0)]
+    if len(bids) < 3:
+        raise ValueError("book has fewer than three bid levels")
+    bids = np.sort(bids, order="price_fx")
+    q2 = bids[-1] if mode == "heal" else bids[0]
+    q6 = bids[-2] if mode == "heal" else bids[1]
+    makers = fifo(int(q2["price_fx"]))
+    pos = np.nonzero((rec["symbol_id"] == sym) & (rec["action"] == ADD))[0]
+    if len(pos) < len(makers) + 1:
+        raise ValueError("too few records of the symbol to rewrite")
+    for i, m in zip(pos, makers):  # the wrong-side cancels
+        r = rec[i]
+        r["price_fx"], r["volume_fx"] = q2["price_fx"], m["volume_fx"]
+        r["oid_id"], r["uuid_id"] = m["oid_id"], m["uuid_id"]
+        r["side"] = 0 if m["side"] == 1 else 1
+        r["action"], r["flags"] = DEL, 0
+    z = rec[pos[len(makers)]]  # the zero-volume ADD keeps the record's own (fresh) oid
+    z["price_fx"], z["volume_fx"], z["side"] = q6["price_fx"], 0, 0
+    return {"q2_price": int(q2["price_fx"]), "q2_cancels": len(makers), "q6_price": int(q6["price_fx"]),
+            "q6_oid": int(z["oid_id"]), "records": [int(i) for i in pos[:len(makers) + 1]]}

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define GOME_ABI_VERSION 7u
+#define GOME_ABI_VERSION 8u
 
 /* ---- status codes (replace the reference's swallowed errors / panics,
  *      rabbitmq.go:44-49,70-72,120-122; nodelink.go:132,142,157) ---------- */
@@ -234,6 +234,11 @@ typedef struct gome_stats {
                                                  1 = deep books, 2 = books with DELs     */
   uint32_t chains_wanted;                     /* chains its candidates asked for (same bits;
                                                  wanted and not enqueued: legacy / cold)  */
+  uint64_t n_quirk_checked;                   /* books in a quirk state (wrong-side cancel Q2,
+                                                 zero-volume maker Q6) the legacy / cold
+                                                 kernels applied this batch (ABI >= 8)    */
+  uint64_t n_requalified;                     /* ... of which healed: back on the flow path
+                                                 from the next batch on (ABI >= 8)        */
 } gome_stats;
 
 typedef struct gome_engine gome_engine;

@@ -24,8 +24,9 @@
  *   - per-batch admission markers (S:comparison, nodepool.go:14-28) under the
  *     deterministic ingress model of literal.run_batches (Q4);
  *   - the boundary's duplicate-oid rule (Q7, gome_abi.h): an admitted ADD whose (S, oid)
- *     rests at batch start, or was carried by an earlier admitted ADD of the batch, is not
- *     applied (literal.py's consumer applies the same rule before DoOrder).
+ *     names a live node when the ADD is applied is not applied (literal.py's
+ *     consume_boundary applies the same rule before DoOrder).  It depends on the queue order
+ *     only, not on where batches start and end.
  * All arithmetic is int64 on value*10^accuracy (exact on the parity domain).
  */
 #include <stdint.h>
@@ -71,10 +72,8 @@ typedef struct oracle {
   uint64_t* adm; /* stores hashed (sym,uuid,oid) triple as two words */
   uint32_t* adm3;
   uint64_t admcap;
-  uint64_t* dupk;   /* (S, oid) keys of the batch's admitted ADDs (Q7) */
-  uint8_t* rest0;   /* per record: an ADD whose (S, oid) rests at batch start */
   uint32_t* dups;   /* batch indices rejected by the Q7 rule */
-  uint64_t ndups, rest0cap;
+  uint64_t ndups, dupcap;
   /* events */
   gome_event* ev;
   uint64_t nev, capev;
@@ -286,16 +285,6 @@ static int adm_first(oracle* o, const gome_order* r) {
   }
 }
 
-/* First admitted ADD of (S, oid) in this batch?  (Q7, the earlier-in-batch half) */
-static int dup_first(oracle* o, uint64_t key) {
-  uint64_t m = o->admcap - 1, h = mix64(key ^ 0x9E3779B97F4A7C15ULL) & m;
-  for (;;) {
-    if (!o->dupk[h]) { o->dupk[h] = key; return 1; }
-    if (o->dupk[h] == key) return 0;
-    h = (h + 1) & m;
-  }
-}
-
 /* ---------------------------------------------------------------- API */
 oracle* oracle_create(uint32_t max_symbols) {
   oracle* o = (oracle*)calloc(1, sizeof(oracle));
@@ -309,7 +298,7 @@ void oracle_destroy(oracle* o) {
   if (!o) return;
   for (uint32_t s = 0; s < o->max_symbols; ++s) free(o->books[s].lv);
   free(o->books); free(o->nodes); free(o->idx); free(o->adm); free(o->adm3); free(o->ev);
-  free(o->dupk); free(o->rest0); free(o->dups);
+  free(o->dups);
   free(o);
 }
 
@@ -322,23 +311,17 @@ int oracle_submit(oracle* o, const gome_order* r, uint64_t n) {
   uint64_t need = 16;
   while (need < 2 * n) need <<= 1;
   if (need > o->admcap) {
-    free(o->adm); free(o->adm3); free(o->dupk);
+    free(o->adm); free(o->adm3);
     o->admcap = need;
     o->adm = (uint64_t*)malloc(need * sizeof(uint64_t));
     o->adm3 = (uint32_t*)malloc(need * 3 * sizeof(uint32_t));
-    o->dupk = (uint64_t*)malloc(need * sizeof(uint64_t));
   }
-  if (n > o->rest0cap) {
-    free(o->rest0); free(o->dups);
-    o->rest0cap = n;
-    o->rest0 = (uint8_t*)malloc(n);
+  if (n > o->dupcap) {
+    free(o->dups);
+    o->dupcap = n;
     o->dups = (uint32_t*)malloc(n * sizeof(uint32_t));
   }
   memset(o->adm, 0, o->admcap * sizeof(uint64_t));
-  memset(o->dupk, 0, o->admcap * sizeof(uint64_t));
-  /* Q7: which ADDs' (S, oid) rest in the book as the batch starts */
-  for (uint64_t i = 0; i < n; ++i)
-    o->rest0[i] = r[i].action == GOME_ADD && idx_find(o, okey(r[i].symbol_id, r[i].oid_id)) >= 0;
   o->ndups = 0;
   o->st.n_dup_oid = 0;
   for (uint64_t i = 0; i < n; ++i) {
@@ -349,7 +332,7 @@ int oracle_submit(oracle* o, const gome_order* r, uint64_t n) {
       int adm = adm_first(o, q); /* engine.go:58-62 (batch model) */
       if (q->flags & GOME_ORD_ADM_HOST) adm = (q->flags & GOME_ORD_ADMITTED) != 0; /* host markers */
       if (!adm) { o->st.n_dropped++; continue; }
-      if (!dup_first(o, okey(q->symbol_id, q->oid_id)) || o->rest0[i]) { /* Q7 */
+      if (idx_find(o, okey(q->symbol_id, q->oid_id)) >= 0) { /* Q7: (S, oid) names a live node */
         o->st.n_dropped++;
         o->st.n_dup_oid++;
         o->dups[o->ndups++] = (uint32_t)i;

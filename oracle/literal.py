@@ -157,13 +157,44 @@ def _go_field_value(kind: str, name: str, v):
     return n if -(1 << (b - 1)) <= n < (1 << (b - 1)) else None
 
 
-def go_unmarshal_order_node(body: str) -> "OrderNode":
+def _go_coerce_utf8(b: bytes) -> str:
+    """Go's unquoteBytes coercion (encoding/json decode.go): each byte that does not start a valid
+    UTF-8 encoding (utf8.DecodeRune -> (RuneError, 1): bad lead, truncated, overlong, surrogate or
+    beyond U+10FFFF) becomes U+FFFD and decoding resumes at the next byte."""
+    out, i, n = [], 0, len(b)
+    while i < n:
+        c = b[i]
+        if c < 0x80:
+            out.append(chr(c))
+            i += 1
+            continue
+        size, lo, hi = (2, 0x80, 0x7FF) if 0xC2 <= c <= 0xDF else (3, 0x800, 0xFFFF) if 0xE0 <= c <= 0xEF else \
+            (4, 0x10000, 0x10FFFF) if 0xF0 <= c <= 0xF4 else (0, 0, 0)
+        cp = None
+        if size and i + size <= n and all(0x80 <= x <= 0xBF for x in b[i + 1:i + size]):
+            v = c & (0x7F >> size)
+            for x in b[i + 1:i + size]:
+                v = (v << 6) | (x & 0x3F)
+            if lo <= v <= hi and not 0xD800 <= v <= 0xDFFF:
+                cp = v
+        if cp is None:
+            out.append("\ufffd")
+            i += 1
+        else:
+            out.append(chr(cp))
+            i += size
+    return "".join(out)
+
+
+def go_unmarshal_order_node(body) -> "OrderNode":
     """json.Unmarshal(body, &OrderNode{}) as rabbitmq.go:118-121 runs it (the error is printed
     and DoOrder still runs): a syntax error decodes nothing (zero node, Action 0, ignored by
     DoOrder); otherwise every field whose JSON value fits its Go type is set, keys matched
     exactly or case-insensitively, later duplicates winning; a field of the wrong type, an
     overflowing number or a null stays zero."""
     node = OrderNode()
+    if isinstance(body, (bytes, bytearray)):
+        body = _go_coerce_utf8(bytes(body))
     try:
         d = json.loads(body, parse_int=_Num, parse_float=_Num, parse_constant=_no_constant,
                        object_pairs_hook=_Obj)
@@ -514,25 +545,34 @@ class GomeLiteral:
         self.PublishNewOrder(n)
 
     def consume(self):  # rabbitmq.go:116-125, one message at a time
-        """One drained batch.  Before DoOrder, the batching consumer's duplicate-oid rule (the
-        boundary's, gome_abi.h): an ADD that holds its admission marker
-        but whose (Symbol, Oid) rests in the book as the batch starts, or was carried by an
-        earlier admitted ADD of the batch, is consumed (marker cleared, engine.go:62) and not
-        applied.  `self.dups` = the batch indices of such ADDs."""
+        """The reference's consumer loop, faithfully: every queued message is decoded and
+        handed to DoOrder (rabbitmq.go:118-124).  A second ADD of a live (Symbol, Oid) corrupts
+        the FIFO here exactly as in the reference (Q7); see consume_boundary."""
         q, self.do_order_q = self.do_order_q, []
-        resting = self.resting_oids()
-        seen = set()
+        for body in q:
+            self.DoOrder(go_unmarshal_order_node(body))
+
+    def consume_boundary(self):
+        """The same loop behind the drop-in boundary's duplicate-oid rule (gome_abi.h; SURVEY
+        Appendix A Q7): an ADD that holds its admission marker but whose (Symbol, Oid) names a
+        live node when it is consumed (an S:node:<oid> field of one of the symbol's S:link:<p>
+        hashes, nodelink.go:119-122) is consumed (marker cleared, engine.go:62) and not applied.
+        The rule depends on the queue order only, not on how the queue is cut into batches.
+        `self.dups` = the positions (in this call's messages) of such ADDs."""
+        q, self.do_order_q = self.do_order_q, []
         self.dups = []
         for i, body in enumerate(q):
             node = go_unmarshal_order_node(body)
-            if node.Action == ADD and self.ExistsPrePool(node):
-                key = (node.Symbol, node.Oid)
-                if key in resting or key in seen:
-                    self.DeletePrePool(node)
-                    self.dups.append(i)
-                    continue
-                seen.add(key)
+            if node.Action == ADD and self.ExistsPrePool(node) and self.oid_live(node.Symbol, node.Oid):
+                self.DeletePrePool(node)
+                self.dups.append(i)
+                continue
             self.DoOrder(node)
+
+    def oid_live(self, symbol: str, oid: str) -> bool:
+        """Does one of the symbol's FIFOs (S:link:<p>) hold the node S:node:<oid>?"""
+        pre, field = symbol + ":link:", symbol + ":node:" + oid
+        return any(field in hv for key, hv in self.cache.h.items() if key.startswith(pre))
 
     def resting_oids(self) -> set:
         """(Symbol, Oid) of every node resting in a FIFO (an S:node:<oid> field of S:link:<p>)."""
@@ -709,6 +749,6 @@ def run_batches(requests_batches, accuracy: int = 8):
                 n = NewOrderNode(req, accuracy)
                 n.Action = action
                 eng.PublishNewOrder(n)
-        eng.consume()
+        eng.consume_boundary()
         results.extend(eng.take_results())
     return eng, results

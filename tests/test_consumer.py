@@ -20,6 +20,7 @@ from oracle.pyoracle import Oracle
 class _OracleEngine:
     def __init__(self, n_sym, max_batch):
         self.o, self.max_batch, self._ev = Oracle(n_sym), max_batch, None
+        self.max_symbols = n_sym
 
     def submit(self, rec, seq_base=0):
         ev = self.o.submit(rec)
@@ -98,16 +99,17 @@ def _run(ops, engine, lit_json: bool):
             lit.grpc_delete_order(arg)
             q.append(lit.do_order_q[-1]) if lit_json else ing.delete_order(arg)
         else:
-            # the reference consumes one message at a time; the duplicate-oid rule (Q7) is per
-            # batch, so the literal consumes the same batches the consumer drains
+            # the reference consumes one message at a time (and so does the literal here); the
+            # consumer drains batches of up to max_batch: the published bytes must not differ
             k = min(arg, len(lit.do_order_q))
-            while k:
-                m = min(k, cons.max_batch)
-                head, lit.do_order_q = lit.do_order_q[:m], lit.do_order_q[m:]
+            for _ in range(k):
+                head, lit.do_order_q = lit.do_order_q[:1], lit.do_order_q[1:]
                 saved, lit.do_order_q = lit.do_order_q, head
-                lit.consume()
+                lit.consume_boundary()
                 lit.do_order_q = saved
                 lit_out += lit.take_results()
+            while k:
+                m = min(k, cons.max_batch)
                 cons.process(q[:m])
                 del q[:m]
                 k -= m
@@ -170,6 +172,9 @@ ODD_MESSAGES = [
     '[1,2,3]', 'null', '{"Action":1', '{"Action":NaN}',  # non-object / syntax errors: zero node
     _msg(oid="11", sym='a\\ud800b', tx="1", price="50000000"),  # lone surrogate -> U+FFFD
     _msg(oid="12", price="5e7", vol="1E8"),            # exponent floats are fine for float64
+    _msg(oid="13", vol="-100000000").encode(),         # raw bytes; a negative Volume: rejected
+    _msg(oid="14", sym="b\xe2\x82z", tx="1", price="50000000").encode("latin-1"),  # invalid UTF-8:
+    _msg(oid="15", sym="b\xed\xa0\x80\xffz", price="50000000").encode("latin-1"),  # U+FFFD per byte
 ]
 
 
@@ -203,23 +208,25 @@ def _run_raw(ops, engine):
             nd.SetDepthHashKey()
             nd.SetNodeLink()
             nd.SetListZsetKey()
-            lit.SetPrePool(nd)
             pre.set(nd.Symbol, nd.Uuid, nd.Oid)
-            lit.do_order_q.append(nd.to_json())  # the literal consumes Go's view of the message
             q.append(arg)
+            if nd.Volume < 0:  # outside the exact domain: the consumer rejects it (not compared)
+                continue
+            lit.SetPrePool(nd)
+            lit.do_order_q.append(nd.to_json())  # the literal consumes Go's view of the message
         elif op == "add":
             lit.grpc_do_order(arg)
             pre.set(arg["symbol"], arg["uuid"], arg["oid"])
             q.append(lit.do_order_q[-1])
         else:
             k = min(arg, len(q))
+            head, lit.do_order_q = lit.do_order_q[:k], lit.do_order_q[k:]
+            saved, lit.do_order_q = lit.do_order_q, head
+            lit.consume_boundary()
+            lit.do_order_q = saved
+            lit_out += lit.take_results()
             while k:
                 m = min(k, cons.max_batch)
-                head, lit.do_order_q = lit.do_order_q[:m], lit.do_order_q[m:]
-                saved, lit.do_order_q = lit.do_order_q, head
-                lit.consume()
-                lit.do_order_q = saved
-                lit_out += lit.take_results()
                 cons.process(q[:m])
                 del q[:m]
                 k -= m
@@ -238,14 +245,31 @@ def test_decode_like_go_unmarshal():
     assert decode_order_node(ODD_MESSAGES[3])["Action"] == 0
     assert decode_order_node(ODD_MESSAGES[6])["Price"] == 45000000.0
     assert decode_order_node(ODD_MESSAGES[7])["Oid"] == "8"
-    assert decode_order_node(ODD_MESSAGES[-2])["Symbol"] == "a�b"
+    assert decode_order_node(ODD_MESSAGES[-5])["Symbol"] == "a\ufffdb"
+    assert decode_order_node(ODD_MESSAGES[-2])["Symbol"] == "b\ufffd\ufffdz"
+    assert decode_order_node(ODD_MESSAGES[-1])["Symbol"] == "b\ufffd\ufffd\ufffd\ufffdz"
 
 
 def test_consumer_odd_messages_match_literal_cpu():
     lit_out, got, cons = _run_raw(_odd_schedule(), _OracleEngine(4, 64))
     assert len(lit_out) > 5
     assert got == lit_out
-    assert cons.consumed == len(ODD_MESSAGES) + 20 and cons.rejected == 0
+    assert cons.consumed == len(ODD_MESSAGES) + 20 and cons.rejected == 1  # (the negative Volume)
+
+
+def test_consumer_rejects_symbols_beyond_max_symbols_and_negative_volumes():
+    """a message the engine would refuse the whole batch for (a Symbol beyond its
+    max_symbols, a negative Volume) is rejected on its own; the rest of the batch is applied."""
+    pre, sink = PrePool(), MatchSink()
+    cons = BatchingConsumer(_OracleEngine(2, 16), pre, sink, max_batch=16)
+    msgs = []
+    for k, (sym, tx, vol) in enumerate([("a", 0, "100000000"), ("b", 1, "100000000"), ("c", 0, "100000000"),
+                                        ("a", 1, "-5"), ("c", 1, "100000000"), ("b", 0, "100000000")]):
+        pre.set(sym, "u", str(k))
+        msgs.append(_msg(sym=sym, oid=str(k), tx=tx, vol=vol))
+    cons.process(msgs)
+    assert cons.consumed == 6 and cons.rejected == 3 and len(pre) == 0
+    assert len(sink.q) == 1 and '"Oid":"5"' in sink.q[0] and '"Oid":"1"' in sink.q[0]  # b's BUY fills b's SALE
 
 
 class _RefusingEngine(_OracleEngine):

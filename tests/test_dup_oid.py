@@ -2,11 +2,13 @@
 
 The reference names a resting node S:node:<oid> without its uuid (ordernode.go:110-112,
 nodelink.go:119-122) and assumes oids unique per symbol (README.md:27); a second live node of the
-same name corrupts its FIFO.  Rule: an admitted ADD whose (symbol, oid) rests in the book at the
-start of its batch, or was carried by an earlier admitted ADD of the same batch, is not applied,
-counted (gome_stats.n_dup_oid) and listed (gome_dup_records).  The literal transliteration applies
-it in its consumer before DoOrder (oracle/literal.py GomeLiteral.consume), the C oracle in
-oracle_submit, the engine in k_adm / k_adm_flag / k_dup_flag before any path sees the batch."""
+same name corrupts its FIFO.  Rule: an admitted ADD whose (symbol, oid) names a live node when the
+ADD is applied is not applied, counted (gome_stats.n_dup_oid) and listed (gome_dup_records).  It
+depends on the queue order only, not on where batches start and end.  The literal
+transliteration applies it in a wrapper around its faithful consumer loop, before DoOrder
+(oracle/literal.py GomeLiteral.consume_boundary), the C oracle in oracle_submit; in the engine the
+admission kernels mark the ADDs whose key rests at batch start or repeats in the batch, their books
+go to the serial kernels, and those probe the cancel index as each marked ADD is applied."""
 import numpy as np
 import pytest
 
@@ -35,14 +37,23 @@ KATS = {
                           [_req(ADD, 7, "u2", p=0.3)]], [[], [], []]),
     # cancelled in an earlier batch, then reused
     "reuse_after_cancel": ([[_req(ADD, 7, "u1")], [_req(DEL, 7, "u1")], [_req(ADD, 7, "u2")]], [[], [], []]),
-    # filled within the batch, then reused in the same batch: still rejected (static rule)
+    # filled within the batch, then reused in the same batch: an ordinary ADD (the node is gone)
     "filled_then_reused_same_batch": ([[_req(ADD, 7, "u1", tx=1, p=0.5), _req(ADD, 8, "u9", p=0.5),
-                                        _req(ADD, 7, "u2", p=0.3)]], [[2]]),
+                                        _req(ADD, 7, "u2", p=0.3)]], [[]]),
+    # partly filled within the batch (still live), then reused: rejected
+    "partly_filled_then_reused_same_batch": ([[_req(ADD, 7, "u1", tx=1, p=0.5, v=2.0), _req(ADD, 8, "u9", p=0.5),
+                                               _req(ADD, 7, "u2", p=0.3)]], [[2]]),
+    # rested in the batch, re-added, then filled and re-added again: rejected, then applied
+    "rejected_then_applied_same_batch": ([[_req(ADD, 7, "u1", tx=1, p=0.5), _req(ADD, 7, "u2", p=0.2),
+                                           _req(ADD, 8, "u9", p=0.5), _req(ADD, 7, "u3", p=0.3)]], [[1]]),
     # an ADD that admission drops (its DEL came first) does not count as carrying the oid
     "dropped_add_does_not_count": ([[_req(DEL, 7, "u1"), _req(ADD, 7, "u1"), _req(ADD, 7, "u2")]], [[]]),
-    # resting at batch start, cancelled earlier in the batch: the re-ADD is still rejected
+    # resting at batch start, cancelled earlier in the batch: the re-ADD is an ordinary ADD
     "resting_cancelled_then_readded": ([[_req(ADD, 7, "u1")], [_req(DEL, 7, "u1"), _req(ADD, 7, "u2")]],
-                                       [[], [1]]),
+                                       [[], []]),
+    # resting at batch start, its cancel has the wrong price (Q3: no-op): the re-ADD is rejected
+    "resting_wrong_price_cancel_then_readded": ([[_req(ADD, 7, "u1")], [_req(DEL, 7, "u1", p=0.6),
+                                                                       _req(ADD, 7, "u2")]], [[], [1]]),
     # another symbol's oid 7 is a different node
     "other_symbol": ([[_req(ADD, 7, "u1", sym="a"), _req(ADD, 7, "u1", sym="b")]], [[]]),
 }
@@ -55,7 +66,7 @@ def _literal(batches):
     for b in batches:
         for a, r in b:
             (eng.grpc_do_order if a == ADD else eng.grpc_delete_order)(r)
-        eng.consume()
+        eng.consume_boundary()
         out += eng.take_results()
         dups.append(list(eng.dups))
     return out, dups
@@ -104,6 +115,35 @@ def _records_to_requests(b):
                                            symbol="s%d" % r["symbol_id"], transaction=int(r["side"]),
                                            price=int(r["price_fx"]) / 1e8, volume=int(r["volume_fx"]) / 1e8)))
     return out
+
+
+def _host_admitted(b):
+    """Admission resolved per record by the host (GOME_ORD_ADM_HOST): every ADD keeps its marker,
+    so no verdict depends on the batch (the Q4 batch model would)."""
+    b = b.copy()
+    b["flags"] = np.where(b["action"] == ADD, 3, 1).astype(b["flags"].dtype)
+    return b
+
+
+def test_dup_rule_does_not_depend_on_batching():
+    """the same message stream cut into batches of 4000, 997 and 1 publishes the same
+    MatchResults and rejects the same records (C oracle; the literal agrees in the test below)."""
+    whole = np.concatenate(_divergent_stream(n=8000, n_symbols=6, batch=4000, seed=29))
+    whole["oid_id"] = (1 + np.random.default_rng(1).integers(0, 200, len(whole))).astype(whole["oid_id"].dtype)
+    whole = _host_admitted(whole)
+    runs = []
+    for bs in (4000, 997, 1):
+        orc = Oracle(6)
+        ev, dups = [], []
+        for k in range(0, len(whole), bs):
+            e = orc.submit(whole[k:k + bs])
+            e["taker_seq"] += k
+            ev.append(e)
+            dups += [k + int(i) for i in orc.dup_records()]
+        runs.append((np.concatenate(ev), dups))
+    assert len(runs[0][1]) > 300
+    for ev, dups in runs[1:]:
+        assert np.array_equal(ev, runs[0][0]) and dups == runs[0][1]
 
 
 def test_divergent_stream_literal_vs_oracle_small():
@@ -160,8 +200,9 @@ def _assign_books(b):
 
 @pytest.mark.gpu
 def test_resting_oid_readded_on_flow_cold_and_legacy_books():
-    """Oids resting at batch start re-added under another uuid, in a hot (flow) book, a cold book
-    and two quirky books (legacy and cold kernels), mixed with fresh ADDs: rejected on every path."""
+    """Oids resting at batch start re-added under another uuid, in a hot book, a cold book and two
+    quirky books (legacy and cold kernels), mixed with fresh ADDs: the serial kernels reject each
+    one whose node is still live when it is applied, exactly as the oracle does."""
     from gome_amd.abi import Engine
     from tests.test_gpu_v4 import _cmp, _cmp_books
     rng = np.random.default_rng(5)
@@ -192,6 +233,9 @@ def test_resting_oid_readded_on_flow_cold_and_legacy_books():
         if i == 0:
             assert len(orc.dup_records()) > 1000
         fl = eng.debug_flow_books()
-        assert (fl["kind"] > 0).any() and (fl["kind"] == 0).any(), fl  # flow and legacy books
+        if i == 0:  # every book holds re-added oids: the serial kernels decide them
+            assert (fl["kind"] == 0).all(), fl
+        else:  # fresh oids only: the hot book is back on the flow path
+            assert (fl["kind"] > 0).any(), fl
         nxt = _assign_books(g.batch(40000))
     _cmp_books(eng, orc, range(4), "re-added oids")

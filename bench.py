@@ -232,6 +232,74 @@ def cpu_baseline(batches, n_symbols, budget_s, threads=1):
     return one, (done / wall, done, wall, used)
 
 
+def consumer_leg(workload, n_symbols, n_msgs, seed, batch=1 << 15, render_threads=8):
+    """The drop-in boundary's own rate: n_msgs doOrder messages (the OrderNode JSON
+    the gRPC side enqueues, main.go:39-52 / ordernode.go:9-36, admission markers set) of the same
+    workload through BatchingConsumer.process -- Go-Unmarshal decode, fixed-point conversion,
+    interning, admission, gome_submit_batch, drain, gome_render_events into MatchResult lines on the
+    sink (rabbitmq.go:116-125, engine.go:154-194) -- at one host thread; then gome_render_events
+    alone over the same events at 1 and render_threads threads."""
+    import ctypes as C
+    from concurrent.futures import ThreadPoolExecutor
+    from gome_amd.abi import Engine
+    from gome_amd.consumer import BatchingConsumer, MatchSink, Names, PrePool, _order_node_json
+    gen, _, _ = make_stream(workload, 0, 1, seed + 7)
+    rec = gen(n_msgs).copy()
+    msgs = [_order_node_json(dict(symbol="s%d" % r["symbol_id"], uuid=str(int(r["uuid_id"])),
+                                  oid=str(int(r["oid_id"])), transaction=int(r["side"])),
+                             int(r["action"]), float(r["price_fx"]), float(r["volume_fx"]), 8) for r in rec]
+    pre, sink, names = PrePool(), MatchSink(), Names()
+    for r in rec:
+        if r["action"] == wl.ADD:
+            pre.set("s%d" % r["symbol_id"], str(int(r["uuid_id"])), str(int(r["oid_id"])))
+    eng = Engine(max_symbols=n_symbols, max_batch=batch, max_nodes=2 * n_msgs + (1 << 20),
+                 max_levels=(1 << 22) + 2 * n_msgs)
+    cons = BatchingConsumer(eng, pre, sink, names, max_batch=batch)
+    evs, recs, bases = [], [], []
+    orig_render = cons.render
+
+    def keep(ev, rc, base):  # (the events of each batch, for the render-only pass)
+        evs.append(ev.copy())
+        recs.append(rc.copy())
+        bases.append(base)
+        return orig_render(ev, rc, base)
+    cons.render = keep
+    t = time.perf_counter()
+    lines = 0
+    for k in range(0, n_msgs, batch):
+        lines += cons.process(msgs[k:k + batch])
+    wall = time.perf_counter() - t
+    lib = cons.lib
+    N = names
+
+    def render(i):
+        ev, rc, base = evs[i], recs[i], bases[i]
+        cap = max(1 << 20, 1400 * len(ev))
+        buf = C.create_string_buffer(cap)
+        k = lib.gome_render_events(ev.ctypes.data, len(ev), rc.ctypes.data, len(rc), base, 8,
+                                   C.cast(N.table("sym"), C.c_void_p), len(N.rev["sym"]),
+                                   C.cast(N.table("uuid"), C.c_void_p), len(N.rev["uuid"]),
+                                   C.cast(N.table("oid"), C.c_void_p), len(N.rev["oid"]),
+                                   N.tx_array().ctypes.data, buf, cap)
+        assert k >= 0
+        return k
+    nev = sum(len(e) for e in evs)
+    out = {"messages": n_msgs, "batch": batch, "messages_per_s": round(n_msgs / wall, 1),
+           "matchresults_per_s": round(lines / wall, 1), "matchresults": lines, "threads": 1,
+           "path": "OrderNode JSON -> BatchingConsumer.process (decode, convert, intern, admit, "
+                   "gome_submit_batch, drain, gome_render_events) -> MatchResult lines on the sink",
+           "render_events_per_s": {}}
+    for th in (1, render_threads):
+        t = time.perf_counter()
+        with ThreadPoolExecutor(max_workers=th) as ex:
+            nbytes = sum(ex.map(render, range(len(evs))))
+        dt = time.perf_counter() - t
+        out["render_events_per_s"][str(th)] = round(nev / dt, 1)
+        out["render_MB_per_s_" + str(th)] = round(nbytes / dt / 1e6, 1)
+    eng.close()
+    return out
+
+
 def pctl(xs, q):
     s = sorted(xs)
     return s[min(len(s) - 1, max(0, int(np.ceil(q * len(s))) - 1))]
@@ -254,6 +322,15 @@ def main():
                     help="process-group backend (nccl = RCCL over xGMI; gloo: CPU collectives, for tests)")
     ap.add_argument("--same-device", action="store_true",
                     help="every rank on device 0 (rehearsing the N-rank path on a one-GPU box)")
+    ap.add_argument("--force-pg", action="store_true",
+                    help="initialise the process group and run the summary gather, the publisher and the "
+                         "digest check at N = 1 too (exercises the RCCL path on a one-GPU box)")
+    ap.add_argument("--inject-quirks", choices=("none", "heal", "stuck"), default="none",
+                    help="rewrite records of the hottest book in batch 1 into a wrong-side cancel (Q2) of a "
+                         "bid level and a zero-volume ADD (Q6) (workload.inject_quirks); warm-up should "
+                         "cover batches 0-2")
+    ap.add_argument("--consumer-msgs", type=int, default=1 << 17,
+                    help="JSON OrderNode messages of the consumer leg (0: off)")
     ap.add_argument("--pool-nodes", type=int, default=0, help="gome_config.max_nodes (0: sized from the run)")
     ap.add_argument("--pool-levels", type=int, default=0, help="gome_config.max_levels (0: sized from the run)")
     ap.add_argument("--step-log", default="", help="write each timed step's engine counters (JSONL)")
@@ -278,7 +355,12 @@ def main():
             sys.exit(2)
     dev = 0 if args.same_device else local
     torch.cuda.set_device(dev)
-    if world > 1:
+    use_pg = world > 1 or args.force_pg  # (the summary gather, publisher and digest check)
+    if use_pg:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29517")
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
         if args.backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
         else:
@@ -296,6 +378,7 @@ def main():
     per_rank = int(round(args.batch * world * share))
     note(f"{args.workload}: generating {warm + steps} batches of {per_rank} records")
     host_batches = [gen(per_rank).copy() for _ in range(warm + steps)]
+    injected = None
     dev_batches = [torch.from_numpy(b.view(np.uint8)).cuda() for b in host_batches]
     torch.cuda.synchronize()
 
@@ -314,10 +397,10 @@ def main():
     hot = hot_symbols(args.workload, rank, world)
     last_dg = [None]
 
-    def publish(st, i):
-        if world > 1:  # per-GPU trade/depth summary to the publisher (RCCL all_gather)
-            last_dg[0] = eng.top_of_book(hot)  # depth digests of this rank's hottest books
-            gather_summary(st, summary, gathered, rank, i, last_dg[0])
+    def publish(st, i, dg):
+        if use_pg:  # per-GPU trade/depth summary to the publisher (RCCL all_gather)
+            last_dg[0] = dg  # depth digests of this rank's hottest books after batch i
+            gather_summary(st, summary, gathered, rank, i, dg)
             if pub is not None:
                 pub.consume(gathered)
 
@@ -327,14 +410,15 @@ def main():
         seq[0] += per_rank
         eng.release_device_events()  # events stay in HBM (a device-side consumer's input)
         st = eng.stats()
-        publish(st, i)
+        publish(st, i, eng.top_of_book(hot) if use_pg else None)
         return st
 
-    # pipelined steps (the default): batch k+1 is enqueued before batch k is collected, so the
-    # host's enqueue of one batch hides under the device's work on the other; the events stay
-    # in HBM (a device-side consumer's input).  The publisher's depth digests need each batch's
-    # books right after it, so N > 1 keeps the synchronous steps.
-    pipelined = not args.sync and world == 1
+    # pipelined steps (the default, any N): batch k+1 is enqueued before batch k is collected, so
+    # the host's enqueue of one batch hides under the device's work on the other; the events stay
+    # in HBM (a device-side consumer's input).  The publisher's depth digests of batch k are read
+    # on the device behind batch k, before batch k+1 (gome_top_of_book_enqueue), and collected
+    # after it: they never stall the pipeline.
+    pipelined = not args.sync
 
     def run_steps(lo, hi, lat, sts, timed):
         tsub = {}
@@ -351,26 +435,47 @@ def main():
             elif rank == 0:
                 note(f"warmup step {k + 1}/{hi}")
 
+        def collect(k):
+            _, _, st = eng.collect_device()
+            eng.release_device_events()
+            publish(st, k, eng.top_of_book_collect() if use_pg else None)
+            done(k, st)
+
         for k in range(lo, hi):
             tsub[k] = time.perf_counter()
             if not pipelined:
                 done(k, step(k))
                 continue
+            if use_pg and k > lo:
+                eng.top_of_book_enqueue(hot)  # (batch k-1's books, before batch k touches them)
             eng.submit_device_async(dev_batches[k].data_ptr(), per_rank, seq_base=seq[0])
             seq[0] += per_rank
             if k > lo:
-                _, _, st = eng.collect_device()
-                eng.release_device_events()
-                done(k - 1, st)
+                collect(k - 1)
         if pipelined and hi > lo:
-            _, _, st = eng.collect_device()
-            eng.release_device_events()
-            done(hi - 1, st)
+            if use_pg:
+                eng.top_of_book_enqueue(hot)
+            collect(hi - 1)
 
     slog = None
-    run_steps(0, warm, None, None, False)
+    w0 = 0
+    if args.inject_quirks != "none":
+        # batch 0 synchronously, then batch 1's records of the hottest book rewritten from the
+        # engine's own snapshot of that book (workload.inject_quirks); warm-up covers batches 0-2
+        if warm < 3:
+            print("--inject-quirks needs --warmup >= 3", file=sys.stderr)
+            sys.exit(2)
+        step(0)
+        hs = int(hot[0])
+        injected = wl.inject_quirks(host_batches[1], hs, eng.levels(hs), lambda p: eng.fifo(hs, p),
+                                    args.inject_quirks)
+        dev_batches[1].copy_(torch.from_numpy(host_batches[1].view(np.uint8)))
+        torch.cuda.synchronize()
+        note(f"injected into batch 1: {injected['q2_cancels']} wrong-side cancels, one zero-volume ADD")
+        w0 = 1
+    run_steps(w0, warm, None, None, False)
     torch.cuda.synchronize()
-    if world > 1:
+    if use_pg:
         dist.barrier()
     if pub is not None:
         pub = SummaryPublisher(world)  # the timed steps only
@@ -379,12 +484,15 @@ def main():
     t0 = time.perf_counter()
     run_steps(warm, warm + steps, lat, sts, True)
     torch.cuda.synchronize()
-    if world > 1:
+    if use_pg:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if slog is not None:
         slog.close()
 
+    dev_lat = [float(s["ms_total"]) for s in sts]
+    if use_pg:  # (the slowest rank's device time per step)
+        dev_lat = combine_ranks(0.0, 0.0, 0.0, 0.0, dev_lat, cdev)[4]
     orders = sum(s["n_orders"] for s in sts)
     fills = sum(s["n_fills"] for s in sts)
     events = sum(s["n_events"] for s in sts)
@@ -409,7 +517,7 @@ def main():
         cands.pop("k_flow_plan_head")
     max_seg = max(s["max_segment"] for s in sts)
     digest_check = None
-    if world > 1:
+    if use_pg:
         g_orders, g_fills, g_events, elapsed, lat = combine_ranks(orders, fills, events, elapsed, lat, cdev)
         # every rank checks the digests it published last against its books' snapshots
         # (gome_snapshot_levels); the publisher gets the mismatch count
@@ -450,18 +558,18 @@ def main():
 
         run_pipe(0, e2e_warm, [])
         torch.cuda.synchronize()
-        if world > 1:
+        if use_pg:
             dist.barrier()
         elat = []
         done_ev[0] = 0
         t1 = time.perf_counter()
         run_pipe(e2e_warm, e2e_warm + e2e_steps, elat)
         torch.cuda.synchronize()
-        if world > 1:
+        if use_pg:
             dist.barrier()
         e_el = time.perf_counter() - t1
         e_orders, e_events = per_rank * e2e_steps, done_ev[0]
-        if world > 1:
+        if use_pg:
             e_orders, _, e_events, e_el, elat = combine_ranks(e_orders, 0.0, e_events, e_el, elat, cdev)
         e2e = {"value": round(e_orders / e_el, 1), "unit": "orders/s", "steps": e2e_steps,
                "ms_per_step": round(e_el / e2e_steps * 1e3, 3),
@@ -497,6 +605,11 @@ def main():
                      f"untimed replay of the same {warm + steps} batches with GOME_FLAG_PHASES")
     kname = max(cands, key=lambda k: cands[k][0])
     ms_dom, bdom, kdesc = cands[kname]
+
+    consumer = None
+    if rank == 0 and world == 1 and args.consumer_msgs > 0:
+        note(f"consumer leg ({args.consumer_msgs} JSON messages)")
+        consumer = consumer_leg(args.workload, n_symbols, args.consumer_msgs, args.seed)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -544,13 +657,18 @@ def main():
                        "parallelism": f"symbol-sharded x{world} (no data-path collective)"},
             "p50_batch_ms": round(pctl(lat, 0.5), 3),
             "p99_batch_ms": round(pctl(lat, 0.99), 3),
+            # per-batch device latency (the batch's first to last kernel on the device; with two
+            # batches in flight a batch starts when the one before it leaves the pipeline's stream)
+            "p50_device_batch_ms": round(pctl(dev_lat, 0.5), 3),
+            "p99_device_batch_ms": round(pctl(dev_lat, 0.99), 3),
             "fills_per_s": round(g_fills / elapsed, 1),
             "events_per_s": round(g_events / elapsed, 1),
             "cancels_per_batch": int(cancels / steps),
             "device_ms_per_batch": round(ms_total, 3),
             "host_enqueue_ms": round(sum(s["ms_host_enqueue"] for s in sts) / steps, 3),
             "steps_mode": ("pipelined: two batches in flight (gome_submit_batch_device_async + "
-                           "gome_collect_device); p50/p99 are submit-to-collect times") if pipelined
+                           "gome_collect_device); p50/p99_batch_ms are submit-to-collect times (two "
+                           "batches), p50/p99_device_batch_ms each batch's own device time") if pipelined
                           else "synchronous: one gome_submit_batch_device per step",
             "match_books_ms": round(ms_match, 3),
             "kernel_ms": {k: round(v[0], 3) for k, v in sorted(cands.items(), key=lambda kv: -kv[1][0])},
@@ -565,6 +683,7 @@ def main():
                          "kernel_ms": round(ms_dom, 3), "alg_bytes_per_launch": int(bdom),
                          "match_phase_alg_bytes": int(balg)},
             "e2e": e2e,
+            "consumer": consumer,
             "cpu_baseline": cpu,
         }
         if "k_flow_plan_head" in cands and cands["k_flow_plan_head"][0] > 0:
@@ -576,13 +695,17 @@ def main():
                                     "frac": round(out["value"] / bound, 4),
                                     "note": "orders per step / the hottest book's plan time: the batch "
                                             "cannot end before that one wavefront does"}
-        if pub is not None and world > 1:
+        if injected is not None:
+            out["config"]["injected"] = dict(injected, records=len(injected["records"]))
+        if consumer is not None:
+            consumer["vs_value"] = round(consumer["messages_per_s"] / out["value"], 6)
+        if pub is not None and use_pg:
             pub.check(int(g_orders), int(g_fills), int(g_events))
             out["publisher"] = pub.summary()
             out["publisher"]["digest_check"] = digest_check
             out["config"]["backend"] = args.backend + (" (all ranks on device 0)" if args.same_device else "")
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if use_pg:
         dist.destroy_process_group()
     eng.close()
 

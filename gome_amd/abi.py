@@ -118,6 +118,8 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.gome_dup_records.argtypes = [VP, P(C.c_uint32), C.c_size_t, P(C.c_size_t)]
     lib.gome_take_deferred.argtypes = [VP]
     lib.gome_top_of_book.argtypes = [VP, VP, C.c_size_t, VP]
+    lib.gome_top_of_book_enqueue.argtypes = [VP, VP, C.c_size_t]
+    lib.gome_top_of_book_collect.argtypes = [VP, VP, C.c_size_t, P(C.c_size_t)]
     lib.gome_snapshot_levels.argtypes = [VP, C.c_uint32, VP, C.c_size_t, P(C.c_size_t)]
     lib.gome_snapshot_fifo.argtypes = [VP, C.c_uint32, C.c_int64, VP, C.c_size_t, P(C.c_size_t)]
     lib.gome_load_books.argtypes = [VP, C.c_size_t, VP, VP, VP, VP, C.c_size_t]
@@ -143,6 +145,7 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
               "gome_fixed_from_double", "gome_fixed_from_scaled", "gome_submit_batch_async",
               "gome_collect", "gome_host_alloc", "gome_load_books", "gome_dup_records",
               "gome_take_deferred", "gome_top_of_book", "gome_submit_batch_device_async",
+              "gome_top_of_book_enqueue", "gome_top_of_book_collect",
               "gome_collect_device"):
         getattr(lib, f).restype = C.c_int32
     _lib = lib
@@ -359,6 +362,19 @@ class Engine:
         out = np.zeros(len(syms), TOB_DTYPE)
         self._check(self.lib.gome_top_of_book(self.h, syms.ctypes.data, len(syms), out.ctypes.data))
         return out
+
+    def top_of_book_enqueue(self, symbols):
+        """gome_top_of_book_enqueue: digests of the books as the last submitted batch leaves them,
+        read on the device behind the batches in flight (collect with top_of_book_collect)."""
+        syms = np.ascontiguousarray(symbols, dtype=np.uint32)
+        self._check(self.lib.gome_top_of_book_enqueue(self.h, syms.ctypes.data, len(syms)))
+        self._tob_n = len(syms)
+
+    def top_of_book_collect(self) -> np.ndarray:
+        n = C.c_size_t()
+        out = np.zeros(getattr(self, "_tob_n", 0), TOB_DTYPE)
+        self._check(self.lib.gome_top_of_book_collect(self.h, out.ctypes.data, len(out), C.byref(n)))
+        return out[:n.value]
 
     def take_deferred(self) -> tuple[int, str]:
         """(status, message) of the first in-flight batch failure a synchronous call collected."""

@@ -307,6 +307,13 @@ struct gome_engine {
   uint32_t* d_tob_syms = nullptr;  // gome_top_of_book's device buffers
   gome_tob* d_tob = nullptr;
   size_t tob_cap = 0;
+  // gome_top_of_book_enqueue: page-locked staging (symbols in, digests out), its completion event
+  uint32_t* h_tob_syms = nullptr;
+  gome_tob* h_tob = nullptr;
+  size_t h_tob_cap = 0, tob_pending = 0;
+  bool tob_queued = false;
+  hipEvent_t tob_done{};
+  gome_status tob_buffers(size_t n);
   size_t pending_pos = 0;
   size_t dev_events = 0, dev_events_pos = 0;  // events of the last device submit
   uint32_t dev_slot = 0;
@@ -359,8 +366,10 @@ struct gome_engine {
           if (ev) (void)hipEventDestroy(ev);
     }
     for (hipEvent_t ev : {fork, join, joinf, prep_h, prep_t, fork_adm, adm_done, seg_done, dp_fork, cnt_fork, cnt_done,
-                          dw_done, dl_done, tl_done})
+                          dw_done, dl_done, tl_done, tob_done})
       if (ev) (void)hipEventDestroy(ev);
+    if (h_tob_syms) (void)hipHostFree(h_tob_syms);
+    if (h_tob) (void)hipHostFree(h_tob);
     if (hot_stream) (void)hipStreamDestroy(hot_stream);
     if (flow_stream) (void)hipStreamDestroy(flow_stream);
     if (copy_stream) (void)hipStreamDestroy(copy_stream);
@@ -397,6 +406,13 @@ struct gome_engine {
   gome_status queue_events(uint32_t slot, size_t n, hipStream_t s);
 };
 
+#define HIPCHK_E(e, x)                                                               \
+  do {                                                                               \
+    hipError_t _e = (x);                                                             \
+    if (_e != hipSuccess)                                                            \
+      return (e)->fail(GOME_E_DEVICE, std::string(#x) + ": " + hipGetErrorString(_e)); \
+  } while (0)
+
 #define HIPCHK(x)                                                                    \
   do {                                                                               \
     hipError_t _e = (x);                                                             \
@@ -422,7 +438,7 @@ gome_status gome_engine::init(const gome_config& c) {
   HIPCHK(hipStreamCreateWithFlags(&flow_stream, hipStreamNonBlocking));
   HIPCHK(hipStreamCreateWithFlags(&copy_stream, hipStreamNonBlocking));
   for (hipEvent_t* ev : {&fork, &join, &joinf, &prep_h, &prep_t, &fork_adm, &adm_done, &seg_done,
-                         &dp_fork, &cnt_fork, &cnt_done, &dw_done, &dl_done, &tl_done})
+                         &dp_fork, &cnt_fork, &cnt_done, &dw_done, &dl_done, &tl_done, &tob_done})
     HIPCHK(hipEventCreateWithFlags(ev, hipEventDisableTiming));
   for (Slot& S : slots) {
     for (hipEvent_t* ev : {&S.ev0, &S.ev1, &S.evm0, &S.evm1, &S.evh0, &S.evh1, &S.evf0, &S.evf1, &S.evc0, &S.evc1})
@@ -1571,23 +1587,26 @@ gome_status gome_get_stats(const gome_engine* e, gome_stats* out) {
   return GOME_OK;
 }
 
+gome_status gome_engine::tob_buffers(size_t n) {
+  if (n <= tob_cap) return GOME_OK;  // (kept between calls: the publisher asks every batch)
+  if (d_tob_syms) release(d_tob_syms);
+  if (d_tob) release(d_tob);
+  d_tob_syms = nullptr;
+  d_tob = nullptr;
+  tob_cap = 0;
+  const size_t cap = std::max<size_t>(n, 64);
+  if (!alloc(&d_tob_syms, cap, "tob symbols") || !alloc(&d_tob, cap, "tob digests")) return GOME_E_CAPACITY;
+  tob_cap = cap;
+  return GOME_OK;
+}
+
 gome_status gome_top_of_book(gome_engine* e, const uint32_t* symbols, size_t n, gome_tob* out) {
   if (!e || (n && (!symbols || !out))) return GOME_E_INVAL;
   DevGuard dg(e->cfg.device);
   if (gome_status s = e->collect_all()) return s;
   if (n == 0) return GOME_OK;
   if (n > (1u << 20)) return e->fail(GOME_E_INVAL, "gome_top_of_book: more than 2^20 symbols");
-  if (n > e->tob_cap) {  // (kept between calls: the publisher asks every batch)
-    if (e->d_tob_syms) e->release(e->d_tob_syms);
-    if (e->d_tob) e->release(e->d_tob);
-    e->d_tob_syms = nullptr;
-    e->d_tob = nullptr;
-    e->tob_cap = 0;
-    const size_t cap = std::max<size_t>(n, 64);
-    if (!e->alloc(&e->d_tob_syms, cap, "tob symbols") || !e->alloc(&e->d_tob, cap, "tob digests"))
-      return GOME_E_CAPACITY;
-    e->tob_cap = cap;
-  }
+  if (gome_status s = e->tob_buffers(n)) return s;
   uint32_t* d_syms = e->d_tob_syms;
   gome_tob* d_out = e->d_tob;
   hipStream_t s = e->stream;
@@ -1601,6 +1620,54 @@ gome_status gome_top_of_book(gome_engine* e, const uint32_t* symbols, size_t n, 
       st = GOME_E_DEVICE;
   }
   return st == GOME_OK ? GOME_OK : e->fail(st, "gome_top_of_book: device error");
+}
+
+// The same digests without waiting: k_tob goes on the pipeline's stream behind the batches
+// already submitted (in flight or not), so it reads the books as the last of them leaves them
+// and before any later submit touches them; gome_top_of_book_collect waits for it alone.
+gome_status gome_top_of_book_enqueue(gome_engine* e, const uint32_t* symbols, size_t n) {
+  if (!e || (n && !symbols)) return GOME_E_INVAL;
+  DevGuard dg(e->cfg.device);
+  if (e->tob_queued) return e->fail(GOME_E_STATE, "gome_top_of_book_enqueue: collect the pending digests first");
+  if (n > (1u << 20)) return e->fail(GOME_E_INVAL, "gome_top_of_book_enqueue: more than 2^20 symbols");
+  if (e->poisoned) return e->fail(GOME_E_STATE, "engine poisoned by an earlier fatal error");
+  if (gome_status s = e->tob_buffers(n)) return s;
+  if (n > e->h_tob_cap) {
+    if (e->h_tob_syms) (void)hipHostFree(e->h_tob_syms);
+    if (e->h_tob) (void)hipHostFree(e->h_tob);
+    e->h_tob_syms = nullptr;
+    e->h_tob = nullptr;
+    e->h_tob_cap = 0;
+    const size_t cap = std::max<size_t>(n, 64);
+    HIPCHK_E(e, hipHostMalloc(reinterpret_cast<void**>(&e->h_tob_syms), cap * 4, hipHostMallocDefault));
+    HIPCHK_E(e, hipHostMalloc(reinterpret_cast<void**>(&e->h_tob), cap * sizeof(gome_tob), hipHostMallocDefault));
+    e->h_tob_cap = cap;
+  }
+  if (n) {
+    std::memcpy(e->h_tob_syms, symbols, n * 4);
+    hipStream_t s = e->stream;
+    HIPCHK_E(e, hipMemcpyAsync(e->d_tob_syms, e->h_tob_syms, n * 4, hipMemcpyHostToDevice, s));
+    k_tob<<<static_cast<uint32_t>((n + 63) / 64), 64, 0, s>>>(e->D, e->d_tob_syms, static_cast<uint32_t>(n), e->d_tob);
+    HIPCHK_E(e, hipGetLastError());
+    HIPCHK_E(e, hipMemcpyAsync(e->h_tob, e->d_tob, n * sizeof(gome_tob), hipMemcpyDeviceToHost, s));
+    HIPCHK_E(e, hipEventRecord(e->tob_done, s));
+  }
+  e->tob_pending = n;
+  e->tob_queued = true;
+  return GOME_OK;
+}
+
+gome_status gome_top_of_book_collect(gome_engine* e, gome_tob* out, size_t cap, size_t* n_out) {
+  if (!e || !n_out || (cap && !out)) return GOME_E_INVAL;
+  DevGuard dg(e->cfg.device);
+  if (!e->tob_queued) return e->fail(GOME_E_NOTFOUND, "gome_top_of_book_collect: nothing enqueued");
+  const size_t n = e->tob_pending;
+  if (n) HIPCHK_E(e, hipEventSynchronize(e->tob_done));
+  std::memcpy(out, e->h_tob, std::min(cap, n) * sizeof(gome_tob));
+  *n_out = n;
+  e->tob_queued = false;
+  e->tob_pending = 0;
+  return GOME_OK;
 }
 
 gome_status gome_dup_records(const gome_engine* e, uint32_t* out, size_t cap, size_t* n_out) {

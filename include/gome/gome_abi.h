@@ -368,6 +368,14 @@ typedef struct gome_tob {
   uint32_t flags, pad;
 } gome_tob;
 gome_status gome_top_of_book(gome_engine* e, const uint32_t* symbols, size_t n, gome_tob* out);
+/* The same digests without collecting the batches in flight (ABI >= 8): enqueued on the pipeline's
+ * stream behind every batch submitted so far, so they describe the books as the last submitted
+ * batch leaves them (a later submit waits for them).  One request at a time; symbols are copied.
+ * gome_top_of_book_collect waits for that request alone and copies min(cap, n) digests
+ * (*n_out = n); GOME_E_NOTFOUND when nothing is enqueued.  With two batches in flight, enqueue
+ * before submitting batch k+1 and collect after collecting batch k: the digests of batch k. */
+gome_status gome_top_of_book_enqueue(gome_engine* e, const uint32_t* symbols, size_t n);
+gome_status gome_top_of_book_collect(gome_engine* e, gome_tob* out, size_t cap, size_t* n_out);
 
 /* ---- book state load (restart from Redis) ------------------- */
 /* The reference restarts from whatever its Redis holds (nodepool.go:14-115,

@@ -43,3 +43,36 @@ def test_bench_two_ranks_same_device(workload):
     assert pub["digest_check"] == {"checked": 16, "mismatches": 0}
     assert len(pub["top_of_book"]) == 2
     assert out["e2e"]["value"] > 0
+
+
+def _bench_json(args, nproc=1, timeout=300):
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="2")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc),
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "bench.py")] + args
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=timeout)
+    assert r.returncode == 0, r.stderr[-4000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    return json.loads(lines[0])
+
+
+@pytest.mark.gpu
+def test_bench_rccl_world1_pipelined_matches_sync():
+    """bench.py's collective path on RCCL (backend nccl, device tensors) at world
+    1 under torch.distributed.run: the per-step summary all_gather, the publisher and the digest
+    check, with pipelined steps whose digests are read on the device behind each batch
+    (gome_top_of_book_enqueue); the same run with synchronous steps publishes the same totals."""
+    base = ["--gpus", "1", "--force-pg", "--backend", "nccl", "--workload", "config3", "--steps", "4",
+            "--warmup", "2", "--batch", str(1 << 18), "--e2e-steps", "0", "--no-cpu-baseline",
+            "--no-phase-pass", "--consumer-msgs", "0"]
+    pipe = _bench_json(base)
+    sync = _bench_json(base + ["--sync"])
+    for out in (pipe, sync):
+        pub = out["publisher"]
+        assert out["config"]["backend"] == "nccl"
+        assert pub["errors"] == [] and pub["steps"] == 4
+        assert pub["digest_check"] == {"checked": 8, "mismatches": 0}
+    assert pipe["steps_mode"].startswith("pipelined") and sync["steps_mode"].startswith("synchronous")
+    for k in ("orders", "fills", "events", "cancels"):
+        assert pipe["publisher"][k] == sync["publisher"][k]
+    assert pipe["publisher"]["top_of_book"] == sync["publisher"]["top_of_book"]

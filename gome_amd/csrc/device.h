@@ -13,7 +13,10 @@
 namespace gome {
 
 constexpr int WAVE = 64;
-constexpr int CH = 32;                 // FIFO slots per chunk
+#ifndef GOME_CH
+#define GOME_CH 32
+#endif
+constexpr int CH = GOME_CH;            // FIFO slots per chunk
 constexpr uint32_t NIL = 0xFFFFFFFFu;
 constexpr uint8_t M_BUY = 1, M_SALE = 2;  // side-set membership bits
 constexpr unsigned long long KEY_EMPTY = 0ull, KEY_TOMB = ~0ull;
@@ -106,7 +109,7 @@ struct Status {
   uint32_t nhot;       // segments handled by k_match_hot (first nhot of seg_order)
   uint32_t lvl_used;   // level slots ever carved from the pool (lvl_bump at batch end)
   uint32_t nquirk;     // books the cold / resume waves finished with BOOK_QUIRK (Dev::quirk)
-  uint32_t pad_q;
+  uint32_t ch_used;    // FIFO chunks ever carved from the pool (ch_bump at batch end)
   // ---- everything below persists across batches (the per-batch reset stops here)
   int32_t free_top;
   uint32_t freed_top;

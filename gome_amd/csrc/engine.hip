@@ -127,7 +127,10 @@ __global__ __launch_bounds__(256) void k_lvl_recycle(Dev D) {
   if (threadIdx.x == 0) {
     D.st->lvl_free_top[c] = top + static_cast<int>(nf);
     D.st->lvl_freed_top[c] = 0;
-    if (c == 0) D.st->lvl_used = min(*D.lvl_bump, D.lvl_cap_total);
+    if (c == 0) {
+      D.st->lvl_used = min(*D.lvl_bump, D.lvl_cap_total);
+      D.st->ch_used = min(*D.ch_bump, D.ch_cap);
+    }
   }
 }
 
@@ -1139,6 +1142,9 @@ gome_status gome_engine::finish(uint32_t sl, uint32_t n) {
   last_maxseg = st.ctr[C_MAXSEG];
   last_n = n;
   stats.chains_wanted = (want_deep ? FL_CH_DEEP : 0u) | (want_canc ? FL_CH_CANCEL : 0u);
+  // FIFO chunks holding nodes (carved from the pool and not on the free stack), with headers
+  stats.chunk_bytes = static_cast<uint64_t>(st.ch_used - std::min<uint32_t>(st.ch_used, static_cast<uint32_t>(std::max(st.free_top, 0)))) *
+                      (CH * sizeof(Node) + sizeof(ChunkHdr));
   stats.n_quirk_checked = st.ctr[C_QUIRK_CHECKED];
   stats.n_requalified = st.ctr[C_REQUAL];
   if (const uint64_t nd = std::min<uint64_t>(st.ctr[C_DUP], n)) {

@@ -239,6 +239,9 @@ typedef struct gome_stats {
                                                  kernels applied this batch (ABI >= 8)    */
   uint64_t n_requalified;                     /* ... of which healed: back on the flow path
                                                  from the next batch on (ABI >= 8)        */
+  uint64_t chunk_bytes;                       /* HBM held by FIFO chunks in use (node slots plus
+                                                 chunk headers) after the batch (ABI >= 8):
+                                                 / n_resting = bytes per resting order     */
 } gome_stats;
 
 typedef struct gome_engine gome_engine;

@@ -300,6 +300,38 @@ def consumer_leg(workload, n_symbols, n_msgs, seed, batch=1 << 15, render_thread
     return out
 
 
+def pcie_peak(nbytes=256 << 20, reps=3):
+    """Measured PCIe copy rates of this GPU (page-locked host memory, one direction at a time
+    and both at once on two streams), GB/s: the bound the e2e leg is compared with."""
+    import torch
+    h = torch.empty(nbytes, dtype=torch.uint8).pin_memory()
+    h2 = torch.empty(nbytes, dtype=torch.uint8).pin_memory()
+    d = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    d2 = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+
+    def timed(fn):
+        best = 1e9
+        for _ in range(reps):
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+            fn()
+            torch.cuda.synchronize()
+            best = min(best, time.perf_counter() - t)
+        return best
+
+    def both():
+        with torch.cuda.stream(s1):
+            d.copy_(h, non_blocking=True)
+        with torch.cuda.stream(s2):
+            h2.copy_(d2, non_blocking=True)
+    th = timed(lambda: d.copy_(h, non_blocking=True))
+    td = timed(lambda: h2.copy_(d2, non_blocking=True))
+    tb = timed(both)
+    return {"h2d_GBps": round(nbytes / th / 1e9, 2), "d2h_GBps": round(nbytes / td / 1e9, 2),
+            "duplex_GBps_each": round(nbytes / tb / 1e9, 2)}
+
+
 def pctl(xs, q):
     s = sorted(xs)
     return s[min(len(s) - 1, max(0, int(np.ceil(q * len(s))) - 1))]
@@ -571,7 +603,15 @@ def main():
         e_orders, e_events = per_rank * e2e_steps, done_ev[0]
         if use_pg:
             e_orders, _, e_events, e_el, elat = combine_ranks(e_orders, 0.0, e_events, e_el, elat, cdev)
+        pk = pcie_peak() if rank == 0 else None
+        in_b, out_b = 32 * per_rank, 64 * e_events / e2e_steps / max(world, 1)
         e2e = {"value": round(e_orders / e_el, 1), "unit": "orders/s", "steps": e2e_steps,
+               "pcie_peak": pk,
+               # the copies' lower bound per step on this rank: H2D and D2H overlapped (duplex rate)
+               # or serialised on one copy stream (one direction at a time)
+               "pcie_bound_ms": None if pk is None else {
+                   "overlapped": round(max(in_b, out_b) / (pk["duplex_GBps_each"] * 1e9) * 1e3, 3),
+                   "serial": round((in_b / (pk["h2d_GBps"] * 1e9) + out_b / (pk["d2h_GBps"] * 1e9)) * 1e3, 3)},
                "ms_per_step": round(e_el / e2e_steps * 1e3, 3),
                "p50_batch_ms": round(pctl(elat, 0.5), 3), "p99_batch_ms": round(pctl(elat, 0.99), 3),
                "events_per_s": round(e_events / e_el, 1),

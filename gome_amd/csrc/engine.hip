@@ -259,6 +259,10 @@ struct gome_engine {
   hipStream_t hot_stream = nullptr;   // tail / near-head flow books, legacy hot kernel
   hipStream_t flow_stream = nullptr;  // the hottest book's plan (critical path)
   hipStream_t copy_stream = nullptr;  // H2D of records, D2H of events (pipelined path)
+  // D2H of collected events on a stream of their own (GOME_D2H_STREAM=1): beside the next
+  // batch's H2D instead of behind it (PCIe is full duplex), if HIP gives it its own hardware
+  // queue (GPU_MAX_HW_QUEUES; with 4, a fifth stream shares one)
+  hipStream_t d2h_stream = nullptr;
   hipEvent_t fork{}, join{}, joinf{}, prep_h{}, prep_t{}, fork_adm{}, adm_done{}, seg_done{};
   hipEvent_t dp_fork{}, cnt_fork{}, cnt_done{}, dw_done{}, dl_done{}, tl_done{};  // the hottest book's deep chain, k_flow_count beside its writes
   Slot slots[GOME_MAX_INFLIGHT];
@@ -376,6 +380,7 @@ struct gome_engine {
     if (hot_stream) (void)hipStreamDestroy(hot_stream);
     if (flow_stream) (void)hipStreamDestroy(flow_stream);
     if (copy_stream) (void)hipStreamDestroy(copy_stream);
+    if (d2h_stream) (void)hipStreamDestroy(d2h_stream);
     if (stream) (void)hipStreamDestroy(stream);
   }
 
@@ -440,6 +445,8 @@ gome_status gome_engine::init(const gome_config& c) {
   HIPCHK(hipStreamCreateWithFlags(&hot_stream, hipStreamNonBlocking));
   HIPCHK(hipStreamCreateWithFlags(&flow_stream, hipStreamNonBlocking));
   HIPCHK(hipStreamCreateWithFlags(&copy_stream, hipStreamNonBlocking));
+  if (const char* g = std::getenv("GOME_D2H_STREAM"); g && std::atoi(g) != 0)
+    HIPCHK(hipStreamCreateWithFlags(&d2h_stream, hipStreamNonBlocking));
   for (hipEvent_t* ev : {&fork, &join, &joinf, &prep_h, &prep_t, &fork_adm, &adm_done, &seg_done,
                          &dp_fork, &cnt_fork, &cnt_done, &dw_done, &dl_done, &tl_done, &tob_done})
     HIPCHK(hipEventCreateWithFlags(ev, hipEventDisableTiming));
@@ -1248,8 +1255,9 @@ gome_status gome_engine::collect(const gome_event** evs, size_t* nev) {
     S.h_cap = cap;
   }
   if (n) {
-    HIPCHK(hipMemcpyAsync(S.h_events, S.d_events, n * sizeof(gome_event), hipMemcpyDeviceToHost, copy_stream));
-    HIPCHK(hipStreamSynchronize(copy_stream));
+    hipStream_t cs = d2h_stream ? d2h_stream : copy_stream;
+    HIPCHK(hipMemcpyAsync(S.h_events, S.d_events, n * sizeof(gome_event), hipMemcpyDeviceToHost, cs));
+    HIPCHK(hipStreamSynchronize(cs));
   }
   *evs = S.h_events;
   *nev = n;

@@ -64,17 +64,17 @@ WORKLOADS = {
 
 def algorithmic_bytes(st: dict) -> int:
     """Bytes match_books must move per launch:
-    32 B per input record read, 64 B per event written, 24 B node write + 16 B index
+    32 B per input record read, 48 B per event written, 24 B node write + 16 B index
     entry per resting order, 24 B node read per maker filled, 40 B (index probe + node)
     per cancel hit.  Level aggregates are not counted."""
-    return (32 * st["n_orders"] + 64 * st["n_events"] + 40 * st["n_rests"]
+    return (32 * st["n_orders"] + 48 * st["n_events"] + 40 * st["n_rests"]
             + 24 * st["n_fills"] + 40 * st["n_cancels"])
 
 
 def hot_algorithmic_bytes(st: dict) -> int:
     """The same per-unit figures restricted to the work done inside k_match_hot / the flow path."""
     ev = st["n_hot_fills"] + st["n_hot_cancels"]
-    return (32 * st["n_hot_orders"] + 64 * ev + 40 * st["n_hot_rests"]
+    return (32 * st["n_hot_orders"] + 48 * ev + 40 * st["n_hot_rests"]
             + 24 * st["n_hot_fills"] + 40 * st["n_hot_cancels"])
 
 
@@ -84,7 +84,7 @@ def cold_algorithmic_bytes(st: dict) -> int:
     f = st["n_fills"] - st["n_hot_fills"]
     c = st["n_cancels"] - st["n_hot_cancels"]
     r = st["n_rests"] - st["n_hot_rests"]
-    return 32 * o + 64 * (f + c) + 40 * r + 24 * f + 40 * c
+    return 32 * o + 48 * (f + c) + 40 * r + 24 * f + 40 * c
 
 
 def plan_algorithmic_bytes(st: dict) -> int:
@@ -106,7 +106,7 @@ def phase_candidates(st: dict) -> dict:
     tr = st["n_rests"] * to // max(n, 1)
     return {
         "k_flow_plan_tail": (ms["tail_plan"], 8 * to + 16 * tt, "serial plans of the tail's flow books"),
-        "k_flow_write_events": (ms["tail_write"], 64 * tf + 36 * tt + 4 * to + 32 * tt + 40 * tr,
+        "k_flow_write_events": (ms["tail_write"], 48 * tf + 36 * tt + 4 * to + 32 * tt + 40 * tr,
                                 "tail: FIFO appends and level arrays beside the events (binary searches) "
                                 "into the arena"),
         "k_flow_level": (ms["tail_level"], 64 * tt + 24 * tf, "tail: per-level reconstruction"),
@@ -115,7 +115,7 @@ def phase_candidates(st: dict) -> dict:
         "k_radix_scatter": (ms["sort"], 68 * n, "radix sort by symbol + segments"),
         "k_adm": (ms["admission"], 48 * n, "admission (Q4) and duplicate oids (Q7)"),
         "k_prep": (ms["records"], 68 * n, "symbol-sorted records"),
-        "k_publish": (ms["publish"], 128 * st["n_events"] + 8 * n,
+        "k_publish": (ms["publish"], 96 * st["n_events"] + 8 * n,
                       "publish-order scan, arena event scatter and the hottest book's events"),
     }
 
@@ -604,7 +604,7 @@ def main():
         if use_pg:
             e_orders, _, e_events, e_el, elat = combine_ranks(e_orders, 0.0, e_events, e_el, elat, cdev)
         pk = pcie_peak() if rank == 0 else None
-        in_b, out_b = 32 * per_rank, 64 * e_events / e2e_steps / max(world, 1)
+        in_b, out_b = 32 * per_rank, 48 * e_events / e2e_steps / max(world, 1)
         e2e = {"value": round(e_orders / e_el, 1), "unit": "orders/s", "steps": e2e_steps,
                "pcie_peak": pk,
                # the copies' lower bound per step on this rank: H2D and D2H overlapped (duplex rate)
@@ -615,7 +615,7 @@ def main():
                "ms_per_step": round(e_el / e2e_steps * 1e3, 3),
                "p50_batch_ms": round(pctl(elat, 0.5), 3), "p99_batch_ms": round(pctl(elat, 0.99), 3),
                "events_per_s": round(e_events / e_el, 1),
-               "pcie_bytes_per_step": int(32 * per_rank * world + 64 * e_events / e2e_steps),
+               "pcie_bytes_per_step": int(32 * per_rank * world + 48 * e_events / e2e_steps),
                "path": "host records -> gome_submit_batch_async (H2D on a copy stream) -> device "
                        "pipeline -> gome_collect (events D2H into page-locked memory); batch k+1's "
                        "H2D and batch k-1's D2H overlap batch k"}

@@ -124,7 +124,7 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.gome_snapshot_fifo.argtypes = [VP, C.c_uint32, C.c_int64, VP, C.c_size_t, P(C.c_size_t)]
     lib.gome_load_books.argtypes = [VP, C.c_size_t, VP, VP, VP, VP, C.c_size_t]
     lib.gome_fixed_from_double.argtypes = [C.c_double, C.c_uint32, P(C.c_int64)]
-    lib.gome_render_match_result.argtypes = [VP, VP, C.c_uint32] + [C.c_char_p] * 6 + [
+    lib.gome_render_match_result.argtypes = [VP, VP, C.c_int64, C.c_uint32] + [C.c_char_p] * 6 + [
         VP, C.c_char_p, C.c_size_t]
     lib.gome_render_match_result.restype = C.c_int64
     lib.gome_render_link_node.argtypes = [C.c_char_p, C.c_int64, C.c_int32, C.c_int64, C.c_uint32] + [
@@ -188,9 +188,10 @@ def tx_table_array(table) -> np.ndarray | None:
     return a
 
 
-def render_match_result(ev: np.void, taker: np.void, symbol: str, taker_uuid: str, taker_oid: str,
-                        maker_uuid: str | None, maker_oid: str | None,
+def render_match_result(ev: np.void, taker: np.void, taker_remaining: int, symbol: str, taker_uuid: str,
+                        taker_oid: str, maker_uuid: str | None, maker_oid: str | None,
                         maker_next_oid: str | None, accuracy: int = 8, tx_table=None) -> str:
+    """One MatchResult line; taker_remaining = Node.Volume (workload.taker_remaining)."""
     lib = load_library()
     e = np.array([ev], dtype=EVENT_DTYPE)
     t = np.array([taker], dtype=ORDER_DTYPE)
@@ -199,7 +200,7 @@ def render_match_result(ev: np.void, taker: np.void, symbol: str, taker_uuid: st
     size = 8192
     while True:  # a short buffer returns -(bytes needed)
         buf = C.create_string_buffer(size)
-        n = lib.gome_render_match_result(e.ctypes.data, t.ctypes.data, accuracy, symbol.encode(),
+        n = lib.gome_render_match_result(e.ctypes.data, t.ctypes.data, int(taker_remaining), accuracy, symbol.encode(),
                                          taker_uuid.encode(), taker_oid.encode(), enc(maker_uuid),
                                          enc(maker_oid), enc(maker_next_oid),
                                          None if tt is None else tt.ctypes.data, buf, len(buf))

@@ -47,30 +47,32 @@ using namespace gome;
 
 // ============================================================== event compaction
 // Arena events -> publish positions; the sequence number is seq_base + the batch index
-// (gome_event.taker_seq / seq_hi, ABI >= 4).
-// Four lanes per 64-B event, 16 B each: a wave reads 1 KiB of the arena per load instruction and
-// writes each event as one whole line (a lane per event read and wrote 64 separate 16-B pieces per
-// instruction).  Quarter 2 holds taker_seq and fill_idx, quarter 3 seq_hi.
+// (gome_event.taker_seq: its low 32 bits).  Three lanes per 48-B event, 16 B each (a wave moves 21
+// events: 1008 B of the arena per load instruction, each event written as whole 16-B pieces); part
+// 1 holds taker_seq (.z) and fill_idx (.w).
 __device__ __forceinline__ void ev_scatter(const gome_event* arena, uint32_t cap, const Status* st,
                                            const uint32_t* ev_off, gome_event* out, unsigned long long seq_base,
                                            uint32_t bid, uint32_t nblk) {
   const uint32_t used = min(st->ev_bump, cap);
-  const uint32_t qt = threadIdx.x & 3u;
-  const uint4* src = reinterpret_cast<const uint4*>(arena);
+  const uint32_t lane = lane_id(), part = lane % 3u, src = lane - part + 1u;
+  const uint32_t waves = (nblk * blockDim.x) >> 6;
+  const uint4* ain = reinterpret_cast<const uint4*>(arena);
   uint4* dst = reinterpret_cast<uint4*>(out);
-  for (uint32_t j = (bid * blockDim.x + threadIdx.x) >> 2; j < used; j += (nblk * blockDim.x) >> 2) {
-    uint4 v = src[4ull * j + qt];
-    const uint32_t idx = __shfl(v.x, static_cast<int>((threadIdx.x & ~3u) | 2u) & 63);   // taker_seq
-    const uint32_t fi = __shfl(v.y, static_cast<int>((threadIdx.x & ~3u) | 2u) & 63);    // fill_idx
-    if (idx == NIL) continue;
-    const unsigned long long sq = seq_base + idx;
-    if (qt == 2) v.x = static_cast<uint32_t>(sq);
-    if (qt == 3) v.w = static_cast<uint32_t>(sq >> 32);
-    dst[4ull * (ev_off[idx] + fi) + qt] = v;
+  for (uint32_t w = (bid * blockDim.x + threadIdx.x) >> 6;; w += waves) {
+    const uint32_t j0 = w * 21u;
+    if (j0 >= used) break;  // (wave-uniform)
+    const uint32_t j = j0 + lane / 3u;
+    const bool ok = lane < 63u && j < used;
+    uint4 v = ok ? ain[3ull * j + part] : make_uint4(0u, 0u, NIL, 0u);
+    const uint32_t idx = __shfl(v.z, static_cast<int>(min(src, 63u)));  // taker_seq
+    const uint32_t fi = __shfl(v.w, static_cast<int>(min(src, 63u)));   // fill_idx
+    if (!ok || idx == NIL) continue;
+    if (part == 1) v.z = static_cast<uint32_t>(seq_base + idx);
+    dst[3ull * (ev_off[idx] + fi) + part] = v;
   }
 }
-static_assert(offsetof(gome_event, taker_seq) == 32 && offsetof(gome_event, fill_idx) == 36 &&
-              offsetof(gome_event, seq_hi) == 60 && sizeof(gome_event) == 64, "ev_scatter's quarters");
+static_assert(offsetof(gome_event, taker_seq) == 24 && offsetof(gome_event, fill_idx) == 28 &&
+              sizeof(gome_event) == 48, "ev_scatter's parts");
 
 // After the publish-order scan, in one launch (no hop to a second stream and back): blocks
 // [0, nscat) place the arena's events, the rest write the hottest book's events (fl_events_hot).

@@ -197,7 +197,7 @@ extern "C" gome_status gome_fixed_from_scaled(double v, int64_t* out) {
 }
 
 extern "C" int64_t gome_render_match_result(const gome_event* ev, const gome_order* taker,
-                                            uint32_t accuracy, const char* symbol,
+                                            int64_t taker_remaining_fx, uint32_t accuracy, const char* symbol,
                                             const char* taker_uuid, const char* taker_oid,
                                             const char* maker_uuid, const char* maker_oid,
                                             const char* maker_next_oid, const int32_t* tx_table,
@@ -212,11 +212,19 @@ extern "C" int64_t gome_render_events(const gome_event* ev, size_t n, const gome
   size_t used = 0;
   bool fits = buf != nullptr;
   char none[1];
+  size_t cur = SIZE_MAX;  // the taker whose fills are being rendered, and its remaining volume
+  int64_t rem = 0;
   for (size_t i = 0; i < n; ++i) {
     const gome_event& e = ev[i];
-    const uint64_t seq = (static_cast<uint64_t>(e.seq_hi) << 32) | e.taker_seq;
-    if (seq < seq_base || seq - seq_base >= batch_n) return INT64_MIN;
-    const gome_order& t = batch[seq - seq_base];
+    // (taker_seq: the low 32 bits of seq_base + batch index)
+    const size_t bi = static_cast<uint32_t>(e.taker_seq - static_cast<uint32_t>(seq_base));
+    if (bi >= batch_n) return INT64_MIN;
+    const gome_order& t = batch[bi];
+    if (bi != cur) {  // Node.Volume: the taker's volume minus its fills so far (engine.go:147,164,184)
+      cur = bi;
+      rem = t.volume_fx;
+    }
+    if (e.kind == GOME_EV_FILL) rem -= e.match_volume_fx;
     if (t.symbol_id >= n_sym || t.uuid_id >= n_uuid || t.oid_id >= n_oid) return INT64_MIN;
     const bool fill = e.kind == GOME_EV_FILL;
     if (fill && (e.maker_uuid_id >= n_uuid || e.maker_oid_id >= n_oid ||
@@ -226,7 +234,7 @@ extern "C" int64_t gome_render_events(const gome_event* ev, size_t n, const gome
     // NUL), else a sizing pass (cap 0) that only counts
     const size_t room = fits && cap > used ? cap - used : 0;
     int64_t k = gome_render_match_result(
-        &e, &t, accuracy, sym_names[t.symbol_id], uuid_names[t.uuid_id], oid_names[t.oid_id],
+        &e, &t, rem, accuracy, sym_names[t.symbol_id], uuid_names[t.uuid_id], oid_names[t.oid_id],
         fill ? uuid_names[e.maker_uuid_id] : nullptr, fill ? oid_names[e.maker_oid_id] : nullptr,
         (fill && !e.maker_is_last) ? oid_names[e.maker_next_oid_id] : nullptr, tx_table,
         room ? buf + used : none, room);
@@ -245,7 +253,7 @@ extern "C" int64_t gome_render_events(const gome_event* ev, size_t n, const gome
 }
 
 extern "C" int64_t gome_render_match_result(const gome_event* ev, const gome_order* taker,
-                                            uint32_t accuracy, const char* symbol,
+                                            int64_t taker_remaining_fx, uint32_t accuracy, const char* symbol,
                                             const char* taker_uuid, const char* taker_oid,
                                             const char* maker_uuid, const char* maker_oid,
                                             const char* maker_next_oid, const int32_t* tx_table,
@@ -268,7 +276,7 @@ extern "C" int64_t gome_render_match_result(const gome_event* ev, const gome_ord
     if (!maker_uuid || !maker_oid) return INT64_MIN;
     // Node: the taker after this fill (engine.go:154,171,190).
     NodeView t{taker->action, taker_uuid, taker_oid, symbol, taker_tx, taker->price_fx,
-               ev->taker_volume_fx, accuracy, false, false, nullptr};
+               taker_remaining_fx, accuracy, false, false, nullptr};
     render_node(o, t);
     // MatchNode: the FIFO head as stored (IsFirst, PrevNode "", Action ADD).
     NodeView m{GOME_ADD, maker_uuid, maker_oid, symbol, maker_tx, ev->price_fx,

@@ -439,10 +439,8 @@ __device__ __forceinline__ int64_t match_level(WaveCtx& W, uint32_t k, int64_t T
       e.price_fx = lv.price;
       e.match_volume_fx = f;
       e.maker_volume_fx = pop ? r : r - f;
-      e.taker_volume_fx = tafter;
       e.taker_seq = seq;
       e.fill_idx = fidx + rank;
-      e.symbol_id = W.sym;
       e.maker_oid_id = o;
       e.maker_uuid_id = u;
       e.maker_next_oid_id = is_last ? 0u : nx_oid;
@@ -450,7 +448,6 @@ __device__ __forceinline__ int64_t match_level(WaveCtx& W, uint32_t k, int64_t T
       e.maker_side = static_cast<uint8_t>(t);
       e.maker_is_last = is_last ? 1 : 0;
       e.pad0 = 0;
-      e.seq_hi = 0;
       W.B.arena[W.ev_base + W.ev_used + rank] = e;
     }
     W.ev_used += narr;
@@ -638,10 +635,8 @@ __device__ __forceinline__ uint32_t do_cancel(WaveCtx& W, int64_t p, uint32_t oi
     e.price_fx = p;
     e.match_volume_fx = 0;
     e.maker_volume_fx = r;
-    e.taker_volume_fx = r;
     e.taker_seq = seq;
     e.fill_idx = 0;
-    e.symbol_id = W.sym;
     e.maker_oid_id = oid;
     e.maker_uuid_id = uuid;
     e.maker_next_oid_id = 0;
@@ -649,7 +644,6 @@ __device__ __forceinline__ uint32_t do_cancel(WaveCtx& W, int64_t p, uint32_t oi
     e.maker_side = static_cast<uint8_t>(side);
     e.maker_is_last = 1;
     e.pad0 = 0;
-    e.seq_hi = 0;
     W.B.arena[W.ev_base + W.ev_used] = e;
   }
   W.ev_used += 1;

@@ -2005,10 +2005,8 @@ __device__ __forceinline__ void fl_emit_wave(const BatchArgs& B, const FlowArgs&
     ev.price_fx = price;
     ev.match_volume_fx = qty;
     ev.maker_volume_fx = full ? pre : pre - qty;
-    ev.taker_volume_fx = tbc - hi_;
     ev.taker_seq = static_cast<uint32_t>(sq);
     ev.fill_idx = fbm + m;
-    ev.symbol_id = sym;
     ev.maker_oid_id = oid;
     ev.maker_uuid_id = uuid;
     ev.maker_next_oid_id = nx;
@@ -2016,7 +2014,6 @@ __device__ __forceinline__ void fl_emit_wave(const BatchArgs& B, const FlowArgs&
     ev.maker_side = static_cast<uint8_t>(tx);
     ev.maker_is_last = static_cast<uint8_t>(lst);
     ev.pad0 = 0;
-    ev.seq_hi = static_cast<uint32_t>(sq >> 32);
     dst[dbase + m] = ev;
   }
 }

@@ -1380,10 +1380,8 @@ __global__ __launch_bounds__(256) void k_fc_events(Dev D, BatchArgs B, FlowArgs 
       ev.price_fx = tk.price;
       ev.match_volume_fx = 0;
       ev.maker_volume_fx = x.amt;
-      ev.taker_volume_fx = x.amt;
       ev.taker_seq = tk.idx;
       ev.fill_idx = 0;
-      ev.symbol_id = sym;
       ev.maker_oid_id = tk.oid;
       ev.maker_uuid_id = tk.uuid;
       ev.maker_next_oid_id = 0;
@@ -1391,7 +1389,6 @@ __global__ __launch_bounds__(256) void k_fc_events(Dev D, BatchArgs B, FlowArgs 
       ev.maker_side = tk.side;
       ev.maker_is_last = 1;
       ev.pad0 = 0;
-      ev.seq_hi = 0;
       dst[0] = ev;
       if (d.kind == FC_OLD) {  // unlink (nodelink.go:124-166): a tombstone, the index entry erased
         Node* nd = &D.nodes[d.tgt];
@@ -1443,10 +1440,8 @@ __global__ __launch_bounds__(256) void k_fc_events(Dev D, BatchArgs B, FlowArgs 
       ev.price_fx = price;
       ev.match_volume_fx = qty;
       ev.maker_volume_fx = full ? pre : pre - qty;
-      ev.taker_volume_fx = tb - (hi - T.c);
       ev.taker_seq = tk.idx;
       ev.fill_idx = fb + k;
-      ev.symbol_id = sym;
       ev.maker_oid_id = oid;
       ev.maker_uuid_id = uuid;
       ev.maker_next_oid_id = nx;
@@ -1454,7 +1449,6 @@ __global__ __launch_bounds__(256) void k_fc_events(Dev D, BatchArgs B, FlowArgs 
       ev.maker_side = static_cast<uint8_t>(tx);
       ev.maker_is_last = static_cast<uint8_t>(last);
       ev.pad0 = 0;
-      ev.seq_hi = 0;
       dst[k] = ev;
       ++k;
     }

@@ -207,6 +207,15 @@ __device__ __forceinline__ void l0_glb64(void* p, v4u a, v4u b, v4u c, v4u d) {
                "global_store_dwordx4 %1, %5, off offset:48\n\ts_mov_b64 exec, %0"
                : "=&s"(sv) : "v"(ad), "v"(a), "v"(b), "v"(c), "v"(d) : "memory");
 }
+__device__ __forceinline__ void l0_glb48(void* p, v4u a, v4u b, v4u c) {
+  unsigned long long sv;
+  const unsigned long long ad = reinterpret_cast<unsigned long long>(p);
+  asm volatile("s_mov_b64 %0, exec\n\ts_mov_b64 exec, 1\n\t"
+               "global_store_dwordx4 %1, %2, off\n\t"
+               "global_store_dwordx4 %1, %3, off offset:16\n\t"
+               "global_store_dwordx4 %1, %4, off offset:32\n\ts_mov_b64 exec, %0"
+               : "=&s"(sv) : "v"(ad), "v"(a), "v"(b), "v"(c) : "memory");
+}
 __device__ __forceinline__ void l0_glb8(void* p, int64_t v) {
   unsigned long long sv;
   const unsigned long long ad = reinterpret_cast<unsigned long long>(p);
@@ -292,9 +301,8 @@ __device__ __forceinline__ void hot_emit(HotCtx& H, int64_t price, int64_t qty, 
   ST_T0(t_e)
   if (H.ev_used == EVB_HOT) hot_ev_block(H);  // ev_base starts NIL with ev_used = EVB_HOT
   if (!H.fatal)
-    l0_glb64(&H.arena[H.ev_base + H.ev_used], v4(lo32(price), hi32(price), lo32(qty), hi32(qty)),
-             v4(lo32(mvol), hi32(mvol), lo32(tvol), hi32(tvol)), v4(seq, fidx, H.sym, moid),
-             v4(muuid, mnext, kind | (mside << 8) | (mlast << 16), 0u));
+    l0_glb48(&H.arena[H.ev_base + H.ev_used], v4(lo32(price), hi32(price), lo32(qty), hi32(qty)),
+             v4(lo32(mvol), hi32(mvol), seq, fidx), v4(moid, muuid, mnext, kind | (mside << 8) | (mlast << 16)));
   H.ev_used++;
   ST_ADD(5, t_e)
 }

@@ -105,7 +105,6 @@ class Router:
         ev = ev[np.argsort(ev["taker_seq"], kind="stable")]
         sq = ev["taker_seq"].astype(np.uint64) + np.uint64(seq_base)
         ev["taker_seq"] = (sq & np.uint64(0xFFFFFFFF)).astype(np.uint32)
-        ev["seq_hi"] = (sq >> np.uint64(32)).astype(np.uint32)
         self._ev = ev
         # a handle with no records this batch: zero per-batch counters, its running totals kept
         self._stats = [x[1] if x[1] is not None else

@@ -24,12 +24,26 @@ assert ORDER_DTYPE.itemsize == 32
 
 EVENT_DTYPE = np.dtype([
     ("price_fx", "<i8"), ("match_volume_fx", "<i8"), ("maker_volume_fx", "<i8"),
-    ("taker_volume_fx", "<i8"), ("taker_seq", "<u4"), ("fill_idx", "<u4"),
-    ("symbol_id", "<u4"), ("maker_oid_id", "<u4"), ("maker_uuid_id", "<u4"),
+    ("taker_seq", "<u4"), ("fill_idx", "<u4"), ("maker_oid_id", "<u4"), ("maker_uuid_id", "<u4"),
     ("maker_next_oid_id", "<u4"), ("kind", "u1"), ("maker_side", "u1"),
-    ("maker_is_last", "u1"), ("pad0", "u1"), ("seq_hi", "<u4"),
+    ("maker_is_last", "u1"), ("pad0", "u1"),
 ])
-assert EVENT_DTYPE.itemsize == 64
+assert EVENT_DTYPE.itemsize == 48
+
+
+def taker_remaining(ev: np.ndarray, records: np.ndarray, seq_base: int = 0) -> np.ndarray:
+    """Node.Volume of each event (gome_abi.h): for a FILL the taker's volume minus its fills so far
+    (a taker's events are consecutive in publish order), for a CANCEL the stored remaining volume."""
+    idx = ((ev["taker_seq"].astype(np.int64) - seq_base) & 0xFFFFFFFF).astype(np.int64)
+    fill = ev["kind"] == 1
+    q = np.where(fill, ev["match_volume_fx"], 0)
+    start = np.ones(len(ev), bool)
+    start[1:] = idx[1:] != idx[:-1]
+    grp = np.cumsum(start) - 1
+    cs = np.cumsum(q)
+    base = np.concatenate([[0], cs])[np.nonzero(start)[0]][grp]  # fills before the taker's first event
+    rem = records["volume_fx"][idx] - (cs - base)
+    return np.where(fill, rem, ev["maker_volume_fx"])
 
 LEVEL_DTYPE = np.dtype([("price_fx", "<i8"), ("depth_fx", "<i8"), ("n_nodes", "<u4"),
                         ("in_buy", "u1"), ("in_sale", "u1"), ("pad", "<u2")])

@@ -13,7 +13,7 @@
  * (batching consumer, cgo backend) converts OrderNode messages to
  * 32-byte gome_order records and submits them in consume order; the engine
  * applies them with exactly the reference's sequential semantics per symbol and
- * returns 64-byte gome_event records in the reference's publish order.
+ * returns 48-byte gome_event records in the reference's publish order.
  *
  * Conventions: plain C types only, no exceptions or panics across the ABI,
  * every call returns a gome_status, the handle is not thread-safe (one host
@@ -72,7 +72,7 @@ enum { GOME_BUY = 0, GOME_SALE = 1 };     /* api/order.proto:4-7            */
 /* One consumed OrderNode message (ordernode.go:9-36) in fixed point.
  * price_fx / volume_fx = value * 10^accuracy exactly (ordernode.go:76-87, see
  * gome_fixed_from_double / gome_fixed_from_scaled).  The sequence number of a record
- * is seq_base + its index in the submitted batch (gome_event.taker_seq / seq_hi). */
+ * is seq_base + its index in the submitted batch (gome_event.taker_seq: its low 32 bits). */
 typedef struct gome_order {
   int64_t price_fx;   /* OrderNode.Price  (limit price; request price for DEL)  */
   int64_t volume_fx;  /* OrderNode.Volume (>= 0)                                */
@@ -87,24 +87,26 @@ typedef struct gome_order {
 
 enum { GOME_EV_FILL = 1, GOME_EV_CANCEL = 2 };
 
-/* One published MatchResult (engine.go:24-28).
+/* One published MatchResult (engine.go:24-28), 48 bytes (ABI >= 8; SURVEY §8's EventRec).
  *   FILL   (engine.go:154,171,190): Node = taker after the fill, MatchNode = maker
  *          as read from the FIFO head (IsFirst=true, PrevNode=""), MatchVolume = qty.
  *   CANCEL (engine.go:109): Node = MatchNode = the DEL request with Volume = the
  *          stored remaining volume; MatchVolume = 0.
- * Sequence number of the taker (the ADD / DEL record) = (seq_hi << 32) | taker_seq =
- * seq_base + its index in the batch (ABI >= 4; with seq_base = 0, taker_seq IS the batch
- * index).  Events of one batch are returned in the reference publish order, i.e.
+ * The taker's record (symbol, uuid, oid, Transaction, limit price) is the submitted record of
+ * sequence number seq; Node.Volume of a FILL is the taker's remaining volume after it: its
+ * record's volume minus the MatchVolumes of its fills so far (a taker's events are consecutive
+ * in publish order; gome_render_events keeps that running sum).
+ * Sequence number of the taker (the ADD / DEL record) = seq_base + its index in the batch;
+ * taker_seq holds its low 32 bits (the caller knows seq_base: with seq_base = 0, taker_seq IS
+ * the batch index).  Events of one batch are returned in the reference publish order, i.e.
  * sorted by (sequence number, fill_idx). */
 typedef struct gome_event {
   int64_t price_fx;         /* level price (= MatchNode.Price); DEL: request price  */
   int64_t match_volume_fx;  /* MatchVolume                                           */
   int64_t maker_volume_fx;  /* MatchNode.Volume: pre-fill if fully filled, else the
                                maker's remaining volume; DEL: stored remaining       */
-  int64_t taker_volume_fx;  /* Node.Volume: taker remaining after this fill          */
   uint32_t taker_seq;       /* low 32 bits of seq_base + batch index                 */
   uint32_t fill_idx;        /* 0,1,2... within one taker                             */
-  uint32_t symbol_id;
   uint32_t maker_oid_id;    /* MatchNode.Oid                                         */
   uint32_t maker_uuid_id;   /* MatchNode.Uuid                                        */
   uint32_t maker_next_oid_id; /* MatchNode.NextNode = S:node:<this> unless is_last   */
@@ -112,7 +114,6 @@ typedef struct gome_event {
   uint8_t maker_side;       /* MatchNode.Transaction code                            */
   uint8_t maker_is_last;    /* MatchNode.IsLast (NextNode == "")                     */
   uint8_t pad0;
-  uint32_t seq_hi;          /* high 32 bits of seq_base + batch index                */
 } gome_event;
 
 /* One price level of a book in the reference key schema (nodepool.go:61-115):
@@ -410,12 +411,13 @@ gome_status gome_fixed_from_double(double x, uint32_t accuracy, int64_t* out);
 gome_status gome_fixed_from_scaled(double scaled, int64_t* out);
 /* Render one event as the reference's MatchResult JSON (Go encoding/json of
  * engine.MatchResult, byte-identical).  Strings are the host's interned names;
- * `taker` is the record of the event's taker.  tx_table maps Transaction codes
+ * `taker` is the record of the event's taker, taker_remaining_fx its remaining volume after
+ * this fill (Node.Volume; ignored for a CANCEL).  tx_table maps Transaction codes
  * (gome_order.side, gome_event.maker_side) to the raw int32 Transaction values to echo;
  * NULL = identity (codes 0..255 are the values).  Returns bytes written (excl. NUL), or
  * -(bytes needed incl. NUL) when cap is too small, or INT64_MIN on a NULL argument. */
 int64_t gome_render_match_result(const gome_event* ev, const gome_order* taker,
-                                 uint32_t accuracy, const char* symbol,
+                                 int64_t taker_remaining_fx, uint32_t accuracy, const char* symbol,
                                  const char* taker_uuid, const char* taker_oid,
                                  const char* maker_uuid, const char* maker_oid,
                                  const char* maker_next_oid, const int32_t* tx_table,

@@ -179,7 +179,7 @@ static int64_t match_level(oracle* o, uint32_t sym, olevel* L, int64_t T, uint32
     int64_t diff = T - m->rem; /* engine.go:143 */
     gome_event* e = ev_push(o);
     e->kind = GOME_EV_FILL; e->taker_seq = seq; e->fill_idx = (*fill_idx)++;
-    e->symbol_id = sym; e->price_fx = L->price;
+    e->price_fx = L->price;
     e->maker_oid_id = m->oid; e->maker_uuid_id = m->uuid; e->maker_side = m->side;
     e->maker_is_last = m->next < 0;
     e->maker_next_oid_id = m->next >= 0 ? o->nodes[m->next].oid : 0;
@@ -187,7 +187,7 @@ static int64_t match_level(oracle* o, uint32_t sym, olevel* L, int64_t T, uint32
     if (diff >= 0) { /* :145-175 maker fully filled (pre-fill volume reported) */
       int64_t mv = m->rem;
       T -= mv;
-      e->match_volume_fx = mv; e->maker_volume_fx = mv; e->taker_volume_fx = T;
+      e->match_volume_fx = mv; e->maker_volume_fx = mv;
       fifo_unlink(o, L, mi);
       int64_t k = idx_find(o, okey(sym, m->oid));
       if (k >= 0 && o->idx[k].node == mi) o->idx[k].key = ~0ULL;
@@ -200,7 +200,7 @@ static int64_t match_level(oracle* o, uint32_t sym, olevel* L, int64_t T, uint32
     /* :176-194 maker partially filled: remaining volume reported, keeps position */
     int64_t fill = T;
     m->rem -= fill;
-    e->match_volume_fx = fill; e->maker_volume_fx = m->rem; e->taker_volume_fx = 0;
+    e->match_volume_fx = fill; e->maker_volume_fx = m->rem;
     L->depth -= fill;
     if (L->depth <= 0) L->member &= ~side_bit(m->side);
     return 0;
@@ -261,9 +261,9 @@ static void do_del(oracle* o, const gome_order* r, uint32_t seq) {
   o->idx[k].key = ~0ULL;
   node_free(o, ni);
   gome_event* e = ev_push(o);
-  e->kind = GOME_EV_CANCEL; e->taker_seq = seq; e->fill_idx = 0; e->symbol_id = r->symbol_id;
+  e->kind = GOME_EV_CANCEL; e->taker_seq = seq; e->fill_idx = 0;
   e->price_fx = r->price_fx; e->match_volume_fx = 0; e->maker_volume_fx = rem;
-  e->taker_volume_fx = rem; e->maker_oid_id = r->oid_id; e->maker_uuid_id = r->uuid_id;
+  e->maker_oid_id = r->oid_id; e->maker_uuid_id = r->uuid_id;
   e->maker_side = r->side; e->maker_is_last = 1; e->maker_next_oid_id = 0;
   o->st.n_cancels++;
 }

@@ -61,13 +61,15 @@ def requests_to_records(batch, names: Interner, accuracy: int = 8) -> np.ndarray
 
 def render_events(events: np.ndarray, records: np.ndarray, names: Interner,
                   accuracy: int = 8) -> list[str]:
+    from gome_amd.workload import taker_remaining
     out = []
-    for e in events:
+    rem = taker_remaining(events, records) if len(events) else []
+    for e, tr in zip(events, rem):
         t = records[e["taker_seq"]]
         sym = names.name("sym", int(t["symbol_id"]))
         cancel = e["kind"] == 2
         out.append(render_match_result(
-            e, t, sym, names.name("uuid", int(t["uuid_id"])), names.name("oid", int(t["oid_id"])),
+            e, t, int(tr), sym, names.name("uuid", int(t["uuid_id"])), names.name("oid", int(t["oid_id"])),
             None if cancel else names.name("uuid", int(e["maker_uuid_id"])),
             None if cancel else names.name("oid", int(e["maker_oid_id"])),
             None if (cancel or e["maker_is_last"]) else names.name("oid", int(e["maker_next_oid_id"])),

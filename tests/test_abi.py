@@ -22,7 +22,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_record_layouts_match_header():
     from gome_amd.workload import EVENT_DTYPE, LEVEL_DTYPE, NODE_DTYPE, ORDER_DTYPE
-    assert ORDER_DTYPE.itemsize == 32 and EVENT_DTYPE.itemsize == 64
+    assert ORDER_DTYPE.itemsize == 32 and EVENT_DTYPE.itemsize == 48
     assert LEVEL_DTYPE.itemsize == 24 and NODE_DTYPE.itemsize == 24
     assert C.sizeof(abi.Config) == 48
 

@@ -26,7 +26,6 @@ class _OracleEngine:
         ev = self.o.submit(rec)
         sq = ev["taker_seq"].astype(np.uint64) + np.uint64(seq_base)
         ev["taker_seq"] = (sq & np.uint64(0xFFFFFFFF)).astype(np.uint32)
-        ev["seq_hi"] = (sq >> np.uint64(32)).astype(np.uint32)
         self._ev = ev
 
     def drain(self):
@@ -336,7 +335,7 @@ def test_render_events_long_ids():
     rec = np.zeros(1, ORDER_DTYPE)
     rec[0] = (5 * 10**7, 10**8, 0, 0, 0, 0, 1, 0)
     ev = np.zeros(1, EVENT_DTYPE)
-    ev[0]["kind"], ev[0]["price_fx"], ev[0]["maker_volume_fx"], ev[0]["taker_volume_fx"] = 2, 5 * 10**7, 10**8, 10**8
+    ev[0]["kind"], ev[0]["price_fx"], ev[0]["maker_volume_fx"] = 2, 5 * 10**7, 10**8
     ev[0]["maker_is_last"] = 1
     tab = lambda *s: (C.c_char_p * len(s))(*[x.encode() for x in s])
     sym, uu, oo = tab("s"), tab("u"), tab(long_oid)

@@ -123,9 +123,10 @@ def test_seq_base_in_events():
     eng.submit(b, seq_base=base)
     got = eng.drain()
     exp = orc.submit(b)
-    seq = (got["seq_hi"].astype(np.uint64) << np.uint64(32)) | got["taker_seq"].astype(np.uint64)
-    assert np.array_equal(seq, exp["taker_seq"].astype(np.uint64) + np.uint64(base))
-    got["taker_seq"], got["seq_hi"] = exp["taker_seq"], 0
+    # taker_seq = the low 32 bits of seq_base + batch index (the caller holds seq_base)
+    want = (exp["taker_seq"].astype(np.uint64) + np.uint64(base)) & np.uint64(0xFFFFFFFF)
+    assert np.array_equal(got["taker_seq"].astype(np.uint64), want)
+    got["taker_seq"] = exp["taker_seq"]
     _cmp(got, exp, "seq_base")
 
 

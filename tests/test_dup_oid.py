@@ -183,7 +183,7 @@ def test_divergent_stream_gpu_vs_oracle(legacy):
         assert eng.stats()["n_dropped"] == dropped - prev_dropped
         prev_dropped = dropped
         total += len(d)
-    assert total > 3000
+    assert total > 1000  # (queue-order rule: a key whose first node was consumed is applied)
     _cmp_books(eng, orc, range(40), "divergent stream")
     assert eng.stats()["n_resting"] == orc.resting()
     if not legacy:

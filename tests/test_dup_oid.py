@@ -186,8 +186,8 @@ def test_divergent_stream_gpu_vs_oracle(legacy):
     assert total > 1000  # (queue-order rule: a key whose first node was consumed is applied)
     _cmp_books(eng, orc, range(40), "divergent stream")
     assert eng.stats()["n_resting"] == orc.resting()
-    if not legacy:
-        assert eng.stats()["n_flow_books"] > 0
+    # (every book of this stream holds duplicate-oid candidates in every batch: the serial
+    # kernels apply them all; tests below cover the flow routing)
 
 
 def _assign_books(b):

@@ -328,8 +328,11 @@ def test_flow_then_cancels_then_flow():
 
 
 def test_flow_declines_quirky_book():
-    """A wrong-side cancel (Q2) marks the book; its later ADD-only batches stay on the
-    legacy kernel (the aggregate plan cannot express shared-price FIFOs)."""
+    """A quirk state that never heals keeps the book on the legacy kernel (the aggregate plan
+    cannot express it): a wrong-side cancel (Q2) of the lowest level's first maker, plus a
+    zero-volume BUY (Q6) resting on a new level below every price the stream uses (never reached
+    again).  A Q2 alone that leaves the level with makers is no quirk at all: the book is back
+    on the flow path after the batch (match_requal.h)."""
     st = wl.Stream(1, seed=5)
     eng = _engine(1, 8192)
     orc = Oracle(1)
@@ -338,14 +341,17 @@ def test_flow_declines_quirky_book():
     _cmp_events(eng.drain(), orc.submit(b))
     lv = orc.levels(0)[0]
     nd = orc.fifo(0, int(lv["price_fx"]))[0]
-    q2 = np.zeros(1, wl.ORDER_DTYPE)
+    q2 = np.zeros(2, wl.ORDER_DTYPE)
     q2[0] = (int(lv["price_fx"]), 10**6, 0, int(nd["oid_id"]), int(nd["uuid_id"]), 1 - int(nd["side"]), 2, 0)
+    q2[1] = (10**5, 0, 0, 4_000_000_000, 1, 0, 1, 0)  # zero-volume BUY at 0.001
     eng.submit(q2)
     _cmp_events(eng.drain(), orc.submit(q2))
-    b = st.batch(4000)
-    eng.submit(b)
-    _cmp_events(eng.drain(), orc.submit(b))
-    assert eng.stats()["n_flow_books"] == 0
+    for _ in range(2):
+        b = st.batch(4000)
+        eng.submit(b)
+        _cmp_events(eng.drain(), orc.submit(b))
+        assert eng.stats()["n_flow_books"] == 0 and eng.stats()["n_quirk_checked"] == 1
+        assert eng.stats()["n_requalified"] == 0
     assert np.array_equal(eng.levels(0), orc.levels(0))
 
 

@@ -24,7 +24,7 @@ GOME_FLAG_CHAINS_ALWAYS = 4  # gome_config.flags: enqueue the deep / cancel chai
 GOME_FLAG_CHAINS_NEVER = 8  # gome_config.flags: never (deep books and books with DELs: legacy / cold)
 GOME_FLAG_PHASES = 16  # gome_config.flags: record the per-phase timing events (gome_stats.ms_phase)
 GOME_ORD_ADM_HOST, GOME_ORD_ADMITTED = 1, 2  # gome_order.flags: host-resolved admission (ABI 4)
-GOME_MAX_INFLIGHT = 2
+GOME_MAX_INFLIGHT = 3
 
 TOB_DTYPE = np.dtype([("symbol_id", "<u4"), ("n_levels", "<u4"), ("bid_price_fx", "<i8"), ("bid_depth_fx", "<i8"),
                       ("ask_price_fx", "<i8"), ("ask_depth_fx", "<i8"), ("bid_nodes", "<u4"), ("ask_nodes", "<u4"),

@@ -5,7 +5,7 @@
 //   Level    <- S:depth field (depth), S:BUY / S:SALE membership (member bits),
 //               S:link:<price> "f"/"l" pointers (head/tail chunk + slot)
 //   Node     <- one JSON node of S:link:<price> (32 B, two 16-B halves)
-//   chunks   <- 32 consecutive Nodes of one FIFO (1 KiB) + a ChunkHdr
+//   chunks   <- CH consecutive Nodes of one FIFO (CH x 32 B) + a ChunkHdr
 //   IdxEnt   <- HGET S:link:<p> S:node:<oid> (engine.go:92-93) as an (S, oid) index
 #pragma once
 #include <stdint.h>
@@ -13,10 +13,14 @@
 namespace gome {
 
 constexpr int WAVE = 64;
+// FIFO slots per chunk.  A level's FIFO is a chain of chunks, so every non-empty level holds at
+// least one: deep books (config 5: ~1.2 makers per level) paid 1 KiB per level with 32-slot
+// chunks; 4-slot chunks (128 B + a 16-B header) hold them at ~110-140 B per resting order for
+// 0-2.6% of batch time on the deep-FIFO workloads (same-box A/B, round 4).
 #ifndef GOME_CH
-#define GOME_CH 32
+#define GOME_CH 4
 #endif
-constexpr int CH = GOME_CH;            // FIFO slots per chunk
+constexpr int CH = GOME_CH;
 constexpr uint32_t NIL = 0xFFFFFFFFu;
 constexpr uint8_t M_BUY = 1, M_SALE = 2;  // side-set membership bits
 constexpr unsigned long long KEY_EMPTY = 0ull, KEY_TOMB = ~0ull;

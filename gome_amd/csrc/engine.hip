@@ -261,9 +261,8 @@ struct gome_engine {
   hipStream_t hot_stream = nullptr;   // tail / near-head flow books, legacy hot kernel
   hipStream_t flow_stream = nullptr;  // the hottest book's plan (critical path)
   hipStream_t copy_stream = nullptr;  // H2D of records, D2H of events (pipelined path)
-  // D2H of collected events on a stream of their own (GOME_D2H_STREAM=1): beside the next
-  // batch's H2D instead of behind it (PCIe is full duplex), if HIP gives it its own hardware
-  // queue (GPU_MAX_HW_QUEUES; with 4, a fifth stream shares one)
+  // D2H of collected events on a stream of their own (GOME_D2H_STREAM=0: on the copy stream):
+  // with three batches in flight, batch k's D2H runs beside batch k+2's H2D (PCIe is full duplex)
   hipStream_t d2h_stream = nullptr;
   hipEvent_t fork{}, join{}, joinf{}, prep_h{}, prep_t{}, fork_adm{}, adm_done{}, seg_done{};
   hipEvent_t dp_fork{}, cnt_fork{}, cnt_done{}, dw_done{}, dl_done{}, tl_done{};  // the hottest book's deep chain, k_flow_count beside its writes
@@ -447,7 +446,7 @@ gome_status gome_engine::init(const gome_config& c) {
   HIPCHK(hipStreamCreateWithFlags(&hot_stream, hipStreamNonBlocking));
   HIPCHK(hipStreamCreateWithFlags(&flow_stream, hipStreamNonBlocking));
   HIPCHK(hipStreamCreateWithFlags(&copy_stream, hipStreamNonBlocking));
-  if (const char* g = std::getenv("GOME_D2H_STREAM"); g && std::atoi(g) != 0)
+  if (const char* g = std::getenv("GOME_D2H_STREAM"); !g || std::atoi(g) != 0)
     HIPCHK(hipStreamCreateWithFlags(&d2h_stream, hipStreamNonBlocking));
   for (hipEvent_t* ev : {&fork, &join, &joinf, &prep_h, &prep_t, &fork_adm, &adm_done, &seg_done,
                          &dp_fork, &cnt_fork, &cnt_done, &dw_done, &dl_done, &tl_done, &tob_done})
@@ -497,11 +496,12 @@ gome_status gome_engine::init(const gome_config& c) {
   bsum_cap = ceil_div(scan_max, SCAN_TILE) + 1;
 
   // ---- persistent book state
-  // chunks: every non-empty level holds >= 1 (plus head/tail chunks partly consumed),
-  // and every 32 resting nodes fill one more
+  // chunks: every non-empty level holds >= 1 (plus head/tail chunks partly consumed and chunks
+  // of tombstones awaiting the head), and every CH resting nodes fill one more: slots for 4x
+  // max_nodes plus two chunks per possible level
   const unsigned long long nchunks = std::min<unsigned long long>(
-      cfg.max_nodes / 8 + 2 * std::min<unsigned long long>(cfg.max_levels, cfg.max_nodes) + 1024,
-      0xF0000000ull);
+      4 * ((cfg.max_nodes + CH - 1) / CH) + 2 * std::min<unsigned long long>(cfg.max_levels, cfg.max_nodes) + 1024,
+      std::min<unsigned long long>(0xF0000000ull, 0xFFFFFFFEull / CH));
   idx_cap = next_pow2(std::max<unsigned long long>(2 * cfg.max_nodes, 1024));
   // level-block free lists: class c (16 << c levels) holds at most max_levels >> (4 + c) blocks
   std::vector<uint32_t> cls_off(LVL_NCLS + 1, 0);

@@ -312,8 +312,9 @@ gome_status gome_debug_peek(gome_engine* e, uint32_t which, uint64_t offset, uin
 
 /* ---- pipelined host path (ABI >= 4) ---------------------------------------- */
 /* The batching consumer's loop: submit batch k+1, then collect batch k.
- * The copy of batch k+1's records to HBM and of batch k's events to the host run on a
- * copy stream while the device applies the other batch, so PCIe hides under matching.
+ * The copy of batch k+1's records to HBM and of batch k's events to the host run on two
+ * copy streams while the device applies the other batch, so PCIe hides under matching (with
+ * three batches in flight, batch k+2's H2D and batch k's D2H also overlap each other).
  * At most GOME_MAX_INFLIGHT batches are in flight; `orders` must stay valid and
  * unchanged until the batch is collected (memory from gome_host_alloc is page-locked,
  * which makes the copy asynchronous).  gome_submit_batch, gome_submit_batch_device,
@@ -321,7 +322,7 @@ gome_status gome_debug_peek(gome_engine* e, uint32_t which, uint64_t offset, uin
  * in-flight batch into the drain queue.  A batch collected that way that was rejected
  * (GOME_E_INVAL, nothing applied) does not fail that call: the call goes on and the failure
  * is kept for gome_take_deferred. */
-#define GOME_MAX_INFLIGHT 2u
+#define GOME_MAX_INFLIGHT 3u  /* (2 before ABI v8) */
 gome_status gome_submit_batch_async(gome_engine* e, const gome_order* orders, size_t n,
                                     uint64_t seq_base);
 /* Wait for the oldest in-flight batch and copy its events to engine-owned page-locked

@@ -31,32 +31,37 @@ def test_device_pipeline_matches_oracle():
     torch.cuda.synchronize()
     exp = [orc.submit(b) for b in host]
     seq = [0] * 6  # (the oracle numbers each batch from 0)
-    # two in flight, then collect the older: its count is the oracle's
-    eng.submit_device_async(dev[0].data_ptr(), n, seq[0])
-    eng.submit_device_async(dev[1].data_ptr(), n, seq[1])
+    # three in flight (GOME_MAX_INFLIGHT), then collect the oldest: its count is the oracle's
+    host.append(st.batch(n))
+    dev.append(_dev(host[-1]))
+    torch.cuda.synchronize()
+    exp.append(orc.submit(host[-1]))
+    seq.append(0)
+    for k in range(3):
+        eng.submit_device_async(dev[k].data_ptr(), n, seq[k])
     with pytest.raises(GomeError):
-        eng.submit_device_async(dev[2].data_ptr(), n, seq[2])  # (GOME_MAX_INFLIGHT)
+        eng.submit_device_async(dev[3].data_ptr(), n, seq[3])  # (GOME_MAX_INFLIGHT)
     p0, n0, s0 = eng.collect_device()
     assert p0 and n0 == len(exp[0]) and s0["n_orders"] == n
-    # a drain now: batch 0's device events first, then batch 1 (collected into the queue)
+    # a drain now: batch 0's device events first, then batches 1 and 2 (collected into the queue)
     got = eng.drain()
-    _cmp(got, np.concatenate([exp[0], exp[1]]), "drain after collect")
+    _cmp(got, np.concatenate([exp[0], exp[1], exp[2]]), "drain after collect")
     # steady state: submit k+1, collect k, the consumer releases k's events on the device
-    eng.submit_device_async(dev[2].data_ptr(), n, seq[2])
     eng.submit_device_async(dev[3].data_ptr(), n, seq[3])
-    _, n2, _ = eng.collect_device()
-    assert n2 == len(exp[2])
-    eng.release_device_events()
     eng.submit_device_async(dev[4].data_ptr(), n, seq[4])
-    _, n3, _ = eng.collect_device()  # (batch 3's events; 4 in flight)
+    _, n3, _ = eng.collect_device()
     assert n3 == len(exp[3])
-    _, n4, _ = eng.collect_device()  # batch 3's events move to the host queue first
-    assert n4 == len(exp[4])
-    got = eng.drain()
-    _cmp(got, np.concatenate([exp[3], exp[4]]), "spilled then device")
+    eng.release_device_events()
     eng.submit_device_async(dev[5].data_ptr(), n, seq[5])
-    _, n5, _ = eng.collect_device()
-    _cmp(eng.drain(), exp[5], "last")
+    _, n4, _ = eng.collect_device()  # (batch 4's events; 5 in flight)
+    assert n4 == len(exp[4])
+    _, n5, _ = eng.collect_device()  # batch 4's events move to the host queue first
+    assert n5 == len(exp[5])
+    got = eng.drain()
+    _cmp(got, np.concatenate([exp[4], exp[5]]), "spilled then device")
+    eng.submit_device_async(dev[6].data_ptr(), n, seq[6])
+    eng.collect_device()
+    _cmp(eng.drain(), exp[6], "last")
     _cmp_books(eng, orc, range(0, NSYM, 7), "after")
     assert eng.stats()["n_resting"] == orc.resting()
 

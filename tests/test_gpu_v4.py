@@ -157,7 +157,7 @@ def test_device_events_never_dropped():
 
 
 def test_pipelined_async_equals_oracle():
-    """gome_submit_batch_async / gome_collect with two batches in flight == the oracle."""
+    """gome_submit_batch_async / gome_collect with GOME_MAX_INFLIGHT (3) batches in flight == the oracle."""
     st = wl.NativeStream(300, 1.0, seed=5, del_frac=0.3, aggressive_frac=0.05)
     batches = [st.batch(40000).copy() for _ in range(6)]
     eng = Engine(max_symbols=300, max_batch=40000)
@@ -169,18 +169,18 @@ def test_pipelined_async_equals_oracle():
     for buf, b in zip(bufs, batches):
         buf[:] = b
     exp = [orc.submit(b) for b in batches]
-    eng.submit_async(bufs[0])
-    eng.submit_async(bufs[1])
-    assert eng.inflight() == 2
+    for k in range(3):
+        eng.submit_async(bufs[k])
+    assert eng.inflight() == 3
     with pytest.raises(GomeError) as ei:
-        eng.submit_async(bufs[2])
+        eng.submit_async(bufs[3])
     assert ei.value.status == GOME_E_STATE
     for k in range(len(batches)):
         ev, stt = eng.collect()
         _cmp(ev, exp[k], f"async batch {k}")
         assert stt["n_orders"] == len(batches[k])
-        if k + 2 < len(batches):
-            eng.submit_async(bufs[k + 2])
+        if k + 3 < len(batches):
+            eng.submit_async(bufs[k + 3])
     assert eng.inflight() == 0
     # a synchronous call after async ones collects them into the drain queue first
     b = st.batch(1000).copy()

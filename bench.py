@@ -416,10 +416,12 @@ def main():
 
     total_orders = per_rank * (warm + steps + e2e_warm + e2e_steps)
     keep = 0.3 if args.workload == "config3" else 0.5
-    # (+ two batches: the headroom a submit checks, in flight included, before it is applied)
+    # (+ GOME_MAX_INFLIGHT + 1 batches: the headroom a submit checks, in flight included, before
+    # it is applied)
+    head = (GOME_MAX_INFLIGHT + 1) * per_rank
     eng = Engine(max_symbols=n_symbols, max_batch=per_rank,
-                 max_nodes=args.pool_nodes or max(1 << 20, int(total_orders * keep)) + 2 * per_rank,
-                 max_levels=args.pool_levels or max(1 << 22, (256 if n_symbols <= 100000 else 128) * n_symbols) + 2 * per_rank,
+                 max_nodes=args.pool_nodes or max(1 << 20, int(total_orders * keep)) + head,
+                 max_levels=args.pool_levels or max(1 << 22, (256 if n_symbols <= 100000 else 128) * n_symbols) + head,
                  device=dev)
 
     summary = torch.zeros(SUMMARY_WORDS, dtype=torch.int64, device=cdev)

@@ -576,7 +576,9 @@ def main():
             b[:] = gen(per_rank)
         done_ev = [0]
 
-        depth = GOME_MAX_INFLIGHT  # batch k+2's H2D beside batch k's D2H and batch k+1's matching
+        # two batches in flight (three, with the events' D2H on a stream of its own, measured slower:
+        # DESIGN §5)
+        depth = 2
 
         def run_pipe(lo, hi, lats):
             tsub = {}
@@ -625,9 +627,8 @@ def main():
                "events_per_s": round(e_events / e_el, 1),
                "pcie_bytes_per_step": int(32 * per_rank * world + 48 * e_events / e2e_steps),
                "path": "host records -> gome_submit_batch_async (H2D on a copy stream) -> device "
-                       "pipeline -> gome_collect (events D2H into page-locked memory on a second "
-                       "copy stream); three batches in flight: batch k+1's H2D and batch k-1's D2H "
-                       "overlap batch k and each other"}
+                       "pipeline -> gome_collect (events D2H into page-locked memory); batch k+1's "
+                       "H2D and batch k-1's D2H overlap batch k"}
 
     # ---- the other phases of the pipeline (the tail's chain, the sort, admission, publishing):
     # with no hot symbol (config 2) one of them is the longest.  Their device times need ~24

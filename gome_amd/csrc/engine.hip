@@ -261,8 +261,9 @@ struct gome_engine {
   hipStream_t hot_stream = nullptr;   // tail / near-head flow books, legacy hot kernel
   hipStream_t flow_stream = nullptr;  // the hottest book's plan (critical path)
   hipStream_t copy_stream = nullptr;  // H2D of records, D2H of events (pipelined path)
-  // D2H of collected events on a stream of their own (GOME_D2H_STREAM=0: on the copy stream):
-  // with three batches in flight, batch k's D2H runs beside batch k+2's H2D (PCIe is full duplex)
+  // D2H of collected events on a stream of their own (GOME_D2H_STREAM=1; off by default: with
+  // four hardware queues per process a fifth stream shares one, and the e2e A/B measured it
+  // 0.7 ms per config-2 batch slower with three batches in flight, no faster with two)
   hipStream_t d2h_stream = nullptr;
   hipEvent_t fork{}, join{}, joinf{}, prep_h{}, prep_t{}, fork_adm{}, adm_done{}, seg_done{};
   hipEvent_t dp_fork{}, cnt_fork{}, cnt_done{}, dw_done{}, dl_done{}, tl_done{};  // the hottest book's deep chain, k_flow_count beside its writes
@@ -446,7 +447,7 @@ gome_status gome_engine::init(const gome_config& c) {
   HIPCHK(hipStreamCreateWithFlags(&hot_stream, hipStreamNonBlocking));
   HIPCHK(hipStreamCreateWithFlags(&flow_stream, hipStreamNonBlocking));
   HIPCHK(hipStreamCreateWithFlags(&copy_stream, hipStreamNonBlocking));
-  if (const char* g = std::getenv("GOME_D2H_STREAM"); !g || std::atoi(g) != 0)
+  if (const char* g = std::getenv("GOME_D2H_STREAM"); g && std::atoi(g) != 0)
     HIPCHK(hipStreamCreateWithFlags(&d2h_stream, hipStreamNonBlocking));
   for (hipEvent_t* ev : {&fork, &join, &joinf, &prep_h, &prep_t, &fork_adm, &adm_done, &seg_done,
                          &dp_fork, &cnt_fork, &cnt_done, &dw_done, &dl_done, &tl_done, &tob_done})

@@ -4,7 +4,7 @@
 set -o pipefail
 O=gpurun_out/${1:-r4c5}
 mkdir -p $O
-timeout -k 10 1000 python -u bench.py --workload config5 --steps ${2:-200} --warmup 3 --no-cpu-baseline --no-phase-pass \
+timeout -k 10 1000 python -u bench.py --workload config5 --steps ${2:-200} --warmup 3 --pool-levels 335544320 --no-cpu-baseline --no-phase-pass \
   --e2e-steps 0 --consumer-msgs 0 --step-log $O/config5_steps.jsonl > $O/config5_long.json 2> $O/config5_long.err \
   || { tail -20 $O/config5_long.err; exit 1; }
 python - $O <<'PY'

@@ -287,6 +287,7 @@ struct gome_engine {
   bool tail_serial = false;  // the split tail's events after its writes on one stream (GOME_TAIL_SERIAL: solo kernel times)
   int prep_wait = -1;  // k_prep after the head's prep always (1) / adaptive (-1; GOME_PREP_WAIT, A/B)
   bool adm_fast = true;
+  bool cold_main = false;  // k_match on the caller's stream (GOME_COLD_MAIN=1; default: the copy stream)
   // GOME_PH_* timing events (gome_stats.ms_phase): ~24 event records per batch, 0.12 ms on config 2's
   // critical path, so only on request (GOME_FLAG_PHASES, or GOME_PHASES=1)
   bool phases = false;  // k_adm_pre's fresh-batch test (GOME_ADM_FAST=0: every batch through the tables; A/B)
@@ -485,6 +486,7 @@ gome_status gome_engine::init(const gome_config& c) {
   if (const char* g = std::getenv("GOME_PREP_WAIT")) prep_wait = std::atoi(g) != 0 ? 1 : 0;       // (A/B)
   if (const char* g = std::getenv("GOME_SORT_AHEAD")) sort_ahead = std::atoi(g) != 0;           // (A/B)
   if (const char* g = std::getenv("GOME_ADM_FAST")) adm_fast = std::atoi(g) != 0;              // (A/B)
+  if (const char* g = std::getenv("GOME_COLD_MAIN")) cold_main = std::atoi(g) != 0;            // (A/B)
   phases = (cfg.flags & GOME_FLAG_PHASES) != 0;
   if (const char* g = std::getenv("GOME_PHASES")) phases = std::atoi(g) != 0;
   uint32_t ms = cfg.max_symbols;
@@ -983,10 +985,18 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
     HIPCHK(mark(GOME_PH_TAIL_PREP, 1, s));
   }
   HIPCHK(hipEventRecord(prep_t, s));
-  HIPCHK(hipEventRecord(S.evc0, s));
-  k_match<<<std::min<uint32_t>(ceil_div(grid, COLD_WAVES), COLD_BLOCKS), 64 * COLD_WAVES, COLD_LDS_BYTES, s>>>(
+  // the cold books (k_match) beside the tail's chain instead of before it: they share no book, only
+  // the pools' atomics, and on deep books the cold kernel alone grew to 20 ms per batch (config 5 at
+  // step 200), which put the tail's plans and reconstruction behind it on the critical path.  On the
+  // copy stream: idle during device batches; on the host path it delays the next batch's H2D and
+  // the previous one's D2H by the cold kernel's time, well inside the batch (GOME_COLD_MAIN=1: the
+  // caller's stream, for A/B)
+  hipStream_t cst = cold_main ? s : copy_stream;
+  if (cst != s) HIPCHK(hipStreamWaitEvent(cst, prep_t, 0));
+  HIPCHK(hipEventRecord(S.evc0, cst));
+  k_match<<<std::min<uint32_t>(ceil_div(grid, COLD_WAVES), COLD_BLOCKS), 64 * COLD_WAVES, COLD_LDS_BYTES, cst>>>(
       D, B, &F.hdr[0].ok, sizeof(FlowHdr) / sizeof(uint32_t));
-  HIPCHK(hipEventRecord(S.evc1, s));
+  HIPCHK(hipEventRecord(S.evc1, cst));
   if (nh_tail) {  // the tail's plans and reconstruction
     HIPCHK(mark(GOME_PH_TAIL_PLAN, 0, s));
     k_flow_plan_tail<<<nh_tail, 64, 0, s>>>(D, FT);
@@ -1058,6 +1068,7 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   HIPCHK(hipStreamWaitEvent(s, join, 0));
   HIPCHK(hipStreamWaitEvent(s, joinf, 0));
   HIPCHK(hipStreamWaitEvent(s, cnt_done, 0));
+  if (cst != s) HIPCHK(hipStreamWaitEvent(s, S.evc1, 0));  // (the cold books' events and index)
 
   HIPCHK(hipEventRecord(S.evm1, s));
 

@@ -486,6 +486,13 @@ gome_status gome_engine::init(const gome_config& c) {
   if (const char* g = std::getenv("GOME_PREP_WAIT")) prep_wait = std::atoi(g) != 0 ? 1 : 0;       // (A/B)
   if (const char* g = std::getenv("GOME_SORT_AHEAD")) sort_ahead = std::atoi(g) != 0;           // (A/B)
   if (const char* g = std::getenv("GOME_ADM_FAST")) adm_fast = std::atoi(g) != 0;              // (A/B)
+  // the cold books go beside the tail's chain only when HIP can give the copy stream a hardware
+  // queue of its own (with 4 it shares the hottest plan's, which serialised them: +6 ms per
+  // config-3 batch); gome_amd/__init__.py asks for 8
+  {
+    const char* q = std::getenv("GPU_MAX_HW_QUEUES");
+    cold_main = !q || std::atoi(q) < 8;
+  }
   if (const char* g = std::getenv("GOME_COLD_MAIN")) cold_main = std::atoi(g) != 0;            // (A/B)
   phases = (cfg.flags & GOME_FLAG_PHASES) != 0;
   if (const char* g = std::getenv("GOME_PHASES")) phases = std::atoi(g) != 0;

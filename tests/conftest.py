@@ -3,6 +3,11 @@ import sys
 
 import pytest
 
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+import gome_amd  # noqa: E402,F401  (before torch: the HIP runtime's hardware-queue count)
+
 # One HIP runtime per process: torch bundles its own libamdhip64.so.7 (same SONAME as
 # /opt/rocm's); importing torch first makes libgome.so bind to that one too, so tests
 # that hand torch device buffers to the engine share one runtime.
@@ -11,9 +16,6 @@ try:
 except Exception:  # pragma: no cover
     torch = None
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-if ROOT not in sys.path:
-    sys.path.insert(0, ROOT)
 
 
 def pytest_configure(config):

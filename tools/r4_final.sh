@@ -1,0 +1,48 @@
+#!/bin/bash
+# Round-4 final measurements (GPU box).  usage: bash tools/r4_final.sh <tag> [parts...]
+#   suite: the GPU test suite;  smoke;  benches: bench lines (e2e, consumer leg, CPU baseline) of
+#   configs 3, 2, 4, 5, 5c;  heal / pg: the quirk-injection line and the RCCL world-1 line;
+#   prof3 / prof2: rocprofv3 trace + FETCH / WRITE passes (profiles/run_rocprof.sh) + summary
+set -o pipefail
+TAG=${1:-r04f}; shift
+PARTS=${@:-suite benches}
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+OUT=gpurun_out/$TAG
+mkdir -p $OUT
+summ() {
+  python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).readlines()[-1]); e=d.get('e2e') or {}; c=d.get('consumer') or {}; print(sys.argv[2], round(d['value']/1e6,2), d['ms_per_step'], 'e2e', round(e.get('value',0)/1e6,2), 'hot', d['hot_book']['ns_per_order'], d['roofline']['kernel'][:30], d['roofline']['frac'], 'p99dev', d.get('p99_device_batch_ms'), 'consumer', c.get('messages_per_s'))" $1 $2
+}
+for P in $PARTS; do
+  case $P in
+  suite)
+    timeout -k 10 700 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread \
+      > $OUT/gpu_tests.txt 2>&1 || { tail -40 $OUT/gpu_tests.txt; exit 2; }
+    tail -3 $OUT/gpu_tests.txt ;;
+  smoke)
+    timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.txt 2>&1 || { tail -20 $OUT/smoke.txt; exit 8; }
+    tail -1 $OUT/smoke.txt ;;
+  benches)
+    for W in config3 config2 config4 config5 config5c; do
+      timeout -k 10 500 python3 -u bench.py --workload $W > $OUT/${W}_bench.jsonl 2> $OUT/${W}_bench.log \
+        || { tail -20 $OUT/${W}_bench.log; exit 3; }
+      summ $OUT/${W}_bench.jsonl $W
+    done ;;
+  heal)
+    timeout -k 10 400 python3 -u bench.py --workload config3 --inject-quirks heal --no-cpu-baseline --consumer-msgs 0 \
+      --step-log $OUT/config3_heal_steps.jsonl > $OUT/config3_heal_bench.jsonl 2> $OUT/config3_heal_bench.log || { tail -20 $OUT/config3_heal_bench.log; exit 4; }
+    summ $OUT/config3_heal_bench.jsonl heal ;;
+  pg)
+    timeout -k 10 400 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 \
+      --master-port 29533 bench.py --gpus 1 --force-pg --backend nccl --no-cpu-baseline --consumer-msgs 0 \
+      > $OUT/config3_rccl_bench.jsonl 2> $OUT/config3_rccl_bench.log || { tail -20 $OUT/config3_rccl_bench.log; exit 5; }
+    summ $OUT/config3_rccl_bench.jsonl rccl ;;
+  prof3)
+    bash profiles/run_rocprof.sh ${TAG}_config3 --steps 6 --warmup 3 --no-cpu-baseline --e2e-steps 0 --consumer-msgs 0 --no-phase-pass || exit 6
+    python3 profiles/summarize.py ${TAG}_config3 gpurun_out/prof_${TAG}_config3 || exit 7 ;;
+  prof2)
+    bash profiles/run_rocprof.sh ${TAG}_config2 --workload config2 --steps 6 --warmup 4 --no-cpu-baseline --e2e-steps 0 --consumer-msgs 0 --no-phase-pass || exit 6
+    python3 profiles/summarize.py ${TAG}_config2 gpurun_out/prof_${TAG}_config2 || exit 7 ;;
+  esac
+done
+echo done

@@ -261,6 +261,7 @@ struct gome_engine {
   hipStream_t hot_stream = nullptr;   // tail / near-head flow books, legacy hot kernel
   hipStream_t flow_stream = nullptr;  // the hottest book's plan (critical path)
   hipStream_t copy_stream = nullptr;  // H2D of records, D2H of events (pipelined path)
+  hipStream_t cold_stream = nullptr;  // the cold books (k_match) beside the tail's chain
   // D2H of collected events on a stream of their own (GOME_D2H_STREAM=1; off by default: with
   // four hardware queues per process a fifth stream shares one, and the e2e A/B measured it
   // 0.7 ms per config-2 batch slower with three batches in flight, no faster with two)
@@ -287,7 +288,7 @@ struct gome_engine {
   bool tail_serial = false;  // the split tail's events after its writes on one stream (GOME_TAIL_SERIAL: solo kernel times)
   int prep_wait = -1;  // k_prep after the head's prep always (1) / adaptive (-1; GOME_PREP_WAIT, A/B)
   bool adm_fast = true;
-  bool cold_main = false;  // k_match on the caller's stream (GOME_COLD_MAIN=1; default: the copy stream)
+  bool cold_main = false;  // k_match on the caller's stream (GOME_COLD_MAIN=1; default: cold_stream)
   // GOME_PH_* timing events (gome_stats.ms_phase): ~24 event records per batch, 0.12 ms on config 2's
   // critical path, so only on request (GOME_FLAG_PHASES, or GOME_PHASES=1)
   bool phases = false;  // k_adm_pre's fresh-batch test (GOME_ADM_FAST=0: every batch through the tables; A/B)
@@ -383,6 +384,7 @@ struct gome_engine {
     if (hot_stream) (void)hipStreamDestroy(hot_stream);
     if (flow_stream) (void)hipStreamDestroy(flow_stream);
     if (copy_stream) (void)hipStreamDestroy(copy_stream);
+    if (cold_stream) (void)hipStreamDestroy(cold_stream);
     if (d2h_stream) (void)hipStreamDestroy(d2h_stream);
     if (stream) (void)hipStreamDestroy(stream);
   }
@@ -448,6 +450,7 @@ gome_status gome_engine::init(const gome_config& c) {
   HIPCHK(hipStreamCreateWithFlags(&hot_stream, hipStreamNonBlocking));
   HIPCHK(hipStreamCreateWithFlags(&flow_stream, hipStreamNonBlocking));
   HIPCHK(hipStreamCreateWithFlags(&copy_stream, hipStreamNonBlocking));
+  HIPCHK(hipStreamCreateWithFlags(&cold_stream, hipStreamNonBlocking));
   if (const char* g = std::getenv("GOME_D2H_STREAM"); g && std::atoi(g) != 0)
     HIPCHK(hipStreamCreateWithFlags(&d2h_stream, hipStreamNonBlocking));
   for (hipEvent_t* ev : {&fork, &join, &joinf, &prep_h, &prep_t, &fork_adm, &adm_done, &seg_done,
@@ -994,11 +997,10 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   HIPCHK(hipEventRecord(prep_t, s));
   // the cold books (k_match) beside the tail's chain instead of before it: they share no book, only
   // the pools' atomics, and on deep books the cold kernel alone grew to 20 ms per batch (config 5 at
-  // step 200), which put the tail's plans and reconstruction behind it on the critical path.  On the
-  // copy stream: idle during device batches; on the host path it delays the next batch's H2D and
-  // the previous one's D2H by the cold kernel's time, well inside the batch (GOME_COLD_MAIN=1: the
-  // caller's stream, for A/B)
-  hipStream_t cst = cold_main ? s : copy_stream;
+  // step 200), which put the tail's plans and reconstruction behind it on the critical path.  On a
+  // stream of its own: on the copy stream it held the next batch's H2D behind it on the host path
+  // (config-2 e2e 5.2 -> 7.1 ms per batch).  GOME_COLD_MAIN=1: the caller's stream, for A/B
+  hipStream_t cst = cold_main ? s : cold_stream;
   if (cst != s) HIPCHK(hipStreamWaitEvent(cst, prep_t, 0));
   HIPCHK(hipEventRecord(S.evc0, cst));
   k_match<<<std::min<uint32_t>(ceil_div(grid, COLD_WAVES), COLD_BLOCKS), 64 * COLD_WAVES, COLD_LDS_BYTES, cst>>>(

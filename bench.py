@@ -405,7 +405,9 @@ def main():
     n_symbols = W["symbols"]
     steps, warm = args.steps, args.warmup
     e2e_steps = steps if args.e2e_steps < 0 else args.e2e_steps
-    e2e_warm = 2 if e2e_steps else 0
+    # (every batch slot once, and once more: the first pass over a slot sizes its page-locked
+    # event buffer, which two warm batches left for the third slot inside the timed region)
+    e2e_warm = GOME_MAX_INFLIGHT + 1 if e2e_steps else 0
     gen, share, top_share = make_stream(args.workload, rank, world, args.seed)
     per_rank = int(round(args.batch * world * share))
     note(f"{args.workload}: generating {warm + steps} batches of {per_rank} records")

@@ -261,7 +261,7 @@ struct gome_engine {
   hipStream_t hot_stream = nullptr;   // tail / near-head flow books, legacy hot kernel
   hipStream_t flow_stream = nullptr;  // the hottest book's plan (critical path)
   hipStream_t copy_stream = nullptr;  // H2D of records, D2H of events (pipelined path)
-  hipStream_t cold_stream = nullptr;  // the cold books (k_match) beside the tail's chain
+  hipStream_t cold_stream = nullptr;  // the cold books on a stream of their own (GOME_COLD_OWN=1; A/B)
   // D2H of collected events on a stream of their own (GOME_D2H_STREAM=1; off by default: with
   // four hardware queues per process a fifth stream shares one, and the e2e A/B measured it
   // 0.7 ms per config-2 batch slower with three batches in flight, no faster with two)
@@ -288,7 +288,8 @@ struct gome_engine {
   bool tail_serial = false;  // the split tail's events after its writes on one stream (GOME_TAIL_SERIAL: solo kernel times)
   int prep_wait = -1;  // k_prep after the head's prep always (1) / adaptive (-1; GOME_PREP_WAIT, A/B)
   bool adm_fast = true;
-  bool cold_main = false;  // k_match on the caller's stream (GOME_COLD_MAIN=1; default: cold_stream)
+  bool cold_main = false;  // k_match on the caller's stream (GOME_COLD_MAIN=1; default: the copy stream)
+  bool copy_busy = false;  // the batch being enqueued came by gome_submit_batch_async (H2D / D2H on the copy stream)
   // GOME_PH_* timing events (gome_stats.ms_phase): ~24 event records per batch, 0.12 ms on config 2's
   // critical path, so only on request (GOME_FLAG_PHASES, or GOME_PHASES=1)
   bool phases = false;  // k_adm_pre's fresh-batch test (GOME_ADM_FAST=0: every batch through the tables; A/B)
@@ -450,7 +451,6 @@ gome_status gome_engine::init(const gome_config& c) {
   HIPCHK(hipStreamCreateWithFlags(&hot_stream, hipStreamNonBlocking));
   HIPCHK(hipStreamCreateWithFlags(&flow_stream, hipStreamNonBlocking));
   HIPCHK(hipStreamCreateWithFlags(&copy_stream, hipStreamNonBlocking));
-  HIPCHK(hipStreamCreateWithFlags(&cold_stream, hipStreamNonBlocking));
   if (const char* g = std::getenv("GOME_D2H_STREAM"); g && std::atoi(g) != 0)
     HIPCHK(hipStreamCreateWithFlags(&d2h_stream, hipStreamNonBlocking));
   for (hipEvent_t* ev : {&fork, &join, &joinf, &prep_h, &prep_t, &fork_adm, &adm_done, &seg_done,
@@ -497,6 +497,8 @@ gome_status gome_engine::init(const gome_config& c) {
     cold_main = !q || std::atoi(q) < 8;
   }
   if (const char* g = std::getenv("GOME_COLD_MAIN")) cold_main = std::atoi(g) != 0;            // (A/B)
+  if (const char* g = std::getenv("GOME_COLD_OWN"); g && std::atoi(g) != 0)                   // (A/B)
+    HIPCHK(hipStreamCreateWithFlags(&cold_stream, hipStreamNonBlocking));
   phases = (cfg.flags & GOME_FLAG_PHASES) != 0;
   if (const char* g = std::getenv("GOME_PHASES")) phases = std::atoi(g) != 0;
   uint32_t ms = cfg.max_symbols;
@@ -997,10 +999,13 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   HIPCHK(hipEventRecord(prep_t, s));
   // the cold books (k_match) beside the tail's chain instead of before it: they share no book, only
   // the pools' atomics, and on deep books the cold kernel alone grew to 20 ms per batch (config 5 at
-  // step 200), which put the tail's plans and reconstruction behind it on the critical path.  On a
-  // stream of its own: on the copy stream it held the next batch's H2D behind it on the host path
-  // (config-2 e2e 5.2 -> 7.1 ms per batch).  GOME_COLD_MAIN=1: the caller's stream, for A/B
-  hipStream_t cst = cold_main ? s : cold_stream;
+  // step 200), which put the tail's plans and reconstruction behind it on the critical path.  On the
+  // copy stream, idle during device and synchronous batches.  Pipelined host batches keep the
+  // caller's stream: there the copy stream carries the next batch's H2D, which waited for the cold
+  // kernel (config-2 e2e 5.24 -> 6.9 ms per batch).  A stream of its own (GOME_COLD_OWN=1) measured
+  // slower at 4, 8 and 16 hardware queues (config 2: 2.3 -> 3.6 ms per batch).
+  // GOME_COLD_MAIN=1: the caller's stream always
+  hipStream_t cst = (cold_main || copy_busy) ? s : cold_stream ? cold_stream : copy_stream;
   if (cst != s) HIPCHK(hipStreamWaitEvent(cst, prep_t, 0));
   HIPCHK(hipEventRecord(S.evc0, cst));
   k_match<<<std::min<uint32_t>(ceil_div(grid, COLD_WAVES), COLD_BLOCKS), 64 * COLD_WAVES, COLD_LDS_BYTES, cst>>>(
@@ -1448,8 +1453,10 @@ gome_status gome_submit_batch_async(gome_engine* e, const gome_order* orders, si
     if (he == hipSuccess) he = hipStreamWaitEvent(e->stream, S.h2d, 0);
     if (he != hipSuccess) return e->fail(GOME_E_DEVICE, hipGetErrorString(he));
     // (no sort ahead here: on the copy stream it delayed the event copies; e2e +2 ms per config-3 batch)
-    if ((st = e->enqueue(S.d_orders, static_cast<uint32_t>(n), e->stream, sl, seq_base, inflight_n)) != GOME_OK)
-      return st;
+    e->copy_busy = true;
+    st = e->enqueue(S.d_orders, static_cast<uint32_t>(n), e->stream, sl, seq_base, inflight_n);
+    e->copy_busy = false;
+    if (st != GOME_OK) return st;
   }
   e->flights.push_back(Flight{sl, static_cast<uint32_t>(n), seq_base, false});
   return GOME_OK;

@@ -95,7 +95,9 @@ enum {
   C_WANT_DEEP, C_WANT_CANC,                               // flow candidates that asked for the deep /
                                                           // cancel chain (enqueued or not)
   C_QUIRK_CHECKED, C_REQUAL,                              // quirk books checked / requalified (k_requalify)
-  C_NCTR = 27
+  C_HEAD_ADD,                                             // the hottest book went through an ADD plan
+  C_EARLY, C_EARLY_MISS,                                  // its plan was the early one / could not be (match_early.h)
+  C_NCTR = 30
 };
 
 // Level blocks (a book's sorted level array) come in power-of-two capacities 16 << c.  A

@@ -38,6 +38,7 @@
 #include "match_flow.h"
 #include "match_flow_cancel.h"
 #include "match_flow_deep.h"
+#include "match_early.h"
 #include "match_hot.h"
 #include "match_requal.h"
 #include "pipeline.h"
@@ -231,6 +232,8 @@ struct Slot {
   uint32_t* d_dup = nullptr;       // batch indices of the ADDs rejected as duplicate oids (Q7)
   size_t h_cap = 0;
   hipEvent_t ev0{}, ev1{}, evm0{}, evm1{}, evh0{}, evh1{}, evf0{}, evf1{}, evc0{}, evc1{};
+  hipEvent_t evx0{}, evx1{};  // the early plan (match_early.h), when the batch enqueued one
+  bool early = false;
   hipEvent_t h2d{}, done{};
   hipEvent_t ph[GOME_NPHASE][2]{};  // GOME_PH_* phase brackets (ph_on: recorded this batch)
   bool ph_on[GOME_NPHASE]{};
@@ -262,12 +265,29 @@ struct gome_engine {
   hipStream_t flow_stream = nullptr;  // the hottest book's plan (critical path)
   hipStream_t copy_stream = nullptr;  // H2D of records, D2H of events (pipelined path)
   hipStream_t cold_stream = nullptr;  // the cold books on a stream of their own (GOME_COLD_OWN=1; A/B)
+  hipStream_t early_stream = nullptr; // the early plan's record work (match_early.h), beside the plan before it
   // D2H of collected events on a stream of their own (GOME_D2H_STREAM=1; off by default: with
   // four hardware queues per process a fifth stream shares one, and the e2e A/B measured it
   // 0.7 ms per config-2 batch slower with three batches in flight, no faster with two)
   hipStream_t d2h_stream = nullptr;
   hipEvent_t fork{}, join{}, joinf{}, prep_h{}, prep_t{}, fork_adm{}, adm_done{}, seg_done{};
   hipEvent_t dp_fork{}, cnt_fork{}, cnt_done{}, dw_done{}, dl_done{}, tl_done{};  // the hottest book's deep chain, k_flow_count beside its writes
+  // the early plan of the hottest book (match_early.h): the last batch's plan done (flow stream),
+  // its oid watermarks folded (hot stream), this batch's early prep and plan done (copy stream)
+  hipEvent_t plan_done{}, oidmax_done{}, xpre_done{}, xprep_done{}, xplan_done{};
+  struct XBuf {
+    XCtl* ctl = nullptr;
+    FlowHdr* hdr = nullptr;
+    FlowLvl* lvl = nullptr;
+    unsigned long long* ord8 = nullptr;
+    Touch* log = nullptr;
+  } xb[2];                         // by batch parity (the next batch's chain runs beside this one's take)
+  FlPrepScr* x_pscr = nullptr;
+  uint32_t *x_adm = nullptr, *x_evc = nullptr;  // predicted verdicts; the early prep_c's ev_count sink
+  uint32_t *x_cnt = nullptr, *x_seg = nullptr, *x_sidx = nullptr;  // the hot symbol's records (k_x_*)
+  bool early_on = true;            // GOME_EARLY=0: never
+  uint32_t head_add = 0;           // bit 0 / 1: the last / the one before finished batch's hottest book took an ADD plan
+  uint32_t bid = 0;                // batches enqueued (FlowArgs::bid)
   Slot slots[GOME_MAX_INFLIGHT];
   uint32_t next_slot = 0;
   std::deque<Flight> flights;
@@ -365,20 +385,22 @@ struct gome_engine {
   ~gome_engine() {
     if (stream) (void)hipStreamSynchronize(stream);
     if (copy_stream) (void)hipStreamSynchronize(copy_stream);
+    if (early_stream) (void)hipStreamSynchronize(early_stream);
     for (void* p : allocs) (void)hipFree(p);
     for (void* p : host_allocs) (void)hipHostFree(p);
     for (Slot& S : slots) {
       if (S.h_st) (void)hipHostFree(S.h_st);
       if (S.h_events) (void)hipHostFree(S.h_events);
       for (hipEvent_t ev : {S.ev0, S.ev1, S.evm0, S.evm1, S.evh0, S.evh1, S.evf0, S.evf1, S.evc0, S.evc1, S.h2d, S.done,
-                            S.sorted})
+                            S.sorted, S.evx0, S.evx1})
         if (ev) (void)hipEventDestroy(ev);
       for (auto& pr : S.ph)
         for (hipEvent_t ev : pr)
           if (ev) (void)hipEventDestroy(ev);
     }
     for (hipEvent_t ev : {fork, join, joinf, prep_h, prep_t, fork_adm, adm_done, seg_done, dp_fork, cnt_fork, cnt_done,
-                          dw_done, dl_done, tl_done, tob_done})
+                          dw_done, dl_done, tl_done, tob_done, plan_done, oidmax_done, xpre_done, xprep_done,
+                          xplan_done})
       if (ev) (void)hipEventDestroy(ev);
     if (h_tob_syms) (void)hipHostFree(h_tob_syms);
     if (h_tob) (void)hipHostFree(h_tob);
@@ -386,6 +408,7 @@ struct gome_engine {
     if (flow_stream) (void)hipStreamDestroy(flow_stream);
     if (copy_stream) (void)hipStreamDestroy(copy_stream);
     if (cold_stream) (void)hipStreamDestroy(cold_stream);
+    if (early_stream) (void)hipStreamDestroy(early_stream);
     if (d2h_stream) (void)hipStreamDestroy(d2h_stream);
     if (stream) (void)hipStreamDestroy(stream);
   }
@@ -454,10 +477,12 @@ gome_status gome_engine::init(const gome_config& c) {
   if (const char* g = std::getenv("GOME_D2H_STREAM"); g && std::atoi(g) != 0)
     HIPCHK(hipStreamCreateWithFlags(&d2h_stream, hipStreamNonBlocking));
   for (hipEvent_t* ev : {&fork, &join, &joinf, &prep_h, &prep_t, &fork_adm, &adm_done, &seg_done,
-                         &dp_fork, &cnt_fork, &cnt_done, &dw_done, &dl_done, &tl_done, &tob_done})
+                         &dp_fork, &cnt_fork, &cnt_done, &dw_done, &dl_done, &tl_done, &tob_done, &plan_done,
+                         &oidmax_done, &xpre_done, &xprep_done, &xplan_done})
     HIPCHK(hipEventCreateWithFlags(ev, hipEventDisableTiming));
   for (Slot& S : slots) {
-    for (hipEvent_t* ev : {&S.ev0, &S.ev1, &S.evm0, &S.evm1, &S.evh0, &S.evh1, &S.evf0, &S.evf1, &S.evc0, &S.evc1})
+    for (hipEvent_t* ev : {&S.ev0, &S.ev1, &S.evm0, &S.evm1, &S.evh0, &S.evh1, &S.evf0, &S.evf1, &S.evc0, &S.evc1,
+                           &S.evx0, &S.evx1})
       HIPCHK(hipEventCreate(ev));
     for (auto& pr : S.ph)
       for (hipEvent_t& ev : pr) HIPCHK(hipEventCreate(&ev));
@@ -600,6 +625,20 @@ gome_status gome_engine::init(const gome_config& c) {
   if (!alloc(&F.tcnt, static_cast<size_t>(FL_HEAD) * F.maxt * FL_CAP, "flow head tile counts") ||
       !alloc(&F.pscr, FL_HEAD, "flow head prep scratch"))
     return GOME_E_CAPACITY;
+  // the early plan's buffers (match_early.h): by batch parity the control block, header, levels,
+  // packed records and log of one book; shared its prep scratch and verdicts
+  for (XBuf& X : xb)
+    if (!alloc(&X.ctl, 1, "early control") || !alloc(&X.hdr, 1, "early header") ||
+        !alloc(&X.lvl, FL_CAP, "early levels") || !alloc(&X.ord8, nb + FL_ORD8_PAD, "early records") ||
+        !alloc(&X.log, ntouch, "early touch log"))
+      return GOME_E_CAPACITY;
+  if (!alloc(&x_pscr, 1, "early prep scratch") || !alloc(&x_adm, nb, "early verdicts") ||
+      !alloc(&x_evc, nb, "early event counts") || !alloc(&x_cnt, 2 * X_FIND_B, "early block counts") ||
+      !alloc(&x_seg, 3, "early segment") || !alloc(&x_sidx, nb, "early permutation"))
+    return GOME_E_CAPACITY;
+  for (XBuf& X : xb) HIPCHK(hipMemsetAsync(X.ctl, 0, sizeof(XCtl), stream));
+  if (const char* g = std::getenv("GOME_EARLY")) early_on = std::atoi(g) != 0;
+  if (early_on) HIPCHK(hipStreamCreateWithFlags(&early_stream, hipStreamNonBlocking));
   // books with DELs (match_flow_cancel.h): per-position scratch, the (symbol, oid)
   // table (generation-tagged: cleared once per 2048 batches)
   fc_hcap = next_pow2(std::max<unsigned long long>(2ull * nb, 1024));
@@ -709,6 +748,12 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   // A/B: config 3 -0.1..0.2 ms, config 2 +0.02 ms)
   const bool dominant = !(last_maxseg * 16 < last_n);
   hipStream_t ss = (ahead && sort_ahead && dominant) ? copy_stream : s;
+  // the hottest book planned early on the copy stream (match_early.h): pipelined device batches
+  // after a batch whose hottest book took an ADD plan (the device checks the rest)
+  const bool early = early_on && ahead && dominant && head_add != 0 && bid > 0 && F.enabled;
+  S.early = early;
+  const uint32_t bid_prev = bid;
+  F.bid = ++bid;
   // per-batch status reset (free_top / freed_top and the level pools persist); admission
   // (flow stream) starts from fork_adm, beside the sort when both are on the caller's stream
   auto status_reset = [&]() -> hipError_t {
@@ -756,6 +801,44 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
     HIPCHK(hipStreamWaitEvent(s, S.sorted, 0));
   }
   k_sort_status<<<1, 1, 0, s>>>(d_st, S.sst);
+
+  // ---- the early plan of the hottest book (match_early.h), on the copy stream: its records and
+  // verdicts and the batch's prices of it now, the price set, records and plan as soon as the last
+  // batch's plan is done (plan_done)
+  XBuf& X = xb[bid & 1];
+  FlowArgs FX = F;
+  FX.hdr = X.hdr; FX.lvl = X.lvl; FX.ord8 = X.ord8; FX.log = X.log; FX.pscr = x_pscr;
+  FX.xlog = 1; FX.h0 = 0; FX.h1 = 1; FX.tb = 0; FX.mb = 0; FX.chains = 0;
+  if (early) {
+    // the records, verdicts and prices on the early stream (the copy stream is still running the
+    // last batch's early plan), the rest after both on the copy stream
+    hipStream_t es = early_stream, ps = copy_stream;
+    Dev Dx = D;
+    Dx.st = reinterpret_cast<Status*>(reinterpret_cast<char*>(X.ctl) + offsetof(XCtl, st));
+    BatchArgs Bx{};
+    Bx.ord = d_ord; Bx.n = n; Bx.seg_order = x_seg; Bx.seg_start = x_seg + 1; Bx.sidx = x_sidx;
+    Bx.adm_flag = x_adm; Bx.ev_count = x_evc; Bx.seq_base = seq_base;
+    const uint32_t xn = std::min<uint32_t>(X_FIND_B, std::max<uint32_t>(1u, ceil_div(n, 4096u)));
+    HIPCHK(hipStreamWaitEvent(es, prep_h, 0));  // (the last batch's head prep: F.hdr[0] names its book)
+    HIPCHK(hipMemsetAsync(X.ctl, 0, sizeof(XCtl), es));
+    HIPCHK(hipMemsetAsync(x_pscr, 0, sizeof(FlPrepScr), es));
+    k_x_count<<<xn, X_FIND_T, 0, es>>>(d_ord, n, F.hdr, bid_prev, x_cnt);
+    k_x_scan<<<1, X_FIND_B, 0, es>>>(F.hdr, bid_prev, x_cnt, xn, x_seg, X.ctl);
+    k_x_scatter<<<xn, X_FIND_T, 0, es>>>(d_ord, n, F.hdr, bid_prev, x_cnt, x_seg, X.ctl, x_sidx);
+    HIPCHK(hipStreamWaitEvent(es, oidmax_done, 0));  // (the last batch's oid watermarks)
+    k_x_adm<<<256, 256, 0, es>>>(Bx, X.ctl, d_oid_max, cfg.max_symbols, x_adm);
+    k_flow_prep_a<<<dim3(FL_PG, 1), FL_PREP_T, 0, es>>>(Dx, Bx, FX);
+    HIPCHK(hipEventRecord(xpre_done, es));
+    HIPCHK(hipStreamWaitEvent(ps, xpre_done, 0));
+    HIPCHK(hipStreamWaitEvent(ps, plan_done, 0));
+    k_x_prep_b<<<1, FL_PREP_T, 0, ps>>>(Bx, FX, F, X.ctl, bid_prev);
+    k_flow_prep_c<<<dim3(FL_PG, 1), FL_PREP_T, 0, ps>>>(Dx, Bx, FX);
+    HIPCHK(hipEventRecord(xprep_done, ps));
+    HIPCHK(hipEventRecord(S.evx0, ps));
+    k_flow_plan_head<<<1, 256, plan_lds, ps>>>(Dx, FX);
+    HIPCHK(hipEventRecord(S.evx1, ps));
+    HIPCHK(hipEventRecord(xplan_done, ps));
+  }
 
   // admission markers depend on the input records only: they run on the flow stream beside
   // the validation, the radix sort and the segmentation (the batch's critical path), enqueued
@@ -834,6 +917,7 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   }
   HIPCHK(hipEventRecord(seg_done, s));
   HIPCHK(hipStreamWaitEvent(flow_stream, seg_done, 0));
+  if (early) HIPCHK(hipStreamWaitEvent(flow_stream, xprep_done, 0));  // (it read F.hdr[0] / F.lvl)
   HIPCHK(hipMemsetAsync(F.pscr, 0, sizeof(FlPrepScr) * FL_HEAD, flow_stream));
   HIPCHK(mark(GOME_PH_HEAD_PREP, 0, flow_stream));
   k_flow_prep_a<<<dim3(FL_PG, nh_head), FL_PREP_T, 0, flow_stream>>>(D, B, FH);
@@ -894,9 +978,16 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   if (c_canc) cancel_prep(FH, nh_head, FL_PG, true, flow_stream);
   HIPCHK(mark(GOME_PH_HEAD_PREP, 1, flow_stream));
   HIPCHK(hipEventRecord(prep_h, flow_stream));
+  if (early) {  // the early inputs against this prep's, then the early plan taken (or not)
+    k_x_cmp<<<256, 256, 0, flow_stream>>>(D, F, FX, X.ctl);
+    HIPCHK(hipStreamWaitEvent(flow_stream, xplan_done, 0));
+    k_x_take<<<1, 128, 0, flow_stream>>>(D, F, FX, X.ctl);
+  }
   HIPCHK(hipEventRecord(S.evf0, flow_stream));
-  k_flow_plan_head<<<1, 256, plan_lds, flow_stream>>>(D, FH0);
+  k_flow_plan_head<<<1, 256, plan_lds, flow_stream>>>(D, FH0);  // (a book planned early: nothing)
   HIPCHK(hipEventRecord(S.evf1, flow_stream));
+  HIPCHK(hipEventRecord(plan_done, flow_stream));
+  if (early) k_x_logcopy<<<1024, 256, 0, flow_stream>>>(F, FX, X.ctl);
   // the other head books' plans need only the head's prep: each takes a whole CU, so they go
   // first, before the tail's prep and plans spread their waves over every CU
   HIPCHK(hipStreamWaitEvent(hot_stream, prep_h, 0));
@@ -1003,9 +1094,9 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   // copy stream, idle during device and synchronous batches.  Pipelined host batches keep the
   // caller's stream: there the copy stream carries the next batch's H2D, which waited for the cold
   // kernel (config-2 e2e 5.24 -> 6.9 ms per batch).  A stream of its own (GOME_COLD_OWN=1) measured
-  // slower at 4, 8 and 16 hardware queues (config 2: 2.3 -> 3.6 ms per batch).
-  // GOME_COLD_MAIN=1: the caller's stream always
-  hipStream_t cst = (cold_main || copy_busy) ? s : cold_stream ? cold_stream : copy_stream;
+  // slower at 4, 8 and 16 hardware queues (config 2: 2.3 -> 3.6 ms per batch).  A batch
+  // with an early plan keeps the copy stream for it.  GOME_COLD_MAIN=1: the caller's stream always
+  hipStream_t cst = (cold_main || copy_busy || early) ? s : cold_stream ? cold_stream : copy_stream;
   if (cst != s) HIPCHK(hipStreamWaitEvent(cst, prep_t, 0));
   HIPCHK(hipEventRecord(S.evc0, cst));
   k_match<<<std::min<uint32_t>(ceil_div(grid, COLD_WAVES), COLD_BLOCKS), 64 * COLD_WAVES, COLD_LDS_BYTES, cst>>>(
@@ -1068,6 +1159,7 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   k_pend_apply<<<dim3(8, 64), 256, 0, hot_stream>>>(D, d_pend, S.seg_start, S.seg_order, B);
   // oid watermarks for the next batches' duplicate-oid probe (the hot stream has slack here)
   k_oid_max<<<gN, T256, 0, hot_stream>>>(n, skeys, d_prep, d_oid_max);
+  HIPCHK(hipEventRecord(oidmax_done, hot_stream));
   if (nh_tail && split_tail && !tail_serial) {  // the tail's events beside its writes (arena; k_publish places them)
     HIPCHK(hipStreamWaitEvent(hot_stream, tl_done, 0));
     k_flow_events_fused_w<<<ceil_div(tail_grid * FL_EV_T, FL_WRITE_T), FL_WRITE_T, 0, hot_stream>>>(D, B, FT);
@@ -1131,7 +1223,11 @@ gome_status gome_engine::finish(uint32_t sl, uint32_t n) {
   (void)hipEventElapsedTime(&ms_total, S.ev0, S.ev1);
   (void)hipEventElapsedTime(&ms_match, S.evm0, S.evm1);
   (void)hipEventElapsedTime(&ms_hot, S.evh0, S.evh1);
-  (void)hipEventElapsedTime(&ms_flow, S.evf0, S.evf1);
+  if (S.early && st.ctr[C_EARLY]) (void)hipEventElapsedTime(&ms_flow, S.evx0, S.evx1);
+  else (void)hipEventElapsedTime(&ms_flow, S.evf0, S.evf1);
+  head_add = ((head_add << 1) | (st.ctr[C_HEAD_ADD] != 0 ? 1u : 0u)) & 3u;
+  stats.n_early = st.ctr[C_EARLY];
+  stats.n_early_miss = st.ctr[C_EARLY_MISS];
   stats.ms_hot = ms_hot;
   stats.ms_flow_plan = ms_flow;
   stats.n_flow_books = st.ctr[C_FLOW_BOOKS];

@@ -1,0 +1,346 @@
+// match_early.h — the hottest book's plan started right after the previous batch's plan.
+//
+// One wavefront plans the hottest book (k_flow_plan_head) and bounds the batch; everything else
+// runs beside it.  But between two batches' plans the pipeline put ~1.1 ms of serial work on
+// config 3: the previous batch's reconstruction and publish, then the next batch's sort,
+// admission and head prep.  The plan needs none of it: a book's plan reads only its level
+// aggregates (price, depth, side: the plan's own final state, FlowHdr / FlowLvl) and the batch's
+// packed records of that book.  So for a pipelined device batch (gome_submit_batch_device_async)
+// whose hottest book was also the previous batch's hottest book on an ADD plan, the engine
+// prepares and plans that book on the copy stream as soon as the previous plan ends:
+//
+//   k_x_count / k_x_scan / k_x_scatter  the records of the previous batch's hottest symbol, in
+//                batch order, at the positions the batch's stable sort will give them (the sort
+//                itself stays on the caller's stream, off the critical path)
+//   k_x_adm      their admission verdicts as k_adm will give them (an ADD alone with its (S, oid)
+//                in the batch, oid above the book's oid_max: its own verdict, pipeline.h); any
+//                DEL, ignored action or oid out of order declines the early plan
+//   k_flow_prep_a  the batch's prices and volume gcd / sum of the book (the head prep's own kernel)
+//   -- the previous batch's plan ends (plan_done) --
+//   k_x_prep_b   the price set: the previous plan's final levels (F.hdr[0] / F.lvl, that batch's
+//                header: FlowHdr::bid) plus the batch's prices; rank, the 32-bit test, XH / XL
+//   k_flow_prep_c  the packed records (into X.ord8), k_flow_plan_head (X.log, FlowArgs::xlog)
+//
+// The batch's own pipeline still prepares the book as before (k_flow_prep_a/b/c into F).  Then
+// k_x_cmp checks that the early inputs equal the normal ones (header, levels, every packed record:
+// the verdicts were predicted, the prices taken from the plan's state instead of the level pool),
+// and k_x_take, once the early plan is done, copies its outputs (final depths, side masks, touch
+// count) into F and marks the header `pre`, so k_flow_plan_head leaves the book alone; the log
+// follows (k_x_logcopy) and the reconstruction runs unchanged.  Anything that differs, or an early
+// plan that was declined, leaves the normal plan to run: the early plan can cost time, never
+// change a result.  gome_stats.n_early_miss counts early plans that were ready but not taken.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "match_flow.h"
+
+namespace gome {
+
+struct XCtl {
+  uint32_t ok;     // k_x_prep_b accepted: XH / XL / X.ord8 describe the batch's hottest book
+  uint32_t bad;    // k_x_adm: a record the prediction does not cover
+  uint32_t mism;   // k_x_cmp: the early inputs differ from the batch's own prep
+  uint32_t used;   // k_x_take: the early plan is the book's plan
+  Status st;       // the early kernels' Dev::st (nhot: 1 = plan the hottest segment, 0 = skip; err)
+};
+
+constexpr uint32_t X_FIND_T = 256, X_FIND_B = 1024;  // k_x_count / k_x_scatter: blocks of contiguous records
+
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t x) { return rl(wave_incl_scan_u32(x), 63); }
+
+// The previous batch's hottest book (its header: an ADD plan of batch bid_prev), or NIL.
+__device__ __forceinline__ uint32_t x_hot_sym(const FlowHdr* hdr, uint32_t bid_prev) {
+  const FlowHdr h = hdr[0];
+  return (h.ok == FL_OK_ADD && h.bid == bid_prev) ? h.sym : NIL;
+}
+
+__device__ __forceinline__ void x_range(uint32_t n, uint32_t& r0, uint32_t& r1) {
+  const uint32_t per = (n + gridDim.x - 1) / gridDim.x;
+  r0 = min(n, blockIdx.x * per);
+  r1 = min(n, r0 + per);
+}
+
+// Per block: records of the hot symbol, and records of lower symbols (the segment's start).
+__global__ __launch_bounds__(X_FIND_T) void k_x_count(const gome_order* ord, uint32_t n, const FlowHdr* hdr,
+                                                      uint32_t bid_prev, uint32_t* cnt) {
+  const uint32_t hs = x_hot_sym(hdr, bid_prev);
+  uint32_t r0, r1;
+  x_range(n, r0, r1);
+  uint32_t c = 0, lt = 0;
+  if (hs != NIL)
+    for (uint32_t i = r0 + threadIdx.x; i < r1; i += X_FIND_T) {
+      const uint32_t sy = ord[i].symbol_id;
+      c += sy == hs ? 1u : 0u;
+      lt += sy < hs ? 1u : 0u;
+    }
+  c = wave_sum_u32(c);
+  lt = wave_sum_u32(lt);
+  __shared__ uint32_t sc[X_FIND_T / 64], sl[X_FIND_T / 64];
+  if (lane_id() == 0) { sc[threadIdx.x >> 6] = c; sl[threadIdx.x >> 6] = lt; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t a = 0, b = 0;
+    for (uint32_t w = 0; w < X_FIND_T / 64; ++w) { a += sc[w]; b += sl[w]; }
+    cnt[blockIdx.x] = a;
+    cnt[gridDim.x + blockIdx.x] = b;
+  }
+}
+
+// Exclusive scan of the blocks' counts; the segment [beg, end) the stable sort will give the hot
+// symbol (xseg = {0, beg, end}: seg_order / seg_start of a one-segment batch), and st.nhot = 1 when
+// it is a flow candidate.  One block of X_FIND_B threads.
+__global__ __launch_bounds__(X_FIND_B) void k_x_scan(const FlowHdr* hdr, uint32_t bid_prev, uint32_t* cnt,
+                                                     uint32_t nblk, uint32_t* xseg, XCtl* X) {
+  __shared__ uint32_t part[X_FIND_B / 64], lts[X_FIND_B / 64];
+  const uint32_t t = threadIdx.x;
+  const uint32_t c = t < nblk ? cnt[t] : 0u, lt = t < nblk ? cnt[nblk + t] : 0u;
+  const uint32_t inc = wave_incl_scan_u32(c), ls = wave_sum_u32(lt);
+  if (lane_id() == 63) part[t >> 6] = inc;
+  if (lane_id() == 0) lts[t >> 6] = ls;
+  __syncthreads();
+  uint32_t before = 0, beg = 0, tot = 0;
+  for (uint32_t w = 0; w < X_FIND_B / 64; ++w) {
+    if (w < (t >> 6)) before += part[w];
+    beg += lts[w];
+    tot += part[w];
+  }
+  if (t < nblk) cnt[t] = before + inc - c;
+  if (t == 0) {
+    xseg[0] = 0;
+    xseg[1] = beg;
+    xseg[2] = beg + tot;
+    X->st.nhot = (x_hot_sym(hdr, bid_prev) != NIL && tot >= (1u << FLOW_MIN_LOG2)) ? 1u : 0u;
+  }
+}
+
+// xsidx[beg + rank] = batch index of the hot symbol's rank-th record (batch order): the slice of
+// the stable sort's permutation that covers the segment.
+__global__ __launch_bounds__(X_FIND_T) void k_x_scatter(const gome_order* ord, uint32_t n, const FlowHdr* hdr,
+                                                        uint32_t bid_prev, const uint32_t* cnt, const uint32_t* xseg,
+                                                        const XCtl* X, uint32_t* xsidx) {
+  if (X->st.nhot == 0) return;
+  const uint32_t hs = x_hot_sym(hdr, bid_prev);
+  uint32_t r0, r1;
+  x_range(n, r0, r1);
+  __shared__ uint32_t wc[X_FIND_T / 64];
+  uint32_t base = xseg[1] + cnt[blockIdx.x];
+  const uint32_t w = threadIdx.x >> 6;
+  for (uint32_t c0 = r0; c0 < r1; c0 += X_FIND_T) {
+    const uint32_t i = c0 + threadIdx.x;
+    const bool m = i < r1 && ord[i].symbol_id == hs;
+    const unsigned long long bm = __ballot(m);
+    if (lane_id() == 0) wc[w] = __popcll(bm);
+    __syncthreads();
+    uint32_t off = 0, all = 0;
+    for (uint32_t k = 0; k < X_FIND_T / 64; ++k) {
+      off += k < w ? wc[k] : 0u;
+      all += wc[k];
+    }
+    if (m) xsidx[base + off + __popcll(bm & lt_mask())] = i;
+    base += all;
+    __syncthreads();
+  }
+}
+
+// The verdicts k_adm will give the hottest segment's records, when they are all ADDs whose oids
+// rise in batch order above the book's oid_max: such a key is alone in the batch and rests
+// nowhere, so on both admission paths (fresh batch or the tables) its verdict is its own.
+__global__ void k_x_adm(BatchArgs Bx, XCtl* X, const uint32_t* oid_max, uint32_t max_symbols, uint32_t* xadm) {
+  if (X->st.nhot == 0) return;
+  const uint32_t seg = Bx.seg_order[0];
+  const uint32_t beg = Bx.seg_start[seg], end = Bx.seg_start[seg + 1];
+  const uint32_t sym = Bx.ord[Bx.sidx[beg]].symbol_id;
+  if (sym >= max_symbols) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) X->bad = 1;
+    return;
+  }
+  const uint32_t om = oid_max[sym];
+  bool bad = false;
+  for (uint32_t b = beg + blockIdx.x * blockDim.x + threadIdx.x; b < end; b += gridDim.x * blockDim.x) {
+    const uint32_t j = Bx.sidx[b];
+    const gome_order o = Bx.ord[j];
+    const uint32_t prev = b == beg ? om : Bx.ord[Bx.sidx[b - 1]].oid_id;
+    if (o.action != GOME_ADD || o.oid_id <= prev) bad = true;
+    xadm[j] = (!(o.flags & GOME_ORD_ADM_HOST) || (o.flags & GOME_ORD_ADMITTED)) ? ADM_V_YES : ADM_V_NO;
+  }
+  if (__any(bad) && lane_id() == 0) atomicOr(&X->bad, 1u);
+}
+
+// The early head prep's price set and header (k_flow_prep_b's, with the book's live levels taken
+// from the previous batch's plan instead of the level pool).  F: the pipeline's own flow args
+// (F.hdr[0] / F.lvl: the previous batch's hottest book after its plan, header of batch bid_prev).
+__global__ __launch_bounds__(FL_PREP_T) void k_x_prep_b(BatchArgs Bx, FlowArgs FX, FlowArgs F, XCtl* X,
+                                                        uint32_t bid_prev) {
+  __shared__ unsigned long long hkey[FL_HASH];
+  __shared__ uint32_t hval[FL_HASH];
+  __shared__ unsigned long long ckey[FL_CAP + FL_PREP_T];
+  __shared__ uint32_t cslot[FL_CAP + FL_PREP_T];
+  __shared__ uint32_t ndist, nc, bad;
+  __shared__ unsigned long long wg[FL_PREP_T / 64], ws[FL_PREP_T / 64];
+  const uint32_t tid = threadIdx.x;
+  FlowHdr* hd = &FX.hdr[0];
+  FlPrepScr* P = FX.pscr;
+  const FlowHdr ph = F.hdr[0];
+  const uint32_t seg = Bx.seg_order[0];
+  const uint32_t beg = Bx.seg_start[seg], end = Bx.seg_start[seg + 1];
+  if (tid == 0) {
+    ndist = nc = 0;
+    bad = (X->st.nhot == 0 || X->bad || P->bad || P->many || P->dels || ph.ok != FL_OK_ADD || ph.bid != bid_prev ||
+           ph.sym != Bx.ord[Bx.sidx[beg]].symbol_id || (end - beg) >= FL_MAX_ORDERS || ph.nl > FL_MAX)
+              ? 1u : 0u;
+  }
+  __syncthreads();
+  if (bad) {
+    if (tid == 0) { hd->ok = 0; X->st.nhot = 0; }
+    return;
+  }
+  uint32_t my_n = 0;
+  for (uint32_t i = tid; i < FL_HASH; i += FL_PREP_T) {
+    hkey[i] = P->key[i];
+    hval[i] = NIL;
+    my_n += hkey[i] ? 1u : 0u;
+  }
+  if (my_n) atomicAdd(&ndist, my_n);
+  __syncthreads();
+  // the previous plan's live levels: side from its final masks, depth from dfin
+  const FlowLvl* LP = F.lvl;
+  unsigned long long mg = 0, msum = 0;
+  if (tid < FL_PG) {
+    mg = P->pg[tid];
+    msum = P->ps[tid];
+  }
+  for (uint32_t q = 1 + tid; q <= ph.nl; q += FL_PREP_T) {
+    const bool sa = ((q < 64 ? ph.amask[0] >> q : ph.amask[1] >> (q - 64)) & 1ull) != 0;
+    const bool sb = ((q < 64 ? ph.bmask[0] >> q : ph.bmask[1] >> (q - 64)) & 1ull) != 0;
+    const int64_t d = LP[q].dfin;
+    if (!sa && !sb) {
+      if (d != 0) bad = 1;
+      continue;
+    }
+    if ((sa && sb) || d <= 0) { bad = 1; continue; }
+    mg = fl_gcd(mg, static_cast<unsigned long long>(d));
+    msum = min(msum + static_cast<unsigned long long>(d), FL_SUM_CAP);
+    bool fresh;
+    const uint32_t sl = fl_set_put(hkey, static_cast<unsigned long long>(LP[q].price) + FL_KEY_OFF, &fresh);
+    if (sl == FL_HASH) { bad = 1; continue; }
+    hval[sl] = q;
+    if (fresh) atomicAdd(&ndist, 1u);
+  }
+  fl_block_gcd_sum(mg, msum, wg, ws);  // (synchronises the block)
+  if (bad || ndist > FL_MAX) {
+    if (tid == 0) { hd->ok = 0; X->st.nhot = 0; }
+    return;
+  }
+  for (uint32_t sl = tid; sl < FL_HASH; sl += FL_PREP_T) {
+    if (hkey[sl]) {
+      const uint32_t i = atomicAdd(&nc, 1u);
+      ckey[i] = hkey[sl];
+      cslot[i] = sl;
+    }
+  }
+  __syncthreads();
+  const uint32_t n = nc;
+  FlowLvl* LV = FX.lvl;
+  if (tid < n) {
+    const unsigned long long key = ckey[tid];
+    uint32_t r = 0;
+    for (uint32_t i = 0; i < n; ++i) r += ckey[i] < key ? 1u : 0u;
+    const uint32_t sl = cslot[tid], q = hval[sl];
+    FlowLvl f{};
+    f.price = static_cast<int64_t>(key - FL_KEY_OFF);
+    f.old = q;  // (the previous plan's level index: informational)
+    f.head = f.tail = NIL;
+    if (q != NIL) {
+      const bool sa = ((q < 64 ? ph.amask[0] >> q : ph.amask[1] >> (q - 64)) & 1ull) != 0;
+      f.d0 = LP[q].dfin;
+      f.mem0 = sa ? M_SALE : M_BUY;
+    }
+    LV[r + 1] = f;
+    hval[sl] = r + 1;
+  }
+  __syncthreads();
+  for (uint32_t i = tid; i < FL_HASH; i += FL_PREP_T) {
+    P->key[i] = hkey[i];
+    P->val[i] = hval[i];
+  }
+  unsigned long long g = mg ? mg : 1;
+  const bool w32 = msum < FL_SUM_CAP && msum / g < (1ull << 32);
+  if (!w32) g = 1;
+  if (tid < ((8u - ((end - beg) & 7u)) & 7u))  // padding to whole half-groups (8 records)
+    FX.ord8[(end - beg) + tid] = fl_rec(false, 0, 0, false, end - beg + tid, w32);
+  if (tid == 0) {
+    FlowHdr x{};
+    x.ok = FL_OK_ADD;
+    x.nl = n;
+    x.sym = ph.sym;
+    x.beg = beg;
+    x.end = end;
+    x.adds = P->adds;
+    x.dropped = P->dropped;
+    x.obase = 0;
+    x.w32 = w32 ? 1u : 0u;
+    x.g = g;
+    *hd = x;
+    X->ok = 1;
+  }
+}
+
+// The early inputs against the batch's own head prep of the same book: header, levels, every
+// packed record (a grid of blocks; block 0 also takes the header and the levels).
+__global__ void k_x_cmp(Dev D, FlowArgs F, FlowArgs FX, XCtl* X) {
+  if (!X->ok) return;
+  const FlowHdr hd = F.hdr[0], xh = FX.hdr[0];
+  bool diff = D.st->nhot == 0 || hd.ok != FL_OK_ADD || xh.ok != FL_OK_ADD || hd.bid != F.bid || hd.nl != xh.nl ||
+              hd.sym != xh.sym || hd.beg != xh.beg || hd.end != xh.end || hd.adds != xh.adds ||
+              hd.dropped != xh.dropped || hd.w32 != xh.w32 || hd.g != xh.g || hd.ndel != 0;
+  if (!diff) {
+    if (blockIdx.x == 0)
+      for (uint32_t q = 1 + threadIdx.x; q <= hd.nl; q += blockDim.x) {
+        const FlowLvl& a = F.lvl[q];
+        const FlowLvl& b = FX.lvl[q];
+        if (a.price != b.price || a.d0 != b.d0 || a.mem0 != b.mem0) diff = true;
+      }
+    const uint32_t m = ((hd.end - hd.beg) + 7u) & ~7u;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < m; i += gridDim.x * blockDim.x)
+      if (F.ord8[hd.obase + i] != FX.ord8[i]) diff = true;
+  }
+  if (__any(diff) && lane_id() == 0) atomicOr(&X->mism, 1u);
+}
+
+// After the early plan: take it (its final depths, side masks and touch count into F, the header
+// marked `pre`) when its inputs matched and it ran clean.
+__global__ void k_x_take(Dev D, FlowArgs F, FlowArgs FX, XCtl* X) {
+  __shared__ uint32_t use;
+  const FlowHdr xh = FX.hdr[0];
+  if (threadIdx.x == 0) {
+    const bool normal = D.st->nhot != 0 && F.hdr[0].ok == FL_OK_ADD;
+    use = (X->ok && !X->mism && X->st.err == 0 && normal) ? 1u : 0u;
+    // (a batch whose hottest book is another symbol than the last one's plans it normally)
+    if (!use && normal && X->ok && F.hdr[0].sym == xh.sym) ctr_add(D, C_EARLY_MISS, 1ull);
+  }
+  __syncthreads();
+  if (!use) return;
+  for (uint32_t q = 1 + threadIdx.x; q <= xh.nl; q += blockDim.x) F.lvl[q].dfin = FX.lvl[q].dfin;
+  if (threadIdx.x == 0) {
+    FlowHdr* w = &F.hdr[0];
+    w->ntouch = xh.ntouch;
+    w->amask[0] = xh.amask[0];
+    w->amask[1] = xh.amask[1];
+    w->bmask[0] = xh.bmask[0];
+    w->bmask[1] = xh.bmask[1];
+    w->pre = 1;
+    X->used = 1;
+    ctr_add(D, C_EARLY, 1ull);
+  }
+}
+
+// The early plan's touch log to where the reconstruction reads the book's log.
+__global__ void k_x_logcopy(FlowArgs F, FlowArgs FX, const XCtl* X) {
+  if (!X->used) return;
+  const FlowHdr xh = FX.hdr[0];
+  const uint4* src = reinterpret_cast<const uint4*>(FX.log);
+  uint4* dst = reinterpret_cast<uint4*>(F.log + static_cast<size_t>(FL_TOUCH_MUL) * xh.beg);
+  for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < xh.ntouch; t += gridDim.x * blockDim.x) dst[t] = src[t];
+}
+
+}  // namespace gome

@@ -138,7 +138,8 @@ struct FlowHdr {
   uint32_t nbsum;      // books with DELs: the DEL windows' total (the cancel prep's C loops)
   uint32_t dc;         // a deep book whose segment holds DELs (the W32DC plan)
   uint32_t dv_ba;      // W32DV: the best ask after the plan (asks lie at or above it)
-  uint32_t pad3[2];
+  uint32_t pre;        // planned early (match_early.h): k_flow_plan_head leaves the book alone
+  uint32_t bid;        // the batch whose prep wrote the header (FlowArgs::bid)
 };
 // FlowHdr::ok: 0 declined, FL_OK_ADD an ADD-only flow book, FL_OK_CANCEL a book with DELs,
 // FL_OK_DEEP an ADD-only head book with more levels than the lane plans hold (match_flow_deep.h)
@@ -242,6 +243,8 @@ struct FlowArgs {
   // (k_flow_tmap), so a wave finds its book with one load instead of a search of toff
   uint32_t* tmap;
   uint32_t tmap_stride, mb;
+  uint32_t bid;        // batch number (FlowHdr::bid)
+  uint32_t xlog;       // the early plan's arguments (match_early.h): the book's log at F.log + 0
 };
 
 __device__ __forceinline__ uint32_t fl_hend(const Dev& D, const FlowArgs& F) { return min(F.h1, D.st->nhot); }
@@ -841,6 +844,7 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep_b(Dev D, BatchArgs B, F
     x.w32 = w32 ? 1u : 0u;
     x.g = g;
     x.ndel = dels;
+    x.bid = F.bid;
     *hd = x;
   }
 }
@@ -1084,7 +1088,7 @@ __device__ __forceinline__ void fl_deep_store(const FlowArgs& F, uint32_t h) {
 template <bool EXCL>
 __device__ __forceinline__ void fl_plan_kernel(const Dev& D, const FlowArgs& F, uint32_t kind) {
   const uint32_t h = F.h0 + blockIdx.x;
-  const bool mine = h < fl_hend(D, F) && uni(F.hdr[h].ok) == kind;
+  const bool mine = h < fl_hend(D, F) && uni(F.hdr[h].ok) == kind && !uni(F.hdr[h].pre);
   if (mine && kind == FL_OK_DEEP) fl_deep_load(F, h);
   if (EXCL) {
     asm volatile("" ::: "v255", "a255");
@@ -1164,11 +1168,12 @@ __device__ __forceinline__ void fl_plan_book(const Dev& D, const FlowArgs& F, ui
     Db = FlDepth{pick(Db.l0, Db.l1, se), 0u, pick(Db.l0, Db.l1, so), 0u};
   }
 
-  FlLog lg{vreg(0u), vreg(0u), vreg(0u), 0u, 0u, 0u, FL_TOUCH_MUL * n, (GOME_GLB v4u*)(F.log + FL_TOUCH_MUL * beg)};
+  const uint32_t lb = F.xlog ? 0u : FL_TOUCH_MUL * beg;  // (the early plan logs into a buffer of its own)
+  FlLog lg{vreg(0u), vreg(0u), vreg(0u), 0u, 0u, 0u, FL_TOUCH_MUL * n, (GOME_GLB v4u*)(F.log + lb)};
   // records are read in half-groups of 8 (the book's stream is padded to whole groups)
   const uint32_t nh = (n + 7) / 8;
   const unsigned long long ob = reinterpret_cast<unsigned long long>(F.ord8 + uni(hd->obase));
-  const unsigned long long logp = reinterpret_cast<unsigned long long>(F.log + FL_TOUCH_MUL * beg);
+  const unsigned long long logp = reinterpret_cast<unsigned long long>(F.log + lb);
   const uint32_t vl16 = lane * 16u;
   uint32_t voff, vt, vpf;
   const uint32_t vzero = 0;
@@ -2748,6 +2753,7 @@ __global__ __launch_bounds__(128) void k_flow_write_fin(Dev D, FlowArgs F) {
   if (threadIdx.x == 0 && F.h0 == 0) {  // k_flow_plan_head's work (its roofline numerator)
     ctr_add(D, C_FLOW_HEAD_ORDERS, static_cast<unsigned long long>(hd.end - hd.beg));
     ctr_add(D, C_FLOW_HEAD_TOUCHES, static_cast<unsigned long long>(hd.ntouch));
+    ctr_add(D, C_HEAD_ADD, 1ull);
   }
 }
 

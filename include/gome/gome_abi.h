@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define GOME_ABI_VERSION 8u
+#define GOME_ABI_VERSION 9u
 
 /* ---- status codes (replace the reference's swallowed errors / panics,
  *      rabbitmq.go:44-49,70-72,120-122; nodelink.go:132,142,157) ---------- */
@@ -243,6 +243,12 @@ typedef struct gome_stats {
   uint64_t chunk_bytes;                       /* HBM held by FIFO chunks in use (node slots plus
                                                  chunk headers) after the batch (ABI >= 8):
                                                  / n_resting = bytes per resting order     */
+  uint64_t n_early;                           /* 1 when the batch's hottest book was planned
+                                                 early, right after the previous batch's plan
+                                                 (pipelined device batches, ABI >= 9)      */
+  uint64_t n_early_miss;                      /* an early plan the batch could not take although
+                                                 its hottest book went through the same plan
+                                                 (0 unless something is wrong; ABI >= 9)   */
 } gome_stats;
 
 typedef struct gome_engine gome_engine;

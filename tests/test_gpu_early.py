@@ -1,0 +1,106 @@
+"""HIP engine (MI355X) — the hottest book planned early (match_early.h).
+
+Pipelined device batches (three in flight) of bench.py's config-3 stream: from the second
+finished batch on, each batch's hottest book is prepared and planned on the copy stream as soon as
+the previous batch's plan ends.  Every batch's events are compared with the C oracle, and the
+books' levels and FIFOs at the end; gome_stats.n_early counts the batches whose plan was the early
+one, n_early_miss the early plans that were ready but not taken (it must stay 0).  The second test
+breaks the early plan's assumptions in single batches (a DEL, oids out of order, another symbol
+hottest, a zero-volume ADD) and checks that the engine stays exact and goes back to early plans
+afterwards; host-resolved verdicts (one refused) keep it."""
+import numpy as np
+import pytest
+
+import bench
+from gome_amd import workload as wl
+from gome_amd.abi import GOME_ORD_ADM_HOST, GOME_ORD_ADMITTED, Engine
+from oracle.pyoracle import Oracle
+from tests.test_gpu_v4 import _cmp, _cmp_books, _hot_and_random
+
+pytestmark = pytest.mark.gpu
+
+N = 1 << 18
+
+
+def _run(batches, nsym, label, **kw):
+    """Submit every batch with three in flight, collect in order; per-batch stats."""
+    import torch
+    eng = Engine(max_symbols=nsym, max_batch=N, max_nodes=(len(batches) + 4) * N, max_levels=1 << 22, **kw)
+    orc = Oracle(nsym)
+    dev = [torch.from_numpy(b.view(np.uint8).copy()).cuda() for b in batches]
+    torch.cuda.synchronize()
+    exp = [orc.submit(b) for b in batches]
+    stats = []
+    nxt = 0
+    for k in range(len(batches)):
+        while nxt < len(batches) and nxt < k + 3:
+            eng.submit_device_async(dev[nxt].data_ptr(), N, 0)
+            nxt += 1
+        _, n, st = eng.collect_device()  # (its events move to the host queue at the next collect)
+        assert n == len(exp[k]), f"{label} batch {k}: {n} events vs oracle {len(exp[k])}"
+        stats.append(st)
+    _cmp(eng.drain(), np.concatenate(exp), label)
+    return eng, orc, stats
+
+
+def test_early_plans_on_the_config3_stream_are_exact():
+    gen, _, _ = bench.shard_stream(100000, 1.0, 0, 1, 42)
+    batches = [gen(N).copy() for _ in range(8)]
+    eng, orc, stats = _run(batches, 100000, "early")
+    early = [int(s["n_early"]) for s in stats]
+    assert sum(int(s["n_early_miss"]) for s in stats) == 0, early
+    assert sum(early[3:]) >= 4, early  # (the first batches have no finished predecessor to go by)
+    z = wl.ZipfSymbols(100000, 1.0)
+    _cmp_books(eng, orc, _hot_and_random(z, 100000, k_rand=50), "early")
+    assert eng.stats()["n_resting"] == orc.resting()
+
+
+def test_early_plan_declines_keep_the_engine_exact():
+    gen, _, _ = bench.shard_stream(100000, 1.0, 0, 1, 7)
+    z = wl.ZipfSymbols(100000, 1.0)
+    hot, second = int(z.rank_to_id[0]), int(z.rank_to_id[1])
+    batches = [gen(N).copy() for _ in range(13)]
+    rng = np.random.default_rng(5)
+
+    def hot_rows(b, sym=hot):
+        return np.flatnonzero(b["symbol_id"] == sym)
+
+    # 4: a DEL of a maker of the hot book (an oid of batch 0) in its segment
+    b = batches[4]
+    r = hot_rows(b)[100]
+    b0 = batches[0]
+    b["action"][r] = wl.DEL
+    b["oid_id"][r] = b0["oid_id"][hot_rows(b0)[5]]
+    b["side"][r] = b0["side"][hot_rows(b0)[5]]
+    # 6: two of the hot book's oids swapped (out of batch order; still unique)
+    b = batches[6]
+    r = hot_rows(b)
+    b["oid_id"][r[10]], b["oid_id"][r[20]] = b["oid_id"][r[20]], b["oid_id"][r[10]]
+    # 8: another symbol is the hottest this batch (9: the hot book again, after another)
+    b = batches[8]
+    r = rng.choice(np.flatnonzero(b["symbol_id"] != hot), size=len(hot_rows(b)) + 5000, replace=False)
+    b["symbol_id"][r] = second
+    # 10: host-resolved admission on the hot book, one record refused
+    b = batches[10]
+    r = hot_rows(b)
+    b["flags"][r] = GOME_ORD_ADM_HOST | GOME_ORD_ADMITTED
+    b["flags"][r[30]] = GOME_ORD_ADM_HOST
+    # 12: a zero-volume ADD (Q6) in the hot book
+    batches[12]["volume_fx"][hot_rows(batches[12])[50]] = 0
+    eng, orc, stats = _run(batches, 100000, "declines")
+    early = [int(s["n_early"]) for s in stats]
+    assert sum(int(s["n_early_miss"]) for s in stats) == 0, early
+    for k in (4, 5, 6, 8, 9, 12):
+        assert early[k] == 0, (k, early)
+    for k in (3, 7, 10, 11):
+        assert early[k] == 1, (k, early)
+    _cmp_books(eng, orc, list(_hot_and_random(z, 100000, k_rand=50)) + [second], "declines")
+    assert eng.stats()["n_resting"] == orc.resting()
+
+
+def test_early_plan_off_is_the_same_engine(monkeypatch):
+    gen, _, _ = bench.shard_stream(100000, 1.0, 0, 1, 11)
+    batches = [gen(N).copy() for _ in range(6)]
+    monkeypatch.setenv("GOME_EARLY", "0")
+    _, _, stats = _run(batches, 100000, "early off")
+    assert all(int(s["n_early"]) == 0 for s in stats)

@@ -720,8 +720,13 @@ def main():
             "host_enqueue_ms": round(sum(s["ms_host_enqueue"] for s in sts) / steps, 3),
             "steps_mode": ("pipelined: two batches in flight (gome_submit_batch_device_async + "
                            "gome_collect_device); p50/p99_batch_ms are submit-to-collect times (two "
-                           "batches), p50/p99_device_batch_ms each batch's own device time") if pipelined
+                           "batches), p50/p99_device_batch_ms each batch's own device time (from its "
+                           "first kernel on the pipeline's stream; an early plan starts before it)") if pipelined
                           else "synchronous: one gome_submit_batch_device per step",
+            # timed steps whose hottest book was planned early (match_early.h: right after the
+            # previous batch's plan), and early plans not taken although ready (0 unless a bug)
+            "early_plans": int(sum(s.get("n_early", 0) for s in sts)),
+            "early_miss": int(sum(s.get("n_early_miss", 0) for s in sts)),
             "match_books_ms": round(ms_match, 3),
             "kernel_ms": {k: round(v[0], 3) for k, v in sorted(cands.items(), key=lambda kv: -kv[1][0])},
             "kernel_ms_source": phase_src,

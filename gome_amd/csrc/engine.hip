@@ -281,11 +281,16 @@ struct gome_engine {
     FlowLvl* lvl = nullptr;
     unsigned long long* ord8 = nullptr;
     Touch* log = nullptr;
+    FlowLvl* dlvl = nullptr;       // deep books' level table (DEEP_CAP)
   } xb[2];                         // by batch parity (the next batch's chain runs beside this one's take)
   FlPrepScr* x_pscr = nullptr;
   uint32_t *x_adm = nullptr, *x_evc = nullptr;  // predicted verdicts; the early prep_c's ev_count sink
   uint32_t *x_cnt = nullptr, *x_seg = nullptr, *x_sidx = nullptr;  // the hot symbol's records (k_x_*)
+  FlPrepScr* x_dscr = nullptr;                 // deep books: prep scratch, price set, sorted prices
+  unsigned long long *x_dkey = nullptr, *x_dnew = nullptr;
+  uint32_t *x_dval = nullptr, *x_dslot = nullptr;
   bool early_on = true;            // GOME_EARLY=0: never
+  bool cold_early = false;         // GOME_COLD_EARLY=1: a batch with an early plan runs its cold books on the early stream (A/B)
   uint32_t head_add = 0;           // bit 0 / 1: the last / the one before finished batch's hottest book took an ADD plan
   uint32_t bid = 0;                // batches enqueued (FlowArgs::bid)
   Slot slots[GOME_MAX_INFLIGHT];
@@ -505,6 +510,10 @@ gome_status gome_engine::init(const gome_config& c) {
       HIPCHK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(plan_lds)));
     HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_deep_prep_b), hipFuncAttributeMaxDynamicSharedMemorySize,
                                static_cast<int>(DEEP_CAP * 8)));
+    HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_xd_sort_new), hipFuncAttributeMaxDynamicSharedMemorySize,
+                               static_cast<int>(DEEP_CAP * 8)));
+    HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_xd_prep_b), hipFuncAttributeMaxDynamicSharedMemorySize,
+                               static_cast<int>(XD_PREP_LDS)));
   }
 
   max_batch = cfg.max_batch;
@@ -630,15 +639,20 @@ gome_status gome_engine::init(const gome_config& c) {
   for (XBuf& X : xb)
     if (!alloc(&X.ctl, 1, "early control") || !alloc(&X.hdr, 1, "early header") ||
         !alloc(&X.lvl, FL_CAP, "early levels") || !alloc(&X.ord8, nb + FL_ORD8_PAD, "early records") ||
-        !alloc(&X.log, ntouch, "early touch log"))
+        !alloc(&X.log, ntouch, "early touch log") || !alloc(&X.dlvl, DEEP_CAP, "early deep levels"))
       return GOME_E_CAPACITY;
   if (!alloc(&x_pscr, 1, "early prep scratch") || !alloc(&x_adm, nb, "early verdicts") ||
       !alloc(&x_evc, nb, "early event counts") || !alloc(&x_cnt, 2 * X_FIND_B, "early block counts") ||
-      !alloc(&x_seg, 3, "early segment") || !alloc(&x_sidx, nb, "early permutation"))
+      !alloc(&x_seg, 3, "early segment") || !alloc(&x_sidx, nb, "early permutation") ||
+      !alloc(&x_dscr, 1, "early deep scratch") || !alloc(&x_dkey, DEEP_HASH, "early deep prices") ||
+      !alloc(&x_dval, DEEP_HASH, "early deep levels of prices") || !alloc(&x_dnew, DEEP_CAP, "early deep sorted prices") ||
+      !alloc(&x_dslot, 1, "early deep slot"))
     return GOME_E_CAPACITY;
   for (XBuf& X : xb) HIPCHK(hipMemsetAsync(X.ctl, 0, sizeof(XCtl), stream));
+  HIPCHK(hipMemsetAsync(x_dslot, 0, 4, stream));  // (the early deep book is deep slot 0's)
   if (const char* g = std::getenv("GOME_EARLY")) early_on = std::atoi(g) != 0;
   if (early_on) HIPCHK(hipStreamCreateWithFlags(&early_stream, hipStreamNonBlocking));
+  if (const char* g = std::getenv("GOME_COLD_EARLY")) cold_early = std::atoi(g) != 0;
   // books with DELs (match_flow_cancel.h): per-position scratch, the (symbol, oid)
   // table (generation-tagged: cleared once per 2048 batches)
   fc_hcap = next_pow2(std::max<unsigned long long>(2ull * nb, 1024));
@@ -809,6 +823,8 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   FlowArgs FX = F;
   FX.hdr = X.hdr; FX.lvl = X.lvl; FX.ord8 = X.ord8; FX.log = X.log; FX.pscr = x_pscr;
   FX.xlog = 1; FX.h0 = 0; FX.h1 = 1; FX.tb = 0; FX.mb = 0; FX.chains = 0;
+  FX.dlvl = X.dlvl; FX.dh_key = x_dkey; FX.dh_val = x_dval; FX.dscr = x_dscr; FX.dslot_h = x_dslot;
+  FX.ds0 = 0; FX.ds1 = 1;
   if (early) {
     // the records, verdicts and prices on the early stream (the copy stream is still running the
     // last batch's early plan), the rest after both on the copy stream
@@ -822,17 +838,24 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
     HIPCHK(hipStreamWaitEvent(es, prep_h, 0));  // (the last batch's head prep: F.hdr[0] names its book)
     HIPCHK(hipMemsetAsync(X.ctl, 0, sizeof(XCtl), es));
     HIPCHK(hipMemsetAsync(x_pscr, 0, sizeof(FlPrepScr), es));
+    HIPCHK(hipMemsetAsync(X.hdr, 0, sizeof(FlowHdr), es));
+    HIPCHK(hipMemsetAsync(x_dscr, 0, sizeof(FlPrepScr), es));
+    HIPCHK(hipMemsetAsync(x_dkey, 0, sizeof(unsigned long long) * DEEP_HASH, es));
     k_x_count<<<xn, X_FIND_T, 0, es>>>(d_ord, n, F.hdr, bid_prev, x_cnt);
     k_x_scan<<<1, X_FIND_B, 0, es>>>(F.hdr, bid_prev, x_cnt, xn, x_seg, X.ctl);
     k_x_scatter<<<xn, X_FIND_T, 0, es>>>(d_ord, n, F.hdr, bid_prev, x_cnt, x_seg, X.ctl, x_sidx);
     HIPCHK(hipStreamWaitEvent(es, oidmax_done, 0));  // (the last batch's oid watermarks)
     k_x_adm<<<256, 256, 0, es>>>(Bx, X.ctl, d_oid_max, cfg.max_symbols, x_adm);
-    k_flow_prep_a<<<dim3(FL_PG, 1), FL_PREP_T, 0, es>>>(Dx, Bx, FX);
+    k_flow_prep_a<<<dim3(FL_PG, 1), FL_PREP_T, 0, es>>>(Dx, Bx, FX);        // (lane plans)
+    k_xd_prep_a<<<FL_PG, FL_PREP_T, 0, es>>>(Bx, FX, X.ctl);                 // (deep plans)
+    k_xd_sort_new<<<1, FL_PREP_T, DEEP_CAP * 8, es>>>(FX, X.ctl, x_dnew);
     HIPCHK(hipEventRecord(xpre_done, es));
     HIPCHK(hipStreamWaitEvent(ps, xpre_done, 0));
     HIPCHK(hipStreamWaitEvent(ps, plan_done, 0));
     k_x_prep_b<<<1, FL_PREP_T, 0, ps>>>(Bx, FX, F, X.ctl, bid_prev);
     k_flow_prep_c<<<dim3(FL_PG, 1), FL_PREP_T, 0, ps>>>(Dx, Bx, FX);
+    k_xd_prep_b<<<1, FL_PREP_T, XD_PREP_LDS, ps>>>(Bx, FX, F, X.ctl, x_dnew, bid_prev);
+    k_deep_prep_c<<<dim3(FL_PG, 1), FL_PREP_T, 0, ps>>>(Dx, Bx, FX);
     HIPCHK(hipEventRecord(xprep_done, ps));
     HIPCHK(hipEventRecord(S.evx0, ps));
     k_flow_plan_head<<<1, 256, plan_lds, ps>>>(Dx, FX);
@@ -1096,7 +1119,8 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   // kernel (config-2 e2e 5.24 -> 6.9 ms per batch).  A stream of its own (GOME_COLD_OWN=1) measured
   // slower at 4, 8 and 16 hardware queues (config 2: 2.3 -> 3.6 ms per batch).  A batch
   // with an early plan keeps the copy stream for it.  GOME_COLD_MAIN=1: the caller's stream always
-  hipStream_t cst = (cold_main || copy_busy || early) ? s : cold_stream ? cold_stream : copy_stream;
+  hipStream_t cst = (early && cold_early) ? early_stream
+                    : (cold_main || copy_busy || early) ? s : cold_stream ? cold_stream : copy_stream;
   if (cst != s) HIPCHK(hipStreamWaitEvent(cst, prep_t, 0));
   HIPCHK(hipEventRecord(S.evc0, cst));
   k_match<<<std::min<uint32_t>(ceil_div(grid, COLD_WAVES), COLD_BLOCKS), 64 * COLD_WAVES, COLD_LDS_BYTES, cst>>>(

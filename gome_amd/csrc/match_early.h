@@ -33,6 +33,7 @@
 #include <hip/hip_runtime.h>
 
 #include "match_flow.h"
+#include "match_flow_deep.h"
 
 namespace gome {
 
@@ -41,17 +42,22 @@ struct XCtl {
   uint32_t bad;    // k_x_adm: a record the prediction does not cover
   uint32_t mism;   // k_x_cmp: the early inputs differ from the batch's own prep
   uint32_t used;   // k_x_take: the early plan is the book's plan
+  uint32_t kind;   // the previous plan of the book: FL_OK_ADD (lane plans) or FL_OK_DEEP
+  uint32_t nnew;   // deep books: the batch's distinct prices (X.dnew, sorted)
+  uint32_t pad[2];
   Status st;       // the early kernels' Dev::st (nhot: 1 = plan the hottest segment, 0 = skip; err)
 };
 
+constexpr uint32_t XD_PREP_LDS = (2 * DEEP_CAP + 2) * 4;  // k_xd_prep_b's two prefix arrays
 constexpr uint32_t X_FIND_T = 256, X_FIND_B = 1024;  // k_x_count / k_x_scatter: blocks of contiguous records
 
 __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t x) { return rl(wave_incl_scan_u32(x), 63); }
 
-// The previous batch's hottest book (its header: an ADD plan of batch bid_prev), or NIL.
+// The previous batch's hottest book (its header: an ADD plan of batch bid_prev, lane or deep), or NIL.
 __device__ __forceinline__ uint32_t x_hot_sym(const FlowHdr* hdr, uint32_t bid_prev) {
   const FlowHdr h = hdr[0];
-  return (h.ok == FL_OK_ADD && h.bid == bid_prev) ? h.sym : NIL;
+  const bool add = h.ok == FL_OK_ADD || (h.ok == FL_OK_DEEP && !h.dc && h.ndel == 0 && h.dslot == 0);
+  return (add && h.bid == bid_prev) ? h.sym : NIL;
 }
 
 __device__ __forceinline__ void x_range(uint32_t n, uint32_t& r0, uint32_t& r1) {
@@ -110,6 +116,7 @@ __global__ __launch_bounds__(X_FIND_B) void k_x_scan(const FlowHdr* hdr, uint32_
     xseg[1] = beg;
     xseg[2] = beg + tot;
     X->st.nhot = (x_hot_sym(hdr, bid_prev) != NIL && tot >= (1u << FLOW_MIN_LOG2)) ? 1u : 0u;
+    X->kind = hdr[0].ok;
   }
 }
 
@@ -183,6 +190,7 @@ __global__ __launch_bounds__(FL_PREP_T) void k_x_prep_b(BatchArgs Bx, FlowArgs F
   const FlowHdr ph = F.hdr[0];
   const uint32_t seg = Bx.seg_order[0];
   const uint32_t beg = Bx.seg_start[seg], end = Bx.seg_start[seg + 1];
+  if (X->kind != FL_OK_ADD) return;  // (a deep book: k_xd_prep_b)
   if (tid == 0) {
     ndist = nc = 0;
     bad = (X->st.nhot == 0 || X->bad || P->bad || P->many || P->dels || ph.ok != FL_OK_ADD || ph.bid != bid_prev ||
@@ -285,21 +293,253 @@ __global__ __launch_bounds__(FL_PREP_T) void k_x_prep_b(BatchArgs Bx, FlowArgs F
   }
 }
 
+// ---- deep books (W32D / W32DV, match_flow_deep.h) -------------------------------------------
+// The batch's prices of the book into the early price set (FX.dh_key, emptied per batch), the
+// volumes' gcd / sum per slice and the counts (k_deep_prep_a's, into the early scratch).
+__global__ __launch_bounds__(FL_PREP_T) void k_xd_prep_a(BatchArgs Bx, FlowArgs FX, XCtl* X) {
+  __shared__ uint32_t adds, dropped, bad, nd;
+  __shared__ unsigned long long wg[FL_PREP_T / 64], ws[FL_PREP_T / 64];
+  if (X->kind != FL_OK_DEEP || X->st.nhot == 0) return;
+  const uint32_t tid = threadIdx.x;
+  FlPrepScr* P = FX.dscr;
+  uint32_t b0, b1;
+  fd_slice(Bx.seg_start[0], Bx.seg_start[1], blockIdx.x, gridDim.x, b0, b1);
+  if (tid == 0) adds = dropped = bad = nd = 0;
+  __syncthreads();
+  unsigned long long mg = 0, msum = 0;
+  uint32_t my_adds = 0, my_drop = 0, my_bad = 0, my_nd = 0;
+  for (uint32_t b = b0 + tid; b < b1; b += FL_PREP_T) {
+    const Prep q = prep_at(Bx, b);
+    if (q.action != GOME_ADD) { my_bad = 1; continue; }
+    my_adds++;
+    if (!q.adm) { my_drop++; continue; }
+    if (q.vol == 0 || q.adm == ADM_V_CHECK) { my_bad = 1; continue; }
+    const unsigned long long v = static_cast<unsigned long long>(q.vol);
+    mg = fl_gcd(mg, v);
+    msum = min(msum + v, FL_SUM_CAP);
+    bool fresh;
+    if (fd_put(FX.dh_key, static_cast<unsigned long long>(q.price) + FL_KEY_OFF, &fresh) == NIL) my_bad = 1;
+    my_nd += fresh ? 1u : 0u;
+  }
+  if (my_adds) atomicAdd(&adds, my_adds);
+  if (my_drop) atomicAdd(&dropped, my_drop);
+  if (my_bad) bad = 1;
+  if (my_nd) atomicAdd(&nd, my_nd);
+  fl_block_gcd_sum(mg, msum, wg, ws);  // (synchronises the block)
+  if (tid == 0) {
+    P->pg[blockIdx.x] = mg;
+    P->ps[blockIdx.x] = msum;
+    if (adds) atomicAdd(&P->d_adds, adds);
+    if (dropped) atomicAdd(&P->d_dropped, dropped);
+    if (bad) atomicOr(&P->d_bad, 1u);
+    if (nd) atomicAdd(&P->d_ndist, nd);
+  }
+}
+
+// The batch's distinct prices of the book, sorted (bitonic in LDS, one workgroup), into dnew:
+// this runs beside the previous plan, so only a merge is left after it.
+// Dynamic LDS: DEEP_CAP keys.
+__global__ __launch_bounds__(FL_PREP_T) void k_xd_sort_new(FlowArgs FX, XCtl* X, unsigned long long* dnew) {
+  __shared__ uint32_t nc;
+  if (X->kind != FL_OK_DEEP || X->st.nhot == 0) return;
+  const uint32_t tid = threadIdx.x;
+  const FlPrepScr* P = FX.dscr;
+  const uint32_t n = P->d_ndist;
+  if (P->d_bad || n > DEEP_CAP - 2) {
+    if (tid == 0) X->bad = 1;
+    return;
+  }
+  unsigned long long* sk = reinterpret_cast<unsigned long long*>(fl_ring);
+  if (tid == 0) nc = 0;
+  __syncthreads();
+  for (uint32_t sl = tid; sl < DEEP_HASH; sl += FL_PREP_T) {
+    const unsigned long long key = FX.dh_key[sl];
+    if (key) sk[atomicAdd(&nc, 1u)] = key;
+  }
+  __syncthreads();
+  uint32_t np = 1024;
+  while (np < n) np <<= 1;
+  for (uint32_t i = n + tid; i < np; i += FL_PREP_T) sk[i] = ~0ull;
+  __syncthreads();
+  for (uint32_t k = 2; k <= np; k <<= 1) {
+    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+      for (uint32_t i = tid; i < np; i += FL_PREP_T) {
+        const uint32_t p = i ^ j;
+        if (p > i) {
+          const unsigned long long a = sk[i], b = sk[p];
+          if ((a > b) == ((i & k) == 0)) {
+            sk[i] = b;
+            sk[p] = a;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (uint32_t i = tid; i < n; i += FL_PREP_T) dnew[i] = sk[i];
+  if (tid == 0) X->nnew = n;
+}
+
+// Exclusive block scan of flags f[0..n) in place (FL_PREP_T threads, chunks of FL_PREP_T);
+// f[n] = the total.
+__device__ __forceinline__ void x_block_scan(uint32_t* f, uint32_t n, uint32_t* wsum) {
+  uint32_t carry = 0;
+  for (uint32_t c0 = 0; c0 < n; c0 += FL_PREP_T) {
+    const uint32_t i = c0 + threadIdx.x;
+    const uint32_t v = i < n ? f[i] : 0u;
+    const uint32_t inc = wave_incl_scan_u32(v);
+    if (lane_id() == 63) wsum[threadIdx.x >> 6] = inc;
+    __syncthreads();
+    uint32_t before = 0, all = 0;
+    for (uint32_t w = 0; w < FL_PREP_T / 64; ++w) {
+      before += w < (threadIdx.x >> 6) ? wsum[w] : 0u;
+      all += wsum[w];
+    }
+    if (i < n) f[i] = carry + before + inc - v;
+    carry += all;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) f[n] = carry;
+  __syncthreads();
+}
+
+// First index in [0, n) whose key is >= x (keys ascending), n if none.
+template <class Key>
+__device__ __forceinline__ uint32_t x_lower(Key key, uint32_t n, unsigned long long x) {
+  uint32_t lo = 0, hi = n;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (key(mid) < x) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
+// The early deep prep after the previous plan: its live levels (F.dlvl of deep slot 0: price,
+// dfin, memf; sorted by price) merged with the batch's sorted prices into the level table
+// (FX.dlvl), each batch price's level into the early set's values, the header.  A merge by
+// ranks (scans and binary searches) instead of k_deep_prep_b's sort of the whole set.
+// Dynamic LDS: two DEEP_CAP + 1 flag / prefix arrays.
+__global__ __launch_bounds__(FL_PREP_T) void k_xd_prep_b(BatchArgs Bx, FlowArgs FX, FlowArgs F, XCtl* X,
+                                                         const unsigned long long* dnew, uint32_t bid_prev) {
+  __shared__ uint32_t bad, wsum[FL_PREP_T / 64];
+  __shared__ unsigned long long wg[FL_PREP_T / 64], ws[FL_PREP_T / 64];
+  if (X->kind != FL_OK_DEEP) return;
+  const uint32_t tid = threadIdx.x;
+  FlowHdr* hd = &FX.hdr[0];
+  const FlPrepScr* P = FX.dscr;
+  const FlowHdr ph = F.hdr[0];
+  const uint32_t beg = Bx.seg_start[0], end = Bx.seg_start[1];
+  const uint32_t nlp = ph.nl, nn = X->nnew;
+  if (tid == 0) {
+    const uint64_t tiles = (static_cast<uint64_t>(FL_TOUCH_MUL) * (end - beg) + FL_TILE - 1) / FL_TILE;
+    bad = (X->st.nhot == 0 || X->bad || P->d_bad || ph.ok != FL_OK_DEEP || ph.dc || ph.ndel || ph.dslot != 0 ||
+           ph.bid != bid_prev || ph.sym != Bx.ord[Bx.sidx[beg]].symbol_id || nlp > DEEP_CAP - 2 || tiles > F.dmaxt)
+              ? 1u : 0u;
+  }
+  __syncthreads();
+  if (bad) {
+    if (tid == 0) X->st.nhot = 0;
+    return;
+  }
+  const FlowLvl* LP = F.dlvl;  // (deep slot 0: the hottest book's)
+  uint32_t* lpre = reinterpret_cast<uint32_t*>(fl_ring);  // [nlp + 1]: live old levels before
+  uint32_t* mpre = lpre + DEEP_CAP + 1;                     // [nn + 1]: batch prices on a live old level before
+  unsigned long long mg = 0, msum = 0;
+  if (tid < FL_PG) {
+    mg = P->pg[tid];
+    msum = P->ps[tid];
+  }
+  for (uint32_t i = tid; i < nlp; i += FL_PREP_T) {
+    const FlowLvl& f = LP[i + 1];
+    const bool live = f.memf != 0;
+    if (live != (f.dfin > 0) || f.memf == (M_BUY | M_SALE)) bad = 1;
+    if (live) {
+      mg = fl_gcd(mg, static_cast<unsigned long long>(f.dfin));
+      msum = min(msum + static_cast<unsigned long long>(f.dfin), FL_SUM_CAP);
+    }
+    lpre[i] = live ? 1u : 0u;
+  }
+  auto oldkey = [&](uint32_t i) { return static_cast<unsigned long long>(LP[i + 1].price) + FL_KEY_OFF; };
+  for (uint32_t i = tid; i < nn; i += FL_PREP_T) {
+    const uint32_t q = x_lower(oldkey, nlp, dnew[i]);
+    mpre[i] = (q < nlp && oldkey(q) == dnew[i] && LP[q + 1].memf != 0) ? 1u : 0u;
+  }
+  fl_block_gcd_sum(mg, msum, wg, ws);  // (synchronises the block)
+  x_block_scan(lpre, nlp, wsum);
+  x_block_scan(mpre, nn, wsum);
+  const uint32_t n = lpre[nlp] + nn - mpre[nn];
+  const unsigned long long g = mg ? mg : 1;
+  const bool w32 = msum < FL_SUM_CAP && msum / g < (1ull << 32);
+  if (bad || n > DEEP_CAP - 2 || !w32) {
+    if (tid == 0) X->st.nhot = 0;
+    return;
+  }
+  FlowLvl* LV = FX.dlvl;
+  // live old levels: rank = live ones before + batch-only prices below
+  for (uint32_t i = tid; i < nlp; i += FL_PREP_T) {
+    const FlowLvl& o = LP[i + 1];
+    if (!o.memf) continue;
+    const uint32_t pos = x_lower([&](uint32_t k) { return dnew[k]; }, nn, oldkey(i));
+    FlowLvl f{};
+    f.price = o.price;
+    f.d0 = o.dfin;
+    f.mem0 = o.memf;
+    f.old = i + 1;  // (the previous plan's level: informational)
+    f.head = f.tail = NIL;
+    f.ig_all = 1;
+    LV[lpre[i] + (pos - mpre[pos]) + 1] = f;
+  }
+  // the batch's prices: a new level unless a live old level has it; each one's level in the set
+  for (uint32_t i = tid; i < nn; i += FL_PREP_T) {
+    const unsigned long long key = dnew[i];
+    const uint32_t q = x_lower(oldkey, nlp, key);  // (live old levels below: lpre[q])
+    const bool on_old = mpre[i + 1] != mpre[i];
+    const uint32_t r = lpre[q] + (i - mpre[i]) + 1;
+    if (!on_old) {
+      FlowLvl f{};
+      f.price = static_cast<int64_t>(key - FL_KEY_OFF);
+      f.old = NIL;
+      f.head = f.tail = NIL;
+      f.ig_all = 1;
+      LV[r] = f;
+    }
+    FX.dh_val[fd_find(FX.dh_key, key)] = r;
+  }
+  if (tid < ((8u - ((end - beg) & 7u)) & 7u)) FX.ord8[(end - beg) + tid] = 0ull;  // no-op padding
+  if (tid == 0) {
+    FlowHdr x{};
+    x.ok = FL_OK_DEEP;
+    x.nl = n;
+    x.sym = ph.sym;
+    x.beg = beg;
+    x.end = end;
+    x.adds = P->d_adds;
+    x.dropped = P->d_dropped;
+    x.obase = 0;
+    x.w32 = 1;
+    x.g = g;
+    x.deep = 1;
+    x.dslot = 0;
+    *hd = x;
+    X->ok = 1;
+  }
+}
+
 // The early inputs against the batch's own head prep of the same book: header, levels, every
 // packed record (a grid of blocks; block 0 also takes the header and the levels).
 __global__ void k_x_cmp(Dev D, FlowArgs F, FlowArgs FX, XCtl* X) {
   if (!X->ok) return;
   const FlowHdr hd = F.hdr[0], xh = FX.hdr[0];
-  bool diff = D.st->nhot == 0 || hd.ok != FL_OK_ADD || xh.ok != FL_OK_ADD || hd.bid != F.bid || hd.nl != xh.nl ||
-              hd.sym != xh.sym || hd.beg != xh.beg || hd.end != xh.end || hd.adds != xh.adds ||
-              hd.dropped != xh.dropped || hd.w32 != xh.w32 || hd.g != xh.g || hd.ndel != 0;
+  const bool kind = (hd.ok == FL_OK_ADD || (hd.ok == FL_OK_DEEP && !hd.dc && hd.dslot == 0)) && xh.ok == hd.ok;
+  bool diff = D.st->nhot == 0 || !kind || hd.bid != F.bid || hd.nl != xh.nl || hd.sym != xh.sym ||
+              hd.beg != xh.beg || hd.end != xh.end || hd.adds != xh.adds || hd.dropped != xh.dropped ||
+              hd.w32 != xh.w32 || hd.g != xh.g || hd.ndel != 0;
   if (!diff) {
-    if (blockIdx.x == 0)
-      for (uint32_t q = 1 + threadIdx.x; q <= hd.nl; q += blockDim.x) {
-        const FlowLvl& a = F.lvl[q];
-        const FlowLvl& b = FX.lvl[q];
-        if (a.price != b.price || a.d0 != b.d0 || a.mem0 != b.mem0) diff = true;
-      }
+    const FlowLvl* A = fl_lvls(F, 0);
+    const FlowLvl* B = fl_lvls(FX, 0);
+    for (uint32_t q = 1 + blockIdx.x * blockDim.x + threadIdx.x; q <= hd.nl; q += gridDim.x * blockDim.x)
+      if (A[q].price != B[q].price || A[q].d0 != B[q].d0 || A[q].mem0 != B[q].mem0) diff = true;
     const uint32_t m = ((hd.end - hd.beg) + 7u) & ~7u;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < m; i += gridDim.x * blockDim.x)
       if (F.ord8[hd.obase + i] != FX.ord8[i]) diff = true;
@@ -307,20 +547,26 @@ __global__ void k_x_cmp(Dev D, FlowArgs F, FlowArgs FX, XCtl* X) {
   if (__any(diff) && lane_id() == 0) atomicOr(&X->mism, 1u);
 }
 
-// After the early plan: take it (its final depths, side masks and touch count into F, the header
+// After the early plan: take it (its final depths and sides, touch count into F, the header
 // marked `pre`) when its inputs matched and it ran clean.
 __global__ void k_x_take(Dev D, FlowArgs F, FlowArgs FX, XCtl* X) {
   __shared__ uint32_t use;
   const FlowHdr xh = FX.hdr[0];
   if (threadIdx.x == 0) {
-    const bool normal = D.st->nhot != 0 && F.hdr[0].ok == FL_OK_ADD;
+    const uint32_t ok = F.hdr[0].ok;
+    const bool normal = D.st->nhot != 0 && (ok == FL_OK_ADD || ok == FL_OK_DEEP) && ok == xh.ok;
     use = (X->ok && !X->mism && X->st.err == 0 && normal) ? 1u : 0u;
     // (a batch whose hottest book is another symbol than the last one's plans it normally)
     if (!use && normal && X->ok && F.hdr[0].sym == xh.sym) ctr_add(D, C_EARLY_MISS, 1ull);
   }
   __syncthreads();
   if (!use) return;
-  for (uint32_t q = 1 + threadIdx.x; q <= xh.nl; q += blockDim.x) F.lvl[q].dfin = FX.lvl[q].dfin;
+  FlowLvl* A = fl_lvls(F, 0);
+  const FlowLvl* B = fl_lvls(FX, 0);
+  for (uint32_t q = 1 + threadIdx.x; q <= xh.nl; q += blockDim.x) {
+    A[q].dfin = B[q].dfin;
+    A[q].memf = B[q].memf;
+  }
   if (threadIdx.x == 0) {
     FlowHdr* w = &F.hdr[0];
     w->ntouch = xh.ntouch;
@@ -328,6 +574,7 @@ __global__ void k_x_take(Dev D, FlowArgs F, FlowArgs FX, XCtl* X) {
     w->amask[1] = xh.amask[1];
     w->bmask[0] = xh.bmask[0];
     w->bmask[1] = xh.bmask[1];
+    w->dv_ba = xh.dv_ba;
     w->pre = 1;
     X->used = 1;
     ctr_add(D, C_EARLY, 1ull);

@@ -1260,10 +1260,11 @@ __device__ __forceinline__ void fl_plan_deep(const Dev& D, const FlowArgs& F, ui
   __builtin_amdgcn_s_setprio(3);
   const uint32_t lane = lane_id();
   const uint32_t beg = uni(hd->beg), end = uni(hd->end), n = end - beg;
-  FlLog lg{vreg(0u), vreg(0u), vreg(0u), 0u, 0u, 0u, FL_TOUCH_MUL * n, (GOME_GLB v4u*)(F.log + FL_TOUCH_MUL * beg)};
+  const uint32_t lb = F.xlog ? 0u : FL_TOUCH_MUL * beg;  // (the early plan logs into a buffer of its own)
+  FlLog lg{vreg(0u), vreg(0u), vreg(0u), 0u, 0u, 0u, FL_TOUCH_MUL * n, (GOME_GLB v4u*)(F.log + lb)};
   const uint32_t nh = (n + 7) / 8;
   const unsigned long long ob = reinterpret_cast<unsigned long long>(F.ord8 + uni(hd->obase));
-  const unsigned long long logp = reinterpret_cast<unsigned long long>(F.log + FL_TOUCH_MUL * beg);
+  const unsigned long long logp = reinterpret_cast<unsigned long long>(F.log + lb);
   const uint32_t vl16 = lane * 16u;
   uint32_t voff, vpf;
   const uint32_t vzero = 0;

@@ -304,6 +304,7 @@ __device__ __forceinline__ void k_deep_prep_b_one(Dev D, BatchArgs B, FlowArgs F
     x.dslot = ds;
     x.ndel = P->d_dels;
     x.dc = P->d_dels ? 1u : 0u;
+    x.bid = F.bid;
     *hd = x;
   }
 }
@@ -728,6 +729,7 @@ __device__ __forceinline__ void k_deep_write_fin_one(Dev D, FlowArgs F, uint32_t
     if (hd.dslot == 0) {  // the hottest book (k_flow_plan_head's work)
       ctr_add(D, C_FLOW_HEAD_ORDERS, static_cast<unsigned long long>(hd.end - hd.beg));
       ctr_add(D, C_FLOW_HEAD_TOUCHES, static_cast<unsigned long long>(hd.ntouch));
+      if (!hd.dc) ctr_add(D, C_HEAD_ADD, 1ull);
     }
   }
   __syncthreads();

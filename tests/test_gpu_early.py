@@ -22,10 +22,10 @@ pytestmark = pytest.mark.gpu
 N = 1 << 18
 
 
-def _run(batches, nsym, label, **kw):
+def _run(batches, nsym, label, levels=1 << 22):
     """Submit every batch with three in flight, collect in order; per-batch stats."""
     import torch
-    eng = Engine(max_symbols=nsym, max_batch=N, max_nodes=(len(batches) + 4) * N, max_levels=1 << 22, **kw)
+    eng = Engine(max_symbols=nsym, max_batch=N, max_nodes=(len(batches) + 4) * N, max_levels=levels)
     orc = Oracle(nsym)
     dev = [torch.from_numpy(b.view(np.uint8).copy()).cuda() for b in batches]
     torch.cuda.synchronize()
@@ -95,6 +95,22 @@ def test_early_plan_declines_keep_the_engine_exact():
     for k in (3, 7, 10, 11):
         assert early[k] == 1, (k, early)
     _cmp_books(eng, orc, list(_hot_and_random(z, 100000, k_rand=50)) + [second], "declines")
+    assert eng.stats()["n_resting"] == orc.resting()
+
+
+def test_early_plans_of_a_deep_book_are_exact():
+    """Config 5 (1M symbols, 4-dp prices): the hottest book has thousands of levels, so its plans
+    are the deep ones (W32DV), and so is its early plan (k_xd_prep_a / k_xd_sort_new / k_xd_prep_b:
+    the previous plan's live levels merged with the batch's sorted prices)."""
+    gen, _, _ = bench.make_stream("config5", 0, 1, 42)
+    batches = [gen(N).copy() for _ in range(8)]
+    eng, orc, stats = _run(batches, 1000000, "deep early", levels=1 << 25)  # (16-level blocks per book)
+    early = [int(s["n_early"]) for s in stats]
+    assert sum(int(s["n_early_miss"]) for s in stats) == 0, early
+    assert sum(early[3:]) >= 4, early
+    assert all(int(s["chains"]) & 1 for s in stats[2:])  # (the deep chain: the book is deep)
+    z = wl.ZipfSymbols(1000000, 1.0)
+    _cmp_books(eng, orc, _hot_and_random(z, 1000000, k_hot=2, k_rand=20), "deep early")
     assert eng.stats()["n_resting"] == orc.resting()
 
 

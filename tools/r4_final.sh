@@ -40,6 +40,10 @@ for P in $PARTS; do
   prof3)
     bash profiles/run_rocprof.sh ${TAG}_config3 --steps 6 --warmup 3 --no-cpu-baseline --e2e-steps 0 --consumer-msgs 0 --no-phase-pass || exit 6
     python3 profiles/summarize.py ${TAG}_config3 gpurun_out/prof_${TAG}_config3 || exit 7 ;;
+  prof4|prof5|prof5c)
+    W=config${P#prof}
+    bash profiles/run_rocprof.sh ${TAG}_$W --workload $W --steps 6 --warmup 4 --no-cpu-baseline --e2e-steps 0 --consumer-msgs 0 --no-phase-pass || exit 6
+    python3 profiles/summarize.py ${TAG}_$W gpurun_out/prof_${TAG}_$W || exit 7 ;;
   prof2)
     bash profiles/run_rocprof.sh ${TAG}_config2 --workload config2 --steps 6 --warmup 4 --no-cpu-baseline --e2e-steps 0 --consumer-msgs 0 --no-phase-pass || exit 6
     python3 profiles/summarize.py ${TAG}_config2 gpurun_out/prof_${TAG}_config2 || exit 7 ;;

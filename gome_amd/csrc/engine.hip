@@ -290,7 +290,9 @@ struct gome_engine {
   unsigned long long *x_dkey = nullptr, *x_dnew = nullptr;
   uint32_t *x_dval = nullptr, *x_dslot = nullptr;
   bool early_on = true;            // GOME_EARLY=0: never
-  bool cold_early = false;         // GOME_COLD_EARLY=1: a batch with an early plan runs its cold books on the early stream (A/B)
+  // a batch with an early plan runs its cold books on the early stream, after the next batch's early
+  // record work (A/B on one box: config 3 +0.3..0.7%, config 5 even; GOME_COLD_EARLY=0: the caller's)
+  bool cold_early = true;
   uint32_t head_add = 0;           // bit 0 / 1: the last / the one before finished batch's hottest book took an ADD plan
   uint32_t bid = 0;                // batches enqueued (FlowArgs::bid)
   Slot slots[GOME_MAX_INFLIGHT];
@@ -1118,7 +1120,8 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   // caller's stream: there the copy stream carries the next batch's H2D, which waited for the cold
   // kernel (config-2 e2e 5.24 -> 6.9 ms per batch).  A stream of its own (GOME_COLD_OWN=1) measured
   // slower at 4, 8 and 16 hardware queues (config 2: 2.3 -> 3.6 ms per batch).  A batch
-  // with an early plan keeps the copy stream for it.  GOME_COLD_MAIN=1: the caller's stream always
+  // with an early plan keeps the copy stream for it and runs the cold books on the early stream
+  // (cold_early).  GOME_COLD_MAIN=1: the caller's stream always
   hipStream_t cst = (early && cold_early) ? early_stream
                     : (cold_main || copy_busy || early) ? s : cold_stream ? cold_stream : copy_stream;
   if (cst != s) HIPCHK(hipStreamWaitEvent(cst, prep_t, 0));

@@ -345,6 +345,7 @@ def main():
     ap.add_argument("--batch", type=int, default=1 << 22, help="orders per GPU per step")
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="config3")
     ap.add_argument("--seed", type=int, default=42)
+    ap.add_argument("--e2e-depth", type=int, default=2, help="host batches in flight in the e2e leg (<= GOME_MAX_INFLIGHT)")
     ap.add_argument("--e2e-steps", type=int, default=-1,
                     help="timed steps of the host-to-host pipelined path (-1: = --steps, 0: off)")
     ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of CPU-baseline work")
@@ -578,9 +579,8 @@ def main():
             b[:] = gen(per_rank)
         done_ev = [0]
 
-        # two batches in flight (three, with the events' D2H on a stream of its own, measured slower:
-        # DESIGN §5)
-        depth = 2
+        # batches in flight on the host path (--e2e-depth)
+        depth = max(1, min(args.e2e_depth, GOME_MAX_INFLIGHT))
 
         def run_pipe(lo, hi, lats):
             tsub = {}

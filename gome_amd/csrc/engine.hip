@@ -766,7 +766,7 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   hipStream_t ss = (ahead && sort_ahead && dominant) ? copy_stream : s;
   // the hottest book planned early on the copy stream (match_early.h): pipelined device batches
   // after a batch whose hottest book took an ADD plan (the device checks the rest)
-  const bool early = early_on && ahead && dominant && head_add != 0 && bid > 0 && F.enabled;
+  const bool early = early_on && (ahead || copy_busy) && dominant && head_add != 0 && bid > 0 && F.enabled;
   S.early = early;
   const uint32_t bid_prev = bid;
   F.bid = ++bid;
@@ -830,7 +830,9 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   if (early) {
     // the records, verdicts and prices on the early stream (the copy stream is still running the
     // last batch's early plan), the rest after both on the copy stream
-    hipStream_t es = early_stream, ps = copy_stream;
+    // (pipelined host batches: the record work on the copy stream right behind the batch's H2D, the
+    // plan on the early stream, so the copy stream stays free for the copies)
+    hipStream_t es = copy_busy ? copy_stream : early_stream, ps = copy_busy ? early_stream : copy_stream;
     Dev Dx = D;
     Dx.st = reinterpret_cast<Status*>(reinterpret_cast<char*>(X.ctl) + offsetof(XCtl, st));
     BatchArgs Bx{};
@@ -1122,7 +1124,7 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   // slower at 4, 8 and 16 hardware queues (config 2: 2.3 -> 3.6 ms per batch).  A batch
   // with an early plan keeps the copy stream for it and runs the cold books on the early stream
   // (cold_early).  GOME_COLD_MAIN=1: the caller's stream always
-  hipStream_t cst = (early && cold_early) ? early_stream
+  hipStream_t cst = (early && cold_early && !copy_busy) ? early_stream
                     : (cold_main || copy_busy || early) ? s : cold_stream ? cold_stream : copy_stream;
   if (cst != s) HIPCHK(hipStreamWaitEvent(cst, prep_t, 0));
   HIPCHK(hipEventRecord(S.evc0, cst));

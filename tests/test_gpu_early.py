@@ -114,6 +114,32 @@ def test_early_plans_of_a_deep_book_are_exact():
     assert eng.stats()["n_resting"] == orc.resting()
 
 
+def test_early_plans_of_pipelined_host_batches_are_exact():
+    """The host path (gome_submit_batch_async / gome_collect: records copied in on the copy stream,
+    events copied out): the early record work runs behind each batch's H2D on the copy stream and
+    the plan on the early stream."""
+    gen, _, _ = bench.shard_stream(100000, 1.0, 0, 1, 21)
+    batches = [gen(N).copy() for _ in range(8)]
+    eng = Engine(max_symbols=100000, max_batch=N, max_nodes=12 * N, max_levels=1 << 22)
+    orc = Oracle(100000)
+    bufs = [eng.host_buffer(N) for _ in batches]
+    for b, buf in zip(batches, bufs):
+        buf[:] = b
+    stats, nxt = [], 0
+    for k in range(len(batches)):
+        while nxt < len(batches) and nxt < k + 3:
+            eng.submit_async(bufs[nxt], 0)
+            nxt += 1
+        ev, st = eng.collect()
+        _cmp(ev, orc.submit(batches[k]), f"host early batch {k}")
+        stats.append(st)
+    early = [int(s["n_early"]) for s in stats]
+    assert sum(int(s["n_early_miss"]) for s in stats) == 0, early
+    assert sum(early[3:]) >= 4, early
+    z = wl.ZipfSymbols(100000, 1.0)
+    _cmp_books(eng, orc, _hot_and_random(z, 100000, k_rand=30), "host early")
+
+
 def test_early_plan_off_is_the_same_engine(monkeypatch):
     gen, _, _ = bench.shard_stream(100000, 1.0, 0, 1, 11)
     batches = [gen(N).copy() for _ in range(6)]

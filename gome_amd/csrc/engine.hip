@@ -531,6 +531,7 @@ gome_status gome_engine::init(const gome_config& c) {
   {
     const char* q = std::getenv("GPU_MAX_HW_QUEUES");
     cold_main = !q || std::atoi(q) < 8;
+    early_on = !cold_main;  // (the early plan's stream needs a queue of its own too)
   }
   if (const char* g = std::getenv("GOME_COLD_MAIN")) cold_main = std::atoi(g) != 0;            // (A/B)
   if (const char* g = std::getenv("GOME_COLD_OWN"); g && std::atoi(g) != 0)                   // (A/B)

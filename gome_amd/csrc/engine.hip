@@ -508,6 +508,7 @@ gome_status gome_engine::init(const gome_config& c) {
     HIPCHK(hipDeviceGetAttribute(&lds, hipDeviceAttributeMaxSharedMemoryPerBlock, cfg.device));
     if (lds < static_cast<int>(FL_DEEP_LDS)) return fail(GOME_E_DEVICE, "device LDS per workgroup below 132 KiB");
     for (const void* k : {reinterpret_cast<const void*>(k_flow_plan_head), reinterpret_cast<const void*>(k_flow_plan_near),
+                          reinterpret_cast<const void*>(k_flow_plan_early),
                           reinterpret_cast<const void*>(k_flow_plan_tail_d)})
       HIPCHK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(plan_lds)));
     HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_deep_prep_b), hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -863,7 +864,7 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
     k_deep_prep_c<<<dim3(FL_PG, 1), FL_PREP_T, 0, ps>>>(Dx, Bx, FX);
     HIPCHK(hipEventRecord(xprep_done, ps));
     HIPCHK(hipEventRecord(S.evx0, ps));
-    k_flow_plan_head<<<1, 256, plan_lds, ps>>>(Dx, FX);
+    k_flow_plan_early<<<1, 256, plan_lds, ps>>>(Dx, FX);
     HIPCHK(hipEventRecord(S.evx1, ps));
     HIPCHK(hipEventRecord(xplan_done, ps));
   }

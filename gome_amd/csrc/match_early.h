@@ -19,7 +19,8 @@
 //   -- the previous batch's plan ends (plan_done) --
 //   k_x_prep_b   the price set: the previous plan's final levels (F.hdr[0] / F.lvl, that batch's
 //                header: FlowHdr::bid) plus the batch's prices; rank, the 32-bit test, XH / XL
-//   k_flow_prep_c  the packed records (into X.ord8), k_flow_plan_head (X.log, FlowArgs::xlog)
+//   k_flow_prep_c  the packed records (into X.ord8), k_flow_plan_early (k_flow_plan_head's code
+//                under its own name, for the profiles; X.log, FlowArgs::xlog)
 //
 // The batch's own pipeline still prepares the book as before (k_flow_prep_a/b/c into F).  Then
 // k_x_cmp checks that the early inputs equal the normal ones (header, levels, every packed record:

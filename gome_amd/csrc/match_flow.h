@@ -1106,6 +1106,10 @@ __device__ __forceinline__ void fl_plan_kernel(const Dev& D, const FlowArgs& F, 
 __global__ __launch_bounds__(256) void k_flow_plan_head(Dev D, FlowArgs F) {
   fl_plan_kernel<true>(D, F, uni(F.hdr[F.h0 + blockIdx.x < fl_hend(D, F) ? F.h0 + blockIdx.x : 0].ok));
 }
+// the hottest book planned early (match_early.h: right after the batch before's plan)
+__global__ __launch_bounds__(256) void k_flow_plan_early(Dev D, FlowArgs F) {
+  fl_plan_kernel<true>(D, F, uni(F.hdr[F.h0 + blockIdx.x < fl_hend(D, F) ? F.h0 + blockIdx.x : 0].ok));
+}
 // the other head books (planned on the tail's stream, beside the hottest)
 __global__ __launch_bounds__(256) void k_flow_plan_near(Dev D, FlowArgs F) {
   fl_plan_kernel<true>(D, F, uni(F.hdr[F.h0 + blockIdx.x < fl_hend(D, F) ? F.h0 + blockIdx.x : 0].ok));

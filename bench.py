@@ -585,11 +585,15 @@ def main():
         # batches in flight on the host path (--e2e-depth)
         depth = max(1, min(args.e2e_depth, GOME_MAX_INFLIGHT))
 
+        host_ms = {"submit": 0.0, "collect": 0.0}  # host time inside the two calls (timed steps)
+
         def run_pipe(lo, hi, lats):
             tsub = {}
 
             def coll(j):
+                tc = time.perf_counter()
                 ev, st = eng.collect(copy=False)
+                host_ms["collect"] += (time.perf_counter() - tc) * 1e3
                 done_ev[0] += len(ev)
                 lats.append((time.perf_counter() - tsub[j]) * 1e3)
                 if rank == 0:
@@ -597,6 +601,7 @@ def main():
             for k in range(lo, hi):
                 tsub[k] = time.perf_counter()
                 eng.submit_async(bufs[k], seq_base=seq[0])
+                host_ms["submit"] += (time.perf_counter() - tsub[k]) * 1e3
                 seq[0] += per_rank
                 if k - lo >= depth - 1:
                     coll(k - depth + 1)
@@ -609,6 +614,7 @@ def main():
             dist.barrier()
         elat = []
         done_ev[0] = 0
+        host_ms["submit"] = host_ms["collect"] = 0.0
         t1 = time.perf_counter()
         run_pipe(e2e_warm, e2e_warm + e2e_steps, elat)
         torch.cuda.synchronize()
@@ -628,6 +634,7 @@ def main():
                    "overlapped": round(max(in_b, out_b) / (pk["duplex_GBps_each"] * 1e9) * 1e3, 3),
                    "serial": round((in_b / (pk["h2d_GBps"] * 1e9) + out_b / (pk["d2h_GBps"] * 1e9)) * 1e3, 3)},
                "ms_per_step": round(e_el / e2e_steps * 1e3, 3),
+               "host_ms_per_step": {k: round(v / e2e_steps, 3) for k, v in host_ms.items()},
                "p50_batch_ms": round(pctl(elat, 0.5), 3), "p99_batch_ms": round(pctl(elat, 0.99), 3),
                "events_per_s": round(e_events / e_el, 1),
                "pcie_bytes_per_step": int(32 * per_rank * world + 48 * e_events / e2e_steps),

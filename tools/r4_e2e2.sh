@@ -9,7 +9,7 @@ for w in ${2:-config2 config3}; do
     for v in ${VARIANTS:-"d2:2:" "d3:3:" "d2s:2:GOME_D2H_STREAM=1" "d3s:3:GOME_D2H_STREAM=1"}; do
       n=${v%%:*}; r=${v#*:}; dep=${r%%:*}; e=${r#*:}; e=${e//,/ }
       env $e timeout -k 10 300 python -u bench.py --workload $w $Q --e2e-depth $dep > $O/${w}_${n}_$rep.json 2> $O/${w}_${n}_$rep.err || { tail -20 $O/${w}_${n}_$rep.err; exit 1; }
-      python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); e=d['e2e']; print(sys.argv[1], round(e['value']/1e6,1), e['ms_per_step'], e['p50_batch_ms'], e['pcie_bound_ms'])" $O/${w}_${n}_$rep.json
+      python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); e=d['e2e']; print(sys.argv[1], round(e['value']/1e6,1), e['ms_per_step'], e['p50_batch_ms'], e['host_ms_per_step'])" $O/${w}_${n}_$rep.json
     done
   done
 done

@@ -13,7 +13,7 @@ import pytest
 
 import bench
 from gome_amd import workload as wl
-from gome_amd.abi import GOME_ORD_ADM_HOST, GOME_ORD_ADMITTED, Engine
+from gome_amd.abi import GOME_E_INVAL, GOME_ORD_ADM_HOST, GOME_ORD_ADMITTED, Engine, GomeError
 from oracle.pyoracle import Oracle
 from tests.test_gpu_v4 import _cmp, _cmp_books, _hot_and_random
 
@@ -138,6 +138,40 @@ def test_early_plans_of_pipelined_host_batches_are_exact():
     assert sum(early[3:]) >= 4, early
     z = wl.ZipfSymbols(100000, 1.0)
     _cmp_books(eng, orc, _hot_and_random(z, 100000, k_rand=30), "host early")
+
+
+def test_rejected_batch_between_early_plans():
+    """A batch the engine rejects (a record outside the domain: nothing of it is applied) while the
+    next batch's early plan is already being prepared from it: that plan must not be taken, and
+    the batches after it are exact and planned early again."""
+    import torch
+    gen, _, _ = bench.shard_stream(100000, 1.0, 0, 1, 33)
+    batches = [gen(N).copy() for _ in range(9)]
+    batches[4]["symbol_id"][777] = 100000  # (>= max_symbols: the whole batch is rejected)
+    eng = Engine(max_symbols=100000, max_batch=N, max_nodes=13 * N, max_levels=1 << 22)
+    orc = Oracle(100000)
+    dev = [torch.from_numpy(b.view(np.uint8).copy()).cuda() for b in batches]
+    torch.cuda.synchronize()
+    exp = [None if k == 4 else orc.submit(b) for k, b in enumerate(batches)]
+    early, got, nxt = [], [], 0
+    for k in range(len(batches)):
+        while nxt < len(batches) and nxt < k + 3:
+            eng.submit_device_async(dev[nxt].data_ptr(), N, 0)
+            nxt += 1
+        if k == 4:
+            with pytest.raises(GomeError) as ei:
+                eng.collect_device()
+            assert ei.value.status == GOME_E_INVAL
+            early.append(0)
+            continue
+        _, n, st = eng.collect_device()
+        assert n == len(exp[k]), f"batch {k}"
+        early.append(int(st["n_early"]))
+        assert int(st["n_early_miss"]) == 0, k
+    _cmp(eng.drain(), np.concatenate([e for e in exp if e is not None]), "around a rejected batch")
+    assert early[5] == 0 and sum(early[6:]) >= 2, early
+    z = wl.ZipfSymbols(100000, 1.0)
+    _cmp_books(eng, orc, _hot_and_random(z, 100000, k_rand=30), "around a rejected batch")
 
 
 def test_early_plan_off_is_the_same_engine(monkeypatch):

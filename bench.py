@@ -586,6 +586,7 @@ def main():
         depth = max(1, min(args.e2e_depth, GOME_MAX_INFLIGHT))
 
         host_ms = {"submit": 0.0, "collect": 0.0}  # host time inside the two calls (timed steps)
+        tdone = []  # host time of each collect's return (the steady-state interval: their median gap)
 
         def run_pipe(lo, hi, lats):
             tsub = {}
@@ -594,6 +595,7 @@ def main():
                 tc = time.perf_counter()
                 ev, st = eng.collect(copy=False)
                 host_ms["collect"] += (time.perf_counter() - tc) * 1e3
+                tdone.append(time.perf_counter())
                 done_ev[0] += len(ev)
                 lats.append((time.perf_counter() - tsub[j]) * 1e3)
                 if rank == 0:
@@ -615,6 +617,7 @@ def main():
         elat = []
         done_ev[0] = 0
         host_ms["submit"] = host_ms["collect"] = 0.0
+        tdone.clear()
         t1 = time.perf_counter()
         run_pipe(e2e_warm, e2e_warm + e2e_steps, elat)
         torch.cuda.synchronize()
@@ -635,6 +638,9 @@ def main():
                    "serial": round((in_b / (pk["h2d_GBps"] * 1e9) + out_b / (pk["d2h_GBps"] * 1e9)) * 1e3, 3)},
                "ms_per_step": round(e_el / e2e_steps * 1e3, 3),
                "host_ms_per_step": {k: round(v / e2e_steps, 3) for k, v in host_ms.items()},
+               # the median gap between two batches' collects: the pipeline's steady-state step,
+               # without the fill (the first H2D) and drain (the last D2H) that a K-step job adds
+               "steady_ms_per_step": round(float(np.median(np.diff(tdone))) * 1e3, 3) if len(tdone) > 2 else None,
                "p50_batch_ms": round(pctl(elat, 0.5), 3), "p99_batch_ms": round(pctl(elat, 0.99), 3),
                "events_per_s": round(e_events / e_el, 1),
                "pcie_bytes_per_step": int(32 * per_rank * world + 48 * e_events / e2e_steps),

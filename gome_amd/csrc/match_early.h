@@ -5,9 +5,11 @@
 // config 3: the previous batch's reconstruction and publish, then the next batch's sort,
 // admission and head prep.  The plan needs none of it: a book's plan reads only its level
 // aggregates (price, depth, side: the plan's own final state, FlowHdr / FlowLvl) and the batch's
-// packed records of that book.  So for a pipelined device batch (gome_submit_batch_device_async)
-// whose hottest book was also the previous batch's hottest book on an ADD plan, the engine
-// prepares and plans that book on the copy stream as soon as the previous plan ends:
+// packed records of that book.  So for a pipelined batch (gome_submit_batch_device_async or
+// gome_submit_batch_async) whose hottest book was also the previous batch's hottest book on an ADD
+// plan (lane or deep), the engine prepares and plans that book as soon as the previous plan ends
+// (device batches: the record work on the early stream, the rest on the copy stream; host batches:
+// the record work behind the H2D on the copy stream, the rest on the early stream):
 //
 //   k_x_count / k_x_scan / k_x_scatter  the records of the previous batch's hottest symbol, in
 //                batch order, at the positions the batch's stable sort will give them (the sort
@@ -21,6 +23,8 @@
 //                header: FlowHdr::bid) plus the batch's prices; rank, the 32-bit test, XH / XL
 //   k_flow_prep_c  the packed records (into X.ord8), k_flow_plan_early (k_flow_plan_head's code
 //                under its own name, for the profiles; X.log, FlowArgs::xlog)
+// Deep books take k_xd_prep_a / k_xd_sort_new (beside the previous plan) and k_xd_prep_b /
+// k_deep_prep_c after it instead of the lane preps (below).
 //
 // The batch's own pipeline still prepares the book as before (k_flow_prep_a/b/c into F).  Then
 // k_x_cmp checks that the early inputs equal the normal ones (header, levels, every packed record:

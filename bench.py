@@ -743,6 +743,8 @@ def main():
             # previous batch's plan), and early plans not taken although ready (0 unless a bug)
             "early_plans": int(sum(s.get("n_early", 0) for s in sts)),
             "early_miss": int(sum(s.get("n_early_miss", 0) for s in sts)),
+            "adm_ahead": int(sum(s.get("n_adm_ahead", 0) for s in sts)),
+            "adm_redo": int(sum(s.get("n_adm_redo", 0) for s in sts)),
             "match_books_ms": round(ms_match, 3),
             "kernel_ms": {k: round(v[0], 3) for k, v in sorted(cands.items(), key=lambda kv: -kv[1][0])},
             "kernel_ms_source": phase_src,

@@ -97,7 +97,8 @@ enum {
   C_QUIRK_CHECKED, C_REQUAL,                              // quirk books checked / requalified (k_requalify)
   C_HEAD_ADD,                                             // the hottest book went through an ADD plan
   C_EARLY, C_EARLY_MISS,                                  // its plan was the early one / could not be (match_early.h)
-  C_NCTR = 30
+  C_ADM_AHEAD, C_ADM_REDO,                                // admission ran ahead / ran again (k_adm_verify)
+  C_NCTR = 32
 };
 
 // Level blocks (a book's sorted level array) come in power-of-two capacities 16 << c.  A

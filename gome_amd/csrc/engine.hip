@@ -234,6 +234,7 @@ struct Slot {
   hipEvent_t ev0{}, ev1{}, evm0{}, evm1{}, evh0{}, evh1{}, evf0{}, evf1{}, evc0{}, evc1{};
   hipEvent_t evx0{}, evx1{};  // the early plan (match_early.h), when the batch enqueued one
   bool early = false;
+  uint32_t* adm_v = nullptr;  // the batch's verdicts when its admission ran ahead (k_adm_verify)
   hipEvent_t h2d{}, done{};
   hipEvent_t ph[GOME_NPHASE][2]{};  // GOME_PH_* phase brackets (ph_on: recorded this batch)
   bool ph_on[GOME_NPHASE]{};
@@ -290,6 +291,12 @@ struct gome_engine {
   unsigned long long *x_dkey = nullptr, *x_dnew = nullptr;
   uint32_t *x_dval = nullptr, *x_dslot = nullptr;
   bool early_on = true;            // GOME_EARLY=0: never
+  // pipelined device batches of a dominated stream that plan late: admission ahead, on the early
+  // stream beside the last batch's plan (k_adm_verify; GOME_ADM_AHEAD=0: never)
+  bool adm_ahead_on = true;
+  hipEvent_t adm_pre_done{};
+  Status* d_adm_st = nullptr;      // the ahead pass's input errors
+  uint32_t* d_adm_redo = nullptr;  // k_adm_verify: the batch's own admission runs again
   // a batch with an early plan runs its cold books on the early stream, after the next batch's early
   // record work (A/B on one box: config 3 +0.3..0.7%, config 5 even; GOME_COLD_EARLY=0: the caller's)
   bool cold_early = true;
@@ -407,7 +414,7 @@ struct gome_engine {
     }
     for (hipEvent_t ev : {fork, join, joinf, prep_h, prep_t, fork_adm, adm_done, seg_done, dp_fork, cnt_fork, cnt_done,
                           dw_done, dl_done, tl_done, tob_done, plan_done, oidmax_done, xpre_done, xprep_done,
-                          xplan_done})
+                          xplan_done, adm_pre_done})
       if (ev) (void)hipEventDestroy(ev);
     if (h_tob_syms) (void)hipHostFree(h_tob_syms);
     if (h_tob) (void)hipHostFree(h_tob);
@@ -485,7 +492,7 @@ gome_status gome_engine::init(const gome_config& c) {
     HIPCHK(hipStreamCreateWithFlags(&d2h_stream, hipStreamNonBlocking));
   for (hipEvent_t* ev : {&fork, &join, &joinf, &prep_h, &prep_t, &fork_adm, &adm_done, &seg_done,
                          &dp_fork, &cnt_fork, &cnt_done, &dw_done, &dl_done, &tl_done, &tob_done, &plan_done,
-                         &oidmax_done, &xpre_done, &xprep_done, &xplan_done})
+                         &oidmax_done, &xpre_done, &xprep_done, &xplan_done, &adm_pre_done})
     HIPCHK(hipEventCreateWithFlags(ev, hipEventDisableTiming));
   for (Slot& S : slots) {
     for (hipEvent_t* ev : {&S.ev0, &S.ev1, &S.evm0, &S.evm1, &S.evh0, &S.evh1, &S.evf0, &S.evf1, &S.evc0, &S.evc1,
@@ -533,6 +540,7 @@ gome_status gome_engine::init(const gome_config& c) {
     const char* q = std::getenv("GPU_MAX_HW_QUEUES");
     cold_main = !q || std::atoi(q) < 8;
     early_on = !cold_main;  // (the early plan's stream needs a queue of its own too)
+    adm_ahead_on = !cold_main;
   }
   if (const char* g = std::getenv("GOME_COLD_MAIN")) cold_main = std::atoi(g) != 0;            // (A/B)
   if (const char* g = std::getenv("GOME_COLD_OWN"); g && std::atoi(g) != 0)                   // (A/B)
@@ -614,9 +622,11 @@ gome_status gome_engine::init(const gome_config& c) {
       !alloc(&d_prep, nb, "prep") || !alloc(&d_pend, nb, "pending inserts") ||
       !alloc(&d_resume, MAX_HOT, "resume records") || !alloc(&d_arena, arena_cap, "event arena"))
     return GOME_E_CAPACITY;
+  if (!alloc(&d_adm_st, 1, "ahead admission status") || !alloc(&d_adm_redo, 1, "ahead admission redo"))
+    return GOME_E_CAPACITY;
   for (Slot& S : slots) {
     if (!alloc(&S.d_orders, nb, "orders") || !alloc(&S.d_events, arena_cap, "events") ||
-        !alloc(&S.d_dup, nb, "duplicate-oid list"))
+        !alloc(&S.d_dup, nb, "duplicate-oid list") || !alloc(&S.adm_v, nb, "ahead verdicts"))
       return GOME_E_CAPACITY;
     S.ev_cap = arena_cap;
   }
@@ -655,7 +665,8 @@ gome_status gome_engine::init(const gome_config& c) {
   for (XBuf& X : xb) HIPCHK(hipMemsetAsync(X.ctl, 0, sizeof(XCtl), stream));
   HIPCHK(hipMemsetAsync(x_dslot, 0, 4, stream));  // (the early deep book is deep slot 0's)
   if (const char* g = std::getenv("GOME_EARLY")) early_on = std::atoi(g) != 0;
-  if (early_on) HIPCHK(hipStreamCreateWithFlags(&early_stream, hipStreamNonBlocking));
+  if (const char* g = std::getenv("GOME_ADM_AHEAD")) adm_ahead_on = std::atoi(g) != 0;
+  if (early_on || adm_ahead_on) HIPCHK(hipStreamCreateWithFlags(&early_stream, hipStreamNonBlocking));
   if (const char* g = std::getenv("GOME_COLD_EARLY")) cold_early = std::atoi(g) != 0;
   // books with DELs (match_flow_cancel.h): per-position scratch, the (symbol, oid)
   // table (generation-tagged: cleared once per 2048 batches)
@@ -770,6 +781,7 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   // after a batch whose hottest book took an ADD plan (the device checks the rest)
   const bool early = early_on && (ahead || copy_busy) && dominant && head_add != 0 && bid > 0 && F.enabled;
   S.early = early;
+  const bool adm_ahead = adm_ahead_on && ahead && dominant && !early && early_stream != nullptr;
   const uint32_t bid_prev = bid;
   F.bid = ++bid;
   // per-batch status reset (free_top / freed_top and the level pools persist); admission
@@ -871,20 +883,46 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
 
   // admission markers depend on the input records only: they run on the flow stream beside
   // the validation, the radix sort and the segmentation (the batch's critical path), enqueued
-  // after the sort so that the main stream's first kernels reach the GPU first
+  // after the sort so that the main stream's first kernels reach the GPU first.  Ahead (the batch
+  // before it in its hottest plan): on the early stream as soon as that batch's admission is done,
+  // without the resting probe; the flow stream then checks that no probe could find a key
+  // (k_adm_verify) and runs the passes again, with it, where one could.
+  uint32_t* const adm_v = adm_ahead ? S.adm_v : d_adm_slot;
+  auto admission = [&](hipStream_t as, Status* ast, bool noprobe, const uint32_t* gate) {
+    k_adm<<<gN, T256, 0, as>>>(d_ord, n, d_adm, adm_v, adm_mask, cfg.max_symbols, ast, D.books, D.idx, D.idx_mask,
+                               d_oid_max, d_multi, d_adm_ctl + 1, noprobe, gate);
+    k_adm_flag<<<gN, T256, 0, as>>>(d_ord, n, adm_v, d_multi, d_dup, d_adm_slot2, d_adm_aux, adm_mask, d_adm,
+                                    d_adm_ctl + 1, gate);
+    k_adm_res<<<gN, T256, 0, as>>>(d_ord, n, adm_v, d_dup, d_adm_slot2, d_first, d_adm_ctl + 1, gate);
+    k_adm_dup<<<gN, T256, 0, as>>>(n, adm_v, d_first, d_adm_ctl + 1, gate);
+    k_adm_clean<<<gN, T256, 0, as>>>(n, d_adm_aux, d_adm_slot2, d_dup, d_first, d_multi, d_adm_ctl + 1, gate);
+  };
+  if (adm_ahead) {
+    HIPCHK(hipStreamWaitEvent(early_stream, adm_done, 0));  // (the tables, the watermark: the last batch's admission)
+    HIPCHK(hipStreamWaitEvent(early_stream, prep_h, 0));    // (after the last batch's head prep: its plan runs)
+    HIPCHK(hipMemsetAsync(d_adm_st, 0, offsetof(Status, free_top), early_stream));
+    HIPCHK(hipMemsetAsync(d_adm_redo, 0, 4, early_stream));
+    k_adm_ctl<<<1, 1, 0, early_stream>>>(d_adm_ctl, adm_fast ? 1u : 0u);
+    k_adm_pre<<<std::min<uint32_t>(gN, 1024), T256, 0, early_stream>>>(d_ord, n, d_adm_ctl);
+    admission(early_stream, d_adm_st, true, nullptr);
+    HIPCHK(hipEventRecord(adm_pre_done, early_stream));
+  }
   HIPCHK(hipStreamWaitEvent(flow_stream, fork_adm, 0));
-  k_adm_ctl<<<1, 1, 0, flow_stream>>>(d_adm_ctl, adm_fast ? 1u : 0u);
-  k_adm_pre<<<std::min<uint32_t>(gN, 1024), T256, 0, flow_stream>>>(d_ord, n, d_adm_ctl);
+  if (!adm_ahead) {
+    k_adm_ctl<<<1, 1, 0, flow_stream>>>(d_adm_ctl, adm_fast ? 1u : 0u);
+    k_adm_pre<<<std::min<uint32_t>(gN, 1024), T256, 0, flow_stream>>>(d_ord, n, d_adm_ctl);
+  }
   if ((++fc_gen & FC_GEN_MASK) == 0) HIPCHK(hipMemsetAsync(F.fc_hash, 0, sizeof(FcHash) * fc_hcap, flow_stream));
   F.fc_gen = fc_gen;
   HIPCHK(mark(GOME_PH_ADMISSION, 0, flow_stream));
-  k_adm<<<gN, T256, 0, flow_stream>>>(d_ord, n, d_adm, d_adm_slot, adm_mask, cfg.max_symbols, d_st, D.books, D.idx,
-                                      D.idx_mask, d_oid_max, d_multi, d_adm_ctl + 1);
-  k_adm_flag<<<gN, T256, 0, flow_stream>>>(d_ord, n, d_adm_slot, d_multi, d_dup, d_adm_slot2, d_adm_aux, adm_mask,
-                                           d_adm, d_adm_ctl + 1);
-  k_adm_res<<<gN, T256, 0, flow_stream>>>(d_ord, n, d_adm_slot, d_dup, d_adm_slot2, d_first, d_adm_ctl + 1);
-  k_adm_dup<<<gN, T256, 0, flow_stream>>>(n, d_adm_slot, d_first, d_adm_ctl + 1);
-  k_adm_clean<<<gN, T256, 0, flow_stream>>>(n, d_adm_aux, d_adm_slot2, d_dup, d_first, d_multi, d_adm_ctl + 1);
+  if (adm_ahead) {
+    HIPCHK(hipStreamWaitEvent(flow_stream, adm_pre_done, 0));
+    k_adm_verify<<<gN, T256, 0, flow_stream>>>(d_ord, n, D.books, d_oid_max, cfg.max_symbols, d_adm_redo, d_st,
+                                               d_adm_st);
+    admission(flow_stream, d_st, false, d_adm_redo);
+  } else {
+    admission(flow_stream, d_st, false, nullptr);
+  }
   HIPCHK(mark(GOME_PH_ADMISSION, 1, flow_stream));
   HIPCHK(hipEventRecord(adm_done, flow_stream));
 
@@ -899,7 +937,7 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   B.arena_cap = arena_cap;
   B.ev_count = d_ev_count;
   B.sidx = sidx;
-  B.adm_flag = d_adm_slot;
+  B.adm_flag = adm_v;
   B.seq_base = seq_base;
   B.dup_list = S.d_dup;
   const uint32_t grid = std::min<uint32_t>(n, cfg.max_symbols);
@@ -1035,7 +1073,7 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   // ---- match_books: one wavefront per book; hot books (LDS) on a second stream,
   //      concurrently with the cold books (HBM)
   HIPCHK(mark(GOME_PH_RECORDS, 0, s));
-  k_prep<<<gN, T256, 0, s>>>(d_ord, n, sidx, d_adm_slot, d_prep);
+  k_prep<<<gN, T256, 0, s>>>(d_ord, n, sidx, adm_v, d_prep);
   HIPCHK(mark(GOME_PH_RECORDS, 1, s));
   HIPCHK(hipEventRecord(S.evm0, s));
   HIPCHK(hipMemsetAsync(F.ig_bump, 0, 4, s));
@@ -1259,6 +1297,8 @@ gome_status gome_engine::finish(uint32_t sl, uint32_t n) {
   head_add = ((head_add << 1) | (st.ctr[C_HEAD_ADD] != 0 ? 1u : 0u)) & 3u;
   stats.n_early = st.ctr[C_EARLY];
   stats.n_early_miss = st.ctr[C_EARLY_MISS];
+  stats.n_adm_ahead = st.ctr[C_ADM_AHEAD];
+  stats.n_adm_redo = st.ctr[C_ADM_REDO];
   stats.ms_hot = ms_hot;
   stats.ms_flow_plan = ms_flow;
   stats.n_flow_books = st.ctr[C_FLOW_BOOKS];

@@ -342,11 +342,16 @@ __global__ void k_adm_pre(const gome_order* ord, uint32_t n, uint32_t* ctl) {
   if (threadIdx.x == 0 && bmax) atomicMax(&ctl[2], bmax);  // (one device atomic per block)
 }
 
+// noprobe (admission ahead of the batch, see k_adm_verify): no resting probe, every verdict as if
+// the key did not rest.  gate (the batch's own admission after an ahead pass that cannot stand):
+// the kernel runs only when *gate is set.
 __global__ void k_adm(const gome_order* ord, uint32_t n, unsigned long long* tab, uint32_t* slot, uint32_t mask,
                       uint32_t max_symbols, Status* st, const Book* books, const IdxEnt* idx,
-                      unsigned long long idx_mask, const uint32_t* oid_max, uint8_t* multi, const uint32_t* notfast) {
+                      unsigned long long idx_mask, const uint32_t* oid_max, uint8_t* multi, const uint32_t* notfast,
+                      bool noprobe = false, const uint32_t* gate = nullptr) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
+  if (i >= n || (gate && !*gate)) return;
+  if (i == 0 && gate) atomicAdd(&st->ctr[C_ADM_REDO], 1ull);
   const gome_order g = ord[i];
   {
     const int64_t lim = 1ll << 53;
@@ -362,8 +367,8 @@ __global__ void k_adm(const gome_order* ord, uint32_t n, unsigned long long* tab
     return;
   }
   if (g.action != GOME_ADD && g.action != GOME_DEL) { slot[i] = NIL; return; }
-  const bool resting = g.action == GOME_ADD && g.oid_id <= oid_max[g.symbol_id] && books[g.symbol_id].n_lvl != 0 &&
-                       idx_live(idx, idx_mask, key_so(g));
+  const bool resting = !noprobe && g.action == GOME_ADD && g.oid_id <= oid_max[g.symbol_id] &&
+                       books[g.symbol_id].n_lvl != 0 && idx_live(idx, idx_mask, key_so(g));
   bool repeat;
   const uint32_t h = adm_insert(tab, mask, mix64(key_so(g)), i, [&](uint32_t c) {
     const gome_order q = ord[c];
@@ -378,9 +383,9 @@ __global__ void k_adm(const gome_order* ord, uint32_t n, unsigned long long* tab
 // slot | ADM_MULTI.  aux[i] = the (S, oid) slot of a shared key's record, else NIL (k_adm_clean).
 __global__ void k_adm_flag(const gome_order* ord, uint32_t n, uint32_t* slot, const uint8_t* multi,
                            unsigned long long* tab2, uint32_t* slot2, uint32_t* aux, uint32_t mask,
-                           unsigned long long* tab, const uint32_t* notfast) {
+                           unsigned long long* tab, const uint32_t* notfast, const uint32_t* gate = nullptr) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n || !*notfast) return;
+  if (i >= n || !*notfast || (gate && !*gate)) return;
   const uint32_t s = slot[i];
   const bool shared = s != NIL && multi[s & ADM_SLOT];
   if (s != NIL) tab[s & ADM_SLOT] = 0ull;  // (k_adm's probes are over: the table is left empty)
@@ -406,9 +411,10 @@ __global__ void k_adm_flag(const gome_order* ord, uint32_t n, uint32_t* slot, co
 // Pass 3 (shared keys): the batch rule / host verdict; an admitted ADD offers its index as the
 // key's first admitted ADD (first[] is NIL between batches).
 __global__ void k_adm_res(const gome_order* ord, uint32_t n, uint32_t* slot, const unsigned long long* tab2,
-                          const uint32_t* slot2, uint32_t* first, const uint32_t* notfast) {
+                          const uint32_t* slot2, uint32_t* first, const uint32_t* notfast,
+                          const uint32_t* gate = nullptr) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n || !*notfast) return;
+  if (i >= n || !*notfast || (gate && !*gate)) return;
   const uint32_t s = slot[i];
   if (!(s & ADM_MULTI)) return;
   const gome_order g = ord[i];
@@ -422,14 +428,39 @@ __global__ void k_adm_res(const gome_order* ord, uint32_t n, uint32_t* slot, con
 
 // Pass 4 (shared keys): final verdicts; an admitted ADD that is not its key's first admitted ADD,
 // or whose oid rests at batch start, is a candidate of the duplicate-oid rule (ADM_V_CHECK).
-__global__ void k_adm_dup(uint32_t n, uint32_t* slot, const uint32_t* first, const uint32_t* notfast) {
+__global__ void k_adm_dup(uint32_t n, uint32_t* slot, const uint32_t* first, const uint32_t* notfast,
+                          const uint32_t* gate = nullptr) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n || !*notfast) return;
+  if (i >= n || !*notfast || (gate && !*gate)) return;
   const uint32_t s = slot[i];
   if (!(s & ADM_MULTI)) return;
   const bool adm = (s & ADM_OK) != 0;
   const bool check = adm && ((s & ADM_RESTING) || first[s & ADM_SLOT] != i);
   slot[i] = !adm ? ADM_V_NO : check ? ADM_V_CHECK : ADM_V_YES;
+}
+
+// Admission ahead of the batch (pipelined batches while the one before is in its hottest plan):
+// the same passes on another stream, without the resting probe (the books are still changing), into
+// the batch slot's own verdicts.  The probe is the only input of the verdicts beyond the records,
+// and at the batch's own time (the books final) it can only find a key where an ADD's oid is at or
+// below its book's oid_max and the book is not empty; where none is, every ahead verdict is the
+// one the batch's own admission would give.  Else *redo is set and the passes run again, with the
+// probe (gated on *redo; the ahead pass left the tables empty).  The ahead pass's input errors (its
+// own Status, ast) join the batch's.
+__global__ void k_adm_verify(const gome_order* ord, uint32_t n, const Book* books, const uint32_t* oid_max,
+                             uint32_t max_symbols, uint32_t* redo, Status* st, const Status* ast) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i == 0) {
+    if (ast->err) atomicOr(&st->err, ast->err);
+    atomicAdd(&st->ctr[C_ADM_AHEAD], 1ull);
+  }
+  bool cand = false;
+  if (i < n) {
+    const gome_order g = ord[i];
+    cand = g.action == GOME_ADD && g.symbol_id < max_symbols && g.oid_id <= oid_max[g.symbol_id] &&
+           books[g.symbol_id].n_lvl != 0;
+  }
+  if (__any(cand) && lane_id() == 0) atomicOr(redo, 1u);
 }
 
 // An ADD with verdict ADM_V_CHECK that the serial kernels found live: rejected (one thread).
@@ -439,9 +470,10 @@ __device__ __forceinline__ void dup_note(Status* st, uint32_t* list, uint32_t i)
 
 // Pass 5 (shared keys): their entries of the second table, first[] and multi[] back to empty.
 __global__ void k_adm_clean(uint32_t n, const uint32_t* aux, const uint32_t* slot2, unsigned long long* tab2,
-                            uint32_t* first, uint8_t* multi, const uint32_t* notfast) {
+                            uint32_t* first, uint8_t* multi, const uint32_t* notfast,
+                            const uint32_t* gate = nullptr) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n || !*notfast) return;
+  if (i >= n || !*notfast || (gate && !*gate)) return;
   const uint32_t h = aux[i];
   if (h == NIL) return;
   tab2[slot2[i]] = 0ull;

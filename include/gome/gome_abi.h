@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define GOME_ABI_VERSION 9u
+#define GOME_ABI_VERSION 10u
 
 /* ---- status codes (replace the reference's swallowed errors / panics,
  *      rabbitmq.go:44-49,70-72,120-122; nodelink.go:132,142,157) ---------- */
@@ -249,6 +249,11 @@ typedef struct gome_stats {
   uint64_t n_early_miss;                      /* an early plan the batch could not take although
                                                  its hottest book went through the same plan
                                                  (0 unless something is wrong; ABI >= 9)   */
+  uint64_t n_adm_ahead;                       /* 1 when the batch's admission ran ahead, beside
+                                                 the previous batch's plan (pipelined device
+                                                 batches, ABI >= 10)                       */
+  uint64_t n_adm_redo;                        /* ... and ran again at the batch's own time: an
+                                                 ADD's key might rest (ABI >= 10)           */
 } gome_stats;
 
 typedef struct gome_engine gome_engine;

@@ -1080,10 +1080,13 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   HIPCHK(hipEventRecord(fork, s));
   HIPCHK(hipStreamWaitEvent(flow_stream, fork, 0));  // (k_prep, the gather bump)
   // deep books: the two-pass level sort and the per-level reconstruction, then the writes
-  auto deep_sort_level = [&](const FlowArgs& R, uint32_t tiles, hipStream_t st) {
+  // (per_level: the hottest book's; with DELs its levels go to k_deep_level_hot)
+  auto deep_sort_level = [&](const FlowArgs& R, uint32_t tiles, hipStream_t st, bool per_level) {
     const uint32_t ns = std::min<uint32_t>(R.ds1 - R.ds0, DEEP_GRID_T);  // (blocks walk the slots)
     deep_sort(R, tiles, st);
-    k_deep_level<<<dim3(DEEP_GRID, ns), 64, 0, st>>>(D, R);
+    const bool hot = per_level && c_canc;
+    k_deep_level<<<dim3(DEEP_GRID, ns), 64, 0, st>>>(D, R, hot ? 1u : 0u);
+    if (hot) k_deep_level_hot<<<DEEP_GRID / 16, FC_LVB_T, 0, st>>>(D, R);
   };
   auto deep_write = [&](const FlowArgs& R, hipStream_t st) {
     const uint32_t ns = std::min<uint32_t>(R.ds1 - R.ds0, DEEP_GRID_T);  // (blocks walk the slots)
@@ -1098,18 +1101,20 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   // cs != st they run beside the writes; k_flow_count still comes after both level passes.
   // fused: the books' events go to the arena, and k_flow_events_fused counts them there (no
   // k_flow_count).
-  auto head_recon = [&](const FlowArgs& R, uint32_t nb, hipStream_t st, hipStream_t cs, bool fused) -> gome_status {
+  // pl: the hottest book (a wave per level of a deep book with DELs)
+  auto head_recon = [&](const FlowArgs& R, uint32_t nb, hipStream_t st, hipStream_t cs, bool fused,
+                        bool pl) -> gome_status {
     const bool split = cs != st;
     if (split) {  // the deep books' level sort (other books than the ones below) beside it
       HIPCHK(hipEventRecord(dp_fork, st));
       HIPCHK(hipStreamWaitEvent(cs, dp_fork, 0));
-      if (c_deep) deep_sort_level(R, FL_SORT_GRID, cs);
+      if (c_deep) deep_sort_level(R, FL_SORT_GRID, cs, pl);
       HIPCHK(hipEventRecord(dl_done, cs));  // (a deep book with DELs: k_fc_count / events wait)
     }
     k_flow_sort_cnt<<<dim3(FL_SORT_GRID, nb), FL_TILE, 0, st>>>(D, R);
     k_flow_sort_scan<<<nb, FL_CAP * FL_SCAN_P, 0, st>>>(D, R);
     k_flow_sort_scatter<<<dim3(FL_SORT_GRID, nb), FL_TILE, 0, st>>>(D, R);
-    if (!split && c_deep) deep_sort_level(R, FL_SORT_GRID, st);
+    if (!split && c_deep) deep_sort_level(R, FL_SORT_GRID, st, pl);
     k_flow_level_wide<<<dim3(FL_CAP, nb), FL_LVB_T, 0, st>>>(D, R);
     toff(R, false, st);
     if (split) {
@@ -1183,7 +1188,7 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
     HIPCHK(mark(GOME_PH_TAIL_SORT, 1, s));
     HIPCHK(mark(GOME_PH_TAIL_LEVEL, 0, s));
     k_flow_level<<<nh_tail, FL_LEVEL_T, 0, s>>>(D, FT);
-    if (c_deep) deep_sort_level(FT, 32, s);
+    if (c_deep) deep_sort_level(FT, 32, s, false);
     HIPCHK(mark(GOME_PH_TAIL_LEVEL, 1, s));
     HIPCHK(mark(GOME_PH_TAIL_COUNT, 0, s));
     toff(FT, false, s);
@@ -1212,7 +1217,7 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   }
   HIPCHK(hipStreamWaitEvent(hot_stream, fork, 0));  // (their reconstruction reads k_prep's records)
   if (nh_near) {
-    if (head_recon(FH1, nh_near, hot_stream, hot_stream, true) != GOME_OK) return GOME_E_DEVICE;
+    if (head_recon(FH1, nh_near, hot_stream, hot_stream, true, false) != GOME_OK) return GOME_E_DEVICE;
     if (head_recon_c(FH1, FH1c, nh_near, hot_stream, false) != GOME_OK) return GOME_E_DEVICE;
     k_flow_events_fused<<<1024, FL_EV_T, 0, hot_stream>>>(D, B, FH1);
     HIPCHK(mark(GOME_PH_NEAR, 1, hot_stream));
@@ -1236,7 +1241,7 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   HIPCHK(hipEventRecord(join, hot_stream));
   // (the hot stream's own work ended long before the hottest book's plan does)
   HIPCHK(mark(GOME_PH_HEAD_RECON, 0, flow_stream));
-  if (head_recon(FH0, 1, flow_stream, hot_stream, false) != GOME_OK) return GOME_E_DEVICE;
+  if (head_recon(FH0, 1, flow_stream, hot_stream, false, true) != GOME_OK) return GOME_E_DEVICE;
   if (head_recon_c(FH0, FH0c, 1, flow_stream, true) != GOME_OK) return GOME_E_DEVICE;
   HIPCHK(mark(GOME_PH_HEAD_RECON, 1, flow_stream));
   HIPCHK(hipEventRecord(joinf, flow_stream));

@@ -1055,7 +1055,7 @@ __device__ __forceinline__ void fc_level_blk(const Dev& D, const FlowArgs& F, ui
   __shared__ uint32_t nr_s, ncan_s;
   const FlowHdr* hd = &F.hdr[h];
   const uint32_t tid = threadIdx.x, lane = lane_id();
-  FlowLvl* Lq = &F.lvl[h * FL_CAP + q];
+  FlowLvl* Lq = fl_lvls(F, h) + q;  // (a lane book's F.lvl row, or a deep book's level table)
   const uint32_t beg = hd->beg;
   const uint32_t L = FL_TOUCH_MUL * beg;
   const unsigned long long g = static_cast<unsigned long long>(hd->g);

@@ -533,9 +533,9 @@ __global__ __launch_bounds__(256) void k_deep_runs(Dev D, FlowArgs F) {
 // ~10k) and most see no touch in a batch; the prep left those in the state fl_level_one would give
 // them (nothing consumed or rested, every old node live, ig_all).  A wave takes the levels whose
 // run starts in its 64 sorted touches.
-__device__ __forceinline__ void k_deep_level_one(Dev D, FlowArgs F, uint32_t slot_i) {
+__device__ __forceinline__ void k_deep_level_one(Dev D, FlowArgs F, uint32_t slot_i, uint32_t skip_dc) {
   const uint32_t h = fd_book(D, F, slot_i);
-  if (!fd_deep(F, h)) return;
+  if (!fd_deep(F, h) || (skip_dc && F.hdr[h].dc)) return;
   const uint32_t nt = F.hdr[h].ntouch, L = FL_TOUCH_MUL * F.hdr[h].beg;
   FlowLvl* LV = fl_lvls(F, h);
   const SEnt* R = F.srt + L;
@@ -558,10 +558,49 @@ __device__ __forceinline__ void k_deep_level_one(Dev D, FlowArgs F, uint32_t slo
     }
   }
 }
-__global__ __launch_bounds__(64) void k_deep_level(Dev D, FlowArgs F) {
+// skip_dc: books with DELs are k_deep_level_hot's (the hottest book's launch)
+__global__ __launch_bounds__(64) void k_deep_level(Dev D, FlowArgs F, uint32_t skip_dc) {
   for (uint32_t i = blockIdx.y; i < fd_nslots(F); i += gridDim.y) {
-    k_deep_level_one(D, F, i);
+    k_deep_level_one(D, F, i, skip_dc);
     __syncthreads();
+  }
+}
+
+// The hottest book's levels after its plan when it has DELs (the batch's critical path).  Its
+// busiest levels carry tens of thousands of touches: on config 5c's streams the aggressive orders'
+// remainders rest at 1.00 / 0.01 and every ordinary order of the other side consumes there, and
+// one wave took 64 of those touches at a time (1.7 ms of k_deep_level).  Here a block takes each
+// level of FC_BIG touches or more (fc_level_blk), then its waves the others, one level each.
+// A level's run counts only where the sorted touches hold exactly it: base / pad1 of a level the
+// cancel prep's key sort gave a run that no touch reached are still that sort's.
+constexpr uint32_t FC_BIG = 1024;
+__device__ __forceinline__ uint32_t fd_run(const FlowLvl* LV, const SEnt* R, uint32_t nt, uint32_t q) {
+  const uint32_t e = LV[q].pad1, b = LV[q].base;
+  const bool ok = e != 0 && e <= nt && b < e && R[b].lvl == q && R[e - 1].lvl == q && (b == 0 || R[b - 1].lvl != q) &&
+                  (e == nt || R[e].lvl != q);
+  return ok ? e - b : 0u;
+}
+__global__ __launch_bounds__(FC_LVB_T) void k_deep_level_hot(Dev D, FlowArgs F) {
+  const uint32_t h = fd_nslots(F) ? fd_book(D, F, 0) : NIL;  // (the hottest book's range: one slot)
+  if (!fd_deep(F, h) || !F.hdr[h].dc) return;
+  const uint32_t nt = F.hdr[h].ntouch, L = FL_TOUCH_MUL * F.hdr[h].beg, nl = F.hdr[h].nl;
+  FlowLvl* LV = fl_lvls(F, h);
+  const SEnt* R = F.srt + L;
+  for (uint32_t q = 1 + blockIdx.x; q <= nl; q += gridDim.x) {
+    const uint32_t cnt = fd_run(LV, R, nt, q);
+    if (cnt < FC_BIG) continue;
+    if (threadIdx.x == 0) LV[q].cnt = cnt;
+    __syncthreads();
+    fc_level_blk(D, F, h, q);
+    __syncthreads();  // (fc_level_blk's shared words, before the next level's)
+  }
+  const uint32_t nw = blockDim.x >> 6, lane = lane_id();
+  for (uint32_t q = 1 + blockIdx.x * nw + (threadIdx.x >> 6); q <= nl; q += gridDim.x * nw) {
+    const uint32_t cnt = uni(fd_run(LV, R, nt, q));
+    if (cnt == 0 || cnt >= FC_BIG) continue;
+    if (lane == 0) LV[q].cnt = cnt;
+    __threadfence_block();  // (fc_level_one reads the count back)
+    fc_level_one(D, F, h, q);
   }
 }
 

@@ -332,6 +332,7 @@ struct gome_engine {
   unsigned long long idx_cap = 0;
   // batch buffers (the sort's and the segments' are per slot: Slot)
   uint32_t* d_bsum = nullptr;
+  bool crank_big = true;   // the head's deep cancel ranks: busy levels a block each (GOME_CRANK_BIG=0: A/B)
   bool sort_ahead = false;  // pipelined device batches sort on the copy stream during the last one's plan (GOME_SORT_AHEAD=1; DESIGN 4.5: off, measured mixed)
   unsigned long long* d_adm = nullptr;  // admission table (k_adm)
   unsigned long long* d_dup = nullptr;  // (S, uuid, oid) table of the records whose (S, oid) repeats
@@ -532,6 +533,7 @@ gome_status gome_engine::init(const gome_config& c) {
   if (const char* g = std::getenv("GOME_TAIL_SERIAL")) tail_serial = std::atoi(g) != 0;         // (profiling)
   if (const char* g = std::getenv("GOME_PREP_WAIT")) prep_wait = std::atoi(g) != 0 ? 1 : 0;       // (A/B)
   if (const char* g = std::getenv("GOME_SORT_AHEAD")) sort_ahead = std::atoi(g) != 0;           // (A/B)
+  if (const char* g = std::getenv("GOME_CRANK_BIG")) crank_big = std::atoi(g) != 0;             // (A/B)
   if (const char* g = std::getenv("GOME_ADM_FAST")) adm_fast = std::atoi(g) != 0;              // (A/B)
   // the cold books go beside the tail's chain only when HIP can give the copy stream a hardware
   // queue of its own (with 4 it shares the hottest plan's, which serialised them: +6 ms per
@@ -1022,7 +1024,9 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
       k_fd_oldwalk<<<dim3(DEEP_GRID, ns), 64, 0, st>>>(D, R);
       k_fd_ckeys<<<dim3(wide ? 256 : 16, ns), 256, 0, st>>>(D, B, R);
       deep_sort(R, wide ? FL_SORT_GRID : 32, st);
-      k_fd_crank<<<dim3(DEEP_GRID, ns), 64, 0, st>>>(D, B, R);
+      const bool big = wide && crank_big;  // (the head's busiest levels a block each)
+      k_fd_crank<<<dim3(DEEP_GRID, ns), 64, 0, st>>>(D, B, R, big ? 1u : 0u);
+      if (big) k_fd_crank_big<<<dim3(16, ns), FC_LVB_T, 0, st>>>(D, B, R);
       k_fd_tbase<<<ns, DEEP_CLAIM_T, 0, st>>>(D, R);
     }
     if (wide) {  // the head: tile-parallel ranks, windows, layout and records

@@ -883,7 +883,57 @@ __device__ __forceinline__ void fd_crank_level(const BatchArgs& B, const FlowArg
   if (lane == 0) LV[q].ttot = tc;
 }
 
-__device__ __forceinline__ void k_fd_crank_one(Dev D, BatchArgs B, FlowArgs F, uint32_t slot_i) {
+// fd_crank_level with a whole block (FC_LVB_T threads) on a level of FC_CRANK_BIG keys or more:
+// on config 5c's streams the aggressive remainders' levels (1.00 / 0.01) hold tens of thousands of
+// the hottest book's records, and one wave walked them 64 at a time (0.5 ms of the head's prep,
+// before the plan).  The two sides' ADD volumes scan as one word (each side's sum is below 2^32 in
+// a W32 book: FlowHdr::w32).
+constexpr uint32_t FC_CRANK_BIG = 2048;
+__device__ __forceinline__ void fd_crank_level_blk(const BatchArgs& B, const FlowArgs& F, const FlowHdr& hd,
+                                                   FlowLvl* LV, const SEnt* R, uint32_t q, uint32_t b, uint32_t e) {
+  int64_t vv = 0, tc = LV[q].c_old;
+  for (uint32_t c0 = b; c0 < e; c0 += blockDim.x) {
+    const uint32_t i = c0 + threadIdx.x;
+    const bool valid = i < e;
+    const uint32_t j = valid ? R[i].j : 0u, bs = hd.beg + j;
+    bool isadd = false, targ = false, isdel = false, sale = false;
+    uint32_t v = 0;
+    if (valid) {
+      const unsigned long long r = F.ord8[hd.obase + j];
+      if (r) {
+        isadd = true;
+        v = static_cast<uint32_t>(r);
+        sale = (r >> 63) != 0;
+        targ = F.fc_tg[bs] != 0;
+      } else {
+        isdel = true;
+        sale = prep_at(B, bs).side == GOME_SALE;
+      }
+    }
+    const int64_t pv = isadd ? (sale ? static_cast<int64_t>(v) << 32 : static_cast<int64_t>(v)) : 0;
+    int64_t tv, tt;
+    const int64_t xv = vv + fl_blk_excl(pv, &tv), xt = tc + fl_blk_excl(targ ? 1 : 0, &tt);
+    const uint32_t before_t = static_cast<uint32_t>(xt);
+    const uint32_t before_v = static_cast<uint32_t>(sale ? static_cast<uint64_t>(xv) >> 32 : static_cast<uint64_t>(xv));
+    if (targ) {
+      FcDel* d = &F.fc_del[F.fc_tg[bs] - 1u];
+      d->oend = before_v + v;
+      d->ov = v;
+      F.fc_rank[bs] = before_t;
+    }
+    if (isdel) {
+      F.fc_del[bs].nb = before_t;
+      F.fc_del[bs].va = before_v;
+    }
+    vv += tv;
+    tc += tt;
+  }
+  if (threadIdx.x == 0) LV[q].ttot = static_cast<uint32_t>(tc);
+}
+
+// big: 0 = every level a wave; 1 = only the levels below FC_CRANK_BIG keys (k_fd_crank_big takes
+// the others)
+__device__ __forceinline__ void k_fd_crank_one(Dev D, BatchArgs B, FlowArgs F, uint32_t slot_i, uint32_t big) {
   const uint32_t h = fd_book(D, F, slot_i);
   if (h == NIL || !fc_deep(F, h)) return;
   const FlowHdr& hd = F.hdr[h];
@@ -897,12 +947,32 @@ __device__ __forceinline__ void k_fd_crank_one(Dev D, BatchArgs B, FlowArgs F, u
     const bool head = i < nt && lv != 0 && (i == 0 || R[i - 1].lvl != lv);
     for (unsigned long long hm = __ballot(head); hm; hm &= hm - 1) {
       const uint32_t q = uni(rl(lv, static_cast<uint32_t>(__builtin_ctzll(hm))));
-      fd_crank_level(B, F, hd, LV, R, q, uni(LV[q].base), uni(LV[q].pad1));  // (k_deep_runs)
+      const uint32_t b = uni(LV[q].base), e = uni(LV[q].pad1);  // (k_deep_runs)
+      if (big && e - b >= FC_CRANK_BIG) continue;
+      fd_crank_level(B, F, hd, LV, R, q, b, e);
     }
   }
 }
-__global__ __launch_bounds__(64) void k_fd_crank(Dev D, BatchArgs B, FlowArgs F) {
-  for (uint32_t i = blockIdx.y; i < fd_nslots(F); i += gridDim.y) k_fd_crank_one(D, B, F, i);
+__global__ __launch_bounds__(64) void k_fd_crank(Dev D, BatchArgs B, FlowArgs F, uint32_t big) {
+  for (uint32_t i = blockIdx.y; i < fd_nslots(F); i += gridDim.y) k_fd_crank_one(D, B, F, i, big);
+}
+// The levels of FC_CRANK_BIG keys or more, a block each (found from the sorted keys: a run's head).
+__global__ __launch_bounds__(FC_LVB_T) void k_fd_crank_big(Dev D, BatchArgs B, FlowArgs F) {
+  for (uint32_t si = blockIdx.y; si < fd_nslots(F); si += gridDim.y) {
+    const uint32_t h = fd_book(D, F, si);
+    if (h == NIL || !fc_deep(F, h)) continue;
+    const FlowHdr& hd = F.hdr[h];
+    const uint32_t nt = hd.ntouch, L = FL_TOUCH_MUL * hd.beg, nl = hd.nl;
+    FlowLvl* LV = fl_lvls(F, h);
+    const SEnt* R = F.srt + L;
+    for (uint32_t q = 1 + blockIdx.x; q <= nl; q += gridDim.x) {
+      const uint32_t b = LV[q].base, e = LV[q].pad1;
+      // (a run of the current sort: this prep's k_deep_runs wrote base / pad1 of every level with keys)
+      if (e < b + FC_CRANK_BIG || e > nt || R[b].lvl != q || R[e - 1].lvl != q) continue;
+      fd_crank_level_blk(B, F, hd, LV, R, q, b, e);
+      __syncthreads();
+    }
+  }
 }
 
 // Per level the first entry of the book's DEL-time array (an exclusive scan of the levels'

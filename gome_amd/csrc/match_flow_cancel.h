@@ -1045,7 +1045,7 @@ __device__ __forceinline__ void fc_level_one(const Dev& D, const FlowArgs& F, ui
   }
 }
 
-constexpr uint32_t FC_LVB_T = FL_LVB_T;
+constexpr uint32_t FC_LVB_T = FL_LVB_T, FC_K = 4;
 
 // fc_level_one with a whole block (FC_LVB_T threads) on one level: the level's touches in
 // block-wide chunks (the long levels of the hottest books hold tens of thousands of touches,
@@ -1065,26 +1065,39 @@ __device__ __forceinline__ void fc_level_blk(const Dev& D, const FlowArgs& F, ui
   RsEnt* RS = F.rs + L + base;
   if (tid == 0) { red_s[0] = 0; nr_s = 0; ncan_s = 0; }
   __syncthreads();
-  // 1. each cancel -> its DEL's record (r, touch); the consumption cursor before each consume
+  // 1. each cancel -> its DEL's record (r, touch); the consumption cursor before each consume.
+  //    FC_K consecutive touches per thread: their loads in flight together, a quarter of the
+  //    block scans (a busy level is tens of thousands of touches)
   int64_t cc = 0, ocan = 0;
   uint32_t nr = 0, ncan_old = 0;
-  for (uint32_t c0 = 0; c0 < cnt; c0 += FC_LVB_T) {
-    const uint32_t i = c0 + tid;
-    const bool valid = i < cnt;
-    SEnt e{};
-    if (valid) e = R[i];
-    const bool isc = valid && e.kind == TK_CONS, isx = valid && e.kind == TK_CANC;
-    if (isx) {
-      FcDel* d = &F.fc_del[beg + e.j];
-      d->r = e.amt;
-      d->ct = e.t;
-      if (d->kind == FC_OLD) { ocan += e.amt; ncan_old++; }
+  for (uint32_t c0 = 0; c0 < cnt; c0 += FC_LVB_T * FC_K) {
+    const uint32_t i0 = c0 + tid * FC_K;
+    SEnt e[FC_K];
+#pragma unroll
+    for (uint32_t u = 0; u < FC_K; ++u)
+      if (i0 + u < cnt) e[u] = R[i0 + u];
+    int64_t sum = 0;
+#pragma unroll
+    for (uint32_t u = 0; u < FC_K; ++u) {
+      if (i0 + u >= cnt) continue;
+      if (e[u].kind == TK_CANC) {
+        FcDel* d = &F.fc_del[beg + e[u].j];
+        d->r = e[u].amt;
+        d->ct = e[u].t;
+        if (d->kind == FC_OLD) { ocan += e[u].amt; ncan_old++; }
+      }
+      sum += e[u].kind == TK_CONS ? e[u].amt : 0;
+      nr += e[u].kind == TK_REST ? 1u : 0u;
     }
     int64_t tot;
-    const int64_t ex = fl_blk_excl(isc ? e.amt : 0, &tot);
-    if (isc) R[i].coord = cc + ex;
+    int64_t run = cc + fl_blk_excl(sum, &tot);
+#pragma unroll
+    for (uint32_t u = 0; u < FC_K; ++u) {
+      if (i0 + u >= cnt || e[u].kind != TK_CONS) continue;
+      R[i0 + u].coord = run;
+      run += e[u].amt;
+    }
     cc += tot;
-    nr += valid && e.kind == TK_REST ? 1u : 0u;
   }
   if (ocan) atomicAdd(reinterpret_cast<unsigned long long*>(&red_s[0]), static_cast<unsigned long long>(ocan));
   if (nr) atomicAdd(&nr_s, nr);
@@ -1097,34 +1110,47 @@ __device__ __forceinline__ void fc_level_blk(const Dev& D, const FlowArgs& F, ui
   // 2. the new makers in FIFO (rest) order, their consumption-space starts and cancels
   int64_t acc = base_new;
   uint32_t k = 0;
-  for (uint32_t c0 = 0; c0 < cnt; c0 += FC_LVB_T) {
-    const uint32_t i = c0 + tid;
-    const bool valid = i < cnt;
-    SEnt e{};
-    if (valid) e = R[i];
-    const bool isr = valid && e.kind == TK_REST;
-    uint32_t ct = NIL;
-    int64_t len = 0;
-    if (isr) {
-      len = e.amt;
-      const uint32_t tg = F.fc_tg[beg + e.j];
-      if (tg) {
-        const FcDel d = F.fc_del[tg - 1u];
-        if (d.ct != NIL) { ct = d.ct; len = e.amt - d.r; }
+  for (uint32_t c0 = 0; c0 < cnt; c0 += FC_LVB_T * FC_K) {
+    const uint32_t i0 = c0 + tid * FC_K;
+    SEnt e[FC_K];
+    uint32_t tg[FC_K];
+#pragma unroll
+    for (uint32_t u = 0; u < FC_K; ++u) {
+      tg[u] = 0;
+      if (i0 + u < cnt) e[u] = R[i0 + u];
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < FC_K; ++u)
+      if (i0 + u < cnt && e[u].kind == TK_REST) tg[u] = F.fc_tg[beg + e[u].j];
+    uint32_t ct[FC_K];
+    int64_t len[FC_K], sum = 0, nsum = 0;
+#pragma unroll
+    for (uint32_t u = 0; u < FC_K; ++u) {
+      const bool isr = i0 + u < cnt && e[u].kind == TK_REST;
+      ct[u] = NIL;
+      len[u] = isr ? e[u].amt : 0;
+      if (isr && tg[u]) {
+        const FcDel d = F.fc_del[tg[u] - 1u];
+        if (d.ct != NIL) { ct[u] = d.ct; len[u] = e[u].amt - d.r; }
       }
+      sum += len[u];
+      nsum += isr ? 1 : 0;
     }
     int64_t tot, ntot;
-    const int64_t ex = fl_blk_excl(len, &tot);
-    const int64_t rk = fl_blk_excl(isr ? 1 : 0, &ntot);
-    if (isr) {
+    int64_t run = acc + fl_blk_excl(sum, &tot);
+    uint32_t rk = k + static_cast<uint32_t>(fl_blk_excl(nsum, &ntot));
+#pragma unroll
+    for (uint32_t u = 0; u < FC_K; ++u) {
+      if (i0 + u >= cnt || e[u].kind != TK_REST) continue;
       RsEnt x;
-      x.e = acc + ex;
-      x.v = e.amt;
-      x.j = e.j;
-      x.t = e.t;
-      x.pad0 = ct;
+      x.e = run;
+      x.v = e[u].amt;
+      x.j = e[u].j;
+      x.t = e[u].t;
+      x.pad0 = ct[u];
       x.pad1 = 0;
-      RS[k + static_cast<uint32_t>(rk)] = x;
+      RS[rk++] = x;
+      run += len[u];
     }
     acc += tot;
     k += static_cast<uint32_t>(ntot);

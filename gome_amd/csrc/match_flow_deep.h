@@ -412,10 +412,18 @@ __device__ __forceinline__ void k_deep_sort_scan_one(Dev D, FlowArgs F, uint32_t
   }
   __syncthreads();
   uint32_t run = tot[k];
-  for (uint32_t tl = 0; tl < ntile; ++tl) {
-    const uint32_t v = tc[tl * FL_CAP + k];
-    tc[tl * FL_CAP + k] = run;
-    run += v;
+  constexpr uint32_t U = 8;  // (eight tiles' loads in flight before their stores, as k_fc_pscan)
+  for (uint32_t t0 = 0; t0 < ntile; t0 += U) {
+    uint32_t v[U];
+#pragma unroll
+    for (uint32_t u = 0; u < U; ++u)
+      if (t0 + u < ntile) v[u] = tc[(t0 + u) * FL_CAP + k];
+#pragma unroll
+    for (uint32_t u = 0; u < U; ++u) {
+      if (t0 + u >= ntile) break;
+      tc[(t0 + u) * FL_CAP + k] = run;
+      run += v[u];
+    }
   }
 }
 __global__ __launch_bounds__(FL_CAP) void k_deep_sort_scan(Dev D, FlowArgs F) {

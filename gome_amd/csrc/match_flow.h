@@ -1693,6 +1693,7 @@ __device__ __forceinline__ void fl_level_one(const Dev& D, const FlowArgs& F, ui
       if (guard > D.ch_cap) { if (lane == 0) atomicOr(&D.st->err, ERR_CORRUPT); return; }
       const uint32_t lim = (c == tail) ? tslot : CH;
       const bool inr = lane < CH && lane >= s0 && lane < lim;
+      const uint32_t nxt = (c == tail) ? NIL : D.chdr[c].next;  // (in flight beside the nodes)
       Node nd{};
       if (inr) nd = D.nodes[c * CH + lane];
       const bool live = inr && nd.rem >= 0;
@@ -1731,8 +1732,7 @@ __device__ __forceinline__ void fl_level_one(const Dev& D, const FlowArgs& F, ui
       }
       if (beyond) have_extra = true;
       E += rl64(inc, 63);
-      const uint32_t nx = (c == tail) ? NIL : uni(D.chdr[c].next);
-      c = nx;
+      c = uni(nxt);
       s0 = 0;
     }
     if (nfr) publish();

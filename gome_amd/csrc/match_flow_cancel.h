@@ -986,6 +986,7 @@ __device__ __forceinline__ void fc_level_one(const Dev& D, const FlowArgs& F, ui
       if (guard > D.ch_cap) { if (lane == 0) atomicOr(&D.st->err, ERR_CORRUPT); return; }
       const uint32_t lim = (c == tail) ? tslot : CH;
       const bool inr = lane < CH && lane >= s0 && lane < lim;
+      const uint32_t nxt = (c == tail) ? NIL : D.chdr[c].next;  // (in flight beside the nodes)
       Node nd{};
       if (inr) nd = D.nodes[c * CH + lane];
       const bool live = inr && nd.rem >= 0;
@@ -1032,7 +1033,7 @@ __device__ __forceinline__ void fc_level_one(const Dev& D, const FlowArgs& F, ui
       }
       if (after) { stop = true; ig_all = false; }
       E += rl64(inc, 63);
-      c = (c == tail) ? NIL : uni(D.chdr[c].next);
+      c = uni(nxt);
       s0 = 0;
     }
     if (!have_surv && ig_all) {
@@ -1196,6 +1197,7 @@ __device__ __forceinline__ void fc_level_blk(const Dev& D, const FlowArgs& F, ui
       if (guard > D.ch_cap) { if (lane == 0) atomicOr(&D.st->err, ERR_CORRUPT); return; }
       const uint32_t lim = (c == tail) ? tslot : CH;
       const bool inr = lane < CH && lane >= s0 && lane < lim;
+      const uint32_t nxt = (c == tail) ? NIL : D.chdr[c].next;  // (in flight beside the nodes)
       Node nd{};
       if (inr) nd = D.nodes[c * CH + lane];
       const bool live = inr && nd.rem >= 0;
@@ -1239,7 +1241,7 @@ __device__ __forceinline__ void fc_level_blk(const Dev& D, const FlowArgs& F, ui
       }
       if (after) { stop = true; ig_all = false; }
       E += rl64(inc, 63);
-      c = (c == tail) ? NIL : uni(D.chdr[c].next);
+      c = uni(nxt);
       s0 = 0;
     }
     if (!have_surv && ig_all) {

@@ -1052,7 +1052,7 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   if (early) {  // the early inputs against this prep's, then the early plan taken (or not)
     k_x_cmp<<<256, 256, 0, flow_stream>>>(D, F, FX, X.ctl);
     HIPCHK(hipStreamWaitEvent(flow_stream, xplan_done, 0));
-    k_x_take<<<1, 128, 0, flow_stream>>>(D, F, FX, X.ctl);
+    k_x_take<<<32, 256, 0, flow_stream>>>(D, F, FX, X.ctl);
   }
   HIPCHK(hipEventRecord(S.evf0, flow_stream));
   k_flow_plan_head<<<1, 256, plan_lds, flow_stream>>>(D, FH0);  // (a book planned early: nothing)

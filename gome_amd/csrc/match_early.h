@@ -53,7 +53,10 @@ struct XCtl {
   Status st;       // the early kernels' Dev::st (nhot: 1 = plan the hottest segment, 0 = skip; err)
 };
 
-constexpr uint32_t XD_PREP_LDS = (2 * DEEP_CAP + 2) * 4;  // k_xd_prep_b's two prefix arrays
+// k_xd_prep_b's two prefix arrays, then every XD_S-th key of the old levels and of the batch's
+// prices (the binary searches' first steps in LDS)
+constexpr uint32_t XD_S = 16, XD_NS = DEEP_CAP / XD_S;
+constexpr uint32_t XD_PREP_LDS = (2 * DEEP_CAP + 2) * 4 + 2 * XD_NS * 8;
 constexpr uint32_t X_FIND_T = 256, X_FIND_B = 1024;  // k_x_count / k_x_scatter: blocks of contiguous records
 
 __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t x) { return rl(wave_incl_scan_u32(x), 63); }
@@ -420,6 +423,28 @@ __device__ __forceinline__ uint32_t x_lower(Key key, uint32_t n, unsigned long l
   return lo;
 }
 
+// x_lower through a sample s[k] = key(k * XD_S), k < ns, in LDS: the sample's search leaves a
+// window of at most XD_S keys, searched in global memory (the hottest deep book's ~10k levels
+// and prices: 14 dependent global loads per search before, ~4 now).
+template <class Key>
+__device__ __forceinline__ uint32_t xs_lower(const unsigned long long* smp, uint32_t ns, Key key, uint32_t n,
+                                             unsigned long long x) {
+  uint32_t lo = 0, hi = ns;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (smp[mid] < x) lo = mid + 1;
+    else hi = mid;
+  }
+  // key((lo - 1) * XD_S) < x <= key(lo * XD_S): the answer is in ((lo - 1) * XD_S, lo * XD_S]
+  uint32_t a = lo ? (lo - 1) * XD_S + 1 : 0u, b = min(lo * XD_S, n);
+  while (a < b) {
+    const uint32_t mid = (a + b) >> 1;
+    if (key(mid) < x) a = mid + 1;
+    else b = mid;
+  }
+  return a;
+}
+
 // The early deep prep after the previous plan: its live levels (F.dlvl of deep slot 0: price,
 // dfin, memf; sorted by price) merged with the batch's sorted prices into the level table
 // (FX.dlvl), each batch price's level into the early set's values, the header.  A merge by
@@ -450,6 +475,14 @@ __global__ __launch_bounds__(FL_PREP_T) void k_xd_prep_b(BatchArgs Bx, FlowArgs 
   const FlowLvl* LP = F.dlvl;  // (deep slot 0: the hottest book's)
   uint32_t* lpre = reinterpret_cast<uint32_t*>(fl_ring);  // [nlp + 1]: live old levels before
   uint32_t* mpre = lpre + DEEP_CAP + 1;                     // [nn + 1]: batch prices on a live old level before
+  unsigned long long* so = reinterpret_cast<unsigned long long*>(mpre + DEEP_CAP + 1);  // samples: old keys
+  unsigned long long* sn = so + XD_NS;                                                // ... batch prices
+  auto oldkey = [&](uint32_t i) { return static_cast<unsigned long long>(LP[i + 1].price) + FL_KEY_OFF; };
+  auto newkey = [&](uint32_t k) { return dnew[k]; };
+  const uint32_t nso = (nlp + XD_S - 1) / XD_S, nsn = (nn + XD_S - 1) / XD_S;
+  for (uint32_t k = tid; k < nso; k += FL_PREP_T) so[k] = oldkey(k * XD_S);
+  for (uint32_t k = tid; k < nsn; k += FL_PREP_T) sn[k] = dnew[k * XD_S];
+  __syncthreads();
   unsigned long long mg = 0, msum = 0;
   if (tid < FL_PG) {
     mg = P->pg[tid];
@@ -465,9 +498,8 @@ __global__ __launch_bounds__(FL_PREP_T) void k_xd_prep_b(BatchArgs Bx, FlowArgs 
     }
     lpre[i] = live ? 1u : 0u;
   }
-  auto oldkey = [&](uint32_t i) { return static_cast<unsigned long long>(LP[i + 1].price) + FL_KEY_OFF; };
   for (uint32_t i = tid; i < nn; i += FL_PREP_T) {
-    const uint32_t q = x_lower(oldkey, nlp, dnew[i]);
+    const uint32_t q = xs_lower(so, nso, oldkey, nlp, dnew[i]);
     mpre[i] = (q < nlp && oldkey(q) == dnew[i] && LP[q + 1].memf != 0) ? 1u : 0u;
   }
   fl_block_gcd_sum(mg, msum, wg, ws);  // (synchronises the block)
@@ -485,7 +517,7 @@ __global__ __launch_bounds__(FL_PREP_T) void k_xd_prep_b(BatchArgs Bx, FlowArgs 
   for (uint32_t i = tid; i < nlp; i += FL_PREP_T) {
     const FlowLvl& o = LP[i + 1];
     if (!o.memf) continue;
-    const uint32_t pos = x_lower([&](uint32_t k) { return dnew[k]; }, nn, oldkey(i));
+    const uint32_t pos = xs_lower(sn, nsn, newkey, nn, oldkey(i));
     FlowLvl f{};
     f.price = o.price;
     f.d0 = o.dfin;
@@ -498,7 +530,7 @@ __global__ __launch_bounds__(FL_PREP_T) void k_xd_prep_b(BatchArgs Bx, FlowArgs 
   // the batch's prices: a new level unless a live old level has it; each one's level in the set
   for (uint32_t i = tid; i < nn; i += FL_PREP_T) {
     const unsigned long long key = dnew[i];
-    const uint32_t q = x_lower(oldkey, nlp, key);  // (live old levels below: lpre[q])
+    const uint32_t q = xs_lower(so, nso, oldkey, nlp, key);  // (live old levels below: lpre[q])
     const bool on_old = mpre[i + 1] != mpre[i];
     const uint32_t r = lpre[q] + (i - mpre[i]) + 1;
     if (!on_old) {
@@ -554,6 +586,8 @@ __global__ void k_x_cmp(Dev D, FlowArgs F, FlowArgs FX, XCtl* X) {
 
 // After the early plan: take it (its final depths and sides, touch count into F, the header
 // marked `pre`) when its inputs matched and it ran clean.
+// (a grid: a deep book's ~10k levels took one block 45 us, on the early chain's critical path;
+// every block decides alike, block 0 writes the header)
 __global__ void k_x_take(Dev D, FlowArgs F, FlowArgs FX, XCtl* X) {
   __shared__ uint32_t use;
   const FlowHdr xh = FX.hdr[0];
@@ -562,17 +596,17 @@ __global__ void k_x_take(Dev D, FlowArgs F, FlowArgs FX, XCtl* X) {
     const bool normal = D.st->nhot != 0 && (ok == FL_OK_ADD || ok == FL_OK_DEEP) && ok == xh.ok;
     use = (X->ok && !X->mism && X->st.err == 0 && normal) ? 1u : 0u;
     // (a batch whose hottest book is another symbol than the last one's plans it normally)
-    if (!use && normal && X->ok && F.hdr[0].sym == xh.sym) ctr_add(D, C_EARLY_MISS, 1ull);
+    if (blockIdx.x == 0 && !use && normal && X->ok && F.hdr[0].sym == xh.sym) ctr_add(D, C_EARLY_MISS, 1ull);
   }
   __syncthreads();
   if (!use) return;
   FlowLvl* A = fl_lvls(F, 0);
   const FlowLvl* B = fl_lvls(FX, 0);
-  for (uint32_t q = 1 + threadIdx.x; q <= xh.nl; q += blockDim.x) {
+  for (uint32_t q = 1 + blockIdx.x * blockDim.x + threadIdx.x; q <= xh.nl; q += gridDim.x * blockDim.x) {
     A[q].dfin = B[q].dfin;
     A[q].memf = B[q].memf;
   }
-  if (threadIdx.x == 0) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
     FlowHdr* w = &F.hdr[0];
     w->ntouch = xh.ntouch;
     w->amask[0] = xh.amask[0];

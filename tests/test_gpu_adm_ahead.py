@@ -92,3 +92,43 @@ def test_admission_ahead_off(monkeypatch):
     monkeypatch.setenv("GOME_ADM_AHEAD", "0")
     _, _, stats = _run(_config4(5, 11), 100000, "adm ahead off")
     assert all(int(s["n_adm_ahead"]) == 0 for s in stats)
+
+
+def test_admission_ahead_soak():
+    """32 pipelined config-4 batches: every one after the first admits ahead, none redoes it, and
+    the events and books stay the oracle's."""
+    batches = _config4(32, 101)
+    eng, orc, stats = _run(batches, 100000, "adm ahead soak")
+    ahead = [int(s["n_adm_ahead"]) for s in stats]
+    assert sum(ahead) >= 30 and all(int(s["n_adm_redo"]) == 0 for s in stats), ahead
+    z = wl.ZipfSymbols(100000, 1.0)
+    _cmp_books(eng, orc, _hot_and_random(z, 100000, k_rand=50), "adm ahead soak")
+    assert eng.stats()["n_resting"] == orc.resting()
+
+
+def test_config5c_pipelined_exact():
+    """Config 5c's stream (deep books with DELs) pipelined three deep at 1 Mi orders per batch:
+    admission ahead, the head's busy levels' cancel ranks a block each (k_fd_crank_big) and the
+    hottest book's reconstruction by level (k_deep_level_hot) together, against the C oracle."""
+    import torch
+    n = 1 << 20
+    gen, _, _ = bench.make_stream("config5c", 0, 1, 42)
+    batches = [gen(n).copy() for _ in range(6)]
+    eng = Engine(max_symbols=1_000_000, max_batch=n, max_nodes=8 * n, max_levels=(64 << 20) + 2 * n)
+    orc = Oracle(1_000_000)
+    dev = [torch.from_numpy(b.view(np.uint8).copy()).cuda() for b in batches]
+    torch.cuda.synchronize()
+    exp = [orc.submit(b) for b in batches]
+    ahead, nxt = [], 0
+    for k in range(len(batches)):
+        while nxt < len(batches) and nxt < k + 3:
+            eng.submit_device_async(dev[nxt].data_ptr(), n, 0)
+            nxt += 1
+        _, cnt, st = eng.collect_device()
+        assert cnt == len(exp[k]), f"5c batch {k}: {cnt} events vs oracle {len(exp[k])}"
+        ahead.append(int(st["n_adm_ahead"]))
+    _cmp(eng.drain(), np.concatenate(exp), "5c pipelined")
+    assert sum(ahead[1:]) >= 4, ahead
+    z = wl.ZipfSymbols(1_000_000, 1.0)
+    _cmp_books(eng, orc, _hot_and_random(z, 1_000_000, k_hot=4, k_rand=30), "5c pipelined")
+    assert eng.stats()["n_resting"] == orc.resting()

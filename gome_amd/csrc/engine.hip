@@ -267,6 +267,60 @@ struct gome_engine {
   hipStream_t copy_stream = nullptr;  // H2D of records, D2H of events (pipelined path)
   hipStream_t cold_stream = nullptr;  // the cold books on a stream of their own (GOME_COLD_OWN=1; A/B)
   hipStream_t early_stream = nullptr; // the early plan's record work (match_early.h), beside the plan before it
+  // The hottest book's plans on a stream of their own restricted to CUs [0, k), every other engine
+  // stream to the rest: the plan wave alone with its CU's instruction cache and L1, and no other
+  // kernel's code or data beside it (GOME_PLAN_CUS=k, default 8; 0: no reserved CUs)
+  hipStream_t plan_stream = nullptr;
+  hipEvent_t pl_fork{}, pl_join{};
+  uint32_t plan_cus = 0;
+  std::vector<uint32_t> cu_rest;  // every CU but the plan's
+  hipError_t new_stream(hipStream_t* st) {
+    return plan_cus ? hipExtStreamCreateWithCUMask(st, static_cast<uint32_t>(cu_rest.size()), cu_rest.data())
+                    : hipStreamCreateWithFlags(st, hipStreamNonBlocking);
+  }
+  // The engine's streams on every CU, for batches after one no book dominated: there the tail's
+  // chain is the critical path, and on the masked queues config 2 ran 5% slower.  set_masked
+  // swaps the two sets (the new streams wait for the old ones' work first).
+  static constexpr int NSET = 5;
+  hipStream_t alt[NSET]{};
+  hipEvent_t sw_ev[NSET]{};
+  bool masked = false;
+  hipStream_t* live_streams(int i) {
+    hipStream_t* v[NSET] = {&stream, &hot_stream, &flow_stream, &copy_stream, &early_stream};
+    return v[i];
+  }
+  hipError_t make_sets() {
+    if (!plan_cus) return hipSuccess;
+    for (int i = 0; i < NSET; ++i) {
+      if (!*live_streams(i)) continue;
+      hipError_t he = hipStreamCreateWithFlags(&alt[i], hipStreamNonBlocking);
+      if (he == hipSuccess) he = hipEventCreateWithFlags(&sw_ev[i], hipEventDisableTiming);
+      if (he != hipSuccess) return he;
+    }
+    masked = true;
+    return hipSuccess;
+  }
+  hipError_t set_masked(bool want) {
+    if (!plan_cus || want == masked) return hipSuccess;
+    for (int i = 0; i < NSET; ++i) {
+      hipStream_t* cur = live_streams(i);
+      if (!*cur) continue;
+      hipError_t he = hipEventRecord(sw_ev[i], *cur);
+      if (he == hipSuccess) he = hipStreamWaitEvent(alt[i], sw_ev[i], 0);
+      if (he != hipSuccess) return he;
+      std::swap(*cur, alt[i]);
+    }
+    masked = want;
+    ++n_set_switch;
+    return hipSuccess;
+  }
+  uint64_t n_set_switch = 0;
+  // before a batch's first stream use: the masked set while the last finished batch had a
+  // dominant book (enqueue's `dominant`), every CU otherwise
+  gome_status pick_streams() {
+    const hipError_t he = set_masked(!(last_maxseg * 16 < last_n));
+    return he == hipSuccess ? GOME_OK : fail(GOME_E_DEVICE, hipGetErrorString(he));
+  }
   // D2H of collected events on a stream of their own (GOME_D2H_STREAM=1; off by default: with
   // four hardware queues per process a fifth stream shares one, and the e2e A/B measured it
   // 0.7 ms per config-2 batch slower with three batches in flight, no faster with two)
@@ -420,6 +474,13 @@ struct gome_engine {
     if (h_tob_syms) (void)hipHostFree(h_tob_syms);
     if (h_tob) (void)hipHostFree(h_tob);
     if (hot_stream) (void)hipStreamDestroy(hot_stream);
+    if (plan_stream) (void)hipStreamDestroy(plan_stream);
+    for (int i = 0; i < NSET; ++i) {
+      if (alt[i]) (void)hipStreamDestroy(alt[i]);
+      if (sw_ev[i]) (void)hipEventDestroy(sw_ev[i]);
+    }
+    if (pl_fork) (void)hipEventDestroy(pl_fork);
+    if (pl_join) (void)hipEventDestroy(pl_join);
     if (flow_stream) (void)hipStreamDestroy(flow_stream);
     if (copy_stream) (void)hipStreamDestroy(copy_stream);
     if (cold_stream) (void)hipStreamDestroy(cold_stream);
@@ -485,12 +546,28 @@ gome_status gome_engine::init(const gome_config& c) {
     return fail(GOME_E_DEVICE, "no HIP device available (the engine has no CPU fallback)");
   if (cfg.device < 0 || cfg.device >= ndev) return fail(GOME_E_INVAL, "gome_config.device out of range");
   HIPCHK(hipSetDevice(cfg.device));
-  HIPCHK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
-  HIPCHK(hipStreamCreateWithFlags(&hot_stream, hipStreamNonBlocking));
-  HIPCHK(hipStreamCreateWithFlags(&flow_stream, hipStreamNonBlocking));
-  HIPCHK(hipStreamCreateWithFlags(&copy_stream, hipStreamNonBlocking));
+  {
+    int ncu = 0;
+    HIPCHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, cfg.device));
+    const char* g = std::getenv("GOME_PLAN_CUS");
+    plan_cus = g ? static_cast<uint32_t>(std::max(0, std::atoi(g))) : 8u;
+    if (plan_cus >= static_cast<uint32_t>(ncu)) plan_cus = 0;
+    const uint32_t words = (static_cast<uint32_t>(ncu) + 31) / 32;
+    cu_rest.assign(words, 0u);
+    std::vector<uint32_t> cu_plan(words, 0u);
+    for (uint32_t c = 0; c < static_cast<uint32_t>(ncu); ++c) (c < plan_cus ? cu_plan : cu_rest)[c / 32] |= 1u << (c % 32);
+    if (plan_cus) {
+      HIPCHK(hipExtStreamCreateWithCUMask(&plan_stream, words, cu_plan.data()));
+      HIPCHK(hipEventCreateWithFlags(&pl_fork, hipEventDisableTiming));
+      HIPCHK(hipEventCreateWithFlags(&pl_join, hipEventDisableTiming));
+    }
+  }
+  HIPCHK(new_stream(&stream));
+  HIPCHK(new_stream(&hot_stream));
+  HIPCHK(new_stream(&flow_stream));
+  HIPCHK(new_stream(&copy_stream));
   if (const char* g = std::getenv("GOME_D2H_STREAM"); g && std::atoi(g) != 0)
-    HIPCHK(hipStreamCreateWithFlags(&d2h_stream, hipStreamNonBlocking));
+    HIPCHK(new_stream(&d2h_stream));
   for (hipEvent_t* ev : {&fork, &join, &joinf, &prep_h, &prep_t, &fork_adm, &adm_done, &seg_done,
                          &dp_fork, &cnt_fork, &cnt_done, &dw_done, &dl_done, &tl_done, &tob_done, &plan_done,
                          &oidmax_done, &xpre_done, &xprep_done, &xplan_done, &adm_pre_done})
@@ -546,7 +623,7 @@ gome_status gome_engine::init(const gome_config& c) {
   }
   if (const char* g = std::getenv("GOME_COLD_MAIN")) cold_main = std::atoi(g) != 0;            // (A/B)
   if (const char* g = std::getenv("GOME_COLD_OWN"); g && std::atoi(g) != 0)                   // (A/B)
-    HIPCHK(hipStreamCreateWithFlags(&cold_stream, hipStreamNonBlocking));
+    HIPCHK(new_stream(&cold_stream));
   phases = (cfg.flags & GOME_FLAG_PHASES) != 0;
   if (const char* g = std::getenv("GOME_PHASES")) phases = std::atoi(g) != 0;
   uint32_t ms = cfg.max_symbols;
@@ -668,7 +745,7 @@ gome_status gome_engine::init(const gome_config& c) {
   HIPCHK(hipMemsetAsync(x_dslot, 0, 4, stream));  // (the early deep book is deep slot 0's)
   if (const char* g = std::getenv("GOME_EARLY")) early_on = std::atoi(g) != 0;
   if (const char* g = std::getenv("GOME_ADM_AHEAD")) adm_ahead_on = std::atoi(g) != 0;
-  if (early_on || adm_ahead_on) HIPCHK(hipStreamCreateWithFlags(&early_stream, hipStreamNonBlocking));
+  if (early_on || adm_ahead_on) HIPCHK(new_stream(&early_stream));
   if (const char* g = std::getenv("GOME_COLD_EARLY")) cold_early = std::atoi(g) != 0;
   // books with DELs (match_flow_cancel.h): per-position scratch, the (symbol, oid)
   // table (generation-tagged: cleared once per 2048 batches)
@@ -710,6 +787,7 @@ gome_status gome_engine::init(const gome_config& c) {
   HIPCHK(hipMemsetAsync(d_adm, 0, (adm_mask + 1ull) * 8, stream));  // (k_adm_flag leaves it empty)
   HIPCHK(hipMemsetAsync(d_pend, 0, sizeof(PendEnt) * nb, stream));
   if (D.idx_mask >= PEND) return fail(GOME_E_INVAL, "gome_config.max_nodes too large (index > 2^31 slots)");
+  HIPCHK(make_sets());
   HIPCHK(hipStreamSynchronize(stream));
   return GOME_OK;
 }
@@ -848,7 +926,9 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
     // last batch's early plan), the rest after both on the copy stream
     // (pipelined host batches: the record work on the copy stream right behind the batch's H2D, the
     // plan on the early stream, so the copy stream stays free for the copies)
-    hipStream_t es = copy_busy ? copy_stream : early_stream, ps = copy_busy ? early_stream : copy_stream;
+    // (GOME_PLAN_CUS: the part after plan_done on the plan's own stream, which then needs no hop)
+    hipStream_t es = copy_busy ? copy_stream : early_stream;
+    hipStream_t ps = plan_stream ? plan_stream : copy_busy ? early_stream : copy_stream;
     Dev Dx = D;
     Dx.st = reinterpret_cast<Status*>(reinterpret_cast<char*>(X.ctl) + offsetof(XCtl, st));
     BatchArgs Bx{};
@@ -1054,9 +1134,23 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
     HIPCHK(hipStreamWaitEvent(flow_stream, xplan_done, 0));
     k_x_take<<<32, 256, 0, flow_stream>>>(D, F, FX, X.ctl);
   }
-  HIPCHK(hipEventRecord(S.evf0, flow_stream));
-  k_flow_plan_head<<<1, 256, plan_lds, flow_stream>>>(D, FH0);  // (a book planned early: nothing)
-  HIPCHK(hipEventRecord(S.evf1, flow_stream));
+  {
+    hipStream_t pst = flow_stream;
+    // (a book planned early skips this launch, and with no dominant book the batch's critical path is
+    // the tail's chain: no hops for either)
+    if (plan_stream && !early && dominant) {
+      HIPCHK(hipEventRecord(pl_fork, flow_stream));
+      HIPCHK(hipStreamWaitEvent(plan_stream, pl_fork, 0));
+      pst = plan_stream;
+    }
+    HIPCHK(hipEventRecord(S.evf0, pst));
+    k_flow_plan_head<<<1, 256, plan_lds, pst>>>(D, FH0);  // (a book planned early: nothing)
+    HIPCHK(hipEventRecord(S.evf1, pst));
+    if (pst == plan_stream) {
+      HIPCHK(hipEventRecord(pl_join, plan_stream));
+      HIPCHK(hipStreamWaitEvent(flow_stream, pl_join, 0));
+    }
+  }
   HIPCHK(hipEventRecord(plan_done, flow_stream));
   if (early) k_x_logcopy<<<1024, 256, 0, flow_stream>>>(F, FX, X.ctl);
   // the other head books' plans need only the head's prep: each takes a whole CU, so they go
@@ -1566,6 +1660,7 @@ const char* gome_last_error(const gome_engine* e) {
 gome_status gome_submit_batch(gome_engine* e, const gome_order* orders, size_t n, uint64_t seq_base) {
   if (!e) return GOME_E_INVAL;
   DevGuard dg(e->cfg.device);
+  if (e->pick_streams() != GOME_OK) return GOME_E_DEVICE;
   gome_status st = e->collect_all();
   if (st != GOME_OK) return st;
   if ((st = e->spill_device_events()) != GOME_OK) return st;
@@ -1587,6 +1682,7 @@ gome_status gome_submit_batch_device(gome_engine* e, const gome_order* dev_order
                                      uint64_t seq_base, void* stream) {
   if (!e) return GOME_E_INVAL;
   DevGuard dg(e->cfg.device);
+  if (e->pick_streams() != GOME_OK) return GOME_E_DEVICE;
   gome_status st = e->collect_all();
   if (st != GOME_OK) return st;
   if ((st = e->spill_device_events()) != GOME_OK) return st;
@@ -1610,6 +1706,7 @@ gome_status gome_submit_batch_device(gome_engine* e, const gome_order* dev_order
 gome_status gome_submit_batch_async(gome_engine* e, const gome_order* orders, size_t n, uint64_t seq_base) {
   if (!e) return GOME_E_INVAL;
   DevGuard dg(e->cfg.device);
+  if (e->pick_streams() != GOME_OK) return GOME_E_DEVICE;
   if (e->flights.size() >= GOME_MAX_INFLIGHT)
     return e->fail(GOME_E_STATE, "GOME_MAX_INFLIGHT batches in flight: gome_collect first");
   gome_status st = e->spill_device_events();
@@ -1642,6 +1739,7 @@ gome_status gome_submit_batch_device_async(gome_engine* e, const gome_order* dev
                                            uint64_t seq_base) {
   if (!e) return GOME_E_INVAL;
   DevGuard dg(e->cfg.device);
+  if (e->pick_streams() != GOME_OK) return GOME_E_DEVICE;
   if (e->flights.size() >= GOME_MAX_INFLIGHT)
     return e->fail(GOME_E_STATE, "GOME_MAX_INFLIGHT batches in flight: gome_collect first");
   gome_status st = e->spill_device_events();

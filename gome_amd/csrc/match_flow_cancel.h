@@ -1304,7 +1304,14 @@ __device__ __forceinline__ FcTouch fc_touch(const FlowArgs& F, uint32_t h, uint3
   T.c = F.srt[L + x.pos].coord;
   T.a = x.amt;
   T.first = fc_find(T.V, T.c);
-  T.last = fc_find(T.V, T.c + T.a - 1);
+  // the last maker: a touch spans a few makers, so step on from the first (neighbouring entries,
+  // one cache line) before a second binary search (~16 dependent loads on a busy level); the
+  // starts rise through the old makers into the new ones, so both give the last start <= x
+  const int64_t xl = T.c + T.a - 1;
+  const uint32_t nm = T.V.ig_n + T.V.nrest;
+  uint32_t m = T.first, st = 0;
+  for (; st < 8 && m + 1 < nm && fc_start(T.V, m + 1) <= xl; ++st) ++m;
+  T.last = st < 8 ? m : fc_find(T.V, xl);
   return T;
 }
 

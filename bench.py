@@ -395,6 +395,9 @@ def main():
         os.environ.setdefault("RANK", "0")
         os.environ.setdefault("WORLD_SIZE", "1")
         if args.backend == "nccl":
+            # (with RCCL in the process the engine's CU-masked plan stream lost 5% per step, for
+            # reasons not established: DESIGN 4.7; such a host keeps every CU shared)
+            os.environ.setdefault("GOME_PLAN_CUS", "0")
             dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
         else:
             dist.init_process_group("gloo")

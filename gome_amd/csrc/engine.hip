@@ -273,6 +273,7 @@ struct gome_engine {
   hipStream_t plan_stream = nullptr;
   hipEvent_t pl_fork{}, pl_join{};
   uint32_t plan_cus = 0;
+  bool plan_prep = true;  // the early plan's prep after plan_done on the plan's stream (GOME_PLAN_PREP=0: A/B)
   std::vector<uint32_t> cu_rest;  // every CU but the plan's
   hipError_t new_stream(hipStream_t* st) {
     return plan_cus ? hipExtStreamCreateWithCUMask(st, static_cast<uint32_t>(cu_rest.size()), cu_rest.data())
@@ -284,24 +285,26 @@ struct gome_engine {
   static constexpr int NSET = 5;
   hipStream_t alt[NSET]{};
   hipEvent_t sw_ev[NSET]{};
-  bool masked = false;
+  bool masked = false, alt_made = false;
   hipStream_t* live_streams(int i) {
     hipStream_t* v[NSET] = {&stream, &hot_stream, &flow_stream, &copy_stream, &early_stream};
     return v[i];
   }
   hipError_t make_sets() {
-    if (!plan_cus) return hipSuccess;
-    for (int i = 0; i < NSET; ++i) {
+    masked = plan_cus != 0;
+    return hipSuccess;
+  }
+  hipError_t set_masked(bool want) {
+    if (!plan_cus || want == masked) return hipSuccess;
+    // (the other set on first use: idle streams still take hardware queues, which RCCL and torch
+    // need too; with both sets made up front the RCCL line lost 5%)
+    for (int i = 0; i < NSET && !alt_made; ++i) {
       if (!*live_streams(i)) continue;
       hipError_t he = hipStreamCreateWithFlags(&alt[i], hipStreamNonBlocking);
       if (he == hipSuccess) he = hipEventCreateWithFlags(&sw_ev[i], hipEventDisableTiming);
       if (he != hipSuccess) return he;
     }
-    masked = true;
-    return hipSuccess;
-  }
-  hipError_t set_masked(bool want) {
-    if (!plan_cus || want == masked) return hipSuccess;
+    alt_made = true;
     for (int i = 0; i < NSET; ++i) {
       hipStream_t* cur = live_streams(i);
       if (!*cur) continue;
@@ -552,6 +555,7 @@ gome_status gome_engine::init(const gome_config& c) {
     const char* g = std::getenv("GOME_PLAN_CUS");
     plan_cus = g ? static_cast<uint32_t>(std::max(0, std::atoi(g))) : 8u;
     if (plan_cus >= static_cast<uint32_t>(ncu)) plan_cus = 0;
+    if (const char* pp = std::getenv("GOME_PLAN_PREP")) plan_prep = std::atoi(pp) != 0;
     const uint32_t words = (static_cast<uint32_t>(ncu) + 31) / 32;
     cu_rest.assign(words, 0u);
     std::vector<uint32_t> cu_plan(words, 0u);
@@ -928,7 +932,7 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
     // plan on the early stream, so the copy stream stays free for the copies)
     // (GOME_PLAN_CUS: the part after plan_done on the plan's own stream, which then needs no hop)
     hipStream_t es = copy_busy ? copy_stream : early_stream;
-    hipStream_t ps = plan_stream ? plan_stream : copy_busy ? early_stream : copy_stream;
+    hipStream_t ps = (plan_stream && plan_prep) ? plan_stream : copy_busy ? early_stream : copy_stream;
     Dev Dx = D;
     Dx.st = reinterpret_cast<Status*>(reinterpret_cast<char*>(X.ctl) + offsetof(XCtl, st));
     BatchArgs Bx{};
@@ -957,10 +961,15 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
     k_xd_prep_b<<<1, FL_PREP_T, XD_PREP_LDS, ps>>>(Bx, FX, F, X.ctl, x_dnew, bid_prev);
     k_deep_prep_c<<<dim3(FL_PG, 1), FL_PREP_T, 0, ps>>>(Dx, Bx, FX);
     HIPCHK(hipEventRecord(xprep_done, ps));
-    HIPCHK(hipEventRecord(S.evx0, ps));
-    k_flow_plan_early<<<1, 256, plan_lds, ps>>>(Dx, FX);
-    HIPCHK(hipEventRecord(S.evx1, ps));
-    HIPCHK(hipEventRecord(xplan_done, ps));
+    hipStream_t pst = ps;
+    if (plan_stream && !plan_prep) {  // (GOME_PLAN_PREP=0: the prep on the copy stream, a hop to the plan's)
+      HIPCHK(hipStreamWaitEvent(plan_stream, xprep_done, 0));
+      pst = plan_stream;
+    }
+    HIPCHK(hipEventRecord(S.evx0, pst));
+    k_flow_plan_early<<<1, 256, plan_lds, pst>>>(Dx, FX);
+    HIPCHK(hipEventRecord(S.evx1, pst));
+    HIPCHK(hipEventRecord(xplan_done, pst));
   }
 
   // admission markers depend on the input records only: they run on the flow stream beside

@@ -403,7 +403,14 @@ __device__ __forceinline__ void k_deep_sort_scan_one(Dev D, FlowArgs F, uint32_t
   const uint32_t ntile = (nt + FL_TILE - 1) / FL_TILE;
   uint32_t* tc = fd_tcnt(F, F.hdr[h].dslot);
   uint32_t s = 0;
-  for (uint32_t tl = 0; tl < ntile; ++tl) s += tc[tl * FL_CAP + k];
+  constexpr uint32_t U = 8;  // (eight tiles' loads in flight: the hottest book's ~600 tiles after its plan)
+  for (uint32_t t0 = 0; t0 < ntile; t0 += U) {
+    uint32_t v[U];
+#pragma unroll
+    for (uint32_t u = 0; u < U; ++u) v[u] = t0 + u < ntile ? tc[(t0 + u) * FL_CAP + k] : 0u;
+#pragma unroll
+    for (uint32_t u = 0; u < U; ++u) s += v[u];
+  }
   tot[k] = s;
   __syncthreads();
   if (k == 0) {
@@ -411,8 +418,7 @@ __device__ __forceinline__ void k_deep_sort_scan_one(Dev D, FlowArgs F, uint32_t
     for (uint32_t i = 0; i < FL_CAP; ++i) { const uint32_t v = tot[i]; tot[i] = acc; acc += v; }
   }
   __syncthreads();
-  uint32_t run = tot[k];
-  constexpr uint32_t U = 8;  // (eight tiles' loads in flight before their stores, as k_fc_pscan)
+  uint32_t run = tot[k];  // (eight tiles' loads in flight before their stores, as k_fc_pscan)
   for (uint32_t t0 = 0; t0 < ntile; t0 += U) {
     uint32_t v[U];
 #pragma unroll

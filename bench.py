@@ -366,6 +366,8 @@ def main():
                     help="JSON OrderNode messages of the consumer leg (0: off)")
     ap.add_argument("--pool-nodes", type=int, default=0, help="gome_config.max_nodes (0: sized from the run)")
     ap.add_argument("--pool-levels", type=int, default=0, help="gome_config.max_levels (0: sized from the run)")
+    ap.add_argument("--plan-cus", type=int, default=None,
+                    help="gome_config.plan_cus (default: 0 = the engine's default; -1 with RCCL)")
     ap.add_argument("--step-log", default="", help="write each timed step's engine counters (JSONL)")
     ap.add_argument("--sync", action="store_true",
                     help="one synchronous gome_submit_batch_device per step (default: two batches in "
@@ -395,9 +397,6 @@ def main():
         os.environ.setdefault("RANK", "0")
         os.environ.setdefault("WORLD_SIZE", "1")
         if args.backend == "nccl":
-            # (with RCCL in the process the engine's CU-masked plan stream lost 5% per step, for
-            # reasons not established: DESIGN 4.7; such a host keeps every CU shared)
-            os.environ.setdefault("GOME_PLAN_CUS", "0")
             dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
         else:
             dist.init_process_group("gloo")
@@ -405,6 +404,9 @@ def main():
 
     from gome_amd.abi import GOME_MAX_INFLIGHT, Engine
 
+    # gome_config.plan_cus: with RCCL in the process the engine's CU-masked plan stream lost 5% per
+    # step in round 4, for reasons not established, so such a host keeps every CU shared
+    plan_cus = args.plan_cus if args.plan_cus is not None else (-1 if use_pg and args.backend == "nccl" else 0)
     W = WORKLOADS[args.workload]
     n_symbols = W["symbols"]
     steps, warm = args.steps, args.warmup
@@ -430,7 +432,7 @@ def main():
     eng = Engine(max_symbols=n_symbols, max_batch=per_rank,
                  max_nodes=args.pool_nodes or max(1 << 20, int(total_orders * keep)) + head,
                  max_levels=args.pool_levels or max(1 << 22, (256 if n_symbols <= 100000 else 128) * n_symbols) + head,
-                 device=dev)
+                 device=dev, plan_cus=plan_cus)
 
     summary = torch.zeros(SUMMARY_WORDS, dtype=torch.int64, device=cdev)
     gathered = torch.zeros(SUMMARY_WORDS * world, dtype=torch.int64, device=cdev)

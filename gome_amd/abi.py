@@ -16,13 +16,17 @@ from .workload import EVENT_DTYPE, LEVEL_DTYPE, NODE_DTYPE, ORDER_DTYPE
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GOME_LIB") or os.path.join(_HERE, "libgome.so")  # GOME_LIB: variant builds (tools/)
 HEADER = os.path.join(os.path.dirname(_HERE), "include", "gome", "gome_abi.h")
-HEADERS = [HEADER, os.path.join(os.path.dirname(_HERE), "include", "gome", "gome_loadgen.h")]
+HEADERS = [HEADER, os.path.join(os.path.dirname(_HERE), "include", "gome", "gome_loadgen.h"),
+           os.path.join(os.path.dirname(_HERE), "include", "gome", "gome_host.h")]
 
 GOME_FLAG_LEGACY_HOT = 1  # gome_config.flags: hot books on the legacy FIFO kernel
 GOME_FLAG_NO_HEADROOM = 2  # gome_config.flags: no pool-headroom check before a submit
 GOME_FLAG_CHAINS_ALWAYS = 4  # gome_config.flags: enqueue the deep / cancel chains on every batch
 GOME_FLAG_CHAINS_NEVER = 8  # gome_config.flags: never (deep books and books with DELs: legacy / cold)
 GOME_FLAG_PHASES = 16  # gome_config.flags: record the per-phase timing events (gome_stats.ms_phase)
+GOME_FLAG_NO_EARLY = 32  # gome_config.flags: never plan the hottest book early
+GOME_FLAG_NO_ADM_AHEAD = 64  # gome_config.flags: never run admission ahead of the batch
+GOME_ABI_VERSION = 11
 GOME_ORD_ADM_HOST, GOME_ORD_ADMITTED = 1, 2  # gome_order.flags: host-resolved admission (ABI 4)
 GOME_MAX_INFLIGHT = 3
 
@@ -48,7 +52,11 @@ class GomeError(RuntimeError):
 class Config(C.Structure):
     _fields_ = [("accuracy", C.c_uint32), ("device", C.c_int32), ("max_symbols", C.c_uint32),
                 ("max_batch", C.c_uint32), ("max_nodes", C.c_uint64), ("max_levels", C.c_uint64),
-                ("max_events", C.c_uint64), ("flags", C.c_uint32), ("pad", C.c_uint32)]
+                ("max_events", C.c_uint64), ("flags", C.c_uint32), ("abi_version", C.c_uint32),
+                ("hw_queues", C.c_uint32), ("plan_cus", C.c_int32)]
+
+
+assert C.sizeof(Config) == 56
 
 
 class Stats(C.Structure):
@@ -135,6 +143,47 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.gome_render_events.argtypes = [VP, C.c_size_t, VP, C.c_size_t, C.c_uint64, C.c_uint32, VP, C.c_size_t,
                                        VP, C.c_size_t, VP, C.c_size_t, VP, VP, C.c_size_t]
     lib.gome_render_events.restype = C.c_int64
+    lib.gome_render_events_mt.argtypes = [VP, C.c_size_t, VP, C.c_size_t, C.c_uint64, C.c_uint32, VP, C.c_size_t,
+                                          VP, C.c_size_t, VP, C.c_size_t, VP, C.c_uint32, VP, C.c_size_t]
+    lib.gome_render_events_mt.restype = C.c_int64
+    # gome_host.h: interning, pre-pool markers, the native OrderNode consumer
+    SZ, CP = C.c_size_t, C.c_char_p
+    lib.gome_names_create.restype = VP
+    lib.gome_names_destroy.argtypes = [VP]
+    lib.gome_names_destroy.restype = None
+    lib.gome_names_intern.argtypes = [VP, C.c_int, CP, SZ]
+    lib.gome_names_intern.restype = C.c_int64
+    lib.gome_names_find.argtypes = [VP, C.c_int, CP, SZ]
+    lib.gome_names_find.restype = C.c_int64
+    lib.gome_names_count.argtypes = [VP, C.c_int]
+    lib.gome_names_count.restype = SZ
+    lib.gome_names_get.argtypes = [VP, C.c_int, C.c_uint32, P(SZ)]
+    lib.gome_names_get.restype = VP
+    lib.gome_names_table.argtypes = [VP, C.c_int]
+    lib.gome_names_table.restype = VP
+    lib.gome_names_tx_code.argtypes = [VP, C.c_int32]
+    lib.gome_names_tx_code.restype = C.c_int32
+    lib.gome_names_tx_table.argtypes = [VP]
+    lib.gome_names_tx_table.restype = P(C.c_int32)
+    lib.gome_names_tx_count.argtypes = [VP]
+    lib.gome_names_tx_count.restype = SZ
+    lib.gome_prepool_create.restype = VP
+    lib.gome_prepool_destroy.argtypes = [VP]
+    lib.gome_prepool_destroy.restype = None
+    lib.gome_prepool_set.argtypes = [VP, CP, SZ, CP, SZ, CP, SZ]
+    lib.gome_prepool_set.restype = None
+    lib.gome_prepool_take.argtypes = [VP, CP, SZ, CP, SZ, CP, SZ]
+    lib.gome_prepool_take.restype = C.c_int32
+    lib.gome_prepool_size.argtypes = [VP]
+    lib.gome_prepool_size.restype = SZ
+    lib.gome_prepool_commit.argtypes = [VP]
+    lib.gome_prepool_commit.restype = None
+    lib.gome_prepool_abort.argtypes = [VP]
+    lib.gome_prepool_abort.restype = None
+    lib.gome_decode_order_nodes.argtypes = [VP, VP, SZ, C.c_uint32, VP, VP, SZ]
+    lib.gome_decode_order_nodes.restype = C.c_int64
+    lib.gome_consume_order_nodes.argtypes = [VP, VP, VP, VP, SZ, C.c_uint32, C.c_uint32, VP, VP, P(SZ), VP]
+    lib.gome_consume_order_nodes.restype = C.c_int32
     lib.gome_gen_create.argtypes = [VP, P(VP)]
     lib.gome_gen_batch.argtypes = [VP, VP, C.c_size_t]
     lib.gome_gen_shares.argtypes = [VP, P(C.c_double), P(C.c_double)]
@@ -236,11 +285,18 @@ class Engine:
 
     def __init__(self, max_symbols: int, max_batch: int, max_nodes: int = 1 << 20,
                  max_levels: int = 1 << 20, accuracy: int = 8, device: int = 0,
-                 max_events: int = 0, flags: int = 0):
+                 max_events: int = 0, flags: int = 0, hw_queues: int | None = None, plan_cus: int = 0):
+        """hw_queues: the hardware queues this process's HIP runtime started with (the stream
+        layout, gome_config.hw_queues); None = what gome_amd recorded at import (gome_amd.hw_queues()).
+        plan_cus: CUs reserved for the hottest book's plan (0 = default, < 0 = none)."""
+        from . import hw_queues as _hw_queues
         self.lib = load_library()
+        if hw_queues is None:
+            hw_queues = _hw_queues()
         cfg = Config(accuracy=accuracy, device=device, max_symbols=max_symbols,
                      max_batch=max_batch, max_nodes=max_nodes, max_levels=max_levels,
-                     max_events=max_events, flags=flags)
+                     max_events=max_events, flags=flags, abi_version=GOME_ABI_VERSION,
+                     hw_queues=hw_queues, plan_cus=plan_cus)
         h = C.c_void_p()
         s = self.lib.gome_create(C.byref(cfg), C.byref(h))
         if s != GOME_OK:
@@ -250,7 +306,7 @@ class Engine:
         self.max_symbols = max_symbols
         self.cfg_kwargs = dict(max_symbols=max_symbols, max_batch=max_batch, max_nodes=max_nodes,
                                max_levels=max_levels, accuracy=accuracy, device=device,
-                               max_events=max_events, flags=flags)
+                               max_events=max_events, flags=flags, hw_queues=hw_queues, plan_cus=plan_cus)
 
     def close(self):
         if getattr(self, "h", None):

@@ -6,6 +6,7 @@ repository snapshot (they are git-ignored, not gpurun-ignored).
 from __future__ import annotations
 
 import glob
+import hashlib
 import os
 import shutil
 import subprocess
@@ -21,16 +22,41 @@ ORACLE_LIB = os.path.join(ORACLE_DIR, "build", "liboracle.so")
 HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
 ARCH = os.environ.get("GOME_OFFLOAD_ARCH", "gfx950")
 
-SOURCES = [os.path.join(CSRC, "engine.hip"), os.path.join(CSRC, "host.cpp"), os.path.join(CSRC, "loadgen.cpp")]
+SOURCES = [os.path.join(CSRC, "engine.hip"), os.path.join(CSRC, "host.cpp"), os.path.join(CSRC, "consume.cpp"),
+           os.path.join(CSRC, "loadgen.cpp")]
 HEADERS = (sorted(glob.glob(os.path.join(CSRC, "*.h"))) + sorted(glob.glob(os.path.join(CSRC, "*.inc"))) +
            sorted(glob.glob(os.path.join(ROOT, "include", "gome", "*.h"))) + [os.path.abspath(__file__)])
 
 
-def _stale(out: str, deps: list[str]) -> bool:
-    if not os.path.exists(out):
-        return True
-    t = os.path.getmtime(out)
-    return any(os.path.getmtime(d) > t for d in deps)
+def _digest(deps: list[str], cmd: list[str]) -> str:
+    """sha256 over the build command and every source's path and content (not mtimes: the
+    snapshot that travels to the GPU box does not keep them in order)."""
+    h = hashlib.sha256("\0".join(cmd).encode())
+    for d in sorted(deps):
+        h.update(os.path.relpath(d, ROOT).encode() + b"\0")
+        with open(d, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()
+
+
+def _stale(out: str, deps: list[str], cmd: list[str]) -> tuple[bool, str]:
+    """(needs a build, digest): the output is current iff its sidecar <out>.sha256 names the
+    digest of these sources built by this command."""
+    dig = _digest(deps, cmd)
+    try:
+        with open(out + ".sha256") as f:
+            cur = f.read().strip() == dig
+    except OSError:
+        cur = False
+    return (not cur or not os.path.exists(out)), dig
+
+
+def _stamp(out: str, dig: str) -> None:
+    with open(out + ".sha256", "w") as f:
+        f.write(dig + "\n")
+
+
+BUILT: list[str] = []  # what the last build_* calls compiled (build() reports it)
 
 
 def _run(cmd: list[str]):
@@ -48,13 +74,16 @@ DEVICE_FLAGS = ["-mllvm", "-sink-common-insts=false"]
 
 
 def build_engine(force: bool = False, extra: list[str] | None = None) -> str:
-    if force or _stale(LIB, SOURCES + HEADERS):
-        tmp = LIB + ".tmp"
-        cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-               "-Wall", "-Wno-unused-result", *DEVICE_FLAGS, "-I", os.path.join(ROOT, "include"),
-               *SOURCES, "-o", tmp] + (extra or [])
+    tmp = LIB + ".tmp"
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+           "-Wall", "-Wno-unused-result", *DEVICE_FLAGS, "-I", os.path.join(ROOT, "include"),
+           *SOURCES, "-o", tmp] + (extra or [])
+    stale, dig = _stale(LIB, SOURCES + HEADERS, cmd)
+    if force or stale:
         _run(cmd)
         os.replace(tmp, LIB)
+        _stamp(LIB, dig)
+        BUILT.append(LIB)
     return LIB
 
 
@@ -70,17 +99,24 @@ def build_stamps() -> str:
 def build_oracle(force: bool = False) -> str:
     src = os.path.join(ORACLE_DIR, "gome_oracle.c")
     deps = [src, os.path.join(ROOT, "include", "gome", "gome_abi.h")]
-    if force or _stale(ORACLE_LIB, deps):
+    tmp = ORACLE_LIB + ".tmp"
+    cmd = ["gcc", "-O2", "-std=c99", "-fPIC", "-shared", "-Wall", src, "-o", tmp]
+    stale, dig = _stale(ORACLE_LIB, deps, cmd)
+    if force or stale:
         os.makedirs(os.path.dirname(ORACLE_LIB), exist_ok=True)
-        tmp = ORACLE_LIB + ".tmp"
-        _run(["gcc", "-O2", "-std=c99", "-fPIC", "-shared", "-Wall", src, "-o", tmp])
+        _run(cmd)
         os.replace(tmp, ORACLE_LIB)
+        _stamp(ORACLE_LIB, dig)
+        BUILT.append(ORACLE_LIB)
     return ORACLE_LIB
 
 
-def build_all(force: bool = False) -> None:
+def build_all(force: bool = False) -> list[str]:
+    """Build what is stale; returns the outputs compiled by this call (empty: all current)."""
+    n = len(BUILT)
     build_engine(force)
     build_oracle(force)
+    return BUILT[n:]
 
 
 if __name__ == "__main__":

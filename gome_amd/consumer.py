@@ -40,212 +40,174 @@ GOME_E_CAPACITY before anything is applied) can be resubmitted with the same ver
 """
 from __future__ import annotations
 
-import codecs
 import ctypes as C
 import json
-import math
 import queue as _queue
-import re
 import threading
 import time
 
 import numpy as np
 
-from .abi import (GOME_ORD_ADM_HOST, GOME_ORD_ADMITTED, GomeError, fixed_from_double,
-                  fixed_from_scaled, load_library)
+from .abi import GomeError, fixed_from_double, load_library
 from .workload import ADD, DEL, ORDER_DTYPE
 
 
+_KIND = {"sym": 0, "uuid": 1, "oid": 2}  # GOME_NAME_SYMBOL / _UUID / _OID (gome_host.h)
+
+
+def _b(s) -> bytes:
+    return s if isinstance(s, (bytes, bytearray)) else str(s).encode("utf-8", "surrogatepass")
+
+
 class Names:
-    """Host interning: symbol / uuid / oid strings <-> u32 ids, Transaction int32 <-> code."""
+    """Host interning (gome_names, gome_host.h): symbol / uuid / oid strings <-> u32 ids,
+    Transaction int32 <-> one-byte code."""
 
     def __init__(self):
-        self.fwd = {"sym": {}, "uuid": {}, "oid": {}}
-        self.rev = {"sym": [], "uuid": [], "oid": []}
-        self._c = {k: [] for k in self.rev}  # bytes kept alive for the C string tables
-        self._tab = {k: None for k in self.rev}
-        self.tx_fwd = {0: 0, 1: 1}
-        self.tx_rev = [0, 1]
-        self._txa = None
+        self.lib = load_library()
+        self.h = self.lib.gome_names_create()
+        if not self.h:
+            raise MemoryError("gome_names_create")
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            self.lib.gome_names_destroy(self.h)
+            self.h = None
 
     def id(self, kind: str, s: str) -> int:
-        d = self.fwd[kind]
-        i = d.get(s)
-        if i is None:
-            i = d[s] = len(self.rev[kind])
-            self.rev[kind].append(s)
-            self._c[kind].append(s.encode())
-            self._tab[kind] = None
+        b = _b(s)
+        i = self.lib.gome_names_intern(self.h, _KIND[kind], b, len(b))
+        if i < 0:
+            raise GomeError(1, "gome_names_intern failed")
         return i
 
+    def find(self, kind: str, s: str) -> int:
+        b = _b(s)
+        return self.lib.gome_names_find(self.h, _KIND[kind], b, len(b))
+
     def name(self, kind: str, i: int) -> str:
-        return self.rev[kind][i]
+        n = C.c_size_t()
+        p = self.lib.gome_names_get(self.h, _KIND[kind], int(i), C.byref(n))
+        if not p:
+            raise IndexError(f"{kind} id {i}")
+        return C.string_at(p, n.value).decode("utf-8", "surrogatepass")
+
+    def count(self, kind: str) -> int:
+        return self.lib.gome_names_count(self.h, _KIND[kind])
 
     def tx_code(self, raw: int) -> int:
-        raw = int(raw)
-        c = self.tx_fwd.get(raw)
-        if c is None:
-            if len(self.tx_rev) == 256:
-                raise GomeError(1, "more than 254 distinct Transaction values outside {0, 1}")
-            c = self.tx_fwd[raw] = len(self.tx_rev)
-            self.tx_rev.append(raw)
-            self._txa = None
+        c = self.lib.gome_names_tx_code(self.h, int(raw))
+        if c < 0:
+            raise GomeError(1, "more than 254 distinct Transaction values outside {0, 1}")
         return c
 
     def tx_raw(self, code: int) -> int:
-        return self.tx_rev[code] if code < len(self.tx_rev) else code
+        return int(self.tx_array()[code])
 
     def table(self, kind: str):
-        t = self._tab[kind]
-        if t is None:
-            t = self._tab[kind] = (C.c_char_p * max(1, len(self._c[kind])))(*self._c[kind])
-        return t
+        """The NUL-terminated strings by id (gome_render_events' tables; valid until the next id)."""
+        return C.c_void_p(self.lib.gome_names_table(self.h, _KIND[kind]))
 
     def tx_array(self) -> np.ndarray:
-        if self._txa is None:
-            a = np.arange(256, dtype=np.int32)
-            a[:len(self.tx_rev)] = self.tx_rev
-            self._txa = a
-        return self._txa
+        """The raw Transaction of every code (a view of the native table)."""
+        return np.ctypeslib.as_array(self.lib.gome_names_tx_table(self.h), shape=(256,))
 
 
 class PrePool:
-    """S:comparison (nodepool.go:14-28): markers keyed (symbol, uuid, oid)."""
+    """S:comparison (nodepool.go:14-28): markers keyed (symbol, uuid, oid) (gome_prepool,
+    gome_host.h; markers may be set from any thread).  The consumer consumes them staged
+    (gome_consume_order_nodes) and commits once the engine took the batch."""
 
     def __init__(self):
-        self._s: set = set()
-        self._lock = threading.Lock()
+        self.lib = load_library()
+        self.h = self.lib.gome_prepool_create()
+        if not self.h:
+            raise MemoryError("gome_prepool_create")
 
-    def stage(self) -> "StagedMarkers":
-        return StagedMarkers(self)
+    def __del__(self):
+        if getattr(self, "h", None):
+            self.lib.gome_prepool_destroy(self.h)
+            self.h = None
 
-    def commit(self, consumed: set):
-        """Remove the markers a staged batch consumed (after the engine accepted the batch)."""
-        with self._lock:
-            self._s -= consumed
+    @staticmethod
+    def _key(symbol, uuid, oid):
+        a, b, c = _b(symbol), _b(uuid), _b(oid)
+        return a, len(a), b, len(b), c, len(c)
 
     def set(self, symbol: str, uuid: str, oid: str):  # SetPrePool (main.go:44-45)
-        with self._lock:
-            self._s.add((symbol, uuid, oid))
+        self.lib.gome_prepool_set(self.h, *self._key(symbol, uuid, oid))
 
     def consume_add(self, symbol: str, uuid: str, oid: str) -> bool:
         """ExistsPrePool + DeletePrePool at consume time (engine.go:58-62)."""
-        with self._lock:
-            k = (symbol, uuid, oid)
-            if k in self._s:
-                self._s.discard(k)
-                return True
-            return False
+        return self.lib.gome_prepool_take(self.h, *self._key(symbol, uuid, oid)) != 0
 
     def consume_del(self, symbol: str, uuid: str, oid: str):  # DeletePrePool (engine.go:90)
-        with self._lock:
-            self._s.discard((symbol, uuid, oid))
-
-    def __len__(self):
-        return len(self._s)
-
-
-class StagedMarkers:
-    """One batch's admission verdicts against the pre-pool, in queue order, without consuming
-    anything yet: an ADD is admitted iff its marker exists and no earlier record of the batch
-    consumed it (ExistsPrePool + DeletePrePool, engine.go:58-62,90)."""
-
-    def __init__(self, pool: PrePool):
-        self.pool, self.consumed = pool, set()
-
-    def consume_add(self, symbol: str, uuid: str, oid: str) -> bool:
-        k = (symbol, uuid, oid)
-        if k in self.consumed:
-            return False
-        with self.pool._lock:
-            ok = k in self.pool._s
-        if ok:
-            self.consumed.add(k)
-        return ok
-
-    def consume_del(self, symbol: str, uuid: str, oid: str):
-        with self.pool._lock:
-            if (symbol, uuid, oid) in self.pool._s:
-                self.consumed.add((symbol, uuid, oid))
+        self.lib.gome_prepool_take(self.h, *self._key(symbol, uuid, oid))
 
     def commit(self):
-        self.pool.commit(self.consumed)
-        self.consumed = set()
+        """Remove the markers the last consumed batch took (the engine accepted it)."""
+        self.lib.gome_prepool_commit(self.h)
+
+    def abort(self):
+        """Forget the last consumed batch's provisional consumption (the engine refused it)."""
+        self.lib.gome_prepool_abort(self.h)
+
+    def __len__(self):
+        return self.lib.gome_prepool_size(self.h)
 
 
 # ---- Go encoding/json Unmarshal of the consumed OrderNode (ordernode.go:9-36) -----------------
-# Only the fields the engine reads; the key fields (OrderHashKey, NodeName, ...) are the ones
-# NewOrderNode derives from them at gRPC time (ordernode.go:89-117).
-_GO_FIELDS = {"action": ("Action", "i", 8), "uuid": ("Uuid", "s", 0), "oid": ("Oid", "s", 0),
-              "symbol": ("Symbol", "s", 0), "transaction": ("Transaction", "i", 32),
-              "price": ("Price", "f", 0), "volume": ("Volume", "f", 0)}
+# Native (gome_decode_order_nodes / gome_consume_order_nodes, gome_host.h): only the fields the
+# engine reads; the key fields (OrderHashKey, NodeName, ...) are the ones NewOrderNode derives
+# from them at gRPC time (ordernode.go:89-117).
+class _Decoded(C.Structure):
+    _fields_ = [("price", C.c_double), ("volume", C.c_double), ("transaction", C.c_int32), ("action", C.c_int8),
+                ("is_object", C.c_uint8), ("pad", C.c_uint16), ("sym_off", C.c_uint32), ("sym_len", C.c_uint32),
+                ("uuid_off", C.c_uint32), ("uuid_len", C.c_uint32), ("oid_off", C.c_uint32), ("oid_len", C.c_uint32)]
 
 
-_LONE_SURROGATE = re.compile("[\ud800-\udfff]")
+class ConsumeStats(C.Structure):
+    _fields_ = [(n, C.c_uint64) for n in ("messages", "records", "rejected", "ignored", "not_objects", "admitted")]
 
 
-class _Lit(str):
-    """Literal text of a JSON number (Go converts numbers from the literal)."""
+def pack_messages(msgs):
+    """(one buffer, offsets[n + 1]) of the message bodies (bytes as they are; str as UTF-8)."""
+    bodies = [m if isinstance(m, bytes) else _b(m) for m in msgs]
+    off = np.zeros(len(bodies) + 1, np.uint64)
+    if bodies:
+        np.cumsum(np.fromiter(map(len, bodies), np.uint64, len(bodies)), out=off[1:])
+    return b"".join(bodies), off
 
 
-class _Pairs(list):
-    """A JSON object's (key, value) pairs in document order."""
-
-
-def _reject_constant(tok):
-    raise ValueError(tok)  # NaN / Infinity are not JSON to Go
-
-
-def _go_bytes_to_str(body) -> str:
-    """Go's encoding/json replaces every byte of invalid UTF-8 with U+FFFD, one per byte
-    (utf8.DecodeRune returns (RuneError, 1)); Python's 'replace' would merge a truncated sequence."""
-    return body.decode("utf-8", errors="gome_go_bytes")
-
-
-def _go_replace(exc):
-    return "\ufffd", exc.start + 1
-
-
-codecs.register_error("gome_go_bytes", _go_replace)
+def decode_order_nodes(msgs, threads: int = 0) -> list[dict]:
+    """json.Unmarshal of each body into an OrderNode, the fields the engine reads: {"Action",
+    "Uuid", "Oid", "Symbol", "Transaction", "Price", "Volume"} (gome_decode_order_nodes).  Keys
+    match exactly or case-insensitively (Go's foldName); later duplicates win; an int field takes
+    only an integer literal within its width (Action int8, Transaction int32), a float field any
+    finite number, a string field only a string; anything else (and null) leaves the zero value; a
+    syntax error or a non-object decodes nothing."""
+    lib = load_library()
+    buf, off = pack_messages(msgs)
+    n = len(off) - 1
+    out = (_Decoded * max(n, 1))()
+    cap = 3 * len(buf) + 1
+    sb = C.create_string_buffer(cap)
+    used = lib.gome_decode_order_nodes(buf, off.ctypes.data, n, threads, out, sb, cap)
+    if used < 0:
+        raise GomeError(1, "gome_decode_order_nodes failed")
+    raw = sb.raw
+    res = []
+    for k in range(n):
+        d = out[k]
+        st = lambda o, ln: raw[o:o + ln].decode("utf-8", "surrogatepass")  # noqa: E731
+        res.append({"Action": d.action, "Uuid": st(d.uuid_off, d.uuid_len), "Oid": st(d.oid_off, d.oid_len),
+                    "Symbol": st(d.sym_off, d.sym_len), "Transaction": d.transaction, "Price": d.price,
+                    "Volume": d.volume})
+    return res
 
 
 def decode_order_node(body) -> dict:
-    """The OrderNode fields json.Unmarshal leaves: {"Action", "Uuid", "Oid", "Symbol",
-    "Transaction", "Price", "Volume"}.  Never raises.  Keys match exactly or case-insensitively
-    (Go's field matching); later duplicates win; an int field takes only an integer literal
-    within its width (Action int8, Transaction int32), a float field any finite number, a
-    string field only a string; anything else (and null) leaves the zero value."""
-    out = {"Action": 0, "Uuid": "", "Oid": "", "Symbol": "", "Transaction": 0, "Price": 0.0, "Volume": 0.0}
-    if isinstance(body, (bytes, bytearray, memoryview)):
-        body = _go_bytes_to_str(bytes(body))
-    try:
-        doc = json.loads(body, parse_int=_Lit, parse_float=_Lit, parse_constant=_reject_constant,
-                         object_pairs_hook=_Pairs)
-    except (ValueError, TypeError, RecursionError):
-        return out  # syntax error: Unmarshal decodes nothing
-    if not isinstance(doc, _Pairs):
-        return out
-    for key, val in doc:
-        f = _GO_FIELDS.get(key.casefold())  # (Unicode folding, as Go's EqualFold: 'ſ' ~ 's')
-        if f is None or val is None:
-            continue
-        name, kind, bits = f
-        if kind == "s":
-            if isinstance(val, str) and not isinstance(val, _Lit):
-                out[name] = _LONE_SURROGATE.sub("\ufffd", val)  # Go decodes a lone \\uD8xx as U+FFFD
-        elif isinstance(val, _Lit):
-            if kind == "f":
-                x = float(val)
-                if not math.isinf(x):  # ParseFloat out of range: UnmarshalTypeError, skipped
-                    out[name] = x
-            else:
-                try:
-                    x = int(val, 10)  # ParseInt: no fraction, no exponent
-                except ValueError:
-                    continue
-                if -(1 << (bits - 1)) <= x < (1 << (bits - 1)):
-                    out[name] = x
-    return out
+    return decode_order_nodes([body])[0]
 
 
 def _order_node_json(req: dict, action: int, price: float, volume: float, accuracy: int) -> str:
@@ -311,20 +273,22 @@ class MatchSink:
 
 
 class BatchingConsumer:
-    """Replaces ConsumeNewOrder (rabbitmq.go:86-130) in front of one engine handle."""
+    """Replaces ConsumeNewOrder (rabbitmq.go:86-130) in front of one engine handle.  The per-message
+    work is native (gome_consume_order_nodes: Go-Unmarshal decode on `threads` threads, conversion,
+    interning, admission in queue order; gome_render_events_mt: the MatchResult lines)."""
 
     def __init__(self, engine, prepool: PrePool, sink: MatchSink, names: Names | None = None,
-                 max_batch: int | None = None, max_wait_us: int = 200, accuracy: int = 8):
+                 max_batch: int | None = None, max_wait_us: int = 200, accuracy: int = 8, threads: int = 8):
         self.eng, self.pre, self.sink = engine, prepool, sink
         self.names = names or Names()
         self.max_batch = int(max_batch or engine.max_batch)
         self.max_wait = max_wait_us * 1e-6
         self.acc = accuracy
+        self.threads = threads
         self.lib = load_library()
         self.max_symbols = getattr(engine, "max_symbols", None)
         self.seq = 0
         self.consumed = self.rejected = self.batches = self.dups = 0
-        self._staged = None
         self._buf = C.create_string_buffer(1 << 20)
 
     # ---- draining ------------------------------------------------------------------
@@ -350,63 +314,37 @@ class BatchingConsumer:
 
     # ---- one batch -------------------------------------------------------------------
     def records(self, msgs) -> np.ndarray:
-        """Decode, convert and admit (in queue order) -> gome_order records.  The admission
-        verdicts come from a staged view of the pre-pool (committed by process() once the
-        engine took the batch)."""
-        N = self.names
-        pre = self._staged = self.pre.stage()
-        rec = np.zeros(len(msgs), ORDER_DTYPE)
-        keep = np.ones(len(msgs), bool)
-        for i, body in enumerate(msgs):
-            o = decode_order_node(body)
-            act, sym, uuid, oid = o["Action"], o["Symbol"], o["Uuid"], o["Oid"]
-            if act not in (ADD, DEL):
-                continue  # DoOrder ignores any other Action (engine.go:46-54): a zero record
-            try:
-                p, v = fixed_from_scaled(o["Price"]), fixed_from_scaled(o["Volume"])
-                if v < 0:  # (the engine's record domain: volume >= 0, gome_abi.h)
-                    raise GomeError(1, "negative Volume")
-                if self.max_symbols is not None and N.fwd["sym"].get(sym, len(N.rev["sym"])) >= self.max_symbols:
-                    raise GomeError(1, "more distinct Symbols than the engine's max_symbols")
-                code = N.tx_code(o["Transaction"])
-            except GomeError:
-                # outside the parity domain (Q5, a negative Volume), or beyond the engine's symbol
-                # range or Transaction code space: not submitted, so it cannot refuse the batch
-                keep[i] = False
-                self.rejected += 1
-                if act == ADD:
-                    pre.consume_add(sym, uuid, oid)
-                else:
-                    pre.consume_del(sym, uuid, oid)
-                continue
-            r = rec[i]
-            r["price_fx"], r["volume_fx"] = p, v
-            r["symbol_id"], r["uuid_id"], r["oid_id"] = N.id("sym", sym), N.id("uuid", uuid), N.id("oid", oid)
-            r["side"] = code
-            r["action"] = act
-            if act == ADD:
-                ok = pre.consume_add(sym, uuid, oid)
-                r["flags"] = GOME_ORD_ADM_HOST | (GOME_ORD_ADMITTED if ok else 0)
-            else:
-                pre.consume_del(sym, uuid, oid)
-                r["flags"] = GOME_ORD_ADM_HOST
-        return rec[keep]
+        """Decode, convert and admit (in queue order) -> gome_order records.  The pre-pool markers
+        are consumed staged (process() commits them once the engine took the batch).  A message
+        outside the engine's domain is counted in `rejected` and not submitted; an Action other
+        than ADD / DEL (a syntax error included) is a zero record, as DoOrder ignores it."""
+        self.pre.abort()  # (a batch refused earlier left nothing behind)
+        buf, off = pack_messages(msgs)
+        n = len(off) - 1
+        rec = np.zeros(n, ORDER_DTYPE)
+        got, st = C.c_size_t(), ConsumeStats()
+        s = self.lib.gome_consume_order_nodes(self.names.h, self.pre.h, buf, off.ctypes.data, n,
+                                              int(self.max_symbols or 0), self.threads, rec.ctypes.data, None,
+                                              C.byref(got), C.byref(st))
+        if s != 0:
+            raise GomeError(s, "gome_consume_order_nodes failed")
+        self.rejected += st.rejected
+        return rec[:got.value]
 
     def render(self, ev: np.ndarray, rec: np.ndarray, seq_base: int) -> list[str]:
         N = self.names
         while True:
-            k = self.lib.gome_render_events(
+            k = self.lib.gome_render_events_mt(
                 ev.ctypes.data, len(ev), rec.ctypes.data, len(rec), seq_base, self.acc,
-                C.cast(N.table("sym"), C.c_void_p), len(N.rev["sym"]),
-                C.cast(N.table("uuid"), C.c_void_p), len(N.rev["uuid"]),
-                C.cast(N.table("oid"), C.c_void_p), len(N.rev["oid"]),
-                N.tx_array().ctypes.data, self._buf, len(self._buf))
+                N.table("sym"), N.count("sym"), N.table("uuid"), N.count("uuid"),
+                N.table("oid"), N.count("oid"), N.tx_array().ctypes.data, self.threads,
+                self._buf, len(self._buf))
             if k >= 0:
                 break
             if k == -(1 << 63):
                 raise GomeError(1, "event references an unknown id")
             self._buf = C.create_string_buffer(int(-k) + (1 << 20))
-        return self._buf.raw[:k].decode().split("\n")[:-1]
+        return C.string_at(self._buf, k).decode().split("\n")[:-1]
 
     def process(self, msgs) -> int:
         """Apply one drained batch; returns the MatchResults published.  Raises only when the
@@ -414,11 +352,16 @@ class BatchingConsumer:
         pre-pool is then untouched and the same messages can be processed again."""
         rec = self.records(msgs)
         if len(rec) > self.eng.max_batch:
+            self.pre.abort()
             raise GomeError(1, "batch larger than the engine's max_batch")
         base = self.seq
         if len(rec):
-            self.eng.submit(rec, seq_base=base)
-        self._staged.commit()  # the engine took the batch: its markers are consumed
+            try:
+                self.eng.submit(rec, seq_base=base)
+            except BaseException:
+                self.pre.abort()
+                raise
+        self.pre.commit()  # the engine took the batch: its markers are consumed
         self.consumed += len(msgs)
         if len(rec) == 0:
             return 0

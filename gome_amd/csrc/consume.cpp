@@ -1,0 +1,926 @@
+// consume.cpp — the batching consumer's per-message work in native code (include/gome/gome_host.h):
+// Go encoding/json decoding of the doOrder OrderNode bodies (rabbitmq.go:118-121), interning,
+// fixed-point conversion and the pre-pool admission markers (engine.go:58-62,90;
+// nodepool.go:14-28), one call per drained batch.  Host-only: no device work.
+#include <algorithm>
+#include <charconv>
+#include <cmath>
+#include <cstdint>
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/gome/gome_host.h"
+
+extern "C" gome_status gome_fixed_from_scaled(double v, int64_t* out);
+
+namespace {
+
+constexpr int MAX_DEPTH = 10000;  // encoding/json scanner.go maxNestingDepth
+
+// ---- UTF-8 (Go unicode/utf8) -------------------------------------------------------------------
+// utf8.DecodeRune: (rune, size), (U+FFFD, 1) for a byte that does not start a valid encoding
+// (bad lead, truncated, overlong, surrogate, beyond U+10FFFF).
+inline uint32_t decode_rune(const unsigned char* p, const unsigned char* e, int* size) {
+  const unsigned c = p[0];
+  *size = 1;
+  if (c < 0x80) return c;
+  auto cont = [&](int k, unsigned lo, unsigned hi) { return p + k < e && p[k] >= lo && p[k] <= hi; };
+  if (c >= 0xC2 && c <= 0xDF) {
+    if (!cont(1, 0x80, 0xBF)) return 0xFFFD;
+    *size = 2;
+    return ((c & 0x1F) << 6) | (p[1] & 0x3F);
+  }
+  if (c >= 0xE0 && c <= 0xEF) {
+    const unsigned lo = c == 0xE0 ? 0xA0 : 0x80, hi = c == 0xED ? 0x9F : 0xBF;
+    if (!cont(1, lo, hi) || !cont(2, 0x80, 0xBF)) return 0xFFFD;
+    *size = 3;
+    return ((c & 0x0F) << 12) | ((p[1] & 0x3F) << 6) | (p[2] & 0x3F);
+  }
+  if (c >= 0xF0 && c <= 0xF4) {
+    const unsigned lo = c == 0xF0 ? 0x90 : 0x80, hi = c == 0xF4 ? 0x8F : 0xBF;
+    if (!cont(1, lo, hi) || !cont(2, 0x80, 0xBF) || !cont(3, 0x80, 0xBF)) return 0xFFFD;
+    *size = 4;
+    return ((c & 0x07) << 18) | ((p[1] & 0x3F) << 12) | ((p[2] & 0x3F) << 6) | (p[3] & 0x3F);
+  }
+  return 0xFFFD;
+}
+
+inline void put_rune(std::string& o, uint32_t r) {
+  if (r < 0x80) {
+    o.push_back(static_cast<char>(r));
+  } else if (r < 0x800) {
+    o.push_back(static_cast<char>(0xC0 | (r >> 6)));
+    o.push_back(static_cast<char>(0x80 | (r & 0x3F)));
+  } else if (r < 0x10000) {
+    o.push_back(static_cast<char>(0xE0 | (r >> 12)));
+    o.push_back(static_cast<char>(0x80 | ((r >> 6) & 0x3F)));
+    o.push_back(static_cast<char>(0x80 | (r & 0x3F)));
+  } else {
+    o.push_back(static_cast<char>(0xF0 | (r >> 18)));
+    o.push_back(static_cast<char>(0x80 | ((r >> 12) & 0x3F)));
+    o.push_back(static_cast<char>(0x80 | ((r >> 6) & 0x3F)));
+    o.push_back(static_cast<char>(0x80 | (r & 0x3F)));
+  }
+}
+
+inline int hexv(unsigned c) {
+  if (c >= '0' && c <= '9') return static_cast<int>(c - '0');
+  if (c >= 'a' && c <= 'f') return static_cast<int>(c - 'a' + 10);
+  if (c >= 'A' && c <= 'F') return static_cast<int>(c - 'A' + 10);
+  return -1;
+}
+inline uint32_t hex4(const unsigned char* q) {
+  return static_cast<uint32_t>((hexv(q[0]) << 12) | (hexv(q[1]) << 8) | (hexv(q[2]) << 4) | hexv(q[3]));
+}
+
+// ---- the decoder -------------------------------------------------------------------------------
+// A decoded string: a view into the body (no escape, ASCII only) or a slice of the thread's arena.
+struct Str {
+  const char* p = nullptr;
+  uint32_t len = 0;
+  int32_t arena = -1;  // >= 0: p is unset, the bytes are arenas[arena][off, off + len)
+  uint32_t off = 0;
+};
+
+enum { F_ACTION, F_UUID, F_OID, F_SYMBOL, F_TX, F_PRICE, F_VOLUME, NF };
+
+struct Dec {
+  double price = 0, volume = 0;
+  int32_t tx = 0;
+  int8_t action = 0;
+  bool is_object = false;
+  Str s[3];  // uuid, oid, symbol
+};
+
+// Field match by Go's foldName (encoding/json fold.go): ASCII letters to upper case, and the two
+// non-ASCII runes whose fold orbit holds an ASCII letter (U+017F long s ~ S, U+212A Kelvin ~ K).
+// An exact match is also a folded match, and the fields' folded names are distinct.
+inline bool eq_fold(const unsigned char* k, const char* up, size_t n) {
+  for (size_t i = 0; i < n; ++i)
+    if ((k[i] | 0x20) != (static_cast<unsigned char>(up[i]) | 0x20)) return false;  // (up: letters only)
+  return true;
+}
+
+int match_field_slow(const unsigned char* k, size_t n);
+
+// ASCII keys by length first (every field name is letters only, so a key byte matches an upper-case
+// letter U iff it is U or U + 32); keys with a byte >= 0x80 take the rune-by-rune fold.
+inline int match_field(const unsigned char* k, size_t n) {
+  switch (n) {
+    case 3: if (eq_fold(k, "OID", 3)) return F_OID; break;
+    case 4: if (eq_fold(k, "UUID", 4)) return F_UUID; break;
+    case 5: if (eq_fold(k, "PRICE", 5)) return F_PRICE; break;
+    case 6:
+      if (eq_fold(k, "ACTION", 6)) return F_ACTION;
+      if (eq_fold(k, "SYMBOL", 6)) return F_SYMBOL;
+      if (eq_fold(k, "VOLUME", 6)) return F_VOLUME;
+      break;
+    case 11: if (eq_fold(k, "TRANSACTION", 11)) return F_TX; break;
+    default: break;
+  }
+  for (size_t i = 0; i < n; ++i)
+    if (k[i] >= 0x80) return match_field_slow(k, n);
+  return -1;
+}
+
+int match_field_slow(const unsigned char* k, size_t n) {
+  static const char* const up[NF] = {"ACTION", "UUID", "OID", "SYMBOL", "TRANSACTION", "PRICE", "VOLUME"};
+  char f[16];
+  size_t m = 0;
+  for (size_t i = 0; i < n;) {
+    if (m >= 12) return -1;
+    const unsigned c = k[i];
+    if (c < 0x80) {
+      f[m++] = static_cast<char>((c >= 'a' && c <= 'z') ? c - 32 : c);
+      ++i;
+      continue;
+    }
+    int sz;
+    const uint32_t r = decode_rune(k + i, k + n, &sz);
+    if (r == 0x17F) f[m++] = 'S';
+    else if (r == 0x212A) f[m++] = 'K';
+    else return -1;
+    i += static_cast<size_t>(sz);
+  }
+  for (int j = 0; j < NF; ++j)
+    if (std::strlen(up[j]) == m && std::memcmp(up[j], f, m) == 0) return j;
+  return -1;
+}
+
+struct Parser {
+  const unsigned char* p;
+  const unsigned char* e;
+  std::string* arena;
+  int32_t arena_id;
+  std::string key;  // a decoded key (slow path)
+
+  void ws() {
+    while (p < e && (*p == ' ' || *p == '\t' || *p == '\n' || *p == '\r')) ++p;
+  }
+
+  // A string at p ('"'): validated (scanner.go stateInString: control bytes are errors, any other
+  // byte passes; escapes \" \\ \/ \b \f \n \r \t \uXXXX); [*s, *t) the raw bytes between the quotes;
+  // *plain: no escape and no byte >= 0x80 (the decoded string is the raw bytes).
+  bool scan_string(const unsigned char** s, const unsigned char** t, bool* plain) {
+    ++p;
+    *s = p;
+    bool pl = true;
+    for (;;) {
+      while (p < e && *p != '"' && *p != '\\' && *p >= 0x20 && *p < 0x80) ++p;  // (the common bytes)
+      if (p >= e) return false;
+      const unsigned c = *p;
+      if (c == '"') break;
+      if (c == '\\') {
+        pl = false;
+        if (p + 1 >= e) return false;
+        const unsigned x = p[1];
+        if (x == 'u') {
+          if (p + 6 > e) return false;
+          for (int k = 2; k < 6; ++k)
+            if (hexv(p[k]) < 0) return false;
+          p += 6;
+        } else if (x == '"' || x == '\\' || x == '/' || x == 'b' || x == 'f' || x == 'n' || x == 'r' || x == 't') {
+          p += 2;
+        } else {
+          return false;
+        }
+        continue;
+      }
+      if (c < 0x20) return false;
+      if (c >= 0x80) pl = false;
+      ++p;
+    }
+    *t = p++;
+    *plain = pl;
+    return true;
+  }
+
+  // encoding/json unquote (decode.go): escapes, surrogate pairs, a lone surrogate -> U+FFFD,
+  // invalid UTF-8 -> U+FFFD per byte.
+  static void unquote(const unsigned char* q, const unsigned char* t, std::string& o) {
+    while (q < t) {
+      const unsigned c = *q;
+      if (c == '\\') {
+        const unsigned x = q[1];
+        if (x != 'u') {
+          char ch = static_cast<char>(x);
+          if (x == 'b') ch = '\b';
+          else if (x == 'f') ch = '\f';
+          else if (x == 'n') ch = '\n';
+          else if (x == 'r') ch = '\r';
+          else if (x == 't') ch = '\t';
+          o.push_back(ch);
+          q += 2;
+          continue;
+        }
+        uint32_t r = hex4(q + 2);
+        q += 6;
+        if (r >= 0xD800 && r < 0xE000) {
+          // utf16.DecodeRune(r, getu4(next)): a pair only for high + \u-escaped low
+          if (r < 0xDC00 && q + 6 <= t && q[0] == '\\' && q[1] == 'u') {
+            const uint32_t r1 = hex4(q + 2);
+            if (r1 >= 0xDC00 && r1 < 0xE000) {
+              put_rune(o, 0x10000 + ((r - 0xD800) << 10) + (r1 - 0xDC00));
+              q += 6;
+              continue;
+            }
+          }
+          r = 0xFFFD;
+        }
+        put_rune(o, r);
+        continue;
+      }
+      if (c < 0x80) {
+        o.push_back(static_cast<char>(c));
+        ++q;
+        continue;
+      }
+      int sz;
+      const uint32_t r = decode_rune(q, t, &sz);
+      if (r == 0xFFFD && sz == 1) put_rune(o, 0xFFFD);
+      else o.append(reinterpret_cast<const char*>(q), static_cast<size_t>(sz));
+      q += sz;
+    }
+  }
+
+  bool string_value(Str* out) {
+    const unsigned char *s, *t;
+    bool plain;
+    if (!scan_string(&s, &t, &plain)) return false;
+    if (!out) return true;
+    if (plain) {
+      out->p = reinterpret_cast<const char*>(s);
+      out->len = static_cast<uint32_t>(t - s);
+      out->arena = -1;
+    } else {
+      const size_t o0 = arena->size();
+      unquote(s, t, *arena);
+      out->arena = arena_id;
+      out->off = static_cast<uint32_t>(o0);
+      out->len = static_cast<uint32_t>(arena->size() - o0);
+    }
+    return true;
+  }
+
+  // A number literal at p (JSON grammar); [*s, p) its text; *is_int: no fraction, no exponent.
+  bool number(const unsigned char** s, bool* is_int) {
+    *s = p;
+    if (*p == '-') ++p;
+    if (p >= e) return false;
+    if (*p == '0') {
+      ++p;
+    } else if (*p >= '1' && *p <= '9') {
+      while (p < e && *p >= '0' && *p <= '9') ++p;
+    } else {
+      return false;
+    }
+    *is_int = true;
+    if (p < e && *p == '.') {
+      ++p;
+      if (p >= e || *p < '0' || *p > '9') return false;
+      while (p < e && *p >= '0' && *p <= '9') ++p;
+      *is_int = false;
+    }
+    if (p < e && (*p == 'e' || *p == 'E')) {
+      ++p;
+      if (p < e && (*p == '+' || *p == '-')) ++p;
+      if (p >= e || *p < '0' || *p > '9') return false;
+      while (p < e && *p >= '0' && *p <= '9') ++p;
+      *is_int = false;
+    }
+    return true;
+  }
+
+  bool literal(const char* w) {
+    const size_t n = std::strlen(w);
+    if (static_cast<size_t>(e - p) < n || std::memcmp(p, w, n) != 0) return false;
+    p += n;
+    return true;
+  }
+
+  // Validate one value at p (after whitespace), nested in `depth` containers; iterative.
+  bool skip_value(int depth) {
+    std::vector<char> st;  // open containers below this value
+    for (;;) {
+      // a value
+      ws();
+      if (p >= e) return false;
+      const unsigned c = *p;
+      bool opened = false;
+      if (c == '{' || c == '[') {
+        if (depth + static_cast<int>(st.size()) + 1 > MAX_DEPTH) return false;
+        ++p;
+        ws();
+        if (p < e && *p == (c == '{' ? '}' : ']')) {
+          ++p;  // empty container: a complete value
+        } else {
+          st.push_back(static_cast<char>(c));
+          opened = true;
+        }
+      } else if (c == '"') {
+        const unsigned char *s, *t;
+        bool pl;
+        if (!scan_string(&s, &t, &pl)) return false;
+      } else if (c == '-' || (c >= '0' && c <= '9')) {
+        const unsigned char* s;
+        bool ii;
+        if (!number(&s, &ii)) return false;
+      } else if (!(literal("true") || literal("false") || literal("null"))) {
+        return false;
+      }
+      if (opened && st.back() == '{') {  // its first key
+        if (!object_key()) return false;
+        continue;
+      }
+      if (opened) continue;  // an array's first element
+      // after a complete value: close containers, or move to the next member / element
+      for (;;) {
+        if (st.empty()) return true;
+        ws();
+        if (p >= e) return false;
+        const char top = st.back();
+        if (*p == ',') {
+          ++p;
+          if (top == '{' && !object_key()) return false;
+          break;
+        }
+        if (*p == (top == '{' ? '}' : ']')) {
+          ++p;
+          st.pop_back();
+          continue;
+        }
+        return false;
+      }
+    }
+  }
+
+  // a value at p whose first byte is c: scalars inline, containers through skip_value
+  bool skip_scalar_or_value(unsigned c) {
+    if (c == '"') {
+      const unsigned char *s, *t;
+      bool pl;
+      return scan_string(&s, &t, &pl);
+    }
+    if (c == '-' || (c >= '0' && c <= '9')) {
+      const unsigned char* s;
+      bool ii;
+      return number(&s, &ii);
+    }
+    if (c == 't') return lit4("true");
+    if (c == 'n') return lit4("null");
+    if (c == 'f') {
+      if (e - p < 5 || std::memcmp(p, "false", 5) != 0) return false;
+      p += 5;
+      return true;
+    }
+    return skip_value(1);
+  }
+  bool lit4(const char* w) {
+    if (e - p < 4 || std::memcmp(p, w, 4) != 0) return false;
+    p += 4;
+    return true;
+  }
+
+  // "key" ws ':' (the value follows)
+  bool object_key() {
+    ws();
+    if (p >= e || *p != '"') return false;
+    const unsigned char *s, *t;
+    bool pl;
+    if (!scan_string(&s, &t, &pl)) return false;
+    ws();
+    if (p >= e || *p != ':') return false;
+    ++p;
+    return true;
+  }
+
+  // json.Unmarshal(body, &OrderNode{}) for the fields the engine reads.
+  bool decode(Dec& d) {
+    ws();
+    if (p >= e) return false;
+    if (*p != '{') {  // a valid non-object decodes nothing (null: no effect; other: type error)
+      if (!skip_value(0)) return false;
+      ws();
+      return false;
+    }
+    Dec t;
+    ++p;
+    ws();
+    if (p < e && *p == '}') {
+      ++p;
+    } else {
+      for (;;) {
+        ws();
+        if (p >= e || *p != '"') return false;
+        const unsigned char *ks, *kt;
+        bool kpl;
+        if (!scan_string(&ks, &kt, &kpl)) return false;
+        int f;
+        if (kpl) {
+          f = match_field(ks, static_cast<size_t>(kt - ks));
+        } else {
+          key.clear();
+          unquote(ks, kt, key);
+          f = match_field(reinterpret_cast<const unsigned char*>(key.data()), key.size());
+        }
+        ws();
+        if (p >= e || *p != ':') return false;
+        ++p;
+        ws();
+        if (p >= e) return false;
+        const unsigned c = *p;
+        if (f < 0) {
+          if (!skip_scalar_or_value(c)) return false;
+        } else if (c == '"') {
+          Str* sv = f == F_UUID ? &t.s[0] : f == F_OID ? &t.s[1] : f == F_SYMBOL ? &t.s[2] : nullptr;
+          if (!string_value(sv)) return false;  // (into a numeric field: a type error, skipped)
+        } else if (c == '-' || (c >= '0' && c <= '9')) {
+          const unsigned char* ns;
+          bool is_int;
+          if (!number(&ns, &is_int)) return false;
+          if (f == F_PRICE || f == F_VOLUME) {
+            double v;
+            if (parse_float(ns, p, &v)) (f == F_PRICE ? t.price : t.volume) = v;
+          } else if ((f == F_ACTION || f == F_TX) && is_int) {
+            int64_t v;
+            const int64_t lo = f == F_ACTION ? -128 : INT32_MIN, hi = f == F_ACTION ? 127 : INT32_MAX;
+            if (parse_int(ns, p, &v) && v >= lo && v <= hi) {
+              if (f == F_ACTION) t.action = static_cast<int8_t>(v);
+              else t.tx = static_cast<int32_t>(v);
+            }
+          }
+        } else {
+          if (!skip_value(1)) return false;  // null, bool, object, array: no effect / type error
+        }
+        ws();
+        if (p >= e) return false;
+        if (*p == ',') {
+          ++p;
+          continue;
+        }
+        if (*p == '}') {
+          ++p;
+          break;
+        }
+        return false;
+      }
+    }
+    ws();
+    if (p != e) return false;
+    t.is_object = true;
+    d = t;
+    return true;
+  }
+
+  // strconv.ParseInt(s, 10, 64): an error (skipped field) beyond int64
+  static bool parse_int(const unsigned char* s, const unsigned char* t, int64_t* out) {
+    bool neg = false;
+    if (*s == '-') {
+      neg = true;
+      ++s;
+    }
+    uint64_t v = 0;
+    const uint64_t lim = neg ? (1ull << 63) : (1ull << 63) - 1;
+    for (; s < t; ++s) {
+      const uint64_t d = static_cast<uint64_t>(*s - '0');
+      if (v > (lim - d) / 10) return false;
+      v = v * 10 + d;
+    }
+    *out = neg ? static_cast<int64_t>(0 - v) : static_cast<int64_t>(v);
+    return true;
+  }
+
+  // strconv.ParseFloat(s, 64): correctly rounded; out of range (+-Inf) is an error (skipped
+  // field), an underflow gives the rounded value (0 or a subnormal)
+  static bool parse_float(const unsigned char* s, const unsigned char* t, double* out) {
+    const char* a = reinterpret_cast<const char*>(s);
+    const char* b = reinterpret_cast<const char*>(t);
+    auto r = std::from_chars(a, b, *out);
+    if (r.ec == std::errc() && r.ptr == b) return std::isfinite(*out);
+    std::string z(a, b);  // (out of range for from_chars: strtod tells overflow from underflow)
+    const double v = std::strtod(z.c_str(), nullptr);
+    if (!std::isfinite(v)) return false;
+    *out = v;
+    return true;
+  }
+};
+
+uint32_t pick_threads(uint32_t threads, size_t n) {
+  uint32_t t = threads ? threads : std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
+  t = std::min<uint32_t>(t, 64);
+  const size_t per = 1024;  // messages per thread worth a thread
+  return static_cast<uint32_t>(std::max<size_t>(1, std::min<size_t>(t, (n + per - 1) / per)));
+}
+
+// Decode messages [0, n) on `nt` threads: dec[i], arenas[thread].
+void decode_all(const char* buf, const uint64_t* off, size_t n, uint32_t nt, std::vector<Dec>& dec,
+                std::vector<std::string>& arenas) {
+  dec.assign(n, Dec{});
+  arenas.assign(nt, std::string());
+  auto work = [&](uint32_t k) {
+    const size_t i0 = n * k / nt, i1 = n * (k + 1) / nt;
+    std::string& ar = arenas[k];
+    ar.reserve(64 * (i1 - i0));
+    Parser ps{nullptr, nullptr, &ar, static_cast<int32_t>(k), {}};
+    for (size_t i = i0; i < i1; ++i) {
+      ps.p = reinterpret_cast<const unsigned char*>(buf + off[i]);
+      ps.e = reinterpret_cast<const unsigned char*>(buf + off[i + 1]);
+      const size_t mark = ar.size();
+      if (!ps.decode(dec[i])) {
+        dec[i] = Dec{};
+        ar.resize(mark);
+      }
+    }
+  };
+  if (nt == 1) {
+    work(0);
+    return;
+  }
+  std::vector<std::thread> th;
+  th.reserve(nt - 1);
+  for (uint32_t k = 1; k < nt; ++k) th.emplace_back(work, k);
+  work(0);
+  for (auto& t : th) t.join();
+}
+
+inline const char* str_ptr(const Str& s, const std::vector<std::string>& arenas) {
+  return s.arena >= 0 ? arenas[static_cast<size_t>(s.arena)].data() + s.off : s.p;
+}
+
+// ---- interning -----------------------------------------------------------------------------------
+inline uint64_t hash_bytes(const char* s, size_t n) {
+  uint64_t h = 0x9E3779B97F4A7C15ull ^ (n * 0xFF51AFD7ED558CCDull);
+  size_t i = 0;
+  for (; i + 8 <= n; i += 8) {
+    uint64_t w;
+    std::memcpy(&w, s + i, 8);
+    h = (h ^ w) * 0xC4CEB9FE1A85EC53ull;
+    h ^= h >> 29;
+  }
+  uint64_t w = 0;
+  std::memcpy(&w, s + i, n - i);
+  h = (h ^ w) * 0xC4CEB9FE1A85EC53ull;
+  h ^= h >> 32;
+  h *= 0xFF51AFD7ED558CCDull;
+  h ^= h >> 33;
+  return h;
+}
+
+// Open addressing; a slot holds (id + 1, the hash's high 32 bits), so a probe that is not the
+// string reads no string.  Strings live NUL-terminated in 1 MiB blocks that never move.
+struct Interner {
+  std::vector<std::unique_ptr<char[]>> blocks;
+  size_t bused = 0, bcap = 0;
+  std::vector<const char*> strs;
+  std::vector<uint32_t> lens;
+  std::vector<uint64_t> hs;
+  std::vector<uint64_t> slot;  // (id + 1) | tag << 32; 0 = empty
+  uint64_t mask = 0;
+
+  const char* store(const char* s, size_t n) {
+    if (n + 1 > bcap - bused) {
+      const size_t cap = std::max<size_t>(1 << 20, n + 1);
+      blocks.emplace_back(new char[cap]);
+      bused = 0;
+      bcap = cap;
+    }
+    char* d = blocks.back().get() + bused;
+    std::memcpy(d, s, n);
+    d[n] = 0;
+    bused += n + 1;
+    return d;
+  }
+  void grow() {
+    const uint64_t cap = std::max<uint64_t>(1024, (mask + 1) * 2);
+    slot.assign(cap, 0);
+    mask = cap - 1;
+    for (uint32_t id = 0; id < strs.size(); ++id) {
+      uint64_t j = hs[id] & mask;
+      while (slot[j]) j = (j + 1) & mask;
+      slot[j] = (id + 1ull) | (hs[id] >> 32 << 32);
+    }
+  }
+  int64_t find(const char* s, size_t n, uint64_t h) const {
+    if (slot.empty()) return -1;
+    const uint64_t tag = h >> 32 << 32;
+    for (uint64_t j = h & mask;; j = (j + 1) & mask) {
+      const uint64_t v = slot[j];
+      if (!v) return -1;
+      if ((v & ~0xFFFFFFFFull) != tag) continue;
+      const uint32_t id = static_cast<uint32_t>(v) - 1;
+      if (lens[id] == n && std::memcmp(strs[id], s, n) == 0) return id;
+    }
+  }
+  uint32_t intern(const char* s, size_t n) {
+    const uint64_t h = hash_bytes(s, n);
+    const int64_t f = find(s, n, h);
+    if (f >= 0) return static_cast<uint32_t>(f);
+    if ((strs.size() + 1) * 2 > mask + 1) grow();
+    const uint32_t id = static_cast<uint32_t>(strs.size());
+    strs.push_back(store(s, n));
+    lens.push_back(static_cast<uint32_t>(n));
+    hs.push_back(h);
+    uint64_t j = h & mask;
+    while (slot[j]) j = (j + 1) & mask;
+    slot[j] = (id + 1ull) | (h >> 32 << 32);
+    return id;
+  }
+};
+
+}  // namespace
+
+struct gome_names {
+  Interner in[3];
+  int32_t tx_raw[GOME_TX_CODES];
+  uint32_t tx_n = 2;
+  gome_names() {
+    for (int i = 0; i < GOME_TX_CODES; ++i) tx_raw[i] = i;
+  }
+  int32_t tx_code(int32_t raw) {
+    if (raw == 0 || raw == 1) return raw;
+    for (uint32_t c = 2; c < tx_n; ++c)
+      if (tx_raw[c] == raw) return static_cast<int32_t>(c);
+    if (tx_n == GOME_TX_CODES) return -1;
+    tx_raw[tx_n] = raw;
+    return static_cast<int32_t>(tx_n++);
+  }
+};
+
+// The markers: open addressing over (hash, key bytes in an arena); a marker the consumer took
+// provisionally is STAGED until commit (-> a tombstone) or abort (-> live again).
+struct gome_prepool {
+  enum : uint8_t { EMPTY = 0, LIVE = 1, TOMB = 2, STAGED = 3 };
+  struct Ent {
+    uint64_t h;
+    uint64_t off;  // key bytes in arena
+    uint32_t len;
+    uint8_t state;
+  };
+  std::mutex mu;
+  std::vector<Ent> tab;
+  uint64_t mask = 0, live = 0, used = 0;  // used: live + staged + tombstones
+  std::vector<char> arena;
+  std::vector<uint64_t> staged;  // slots
+  std::string kb;                // the consumer's key scratch
+
+  static void key(std::string& k, const char* s, size_t sn, const char* u, size_t un, const char* o, size_t on) {
+    k.clear();
+    const uint32_t a = static_cast<uint32_t>(sn), b = static_cast<uint32_t>(un);
+    k.append(reinterpret_cast<const char*>(&a), 4).append(s, sn);
+    k.append(reinterpret_cast<const char*>(&b), 4).append(u, un);
+    k.append(o, on);
+  }
+  bool same(const Ent& x, uint64_t h, const std::string& k) const {
+    return x.h == h && x.len == k.size() && std::memcmp(arena.data() + x.off, k.data(), k.size()) == 0;
+  }
+  // slot of the key (LIVE or STAGED), or -1
+  int64_t find(const std::string& k, uint64_t h) const {
+    if (tab.empty()) return -1;
+    for (uint64_t j = h & mask;; j = (j + 1) & mask) {
+      const Ent& x = tab[j];
+      if (x.state == EMPTY) return -1;
+      if (x.state != TOMB && same(x, h, k)) return static_cast<int64_t>(j);
+    }
+  }
+  void rebuild(uint64_t cap) {  // (drops tombstones and their key bytes)
+    std::vector<Ent> old;
+    old.swap(tab);
+    std::vector<char> oa;
+    oa.swap(arena);
+    tab.assign(cap, Ent{0, 0, 0, EMPTY});
+    mask = cap - 1;
+    used = 0;
+    for (const Ent& x : old) {
+      if (x.state != LIVE && x.state != STAGED) continue;
+      uint64_t j = x.h & mask;
+      while (tab[j].state != EMPTY) j = (j + 1) & mask;
+      tab[j] = Ent{x.h, arena.size(), x.len, x.state};
+      arena.insert(arena.end(), oa.begin() + static_cast<long>(x.off), oa.begin() + static_cast<long>(x.off + x.len));
+      ++used;
+    }
+    staged.clear();  // (slots moved: re-list the staged ones)
+    for (uint64_t j = 0; j < cap; ++j)
+      if (tab[j].state == STAGED) staged.push_back(j);
+  }
+  void set(const std::string& k) {
+    const uint64_t h = hash_bytes(k.data(), k.size());
+    if (find(k, h) >= 0) return;  // (a staged marker set again stays staged: commit removes it)
+    if ((used + 1) * 2 > mask + 1) rebuild(std::max<uint64_t>(1024, (live + 1) * 4 > mask + 1 ? (mask + 1) * 2 : mask + 1));
+    uint64_t j = h & mask;
+    while (tab[j].state == LIVE || tab[j].state == STAGED) j = (j + 1) & mask;
+    if (tab[j].state == EMPTY) ++used;
+    tab[j] = Ent{h, arena.size(), static_cast<uint32_t>(k.size()), LIVE};
+    arena.insert(arena.end(), k.begin(), k.end());
+    ++live;
+  }
+  bool take(const std::string& k) {
+    const int64_t j = find(k, hash_bytes(k.data(), k.size()));
+    if (j < 0 || tab[static_cast<size_t>(j)].state != LIVE) return false;
+    tab[static_cast<size_t>(j)].state = TOMB;
+    --live;
+    return true;
+  }
+  // the staged ExistsPrePool + DeletePrePool of an ADD (engine.go:58-62), and the staged
+  // DeletePrePool of a DEL (engine.go:90): a LIVE marker becomes STAGED
+  bool stage(const std::string& k) {
+    std::lock_guard<std::mutex> g(mu);
+    const int64_t j = find(k, hash_bytes(k.data(), k.size()));
+    if (j < 0 || tab[static_cast<size_t>(j)].state != LIVE) return false;
+    tab[static_cast<size_t>(j)].state = STAGED;
+    staged.push_back(static_cast<uint64_t>(j));
+    return true;
+  }
+  void commit() {
+    std::lock_guard<std::mutex> g(mu);
+    for (uint64_t j : staged)
+      if (tab[j].state == STAGED) {
+        tab[j].state = TOMB;
+        --live;
+      }
+    staged.clear();
+  }
+  void abort() {
+    std::lock_guard<std::mutex> g(mu);
+    for (uint64_t j : staged)
+      if (tab[j].state == STAGED) tab[j].state = LIVE;
+    staged.clear();
+  }
+};
+
+extern "C" {
+
+gome_names* gome_names_create(void) { return new (std::nothrow) gome_names(); }
+void gome_names_destroy(gome_names* nm) { delete nm; }
+
+int64_t gome_names_intern(gome_names* nm, int kind, const char* s, size_t len) {
+  if (!nm || kind < 0 || kind > 2 || (!s && len) || len > 0xFFFFFFFFu) return -1;
+  return nm->in[kind].intern(s ? s : "", len);
+}
+
+int64_t gome_names_find(const gome_names* nm, int kind, const char* s, size_t len) {
+  if (!nm || kind < 0 || kind > 2 || (!s && len)) return -1;
+  return nm->in[kind].find(s ? s : "", len, hash_bytes(s ? s : "", len));
+}
+
+size_t gome_names_count(const gome_names* nm, int kind) {
+  return (nm && kind >= 0 && kind <= 2) ? nm->in[kind].strs.size() : 0;
+}
+
+const char* gome_names_get(const gome_names* nm, int kind, uint32_t id, size_t* len) {
+  if (!nm || kind < 0 || kind > 2 || id >= nm->in[kind].strs.size()) return nullptr;
+  if (len) *len = nm->in[kind].lens[id];
+  return nm->in[kind].strs[id];
+}
+
+const char* const* gome_names_table(gome_names* nm, int kind) {
+  if (!nm || kind < 0 || kind > 2) return nullptr;
+  static const char* const empty[1] = {""};
+  return nm->in[kind].strs.empty() ? empty : nm->in[kind].strs.data();
+}
+
+int32_t gome_names_tx_code(gome_names* nm, int32_t raw) { return nm ? nm->tx_code(raw) : -1; }
+const int32_t* gome_names_tx_table(const gome_names* nm) { return nm ? nm->tx_raw : nullptr; }
+size_t gome_names_tx_count(const gome_names* nm) { return nm ? nm->tx_n : 0; }
+
+gome_prepool* gome_prepool_create(void) { return new (std::nothrow) gome_prepool(); }
+void gome_prepool_destroy(gome_prepool* pp) { delete pp; }
+
+void gome_prepool_set(gome_prepool* pp, const char* sym, size_t sym_len, const char* uuid, size_t uuid_len,
+                      const char* oid, size_t oid_len) {
+  if (!pp || (!sym && sym_len) || (!uuid && uuid_len) || (!oid && oid_len)) return;
+  std::string k;
+  gome_prepool::key(k, sym, sym_len, uuid, uuid_len, oid, oid_len);
+  std::lock_guard<std::mutex> g(pp->mu);
+  pp->set(k);
+}
+
+int32_t gome_prepool_take(gome_prepool* pp, const char* sym, size_t sym_len, const char* uuid, size_t uuid_len,
+                          const char* oid, size_t oid_len) {
+  if (!pp || (!sym && sym_len) || (!uuid && uuid_len) || (!oid && oid_len)) return 0;
+  std::string k;
+  gome_prepool::key(k, sym, sym_len, uuid, uuid_len, oid, oid_len);
+  std::lock_guard<std::mutex> g(pp->mu);
+  return pp->take(k) ? 1 : 0;
+}
+
+size_t gome_prepool_size(const gome_prepool* pp) {
+  if (!pp) return 0;
+  std::lock_guard<std::mutex> g(const_cast<gome_prepool*>(pp)->mu);
+  return pp->live;
+}
+
+void gome_prepool_commit(gome_prepool* pp) {
+  if (pp) pp->commit();
+}
+
+void gome_prepool_abort(gome_prepool* pp) {
+  if (pp) pp->abort();
+}
+
+int64_t gome_decode_order_nodes(const char* buf, const uint64_t* off, size_t n, uint32_t threads,
+                                gome_decoded_node* out, char* strbuf, size_t strcap) {
+  if ((n && (!buf || !off || !out)) || (!strbuf && strcap)) return INT64_MIN;
+  std::vector<Dec> dec;
+  std::vector<std::string> arenas;
+  decode_all(buf, off, n, pick_threads(threads, n), dec, arenas);
+  size_t used = 0;
+  for (size_t i = 0; i < n; ++i)
+    for (const Str& s : dec[i].s) used += s.len;
+  if (used > strcap) return -static_cast<int64_t>(used);
+  size_t at = 0;
+  for (size_t i = 0; i < n; ++i) {
+    const Dec& d = dec[i];
+    gome_decoded_node& o = out[i];
+    o = gome_decoded_node{};
+    o.price = d.price;
+    o.volume = d.volume;
+    o.transaction = d.tx;
+    o.action = d.action;
+    o.is_object = d.is_object ? 1 : 0;
+    uint32_t* fo[3][2] = {{&o.uuid_off, &o.uuid_len}, {&o.oid_off, &o.oid_len}, {&o.sym_off, &o.sym_len}};
+    for (int k = 0; k < 3; ++k) {
+      const Str& s = d.s[k];
+      if (s.len) std::memcpy(strbuf + at, str_ptr(s, arenas), s.len);
+      *fo[k][0] = static_cast<uint32_t>(at);
+      *fo[k][1] = s.len;
+      at += s.len;
+    }
+  }
+  return static_cast<int64_t>(used);
+}
+
+gome_status gome_consume_order_nodes(gome_names* nm, gome_prepool* pp, const char* buf, const uint64_t* off, size_t n,
+                                     uint32_t max_symbols, uint32_t threads, gome_order* out, uint32_t* msg_index,
+                                     size_t* n_out, gome_consume_stats* st) {
+  if (!nm || !pp || !n_out || (n && (!buf || !off || !out))) return GOME_E_INVAL;
+  std::vector<Dec> dec;
+  std::vector<std::string> arenas;
+  decode_all(buf, off, n, pick_threads(threads, n), dec, arenas);
+  gome_consume_stats s{};
+  s.messages = n;
+  size_t k = 0;
+  for (size_t i = 0; i < n; ++i) {
+    const Dec& d = dec[i];
+    s.not_objects += d.is_object ? 0 : 1;
+    const int act = d.action;
+    if (act != GOME_ADD && act != GOME_DEL) {  // DoOrder ignores it (engine.go:46-54): a zero record
+      out[k] = gome_order{};
+      if (msg_index) msg_index[k] = static_cast<uint32_t>(i);
+      ++k;
+      ++s.ignored;
+      continue;
+    }
+    const char* sym = str_ptr(d.s[2], arenas);
+    const char* uuid = str_ptr(d.s[0], arenas);
+    const char* oid = str_ptr(d.s[1], arenas);
+    const size_t sl = d.s[2].len, ul = d.s[0].len, ol = d.s[1].len;
+    int64_t p = 0, v = 0;
+    bool bad = gome_fixed_from_scaled(d.price, &p) != GOME_OK || gome_fixed_from_scaled(d.volume, &v) != GOME_OK || v < 0;
+    if (!bad && max_symbols) {
+      const int64_t sid = nm->in[0].find(sym ? sym : "", sl, hash_bytes(sym ? sym : "", sl));
+      const uint64_t would = sid >= 0 ? static_cast<uint64_t>(sid) : nm->in[0].strs.size();
+      bad = would >= max_symbols;
+    }
+    int32_t code = 0;
+    if (!bad) {
+      code = nm->tx_code(d.tx);
+      bad = code < 0;
+    }
+    std::string& key = pp->kb;
+    gome_prepool::key(key, sym ? sym : "", sl, uuid ? uuid : "", ul, oid ? oid : "", ol);
+    if (bad) {  // outside the engine's domain: not submitted (its marker is consumed as DoOrder would)
+      ++s.rejected;
+      pp->stage(key);
+      continue;
+    }
+    gome_order& r = out[k];
+    r.price_fx = p;
+    r.volume_fx = v;
+    r.symbol_id = nm->in[0].intern(sym ? sym : "", sl);
+    r.uuid_id = nm->in[1].intern(uuid ? uuid : "", ul);
+    r.oid_id = nm->in[2].intern(oid ? oid : "", ol);
+    r.side = static_cast<uint8_t>(code);
+    r.action = static_cast<uint8_t>(act);
+    if (act == GOME_ADD) {
+      const bool ok = pp->stage(key);
+      s.admitted += ok ? 1 : 0;
+      r.flags = static_cast<uint16_t>(GOME_ORD_ADM_HOST | (ok ? GOME_ORD_ADMITTED : 0));
+    } else {
+      pp->stage(key);
+      r.flags = GOME_ORD_ADM_HOST;
+    }
+    if (msg_index) msg_index[k] = static_cast<uint32_t>(i);
+    ++k;
+  }
+  s.records = k;
+  *n_out = k;
+  if (st) *st = s;
+  return GOME_OK;
+}
+
+}  // extern "C"

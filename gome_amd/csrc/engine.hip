@@ -248,7 +248,6 @@ struct Slot {
   uint32_t* seg_order = nullptr;
   uint32_t* bcnt = nullptr;       // 32 counts + 32 offsets
   Status* sst = nullptr;          // the segmentation's nseg / nhot / C_MAXSEG, copied to Status by k_sort_status
-  hipEvent_t sorted{};
 };
 
 struct Flight {
@@ -265,15 +264,14 @@ struct gome_engine {
   hipStream_t hot_stream = nullptr;   // tail / near-head flow books, legacy hot kernel
   hipStream_t flow_stream = nullptr;  // the hottest book's plan (critical path)
   hipStream_t copy_stream = nullptr;  // H2D of records, D2H of events (pipelined path)
-  hipStream_t cold_stream = nullptr;  // the cold books on a stream of their own (GOME_COLD_OWN=1; A/B)
   hipStream_t early_stream = nullptr; // the early plan's record work (match_early.h), beside the plan before it
   // The hottest book's plans on a stream of their own restricted to CUs [0, k), every other engine
   // stream to the rest: the plan wave alone with its CU's instruction cache and L1, and no other
-  // kernel's code or data beside it (GOME_PLAN_CUS=k, default 8; 0: no reserved CUs)
+  // kernel's code or data beside it (gome_config.plan_cus, default 8; none below 8 queues)
   hipStream_t plan_stream = nullptr;
   hipEvent_t pl_fork{}, pl_join{};
   uint32_t plan_cus = 0;
-  bool plan_prep = true;  // the early plan's prep after plan_done on the plan's stream (GOME_PLAN_PREP=0: A/B)
+  uint32_t hw_queues = 4;  // the process's hardware queues (gome_config.hw_queues; layout)
   std::vector<uint32_t> cu_rest;  // every CU but the plan's
   hipError_t new_stream(hipStream_t* st) {
     return plan_cus ? hipExtStreamCreateWithCUMask(st, static_cast<uint32_t>(cu_rest.size()), cu_rest.data())
@@ -324,10 +322,6 @@ struct gome_engine {
     const hipError_t he = set_masked(!(last_maxseg * 16 < last_n));
     return he == hipSuccess ? GOME_OK : fail(GOME_E_DEVICE, hipGetErrorString(he));
   }
-  // D2H of collected events on a stream of their own (GOME_D2H_STREAM=1; off by default: with
-  // four hardware queues per process a fifth stream shares one, and the e2e A/B measured it
-  // 0.7 ms per config-2 batch slower with three batches in flight, no faster with two)
-  hipStream_t d2h_stream = nullptr;
   hipEvent_t fork{}, join{}, joinf{}, prep_h{}, prep_t{}, fork_adm{}, adm_done{}, seg_done{};
   hipEvent_t dp_fork{}, cnt_fork{}, cnt_done{}, dw_done{}, dl_done{}, tl_done{};  // the hottest book's deep chain, k_flow_count beside its writes
   // the early plan of the hottest book (match_early.h): the last batch's plan done (flow stream),
@@ -347,16 +341,13 @@ struct gome_engine {
   FlPrepScr* x_dscr = nullptr;                 // deep books: prep scratch, price set, sorted prices
   unsigned long long *x_dkey = nullptr, *x_dnew = nullptr;
   uint32_t *x_dval = nullptr, *x_dslot = nullptr;
-  bool early_on = true;            // GOME_EARLY=0: never
+  bool early_on = true;            // (GOME_FLAG_NO_EARLY: never)
   // pipelined device batches of a dominated stream that plan late: admission ahead, on the early
-  // stream beside the last batch's plan (k_adm_verify; GOME_ADM_AHEAD=0: never)
+  // stream beside the last batch's plan (k_adm_verify; GOME_FLAG_NO_ADM_AHEAD: never)
   bool adm_ahead_on = true;
   hipEvent_t adm_pre_done{};
   Status* d_adm_st = nullptr;      // the ahead pass's input errors
   uint32_t* d_adm_redo = nullptr;  // k_adm_verify: the batch's own admission runs again
-  // a batch with an early plan runs its cold books on the early stream, after the next batch's early
-  // record work (A/B on one box: config 3 +0.3..0.7%, config 5 even; GOME_COLD_EARLY=0: the caller's)
-  bool cold_early = true;
   uint32_t head_add = 0;           // bit 0 / 1: the last / the one before finished batch's hottest book took an ADD plan
   uint32_t bid = 0;                // batches enqueued (FlowArgs::bid)
   Slot slots[GOME_MAX_INFLIGHT];
@@ -370,27 +361,18 @@ struct gome_engine {
   Status* d_st = nullptr;
   // capacities
   uint32_t max_batch = 0, key_bits = 1, passes = 1, dbits = 1;
-  uint32_t tail_grid = 4096;  // blocks of the tail's per-touch kernels (GOME_TAIL_GRID; 4096 measured 5% faster than 1024 on config 2)
-  // the tail's writes (caller's stream) and events (hot stream, after the near books and the
-  // legacy kernels) as two kernels side by side, when the last batch had no dominant book: 0.07 ms
-  // faster on config 2, but the split events kernel's traffic slows a concurrent hottest-book
-  // plan (config 3: +0.2 ms), so with a hot book the fused launch (GOME_TAIL_SPLIT=0/1 forces)
-  int tail_split = -1;
-  bool tail_serial = false;  // the split tail's events after its writes on one stream (GOME_TAIL_SERIAL: solo kernel times)
-  int prep_wait = -1;  // k_prep after the head's prep always (1) / adaptive (-1; GOME_PREP_WAIT, A/B)
-  bool adm_fast = true;
-  bool cold_main = false;  // k_match on the caller's stream (GOME_COLD_MAIN=1; default: the copy stream)
+  // blocks of the tail's per-touch kernels (4096 measured 5% faster than 1024 on config 2)
+  static constexpr uint32_t tail_grid = 4096;
+  bool cold_main = false;  // k_match on the caller's stream (fewer than 8 hardware queues; default: the copy stream)
   bool copy_busy = false;  // the batch being enqueued came by gome_submit_batch_async (H2D / D2H on the copy stream)
   // GOME_PH_* timing events (gome_stats.ms_phase): ~24 event records per batch, 0.12 ms on config 2's
-  // critical path, so only on request (GOME_FLAG_PHASES, or GOME_PHASES=1)
-  bool phases = false;  // k_adm_pre's fresh-batch test (GOME_ADM_FAST=0: every batch through the tables; A/B)
+  // critical path, so only on request (GOME_FLAG_PHASES)
+  bool phases = false;
   uint64_t last_maxseg = 0, last_n = 0;  // the last finished batch's hottest book / size
   uint32_t hist_cap = 0, bsum_cap = 0;
   unsigned long long idx_cap = 0;
   // batch buffers (the sort's and the segments' are per slot: Slot)
   uint32_t* d_bsum = nullptr;
-  bool crank_big = true;   // the head's deep cancel ranks: busy levels a block each (GOME_CRANK_BIG=0: A/B)
-  bool sort_ahead = false;  // pipelined device batches sort on the copy stream during the last one's plan (GOME_SORT_AHEAD=1; DESIGN 4.5: off, measured mixed)
   unsigned long long* d_adm = nullptr;  // admission table (k_adm)
   unsigned long long* d_dup = nullptr;  // (S, uuid, oid) table of the records whose (S, oid) repeats
   uint8_t* d_multi = nullptr;           // per (S, oid) slot: the key repeats in the batch
@@ -464,7 +446,7 @@ struct gome_engine {
       if (S.h_st) (void)hipHostFree(S.h_st);
       if (S.h_events) (void)hipHostFree(S.h_events);
       for (hipEvent_t ev : {S.ev0, S.ev1, S.evm0, S.evm1, S.evh0, S.evh1, S.evf0, S.evf1, S.evc0, S.evc1, S.h2d, S.done,
-                            S.sorted, S.evx0, S.evx1})
+                            S.evx0, S.evx1})
         if (ev) (void)hipEventDestroy(ev);
       for (auto& pr : S.ph)
         for (hipEvent_t ev : pr)
@@ -486,9 +468,7 @@ struct gome_engine {
     if (pl_join) (void)hipEventDestroy(pl_join);
     if (flow_stream) (void)hipStreamDestroy(flow_stream);
     if (copy_stream) (void)hipStreamDestroy(copy_stream);
-    if (cold_stream) (void)hipStreamDestroy(cold_stream);
     if (early_stream) (void)hipStreamDestroy(early_stream);
-    if (d2h_stream) (void)hipStreamDestroy(d2h_stream);
     if (stream) (void)hipStreamDestroy(stream);
   }
 
@@ -536,8 +516,22 @@ struct gome_engine {
       return fail(GOME_E_DEVICE, std::string(#x) + ": " + hipGetErrorString(_e));    \
   } while (0)
 
+// GPU_MAX_HW_QUEUES as set now (HIP's default 4 if unset or not a number): the layout's fallback
+// when the host does not say how many queues its runtime started with (gome_config.hw_queues)
+static uint32_t env_hw_queues() {
+  const char* q = std::getenv("GPU_MAX_HW_QUEUES");
+  if (!q || !*q) return 4;
+  char* end = nullptr;
+  const long v = std::strtol(q, &end, 10);
+  return (end && *end == 0 && v > 0 && v < 1024) ? static_cast<uint32_t>(v) : 4u;
+}
+
 gome_status gome_engine::init(const gome_config& c) {
   cfg = c;
+  if (cfg.abi_version != GOME_ABI_VERSION)
+    return fail(GOME_E_INVAL, "gome_config.abi_version is " + std::to_string(cfg.abi_version) +
+                                  ", this library is ABI " + std::to_string(GOME_ABI_VERSION) +
+                                  " (rebuild the caller against include/gome/gome_abi.h)");
   if (cfg.accuracy == 0) cfg.accuracy = 8;
   if (!cfg.max_symbols || !cfg.max_batch || !cfg.max_nodes || !cfg.max_levels)
     return fail(GOME_E_INVAL, "gome_config: max_symbols, max_batch, max_nodes, max_levels must be > 0");
@@ -549,13 +543,18 @@ gome_status gome_engine::init(const gome_config& c) {
     return fail(GOME_E_DEVICE, "no HIP device available (the engine has no CPU fallback)");
   if (cfg.device < 0 || cfg.device >= ndev) return fail(GOME_E_INVAL, "gome_config.device out of range");
   HIPCHK(hipSetDevice(cfg.device));
+  // ---- stream layout: with fewer than 8 hardware queues the engine's streams would
+  // share them (the copy stream with the hottest plan's: +6 ms per config-3 batch), so the cold books
+  // stay on the caller's stream and there is no early plan, no admission ahead and no plan stream
+  hw_queues = cfg.hw_queues ? cfg.hw_queues : env_hw_queues();
+  cold_main = hw_queues < 8;
+  early_on = !cold_main && !(cfg.flags & GOME_FLAG_NO_EARLY);
+  adm_ahead_on = !cold_main && !(cfg.flags & GOME_FLAG_NO_ADM_AHEAD);
   {
     int ncu = 0;
     HIPCHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, cfg.device));
-    const char* g = std::getenv("GOME_PLAN_CUS");
-    plan_cus = g ? static_cast<uint32_t>(std::max(0, std::atoi(g))) : 8u;
+    plan_cus = cfg.plan_cus < 0 ? 0u : cfg.plan_cus > 0 ? static_cast<uint32_t>(cfg.plan_cus) : cold_main ? 0u : 8u;
     if (plan_cus >= static_cast<uint32_t>(ncu)) plan_cus = 0;
-    if (const char* pp = std::getenv("GOME_PLAN_PREP")) plan_prep = std::atoi(pp) != 0;
     const uint32_t words = (static_cast<uint32_t>(ncu) + 31) / 32;
     cu_rest.assign(words, 0u);
     std::vector<uint32_t> cu_plan(words, 0u);
@@ -570,8 +569,6 @@ gome_status gome_engine::init(const gome_config& c) {
   HIPCHK(new_stream(&hot_stream));
   HIPCHK(new_stream(&flow_stream));
   HIPCHK(new_stream(&copy_stream));
-  if (const char* g = std::getenv("GOME_D2H_STREAM"); g && std::atoi(g) != 0)
-    HIPCHK(new_stream(&d2h_stream));
   for (hipEvent_t* ev : {&fork, &join, &joinf, &prep_h, &prep_t, &fork_adm, &adm_done, &seg_done,
                          &dp_fork, &cnt_fork, &cnt_done, &dw_done, &dl_done, &tl_done, &tob_done, &plan_done,
                          &oidmax_done, &xpre_done, &xprep_done, &xplan_done, &adm_pre_done})
@@ -584,7 +581,6 @@ gome_status gome_engine::init(const gome_config& c) {
       for (hipEvent_t& ev : pr) HIPCHK(hipEventCreate(&ev));
     HIPCHK(hipEventCreateWithFlags(&S.h2d, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&S.done, hipEventDisableTiming));
-    HIPCHK(hipEventCreateWithFlags(&S.sorted, hipEventDisableTiming));
     HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&S.h_st), sizeof(Status), hipHostMallocDefault));
   }
   HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_match_hot),
@@ -609,27 +605,7 @@ gome_status gome_engine::init(const gome_config& c) {
   }
 
   max_batch = cfg.max_batch;
-  if (const char* g = std::getenv("GOME_TAIL_GRID")) tail_grid = std::max(64, std::atoi(g));  // (tuning)
-  if (const char* g = std::getenv("GOME_TAIL_SPLIT")) tail_split = std::atoi(g) != 0 ? 1 : 0;  // (A/B)
-  if (const char* g = std::getenv("GOME_TAIL_SERIAL")) tail_serial = std::atoi(g) != 0;         // (profiling)
-  if (const char* g = std::getenv("GOME_PREP_WAIT")) prep_wait = std::atoi(g) != 0 ? 1 : 0;       // (A/B)
-  if (const char* g = std::getenv("GOME_SORT_AHEAD")) sort_ahead = std::atoi(g) != 0;           // (A/B)
-  if (const char* g = std::getenv("GOME_CRANK_BIG")) crank_big = std::atoi(g) != 0;             // (A/B)
-  if (const char* g = std::getenv("GOME_ADM_FAST")) adm_fast = std::atoi(g) != 0;              // (A/B)
-  // the cold books go beside the tail's chain only when HIP can give the copy stream a hardware
-  // queue of its own (with 4 it shares the hottest plan's, which serialised them: +6 ms per
-  // config-3 batch); gome_amd/__init__.py asks for 8
-  {
-    const char* q = std::getenv("GPU_MAX_HW_QUEUES");
-    cold_main = !q || std::atoi(q) < 8;
-    early_on = !cold_main;  // (the early plan's stream needs a queue of its own too)
-    adm_ahead_on = !cold_main;
-  }
-  if (const char* g = std::getenv("GOME_COLD_MAIN")) cold_main = std::atoi(g) != 0;            // (A/B)
-  if (const char* g = std::getenv("GOME_COLD_OWN"); g && std::atoi(g) != 0)                   // (A/B)
-    HIPCHK(new_stream(&cold_stream));
   phases = (cfg.flags & GOME_FLAG_PHASES) != 0;
-  if (const char* g = std::getenv("GOME_PHASES")) phases = std::atoi(g) != 0;
   uint32_t ms = cfg.max_symbols;
   key_bits = (ms <= 1) ? 1 : 32 - __builtin_clz(ms - 1);
   passes = (key_bits + RS_MAXBITS - 1) / RS_MAXBITS;
@@ -747,10 +723,7 @@ gome_status gome_engine::init(const gome_config& c) {
     return GOME_E_CAPACITY;
   for (XBuf& X : xb) HIPCHK(hipMemsetAsync(X.ctl, 0, sizeof(XCtl), stream));
   HIPCHK(hipMemsetAsync(x_dslot, 0, 4, stream));  // (the early deep book is deep slot 0's)
-  if (const char* g = std::getenv("GOME_EARLY")) early_on = std::atoi(g) != 0;
-  if (const char* g = std::getenv("GOME_ADM_AHEAD")) adm_ahead_on = std::atoi(g) != 0;
   if (early_on || adm_ahead_on) HIPCHK(new_stream(&early_stream));
-  if (const char* g = std::getenv("GOME_COLD_EARLY")) cold_early = std::atoi(g) != 0;
   // books with DELs (match_flow_cancel.h): per-position scratch, the (symbol, oid)
   // table (generation-tagged: cleared once per 2048 batches)
   fc_hcap = next_pow2(std::max<unsigned long long>(2ull * nb, 1024));
@@ -851,16 +824,11 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
     S.ph_on[ph] = true;
     return hipEventRecord(S.ph[ph][end], st);
   };
-  // ---- stable radix sort of (symbol_id, seq) and the segments, into the slot's buffers.  They
-  // read only the records, so a pipelined batch (ahead: its records are complete on the copy
-  // stream, H2D included) sorts there as soon as the batch before it has started its hottest
-  // book's plan (that batch's head prep done: prep_h, recorded by its enqueue), beside that
-  // plan; the caller's stream picks the results up with one small status copy.
-  // (only when one book dominates the batch: with none, the caller's stream carries the batch's
-  // critical path from start to end and the early sort only competes with the batch before;
-  // A/B: config 3 -0.1..0.2 ms, config 2 +0.02 ms)
+  // ---- stable radix sort of (symbol_id, seq) and the segments, into the slot's buffers, on the
+  // caller's stream.  (Sorting a pipelined batch on the copy stream during the last batch's plan was
+  // measured in round 3 and dropped: its record reads slowed the concurrent plan)
   const bool dominant = !(last_maxseg * 16 < last_n);
-  hipStream_t ss = (ahead && sort_ahead && dominant) ? copy_stream : s;
+  hipStream_t ss = s;
   // the hottest book planned early on the copy stream (match_early.h): pipelined device batches
   // after a batch whose hottest book took an ADD plan (the device checks the rest)
   const bool early = early_on && (ahead || copy_busy) && dominant && head_add != 0 && bid > 0 && F.enabled;
@@ -874,8 +842,7 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
     hipError_t he = hipMemsetAsync(d_st, 0, offsetof(Status, free_top), s);
     return he == hipSuccess ? hipEventRecord(fork_adm, s) : he;
   };
-  if (ss == s) HIPCHK(status_reset());
-  else HIPCHK(hipStreamWaitEvent(ss, prep_h, 0));
+  HIPCHK(status_reset());
   const uint32_t T256 = 256, gN = ceil_div(n, T256);
   HIPCHK(mark(GOME_PH_SORT, 0, ss));
   HIPCHK(hipMemsetAsync(S.sst, 0, sizeof(Status), ss));
@@ -909,11 +876,6 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   k_seg_bscan<<<1, 64, 0, ss>>>(S.bcnt, S.bcnt + 32, S.sst, FLOW_MIN_LOG2, MAX_FLOW);
   k_seg_scatter<<<gN, T256, 0, ss>>>(S.seg_start, S.sst, S.bcnt + 32, S.seg_order);
   HIPCHK(mark(GOME_PH_SORT, 1, ss));
-  if (ss != s) {
-    HIPCHK(hipEventRecord(S.sorted, ss));
-    HIPCHK(status_reset());
-    HIPCHK(hipStreamWaitEvent(s, S.sorted, 0));
-  }
   k_sort_status<<<1, 1, 0, s>>>(d_st, S.sst);
 
   // ---- the early plan of the hottest book (match_early.h), on the copy stream: its records and
@@ -932,7 +894,7 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
     // plan on the early stream, so the copy stream stays free for the copies)
     // (GOME_PLAN_CUS: the part after plan_done on the plan's own stream, which then needs no hop)
     hipStream_t es = copy_busy ? copy_stream : early_stream;
-    hipStream_t ps = (plan_stream && plan_prep) ? plan_stream : copy_busy ? early_stream : copy_stream;
+    hipStream_t ps = plan_stream ? plan_stream : copy_busy ? early_stream : copy_stream;
     Dev Dx = D;
     Dx.st = reinterpret_cast<Status*>(reinterpret_cast<char*>(X.ctl) + offsetof(XCtl, st));
     BatchArgs Bx{};
@@ -962,10 +924,6 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
     k_deep_prep_c<<<dim3(FL_PG, 1), FL_PREP_T, 0, ps>>>(Dx, Bx, FX);
     HIPCHK(hipEventRecord(xprep_done, ps));
     hipStream_t pst = ps;
-    if (plan_stream && !plan_prep) {  // (GOME_PLAN_PREP=0: the prep on the copy stream, a hop to the plan's)
-      HIPCHK(hipStreamWaitEvent(plan_stream, xprep_done, 0));
-      pst = plan_stream;
-    }
     HIPCHK(hipEventRecord(S.evx0, pst));
     k_flow_plan_early<<<1, 256, plan_lds, pst>>>(Dx, FX);
     HIPCHK(hipEventRecord(S.evx1, pst));
@@ -993,14 +951,14 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
     HIPCHK(hipStreamWaitEvent(early_stream, prep_h, 0));    // (after the last batch's head prep: its plan runs)
     HIPCHK(hipMemsetAsync(d_adm_st, 0, offsetof(Status, free_top), early_stream));
     HIPCHK(hipMemsetAsync(d_adm_redo, 0, 4, early_stream));
-    k_adm_ctl<<<1, 1, 0, early_stream>>>(d_adm_ctl, adm_fast ? 1u : 0u);
+    k_adm_ctl<<<1, 1, 0, early_stream>>>(d_adm_ctl, 1u);
     k_adm_pre<<<std::min<uint32_t>(gN, 1024), T256, 0, early_stream>>>(d_ord, n, d_adm_ctl);
     admission(early_stream, d_adm_st, true, nullptr);
     HIPCHK(hipEventRecord(adm_pre_done, early_stream));
   }
   HIPCHK(hipStreamWaitEvent(flow_stream, fork_adm, 0));
   if (!adm_ahead) {
-    k_adm_ctl<<<1, 1, 0, flow_stream>>>(d_adm_ctl, adm_fast ? 1u : 0u);
+    k_adm_ctl<<<1, 1, 0, flow_stream>>>(d_adm_ctl, 1u);
     k_adm_pre<<<std::min<uint32_t>(gN, 1024), T256, 0, flow_stream>>>(d_ord, n, d_adm_ctl);
   }
   if ((++fc_gen & FC_GEN_MASK) == 0) HIPCHK(hipMemsetAsync(F.fc_hash, 0, sizeof(FcHash) * fc_hcap, flow_stream));
@@ -1044,7 +1002,11 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   const bool c_deep = (ch & FL_CH_DEEP) != 0, c_canc = (ch & FL_CH_CANCEL) != 0;
   S.chains = ch;
   F.chains = ch;
-  const bool split_tail = tail_split >= 0 ? tail_split != 0 : last_maxseg * 16 < last_n;
+  // the tail's writes (caller's stream) and events (hot stream, after the near books and the legacy
+  // kernels) as two kernels side by side when the last batch had no dominant book: 0.07 ms faster on
+  // config 2, but the split events kernel's traffic slows a concurrent hottest-book plan (config 3:
+  // +0.2 ms), so with a hot book one fused launch
+  const bool split_tail = !dominant;
   FlowArgs FH = F, FH0 = F, FH1 = F, FT = F;
   FH.h0 = 0; FH.h1 = FL_HEAD; FH.tb = 0;
   FH0.h0 = 0; FH0.h1 = 1; FH0.tb = 0; FH0.mb = 0;
@@ -1113,7 +1075,7 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
       k_fd_oldwalk<<<dim3(DEEP_GRID, ns), 64, 0, st>>>(D, R);
       k_fd_ckeys<<<dim3(wide ? 256 : 16, ns), 256, 0, st>>>(D, B, R);
       deep_sort(R, wide ? FL_SORT_GRID : 32, st);
-      const bool big = wide && crank_big;  // (the head's busiest levels a block each)
+      const bool big = wide;  // (the head's busiest levels a block each)
       k_fd_crank<<<dim3(DEEP_GRID, ns), 64, 0, st>>>(D, B, R, big ? 1u : 0u);
       if (big) k_fd_crank_big<<<dim3(16, ns), FC_LVB_T, 0, st>>>(D, B, R);
       k_fd_tbase<<<ns, DEEP_CLAIM_T, 0, st>>>(D, R);
@@ -1175,7 +1137,7 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   // path) have the memory system first; the cold books have slack
   // (only when one book dominates the batch, the split_tail test: A/B r3j, without the wait
   // config 2 -0.14 ms, config 3 +0.2 ms; with no dominant book the tail's chain is the critical path)
-  if (!split_tail || prep_wait > 0) HIPCHK(hipStreamWaitEvent(s, prep_h, 0));
+  if (!split_tail) HIPCHK(hipStreamWaitEvent(s, prep_h, 0));
 
   // ---- match_books: one wavefront per book; hot books (LDS) on a second stream,
   //      concurrently with the cold books (HBM)
@@ -1272,12 +1234,11 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   // step 200), which put the tail's plans and reconstruction behind it on the critical path.  On the
   // copy stream, idle during device and synchronous batches.  Pipelined host batches keep the
   // caller's stream: there the copy stream carries the next batch's H2D, which waited for the cold
-  // kernel (config-2 e2e 5.24 -> 6.9 ms per batch).  A stream of its own (GOME_COLD_OWN=1) measured
-  // slower at 4, 8 and 16 hardware queues (config 2: 2.3 -> 3.6 ms per batch).  A batch
-  // with an early plan keeps the copy stream for it and runs the cold books on the early stream
-  // (cold_early).  GOME_COLD_MAIN=1: the caller's stream always
-  hipStream_t cst = (early && cold_early && !copy_busy) ? early_stream
-                    : (cold_main || copy_busy || early) ? s : cold_stream ? cold_stream : copy_stream;
+  // kernel (config-2 e2e 5.24 -> 6.9 ms per batch).  A stream of its own measured slower at 4, 8
+  // and 16 hardware queues (config 2: 2.3 -> 3.6 ms per batch).  A batch with an early
+  // plan keeps the copy stream for it and runs the cold books on the early stream (A/B: config 3
+  // +0.3..0.7%, config 5 even).  Fewer than 8 hardware queues (cold_main): the caller's stream
+  hipStream_t cst = (early && !copy_busy) ? early_stream : (cold_main || copy_busy || early) ? s : copy_stream;
   if (cst != s) HIPCHK(hipStreamWaitEvent(cst, prep_t, 0));
   HIPCHK(hipEventRecord(S.evc0, cst));
   k_match<<<std::min<uint32_t>(ceil_div(grid, COLD_WAVES), COLD_BLOCKS), 64 * COLD_WAVES, COLD_LDS_BYTES, cst>>>(
@@ -1306,7 +1267,6 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
     if (split_tail) {
       HIPCHK(hipEventRecord(tl_done, s));  // (the events run on the hot stream, below)
       k_flow_write<<<nh_tail, FL_WRITE_T, 0, s>>>(D, B, FT);
-      if (tail_serial) k_flow_events_fused_w<<<ceil_div(tail_grid * FL_EV_T, FL_WRITE_T), FL_WRITE_T, 0, s>>>(D, B, FT);
     } else {
       k_flow_write_events<<<nh_tail + ceil_div(tail_grid * FL_EV_T, FL_WRITE_T), FL_WRITE_T, 0, s>>>(D, B, FT, nh_tail);
     }
@@ -1341,7 +1301,7 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   // oid watermarks for the next batches' duplicate-oid probe (the hot stream has slack here)
   k_oid_max<<<gN, T256, 0, hot_stream>>>(n, skeys, d_prep, d_oid_max);
   HIPCHK(hipEventRecord(oidmax_done, hot_stream));
-  if (nh_tail && split_tail && !tail_serial) {  // the tail's events beside its writes (arena; k_publish places them)
+  if (nh_tail && split_tail) {  // the tail's events beside its writes (arena; k_publish places them)
     HIPCHK(hipStreamWaitEvent(hot_stream, tl_done, 0));
     k_flow_events_fused_w<<<ceil_div(tail_grid * FL_EV_T, FL_WRITE_T), FL_WRITE_T, 0, hot_stream>>>(D, B, FT);
   }
@@ -1562,7 +1522,7 @@ gome_status gome_engine::collect(const gome_event** evs, size_t* nev) {
     S.h_cap = cap;
   }
   if (n) {
-    hipStream_t cs = d2h_stream ? d2h_stream : copy_stream;
+    hipStream_t cs = copy_stream;
     HIPCHK(hipMemcpyAsync(S.h_events, S.d_events, n * sizeof(gome_event), hipMemcpyDeviceToHost, cs));
     HIPCHK(hipStreamSynchronize(cs));
   }

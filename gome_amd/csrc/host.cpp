@@ -2,14 +2,18 @@
 //   * exact fixed-point conversion (ordernode.go:76-87 via shopspring/decimal v1.2.0)
 //   * MatchResult JSON rendering byte-identical to Go encoding/json of
 //     engine.MatchResult (engine.go:24-28) / engine.OrderNode (ordernode.go:9-36)
+#include <algorithm>
 #include <charconv>
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <thread>
+#include <vector>
 
 #include "../../include/gome/gome_abi.h"
+#include "../../include/gome/gome_host.h"
 
 namespace {
 
@@ -67,12 +71,19 @@ struct Out {
   void putc(char c) { put(&c, 1); }
 };
 
-// encoding/json string encoder with HTML escaping (the default for json.Marshal).
-void json_string(Out& o, const char* s) {
+// encoding/json string encoder with HTML escaping (the default for json.Marshal), without the
+// quotes: the key strings are concatenations (S + ":node:" + oid), and escaping is per character,
+// so each piece is escaped in turn between one pair of quotes.
+void json_escape(Out& o, const char* s) {
   static const char hex[] = "0123456789abcdef";
-  o.putc('"');
-  for (const unsigned char* p = reinterpret_cast<const unsigned char*>(s); *p; ++p) {
-    unsigned char c = *p;
+  const unsigned char* p = reinterpret_cast<const unsigned char*>(s);
+  for (;;) {  // runs of bytes that need no escape in one copy
+    const unsigned char* q = p;
+    while (*q >= 0x20 && *q != '"' && *q != '\\' && *q != '<' && *q != '>' && *q != '&' && *q != 0xE2) ++q;
+    if (q != p) o.put(reinterpret_cast<const char*>(p), static_cast<size_t>(q - p));
+    p = q;
+    if (!*p) return;
+    const unsigned char c = *p;
     if (c == '"') o.put("\\\"");
     else if (c == '\\') o.put("\\\\");
     else if (c == '\n') o.put("\\n");
@@ -87,7 +98,20 @@ void json_string(Out& o, const char* s) {
     } else {
       o.putc(static_cast<char>(c));
     }
+    ++p;
   }
+}
+
+void json_string(Out& o, const char* s) {
+  o.putc('"');
+  json_escape(o, s);
+  o.putc('"');
+}
+
+// "a" + "b" + ... as one JSON string
+void json_cat(Out& o, std::initializer_list<const char*> parts) {
+  o.putc('"');
+  for (const char* x : parts) json_escape(o, x);
   o.putc('"');
 }
 
@@ -113,12 +137,9 @@ void json_float(Out& o, double f) {
 
 void json_int(Out& o, long long v) {
   char b[32];
-  int k = std::snprintf(b, sizeof b, "%lld", v);
-  o.put(b, static_cast<size_t>(k));
+  auto r = std::to_chars(b, b + sizeof b, v);
+  o.put(b, static_cast<size_t>(r.ptr - b));
 }
-
-// decimal.NewFromFloat(price).String() for an integer-valued price (ordernode.go:106,115).
-std::string price_str(int64_t p) { return std::to_string(p); }
 
 struct NodeView {
   int action;
@@ -136,7 +157,10 @@ struct NodeView {
 // encoding/json of OrderNode, fields in declaration order (ordernode.go:9-36), keys
 // built as SetOrderHashKey/SetListZsetKey/SetDepthHashKey/SetNodeName/SetNodeLink.
 void render_node(Out& o, const NodeView& v) {
-  std::string S(v.symbol), P = price_str(v.price);
+  // decimal.NewFromFloat(price).String() for an integer-valued price (ordernode.go:106,115)
+  char P[32];
+  *std::to_chars(P, P + sizeof P - 1, static_cast<long long>(v.price)).ptr = 0;
+  const char* S = v.symbol;
   bool sale = v.transaction == GOME_SALE;
   o.put("{\"Action\":"); json_int(o, v.action);
   o.put(",\"Uuid\":"); json_string(o, v.uuid);
@@ -146,21 +170,22 @@ void render_node(Out& o, const NodeView& v) {
   o.put(",\"Price\":"); json_float(o, static_cast<double>(v.price));
   o.put(",\"Volume\":"); json_float(o, static_cast<double>(v.volume));
   o.put(",\"Accuracy\":"); json_int(o, v.accuracy);
-  o.put(",\"NodeName\":"); json_string(o, (S + ":node:" + v.oid).c_str());
+  o.put(",\"NodeName\":"); json_cat(o, {S, ":node:", v.oid});
   o.put(",\"IsFirst\":"); o.put(v.is_first ? "true" : "false");
   o.put(",\"IsLast\":"); o.put(v.is_last ? "true" : "false");
   o.put(",\"PrevNode\":");
-  json_string(o, v.prev_oid ? (S + ":node:" + v.prev_oid).c_str() : "");
+  if (v.prev_oid) json_cat(o, {S, ":node:", v.prev_oid});
+  else o.put("\"\"");
   o.put(",\"NextNode\":");
-  json_string(o, v.next_oid ? (S + ":node:" + v.next_oid).c_str() : "");
-  o.put(",\"NodeLink\":"); json_string(o, (S + ":link:" + P).c_str());
-  o.put(",\"OrderHashKey\":"); json_string(o, (S + ":comparison").c_str());
-  o.put(",\"OrderHashField\":");
-  json_string(o, (S + ":" + v.uuid + ":" + v.oid).c_str());
-  o.put(",\"OrderListZsetKey\":"); json_string(o, (S + (sale ? ":SALE" : ":BUY")).c_str());
-  o.put(",\"OrderListZsetRKey\":"); json_string(o, (S + (sale ? ":BUY" : ":SALE")).c_str());
-  o.put(",\"OrderDepthHashKey\":"); json_string(o, (S + ":depth").c_str());
-  o.put(",\"OrderDepthHashField\":"); json_string(o, (S + ":depth:" + P).c_str());
+  if (v.next_oid) json_cat(o, {S, ":node:", v.next_oid});
+  else o.put("\"\"");
+  o.put(",\"NodeLink\":"); json_cat(o, {S, ":link:", P});
+  o.put(",\"OrderHashKey\":"); json_cat(o, {S, ":comparison"});
+  o.put(",\"OrderHashField\":"); json_cat(o, {S, ":", v.uuid, ":", v.oid});
+  o.put(",\"OrderListZsetKey\":"); json_cat(o, {S, sale ? ":SALE" : ":BUY"});
+  o.put(",\"OrderListZsetRKey\":"); json_cat(o, {S, sale ? ":BUY" : ":SALE"});
+  o.put(",\"OrderDepthHashKey\":"); json_cat(o, {S, ":depth"});
+  o.put(",\"OrderDepthHashField\":"); json_cat(o, {S, ":depth:", P});
   o.putc('}');
 }
 
@@ -292,4 +317,57 @@ extern "C" int64_t gome_render_match_result(const gome_event* ev, const gome_ord
   if (!o.ok) return -static_cast<int64_t>(o.n + 1);  // the buffer size it needs
   buf[o.n] = 0;
   return static_cast<int64_t>(o.n);
+}
+
+// gome_render_events over `threads` pieces cut at taker boundaries (a taker's Node.Volume is a
+// running sum over its consecutive events), each rendered into a buffer of its own and copied
+// out in publish order.
+extern "C" int64_t gome_render_events_mt(const gome_event* ev, size_t n, const gome_order* batch, size_t batch_n,
+                                         uint64_t seq_base, uint32_t accuracy, const char* const* sym_names,
+                                         size_t n_sym, const char* const* uuid_names, size_t n_uuid,
+                                         const char* const* oid_names, size_t n_oid, const int32_t* tx_table,
+                                         uint32_t threads, char* buf, size_t cap) {
+  if ((n && (!ev || !batch)) || !sym_names || !uuid_names || !oid_names || (!buf && cap)) return INT64_MIN;
+  uint32_t t = threads ? threads : std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
+  t = static_cast<uint32_t>(std::max<size_t>(1, std::min<size_t>({t, 64, (n + 255) / 256})));
+  std::vector<size_t> cut(t + 1, n);
+  cut[0] = 0;
+  for (uint32_t k = 1; k < t; ++k) {
+    size_t i = std::max(cut[k - 1], n * k / t);
+    while (i > cut[k - 1] && i < n && ev[i].taker_seq == ev[i - 1].taker_seq) ++i;
+    cut[k] = i;
+  }
+  std::vector<std::vector<char>> piece(t);
+  std::vector<int64_t> got(t, 0);
+  auto work = [&](uint32_t k) {
+    const size_t a = cut[k], b = cut[k + 1];
+    std::vector<char>& pb = piece[k];
+    pb.resize(std::max<size_t>(4096, (b - a) * 1400));
+    for (;;) {
+      const int64_t r = gome_render_events(ev + a, b - a, batch, batch_n, seq_base, accuracy, sym_names, n_sym,
+                                           uuid_names, n_uuid, oid_names, n_oid, tx_table, pb.data(), pb.size());
+      if (r == INT64_MIN || r >= 0) {
+        got[k] = r;
+        return;
+      }
+      pb.resize(static_cast<size_t>(-r) + 1);
+    }
+  };
+  std::vector<std::thread> th;
+  for (uint32_t k = 1; k < t; ++k) th.emplace_back(work, k);
+  work(0);
+  for (auto& x : th) x.join();
+  size_t total = 0;
+  for (uint32_t k = 0; k < t; ++k) {
+    if (got[k] == INT64_MIN) return INT64_MIN;
+    total += static_cast<size_t>(got[k]);
+  }
+  if (total + 1 > cap) return -static_cast<int64_t>(total + 1);
+  size_t at = 0;
+  for (uint32_t k = 0; k < t; ++k) {
+    std::memcpy(buf + at, piece[k].data(), static_cast<size_t>(got[k]));
+    at += static_cast<size_t>(got[k]);
+  }
+  buf[at] = 0;
+  return static_cast<int64_t>(total);
 }

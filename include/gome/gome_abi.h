@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define GOME_ABI_VERSION 10u
+#define GOME_ABI_VERSION 11u
 
 /* ---- status codes (replace the reference's swallowed errors / panics,
  *      rabbitmq.go:44-49,70-72,120-122; nodelink.go:132,142,157) ---------- */
@@ -160,6 +160,11 @@ typedef struct gome_node {
 /* gome_stats.ms_phase (per-phase device times) needs ~24 timing-event records per batch on the
  * pipeline's streams (0.12 ms per config-2 batch); they are recorded only with this flag. */
 #define GOME_FLAG_PHASES 16u
+/* Stream layout (ABI >= 11).  The early plan of the hottest book (§4.8) and
+ * admission ahead of the batch (§4.9) are on by default when the process has at least 8 hardware
+ * queues (gome_config.hw_queues); these flags turn them off (A/B and tests: same results). */
+#define GOME_FLAG_NO_EARLY 32u
+#define GOME_FLAG_NO_ADM_AHEAD 64u
 
 typedef struct gome_config {
   uint32_t accuracy;       /* gomengine.accuracy (config.yaml.example:23-24), default 8 */
@@ -170,7 +175,20 @@ typedef struct gome_config {
   uint64_t max_levels;     /* level-record capacity (all books)                          */
   uint64_t max_events;     /* event capacity per batch (0: derived from max_batch)       */
   uint32_t flags;          /* GOME_FLAG_* (0 = defaults)                                 */
-  uint32_t pad;
+  uint32_t abi_version;    /* must be GOME_ABI_VERSION: gome_create refuses any other value,
+                              so a caller built against another ABI fails loudly (ABI <= 10
+                              had a zero pad word here)                                 */
+  /* Hardware queues the process's HIP runtime has: GPU_MAX_HW_QUEUES as the runtime read it
+   * when it started (HIP's default is 4).  Streams beyond that share queues and run one after
+   * another, so the engine picks its stream layout from this count: with >= 8 the cold books
+   * run beside the tail's chain, the hottest book is planned early and admission runs ahead;
+   * below 8, the four-stream layout.  0: the variable's value at gome_create (4 if unset or
+   * not a number) -- correct only when nothing started HIP before the variable was set. */
+  uint32_t hw_queues;
+  /* CUs reserved for the hottest book's plan (a CU-masked stream, every other stream masked off
+   * them): 0 = the default (8 with >= 8 hardware queues, else none), < 0 = none,
+   * k > 0 = k. */
+  int32_t plan_cus;
 } gome_config;
 
 /* gome_stats.ms_phase (ABI >= 5): device time of the pipeline's phases in the last batch, each

@@ -186,6 +186,17 @@ def _go_coerce_utf8(b: bytes) -> str:
     return "".join(out)
 
 
+def go_fold_name(key: str) -> str:
+    """encoding/json's case-insensitive key match (Go 1.21 fold.go foldName: ASCII letters to upper
+    case, any other rune to the smallest rune of its unicode.SimpleFold orbit; earlier Go:
+    bytes.EqualFold, the same orbits).  The field names are ASCII, and the only non-ASCII runes
+    whose orbit holds an ASCII letter are U+017F (long s ~ S) and U+212A (Kelvin sign ~ K); every
+    other non-ASCII rune is left as it is here, which keeps it from matching any field, as in Go.
+    (Python's str.casefold is not this: it maps U+FB01 'fi' to "fi" and U+00DF to "ss".)"""
+    return "".join("S" if c == "\u017f" else "K" if c == "\u212a" else c.upper() if "a" <= c <= "z" else c
+                   for c in key)
+
+
 def go_unmarshal_order_node(body) -> "OrderNode":
     """json.Unmarshal(body, &OrderNode{}) as rabbitmq.go:118-121 runs it (the error is printed
     and DoOrder still runs): a syntax error decodes nothing (zero node, Action 0, ignored by
@@ -203,9 +214,9 @@ def go_unmarshal_order_node(body) -> "OrderNode":
     if not isinstance(d, _Obj):
         return node  # null: no effect; any other top-level type: UnmarshalTypeError
     exact = {n: (n, k) for n, k in NODE_FIELDS}
-    folded = {n.casefold(): (n, k) for n, k in NODE_FIELDS}
+    folded = {go_fold_name(n): (n, k) for n, k in NODE_FIELDS}
     for key, v in d:
-        f = exact.get(key) or folded.get(key.casefold())
+        f = exact.get(key) or folded.get(go_fold_name(key))
         if f is None:
             continue
         x = _go_field_value(f[1], f[0], v)

@@ -17,14 +17,14 @@ def test_library_exports_every_declared_symbol():
     assert len(names) >= 14
     for n in names:
         assert hasattr(lib, n), n
-    assert lib.gome_abi_version() == 10
+    assert lib.gome_abi_version() == abi.GOME_ABI_VERSION == 11
 
 
 def test_record_layouts_match_header():
     from gome_amd.workload import EVENT_DTYPE, LEVEL_DTYPE, NODE_DTYPE, ORDER_DTYPE
     assert ORDER_DTYPE.itemsize == 32 and EVENT_DTYPE.itemsize == 48
     assert LEVEL_DTYPE.itemsize == 24 and NODE_DTYPE.itemsize == 24
-    assert C.sizeof(abi.Config) == 48
+    assert C.sizeof(abi.Config) == 56
 
 
 @pytest.mark.parametrize("x", [0.0, 0.1, 0.29, 0.57, 1.0, 12.34, 0.00000001, 123456.12345678,
@@ -65,6 +65,28 @@ def test_create_without_gpu_fails_loudly():
     with pytest.raises(abi.GomeError) as ei:
         abi.Engine(max_symbols=4, max_batch=16)
     assert ei.value.status == abi.GOME_E_DEVICE
+
+
+def test_create_refuses_a_stale_abi_version():
+    """gome_config.abi_version sits where ABI <= 10 had a zero pad word: a caller built against an
+    older header is refused before anything else (no silent argument shift)."""
+    lib = abi.load_library()
+    for v in (0, 10, 12):
+        cfg = abi.Config(max_symbols=4, max_batch=16, max_nodes=64, max_levels=64, abi_version=v)
+        h = C.c_void_p()
+        assert lib.gome_create(C.byref(cfg), C.byref(h)) == abi.GOME_E_INVAL
+        msg = lib.gome_last_error(None).decode()
+        assert f"abi_version is {v}" in msg and "ABI 11" in msg, msg
+
+
+def test_hw_queue_count_parsing():
+    """gome_amd records the hardware queues HIP will have; odd values of the variable read as
+    unset (HIP's default 4) instead of raising at import."""
+    import gome_amd
+    assert gome_amd._parse_queues("16") == 16 and gome_amd._parse_queues(" 8 ") == 8
+    for bad in ("", "abc", "0", "-3", None, "4.5"):
+        assert gome_amd._parse_queues(bad) is None
+    assert gome_amd.hw_queues() >= 4
 
 
 # ---- ABI v4 boundary fixes ------------------------------------------------------------

@@ -11,7 +11,7 @@ import pytest
 
 import bench
 from gome_amd import workload as wl
-from gome_amd.abi import GOME_E_INVAL, Engine, GomeError
+from gome_amd.abi import GOME_E_INVAL, GOME_FLAG_NO_ADM_AHEAD, Engine, GomeError
 from oracle.pyoracle import Oracle
 from tests.test_gpu_early import N, _run
 from tests.test_gpu_v4 import _cmp, _cmp_books, _hot_and_random
@@ -88,9 +88,8 @@ def test_rejected_batch_with_admission_ahead():
     _cmp_books(eng, orc, _hot_and_random(z, 100000, k_rand=30), "around a rejected batch")
 
 
-def test_admission_ahead_off(monkeypatch):
-    monkeypatch.setenv("GOME_ADM_AHEAD", "0")
-    _, _, stats = _run(_config4(5, 11), 100000, "adm ahead off")
+def test_admission_ahead_off():
+    _, _, stats = _run(_config4(5, 11), 100000, "adm ahead off", flags=GOME_FLAG_NO_ADM_AHEAD)
     assert all(int(s["n_adm_ahead"]) == 0 for s in stats)
 
 

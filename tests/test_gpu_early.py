@@ -13,7 +13,7 @@ import pytest
 
 import bench
 from gome_amd import workload as wl
-from gome_amd.abi import GOME_E_INVAL, GOME_ORD_ADM_HOST, GOME_ORD_ADMITTED, Engine, GomeError
+from gome_amd.abi import GOME_E_INVAL, GOME_FLAG_NO_EARLY, GOME_ORD_ADM_HOST, GOME_ORD_ADMITTED, Engine, GomeError
 from oracle.pyoracle import Oracle
 from tests.test_gpu_v4 import _cmp, _cmp_books, _hot_and_random
 
@@ -22,10 +22,11 @@ pytestmark = pytest.mark.gpu
 N = 1 << 18
 
 
-def _run(batches, nsym, label, levels=1 << 22):
-    """Submit every batch with three in flight, collect in order; per-batch stats."""
+def _run(batches, nsym, label, levels=1 << 22, **kw):
+    """Submit every batch with three in flight, collect in order; per-batch stats.  kw: more
+    Engine arguments (layout flags, hw_queues, plan_cus)."""
     import torch
-    eng = Engine(max_symbols=nsym, max_batch=N, max_nodes=(len(batches) + 4) * N, max_levels=levels)
+    eng = Engine(max_symbols=nsym, max_batch=N, max_nodes=(len(batches) + 4) * N, max_levels=levels, **kw)
     orc = Oracle(nsym)
     dev = [torch.from_numpy(b.view(np.uint8).copy()).cuda() for b in batches]
     torch.cuda.synchronize()
@@ -174,9 +175,8 @@ def test_rejected_batch_between_early_plans():
     _cmp_books(eng, orc, _hot_and_random(z, 100000, k_rand=30), "around a rejected batch")
 
 
-def test_early_plan_off_is_the_same_engine(monkeypatch):
+def test_early_plan_off_is_the_same_engine():
     gen, _, _ = bench.shard_stream(100000, 1.0, 0, 1, 11)
     batches = [gen(N).copy() for _ in range(6)]
-    monkeypatch.setenv("GOME_EARLY", "0")
-    _, _, stats = _run(batches, 100000, "early off")
+    _, _, stats = _run(batches, 100000, "early off", flags=GOME_FLAG_NO_EARLY)
     assert all(int(s["n_early"]) == 0 for s in stats)

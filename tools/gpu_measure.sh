@@ -1,7 +1,9 @@
 #!/bin/bash
-# Round-4 final measurements (GPU box).  usage: bash tools/r4_final.sh <tag> [parts...]
+# Measurements on the GPU box.  usage: bash tools/gpu_measure.sh <tag> [parts...]
 #   suite: the GPU test suite;  smoke;  benches: bench lines (e2e, consumer leg, CPU baseline) of
 #   configs 3, 2, 4, 5, 5c;  heal / pg: the quirk-injection line and the RCCL world-1 line;
+#   tests <pytest args>: a subset of the GPU suite (e.g. tests=tests/test_a_layouts_gpu.py);
+#   q4: the config-3 bench line in a process whose HIP runtime has 4 hardware queues;
 #   prof3 / prof2: rocprofv3 trace + FETCH / WRITE passes (profiles/run_rocprof.sh) + summary
 set -o pipefail
 TAG=${1:-r04f}; shift
@@ -19,6 +21,14 @@ for P in $PARTS; do
     timeout -k 10 700 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread \
       > $OUT/gpu_tests.txt 2>&1 || { tail -40 $OUT/gpu_tests.txt; exit 2; }
     tail -3 $OUT/gpu_tests.txt ;;
+  tests=*)
+    timeout -k 10 900 python -u -m pytest ${P#tests=} -m gpu -v --timeout 600 --timeout-method thread \
+      > $OUT/gpu_subset.txt 2>&1 || { tail -60 $OUT/gpu_subset.txt; exit 2; }
+    tail -8 $OUT/gpu_subset.txt ;;
+  q4)
+    GOME_HW_QUEUES=4 timeout -k 10 400 python3 -u bench.py --workload config3 --no-cpu-baseline --consumer-msgs 0 \
+      > $OUT/config3_q4_bench.jsonl 2> $OUT/config3_q4_bench.log || { tail -20 $OUT/config3_q4_bench.log; exit 9; }
+    summ $OUT/config3_q4_bench.jsonl q4 ;;
   smoke)
     timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.txt 2>&1 || { tail -20 $OUT/smoke.txt; exit 8; }
     tail -1 $OUT/smoke.txt ;;

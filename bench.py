@@ -189,6 +189,23 @@ def combine_ranks(orders, fills, events, elapsed, lat, device):
     return o, f, ev, float(e.item()), lt.tolist()
 
 
+def rank_batch(batch, world, share, scaling="weak"):
+    """Records of one rank per step.  weak: `batch` orders per GPU (the global stream holds world x
+    batch, each rank its symbols' share of it); strong: `batch` orders per step in all, split over
+    the ranks by their symbols' share."""
+    return int(round(batch * (world if scaling == "weak" else 1) * share))
+
+
+def per_rank_values(x, rank, world, device):
+    """Every rank's value of x, in rank order, on every rank (one all_reduce of a one-hot vector)."""
+    import torch
+    import torch.distributed as dist
+    t = torch.zeros(world, dtype=torch.float64, device=device)
+    t[rank] = float(x)
+    dist.all_reduce(t)
+    return [round(float(v), 3) for v in t.tolist()]
+
+
 def gather_summary(st, summary, gathered, rank=0, step=0, digests=None):
     """Per-GPU trade/depth summary to every rank (the publisher feed)."""
     import torch.distributed as dist
@@ -232,29 +249,30 @@ def cpu_baseline(batches, n_symbols, budget_s, threads=1):
     return one, (done / wall, done, wall, used)
 
 
-def consumer_leg(workload, n_symbols, n_msgs, seed, batch=1 << 15, render_threads=8):
-    """The drop-in boundary's own rate: n_msgs doOrder messages (the OrderNode JSON
-    the gRPC side enqueues, main.go:39-52 / ordernode.go:9-36, admission markers set) of the same
-    workload through BatchingConsumer.process -- Go-Unmarshal decode, fixed-point conversion,
-    interning, admission, gome_submit_batch, drain, gome_render_events into MatchResult lines on the
-    sink (rabbitmq.go:116-125, engine.go:154-194) -- at one host thread; then gome_render_events
-    alone over the same events at 1 and render_threads threads."""
+def consumer_leg(workload, n_symbols, n_msgs, seed, batch=1 << 15, threads=8):
+    """The drop-in boundary's own rate: n_msgs doOrder messages (the OrderNode
+    JSON bodies the gRPC side enqueues, main.go:39-52 / ordernode.go:9-36, admission markers set) of
+    the same workload through BatchingConsumer.process -- native Go-Unmarshal decode on `threads`
+    threads, fixed-point conversion, interning, admission (gome_consume_order_nodes),
+    gome_submit_batch, drain, gome_render_events_mt into MatchResult lines on the sink
+    (rabbitmq.go:116-125, engine.go:154-194); then the renderer alone over the same events at 1 and
+    `threads` threads."""
     import ctypes as C
-    from concurrent.futures import ThreadPoolExecutor
     from gome_amd.abi import Engine
     from gome_amd.consumer import BatchingConsumer, MatchSink, Names, PrePool, _order_node_json
     gen, _, _ = make_stream(workload, 0, 1, seed + 7)
     rec = gen(n_msgs).copy()
     msgs = [_order_node_json(dict(symbol="s%d" % r["symbol_id"], uuid=str(int(r["uuid_id"])),
                                   oid=str(int(r["oid_id"])), transaction=int(r["side"])),
-                             int(r["action"]), float(r["price_fx"]), float(r["volume_fx"]), 8) for r in rec]
+                             int(r["action"]), float(r["price_fx"]), float(r["volume_fx"]), 8).encode()
+            for r in rec]  # (AMQP delivers bytes)
     pre, sink, names = PrePool(), MatchSink(), Names()
     for r in rec:
         if r["action"] == wl.ADD:
             pre.set("s%d" % r["symbol_id"], str(int(r["uuid_id"])), str(int(r["oid_id"])))
     eng = Engine(max_symbols=n_symbols, max_batch=batch, max_nodes=2 * n_msgs + (1 << 20),
                  max_levels=(1 << 22) + 2 * n_msgs)
-    cons = BatchingConsumer(eng, pre, sink, names, max_batch=batch)
+    cons = BatchingConsumer(eng, pre, sink, names, max_batch=batch, threads=threads)
     evs, recs, bases = [], [], []
     orig_render = cons.render
 
@@ -271,28 +289,23 @@ def consumer_leg(workload, n_symbols, n_msgs, seed, batch=1 << 15, render_thread
     wall = time.perf_counter() - t
     lib = cons.lib
     N = names
-
-    def render(i):
-        ev, rc, base = evs[i], recs[i], bases[i]
-        cap = max(1 << 20, 1400 * len(ev))
-        buf = C.create_string_buffer(cap)
-        k = lib.gome_render_events(ev.ctypes.data, len(ev), rc.ctypes.data, len(rc), base, 8,
-                                   C.cast(N.table("sym"), C.c_void_p), len(N.rev["sym"]),
-                                   C.cast(N.table("uuid"), C.c_void_p), len(N.rev["uuid"]),
-                                   C.cast(N.table("oid"), C.c_void_p), len(N.rev["oid"]),
-                                   N.tx_array().ctypes.data, buf, cap)
-        assert k >= 0
-        return k
     nev = sum(len(e) for e in evs)
     out = {"messages": n_msgs, "batch": batch, "messages_per_s": round(n_msgs / wall, 1),
-           "matchresults_per_s": round(lines / wall, 1), "matchresults": lines, "threads": 1,
-           "path": "OrderNode JSON -> BatchingConsumer.process (decode, convert, intern, admit, "
-                   "gome_submit_batch, drain, gome_render_events) -> MatchResult lines on the sink",
+           "matchresults_per_s": round(lines / wall, 1), "matchresults": lines, "threads": threads,
+           "path": "OrderNode JSON bytes -> BatchingConsumer.process (gome_consume_order_nodes: decode, convert, "
+                   "intern, admit; gome_submit_batch, drain, gome_render_events_mt) -> MatchResult lines on the sink",
            "render_events_per_s": {}}
-    for th in (1, render_threads):
+    for th in (1, threads):
+        nbytes = 0
         t = time.perf_counter()
-        with ThreadPoolExecutor(max_workers=th) as ex:
-            nbytes = sum(ex.map(render, range(len(evs))))
+        for ev, rc, base in zip(evs, recs, bases):
+            cap = max(1 << 20, 1400 * len(ev))
+            buf = C.create_string_buffer(cap)
+            k = lib.gome_render_events_mt(ev.ctypes.data, len(ev), rc.ctypes.data, len(rc), base, 8,
+                                          N.table("sym"), N.count("sym"), N.table("uuid"), N.count("uuid"),
+                                          N.table("oid"), N.count("oid"), N.tx_array().ctypes.data, th, buf, cap)
+            assert k >= 0
+            nbytes += k
         dt = time.perf_counter() - t
         out["render_events_per_s"][str(th)] = round(nev / dt, 1)
         out["render_MB_per_s_" + str(th)] = round(nbytes / dt / 1e6, 1)
@@ -359,13 +372,16 @@ def main():
                     help="initialise the process group and run the summary gather, the publisher and the "
                          "digest check at N = 1 too (exercises the RCCL path on a one-GPU box)")
     ap.add_argument("--inject-quirks", choices=("none", "heal", "stuck"), default="none",
-                    help="rewrite records of the hottest book in batch 1 into a wrong-side cancel (Q2) of a "
-                         "bid level and a zero-volume ADD (Q6) (workload.inject_quirks); warm-up should "
-                         "cover batches 0-2")
+                    help="rewrite records of the hottest book in the first timed batch into wrong-side "
+                         "cancels (Q2) of a bid level and a zero-volume ADD (Q6) (workload.inject_quirks); "
+                         "the line's quirk_batch reports that batch's device time beside its neighbours'")
     ap.add_argument("--consumer-msgs", type=int, default=1 << 17,
                     help="JSON OrderNode messages of the consumer leg (0: off)")
     ap.add_argument("--pool-nodes", type=int, default=0, help="gome_config.max_nodes (0: sized from the run)")
     ap.add_argument("--pool-levels", type=int, default=0, help="gome_config.max_levels (0: sized from the run)")
+    ap.add_argument("--scaling", choices=("weak", "strong"), default="weak",
+                    help="weak: --batch orders per GPU per step; strong: --batch orders per step in all, "
+                         "split over the GPUs (DESIGN 7)")
     ap.add_argument("--plan-cus", type=int, default=None,
                     help="gome_config.plan_cus (default: 0 = the engine's default; -1 with RCCL)")
     ap.add_argument("--step-log", default="", help="write each timed step's engine counters (JSONL)")
@@ -415,7 +431,7 @@ def main():
     # event buffer, which two warm batches left for the third slot inside the timed region)
     e2e_warm = GOME_MAX_INFLIGHT + 1 if e2e_steps else 0
     gen, share, top_share = make_stream(args.workload, rank, world, args.seed)
-    per_rank = int(round(args.batch * world * share))
+    per_rank = rank_batch(args.batch, world, share, args.scaling)
     note(f"{args.workload}: generating {warm + steps} batches of {per_rank} records")
     host_batches = [gen(per_rank).copy() for _ in range(warm + steps)]
     injected = None
@@ -502,23 +518,19 @@ def main():
             collect(hi - 1)
 
     slog = None
-    w0 = 0
-    if args.inject_quirks != "none":
-        # batch 0 synchronously, then batch 1's records of the hottest book rewritten from the
-        # engine's own snapshot of that book (workload.inject_quirks); warm-up covers batches 0-2
-        if warm < 3:
-            print("--inject-quirks needs --warmup >= 3", file=sys.stderr)
-            sys.exit(2)
-        step(0)
-        hs = int(hot[0])
-        injected = wl.inject_quirks(host_batches[1], hs, eng.levels(hs), lambda p: eng.fifo(hs, p),
-                                    args.inject_quirks)
-        dev_batches[1].copy_(torch.from_numpy(host_batches[1].view(np.uint8)))
-        torch.cuda.synchronize()
-        note(f"injected into batch 1: {injected['q2_cancels']} wrong-side cancels, one zero-volume ADD")
-        w0 = 1
-    run_steps(w0, warm, None, None, False)
+    run_steps(0, warm, None, None, False)
     torch.cuda.synchronize()
+    if args.inject_quirks != "none":
+        # the FIRST TIMED batch's records of the hottest book rewritten from the engine's own
+        # snapshot of that book after the warm-up (workload.inject_quirks), so the batch that
+        # carries the quirks is timed; the line reports its own device time beside its neighbours'
+        hs = int(hot[0])
+        injected = wl.inject_quirks(host_batches[warm], hs, eng.levels(hs), lambda p: eng.fifo(hs, p),
+                                    args.inject_quirks)
+        dev_batches[warm].copy_(torch.from_numpy(host_batches[warm].view(np.uint8)))
+        torch.cuda.synchronize()
+        note(f"injected into batch {warm} (the first timed one): {injected['q2_cancels']} wrong-side cancels, "
+             f"one zero-volume ADD")
     if use_pg:
         dist.barrier()
     if pub is not None:
@@ -535,7 +547,9 @@ def main():
         slog.close()
 
     dev_lat = [float(s["ms_total"]) for s in sts]
-    if use_pg:  # (the slowest rank's device time per step)
+    p99_ranks = [round(pctl(dev_lat, 0.99), 3)]
+    if use_pg:  # (each rank's own p99, then the slowest rank's device time per step)
+        p99_ranks = per_rank_values(p99_ranks[0], rank, world, cdev)
         dev_lat = combine_ranks(0.0, 0.0, 0.0, 0.0, dev_lat, cdev)[4]
     orders = sum(s["n_orders"] for s in sts)
     fills = sum(s["n_fills"] for s in sts)
@@ -636,11 +650,14 @@ def main():
         in_b, out_b = 32 * per_rank, 48 * e_events / e2e_steps / max(world, 1)
         e2e = {"value": round(e_orders / e_el, 1), "unit": "orders/s", "steps": e2e_steps,
                "pcie_peak": pk,
-               # the copies' lower bound per step on this rank: H2D and D2H overlapped (duplex rate)
-               # or serialised on one copy stream (one direction at a time)
+               # the copies' time per step on this rank at the measured one-way rates: H2D and D2H
+               # overlapped (PCIe is full duplex: the slower direction bounds the step) or serialised
+               # (one after the other).  overlapped <= serial by construction; the measured rate with
+               # both directions at once (pcie_peak.duplex_GBps_each) is reported beside them
                "pcie_bound_ms": None if pk is None else {
-                   "overlapped": round(max(in_b, out_b) / (pk["duplex_GBps_each"] * 1e9) * 1e3, 3),
-                   "serial": round((in_b / (pk["h2d_GBps"] * 1e9) + out_b / (pk["d2h_GBps"] * 1e9)) * 1e3, 3)},
+                   "overlapped": round(max(in_b / (pk["h2d_GBps"] * 1e9), out_b / (pk["d2h_GBps"] * 1e9)) * 1e3, 3),
+                   "serial": round((in_b / (pk["h2d_GBps"] * 1e9) + out_b / (pk["d2h_GBps"] * 1e9)) * 1e3, 3),
+                   "duplex_measured": round(max(in_b, out_b) / (pk["duplex_GBps_each"] * 1e9) * 1e3, 3)},
                "ms_per_step": round(e_el / e2e_steps * 1e3, 3),
                "host_ms_per_step": {k: round(v / e2e_steps, 3) for k, v in host_ms.items()},
                # the median gap between two batches' collects: the pipeline's steady-state step,
@@ -720,13 +737,14 @@ def main():
             "warmup": warm,
             "ms_per_step": round(elapsed / steps * 1e3, 3),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": args.scaling,
             "vs_baseline": None,
             "dtype": "int64",
             "data": "synthetic (seeded doorder.go distribution, Zipf symbols)",
             "config": {"workload": W["desc"].format(**W), "name": args.workload,
                        "symbols": n_symbols, "zipf_s": W["zipf"],
-                       "batch_per_gpu": per_rank, "global_batch": per_rank * world,
+                       "batch_per_gpu": per_rank,
+                       "global_batch": per_rank * world if args.scaling == "weak" else args.batch,
                        "parallelism": f"symbol-sharded x{world} (no data-path collective)"},
             "p50_batch_ms": round(pctl(lat, 0.5), 3),
             "p99_batch_ms": round(pctl(lat, 0.99), 3),
@@ -734,6 +752,7 @@ def main():
             # batches in flight a batch starts when the one before it leaves the pipeline's stream)
             "p50_device_batch_ms": round(pctl(dev_lat, 0.5), 3),
             "p99_device_batch_ms": round(pctl(dev_lat, 0.99), 3),
+            "p99_device_batch_ms_per_rank": p99_ranks,
             "fills_per_s": round(g_fills / elapsed, 1),
             "events_per_s": round(g_events / elapsed, 1),
             "cancels_per_batch": int(cancels / steps),
@@ -777,6 +796,14 @@ def main():
                                             "cannot end before that one wavefront does"}
         if injected is not None:
             out["config"]["injected"] = dict(injected, records=len(injected["records"]))
+            clean = [float(s["ms_total"]) for s in sts[2:]]  # (the injected batch and the one after it aside)
+            out["quirk_batch"] = {
+                "injected_batch_device_ms": round(float(sts[0]["ms_total"]), 3),
+                "next_batch_device_ms": round(float(sts[1]["ms_total"]), 3) if len(sts) > 1 else None,
+                "clean_median_device_ms": round(float(np.median(clean)), 3) if clean else None,
+                "ratio": round(float(sts[0]["ms_total"]) / float(np.median(clean)), 3) if clean else None,
+                "legacy_hot_orders": [int(s["n_hot_orders"]) - int(s["n_flow_orders"]) for s in sts[:3]],
+                "flow_head_orders": [int(s["n_flow_head_orders"]) for s in sts[:3]]}
         if consumer is not None:
             consumer["vs_value"] = round(consumer["messages_per_s"] / out["value"], 6)
         if pub is not None and use_pg:

@@ -66,7 +66,7 @@ def _stream(workload, k=5):
 
 def _engine(nb, kw):
     from gome_amd.abi import Engine
-    return Engine(max_symbols=100000, max_batch=N, max_nodes=(nb + 4) * N, max_levels=1 << 23, **kw)
+    return Engine(max_symbols=100000, max_batch=N, max_nodes=(nb + 4) * N, max_levels=(nb + 4) * N, **kw)
 
 
 def run_device(workload, kw, label):

@@ -90,8 +90,9 @@ def _worker(rank, world, port, out_dir):
             bench.gather_summary(st, summary, gathered, rank, step)
             pub.consume(gathered)
         ok = pub.check(3 * (2000 + 1), 3 * 10, 3 * 20)
+        p99 = bench.per_rank_values(10.0 + rank, rank, world, "cpu")  # (each rank's own p99)
         np.save(os.path.join(out_dir, f"r{rank}.npy"),
-                np.array([o, f, e, el] + lat + gathered.tolist() + [float(ok), float(pub.steps)],
+                np.array([o, f, e, el] + lat + gathered.tolist() + [float(ok), float(pub.steps)] + p99,
                          dtype=np.float64))
     finally:
         dist.destroy_process_group()
@@ -112,5 +113,19 @@ def test_gloo_world2_reductions():
         for rk in range(world):
             row = [g[rk, idx[k]] for k in ("n_orders", "n_fills", "n_events", "n_resting", "max_segment", "rank", "step")]
             assert row == [1000 + rk, 10 * rk, 20 * rk, 5 + rk, 77 + rk, rk, 2]
-        assert r[-2] == 1.0 and r[-1] == 3.0             # publisher totals == job totals
+        assert r[-4] == 1.0 and r[-3] == 3.0             # publisher totals == job totals
+        assert list(r[-2:]) == [10.0, 11.0]              # every rank's p99, in rank order
     assert res[0].tobytes() == res[1].tobytes()
+
+
+@pytest.mark.parametrize("world", [1, 2, 4, 8])
+def test_strong_and_weak_rank_batches(world):
+    """Strong scaling splits --batch over the ranks by their symbols' share (the ranks' records
+    sum to the global batch); weak scaling gives each rank its share of world x batch."""
+    batch = 1 << 22
+    strong = [bench.rank_batch(batch, world, bench.shard_stream(100000, 1.0, r, world, 42)[1], "strong")
+              for r in range(world)]
+    weak = [bench.rank_batch(batch, world, bench.shard_stream(100000, 1.0, r, world, 42)[1], "weak")
+            for r in range(world)]
+    assert abs(sum(strong) - batch) <= world and abs(sum(weak) - world * batch) <= world
+    assert strong[0] == max(strong)  # (rank 0 owns the hottest symbol: Zipf rank 0)

@@ -2,7 +2,7 @@
 # Measurements on the GPU box.  usage: bash tools/gpu_measure.sh <tag> [parts...]
 #   suite: the GPU test suite;  smoke;  benches: bench lines (e2e, consumer leg, CPU baseline) of
 #   configs 3, 2, 4, 5, 5c;  heal / pg: the quirk-injection line and the RCCL world-1 line;
-#   tests <pytest args>: a subset of the GPU suite (e.g. tests=tests/test_a_layouts_gpu.py);
+#   tests=<files, comma-separated>: a subset of the GPU suite (e.g. tests=tests/test_a_layouts_gpu.py);
 #   q4: the config-3 bench line in a process whose HIP runtime has 4 hardware queues;
 #   prof3 / prof2: rocprofv3 trace + FETCH / WRITE passes (profiles/run_rocprof.sh) + summary
 set -o pipefail
@@ -22,7 +22,8 @@ for P in $PARTS; do
       > $OUT/gpu_tests.txt 2>&1 || { tail -40 $OUT/gpu_tests.txt; exit 2; }
     tail -3 $OUT/gpu_tests.txt ;;
   tests=*)
-    timeout -k 10 900 python -u -m pytest ${P#tests=} -m gpu -v --timeout 600 --timeout-method thread \
+    T=${P#tests=}
+    timeout -k 10 900 python -u -m pytest ${T//,/ } -m gpu -v --timeout 600 --timeout-method thread \
       > $OUT/gpu_subset.txt 2>&1 || { tail -60 $OUT/gpu_subset.txt; exit 2; }
     tail -8 $OUT/gpu_subset.txt ;;
   q4)
@@ -32,8 +33,9 @@ for P in $PARTS; do
   smoke)
     timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.txt 2>&1 || { tail -20 $OUT/smoke.txt; exit 8; }
     tail -1 $OUT/smoke.txt ;;
-  benches)
-    for W in config3 config2 config4 config5 config5c; do
+  bench3|bench2|bench4|bench5|bench5c|benches)
+    WS="config${P#bench}"; [ $P = benches ] && WS="config3 config2 config4 config5 config5c"
+    for W in $WS; do
       timeout -k 10 500 python3 -u bench.py --workload $W > $OUT/${W}_bench.jsonl 2> $OUT/${W}_bench.log \
         || { tail -20 $OUT/${W}_bench.log; exit 3; }
       summ $OUT/${W}_bench.jsonl $W

@@ -371,7 +371,7 @@ def main():
     ap.add_argument("--force-pg", action="store_true",
                     help="initialise the process group and run the summary gather, the publisher and the "
                          "digest check at N = 1 too (exercises the RCCL path on a one-GPU box)")
-    ap.add_argument("--inject-quirks", choices=("none", "heal", "stuck"), default="none",
+    ap.add_argument("--inject-quirks", choices=("none", "heal", "stuck", "q2heal", "q2stuck"), default="none",
                     help="rewrite records of the hottest book in the first timed batch into wrong-side "
                          "cancels (Q2) of a bid level and a zero-volume ADD (Q6) (workload.inject_quirks); "
                          "the line's quirk_batch reports that batch's device time beside its neighbours'")
@@ -529,8 +529,8 @@ def main():
                                     args.inject_quirks)
         dev_batches[warm].copy_(torch.from_numpy(host_batches[warm].view(np.uint8)))
         torch.cuda.synchronize()
-        note(f"injected into batch {warm} (the first timed one): {injected['q2_cancels']} wrong-side cancels, "
-             f"one zero-volume ADD")
+        note(f"injected into batch {warm} (the first timed one): {injected['q2_cancels']} wrong-side cancels"
+             + ("" if injected["q6_oid"] is None else ", one zero-volume ADD"))
     if use_pg:
         dist.barrier()
     if pub is not None:

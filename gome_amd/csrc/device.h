@@ -98,6 +98,9 @@ enum {
   C_HEAD_ADD,                                             // the hottest book went through an ADD plan
   C_EARLY, C_EARLY_MISS,                                  // its plan was the early one / could not be (match_early.h)
   C_ADM_AHEAD, C_ADM_REDO,                                // admission ran ahead / ran again (k_adm_verify)
+  C_FLOW_STALE, C_FLOW_BAIL,                              // head books planned with stale members (Q2) /
+                                                          // handed to the legacy kernel after their plan
+  C_FLOW_ZERO,                                            // head books planned with zero-volume ADDs (Q6)
   C_NCTR = 32
 };
 

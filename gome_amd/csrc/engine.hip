@@ -1172,7 +1172,7 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   // k_flow_count).
   // pl: the hottest book (a wave per level of a deep book with DELs)
   auto head_recon = [&](const FlowArgs& R, uint32_t nb, hipStream_t st, hipStream_t cs, bool fused,
-                        bool pl) -> gome_status {
+                        bool pl, bool hand_wait) -> gome_status {
     const bool split = cs != st;
     if (split) {  // the deep books' level sort (other books than the ones below) beside it
       HIPCHK(hipEventRecord(dp_fork, st));
@@ -1183,6 +1183,17 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
     k_flow_sort_cnt<<<dim3(FL_SORT_GRID, nb), FL_TILE, 0, st>>>(D, R);
     k_flow_sort_scan<<<nb, FL_CAP * FL_SCAN_P, 0, st>>>(D, R);
     k_flow_sort_scatter<<<dim3(FL_SORT_GRID, nb), FL_TILE, 0, st>>>(D, R);
+    // books planned with stale members (Q2) or zero-volume ADDs (Q6): an order that rested on the
+    // other side of a stale price, or a zero-volume maker, hands its book to the legacy kernel
+    // (k_flow_zero_check, k_flow_stale_check), on this stream, before any of the book is written;
+    // for the hottest book after the hot stream's main legacy launch and its index inserts
+    // (hand_wait), which the near books' stream has behind it anyway
+    k_flow_zero_check<<<dim3(64, nb), 256, 0, st>>>(D, R);
+    k_flow_stale_check<<<nb, FL_CAP, 0, st>>>(D, B, R);
+    if (hand_wait) HIPCHK(hipStreamWaitEvent(st, oidmax_done, 0));
+    k_match_hot<<<R.h0 + nb, 64, HOT_LDS_BYTES, st>>>(D, B, d_pend, d_resume, F.hdr, 1u, R.h0, R.h0 + nb);
+    k_match_resume<<<R.h0 + nb, 64, 0, st>>>(D, B, d_resume, F.hdr, R.h0, R.h0 + nb);
+    k_pend_apply<<<dim3(8, R.h0 + nb), 256, 0, st>>>(D, d_pend, S.seg_start, S.seg_order, B, F.hdr, R.h0, R.h0 + nb);
     if (!split && c_deep) deep_sort_level(R, FL_SORT_GRID, st, pl);
     k_flow_level_wide<<<dim3(FL_CAP, nb), FL_LVB_T, 0, st>>>(D, R);
     toff(R, false, st);
@@ -1284,7 +1295,7 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   }
   HIPCHK(hipStreamWaitEvent(hot_stream, fork, 0));  // (their reconstruction reads k_prep's records)
   if (nh_near) {
-    if (head_recon(FH1, nh_near, hot_stream, hot_stream, true, false) != GOME_OK) return GOME_E_DEVICE;
+    if (head_recon(FH1, nh_near, hot_stream, hot_stream, true, false, false) != GOME_OK) return GOME_E_DEVICE;
     if (head_recon_c(FH1, FH1c, nh_near, hot_stream, false) != GOME_OK) return GOME_E_DEVICE;
     k_flow_events_fused<<<1024, FL_EV_T, 0, hot_stream>>>(D, B, FH1);
     HIPCHK(mark(GOME_PH_NEAR, 1, hot_stream));
@@ -1308,7 +1319,7 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   HIPCHK(hipEventRecord(join, hot_stream));
   // (the hot stream's own work ended long before the hottest book's plan does)
   HIPCHK(mark(GOME_PH_HEAD_RECON, 0, flow_stream));
-  if (head_recon(FH0, 1, flow_stream, hot_stream, false, true) != GOME_OK) return GOME_E_DEVICE;
+  if (head_recon(FH0, 1, flow_stream, hot_stream, false, true, true) != GOME_OK) return GOME_E_DEVICE;
   if (head_recon_c(FH0, FH0c, 1, flow_stream, true) != GOME_OK) return GOME_E_DEVICE;
   HIPCHK(mark(GOME_PH_HEAD_RECON, 1, flow_stream));
   HIPCHK(hipEventRecord(joinf, flow_stream));
@@ -1371,6 +1382,8 @@ gome_status gome_engine::finish(uint32_t sl, uint32_t n) {
   stats.n_early_miss = st.ctr[C_EARLY_MISS];
   stats.n_adm_ahead = st.ctr[C_ADM_AHEAD];
   stats.n_adm_redo = st.ctr[C_ADM_REDO];
+  stats.n_flow_stale = st.ctr[C_FLOW_STALE];
+  stats.n_flow_bail = st.ctr[C_FLOW_BAIL];
   stats.ms_hot = ms_hot;
   stats.ms_flow_plan = ms_flow;
   stats.n_flow_books = st.ctr[C_FLOW_BOOKS];

@@ -140,6 +140,10 @@ struct FlowHdr {
   uint32_t dv_ba;      // W32DV: the best ask after the plan (asks lie at or above it)
   uint32_t pre;        // planned early (match_early.h): k_flow_plan_head leaves the book alone
   uint32_t bid;        // the batch whose prep wrote the header (FlowArgs::bid)
+  uint32_t nstale;     // stale side-set members in the level table (Q2, k_flow_stale_check)
+  uint32_t bail;       // set with ok = 0 by k_flow_stale_check: the legacy kernel applies the book
+  uint32_t nzero;      // admitted zero-volume ADDs of the segment (Q6, k_flow_zero_check)
+  uint32_t haz;        // k_flow_zero_check: one of them rested (a zero-volume maker): hand over
 };
 // FlowHdr::ok: 0 declined, FL_OK_ADD an ADD-only flow book, FL_OK_CANCEL a book with DELs,
 // FL_OK_DEEP an ADD-only head book with more levels than the lane plans hold (match_flow_deep.h)
@@ -184,6 +188,11 @@ struct FlowLvl {
   uint32_t pad3;
 };
 static_assert(sizeof(FlowLvl) % 16 == 0, "FlowLvl alignment");
+
+// A level that is a stale member at batch start (Q2: one side's set, no FIFO, depth 0; k_flow_prep_b).
+__device__ __forceinline__ bool fl_stale0(const FlowLvl& f) {
+  return f.old != NIL && f.nv0 == 0 && f.d0 == 0 && (f.mem0 == M_BUY || f.mem0 == M_SALE);
+}
 
 constexpr uint32_t FC_TOFF = MAX_FLOW + 16;  // second toff region for books with DELs
 constexpr uint32_t FC_GEN_MASK = 0x7FF;   // generation bits of an FcHash key
@@ -305,7 +314,7 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep(Dev D, BatchArgs B, Flo
   const uint32_t beg = B.seg_start[seg], end = B.seg_start[seg + 1];
   const uint32_t sym = B.ord[B.prep[beg].idx].symbol_id;
   if (D.st->err & ERR_INPUT) {  // (the batch is rejected; sym may be out of range)
-    if (tid == 0) { hd->ok = 0; hd->deep = 0; }
+    if (tid == 0) { hd->ok = 0; hd->deep = 0; hd->bail = 0; }
     return;
   }
   const Book bk = D.books[sym];
@@ -464,7 +473,7 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep(Dev D, BatchArgs B, Flo
   const bool w32 = sum < FL_SUM_CAP && sum / g < (dels ? (1ull << 31) : (1ull << 32));
   if (!w32) g = 1;
   if (dels && !w32) {  // the cancel plan is 32-bit only
-    if (tid == 0) { hd->ok = 0; hd->deep = 0; }
+    if (tid == 0) { hd->ok = 0; hd->deep = 0; hd->bail = 0; }
     return;
   }
   if (tid < ((8u - ((end - beg) & 7u)) & 7u))  // padding to whole half-groups (8 records)
@@ -530,6 +539,7 @@ struct FlPrepScr {
   unsigned long long pg[FL_PG], ps[FL_PG];  // per-slice gcd and saturated sum of volumes
   uint32_t adds, dropped, bad, dels;
   uint32_t many;       // more distinct prices than the lane plans hold: a deep-book candidate
+  uint32_t zeros;      // admitted zero-volume ADDs (Q6): k_flow_prep_b takes them on long head books
   // the deep prep's own totals (match_flow_deep.h)
   uint32_t d_adds, d_dropped, d_dels, d_bad, d_ndist;
   // a deep tail book's chunk ids for its FIFO appends, claimed once for all its levels
@@ -643,7 +653,7 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep_a(Dev D, BatchArgs B, F
   if (tid == 0) ndist = bad = adds = dropped = dels = many = 0;
   __syncthreads();
   unsigned long long mg = 0, msum = 0;
-  uint32_t my_adds = 0, my_drop = 0, my_bad = 0, my_dels = 0, my_many = 0;
+  uint32_t my_adds = 0, my_drop = 0, my_bad = 0, my_dels = 0, my_many = 0, my_zero = 0;
   // (every thread stops once the block's distinct prices overflowed: a deep candidate, whose
   // own prep starts over)
   for (uint32_t c0 = b0 + tid; c0 < b1 && !my_bad && !my_many && *reinterpret_cast<volatile uint32_t*>(&ndist) <= FL_MAX;
@@ -662,7 +672,8 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep_a(Dev D, BatchArgs B, F
       if (q.action != GOME_ADD) continue;
       my_adds++;
       if (!q.adm) { my_drop++; continue; }
-      if (q.vol == 0 || q.adm == ADM_V_CHECK) { my_bad = 1; break; }  // (Q6; Q7 candidates: serial kernels)
+      if (q.adm == ADM_V_CHECK) { my_bad = 1; break; }  // (Q7 candidates: serial kernels)
+      my_zero += q.vol == 0 ? 1u : 0u;  // (Q6: k_flow_prep_b decides; gcd(g, 0) = g, the sum unchanged)
       const unsigned long long v = static_cast<unsigned long long>(q.vol);
       const double qd = static_cast<double>(v) / static_cast<double>(mg ? mg : 1);
       if (mg == 0 || static_cast<unsigned long long>(qd) * mg != v) mg = fl_gcd(mg, v);
@@ -675,6 +686,7 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep_a(Dev D, BatchArgs B, F
   if (my_adds) atomicAdd(&adds, my_adds);
   if (my_drop) atomicAdd(&dropped, my_drop);
   if (my_dels) atomicAdd(&dels, my_dels);
+  if (my_zero) atomicAdd(&P->zeros, my_zero);
   if (my_bad) bad = 1;
   if (my_many) many = 1;
   fl_block_gcd_sum(mg, msum, wg, ws);  // (synchronises the block)
@@ -701,7 +713,7 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep_b(Dev D, BatchArgs B, F
   __shared__ uint32_t hval[FL_HASH];
   __shared__ unsigned long long ckey[FL_CAP + FL_PREP_T];
   __shared__ uint32_t cslot[FL_CAP + FL_PREP_T];
-  __shared__ uint32_t ndist, nc, bad, deepc;
+  __shared__ uint32_t ndist, nc, bad, deepc, nstale;
   __shared__ unsigned long long wg[FL_PREP_T / 64], ws[FL_PREP_T / 64];
   const uint32_t hb = blockIdx.x, h = F.h0 + hb, tid = threadIdx.x;
   if (h >= fl_hend(D, F)) return;
@@ -711,13 +723,28 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep_b(Dev D, BatchArgs B, F
   const uint32_t beg = B.seg_start[seg], end = B.seg_start[seg + 1];
   const uint32_t sym = B.ord[B.sidx[beg]].symbol_id;
   if (D.st->err & ERR_INPUT) {  // (the batch is rejected; sym may be out of range)
-    if (tid == 0) { hd->ok = 0; hd->deep = 0; }
+    if (tid == 0) { hd->ok = 0; hd->deep = 0; hd->bail = 0; }
     return;
   }
   const Book bk = D.books[sym];
+  // Stale side-set members (Q2): a wrong-side cancel that empties a level ZREMs the
+  // request's side set, so the level stays in its true side's set with no FIFO and depth 0.  A
+  // taker that reaches it in the reference finds no node and moves on (MatchOrder returns at an
+  // empty FIFO, engine.go:139-142), and a same-side rest there is an ordinary rest: the plans,
+  // which see a depth of 0 as "no level", are exact for both.  Only an order resting on the OTHER
+  // side at that price is not (the level would be a member of both sets), which
+  // k_flow_stale_check finds after the plan: the book then goes to the legacy kernel
+  // (k_match_hot mode 1).  Head books of at least LEGACY_HOT_MIN orders without DELs only (the
+  // cold kernel never takes such a book, so a late hand-over cannot race with it).
+  // Zero-volume ADDs (Q6) under the same conditions: one that crosses takes 0 at the best opposite
+  // level, the reference's one 0-fill with the maker unchanged (engine.go:176-194), which the plans
+  // log as a CONS touch of 0; one that rests leaves a zero-volume maker in the FIFO, which the
+  // reconstruction does not model: k_flow_zero_check finds its REST of 0 and hands the book over.
+  const bool stale_ok = (end - beg) >= LEGACY_HOT_MIN && P->dels == 0;
   if (tid == 0) {
-    ndist = nc = 0;
+    ndist = nc = nstale = 0;
     const bool base_bad = !F.enabled || P->bad || (bk.pad & BOOK_QUIRK) || (D.st->err & ERR_INPUT) ||
+                          (P->zeros && !stale_ok) ||
                           (end - beg) >= FL_MAX_ORDERS;
     const bool many = P->many || bk.n_lvl > FL_MAX;
     // more levels than lanes: the deep plan's candidate (match_flow_deep.h re-checks the rest)
@@ -730,6 +757,7 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep_b(Dev D, BatchArgs B, F
   if (bad) {
     if (tid == 0) {
       hd->ok = 0;
+      hd->bail = 0;
       hd->deep = deepc;
       hd->dslot = h;
       if (deepc) F.dslot_h[h] = h;
@@ -755,12 +783,17 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep_b(Dev D, BatchArgs B, F
     const Level x = L0[k];
     const uint32_t nm = (x.member & M_BUY ? 1u : 0u) + (x.member & M_SALE ? 1u : 0u);
     if (x.nlive == 0) {
-      if (x.depth != 0 || x.member != 0) bad = 1;
-      continue;
+      const bool stale = stale_ok && x.depth == 0 && nm == 1 && x.head == NIL;
+      if (!stale) {
+        if (x.depth != 0 || x.member != 0) bad = 1;
+        continue;
+      }
+      atomicAdd(&nstale, 1u);  // (in the table, so a rest at its price lands in this level)
+    } else {
+      if (x.depth <= 0 || nm != 1) { bad = 1; continue; }
+      mg = fl_gcd(mg, static_cast<unsigned long long>(x.depth));
+      msum = min(msum + static_cast<unsigned long long>(x.depth), FL_SUM_CAP);
     }
-    if (x.depth <= 0 || nm != 1) { bad = 1; continue; }
-    mg = fl_gcd(mg, static_cast<unsigned long long>(x.depth));
-    msum = min(msum + static_cast<unsigned long long>(x.depth), FL_SUM_CAP);
     bool fresh;
     const uint32_t sl = fl_set_put(hkey, static_cast<unsigned long long>(x.price) + FL_KEY_OFF, &fresh);
     if (sl == FL_HASH) { bad = 1; continue; }
@@ -771,6 +804,7 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep_b(Dev D, BatchArgs B, F
   if (bad || ndist > FL_MAX) {
     if (tid == 0) {
       hd->ok = 0;
+      hd->bail = 0;
       hd->deep = (!bad && ndist <= DEEP_CAP - 2) ? 1u : 0u;
       if (hd->deep) ctr_add(D, C_WANT_DEEP, 1ull);
       if (!(F.chains & FL_CH_DEEP)) hd->deep = 0;
@@ -823,7 +857,7 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep_b(Dev D, BatchArgs B, F
   const bool w32 = msum < FL_SUM_CAP && msum / g < (dels ? (1ull << 31) : (1ull << 32));
   if (!w32) g = 1;
   if (dels && !w32) {  // the cancel plan is 32-bit only
-    if (tid == 0) { hd->ok = 0; hd->deep = 0; }
+    if (tid == 0) { hd->ok = 0; hd->deep = 0; hd->bail = 0; }
     return;
   }
   const uint32_t obase = fl_obase(beg, seg);
@@ -845,6 +879,10 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep_b(Dev D, BatchArgs B, F
     x.g = g;
     x.ndel = dels;
     x.bid = F.bid;
+    x.nstale = nstale;
+    x.nzero = P->zeros;
+    if (nstale) ctr_add(D, C_FLOW_STALE, 1ull);
+    if (x.nzero) ctr_add(D, C_FLOW_ZERO, 1ull);
     *hd = x;
   }
 }
@@ -1445,14 +1483,14 @@ __device__ __forceinline__ int64_t fl_blk_excl(int64_t x, int64_t* total) {
 // fl_level_one's touch scan with a whole block (FL_LVB_T threads) on one level: the level's
 // touches in block-wide chunks (the hottest book's levels hold thousands of touches).
 __device__ __forceinline__ void fl_level_scan_blk(const FlowArgs& F, uint32_t h, uint32_t q, int64_t& cfin,
-                                                  uint32_t& nr) {
+                                                  uint32_t& nr, uint32_t* ncons = nullptr) {
   const FlowHdr* hd = &F.hdr[h];
   FlowLvl* Lq = fl_lvls(F, h) + q;
   const uint32_t L = FL_TOUCH_MUL * hd->beg, base = Lq->base, cnt = Lq->cnt;
   SEnt* R = F.srt + L + base;
   RsEnt* RS = F.rs + L + base;
   int64_t cc = 0, rr = Lq->d0;
-  uint32_t n = 0;
+  uint32_t n = 0, nc = 0;
   for (uint32_t c0 = 0; c0 < cnt; c0 += FL_LVB_T) {
     const uint32_t i = c0 + threadIdx.x;
     const bool valid = i < cnt;
@@ -1463,6 +1501,7 @@ __device__ __forceinline__ void fl_level_scan_blk(const FlowArgs& F, uint32_t h,
     const int64_t xc = fl_blk_excl(isc ? e.amt : 0, &tc);
     const int64_t xr = fl_blk_excl(isr ? e.amt : 0, &tr);
     const int64_t xn = fl_blk_excl(isr ? 1 : 0, &tn);
+    nc += static_cast<uint32_t>(__syncthreads_count(isc));
     if (isc) R[i].coord = cc + xc;
     if (isr) {
       const int64_t e0 = rr + xr;
@@ -1481,6 +1520,7 @@ __device__ __forceinline__ void fl_level_scan_blk(const FlowArgs& F, uint32_t h,
   }
   cfin = cc;
   nr = n;
+  if (ncons) *ncons = nc;
 }
 
 // ============================================================== events of one touch
@@ -1557,7 +1597,8 @@ __device__ __forceinline__ void fl_level_fc(const FlowArgs& F, uint32_t L, uint3
     const bool cons = i < cnt && e.kind == TK_CONS;
     const unsigned long long cm = __ballot(cons);
     if (!cm) continue;
-    const int64_t x = e.coord + e.amt - 1;
+    // (a CONS of 0, a zero-volume taker (Q6): the one maker at its cursor, MatchVolume 0)
+    const int64_t x = e.coord + (e.amt ? e.amt : 1) - 1;
     const int l0 = static_cast<int>(__builtin_ctzll(cm)), l1 = 63 - static_cast<int>(__builtin_clzll(cm));
     const uint32_t b = nw == 1 ? carry : fl_find(IG, ig_n, RS, nrest, d0, __shfl(e.coord, l0));
     const uint32_t f = fl_wave_find(IG, ig_n, RS, nrest, d0, cons, e.coord, b);
@@ -1594,7 +1635,7 @@ __device__ __forceinline__ void fl_freed_flush(const Dev& D, FlFreed* stg) {
 __device__ __forceinline__ void fl_level_one(const Dev& D, const FlowArgs& F, uint32_t h, uint32_t q,
                                              uint32_t run_base = NIL, uint32_t run_cnt = 0,
                                              uint32_t ig_pre = NIL, int64_t pre_cfin = -1, uint32_t pre_nr = 0,
-                                             bool fc_here = true, FlFreed* stg = nullptr) {
+                                             bool fc_here = true, FlFreed* stg = nullptr, bool gather0 = false) {
   const FlowHdr* hd = &F.hdr[h];
   const uint32_t lane = lane_id();
   FlowLvl* Lq = fl_lvls(F, h) + q;
@@ -1653,7 +1694,8 @@ __device__ __forceinline__ void fl_level_one(const Dev& D, const FlowArgs& F, ui
   uint32_t hslot = uni(Lq->hslot), tslot = uni(Lq->tslot);
   uint32_t ig_base = 0, ng = 0, consumed = 0;
   bool have_extra = false;
-  if (nv0 > 0 && cfin > 0) {
+  // (gather0: a CONS of 0 reads the maker at the cursor even when nothing was consumed)
+  if (nv0 > 0 && (cfin > 0 || gather0)) {
     uint32_t b = ig_pre;
     if (ig_pre == NIL) {
       if (lane == 0) b = atomicAdd(F.ig_bump, nv0);
@@ -1770,7 +1812,7 @@ __device__ __forceinline__ void fl_level_one(const Dev& D, const FlowArgs& F, ui
       rr += rl64(ir, 63);
       if (cm) {  // (a consume fills makers that rested before it: up to this chunk's, written above)
         __threadfence_block();
-        const int64_t c = c1 + ic - ac, x = c + ac - 1;
+        const int64_t c = c1 + ic - ac, x = c + (ac ? ac : 1) - 1;  // (a CONS of 0: fl_level_fc)
         const int l0 = static_cast<int>(__builtin_ctzll(cm)), l1 = 63 - static_cast<int>(__builtin_clzll(cm));
         const uint32_t f = fl_wave_find(IG, ng, RS, nr, d0, isc, c, carry);
         const uint32_t l = fl_wave_find(IG, ng, RS, nr, d0, isc, x, __shfl(f, l0));
@@ -2407,7 +2449,7 @@ __device__ __forceinline__ void fl_write_finish(const Dev& D, const FlowHdr& hd,
   if (threadIdx.x == 0) {
     uint32_t c = 0;
     for (uint32_t q = 1; q <= hd.nl; ++q) {
-      const uint32_t k = lv[q].nlive > 0 ? 1u : 0u;
+      const uint32_t k = (lv[q].nlive > 0 || lv[q].member != 0) ? 1u : 0u;  // (member, no node: stale)
       keep[q] = k ? c : NIL;
       c += k;
     }
@@ -2723,6 +2765,9 @@ __global__ __launch_bounds__(FL_LVB_T) void k_flow_write_lv_blk(Dev D, BatchArgs
   uint32_t mem = 0;
   if (((q < 64 ? hd.amask[0] : hd.amask[1]) >> (q & 63)) & 1ull) mem |= M_SALE;
   if (((q < 64 ? hd.bmask[0] : hd.bmask[1]) >> (q & 63)) & 1ull) mem |= M_BUY;
+  // a stale member no order touched stays one (a touch of it heals or, k_flow_stale_check, bails)
+  const bool stale = fl_stale0(f) && f.cnt == 0;
+  if (stale) mem = f.mem0;
   x.member = static_cast<uint8_t>(mem);
   if (x.nlive == 0) {
     x.hslot = x.tslot = 0;
@@ -2737,9 +2782,11 @@ __global__ __launch_bounds__(FL_LVB_T) void k_flow_write_lv_blk(Dev D, BatchArgs
     x.tail = need ? chunk_id(need - 1) : f.tail;
     x.tslot = static_cast<uint8_t>(need ? (S - room) - (need - 1) * CH : s0 + S);
   }
-  // clean-book invariant: nodes <=> positive depth <=> one side-set membership
-  const bool ok = (x.nlive > 0) == (x.depth > 0) && (x.nlive > 0) == (mem == M_BUY || mem == M_SALE) &&
-                  (x.nlive > 0 || mem == 0);
+  // clean-book invariant: nodes <=> positive depth <=> one side-set membership (or an untouched
+  // stale member: no nodes, depth 0, one side)
+  const bool ok = stale ? (x.nlive == 0 && x.depth == 0)
+                        : (x.nlive > 0) == (x.depth > 0) && (x.nlive > 0) == (mem == M_BUY || mem == M_SALE) &&
+                              (x.nlive > 0 || mem == 0);
   if (!ok) atomicOr(&D.st->err, ERR_CORRUPT);
   F.lvout[h * FL_CAP + q] = x;
 }
@@ -2925,17 +2972,68 @@ __global__ __launch_bounds__(FL_TILE) void k_flow_sort_scatter(Dev D, FlowArgs F
   }
 }
 
+// Books planned with zero-volume ADDs (Q6, k_flow_prep_b): a REST touch of 0 at a real level (the
+// no-op records rest 0 at the sentinel level 0) is a zero-volume maker; FlowHdr::haz hands the book
+// over (k_flow_stale_check).  Grid-stride over the book's log, only for such books.
+__global__ __launch_bounds__(256) void k_flow_zero_check(Dev D, FlowArgs F) {
+  const uint32_t h = F.h0 + blockIdx.y;
+  if (h >= fl_hend(D, F)) return;
+  FlowHdr* hd = &F.hdr[h];
+  if (hd->ok != FL_OK_ADD || hd->nzero == 0) return;
+  const uint32_t nt = hd->ntouch, L = FL_TOUCH_MUL * hd->beg;
+  bool z = false;
+  for (uint32_t t = blockIdx.x * 256 + threadIdx.x; t < nt; t += gridDim.x * 256) {
+    const Touch x = F.log[L + t];
+    z = z || (((x.kr >> 7) & 1u) == TK_REST && x.amt == 0 && (x.kr & 127u) != 0);
+  }
+  if (__any(z) && lane_id() == 0) atomicOr(&hd->haz, 1u);
+}
+
+// After the head's level sort: a book planned with stale members is exact unless an order rested
+// at a stale price on the side opposite its membership before a same-side rest healed it (the
+// reference would then hold the price in both side sets, and a later taker of the resting side
+// could meet its own side's maker there: SURVEY Appendix A Q2).  The plan never consumes at a
+// stale level before a rest there (its depth is 0), so the first touch of the level's run, in time
+// order, decides.  Such a book is handed to the legacy kernel: bail, then ok = 0, so every later
+// flow kernel skips it and k_match_hot (mode 1) applies it from its unchanged state (nothing of the
+// book has been written yet: the plan and the sort write scratch only).  One thread per level.
+__global__ __launch_bounds__(FL_CAP) void k_flow_stale_check(Dev D, BatchArgs B, FlowArgs F) {
+  __shared__ uint32_t haz;
+  const uint32_t h = F.h0 + blockIdx.x, q = threadIdx.x;
+  if (h >= fl_hend(D, F)) return;
+  FlowHdr* hd = &F.hdr[h];
+  if (hd->ok != FL_OK_ADD || (hd->nstale == 0 && hd->haz == 0)) return;
+  if (q == 0) haz = hd->haz;
+  __syncthreads();
+  if (q >= 1 && q <= hd->nl) {
+    const FlowLvl f = F.lvl[h * FL_CAP + q];
+    if (fl_stale0(f) && f.cnt) {
+      const SEnt e = F.srt[FL_TOUCH_MUL * hd->beg + f.base];
+      const bool sale = B.prep[hd->beg + e.j].side == GOME_SALE;
+      if (e.kind != TK_REST || sale != (f.mem0 == M_SALE)) atomicOr(&haz, 1u);
+    }
+  }
+  __syncthreads();
+  if (q == 0 && haz) {
+    __hip_atomic_store(&hd->bail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __threadfence();
+    __hip_atomic_store(&hd->ok, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    ctr_add(D, C_FLOW_BAIL, 1ull);
+  }
+}
+
 __global__ __launch_bounds__(FL_LVB_T) void k_flow_level_wide(Dev D, FlowArgs F) {
   const uint32_t h = F.h0 + blockIdx.y, q = blockIdx.x;
   if (h >= fl_hend(D, F) || F.hdr[h].ok != FL_OK_ADD) return;
   if (q == 0 || q > F.hdr[h].nl) return;
   int64_t cfin;
-  uint32_t nr;
-  fl_level_scan_blk(F, h, q, cfin, nr);
-  if (threadIdx.x < 64) fl_level_one(D, F, h, q, NIL, 0, NIL, cfin, nr, false);
+  uint32_t nr, ncons;
+  fl_level_scan_blk(F, h, q, cfin, nr, &ncons);
+  const bool z0 = cfin == 0 && ncons > 0;  // (only CONS touches of 0: zero-volume takers, Q6)
+  if (threadIdx.x < 64) fl_level_one(D, F, h, q, NIL, 0, NIL, cfin, nr, false, nullptr, z0);
   __syncthreads();  // (wave 0's level record, then the whole block searches)
   const FlowLvl* Lq = F.lvl + h * FL_CAP + q;
-  if (cfin > 0)
+  if (cfin > 0 || z0)
     fl_level_fc(F, FL_TOUCH_MUL * F.hdr[h].beg, q, Lq->base, Lq->cnt, F.ig + Lq->ig_base, Lq->ig_n, Lq->nrest, Lq->d0,
                 threadIdx.x >> 6, FL_LVB_T / 64);
 }

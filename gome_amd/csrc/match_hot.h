@@ -1135,12 +1135,25 @@ __device__ __forceinline__ void hot_resolve_pending(HotCtx& H) {
   for (uint32_t i = lane_id(); i < H.npend; i += 64) H.pend[i].used = 0;
 }
 
+// A head book the flow path planned and then handed over (FlowHdr::bail, k_flow_stale_check): the
+// check stores bail, then ok = 0 (release), so a reader that sees ok == 0 from it sees bail too.
+__device__ __forceinline__ bool hot_bailed(const FlowHdr* flow, uint32_t h, bool* ok) {
+  *ok = __hip_atomic_load(const_cast<uint32_t*>(&flow[h].ok), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != 0;
+  return !*ok && __hip_atomic_load(const_cast<uint32_t*>(&flow[h].bail), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+}
+
+// mode 0: the candidates the flow path declined at its prep (the main launch); mode 1: the books of
+// candidates [h0, h1) it handed over after their plan (bail), on the stream of their reconstruction.
 __global__ __launch_bounds__(64) void k_match_hot(Dev D, BatchArgs B, PendEnt* pend_arena,
-                                                   ResumeRec* resume, const FlowHdr* flow) {
+                                                   ResumeRec* resume, const FlowHdr* flow, uint32_t mode = 0,
+                                                   uint32_t h0 = 0, uint32_t h1 = 0) {
   extern __shared__ __align__(16) unsigned char smem[];
   if (blockIdx.x >= D.st->nhot || (D.st->err & ERR_INPUT)) return;
-  if (flow[blockIdx.x].ok ||  // applied by the flow path (match_flow.h)
-      B.seg_start[B.seg_order[blockIdx.x] + 1] - B.seg_start[B.seg_order[blockIdx.x]] < LEGACY_HOT_MIN) {
+  bool fok;
+  const bool bailed = hot_bailed(flow, blockIdx.x, &fok);
+  if (mode == 1 && (blockIdx.x < h0 || blockIdx.x >= h1 || !bailed)) return;
+  if (mode == 0 && (fok || bailed ||  // applied by the flow path (match_flow.h), or handed over later
+      B.seg_start[B.seg_order[blockIdx.x] + 1] - B.seg_start[B.seg_order[blockIdx.x]] < LEGACY_HOT_MIN)) {
     if (lane_id() == 0) resume[blockIdx.x].valid = 0;  // declined and short: the cold kernel
     return;
   }
@@ -1357,8 +1370,14 @@ __global__ __launch_bounds__(64) void k_match_hot(Dev D, BatchArgs B, PendEnt* p
 }
 
 // Continue hot books that left the lane path (see ResumeRec) on the HBM path.
-__global__ __launch_bounds__(64) void k_match_resume(Dev D, BatchArgs B, const ResumeRec* resume) {
+__global__ __launch_bounds__(64) void k_match_resume(Dev D, BatchArgs B, const ResumeRec* resume,
+                                                      const FlowHdr* flow = nullptr, uint32_t h0 = 0,
+                                                      uint32_t h1 = 0) {
   if (blockIdx.x >= D.st->nhot || (D.st->err & ERR_INPUT)) return;
+  if (flow) {  // (mode 1: the handed-over books of [h0, h1) only)
+    bool fok;
+    if (blockIdx.x < h0 || blockIdx.x >= h1 || !hot_bailed(flow, blockIdx.x, &fok)) return;
+  }
   const ResumeRec rr = resume[blockIdx.x];
   if (!rr.valid) return;
   const uint32_t seg = B.seg_order[blockIdx.x];
@@ -1374,10 +1393,13 @@ __global__ __launch_bounds__(64) void k_match_resume(Dev D, BatchArgs B, const R
 // entry that is still live and was not flushed in-kernel, and store the node's real index
 // slot into its chunk (HBM; the kernel has written its LDS caches back).
 __global__ void k_pend_apply(const Dev D, PendEnt* pend, const uint32_t* seg_start,
-                             const uint32_t* seg_order, const BatchArgs B) {
+                             const uint32_t* seg_order, const BatchArgs B, const FlowHdr* flow = nullptr,
+                             uint32_t h0 = 0, uint32_t h1 = 0) {
   const uint32_t nhot = min(D.st->nhot, MAX_HOT);
   const unsigned long long mask = D.idx_mask;
   for (uint32_t h = blockIdx.y; h < nhot; h += gridDim.y) {
+    bool fok;
+    if (flow && (h < h0 || h >= h1 || !hot_bailed(flow, h, &fok))) continue;  // (mode 1)
     const uint32_t seg = seg_order[h];
     const uint32_t beg = seg_start[seg], end = seg_start[seg + 1];
     const uint32_t sym = B.ord[B.prep[beg].idx].symbol_id;

@@ -23,9 +23,10 @@
 namespace gome {
 
 // The flow plans' precondition on one book (a whole wave, wave-uniform result):
-//  * every level in S:BUY or S:SALE is in exactly one of them, has live FIFO nodes and depth > 0;
-//    every other level has no node and depth 0 (nothing observable a sweep could meet);
-//  * every bid lies below every ask (levels are sorted by price);
+//  * every level in S:BUY or S:SALE is in exactly one of them, has live FIFO nodes and depth > 0,
+//    or is a stale member (Q2: no node, depth 0: the head books' lane plans take it, k_flow_prep_b,
+//    every other prep declines it); every other level has no node and depth 0;
+//  * every bid lies below every ask (levels are sorted by price; stale members aside);
 //  * every live node of a member level has a positive remaining volume (no Q6 maker) and the
 //    level's side, and the level's FIFO holds exactly nlive nodes summing to its depth.
 // The level checks come first: a book that is still stale fails them without a FIFO walk.
@@ -41,10 +42,11 @@ __device__ __forceinline__ bool book_requalifies(const Dev& D, uint32_t sym) {
     bool bad = false, bid = false, ask = false;
     if (k < nl) {
       const Level x = L[k];
-      bid = x.member == M_BUY;
-      ask = x.member == M_SALE;
+      const bool stale = x.member && x.member != (M_BUY | M_SALE) && x.nlive == 0 && x.depth == 0 && x.head == NIL;
+      bid = x.member == M_BUY && !stale;
+      ask = x.member == M_SALE && !stale;
       if (x.member == (M_BUY | M_SALE)) bad = true;
-      else if (x.member) bad = x.nlive == 0 || x.depth <= 0 || x.head == NIL;
+      else if (x.member) bad = !stale && (x.nlive == 0 || x.depth <= 0 || x.head == NIL);
       else bad = x.nlive != 0 || x.depth != 0 || x.head != NIL;
     }
     if (__ballot(bad)) return false;
@@ -55,7 +57,7 @@ __device__ __forceinline__ bool book_requalifies(const Dev& D, uint32_t sym) {
   if (last_bid >= 0 && first_ask != NIL && static_cast<uint32_t>(last_bid) > first_ask) return false;
   for (uint32_t k = 0; k < nl; ++k) {
     const Level x = L[k];
-    if (!x.member) continue;
+    if (!x.member || x.head == NIL) continue;  // (a stale member: checked above)
     const bool sale = x.member == M_SALE;
     uint32_t c = uni(x.head), s0 = uni(x.hslot), cnt = 0;
     const uint32_t tail = uni(x.tail), tslot = uni(x.tslot);

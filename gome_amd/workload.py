@@ -247,15 +247,17 @@ def inject_quirks(rec: np.ndarray, sym: int, levels: np.ndarray, fifo, mode: str
         as a zero-volume maker behind that level's FIFO (engine.go:69-82).
     mode "heal": the Q2 level is the best bid and the Q6 level the second best, where the stream
     soon rests and consumes again (the reference's state heals); mode "stuck": the Q2 level is
-    the lowest bid, which the stream never reaches again (the quirk stays).  `levels` / `fifo`
+    the lowest bid, which the stream never reaches again (the quirk stays).  Modes "q2heal" /
+    "q2stuck": the same wrong-side cancels without the zero-volume ADD.  `levels` / `fifo`
     are the book's state before `rec` (gome_snapshot_levels / gome_snapshot_fifo, or the
     oracle's).  Returns what was injected."""
     bids = levels[(levels["in_buy"] != 0) & (levels["in_sale"] == 0) & (levels["n_nodes"] > 0)]
     if len(bids) < 3:
         raise ValueError("book has fewer than three bid levels")
     bids = np.sort(bids, order="price_fx")
-    q2 = bids[-1] if mode == "heal" else bids[0]
-    q6 = bids[-2] if mode == "heal" else bids[1]
+    heal = mode in ("heal", "q2heal")
+    q2 = bids[-1] if heal else bids[0]
+    q6 = bids[-2] if heal else bids[1]
     makers = fifo(int(q2["price_fx"]))
     pos = np.nonzero((rec["symbol_id"] == sym) & (rec["action"] == ADD))[0]
     if len(pos) < len(makers) + 1:
@@ -266,6 +268,9 @@ def inject_quirks(rec: np.ndarray, sym: int, levels: np.ndarray, fifo, mode: str
         r["oid_id"], r["uuid_id"] = m["oid_id"], m["uuid_id"]
         r["side"] = 0 if m["side"] == 1 else 1
         r["action"], r["flags"] = DEL, 0
+    if mode.startswith("q2"):
+        return {"q2_price": int(q2["price_fx"]), "q2_cancels": len(makers), "q6_price": None,
+                "q6_oid": None, "records": [int(i) for i in pos[:len(makers)]]}
     z = rec[pos[len(makers)]]  # the zero-volume ADD keeps the record's own (fresh) oid
     z["price_fx"], z["volume_fx"], z["side"] = q6["price_fx"], 0, 0
     return {"q2_price": int(q2["price_fx"]), "q2_cancels": len(makers), "q6_price": int(q6["price_fx"]),

@@ -272,6 +272,12 @@ typedef struct gome_stats {
                                                  batches, ABI >= 10)                       */
   uint64_t n_adm_redo;                        /* ... and ran again at the batch's own time: an
                                                  ADD's key might rest (ABI >= 10)           */
+  uint64_t n_flow_stale;                      /* head books planned on the flow path with stale
+                                                 side-set members (Q2: a member level with no
+                                                 FIFO, left by a wrong-side cancel; ABI >= 11) */
+  uint64_t n_flow_bail;                       /* ... of which an order rested on the other side
+                                                 of a stale price: the book went to the legacy
+                                                 kernel after its plan (ABI >= 11)          */
 } gome_stats;
 
 typedef struct gome_engine gome_engine;

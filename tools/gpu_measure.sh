@@ -30,6 +30,23 @@ for P in $PARTS; do
     GOME_HW_QUEUES=4 timeout -k 10 400 python3 -u bench.py --workload config3 --no-cpu-baseline --consumer-msgs 0 \
       > $OUT/config3_q4_bench.jsonl 2> $OUT/config3_q4_bench.log || { tail -20 $OUT/config3_q4_bench.log; exit 9; }
     summ $OUT/config3_q4_bench.jsonl q4 ;;
+  pcie)
+    timeout -k 10 120 ./tools/pcie_duplex 256 > $OUT/pcie_duplex.json 2>&1 || { cat $OUT/pcie_duplex.json; exit 10; }
+    cat $OUT/pcie_duplex.json ;;
+  rcclab)
+    # the RCCL layout: CU-masked plan stream (plan_cus default) vs every CU shared, alternating, and
+    # the plain N=1 line (no process group) beside them
+    Q="--steps 10 --warmup 4 --no-cpu-baseline --consumer-msgs 0 --e2e-steps 0 --no-phase-pass"
+    for R in 1 2; do
+      for V in 0 -1; do
+        timeout -k 10 300 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 \
+          --master-port $((29540 + R)) bench.py --gpus 1 --force-pg --backend nccl --plan-cus $V $Q \
+          > $OUT/rccl_pc${V}_$R.jsonl 2> $OUT/rccl_pc${V}_$R.log || { tail -20 $OUT/rccl_pc${V}_$R.log; exit 11; }
+        summ $OUT/rccl_pc${V}_$R.jsonl rccl_pc$V
+      done
+      timeout -k 10 300 python3 -u bench.py $Q > $OUT/plain_$R.jsonl 2> $OUT/plain_$R.log || { tail -20 $OUT/plain_$R.log; exit 12; }
+      summ $OUT/plain_$R.jsonl plain
+    done ;;
   smoke)
     timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.txt 2>&1 || { tail -20 $OUT/smoke.txt; exit 8; }
     tail -1 $OUT/smoke.txt ;;

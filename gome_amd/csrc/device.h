@@ -65,6 +65,11 @@ struct Book {
 // such a state.  Cleared after a batch by k_requalify (match_requal.h) once the book's state
 // is again one the flow plans assume (the reference's state heals: nodepool.go:76-83).
 constexpr uint32_t BOOK_QUIRK = 1u;
+// Book::pad: the book may hold zero-volume makers (Q6), and Level::pad L_ZERO marks the levels that
+// do (k_requalify sets both; the head books' lane plans keep them, match_flow.h; any other kernel
+// that applies such a book sets BOOK_QUIRK, so k_requalify recomputes the marks after it).
+constexpr uint32_t BOOK_ZERO = 2u;
+constexpr uint8_t L_ZERO = 1u;
 
 struct IdxEnt {
   unsigned long long key;  // ((S+1) << 32) | oid ; 0 empty, ~0 tombstone
@@ -101,7 +106,7 @@ enum {
   C_FLOW_STALE, C_FLOW_BAIL,                              // head books planned with stale members (Q2) /
                                                           // handed to the legacy kernel after their plan
   C_FLOW_ZERO,                                            // head books planned with zero-volume ADDs (Q6)
-  C_NCTR = 32
+  C_NCTR = 40
 };
 
 // Level blocks (a book's sorted level array) come in power-of-two capacities 16 << c.  A
@@ -152,10 +157,10 @@ struct Dev {
 
 // The batch counters are added by thousands of waves.  Device-scope atomics on one address (or
 // one cache line) serialise -- 64k of them cost ~0.3 ms on the tail's event pass -- so the adds
-// go to one of CTR_STRIPES 256-B stripes (by workgroup) and k_ctr_fold sums the stripes into
+// go to one of CTR_STRIPES stripes (by workgroup) and k_ctr_fold sums the stripes into
 // Status::ctr at the batch's end (and zeroes them).  Counters a kernel reads back during the
 // batch (C_DUP: a list index; C_MAXSEG: atomicMax) stay on Status.
-constexpr uint32_t CTR_STRIPES = 64, CTR_STRIDE = 32;
+constexpr uint32_t CTR_STRIPES = 64, CTR_STRIDE = 48;  // (384-B stripes: three 128-B lines)
 static_assert(C_NCTR <= CTR_STRIDE, "one stripe holds every counter");
 __device__ __forceinline__ void ctr_add(const Dev& D, uint32_t c, unsigned long long v) {
   const uint32_t s = (blockIdx.x + 13u * blockIdx.y) & (CTR_STRIPES - 1);

@@ -734,6 +734,7 @@ __device__ __forceinline__ void wave_next_book(WaveCtx& W, uint32_t sym) {
   W.nl = uni(bk.n_lvl);
   W.cap = W.hcap = uni(bk.lvl_cap);
   W.flags = uni(bk.pad);
+  if (W.flags & BOOK_ZERO) W.flags |= BOOK_QUIRK;  // (its levels' L_ZERO marks: k_requalify's to redo)
   W.L = W.D.lvl + W.base;
   W.in_lds = W.lds != nullptr && W.nl <= COLD_LDS_LVLS;
   if (W.in_lds) {

@@ -143,7 +143,8 @@ struct FlowHdr {
   uint32_t nstale;     // stale side-set members in the level table (Q2, k_flow_stale_check)
   uint32_t bail;       // set with ok = 0 by k_flow_stale_check: the legacy kernel applies the book
   uint32_t nzero;      // admitted zero-volume ADDs of the segment (Q6, k_flow_zero_check)
-  uint32_t haz;        // k_flow_zero_check: one of them rested (a zero-volume maker): hand over
+  uint32_t nzlev;      // levels that may hold zero-volume makers at batch start (FlowLvl::z0)
+  uint32_t haz;        // k_flow_zero_check: a zero-volume maker the reconstruction cannot take
 };
 // FlowHdr::ok: 0 declined, FL_OK_ADD an ADD-only flow book, FL_OK_CANCEL a book with DELs,
 // FL_OK_DEEP an ADD-only head book with more levels than the lane plans hold (match_flow_deep.h)
@@ -179,7 +180,7 @@ struct FlowLvl {
   uint32_t pad0, pad1;
   // books with DELs (match_flow_cancel.h): the targets of the level's DELs
   uint32_t c_old;    // old (pre-batch) makers targeted by a DEL of the batch
-  uint32_t cring;    // (unused)
+  uint32_t z0;       // the level's FIFO may hold zero-volume makers at batch start (Level::pad L_ZERO)
   uint32_t rbase;    // (unused)
   uint32_t ocan;     // cancelled volume of old makers (plan units), set by the recon
   uint32_t memf;     // deep books: membership after the batch (M_BUY / M_SALE)
@@ -321,7 +322,7 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep(Dev D, BatchArgs B, Flo
   for (uint32_t i = tid; i < FL_HASH; i += FL_PREP_T) { hkey[i] = 0; hval[i] = NIL; }
   if (tid == 0) {
     ndist = nc = adds = dropped = dels = 0;
-    bad = (!F.enabled || (bk.pad & BOOK_QUIRK) || (D.st->err & ERR_INPUT) || (end - beg) >= FL_MAX_ORDERS) ? 1u : 0u;
+    bad = (!F.enabled || (bk.pad & (BOOK_QUIRK | BOOK_ZERO)) || (D.st->err & ERR_INPUT) || (end - beg) >= FL_MAX_ORDERS) ? 1u : 0u;
     many = bk.n_lvl > FL_MAX ? 1u : 0u;  // more levels than lanes: a deep candidate
   }
   __syncthreads();
@@ -713,7 +714,7 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep_b(Dev D, BatchArgs B, F
   __shared__ uint32_t hval[FL_HASH];
   __shared__ unsigned long long ckey[FL_CAP + FL_PREP_T];
   __shared__ uint32_t cslot[FL_CAP + FL_PREP_T];
-  __shared__ uint32_t ndist, nc, bad, deepc, nstale;
+  __shared__ uint32_t ndist, nc, bad, deepc, nstale, nzlev;
   __shared__ unsigned long long wg[FL_PREP_T / 64], ws[FL_PREP_T / 64];
   const uint32_t hb = blockIdx.x, h = F.h0 + hb, tid = threadIdx.x;
   if (h >= fl_hend(D, F)) return;
@@ -742,9 +743,9 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep_b(Dev D, BatchArgs B, F
   // reconstruction does not model: k_flow_zero_check finds its REST of 0 and hands the book over.
   const bool stale_ok = (end - beg) >= LEGACY_HOT_MIN && P->dels == 0;
   if (tid == 0) {
-    ndist = nc = nstale = 0;
+    ndist = nc = nstale = nzlev = 0;
     const bool base_bad = !F.enabled || P->bad || (bk.pad & BOOK_QUIRK) || (D.st->err & ERR_INPUT) ||
-                          (P->zeros && !stale_ok) ||
+                          ((P->zeros || (bk.pad & BOOK_ZERO)) && !stale_ok) ||
                           (end - beg) >= FL_MAX_ORDERS;
     const bool many = P->many || bk.n_lvl > FL_MAX;
     // more levels than lanes: the deep plan's candidate (match_flow_deep.h re-checks the rest)
@@ -842,6 +843,8 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep_b(Dev D, BatchArgs B, F
       f.hslot = x.hslot;
       f.tslot = x.tslot;
       f.mem0 = x.member;
+      f.z0 = (bk.pad & BOOK_ZERO) && (x.pad & L_ZERO) ? 1u : 0u;
+      if (f.z0) atomicAdd(&nzlev, 1u);
     }
     LV[r + 1] = f;
     hval[sl] = r + 1;
@@ -881,8 +884,9 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep_b(Dev D, BatchArgs B, F
     x.bid = F.bid;
     x.nstale = nstale;
     x.nzero = P->zeros;
+    x.nzlev = nzlev;
     if (nstale) ctr_add(D, C_FLOW_STALE, 1ull);
-    if (x.nzero) ctr_add(D, C_FLOW_ZERO, 1ull);
+    if (x.nzero || nzlev) ctr_add(D, C_FLOW_ZERO, 1ull);
     *hd = x;
   }
 }
@@ -2314,7 +2318,9 @@ __device__ __forceinline__ FlWPlan fl_wplan(const FlowLvl& f, const RsEnt* RS) {
     uint32_t lo = 0, hi = f.nrest;  // first r with e + v > cfin
     while (lo < hi) {
       const uint32_t mid = (lo + hi) >> 1;
-      if (RS[mid].e + RS[mid].v > f.cfin) hi = mid; else lo = mid + 1;
+      // (a zero-volume maker (Q6) survives at the cursor: width 1; it rests after every consume of its
+      // level, k_flow_zero_check)
+      if (RS[mid].e + (RS[mid].v ? RS[mid].v : 1) > f.cfin) hi = mid; else lo = mid + 1;
     }
     w.rf = lo;
   }
@@ -2446,6 +2452,7 @@ __device__ __forceinline__ Level fl_write_level(const Dev& D, const BatchArgs& B
 // the batch counters.  Called by every thread of the block after lv is complete.
 __device__ __forceinline__ void fl_write_finish(const Dev& D, const FlowHdr& hd, Level* lv, uint32_t* keep,
                                                 uint32_t& base_s, uint32_t& cap_s, uint32_t& nout_s) {
+  __shared__ uint32_t zflag_s;
   if (threadIdx.x == 0) {
     uint32_t c = 0;
     for (uint32_t q = 1; q <= hd.nl; ++q) {
@@ -2454,6 +2461,9 @@ __device__ __forceinline__ void fl_write_finish(const Dev& D, const FlowHdr& hd,
       c += k;
     }
     nout_s = c;
+    uint32_t anyz = 0;  // (levels that may hold zero-volume makers: BOOK_ZERO)
+    for (uint32_t q = 1; q <= hd.nl; ++q) anyz |= keep[q] != NIL && (lv[q].pad & L_ZERO) ? 1u : 0u;
+    zflag_s = anyz ? BOOK_ZERO : 0u;
     const Book bk = D.books[hd.sym];
     uint32_t base = bk.lvl_base, cap = bk.lvl_cap;
     if (c > cap) {
@@ -2482,7 +2492,7 @@ __device__ __forceinline__ void fl_write_finish(const Dev& D, const FlowHdr& hd,
     nb.lvl_base = base_s;
     nb.n_lvl = nout;
     nb.lvl_cap = cap_s;
-    nb.pad = 0;
+    nb.pad = zflag_s;
     D.books[hd.sym] = nb;
     ctr_add(D, C_RESTS, static_cast<unsigned long long>(hd.rests));
     ctr_add(D, C_HOT_RESTS, static_cast<unsigned long long>(hd.rests));
@@ -2688,6 +2698,7 @@ __global__ __launch_bounds__(FL_LVB_T) void k_flow_write_lv_blk(Dev D, BatchArgs
   const FlWPlan wp = fl_wplan(f, RS);
   const uint32_t rf = wp.rf, S = wp.S, s0 = wp.s0, room = wp.room, need = wp.need;
   const bool fresh = wp.fresh;
+  bool zs = false;
   if (tid == 0) {  // claim `need` chunk ids: free stack first, then the bump pointer
     int t = 0;
     uint32_t nst = 0, bb = 0;
@@ -2754,7 +2765,10 @@ __global__ __launch_bounds__(FL_LVB_T) void k_flow_write_lv_blk(Dev D, BatchArgs
     nd.ixs = static_cast<uint32_t>(hh);
     nd.tx = mk.side;
     D.nodes[loc] = nd;
+    zs = zs || r.v == 0;
   }
+  // the level may hold zero-volume makers: old ones (z0) or one appended now (Q6)
+  const bool zl = __syncthreads_or(zs) || f.z0;
   if (tid != 0) return;
   ctr_pops(D, fl_level_pops(f, rf));
   Level x{};
@@ -2788,6 +2802,7 @@ __global__ __launch_bounds__(FL_LVB_T) void k_flow_write_lv_blk(Dev D, BatchArgs
                         : (x.nlive > 0) == (x.depth > 0) && (x.nlive > 0) == (mem == M_BUY || mem == M_SALE) &&
                               (x.nlive > 0 || mem == 0);
   if (!ok) atomicOr(&D.st->err, ERR_CORRUPT);
+  x.pad = zl ? L_ZERO : 0u;
   F.lvout[h * FL_CAP + q] = x;
 }
 
@@ -2972,21 +2987,41 @@ __global__ __launch_bounds__(FL_TILE) void k_flow_sort_scatter(Dev D, FlowArgs F
   }
 }
 
-// Books planned with zero-volume ADDs (Q6, k_flow_prep_b): a REST touch of 0 at a real level (the
-// no-op records rest 0 at the sentinel level 0) is a zero-volume maker; FlowHdr::haz hands the book
-// over (k_flow_stale_check).  Grid-stride over the book's log, only for such books.
-__global__ __launch_bounds__(256) void k_flow_zero_check(Dev D, FlowArgs F) {
-  const uint32_t h = F.h0 + blockIdx.y;
+// Books planned with zero-volume ADDs (Q6, k_flow_prep_b) or holding zero-volume makers (FlowLvl::z0):
+// the reconstruction takes a zero-volume maker only where no order reaches it this batch.  One block
+// per (book, level), the level's run in time order with block scans; hazards (FlowHdr::haz, handed
+// over by k_flow_stale_check):
+//  * a REST of 0 while the level's depth is 0: the reference makes it a side-set member of depth 0
+//    (SetPoolDepth, engine.go:78-80), which the plans, seeing depth 0 as "no level", would not visit;
+//  * a CONS (of any amount) after a zero-volume maker may be in the FIFO (z0, or a REST of 0 earlier in
+//    the run): the fills would have to pop it (engine.go:145-175).
+// A REST of 0 with depth > 0 and no CONS after it is an ordinary FIFO append (fl_wplan).
+__global__ __launch_bounds__(FL_LVB_T) void k_flow_zero_check(Dev D, FlowArgs F) {
+  const uint32_t h = F.h0 + blockIdx.y, q = blockIdx.x, tid = threadIdx.x;
   if (h >= fl_hend(D, F)) return;
   FlowHdr* hd = &F.hdr[h];
-  if (hd->ok != FL_OK_ADD || hd->nzero == 0) return;
-  const uint32_t nt = hd->ntouch, L = FL_TOUCH_MUL * hd->beg;
-  bool z = false;
-  for (uint32_t t = blockIdx.x * 256 + threadIdx.x; t < nt; t += gridDim.x * 256) {
-    const Touch x = F.log[L + t];
-    z = z || (((x.kr >> 7) & 1u) == TK_REST && x.amt == 0 && (x.kr & 127u) != 0);
+  if (hd->ok != FL_OK_ADD || (hd->nzero == 0 && hd->nzlev == 0) || q == 0 || q > hd->nl) return;
+  const FlowLvl* Lq = F.lvl + h * FL_CAP + q;
+  const uint32_t cnt = Lq->cnt;
+  if (!cnt) return;
+  const SEnt* R = F.srt + FL_TOUCH_MUL * hd->beg + Lq->base;
+  int64_t run = Lq->d0;      // the level's depth before the chunk
+  bool zero = Lq->z0 != 0;   // a zero-volume maker may be in the FIFO before the chunk
+  bool haz = false;
+  for (uint32_t c0 = 0; c0 < cnt; c0 += FL_LVB_T) {
+    const uint32_t i = c0 + tid;
+    const bool valid = i < cnt;
+    SEnt e{};
+    if (valid) e = R[i];
+    const bool isr = valid && e.kind == TK_REST, isc = valid && e.kind == TK_CONS, zr = isr && e.amt == 0;
+    int64_t tot, tz;
+    const int64_t before = run + fl_blk_excl(isr ? e.amt : isc ? -e.amt : 0, &tot);
+    const int64_t zb = fl_blk_excl(zr ? 1 : 0, &tz);
+    haz = haz || (zr && before == 0) || (isc && (zero || zb > 0));
+    run += tot;
+    zero = zero || tz > 0;
   }
-  if (__any(z) && lane_id() == 0) atomicOr(&hd->haz, 1u);
+  if (__syncthreads_or(haz) && tid == 0) atomicOr(&hd->haz, 1u);
 }
 
 // After the head's level sort: a book planned with stale members is exact unless an order rested

@@ -1201,7 +1201,7 @@ __global__ __launch_bounds__(64) void k_match_hot(Dev D, BatchArgs B, PendEnt* p
     S->env = e;
     S->nfree = NCS;
     S->npool = S->nfreed = S->nflushed = 0;
-    S->bflags = bk.pad;
+    S->bflags = bk.pad | ((bk.pad & BOOK_ZERO) ? BOOK_QUIRK : 0u);  // (L_ZERO marks: k_requalify redoes them)
     S->rr = ResumeRec{};
   }
 #ifdef GOME_STAMPS

@@ -27,14 +27,17 @@ namespace gome {
 //    or is a stale member (Q2: no node, depth 0: the head books' lane plans take it, k_flow_prep_b,
 //    every other prep declines it); every other level has no node and depth 0;
 //  * every bid lies below every ask (levels are sorted by price; stale members aside);
-//  * every live node of a member level has a positive remaining volume (no Q6 maker) and the
-//    level's side, and the level's FIFO holds exactly nlive nodes summing to its depth.
+//  * every live node of a member level has the level's side, or a zero remaining volume (a Q6
+//    maker, any side: the head books' lane plans take the book while no order reaches it, marked
+//    L_ZERO on its level and BOOK_ZERO on the book), and the level's FIFO holds exactly nlive nodes
+//    summing to its depth.
 // The level checks come first: a book that is still stale fails them without a FIFO walk.
-__device__ __forceinline__ bool book_requalifies(const Dev& D, uint32_t sym) {
+// Returns -1 (no), 0 (yes), 1 (yes, with zero-volume makers: BOOK_ZERO); sets the levels' L_ZERO.
+__device__ __forceinline__ int book_requalifies(const Dev& D, uint32_t sym) {
   const uint32_t lane = lane_id();
   const Book bk = D.books[sym];
   const uint32_t nl = uni(bk.n_lvl);
-  const Level* L = D.lvl + uni(bk.lvl_base);
+  Level* L = D.lvl + uni(bk.lvl_base);
   int32_t last_bid = -1;
   uint32_t first_ask = NIL;
   for (uint32_t w0 = 0; w0 < nl; w0 += 64) {
@@ -49,22 +52,24 @@ __device__ __forceinline__ bool book_requalifies(const Dev& D, uint32_t sym) {
       else if (x.member) bad = !stale && (x.nlive == 0 || x.depth <= 0 || x.head == NIL);
       else bad = x.nlive != 0 || x.depth != 0 || x.head != NIL;
     }
-    if (__ballot(bad)) return false;
+    if (__ballot(bad)) return -1;
     const unsigned long long bm = __ballot(bid), am = __ballot(ask);
     if (bm) last_bid = static_cast<int32_t>(w0 + 63u - static_cast<uint32_t>(__builtin_clzll(bm)));
     if (am && first_ask == NIL) first_ask = w0 + static_cast<uint32_t>(__builtin_ctzll(am));
   }
-  if (last_bid >= 0 && first_ask != NIL && static_cast<uint32_t>(last_bid) > first_ask) return false;
+  if (last_bid >= 0 && first_ask != NIL && static_cast<uint32_t>(last_bid) > first_ask) return -1;
+  bool anyz = false;
   for (uint32_t k = 0; k < nl; ++k) {
     const Level x = L[k];
+    if (lane == 0 && (x.pad & L_ZERO)) L[k].pad = 0;  // (set below where a zero-volume maker rests)
     if (!x.member || x.head == NIL) continue;  // (a stale member: checked above)
     const bool sale = x.member == M_SALE;
     uint32_t c = uni(x.head), s0 = uni(x.hslot), cnt = 0;
     const uint32_t tail = uni(x.tail), tslot = uni(x.tslot);
     int64_t sum = 0;
-    bool bad = false;
+    bool bad = false, zero = false;
     for (uint32_t guard = 0; c != NIL; ++guard) {
-      if (guard > D.ch_cap) return false;
+      if (guard > D.ch_cap) return -1;
       const uint32_t lim = (c == tail) ? tslot : CH;
       int64_t r = -1;
       uint32_t tx = 0;
@@ -74,15 +79,20 @@ __device__ __forceinline__ bool book_requalifies(const Dev& D, uint32_t sym) {
         tx = nd.tx;
       }
       const bool live = r >= 0;
-      bad = bad || (live && (r == 0 || ((tx == GOME_SALE) != sale)));
+      bad = bad || (live && r > 0 && ((tx == GOME_SALE) != sale));
+      zero = zero || (live && r == 0);
       cnt += static_cast<uint32_t>(__popcll(__ballot(live)));
       sum += rl64(wave_incl_scan(live ? r : 0), 63);
       c = (c == tail) ? NIL : uni(D.chdr[c].next);
       s0 = 0;
     }
-    if (__ballot(bad) || cnt != x.nlive || sum != x.depth) return false;
+    if (__ballot(bad) || cnt != x.nlive || sum != x.depth) return -1;
+    if (__ballot(zero)) {
+      anyz = true;
+      if (lane == 0) L[k].pad = L_ZERO;
+    }
   }
-  return true;
+  return anyz ? 1 : 0;
 }
 
 // After a batch's book kernels: the books the cold / resume waves listed (Dev::quirk) and the
@@ -104,11 +114,11 @@ __global__ __launch_bounds__(256) void k_requalify(Dev D, BatchArgs B, const Flo
       sym = uni(B.ord[B.prep[beg].idx].symbol_id);
     }
     if (!(uni(D.books[sym].pad) & BOOK_QUIRK)) continue;
-    const bool ok = book_requalifies(D, sym);
+    const int ok = book_requalifies(D, sym);
     if (lane_id() == 0) {
       ctr_add(D, C_QUIRK_CHECKED, 1);
-      if (ok) {
-        atomicAnd(&D.books[sym].pad, ~BOOK_QUIRK);
+      if (ok >= 0) {
+        D.books[sym].pad = ok ? BOOK_ZERO : 0u;
         ctr_add(D, C_REQUAL, 1);
       }
     }

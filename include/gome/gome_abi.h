@@ -275,9 +275,13 @@ typedef struct gome_stats {
   uint64_t n_flow_stale;                      /* head books planned on the flow path with stale
                                                  side-set members (Q2: a member level with no
                                                  FIFO, left by a wrong-side cancel; ABI >= 11) */
-  uint64_t n_flow_bail;                       /* ... of which an order rested on the other side
-                                                 of a stale price: the book went to the legacy
-                                                 kernel after its plan (ABI >= 11)          */
+  uint64_t n_flow_bail;                       /* head books the legacy kernel applied after their
+                                                 plan: an order rested on the other side of a
+                                                 stale price, or a zero-volume maker an order
+                                                 reaches (ABI >= 11)                        */
+  uint64_t n_flow_zero;                       /* head books planned on the flow path with
+                                                 zero-volume ADDs or zero-volume makers (Q6;
+                                                 ABI >= 11)                                 */
 } gome_stats;
 
 typedef struct gome_engine gome_engine;

@@ -581,9 +581,17 @@ class GomeLiteral:
             self.DoOrder(node)
 
     def oid_live(self, symbol: str, oid: str) -> bool:
-        """Does one of the symbol's FIFOs (S:link:<p>) hold the node S:node:<oid>?"""
+        """Does one of the symbol's FIFOs (S:link:<p>) hold the node S:node:<oid>?  The symbol's
+        link hashes are listed once per change of the hash keys (a new or deleted price level), not
+        per call (the scan of every key per admitted ADD made this quadratic)."""
         pre, field = symbol + ":link:", symbol + ":node:" + oid
-        return any(field in hv for key, hv in self.cache.h.items() if key.startswith(pre))
+        cache = self.__dict__.setdefault("_link_keys", {})
+        n = len(self.cache.h)
+        got = cache.get(symbol)
+        if got is None or got[0] != n:
+            got = cache[symbol] = (n, [key for key in self.cache.h if key.startswith(pre)])
+        h = self.cache.h
+        return any(field in h.get(key, ()) for key in got[1])
 
     def resting_oids(self) -> set:
         """(Symbol, Oid) of every node resting in a FIFO (an S:node:<oid> field of S:link:<p>)."""

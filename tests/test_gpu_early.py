@@ -91,7 +91,7 @@ def test_early_plan_declines_keep_the_engine_exact():
     eng, orc, stats = _run(batches, 100000, "declines")
     early = [int(s["n_early"]) for s in stats]
     assert sum(int(s["n_early_miss"]) for s in stats) == 0, early
-    for k in (4, 5, 6, 8, 9, 12):
+    for k in (4, 5, 6, 8, 9):  # (12: a zero-volume ADD may plan early since round 5: Q6 on the flow path)
         assert early[k] == 0, (k, early)
     for k in (3, 7, 10, 11):
         assert early[k] == 1, (k, early)

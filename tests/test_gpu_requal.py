@@ -52,63 +52,88 @@ def test_quirks_heal_and_the_hottest_book_returns_to_the_flow_path():
     assert all(k != 0 for k in kinds[healed[0] + 1:]), (kinds, req)
 
 
-def test_quirk_that_does_not_heal_stays_on_legacy_and_exact():
-    kinds, req = _run("stuck", batches=4)
-    assert kinds[0] != 0 and all(k == 0 for k in kinds[1:]), kinds
-    assert all(r == 0 for _, r in req) and all(c >= 1 for c, _ in req[1:]), req
+def test_quirks_that_do_not_heal_stay_on_the_flow_path():
+    """The same quirks at the bottom of the bid book, which the stream never reaches again: batch 1
+    applies them on the legacy kernel; the stale member (Q2) and the zero-volume maker (Q6, marked
+    L_ZERO / BOOK_ZERO by k_requalify) then ride along on the flow path (round 5; in round 4 the book
+    stayed on the ~23x slower legacy kernel for good), exact throughout."""
+    kinds, req = _run("stuck", batches=5)
+    assert kinds[0] != 0 and kinds[1] == 0, kinds
+    assert all(k != 0 for k in kinds[2:]), (kinds, req)
+    assert req[1][1] >= 1, req
 
 
 # ---- stale members on the flow path (Q2 alone; VERDICT r4 next #3) -----------------------------
-def test_stale_member_stays_on_the_flow_path():
-    """Wrong-side cancels of every maker of the lowest bid (never reached again): batch 1 applies
-    them on the legacy kernel (a book with DELs of the wrong side), the level stays in S:BUY with no
-    FIFO, k_requalify accepts the stale member, and from batch 2 on the hottest book is planned on
-    the flow path with it (n_flow_stale), exact throughout."""
-    kinds, req = _run("q2stuck", batches=5)
-    assert kinds[0] != 0 and kinds[1] == 0, kinds
-    assert all(k != 0 for k in kinds[2:]), (kinds, req)
-    assert req[1][1] >= 1, req  # (requalified after batch 1 with the stale level)
+def _move_away(b, sym, p, after=-1):
+    """Records of `sym` at price p (the rows after `after`) move one tick up, so nothing rests or
+    trades there: the stale member stays stale."""
+    rows = np.nonzero(b["symbol_id"] == sym)[0]
+    rows = rows[(rows > after) & (b["price_fx"][rows] == p)]
+    b["price_fx"][rows] = p + 10 ** 6
 
 
-def _hand_over(rank, seed, batches=5):
-    """Batch 1: wrong-side cancels of every maker of symbol `rank`'s lowest bid (its first records:
-    a stale member from then on); batch 2: planned with it; batch 3: the book's first record is a
-    SALE at the stale price with a volume above the whole bid side, so it sweeps every real bid and
-    rests there: the price is then in both side sets in the reference, where a later SALE taker
-    would meet that SALE maker.  k_flow_stale_check hands the book to the legacy kernel after its
-    plan; every batch's events and the books at the end are the oracle's."""
+def _stale_inject(b, sym, eng):
+    """Wrong-side cancels of every maker of `sym`'s lowest bid (its first records), the rest of the
+    symbol's records at that price moved away: a stale member of S:BUY from this batch on."""
+    info = wl.inject_quirks(b, sym, eng.levels(sym), lambda p: eng.fifo(sym, p), "q2stuck")
+    assert info["q2_cancels"] >= 1
+    _move_away(b, sym, info["q2_price"], after=max(info["records"]))
+    return info["q2_price"]
+
+
+def _stale_run(rank, seed, hazard, batches=5):
+    """Batch 1: a stale member made (on the legacy kernel: a book with wrong-side DELs); then the
+    book on the flow path with it; with `hazard`, batch 2's first record of the book is a SALE at
+    the stale price with a volume above the whole bid side, so it sweeps every real bid and rests
+    there (the price in both side sets in the reference, where a later SALE taker would meet that
+    SALE maker): k_flow_stale_check hands the book to the legacy kernel after its plan.  Every
+    batch's events and the books at the end are the oracle's."""
     gen, _, _ = bench.shard_stream(100000, 1.0, 0, 1, seed)
     z = wl.ZipfSymbols(100000, 1.0)
     sym = int(z.rank_to_id[rank])
     eng = Engine(max_symbols=100000, max_batch=N, max_nodes=(batches + 1) * N, max_levels=1 << 22)
     orc = Oracle(100000)
-    stale_p, bails, stales = None, [], []
+    p, out = None, []
     for i in range(batches):
         b = gen(N).copy()
         if i == 1:
-            stale_p = wl.inject_quirks(b, sym, eng.levels(sym), lambda p: eng.fifo(sym, p), "q2stuck")["q2_price"]
-        if i == 3:
-            r = np.nonzero(b["symbol_id"] == sym)[0][0]
-            b["price_fx"][r], b["side"][r], b["action"][r], b["volume_fx"][r] = stale_p, 1, wl.ADD, 10 ** 14
+            p = _stale_inject(b, sym, eng)
+        elif i >= 2:
+            _move_away(b, sym, p)
+            if hazard and i == 2:
+                r = np.nonzero(b["symbol_id"] == sym)[0][0]
+                b["price_fx"][r], b["side"][r], b["action"][r], b["volume_fx"][r] = p, 1, wl.ADD, 10 ** 14
         eng.submit(b)
-        _cmp(eng.drain(), orc.submit(b), f"hand-over rank {rank} batch {i}")
+        _cmp(eng.drain(), orc.submit(b), f"stale rank {rank} batch {i}")
         st = eng.stats()
-        bails.append(int(st["n_flow_bail"]))
-        stales.append(int(st["n_flow_stale"]))
-    _cmp_books(eng, orc, [sym] + _hot_and_random(z, 100000, k_rand=30), f"hand-over rank {rank}")
+        fl = eng.debug_flow_books()
+        kind = int(fl["kind"][list(fl["symbol_id"]).index(sym)]) if sym in list(fl["symbol_id"]) else -1
+        out.append((kind, int(st["n_flow_stale"]), int(st["n_flow_bail"])))
+    _cmp_books(eng, orc, [sym] + _hot_and_random(z, 100000, k_rand=30), f"stale rank {rank}")
     assert eng.stats()["n_resting"] == orc.resting()
-    return stales, bails
+    lv = orc.levels(sym)
+    return out, lv[lv["price_fx"] == p]
+
+
+def test_stale_member_stays_on_the_flow_path():
+    """The hottest book with a stale member of S:BUY (no FIFO, depth 0) is planned on the flow path
+    from the batch after the one that made it (k_requalify accepts it, n_flow_stale), exact, and the
+    stale member is still there at the end (levels compared with the oracle's)."""
+    out, lv = _stale_run(0, 42, hazard=False)
+    assert out[1][0] == 0, out                            # (the wrong-side cancels: legacy)
+    assert all(k != 0 and s >= 1 and x == 0 for k, s, x in out[2:]), out
+    assert len(lv) == 1 and lv["in_buy"][0] == 1 and lv["n_nodes"][0] == 0, lv
 
 
 def test_order_resting_opposite_a_stale_price_hands_the_book_to_legacy():
-    stales, bails = _hand_over(0, 42)
-    assert stales[2] >= 1 and stales[3] >= 1 and bails[2] == 0 and bails[3] >= 1, (stales, bails)
+    out, _ = _stale_run(0, 42, hazard=True)
+    assert out[2][1] >= 1 and out[2][2] >= 1 and out[2][0] == 0, out
 
 
 def test_near_book_hand_over():
     """The same for the second-hottest book (the near books' reconstruction on the hot stream)."""
-    stales, bails = _hand_over(1, 43)
-    assert stales[3] >= 1 and bails[3] >= 1, (stales, bails)
+    out, _ = _stale_run(1, 43, hazard=True)
+    assert out[2][1] >= 1 and out[2][2] >= 1, out
 
 
 # ---- zero-volume ADDs (Q6) on the flow path -----------------------------------------------------
@@ -149,14 +174,44 @@ def test_zero_volume_takers_stay_on_the_flow_path():
     assert all(k != 0 for k, _, _ in out), out
 
 
-def test_zero_volume_maker_hands_the_book_to_legacy():
-    """A zero-volume ADD that rests (a zero-volume maker, which the reconstruction does not model):
-    k_flow_zero_check hands the book to the legacy kernel after its plan, exact; the maker's book is
-    a quirk book afterwards (BOOK_QUIRK) until it heals."""
+def _hot_rows(b, hot):
+    return np.nonzero((b["symbol_id"] == hot) & (b["action"] == wl.ADD))[0]
+
+
+def test_zero_volume_maker_no_order_reaches_stays_on_the_flow_path():
+    """A zero-volume ADD resting at the lowest bid (behind its makers, depth > 0): an ordinary FIFO
+    append on the flow path; no order reaches it later, so the book stays on the flow path with the
+    zero-volume maker in its FIFO (BOOK_ZERO), exact."""
     def edit(b, hot, eng):
         lv = eng.levels(hot)
         bids = np.sort(lv[(lv["in_buy"] != 0) & (lv["n_nodes"] > 0)], order="price_fx")
-        r = np.nonzero((b["symbol_id"] == hot) & (b["action"] == wl.ADD))[0][100]
+        r = _hot_rows(b, hot)[100]
         b["volume_fx"][r], b["side"][r], b["price_fx"][r] = 0, 0, bids["price_fx"][0]
-    out = _zero_run(45, edit)
-    assert out[2][1] >= 1 and out[2][2] >= 1 and out[2][0] == 0, out
+    out = _zero_run(45, edit, batches=5)
+    assert all(k != 0 for k, _, _ in out) and all(x == 0 for _, _, x in out), out
+    assert all(z >= 1 for _, z, _ in out[2:]), out
+
+
+def test_zero_volume_maker_at_a_new_price_hands_the_book_to_legacy():
+    """A zero-volume BUY below every level: the reference makes it a side-set member of depth 0
+    (SetPoolDepth), which the plans would not visit: k_flow_zero_check hands the book to the legacy
+    kernel after its plan, exact."""
+    def edit(b, hot, eng):
+        r = _hot_rows(b, hot)[100]
+        b["volume_fx"][r], b["side"][r], b["price_fx"][r] = 0, 0, 1
+    out = _zero_run(46, edit)
+    assert out[2][0] == 0 and out[2][1] >= 1 and out[2][2] >= 1, out
+
+
+def test_zero_volume_maker_reached_hands_the_book_to_legacy():
+    """A zero-volume BUY at the best bid followed by a SALE sweeping every bid: a consume after a
+    zero-volume maker may be in the FIFO (the fills would pop it), so the book goes to the legacy
+    kernel after its plan, exact."""
+    def edit(b, hot, eng):
+        lv = eng.levels(hot)
+        bids = np.sort(lv[(lv["in_buy"] != 0) & (lv["n_nodes"] > 0)], order="price_fx")
+        rows = _hot_rows(b, hot)
+        b["volume_fx"][rows[0]], b["side"][rows[0]], b["price_fx"][rows[0]] = 0, 0, bids["price_fx"][-1]
+        b["volume_fx"][rows[1]], b["side"][rows[1]], b["price_fx"][rows[1]] = 10 ** 14, 1, 10 ** 6
+    out = _zero_run(47, edit)
+    assert out[2][0] == 0 and out[2][2] >= 1, out

@@ -76,7 +76,8 @@ class Stats(C.Structure):
         ("n_quirk_checked", C.c_uint64), ("n_requalified", C.c_uint64), ("chunk_bytes", C.c_uint64),
         ("n_early", C.c_uint64), ("n_early_miss", C.c_uint64),
         ("n_adm_ahead", C.c_uint64), ("n_adm_redo", C.c_uint64),
-        ("n_flow_stale", C.c_uint64), ("n_flow_bail", C.c_uint64), ("n_flow_zero", C.c_uint64)]
+        ("n_flow_stale", C.c_uint64), ("n_flow_bail", C.c_uint64), ("n_flow_zero", C.c_uint64),
+        ("n_flow_wrong", C.c_uint64)]
 
     def as_dict(self):
         d = {n: getattr(self, n) for n, _ in self._fields_}

@@ -70,6 +70,10 @@ constexpr uint32_t BOOK_QUIRK = 1u;
 // that applies such a book sets BOOK_QUIRK, so k_requalify recomputes the marks after it).
 constexpr uint32_t BOOK_ZERO = 2u;
 constexpr uint8_t L_ZERO = 1u;
+// Book::pad: the book may hold stale side-set members (Q2: member, no FIFO, depth 0), so a bid
+// may lie above an ask (a stale one) and the cold kernel's bid/ask split scan does not hold
+// (set by k_requalify and the flow writes that keep such a level; cleared by a later requalify).
+constexpr uint32_t BOOK_STALE = 4u;
 
 struct IdxEnt {
   unsigned long long key;  // ((S+1) << 32) | oid ; 0 empty, ~0 tombstone
@@ -106,6 +110,7 @@ enum {
   C_FLOW_STALE, C_FLOW_BAIL,                              // head books planned with stale members (Q2) /
                                                           // handed to the legacy kernel after their plan
   C_FLOW_ZERO,                                            // head books planned with zero-volume ADDs (Q6)
+  C_FLOW_WRONG,                                           // head books with wrong-side cancels (Q2) on the cancel path
   C_NCTR = 40
 };
 

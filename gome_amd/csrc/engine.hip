@@ -1188,8 +1188,12 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
     // (k_flow_zero_check, k_flow_stale_check), on this stream, before any of the book is written;
     // for the hottest book after the hot stream's main legacy launch and its index inserts
     // (hand_wait), which the near books' stream has behind it anyway
+    // (books with DELs: stale members and wrong-side cancels, k_fc_stale_level; a bailed one's
+    // old targets unmarked)
     k_flow_zero_check<<<dim3(FL_CAP, nb), FL_LVB_T, 0, st>>>(D, R);
+    if (c_canc) k_fc_stale_level<<<dim3(FL_CAP, nb), FL_LVB_T, 0, st>>>(D, B, R);
     k_flow_stale_check<<<nb, FL_CAP, 0, st>>>(D, B, R);
+    if (c_canc) k_fc_unmark_bailed<<<dim3(FL_PG, nb), 256, 0, st>>>(D, B, R);
     if (hand_wait) HIPCHK(hipStreamWaitEvent(st, oidmax_done, 0));
     k_match_hot<<<R.h0 + nb, 64, HOT_LDS_BYTES, st>>>(D, B, d_pend, d_resume, F.hdr, 1u, R.h0, R.h0 + nb);
     k_match_resume<<<R.h0 + nb, 64, 0, st>>>(D, B, d_resume, F.hdr, R.h0, R.h0 + nb);
@@ -1385,6 +1389,7 @@ gome_status gome_engine::finish(uint32_t sl, uint32_t n) {
   stats.n_flow_stale = st.ctr[C_FLOW_STALE];
   stats.n_flow_bail = st.ctr[C_FLOW_BAIL];
   stats.n_flow_zero = st.ctr[C_FLOW_ZERO];
+  stats.n_flow_wrong = st.ctr[C_FLOW_WRONG];
   stats.ms_hot = ms_hot;
   stats.ms_flow_plan = ms_flow;
   stats.n_flow_books = st.ctr[C_FLOW_BOOKS];

@@ -531,12 +531,12 @@ __device__ __forceinline__ uint32_t do_add(WaveCtx& W, int64_t p, int64_t vol, u
   bool crossed = false;
   uint32_t fidx = 0;
   // GetReverseDepth (nodepool.go:86-115): opposite-side levels crossing p, best first.  In a
-  // book without quirks every bid is below every ask (a rest follows a complete sweep), so on a
+  // book without quirks or stale members every bid is below every ask (a rest follows a complete sweep), so on a
   // deep book the scan starts just above the highest bid <= p (BUY) or just below the lowest
   // ask >= p (SALE) instead of walking the book's other side from its far end.
   uint32_t up0 = 0;
   int32_t dn0 = static_cast<int32_t>(W.nl);
-  if (!(W.flags & BOOK_QUIRK) && W.nl > COLD_SCAN_FROM) {
+  if (!(W.flags & (BOOK_QUIRK | BOOK_STALE)) && W.nl > COLD_SCAN_FROM) {
     uint32_t pos;
     const bool at = level_search(W, p, pos);
     if (!sale) {

@@ -144,7 +144,8 @@ struct FlowHdr {
   uint32_t bail;       // set with ok = 0 by k_flow_stale_check: the legacy kernel applies the book
   uint32_t nzero;      // admitted zero-volume ADDs of the segment (Q6, k_flow_zero_check)
   uint32_t nzlev;      // levels that may hold zero-volume makers at batch start (FlowLvl::z0)
-  uint32_t haz;        // k_flow_zero_check: a zero-volume maker the reconstruction cannot take
+  uint32_t haz;        // k_flow_zero_check / k_fc_stale_level: a state the reconstruction cannot take
+  uint32_t nwrong;     // books with DELs: wrong-side cancels that find their maker (Q2, k_fc_resolve)
 };
 // FlowHdr::ok: 0 declined, FL_OK_ADD an ADD-only flow book, FL_OK_CANCEL a book with DELs,
 // FL_OK_DEEP an ADD-only head book with more levels than the lane plans hold (match_flow_deep.h)
@@ -181,12 +182,13 @@ struct FlowLvl {
   // books with DELs (match_flow_cancel.h): the targets of the level's DELs
   uint32_t c_old;    // old (pre-batch) makers targeted by a DEL of the batch
   uint32_t z0;       // the level's FIFO may hold zero-volume makers at batch start (Level::pad L_ZERO)
-  uint32_t rbase;    // (unused)
+  uint32_t c_wrong;  // wrong-side DELs (Q2) whose maker rests at this level (k_fc_resolve)
   uint32_t ocan;     // cancelled volume of old makers (plan units), set by the recon
   uint32_t memf;     // deep books: membership after the batch (M_BUY / M_SALE)
   uint32_t ttot;     // targets of the level (old + new): ranks 0 .. ttot - 1
   uint32_t tbase;    // first entry of the level's DEL-time array in FlowArgs::fc_dt (book-local)
-  uint32_t pad3;
+  uint32_t mfin;     // books with DELs: the level ends a stale member of this set (M_BUY / M_SALE;
+                     // k_fc_stale_level), 0 if not
 };
 static_assert(sizeof(FlowLvl) % 16 == 0, "FlowLvl alignment");
 
@@ -735,17 +737,20 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep_b(Dev D, BatchArgs B, F
   // which see a depth of 0 as "no level", are exact for both.  Only an order resting on the OTHER
   // side at that price is not (the level would be a member of both sets), which
   // k_flow_stale_check finds after the plan: the book then goes to the legacy kernel
-  // (k_match_hot mode 1).  Head books of at least LEGACY_HOT_MIN orders without DELs only (the
-  // cold kernel never takes such a book, so a late hand-over cannot race with it).
+  // (k_match_hot mode 1).  Head books of at least LEGACY_HOT_MIN orders only (the cold kernel
+  // never takes such a book, so a late hand-over cannot race with it); with DELs, the cancel path
+  // also takes wrong-side cancels that make such a level (k_fc_resolve, k_fc_stale_level).
   // Zero-volume ADDs (Q6) under the same conditions: one that crosses takes 0 at the best opposite
   // level, the reference's one 0-fill with the maker unchanged (engine.go:176-194), which the plans
   // log as a CONS touch of 0; one that rests leaves a zero-volume maker in the FIFO, which the
   // reconstruction does not model: k_flow_zero_check finds its REST of 0 and hands the book over.
-  const bool stale_ok = (end - beg) >= LEGACY_HOT_MIN && P->dels == 0;
+  // With DELs (the cancel path) a zero-volume taker or a DEL of a zero-volume maker hands it over
+  // too (k_flow_zero_check, k_fc_resolve).
+  const bool stale_ok = (end - beg) >= LEGACY_HOT_MIN, zero_ok = stale_ok;
   if (tid == 0) {
     ndist = nc = nstale = nzlev = 0;
     const bool base_bad = !F.enabled || P->bad || (bk.pad & BOOK_QUIRK) || (D.st->err & ERR_INPUT) ||
-                          ((P->zeros || (bk.pad & BOOK_ZERO)) && !stale_ok) ||
+                          ((P->zeros || (bk.pad & BOOK_ZERO)) && !zero_ok) ||
                           (end - beg) >= FL_MAX_ORDERS;
     const bool many = P->many || bk.n_lvl > FL_MAX;
     // more levels than lanes: the deep plan's candidate (match_flow_deep.h re-checks the rest)
@@ -2461,9 +2466,13 @@ __device__ __forceinline__ void fl_write_finish(const Dev& D, const FlowHdr& hd,
       c += k;
     }
     nout_s = c;
-    uint32_t anyz = 0;  // (levels that may hold zero-volume makers: BOOK_ZERO)
-    for (uint32_t q = 1; q <= hd.nl; ++q) anyz |= keep[q] != NIL && (lv[q].pad & L_ZERO) ? 1u : 0u;
-    zflag_s = anyz ? BOOK_ZERO : 0u;
+    uint32_t fl = 0;  // levels that may hold zero-volume makers (BOOK_ZERO); stale members (BOOK_STALE)
+    for (uint32_t q = 1; q <= hd.nl; ++q) {
+      if (keep[q] == NIL) continue;
+      if (lv[q].pad & L_ZERO) fl |= BOOK_ZERO;
+      if (lv[q].nlive == 0) fl |= BOOK_STALE;
+    }
+    zflag_s = fl;
     const Book bk = D.books[hd.sym];
     uint32_t base = bk.lvl_base, cap = bk.lvl_cap;
     if (c > cap) {
@@ -2987,6 +2996,29 @@ __global__ __launch_bounds__(FL_TILE) void k_flow_sort_scatter(Dev D, FlowArgs F
   }
 }
 
+// Block-wide exclusive max of one uint32 per thread (FL_LVB_T threads); *total = the block's max.
+__device__ __forceinline__ uint32_t fl_blk_max_excl(uint32_t x, uint32_t* total) {
+  __shared__ uint32_t wm[FL_LVB_W];
+  const uint32_t w = threadIdx.x >> 6, lane = lane_id();
+  uint32_t inc = x;
+  for (uint32_t off = 1; off < 64; off <<= 1) {
+    const uint32_t v = __shfl_up(inc, off);
+    if (lane >= off) inc = max(inc, v);
+  }
+  const uint32_t ex = max(__shfl_up(inc, 1), 0u);
+  if (lane == 63u) wm[w] = inc;
+  __syncthreads();
+  uint32_t before = 0, tot = 0;
+  for (uint32_t k = 0; k < FL_LVB_W; ++k) {
+    const uint32_t v = wm[k];
+    before = k < w ? max(before, v) : before;
+    tot = max(tot, v);
+  }
+  __syncthreads();  // (wm is reused by the next call)
+  *total = tot;
+  return max(before, lane ? ex : 0u);
+}
+
 // Books planned with zero-volume ADDs (Q6, k_flow_prep_b) or holding zero-volume makers (FlowLvl::z0):
 // the reconstruction takes a zero-volume maker only where no order reaches it this batch.  One block
 // per (book, level), the level's run in time order with block scans; hazards (FlowHdr::haz, handed
@@ -2995,12 +3027,15 @@ __global__ __launch_bounds__(FL_TILE) void k_flow_sort_scatter(Dev D, FlowArgs F
 //    (SetPoolDepth, engine.go:78-80), which the plans, seeing depth 0 as "no level", would not visit;
 //  * a CONS (of any amount) after a zero-volume maker may be in the FIFO (z0, or a REST of 0 earlier in
 //    the run): the fills would have to pop it (engine.go:145-175).
-// A REST of 0 with depth > 0 and no CONS after it is an ordinary FIFO append (fl_wplan).
+// A REST of 0 with depth > 0 and no CONS after it is an ordinary FIFO append (fl_wplan).  Books with
+// DELs (the cancel path): a cancel lowers the depth like a CONS; a CONS of 0 (a zero-volume taker,
+// whose one 0-fill the cancel path's events do not model) is a hazard as well.
 __global__ __launch_bounds__(FL_LVB_T) void k_flow_zero_check(Dev D, FlowArgs F) {
   const uint32_t h = F.h0 + blockIdx.y, q = blockIdx.x, tid = threadIdx.x;
   if (h >= fl_hend(D, F)) return;
   FlowHdr* hd = &F.hdr[h];
-  if (hd->ok != FL_OK_ADD || (hd->nzero == 0 && hd->nzlev == 0) || q == 0 || q > hd->nl) return;
+  const bool canc = hd->ok == FL_OK_CANCEL && !hd->fc_bad;
+  if ((hd->ok != FL_OK_ADD && !canc) || (hd->nzero == 0 && hd->nzlev == 0) || q == 0 || q > hd->nl) return;
   const FlowLvl* Lq = F.lvl + h * FL_CAP + q;
   const uint32_t cnt = Lq->cnt;
   if (!cnt) return;
@@ -3014,10 +3049,11 @@ __global__ __launch_bounds__(FL_LVB_T) void k_flow_zero_check(Dev D, FlowArgs F)
     SEnt e{};
     if (valid) e = R[i];
     const bool isr = valid && e.kind == TK_REST, isc = valid && e.kind == TK_CONS, zr = isr && e.amt == 0;
+    const bool isx = valid && e.kind == TK_CANC;
     int64_t tot, tz;
-    const int64_t before = run + fl_blk_excl(isr ? e.amt : isc ? -e.amt : 0, &tot);
+    const int64_t before = run + fl_blk_excl(isr ? e.amt : (isc || isx) ? -e.amt : 0, &tot);
     const int64_t zb = fl_blk_excl(zr ? 1 : 0, &tz);
-    haz = haz || (zr && before == 0) || (isc && (zero || zb > 0));
+    haz = haz || (zr && before == 0) || (isc && (zero || zb > 0 || (canc && e.amt == 0)));
     run += tot;
     zero = zero || tz > 0;
   }
@@ -3037,10 +3073,14 @@ __global__ __launch_bounds__(FL_CAP) void k_flow_stale_check(Dev D, BatchArgs B,
   const uint32_t h = F.h0 + blockIdx.x, q = threadIdx.x;
   if (h >= fl_hend(D, F)) return;
   FlowHdr* hd = &F.hdr[h];
-  if (hd->ok != FL_OK_ADD || (hd->nstale == 0 && hd->haz == 0)) return;
-  if (q == 0) haz = hd->haz;
+  const bool canc = hd->ok == FL_OK_CANCEL;  // (its levels: k_fc_stale_level, which ran before)
+  if ((hd->ok != FL_OK_ADD && !canc) || (hd->nstale == 0 && hd->haz == 0 && hd->nwrong == 0)) return;
+  if (q == 0) {
+    haz = hd->haz;
+    if (hd->nwrong) ctr_add(D, C_FLOW_WRONG, 1ull);
+  }
   __syncthreads();
-  if (q >= 1 && q <= hd->nl) {
+  if (!canc && q >= 1 && q <= hd->nl) {
     const FlowLvl f = F.lvl[h * FL_CAP + q];
     if (fl_stale0(f) && f.cnt) {
       const SEnt e = F.srt[FL_TOUCH_MUL * hd->beg + f.base];

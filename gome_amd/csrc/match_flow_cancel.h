@@ -22,7 +22,11 @@
 //   k_fc_hash_claim / k_fc_hash_count   (symbol, oid) table of the books' ADD / DEL records
 //   k_fc_resolve    each DEL's target: an earlier admitted ADD of the segment (new maker) or a
 //                   resting node (old maker, the cancel index); Q3 (wrong price) and DELs whose
-//                   oid is not resting are no-ops; Q2 (wrong side) and duplicate oids decline
+//                   oid is not resting are no-ops; duplicate oids decline; Q2 (wrong side:
+//                   the depth and FIFO change as for the maker's side, only the ZREM misses,
+//                   engine.go:87-116) is taken by the head books' lane plans, which then
+//                   compute with the maker's side (fc_del_sale) and leave the membership to
+//                   k_fc_stale_level; every other book declines
 //   k_fc_oldwalk    old targets' FIFO ranks, arrival ends and volumes (a walk of their level)
 //   head books, tile-parallel: k_fc_pcnt / k_fc_pscan / k_fc_prank   targeted ADDs' ranks per
 //                   level, each DEL's count of targets that arrived before it, and the (level,
@@ -98,6 +102,12 @@ __device__ __forceinline__ unsigned long long fc_key(const FlowArgs& F, uint32_t
   return (static_cast<unsigned long long>(F.fc_gen & FC_GEN_MASK) << 53) |
          (static_cast<unsigned long long>(sym + 1) << 32) | oid;
 }
+
+// The side of the target of the DEL at segment position b (the maker's: a wrong-side cancel's
+// request says the other, Q2), which k_fc_resolve keeps in FlowArgs::fc_rank (a DEL position's
+// entry is free: ranks are the targeted ADDs').  (Read back from there rather than reloaded from
+// the node or the ADD: the dual-source load miscompiled beside the window code, gfx950.)
+__device__ __forceinline__ bool fc_del_sale(const FlowArgs& F, uint32_t b) { return F.fc_rank[b] != 0u; }
 
 // Slice [b0, b1) of book h's segment for block x of `nx`.
 __device__ __forceinline__ void fc_slice(const FlowHdr& hd, uint32_t x, uint32_t nx, uint32_t& b0, uint32_t& b1) {
@@ -231,6 +241,9 @@ __global__ __launch_bounds__(256) void k_fc_resolve(Dev D, BatchArgs B, FlowArgs
   const FlowHdr hd = F.hdr[h];
   FlowLvl* LV = fl_lvls(F, h);
   const uint32_t lmask = hd.ok == FL_OK_DEEP ? 0x3FFFu : 127u;  // a record's level bits
+  // wrong-side cancels (Q2): the head books' lane plans, which k_fc_stale_level checks and hands
+  // to the legacy kernel when the stale member they make is observable
+  const bool q2_ok = hd.ok == FL_OK_CANCEL && h < FL_HEAD && hd.end - hd.beg >= LEGACY_HOT_MIN;
   uint32_t b0, b1;
   fc_slice(hd, blockIdx.x, gridDim.x, b0, b1);
   for (uint32_t b = b0 + threadIdx.x; b < b1; b += blockDim.x) {
@@ -254,10 +267,17 @@ __global__ __launch_bounds__(256) void k_fc_resolve(Dev D, BatchArgs B, FlowArgs
       if (loc != NIL) { fc_decline(F, h, FC_BAD_Q7); continue; }  // the oid rests already: duplicate (Q7)
       const Prep a = prep_at(B, e.add_pos);
       if (a.price != q.price) continue;                 // S:link:<request price> misses (Q3)
-      if ((a.side == GOME_SALE) != sale) { fc_decline(F, h, FC_BAD_Q2); continue; }  // wrong side (Q2)
+      const bool wrong = (a.side == GOME_SALE) != sale;  // wrong side (Q2)
+      if (wrong && !q2_ok) { fc_decline(F, h, FC_BAD_Q2); continue; }
+      if (a.vol == 0) atomicOr(&F.hdr[h].haz, 1u);  // a zero-volume maker's cancel (Q6): k_flow_stale_check
       d.kind = FC_NEW;
       d.tgt = e.add_pos;
+      F.fc_rank[b] = a.side == GOME_SALE ? 1u : 0u;
       d.li = static_cast<uint32_t>(F.ord8[hd.obase + (e.add_pos - hd.beg)] >> 32) & lmask;
+      if (wrong) {
+        atomicAdd(&F.hdr[h].nwrong, 1u);
+        atomicAdd(&LV[d.li].c_wrong, 1u);
+      }
       F.fc_del[b] = d;
       F.fc_tg[e.add_pos] = b + 1;
       continue;
@@ -266,11 +286,18 @@ __global__ __launch_bounds__(256) void k_fc_resolve(Dev D, BatchArgs B, FlowArgs
     if (D.chdr[loc / CH].price != q.price) continue;                     // Q3
     const Node nd = D.nodes[loc];
     if (nd.rem < 0) continue;
-    if ((nd.tx == GOME_SALE) != sale) { fc_decline(F, h, FC_BAD_Q2); continue; }   // Q2
+    const bool wrong = (nd.tx == GOME_SALE) != sale;  // Q2
+    if (wrong && !q2_ok) { fc_decline(F, h, FC_BAD_Q2); continue; }
+    if (nd.rem == 0) atomicOr(&F.hdr[h].haz, 1u);  // a zero-volume maker's cancel (Q6): k_flow_stale_check
     const uint32_t li = fc_level_of(LV, hd.nl, q.price);
     if (li == 0) { fc_decline(F, h, FC_BAD_LEVEL); continue; }
+    if (wrong) {
+      atomicAdd(&F.hdr[h].nwrong, 1u);
+      atomicAdd(&LV[li].c_wrong, 1u);
+    }
     d.kind = FC_OLD;
     d.tgt = loc;
+    F.fc_rank[b] = nd.tx == GOME_SALE ? 1u : 0u;
     d.ixs = ixs;
     d.li = li;
     F.fc_del[b] = d;
@@ -501,7 +528,7 @@ __global__ __launch_bounds__(FC_PASS_T) void k_fc_pass(Dev D, BatchArgs B, FlowA
         if (d.kind != FC_NONE) {
           isd = true;
           k = d.li;
-          sale = prep_at(B, b).side == GOME_SALE;
+          sale = fc_del_sale(F, b);
           qkey = k | (sale ? 128u : 0u);
         }
       }
@@ -549,7 +576,7 @@ __global__ __launch_bounds__(FC_PASS_T) void k_fc_pass(Dev D, BatchArgs B, FlowA
     if (prep_at(B, b).action != GOME_DEL) continue;
     const FcDel d = F.fc_del[b];
     if (d.kind == FC_NONE) continue;
-    const uint32_t nb = fc_window(F, hd, LV, b, d, d.rank, d.nb, prep_at(B, b).side == GOME_SALE);
+    const uint32_t nb = fc_window(F, hd, LV, b, d, d.rank, d.nb, fc_del_sale(F, b));
     nbsum += nb;
     atomicMax(&mw_s, nb + 1u);
     if (nb >= FC_NB_MAX) atomicOr(&bad_s, FC_BAD_RING);
@@ -571,7 +598,7 @@ __global__ __launch_bounds__(FC_PASS_T) void k_fc_pass(Dev D, BatchArgs B, FlowA
     const uint32_t b = hd.beg + i;
     if (prep_at(B, b).action != GOME_DEL) continue;
     const FcDel d = F.fc_del[b];
-    if (d.kind != FC_NONE) F.ord8[hd.obase + i] = fc_del_rec(F, hd, LV, b, d, prep_at(B, b).side == GOME_SALE);
+    if (d.kind != FC_NONE) F.ord8[hd.obase + i] = fc_del_rec(F, hd, LV, b, d, fc_del_sale(F, b));
   }
 }
 
@@ -685,7 +712,7 @@ __global__ __launch_bounds__(FL_TILE) void k_fc_prank(Dev D, BatchArgs B, FlowAr
         if (d.kind != FC_NONE) {
           isd = true;
           k = d.li;
-          qkey = k | (prep_at(B, b).side == GOME_SALE ? 128u : 0u);
+          qkey = k | (fc_del_sale(F, b) ? 128u : 0u);
         }
       }
     }
@@ -736,7 +763,7 @@ __global__ __launch_bounds__(256) void k_fc_pwin(Dev D, BatchArgs B, FlowArgs F,
     const FcDel d = F.fc_del[b];
     if (d.kind == FC_NONE) continue;
     const uint32_t rk = d.kind == FC_NEW ? F.fc_rank[d.tgt] : d.rank;
-    const uint32_t nb = fc_window(F, hd, LV, b, d, rk, d.nb, prep_at(B, b).side == GOME_SALE);
+    const uint32_t nb = fc_window(F, hd, LV, b, d, rk, d.nb, fc_del_sale(F, b));
     nbsum += nb;
     atomicMax(&mw_s, nb + 1u);
     if (nb >= FC_NB_MAX) bad |= FC_BAD_RING;
@@ -776,7 +803,7 @@ __global__ __launch_bounds__(256) void k_fc_precs(Dev D, BatchArgs B, FlowArgs F
       if (q.action == GOME_DEL) {
         d = F.fc_del[b];
         isd = d.kind != FC_NONE;
-        sale = q.side == GOME_SALE;
+        sale = isd && fc_del_sale(F, b);
       }
     }
     const bool longw = isd && d.nb > 32;
@@ -820,6 +847,86 @@ __global__ void k_fc_route(Dev D, FlowArgs F) {
   if (h < fl_hend(D, F) && fc_dels(F, h) && F.hdr[h].fc_bad) {
     F.hdr[h].ok = 0;  // (a declined deep book's price set was cleared by k_fd_decline)
     F.hdr[h].deep = 0;
+  }
+}
+
+// ---- after the plan and the level sort: stale members of the head books with DELs (Q2) ------
+// A level's side-set membership follows its last state-setting event in time order: a REST of side
+// s makes it a member of s (ZADD, engine.go:80); a fill or a cancel that leaves depth 0 ZREMs the
+// maker's set (DeletePoolMatchOrder / DeletePoolDepth, nodepool.go:76-83), except that a wrong-side
+// cancel ZREMs the request's set, which leaves the level a stale member of s (no FIFO, depth 0).
+// Takers pass a stale member by (MatchOrder returns at an empty FIFO) and the plan, seeing depth 0,
+// passes it too; a same-side REST heals it.  A REST on the other side while the level is stale would
+// put the price in both sets: hazard, the book goes to the legacy kernel (k_flow_stale_check).  One
+// block per (book, level) with a stale member at batch start or a wrong-side cancel, the run in
+// time order with block scans: the depth after each touch, then the last state before each
+// (codes ST_*, max-scan of (index, code)); FlowLvl::mfin gets the level's stale membership after
+// the batch (fc_write_level keeps it).
+enum : uint32_t { ST_BUY = 1, ST_SALE = 2, ST_NONE = 3, ST_STALE_BUY = 4, ST_STALE_SALE = 5 };
+
+__global__ __launch_bounds__(FL_LVB_T) void k_fc_stale_level(Dev D, BatchArgs B, FlowArgs F) {
+  const uint32_t h = F.h0 + blockIdx.y, q = blockIdx.x, tid = threadIdx.x;
+  if (h >= fl_hend(D, F)) return;
+  FlowHdr* hd = &F.hdr[h];
+  if (hd->ok != FL_OK_CANCEL || hd->fc_bad || (hd->nstale == 0 && hd->nwrong == 0) || q == 0 || q > hd->nl) return;
+  FlowLvl* Lq = F.lvl + h * FL_CAP + q;
+  const bool st0 = fl_stale0(*Lq);
+  if (!st0 && Lq->c_wrong == 0) return;
+  const uint32_t cnt = Lq->cnt, beg = hd->beg;
+  const SEnt* R = F.srt + FL_TOUCH_MUL * beg + Lq->base;
+  uint32_t state = st0 ? (Lq->mem0 == M_SALE ? ST_STALE_SALE : ST_STALE_BUY)
+                       : Lq->d0 > 0 ? (Lq->mem0 == M_SALE ? ST_SALE : ST_BUY) : ST_NONE;
+  uint32_t carry = 0;      // (index + 1) << 3 | code of the last state-setting touch of earlier chunks
+  int64_t run = Lq->d0;    // the level's depth before the chunk
+  bool haz = false;
+  for (uint32_t c0 = 0; c0 < cnt; c0 += FL_LVB_T) {
+    const uint32_t i = c0 + tid;
+    const bool valid = i < cnt;
+    SEnt e{};
+    if (valid) e = R[i];
+    const bool isr = valid && e.kind == TK_REST, isc = valid && e.kind == TK_CONS, isx = valid && e.kind == TK_CANC;
+    int64_t tot;
+    const int64_t after = run + fl_blk_excl(isr ? e.amt : (isc || isx) ? -e.amt : 0, &tot) +
+                          (isr ? e.amt : (isc || isx) ? -e.amt : 0);
+    bool rsale = false;
+    uint32_t code = 0;
+    if (isr) {
+      rsale = prep_at(B, beg + e.j).side == GOME_SALE;
+      code = rsale ? ST_SALE : ST_BUY;
+    } else if ((isc || isx) && e.amt > 0 && after == 0) {
+      code = ST_NONE;
+      if (isx) {
+        const bool msale = fc_del_sale(F, beg + e.j);
+        if ((prep_at(B, beg + e.j).side == GOME_SALE) != msale) code = msale ? ST_STALE_SALE : ST_STALE_BUY;
+      }
+    }
+    uint32_t mtot;
+    const uint32_t prev_key = max(carry, fl_blk_max_excl(code ? ((i + 1u) << 3) | code : 0u, &mtot));
+    const uint32_t prev = prev_key ? (prev_key & 7u) : state;
+    if (isr && (prev == (rsale ? ST_STALE_BUY : ST_STALE_SALE))) haz = true;  // the other side's stale price
+    carry = max(carry, mtot);
+    run += tot;
+  }
+  if (__syncthreads_or(haz) && tid == 0) atomicOr(&hd->haz, 1u);
+  if (tid == 0) {
+    const uint32_t fin = carry ? (carry & 7u) : state;
+    Lq->mfin = fin == ST_STALE_BUY ? M_BUY : fin == ST_STALE_SALE ? M_SALE : 0u;
+  }
+}
+
+// A head book with DELs handed to the legacy kernel after its plan (k_flow_stale_check): its old
+// targets' marks go (as k_fc_unmark's for a declined book).
+__global__ __launch_bounds__(256) void k_fc_unmark_bailed(Dev D, BatchArgs B, FlowArgs F) {
+  const uint32_t h = F.h0 + blockIdx.y;
+  if (h >= fl_hend(D, F)) return;
+  const FlowHdr hd = F.hdr[h];
+  if (!hd.bail || !hd.ndel) return;
+  uint32_t b0, b1;
+  fc_slice(hd, blockIdx.x, gridDim.x, b0, b1);
+  for (uint32_t b = b0 + threadIdx.x; b < b1; b += blockDim.x) {
+    if (prep_at(B, b).action != GOME_DEL) continue;
+    const FcDel d = F.fc_del[b];
+    if (d.kind == FC_OLD) D.nodes[d.tgt].pad = 0;
   }
 }
 
@@ -1520,15 +1627,18 @@ __device__ __forceinline__ Level fc_write_level(const Dev& D, const BatchArgs& B
   // survivors among the new makers: not cancelled, not filled to the end (in FIFO order); a
   // maker starting before the consumption end keeps e + v - cfin
   uint32_t S = 0;
+  bool zl = f.z0 != 0;  // the level may hold zero-volume makers (Q6, Level::pad L_ZERO)
   for (uint32_t c0 = 0; c0 < V.nrest; c0 += 64) {
     const uint32_t i = c0 + lane;
     bool sv = false;
     if (i < V.nrest) {
       const RsEnt r = V.RS[i];
       sv = r.pad0 == NIL && r.e + r.v > f.cfin;
+      zl = zl || (sv && r.v == 0);
     }
     S += __popcll(__ballot(sv));
   }
+  x.pad = __ballot(zl) ? L_ZERO : 0u;
   const bool fresh = f.nlive0 == 0;
   const uint32_t s0 = fresh ? 0u : f.tslot;
   const uint32_t room = fresh ? 0u : CH - s0;
@@ -1611,6 +1721,9 @@ __device__ __forceinline__ Level fc_write_level(const Dev& D, const BatchArgs& B
     if (((q < 64 ? hd.amask[0] : hd.amask[1]) >> (q & 63)) & 1ull) mem |= M_SALE;
     if (((q < 64 ? hd.bmask[0] : hd.bmask[1]) >> (q & 63)) & 1ull) mem |= M_BUY;
   }
+  // a level that ends without makers: no member, or a stale one (Q2, k_fc_stale_level)
+  const bool mem_ok = x.nlive > 0 || mem == 0 || mem == f.mfin;
+  if (x.nlive == 0) mem = f.mfin;
   x.member = static_cast<uint8_t>(mem);
   if (x.nlive == 0) {
     x.hslot = x.tslot = 0;
@@ -1625,8 +1738,7 @@ __device__ __forceinline__ Level fc_write_level(const Dev& D, const BatchArgs& B
     x.tail = need ? chunk_id(need - 1) : f.tail;
     x.tslot = static_cast<uint8_t>(need ? (S - room) - (need - 1) * CH : s0 + S);
   }
-  const bool ok = (x.nlive > 0) == (x.depth > 0) && (x.nlive > 0) == (mem == M_BUY || mem == M_SALE) &&
-                  (x.nlive > 0 || mem == 0);
+  const bool ok = (x.nlive > 0) == (x.depth > 0) && (x.nlive == 0 || mem == M_BUY || mem == M_SALE) && mem_ok;
   if (!ok && lane == 0) atomicOr(&D.st->err, ERR_CORRUPT);
   return x;
 }

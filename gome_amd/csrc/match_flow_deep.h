@@ -189,7 +189,7 @@ __device__ __forceinline__ void k_deep_prep_b_one(Dev D, BatchArgs B, FlowArgs F
   if (tid == 0) {
     // (a segment with DELs takes the W32DC plan after the cancel prep)
     const uint64_t tiles = (static_cast<uint64_t>(FL_TOUCH_MUL) * (end - beg) + FL_TILE - 1) / FL_TILE;
-    bad = (P->d_bad || (bk.pad & (BOOK_QUIRK | BOOK_ZERO)) || bk.n_lvl > DEEP_CAP - 2 || tiles > fd_tiles(F, ds)) ? 1u : 0u;
+    bad = (P->d_bad || (bk.pad & (BOOK_QUIRK | BOOK_ZERO | BOOK_STALE)) || bk.n_lvl > DEEP_CAP - 2 || tiles > fd_tiles(F, ds)) ? 1u : 0u;
     if (!bad && P->d_dels) {  // the W32DC plan needs the cancel chain
       ctr_add(D, C_WANT_CANC, 1ull);
       if (!(F.chains & FL_CH_CANCEL)) bad = 1;

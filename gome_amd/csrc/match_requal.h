@@ -32,7 +32,8 @@ namespace gome {
 //    L_ZERO on its level and BOOK_ZERO on the book), and the level's FIFO holds exactly nlive nodes
 //    summing to its depth.
 // The level checks come first: a book that is still stale fails them without a FIFO walk.
-// Returns -1 (no), 0 (yes), 1 (yes, with zero-volume makers: BOOK_ZERO); sets the levels' L_ZERO.
+// Returns -1 (no), else the book's flags after it: BOOK_ZERO (zero-volume makers), BOOK_STALE (stale
+// members); sets the levels' L_ZERO.
 __device__ __forceinline__ int book_requalifies(const Dev& D, uint32_t sym) {
   const uint32_t lane = lane_id();
   const Book bk = D.books[sym];
@@ -40,6 +41,7 @@ __device__ __forceinline__ int book_requalifies(const Dev& D, uint32_t sym) {
   Level* L = D.lvl + uni(bk.lvl_base);
   int32_t last_bid = -1;
   uint32_t first_ask = NIL;
+  bool anys = false;
   for (uint32_t w0 = 0; w0 < nl; w0 += 64) {
     const uint32_t k = w0 + lane;
     bool bad = false, bid = false, ask = false;
@@ -53,6 +55,7 @@ __device__ __forceinline__ int book_requalifies(const Dev& D, uint32_t sym) {
       else bad = x.nlive != 0 || x.depth != 0 || x.head != NIL;
     }
     if (__ballot(bad)) return -1;
+    if (__ballot(k < nl && L[k].member && !bid && !ask)) anys = true;
     const unsigned long long bm = __ballot(bid), am = __ballot(ask);
     if (bm) last_bid = static_cast<int32_t>(w0 + 63u - static_cast<uint32_t>(__builtin_clzll(bm)));
     if (am && first_ask == NIL) first_ask = w0 + static_cast<uint32_t>(__builtin_ctzll(am));
@@ -92,7 +95,7 @@ __device__ __forceinline__ int book_requalifies(const Dev& D, uint32_t sym) {
       if (lane == 0) L[k].pad = L_ZERO;
     }
   }
-  return anyz ? 1 : 0;
+  return static_cast<int>((anyz ? BOOK_ZERO : 0u) | (anys ? BOOK_STALE : 0u));
 }
 
 // After a batch's book kernels: the books the cold / resume waves listed (Dev::quirk) and the
@@ -118,7 +121,7 @@ __global__ __launch_bounds__(256) void k_requalify(Dev D, BatchArgs B, const Flo
     if (lane_id() == 0) {
       ctr_add(D, C_QUIRK_CHECKED, 1);
       if (ok >= 0) {
-        D.books[sym].pad = ok ? BOOK_ZERO : 0u;
+        D.books[sym].pad = static_cast<uint32_t>(ok);
         ctr_add(D, C_REQUAL, 1);
       }
     }

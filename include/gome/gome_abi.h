@@ -282,6 +282,8 @@ typedef struct gome_stats {
   uint64_t n_flow_zero;                       /* head books planned on the flow path with
                                                  zero-volume ADDs or zero-volume makers (Q6;
                                                  ABI >= 11)                                 */
+  uint64_t n_flow_wrong;                      /* head books whose wrong-side cancels (Q2)
+                                                 the flow cancel path applied (ABI >= 11)   */
 } gome_stats;
 
 typedef struct gome_engine gome_engine;

@@ -26,7 +26,7 @@ def _run(mode, batches=5):
     hot = int(z.rank_to_id[0])
     eng = Engine(max_symbols=100000, max_batch=N, max_nodes=batches * N, max_levels=1 << 22)
     orc = Oracle(100000)
-    kinds, req = [], []
+    kinds, req, wrong = [], [], []
     for i in range(batches):
         b = gen(N).copy()
         if i == 1:
@@ -39,28 +39,32 @@ def _run(mode, batches=5):
         assert int(fl["symbol_id"][0]) == hot
         kinds.append(int(fl["kind"][0]))
         req.append((st["n_quirk_checked"], st["n_requalified"]))
+        wrong.append(int(st["n_flow_wrong"]))
     _cmp_books(eng, orc, _hot_and_random(z, 100000, k_rand=50), mode)
     assert eng.stats()["n_resting"] == orc.resting()
-    return kinds, req
+    return kinds, req, wrong
 
 
 def test_quirks_heal_and_the_hottest_book_returns_to_the_flow_path():
-    kinds, req = _run("heal")
-    assert kinds[0] != 0 and kinds[1] == 0, kinds        # flow, then legacy for the injected batch
-    healed = [i for i, (c, r) in enumerate(req) if r]
-    assert healed and healed[0] <= 2, req                 # healed within two batches
-    assert all(k != 0 for k in kinds[healed[0] + 1:]), (kinds, req)
+    """The quirks at the best bids, where the stream soon trades: the injected batch's wrong-side
+    cancels run on the flow cancel path, and the zero-volume maker, which a taker soon reaches, hands
+    the book to the legacy kernel after its plan (k_flow_zero_check); k_requalify returns it to the
+    flow path once the reference's state has healed."""
+    kinds, req, wrong = _run("heal")
+    assert kinds[0] != 0 and wrong[1] >= 1, (kinds, wrong)
+    assert all(k != 0 for k in kinds[3:]), (kinds, req)
 
 
 def test_quirks_that_do_not_heal_stay_on_the_flow_path():
     """The same quirks at the bottom of the bid book, which the stream never reaches again: batch 1
     applies them on the legacy kernel; the stale member (Q2) and the zero-volume maker (Q6, marked
     L_ZERO / BOOK_ZERO by k_requalify) then ride along on the flow path (round 5; in round 4 the book
-    stayed on the ~23x slower legacy kernel for good), exact throughout."""
-    kinds, req = _run("stuck", batches=5)
-    assert kinds[0] != 0 and kinds[1] == 0, kinds
-    assert all(k != 0 for k in kinds[2:]), (kinds, req)
-    assert req[1][1] >= 1, req
+    stayed on the ~23x slower legacy kernel for good), exact throughout; the injected batch itself runs
+    on the flow cancel path (its wrong-side cancels, FlowHdr::nwrong, and the zero-volume ADD resting
+    behind a level's makers)."""
+    kinds, req, wrong = _run("stuck", batches=5)
+    assert all(k != 0 for k in kinds), (kinds, req)   # the injected batch too (round 5)
+    assert wrong[1] >= 1, wrong
 
 
 # ---- stale members on the flow path (Q2 alone; VERDICT r4 next #3) -----------------------------
@@ -81,7 +85,7 @@ def _stale_inject(b, sym, eng):
     return info["q2_price"]
 
 
-def _stale_run(rank, seed, hazard, batches=5):
+def _stale_run(rank, seed, hazard, batches=5, edit1=None):
     """Batch 1: a stale member made (on the legacy kernel: a book with wrong-side DELs); then the
     book on the flow path with it; with `hazard`, batch 2's first record of the book is a SALE at
     the stale price with a volume above the whole bid side, so it sweeps every real bid and rests
@@ -98,6 +102,8 @@ def _stale_run(rank, seed, hazard, batches=5):
         b = gen(N).copy()
         if i == 1:
             p = _stale_inject(b, sym, eng)
+            if edit1 is not None:
+                edit1(b, sym, p)
         elif i >= 2:
             _move_away(b, sym, p)
             if hazard and i == 2:
@@ -108,7 +114,7 @@ def _stale_run(rank, seed, hazard, batches=5):
         st = eng.stats()
         fl = eng.debug_flow_books()
         kind = int(fl["kind"][list(fl["symbol_id"]).index(sym)]) if sym in list(fl["symbol_id"]) else -1
-        out.append((kind, int(st["n_flow_stale"]), int(st["n_flow_bail"])))
+        out.append((kind, int(st["n_flow_stale"]), int(st["n_flow_bail"]), int(st["n_flow_wrong"])))
     _cmp_books(eng, orc, [sym] + _hot_and_random(z, 100000, k_rand=30), f"stale rank {rank}")
     assert eng.stats()["n_resting"] == orc.resting()
     lv = orc.levels(sym)
@@ -120,8 +126,8 @@ def test_stale_member_stays_on_the_flow_path():
     from the batch after the one that made it (k_requalify accepts it, n_flow_stale), exact, and the
     stale member is still there at the end (levels compared with the oracle's)."""
     out, lv = _stale_run(0, 42, hazard=False)
-    assert out[1][0] == 0, out                            # (the wrong-side cancels: legacy)
-    assert all(k != 0 and s >= 1 and x == 0 for k, s, x in out[2:]), out
+    assert out[1][0] != 0 and out[1][3] >= 1 and out[1][2] == 0, out  # (the wrong-side cancels: flow)
+    assert all(k != 0 and s >= 1 and x == 0 for k, s, x, _ in out[2:]), out
     assert len(lv) == 1 and lv["in_buy"][0] == 1 and lv["n_nodes"][0] == 0, lv
 
 
@@ -134,6 +140,37 @@ def test_near_book_hand_over():
     """The same for the second-hottest book (the near books' reconstruction on the hot stream)."""
     out, _ = _stale_run(1, 43, hazard=True)
     assert out[2][1] >= 1 and out[2][2] >= 1, out
+
+
+def test_wrong_side_cancels_then_a_rest_across_in_the_same_batch_hand_over():
+    """The wrong-side cancels empty the lowest bid (a stale member of S:BUY from then on) and, later
+    in the same batch, a SALE sweeps every bid and rests at that price: k_fc_stale_level finds the
+    REST on the other side of the stale price and the book goes to the legacy kernel, exact."""
+    def edit1(b, sym, p):
+        r = np.nonzero(b["symbol_id"] == sym)[0][5000]
+        b["price_fx"][r], b["side"][r], b["action"][r], b["volume_fx"][r] = p, 1, wl.ADD, 10 ** 14
+    out, _ = _stale_run(0, 42, hazard=False, edit1=edit1)
+    assert out[1][0] == 0 and out[1][2] >= 1 and out[1][3] >= 1, out
+
+
+def test_wrong_side_cancel_of_a_new_maker():
+    """A BUY rests at a price of its own between two bids and a DEL with the SALE side cancels it a
+    few records later (the cancel path's new-maker target): the level stays a stale member of
+    S:BUY; at a second such price a later BUY rests again, which heals it.  On the flow path
+    (n_flow_wrong), exact, the levels compared with the oracle's."""
+    def edit1(b, sym, p):
+        rows = np.nonzero((b["symbol_id"] == sym) & (b["action"] == wl.ADD))[0]
+        for k, (a, heal) in enumerate(((2000, False), (3000, True))):
+            pn = p + 10 ** 6 * (k + 2) + 1
+            ra, rd, rh = rows[a], rows[a + 5], rows[a + 10]
+            b["price_fx"][ra], b["side"][ra], b["volume_fx"][ra] = pn, 0, 10 ** 8
+            b["action"][rd], b["flags"][rd], b["price_fx"][rd], b["side"][rd] = wl.DEL, 0, pn, 1
+            b["oid_id"][rd], b["uuid_id"][rd], b["volume_fx"][rd] = b["oid_id"][ra], b["uuid_id"][ra], 10 ** 8
+            if heal:
+                b["price_fx"][rh], b["side"][rh], b["volume_fx"][rh] = pn, 0, 10 ** 8
+    out, _ = _stale_run(0, 42, hazard=False, edit1=edit1)
+    assert all(k != 0 and x == 0 for k, _, x, _ in out), out
+    assert out[1][3] >= 1, out
 
 
 # ---- zero-volume ADDs (Q6) on the flow path -----------------------------------------------------

@@ -371,9 +371,10 @@ def main():
     ap.add_argument("--force-pg", action="store_true",
                     help="initialise the process group and run the summary gather, the publisher and the "
                          "digest check at N = 1 too (exercises the RCCL path on a one-GPU box)")
-    ap.add_argument("--inject-quirks", choices=("none", "heal", "stuck", "q2heal", "q2stuck"), default="none",
+    ap.add_argument("--inject-quirks", choices=("none", "heal", "stuck", "q2heal", "q2stuck", "zero"), default="none",
                     help="rewrite records of the hottest book in the first timed batch into wrong-side "
-                         "cancels (Q2) of a bid level and a zero-volume ADD (Q6) (workload.inject_quirks); "
+                         "cancels (Q2) of a bid level and a zero-volume ADD (Q6), or (zero) zero-volume "
+                         "ADDs only (workload.inject_quirks); "
                          "the line's quirk_batch reports that batch's device time beside its neighbours'")
     ap.add_argument("--consumer-msgs", type=int, default=1 << 17,
                     help="JSON OrderNode messages of the consumer leg (0: off)")
@@ -530,7 +531,8 @@ def main():
         dev_batches[warm].copy_(torch.from_numpy(host_batches[warm].view(np.uint8)))
         torch.cuda.synchronize()
         note(f"injected into batch {warm} (the first timed one): {injected['q2_cancels']} wrong-side cancels"
-             + ("" if injected["q6_oid"] is None else ", one zero-volume ADD"))
+             + ("" if injected["q6_oid"] is None else f", {len(injected['records']) - injected['q2_cancels']} "
+                "zero-volume ADDs"))
     if use_pg:
         dist.barrier()
     if pub is not None:
@@ -606,6 +608,7 @@ def main():
 
         host_ms = {"submit": 0.0, "collect": 0.0}  # host time inside the two calls (timed steps)
         tdone = []  # host time of each collect's return (the steady-state interval: their median gap)
+        edev = []   # each collected batch's device time (Status timing: first kernel to last)
 
         def run_pipe(lo, hi, lats):
             tsub = {}
@@ -615,6 +618,7 @@ def main():
                 ev, st = eng.collect(copy=False)
                 host_ms["collect"] += (time.perf_counter() - tc) * 1e3
                 tdone.append(time.perf_counter())
+                edev.append(float(st["ms_total"]))
                 done_ev[0] += len(ev)
                 lats.append((time.perf_counter() - tsub[j]) * 1e3)
                 if rank == 0:
@@ -637,6 +641,7 @@ def main():
         done_ev[0] = 0
         host_ms["submit"] = host_ms["collect"] = 0.0
         tdone.clear()
+        edev.clear()
         t1 = time.perf_counter()
         run_pipe(e2e_warm, e2e_warm + e2e_steps, elat)
         torch.cuda.synchronize()
@@ -663,6 +668,7 @@ def main():
                # the median gap between two batches' collects: the pipeline's steady-state step,
                # without the fill (the first H2D) and drain (the last D2H) that a K-step job adds
                "steady_ms_per_step": round(float(np.median(np.diff(tdone))) * 1e3, 3) if len(tdone) > 2 else None,
+               "device_ms_per_batch_median": round(float(np.median(edev)), 3) if edev else None,
                "p50_batch_ms": round(pctl(elat, 0.5), 3), "p99_batch_ms": round(pctl(elat, 0.99), 3),
                "events_per_s": round(e_events / e_el, 1),
                "pcie_bytes_per_step": int(32 * per_rank * world + 48 * e_events / e2e_steps),
@@ -803,7 +809,9 @@ def main():
                 "clean_median_device_ms": round(float(np.median(clean)), 3) if clean else None,
                 "ratio": round(float(sts[0]["ms_total"]) / float(np.median(clean)), 3) if clean else None,
                 "legacy_hot_orders": [int(s["n_hot_orders"]) - int(s["n_flow_orders"]) for s in sts[:3]],
-                "flow_head_orders": [int(s["n_flow_head_orders"]) for s in sts[:3]]}
+                "flow_head_orders": [int(s["n_flow_head_orders"]) for s in sts[:3]],
+                "flow_wrong_zero_stale_bail": [[int(s[k]) for k in ("n_flow_wrong", "n_flow_zero", "n_flow_stale",
+                                                                    "n_flow_bail")] for s in sts[:3]]}
         if consumer is not None:
             consumer["vs_value"] = round(consumer["messages_per_s"] / out["value"], 6)
         if pub is not None and use_pg:

@@ -26,8 +26,11 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <condition_variable>
 #include <deque>
+#include <mutex>
 #include <set>
+#include <thread>
 #include <unordered_set>
 #include <string>
 #include <vector>
@@ -229,6 +232,11 @@ struct Slot {
   uint32_t ev_cap = 0;
   Status* h_st = nullptr;          // page-locked copy of the batch's Status
   gome_event* h_events = nullptr;  // page-locked event copy (gome_collect)
+  // async host batches: the event copy, issued by the engine's copy thread the moment the batch
+  // is done (gome_engine::d2h_loop); d2h_state: 0 none, 1 queued, 2 issued (d2h recorded), 3 failed
+  int d2h_state = 0;
+  hipError_t d2h_err = hipSuccess;
+  hipEvent_t d2h{};
   uint32_t* d_dup = nullptr;       // batch indices of the ADDs rejected as duplicate oids (Q7)
   size_t h_cap = 0;
   hipEvent_t ev0{}, ev1{}, evm0{}, evm1{}, evh0{}, evh1{}, evf0{}, evf1{}, evc0{}, evc1{};
@@ -265,6 +273,9 @@ struct gome_engine {
   hipStream_t flow_stream = nullptr;  // the hottest book's plan (critical path)
   hipStream_t copy_stream = nullptr;  // H2D of records, D2H of events (pipelined path)
   hipStream_t early_stream = nullptr; // the early plan's record work (match_early.h), beside the plan before it
+  hipStream_t d2h_stream = nullptr;   // event copies (gome_collect), beside the next batch's H2D and pipeline
+  hipStream_t h2d_stream = nullptr;   // async host batches' record copies: nothing else on it, so the next
+                                      // batch's H2D never waits behind this batch's work
   // The hottest book's plans on a stream of their own restricted to CUs [0, k), every other engine
   // stream to the rest: the plan wave alone with its CU's instruction cache and L1, and no other
   // kernel's code or data beside it (gome_config.plan_cus, default 8; none below 8 queues)
@@ -437,16 +448,26 @@ struct gome_engine {
       if (*it == p) { (void)hipFree(p); allocs.erase(it); return; }
   }
   ~gome_engine() {
+    if (d2h_thr.joinable()) {
+      {
+        std::lock_guard<std::mutex> lk(d2h_mu);
+        d2h_stop = true;
+      }
+      d2h_cv.notify_all();
+      d2h_thr.join();
+    }
     if (stream) (void)hipStreamSynchronize(stream);
     if (copy_stream) (void)hipStreamSynchronize(copy_stream);
     if (early_stream) (void)hipStreamSynchronize(early_stream);
+    if (d2h_stream) (void)hipStreamSynchronize(d2h_stream);
+    if (h2d_stream) (void)hipStreamSynchronize(h2d_stream);
     for (void* p : allocs) (void)hipFree(p);
     for (void* p : host_allocs) (void)hipHostFree(p);
     for (Slot& S : slots) {
       if (S.h_st) (void)hipHostFree(S.h_st);
       if (S.h_events) (void)hipHostFree(S.h_events);
       for (hipEvent_t ev : {S.ev0, S.ev1, S.evm0, S.evm1, S.evh0, S.evh1, S.evf0, S.evf1, S.evc0, S.evc1, S.h2d, S.done,
-                            S.evx0, S.evx1})
+                            S.evx0, S.evx1, S.d2h})
         if (ev) (void)hipEventDestroy(ev);
       for (auto& pr : S.ph)
         for (hipEvent_t ev : pr)
@@ -468,6 +489,8 @@ struct gome_engine {
     if (pl_join) (void)hipEventDestroy(pl_join);
     if (flow_stream) (void)hipStreamDestroy(flow_stream);
     if (copy_stream) (void)hipStreamDestroy(copy_stream);
+    if (d2h_stream) (void)hipStreamDestroy(d2h_stream);
+    if (h2d_stream) (void)hipStreamDestroy(h2d_stream);
     if (early_stream) (void)hipStreamDestroy(early_stream);
     if (stream) (void)hipStreamDestroy(stream);
   }
@@ -497,6 +520,69 @@ struct gome_engine {
     return k;
   }
   gome_status collect(const gome_event** evs, size_t* nev);
+  // The copy thread: async host batches' event copies, issued the moment each batch is done (its
+  // count is known then), so they run beside the next batch's H2D and pipeline instead of waiting
+  // for gome_collect.  (Round 5, config 2 e2e: a copy issued at submit behind a wait on the batch
+  // held the copy engine and the next H2D behind it, 8.2 ms a step; a kernel writing the events to
+  // mapped host memory slowed the next batch's pipeline 2.4x; a copy issued at gome_collect kept
+  // the host from the next submit for its whole length, 5.2 ms.)
+  std::thread d2h_thr;
+  std::mutex d2h_mu;
+  std::condition_variable d2h_cv;
+  std::deque<uint32_t> d2h_q;
+  bool d2h_stop = false;
+  void d2h_queue(uint32_t sl) {
+    {
+      std::lock_guard<std::mutex> lk(d2h_mu);
+      if (!d2h_thr.joinable()) d2h_thr = std::thread([this] { d2h_loop(); });
+      slots[sl].d2h_state = 1;
+      d2h_q.push_back(sl);
+    }
+    d2h_cv.notify_all();
+  }
+  void d2h_loop() {
+    (void)hipSetDevice(cfg.device);
+    for (;;) {
+      uint32_t sl;
+      {
+        std::unique_lock<std::mutex> lk(d2h_mu);
+        d2h_cv.wait(lk, [&] { return d2h_stop || !d2h_q.empty(); });
+        if (d2h_q.empty()) return;  // (stop, nothing queued)
+        sl = d2h_q.front();
+        d2h_q.pop_front();
+      }
+      Slot& S = slots[sl];
+      hipError_t he = hipEventSynchronize(S.done);
+      const size_t n = he == hipSuccess ? S.h_st->n_events : 0;
+      if (he == hipSuccess && n > S.h_cap) {  // (the caller touches the buffer only after state 2)
+        if (S.h_events) (void)hipHostFree(S.h_events);
+        S.h_events = nullptr;
+        S.h_cap = 0;
+        he = hipHostMalloc(reinterpret_cast<void**>(&S.h_events), (n + n / 4 + 1024) * sizeof(gome_event),
+                           hipHostMallocDefault);
+        if (he == hipSuccess) S.h_cap = n + n / 4 + 1024;
+      }
+      if (he == hipSuccess && n)
+        he = hipMemcpyAsync(S.h_events, S.d_events, n * sizeof(gome_event), hipMemcpyDeviceToHost, d2h_stream);
+      if (he == hipSuccess) he = hipEventRecord(S.d2h, d2h_stream);
+      {
+        std::lock_guard<std::mutex> lk(d2h_mu);
+        S.d2h_err = he;
+        S.d2h_state = he == hipSuccess ? 2 : 3;
+      }
+      d2h_cv.notify_all();
+    }
+  }
+  // slot S's page-locked event buffer with room for `cap` events (none in flight)
+  gome_status host_events(Slot& S, size_t cap) {
+    if (S.h_events) (void)hipHostFree(S.h_events);
+    S.h_events = nullptr;
+    S.h_cap = 0;
+    hipError_t he = hipHostMalloc(reinterpret_cast<void**>(&S.h_events), cap * sizeof(gome_event), hipHostMallocDefault);
+    if (he != hipSuccess) return fail(GOME_E_DEVICE, std::string("event buffer: ") + hipGetErrorString(he));
+    S.h_cap = cap;
+    return GOME_OK;
+  }
   gome_status collect_all();
   gome_status spill_device_events();
   gome_status queue_events(uint32_t slot, size_t n, hipStream_t s);
@@ -569,6 +655,8 @@ gome_status gome_engine::init(const gome_config& c) {
   HIPCHK(new_stream(&hot_stream));
   HIPCHK(new_stream(&flow_stream));
   HIPCHK(new_stream(&copy_stream));
+  HIPCHK(new_stream(&d2h_stream));
+  HIPCHK(new_stream(&h2d_stream));
   for (hipEvent_t* ev : {&fork, &join, &joinf, &prep_h, &prep_t, &fork_adm, &adm_done, &seg_done,
                          &dp_fork, &cnt_fork, &cnt_done, &dw_done, &dl_done, &tl_done, &tob_done, &plan_done,
                          &oidmax_done, &xpre_done, &xprep_done, &xplan_done, &adm_pre_done})
@@ -582,6 +670,7 @@ gome_status gome_engine::init(const gome_config& c) {
     HIPCHK(hipEventCreateWithFlags(&S.h2d, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&S.done, hipEventDisableTiming));
     HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&S.h_st), sizeof(Status), hipHostMallocDefault));
+    HIPCHK(hipEventCreateWithFlags(&S.d2h, hipEventDisableTiming));
   }
   HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_match_hot),
                              hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(HOT_LDS_BYTES)));
@@ -1529,21 +1618,28 @@ gome_status gome_engine::collect(const gome_event** evs, size_t* nev) {
   if (f.n == 0) return GOME_OK;
   Slot& S = slots[f.slot];
   HIPCHK(hipEventSynchronize(S.done));
+  bool copied = false;
+  int ds = 0;
+  {  // an async host batch: the copy thread issued its event copy at its end
+    std::unique_lock<std::mutex> lk(d2h_mu);
+    if (S.d2h_state) {
+      d2h_cv.wait(lk, [&] { return S.d2h_state >= 2; });
+      ds = S.d2h_state;
+      S.d2h_state = 0;
+    }
+  }
+  if (ds) {
+    if (ds == 3) return fail(GOME_E_DEVICE, std::string("event copy: ") + hipGetErrorString(S.d2h_err));
+    HIPCHK(hipEventSynchronize(S.d2h));
+    copied = true;
+  }
   gome_status st = finish(f.slot, f.n);
   if (st != GOME_OK) return st;
   const size_t n = S.h_st->n_events;
-  if (n > S.h_cap) {
-    if (S.h_events) (void)hipHostFree(S.h_events);
-    S.h_events = nullptr;
-    S.h_cap = 0;
-    const size_t cap = n + n / 4 + 1024;
-    HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&S.h_events), cap * sizeof(gome_event), hipHostMallocDefault));
-    S.h_cap = cap;
-  }
-  if (n) {
-    hipStream_t cs = copy_stream;
-    HIPCHK(hipMemcpyAsync(S.h_events, S.d_events, n * sizeof(gome_event), hipMemcpyDeviceToHost, cs));
-    HIPCHK(hipStreamSynchronize(cs));
+  if (!copied && n) {
+    if (n > S.h_cap && (st = host_events(S, n + n / 4 + 1024)) != GOME_OK) return st;
+    HIPCHK(hipMemcpyAsync(S.h_events, S.d_events, n * sizeof(gome_event), hipMemcpyDeviceToHost, d2h_stream));
+    HIPCHK(hipStreamSynchronize(d2h_stream));
   }
   *evs = S.h_events;
   *nev = n;
@@ -1707,10 +1803,12 @@ gome_status gome_submit_batch_async(gome_engine* e, const gome_order* orders, si
   if (n) {
     Slot& S = e->slots[sl];
     e->used = true;
-    // the records travel on the copy stream (beside the batch in flight); the pipeline waits
+    // the records travel on the H2D stream (beside the batch in flight and the last one's event
+    // copy); the pipeline waits.  (On the copy stream, which the pipeline also uses, batch k+2's
+    // H2D queued behind batch k+1's early work: e2e 5.6 ms per config-2 step, round 5.)
     hipError_t he = hipMemcpyAsync(S.d_orders, orders, n * sizeof(gome_order), hipMemcpyHostToDevice,
-                                   e->copy_stream);
-    if (he == hipSuccess) he = hipEventRecord(S.h2d, e->copy_stream);
+                                   e->h2d_stream);
+    if (he == hipSuccess) he = hipEventRecord(S.h2d, e->h2d_stream);
     if (he == hipSuccess) he = hipStreamWaitEvent(e->stream, S.h2d, 0);
     if (he != hipSuccess) return e->fail(GOME_E_DEVICE, hipGetErrorString(he));
     // (no sort ahead here: on the copy stream it delayed the event copies; e2e +2 ms per config-3 batch)
@@ -1718,6 +1816,7 @@ gome_status gome_submit_batch_async(gome_engine* e, const gome_order* orders, si
     st = e->enqueue(S.d_orders, static_cast<uint32_t>(n), e->stream, sl, seq_base, inflight_n);
     e->copy_busy = false;
     if (st != GOME_OK) return st;
+    e->d2h_queue(sl);
   }
   e->flights.push_back(Flight{sl, static_cast<uint32_t>(n), seq_base, false});
   return GOME_OK;

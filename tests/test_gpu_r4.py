@@ -80,7 +80,7 @@ def test_oid_watermark_crossed_and_wrapped_stays_exact():
 
 
 def test_consumer_leg_runs():
-    out = bench.consumer_leg("config3", 100000, 1 << 13, 42, batch=1 << 11, render_threads=2)
+    out = bench.consumer_leg("config3", 100000, 1 << 13, 42, batch=1 << 11, threads=2)
     assert out["messages"] == 1 << 13 and out["messages_per_s"] > 0 and out["matchresults"] > 1000
     assert out["render_events_per_s"]["1"] > 0 and out["render_events_per_s"]["2"] > 0
 

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Measurements on the GPU box.  usage: bash tools/gpu_measure.sh <tag> [parts...]
 #   suite: the GPU test suite;  smoke;  benches: bench lines (e2e, consumer leg, CPU baseline) of
-#   configs 3, 2, 4, 5, 5c;  heal / pg: the quirk-injection line and the RCCL world-1 line;
+#   configs 3, 2, 4, 5, 5c;  heal / quirks / pg: the quirk-injection line(s) and the RCCL world-1 line;
 #   tests=<files, comma-separated>: a subset of the GPU suite (e.g. tests=tests/test_a_layouts_gpu.py);
 #   q4: the config-3 bench line in a process whose HIP runtime has 4 hardware queues;
 #   prof3 / prof2: rocprofv3 trace + FETCH / WRITE passes (profiles/run_rocprof.sh) + summary
@@ -61,6 +61,23 @@ for P in $PARTS; do
     timeout -k 10 400 python3 -u bench.py --workload config3 --inject-quirks heal --no-cpu-baseline --consumer-msgs 0 \
       --step-log $OUT/config3_heal_steps.jsonl > $OUT/config3_heal_bench.jsonl 2> $OUT/config3_heal_bench.log || { tail -20 $OUT/config3_heal_bench.log; exit 4; }
     summ $OUT/config3_heal_bench.jsonl heal ;;
+  quirks)
+    # quirk injection into the first timed batch (bench.py --inject-quirks): Q2 + Q6 at the bottom /
+    # top of the bid book, Q2 alone, Q6 alone
+    for M in stuck q2stuck zero heal; do
+      timeout -k 10 400 python3 -u bench.py --workload config3 --inject-quirks $M --no-cpu-baseline --consumer-msgs 0 \
+        > $OUT/config3_${M}_bench.jsonl 2> $OUT/config3_${M}_bench.log || { tail -20 $OUT/config3_${M}_bench.log; exit 4; }
+      summ $OUT/config3_${M}_bench.jsonl $M
+      python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).readlines()[-1]); print(json.dumps(d.get('quirk_batch')))" $OUT/config3_${M}_bench.jsonl
+    done ;;
+  e2e2|e2e3)
+    # the host path of config 2 / 3 (records from page-locked host memory, events back) at host depths 2 and 3
+    W=config${P#e2e}
+    for DP in 2 3; do
+      timeout -k 10 300 python3 -u bench.py --workload $W --steps 10 --warmup 4 --no-cpu-baseline --consumer-msgs 0 --e2e-depth $DP \
+        > $OUT/${W}_e2e$DP.jsonl 2> $OUT/${W}_e2e$DP.log || { tail -20 $OUT/${W}_e2e$DP.log; exit 13; }
+      python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).readlines()[-1]); e=d['e2e']; print(sys.argv[2], d['ms_per_step'], e['steady_ms_per_step'], e['pcie_bound_ms'], e['host_ms_per_step'], e.get('device_ms_per_batch_median'), e['pcie_peak'])" $OUT/${W}_e2e$DP.jsonl depth$DP
+    done ;;
   pg)
     timeout -k 10 400 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 \
       --master-port 29533 bench.py --gpus 1 --force-pg --backend nccl --no-cpu-baseline --consumer-msgs 0 \

@@ -1,15 +1,17 @@
-// pcie_duplex.hip — PCIe copy rates of one MI355X from page-locked host memory: H2D alone, D2H
-// alone, and both at once on two streams, each way through
-// hipMemcpyAsync (the runtime picks SDMA or a blit kernel) and through a kernel that reads / writes
-// the host buffer directly (mapped page-locked memory, 16-B lanes).
+// pcie_duplex.hip — PCIe copy rates of one MI355X from page-locked host memory (VERDICT
+// r4 next #6): H2D alone, D2H alone and both at once on two streams through hipMemcpyAsync, for
+// each hipHostMalloc flavour (the engine's event buffer and the caller's record buffers are
+// hipHostMallocDefault), and the same through a kernel that reads / writes mapped host memory
+// (16-B lanes).  One JSON line.
 // Build: hipcc --offload-arch=gfx950 -O2 tools/pcie_duplex.hip -o tools/pcie_duplex
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
-#include <algorithm>
+#include <string>
 
 #define CK(x)                                                                        \
   do {                                                                               \
@@ -34,20 +36,13 @@ static double now_s() {
 int main(int argc, char** argv) {
   const size_t nb = (argc > 1 ? std::strtoull(argv[1], nullptr, 10) : 256) << 20;
   const int reps = 5;
-  void *h_in, *h_out, *d_in, *d_out;
-  CK(hipHostMalloc(&h_in, nb, hipHostMallocMapped));
-  CK(hipHostMalloc(&h_out, nb, hipHostMallocMapped));
+  void *d_in, *d_out;
   CK(hipMalloc(&d_in, nb));
   CK(hipMalloc(&d_out, nb));
-  std::memset(h_in, 1, nb);
   CK(hipMemset(d_out, 2, nb));
-  void *hm_in, *hm_out;  // device pointers of the mapped host buffers
-  CK(hipHostGetDevicePointer(&hm_in, h_in, 0));
-  CK(hipHostGetDevicePointer(&hm_out, h_out, 0));
   hipStream_t s1, s2;
   CK(hipStreamCreateWithFlags(&s1, hipStreamNonBlocking));
   CK(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
-  const size_t n16 = nb / 16;
   auto best = [&](auto fn) {
     double b = 1e9;
     for (int r = 0; r < reps; ++r) {
@@ -59,25 +54,44 @@ int main(int argc, char** argv) {
     }
     return nb / b / 1e9;
   };
-  const double h2d = best([&] { CK(hipMemcpyAsync(d_in, h_in, nb, hipMemcpyHostToDevice, s1)); });
-  const double d2h = best([&] { CK(hipMemcpyAsync(h_out, d_out, nb, hipMemcpyDeviceToHost, s2)); });
-  const double both = best([&] {
-    CK(hipMemcpyAsync(d_in, h_in, nb, hipMemcpyHostToDevice, s1));
-    CK(hipMemcpyAsync(h_out, d_out, nb, hipMemcpyDeviceToHost, s2));
-  });
-  const double kh2d = best([&] { k_copy16<<<1024, 256, 0, s1>>>((const uint4*)hm_in, (uint4*)d_in, n16); });
-  const double kd2h = best([&] { k_copy16<<<1024, 256, 0, s2>>>((const uint4*)d_out, (uint4*)hm_out, n16); });
-  const double kboth = best([&] {
-    k_copy16<<<1024, 256, 0, s1>>>((const uint4*)hm_in, (uint4*)d_in, n16);
-    k_copy16<<<1024, 256, 0, s2>>>((const uint4*)d_out, (uint4*)hm_out, n16);
-  });
-  const double mixed = best([&] {  // H2D through the copy engine, D2H by kernel writes
-    CK(hipMemcpyAsync(d_in, h_in, nb, hipMemcpyHostToDevice, s1));
-    k_copy16<<<1024, 256, 0, s2>>>((const uint4*)d_out, (uint4*)hm_out, n16);
-  });
-  std::printf("{\"MiB\": %zu, \"memcpy\": {\"h2d_GBps\": %.2f, \"d2h_GBps\": %.2f, \"both_GBps_each\": %.2f}, "
-              "\"kernel\": {\"h2d_GBps\": %.2f, \"d2h_GBps\": %.2f, \"both_GBps_each\": %.2f}, "
-              "\"memcpy_h2d_kernel_d2h_GBps_each\": %.2f}\n",
-              nb >> 20, h2d, d2h, both, kh2d, kd2h, kboth, mixed);
+  std::string out = "{\"MiB\": " + std::to_string(nb >> 20);
+  const struct { const char* name; unsigned flags; } kinds[] = {
+      {"default", hipHostMallocDefault}, {"mapped", hipHostMallocMapped},
+      {"coherent", hipHostMallocCoherent}, {"noncoherent", hipHostMallocNonCoherent}};
+  for (const auto& k : kinds) {
+    void *h_in, *h_out;
+    CK(hipHostMalloc(&h_in, nb, k.flags));
+    CK(hipHostMalloc(&h_out, nb, k.flags));
+    std::memset(h_in, 1, nb);
+    std::memset(h_out, 0, nb);
+    const double h2d = best([&] { CK(hipMemcpyAsync(d_in, h_in, nb, hipMemcpyHostToDevice, s1)); });
+    const double d2h = best([&] { CK(hipMemcpyAsync(h_out, d_out, nb, hipMemcpyDeviceToHost, s2)); });
+    const double both = best([&] {
+      CK(hipMemcpyAsync(d_in, h_in, nb, hipMemcpyHostToDevice, s1));
+      CK(hipMemcpyAsync(h_out, d_out, nb, hipMemcpyDeviceToHost, s2));
+    });
+    char buf[256];
+    std::snprintf(buf, sizeof buf, ", \"%s\": {\"h2d_GBps\": %.2f, \"d2h_GBps\": %.2f, \"both_GBps_each\": %.2f}", k.name,
+                  h2d, d2h, both);
+    out += buf;
+    if (k.flags == hipHostMallocMapped) {
+      void *hm_in, *hm_out;
+      CK(hipHostGetDevicePointer(&hm_in, h_in, 0));
+      CK(hipHostGetDevicePointer(&hm_out, h_out, 0));
+      const size_t n16 = nb / 16;
+      const double kh2d = best([&] { k_copy16<<<1024, 256, 0, s1>>>((const uint4*)hm_in, (uint4*)d_in, n16); });
+      const double kd2h = best([&] { k_copy16<<<1024, 256, 0, s2>>>((const uint4*)d_out, (uint4*)hm_out, n16); });
+      const double kboth = best([&] {
+        k_copy16<<<1024, 256, 0, s1>>>((const uint4*)hm_in, (uint4*)d_in, n16);
+        k_copy16<<<1024, 256, 0, s2>>>((const uint4*)d_out, (uint4*)hm_out, n16);
+      });
+      std::snprintf(buf, sizeof buf, ", \"kernel_mapped\": {\"h2d_GBps\": %.2f, \"d2h_GBps\": %.2f, \"both_GBps_each\": %.2f}",
+                    kh2d, kd2h, kboth);
+      out += buf;
+    }
+    CK(hipHostFree(h_in));
+    CK(hipHostFree(h_out));
+  }
+  std::printf("%s}\n", out.c_str());
   return 0;
 }

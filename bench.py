@@ -358,7 +358,7 @@ def main():
     ap.add_argument("--batch", type=int, default=1 << 22, help="orders per GPU per step")
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="config3")
     ap.add_argument("--seed", type=int, default=42)
-    ap.add_argument("--e2e-depth", type=int, default=2, help="host batches in flight in the e2e leg (<= GOME_MAX_INFLIGHT)")
+    ap.add_argument("--e2e-depth", type=int, default=3, help="host batches in flight in the e2e leg (<= GOME_MAX_INFLIGHT)")
     ap.add_argument("--e2e-steps", type=int, default=-1,
                     help="timed steps of the host-to-host pipelined path (-1: = --steps, 0: off)")
     ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of CPU-baseline work")
@@ -669,6 +669,7 @@ def main():
                # without the fill (the first H2D) and drain (the last D2H) that a K-step job adds
                "steady_ms_per_step": round(float(np.median(np.diff(tdone))) * 1e3, 3) if len(tdone) > 2 else None,
                "device_ms_per_batch_median": round(float(np.median(edev)), 3) if edev else None,
+               "collect_gaps_ms": [round(x * 1e3, 2) for x in np.diff(tdone)],
                "p50_batch_ms": round(pctl(elat, 0.5), 3), "p99_batch_ms": round(pctl(elat, 0.99), 3),
                "events_per_s": round(e_events / e_el, 1),
                "pcie_bytes_per_step": int(32 * per_rank * world + 48 * e_events / e2e_steps),

@@ -89,8 +89,37 @@ int main(int argc, char** argv) {
                     kh2d, kd2h, kboth);
       out += buf;
     }
+    if (k.flags == hipHostMallocDefault) {  // the same buffers, copies of kind hipMemcpyDefault
+      const double h2 = best([&] { CK(hipMemcpyAsync(d_in, h_in, nb, hipMemcpyDefault, s1)); });
+      const double d2 = best([&] { CK(hipMemcpyAsync(h_out, d_out, nb, hipMemcpyDefault, s2)); });
+      char b2[160];
+      std::snprintf(b2, sizeof b2, ", \"default_kind\": {\"h2d_GBps\": %.2f, \"d2h_GBps\": %.2f}", h2, d2);
+      out += b2;
+    }
     CK(hipHostFree(h_in));
     CK(hipHostFree(h_out));
+  }
+  {  // malloc'd memory registered with hipHostRegister (how some hosts pin their buffers)
+    void *h_in = nullptr, *h_out = nullptr;
+    if (posix_memalign(&h_in, 4096, nb) || posix_memalign(&h_out, 4096, nb)) return 1;
+    std::memset(h_in, 1, nb);
+    std::memset(h_out, 0, nb);
+    CK(hipHostRegister(h_in, nb, hipHostRegisterDefault));
+    CK(hipHostRegister(h_out, nb, hipHostRegisterDefault));
+    const double h2d = best([&] { CK(hipMemcpyAsync(d_in, h_in, nb, hipMemcpyHostToDevice, s1)); });
+    const double d2h = best([&] { CK(hipMemcpyAsync(h_out, d_out, nb, hipMemcpyDeviceToHost, s2)); });
+    const double both = best([&] {
+      CK(hipMemcpyAsync(d_in, h_in, nb, hipMemcpyHostToDevice, s1));
+      CK(hipMemcpyAsync(h_out, d_out, nb, hipMemcpyDeviceToHost, s2));
+    });
+    char buf[200];
+    std::snprintf(buf, sizeof buf, ", \"registered\": {\"h2d_GBps\": %.2f, \"d2h_GBps\": %.2f, \"both_GBps_each\": %.2f}",
+                  h2d, d2h, both);
+    out += buf;
+    CK(hipHostUnregister(h_in));
+    CK(hipHostUnregister(h_out));
+    free(h_in);
+    free(h_out);
   }
   std::printf("%s}\n", out.c_str());
   return 0;

@@ -29,6 +29,7 @@ from __future__ import annotations
 
 import argparse
 import json
+from contextlib import nullcontext
 import os
 import sys
 import threading
@@ -384,7 +385,7 @@ def main():
                     help="weak: --batch orders per GPU per step; strong: --batch orders per step in all, "
                          "split over the GPUs (DESIGN 7)")
     ap.add_argument("--plan-cus", type=int, default=None,
-                    help="gome_config.plan_cus (default: 0 = the engine's default; -1 with RCCL)")
+                    help="gome_config.plan_cus (default: 0 = the engine's default, 8 plan CUs; -1: none)")
     ap.add_argument("--step-log", default="", help="write each timed step's engine counters (JSONL)")
     ap.add_argument("--sync", action="store_true",
                     help="one synchronous gome_submit_batch_device per step (default: two batches in "
@@ -421,9 +422,12 @@ def main():
 
     from gome_amd.abi import GOME_MAX_INFLIGHT, Engine
 
-    # gome_config.plan_cus: with RCCL in the process the engine's CU-masked plan stream lost 5% per
-    # step in round 4, for reasons not established, so such a host keeps every CU shared
-    plan_cus = args.plan_cus if args.plan_cus is not None else (-1 if use_pg and args.backend == "nccl" else 0)
+    # gome_config.plan_cus: the engine's default (8 CUs reserved for the hottest book's plan) with or
+    # without RCCL.  (Round 4 lost 5% per step with RCCL and plan CUs; round 5 found why: the CU-masked
+    # streams (hipExtStreamCreateWithCUMask) are blocking streams, so the publisher's torch work on the
+    # legacy default stream waited for every engine kernel enqueued before it, the next batch's
+    # whole plan included.  The publisher now runs on a stream of its own; DESIGN 4.7, INTEGRATION.)
+    plan_cus = args.plan_cus if args.plan_cus is not None else 0
     W = WORKLOADS[args.workload]
     n_symbols = W["symbols"]
     steps, warm = args.steps, args.warmup
@@ -453,6 +457,10 @@ def main():
 
     summary = torch.zeros(SUMMARY_WORDS, dtype=torch.int64, device=cdev)
     gathered = torch.zeros(SUMMARY_WORDS * world, dtype=torch.int64, device=cdev)
+    # the publisher's torch work (summary packing, the all_gather, its readback) on a non-blocking
+    # stream: never on the legacy default stream, which the engine's CU-masked (blocking) streams
+    # synchronise with
+    pub_stream = torch.cuda.Stream() if cdev == "cuda" else None
     pub = SummaryPublisher(world) if rank == 0 else None
     seq = [0]
     hot = hot_symbols(args.workload, rank, world)
@@ -461,9 +469,10 @@ def main():
     def publish(st, i, dg):
         if use_pg:  # per-GPU trade/depth summary to the publisher (RCCL all_gather)
             last_dg[0] = dg  # depth digests of this rank's hottest books after batch i
-            gather_summary(st, summary, gathered, rank, i, dg)
-            if pub is not None:
-                pub.consume(gathered)
+            with torch.cuda.stream(pub_stream) if pub_stream is not None else nullcontext():
+                gather_summary(st, summary, gathered, rank, i, dg)
+                if pub is not None:
+                    pub.consume(gathered)
 
     def step(i):
         b = dev_batches[i]

@@ -275,14 +275,14 @@ def consumer_leg(workload, n_symbols, n_msgs, seed, batch=1 << 15, threads=8):
                  max_levels=(1 << 22) + 2 * n_msgs)
     cons = BatchingConsumer(eng, pre, sink, names, max_batch=batch, threads=threads)
     evs, recs, bases = [], [], []
-    orig_render = cons.render
+    orig_render = cons.render_block
 
     def keep(ev, rc, base):  # (the events of each batch, for the render-only pass)
         evs.append(ev.copy())
         recs.append(rc.copy())
         bases.append(base)
         return orig_render(ev, rc, base)
-    cons.render = keep
+    cons.render_block = keep
     t = time.perf_counter()
     lines = 0
     for k in range(0, n_msgs, batch):

@@ -251,20 +251,52 @@ class Ingress:
 
 
 class MatchSink:
-    """The matchOrder queue and its consumer (rabbitmq.go:132-177: decode and log)."""
+    """The matchOrder queue and its consumer (rabbitmq.go:132-177: decode and log).  Rendered batches
+    arrive as blocks of newline-terminated MatchResult lines (one message each) and stay bytes until
+    something reads them (`q`, consume): splitting each batch into Python strings on the consumer's
+    thread cost more than the native render itself."""
 
     def __init__(self, log=None):
-        self.q: list[str] = []
+        self._q: list[str] = []
+        self._blocks: list[bytes] = []
+        self.published = 0  # messages published
         self.log = log
         self.lock = threading.Lock()
 
     def publish_many(self, lines):
         with self.lock:
-            self.q.extend(lines)
+            self._flush()
+            self._q.extend(lines)
+            self.published += len(lines)
+
+    def publish_block(self, block: bytes, n: int):
+        """n newline-terminated lines, in publish order."""
+        with self.lock:
+            self._blocks.append(block)
+            self.published += n
+
+    def _flush(self):
+        for b in self._blocks:
+            self._q.extend(b.decode().split("\n")[:-1])
+        self._blocks.clear()
+
+    @property
+    def q(self) -> list[str]:
+        """The queued MatchResult lines (str), oldest first."""
+        with self.lock:
+            self._flush()
+            return self._q
+
+    @q.setter
+    def q(self, v):
+        with self.lock:
+            self._blocks.clear()
+            self._q = list(v)
 
     def consume(self) -> list[dict]:
         with self.lock:
-            out, self.q = self.q, []
+            self._flush()
+            out, self._q = self._q, []
         res = [json.loads(x) for x in out]
         if self.log:
             for r in res:
@@ -331,7 +363,8 @@ class BatchingConsumer:
         self.rejected += st.rejected
         return rec[:got.value]
 
-    def render(self, ev: np.ndarray, rec: np.ndarray, seq_base: int) -> list[str]:
+    def render_block(self, ev: np.ndarray, rec: np.ndarray, seq_base: int) -> bytes:
+        """The batch's MatchResult lines as one block of bytes (newline-terminated)."""
         N = self.names
         while True:
             k = self.lib.gome_render_events_mt(
@@ -344,7 +377,10 @@ class BatchingConsumer:
             if k == -(1 << 63):
                 raise GomeError(1, "event references an unknown id")
             self._buf = C.create_string_buffer(int(-k) + (1 << 20))
-        return C.string_at(self._buf, k).decode().split("\n")[:-1]
+        return C.string_at(self._buf, k)
+
+    def render(self, ev: np.ndarray, rec: np.ndarray, seq_base: int) -> list[str]:
+        return self.render_block(ev, rec, seq_base).decode().split("\n")[:-1]
 
     def process(self, msgs) -> int:
         """Apply one drained batch; returns the MatchResults published.  Raises only when the
@@ -368,10 +404,11 @@ class BatchingConsumer:
         self.seq += len(rec)
         self.dups += int(self.eng.stats()["n_dup_oid"])
         ev = self.eng.drain()
-        lines = self.render(ev, rec, base)
-        self.sink.publish_many(lines)
+        block = self.render_block(ev, rec, base)
+        n = block.count(b"\n")
+        self.sink.publish_block(block, n)
         self.batches += 1
-        return len(lines)
+        return n
 
     def poll(self, q, block_s: float = 0.0) -> int:
         msgs = self.drain(q, block_s)

@@ -1176,11 +1176,13 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
       k_fc_prank<<<dim3(FL_SORT_GRID, nb), FL_TILE, 0, st>>>(D, B, R);
       k_fc_pwin<<<dim3(px, nb), 256, 0, st>>>(D, B, R, 0u);
       k_fc_precs<<<dim3(px, nb), 256, 0, st>>>(D, B, R, 0u);
+      k_fc_precs_long<<<dim3(64, nb), 256, 0, st>>>(D, B, R, 0u);
     } else {
       k_fc_oldwalk_book<<<nb, 1024, 0, st>>>(D, R);
       k_fc_pass<<<nb, FC_PASS_T, 0, st>>>(D, B, R);
       k_fc_pwin<<<dim3(px, nb), 256, 0, st>>>(D, B, R, 1u);
       k_fc_precs<<<dim3(px, nb), 256, 0, st>>>(D, B, R, 1u);
+      k_fc_precs_long<<<dim3(16, nb), 256, 0, st>>>(D, B, R, 1u);
     }
     if (c_deep) k_fd_decline<<<ns, 256, 0, st>>>(D, R);
     k_fc_unmark<<<dim3(px, nb), 256, 0, st>>>(D, B, R);

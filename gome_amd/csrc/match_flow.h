@@ -146,6 +146,7 @@ struct FlowHdr {
   uint32_t nzlev;      // levels that may hold zero-volume makers at batch start (FlowLvl::z0)
   uint32_t haz;        // k_flow_zero_check / k_fc_stale_level: a state the reconstruction cannot take
   uint32_t nwrong;     // books with DELs: wrong-side cancels that find their maker (Q2, k_fc_resolve)
+  uint32_t nlong;      // books with DELs: DELs with a long window (k_fc_precs -> k_fc_precs_long)
 };
 // FlowHdr::ok: 0 declined, FL_OK_ADD an ADD-only flow book, FL_OK_CANCEL a book with DELs,
 // FL_OK_DEEP an ADD-only head book with more levels than the lane plans hold (match_flow_deep.h)

@@ -109,6 +109,12 @@ __device__ __forceinline__ unsigned long long fc_key(const FlowArgs& F, uint32_t
 // the node or the ADD: the dual-source load miscompiled beside the window code, gfx950.)
 __device__ __forceinline__ bool fc_del_sale(const FlowArgs& F, uint32_t b) { return F.fc_rank[b] != 0u; }
 
+// Book h's list of long-window DELs (k_fc_precs -> k_fc_precs_long): its touch-fill scratch
+// (FlowArgs::tfc, free until the reconstruction), as 32-bit positions.
+__device__ __forceinline__ uint32_t* fc_long_list(const FlowArgs& F, const FlowHdr& hd) {
+  return reinterpret_cast<uint32_t*>(F.tfc + static_cast<size_t>(FL_TOUCH_MUL) * hd.beg);
+}
+
 // Slice [b0, b1) of book h's segment for block x of `nx`.
 __device__ __forceinline__ void fc_slice(const FlowHdr& hd, uint32_t x, uint32_t nx, uint32_t& b0, uint32_t& b1) {
   const uint64_t len = hd.end - hd.beg;
@@ -163,6 +169,7 @@ __global__ __launch_bounds__(256) void k_fc_hash_claim(Dev D, BatchArgs B, FlowA
   fc_slice(hd, blockIdx.x, gridDim.x, b0, b1);
   const bool claim = hd.sym < FC_MAXKEY_SYM;
   if (!claim && threadIdx.x == 0) fc_decline(F, h, FC_BAD_SYM);
+  if (blockIdx.x == 0 && threadIdx.x == 0) F.hdr[h].nlong = 0;  // (k_fc_precs' long-window list)
   if (hd.end - hd.beg + 8 > FC_MAX_ORDERS && blockIdx.x == 0 && threadIdx.x == 0) fc_decline(F, h, FC_BAD_RING);
   for (uint32_t b = b0 + threadIdx.x; b < b1; b += blockDim.x) {
     F.fc_tg[b] = 0;
@@ -792,8 +799,11 @@ __global__ __launch_bounds__(256) void k_fc_precs(Dev D, BatchArgs B, FlowArgs F
   uint32_t b0, b1;
   fc_slice(hd, blockIdx.x, gridDim.x, b0, b1);
   const uint32_t lane = lane_id();
-  // a DEL with a short window loops over it alone; the wave shares the long ones (the
-  // hottest books' busiest levels hold thousands of targets)
+  // a DEL with a short window loops over it alone; the long ones (the hottest books' busiest
+  // levels hold thousands of targets) go to a list that k_fc_precs_long deals out one per wave:
+  // as one wave's serial loop here, a run of consecutive long-window DELs (e.g. 453 wrong-side
+  // cancels of one level's makers, one after another) took 11.4 ms
+  uint32_t* longl = fc_long_list(F, hd);
   for (uint32_t bw = b0 + (threadIdx.x & ~63u); bw < b1; bw += blockDim.x) {
     const uint32_t b = bw + lane;
     FcDel d{};
@@ -808,22 +818,27 @@ __global__ __launch_bounds__(256) void k_fc_precs(Dev D, BatchArgs B, FlowArgs F
     }
     const bool longw = isd && d.nb > 32;
     if (isd && !longw) F.ord8[hd.obase + (b - hd.beg)] = fc_del_rec(F, hd, LV, b, d, sale);
-    for (unsigned long long lm = __ballot(longw); lm; lm &= lm - 1) {
-      const uint32_t src = static_cast<uint32_t>(__builtin_ctzll(lm));
-      FcDel ds{};
-      ds.kind = __shfl(d.kind, src);
-      ds.li = __shfl(d.li, src);
-      ds.rank = __shfl(d.rank, src);
-      ds.nb = __shfl(d.nb, src);
-      ds.oend = __shfl(d.oend, src);
-      ds.ov = __shfl(d.ov, src);
-      ds.va = __shfl(d.va, src);
-      const uint32_t bs = __shfl(b, src);
-      const bool ss = __shfl(sale ? 1u : 0u, src) != 0u;
-      uint32_t c = fc_del_c(F, hd, LV, bs, ds, ss, 1u + lane, 64u);
-      for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off);
-      if (lane == src) F.ord8[hd.obase + (bs - hd.beg)] = fc_del_rec_c(hd, LV, ds, ss, c);
-    }
+    if (longw) longl[atomicAdd(&F.hdr[h].nlong, 1u)] = b;
+  }
+}
+
+// The long-window DELs of k_fc_precs, one wave each (lanes stride the window).
+__global__ __launch_bounds__(256) void k_fc_precs_long(Dev D, BatchArgs B, FlowArgs F, uint32_t only_deep) {
+  const uint32_t h = F.h0 + blockIdx.y;
+  if (h >= fl_hend(D, F) || !fc_book(F, h) || (only_deep && F.hdr[h].ok != FL_OK_DEEP)) return;
+  const FlowHdr hd = F.hdr[h];
+  if (hd.nbsum > FC_NBSUM_MUL * (hd.end - hd.beg) + FC_NBSUM_ADD) return;  // (declined by k_fc_precs)
+  const FlowLvl* LV = fl_lvls(F, h);
+  const uint32_t* longl = fc_long_list(F, hd);
+  const uint32_t lane = lane_id();
+  const uint32_t W = gridDim.x * (blockDim.x >> 6);
+  for (uint32_t i = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); i < hd.nlong; i += W) {
+    const uint32_t b = uni(longl[i]);
+    const FcDel d = F.fc_del[b];
+    const bool sale = fc_del_sale(F, b);
+    uint32_t c = fc_del_c(F, hd, LV, b, d, sale, 1u + lane, 64u);
+    for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off);
+    if (lane == 0) F.ord8[hd.obase + (b - hd.beg)] = fc_del_rec_c(hd, LV, d, sale, c);
   }
 }
 

@@ -65,11 +65,17 @@ struct Book {
 // such a state.  Cleared after a batch by k_requalify (match_requal.h) once the book's state
 // is again one the flow plans assume (the reference's state heals: nodepool.go:76-83).
 constexpr uint32_t BOOK_QUIRK = 1u;
-// Book::pad: the book may hold zero-volume makers (Q6), and Level::pad L_ZERO marks the levels that
-// do (k_requalify sets both; the head books' lane plans keep them, match_flow.h; any other kernel
-// that applies such a book sets BOOK_QUIRK, so k_requalify recomputes the marks after it).
+// Book::pad: the book may hold zero-volume makers (Q6), and Level::pad counts the zero-volume makers
+// in each level's FIFO (L_ZERO_SAT: that many or more; k_requalify sets both, the head books' flow
+// writes keep them, match_flow.h; any other kernel that applies such a book sets BOOK_QUIRK, so
+// k_requalify recounts after it).
 constexpr uint32_t BOOK_ZERO = 2u;
-constexpr uint8_t L_ZERO = 1u;
+constexpr uint8_t L_ZERO_SAT = 255u;
+// a level's zero-volume maker count after `popped` of `before` left and `added` joined
+__host__ __device__ constexpr uint8_t l_zero_count(uint32_t before, uint32_t popped, uint32_t added) {
+  return before >= L_ZERO_SAT ? L_ZERO_SAT
+                              : static_cast<uint8_t>(before - popped + added < L_ZERO_SAT ? before - popped + added : L_ZERO_SAT);
+}
 // Book::pad: the book may hold stale side-set members (Q2: member, no FIFO, depth 0), so a bid
 // may lie above an ask (a stale one) and the cold kernel's bid/ask split scan does not hold
 // (set by k_requalify and the flow writes that keep such a level; cleared by a later requalify).

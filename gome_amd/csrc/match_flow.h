@@ -182,7 +182,7 @@ struct FlowLvl {
   uint32_t pad0, pad1;
   // books with DELs (match_flow_cancel.h): the targets of the level's DELs
   uint32_t c_old;    // old (pre-batch) makers targeted by a DEL of the batch
-  uint32_t z0;       // the level's FIFO may hold zero-volume makers at batch start (Level::pad L_ZERO)
+  uint32_t z0;       // zero-volume makers in the level's FIFO at batch start (Level::pad; L_ZERO_SAT: or more)
   uint32_t c_wrong;  // wrong-side DELs (Q2) whose maker rests at this level (k_fc_resolve)
   uint32_t ocan;     // cancelled volume of old makers (plan units), set by the recon
   uint32_t memf;     // deep books: membership after the batch (M_BUY / M_SALE)
@@ -190,6 +190,8 @@ struct FlowLvl {
   uint32_t tbase;    // first entry of the level's DEL-time array in FlowArgs::fc_dt (book-local)
   uint32_t mfin;     // books with DELs: the level ends a stale member of this set (M_BUY / M_SALE;
                      // k_fc_stale_level), 0 if not
+  uint32_t zpop;     // ADD books: old zero-volume makers the batch popped (fl_level_one's gather)
+  uint32_t pad4, pad5, pad6;
 };
 static_assert(sizeof(FlowLvl) % 16 == 0, "FlowLvl alignment");
 
@@ -849,7 +851,7 @@ __global__ __launch_bounds__(FL_PREP_T) void k_flow_prep_b(Dev D, BatchArgs B, F
       f.hslot = x.hslot;
       f.tslot = x.tslot;
       f.mem0 = x.member;
-      f.z0 = (bk.pad & BOOK_ZERO) && (x.pad & L_ZERO) ? 1u : 0u;
+      f.z0 = (bk.pad & BOOK_ZERO) ? x.pad : 0u;
       if (f.z0) atomicAdd(&nzlev, 1u);
     }
     LV[r + 1] = f;
@@ -1554,10 +1556,22 @@ __device__ __forceinline__ uint32_t fl_find(const IgEnt* IG, uint32_t ig_n, cons
   return ig_n + lo;
 }
 
+// Zero-volume makers (Q6) share their successor's start.  A consume whose cursor is c fills first
+// the zero-volume makers starting at c (the FIFO head: everything before them is gone, and the
+// consume before stopped at c with diff == 0, engine.go:162-175), so its first maker steps back
+// from fl_find's (the last start <= c) over those: a maker before the found one with start c has
+// length 0 (k_flow_zero_check hands over a book where a consume leaves depth 0 beside one, or a
+// zero-volume taker meets one).
+__device__ __forceinline__ uint32_t fl_first_back(const IgEnt* IG, uint32_t ig_n, const RsEnt* RS, uint32_t f, int64_t c) {
+  while (f > 0 && (f - 1 < ig_n ? IG[f - 1].e : RS[f - 1 - ig_n].e) == c) --f;
+  return f;
+}
+
 // Wave-cooperative fl_find: every lane's query q (lanes with !valid ignored), b a maker at or
 // before every valid query's.  Windows of 64 consecutive makers from b (one coalesced read into
 // the lanes) searched by shuffles; a query beyond FL_FC_WIN windows searches alone.  Makers'
-// starts strictly ascend (no zero-volume maker in a clean book), IG then RS, from 0.
+// starts ascend (strictly but for zero-volume makers, which share their successor's), IG then RS,
+// from 0.
 constexpr int FL_FC_WIN = 3;
 __device__ __forceinline__ uint32_t fl_wave_find(const IgEnt* IG, uint32_t ig_n, const RsEnt* RS, uint32_t nrest,
                                                  int64_t d0, bool valid, int64_t q, uint32_t b) {
@@ -1595,7 +1609,7 @@ __device__ __forceinline__ uint32_t fl_wave_find(const IgEnt* IG, uint32_t ig_n,
 // chunk's ended; interleaved waves find their chunk's first maker by one search.
 __device__ __forceinline__ void fl_level_fc(const FlowArgs& F, uint32_t L, uint32_t q, uint32_t base, uint32_t cnt,
                                             const IgEnt* IG, uint32_t ig_n, uint32_t nrest, int64_t d0, uint32_t w,
-                                            uint32_t nw) {
+                                            uint32_t nw, bool zl = false) {
   const SEnt* R = F.srt + L + base;
   const RsEnt* RS = F.rs + L + base;
   const uint32_t lane = lane_id();
@@ -1611,10 +1625,11 @@ __device__ __forceinline__ void fl_level_fc(const FlowArgs& F, uint32_t L, uint3
     const int64_t x = e.coord + (e.amt ? e.amt : 1) - 1;
     const int l0 = static_cast<int>(__builtin_ctzll(cm)), l1 = 63 - static_cast<int>(__builtin_clzll(cm));
     const uint32_t b = nw == 1 ? carry : fl_find(IG, ig_n, RS, nrest, d0, __shfl(e.coord, l0));
-    const uint32_t f = fl_wave_find(IG, ig_n, RS, nrest, d0, cons, e.coord, b);
-    const uint32_t l = fl_wave_find(IG, ig_n, RS, nrest, d0, cons, x, __shfl(f, l0));
+    const uint32_t f0 = fl_wave_find(IG, ig_n, RS, nrest, d0, cons, e.coord, b);
+    const uint32_t l = fl_wave_find(IG, ig_n, RS, nrest, d0, cons, x, __shfl(f0, l0));
     carry = __shfl(l, l1);
     if (cons) {
+      const uint32_t f = zl && e.amt ? fl_first_back(IG, ig_n, RS, f0, e.coord) : f0;
       FlTouchFc y;
       y.first = f;
       y.last = l;
@@ -1657,6 +1672,7 @@ __device__ __forceinline__ void fl_level_one(const Dev& D, const FlowArgs& F, ui
   int64_t cc = 0, rr = d0;
   uint32_t nr = 0;
   const unsigned long long ltm = lt_mask();
+  const bool zl = Lq->z0 || hd->nzero;  // (the level may hold zero-volume makers: fl_first_back)
   if (pre_cfin >= 0) {  // (the touch scan ran block-wide: fl_level_scan_blk)
     cc = pre_cfin;
     nr = pre_nr;
@@ -1702,7 +1718,7 @@ __device__ __forceinline__ void fl_level_one(const Dev& D, const FlowArgs& F, ui
   const int64_t cfin = cc;
   uint32_t nv0 = uni(Lq->nv0), head = uni(Lq->head), tail = uni(Lq->tail);
   uint32_t hslot = uni(Lq->hslot), tslot = uni(Lq->tslot);
-  uint32_t ig_base = 0, ng = 0, consumed = 0;
+  uint32_t ig_base = 0, ng = 0, consumed = 0, zpopped = 0;
   bool have_extra = false;
   // (gather0: a CONS of 0 reads the maker at the cursor even when nothing was consumed)
   if (nv0 > 0 && (cfin > 0 || gather0)) {
@@ -1767,11 +1783,14 @@ __device__ __forceinline__ void fl_level_one(const Dev& D, const FlowArgs& F, ui
         IG[ng + __popcll(tm & ltm)] = g;
       }
       ng += __popcll(tm);
-      const bool cons = live && em + nd.rem <= cfin;
+      // (a zero-volume maker is consumed, popped, only strictly before the consumption end: one at
+      // the end was not reached, engine.go:162-175)
+      const bool cons = live && em + nd.rem <= cfin && (nd.rem > 0 || em < cfin);
       if (cons) __hip_atomic_store(&D.idx[nd.ixs].key, KEY_TOMB, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       consumed += __popcll(__ballot(cons));
+      zpopped += __popcll(__ballot(cons && nd.rem == 0));
       if (!have_surv) {
-        const unsigned long long sv = __ballot(live && em + nd.rem > cfin);
+        const unsigned long long sv = __ballot(live && !cons);
         if (sv) {
           have_surv = true;
           nh = c;
@@ -1824,10 +1843,11 @@ __device__ __forceinline__ void fl_level_one(const Dev& D, const FlowArgs& F, ui
         __threadfence_block();
         const int64_t c = c1 + ic - ac, x = c + (ac ? ac : 1) - 1;  // (a CONS of 0: fl_level_fc)
         const int l0 = static_cast<int>(__builtin_ctzll(cm)), l1 = 63 - static_cast<int>(__builtin_clzll(cm));
-        const uint32_t f = fl_wave_find(IG, ng, RS, nr, d0, isc, c, carry);
-        const uint32_t l = fl_wave_find(IG, ng, RS, nr, d0, isc, x, __shfl(f, l0));
+        const uint32_t f0 = fl_wave_find(IG, ng, RS, nr, d0, isc, c, carry);
+        const uint32_t l = fl_wave_find(IG, ng, RS, nr, d0, isc, x, __shfl(f0, l0));
         carry = __shfl(l, l1);
         if (isc) {
+          const uint32_t f = zl && ac ? fl_first_back(IG, ng, RS, f0, c) : f0;
           FlTouchFc y;
           y.first = f;
           y.last = l;
@@ -1851,6 +1871,7 @@ __device__ __forceinline__ void fl_level_one(const Dev& D, const FlowArgs& F, ui
     Lq->hslot = hslot;
     Lq->tslot = tslot;
     Lq->nlive0 = nv0 - consumed;
+    Lq->zpop = zpopped;
   }
 }
 
@@ -2470,7 +2491,7 @@ __device__ __forceinline__ void fl_write_finish(const Dev& D, const FlowHdr& hd,
     uint32_t fl = 0;  // levels that may hold zero-volume makers (BOOK_ZERO); stale members (BOOK_STALE)
     for (uint32_t q = 1; q <= hd.nl; ++q) {
       if (keep[q] == NIL) continue;
-      if (lv[q].pad & L_ZERO) fl |= BOOK_ZERO;
+      if (lv[q].pad) fl |= BOOK_ZERO;
       if (lv[q].nlive == 0) fl |= BOOK_STALE;
     }
     zflag_s = fl;
@@ -2708,8 +2729,10 @@ __global__ __launch_bounds__(FL_LVB_T) void k_flow_write_lv_blk(Dev D, BatchArgs
   const FlWPlan wp = fl_wplan(f, RS);
   const uint32_t rf = wp.rf, S = wp.S, s0 = wp.s0, room = wp.room, need = wp.need;
   const bool fresh = wp.fresh;
-  bool zs = false;
+  __shared__ uint32_t zadd_s;
+  uint32_t zs = 0;
   if (tid == 0) {  // claim `need` chunk ids: free stack first, then the bump pointer
+    zadd_s = 0;
     int t = 0;
     uint32_t nst = 0, bb = 0;
     if (need) {
@@ -2775,10 +2798,13 @@ __global__ __launch_bounds__(FL_LVB_T) void k_flow_write_lv_blk(Dev D, BatchArgs
     nd.ixs = static_cast<uint32_t>(hh);
     nd.tx = mk.side;
     D.nodes[loc] = nd;
-    zs = zs || r.v == 0;
+    zs += r.v == 0 ? 1u : 0u;
   }
-  // the level may hold zero-volume makers: old ones (z0) or one appended now (Q6)
-  const bool zl = __syncthreads_or(zs) || f.z0;
+  // zero-volume makers in the level's FIFO after the batch (Q6): the old ones the batch did not pop
+  // and the ones appended now (Level::pad)
+  if (zs) atomicAdd(&zadd_s, zs);
+  __syncthreads();
+  const uint32_t zadd = zadd_s;
   if (tid != 0) return;
   ctr_pops(D, fl_level_pops(f, rf));
   Level x{};
@@ -2812,7 +2838,7 @@ __global__ __launch_bounds__(FL_LVB_T) void k_flow_write_lv_blk(Dev D, BatchArgs
                         : (x.nlive > 0) == (x.depth > 0) && (x.nlive > 0) == (mem == M_BUY || mem == M_SALE) &&
                               (x.nlive > 0 || mem == 0);
   if (!ok) atomicOr(&D.st->err, ERR_CORRUPT);
-  x.pad = zl ? L_ZERO : 0u;
+  x.pad = x.nlive ? l_zero_count(f.z0, f.zpop, zadd) : 0u;
   F.lvout[h * FL_CAP + q] = x;
 }
 
@@ -3020,15 +3046,41 @@ __device__ __forceinline__ uint32_t fl_blk_max_excl(uint32_t x, uint32_t* total)
   return max(before, lane ? ex : 0u);
 }
 
+// Block-wide exclusive max of one int64 per thread (FL_LVB_T threads; -1 where nothing precedes);
+// *total = the block's max.
+__device__ __forceinline__ int64_t fl_blk_max64_excl(int64_t x, int64_t* total) {
+  __shared__ int64_t wm64[FL_LVB_W];
+  const uint32_t w = threadIdx.x >> 6, lane = lane_id();
+  int64_t inc = x;
+  for (uint32_t off = 1; off < 64; off <<= 1) {
+    const int64_t v = __shfl_up(inc, off);
+    if (lane >= off) inc = max(inc, v);
+  }
+  const int64_t ex = __shfl_up(inc, 1);
+  if (lane == 63u) wm64[w] = inc;
+  __syncthreads();
+  int64_t before = -1, tot = -1;
+  for (uint32_t k = 0; k < FL_LVB_W; ++k) {
+    const int64_t v = wm64[k];
+    before = k < w ? max(before, v) : before;
+    tot = max(tot, v);
+  }
+  __syncthreads();  // (wm64 is reused by the next call)
+  *total = tot;
+  return max(before, lane ? ex : static_cast<int64_t>(-1));
+}
+
 // Books planned with zero-volume ADDs (Q6, k_flow_prep_b) or holding zero-volume makers (FlowLvl::z0):
-// the reconstruction takes a zero-volume maker only where no order reaches it this batch.  One block
+// the reconstruction takes a zero-volume maker where no order reaches it, and (ADD books) where a
+// consume passes it with volume to spare at the level (it pops it with a 0-fill, engine.go:145-161).  One block
 // per (book, level), the level's run in time order with block scans; hazards (FlowHdr::haz, handed
 // over by k_flow_stale_check):
 //  * a REST of 0 while the level's depth is 0: the reference makes it a side-set member of depth 0
 //    (SetPoolDepth, engine.go:78-80), which the plans, seeing depth 0 as "no level", would not visit;
-//  * a CONS (of any amount) after a zero-volume maker may be in the FIFO (z0, or a REST of 0 earlier in
-//    the run): the fills would have to pop it (engine.go:145-175).
-// A REST of 0 with depth > 0 and no CONS after it is an ordinary FIFO append (fl_wplan).  Books with
+//  * after a zero-volume maker may be in the FIFO (z0, or a REST of 0 earlier in the run): a CONS that
+//    empties the level or a CONS of 0 (ADD books), any CONS (cancel books).
+// A REST of 0 with depth > 0 is an ordinary FIFO append (fl_wplan), popped by the first consume
+// that passes it (fl_first_back; the gather in fl_level_one).  Books with
 // DELs (the cancel path): a cancel lowers the depth like a CONS; a CONS of 0 (a zero-volume taker,
 // whose one 0-fill the cancel path's events do not model) is a hazard as well.
 __global__ __launch_bounds__(FL_LVB_T) void k_flow_zero_check(Dev D, FlowArgs F) {
@@ -3041,8 +3093,11 @@ __global__ __launch_bounds__(FL_LVB_T) void k_flow_zero_check(Dev D, FlowArgs F)
   const uint32_t cnt = Lq->cnt;
   if (!cnt) return;
   const SEnt* R = F.srt + FL_TOUCH_MUL * hd->beg + Lq->base;
-  int64_t run = Lq->d0;      // the level's depth before the chunk
-  bool zero = Lq->z0 != 0;   // a zero-volume maker may be in the FIFO before the chunk
+  const int64_t d0 = Lq->d0;
+  int64_t run = d0;          // the level's depth before the chunk
+  int64_t rr = d0, cc = 0;   // arrival end and consumption cursor before the chunk (volume coordinates)
+  int64_t zlast = -1;        // start of the latest zero-volume maker rested before the chunk (-1: none)
+  bool zero = Lq->z0 != 0;   // cancel books: a zero-volume maker may be in the FIFO before the chunk
   bool haz = false;
   for (uint32_t c0 = 0; c0 < cnt; c0 += FL_LVB_T) {
     const uint32_t i = c0 + tid;
@@ -3051,11 +3106,28 @@ __global__ __launch_bounds__(FL_LVB_T) void k_flow_zero_check(Dev D, FlowArgs F)
     if (valid) e = R[i];
     const bool isr = valid && e.kind == TK_REST, isc = valid && e.kind == TK_CONS, zr = isr && e.amt == 0;
     const bool isx = valid && e.kind == TK_CANC;
-    int64_t tot, tz;
+    int64_t tot, tz, tr, tc, tzm;
     const int64_t before = run + fl_blk_excl(isr ? e.amt : (isc || isx) ? -e.amt : 0, &tot);
     const int64_t zb = fl_blk_excl(zr ? 1 : 0, &tz);
-    haz = haz || (zr && before == 0) || (isc && (zero || zb > 0 || (canc && e.amt == 0)));
+    const int64_t rb = rr + fl_blk_excl(isr ? e.amt : 0, &tr);  // this REST's start
+    const int64_t cb = cc + fl_blk_excl(isc ? e.amt : 0, &tc);  // this CONS's cursor
+    const int64_t zm = max(zlast, fl_blk_max64_excl(zr ? rb : -1, &tzm));
+    if (canc) {  // cancel books: any consume after a zero-volume maker may be in the FIFO
+      haz = haz || (zr && before == 0) || (isc && (zero || zb > 0 || e.amt == 0));
+    } else {
+      // ADD books: a zero-volume maker is in the FIFO until a consume passes its start (an old
+      // one: until the cursor passes the old FIFO's end).  A consume that leaves depth > 0 pops the
+      // ones it passes (fl_first_back, the intervals); one that empties the level (the taker would
+      // pop those at its end if it went on, or leave them in a FIFO whose level left its set) or a
+      // zero-volume taker meeting one (diff == 0 pops it and the cursor stays) is a hazard, and so
+      // is a REST of 0 at depth 0.
+      const bool zp = (Lq->z0 && cb <= d0) || zm >= cb;
+      haz = haz || (zr && before == 0) || (isc && zp && (e.amt == 0 || before - e.amt == 0));
+    }
     run += tot;
+    rr += tr;
+    cc += tc;
+    zlast = max(zlast, tzm);
     zero = zero || tz > 0;
   }
   if (__syncthreads_or(haz) && tid == 0) atomicOr(&hd->haz, 1u);
@@ -3111,7 +3183,7 @@ __global__ __launch_bounds__(FL_LVB_T) void k_flow_level_wide(Dev D, FlowArgs F)
   const FlowLvl* Lq = F.lvl + h * FL_CAP + q;
   if (cfin > 0 || z0)
     fl_level_fc(F, FL_TOUCH_MUL * F.hdr[h].beg, q, Lq->base, Lq->cnt, F.ig + Lq->ig_base, Lq->ig_n, Lq->nrest, Lq->d0,
-                threadIdx.x >> 6, FL_LVB_T / 64);
+                threadIdx.x >> 6, FL_LVB_T / 64, Lq->z0 || F.hdr[h].nzero);
 }
 
 }  // namespace gome

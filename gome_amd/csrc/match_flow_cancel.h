@@ -1642,18 +1642,17 @@ __device__ __forceinline__ Level fc_write_level(const Dev& D, const BatchArgs& B
   // survivors among the new makers: not cancelled, not filled to the end (in FIFO order); a
   // maker starting before the consumption end keeps e + v - cfin
   uint32_t S = 0;
-  bool zl = f.z0 != 0;  // the level may hold zero-volume makers (Q6, Level::pad L_ZERO)
+  uint32_t zadd = 0;  // zero-volume makers appended (Q6; the cancel path pops none: k_flow_zero_check)
   for (uint32_t c0 = 0; c0 < V.nrest; c0 += 64) {
     const uint32_t i = c0 + lane;
     bool sv = false;
     if (i < V.nrest) {
       const RsEnt r = V.RS[i];
       sv = r.pad0 == NIL && r.e + r.v > f.cfin;
-      zl = zl || (sv && r.v == 0);
     }
     S += __popcll(__ballot(sv));
+    zadd += __popcll(__ballot(sv && i < V.nrest && V.RS[i].v == 0));
   }
-  x.pad = __ballot(zl) ? L_ZERO : 0u;
   const bool fresh = f.nlive0 == 0;
   const uint32_t s0 = fresh ? 0u : f.tslot;
   const uint32_t room = fresh ? 0u : CH - s0;
@@ -1729,6 +1728,7 @@ __device__ __forceinline__ Level fc_write_level(const Dev& D, const BatchArgs& B
   }
   x.depth = f.dfin;
   x.nlive = f.nlive0 + S;
+  x.pad = x.nlive ? l_zero_count(f.z0, 0u, zadd) : 0u;
   uint32_t mem = 0;
   if (hd.ok == FL_OK_DEEP) {
     mem = f.memf;

@@ -64,13 +64,14 @@ __device__ __forceinline__ int book_requalifies(const Dev& D, uint32_t sym) {
   bool anyz = false;
   for (uint32_t k = 0; k < nl; ++k) {
     const Level x = L[k];
-    if (lane == 0 && (x.pad & L_ZERO)) L[k].pad = 0;  // (set below where a zero-volume maker rests)
+    if (lane == 0 && x.pad) L[k].pad = 0;  // (set below where zero-volume makers rest: their count)
     if (!x.member || x.head == NIL) continue;  // (a stale member: checked above)
     const bool sale = x.member == M_SALE;
     uint32_t c = uni(x.head), s0 = uni(x.hslot), cnt = 0;
     const uint32_t tail = uni(x.tail), tslot = uni(x.tslot);
     int64_t sum = 0;
-    bool bad = false, zero = false;
+    bool bad = false;
+    uint32_t zc = 0;
     for (uint32_t guard = 0; c != NIL; ++guard) {
       if (guard > D.ch_cap) return -1;
       const uint32_t lim = (c == tail) ? tslot : CH;
@@ -83,16 +84,16 @@ __device__ __forceinline__ int book_requalifies(const Dev& D, uint32_t sym) {
       }
       const bool live = r >= 0;
       bad = bad || (live && r > 0 && ((tx == GOME_SALE) != sale));
-      zero = zero || (live && r == 0);
+      zc += static_cast<uint32_t>(__popcll(__ballot(live && r == 0)));
       cnt += static_cast<uint32_t>(__popcll(__ballot(live)));
       sum += rl64(wave_incl_scan(live ? r : 0), 63);
       c = (c == tail) ? NIL : uni(D.chdr[c].next);
       s0 = 0;
     }
     if (__ballot(bad) || cnt != x.nlive || sum != x.depth) return -1;
-    if (__ballot(zero)) {
+    if (zc) {
       anyz = true;
-      if (lane == 0) L[k].pad = L_ZERO;
+      if (lane == 0) L[k].pad = l_zero_count(zc, 0u, 0u);
     }
   }
   return static_cast<int>((anyz ? BOOK_ZERO : 0u) | (anys ? BOOK_STALE : 0u));

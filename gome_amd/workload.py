@@ -252,13 +252,14 @@ def inject_quirks(rec: np.ndarray, sym: int, levels: np.ndarray, fifo, mode: str
     are the book's state before `rec` (gome_snapshot_levels / gome_snapshot_fifo, or the
     oracle's).  Mode "zero": zero-volume ADDs only (Q6, "Volume": 0 or null): six takers that cross
     (BUYs at 1.00, SALEs at 0.01: one 0-fill each at the best opposite level, engine.go:176-194),
-    spread over the batch, and one BUY resting behind the lowest bid's makers.  Returns what was
-    injected."""
+    spread over the batch, and one BUY resting behind the lowest bid's makers; "zeroheal": the same
+    with the resting one behind the best bid's makers, where the stream's SALEs soon reach it and pop
+    it with a 0-fill (engine.go:145-161).  Returns what was injected."""
     bids = levels[(levels["in_buy"] != 0) & (levels["in_sale"] == 0) & (levels["n_nodes"] > 0)]
     if len(bids) < 3:
         raise ValueError("book has fewer than three bid levels")
     bids = np.sort(bids, order="price_fx")
-    if mode == "zero":
+    if mode in ("zero", "zeroheal"):
         pos = np.nonzero((rec["symbol_id"] == sym) & (rec["action"] == ADD))[0]
         picks = pos[(np.array([0.001, 0.1, 0.3, 0.5, 0.7, 0.9, 0.95]) * len(pos)).astype(int)]
         for k, i in enumerate(picks[:6]):
@@ -266,8 +267,9 @@ def inject_quirks(rec: np.ndarray, sym: int, levels: np.ndarray, fifo, mode: str
             rec["volume_fx"][i], rec["side"][i] = 0, 1 if sale else 0
             rec["price_fx"][i] = FX // 100 if sale else FX
         z = picks[6]
-        rec["volume_fx"][z], rec["side"][z], rec["price_fx"][z] = 0, 0, bids[0]["price_fx"]
-        return {"q2_price": None, "q2_cancels": 0, "q6_price": int(bids[0]["price_fx"]),
+        zb = bids[-1] if mode == "zeroheal" else bids[0]
+        rec["volume_fx"][z], rec["side"][z], rec["price_fx"][z] = 0, 0, zb["price_fx"]
+        return {"q2_price": None, "q2_cancels": 0, "q6_price": int(zb["price_fx"]),
                 "q6_oid": int(rec["oid_id"][z]), "records": [int(i) for i in picks]}
     heal = mode in ("heal", "q2heal")
     q2 = bids[-1] if heal else bids[0]

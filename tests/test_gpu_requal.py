@@ -229,6 +229,25 @@ def test_zero_volume_maker_no_order_reaches_stays_on_the_flow_path():
     assert all(z >= 1 for _, z, _ in out[2:]), out
 
 
+def test_zero_volume_maker_popped_by_a_passing_taker_stays_on_the_flow_path():
+    """A zero-volume BUY behind the best bid's makers, a BUY of 1.00 behind it, then a SALE at the best
+    bid for the level's depth + 0.50: the SALE fills every old maker, pops the zero-volume one with a
+    0-fill (MatchOrder's diff > 0 branch, engine.go:145-161) and takes half of the new BUY, leaving the
+    level's depth > 0.  The reconstruction pops it (fl_first_back, the intervals), so the book stays
+    on the flow path with no hand-over, exact."""
+    def edit(b, hot, eng):
+        lv = eng.levels(hot)
+        bids = np.sort(lv[(lv["in_buy"] != 0) & (lv["n_nodes"] > 0)], order="price_fx")
+        best = bids[-1]
+        rows = _hot_rows(b, hot)[:3]
+        b["volume_fx"][rows[0]], b["side"][rows[0]], b["price_fx"][rows[0]] = 0, 0, best["price_fx"]
+        b["volume_fx"][rows[1]], b["side"][rows[1]], b["price_fx"][rows[1]] = 10 ** 8, 0, best["price_fx"]
+        b["volume_fx"][rows[2]], b["side"][rows[2]] = int(best["depth_fx"]) + 5 * 10 ** 7, 1
+        b["price_fx"][rows[2]] = best["price_fx"]
+    out = _zero_run(48, edit)
+    assert out[2][0] != 0 and out[2][1] >= 1 and out[2][2] == 0, out
+
+
 def test_zero_volume_maker_at_a_new_price_hands_the_book_to_legacy():
     """A zero-volume BUY below every level: the reference makes it a side-set member of depth 0
     (SetPoolDepth), which the plans would not visit: k_flow_zero_check hands the book to the legacy

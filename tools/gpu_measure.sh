@@ -64,7 +64,7 @@ for P in $PARTS; do
   quirks)
     # quirk injection into the first timed batch (bench.py --inject-quirks): Q2 + Q6 at the bottom /
     # top of the bid book, Q2 alone, Q6 alone
-    for M in stuck q2stuck zero heal; do
+    for M in stuck q2stuck zero zeroheal heal; do
       timeout -k 10 400 python3 -u bench.py --workload config3 --inject-quirks $M --no-cpu-baseline --consumer-msgs 0 \
         > $OUT/config3_${M}_bench.jsonl 2> $OUT/config3_${M}_bench.log || { tail -20 $OUT/config3_${M}_bench.log; exit 4; }
       summ $OUT/config3_${M}_bench.jsonl $M

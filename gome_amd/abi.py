@@ -125,6 +125,8 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.gome_debug_flow_books.restype = C.c_int32
     lib.gome_debug_peek.argtypes = [VP, C.c_uint32, C.c_uint64, C.c_uint64, VP]
     lib.gome_debug_peek.restype = C.c_int32
+    lib.gome_debug_fifo_shape.argtypes = [VP, C.c_uint32, VP, C.c_size_t, C.POINTER(C.c_size_t)]
+    lib.gome_debug_fifo_shape.restype = C.c_int32
     lib.gome_release_device_events.restype = C.c_int32
     lib.gome_get_stats.argtypes = [VP, P(Stats)]
     lib.gome_dup_records.argtypes = [VP, P(C.c_uint32), C.c_size_t, P(C.c_size_t)]
@@ -401,6 +403,14 @@ class Engine:
         buf = C.create_string_buffer(max(nbytes, 1))
         self._check(self.lib.gome_debug_peek(self.h, which, offset, nbytes, buf))
         return buf.raw[:nbytes]
+
+    def debug_fifo_shape(self, symbol_id: int) -> np.ndarray:
+        """Per level of a book: (price_fx, live nodes, dead slots, chunks) (gome_debug_fifo_shape)."""
+        n = C.c_size_t()
+        self._check(self.lib.gome_debug_fifo_shape(self.h, symbol_id, None, 0, C.byref(n)))
+        out = np.zeros((n.value, 4), np.int64)
+        self._check(self.lib.gome_debug_fifo_shape(self.h, symbol_id, out.ctypes.data, n.value, C.byref(n)))
+        return out
 
     def stats(self) -> dict:
         st = Stats()

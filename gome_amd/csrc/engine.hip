@@ -334,6 +334,8 @@ struct gome_engine {
     return he == hipSuccess ? GOME_OK : fail(GOME_E_DEVICE, hipGetErrorString(he));
   }
   hipEvent_t fork{}, join{}, joinf{}, prep_h{}, prep_t{}, fork_adm{}, adm_done{}, seg_done{};
+  hipEvent_t ho_fork{};  // the hottest book's post-plan checks done (its hand-over kernels fork there)
+  hipEvent_t tfc_fork{}, tfc_done{};  // the tail's sort done / its cancel books' level pass done
   hipEvent_t dp_fork{}, cnt_fork{}, cnt_done{}, dw_done{}, dl_done{}, tl_done{};  // the hottest book's deep chain, k_flow_count beside its writes
   // the early plan of the hottest book (match_early.h): the last batch's plan done (flow stream),
   // its oid watermarks folded (hot stream), this batch's early prep and plan done (copy stream)
@@ -473,7 +475,7 @@ struct gome_engine {
         for (hipEvent_t ev : pr)
           if (ev) (void)hipEventDestroy(ev);
     }
-    for (hipEvent_t ev : {fork, join, joinf, prep_h, prep_t, fork_adm, adm_done, seg_done, dp_fork, cnt_fork, cnt_done,
+    for (hipEvent_t ev : {fork, join, joinf, prep_h, prep_t, fork_adm, adm_done, seg_done, ho_fork, tfc_fork, tfc_done, dp_fork, cnt_fork, cnt_done,
                           dw_done, dl_done, tl_done, tob_done, plan_done, oidmax_done, xpre_done, xprep_done,
                           xplan_done, adm_pre_done})
       if (ev) (void)hipEventDestroy(ev);
@@ -657,7 +659,7 @@ gome_status gome_engine::init(const gome_config& c) {
   HIPCHK(new_stream(&copy_stream));
   HIPCHK(new_stream(&d2h_stream));
   HIPCHK(new_stream(&h2d_stream));
-  for (hipEvent_t* ev : {&fork, &join, &joinf, &prep_h, &prep_t, &fork_adm, &adm_done, &seg_done,
+  for (hipEvent_t* ev : {&fork, &join, &joinf, &prep_h, &prep_t, &fork_adm, &adm_done, &seg_done, &ho_fork, &tfc_fork, &tfc_done,
                          &dp_fork, &cnt_fork, &cnt_done, &dw_done, &dl_done, &tl_done, &tob_done, &plan_done,
                          &oidmax_done, &xpre_done, &xprep_done, &xplan_done, &adm_pre_done})
     HIPCHK(hipEventCreateWithFlags(ev, hipEventDisableTiming));
@@ -1281,14 +1283,24 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
     // (hand_wait), which the near books' stream has behind it anyway
     // (books with DELs: stale members and wrong-side cancels, k_fc_stale_level; a bailed one's
     // old targets unmarked)
-    k_flow_zero_check<<<dim3(FL_CAP, nb), FL_LVB_T, 0, st>>>(D, R);
-    if (c_canc) k_fc_stale_level<<<dim3(FL_CAP, nb), FL_LVB_T, 0, st>>>(D, B, R);
+    k_flow_zero_check<<<dim3(FL_CAP, nb), 64, 0, st>>>(D, R);
+    if (c_canc) k_fc_stale_level<<<dim3(FL_CAP, nb), 64, 0, st>>>(D, B, R);
     k_flow_stale_check<<<nb, FL_CAP, 0, st>>>(D, B, R);
     if (c_canc) k_fc_unmark_bailed<<<dim3(FL_PG, nb), 256, 0, st>>>(D, B, R);
-    if (hand_wait) HIPCHK(hipStreamWaitEvent(st, oidmax_done, 0));
-    k_match_hot<<<R.h0 + nb, 64, HOT_LDS_BYTES, st>>>(D, B, d_pend, d_resume, F.hdr, 1u, R.h0, R.h0 + nb);
-    k_match_resume<<<R.h0 + nb, 64, 0, st>>>(D, B, d_resume, F.hdr, R.h0, R.h0 + nb);
-    k_pend_apply<<<dim3(8, R.h0 + nb), 256, 0, st>>>(D, d_pend, S.seg_start, S.seg_order, B, F.hdr, R.h0, R.h0 + nb);
+    // the hand-over kernels (the legacy kernel in mode 1 for a bailed book, almost always a launch
+    // with nothing to do): for the hottest book on the other stream, off its critical path (they
+    // took 0.1 ms each on config 5c's, waiting for room on busy CUs); the batch's join waits for
+    // that stream before the publish.  The flow kernels after the checks skip a bailed book.
+    hipStream_t hs = st;
+    if (hand_wait && split) {
+      HIPCHK(hipEventRecord(ho_fork, st));
+      HIPCHK(hipStreamWaitEvent(cs, ho_fork, 0));
+      hs = cs;
+    }
+    if (hand_wait) HIPCHK(hipStreamWaitEvent(hs, oidmax_done, 0));
+    k_match_hot<<<R.h0 + nb, 64, HOT_LDS_BYTES, hs>>>(D, B, d_pend, d_resume, F.hdr, 1u, R.h0, R.h0 + nb);
+    k_match_resume<<<R.h0 + nb, 64, 0, hs>>>(D, B, d_resume, F.hdr, R.h0, R.h0 + nb);
+    k_pend_apply<<<dim3(8, R.h0 + nb), 256, 0, hs>>>(D, d_pend, S.seg_start, S.seg_order, B, F.hdr, R.h0, R.h0 + nb);
     if (!split && c_deep) deep_sort_level(R, FL_SORT_GRID, st, pl);
     k_flow_level_wide<<<dim3(FL_CAP, nb), FL_LVB_T, 0, st>>>(D, R);
     toff(R, false, st);
@@ -1360,6 +1372,17 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
     HIPCHK(mark(GOME_PH_TAIL_SORT, 0, s));
     k_flow_sort<<<nh_tail, FL_SORT_T, 0, s>>>(D, FT);
     HIPCHK(mark(GOME_PH_TAIL_SORT, 1, s));
+    // the level pass of the tail's lane books with DELs needs only their sorted touches: on the
+    // cold books' stream (idle by the time the tail's plans end), beside the deep books' sort and
+    // level pass, which took 15 ms on config 5c's tail and had it behind them, 2.8 ms after the
+    // hottest book's plan ended, where it slowed that book's reconstruction (gpurun_out/r05ap)
+    const bool tfc_split = c_canc && cst != s;
+    if (tfc_split) {
+      HIPCHK(hipEventRecord(tfc_fork, s));
+      HIPCHK(hipStreamWaitEvent(cst, tfc_fork, 0));
+      k_fc_level_book<<<nh_tail, 1024, 0, cst>>>(D, FT);
+      HIPCHK(hipEventRecord(tfc_done, cst));
+    }
     HIPCHK(mark(GOME_PH_TAIL_LEVEL, 0, s));
     k_flow_level<<<nh_tail, FL_LEVEL_T, 0, s>>>(D, FT);
     if (c_deep) deep_sort_level(FT, 32, s, false);
@@ -1380,7 +1403,8 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
     HIPCHK(mark(GOME_PH_TAIL_EVENTS, 0, s));
     if (c_deep) deep_write(FT, s);
     if (c_canc) {
-      k_fc_level_book<<<nh_tail, 1024, 0, s>>>(D, FT);
+      if (tfc_split) HIPCHK(hipStreamWaitEvent(s, tfc_done, 0));
+      else k_fc_level_book<<<nh_tail, 1024, 0, s>>>(D, FT);
       toff(FTc, true, s);
       k_fc_count<<<1024, 256, 0, s>>>(D, B, FTc);
       k_fc_write_book<<<nh_tail, FL_WRITE_T, 0, s>>>(D, B, FTc);
@@ -1985,6 +2009,40 @@ gome_status gome_debug_peek(gome_engine* e, uint32_t which, uint64_t offset, uin
   if (offset > size || bytes > size - offset) return GOME_E_INVAL;
   if (bytes && hipMemcpy(out, static_cast<const char*>(base) + offset, bytes, hipMemcpyDeviceToHost) != hipSuccess)
     return e->fail(GOME_E_DEVICE, "gome_debug_peek: copy failed");
+  return GOME_OK;
+}
+
+gome_status gome_debug_fifo_shape(gome_engine* e, uint32_t sym, int64_t* out, size_t cap, size_t* n_out) {
+  if (!e || !n_out || (cap && !out)) return GOME_E_INVAL;
+  DevGuard dg(e->cfg.device);
+  if (gome_status st = e->collect_all()) return st;
+  if (sym >= e->cfg.max_symbols) return e->fail(GOME_E_NOTFOUND, "symbol_id out of range");
+  Book bk;
+  if (hipMemcpy(&bk, e->D.books + sym, sizeof bk, hipMemcpyDeviceToHost) != hipSuccess)
+    return e->fail(GOME_E_DEVICE, "fifo shape copy failed");
+  std::vector<Level> lv(bk.n_lvl);
+  std::vector<ChunkHdr> ch(e->D.ch_cap);
+  std::vector<Node> nd(static_cast<size_t>(e->D.ch_cap) * CH);
+  if ((bk.n_lvl && hipMemcpy(lv.data(), e->D.lvl + bk.lvl_base, bk.n_lvl * sizeof(Level), hipMemcpyDeviceToHost) != hipSuccess) ||
+      hipMemcpy(ch.data(), e->D.chdr, ch.size() * sizeof(ChunkHdr), hipMemcpyDeviceToHost) != hipSuccess ||
+      hipMemcpy(nd.data(), e->D.nodes, nd.size() * sizeof(Node), hipMemcpyDeviceToHost) != hipSuccess)
+    return e->fail(GOME_E_DEVICE, "fifo shape copy failed");
+  for (size_t k = 0; k < lv.size() && k < cap; ++k) {
+    const Level& L = lv[k];
+    int64_t live = 0, dead = 0, nch = 0;
+    uint32_t c = L.head;
+    for (uint32_t s0 = L.hslot; c != NIL && nch <= e->D.ch_cap; s0 = 0) {
+      const uint32_t hi = (c == L.tail) ? L.tslot : CH;
+      for (uint32_t sl = s0; sl < hi; ++sl) (nd[static_cast<size_t>(c) * CH + sl].rem < 0 ? dead : live)++;
+      ++nch;
+      c = (c == L.tail) ? NIL : ch[c].next;
+    }
+    out[4 * k] = L.price;
+    out[4 * k + 1] = live;
+    out[4 * k + 2] = dead;
+    out[4 * k + 3] = nch;
+  }
+  *n_out = lv.size();
   return GOME_OK;
 }
 

@@ -3023,53 +3023,6 @@ __global__ __launch_bounds__(FL_TILE) void k_flow_sort_scatter(Dev D, FlowArgs F
   }
 }
 
-// Block-wide exclusive max of one uint32 per thread (FL_LVB_T threads); *total = the block's max.
-__device__ __forceinline__ uint32_t fl_blk_max_excl(uint32_t x, uint32_t* total) {
-  __shared__ uint32_t wm[FL_LVB_W];
-  const uint32_t w = threadIdx.x >> 6, lane = lane_id();
-  uint32_t inc = x;
-  for (uint32_t off = 1; off < 64; off <<= 1) {
-    const uint32_t v = __shfl_up(inc, off);
-    if (lane >= off) inc = max(inc, v);
-  }
-  const uint32_t ex = max(__shfl_up(inc, 1), 0u);
-  if (lane == 63u) wm[w] = inc;
-  __syncthreads();
-  uint32_t before = 0, tot = 0;
-  for (uint32_t k = 0; k < FL_LVB_W; ++k) {
-    const uint32_t v = wm[k];
-    before = k < w ? max(before, v) : before;
-    tot = max(tot, v);
-  }
-  __syncthreads();  // (wm is reused by the next call)
-  *total = tot;
-  return max(before, lane ? ex : 0u);
-}
-
-// Block-wide exclusive max of one int64 per thread (FL_LVB_T threads; -1 where nothing precedes);
-// *total = the block's max.
-__device__ __forceinline__ int64_t fl_blk_max64_excl(int64_t x, int64_t* total) {
-  __shared__ int64_t wm64[FL_LVB_W];
-  const uint32_t w = threadIdx.x >> 6, lane = lane_id();
-  int64_t inc = x;
-  for (uint32_t off = 1; off < 64; off <<= 1) {
-    const int64_t v = __shfl_up(inc, off);
-    if (lane >= off) inc = max(inc, v);
-  }
-  const int64_t ex = __shfl_up(inc, 1);
-  if (lane == 63u) wm64[w] = inc;
-  __syncthreads();
-  int64_t before = -1, tot = -1;
-  for (uint32_t k = 0; k < FL_LVB_W; ++k) {
-    const int64_t v = wm64[k];
-    before = k < w ? max(before, v) : before;
-    tot = max(tot, v);
-  }
-  __syncthreads();  // (wm64 is reused by the next call)
-  *total = tot;
-  return max(before, lane ? ex : static_cast<int64_t>(-1));
-}
-
 // Books planned with zero-volume ADDs (Q6, k_flow_prep_b) or holding zero-volume makers (FlowLvl::z0):
 // the reconstruction takes a zero-volume maker where no order reaches it, and (ADD books) where a
 // consume passes it with volume to spare at the level (it pops it with a 0-fill, engine.go:145-161).  One block
@@ -3083,8 +3036,28 @@ __device__ __forceinline__ int64_t fl_blk_max64_excl(int64_t x, int64_t* total) 
 // that passes it (fl_first_back; the gather in fl_level_one).  Books with
 // DELs (the cancel path): a cancel lowers the depth like a CONS; a CONS of 0 (a zero-volume taker,
 // whose one 0-fill the cancel path's events do not model) is a hazard as well.
-__global__ __launch_bounds__(FL_LVB_T) void k_flow_zero_check(Dev D, FlowArgs F) {
-  const uint32_t h = F.h0 + blockIdx.y, q = blockIdx.x, tid = threadIdx.x;
+// Wave-wide exclusive scans (one wave per level: the checks run in the rare batches that need them,
+// and a launch of small blocks gets onto busy CUs at once; 1024-thread blocks waited ~0.8 ms for
+// room on config 5c's critical path even when every block had nothing to do).
+__device__ __forceinline__ int64_t fl_wave_excl(int64_t x, int64_t* total) {
+  const int64_t inc = wave_incl_scan(x);
+  *total = rl64(inc, 63);
+  return inc - x;
+}
+__device__ __forceinline__ int64_t fl_wave_max_excl(int64_t x, int64_t* total) {
+  const uint32_t lane = lane_id();
+  int64_t inc = x;
+  for (uint32_t off = 1; off < 64; off <<= 1) {
+    const int64_t v = __shfl_up(inc, off);
+    if (lane >= off) inc = max(inc, v);
+  }
+  *total = rl64(inc, 63);
+  const int64_t ex = __shfl_up(inc, 1);
+  return lane ? ex : static_cast<int64_t>(-1);
+}
+
+__global__ __launch_bounds__(64) void k_flow_zero_check(Dev D, FlowArgs F) {
+  const uint32_t h = F.h0 + blockIdx.y, q = blockIdx.x, lane = lane_id();
   if (h >= fl_hend(D, F)) return;
   FlowHdr* hd = &F.hdr[h];
   const bool canc = hd->ok == FL_OK_CANCEL && !hd->fc_bad;
@@ -3099,19 +3072,19 @@ __global__ __launch_bounds__(FL_LVB_T) void k_flow_zero_check(Dev D, FlowArgs F)
   int64_t zlast = -1;        // start of the latest zero-volume maker rested before the chunk (-1: none)
   bool zero = Lq->z0 != 0;   // cancel books: a zero-volume maker may be in the FIFO before the chunk
   bool haz = false;
-  for (uint32_t c0 = 0; c0 < cnt; c0 += FL_LVB_T) {
-    const uint32_t i = c0 + tid;
+  for (uint32_t c0 = 0; c0 < cnt; c0 += 64) {
+    const uint32_t i = c0 + lane;
     const bool valid = i < cnt;
     SEnt e{};
     if (valid) e = R[i];
     const bool isr = valid && e.kind == TK_REST, isc = valid && e.kind == TK_CONS, zr = isr && e.amt == 0;
     const bool isx = valid && e.kind == TK_CANC;
     int64_t tot, tz, tr, tc, tzm;
-    const int64_t before = run + fl_blk_excl(isr ? e.amt : (isc || isx) ? -e.amt : 0, &tot);
-    const int64_t zb = fl_blk_excl(zr ? 1 : 0, &tz);
-    const int64_t rb = rr + fl_blk_excl(isr ? e.amt : 0, &tr);  // this REST's start
-    const int64_t cb = cc + fl_blk_excl(isc ? e.amt : 0, &tc);  // this CONS's cursor
-    const int64_t zm = max(zlast, fl_blk_max64_excl(zr ? rb : -1, &tzm));
+    const int64_t before = run + fl_wave_excl(isr ? e.amt : (isc || isx) ? -e.amt : 0, &tot);
+    const int64_t zb = fl_wave_excl(zr ? 1 : 0, &tz);
+    const int64_t rb = rr + fl_wave_excl(isr ? e.amt : 0, &tr);  // this REST's start
+    const int64_t cb = cc + fl_wave_excl(isc ? e.amt : 0, &tc);  // this CONS's cursor
+    const int64_t zm = max(zlast, fl_wave_max_excl(zr ? rb : -1, &tzm));
     if (canc) {  // cancel books: any consume after a zero-volume maker may be in the FIFO
       haz = haz || (zr && before == 0) || (isc && (zero || zb > 0 || e.amt == 0));
     } else {
@@ -3130,7 +3103,7 @@ __global__ __launch_bounds__(FL_LVB_T) void k_flow_zero_check(Dev D, FlowArgs F)
     zlast = max(zlast, tzm);
     zero = zero || tz > 0;
   }
-  if (__syncthreads_or(haz) && tid == 0) atomicOr(&hd->haz, 1u);
+  if (__ballot(haz) && lane == 0) atomicOr(&hd->haz, 1u);
 }
 
 // After the head's level sort: a book planned with stale members is exact unless an order rested

@@ -879,8 +879,8 @@ __global__ void k_fc_route(Dev D, FlowArgs F) {
 // the batch (fc_write_level keeps it).
 enum : uint32_t { ST_BUY = 1, ST_SALE = 2, ST_NONE = 3, ST_STALE_BUY = 4, ST_STALE_SALE = 5 };
 
-__global__ __launch_bounds__(FL_LVB_T) void k_fc_stale_level(Dev D, BatchArgs B, FlowArgs F) {
-  const uint32_t h = F.h0 + blockIdx.y, q = blockIdx.x, tid = threadIdx.x;
+__global__ __launch_bounds__(64) void k_fc_stale_level(Dev D, BatchArgs B, FlowArgs F) {
+  const uint32_t h = F.h0 + blockIdx.y, q = blockIdx.x, lane = lane_id();
   if (h >= fl_hend(D, F)) return;
   FlowHdr* hd = &F.hdr[h];
   if (hd->ok != FL_OK_CANCEL || hd->fc_bad || (hd->nstale == 0 && hd->nwrong == 0) || q == 0 || q > hd->nl) return;
@@ -891,18 +891,18 @@ __global__ __launch_bounds__(FL_LVB_T) void k_fc_stale_level(Dev D, BatchArgs B,
   const SEnt* R = F.srt + FL_TOUCH_MUL * beg + Lq->base;
   uint32_t state = st0 ? (Lq->mem0 == M_SALE ? ST_STALE_SALE : ST_STALE_BUY)
                        : Lq->d0 > 0 ? (Lq->mem0 == M_SALE ? ST_SALE : ST_BUY) : ST_NONE;
-  uint32_t carry = 0;      // (index + 1) << 3 | code of the last state-setting touch of earlier chunks
+  int64_t carry = -1;      // (index + 1) << 3 | code of the last state-setting touch of earlier chunks
   int64_t run = Lq->d0;    // the level's depth before the chunk
   bool haz = false;
-  for (uint32_t c0 = 0; c0 < cnt; c0 += FL_LVB_T) {
-    const uint32_t i = c0 + tid;
+  for (uint32_t c0 = 0; c0 < cnt; c0 += 64) {
+    const uint32_t i = c0 + lane;
     const bool valid = i < cnt;
     SEnt e{};
     if (valid) e = R[i];
     const bool isr = valid && e.kind == TK_REST, isc = valid && e.kind == TK_CONS, isx = valid && e.kind == TK_CANC;
+    const int64_t delta = isr ? e.amt : (isc || isx) ? -e.amt : 0;
     int64_t tot;
-    const int64_t after = run + fl_blk_excl(isr ? e.amt : (isc || isx) ? -e.amt : 0, &tot) +
-                          (isr ? e.amt : (isc || isx) ? -e.amt : 0);
+    const int64_t after = run + fl_wave_excl(delta, &tot) + delta;
     bool rsale = false;
     uint32_t code = 0;
     if (isr) {
@@ -915,16 +915,17 @@ __global__ __launch_bounds__(FL_LVB_T) void k_fc_stale_level(Dev D, BatchArgs B,
         if ((prep_at(B, beg + e.j).side == GOME_SALE) != msale) code = msale ? ST_STALE_SALE : ST_STALE_BUY;
       }
     }
-    uint32_t mtot;
-    const uint32_t prev_key = max(carry, fl_blk_max_excl(code ? ((i + 1u) << 3) | code : 0u, &mtot));
-    const uint32_t prev = prev_key ? (prev_key & 7u) : state;
+    int64_t mtot;
+    const int64_t key = code ? (static_cast<int64_t>(i + 1) << 3) | code : -1;
+    const int64_t prev_key = max(carry, fl_wave_max_excl(key, &mtot));
+    const uint32_t prev = prev_key >= 0 ? static_cast<uint32_t>(prev_key & 7) : state;
     if (isr && (prev == (rsale ? ST_STALE_BUY : ST_STALE_SALE))) haz = true;  // the other side's stale price
     carry = max(carry, mtot);
     run += tot;
   }
-  if (__syncthreads_or(haz) && tid == 0) atomicOr(&hd->haz, 1u);
-  if (tid == 0) {
-    const uint32_t fin = carry ? (carry & 7u) : state;
+  if (__ballot(haz) && lane == 0) atomicOr(&hd->haz, 1u);
+  if (lane == 0) {
+    const uint32_t fin = carry >= 0 ? static_cast<uint32_t>(carry & 7) : state;
     Lq->mfin = fin == ST_STALE_BUY ? M_BUY : fin == ST_STALE_SALE ? M_SALE : 0u;
   }
 }

@@ -350,6 +350,10 @@ gome_status gome_debug_flow_books(gome_engine* e, uint32_t* out, size_t cap, siz
  * arrays after the last batch (0 headers, 1 level slots, 2 DEL records, 3 targeted-ADD ranks,
  * 4 DEL-of-ADD links, 5 packed records). */
 gome_status gome_debug_peek(gome_engine* e, uint32_t which, uint64_t offset, uint64_t bytes, void* out);
+/* Diagnostics: the shape of one book's FIFOs, 4 words per level in the book's level order
+ * {price_fx, live nodes, dead slots (cancelled / consumed, still linked), chunks}.  *n_out =
+ * levels (only cap are written). */
+gome_status gome_debug_fifo_shape(gome_engine* e, uint32_t symbol_id, int64_t* out, size_t cap, size_t* n_out);
 
 /* ---- pipelined host path (ABI >= 4) ---------------------------------------- */
 /* The batching consumer's loop: submit batch k+1, then collect batch k.

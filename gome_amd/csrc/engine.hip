@@ -121,6 +121,15 @@ __global__ void k_ctr_fold(Dev D) {
     D.ctr_s[k * CTR_STRIDE + c] = 0;
   }
   D.st->ctr[c] += v;
+#ifdef GOME_PROBE_LEVEL
+  if (c == 0) {
+    printf("PROBE levels %llu t12 %llu t3 %llu walk %llu max %llu cnt %llu slow %llu maxcnt %llu | waves %llu wsum %llu wmax %llu w>10us %llu span %llu\n",
+           g_probe[2], g_probe[0], g_probe[1], g_probe[3], g_probe[4], g_probe[5], g_probe[6], g_probe[7], g_probe[8],
+           g_probe[9], g_probe[10], g_probe[11], g_probe[13] - g_probe[12]);
+    for (int k = 0; k < 16; ++k) g_probe[k] = 0;
+    g_probe[12] = ~0ull;
+  }
+#endif
 }
 
 __global__ __launch_bounds__(256) void k_lvl_recycle(Dev D) {
@@ -1248,6 +1257,9 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
     deep_sort(R, tiles, st);
     const bool hot = per_level && c_canc;
     k_deep_level<<<dim3(DEEP_GRID, ns), 64, 0, st>>>(D, R, hot ? 1u : 0u);
+    // (after k_deep_level: a level pass overwrites its level's run end, FlowLvl::pad1, which
+    // k_deep_level reads and fd_run checks)
+    if (!hot && c_canc) k_deep_level_big<<<dim3(DEEP_BIG_GRID, ns), FC_LVB_T, 0, st>>>(D, R);
     if (hot) k_deep_level_hot<<<DEEP_GRID / 16, FC_LVB_T, 0, st>>>(D, R);
   };
   auto deep_write = [&](const FlowArgs& R, hipStream_t st) {

@@ -1009,6 +1009,11 @@ __device__ __forceinline__ uint32_t fc_find(const FcLvlView& V, int64_t x) {
   return V.ig_n + lo;
 }
 
+#ifdef GOME_PROBE_LEVEL
+// (tuning builds: the level passes' time split, summed over a batch; k_ctr_fold prints and clears)
+__device__ unsigned long long g_probe[16];
+#endif
+
 // ---- k_fc_level: one wave per (book, level) ----------------------------------------------
 __device__ __forceinline__ void fc_level_one(const Dev& D, const FlowArgs& F, uint32_t h, uint32_t q) {
   const FlowHdr* hd = &F.hdr[h];
@@ -1022,6 +1027,10 @@ __device__ __forceinline__ void fc_level_one(const Dev& D, const FlowArgs& F, ui
   const int64_t d0 = uni64(Lq->d0);
   SEnt* R = F.srt + L + base;
   RsEnt* RS = F.rs + L + base;
+#ifdef GOME_PROBE_LEVEL  // (tuning builds, tools/build_variant.py: slow levels on stdout)
+  const uint64_t pt0 = wall_clock64();
+  uint32_t pwalk = 0;
+#endif
   // 1. each cancel -> its DEL's record (r, touch); the consumption cursor before each consume
   int64_t cc = 0, ocan = 0;
   uint32_t nr = 0, ncan_old = 0;
@@ -1085,6 +1094,9 @@ __device__ __forceinline__ void fc_level_one(const Dev& D, const FlowArgs& F, ui
     k += __popcll(rm);
   }
   const int64_t qend = acc;
+#ifdef GOME_PROBE_LEVEL
+  const uint64_t pt1 = wall_clock64();
+#endif
   // 3. the old FIFO, gathered through the consumption end, then on through targeted makers (a
   //    later cancel may remove them) to the first untargeted one (never cancelled, so a
   //    MatchNode.NextNode search stops there)
@@ -1158,6 +1170,9 @@ __device__ __forceinline__ void fc_level_one(const Dev& D, const FlowArgs& F, ui
       E += rl64(inc, 63);
       c = uni(nxt);
       s0 = 0;
+#ifdef GOME_PROBE_LEVEL
+      ++pwalk;
+#endif
     }
     if (!have_surv && ig_all) {
       head = ttail = NIL;
@@ -1168,6 +1183,21 @@ __device__ __forceinline__ void fc_level_one(const Dev& D, const FlowArgs& F, ui
     }
     // (!have_surv && !ig_all cannot happen: the untargeted stop maker survives)
   }
+#ifdef GOME_PROBE_LEVEL
+  {
+    const uint64_t pt2 = wall_clock64();
+    if (lane == 0) {
+      atomicAdd(&g_probe[0], pt1 - pt0);
+      atomicAdd(&g_probe[1], pt2 - pt1);
+      atomicAdd(&g_probe[2], 1ull);
+      atomicAdd(&g_probe[3], static_cast<unsigned long long>(pwalk));
+      atomicMax(&g_probe[4], pt2 - pt0);
+      atomicAdd(&g_probe[5], static_cast<unsigned long long>(cnt));
+      if (pt2 - pt0 > GOME_PROBE_LEVEL) atomicAdd(&g_probe[6], 1ull);
+      atomicMax(&g_probe[7], static_cast<unsigned long long>(cnt));
+    }
+  }
+#endif
   if (lane == 0) {
     Lq->cfin = cfin;
     Lq->nrest = nr;
@@ -1186,6 +1216,8 @@ __device__ __forceinline__ void fc_level_one(const Dev& D, const FlowArgs& F, ui
 }
 
 constexpr uint32_t FC_LVB_T = FL_LVB_T, FC_K = 4;
+// a level of FC_BIG touches or more takes a whole block (fc_level_blk), smaller ones a wave
+constexpr uint32_t FC_BIG = 1024;
 
 // fc_level_one with a whole block (FC_LVB_T threads) on one level: the level's touches in
 // block-wide chunks (the long levels of the hottest books hold tens of thousands of touches,
@@ -1405,10 +1437,22 @@ __global__ __launch_bounds__(64) void k_fc_level_wide(Dev D, FlowArgs F) {
   fc_level_one(D, F, h, q);
 }
 
-__global__ __launch_bounds__(1024) void k_fc_level_book(Dev D, FlowArgs F) {
+// The tail's books: a block per book.  Its busiest levels first, each with the whole block (the
+// aggressive orders' remainders rest at 1.00 / 0.01 and the other side's orders consume there: one
+// wave took 64 of those touches at a time, and config 4's tail level pass took 5.8 ms), then the
+// others a wave each.
+__global__ __launch_bounds__(FC_LVB_T) void k_fc_level_book(Dev D, FlowArgs F) {
   const uint32_t h = F.h0 + blockIdx.x;
   if (h >= fl_hend(D, F) || !fc_lane(F, h)) return;
-  for (uint32_t q = 1 + (threadIdx.x >> 6); q <= F.hdr[h].nl; q += blockDim.x / 64) fc_level_one(D, F, h, uni(q));
+  const uint32_t nl = F.hdr[h].nl;
+  const FlowLvl* LV = fl_lvls(F, h);
+  for (uint32_t q = 1; q <= nl; ++q) {
+    if (LV[q].cnt < FC_BIG) continue;
+    fc_level_blk(D, F, h, q);
+    __syncthreads();  // (fc_level_blk's shared words, before the next level's)
+  }
+  for (uint32_t q = 1 + (threadIdx.x >> 6); q <= nl; q += blockDim.x / 64)
+    if (uni(LV[q].cnt) < FC_BIG) fc_level_one(D, F, h, uni(q));
 }
 
 // ---- fills of one consume touch ----------------------------------------------------------

@@ -562,6 +562,7 @@ __device__ __forceinline__ void k_deep_level_one(Dev D, FlowArgs F, uint32_t slo
     for (unsigned long long hm = __ballot(head); hm; hm &= hm - 1) {
       const uint32_t q = uni(rl(lv, static_cast<uint32_t>(__builtin_ctzll(hm))));
       const uint32_t e = uni(LV[q].pad1), b = uni(LV[q].base);  // (k_deep_runs)
+      if (dc && e - b >= FC_BIG) continue;  // (k_deep_level_big)
       if (lane == 0) LV[q].cnt = e - b;
       if (dc) {
         __threadfence_block();  // (fc_level_one reads the count back)
@@ -572,11 +573,48 @@ __device__ __forceinline__ void k_deep_level_one(Dev D, FlowArgs F, uint32_t slo
     }
   }
 }
-// skip_dc: books with DELs are k_deep_level_hot's (the hottest book's launch)
+// skip_dc: books with DELs are k_deep_level_hot's (the hottest book's launch); otherwise a book
+// with DELs leaves its levels of FC_BIG touches or more to k_deep_level_big
 __global__ __launch_bounds__(64) void k_deep_level(Dev D, FlowArgs F, uint32_t skip_dc) {
+#ifdef GOME_PROBE_LEVEL
+  const uint64_t t0 = wall_clock64();
+#endif
   for (uint32_t i = blockIdx.y; i < fd_nslots(F); i += gridDim.y) {
     k_deep_level_one(D, F, i, skip_dc);
     __syncthreads();
+  }
+#ifdef GOME_PROBE_LEVEL
+  if (threadIdx.x == 0) {
+    const uint64_t t = wall_clock64() - t0;
+    atomicAdd(&g_probe[8], 1ull);
+    atomicAdd(&g_probe[9], t);
+    atomicMax(&g_probe[10], t);
+    if (t > 1000) atomicAdd(&g_probe[11], 1ull);
+    atomicMin(&g_probe[12], t0);
+    atomicMax(&g_probe[13], t0 + t);
+  }
+#endif
+}
+
+// The tail's deep books with DELs: their levels of FC_BIG touches or more, a block each (the
+// tail's level pass took 15 ms on config 5c, one wave per level; gpurun_out/r05ar).
+__device__ __forceinline__ uint32_t fd_run(const FlowLvl* LV, const SEnt* R, uint32_t nt, uint32_t q);
+constexpr uint32_t DEEP_BIG_GRID = 8;  // blocks per deep book
+__global__ __launch_bounds__(FC_LVB_T) void k_deep_level_big(Dev D, FlowArgs F) {
+  for (uint32_t i = blockIdx.y; i < fd_nslots(F); i += gridDim.y) {
+    const uint32_t h = fd_book(D, F, i);
+    if (!fd_deep(F, h) || !F.hdr[h].dc) continue;
+    const uint32_t nt = F.hdr[h].ntouch, L = FL_TOUCH_MUL * F.hdr[h].beg, nl = F.hdr[h].nl;
+    FlowLvl* LV = fl_lvls(F, h);
+    const SEnt* R = F.srt + L;
+    for (uint32_t q = 1 + blockIdx.x; q <= nl; q += gridDim.x) {
+      const uint32_t cnt = fd_run(LV, R, nt, q);
+      if (cnt < FC_BIG) continue;
+      if (threadIdx.x == 0) LV[q].cnt = cnt;
+      __syncthreads();
+      fc_level_blk(D, F, h, q);
+      __syncthreads();
+    }
   }
 }
 
@@ -587,7 +625,6 @@ __global__ __launch_bounds__(64) void k_deep_level(Dev D, FlowArgs F, uint32_t s
 // level of FC_BIG touches or more (fc_level_blk), then its waves the others, one level each.
 // A level's run counts only where the sorted touches hold exactly it: base / pad1 of a level the
 // cancel prep's key sort gave a run that no touch reached are still that sort's.
-constexpr uint32_t FC_BIG = 1024;
 __device__ __forceinline__ uint32_t fd_run(const FlowLvl* LV, const SEnt* R, uint32_t nt, uint32_t q) {
   const uint32_t e = LV[q].pad1, b = LV[q].base;
   const bool ok = e != 0 && e <= nt && b < e && R[b].lvl == q && R[e - 1].lvl == q && (b == 0 || R[b - 1].lvl != q) &&

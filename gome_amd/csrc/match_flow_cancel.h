@@ -1215,6 +1215,158 @@ __device__ __forceinline__ void fc_level_one(const Dev& D, const FlowArgs& F, ui
   }
 }
 
+// fc_level_one by ONE lane, for a level of at most FC_LANE_MAX touches (the same outputs; the
+// DEL records it writes in step 1 are the ones it reads back in steps 2 and 3, a level's own
+// cancels, so no fence).  The tail's deep books hold ~600k levels per batch with ~3 touches each
+// (config 5c, GOME_PROBE_LEVEL): one wave took them one after another, each a chain of dependent
+// loads, and k_deep_level ran 15 ms.  Lanes take their levels side by side.
+constexpr uint32_t FC_LANE_MAX = 16;
+__device__ __forceinline__ void fc_level_lane(const Dev& D, const FlowArgs& F, uint32_t h, uint32_t q, uint32_t cnt) {
+  const FlowHdr* hd = &F.hdr[h];
+  FlowLvl* Lq = fl_lvls(F, h) + q;
+  const uint32_t beg = hd->beg;
+  const uint32_t L = FL_TOUCH_MUL * beg;
+  const unsigned long long g = static_cast<unsigned long long>(hd->g);
+  const uint32_t base = Lq->base;
+  const int64_t d0 = Lq->d0;
+  SEnt* R = F.srt + L + base;
+  RsEnt* RS = F.rs + L + base;
+  // 1. cancels -> their DEL records; the consumption cursor before each consume
+  int64_t cc = 0, ocan = 0;
+  uint32_t nr = 0, ncan_old = 0;
+  for (uint32_t i = 0; i < cnt; ++i) {
+    const SEnt e = R[i];
+    if (e.kind == TK_CANC) {
+      FcDel* d = &F.fc_del[beg + e.j];
+      d->r = e.amt;
+      d->ct = e.t;
+      if (d->kind == FC_OLD) { ocan += e.amt; ncan_old++; }
+    } else if (e.kind == TK_CONS) {
+      R[i].coord = cc;
+      cc += e.amt;
+    } else if (e.kind == TK_REST) {
+      nr++;
+    }
+  }
+  const int64_t cfin = cc;
+  // 2. the new makers in FIFO order
+  int64_t acc = d0 - ocan;
+  uint32_t k = 0;
+  for (uint32_t i = 0; i < cnt; ++i) {
+    const SEnt e = R[i];
+    if (e.kind != TK_REST) continue;
+    uint32_t ct = NIL;
+    int64_t len = e.amt;
+    const uint32_t tg = F.fc_tg[beg + e.j];
+    if (tg) {
+      const FcDel d = F.fc_del[tg - 1u];
+      if (d.ct != NIL) { ct = d.ct; len = e.amt - d.r; }
+    }
+    RsEnt x;
+    x.e = acc;
+    x.v = e.amt;
+    x.j = e.j;
+    x.t = e.t;
+    x.pad0 = ct;
+    x.pad1 = 0;
+    RS[k++] = x;
+    acc += len;
+  }
+  const int64_t qend = acc;
+  // 3. the old FIFO (fc_level_one's walk, a chunk's slots in order)
+  const uint32_t nv0 = Lq->nv0, tail = Lq->tail, tslot = Lq->tslot;
+  uint32_t head = Lq->head, hslot = Lq->hslot;
+  uint32_t ttail = tail, ttslot = tslot;
+  uint32_t ig_base = 0, ng = 0, consumed = 0;
+  bool ig_all = true;
+  if (nv0 > 0 && (cfin > 0 || Lq->c_old)) {
+    ig_base = atomicAdd(F.ig_bump, nv0);
+    if (static_cast<unsigned long long>(ig_base) + nv0 > F.ig_cap) {
+      atomicOr(&D.st->err, ERR_CHUNKS);
+      return;
+    }
+    IgEnt* IG = F.ig + ig_base;
+    int64_t E = 0;
+    bool have_surv = false, stop = false;
+    uint32_t c = head, s0 = hslot, nh = NIL, nhs = 0;
+    for (uint32_t guard = 0; c != NIL && !stop; ++guard) {
+      if (guard > D.ch_cap) { atomicOr(&D.st->err, ERR_CORRUPT); return; }
+      const uint32_t lim = (c == tail) ? tslot : CH;
+      const uint32_t nxt = (c == tail) ? NIL : D.chdr[c].next;
+      Node nd[CH];
+#pragma unroll
+      for (uint32_t s = 0; s < CH; ++s) {
+        nd[s] = Node{};
+        if (s >= s0 && s < lim) nd[s] = D.nodes[c * CH + s];
+      }
+      bool taking = true, surv_here = false;
+#pragma unroll
+      for (uint32_t s = 0; s < CH; ++s) {
+        const bool live = s >= s0 && s < lim && nd[s].rem >= 0;
+        if (!live) continue;
+        const bool targ = nd[s].pad != 0;
+        uint32_t ct = NIL;
+        int64_t len = nd[s].rem;
+        if (targ) {
+          const FcDel d = F.fc_del[static_cast<uint32_t>(nd[s].pad) - 1u];
+          if (d.ct != NIL) { ct = d.ct; len = nd[s].rem - d.r; }
+        }
+        const int64_t em = E;
+        E += len;
+        if (taking) {  // (every live maker through the first untargeted one at or past the consumption end)
+          IgEnt gq;
+          gq.e = em;
+          gq.v = nd[s].rem;
+          gq.oid = nd[s].oid;
+          gq.uuid = nd[s].uuid;
+          gq.tx = nd[s].tx;
+          gq.pad = ct;
+          IG[ng++] = gq;
+          if (em >= cfin && !targ) { taking = false; stop = true; ig_all = false; }
+        }
+        const bool cons = ct == NIL && em + nd[s].rem <= cfin;
+        if (cons) {
+          __hip_atomic_store(&D.idx[nd[s].ixs].key, KEY_TOMB, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          consumed++;
+        }
+        if (!have_surv && !surv_here && ct == NIL && em + nd[s].rem > cfin) {
+          surv_here = true;
+          nh = c;
+          nhs = s;
+          if (em < cfin) D.nodes[c * CH + s].rem = em + nd[s].rem - cfin;  // partial head
+        }
+      }
+      if (!have_surv) {
+        if (surv_here) have_surv = true;
+        else D.freed_ids[atomicAdd(&D.st->freed_top, 1u)] = c;
+      }
+      c = nxt;
+      s0 = 0;
+    }
+    if (!have_surv && ig_all) {
+      head = ttail = NIL;
+      hslot = ttslot = 0;
+    } else if (have_surv) {
+      head = nh;
+      hslot = nhs;
+    }
+  }
+  Lq->cnt = cnt;
+  Lq->cfin = cfin;
+  Lq->nrest = nr;
+  Lq->ig_base = ig_base;
+  Lq->ig_n = ng;
+  Lq->ig_all = ig_all ? 1u : 0u;
+  Lq->head = head;
+  Lq->tail = ttail;
+  Lq->hslot = hslot;
+  Lq->tslot = ttslot;
+  Lq->nlive0 = nv0 - consumed - ncan_old;
+  Lq->ocan = static_cast<uint32_t>(static_cast<uint64_t>(ocan) / g);
+  Lq->pad0 = static_cast<uint32_t>(static_cast<uint64_t>(qend));
+  Lq->pad1 = static_cast<uint32_t>(static_cast<uint64_t>(qend) >> 32);
+}
+
 constexpr uint32_t FC_LVB_T = FL_LVB_T, FC_K = 4;
 // a level of FC_BIG touches or more takes a whole block (fc_level_blk), smaller ones a wave
 constexpr uint32_t FC_BIG = 1024;
@@ -1446,13 +1598,19 @@ __global__ __launch_bounds__(FC_LVB_T) void k_fc_level_book(Dev D, FlowArgs F) {
   if (h >= fl_hend(D, F) || !fc_lane(F, h)) return;
   const uint32_t nl = F.hdr[h].nl;
   const FlowLvl* LV = fl_lvls(F, h);
+  for (uint32_t q = 1 + threadIdx.x; q <= nl; q += blockDim.x) {  // small levels: a lane each
+    const uint32_t cnt = LV[q].cnt;
+    if (cnt <= FC_LANE_MAX) fc_level_lane(D, F, h, q, cnt);
+  }
   for (uint32_t q = 1; q <= nl; ++q) {
     if (LV[q].cnt < FC_BIG) continue;
     fc_level_blk(D, F, h, q);
     __syncthreads();  // (fc_level_blk's shared words, before the next level's)
   }
-  for (uint32_t q = 1 + (threadIdx.x >> 6); q <= nl; q += blockDim.x / 64)
-    if (uni(LV[q].cnt) < FC_BIG) fc_level_one(D, F, h, uni(q));
+  for (uint32_t q = 1 + (threadIdx.x >> 6); q <= nl; q += blockDim.x / 64) {
+    const uint32_t cnt = uni(LV[q].cnt);
+    if (cnt > FC_LANE_MAX && cnt < FC_BIG) fc_level_one(D, F, h, uni(q));
+  }
 }
 
 // ---- fills of one consume touch ----------------------------------------------------------

@@ -558,7 +558,14 @@ __device__ __forceinline__ void k_deep_level_one(Dev D, FlowArgs F, uint32_t slo
   for (uint32_t i0 = blockIdx.x * 64u; i0 < nt; i0 += gridDim.x * 64u) {
     const uint32_t i = i0 + lane;
     const uint32_t lv = i < nt ? R[i].lvl : 0u;
-    const bool head = i < nt && (i == 0 || R[i - 1].lvl != lv);
+    bool head = i < nt && (i == 0 || R[i - 1].lvl != lv);
+    if (dc && head) {  // a level of few touches: its lane (fc_level_lane)
+      const uint32_t n = LV[lv].pad1 - LV[lv].base;
+      if (n <= FC_LANE_MAX) {
+        fc_level_lane(D, F, h, lv, n);
+        head = false;
+      }
+    }
     for (unsigned long long hm = __ballot(head); hm; hm &= hm - 1) {
       const uint32_t q = uni(rl(lv, static_cast<uint32_t>(__builtin_ctzll(hm))));
       const uint32_t e = uni(LV[q].pad1), b = uni(LV[q].base);  // (k_deep_runs)
@@ -645,10 +652,14 @@ __global__ __launch_bounds__(FC_LVB_T) void k_deep_level_hot(Dev D, FlowArgs F) 
     fc_level_blk(D, F, h, q);
     __syncthreads();  // (fc_level_blk's shared words, before the next level's)
   }
+  for (uint32_t q = 1 + blockIdx.x * blockDim.x + threadIdx.x; q <= nl; q += gridDim.x * blockDim.x) {
+    const uint32_t cnt = fd_run(LV, R, nt, q);  // (small levels: a lane each)
+    if (cnt != 0 && cnt <= FC_LANE_MAX) fc_level_lane(D, F, h, q, cnt);
+  }
   const uint32_t nw = blockDim.x >> 6, lane = lane_id();
   for (uint32_t q = 1 + blockIdx.x * nw + (threadIdx.x >> 6); q <= nl; q += gridDim.x * nw) {
     const uint32_t cnt = uni(fd_run(LV, R, nt, q));
-    if (cnt == 0 || cnt >= FC_BIG) continue;
+    if (cnt <= FC_LANE_MAX || cnt >= FC_BIG) continue;
     if (lane == 0) LV[q].cnt = cnt;
     __threadfence_block();  // (fc_level_one reads the count back)
     fc_level_one(D, F, h, q);

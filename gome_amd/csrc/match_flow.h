@@ -1875,6 +1875,154 @@ __device__ __forceinline__ void fl_level_one(const Dev& D, const FlowArgs& F, ui
   }
 }
 
+// fl_level_one (its fused path: no pre-scan, contexts made here) by ONE lane, for a level of at
+// most FL_LANE_MAX touches, with the same outputs: the level's consumption, the old FIFO's gather
+// (a chunk's slots in order), the new makers, then each CONS touch's makers (fl_find_all over the
+// gathered and the new makers, as fl_wave_find).  Deep books hold thousands of touched levels of a
+// few touches each per batch, which one wave took one after another (k_deep_level).
+constexpr uint32_t FL_LANE_MAX = 16;
+__device__ __forceinline__ uint32_t fl_find_all(const IgEnt* IG, uint32_t ig_n, const RsEnt* RS, uint32_t nrest, int64_t x) {
+  uint32_t lo = 0, hi = ig_n + nrest;  // the last maker whose start <= x (starts ascend, IG then RS)
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if ((mid < ig_n ? IG[mid].e : RS[mid - ig_n].e) <= x) lo = mid; else hi = mid;
+  }
+  return lo;
+}
+// ig_pre / stg: as fl_level_one's (the gather's claimed space, the workgroup's freed-chunk stage).
+__device__ __forceinline__ void fl_level_lane(const Dev& D, const FlowArgs& F, uint32_t h, uint32_t q, uint32_t base,
+                                              uint32_t cnt, uint32_t ig_pre = NIL, FlFreed* stg = nullptr) {
+  const FlowHdr* hd = &F.hdr[h];
+  FlowLvl* Lq = fl_lvls(F, h) + q;
+  const uint32_t L = FL_TOUCH_MUL * hd->beg;
+  const int64_t d0 = Lq->d0;
+  const SEnt* R = F.srt + L + base;
+  RsEnt* RS = F.rs + L + base;
+  const bool zl = Lq->z0 || hd->nzero;
+  int64_t cfin = 0;
+  for (uint32_t i = 0; i < cnt; ++i)
+    if (R[i].kind == TK_CONS) cfin += R[i].amt;
+  uint32_t nv0 = Lq->nv0, head = Lq->head, tail = Lq->tail;
+  uint32_t hslot = Lq->hslot, tslot = Lq->tslot;
+  uint32_t ig_base = 0, ng = 0, consumed = 0, zpopped = 0;
+  bool have_extra = false;
+  if (nv0 > 0 && cfin > 0) {
+    ig_base = ig_pre != NIL ? ig_pre : atomicAdd(F.ig_bump, nv0);
+    if (static_cast<unsigned long long>(ig_base) + nv0 > F.ig_cap) {
+      atomicOr(&D.st->err, ERR_CHUNKS);
+      return;
+    }
+    IgEnt* IG = F.ig + ig_base;
+    int64_t E = 0;
+    bool have_surv = false;
+    uint32_t c = head, s0 = hslot, nh = NIL, nhs = 0;
+    for (uint32_t guard = 0; c != NIL && !have_extra; ++guard) {
+      if (guard > D.ch_cap) { atomicOr(&D.st->err, ERR_CORRUPT); return; }
+      const uint32_t lim = (c == tail) ? tslot : CH;
+      const uint32_t nxt = (c == tail) ? NIL : D.chdr[c].next;
+      Node nd[CH];
+#pragma unroll
+      for (uint32_t s = 0; s < CH; ++s) {
+        nd[s] = Node{};
+        if (s >= s0 && s < lim) nd[s] = D.nodes[c * CH + s];
+      }
+      bool surv_here = false;
+#pragma unroll
+      for (uint32_t s = 0; s < CH; ++s) {
+        if (!(s >= s0 && s < lim && nd[s].rem >= 0)) continue;  // (live makers only)
+        const int64_t em = E;
+        E += nd[s].rem;
+        if (!have_extra) {  // every maker before the consumption end, then the first at or past it
+          IgEnt g;
+          g.e = em;
+          g.v = nd[s].rem;
+          g.oid = nd[s].oid;
+          g.uuid = nd[s].uuid;
+          g.tx = nd[s].tx;
+          g.pad = 0;
+          IG[ng++] = g;
+          if (em >= cfin) have_extra = true;
+        }
+        const bool cons = em + nd[s].rem <= cfin && (nd[s].rem > 0 || em < cfin);
+        if (cons) {
+          __hip_atomic_store(&D.idx[nd[s].ixs].key, KEY_TOMB, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          consumed++;
+          if (nd[s].rem == 0) zpopped++;
+        }
+        if (!have_surv && !surv_here && !cons) {
+          surv_here = true;
+          nh = c;
+          nhs = s;
+          if (em < cfin) D.nodes[c * CH + s].rem = em + nd[s].rem - cfin;  // partial head
+        }
+      }
+      if (!have_surv) {
+        if (surv_here) {
+          have_surv = true;
+        } else {  // a fully consumed chunk
+          const uint32_t k = stg ? atomicAdd(&stg->n, 1u) : FL_FREED_LDS;
+          if (k < FL_FREED_LDS) stg->ids[k] = c;
+          else D.freed_ids[atomicAdd(&D.st->freed_top, 1u)] = c;
+        }
+      }
+      c = nxt;
+      s0 = 0;
+    }
+    if (!have_surv) {
+      head = tail = NIL;
+      hslot = tslot = 0;
+    } else {
+      head = nh;
+      hslot = nhs;
+    }
+  }
+  // the new makers, then each CONS touch's makers (every new maker of the level written first, as
+  // fl_level_one's 64-touch chunk)
+  int64_t rr = d0;
+  uint32_t nr = 0;
+  for (uint32_t i = 0; i < cnt; ++i) {
+    const SEnt e = R[i];
+    if (e.kind != TK_REST) continue;
+    RsEnt x;
+    x.e = rr;
+    x.v = e.amt;
+    x.j = e.j;
+    x.t = e.t;
+    x.pad0 = x.pad1 = 0;
+    RS[nr++] = x;
+    rr += e.amt;
+  }
+  const IgEnt* IG = F.ig + ig_base;
+  int64_t c1 = 0;
+  for (uint32_t i = 0; i < cnt; ++i) {
+    const SEnt e = R[i];
+    if (e.kind != TK_CONS) continue;
+    const int64_t c = c1, x = c + (e.amt ? e.amt : 1) - 1;
+    const uint32_t f0 = fl_find_all(IG, ng, RS, nr, c);
+    const uint32_t l = fl_find_all(IG, ng, RS, nr, x);
+    FlTouchFc y;
+    y.first = zl && e.amt ? fl_first_back(IG, ng, RS, f0, c) : f0;
+    y.last = l;
+    y.lvl = q;
+    y.pad = 0;
+    y.coord = c;
+    F.tfc[L + e.t] = y;
+    c1 += e.amt;
+  }
+  Lq->cfin = cfin;
+  Lq->nrest = nr;
+  Lq->ig_base = ig_base;
+  Lq->ig_n = ng;
+  Lq->ig_all = have_extra ? 0u : 1u;
+  Lq->head = head;
+  Lq->tail = tail;
+  Lq->hslot = hslot;
+  Lq->tslot = tslot;
+  Lq->nlive0 = nv0 - consumed;
+  Lq->zpop = zpopped;
+  Lq->cnt = cnt;
+}
+
 constexpr uint32_t FL_LEVEL_T = 1024;
 // Tail books: one workgroup per book, its waves take the levels in turn.  The book's gathered-
 // maker space is claimed once (every touched level with old makers: a superset of the levels
@@ -1909,8 +2057,12 @@ __global__ __launch_bounds__(FL_LEVEL_T) void k_flow_level(Dev D, FlowArgs F) {
     if (tid == 0) stg.n = 0;
   }
   __syncthreads();
+  for (uint32_t q = 1 + tid; q <= nl; q += FL_LEVEL_T) {  // levels of few touches: a lane each
+    const uint32_t cnt = LV[q].cnt;
+    if (cnt <= FL_LANE_MAX) fl_level_lane(D, F, h, q, LV[q].base, cnt, igo[q], &stg);
+  }
   for (uint32_t q = 1 + (tid >> 6); q <= nl; q += FL_LEVEL_T / 64)
-    fl_level_one(D, F, h, uni(q), NIL, 0, igo[q], -1, 0, true, &stg);
+    if (uni(LV[q].cnt) > FL_LANE_MAX) fl_level_one(D, F, h, uni(q), NIL, 0, igo[q], -1, 0, true, &stg);
   __syncthreads();
   fl_freed_flush(D, &stg);
 }

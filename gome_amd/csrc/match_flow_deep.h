@@ -172,6 +172,82 @@ __global__ __launch_bounds__(FL_PREP_T) void k_deep_prep_a(Dev D, BatchArgs B, F
 
 // ---- prep b: old levels into the set, the sorted level table, the header -----------------
 // Dynamic LDS: DEEP_CAP keys (the sort).
+// Ranks of a deep book's price set (keys in its DEEP_HASH slots, n of them) by a bitmap over the
+// grid the keys lie on, calling put(rank, key, slot) for each; false (nothing done) when the
+// offsets from the lowest key over their gcd span more than FD_RANK_BITS.  The whole block; the
+// bitmap and its word prefix in the dynamic LDS (fl_ring).
+constexpr uint32_t FD_RANK_BITS = 1u << 17, FD_RANK_WORDS = FD_RANK_BITS / 32;
+template <class Put>
+__device__ __forceinline__ bool fd_rank_grid(const unsigned long long* keys, const uint32_t* vals, uint32_t n, Put put) {
+  __shared__ unsigned long long kmin_s, kmax_s, g_s[FL_PREP_T / 64];
+  __shared__ uint32_t cnt_s, part_s[FL_PREP_T / 64];
+  const uint32_t tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
+  if (tid == 0) { kmin_s = ~0ull; kmax_s = 0; cnt_s = 0; }
+  __syncthreads();
+  unsigned long long mn = ~0ull, mx = 0;
+  for (uint32_t sl = tid; sl < DEEP_HASH; sl += FL_PREP_T) {
+    const unsigned long long k = keys[sl];
+    if (k) { mn = min(mn, k); mx = max(mx, k); }
+  }
+  atomicMin(&kmin_s, mn);
+  atomicMax(&kmax_s, mx);
+  __syncthreads();
+  const unsigned long long kmin = kmin_s, kmax = kmax_s;
+  unsigned long long g = 0;
+  for (uint32_t sl = tid; sl < DEEP_HASH; sl += FL_PREP_T) {
+    const unsigned long long k = keys[sl];
+    if (k) g = fl_gcd(g, k - kmin);
+  }
+  for (int off = 32; off > 0; off >>= 1) g = fl_gcd(g, __shfl_xor(g, off));
+  if (lane == 0) g_s[w] = g;
+  __syncthreads();
+  g = 0;
+  for (uint32_t k = 0; k < FL_PREP_T / 64; ++k) g = fl_gcd(g, g_s[k]);
+  if (!g) g = 1;  // (one key)
+  if (n == 0 || kmax < kmin || (kmax - kmin) / g >= FD_RANK_BITS) return false;  // (uniform)
+  uint32_t* bm = reinterpret_cast<uint32_t*>(fl_ring);
+  uint32_t* pre = bm + FD_RANK_WORDS;
+  for (uint32_t i = tid; i < FD_RANK_WORDS; i += FL_PREP_T) bm[i] = 0;
+  __syncthreads();
+  for (uint32_t sl = tid; sl < DEEP_HASH; sl += FL_PREP_T) {
+    const unsigned long long k = keys[sl];
+    if (k) {
+      const uint32_t x = static_cast<uint32_t>((k - kmin) / g);
+      atomicOr(&bm[x >> 5], 1u << (x & 31));
+    }
+  }
+  __syncthreads();
+  // exclusive prefix of the words' popcounts: FD_RANK_WORDS / FL_PREP_T consecutive words a thread
+  constexpr uint32_t PW = FD_RANK_WORDS / FL_PREP_T;
+  static_assert(FD_RANK_WORDS % FL_PREP_T == 0, "whole words per thread");
+  uint32_t loc[PW], s = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < PW; ++k) {
+    loc[k] = s;
+    s += __popc(bm[tid * PW + k]);
+  }
+  const uint32_t inc = wave_incl_scan_u32(s);
+  if (lane == 63) part_s[w] = inc;
+  __syncthreads();
+  uint32_t before = 0, tot = 0;
+  for (uint32_t k = 0; k < FL_PREP_T / 64; ++k) {
+    before += k < w ? part_s[k] : 0u;
+    tot += part_s[k];
+  }
+  const uint32_t ex = before + inc - s;
+#pragma unroll
+  for (uint32_t k = 0; k < PW; ++k) pre[tid * PW + k] = ex + loc[k];
+  __syncthreads();
+  if (tot != n) return false;  // (uniform: every key set its own bit)
+  for (uint32_t sl = tid; sl < DEEP_HASH; sl += FL_PREP_T) {
+    const unsigned long long k = keys[sl];
+    if (!k) continue;
+    const uint32_t x = static_cast<uint32_t>((k - kmin) / g);
+    put(pre[x >> 5] + __popc(bm[x >> 5] & ((1u << (x & 31)) - 1u)), k, sl);
+  }
+  return true;
+}
+
 __device__ __forceinline__ void k_deep_prep_b_one(Dev D, BatchArgs B, FlowArgs F, uint32_t slot_i) {
   __shared__ uint32_t bad, ndist, nc;
   __shared__ unsigned long long wg[FL_PREP_T / 64], ws[FL_PREP_T / 64];
@@ -233,8 +309,36 @@ __device__ __forceinline__ void k_deep_prep_b_one(Dev D, BatchArgs B, FlowArgs F
     fd_clear(F, ds);
     return;
   }
-  // the set's keys, sorted (bitonic over the next power of two)
   const uint32_t n = ndist;
+  FlowLvl* LV = F.dlvl + static_cast<size_t>(ds) * DEEP_CAP;
+  auto put_level = [&](uint32_t r, unsigned long long key, uint32_t sl) {  // level r + 1 = the r-th price
+    const uint32_t old = vals[sl];
+    FlowLvl f{};
+    f.price = static_cast<int64_t>(key - FL_KEY_OFF);
+    f.old = old;
+    f.head = f.tail = NIL;
+    f.ig_all = 1;  // (what k_deep_level leaves on a level the batch does not touch: it skips them)
+    if (old != NIL) {
+      const Level x = L0[old];
+      f.d0 = x.depth;
+      f.nv0 = x.nlive;
+      f.head = x.head;
+      f.tail = x.tail;
+      f.hslot = x.hslot;
+      f.tslot = x.tslot;
+      f.mem0 = x.member;
+      f.nlive0 = x.nlive;
+    }
+    LV[r + 1] = f;
+    vals[sl] = r + 1;  // (the set maps price -> level from here on)
+  };
+  // The keys' ranks.  Prices on a grid (a book's prices are multiples of its tick): the offsets
+  // from the lowest key over their gcd index a bitmap of FD_RANK_BITS in LDS, and a key's rank is
+  // the bits below its own (popcounts and a scan of the words); a bitonic sort of up to DEEP_CAP
+  // keys in LDS took ~250 us of the hottest book's prep (config 5c).  Other sets: the sort.
+  if (fd_rank_grid(keys, vals, n, put_level)) goto fd_prep_b_hdr;
+  {
+  // the set's keys, sorted (bitonic over the next power of two)
   uint32_t np = 1024;
   while (np < n) np <<= 1;
   unsigned long long* sk = reinterpret_cast<unsigned long long*>(fl_ring);
@@ -260,31 +364,12 @@ __device__ __forceinline__ void k_deep_prep_b_one(Dev D, BatchArgs B, FlowArgs F
       __syncthreads();
     }
   }
-  // level r + 1 = the r-th price; the set maps price -> level from here on
-  FlowLvl* LV = F.dlvl + static_cast<size_t>(ds) * DEEP_CAP;
   for (uint32_t r = tid; r < n; r += FL_PREP_T) {
     const unsigned long long key = sk[r];
-    const uint32_t sl = fd_find(keys, key);
-    const uint32_t old = vals[sl];
-    FlowLvl f{};
-    f.price = static_cast<int64_t>(key - FL_KEY_OFF);
-    f.old = old;
-    f.head = f.tail = NIL;
-    f.ig_all = 1;  // (what k_deep_level leaves on a level the batch does not touch: it skips them)
-    if (old != NIL) {
-      const Level x = L0[old];
-      f.d0 = x.depth;
-      f.nv0 = x.nlive;
-      f.head = x.head;
-      f.tail = x.tail;
-      f.hslot = x.hslot;
-      f.tslot = x.tslot;
-      f.mem0 = x.member;
-      f.nlive0 = x.nlive;
-    }
-    LV[r + 1] = f;
-    vals[sl] = r + 1;
+    put_level(r, key, fd_find(keys, key));
   }
+  }
+fd_prep_b_hdr:
   const uint32_t obase = fl_obase(beg, seg);
   if (tid < ((8u - ((end - beg) & 7u)) & 7u)) F.ord8[obase + (end - beg) + tid] = 0ull;  // no-op padding
   if (tid == 0) {
@@ -559,10 +644,13 @@ __device__ __forceinline__ void k_deep_level_one(Dev D, FlowArgs F, uint32_t slo
     const uint32_t i = i0 + lane;
     const uint32_t lv = i < nt ? R[i].lvl : 0u;
     bool head = i < nt && (i == 0 || R[i - 1].lvl != lv);
-    if (dc && head) {  // a level of few touches: its lane (fc_level_lane)
-      const uint32_t n = LV[lv].pad1 - LV[lv].base;
-      if (n <= FC_LANE_MAX) {
+    if (head) {  // a level of few touches: its lane (fc_level_lane, fl_level_lane)
+      const uint32_t b = LV[lv].base, n = LV[lv].pad1 - b;
+      if (dc && n <= FC_LANE_MAX) {
         fc_level_lane(D, F, h, lv, n);
+        head = false;
+      } else if (!dc && n <= FL_LANE_MAX) {
+        fl_level_lane(D, F, h, lv, b, n);
         head = false;
       }
     }
@@ -953,39 +1041,54 @@ __device__ __forceinline__ void fd_crank_level(const BatchArgs& B, const FlowArg
 constexpr uint32_t FC_CRANK_BIG = 2048;
 __device__ __forceinline__ void fd_crank_level_blk(const BatchArgs& B, const FlowArgs& F, const FlowHdr& hd,
                                                    FlowLvl* LV, const SEnt* R, uint32_t q, uint32_t b, uint32_t e) {
+  // FD_CK consecutive keys per thread: their three dependent loads (key, record, target link) in
+  // flight together, a quarter of the block scans
+  constexpr uint32_t FD_CK = 4;
   int64_t vv = 0, tc = LV[q].c_old;
-  for (uint32_t c0 = b; c0 < e; c0 += blockDim.x) {
-    const uint32_t i = c0 + threadIdx.x;
-    const bool valid = i < e;
-    const uint32_t j = valid ? R[i].j : 0u, bs = hd.beg + j;
-    bool isadd = false, targ = false, isdel = false, sale = false;
-    uint32_t v = 0;
-    if (valid) {
-      const unsigned long long r = F.ord8[hd.obase + j];
-      if (r) {
-        isadd = true;
-        v = static_cast<uint32_t>(r);
-        sale = (r >> 63) != 0;
-        targ = F.fc_tg[bs] != 0;
-      } else {
-        isdel = true;
-        sale = prep_at(B, bs).side == GOME_SALE;
+  for (uint32_t c0 = b; c0 < e; c0 += blockDim.x * FD_CK) {
+    const uint32_t i0 = c0 + threadIdx.x * FD_CK;
+    uint32_t j[FD_CK], tg[FD_CK], v[FD_CK];
+    unsigned long long r[FD_CK];
+    bool sale[FD_CK];
+#pragma unroll
+    for (uint32_t u = 0; u < FD_CK; ++u) j[u] = i0 + u < e ? R[i0 + u].j : 0u;
+#pragma unroll
+    for (uint32_t u = 0; u < FD_CK; ++u) r[u] = i0 + u < e ? F.ord8[hd.obase + j[u]] : 0ull;
+    int64_t sv = 0, st = 0;
+#pragma unroll
+    for (uint32_t u = 0; u < FD_CK; ++u) {
+      const uint32_t bs = hd.beg + j[u];
+      tg[u] = 0;
+      v[u] = static_cast<uint32_t>(r[u]);
+      sale[u] = (r[u] >> 63) != 0;
+      if (i0 + u < e) {
+        if (r[u]) tg[u] = F.fc_tg[bs];
+        else sale[u] = prep_at(B, bs).side == GOME_SALE;  // (a DEL with a target: the only other keys)
       }
+      sv += r[u] ? (sale[u] ? static_cast<int64_t>(v[u]) << 32 : static_cast<int64_t>(v[u])) : 0;
+      st += tg[u] ? 1 : 0;
     }
-    const int64_t pv = isadd ? (sale ? static_cast<int64_t>(v) << 32 : static_cast<int64_t>(v)) : 0;
     int64_t tv, tt;
-    const int64_t xv = vv + fl_blk_excl(pv, &tv), xt = tc + fl_blk_excl(targ ? 1 : 0, &tt);
-    const uint32_t before_t = static_cast<uint32_t>(xt);
-    const uint32_t before_v = static_cast<uint32_t>(sale ? static_cast<uint64_t>(xv) >> 32 : static_cast<uint64_t>(xv));
-    if (targ) {
-      FcDel* d = &F.fc_del[F.fc_tg[bs] - 1u];
-      d->oend = before_v + v;
-      d->ov = v;
-      F.fc_rank[bs] = before_t;
-    }
-    if (isdel) {
-      F.fc_del[bs].nb = before_t;
-      F.fc_del[bs].va = before_v;
+    int64_t xv = vv + fl_blk_excl(sv, &tv), xt = tc + fl_blk_excl(st, &tt);
+#pragma unroll
+    for (uint32_t u = 0; u < FD_CK; ++u) {
+      if (i0 + u >= e) continue;
+      const uint32_t bs = hd.beg + j[u];
+      const uint32_t before_t = static_cast<uint32_t>(xt);
+      const uint32_t before_v = static_cast<uint32_t>(sale[u] ? static_cast<uint64_t>(xv) >> 32 : static_cast<uint64_t>(xv));
+      if (tg[u]) {
+        FcDel* d = &F.fc_del[tg[u] - 1u];
+        d->oend = before_v + v[u];
+        d->ov = v[u];
+        F.fc_rank[bs] = before_t;
+        xt += 1;
+      }
+      if (r[u]) {
+        xv += sale[u] ? static_cast<int64_t>(v[u]) << 32 : static_cast<int64_t>(v[u]);
+      } else {
+        F.fc_del[bs].nb = before_t;
+        F.fc_del[bs].va = before_v;
+      }
     }
     vv += tv;
     tc += tt;

@@ -2057,12 +2057,10 @@ __global__ __launch_bounds__(FL_LEVEL_T) void k_flow_level(Dev D, FlowArgs F) {
     if (tid == 0) stg.n = 0;
   }
   __syncthreads();
-  for (uint32_t q = 1 + tid; q <= nl; q += FL_LEVEL_T) {  // levels of few touches: a lane each
-    const uint32_t cnt = LV[q].cnt;
-    if (cnt <= FL_LANE_MAX) fl_level_lane(D, F, h, q, LV[q].base, cnt, igo[q], &stg);
-  }
+  // (the lane pass, fl_level_lane, measured 1.5% slower on config 2 here: its tail books' levels
+  // hold tens of touches, r05ba)
   for (uint32_t q = 1 + (tid >> 6); q <= nl; q += FL_LEVEL_T / 64)
-    if (uni(LV[q].cnt) > FL_LANE_MAX) fl_level_one(D, F, h, uni(q), NIL, 0, igo[q], -1, 0, true, &stg);
+    fl_level_one(D, F, h, uni(q), NIL, 0, igo[q], -1, 0, true, &stg);
   __syncthreads();
   fl_freed_flush(D, &stg);
 }

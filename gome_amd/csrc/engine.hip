@@ -126,7 +126,9 @@ __global__ void k_ctr_fold(Dev D) {
     printf("PROBE levels %llu t12 %llu t3 %llu walk %llu max %llu cnt %llu slow %llu maxcnt %llu | waves %llu wsum %llu wmax %llu w>10us %llu span %llu\n",
            g_probe[2], g_probe[0], g_probe[1], g_probe[3], g_probe[4], g_probe[5], g_probe[6], g_probe[7], g_probe[8],
            g_probe[9], g_probe[10], g_probe[11], g_probe[13] - g_probe[12]);
-    for (int k = 0; k < 16; ++k) g_probe[k] = 0;
+    printf("PROBE prep_b old %llu gcd %llu rank %llu hdr %llu | rank: minmax %llu gcd %llu bits %llu scan %llu put %llu\n",
+           g_probe[16], g_probe[17], g_probe[18], g_probe[19], g_probe[20], g_probe[21], g_probe[22], g_probe[23], g_probe[24]);
+    for (int k = 0; k < 32; ++k) g_probe[k] = 0;
     g_probe[12] = ~0ull;
   }
 #endif
@@ -1148,6 +1150,7 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
     const uint32_t ns = std::min<uint32_t>(R.ds1 - R.ds0, DEEP_GRID_T);  // (blocks walk the slots)
     k_deep_prep_a<<<dim3(px, ns), FL_PREP_T, 0, st>>>(D, B, R);
     k_deep_prep_b<<<ns, FL_PREP_T, DEEP_CAP * 8, st>>>(D, B, R);
+    k_deep_prep_put<<<dim3(px, ns), FL_PREP_T, 0, st>>>(D, R);
     k_deep_prep_c<<<dim3(px, ns), FL_PREP_T, 0, st>>>(D, B, R);
   };
   if (c_deep) deep_prep(FH, FL_PG, flow_stream);

@@ -552,6 +552,7 @@ struct FlPrepScr {
   // (k_deep_claim; see FlClaim)
   int32_t c_t;
   uint32_t c_nst, c_bb, c_ok;
+  uint32_t d_put;      // k_deep_prep_b ranked the set by its grid: k_deep_prep_put fills the level table
 };
 
 // A book's chunk ids for all its levels' FIFO appends, claimed at once: id j = j < c_nst ?

@@ -1011,7 +1011,10 @@ __device__ __forceinline__ uint32_t fc_find(const FcLvlView& V, int64_t x) {
 
 #ifdef GOME_PROBE_LEVEL
 // (tuning builds: the level passes' time split, summed over a batch; k_ctr_fold prints and clears)
-__device__ unsigned long long g_probe[16];
+__device__ unsigned long long g_probe[32];
+#define GOME_PROBE_T(k, t0) do { if (threadIdx.x == 0) atomicAdd(&g_probe[k], wall_clock64() - (t0)); } while (0)
+#else
+#define GOME_PROBE_T(k, t0) do { } while (0)
 #endif
 
 // ---- k_fc_level: one wave per (book, level) ----------------------------------------------

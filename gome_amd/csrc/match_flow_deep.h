@@ -173,16 +173,34 @@ __global__ __launch_bounds__(FL_PREP_T) void k_deep_prep_a(Dev D, BatchArgs B, F
 // ---- prep b: old levels into the set, the sorted level table, the header -----------------
 // Dynamic LDS: DEEP_CAP keys (the sort).
 // Ranks of a deep book's price set (keys in its DEEP_HASH slots, n of them) by a bitmap over the
-// grid the keys lie on, calling put(rank, key, slot) for each; false (nothing done) when the
-// offsets from the lowest key over their gcd span more than FD_RANK_BITS.  The whole block; the
-// bitmap and its word prefix in the dynamic LDS (fl_ring).
+// grid the keys lie on: slot[r] = the hash slot of the r-th key (LDS).  False (nothing done) when
+// the keys span 2^32 or more, or their offsets from the lowest key over their gcd more than
+// FD_RANK_BITS.  The whole block; the bitmap, its word prefix and slot[] in the dynamic LDS.
 constexpr uint32_t FD_RANK_BITS = 1u << 17, FD_RANK_WORDS = FD_RANK_BITS / 32;
-template <class Put>
-__device__ __forceinline__ bool fd_rank_grid(const unsigned long long* keys, const uint32_t* vals, uint32_t n, Put put) {
-  __shared__ unsigned long long kmin_s, kmax_s, g_s[FL_PREP_T / 64];
-  __shared__ uint32_t cnt_s, part_s[FL_PREP_T / 64];
+__device__ __forceinline__ uint32_t fd_gcd32(uint32_t a, uint32_t b) {  // (binary: no divisions)
+  if (!a) return b;
+  if (!b) return a;
+  const int sh = __builtin_ctz(a | b);
+  a >>= __builtin_ctz(a);
+  do {
+    b >>= __builtin_ctz(b);
+    if (a > b) { const uint32_t t = a; a = b; b = t; }
+    b -= a;
+  } while (b);
+  return a << sh;
+}
+__device__ __forceinline__ bool fd_rank_grid(const unsigned long long* keys, uint32_t n, uint32_t** slot_out) {
+  __shared__ unsigned long long kmin_s, kmax_s;
+  __shared__ uint32_t g_s[FL_PREP_T / 64], part_s[FL_PREP_T / 64];
   const uint32_t tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
-  if (tid == 0) { kmin_s = ~0ull; kmax_s = 0; cnt_s = 0; }
+#ifdef GOME_PROBE_LEVEL
+  const bool pr = blockIdx.x == 0 && n > 4096;
+  uint64_t pt = wall_clock64();
+#define PR(k) do { if (pr) { GOME_PROBE_T(k, pt); pt = wall_clock64(); } } while (0)
+#else
+#define PR(k) do { } while (0)
+#endif
+  if (tid == 0) { kmin_s = ~0ull; kmax_s = 0; }
   __syncthreads();
   unsigned long long mn = ~0ull, mx = 0;
   for (uint32_t sl = tid; sl < DEEP_HASH; sl += FL_PREP_T) {
@@ -192,34 +210,40 @@ __device__ __forceinline__ bool fd_rank_grid(const unsigned long long* keys, con
   atomicMin(&kmin_s, mn);
   atomicMax(&kmax_s, mx);
   __syncthreads();
+  PR(20);
   const unsigned long long kmin = kmin_s, kmax = kmax_s;
-  unsigned long long g = 0;
+  if (n == 0 || kmax < kmin || kmax - kmin >= (1ull << 32)) return false;  // (uniform)
+  uint32_t g = 0;
   for (uint32_t sl = tid; sl < DEEP_HASH; sl += FL_PREP_T) {
     const unsigned long long k = keys[sl];
-    if (k) g = fl_gcd(g, k - kmin);
+    if (k) g = fd_gcd32(g, static_cast<uint32_t>(k - kmin));
   }
-  for (int off = 32; off > 0; off >>= 1) g = fl_gcd(g, __shfl_xor(g, off));
+  for (int off = 32; off > 0; off >>= 1) g = fd_gcd32(g, __shfl_xor(g, off));
   if (lane == 0) g_s[w] = g;
   __syncthreads();
   g = 0;
-  for (uint32_t k = 0; k < FL_PREP_T / 64; ++k) g = fl_gcd(g, g_s[k]);
+  for (uint32_t k = 0; k < FL_PREP_T / 64; ++k) g = fd_gcd32(g, g_s[k]);
   if (!g) g = 1;  // (one key)
-  if (n == 0 || kmax < kmin || (kmax - kmin) / g >= FD_RANK_BITS) return false;  // (uniform)
+  PR(21);
+  if (static_cast<uint32_t>(kmax - kmin) / g >= FD_RANK_BITS) return false;
   uint32_t* bm = reinterpret_cast<uint32_t*>(fl_ring);
   uint32_t* pre = bm + FD_RANK_WORDS;
+  uint32_t* slot = pre + FD_RANK_WORDS;  // [DEEP_CAP]
   for (uint32_t i = tid; i < FD_RANK_WORDS; i += FL_PREP_T) bm[i] = 0;
   __syncthreads();
   for (uint32_t sl = tid; sl < DEEP_HASH; sl += FL_PREP_T) {
     const unsigned long long k = keys[sl];
     if (k) {
-      const uint32_t x = static_cast<uint32_t>((k - kmin) / g);
+      const uint32_t x = static_cast<uint32_t>(k - kmin) / g;
       atomicOr(&bm[x >> 5], 1u << (x & 31));
     }
   }
   __syncthreads();
+  PR(22);
   // exclusive prefix of the words' popcounts: FD_RANK_WORDS / FL_PREP_T consecutive words a thread
   constexpr uint32_t PW = FD_RANK_WORDS / FL_PREP_T;
   static_assert(FD_RANK_WORDS % FL_PREP_T == 0, "whole words per thread");
+  static_assert(2 * FD_RANK_WORDS * 4 + DEEP_CAP * 4 <= DEEP_CAP * 8, "bitmap, prefix and slots in the sort's LDS");
   uint32_t loc[PW], s = 0;
 #pragma unroll
   for (uint32_t k = 0; k < PW; ++k) {
@@ -238,13 +262,18 @@ __device__ __forceinline__ bool fd_rank_grid(const unsigned long long* keys, con
 #pragma unroll
   for (uint32_t k = 0; k < PW; ++k) pre[tid * PW + k] = ex + loc[k];
   __syncthreads();
-  if (tot != n) return false;  // (uniform: every key set its own bit)
+  PR(23);
+  if (tot != n || n > DEEP_CAP) return false;  // (uniform: every key set its own bit)
   for (uint32_t sl = tid; sl < DEEP_HASH; sl += FL_PREP_T) {
     const unsigned long long k = keys[sl];
     if (!k) continue;
-    const uint32_t x = static_cast<uint32_t>((k - kmin) / g);
-    put(pre[x >> 5] + __popc(bm[x >> 5] & ((1u << (x & 31)) - 1u)), k, sl);
+    const uint32_t x = static_cast<uint32_t>(k - kmin) / g;
+    slot[pre[x >> 5] + __popc(bm[x >> 5] & ((1u << (x & 31)) - 1u))] = sl;
   }
+  __syncthreads();
+  PR(24);
+#undef PR
+  *slot_out = slot;
   return true;
 }
 
@@ -280,6 +309,13 @@ __device__ __forceinline__ void k_deep_prep_b_one(Dev D, BatchArgs B, FlowArgs F
     return;
   }
   const Level* L0 = D.lvl + bk.lvl_base;
+#ifdef GOME_PROBE_LEVEL
+  const bool pr = slot_i == 0;
+  uint64_t pt = wall_clock64();
+#define PB(k) do { if (pr) { GOME_PROBE_T(k, pt); pt = wall_clock64(); } } while (0)
+#else
+#define PB(k) do { } while (0)
+#endif
   unsigned long long mg = 0, msum = 0;
   if (tid < FL_PG) {
     mg = P->pg[tid];
@@ -301,7 +337,10 @@ __device__ __forceinline__ void k_deep_prep_b_one(Dev D, BatchArgs B, FlowArgs F
     vals[sl] = k;  // the old level (vals start NIL)
     if (fresh) atomicAdd(&ndist, 1u);
   }
+  __syncthreads();
+  PB(16);
   fl_block_gcd_sum(mg, msum, wg, ws);  // (synchronises the block)
+  PB(17);
   const unsigned long long g = mg ? mg : 1;
   const bool w32 = msum < FL_SUM_CAP && msum / g < (1ull << 32);
   if (bad || ndist > DEEP_CAP - 2 || !w32) {
@@ -336,7 +375,16 @@ __device__ __forceinline__ void k_deep_prep_b_one(Dev D, BatchArgs B, FlowArgs F
   // from the lowest key over their gcd index a bitmap of FD_RANK_BITS in LDS, and a key's rank is
   // the bits below its own (popcounts and a scan of the words); a bitonic sort of up to DEEP_CAP
   // keys in LDS took ~250 us of the hottest book's prep (config 5c).  Other sets: the sort.
-  if (fd_rank_grid(keys, vals, n, put_level)) goto fd_prep_b_hdr;
+  uint32_t* slot = nullptr;
+  if (fd_rank_grid(keys, n, &slot)) {
+    // each rank's hash slot into its level row; k_deep_prep_put fills the rows, many blocks a book
+    // (one block took ~0.2 ms of the hottest book's prep here, three dependent loads per level)
+    for (uint32_t r = tid; r < n; r += FL_PREP_T) LV[r + 1].pad4 = slot[r];
+    if (tid == 0) P->d_put = 1;
+    __syncthreads();
+    PB(18);
+    goto fd_prep_b_hdr;
+  }
   {
   // the set's keys, sorted (bitonic over the next power of two)
   uint32_t np = 1024;
@@ -371,6 +419,7 @@ __device__ __forceinline__ void k_deep_prep_b_one(Dev D, BatchArgs B, FlowArgs F
   }
 fd_prep_b_hdr:
   const uint32_t obase = fl_obase(beg, seg);
+#undef PB
   if (tid < ((8u - ((end - beg) & 7u)) & 7u)) F.ord8[obase + (end - beg) + tid] = 0ull;  // no-op padding
   if (tid == 0) {
     FlowHdr x{};
@@ -393,6 +442,47 @@ fd_prep_b_hdr:
     *hd = x;
   }
 }
+// The level table of a set k_deep_prep_b ranked by its grid: row r + 1 from the r-th key's hash
+// slot (FlowLvl::pad4): its price, its old level's FIFO and depth; the set maps price -> level.
+__device__ __forceinline__ void k_deep_prep_put_one(Dev D, FlowArgs F, uint32_t slot_i) {
+  const uint32_t h = fd_book(D, F, slot_i);
+  if (!fd_deep(F, h)) return;
+  const FlowHdr& hd = F.hdr[h];
+  const uint32_t ds = hd.dslot;
+  if (!F.dscr[ds].d_put) return;
+  const unsigned long long* keys = F.dh_key + static_cast<size_t>(ds) * DEEP_HASH;
+  uint32_t* vals = F.dh_val + static_cast<size_t>(ds) * DEEP_HASH;
+  FlowLvl* LV = F.dlvl + static_cast<size_t>(ds) * DEEP_CAP;
+  const Level* L0 = D.lvl + D.books[hd.sym].lvl_base;
+  const uint32_t n = hd.nl;
+  for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r < n; r += gridDim.x * blockDim.x) {
+    const uint32_t sl = LV[r + 1].pad4;
+    const unsigned long long key = keys[sl];
+    const uint32_t old = vals[sl];
+    FlowLvl f{};
+    f.price = static_cast<int64_t>(key - FL_KEY_OFF);
+    f.old = old;
+    f.head = f.tail = NIL;
+    f.ig_all = 1;  // (what k_deep_level leaves on a level the batch does not touch: it skips them)
+    if (old != NIL) {
+      const Level x = L0[old];
+      f.d0 = x.depth;
+      f.nv0 = x.nlive;
+      f.head = x.head;
+      f.tail = x.tail;
+      f.hslot = x.hslot;
+      f.tslot = x.tslot;
+      f.mem0 = x.member;
+      f.nlive0 = x.nlive;
+    }
+    LV[r + 1] = f;
+    vals[sl] = r + 1;
+  }
+}
+__global__ __launch_bounds__(FL_PREP_T) void k_deep_prep_put(Dev D, FlowArgs F) {
+  for (uint32_t i = blockIdx.y; i < fd_nslots(F); i += gridDim.y) k_deep_prep_put_one(D, F, i);
+}
+
 __global__ __launch_bounds__(FL_PREP_T) void k_deep_prep_b(Dev D, BatchArgs B, FlowArgs F) {
   for (uint32_t i = blockIdx.x; i < fd_nslots(F); i += gridDim.x) {
     k_deep_prep_b_one(D, B, F, i);

@@ -125,8 +125,9 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.gome_debug_flow_books.restype = C.c_int32
     lib.gome_debug_peek.argtypes = [VP, C.c_uint32, C.c_uint64, C.c_uint64, VP]
     lib.gome_debug_peek.restype = C.c_int32
-    lib.gome_debug_fifo_shape.argtypes = [VP, C.c_uint32, VP, C.c_size_t, C.POINTER(C.c_size_t)]
-    lib.gome_debug_fifo_shape.restype = C.c_int32
+    if hasattr(lib, "gome_debug_fifo_shape"):  # (diagnostics; variant builds of older trees lack it)
+        lib.gome_debug_fifo_shape.argtypes = [VP, C.c_uint32, VP, C.c_size_t, C.POINTER(C.c_size_t)]
+        lib.gome_debug_fifo_shape.restype = C.c_int32
     lib.gome_release_device_events.restype = C.c_int32
     lib.gome_get_stats.argtypes = [VP, P(Stats)]
     lib.gome_dup_records.argtypes = [VP, P(C.c_uint32), C.c_size_t, P(C.c_size_t)]

@@ -347,6 +347,7 @@ struct gome_engine {
   hipEvent_t fork{}, join{}, joinf{}, prep_h{}, prep_t{}, fork_adm{}, adm_done{}, seg_done{};
   hipEvent_t ho_fork{};  // the hottest book's post-plan checks done (its hand-over kernels fork there)
   hipEvent_t tfc_fork{}, tfc_done{};  // the tail's sort done / its cancel books' level pass done
+  hipEvent_t sort_done{};  // a batch's radix sort and segments, sorted ahead on the copy stream
   hipEvent_t dp_fork{}, cnt_fork{}, cnt_done{}, dw_done{}, dl_done{}, tl_done{};  // the hottest book's deep chain, k_flow_count beside its writes
   // the early plan of the hottest book (match_early.h): the last batch's plan done (flow stream),
   // its oid watermarks folded (hot stream), this batch's early prep and plan done (copy stream)
@@ -452,6 +453,13 @@ struct gome_engine {
       err = std::string("hipMalloc failed for ") + what + " (" + std::to_string(bytes) + " B)";
       return false;
     }
+    // every buffer starts zeroed: nothing a batch reads may depend on what an earlier engine in the
+    // process left in the memory (the allocator hands it back as it was)
+    if (hipMemset(q, 0, bytes) != hipSuccess) {
+      (void)hipFree(q);
+      err = std::string("hipMemset failed for ") + what;
+      return false;
+    }
     allocs.push_back(q);
     *p = static_cast<T*>(q);
     return true;
@@ -486,7 +494,7 @@ struct gome_engine {
         for (hipEvent_t ev : pr)
           if (ev) (void)hipEventDestroy(ev);
     }
-    for (hipEvent_t ev : {fork, join, joinf, prep_h, prep_t, fork_adm, adm_done, seg_done, ho_fork, tfc_fork, tfc_done, dp_fork, cnt_fork, cnt_done,
+    for (hipEvent_t ev : {fork, join, joinf, prep_h, prep_t, fork_adm, adm_done, seg_done, ho_fork, tfc_fork, tfc_done, sort_done, dp_fork, cnt_fork, cnt_done,
                           dw_done, dl_done, tl_done, tob_done, plan_done, oidmax_done, xpre_done, xprep_done,
                           xplan_done, adm_pre_done})
       if (ev) (void)hipEventDestroy(ev);
@@ -670,7 +678,7 @@ gome_status gome_engine::init(const gome_config& c) {
   HIPCHK(new_stream(&copy_stream));
   HIPCHK(new_stream(&d2h_stream));
   HIPCHK(new_stream(&h2d_stream));
-  for (hipEvent_t* ev : {&fork, &join, &joinf, &prep_h, &prep_t, &fork_adm, &adm_done, &seg_done, &ho_fork, &tfc_fork, &tfc_done,
+  for (hipEvent_t* ev : {&fork, &join, &joinf, &prep_h, &prep_t, &fork_adm, &adm_done, &seg_done, &ho_fork, &tfc_fork, &tfc_done, &sort_done,
                          &dp_fork, &cnt_fork, &cnt_done, &dw_done, &dl_done, &tl_done, &tob_done, &plan_done,
                          &oidmax_done, &xpre_done, &xprep_done, &xplan_done, &adm_pre_done})
     HIPCHK(hipEventCreateWithFlags(ev, hipEventDisableTiming));
@@ -946,6 +954,16 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   };
   HIPCHK(status_reset());
   const uint32_t T256 = 256, gN = ceil_div(n, T256);
+  // A pipelined device batch whose hottest book plans late (no early plan: books with DELs): its
+  // sort on the copy stream from the last batch's plan end, beside that batch's reconstruction
+  // and publish, instead of after them (the sort needs only this batch's records, and the slot's
+  // buffers were free once the batch before the last one ended, which that plan comes after).  Not
+  // while the plan runs: its record reads slowed a concurrent plan (round 3).
+  const bool sort_ahead = ahead && !early && !copy_busy && !cold_main && dominant && bid_prev > 0;
+  if (sort_ahead) {
+    HIPCHK(hipStreamWaitEvent(copy_stream, plan_done, 0));
+    ss = copy_stream;
+  }
   HIPCHK(mark(GOME_PH_SORT, 0, ss));
   HIPCHK(hipMemsetAsync(S.sst, 0, sizeof(Status), ss));
   const uint32_t nblk = ceil_div(n, RS_TILE);
@@ -978,6 +996,10 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   k_seg_bscan<<<1, 64, 0, ss>>>(S.bcnt, S.bcnt + 32, S.sst, FLOW_MIN_LOG2, MAX_FLOW);
   k_seg_scatter<<<gN, T256, 0, ss>>>(S.seg_start, S.sst, S.bcnt + 32, S.seg_order);
   HIPCHK(mark(GOME_PH_SORT, 1, ss));
+  if (ss != s) {
+    HIPCHK(hipEventRecord(sort_done, ss));
+    HIPCHK(hipStreamWaitEvent(s, sort_done, 0));
+  }
   k_sort_status<<<1, 1, 0, s>>>(d_st, S.sst);
 
   // ---- the early plan of the hottest book (match_early.h), on the copy stream: its records and

@@ -75,6 +75,21 @@ def test_chain_transitions_keep_parity():
 def test_chains_never_and_always(flags):
     """Deep books with DELs (config 5c's mix at a small scale): with the chains never enqueued
     every such book takes the legacy / cold kernels; always enqueued, the flow path."""
+    _chains_case(flags)
+
+
+def test_chains_always_after_early_plans():
+    """The always-enqueued case in a process whose earlier engine ran early plans: its device memory
+    comes back to the new engine as it was left.  This order faulted (an illegal access) until every
+    allocation started zeroed (gpurun_out/r05bg-r05bm)."""
+    import bench
+    from tests.test_gpu_early import _run as early_run
+    gen, _, _ = bench.shard_stream(100000, 1.0, 0, 1, 11)
+    early_run([gen(1 << 18).copy() for _ in range(4)], 100000, "early, then chains")
+    _chains_case(GOME_FLAG_CHAINS_ALWAYS)
+
+
+def _chains_case(flags):
     n = 1 << 16
     gen_syms = 500
     eng = Engine(max_symbols=gen_syms, max_batch=n, max_nodes=1 << 21, max_levels=1 << 21, flags=flags)

@@ -1224,7 +1224,10 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
     k_fc_unmark<<<dim3(px, nb), 256, 0, st>>>(D, B, R);
     k_fc_route<<<ceil_div(nb, 256), 256, 0, st>>>(D, R);
   };
-  if (c_canc) cancel_prep(FH, nh_head, FL_PG, true, flow_stream);
+  // (the head's per-record cancel prep kernels: 512 blocks a book, each a short slice of the hottest
+  // book's records, whose loops are chains of hash and index probes: config 4 +1.5% over 64,
+  // gpurun_out/r05br, r05bs)
+  if (c_canc) cancel_prep(FH, nh_head, 8 * FL_PG, true, flow_stream);
   HIPCHK(mark(GOME_PH_HEAD_PREP, 1, flow_stream));
   HIPCHK(hipEventRecord(prep_h, flow_stream));
   if (early) {  // the early inputs against this prep's, then the early plan taken (or not)

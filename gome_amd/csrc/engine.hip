@@ -352,6 +352,7 @@ struct gome_engine {
   // the early plan of the hottest book (match_early.h): the last batch's plan done (flow stream),
   // its oid watermarks folded (hot stream), this batch's early prep and plan done (copy stream)
   hipEvent_t plan_done{}, oidmax_done{}, xpre_done{}, xprep_done{}, xplan_done{};
+  hipEvent_t xcmp_done{}, xtake_done{};  // k_x_cmp done (flow stream), k_x_take done (plan stream)
   struct XBuf {
     XCtl* ctl = nullptr;
     FlowHdr* hdr = nullptr;
@@ -496,7 +497,7 @@ struct gome_engine {
     }
     for (hipEvent_t ev : {fork, join, joinf, prep_h, prep_t, fork_adm, adm_done, seg_done, ho_fork, tfc_fork, tfc_done, sort_done, dp_fork, cnt_fork, cnt_done,
                           dw_done, dl_done, tl_done, tob_done, plan_done, oidmax_done, xpre_done, xprep_done,
-                          xplan_done, adm_pre_done})
+                          xplan_done, xcmp_done, xtake_done, adm_pre_done})
       if (ev) (void)hipEventDestroy(ev);
     if (h_tob_syms) (void)hipHostFree(h_tob_syms);
     if (h_tob) (void)hipHostFree(h_tob);
@@ -680,7 +681,7 @@ gome_status gome_engine::init(const gome_config& c) {
   HIPCHK(new_stream(&h2d_stream));
   for (hipEvent_t* ev : {&fork, &join, &joinf, &prep_h, &prep_t, &fork_adm, &adm_done, &seg_done, &ho_fork, &tfc_fork, &tfc_done, &sort_done,
                          &dp_fork, &cnt_fork, &cnt_done, &dw_done, &dl_done, &tl_done, &tob_done, &plan_done,
-                         &oidmax_done, &xpre_done, &xprep_done, &xplan_done, &adm_pre_done})
+                         &oidmax_done, &xpre_done, &xprep_done, &xplan_done, &xcmp_done, &xtake_done, &adm_pre_done})
     HIPCHK(hipEventCreateWithFlags(ev, hipEventDisableTiming));
   for (Slot& S : slots) {
     for (hipEvent_t* ev : {&S.ev0, &S.ev1, &S.evm0, &S.evm1, &S.evh0, &S.evh1, &S.evf0, &S.evf1, &S.evc0, &S.evc1,
@@ -1041,7 +1042,11 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
     k_xd_sort_new<<<1, FL_PREP_T, DEEP_CAP * 8, es>>>(FX, X.ctl, x_dnew);
     HIPCHK(hipEventRecord(xpre_done, es));
     HIPCHK(hipStreamWaitEvent(ps, xpre_done, 0));
-    HIPCHK(hipStreamWaitEvent(ps, plan_done, 0));
+    // On the plan's own stream the last batch's plan, or its early plan's k_x_take, wrote F.hdr[0] /
+    // F.lvl on this stream before: no hop through the flow stream (plan_done) between two plans.
+    // (An early plan not taken has its fallback plan on the flow stream, which this chain may then
+    // read half-written: k_x_cmp finds that and this early plan is not taken either.)
+    if (ps != plan_stream) HIPCHK(hipStreamWaitEvent(ps, plan_done, 0));
     k_x_prep_b<<<1, FL_PREP_T, 0, ps>>>(Bx, FX, F, X.ctl, bid_prev);
     k_flow_prep_c<<<dim3(FL_PG, 1), FL_PREP_T, 0, ps>>>(Dx, Bx, FX);
     k_xd_prep_b<<<1, FL_PREP_T, XD_PREP_LDS, ps>>>(Bx, FX, F, X.ctl, x_dnew, bid_prev);
@@ -1232,8 +1237,16 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   HIPCHK(hipEventRecord(prep_h, flow_stream));
   if (early) {  // the early inputs against this prep's, then the early plan taken (or not)
     k_x_cmp<<<256, 256, 0, flow_stream>>>(D, F, FX, X.ctl);
-    HIPCHK(hipStreamWaitEvent(flow_stream, xplan_done, 0));
-    k_x_take<<<32, 256, 0, flow_stream>>>(D, F, FX, X.ctl);
+    if (plan_stream) {  // (right behind the early plan on its stream: the next early chain follows it there)
+      HIPCHK(hipEventRecord(xcmp_done, flow_stream));
+      HIPCHK(hipStreamWaitEvent(plan_stream, xcmp_done, 0));
+      k_x_take<<<32, 256, 0, plan_stream>>>(D, F, FX, X.ctl);
+      HIPCHK(hipEventRecord(xtake_done, plan_stream));
+      HIPCHK(hipStreamWaitEvent(flow_stream, xtake_done, 0));
+    } else {
+      HIPCHK(hipStreamWaitEvent(flow_stream, xplan_done, 0));
+      k_x_take<<<32, 256, 0, flow_stream>>>(D, F, FX, X.ctl);
+    }
   }
   {
     hipStream_t pst = flow_stream;

@@ -960,6 +960,7 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   // and publish, instead of after them (the sort needs only this batch's records, and the slot's
   // buffers were free once the batch before the last one ended, which that plan comes after).  Not
   // while the plan runs: its record reads slowed a concurrent plan (round 3).
+  // (A/B on one box: config 4 +0.6%, config 5c +0.3%, gpurun_out/r05bw)
   const bool sort_ahead = ahead && !early && !copy_busy && !cold_main && dominant && bid_prev > 0;
   if (sort_ahead) {
     HIPCHK(hipStreamWaitEvent(copy_stream, plan_done, 0));

@@ -367,6 +367,7 @@ struct gome_engine {
   FlPrepScr* x_dscr = nullptr;                 // deep books: prep scratch, price set, sorted prices
   unsigned long long *x_dkey = nullptr, *x_dnew = nullptr;
   uint32_t *x_dval = nullptr, *x_dslot = nullptr;
+  XComp* x_comp = nullptr;  // the early lane plan's records, gathered before the last plan's end
   bool early_on = true;            // (GOME_FLAG_NO_EARLY: never)
   // pipelined device batches of a dominated stream that plan late: admission ahead, on the early
   // stream beside the last batch's plan (k_adm_verify; GOME_FLAG_NO_ADM_AHEAD: never)
@@ -826,7 +827,7 @@ gome_status gome_engine::init(const gome_config& c) {
         !alloc(&X.log, ntouch, "early touch log") || !alloc(&X.dlvl, DEEP_CAP, "early deep levels"))
       return GOME_E_CAPACITY;
   if (!alloc(&x_pscr, 1, "early prep scratch") || !alloc(&x_adm, nb, "early verdicts") ||
-      !alloc(&x_evc, nb, "early event counts") || !alloc(&x_cnt, 2 * X_FIND_B, "early block counts") ||
+      !alloc(&x_evc, nb, "early event counts") || !alloc(&x_comp, nb, "early gathered records") || !alloc(&x_cnt, 2 * X_FIND_B, "early block counts") ||
       !alloc(&x_seg, 3, "early segment") || !alloc(&x_sidx, nb, "early permutation") ||
       !alloc(&x_dscr, 1, "early deep scratch") || !alloc(&x_dkey, DEEP_HASH, "early deep prices") ||
       !alloc(&x_dval, DEEP_HASH, "early deep levels of prices") || !alloc(&x_dnew, DEEP_CAP, "early deep sorted prices") ||
@@ -1038,6 +1039,7 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
     k_x_scatter<<<xn, X_FIND_T, 0, es>>>(d_ord, n, F.hdr, bid_prev, x_cnt, x_seg, X.ctl, x_sidx);
     HIPCHK(hipStreamWaitEvent(es, oidmax_done, 0));  // (the last batch's oid watermarks)
     k_x_adm<<<256, 256, 0, es>>>(Bx, X.ctl, d_oid_max, cfg.max_symbols, x_adm);
+    k_x_gather<<<1024, 256, 0, es>>>(Bx, x_seg, x_comp);
     k_flow_prep_a<<<dim3(FL_PG, 1), FL_PREP_T, 0, es>>>(Dx, Bx, FX);        // (lane plans)
     k_xd_prep_a<<<FL_PG, FL_PREP_T, 0, es>>>(Bx, FX, X.ctl);                 // (deep plans)
     k_xd_sort_new<<<1, FL_PREP_T, DEEP_CAP * 8, es>>>(FX, X.ctl, x_dnew);
@@ -1049,7 +1051,7 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
     // read half-written: k_x_cmp finds that and this early plan is not taken either.)
     if (ps != plan_stream) HIPCHK(hipStreamWaitEvent(ps, plan_done, 0));
     k_x_prep_b<<<1, FL_PREP_T, 0, ps>>>(Bx, FX, F, X.ctl, bid_prev);
-    k_flow_prep_c<<<dim3(FL_PG, 1), FL_PREP_T, 0, ps>>>(Dx, Bx, FX);
+    k_x_prep_c<<<ps == plan_stream ? 2 * plan_cus : FL_PG, FL_PREP_T, 0, ps>>>(Dx, FX, x_comp);
     k_xd_prep_b<<<1, FL_PREP_T, XD_PREP_LDS, ps>>>(Bx, FX, F, X.ctl, x_dnew, bid_prev);
     k_deep_prep_c<<<dim3(FL_PG, 1), FL_PREP_T, 0, ps>>>(Dx, Bx, FX);
     HIPCHK(hipEventRecord(xprep_done, ps));

@@ -181,6 +181,67 @@ __global__ void k_x_adm(BatchArgs Bx, XCtl* X, const uint32_t* oid_max, uint32_t
   if (__any(bad) && lane_id() == 0) atomicOr(&X->bad, 1u);
 }
 
+// The lane plan's records in two halves around the last plan's end.  Before it (early stream),
+// k_x_gather reads each of the segment's records through the permutation (the dependent loads)
+// into a compact 16-B entry in segment order: the price key, and for an admitted ADD its volume
+// with bit 63 set and bit 62 for a SALE.  After it (plan stream, on the plan's CUs), k_x_prep_c
+// maps the key to its level and writes the record, k_flow_prep_c's output: reading the compact
+// entries in order took the early chain's k_flow_prep_c 109 us -> (config 3, gpurun_out/r05bx).
+struct XComp {
+  unsigned long long key, v;
+};
+__global__ __launch_bounds__(256) void k_x_gather(BatchArgs Bx, const uint32_t* __restrict__ xseg, XComp* __restrict__ out) {
+  const uint32_t beg = xseg[1], end = xseg[2];
+  for (uint32_t b = beg + blockIdx.x * blockDim.x + threadIdx.x; b < end; b += gridDim.x * blockDim.x) {
+    const Prep q = prep_at(Bx, b);
+    XComp c;
+    c.key = static_cast<unsigned long long>(q.price) + FL_KEY_OFF;
+    c.v = (q.action == GOME_ADD && q.adm)
+              ? static_cast<unsigned long long>(q.vol) | (1ull << 63) | (q.side == GOME_SALE ? 1ull << 62 : 0ull)
+              : 0ull;
+    out[b - beg] = c;
+  }
+}
+constexpr uint32_t X_PREPC_U = 4;
+__global__ __launch_bounds__(FL_PREP_T) void k_x_prep_c(Dev D, FlowArgs F, const XComp* __restrict__ comp) {
+  __shared__ unsigned long long hkey[FL_HASH];
+  __shared__ uint32_t hval[FL_HASH];
+  const uint32_t h = F.h0, tid = threadIdx.x;
+  if (h >= fl_hend(D, F) || !uni(F.hdr[h].ok)) return;
+  const FlPrepScr* P = F.pscr;
+  const FlowHdr* hd = &F.hdr[h];
+  const uint32_t n = hd->end - hd->beg, obase = hd->obase;
+  const bool w32 = hd->w32 != 0;
+  const unsigned long long g = hd->g;
+  for (uint32_t i = tid; i < FL_HASH; i += FL_PREP_T) {
+    hkey[i] = P->key[i];
+    hval[i] = P->val[i];
+  }
+  __syncthreads();
+  const uint32_t stride = gridDim.x * FL_PREP_T;
+  for (uint32_t i0 = blockIdx.x * FL_PREP_T + tid; i0 < n; i0 += X_PREPC_U * stride) {
+    XComp c[X_PREPC_U];
+#pragma unroll
+    for (uint32_t u = 0; u < X_PREPC_U; ++u)
+      if (i0 + u * stride < n) c[u] = comp[i0 + u * stride];
+#pragma unroll
+    for (uint32_t u = 0; u < X_PREPC_U; ++u) {
+      const uint32_t i = i0 + u * stride;
+      if (i >= n) break;
+      unsigned long long rec = fl_rec(false, 0, 0, false, i, w32);
+      if (c[u].v >> 63) {
+        const unsigned long long key = c[u].key;
+        uint32_t s = fl_hash(key);
+        while (hkey[s] != key) s = (s + 1) & (FL_HASH - 1);
+        const unsigned long long vol = c[u].v & ((1ull << 62) - 1ull);
+        const unsigned long long v = w32 ? static_cast<unsigned long long>(static_cast<double>(vol) / static_cast<double>(g)) : vol;
+        rec = fl_rec(true, hval[s], v, ((c[u].v >> 62) & 1ull) != 0, i, w32);
+      }
+      F.ord8[obase + i] = rec;
+    }
+  }
+}
+
 // The early head prep's price set and header (k_flow_prep_b's, with the book's live levels taken
 // from the previous batch's plan instead of the level pool).  F: the pipeline's own flow args
 // (F.hdr[0] / F.lvl: the previous batch's hottest book after its plan, header of batch bid_prev).

@@ -353,6 +353,9 @@ struct gome_engine {
   // its oid watermarks folded (hot stream), this batch's early prep and plan done (copy stream)
   hipEvent_t plan_done{}, oidmax_done{}, xpre_done{}, xprep_done{}, xplan_done{};
   hipEvent_t xcmp_done{}, xtake_done{};  // k_x_cmp done (flow stream), k_x_take done (plan stream)
+  // the last enqueued batch's final F.hdr[0] / F.lvl writer (its plan or its early plan's k_x_take)
+  // ran on the plan stream: the next early chain there needs no plan_done (device batches only)
+  bool f_on_plan = false;
   struct XBuf {
     XCtl* ctl = nullptr;
     FlowHdr* hdr = nullptr;
@@ -1049,7 +1052,9 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
     // F.lvl on this stream before: no hop through the flow stream (plan_done) between two plans.
     // (An early plan not taken has its fallback plan on the flow stream, which this chain may then
     // read half-written: k_x_cmp finds that and this early plan is not taken either.)
-    if (ps != plan_stream) HIPCHK(hipStreamWaitEvent(ps, plan_done, 0));
+    // (Device batches only: on the host path, three batches in flight, every other batch's early
+    // plan came 13 ms late without this wait, config 3's e2e 147.7 -> 120.7M, gpurun_out/r05cb.)
+    if (!(ps == plan_stream && f_on_plan && !copy_busy)) HIPCHK(hipStreamWaitEvent(ps, plan_done, 0));
     k_x_prep_b<<<1, FL_PREP_T, 0, ps>>>(Bx, FX, F, X.ctl, bid_prev);
     k_x_prep_c<<<ps == plan_stream ? 2 * plan_cus : FL_PG, FL_PREP_T, 0, ps>>>(Dx, FX, x_comp);
     k_xd_prep_b<<<1, FL_PREP_T, XD_PREP_LDS, ps>>>(Bx, FX, F, X.ctl, x_dnew, bid_prev);
@@ -1240,7 +1245,7 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   HIPCHK(hipEventRecord(prep_h, flow_stream));
   if (early) {  // the early inputs against this prep's, then the early plan taken (or not)
     k_x_cmp<<<256, 256, 0, flow_stream>>>(D, F, FX, X.ctl);
-    if (plan_stream) {  // (right behind the early plan on its stream: the next early chain follows it there)
+    if (plan_stream && !copy_busy) {  // (right behind the early plan: the next early chain follows it there)
       HIPCHK(hipEventRecord(xcmp_done, flow_stream));
       HIPCHK(hipStreamWaitEvent(plan_stream, xcmp_done, 0));
       k_x_take<<<32, 256, 0, plan_stream>>>(D, F, FX, X.ctl);
@@ -1267,6 +1272,7 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
       HIPCHK(hipEventRecord(pl_join, plan_stream));
       HIPCHK(hipStreamWaitEvent(flow_stream, pl_join, 0));
     }
+    f_on_plan = plan_stream && (pst == plan_stream || (early && !copy_busy));
   }
   HIPCHK(hipEventRecord(plan_done, flow_stream));
   if (early) k_x_logcopy<<<1024, 256, 0, flow_stream>>>(F, FX, X.ctl);

@@ -197,6 +197,11 @@ def rank_batch(batch, world, share, scaling="weak"):
     return int(round(batch * (world if scaling == "weak" else 1) * share))
 
 
+def hottest_book_orders(rec) -> int:
+    """Orders of the batch's hottest book (its longest symbol segment): the serial plan's length."""
+    return int(np.bincount(rec["symbol_id"]).max()) if len(rec) else 0
+
+
 def per_rank_values(x, rank, world, device):
     """Every rank's value of x, in rank order, on every rank (one all_reduce of a one-hot vector)."""
     import torch
@@ -381,9 +386,11 @@ def main():
                     help="JSON OrderNode messages of the consumer leg (0: off)")
     ap.add_argument("--pool-nodes", type=int, default=0, help="gome_config.max_nodes (0: sized from the run)")
     ap.add_argument("--pool-levels", type=int, default=0, help="gome_config.max_levels (0: sized from the run)")
-    ap.add_argument("--scaling", choices=("weak", "strong"), default="weak",
-                    help="weak: --batch orders per GPU per step; strong: --batch orders per step in all, "
-                         "split over the GPUs (DESIGN 7)")
+    ap.add_argument("--scaling", choices=("weak", "strong"), default="strong",
+                    help="strong (default): --batch orders per step in all, split over the GPUs by their "
+                         "symbols' share, so rank 0's hottest book -- the batch's serial plan -- gets the same "
+                         "orders per step at every N and the p99 batch latency stays that of one GPU; weak: "
+                         "--batch orders per GPU per step (rank 0's hottest book N times longer; DESIGN 7)")
     ap.add_argument("--plan-cus", type=int, default=None,
                     help="gome_config.plan_cus (default: 0 = the engine's default, 8 plan CUs; -1: none)")
     ap.add_argument("--step-log", default="", help="write each timed step's engine counters (JSONL)")
@@ -588,6 +595,9 @@ def main():
     if sum(s["n_flow_books"] for s in sts) == 0:
         cands.pop(plan_key)
     max_seg = max(s["max_segment"] for s in sts)
+    # the hottest book's orders per step on each rank: the serial plan that bounds the rank's batch
+    # (flat in N under strong scaling, N x under weak)
+    hot_ranks = per_rank_values(max_seg, rank, world, cdev) if use_pg else [int(max_seg)]
     digest_check = None
     if use_pg:
         g_orders, g_fills, g_events, elapsed, lat = combine_ranks(orders, fills, events, elapsed, lat, cdev)
@@ -769,6 +779,7 @@ def main():
             "p50_device_batch_ms": round(pctl(dev_lat, 0.5), 3),
             "p99_device_batch_ms": round(pctl(dev_lat, 0.99), 3),
             "p99_device_batch_ms_per_rank": p99_ranks,
+            "hot_book_orders_per_rank": [int(x) for x in hot_ranks],
             "fills_per_s": round(g_fills / elapsed, 1),
             "events_per_s": round(g_events / elapsed, 1),
             "cancels_per_batch": int(cancels / steps),
@@ -797,6 +808,10 @@ def main():
                          "traffic": traffic, "kernel": f"{kname} ({kdesc})",
                          "kernel_ms": round(ms_dom, 3), "alg_bytes_per_launch": int(bdom),
                          "match_phase_alg_bytes": int(balg)},
+            # SURVEY §8d's primary metric (host records in, H2D + pipeline + D2H, events back in host
+            # memory) from the same run; `value` keeps the records resident in HBM (the bench contract:
+            # a PCIe-inclusive rate is reported beside it, never as it)
+            "value_e2e": e2e["value"] if e2e else None,
             "e2e": e2e,
             "consumer": consumer,
             "cpu_baseline": cpu,

@@ -26,7 +26,8 @@ GOME_FLAG_CHAINS_NEVER = 8  # gome_config.flags: never (deep books and books wit
 GOME_FLAG_PHASES = 16  # gome_config.flags: record the per-phase timing events (gome_stats.ms_phase)
 GOME_FLAG_NO_EARLY = 32  # gome_config.flags: never plan the hottest book early
 GOME_FLAG_NO_ADM_AHEAD = 64  # gome_config.flags: never run admission ahead of the batch
-GOME_ABI_VERSION = 11
+GOME_FLAG_POISON = 128  # gome_config.flags: test builds: device buffers start 0xA5-filled (reads of unwritten scratch show)
+GOME_ABI_VERSION = 12
 GOME_ORD_ADM_HOST, GOME_ORD_ADMITTED = 1, 2  # gome_order.flags: host-resolved admission (ABI 4)
 GOME_MAX_INFLIGHT = 3
 

@@ -652,9 +652,12 @@ struct gome_names {
 };
 
 // The markers: open addressing over (hash, key bytes in an arena); a marker the consumer took
-// provisionally is STAGED until commit (-> a tombstone) or abort (-> live again).
+// provisionally is STAGED until commit (-> a tombstone) or abort (-> live again).  A STAGED marker
+// set again before the commit (the gRPC side's SetPrePool after the consumer's DeletePrePool,
+// nodepool.go:14-28) is RESET: commit leaves it LIVE (the new marker), abort LIVE too (one key, one
+// marker).
 struct gome_prepool {
-  enum : uint8_t { EMPTY = 0, LIVE = 1, TOMB = 2, STAGED = 3 };
+  enum : uint8_t { EMPTY = 0, LIVE = 1, TOMB = 2, STAGED = 3, RESET = 4 };
   struct Ent {
     uint64_t h;
     uint64_t off;  // key bytes in arena
@@ -696,7 +699,7 @@ struct gome_prepool {
     mask = cap - 1;
     used = 0;
     for (const Ent& x : old) {
-      if (x.state != LIVE && x.state != STAGED) continue;
+      if (x.state != LIVE && x.state != STAGED && x.state != RESET) continue;
       uint64_t j = x.h & mask;
       while (tab[j].state != EMPTY) j = (j + 1) & mask;
       tab[j] = Ent{x.h, arena.size(), x.len, x.state};
@@ -705,14 +708,18 @@ struct gome_prepool {
     }
     staged.clear();  // (slots moved: re-list the staged ones)
     for (uint64_t j = 0; j < cap; ++j)
-      if (tab[j].state == STAGED) staged.push_back(j);
+      if (tab[j].state == STAGED || tab[j].state == RESET) staged.push_back(j);
   }
   void set(const std::string& k) {
     const uint64_t h = hash_bytes(k.data(), k.size());
-    if (find(k, h) >= 0) return;  // (a staged marker set again stays staged: commit removes it)
+    const int64_t f = find(k, h);
+    if (f >= 0) {  // (a staged marker set again: the commit keeps it)
+      if (tab[static_cast<size_t>(f)].state == STAGED) tab[static_cast<size_t>(f)].state = RESET;
+      return;
+    }
     if ((used + 1) * 2 > mask + 1) rebuild(std::max<uint64_t>(1024, (live + 1) * 4 > mask + 1 ? (mask + 1) * 2 : mask + 1));
     uint64_t j = h & mask;
-    while (tab[j].state == LIVE || tab[j].state == STAGED) j = (j + 1) & mask;
+    while (tab[j].state == LIVE || tab[j].state == STAGED || tab[j].state == RESET) j = (j + 1) & mask;
     if (tab[j].state == EMPTY) ++used;
     tab[j] = Ent{h, arena.size(), static_cast<uint32_t>(k.size()), LIVE};
     arena.insert(arena.end(), k.begin(), k.end());
@@ -720,8 +727,14 @@ struct gome_prepool {
   }
   bool take(const std::string& k) {
     const int64_t j = find(k, hash_bytes(k.data(), k.size()));
-    if (j < 0 || tab[static_cast<size_t>(j)].state != LIVE) return false;
-    tab[static_cast<size_t>(j)].state = TOMB;
+    if (j < 0) return false;
+    uint8_t& st = tab[static_cast<size_t>(j)].state;
+    if (st == RESET) {  // (the re-set marker taken: the consumer's staged take still pending)
+      st = STAGED;
+      return true;
+    }
+    if (st != LIVE) return false;
+    st = TOMB;
     --live;
     return true;
   }
@@ -730,8 +743,14 @@ struct gome_prepool {
   bool stage(const std::string& k) {
     std::lock_guard<std::mutex> g(mu);
     const int64_t j = find(k, hash_bytes(k.data(), k.size()));
-    if (j < 0 || tab[static_cast<size_t>(j)].state != LIVE) return false;
-    tab[static_cast<size_t>(j)].state = STAGED;
+    if (j < 0) return false;
+    uint8_t& st = tab[static_cast<size_t>(j)].state;
+    if (st == RESET) {  // (the re-set marker consumed again in the same window; already listed)
+      st = STAGED;
+      return true;
+    }
+    if (st != LIVE) return false;
+    st = STAGED;
     staged.push_back(static_cast<uint64_t>(j));
     return true;
   }
@@ -741,13 +760,15 @@ struct gome_prepool {
       if (tab[j].state == STAGED) {
         tab[j].state = TOMB;
         --live;
+      } else if (tab[j].state == RESET) {
+        tab[j].state = LIVE;
       }
     staged.clear();
   }
   void abort() {
     std::lock_guard<std::mutex> g(mu);
     for (uint64_t j : staged)
-      if (tab[j].state == STAGED) tab[j].state = LIVE;
+      if (tab[j].state == STAGED || tab[j].state == RESET) tab[j].state = LIVE;
     staged.clear();
   }
 };

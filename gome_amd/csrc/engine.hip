@@ -458,9 +458,12 @@ struct gome_engine {
       err = std::string("hipMalloc failed for ") + what + " (" + std::to_string(bytes) + " B)";
       return false;
     }
-    // every buffer starts zeroed: nothing a batch reads may depend on what an earlier engine in the
-    // process left in the memory (the allocator hands it back as it was)
-    if (hipMemset(q, 0, bytes) != hipSuccess) {
+    // Every buffer starts zeroed (defence: the allocator hands memory back as an earlier engine in
+    // the process left it).  No kernel may depend on it: a buffer a batch reads is written first,
+    // by a per-batch reset or by init's own memsets.  GOME_FLAG_POISON (test hosts) fills 0xA5
+    // instead, so a read of scratch nobody wrote shows as an out-of-range value.  (Round 5's fault,
+    // the deep level pass read its sentinel row 0, which no prep wrote.)
+    if (hipMemset(q, (cfg.flags & GOME_FLAG_POISON) ? 0xA5 : 0, bytes) != hipSuccess) {
       (void)hipFree(q);
       err = std::string("hipMemset failed for ") + what;
       return false;

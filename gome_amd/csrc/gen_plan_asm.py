@@ -28,7 +28,7 @@ Two variants: W=64 (volumes and depths as 64-bit SGPR pairs / two lane registers
 and W=32 (the book's volumes divided by their GCD fit 32 bits: one register each, half the
 lane traffic and no carry chains).  k_flow_prep picks the variant per book.
 
-Run: python gome_amd/csrc/gen_plan_asm.py   (writes flow_plan_asm.inc next to this file)
+Run: python gome_amd/csrc/gen_plan_asm.py [--out PATH]   (default: flow_plan_asm.inc next to this file)
 Semantics follow engine.go:56-136 / nodepool.go:61-115 at the aggregate level; see the
 comments of k_flow_plan in match_flow.h.
 """
@@ -1399,9 +1399,13 @@ def aligned(lines: list[str]) -> list[str]:
 
 
 def main():
-    import sys
+    import argparse
     here = os.path.dirname(os.path.abspath(__file__))
-    out = sys.argv[1] if len(sys.argv) > 1 else os.path.join(here, "flow_plan_asm.inc")
+    ap = argparse.ArgumentParser(description="Generate the flow plans' asm loops (flow_plan_asm.inc). "
+                                             "Tuning knobs come from GOME_PLAN_* environment variables.")
+    ap.add_argument("--out", default=os.path.join(here, "flow_plan_asm.inc"),
+                    help="output path (default: flow_plan_asm.inc next to this script)")
+    out = ap.parse_args().out
     with open(out, "w") as f:
         f.write("// Generated by gen_plan_asm.py — do not edit.\n")
         for w, g in ((64, Gen(64)), (32, Gen(32)), ("32C", GenC()), ("32D", GenD()), ("32DC", GenDC()),

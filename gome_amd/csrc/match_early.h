@@ -606,6 +606,10 @@ __global__ __launch_bounds__(FL_PREP_T) void k_xd_prep_b(BatchArgs Bx, FlowArgs 
   }
   if (tid < ((8u - ((end - beg) & 7u)) & 7u)) FX.ord8[(end - beg) + tid] = 0ull;  // no-op padding
   if (tid == 0) {
+    FlowLvl z{};  // the bid sentinel's row, clean (as k_deep_prep_b)
+    z.old = NIL;
+    z.head = z.tail = NIL;
+    LV[0] = z;
     FlowHdr x{};
     x.ok = FL_OK_DEEP;
     x.nl = n;

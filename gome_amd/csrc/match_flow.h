@@ -32,12 +32,16 @@
 //   k_flow_write   (one workgroup per book) appends the surviving new makers to the FIFOs,
 //                  inserts them into the cancel index, rewrites the level array.
 //
-// Eligibility (else the book takes the legacy hot path, bit-exact as before): the segment
-// has no DEL and no zero-volume admitted ADD (quirk Q6), the book carries no quirk state
-// (Q2 wrong-side cancels / zero-volume makers ever seen, Book::flags), and the book's live
-// levels plus the batch's new prices fit FL_CAP lanes.  Under those conditions every live
-// level has nodes, positive depth and exactly one side-set membership, which is what makes
-// the aggregate plan exact.
+// Eligibility (else the book takes the legacy hot path, bit-exact as before): no
+// duplicate-oid candidate (Q7) in the segment and no BOOK_QUIRK state (a state only the legacy /
+// cold kernels apply).  A segment with DELs takes the cancel plans (match_flow_cancel.h, W32C /
+// W32DC); more levels than FL_CAP lanes the deep plans (match_flow_deep.h).  Every live level
+// then has nodes, positive depth and exactly one side-set membership, which is what makes the
+// aggregate plan exact -- except the states the head books of at least LEGACY_HOT_MIN orders may
+// carry: stale side-set members (Q2), zero-volume takers and makers (Q6, BOOK_ZERO)
+// and wrong-side cancels, each checked after the plan (k_flow_zero_check, k_flow_stale_check,
+// k_fc_stale_level), which hand the book to the legacy kernel before any of it is written where
+// the aggregate view cannot say what the reference does.
 #pragma once
 #include <hip/hip_runtime.h>
 

@@ -422,6 +422,11 @@ fd_prep_b_hdr:
 #undef PB
   if (tid < ((8u - ((end - beg) & 7u)) & 7u)) F.ord8[obase + (end - beg) + tid] = 0ull;  // no-op padding
   if (tid == 0) {
+    // the bid sentinel's row: no old level, no FIFO (no level pass reads it; a clean row all the same)
+    FlowLvl z{};
+    z.old = NIL;
+    z.head = z.tail = NIL;
+    LV[0] = z;
     FlowHdr x{};
     x.ok = FL_OK_DEEP;
     x.nl = n;
@@ -733,7 +738,11 @@ __device__ __forceinline__ void k_deep_level_one(Dev D, FlowArgs F, uint32_t slo
   for (uint32_t i0 = blockIdx.x * 64u; i0 < nt; i0 += gridDim.x * 64u) {
     const uint32_t i = i0 + lane;
     const uint32_t lv = i < nt ? R[i].lvl : 0u;
-    bool head = i < nt && (i == 0 || R[i - 1].lvl != lv);
+    // (not the bid sentinel's run, level 0: it holds only the no-op rests of 0 of dropped ADDs,
+    // DELs that find nothing and the padding, and nothing is rebuilt there -- as every lane level
+    // pass skips q == 0.  Until round 6 it was walked as a level: fc_level_lane read row 0's FIFO
+    // and target count, which no prep writes, and a fresh engine on recycled memory faulted.)
+    bool head = i < nt && lv != 0 && (i == 0 || R[i - 1].lvl != lv);
     if (head) {  // a level of few touches: its lane (fc_level_lane, fl_level_lane)
       const uint32_t b = LV[lv].base, n = LV[lv].pad1 - b;
       if (dc && n <= FC_LANE_MAX) {

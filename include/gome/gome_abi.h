@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define GOME_ABI_VERSION 11u
+#define GOME_ABI_VERSION 12u
 
 /* ---- status codes (replace the reference's swallowed errors / panics,
  *      rabbitmq.go:44-49,70-72,120-122; nodelink.go:132,142,157) ---------- */
@@ -165,6 +165,11 @@ typedef struct gome_node {
  * queues (gome_config.hw_queues); these flags turn them off (A/B and tests: same results). */
 #define GOME_FLAG_NO_EARLY 32u
 #define GOME_FLAG_NO_ADM_AHEAD 64u
+/* Test builds of a host (ABI >= 12): every device buffer of the handle starts filled with 0xA5
+ * bytes instead of zeros, so a kernel that reads scratch it never wrote sees an out-of-range
+ * index or an absurd count (an error or a fault) instead of a benign zero.  Same results as
+ * the default when no such read exists; never for production. */
+#define GOME_FLAG_POISON 128u
 
 typedef struct gome_config {
   uint32_t accuracy;       /* gomengine.accuracy (config.yaml.example:23-24), default 8 */

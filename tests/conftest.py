@@ -20,6 +20,16 @@ except Exception:  # pragma: no cover
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs the HIP engine)")
+    # GOME_TEST_POISON=1: every engine a test creates starts its device buffers 0xA5-filled
+    # (GOME_FLAG_POISON), so a kernel reading scratch it never wrote shows up in the whole suite
+    if os.environ.get("GOME_TEST_POISON") == "1":
+        from gome_amd import abi
+        init = abi.Engine.__init__
+
+        def poisoned(self, *a, flags: int = 0, **kw):
+            init(self, *a, flags=flags | abi.GOME_FLAG_POISON, **kw)
+
+        abi.Engine.__init__ = poisoned
 
 
 @pytest.fixture(scope="session", autouse=True)

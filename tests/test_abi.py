@@ -17,7 +17,7 @@ def test_library_exports_every_declared_symbol():
     assert len(names) >= 14
     for n in names:
         assert hasattr(lib, n), n
-    assert lib.gome_abi_version() == abi.GOME_ABI_VERSION == 11
+    assert lib.gome_abi_version() == abi.GOME_ABI_VERSION == 12
 
 
 def test_record_layouts_match_header():

@@ -6,7 +6,7 @@ import numpy as np
 import pytest
 
 from gome_amd import workload as wl
-from gome_amd.abi import GOME_FLAG_CHAINS_ALWAYS, GOME_FLAG_CHAINS_NEVER, Engine
+from gome_amd.abi import GOME_FLAG_CHAINS_ALWAYS, GOME_FLAG_CHAINS_NEVER, GOME_FLAG_POISON, Engine
 from oracle.pyoracle import Oracle
 from tests.test_gpu_v4 import _cmp, _cmp_books
 
@@ -80,13 +80,23 @@ def test_chains_never_and_always(flags):
 
 def test_chains_always_after_early_plans():
     """The always-enqueued case in a process whose earlier engine ran early plans: its device memory
-    comes back to the new engine as it was left.  This order faulted (an illegal access) until every
-    allocation started zeroed (gpurun_out/r05bg-r05bm)."""
+    comes back to the new engine as it was left.  This order faulted (an illegal access) in round 5:
+    the deep level pass walked the bid sentinel's row 0 of a deep book's level table, which no prep
+    writes, as a level (fc_level_lane: its FIFO head and target count came from the recycled memory;
+    profiles/evidence/r05bg-r05bm)."""
     import bench
     from tests.test_gpu_early import _run as early_run
     gen, _, _ = bench.shard_stream(100000, 1.0, 0, 1, 11)
     early_run([gen(1 << 18).copy() for _ in range(4)], 100000, "early, then chains")
     _chains_case(GOME_FLAG_CHAINS_ALWAYS)
+
+
+def test_chains_always_on_poisoned_memory():
+    """The same deep books with DELs on an engine whose every buffer starts 0xA5-filled
+    (GOME_FLAG_POISON): before the fix, row 0's node count read 0xA5A5A5A5 and the batch failed
+    with ERR_CHUNKS (the gather's claim overflowed) -- deterministically, not by the luck of what
+    an earlier engine left."""
+    _chains_case(GOME_FLAG_CHAINS_ALWAYS | GOME_FLAG_POISON)
 
 
 def _chains_case(flags):
@@ -100,11 +110,11 @@ def _chains_case(flags):
         eng.submit(b)
         _cmp(eng.drain(), orc.submit(b), f"flags {flags} batch {i}")
         s = eng.stats()
-        if flags == GOME_FLAG_CHAINS_NEVER:
+        if flags & GOME_FLAG_CHAINS_NEVER:
             assert s["chains"] == 0 and s["n_flow_cancels"] == 0
         else:
             assert s["chains"] == CH_DEEP | CH_CANC
-    if flags == GOME_FLAG_CHAINS_ALWAYS:
+    if flags & GOME_FLAG_CHAINS_ALWAYS:
         assert eng.stats()["n_flow_cancels"] > 0
     z = wl.ZipfSymbols(gen_syms, 1.0)
     _cmp_books(eng, orc, [int(z.rank_to_id[r]) for r in range(8)] + list(range(0, gen_syms, 41)), f"flags {flags}")

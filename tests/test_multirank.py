@@ -129,3 +129,45 @@ def test_strong_and_weak_rank_batches(world):
             for r in range(world)]
     assert abs(sum(strong) - batch) <= world and abs(sum(weak) - world * batch) <= world
     assert strong[0] == max(strong)  # (rank 0 owns the hottest symbol: Zipf rank 0)
+
+
+def _scaling_worker(rank, world, port, out_dir, mode, batch, steps):
+    """bench.py's rank code for the stream: this rank's batches at `mode`, the hottest book's orders
+    per step (the serial plan that bounds the rank's batch on the GPU), every rank's p99 of it."""
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        gen, share, _ = bench.make_stream("config3", rank, world, 42)
+        n = bench.rank_batch(batch, world, share, mode)
+        hot = [bench.hottest_book_orders(gen(n)) for _ in range(steps)]
+        p99 = bench.per_rank_values(bench.pctl(hot, 0.99), rank, world, "cpu")
+        _, _, _, _, step_max = bench.combine_ranks(float(n), 0.0, 0.0, 0.0, [float(h) for h in hot], "cpu")
+        np.save(os.path.join(out_dir, f"s{rank}.npy"), np.array(p99 + step_max, dtype=np.float64))
+    finally:
+        dist.destroy_process_group()
+
+
+def _hot_p99(world, mode, batch=1 << 19, steps=6):
+    if world == 1:
+        gen, share, _ = bench.make_stream("config3", 0, 1, 42)
+        n = bench.rank_batch(batch, 1, share, mode)
+        return [bench.pctl([bench.hottest_book_orders(gen(n)) for _ in range(steps)], 0.99)]
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_scaling_worker, args=(world, _free_port(), d, mode, batch, steps), nprocs=world, join=True)
+        res = [np.load(os.path.join(d, f"s{r}.npy")) for r in range(world)]
+    assert res[0].tobytes() == res[1].tobytes()
+    return list(res[0][:world])
+
+
+def test_strong_scaling_keeps_the_hottest_book_flat_in_n():
+    """bench.py's default (--scaling strong) at world 2 over gloo: rank 0 still owns the hottest
+    symbol, and its hottest book gets the same orders per step as one GPU's (the plan that sets the
+    p99 batch latency), while weak scaling doubles it."""
+    one = _hot_p99(1, "strong")[0]
+    strong = _hot_p99(2, "strong")
+    weak = _hot_p99(2, "weak")
+    assert abs(strong[0] / one - 1.0) < 0.03, (one, strong)
+    assert strong[1] < strong[0]  # (rank 1's hottest is the Zipf rank-1 symbol)
+    assert abs(weak[0] / one - 2.0) < 0.06, (one, weak)

@@ -27,7 +27,7 @@ tmp = tempfile.mkdtemp(prefix=f"gv_{tag}_")
 shutil.copytree(os.path.join(ROOT, "include"), os.path.join(tmp, "include"))
 shutil.copytree(build.CSRC, os.path.join(tmp, "gome_amd", "csrc"))
 csrc = os.path.join(tmp, "gome_amd", "csrc")
-subprocess.run([sys.executable, os.path.join(csrc, "gen_plan_asm.py"), os.path.join(csrc, "flow_plan_asm.inc")],
+subprocess.run([sys.executable, os.path.join(csrc, "gen_plan_asm.py"), "--out", os.path.join(csrc, "flow_plan_asm.inc")],
                env=env, check=True)
 out = os.path.join(build.PKG, f"libgome_{tag}.so")
 srcs = [os.path.join(csrc, os.path.basename(s)) for s in build.SOURCES]

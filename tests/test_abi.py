@@ -71,12 +71,12 @@ def test_create_refuses_a_stale_abi_version():
     """gome_config.abi_version sits where ABI <= 10 had a zero pad word: a caller built against an
     older header is refused before anything else (no silent argument shift)."""
     lib = abi.load_library()
-    for v in (0, 10, 12):
+    for v in (0, 11, 13):
         cfg = abi.Config(max_symbols=4, max_batch=16, max_nodes=64, max_levels=64, abi_version=v)
         h = C.c_void_p()
         assert lib.gome_create(C.byref(cfg), C.byref(h)) == abi.GOME_E_INVAL
         msg = lib.gome_last_error(None).decode()
-        assert f"abi_version is {v}" in msg and "ABI 11" in msg, msg
+        assert f"abi_version is {v}" in msg and f"ABI {abi.GOME_ABI_VERSION}" in msg, msg
 
 
 def test_hw_queue_count_parsing():

@@ -99,46 +99,49 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
             "(the engine has no CPU fallback)")
     lib = C.CDLL(path)
     P, VP = C.POINTER, C.c_void_p
-    lib.gome_create.argtypes = [P(Config), P(VP)]
-    lib.gome_destroy.argtypes = [VP]
-    lib.gome_destroy.restype = None
-    lib.gome_last_error.argtypes = [VP]
-    lib.gome_last_error.restype = C.c_char_p
-    lib.gome_abi_version.restype = C.c_uint32
-    lib.gome_submit_batch.argtypes = [VP, VP, C.c_size_t, C.c_uint64]
-    lib.gome_submit_batch_device.argtypes = [VP, VP, C.c_size_t, C.c_uint64, VP]
-    lib.gome_submit_batch_async.argtypes = [VP, VP, C.c_size_t, C.c_uint64]
-    lib.gome_collect.argtypes = [VP, P(VP), P(C.c_size_t), P(Stats)]
-    lib.gome_submit_batch_device_async.argtypes = [VP, VP, C.c_size_t, C.c_uint64]
-    lib.gome_collect_device.argtypes = [VP, P(VP), P(C.c_size_t), P(Stats)]
-    lib.gome_inflight.argtypes = [VP]
-    lib.gome_inflight.restype = C.c_size_t
-    lib.gome_host_alloc.argtypes = [VP, C.c_size_t, P(VP)]
-    lib.gome_host_free.argtypes = [VP, VP]
-    lib.gome_host_free.restype = None
-    lib.gome_fixed_from_scaled.argtypes = [C.c_double, P(C.c_int64)]
-    lib.gome_drain_events.argtypes = [VP, VP, C.c_size_t, P(C.c_size_t)]
-    lib.gome_pending_events.argtypes = [VP]
-    lib.gome_pending_events.restype = C.c_size_t
-    lib.gome_device_events.argtypes = [VP, P(VP), P(C.c_size_t)]
-    lib.gome_release_device_events.argtypes = [VP]
-    lib.gome_debug_flow_books.argtypes = [VP, C.POINTER(C.c_uint32), C.c_size_t, C.POINTER(C.c_size_t)]
-    lib.gome_debug_flow_books.restype = C.c_int32
-    lib.gome_debug_peek.argtypes = [VP, C.c_uint32, C.c_uint64, C.c_uint64, VP]
-    lib.gome_debug_peek.restype = C.c_int32
-    if hasattr(lib, "gome_debug_fifo_shape"):  # (diagnostics; variant builds of older trees lack it)
-        lib.gome_debug_fifo_shape.argtypes = [VP, C.c_uint32, VP, C.c_size_t, C.POINTER(C.c_size_t)]
-        lib.gome_debug_fifo_shape.restype = C.c_int32
-    lib.gome_release_device_events.restype = C.c_int32
-    lib.gome_get_stats.argtypes = [VP, P(Stats)]
-    lib.gome_dup_records.argtypes = [VP, P(C.c_uint32), C.c_size_t, P(C.c_size_t)]
-    lib.gome_take_deferred.argtypes = [VP]
-    lib.gome_top_of_book.argtypes = [VP, VP, C.c_size_t, VP]
-    lib.gome_top_of_book_enqueue.argtypes = [VP, VP, C.c_size_t]
-    lib.gome_top_of_book_collect.argtypes = [VP, VP, C.c_size_t, P(C.c_size_t)]
-    lib.gome_snapshot_levels.argtypes = [VP, C.c_uint32, VP, C.c_size_t, P(C.c_size_t)]
-    lib.gome_snapshot_fifo.argtypes = [VP, C.c_uint32, C.c_int64, VP, C.c_size_t, P(C.c_size_t)]
-    lib.gome_load_books.argtypes = [VP, C.c_size_t, VP, VP, VP, VP, C.c_size_t]
+    # a host-layer-only build (host.cpp, consume.cpp, loadgen.cpp: the sanitizer build of
+    # tests/test_host_sanitizers.py) has no engine entry points
+    engine = hasattr(lib, "gome_create")
+    if engine:
+        lib.gome_create.argtypes = [P(Config), P(VP)]
+        lib.gome_destroy.argtypes = [VP]
+        lib.gome_destroy.restype = None
+        lib.gome_last_error.argtypes = [VP]
+        lib.gome_last_error.restype = C.c_char_p
+        lib.gome_abi_version.restype = C.c_uint32
+        lib.gome_submit_batch.argtypes = [VP, VP, C.c_size_t, C.c_uint64]
+        lib.gome_submit_batch_device.argtypes = [VP, VP, C.c_size_t, C.c_uint64, VP]
+        lib.gome_submit_batch_async.argtypes = [VP, VP, C.c_size_t, C.c_uint64]
+        lib.gome_collect.argtypes = [VP, P(VP), P(C.c_size_t), P(Stats)]
+        lib.gome_submit_batch_device_async.argtypes = [VP, VP, C.c_size_t, C.c_uint64]
+        lib.gome_collect_device.argtypes = [VP, P(VP), P(C.c_size_t), P(Stats)]
+        lib.gome_inflight.argtypes = [VP]
+        lib.gome_inflight.restype = C.c_size_t
+        lib.gome_host_alloc.argtypes = [VP, C.c_size_t, P(VP)]
+        lib.gome_host_free.argtypes = [VP, VP]
+        lib.gome_host_free.restype = None
+        lib.gome_drain_events.argtypes = [VP, VP, C.c_size_t, P(C.c_size_t)]
+        lib.gome_pending_events.argtypes = [VP]
+        lib.gome_pending_events.restype = C.c_size_t
+        lib.gome_device_events.argtypes = [VP, P(VP), P(C.c_size_t)]
+        lib.gome_release_device_events.argtypes = [VP]
+        lib.gome_debug_flow_books.argtypes = [VP, C.POINTER(C.c_uint32), C.c_size_t, C.POINTER(C.c_size_t)]
+        lib.gome_debug_flow_books.restype = C.c_int32
+        lib.gome_debug_peek.argtypes = [VP, C.c_uint32, C.c_uint64, C.c_uint64, VP]
+        lib.gome_debug_peek.restype = C.c_int32
+        if hasattr(lib, "gome_debug_fifo_shape"):  # (diagnostics; variant builds of older trees lack it)
+            lib.gome_debug_fifo_shape.argtypes = [VP, C.c_uint32, VP, C.c_size_t, C.POINTER(C.c_size_t)]
+            lib.gome_debug_fifo_shape.restype = C.c_int32
+        lib.gome_release_device_events.restype = C.c_int32
+        lib.gome_get_stats.argtypes = [VP, P(Stats)]
+        lib.gome_dup_records.argtypes = [VP, P(C.c_uint32), C.c_size_t, P(C.c_size_t)]
+        lib.gome_take_deferred.argtypes = [VP]
+        lib.gome_top_of_book.argtypes = [VP, VP, C.c_size_t, VP]
+        lib.gome_top_of_book_enqueue.argtypes = [VP, VP, C.c_size_t]
+        lib.gome_top_of_book_collect.argtypes = [VP, VP, C.c_size_t, P(C.c_size_t)]
+        lib.gome_snapshot_levels.argtypes = [VP, C.c_uint32, VP, C.c_size_t, P(C.c_size_t)]
+        lib.gome_snapshot_fifo.argtypes = [VP, C.c_uint32, C.c_int64, VP, C.c_size_t, P(C.c_size_t)]
+        lib.gome_load_books.argtypes = [VP, C.c_size_t, VP, VP, VP, VP, C.c_size_t]
     lib.gome_fixed_from_double.argtypes = [C.c_double, C.c_uint32, P(C.c_int64)]
     lib.gome_render_match_result.argtypes = [VP, VP, C.c_int64, C.c_uint32] + [C.c_char_p] * 6 + [
         VP, C.c_char_p, C.c_size_t]
@@ -197,14 +200,16 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.gome_gen_destroy.restype = None
     for f in ("gome_gen_create", "gome_gen_batch", "gome_gen_shares"):
         getattr(lib, f).restype = C.c_int32
-    for f in ("gome_create", "gome_submit_batch", "gome_submit_batch_device", "gome_drain_events",
-              "gome_device_events", "gome_get_stats", "gome_snapshot_levels", "gome_snapshot_fifo",
-              "gome_fixed_from_double", "gome_fixed_from_scaled", "gome_submit_batch_async",
-              "gome_collect", "gome_host_alloc", "gome_load_books", "gome_dup_records",
-              "gome_take_deferred", "gome_top_of_book", "gome_submit_batch_device_async",
-              "gome_top_of_book_enqueue", "gome_top_of_book_collect",
-              "gome_collect_device"):
+    lib.gome_fixed_from_scaled.argtypes = [C.c_double, P(C.c_int64)]
+    for f in ("gome_fixed_from_double", "gome_fixed_from_scaled"):
         getattr(lib, f).restype = C.c_int32
+    if engine:
+        for f in ("gome_create", "gome_submit_batch", "gome_submit_batch_device", "gome_drain_events",
+                  "gome_device_events", "gome_get_stats", "gome_snapshot_levels", "gome_snapshot_fifo",
+                  "gome_submit_batch_async", "gome_collect", "gome_host_alloc", "gome_load_books",
+                  "gome_dup_records", "gome_take_deferred", "gome_top_of_book", "gome_submit_batch_device_async",
+                  "gome_top_of_book_enqueue", "gome_top_of_book_collect", "gome_collect_device"):
+            getattr(lib, f).restype = C.c_int32
     _lib = lib
     return lib
 

@@ -30,8 +30,10 @@ HEADERS = (sorted(glob.glob(os.path.join(CSRC, "*.h"))) + sorted(glob.glob(os.pa
 
 def _digest(deps: list[str], cmd: list[str]) -> str:
     """sha256 over the build command and every source's path and content (not mtimes: the
-    snapshot that travels to the GPU box does not keep them in order)."""
-    h = hashlib.sha256("\0".join(cmd).encode())
+    snapshot that travels to the GPU box does not keep them in order).  Paths inside the tree are
+    hashed relative to it, so a checkout elsewhere (the GPU box's snapshot) is not stale."""
+    rel = [os.path.relpath(c, ROOT) if os.path.isabs(c) and c.startswith(ROOT + os.sep) else c for c in cmd]
+    h = hashlib.sha256("\0".join(rel).encode())
     for d in sorted(deps):
         h.update(os.path.relpath(d, ROOT).encode() + b"\0")
         with open(d, "rb") as f:
@@ -93,6 +95,27 @@ def build_stamps() -> str:
     cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-DGOME_STAMPS", *DEVICE_FLAGS,
            "-I", os.path.join(ROOT, "include"), *SOURCES, "-o", out]
     _run(cmd)
+    return out
+
+
+def build_host_sanitized(force: bool = False) -> str:
+    """Test-only: the host layer (host.cpp, consume.cpp, loadgen.cpp: JSON decode, interning,
+    pre-pool markers, MatchResult render, load generator; no device code) built by g++ with
+    AddressSanitizer + UndefinedBehaviorSanitizer into libgome_host_asan.so, never loaded by the
+    product.  tests/test_host_sanitizers.py loads it (GOME_LIB, the sanitizer runtimes preloaded)
+    under the decoder and consumer tests (SURVEY §5, VERDICT r5 next #6)."""
+    out = os.path.join(PKG, "libgome_host_asan.so")
+    tmp = out + ".tmp"
+    srcs = [s for s in SOURCES if not s.endswith(".hip")]
+    cmd = ["g++", "-std=c++17", "-O1", "-g", "-fPIC", "-shared", "-fno-omit-frame-pointer",
+           "-fsanitize=address,undefined", "-fno-sanitize-recover=undefined", "-Wall", "-Wno-unused-result",
+           "-I", os.path.join(ROOT, "include"), *srcs, "-o", tmp]
+    stale, dig = _stale(out, srcs + HEADERS, cmd)
+    if force or stale:
+        _run(cmd)
+        os.replace(tmp, out)
+        _stamp(out, dig)
+        BUILT.append(out)
     return out
 
 

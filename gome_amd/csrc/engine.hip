@@ -463,7 +463,11 @@ struct gome_engine {
     // by a per-batch reset or by init's own memsets.  GOME_FLAG_POISON (test hosts) fills 0xA5
     // instead, so a read of scratch nobody wrote shows as an out-of-range value.  (Round 5's fault,
     // the deep level pass read its sentinel row 0, which no prep wrote.)
-    if (hipMemset(q, (cfg.flags & GOME_FLAG_POISON) ? 0xA5 : 0, bytes) != hipSuccess) {
+    // The fill goes on the engine's own stream, ahead of init's explicit memsets and copies on it:
+    // a plain hipMemset runs on the legacy null stream, which the engine's non-blocking streams do
+    // not wait for, so it could land after them (round 6: a 0xA5 fill over the zeroed headers
+    // faulted; a zero fill can clobber d_first / dh_val's 0xFF and the level-class table).
+    if (hipMemsetAsync(q, (cfg.flags & GOME_FLAG_POISON) ? 0xA5 : 0, bytes, stream) != hipSuccess) {
       (void)hipFree(q);
       err = std::string("hipMemset failed for ") + what;
       return false;
@@ -925,6 +929,7 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
       S.ev_cap = ncap;
       if (!alloc(&S.d_events, S.ev_cap, "events")) { poisoned = true; return GOME_E_CAPACITY; }
     }
+    HIPCHK(hipStreamSynchronize(stream));  // (alloc's fill, before the batch's streams use them)
   }
   // cancel-index hygiene: erases leave tombstones and lookups that miss stop only at an EMPTY
   // slot, so rebuild the table from the live nodes before it fills up (70%)

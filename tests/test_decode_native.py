@@ -187,3 +187,65 @@ def test_consume_records_and_markers():
 def test_pack_messages_offsets():
     buf, off = pack_messages(["ab", b"", "é"])
     assert buf == b"ab\xc3\xa9" and off.tolist() == [0, 2, 2, 4]
+
+
+def test_staged_marker_set_again_survives_the_commit():
+    """the gRPC side's SetPrePool of a key the consumer has staged (consumed by a batch not
+    yet committed) leaves a live marker, as SetPrePool after DeletePrePool does in the reference
+    (nodepool.go:14-28); abort keeps one marker; a take of the re-set marker consumes it."""
+    names, pre = Names(), PrePool()
+    cons = BatchingConsumer(type("E", (), {"max_batch": 16, "max_symbols": 4})(), pre, MatchSink(), names)
+    pre.set("s", "u", "1")
+    assert cons.records([_msg(oid="1")])["flags"].tolist() == [3]  # staged
+    pre.set("s", "u", "1")                                          # set again before the commit
+    pre.commit()
+    assert len(pre) == 1
+    assert cons.records([_msg(oid="1")])["flags"].tolist() == [3]  # the new marker admits it
+    pre.set("s", "u", "1")
+    pre.abort()
+    assert len(pre) == 1
+    cons.records([_msg(oid="1")])
+    pre.set("s", "u", "1")
+    assert pre.consume_add("s", "u", "1")                           # the re-set marker taken
+    pre.commit()
+    assert len(pre) == 0
+
+
+# ---- Hypothesis: structured damage to valid OrderNode bodies (also the corpus of the sanitizer run,
+# tests/test_host_sanitizers.py): truncated UTF-8 sequences, nesting, long escapes, duplicate keys
+from hypothesis import HealthCheck, given, settings, strategies as hs  # noqa: E402
+
+_UTF8 = [b"\xc3", b"\xe2\x82", b"\xf0\x9f\x98", b"\xed\xa0", b"\xf4\x90", b"\xc0", b"\xff", b"\x80\x80"]
+_ESC = ["\\n", "\\\"", "\\\\", "\\/", "\\u0041", "\\ud83d\\ude00", "\\ud800", "\\udc00", "\\u00e9", "\\t"]
+
+
+@hs.composite
+def _damaged(draw):
+    k = draw(hs.integers(0, 63))
+    body = _msg(oid=str(k), tx=k % 2, price=str(40000000 + k), vol="100000000").encode()
+    kind = draw(hs.sampled_from(["utf8", "nest", "escape", "dup", "cut"]))
+    if kind == "utf8":  # a truncated or invalid UTF-8 sequence inside a string value
+        at = body.index(b'"Symbol":"') + 10
+        body = body[:at] + draw(hs.sampled_from(_UTF8)) * draw(hs.integers(1, 3)) + body[at:]
+    elif kind == "nest":  # an extra member nested d deep (arrays and objects)
+        d = draw(hs.integers(1, 400))
+        o = draw(hs.sampled_from(["[", '{"n":']))
+        c = "]" if o == "[" else "}"
+        body = body[:-1] + b',"x":' + (o * d + "1" + c * d).encode() + b"}"
+    elif kind == "escape":  # long runs of escapes in a string the engine reads
+        s = "".join(draw(hs.lists(hs.sampled_from(_ESC), min_size=1, max_size=300)))
+        body = body[:-1] + b',"Uuid":"' + s.encode() + b'"}'
+    elif kind == "dup":  # duplicate and case-folded keys: the last one wins
+        key = draw(hs.sampled_from(["Action", "action", "ACTION", "Price", "pRICE", "Symbol", "\\u0053ymbol"]))
+        val = draw(hs.sampled_from(["1", "2", "null", '"s"', "1e3", "[]"]))
+        body = body[:-1] + f',"{key}":{val}'.encode() * draw(hs.integers(1, 4)) + b"}"
+    else:  # truncated anywhere
+        body = body[:draw(hs.integers(0, len(body)))]
+    return body
+
+
+@settings(max_examples=300, deadline=None, suppress_health_check=[HealthCheck.too_slow])
+@given(hs.lists(_damaged(), min_size=1, max_size=24))
+def test_damaged_messages_match_literal(msgs):
+    _check(msgs)
+    _check(msgs, threads=3)

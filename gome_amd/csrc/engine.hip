@@ -1040,6 +1040,9 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
     Bx.adm_flag = x_adm; Bx.ev_count = x_evc; Bx.seq_base = seq_base;
     const uint32_t xn = std::min<uint32_t>(X_FIND_B, std::max<uint32_t>(1u, ceil_div(n, 4096u)));
     HIPCHK(hipStreamWaitEvent(es, prep_h, 0));  // (the last batch's head prep: F.hdr[0] names its book)
+    // a host batch's records arrive by the H2D stream: the record work waits for them (until round 6
+    // it read the slot's previous records, which k_x_cmp then refused; a poisoned fresh slot faulted)
+    if (copy_busy) HIPCHK(hipStreamWaitEvent(es, S.h2d, 0));
     HIPCHK(hipMemsetAsync(X.ctl, 0, sizeof(XCtl), es));
     HIPCHK(hipMemsetAsync(x_pscr, 0, sizeof(FlPrepScr), es));
     HIPCHK(hipMemsetAsync(X.hdr, 0, sizeof(FlowHdr), es));

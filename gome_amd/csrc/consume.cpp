@@ -15,6 +15,7 @@
 #include <vector>
 
 #include "../../include/gome/gome_host.h"
+#include "host_pool.h"
 
 extern "C" gome_status gome_fixed_from_scaled(double v, int64_t* out);
 
@@ -537,15 +538,7 @@ void decode_all(const char* buf, const uint64_t* off, size_t n, uint32_t nt, std
       }
     }
   };
-  if (nt == 1) {
-    work(0);
-    return;
-  }
-  std::vector<std::thread> th;
-  th.reserve(nt - 1);
-  for (uint32_t k = 1; k < nt; ++k) th.emplace_back(work, k);
-  work(0);
-  for (auto& t : th) t.join();
+  gome_host::Pool::get().run(nt, work);
 }
 
 inline const char* str_ptr(const Str& s, const std::vector<std::string>& arenas) {
@@ -616,8 +609,11 @@ struct Interner {
       if (lens[id] == n && std::memcmp(strs[id], s, n) == 0) return id;
     }
   }
-  uint32_t intern(const char* s, size_t n) {
-    const uint64_t h = hash_bytes(s, n);
+  void prefetch(uint64_t h) const {
+    if (!slot.empty()) __builtin_prefetch(&slot[h & mask]);
+  }
+  uint32_t intern(const char* s, size_t n) { return intern_h(s, n, hash_bytes(s, n)); }
+  uint32_t intern_h(const char* s, size_t n, uint64_t h) {
     const int64_t f = find(s, n, h);
     if (f >= 0) return static_cast<uint32_t>(f);
     if ((strs.size() + 1) * 2 > mask + 1) grow();
@@ -678,17 +674,21 @@ struct gome_prepool {
     k.append(reinterpret_cast<const char*>(&b), 4).append(u, un);
     k.append(o, on);
   }
-  bool same(const Ent& x, uint64_t h, const std::string& k) const {
-    return x.h == h && x.len == k.size() && std::memcmp(arena.data() + x.off, k.data(), k.size()) == 0;
+  bool same(const Ent& x, uint64_t h, const char* k, size_t n) const {
+    return x.h == h && x.len == n && std::memcmp(arena.data() + x.off, k, n) == 0;
   }
-  // slot of the key (LIVE or STAGED), or -1
-  int64_t find(const std::string& k, uint64_t h) const {
+  // slot of the key (LIVE, STAGED or RESET), or -1
+  int64_t find(const char* k, size_t n, uint64_t h) const {
     if (tab.empty()) return -1;
     for (uint64_t j = h & mask;; j = (j + 1) & mask) {
       const Ent& x = tab[j];
       if (x.state == EMPTY) return -1;
-      if (x.state != TOMB && same(x, h, k)) return static_cast<int64_t>(j);
+      if (x.state != TOMB && same(x, h, k, n)) return static_cast<int64_t>(j);
     }
+  }
+  int64_t find(const std::string& k, uint64_t h) const { return find(k.data(), k.size(), h); }
+  void prefetch(uint64_t h) const {
+    if (!tab.empty()) __builtin_prefetch(&tab[h & mask]);
   }
   void rebuild(uint64_t cap) {  // (drops tombstones and their key bytes)
     std::vector<Ent> old;
@@ -742,7 +742,11 @@ struct gome_prepool {
   // DeletePrePool of a DEL (engine.go:90): a LIVE marker becomes STAGED
   bool stage(const std::string& k) {
     std::lock_guard<std::mutex> g(mu);
-    const int64_t j = find(k, hash_bytes(k.data(), k.size()));
+    return stage_locked(k.data(), k.size(), hash_bytes(k.data(), k.size()));
+  }
+  // (the caller holds mu: the consumer takes it once per batch)
+  bool stage_locked(const char* k, size_t n, uint64_t h) {
+    const int64_t j = find(k, n, h);
     if (j < 0) return false;
     uint8_t& st = tab[static_cast<size_t>(j)].state;
     if (st == RESET) {  // (the re-set marker consumed again in the same window; already listed)
@@ -881,11 +885,62 @@ gome_status gome_consume_order_nodes(gome_names* nm, gome_prepool* pp, const cha
   if (!nm || !pp || !n_out || (n && (!buf || !off || !out))) return GOME_E_INVAL;
   std::vector<Dec> dec;
   std::vector<std::string> arenas;
-  decode_all(buf, off, n, pick_threads(threads, n), dec, arenas);
+  const uint32_t nt = pick_threads(threads, n);
+  decode_all(buf, off, n, nt, dec, arenas);
+  // Per message, on the pool: the hashes the queue-order pass probes with (symbol, uuid, oid and the
+  // marker key, built here as gome_prepool::key builds it).  The pass itself is serial -- ids are
+  // handed out in first-seen order and markers are consumed in queue order (engine.go:58-62,90) --
+  // and bound by its table probes' cache misses (the oid and marker tables hold millions of keys):
+  // with the hashes known it prefetches the slots PF messages ahead (round 6; the pass cost ~1 us a
+  // message before, as much as the 8-thread decode).
+  struct Pre {
+    uint64_t hs, hu, ho, hk;
+    uint32_t koff, klen, ka;  // the marker key: karena[ka][koff, koff + klen)
+  };
+  std::vector<Pre> pre(n);
+  std::vector<std::string> karena(nt);
+  gome_host::Pool::get().run(nt, [&](uint32_t t) {
+    const size_t i0 = n * t / nt, i1 = n * (t + 1) / nt;
+    std::string& ka = karena[t];
+    ka.reserve(48 * (i1 - i0));
+    for (size_t i = i0; i < i1; ++i) {
+      const Dec& d = dec[i];
+      Pre& q = pre[i];
+      if (d.action != GOME_ADD && d.action != GOME_DEL) continue;
+      const char* sym = str_ptr(d.s[2], arenas);
+      const char* uuid = str_ptr(d.s[0], arenas);
+      const char* oid = str_ptr(d.s[1], arenas);
+      const size_t sl = d.s[2].len, ul = d.s[0].len, ol = d.s[1].len;
+      q.hs = hash_bytes(sym ? sym : "", sl);
+      q.hu = hash_bytes(uuid ? uuid : "", ul);
+      q.ho = hash_bytes(oid ? oid : "", ol);
+      const size_t k0 = ka.size();
+      const uint32_t a = static_cast<uint32_t>(sl), b = static_cast<uint32_t>(ul);
+      ka.append(reinterpret_cast<const char*>(&a), 4).append(sym ? sym : "", sl);
+      ka.append(reinterpret_cast<const char*>(&b), 4).append(uuid ? uuid : "", ul);
+      ka.append(oid ? oid : "", ol);
+      q.koff = static_cast<uint32_t>(k0);
+      q.ka = t;
+      q.klen = static_cast<uint32_t>(ka.size() - k0);
+      q.hk = hash_bytes(ka.data() + k0, q.klen);
+    }
+  });
   gome_consume_stats s{};
   s.messages = n;
   size_t k = 0;
+  constexpr size_t PF = 16;  // messages of prefetch distance
+  std::lock_guard<std::mutex> lock(pp->mu);  // (the markers, once for the batch)
   for (size_t i = 0; i < n; ++i) {
+    if (i + PF < n) {
+      const Dec& f = dec[i + PF];
+      if (f.action == GOME_ADD || f.action == GOME_DEL) {
+        const Pre& q = pre[i + PF];
+        nm->in[0].prefetch(q.hs);
+        nm->in[1].prefetch(q.hu);
+        nm->in[2].prefetch(q.ho);
+        pp->prefetch(q.hk);
+      }
+    }
     const Dec& d = dec[i];
     s.not_objects += d.is_object ? 0 : 1;
     const int act = d.action;
@@ -896,6 +951,7 @@ gome_status gome_consume_order_nodes(gome_names* nm, gome_prepool* pp, const cha
       ++s.ignored;
       continue;
     }
+    const Pre& q = pre[i];
     const char* sym = str_ptr(d.s[2], arenas);
     const char* uuid = str_ptr(d.s[0], arenas);
     const char* oid = str_ptr(d.s[1], arenas);
@@ -903,7 +959,7 @@ gome_status gome_consume_order_nodes(gome_names* nm, gome_prepool* pp, const cha
     int64_t p = 0, v = 0;
     bool bad = gome_fixed_from_scaled(d.price, &p) != GOME_OK || gome_fixed_from_scaled(d.volume, &v) != GOME_OK || v < 0;
     if (!bad && max_symbols) {
-      const int64_t sid = nm->in[0].find(sym ? sym : "", sl, hash_bytes(sym ? sym : "", sl));
+      const int64_t sid = nm->in[0].find(sym ? sym : "", sl, q.hs);
       const uint64_t would = sid >= 0 ? static_cast<uint64_t>(sid) : nm->in[0].strs.size();
       bad = would >= max_symbols;
     }
@@ -912,27 +968,26 @@ gome_status gome_consume_order_nodes(gome_names* nm, gome_prepool* pp, const cha
       code = nm->tx_code(d.tx);
       bad = code < 0;
     }
-    std::string& key = pp->kb;
-    gome_prepool::key(key, sym ? sym : "", sl, uuid ? uuid : "", ul, oid ? oid : "", ol);
+    const char* key = karena[q.ka].data() + q.koff;
     if (bad) {  // outside the engine's domain: not submitted (its marker is consumed as DoOrder would)
       ++s.rejected;
-      pp->stage(key);
+      pp->stage_locked(key, q.klen, q.hk);
       continue;
     }
     gome_order& r = out[k];
     r.price_fx = p;
     r.volume_fx = v;
-    r.symbol_id = nm->in[0].intern(sym ? sym : "", sl);
-    r.uuid_id = nm->in[1].intern(uuid ? uuid : "", ul);
-    r.oid_id = nm->in[2].intern(oid ? oid : "", ol);
+    r.symbol_id = nm->in[0].intern_h(sym ? sym : "", sl, q.hs);
+    r.uuid_id = nm->in[1].intern_h(uuid ? uuid : "", ul, q.hu);
+    r.oid_id = nm->in[2].intern_h(oid ? oid : "", ol, q.ho);
     r.side = static_cast<uint8_t>(code);
     r.action = static_cast<uint8_t>(act);
     if (act == GOME_ADD) {
-      const bool ok = pp->stage(key);
+      const bool ok = pp->stage_locked(key, q.klen, q.hk);
       s.admitted += ok ? 1 : 0;
       r.flags = static_cast<uint16_t>(GOME_ORD_ADM_HOST | (ok ? GOME_ORD_ADMITTED : 0));
     } else {
-      pp->stage(key);
+      pp->stage_locked(key, q.klen, q.hk);
       r.flags = GOME_ORD_ADM_HOST;
     }
     if (msg_index) msg_index[k] = static_cast<uint32_t>(i);

@@ -179,6 +179,21 @@ def pack_messages(msgs):
     return b"".join(bodies), off
 
 
+class PackedQueue:
+    """doOrder deliveries as one buffer of bodies plus offsets (how an AMQP client reads them off its
+    socket): batches are (buf, offsets[k:k + m + 1]) views, no per-message objects and no copy."""
+
+    def __init__(self, msgs):
+        self.buf, self.off = pack_messages(msgs)
+
+    def __len__(self):
+        return len(self.off) - 1
+
+    def batches(self, m: int):
+        for k in range(0, len(self), m):
+            yield self.buf, self.off[k:min(k + m, len(self)) + 1]
+
+
 def decode_order_nodes(msgs, threads: int = 0) -> list[dict]:
     """json.Unmarshal of each body into an OrderNode, the fields the engine reads: {"Action",
     "Uuid", "Oid", "Symbol", "Transaction", "Price", "Volume"} (gome_decode_order_nodes).  Keys
@@ -269,15 +284,15 @@ class MatchSink:
             self._q.extend(lines)
             self.published += len(lines)
 
-    def publish_block(self, block: bytes, n: int):
-        """n newline-terminated lines, in publish order."""
+    def publish_block(self, block, n: int):
+        """n newline-terminated lines, in publish order (bytes or a buffer the sink now owns)."""
         with self.lock:
             self._blocks.append(block)
             self.published += n
 
     def _flush(self):
         for b in self._blocks:
-            self._q.extend(b.decode().split("\n")[:-1])
+            self._q.extend(bytes(b).decode().split("\n")[:-1])
         self._blocks.clear()
 
     @property
@@ -321,7 +336,6 @@ class BatchingConsumer:
         self.max_symbols = getattr(engine, "max_symbols", None)
         self.seq = 0
         self.consumed = self.rejected = self.batches = self.dups = 0
-        self._buf = C.create_string_buffer(1 << 20)
 
     # ---- draining ------------------------------------------------------------------
     def drain(self, q, block_s: float = 0.0) -> list:
@@ -345,15 +359,17 @@ class BatchingConsumer:
         return msgs
 
     # ---- one batch -------------------------------------------------------------------
-    def records(self, msgs) -> np.ndarray:
+    def records(self, msgs, out: np.ndarray | None = None) -> np.ndarray:
         """Decode, convert and admit (in queue order) -> gome_order records.  The pre-pool markers
         are consumed staged (process() commits them once the engine took the batch).  A message
         outside the engine's domain is counted in `rejected` and not submitted; an Action other
-        than ADD / DEL (a syntax error included) is a zero record, as DoOrder ignores it."""
+        than ADD / DEL (a syntax error included) is a zero record, as DoOrder ignores it.
+        msgs: the message bodies, or one packed delivery buffer (buf, offsets[n + 1]) (PackedQueue);
+        out: where the records go (e.g. a page-locked buffer of the engine's, >= n records)."""
         self.pre.abort()  # (a batch refused earlier left nothing behind)
-        buf, off = pack_messages(msgs)
+        buf, off = msgs if isinstance(msgs, tuple) else pack_messages(msgs)
         n = len(off) - 1
-        rec = np.zeros(n, ORDER_DTYPE)
+        rec = np.zeros(n, ORDER_DTYPE) if out is None else out
         got, st = C.c_size_t(), ConsumeStats()
         s = self.lib.gome_consume_order_nodes(self.names.h, self.pre.h, buf, off.ctypes.data, n,
                                               int(self.max_symbols or 0), self.threads, rec.ctypes.data, None,
@@ -363,24 +379,26 @@ class BatchingConsumer:
         self.rejected += st.rejected
         return rec[:got.value]
 
-    def render_block(self, ev: np.ndarray, rec: np.ndarray, seq_base: int) -> bytes:
-        """The batch's MatchResult lines as one block of bytes (newline-terminated)."""
+    def render_block(self, ev: np.ndarray, rec: np.ndarray, seq_base: int):
+        """The batch's MatchResult lines (newline-terminated), rendered straight into a buffer of
+        their own that the caller keeps (a memoryview; no copy of the block afterwards)."""
         N = self.names
+        cap = 1400 * len(ev) + (1 << 16)
         while True:
+            out = np.empty(cap, np.uint8)
             k = self.lib.gome_render_events_mt(
                 ev.ctypes.data, len(ev), rec.ctypes.data, len(rec), seq_base, self.acc,
                 N.table("sym"), N.count("sym"), N.table("uuid"), N.count("uuid"),
                 N.table("oid"), N.count("oid"), N.tx_array().ctypes.data, self.threads,
-                self._buf, len(self._buf))
+                out.ctypes.data, cap)
             if k >= 0:
-                break
+                return memoryview(out)[:k]
             if k == -(1 << 63):
                 raise GomeError(1, "event references an unknown id")
-            self._buf = C.create_string_buffer(int(-k) + (1 << 20))
-        return C.string_at(self._buf, k)
+            cap = int(-k) + (1 << 16)
 
     def render(self, ev: np.ndarray, rec: np.ndarray, seq_base: int) -> list[str]:
-        return self.render_block(ev, rec, seq_base).decode().split("\n")[:-1]
+        return bytes(self.render_block(ev, rec, seq_base)).decode().split("\n")[:-1]
 
     def process(self, msgs) -> int:
         """Apply one drained batch; returns the MatchResults published.  Raises only when the
@@ -404,11 +422,57 @@ class BatchingConsumer:
         self.seq += len(rec)
         self.dups += int(self.eng.stats()["n_dup_oid"])
         ev = self.eng.drain()
-        block = self.render_block(ev, rec, base)
-        n = block.count(b"\n")
-        self.sink.publish_block(block, n)
+        self.sink.publish_block(self.render_block(ev, rec, base), len(ev))  # (one line per event)
         self.batches += 1
-        return n
+        return len(ev)
+
+    def process_stream(self, batches, depth: int = 2) -> int:
+        """Apply drained batches in order with up to `depth` of them in flight on the engine
+        (gome_submit_batch_async / gome_collect): batch k+1's decode, admission and H2D run while
+        the device applies batch k, and each batch's MatchResults are rendered as it is collected.
+        Publishes exactly what process() would, batch after batch (the markers of a batch are
+        committed when the engine took it, as there).  Engines without the async calls (test
+        doubles) take process() per batch."""
+        if not hasattr(self.eng, "submit_async"):
+            return sum(self.process(b) for b in batches)
+        from collections import deque
+        depth = max(1, min(depth, 3))
+        ring = [self.eng.host_buffer(self.max_batch) for _ in range(depth + 1)]
+        flight = deque()  # (records, seq base, messages)
+        total, slot = 0, 0
+
+        def finish():
+            rec, base, nm = flight.popleft()
+            ev, st = self.eng.collect(copy=False)
+            self.dups += int(st["n_dup_oid"])
+            if len(ev):
+                self.sink.publish_block(self.render_block(ev, rec, base), len(ev))
+                self.batches += 1
+            return len(ev)
+
+        for msgs in batches:
+            n = (len(msgs[1]) - 1) if isinstance(msgs, tuple) else len(msgs)
+            if n > self.max_batch:
+                raise GomeError(1, "batch larger than the engine's max_batch")
+            rec = self.records(msgs, out=ring[slot][:n])
+            slot = (slot + 1) % len(ring)
+            base = self.seq
+            if len(rec):
+                try:
+                    self.eng.submit_async(rec, seq_base=base)
+                except BaseException:
+                    self.pre.abort()
+                    raise
+            self.pre.commit()
+            self.consumed += n
+            if len(rec):
+                self.seq += len(rec)
+                flight.append((rec, base, n))
+            while len(flight) >= depth:
+                total += finish()
+        while flight:
+            total += finish()
+        return total
 
     def poll(self, q, block_s: float = 0.0) -> int:
         msgs = self.drain(q, block_s)

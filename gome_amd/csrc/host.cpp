@@ -8,12 +8,15 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
+#include <memory>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
 
 #include "../../include/gome/gome_abi.h"
 #include "../../include/gome/gome_host.h"
+#include "host_pool.h"
 
 namespace {
 
@@ -320,8 +323,20 @@ extern "C" int64_t gome_render_match_result(const gome_event* ev, const gome_ord
 }
 
 // gome_render_events over `threads` pieces cut at taker boundaries (a taker's Node.Volume is a
-// running sum over its consecutive events), each rendered into a buffer of its own and copied
-// out in publish order.
+// running sum over its consecutive events): each piece rendered into a buffer of its own, then the
+// pieces copied into the caller's buffer at their offsets, both on the host worker pool (host_pool.h).
+// The piece buffers are kept from call to call (no per-call allocation, zero fill or thread start:
+// ADVICE r5; one call at a time takes them).
+namespace {
+struct RenderPiece {
+  std::unique_ptr<char[]> b;
+  size_t cap = 0;
+  int64_t got = 0;
+};
+std::mutex g_render_mu;
+std::vector<RenderPiece> g_pieces;
+}  // namespace
+
 extern "C" int64_t gome_render_events_mt(const gome_event* ev, size_t n, const gome_order* batch, size_t batch_n,
                                          uint64_t seq_base, uint32_t accuracy, const char* const* sym_names,
                                          size_t n_sym, const char* const* uuid_names, size_t n_uuid,
@@ -337,37 +352,37 @@ extern "C" int64_t gome_render_events_mt(const gome_event* ev, size_t n, const g
     while (i > cut[k - 1] && i < n && ev[i].taker_seq == ev[i - 1].taker_seq) ++i;
     cut[k] = i;
   }
-  std::vector<std::vector<char>> piece(t);
-  std::vector<int64_t> got(t, 0);
-  auto work = [&](uint32_t k) {
+  std::lock_guard<std::mutex> one(g_render_mu);
+  if (g_pieces.size() < t) g_pieces.resize(t);
+  auto render = [&](uint32_t k) {
     const size_t a = cut[k], b = cut[k + 1];
-    std::vector<char>& pb = piece[k];
-    pb.resize(std::max<size_t>(4096, (b - a) * 1400));
+    RenderPiece& pc = g_pieces[k];
+    size_t want = std::max<size_t>(4096, (b - a) * 1400);
     for (;;) {
+      if (pc.cap < want) {
+        pc.b.reset(new char[want]);  // (not zero-filled)
+        pc.cap = want;
+      }
       const int64_t r = gome_render_events(ev + a, b - a, batch, batch_n, seq_base, accuracy, sym_names, n_sym,
-                                           uuid_names, n_uuid, oid_names, n_oid, tx_table, pb.data(), pb.size());
+                                           uuid_names, n_uuid, oid_names, n_oid, tx_table, pc.b.get(), pc.cap);
       if (r == INT64_MIN || r >= 0) {
-        got[k] = r;
+        pc.got = r;
         return;
       }
-      pb.resize(static_cast<size_t>(-r) + 1);
+      want = static_cast<size_t>(-r) + 1;
     }
   };
-  std::vector<std::thread> th;
-  for (uint32_t k = 1; k < t; ++k) th.emplace_back(work, k);
-  work(0);
-  for (auto& x : th) x.join();
-  size_t total = 0;
+  gome_host::Pool::get().run(t, render);
+  std::vector<size_t> at(t + 1, 0);
   for (uint32_t k = 0; k < t; ++k) {
-    if (got[k] == INT64_MIN) return INT64_MIN;
-    total += static_cast<size_t>(got[k]);
+    if (g_pieces[k].got == INT64_MIN) return INT64_MIN;
+    at[k + 1] = at[k] + static_cast<size_t>(g_pieces[k].got);
   }
+  const size_t total = at[t];
   if (total + 1 > cap) return -static_cast<int64_t>(total + 1);
-  size_t at = 0;
-  for (uint32_t k = 0; k < t; ++k) {
-    std::memcpy(buf + at, piece[k].data(), static_cast<size_t>(got[k]));
-    at += static_cast<size_t>(got[k]);
-  }
-  buf[at] = 0;
+  gome_host::Pool::get().run(t, [&](uint32_t k) {
+    std::memcpy(buf + at[k], g_pieces[k].b.get(), static_cast<size_t>(g_pieces[k].got));
+  });
+  buf[total] = 0;
   return static_cast<int64_t>(total);
 }

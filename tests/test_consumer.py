@@ -413,3 +413,35 @@ def test_consumer_through_router_matches_literal_gpu(world):
     lit_out, got, cons = _run(_schedule(500 + world, n_ops=1500), r, True)
     assert len(lit_out) > 100 and got == lit_out
     r.close()
+
+
+def _stream_ops(seed, n=6000):
+    """A queue of doOrder messages with every marker set before consumption (no interleaving)."""
+    ops = [op for op in _schedule(seed, n_ops=n) if op[0] != "take"]
+    return ops + [("take", 10**9)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("packed", [False, True])
+def test_consumer_pipelined_stream_matches_literal_gpu(packed):
+    """process_stream (two batches in flight, records straight into page-locked buffers, MatchResults
+    rendered as each batch is collected) publishes exactly the literal reference's bytes, from a
+    list of bodies or from one packed delivery buffer (PackedQueue)."""
+    from gome_amd.abi import Engine
+    from gome_amd.consumer import PackedQueue
+    lit_out, _, _ = _run(_stream_ops(300), _OracleEngine(3, 64), True)
+    lit = GomeLiteral()
+    pre, sink, names = PrePool(), MatchSink(), Names()
+    q = []
+    for op, arg in _stream_ops(300)[:-1]:
+        if op == "add":
+            lit.grpc_do_order(arg)
+            pre.set(arg["symbol"], arg["uuid"], arg["oid"])
+        else:
+            lit.grpc_delete_order(arg)
+        q.append(lit.do_order_q[-1])
+    cons = BatchingConsumer(Engine(max_symbols=3, max_batch=256), pre, sink, names, max_batch=256)
+    batches = PackedQueue(q).batches(256) if packed else (q[k:k + 256] for k in range(0, len(q), 256))
+    n = cons.process_stream(batches)
+    assert n == len(lit_out) and sink.q == lit_out
+    assert cons.consumed == len(q) and len(pre) == 0

@@ -256,13 +256,14 @@ def cpu_baseline(batches, n_symbols, budget_s, threads=1):
 
 
 def consumer_leg(workload, n_symbols, n_msgs, seed, batch=1 << 15, threads=8):
-    """The drop-in boundary's own rate: n_msgs doOrder messages (the OrderNode
-    JSON bodies the gRPC side enqueues, main.go:39-52 / ordernode.go:9-36, admission markers set) of
-    the same workload through BatchingConsumer.process -- native Go-Unmarshal decode on `threads`
-    threads, fixed-point conversion, interning, admission (gome_consume_order_nodes),
-    gome_submit_batch, drain, gome_render_events_mt into MatchResult lines on the sink
-    (rabbitmq.go:116-125, engine.go:154-194); then the renderer alone over the same events at 1 and
-    `threads` threads."""
+    """The drop-in boundary's own rate: n_msgs doOrder messages (the
+    OrderNode JSON bodies the gRPC side enqueues, main.go:39-52 / ordernode.go:9-36, admission markers
+    set) of the same workload through BatchingConsumer.process_stream -- native Go-Unmarshal decode on
+    `threads` threads, fixed-point conversion, interning, admission (gome_consume_order_nodes), two
+    batches in flight on the engine (gome_submit_batch_async / gome_collect), gome_render_events_mt
+    into MatchResult lines on the sink (rabbitmq.go:116-125, engine.go:154-194); then the same
+    messages through process() as Python objects (round 5's leg) and the renderer alone over the
+    same events at 1 and `threads` threads."""
     import ctypes as C
     from gome_amd.abi import Engine
     from gome_amd.consumer import BatchingConsumer, MatchSink, Names, PrePool, _order_node_json
@@ -279,37 +280,65 @@ def consumer_leg(workload, n_symbols, n_msgs, seed, batch=1 << 15, threads=8):
     eng = Engine(max_symbols=n_symbols, max_batch=batch, max_nodes=2 * n_msgs + (1 << 20),
                  max_levels=(1 << 22) + 2 * n_msgs)
     cons = BatchingConsumer(eng, pre, sink, names, max_batch=batch, threads=threads)
+    # the deliveries as one buffer of bodies + offsets (how an AMQP client reads them off its socket;
+    # PackedQueue), two batches in flight (process_stream: decode and H2D of batch k+1 beside the
+    # device's batch k, each batch rendered as it is collected)
+    from gome_amd.consumer import PackedQueue
+    packed = PackedQueue(msgs)
+    t = time.perf_counter()
+    lines = cons.process_stream(packed.batches(batch))
+    wall = time.perf_counter() - t
+    phases = {k: round(v * 1e3, 2) for k, v in cons.phase_s.items()}
+    # the same messages as Python bytes objects through process(), one synchronous batch at a time
+    # (round 5's leg), on a fresh engine and pre-pool with the same markers
+    pre2, sink2, names2 = PrePool(), MatchSink(), Names()
+    for r in rec:
+        if r["action"] == wl.ADD:
+            pre2.set("s%d" % r["symbol_id"], str(int(r["uuid_id"])), str(int(r["oid_id"])))
+    eng2 = Engine(max_symbols=n_symbols, max_batch=batch, max_nodes=2 * n_msgs + (1 << 20),
+                  max_levels=(1 << 22) + 2 * n_msgs)
+    cons2 = BatchingConsumer(eng2, pre2, sink2, names2, max_batch=batch, threads=threads)
     evs, recs, bases = [], [], []
-    orig_render = cons.render_block
+    orig_render = cons2.render_block
 
-    def keep(ev, rc, base):  # (the events of each batch, for the render-only pass)
+    def keep(ev, rc, base):  # (the events of each batch, for the render-only pass below)
         evs.append(ev.copy())
         recs.append(rc.copy())
         bases.append(base)
         return orig_render(ev, rc, base)
-    cons.render_block = keep
-    t = time.perf_counter()
-    lines = 0
+    cons2.render_block = keep
+    t2 = time.perf_counter()
+    lines2 = 0
     for k in range(0, n_msgs, batch):
-        lines += cons.process(msgs[k:k + batch])
-    wall = time.perf_counter() - t
+        lines2 += cons2.process(msgs[k:k + batch])
+    wall2 = time.perf_counter() - t2
+    same = lines2 == lines and sink2.q == sink.q
+    eng2.close()
     lib = cons.lib
-    N = names
+    N = names2
     nev = sum(len(e) for e in evs)
     out = {"messages": n_msgs, "batch": batch, "messages_per_s": round(n_msgs / wall, 1),
            "matchresults_per_s": round(lines / wall, 1), "matchresults": lines, "threads": threads,
-           "path": "OrderNode JSON bytes -> BatchingConsumer.process (gome_consume_order_nodes: decode, convert, "
-                   "intern, admit; gome_submit_batch, drain, gome_render_events_mt) -> MatchResult lines on the sink",
+           "path": "OrderNode JSON deliveries (one buffer + offsets) -> BatchingConsumer.process_stream "
+                   "(gome_consume_order_nodes: decode, convert, intern, admit into page-locked records; "
+                   "gome_submit_batch_async, two batches in flight; gome_collect; gome_render_events_mt "
+                   "straight into the sink's block) -> MatchResult lines on the sink",
+           "host_ms": phases,
+           "list_messages_per_s": round(n_msgs / wall2, 1),
+           "list_path": "the same messages as Python bytes objects through BatchingConsumer.process, one "
+                        "synchronous batch at a time (packing included); sink bytes identical: " + str(same),
            "render_events_per_s": {}}
+    cap = max(1 << 20, 1400 * max((len(e) for e in evs), default=0))
+    rbuf = np.empty(cap, np.uint8)
+    rbuf[::4096] = 0  # (its pages touched once, outside the timing)
     for th in (1, threads):
         nbytes = 0
         t = time.perf_counter()
         for ev, rc, base in zip(evs, recs, bases):
-            cap = max(1 << 20, 1400 * len(ev))
-            buf = C.create_string_buffer(cap)
             k = lib.gome_render_events_mt(ev.ctypes.data, len(ev), rc.ctypes.data, len(rc), base, 8,
                                           N.table("sym"), N.count("sym"), N.table("uuid"), N.count("uuid"),
-                                          N.table("oid"), N.count("oid"), N.tx_array().ctypes.data, th, buf, cap)
+                                          N.table("oid"), N.count("oid"), N.tx_array().ctypes.data, th,
+                                          rbuf.ctypes.data, cap)
             assert k >= 0
             nbytes += k
         dt = time.perf_counter() - t

@@ -336,6 +336,9 @@ class BatchingConsumer:
         self.max_symbols = getattr(engine, "max_symbols", None)
         self.seq = 0
         self.consumed = self.rejected = self.batches = self.dups = 0
+        # process_stream's host time per phase (s): decode + admission, submit, collect (waits for
+        # the device), render
+        self.phase_s = {"records": 0.0, "submit": 0.0, "collect": 0.0, "render": 0.0}
 
     # ---- draining ------------------------------------------------------------------
     def drain(self, q, block_s: float = 0.0) -> list:
@@ -441,20 +444,29 @@ class BatchingConsumer:
         flight = deque()  # (records, seq base, messages)
         total, slot = 0, 0
 
+        ph = self.phase_s
+        clk = time.perf_counter
+
         def finish():
             rec, base, nm = flight.popleft()
+            t0 = clk()
             ev, st = self.eng.collect(copy=False)
+            t1 = clk()
             self.dups += int(st["n_dup_oid"])
             if len(ev):
                 self.sink.publish_block(self.render_block(ev, rec, base), len(ev))
                 self.batches += 1
+            ph["collect"] += t1 - t0
+            ph["render"] += clk() - t1
             return len(ev)
 
         for msgs in batches:
             n = (len(msgs[1]) - 1) if isinstance(msgs, tuple) else len(msgs)
             if n > self.max_batch:
                 raise GomeError(1, "batch larger than the engine's max_batch")
+            t0 = clk()
             rec = self.records(msgs, out=ring[slot][:n])
+            t1 = clk()
             slot = (slot + 1) % len(ring)
             base = self.seq
             if len(rec):
@@ -464,6 +476,8 @@ class BatchingConsumer:
                     self.pre.abort()
                     raise
             self.pre.commit()
+            ph["records"] += t1 - t0
+            ph["submit"] += clk() - t1
             self.consumed += n
             if len(rec):
                 self.seq += len(rec)

@@ -432,60 +432,74 @@ class BatchingConsumer:
     def process_stream(self, batches, depth: int = 2) -> int:
         """Apply drained batches in order with up to `depth` of them in flight on the engine
         (gome_submit_batch_async / gome_collect): batch k+1's decode, admission and H2D run while
-        the device applies batch k, and each batch's MatchResults are rendered as it is collected.
-        Publishes exactly what process() would, batch after batch (the markers of a batch are
-        committed when the engine took it, as there).  Engines without the async calls (test
-        doubles) take process() per batch."""
+        the device applies batch k, and batch k's MatchResults are rendered (on the renderer's own
+        worker pool, by a helper thread) while batch k+2 is decoded.  Publishes exactly what
+        process() would, batch after batch (the markers of a batch are committed when the engine
+        took it, as there).  The engine handle is only ever called from this thread.  Engines
+        without the async calls (test doubles) take process() per batch."""
         if not hasattr(self.eng, "submit_async"):
             return sum(self.process(b) for b in batches)
         from collections import deque
+        from concurrent.futures import ThreadPoolExecutor
         depth = max(1, min(depth, 3))
-        ring = [self.eng.host_buffer(self.max_batch) for _ in range(depth + 1)]
-        flight = deque()  # (records, seq base, messages)
-        total, slot = 0, 0
-
+        # records stay valid until their batch is rendered: depth in flight, one rendering, one new
+        ring = [self.eng.host_buffer(self.max_batch) for _ in range(depth + 2)]
+        flight = deque()  # (records, seq base)
         ph = self.phase_s
         clk = time.perf_counter
+        total, slot, pending = 0, 0, None
 
-        def finish():
-            rec, base, nm = flight.popleft()
+        def render(ev, rec, base):  # (helper thread: the events' buffer stays valid until the next collect)
+            t0 = clk()
+            self.sink.publish_block(self.render_block(ev, rec, base), len(ev))
+            ph["render"] += clk() - t0
+
+        def finish(ex):
+            nonlocal pending
+            rec, base = flight.popleft()
+            if pending is not None:  # (the last render must be done before the next collect)
+                pending.result()
+                pending = None
             t0 = clk()
             ev, st = self.eng.collect(copy=False)
-            t1 = clk()
+            ph["collect"] += clk() - t0
             self.dups += int(st["n_dup_oid"])
             if len(ev):
-                self.sink.publish_block(self.render_block(ev, rec, base), len(ev))
                 self.batches += 1
-            ph["collect"] += t1 - t0
-            ph["render"] += clk() - t1
+                pending = ex.submit(render, ev, rec, base)
             return len(ev)
 
-        for msgs in batches:
-            n = (len(msgs[1]) - 1) if isinstance(msgs, tuple) else len(msgs)
-            if n > self.max_batch:
-                raise GomeError(1, "batch larger than the engine's max_batch")
-            t0 = clk()
-            rec = self.records(msgs, out=ring[slot][:n])
-            t1 = clk()
-            slot = (slot + 1) % len(ring)
-            base = self.seq
-            if len(rec):
-                try:
-                    self.eng.submit_async(rec, seq_base=base)
-                except BaseException:
-                    self.pre.abort()
-                    raise
-            self.pre.commit()
-            ph["records"] += t1 - t0
-            ph["submit"] += clk() - t1
-            self.consumed += n
-            if len(rec):
-                self.seq += len(rec)
-                flight.append((rec, base, n))
-            while len(flight) >= depth:
-                total += finish()
-        while flight:
-            total += finish()
+        with ThreadPoolExecutor(max_workers=1) as ex:
+            try:
+                for msgs in batches:
+                    n = (len(msgs[1]) - 1) if isinstance(msgs, tuple) else len(msgs)
+                    if n > self.max_batch:
+                        raise GomeError(1, "batch larger than the engine's max_batch")
+                    t0 = clk()
+                    rec = self.records(msgs, out=ring[slot][:n])
+                    t1 = clk()
+                    slot = (slot + 1) % len(ring)
+                    base = self.seq
+                    if len(rec):
+                        try:
+                            self.eng.submit_async(rec, seq_base=base)
+                        except BaseException:
+                            self.pre.abort()
+                            raise
+                    self.pre.commit()
+                    ph["records"] += t1 - t0
+                    ph["submit"] += clk() - t1
+                    self.consumed += n
+                    if len(rec):
+                        self.seq += len(rec)
+                        flight.append((rec, base))
+                    while len(flight) >= depth:
+                        total += finish(ex)
+                while flight:
+                    total += finish(ex)
+            finally:
+                if pending is not None:
+                    pending.result()
         return total
 
     def poll(self, q, block_s: float = 0.0) -> int:

@@ -394,6 +394,7 @@ struct gome_engine {
   // blocks of the tail's per-touch kernels (4096 measured 5% faster than 1024 on config 2)
   static constexpr uint32_t tail_grid = 4096;
   bool cold_main = false;  // k_match on the caller's stream (fewer than 8 hardware queues; default: the copy stream)
+  bool q4 = false;         // 4 to 7 hardware queues: cold_main, and the early plan on a fourth stream
   bool copy_busy = false;  // the batch being enqueued came by gome_submit_batch_async (H2D / D2H on the copy stream)
   // GOME_PH_* timing events (gome_stats.ms_phase): ~24 event records per batch, 0.12 ms on config 2's
   // critical path, so only on request (GOME_FLAG_PHASES)
@@ -667,7 +668,13 @@ gome_status gome_engine::init(const gome_config& c) {
   // stay on the caller's stream and there is no early plan, no admission ahead and no plan stream
   hw_queues = cfg.hw_queues ? cfg.hw_queues : env_hw_queues();
   cold_main = hw_queues < 8;
-  early_on = !cold_main && !(cfg.flags & GOME_FLAG_NO_EARLY);
+  // four hardware queues (HIP's default, a host that does not raise GPU_MAX_HW_QUEUES): the caller's,
+  // flow and hot streams, and the early plan on a fourth stream created right after them, so it
+  // takes the fourth queue (streams beyond the count share queues, tools/queue_map.hip; the later
+  // copy streams share with these, and carry work only on the host path).  Its record work and the
+  // plan go on that one stream, the cold books on the caller's.
+  q4 = cold_main && hw_queues >= 4;
+  early_on = (!cold_main || q4) && !(cfg.flags & GOME_FLAG_NO_EARLY);
   adm_ahead_on = !cold_main && !(cfg.flags & GOME_FLAG_NO_ADM_AHEAD);
   {
     int ncu = 0;
@@ -685,8 +692,14 @@ gome_status gome_engine::init(const gome_config& c) {
     }
   }
   HIPCHK(new_stream(&stream));
-  HIPCHK(new_stream(&hot_stream));
-  HIPCHK(new_stream(&flow_stream));
+  if (q4) {  // (creation order decides which streams share a hardware queue)
+    HIPCHK(new_stream(&flow_stream));
+    HIPCHK(new_stream(&hot_stream));
+    if (early_on) HIPCHK(new_stream(&early_stream));
+  } else {
+    HIPCHK(new_stream(&hot_stream));
+    HIPCHK(new_stream(&flow_stream));
+  }
   HIPCHK(new_stream(&copy_stream));
   HIPCHK(new_stream(&d2h_stream));
   HIPCHK(new_stream(&h2d_stream));
@@ -845,7 +858,7 @@ gome_status gome_engine::init(const gome_config& c) {
     return GOME_E_CAPACITY;
   for (XBuf& X : xb) HIPCHK(hipMemsetAsync(X.ctl, 0, sizeof(XCtl), stream));
   HIPCHK(hipMemsetAsync(x_dslot, 0, 4, stream));  // (the early deep book is deep slot 0's)
-  if (early_on || adm_ahead_on) HIPCHK(new_stream(&early_stream));
+  if ((early_on || adm_ahead_on) && !early_stream) HIPCHK(new_stream(&early_stream));
   // books with DELs (match_flow_cancel.h): per-position scratch, the (symbol, oid)
   // table (generation-tagged: cleared once per 2048 batches)
   fc_hcap = next_pow2(std::max<unsigned long long>(2ull * nb, 1024));
@@ -1031,8 +1044,8 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
     // (pipelined host batches: the record work on the copy stream right behind the batch's H2D, the
     // plan on the early stream, so the copy stream stays free for the copies)
     // (GOME_PLAN_CUS: the part after plan_done on the plan's own stream, which then needs no hop)
-    hipStream_t es = copy_busy ? copy_stream : early_stream;
-    hipStream_t ps = plan_stream ? plan_stream : copy_busy ? early_stream : copy_stream;
+    hipStream_t es = (copy_busy && !q4) ? copy_stream : early_stream;
+    hipStream_t ps = plan_stream ? plan_stream : (copy_busy || q4) ? early_stream : copy_stream;
     Dev Dx = D;
     Dx.st = reinterpret_cast<Status*>(reinterpret_cast<char*>(X.ctl) + offsetof(XCtl, st));
     BatchArgs Bx{};
@@ -1429,7 +1442,7 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   // and 16 hardware queues (config 2: 2.3 -> 3.6 ms per batch).  A batch with an early
   // plan keeps the copy stream for it and runs the cold books on the early stream (A/B: config 3
   // +0.3..0.7%, config 5 even).  Fewer than 8 hardware queues (cold_main): the caller's stream
-  hipStream_t cst = (early && !copy_busy) ? early_stream : (cold_main || copy_busy || early) ? s : copy_stream;
+  hipStream_t cst = cold_main ? s : (early && !copy_busy) ? early_stream : (copy_busy || early) ? s : copy_stream;
   if (cst != s) HIPCHK(hipStreamWaitEvent(cst, prep_t, 0));
   HIPCHK(hipEventRecord(S.evc0, cst));
   k_match<<<std::min<uint32_t>(ceil_div(grid, COLD_WAVES), COLD_BLOCKS), 64 * COLD_WAVES, COLD_LDS_BYTES, cst>>>(

@@ -372,7 +372,7 @@ extern "C" int64_t gome_render_events_mt(const gome_event* ev, size_t n, const g
       want = static_cast<size_t>(-r) + 1;
     }
   };
-  gome_host::Pool::get().run(t, render);
+  gome_host::Pool::get(1).run(t, render);
   std::vector<size_t> at(t + 1, 0);
   for (uint32_t k = 0; k < t; ++k) {
     if (g_pieces[k].got == INT64_MIN) return INT64_MIN;
@@ -380,7 +380,7 @@ extern "C" int64_t gome_render_events_mt(const gome_event* ev, size_t n, const g
   }
   const size_t total = at[t];
   if (total + 1 > cap) return -static_cast<int64_t>(total + 1);
-  gome_host::Pool::get().run(t, [&](uint32_t k) {
+  gome_host::Pool::get(1).run(t, [&](uint32_t k) {
     std::memcpy(buf + at[k], g_pieces[k].b.get(), static_cast<size_t>(g_pieces[k].got));
   });
   buf[total] = 0;

@@ -21,9 +21,11 @@ class Pool {
  public:
   static constexpr uint32_t MAX_WORKERS = 63;
 
-  static Pool& get() {
-    static Pool p;  // (joined at exit: the destructor stops the workers)
-    return p;
+  // Two pools: 0 for the decode and admission (consume.cpp), 1 for the render (host.cpp), so a
+  // consumer can render batch k while it decodes batch k + 1 (BatchingConsumer.process_stream).
+  static Pool& get(int which = 0) {
+    static Pool p[2];  // (joined at exit: the destructors stop the workers)
+    return p[which & 1];
   }
 
   void run(uint32_t n, const std::function<void(uint32_t)>& fn) {

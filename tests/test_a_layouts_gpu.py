@@ -3,7 +3,8 @@ size (tests/layout_check.py says what each leg runs).
 
 * the four-queue layout in a fresh process whose HIP runtime really has 4 hardware queues
   (GPU_MAX_HW_QUEUES=4, what a host that does not set the variable gets): started before this
-  process touches the GPU (the file name sorts first);
+  process touches the GPU (the file name sorts first); since round 6 it plans the hottest book
+  early on a fourth stream of its own;
 * the same layout chosen by gome_config.hw_queues = 4 in this process (16 real queues: the layout's
   own event dependencies, without the serialisation a shared queue adds);
 * no reserved plan CUs (gome_config.plan_cus < 0: the layout of a host beside RCCL);
@@ -27,6 +28,12 @@ def _no_early(res):
     return all(x == 0 for leg in res.values() if isinstance(leg, dict) for x in leg.get("early", []) + leg.get("adm_ahead", []))
 
 
+def _four_queue(res):
+    """The four-queue layout (round 6): the early plan on its own fourth stream, no admission ahead."""
+    return (sum(res["config3_device"]["early"]) >= 2 and sum(res["config3_host"]["early"]) >= 1 and
+            all(x == 0 for leg in res.values() if isinstance(leg, dict) for x in leg.get("adm_ahead", [])))
+
+
 def test_four_hw_queues_in_a_fresh_process():
     env = dict(os.environ, GPU_MAX_HW_QUEUES="4", GOME_HW_QUEUES="4", OMP_NUM_THREADS="4")
     r = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "layout_check.py")], cwd=ROOT, env=env,
@@ -34,14 +41,14 @@ def test_four_hw_queues_in_a_fresh_process():
     assert r.returncode == 0, r.stderr[-4000:]
     res = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
     assert res["hw_queues"] == 4 and res["GPU_MAX_HW_QUEUES"] == "4", res
-    assert _no_early(res), res  # (the four-stream layout: no early plan, no admission ahead)
+    assert _four_queue(res), res
     assert min(res["config4_device"]["flow_cancels"]) > 100000, res
 
 
 def test_four_queue_layout_by_config():
     from tests.layout_check import check_layout
     res = check_layout(dict(hw_queues=4), "hw_queues=4")
-    assert _no_early(res), res
+    assert _four_queue(res), res
 
 
 def test_no_plan_cus_layout():

@@ -3225,7 +3225,7 @@ __global__ __launch_bounds__(64) void k_flow_zero_check(Dev D, FlowArgs F) {
   int64_t run = d0;          // the level's depth before the chunk
   int64_t rr = d0, cc = 0;   // arrival end and consumption cursor before the chunk (volume coordinates)
   int64_t zlast = -1;        // start of the latest zero-volume maker rested before the chunk (-1: none)
-  bool zero = Lq->z0 != 0;   // cancel books: a zero-volume maker may be in the FIFO before the chunk
+  int64_t wlast = -1;        // cancel books: the latest reach point of a zero-volume maker (below)
   bool haz = false;
   for (uint32_t c0 = 0; c0 < cnt; c0 += 64) {
     const uint32_t i = c0 + lane;
@@ -3234,14 +3234,27 @@ __global__ __launch_bounds__(64) void k_flow_zero_check(Dev D, FlowArgs F) {
     if (valid) e = R[i];
     const bool isr = valid && e.kind == TK_REST, isc = valid && e.kind == TK_CONS, zr = isr && e.amt == 0;
     const bool isx = valid && e.kind == TK_CANC;
-    int64_t tot, tz, tr, tc, tzm;
+    int64_t tot, tr, tc, tzm;
     const int64_t before = run + fl_wave_excl(isr ? e.amt : (isc || isx) ? -e.amt : 0, &tot);
-    const int64_t zb = fl_wave_excl(zr ? 1 : 0, &tz);
     const int64_t rb = rr + fl_wave_excl(isr ? e.amt : 0, &tr);  // this REST's start
     const int64_t cb = cc + fl_wave_excl(isc ? e.amt : 0, &tc);  // this CONS's cursor
     const int64_t zm = max(zlast, fl_wave_max_excl(zr ? rb : -1, &tzm));
-    if (canc) {  // cancel books: any consume after a zero-volume maker may be in the FIFO
-      haz = haz || (zr && before == 0) || (isc && (zero || zb > 0 || e.amt == 0));
+    if (canc) {
+      // Cancel books (round 6: their reconstruction pops zero-volume makers, fc_fills).  A
+      // zero-volume maker rested at depth D after C of the level was consumed is reached once the
+      // consumption passes W = C + D: exactly in consumption space when no cancel removes volume
+      // ahead of it, an upper bound otherwise (a cancel may hit a maker behind it).  A consume or
+      // cancel that empties the level while some W >= the consumption after it (the maker may still
+      // be in the FIFO: the reference leaves it in a FIFO whose level left its set, or the taker
+      // pops it at the level's end) is a hazard, and so are a REST of 0 at depth 0 and a CONS of 0
+      // (a zero-volume taker, whose 0-fill the cancel events do not model).  Old zero-volume makers:
+      // W = d0.
+      int64_t twm;
+      const int64_t wm = max(wlast, fl_wave_max_excl(zr ? before + cb : -1, &twm));
+      const int64_t cend = cb + (isc ? e.amt : 0);
+      const bool present = (Lq->z0 && d0 >= cend) || wm >= cend;
+      haz = haz || (zr && before == 0) || (isc && e.amt == 0) || ((isc || isx) && before - e.amt == 0 && present);
+      wlast = max(wlast, twm);
     } else {
       // ADD books: a zero-volume maker is in the FIFO until a consume passes its start (an old
       // one: until the cursor passes the old FIFO's end).  A consume that leaves depth > 0 pops the
@@ -3256,7 +3269,6 @@ __global__ __launch_bounds__(64) void k_flow_zero_check(Dev D, FlowArgs F) {
     rr += tr;
     cc += tc;
     zlast = max(zlast, tzm);
-    zero = zero || tz > 0;
   }
   if (__ballot(haz) && lane == 0) atomicOr(&hd->haz, 1u);
 }

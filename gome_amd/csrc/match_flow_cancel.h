@@ -1106,7 +1106,7 @@ __device__ __forceinline__ void fc_level_one(const Dev& D, const FlowArgs& F, ui
   const uint32_t nv0 = uni(Lq->nv0), tail = uni(Lq->tail), tslot = uni(Lq->tslot);
   uint32_t head = uni(Lq->head), hslot = uni(Lq->hslot);
   uint32_t ttail = tail, ttslot = tslot;
-  uint32_t ig_base = 0, ng = 0, consumed = 0;
+  uint32_t ig_base = 0, ng = 0, consumed = 0, zpopped = 0;
   bool ig_all = true;
   if (nv0 > 0 && (cfin > 0 || uni(Lq->c_old))) {
     uint32_t bb = 0;
@@ -1153,11 +1153,14 @@ __device__ __forceinline__ void fc_level_one(const Dev& D, const FlowArgs& F, ui
       }
       ng += __popcll(tm);
       // fully consumed (uncancelled) makers leave with their index entries
-      const bool cons = live && ct == NIL && em + nd.rem <= cfin;
+      // (a zero-volume maker (Q6) is popped only strictly before the consumption end, as the ADD
+      // path's gather: engine.go:145-161 pops it with a 0-fill when the taker goes on)
+      const bool cons = live && ct == NIL && em + nd.rem <= cfin && (nd.rem > 0 || em < cfin);
       if (cons) __hip_atomic_store(&D.idx[nd.ixs].key, KEY_TOMB, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       consumed += __popcll(__ballot(cons));
+      zpopped += __popcll(__ballot(cons && nd.rem == 0));
       if (!have_surv) {
-        const unsigned long long sv = __ballot(live && ct == NIL && em + nd.rem > cfin);
+        const unsigned long long sv = __ballot(live && ct == NIL && !cons);
         if (sv) {
           have_surv = true;
           nh = c;
@@ -1212,6 +1215,7 @@ __device__ __forceinline__ void fc_level_one(const Dev& D, const FlowArgs& F, ui
     Lq->hslot = hslot;
     Lq->tslot = ttslot;
     Lq->nlive0 = nv0 - consumed - ncan_old;
+    Lq->zpop = zpopped;
     Lq->ocan = static_cast<uint32_t>(static_cast<uint64_t>(ocan) / g);
     Lq->pad0 = static_cast<uint32_t>(static_cast<uint64_t>(qend));
     Lq->pad1 = static_cast<uint32_t>(static_cast<uint64_t>(qend) >> 32);
@@ -1280,7 +1284,7 @@ __device__ __forceinline__ void fc_level_lane(const Dev& D, const FlowArgs& F, u
   const uint32_t nv0 = Lq->nv0, tail = Lq->tail, tslot = Lq->tslot;
   uint32_t head = Lq->head, hslot = Lq->hslot;
   uint32_t ttail = tail, ttslot = tslot;
-  uint32_t ig_base = 0, ng = 0, consumed = 0;
+  uint32_t ig_base = 0, ng = 0, consumed = 0, zpopped = 0;
   bool ig_all = true;
   if (nv0 > 0 && (cfin > 0 || Lq->c_old)) {
     ig_base = atomicAdd(F.ig_bump, nv0);
@@ -1327,12 +1331,13 @@ __device__ __forceinline__ void fc_level_lane(const Dev& D, const FlowArgs& F, u
           IG[ng++] = gq;
           if (em >= cfin && !targ) { taking = false; stop = true; ig_all = false; }
         }
-        const bool cons = ct == NIL && em + nd[s].rem <= cfin;
+        const bool cons = ct == NIL && em + nd[s].rem <= cfin && (nd[s].rem > 0 || em < cfin);  // (Q6 as above)
         if (cons) {
           __hip_atomic_store(&D.idx[nd[s].ixs].key, KEY_TOMB, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           consumed++;
+          if (nd[s].rem == 0) zpopped++;
         }
-        if (!have_surv && !surv_here && ct == NIL && em + nd[s].rem > cfin) {
+        if (!have_surv && !surv_here && ct == NIL && !cons) {
           surv_here = true;
           nh = c;
           nhs = s;
@@ -1365,6 +1370,7 @@ __device__ __forceinline__ void fc_level_lane(const Dev& D, const FlowArgs& F, u
   Lq->hslot = hslot;
   Lq->tslot = ttslot;
   Lq->nlive0 = nv0 - consumed - ncan_old;
+  Lq->zpop = zpopped;
   Lq->ocan = static_cast<uint32_t>(static_cast<uint64_t>(ocan) / g);
   Lq->pad0 = static_cast<uint32_t>(static_cast<uint64_t>(qend));
   Lq->pad1 = static_cast<uint32_t>(static_cast<uint64_t>(qend) >> 32);
@@ -1489,7 +1495,7 @@ __device__ __forceinline__ void fc_level_blk(const Dev& D, const FlowArgs& F, ui
   const uint32_t nv0 = Lq->nv0, tail = Lq->tail, tslot = Lq->tslot;
   uint32_t head = Lq->head, hslot = Lq->hslot;
   uint32_t ttail = tail, ttslot = tslot;
-  uint32_t ig_base = 0, ng = 0, consumed = 0;
+  uint32_t ig_base = 0, ng = 0, consumed = 0, zpopped = 0;
   bool ig_all = true;
   if (nv0 > 0 && (cfin > 0 || Lq->c_old)) {
     uint32_t bb = 0;
@@ -1535,11 +1541,14 @@ __device__ __forceinline__ void fc_level_blk(const Dev& D, const FlowArgs& F, ui
         IG[ng + __popcll(tm & ltm)] = gq;
       }
       ng += __popcll(tm);
-      const bool cons = live && ct == NIL && em + nd.rem <= cfin;
+      // (a zero-volume maker (Q6) is popped only strictly before the consumption end, as the ADD
+      // path's gather: engine.go:145-161 pops it with a 0-fill when the taker goes on)
+      const bool cons = live && ct == NIL && em + nd.rem <= cfin && (nd.rem > 0 || em < cfin);
       if (cons) __hip_atomic_store(&D.idx[nd.ixs].key, KEY_TOMB, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       consumed += __popcll(__ballot(cons));
+      zpopped += __popcll(__ballot(cons && nd.rem == 0));
       if (!have_surv) {
-        const unsigned long long sv = __ballot(live && ct == NIL && em + nd.rem > cfin);
+        const unsigned long long sv = __ballot(live && ct == NIL && !cons);
         if (sv) {
           have_surv = true;
           nh = c;
@@ -1573,6 +1582,7 @@ __device__ __forceinline__ void fc_level_blk(const Dev& D, const FlowArgs& F, ui
     Lq->hslot = hslot;
     Lq->tslot = ttslot;
     Lq->nlive0 = nv0 - consumed - ncan_s;
+    Lq->zpop = zpopped;
     Lq->ocan = static_cast<uint32_t>(static_cast<uint64_t>(ocan_t) / g);
     Lq->pad0 = static_cast<uint32_t>(static_cast<uint64_t>(qend));
     Lq->pad1 = static_cast<uint32_t>(static_cast<uint64_t>(qend) >> 32);
@@ -1632,6 +1642,10 @@ __device__ __forceinline__ FcTouch fc_touch(const FlowArgs& F, uint32_t h, uint3
   T.c = F.srt[L + x.pos].coord;
   T.a = x.amt;
   T.first = fc_find(T.V, T.c);
+  // a level that may hold zero-volume makers (Q6): the ones starting at the cursor are popped by
+  // this consume too (they share the start of the maker fc_find lands on; fl_first_back)
+  if ((T.Lq->z0 || F.hdr[h].nzero) && T.a > 0)
+    while (T.first > 0 && fc_start(T.V, T.first - 1) == T.c) --T.first;
   // the last maker: a touch spans a few makers, so step on from the first (neighbouring entries,
   // one cache line) before a second binary search (~16 dependent loads on a busy level); the
   // starts rise through the old makers into the new ones, so both give the last start <= x
@@ -1643,13 +1657,22 @@ __device__ __forceinline__ FcTouch fc_touch(const FlowArgs& F, uint32_t h, uint3
   return T;
 }
 
+// A maker of zero length in consumption space fills nothing (cancelled before any consumption),
+// except a zero-volume maker (Q6: volume 0, never cancelled in a flow batch -- its DEL is a hazard,
+// k_fc_resolve) that starts inside the consume [c, c + a): MatchOrder pops it with a 0-fill and
+// goes on (engine.go:145-161).
+__device__ __forceinline__ bool fc_fills(const FcLvlView& V, uint32_t m, int64_t c, int64_t a) {
+  if (fc_len(V, m) > 0) return true;
+  const int64_t e = fc_start(V, m);
+  return fc_vol(V, m) == 0 && e >= c && e < c + a;
+}
+
 // Fills of a consume touch: makers of [first, last] with volume in consumption space.
 __device__ __forceinline__ uint32_t fc_nfills(const FcTouch& T, uint32_t& pops) {
   uint32_t nf = 0;
   pops = 0;
   for (uint32_t m = T.first; m <= T.last; ++m) {
-    const int64_t len = fc_len(T.V, m);
-    if (len <= 0) continue;
+    if (!fc_fills(T.V, m, T.c, T.a)) continue;
     ++nf;
     if (fc_start(T.V, m) + fc_vol(T.V, m) <= T.c + T.a) ++pops;  // filled to its whole volume
   }
@@ -1789,8 +1812,8 @@ __global__ __launch_bounds__(256) void k_fc_events(Dev D, BatchArgs B, FlowArgs 
     const uint32_t fb = F.fbase[L + t];
     uint32_t k = 0;
     for (uint32_t m = T.first; m <= T.last; ++m) {
+      if (!fc_fills(V, m, T.c, T.a)) continue;
       const int64_t len = fc_len(V, m);
-      if (len <= 0) continue;
       const int64_t e = fc_start(V, m), v = fc_vol(V, m);
       uint32_t oid, uuid, tx;
       if (m < V.ig_n) {
@@ -1848,13 +1871,13 @@ __device__ __forceinline__ Level fc_write_level(const Dev& D, const BatchArgs& B
   // survivors among the new makers: not cancelled, not filled to the end (in FIFO order); a
   // maker starting before the consumption end keeps e + v - cfin
   uint32_t S = 0;
-  uint32_t zadd = 0;  // zero-volume makers appended (Q6; the cancel path pops none: k_flow_zero_check)
+  uint32_t zadd = 0;  // zero-volume makers appended (Q6; the old ones the batch popped: FlowLvl::zpop)
   for (uint32_t c0 = 0; c0 < V.nrest; c0 += 64) {
     const uint32_t i = c0 + lane;
     bool sv = false;
     if (i < V.nrest) {
       const RsEnt r = V.RS[i];
-      sv = r.pad0 == NIL && r.e + r.v > f.cfin;
+      sv = r.pad0 == NIL && (r.e + r.v > f.cfin || (r.v == 0 && r.e >= f.cfin));  // (Q6: as the gather)
     }
     S += __popcll(__ballot(sv));
     zadd += __popcll(__ballot(sv && i < V.nrest && V.RS[i].v == 0));
@@ -1894,7 +1917,7 @@ __device__ __forceinline__ Level fc_write_level(const Dev& D, const BatchArgs& B
     bool sv = false;
     if (i < V.nrest) {
       r = V.RS[i];
-      sv = r.pad0 == NIL && r.e + r.v > f.cfin;
+      sv = r.pad0 == NIL && (r.e + r.v > f.cfin || (r.v == 0 && r.e >= f.cfin));
     }
     const unsigned long long sm = __ballot(sv);
     if (sv) {
@@ -1934,7 +1957,7 @@ __device__ __forceinline__ Level fc_write_level(const Dev& D, const BatchArgs& B
   }
   x.depth = f.dfin;
   x.nlive = f.nlive0 + S;
-  x.pad = x.nlive ? l_zero_count(f.z0, 0u, zadd) : 0u;
+  x.pad = x.nlive ? l_zero_count(f.z0, f.zpop, zadd) : 0u;
   uint32_t mem = 0;
   if (hd.ok == FL_OK_DEEP) {
     mem = f.memf;

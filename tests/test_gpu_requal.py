@@ -26,7 +26,7 @@ def _run(mode, batches=5):
     hot = int(z.rank_to_id[0])
     eng = Engine(max_symbols=100000, max_batch=N, max_nodes=batches * N, max_levels=1 << 22)
     orc = Oracle(100000)
-    kinds, req, wrong = [], [], []
+    kinds, req, wrong, bails = [], [], [], []
     for i in range(batches):
         b = gen(N).copy()
         if i == 1:
@@ -40,19 +40,21 @@ def _run(mode, batches=5):
         kinds.append(int(fl["kind"][0]))
         req.append((st["n_quirk_checked"], st["n_requalified"]))
         wrong.append(int(st["n_flow_wrong"]))
+        bails.append(int(st["n_flow_bail"]))
     _cmp_books(eng, orc, _hot_and_random(z, 100000, k_rand=50), mode)
     assert eng.stats()["n_resting"] == orc.resting()
+    _run.bails = bails
     return kinds, req, wrong
 
 
 def test_quirks_heal_and_the_hottest_book_returns_to_the_flow_path():
     """The quirks at the best bids, where the stream soon trades: the injected batch's wrong-side
-    cancels run on the flow cancel path, and the zero-volume maker, which a taker soon reaches, hands
-    the book to the legacy kernel after its plan (k_flow_zero_check); k_requalify returns it to the
-    flow path once the reference's state has healed."""
+    cancels run on the flow cancel path, and the zero-volume maker, which the stream's SALEs reach
+    and pop with a 0-fill (engine.go:145-161), is popped by the cancel path's reconstruction too
+    (round 6, fc_fills): the book stays on the flow path in every batch, no hand-over, exact."""
     kinds, req, wrong = _run("heal")
     assert kinds[0] != 0 and wrong[1] >= 1, (kinds, wrong)
-    assert all(k != 0 for k in kinds[3:]), (kinds, req)
+    assert all(k != 0 for k in kinds) and sum(_run.bails) == 0, (kinds, _run.bails)
 
 
 def test_quirks_that_do_not_heal_stay_on_the_flow_path():
@@ -270,4 +272,54 @@ def test_zero_volume_maker_reached_hands_the_book_to_legacy():
         b["volume_fx"][rows[0]], b["side"][rows[0]], b["price_fx"][rows[0]] = 0, 0, bids["price_fx"][-1]
         b["volume_fx"][rows[1]], b["side"][rows[1]], b["price_fx"][rows[1]] = 10 ** 14, 1, 10 ** 6
     out = _zero_run(47, edit)
+    assert out[2][0] == 0 and out[2][2] >= 1, out
+
+
+def _del_of(b, row, eng, hot, price, k=0):
+    """Record `row` becomes a DEL of the k-th maker of the hot book's FIFO at `price` (delorder.go)."""
+    m = eng.fifo(hot, int(price))[k]
+    b["action"][row], b["flags"][row] = wl.DEL, 0
+    b["oid_id"][row], b["uuid_id"][row], b["side"][row] = m["oid_id"], m["uuid_id"], m["side"]
+    b["price_fx"][row], b["volume_fx"][row] = price, m["volume_fx"]
+
+
+def test_zero_volume_maker_popped_in_a_batch_with_dels_stays_on_the_flow_path():
+    """Round 6: the passing-taker case of the test above in a batch with DELs --
+    one of a maker at the lowest bid, one of the best bid's first maker, ahead of the zero-volume maker
+    (a cancel that moves it in consumption space) -- so the book takes the cancel path, whose
+    reconstruction now pops the zero-volume maker with a 0-fill (fc_fills, the gathers): exact, the
+    book on the flow path (kind != 0), no hand-over."""
+    def edit(b, hot, eng):
+        lv = eng.levels(hot)
+        bids = np.sort(lv[(lv["in_buy"] != 0) & (lv["n_nodes"] > 1)], order="price_fx")
+        best = bids[-1]
+        f = eng.fifo(hot, int(best["price_fx"]))
+        rows = _hot_rows(b, hot)[:5]
+        _del_of(b, rows[0], eng, hot, bids[0]["price_fx"])
+        _del_of(b, rows[1], eng, hot, best["price_fx"])            # (ahead of the zero-volume maker)
+        b["volume_fx"][rows[2]], b["side"][rows[2]], b["price_fx"][rows[2]] = 0, 0, best["price_fx"]
+        b["volume_fx"][rows[3]], b["side"][rows[3]], b["price_fx"][rows[3]] = 10 ** 8, 0, best["price_fx"]
+        left = int(best["depth_fx"]) - int(f[0]["volume_fx"])
+        b["volume_fx"][rows[4]], b["side"][rows[4]] = left + 5 * 10 ** 7, 1
+        b["price_fx"][rows[4]] = best["price_fx"]
+    out = _zero_run(49, edit)
+    assert out[2][0] != 0 and out[2][1] >= 1 and out[2][2] == 0, out
+    assert all(k != 0 for k, _, _ in out), out
+
+
+def test_zero_volume_maker_left_at_an_emptied_level_with_dels_hands_over():
+    """The hazard the cancel path keeps: a SALE that takes exactly the best bid's depth (every maker
+    ahead of the zero-volume one) in a batch with DELs empties the level with the zero-volume maker
+    still in its FIFO (the reference leaves it in a FIFO whose level left its set): k_flow_zero_check
+    hands the book to the legacy kernel after its plan, exact."""
+    def edit(b, hot, eng):
+        lv = eng.levels(hot)
+        bids = np.sort(lv[(lv["in_buy"] != 0) & (lv["n_nodes"] > 0)], order="price_fx")
+        best = bids[-1]
+        rows = _hot_rows(b, hot)[:3]
+        _del_of(b, rows[0], eng, hot, bids[0]["price_fx"])
+        b["volume_fx"][rows[1]], b["side"][rows[1]], b["price_fx"][rows[1]] = 0, 0, best["price_fx"]
+        b["volume_fx"][rows[2]], b["side"][rows[2]] = int(best["depth_fx"]), 1
+        b["price_fx"][rows[2]] = best["price_fx"]
+    out = _zero_run(50, edit)
     assert out[2][0] == 0 and out[2][2] >= 1, out

@@ -612,6 +612,12 @@ struct Interner {
   void prefetch(uint64_t h) const {
     if (!slot.empty()) __builtin_prefetch(&slot[h & mask]);
   }
+  // second stage (the slot is in cache by now): the string its first probe compares against
+  void prefetch2(uint64_t h) const {
+    if (slot.empty()) return;
+    const uint64_t v = slot[h & mask];
+    if (v && (v & ~0xFFFFFFFFull) == (h >> 32 << 32)) __builtin_prefetch(strs[static_cast<uint32_t>(v) - 1]);
+  }
   uint32_t intern(const char* s, size_t n) { return intern_h(s, n, hash_bytes(s, n)); }
   uint32_t intern_h(const char* s, size_t n, uint64_t h) {
     const int64_t f = find(s, n, h);
@@ -689,6 +695,11 @@ struct gome_prepool {
   int64_t find(const std::string& k, uint64_t h) const { return find(k.data(), k.size(), h); }
   void prefetch(uint64_t h) const {
     if (!tab.empty()) __builtin_prefetch(&tab[h & mask]);
+  }
+  void prefetch2(uint64_t h) const {  // (second stage: the key bytes of the slot's entry)
+    if (tab.empty()) return;
+    const Ent& x = tab[h & mask];
+    if (x.state != EMPTY && x.h == h) __builtin_prefetch(arena.data() + x.off);
   }
   void rebuild(uint64_t cap) {  // (drops tombstones and their key bytes)
     std::vector<Ent> old;
@@ -939,6 +950,16 @@ gome_status gome_consume_order_nodes(gome_names* nm, gome_prepool* pp, const cha
         nm->in[1].prefetch(q.hu);
         nm->in[2].prefetch(q.ho);
         pp->prefetch(q.hk);
+      }
+    }
+    if (i + PF / 2 < n) {  // (the strings and marker keys the probes of message i + PF / 2 compare)
+      const Dec& f = dec[i + PF / 2];
+      if (f.action == GOME_ADD || f.action == GOME_DEL) {
+        const Pre& q = pre[i + PF / 2];
+        nm->in[0].prefetch2(q.hs);
+        nm->in[1].prefetch2(q.hu);
+        nm->in[2].prefetch2(q.ho);
+        pp->prefetch2(q.hk);
       }
     }
     const Dec& d = dec[i];

@@ -406,7 +406,7 @@ def main():
     ap.add_argument("--force-pg", action="store_true",
                     help="initialise the process group and run the summary gather, the publisher and the "
                          "digest check at N = 1 too (exercises the RCCL path on a one-GPU box)")
-    ap.add_argument("--inject-quirks", choices=("none", "heal", "stuck", "q2heal", "q2stuck", "zero", "zeroheal"), default="none",
+    ap.add_argument("--inject-quirks", choices=("none", "heal", "stuck", "q2heal", "q2stuck", "zero", "zeroheal", "zerodel"), default="none",
                     help="rewrite records of the hottest book in the first timed batch into wrong-side "
                          "cancels (Q2) of a bid level and a zero-volume ADD (Q6), or (zero) zero-volume "
                          "ADDs only (workload.inject_quirks); "

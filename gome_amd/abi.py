@@ -155,6 +155,9 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.gome_render_events_mt.argtypes = [VP, C.c_size_t, VP, C.c_size_t, C.c_uint64, C.c_uint32, VP, C.c_size_t,
                                           VP, C.c_size_t, VP, C.c_size_t, VP, C.c_uint32, VP, C.c_size_t]
     lib.gome_render_events_mt.restype = C.c_int64
+    lib.gome_render_events_names.argtypes = [VP, C.c_size_t, VP, C.c_size_t, C.c_uint64, C.c_uint32, VP, C.c_uint32,
+                                             VP, C.c_size_t]
+    lib.gome_render_events_names.restype = C.c_int64
     # gome_host.h: interning, pre-pool markers, the native OrderNode consumer
     SZ, CP = C.c_size_t, C.c_char_p
     lib.gome_names_create.restype = VP

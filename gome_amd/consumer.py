@@ -385,15 +385,14 @@ class BatchingConsumer:
     def render_block(self, ev: np.ndarray, rec: np.ndarray, seq_base: int):
         """The batch's MatchResult lines (newline-terminated), rendered straight into a buffer of
         their own that the caller keeps (a memoryview; no copy of the block afterwards)."""
-        N = self.names
         cap = 1400 * len(ev) + (1 << 16)
         while True:
             out = np.empty(cap, np.uint8)
-            k = self.lib.gome_render_events_mt(
-                ev.ctypes.data, len(ev), rec.ctypes.data, len(rec), seq_base, self.acc,
-                N.table("sym"), N.count("sym"), N.table("uuid"), N.count("uuid"),
-                N.table("oid"), N.count("oid"), N.tx_array().ctypes.data, self.threads,
-                out.ctypes.data, cap)
+            # (the name tables are read under the names' lock: process_stream renders on a helper
+            # thread while this thread interns the next batch's names, which may move a table)
+            k = self.lib.gome_render_events_names(
+                ev.ctypes.data, len(ev), rec.ctypes.data, len(rec), seq_base, self.acc, self.names.h,
+                self.threads, out.ctypes.data, cap)
             if k >= 0:
                 return memoryview(out)[:k]
             if k == -(1 << 63):

@@ -10,6 +10,7 @@
 #include <cstring>
 #include <memory>
 #include <mutex>
+#include <shared_mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -569,7 +570,10 @@ inline uint64_t hash_bytes(const char* s, size_t n) {
 struct Interner {
   std::vector<std::unique_ptr<char[]>> blocks;
   size_t bused = 0, bcap = 0;
+  // by id; its reallocation (the only change a reader of older ids can see) happens under *gmu,
+  // which gome_render_events_names holds shared while it renders beside the next batch's decode
   std::vector<const char*> strs;
+  std::shared_mutex* gmu = nullptr;
   std::vector<uint32_t> lens;
   std::vector<uint64_t> hs;
   std::vector<uint64_t> slot;  // (id + 1) | tag << 32; 0 = empty
@@ -624,6 +628,10 @@ struct Interner {
     if (f >= 0) return static_cast<uint32_t>(f);
     if ((strs.size() + 1) * 2 > mask + 1) grow();
     const uint32_t id = static_cast<uint32_t>(strs.size());
+    if (strs.size() == strs.capacity()) {  // (the table moves: not while a render reads it)
+      std::unique_lock<std::shared_mutex> lk(*gmu);
+      strs.reserve(std::max<size_t>(1024, strs.capacity() * 2));
+    }
     strs.push_back(store(s, n));
     lens.push_back(static_cast<uint32_t>(n));
     hs.push_back(h);
@@ -640,8 +648,10 @@ struct gome_names {
   Interner in[3];
   int32_t tx_raw[GOME_TX_CODES];
   uint32_t tx_n = 2;
+  std::shared_mutex mu;  // the id tables' moves (Interner::gmu)
   gome_names() {
     for (int i = 0; i < GOME_TX_CODES; ++i) tx_raw[i] = i;
+    for (Interner& x : in) x.gmu = &mu;
   }
   int32_t tx_code(int32_t raw) {
     if (raw == 0 || raw == 1) return raw;
@@ -820,6 +830,22 @@ const char* const* gome_names_table(gome_names* nm, int kind) {
 }
 
 int32_t gome_names_tx_code(gome_names* nm, int32_t raw) { return nm ? nm->tx_code(raw) : -1; }
+
+int64_t gome_render_events_names(const gome_event* ev, size_t n, const gome_order* batch, size_t batch_n,
+                                 uint64_t seq_base, uint32_t accuracy, gome_names* nm, uint32_t threads, char* buf,
+                                 size_t cap) {
+  if (!nm) return INT64_MIN;
+  std::shared_lock<std::shared_mutex> lk(nm->mu);  // (the tables stay where they are meanwhile)
+  const char* const* t[3];
+  size_t c[3];
+  static const char* const empty[1] = {nullptr};
+  for (int k = 0; k < 3; ++k) {
+    c[k] = nm->in[k].strs.size();
+    t[k] = c[k] ? nm->in[k].strs.data() : empty;
+  }
+  return gome_render_events_mt(ev, n, batch, batch_n, seq_base, accuracy, t[0], c[0], t[1], c[1], t[2], c[2],
+                               nm->tx_raw, threads, buf, cap);
+}
 const int32_t* gome_names_tx_table(const gome_names* nm) { return nm ? nm->tx_raw : nullptr; }
 size_t gome_names_tx_count(const gome_names* nm) { return nm ? nm->tx_n : 0; }
 

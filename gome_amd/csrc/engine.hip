@@ -352,9 +352,10 @@ struct gome_engine {
   // the early plan of the hottest book (match_early.h): the last batch's plan done (flow stream),
   // its oid watermarks folded (hot stream), this batch's early prep and plan done (copy stream)
   hipEvent_t plan_done{}, oidmax_done{}, xpre_done{}, xprep_done{}, xplan_done{};
-  hipEvent_t xcmp_done{}, xtake_done{};  // k_x_cmp done (flow stream), k_x_take done (plan stream)
-  // the last enqueued batch's final F.hdr[0] / F.lvl writer (its plan or its early plan's k_x_take)
-  // ran on the plan stream: the next early chain there needs no plan_done (device batches only)
+  hipEvent_t xcmp_done{};  // k_x_cmp done (flow stream)
+  // the last enqueued batch's final F.hdr[0] / F.lvl writers (its plan, or its early plan's k_x_take and
+  // the fallback plan behind it) ran on the plan stream: the next early chain there needs no plan_done
+  // (device batches only)
   bool f_on_plan = false;
   struct XBuf {
     XCtl* ctl = nullptr;
@@ -509,7 +510,7 @@ struct gome_engine {
     }
     for (hipEvent_t ev : {fork, join, joinf, prep_h, prep_t, fork_adm, adm_done, seg_done, ho_fork, tfc_fork, tfc_done, sort_done, dp_fork, cnt_fork, cnt_done,
                           dw_done, dl_done, tl_done, tob_done, plan_done, oidmax_done, xpre_done, xprep_done,
-                          xplan_done, xcmp_done, xtake_done, adm_pre_done})
+                          xplan_done, xcmp_done, adm_pre_done})
       if (ev) (void)hipEventDestroy(ev);
     if (h_tob_syms) (void)hipHostFree(h_tob_syms);
     if (h_tob) (void)hipHostFree(h_tob);
@@ -705,7 +706,7 @@ gome_status gome_engine::init(const gome_config& c) {
   HIPCHK(new_stream(&h2d_stream));
   for (hipEvent_t* ev : {&fork, &join, &joinf, &prep_h, &prep_t, &fork_adm, &adm_done, &seg_done, &ho_fork, &tfc_fork, &tfc_done, &sort_done,
                          &dp_fork, &cnt_fork, &cnt_done, &dw_done, &dl_done, &tl_done, &tob_done, &plan_done,
-                         &oidmax_done, &xpre_done, &xprep_done, &xplan_done, &xcmp_done, &xtake_done, &adm_pre_done})
+                         &oidmax_done, &xpre_done, &xprep_done, &xplan_done, &xcmp_done, &adm_pre_done})
     HIPCHK(hipEventCreateWithFlags(ev, hipEventDisableTiming));
   for (Slot& S : slots) {
     for (hipEvent_t* ev : {&S.ev0, &S.ev1, &S.evm0, &S.evm1, &S.evh0, &S.evh1, &S.evf0, &S.evf1, &S.evc0, &S.evc1,
@@ -1072,10 +1073,9 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
     k_xd_sort_new<<<1, FL_PREP_T, DEEP_CAP * 8, es>>>(FX, X.ctl, x_dnew);
     HIPCHK(hipEventRecord(xpre_done, es));
     HIPCHK(hipStreamWaitEvent(ps, xpre_done, 0));
-    // On the plan's own stream the last batch's plan, or its early plan's k_x_take, wrote F.hdr[0] /
-    // F.lvl on this stream before: no hop through the flow stream (plan_done) between two plans.
-    // (An early plan not taken has its fallback plan on the flow stream, which this chain may then
-    // read half-written: k_x_cmp finds that and this early plan is not taken either.)
+    // On the plan's own stream the last batch's plan, or its early plan's k_x_take (and the fallback
+    // plan when that early plan was not taken), wrote F.hdr[0] / F.lvl on this stream before: no hop
+    // through the flow stream (plan_done) between two plans.
     // (Device batches only: on the host path, three batches in flight, every other batch's early
     // plan came 13 ms late without this wait, config 3's e2e 147.7 -> 120.7M, gpurun_out/r05cb.)
     if (!(ps == plan_stream && f_on_plan && !copy_busy)) HIPCHK(hipStreamWaitEvent(ps, plan_done, 0));
@@ -1273,8 +1273,6 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
       HIPCHK(hipEventRecord(xcmp_done, flow_stream));
       HIPCHK(hipStreamWaitEvent(plan_stream, xcmp_done, 0));
       k_x_take<<<32, 256, 0, plan_stream>>>(D, F, FX, X.ctl);
-      HIPCHK(hipEventRecord(xtake_done, plan_stream));
-      HIPCHK(hipStreamWaitEvent(flow_stream, xtake_done, 0));
     } else {
       HIPCHK(hipStreamWaitEvent(flow_stream, xplan_done, 0));
       k_x_take<<<32, 256, 0, flow_stream>>>(D, F, FX, X.ctl);
@@ -1282,12 +1280,17 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   }
   {
     hipStream_t pst = flow_stream;
-    // (a book planned early skips this launch, and with no dominant book the batch's critical path is
-    // the tail's chain: no hops for either)
+    // (with no dominant book the batch's critical path is the tail's chain: no hops for it.  A book
+    // planned early skips this launch; one whose early plan was not taken is planned here, on the
+    // plan stream right behind k_x_take, so whatever writes F.hdr[0] / F.lvl last — the take or this
+    // fallback — runs there before the next early chain reads them: ADVICE r5, the fallback used to
+    // run on the flow stream beside that chain.)
     if (plan_stream && !early && dominant) {
       HIPCHK(hipEventRecord(pl_fork, flow_stream));
       HIPCHK(hipStreamWaitEvent(plan_stream, pl_fork, 0));
       pst = plan_stream;
+    } else if (plan_stream && early && !copy_busy) {
+      pst = plan_stream;  // (behind k_x_take, which waited for k_x_cmp and so for the head prep)
     }
     HIPCHK(hipEventRecord(S.evf0, pst));
     k_flow_plan_head<<<1, 256, plan_lds, pst>>>(D, FH0);  // (a book planned early: nothing)
@@ -1296,7 +1299,7 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
       HIPCHK(hipEventRecord(pl_join, plan_stream));
       HIPCHK(hipStreamWaitEvent(flow_stream, pl_join, 0));
     }
-    f_on_plan = plan_stream && (pst == plan_stream || (early && !copy_busy));
+    f_on_plan = plan_stream && pst == plan_stream;
   }
   HIPCHK(hipEventRecord(plan_done, flow_stream));
   if (early) k_x_logcopy<<<1024, 256, 0, flow_stream>>>(F, FX, X.ctl);

@@ -148,13 +148,21 @@ struct FlowHdr {
   uint32_t bail;       // set with ok = 0 by k_flow_stale_check: the legacy kernel applies the book
   uint32_t nzero;      // admitted zero-volume ADDs of the segment (Q6, k_flow_zero_check)
   uint32_t nzlev;      // levels that may hold zero-volume makers at batch start (FlowLvl::z0)
-  uint32_t haz;        // k_flow_zero_check / k_fc_stale_level: a state the reconstruction cannot take
+  uint32_t haz;        // k_flow_zero_check / k_fc_stale_level / k_fc_resolve: a state the reconstruction
+                       // cannot take (HZ_* bits: which check found it; diagnostics read them)
   uint32_t nwrong;     // books with DELs: wrong-side cancels that find their maker (Q2, k_fc_resolve)
   uint32_t nlong;      // books with DELs: DELs with a long window (k_fc_precs -> k_fc_precs_long)
 };
+static_assert(offsetof(FlowHdr, haz) == 144, "FlowHdr::haz offset (tools/heal_diag.py reads it)");
 // FlowHdr::ok: 0 declined, FL_OK_ADD an ADD-only flow book, FL_OK_CANCEL a book with DELs,
 // FL_OK_DEEP an ADD-only head book with more levels than the lane plans hold (match_flow_deep.h)
 constexpr uint32_t FL_OK_ADD = 1, FL_OK_CANCEL = 2, FL_OK_DEEP = 3;
+// FlowHdr::haz: a REST of 0 at depth 0, a CONS of 0 on the cancel path, a consume that empties a level
+// and stops beside a zero-volume maker, a zero-volume taker meeting one (ADD path), a cancel that
+// empties a level beside one, a cancel of one, a rest across a stale price (Q2)
+enum : uint32_t {
+  HZ_ZREST0 = 1, HZ_ZCONS0 = 2, HZ_ZSTOP = 4, HZ_ZTAKER = 8, HZ_ZDELEMPTY = 16, HZ_ZDEL = 32, HZ_STALE = 64
+};
 constexpr uint32_t FL_CH_DEEP = 1, FL_CH_CANCEL = 2;  // FlowArgs::chains
 constexpr uint32_t DEEP_CAP = 16384;     // level slots of a deep book (0 and DEEP_CAP - 1: sentinels)
 constexpr uint32_t DEEP_HASH = 1u << 16; // price-set slots of a deep book (global memory)
@@ -195,7 +203,9 @@ struct FlowLvl {
   uint32_t mfin;     // books with DELs: the level ends a stale member of this set (M_BUY / M_SALE;
                      // k_fc_stale_level), 0 if not
   uint32_t zpop;     // ADD books: old zero-volume makers the batch popped (fl_level_one's gather)
-  uint32_t pad4, pad5, pad6;
+  uint32_t pad4;
+  uint32_t zcont;    // levels that may hold zero-volume makers: the last consume went on (fl_run_cont)
+  uint32_t pad6;
 };
 static_assert(sizeof(FlowLvl) % 16 == 0, "FlowLvl alignment");
 
@@ -1572,6 +1582,43 @@ __device__ __forceinline__ uint32_t fl_first_back(const IgEnt* IG, uint32_t ig_n
   return f;
 }
 
+// The level-end continuation (Q6).  A consume that takes a level's whole depth with volume to spare
+// goes on (MatchOrder's diff > 0 branch recurses, engine.go:145-161): it pops the zero-volume makers
+// still at the level's end with 0-fills before Match moves to the next level or the taker rests
+// (engine.go:129-131).  A taker that stopped there (diff == 0) leaves them.  It went on exactly when
+// its next touch in the log (in time order, an order's touches consecutive) is its own.  cb: a book
+// with DELs (tk_jc).
+__device__ __forceinline__ bool fl_cont(const FlowArgs& F, uint32_t L, uint32_t nt, uint32_t t, bool cb) {
+  return t + 1 < nt && tk_jb(F.log[L + t], cb) == tk_jb(F.log[L + t + 1], cb);
+}
+// ... of the consume before run entry i (the level's previous CONS in time order, which ended at this
+// one's cursor): the zero-volume makers starting at the cursor are then gone, not this consume's
+// first fills (fl_first_back).  Walked back one entry at a time: levels that may hold zero-volume
+// makers only (a run's CONS gaps add up to its length).
+__device__ __forceinline__ bool fl_prev_cont(const FlowArgs& F, uint32_t L, uint32_t nt, const SEnt* R, uint32_t i,
+                                             bool cb) {
+  while (i-- > 0)
+    if (R[i].kind == TK_CONS) return R[i].amt > 0 && fl_cont(F, L, nt, R[i].t, cb);
+  return false;
+}
+// ... of the level's last consume (FlowLvl::zcont): the zero-volume makers at the consumption end
+// are popped, not survivors.
+__device__ __forceinline__ bool fl_run_cont(const FlowArgs& F, uint32_t L, uint32_t nt, const SEnt* R, uint32_t cnt,
+                                            bool cb) {
+  return fl_prev_cont(F, L, nt, R, cnt, cb);
+}
+// A continuing consume's last maker steps on over the zero-volume makers starting at its end x
+// (the mirror of fl_first_back; a maker that rested there after it has volume, or starts later).
+__device__ __forceinline__ uint32_t fl_last_fwd(const IgEnt* IG, uint32_t ig_n, const RsEnt* RS, uint32_t nrest,
+                                                uint32_t l, int64_t x) {
+  for (uint32_t m = l + 1; m < ig_n + nrest; ++m) {
+    const bool old = m < ig_n;
+    if ((old ? IG[m].v : RS[m - ig_n].v) != 0 || (old ? IG[m].e : RS[m - ig_n].e) != x) break;
+    l = m;
+  }
+  return l;
+}
+
 // Wave-cooperative fl_find: every lane's query q (lanes with !valid ignored), b a maker at or
 // before every valid query's.  Windows of 64 consecutive makers from b (one coalesced read into
 // the lanes) searched by shuffles; a query beyond FL_FC_WIN windows searches alone.  Makers'
@@ -1614,7 +1661,7 @@ __device__ __forceinline__ uint32_t fl_wave_find(const IgEnt* IG, uint32_t ig_n,
 // chunk's ended; interleaved waves find their chunk's first maker by one search.
 __device__ __forceinline__ void fl_level_fc(const FlowArgs& F, uint32_t L, uint32_t q, uint32_t base, uint32_t cnt,
                                             const IgEnt* IG, uint32_t ig_n, uint32_t nrest, int64_t d0, uint32_t w,
-                                            uint32_t nw, bool zl = false) {
+                                            uint32_t nw, bool zl = false, uint32_t nt = 0) {
   const SEnt* R = F.srt + L + base;
   const RsEnt* RS = F.rs + L + base;
   const uint32_t lane = lane_id();
@@ -1634,10 +1681,14 @@ __device__ __forceinline__ void fl_level_fc(const FlowArgs& F, uint32_t L, uint3
     const uint32_t l = fl_wave_find(IG, ig_n, RS, nrest, d0, cons, x, __shfl(f0, l0));
     carry = __shfl(l, l1);
     if (cons) {
-      const uint32_t f = zl && e.amt ? fl_first_back(IG, ig_n, RS, f0, e.coord) : f0;
+      uint32_t f = f0, ll = l;
+      if (zl && e.amt) {  // (zero-volume makers at the cursor, and at the end of a consume that went on)
+        if (!fl_prev_cont(F, L, nt, R, i, false)) f = fl_first_back(IG, ig_n, RS, f0, e.coord);
+        if (fl_cont(F, L, nt, e.t, false)) ll = fl_last_fwd(IG, ig_n, RS, nrest, l, e.coord + e.amt);
+      }
       FlTouchFc y;
       y.first = f;
-      y.last = l;
+      y.last = ll;
       y.lvl = q;
       y.pad = 0;
       y.coord = e.coord;
@@ -1721,6 +1772,9 @@ __device__ __forceinline__ void fl_level_one(const Dev& D, const FlowArgs& F, ui
     nr += __popcll(rm);
   }
   const int64_t cfin = cc;
+  // (a level that may hold zero-volume makers: the level-end continuation, fl_cont)
+  const uint32_t nt = zl ? uni(hd->ntouch) : 0u;
+  const bool lcont = zl && cfin > 0 && fl_run_cont(F, L, nt, R, cnt, false);
   uint32_t nv0 = uni(Lq->nv0), head = uni(Lq->head), tail = uni(Lq->tail);
   uint32_t hslot = uni(Lq->hslot), tslot = uni(Lq->tslot);
   uint32_t ig_base = 0, ng = 0, consumed = 0, zpopped = 0;
@@ -1773,9 +1827,10 @@ __device__ __forceinline__ void fl_level_one(const Dev& D, const FlowArgs& F, ui
       const int64_t x = live ? nd.rem : 0;
       const int64_t inc = wave_incl_scan(x);
       const int64_t em = E + inc - x;
-      const unsigned long long beyond = __ballot(live && em >= cfin);
+      const bool zend = lcont && live && nd.rem == 0 && em == cfin;  // (popped by the last consume, going on)
+      const unsigned long long beyond = __ballot(live && em >= cfin && !zend);
       const uint32_t fb = beyond ? static_cast<uint32_t>(__builtin_ctzll(beyond)) : 64u;
-      const bool take = live && (em < cfin || lane == fb);
+      const bool take = live && (em < cfin || zend || lane == fb);
       const unsigned long long tm = __ballot(take);
       if (take) {
         IgEnt g;
@@ -1788,9 +1843,10 @@ __device__ __forceinline__ void fl_level_one(const Dev& D, const FlowArgs& F, ui
         IG[ng + __popcll(tm & ltm)] = g;
       }
       ng += __popcll(tm);
-      // (a zero-volume maker is consumed, popped, only strictly before the consumption end: one at
-      // the end was not reached, engine.go:162-175)
-      const bool cons = live && em + nd.rem <= cfin && (nd.rem > 0 || em < cfin);
+      // (a zero-volume maker is consumed, popped, strictly before the consumption end, or at it when
+      // the last consume went on: one at the end was not reached by a taker that stopped there,
+      // engine.go:162-175)
+      const bool cons = live && em + nd.rem <= cfin && (nd.rem > 0 || em < cfin || zend);
       if (cons) __hip_atomic_store(&D.idx[nd.ixs].key, KEY_TOMB, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       consumed += __popcll(__ballot(cons));
       zpopped += __popcll(__ballot(cons && nd.rem == 0));
@@ -1852,10 +1908,14 @@ __device__ __forceinline__ void fl_level_one(const Dev& D, const FlowArgs& F, ui
         const uint32_t l = fl_wave_find(IG, ng, RS, nr, d0, isc, x, __shfl(f0, l0));
         carry = __shfl(l, l1);
         if (isc) {
-          const uint32_t f = zl && ac ? fl_first_back(IG, ng, RS, f0, c) : f0;
+          uint32_t f = f0, ll = l;
+          if (zl && ac) {  // (as fl_level_fc)
+            if (!fl_prev_cont(F, L, nt, R, i, false)) f = fl_first_back(IG, ng, RS, f0, c);
+            if (fl_cont(F, L, nt, e.t, false)) ll = fl_last_fwd(IG, ng, RS, nr, l, c + ac);
+          }
           FlTouchFc y;
           y.first = f;
-          y.last = l;
+          y.last = ll;
           y.lvl = q;
           y.pad = 0;
           y.coord = c;
@@ -1877,6 +1937,7 @@ __device__ __forceinline__ void fl_level_one(const Dev& D, const FlowArgs& F, ui
     Lq->tslot = tslot;
     Lq->nlive0 = nv0 - consumed;
     Lq->zpop = zpopped;
+    Lq->zcont = lcont ? 1u : 0u;
   }
 }
 
@@ -1907,6 +1968,8 @@ __device__ __forceinline__ void fl_level_lane(const Dev& D, const FlowArgs& F, u
   int64_t cfin = 0;
   for (uint32_t i = 0; i < cnt; ++i)
     if (R[i].kind == TK_CONS) cfin += R[i].amt;
+  const uint32_t nt = zl ? hd->ntouch : 0u;
+  const bool lcont = zl && cfin > 0 && fl_run_cont(F, L, nt, R, cnt, false);  // (fl_level_one)
   uint32_t nv0 = Lq->nv0, head = Lq->head, tail = Lq->tail;
   uint32_t hslot = Lq->hslot, tslot = Lq->tslot;
   uint32_t ig_base = 0, ng = 0, consumed = 0, zpopped = 0;
@@ -1937,6 +2000,7 @@ __device__ __forceinline__ void fl_level_lane(const Dev& D, const FlowArgs& F, u
         if (!(s >= s0 && s < lim && nd[s].rem >= 0)) continue;  // (live makers only)
         const int64_t em = E;
         E += nd[s].rem;
+        const bool zend = lcont && nd[s].rem == 0 && em == cfin;
         if (!have_extra) {  // every maker before the consumption end, then the first at or past it
           IgEnt g;
           g.e = em;
@@ -1946,9 +2010,9 @@ __device__ __forceinline__ void fl_level_lane(const Dev& D, const FlowArgs& F, u
           g.tx = nd[s].tx;
           g.pad = 0;
           IG[ng++] = g;
-          if (em >= cfin) have_extra = true;
+          if (em >= cfin && !zend) have_extra = true;
         }
-        const bool cons = em + nd[s].rem <= cfin && (nd[s].rem > 0 || em < cfin);
+        const bool cons = em + nd[s].rem <= cfin && (nd[s].rem > 0 || em < cfin || zend);
         if (cons) {
           __hip_atomic_store(&D.idx[nd[s].ixs].key, KEY_TOMB, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           consumed++;
@@ -2006,8 +2070,8 @@ __device__ __forceinline__ void fl_level_lane(const Dev& D, const FlowArgs& F, u
     const uint32_t f0 = fl_find_all(IG, ng, RS, nr, c);
     const uint32_t l = fl_find_all(IG, ng, RS, nr, x);
     FlTouchFc y;
-    y.first = zl && e.amt ? fl_first_back(IG, ng, RS, f0, c) : f0;
-    y.last = l;
+    y.first = zl && e.amt && !fl_prev_cont(F, L, nt, R, i, false) ? fl_first_back(IG, ng, RS, f0, c) : f0;
+    y.last = zl && e.amt && fl_cont(F, L, nt, e.t, false) ? fl_last_fwd(IG, ng, RS, nr, l, c + e.amt) : l;
     y.lvl = q;
     y.pad = 0;
     y.coord = c;
@@ -2025,6 +2089,7 @@ __device__ __forceinline__ void fl_level_lane(const Dev& D, const FlowArgs& F, u
   Lq->tslot = tslot;
   Lq->nlive0 = nv0 - consumed;
   Lq->zpop = zpopped;
+  Lq->zcont = lcont ? 1u : 0u;
   Lq->cnt = cnt;
 }
 
@@ -2496,13 +2561,15 @@ struct FlWPlan {
 __device__ __forceinline__ FlWPlan fl_wplan(const FlowLvl& f, const RsEnt* RS) {
   FlWPlan w;
   w.rf = 0;
-  if (f.cfin > f.d0) {
+  // (zcont: the last consume went on and popped the zero-volume makers at the consumption end)
+  const bool zc = f.cfin > 0 && f.zcont;
+  if (f.cfin > f.d0 || (zc && f.cfin == f.d0)) {
     uint32_t lo = 0, hi = f.nrest;  // first r with e + v > cfin
     while (lo < hi) {
       const uint32_t mid = (lo + hi) >> 1;
-      // (a zero-volume maker (Q6) survives at the cursor: width 1; it rests after every consume of its
-      // level, k_flow_zero_check)
-      if (RS[mid].e + (RS[mid].v ? RS[mid].v : 1) > f.cfin) hi = mid; else lo = mid + 1;
+      // (a zero-volume maker (Q6) survives at the cursor: width 1, unless the last consume went on,
+      // fl_cont; it rests after every consume of its level, k_flow_zero_check)
+      if (RS[mid].e + (RS[mid].v ? RS[mid].v : (zc ? 0 : 1)) > f.cfin) hi = mid; else lo = mid + 1;
     }
     w.rf = lo;
   }
@@ -3220,13 +3287,14 @@ __global__ __launch_bounds__(64) void k_flow_zero_check(Dev D, FlowArgs F) {
   const FlowLvl* Lq = F.lvl + h * FL_CAP + q;
   const uint32_t cnt = Lq->cnt;
   if (!cnt) return;
-  const SEnt* R = F.srt + FL_TOUCH_MUL * hd->beg + Lq->base;
+  const uint32_t L = FL_TOUCH_MUL * hd->beg, nt = hd->ntouch;
+  const SEnt* R = F.srt + L + Lq->base;
   const int64_t d0 = Lq->d0;
   int64_t run = d0;          // the level's depth before the chunk
   int64_t rr = d0, cc = 0;   // arrival end and consumption cursor before the chunk (volume coordinates)
   int64_t zlast = -1;        // start of the latest zero-volume maker rested before the chunk (-1: none)
   int64_t wlast = -1;        // cancel books: the latest reach point of a zero-volume maker (below)
-  bool haz = false;
+  uint32_t hz = 0;           // HZ_* found by this lane
   for (uint32_t c0 = 0; c0 < cnt; c0 += 64) {
     const uint32_t i = c0 + lane;
     const bool valid = i < cnt;
@@ -3239,38 +3307,44 @@ __global__ __launch_bounds__(64) void k_flow_zero_check(Dev D, FlowArgs F) {
     const int64_t rb = rr + fl_wave_excl(isr ? e.amt : 0, &tr);  // this REST's start
     const int64_t cb = cc + fl_wave_excl(isc ? e.amt : 0, &tc);  // this CONS's cursor
     const int64_t zm = max(zlast, fl_wave_max_excl(zr ? rb : -1, &tzm));
+    // a consume that empties the level and goes on pops the zero-volume makers at its end (fl_cont)
+    const bool cont = isc && e.amt > 0 && before - e.amt == 0 && fl_cont(F, L, nt, e.t, canc);
     if (canc) {
       // Cancel books (round 6: their reconstruction pops zero-volume makers, fc_fills).  A
       // zero-volume maker rested at depth D after C of the level was consumed is reached once the
       // consumption passes W = C + D: exactly in consumption space when no cancel removes volume
       // ahead of it, an upper bound otherwise (a cancel may hit a maker behind it).  A consume or
       // cancel that empties the level while some W >= the consumption after it (the maker may still
-      // be in the FIFO: the reference leaves it in a FIFO whose level left its set, or the taker
-      // pops it at the level's end) is a hazard, and so are a REST of 0 at depth 0 and a CONS of 0
-      // (a zero-volume taker, whose 0-fill the cancel events do not model).  Old zero-volume makers:
-      // W = d0.
+      // be in the FIFO, which the reference leaves in place, its level out of its set) is a hazard,
+      // unless it is a consume that goes on and pops them (fl_cont); so are a REST of 0 at depth 0 and a
+      // CONS of 0 (a zero-volume taker, whose 0-fill the cancel events do not model).  Old zero-volume
+      // makers: W = d0.
       int64_t twm;
       const int64_t wm = max(wlast, fl_wave_max_excl(zr ? before + cb : -1, &twm));
       const int64_t cend = cb + (isc ? e.amt : 0);
       const bool present = (Lq->z0 && d0 >= cend) || wm >= cend;
-      haz = haz || (zr && before == 0) || (isc && e.amt == 0) || ((isc || isx) && before - e.amt == 0 && present);
+      const bool empt = before - e.amt == 0 && present;
+      hz |= (zr && before == 0 ? HZ_ZREST0 : 0u) | (isc && e.amt == 0 ? HZ_ZCONS0 : 0u) |
+            (isc && !cont && empt ? HZ_ZSTOP : 0u) | (isx && empt ? HZ_ZDELEMPTY : 0u);
       wlast = max(wlast, twm);
     } else {
       // ADD books: a zero-volume maker is in the FIFO until a consume passes its start (an old
       // one: until the cursor passes the old FIFO's end).  A consume that leaves depth > 0 pops the
-      // ones it passes (fl_first_back, the intervals); one that empties the level (the taker would
-      // pop those at its end if it went on, or leave them in a FIFO whose level left its set) or a
-      // zero-volume taker meeting one (diff == 0 pops it and the cursor stays) is a hazard, and so
-      // is a REST of 0 at depth 0.
+      // ones it passes (fl_first_back, the intervals), and one that empties the level and goes on
+      // the ones at its end too (fl_cont); one that empties the level and stops there (it leaves
+      // them in a FIFO whose level left its set) or a zero-volume taker meeting one (diff == 0 pops
+      // it and the cursor stays) is a hazard, and so is a REST of 0 at depth 0.
       const bool zp = (Lq->z0 && cb <= d0) || zm >= cb;
-      haz = haz || (zr && before == 0) || (isc && zp && (e.amt == 0 || before - e.amt == 0));
+      hz |= (zr && before == 0 ? HZ_ZREST0 : 0u) | (isc && zp && e.amt == 0 ? HZ_ZTAKER : 0u) |
+            (isc && zp && e.amt > 0 && before - e.amt == 0 && !cont ? HZ_ZSTOP : 0u);
     }
     run += tot;
     rr += tr;
     cc += tc;
     zlast = max(zlast, tzm);
   }
-  if (__ballot(haz) && lane == 0) atomicOr(&hd->haz, 1u);
+  for (int off = 32; off > 0; off >>= 1) hz |= __shfl_xor(hz, off);
+  if (hz && lane == 0) atomicOr(&hd->haz, hz);
 }
 
 // After the head's level sort: a book planned with stale members is exact unless an order rested
@@ -3323,7 +3397,7 @@ __global__ __launch_bounds__(FL_LVB_T) void k_flow_level_wide(Dev D, FlowArgs F)
   const FlowLvl* Lq = F.lvl + h * FL_CAP + q;
   if (cfin > 0 || z0)
     fl_level_fc(F, FL_TOUCH_MUL * F.hdr[h].beg, q, Lq->base, Lq->cnt, F.ig + Lq->ig_base, Lq->ig_n, Lq->nrest, Lq->d0,
-                threadIdx.x >> 6, FL_LVB_T / 64, Lq->z0 || F.hdr[h].nzero);
+                threadIdx.x >> 6, FL_LVB_T / 64, Lq->z0 || F.hdr[h].nzero, F.hdr[h].ntouch);
 }
 
 }  // namespace gome

@@ -276,7 +276,7 @@ __global__ __launch_bounds__(256) void k_fc_resolve(Dev D, BatchArgs B, FlowArgs
       if (a.price != q.price) continue;                 // S:link:<request price> misses (Q3)
       const bool wrong = (a.side == GOME_SALE) != sale;  // wrong side (Q2)
       if (wrong && !q2_ok) { fc_decline(F, h, FC_BAD_Q2); continue; }
-      if (a.vol == 0) atomicOr(&F.hdr[h].haz, 1u);  // a zero-volume maker's cancel (Q6): k_flow_stale_check
+      if (a.vol == 0) atomicOr(&F.hdr[h].haz, HZ_ZDEL);  // a zero-volume maker's cancel (Q6): k_flow_stale_check
       d.kind = FC_NEW;
       d.tgt = e.add_pos;
       F.fc_rank[b] = a.side == GOME_SALE ? 1u : 0u;
@@ -295,7 +295,7 @@ __global__ __launch_bounds__(256) void k_fc_resolve(Dev D, BatchArgs B, FlowArgs
     if (nd.rem < 0) continue;
     const bool wrong = (nd.tx == GOME_SALE) != sale;  // Q2
     if (wrong && !q2_ok) { fc_decline(F, h, FC_BAD_Q2); continue; }
-    if (nd.rem == 0) atomicOr(&F.hdr[h].haz, 1u);  // a zero-volume maker's cancel (Q6): k_flow_stale_check
+    if (nd.rem == 0) atomicOr(&F.hdr[h].haz, HZ_ZDEL);  // a zero-volume maker's cancel (Q6): k_flow_stale_check
     const uint32_t li = fc_level_of(LV, hd.nl, q.price);
     if (li == 0) { fc_decline(F, h, FC_BAD_LEVEL); continue; }
     if (wrong) {
@@ -923,7 +923,7 @@ __global__ __launch_bounds__(64) void k_fc_stale_level(Dev D, BatchArgs B, FlowA
     carry = max(carry, mtot);
     run += tot;
   }
-  if (__ballot(haz) && lane == 0) atomicOr(&hd->haz, 1u);
+  if (__ballot(haz) && lane == 0) atomicOr(&hd->haz, HZ_STALE);
   if (lane == 0) {
     const uint32_t fin = carry >= 0 ? static_cast<uint32_t>(carry & 7) : state;
     Lq->mfin = fin == ST_STALE_BUY ? M_BUY : fin == ST_STALE_SALE ? M_SALE : 0u;
@@ -1062,6 +1062,9 @@ __device__ __forceinline__ void fc_level_one(const Dev& D, const FlowArgs& F, ui
   __threadfence();  // the DEL records are read back below (by other lanes)
   const int64_t cfin = cc;
   const int64_t base_new = d0 - ocan;
+  // (a level that may hold zero-volume makers: the level-end continuation, fl_cont)
+  const bool zl = Lq->z0 || hd->nzero;
+  const bool lcont = zl && cfin > 0 && fl_run_cont(F, L, uni(hd->ntouch), R, cnt, true);
   // 2. the new makers in FIFO (rest) order, their consumption-space starts and cancels
   int64_t acc = base_new;
   uint32_t k = 0;
@@ -1137,7 +1140,8 @@ __device__ __forceinline__ void fc_level_one(const Dev& D, const FlowArgs& F, ui
       }
       const int64_t inc = wave_incl_scan(len);
       const int64_t em = E + inc - len;
-      const unsigned long long after = __ballot(live && em >= cfin && !targ);
+      const bool zend = lcont && live && !targ && nd.rem == 0 && em == cfin;  // (popped: the last consume went on)
+      const unsigned long long after = __ballot(live && em >= cfin && !targ && !zend);
       const uint32_t fb = after ? static_cast<uint32_t>(__builtin_ctzll(after)) : 64u;
       const bool take = live && lane <= fb;
       const unsigned long long tm = __ballot(take);
@@ -1153,9 +1157,10 @@ __device__ __forceinline__ void fc_level_one(const Dev& D, const FlowArgs& F, ui
       }
       ng += __popcll(tm);
       // fully consumed (uncancelled) makers leave with their index entries
-      // (a zero-volume maker (Q6) is popped only strictly before the consumption end, as the ADD
-      // path's gather: engine.go:145-161 pops it with a 0-fill when the taker goes on)
-      const bool cons = live && ct == NIL && em + nd.rem <= cfin && (nd.rem > 0 || em < cfin);
+      // (a zero-volume maker (Q6) is popped strictly before the consumption end, or at it when the
+      // last consume went on, as the ADD path's gather: engine.go:145-161 pops it with a 0-fill
+      // when the taker goes on)
+      const bool cons = live && ct == NIL && em + nd.rem <= cfin && (nd.rem > 0 || em < cfin || zend);
       if (cons) __hip_atomic_store(&D.idx[nd.ixs].key, KEY_TOMB, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       consumed += __popcll(__ballot(cons));
       zpopped += __popcll(__ballot(cons && nd.rem == 0));
@@ -1216,6 +1221,7 @@ __device__ __forceinline__ void fc_level_one(const Dev& D, const FlowArgs& F, ui
     Lq->tslot = ttslot;
     Lq->nlive0 = nv0 - consumed - ncan_old;
     Lq->zpop = zpopped;
+    Lq->zcont = lcont ? 1u : 0u;
     Lq->ocan = static_cast<uint32_t>(static_cast<uint64_t>(ocan) / g);
     Lq->pad0 = static_cast<uint32_t>(static_cast<uint64_t>(qend));
     Lq->pad1 = static_cast<uint32_t>(static_cast<uint64_t>(qend) >> 32);
@@ -1256,6 +1262,7 @@ __device__ __forceinline__ void fc_level_lane(const Dev& D, const FlowArgs& F, u
     }
   }
   const int64_t cfin = cc;
+  const bool lcont = (Lq->z0 || hd->nzero) && cfin > 0 && fl_run_cont(F, L, hd->ntouch, R, cnt, true);  // (fc_level_one)
   // 2. the new makers in FIFO order
   int64_t acc = d0 - ocan;
   uint32_t k = 0;
@@ -1320,6 +1327,7 @@ __device__ __forceinline__ void fc_level_lane(const Dev& D, const FlowArgs& F, u
         }
         const int64_t em = E;
         E += len;
+        const bool zend = lcont && !targ && nd[s].rem == 0 && em == cfin;
         if (taking) {  // (every live maker through the first untargeted one at or past the consumption end)
           IgEnt gq;
           gq.e = em;
@@ -1329,9 +1337,9 @@ __device__ __forceinline__ void fc_level_lane(const Dev& D, const FlowArgs& F, u
           gq.tx = nd[s].tx;
           gq.pad = ct;
           IG[ng++] = gq;
-          if (em >= cfin && !targ) { taking = false; stop = true; ig_all = false; }
+          if (em >= cfin && !targ && !zend) { taking = false; stop = true; ig_all = false; }
         }
-        const bool cons = ct == NIL && em + nd[s].rem <= cfin && (nd[s].rem > 0 || em < cfin);  // (Q6 as above)
+        const bool cons = ct == NIL && em + nd[s].rem <= cfin && (nd[s].rem > 0 || em < cfin || zend);  // (Q6 as above)
         if (cons) {
           __hip_atomic_store(&D.idx[nd[s].ixs].key, KEY_TOMB, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           consumed++;
@@ -1371,6 +1379,7 @@ __device__ __forceinline__ void fc_level_lane(const Dev& D, const FlowArgs& F, u
   Lq->tslot = ttslot;
   Lq->nlive0 = nv0 - consumed - ncan_old;
   Lq->zpop = zpopped;
+  Lq->zcont = lcont ? 1u : 0u;
   Lq->ocan = static_cast<uint32_t>(static_cast<uint64_t>(ocan) / g);
   Lq->pad0 = static_cast<uint32_t>(static_cast<uint64_t>(qend));
   Lq->pad1 = static_cast<uint32_t>(static_cast<uint64_t>(qend) >> 32);
@@ -1491,6 +1500,7 @@ __device__ __forceinline__ void fc_level_blk(const Dev& D, const FlowArgs& F, ui
   const int64_t qend = acc;
   // 3. the old FIFO (wave 0), as fc_level_one
   if (tid >= 64) return;
+  const bool lcont = (Lq->z0 || hd->nzero) && cfin > 0 && fl_run_cont(F, L, hd->ntouch, R, cnt, true);
   const unsigned long long ltm = lt_mask();
   const uint32_t nv0 = Lq->nv0, tail = Lq->tail, tslot = Lq->tslot;
   uint32_t head = Lq->head, hslot = Lq->hslot;
@@ -1526,7 +1536,8 @@ __device__ __forceinline__ void fc_level_blk(const Dev& D, const FlowArgs& F, ui
       }
       const int64_t inc = wave_incl_scan(len);
       const int64_t em = E + inc - len;
-      const unsigned long long after = __ballot(live && em >= cfin && !targ);
+      const bool zend = lcont && live && !targ && nd.rem == 0 && em == cfin;
+      const unsigned long long after = __ballot(live && em >= cfin && !targ && !zend);
       const uint32_t fb = after ? static_cast<uint32_t>(__builtin_ctzll(after)) : 64u;
       const bool take = live && lane <= fb;
       const unsigned long long tm = __ballot(take);
@@ -1541,9 +1552,9 @@ __device__ __forceinline__ void fc_level_blk(const Dev& D, const FlowArgs& F, ui
         IG[ng + __popcll(tm & ltm)] = gq;
       }
       ng += __popcll(tm);
-      // (a zero-volume maker (Q6) is popped only strictly before the consumption end, as the ADD
-      // path's gather: engine.go:145-161 pops it with a 0-fill when the taker goes on)
-      const bool cons = live && ct == NIL && em + nd.rem <= cfin && (nd.rem > 0 || em < cfin);
+      // (a zero-volume maker (Q6) is popped strictly before the consumption end, or at it when the
+      // last consume went on: fc_level_one)
+      const bool cons = live && ct == NIL && em + nd.rem <= cfin && (nd.rem > 0 || em < cfin || zend);
       if (cons) __hip_atomic_store(&D.idx[nd.ixs].key, KEY_TOMB, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       consumed += __popcll(__ballot(cons));
       zpopped += __popcll(__ballot(cons && nd.rem == 0));
@@ -1583,6 +1594,7 @@ __device__ __forceinline__ void fc_level_blk(const Dev& D, const FlowArgs& F, ui
     Lq->tslot = ttslot;
     Lq->nlive0 = nv0 - consumed - ncan_s;
     Lq->zpop = zpopped;
+    Lq->zcont = lcont ? 1u : 0u;
     Lq->ocan = static_cast<uint32_t>(static_cast<uint64_t>(ocan_t) / g);
     Lq->pad0 = static_cast<uint32_t>(static_cast<uint64_t>(qend));
     Lq->pad1 = static_cast<uint32_t>(static_cast<uint64_t>(qend) >> 32);
@@ -1632,9 +1644,11 @@ struct FcTouch {
   const FlowLvl* Lq;
   int64_t c, a;           // cursor before the touch, amount
   uint32_t first, last;   // makers spanned
+  bool cont;              // the consume went on past the level (fl_cont; levels with zero-volume makers)
 };
 
-__device__ __forceinline__ FcTouch fc_touch(const FlowArgs& F, uint32_t h, uint32_t L, const Touch& x) {
+// t: the touch's log index (book-local)
+__device__ __forceinline__ FcTouch fc_touch(const FlowArgs& F, uint32_t h, uint32_t L, const Touch& x, uint32_t t) {
   FcTouch T;
   const uint32_t k = F.hdr[h].ok == FL_OK_DEEP ? F.srt[L + x.pos].lvl : (x.kr & 127u);
   T.Lq = fl_lvls(F, h) + k;
@@ -1642,10 +1656,19 @@ __device__ __forceinline__ FcTouch fc_touch(const FlowArgs& F, uint32_t h, uint3
   T.c = F.srt[L + x.pos].coord;
   T.a = x.amt;
   T.first = fc_find(T.V, T.c);
+  T.cont = false;
   // a level that may hold zero-volume makers (Q6): the ones starting at the cursor are popped by
-  // this consume too (they share the start of the maker fc_find lands on; fl_first_back)
-  if ((T.Lq->z0 || F.hdr[h].nzero) && T.a > 0)
-    while (T.first > 0 && fc_start(T.V, T.first - 1) == T.c) --T.first;
+  // this consume too (they share the start of the maker fc_find lands on; fl_first_back), unless
+  // the consume before it went on and popped them; a consume that goes on pops the ones at its end
+  // (fl_cont)
+  const bool zl = (T.Lq->z0 || F.hdr[h].nzero) && T.a > 0;
+  if (zl) {
+    const uint32_t nt = F.hdr[h].ntouch;
+    T.cont = fl_cont(F, L, nt, t, true);
+    const uint32_t base = T.Lq->base;
+    if (!fl_prev_cont(F, L, nt, F.srt + L + base, x.pos - base, true))
+      while (T.first > 0 && fc_start(T.V, T.first - 1) == T.c) --T.first;
+  }
   // the last maker: a touch spans a few makers, so step on from the first (neighbouring entries,
   // one cache line) before a second binary search (~16 dependent loads on a busy level); the
   // starts rise through the old makers into the new ones, so both give the last start <= x
@@ -1654,17 +1677,20 @@ __device__ __forceinline__ FcTouch fc_touch(const FlowArgs& F, uint32_t h, uint3
   uint32_t m = T.first, st = 0;
   for (; st < 8 && m + 1 < nm && fc_start(T.V, m + 1) <= xl; ++st) ++m;
   T.last = st < 8 ? m : fc_find(T.V, xl);
+  // (going on: over the zero-length makers at the end, the zero-volume ones among them filled)
+  if (T.cont)
+    while (T.last + 1 < nm && fc_len(T.V, T.last + 1) == 0 && fc_start(T.V, T.last + 1) == T.c + T.a) ++T.last;
   return T;
 }
 
 // A maker of zero length in consumption space fills nothing (cancelled before any consumption),
 // except a zero-volume maker (Q6: volume 0, never cancelled in a flow batch -- its DEL is a hazard,
-// k_fc_resolve) that starts inside the consume [c, c + a): MatchOrder pops it with a 0-fill and
-// goes on (engine.go:145-161).
-__device__ __forceinline__ bool fc_fills(const FcLvlView& V, uint32_t m, int64_t c, int64_t a) {
+// k_fc_resolve) that starts inside the consume [c, c + a), or at its end c + a when the consume
+// goes on (cont): MatchOrder pops it with a 0-fill and goes on (engine.go:145-161).
+__device__ __forceinline__ bool fc_fills(const FcLvlView& V, uint32_t m, int64_t c, int64_t a, bool cont) {
   if (fc_len(V, m) > 0) return true;
   const int64_t e = fc_start(V, m);
-  return fc_vol(V, m) == 0 && e >= c && e < c + a;
+  return fc_vol(V, m) == 0 && e >= c && (e < c + a || (cont && e == c + a));
 }
 
 // Fills of a consume touch: makers of [first, last] with volume in consumption space.
@@ -1672,7 +1698,7 @@ __device__ __forceinline__ uint32_t fc_nfills(const FcTouch& T, uint32_t& pops) 
   uint32_t nf = 0;
   pops = 0;
   for (uint32_t m = T.first; m <= T.last; ++m) {
-    if (!fc_fills(T.V, m, T.c, T.a)) continue;
+    if (!fc_fills(T.V, m, T.c, T.a, T.cont)) continue;
     ++nf;
     if (fc_start(T.V, m) + fc_vol(T.V, m) <= T.c + T.a) ++pops;  // filled to its whole volume
   }
@@ -1697,7 +1723,7 @@ __global__ void k_fc_count(Dev D, BatchArgs B, FlowArgs F) {
       const uint32_t kind = tk_kind(y.kr, true);
       if (kind == TK_CONS) {
         uint32_t pp;
-        const uint32_t nf = fc_nfills(fc_touch(F, h, L, y), pp);
+        const uint32_t nf = fc_nfills(fc_touch(F, h, L, y, u), pp);
         acc += nf;
         fills += nf;
         pops += pp;
@@ -1747,7 +1773,7 @@ __global__ __launch_bounds__(256) void k_fc_events(Dev D, BatchArgs B, FlowArgs 
       kind = tk_kind(x.kr, true);
       if (kind == TK_CONS) {
         uint32_t pp;
-        T = fc_touch(F, h, L, x);
+        T = fc_touch(F, h, L, x, t);
         cnt = fc_nfills(T, pp);
       } else if (kind == TK_CANC) {
         cnt = 1;
@@ -1812,7 +1838,7 @@ __global__ __launch_bounds__(256) void k_fc_events(Dev D, BatchArgs B, FlowArgs 
     const uint32_t fb = F.fbase[L + t];
     uint32_t k = 0;
     for (uint32_t m = T.first; m <= T.last; ++m) {
-      if (!fc_fills(V, m, T.c, T.a)) continue;
+      if (!fc_fills(V, m, T.c, T.a, T.cont)) continue;
       const int64_t len = fc_len(V, m);
       const int64_t e = fc_start(V, m), v = fc_vol(V, m);
       uint32_t oid, uuid, tx;
@@ -1872,12 +1898,14 @@ __device__ __forceinline__ Level fc_write_level(const Dev& D, const BatchArgs& B
   // maker starting before the consumption end keeps e + v - cfin
   uint32_t S = 0;
   uint32_t zadd = 0;  // zero-volume makers appended (Q6; the old ones the batch popped: FlowLvl::zpop)
+  const bool zc = f.cfin > 0 && f.zcont;
   for (uint32_t c0 = 0; c0 < V.nrest; c0 += 64) {
     const uint32_t i = c0 + lane;
     bool sv = false;
     if (i < V.nrest) {
       const RsEnt r = V.RS[i];
-      sv = r.pad0 == NIL && (r.e + r.v > f.cfin || (r.v == 0 && r.e >= f.cfin));  // (Q6: as the gather)
+      // (Q6: as the gather; one at the consumption end is popped when the last consume went on)
+      sv = r.pad0 == NIL && (r.e + r.v > f.cfin || (r.v == 0 && r.e >= f.cfin && !(r.e == f.cfin && zc)));
     }
     S += __popcll(__ballot(sv));
     zadd += __popcll(__ballot(sv && i < V.nrest && V.RS[i].v == 0));
@@ -1917,7 +1945,7 @@ __device__ __forceinline__ Level fc_write_level(const Dev& D, const BatchArgs& B
     bool sv = false;
     if (i < V.nrest) {
       r = V.RS[i];
-      sv = r.pad0 == NIL && (r.e + r.v > f.cfin || (r.v == 0 && r.e >= f.cfin));
+      sv = r.pad0 == NIL && (r.e + r.v > f.cfin || (r.v == 0 && r.e >= f.cfin && !(r.e == f.cfin && zc)));
     }
     const unsigned long long sm = __ballot(sv);
     if (sv) {

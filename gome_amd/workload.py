@@ -254,11 +254,24 @@ def inject_quirks(rec: np.ndarray, sym: int, levels: np.ndarray, fifo, mode: str
     (BUYs at 1.00, SALEs at 0.01: one 0-fill each at the best opposite level, engine.go:176-194),
     spread over the batch, and one BUY resting behind the lowest bid's makers; "zeroheal": the same
     with the resting one behind the best bid's makers, where the stream's SALEs soon reach it and pop
-    it with a 0-fill (engine.go:145-161).  Returns what was injected."""
+    it with a 0-fill (engine.go:145-161); "zerodel": that zero-volume maker alone, in a batch with a
+    DEL (of the lowest bid's first maker), so the book takes the cancel path.  Returns what was
+    injected."""
     bids = levels[(levels["in_buy"] != 0) & (levels["in_sale"] == 0) & (levels["n_nodes"] > 0)]
     if len(bids) < 3:
         raise ValueError("book has fewer than three bid levels")
     bids = np.sort(bids, order="price_fx")
+    if mode == "zerodel":
+        pos = np.nonzero((rec["symbol_id"] == sym) & (rec["action"] == ADD))[0]
+        m = fifo(int(bids[0]["price_fx"]))[0]  # a DEL of the lowest bid's first maker: the cancel path
+        d = rec[pos[0]]
+        d["action"], d["flags"], d["oid_id"], d["uuid_id"] = DEL, 0, m["oid_id"], m["uuid_id"]
+        d["side"], d["price_fx"], d["volume_fx"] = m["side"], bids[0]["price_fx"], m["volume_fx"]
+        z = pos[len(pos) // 1000 + 1]
+        zb = bids[-1]
+        rec["volume_fx"][z], rec["side"][z], rec["price_fx"][z] = 0, 0, zb["price_fx"]
+        return {"q2_price": None, "q2_cancels": 0, "q6_price": int(zb["price_fx"]),
+                "q6_oid": int(rec["oid_id"][z]), "dels": 1, "records": [int(pos[0]), int(z)]}
     if mode in ("zero", "zeroheal"):
         pos = np.nonzero((rec["symbol_id"] == sym) & (rec["action"] == ADD))[0]
         picks = pos[(np.array([0.001, 0.1, 0.3, 0.5, 0.7, 0.9, 0.95]) * len(pos)).astype(int)]

@@ -30,8 +30,10 @@
  *   - strings: escapes decoded, a lone UTF-16 surrogate escape -> U+FFFD, every byte that does
  *     not start a valid UTF-8 encoding -> U+FFFD.
  *
- * Thread safety: a gome_names is used by one consumer thread; a gome_prepool may take markers
- * (gome_prepool_set) from any thread while one consumer consumes.
+ * Thread safety: a gome_names is interned by one consumer thread, and rendered from by
+ * gome_render_events_names on another at the same time (the pipelined consumer renders batch k
+ * while it decodes batch k + 1); a gome_prepool may take markers (gome_prepool_set) from any thread
+ * while one consumer consumes.
  */
 #ifndef GOME_HOST_H
 #define GOME_HOST_H
@@ -55,7 +57,7 @@ size_t gome_names_count(const gome_names* nm, int kind);
 /* The string of an id (NUL-terminated; *len = its length), or NULL. */
 const char* gome_names_get(const gome_names* nm, int kind, uint32_t id, size_t* len);
 /* Every string of a kind by id, NUL-terminated: the tables gome_render_events takes.  Valid
- * until the next intern of that kind. */
+ * until the next intern of that kind (gome_render_events_names reads them safely beside one). */
 const char* const* gome_names_table(gome_names* nm, int kind);
 /* Transaction int32 -> one-byte code (0 / 1 for 0 / 1, then first-seen order: gome_abi.h);
  * -1 once 256 codes exist. */
@@ -124,6 +126,13 @@ int64_t gome_render_events_mt(const gome_event* ev, size_t n, const gome_order* 
                               uint64_t seq_base, uint32_t accuracy, const char* const* sym_names, size_t n_sym,
                               const char* const* uuid_names, size_t n_uuid, const char* const* oid_names,
                               size_t n_oid, const int32_t* tx_table, uint32_t threads, char* buf, size_t cap);
+
+/* gome_render_events_mt with the name tables of nm, read under its lock: safe beside
+ * gome_consume_order_nodes interning into nm on another thread (an intern that moves a table
+ * waits for the render).  The events may only name ids interned before the call. */
+int64_t gome_render_events_names(const gome_event* ev, size_t n, const gome_order* batch, size_t batch_n,
+                                 uint64_t seq_base, uint32_t accuracy, gome_names* nm, uint32_t threads, char* buf,
+                                 size_t cap);
 
 #ifdef __cplusplus
 }

@@ -445,3 +445,46 @@ def test_consumer_pipelined_stream_matches_literal_gpu(packed):
     n = cons.process_stream(batches)
     assert n == len(lit_out) and sink.q == lit_out
     assert cons.consumed == len(q) and len(pre) == 0
+
+
+def test_render_beside_interning_reads_stable_tables():
+    """process_stream renders batch k on a helper thread while this thread interns batch k + 1's
+    names; an intern that outgrows an id table moves it (round 6: the r06i GPU run segfaulted in
+    the render).  gome_render_events_names reads the tables under the names' lock, so renders beside
+    300k interns (every table move included) all give the same bytes."""
+    import ctypes as C
+    import threading
+    from gome_amd.abi import load_library
+    from gome_amd.workload import EVENT_DTYPE, ORDER_DTYPE
+    lib = load_library()
+    names = Names()
+    for kind, s in (("sym", "s"), ("uuid", "u"), ("oid", "o")):
+        assert names.id(kind, s) == 0
+    rec = np.zeros(1, ORDER_DTYPE)
+    rec[0] = (5 * 10**7, 10**8, 0, 0, 0, 0, 1, 0)
+    ev = np.zeros(64, EVENT_DTYPE)
+    ev["kind"], ev["price_fx"], ev["maker_volume_fx"], ev["maker_is_last"] = 2, 5 * 10**7, 10**8, 1
+    ev["fill_idx"] = np.arange(64)
+
+    def render():
+        buf = C.create_string_buffer(1 << 20)
+        n = lib.gome_render_events_names(ev.ctypes.data, len(ev), rec.ctypes.data, 1, 0, 8, names.h, 2, buf, 1 << 20)
+        assert n > 0
+        return buf.raw[:n]
+
+    want = render()
+    got, stop = [], threading.Event()
+
+    def loop():
+        while not stop.is_set():
+            got.append(render())
+
+    t = threading.Thread(target=loop)
+    t.start()
+    try:
+        for i in range(1, 300000):
+            names.id("oid", f"o{i}")
+    finally:
+        stop.set()
+        t.join()
+    assert len(got) > 10 and all(g == want for g in got)

@@ -93,6 +93,9 @@ def test_early_plan_declines_keep_the_engine_exact():
     assert sum(int(s["n_early_miss"]) for s in stats) == 0, early
     for k in (4, 5, 6, 8, 9):  # (12: a zero-volume ADD may plan early since round 5: Q6 on the flow path)
         assert early[k] == 0, (k, early)
+    # 7: the batch after a declined early plan (6) is early-eligible; its early chain reads the book
+    # state batch 6's fallback plan wrote, which runs on the plan stream right behind k_x_take so the
+    # chain is ordered after it (it ran on the flow stream beside that chain)
     for k in (3, 7, 10, 11):
         assert early[k] == 1, (k, early)
     _cmp_books(eng, orc, list(_hot_and_random(z, 100000, k_rand=50)) + [second], "declines")

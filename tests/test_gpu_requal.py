@@ -6,6 +6,8 @@ heals (nodepool.go:76-83, engine.go:145-175); k_requalify (match_requal.h) clear
 has.  On bench.py's config-3 stream, the hottest book gets both quirks injected in batch 1
 (workload.inject_quirks, through the engine's own snapshot of the book), and every batch is
 compared event for event with the C oracle; the books' levels and FIFOs at the end too."""
+import struct
+
 import numpy as np
 import pytest
 
@@ -18,6 +20,8 @@ from tests.test_gpu_v4 import _cmp, _cmp_books, _hot_and_random
 pytestmark = pytest.mark.gpu
 
 N = 1 << 20
+HAZ_OFF = 144  # FlowHdr::haz (match_flow.h static_assert); HZ_* bits
+HZ_STALE = 64
 
 
 def _run(mode, batches=5):
@@ -26,7 +30,7 @@ def _run(mode, batches=5):
     hot = int(z.rank_to_id[0])
     eng = Engine(max_symbols=100000, max_batch=N, max_nodes=batches * N, max_levels=1 << 22)
     orc = Oracle(100000)
-    kinds, req, wrong, bails = [], [], [], []
+    kinds, req, wrong, bails, hazs = [], [], [], [], []
     for i in range(batches):
         b = gen(N).copy()
         if i == 1:
@@ -41,20 +45,26 @@ def _run(mode, batches=5):
         req.append((st["n_quirk_checked"], st["n_requalified"]))
         wrong.append(int(st["n_flow_wrong"]))
         bails.append(int(st["n_flow_bail"]))
+        hazs.append(struct.unpack("<I", eng.debug_peek(0, HAZ_OFF, 4))[0])  # (FlowHdr::haz of the hottest book)
     _cmp_books(eng, orc, _hot_and_random(z, 100000, k_rand=50), mode)
     assert eng.stats()["n_resting"] == orc.resting()
-    _run.bails = bails
+    _run.bails, _run.hazs = bails, hazs
     return kinds, req, wrong
 
 
 def test_quirks_heal_and_the_hottest_book_returns_to_the_flow_path():
-    """The quirks at the best bids, where the stream soon trades: the injected batch's wrong-side
-    cancels run on the flow cancel path, and the zero-volume maker, which the stream's SALEs reach
-    and pop with a 0-fill (engine.go:145-161), is popped by the cancel path's reconstruction too
-    (round 6, fc_fills): the book stays on the flow path in every batch, no hand-over, exact."""
+    """The quirks at the best bids, where the stream soon trades.  The zero-volume maker behind the
+    second-best bid is popped by a SALE that sweeps that level and goes on (the level-end
+    continuation, round 6).  What hands the injected batch to the legacy kernel is the stale bid
+    alone (FlowHdr::haz == HZ_STALE): a SALE rests at the stale price (in S:BUY, no FIFO), and a later
+    SALE taker reaches that price through S:BUY and fills against the resting SALE -- a same-side
+    fill the reference really publishes (the oracle's batch 1: one fill whose maker and taker are
+    both SALEs), which no aggregate plan can express.  The batches after it are on the flow path
+    again, exact throughout."""
     kinds, req, wrong = _run("heal")
     assert kinds[0] != 0 and wrong[1] >= 1, (kinds, wrong)
-    assert all(k != 0 for k in kinds) and sum(_run.bails) == 0, (kinds, _run.bails)
+    assert kinds[1] == 0 and _run.hazs[1] == HZ_STALE, (kinds, [hex(h) for h in _run.hazs])
+    assert all(k != 0 for k in kinds[2:]) and sum(_run.bails) == 1, (kinds, _run.bails)
 
 
 def test_quirks_that_do_not_heal_stay_on_the_flow_path():
@@ -261,10 +271,13 @@ def test_zero_volume_maker_at_a_new_price_hands_the_book_to_legacy():
     assert out[2][0] == 0 and out[2][1] >= 1 and out[2][2] >= 1, out
 
 
-def test_zero_volume_maker_reached_hands_the_book_to_legacy():
-    """A zero-volume BUY at the best bid followed by a SALE sweeping every bid: a consume after a
-    zero-volume maker may be in the FIFO (the fills would pop it), so the book goes to the legacy
-    kernel after its plan, exact."""
+def test_zero_volume_maker_at_the_end_of_a_swept_level_stays_on_the_flow_path():
+    """A zero-volume BUY at the best bid (the last maker of its FIFO) followed by a SALE sweeping
+    every bid: the SALE takes the level's whole depth with volume to spare, so MatchOrder's diff > 0
+    branch goes on and pops the zero-volume maker at the level's end with a 0-fill before Match moves
+    to the next bid (engine.go:145-161, 129-131).  The level-end continuation (round 6, fl_cont: the
+    taker's next touch is its own) pops it in the reconstruction too; until round 6 this handed the
+    book to the legacy kernel.  Exact, the book on the flow path, no hand-over."""
     def edit(b, hot, eng):
         lv = eng.levels(hot)
         bids = np.sort(lv[(lv["in_buy"] != 0) & (lv["n_nodes"] > 0)], order="price_fx")
@@ -272,7 +285,8 @@ def test_zero_volume_maker_reached_hands_the_book_to_legacy():
         b["volume_fx"][rows[0]], b["side"][rows[0]], b["price_fx"][rows[0]] = 0, 0, bids["price_fx"][-1]
         b["volume_fx"][rows[1]], b["side"][rows[1]], b["price_fx"][rows[1]] = 10 ** 14, 1, 10 ** 6
     out = _zero_run(47, edit)
-    assert out[2][0] == 0 and out[2][2] >= 1, out
+    assert out[2][0] != 0 and out[2][1] >= 1 and out[2][2] == 0, out
+    assert all(k != 0 for k, _, _ in out), out
 
 
 def _del_of(b, row, eng, hot, price, k=0):
@@ -323,3 +337,23 @@ def test_zero_volume_maker_left_at_an_emptied_level_with_dels_hands_over():
         b["price_fx"][rows[2]] = best["price_fx"]
     out = _zero_run(50, edit)
     assert out[2][0] == 0 and out[2][2] >= 1, out
+
+
+def test_zero_volume_maker_at_the_end_of_a_swept_level_with_dels_stays_on_the_flow_path():
+    """The level-end continuation on the cancel path: the batch of the test above holds a DEL (a
+    maker of the lowest bid), a zero-volume BUY rests behind the best bid's makers, and a SALE at the
+    best bid for the level's depth + 1.00 takes every maker, pops the zero-volume one at the level's
+    end (fc_touch / fc_fills with the consume going on, the gathers' FlowLvl::zcont) and rests its
+    remainder there: exact, the book on the flow path, no hand-over."""
+    def edit(b, hot, eng):
+        lv = eng.levels(hot)
+        bids = np.sort(lv[(lv["in_buy"] != 0) & (lv["n_nodes"] > 0)], order="price_fx")
+        best = bids[-1]
+        rows = _hot_rows(b, hot)[:3]
+        _del_of(b, rows[0], eng, hot, bids[0]["price_fx"])
+        b["volume_fx"][rows[1]], b["side"][rows[1]], b["price_fx"][rows[1]] = 0, 0, best["price_fx"]
+        b["volume_fx"][rows[2]], b["side"][rows[2]] = int(best["depth_fx"]) + 10 ** 8, 1
+        b["price_fx"][rows[2]] = best["price_fx"]
+    out = _zero_run(51, edit)
+    assert out[2][0] != 0 and out[2][1] >= 1 and out[2][2] == 0, out
+    assert all(k != 0 for k, _, _ in out), out

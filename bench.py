@@ -321,8 +321,9 @@ def consumer_leg(workload, n_symbols, n_msgs, seed, batch=1 << 15, threads=8):
            "matchresults_per_s": round(lines / wall, 1), "matchresults": lines, "threads": threads,
            "path": "OrderNode JSON deliveries (one buffer + offsets) -> BatchingConsumer.process_stream "
                    "(gome_consume_order_nodes: decode, convert, intern, admit into page-locked records; "
-                   "gome_submit_batch_async, two batches in flight; gome_collect; gome_render_events_mt "
-                   "straight into the sink's block) -> MatchResult lines on the sink",
+                   "gome_submit_batch_async, two batches in flight; gome_collect; gome_render_events_names "
+                   "on a helper thread, beside the next batch's decode, straight into the sink's block) -> "
+                   "MatchResult lines on the sink; host_ms.native_*: the consume call's own split",
            "host_ms": phases,
            "list_messages_per_s": round(n_msgs / wall2, 1),
            "list_path": "the same messages as Python bytes objects through BatchingConsumer.process, one "

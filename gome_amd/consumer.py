@@ -167,7 +167,8 @@ class _Decoded(C.Structure):
 
 
 class ConsumeStats(C.Structure):
-    _fields_ = [(n, C.c_uint64) for n in ("messages", "records", "rejected", "ignored", "not_objects", "admitted")]
+    _fields_ = [(n, C.c_uint64) for n in ("messages", "records", "rejected", "ignored", "not_objects", "admitted",
+                                          "ns_decode", "ns_prepare", "ns_queue")]
 
 
 def pack_messages(msgs):
@@ -338,7 +339,8 @@ class BatchingConsumer:
         self.consumed = self.rejected = self.batches = self.dups = 0
         # process_stream's host time per phase (s): decode + admission, submit, collect (waits for
         # the device), render
-        self.phase_s = {"records": 0.0, "submit": 0.0, "collect": 0.0, "render": 0.0}
+        self.phase_s = {"records": 0.0, "submit": 0.0, "collect": 0.0, "render": 0.0,
+                        "native_decode": 0.0, "native_prepare": 0.0, "native_queue": 0.0}
 
     # ---- draining ------------------------------------------------------------------
     def drain(self, q, block_s: float = 0.0) -> list:
@@ -380,6 +382,8 @@ class BatchingConsumer:
         if s != 0:
             raise GomeError(s, "gome_consume_order_nodes failed")
         self.rejected += st.rejected
+        for k in ("decode", "prepare", "queue"):  # (the native call's own split, seconds)
+            self.phase_s["native_" + k] += getattr(st, "ns_" + k) * 1e-9
         return rec[:got.value]
 
     def render_block(self, ev: np.ndarray, rec: np.ndarray, seq_base: int):

@@ -4,6 +4,7 @@
 // nodepool.go:14-28), one call per drained batch.  Host-only: no device work.
 #include <algorithm>
 #include <charconv>
+#include <chrono>
 #include <cmath>
 #include <cstdint>
 #include <cstdlib>
@@ -923,7 +924,13 @@ gome_status gome_consume_order_nodes(gome_names* nm, gome_prepool* pp, const cha
   std::vector<Dec> dec;
   std::vector<std::string> arenas;
   const uint32_t nt = pick_threads(threads, n);
+  using clk = std::chrono::steady_clock;
+  const auto ns = [](clk::time_point a, clk::time_point b) {
+    return static_cast<uint64_t>(std::chrono::duration_cast<std::chrono::nanoseconds>(b - a).count());
+  };
+  const auto t0 = clk::now();
   decode_all(buf, off, n, nt, dec, arenas);
+  const auto t1 = clk::now();
   // Per message, on the pool: the hashes the queue-order pass probes with (symbol, uuid, oid and the
   // marker key, built here as gome_prepool::key builds it).  The pass itself is serial -- ids are
   // handed out in first-seen order and markers are consumed in queue order (engine.go:58-62,90) --
@@ -962,6 +969,7 @@ gome_status gome_consume_order_nodes(gome_names* nm, gome_prepool* pp, const cha
       q.hk = hash_bytes(ka.data() + k0, q.klen);
     }
   });
+  const auto t2 = clk::now();
   gome_consume_stats s{};
   s.messages = n;
   size_t k = 0;
@@ -1041,6 +1049,9 @@ gome_status gome_consume_order_nodes(gome_names* nm, gome_prepool* pp, const cha
     ++k;
   }
   s.records = k;
+  s.ns_decode = ns(t0, t1);
+  s.ns_prepare = ns(t1, t2);
+  s.ns_queue = ns(t2, clk::now());
   *n_out = k;
   if (st) *st = s;
   return GOME_OK;

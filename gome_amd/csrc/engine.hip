@@ -89,6 +89,15 @@ __global__ __launch_bounds__(256) void k_publish(Dev D, BatchArgs B, FlowArgs F,
 }
 
 // Freed FIFO chunks of this batch -> free pool (two kernels: copy, then counters).
+// The stream-layout probe (four hardware queues): a ~2 ms spin on one stream, an empty kernel on the
+// other; the empty one finishing late means the two streams share a hardware queue.
+__global__ void k_probe_spin(unsigned long long ticks) {
+  const unsigned long long t0 = wall_clock64();
+  while (wall_clock64() - t0 < ticks) {
+  }
+}
+__global__ void k_probe_nop() {}
+
 __global__ void k_recycle_copy(Dev D) {
   const int top = max(D.st->free_top, 0);
   const uint32_t nf = D.st->freed_top;
@@ -298,6 +307,60 @@ struct gome_engine {
   hipError_t new_stream(hipStream_t* st) {
     return plan_cus ? hipExtStreamCreateWithCUMask(st, static_cast<uint32_t>(cu_rest.size()), cu_rest.data())
                     : hipStreamCreateWithFlags(st, hipStreamNonBlocking);
+  }
+  // Whether stream b waits for work on stream a: they share a hardware queue (tools/queue_map.hip).
+  hipError_t shares_queue(hipStream_t a, hipStream_t b, bool* shared) {
+    int khz = 0;
+    hipError_t he = hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, cfg.device);
+    hipEvent_t ev{};
+    if (he == hipSuccess) he = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+    if (he == hipSuccess) he = hipStreamSynchronize(a);
+    if (he == hipSuccess) he = hipStreamSynchronize(b);
+    if (he != hipSuccess) return he;
+    k_probe_spin<<<1, 64, 0, a>>>(2ull * static_cast<unsigned long long>(khz));  // (~2 ms)
+    k_probe_nop<<<1, 64, 0, b>>>();
+    he = hipEventRecord(ev, b);
+    const auto t0 = std::chrono::steady_clock::now();
+    if (he == hipSuccess) he = hipEventSynchronize(ev);
+    const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    const hipError_t h2 = hipStreamSynchronize(a);
+    (void)hipEventDestroy(ev);
+    *shared = ms > 1.0;
+    return he != hipSuccess ? he : h2;
+  }
+  // Four hardware queues: a stream for the early plan whose queue is none of the caller's, flow and
+  // hot streams'.  HIP hands queues to new streams by how many streams each already carries, so which
+  // stream gets which queue depends on what the host created before the engine (torch's null-stream
+  // work, RCCL's streams): the first of up to 6 new streams the probe finds alone is the early stream,
+  // the others become the copy streams (work only on the host path).  None alone: the last one
+  // (exact either way; only slower).  Round 6's first 4-queue layout relied on creation order and
+  // its early plan shared the hot stream's queue under torch: 99M orders/s instead of 146.6M.
+  hipError_t q4_early_stream() {
+    std::vector<hipStream_t> spare;
+    for (int k = 0; k < 6 && !early_stream; ++k) {
+      hipStream_t c{};
+      hipError_t he = new_stream(&c);
+      if (he != hipSuccess) return he;
+      bool any = false;
+      for (hipStream_t x : {stream, flow_stream, hot_stream}) {
+        bool sh = false;
+        if ((he = shares_queue(x, c, &sh)) != hipSuccess) return he;
+        any = any || sh;
+      }
+      if (any) spare.push_back(c);
+      else early_stream = c;
+    }
+    if (!early_stream) {
+      early_stream = spare.back();
+      spare.pop_back();
+    }
+    for (hipStream_t* st : {&copy_stream, &d2h_stream, &h2d_stream}) {
+      if (spare.empty()) break;
+      *st = spare.back();
+      spare.pop_back();
+    }
+    for (hipStream_t c : spare) (void)hipStreamDestroy(c);
+    return hipSuccess;
   }
   // The engine's streams on every CU, for batches after one no book dominated: there the tail's
   // chain is the critical path, and on the masked queues config 2 ran 5% slower.  set_masked
@@ -693,17 +756,16 @@ gome_status gome_engine::init(const gome_config& c) {
     }
   }
   HIPCHK(new_stream(&stream));
-  if (q4) {  // (creation order decides which streams share a hardware queue)
+  if (q4) {
     HIPCHK(new_stream(&flow_stream));
     HIPCHK(new_stream(&hot_stream));
-    if (early_on) HIPCHK(new_stream(&early_stream));
+    if (early_on) HIPCHK(q4_early_stream());
   } else {
     HIPCHK(new_stream(&hot_stream));
     HIPCHK(new_stream(&flow_stream));
   }
-  HIPCHK(new_stream(&copy_stream));
-  HIPCHK(new_stream(&d2h_stream));
-  HIPCHK(new_stream(&h2d_stream));
+  for (hipStream_t* st : {&copy_stream, &d2h_stream, &h2d_stream})
+    if (!*st) HIPCHK(new_stream(st));
   for (hipEvent_t* ev : {&fork, &join, &joinf, &prep_h, &prep_t, &fork_adm, &adm_done, &seg_done, &ho_fork, &tfc_fork, &tfc_done, &sort_done,
                          &dp_fork, &cnt_fork, &cnt_done, &dw_done, &dl_done, &tl_done, &tob_done, &plan_done,
                          &oidmax_done, &xpre_done, &xprep_done, &xplan_done, &xcmp_done, &adm_pre_done})

@@ -267,7 +267,7 @@ def inject_quirks(rec: np.ndarray, sym: int, levels: np.ndarray, fifo, mode: str
         d = rec[pos[0]]
         d["action"], d["flags"], d["oid_id"], d["uuid_id"] = DEL, 0, m["oid_id"], m["uuid_id"]
         d["side"], d["price_fx"], d["volume_fx"] = m["side"], bids[0]["price_fx"], m["volume_fx"]
-        z = pos[len(pos) // 1000 + 1]
+        z = pos[1]  # (right after the DEL: the book is still the snapshot's, so it rests behind the best bid)
         zb = bids[-1]
         rec["volume_fx"][z], rec["side"][z], rec["price_fx"][z] = 0, 0, zb["price_fx"]
         return {"q2_price": None, "q2_cancels": 0, "q6_price": int(zb["price_fx"]),

@@ -110,6 +110,9 @@ typedef struct gome_consume_stats {
   uint64_t ignored;        /* Action not ADD / DEL (syntax errors included)                    */
   uint64_t not_objects;    /* bodies that decoded nothing (syntax error / not an object)       */
   uint64_t admitted;       /* ADDs whose marker existed                                        */
+  uint64_t ns_decode;      /* wall time of the parallel decode                                 */
+  uint64_t ns_prepare;     /* ... of the parallel pass that hashes and builds the marker keys  */
+  uint64_t ns_queue;       /* ... of the queue-order pass (interning, markers, records)        */
 } gome_consume_stats;
 /* Decode, convert and admit messages buf[off[i], off[i + 1]) in queue order.  out[] receives
  * *n_out <= n records (the rejected messages are dropped), msg_index[] (optional) each record's

@@ -168,7 +168,7 @@ class _Decoded(C.Structure):
 
 class ConsumeStats(C.Structure):
     _fields_ = [(n, C.c_uint64) for n in ("messages", "records", "rejected", "ignored", "not_objects", "admitted",
-                                          "ns_decode", "ns_prepare", "ns_queue")]
+                                          "ns_decode", "ns_prepare", "ns_queue", "queue_parallel")]
 
 
 def pack_messages(msgs):
@@ -341,6 +341,7 @@ class BatchingConsumer:
         # the device), render
         self.phase_s = {"records": 0.0, "submit": 0.0, "collect": 0.0, "render": 0.0,
                         "native_decode": 0.0, "native_prepare": 0.0, "native_queue": 0.0}
+        self.parallel_batches = 0  # (batches whose queue-order work ran shard by shard)
 
     # ---- draining ------------------------------------------------------------------
     def drain(self, q, block_s: float = 0.0) -> list:
@@ -384,6 +385,7 @@ class BatchingConsumer:
         self.rejected += st.rejected
         for k in ("decode", "prepare", "queue"):  # (the native call's own split, seconds)
             self.phase_s["native_" + k] += getattr(st, "ns_" + k) * 1e-9
+        self.parallel_batches += int(st.queue_parallel)
         return rec[:got.value]
 
     def render_block(self, ev: np.ndarray, rec: np.ndarray, seq_base: int):
@@ -438,38 +440,42 @@ class BatchingConsumer:
         the device applies batch k, and batch k's MatchResults are rendered (on the renderer's own
         worker pool, by a helper thread) while batch k+2 is decoded.  Publishes exactly what
         process() would, batch after batch (the markers of a batch are committed when the engine
-        took it, as there).  The engine handle is only ever called from this thread.  Engines
+        took it, as there).  Renders queue on one helper thread (in batch order: the sink's order),
+        at most two behind the collects.  The engine handle is only ever called from this thread.  Engines
         without the async calls (test doubles) take process() per batch."""
         if not hasattr(self.eng, "submit_async"):
             return sum(self.process(b) for b in batches)
         from collections import deque
         from concurrent.futures import ThreadPoolExecutor
         depth = max(1, min(depth, 3))
-        # records stay valid until their batch is rendered: depth in flight, one rendering, one new
-        ring = [self.eng.host_buffer(self.max_batch) for _ in range(depth + 2)]
+        RENDERS = 2  # renders queued on the helper at most (their events are copies, their records in the ring)
+        # records stay valid until their batch is rendered: depth in flight, RENDERS queued or
+        # rendering, one new
+        ring = [self.eng.host_buffer(self.max_batch) for _ in range(depth + RENDERS + 1)]
         flight = deque()  # (records, seq base)
+        pending = deque()  # the helper's renders, oldest first
         ph = self.phase_s
         clk = time.perf_counter
-        total, slot, pending = 0, 0, None
+        total, slot = 0, 0
 
-        def render(ev, rec, base):  # (helper thread: the events' buffer stays valid until the next collect)
+        def render(ev, rec, base):  # (helper thread, one batch after another: the sink's order)
             t0 = clk()
             self.sink.publish_block(self.render_block(ev, rec, base), len(ev))
             ph["render"] += clk() - t0
 
         def finish(ex):
-            nonlocal pending
             rec, base = flight.popleft()
-            if pending is not None:  # (the last render must be done before the next collect)
-                pending.result()
-                pending = None
+            while len(pending) >= RENDERS:  # (a ring slot must not be reused under a render)
+                pending.popleft().result()
             t0 = clk()
-            ev, st = self.eng.collect(copy=False)
+            # (a copy of the events, ~48 B each: the engine's buffer is the next collect's, and the
+            # render need not finish before it)
+            ev, st = self.eng.collect(copy=True)
             ph["collect"] += clk() - t0
             self.dups += int(st["n_dup_oid"])
             if len(ev):
                 self.batches += 1
-                pending = ex.submit(render, ev, rec, base)
+                pending.append(ex.submit(render, ev, rec, base))
             return len(ev)
 
         with ThreadPoolExecutor(max_workers=1) as ex:
@@ -501,8 +507,8 @@ class BatchingConsumer:
                 while flight:
                     total += finish(ex)
             finally:
-                if pending is not None:
-                    pending.result()
+                while pending:
+                    pending.popleft().result()
         return total
 
     def poll(self, q, block_s: float = 0.0) -> int:

@@ -524,10 +524,14 @@ uint32_t pick_threads(uint32_t threads, size_t n) {
 void decode_all(const char* buf, const uint64_t* off, size_t n, uint32_t nt, std::vector<Dec>& dec,
                 std::vector<std::string>& arenas) {
   dec.assign(n, Dec{});
-  arenas.assign(nt, std::string());
+  arenas.resize(nt);
+  for (std::string& a : arenas) a.clear();  // (capacity kept: a consumer's scratch is reused per batch)
   auto work = [&](uint32_t k) {
     const size_t i0 = n * k / nt, i1 = n * (k + 1) / nt;
-    std::string& ar = arenas[k];
+    // (the thread's own string object while it appends: the vector's neighbouring string objects
+    // share cache lines, and every append writes the size)
+    std::string ar;
+    ar.swap(arenas[k]);
     ar.reserve(64 * (i1 - i0));
     Parser ps{nullptr, nullptr, &ar, static_cast<int32_t>(k), {}};
     for (size_t i = i0; i < i1; ++i) {
@@ -539,6 +543,7 @@ void decode_all(const char* buf, const uint64_t* off, size_t n, uint32_t nt, std
         ar.resize(mark);
       }
     }
+    arenas[k].swap(ar);
   };
   gome_host::Pool::get().run(nt, work);
 }
@@ -566,87 +571,161 @@ inline uint64_t hash_bytes(const char* s, size_t n) {
   return h;
 }
 
-// Open addressing; a slot holds (id + 1, the hash's high 32 bits), so a probe that is not the
-// string reads no string.  Strings live NUL-terminated in 1 MiB blocks that never move.
+// Open addressing, in IN_SHARDS tables by the hash's top bits (so a batch's new names can be
+// interned shard by shard on several threads, gome_consume_order_nodes); a slot holds (id + 1, the
+// hash's high 32 bits), so a probe that is not the string reads no string.  Ids are global, handed
+// out in first-seen order; strings live NUL-terminated in 1 MiB blocks (per shard) that never move.
+// During a parallel intern a slot may hold a provisional entry (IN_PROV | its index in the shard's
+// batch list) until the batch's new names get their ids.
+constexpr uint32_t IN_SHARDS = 64, IN_PROV = 0x80000000u;
+inline uint32_t in_shard(uint64_t h) { return static_cast<uint32_t>(h >> 58); }
+
 struct Interner {
-  std::vector<std::unique_ptr<char[]>> blocks;
-  size_t bused = 0, bcap = 0;
+  struct Fresh {
+    const char* s;
+    uint32_t n;
+    uint32_t first;  // the message that names it first (queue order)
+    uint64_t h;
+  };
+  struct alignas(64) Store {  // string blocks that never move (a shard's, or a pool thread's)
+    std::vector<std::unique_ptr<char[]>> blocks;
+    size_t bused = 0, bcap = 0;
+  };
+  struct alignas(64) Shard : Store {  // (a cache line of its own: neighbouring shards are other threads')
+    std::vector<uint64_t> slot;  // (id + 1 or IN_PROV | fresh index) | tag << 32; 0 = empty
+    uint64_t mask = 0;
+    std::vector<uint32_t> ids;   // the shard's ids (its rehash)
+    std::vector<Fresh> fresh;    // a parallel intern's new names, in queue order
+    std::vector<uint32_t> fresh_id;
+  };
+  Shard sh[IN_SHARDS];
   // by id; its reallocation (the only change a reader of older ids can see) happens under *gmu,
   // which gome_render_events_names holds shared while it renders beside the next batch's decode
   std::vector<const char*> strs;
-  std::shared_mutex* gmu = nullptr;
   std::vector<uint32_t> lens;
   std::vector<uint64_t> hs;
-  std::vector<uint64_t> slot;  // (id + 1) | tag << 32; 0 = empty
-  uint64_t mask = 0;
+  std::shared_mutex* gmu = nullptr;
 
-  const char* store(const char* s, size_t n) {
-    if (n + 1 > bcap - bused) {
-      const size_t cap = std::max<size_t>(1 << 20, n + 1);
-      blocks.emplace_back(new char[cap]);
-      bused = 0;
-      bcap = cap;
-    }
-    char* d = blocks.back().get() + bused;
-    std::memcpy(d, s, n);
-    d[n] = 0;
-    bused += n + 1;
-    return d;
+  std::vector<Store> tstore;  // the pool threads' (a parallel intern stores its new names there)
+  void reserve_stores(uint32_t nt) {
+    if (tstore.size() < nt) tstore.resize(nt);
   }
-  void grow() {
-    const uint64_t cap = std::max<uint64_t>(1024, (mask + 1) * 2);
-    slot.assign(cap, 0);
-    mask = cap - 1;
-    for (uint32_t id = 0; id < strs.size(); ++id) {
-      uint64_t j = hs[id] & mask;
-      while (slot[j]) j = (j + 1) & mask;
-      slot[j] = (id + 1ull) | (hs[id] >> 32 << 32);
+  static const char* store(Store& d, const char* s, size_t n) {
+    if (n + 1 > d.bcap - d.bused) {  // (blocks of 4 KiB doubling to 1 MiB: 3 x 64 shards start small)
+      const size_t cap = std::max<size_t>(std::min<size_t>(size_t{4096} << d.blocks.size(), 1 << 20), n + 1);
+      d.blocks.emplace_back(new char[cap]);
+      d.bused = 0;
+      d.bcap = cap;
+    }
+    char* p = d.blocks.back().get() + d.bused;
+    std::memcpy(p, s, n);
+    p[n] = 0;
+    d.bused += n + 1;
+    return p;
+  }
+  static void put(Shard& d, uint64_t h, uint64_t v) {
+    uint64_t j = h & d.mask;
+    while (d.slot[j]) j = (j + 1) & d.mask;
+    d.slot[j] = v | (h >> 32 << 32);
+  }
+  // room for one more entry (its ids and the provisional ones, rehashed)
+  void reserve1(Shard& d) {
+    if ((d.ids.size() + d.fresh.size() + 1) * 2 <= d.mask + 1) return;
+    const uint64_t cap = std::max<uint64_t>(1024, (d.mask + 1) * 2);
+    d.slot.assign(cap, 0);
+    d.mask = cap - 1;
+    for (uint32_t id : d.ids) put(d, hs[id], id + 1ull);
+    for (uint32_t l = 0; l < d.fresh.size(); ++l) put(d, d.fresh[l].h, IN_PROV | l);
+  }
+  // the slot value of the string (id + 1, or IN_PROV | fresh index during a parallel intern), or 0
+  uint32_t lookup(const Shard& d, const char* s, size_t n, uint64_t h) const {
+    if (d.slot.empty()) return 0;
+    const uint64_t tag = h >> 32 << 32;
+    for (uint64_t j = h & d.mask;; j = (j + 1) & d.mask) {
+      const uint64_t v = d.slot[j];
+      if (!v) return 0;
+      if ((v & ~0xFFFFFFFFull) != tag) continue;
+      const uint32_t x = static_cast<uint32_t>(v);
+      if (x & IN_PROV) {
+        const Fresh& f = d.fresh[x & ~IN_PROV];
+        if (f.n == n && std::memcmp(f.s, s, n) == 0) return x;
+      } else if (lens[x - 1] == n && std::memcmp(strs[x - 1], s, n) == 0) {
+        return x;
+      }
     }
   }
   int64_t find(const char* s, size_t n, uint64_t h) const {
-    if (slot.empty()) return -1;
-    const uint64_t tag = h >> 32 << 32;
-    for (uint64_t j = h & mask;; j = (j + 1) & mask) {
-      const uint64_t v = slot[j];
-      if (!v) return -1;
-      if ((v & ~0xFFFFFFFFull) != tag) continue;
-      const uint32_t id = static_cast<uint32_t>(v) - 1;
-      if (lens[id] == n && std::memcmp(strs[id], s, n) == 0) return id;
-    }
+    const uint32_t x = lookup(sh[in_shard(h)], s, n, h);
+    return (x && !(x & IN_PROV)) ? static_cast<int64_t>(x - 1) : -1;
   }
   void prefetch(uint64_t h) const {
-    if (!slot.empty()) __builtin_prefetch(&slot[h & mask]);
+    const Shard& d = sh[in_shard(h)];
+    if (!d.slot.empty()) __builtin_prefetch(&d.slot[h & d.mask]);
   }
   // second stage (the slot is in cache by now): the string its first probe compares against
   void prefetch2(uint64_t h) const {
-    if (slot.empty()) return;
-    const uint64_t v = slot[h & mask];
-    if (v && (v & ~0xFFFFFFFFull) == (h >> 32 << 32)) __builtin_prefetch(strs[static_cast<uint32_t>(v) - 1]);
+    const Shard& d = sh[in_shard(h)];
+    if (d.slot.empty()) return;
+    const uint64_t v = d.slot[h & d.mask];
+    if (v && (v & ~0xFFFFFFFFull) == (h >> 32 << 32) && !(static_cast<uint32_t>(v) & IN_PROV))
+      __builtin_prefetch(strs[static_cast<uint32_t>(v) - 1]);
+  }
+  // room in the id tables for `more` new ids (they move: not while a render reads them)
+  void grow_tables(size_t more) {
+    const size_t want = strs.size() + more;
+    if (want <= strs.capacity()) return;
+    std::unique_lock<std::shared_mutex> lk(*gmu);
+    strs.reserve(std::max<size_t>({1024, strs.capacity() * 2, want}));
+  }
+  // the id tables `more` longer at once (a parallel intern's new names; their entries are written
+  // after, each by its shard's thread: a render never reads ids of the batch being interned)
+  void extend_tables(size_t more) {
+    grow_tables(more);
+    std::unique_lock<std::shared_mutex> lk(*gmu);
+    strs.resize(strs.size() + more);
+    lens.resize(lens.size() + more);
+    hs.resize(hs.size() + more);
   }
   uint32_t intern(const char* s, size_t n) { return intern_h(s, n, hash_bytes(s, n)); }
   uint32_t intern_h(const char* s, size_t n, uint64_t h) {
-    const int64_t f = find(s, n, h);
-    if (f >= 0) return static_cast<uint32_t>(f);
-    if ((strs.size() + 1) * 2 > mask + 1) grow();
+    Shard& d = sh[in_shard(h)];
+    const uint32_t x = lookup(d, s, n, h);
+    if (x) return x - 1;
+    reserve1(d);
+    grow_tables(1);
     const uint32_t id = static_cast<uint32_t>(strs.size());
-    if (strs.size() == strs.capacity()) {  // (the table moves: not while a render reads it)
-      std::unique_lock<std::shared_mutex> lk(*gmu);
-      strs.reserve(std::max<size_t>(1024, strs.capacity() * 2));
-    }
-    strs.push_back(store(s, n));
+    strs.push_back(store(d, s, n));
     lens.push_back(static_cast<uint32_t>(n));
     hs.push_back(h);
-    uint64_t j = h & mask;
-    while (slot[j]) j = (j + 1) & mask;
-    slot[j] = (id + 1ull) | (h >> 32 << 32);
+    d.ids.push_back(id);
+    put(d, h, id + 1ull);
     return id;
   }
 };
 
 }  // namespace
 
+namespace {
+struct ConsumePre {  // gome_consume_order_nodes: one message's probes and values
+  uint64_t hs, hu, ho, hk;
+  int64_t p, v;
+  uint32_t koff, klen, ka;  // the marker key: karena[ka][koff, koff + klen)
+  uint8_t kind;             // 0 ignored action, 1 outside the domain (price / volume), 2 good
+};
+struct ConsumeScratch {
+  std::vector<Dec> dec;
+  std::vector<std::string> arenas, karena;
+  std::vector<ConsumePre> pre;
+  std::vector<uint32_t> odd_tx, cnt, kbase;
+  std::vector<uint32_t> idx[4], pos[4], start[4], ref[3], first[3], newmsg[3], owner;
+  std::vector<uint8_t> adm;
+  std::vector<gome_consume_stats> ps;
+};
+}  // namespace
+
 struct gome_names {
   Interner in[3];
+  ConsumeScratch scratch;  // (the consumer thread's, batch after batch)
   int32_t tx_raw[GOME_TX_CODES];
   uint32_t tx_n = 2;
   std::shared_mutex mu;  // the id tables' moves (Interner::gmu)
@@ -664,12 +743,17 @@ struct gome_names {
   }
 };
 
-// The markers: open addressing over (hash, key bytes in an arena); a marker the consumer took
-// provisionally is STAGED until commit (-> a tombstone) or abort (-> live again).  A STAGED marker
-// set again before the commit (the gRPC side's SetPrePool after the consumer's DeletePrePool,
-// nodepool.go:14-28) is RESET: commit leaves it LIVE (the new marker), abort LIVE too (one key, one
-// marker).
-struct gome_prepool {
+// The markers: open addressing over (hash, key bytes in an arena), in PP_SHARDS tables by the
+// hash's top bits, each with its lock (the consumer stages a batch's markers shard by shard on
+// several threads; the gRPC side's gome_prepool_set takes one shard's lock).  A marker the consumer
+// took provisionally is STAGED until commit (-> a tombstone) or abort (-> live again).  A STAGED
+// marker set again before the commit (the gRPC side's SetPrePool after the consumer's
+// DeletePrePool, nodepool.go:14-28) is RESET: commit leaves it LIVE (the new marker), abort LIVE too
+// (one key, one marker).
+constexpr uint32_t PP_SHARDS = 64;
+inline uint32_t pp_shard(uint64_t h) { return static_cast<uint32_t>(h >> 58); }
+
+struct alignas(64) PPShard {  // (a cache line of its own: neighbouring shards are other threads')
   enum : uint8_t { EMPTY = 0, LIVE = 1, TOMB = 2, STAGED = 3, RESET = 4 };
   struct Ent {
     uint64_t h;
@@ -682,15 +766,7 @@ struct gome_prepool {
   uint64_t mask = 0, live = 0, used = 0;  // used: live + staged + tombstones
   std::vector<char> arena;
   std::vector<uint64_t> staged;  // slots
-  std::string kb;                // the consumer's key scratch
 
-  static void key(std::string& k, const char* s, size_t sn, const char* u, size_t un, const char* o, size_t on) {
-    k.clear();
-    const uint32_t a = static_cast<uint32_t>(sn), b = static_cast<uint32_t>(un);
-    k.append(reinterpret_cast<const char*>(&a), 4).append(s, sn);
-    k.append(reinterpret_cast<const char*>(&b), 4).append(u, un);
-    k.append(o, on);
-  }
   bool same(const Ent& x, uint64_t h, const char* k, size_t n) const {
     return x.h == h && x.len == n && std::memcmp(arena.data() + x.off, k, n) == 0;
   }
@@ -703,7 +779,6 @@ struct gome_prepool {
       if (x.state != TOMB && same(x, h, k, n)) return static_cast<int64_t>(j);
     }
   }
-  int64_t find(const std::string& k, uint64_t h) const { return find(k.data(), k.size(), h); }
   void prefetch(uint64_t h) const {
     if (!tab.empty()) __builtin_prefetch(&tab[h & mask]);
   }
@@ -732,9 +807,8 @@ struct gome_prepool {
     for (uint64_t j = 0; j < cap; ++j)
       if (tab[j].state == STAGED || tab[j].state == RESET) staged.push_back(j);
   }
-  void set(const std::string& k) {
-    const uint64_t h = hash_bytes(k.data(), k.size());
-    const int64_t f = find(k, h);
+  void set(const char* k, size_t n, uint64_t h) {
+    const int64_t f = find(k, n, h);
     if (f >= 0) {  // (a staged marker set again: the commit keeps it)
       if (tab[static_cast<size_t>(f)].state == STAGED) tab[static_cast<size_t>(f)].state = RESET;
       return;
@@ -743,12 +817,12 @@ struct gome_prepool {
     uint64_t j = h & mask;
     while (tab[j].state == LIVE || tab[j].state == STAGED || tab[j].state == RESET) j = (j + 1) & mask;
     if (tab[j].state == EMPTY) ++used;
-    tab[j] = Ent{h, arena.size(), static_cast<uint32_t>(k.size()), LIVE};
-    arena.insert(arena.end(), k.begin(), k.end());
+    tab[j] = Ent{h, arena.size(), static_cast<uint32_t>(n), LIVE};
+    arena.insert(arena.end(), k, k + n);
     ++live;
   }
-  bool take(const std::string& k) {
-    const int64_t j = find(k, hash_bytes(k.data(), k.size()));
+  bool take(const char* k, size_t n, uint64_t h) {
+    const int64_t j = find(k, n, h);
     if (j < 0) return false;
     uint8_t& st = tab[static_cast<size_t>(j)].state;
     if (st == RESET) {  // (the re-set marker taken: the consumer's staged take still pending)
@@ -761,12 +835,7 @@ struct gome_prepool {
     return true;
   }
   // the staged ExistsPrePool + DeletePrePool of an ADD (engine.go:58-62), and the staged
-  // DeletePrePool of a DEL (engine.go:90): a LIVE marker becomes STAGED
-  bool stage(const std::string& k) {
-    std::lock_guard<std::mutex> g(mu);
-    return stage_locked(k.data(), k.size(), hash_bytes(k.data(), k.size()));
-  }
-  // (the caller holds mu: the consumer takes it once per batch)
+  // DeletePrePool of a DEL (engine.go:90): a LIVE marker becomes STAGED.  (The caller holds mu.)
   bool stage_locked(const char* k, size_t n, uint64_t h) {
     const int64_t j = find(k, n, h);
     if (j < 0) return false;
@@ -797,6 +866,18 @@ struct gome_prepool {
       if (tab[j].state == STAGED || tab[j].state == RESET) tab[j].state = LIVE;
     staged.clear();
   }
+};
+
+struct gome_prepool {
+  PPShard sh[PP_SHARDS];
+  static void key(std::string& k, const char* s, size_t sn, const char* u, size_t un, const char* o, size_t on) {
+    k.clear();
+    const uint32_t a = static_cast<uint32_t>(sn), b = static_cast<uint32_t>(un);
+    k.append(reinterpret_cast<const char*>(&a), 4).append(s, sn);
+    k.append(reinterpret_cast<const char*>(&b), 4).append(u, un);
+    k.append(o, on);
+  }
+  PPShard& of(uint64_t h) { return sh[pp_shard(h)]; }
 };
 
 extern "C" {
@@ -858,8 +939,10 @@ void gome_prepool_set(gome_prepool* pp, const char* sym, size_t sym_len, const c
   if (!pp || (!sym && sym_len) || (!uuid && uuid_len) || (!oid && oid_len)) return;
   std::string k;
   gome_prepool::key(k, sym, sym_len, uuid, uuid_len, oid, oid_len);
-  std::lock_guard<std::mutex> g(pp->mu);
-  pp->set(k);
+  const uint64_t h = hash_bytes(k.data(), k.size());
+  PPShard& d = pp->of(h);
+  std::lock_guard<std::mutex> g(d.mu);
+  d.set(k.data(), k.size(), h);
 }
 
 int32_t gome_prepool_take(gome_prepool* pp, const char* sym, size_t sym_len, const char* uuid, size_t uuid_len,
@@ -867,22 +950,30 @@ int32_t gome_prepool_take(gome_prepool* pp, const char* sym, size_t sym_len, con
   if (!pp || (!sym && sym_len) || (!uuid && uuid_len) || (!oid && oid_len)) return 0;
   std::string k;
   gome_prepool::key(k, sym, sym_len, uuid, uuid_len, oid, oid_len);
-  std::lock_guard<std::mutex> g(pp->mu);
-  return pp->take(k) ? 1 : 0;
+  const uint64_t h = hash_bytes(k.data(), k.size());
+  PPShard& d = pp->of(h);
+  std::lock_guard<std::mutex> g(d.mu);
+  return d.take(k.data(), k.size(), h) ? 1 : 0;
 }
 
 size_t gome_prepool_size(const gome_prepool* pp) {
   if (!pp) return 0;
-  std::lock_guard<std::mutex> g(const_cast<gome_prepool*>(pp)->mu);
-  return pp->live;
+  size_t n = 0;
+  for (PPShard& d : const_cast<gome_prepool*>(pp)->sh) {
+    std::lock_guard<std::mutex> g(d.mu);
+    n += d.live;
+  }
+  return n;
 }
 
 void gome_prepool_commit(gome_prepool* pp) {
-  if (pp) pp->commit();
+  if (pp)
+    for (PPShard& d : pp->sh) d.commit();
 }
 
 void gome_prepool_abort(gome_prepool* pp) {
-  if (pp) pp->abort();
+  if (pp)
+    for (PPShard& d : pp->sh) d.abort();
 }
 
 int64_t gome_decode_order_nodes(const char* buf, const uint64_t* off, size_t n, uint32_t threads,
@@ -921,35 +1012,40 @@ gome_status gome_consume_order_nodes(gome_names* nm, gome_prepool* pp, const cha
                                      uint32_t max_symbols, uint32_t threads, gome_order* out, uint32_t* msg_index,
                                      size_t* n_out, gome_consume_stats* st) {
   if (!nm || !pp || !n_out || (n && (!buf || !off || !out))) return GOME_E_INVAL;
-  std::vector<Dec> dec;
-  std::vector<std::string> arenas;
+  // (the names' scratch, reused batch after batch: fresh multi-megabyte vectors were page-faulted in
+  // by every pool thread at once, and the faults, not the work, set the parallel passes' time)
+  ConsumeScratch& W = nm->scratch;
+  std::vector<Dec>& dec = W.dec;
+  std::vector<std::string>& arenas = W.arenas;
   const uint32_t nt = pick_threads(threads, n);
   using clk = std::chrono::steady_clock;
   const auto ns = [](clk::time_point a, clk::time_point b) {
     return static_cast<uint64_t>(std::chrono::duration_cast<std::chrono::nanoseconds>(b - a).count());
   };
+  gome_host::Pool& pool = gome_host::Pool::get();
   const auto t0 = clk::now();
   decode_all(buf, off, n, nt, dec, arenas);
   const auto t1 = clk::now();
-  // Per message, on the pool: the hashes the queue-order pass probes with (symbol, uuid, oid and the
-  // marker key, built here as gome_prepool::key builds it).  The pass itself is serial -- ids are
-  // handed out in first-seen order and markers are consumed in queue order (engine.go:58-62,90) --
-  // and bound by its table probes' cache misses (the oid and marker tables hold millions of keys):
-  // with the hashes known it prefetches the slots PF messages ahead (round 6; the pass cost ~1 us a
-  // message before, as much as the 8-thread decode).
-  struct Pre {
-    uint64_t hs, hu, ho, hk;
-    uint32_t koff, klen, ka;  // the marker key: karena[ka][koff, koff + klen)
-  };
-  std::vector<Pre> pre(n);
-  std::vector<std::string> karena(nt);
-  gome_host::Pool::get().run(nt, [&](uint32_t t) {
+  // Per message, on the pool: the hashes the queue-order work probes with (symbol, uuid, oid and the
+  // marker key, built here as gome_prepool::key builds it), the fixed-point values, and whether the
+  // batch can take the parallel path below.
+  std::vector<ConsumePre>& pre = W.pre;
+  std::vector<std::string>& karena = W.karena;
+  std::vector<uint32_t>& odd_tx = W.odd_tx;
+  pre.resize(n);
+  karena.resize(nt);
+  for (std::string& a : karena) a.clear();
+  odd_tx.assign(nt, 0);
+  pool.run(nt, [&](uint32_t t) {
     const size_t i0 = n * t / nt, i1 = n * (t + 1) / nt;
-    std::string& ka = karena[t];
+    std::string ka;  // (the thread's own while it appends, as decode_all's arenas)
+    ka.swap(karena[t]);
     ka.reserve(48 * (i1 - i0));
+    uint32_t odd = 0;
     for (size_t i = i0; i < i1; ++i) {
       const Dec& d = dec[i];
-      Pre& q = pre[i];
+      ConsumePre& q = pre[i];
+      q.kind = 0;
       if (d.action != GOME_ADD && d.action != GOME_DEL) continue;
       const char* sym = str_ptr(d.s[2], arenas);
       const char* uuid = str_ptr(d.s[0], arenas);
@@ -967,88 +1063,375 @@ gome_status gome_consume_order_nodes(gome_names* nm, gome_prepool* pp, const cha
       q.ka = t;
       q.klen = static_cast<uint32_t>(ka.size() - k0);
       q.hk = hash_bytes(ka.data() + k0, q.klen);
+      const bool bad = gome_fixed_from_scaled(d.price, &q.p) != GOME_OK ||
+                       gome_fixed_from_scaled(d.volume, &q.v) != GOME_OK || q.v < 0;
+      q.kind = bad ? 1 : 2;
+      if (bad) continue;
+      odd += (d.tx != 0 && d.tx != 1) ? 1u : 0u;  // (the parallel path's precondition)
     }
+    odd_tx[t] = odd;
+    karena[t].swap(ka);
   });
   const auto t2 = clk::now();
   gome_consume_stats s{};
   s.messages = n;
+  // The queue-order work -- ids handed out in first-seen order, markers consumed in queue order
+  // (engine.go:58-62,90) -- in parallel where the order it must respect allows: a name's id depends
+  // only on which messages named a new name first, and a marker's fate only on the messages with
+  // its key.  So each kind's new names are found shard by shard (a shard's messages in queue order,
+  // on the pool), numbered by their first message, and the markers staged shard by shard.  Two
+  // rules break that independence and take the serial pass instead: a Symbol that would reach the
+  // engine's max_symbols (its message is dropped, so later names shift), and a Transaction outside
+  // 0 / 1 (its code is handed out in queue order and a 257th drops the message).
+  uint32_t odd = 0;
+  for (uint32_t t = 0; t < nt; ++t) odd += odd_tx[t];
+  bool parallel = nt > 1 && odd == 0;
   size_t k = 0;
-  constexpr size_t PF = 16;  // messages of prefetch distance
-  std::lock_guard<std::mutex> lock(pp->mu);  // (the markers, once for the batch)
-  for (size_t i = 0; i < n; ++i) {
-    if (i + PF < n) {
-      const Dec& f = dec[i + PF];
-      if (f.action == GOME_ADD || f.action == GOME_DEL) {
-        const Pre& q = pre[i + PF];
+  if (parallel) {
+    const uint32_t NS = IN_SHARDS;
+    constexpr uint32_t QPF = 16;  // prefetch distance (messages)
+    static_assert(PP_SHARDS == IN_SHARDS, "one pass over the shards of both kinds of table");
+    auto hash_of = [&](const ConsumePre& q, int kk) { return kk == 0 ? q.hs : kk == 1 ? q.hu : q.ho; };
+    auto si_of = [](int kk) { return kk == 0 ? 2 : kk == 1 ? 0 : 1; };  // (Dec::s order: uuid, oid, symbol)
+    // 1. every name looked up in the tables as the batch found them, read-only, by message range
+    //    (a name's messages spread over the threads however skewed the names are: the hottest
+    //    symbol alone is 8% of config 3's messages): ref = id + 1, or 0 for a name not seen before
+    std::vector<uint32_t>* ref = W.ref;
+    for (int kk = 0; kk < 3; ++kk) ref[kk].resize(n);
+    pool.run(nt, [&](uint32_t t) {
+      const size_t i0 = n * t / nt, i1 = n * (t + 1) / nt;
+      for (size_t i = i0; i < i1; ++i) {
+        if (i + QPF < i1 && pre[i + QPF].kind == 2)
+          for (int kk = 0; kk < 3; ++kk) nm->in[kk].prefetch(hash_of(pre[i + QPF], kk));
+        if (i + QPF / 2 < i1 && pre[i + QPF / 2].kind == 2)
+          for (int kk = 0; kk < 3; ++kk) nm->in[kk].prefetch2(hash_of(pre[i + QPF / 2], kk));
+        if (pre[i].kind != 2) continue;
+        for (int kk = 0; kk < 3; ++kk) {
+          const Str& x = dec[i].s[si_of(kk)];
+          const char* str = str_ptr(x, arenas);
+          const uint64_t h = hash_of(pre[i], kk);
+          ref[kk][i] = nm->in[kk].lookup(nm->in[kk].sh[in_shard(h)], str ? str : "", x.len, h);
+        }
+      }
+    });
+    // 2. the names not seen before and every marker, by shard: a counting sort of their messages
+    //    (queue order kept), then a shard's messages in order on one thread -- the first message of
+    //    a new name gives it a provisional entry, a marker is staged
+    std::vector<uint32_t>* idx = W.idx;      // new names of kind 0..2 (interner shards), markers (pre-pool shards)
+    std::vector<uint32_t>* start = W.start;
+    std::vector<uint32_t>& cnt = W.cnt;
+    cnt.assign(static_cast<size_t>(nt) * NS * 4, 0);
+    auto shard_of = [&](size_t i, int kk) -> uint32_t {
+      return kk < 3 ? in_shard(hash_of(pre[i], kk)) : pp_shard(pre[i].hk);
+    };
+    auto wanted = [&](size_t i, int kk) { return kk < 3 ? pre[i].kind == 2 && ref[kk][i] == 0 : pre[i].kind != 0; };
+    pool.run(nt, [&](uint32_t t) {
+      const size_t i0 = n * t / nt, i1 = n * (t + 1) / nt;
+      uint32_t* c = &cnt[static_cast<size_t>(t) * NS * 4];
+      for (size_t i = i0; i < i1; ++i)
+        for (int kk = 0; kk < 4; ++kk)
+          if (wanted(i, kk)) c[kk * NS + shard_of(i, kk)]++;
+    });
+    for (int kk = 0; kk < 4; ++kk) {
+      start[kk].assign(NS + 1, 0);
+      uint32_t run = 0;
+      for (uint32_t sh = 0; sh < NS; ++sh) {
+        start[kk][sh] = run;
+        for (uint32_t t = 0; t < nt; ++t) {
+          uint32_t& c = cnt[(static_cast<size_t>(t) * 4 + kk) * NS + sh];
+          const uint32_t v = c;
+          c = run;
+          run += v;
+        }
+      }
+      start[kk][NS] = run;
+      idx[kk].resize(run);
+    }
+    pool.run(nt, [&](uint32_t t) {
+      const size_t i0 = n * t / nt, i1 = n * (t + 1) / nt;
+      uint32_t* c = &cnt[static_cast<size_t>(t) * NS * 4];
+      for (size_t i = i0; i < i1; ++i)
+        for (int kk = 0; kk < 4; ++kk)
+          if (wanted(i, kk)) idx[kk][c[kk * NS + shard_of(i, kk)]++] = static_cast<uint32_t>(i);
+    });
+    // (outputs by position in idx[], written by one thread each: indexed by message they would be
+    // written from every thread at neighbouring addresses)
+    std::vector<uint32_t>* nref = W.first;  // a new name's message: IN_PROV | its shard's fresh index
+    std::vector<uint8_t>& adm = W.adm;
+    for (int kk = 0; kk < 3; ++kk) nref[kk].resize(idx[kk].size());
+    adm.assign(idx[3].size(), 0);
+    auto names_pass = [&](uint32_t sh, int kk) {
+      Interner& in = nm->in[kk];
+      Interner::Shard& d = in.sh[sh];
+      d.fresh.clear();
+      for (uint32_t r = start[kk][sh]; r < start[kk][sh + 1]; ++r) {
+        const uint32_t i = idx[kk][r];
+        const uint64_t h = hash_of(pre[i], kk);
+        const Str& x = dec[i].s[si_of(kk)];
+        const char* str = str_ptr(x, arenas);
+        uint32_t v = in.lookup(d, str ? str : "", x.len, h);  // (a provisional entry of this batch, or none)
+        if (!v) {
+          in.reserve1(d);
+          v = IN_PROV | static_cast<uint32_t>(d.fresh.size());
+          d.fresh.push_back(Interner::Fresh{str ? str : "", x.len, i, h});
+          Interner::put(d, h, v);
+        }
+        nref[kk][r] = v;
+      }
+    };
+    // the symbols first: the batch's new ones must fit the engine's symbol range (else the serial
+    // pass, which drops the messages whose symbol would not fit; their provisional entries go)
+    pool.run(nt, [&](uint32_t t) {
+      for (uint32_t sh = t; sh < NS; sh += nt) names_pass(sh, 0);
+    });
+    size_t new_syms = 0;
+    for (const Interner::Shard& d : nm->in[0].sh) new_syms += d.fresh.size();
+    if (max_symbols && nm->in[0].strs.size() + new_syms > max_symbols) {
+      for (Interner::Shard& d : nm->in[0].sh) {
+        if (d.fresh.empty()) continue;
+        d.fresh.clear();
+        std::fill(d.slot.begin(), d.slot.end(), 0ull);
+        for (uint32_t id : d.ids) Interner::put(d, nm->in[0].hs[id], id + 1ull);
+      }
+      parallel = false;
+    }
+    if (parallel) {
+      pool.run(nt, [&](uint32_t t) {
+        for (uint32_t sh = t; sh < NS; sh += nt) {
+          names_pass(sh, 1);
+          names_pass(sh, 2);
+          PPShard& d = pp->sh[sh];
+          std::lock_guard<std::mutex> g(d.mu);
+          const uint32_t r1 = start[3][sh + 1];
+          for (uint32_t r = start[3][sh]; r < r1; ++r) {
+            if (r + 2 * QPF < r1) __builtin_prefetch(&pre[idx[3][r + 2 * QPF]]);
+            if (r + QPF < r1) d.prefetch(pre[idx[3][r + QPF]].hk);
+            if (r + QPF / 2 < r1) d.prefetch2(pre[idx[3][r + QPF / 2]].hk);
+            const ConsumePre& q = pre[idx[3][r]];
+            adm[r] = d.stage_locked(karena[q.ka].data() + q.koff, q.klen, q.hk) ? 1 : 0;
+          }
+        }
+      });
+      // 3. ids of each kind's new names in the order of their first messages: a shard's fresh
+      //    entries are in its queue order, so a merge by first message numbers them (newmsg: the
+      //    fresh entries in id order, as (shard, index))
+      bool any_new = false;
+      size_t base[3];
+      for (int kk = 0; kk < 3; ++kk) {
+        Interner& in = nm->in[kk];
+        std::vector<uint32_t>& order = W.newmsg[kk];
+        order.clear();
+        base[kk] = in.strs.size();
+        // (each message introduces at most one name of a kind: the entries by first message, then
+        // read in message order)
+        std::vector<uint32_t>& owner = W.owner;
+        bool any = false;
+        for (uint32_t sh = 0; sh < NS && !any; ++sh) any = !in.sh[sh].fresh.empty();
+        if (!any) continue;
+        owner.assign(n, ~0u);
+        for (uint32_t sh = 0; sh < NS; ++sh)
+          for (uint32_t l = 0; l < in.sh[sh].fresh.size(); ++l) owner[in.sh[sh].fresh[l].first] = sh << 24 | l;
+        for (size_t i = 0; i < n; ++i)
+          if (owner[i] != ~0u) order.push_back(owner[i]);
+        for (Interner::Shard& d : in.sh) d.fresh_id.resize(d.fresh.size());
+        in.extend_tables(order.size());
+        in.reserve_stores(nt);
+        any_new = true;
+      }
+      if (any_new)
+        pool.run(nt, [&](uint32_t t) {
+          for (int kk = 0; kk < 3; ++kk) {
+            Interner& in = nm->in[kk];
+            // the new names stored and their id entries written, a range of ids per thread (by shard,
+            // the threads would write neighbouring ids: the same cache lines)
+            const std::vector<uint32_t>& order = W.newmsg[kk];
+            const size_t a = order.size() * t / nt, b = order.size() * (t + 1) / nt;
+            for (size_t r = a; r < b; ++r) {
+              Interner::Shard& d = in.sh[order[r] >> 24];
+              const uint32_t l = order[r] & 0xFFFFFF;
+              const Interner::Fresh& f = d.fresh[l];
+              const size_t id = base[kk] + r;
+              in.strs[id] = Interner::store(in.tstore[t], f.s, f.n);
+              in.lens[id] = f.n;
+              in.hs[id] = f.h;
+              d.fresh_id[l] = static_cast<uint32_t>(id);
+            }
+          }
+        });
+      if (any_new)
+        pool.run(nt, [&](uint32_t t) {  // (... and the shards' slots given the ids)
+          for (int kk = 0; kk < 3; ++kk)
+            for (uint32_t sh = t; sh < NS; sh += nt) {
+              Interner::Shard& d = nm->in[kk].sh[sh];
+              for (uint32_t l = 0; l < d.fresh.size(); ++l) {
+                const uint32_t id = d.fresh_id[l];
+                const uint64_t h = d.fresh[l].h;
+                d.ids.push_back(id);
+                for (uint64_t j = h & d.mask;; j = (j + 1) & d.mask)
+                  if (static_cast<uint32_t>(d.slot[j]) == (IN_PROV | l)) {
+                    d.slot[j] = (id + 1ull) | (h >> 32 << 32);
+                    break;
+                  }
+              }
+            }
+        });
+      // 4. the records, in message order (the rejected ones dropped): a new name's id through its
+      //    message's position in idx[] (the position of each message: counted again per range)
+      std::vector<uint32_t>* pos = W.pos;
+      for (int kk = 0; kk < 4; ++kk) pos[kk].resize(n);
+      pool.run(nt, [&](uint32_t t) {  // (each message's position in idx[kk], by its own range)
+        for (int kk = 0; kk < 4; ++kk)
+          for (uint32_t sh = 0; sh < NS; ++sh) {
+            // (the thread's messages of shard sh sit at [c0, c1) of the bucket, in message order)
+            const uint32_t c1 = cnt[(static_cast<size_t>(t) * 4 + kk) * NS + sh];
+            const uint32_t c0 = t == 0 ? start[kk][sh] : cnt[(static_cast<size_t>(t - 1) * 4 + kk) * NS + sh];
+            for (uint32_t r = c0; r < c1; ++r) pos[kk][idx[kk][r]] = r;
+          }
+      });
+      std::vector<uint32_t>& kbase = W.kbase;
+      kbase.assign(nt + 1, 0);
+      for (uint32_t t = 0; t < nt; ++t) {
+        const size_t i0 = n * t / nt, i1 = n * (t + 1) / nt;
+        uint32_t c = 0;
+        for (size_t i = i0; i < i1; ++i) c += pre[i].kind == 1 ? 0u : 1u;
+        kbase[t + 1] = kbase[t] + c;
+      }
+      auto id_of = [&](size_t i, int kk) -> uint32_t {
+        const uint32_t x = ref[kk][i];
+        if (x) return x - 1;
+        const uint32_t v = nref[kk][pos[kk][i]];
+        return nm->in[kk].sh[in_shard(hash_of(pre[i], kk))].fresh_id[v & ~IN_PROV];
+      };
+      std::vector<gome_consume_stats>& ps = W.ps;
+      ps.assign(nt, gome_consume_stats{});
+      pool.run(nt, [&](uint32_t t) {
+        const size_t i0 = n * t / nt, i1 = n * (t + 1) / nt;
+        gome_consume_stats c{};  // (the thread's own: ps[] entries share cache lines)
+        size_t kk = kbase[t];
+        for (size_t i = i0; i < i1; ++i) {
+          const Dec& d = dec[i];
+          const ConsumePre& q = pre[i];
+          c.not_objects += d.is_object ? 0 : 1;
+          if (q.kind == 0) {  // DoOrder ignores it (engine.go:46-54): a zero record
+            out[kk] = gome_order{};
+            if (msg_index) msg_index[kk] = static_cast<uint32_t>(i);
+            ++kk;
+            ++c.ignored;
+            continue;
+          }
+          if (q.kind == 1) {  // outside the engine's domain: not submitted (its marker was consumed)
+            ++c.rejected;
+            continue;
+          }
+          gome_order& r = out[kk];
+          r = gome_order{};
+          r.price_fx = q.p;
+          r.volume_fx = q.v;
+          r.symbol_id = id_of(i, 0);
+          r.uuid_id = id_of(i, 1);
+          r.oid_id = id_of(i, 2);
+          r.side = static_cast<uint8_t>(d.tx);
+          r.action = static_cast<uint8_t>(d.action);
+          if (d.action == GOME_ADD) {
+            const uint8_t ok = adm[pos[3][i]];
+            c.admitted += ok;
+            r.flags = static_cast<uint16_t>(GOME_ORD_ADM_HOST | (ok ? GOME_ORD_ADMITTED : 0));
+          } else {
+            r.flags = GOME_ORD_ADM_HOST;
+          }
+          if (msg_index) msg_index[kk] = static_cast<uint32_t>(i);
+          ++kk;
+        }
+        ps[t] = c;
+      });
+      for (Interner& in : nm->in)
+        for (Interner::Shard& d : in.sh) d.fresh.clear();
+      for (const gome_consume_stats& c : ps) {
+        s.not_objects += c.not_objects;
+        s.ignored += c.ignored;
+        s.rejected += c.rejected;
+        s.admitted += c.admitted;
+      }
+      k = kbase[nt];
+    }
+  }
+  if (!parallel) {
+    // The serial pass: one message after another, bound by its table probes' cache misses (the oid
+    // and marker tables hold millions of keys), so it prefetches the slots PF messages ahead.
+    constexpr size_t PF = 16;  // messages of prefetch distance
+    std::vector<std::unique_lock<std::mutex>> locks;  // (every marker shard, in shard order, once for the batch)
+    locks.reserve(PP_SHARDS);
+    for (PPShard& d : pp->sh) locks.emplace_back(d.mu);
+    for (size_t i = 0; i < n; ++i) {
+      if (i + PF < n && pre[i + PF].kind != 0) {
+        const ConsumePre& q = pre[i + PF];
         nm->in[0].prefetch(q.hs);
         nm->in[1].prefetch(q.hu);
         nm->in[2].prefetch(q.ho);
-        pp->prefetch(q.hk);
+        pp->of(q.hk).prefetch(q.hk);
       }
-    }
-    if (i + PF / 2 < n) {  // (the strings and marker keys the probes of message i + PF / 2 compare)
-      const Dec& f = dec[i + PF / 2];
-      if (f.action == GOME_ADD || f.action == GOME_DEL) {
-        const Pre& q = pre[i + PF / 2];
+      if (i + PF / 2 < n && pre[i + PF / 2].kind != 0) {  // (the strings and keys its probes compare)
+        const ConsumePre& q = pre[i + PF / 2];
         nm->in[0].prefetch2(q.hs);
         nm->in[1].prefetch2(q.hu);
         nm->in[2].prefetch2(q.ho);
-        pp->prefetch2(q.hk);
+        pp->of(q.hk).prefetch2(q.hk);
       }
-    }
-    const Dec& d = dec[i];
-    s.not_objects += d.is_object ? 0 : 1;
-    const int act = d.action;
-    if (act != GOME_ADD && act != GOME_DEL) {  // DoOrder ignores it (engine.go:46-54): a zero record
-      out[k] = gome_order{};
+      const Dec& d = dec[i];
+      s.not_objects += d.is_object ? 0 : 1;
+      const ConsumePre& q = pre[i];
+      if (q.kind == 0) {  // DoOrder ignores it (engine.go:46-54): a zero record
+        out[k] = gome_order{};
+        if (msg_index) msg_index[k] = static_cast<uint32_t>(i);
+        ++k;
+        ++s.ignored;
+        continue;
+      }
+      const char* sym = str_ptr(d.s[2], arenas);
+      const char* uuid = str_ptr(d.s[0], arenas);
+      const char* oid = str_ptr(d.s[1], arenas);
+      const size_t sl = d.s[2].len, ul = d.s[0].len, ol = d.s[1].len;
+      bool bad = q.kind == 1;
+      if (!bad && max_symbols) {
+        const int64_t sid = nm->in[0].find(sym ? sym : "", sl, q.hs);
+        const uint64_t would = sid >= 0 ? static_cast<uint64_t>(sid) : nm->in[0].strs.size();
+        bad = would >= max_symbols;
+      }
+      int32_t code = 0;
+      if (!bad) {
+        code = nm->tx_code(d.tx);
+        bad = code < 0;
+      }
+      const char* key = karena[q.ka].data() + q.koff;
+      PPShard& ps = pp->of(q.hk);
+      if (bad) {  // outside the engine's domain: not submitted (its marker is consumed as DoOrder would)
+        ++s.rejected;
+        ps.stage_locked(key, q.klen, q.hk);
+        continue;
+      }
+      gome_order& r = out[k];
+      r = gome_order{};
+      r.price_fx = q.p;
+      r.volume_fx = q.v;
+      r.symbol_id = nm->in[0].intern_h(sym ? sym : "", sl, q.hs);
+      r.uuid_id = nm->in[1].intern_h(uuid ? uuid : "", ul, q.hu);
+      r.oid_id = nm->in[2].intern_h(oid ? oid : "", ol, q.ho);
+      r.side = static_cast<uint8_t>(code);
+      r.action = static_cast<uint8_t>(d.action);
+      if (d.action == GOME_ADD) {
+        const bool ok = ps.stage_locked(key, q.klen, q.hk);
+        s.admitted += ok ? 1 : 0;
+        r.flags = static_cast<uint16_t>(GOME_ORD_ADM_HOST | (ok ? GOME_ORD_ADMITTED : 0));
+      } else {
+        ps.stage_locked(key, q.klen, q.hk);
+        r.flags = GOME_ORD_ADM_HOST;
+      }
       if (msg_index) msg_index[k] = static_cast<uint32_t>(i);
       ++k;
-      ++s.ignored;
-      continue;
     }
-    const Pre& q = pre[i];
-    const char* sym = str_ptr(d.s[2], arenas);
-    const char* uuid = str_ptr(d.s[0], arenas);
-    const char* oid = str_ptr(d.s[1], arenas);
-    const size_t sl = d.s[2].len, ul = d.s[0].len, ol = d.s[1].len;
-    int64_t p = 0, v = 0;
-    bool bad = gome_fixed_from_scaled(d.price, &p) != GOME_OK || gome_fixed_from_scaled(d.volume, &v) != GOME_OK || v < 0;
-    if (!bad && max_symbols) {
-      const int64_t sid = nm->in[0].find(sym ? sym : "", sl, q.hs);
-      const uint64_t would = sid >= 0 ? static_cast<uint64_t>(sid) : nm->in[0].strs.size();
-      bad = would >= max_symbols;
-    }
-    int32_t code = 0;
-    if (!bad) {
-      code = nm->tx_code(d.tx);
-      bad = code < 0;
-    }
-    const char* key = karena[q.ka].data() + q.koff;
-    if (bad) {  // outside the engine's domain: not submitted (its marker is consumed as DoOrder would)
-      ++s.rejected;
-      pp->stage_locked(key, q.klen, q.hk);
-      continue;
-    }
-    gome_order& r = out[k];
-    r.price_fx = p;
-    r.volume_fx = v;
-    r.symbol_id = nm->in[0].intern_h(sym ? sym : "", sl, q.hs);
-    r.uuid_id = nm->in[1].intern_h(uuid ? uuid : "", ul, q.hu);
-    r.oid_id = nm->in[2].intern_h(oid ? oid : "", ol, q.ho);
-    r.side = static_cast<uint8_t>(code);
-    r.action = static_cast<uint8_t>(act);
-    if (act == GOME_ADD) {
-      const bool ok = pp->stage_locked(key, q.klen, q.hk);
-      s.admitted += ok ? 1 : 0;
-      r.flags = static_cast<uint16_t>(GOME_ORD_ADM_HOST | (ok ? GOME_ORD_ADMITTED : 0));
-    } else {
-      pp->stage_locked(key, q.klen, q.hk);
-      r.flags = GOME_ORD_ADM_HOST;
-    }
-    if (msg_index) msg_index[k] = static_cast<uint32_t>(i);
-    ++k;
   }
   s.records = k;
+  s.queue_parallel = parallel ? 1 : 0;
   s.ns_decode = ns(t0, t1);
   s.ns_prepare = ns(t1, t2);
   s.ns_queue = ns(t2, clk::now());

@@ -112,7 +112,10 @@ typedef struct gome_consume_stats {
   uint64_t admitted;       /* ADDs whose marker existed                                        */
   uint64_t ns_decode;      /* wall time of the parallel decode                                 */
   uint64_t ns_prepare;     /* ... of the parallel pass that hashes and builds the marker keys  */
-  uint64_t ns_queue;       /* ... of the queue-order pass (interning, markers, records)        */
+  uint64_t ns_queue;       /* ... of the queue-order work (interning, markers, records)        */
+  uint64_t queue_parallel; /* 1: that work ran shard by shard on the pool; 0: message by message
+                              (a Transaction outside 0 / 1, or a Symbol range the batch could
+                              fill, keeps it serial; so does a batch below 2048 messages)      */
 } gome_consume_stats;
 /* Decode, convert and admit messages buf[off[i], off[i + 1]) in queue order.  out[] receives
  * *n_out <= n records (the rejected messages are dropped), msg_index[] (optional) each record's

@@ -9,6 +9,7 @@ syntax errors: the validator must agree byte for byte on what is JSON).  The sev
 engine reads are compared exactly (floats bit for bit).  Nesting deeper than Python's json can
 parse is checked against Go's documented limit (maxNestingDepth 10000) alone: parity unpinned
 there (the literal cannot parse it)."""
+import json
 import struct
 
 import numpy as np
@@ -182,6 +183,77 @@ def test_consume_records_and_markers():
     pre.commit()
     assert len(pre) == 0
     assert lib_names.count("sym") == 1 and lib_names.name("oid", 1) == "3"
+
+
+def _queue_batch(rng, n, odd_tx=False):
+    """A batch that exercises the queue-order rules: names new and seen (in and across batches),
+    repeated keys (a DEL of a same-batch ADD, an ADD repeated), markers set once, twice or never,
+    rejected and ignored messages."""
+    out = []
+    for k in range(n):
+        r = rng.random()
+        sym = f"S{int(rng.zipf(1.3)) % 300}"
+        uuid = f"u{int(rng.integers(40))}"
+        oid = str(int(rng.integers(3 * n)))  # (~1 in 6 repeats within the batch)
+        tx = 5 if odd_tx and rng.random() < 0.01 else int(rng.integers(2))
+        if r < 0.03:
+            out.append(_msg(oid=oid, sym=sym, uuid=uuid, vol="-5"))             # rejected (volume)
+        elif r < 0.05:
+            out.append(_msg(oid=oid, sym=sym, uuid=uuid, price="0.5"))          # rejected (not scaled)
+        elif r < 0.07:
+            out.append(_msg(action=3, oid=oid, sym=sym, uuid=uuid))             # ignored action
+        elif r < 0.08:
+            out.append("{bad")
+        else:
+            out.append(_msg(action=2 if r < 0.35 else 1, oid=oid, sym=sym, uuid=uuid, tx=tx,
+                            price=str(int(rng.integers(1, 100)) * 10**6)))
+    return out
+
+
+def _queue_run(batches, threads, marks, max_symbols=0):
+    names, pre = Names(), PrePool()
+    for s_, u_, o_ in marks:
+        pre.set(s_, u_, o_)
+    cons = BatchingConsumer(type("E", (), {"max_batch": 1 << 16, "max_symbols": max_symbols})(), pre, MatchSink(),
+                            names, threads=threads)
+    outs = []
+    for i, b in enumerate(batches):
+        rec = cons.records(b)
+        outs.append((rec.copy(), cons.rejected, len(pre)))
+        if i % 3 == 1:
+            pre.abort()
+            rec = cons.records(b)  # (the same batch again after a refusal: the same verdicts)
+            outs.append((rec.copy(), cons.rejected, len(pre)))
+        pre.commit()
+        for s_, u_, o_ in marks[i::len(batches)]:  # (the gRPC side re-sets some markers between batches)
+            pre.set(s_, u_, o_)
+    tables = {k: [names.name(k, j) for j in range(names.count(k))] for k in ("sym", "uuid", "oid")}
+    _queue_run.parallel = cons.parallel_batches
+    return outs, tables, len(pre)
+
+
+@pytest.mark.parametrize("odd_tx,max_symbols", [(False, 0), (False, 280), (True, 0)])
+def test_parallel_queue_pass_matches_the_serial_one(odd_tx, max_symbols):
+    """Round 6: gome_consume_order_nodes interns a batch's new names shard by shard (numbered by
+    their first message) and stages its markers shard by shard on its worker pool, instead of one
+    message after another.  The records, admission verdicts, rejections, the name tables (id by id)
+    and the markers left must be the serial pass's (threads = 1) exactly, over batches that repeat
+    names and keys within and across batches, abort and re-consume, and re-set markers; with odd
+    Transactions or a Symbol range that the batch could fill, the batch takes the serial pass."""
+    rng = np.random.default_rng(11 + max_symbols + odd_tx)
+    batches = [_queue_batch(rng, 6000, odd_tx) for _ in range(5)]
+    adds = [json.loads(m) for b in batches for m in b if m.startswith('{"Action":1')]
+    marks = [(a["Symbol"], a["Uuid"], a["Oid"]) for a in adds if rng.random() < 0.5]
+    par = _queue_run(batches, 8, marks, max_symbols)
+    npar = _queue_run.parallel
+    ser = _queue_run(batches, 1, marks, max_symbols)
+    assert _queue_run.parallel == 0
+    assert npar == (0 if (odd_tx or max_symbols) else 7), npar  # (5 batches, 2 consumed twice)
+    assert par[1] == ser[1] and par[2] == ser[2]
+    for (ra, ja, pa), (rb, jb, pb) in zip(par[0], ser[0]):
+        assert ja == jb and pa == pb
+        assert np.array_equal(ra, rb)
+    assert sum(int((r["flags"] == 3).sum()) for r, _, _ in par[0]) > 1000  # (admitted ADDs)
 
 
 def test_pack_messages_offsets():

@@ -3246,18 +3246,19 @@ __global__ __launch_bounds__(FL_TILE) void k_flow_sort_scatter(Dev D, FlowArgs F
 }
 
 // Books planned with zero-volume ADDs (Q6, k_flow_prep_b) or holding zero-volume makers (FlowLvl::z0):
-// the reconstruction takes a zero-volume maker where no order reaches it, and (ADD books) where a
-// consume passes it with volume to spare at the level (it pops it with a 0-fill, engine.go:145-161).  One block
+// the reconstruction takes a zero-volume maker where no order reaches it, and where a consume passes
+// it or goes on past the level's end (it pops it with a 0-fill, engine.go:145-161).  One block
 // per (book, level), the level's run in time order with block scans; hazards (FlowHdr::haz, handed
 // over by k_flow_stale_check):
 //  * a REST of 0 while the level's depth is 0: the reference makes it a side-set member of depth 0
 //    (SetPoolDepth, engine.go:78-80), which the plans, seeing depth 0 as "no level", would not visit;
 //  * after a zero-volume maker may be in the FIFO (z0, or a REST of 0 earlier in the run): a CONS that
-//    empties the level or a CONS of 0 (ADD books), any CONS (cancel books).
+//    empties the level and stops there, or a CONS of 0 (ADD books: it meets the maker; cancel books:
+//    the maker may be its head).
 // A REST of 0 with depth > 0 is an ordinary FIFO append (fl_wplan), popped by the first consume
-// that passes it (fl_first_back; the gather in fl_level_one).  Books with
-// DELs (the cancel path): a cancel lowers the depth like a CONS; a CONS of 0 (a zero-volume taker,
-// whose one 0-fill the cancel path's events do not model) is a hazard as well.
+// that passes it (fl_first_back; the gather in fl_level_one).  Books with DELs (the cancel path): a
+// cancel lowers the depth like a CONS, and one that empties the level beside a zero-volume maker is a
+// hazard too.
 // Wave-wide exclusive scans (one wave per level: the checks run in the rare batches that need them,
 // and a launch of small blocks gets onto busy CUs at once; 1024-thread blocks waited ~0.8 ms for
 // room on config 5c's critical path even when every block had nothing to do).
@@ -3317,14 +3318,16 @@ __global__ __launch_bounds__(64) void k_flow_zero_check(Dev D, FlowArgs F) {
       // cancel that empties the level while some W >= the consumption after it (the maker may still
       // be in the FIFO, which the reference leaves in place, its level out of its set) is a hazard,
       // unless it is a consume that goes on and pops them (fl_cont); so are a REST of 0 at depth 0 and a
-      // CONS of 0 (a zero-volume taker, whose 0-fill the cancel events do not model).  Old zero-volume
+      // CONS of 0 (a zero-volume taker) where a zero-volume maker may be its head.  Old zero-volume
       // makers: W = d0.
       int64_t twm;
       const int64_t wm = max(wlast, fl_wave_max_excl(zr ? before + cb : -1, &twm));
       const int64_t cend = cb + (isc ? e.amt : 0);
       const bool present = (Lq->z0 && d0 >= cend) || wm >= cend;
       const bool empt = before - e.amt == 0 && present;
-      hz |= (zr && before == 0 ? HZ_ZREST0 : 0u) | (isc && e.amt == 0 ? HZ_ZCONS0 : 0u) |
+      // (a CONS of 0 fills the head of the FIFO, fc_head_at; if that may be a zero-volume maker,
+      // diff == 0 pops it: the hazard)
+      hz |= (zr && before == 0 ? HZ_ZREST0 : 0u) | (isc && e.amt == 0 && (Lq->z0 || wm >= 0) ? HZ_ZCONS0 : 0u) |
             (isc && !cont && empt ? HZ_ZSTOP : 0u) | (isx && empt ? HZ_ZDELEMPTY : 0u);
       wlast = max(wlast, twm);
     } else {

@@ -1036,7 +1036,7 @@ __device__ __forceinline__ void fc_level_one(const Dev& D, const FlowArgs& F, ui
 #endif
   // 1. each cancel -> its DEL's record (r, touch); the consumption cursor before each consume
   int64_t cc = 0, ocan = 0;
-  uint32_t nr = 0, ncan_old = 0;
+  uint32_t nr = 0, ncan_old = 0, ncons = 0;
   for (uint32_t c0 = 0; c0 < cnt; c0 += 64) {
     const uint32_t i = c0 + lane;
     const bool valid = i < cnt;
@@ -1054,6 +1054,7 @@ __device__ __forceinline__ void fc_level_one(const Dev& D, const FlowArgs& F, ui
     if (isc) R[i].coord = cc + ic - ac;
     cc += rl64(ic, 63);
     nr += __popcll(__ballot(valid && e.kind == TK_REST));
+    ncons += __popcll(__ballot(isc));
   }
   for (int off = 32; off > 0; off >>= 1) {
     ocan += __shfl_xor(ocan, off);
@@ -1111,7 +1112,8 @@ __device__ __forceinline__ void fc_level_one(const Dev& D, const FlowArgs& F, ui
   uint32_t ttail = tail, ttslot = tslot;
   uint32_t ig_base = 0, ng = 0, consumed = 0, zpopped = 0;
   bool ig_all = true;
-  if (nv0 > 0 && (cfin > 0 || uni(Lq->c_old))) {
+  // (a CONS of 0 -- a zero-volume taker -- reads the head even when nothing was consumed)
+  if (nv0 > 0 && (cfin > 0 || uni(Lq->c_old) || ncons)) {
     uint32_t bb = 0;
     if (lane == 0) bb = atomicAdd(F.ig_bump, nv0);
     ig_base = uni(bb);
@@ -1246,7 +1248,7 @@ __device__ __forceinline__ void fc_level_lane(const Dev& D, const FlowArgs& F, u
   RsEnt* RS = F.rs + L + base;
   // 1. cancels -> their DEL records; the consumption cursor before each consume
   int64_t cc = 0, ocan = 0;
-  uint32_t nr = 0, ncan_old = 0;
+  uint32_t nr = 0, ncan_old = 0, ncons = 0;
   for (uint32_t i = 0; i < cnt; ++i) {
     const SEnt e = R[i];
     if (e.kind == TK_CANC) {
@@ -1257,6 +1259,7 @@ __device__ __forceinline__ void fc_level_lane(const Dev& D, const FlowArgs& F, u
     } else if (e.kind == TK_CONS) {
       R[i].coord = cc;
       cc += e.amt;
+      ++ncons;
     } else if (e.kind == TK_REST) {
       nr++;
     }
@@ -1293,7 +1296,7 @@ __device__ __forceinline__ void fc_level_lane(const Dev& D, const FlowArgs& F, u
   uint32_t ttail = tail, ttslot = tslot;
   uint32_t ig_base = 0, ng = 0, consumed = 0, zpopped = 0;
   bool ig_all = true;
-  if (nv0 > 0 && (cfin > 0 || Lq->c_old)) {
+  if (nv0 > 0 && (cfin > 0 || Lq->c_old || ncons)) {  // (fc_level_one)
     ig_base = atomicAdd(F.ig_bump, nv0);
     if (static_cast<unsigned long long>(ig_base) + nv0 > F.ig_cap) {
       atomicOr(&D.st->err, ERR_CHUNKS);
@@ -1394,7 +1397,7 @@ constexpr uint32_t FC_BIG = 1024;
 // which one wave walks 64 at a time); the old FIFO's gather stays with wave 0.
 __device__ __forceinline__ void fc_level_blk(const Dev& D, const FlowArgs& F, uint32_t h, uint32_t q) {
   __shared__ int64_t red_s[2];
-  __shared__ uint32_t nr_s, ncan_s;
+  __shared__ uint32_t nr_s, ncan_s, ncons_s;
   const FlowHdr* hd = &F.hdr[h];
   const uint32_t tid = threadIdx.x, lane = lane_id();
   FlowLvl* Lq = fl_lvls(F, h) + q;  // (a lane book's F.lvl row, or a deep book's level table)
@@ -1405,13 +1408,13 @@ __device__ __forceinline__ void fc_level_blk(const Dev& D, const FlowArgs& F, ui
   const int64_t d0 = Lq->d0;
   SEnt* R = F.srt + L + base;
   RsEnt* RS = F.rs + L + base;
-  if (tid == 0) { red_s[0] = 0; nr_s = 0; ncan_s = 0; }
+  if (tid == 0) { red_s[0] = 0; nr_s = 0; ncan_s = 0; ncons_s = 0; }
   __syncthreads();
   // 1. each cancel -> its DEL's record (r, touch); the consumption cursor before each consume.
   //    FC_K consecutive touches per thread: their loads in flight together, a quarter of the
   //    block scans (a busy level is tens of thousands of touches)
   int64_t cc = 0, ocan = 0;
-  uint32_t nr = 0, ncan_old = 0;
+  uint32_t nr = 0, ncan_old = 0, nc = 0;
   for (uint32_t c0 = 0; c0 < cnt; c0 += FC_LVB_T * FC_K) {
     const uint32_t i0 = c0 + tid * FC_K;
     SEnt e[FC_K];
@@ -1430,6 +1433,7 @@ __device__ __forceinline__ void fc_level_blk(const Dev& D, const FlowArgs& F, ui
       }
       sum += e[u].kind == TK_CONS ? e[u].amt : 0;
       nr += e[u].kind == TK_REST ? 1u : 0u;
+      nc += e[u].kind == TK_CONS ? 1u : 0u;
     }
     int64_t tot;
     int64_t run = cc + fl_blk_excl(sum, &tot);
@@ -1444,6 +1448,7 @@ __device__ __forceinline__ void fc_level_blk(const Dev& D, const FlowArgs& F, ui
   if (ocan) atomicAdd(reinterpret_cast<unsigned long long*>(&red_s[0]), static_cast<unsigned long long>(ocan));
   if (nr) atomicAdd(&nr_s, nr);
   if (ncan_old) atomicAdd(&ncan_s, ncan_old);
+  if (nc) atomicAdd(&ncons_s, nc);
   __threadfence();  // the DEL records are read back below (by other threads)
   __syncthreads();
   const int64_t ocan_t = red_s[0];
@@ -1507,7 +1512,7 @@ __device__ __forceinline__ void fc_level_blk(const Dev& D, const FlowArgs& F, ui
   uint32_t ttail = tail, ttslot = tslot;
   uint32_t ig_base = 0, ng = 0, consumed = 0, zpopped = 0;
   bool ig_all = true;
-  if (nv0 > 0 && (cfin > 0 || Lq->c_old)) {
+  if (nv0 > 0 && (cfin > 0 || Lq->c_old || ncons_s)) {  // (fc_level_one)
     uint32_t bb = 0;
     if (lane == 0) bb = atomicAdd(F.ig_bump, nv0);
     ig_base = uni(bb);
@@ -1647,6 +1652,24 @@ struct FcTouch {
   bool cont;              // the consume went on past the level (fl_cont; levels with zero-volume makers)
 };
 
+// The head of a level's FIFO when the consume at cursor c, log index t, came (a zero-volume taker:
+// MatchOrder fills its first node, engine.go:138-198).  f = fc_find(c).  A maker spanning c is
+// partly consumed, so live: the head.  Makers starting at c with length 0 were cancelled before any
+// consumption -- after t some of them, which were live at t and ahead of the one with volume: the
+// first of those that had arrived and was not yet cancelled at t is the head.  (A zero-volume maker
+// there is a hazard, k_flow_zero_check: diff == 0 pops it.)
+__device__ __forceinline__ uint32_t fc_head_at(const FcLvlView& V, uint32_t f, int64_t c, uint32_t t) {
+  if (fc_start(V, f) != c) return f;
+  uint32_t m = f;
+  while (m > 0 && fc_start(V, m - 1) == c) --m;
+  for (; m < f; ++m) {
+    const bool arrived = m < V.ig_n || V.RS[m - V.ig_n].t < t;
+    const uint32_t ct = fc_ct(V, m);
+    if (arrived && (ct == NIL || ct > t)) return m;
+  }
+  return f;
+}
+
 // t: the touch's log index (book-local)
 __device__ __forceinline__ FcTouch fc_touch(const FlowArgs& F, uint32_t h, uint32_t L, const Touch& x, uint32_t t) {
   FcTouch T;
@@ -1657,6 +1680,10 @@ __device__ __forceinline__ FcTouch fc_touch(const FlowArgs& F, uint32_t h, uint3
   T.a = x.amt;
   T.first = fc_find(T.V, T.c);
   T.cont = false;
+  if (T.a == 0) {  // a zero-volume taker (Q6): one 0-fill, of the FIFO's head at its time
+    T.first = T.last = fc_head_at(T.V, T.first, T.c, t);
+    return T;
+  }
   // a level that may hold zero-volume makers (Q6): the ones starting at the cursor are popped by
   // this consume too (they share the start of the maker fc_find lands on; fl_first_back), unless
   // the consume before it went on and popped them; a consume that goes on pops the ones at its end
@@ -1697,6 +1724,7 @@ __device__ __forceinline__ bool fc_fills(const FcLvlView& V, uint32_t m, int64_t
 __device__ __forceinline__ uint32_t fc_nfills(const FcTouch& T, uint32_t& pops) {
   uint32_t nf = 0;
   pops = 0;
+  if (T.a == 0) return 1;  // (a zero-volume taker: one 0-fill, nothing popped)
   for (uint32_t m = T.first; m <= T.last; ++m) {
     if (!fc_fills(T.V, m, T.c, T.a, T.cont)) continue;
     ++nf;
@@ -1838,7 +1866,7 @@ __global__ __launch_bounds__(256) void k_fc_events(Dev D, BatchArgs B, FlowArgs 
     const uint32_t fb = F.fbase[L + t];
     uint32_t k = 0;
     for (uint32_t m = T.first; m <= T.last; ++m) {
-      if (!fc_fills(V, m, T.c, T.a, T.cont)) continue;
+      if (T.a > 0 && !fc_fills(V, m, T.c, T.a, T.cont)) continue;  // (a zero-volume taker: its head)
       const int64_t len = fc_len(V, m);
       const int64_t e = fc_start(V, m), v = fc_vol(V, m);
       uint32_t oid, uuid, tx;

@@ -357,3 +357,23 @@ def test_zero_volume_maker_at_the_end_of_a_swept_level_with_dels_stays_on_the_fl
     out = _zero_run(51, edit)
     assert out[2][0] != 0 and out[2][1] >= 1 and out[2][2] == 0, out
     assert all(k != 0 for k, _, _ in out), out
+
+
+def test_zero_volume_takers_in_a_batch_with_dels_stay_on_the_flow_path():
+    """Zero-volume takers on the cancel path (round 6): the batch of the zero-taker test above plus a
+    DEL (a maker of the lowest bid), so the book takes the cancel plan.  Each taker's CONS of 0 fills
+    the head of the best opposite level's FIFO at its time (fc_head_at: the first maker then live,
+    a maker cancelled later included) with one 0-fill; exact, the book on the flow path."""
+    def edit(b, hot, eng):
+        lv = eng.levels(hot)
+        bids = np.sort(lv[(lv["in_buy"] != 0) & (lv["n_nodes"] > 0)], order="price_fx")
+        rows = _hot_rows(b, hot)
+        _del_of(b, rows[0], eng, hot, bids[0]["price_fx"])
+        picks = rows[(np.array([0.0002, 0.01, 0.3, 0.6, 0.95]) * len(rows)).astype(int)]
+        for k, r in enumerate(picks):
+            sale = k % 2 == 1
+            b["volume_fx"][r], b["side"][r] = 0, 1 if sale else 0
+            b["price_fx"][r] = 10 ** 6 if sale else 10 ** 8
+    out = _zero_run(52, edit)
+    assert out[2][0] != 0 and out[2][1] >= 1 and out[2][2] == 0, out
+    assert all(k != 0 for k, _, _ in out), out

@@ -255,7 +255,7 @@ def cpu_baseline(batches, n_symbols, budget_s, threads=1):
     return one, (done / wall, done, wall, used)
 
 
-def consumer_leg(workload, n_symbols, n_msgs, seed, batch=1 << 15, threads=8):
+def consumer_leg(workload, n_symbols, n_msgs, seed, batch=1 << 15, threads=8, render_threads=None):
     """The drop-in boundary's own rate: n_msgs doOrder messages (the
     OrderNode JSON bodies the gRPC side enqueues, main.go:39-52 / ordernode.go:9-36, admission markers
     set) of the same workload through BatchingConsumer.process_stream -- native Go-Unmarshal decode on
@@ -279,7 +279,7 @@ def consumer_leg(workload, n_symbols, n_msgs, seed, batch=1 << 15, threads=8):
             pre.set("s%d" % r["symbol_id"], str(int(r["uuid_id"])), str(int(r["oid_id"])))
     eng = Engine(max_symbols=n_symbols, max_batch=batch, max_nodes=2 * n_msgs + (1 << 20),
                  max_levels=(1 << 22) + 2 * n_msgs)
-    cons = BatchingConsumer(eng, pre, sink, names, max_batch=batch, threads=threads)
+    cons = BatchingConsumer(eng, pre, sink, names, max_batch=batch, threads=threads, render_threads=render_threads)
     # the deliveries as one buffer of bodies + offsets (how an AMQP client reads them off its socket;
     # PackedQueue), two batches in flight (process_stream: decode and H2D of batch k+1 beside the
     # device's batch k, each batch rendered as it is collected)
@@ -319,6 +319,7 @@ def consumer_leg(workload, n_symbols, n_msgs, seed, batch=1 << 15, threads=8):
     nev = sum(len(e) for e in evs)
     out = {"messages": n_msgs, "batch": batch, "messages_per_s": round(n_msgs / wall, 1),
            "matchresults_per_s": round(lines / wall, 1), "matchresults": lines, "threads": threads,
+           "render_threads": cons.render_threads,
            "path": "OrderNode JSON deliveries (one buffer + offsets) -> BatchingConsumer.process_stream "
                    "(gome_consume_order_nodes: decode, convert, intern, admit into page-locked records; "
                    "gome_submit_batch_async, two batches in flight; gome_collect; gome_render_events_names "
@@ -412,6 +413,8 @@ def main():
                          "cancels (Q2) of a bid level and a zero-volume ADD (Q6), or (zero) zero-volume "
                          "ADDs only (workload.inject_quirks); "
                          "the line's quirk_batch reports that batch's device time beside its neighbours'")
+    ap.add_argument("--consumer-render-threads", type=int, default=0,
+                    help="the consumer leg's render threads (0: as many as its 8 decode threads)")
     ap.add_argument("--consumer-msgs", type=int, default=1 << 17,
                     help="JSON OrderNode messages of the consumer leg (0: off)")
     ap.add_argument("--pool-nodes", type=int, default=0, help="gome_config.max_nodes (0: sized from the run)")
@@ -755,7 +758,8 @@ def main():
     consumer = None
     if rank == 0 and world == 1 and args.consumer_msgs > 0:
         note(f"consumer leg ({args.consumer_msgs} JSON messages)")
-        consumer = consumer_leg(args.workload, n_symbols, args.consumer_msgs, args.seed)
+        consumer = consumer_leg(args.workload, n_symbols, args.consumer_msgs, args.seed,
+                                render_threads=args.consumer_render_threads or None)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

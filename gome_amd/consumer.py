@@ -326,13 +326,17 @@ class BatchingConsumer:
     interning, admission in queue order; gome_render_events_mt: the MatchResult lines)."""
 
     def __init__(self, engine, prepool: PrePool, sink: MatchSink, names: Names | None = None,
-                 max_batch: int | None = None, max_wait_us: int = 200, accuracy: int = 8, threads: int = 8):
+                 max_batch: int | None = None, max_wait_us: int = 200, accuracy: int = 8, threads: int = 8,
+                 render_threads: int | None = None):
         self.eng, self.pre, self.sink = engine, prepool, sink
         self.names = names or Names()
         self.max_batch = int(max_batch or engine.max_batch)
         self.max_wait = max_wait_us * 1e-6
         self.acc = accuracy
         self.threads = threads
+        # (the render's pool: as many threads as the decode's by default -- half measured slower on
+        # the GPU box, the render then outlasting the next batch's decode, gpurun_out/r06v)
+        self.render_threads = render_threads or threads
         self.lib = load_library()
         self.max_symbols = getattr(engine, "max_symbols", None)
         self.seq = 0
@@ -398,7 +402,7 @@ class BatchingConsumer:
             # thread while this thread interns the next batch's names, which may move a table)
             k = self.lib.gome_render_events_names(
                 ev.ctypes.data, len(ev), rec.ctypes.data, len(rec), seq_base, self.acc, self.names.h,
-                self.threads, out.ctypes.data, cap)
+                self.render_threads, out.ctypes.data, cap)
             if k >= 0:
                 return memoryview(out)[:k]
             if k == -(1 << 63):

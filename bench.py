@@ -255,7 +255,7 @@ def cpu_baseline(batches, n_symbols, budget_s, threads=1):
     return one, (done / wall, done, wall, used)
 
 
-def consumer_leg(workload, n_symbols, n_msgs, seed, batch=1 << 15, threads=8, render_threads=None):
+def consumer_leg(workload, n_symbols, n_msgs, seed, batch=1 << 15, threads=8, render_threads=None, warm_batches=4):
     """The drop-in boundary's own rate: n_msgs doOrder messages (the
     OrderNode JSON bodies the gRPC side enqueues, main.go:39-52 / ordernode.go:9-36, admission markers
     set) of the same workload through BatchingConsumer.process_stream -- native Go-Unmarshal decode on
@@ -263,12 +263,17 @@ def consumer_leg(workload, n_symbols, n_msgs, seed, batch=1 << 15, threads=8, re
     batches in flight on the engine (gome_submit_batch_async / gome_collect), gome_render_events_mt
     into MatchResult lines on the sink (rabbitmq.go:116-125, engine.go:154-194); then the same
     messages through process() as Python objects (round 5's leg) and the renderer alone over the
-    same events at 1 and `threads` threads."""
+    same events at 1 and `threads` threads.  Both consumers first take `warm_batches` batches of the
+    same stream, untimed (as the main leg's warmup steps): the first batches of a process pay one-time
+    costs -- the engine's second stream set is made when the first batch no book dominated is
+    collected (46 ms on config 2's third submit, tools/consumer_submit_probe.py), the pools' threads
+    start, the scratch is faulted in -- which that pass's own rate (`cold_messages_per_s`) shows."""
     import ctypes as C
     from gome_amd.abi import Engine
     from gome_amd.consumer import BatchingConsumer, MatchSink, Names, PrePool, _order_node_json
     gen, _, _ = make_stream(workload, 0, 1, seed + 7)
-    rec = gen(n_msgs).copy()
+    n_warm = warm_batches * batch
+    rec = gen(n_warm + n_msgs).copy()
     msgs = [_order_node_json(dict(symbol="s%d" % r["symbol_id"], uuid=str(int(r["uuid_id"])),
                                   oid=str(int(r["oid_id"])), transaction=int(r["side"])),
                              int(r["action"]), float(r["price_fx"]), float(r["volume_fx"]), 8).encode()
@@ -277,14 +282,20 @@ def consumer_leg(workload, n_symbols, n_msgs, seed, batch=1 << 15, threads=8, re
     for r in rec:
         if r["action"] == wl.ADD:
             pre.set("s%d" % r["symbol_id"], str(int(r["uuid_id"])), str(int(r["oid_id"])))
-    eng = Engine(max_symbols=n_symbols, max_batch=batch, max_nodes=2 * n_msgs + (1 << 20),
-                 max_levels=(1 << 22) + 2 * n_msgs)
+    eng = Engine(max_symbols=n_symbols, max_batch=batch, max_nodes=2 * (n_warm + n_msgs) + (1 << 20),
+                 max_levels=(1 << 22) + 2 * (n_warm + n_msgs))
     cons = BatchingConsumer(eng, pre, sink, names, max_batch=batch, threads=threads, render_threads=render_threads)
     # the deliveries as one buffer of bodies + offsets (how an AMQP client reads them off its socket;
     # PackedQueue), two batches in flight (process_stream: decode and H2D of batch k+1 beside the
     # device's batch k, each batch rendered as it is collected)
     from gome_amd.consumer import PackedQueue
-    packed = PackedQueue(msgs)
+    t = time.perf_counter()
+    lines_warm = cons.process_stream(PackedQueue(msgs[:n_warm]).batches(batch)) if n_warm else 0
+    wall_warm = time.perf_counter() - t
+    for k in cons.phase_s:
+        cons.phase_s[k] = 0.0
+    cons.queue_steps_s = [0.0] * len(cons.queue_steps_s)
+    packed = PackedQueue(msgs[n_warm:])
     t = time.perf_counter()
     lines = cons.process_stream(packed.batches(batch))
     wall = time.perf_counter() - t
@@ -295,8 +306,8 @@ def consumer_leg(workload, n_symbols, n_msgs, seed, batch=1 << 15, threads=8, re
     for r in rec:
         if r["action"] == wl.ADD:
             pre2.set("s%d" % r["symbol_id"], str(int(r["uuid_id"])), str(int(r["oid_id"])))
-    eng2 = Engine(max_symbols=n_symbols, max_batch=batch, max_nodes=2 * n_msgs + (1 << 20),
-                  max_levels=(1 << 22) + 2 * n_msgs)
+    eng2 = Engine(max_symbols=n_symbols, max_batch=batch, max_nodes=2 * (n_warm + n_msgs) + (1 << 20),
+                  max_levels=(1 << 22) + 2 * (n_warm + n_msgs))
     cons2 = BatchingConsumer(eng2, pre2, sink2, names2, max_batch=batch, threads=threads)
     evs, recs, bases = [], [], []
     orig_render = cons2.render_block
@@ -306,19 +317,22 @@ def consumer_leg(workload, n_symbols, n_msgs, seed, batch=1 << 15, threads=8, re
         recs.append(rc.copy())
         bases.append(base)
         return orig_render(ev, rc, base)
+    lines2 = 0
+    for k in range(0, n_warm, batch):
+        lines2 += cons2.process(msgs[k:k + batch])
     cons2.render_block = keep
     t2 = time.perf_counter()
-    lines2 = 0
-    for k in range(0, n_msgs, batch):
+    for k in range(n_warm, n_warm + n_msgs, batch):
         lines2 += cons2.process(msgs[k:k + batch])
     wall2 = time.perf_counter() - t2
-    same = lines2 == lines and sink2.q == sink.q
+    same = lines2 == lines + lines_warm and sink2.q == sink.q
     eng2.close()
     lib = cons.lib
     N = names2
     nev = sum(len(e) for e in evs)
     out = {"messages": n_msgs, "batch": batch, "messages_per_s": round(n_msgs / wall, 1),
            "matchresults_per_s": round(lines / wall, 1), "matchresults": lines, "threads": threads,
+           "warm_messages": n_warm, "cold_messages_per_s": round(n_warm / wall_warm, 1) if n_warm else None,
            "render_threads": cons.render_threads,
            "path": "OrderNode JSON deliveries (one buffer + offsets) -> BatchingConsumer.process_stream "
                    "(gome_consume_order_nodes: decode, convert, intern, admit into page-locked records; "
@@ -326,6 +340,7 @@ def consumer_leg(workload, n_symbols, n_msgs, seed, batch=1 << 15, threads=8, re
                    "on a helper thread, beside the next batch's decode, straight into the sink's block) -> "
                    "MatchResult lines on the sink; host_ms.native_*: the consume call's own split",
            "host_ms": phases,
+           "queue_steps_ms": [round(v * 1e3, 2) for v in cons.queue_steps_s],
            "list_messages_per_s": round(n_msgs / wall2, 1),
            "list_path": "the same messages as Python bytes objects through BatchingConsumer.process, one "
                         "synchronous batch at a time (packing included); sink bytes identical: " + str(same),
@@ -415,8 +430,10 @@ def main():
                          "the line's quirk_batch reports that batch's device time beside its neighbours'")
     ap.add_argument("--consumer-render-threads", type=int, default=0,
                     help="the consumer leg's render threads (0: as many as its 8 decode threads)")
-    ap.add_argument("--consumer-msgs", type=int, default=1 << 17,
-                    help="JSON OrderNode messages of the consumer leg (0: off)")
+    ap.add_argument("--consumer-msgs", type=int, default=1 << 18,
+                    help="JSON OrderNode messages of the consumer leg, timed (0: off)")
+    ap.add_argument("--consumer-warm-batches", type=int, default=4,
+                    help="batches of the consumer leg's stream taken untimed first (one-time costs)")
     ap.add_argument("--pool-nodes", type=int, default=0, help="gome_config.max_nodes (0: sized from the run)")
     ap.add_argument("--pool-levels", type=int, default=0, help="gome_config.max_levels (0: sized from the run)")
     ap.add_argument("--scaling", choices=("weak", "strong"), default="strong",
@@ -759,7 +776,8 @@ def main():
     if rank == 0 and world == 1 and args.consumer_msgs > 0:
         note(f"consumer leg ({args.consumer_msgs} JSON messages)")
         consumer = consumer_leg(args.workload, n_symbols, args.consumer_msgs, args.seed,
-                                render_threads=args.consumer_render_threads or None)
+                                render_threads=args.consumer_render_threads or None,
+                                warm_batches=args.consumer_warm_batches)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

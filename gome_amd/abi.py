@@ -196,6 +196,8 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.gome_decode_order_nodes.restype = C.c_int64
     lib.gome_consume_order_nodes.argtypes = [VP, VP, VP, VP, SZ, C.c_uint32, C.c_uint32, VP, VP, P(SZ), VP]
     lib.gome_consume_order_nodes.restype = C.c_int32
+    lib.gome_consume_last_steps.argtypes = [VP, VP, SZ]
+    lib.gome_consume_last_steps.restype = SZ
     lib.gome_gen_create.argtypes = [VP, P(VP)]
     lib.gome_gen_batch.argtypes = [VP, VP, C.c_size_t]
     lib.gome_gen_shares.argtypes = [VP, P(C.c_double), P(C.c_double)]

@@ -346,6 +346,8 @@ class BatchingConsumer:
         self.phase_s = {"records": 0.0, "submit": 0.0, "collect": 0.0, "render": 0.0,
                         "native_decode": 0.0, "native_prepare": 0.0, "native_queue": 0.0}
         self.parallel_batches = 0  # (batches whose queue-order work ran shard by shard)
+        # the parallel queue-order path's steps (s, summed over batches; gome_consume_last_steps)
+        self.queue_steps_s = [0.0] * 10
 
     # ---- draining ------------------------------------------------------------------
     def drain(self, q, block_s: float = 0.0) -> list:
@@ -390,6 +392,10 @@ class BatchingConsumer:
         for k in ("decode", "prepare", "queue"):  # (the native call's own split, seconds)
             self.phase_s["native_" + k] += getattr(st, "ns_" + k) * 1e-9
         self.parallel_batches += int(st.queue_parallel)
+        steps = (C.c_uint64 * len(self.queue_steps_s))()
+        self.lib.gome_consume_last_steps(self.names.h, steps, len(steps))
+        for i, v in enumerate(steps):
+            self.queue_steps_s[i] += v * 1e-9
         return rec[:got.value]
 
     def render_block(self, ev: np.ndarray, rec: np.ndarray, seq_base: int):

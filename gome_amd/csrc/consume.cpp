@@ -720,6 +720,7 @@ struct ConsumeScratch {
   std::vector<uint32_t> idx[4], pos[4], start[4], ref[3], first[3], newmsg[3], owner;
   std::vector<uint8_t> adm;
   std::vector<gome_consume_stats> ps;
+  uint64_t step_ns[GOME_CONSUME_STEPS] = {};  // the last call's parallel queue-order steps (gome_consume_last_steps)
 };
 }  // namespace
 
@@ -913,6 +914,13 @@ const char* const* gome_names_table(gome_names* nm, int kind) {
 
 int32_t gome_names_tx_code(gome_names* nm, int32_t raw) { return nm ? nm->tx_code(raw) : -1; }
 
+size_t gome_consume_last_steps(const gome_names* nm, uint64_t* ns, size_t n) {
+  if (!nm) return 0;
+  const size_t k = std::min<size_t>(n, GOME_CONSUME_STEPS);
+  for (size_t i = 0; ns && i < k; ++i) ns[i] = nm->scratch.step_ns[i];
+  return GOME_CONSUME_STEPS;
+}
+
 int64_t gome_render_events_names(const gome_event* ev, size_t n, const gome_order* batch, size_t batch_n,
                                  uint64_t seq_base, uint32_t accuracy, gome_names* nm, uint32_t threads, char* buf,
                                  size_t cap) {
@@ -1087,6 +1095,13 @@ gome_status gome_consume_order_nodes(gome_names* nm, gome_prepool* pp, const cha
   for (uint32_t t = 0; t < nt; ++t) odd += odd_tx[t];
   bool parallel = nt > 1 && odd == 0;
   size_t k = 0;
+  for (uint64_t& x : W.step_ns) x = 0;
+  auto lt = clk::now();
+  auto lap = [&](int i) {  // (one step of the parallel path done)
+    const auto t = clk::now();
+    W.step_ns[i] = ns(lt, t);
+    lt = t;
+  };
   if (parallel) {
     const uint32_t NS = IN_SHARDS;
     constexpr uint32_t QPF = 16;  // prefetch distance (messages)
@@ -1114,6 +1129,7 @@ gome_status gome_consume_order_nodes(gome_names* nm, gome_prepool* pp, const cha
         }
       }
     });
+    lap(0);
     // 2. the names not seen before and every marker, by shard: a counting sort of their messages
     //    (queue order kept), then a shard's messages in order on one thread -- the first message of
     //    a new name gives it a provisional entry, a marker is staged
@@ -1154,6 +1170,7 @@ gome_status gome_consume_order_nodes(gome_names* nm, gome_prepool* pp, const cha
         for (int kk = 0; kk < 4; ++kk)
           if (wanted(i, kk)) idx[kk][c[kk * NS + shard_of(i, kk)]++] = static_cast<uint32_t>(i);
     });
+    lap(1);
     // (outputs by position in idx[], written by one thread each: indexed by message they would be
     // written from every thread at neighbouring addresses)
     std::vector<uint32_t>* nref = W.first;  // a new name's message: IN_PROV | its shard's fresh index
@@ -1184,6 +1201,7 @@ gome_status gome_consume_order_nodes(gome_names* nm, gome_prepool* pp, const cha
     pool.run(nt, [&](uint32_t t) {
       for (uint32_t sh = t; sh < NS; sh += nt) names_pass(sh, 0);
     });
+    lap(2);
     size_t new_syms = 0;
     for (const Interner::Shard& d : nm->in[0].sh) new_syms += d.fresh.size();
     if (max_symbols && nm->in[0].strs.size() + new_syms > max_symbols) {
@@ -1212,6 +1230,7 @@ gome_status gome_consume_order_nodes(gome_names* nm, gome_prepool* pp, const cha
           }
         }
       });
+      lap(3);
       // 3. ids of each kind's new names in the order of their first messages: a shard's fresh
       //    entries are in its queue order, so a merge by first message numbers them (newmsg: the
       //    fresh entries in id order, as (shard, index))
@@ -1238,6 +1257,7 @@ gome_status gome_consume_order_nodes(gome_names* nm, gome_prepool* pp, const cha
         in.reserve_stores(nt);
         any_new = true;
       }
+      lap(4);
       if (any_new)
         pool.run(nt, [&](uint32_t t) {
           for (int kk = 0; kk < 3; ++kk) {
@@ -1258,6 +1278,7 @@ gome_status gome_consume_order_nodes(gome_names* nm, gome_prepool* pp, const cha
             }
           }
         });
+      lap(5);
       if (any_new)
         pool.run(nt, [&](uint32_t t) {  // (... and the shards' slots given the ids)
           for (int kk = 0; kk < 3; ++kk)
@@ -1275,6 +1296,7 @@ gome_status gome_consume_order_nodes(gome_names* nm, gome_prepool* pp, const cha
               }
             }
         });
+      lap(6);
       // 4. the records, in message order (the rejected ones dropped): a new name's id through its
       //    message's position in idx[] (the position of each message: counted again per range)
       std::vector<uint32_t>* pos = W.pos;
@@ -1288,6 +1310,7 @@ gome_status gome_consume_order_nodes(gome_names* nm, gome_prepool* pp, const cha
             for (uint32_t r = c0; r < c1; ++r) pos[kk][idx[kk][r]] = r;
           }
       });
+      lap(7);
       std::vector<uint32_t>& kbase = W.kbase;
       kbase.assign(nt + 1, 0);
       for (uint32_t t = 0; t < nt; ++t) {
@@ -1344,6 +1367,7 @@ gome_status gome_consume_order_nodes(gome_names* nm, gome_prepool* pp, const cha
         }
         ps[t] = c;
       });
+      lap(8);
       for (Interner& in : nm->in)
         for (Interner::Shard& d : in.sh) d.fresh.clear();
       for (const gome_consume_stats& c : ps) {
@@ -1430,6 +1454,8 @@ gome_status gome_consume_order_nodes(gome_names* nm, gome_prepool* pp, const cha
       ++k;
     }
   }
+  if (parallel) lap(9);
+  else for (uint64_t& x : W.step_ns) x = 0;  // (a batch that fell back to the serial pass)
   s.records = k;
   s.queue_parallel = parallel ? 1 : 0;
   s.ns_decode = ns(t0, t1);

@@ -125,6 +125,14 @@ gome_status gome_consume_order_nodes(gome_names* nm, gome_prepool* pp, const cha
                                      uint32_t max_symbols, uint32_t threads, gome_order* out, uint32_t* msg_index,
                                      size_t* n_out, gome_consume_stats* st);
 
+/* Diagnostics: the wall time (ns) of each step of the last gome_consume_order_nodes call on nm
+ * (its parallel queue-order path: 0 lookups, 1 bucket by shard, 2 new symbols, 3 new uuids / oids
+ * and markers, 4 id order, 5 new names stored, 6 their slots, 7 positions, 8 records, 9 the rest;
+ * zeros where the call took the serial pass).  Copies min(n, GOME_CONSUME_STEPS) values into ns
+ * and returns GOME_CONSUME_STEPS (0 for a null nm). */
+#define GOME_CONSUME_STEPS 10
+size_t gome_consume_last_steps(const gome_names* nm, uint64_t* ns, size_t n);
+
 /* gome_render_events (gome_abi.h) on several threads: the events are split at taker boundaries
  * and the pieces concatenated in publish order (the same bytes).  Returns the bytes written, or
  * -(bytes needed) when cap is short, or INT64_MIN on a bad argument / unknown id. */

@@ -229,6 +229,7 @@ def _queue_run(batches, threads, marks, max_symbols=0):
             pre.set(s_, u_, o_)
     tables = {k: [names.name(k, j) for j in range(names.count(k))] for k in ("sym", "uuid", "oid")}
     _queue_run.parallel = cons.parallel_batches
+    _queue_run.steps = cons.queue_steps_s
     return outs, tables, len(pre)
 
 
@@ -245,10 +246,12 @@ def test_parallel_queue_pass_matches_the_serial_one(odd_tx, max_symbols):
     adds = [json.loads(m) for b in batches for m in b if m.startswith('{"Action":1')]
     marks = [(a["Symbol"], a["Uuid"], a["Oid"]) for a in adds if rng.random() < 0.5]
     par = _queue_run(batches, 8, marks, max_symbols)
-    npar = _queue_run.parallel
+    npar, steps = _queue_run.parallel, _queue_run.steps
     ser = _queue_run(batches, 1, marks, max_symbols)
     assert _queue_run.parallel == 0
     assert npar == (0 if (odd_tx or max_symbols) else 7), npar  # (5 batches, 2 consumed twice)
+    # (gome_consume_last_steps: the parallel path's step times; all zero where every batch was serial)
+    assert (sum(steps) > 0) == (npar > 0) and sum(_queue_run.steps) == 0
     assert par[1] == ser[1] and par[2] == ser[2]
     for (ra, ja, pa), (rb, jb, pb) in zip(par[0], ser[0]):
         assert ja == jb and pa == pb

@@ -1051,6 +1051,8 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   // (A/B on one box: config 4 +0.6%, config 5c +0.3%, gpurun_out/r05bw)
   const bool sort_ahead = ahead && !early && !copy_busy && !cold_main && dominant && bid_prev > 0;
   if (sort_ahead) {
+    // (beside the plan instead, from the slot's last batch's end: even, config 4 / 5c +0.1..0.5%,
+    // gpurun_out/r06x)
     HIPCHK(hipStreamWaitEvent(copy_stream, plan_done, 0));
     ss = copy_stream;
   }
@@ -1422,7 +1424,7 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
       HIPCHK(hipEventRecord(dp_fork, st));
       HIPCHK(hipStreamWaitEvent(cs, dp_fork, 0));
       if (c_deep) deep_sort_level(R, FL_SORT_GRID, cs, pl);
-      HIPCHK(hipEventRecord(dl_done, cs));  // (a deep book with DELs: k_fc_count / events wait)
+      HIPCHK(hipEventRecord(dl_done, cs));  // (a deep book with DELs: k_fc_count_* / events wait)
     }
     k_flow_sort_cnt<<<dim3(FL_SORT_GRID, nb), FL_TILE, 0, st>>>(D, R);
     k_flow_sort_scan<<<nb, FL_CAP * FL_SCAN_P, 0, st>>>(D, R);
@@ -1476,7 +1478,8 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
     k_fc_level_blk<<<dim3(FL_CAP, nb), FC_LVB_T, 0, st>>>(D, R);
     if (split) HIPCHK(hipStreamWaitEvent(st, dl_done, 0));  // (the deep books' level pass ran on cs)
     toff(Rc, true, st);
-    k_fc_count<<<1024, 256, 0, st>>>(D, B, Rc);
+    k_fc_count_nf<<<1024, 256, 0, st>>>(D, B, Rc);
+    k_fc_count_run<<<1024, 256, 0, st>>>(D, B, Rc);
     k_fc_write_lv<<<dim3(FL_CAP, nb), 64, 0, st>>>(D, B, Rc);
     k_fc_fin<<<nb, 128, 0, st>>>(D, Rc);
     k_fc_events<<<1024, 256, 0, st>>>(D, B, Rc);
@@ -1557,7 +1560,8 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
       if (tfc_split) HIPCHK(hipStreamWaitEvent(s, tfc_done, 0));
       else k_fc_level_book<<<nh_tail, 1024, 0, s>>>(D, FT);
       toff(FTc, true, s);
-      k_fc_count<<<1024, 256, 0, s>>>(D, B, FTc);
+      k_fc_count_nf<<<1024, 256, 0, s>>>(D, B, FTc);
+      k_fc_count_run<<<1024, 256, 0, s>>>(D, B, FTc);
       k_fc_write_book<<<nh_tail, FL_WRITE_T, 0, s>>>(D, B, FTc);
       k_fc_events<<<1024, 256, 0, s>>>(D, B, FTc);
     }

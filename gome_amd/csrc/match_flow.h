@@ -2183,7 +2183,7 @@ __global__ __launch_bounds__(1024) void k_flow_toff(Dev D, FlowArgs F) {
   uint32_t* toff = F.toff + F.tb;
   const uint32_t per = (nb + 1023) / 1024, b0 = tid * per;
   uint32_t s = 0;
-  // (deep books with DELs count with the books with DELs: k_fc_count / k_fc_events)
+  // (deep books with DELs count with the books with DELs: k_fc_count_nf / k_fc_events)
   auto mine = [&](const FlowHdr& x) {
     return x.ok == FL_OK_DEEP ? (KIND == (x.dc ? FL_OK_CANCEL : FL_OK_ADD)) : x.ok == KIND;
   };

@@ -37,7 +37,7 @@
 //   k_fc_level      per level: cancels -> their DEL's record; the consumption-space layout of
 //                   the makers (a cancelled maker only spans what was consumed before its
 //                   cancel), the gathered old makers, the new makers
-//   k_fc_count / k_fc_events   fills as interval intersections (zero-length makers skipped,
+//   k_fc_count_nf / _run, k_fc_events   fills as interval intersections (zero-length makers skipped,
 //                   MatchNode.NextNode skips makers cancelled before the fill), cancel events,
 //                   tombstones of cancelled old makers
 //   k_fc_write      surviving new makers appended, the level records; k_fc_fin the book.
@@ -1733,34 +1733,32 @@ __device__ __forceinline__ uint32_t fc_nfills(const FcTouch& T, uint32_t& pops) 
   return nf;
 }
 
-// ---- k_fc_count: events per touch and per order (thread per touch of the range's books) ----
-__global__ void k_fc_count(Dev D, BatchArgs B, FlowArgs F) {
+// ---- k_fc_count_nf / k_fc_count_run: events per touch and per order -----------------------
+// A touch's fills cost a binary search of its level's makers (fc_touch: ~16 dependent loads on a
+// busy level), so they are counted a thread per touch (k_fc_count_nf, into fbase), and only then
+// summed per order (k_fc_count_run: the order's first touch walks its touches' counts, a few cache
+// lines).  One pass that walked each order's touches from its first (round 5) ran as long as the
+// longest sweep's chain of searches: 0.32 ms on config 4's hottest book (orders of 74 levels).
+__global__ void k_fc_count_nf(Dev D, BatchArgs B, FlowArgs F) {
   const uint32_t hend = fl_hend(D, F), nb = hend > F.h0 ? hend - F.h0 : 0u;
   const uint32_t total = nb ? F.toff[F.tb + nb] : 0u;
   unsigned long long fills = 0, pops = 0, cancels = 0;
   for (uint32_t gt = blockIdx.x * blockDim.x + threadIdx.x; gt < total; gt += gridDim.x * blockDim.x) {
     const uint32_t hb = fl_book_of_wave(F, nb, gt - lane_id(), gt), h = F.h0 + hb, t = gt - F.toff[F.tb + hb];
-    const uint32_t nt = F.hdr[h].ntouch, beg = F.hdr[h].beg, L = FL_TOUCH_MUL * beg;
+    const uint32_t L = FL_TOUCH_MUL * F.hdr[h].beg;
     const Touch x = F.log[L + t];
-    if (t > 0 && tk_jc(F.log[L + t - 1]) == tk_jc(x)) continue;
-    uint32_t acc = 0;
-    for (uint32_t u = t; u < nt; ++u) {
-      const Touch y = (u == t) ? x : F.log[L + u];
-      if (tk_jc(y) != tk_jc(x)) break;
-      F.fbase[L + u] = acc;
-      const uint32_t kind = tk_kind(y.kr, true);
-      if (kind == TK_CONS) {
-        uint32_t pp;
-        const uint32_t nf = fc_nfills(fc_touch(F, h, L, y, u), pp);
-        acc += nf;
-        fills += nf;
-        pops += pp;
-      } else if (kind == TK_CANC) {
-        acc += 1;
-        cancels += 1;
-      }
+    const uint32_t kind = tk_kind(x.kr, true);
+    uint32_t nf = 0;
+    if (kind == TK_CONS) {
+      uint32_t pp;
+      nf = fc_nfills(fc_touch(F, h, L, x, t), pp);
+      fills += nf;
+      pops += pp;
+    } else if (kind == TK_CANC) {
+      nf = 1;
+      cancels += 1;
     }
-    if (tk_jc(x) < F.hdr[h].end - beg) B.ev_count[prep_at(B, beg + tk_jc(x)).idx] = acc;  // not padding
+    F.fbase[L + t] = nf;
   }
   for (int off = 32; off > 0; off >>= 1) {
     fills += __shfl_xor(fills, off);
@@ -1774,6 +1772,25 @@ __global__ void k_fc_count(Dev D, BatchArgs B, FlowArgs F) {
     ctr_add(D, C_HOT_CANCELS, cancels);
     ctr_add(D, C_FLOW_CANCELS, cancels);
     ctr_add(D, C_RESTING_DELTA, static_cast<unsigned long long>(-static_cast<long long>(pops + cancels)));
+  }
+}
+
+// fbase: each touch's count -> the order's events before it; the order's total -> ev_count
+__global__ void k_fc_count_run(Dev D, BatchArgs B, FlowArgs F) {
+  const uint32_t hend = fl_hend(D, F), nb = hend > F.h0 ? hend - F.h0 : 0u;
+  const uint32_t total = nb ? F.toff[F.tb + nb] : 0u;
+  for (uint32_t gt = blockIdx.x * blockDim.x + threadIdx.x; gt < total; gt += gridDim.x * blockDim.x) {
+    const uint32_t hb = fl_book_of_wave(F, nb, gt - lane_id(), gt), h = F.h0 + hb, t = gt - F.toff[F.tb + hb];
+    const uint32_t nt = F.hdr[h].ntouch, beg = F.hdr[h].beg, L = FL_TOUCH_MUL * beg;
+    const uint32_t j = tk_jc(F.log[L + t]);
+    if (t > 0 && tk_jc(F.log[L + t - 1]) == j) continue;
+    uint32_t acc = 0;
+    for (uint32_t u = t; u < nt && (u == t || tk_jc(F.log[L + u]) == j); ++u) {
+      const uint32_t v = F.fbase[L + u];
+      F.fbase[L + u] = acc;
+      acc += v;
+    }
+    if (j < F.hdr[h].end - beg) B.ev_count[prep_at(B, beg + j).idx] = acc;  // not padding
   }
 }
 

@@ -914,7 +914,7 @@ __device__ __forceinline__ void k_deep_write_lv_one(Dev D, BatchArgs B, FlowArgs
   const FlowLvl* LV = fl_lvls(F, h);
   Level* out = F.dlvout + static_cast<size_t>(hd.dslot) * DEEP_CAP;
   const uint32_t lane = lane_id();
-  uint32_t pops = 0;  // (ADD books: fl_level_pops; books with DELs count theirs in k_fc_count)
+  uint32_t pops = 0;  // (ADD books: fl_level_pops; books with DELs count theirs in k_fc_count_nf)
   // A wave takes 64 consecutive levels: the untouched ones (no touch, so no append and nothing
   // consumed: the prep's FlowLvl is final) one per lane, then the touched ones one at a time.
   for (uint32_t q0 = 1 + blockIdx.x * 64u; q0 <= hd.nl; q0 += gridDim.x * 64u) {

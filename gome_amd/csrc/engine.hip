@@ -932,6 +932,9 @@ gome_status gome_engine::init(const gome_config& c) {
       !alloc(&F.tvol, static_cast<size_t>(FL_HEAD) * F.maxt * FC_KEYS, "flow head tile volumes") ||
       !alloc(&F.fc_hash, fc_hcap, "flow cancel table"))
     return GOME_E_CAPACITY;
+  F.fcb_cap = static_cast<uint32_t>(ceil_div(ntouch, FCB_CK) + FCB_HCAP);
+  if (!alloc(&F.fcb_ctl, 2, "huge level passes") || !alloc(&F.fcb, 2ull * F.fcb_cap, "huge level chunks"))
+    return GOME_E_CAPACITY;
   HIPCHK(hipMemsetAsync(F.fc_hash, 0, sizeof(FcHash) * fc_hcap, stream));
   // deep books (match_flow_deep.h): per deep slot
   F.dmaxt = F.maxt;
@@ -1044,16 +1047,16 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   HIPCHK(status_reset());
   const uint32_t T256 = 256, gN = ceil_div(n, T256);
   // A pipelined device batch whose hottest book plans late (no early plan: books with DELs): its
-  // sort on the copy stream from the last batch's plan end, beside that batch's reconstruction
-  // and publish, instead of after them (the sort needs only this batch's records, and the slot's
-  // buffers were free once the batch before the last one ended, which that plan comes after).  Not
-  // while the plan runs: its record reads slowed a concurrent plan (round 3).
-  // (A/B on one box: config 4 +0.6%, config 5c +0.3%, gpurun_out/r05bw)
+  // sort on the copy stream as soon as the slot's buffers are free (the slot's last batch ended),
+  // beside the last batch's plan, so that only the last batch's reconstruction and publish stand
+  // between two plans (the sort needs only this batch's records).  Round 3 measured a sort beside
+  // the plan slowing it (its record reads); with the plan's CUs reserved (plan_cus) it does not:
+  // 78.0 ns per order either way, config 4 +1.2%, config 5c +0.2% against the sort from the last
+  // plan's end (same-box A/B, gpurun_out/r06ac; before the chunked huge levels and the split event
+  // count shortened the reconstruction, the sort was not on the critical path: r06x, even).
   const bool sort_ahead = ahead && !early && !copy_busy && !cold_main && dominant && bid_prev > 0;
   if (sort_ahead) {
-    // (beside the plan instead, from the slot's last batch's end: even, config 4 / 5c +0.1..0.5%,
-    // gpurun_out/r06x)
-    HIPCHK(hipStreamWaitEvent(copy_stream, plan_done, 0));
+    HIPCHK(hipStreamWaitEvent(copy_stream, S.done, 0));
     ss = copy_stream;
   }
   HIPCHK(mark(GOME_PH_SORT, 0, ss));
@@ -1393,6 +1396,16 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   HIPCHK(hipStreamWaitEvent(flow_stream, fork, 0));  // (k_prep, the gather bump)
   // deep books: the two-pass level sort and the per-level reconstruction, then the writes
   // (per_level: the hottest book's; with DELs its levels go to k_deep_level_hot)
+  // the hottest book's levels of FC_HUGE touches or more, by chunks (match_flow_deep.h, k_fcb_*;
+  // deep: 0 for a lane book, 1 for a deep one), before the block / wave passes of its other levels
+  auto huge_levels = [&](const FlowArgs& R, uint32_t deep, hipStream_t st) {
+    k_fcb_list<<<1, 1024, 0, st>>>(D, R, deep);
+    k_fcb_sum1<<<FCB_GRID, FCB_T, 0, st>>>(D, R, deep);
+    k_fcb_sum2<<<FCB_GRID, FCB_T, 0, st>>>(D, R, deep);
+    k_fcb_scan<<<64, 64, 0, st>>>(D, R, deep);
+    k_fcb_write<<<FCB_GRID, FCB_T, 0, st>>>(D, R, deep);
+    k_fcb_fifo<<<64, 64, 0, st>>>(D, R, deep);
+  };
   auto deep_sort_level = [&](const FlowArgs& R, uint32_t tiles, hipStream_t st, bool per_level) {
     const uint32_t ns = std::min<uint32_t>(R.ds1 - R.ds0, DEEP_GRID_T);  // (blocks walk the slots)
     deep_sort(R, tiles, st);
@@ -1401,7 +1414,10 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
     // (after k_deep_level: a level pass overwrites its level's run end, FlowLvl::pad1, which
     // k_deep_level reads and fd_run checks)
     if (!hot && c_canc) k_deep_level_big<<<dim3(DEEP_BIG_GRID, ns), FC_LVB_T, 0, st>>>(D, R);
-    if (hot) k_deep_level_hot<<<DEEP_GRID / 16, FC_LVB_T, 0, st>>>(D, R);
+    if (hot) {
+      huge_levels(R, 1u, st);
+      k_deep_level_hot<<<DEEP_GRID / 16, FC_LVB_T, 0, st>>>(D, R);
+    }
   };
   auto deep_write = [&](const FlowArgs& R, hipStream_t st) {
     const uint32_t ns = std::min<uint32_t>(R.ds1 - R.ds0, DEEP_GRID_T);  // (blocks walk the slots)
@@ -1475,7 +1491,8 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   // books with DELs (match_flow_cancel.h); their events go to the arena
   auto head_recon_c = [&](const FlowArgs& R, const FlowArgs& Rc, uint32_t nb, hipStream_t st, bool split) -> gome_status {
     if (!c_canc) return GOME_OK;
-    k_fc_level_blk<<<dim3(FL_CAP, nb), FC_LVB_T, 0, st>>>(D, R);
+    if (split) huge_levels(R, 0u, st);  // (the hottest book's call: nb == 1)
+    k_fc_level_blk<<<dim3(FL_CAP, nb), FC_LVB_T, 0, st>>>(D, R, split ? 1u : 0u);
     if (split) HIPCHK(hipStreamWaitEvent(st, dl_done, 0));  // (the deep books' level pass ran on cs)
     toff(Rc, true, st);
     k_fc_count_nf<<<1024, 256, 0, st>>>(D, B, Rc);
@@ -2159,6 +2176,7 @@ gome_status gome_debug_peek(gome_engine* e, uint32_t which, uint64_t offset, uin
     case 3: base = e->F.fc_rank; size = 4 * nb; break;
     case 4: base = e->F.fc_tg; size = 4 * nb; break;
     case 5: base = e->F.ord8; size = 8 * (static_cast<uint64_t>(gome::FL_ORD8_MUL) * nb + gome::FL_ORD8_PAD); break;
+    case 6: base = e->F.fcb_ctl; size = 2 * sizeof(gome::FcbCtl); break;
     default: return GOME_E_INVAL;
   }
   if (offset > size || bytes > size - offset) return GOME_E_INVAL;

@@ -219,6 +219,8 @@ constexpr uint32_t FC_GEN_MASK = 0x7FF;   // generation bits of an FcHash key
 
 struct FcDel;  // a DEL record's target (match_flow_cancel.h)
 struct FcHash;
+struct FcbChunk;  // the chunked pass of a huge level (match_flow_deep.h)
+struct FcbCtl;
 
 struct FlowArgs {
   FlowHdr* hdr;        // [MAX_HOT]
@@ -274,6 +276,11 @@ struct FlowArgs {
   uint32_t tmap_stride, mb;
   uint32_t bid;        // batch number (FlowHdr::bid)
   uint32_t xlog;       // the early plan's arguments (match_early.h): the book's log at F.log + 0
+  // the hottest book's huge levels (k_fcb_*): a control block and fcb_cap chunks for a lane book
+  // ([0]) and a deep book ([1])
+  FcbCtl* fcb_ctl;     // [2]
+  FcbChunk* fcb;       // [2 * fcb_cap]
+  uint32_t fcb_cap;
 };
 
 __device__ __forceinline__ uint32_t fl_hend(const Dev& D, const FlowArgs& F) { return min(F.h1, D.st->nhot); }

@@ -1392,119 +1392,15 @@ constexpr uint32_t FC_LVB_T = FL_LVB_T, FC_K = 4;
 // a level of FC_BIG touches or more takes a whole block (fc_level_blk), smaller ones a wave
 constexpr uint32_t FC_BIG = 1024;
 
-// fc_level_one with a whole block (FC_LVB_T threads) on one level: the level's touches in
-// block-wide chunks (the long levels of the hottest books hold tens of thousands of touches,
-// which one wave walks 64 at a time); the old FIFO's gather stays with wave 0.
-__device__ __forceinline__ void fc_level_blk(const Dev& D, const FlowArgs& F, uint32_t h, uint32_t q) {
-  __shared__ int64_t red_s[2];
-  __shared__ uint32_t nr_s, ncan_s, ncons_s;
-  const FlowHdr* hd = &F.hdr[h];
-  const uint32_t tid = threadIdx.x, lane = lane_id();
-  FlowLvl* Lq = fl_lvls(F, h) + q;  // (a lane book's F.lvl row, or a deep book's level table)
-  const uint32_t beg = hd->beg;
-  const uint32_t L = FL_TOUCH_MUL * beg;
+// A big level's pass, step 3 (one wave): its old FIFO gathered (the makers the batch reaches, their
+// consumption-space starts), the consumed ones tombstoned, the partial head cut, and the level's
+// results; cfin / ncons / nrest / ncan_old / ocan_t / qend from steps 1-2 (fc_level_blk, or the
+// chunked pass of a huge level, k_fcb_*).
+__device__ __forceinline__ void fc_level_fifo(const Dev& D, const FlowArgs& F, const FlowHdr* hd, FlowLvl* Lq,
+                                              const SEnt* R, uint32_t cnt, uint32_t L, int64_t cfin, uint32_t ncons_s,
+                                              uint32_t nr_s, uint32_t ncan_s, int64_t ocan_t, int64_t qend) {
+  const uint32_t lane = lane_id();
   const unsigned long long g = static_cast<unsigned long long>(hd->g);
-  const uint32_t base = Lq->base, cnt = Lq->cnt;
-  const int64_t d0 = Lq->d0;
-  SEnt* R = F.srt + L + base;
-  RsEnt* RS = F.rs + L + base;
-  if (tid == 0) { red_s[0] = 0; nr_s = 0; ncan_s = 0; ncons_s = 0; }
-  __syncthreads();
-  // 1. each cancel -> its DEL's record (r, touch); the consumption cursor before each consume.
-  //    FC_K consecutive touches per thread: their loads in flight together, a quarter of the
-  //    block scans (a busy level is tens of thousands of touches)
-  int64_t cc = 0, ocan = 0;
-  uint32_t nr = 0, ncan_old = 0, nc = 0;
-  for (uint32_t c0 = 0; c0 < cnt; c0 += FC_LVB_T * FC_K) {
-    const uint32_t i0 = c0 + tid * FC_K;
-    SEnt e[FC_K];
-#pragma unroll
-    for (uint32_t u = 0; u < FC_K; ++u)
-      if (i0 + u < cnt) e[u] = R[i0 + u];
-    int64_t sum = 0;
-#pragma unroll
-    for (uint32_t u = 0; u < FC_K; ++u) {
-      if (i0 + u >= cnt) continue;
-      if (e[u].kind == TK_CANC) {
-        FcDel* d = &F.fc_del[beg + e[u].j];
-        d->r = e[u].amt;
-        d->ct = e[u].t;
-        if (d->kind == FC_OLD) { ocan += e[u].amt; ncan_old++; }
-      }
-      sum += e[u].kind == TK_CONS ? e[u].amt : 0;
-      nr += e[u].kind == TK_REST ? 1u : 0u;
-      nc += e[u].kind == TK_CONS ? 1u : 0u;
-    }
-    int64_t tot;
-    int64_t run = cc + fl_blk_excl(sum, &tot);
-#pragma unroll
-    for (uint32_t u = 0; u < FC_K; ++u) {
-      if (i0 + u >= cnt || e[u].kind != TK_CONS) continue;
-      R[i0 + u].coord = run;
-      run += e[u].amt;
-    }
-    cc += tot;
-  }
-  if (ocan) atomicAdd(reinterpret_cast<unsigned long long*>(&red_s[0]), static_cast<unsigned long long>(ocan));
-  if (nr) atomicAdd(&nr_s, nr);
-  if (ncan_old) atomicAdd(&ncan_s, ncan_old);
-  if (nc) atomicAdd(&ncons_s, nc);
-  __threadfence();  // the DEL records are read back below (by other threads)
-  __syncthreads();
-  const int64_t ocan_t = red_s[0];
-  const int64_t cfin = cc;
-  const int64_t base_new = d0 - ocan_t;
-  // 2. the new makers in FIFO (rest) order, their consumption-space starts and cancels
-  int64_t acc = base_new;
-  uint32_t k = 0;
-  for (uint32_t c0 = 0; c0 < cnt; c0 += FC_LVB_T * FC_K) {
-    const uint32_t i0 = c0 + tid * FC_K;
-    SEnt e[FC_K];
-    uint32_t tg[FC_K];
-#pragma unroll
-    for (uint32_t u = 0; u < FC_K; ++u) {
-      tg[u] = 0;
-      if (i0 + u < cnt) e[u] = R[i0 + u];
-    }
-#pragma unroll
-    for (uint32_t u = 0; u < FC_K; ++u)
-      if (i0 + u < cnt && e[u].kind == TK_REST) tg[u] = F.fc_tg[beg + e[u].j];
-    uint32_t ct[FC_K];
-    int64_t len[FC_K], sum = 0, nsum = 0;
-#pragma unroll
-    for (uint32_t u = 0; u < FC_K; ++u) {
-      const bool isr = i0 + u < cnt && e[u].kind == TK_REST;
-      ct[u] = NIL;
-      len[u] = isr ? e[u].amt : 0;
-      if (isr && tg[u]) {
-        const FcDel d = F.fc_del[tg[u] - 1u];
-        if (d.ct != NIL) { ct[u] = d.ct; len[u] = e[u].amt - d.r; }
-      }
-      sum += len[u];
-      nsum += isr ? 1 : 0;
-    }
-    int64_t tot, ntot;
-    int64_t run = acc + fl_blk_excl(sum, &tot);
-    uint32_t rk = k + static_cast<uint32_t>(fl_blk_excl(nsum, &ntot));
-#pragma unroll
-    for (uint32_t u = 0; u < FC_K; ++u) {
-      if (i0 + u >= cnt || e[u].kind != TK_REST) continue;
-      RsEnt x;
-      x.e = run;
-      x.v = e[u].amt;
-      x.j = e[u].j;
-      x.t = e[u].t;
-      x.pad0 = ct[u];
-      x.pad1 = 0;
-      RS[rk++] = x;
-      run += len[u];
-    }
-    acc += tot;
-    k += static_cast<uint32_t>(ntot);
-  }
-  const int64_t qend = acc;
-  // 3. the old FIFO (wave 0), as fc_level_one
-  if (tid >= 64) return;
   const bool lcont = (Lq->z0 || hd->nzero) && cfin > 0 && fl_run_cont(F, L, hd->ntouch, R, cnt, true);
   const unsigned long long ltm = lt_mask();
   const uint32_t nv0 = Lq->nv0, tail = Lq->tail, tslot = Lq->tslot;
@@ -1606,10 +1502,128 @@ __device__ __forceinline__ void fc_level_blk(const Dev& D, const FlowArgs& F, ui
   }
 }
 
-// The head books' levels: a block per (book, level).
-__global__ __launch_bounds__(FC_LVB_T) void k_fc_level_blk(Dev D, FlowArgs F) {
+
+// fc_level_one with a whole block (FC_LVB_T threads) on one level: the level's touches in
+// block-wide chunks (the long levels of the hottest books hold tens of thousands of touches,
+// which one wave walks 64 at a time); the old FIFO's gather stays with wave 0.
+__device__ __forceinline__ void fc_level_blk(const Dev& D, const FlowArgs& F, uint32_t h, uint32_t q) {
+  __shared__ int64_t red_s[2];
+  __shared__ uint32_t nr_s, ncan_s, ncons_s;
+  const FlowHdr* hd = &F.hdr[h];
+  const uint32_t tid = threadIdx.x;
+  FlowLvl* Lq = fl_lvls(F, h) + q;  // (a lane book's F.lvl row, or a deep book's level table)
+  const uint32_t beg = hd->beg;
+  const uint32_t L = FL_TOUCH_MUL * beg;
+  const uint32_t base = Lq->base, cnt = Lq->cnt;
+  const int64_t d0 = Lq->d0;
+  SEnt* R = F.srt + L + base;
+  RsEnt* RS = F.rs + L + base;
+  if (tid == 0) { red_s[0] = 0; nr_s = 0; ncan_s = 0; ncons_s = 0; }
+  __syncthreads();
+  // 1. each cancel -> its DEL's record (r, touch); the consumption cursor before each consume.
+  //    FC_K consecutive touches per thread: their loads in flight together, a quarter of the
+  //    block scans (a busy level is tens of thousands of touches)
+  int64_t cc = 0, ocan = 0;
+  uint32_t nr = 0, ncan_old = 0, nc = 0;
+  for (uint32_t c0 = 0; c0 < cnt; c0 += FC_LVB_T * FC_K) {
+    const uint32_t i0 = c0 + tid * FC_K;
+    SEnt e[FC_K];
+#pragma unroll
+    for (uint32_t u = 0; u < FC_K; ++u)
+      if (i0 + u < cnt) e[u] = R[i0 + u];
+    int64_t sum = 0;
+#pragma unroll
+    for (uint32_t u = 0; u < FC_K; ++u) {
+      if (i0 + u >= cnt) continue;
+      if (e[u].kind == TK_CANC) {
+        FcDel* d = &F.fc_del[beg + e[u].j];
+        d->r = e[u].amt;
+        d->ct = e[u].t;
+        if (d->kind == FC_OLD) { ocan += e[u].amt; ncan_old++; }
+      }
+      sum += e[u].kind == TK_CONS ? e[u].amt : 0;
+      nr += e[u].kind == TK_REST ? 1u : 0u;
+      nc += e[u].kind == TK_CONS ? 1u : 0u;
+    }
+    int64_t tot;
+    int64_t run = cc + fl_blk_excl(sum, &tot);
+#pragma unroll
+    for (uint32_t u = 0; u < FC_K; ++u) {
+      if (i0 + u >= cnt || e[u].kind != TK_CONS) continue;
+      R[i0 + u].coord = run;
+      run += e[u].amt;
+    }
+    cc += tot;
+  }
+  if (ocan) atomicAdd(reinterpret_cast<unsigned long long*>(&red_s[0]), static_cast<unsigned long long>(ocan));
+  if (nr) atomicAdd(&nr_s, nr);
+  if (ncan_old) atomicAdd(&ncan_s, ncan_old);
+  if (nc) atomicAdd(&ncons_s, nc);
+  __threadfence();  // the DEL records are read back below (by other threads)
+  __syncthreads();
+  const int64_t ocan_t = red_s[0];
+  const int64_t cfin = cc;
+  const int64_t base_new = d0 - ocan_t;
+  // 2. the new makers in FIFO (rest) order, their consumption-space starts and cancels
+  int64_t acc = base_new;
+  uint32_t k = 0;
+  for (uint32_t c0 = 0; c0 < cnt; c0 += FC_LVB_T * FC_K) {
+    const uint32_t i0 = c0 + tid * FC_K;
+    SEnt e[FC_K];
+    uint32_t tg[FC_K];
+#pragma unroll
+    for (uint32_t u = 0; u < FC_K; ++u) {
+      tg[u] = 0;
+      if (i0 + u < cnt) e[u] = R[i0 + u];
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < FC_K; ++u)
+      if (i0 + u < cnt && e[u].kind == TK_REST) tg[u] = F.fc_tg[beg + e[u].j];
+    uint32_t ct[FC_K];
+    int64_t len[FC_K], sum = 0, nsum = 0;
+#pragma unroll
+    for (uint32_t u = 0; u < FC_K; ++u) {
+      const bool isr = i0 + u < cnt && e[u].kind == TK_REST;
+      ct[u] = NIL;
+      len[u] = isr ? e[u].amt : 0;
+      if (isr && tg[u]) {
+        const FcDel d = F.fc_del[tg[u] - 1u];
+        if (d.ct != NIL) { ct[u] = d.ct; len[u] = e[u].amt - d.r; }
+      }
+      sum += len[u];
+      nsum += isr ? 1 : 0;
+    }
+    int64_t tot, ntot;
+    int64_t run = acc + fl_blk_excl(sum, &tot);
+    uint32_t rk = k + static_cast<uint32_t>(fl_blk_excl(nsum, &ntot));
+#pragma unroll
+    for (uint32_t u = 0; u < FC_K; ++u) {
+      if (i0 + u >= cnt || e[u].kind != TK_REST) continue;
+      RsEnt x;
+      x.e = run;
+      x.v = e[u].amt;
+      x.j = e[u].j;
+      x.t = e[u].t;
+      x.pad0 = ct[u];
+      x.pad1 = 0;
+      RS[rk++] = x;
+      run += len[u];
+    }
+    acc += tot;
+    k += static_cast<uint32_t>(ntot);
+  }
+  const int64_t qend = acc;
+  // 3. the old FIFO (wave 0), as fc_level_one
+  if (tid >= 64) return;
+  fc_level_fifo(D, F, hd, Lq, R, cnt, L, cfin, ncons_s, nr_s, ncan_s, ocan_t, qend);
+}
+
+// The head books' levels: a block per (book, level).  huge: the hottest book's launch, after
+// k_fcb_list marked its huge levels (their chunked pass, match_flow_deep.h)
+__global__ __launch_bounds__(FC_LVB_T) void k_fc_level_blk(Dev D, FlowArgs F, uint32_t huge) {
   const uint32_t h = F.h0 + blockIdx.y, q = blockIdx.x;
   if (h >= fl_hend(D, F) || !fc_lane(F, h) || q == 0 || q > F.hdr[h].nl) return;
+  if (huge && fl_lvls(F, h)[q].pad6) return;
   fc_level_blk(D, F, h, q);
 }
 

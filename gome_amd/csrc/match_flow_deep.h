@@ -825,14 +825,350 @@ __device__ __forceinline__ uint32_t fd_run(const FlowLvl* LV, const SEnt* R, uin
                   (e == nt || R[e].lvl != q);
   return ok ? e - b : 0u;
 }
+
+// ---- huge levels: one level's steps 1-2 over many blocks (the hottest book's) ----------------
+// Config 4's and 5c's hottest books hold two levels of ~50k touches each per batch (the aggressive
+// orders' remainders at 1.00 / 0.01, consumed there by every ordinary order of the other side).
+// fc_level_blk took such a level FC_LVB_T * FC_K touches at a time, each chunk a chain of dependent
+// loads and block scans: 0.34 ms (config 4, k_fc_level_blk) and 0.57 ms (config 5c,
+// k_deep_level_hot) on the batch's critical path.  A level of FC_HUGE touches or more instead goes
+// by chunks of FCB_CK touches, a block each: per-chunk sums (k_fcb_sum1: the cancels' DEL records,
+// the consumed volume, the counts; k_fcb_sum2: the new makers' lengths, which read those records),
+// their prefixes per level (k_fcb_scan), the consume cursors and the new makers written per chunk
+// (k_fcb_write), then fc_level_fifo per level (k_fcb_fifo).  k_fcb_list picks the levels first and
+// marks them (FlowLvl::pad6 = 1): k_fc_level_blk and k_deep_level_hot skip them.
+constexpr uint32_t FCB_T = 256, FCB_K = 4, FCB_CK = FCB_T * FCB_K;
+constexpr uint32_t FC_HUGE = 16384;
+constexpr uint32_t FCB_HCAP = 512;  // huge levels per pass (beyond: fc_level_blk, unmarked)
+constexpr uint32_t FCB_GRID = 512;
+struct FcbChunk {
+  int64_t cons, ocan, rlen;      // consumed volume, cancelled old volume, new makers' lengths
+  int64_t pcons, prlen;          // their exclusive prefixes within the level (k_fcb_scan)
+  uint32_t nr, nc, ncan, pnr;    // rests, consumes, cancels of old makers; the rests before the chunk
+};
+struct FcbCtl {
+  uint32_t n, total, h, pad;
+  uint32_t q[FCB_HCAP];
+  uint32_t off[FCB_HCAP + 1];    // each listed level's first chunk; off[n] = total
+  int64_t cfin[FCB_HCAP], ocan[FCB_HCAP], qend[FCB_HCAP];
+  uint32_t nr[FCB_HCAP], nc[FCB_HCAP], ncan[FCB_HCAP];
+};
+static_assert(sizeof(FcbCtl) == 22552, "tests/test_gpu_huge_levels.py reads the control blocks by this size");
+
+// the hottest book of the pass, or NIL: a lane book with DELs (k_fc_level_blk's) or a deep one
+// (k_deep_level_hot's), by the same tests as those kernels
+__device__ __forceinline__ uint32_t fcb_book(const Dev& D, const FlowArgs& F, uint32_t deep) {
+  if (deep) {
+    const uint32_t h = fd_nslots(F) ? fd_book(D, F, 0) : NIL;
+    return (fd_deep(F, h) && F.hdr[h].dc) ? h : NIL;
+  }
+  const uint32_t h = F.h0;
+  return (h < fl_hend(D, F) && fc_lane(F, h)) ? h : NIL;
+}
+
+__global__ __launch_bounds__(1024) void k_fcb_list(Dev D, FlowArgs F, uint32_t deep) {
+  FcbCtl* C = F.fcb_ctl + deep;
+  __shared__ uint32_t n_s;
+  const uint32_t h = fcb_book(D, F, deep);
+  if (threadIdx.x == 0) n_s = 0;
+  __syncthreads();
+  if (h != NIL) {
+    const uint32_t nl = F.hdr[h].nl, nt = F.hdr[h].ntouch;
+    FlowLvl* LV = fl_lvls(F, h);
+    const SEnt* R = F.srt + FL_TOUCH_MUL * F.hdr[h].beg;
+    for (uint32_t q = 1 + threadIdx.x; q <= nl; q += blockDim.x) {
+      const uint32_t cnt = deep ? fd_run(LV, R, nt, q) : LV[q].cnt;
+      uint32_t mark = 0;
+      if (cnt >= FC_HUGE) {
+        const uint32_t k = atomicAdd(&n_s, 1u);
+        if (k < FCB_HCAP) {
+          C->q[k] = q;
+          mark = 1;
+          if (deep) LV[q].cnt = cnt;  // (as k_deep_level_hot sets it for fc_level_blk)
+        }
+      }
+      LV[q].pad6 = mark;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t n = h == NIL ? 0u : min(n_s, FCB_HCAP);
+    uint32_t off = 0;
+    for (uint32_t k = 0; k < n; ++k) {
+      C->off[k] = off;
+      off += (fl_lvls(F, h)[C->q[k]].cnt + FCB_CK - 1) / FCB_CK;
+    }
+    C->off[n] = off;
+    C->n = n;
+    C->total = off;
+    C->h = h;
+  }
+}
+
+// the listed level whose chunks hold chunk g: off[k] <= g < off[k + 1]
+__device__ __forceinline__ uint32_t fcb_slot(const FcbCtl* C, uint32_t g) {
+  uint32_t lo = 0, hi = C->n;
+  while (hi - lo > 1) {
+    const uint32_t m = (lo + hi) >> 1;
+    if (C->off[m] <= g) lo = m;
+    else hi = m;
+  }
+  return lo;
+}
+
+// block totals of up to 5 values (FCB_T threads); every thread gets them
+__device__ __forceinline__ void fcb_totals(int64_t (&v)[5]) {
+  __shared__ int64_t ws[5][FCB_T / 64];
+  const uint32_t w = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < 5; ++k) {
+    int64_t x = v[k];
+    for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off);
+    if ((threadIdx.x & 63u) == 0) ws[k][w] = x;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 5; ++k) {
+    int64_t t = 0;
+    for (uint32_t j = 0; j < FCB_T / 64; ++j) t += ws[k][j];
+    v[k] = t;
+  }
+  __syncthreads();  // (ws is reused by the next chunk)
+}
+
+// exclusive block prefixes of 3 values (FCB_T threads)
+__device__ __forceinline__ void fcb_excl(int64_t (&v)[3]) {
+  __shared__ int64_t ws[3][FCB_T / 64];
+  const uint32_t w = threadIdx.x >> 6;
+  int64_t inc[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    inc[k] = wave_incl_scan(v[k]);
+    if ((threadIdx.x & 63u) == 63u) ws[k][w] = inc[k];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    int64_t before = 0;
+    for (uint32_t j = 0; j < w; ++j) before += ws[k][j];
+    v[k] = before + inc[k] - v[k];
+  }
+  __syncthreads();
+}
+
+struct FcbView {  // a chunk's level
+  uint32_t sl, q, c, beg, cnt;
+  FlowLvl* Lq;
+  SEnt* R;
+  RsEnt* RS;
+};
+__device__ __forceinline__ FcbView fcb_view(const FlowArgs& F, const FcbCtl* C, uint32_t g) {
+  FcbView v;
+  v.sl = fcb_slot(C, g);
+  v.q = C->q[v.sl];
+  v.c = g - C->off[v.sl];
+  const FlowHdr* hd = &F.hdr[C->h];
+  v.beg = hd->beg;
+  v.Lq = fl_lvls(F, C->h) + v.q;
+  v.cnt = v.Lq->cnt;
+  const uint32_t L = FL_TOUCH_MUL * v.beg;
+  v.R = F.srt + L + v.Lq->base;
+  v.RS = F.rs + L + v.Lq->base;
+  return v;
+}
+
+// step 1 of fc_level_blk per chunk: each cancel -> its DEL's record (r, touch); the chunk's sums
+__global__ __launch_bounds__(FCB_T) void k_fcb_sum1(Dev D, FlowArgs F, uint32_t deep) {
+  const FcbCtl* C = F.fcb_ctl + deep;
+  FcbChunk* K = F.fcb + static_cast<size_t>(deep) * F.fcb_cap;
+  const uint32_t total = C->total;
+  for (uint32_t g = blockIdx.x; g < total; g += gridDim.x) {
+    const FcbView V = fcb_view(F, C, g);
+    const uint32_t i0 = V.c * FCB_CK + threadIdx.x * FCB_K;
+    SEnt e[FCB_K];
+#pragma unroll
+    for (uint32_t u = 0; u < FCB_K; ++u)
+      if (i0 + u < V.cnt) e[u] = V.R[i0 + u];
+    int64_t v[5] = {0, 0, 0, 0, 0};  // cons, ocan, nr, nc, ncan
+#pragma unroll
+    for (uint32_t u = 0; u < FCB_K; ++u) {
+      if (i0 + u >= V.cnt) continue;
+      if (e[u].kind == TK_CANC) {
+        FcDel* d = &F.fc_del[V.beg + e[u].j];
+        d->r = e[u].amt;
+        d->ct = e[u].t;
+        if (d->kind == FC_OLD) { v[1] += e[u].amt; v[4] += 1; }
+      }
+      v[0] += e[u].kind == TK_CONS ? e[u].amt : 0;
+      v[2] += e[u].kind == TK_REST ? 1 : 0;
+      v[3] += e[u].kind == TK_CONS ? 1 : 0;
+    }
+    fcb_totals(v);
+    if (threadIdx.x == 0) {
+      K[g].cons = v[0];
+      K[g].ocan = v[1];
+      K[g].nr = static_cast<uint32_t>(v[2]);
+      K[g].nc = static_cast<uint32_t>(v[3]);
+      K[g].ncan = static_cast<uint32_t>(v[4]);
+    }
+  }
+}
+
+// a rest touch's length in consumption space: its volume, less what its DEL (if it came) removed
+__device__ __forceinline__ int64_t fcb_rest_len(const FlowArgs& F, uint32_t beg, const SEnt& e, uint32_t& ct) {
+  ct = NIL;
+  const uint32_t tg = F.fc_tg[beg + e.j];
+  if (tg) {
+    const FcDel d = F.fc_del[tg - 1u];
+    if (d.ct != NIL) {
+      ct = d.ct;
+      return e.amt - d.r;
+    }
+  }
+  return e.amt;
+}
+
+// step 2's sums per chunk: the new makers' lengths
+__global__ __launch_bounds__(FCB_T) void k_fcb_sum2(Dev D, FlowArgs F, uint32_t deep) {
+  const FcbCtl* C = F.fcb_ctl + deep;
+  FcbChunk* K = F.fcb + static_cast<size_t>(deep) * F.fcb_cap;
+  const uint32_t total = C->total;
+  for (uint32_t g = blockIdx.x; g < total; g += gridDim.x) {
+    const FcbView V = fcb_view(F, C, g);
+    const uint32_t i0 = V.c * FCB_CK + threadIdx.x * FCB_K;
+    SEnt e[FCB_K];
+#pragma unroll
+    for (uint32_t u = 0; u < FCB_K; ++u)
+      if (i0 + u < V.cnt) e[u] = V.R[i0 + u];
+    int64_t v[5] = {0, 0, 0, 0, 0};
+#pragma unroll
+    for (uint32_t u = 0; u < FCB_K; ++u) {
+      if (i0 + u >= V.cnt || e[u].kind != TK_REST) continue;
+      uint32_t ct;
+      v[0] += fcb_rest_len(F, V.beg, e[u], ct);
+    }
+    fcb_totals(v);
+    if (threadIdx.x == 0) K[g].rlen = v[0];
+  }
+}
+
+// per listed level (a wave each): the chunks' exclusive prefixes and the level's totals
+__global__ __launch_bounds__(64) void k_fcb_scan(Dev D, FlowArgs F, uint32_t deep) {
+  FcbCtl* C = F.fcb_ctl + deep;
+  FcbChunk* K = F.fcb + static_cast<size_t>(deep) * F.fcb_cap;
+  const uint32_t lane = lane_id();
+  for (uint32_t sl = blockIdx.x; sl < C->n; sl += gridDim.x) {
+    const uint32_t a = C->off[sl], b = C->off[sl + 1];
+    int64_t cons = 0, ocan = 0, rlen = 0, nr = 0, nc = 0, ncan = 0;
+    for (uint32_t g0 = a; g0 < b; g0 += 64) {
+      const uint32_t g = g0 + lane;
+      const bool in = g < b;
+      const int64_t xc = in ? K[g].cons : 0, xr = in ? K[g].rlen : 0, xn = in ? K[g].nr : 0;
+      const int64_t ic = wave_incl_scan(xc), ir = wave_incl_scan(xr), in_ = wave_incl_scan(xn);
+      if (in) {
+        K[g].pcons = cons + ic - xc;
+        K[g].prlen = rlen + ir - xr;
+        K[g].pnr = static_cast<uint32_t>(nr + in_ - xn);
+      }
+      cons += rl64(ic, 63);
+      rlen += rl64(ir, 63);
+      nr += rl64(in_, 63);
+      int64_t xo = in ? K[g].ocan : 0, xq = in ? K[g].nc : 0, xk = in ? K[g].ncan : 0;
+      for (int off = 32; off > 0; off >>= 1) {
+        xo += __shfl_xor(xo, off);
+        xq += __shfl_xor(xq, off);
+        xk += __shfl_xor(xk, off);
+      }
+      ocan += xo;
+      nc += xq;
+      ncan += xk;
+    }
+    if (lane == 0) {
+      const FlowLvl* Lq = fl_lvls(F, C->h) + C->q[sl];
+      C->cfin[sl] = cons;
+      C->ocan[sl] = ocan;
+      C->qend[sl] = Lq->d0 - ocan + rlen;
+      C->nr[sl] = static_cast<uint32_t>(nr);
+      C->nc[sl] = static_cast<uint32_t>(nc);
+      C->ncan[sl] = static_cast<uint32_t>(ncan);
+    }
+  }
+}
+
+// per chunk: each consume's cursor before it, each new maker (its start, volume, order, touch and
+// cancel touch) at its rest rank -- fc_level_blk's writes of steps 1 and 2
+__global__ __launch_bounds__(FCB_T) void k_fcb_write(Dev D, FlowArgs F, uint32_t deep) {
+  const FcbCtl* C = F.fcb_ctl + deep;
+  const FcbChunk* K = F.fcb + static_cast<size_t>(deep) * F.fcb_cap;
+  const uint32_t total = C->total;
+  for (uint32_t g = blockIdx.x; g < total; g += gridDim.x) {
+    const FcbView V = fcb_view(F, C, g);
+    const uint32_t i0 = V.c * FCB_CK + threadIdx.x * FCB_K;
+    SEnt e[FCB_K];
+#pragma unroll
+    for (uint32_t u = 0; u < FCB_K; ++u)
+      if (i0 + u < V.cnt) e[u] = V.R[i0 + u];
+    uint32_t ct[FCB_K];
+    int64_t len[FCB_K];
+    int64_t v[3] = {0, 0, 0};  // consumed volume, new makers' lengths, rests
+#pragma unroll
+    for (uint32_t u = 0; u < FCB_K; ++u) {
+      ct[u] = NIL;
+      len[u] = 0;
+      if (i0 + u >= V.cnt) continue;
+      if (e[u].kind == TK_CONS) v[0] += e[u].amt;
+      if (e[u].kind == TK_REST) {
+        len[u] = fcb_rest_len(F, V.beg, e[u], ct[u]);
+        v[1] += len[u];
+        v[2] += 1;
+      }
+    }
+    fcb_excl(v);
+    int64_t cc = K[g].pcons + v[0];
+    int64_t run = V.Lq->d0 - C->ocan[V.sl] + K[g].prlen + v[1];
+    uint32_t rk = K[g].pnr + static_cast<uint32_t>(v[2]);
+#pragma unroll
+    for (uint32_t u = 0; u < FCB_K; ++u) {
+      if (i0 + u >= V.cnt) continue;
+      if (e[u].kind == TK_CONS) {
+        V.R[i0 + u].coord = cc;
+        cc += e[u].amt;
+      } else if (e[u].kind == TK_REST) {
+        RsEnt x;
+        x.e = run;
+        x.v = e[u].amt;
+        x.j = e[u].j;
+        x.t = e[u].t;
+        x.pad0 = ct[u];
+        x.pad1 = 0;
+        V.RS[rk++] = x;
+        run += len[u];
+      }
+    }
+  }
+}
+
+// per listed level (a wave each): the old FIFO step with the level's totals
+__global__ __launch_bounds__(64) void k_fcb_fifo(Dev D, FlowArgs F, uint32_t deep) {
+  const FcbCtl* C = F.fcb_ctl + deep;
+  for (uint32_t sl = blockIdx.x; sl < C->n; sl += gridDim.x) {
+    const FlowHdr* hd = &F.hdr[C->h];
+    FlowLvl* Lq = fl_lvls(F, C->h) + C->q[sl];
+    const uint32_t L = FL_TOUCH_MUL * hd->beg;
+    fc_level_fifo(D, F, hd, Lq, F.srt + L + Lq->base, Lq->cnt, L, C->cfin[sl], C->nc[sl], C->nr[sl], C->ncan[sl],
+                  C->ocan[sl], C->qend[sl]);
+  }
+}
+
 __global__ __launch_bounds__(FC_LVB_T) void k_deep_level_hot(Dev D, FlowArgs F) {
   const uint32_t h = fd_nslots(F) ? fd_book(D, F, 0) : NIL;  // (the hottest book's range: one slot)
   if (!fd_deep(F, h) || !F.hdr[h].dc) return;
   const uint32_t nt = F.hdr[h].ntouch, L = FL_TOUCH_MUL * F.hdr[h].beg, nl = F.hdr[h].nl;
   FlowLvl* LV = fl_lvls(F, h);
   const SEnt* R = F.srt + L;
+  // (the huge levels went by chunks, k_fcb_*: marked, and their run ends already rewritten)
   for (uint32_t q = 1 + blockIdx.x; q <= nl; q += gridDim.x) {
-    const uint32_t cnt = fd_run(LV, R, nt, q);
+    const uint32_t cnt = LV[q].pad6 ? 0u : fd_run(LV, R, nt, q);
     if (cnt < FC_BIG) continue;
     if (threadIdx.x == 0) LV[q].cnt = cnt;
     __syncthreads();
@@ -840,12 +1176,12 @@ __global__ __launch_bounds__(FC_LVB_T) void k_deep_level_hot(Dev D, FlowArgs F) 
     __syncthreads();  // (fc_level_blk's shared words, before the next level's)
   }
   for (uint32_t q = 1 + blockIdx.x * blockDim.x + threadIdx.x; q <= nl; q += gridDim.x * blockDim.x) {
-    const uint32_t cnt = fd_run(LV, R, nt, q);  // (small levels: a lane each)
+    const uint32_t cnt = LV[q].pad6 ? 0u : fd_run(LV, R, nt, q);  // (small levels: a lane each)
     if (cnt != 0 && cnt <= FC_LANE_MAX) fc_level_lane(D, F, h, q, cnt);
   }
   const uint32_t nw = blockDim.x >> 6, lane = lane_id();
   for (uint32_t q = 1 + blockIdx.x * nw + (threadIdx.x >> 6); q <= nl; q += gridDim.x * nw) {
-    const uint32_t cnt = uni(fd_run(LV, R, nt, q));
+    const uint32_t cnt = uni(LV[q].pad6 ? 0u : fd_run(LV, R, nt, q));
     if (cnt <= FC_LANE_MAX || cnt >= FC_BIG) continue;
     if (lane == 0) LV[q].cnt = cnt;
     __threadfence_block();  // (fc_level_one reads the count back)

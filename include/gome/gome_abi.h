@@ -353,7 +353,8 @@ gome_status gome_dup_records(const gome_engine* e, uint32_t* out, size_t cap, si
 gome_status gome_debug_flow_books(gome_engine* e, uint32_t* out, size_t cap, size_t* n_out);
 /* Diagnostics: raw bytes [offset, offset + bytes) of one of the flow path's device scratch
  * arrays after the last batch (0 headers, 1 level slots, 2 DEL records, 3 targeted-ADD ranks,
- * 4 DEL-of-ADD links, 5 packed records). */
+ * 4 DEL-of-ADD links, 5 packed records, 6 the hottest book's huge-level passes: two control blocks,
+ * lane book then deep book, each starting {levels taken, chunks, book, 0} as uint32). */
 gome_status gome_debug_peek(gome_engine* e, uint32_t which, uint64_t offset, uint64_t bytes, void* out);
 /* Diagnostics: the shape of one book's FIFOs, 4 words per level in the book's level order
  * {price_fx, live nodes, dead slots (cancelled / consumed, still linked), chunks}.  *n_out =

@@ -1306,7 +1306,7 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
       deep_sort(R, wide ? FL_SORT_GRID : 32, st);
       const bool big = wide;  // (the head's busiest levels a block each)
       k_fd_crank<<<dim3(DEEP_GRID, ns), 64, 0, st>>>(D, B, R, big ? 1u : 0u);
-      if (big) k_fd_crank_big<<<dim3(16, ns), FC_LVB_T, 0, st>>>(D, B, R);
+      if (big) k_fd_crank_big<<<dim3(FD_CRANK_GRID, ns), FC_LVB_T, 0, st>>>(D, B, R);
       k_fd_tbase<<<ns, DEEP_CLAIM_T, 0, st>>>(D, R);
     }
     if (wide) {  // the head: tile-parallel ranks, windows, layout and records
@@ -1416,7 +1416,7 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
     if (!hot && c_canc) k_deep_level_big<<<dim3(DEEP_BIG_GRID, ns), FC_LVB_T, 0, st>>>(D, R);
     if (hot) {
       huge_levels(R, 1u, st);
-      k_deep_level_hot<<<DEEP_GRID / 16, FC_LVB_T, 0, st>>>(D, R);
+      k_deep_level_hot<<<DLH_GRID, FC_LVB_T, 0, st>>>(D, R);
     }
   };
   auto deep_write = [&](const FlowArgs& R, hipStream_t st) {

@@ -1160,30 +1160,51 @@ __global__ __launch_bounds__(64) void k_fcb_fifo(Dev D, FlowArgs F, uint32_t dee
   }
 }
 
+// The block's levels (q = 1 + blockIdx.x mod gridDim.x) are sized all at once, a thread each, before
+// any of them is rebuilt (a level's pass rewrites its run end, FlowLvl::pad1, which fd_run checks):
+// the small ones rebuilt there by their thread (fc_level_lane), the big ones listed for the whole
+// block (fc_level_blk) and the others for a wave each (fc_level_one).  (Until round 6 each block
+// walked its levels one after another to find the big ones, two dependent loads a level: 0.42 ms
+// of config 5c's critical path for its ~16k levels, gpurun_out/prof_r06ae_config5c.)
+constexpr uint32_t DLH_GRID = DEEP_GRID / 16, DLH_CAP = 512;
+static_assert(DEEP_CAP <= DLH_GRID * DLH_CAP, "k_deep_level_hot's per-block level lists");
 __global__ __launch_bounds__(FC_LVB_T) void k_deep_level_hot(Dev D, FlowArgs F) {
+  __shared__ uint32_t big_q[DLH_CAP], big_c[DLH_CAP], mid_q[DLH_CAP], mid_c[DLH_CAP];
+  __shared__ uint32_t nbig, nmid;
   const uint32_t h = fd_nslots(F) ? fd_book(D, F, 0) : NIL;  // (the hottest book's range: one slot)
   if (!fd_deep(F, h) || !F.hdr[h].dc) return;
   const uint32_t nt = F.hdr[h].ntouch, L = FL_TOUCH_MUL * F.hdr[h].beg, nl = F.hdr[h].nl;
   FlowLvl* LV = fl_lvls(F, h);
   const SEnt* R = F.srt + L;
+  if (threadIdx.x == 0) nbig = nmid = 0;
+  __syncthreads();
   // (the huge levels went by chunks, k_fcb_*: marked, and their run ends already rewritten)
-  for (uint32_t q = 1 + blockIdx.x; q <= nl; q += gridDim.x) {
+  for (uint32_t q = 1 + blockIdx.x + gridDim.x * threadIdx.x; q <= nl; q += gridDim.x * blockDim.x) {
     const uint32_t cnt = LV[q].pad6 ? 0u : fd_run(LV, R, nt, q);
-    if (cnt < FC_BIG) continue;
-    if (threadIdx.x == 0) LV[q].cnt = cnt;
+    if (cnt >= FC_BIG) {
+      const uint32_t k = atomicAdd(&nbig, 1u);
+      big_q[k] = q;
+      big_c[k] = cnt;
+    } else if (cnt > FC_LANE_MAX) {
+      const uint32_t k = atomicAdd(&nmid, 1u);
+      mid_q[k] = q;
+      mid_c[k] = cnt;
+    } else if (cnt != 0) {
+      fc_level_lane(D, F, h, q, cnt);
+    }
+  }
+  __syncthreads();
+  for (uint32_t k = 0; k < nbig; ++k) {
+    const uint32_t q = big_q[k];
+    if (threadIdx.x == 0) LV[q].cnt = big_c[k];
     __syncthreads();
     fc_level_blk(D, F, h, q);
     __syncthreads();  // (fc_level_blk's shared words, before the next level's)
   }
-  for (uint32_t q = 1 + blockIdx.x * blockDim.x + threadIdx.x; q <= nl; q += gridDim.x * blockDim.x) {
-    const uint32_t cnt = LV[q].pad6 ? 0u : fd_run(LV, R, nt, q);  // (small levels: a lane each)
-    if (cnt != 0 && cnt <= FC_LANE_MAX) fc_level_lane(D, F, h, q, cnt);
-  }
   const uint32_t nw = blockDim.x >> 6, lane = lane_id();
-  for (uint32_t q = 1 + blockIdx.x * nw + (threadIdx.x >> 6); q <= nl; q += gridDim.x * nw) {
-    const uint32_t cnt = uni(LV[q].pad6 ? 0u : fd_run(LV, R, nt, q));
-    if (cnt <= FC_LANE_MAX || cnt >= FC_BIG) continue;
-    if (lane == 0) LV[q].cnt = cnt;
+  for (uint32_t k = threadIdx.x >> 6; k < nmid; k += nw) {
+    const uint32_t q = mid_q[k];
+    if (lane == 0) LV[q].cnt = mid_c[k];
     __threadfence_block();  // (fc_level_one reads the count back)
     fc_level_one(D, F, h, q);
   }
@@ -1557,6 +1578,7 @@ __global__ __launch_bounds__(64) void k_fd_crank(Dev D, BatchArgs B, FlowArgs F,
   for (uint32_t i = blockIdx.y; i < fd_nslots(F); i += gridDim.y) k_fd_crank_one(D, B, F, i, big);
 }
 // The levels of FC_CRANK_BIG keys or more, a block each (found from the sorted keys: a run's head).
+constexpr uint32_t FD_CRANK_GRID = 16, FD_CRANK_CAP = DEEP_CAP / FD_CRANK_GRID;
 __global__ __launch_bounds__(FC_LVB_T) void k_fd_crank_big(Dev D, BatchArgs B, FlowArgs F) {
   for (uint32_t si = blockIdx.y; si < fd_nslots(F); si += gridDim.y) {
     const uint32_t h = fd_book(D, F, si);
@@ -1565,13 +1587,24 @@ __global__ __launch_bounds__(FC_LVB_T) void k_fd_crank_big(Dev D, BatchArgs B, F
     const uint32_t nt = hd.ntouch, L = FL_TOUCH_MUL * hd.beg, nl = hd.nl;
     FlowLvl* LV = fl_lvls(F, h);
     const SEnt* R = F.srt + L;
-    for (uint32_t q = 1 + blockIdx.x; q <= nl; q += gridDim.x) {
+    // the block's big levels found a thread per level first (one after another, two dependent
+    // loads each, the 16 blocks took 0.28 ms over config 5c's ~16k levels), then ranked a block each
+    __shared__ uint32_t big_q[FD_CRANK_CAP], nbig;
+    if (threadIdx.x == 0) nbig = 0;
+    __syncthreads();
+    for (uint32_t q = 1 + blockIdx.x + gridDim.x * threadIdx.x; q <= nl; q += gridDim.x * blockDim.x) {
       const uint32_t b = LV[q].base, e = LV[q].pad1;
       // (a run of the current sort: this prep's k_deep_runs wrote base / pad1 of every level with keys)
       if (e < b + FC_CRANK_BIG || e > nt || R[b].lvl != q || R[e - 1].lvl != q) continue;
-      fd_crank_level_blk(B, F, hd, LV, R, q, b, e);
+      big_q[atomicAdd(&nbig, 1u)] = q;
+    }
+    __syncthreads();
+    for (uint32_t k = 0; k < nbig; ++k) {
+      const uint32_t q = big_q[k];
+      fd_crank_level_blk(B, F, hd, LV, R, q, LV[q].base, LV[q].pad1);
       __syncthreads();
     }
+    __syncthreads();  // (nbig, before the next slot's list)
   }
 }
 

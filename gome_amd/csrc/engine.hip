@@ -1352,6 +1352,8 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
     // plan stream right behind k_x_take, so whatever writes F.hdr[0] / F.lvl last — the take or this
     // fallback — runs there before the next early chain reads them: ADVICE r5, the fallback used to
     // run on the flow stream beside that chain.)
+    // (the plan on the flow stream instead, on every CU but the plan's, skipping this hop: the plan
+    // 78 -> 81 ns per order, config 4 -2.3%, 5c -3.1%, gpurun_out/r06ag)
     if (plan_stream && !early && dominant) {
       HIPCHK(hipEventRecord(pl_fork, flow_stream));
       HIPCHK(hipStreamWaitEvent(plan_stream, pl_fork, 0));
@@ -1399,7 +1401,9 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
   // the hottest book's levels of FC_HUGE touches or more, by chunks (match_flow_deep.h, k_fcb_*;
   // deep: 0 for a lane book, 1 for a deep one), before the block / wave passes of its other levels
   auto huge_levels = [&](const FlowArgs& R, uint32_t deep, hipStream_t st) {
-    k_fcb_list<<<1, 1024, 0, st>>>(D, R, deep);
+    (void)hipMemsetAsync(&R.fcb_ctl[deep].n, 0, 4, st);  // (an error is sticky: the next checked call reports it)
+    k_fcb_list<<<FCB_LIST_GRID, 1024, 0, st>>>(D, R, deep);
+    k_fcb_off<<<1, 64, 0, st>>>(D, R, deep);
     k_fcb_sum1<<<FCB_GRID, FCB_T, 0, st>>>(D, R, deep);
     k_fcb_sum2<<<FCB_GRID, FCB_T, 0, st>>>(D, R, deep);
     k_fcb_scan<<<64, 64, 0, st>>>(D, R, deep);

@@ -835,8 +835,8 @@ __device__ __forceinline__ uint32_t fd_run(const FlowLvl* LV, const SEnt* R, uin
 // by chunks of FCB_CK touches, a block each: per-chunk sums (k_fcb_sum1: the cancels' DEL records,
 // the consumed volume, the counts; k_fcb_sum2: the new makers' lengths, which read those records),
 // their prefixes per level (k_fcb_scan), the consume cursors and the new makers written per chunk
-// (k_fcb_write), then fc_level_fifo per level (k_fcb_fifo).  k_fcb_list picks the levels first and
-// marks them (FlowLvl::pad6 = 1): k_fc_level_blk and k_deep_level_hot skip them.
+// (k_fcb_write), then fc_level_fifo per level (k_fcb_fifo).  k_fcb_list / _off pick the levels first and
+// mark them (FlowLvl::pad6 = 1): k_fc_level_blk and k_deep_level_hot skip them.
 constexpr uint32_t FCB_T = 256, FCB_K = 4, FCB_CK = FCB_T * FCB_K;
 constexpr uint32_t FC_HUGE = 16384;
 constexpr uint32_t FCB_HCAP = 512;  // huge levels per pass (beyond: fc_level_blk, unmarked)
@@ -866,43 +866,46 @@ __device__ __forceinline__ uint32_t fcb_book(const Dev& D, const FlowArgs& F, ui
   return (h < fl_hend(D, F) && fc_lane(F, h)) ? h : NIL;
 }
 
+// (many blocks: a deep book has up to DEEP_CAP levels, and one block sized them 1024 at a time, 67 us
+// on config 5c's; C->n was zeroed before the launch)
+constexpr uint32_t FCB_LIST_GRID = 16;
 __global__ __launch_bounds__(1024) void k_fcb_list(Dev D, FlowArgs F, uint32_t deep) {
   FcbCtl* C = F.fcb_ctl + deep;
-  __shared__ uint32_t n_s;
   const uint32_t h = fcb_book(D, F, deep);
-  if (threadIdx.x == 0) n_s = 0;
-  __syncthreads();
-  if (h != NIL) {
-    const uint32_t nl = F.hdr[h].nl, nt = F.hdr[h].ntouch;
-    FlowLvl* LV = fl_lvls(F, h);
-    const SEnt* R = F.srt + FL_TOUCH_MUL * F.hdr[h].beg;
-    for (uint32_t q = 1 + threadIdx.x; q <= nl; q += blockDim.x) {
-      const uint32_t cnt = deep ? fd_run(LV, R, nt, q) : LV[q].cnt;
-      uint32_t mark = 0;
-      if (cnt >= FC_HUGE) {
-        const uint32_t k = atomicAdd(&n_s, 1u);
-        if (k < FCB_HCAP) {
-          C->q[k] = q;
-          mark = 1;
-          if (deep) LV[q].cnt = cnt;  // (as k_deep_level_hot sets it for fc_level_blk)
-        }
+  if (h == NIL) return;
+  const uint32_t nl = F.hdr[h].nl, nt = F.hdr[h].ntouch;
+  FlowLvl* LV = fl_lvls(F, h);
+  const SEnt* R = F.srt + FL_TOUCH_MUL * F.hdr[h].beg;
+  for (uint32_t q = 1 + blockIdx.x * blockDim.x + threadIdx.x; q <= nl; q += gridDim.x * blockDim.x) {
+    const uint32_t cnt = deep ? fd_run(LV, R, nt, q) : LV[q].cnt;
+    uint32_t mark = 0;
+    if (cnt >= FC_HUGE) {
+      const uint32_t k = atomicAdd(&C->n, 1u);
+      if (k < FCB_HCAP) {
+        C->q[k] = q;
+        mark = 1;
+        if (deep) LV[q].cnt = cnt;  // (as k_deep_level_hot sets it for fc_level_blk)
       }
-      LV[q].pad6 = mark;
     }
+    LV[q].pad6 = mark;
   }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const uint32_t n = h == NIL ? 0u : min(n_s, FCB_HCAP);
-    uint32_t off = 0;
-    for (uint32_t k = 0; k < n; ++k) {
-      C->off[k] = off;
-      off += (fl_lvls(F, h)[C->q[k]].cnt + FCB_CK - 1) / FCB_CK;
-    }
-    C->off[n] = off;
-    C->n = n;
-    C->total = off;
-    C->h = h;
+}
+
+// the listed levels' first chunks (one thread)
+__global__ void k_fcb_off(Dev D, FlowArgs F, uint32_t deep) {
+  FcbCtl* C = F.fcb_ctl + deep;
+  const uint32_t h = fcb_book(D, F, deep);
+  if (threadIdx.x != 0) return;
+  const uint32_t n = h == NIL ? 0u : min(C->n, FCB_HCAP);
+  uint32_t off = 0;
+  for (uint32_t k = 0; k < n; ++k) {
+    C->off[k] = off;
+    off += (fl_lvls(F, h)[C->q[k]].cnt + FCB_CK - 1) / FCB_CK;
   }
+  C->off[n] = off;
+  C->n = n;
+  C->total = off;
+  C->h = h;
 }
 
 // the listed level whose chunks hold chunk g: off[k] <= g < off[k + 1]

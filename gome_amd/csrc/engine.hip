@@ -1312,7 +1312,7 @@ gome_status gome_engine::enqueue(const gome_order* d_ord, uint32_t n, hipStream_
     if (wide) {  // the head: tile-parallel ranks, windows, layout and records
       k_fc_oldwalk_wide<<<dim3(FL_CAP, nb), 64, 0, st>>>(D, R);
       k_fc_pcnt<<<dim3(FL_SORT_GRID, nb), FL_TILE, 0, st>>>(D, B, R);
-      k_fc_pscan<<<nb, FL_CAP, 0, st>>>(D, R);
+      k_fc_pscan<<<nb, FL_CAP * FC_PSCAN_G, 0, st>>>(D, R);
       k_fc_prank<<<dim3(FL_SORT_GRID, nb), FL_TILE, 0, st>>>(D, B, R);
       k_fc_pwin<<<dim3(px, nb), 256, 0, st>>>(D, B, R, 0u);
       k_fc_precs<<<dim3(px, nb), 256, 0, st>>>(D, B, R, 0u);

@@ -652,27 +652,62 @@ __global__ __launch_bounds__(FL_TILE) void k_fc_pcnt(Dev D, BatchArgs B, FlowArg
 }
 
 // Per book: tile offsets per level from its old targets, per key from 0 (in place); the level
-// bases of the DEL-time arrays.
-__global__ __launch_bounds__(FL_CAP) void k_fc_pscan(Dev D, FlowArgs F) {
-  const uint32_t h = F.h0 + blockIdx.x, k = threadIdx.x;
+// bases of the DEL-time arrays.  FC_PSCAN_G groups of FL_CAP threads take a contiguous range of the
+// tiles each: their sums, the groups' prefixes, then the offsets written.  (One group walked the
+// hottest book's ~340 tiles eight at a time: 43 dependent round trips, 59 us on config 4's critical
+// path, gpurun_out/prof_r06ac_config4.)
+constexpr uint32_t FC_PSCAN_G = 8;
+__global__ __launch_bounds__(FL_CAP * FC_PSCAN_G) void k_fc_pscan(Dev D, FlowArgs F) {
+  __shared__ uint32_t sv[FC_PSCAN_G][FL_CAP], sb[FC_PSCAN_G][FL_CAP], ss[FC_PSCAN_G][FL_CAP];
+  const uint32_t h = F.h0 + blockIdx.x, k = threadIdx.x % FL_CAP, grp = threadIdx.x / FL_CAP;
   if (h >= fl_hend(D, F) || !fc_lane(F, h)) return;
   const FlowHdr& hd = F.hdr[h];
   FlowLvl* LV = F.lvl + h * FL_CAP;
   const uint32_t ntile = (hd.end - hd.beg + FL_TILE - 1) / FL_TILE;
+  const uint32_t per = (ntile + FC_PSCAN_G - 1) / FC_PSCAN_G;
+  const uint32_t t_beg = min(ntile, grp * per), t_end = min(ntile, t_beg + per);
   const bool lv = k >= 1 && k <= hd.nl;
-  uint32_t run = lv ? LV[k].c_old : 0u;
   uint32_t* tc = F.tcnt + static_cast<size_t>(h) * F.maxt * FL_CAP;
   uint32_t* tvv = F.tvol + static_cast<size_t>(h) * F.maxt * FC_KEYS;
-  uint32_t rb = 0, rs = 0;
-  // (eight tiles' loads in flight before their stores: one tile at a time, the hottest book's
-  // ~340 tiles were a chain of dependent round trips, 0.1 ms before the plan)
-  constexpr uint32_t U = 8;
-  for (uint32_t t0 = 0; t0 < ntile; t0 += U) {
+  constexpr uint32_t U = 8;  // (eight tiles' loads in flight together)
+  uint32_t a = 0, ab = 0, as = 0;
+  for (uint32_t t0 = t_beg; t0 < t_end; t0 += U) {
     uint32_t v[U], vb[U], vs[U];
 #pragma unroll
     for (uint32_t u = 0; u < U; ++u) {
       const uint32_t tl = t0 + u;
-      if (tl < ntile) {
+      const bool in = tl < t_end;
+      v[u] = in ? tc[tl * FL_CAP + k] : 0u;
+      vb[u] = in ? tvv[tl * FC_KEYS + k] : 0u;
+      vs[u] = in ? tvv[tl * FC_KEYS + FL_CAP + k] : 0u;
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < U; ++u) {
+      a += v[u];
+      ab += vb[u];
+      as += vs[u];
+    }
+  }
+  sv[grp][k] = a;
+  sb[grp][k] = ab;
+  ss[grp][k] = as;
+  __syncthreads();
+  uint32_t run = lv ? LV[k].c_old : 0u, rb = 0, rs = 0, tot = run;
+  for (uint32_t g = 0; g < FC_PSCAN_G; ++g) {
+    const uint32_t x = sv[g][k];
+    tot += x;
+    if (g < grp) {
+      run += x;
+      rb += sb[g][k];
+      rs += ss[g][k];
+    }
+  }
+  for (uint32_t t0 = t_beg; t0 < t_end; t0 += U) {
+    uint32_t v[U], vb[U], vs[U];
+#pragma unroll
+    for (uint32_t u = 0; u < U; ++u) {
+      const uint32_t tl = t0 + u;
+      if (tl < t_end) {
         v[u] = tc[tl * FL_CAP + k];
         vb[u] = tvv[tl * FC_KEYS + k];
         vs[u] = tvv[tl * FC_KEYS + FL_CAP + k];
@@ -681,7 +716,7 @@ __global__ __launch_bounds__(FL_CAP) void k_fc_pscan(Dev D, FlowArgs F) {
 #pragma unroll
     for (uint32_t u = 0; u < U; ++u) {
       const uint32_t tl = t0 + u;
-      if (tl >= ntile) break;
+      if (tl >= t_end) break;
       tc[tl * FL_CAP + k] = run;
       run += v[u];
       tvv[tl * FC_KEYS + k] = rb;
@@ -690,7 +725,7 @@ __global__ __launch_bounds__(FL_CAP) void k_fc_pscan(Dev D, FlowArgs F) {
       rs += vs[u];
     }
   }
-  fc_time_bases(LV, k, lv ? run : 0u);
+  fc_time_bases(LV, threadIdx.x, lv && grp == 0 ? tot : 0u);  // (threads >= FL_CAP: nothing)
 }
 
 // Targeted ADDs' ranks; a DEL's count of its level's targets that arrived before it (in nb); the

@@ -200,12 +200,28 @@ __device__ __forceinline__ bool fd_rank_grid(const unsigned long long* keys, uin
 #else
 #define PR(k) do { } while (0)
 #endif
+  // one pass for the bounds and the grid (two passes over the 2^16 slots until round 6): a thread
+  // takes the offsets of its keys from its first one, and the gcd of those and of the threads' first
+  // keys' offsets from the lowest key is the grid (the offsets from any one key of the set generate
+  // the same lattice as the offsets from the lowest)
   if (tid == 0) { kmin_s = ~0ull; kmax_s = 0; }
   __syncthreads();
-  unsigned long long mn = ~0ull, mx = 0;
-  for (uint32_t sl = tid; sl < DEEP_HASH; sl += FL_PREP_T) {
-    const unsigned long long k = keys[sl];
-    if (k) { mn = min(mn, k); mx = max(mx, k); }
+  unsigned long long mn = ~0ull, mx = 0, r = 0;
+  uint32_t g = 0;
+  constexpr uint32_t U = 4;  // (four loads in flight a thread)
+  for (uint32_t s0 = tid; s0 < DEEP_HASH; s0 += U * FL_PREP_T) {
+    unsigned long long kk[U];
+#pragma unroll
+    for (uint32_t u = 0; u < U; ++u) kk[u] = s0 + u * FL_PREP_T < DEEP_HASH ? keys[s0 + u * FL_PREP_T] : 0ull;
+#pragma unroll
+    for (uint32_t u = 0; u < U; ++u) {
+      const unsigned long long k = kk[u];
+      if (!k) continue;
+      mn = min(mn, k);
+      mx = max(mx, k);
+      if (!r) r = k;
+      else g = fd_gcd32(g, static_cast<uint32_t>(k >= r ? k - r : r - k));  // (garbage past 2^32: refused below)
+    }
   }
   atomicMin(&kmin_s, mn);
   atomicMax(&kmax_s, mx);
@@ -213,11 +229,7 @@ __device__ __forceinline__ bool fd_rank_grid(const unsigned long long* keys, uin
   PR(20);
   const unsigned long long kmin = kmin_s, kmax = kmax_s;
   if (n == 0 || kmax < kmin || kmax - kmin >= (1ull << 32)) return false;  // (uniform)
-  uint32_t g = 0;
-  for (uint32_t sl = tid; sl < DEEP_HASH; sl += FL_PREP_T) {
-    const unsigned long long k = keys[sl];
-    if (k) g = fd_gcd32(g, static_cast<uint32_t>(k - kmin));
-  }
+  if (r) g = fd_gcd32(g, static_cast<uint32_t>(r - kmin));
   for (int off = 32; off > 0; off >>= 1) g = fd_gcd32(g, __shfl_xor(g, off));
   if (lane == 0) g_s[w] = g;
   __syncthreads();
@@ -231,10 +243,14 @@ __device__ __forceinline__ bool fd_rank_grid(const unsigned long long* keys, uin
   uint32_t* slot = pre + FD_RANK_WORDS;  // [DEEP_CAP]
   for (uint32_t i = tid; i < FD_RANK_WORDS; i += FL_PREP_T) bm[i] = 0;
   __syncthreads();
-  for (uint32_t sl = tid; sl < DEEP_HASH; sl += FL_PREP_T) {
-    const unsigned long long k = keys[sl];
-    if (k) {
-      const uint32_t x = static_cast<uint32_t>(k - kmin) / g;
+  for (uint32_t s0 = tid; s0 < DEEP_HASH; s0 += U * FL_PREP_T) {
+    unsigned long long kk[U];
+#pragma unroll
+    for (uint32_t u = 0; u < U; ++u) kk[u] = s0 + u * FL_PREP_T < DEEP_HASH ? keys[s0 + u * FL_PREP_T] : 0ull;
+#pragma unroll
+    for (uint32_t u = 0; u < U; ++u) {
+      if (!kk[u]) continue;
+      const uint32_t x = static_cast<uint32_t>(kk[u] - kmin) / g;
       atomicOr(&bm[x >> 5], 1u << (x & 31));
     }
   }
@@ -264,11 +280,16 @@ __device__ __forceinline__ bool fd_rank_grid(const unsigned long long* keys, uin
   __syncthreads();
   PR(23);
   if (tot != n || n > DEEP_CAP) return false;  // (uniform: every key set its own bit)
-  for (uint32_t sl = tid; sl < DEEP_HASH; sl += FL_PREP_T) {
-    const unsigned long long k = keys[sl];
-    if (!k) continue;
-    const uint32_t x = static_cast<uint32_t>(k - kmin) / g;
-    slot[pre[x >> 5] + __popc(bm[x >> 5] & ((1u << (x & 31)) - 1u))] = sl;
+  for (uint32_t s0 = tid; s0 < DEEP_HASH; s0 += U * FL_PREP_T) {
+    unsigned long long kk[U];
+#pragma unroll
+    for (uint32_t u = 0; u < U; ++u) kk[u] = s0 + u * FL_PREP_T < DEEP_HASH ? keys[s0 + u * FL_PREP_T] : 0ull;
+#pragma unroll
+    for (uint32_t u = 0; u < U; ++u) {
+      if (!kk[u]) continue;
+      const uint32_t x = static_cast<uint32_t>(kk[u] - kmin) / g;
+      slot[pre[x >> 5] + __popc(bm[x >> 5] & ((1u << (x & 31)) - 1u))] = s0 + u * FL_PREP_T;
+    }
   }
   __syncthreads();
   PR(24);
